@@ -1,0 +1,323 @@
+/* mjhip.h — C-ABI of the MI355X batched inverse-dynamics engine (libmjhip.so).
+ *
+ * This is the drop-in boundary for the reference's inverse-dynamics path
+ * (fancifulland2718/mujoco_InverseDynamicsTest = MuJoCo 3.3.1 + local edits):
+ *
+ *   reference entry point (file:line)                          replaced by
+ *   ---------------------------------------------------------  -------------------------------
+ *   mj_inverse        src/engine/engine_inverse.c:266          mjhip_inverse
+ *                     include/mujoco/mujoco.h:283-284
+ *   mj_inverseSkip    src/engine/engine_inverse.c:197          mjhip_inverseSkip
+ *                     include/mujoco/mujoco.h:289-292
+ *   mj_invPosition    src/engine/engine_inverse.c:37           mjhip_invPosition
+ *   mj_invVelocity    src/engine/engine_inverse.c:73           mjhip_invVelocity
+ *   mj_invConstraint  src/engine/engine_inverse.c:169          mjhip_invConstraint
+ *                     (all three: src/engine/engine_inverse.h:27-43)
+ *   mj_compareFwdInv  src/engine/engine_inverse.c:275          mjhip_compareFwdInv
+ *   mj_rne            src/engine/engine_core_smooth.c:1969     mjhip_rne
+ *                     include/mujoco/mujoco.h:361
+ *   mjd_inverseFD     src/engine/engine_derivative_fd.c:611    mjhip_inverseFDBatch (batched)
+ *                     include/mujoco/mujoco.h:1244-1247
+ *   (batch of mj_inverse calls over one mjModel, the data-parallel pattern of
+ *    python/mujoco/rollout.cc:180-220 and sample/testspeed.cc:177-227)
+ *                                                              mjhip_inverseBatch
+ *
+ * Types: mjtNum is double (include/mujoco/mjtnum.h:21-22); mjtByte is unsigned char.
+ * mjhipModel / mjhipData hold the reference's field names, element types and row-major
+ * shapes (include/mujoco/mjxmacro.h), so a maintainer's adapter can fill them by plain
+ * pointer assignment from a real mjModel/mjData.
+ *
+ * Errors: the reference has no return codes (fatal -> mju_error, soft -> mj_warning,
+ * engine_util_errmem.c:118-150, engine_support.c:1650-1667). The single-instance entry
+ * points keep that behaviour through a user-settable error callback; the batch entry
+ * points return an mjhipStatus and never exit. Every compute entry point runs on the GPU;
+ * there is no CPU fallback: without a usable HIP device the call fails with
+ * MJHIP_ERR_NO_DEVICE.
+ */
+#ifndef MJHIP_H_
+#define MJHIP_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#include "mjhip_fields.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(_WIN32)
+  #define MJHIP_API __declspec(dllexport)
+#else
+  #define MJHIP_API __attribute__((visibility("default")))
+#endif
+
+typedef double mjtNum;
+typedef unsigned char mjtByte;
+
+/*---------------------------- constants (include/mujoco/mjmodel.h:24-45, mjtnum.h:23) ----*/
+#define mjhipPI      3.14159265358979323846
+#define mjhipMINVAL  1E-15
+#define mjhipMAXVAL  1E+10
+#define mjhipMINIMP  0.0001
+#define mjhipMAXIMP  0.9999
+#define mjhipNREF    2
+#define mjhipNIMP    5
+
+/*---------------------------- enums: same values as the reference ------------------------*/
+typedef enum mjhipDisableBit_ {      /* mjmodel.h:50-68 */
+  mjhipDSBL_CONSTRAINT   = 1 << 0,
+  mjhipDSBL_EQUALITY     = 1 << 1,
+  mjhipDSBL_FRICTIONLOSS = 1 << 2,
+  mjhipDSBL_LIMIT        = 1 << 3,
+  mjhipDSBL_CONTACT      = 1 << 4,
+  mjhipDSBL_PASSIVE      = 1 << 5,
+  mjhipDSBL_GRAVITY      = 1 << 6,
+  mjhipDSBL_CLAMPCTRL    = 1 << 7,
+  mjhipDSBL_WARMSTART    = 1 << 8,
+  mjhipDSBL_FILTERPARENT = 1 << 9,
+  mjhipDSBL_ACTUATION    = 1 << 10,
+  mjhipDSBL_REFSAFE      = 1 << 11,
+  mjhipDSBL_SENSOR       = 1 << 12,
+  mjhipDSBL_MIDPHASE     = 1 << 13,
+  mjhipDSBL_EULERDAMP    = 1 << 14,
+  mjhipDSBL_AUTORESET    = 1 << 15,
+  mjhipDSBL_NATIVECCD    = 1 << 16
+} mjhipDisableBit;
+
+typedef enum mjhipEnableBit_ {       /* mjmodel.h:70-79 */
+  mjhipENBL_OVERRIDE    = 1 << 0,
+  mjhipENBL_ENERGY      = 1 << 1,
+  mjhipENBL_FWDINV      = 1 << 2,
+  mjhipENBL_INVDISCRETE = 1 << 3,
+  mjhipENBL_MULTICCD    = 1 << 4,
+  mjhipENBL_ISLAND      = 1 << 5
+} mjhipEnableBit;
+
+typedef enum mjhipJoint_ {           /* mjmodel.h mjtJoint */
+  mjhipJNT_FREE = 0, mjhipJNT_BALL, mjhipJNT_SLIDE, mjhipJNT_HINGE
+} mjhipJoint;
+
+typedef enum mjhipGeom_ {            /* mjmodel.h mjtGeom */
+  mjhipGEOM_PLANE = 0, mjhipGEOM_HFIELD, mjhipGEOM_SPHERE, mjhipGEOM_CAPSULE,
+  mjhipGEOM_ELLIPSOID, mjhipGEOM_CYLINDER, mjhipGEOM_BOX, mjhipGEOM_MESH, mjhipGEOM_SDF
+} mjhipGeom;
+
+typedef enum mjhipCamLight_ {        /* mjmodel.h mjtCamLight */
+  mjhipCAMLIGHT_FIXED = 0, mjhipCAMLIGHT_TRACK, mjhipCAMLIGHT_TRACKCOM,
+  mjhipCAMLIGHT_TARGETBODY, mjhipCAMLIGHT_TARGETBODYCOM
+} mjhipCamLight;
+
+typedef enum mjhipWrap_ {            /* mjmodel.h:191-198 */
+  mjhipWRAP_NONE = 0, mjhipWRAP_JOINT, mjhipWRAP_PULLEY, mjhipWRAP_SITE,
+  mjhipWRAP_SPHERE, mjhipWRAP_CYLINDER
+} mjhipWrap;
+
+typedef enum mjhipTrn_ {             /* mjmodel.h:201-210 */
+  mjhipTRN_JOINT = 0, mjhipTRN_JOINTINPARENT, mjhipTRN_SLIDERCRANK, mjhipTRN_TENDON,
+  mjhipTRN_SITE, mjhipTRN_BODY, mjhipTRN_UNDEFINED = 1000
+} mjhipTrn;
+
+typedef enum mjhipDyn_ {             /* mjmodel.h mjtDyn */
+  mjhipDYN_NONE = 0, mjhipDYN_INTEGRATOR, mjhipDYN_FILTER, mjhipDYN_FILTEREXACT,
+  mjhipDYN_MUSCLE, mjhipDYN_USER
+} mjhipDyn;
+
+typedef enum mjhipGain_ {            /* mjmodel.h mjtGain */
+  mjhipGAIN_FIXED = 0, mjhipGAIN_AFFINE, mjhipGAIN_MUSCLE, mjhipGAIN_USER
+} mjhipGain;
+
+typedef enum mjhipBias_ {            /* mjmodel.h mjtBias */
+  mjhipBIAS_NONE = 0, mjhipBIAS_AFFINE, mjhipBIAS_MUSCLE, mjhipBIAS_USER
+} mjhipBias;
+
+typedef enum mjhipSameFrame_ {       /* mjmodel.h:379-385 */
+  mjhipSAMEFRAME_NONE = 0, mjhipSAMEFRAME_BODY, mjhipSAMEFRAME_INERTIA,
+  mjhipSAMEFRAME_BODYROT, mjhipSAMEFRAME_INERTIAROT
+} mjhipSameFrame;
+
+typedef enum mjhipStage_ {           /* mjmodel.h:363-368 */
+  mjhipSTAGE_NONE = 0, mjhipSTAGE_POS, mjhipSTAGE_VEL, mjhipSTAGE_ACC
+} mjhipStage;
+
+typedef enum mjhipIntegrator_ {      /* mjmodel.h mjtIntegrator */
+  mjhipINT_EULER = 0, mjhipINT_RK4, mjhipINT_IMPLICIT, mjhipINT_IMPLICITFAST
+} mjhipIntegrator;
+
+typedef enum mjhipJacobian_ {        /* mjmodel.h mjtJacobian */
+  mjhipJAC_DENSE = 0, mjhipJAC_SPARSE, mjhipJAC_AUTO
+} mjhipJacobian;
+
+typedef enum mjhipCone_ {            /* mjmodel.h mjtCone */
+  mjhipCONE_PYRAMIDAL = 0, mjhipCONE_ELLIPTIC
+} mjhipCone;
+
+/*---------------------------- option (include/mujoco/mjmodel.h mjOption) -----------------*/
+typedef struct mjhipOption_ {
+  mjtNum timestep;
+  mjtNum impratio;
+  mjtNum gravity[3];
+  mjtNum wind[3];
+  mjtNum density;
+  mjtNum viscosity;
+  mjtNum o_margin;
+  mjtNum o_solref[mjhipNREF];
+  mjtNum o_solimp[mjhipNIMP];
+  int integrator;
+  int cone;
+  int jacobian;
+  int disableflags;
+  int enableflags;
+} mjhipOption;
+
+/*---------------------------- model: sizes + field pointers ------------------------------*/
+typedef struct mjhipModel_ {
+#define XS(name) int name;
+  MJHIP_MODEL_SIZES
+#undef XS
+  mjhipOption opt;
+#define X(type, name, d0, d1) type* name;
+  MJHIP_MODEL_POINTERS
+#undef X
+} mjhipModel;
+
+/*---------------------------- data (single instance, host memory) ------------------------*/
+/* Status bits set per instance by every compute entry point (the batched analogue of the
+ * reference's mj_warning counters, engine_support.c:1650-1667, and of the efc overflow
+ * warning mjWARN_CNSTRFULL, engine_core_constraint.c:65-72). Nothing aborts a batch. */
+typedef enum mjhipInstanceStatus_ {
+  MJHIP_INST_OK            = 0,
+  MJHIP_INST_BADQPOS       = 1 << 0,   /* nan/|x|>mjMAXVAL in qpos (mj_checkPos semantics) */
+  MJHIP_INST_BADQVEL       = 1 << 1,
+  MJHIP_INST_BADQACC       = 1 << 2,
+  MJHIP_INST_INERTIA       = 1 << 3,   /* small/negative pivot in LTDL (mjWARN_INERTIA) */
+  MJHIP_INST_CNSTRFULL     = 1 << 4,   /* more constraint rows than the per-instance capacity */
+  MJHIP_INST_UNSUPPORTED   = 1 << 5    /* model feature not implemented on the device path */
+} mjhipInstanceStatus;
+
+typedef struct mjhipData_ {
+  int nefc;                 /* number of constraint rows of the last call */
+  int status;               /* mjhipInstanceStatus bits of the last call */
+  mjtNum solver_fwdinv[2];  /* mjdata.h:186, written by mjhip_compareFwdInv */
+  /* inputs and every fp64 output field of mj_inverseSkip, reference names */
+#define XD(name, d0, d1, stage) mjtNum* name;
+  MJHIP_DATA_FIELDS
+#undef XD
+  /* fields read by the fwd/inv comparison harness (inverse_test.cpp:51-73) */
+  mjtNum* qfrc_applied;     /* nv */
+  mjtNum* xfrc_applied;     /* nbody x 6 */
+  mjtNum* qfrc_actuator;    /* nv */
+  mjtNum* ctrl;             /* nu */
+} mjhipData;
+
+/*---------------------------- status codes of the batch API ------------------------------*/
+typedef enum mjhipStatus_ {
+  MJHIP_OK              = 0,
+  MJHIP_ERR_NO_DEVICE   = -1,   /* no usable HIP device: there is no CPU fallback */
+  MJHIP_ERR_ARG         = -2,   /* bad argument (null pointer, size, stage) */
+  MJHIP_ERR_HIP         = -3,   /* a HIP runtime call failed; see mjhip_lastError */
+  MJHIP_ERR_MODEL       = -4,   /* model uses a feature the device path does not support */
+  MJHIP_ERR_CAPACITY    = -5,   /* batch larger than the context capacity */
+  MJHIP_ERR_INSTANCE    = 1     /* call completed; at least one instance has a status bit */
+} mjhipStatus;
+
+/* flags for mjhipBatchDesc.flags */
+#define MJHIP_FLAG_DEVICE_PTRS   (1 << 0)  /* qpos/qvel/qacc/qfrc pointers are device memory */
+#define MJHIP_FLAG_MIRROR_INPUT  (1 << 1)  /* inputs already in the device mirror (skip upload) */
+#define MJHIP_FLAG_NO_MIRROR     (1 << 2)  /* write only qfrc_inverse (+ fields a later skip
+                                              call needs are then NOT available) */
+
+/* Mirror layout on the device (the "batched SoA mirror" of SURVEY.md §7 L1):
+ * every per-instance field F of size S = d0*d1 is stored as
+ *     F[(blk*S + k)*64 + lane],  instance = blk*64 + lane,  k = 0..S-1
+ * i.e. 64-instance blocks (one wavefront), component-major inside a block, so one
+ * wavefront's access to component k of F is one contiguous 512-byte segment. */
+#define MJHIP_BLOCK 64
+
+/*---------------------------- library / device ---------------------------------------------*/
+MJHIP_API const char* mjhip_version(void);
+MJHIP_API int mjhip_deviceCount(void);
+MJHIP_API const char* mjhip_lastError(void);
+/* error callback for the single-instance entry points (mju_user_error analogue);
+ * default prints and returns (it never exits the process). */
+MJHIP_API void mjhip_setErrorCallback(void (*cb)(const char* msg));
+
+/* size of a per-instance field in doubles (mjxmacro dims), -1 if unknown */
+MJHIP_API int mjhip_fieldSize(const mjhipModel* m, const char* name);
+/* number of fp64 mjData values written per instance by mj_inverseSkip(skipstage=NONE):
+ * W in SURVEY.md §8d (2,563 for the humanoid) */
+MJHIP_API int mjhip_outputDoubles(const mjhipModel* m);
+
+/*---------------------------- batched engine -----------------------------------------------*/
+typedef struct mjhipContext_ mjhipContext;
+
+/* upload the model to `device` and allocate a mirror for `capacity` instances */
+MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
+                                  mjhipContext** out);
+MJHIP_API void mjhip_contextFree(mjhipContext* c);
+MJHIP_API int mjhip_contextCapacity(const mjhipContext* c);
+/* HIP stream used by the context (hipStream_t as void*); may be replaced by the caller */
+MJHIP_API void* mjhip_contextStream(mjhipContext* c);
+MJHIP_API int mjhip_contextSetStream(mjhipContext* c, void* stream);
+
+/* Batched mj_inverseSkip over B instances of one model.
+ * qpos (B x nq), qvel (B x nv), qacc (B x nv) in, qfrc_inverse (B x nv) out: row-major,
+ * one row per instance (the layout of rollout.cc's state arrays). Host pointers unless
+ * MJHIP_FLAG_DEVICE_PTRS. qfrc_inverse may be NULL (result stays in the mirror).
+ * skipstage/skipsensor have the reference semantics (engine_inverse.c:197-261); with
+ * skipstage > NONE the earlier-stage fields must already be in the mirror (a previous
+ * call on the same context, or mjhip_mirrorUpload). status (B ints, host) may be NULL.
+ * Asynchronous w.r.t. the host only with MJHIP_FLAG_DEVICE_PTRS. */
+MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B,
+                                 const mjtNum* qpos, const mjtNum* qvel, const mjtNum* qacc,
+                                 mjtNum* qfrc_inverse, int skipstage, int skipsensor,
+                                 int flags, int* status);
+
+/* copy one mirror field (reference name) of instances [first, first+count) to/from host
+ * memory in the reference's per-instance row-major layout (count x fieldSize) */
+MJHIP_API int mjhip_mirrorDownload(mjhipContext* c, const char* field, int first, int count,
+                                   mjtNum* dst);
+MJHIP_API int mjhip_mirrorUpload(mjhipContext* c, const char* field, int first, int count,
+                                 const mjtNum* src);
+/* device pointer of a mirror field (block layout above) */
+MJHIP_API void* mjhip_mirrorDevicePtr(mjhipContext* c, const char* field);
+/* per-instance status words of the last call (device pointer, B ints) */
+MJHIP_API int mjhip_statusDownload(mjhipContext* c, int first, int count, int* dst);
+
+/* Batched mjd_inverseFD (engine_derivative_fd.c:611-719) with flg_actuation = 0 and no
+ * sensor outputs: for each of B base states, forward differences with step eps of
+ * qfrc_inverse w.r.t. qacc (DfDa), qvel (DfDv) and qpos (DfDq, via mj_integratePos),
+ * each nv x nv in the reference's transposed layout, plus DmDq (nv x nM) if non-NULL.
+ * Outputs are B x nv x nv row-major (host pointers unless MJHIP_FLAG_DEVICE_PTRS). */
+MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B,
+                                   const mjtNum* qpos, const mjtNum* qvel, const mjtNum* qacc,
+                                   mjtNum eps, mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa,
+                                   mjtNum* DmDq, int flags);
+
+/* Time `reps` back-to-back launches of the fused inverse kernel on the context's stream
+ * with HIP events (device-resident mirror inputs, B instances). Writes the average
+ * milliseconds per launch to *ms. Used by bench.py for the roofline figure. */
+MJHIP_API int mjhip_timeInverseKernel(mjhipContext* c, int B, int reps, int skipstage,
+                                      int flags, float* ms);
+
+/*---------------------------- single-instance drop-in -------------------------------------*/
+/* Same semantics and outputs as the reference functions named above; they run a batch of
+ * one instance on the GPU (device 0 unless mjhip_setDevice), uploading the fields a
+ * skipped stage would have read from d and writing every output field back into d. */
+MJHIP_API void mjhip_setDevice(int device);
+MJHIP_API void mjhip_inverse(const mjhipModel* m, mjhipData* d);
+MJHIP_API void mjhip_inverseSkip(const mjhipModel* m, mjhipData* d, int skipstage,
+                                 int skipsensor);
+MJHIP_API void mjhip_invPosition(const mjhipModel* m, mjhipData* d);
+MJHIP_API void mjhip_invVelocity(const mjhipModel* m, mjhipData* d);
+MJHIP_API void mjhip_invConstraint(const mjhipModel* m, mjhipData* d);
+MJHIP_API void mjhip_rne(const mjhipModel* m, mjhipData* d, int flg_acc, mjtNum* result);
+MJHIP_API void mjhip_compareFwdInv(const mjhipModel* m, mjhipData* d);
+/* release the per-model device state cached by the single-instance entry points */
+MJHIP_API void mjhip_releaseModel(const mjhipModel* m);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif  /* MJHIP_H_ */

@@ -1,0 +1,237 @@
+/* mjhip_fields.h — field tables (X-macros) shared by the C-ABI, the HIP kernels,
+ * the CPU oracle and the Python host mirror (which parses this file).
+ *
+ * Names, element types and per-field shapes follow the reference's own tables:
+ *   model fields : /root/reference/include/mujoco/mjxmacro.h:183- (MJMODEL_POINTERS)
+ *   data fields  : /root/reference/include/mujoco/mjxmacro.h:594-699 (MJDATA_POINTERS)
+ * Only the subset the inverse-dynamics path reads or writes is kept.
+ * Row-major per field, exactly as in the reference (e.g. xmat is nbody x 9).
+ *
+ * The three sparse-structure arrays C_rownnz/C_rowadr/C_colind/mapM2C live in mjData in
+ * the reference (engine_io.c:1977-1989) but are model constants; here they are model fields.
+ *
+ * Syntax (one entry per line, parsed by mujoco_inversedynamicstest_amd/fields.py):
+ *   X(ctype, name, dim0, dim1)   dim0 is a size name, dim1 an integer or MJ_M(size)
+ */
+#ifndef MJHIP_FIELDS_H_
+#define MJHIP_FIELDS_H_
+
+/* integer sizes of the model (mjModel scalar ints, mjmodel.h) */
+#define MJHIP_MODEL_SIZES \
+  XS(nq)          \
+  XS(nv)          \
+  XS(nu)          \
+  XS(na)          \
+  XS(nbody)       \
+  XS(njnt)        \
+  XS(ngeom)       \
+  XS(nsite)       \
+  XS(ncam)        \
+  XS(nlight)      \
+  XS(ntendon)     \
+  XS(nwrap)       \
+  XS(nM)          \
+  XS(nC)          \
+  XS(nD)          \
+  XS(nJmom)       \
+  XS(nmocap)      \
+  XS(ngravcomp)   \
+  XS(nexclude)    \
+  XS(nkey)        \
+  XS(ntree)
+
+/* model arrays (mjxmacro.h MJMODEL_POINTERS order within each group) */
+#define MJHIP_MODEL_POINTERS \
+  X(mjtNum,  qpos0,                nq,        1) \
+  X(mjtNum,  qpos_spring,          nq,        1) \
+  X(int,     body_parentid,        nbody,     1) \
+  X(int,     body_rootid,          nbody,     1) \
+  X(int,     body_weldid,          nbody,     1) \
+  X(int,     body_mocapid,         nbody,     1) \
+  X(int,     body_jntnum,          nbody,     1) \
+  X(int,     body_jntadr,          nbody,     1) \
+  X(int,     body_dofnum,          nbody,     1) \
+  X(int,     body_dofadr,          nbody,     1) \
+  X(int,     body_treeid,          nbody,     1) \
+  X(int,     body_geomnum,         nbody,     1) \
+  X(int,     body_geomadr,         nbody,     1) \
+  X(mjtByte, body_simple,          nbody,     1) \
+  X(mjtByte, body_sameframe,       nbody,     1) \
+  X(mjtNum,  body_pos,             nbody,     3) \
+  X(mjtNum,  body_quat,            nbody,     4) \
+  X(mjtNum,  body_ipos,            nbody,     3) \
+  X(mjtNum,  body_iquat,           nbody,     4) \
+  X(mjtNum,  body_mass,            nbody,     1) \
+  X(mjtNum,  body_subtreemass,     nbody,     1) \
+  X(mjtNum,  body_inertia,         nbody,     3) \
+  X(mjtNum,  body_invweight0,      nbody,     2) \
+  X(mjtNum,  body_gravcomp,        nbody,     1) \
+  X(mjtNum,  body_margin,          nbody,     1) \
+  X(int,     body_contype,         nbody,     1) \
+  X(int,     body_conaffinity,     nbody,     1) \
+  X(int,     jnt_type,             njnt,      1) \
+  X(int,     jnt_qposadr,          njnt,      1) \
+  X(int,     jnt_dofadr,           njnt,      1) \
+  X(int,     jnt_bodyid,           njnt,      1) \
+  X(int,     jnt_group,            njnt,      1) \
+  X(mjtByte, jnt_limited,          njnt,      1) \
+  X(mjtByte, jnt_actgravcomp,      njnt,      1) \
+  X(mjtNum,  jnt_solref,           njnt,      2) \
+  X(mjtNum,  jnt_solimp,           njnt,      5) \
+  X(mjtNum,  jnt_pos,              njnt,      3) \
+  X(mjtNum,  jnt_axis,             njnt,      3) \
+  X(mjtNum,  jnt_stiffness,        njnt,      1) \
+  X(mjtNum,  jnt_range,            njnt,      2) \
+  X(mjtNum,  jnt_margin,           njnt,      1) \
+  X(int,     dof_bodyid,           nv,        1) \
+  X(int,     dof_jntid,            nv,        1) \
+  X(int,     dof_parentid,         nv,        1) \
+  X(int,     dof_treeid,           nv,        1) \
+  X(int,     dof_Madr,             nv,        1) \
+  X(int,     dof_simplenum,        nv,        1) \
+  X(mjtNum,  dof_solref,           nv,        2) \
+  X(mjtNum,  dof_solimp,           nv,        5) \
+  X(mjtNum,  dof_frictionloss,     nv,        1) \
+  X(mjtNum,  dof_armature,         nv,        1) \
+  X(mjtNum,  dof_damping,          nv,        1) \
+  X(mjtNum,  dof_invweight0,       nv,        1) \
+  X(mjtNum,  dof_M0,               nv,        1) \
+  X(int,     geom_type,            ngeom,     1) \
+  X(int,     geom_contype,         ngeom,     1) \
+  X(int,     geom_conaffinity,     ngeom,     1) \
+  X(int,     geom_condim,          ngeom,     1) \
+  X(int,     geom_bodyid,          ngeom,     1) \
+  X(int,     geom_group,           ngeom,     1) \
+  X(int,     geom_priority,        ngeom,     1) \
+  X(mjtByte, geom_sameframe,       ngeom,     1) \
+  X(mjtNum,  geom_solmix,          ngeom,     1) \
+  X(mjtNum,  geom_solref,          ngeom,     2) \
+  X(mjtNum,  geom_solimp,          ngeom,     5) \
+  X(mjtNum,  geom_size,            ngeom,     3) \
+  X(mjtNum,  geom_rbound,          ngeom,     1) \
+  X(mjtNum,  geom_pos,             ngeom,     3) \
+  X(mjtNum,  geom_quat,            ngeom,     4) \
+  X(mjtNum,  geom_friction,        ngeom,     3) \
+  X(mjtNum,  geom_margin,          ngeom,     1) \
+  X(mjtNum,  geom_gap,             ngeom,     1) \
+  X(int,     site_type,            nsite,     1) \
+  X(int,     site_bodyid,          nsite,     1) \
+  X(mjtByte, site_sameframe,       nsite,     1) \
+  X(mjtNum,  site_size,            nsite,     3) \
+  X(mjtNum,  site_pos,             nsite,     3) \
+  X(mjtNum,  site_quat,            nsite,     4) \
+  X(int,     cam_mode,             ncam,      1) \
+  X(int,     cam_bodyid,           ncam,      1) \
+  X(int,     cam_targetbodyid,     ncam,      1) \
+  X(mjtNum,  cam_pos,              ncam,      3) \
+  X(mjtNum,  cam_quat,             ncam,      4) \
+  X(mjtNum,  cam_poscom0,          ncam,      3) \
+  X(mjtNum,  cam_pos0,             ncam,      3) \
+  X(mjtNum,  cam_mat0,             ncam,      9) \
+  X(int,     light_mode,           nlight,    1) \
+  X(int,     light_bodyid,         nlight,    1) \
+  X(int,     light_targetbodyid,   nlight,    1) \
+  X(mjtNum,  light_pos,            nlight,    3) \
+  X(mjtNum,  light_dir,            nlight,    3) \
+  X(mjtNum,  light_poscom0,        nlight,    3) \
+  X(mjtNum,  light_pos0,           nlight,    3) \
+  X(mjtNum,  light_dir0,           nlight,    3) \
+  X(int,     tendon_adr,           ntendon,   1) \
+  X(int,     tendon_num,           ntendon,   1) \
+  X(mjtByte, tendon_limited,       ntendon,   1) \
+  X(mjtNum,  tendon_solref_lim,    ntendon,   2) \
+  X(mjtNum,  tendon_solimp_lim,    ntendon,   5) \
+  X(mjtNum,  tendon_range,         ntendon,   2) \
+  X(mjtNum,  tendon_margin,        ntendon,   1) \
+  X(mjtNum,  tendon_stiffness,     ntendon,   1) \
+  X(mjtNum,  tendon_damping,       ntendon,   1) \
+  X(mjtNum,  tendon_lengthspring,  ntendon,   2) \
+  X(mjtNum,  tendon_length0,       ntendon,   1) \
+  X(mjtNum,  tendon_invweight0,    ntendon,   1) \
+  X(int,     wrap_type,            nwrap,     1) \
+  X(int,     wrap_objid,           nwrap,     1) \
+  X(mjtNum,  wrap_prm,             nwrap,     1) \
+  X(int,     actuator_trntype,     nu,        1) \
+  X(int,     actuator_dyntype,     nu,        1) \
+  X(int,     actuator_gaintype,    nu,        1) \
+  X(int,     actuator_biastype,    nu,        1) \
+  X(int,     actuator_trnid,       nu,        2) \
+  X(mjtByte, actuator_ctrllimited, nu,        1) \
+  X(mjtByte, actuator_forcelimited, nu,       1) \
+  X(mjtNum,  actuator_dynprm,      nu,        10) \
+  X(mjtNum,  actuator_gainprm,     nu,        10) \
+  X(mjtNum,  actuator_biasprm,     nu,        10) \
+  X(mjtNum,  actuator_ctrlrange,   nu,        2) \
+  X(mjtNum,  actuator_forcerange,  nu,        2) \
+  X(mjtNum,  actuator_gear,        nu,        6) \
+  X(mjtNum,  actuator_length0,     nu,        1) \
+  X(mjtNum,  actuator_acc0,        nu,        1) \
+  X(int,     exclude_signature,    nexclude,  1) \
+  X(mjtNum,  key_qpos,             nkey,      MJ_M(nq)) \
+  X(int,     C_rownnz,             nv,        1) \
+  X(int,     C_rowadr,             nv,        1) \
+  X(int,     C_colind,             nC,        1) \
+  X(int,     mapM2C,               nC,        1) \
+  X(int,     moment_rownnz,        nu,        1) \
+  X(int,     moment_rowadr,        nu,        1) \
+  X(int,     moment_colind,        nJmom,     1)
+
+/* Per-instance fp64 mjData fields produced or consumed by mj_inverseSkip, in pipeline order.
+ * XD(name, dim0, dim1, stage): stage 0 = input, 1 = position, 2 = velocity, 3 = acceleration.
+ * The sum over stages 1..3 of dim0*dim1 is W in SURVEY.md §8d (2,563 for the humanoid). */
+#define MJHIP_DATA_INPUTS \
+  XD(qpos,              nq,      1,   0) \
+  XD(qvel,              nv,      1,   0) \
+  XD(qacc,              nv,      1,   0)
+
+#define MJHIP_DATA_POSITION \
+  XD(xpos,              nbody,   3,   1) \
+  XD(xquat,             nbody,   4,   1) \
+  XD(xmat,              nbody,   9,   1) \
+  XD(xipos,             nbody,   3,   1) \
+  XD(ximat,             nbody,   9,   1) \
+  XD(xanchor,           njnt,    3,   1) \
+  XD(xaxis,             njnt,    3,   1) \
+  XD(geom_xpos,         ngeom,   3,   1) \
+  XD(geom_xmat,         ngeom,   9,   1) \
+  XD(site_xpos,         nsite,   3,   1) \
+  XD(site_xmat,         nsite,   9,   1) \
+  XD(cam_xpos,          ncam,    3,   1) \
+  XD(cam_xmat,          ncam,    9,   1) \
+  XD(light_xpos,        nlight,  3,   1) \
+  XD(light_xdir,        nlight,  3,   1) \
+  XD(subtree_com,       nbody,   3,   1) \
+  XD(cdof,              nv,      6,   1) \
+  XD(cinert,            nbody,   10,  1) \
+  XD(ten_length,        ntendon, 1,   1) \
+  XD(ten_J,             ntendon, MJ_M(nv), 1) \
+  XD(actuator_length,   nu,      1,   1) \
+  XD(actuator_moment,   nJmom,   1,   1) \
+  XD(crb,               nbody,   10,  1) \
+  XD(qM,                nM,      1,   1) \
+  XD(qLD,               nC,      1,   1) \
+  XD(qLDiagInv,         nv,      1,   1)
+
+#define MJHIP_DATA_VELOCITY \
+  XD(ten_velocity,      ntendon, 1,   2) \
+  XD(actuator_velocity, nu,      1,   2) \
+  XD(cvel,              nbody,   6,   2) \
+  XD(cdof_dot,          nv,      6,   2) \
+  XD(qfrc_spring,       nv,      1,   2) \
+  XD(qfrc_damper,       nv,      1,   2) \
+  XD(qfrc_gravcomp,     nv,      1,   2) \
+  XD(qfrc_fluid,        nv,      1,   2) \
+  XD(qfrc_passive,      nv,      1,   2) \
+  XD(qfrc_bias,         nv,      1,   2)
+
+#define MJHIP_DATA_ACCELERATION \
+  XD(qfrc_constraint,   nv,      1,   3) \
+  XD(qfrc_inverse,      nv,      1,   3)
+
+#define MJHIP_DATA_FIELDS \
+  MJHIP_DATA_INPUTS       \
+  MJHIP_DATA_POSITION     \
+  MJHIP_DATA_VELOCITY     \
+  MJHIP_DATA_ACCELERATION
+
+#endif  /* MJHIP_FIELDS_H_ */

@@ -1,0 +1,127 @@
+"""Field tables shared with C/HIP: parsed from include/mjhip_fields.h.
+
+The header is the single source of truth for the names, element types and shapes of the
+model and per-instance data fields (which follow the reference's
+include/mujoco/mjxmacro.h tables). This module turns it into ctypes structures that are
+binary-compatible with ``mjhipModel`` / ``mjhipData`` in include/mjhip.h.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+REPO_ROOT = os.path.dirname(_HERE)
+INCLUDE_DIR = os.path.join(REPO_ROOT, "include")
+FIELDS_HEADER = os.path.join(INCLUDE_DIR, "mjhip_fields.h")
+
+CTYPE = {"mjtNum": ctypes.c_double, "int": ctypes.c_int, "mjtByte": ctypes.c_ubyte}
+NPTYPE = {"mjtNum": np.float64, "int": np.int32, "mjtByte": np.uint8}
+
+
+@dataclass(frozen=True)
+class ModelField:
+  ctype: str
+  name: str
+  dim0: str
+  dim1: str  # integer literal or MJ_M(size)
+
+  def shape(self, sizes: dict) -> tuple:
+    return (sizes[self.dim0], _dim(self.dim1, sizes))
+
+
+@dataclass(frozen=True)
+class DataField:
+  name: str
+  dim0: str
+  dim1: str
+  stage: int  # 0 input, 1 position, 2 velocity, 3 acceleration
+
+  def size(self, sizes: dict) -> int:
+    return sizes[self.dim0] * _dim(self.dim1, sizes)
+
+
+def _dim(tok: str, sizes: dict) -> int:
+  m = re.fullmatch(r"MJ_M\((\w+)\)", tok)
+  if m:
+    return sizes[m.group(1)]
+  return int(tok)
+
+
+def _macro_body(text: str, name: str) -> str:
+  m = re.search(r"#define\s+" + name + r"\s*\\\n(.*?)(?:\n\s*\n|\n#)", text, re.S)
+  if not m:
+    raise RuntimeError(f"macro {name} not found in {FIELDS_HEADER}")
+  return m.group(1)
+
+
+def _parse():
+  text = open(FIELDS_HEADER).read()
+  sizes = re.findall(r"XS\((\w+)\)", _macro_body(text, "MJHIP_MODEL_SIZES"))
+  model = []
+  for ct, nm, d0, d1 in re.findall(
+      r"X\(\s*(\w+)\s*,\s*(\w+)\s*,\s*(\w+)\s*,\s*([\w()]+)\s*\)",
+      _macro_body(text, "MJHIP_MODEL_POINTERS")):
+    model.append(ModelField(ct, nm, d0, d1))
+  data = []
+  for group in ("MJHIP_DATA_INPUTS", "MJHIP_DATA_POSITION", "MJHIP_DATA_VELOCITY",
+                "MJHIP_DATA_ACCELERATION"):
+    for nm, d0, d1, st in re.findall(
+        r"XD\(\s*(\w+)\s*,\s*(\w+)\s*,\s*([\w()]+)\s*,\s*(\d)\s*\)",
+        _macro_body(text, group)):
+      data.append(DataField(nm, d0, d1, int(st)))
+  return sizes, model, data
+
+
+MODEL_SIZES, MODEL_FIELDS, DATA_FIELDS = _parse()
+MODEL_FIELD = {f.name: f for f in MODEL_FIELDS}
+DATA_FIELD = {f.name: f for f in DATA_FIELDS}
+
+
+class Option(ctypes.Structure):
+  """mjhipOption (include/mjhip.h), the subset of mjOption (mjmodel.h) on the path."""
+  _fields_ = [
+      ("timestep", ctypes.c_double),
+      ("impratio", ctypes.c_double),
+      ("gravity", ctypes.c_double * 3),
+      ("wind", ctypes.c_double * 3),
+      ("density", ctypes.c_double),
+      ("viscosity", ctypes.c_double),
+      ("o_margin", ctypes.c_double),
+      ("o_solref", ctypes.c_double * 2),
+      ("o_solimp", ctypes.c_double * 5),
+      ("integrator", ctypes.c_int),
+      ("cone", ctypes.c_int),
+      ("jacobian", ctypes.c_int),
+      ("disableflags", ctypes.c_int),
+      ("enableflags", ctypes.c_int),
+  ]
+
+
+class CModel(ctypes.Structure):
+  _fields_ = ([(s, ctypes.c_int) for s in MODEL_SIZES] + [("opt", Option)] +
+              [(f.name, ctypes.POINTER(CTYPE[f.ctype])) for f in MODEL_FIELDS])
+
+
+class CData(ctypes.Structure):
+  _fields_ = ([("nefc", ctypes.c_int), ("status", ctypes.c_int),
+               ("solver_fwdinv", ctypes.c_double * 2)] +
+              [(f.name, ctypes.POINTER(ctypes.c_double)) for f in DATA_FIELDS] +
+              [("qfrc_applied", ctypes.POINTER(ctypes.c_double)),
+               ("xfrc_applied", ctypes.POINTER(ctypes.c_double)),
+               ("qfrc_actuator", ctypes.POINTER(ctypes.c_double)),
+               ("ctrl", ctypes.POINTER(ctypes.c_double))])
+
+
+def output_doubles(sizes: dict) -> int:
+  """W of SURVEY.md §8d: fp64 mjData values written by mj_inverseSkip(NONE)."""
+  return sum(f.size(sizes) for f in DATA_FIELDS if f.stage > 0)
+
+
+def input_doubles(sizes: dict) -> int:
+  """R of SURVEY.md §8d: fp64 values read per instance (qpos, qvel, qacc)."""
+  return sum(f.size(sizes) for f in DATA_FIELDS if f.stage == 0)

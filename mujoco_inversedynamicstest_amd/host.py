@@ -1,0 +1,84 @@
+"""Host-side mjModel/mjData views for the C-ABI (ctypes structs over numpy arrays).
+
+``model_struct(m)`` builds the ``mjhipModel`` struct of include/mjhip.h from a compiled
+Model (pointer fields alias the Model's numpy arrays, which the struct keeps alive), and
+``MjData`` holds one instance's fields in the reference's per-field row-major layout
+(include/mujoco/mjdata.h via mjxmacro.h) behind an ``mjhipData`` struct.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import fields
+
+
+def model_struct(m) -> fields.CModel:
+  s = fields.CModel()
+  keep = []
+  for k in fields.MODEL_SIZES:
+    setattr(s, k, int(m.sizes.get(k, 0)))
+  o = s.opt
+  for k in ("timestep", "impratio", "density", "viscosity", "o_margin"):
+    setattr(o, k, float(m.opt[k]))
+  for k, n in (("gravity", 3), ("wind", 3), ("o_solref", 2), ("o_solimp", 5)):
+    arr = getattr(o, k)
+    for i in range(n):
+      arr[i] = float(m.opt[k][i])
+  for k in ("integrator", "cone", "jacobian", "disableflags", "enableflags"):
+    setattr(o, k, int(m.opt[k]))
+  for f in fields.MODEL_FIELDS:
+    a = np.ascontiguousarray(getattr(m, f.name), dtype=fields.NPTYPE[f.ctype])
+    if a is not getattr(m, f.name):
+      setattr(m, f.name, a)
+    keep.append(a)
+    if a.size:
+      setattr(s, f.name, a.ctypes.data_as(ctypes.POINTER(fields.CTYPE[f.ctype])))
+  s._keep = keep
+  return s
+
+
+class MjData:
+  """One instance of the per-instance fields (mjData subset), numpy-backed."""
+
+  def __init__(self, m):
+    self.m = m
+    sizes = m.sizes
+    self._arrays = {}
+    for f in fields.DATA_FIELDS:
+      n = f.size(sizes)
+      self._arrays[f.name] = np.zeros(max(n, 1))
+    for name, n in (("qfrc_applied", m.nv), ("qfrc_actuator", m.nv),
+                    ("xfrc_applied", 6 * m.nbody), ("ctrl", m.nu)):
+      self._arrays[name] = np.zeros(max(n, 1))
+    # reference defaults (mj_resetData): qpos = qpos0, world body identity frames
+    self._arrays["qpos"][:m.nq] = m.qpos0
+    self.struct = fields.CData()
+    for name, a in self._arrays.items():
+      setattr(self.struct, name, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+
+  def __getattr__(self, k):
+    arrs = self.__dict__.get("_arrays")
+    if arrs is not None and k in arrs:
+      f = fields.DATA_FIELD.get(k)
+      n = f.size(self.m.sizes) if f else len(arrs[k])
+      if k in ("qfrc_applied", "qfrc_actuator"):
+        n = self.m.nv
+      elif k == "xfrc_applied":
+        n = 6 * self.m.nbody
+      elif k == "ctrl":
+        n = self.m.nu
+      return arrs[k][:n]
+    raise AttributeError(k)
+
+  @property
+  def nefc(self):
+    return self.struct.nefc
+
+  @property
+  def solver_fwdinv(self):
+    return np.array(self.struct.solver_fwdinv[:2])
+
+  def ptr(self):
+    return ctypes.byref(self.struct)

@@ -1,0 +1,1505 @@
+"""MJCF-subset model compiler: XML -> compiled model arrays with mjModel field names.
+
+The reference's model compiler (src/user, src/xml) cannot be built offline (it needs
+tinyxml2/qhull/lodepng/... that CMake would fetch: SURVEY.md §8c), so this module restates
+the compiler semantics the inverse-dynamics path depends on, for the MJCF subset used by
+model/humanoid/humanoid.xml, src/inverse/test.xml and the reference's inverse/inertia/
+derivative test models. Reference semantics followed:
+
+  * default classes / childclass resolution         src/xml/xml_native_reader.cc
+  * body tree, rootid/weldid, sameframe, simple       src/user/user_model.cc:2174-2380
+  * qpos0 / qpos_spring                               src/user/user_model.cc:2300-2325
+  * dof_Madr, nM, nD, dof_simplenum, nC               src/user/user_model.cc:2539-2617
+  * joint compile (limits deg->rad, axis normalize)   src/user/user_objects.cc:2149-2260
+  * geom fromto / orientation / volume / inertia      src/user/user_objects.cc:2384-2560, 2911-3080
+  * body inertial frame from geoms (+eig3)            src/user/user_objects.cc:1507-1575, 1637-1735
+  * orientation alternatives                          src/user/user_objects.cc:240-350
+  * math helpers (z2quat, frame2quat, eig3, ...)      src/user/user_util.cc:149-800
+  * nJmom                                              src/user/user_model.cc:2703-2750
+  * C sparse structure, mapM2C                        src/engine/engine_io.c:929-1018, 1135-1259
+
+Model constants computed by mj_setConst (dof_M0, *_invweight0, tendon_length0,
+lengthspring, cam/light offsets) are filled by setconst.py.
+
+Compiled-model parity against MuJoCo's own compiler is UNPINNED: no reference test pins
+compiled humanoid masses/inertias and the compiler cannot run here.
+"""
+from __future__ import annotations
+
+import math
+import os
+import xml.etree.ElementTree as ET
+
+import numpy as np
+
+from . import fields
+
+mjPI = 3.14159265358979323846
+mjEPS = 1e-14          # src/user/user_util.h:25
+kFrameEps = 1e-6       # src/user/user_model.cc:62
+kEigEPS = 1e-12        # src/user/user_util.cc:649
+
+JNT = {"free": 0, "ball": 1, "slide": 2, "hinge": 3}
+GEOM = {"plane": 0, "hfield": 1, "sphere": 2, "capsule": 3, "ellipsoid": 4,
+        "cylinder": 5, "box": 6, "mesh": 7, "sdf": 8}
+CAMLIGHT = {"fixed": 0, "track": 1, "trackcom": 2, "targetbody": 3, "targetbodycom": 4}
+INTEGRATOR = {"Euler": 0, "RK4": 1, "implicit": 2, "implicitfast": 3}
+JACOBIAN = {"dense": 0, "sparse": 1, "auto": 2}
+CONE = {"pyramidal": 0, "elliptic": 1}
+DISABLE = {"constraint": 0, "equality": 1, "frictionloss": 2, "limit": 3, "contact": 4,
+           "passive": 5, "gravity": 6, "clampctrl": 7, "warmstart": 8, "filterparent": 9,
+           "actuation": 10, "refsafe": 11, "sensor": 12, "midphase": 13, "eulerdamp": 14,
+           "autoreset": 15, "nativeccd": 16}
+ENABLE = {"override": 0, "energy": 1, "fwdinv": 2, "invdiscrete": 3, "multiccd": 4,
+          "island": 5}
+
+
+class MJCFError(ValueError):
+  pass
+
+
+#--------------------------------- compiler math (src/user/user_util.cc) -------------------
+
+def normvec(v):
+  """mjuu_normvec (user_util.cc:149): normalize unless within mjEPS of unit length."""
+  nrm = 0.0
+  for x in v:
+    nrm += x * x
+  if nrm < mjEPS:
+    return 0.0
+  nrm = math.sqrt(nrm)
+  if abs(nrm - 1) > mjEPS:
+    for i in range(len(v)):
+      v[i] /= nrm
+  return nrm
+
+
+def quat2mat(q):
+  """mjuu_quat2mat (user_util.cc:196)."""
+  if q[0] == 1 and q[1] == 0 and q[2] == 0 and q[3] == 0:
+    return [1.0, 0, 0, 0, 1.0, 0, 0, 0, 1.0]
+  q00 = q[0]*q[0]; q01 = q[0]*q[1]; q02 = q[0]*q[2]; q03 = q[0]*q[3]
+  q11 = q[1]*q[1]; q12 = q[1]*q[2]; q13 = q[1]*q[3]
+  q22 = q[2]*q[2]; q23 = q[2]*q[3]; q33 = q[3]*q[3]
+  r = [0.0] * 9
+  r[0] = q00 + q11 - q22 - q33
+  r[4] = q00 - q11 + q22 - q33
+  r[8] = q00 - q11 - q22 + q33
+  r[1] = 2*(q12 - q03)
+  r[2] = 2*(q13 + q02)
+  r[3] = 2*(q12 + q03)
+  r[5] = 2*(q23 - q01)
+  r[6] = 2*(q13 - q02)
+  r[7] = 2*(q23 + q01)
+  return r
+
+
+def mulquat(qa, qb):
+  """mjuu_mulquat (user_util.cc:239): product, normalized."""
+  t = [qa[0]*qb[0] - qa[1]*qb[1] - qa[2]*qb[2] - qa[3]*qb[3],
+       qa[0]*qb[1] + qa[1]*qb[0] + qa[2]*qb[3] - qa[3]*qb[2],
+       qa[0]*qb[2] - qa[1]*qb[3] + qa[2]*qb[0] + qa[3]*qb[1],
+       qa[0]*qb[3] + qa[1]*qb[2] - qa[2]*qb[1] + qa[3]*qb[0]]
+  normvec(t)
+  return t
+
+
+def crossvec(a, b):
+  return [a[1]*b[2] - a[2]*b[1], a[2]*b[0] - a[0]*b[2], a[0]*b[1] - a[1]*b[0]]
+
+
+def z2quat(vec):
+  """mjuu_z2quat (user_util.cc:384): minimal rotation from (0,0,1) to vec."""
+  q = [0.0] + crossvec([0.0, 0.0, 1.0], vec)
+  v = q[1:]
+  s = normvec(v)
+  q[1:] = v
+  if s < 1e-10:
+    q[1] = 1.0
+    q[2] = q[3] = 0.0
+  ang = math.atan2(s, vec[2])
+  q[0] = math.cos(ang/2)
+  q[1] *= math.sin(ang/2)
+  q[2] *= math.sin(ang/2)
+  q[3] *= math.sin(ang/2)
+  return q
+
+
+def frame2quat(x, y, z):
+  """mjuu_frame2quat (user_util.cc:401); axes are matrix columns."""
+  mat = [x, y, z]
+  q = [0.0] * 4
+  if mat[0][0] + mat[1][1] + mat[2][2] > 0:
+    q[0] = 0.5 * math.sqrt(1 + mat[0][0] + mat[1][1] + mat[2][2])
+    q[1] = 0.25 * (mat[1][2] - mat[2][1]) / q[0]
+    q[2] = 0.25 * (mat[2][0] - mat[0][2]) / q[0]
+    q[3] = 0.25 * (mat[0][1] - mat[1][0]) / q[0]
+  elif mat[0][0] > mat[1][1] and mat[0][0] > mat[2][2]:
+    q[1] = 0.5 * math.sqrt(1 + mat[0][0] - mat[1][1] - mat[2][2])
+    q[0] = 0.25 * (mat[1][2] - mat[2][1]) / q[1]
+    q[2] = 0.25 * (mat[1][0] + mat[0][1]) / q[1]
+    q[3] = 0.25 * (mat[2][0] + mat[0][2]) / q[1]
+  elif mat[1][1] > mat[2][2]:
+    q[2] = 0.5 * math.sqrt(1 - mat[0][0] + mat[1][1] - mat[2][2])
+    q[0] = 0.25 * (mat[2][0] - mat[0][2]) / q[2]
+    q[1] = 0.25 * (mat[1][0] + mat[0][1]) / q[2]
+    q[3] = 0.25 * (mat[2][1] + mat[1][2]) / q[2]
+  else:
+    q[3] = 0.5 * math.sqrt(1 - mat[0][0] - mat[1][1] + mat[2][2])
+    q[0] = 0.25 * (mat[0][1] - mat[1][0]) / q[3]
+    q[1] = 0.25 * (mat[2][0] + mat[0][2]) / q[3]
+    q[2] = 0.25 * (mat[2][1] + mat[1][2]) / q[3]
+  normvec(q)
+  return q
+
+
+def mulvecmat(vec, mat):
+  """mjuu_mulvecmat (user_util.cc:251): mat * vec (3x3 row-major)."""
+  return [mat[0]*vec[0] + mat[1]*vec[1] + mat[2]*vec[2],
+          mat[3]*vec[0] + mat[4]*vec[1] + mat[5]*vec[2],
+          mat[6]*vec[0] + mat[7]*vec[1] + mat[8]*vec[2]]
+
+
+def rotvecquat(vec, quat):
+  return mulvecmat(vec, quat2mat(quat))
+
+
+def globalinertia(local, quat):
+  """mjuu_globalinertia (user_util.cc:498)."""
+  mat = quat2mat(quat)
+  tmp = [mat[0]*local[0], mat[3]*local[0], mat[6]*local[0],
+         mat[1]*local[1], mat[4]*local[1], mat[7]*local[1],
+         mat[2]*local[2], mat[5]*local[2], mat[8]*local[2]]
+  return [mat[0]*tmp[0] + mat[1]*tmp[3] + mat[2]*tmp[6],
+          mat[3]*tmp[1] + mat[4]*tmp[4] + mat[5]*tmp[7],
+          mat[6]*tmp[2] + mat[7]*tmp[5] + mat[8]*tmp[8],
+          mat[0]*tmp[1] + mat[1]*tmp[4] + mat[2]*tmp[7],
+          mat[0]*tmp[2] + mat[1]*tmp[5] + mat[2]*tmp[8],
+          mat[3]*tmp[2] + mat[4]*tmp[5] + mat[5]*tmp[8]]
+
+
+def offcenter(mass, vec):
+  """mjuu_offcenter (user_util.cc:519)."""
+  return [mass*(vec[1]*vec[1] + vec[2]*vec[2]),
+          mass*(vec[0]*vec[0] + vec[2]*vec[2]),
+          mass*(vec[0]*vec[0] + vec[1]*vec[1]),
+          -mass*vec[0]*vec[1],
+          -mass*vec[0]*vec[2],
+          -mass*vec[1]*vec[2]]
+
+
+def _mulmat(a, b):
+  return [sum(a[3*i+k]*b[3*k+j] for k in range(3)) for i in range(3) for j in range(3)]
+
+
+def _mulmat_ordered(a, b):
+  # mjuu_mulmat: res[i,j] = a[i,0]*b[0,j] + a[i,1]*b[1,j] + a[i,2]*b[2,j]
+  r = [0.0] * 9
+  for i in range(3):
+    for j in range(3):
+      r[3*i+j] = a[3*i]*b[j] + a[3*i+1]*b[3+j] + a[3*i+2]*b[6+j]
+  return r
+
+
+def _transpose(a):
+  return [a[0], a[3], a[6], a[1], a[4], a[7], a[2], a[5], a[8]]
+
+
+def eig3(mat):
+  """mjuu_eig3 (user_util.cc:650): Jacobi eigen-decomposition, eigenvalues descending."""
+  quat = [1.0, 0.0, 0.0, 0.0]
+  eigval = [0.0] * 3
+  for _ in range(500):
+    eigvec = quat2mat(quat)
+    tmp = _mulmat_ordered(_transpose(eigvec), mat)
+    D = _mulmat_ordered(tmp, eigvec)
+    eigval = [D[0], D[4], D[8]]
+    if abs(D[1]) > abs(D[2]) and abs(D[1]) > abs(D[5]):
+      rk, ck, rotk = 0, 1, 2
+    elif abs(D[2]) > abs(D[5]):
+      rk, ck, rotk = 0, 2, 1
+    else:
+      rk, ck, rotk = 1, 2, 0
+    if abs(D[3*rk+ck]) < kEigEPS:
+      break
+    tau = (D[4*ck] - D[4*rk]) / (2*D[3*rk+ck])
+    if tau >= 0:
+      t = 1.0/(tau + math.sqrt(1 + tau*tau))
+    else:
+      t = -1.0/(-tau + math.sqrt(1 + tau*tau))
+    c = 1.0/math.sqrt(1 + t*t)
+    if c > 1.0 - kEigEPS:
+      break
+    q = [0.0, 0.0, 0.0, 0.0]
+    q[rotk+1] = -math.sqrt(0.5-0.5*c) if tau >= 0 else math.sqrt(0.5-0.5*c)
+    if rotk == 1:
+      q[rotk+1] = -q[rotk+1]
+    q[0] = math.sqrt(1.0 - q[rotk+1]*q[rotk+1])
+    normvec(q)
+    quat = mulquat(quat, q)
+    normvec(quat)
+  for j in range(3):
+    j1 = j % 2
+    if eigval[j1] + kEigEPS < eigval[j1+1]:
+      eigval[j1], eigval[j1+1] = eigval[j1+1], eigval[j1]
+      q = [0.707106781186548, 0.0, 0.0, 0.0]
+      q[(j1+2) % 3 + 1] = q[0]
+      quat = mulquat(quat, q)
+      normvec(quat)
+  return eigval, quat
+
+
+def full_inertia(full6):
+  """mjuu_fullInertia (user_util.cc:774)."""
+  full = [full6[0], full6[3], full6[4],
+          full6[3], full6[1], full6[5],
+          full6[4], full6[5], full6[2]]
+  eigval, quat = eig3(full)
+  if eigval[2] < mjEPS:
+    raise MJCFError("inertia must have positive eigenvalues")
+  return quat, eigval
+
+
+def is_same_vec(a, b):
+  return all(abs(a[i] - b[i]) < kFrameEps for i in range(3))
+
+
+def is_same_quat(a, b):
+  minus = all(abs(a[i] - b[i]) < kFrameEps for i in range(4))
+  plus = all(abs(a[i] + b[i]) < kFrameEps for i in range(4))
+  return minus or plus
+
+
+def is_same_pose(p1, p2, q1, q2):
+  """IsSamePose (user_model.cc:95)."""
+  if p1 is not None and p2 is not None and not is_same_vec(p1, p2):
+    return False
+  if q1 is not None and q2 is not None and not is_same_quat(q1, q2):
+    return False
+  return True
+
+
+def is_null_pose(p, q):
+  return is_same_pose(p, [0, 0, 0] if p is not None else None, q,
+                      [1, 0, 0, 0] if q is not None else None)
+
+
+#--------------------------------- XML helpers ---------------------------------------------
+
+def _floats(s):
+  return [float(x) for x in s.split()]
+
+
+class _Defaults:
+  """One default class: per-element attribute dicts, inheriting from the parent class."""
+
+  def __init__(self, name, parent=None):
+    self.name = name
+    self.parent = parent
+    self.attrs = {}  # element tag -> {attr: str}
+
+  def get(self, tag):
+    out = dict(self.parent.get(tag)) if self.parent else {}
+    out.update(self.attrs.get(tag, {}))
+    return out
+
+
+ACTUATOR_TAGS = ("general", "motor", "position", "velocity")
+
+
+def _resolve_orientation(attrs, degree, eulerseq, quat):
+  """ResolveOrientation (user_objects.cc:240) for axisangle/xyaxes/zaxis/euler."""
+  if "axisangle" in attrs:
+    aa = _floats(attrs["axisangle"])
+    if degree:
+      aa[3] = aa[3] / 180.0 * mjPI
+    ax = aa[:3]
+    if normvec(ax) < mjEPS:
+      raise MJCFError("axisangle too small")
+    ang2 = aa[3]/2
+    return [math.cos(ang2), math.sin(ang2)*ax[0], math.sin(ang2)*ax[1], math.sin(ang2)*ax[2]]
+  if "xyaxes" in attrs:
+    xy = _floats(attrs["xyaxes"])
+    x = xy[:3]
+    y = xy[3:]
+    if normvec(x) < mjEPS:
+      raise MJCFError("xaxis too small")
+    d = x[0]*y[0] + x[1]*y[1] + x[2]*y[2]
+    y[0] -= x[0]*d
+    y[1] -= x[1]*d
+    y[2] -= x[2]*d
+    if normvec(y) < mjEPS:
+      raise MJCFError("yaxis too small")
+    z = crossvec(x, y)
+    if normvec(z) < mjEPS:
+      raise MJCFError("cross(xaxis, yaxis) too small")
+    return frame2quat(x, y, z)
+  if "zaxis" in attrs:
+    z = _floats(attrs["zaxis"])
+    if normvec(z) < mjEPS:
+      raise MJCFError("zaxis too small")
+    return z2quat(z)
+  if "euler" in attrs:
+    eu = _floats(attrs["euler"])
+    if degree:
+      eu = [e / 180.0 * mjPI for e in eu]
+    q = [1.0, 0.0, 0.0, 0.0]
+    for i in range(3):
+      qrot = [math.cos(eu[i]/2), 0.0, 0.0, 0.0]
+      sa = math.sin(eu[i]/2)
+      ax = eulerseq[i]
+      qrot["xyz".index(ax.lower()) + 1] = sa
+      if ax.islower():   # moving axes: post-multiply
+        q = mulquat(q, qrot)
+      else:              # fixed axes: pre-multiply
+        q = mulquat(qrot, q)
+    return q
+  return quat
+
+
+#--------------------------------- compiled objects ----------------------------------------
+
+class Body:
+  def __init__(self, parent, attrs, cls, childclass):
+    self.parent = parent
+    self.attrs = attrs
+    self.cls = cls
+    self.childclass = childclass
+    self.children = []
+    self.joints = []
+    self.geoms = []
+    self.sites = []
+    self.cams = []
+    self.lights = []
+    self.inertial = None
+    self.id = -1
+    self.name = attrs.get("name", "")
+
+
+class Model:
+  """A compiled model: sizes + numpy arrays named as in mjModel (see include/mjhip_fields.h).
+
+  ``sizes`` maps size names to ints, ``opt`` is a dict of mjOption values and every model
+  field of the field table is an attribute holding a numpy array of shape (dim0, dim1).
+  """
+
+  def __init__(self):
+    self.sizes = {}
+    self.opt = {}
+    self.names = {}
+
+  def __getitem__(self, k):
+    return getattr(self, k)
+
+  # convenience
+  def __getattr__(self, k):
+    sizes = self.__dict__.get("sizes", {})
+    if k in sizes:
+      return sizes[k]
+    raise AttributeError(k)
+
+  def save(self, path):
+    """Save as .npz (numeric arrays only: loadable with allow_pickle=False)."""
+    arrs = {"__sizes_keys": np.array(list(self.sizes.keys())),
+            "__sizes_vals": np.array(list(self.sizes.values()), dtype=np.int64)}
+    for k, v in self.opt.items():
+      arrs["__opt_" + k] = np.asarray(v)
+    for f in fields.MODEL_FIELDS:
+      arrs[f.name] = getattr(self, f.name)
+    for k, v in self.names.items():
+      arrs["__names_" + k] = np.array(v if v else [""])
+    np.savez(path, **arrs)
+
+  @staticmethod
+  def load(path):
+    z = np.load(path, allow_pickle=False)
+    m = Model()
+    m.sizes = {str(k): int(v) for k, v in zip(z["__sizes_keys"], z["__sizes_vals"])}
+    for k in z.files:
+      if k.startswith("__opt_"):
+        v = z[k]
+        m.opt[k[6:]] = v.tolist() if v.ndim else (int(v) if v.dtype.kind == "i" else float(v))
+      elif k.startswith("__names_"):
+        lst = [str(x) for x in z[k]]
+        m.names[k[8:]] = [] if lst == [""] and m.sizes.get(_NAME_SIZE.get(k[8:], ""), 0) == 0 else lst
+    for f in fields.MODEL_FIELDS:
+      setattr(m, f.name, np.ascontiguousarray(z[f.name]))
+    return m
+
+
+_NAME_SIZE = {"body": "nbody", "jnt": "njnt", "geom": "ngeom", "site": "nsite", "cam": "ncam",
+              "light": "nlight", "tendon": "ntendon", "actuator": "nu", "key": "nkey"}
+
+
+class MJCFCompiler:
+  """Compile an MJCF file/string into a Model (subset; raises MJCFError otherwise)."""
+
+  def __init__(self):
+    self.degree = True
+    self.inertiafromgeom = "auto"
+    self.autolimits = True
+    self.eulerseq = "xyz"
+    self.boundmass = 0.0
+    self.boundinertia = 0.0
+    self.balanceinertia = False
+    self.inertiagrouprange = (0, 5)
+    self.opt = {"timestep": 0.002, "impratio": 1.0, "gravity": [0.0, 0.0, -9.81],
+                "wind": [0.0, 0.0, 0.0], "density": 0.0, "viscosity": 0.0, "o_margin": 0.0,
+                "o_solref": [0.02, 1.0], "o_solimp": [0.9, 0.95, 0.001, 0.5, 2.0],
+                "integrator": 0, "cone": 0, "jacobian": 2, "disableflags": 0,
+                "enableflags": 0}
+    self.classes = {}
+    self.bodies = []
+    self.tendons = []
+    self.actuators = []
+    self.excludes = []
+    self.keys = []
+
+  # ---------------------------------------------------------------- parsing
+  def _parse_defaults(self, el, parent):
+    name = el.get("class", "main")
+    d = _Defaults(name, parent)
+    self.classes[name] = d
+    for ch in el:
+      if ch.tag == "default":
+        self._parse_defaults(ch, d)
+      else:
+        tag = "joint" if ch.tag == "freejoint" else ch.tag
+        d.attrs.setdefault(tag, {}).update(ch.attrib)
+
+  def _elem_attrs(self, el, tag, childclass):
+    cls = el.get("class", childclass or "main")
+    if cls not in self.classes:
+      raise MJCFError(f"unknown default class '{cls}'")
+    a = self.classes[cls].get(tag)
+    a.update(el.attrib)
+    return a
+
+  def _parse_body(self, el, parent, childclass):
+    attrs = dict(el.attrib)
+    cc = attrs.get("childclass", childclass)
+    b = Body(parent, attrs, attrs.get("class", childclass), cc)
+    self.bodies.append(b)
+    for ch in el:
+      t = ch.tag
+      if t == "body":
+        b.children.append(self._parse_body(ch, b, cc))
+      elif t == "joint":
+        b.joints.append(self._elem_attrs(ch, "joint", cc))
+      elif t == "freejoint":
+        a = {"type": "free"}
+        for k in ("name", "align", "group"):
+          if k in ch.attrib:
+            a[k] = ch.attrib[k]
+        b.joints.append(a)
+      elif t == "geom":
+        b.geoms.append(self._elem_attrs(ch, "geom", cc))
+      elif t == "site":
+        b.sites.append(self._elem_attrs(ch, "site", cc))
+      elif t == "camera":
+        b.cams.append(self._elem_attrs(ch, "camera", cc))
+      elif t == "light":
+        b.lights.append(self._elem_attrs(ch, "light", cc))
+      elif t == "inertial":
+        b.inertial = dict(ch.attrib)
+      else:
+        raise MJCFError(f"unsupported body child element <{t}>")
+    return b
+
+  def parse(self, root):
+    if root.tag != "mujoco":
+      raise MJCFError("root element must be <mujoco>")
+    self.model_name = root.get("model", "")
+    self.classes["main"] = _Defaults("main")
+    for el in root:
+      if el.tag == "default":
+        # top-level <default> is class "main"; its children are classes
+        top = self.classes["main"]
+        for ch in el:
+          if ch.tag == "default":
+            self._parse_defaults(ch, top)
+          else:
+            tag = "joint" if ch.tag == "freejoint" else ch.tag
+            top.attrs.setdefault(tag, {}).update(ch.attrib)
+    for el in root:
+      t = el.tag
+      if t == "compiler":
+        a = el.attrib
+        if "angle" in a:
+          self.degree = a["angle"] == "degree"
+        self.inertiafromgeom = a.get("inertiafromgeom", self.inertiafromgeom)
+        if "autolimits" in a:
+          self.autolimits = a["autolimits"] == "true"
+        self.eulerseq = a.get("eulerseq", self.eulerseq)
+        self.boundmass = float(a.get("boundmass", self.boundmass))
+        self.boundinertia = float(a.get("boundinertia", self.boundinertia))
+        if "balanceinertia" in a:
+          self.balanceinertia = a["balanceinertia"] == "true"
+        if "inertiagrouprange" in a:
+          self.inertiagrouprange = tuple(int(x) for x in a["inertiagrouprange"].split())
+      elif t == "option":
+        self._parse_option(el)
+      elif t == "worldbody":
+        self._parse_worldbody(el)
+      elif t == "tendon":
+        for ch in el:
+          if ch.tag != "fixed":
+            raise MJCFError(f"unsupported tendon <{ch.tag}> (spatial tendons are next)")
+          a = self._elem_attrs(ch, "tendon", None)
+          joints = [(j.get("joint"), float(j.get("coef", "1"))) for j in ch if j.tag == "joint"]
+          self.tendons.append((a, joints))
+      elif t == "actuator":
+        for ch in el:
+          if ch.tag not in ACTUATOR_TAGS:
+            raise MJCFError(f"unsupported actuator <{ch.tag}>")
+          a = self._elem_attrs(ch, ch.tag, None)
+          a["__tag"] = ch.tag
+          self.actuators.append(a)
+      elif t == "contact":
+        for ch in el:
+          if ch.tag == "exclude":
+            self.excludes.append((ch.get("body1"), ch.get("body2")))
+          else:
+            raise MJCFError(f"unsupported contact element <{ch.tag}>")
+      elif t == "keyframe":
+        for ch in el:
+          self.keys.append(dict(ch.attrib))
+      elif t in ("visual", "asset", "statistic", "default", "compiler", "size", "sensor",
+                 "extension"):
+        continue  # no effect on the inverse-dynamics path
+      else:
+        raise MJCFError(f"unsupported top-level element <{t}>")
+
+  def _parse_option(self, el):
+    a = el.attrib
+    o = self.opt
+    for k in ("timestep", "impratio", "density", "viscosity", "o_margin"):
+      if k in a:
+        o[k] = float(a[k])
+    for k in ("gravity", "wind", "o_solref", "o_solimp"):
+      if k in a:
+        o[k] = _floats(a[k])
+    if "integrator" in a:
+      o["integrator"] = INTEGRATOR[a["integrator"]]
+    if "jacobian" in a:
+      o["jacobian"] = JACOBIAN[a["jacobian"]]
+    if "cone" in a:
+      o["cone"] = CONE[a["cone"]]
+    for ch in el:
+      if ch.tag == "flag":
+        for k, v in ch.attrib.items():
+          if k in DISABLE:
+            bit = 1 << DISABLE[k]
+            if v == "disable":
+              o["disableflags"] |= bit
+            else:
+              o["disableflags"] &= ~bit
+          elif k in ENABLE:
+            bit = 1 << ENABLE[k]
+            if v == "enable":
+              o["enableflags"] |= bit
+            else:
+              o["enableflags"] &= ~bit
+          else:
+            raise MJCFError(f"unknown flag '{k}'")
+
+  def _parse_worldbody(self, el):
+    world = Body(None, {"name": "world"}, None, None)
+    self.bodies.insert(0, world)
+    for ch in el:
+      t = ch.tag
+      if t == "body":
+        world.children.append(self._parse_body(ch, world, None))
+      elif t == "geom":
+        world.geoms.append(self._elem_attrs(ch, "geom", None))
+      elif t == "site":
+        world.sites.append(self._elem_attrs(ch, "site", None))
+      elif t == "camera":
+        world.cams.append(self._elem_attrs(ch, "camera", None))
+      elif t == "light":
+        world.lights.append(self._elem_attrs(ch, "light", None))
+      else:
+        raise MJCFError(f"unsupported worldbody element <{t}>")
+
+  # ---------------------------------------------------------------- compile
+  def _order_bodies(self):
+    # depth-first pre-order (mjCModel body list order)
+    order = []
+
+    def rec(b):
+      order.append(b)
+      for c in b.children:
+        rec(c)
+    rec(self.bodies[0])
+    for i, b in enumerate(order):
+      b.id = i
+    self.bodies = order
+
+  def _compile_geom(self, a, inferinertia):
+    g = {}
+    g["type"] = GEOM[a.get("type", "sphere")]
+    size = [0.0, 0.0, 0.0]
+    if "size" in a:
+      s = _floats(a["size"])
+      size[:len(s)] = s
+    pos = _floats(a["pos"]) if "pos" in a else [0.0, 0.0, 0.0]
+    quat = _floats(a["quat"]) if "quat" in a else [1.0, 0.0, 0.0, 0.0]
+    normvec(quat)
+    if "fromto" in a:
+      if g["type"] not in (GEOM["capsule"], GEOM["cylinder"], GEOM["ellipsoid"], GEOM["box"]):
+        raise MJCFError("fromto requires capsule, cylinder, box or ellipsoid in geom")
+      if pos[0] or pos[1] or pos[2]:
+        raise MJCFError("both pos and fromto defined in geom")
+      ft = _floats(a["fromto"])
+      vec = [ft[0]-ft[3], ft[1]-ft[4], ft[2]-ft[5]]
+      size[1] = normvec(vec)/2
+      if size[1] < mjEPS:
+        raise MJCFError("fromto points too close in geom")
+      if g["type"] in (GEOM["ellipsoid"], GEOM["box"]):
+        size[2] = size[1]
+        size[1] = size[0]
+      pos = [(ft[0]+ft[3])/2, (ft[1]+ft[4])/2, (ft[2]+ft[5])/2]
+      quat = z2quat(vec)
+    else:
+      quat = _resolve_orientation(a, self.degree, self.eulerseq, quat)
+    t = g["type"]
+    if t == GEOM["mesh"] or t == GEOM["hfield"] or t == GEOM["sdf"]:
+      raise MJCFError("mesh/hfield/sdf geoms are not in the supported subset")
+    g["size"] = size
+    g["pos"] = pos
+    g["quat"] = quat
+    g["group"] = int(a.get("group", 0))
+    g["contype"] = int(a.get("contype", 1))
+    g["conaffinity"] = int(a.get("conaffinity", 1))
+    g["condim"] = int(a.get("condim", 3))
+    g["priority"] = int(a.get("priority", 0))
+    fr = _floats(a["friction"]) if "friction" in a else []
+    g["friction"] = [1.0, 0.005, 0.0001]
+    g["friction"][:len(fr)] = fr
+    g["solmix"] = float(a.get("solmix", 1.0))
+    g["solref"] = _floats(a["solref"]) if "solref" in a else [0.02, 1.0]
+    si = _floats(a["solimp"]) if "solimp" in a else []
+    g["solimp"] = [0.9, 0.95, 0.001, 0.5, 2.0]
+    g["solimp"][:len(si)] = si
+    g["margin"] = float(a.get("margin", 0.0))
+    g["gap"] = float(a.get("gap", 0.0))
+    g["name"] = a.get("name", "")
+    # mass and inertia (user_objects.cc:3052-3080), typeinertia = volume
+    g["mass"] = 0.0
+    g["inertia"] = [0.0, 0.0, 0.0]
+    if inferinertia:
+      vol = _geom_volume(t, size)
+      if "mass" in a:
+        mass = float(a["mass"])
+        if mass == 0:
+          g["mass"] = 0.0
+        elif vol > mjEPS:
+          g["mass"] = mass
+          g["inertia"] = _geom_inertia(t, size, mass)
+      else:
+        density = float(a.get("density", 1000.0))
+        if density != 0:
+          g["mass"] = density * vol
+          g["inertia"] = _geom_inertia(t, size, g["mass"])
+    g["rbound"] = _geom_rbound(t, size)
+    return g
+
+  def compile(self) -> Model:
+    self._order_bodies()
+    bodies = self.bodies
+    nbody = len(bodies)
+    # ---- per-body compile (mjCBody::Compile)
+    jnts, geoms, sites, cams, lights = [], [], [], [], []
+    for b in bodies:
+      a = b.attrs
+      b.pos = _floats(a["pos"]) if "pos" in a else [0.0, 0.0, 0.0]
+      b.quat = _floats(a["quat"]) if "quat" in a else [1.0, 0.0, 0.0, 0.0]
+      normvec(b.quat)
+      b.quat = _resolve_orientation(a, self.degree, self.eulerseq, b.quat)
+      b.mocap = a.get("mocap", "false") == "true"
+      if b.mocap:
+        raise MJCFError("mocap bodies are not in the supported subset")
+      b.gravcomp = float(a.get("gravcomp", 0.0))
+      b.ipos = None
+      b.iquat = [1.0, 0.0, 0.0, 0.0]
+      b.mass = 0.0
+      b.inertia = [0.0, 0.0, 0.0]
+      explicit = b.inertial is not None
+      if explicit:
+        ia = b.inertial
+        b.ipos = _floats(ia["pos"])
+        b.mass = float(ia["mass"])
+        if "fullinertia" in ia:
+          b.iquat, b.inertia = full_inertia(_floats(ia["fullinertia"]))
+        else:
+          b.inertia = _floats(ia.get("diaginertia", "0 0 0"))
+          q = _floats(ia["quat"]) if "quat" in ia else [1.0, 0.0, 0.0, 0.0]
+          normvec(q)
+          b.iquat = _resolve_orientation(ia, self.degree, self.eulerseq, q)
+      b.cgeoms = []
+      for ga in b.geoms:
+        infer = (b.id > 0 and (not explicit or self.inertiafromgeom == "true") and
+                 self.inertiagrouprange[0] <= int(ga.get("group", 0)) <= self.inertiagrouprange[1])
+        b.cgeoms.append(self._compile_geom(ga, infer))
+      if b.id > 0 and (self.inertiafromgeom == "true" or
+                       (b.ipos is None and self.inertiafromgeom == "auto")):
+        self._inertia_from_geom(b)
+      if b.ipos is None:
+        b.ipos = list(b.pos)
+        b.iquat = list(b.quat)
+      if b.id > 0:
+        b.mass = max(b.mass, self.boundmass)
+        b.inertia = [max(x, self.boundinertia) for x in b.inertia]
+        I = b.inertia
+        if I[0] + I[1] < I[2] or I[0] + I[2] < I[1] or I[1] + I[2] < I[0]:
+          if self.balanceinertia:
+            b.inertia = [(I[0] + I[1] + I[2])/3.0] * 3
+          else:
+            raise MJCFError("inertia must satisfy A + B >= C")
+      # free-joint alignment (user_objects.cc:1751-1776): only with align="true"
+      if (len(b.joints) == 1 and b.joints[0].get("type") == "free" and not b.children and
+          b.joints[0].get("align", "auto") == "true"):
+        raise MJCFError("free-joint alignment is not in the supported subset")
+    # weldid (mjCBody::Compile sets children's weldid)
+    for b in bodies:
+      if b.id == 0:
+        b.weldid = 0
+      for c in b.children:
+        c.weldid = c.id if c.joints else b.weldid
+    # ---- joints
+    for b in bodies:
+      b.cjoints = []
+      for ja in b.joints:
+        j = self._compile_joint(ja)
+        j["body"] = b.id
+        b.cjoints.append(j)
+        jnts.append(j)
+      b.dofnum = sum(_jnt_nv(j["type"]) for j in b.cjoints)
+    # ---- assign ids: joints, geoms, sites, cams, lights in body order
+    for b in bodies:
+      for g in b.cgeoms:
+        g["body"] = b.id
+        geoms.append(g)
+      for sa in b.sites:
+        sites.append(self._compile_site(sa, b.id))
+      for ca in b.cams:
+        cams.append(self._compile_cam(ca, b.id))
+      for la in b.lights:
+        lights.append(self._compile_light(la, b.id))
+    return self._emit(jnts, geoms, sites, cams, lights)
+
+  def _inertia_from_geom(self, b):
+    sel = [g for g in b.cgeoms
+           if self.inertiagrouprange[0] <= g["group"] <= self.inertiagrouprange[1]]
+    if len(sel) == 1:
+      g = sel[0]
+      b.ipos = list(g["pos"])
+      b.iquat = list(g["quat"])
+      b.mass = g["mass"]
+      b.inertia = list(g["inertia"])
+    elif len(sel) > 1:
+      mass = 0.0
+      com = [0.0, 0.0, 0.0]
+      for g in sel:
+        mass += g["mass"]
+        com[0] += g["mass"] * g["pos"][0]
+        com[1] += g["mass"] * g["pos"][1]
+        com[2] += g["mass"] * g["pos"][2]
+      if mass < mjEPS:
+        raise MJCFError("body mass is too small, cannot compute center of mass")
+      ipos = [com[0]/mass, com[1]/mass, com[2]/mass]
+      toti = [0.0] * 6
+      for g in sel:
+        dpos = [g["pos"][0] - ipos[0], g["pos"][1] - ipos[1], g["pos"][2] - ipos[2]]
+        i0 = globalinertia(g["inertia"], g["quat"])
+        i1 = offcenter(g["mass"], dpos)
+        for j in range(6):
+          toti[j] = toti[j] + i0[j] + i1[j]
+      b.mass = mass
+      b.ipos = ipos
+      b.iquat, b.inertia = full_inertia(toti)
+
+  def _compile_joint(self, a):
+    t = JNT[a.get("type", "hinge")]
+    j = {"type": t, "name": a.get("name", "")}
+    rng = _floats(a["range"]) if "range" in a else [0.0, 0.0]
+    lim = a.get("limited", "auto")
+    if t == JNT["free"]:
+      limited = False
+    elif lim == "auto":
+      hasrange = not (rng[0] == 0 and rng[1] == 0)
+      if not self.autolimits and hasrange:
+        raise MJCFError("joint has range but limited is auto and autolimits is false")
+      limited = hasrange if self.autolimits else False
+    else:
+      limited = lim == "true"
+    if limited:
+      if rng[0] >= rng[1] and t != JNT["ball"]:
+        raise MJCFError("range[0] should be smaller than range[1] in joint")
+      if self.degree and t in (JNT["hinge"], JNT["ball"]):
+        if rng[0]:
+          rng[0] *= mjPI/180.0
+        if rng[1]:
+          rng[1] *= mjPI/180.0
+    axis = _floats(a["axis"]) if "axis" in a else [0.0, 0.0, 1.0]
+    if t in (JNT["free"], JNT["ball"]):
+      axis = [0.0, 0.0, 1.0]
+    if normvec(axis) < mjEPS:
+      raise MJCFError("axis too small in joint")
+    pos = _floats(a["pos"]) if "pos" in a else [0.0, 0.0, 0.0]
+    if t == JNT["free"]:
+      pos = [0.0, 0.0, 0.0]
+    ref = float(a.get("ref", 0.0))
+    springref = float(a.get("springref", 0.0))
+    if t == JNT["hinge"] and self.degree:
+      ref *= mjPI/180.0
+      springref *= mjPI/180.0
+    j.update(limited=limited, range=rng, axis=axis, pos=pos, ref=ref, springref=springref,
+             stiffness=float(a.get("stiffness", 0.0)), damping=float(a.get("damping", 0.0)),
+             armature=float(a.get("armature", 0.0)),
+             frictionloss=float(a.get("frictionloss", 0.0)),
+             margin=float(a.get("margin", 0.0)), group=int(a.get("group", 0)),
+             actgravcomp=a.get("actuatorgravcomp", "false") == "true")
+    sr = _floats(a["solreflimit"]) if "solreflimit" in a else [0.02, 1.0]
+    si = [0.9, 0.95, 0.001, 0.5, 2.0]
+    if "solimplimit" in a:
+      v = _floats(a["solimplimit"])
+      si[:len(v)] = v
+    j["solref"] = sr
+    j["solimp"] = si
+    fsr = _floats(a["solreffriction"]) if "solreffriction" in a else [0.02, 1.0]
+    fsi = [0.9, 0.95, 0.001, 0.5, 2.0]
+    if "solimpfriction" in a:
+      v = _floats(a["solimpfriction"])
+      fsi[:len(v)] = v
+    j["solref_f"] = fsr
+    j["solimp_f"] = fsi
+    return j
+
+  def _compile_site(self, a, bid):
+    pos = _floats(a["pos"]) if "pos" in a else [0.0, 0.0, 0.0]
+    quat = _floats(a["quat"]) if "quat" in a else [1.0, 0.0, 0.0, 0.0]
+    normvec(quat)
+    quat = _resolve_orientation(a, self.degree, self.eulerseq, quat)
+    size = [0.005, 0.005, 0.005]
+    if "size" in a:
+      s = _floats(a["size"])
+      size[:len(s)] = s
+    return {"body": bid, "pos": pos, "quat": quat, "size": size,
+            "type": GEOM[a.get("type", "sphere")], "name": a.get("name", "")}
+
+  def _compile_cam(self, a, bid):
+    pos = _floats(a["pos"]) if "pos" in a else [0.0, 0.0, 0.0]
+    quat = _floats(a["quat"]) if "quat" in a else [1.0, 0.0, 0.0, 0.0]
+    normvec(quat)
+    quat = _resolve_orientation(a, self.degree, self.eulerseq, quat)
+    return {"body": bid, "pos": pos, "quat": quat, "mode": CAMLIGHT[a.get("mode", "fixed")],
+            "target": a.get("target"), "name": a.get("name", "")}
+
+  def _compile_light(self, a, bid):
+    pos = _floats(a["pos"]) if "pos" in a else [0.0, 0.0, 0.0]
+    d = _floats(a["dir"]) if "dir" in a else [0.0, 0.0, -1.0]
+    normvec(d)
+    return {"body": bid, "pos": pos, "dir": d, "mode": CAMLIGHT[a.get("mode", "fixed")],
+            "target": a.get("target"), "name": a.get("name", "")}
+
+  # ---------------------------------------------------------------- emit mjModel arrays
+  def _emit(self, jnts, geoms, sites, cams, lights) -> Model:
+    bodies = self.bodies
+    nbody, njnt = len(bodies), len(jnts)
+    nq = sum(_jnt_nq(j["type"]) for j in jnts)
+    nv = sum(_jnt_nv(j["type"]) for j in jnts)
+    bname = {b.name: b.id for b in bodies if b.name}
+    jname = {j["name"]: i for i, j in enumerate(jnts) if j["name"]}
+    m = Model()
+    s = m.sizes
+    s.update(nq=nq, nv=nv, nbody=nbody, njnt=njnt, ngeom=len(geoms), nsite=len(sites),
+             ncam=len(cams), nlight=len(lights), na=0, nmocap=0)
+    A = {}
+
+    def arr(name, shape, dtype, fill=0):
+      a = np.full(shape, fill, dtype=dtype)
+      A[name] = a
+      return a
+
+    # bodies
+    parentid = arr("body_parentid", nbody, np.int32)
+    rootid = arr("body_rootid", nbody, np.int32)
+    weldid = arr("body_weldid", nbody, np.int32)
+    arr("body_mocapid", nbody, np.int32, -1)
+    jntnum = arr("body_jntnum", nbody, np.int32)
+    jntadr = arr("body_jntadr", nbody, np.int32, -1)
+    dofnum = arr("body_dofnum", nbody, np.int32)
+    dofadr = arr("body_dofadr", nbody, np.int32, -1)
+    geomnum = arr("body_geomnum", nbody, np.int32)
+    geomadr = arr("body_geomadr", nbody, np.int32, -1)
+    simple = arr("body_simple", nbody, np.uint8)
+    sameframe = arr("body_sameframe", nbody, np.uint8)
+    bpos = arr("body_pos", (nbody, 3), np.float64)
+    bquat = arr("body_quat", (nbody, 4), np.float64)
+    bipos = arr("body_ipos", (nbody, 3), np.float64)
+    biquat = arr("body_iquat", (nbody, 4), np.float64)
+    bmass = arr("body_mass", nbody, np.float64)
+    binertia = arr("body_inertia", (nbody, 3), np.float64)
+    bgrav = arr("body_gravcomp", nbody, np.float64)
+    bmargin = arr("body_margin", nbody, np.float64)
+    bcontype = arr("body_contype", nbody, np.int32)
+    bconaff = arr("body_conaffinity", nbody, np.int32)
+    # joints / dofs
+    jtype = arr("jnt_type", njnt, np.int32)
+    jqadr = arr("jnt_qposadr", njnt, np.int32)
+    jdadr = arr("jnt_dofadr", njnt, np.int32)
+    jbody = arr("jnt_bodyid", njnt, np.int32)
+    jgroup = arr("jnt_group", njnt, np.int32)
+    jlim = arr("jnt_limited", njnt, np.uint8)
+    jagc = arr("jnt_actgravcomp", njnt, np.uint8)
+    jsolref = arr("jnt_solref", (njnt, 2), np.float64)
+    jsolimp = arr("jnt_solimp", (njnt, 5), np.float64)
+    jpos = arr("jnt_pos", (njnt, 3), np.float64)
+    jaxis = arr("jnt_axis", (njnt, 3), np.float64)
+    jstiff = arr("jnt_stiffness", njnt, np.float64)
+    jrange = arr("jnt_range", (njnt, 2), np.float64)
+    jmargin = arr("jnt_margin", njnt, np.float64)
+    qpos0 = arr("qpos0", nq, np.float64)
+    qspring = arr("qpos_spring", nq, np.float64)
+    dbody = arr("dof_bodyid", nv, np.int32)
+    djnt = arr("dof_jntid", nv, np.int32)
+    dparent = arr("dof_parentid", nv, np.int32)
+    dsolref = arr("dof_solref", (nv, 2), np.float64)
+    dsolimp = arr("dof_solimp", (nv, 5), np.float64)
+    dfloss = arr("dof_frictionloss", nv, np.float64)
+    darm = arr("dof_armature", nv, np.float64)
+    ddamp = arr("dof_damping", nv, np.float64)
+    arr("dof_invweight0", nv, np.float64)
+    arr("dof_M0", nv, np.float64)
+
+    jadr = qadr = dadr = 0
+    lastdof = {}
+    jid_of = {}
+    for b in bodies:
+      i = b.id
+      par = b.parent
+      parentid[i] = par.id if par else 0
+      weldid[i] = b.weldid
+      jntnum[i] = len(b.cjoints)
+      jntadr[i] = jadr if b.cjoints else -1
+      dofnum[i] = b.dofnum
+      dofadr[i] = dadr if b.dofnum else -1
+      geomnum[i] = len(b.cgeoms)
+      bpos[i] = b.pos
+      bquat[i] = b.quat
+      bipos[i] = b.ipos
+      biquat[i] = b.iquat
+      bmass[i] = b.mass
+      binertia[i] = b.inertia
+      bgrav[i] = b.gravcomp
+      nfree = sum(1 for j in b.cjoints if j["type"] == JNT["free"])
+      if nfree > 1 or (nfree == 1 and len(b.cjoints) > 1):
+        raise MJCFError("free joint can only appear by itself")
+      if nfree and par and par.id != 0:
+        raise MJCFError("free joint can only be used on top level")
+      rootid[i] = i if (i == 0 or (par and par.id == 0)) else rootid[par.id]
+      lastdof[i] = lastdof[par.id] if par else -1
+      if is_null_pose(b.ipos, b.iquat):
+        sf = 1  # BODY
+      elif is_null_pose(None, b.iquat):
+        sf = 3  # BODYROT
+      else:
+        sf = 0
+      sameframe[i] = sf
+      pid = parentid[i]
+      simple[i] = 1 if (sf == 1 and (rootid[i] == i or
+                                     (parentid[pid] == 0 and dofnum[pid] == 0))) else 0
+      if parentid[i] > 0:
+        simple[parentid[i]] = 0
+      rotfound = False
+      for j in b.cjoints:
+        t = j["type"]
+        jtype[jadr] = t
+        jgroup[jadr] = j["group"]
+        jlim[jadr] = 1 if j["limited"] else 0
+        jagc[jadr] = 1 if j["actgravcomp"] else 0
+        jqadr[jadr] = qadr
+        jdadr[jadr] = dadr
+        jbody[jadr] = i
+        jpos[jadr] = j["pos"]
+        jaxis[jadr] = j["axis"]
+        jstiff[jadr] = j["stiffness"]
+        jrange[jadr] = j["range"]
+        jsolref[jadr] = j["solref"]
+        jsolimp[jadr] = j["solimp"]
+        jmargin[jadr] = j["margin"]
+        jid_of[id(j)] = jadr
+        ax = j["axis"]
+        aligned = ((abs(ax[0]) > mjEPS) + (abs(ax[1]) > mjEPS) + (abs(ax[2]) > mjEPS)) == 1
+        if (rotfound or not is_null_pose(j["pos"], None) or
+            (t in (JNT["hinge"], JNT["slide"]) and not aligned)):
+          simple[i] = 0
+        if t in (JNT["ball"], JNT["hinge"]):
+          rotfound = True
+        if t == JNT["free"]:
+          qpos0[qadr:qadr+3] = b.pos
+          qpos0[qadr+3:qadr+7] = b.quat
+          qspring[qadr:qadr+7] = qpos0[qadr:qadr+7]
+        elif t == JNT["ball"]:
+          qpos0[qadr:qadr+4] = [1, 0, 0, 0]
+          qspring[qadr:qadr+4] = qpos0[qadr:qadr+4]
+        else:
+          qpos0[qadr] = j["ref"]
+          qspring[qadr] = j["springref"]
+        for _ in range(_jnt_nv(t)):
+          dbody[dadr] = i
+          djnt[dadr] = jadr
+          dsolref[dadr] = j["solref_f"]
+          dsolimp[dadr] = j["solimp_f"]
+          dfloss[dadr] = j["frictionloss"]
+          darm[dadr] = j["armature"]
+          ddamp[dadr] = j["damping"]
+          dparent[dadr] = lastdof[i]
+          lastdof[i] = dadr
+          dadr += 1
+        jadr += 1
+        qadr += _jnt_nq(t)
+      if simple[i] and dofnum[i]:
+        simple[i] = 2
+        for j in b.cjoints:
+          if j["type"] != JNT["slide"]:
+            simple[i] = 1
+            break
+    # geoms
+    ng = len(geoms)
+    g_int = {k: arr("geom_" + k, ng, np.int32) for k in
+             ("type", "contype", "conaffinity", "condim", "bodyid", "group", "priority")}
+    gsf = arr("geom_sameframe", ng, np.uint8)
+    g_f = {"solmix": arr("geom_solmix", ng, np.float64),
+           "rbound": arr("geom_rbound", ng, np.float64),
+           "margin": arr("geom_margin", ng, np.float64),
+           "gap": arr("geom_gap", ng, np.float64)}
+    gsolref = arr("geom_solref", (ng, 2), np.float64)
+    gsolimp = arr("geom_solimp", (ng, 5), np.float64)
+    gsize = arr("geom_size", (ng, 3), np.float64)
+    gpos = arr("geom_pos", (ng, 3), np.float64)
+    gquat = arr("geom_quat", (ng, 4), np.float64)
+    gfric = arr("geom_friction", (ng, 3), np.float64)
+    for gi, g in enumerate(geoms):
+      b = bodies[g["body"]]
+      if geomadr[b.id] < 0:
+        geomadr[b.id] = gi
+      g_int["type"][gi] = g["type"]
+      g_int["contype"][gi] = g["contype"]
+      g_int["conaffinity"][gi] = g["conaffinity"]
+      g_int["condim"][gi] = g["condim"]
+      g_int["bodyid"][gi] = g["body"]
+      g_int["group"][gi] = g["group"]
+      g_int["priority"][gi] = g["priority"]
+      if g["type"] == GEOM["plane"] and b.weldid != 0:
+        raise MJCFError("plane only allowed in static bodies")
+      g_f["solmix"][gi] = g["solmix"]
+      g_f["rbound"][gi] = g["rbound"]
+      g_f["margin"][gi] = g["margin"]
+      g_f["gap"][gi] = g["gap"]
+      gsolref[gi] = g["solref"]
+      gsolimp[gi] = g["solimp"]
+      gsize[gi] = g["size"]
+      gpos[gi] = g["pos"]
+      gquat[gi] = g["quat"]
+      gfric[gi] = g["friction"]
+      gsf[gi] = _sameframe(g["pos"], g["quat"], b.ipos, b.iquat)
+      bcontype[b.id] |= g["contype"]
+      bconaff[b.id] |= g["conaffinity"]
+      bmargin[b.id] = max(bmargin[b.id], g["margin"])
+    # sites
+    ns = len(sites)
+    stype = arr("site_type", ns, np.int32)
+    sbody = arr("site_bodyid", ns, np.int32)
+    ssf = arr("site_sameframe", ns, np.uint8)
+    ssize = arr("site_size", (ns, 3), np.float64)
+    spos = arr("site_pos", (ns, 3), np.float64)
+    squat = arr("site_quat", (ns, 4), np.float64)
+    for si_, st in enumerate(sites):
+      b = bodies[st["body"]]
+      stype[si_] = st["type"]
+      sbody[si_] = st["body"]
+      ssize[si_] = st["size"]
+      spos[si_] = st["pos"]
+      squat[si_] = st["quat"]
+      ssf[si_] = _sameframe(st["pos"], st["quat"], b.ipos, b.iquat)
+    # cameras / lights
+    nc = len(cams)
+    cmode = arr("cam_mode", nc, np.int32)
+    cbody = arr("cam_bodyid", nc, np.int32)
+    ctarget = arr("cam_targetbodyid", nc, np.int32, -1)
+    cpos = arr("cam_pos", (nc, 3), np.float64)
+    cquat = arr("cam_quat", (nc, 4), np.float64)
+    arr("cam_poscom0", (nc, 3), np.float64)
+    arr("cam_pos0", (nc, 3), np.float64)
+    arr("cam_mat0", (nc, 9), np.float64)
+    for ci, c in enumerate(cams):
+      cmode[ci] = c["mode"]
+      cbody[ci] = c["body"]
+      cpos[ci] = c["pos"]
+      cquat[ci] = c["quat"]
+      if c["target"]:
+        ctarget[ci] = bname[c["target"]]
+    nl = len(lights)
+    lmode = arr("light_mode", nl, np.int32)
+    lbody = arr("light_bodyid", nl, np.int32)
+    ltarget = arr("light_targetbodyid", nl, np.int32, -1)
+    lpos = arr("light_pos", (nl, 3), np.float64)
+    ldir = arr("light_dir", (nl, 3), np.float64)
+    arr("light_poscom0", (nl, 3), np.float64)
+    arr("light_pos0", (nl, 3), np.float64)
+    arr("light_dir0", (nl, 3), np.float64)
+    for li, l in enumerate(lights):
+      lmode[li] = l["mode"]
+      lbody[li] = l["body"]
+      lpos[li] = l["pos"]
+      ldir[li] = l["dir"]
+      if l["target"]:
+        ltarget[li] = bname[l["target"]]
+    # tendons (fixed only)
+    nt = len(self.tendons)
+    nwrap = sum(len(jl) for _, jl in self.tendons)
+    tadr = arr("tendon_adr", nt, np.int32)
+    tnum = arr("tendon_num", nt, np.int32)
+    tlim = arr("tendon_limited", nt, np.uint8)
+    tsolref = arr("tendon_solref_lim", (nt, 2), np.float64)
+    tsolimp = arr("tendon_solimp_lim", (nt, 5), np.float64)
+    trange = arr("tendon_range", (nt, 2), np.float64)
+    tmargin = arr("tendon_margin", nt, np.float64)
+    tstiff = arr("tendon_stiffness", nt, np.float64)
+    tdamp = arr("tendon_damping", nt, np.float64)
+    tls = arr("tendon_lengthspring", (nt, 2), np.float64)
+    arr("tendon_length0", nt, np.float64)
+    arr("tendon_invweight0", nt, np.float64)
+    wtype = arr("wrap_type", nwrap, np.int32)
+    wobj = arr("wrap_objid", nwrap, np.int32)
+    wprm = arr("wrap_prm", nwrap, np.float64)
+    w = 0
+    for ti, (ta, jl) in enumerate(self.tendons):
+      tadr[ti] = w
+      tnum[ti] = len(jl)
+      rng = _floats(ta["range"]) if "range" in ta else [0.0, 0.0]
+      lim = ta.get("limited", "auto")
+      if lim == "auto":
+        limited = self.autolimits and not (rng[0] == 0 and rng[1] == 0)
+      else:
+        limited = lim == "true"
+      if limited and rng[0] >= rng[1]:
+        raise MJCFError("invalid tendon range")
+      tlim[ti] = limited
+      trange[ti] = rng
+      tsolref[ti] = _floats(ta["solreflimit"]) if "solreflimit" in ta else [0.02, 1.0]
+      si = [0.9, 0.95, 0.001, 0.5, 2.0]
+      if "solimplimit" in ta:
+        v = _floats(ta["solimplimit"])
+        si[:len(v)] = v
+      tsolimp[ti] = si
+      tmargin[ti] = float(ta.get("margin", 0.0))
+      tstiff[ti] = float(ta.get("stiffness", 0.0))
+      tdamp[ti] = float(ta.get("damping", 0.0))
+      sl = _floats(ta["springlength"]) if "springlength" in ta else [-1.0, -1.0]
+      if len(sl) == 1:
+        sl = [sl[0], sl[0]]
+      tls[ti] = sl
+      for jn, coef in jl:
+        if jn not in jname:
+          raise MJCFError(f"unknown joint '{jn}' in tendon")
+        wtype[w] = 1  # mjWRAP_JOINT
+        wobj[w] = jname[jn]
+        wprm[w] = coef
+        w += 1
+    # actuators (joint transmission)
+    nu = len(self.actuators)
+    atrn = arr("actuator_trntype", nu, np.int32)
+    adyn = arr("actuator_dyntype", nu, np.int32)
+    again = arr("actuator_gaintype", nu, np.int32)
+    abias = arr("actuator_biastype", nu, np.int32)
+    atrnid = arr("actuator_trnid", (nu, 2), np.int32, -1)
+    actl = arr("actuator_ctrllimited", nu, np.uint8)
+    afl = arr("actuator_forcelimited", nu, np.uint8)
+    adynprm = arr("actuator_dynprm", (nu, 10), np.float64)
+    againprm = arr("actuator_gainprm", (nu, 10), np.float64)
+    abiasprm = arr("actuator_biasprm", (nu, 10), np.float64)
+    actr = arr("actuator_ctrlrange", (nu, 2), np.float64)
+    afr = arr("actuator_forcerange", (nu, 2), np.float64)
+    agear = arr("actuator_gear", (nu, 6), np.float64)
+    arr("actuator_length0", nu, np.float64)
+    arr("actuator_acc0", nu, np.float64)
+    for ai, a in enumerate(self.actuators):
+      tag = a["__tag"]
+      if "joint" not in a:
+        raise MJCFError("only joint transmissions are in the supported subset "
+                        "(slider-crank/site/tendon/body transmissions are next)")
+      atrn[ai] = 0
+      atrnid[ai, 0] = jname[a["joint"]]
+      gear = [1.0, 0, 0, 0, 0, 0]
+      if "gear" in a:
+        g = _floats(a["gear"])
+        gear[:len(g)] = g
+      agear[ai] = gear
+      adynprm[ai, 0] = 1.0
+      againprm[ai, 0] = 1.0
+      if tag == "general":
+        if "gainprm" in a:
+          v = _floats(a["gainprm"])
+          againprm[ai, :len(v)] = v
+        if "biasprm" in a:
+          v = _floats(a["biasprm"])
+          abiasprm[ai, :len(v)] = v
+        again[ai] = {"fixed": 0, "affine": 1}[a.get("gaintype", "fixed")]
+        abias[ai] = {"none": 0, "affine": 1}[a.get("biastype", "none")]
+        if a.get("dyntype", "none") != "none":
+          raise MJCFError("actuator dynamics are not in the supported subset")
+      elif tag == "position":
+        kp = float(a.get("kp", 1.0))
+        kv = float(a.get("kv", 0.0))
+        againprm[ai, 0] = kp
+        abias[ai] = 1
+        abiasprm[ai, 1] = -kp
+        abiasprm[ai, 2] = -kv
+      elif tag == "velocity":
+        kv = float(a.get("kv", 1.0))
+        againprm[ai, 0] = kv
+        abias[ai] = 1
+        abiasprm[ai, 2] = -kv
+      cr = _floats(a["ctrlrange"]) if "ctrlrange" in a else [0.0, 0.0]
+      cl = a.get("ctrllimited", "auto")
+      actl[ai] = (not (cr[0] == 0 and cr[1] == 0)) if cl == "auto" else (cl == "true")
+      actr[ai] = cr
+      fr = _floats(a["forcerange"]) if "forcerange" in a else [0.0, 0.0]
+      fl = a.get("forcelimited", "auto")
+      afl[ai] = (not (fr[0] == 0 and fr[1] == 0)) if fl == "auto" else (fl == "true")
+      afr[ai] = fr
+    # exclude pairs: signature = (body1 << 16) + body2 with body1 < body2
+    nex = len(self.excludes)
+    exs = arr("exclude_signature", nex, np.int32)
+    for ei, (b1, b2) in enumerate(self.excludes):
+      i1, i2 = bname[b1], bname[b2]
+      exs[ei] = (min(i1, i2) << 16) + max(i1, i2)
+    # keyframes
+    nkey = len(self.keys)
+    kq = arr("key_qpos", (nkey, nq), np.float64)
+    for ki, k in enumerate(self.keys):
+      kq[ki] = qpos0
+      if "qpos" in k:
+        kq[ki] = _floats(k["qpos"])
+    s.update(nu=nu, ntendon=nt, nwrap=nwrap, nexclude=nex, nkey=nkey)
+    # ---- dof tree quantities (user_model.cc:2441-2617)
+    ntree = 0
+    dtree = arr("dof_treeid", nv, np.int32)
+    for i in range(nv):
+      if dparent[i] == -1:
+        ntree += 1
+      dtree[i] = ntree - 1
+    btree = arr("body_treeid", nbody, np.int32, -1)
+    for i in range(nbody):
+      wid = weldid[i]
+      if dofnum[wid]:
+        btree[i] = dtree[dofadr[wid]]
+    s["ntree"] = ntree
+    s["ngravcomp"] = int(np.sum(bgrav > 0))
+    Madr = arr("dof_Madr", nv, np.int32)
+    nM = 0
+    for i in range(nv):
+      Madr[i] = nM
+      j = i
+      while j >= 0:
+        nM += 1
+        j = dparent[j]
+    s["nM"] = nM
+    s["nD"] = 2*nM - nv
+    simplenum = arr("dof_simplenum", nv, np.int32)
+    count = 0
+    for i in range(nv - 1, -1, -1):
+      count = count + 1 if simple[dbody[i]] else 0
+      simplenum[i] = count
+    nOD = 0
+    for i in range(nv):
+      if not simplenum[i]:
+        j = i
+        while j >= 0:
+          if j != i:
+            nOD += 1
+          j = dparent[j]
+    s["nC"] = nC = nOD + nv
+    # C sparse structure and mapM2C (engine_io.c:929-1018, 1135-1259; reduced=1)
+    rownnz = arr("C_rownnz", nv, np.int32)
+    rowadr = arr("C_rowadr", nv, np.int32)
+    colind = arr("C_colind", nC, np.int32)
+    mapM2C = arr("mapM2C", nC, np.int32, -1)
+    for i in range(nv - 1, -1, -1):
+      rownnz[i] += 1
+      if not simplenum[i]:
+        j = i
+        while True:
+          j = dparent[j]
+          if j < 0:
+            break
+          rownnz[i] += 1
+    for i in range(1, nv):
+      rowadr[i] = rowadr[i-1] + rownnz[i-1]
+    remaining = rownnz.copy()
+    for i in range(nv - 1, -1, -1):
+      remaining[i] -= 1
+      colind[rowadr[i] + remaining[i]] = i
+      adr = Madr[i]
+      mapM2C[rowadr[i] + remaining[i]] = adr
+      adr += 1
+      if not simplenum[i]:
+        j = i
+        while True:
+          j = dparent[j]
+          if j < 0:
+            break
+          remaining[i] -= 1
+          colind[rowadr[i] + remaining[i]] = j
+          mapM2C[rowadr[i] + remaining[i]] = adr
+          adr += 1
+    if nv and (remaining != 0).any():
+      raise MJCFError("unexpected remaining")  # SHOULD NOT OCCUR
+    # actuator moment sparse structure for joint transmissions (smooth.c:896-916)
+    nJmom = 0
+    mrownnz = arr("moment_rownnz", nu, np.int32)
+    mrowadr = arr("moment_rowadr", nu, np.int32)
+    for ai in range(nu):
+      jid = atrnid[ai, 0]
+      cnt = {0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[jid])]
+      if cnt != 1:
+        raise MJCFError("ball/free joint transmissions are not in the supported subset")
+      mrownnz[ai] = 1
+      mrowadr[ai] = nJmom
+      nJmom += cnt
+    mcol = arr("moment_colind", nJmom, np.int32)
+    for ai in range(nu):
+      mcol[mrowadr[ai]] = jdadr[atrnid[ai, 0]]
+    s["nJmom"] = nJmom
+    # scalars and names
+    m.opt = {k: (list(v) if isinstance(v, list) else v) for k, v in self.opt.items()}
+    for k, v in A.items():
+      setattr(m, k, v)
+    arr("body_subtreemass", nbody, np.float64)
+    arr("body_invweight0", (nbody, 2), np.float64)
+    setattr(m, "body_subtreemass", A["body_subtreemass"])
+    setattr(m, "body_invweight0", A["body_invweight0"])
+    m.names = {"body": [b.name for b in bodies], "jnt": [j["name"] for j in jnts],
+               "geom": [g["name"] for g in geoms], "site": [x["name"] for x in sites],
+               "cam": [c["name"] for c in cams], "light": [l["name"] for l in lights],
+               "tendon": [ta.get("name", "") for ta, _ in self.tendons],
+               "actuator": [a.get("name", "") for a in self.actuators],
+               "key": [k.get("name", "") for k in self.keys]}
+    m.model_name = getattr(self, "model_name", "")
+    # check every field of the table is present with the right shape
+    for f in fields.MODEL_FIELDS:
+      a = getattr(m, f.name)
+      want = f.shape(m.sizes)
+      if want[1] == 1:
+        want = want[:1]
+      setattr(m, f.name, np.ascontiguousarray(a.reshape(want).astype(fields.NPTYPE[f.ctype])))
+    return m
+
+
+def _sameframe(pos, quat, ipos, iquat):
+  """Geom/site sameframe (user_model.cc:2404-2416, 2444-2456)."""
+  if is_null_pose(pos, quat):
+    return 1      # BODY
+  if is_null_pose(None, quat):
+    return 3      # BODYROT
+  if is_same_pose(pos, ipos, quat, iquat):
+    return 2      # INERTIA
+  if is_same_pose(None, None, quat, iquat):
+    return 4      # INERTIAROT
+  return 0
+
+
+def _jnt_nq(t):
+  return {0: 7, 1: 4, 2: 1, 3: 1}[t]
+
+
+def _jnt_nv(t):
+  return {0: 6, 1: 3, 2: 1, 3: 1}[t]
+
+
+def _geom_volume(t, size):
+  """mjCGeom::GetVolume, typeinertia = volume (user_objects.cc:2384-2460)."""
+  if t == GEOM["sphere"]:
+    r = size[0]
+    return 4 * mjPI * r * r * r / 3
+  if t == GEOM["capsule"]:
+    h = 2 * size[1]
+    r = size[0]
+    return mjPI * (r * r * h + 4 * r * r * r / 3)
+  if t == GEOM["cylinder"]:
+    h = 2 * size[1]
+    r = size[0]
+    return mjPI * r * r * h
+  if t == GEOM["ellipsoid"]:
+    return 4 * mjPI * size[0] * size[1] * size[2] / 3
+  if t in (GEOM["box"], GEOM["hfield"]):
+    return size[0] * size[1] * size[2] * 8
+  return 0.0
+
+
+def _geom_inertia(t, size, mass):
+  """mjCGeom::SetInertia, typeinertia = volume (user_objects.cc:2474-2560)."""
+  if t == GEOM["sphere"]:
+    v = 2 * mass * size[0] * size[0] / 5
+    return [v, v, v]
+  if t == GEOM["capsule"]:
+    height = 2 * size[1]
+    radius = size[0]
+    sphere_mass = mass * 4 * radius / (4 * radius + 3 * height)
+    cylinder_mass = mass - sphere_mass
+    i0 = cylinder_mass * (3 * radius * radius + height * height) / 12
+    i2 = cylinder_mass * radius * radius / 2
+    sphere_inertia = 2 * sphere_mass * radius * radius / 5
+    i0 += sphere_inertia + sphere_mass * height * (3 * radius + 2 * height) / 8
+    i1 = i0
+    i2 += sphere_inertia
+    return [i0, i1, i2]
+  if t == GEOM["cylinder"]:
+    height = 2 * size[1]
+    radius = size[0]
+    i0 = mass * (3 * radius * radius + height * height) / 12
+    return [i0, i0, mass * radius * radius / 2]
+  if t == GEOM["ellipsoid"]:
+    s = size
+    return [mass * (s[1]*s[1] + s[2]*s[2]) / 5, mass * (s[0]*s[0] + s[2]*s[2]) / 5,
+            mass * (s[0]*s[0] + s[1]*s[1]) / 5]
+  if t == GEOM["box"]:
+    s = size
+    return [mass * (s[1]*s[1] + s[2]*s[2]) / 3, mass * (s[0]*s[0] + s[2]*s[2]) / 3,
+            mass * (s[0]*s[0] + s[1]*s[1]) / 3]
+  return [0.0, 0.0, 0.0]
+
+
+def _geom_rbound(t, size):
+  """mjCGeom::GetRBound (radius of the bounding sphere)."""
+  if t == GEOM["sphere"]:
+    return size[0]
+  if t == GEOM["capsule"]:
+    return size[0] + size[1]
+  if t == GEOM["cylinder"]:
+    return math.sqrt(size[0]*size[0] + size[1]*size[1])
+  if t == GEOM["ellipsoid"]:
+    return max(size[0], size[1], size[2])
+  if t == GEOM["box"]:
+    return math.sqrt(size[0]*size[0] + size[1]*size[1] + size[2]*size[2])
+  return 0.0
+
+
+def load_xml_string(text: str, basedir: str | None = None) -> Model:
+  """Compile an MJCF string (the LoadModelFromString of test/fixture.h:85-97)."""
+  from . import setconst
+  root = ET.fromstring(text)
+  c = MJCFCompiler()
+  c.parse(root)
+  m = c.compile()
+  setconst.set_const(m)
+  return m
+
+
+def load_xml(path: str) -> Model:
+  """Compile an MJCF file (mj_loadXML, src/xml/xml_api.cc:97, restricted to the subset)."""
+  with open(path) as f:
+    return load_xml_string(f.read(), os.path.dirname(os.path.abspath(path)))

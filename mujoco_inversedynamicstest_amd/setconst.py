@@ -1,0 +1,283 @@
+"""Compile-time model constants (mj_setConst, src/engine/engine_setconst.c:580-597).
+
+Evaluates the model once at qpos0 (and once at qpos_spring) on the host to fill the
+constant fields the inverse path reads:
+
+  body_subtreemass                      engine_setconst.c:582-588
+  dof_M0 (used by simple dofs in crb)   engine_setconst.c:37-59  (mj_setM0)
+  body_invweight0, dof_invweight0       engine_setconst.c:124-210 (constraint diagApprox)
+  tendon_invweight0, actuator_acc0      engine_setconst.c:212-300
+  tendon_length0, actuator_length0      engine_setconst.c:108-111
+  cam_pos0/poscom0/mat0, light_*0       engine_setconst.c:346-373
+  tendon_lengthspring (if -1)           engine_setconst.c:560-575 (setSpring)
+
+This runs once per model load, never per instance: it is the model compiler's job (the
+reference runs it inside mj_compile), not a CPU path for mj_inverse. Dense numpy linear
+algebra is used where the reference solves with its sparse LTDL; the constants therefore
+match the reference's to rounding, not bit-for-bit (compiled-model parity is unpinned,
+DESIGN.md).
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from . import mjcf
+
+
+def _quat2mat(q):
+  return np.array(mjcf.quat2mat(list(q))).reshape(3, 3)
+
+
+def _mulquat(a, b):
+  return np.array([a[0]*b[0] - a[1]*b[1] - a[2]*b[2] - a[3]*b[3],
+                   a[0]*b[1] + a[1]*b[0] + a[2]*b[3] - a[3]*b[2],
+                   a[0]*b[2] - a[1]*b[3] + a[2]*b[0] + a[3]*b[1],
+                   a[0]*b[3] + a[1]*b[2] - a[2]*b[1] + a[3]*b[0]])
+
+
+def _rot(v, q):
+  return _quat2mat(q) @ np.asarray(v)
+
+
+def _axis_angle_quat(axis, ang):
+  if ang == 0:
+    return np.array([1.0, 0, 0, 0])
+  s = np.sin(ang*0.5)
+  return np.array([np.cos(ang*0.5), axis[0]*s, axis[1]*s, axis[2]*s])
+
+
+def _normq(q):
+  n = np.linalg.norm(q)
+  return q / n if n > 1e-15 else np.array([1.0, 0, 0, 0])
+
+
+class _Eval:
+  """qpos-dependent quantities of one configuration (mj_kinematics/mj_comPos/mj_crb)."""
+
+  def __init__(self, m, qpos):
+    nb = m.nbody
+    self.xpos = np.zeros((nb, 3))
+    self.xquat = np.zeros((nb, 4))
+    self.xquat[0, 0] = 1
+    self.xmat = np.zeros((nb, 3, 3))
+    self.xmat[0] = np.eye(3)
+    self.xanchor = np.zeros((m.njnt, 3))
+    self.xaxis = np.zeros((m.njnt, 3))
+    for i in range(1, nb):
+      ja, jn = m.body_jntadr[i], m.body_jntnum[i]
+      if jn == 1 and m.jnt_type[ja] == 0:
+        qa = m.jnt_qposadr[ja]
+        xpos = qpos[qa:qa+3].copy()
+        xquat = _normq(qpos[qa+3:qa+7].copy())
+        self.xanchor[ja] = xpos
+        self.xaxis[ja] = m.jnt_axis[ja]
+      else:
+        pid = m.body_parentid[i]
+        if pid:
+          xpos = self.xmat[pid] @ m.body_pos[i] + self.xpos[pid]
+          xquat = _mulquat(self.xquat[pid], m.body_quat[i])
+        else:
+          xpos = m.body_pos[i].copy()
+          xquat = m.body_quat[i].copy()
+        for j in range(ja, ja + jn):
+          qa = m.jnt_qposadr[j]
+          xaxis = _rot(m.jnt_axis[j], xquat)
+          xanchor = _rot(m.jnt_pos[j], xquat) + xpos
+          t = m.jnt_type[j]
+          if t == 2:
+            xpos = xpos + xaxis * (qpos[qa] - m.qpos0[qa])
+          else:
+            qloc = _normq(qpos[qa:qa+4].copy()) if t == 1 else \
+                _axis_angle_quat(m.jnt_axis[j], qpos[qa] - m.qpos0[qa])
+            xquat = _mulquat(xquat, qloc)
+            xpos = xanchor - _rot(m.jnt_pos[j], xquat)
+          self.xanchor[j] = xanchor
+          self.xaxis[j] = xaxis
+      xquat = _normq(xquat)
+      self.xquat[i] = xquat
+      self.xpos[i] = xpos
+      self.xmat[i] = _quat2mat(xquat)
+    self.xipos = np.zeros((nb, 3))
+    self.ximat = np.zeros((nb, 3, 3))
+    self.ximat[0] = np.eye(3)
+    for i in range(1, nb):
+      self.xipos[i] = self.xmat[i] @ m.body_ipos[i] + self.xpos[i]
+      self.ximat[i] = _quat2mat(_mulquat(self.xquat[i], m.body_iquat[i]))
+    # subtree com (smooth.c:183-215)
+    com = np.zeros((nb, 3))
+    ms = np.zeros(nb)
+    for i in range(nb - 1, -1, -1):
+      com[i] += self.xipos[i] * m.body_mass[i]
+      ms[i] += m.body_mass[i]
+      if i:
+        j = m.body_parentid[i]
+        com[j] += com[i]
+        ms[j] += ms[i]
+      com[i] = self.xipos[i] if ms[i] < 1e-15 else com[i] / max(1e-15, ms[i])
+    self.subtree_com = com
+    # cdof (smooth.c:225-266)
+    self.cdof = np.zeros((m.nv, 6))
+    for j in range(m.njnt):
+      da = m.jnt_dofadr[j]
+      bi = m.jnt_bodyid[j]
+      off = com[m.body_rootid[bi]] - self.xanchor[j]
+      t = m.jnt_type[j]
+      if t in (0, 1):
+        skip = 0
+        if t == 0:
+          for k in range(3):
+            self.cdof[da + k, 3 + k] = 1
+          skip = 3
+        for k in range(3):
+          ax = self.xmat[bi][:, k]
+          self.cdof[da + skip + k, :3] = ax
+          self.cdof[da + skip + k, 3:] = np.cross(ax, off)
+      elif t == 2:
+        self.cdof[da, 3:] = self.xaxis[j]
+      else:
+        self.cdof[da, :3] = self.xaxis[j]
+        self.cdof[da, 3:] = np.cross(self.xaxis[j], off)
+    # spatial inertia at subtree com (6x6) per body
+    self.I6 = np.zeros((nb, 6, 6))
+    for i in range(1, nb):
+      R = self.ximat[i]
+      Ic = R @ np.diag(m.body_inertia[i]) @ R.T
+      c = self.xipos[i] - com[m.body_rootid[i]]
+      mass = m.body_mass[i]
+      cx = np.array([[0, -c[2], c[1]], [c[2], 0, -c[0]], [-c[1], c[0], 0]])
+      I6 = np.zeros((6, 6))
+      I6[:3, :3] = Ic - mass * cx @ cx
+      I6[:3, 3:] = mass * cx
+      I6[3:, :3] = -mass * cx
+      I6[3:, 3:] = mass * np.eye(3)
+      self.I6[i] = I6
+    # composite inertia and dense M
+    crb = self.I6.copy()
+    for i in range(nb - 1, 0, -1):
+      if m.body_parentid[i] > 0:
+        crb[m.body_parentid[i]] += crb[i]
+    self.crb = crb
+    M = np.zeros((m.nv, m.nv))
+    for i in range(m.nv):
+      buf = crb[m.dof_bodyid[i]] @ self.cdof[i]
+      j = i
+      while j >= 0:
+        M[i, j] = M[j, i] = self.cdof[j] @ buf
+        j = m.dof_parentid[j]
+      M[i, i] += m.dof_armature[i]
+    self.M = M
+
+  def jac_point(self, m, body, point):
+    """mj_jac (engine_support.c:389-441): 3 x nv translation and rotation Jacobians."""
+    jacp = np.zeros((3, m.nv))
+    jacr = np.zeros((3, m.nv))
+    if m.body_dofnum[body] == 0:
+      # walk up to the first ancestor with dofs
+      b = body
+      while b > 0 and m.body_dofnum[b] == 0:
+        b = m.body_parentid[b]
+      if b == 0:
+        return jacp, jacr
+      j = m.body_dofadr[b] + m.body_dofnum[b] - 1
+    else:
+      j = m.body_dofadr[body] + m.body_dofnum[body] - 1
+    off = point - self.subtree_com[m.body_rootid[body]]
+    while j >= 0:
+      c = self.cdof[j]
+      jacr[:, j] = c[:3]
+      jacp[:, j] = c[3:] + np.cross(c[:3], off)
+      j = m.dof_parentid[j]
+    return jacp, jacr
+
+
+def set_const(m):
+  """Fill the compile-time constants of `m` in place (mj_setConst subset)."""
+  nv, nb = m.nv, m.nbody
+  # subtree mass
+  stm = m.body_mass.astype(np.float64).copy()
+  for i in range(nb - 1, 0, -1):
+    stm[m.body_parentid[i]] += stm[i]
+  m.body_subtreemass[:] = stm
+  e = _Eval(m, m.qpos0.astype(np.float64))
+  # dof_M0 (mj_setM0): armature + cdof_i . (crb_i cdof_i)
+  for i in range(nv):
+    m.dof_M0[i] = m.dof_armature[i] + e.cdof[i] @ (e.crb[m.dof_bodyid[i]] @ e.cdof[i])
+  Minv = np.linalg.inv(e.M) if nv else np.zeros((0, 0))
+  # body_invweight0
+  m.body_invweight0[:] = 0
+  for i in range(1, nb):
+    if m.body_weldid[i] == 0:
+      continue
+    if m.body_simple[i] == 2:
+      m.body_invweight0[i] = [1 / max(1e-15, m.body_mass[i]), 0]
+      continue
+    jacp, jacr = e.jac_point(m, i, e.xipos[i])
+    J = np.vstack([jacp, jacr])
+    A = J @ Minv @ J.T if nv else np.zeros((6, 6))
+    m.body_invweight0[i, 0] = (A[0, 0] + A[1, 1] + A[2, 2]) / 3
+    m.body_invweight0[i, 1] = (A[3, 3] + A[4, 4] + A[5, 5]) / 3
+  # dof_invweight0
+  for j in range(m.njnt):
+    da = m.jnt_dofadr[j]
+    bi = m.jnt_bodyid[j]
+    if m.body_simple[bi] == 2:
+      m.dof_invweight0[da] = 1 / max(1e-15, m.body_mass[bi])
+      continue
+    t = m.jnt_type[j]
+    dn = {0: 6, 1: 3}.get(int(t), 1)
+    A = Minv[da:da+dn, da:da+dn]
+    if dn == 6:
+      m.dof_invweight0[da:da+3] = np.trace(A[:3, :3]) / 3
+      m.dof_invweight0[da+3:da+6] = np.trace(A[3:, 3:]) / 3
+    elif dn == 3:
+      m.dof_invweight0[da:da+3] = np.trace(A) / 3
+    else:
+      m.dof_invweight0[da] = A[0, 0]
+  # tendons (fixed): length and dense J at qpos0
+  def tendon(q):
+    L = np.zeros(m.ntendon)
+    J = np.zeros((m.ntendon, nv))
+    for t in range(m.ntendon):
+      adr, num = m.tendon_adr[t], m.tendon_num[t]
+      for w in range(adr, adr + num):
+        k = m.wrap_objid[w]
+        L[t] += m.wrap_prm[w] * q[m.jnt_qposadr[k]]
+        J[t, m.jnt_dofadr[k]] = m.wrap_prm[w]
+    return L, J
+  L0, J0 = tendon(m.qpos0)
+  m.tendon_length0[:] = L0
+  for t in range(m.ntendon):
+    m.tendon_invweight0[t] = J0[t] @ Minv @ J0[t] if nv else 0.0
+  # actuators (joint transmission)
+  for a in range(m.nu):
+    jid = m.actuator_trnid[a, 0]
+    g = m.actuator_gear[a, 0]
+    m.actuator_length0[a] = m.qpos0[m.jnt_qposadr[jid]] * g
+    mom = np.zeros(nv)
+    mom[m.jnt_dofadr[jid]] = g
+    m.actuator_acc0[a] = np.linalg.norm(Minv @ mom) if nv else 0.0
+  # cameras / lights at qpos0 in fixed mode (engine_setconst.c:346-373)
+  for c in range(m.ncam):
+    b = m.cam_bodyid[c]
+    pos = e.xmat[b] @ m.cam_pos[c] + e.xpos[b]
+    mat = _quat2mat(_mulquat(e.xquat[b], m.cam_quat[c]))
+    t = m.cam_targetbodyid[c]
+    m.cam_pos0[c] = pos - e.xpos[b]
+    m.cam_poscom0[c] = pos - e.subtree_com[t if t >= 0 else b]
+    m.cam_mat0[c] = mat.reshape(9)
+  for l in range(m.nlight):
+    b = m.light_bodyid[l]
+    pos = e.xmat[b] @ m.light_pos[l] + e.xpos[b]
+    d = _rot(m.light_dir[l], e.xquat[b])
+    n = np.linalg.norm(d)
+    d = d / n if n >= 1e-15 else np.array([1.0, 0, 0])
+    t = m.light_targetbodyid[l]
+    m.light_pos0[l] = pos - e.xpos[b]
+    m.light_poscom0[l] = pos - e.subtree_com[t if t >= 0 else b]
+    m.light_dir0[l] = d
+  # tendon spring length at qpos_spring (setSpring)
+  Ls, _ = tendon(m.qpos_spring)
+  for t in range(m.ntendon):
+    if m.tendon_lengthspring[t, 0] == -1 and m.tendon_lengthspring[t, 1] == -1:
+      m.tendon_lengthspring[t] = Ls[t]
+  return m

@@ -1,0 +1,1611 @@
+/* mj_oracle.c — TEST INFRASTRUCTURE ONLY (see mj_oracle.h).
+ *
+ * Line-by-line CPU restatement of the reference's mj_inverse path, each function citing
+ * the reference file:line it follows (paths relative to the reference root,
+ * /root/reference). Scalar (non-AVX) summation orders. Compiled with -O2
+ * -ffp-contract=off so no FMA contraction changes rounding.
+ */
+#define _GNU_SOURCE
+#include "mj_oracle.h"
+
+#include <math.h>
+#include <pthread.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define mjMINVAL mjhipMINVAL
+#define mjMAX(a, b) (((a) > (b)) ? (a) : (b))
+#define mjMIN(a, b) (((a) < (b)) ? (a) : (b))
+#define mjDISABLED(x) (m->opt.disableflags & (x))
+#define mjENABLED(x) (m->opt.enableflags & (x))
+
+/*============================ engine_util_blas.c ==========================================*/
+
+static void mju_zero3(mjtNum r[3]) { r[0] = r[1] = r[2] = 0; }
+static void mju_copy3(mjtNum r[3], const mjtNum a[3]) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+static void mju_copy4(mjtNum r[4], const mjtNum a[4]) {
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+}
+static void mju_scl3(mjtNum r[3], const mjtNum a[3], mjtNum s) {
+  r[0] = a[0]*s; r[1] = a[1]*s; r[2] = a[2]*s;
+}
+static void mju_add3(mjtNum r[3], const mjtNum a[3], const mjtNum b[3]) {
+  r[0] = a[0]+b[0]; r[1] = a[1]+b[1]; r[2] = a[2]+b[2];
+}
+static void mju_sub3(mjtNum r[3], const mjtNum a[3], const mjtNum b[3]) {
+  r[0] = a[0]-b[0]; r[1] = a[1]-b[1]; r[2] = a[2]-b[2];
+}
+static void mju_addTo3(mjtNum r[3], const mjtNum a[3]) { r[0] += a[0]; r[1] += a[1]; r[2] += a[2]; }
+static void mju_addToScl3(mjtNum r[3], const mjtNum a[3], mjtNum s) {
+  r[0] += a[0]*s; r[1] += a[1]*s; r[2] += a[2]*s;
+}
+static void mju_cross(mjtNum r[3], const mjtNum a[3], const mjtNum b[3]) {   /* blas.c */
+  mjtNum tmp[3] = {a[1]*b[2] - a[2]*b[1], a[2]*b[0] - a[0]*b[2], a[0]*b[1] - a[1]*b[0]};
+  r[0] = tmp[0]; r[1] = tmp[1]; r[2] = tmp[2];
+}
+
+/* engine_util_blas.c:123-140 */
+static mjtNum mju_normalize3(mjtNum v[3]) {
+  mjtNum norm = sqrt(v[0]*v[0] + v[1]*v[1] + v[2]*v[2]);
+  if (norm < mjMINVAL) {
+    v[0] = 1; v[1] = 0; v[2] = 0;
+  } else {
+    mjtNum normInv = 1/norm;
+    v[0] *= normInv; v[1] *= normInv; v[2] *= normInv;
+  }
+  return norm;
+}
+
+/* engine_util_blas.c:165-176 */
+static void mju_mulMatVec3(mjtNum res[3], const mjtNum mat[9], const mjtNum vec[3]) {
+  mjtNum tmp[3] = {
+    mat[0]*vec[0] + mat[1]*vec[1] + mat[2]*vec[2],
+    mat[3]*vec[0] + mat[4]*vec[1] + mat[5]*vec[2],
+    mat[6]*vec[0] + mat[7]*vec[1] + mat[8]*vec[2]
+  };
+  res[0] = tmp[0]; res[1] = tmp[1]; res[2] = tmp[2];
+}
+
+/* engine_util_blas.c:269-285 */
+static mjtNum mju_normalize4(mjtNum v[4]) {
+  mjtNum norm = sqrt(v[0]*v[0] + v[1]*v[1] + v[2]*v[2] + v[3]*v[3]);
+  if (norm < mjMINVAL) {
+    v[0] = 1; v[1] = 0; v[2] = 0; v[3] = 0;
+  } else if (fabs(norm - 1) > mjMINVAL) {
+    mjtNum normInv = 1/norm;
+    v[0] *= normInv; v[1] *= normInv; v[2] *= normInv; v[3] *= normInv;
+  }
+  return norm;
+}
+
+static void mju_zero(mjtNum* r, int n) { memset(r, 0, n*sizeof(mjtNum)); }
+static void mju_copy(mjtNum* r, const mjtNum* a, int n) { memcpy(r, a, n*sizeof(mjtNum)); }
+static void mju_scl(mjtNum* r, const mjtNum* a, mjtNum s, int n) {            /* :342-383 */
+  for (int i = 0; i < n; i++) r[i] = a[i]*s;
+}
+static void mju_add(mjtNum* r, const mjtNum* a, const mjtNum* b, int n) {    /* :387 */
+  for (int i = 0; i < n; i++) r[i] = a[i] + b[i];
+}
+static void mju_sub(mjtNum* r, const mjtNum* a, const mjtNum* b, int n) {    /* :430 */
+  for (int i = 0; i < n; i++) r[i] = a[i] - b[i];
+}
+static void mju_addTo(mjtNum* r, const mjtNum* a, int n) {                    /* :473 */
+  for (int i = 0; i < n; i++) r[i] += a[i];
+}
+static void mju_subFrom(mjtNum* r, const mjtNum* a, int n) {                  /* :516 */
+  for (int i = 0; i < n; i++) r[i] -= a[i];
+}
+static void mju_addToScl(mjtNum* r, const mjtNum* a, mjtNum s, int n) {      /* :559-600 */
+  for (int i = 0; i < n; i++) r[i] += a[i]*s;
+}
+
+/* engine_util_blas.c:680-741, scalar branch: four lanes, then (r0+r2)+(r1+r3), then tail */
+static mjtNum mju_dot(const mjtNum* a, const mjtNum* b, int n) {
+  mjtNum res = 0;
+  int i = 0;
+  int n_4 = n - 4;
+  mjtNum r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  for (; i <= n_4; i += 4) {
+    r0 += a[i]*b[i];
+    r1 += a[i+1]*b[i+1];
+    r2 += a[i+2]*b[i+2];
+    r3 += a[i+3]*b[i+3];
+  }
+  res = (r0 + r2) + (r1 + r3);
+  int n_i = n - i;
+  if (n_i == 3) {
+    res += a[i]*b[i] + a[i+1]*b[i+1] + a[i+2]*b[i+2];
+  } else if (n_i == 2) {
+    res += a[i]*b[i] + a[i+1]*b[i+1];
+  } else if (n_i == 1) {
+    res += a[i]*b[i];
+  }
+  return res;
+}
+
+static mjtNum mju_norm(const mjtNum* a, int n) { return sqrt(mju_dot(a, a, n)); }
+
+/* engine_util_blas.c:747-752 */
+static void mju_mulMatVec(mjtNum* res, const mjtNum* mat, const mjtNum* vec, int nr, int nc) {
+  for (int r = 0; r < nr; r++) res[r] = mju_dot(mat + r*nc, vec, nc);
+}
+
+/* engine_util_blas.c:756-766 */
+static void mju_mulMatTVec(mjtNum* res, const mjtNum* mat, const mjtNum* vec, int nr, int nc) {
+  mjtNum tmp;
+  mju_zero(res, nc);
+  for (int r = 0; r < nr; r++) {
+    if ((tmp = vec[r])) mju_addToScl(res, mat + r*nc, tmp, nc);
+  }
+}
+
+static int mju_isZero(const mjtNum* v, int n) {
+  for (int i = 0; i < n; i++) if (v[i] != 0) return 0;
+  return 1;
+}
+
+/* engine_util_sparse.h:115-160 (scalar branch) */
+static mjtNum mju_dotSparse(const mjtNum* v1, const mjtNum* v2, int nnz1, const int* ind1) {
+  int i = 0;
+  mjtNum res = 0;
+  int n_4 = nnz1 - 4;
+  mjtNum r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  for (; i <= n_4; i += 4) {
+    r0 += v1[i+0]*v2[ind1[i+0]];
+    r1 += v1[i+1]*v2[ind1[i+1]];
+    r2 += v1[i+2]*v2[ind1[i+2]];
+    r3 += v1[i+3]*v2[ind1[i+3]];
+  }
+  res = (r0 + r2) + (r1 + r3);
+  for (; i < nnz1; i++) res += v1[i]*v2[ind1[i]];
+  return res;
+}
+
+/*============================ engine_util_spatial.c =======================================*/
+
+/* :23-46 */
+static void mju_rotVecQuat(mjtNum res[3], const mjtNum vec[3], const mjtNum quat[4]) {
+  if (vec[0] == 0 && vec[1] == 0 && vec[2] == 0) {
+    mju_zero3(res);
+  } else if (quat[0] == 1 && quat[1] == 0 && quat[2] == 0 && quat[3] == 0) {
+    mju_copy3(res, vec);
+  } else {
+    mjtNum tmp[3] = {
+      quat[0]*vec[0] + quat[2]*vec[2] - quat[3]*vec[1],
+      quat[0]*vec[1] + quat[3]*vec[0] - quat[1]*vec[2],
+      quat[0]*vec[2] + quat[1]*vec[1] - quat[2]*vec[0]
+    };
+    res[0] = vec[0] + 2 * (quat[2]*tmp[2] - quat[3]*tmp[1]);
+    res[1] = vec[1] + 2 * (quat[3]*tmp[0] - quat[1]*tmp[2]);
+    res[2] = vec[2] + 2 * (quat[1]*tmp[1] - quat[2]*tmp[0]);
+  }
+}
+
+/* :62-74 */
+static void mju_mulQuat(mjtNum res[4], const mjtNum qa[4], const mjtNum qb[4]) {
+  mjtNum tmp[4] = {
+    qa[0]*qb[0] - qa[1]*qb[1] - qa[2]*qb[2] - qa[3]*qb[3],
+    qa[0]*qb[1] + qa[1]*qb[0] + qa[2]*qb[3] - qa[3]*qb[2],
+    qa[0]*qb[2] - qa[1]*qb[3] + qa[2]*qb[0] + qa[3]*qb[1],
+    qa[0]*qb[3] + qa[1]*qb[2] - qa[2]*qb[1] + qa[3]*qb[0]
+  };
+  res[0] = tmp[0]; res[1] = tmp[1]; res[2] = tmp[2]; res[3] = tmp[3];
+}
+
+/* :97-114 */
+static void mju_axisAngle2Quat(mjtNum res[4], const mjtNum axis[3], mjtNum angle) {
+  if (angle == 0) {
+    res[0] = 1; res[1] = 0; res[2] = 0; res[3] = 0;
+  } else {
+    mjtNum s = sin(angle*0.5);
+    res[0] = cos(angle*0.5);
+    res[1] = axis[0]*s;
+    res[2] = axis[1]*s;
+    res[3] = axis[2]*s;
+  }
+}
+
+/* :119-133 */
+static void mju_quat2Vel(mjtNum res[3], const mjtNum quat[4], mjtNum dt) {
+  mjtNum axis[3] = {quat[1], quat[2], quat[3]};
+  mjtNum sin_a_2 = mju_normalize3(axis);
+  mjtNum speed = 2 * atan2(sin_a_2, quat[0]);
+  if (speed > mjhipPI) speed -= 2*mjhipPI;
+  speed /= dt;
+  mju_scl3(res, axis, speed);
+}
+
+/* :138-146 */
+static void mju_subQuat(mjtNum res[3], const mjtNum qa[4], const mjtNum qb[4]) {
+  mjtNum qneg[4] = {qb[0], -qb[1], -qb[2], -qb[3]}, qdif[4];
+  mju_mulQuat(qdif, qneg, qa);
+  mju_quat2Vel(res, qdif, 1);
+}
+
+/* :151-187 */
+static void mju_quat2Mat(mjtNum res[9], const mjtNum quat[4]) {
+  if (quat[0] == 1 && quat[1] == 0 && quat[2] == 0 && quat[3] == 0) {
+    res[0] = 1; res[1] = 0; res[2] = 0;
+    res[3] = 0; res[4] = 1; res[5] = 0;
+    res[6] = 0; res[7] = 0; res[8] = 1;
+  } else {
+    const mjtNum q00 = quat[0]*quat[0], q01 = quat[0]*quat[1], q02 = quat[0]*quat[2];
+    const mjtNum q03 = quat[0]*quat[3], q11 = quat[1]*quat[1], q12 = quat[1]*quat[2];
+    const mjtNum q13 = quat[1]*quat[3], q22 = quat[2]*quat[2], q23 = quat[2]*quat[3];
+    const mjtNum q33 = quat[3]*quat[3];
+    res[0] = q00 + q11 - q22 - q33;
+    res[4] = q00 - q11 + q22 - q33;
+    res[8] = q00 - q11 - q22 + q33;
+    res[1] = 2*(q12 - q03);
+    res[2] = 2*(q13 + q02);
+    res[3] = 2*(q12 + q03);
+    res[5] = 2*(q23 - q01);
+    res[6] = 2*(q13 - q02);
+    res[7] = 2*(q23 + q01);
+  }
+}
+
+/* :241-250 */
+static void mju_quatIntegrate(mjtNum quat[4], const mjtNum vel[3], mjtNum scale) {
+  mjtNum angle, tmp[4], qrot[4];
+  mju_copy3(tmp, vel);
+  angle = scale * mju_normalize3(tmp);
+  mju_axisAngle2Quat(qrot, tmp, angle);
+  mju_normalize4(quat);
+  mju_mulQuat(quat, quat, qrot);
+}
+
+/* :385-396 */
+static void mju_crossMotion(mjtNum res[6], const mjtNum vel[6], const mjtNum v[6]) {
+  res[0] = -vel[2]*v[1] + vel[1]*v[2];
+  res[1] =  vel[2]*v[0] - vel[0]*v[2];
+  res[2] = -vel[1]*v[0] + vel[0]*v[1];
+  res[3] = -vel[2]*v[4] + vel[1]*v[5];
+  res[4] =  vel[2]*v[3] - vel[0]*v[5];
+  res[5] = -vel[1]*v[3] + vel[0]*v[4];
+  res[3] += -vel[5]*v[1] + vel[4]*v[2];
+  res[4] +=  vel[5]*v[0] - vel[3]*v[2];
+  res[5] += -vel[4]*v[0] + vel[3]*v[1];
+}
+
+/* :401-412 */
+static void mju_crossForce(mjtNum res[6], const mjtNum vel[6], const mjtNum f[6]) {
+  res[0] = -vel[2]*f[1] + vel[1]*f[2];
+  res[1] =  vel[2]*f[0] - vel[0]*f[2];
+  res[2] = -vel[1]*f[0] + vel[0]*f[1];
+  res[3] = -vel[2]*f[4] + vel[1]*f[5];
+  res[4] =  vel[2]*f[3] - vel[0]*f[5];
+  res[5] = -vel[1]*f[3] + vel[0]*f[4];
+  res[0] += -vel[5]*f[4] + vel[4]*f[5];
+  res[1] +=  vel[5]*f[3] - vel[3]*f[5];
+  res[2] += -vel[4]*f[3] + vel[3]*f[4];
+}
+
+/* :417-447 */
+static void mju_inertCom(mjtNum res[10], const mjtNum inert[3], const mjtNum mat[9],
+                         const mjtNum dif[3], mjtNum mass) {
+  mjtNum tmp[9] = {mat[0]*inert[0], mat[3]*inert[0], mat[6]*inert[0],
+                   mat[1]*inert[1], mat[4]*inert[1], mat[7]*inert[1],
+                   mat[2]*inert[2], mat[5]*inert[2], mat[8]*inert[2]};
+  res[0] = mat[0]*tmp[0] + mat[1]*tmp[3] + mat[2]*tmp[6];
+  res[1] = mat[3]*tmp[1] + mat[4]*tmp[4] + mat[5]*tmp[7];
+  res[2] = mat[6]*tmp[2] + mat[7]*tmp[5] + mat[8]*tmp[8];
+  res[3] = mat[0]*tmp[1] + mat[1]*tmp[4] + mat[2]*tmp[7];
+  res[4] = mat[0]*tmp[2] + mat[1]*tmp[5] + mat[2]*tmp[8];
+  res[5] = mat[3]*tmp[2] + mat[4]*tmp[5] + mat[5]*tmp[8];
+  res[0] += mass*(dif[1]*dif[1] + dif[2]*dif[2]);
+  res[1] += mass*(dif[0]*dif[0] + dif[2]*dif[2]);
+  res[2] += mass*(dif[0]*dif[0] + dif[1]*dif[1]);
+  res[3] -= mass*dif[0]*dif[1];
+  res[4] -= mass*dif[0]*dif[2];
+  res[5] -= mass*dif[1]*dif[2];
+  res[6] = mass*dif[0];
+  res[7] = mass*dif[1];
+  res[8] = mass*dif[2];
+  res[9] = mass;
+}
+
+/* :452-459 */
+static void mju_mulInertVec(mjtNum res[6], const mjtNum i[10], const mjtNum v[6]) {
+  res[0] = i[0]*v[0] + i[3]*v[1] + i[4]*v[2] - i[8]*v[4] + i[7]*v[5];
+  res[1] = i[3]*v[0] + i[1]*v[1] + i[5]*v[2] + i[8]*v[3] - i[6]*v[5];
+  res[2] = i[4]*v[0] + i[5]*v[1] + i[2]*v[2] - i[7]*v[3] + i[6]*v[4];
+  res[3] = i[8]*v[1] - i[7]*v[2] + i[9]*v[3];
+  res[4] = i[6]*v[2] - i[8]*v[0] + i[9]*v[4];
+  res[5] = i[7]*v[0] - i[6]*v[1] + i[9]*v[5];
+}
+
+/* :464-476 */
+static void mju_dofCom(mjtNum res[6], const mjtNum axis[3], const mjtNum offset[3]) {
+  if (offset) {
+    mju_copy3(res, axis);
+    mju_cross(res+3, axis, offset);
+  } else {
+    mju_zero3(res);
+    mju_copy3(res+3, axis);
+  }
+}
+
+/* :481-489 */
+static void mju_mulDofVec(mjtNum* res, const mjtNum* dof, const mjtNum* vec, int n) {
+  if (n == 1) {
+    mju_scl(res, dof, vec[0], 6);
+  } else if (n <= 0) {
+    mju_zero(res, 6);
+  } else {
+    mju_mulMatTVec(res, dof, vec, n, 6);
+  }
+}
+
+/*============================ engine_support.c ============================================*/
+
+/* :1565-1606 */
+static void mj_local2Global(mjhipData* d, mjtNum xpos[3], mjtNum xmat[9], const mjtNum pos[3],
+                            const mjtNum quat[4], int body, mjtByte sameframe) {
+  if (xpos && pos) {
+    switch (sameframe) {
+    case mjhipSAMEFRAME_NONE:
+    case mjhipSAMEFRAME_BODYROT:
+    case mjhipSAMEFRAME_INERTIAROT:
+      mju_mulMatVec3(xpos, d->xmat+9*body, pos);
+      mju_addTo3(xpos, d->xpos+3*body);
+      break;
+    case mjhipSAMEFRAME_BODY:
+      mju_copy3(xpos, d->xpos+3*body);
+      break;
+    case mjhipSAMEFRAME_INERTIA:
+      mju_copy3(xpos, d->xipos+3*body);
+      break;
+    }
+  }
+  if (xmat && quat) {
+    mjtNum tmp[4];
+    switch (sameframe) {
+    case mjhipSAMEFRAME_NONE:
+      mju_mulQuat(tmp, d->xquat+4*body, quat);
+      mju_quat2Mat(xmat, tmp);
+      break;
+    case mjhipSAMEFRAME_BODY:
+    case mjhipSAMEFRAME_BODYROT:
+      mju_copy(xmat, d->xmat+9*body, 9);
+      break;
+    case mjhipSAMEFRAME_INERTIA:
+    case mjhipSAMEFRAME_INERTIAROT:
+      mju_copy(xmat, d->ximat+9*body, 9);
+      break;
+    }
+  }
+}
+
+/* :389-441, dense */
+static void mj_jac(const mjhipModel* m, const mjhipData* d, mjtNum* jacp, mjtNum* jacr,
+                   const mjtNum point[3], int body) {
+  int nv = m->nv;
+  mjtNum offset[3];
+  if (jacp) {
+    mju_zero(jacp, 3*nv);
+    mju_sub3(offset, point, d->subtree_com+3*m->body_rootid[body]);
+  }
+  if (jacr) mju_zero(jacr, 3*nv);
+  while (body && !m->body_dofnum[body]) body = m->body_parentid[body];
+  if (!body) return;
+  int i = m->body_dofadr[body] + m->body_dofnum[body] - 1;
+  while (i >= 0) {
+    mjtNum* cdof = d->cdof+6*i;
+    if (jacr) {
+      jacr[i+0*nv] = cdof[0];
+      jacr[i+1*nv] = cdof[1];
+      jacr[i+2*nv] = cdof[2];
+    }
+    if (jacp) {
+      mjtNum tmp[3];
+      mju_cross(tmp, cdof, offset);
+      jacp[i+0*nv] = cdof[3] + tmp[0];
+      jacp[i+1*nv] = cdof[4] + tmp[1];
+      jacp[i+2*nv] = cdof[5] + tmp[2];
+    }
+    i = m->dof_parentid[i];
+  }
+}
+
+/* :1194-1251, dense case */
+static void mj_applyFT(const mjhipModel* m, mjhipData* d, const mjtNum force[3],
+                       const mjtNum torque[3], const mjtNum point[3], int body,
+                       mjtNum* qfrc_target) {
+  int nv = m->nv;
+  mjtNum* jacp = force ? (mjtNum*)malloc(3*nv*sizeof(mjtNum)) : NULL;
+  mjtNum* jacr = torque ? (mjtNum*)malloc(3*nv*sizeof(mjtNum)) : NULL;
+  mjtNum* qforce = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  mj_jac(m, d, jacp, jacr, point, body);
+  if (force) {
+    mju_mulMatTVec(qforce, jacp, force, 3, nv);
+    mju_addTo(qfrc_target, qforce, nv);
+  }
+  if (torque) {
+    mju_mulMatTVec(qforce, jacr, torque, 3, nv);
+    mju_addTo(qfrc_target, qforce, nv);
+  }
+  free(jacp); free(jacr); free(qforce);
+}
+
+/* :1254-1261 */
+void or_xfrcAccumulate(const mjhipModel* m, mjhipData* d, mjtNum* qfrc) {
+  for (int i = 1; i < m->nbody; i++) {
+    if (!mju_isZero(d->xfrc_applied+6*i, 6)) {
+      mj_applyFT(m, d, d->xfrc_applied+6*i, d->xfrc_applied+6*i+3, d->xipos+3*i, i, qfrc);
+    }
+  }
+}
+
+/* :1518-1550 */
+static void mj_integratePos(const mjhipModel* m, mjtNum* qpos, const mjtNum* qvel, mjtNum dt) {
+  for (int j = 0; j < m->njnt; j++) {
+    int padr = m->jnt_qposadr[j];
+    int vadr = m->jnt_dofadr[j];
+    switch (m->jnt_type[j]) {
+    case mjhipJNT_FREE:
+      for (int i = 0; i < 3; i++) qpos[padr+i] += dt * qvel[vadr+i];
+      padr += 3;
+      vadr += 3;
+      /* fallthrough */
+    case mjhipJNT_BALL:
+      mju_quatIntegrate(qpos+padr, qvel+vadr, dt);
+      break;
+    case mjhipJNT_HINGE:
+    case mjhipJNT_SLIDE:
+      qpos[padr] += dt * qvel[vadr];
+    }
+  }
+}
+
+/*============================ engine_core_smooth.c ========================================*/
+
+/* mj_isSparse, engine_core_constraint.c:96-103 */
+static int mj_isSparse(const mjhipModel* m) {
+  return m->opt.jacobian == mjhipJAC_SPARSE || (m->opt.jacobian == mjhipJAC_AUTO && m->nv >= 60);
+}
+
+/* :38-178 */
+void or_kinematics(const mjhipModel* m, mjhipData* d) {
+  int nbody = m->nbody, nsite = m->nsite, ngeom = m->ngeom;
+  mju_zero3(d->xpos);
+  d->xquat[0] = 1; d->xquat[1] = d->xquat[2] = d->xquat[3] = 0;
+  mju_zero3(d->xipos);
+  mju_zero(d->xmat, 9);
+  mju_zero(d->ximat, 9);
+  d->xmat[0] = d->xmat[4] = d->xmat[8] = 1;
+  d->ximat[0] = d->ximat[4] = d->ximat[8] = 1;
+
+  for (int i = 1; i < nbody; i++) {
+    mjtNum xpos[3], xquat[4];
+    int jntadr = m->body_jntadr[i];
+    int jntnum = m->body_jntnum[i];
+
+    if (jntnum == 1 && m->jnt_type[jntadr] == mjhipJNT_FREE) {
+      int qadr = m->jnt_qposadr[jntadr];
+      mju_copy3(xpos, d->qpos+qadr);
+      mju_copy4(xquat, d->qpos+qadr+3);
+      mju_normalize4(xquat);
+      mju_copy3(d->xanchor+3*jntadr, xpos);
+      mju_copy3(d->xaxis+3*jntadr, m->jnt_axis+3*jntadr);
+    } else {
+      int pid = m->body_parentid[i];
+      mjtNum* bodypos = m->body_pos+3*i;
+      mjtNum* bodyquat = m->body_quat+4*i;   /* no mocap bodies in the supported subset */
+      if (pid) {
+        mju_mulMatVec3(xpos, d->xmat+9*pid, bodypos);
+        mju_addTo3(xpos, d->xpos+3*pid);
+        mju_mulQuat(xquat, d->xquat+4*pid, bodyquat);
+      } else {
+        mju_copy3(xpos, bodypos);
+        mju_copy4(xquat, bodyquat);
+      }
+      mjtNum xanchor[3], xaxis[3];
+      for (int j = 0; j < jntnum; j++) {
+        int jid = jntadr + j;
+        int qadr = m->jnt_qposadr[jid];
+        int jtype = m->jnt_type[jid];
+        mju_rotVecQuat(xaxis, m->jnt_axis+3*jid, xquat);
+        mju_rotVecQuat(xanchor, m->jnt_pos+3*jid, xquat);
+        mju_addTo3(xanchor, xpos);
+        switch (jtype) {
+        case mjhipJNT_SLIDE:
+          mju_addToScl3(xpos, xaxis, d->qpos[qadr] - m->qpos0[qadr]);
+          break;
+        case mjhipJNT_BALL:
+        case mjhipJNT_HINGE:
+          {
+            mjtNum qloc[4];
+            if (jtype == mjhipJNT_BALL) {
+              mju_copy4(qloc, d->qpos+qadr);
+              mju_normalize4(qloc);
+            } else {
+              mju_axisAngle2Quat(qloc, m->jnt_axis+3*jid, d->qpos[qadr] - m->qpos0[qadr]);
+            }
+            mju_mulQuat(xquat, xquat, qloc);
+            mjtNum vec[3];
+            mju_rotVecQuat(vec, m->jnt_pos+3*jid, xquat);
+            mju_sub3(xpos, xanchor, vec);
+          }
+          break;
+        }
+        mju_copy3(d->xanchor+3*jid, xanchor);
+        mju_copy3(d->xaxis+3*jid, xaxis);
+      }
+    }
+    mju_normalize4(xquat);
+    mju_copy4(d->xquat+4*i, xquat);
+    mju_copy3(d->xpos+3*i, xpos);
+    mju_quat2Mat(d->xmat+9*i, xquat);
+  }
+
+  for (int i = 1; i < nbody; i++) {
+    mj_local2Global(d, d->xipos+3*i, d->ximat+9*i, m->body_ipos+3*i, m->body_iquat+4*i,
+                    i, m->body_sameframe[i]);
+  }
+  for (int i = 0; i < ngeom; i++) {
+    mj_local2Global(d, d->geom_xpos+3*i, d->geom_xmat+9*i, m->geom_pos+3*i,
+                    m->geom_quat+4*i, m->geom_bodyid[i], m->geom_sameframe[i]);
+  }
+  for (int i = 0; i < nsite; i++) {
+    mj_local2Global(d, d->site_xpos+3*i, d->site_xmat+9*i, m->site_pos+3*i,
+                    m->site_quat+4*i, m->site_bodyid[i], m->site_sameframe[i]);
+  }
+}
+
+/* :183-270 */
+void or_comPos(const mjhipModel* m, mjhipData* d) {
+  int nbody = m->nbody, njnt = m->njnt;
+  mjtNum offset[3], axis[3];
+  mjtNum* mass_subtree = (mjtNum*)calloc(nbody, sizeof(mjtNum));
+  mju_zero(d->subtree_com, nbody*3);
+  for (int i = nbody-1; i >= 0; i--) {
+    mju_addToScl3(d->subtree_com+3*i, d->xipos+3*i, m->body_mass[i]);
+    mass_subtree[i] += m->body_mass[i];
+    if (i) {
+      int j = m->body_parentid[i];
+      mju_addTo3(d->subtree_com+3*j, d->subtree_com+3*i);
+      mass_subtree[j] += mass_subtree[i];
+    }
+    if (mass_subtree[i] < mjMINVAL) {
+      mju_copy3(d->subtree_com+3*i, d->xipos+3*i);
+    } else {
+      mju_scl3(d->subtree_com+3*i, d->subtree_com+3*i, 1.0/mjMAX(mjMINVAL, mass_subtree[i]));
+    }
+  }
+  mju_zero(d->cinert, 10);
+  for (int i = 1; i < nbody; i++) {
+    mju_sub3(offset, d->xipos+3*i, d->subtree_com+3*m->body_rootid[i]);
+    mju_inertCom(d->cinert+10*i, m->body_inertia+3*i, d->ximat+9*i, offset, m->body_mass[i]);
+  }
+  for (int j = 0; j < njnt; j++) {
+    int da = 6*m->jnt_dofadr[j];
+    int bi = m->jnt_bodyid[j];
+    mju_sub3(offset, d->subtree_com+3*m->body_rootid[bi], d->xanchor+3*j);
+    int skip = 0;
+    switch (m->jnt_type[j]) {
+    case mjhipJNT_FREE:
+      mju_zero(d->cdof+da, 18);
+      for (int i = 0; i < 3; i++) d->cdof[da+3+7*i] = 1;
+      skip = 18;
+      /* fallthrough */
+    case mjhipJNT_BALL:
+      for (int i = 0; i < 3; i++) {
+        axis[0] = d->xmat[9*bi+i+0];
+        axis[1] = d->xmat[9*bi+i+3];
+        axis[2] = d->xmat[9*bi+i+6];
+        mju_dofCom(d->cdof+da+skip+6*i, axis, offset);
+      }
+      break;
+    case mjhipJNT_SLIDE:
+      mju_dofCom(d->cdof+da, d->xaxis+3*j, 0);
+      break;
+    case mjhipJNT_HINGE:
+      mju_dofCom(d->cdof+da, d->xaxis+3*j, offset);
+      break;
+    }
+  }
+  free(mass_subtree);
+}
+
+/* :275-392 */
+static void or_camlight(const mjhipModel* m, mjhipData* d) {
+  mjtNum pos[3], matT[9];
+  for (int i = 0; i < m->ncam; i++) {
+    mj_local2Global(d, d->cam_xpos+3*i, d->cam_xmat+9*i, m->cam_pos+3*i, m->cam_quat+4*i,
+                    m->cam_bodyid[i], 0);
+    int id = m->cam_bodyid[i];
+    int id1 = m->cam_targetbodyid[i];
+    switch (m->cam_mode[i]) {
+    case mjhipCAMLIGHT_FIXED:
+      break;
+    case mjhipCAMLIGHT_TRACK:
+    case mjhipCAMLIGHT_TRACKCOM:
+      mju_copy(d->cam_xmat+9*i, m->cam_mat0+9*i, 9);
+      if (m->cam_mode[i] == mjhipCAMLIGHT_TRACK) {
+        mju_add3(d->cam_xpos+3*i, d->xpos+3*id, m->cam_pos0+3*i);
+      } else {
+        mju_add3(d->cam_xpos+3*i, d->subtree_com+3*id, m->cam_poscom0+3*i);
+      }
+      break;
+    case mjhipCAMLIGHT_TARGETBODY:
+    case mjhipCAMLIGHT_TARGETBODYCOM:
+      if (id1 >= 0) {
+        if (m->cam_mode[i] == mjhipCAMLIGHT_TARGETBODY) {
+          mju_copy3(pos, d->xpos+3*id1);
+        } else {
+          mju_copy3(pos, d->subtree_com+3*id1);
+        }
+        mju_sub3(matT+6, d->cam_xpos+3*i, pos);
+        mju_normalize3(matT+6);
+        matT[3] = 0; matT[4] = 0; matT[5] = 1;
+        mju_cross(matT, matT+3, matT+6);
+        mju_normalize3(matT);
+        mju_cross(matT+3, matT+6, matT);
+        mju_normalize3(matT+3);
+        /* mju_transpose(cam_xmat, matT, 3, 3) */
+        for (int r = 0; r < 3; r++)
+          for (int c = 0; c < 3; c++) d->cam_xmat[9*i + 3*c + r] = matT[3*r + c];
+      }
+    }
+  }
+  for (int i = 0; i < m->nlight; i++) {
+    mj_local2Global(d, d->light_xpos+3*i, 0, m->light_pos+3*i, 0, m->light_bodyid[i], 0);
+    mju_rotVecQuat(d->light_xdir+3*i, m->light_dir+3*i, d->xquat+4*m->light_bodyid[i]);
+    int id = m->light_bodyid[i];
+    int id1 = m->light_targetbodyid[i];
+    switch (m->light_mode[i]) {
+    case mjhipCAMLIGHT_FIXED:
+      break;
+    case mjhipCAMLIGHT_TRACK:
+    case mjhipCAMLIGHT_TRACKCOM:
+      mju_copy3(d->light_xdir+3*i, m->light_dir0+3*i);
+      if (m->light_mode[i] == mjhipCAMLIGHT_TRACK) {
+        mju_add3(d->light_xpos+3*i, d->xpos+3*id, m->light_pos0+3*i);
+      } else {
+        mju_add3(d->light_xpos+3*i, d->subtree_com+3*id, m->light_poscom0+3*i);
+      }
+      break;
+    case mjhipCAMLIGHT_TARGETBODY:
+    case mjhipCAMLIGHT_TARGETBODYCOM:
+      if (id1 >= 0) {
+        if (m->light_mode[i] == mjhipCAMLIGHT_TARGETBODY) {
+          mju_copy3(pos, d->xpos+3*id1);
+        } else {
+          mju_copy3(pos, d->subtree_com+3*id1);
+        }
+        mju_sub3(d->light_xdir+3*i, pos, d->light_xpos+3*i);
+      }
+    }
+    mju_normalize3(d->light_xdir+3*i);
+  }
+}
+
+/* :651-723, fixed tendons, dense Jacobian */
+static void or_tendon(const mjhipModel* m, mjhipData* d) {
+  int nv = m->nv, nten = m->ntendon;
+  mjtNum *L = d->ten_length, *J = d->ten_J;
+  if (!nten) return;
+  mju_zero(L, nten);
+  mju_zero(J, nten*nv);
+  for (int i = 0; i < nten; i++) {
+    int adr = m->tendon_adr[i];
+    int tendon_num = m->tendon_num[i];
+    if (m->wrap_type[adr] == mjhipWRAP_JOINT) {
+      for (int j = 0; j < tendon_num; j++) {
+        int k = m->wrap_objid[adr+j];
+        L[i] += m->wrap_prm[adr+j] * d->qpos[m->jnt_qposadr[k]];
+        J[i*nv + m->jnt_dofadr[k]] = m->wrap_prm[adr+j];
+      }
+    }
+  }
+}
+
+/* :865-916, joint transmission (slide/hinge) */
+static void or_transmission(const mjhipModel* m, mjhipData* d) {
+  int nu = m->nu;
+  int* rowadr = m->moment_rowadr;
+  for (int i = 0; i < nu; i++) {
+    int adr = rowadr[i];
+    int id = m->actuator_trnid[2*i];
+    mjtNum* gear = m->actuator_gear+6*i;
+    d->actuator_length[i] = d->qpos[m->jnt_qposadr[id]]*gear[0];
+    d->actuator_moment[adr] = gear[0];
+  }
+}
+
+/* :1353-1401 */
+void or_crb(const mjhipModel* m, mjhipData* d) {
+  mjtNum buf[6];
+  mjtNum* crb = d->crb;
+  int last_body = m->nbody - 1, nv = m->nv;
+  mju_copy(crb, d->cinert, 10*m->nbody);
+  for (int i = last_body; i > 0; i--) {
+    if (m->body_parentid[i] > 0) mju_addTo(crb+10*m->body_parentid[i], crb+10*i, 10);
+  }
+  mju_zero(d->qM, m->nM);
+  for (int i = 0; i < nv; i++) {
+    if (m->dof_simplenum[i]) {
+      int n = i + m->dof_simplenum[i];
+      for (; i < n; i++) d->qM[m->dof_Madr[i]] = m->dof_M0[i];
+      if (i == nv) break;
+    }
+    int Madr_ij = m->dof_Madr[i];
+    d->qM[Madr_ij] = m->dof_armature[i];
+    mju_mulInertVec(buf, crb+10*m->dof_bodyid[i], d->cdof+6*i);
+    for (int j = i; j >= 0; j = m->dof_parentid[j]) {
+      d->qM[Madr_ij++] += mju_dot(d->cdof+6*j, buf, 6);
+    }
+  }
+}
+
+/* :1483-1511 */
+static void mj_factorI(mjtNum* mat, mjtNum* diaginv, int nv, const int* rownnz,
+                       const int* rowadr, const int* diagnum, const int* colind) {
+  for (int k = nv-1; k >= 0; k--) {
+    int rowadr_k = rowadr[k];
+    int diag_k = rowadr_k + rownnz[k] - 1;
+    mjtNum invD = 1 / mat[diag_k];
+    if (diaginv) diaginv[k] = invD;
+    if (diagnum[k]) continue;
+    for (int adr = diag_k - 1; adr >= rowadr_k; adr--) {
+      mjtNum tmp = mat[adr] * invD;
+      int i = colind[adr];
+      mju_addToScl(mat + rowadr[i], mat + rowadr_k, -tmp, rownnz[i]);
+      mat[adr] = tmp;
+    }
+  }
+}
+
+/* :1470-1478 */
+void or_factorM(const mjhipModel* m, mjhipData* d) {
+  for (int i = 0; i < m->nC; i++) d->qLD[i] = d->qM[m->mapM2C[i]];
+  mj_factorI(d->qLD, d->qLDiagInv, m->nv, m->C_rownnz, m->C_rowadr, m->dof_simplenum,
+             m->C_colind);
+}
+
+/* :1629-1707 */
+static void mj_solveLD(mjtNum* x, const mjtNum* qLDs, const mjtNum* qLDiagInv, int nv, int n,
+                       const int* rownnz, const int* rowadr, const int* diagnum,
+                       const int* colind) {
+  for (int i = nv-1; i > 0; i--) {
+    if (diagnum[i]) continue;
+    int start = rowadr[i];
+    int end = start + rownnz[i] - 1;
+    for (int offset = 0; offset < n*nv; offset += nv) {
+      mjtNum x_i;
+      if ((x_i = x[i+offset])) {
+        for (int adr = start; adr < end; adr++) x[offset + colind[adr]] -= qLDs[adr] * x_i;
+      }
+    }
+  }
+  for (int i = 0; i < nv; i++) {
+    mjtNum invD_i = qLDiagInv[i];
+    for (int offset = 0; offset < n*nv; offset += nv) x[i+offset] *= invD_i;
+  }
+  for (int i = 1; i < nv; i++) {
+    if (diagnum[i]) {
+      i += diagnum[i] - 1;
+      continue;
+    }
+    int dd;
+    if ((dd = rownnz[i] - 1) > 0) {
+      int adr = rowadr[i];
+      for (int offset = 0; offset < n*nv; offset += nv) {
+        x[i+offset] -= mju_dotSparse(qLDs+adr, x+offset, dd, colind+adr);
+      }
+    }
+  }
+}
+
+/* :1713-1719 */
+void or_solveM(const mjhipModel* m, const mjhipData* d, mjtNum* x, const mjtNum* y, int n) {
+  if (x != y) mju_copy(x, y, n*m->nv);
+  mj_solveLD(x, d->qLD, d->qLDiagInv, m->nv, n, m->C_rownnz, m->C_rowadr, m->dof_simplenum,
+             m->C_colind);
+}
+
+/* mj_fullM, engine_support.c (dense symmetric M from qM) */
+void or_fullM(const mjhipModel* m, mjtNum* dst, const mjtNum* M) {
+  int nv = m->nv, adr = 0;
+  mju_zero(dst, nv*nv);
+  for (int i = 0; i < nv; i++) {
+    int j = i;
+    while (j >= 0) {
+      dst[i*nv+j] = M[adr];
+      dst[j*nv+i] = M[adr];
+      j = m->dof_parentid[j];
+      adr++;
+    }
+  }
+}
+
+/* :1833-1896 */
+static void or_comVel(const mjhipModel* m, mjhipData* d) {
+  int nbody = m->nbody;
+  mju_zero(d->cvel, 6);
+  for (int i = 1; i < nbody; i++) {
+    int bda = m->body_dofadr[i];
+    mjtNum cvel[6];
+    mju_copy(cvel, d->cvel + 6*m->body_parentid[i], 6);
+    int dofnum = m->body_dofnum[i];
+    mjtNum cdofdot[36];
+    for (int j = 0; j < dofnum; j++) {
+      mjtNum tmp[6];
+      switch (m->jnt_type[m->dof_jntid[bda + j]]) {
+      case mjhipJNT_FREE:
+        mju_zero(cdofdot, 18);
+        mju_mulDofVec(tmp, d->cdof + 6*bda, d->qvel + bda, 3);
+        mju_addTo(cvel, tmp, 6);
+        j += 3;
+        /* fallthrough */
+      case mjhipJNT_BALL:
+        for (int k = 0; k < 3; k++) {
+          mju_crossMotion(cdofdot + 6*(j + k), cvel, d->cdof + 6*(bda + j + k));
+        }
+        mju_mulDofVec(tmp, d->cdof + 6*(bda + j), d->qvel + bda + j, 3);
+        mju_addTo(cvel, tmp, 6);
+        j += 2;
+        break;
+      default:
+        mju_crossMotion(cdofdot + 6*j, cvel, d->cdof + 6*(bda + j));
+        mju_mulDofVec(tmp, d->cdof + 6*(bda + j), d->qvel + bda + j, 1);
+        mju_addTo(cvel, tmp, 6);
+      }
+    }
+    mju_copy(d->cvel + 6*i, cvel, 6);
+    if (dofnum) mju_copy(d->cdof_dot + 6*bda, cdofdot, 6*dofnum);
+  }
+}
+
+/* :1969-2023 */
+void or_rne(const mjhipModel* m, mjhipData* d, int flg_acc, mjtNum* result) {
+  int nbody = m->nbody, nv = m->nv;
+  mjtNum tmp[6], tmp1[6];
+  mjtNum* loc_cacc = (mjtNum*)malloc(nbody*6*sizeof(mjtNum));
+  mjtNum* loc_cfrc_body = (mjtNum*)malloc(nbody*6*sizeof(mjtNum));
+  mju_zero(loc_cacc, 6);
+  if (!mjDISABLED(mjhipDSBL_GRAVITY)) mju_scl3(loc_cacc + 3, m->opt.gravity, -1);
+  for (int i = 1; i < nbody; i++) {
+    int bda = m->body_dofadr[i];
+    mju_mulDofVec(tmp, d->cdof_dot + 6*bda, d->qvel + bda, m->body_dofnum[i]);
+    mju_add(loc_cacc + 6*i, loc_cacc + 6*m->body_parentid[i], tmp, 6);
+    if (flg_acc) {
+      mju_mulDofVec(tmp, d->cdof + 6*bda, d->qacc + bda, m->body_dofnum[i]);
+      mju_addTo(loc_cacc + 6*i, tmp, 6);
+    }
+    mju_mulInertVec(loc_cfrc_body + 6*i, d->cinert + 10*i, loc_cacc + 6*i);
+    mju_mulInertVec(tmp, d->cinert + 10*i, d->cvel + 6*i);
+    mju_crossForce(tmp1, d->cvel + 6*i, tmp);
+    mju_addTo(loc_cfrc_body + 6*i, tmp1, 6);
+  }
+  mju_zero(loc_cfrc_body, 6);
+  for (int i = nbody - 1; i > 0; i--) {
+    if (m->body_parentid[i]) {
+      mju_addTo(loc_cfrc_body + 6*m->body_parentid[i], loc_cfrc_body + 6*i, 6);
+    }
+  }
+  for (int i = 0; i < nv; i++) {
+    result[i] = mju_dot(d->cdof + 6*i, loc_cfrc_body + 6*m->dof_bodyid[i], 6);
+  }
+  free(loc_cacc);
+  free(loc_cfrc_body);
+}
+
+/*============================ engine_passive.c ============================================*/
+
+/* :57-378 (joint springs, dof dampers, dense tendon spring-dampers) */
+static void or_springdamper(const mjhipModel* m, mjhipData* d) {
+  int nv = m->nv, njnt = m->njnt, ntendon = m->ntendon;
+  for (int i = 0; i < njnt; i++) {
+    mjtNum stiffness = m->jnt_stiffness[i];
+    if (stiffness == 0) continue;
+    int padr = m->jnt_qposadr[i];
+    int dadr = m->jnt_dofadr[i];
+    switch (m->jnt_type[i]) {
+    case mjhipJNT_FREE:
+      d->qfrc_spring[dadr+0] = -stiffness*(d->qpos[padr+0] - m->qpos_spring[padr+0]);
+      d->qfrc_spring[dadr+1] = -stiffness*(d->qpos[padr+1] - m->qpos_spring[padr+1]);
+      d->qfrc_spring[dadr+2] = -stiffness*(d->qpos[padr+2] - m->qpos_spring[padr+2]);
+      dadr += 3;
+      padr += 3;
+      /* fallthrough */
+    case mjhipJNT_BALL:
+      {
+        mjtNum dif[3], quat[4];
+        mju_copy4(quat, d->qpos+padr);
+        mju_normalize4(quat);
+        mju_subQuat(dif, quat, m->qpos_spring + padr);
+        d->qfrc_spring[dadr+0] = -stiffness*dif[0];
+        d->qfrc_spring[dadr+1] = -stiffness*dif[1];
+        d->qfrc_spring[dadr+2] = -stiffness*dif[2];
+      }
+      break;
+    case mjhipJNT_SLIDE:
+    case mjhipJNT_HINGE:
+      d->qfrc_spring[dadr] = -stiffness*(d->qpos[padr] - m->qpos_spring[padr]);
+      break;
+    }
+  }
+  for (int i = 0; i < nv; i++) {
+    mjtNum damping = m->dof_damping[i];
+    if (damping != 0) d->qfrc_damper[i] = -damping*d->qvel[i];
+  }
+  for (int i = 0; i < ntendon; i++) {
+    mjtNum stiffness = m->tendon_stiffness[i];
+    mjtNum damping = m->tendon_damping[i];
+    if (stiffness == 0 && damping == 0) continue;
+    mjtNum length = d->ten_length[i];
+    mjtNum lower = m->tendon_lengthspring[2*i];
+    mjtNum upper = m->tendon_lengthspring[2*i+1];
+    mjtNum frc_spring = 0;
+    if (length > upper) {
+      frc_spring = stiffness * (upper - length);
+    } else if (length < lower) {
+      frc_spring = stiffness * (lower - length);
+    }
+    mjtNum frc_damper = -damping * d->ten_velocity[i];
+    if (frc_spring) mju_addToScl(d->qfrc_spring, d->ten_J+i*nv, frc_spring, nv);
+    if (frc_damper) mju_addToScl(d->qfrc_damper, d->ten_J+i*nv, frc_damper, nv);
+  }
+}
+
+/* :381-399 */
+static int or_gravcomp(const mjhipModel* m, mjhipData* d) {
+  if (!m->ngravcomp || mjDISABLED(mjhipDSBL_GRAVITY) ||
+      sqrt(m->opt.gravity[0]*m->opt.gravity[0] + m->opt.gravity[1]*m->opt.gravity[1] +
+           m->opt.gravity[2]*m->opt.gravity[2]) == 0) {
+    return 0;
+  }
+  int has_gravcomp = 0;
+  mjtNum force[3], torque[3] = {0};
+  for (int i = 1; i < m->nbody; i++) {
+    if (m->body_gravcomp[i]) {
+      has_gravcomp = 1;
+      mju_scl3(force, m->opt.gravity, -(m->body_mass[i]*m->body_gravcomp[i]));
+      mj_applyFT(m, d, force, torque, d->xipos+3*i, i, d->qfrc_gravcomp);
+    }
+  }
+  return has_gravcomp;
+}
+
+/* :436-493 (fluid forces need density/viscosity > 0: not in the supported subset) */
+static void or_passive(const mjhipModel* m, mjhipData* d) {
+  int nv = m->nv;
+  mju_zero(d->qfrc_spring, nv);
+  mju_zero(d->qfrc_damper, nv);
+  mju_zero(d->qfrc_gravcomp, nv);
+  mju_zero(d->qfrc_fluid, nv);
+  mju_zero(d->qfrc_passive, nv);
+  if (mjDISABLED(mjhipDSBL_PASSIVE)) return;
+  or_springdamper(m, d);
+  int has_gravcomp = or_gravcomp(m, d);
+  mju_add(d->qfrc_passive, d->qfrc_spring, d->qfrc_damper, nv);
+  if (has_gravcomp) {
+    for (int i = 0; i < m->njnt; i++) {
+      if (m->jnt_actgravcomp[i]) continue;
+      int dofnum = m->jnt_type[i] == mjhipJNT_FREE ? 6 : (m->jnt_type[i] == mjhipJNT_BALL ? 3 : 1);
+      int dofadr = m->jnt_dofadr[i];
+      for (int j = 0; j < dofnum; j++) d->qfrc_passive[dofadr+j] += d->qfrc_gravcomp[dofadr+j];
+    }
+  }
+}
+
+/*============================ engine_core_constraint.c ====================================*/
+
+int or_efcCapacity(const mjhipModel* m) {
+  int n = 0;
+  for (int i = 0; i < m->njnt; i++) {
+    if (m->jnt_limited[i]) n += (m->jnt_type[i] == mjhipJNT_BALL) ? 1 : 2;
+  }
+  for (int i = 0; i < m->ntendon; i++) {
+    if (m->tendon_limited[i]) n += 2;
+  }
+  for (int i = 0; i < m->nv; i++) {
+    if (m->dof_frictionloss[i] > 0) n += 1;
+  }
+  return n;
+}
+
+/* :265-356, dense Jacobian branch */
+static void mj_addConstraint(const mjhipModel* m, orEfc* e, const mjtNum* jac, const mjtNum* pos,
+                             const mjtNum* margin, mjtNum frictionloss, int size, int type,
+                             int id) {
+  int empty = 1, nv = m->nv, nefc = e->nefc;
+  for (int i = 0; i < size*nv; i++) {
+    if (jac[i]) {
+      empty = 0;
+      break;
+    }
+  }
+  if (empty) return;
+  mju_copy(e->efc_J + nefc*nv, jac, size*nv);
+  for (int i = 0; i < size; i++) {
+    e->efc_pos[nefc+i] = (pos ? pos[i] : 0);
+    e->efc_margin[nefc+i] = (margin ? margin[i] : 0);
+    e->efc_frictionloss[nefc+i] = frictionloss;
+    e->efc_type[nefc+i] = type;
+    e->efc_id[nefc+i] = id;
+  }
+  e->nefc += size;
+  if (type == orCNSTR_FRICTION_DOF || type == orCNSTR_FRICTION_TENDON) {
+    e->nf += size;
+  } else if (type == orCNSTR_LIMIT_JOINT || type == orCNSTR_LIMIT_TENDON) {
+    e->nl += size;
+  }
+}
+
+/* mj_instantiateFriction :768-822, dof friction (dense) */
+static void or_instantiateFriction(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum* jac) {
+  int nv = m->nv;
+  (void)d;
+  if (mjDISABLED(mjhipDSBL_FRICTIONLOSS)) return;
+  for (int i = 0; i < nv; i++) {
+    if (m->dof_frictionloss[i] > 0) {
+      mju_zero(jac, nv);
+      jac[i] = 1;
+      mj_addConstraint(m, e, jac, 0, 0, m->dof_frictionloss[i], 1, orCNSTR_FRICTION_DOF, i);
+    }
+  }
+}
+
+/* :824-959, dense */
+static void or_instantiateLimit(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum* jac) {
+  int side, nv = m->nv;
+  mjtNum margin, value, dist, angleAxis[3];
+  if (mjDISABLED(mjhipDSBL_LIMIT)) return;
+  for (int i = 0; i < m->njnt; i++) {
+    if (m->jnt_limited[i]) {
+      margin = m->jnt_margin[i];
+      if (m->jnt_type[i] == mjhipJNT_SLIDE || m->jnt_type[i] == mjhipJNT_HINGE) {
+        value = d->qpos[m->jnt_qposadr[i]];
+        for (side = -1; side <= 1; side += 2) {
+          dist = side * (m->jnt_range[2*i+(side+1)/2] - value);
+          if (dist < margin) {
+            mju_zero(jac, nv);
+            jac[m->jnt_dofadr[i]] = -(mjtNum)side;
+            mj_addConstraint(m, e, jac, &dist, &margin, 0, 1, orCNSTR_LIMIT_JOINT, i);
+          }
+        }
+      } else if (m->jnt_type[i] == mjhipJNT_BALL) {
+        int adr = m->jnt_qposadr[i];
+        mjtNum quat[4] = {d->qpos[adr], d->qpos[adr+1], d->qpos[adr+2], d->qpos[adr+3]};
+        mju_normalize4(quat);
+        mju_quat2Vel(angleAxis, quat, 1);
+        value = mju_normalize3(angleAxis);
+        dist = mjMAX(m->jnt_range[2*i], m->jnt_range[2*i+1]) - value;
+        if (dist < margin) {
+          mju_zero(jac, nv);
+          mju_scl3(jac + m->jnt_dofadr[i], angleAxis, -1);
+          mj_addConstraint(m, e, jac, &dist, &margin, 0, 1, orCNSTR_LIMIT_JOINT, i);
+        }
+      }
+    }
+  }
+  for (int i = 0; i < m->ntendon; i++) {
+    if (m->tendon_limited[i]) {
+      value = d->ten_length[i];
+      margin = m->tendon_margin[i];
+      for (side = -1; side <= 1; side += 2) {
+        dist = side * (m->tendon_range[2*i+(side+1)/2] - value);
+        if (dist < margin) {
+          mju_scl(jac, d->ten_J+i*nv, -side, nv);
+          mj_addConstraint(m, e, jac, &dist, &margin, 0, 1, orCNSTR_LIMIT_TENDON, i);
+        }
+      }
+    }
+  }
+}
+
+/* :1138-1311 (limit and friction rows) */
+static void or_diagApprox(const mjhipModel* m, orEfc* e) {
+  for (int i = 0; i < e->nefc; i++) {
+    int id = e->efc_id[i];
+    switch (e->efc_type[i]) {
+    case orCNSTR_FRICTION_DOF:
+      e->efc_diagApprox[i] = m->dof_invweight0[id];
+      break;
+    case orCNSTR_LIMIT_JOINT:
+      e->efc_diagApprox[i] = m->dof_invweight0[m->jnt_dofadr[id]];
+      break;
+    case orCNSTR_LIMIT_TENDON:
+      e->efc_diagApprox[i] = m->tendon_invweight0[id];
+      break;
+    }
+  }
+}
+
+/* :1316-1371 (limit and friction rows; solreffriction only applies to contacts) */
+static void getsolparam(const mjhipModel* m, const orEfc* e, int i, mjtNum* solref,
+                        mjtNum* solimp) {
+  int id = e->efc_id[i];
+  switch (e->efc_type[i]) {
+  case orCNSTR_LIMIT_JOINT:
+    mju_copy(solref, m->jnt_solref+2*id, 2);
+    mju_copy(solimp, m->jnt_solimp+5*id, 5);
+    break;
+  case orCNSTR_FRICTION_DOF:
+    mju_copy(solref, m->dof_solref+2*id, 2);
+    mju_copy(solimp, m->dof_solimp+5*id, 5);
+    break;
+  case orCNSTR_LIMIT_TENDON:
+    mju_copy(solref, m->tendon_solref_lim+2*id, 2);
+    mju_copy(solimp, m->tendon_solimp_lim+5*id, 5);
+    break;
+  }
+  if ((solref[0] > 0) ^ (solref[1] > 0)) {   /* mixed format: default (0.02, 1) */
+    solref[0] = 0.02;
+    solref[1] = 1;
+  }
+  if (!mjDISABLED(mjhipDSBL_REFSAFE) && solref[0] > 0) {
+    solref[0] = mjMAX(solref[0], 2*m->opt.timestep);
+  }
+  solimp[0] = mjMIN(mjhipMAXIMP, mjMAX(mjhipMINIMP, solimp[0]));
+  solimp[1] = mjMIN(mjhipMAXIMP, mjMAX(mjhipMINIMP, solimp[1]));
+  solimp[2] = mjMAX(0, solimp[2]);
+  solimp[3] = mjMIN(mjhipMAXIMP, mjMAX(mjhipMINIMP, solimp[3]));
+  solimp[4] = mjMAX(1, solimp[4]);
+}
+
+/* :1413-1421 */
+static mjtNum power(mjtNum a, mjtNum b) {
+  if (b == 1) return a;
+  else if (b == 2) return a*a;
+  return pow(a, b);
+}
+
+/* :1425-1480 */
+static void getimpedance(const mjtNum* solimp, mjtNum pos, mjtNum margin, mjtNum* imp,
+                         mjtNum* impP) {
+  if (solimp[0] == solimp[1] || solimp[2] <= mjMINVAL) {
+    *imp = 0.5*(solimp[0] + solimp[1]);
+    *impP = 0;
+    return;
+  }
+  mjtNum x = (pos-margin) / solimp[2];
+  mjtNum sgn = 1;
+  if (x < 0) {
+    x = -x;
+    sgn = -1;
+  }
+  if (x >= 1 || x <= 0) {
+    *imp = (x >= 1 ? solimp[1] : solimp[0]);
+    *impP = 0;
+    return;
+  }
+  mjtNum y, yP;
+  if (solimp[4] == 1) {
+    y = x;
+    yP = 1;
+  } else if (x <= solimp[3]) {
+    mjtNum a = 1/power(solimp[3], solimp[4]-1);
+    y = a*power(x, solimp[4]);
+    yP = solimp[4] * a*power(x, solimp[4]-1);
+  } else {
+    mjtNum b = 1/power(1-solimp[3], solimp[4]-1);
+    y = 1-b*power(1-x, solimp[4]);
+    yP = solimp[4] * b*power(1-x, solimp[4]-1);
+  }
+  *imp = solimp[0] + y*(solimp[1]-solimp[0]);
+  *impP = yP * sgn * (solimp[1]-solimp[0]) / solimp[2];
+}
+
+/* :1494-1608 (dim = 1 rows: limits and friction) */
+static void or_makeImpedance(const mjhipModel* m, orEfc* e) {
+  int nefc = e->nefc;
+  mjtNum *R = e->efc_R, *KBIP = e->efc_KBIP;
+  mjtNum imp, impP, solref[2], solimp[5];
+  for (int i = 0; i < nefc; i++) {
+    getsolparam(m, e, i, solref, solimp);
+    mjtNum pos = e->efc_pos[i];
+    getimpedance(solimp, pos, e->efc_margin[i], &imp, &impP);
+    R[i] = mjMAX(mjMINVAL, (1-imp)*e->efc_diagApprox[i]/imp);
+    int tp = e->efc_type[i];
+    mjtNum* ref = solref;
+    if (tp == orCNSTR_FRICTION_DOF || tp == orCNSTR_FRICTION_TENDON) {
+      KBIP[4*i] = 0;
+    } else if (ref[0] > 0) {
+      KBIP[4*i] = 1 / mjMAX(mjMINVAL, solimp[1]*solimp[1] * ref[0]*ref[0] * ref[1]*ref[1]);
+    } else {
+      KBIP[4*i] = -ref[0] / mjMAX(mjMINVAL, solimp[1]*solimp[1]);
+    }
+    if (ref[1] > 0) {
+      KBIP[4*i+1] = 2 / mjMAX(mjMINVAL, solimp[1]*ref[0]);
+    } else {
+      KBIP[4*i+1] = -ref[1] / mjMAX(mjMINVAL, solimp[1]);
+    }
+    KBIP[4*i+2] = imp;
+    KBIP[4*i+3] = impP;
+  }
+  for (int i = 0; i < nefc; i++) e->efc_D[i] = 1 / R[i];
+  for (int i = 0; i < nefc; i++) {
+    e->efc_diagApprox[i] = R[i] * KBIP[4*i+2] / (1-KBIP[4*i+2]);
+  }
+}
+
+/* :2005-2116 (dense; equality and contacts are outside the supported subset) */
+static void or_makeConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  e->ne = e->nf = e->nl = e->nefc = 0;
+  if (mjDISABLED(mjhipDSBL_CONSTRAINT)) return;
+  mjtNum* jac = (mjtNum*)malloc((m->nv > 0 ? m->nv : 1)*sizeof(mjtNum));
+  or_instantiateFriction(m, d, e, jac);
+  or_instantiateLimit(m, d, e, jac);
+  free(jac);
+  if (!e->nefc) return;
+  or_diagApprox(m, e);
+  or_makeImpedance(m, e);
+}
+
+/* :2362-2375 */
+static void or_referenceConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  int nefc = e->nefc;
+  mjtNum* KBIP = e->efc_KBIP;
+  if (nefc) mju_mulMatVec(e->efc_vel, e->efc_J, d->qvel, nefc, m->nv);
+  for (int i = 0; i < nefc; i++) {
+    e->efc_aref[i] = -KBIP[4*i+1]*e->efc_vel[i]
+                     -KBIP[4*i]*KBIP[4*i+2]*(e->efc_pos[i]-e->efc_margin[i]);
+  }
+}
+
+/* :2387-2549 (island < 0, cost = NULL); this fork leaves the elliptic branch empty */
+static void or_constraintUpdate(const mjhipModel* m, mjhipData* d, orEfc* e, const mjtNum* jar) {
+  int ne = e->ne, nf = e->nf, nefc = e->nefc;
+  const mjtNum *D = e->efc_D, *R = e->efc_R, *floss = e->efc_frictionloss;
+  mjtNum* force = e->efc_force;
+  if (!nefc) {
+    mju_zero(d->qfrc_constraint, m->nv);
+    return;
+  }
+  for (int i = 0; i < nefc; i++) force[i] = -D[i] * jar[i];
+  for (int i = 0; i < nefc; i++) {
+    if (i < ne) {
+      e->efc_state[i] = orCNSTRSTATE_QUADRATIC;
+      continue;
+    }
+    if (i < ne + nf) {
+      if (jar[i] <= -R[i] * floss[i]) {
+        force[i] = floss[i];
+        e->efc_state[i] = orCNSTRSTATE_LINEARNEG;
+      } else if (jar[i] >= R[i] * floss[i]) {
+        force[i] = -floss[i];
+        e->efc_state[i] = orCNSTRSTATE_LINEARPOS;
+      } else {
+        e->efc_state[i] = orCNSTRSTATE_QUADRATIC;
+      }
+      continue;
+    }
+    if (e->efc_type[i] != orCNSTR_CONTACT_ELLIPTIC) {
+      if (jar[i] >= 0) {
+        force[i] = 0;
+        e->efc_state[i] = orCNSTRSTATE_SATISFIED;
+      } else {
+        e->efc_state[i] = orCNSTRSTATE_QUADRATIC;
+      }
+    }
+  }
+  /* mj_mulJacTVec, dense: mju_mulMatTVec (engine_core_constraint.c:426-442) */
+  mju_mulMatTVec(d->qfrc_constraint, e->efc_J, e->efc_force, nefc, m->nv);
+}
+
+/*============================ engine_forward.c / engine_inverse.c =========================*/
+
+/* engine_forward.c:193-231 */
+static void or_fwdVelocity(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  mju_mulMatVec(d->ten_velocity, d->ten_J, d->qvel, m->ntendon, m->nv);
+  if (!mjDISABLED(mjhipDSBL_ACTUATION)) {
+    for (int r = 0; r < m->nu; r++) {
+      d->actuator_velocity[r] = mju_dotSparse(d->actuator_moment + m->moment_rowadr[r], d->qvel,
+                                              m->moment_rownnz[r],
+                                              m->moment_colind + m->moment_rowadr[r]);
+    }
+  }
+  or_comVel(m, d);
+  or_passive(m, d);
+  or_referenceConstraint(m, d, e);
+  or_rne(m, d, 0, d->qfrc_bias);
+}
+
+/* engine_inverse.c:37-68 (mj_collision: no contacts in the supported subset) */
+static void or_invPosition(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  or_kinematics(m, d);
+  or_comPos(m, d);
+  or_camlight(m, d);
+  or_tendon(m, d);
+  or_crb(m, d);
+  or_factorM(m, d);
+  or_makeConstraint(m, d, e);
+  or_transmission(m, d);
+}
+
+/* engine_inverse.c:169-192 */
+static void or_invConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  int nefc = e->nefc;
+  if (!nefc) {
+    mju_zero(d->qfrc_constraint, m->nv);
+    return;
+  }
+  mjtNum* jar = (mjtNum*)malloc(nefc*sizeof(mjtNum));
+  mju_mulMatVec(jar, e->efc_J, d->qacc, nefc, m->nv);
+  mju_subFrom(jar, e->efc_aref, nefc);
+  or_constraintUpdate(m, d, e, jar);
+  free(jar);
+}
+
+/* engine_inverse.c:197-261 (sensors/energy: none in the supported subset;
+ * mjENBL_INVDISCRETE is not supported by the oracle) */
+void or_inverseSkip(const mjhipModel* m, mjhipData* d, orEfc* e, int skipstage,
+                    int skipsensor) {
+  int nv = m->nv;
+  (void)skipsensor;
+  if (skipstage < mjhipSTAGE_POS) or_invPosition(m, d, e);
+  if (skipstage < mjhipSTAGE_VEL) or_fwdVelocity(m, d, e);
+  or_invConstraint(m, d, e);
+  or_rne(m, d, 1, d->qfrc_inverse);
+  for (int i = 0; i < nv; i++) {
+    d->qfrc_inverse[i] += m->dof_armature[i] * d->qacc[i]
+                          - d->qfrc_passive[i] - d->qfrc_constraint[i];
+  }
+  d->nefc = e->nefc;
+}
+
+/* engine_inverse.c:266-269 */
+void or_inverse(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  or_inverseSkip(m, d, e, mjhipSTAGE_NONE, 0);
+}
+
+/*============================ forward harness (engine_forward.c) ===========================*/
+
+/* mj_fwdActuation :276-515 for gain fixed/affine, bias none/affine, no dynamics, joint
+ * transmission; qfrc_actuator = moment' * force */
+static void or_fwdActuation(const mjhipModel* m, mjhipData* d) {
+  int nv = m->nv, nu = m->nu;
+  mju_zero(d->qfrc_actuator, nv);
+  if (mjDISABLED(mjhipDSBL_ACTUATION) || !nu) return;
+  mjtNum* force = (mjtNum*)calloc(nu, sizeof(mjtNum));
+  for (int i = 0; i < nu; i++) {
+    mjtNum ctrl = d->ctrl ? d->ctrl[i] : 0;
+    if (m->actuator_ctrllimited[i] && !mjDISABLED(mjhipDSBL_CLAMPCTRL)) {
+      mjtNum* r = m->actuator_ctrlrange + 2*i;
+      ctrl = ctrl < r[0] ? r[0] : (ctrl > r[1] ? r[1] : ctrl);
+    }
+    mjtNum* prm = m->actuator_gainprm + 10*i;
+    mjtNum gain = prm[0];
+    if (m->actuator_gaintype[i] == mjhipGAIN_AFFINE) {
+      gain = prm[0] + prm[1]*d->actuator_length[i] + prm[2]*d->actuator_velocity[i];
+    }
+    force[i] = gain * ctrl;
+    if (m->actuator_biastype[i] == mjhipBIAS_AFFINE) {
+      prm = m->actuator_biasprm + 10*i;
+      force[i] += prm[0] + prm[1]*d->actuator_length[i] + prm[2]*d->actuator_velocity[i];
+    }
+    if (m->actuator_forcelimited[i]) {
+      mjtNum* r = m->actuator_forcerange + 2*i;
+      force[i] = force[i] < r[0] ? r[0] : (force[i] > r[1] ? r[1] : force[i]);
+    }
+  }
+  for (int i = 0; i < nu; i++) {       /* mju_mulMatTVecSparse */
+    if (!force[i]) continue;
+    int adr = m->moment_rowadr[i];
+    for (int j = 0; j < m->moment_rownnz[i]; j++) {
+      d->qfrc_actuator[m->moment_colind[adr+j]] += d->actuator_moment[adr+j]*force[i];
+    }
+  }
+  free(force);
+}
+
+/* mj_forward for constraint-free states: position, velocity, actuation, acceleration,
+ * with qacc = qacc_smooth (engine_forward.c:520-531, :654-: nefc = 0) */
+int or_forward(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  int nv = m->nv;
+  or_invPosition(m, d, e);
+  or_fwdVelocity(m, d, e);
+  or_fwdActuation(m, d);
+  mjtNum* qfrc_smooth = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  mju_sub(qfrc_smooth, d->qfrc_passive, d->qfrc_bias, nv);
+  mju_addTo(qfrc_smooth, d->qfrc_applied, nv);
+  mju_addTo(qfrc_smooth, d->qfrc_actuator, nv);
+  or_xfrcAccumulate(m, d, qfrc_smooth);
+  or_solveM(m, d, d->qacc, qfrc_smooth, 1);
+  mju_zero(d->qfrc_constraint, nv);
+  free(qfrc_smooth);
+  d->nefc = e->nefc;
+  return e->nefc;
+}
+
+/* mj_RungeKutta(m, d, 4), engine_forward.c:842-941 (na = 0) */
+void or_rungeKutta4(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  static const mjtNum A[9] = {0.5, 0, 0, 0, 0.5, 0, 0, 0, 1};
+  static const mjtNum Bt[4] = {1.0/6.0, 1.0/3.0, 1.0/3.0, 1.0/6.0};
+  int nv = m->nv, nq = m->nq, N = 4;
+  mjtNum h = m->opt.timestep;
+  mjtNum *X[4], *F[4];
+  mjtNum* dX = (mjtNum*)malloc(2*nv*sizeof(mjtNum));
+  for (int i = 0; i < N; i++) {
+    X[i] = (mjtNum*)malloc((nq+nv)*sizeof(mjtNum));
+    F[i] = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  }
+  mju_copy(X[0], d->qpos, nq);
+  mju_copy(X[0]+nq, d->qvel, nv);
+  mju_copy(F[0], d->qacc, nv);
+  for (int i = 1; i < N; i++) {
+    mju_zero(dX, 2*nv);
+    for (int j = 0; j < i; j++) {
+      mju_addToScl(dX, X[j]+nq, A[(i-1)*(N-1)+j], nv);
+      mju_addToScl(dX+nv, F[j], A[(i-1)*(N-1)+j], nv);
+    }
+    mju_copy(X[i], X[0], nq+nv);
+    mj_integratePos(m, X[i], dX, h);
+    mju_addToScl(X[i]+nq, dX+nv, h, nv);
+    mju_copy(d->qpos, X[i], nq);
+    mju_copy(d->qvel, X[i]+nq, nv);
+    or_forward(m, d, e);
+    mju_copy(F[i], d->qacc, nv);
+  }
+  mju_zero(dX, 2*nv);
+  for (int j = 0; j < N; j++) {
+    mju_addToScl(dX, X[j]+nq, Bt[j], nv);
+    mju_addToScl(dX+nv, F[j], Bt[j], nv);
+  }
+  mju_copy(d->qpos, X[0], nq);
+  mju_copy(d->qvel, X[0]+nq, nv);
+  /* mj_advance(m, d, 0, dX+nv, dX): qvel += h*qacc, then integratePos with dX */
+  mju_addToScl(d->qvel, dX+nv, h, nv);
+  mj_integratePos(m, d->qpos, dX, h);
+  for (int i = 0; i < N; i++) {
+    free(X[i]);
+    free(F[i]);
+  }
+  free(dX);
+}
+
+/*============================ engine_derivative_fd.c ======================================*/
+
+/* :48-53 */
+static void diff(mjtNum* dx, const mjtNum* x1, const mjtNum* x2, mjtNum h, int n) {
+  mjtNum inv_h = 1/h;
+  for (int i = 0; i < n; i++) dx[i] = inv_h * (x2[i] - x1[i]);
+}
+
+/* :611-719 with flg_actuation = 0, no sensor outputs */
+void or_inverseFD(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum eps, mjtNum* DfDq,
+                  mjtNum* DfDv, mjtNum* DfDa, mjtNum* DmDq) {
+  int nq = m->nq, nv = m->nv, nM = m->nM;
+  mjtNum* pos = (mjtNum*)malloc(nq*sizeof(mjtNum));
+  mjtNum* force = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  mjtNum* force_plus = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  mjtNum* mass = (mjtNum*)malloc(nM*sizeof(mjtNum));
+  mjtNum* mass_plus = (mjtNum*)malloc(nM*sizeof(mjtNum));
+  mjtNum* dpos = (mjtNum*)calloc(nv, sizeof(mjtNum));
+  mju_copy(pos, d->qpos, nq);
+  or_inverseSkip(m, d, e, mjhipSTAGE_NONE, 1);
+  mju_copy(force, d->qfrc_inverse, nv);
+  mju_copy(mass, d->qM, nM);
+  if (DfDa) {
+    for (int i = 0; i < nv; i++) {
+      mjtNum tmp = d->qacc[i];
+      d->qacc[i] += eps;
+      or_inverseSkip(m, d, e, mjhipSTAGE_VEL, 1);
+      d->qacc[i] = tmp;
+      diff(DfDa + i*nv, force, d->qfrc_inverse, eps, nv);
+    }
+  }
+  if (DfDv) {
+    for (int i = 0; i < nv; i++) {
+      mjtNum tmp = d->qvel[i];
+      d->qvel[i] += eps;
+      or_inverseSkip(m, d, e, mjhipSTAGE_POS, 1);
+      d->qvel[i] = tmp;
+      diff(DfDv + i*nv, force, d->qfrc_inverse, eps, nv);
+    }
+  }
+  if (DfDq || DmDq) {
+    for (int i = 0; i < nv; i++) {
+      mju_zero(dpos, nv);
+      dpos[i] = 1;
+      mj_integratePos(m, d->qpos, dpos, eps);
+      or_inverseSkip(m, d, e, mjhipSTAGE_NONE, 1);
+      mju_copy(d->qpos, pos, nq);
+      if (DfDq) diff(DfDq + i*nv, force, d->qfrc_inverse, eps, nv);
+      mju_copy(force_plus, d->qfrc_inverse, nv);
+      mju_copy(mass_plus, d->qM, nM);
+      if (DmDq) diff(DmDq + i*nM, mass, mass_plus, eps, nM);
+    }
+  }
+  /* like the reference, d keeps the outputs of the last perturbed evaluation */
+  free(pos); free(force); free(force_plus); free(mass); free(mass_plus); free(dpos);
+}
+
+/*============================ CPU baseline =================================================*/
+
+typedef struct {
+  const mjhipModel* m;
+  const mjtNum *qpos, *qvel, *qacc;
+  mjtNum* qfrc;
+  int B, chunk;
+  int* next;               /* shared chunk counter */
+  pthread_mutex_t* lock;
+} orJob;
+
+static mjtNum* alloc_data(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  size_t total = 0;
+  int cap = or_efcCapacity(m);
+#define MJ_M(n) m->n
+#define XD(name, d0, d1, stage) total += (size_t)(m->d0) * (d1);
+  MJHIP_DATA_FIELDS
+#undef XD
+  total += 2*(size_t)m->nv + 6*(size_t)m->nbody + m->nu;
+  total += (size_t)cap * (m->nv + 14);
+  mjtNum* buf = (mjtNum*)calloc(total + 1, sizeof(mjtNum));
+  mjtNum* p = buf;
+  memset(d, 0, sizeof(*d));
+#define XD(name, d0, d1, stage) d->name = p; p += (size_t)(m->d0) * (d1);
+  MJHIP_DATA_FIELDS
+#undef XD
+#undef MJ_M
+  d->qfrc_applied = p; p += m->nv;
+  d->qfrc_actuator = p; p += m->nv;
+  d->xfrc_applied = p; p += 6*m->nbody;
+  d->ctrl = p; p += m->nu;
+  memset(e, 0, sizeof(*e));
+  e->capacity = cap;
+  e->efc_J = p; p += (size_t)cap*m->nv;
+  e->efc_pos = p; p += cap;
+  e->efc_margin = p; p += cap;
+  e->efc_frictionloss = p; p += cap;
+  e->efc_diagApprox = p; p += cap;
+  e->efc_KBIP = p; p += 4*(size_t)cap;
+  e->efc_D = p; p += cap;
+  e->efc_R = p; p += cap;
+  e->efc_vel = p; p += cap;
+  e->efc_aref = p; p += cap;
+  e->efc_force = p; p += cap;
+  e->efc_type = (int*)calloc(3*(size_t)cap + 1, sizeof(int));
+  e->efc_id = e->efc_type + cap;
+  e->efc_state = e->efc_id + cap;
+  return buf;
+}
+
+static void* worker(void* arg) {
+  orJob* J = (orJob*)arg;
+  const mjhipModel* m = J->m;
+  mjhipData d;
+  orEfc e;
+  mjtNum* buf = alloc_data(m, &d, &e);
+  for (;;) {
+    pthread_mutex_lock(J->lock);
+    int start = *J->next;
+    *J->next += J->chunk;
+    pthread_mutex_unlock(J->lock);
+    if (start >= J->B) break;
+    int end = start + J->chunk < J->B ? start + J->chunk : J->B;
+    for (int k = start; k < end; k++) {
+      mju_copy(d.qpos, J->qpos + (size_t)k*m->nq, m->nq);
+      mju_copy(d.qvel, J->qvel + (size_t)k*m->nv, m->nv);
+      mju_copy(d.qacc, J->qacc + (size_t)k*m->nv, m->nv);
+      or_inverse(m, &d, &e);
+      mju_copy(J->qfrc + (size_t)k*m->nv, d.qfrc_inverse, m->nv);
+    }
+  }
+  free(e.efc_type);
+  free(buf);
+  return NULL;
+}
+
+double or_inverseBatch(const mjhipModel* m, int B, const mjtNum* qpos, const mjtNum* qvel,
+                       const mjtNum* qacc, mjtNum* qfrc_inverse, int nthread) {
+  if (nthread < 1) nthread = 1;
+  int chunk = B / (10*nthread);
+  if (chunk < 1) chunk = 1;
+  int next = 0;
+  pthread_mutex_t lock = PTHREAD_MUTEX_INITIALIZER;
+  orJob job = {m, qpos, qvel, qacc, qfrc_inverse, B, chunk, &next, &lock};
+  pthread_t* th = (pthread_t*)malloc(nthread*sizeof(pthread_t));
+  struct timespec t0, t1;
+  clock_gettime(CLOCK_MONOTONIC, &t0);
+  for (int i = 0; i < nthread; i++) pthread_create(&th[i], NULL, worker, &job);
+  for (int i = 0; i < nthread; i++) pthread_join(th[i], NULL);
+  clock_gettime(CLOCK_MONOTONIC, &t1);
+  free(th);
+  return (t1.tv_sec - t0.tv_sec) + 1e-9*(t1.tv_nsec - t0.tv_nsec);
+}

@@ -1,0 +1,88 @@
+/* mj_oracle.h — TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of the reference's inverse-dynamics path (MuJoCo 3.3.1 fork,
+ * fancifulland2718/mujoco_InverseDynamicsTest), used as the parity checker for the HIP
+ * engine. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load
+ * liboracle.so; the product library (libmjhip.so) never links or calls it.
+ *
+ * Parity pinning: the reference cannot be built in this image (src/engine/engine_support.c
+ * includes engine_collision_convex.h -> <ccd/vec3.h>, libccd v2.1 @7931e764 is absent and
+ * stand-in headers are not allowed), so this restatement is pinned by the reference's own
+ * known-answer/property tests restated in tests/test_oracle_pins.py (LinearSystemInverse,
+ * FactorI/FactorIs, SolveLDs, MjDataWorldBodyValuesAreInitialized, the fwd/inv identity of
+ * src/inverse/inverse_test.cpp and mj_compareFwdInv) — there are no golden vectors in the
+ * reference. Summation orders follow the scalar (non-AVX) reference code, which the
+ * reference states reproduces its AVX order for mju_dot (engine_util_blas.c:715-729).
+ */
+#ifndef MJ_ORACLE_H_
+#define MJ_ORACLE_H_
+
+#include "../include/mjhip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* constraint rows (the reference's efc_* arena arrays, mjxmacro.h MJDATA_ARENA_POINTERS) */
+typedef struct orEfc_ {
+  int capacity;       /* rows allocated */
+  int nefc, ne, nf, nl;
+  int* efc_type;      /* mjtConstraint */
+  int* efc_id;
+  int* efc_state;     /* mjtConstraintState */
+  mjtNum* efc_J;      /* capacity x nv, dense */
+  mjtNum* efc_pos;
+  mjtNum* efc_margin;
+  mjtNum* efc_frictionloss;
+  mjtNum* efc_diagApprox;
+  mjtNum* efc_KBIP;   /* capacity x 4 */
+  mjtNum* efc_D;
+  mjtNum* efc_R;
+  mjtNum* efc_vel;
+  mjtNum* efc_aref;
+  mjtNum* efc_force;
+} orEfc;
+
+/* mjtConstraint / mjtConstraintState values (mjmodel.h) */
+enum { orCNSTR_EQUALITY = 0, orCNSTR_FRICTION_DOF, orCNSTR_FRICTION_TENDON,
+       orCNSTR_LIMIT_JOINT, orCNSTR_LIMIT_TENDON, orCNSTR_CONTACT_FRICTIONLESS,
+       orCNSTR_CONTACT_PYRAMIDAL, orCNSTR_CONTACT_ELLIPTIC };
+enum { orCNSTRSTATE_SATISFIED = 0, orCNSTRSTATE_QUADRATIC, orCNSTRSTATE_LINEARNEG,
+       orCNSTRSTATE_LINEARPOS, orCNSTRSTATE_CONE };
+
+int  or_efcCapacity(const mjhipModel* m);
+
+/* pipeline (engine_inverse.c) */
+void or_inverseSkip(const mjhipModel* m, mjhipData* d, orEfc* efc, int skipstage,
+                    int skipsensor);
+void or_inverse(const mjhipModel* m, mjhipData* d, orEfc* efc);
+
+/* individual stages, exported for the pin tests */
+void or_kinematics(const mjhipModel* m, mjhipData* d);
+void or_comPos(const mjhipModel* m, mjhipData* d);
+void or_crb(const mjhipModel* m, mjhipData* d);
+void or_factorM(const mjhipModel* m, mjhipData* d);
+void or_solveM(const mjhipModel* m, const mjhipData* d, mjtNum* x, const mjtNum* y, int n);
+void or_rne(const mjhipModel* m, mjhipData* d, int flg_acc, mjtNum* result);
+void or_fullM(const mjhipModel* m, mjtNum* dst, const mjtNum* M);
+
+/* forward dynamics harness for the fwd/inv identity (engine_forward.c), constraint-free
+ * states only: returns nefc (the caller checks 0) */
+int  or_forward(const mjhipModel* m, mjhipData* d, orEfc* efc);
+void or_xfrcAccumulate(const mjhipModel* m, mjhipData* d, mjtNum* qfrc);
+void or_rungeKutta4(const mjhipModel* m, mjhipData* d, orEfc* efc);
+
+/* mjd_inverseFD (engine_derivative_fd.c:611-719), flg_actuation = 0, no sensors */
+void or_inverseFD(const mjhipModel* m, mjhipData* d, orEfc* efc, mjtNum eps,
+                  mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DmDq);
+
+/* CPU baseline: B instances of mj_inverse over `nthread` threads, one data per thread,
+ * static chunks of B/(10*nthread) (python/mujoco/rollout.cc:307-317). Returns seconds. */
+double or_inverseBatch(const mjhipModel* m, int B, const mjtNum* qpos, const mjtNum* qvel,
+                       const mjtNum* qacc, mjtNum* qfrc_inverse, int nthread);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif  /* MJ_ORACLE_H_ */

@@ -1,0 +1,157 @@
+"""ctypes binding of liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+The CPU restatement of the reference's mj_inverse path (mj_oracle.c) is the parity checker
+for the HIP engine. Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg
+may import this module; the product package never does.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+from mujoco_inversedynamicstest_amd import fields, host
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_lib = None
+
+_D = ctypes.POINTER(ctypes.c_double)
+
+
+class Efc(ctypes.Structure):
+  _fields_ = ([("capacity", ctypes.c_int), ("nefc", ctypes.c_int), ("ne", ctypes.c_int),
+               ("nf", ctypes.c_int), ("nl", ctypes.c_int),
+               ("efc_type", ctypes.POINTER(ctypes.c_int)),
+               ("efc_id", ctypes.POINTER(ctypes.c_int)),
+               ("efc_state", ctypes.POINTER(ctypes.c_int))] +
+              [(n, _D) for n in ("efc_J", "efc_pos", "efc_margin", "efc_frictionloss",
+                                 "efc_diagApprox", "efc_KBIP", "efc_D", "efc_R", "efc_vel",
+                                 "efc_aref", "efc_force")])
+
+
+def build():
+  subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib():
+  global _lib
+  if _lib is None:
+    if not os.path.exists(_LIB):
+      build()
+    L = ctypes.CDLL(_LIB)
+    M = ctypes.POINTER(fields.CModel)
+    Dp = ctypes.POINTER(fields.CData)
+    E = ctypes.POINTER(Efc)
+    L.or_efcCapacity.argtypes = [M]
+    L.or_inverseSkip.argtypes = [M, Dp, E, ctypes.c_int, ctypes.c_int]
+    L.or_inverse.argtypes = [M, Dp, E]
+    for fn in ("or_kinematics", "or_comPos", "or_crb", "or_factorM"):
+      getattr(L, fn).argtypes = [M, Dp]
+    L.or_solveM.argtypes = [M, Dp, _D, _D, ctypes.c_int]
+    L.or_rne.argtypes = [M, Dp, ctypes.c_int, _D]
+    L.or_fullM.argtypes = [M, _D, _D]
+    L.or_forward.argtypes = [M, Dp, E]
+    L.or_forward.restype = ctypes.c_int
+    L.or_xfrcAccumulate.argtypes = [M, Dp, _D]
+    L.or_rungeKutta4.argtypes = [M, Dp, E]
+    L.or_inverseFD.argtypes = [M, Dp, E, ctypes.c_double, _D, _D, _D, _D]
+    L.or_inverseBatch.argtypes = [M, ctypes.c_int, _D, _D, _D, _D, ctypes.c_int]
+    L.or_inverseBatch.restype = ctypes.c_double
+    _lib = L
+  return _lib
+
+
+def _p(a):
+  return None if a is None else a.ctypes.data_as(_D)
+
+
+class Oracle:
+  """Single-instance CPU reference bound to one compiled model."""
+
+  def __init__(self, m):
+    self.m = m
+    self.cm = host.model_struct(m)
+    self.L = lib()
+    self.d = host.MjData(m)
+    cap = max(self.L.or_efcCapacity(ctypes.byref(self.cm)), 1)
+    nv = max(m.nv, 1)
+    self._efc_arrays = {n: np.zeros(cap * k) for n, k in
+                        (("efc_J", nv), ("efc_pos", 1), ("efc_margin", 1),
+                         ("efc_frictionloss", 1), ("efc_diagApprox", 1), ("efc_KBIP", 4),
+                         ("efc_D", 1), ("efc_R", 1), ("efc_vel", 1), ("efc_aref", 1),
+                         ("efc_force", 1))}
+    self._efc_int = {n: np.zeros(cap, dtype=np.int32) for n in
+                     ("efc_type", "efc_id", "efc_state")}
+    self.efc = Efc()
+    self.efc.capacity = cap
+    for n, a in self._efc_arrays.items():
+      setattr(self.efc, n, _p(a))
+    for n, a in self._efc_int.items():
+      setattr(self.efc, n, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+
+  def _args(self):
+    return ctypes.byref(self.cm), ctypes.byref(self.d.struct), ctypes.byref(self.efc)
+
+  def set_state(self, qpos=None, qvel=None, qacc=None):
+    if qpos is not None:
+      self.d.qpos[:] = qpos
+    if qvel is not None:
+      self.d.qvel[:] = qvel
+    if qacc is not None:
+      self.d.qacc[:] = qacc
+
+  def inverse(self, qpos=None, qvel=None, qacc=None, skipstage=0, skipsensor=0):
+    self.set_state(qpos, qvel, qacc)
+    self.L.or_inverseSkip(*self._args(), skipstage, skipsensor)
+    return self.d.qfrc_inverse.copy()
+
+  def forward(self):
+    return self.L.or_forward(*self._args())
+
+  def rk4(self):
+    self.L.or_rungeKutta4(*self._args())
+
+  def xfrc_accumulate(self, qfrc):
+    self.L.or_xfrcAccumulate(ctypes.byref(self.cm), ctypes.byref(self.d.struct), _p(qfrc))
+
+  def solveM(self, y):
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    n = y.size // self.m.nv
+    x = np.zeros_like(y)
+    self.L.or_solveM(ctypes.byref(self.cm), ctypes.byref(self.d.struct), _p(x), _p(y), n)
+    return x
+
+  def fullM(self, M=None):
+    M = self.d.qM if M is None else np.ascontiguousarray(M)
+    out = np.zeros((self.m.nv, self.m.nv))
+    self.L.or_fullM(ctypes.byref(self.cm), _p(out), _p(M))
+    return out
+
+  def efc_field(self, name):
+    if name in self._efc_arrays:
+      k = self._efc_arrays[name].size // self.efc.capacity
+      return self._efc_arrays[name][:self.efc.nefc * k]
+    return self._efc_int[name][:self.efc.nefc]
+
+  def inverse_fd(self, eps=1e-6, dmdq=False):
+    nv, nM = self.m.nv, self.m.nM
+    DfDq = np.zeros((nv, nv))
+    DfDv = np.zeros((nv, nv))
+    DfDa = np.zeros((nv, nv))
+    DmDq = np.zeros((nv, nM)) if dmdq else None
+    self.L.or_inverseFD(*self._args(), eps, _p(DfDq), _p(DfDv), _p(DfDa), _p(DmDq))
+    return DfDq, DfDv, DfDa, DmDq
+
+  def inverse_batch(self, qpos, qvel, qacc, nthread=1):
+    """CPU baseline over B instances; returns (qfrc_inverse [B, nv], seconds)."""
+    qpos = np.ascontiguousarray(qpos, dtype=np.float64)
+    qvel = np.ascontiguousarray(qvel, dtype=np.float64)
+    qacc = np.ascontiguousarray(qacc, dtype=np.float64)
+    B = qpos.shape[0]
+    out = np.zeros((B, self.m.nv))
+    t = self.L.or_inverseBatch(ctypes.byref(self.cm), B, _p(qpos), _p(qvel), _p(qacc),
+                               _p(out), nthread)
+    return out, t
