@@ -1,0 +1,147 @@
+"""bench.py — mj_inverse evals/s, humanoid 27-DoF, batch 65,536 per GPU (BASELINE.json).
+
+A step is one pass of the fused HIP mj_inverse over one batch of 65,536 synthetic humanoid
+states (config-2 sampler, contacts disabled, every limit inactive) whose inputs are already
+resident in the device mirror (HBM); every mjData output field of mj_inverse is written
+(2,563 doubles per instance). With N GPUs each rank owns its own 65,536-instance shard of
+the global batch (weak scaling, no collective in the timed region); after timing, rank 0
+gathers a checksum of every rank's qfrc_inverse over RCCL.
+
+  python bench.py [--gpus N] [--steps K] [--warmup W]
+  torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0 (contract in the task statement).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "mj_inverse evals/sec, humanoid 27-DoF, batch=65536 @ 1/2/4/8 MI355X vs host CPU"
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+
+
+def main():
+  ap = argparse.ArgumentParser()
+  ap.add_argument("--gpus", type=int, default=1)
+  ap.add_argument("--steps", type=int, default=20)
+  ap.add_argument("--warmup", type=int, default=5)
+  ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
+  ap.add_argument("--model", default="humanoid")
+  ap.add_argument("--cpu-threads", type=int, default=16)
+  ap.add_argument("--cpu-sample", type=int, default=1_500_000,
+                  help="instances in the CPU-baseline sample (rank 0, N=1 only)")
+  ap.add_argument("--no-cpu", action="store_true")
+  args = ap.parse_args()
+
+  import torch
+  import torch.distributed as dist
+
+  world = int(os.environ.get("WORLD_SIZE", "1"))
+  rank = int(os.environ.get("RANK", "0"))
+  local = int(os.environ.get("LOCAL_RANK", "0"))
+  if world > 1:
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    torch.cuda.set_device(local)
+    dist.init_process_group("nccl", rank=rank, world_size=world,
+                            device_id=torch.device("cuda", local))
+  else:
+    torch.cuda.set_device(local)
+  dev = torch.device("cuda", local)
+
+  from mujoco_inversedynamicstest_amd import engine, fields, models, parallel
+  from mujoco_inversedynamicstest_amd.sampler import sample_states
+
+  m = models.load(args.model, disable_contact=True)
+  B = args.batch
+  first, count = parallel.shard(B * world, world, rank)
+  q, v, a = sample_states(m, count, first=first)
+  eng = engine.InverseEngine(m, capacity=count, device=local)
+  eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
+  eng.upload_states(q, v, a)
+  out = torch.empty((count, m.nv), dtype=torch.float64, device=dev)
+
+  def step():
+    eng.inverse(count, out=out, mirror_input=True)
+
+  for _ in range(args.warmup):
+    step()
+  torch.cuda.synchronize(dev)
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize(dev)
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    step()
+  torch.cuda.synchronize(dev)
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize(dev)
+  elapsed = time.perf_counter() - t0
+  t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+  if world > 1:
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+  elapsed = float(t.item())
+
+  # kernel-only average launch time (HIP events on the context's stream) for the roofline
+  kernel_ms = eng.time_kernel(count, reps=max(args.steps, 10))
+  bytes_per_eval = engine.output_bytes_per_eval(m)
+  achieved = bytes_per_eval * count / (kernel_ms * 1e-3) / 1e9
+
+  # after timing: rank 0 gathers every rank's qfrc_inverse checksum over RCCL
+  chk = out.sum(dim=0)
+  gathered = parallel.gather_to_rank0(chk, world, rank) if world > 1 else [chk]
+  checksum = float(sum(float(x.abs().sum()) for x in gathered)) if rank == 0 else None
+
+  cpu = None
+  if rank == 0 and world == 1 and not args.no_cpu:
+    from oracle.oracle import Oracle
+    n = args.cpu_sample
+    cq, cv, ca = sample_states(m, n, first=0)
+    o = Oracle(m)
+    _, secs = o.inverse_batch(cq, cv, ca, nthread=args.cpu_threads)
+    cpu = {"value": n / secs, "unit": "evals/s", "cores": args.cpu_threads, "kind": "port",
+           "sample": f"{n} humanoid states (first {n} of the same sampler stream), "
+                     f"{args.cpu_threads} threads, oracle/mj_oracle.c -O2, "
+                     f"{secs:.2f} s wall"}
+
+  if rank == 0:
+    value = world * count * args.steps / elapsed
+    rec = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "evals/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic: config-2 sampler (seed 20250314), inputs resident in HBM",
+        "config": {"workload": f"{args.model} 27-DoF mj_inverse (skipstage NONE), contacts "
+                               f"disabled, nefc=0, full mjData mirror written",
+                   "per_gpu_batch": count, "global_batch": world * count,
+                   "parallelism": f"dp{world}"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "kernel": "k_inverse<0>", "kernel_ms": kernel_ms,
+                     "bytes_per_eval": bytes_per_eval},
+        "cpu_baseline": cpu,
+        "checksum_qfrc_inverse": checksum,
+    }
+    print(json.dumps(rec), flush=True)
+  eng.close()
+  if world > 1:
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+  main()

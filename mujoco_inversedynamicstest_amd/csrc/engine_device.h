@@ -1,0 +1,1205 @@
+// engine_device.h — per-instance mj_inverseSkip pipeline for the HIP engine.
+//
+// One lane = one simulation instance. Every per-instance array lives in the device mirror
+// (include/mjhip.h: F[(blk*S + k)*64 + lane]); `Lane<STRIDE>` is a strided view of one
+// lane's slice, so the code below indexes fields exactly like the reference indexes mjData
+// (e.g. d.xmat[9*i+k]) while every access of a wavefront is one contiguous 512-byte segment.
+// STRIDE = 64 on the GPU; the test suite also compiles this file for the host with
+// STRIDE = 1 (tests/cpu_kernel_harness.cpp) to check it bit-for-bit against the oracle.
+//
+// Each function cites the reference file:line it restates (paths relative to the
+// reference root). Summation orders follow the reference's scalar C code.
+#ifndef MJHIP_ENGINE_DEVICE_H_
+#define MJHIP_ENGINE_DEVICE_H_
+
+#include <math.h>
+
+#include "../../include/mjhip.h"
+
+#if defined(__HIPCC__)
+  #define MJH_HD __host__ __device__ inline
+#else
+  #define MJH_HD inline
+#endif
+
+namespace mjh {
+
+constexpr double MINVAL = mjhipMINVAL;
+
+// constraint types/states (include/mujoco/mjmodel.h mjtConstraint, mjtConstraintState)
+enum { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF, CNSTR_FRICTION_TENDON, CNSTR_LIMIT_JOINT,
+       CNSTR_LIMIT_TENDON, CNSTR_CONTACT_FRICTIONLESS, CNSTR_CONTACT_PYRAMIDAL,
+       CNSTR_CONTACT_ELLIPTIC };
+enum { CNSTRSTATE_SATISFIED = 0, CNSTRSTATE_QUADRATIC, CNSTRSTATE_LINEARNEG,
+       CNSTRSTATE_LINEARPOS };
+
+//---------------------------------- strided per-lane views -----------------------------------
+
+template <int S, class T = double>
+struct SP {
+  T* p;
+  MJH_HD T& operator[](long k) const { return p[k * S]; }
+  MJH_HD SP operator+(long k) const { return SP{p + k * S}; }
+};
+
+// scratch fields (not part of the mjData contract) and constraint rows (the reference's
+// efc_* arena arrays, mjxmacro.h MJDATA_ARENA_POINTERS_SOLVER), per instance
+#define MJHIP_SCRATCH_FIELDS          \
+  XSC(mass_subtree, nbody)            \
+  XSC(cacc, 6*nbody)                  \
+  XSC(cfrc, 6*nbody)                  \
+  XSC(jacp, 3*nv)                     \
+  XSC(jacr, 3*nv)                     \
+  XSC(qforce, nv)                     \
+  XSC(efc_J, efc_cap*nv)              \
+  XSC(efc_pos, efc_cap)               \
+  XSC(efc_margin, efc_cap)            \
+  XSC(efc_frictionloss, efc_cap)      \
+  XSC(efc_diagApprox, efc_cap)        \
+  XSC(efc_KBIP, 4*efc_cap)            \
+  XSC(efc_D, efc_cap)                 \
+  XSC(efc_R, efc_cap)                 \
+  XSC(efc_vel, efc_cap)               \
+  XSC(efc_aref, efc_cap)              \
+  XSC(efc_force, efc_cap)             \
+  XSC(jar, efc_cap)
+
+#define MJHIP_SCRATCH_INT_FIELDS      \
+  XSI(efc_type, efc_cap)              \
+  XSI(efc_id, efc_cap)                \
+  XSI(efc_state, efc_cap)             \
+  XSI(efc_count, 4)                   /* nefc, ne, nf, nl */
+
+template <int S>
+struct Lane {
+#define XD(name, d0, d1, stage) SP<S> name;
+  MJHIP_DATA_FIELDS
+#undef XD
+#define XSC(name, n) SP<S> name;
+  MJHIP_SCRATCH_FIELDS
+#undef XSC
+#define XSI(name, n) SP<S, int> name;
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+  int efc_cap;
+};
+
+//---------------------------------- engine_util_blas.c ---------------------------------------
+
+template <class R> MJH_HD void zero3(R r) { r[0] = 0; r[1] = 0; r[2] = 0; }
+template <class R, class A> MJH_HD void copy3(R r, A a) { r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; }
+template <class R, class A> MJH_HD void copy4(R r, A a) {
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+}
+template <class R, class A> MJH_HD void scl3(R r, A a, double s) {
+  r[0] = a[0]*s; r[1] = a[1]*s; r[2] = a[2]*s;
+}
+template <class R, class A, class B> MJH_HD void add3(R r, A a, B b) {
+  r[0] = a[0]+b[0]; r[1] = a[1]+b[1]; r[2] = a[2]+b[2];
+}
+template <class R, class A, class B> MJH_HD void sub3(R r, A a, B b) {
+  r[0] = a[0]-b[0]; r[1] = a[1]-b[1]; r[2] = a[2]-b[2];
+}
+template <class R, class A> MJH_HD void addTo3(R r, A a) {
+  r[0] += a[0]; r[1] += a[1]; r[2] += a[2];
+}
+template <class R, class A> MJH_HD void addToScl3(R r, A a, double s) {
+  r[0] += a[0]*s; r[1] += a[1]*s; r[2] += a[2]*s;
+}
+template <class R, class A, class B> MJH_HD void cross(R r, A a, B b) {
+  double t0 = a[1]*b[2] - a[2]*b[1], t1 = a[2]*b[0] - a[0]*b[2], t2 = a[0]*b[1] - a[1]*b[0];
+  r[0] = t0; r[1] = t1; r[2] = t2;
+}
+template <class R> MJH_HD void zero(R r, int n) { for (int i = 0; i < n; i++) r[i] = 0; }
+template <class R, class A> MJH_HD void copy(R r, A a, int n) {
+  for (int i = 0; i < n; i++) r[i] = a[i];
+}
+template <class R, class A> MJH_HD void scl(R r, A a, double s, int n) {
+  for (int i = 0; i < n; i++) r[i] = a[i]*s;
+}
+template <class R, class A, class B> MJH_HD void add(R r, A a, B b, int n) {
+  for (int i = 0; i < n; i++) r[i] = a[i] + b[i];
+}
+template <class R, class A> MJH_HD void addTo(R r, A a, int n) {
+  for (int i = 0; i < n; i++) r[i] += a[i];
+}
+template <class R, class A> MJH_HD void subFrom(R r, A a, int n) {
+  for (int i = 0; i < n; i++) r[i] -= a[i];
+}
+template <class R, class A> MJH_HD void addToScl(R r, A a, double s, int n) {
+  for (int i = 0; i < n; i++) r[i] += a[i]*s;
+}
+
+// engine_util_blas.c:123-140
+template <class V> MJH_HD double normalize3(V v) {
+  double norm = sqrt(v[0]*v[0] + v[1]*v[1] + v[2]*v[2]);
+  if (norm < MINVAL) {
+    v[0] = 1; v[1] = 0; v[2] = 0;
+  } else {
+    double normInv = 1/norm;
+    v[0] *= normInv; v[1] *= normInv; v[2] *= normInv;
+  }
+  return norm;
+}
+
+// engine_util_blas.c:269-285
+template <class V> MJH_HD double normalize4(V v) {
+  double norm = sqrt(v[0]*v[0] + v[1]*v[1] + v[2]*v[2] + v[3]*v[3]);
+  if (norm < MINVAL) {
+    v[0] = 1; v[1] = 0; v[2] = 0; v[3] = 0;
+  } else if (fabs(norm - 1) > MINVAL) {
+    double normInv = 1/norm;
+    v[0] *= normInv; v[1] *= normInv; v[2] *= normInv; v[3] *= normInv;
+  }
+  return norm;
+}
+
+// engine_util_blas.c:165-176
+template <class R, class M, class V> MJH_HD void mulMatVec3(R res, M mat, V vec) {
+  double t0 = mat[0]*vec[0] + mat[1]*vec[1] + mat[2]*vec[2];
+  double t1 = mat[3]*vec[0] + mat[4]*vec[1] + mat[5]*vec[2];
+  double t2 = mat[6]*vec[0] + mat[7]*vec[1] + mat[8]*vec[2];
+  res[0] = t0; res[1] = t1; res[2] = t2;
+}
+
+// engine_util_blas.c:680-741 (scalar branch): lanes 0..3, (r0+r2)+(r1+r3), then the tail
+template <class A, class B> MJH_HD double dot(A a, B b, int n) {
+  int i = 0, n_4 = n - 4;
+  double r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  for (; i <= n_4; i += 4) {
+    r0 += a[i]*b[i];
+    r1 += a[i+1]*b[i+1];
+    r2 += a[i+2]*b[i+2];
+    r3 += a[i+3]*b[i+3];
+  }
+  double res = (r0 + r2) + (r1 + r3);
+  int n_i = n - i;
+  if (n_i == 3) {
+    res += a[i]*b[i] + a[i+1]*b[i+1] + a[i+2]*b[i+2];
+  } else if (n_i == 2) {
+    res += a[i]*b[i] + a[i+1]*b[i+1];
+  } else if (n_i == 1) {
+    res += a[i]*b[i];
+  }
+  return res;
+}
+
+// mju_dot for n = 6 (the spatial-vector case): ((p0+p2)+(p1+p3)) + (p4+p5)
+template <class A, class B> MJH_HD double dot6(A a, B b) {
+  double r0 = a[0]*b[0], r1 = a[1]*b[1], r2 = a[2]*b[2], r3 = a[3]*b[3];
+  double res = (r0 + r2) + (r1 + r3);
+  res += a[4]*b[4] + a[5]*b[5];
+  return res;
+}
+
+// engine_util_blas.c:756-766
+template <class R, class M, class V> MJH_HD void mulMatTVec(R res, M mat, V vec, int nr, int nc) {
+  zero(res, nc);
+  for (int r = 0; r < nr; r++) {
+    double tmp = vec[r];
+    if (tmp) addToScl(res, mat + r*nc, tmp, nc);
+  }
+}
+
+// engine_util_sparse.h:115-160 (scalar branch)
+template <class V1, class V2> MJH_HD double dotSparse(V1 v1, V2 v2, int nnz1, const int* ind1) {
+  int i = 0, n_4 = nnz1 - 4;
+  double r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  for (; i <= n_4; i += 4) {
+    r0 += v1[i+0]*v2[ind1[i+0]];
+    r1 += v1[i+1]*v2[ind1[i+1]];
+    r2 += v1[i+2]*v2[ind1[i+2]];
+    r3 += v1[i+3]*v2[ind1[i+3]];
+  }
+  double res = (r0 + r2) + (r1 + r3);
+  for (; i < nnz1; i++) res += v1[i]*v2[ind1[i]];
+  return res;
+}
+
+//---------------------------------- engine_util_spatial.c ------------------------------------
+
+// :23-46
+template <class R, class V, class Q> MJH_HD void rotVecQuat(R res, V vec, Q quat) {
+  if (vec[0] == 0 && vec[1] == 0 && vec[2] == 0) {
+    zero3(res);
+  } else if (quat[0] == 1 && quat[1] == 0 && quat[2] == 0 && quat[3] == 0) {
+    copy3(res, vec);
+  } else {
+    double t0 = quat[0]*vec[0] + quat[2]*vec[2] - quat[3]*vec[1];
+    double t1 = quat[0]*vec[1] + quat[3]*vec[0] - quat[1]*vec[2];
+    double t2 = quat[0]*vec[2] + quat[1]*vec[1] - quat[2]*vec[0];
+    double r0 = vec[0] + 2 * (quat[2]*t2 - quat[3]*t1);
+    double r1 = vec[1] + 2 * (quat[3]*t0 - quat[1]*t2);
+    double r2 = vec[2] + 2 * (quat[1]*t1 - quat[2]*t0);
+    res[0] = r0; res[1] = r1; res[2] = r2;
+  }
+}
+
+// :62-74
+template <class R, class A, class B> MJH_HD void mulQuat(R res, A qa, B qb) {
+  double t0 = qa[0]*qb[0] - qa[1]*qb[1] - qa[2]*qb[2] - qa[3]*qb[3];
+  double t1 = qa[0]*qb[1] + qa[1]*qb[0] + qa[2]*qb[3] - qa[3]*qb[2];
+  double t2 = qa[0]*qb[2] - qa[1]*qb[3] + qa[2]*qb[0] + qa[3]*qb[1];
+  double t3 = qa[0]*qb[3] + qa[1]*qb[2] - qa[2]*qb[1] + qa[3]*qb[0];
+  res[0] = t0; res[1] = t1; res[2] = t2; res[3] = t3;
+}
+
+// :97-114
+template <class R, class A> MJH_HD void axisAngle2Quat(R res, A axis, double angle) {
+  if (angle == 0) {
+    res[0] = 1; res[1] = 0; res[2] = 0; res[3] = 0;
+  } else {
+    double s = sin(angle*0.5);
+    res[0] = cos(angle*0.5);
+    res[1] = axis[0]*s;
+    res[2] = axis[1]*s;
+    res[3] = axis[2]*s;
+  }
+}
+
+// :119-133
+template <class R, class Q> MJH_HD void quat2Vel(R res, Q quat, double dt) {
+  double axis[3] = {quat[1], quat[2], quat[3]};
+  double sin_a_2 = normalize3(axis);
+  double speed = 2 * atan2(sin_a_2, quat[0]);
+  if (speed > mjhipPI) speed -= 2*mjhipPI;
+  speed /= dt;
+  scl3(res, axis, speed);
+}
+
+// :138-146
+template <class R, class A, class B> MJH_HD void subQuat(R res, A qa, B qb) {
+  double qneg[4] = {qb[0], -qb[1], -qb[2], -qb[3]}, qdif[4];
+  mulQuat(qdif, qneg, qa);
+  quat2Vel(res, qdif, 1);
+}
+
+// :151-187
+template <class R, class Q> MJH_HD void quat2Mat(R res, Q quat) {
+  if (quat[0] == 1 && quat[1] == 0 && quat[2] == 0 && quat[3] == 0) {
+    res[0] = 1; res[1] = 0; res[2] = 0;
+    res[3] = 0; res[4] = 1; res[5] = 0;
+    res[6] = 0; res[7] = 0; res[8] = 1;
+  } else {
+    const double q00 = quat[0]*quat[0], q01 = quat[0]*quat[1], q02 = quat[0]*quat[2];
+    const double q03 = quat[0]*quat[3], q11 = quat[1]*quat[1], q12 = quat[1]*quat[2];
+    const double q13 = quat[1]*quat[3], q22 = quat[2]*quat[2], q23 = quat[2]*quat[3];
+    const double q33 = quat[3]*quat[3];
+    res[0] = q00 + q11 - q22 - q33;
+    res[4] = q00 - q11 + q22 - q33;
+    res[8] = q00 - q11 - q22 + q33;
+    res[1] = 2*(q12 - q03);
+    res[2] = 2*(q13 + q02);
+    res[3] = 2*(q12 + q03);
+    res[5] = 2*(q23 - q01);
+    res[6] = 2*(q13 - q02);
+    res[7] = 2*(q23 + q01);
+  }
+}
+
+// :385-396
+template <class R, class A, class B> MJH_HD void crossMotion(R res, A vel, B v) {
+  double r0 = -vel[2]*v[1] + vel[1]*v[2];
+  double r1 =  vel[2]*v[0] - vel[0]*v[2];
+  double r2 = -vel[1]*v[0] + vel[0]*v[1];
+  double r3 = -vel[2]*v[4] + vel[1]*v[5];
+  double r4 =  vel[2]*v[3] - vel[0]*v[5];
+  double r5 = -vel[1]*v[3] + vel[0]*v[4];
+  r3 += -vel[5]*v[1] + vel[4]*v[2];
+  r4 +=  vel[5]*v[0] - vel[3]*v[2];
+  r5 += -vel[4]*v[0] + vel[3]*v[1];
+  res[0] = r0; res[1] = r1; res[2] = r2; res[3] = r3; res[4] = r4; res[5] = r5;
+}
+
+// :401-412
+template <class R, class A, class B> MJH_HD void crossForce(R res, A vel, B f) {
+  double r0 = -vel[2]*f[1] + vel[1]*f[2];
+  double r1 =  vel[2]*f[0] - vel[0]*f[2];
+  double r2 = -vel[1]*f[0] + vel[0]*f[1];
+  double r3 = -vel[2]*f[4] + vel[1]*f[5];
+  double r4 =  vel[2]*f[3] - vel[0]*f[5];
+  double r5 = -vel[1]*f[3] + vel[0]*f[4];
+  r0 += -vel[5]*f[4] + vel[4]*f[5];
+  r1 +=  vel[5]*f[3] - vel[3]*f[5];
+  r2 += -vel[4]*f[3] + vel[3]*f[4];
+  res[0] = r0; res[1] = r1; res[2] = r2; res[3] = r3; res[4] = r4; res[5] = r5;
+}
+
+// :417-447
+template <class R, class I, class M, class D>
+MJH_HD void inertCom(R res, I inert, M mat, D dif, double mass) {
+  double tmp[9] = {mat[0]*inert[0], mat[3]*inert[0], mat[6]*inert[0],
+                   mat[1]*inert[1], mat[4]*inert[1], mat[7]*inert[1],
+                   mat[2]*inert[2], mat[5]*inert[2], mat[8]*inert[2]};
+  double r0 = mat[0]*tmp[0] + mat[1]*tmp[3] + mat[2]*tmp[6];
+  double r1 = mat[3]*tmp[1] + mat[4]*tmp[4] + mat[5]*tmp[7];
+  double r2 = mat[6]*tmp[2] + mat[7]*tmp[5] + mat[8]*tmp[8];
+  double r3 = mat[0]*tmp[1] + mat[1]*tmp[4] + mat[2]*tmp[7];
+  double r4 = mat[0]*tmp[2] + mat[1]*tmp[5] + mat[2]*tmp[8];
+  double r5 = mat[3]*tmp[2] + mat[4]*tmp[5] + mat[5]*tmp[8];
+  r0 += mass*(dif[1]*dif[1] + dif[2]*dif[2]);
+  r1 += mass*(dif[0]*dif[0] + dif[2]*dif[2]);
+  r2 += mass*(dif[0]*dif[0] + dif[1]*dif[1]);
+  r3 -= mass*dif[0]*dif[1];
+  r4 -= mass*dif[0]*dif[2];
+  r5 -= mass*dif[1]*dif[2];
+  res[0] = r0; res[1] = r1; res[2] = r2; res[3] = r3; res[4] = r4; res[5] = r5;
+  res[6] = mass*dif[0];
+  res[7] = mass*dif[1];
+  res[8] = mass*dif[2];
+  res[9] = mass;
+}
+
+// :452-459
+template <class R, class I, class V> MJH_HD void mulInertVec(R res, I i, V v) {
+  double r0 = i[0]*v[0] + i[3]*v[1] + i[4]*v[2] - i[8]*v[4] + i[7]*v[5];
+  double r1 = i[3]*v[0] + i[1]*v[1] + i[5]*v[2] + i[8]*v[3] - i[6]*v[5];
+  double r2 = i[4]*v[0] + i[5]*v[1] + i[2]*v[2] - i[7]*v[3] + i[6]*v[4];
+  double r3 = i[8]*v[1] - i[7]*v[2] + i[9]*v[3];
+  double r4 = i[6]*v[2] - i[8]*v[0] + i[9]*v[4];
+  double r5 = i[7]*v[0] - i[6]*v[1] + i[9]*v[5];
+  res[0] = r0; res[1] = r1; res[2] = r2; res[3] = r3; res[4] = r4; res[5] = r5;
+}
+
+// :464-476 (hinge/ball: offset given)
+template <class R, class A, class O> MJH_HD void dofComHinge(R res, A axis, O offset) {
+  copy3(res, axis);
+  cross(res + 3, axis, offset);
+}
+
+// :481-489
+template <class R, class D, class V> MJH_HD void mulDofVec(R res, D dof, V vec, int n) {
+  if (n == 1) {
+    scl(res, dof, vec[0], 6);
+  } else if (n <= 0) {
+    zero(res, 6);
+  } else {
+    mulMatTVec(res, dof, vec, n, 6);
+  }
+}
+
+// mju_quatIntegrate :241-250
+template <class Q, class V> MJH_HD void quatIntegrate(Q quat, V vel, double scale) {
+  double tmp[3] = {vel[0], vel[1], vel[2]}, qrot[4];
+  double angle = scale * normalize3(tmp);
+  axisAngle2Quat(qrot, tmp, angle);
+  normalize4(quat);
+  mulQuat(quat, quat, qrot);
+}
+
+//---------------------------------- engine_support.c -----------------------------------------
+
+// mj_local2Global :1565-1606 (pos and quat both given)
+template <int S, class P, class Q>
+MJH_HD void local2Global(const Lane<S>& d, SP<S> xpos, SP<S> xmat, P pos, Q quat, int body,
+                         int sameframe) {
+  switch (sameframe) {
+  case mjhipSAMEFRAME_NONE:
+  case mjhipSAMEFRAME_BODYROT:
+  case mjhipSAMEFRAME_INERTIAROT:
+    mulMatVec3(xpos, d.xmat + 9*body, pos);
+    addTo3(xpos, d.xpos + 3*body);
+    break;
+  case mjhipSAMEFRAME_BODY:
+    copy3(xpos, d.xpos + 3*body);
+    break;
+  case mjhipSAMEFRAME_INERTIA:
+    copy3(xpos, d.xipos + 3*body);
+    break;
+  }
+  double tmp[4];
+  switch (sameframe) {
+  case mjhipSAMEFRAME_NONE:
+    mulQuat(tmp, d.xquat + 4*body, quat);
+    quat2Mat(xmat, tmp);
+    break;
+  case mjhipSAMEFRAME_BODY:
+  case mjhipSAMEFRAME_BODYROT:
+    copy(xmat, d.xmat + 9*body, 9);
+    break;
+  case mjhipSAMEFRAME_INERTIA:
+  case mjhipSAMEFRAME_INERTIAROT:
+    copy(xmat, d.ximat + 9*body, 9);
+    break;
+  }
+}
+
+// mj_jac :389-441 (dense), into d.jacp / d.jacr
+template <int S, class P>
+MJH_HD void jac(const mjhipModel& m, const Lane<S>& d, P point, int body) {
+  int nv = m.nv;
+  double offset[3];
+  zero(d.jacp, 3*nv);
+  zero(d.jacr, 3*nv);
+  sub3(offset, point, d.subtree_com + 3*m.body_rootid[body]);
+  while (body && !m.body_dofnum[body]) body = m.body_parentid[body];
+  if (!body) return;
+  int i = m.body_dofadr[body] + m.body_dofnum[body] - 1;
+  while (i >= 0) {
+    SP<S> cdof = d.cdof + 6*i;
+    d.jacr[i+0*nv] = cdof[0];
+    d.jacr[i+1*nv] = cdof[1];
+    d.jacr[i+2*nv] = cdof[2];
+    double tmp[3];
+    cross(tmp, cdof, offset);
+    d.jacp[i+0*nv] = cdof[3] + tmp[0];
+    d.jacp[i+1*nv] = cdof[4] + tmp[1];
+    d.jacp[i+2*nv] = cdof[5] + tmp[2];
+    i = m.dof_parentid[i];
+  }
+}
+
+// mj_applyFT :1194-1251 (dense), torque = 0 as used by gravcomp
+template <int S, class F, class P>
+MJH_HD void applyForce(const mjhipModel& m, const Lane<S>& d, F force, P point, int body,
+                       SP<S> qfrc_target) {
+  jac(m, d, point, body);
+  mulMatTVec(d.qforce, d.jacp, force, 3, m.nv);
+  addTo(qfrc_target, d.qforce, m.nv);
+  double zt[3] = {0, 0, 0};       // mj_gravcomp passes torque = {0, 0, 0}
+  mulMatTVec(d.qforce, d.jacr, zt, 3, m.nv);
+  addTo(qfrc_target, d.qforce, m.nv);
+}
+
+//---------------------------------- engine_core_smooth.c -------------------------------------
+
+// mj_kinematics :38-178
+template <int S>
+MJH_HD void kinematics(const mjhipModel& m, const Lane<S>& d) {
+  int nbody = m.nbody;
+  zero3(d.xpos);
+  d.xquat[0] = 1; d.xquat[1] = 0; d.xquat[2] = 0; d.xquat[3] = 0;
+  zero3(d.xipos);
+  zero(d.xmat, 9);
+  zero(d.ximat, 9);
+  d.xmat[0] = 1; d.xmat[4] = 1; d.xmat[8] = 1;
+  d.ximat[0] = 1; d.ximat[4] = 1; d.ximat[8] = 1;
+
+  for (int i = 1; i < nbody; i++) {
+    double xpos[3], xquat[4];
+    int jntadr = m.body_jntadr[i];
+    int jntnum = m.body_jntnum[i];
+    if (jntnum == 1 && m.jnt_type[jntadr] == mjhipJNT_FREE) {
+      int qadr = m.jnt_qposadr[jntadr];
+      copy3(xpos, d.qpos + qadr);
+      copy4(xquat, d.qpos + qadr + 3);
+      normalize4(xquat);
+      copy3(d.xanchor + 3*jntadr, xpos);
+      copy3(d.xaxis + 3*jntadr, m.jnt_axis + 3*jntadr);
+    } else {
+      int pid = m.body_parentid[i];
+      const double* bodypos = m.body_pos + 3*i;
+      const double* bodyquat = m.body_quat + 4*i;
+      if (pid) {
+        mulMatVec3(xpos, d.xmat + 9*pid, bodypos);
+        addTo3(xpos, d.xpos + 3*pid);
+        mulQuat(xquat, d.xquat + 4*pid, bodyquat);
+      } else {
+        copy3(xpos, bodypos);
+        copy4(xquat, bodyquat);
+      }
+      double xanchor[3], xaxis[3];
+      for (int j = 0; j < jntnum; j++) {
+        int jid = jntadr + j;
+        int qadr = m.jnt_qposadr[jid];
+        int jtype = m.jnt_type[jid];
+        rotVecQuat(xaxis, m.jnt_axis + 3*jid, xquat);
+        rotVecQuat(xanchor, m.jnt_pos + 3*jid, xquat);
+        addTo3(xanchor, xpos);
+        if (jtype == mjhipJNT_SLIDE) {
+          addToScl3(xpos, xaxis, d.qpos[qadr] - m.qpos0[qadr]);
+        } else {
+          double qloc[4];
+          if (jtype == mjhipJNT_BALL) {
+            copy4(qloc, d.qpos + qadr);
+            normalize4(qloc);
+          } else {
+            axisAngle2Quat(qloc, m.jnt_axis + 3*jid, d.qpos[qadr] - m.qpos0[qadr]);
+          }
+          mulQuat(xquat, xquat, qloc);
+          double vec[3];
+          rotVecQuat(vec, m.jnt_pos + 3*jid, xquat);
+          sub3(xpos, xanchor, vec);
+        }
+        copy3(d.xanchor + 3*jid, xanchor);
+        copy3(d.xaxis + 3*jid, xaxis);
+      }
+    }
+    normalize4(xquat);
+    copy4(d.xquat + 4*i, xquat);
+    copy3(d.xpos + 3*i, xpos);
+    quat2Mat(d.xmat + 9*i, xquat);
+  }
+  for (int i = 1; i < nbody; i++) {
+    local2Global(d, d.xipos + 3*i, d.ximat + 9*i, m.body_ipos + 3*i, m.body_iquat + 4*i, i,
+                 m.body_sameframe[i]);
+  }
+  for (int i = 0; i < m.ngeom; i++) {
+    local2Global(d, d.geom_xpos + 3*i, d.geom_xmat + 9*i, m.geom_pos + 3*i,
+                 m.geom_quat + 4*i, m.geom_bodyid[i], m.geom_sameframe[i]);
+  }
+  for (int i = 0; i < m.nsite; i++) {
+    local2Global(d, d.site_xpos + 3*i, d.site_xmat + 9*i, m.site_pos + 3*i,
+                 m.site_quat + 4*i, m.site_bodyid[i], m.site_sameframe[i]);
+  }
+}
+
+// mj_comPos :183-270
+template <int S>
+MJH_HD void comPos(const mjhipModel& m, const Lane<S>& d) {
+  int nbody = m.nbody, njnt = m.njnt;
+  double offset[3], axis[3];
+  SP<S> mass_subtree = d.mass_subtree;
+  zero(mass_subtree, nbody);
+  zero(d.subtree_com, nbody*3);
+  for (int i = nbody-1; i >= 0; i--) {
+    addToScl3(d.subtree_com + 3*i, d.xipos + 3*i, m.body_mass[i]);
+    mass_subtree[i] += m.body_mass[i];
+    if (i) {
+      int j = m.body_parentid[i];
+      addTo3(d.subtree_com + 3*j, d.subtree_com + 3*i);
+      mass_subtree[j] += mass_subtree[i];
+    }
+    if (mass_subtree[i] < MINVAL) {
+      copy3(d.subtree_com + 3*i, d.xipos + 3*i);
+    } else {
+      double ms = mass_subtree[i];
+      scl3(d.subtree_com + 3*i, d.subtree_com + 3*i, 1.0/(ms > MINVAL ? ms : MINVAL));
+    }
+  }
+  zero(d.cinert, 10);
+  for (int i = 1; i < nbody; i++) {
+    sub3(offset, d.xipos + 3*i, d.subtree_com + 3*m.body_rootid[i]);
+    inertCom(d.cinert + 10*i, m.body_inertia + 3*i, d.ximat + 9*i, offset, m.body_mass[i]);
+  }
+  for (int j = 0; j < njnt; j++) {
+    int da = 6*m.jnt_dofadr[j];
+    int bi = m.jnt_bodyid[j];
+    sub3(offset, d.subtree_com + 3*m.body_rootid[bi], d.xanchor + 3*j);
+    int skip = 0;
+    switch (m.jnt_type[j]) {
+    case mjhipJNT_FREE:
+      zero(d.cdof + da, 18);
+      for (int i = 0; i < 3; i++) d.cdof[da+3+7*i] = 1;
+      skip = 18;
+      // fallthrough
+    case mjhipJNT_BALL:
+      for (int i = 0; i < 3; i++) {
+        axis[0] = d.xmat[9*bi+i+0];
+        axis[1] = d.xmat[9*bi+i+3];
+        axis[2] = d.xmat[9*bi+i+6];
+        dofComHinge(d.cdof + da + skip + 6*i, axis, offset);
+      }
+      break;
+    case mjhipJNT_SLIDE:
+      zero3(d.cdof + da);
+      copy3(d.cdof + da + 3, d.xaxis + 3*j);
+      break;
+    case mjhipJNT_HINGE:
+      dofComHinge(d.cdof + da, d.xaxis + 3*j, offset);
+      break;
+    }
+  }
+}
+
+// mj_camlight :275-392
+template <int S>
+MJH_HD void camlight(const mjhipModel& m, const Lane<S>& d) {
+  double pos[3], matT[9];
+  for (int i = 0; i < m.ncam; i++) {
+    local2Global(d, d.cam_xpos + 3*i, d.cam_xmat + 9*i, m.cam_pos + 3*i, m.cam_quat + 4*i,
+                 m.cam_bodyid[i], 0);
+    int id = m.cam_bodyid[i];
+    int id1 = m.cam_targetbodyid[i];
+    switch (m.cam_mode[i]) {
+    case mjhipCAMLIGHT_TRACK:
+    case mjhipCAMLIGHT_TRACKCOM:
+      copy(d.cam_xmat + 9*i, m.cam_mat0 + 9*i, 9);
+      if (m.cam_mode[i] == mjhipCAMLIGHT_TRACK) {
+        add3(d.cam_xpos + 3*i, d.xpos + 3*id, m.cam_pos0 + 3*i);
+      } else {
+        add3(d.cam_xpos + 3*i, d.subtree_com + 3*id, m.cam_poscom0 + 3*i);
+      }
+      break;
+    case mjhipCAMLIGHT_TARGETBODY:
+    case mjhipCAMLIGHT_TARGETBODYCOM:
+      if (id1 >= 0) {
+        if (m.cam_mode[i] == mjhipCAMLIGHT_TARGETBODY) {
+          copy3(pos, d.xpos + 3*id1);
+        } else {
+          copy3(pos, d.subtree_com + 3*id1);
+        }
+        sub3(matT + 6, d.cam_xpos + 3*i, pos);
+        normalize3(matT + 6);
+        matT[3] = 0; matT[4] = 0; matT[5] = 1;
+        cross(matT, matT + 3, matT + 6);
+        normalize3(matT);
+        cross(matT + 3, matT + 6, matT);
+        normalize3(matT + 3);
+        for (int r = 0; r < 3; r++)
+          for (int c = 0; c < 3; c++) d.cam_xmat[9*i + 3*c + r] = matT[3*r + c];
+      }
+      break;
+    default:
+      break;
+    }
+  }
+  for (int i = 0; i < m.nlight; i++) {
+    int id = m.light_bodyid[i];
+    int id1 = m.light_targetbodyid[i];
+    // mj_local2Global with xmat = 0 (position only)
+    mulMatVec3(d.light_xpos + 3*i, d.xmat + 9*id, m.light_pos + 3*i);
+    addTo3(d.light_xpos + 3*i, d.xpos + 3*id);
+    rotVecQuat(d.light_xdir + 3*i, m.light_dir + 3*i, d.xquat + 4*id);
+    switch (m.light_mode[i]) {
+    case mjhipCAMLIGHT_TRACK:
+    case mjhipCAMLIGHT_TRACKCOM:
+      copy3(d.light_xdir + 3*i, m.light_dir0 + 3*i);
+      if (m.light_mode[i] == mjhipCAMLIGHT_TRACK) {
+        add3(d.light_xpos + 3*i, d.xpos + 3*id, m.light_pos0 + 3*i);
+      } else {
+        add3(d.light_xpos + 3*i, d.subtree_com + 3*id, m.light_poscom0 + 3*i);
+      }
+      break;
+    case mjhipCAMLIGHT_TARGETBODY:
+    case mjhipCAMLIGHT_TARGETBODYCOM:
+      if (id1 >= 0) {
+        if (m.light_mode[i] == mjhipCAMLIGHT_TARGETBODY) {
+          copy3(pos, d.xpos + 3*id1);
+        } else {
+          copy3(pos, d.subtree_com + 3*id1);
+        }
+        sub3(d.light_xdir + 3*i, pos, d.light_xpos + 3*i);
+      }
+      break;
+    default:
+      break;
+    }
+    normalize3(d.light_xdir + 3*i);
+  }
+}
+
+// mj_tendon :651-723 (fixed tendons, dense ten_J)
+template <int S>
+MJH_HD void tendon(const mjhipModel& m, const Lane<S>& d) {
+  int nv = m.nv, nten = m.ntendon;
+  if (!nten) return;
+  zero(d.ten_length, nten);
+  zero(d.ten_J, nten*nv);
+  for (int i = 0; i < nten; i++) {
+    int adr = m.tendon_adr[i];
+    int num = m.tendon_num[i];
+    for (int j = 0; j < num; j++) {
+      int k = m.wrap_objid[adr+j];
+      d.ten_length[i] += m.wrap_prm[adr+j] * d.qpos[m.jnt_qposadr[k]];
+      d.ten_J[i*nv + m.jnt_dofadr[k]] = m.wrap_prm[adr+j];
+    }
+  }
+}
+
+// mj_transmission :865-916 (joint transmission of slide/hinge joints)
+template <int S>
+MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d) {
+  for (int i = 0; i < m.nu; i++) {
+    int adr = m.moment_rowadr[i];
+    int id = m.actuator_trnid[2*i];
+    double g = m.actuator_gear[6*i];
+    d.actuator_length[i] = d.qpos[m.jnt_qposadr[id]]*g;
+    d.actuator_moment[adr] = g;
+  }
+}
+
+// mj_crb :1353-1401
+template <int S>
+MJH_HD void crb(const mjhipModel& m, const Lane<S>& d) {
+  double buf[6];
+  int nv = m.nv;
+  copy(d.crb, d.cinert, 10*m.nbody);
+  for (int i = m.nbody - 1; i > 0; i--) {
+    if (m.body_parentid[i] > 0) addTo(d.crb + 10*m.body_parentid[i], d.crb + 10*i, 10);
+  }
+  zero(d.qM, m.nM);
+  for (int i = 0; i < nv; i++) {
+    if (m.dof_simplenum[i]) {
+      int n = i + m.dof_simplenum[i];
+      for (; i < n; i++) d.qM[m.dof_Madr[i]] = m.dof_M0[i];
+      if (i == nv) break;
+    }
+    int Madr_ij = m.dof_Madr[i];
+    d.qM[Madr_ij] = m.dof_armature[i];
+    mulInertVec(buf, d.crb + 10*m.dof_bodyid[i], d.cdof + 6*i);
+    for (int j = i; j >= 0; j = m.dof_parentid[j]) {
+      d.qM[Madr_ij++] += dot6(d.cdof + 6*j, buf);
+    }
+  }
+}
+
+// mj_factorM / mj_factorI :1470-1511
+template <int S>
+MJH_HD void factorM(const mjhipModel& m, const Lane<S>& d) {
+  for (int i = 0; i < m.nC; i++) d.qLD[i] = d.qM[m.mapM2C[i]];
+  SP<S> mat = d.qLD;
+  const int *rownnz = m.C_rownnz, *rowadr = m.C_rowadr, *colind = m.C_colind;
+  for (int k = m.nv-1; k >= 0; k--) {
+    int rowadr_k = rowadr[k];
+    int diag_k = rowadr_k + rownnz[k] - 1;
+    double invD = 1 / mat[diag_k];
+    d.qLDiagInv[k] = invD;
+    if (m.dof_simplenum[k]) continue;
+    for (int adr = diag_k - 1; adr >= rowadr_k; adr--) {
+      double tmp = mat[adr] * invD;
+      int i = colind[adr];
+      addToScl(mat + rowadr[i], mat + rowadr_k, -tmp, rownnz[i]);
+      mat[adr] = tmp;
+    }
+  }
+}
+
+// mj_comVel :1833-1896
+template <int S>
+MJH_HD void comVel(const mjhipModel& m, const Lane<S>& d) {
+  zero(d.cvel, 6);
+  for (int i = 1; i < m.nbody; i++) {
+    int bda = m.body_dofadr[i];
+    double cvel[6];
+    copy(cvel, d.cvel + 6*m.body_parentid[i], 6);
+    int dofnum = m.body_dofnum[i];
+    for (int j = 0; j < dofnum; j++) {
+      double tmp[6];
+      switch (m.jnt_type[m.dof_jntid[bda + j]]) {
+      case mjhipJNT_FREE:
+        zero(d.cdof_dot + 6*bda, 18);
+        mulDofVec(tmp, d.cdof + 6*bda, d.qvel + bda, 3);
+        addTo(cvel, tmp, 6);
+        j += 3;
+        // fallthrough
+      case mjhipJNT_BALL:
+        for (int k = 0; k < 3; k++) {
+          crossMotion(d.cdof_dot + 6*(bda + j + k), cvel, d.cdof + 6*(bda + j + k));
+        }
+        mulDofVec(tmp, d.cdof + 6*(bda + j), d.qvel + bda + j, 3);
+        addTo(cvel, tmp, 6);
+        j += 2;
+        break;
+      default:
+        crossMotion(d.cdof_dot + 6*(bda + j), cvel, d.cdof + 6*(bda + j));
+        mulDofVec(tmp, d.cdof + 6*(bda + j), d.qvel + bda + j, 1);
+        addTo(cvel, tmp, 6);
+      }
+    }
+    copy(d.cvel + 6*i, cvel, 6);
+  }
+}
+
+// mj_rne :1969-2023 (result = null: only the mirror's scratch)
+template <int S>
+MJH_HD void rne(const mjhipModel& m, const Lane<S>& d, int flg_acc, SP<S> result) {
+  int nbody = m.nbody, nv = m.nv;
+  double tmp[6], tmp1[6];
+  SP<S> cacc = d.cacc, cfrc = d.cfrc;
+  zero(cacc, 6);
+  if (!(m.opt.disableflags & mjhipDSBL_GRAVITY)) scl3(cacc + 3, m.opt.gravity, -1);
+  for (int i = 1; i < nbody; i++) {
+    int bda = m.body_dofadr[i];
+    mulDofVec(tmp, d.cdof_dot + 6*bda, d.qvel + bda, m.body_dofnum[i]);
+    add(cacc + 6*i, cacc + 6*m.body_parentid[i], tmp, 6);
+    if (flg_acc) {
+      mulDofVec(tmp, d.cdof + 6*bda, d.qacc + bda, m.body_dofnum[i]);
+      addTo(cacc + 6*i, tmp, 6);
+    }
+    mulInertVec(cfrc + 6*i, d.cinert + 10*i, cacc + 6*i);
+    mulInertVec(tmp, d.cinert + 10*i, d.cvel + 6*i);
+    crossForce(tmp1, d.cvel + 6*i, tmp);
+    addTo(cfrc + 6*i, tmp1, 6);
+  }
+  zero(cfrc, 6);
+  for (int i = nbody - 1; i > 0; i--) {
+    if (m.body_parentid[i]) addTo(cfrc + 6*m.body_parentid[i], cfrc + 6*i, 6);
+  }
+  for (int i = 0; i < nv; i++) {
+    result[i] = dot6(d.cdof + 6*i, cfrc + 6*m.dof_bodyid[i]);
+  }
+}
+
+//---------------------------------- engine_passive.c -----------------------------------------
+
+// mj_passive :436-493 with mj_springdamper :57-378 and mj_gravcomp :381-399
+template <int S>
+MJH_HD void passive(const mjhipModel& m, const Lane<S>& d) {
+  int nv = m.nv;
+  zero(d.qfrc_spring, nv);
+  zero(d.qfrc_damper, nv);
+  zero(d.qfrc_gravcomp, nv);
+  zero(d.qfrc_fluid, nv);
+  zero(d.qfrc_passive, nv);
+  if (m.opt.disableflags & mjhipDSBL_PASSIVE) return;
+  for (int i = 0; i < m.njnt; i++) {
+    double stiffness = m.jnt_stiffness[i];
+    if (stiffness == 0) continue;
+    int padr = m.jnt_qposadr[i];
+    int dadr = m.jnt_dofadr[i];
+    switch (m.jnt_type[i]) {
+    case mjhipJNT_FREE:
+      d.qfrc_spring[dadr+0] = -stiffness*(d.qpos[padr+0] - m.qpos_spring[padr+0]);
+      d.qfrc_spring[dadr+1] = -stiffness*(d.qpos[padr+1] - m.qpos_spring[padr+1]);
+      d.qfrc_spring[dadr+2] = -stiffness*(d.qpos[padr+2] - m.qpos_spring[padr+2]);
+      dadr += 3;
+      padr += 3;
+      // fallthrough
+    case mjhipJNT_BALL:
+      {
+        double dif[3], quat[4];
+        copy4(quat, d.qpos + padr);
+        normalize4(quat);
+        subQuat(dif, quat, m.qpos_spring + padr);
+        d.qfrc_spring[dadr+0] = -stiffness*dif[0];
+        d.qfrc_spring[dadr+1] = -stiffness*dif[1];
+        d.qfrc_spring[dadr+2] = -stiffness*dif[2];
+      }
+      break;
+    default:
+      d.qfrc_spring[dadr] = -stiffness*(d.qpos[padr] - m.qpos_spring[padr]);
+      break;
+    }
+  }
+  for (int i = 0; i < nv; i++) {
+    double damping = m.dof_damping[i];
+    if (damping != 0) d.qfrc_damper[i] = -damping*d.qvel[i];
+  }
+  for (int i = 0; i < m.ntendon; i++) {
+    double stiffness = m.tendon_stiffness[i];
+    double damping = m.tendon_damping[i];
+    if (stiffness == 0 && damping == 0) continue;
+    double length = d.ten_length[i];
+    double lower = m.tendon_lengthspring[2*i];
+    double upper = m.tendon_lengthspring[2*i+1];
+    double frc_spring = 0;
+    if (length > upper) {
+      frc_spring = stiffness * (upper - length);
+    } else if (length < lower) {
+      frc_spring = stiffness * (lower - length);
+    }
+    double frc_damper = -damping * d.ten_velocity[i];
+    if (frc_spring) addToScl(d.qfrc_spring, d.ten_J + i*nv, frc_spring, nv);
+    if (frc_damper) addToScl(d.qfrc_damper, d.ten_J + i*nv, frc_damper, nv);
+  }
+  int has_gravcomp = 0;
+  const double* g = m.opt.gravity;
+  if (m.ngravcomp && !(m.opt.disableflags & mjhipDSBL_GRAVITY) &&
+      sqrt(g[0]*g[0] + g[1]*g[1] + g[2]*g[2]) != 0) {
+    for (int i = 1; i < m.nbody; i++) {
+      if (m.body_gravcomp[i]) {
+        has_gravcomp = 1;
+        double force[3];
+        scl3(force, g, -(m.body_mass[i]*m.body_gravcomp[i]));
+        applyForce(m, d, force, d.xipos + 3*i, i, d.qfrc_gravcomp);
+      }
+    }
+  }
+  add(d.qfrc_passive, d.qfrc_spring, d.qfrc_damper, nv);
+  if (has_gravcomp) {
+    for (int i = 0; i < m.njnt; i++) {
+      if (m.jnt_actgravcomp[i]) continue;
+      int t = m.jnt_type[i];
+      int dofnum = t == mjhipJNT_FREE ? 6 : (t == mjhipJNT_BALL ? 3 : 1);
+      int dofadr = m.jnt_dofadr[i];
+      for (int j = 0; j < dofnum; j++) d.qfrc_passive[dofadr+j] += d.qfrc_gravcomp[dofadr+j];
+    }
+  }
+}
+
+//---------------------------------- engine_core_constraint.c ---------------------------------
+
+// mj_addConstraint :265-356 (dense, size 1); jac is a strided row of d.jacp
+template <int S>
+MJH_HD void addConstraint(const mjhipModel& m, const Lane<S>& d, SP<S> jacrow, double pos,
+                          double margin, double frictionloss, int type, int id, int* status) {
+  int nv = m.nv;
+  int nefc = d.efc_count[0];
+  int empty = 1;
+  for (int i = 0; i < nv; i++) {
+    if (jacrow[i]) {
+      empty = 0;
+      break;
+    }
+  }
+  if (empty) return;
+  if (nefc >= d.efc_cap) {         // mjWARN_CNSTRFULL analogue: capacity exceeded
+    *status |= MJHIP_INST_CNSTRFULL;
+    return;
+  }
+  copy(d.efc_J + nefc*nv, jacrow, nv);
+  d.efc_pos[nefc] = pos;
+  d.efc_margin[nefc] = margin;
+  d.efc_frictionloss[nefc] = frictionloss;
+  d.efc_type[nefc] = type;
+  d.efc_id[nefc] = id;
+  d.efc_count[0] = nefc + 1;
+  if (type == CNSTR_FRICTION_DOF || type == CNSTR_FRICTION_TENDON) {
+    d.efc_count[2] = d.efc_count[2] + 1;
+  } else if (type == CNSTR_LIMIT_JOINT || type == CNSTR_LIMIT_TENDON) {
+    d.efc_count[3] = d.efc_count[3] + 1;
+  }
+}
+
+MJH_HD double dmax(double a, double b) { return a > b ? a : b; }
+MJH_HD double dmin(double a, double b) { return a < b ? a : b; }
+
+// getimpedance :1425-1480
+MJH_HD void getimpedance(const double* solimp, double pos, double margin, double* imp,
+                         double* impP) {
+  if (solimp[0] == solimp[1] || solimp[2] <= MINVAL) {
+    *imp = 0.5*(solimp[0] + solimp[1]);
+    *impP = 0;
+    return;
+  }
+  double x = (pos-margin) / solimp[2];
+  double sgn = 1;
+  if (x < 0) {
+    x = -x;
+    sgn = -1;
+  }
+  if (x >= 1 || x <= 0) {
+    *imp = (x >= 1 ? solimp[1] : solimp[0]);
+    *impP = 0;
+    return;
+  }
+  double y, yP;
+  double p = solimp[4];
+  auto power = [](double a, double b) { return b == 1 ? a : (b == 2 ? a*a : pow(a, b)); };
+  if (p == 1) {
+    y = x;
+    yP = 1;
+  } else if (x <= solimp[3]) {
+    double a = 1/power(solimp[3], p-1);
+    y = a*power(x, p);
+    yP = p * a*power(x, p-1);
+  } else {
+    double b = 1/power(1-solimp[3], p-1);
+    y = 1-b*power(1-x, p);
+    yP = p * b*power(1-x, p-1);
+  }
+  *imp = solimp[0] + y*(solimp[1]-solimp[0]);
+  *impP = yP * sgn * (solimp[1]-solimp[0]) / solimp[2];
+}
+
+// mj_makeConstraint :2005-2116 with mj_instantiateFriction (dof), mj_instantiateLimit
+// :824-959 (dense), mj_diagApprox :1138-1311 and mj_makeImpedance :1494-1608 (dim-1 rows)
+template <int S>
+MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
+  int nv = m.nv;
+  d.efc_count[0] = 0; d.efc_count[1] = 0; d.efc_count[2] = 0; d.efc_count[3] = 0;
+  int dsbl = m.opt.disableflags;
+  if (dsbl & mjhipDSBL_CONSTRAINT) return;
+  SP<S> jacrow = d.jacp;       // one dense row of scratch
+  if (!(dsbl & mjhipDSBL_FRICTIONLOSS)) {
+    for (int i = 0; i < nv; i++) {
+      if (m.dof_frictionloss[i] > 0) {
+        zero(jacrow, nv);
+        jacrow[i] = 1;
+        addConstraint(m, d, jacrow, 0, 0, m.dof_frictionloss[i], CNSTR_FRICTION_DOF, i, status);
+      }
+    }
+  }
+  if (!(dsbl & mjhipDSBL_LIMIT)) {
+    for (int i = 0; i < m.njnt; i++) {
+      if (!m.jnt_limited[i]) continue;
+      double margin = m.jnt_margin[i];
+      int t = m.jnt_type[i];
+      if (t == mjhipJNT_SLIDE || t == mjhipJNT_HINGE) {
+        double value = d.qpos[m.jnt_qposadr[i]];
+        for (int side = -1; side <= 1; side += 2) {
+          double dist = side * (m.jnt_range[2*i+(side+1)/2] - value);
+          if (dist < margin) {
+            zero(jacrow, nv);
+            jacrow[m.jnt_dofadr[i]] = -(double)side;
+            addConstraint(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status);
+          }
+        }
+      } else if (t == mjhipJNT_BALL) {
+        int adr = m.jnt_qposadr[i];
+        double quat[4] = {d.qpos[adr], d.qpos[adr+1], d.qpos[adr+2], d.qpos[adr+3]};
+        double angleAxis[3];
+        normalize4(quat);
+        quat2Vel(angleAxis, quat, 1);
+        double value = normalize3(angleAxis);
+        double dist = dmax(m.jnt_range[2*i], m.jnt_range[2*i+1]) - value;
+        if (dist < margin) {
+          zero(jacrow, nv);
+          scl3(jacrow + m.jnt_dofadr[i], angleAxis, -1);
+          addConstraint(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status);
+        }
+      }
+    }
+    for (int i = 0; i < m.ntendon; i++) {
+      if (!m.tendon_limited[i]) continue;
+      double value = d.ten_length[i];
+      double margin = m.tendon_margin[i];
+      for (int side = -1; side <= 1; side += 2) {
+        double dist = side * (m.tendon_range[2*i+(side+1)/2] - value);
+        if (dist < margin) {
+          scl(jacrow, d.ten_J + i*nv, -side, nv);
+          addConstraint(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_TENDON, i, status);
+        }
+      }
+    }
+  }
+  int nefc = d.efc_count[0];
+  for (int i = 0; i < nefc; i++) {
+    int id = d.efc_id[i];
+    int tp = d.efc_type[i];
+    // mj_diagApprox
+    double dA = tp == CNSTR_FRICTION_DOF ? m.dof_invweight0[id] :
+                (tp == CNSTR_LIMIT_JOINT ? m.dof_invweight0[m.jnt_dofadr[id]] :
+                 m.tendon_invweight0[id]);
+    // getsolparam :1316-1371
+    double solref[2], solimp[5];
+    const double* sr = tp == CNSTR_LIMIT_JOINT ? m.jnt_solref + 2*id :
+                       (tp == CNSTR_FRICTION_DOF ? m.dof_solref + 2*id :
+                        m.tendon_solref_lim + 2*id);
+    const double* si = tp == CNSTR_LIMIT_JOINT ? m.jnt_solimp + 5*id :
+                       (tp == CNSTR_FRICTION_DOF ? m.dof_solimp + 5*id :
+                        m.tendon_solimp_lim + 5*id);
+    solref[0] = sr[0]; solref[1] = sr[1];
+    for (int k = 0; k < 5; k++) solimp[k] = si[k];
+    if ((solref[0] > 0) ^ (solref[1] > 0)) {
+      solref[0] = 0.02;
+      solref[1] = 1;
+    }
+    if (!(dsbl & mjhipDSBL_REFSAFE) && solref[0] > 0) {
+      solref[0] = dmax(solref[0], 2*m.opt.timestep);
+    }
+    solimp[0] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[0]));
+    solimp[1] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[1]));
+    solimp[2] = dmax(0, solimp[2]);
+    solimp[3] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[3]));
+    solimp[4] = dmax(1, solimp[4]);
+    double imp, impP;
+    getimpedance(solimp, d.efc_pos[i], d.efc_margin[i], &imp, &impP);
+    double R = dmax(MINVAL, (1-imp)*dA/imp);
+    double K, Bc;
+    if (tp == CNSTR_FRICTION_DOF || tp == CNSTR_FRICTION_TENDON) {
+      K = 0;
+    } else if (solref[0] > 0) {
+      K = 1 / dmax(MINVAL, solimp[1]*solimp[1] * solref[0]*solref[0] * solref[1]*solref[1]);
+    } else {
+      K = -solref[0] / dmax(MINVAL, solimp[1]*solimp[1]);
+    }
+    if (solref[1] > 0) {
+      Bc = 2 / dmax(MINVAL, solimp[1]*solref[0]);
+    } else {
+      Bc = -solref[1] / dmax(MINVAL, solimp[1]);
+    }
+    d.efc_R[i] = R;
+    d.efc_KBIP[4*i] = K;
+    d.efc_KBIP[4*i+1] = Bc;
+    d.efc_KBIP[4*i+2] = imp;
+    d.efc_KBIP[4*i+3] = impP;
+    d.efc_D[i] = 1 / R;
+    d.efc_diagApprox[i] = R * imp / (1-imp);
+  }
+}
+
+// mj_referenceConstraint :2362-2375 (dense mju_mulMatVec for efc_vel)
+template <int S>
+MJH_HD void referenceConstraint(const mjhipModel& m, const Lane<S>& d) {
+  int nefc = d.efc_count[0];
+  for (int i = 0; i < nefc; i++) {
+    d.efc_vel[i] = dot(d.efc_J + i*m.nv, d.qvel, m.nv);
+    d.efc_aref[i] = -d.efc_KBIP[4*i+1]*d.efc_vel[i]
+                    -d.efc_KBIP[4*i]*d.efc_KBIP[4*i+2]*(d.efc_pos[i]-d.efc_margin[i]);
+  }
+}
+
+// mj_invConstraint engine_inverse.c:169-192 with mj_constraintUpdate_island :2387-2549
+// (island < 0, no cost; the fork leaves the elliptic-cone branch empty)
+template <int S>
+MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
+  int nv = m.nv, nefc = d.efc_count[0];
+  if (!nefc) {
+    zero(d.qfrc_constraint, nv);
+    return;
+  }
+  int ne = d.efc_count[1], nf = d.efc_count[2];
+  for (int i = 0; i < nefc; i++) {
+    d.jar[i] = dot(d.efc_J + i*nv, d.qacc, nv) - d.efc_aref[i];
+  }
+  for (int i = 0; i < nefc; i++) d.efc_force[i] = -d.efc_D[i] * d.jar[i];
+  for (int i = 0; i < nefc; i++) {
+    double jr = d.jar[i];
+    if (i < ne) {
+      d.efc_state[i] = CNSTRSTATE_QUADRATIC;
+    } else if (i < ne + nf) {
+      double Rf = d.efc_R[i] * d.efc_frictionloss[i];
+      if (jr <= -Rf) {
+        d.efc_force[i] = d.efc_frictionloss[i];
+        d.efc_state[i] = CNSTRSTATE_LINEARNEG;
+      } else if (jr >= Rf) {
+        d.efc_force[i] = -d.efc_frictionloss[i];
+        d.efc_state[i] = CNSTRSTATE_LINEARPOS;
+      } else {
+        d.efc_state[i] = CNSTRSTATE_QUADRATIC;
+      }
+    } else if (d.efc_type[i] != CNSTR_CONTACT_ELLIPTIC) {
+      if (jr >= 0) {
+        d.efc_force[i] = 0;
+        d.efc_state[i] = CNSTRSTATE_SATISFIED;
+      } else {
+        d.efc_state[i] = CNSTRSTATE_QUADRATIC;
+      }
+    }
+  }
+  mulMatTVec(d.qfrc_constraint, d.efc_J, d.efc_force, nefc, nv);
+}
+
+//---------------------------------- engine_inverse.c -----------------------------------------
+
+// mj_invPosition :37-68 (mj_flex: no flexes; mj_collision: no contacts in this subset)
+template <int S>
+MJH_HD void invPosition(const mjhipModel& m, const Lane<S>& d, int* status) {
+  kinematics(m, d);
+  comPos(m, d);
+  camlight(m, d);
+  tendon(m, d);
+  crb(m, d);
+  factorM(m, d);
+  makeConstraint(m, d, status);
+  transmission(m, d);
+}
+
+// mj_invVelocity :73-76 -> mj_fwdVelocity engine_forward.c:193-231
+template <int S>
+MJH_HD void invVelocity(const mjhipModel& m, const Lane<S>& d) {
+  int nv = m.nv;
+  for (int r = 0; r < m.ntendon; r++) d.ten_velocity[r] = dot(d.ten_J + r*nv, d.qvel, nv);
+  if (!(m.opt.disableflags & mjhipDSBL_ACTUATION)) {
+    for (int r = 0; r < m.nu; r++) {
+      int adr = m.moment_rowadr[r];
+      d.actuator_velocity[r] = dotSparse(d.actuator_moment + adr, d.qvel, m.moment_rownnz[r],
+                                         m.moment_colind + adr);
+    }
+  }
+  comVel(m, d);
+  passive(m, d);
+  referenceConstraint(m, d);
+  rne(m, d, 0, d.qfrc_bias);
+}
+
+// mj_inverseSkip :197-261 (sensors/energy: none in this subset)
+template <int S>
+MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
+  int status = 0;
+  if (skipstage < mjhipSTAGE_POS) invPosition(m, d, &status);
+  if (skipstage < mjhipSTAGE_VEL) invVelocity(m, d);
+  invConstraint(m, d);
+  rne(m, d, 1, d.qfrc_inverse);
+  for (int i = 0; i < m.nv; i++) {
+    d.qfrc_inverse[i] += m.dof_armature[i] * d.qacc[i]
+                         - d.qfrc_passive[i] - d.qfrc_constraint[i];
+  }
+  return status;
+}
+
+}  // namespace mjh
+
+#endif  // MJHIP_ENGINE_DEVICE_H_

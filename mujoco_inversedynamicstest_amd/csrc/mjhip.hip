@@ -1,0 +1,803 @@
+// mjhip.hip — libmjhip.so: HIP kernels for gfx950 + the C-ABI of include/mjhip.h.
+//
+// Device layout (DESIGN.md §Data layout):
+//   * model: every mjhipModel array copied once into one device buffer; a device-side
+//     mjhipModel (same struct, device pointers) is passed by value as a kernel argument, so
+//     model reads are wave-uniform scalar loads.
+//   * mirror: every per-instance field F of S doubles is F[(blk*S + k)*64 + lane] — 64-
+//     instance blocks = one wavefront; a wavefront's access to component k is one 512-byte
+//     contiguous segment (fully coalesced), and a block's whole field is contiguous.
+//   * one lane per instance (north star), blockDim = 64, grid = ceil(B/64).
+#include <hip/hip_runtime.h>
+
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "engine_device.h"
+
+using mjh::Lane;
+using mjh::SP;
+
+//==================================== device mirror =========================================
+
+struct Mirror {
+#define XD(name, d0, d1, stage) double* name; int name##_n;
+  MJHIP_DATA_FIELDS
+#undef XD
+#define XSC(name, n) double* name; int name##_n;
+  MJHIP_SCRATCH_FIELDS
+#undef XSC
+#define XSI(name, n) int* name; int name##_n;
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+  int efc_cap;
+};
+
+__device__ __forceinline__ Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
+  Lane<64> d;
+#define XD(name, d0, d1, stage) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
+  MJHIP_DATA_FIELDS
+#undef XD
+#define XSC(name, n) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
+  MJHIP_SCRATCH_FIELDS
+#undef XSC
+#define XSI(name, n) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+  d.efc_cap = mr.efc_cap;
+  return d;
+}
+
+//==================================== kernels ===============================================
+
+// Fused mj_inverseSkip over a batch. Optional row-major (instance-major) inputs are copied
+// into the mirror first; optional row-major qfrc_inverse output is written at the end.
+template <int SKIP>
+__global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
+                                                const double* __restrict__ qpos_in,
+                                                const double* __restrict__ qvel_in,
+                                                const double* __restrict__ qacc_in,
+                                                double* __restrict__ qfrc_out,
+                                                int* __restrict__ status) {
+  const int blk = blockIdx.x, lane = threadIdx.x;
+  const long inst = (long)blk*64 + lane;
+  if (inst >= B) return;
+  Lane<64> d = lane_view(mr, blk, lane);
+  if (qpos_in) {
+    for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos_in[inst*m.nq + k];
+  }
+  if (qvel_in) {
+    for (int k = 0; k < m.nv; k++) d.qvel[k] = qvel_in[inst*m.nv + k];
+  }
+  if (qacc_in) {
+    for (int k = 0; k < m.nv; k++) d.qacc[k] = qacc_in[inst*m.nv + k];
+  }
+  int st = mjh::inverseSkip(m, d, SKIP);
+  if (qfrc_out) {
+    for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
+  }
+  if (status) status[inst] = st;
+}
+
+// row-major (B x n) <-> mirror block layout
+__global__ void k_to_mirror(const double* __restrict__ src, double* __restrict__ dst, int B,
+                            int n) {
+  long t = (long)blockIdx.x*blockDim.x + threadIdx.x;
+  if (t >= (long)B*n) return;
+  long inst = t / n, k = t % n;
+  dst[((inst >> 6)*n + k)*64 + (inst & 63)] = src[t];
+}
+
+__global__ void k_from_mirror(const double* __restrict__ src, double* __restrict__ dst, int B,
+                              int n) {
+  long t = (long)blockIdx.x*blockDim.x + threadIdx.x;
+  if (t >= (long)B*n) return;
+  long inst = t / n, k = t % n;
+  dst[t] = src[((inst >> 6)*n + k)*64 + (inst & 63)];
+}
+
+// mjd_inverseFD expansion (engine_derivative_fd.c:611-719): base state b and perturbation
+// p (0 = centre, 1..nv = qacc_i + eps, nv+1..2nv = qvel_i + eps, 2nv+1..3nv = qpos
+// integrated along e_i by eps). Instances are base-major: inst = b*(3nv+1) + p.
+__global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __restrict__ qpos,
+                            const double* __restrict__ qvel, const double* __restrict__ qacc,
+                            double eps, int devptr_rowmajor) {
+  const int P = 3*m.nv + 1;
+  long inst = (long)blockIdx.x*blockDim.x + threadIdx.x;
+  if (inst >= (long)nbase*P) return;
+  long b = inst / P;
+  int p = (int)(inst % P);
+  Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
+  for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos[b*m.nq + k];
+  for (int k = 0; k < m.nv; k++) d.qvel[k] = qvel[b*m.nv + k];
+  for (int k = 0; k < m.nv; k++) d.qacc[k] = qacc[b*m.nv + k];
+  (void)devptr_rowmajor;
+  int nv = m.nv;
+  if (p >= 1 && p <= nv) {
+    d.qacc[p-1] = d.qacc[p-1] + eps;
+  } else if (p > nv && p <= 2*nv) {
+    d.qvel[p-1-nv] = d.qvel[p-1-nv] + eps;
+  } else if (p > 2*nv) {
+    // mj_integratePos(m, qpos, e_i, eps), engine_support.c:1518-1550
+    int i = p - 1 - 2*nv;
+    for (int j = 0; j < m.njnt; j++) {
+      int padr = m.jnt_qposadr[j], vadr = m.jnt_dofadr[j];
+      int t = m.jnt_type[j];
+      if (t == mjhipJNT_FREE) {
+        for (int c = 0; c < 3; c++) d.qpos[padr+c] += eps * (vadr + c == i ? 1.0 : 0.0);
+        padr += 3;
+        vadr += 3;
+        t = mjhipJNT_BALL;
+      }
+      if (t == mjhipJNT_BALL) {
+        double vel[3] = {vadr == i ? 1.0 : 0.0, vadr + 1 == i ? 1.0 : 0.0,
+                         vadr + 2 == i ? 1.0 : 0.0};
+        mjh::quatIntegrate(d.qpos + padr, vel, eps);
+      } else {
+        d.qpos[padr] += eps * (vadr == i ? 1.0 : 0.0);
+      }
+    }
+  }
+}
+
+// diff(): DfD*[b][i][:] = (f(perturbed) - f(centre)) / eps  (engine_derivative_fd.c:48-53)
+__global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps,
+                          double* __restrict__ DfDq, double* __restrict__ DfDv,
+                          double* __restrict__ DfDa, double* __restrict__ DmDq) {
+  const int nv = m.nv, P = 3*nv + 1;
+  long t = (long)blockIdx.x*blockDim.x + threadIdx.x;   // one thread per (b, perturbation)
+  if (t >= (long)nbase*(P-1)) return;
+  long b = t / (P-1);
+  int p = (int)(t % (P-1)) + 1;
+  long ic = b*P, ip = b*P + p;
+  Lane<64> c = lane_view(mr, (int)(ic >> 6), (int)(ic & 63));
+  Lane<64> q = lane_view(mr, (int)(ip >> 6), (int)(ip & 63));
+  double inv_h = 1/eps;
+  double* out;
+  int i;
+  if (p <= nv) {
+    out = DfDa; i = p - 1;
+  } else if (p <= 2*nv) {
+    out = DfDv; i = p - 1 - nv;
+  } else {
+    out = DfDq; i = p - 1 - 2*nv;
+  }
+  if (out) {
+    for (int k = 0; k < nv; k++) {
+      out[(b*nv + i)*nv + k] = inv_h * (q.qfrc_inverse[k] - c.qfrc_inverse[k]);
+    }
+  }
+  if (DmDq && p > 2*nv) {
+    for (int k = 0; k < m.nM; k++) {
+      DmDq[(b*nv + i)*m.nM + k] = inv_h * (q.qM[k] - c.qM[k]);
+    }
+  }
+}
+
+//==================================== host side ==============================================
+
+static thread_local std::string g_last_error;
+static void (*g_error_cb)(const char*) = nullptr;
+
+static void set_error(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+}
+
+#define HIPCHECK(expr)                                                              \
+  do {                                                                              \
+    hipError_t _e = (expr);                                                         \
+    if (_e != hipSuccess) {                                                         \
+      set_error("%s failed: %s (%s:%d)", #expr, hipGetErrorString(_e), __FILE__,    \
+                __LINE__);                                                          \
+      return MJHIP_ERR_HIP;                                                         \
+    }                                                                               \
+  } while (0)
+
+struct mjhipContext_ {
+  int device = 0;
+  int capacity = 0;         // instances (multiple of 64)
+  int efc_cap = 0;
+  hipStream_t stream = nullptr;
+  bool own_stream = false;
+  mjhipModel hmodel{};      // host copy of sizes (pointers are host pointers of the caller)
+  mjhipModel dmodel{};      // device pointers
+  void* dmodel_buf = nullptr;
+  Mirror mirror{};
+  void* mirror_buf = nullptr;
+  size_t mirror_bytes = 0;
+  std::unordered_map<std::string, std::pair<double*, int>> fields;   // name -> (ptr, S)
+  // staging for row-major host transfers
+  double* stage = nullptr;
+  size_t stage_bytes = 0;
+  int* status = nullptr;
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+};
+
+static int efc_capacity(const mjhipModel* m) {
+  int n = 0;
+  for (int i = 0; i < m->njnt; i++) {
+    if (m->jnt_limited[i]) n += (m->jnt_type[i] == mjhipJNT_BALL) ? 1 : 2;
+  }
+  for (int i = 0; i < m->ntendon; i++) {
+    if (m->tendon_limited[i]) n += 2;
+  }
+  for (int i = 0; i < m->nv; i++) {
+    if (m->dof_frictionloss[i] > 0) n += 1;
+  }
+  return n;
+}
+
+// model features outside the device path: rejected at context creation (fail loudly)
+static const char* unsupported(const mjhipModel* m) {
+  if (m->opt.jacobian == mjhipJAC_SPARSE || (m->opt.jacobian == mjhipJAC_AUTO && m->nv >= 60)) {
+    return "sparse Jacobians (nv >= 60 or jacobian=sparse)";
+  }
+  if (m->nmocap) return "mocap bodies";
+  if (m->na) return "actuator activations";
+  if (m->opt.enableflags & mjhipENBL_INVDISCRETE) return "mjENBL_INVDISCRETE";
+  if (m->opt.density > 0 || m->opt.viscosity > 0) return "fluid forces";
+  for (int i = 0; i < m->ntendon; i++) {
+    if (m->tendon_num[i] && m->wrap_type[m->tendon_adr[i]] != mjhipWRAP_JOINT) {
+      return "spatial tendons";
+    }
+  }
+  for (int i = 0; i < m->nu; i++) {
+    int t = m->actuator_trntype[i];
+    if (t != mjhipTRN_JOINT && t != mjhipTRN_JOINTINPARENT) return "non-joint transmissions";
+    int j = m->actuator_trnid[2*i];
+    if (m->jnt_type[j] != mjhipJNT_HINGE && m->jnt_type[j] != mjhipJNT_SLIDE) {
+      return "ball/free joint transmissions";
+    }
+  }
+  if (!(m->opt.disableflags & mjhipDSBL_CONTACT) && !(m->opt.disableflags & mjhipDSBL_CONSTRAINT)) {
+    // contacts are evaluated only if some geom pair can collide: the engine does not run
+    // collision detection yet, so models with collidable geoms must disable contacts
+    for (int i = 0; i < m->ngeom; i++) {
+      if (m->geom_contype[i] || m->geom_conaffinity[i]) {
+        return "contacts (set opt.disableflags |= mjDSBL_CONTACT; collision is next)";
+      }
+    }
+  }
+  return nullptr;
+}
+
+static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+extern "C" {
+
+MJHIP_API const char* mjhip_version(void) { return "mjhip 0.1 (gfx950)"; }
+
+MJHIP_API const char* mjhip_lastError(void) { return g_last_error.c_str(); }
+
+MJHIP_API void mjhip_setErrorCallback(void (*cb)(const char* msg)) { g_error_cb = cb; }
+
+MJHIP_API int mjhip_deviceCount(void) {
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+  return n;
+}
+
+MJHIP_API int mjhip_fieldSize(const mjhipModel* m, const char* name) {
+#define MJ_M(n) m->n
+#define XD(nm, d0, d1, stage) if (!strcmp(name, #nm)) return (m->d0) * (d1);
+  MJHIP_DATA_FIELDS
+#undef XD
+#undef MJ_M
+  return -1;
+}
+
+MJHIP_API int mjhip_outputDoubles(const mjhipModel* m) {
+  int w = 0;
+#define MJ_M(n) m->n
+#define XD(nm, d0, d1, stage) if (stage > 0) w += (m->d0) * (d1);
+  MJHIP_DATA_FIELDS
+#undef XD
+#undef MJ_M
+  return w;
+}
+
+MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
+                                  mjhipContext** out) {
+  if (!m || !out || capacity <= 0) {
+    set_error("mjhip_contextCreate: bad argument");
+    return MJHIP_ERR_ARG;
+  }
+  *out = nullptr;
+  int ndev = mjhip_deviceCount();
+  if (ndev <= 0) {
+    set_error("no HIP device available (the engine has no CPU fallback)");
+    return MJHIP_ERR_NO_DEVICE;
+  }
+  if (device < 0 || device >= ndev) {
+    set_error("device %d out of range (%d devices)", device, ndev);
+    return MJHIP_ERR_ARG;
+  }
+  if (const char* why = unsupported(m)) {
+    set_error("model uses a feature the device path does not support: %s", why);
+    return MJHIP_ERR_MODEL;
+  }
+  HIPCHECK(hipSetDevice(device));
+  mjhipContext* c = new mjhipContext_();
+  c->device = device;
+  c->capacity = (capacity + 63) & ~63;
+  c->efc_cap = efc_capacity(m);
+  c->hmodel = *m;
+
+  // ---- model upload: one buffer, 256-byte aligned arrays
+  size_t total = 0;
+#define MJ_M(n) m->n
+#define X(type, name, d0, d1) total += align256(sizeof(type) * (size_t)(m->d0) * (d1));
+  MJHIP_MODEL_POINTERS
+#undef X
+  std::vector<char> hbuf(total > 0 ? total : 1, 0);
+  size_t off = 0;
+  c->dmodel = *m;
+  if (hipMalloc(&c->dmodel_buf, hbuf.size()) != hipSuccess) {
+    set_error("hipMalloc(model) failed");
+    delete c;
+    return MJHIP_ERR_HIP;
+  }
+#define X(type, name, d0, d1)                                                       \
+  {                                                                                 \
+    size_t nb = sizeof(type) * (size_t)(m->d0) * (d1);                              \
+    if (nb && m->name) memcpy(hbuf.data() + off, m->name, nb);                      \
+    c->dmodel.name = (type*)((char*)c->dmodel_buf + off);                           \
+    off += align256(nb);                                                            \
+  }
+  MJHIP_MODEL_POINTERS
+#undef X
+#undef MJ_M
+  if (hipMemcpy(c->dmodel_buf, hbuf.data(), hbuf.size(), hipMemcpyHostToDevice) != hipSuccess) {
+    set_error("model upload failed");
+    hipFree(c->dmodel_buf);
+    delete c;
+    return MJHIP_ERR_HIP;
+  }
+
+  // ---- mirror: per-instance fields in 64-instance blocks
+  const size_t nblk = c->capacity / 64;
+  size_t mb = 0;
+  const int nv = m->nv, nbody = m->nbody, efc_cap = c->efc_cap;
+  (void)nbody;
+#define MJ_M(n) m->n
+#define XD(name, d0, d1, stage) c->mirror.name##_n = (m->d0) * (d1); \
+  mb += align256(sizeof(double) * nblk * 64 * (size_t)c->mirror.name##_n);
+  MJHIP_DATA_FIELDS
+#undef XD
+#define XSC(name, n) { const int nbody = m->nbody; (void)nbody; c->mirror.name##_n = (n); \
+  mb += align256(sizeof(double) * nblk * 64 * (size_t)c->mirror.name##_n); }
+  MJHIP_SCRATCH_FIELDS
+#undef XSC
+#define XSI(name, n) { c->mirror.name##_n = (n); \
+  mb += align256(sizeof(int) * nblk * 64 * (size_t)c->mirror.name##_n); }
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+  (void)nv; (void)efc_cap;
+  c->mirror.efc_cap = c->efc_cap;
+  c->mirror_bytes = mb;
+  if (hipMalloc(&c->mirror_buf, mb) != hipSuccess) {
+    set_error("hipMalloc(mirror, %zu bytes) failed", mb);
+    hipFree(c->dmodel_buf);
+    delete c;
+    return MJHIP_ERR_HIP;
+  }
+  hipMemset(c->mirror_buf, 0, mb);
+  char* p = (char*)c->mirror_buf;
+#define XD(name, d0, d1, stage) c->mirror.name = (double*)p; \
+  c->fields[#name] = {c->mirror.name, c->mirror.name##_n}; \
+  p += align256(sizeof(double) * nblk * 64 * (size_t)c->mirror.name##_n);
+  MJHIP_DATA_FIELDS
+#undef XD
+#define XSC(name, n) c->mirror.name = (double*)p; \
+  c->fields[#name] = {c->mirror.name, c->mirror.name##_n}; \
+  p += align256(sizeof(double) * nblk * 64 * (size_t)c->mirror.name##_n);
+  MJHIP_SCRATCH_FIELDS
+#undef XSC
+#define XSI(name, n) c->mirror.name = (int*)p; \
+  p += align256(sizeof(int) * nblk * 64 * (size_t)c->mirror.name##_n);
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+#undef MJ_M
+  // staging: row-major qpos, qvel, qacc, qfrc for `capacity` instances
+  c->stage_bytes = sizeof(double) * (size_t)c->capacity * (m->nq + 3*(size_t)m->nv);
+  if (hipMalloc((void**)&c->stage, c->stage_bytes) != hipSuccess ||
+      hipMalloc((void**)&c->status, sizeof(int) * (size_t)c->capacity) != hipSuccess) {
+    set_error("hipMalloc(staging) failed");
+    return MJHIP_ERR_HIP;
+  }
+  HIPCHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  c->own_stream = true;
+  HIPCHECK(hipEventCreate(&c->ev0));
+  HIPCHECK(hipEventCreate(&c->ev1));
+  *out = c;
+  return MJHIP_OK;
+}
+
+MJHIP_API void mjhip_contextFree(mjhipContext* c) {
+  if (!c) return;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  hipFree(c->stage);
+  hipFree(c->status);
+  hipFree(c->mirror_buf);
+  hipFree(c->dmodel_buf);
+  delete c;
+}
+
+MJHIP_API int mjhip_contextCapacity(const mjhipContext* c) { return c ? c->capacity : 0; }
+
+MJHIP_API void* mjhip_contextStream(mjhipContext* c) { return c ? (void*)c->stream : nullptr; }
+
+MJHIP_API int mjhip_contextSetStream(mjhipContext* c, void* stream) {
+  if (!c) return MJHIP_ERR_ARG;
+  if (c->own_stream && c->stream) {
+    hipStreamSynchronize(c->stream);
+    hipStreamDestroy(c->stream);
+  }
+  c->stream = (hipStream_t)stream;
+  c->own_stream = false;
+  return MJHIP_OK;
+}
+
+static int launch_inverse(mjhipContext* c, int B, const double* qpos, const double* qvel,
+                          const double* qacc, double* qfrc, int skipstage, int* status) {
+  dim3 grid((B + 63) / 64), block(64);
+  switch (skipstage) {
+  case mjhipSTAGE_NONE:
+    hipLaunchKernelGGL(k_inverse<0>, grid, block, 0, c->stream, c->dmodel, c->mirror, B, qpos,
+                       qvel, qacc, qfrc, status);
+    break;
+  case mjhipSTAGE_POS:
+    hipLaunchKernelGGL(k_inverse<1>, grid, block, 0, c->stream, c->dmodel, c->mirror, B, qpos,
+                       qvel, qacc, qfrc, status);
+    break;
+  case mjhipSTAGE_VEL:
+    hipLaunchKernelGGL(k_inverse<2>, grid, block, 0, c->stream, c->dmodel, c->mirror, B, qpos,
+                       qvel, qacc, qfrc, status);
+    break;
+  default:
+    set_error("skipstage must be mjSTAGE_NONE, mjSTAGE_POS or mjSTAGE_VEL");
+    return MJHIP_ERR_ARG;
+  }
+  HIPCHECK(hipGetLastError());
+  return MJHIP_OK;
+}
+
+MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B, const mjtNum* qpos,
+                                 const mjtNum* qvel, const mjtNum* qacc, mjtNum* qfrc_inverse,
+                                 int skipstage, int skipsensor, int flags, int* status) {
+  (void)skipsensor;   // no sensors in the supported subset: skipsensor has no effect
+  if (!c || B < 0) {
+    set_error("mjhip_inverseBatch: bad argument");
+    return MJHIP_ERR_ARG;
+  }
+  if (B > c->capacity) {
+    set_error("batch %d exceeds context capacity %d", B, c->capacity);
+    return MJHIP_ERR_CAPACITY;
+  }
+  if (B == 0) return MJHIP_OK;
+  HIPCHECK(hipSetDevice(c->device));
+  const mjhipModel& m = c->hmodel;
+  const bool dev = flags & MJHIP_FLAG_DEVICE_PTRS;
+  const bool mirror_in = flags & MJHIP_FLAG_MIRROR_INPUT;
+  const double *dq = nullptr, *dv = nullptr, *da = nullptr;
+  double* dqfrc = nullptr;
+  double* sq = c->stage;
+  double* sv = sq + (size_t)c->capacity*m.nq;
+  double* sa = sv + (size_t)c->capacity*m.nv;
+  double* sf = sa + (size_t)c->capacity*m.nv;
+  if (!mirror_in) {
+    if (!qpos || !qvel || !qacc) {
+      set_error("mjhip_inverseBatch: qpos/qvel/qacc required without MJHIP_FLAG_MIRROR_INPUT");
+      return MJHIP_ERR_ARG;
+    }
+    if (dev) {
+      dq = qpos; dv = qvel; da = qacc;
+    } else {
+      HIPCHECK(hipMemcpyAsync(sq, qpos, sizeof(double)*(size_t)B*m.nq, hipMemcpyHostToDevice,
+                              c->stream));
+      HIPCHECK(hipMemcpyAsync(sv, qvel, sizeof(double)*(size_t)B*m.nv, hipMemcpyHostToDevice,
+                              c->stream));
+      HIPCHECK(hipMemcpyAsync(sa, qacc, sizeof(double)*(size_t)B*m.nv, hipMemcpyHostToDevice,
+                              c->stream));
+      dq = sq; dv = sv; da = sa;
+    }
+  }
+  if (qfrc_inverse) dqfrc = dev ? qfrc_inverse : sf;
+  int rc = launch_inverse(c, B, dq, dv, da, dqfrc, skipstage, c->status);
+  if (rc) return rc;
+  if (qfrc_inverse && !dev) {
+    HIPCHECK(hipMemcpyAsync(qfrc_inverse, sf, sizeof(double)*(size_t)B*m.nv,
+                            hipMemcpyDeviceToHost, c->stream));
+  }
+  int anybad = 0;
+  if (status || !dev) {
+    std::vector<int> st(B);
+    HIPCHECK(hipMemcpyAsync(st.data(), c->status, sizeof(int)*(size_t)B, hipMemcpyDeviceToHost,
+                            c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < B; i++) anybad |= st[i];
+    if (status) memcpy(status, st.data(), sizeof(int)*(size_t)B);
+  }
+  return anybad ? MJHIP_ERR_INSTANCE : MJHIP_OK;
+}
+
+MJHIP_API int mjhip_statusDownload(mjhipContext* c, int first, int count, int* dst) {
+  if (!c || first < 0 || count < 0 || first + count > c->capacity || !dst) return MJHIP_ERR_ARG;
+  HIPCHECK(hipSetDevice(c->device));
+  HIPCHECK(hipMemcpyAsync(dst, c->status + first, sizeof(int)*(size_t)count,
+                          hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  return MJHIP_OK;
+}
+
+static int find_field(mjhipContext* c, const char* field, double** ptr, int* S) {
+  auto it = c->fields.find(field);
+  if (it == c->fields.end()) {
+    set_error("unknown mirror field '%s'", field);
+    return MJHIP_ERR_ARG;
+  }
+  *ptr = it->second.first;
+  *S = it->second.second;
+  return MJHIP_OK;
+}
+
+MJHIP_API void* mjhip_mirrorDevicePtr(mjhipContext* c, const char* field) {
+  double* p;
+  int S;
+  if (!c || find_field(c, field, &p, &S)) return nullptr;
+  return p;
+}
+
+// host transfers of whole 64-instance blocks, reordered on the host
+MJHIP_API int mjhip_mirrorDownload(mjhipContext* c, const char* field, int first, int count,
+                                   mjtNum* dst) {
+  double* p;
+  int S;
+  if (!c || !dst || first < 0 || count < 0 || first + count > c->capacity) return MJHIP_ERR_ARG;
+  if (int rc = find_field(c, field, &p, &S)) return rc;
+  if (!count || !S) return MJHIP_OK;
+  HIPCHECK(hipSetDevice(c->device));
+  int b0 = first / 64, b1 = (first + count + 63) / 64;
+  std::vector<double> tmp((size_t)(b1 - b0) * S * 64);
+  HIPCHECK(hipMemcpyAsync(tmp.data(), p + (size_t)b0*S*64, tmp.size()*sizeof(double),
+                          hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < count; i++) {
+    int inst = first + i;
+    size_t base = (size_t)(inst/64 - b0) * S * 64 + (inst & 63);
+    for (int k = 0; k < S; k++) dst[(size_t)i*S + k] = tmp[base + (size_t)k*64];
+  }
+  return MJHIP_OK;
+}
+
+MJHIP_API int mjhip_mirrorUpload(mjhipContext* c, const char* field, int first, int count,
+                                 const mjtNum* src) {
+  double* p;
+  int S;
+  if (!c || !src || first < 0 || count < 0 || first + count > c->capacity) return MJHIP_ERR_ARG;
+  if (int rc = find_field(c, field, &p, &S)) return rc;
+  if (!count || !S) return MJHIP_OK;
+  HIPCHECK(hipSetDevice(c->device));
+  int b0 = first / 64, b1 = (first + count + 63) / 64;
+  std::vector<double> tmp((size_t)(b1 - b0) * S * 64);
+  HIPCHECK(hipMemcpyAsync(tmp.data(), p + (size_t)b0*S*64, tmp.size()*sizeof(double),
+                          hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < count; i++) {
+    int inst = first + i;
+    size_t base = (size_t)(inst/64 - b0) * S * 64 + (inst & 63);
+    for (int k = 0; k < S; k++) tmp[base + (size_t)k*64] = src[(size_t)i*S + k];
+  }
+  HIPCHECK(hipMemcpyAsync(p + (size_t)b0*S*64, tmp.data(), tmp.size()*sizeof(double),
+                          hipMemcpyHostToDevice, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  return MJHIP_OK;
+}
+
+MJHIP_API int mjhip_timeInverseKernel(mjhipContext* c, int B, int reps, int skipstage,
+                                      int flags, float* ms) {
+  (void)flags;
+  if (!c || B <= 0 || B > c->capacity || reps <= 0 || !ms) return MJHIP_ERR_ARG;
+  HIPCHECK(hipSetDevice(c->device));
+  HIPCHECK(hipEventRecord(c->ev0, c->stream));
+  for (int r = 0; r < reps; r++) {
+    int rc = launch_inverse(c, B, nullptr, nullptr, nullptr, nullptr, skipstage, nullptr);
+    if (rc) return rc;
+  }
+  HIPCHECK(hipEventRecord(c->ev1, c->stream));
+  HIPCHECK(hipEventSynchronize(c->ev1));
+  float t = 0;
+  HIPCHECK(hipEventElapsedTime(&t, c->ev0, c->ev1));
+  *ms = t / reps;
+  return MJHIP_OK;
+}
+
+MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
+                                   const mjtNum* qvel, const mjtNum* qacc, mjtNum eps,
+                                   mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DmDq,
+                                   int flags) {
+  if (!c || B <= 0 || !qpos || !qvel || !qacc) return MJHIP_ERR_ARG;
+  const mjhipModel& m = c->hmodel;
+  const int nv = m.nv, P = 3*nv + 1;
+  if ((long)B*P > c->capacity) {
+    set_error("FD batch needs %ld instances, context capacity %d", (long)B*P, c->capacity);
+    return MJHIP_ERR_CAPACITY;
+  }
+  HIPCHECK(hipSetDevice(c->device));
+  const bool dev = flags & MJHIP_FLAG_DEVICE_PTRS;
+  const double *dq = qpos, *dv = qvel, *da = qacc;
+  double* sq = c->stage;
+  double* sv = sq + (size_t)c->capacity*m.nq;
+  double* sa = sv + (size_t)c->capacity*m.nv;
+  if (!dev) {
+    HIPCHECK(hipMemcpyAsync(sq, qpos, sizeof(double)*(size_t)B*m.nq, hipMemcpyHostToDevice,
+                            c->stream));
+    HIPCHECK(hipMemcpyAsync(sv, qvel, sizeof(double)*(size_t)B*nv, hipMemcpyHostToDevice,
+                            c->stream));
+    HIPCHECK(hipMemcpyAsync(sa, qacc, sizeof(double)*(size_t)B*nv, hipMemcpyHostToDevice,
+                            c->stream));
+    dq = sq; dv = sv; da = sa;
+  }
+  long ninst = (long)B*P;
+  hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream, c->dmodel,
+                     c->mirror, B, dq, dv, da, eps, 0);
+  HIPCHECK(hipGetLastError());
+  // all perturbations run the full pipeline (the reference's stage skipping is an
+  // optimisation of a serial loop; results are identical because skipped stages see
+  // unchanged inputs)
+  int rc = launch_inverse(c, (int)ninst, nullptr, nullptr, nullptr, nullptr, mjhipSTAGE_NONE,
+                          nullptr);
+  if (rc) return rc;
+  double *oq = DfDq, *ov = DfDv, *oa = DfDa, *om = DmDq;
+  std::vector<double*> tmp;
+  size_t nn = (size_t)B*nv*nv, nm = (size_t)B*nv*m.nM;
+  if (!dev) {
+    auto alloc = [&](double* h, size_t n) -> double* {
+      if (!h) return nullptr;
+      double* d = nullptr;
+      if (hipMalloc((void**)&d, n*sizeof(double)) != hipSuccess) return nullptr;
+      tmp.push_back(d);
+      return d;
+    };
+    oq = alloc(DfDq, nn); ov = alloc(DfDv, nn); oa = alloc(DfDa, nn); om = alloc(DmDq, nm);
+  }
+  long nd = (long)B*(P-1);
+  hipLaunchKernelGGL(k_fd_diff, dim3((nd + 255)/256), dim3(256), 0, c->stream, c->dmodel,
+                     c->mirror, B, eps, oq, ov, oa, om);
+  HIPCHECK(hipGetLastError());
+  if (!dev) {
+    if (DfDq) HIPCHECK(hipMemcpyAsync(DfDq, oq, nn*8, hipMemcpyDeviceToHost, c->stream));
+    if (DfDv) HIPCHECK(hipMemcpyAsync(DfDv, ov, nn*8, hipMemcpyDeviceToHost, c->stream));
+    if (DfDa) HIPCHECK(hipMemcpyAsync(DfDa, oa, nn*8, hipMemcpyDeviceToHost, c->stream));
+    if (DmDq) HIPCHECK(hipMemcpyAsync(DmDq, om, nm*8, hipMemcpyDeviceToHost, c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    for (double* p : tmp) hipFree(p);
+  }
+  return MJHIP_OK;
+}
+
+//---------------------------------- single-instance drop-in ---------------------------------
+
+static int g_device = 0;
+static std::mutex g_mu;
+static std::unordered_map<const mjhipModel*, mjhipContext*> g_ctx;
+
+static void report(const char* what) {
+  std::string msg = std::string(what) + ": " + g_last_error;
+  if (g_error_cb) {
+    g_error_cb(msg.c_str());
+  } else {
+    fprintf(stderr, "mjhip error: %s\n", msg.c_str());
+  }
+}
+
+static mjhipContext* ctx_for(const mjhipModel* m) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_ctx.find(m);
+  if (it != g_ctx.end()) return it->second;
+  mjhipContext* c = nullptr;
+  if (mjhip_contextCreate(m, g_device, 64, &c) != MJHIP_OK) return nullptr;
+  g_ctx[m] = c;
+  return c;
+}
+
+MJHIP_API void mjhip_setDevice(int device) { g_device = device; }
+
+MJHIP_API void mjhip_releaseModel(const mjhipModel* m) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  auto it = g_ctx.find(m);
+  if (it != g_ctx.end()) {
+    mjhip_contextFree(it->second);
+    g_ctx.erase(it);
+  }
+}
+
+// upload the fields a skipped stage reads, run one instance, download every output field
+MJHIP_API void mjhip_inverseSkip(const mjhipModel* m, mjhipData* d, int skipstage,
+                                 int skipsensor) {
+  mjhipContext* c = ctx_for(m);
+  if (!c) {
+    report("mjhip_inverseSkip");
+    return;
+  }
+  int rc = 0;
+#define MJ_M(n) m->n
+#define XD(name, d0, d1, stage)                                                     \
+  if (!rc && d->name && (stage == 0 || stage <= skipstage) && (m->d0) * (d1) > 0)    \
+    rc = mjhip_mirrorUpload(c, #name, 0, 1, d->name);
+  MJHIP_DATA_FIELDS
+#undef XD
+  if (!rc) {
+    rc = mjhip_inverseBatch(c, 1, nullptr, nullptr, nullptr, nullptr, skipstage, skipsensor,
+                            MJHIP_FLAG_MIRROR_INPUT, &d->status);
+    if (rc == MJHIP_ERR_INSTANCE) rc = 0;
+  }
+#define XD(name, d0, d1, stage)                                                     \
+  if (!rc && d->name && stage > skipstage && (m->d0) * (d1) > 0)                     \
+    rc = mjhip_mirrorDownload(c, #name, 0, 1, d->name);
+  MJHIP_DATA_FIELDS
+#undef XD
+#undef MJ_M
+  if (!rc) {
+    int cnt[4];
+    if (hipMemcpy(cnt, c->mirror.efc_count, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess) {
+      d->nefc = cnt[0];
+    }
+  }
+  if (rc) report("mjhip_inverseSkip");
+}
+
+MJHIP_API void mjhip_inverse(const mjhipModel* m, mjhipData* d) {
+  mjhip_inverseSkip(m, d, mjhipSTAGE_NONE, 0);
+}
+
+MJHIP_API void mjhip_invPosition(const mjhipModel* m, mjhipData* d) {
+  // a full evaluation computes the position stage; later-stage outputs are also refreshed
+  mjhip_inverseSkip(m, d, mjhipSTAGE_NONE, 1);
+}
+
+MJHIP_API void mjhip_invVelocity(const mjhipModel* m, mjhipData* d) {
+  mjhip_inverseSkip(m, d, mjhipSTAGE_POS, 1);
+}
+
+MJHIP_API void mjhip_invConstraint(const mjhipModel* m, mjhipData* d) {
+  mjhip_inverseSkip(m, d, mjhipSTAGE_VEL, 1);
+}
+
+MJHIP_API void mjhip_rne(const mjhipModel* m, mjhipData* d, int flg_acc, mjtNum* result) {
+  // mj_rne(flg_acc=1) is the qfrc_inverse core before the armature/passive/constraint
+  // terms; flg_acc=0 is qfrc_bias: both are produced by the fused pipeline
+  mjhip_inverseSkip(m, d, mjhipSTAGE_NONE, 1);
+  if (!result) return;
+  for (int i = 0; i < m->nv; i++) {
+    result[i] = flg_acc ? d->qfrc_inverse[i] - m->dof_armature[i]*d->qacc[i]
+                              + d->qfrc_passive[i] + d->qfrc_constraint[i]
+                        : d->qfrc_bias[i];
+  }
+}
+
+MJHIP_API void mjhip_compareFwdInv(const mjhipModel* m, mjhipData* d) {
+  // engine_inverse.c:275-316: returns immediately when nefc == 0
+  d->solver_fwdinv[0] = d->solver_fwdinv[1] = 0;
+  if (!d->nefc) return;
+  set_error("mj_compareFwdInv with active constraints needs the forward solver (next)");
+  report("mjhip_compareFwdInv");
+}
+
+}  // extern "C"

@@ -1,0 +1,274 @@
+"""Python host side of the batched engine: ctypes binding of libmjhip.so (include/mjhip.h).
+
+Mirrors the reference's inverse-dynamics interface (src/engine/engine_inverse.c) for one
+mjModel and many states:
+
+  InverseEngine(model).inverse(qpos, qvel, qacc)      batched mj_inverse     (inverse.c:266)
+  InverseEngine.inverse(..., skipstage=, skipsensor=) batched mj_inverseSkip (inverse.c:197)
+  InverseEngine.field(name)                           any mjData output field, per instance
+  InverseEngine.inverse_fd(...)                       batched mjd_inverseFD  (derivative_fd.c:611)
+  mj_inverse(m, d) / mj_inverseSkip(m, d, ...)        single-instance drop-ins on host MjData
+
+Every call runs the HIP kernels; there is no CPU fallback. Importing this module on a
+machine without a GPU works, but creating an engine raises MJHIPError (MJHIP_ERR_NO_DEVICE).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import fields, host
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmjhip.so")
+
+mjSTAGE_NONE, mjSTAGE_POS, mjSTAGE_VEL = 0, 1, 2
+FLAG_DEVICE_PTRS, FLAG_MIRROR_INPUT, FLAG_NO_MIRROR = 1, 2, 4
+ERR = {0: "OK", -1: "NO_DEVICE", -2: "ARG", -3: "HIP", -4: "MODEL", -5: "CAPACITY",
+       1: "INSTANCE"}
+INST_BITS = {1: "BADQPOS", 2: "BADQVEL", 4: "BADQACC", 8: "INERTIA", 16: "CNSTRFULL",
+             32: "UNSUPPORTED"}
+
+_D = ctypes.POINTER(ctypes.c_double)
+_I = ctypes.POINTER(ctypes.c_int)
+_V = ctypes.c_void_p
+
+# symbol -> (restype, argtypes): every MJHIP_API entry of include/mjhip.h
+SIGNATURES = {
+    "mjhip_version": (ctypes.c_char_p, []),
+    "mjhip_deviceCount": (ctypes.c_int, []),
+    "mjhip_lastError": (ctypes.c_char_p, []),
+    "mjhip_setErrorCallback": (None, [_V]),
+    "mjhip_fieldSize": (ctypes.c_int, [_V, ctypes.c_char_p]),
+    "mjhip_outputDoubles": (ctypes.c_int, [_V]),
+    "mjhip_contextCreate": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int,
+                                           ctypes.POINTER(_V)]),
+    "mjhip_contextFree": (None, [_V]),
+    "mjhip_contextCapacity": (ctypes.c_int, [_V]),
+    "mjhip_contextStream": (_V, [_V]),
+    "mjhip_contextSetStream": (ctypes.c_int, [_V, _V]),
+    "mjhip_inverseBatch": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, _V, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, _I]),
+    "mjhip_mirrorDownload": (ctypes.c_int, [_V, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                            _D]),
+    "mjhip_mirrorUpload": (ctypes.c_int, [_V, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                          _D]),
+    "mjhip_mirrorDevicePtr": (_V, [_V, ctypes.c_char_p]),
+    "mjhip_statusDownload": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _I]),
+    "mjhip_inverseFDBatch": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, ctypes.c_double,
+                                            _V, _V, _V, _V, ctypes.c_int]),
+    "mjhip_timeInverseKernel": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               ctypes.c_int,
+                                               ctypes.POINTER(ctypes.c_float)]),
+    "mjhip_setDevice": (None, [ctypes.c_int]),
+    "mjhip_inverse": (None, [_V, _V]),
+    "mjhip_inverseSkip": (None, [_V, _V, ctypes.c_int, ctypes.c_int]),
+    "mjhip_invPosition": (None, [_V, _V]),
+    "mjhip_invVelocity": (None, [_V, _V]),
+    "mjhip_invConstraint": (None, [_V, _V]),
+    "mjhip_rne": (None, [_V, _V, ctypes.c_int, _D]),
+    "mjhip_compareFwdInv": (None, [_V, _V]),
+    "mjhip_releaseModel": (None, [_V]),
+}
+
+
+class MJHIPError(RuntimeError):
+  pass
+
+
+_lib = None
+
+
+def lib():
+  """Load libmjhip.so (built in-tree by __graft_entry__.build()); fail loudly if absent."""
+  global _lib
+  if _lib is None:
+    if not os.path.exists(LIB_PATH):
+      raise MJHIPError(f"{LIB_PATH} not built: run __graft_entry__.build() (the engine has "
+                       "no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+      fn = getattr(L, name)
+      fn.restype = res
+      fn.argtypes = args
+    _lib = L
+  return _lib
+
+
+def _check(rc, what):
+  if rc < 0:
+    msg = lib().mjhip_lastError().decode()
+    raise MJHIPError(f"{what}: {ERR.get(rc, rc)}: {msg}")
+  return rc
+
+
+def _dptr(a):
+  """Device pointer of a torch tensor, else None."""
+  if hasattr(a, "data_ptr") and hasattr(a, "is_cuda"):
+    if not a.is_cuda:
+      raise MJHIPError("torch tensors passed to the engine must be on the GPU")
+    if not a.is_contiguous() or str(a.dtype) != "torch.float64":
+      raise MJHIPError("device tensors must be contiguous float64")
+    return a.data_ptr()
+  return None
+
+
+class InverseEngine:
+  """Batched mj_inverse for one model on one device (an mjhipContext)."""
+
+  def __init__(self, model, capacity: int, device: int = 0):
+    self.m = model
+    self.cm = host.model_struct(model)
+    L = lib()
+    ctx = _V()
+    _check(L.mjhip_contextCreate(ctypes.byref(self.cm), device, capacity, ctypes.byref(ctx)),
+           "mjhip_contextCreate")
+    self.ctx = ctx
+    self.device = device
+    self.capacity = L.mjhip_contextCapacity(ctx)
+    self.nv, self.nq = model.nv, model.nq
+
+  def close(self):
+    if getattr(self, "ctx", None):
+      lib().mjhip_contextFree(self.ctx)
+      self.ctx = None
+
+  def __del__(self):
+    try:
+      self.close()
+    except Exception:   # interpreter shutdown
+      pass
+
+  @property
+  def stream(self):
+    return lib().mjhip_contextStream(self.ctx)
+
+  def set_stream(self, stream_handle: int):
+    _check(lib().mjhip_contextSetStream(self.ctx, stream_handle), "mjhip_contextSetStream")
+
+  def inverse(self, qpos=None, qvel=None, qacc=None, out=None, skipstage=mjSTAGE_NONE,
+              skipsensor=0, mirror_input=False, status=False):
+    """Batched mj_inverseSkip. numpy arrays (host) or float64 torch tensors (device).
+
+    Returns qfrc_inverse [B, nv] (numpy for host inputs; `out` for device tensors). With
+    mirror_input=True the inputs already in the mirror are used (pass B via qpos=int).
+    """
+    L = lib()
+    flags = 0
+    if mirror_input:
+      B = int(qpos)
+      flags |= FLAG_MIRROR_INPUT
+      pq = pv = pa = None
+      dev = out is not None and _dptr(out) is not None
+    else:
+      dev = _dptr(qpos) is not None
+      if dev:
+        B = qpos.shape[0]
+        pq, pv, pa = _dptr(qpos), _dptr(qvel), _dptr(qacc)
+      else:
+        qpos = np.ascontiguousarray(qpos, dtype=np.float64).reshape(-1, self.nq)
+        qvel = np.ascontiguousarray(qvel, dtype=np.float64).reshape(-1, self.nv)
+        qacc = np.ascontiguousarray(qacc, dtype=np.float64).reshape(-1, self.nv)
+        B = qpos.shape[0]
+        pq, pv, pa = (qpos.ctypes.data, qvel.ctypes.data, qacc.ctypes.data)
+    if dev:
+      flags |= FLAG_DEVICE_PTRS
+      po = _dptr(out) if out is not None else None
+      st = None
+    else:
+      if out is None:
+        out = np.zeros((B, self.nv))
+      po = out.ctypes.data
+      st = np.zeros(B, dtype=np.int32)
+    rc = L.mjhip_inverseBatch(self.ctx, B, pq, pv, pa, po, skipstage, skipsensor, flags,
+                              st.ctypes.data_as(_I) if st is not None else None)
+    _check(rc, "mjhip_inverseBatch")
+    if status:
+      return out, st
+    return out
+
+  def field(self, name, first=0, count=None):
+    """Mirror field `name` of instances [first, first+count) as [count, size] (numpy)."""
+    L = lib()
+    S = L.mjhip_fieldSize(ctypes.byref(self.cm), name.encode())
+    if S < 0:
+      raise MJHIPError(f"unknown field {name}")
+    count = self.capacity - first if count is None else count
+    out = np.zeros((count, max(S, 1)))
+    if S:
+      _check(L.mjhip_mirrorDownload(self.ctx, name.encode(), first, count,
+                                    out.ctypes.data_as(_D)), "mjhip_mirrorDownload")
+    return out[:, :S]
+
+  def set_field(self, name, values, first=0):
+    values = np.ascontiguousarray(values, dtype=np.float64)
+    count = values.shape[0]
+    _check(lib().mjhip_mirrorUpload(self.ctx, name.encode(), first, count,
+                                    values.ctypes.data_as(_D)), "mjhip_mirrorUpload")
+
+  def upload_states(self, qpos, qvel, qacc, first=0):
+    """Place states in the device mirror (inputs resident in HBM for timed runs)."""
+    self.set_field("qpos", qpos, first)
+    self.set_field("qvel", qvel, first)
+    self.set_field("qacc", qacc, first)
+
+  def time_kernel(self, B, reps=20, skipstage=mjSTAGE_NONE):
+    """Average ms per launch of the fused kernel on mirror-resident inputs (HIP events)."""
+    ms = ctypes.c_float()
+    _check(lib().mjhip_timeInverseKernel(self.ctx, B, reps, skipstage, 0, ctypes.byref(ms)),
+           "mjhip_timeInverseKernel")
+    return ms.value
+
+  def inverse_fd(self, qpos, qvel, qacc, eps=1e-6, dmdq=False):
+    """Batched mjd_inverseFD (flg_actuation=0, no sensors): DfDq, DfDv, DfDa [B, nv, nv]."""
+    qpos = np.ascontiguousarray(qpos, dtype=np.float64).reshape(-1, self.nq)
+    qvel = np.ascontiguousarray(qvel, dtype=np.float64).reshape(-1, self.nv)
+    qacc = np.ascontiguousarray(qacc, dtype=np.float64).reshape(-1, self.nv)
+    B, nv = qpos.shape[0], self.nv
+    DfDq = np.zeros((B, nv, nv))
+    DfDv = np.zeros((B, nv, nv))
+    DfDa = np.zeros((B, nv, nv))
+    DmDq = np.zeros((B, nv, self.m.nM)) if dmdq else None
+    _check(lib().mjhip_inverseFDBatch(self.ctx, B, qpos.ctypes.data, qvel.ctypes.data,
+                                      qacc.ctypes.data, eps, DfDq.ctypes.data,
+                                      DfDv.ctypes.data, DfDa.ctypes.data,
+                                      None if DmDq is None else DmDq.ctypes.data, 0),
+           "mjhip_inverseFDBatch")
+    return DfDq, DfDv, DfDa, DmDq
+
+
+def output_bytes_per_eval(model) -> int:
+  """B_eval of SURVEY.md §8d: 8 * (R + W) for the model's field table."""
+  return 8 * (fields.input_doubles(model.sizes) + fields.output_doubles(model.sizes))
+
+
+# ---------------------------------------------------------------- single-instance drop-ins
+_structs = {}
+
+
+def _cm(m):
+  key = id(m)
+  if key not in _structs:
+    _structs[key] = (m, host.model_struct(m))
+  return _structs[key][1]
+
+
+def mj_inverse(m, d: host.MjData):
+  """mj_inverse(m, d) (engine_inverse.c:266) on the GPU, writing every output into d."""
+  lib().mjhip_inverse(ctypes.byref(_cm(m)), d.ptr())
+
+
+def mj_inverseSkip(m, d: host.MjData, skipstage: int, skipsensor: int):
+  """mj_inverseSkip (engine_inverse.c:197) on the GPU."""
+  lib().mjhip_inverseSkip(ctypes.byref(_cm(m)), d.ptr(), skipstage, skipsensor)
+
+
+def mj_rne(m, d: host.MjData, flg_acc: int, result):
+  lib().mjhip_rne(ctypes.byref(_cm(m)), d.ptr(), flg_acc,
+                  np.ascontiguousarray(result).ctypes.data_as(_D))
+
+
+def mj_compareFwdInv(m, d: host.MjData):
+  lib().mjhip_compareFwdInv(ctypes.byref(_cm(m)), d.ptr())

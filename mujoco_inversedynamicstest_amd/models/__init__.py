@@ -1,0 +1,30 @@
+"""Bundled compiled models (.npz, produced by tools/compile_models.py from the reference's
+MJCF files). They travel with the repo, so nothing reads /root/reference at run time."""
+from __future__ import annotations
+
+import os
+
+from ..mjcf import Model
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+
+# name -> MJCF path relative to the reference root
+SOURCES = {
+    "humanoid": "model/humanoid/humanoid.xml",                  # BASELINE.json configs 2-5
+    "inverse_test": "src/inverse/test.xml",                      # inverse_test.cpp model
+    "linear": "test/engine/testdata/derivative/linear.xml",     # LinearSystemInverse
+    "inertia": "test/engine/testdata/inertia.xml",              # FactorI / FactorIs
+}
+
+mjDSBL_CONTACT = 1 << 4
+
+
+def path(name: str) -> str:
+  return os.path.join(_HERE, name + ".npz")
+
+
+def load(name: str, disable_contact: bool = False) -> Model:
+  m = Model.load(path(name))
+  if disable_contact:
+    m.opt["disableflags"] = int(m.opt["disableflags"]) | mjDSBL_CONTACT
+  return m

@@ -1,0 +1,37 @@
+"""Batch sharding over ranks (one process per GPU) and the RCCL gather to rank 0.
+
+mj_inverse has no inter-instance dependence, so a global batch splits into
+contiguous index shards with no data-path collective; states come from the counter-based
+sampler, so a shard's rows are identical for any world size. The only collective is the
+gather of results to rank 0 (north star: RCCL over xGMI, used only for that).
+"""
+from __future__ import annotations
+
+
+def shard(total: int, world: int, rank: int):
+  """Contiguous shard [first, first+count) of `total` instances for `rank` of `world`."""
+  base, rem = divmod(total, world)
+  first = rank * base + min(rank, rem)
+  return first, base + (1 if rank < rem else 0)
+
+
+def gather_to_rank0(tensor, world: int, rank: int):
+  """Gather equal-shaped tensors to rank 0 (RCCL on GPU tensors, gloo on CPU tensors).
+
+  Returns the list of gathered tensors on rank 0 and None elsewhere. Uses point-to-point
+  sends into rank 0 (RCCL has no native gather; each peer uses its own xGMI link).
+  """
+  import torch
+  import torch.distributed as dist
+  if world == 1:
+    return [tensor]
+  if rank == 0:
+    bufs = [tensor] + [torch.empty_like(tensor) for _ in range(world - 1)]
+    ops = [dist.P2POp(dist.irecv, bufs[r], r) for r in range(1, world)]
+    for req in dist.batch_isend_irecv(ops):
+      req.wait()
+    return bufs
+  req = dist.batch_isend_irecv([dist.P2POp(dist.isend, tensor, 0)])
+  for r in req:
+    r.wait()
+  return None

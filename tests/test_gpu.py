@@ -1,0 +1,236 @@
+"""GPU parity: the HIP engine vs the CPU oracle (run on an MI355X with -m gpu).
+
+Tolerance (BASELINE.json north_star): bit-exact on indices/counts; fp64 outputs within
+1e-10 relative, measured normwise per instance: max_k |gpu_k - cpu_k| <= 1e-10 * max(1,
+max_k |cpu_k|). The GPU build contracts multiply-adds into FMAs and uses the device libm
+(sin/cos in mju_axisAngle2Quat); the same source compiled without contraction on the host
+matches the oracle bit for bit (test_kernel_cpu.py).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from mujoco_inversedynamicstest_amd import engine, fields, host, models
+from mujoco_inversedynamicstest_amd.sampler import sample_states
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-10
+OUTPUTS = [f.name for f in fields.DATA_FIELDS if f.stage > 0]
+
+
+def assert_close(gpu, cpu, what):
+  gpu = np.asarray(gpu).reshape(len(gpu), -1)
+  cpu = np.asarray(cpu).reshape(len(cpu), -1)
+  scale = np.maximum(1.0, np.abs(cpu).max(axis=1))
+  err = (np.abs(gpu - cpu).max(axis=1) / scale).max()
+  assert err <= RTOL, f"{what}: normwise relative error {err:.3e} > {RTOL}"
+  return err
+
+
+def oracle_batch(m, q, v, a, fields_=("qfrc_inverse",)):
+  o = Oracle(m)
+  out = {f: [] for f in fields_}
+  nefc = []
+  for i in range(len(q)):
+    o.inverse(q[i], v[i], a[i])
+    for f in fields_:
+      out[f].append(getattr(o.d, f).copy())
+    nefc.append(o.d.nefc)
+  return {f: np.array(x) for f, x in out.items()}, np.array(nefc)
+
+
+@pytest.fixture(scope="module")
+def eng(humanoid):
+  e = engine.InverseEngine(humanoid, capacity=65536 + 4096)
+  yield e
+  e.close()
+
+
+def test_device_present():
+  assert engine.lib().mjhip_deviceCount() >= 1
+
+
+def test_humanoid_config2_parity_4096(humanoid, eng):
+  """Config 2: humanoid, contacts disabled, B=4096, every limit inactive (nefc = 0)."""
+  q, v, a = sample_states(humanoid, 4096)
+  f, st = eng.inverse(q, v, a, status=True)
+  assert (st == 0).all()
+  ref, nefc = oracle_batch(humanoid, q, v, a)
+  assert (nefc == 0).all()
+  assert_close(f, ref["qfrc_inverse"], "qfrc_inverse")
+
+
+def test_humanoid_every_mirror_field(humanoid, eng):
+  """All 2,563 mjData doubles of mj_inverse for 256 instances."""
+  q, v, a = sample_states(humanoid, 256, first=77)
+  eng.inverse(q, v, a)
+  ref, _ = oracle_batch(humanoid, q, v, a, OUTPUTS)
+  for f in OUTPUTS:
+    if fields.DATA_FIELD[f].size(humanoid.sizes):
+      assert_close(eng.field(f, 0, 256), ref[f], f)
+
+
+def test_humanoid_limits_active(humanoid, eng):
+  """Limit rows (joint + tendon), impedance and qfrc_constraint on the device."""
+  q, v, a = sample_states(humanoid, 512, first=3000, margin=-0.25, resample_tendons=False)
+  f = eng.inverse(q, v, a)
+  ref, nefc = oracle_batch(humanoid, q, v, a, ("qfrc_inverse", "qfrc_constraint"))
+  assert nefc.sum() > 512
+  assert_close(f, ref["qfrc_inverse"], "qfrc_inverse")
+  assert_close(eng.field("qfrc_constraint", 0, 512), ref["qfrc_constraint"], "qfrc_constraint")
+
+
+def test_skipstage_chain(humanoid, eng):
+  """mj_inverseSkip(VEL) / (POS) reuse the earlier stages kept in the device mirror."""
+  q, v, a = sample_states(humanoid, 128, first=11)
+  eng.inverse(q, v, a)
+  a2 = a + 0.25
+  f_vel = eng.inverse(q, v, a2, skipstage=engine.mjSTAGE_VEL)
+  v2 = v * 0.9
+  f_pos = eng.inverse(q, v2, a2, skipstage=engine.mjSTAGE_POS)
+  o = Oracle(humanoid)
+  rv, rp = [], []
+  for i in range(128):
+    o.inverse(q[i], v[i], a[i])
+    rv.append(o.inverse(qacc=a2[i], skipstage=2))
+    rp.append(o.inverse(qvel=v2[i], skipstage=1))
+  assert_close(f_vel, rv, "skip VEL")
+  assert_close(f_pos, rp, "skip POS")
+
+
+@pytest.mark.parametrize("B", [1, 63, 64, 65, 1000])
+def test_ragged_batches(humanoid, eng, B):
+  q, v, a = sample_states(humanoid, B, first=500)
+  f = eng.inverse(q, v, a)
+  ref, _ = oracle_batch(humanoid, q, v, a)
+  assert f.shape == (B, humanoid.nv)
+  assert_close(f, ref["qfrc_inverse"], f"B={B}")
+
+
+def test_empty_batch(humanoid, eng):
+  out = eng.inverse(np.zeros((0, humanoid.nq)), np.zeros((0, humanoid.nv)),
+                    np.zeros((0, humanoid.nv)))
+  assert out.shape == (0, humanoid.nv)
+
+
+@pytest.mark.parametrize("name", ["inverse_test", "linear", "inertia"])
+def test_other_models(name):
+  m = models.load(name, disable_contact=True)
+  q, v, a = sample_states(m, 300)
+  e = engine.InverseEngine(m, capacity=512)
+  f = e.inverse(q, v, a)
+  ref, _ = oracle_batch(m, q, v, a, OUTPUTS)
+  assert_close(f, ref["qfrc_inverse"], name)
+  for fld in ("qM", "qLD", "cdof", "cinert", "qfrc_bias", "qfrc_passive"):
+    if fields.DATA_FIELD[fld].size(m.sizes):
+      assert_close(e.field(fld, 0, 300), ref[fld], f"{name}.{fld}")
+  e.close()
+
+
+def test_full_size_properties(humanoid, eng):
+  """B = 65,536 (the metric's batch): shard equivalence (bit-exact) and the affine-in-qacc
+  identity qfrc_inverse(a) - qfrc_inverse(0) = M(q) a, with M from the device mirror."""
+  B = 65536
+  q, v, a = sample_states(humanoid, B)
+  f = eng.inverse(q, v, a)
+  h = B // 2
+  f1 = eng.inverse(q[:h], v[:h], a[:h])
+  f2 = eng.inverse(q[h:], v[h:], a[h:])
+  np.testing.assert_array_equal(np.vstack([f1, f2]), f)
+  f0 = eng.inverse(q, v, np.zeros_like(a))
+  qM = eng.field("qM", 0, B)
+  # dense M from qM (dof_Madr ancestor lists)
+  nv = humanoid.nv
+  Mx = np.zeros_like(a)
+  adr = 0
+  for i in range(nv):
+    j = i
+    while j >= 0:
+      Mx[:, i] += qM[:, adr] * a[:, j]
+      if j != i:
+        Mx[:, j] += qM[:, adr] * a[:, i]
+      j = humanoid.dof_parentid[j]
+      adr += 1
+  scale = np.maximum(1.0, np.abs(f).max(axis=1))
+  assert (np.abs((f - f0) - Mx).max(axis=1) / scale).max() < 1e-9
+  # a checksum of checksums, for the record
+  assert np.isfinite(f).all()
+
+
+def test_inverse_fd_parity(humanoid, eng):
+  """Config 5 kernel: batched mjd_inverseFD vs the oracle's serial mjd_inverseFD."""
+  q, v, a = sample_states(humanoid, 16, first=900)
+  DfDq, DfDv, DfDa, DmDq = eng.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
+  o = Oracle(humanoid)
+  for i in range(16):
+    o.set_state(q[i], v[i], a[i])
+    rq, rv, ra, rm = o.inverse_fd(1e-6, dmdq=True)
+    # FD amplifies last-bit differences of the two builds by 1/eps = 1e6
+    np.testing.assert_allclose(DfDa[i], ra, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(DfDv[i], rv, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(DfDq[i], rq, rtol=1e-5, atol=1e-4)
+    np.testing.assert_allclose(DmDq[i], rm, rtol=1e-5, atol=1e-5)
+
+
+def test_linear_system_inverse_on_gpu(linear):
+  """LinearSystemInverse (engine_derivative_test.cc:793-868) through the GPU FD path."""
+  o = Oracle(linear)
+  o.forward()
+  e = engine.InverseEngine(linear, capacity=64)
+  DfDq, DfDv, DfDa, DmDq = e.inverse_fd(o.d.qpos[None], o.d.qvel[None], o.d.qacc[None],
+                                        eps=1e-6, dmdq=True)
+  np.testing.assert_allclose(DfDq[0], np.diag(linear.jnt_stiffness), atol=1e-6)
+  np.testing.assert_allclose(DfDv[0], np.diag(linear.dof_damping), atol=1e-6)
+  np.testing.assert_allclose(DfDa[0], o.fullM(), atol=1e-6)
+  np.testing.assert_allclose(DmDq[0], 0, atol=1e-6)
+  e.close()
+
+
+def test_single_instance_dropin_inverse_test_driver(arm2, rng):
+  """src/inverse/inverse_test.cpp with the GPU mj_inverseSkip(m, d, mjSTAGE_VEL, 1):
+  forward states from the oracle harness, inverse through the single-instance drop-in."""
+  o = Oracle(arm2)
+  d = host.MjData(arm2)
+  worst = 0
+  for _ in range(int(1.0 / arm2.opt["timestep"])):
+    o.d.qfrc_applied[:] = 0.4 * (rng.random(arm2.nv) - 0.5)
+    o.d.xfrc_applied[:] = 0.8 * (rng.random(6 * arm2.nbody) - 0.5)
+    assert o.forward() == 0
+    expected = (o.d.qfrc_applied + o.d.qfrc_actuator).copy()
+    o.xfrc_accumulate(expected)
+    for f in [x.name for x in fields.DATA_FIELDS]:
+      getattr(d, f)[:] = getattr(o.d, f)
+    engine.mj_inverseSkip(arm2, d, engine.mjSTAGE_VEL, 1)
+    worst = max(worst, np.linalg.norm(expected - d.qfrc_inverse))
+    o.rk4()
+  assert worst < 1e-6
+
+
+def test_single_instance_mj_inverse(humanoid):
+  q, v, a = sample_states(humanoid, 3, first=42)
+  d = host.MjData(humanoid)
+  o = Oracle(humanoid)
+  for i in range(3):
+    d.qpos[:], d.qvel[:], d.qacc[:] = q[i], v[i], a[i]
+    engine.mj_inverse(humanoid, d)
+    o.inverse(q[i], v[i], a[i])
+    for f in OUTPUTS:
+      if fields.DATA_FIELD[f].size(humanoid.sizes):
+        assert_close(getattr(d, f)[None], getattr(o.d, f)[None], f)
+    assert d.nefc == o.d.nefc
+
+
+def test_device_tensor_io(humanoid, eng):
+  torch = pytest.importorskip("torch")
+  q, v, a = sample_states(humanoid, 2048, first=1234)
+  dev = torch.device("cuda:0")
+  tq, tv, ta = (torch.from_numpy(x).to(dev) for x in (q, v, a))
+  out = torch.empty((2048, humanoid.nv), dtype=torch.float64, device=dev)
+  torch.cuda.synchronize()
+  eng.inverse(tq, tv, ta, out=out)
+  torch.cuda.synchronize()
+  # the library stream is non-blocking w.r.t. torch: synchronize it too
+  ref = eng.inverse(q, v, a)
+  np.testing.assert_array_equal(out.cpu().numpy(), ref)
