@@ -85,6 +85,13 @@ def lib():
   """Load libmjhip.so (built in-tree by __graft_entry__.build()); fail loudly if absent."""
   global _lib
   if _lib is None:
+    # One HIP runtime per process: torch ships its own libamdhip64.so (same SONAME as
+    # /opt/rocm's). Loading torch first makes libmjhip.so bind to that runtime, so device
+    # pointers and streams can be shared with torch (bench.py, tests, RCCL).
+    try:
+      import torch  # noqa: F401
+    except ImportError:
+      pass
     if not os.path.exists(LIB_PATH):
       raise MJHIPError(f"{LIB_PATH} not built: run __graft_entry__.build() (the engine has "
                        "no CPU fallback)")

@@ -18,7 +18,7 @@ from __future__ import annotations
 import numpy as np
 
 GOLDEN = np.uint64(0x9E3779B97F4A7C15)
-STRIDE = 4096          # draws per instance stream
+STRIDE = 1 << 16       # draws per instance stream
 ATTEMPT = 256          # draws reserved per resampling attempt
 SEED = 20250314
 
@@ -106,7 +106,7 @@ def _tendon_ok(m, q, tmargin):
 
 
 def sample_states(m, n, first=0, seed=SEED, margin=0.05, acc_std=10.0,
-                  resample_tendons=True, max_attempts=14):
+                  resample_tendons=True, max_attempts=200):
   """Return (qpos [n,nq], qvel [n,nv], qacc [n,nv]) for instances first..first+n-1."""
   idx = np.arange(first, first + n, dtype=np.uint64)
   st = _Stream(seed, idx, np.zeros(n, dtype=np.int64))
