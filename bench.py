@@ -91,6 +91,7 @@ def main():
 
   # kernel-only average launch time (HIP events on the context's stream) for the roofline
   kernel_ms = eng.time_kernel(count, reps=max(args.steps, 10))
+  generic_ms = eng.time_kernel(count, reps=5, generic=True)
   bytes_per_eval = engine.output_bytes_per_eval(m)
   achieved = bytes_per_eval * count / (kernel_ms * 1e-3) / 1e9
 
@@ -132,7 +133,9 @@ def main():
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "kernel": "k_inverse<0>", "kernel_ms": kernel_ms,
+                     "kernel": f"k_fast_{eng.fast_kernel}+k_inverse_list" if eng.fast_kernel
+                               else "k_inverse<0>",
+                     "kernel_ms": kernel_ms, "generic_kernel_ms": generic_ms,
                      "bytes_per_eval": bytes_per_eval},
         "cpu_baseline": cpu,
         "checksum_qfrc_inverse": checksum,

@@ -224,8 +224,9 @@ typedef enum mjhipStatus_ {
 /* flags for mjhipBatchDesc.flags */
 #define MJHIP_FLAG_DEVICE_PTRS   (1 << 0)  /* qpos/qvel/qacc/qfrc pointers are device memory */
 #define MJHIP_FLAG_MIRROR_INPUT  (1 << 1)  /* inputs already in the device mirror (skip upload) */
-#define MJHIP_FLAG_NO_MIRROR     (1 << 2)  /* write only qfrc_inverse (+ fields a later skip
-                                              call needs are then NOT available) */
+#define MJHIP_FLAG_NO_MIRROR     (1 << 2)  /* reserved: write only qfrc_inverse */
+#define MJHIP_FLAG_GENERIC       (1 << 3)  /* force the generic (model-data-driven) kernel
+                                              even when a straight-line kernel matches */
 
 /* Mirror layout on the device (the "batched SoA mirror" of SURVEY.md §7 L1):
  * every per-instance field F of size S = d0*d1 is stored as
@@ -256,6 +257,12 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
                                   mjhipContext** out);
 MJHIP_API void mjhip_contextFree(mjhipContext* c);
 MJHIP_API int mjhip_contextCapacity(const mjhipContext* c);
+/* name of the straight-line (model-specialized) kernel selected for the context's model by
+ * signature, or NULL when the generic kernel runs */
+MJHIP_API const char* mjhip_contextFastKernel(const mjhipContext* c);
+/* instances of the last fast-path call that had active constraint rows and were recomputed
+ * by the generic kernel (blocking read; -1 on error) */
+MJHIP_API int mjhip_worklistCount(mjhipContext* c);
 /* HIP stream used by the context (hipStream_t as void*); may be replaced by the caller */
 MJHIP_API void* mjhip_contextStream(mjhipContext* c);
 MJHIP_API int mjhip_contextSetStream(mjhipContext* c, void* stream);

@@ -1202,4 +1202,40 @@ MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
 
 }  // namespace mjh
 
+//---------------------------------- device mirror (include/mjhip.h layout) ------------------
+
+struct Mirror {
+#define XD(name, d0, d1, stage) double* name; int name##_n;
+  MJHIP_DATA_FIELDS
+#undef XD
+#define XSC(name, n) double* name; int name##_n;
+  MJHIP_SCRATCH_FIELDS
+#undef XSC
+#define XSI(name, n) int* name; int name##_n;
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+  int efc_cap;
+};
+
+MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
+  mjh::Lane<64> d;
+#define XD(name, d0, d1, stage) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
+  MJHIP_DATA_FIELDS
+#undef XD
+#define XSC(name, n) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
+  MJHIP_SCRATCH_FIELDS
+#undef XSC
+#define XSI(name, n) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+  d.efc_cap = mr.efc_cap;
+  return d;
+}
+
+#if defined(__HIPCC__)
+  #define MJH_ATOMIC_ADD(p, v) atomicAdd((p), (v))
+#else
+  #define MJH_ATOMIC_ADD(p, v) ((*(p) += (v)) - (v))
+#endif
+
 #endif  // MJHIP_ENGINE_DEVICE_H_

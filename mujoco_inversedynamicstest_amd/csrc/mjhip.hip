@@ -25,37 +25,41 @@
 using mjh::Lane;
 using mjh::SP;
 
-//==================================== device mirror =========================================
+//==================================== kernels ===============================================
 
-struct Mirror {
-#define XD(name, d0, d1, stage) double* name; int name##_n;
-  MJHIP_DATA_FIELDS
-#undef XD
-#define XSC(name, n) double* name; int name##_n;
-  MJHIP_SCRATCH_FIELDS
-#undef XSC
-#define XSI(name, n) int* name; int name##_n;
-  MJHIP_SCRATCH_INT_FIELDS
-#undef XSI
-  int efc_cap;
+// Straight-line kernels generated per bundled model by codegen.py (build()), selected by
+// model signature; each appends limit-active instances to a work-list that k_inverse_list
+// then recomputes with the generic pipeline.
+struct FastKernelEntry {
+  unsigned long long sig;
+  void (*launch)(dim3, dim3, hipStream_t, const Mirror&, int, const double*, const double*,
+                 const double*, double*, int*, int*, int*, int*);
+  const char* name;
 };
+#if __has_include("gen_fast.inc")
+#include "gen_fast.inc"
+#else
+static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr}};
+#endif
 
-__device__ __forceinline__ Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
-  Lane<64> d;
-#define XD(name, d0, d1, stage) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
-  MJHIP_DATA_FIELDS
-#undef XD
-#define XSC(name, n) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
-  MJHIP_SCRATCH_FIELDS
-#undef XSC
-#define XSI(name, n) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
-  MJHIP_SCRATCH_INT_FIELDS
-#undef XSI
-  d.efc_cap = mr.efc_cap;
-  return d;
+// generic pipeline over the instances of a work-list (limit-active instances of the fast
+// path); grid = ceil(B/64) blocks, threads past *count exit at once
+__global__ __launch_bounds__(64) void k_inverse_list(mjhipModel m, Mirror mr,
+                                                     const int* __restrict__ worklist,
+                                                     const int* __restrict__ count,
+                                                     double* __restrict__ qfrc_out,
+                                                     int* __restrict__ status) {
+  const long g = (long)blockIdx.x*64 + threadIdx.x;
+  if (g >= *count) return;
+  const long inst = worklist[g];
+  Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
+  int st = mjh::inverseSkip(m, d, mjhipSTAGE_NONE);
+  if (qfrc_out) {
+    for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
+  }
+  if (status) status[inst] = st;
 }
 
-//==================================== kernels ===============================================
 
 // Fused mj_inverseSkip over a batch. Optional row-major (instance-major) inputs are copied
 // into the mirror first; optional row-major qfrc_inverse output is written at the end.
@@ -223,7 +227,44 @@ struct mjhipContext_ {
   size_t stage_bytes = 0;
   int* status = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  const FastKernelEntry* fast = nullptr;   // straight-line kernel for this model, if any
+  int* worklist = nullptr;                 // capacity + 1 ints: [count, list...]
 };
+
+// FNV-1a 64 over sizes, options and every model array (= fields.model_signature in Python)
+static unsigned long long model_signature(const mjhipModel* m) {
+  unsigned long long h = 0xcbf29ce484222325ull;
+  auto feed = [&](const void* p, size_t n) {
+    const unsigned char* b = (const unsigned char*)p;
+    for (size_t i = 0; i < n; i++) {
+      h ^= b[i];
+      h *= 0x100000001b3ull;
+    }
+  };
+#define XS(name) { int v = m->name; feed(&v, 4); }
+  MJHIP_MODEL_SIZES
+#undef XS
+  feed(&m->opt.timestep, 8);
+  feed(&m->opt.impratio, 8);
+  feed(m->opt.gravity, 24);
+  feed(m->opt.wind, 24);
+  feed(&m->opt.density, 8);
+  feed(&m->opt.viscosity, 8);
+  feed(&m->opt.o_margin, 8);
+  feed(m->opt.o_solref, 16);
+  feed(m->opt.o_solimp, 40);
+  feed(&m->opt.integrator, 4);
+  feed(&m->opt.cone, 4);
+  feed(&m->opt.jacobian, 4);
+  feed(&m->opt.disableflags, 4);
+  feed(&m->opt.enableflags, 4);
+#define MJ_M(n) m->n
+#define X(type, name, d0, d1) if (m->name) feed(m->name, sizeof(type) * (size_t)(m->d0) * (d1));
+  MJHIP_MODEL_POINTERS
+#undef X
+#undef MJ_M
+  return h;
+}
 
 static int efc_capacity(const mjhipModel* m) {
   int n = 0;
@@ -417,6 +458,17 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
     set_error("hipMalloc(staging) failed");
     return MJHIP_ERR_HIP;
   }
+  if (hipMalloc((void**)&c->worklist, sizeof(int) * ((size_t)c->capacity + 1)) != hipSuccess) {
+    set_error("hipMalloc(worklist) failed");
+    return MJHIP_ERR_HIP;
+  }
+  const char* nofast = getenv("MJHIP_DISABLE_FAST");
+  if (!(nofast && nofast[0] == '1')) {
+    unsigned long long sig = model_signature(m);
+    for (const FastKernelEntry* e = g_fast_kernels; e->launch; e++) {
+      if (e->sig == sig) c->fast = e;
+    }
+  }
   HIPCHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
   c->own_stream = true;
   HIPCHECK(hipEventCreate(&c->ev0));
@@ -434,12 +486,24 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   if (c->ev1) hipEventDestroy(c->ev1);
   hipFree(c->stage);
   hipFree(c->status);
+  hipFree(c->worklist);
   hipFree(c->mirror_buf);
   hipFree(c->dmodel_buf);
   delete c;
 }
 
 MJHIP_API int mjhip_contextCapacity(const mjhipContext* c) { return c ? c->capacity : 0; }
+
+MJHIP_API const char* mjhip_contextFastKernel(const mjhipContext* c) {
+  return (c && c->fast) ? c->fast->name : nullptr;
+}
+
+MJHIP_API int mjhip_worklistCount(mjhipContext* c) {
+  if (!c) return -1;
+  int n = 0;
+  if (hipMemcpy(&n, c->worklist, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return n;
+}
 
 MJHIP_API void* mjhip_contextStream(mjhipContext* c) { return c ? (void*)c->stream : nullptr; }
 
@@ -455,8 +519,19 @@ MJHIP_API int mjhip_contextSetStream(mjhipContext* c, void* stream) {
 }
 
 static int launch_inverse(mjhipContext* c, int B, const double* qpos, const double* qvel,
-                          const double* qacc, double* qfrc, int skipstage, int* status) {
+                          const double* qacc, double* qfrc, int skipstage, int* status,
+                          int flags = 0) {
   dim3 grid((B + 63) / 64), block(64);
+  if (skipstage == mjhipSTAGE_NONE && c->fast && !(flags & MJHIP_FLAG_GENERIC)) {
+    HIPCHECK(hipMemsetAsync(c->worklist, 0, sizeof(int), c->stream));
+    c->fast->launch(grid, block, c->stream, c->mirror, B, qpos, qvel, qacc, qfrc, status,
+                    c->worklist + 1, c->worklist, c->mirror.efc_count);
+    HIPCHECK(hipGetLastError());
+    hipLaunchKernelGGL(k_inverse_list, grid, block, 0, c->stream, c->dmodel, c->mirror,
+                       (const int*)(c->worklist + 1), (const int*)c->worklist, qfrc, status);
+    HIPCHECK(hipGetLastError());
+    return MJHIP_OK;
+  }
   switch (skipstage) {
   case mjhipSTAGE_NONE:
     hipLaunchKernelGGL(k_inverse<0>, grid, block, 0, c->stream, c->dmodel, c->mirror, B, qpos,
@@ -519,7 +594,7 @@ MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B, const mjtNum* qpos,
     }
   }
   if (qfrc_inverse) dqfrc = dev ? qfrc_inverse : sf;
-  int rc = launch_inverse(c, B, dq, dv, da, dqfrc, skipstage, c->status);
+  int rc = launch_inverse(c, B, dq, dv, da, dqfrc, skipstage, c->status, flags);
   if (rc) return rc;
   if (qfrc_inverse && !dev) {
     HIPCHECK(hipMemcpyAsync(qfrc_inverse, sf, sizeof(double)*(size_t)B*m.nv,
@@ -612,12 +687,12 @@ MJHIP_API int mjhip_mirrorUpload(mjhipContext* c, const char* field, int first, 
 
 MJHIP_API int mjhip_timeInverseKernel(mjhipContext* c, int B, int reps, int skipstage,
                                       int flags, float* ms) {
-  (void)flags;
   if (!c || B <= 0 || B > c->capacity || reps <= 0 || !ms) return MJHIP_ERR_ARG;
   HIPCHECK(hipSetDevice(c->device));
   HIPCHECK(hipEventRecord(c->ev0, c->stream));
   for (int r = 0; r < reps; r++) {
-    int rc = launch_inverse(c, B, nullptr, nullptr, nullptr, nullptr, skipstage, nullptr);
+    int rc = launch_inverse(c, B, nullptr, nullptr, nullptr, nullptr, skipstage, nullptr,
+                            flags);
     if (rc) return rc;
   }
   HIPCHECK(hipEventRecord(c->ev1, c->stream));

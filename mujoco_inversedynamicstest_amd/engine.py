@@ -25,7 +25,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmjhip.so")
 
 mjSTAGE_NONE, mjSTAGE_POS, mjSTAGE_VEL = 0, 1, 2
-FLAG_DEVICE_PTRS, FLAG_MIRROR_INPUT, FLAG_NO_MIRROR = 1, 2, 4
+FLAG_DEVICE_PTRS, FLAG_MIRROR_INPUT, FLAG_NO_MIRROR, FLAG_GENERIC = 1, 2, 4, 8
 ERR = {0: "OK", -1: "NO_DEVICE", -2: "ARG", -3: "HIP", -4: "MODEL", -5: "CAPACITY",
        1: "INSTANCE"}
 INST_BITS = {1: "BADQPOS", 2: "BADQVEL", 4: "BADQACC", 8: "INERTIA", 16: "CNSTRFULL",
@@ -47,6 +47,8 @@ SIGNATURES = {
                                            ctypes.POINTER(_V)]),
     "mjhip_contextFree": (None, [_V]),
     "mjhip_contextCapacity": (ctypes.c_int, [_V]),
+    "mjhip_contextFastKernel": (ctypes.c_char_p, [_V]),
+    "mjhip_worklistCount": (ctypes.c_int, [_V]),
     "mjhip_contextStream": (_V, [_V]),
     "mjhip_contextSetStream": (ctypes.c_int, [_V, _V]),
     "mjhip_inverseBatch": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, _V, ctypes.c_int,
@@ -155,15 +157,24 @@ class InverseEngine:
   def set_stream(self, stream_handle: int):
     _check(lib().mjhip_contextSetStream(self.ctx, stream_handle), "mjhip_contextSetStream")
 
+  @property
+  def fast_kernel(self):
+    """Name of the model-specialized kernel in use, or None (generic kernel)."""
+    n = lib().mjhip_contextFastKernel(self.ctx)
+    return n.decode() if n else None
+
+  def worklist_count(self):
+    return lib().mjhip_worklistCount(self.ctx)
+
   def inverse(self, qpos=None, qvel=None, qacc=None, out=None, skipstage=mjSTAGE_NONE,
-              skipsensor=0, mirror_input=False, status=False):
+              skipsensor=0, mirror_input=False, status=False, generic=False):
     """Batched mj_inverseSkip. numpy arrays (host) or float64 torch tensors (device).
 
     Returns qfrc_inverse [B, nv] (numpy for host inputs; `out` for device tensors). With
     mirror_input=True the inputs already in the mirror are used (pass B via qpos=int).
     """
     L = lib()
-    flags = 0
+    flags = FLAG_GENERIC if generic else 0
     if mirror_input:
       B = int(qpos)
       flags |= FLAG_MIRROR_INPUT
@@ -221,10 +232,12 @@ class InverseEngine:
     self.set_field("qvel", qvel, first)
     self.set_field("qacc", qacc, first)
 
-  def time_kernel(self, B, reps=20, skipstage=mjSTAGE_NONE):
-    """Average ms per launch of the fused kernel on mirror-resident inputs (HIP events)."""
+  def time_kernel(self, B, reps=20, skipstage=mjSTAGE_NONE, generic=False):
+    """Average ms per launch of the mj_inverse kernels on mirror-resident inputs (HIP
+    events on the context's stream; fast path = straight-line kernel + work-list kernel)."""
     ms = ctypes.c_float()
-    _check(lib().mjhip_timeInverseKernel(self.ctx, B, reps, skipstage, 0, ctypes.byref(ms)),
+    _check(lib().mjhip_timeInverseKernel(self.ctx, B, reps, skipstage,
+                                         FLAG_GENERIC if generic else 0, ctypes.byref(ms)),
            "mjhip_timeInverseKernel")
     return ms.value
 

@@ -125,3 +125,37 @@ def output_doubles(sizes: dict) -> int:
 def input_doubles(sizes: dict) -> int:
   """R of SURVEY.md §8d: fp64 values read per instance (qpos, qvel, qacc)."""
   return sum(f.size(sizes) for f in DATA_FIELDS if f.stage == 0)
+
+
+def model_signature(m) -> int:
+  """FNV-1a 64 over sizes, options and every model array, in field-table order.
+
+  Identical to model_signature() in csrc/mjhip.hip, so a generated straight-line kernel is
+  only ever used for a bit-identical model.
+  """
+  h = 0xcbf29ce484222325
+  prime = 0x100000001b3
+  mask = (1 << 64) - 1
+
+  def feed(b: bytes):
+    nonlocal h
+    for byte in b:
+      h ^= byte
+      h = (h * prime) & mask
+
+  for k in MODEL_SIZES:
+    feed(np.int32(m.sizes.get(k, 0)).tobytes())
+  o = m.opt
+  for k in ("timestep", "impratio"):
+    feed(np.float64(o[k]).tobytes())
+  for k, n in (("gravity", 3), ("wind", 3)):
+    feed(np.asarray(o[k], dtype=np.float64)[:n].tobytes())
+  for k in ("density", "viscosity", "o_margin"):
+    feed(np.float64(o[k]).tobytes())
+  feed(np.asarray(o["o_solref"], dtype=np.float64)[:2].tobytes())
+  feed(np.asarray(o["o_solimp"], dtype=np.float64)[:5].tobytes())
+  for k in ("integrator", "cone", "jacobian", "disableflags", "enableflags"):
+    feed(np.int32(o[k]).tobytes())
+  for f in MODEL_FIELDS:
+    feed(np.ascontiguousarray(getattr(m, f.name), dtype=NPTYPE[f.ctype]).tobytes())
+  return h

@@ -1,0 +1,60 @@
+// codegen_harness.cpp — TEST ONLY: host build of a generated straight-line body
+// (codegen.py) plus the generic pipeline for its work-list, over a host mirror, so the test
+// suite can check the generated code bit-for-bit against the oracle without a GPU.
+#include <stdlib.h>
+#include <string.h>
+
+#include "../mujoco_inversedynamicstest_amd/csrc/engine_device.h"
+#include GEN_INC
+
+// fields: concatenated per-instance outputs, row-major [field][inst][k] in MJHIP_DATA_FIELDS
+// order; returns the number of work-list (limit-active) instances
+extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const double* qvel,
+                      const double* qacc, double* out, int efc_cap) {
+  const int nblk = (B + 63) / 64;
+  Mirror mr;
+  memset(&mr, 0, sizeof(mr));
+  const int nv = m->nv, nbody = m->nbody;
+  (void)nv; (void)nbody;
+#define MJ_M(n) m->n
+#define XD(name, d0, d1, stage) mr.name##_n = (m->d0) * (d1); \
+  mr.name = (double*)calloc((size_t)nblk * 64 * (mr.name##_n + 1), sizeof(double));
+  MJHIP_DATA_FIELDS
+#undef XD
+#define XSC(name, n) mr.name##_n = (n); \
+  mr.name = (double*)calloc((size_t)nblk * 64 * ((n) + 1), sizeof(double));
+  MJHIP_SCRATCH_FIELDS
+#undef XSC
+#define XSI(name, n) mr.name##_n = (n); \
+  mr.name = (int*)calloc((size_t)nblk * 64 * ((n) + 1), sizeof(int));
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+  mr.efc_cap = efc_cap;
+  int* wl = (int*)calloc(B + 1, sizeof(int));
+  int wc = 0;
+  for (int i = 0; i < B; i++) {
+    FAST_BODY(mr, i / 64, i % 64, B, qpos, qvel, qacc, nullptr, nullptr, wl, &wc,
+              mr.efc_count);
+  }
+  for (int g = 0; g < wc; g++) {
+    int inst = wl[g];
+    mjh::Lane<64> d = lane_view(mr, inst / 64, inst % 64);
+    mjh::inverseSkip(*m, d, 0);
+  }
+  size_t off = 0;
+#define XD(name, d0, d1, stage) { int S = mr.name##_n; \
+  for (int i = 0; i < B; i++) for (int k = 0; k < S; k++) \
+    out[off + (size_t)i*S + k] = mr.name[((size_t)(i/64)*S + k)*64 + (i%64)]; \
+  off += (size_t)B*S; free(mr.name); }
+  MJHIP_DATA_FIELDS
+#undef XD
+#undef MJ_M
+#define XSC(name, n) free(mr.name);
+  MJHIP_SCRATCH_FIELDS
+#undef XSC
+#define XSI(name, n) free(mr.name);
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+  free(wl);
+  return wc;
+}

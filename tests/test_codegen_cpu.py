@@ -1,0 +1,103 @@
+"""Generated straight-line kernels (codegen.py), compiled for the host, vs the oracle.
+
+With -ffp-contract=off every mjData output of the generated code must equal the oracle's
+BIT FOR BIT, including instances whose limits are active (those take the work-list path
+through the generic pipeline).
+"""
+import ctypes
+import hashlib
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from mujoco_inversedynamicstest_amd import codegen, fields, host, mjcf, models
+from mujoco_inversedynamicstest_amd.sampler import sample_states
+from oracle.oracle import Oracle
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(HERE, "_build")
+
+
+def build(m, name):
+  src = codegen.generate(m, name)
+  tag = hashlib.sha1(src.encode()).hexdigest()[:10]
+  os.makedirs(BUILD, exist_ok=True)
+  inc = os.path.join(BUILD, f"gen_{name}_{tag}.inc")
+  so = os.path.join(BUILD, f"libcg_{name}_{tag}.so")
+  if not os.path.exists(so):
+    open(inc, "w").write(src)
+    subprocess.run(["g++", "-std=c++17", "-O1", "-ffp-contract=off", "-fPIC", "-shared",
+                    f'-DGEN_INC="{inc}"', f"-DFAST_BODY=fast_body_{name}", "-o", so,
+                    os.path.join(HERE, "codegen_harness.cpp")], check=True)
+  L = ctypes.CDLL(so)
+  L.cg_run.restype = ctypes.c_int
+  L.cg_run.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4 + [ctypes.c_int]
+  return L
+
+
+def run_and_compare(m, name, q, v, a):
+  L = build(m, name)
+  o = Oracle(m)
+  cm = host.model_struct(m)
+  B = len(q)
+  sizes = {f.name: f.size(m.sizes) for f in fields.DATA_FIELDS}
+  out = np.zeros(sum(sizes.values()) * B)
+  q, v, a = (np.ascontiguousarray(x) for x in (q, v, a))
+  nwl = L.cg_run(ctypes.byref(cm), B, q.ctypes.data, v.ctypes.data, a.ctypes.data,
+                 out.ctypes.data, o.efc.capacity)
+  res, off = {}, 0
+  for f in fields.DATA_FIELDS:
+    res[f.name] = out[off:off + B * sizes[f.name]].reshape(B, sizes[f.name])
+    off += B * sizes[f.name]
+  nefc = 0
+  for i in range(B):
+    o.inverse(q[i], v[i], a[i])
+    nefc += o.d.nefc > 0
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(res[f.name][i], getattr(o.d, f.name),
+                                      err_msg=f"{name}.{f.name} inst {i}")
+  assert nwl == nefc
+  return nwl
+
+
+def test_humanoid_generated_bitexact(humanoid):
+  q, v, a = sample_states(humanoid, 96)
+  assert run_and_compare(humanoid, "humanoid", q, v, a) == 0
+
+
+def test_humanoid_generated_worklist(humanoid):
+  q, v, a = sample_states(humanoid, 64, first=5000, margin=-0.1, resample_tendons=False)
+  assert run_and_compare(humanoid, "humanoid", q, v, a) > 10
+
+
+@pytest.mark.parametrize("name", ["inverse_test", "linear", "inertia"])
+def test_small_models_generated_bitexact(name):
+  m = models.load(name, disable_contact=True)
+  q, v, a = sample_states(m, 40, first=3)
+  run_and_compare(m, name, q, v, a)
+
+
+def test_generated_all_branches():
+  """gravcomp, ball/slide/free joints, tendon spring-damper, cameras/lights of all modes."""
+  xml = """<mujoco><option><flag contact="disable"/></option><worldbody>
+    <light mode="targetbody" target="b1" pos="1 0 2"/><light mode="track" pos="0 1 2"/>
+    <camera mode="targetbodycom" target="b1" pos="2 0 1"/>
+    <body name="b1" pos="0 0 1" gravcomp="0.7"><freejoint/><geom size=".1"/>
+      <camera mode="track" pos="0 -1 0"/><site pos=".1 0 0" euler="0 30 0"/>
+      <body pos=".2 0 0" gravcomp="1"><joint name="a" axis="0 1 0" damping=".3"
+          range="-90 90"/>
+        <geom type="capsule" fromto="0 0 0 .3 0 0" size=".05"/>
+        <body pos=".3 0 0"><joint name="b" type="ball" stiffness="2" pos="0 0 .01"/>
+          <geom type="box" size=".05 .1 .02" pos=".1 0 0" euler="10 20 30"/>
+          <geom type="sphere" size=".03" pos="0 .05 0"/></body>
+        <body pos=".3 0 0"><joint name="c" type="slide" axis="1 1 0" stiffness="3"/>
+          <geom size=".04"/></body>
+      </body></body></worldbody>
+    <tendon><fixed stiffness="5" damping=".2" springlength=".1" range="-1 1">
+      <joint joint="a" coef="1"/><joint joint="c" coef="-.5"/></fixed></tendon></mujoco>"""
+  m = mjcf.load_xml_string(xml)
+  q, v, a = sample_states(m, 40)
+  run_and_compare(m, "allbranches", q, v, a)

@@ -234,3 +234,22 @@ def test_device_tensor_io(humanoid, eng):
   # the library stream is non-blocking w.r.t. torch: synchronize it too
   ref = eng.inverse(q, v, a)
   np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+def test_fast_kernel_selected(eng):
+  """The bundled humanoid runs the model-specialized straight-line kernel (codegen.py)."""
+  assert eng.fast_kernel == "humanoid"
+
+
+def test_fast_vs_generic_and_worklist(humanoid, eng):
+  """Fast path (straight-line + work-list) vs the generic kernel on mixed states: every
+  instance whose limits are active is recomputed through the work-list."""
+  q, v, a = sample_states(humanoid, 2048, first=20000, margin=-0.02, resample_tendons=False)
+  f_fast = eng.inverse(q, v, a)
+  n_wl = eng.worklist_count()
+  f_gen = eng.inverse(q, v, a, generic=True)
+  _, nefc = oracle_batch(humanoid, q, v, a)
+  assert n_wl == int((nefc > 0).sum()) > 0
+  assert_close(f_fast, f_gen, "fast vs generic")
+  ref, _ = oracle_batch(humanoid, q, v, a)
+  assert_close(f_fast, ref["qfrc_inverse"], "fast vs oracle")
