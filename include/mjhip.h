@@ -6,14 +6,17 @@
  *   reference entry point (file:line)                          replaced by
  *   ---------------------------------------------------------  -------------------------------
  *   mj_inverse        src/engine/engine_inverse.c:266          mjhip_inverse
- *                     include/mujoco/mujoco.h:283-284
+ *                     include/mujoco/mujoco.h:131
  *   mj_inverseSkip    src/engine/engine_inverse.c:197          mjhip_inverseSkip
- *                     include/mujoco/mujoco.h:289-292
+ *                     include/mujoco/mujoco.h:137
  *   mj_invPosition    src/engine/engine_inverse.c:37           mjhip_invPosition
+ *                     src/engine/engine_inverse.h:34
  *   mj_invVelocity    src/engine/engine_inverse.c:73           mjhip_invVelocity
+ *                     src/engine/engine_inverse.h:37
  *   mj_invConstraint  src/engine/engine_inverse.c:169          mjhip_invConstraint
- *                     (all three: src/engine/engine_inverse.h:27-43)
+ *                     src/engine/engine_inverse.h:40
  *   mj_compareFwdInv  src/engine/engine_inverse.c:275          mjhip_compareFwdInv
+ *                     src/engine/engine_inverse.h:43
  *   mj_rne            src/engine/engine_core_smooth.c:1969     mjhip_rne
  *                     include/mujoco/mujoco.h:361
  *   mjd_inverseFD     src/engine/engine_derivative_fd.c:611    mjhip_inverseFDBatch (batched)

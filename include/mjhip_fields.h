@@ -40,8 +40,8 @@
   XS(nkey)        \
   XS(ntree)
 
-/* model arrays (mjxmacro.h MJMODEL_POINTERS order within each group) */
-#define MJHIP_MODEL_POINTERS \
+/* model arrays that live in mjModel in the reference (mjxmacro.h MJMODEL_POINTERS) */
+#define MJHIP_MODEL_POINTERS_M \
   X(mjtNum,  qpos0,                nq,        1) \
   X(mjtNum,  qpos_spring,          nq,        1) \
   X(int,     body_parentid,        nbody,     1) \
@@ -167,7 +167,12 @@
   X(mjtNum,  actuator_length0,     nu,        1) \
   X(mjtNum,  actuator_acc0,        nu,        1) \
   X(int,     exclude_signature,    nexclude,  1) \
-  X(mjtNum,  key_qpos,             nkey,      MJ_M(nq)) \
+  X(mjtNum,  key_qpos,             nkey,      MJ_M(nq))
+
+/* model-constant sparse structures that live in mjData in the reference
+ * (engine_io.c:1977-1989 for C/mapM2C; mj_transmission writes moment_* each call,
+ * engine_core_smooth.c:865-916, constant for joint transmissions) */
+#define MJHIP_MODEL_POINTERS_D \
   X(int,     C_rownnz,             nv,        1) \
   X(int,     C_rowadr,             nv,        1) \
   X(int,     C_colind,             nC,        1) \
@@ -175,6 +180,10 @@
   X(int,     moment_rownnz,        nu,        1) \
   X(int,     moment_rowadr,        nu,        1) \
   X(int,     moment_colind,        nJmom,     1)
+
+#define MJHIP_MODEL_POINTERS \
+  MJHIP_MODEL_POINTERS_M      \
+  MJHIP_MODEL_POINTERS_D
 
 /* Per-instance fp64 mjData fields produced or consumed by mj_inverseSkip, in pipeline order.
  * XD(name, dim0, dim1, stage): stage 0 = input, 1 = position, 2 = velocity, 3 = acceleration.

@@ -1112,7 +1112,7 @@ MJH_HD void referenceConstraint(const mjhipModel& m, const Lane<S>& d) {
 }
 
 // mj_invConstraint engine_inverse.c:169-192 with mj_constraintUpdate_island :2387-2549
-// (island < 0, no cost; the fork leaves the elliptic-cone branch empty)
+// (island < 0, no cost; elliptic-cone rows come only from contacts: outside this subset)
 template <int S>
 MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
   int nv = m.nv, nefc = d.efc_count[0];

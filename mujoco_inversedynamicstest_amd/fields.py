@@ -63,10 +63,11 @@ def _parse():
   text = open(FIELDS_HEADER).read()
   sizes = re.findall(r"XS\((\w+)\)", _macro_body(text, "MJHIP_MODEL_SIZES"))
   model = []
-  for ct, nm, d0, d1 in re.findall(
-      r"X\(\s*(\w+)\s*,\s*(\w+)\s*,\s*(\w+)\s*,\s*([\w()]+)\s*\)",
-      _macro_body(text, "MJHIP_MODEL_POINTERS")):
-    model.append(ModelField(ct, nm, d0, d1))
+  for group in ("MJHIP_MODEL_POINTERS_M", "MJHIP_MODEL_POINTERS_D"):
+    for ct, nm, d0, d1 in re.findall(
+        r"X\(\s*(\w+)\s*,\s*(\w+)\s*,\s*(\w+)\s*,\s*([\w()]+)\s*\)",
+        _macro_body(text, group)):
+      model.append(ModelField(ct, nm, d0, d1))
   data = []
   for group in ("MJHIP_DATA_INPUTS", "MJHIP_DATA_POSITION", "MJHIP_DATA_VELOCITY",
                 "MJHIP_DATA_ACCELERATION"):

@@ -1248,7 +1248,8 @@ static void or_referenceConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) 
   }
 }
 
-/* :2387-2549 (island < 0, cost = NULL); this fork leaves the elliptic branch empty */
+/* :2387-2549 (island < 0, cost = NULL); elliptic-cone rows come only from contacts, which
+ * are outside the supported subset */
 static void or_constraintUpdate(const mjhipModel* m, mjhipData* d, orEfc* e, const mjtNum* jar) {
   int ne = e->ne, nf = e->nf, nefc = e->nefc;
   const mjtNum *D = e->efc_D, *R = e->efc_R, *floss = e->efc_frictionloss;
