@@ -133,8 +133,8 @@ def main():
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "kernel": f"k_fast_{eng.fast_kernel}+k_inverse_list" if eng.fast_kernel
-                               else "k_inverse<0>",
+                     "kernel": (f"k_pos+k_fac+k_vel+k_acc_{eng.fast_kernel}+k_inverse_list"
+                                if eng.fast_kernel else "k_inverse<0>"),
                      "kernel_ms": kernel_ms, "generic_kernel_ms": generic_ms,
                      "bytes_per_eval": bytes_per_eval},
         "cpu_baseline": cpu,

@@ -154,6 +154,39 @@ template <class V> MJH_HD double normalize4(V v) {
   return norm;
 }
 
+// Branch-free forms of addToScl-if-nonzero / normalize3 / normalize4 for the generated
+// kernels. Results are identical to the branching forms (same operations, selected). A
+// straight-line body without branches is one scheduling region, so the compiler cannot sink
+// computation into later basic blocks, away from the loads the kernel prefetched for it.
+template <class R, class A> MJH_HD void addToSclIf(R r, A a, double s, int n) {
+  for (int i = 0; i < n; i++) {
+    double t = r[i] + a[i]*s;
+    r[i] = s ? t : r[i];
+  }
+}
+
+template <class V> MJH_HD double normalize3s(V v) {
+  double norm = sqrt(v[0]*v[0] + v[1]*v[1] + v[2]*v[2]);
+  bool small = norm < MINVAL;
+  double normInv = 1/norm;
+  double a0 = v[0]*normInv, a1 = v[1]*normInv, a2 = v[2]*normInv;
+  v[0] = small ? 1.0 : a0; v[1] = small ? 0.0 : a1; v[2] = small ? 0.0 : a2;
+  return norm;
+}
+
+template <class V> MJH_HD double normalize4s(V v) {
+  double norm = sqrt(v[0]*v[0] + v[1]*v[1] + v[2]*v[2] + v[3]*v[3]);
+  bool small = norm < MINVAL;
+  bool scale = !small && fabs(norm - 1) > MINVAL;
+  double normInv = 1/norm;
+  double a0 = v[0]*normInv, a1 = v[1]*normInv, a2 = v[2]*normInv, a3 = v[3]*normInv;
+  v[0] = small ? 1.0 : (scale ? a0 : v[0]);
+  v[1] = small ? 0.0 : (scale ? a1 : v[1]);
+  v[2] = small ? 0.0 : (scale ? a2 : v[2]);
+  v[3] = small ? 0.0 : (scale ? a3 : v[3]);
+  return norm;
+}
+
 // engine_util_blas.c:165-176
 template <class R, class M, class V> MJH_HD void mulMatVec3(R res, M mat, V vec) {
   double t0 = mat[0]*vec[0] + mat[1]*vec[1] + mat[2]*vec[2];
@@ -1236,6 +1269,24 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
   #define MJH_ATOMIC_ADD(p, v) atomicAdd((p), (v))
 #else
   #define MJH_ATOMIC_ADD(p, v) ((*(p) += (v)) - (v))
+#endif
+
+// Value barrier: the compiler must treat x as recomputed here, so expressions of x after the
+// barrier are not merged with the same expressions before it (used by the generated kernels
+// to recompute kinematics instead of keeping the first pass's frames live). No code emitted.
+#if defined(__HIP_DEVICE_COMPILE__)
+  #define MJH_OPAQUE(x) asm volatile("" : "+v"(x))
+#else
+  #define MJH_OPAQUE(x) asm volatile("" : "+m"(x))
+#endif
+
+// Scheduling fence for the generated kernels: the machine scheduler may not move any
+// instruction across it. It keeps a body's prefetched loads from being hoisted to the top of
+// the kernel, where they would all be live at once and spill.
+#if defined(__HIP_DEVICE_COMPILE__)
+  #define MJH_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+#else
+  #define MJH_SCHED_FENCE() ((void)0)
 #endif
 
 #endif  // MJHIP_ENGINE_DEVICE_H_
