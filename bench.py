@@ -55,7 +55,7 @@ def main():
     torch.cuda.set_device(local)
   dev = torch.device("cuda", local)
 
-  from mujoco_inversedynamicstest_amd import engine, fields, models, parallel
+  from mujoco_inversedynamicstest_amd import codegen, engine, fields, models, parallel
   from mujoco_inversedynamicstest_amd.sampler import sample_states
 
   m = models.load(args.model, disable_contact=True)
@@ -133,8 +133,8 @@ def main():
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
-                     "kernel": (f"k_pos+k_fac+k_vel+k_acc_{eng.fast_kernel}+k_inverse_list"
-                                if eng.fast_kernel else "k_inverse<0>"),
+                     "kernel": ("+".join(f"k_{st}_{eng.fast_kernel}" for st in codegen.STAGES)
+                                + "+k_inverse_list" if eng.fast_kernel else "k_inverse<0>"),
                      "kernel_ms": kernel_ms, "generic_kernel_ms": generic_ms,
                      "bytes_per_eval": bytes_per_eval},
         "cpu_baseline": cpu,

@@ -46,8 +46,9 @@ import numpy as np
 from . import fields
 
 FREE, BALL, SLIDE, HINGE = 0, 1, 2, 3
-STAGES = ("pos", "fac", "vel", "acc")
-PREFETCH = 2      # bodies (pre-order) between a body's mirror loads and their first use
+STAGES = ("pos", "fac", "va")
+FRAMES_IN_PASS1 = True   # k_pos: pass 1 stores the frames, pass 2 cinert/cdof/crb/qM
+PREFETCH = 1      # tree-pass events between a body's mirror loads and their first use
 
 
 def lit(x) -> str:
@@ -291,7 +292,7 @@ def _emit_frame(G: _Stage, i, store):
         E(f"mjh::sub3(xpos_{i}, xanchor_{j}, vec);")
       E.close()
   E(f"mjh::normalize4s(xquat_{i});")
-  E(f"mjh::quat2Mat(xmat_{i}, xquat_{i});")
+  E(f"mjh::quat2Mats(xmat_{i}, xquat_{i});")
   if store:
     G.stv("xquat", 4 * i, f"xquat_{i}", 4)
     G.stv("xpos", 3 * i, f"xpos_{i}", 3)
@@ -319,7 +320,7 @@ def _emit_local2global(G: _Stage, dst_pos, dst_mat, pos, quat, body, sf, with_ma
       E(f"const double lq[4] = {arr_lit(quat)};")
       E("double tmp[4];")
       E(f"mjh::mulQuat(tmp, xquat_{body}, lq);")
-      E(f"mjh::quat2Mat({dst_mat}, tmp);")
+      E(f"mjh::quat2Mats({dst_mat}, tmp);")
     elif sf in (1, 3):
       E(f"mjh::copy({dst_mat}, xmat_{body}, 9);")
     else:
@@ -355,6 +356,8 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
   G = _Stage(M, store_fields)
   E, m = G.E, M.m
   nq, nv, dsbl = M.nq, M.nv, M.dsbl
+  # the next call's work-list counter (two alternate; stream order makes this safe)
+  E("if (worklist_next && blk == 0 && lane == 0) *worklist_next = 0;")
   G.prologue(check_flag=False)
   G.pointers([f.name for f in fields.DATA_FIELDS if f.stage <= 1])
   E(f"double qpos[{max(nq, 1)}];")
@@ -427,6 +430,16 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
       G.st("actuator_length", a, f"qpos[{int(m.jnt_qposadr[jid])}]*{lit(g)}")
       G.st("actuator_moment", int(m.moment_rowadr[a]), lit(g))
 
+  cams = {}
+  for c in range(m.ncam):
+    cams.setdefault(int(m.cam_bodyid[c]), []).append(("cam", c))
+  for l in range(m.nlight):
+    cams.setdefault(int(m.light_bodyid[l]), []).append(("light", l))
+  geoms, sites = {}, {}
+  for g in range(m.ngeom):
+    geoms.setdefault(int(m.geom_bodyid[g]), []).append(g)
+  for s in range(m.nsite):
+    sites.setdefault(int(m.site_bodyid[s]), []).append(s)
   # ---- pass 1: kinematics -> subtree centers of mass (mj_comPos :183-208)
   E("// ---- tree pass 1: mj_kinematics -> mj_comPos subtree_com (post-order = descending)")
   need_stc, need_xpos = _camlight_needs(m)
@@ -438,12 +451,37 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
     E(f"double keep_xpos_{b}[3];")
   _world_frame(E)
 
+  def frame_outputs(i):
+    """xipos/ximat, geom and site frames of body i (stored by whichever pass owns them)."""
+    G.stv("xipos", 3 * i, f"xipos_{i}", 3)
+    G.stv("ximat", 9 * i, f"ximat_{i}", 9)
+    for g in geoms.get(i, []):
+      E.open()
+      _emit_local2global(G, "gp", "gm", m.geom_pos[g], m.geom_quat[g], i,
+                         int(m.geom_sameframe[g]))
+      G.stv("geom_xpos", 3 * g, "gp", 3)
+      G.stv("geom_xmat", 9 * g, "gm", 9)
+      E.close()
+    for s in sites.get(i, []):
+      E.open()
+      _emit_local2global(G, "sp", "sm", m.site_pos[s], m.site_quat[s], i,
+                         int(m.site_sameframe[s]))
+      G.stv("site_xpos", 3 * s, "sp", 3)
+      G.stv("site_xmat", 9 * s, "sm", 9)
+      E.close()
+
   def pre1(i):
     E.open(f"{{  // body {i}")
     if i:
-      _emit_frame(G, i, store=False)
-      _emit_local2global(G, f"xipos_{i}", None, m.body_ipos[i], m.body_iquat[i], i,
-                         int(m.body_sameframe[i]), with_mat=False)
+      _emit_frame(G, i, store=FRAMES_IN_PASS1)
+      _emit_local2global(G, f"xipos_{i}", f"ximat_{i}", m.body_ipos[i], m.body_iquat[i], i,
+                         int(m.body_sameframe[i]), with_mat=FRAMES_IN_PASS1)
+    elif FRAMES_IN_PASS1:
+      G.stv("xpos", 0, "xpos_0", 3)
+      G.stv("xquat", 0, "xquat_0", 4)
+      G.stv("xmat", 0, "xmat_0", 9)
+    if FRAMES_IN_PASS1:
+      frame_outputs(i)
     if i in need_xpos:
       E(f"mjh::copy3(keep_xpos_{i}, xpos_{i});")
     E(f"double stc_{i}[3] = {{0.0, 0.0, 0.0}};")
@@ -468,44 +506,21 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
   E("// ---- tree pass 2: kinematics (stored), cinert, cdof, camlight, crb, qM")
   E(f"for (int k = 0; k < {nq}; k++) MJH_OPAQUE(qpos[k]);")
 
-  cams = {}
-  for c in range(m.ncam):
-    cams.setdefault(int(m.cam_bodyid[c]), []).append(("cam", c))
-  for l in range(m.nlight):
-    cams.setdefault(int(m.light_bodyid[l]), []).append(("light", l))
-  geoms, sites = {}, {}
-  for g in range(m.ngeom):
-    geoms.setdefault(int(m.geom_bodyid[g]), []).append(g)
-  for s in range(m.nsite):
-    sites.setdefault(int(m.site_bodyid[s]), []).append(s)
 
   def pre2(i):
     E.open(f"{{  // body {i}")
     if i:
-      _emit_frame(G, i, store=True)
+      _emit_frame(G, i, store=not FRAMES_IN_PASS1)
       _emit_local2global(G, f"xipos_{i}", f"ximat_{i}", m.body_ipos[i], m.body_iquat[i], i,
                          int(m.body_sameframe[i]))
     else:
       _world_frame(E)
-      G.stv("xpos", 0, "xpos_0", 3)
-      G.stv("xquat", 0, "xquat_0", 4)
-      G.stv("xmat", 0, "xmat_0", 9)
-    G.stv("xipos", 3 * i, f"xipos_{i}", 3)
-    G.stv("ximat", 9 * i, f"ximat_{i}", 9)
-    for g in geoms.get(i, []):
-      E.open()
-      _emit_local2global(G, "gp", "gm", m.geom_pos[g], m.geom_quat[g], i,
-                         int(m.geom_sameframe[g]))
-      G.stv("geom_xpos", 3 * g, "gp", 3)
-      G.stv("geom_xmat", 9 * g, "gm", 9)
-      E.close()
-    for s in sites.get(i, []):
-      E.open()
-      _emit_local2global(G, "sp", "sm", m.site_pos[s], m.site_quat[s], i,
-                         int(m.site_sameframe[s]))
-      G.stv("site_xpos", 3 * s, "sp", 3)
-      G.stv("site_xmat", 9 * s, "sm", 9)
-      E.close()
+      if not FRAMES_IN_PASS1:
+        G.stv("xpos", 0, "xpos_0", 3)
+        G.stv("xquat", 0, "xquat_0", 4)
+        G.stv("xmat", 0, "xmat_0", 9)
+    if not FRAMES_IN_PASS1:
+      frame_outputs(i)
     for kind, c in cams.get(i, []):
       _emit_camlight(G, kind, c)
     # cinert (mj_comPos :211-222), crb starts as a copy (mj_crb :1360)
@@ -701,15 +716,19 @@ def _gravity_acc(M, E):
     E(f"cacc_0[3] = {lit(g[0])}*-1; cacc_0[4] = {lit(g[1])}*-1; cacc_0[5] = {lit(g[2])}*-1;")
 
 
-def _gen_vel(M: _Model, store_fields=None) -> str:
+def _gen_va(M: _Model, store_fields=None) -> str:
+  """Velocity and acceleration stages in one kernel: fwdVelocity, passive, then one tree
+  pass with mj_comVel and both mj_rne calls (flg_acc = 0 -> qfrc_bias, 1 -> qfrc_inverse).
+  The two RNE recursions share cdof_dot*qvel and the gyroscopic term cvel x (cinert*cvel),
+  which the reference computes identically in each call."""
   G = _Stage(M, store_fields)
   E, m = G.E, M.m
   nv, nq, dsbl = M.nv, M.nq, M.dsbl
   G.prologue()
-  G.pointers(["qpos", "qvel", "cinert", "cdof", "xipos", "subtree_com", "ten_length",
-              "ten_velocity",
-              "actuator_velocity", "cvel", "cdof_dot", "qfrc_spring", "qfrc_damper",
-              "qfrc_gravcomp", "qfrc_fluid", "qfrc_passive", "qfrc_bias"])
+  G.pointers(["qpos", "qvel", "qacc", "cinert", "cdof", "xipos", "subtree_com", "ten_length",
+              "ten_velocity", "actuator_velocity", "cvel", "cdof_dot", "qfrc_spring",
+              "qfrc_damper", "qfrc_gravcomp", "qfrc_fluid", "qfrc_passive", "qfrc_bias",
+              "qfrc_constraint", "qfrc_inverse"])
   G.load("qpos", "qpos", nq)
   G.load("qvel", "qvel", nv)
   if m.ntendon:
@@ -799,11 +818,17 @@ def _gen_vel(M: _Model, store_fields=None) -> str:
     else:
       G.st("qfrc_passive", dof, f"qfs[{dof}] + qfd[{dof}]")
 
-  # mj_comVel (:1833-1896) fused with mj_rne(flg_acc = 0) (:1969-2023) in one tree pass
-  E("// ---- tree pass: mj_comVel + mj_rne(flg_acc=0) -> qfrc_bias")
+  # mj_comVel (:1833-1896) and both mj_rne calls (:1969-2023) in one tree pass
+  E("// ---- tree pass: mj_comVel + mj_rne(flg_acc=0) + mj_rne(flg_acc=1)")
   E("double cvel_0[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};")
   G.stv("cvel", 0, "cvel_0", 6)
   _gravity_acc(M, E)
+  E("double acca_0[6]; mjh::copy(acca_0, cacc_0, 6);")
+  E(f"double qacc[{nv}];")
+  # row-major qfrc_inverse copy, or (no output array) a harmless second write of the mirror
+  # slot: a select instead of a branch keeps the pass one scheduling region
+  E(f"double* qo = qfrc_out ? qfrc_out + inst*{nv} : P_qfrc_inverse;")
+  E(f"const long qo_stride = qfrc_out ? 1 : 64;")
 
   def pre(i):
     if not i:
@@ -852,12 +877,40 @@ def _gen_vel(M: _Model, store_fields=None) -> str:
     G.stv("cvel", 6 * i, f"cvel_{i}", 6)
     for k in range(bda, bda + dn):
       G.stv("cdof_dot", 6 * k, f"cdofdot_{k}", 6)
-    _emit_rne_forward(E, M, i, flg_acc=False)
+    # forward step of both recursions (engine_core_smooth.c:1986-2006)
+    E(f"double cacc_{i}[6], cfrc_{i}[6], acca_{i}[6], frca_{i}[6];")
+    E.open()
+    E("double tmp[6], tmp1[6];")
+    _emit_muldofvec(E, "tmp", "cdofdot", bda, dn, "qvel")
+    E(f"mjh::add(cacc_{i}, cacc_{p}, tmp, 6);")
+    E(f"mjh::add(acca_{i}, acca_{p}, tmp, 6);")
+    _emit_muldofvec(E, "tmp", "cdof", bda, dn, "qacc")
+    E(f"mjh::addTo(acca_{i}, tmp, 6);")
+    E(f"mjh::mulInertVec(cfrc_{i}, cinert_{i}, cacc_{i});")
+    E(f"mjh::mulInertVec(frca_{i}, cinert_{i}, acca_{i});")
+    E(f"mjh::mulInertVec(tmp, cinert_{i}, cvel_{i});")
+    E(f"mjh::crossForce(tmp1, cvel_{i}, tmp);")
+    E(f"mjh::addTo(cfrc_{i}, tmp1, 6);")
+    E(f"mjh::addTo(frca_{i}, tmp1, 6);")
+    E.close()
 
   def post(i):
     if not i:
       return
-    _emit_rne_backward(G, M, i, "qfrc_bias")
+    # cfrc_i is final (children added in descending order): project, then add to the parent
+    # (engine_core_smooth.c:2008-2022); qfrc_inverse += armature*qacc - passive - constraint
+    for k in range(M.bdofadr[i], M.bdofadr[i] + M.bdofnum[i]):
+      G.st("qfrc_bias", k, f"mjh::dot6(cdofp_{k}, cfrc_{i})")
+      E.open()
+      E(f"double qfi = mjh::dot6(cdofp_{k}, frca_{i});")
+      E(f"qfi += {lit(m.dof_armature[k])} * qacc[{k}] - qfp_{k} - 0.0;")
+      G.st("qfrc_constraint", k, "0.0")
+      G.st("qfrc_inverse", k, "qfi")
+      E(f"qo[{k}*qo_stride] = qfi;")
+      E.close()
+    if M.parent[i]:
+      E(f"mjh::addTo(cfrc_{M.parent[i]}, cfrc_{i}, 6);")
+      E(f"mjh::addTo(frca_{M.parent[i]}, frca_{i}, 6);")
     E.close()
 
   def loads(kind, i):
@@ -866,15 +919,17 @@ def _gen_vel(M: _Model, store_fields=None) -> str:
       decls = [f"double cinert_{i}[10];"] + [f"double cdof_{k}[6];" for k in dofs]
       ld = _vec_loads(f"cinert_{i}", "cinert", 10 * i, 10)
       for k in dofs:
-        ld += _vec_loads(f"cdof_{k}", "cdof", 6 * k, 6)
-    else:   # the projection reloads cdof rather than keeping it live along the path
-      decls = [f"double cdofp_{k}[6];" for k in dofs]
+        ld += _vec_loads(f"cdof_{k}", "cdof", 6 * k, 6) + [(f"qacc[{k}]", "qacc", k)]
+    else:   # the projections reload cdof rather than keeping it live along the path
+      decls = [f"double cdofp_{k}[6], qfp_{k};" for k in dofs]
       ld = []
       for k in dofs:
-        ld += _vec_loads(f"cdofp_{k}", "cdof", 6 * k, 6)
+        ld += _vec_loads(f"cdofp_{k}", "cdof", 6 * k, 6) + [(f"qfp_{k}", "qfrc_passive", k)]
     return decls, ld
 
   _prefetched_dfs(G, loads, pre, post, PREFETCH)
+  E("ec[0] = 0; ec[64] = 0; ec[128] = 0; ec[192] = 0;")
+  E("if (status) status[inst] = 0;")
   return E.text()
 
 
@@ -915,94 +970,6 @@ def _emit_applyforce(E, M, b):
   E.close()
 
 
-def _emit_rne_forward(E, M, i, flg_acc):
-  """mj_rne forward step for body i (engine_core_smooth.c:1986-2006)."""
-  bda, dn = M.bdofadr[i], M.bdofnum[i]
-  E(f"double cacc_{i}[6], cfrc_{i}[6];")
-  E.open()
-  E("double tmp[6], tmp1[6];")
-  _emit_muldofvec(E, "tmp", "cdofdot", bda, dn, "qvel")
-  E(f"mjh::add(cacc_{i}, cacc_{M.parent[i]}, tmp, 6);")
-  if flg_acc:
-    _emit_muldofvec(E, "tmp", "cdof", bda, dn, "qacc")
-    E(f"mjh::addTo(cacc_{i}, tmp, 6);")
-  E(f"mjh::mulInertVec(cfrc_{i}, cinert_{i}, cacc_{i});")
-  E(f"mjh::mulInertVec(tmp, cinert_{i}, cvel_{i});")
-  E(f"mjh::crossForce(tmp1, cvel_{i}, tmp);")
-  E(f"mjh::addTo(cfrc_{i}, tmp1, 6);")
-  E.close()
-
-
-def _emit_rne_backward(G, M, i, field):
-  """cfrc_i is final (children added in descending order): project onto the body's dofs,
-  then add into the parent (engine_core_smooth.c:2008-2022)."""
-  E = G.E
-  for k in range(M.bdofadr[i], M.bdofadr[i] + M.bdofnum[i]):
-    if field == "qfrc_bias":
-      G.st(field, k, f"mjh::dot6(cdofp_{k}, cfrc_{i})")
-    else:
-      # qfrc_inverse += armature*qacc - qfrc_passive - qfrc_constraint (nefc = 0)
-      E(f"qfi_{k} = mjh::dot6(cdofp_{k}, cfrc_{i});")
-      E(f"qfi_{k} += {lit(M.m.dof_armature[k])} * qacc[{k}] - qfp_{k} - 0.0;")
-  if M.parent[i]:
-    E(f"mjh::addTo(cfrc_{M.parent[i]}, cfrc_{i}, 6);")
-
-
-def _gen_acc(M: _Model, store_fields=None) -> str:
-  G = _Stage(M, store_fields)
-  E, m = G.E, M.m
-  nv = M.nv
-  G.prologue()
-  G.pointers(["qvel", "qacc", "cinert", "cdof", "cvel", "cdof_dot", "qfrc_passive",
-              "qfrc_constraint", "qfrc_inverse"])
-  E(f"double qvel[{nv}], qacc[{nv}], {', '.join(f'qfi_{k}' for k in range(nv))};")
-  E("// ---- mj_invConstraint (nefc = 0) and mj_rne(flg_acc = 1)")
-  _gravity_acc(M, E)
-
-  def pre(i):
-    if not i:
-      return
-    bda, dn = M.bdofadr[i], M.bdofnum[i]
-    E.open(f"{{  // body {i}")
-    _emit_rne_forward(E, M, i, flg_acc=True)
-
-  def post(i):
-    if not i:
-      return
-    _emit_rne_backward(G, M, i, "qfrc_inverse")
-    E.close()
-
-  def loads(kind, i):
-    dofs = range(M.bdofadr[i], M.bdofadr[i] + M.bdofnum[i])
-    if kind == "pre":
-      decls = [f"double cinert_{i}[10], cvel_{i}[6];"]
-      ld = _vec_loads(f"cinert_{i}", "cinert", 10 * i, 10) + _vec_loads(f"cvel_{i}", "cvel",
-                                                                         6 * i, 6)
-      for k in dofs:
-        decls.append(f"double cdof_{k}[6], cdofdot_{k}[6];")
-        ld += _vec_loads(f"cdof_{k}", "cdof", 6 * k, 6)
-        ld += _vec_loads(f"cdofdot_{k}", "cdof_dot", 6 * k, 6)
-        ld += [(f"qvel[{k}]", "qvel", k), (f"qacc[{k}]", "qacc", k)]
-    else:
-      decls = [f"double cdofp_{k}[6], qfp_{k};" for k in dofs]
-      ld = []
-      for k in dofs:
-        ld += _vec_loads(f"cdofp_{k}", "cdof", 6 * k, 6) + [(f"qfp_{k}", "qfrc_passive", k)]
-    return decls, ld
-
-  _prefetched_dfs(G, loads, pre, post, PREFETCH)
-  for k in range(nv):
-    G.st("qfrc_constraint", k, "0.0")
-    G.st("qfrc_inverse", k, f"qfi_{k}")
-  E("if (qfrc_out) {")
-  for k in range(nv):
-    E(f"  qfrc_out[inst*{nv} + {k}] = qfi_{k};")
-  E("}")
-  E("ec[0] = 0; ec[64] = 0; ec[128] = 0; ec[192] = 0;")
-  E("if (status) status[inst] = 0;")
-  return E.text()
-
-
 # ------------------------------------------------------------------------------ assembly
 def model_hash(m) -> str:
   h = hashlib.sha1()
@@ -1015,13 +982,15 @@ def model_hash(m) -> str:
 _SIG = {
     "pos": ("const double* __restrict__ qpos_in, const double* __restrict__ qvel_in, "
             "const double* __restrict__ qacc_in, int* __restrict__ worklist, "
-            "int* __restrict__ worklist_count, int* __restrict__ efc_count",
-            "qpos_in, qvel_in, qacc_in, worklist, worklist_count, efc_count"),
+            "int* __restrict__ worklist_count, int* __restrict__ worklist_next, "
+            "int* __restrict__ efc_count",
+            "qpos_in, qvel_in, qacc_in, worklist, worklist_count, worklist_next, efc_count"),
     "fac": ("int* __restrict__ efc_count", "efc_count"),
-    "vel": ("int* __restrict__ efc_count", "efc_count"),
-    "acc": ("double* __restrict__ qfrc_out, int* __restrict__ status, "
-            "int* __restrict__ efc_count", "qfrc_out, status, efc_count"),
+    "va": ("double* __restrict__ qfrc_out, int* __restrict__ status, "
+           "int* __restrict__ efc_count", "qfrc_out, status, efc_count"),
 }
+_GEN = {"pos": lambda M, sf: _gen_pos(M, sf), "fac": lambda M, sf: _gen_fac(M, sf),
+        "va": lambda M, sf: _gen_va(M, sf)}
 
 
 def generate(m, name: str, store_fields=None) -> str:
@@ -1036,8 +1005,7 @@ def generate(m, name: str, store_fields=None) -> str:
   if why:
     raise ValueError(f"model '{name}' cannot use the straight-line kernels: {why}")
   M = _Model(m)
-  bodies = {"pos": _gen_pos(M, store_fields), "fac": _gen_fac(M, store_fields),
-            "vel": _gen_vel(M, store_fields), "acc": _gen_acc(M, store_fields)}
+  bodies = {st: _GEN[st](M, store_fields) for st in STAGES}
   out = [f"// GENERATED by mujoco_inversedynamicstest_amd/codegen.py -- do not edit.",
          f"// model '{name}' (nq={m.nq} nv={m.nv} nbody={m.nbody}), hash {model_hash(m)}"]
   for st in STAGES:
@@ -1048,13 +1016,10 @@ def generate(m, name: str, store_fields=None) -> str:
     const Mirror& mr, int blk, int lane, int B, const double* __restrict__ qpos_in,
     const double* __restrict__ qvel_in, const double* __restrict__ qacc_in,
     double* __restrict__ qfrc_out, int* __restrict__ status, int* __restrict__ worklist,
-    int* __restrict__ worklist_count, int* __restrict__ efc_count) {{
-  fast_pos_{name}(mr, blk, lane, B, {_SIG['pos'][1]});
-  fast_fac_{name}(mr, blk, lane, B, {_SIG['fac'][1]});
-  fast_vel_{name}(mr, blk, lane, B, {_SIG['vel'][1]});
-  fast_acc_{name}(mr, blk, lane, B, {_SIG['acc'][1]});
-}}
-""")
+    int* __restrict__ worklist_count, int* __restrict__ worklist_next,
+    int* __restrict__ efc_count) {{
+""" + "".join(f"  fast_{st}_{name}(mr, blk, lane, B, {_SIG[st][1]});\n" for st in STAGES)
+             + "}\n")
   out.append("#if defined(__HIPCC__)")
   for st in STAGES:
     params, args = _SIG[st]
@@ -1062,7 +1027,7 @@ def generate(m, name: str, store_fields=None) -> str:
                f"{params}) {{\n  fast_{st}_{name}(mr, blockIdx.x, threadIdx.x, B, {args});\n}}")
   out.append(f"""static void launch_fast_{name}(dim3 g, dim3 b, hipStream_t s, const Mirror& mr,
     int B, const double* qpos_in, const double* qvel_in, const double* qacc_in, double* qfrc_out,
-    int* status, int* worklist, int* worklist_count, int* efc_count) {{""")
+    int* status, int* worklist, int* worklist_count, int* worklist_next, int* efc_count) {{""")
   for st in STAGES:
     out.append(f"  hipLaunchKernelGGL(k_{st}_{name}, g, b, 0, s, mr, B, {_SIG[st][1]});")
   out.append("}")

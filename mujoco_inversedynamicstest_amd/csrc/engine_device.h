@@ -330,6 +330,22 @@ template <class R, class Q> MJH_HD void quat2Mat(R res, Q quat) {
   }
 }
 
+// quat2Mat with the identity test as selects (generated kernels; see normalize4s)
+template <class R, class Q> MJH_HD void quat2Mats(R res, Q quat) {
+  const bool id = quat[0] == 1 && quat[1] == 0 && quat[2] == 0 && quat[3] == 0;
+  const double q00 = quat[0]*quat[0], q01 = quat[0]*quat[1], q02 = quat[0]*quat[2];
+  const double q03 = quat[0]*quat[3], q11 = quat[1]*quat[1], q12 = quat[1]*quat[2];
+  const double q13 = quat[1]*quat[3], q22 = quat[2]*quat[2], q23 = quat[2]*quat[3];
+  const double q33 = quat[3]*quat[3];
+  const double r0 = q00 + q11 - q22 - q33, r4 = q00 - q11 + q22 - q33;
+  const double r8 = q00 - q11 - q22 + q33;
+  const double r1 = 2*(q12 - q03), r2 = 2*(q13 + q02), r3 = 2*(q12 + q03);
+  const double r5 = 2*(q23 - q01), r6 = 2*(q13 - q02), r7 = 2*(q23 + q01);
+  res[0] = id ? 1.0 : r0; res[1] = id ? 0.0 : r1; res[2] = id ? 0.0 : r2;
+  res[3] = id ? 0.0 : r3; res[4] = id ? 1.0 : r4; res[5] = id ? 0.0 : r5;
+  res[6] = id ? 0.0 : r6; res[7] = id ? 0.0 : r7; res[8] = id ? 1.0 : r8;
+}
+
 // :385-396
 template <class R, class A, class B> MJH_HD void crossMotion(R res, A vel, B v) {
   double r0 = -vel[2]*v[1] + vel[1]*v[2];

@@ -33,7 +33,7 @@ using mjh::SP;
 struct FastKernelEntry {
   unsigned long long sig;
   void (*launch)(dim3, dim3, hipStream_t, const Mirror&, int, const double*, const double*,
-                 const double*, double*, int*, int*, int*, int*);
+                 const double*, double*, int*, int*, int*, int*, int*);
   const char* name;
 };
 #if __has_include("gen_fast.inc")
@@ -228,7 +228,9 @@ struct mjhipContext_ {
   int* status = nullptr;
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   const FastKernelEntry* fast = nullptr;   // straight-line kernel for this model, if any
-  int* worklist = nullptr;                 // capacity + 1 ints: [count, list...]
+  int* worklist = nullptr;                 // capacity + 2 ints: [count0, count1, list...]
+  int wl_parity = 0;                       // counter the next fast launch uses
+  int wl_last = 0;                         // counter the last fast launch used
 };
 
 // FNV-1a 64 over sizes, options and every model array (= fields.model_signature in Python)
@@ -458,7 +460,8 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
     set_error("hipMalloc(staging) failed");
     return MJHIP_ERR_HIP;
   }
-  if (hipMalloc((void**)&c->worklist, sizeof(int) * ((size_t)c->capacity + 1)) != hipSuccess) {
+  if (hipMalloc((void**)&c->worklist, sizeof(int) * ((size_t)c->capacity + 2)) != hipSuccess ||
+      hipMemset(c->worklist, 0, 2 * sizeof(int)) != hipSuccess) {
     set_error("hipMalloc(worklist) failed");
     return MJHIP_ERR_HIP;
   }
@@ -501,7 +504,8 @@ MJHIP_API const char* mjhip_contextFastKernel(const mjhipContext* c) {
 MJHIP_API int mjhip_worklistCount(mjhipContext* c) {
   if (!c) return -1;
   int n = 0;
-  if (hipMemcpy(&n, c->worklist, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  if (hipMemcpy(&n, c->worklist + c->wl_last, sizeof(int), hipMemcpyDeviceToHost) != hipSuccess)
+    return -1;
   return n;
 }
 
@@ -523,13 +527,18 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
                           int flags = 0) {
   dim3 grid((B + 63) / 64), block(64);
   if (skipstage == mjhipSTAGE_NONE && c->fast && !(flags & MJHIP_FLAG_GENERIC)) {
-    HIPCHECK(hipMemsetAsync(c->worklist, 0, sizeof(int), c->stream));
+    // two work-list counters alternate: this launch counts into `cnt` (zeroed by the
+    // previous launch's k_pos, or at context creation) and zeroes `nxt` for the next one
+    int* cnt = c->worklist + c->wl_parity;
+    int* nxt = c->worklist + (c->wl_parity ^ 1);
     c->fast->launch(grid, block, c->stream, c->mirror, B, qpos, qvel, qacc, qfrc, status,
-                    c->worklist + 1, c->worklist, c->mirror.efc_count);
+                    c->worklist + 2, cnt, nxt, c->mirror.efc_count);
     HIPCHECK(hipGetLastError());
     hipLaunchKernelGGL(k_inverse_list, grid, block, 0, c->stream, c->dmodel, c->mirror,
-                       (const int*)(c->worklist + 1), (const int*)c->worklist, qfrc, status);
+                       (const int*)(c->worklist + 2), (const int*)cnt, qfrc, status);
     HIPCHECK(hipGetLastError());
+    c->wl_last = c->wl_parity;
+    c->wl_parity ^= 1;
     return MJHIP_OK;
   }
   switch (skipstage) {

@@ -31,9 +31,9 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
 #undef XSI
   mr.efc_cap = efc_cap;
   int* wl = (int*)calloc(B + 1, sizeof(int));
-  int wc = 0;
+  int wc = 0, wnext = 1;
   for (int i = 0; i < B; i++) {
-    FAST_BODY(mr, i / 64, i % 64, B, qpos, qvel, qacc, nullptr, nullptr, wl, &wc,
+    FAST_BODY(mr, i / 64, i % 64, B, qpos, qvel, qacc, nullptr, nullptr, wl, &wc, &wnext,
               mr.efc_count);
   }
   for (int g = 0; g < wc; g++) {
