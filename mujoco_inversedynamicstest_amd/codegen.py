@@ -48,6 +48,7 @@ from . import fields
 FREE, BALL, SLIDE, HINGE = 0, 1, 2, 3
 STAGES = ("pos", "fac", "va")
 FRAMES_IN_PASS1 = True   # k_pos: pass 1 stores the frames, pass 2 cinert/cdof/crb/qM
+MAX_LDS_HINGES = 32
 PREFETCH = 1      # tree-pass events between a body's mirror loads and their first use
 
 
@@ -132,6 +133,10 @@ class _Model:
       if i:
         ms[self.parent[i]] = ms[self.parent[i]] + ms[i]
     self.subtree_mass = ms
+    # hinge joints whose sin/cos k_pos evaluates once, into LDS (2 doubles per lane each;
+    # 4 waves per CU must fit in 160 KB)
+    hinges = [j for j in range(m.njnt) if int(m.jnt_type[j]) == HINGE]
+    self.trig = {j: h for h, j in enumerate(hinges)} if 0 < len(hinges) <= MAX_LDS_HINGES else {}
     self.ten_terms = []
     for t in range(m.ntendon):
       adr, num = int(m.tendon_adr[t]), int(m.tendon_num[t])
@@ -285,7 +290,12 @@ def _emit_frame(G: _Stage, i, store):
           E(f"mjh::copy4(qloc, qpos + {qa});")
           E("mjh::normalize4s(qloc);")
         else:
-          E(f"mjh::axisAngle2Quat(qloc, jaxis, qpos[{qa}] - {lit(m.qpos0[qa])});")
+          if j in M.trig:
+            h = M.trig[j]
+            E(f"mjh::axisAngle2QuatSC(qloc, jaxis, qpos[{qa}] - {lit(m.qpos0[qa])}, "
+              f"trig[{2 * h}*64 + lane], trig[{2 * h + 1}*64 + lane]);")
+          else:
+            E(f"mjh::axisAngle2Quat(qloc, jaxis, qpos[{qa}] - {lit(m.qpos0[qa])});")
         E(f"mjh::mulQuat(xquat_{i}, xquat_{i}, qloc);")
         E("double vec[3];")
         E(f"mjh::rotVecQuat(vec, jpos, xquat_{i});")
@@ -440,6 +450,18 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
     geoms.setdefault(int(m.geom_bodyid[g]), []).append(g)
   for s in range(m.nsite):
     sites.setdefault(int(m.site_bodyid[s]), []).append(s)
+  if M.trig:
+    # every hinge's sin/cos once, into LDS: both tree passes read them, so neither carries
+    # the branches of the trig functions' argument reduction
+    E("// ---- hinge half-angle sin/cos (mju_axisAngle2Quat, engine_util_spatial.c:78-90)")
+    for j, h in M.trig.items():
+      qa = int(m.jnt_qposadr[j])
+      E.open()
+      E(f"double s, c, a = (qpos[{qa}] - {lit(m.qpos0[qa])})*0.5;")
+      E("MJH_SINCOS(a, s, c);")
+      E(f"trig[{2 * h}*64 + lane] = s; trig[{2 * h + 1}*64 + lane] = c;")
+      E.close()
+    E("MJH_MEM_BARRIER();")
   # ---- pass 1: kinematics -> subtree centers of mass (mj_comPos :183-208)
   E("// ---- tree pass 1: mj_kinematics -> mj_comPos subtree_com (post-order = descending)")
   need_stc, need_xpos = _camlight_needs(m)
@@ -505,6 +527,8 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
   # (which would keep every frame live across the passes)
   E("// ---- tree pass 2: kinematics (stored), cinert, cdof, camlight, crb, qM")
   E(f"for (int k = 0; k < {nq}; k++) MJH_OPAQUE(qpos[k]);")
+  if M.trig:
+    E("MJH_MEM_BARRIER();")
 
 
   def pre2(i):
@@ -983,8 +1007,8 @@ _SIG = {
     "pos": ("const double* __restrict__ qpos_in, const double* __restrict__ qvel_in, "
             "const double* __restrict__ qacc_in, int* __restrict__ worklist, "
             "int* __restrict__ worklist_count, int* __restrict__ worklist_next, "
-            "int* __restrict__ efc_count",
-            "qpos_in, qvel_in, qacc_in, worklist, worklist_count, worklist_next, efc_count"),
+            "int* __restrict__ efc_count, double* __restrict__ trig",
+            "qpos_in, qvel_in, qacc_in, worklist, worklist_count, worklist_next, efc_count, trig"),
     "fac": ("int* __restrict__ efc_count", "efc_count"),
     "va": ("double* __restrict__ qfrc_out, int* __restrict__ status, "
            "int* __restrict__ efc_count", "qfrc_out, status, efc_count"),
@@ -1018,18 +1042,25 @@ def generate(m, name: str, store_fields=None) -> str:
     double* __restrict__ qfrc_out, int* __restrict__ status, int* __restrict__ worklist,
     int* __restrict__ worklist_count, int* __restrict__ worklist_next,
     int* __restrict__ efc_count) {{
+  double trig[{max(1, 2 * len(M.trig) * 64)}];   // LDS on the device (k_pos)
 """ + "".join(f"  fast_{st}_{name}(mr, blk, lane, B, {_SIG[st][1]});\n" for st in STAGES)
              + "}\n")
   out.append("#if defined(__HIPCC__)")
   for st in STAGES:
     params, args = _SIG[st]
+    if st == "pos":
+      params = params.replace(", double* __restrict__ trig", "")
+      decl = f"  __shared__ double trig[{max(1, 2 * len(M.trig) * 64)}];\n"
+    else:
+      decl = ""
     out.append(f"__global__ __launch_bounds__(64, 1) void k_{st}_{name}(Mirror mr, int B, "
-               f"{params}) {{\n  fast_{st}_{name}(mr, blockIdx.x, threadIdx.x, B, {args});\n}}")
+               f"{params}) {{\n{decl}  fast_{st}_{name}(mr, blockIdx.x, threadIdx.x, B, {args});\n}}")
   out.append(f"""static void launch_fast_{name}(dim3 g, dim3 b, hipStream_t s, const Mirror& mr,
     int B, const double* qpos_in, const double* qvel_in, const double* qacc_in, double* qfrc_out,
     int* status, int* worklist, int* worklist_count, int* worklist_next, int* efc_count) {{""")
   for st in STAGES:
-    out.append(f"  hipLaunchKernelGGL(k_{st}_{name}, g, b, 0, s, mr, B, {_SIG[st][1]});")
+    args = _SIG[st][1].replace(", trig", "")
+    out.append(f"  hipLaunchKernelGGL(k_{st}_{name}, g, b, 0, s, mr, B, {args});")
   out.append("}")
   out.append("#endif")
   return "\n".join(out) + "\n"

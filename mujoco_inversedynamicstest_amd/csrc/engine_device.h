@@ -290,6 +290,16 @@ template <class R, class A> MJH_HD void axisAngle2Quat(R res, A axis, double ang
   }
 }
 
+// axisAngle2Quat with s = sin(angle/2), c = cos(angle/2) computed elsewhere, as selects
+template <class R, class A> MJH_HD void axisAngle2QuatSC(R res, A axis, double angle, double s,
+                                                         double c) {
+  const bool z = angle == 0;
+  res[0] = z ? 1.0 : c;
+  res[1] = z ? 0.0 : axis[0]*s;
+  res[2] = z ? 0.0 : axis[1]*s;
+  res[3] = z ? 0.0 : axis[2]*s;
+}
+
 // :119-133
 template <class R, class Q> MJH_HD void quat2Vel(R res, Q quat, double dt) {
   double axis[3] = {quat[1], quat[2], quat[3]};
@@ -1303,6 +1313,17 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
   #define MJH_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 #else
   #define MJH_SCHED_FENCE() ((void)0)
+#endif
+
+// Compiler memory barrier (no instruction): values written to LDS before it are re-read from
+// LDS after it instead of being forwarded in registers.
+#define MJH_MEM_BARRIER() asm volatile("" ::: "memory")
+
+// sin and cos of one argument (device: one shared argument reduction)
+#if defined(__HIP_DEVICE_COMPILE__)
+  #define MJH_SINCOS(x, s, c) sincos((x), &(s), &(c))
+#else
+  #define MJH_SINCOS(x, s, c) ((s) = sin(x), (c) = cos(x))
 #endif
 
 #endif  // MJHIP_ENGINE_DEVICE_H_
