@@ -27,6 +27,23 @@ METRIC = "mj_inverse evals/sec, humanoid 27-DoF, batch=65536 @ 1/2/4/8 MI355X vs
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
 
 
+def pmc_traffic(eng, model, count):
+  """HBM bytes per launch from the newest committed PMC summary (tools/pmc.sh +
+  tools/pmc_summary.py) if it was measured on the kernels this run used, else None."""
+  import glob
+  from mujoco_inversedynamicstest_amd import codegen
+  if not eng.fast_kernel:
+    return None, None
+  want = {f"k_{st}_{eng.fast_kernel}" for st in codegen.STAGES}
+  for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")),
+                     reverse=True):
+    rec = json.load(open(path))
+    if rec.get("model") == model and want <= set(rec["kernels"]):
+      per_eval = rec["traffic_bytes_per_eval"]
+      return per_eval * count, os.path.relpath(path, ROOT)
+  return None, None
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("--gpus", type=int, default=1)
@@ -94,6 +111,7 @@ def main():
   generic_ms = eng.time_kernel(count, reps=5, generic=True)
   bytes_per_eval = engine.output_bytes_per_eval(m)
   achieved = bytes_per_eval * count / (kernel_ms * 1e-3) / 1e9
+  traffic, traffic_src = pmc_traffic(eng, args.model, count)
 
   # after timing: rank 0 gathers every rank's qfrc_inverse checksum over RCCL
   chk = out.sum(dim=0)
@@ -132,7 +150,9 @@ def main():
                    "per_gpu_batch": count, "global_batch": world * count,
                    "parallelism": f"dp{world}"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
-                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                     "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                     "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
+                     "algorithmic_bytes_per_launch": bytes_per_eval * count,
                      "kernel": ("+".join(f"k_{st}_{eng.fast_kernel}" for st in codegen.STAGES)
                                 + "+k_inverse_list" if eng.fast_kernel else "k_inverse<0>"),
                      "kernel_ms": kernel_ms, "generic_kernel_ms": generic_ms,

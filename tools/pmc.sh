@@ -16,4 +16,5 @@ for group in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY" "F
   echo "pmc pass $n ($group) rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done
-exit 0
+python tools/pmc_summary.py gpurun_out gpurun_out/pmc_traffic.json > gpurun_out/pmc_summary.log 2>&1
+exit $?
