@@ -166,6 +166,7 @@ typedef struct mjhipOption_ {
   mjtNum o_margin;
   mjtNum o_solref[mjhipNREF];
   mjtNum o_solimp[mjhipNIMP];
+  mjtNum o_friction[5];
   int integrator;
   int cone;
   int jacobian;
@@ -287,6 +288,16 @@ MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B,
  * memory in the reference's per-instance row-major layout (count x fieldSize) */
 MJHIP_API int mjhip_mirrorDownload(mjhipContext* c, const char* field, int first, int count,
                                    mjtNum* dst);
+
+/* Int per-instance arrays of the device path: the reference's mjData int arrays on this path
+ * (efc_type, efc_id, efc_state; contact dim/geom/exclude/efc_address as con_*) and the counts
+ * efc_count = {nefc, ne, nf, nl}, con_count = {ncon}. Rows of mjhip_fieldSizeInt() ints. */
+MJHIP_API int mjhip_mirrorDownloadInt(mjhipContext* c, const char* field, int first, int count,
+                                      int* dst);
+MJHIP_API int mjhip_fieldSizeInt(const mjhipContext* c, const char* field);
+/* doubles per instance of any fp64 mirror field of this context: the mjData fields and the
+ * device path's per-instance arrays (efc_* rows, con_* contacts); -1 if unknown */
+MJHIP_API int mjhip_mirrorFieldSize(const mjhipContext* c, const char* field);
 MJHIP_API int mjhip_mirrorUpload(mjhipContext* c, const char* field, int first, int count,
                                  const mjtNum* src);
 /* device pointer of a mirror field (block layout above) */

@@ -1,0 +1,161 @@
+/* mjhip_contact.h — static contact rules and per-instance capacities.
+ *
+ * Shared by the HIP engine, its host harnesses and the CPU oracle, so all three size their
+ * contact and constraint arrays identically.
+ *
+ * Reference (MuJoCo 3.3.1 fork, src/engine/engine_collision_driver.c):
+ *   canCollide / canCollide2 / filterBitmask / filterBodyPair  :105-200
+ *   mj_broadphase: always-colliding world pairs + weld-filtered SAP pairs  :1148-1286
+ *   mj_collision: body bitmask, exclude signatures, geom pairs  :265-497
+ *   mj_collideGeoms: type order, collision table, geom bitmask  :1440-1620
+ *   mj_contactParam (condim)  :1289-1384
+ *
+ * The broadphase's bounding boxes are inflated by each geom's rbound + margin, so they never
+ * reject a pair the narrowphase would report. A body pair is therefore a candidate exactly
+ * when it passes the static rules below. mj_collision processes candidates in signature
+ * order ((b1 << 16) + b2, b1 < b2), and each primitive pair yields at most 2 contacts.
+ */
+#ifndef MJHIP_CONTACT_H_
+#define MJHIP_CONTACT_H_
+
+#include "mjhip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__HIPCC__)
+  #define MJHIP_CONTACT_HD __host__ __device__ static inline
+#else
+  #define MJHIP_CONTACT_HD static inline
+#endif
+
+/* geom-level bitmask filter (filterBitmask): 1 = cannot collide */
+MJHIP_CONTACT_HD int mjhip_filterBitmask(int contype1, int conaffinity1, int contype2,
+                                         int conaffinity2) {
+  return !(contype1 & conaffinity2) && !(contype2 & conaffinity1);
+}
+
+/* weld filter (filterBodyPair): 1 = skip */
+MJHIP_CONTACT_HD int mjhip_filterBodyPair(int weld1, int pweld1, int weld2, int pweld2,
+                                          int dsbl_filterparent) {
+  if (weld1 == weld2) return 1;
+  if (!dsbl_filterparent && weld1 != 0 && weld2 != 0 && (weld1 == pweld2 || weld2 == pweld1)) {
+    return 1;
+  }
+  return 0;
+}
+
+/* body pair b1 < b2 that mj_broadphase can return and mj_collision does not filter
+ * (body bitmask, exclude list); the geom-level tests come after */
+MJHIP_CONTACT_HD int mjhip_bodyPairCandidate(const mjhipModel* m, int b1, int b2) {
+  const int can1 = m->body_contype[b1] || m->body_conaffinity[b1];
+  const int can2 = m->body_contype[b2] || m->body_conaffinity[b2];
+  if (!can1 || !can2) return 0;
+  const int weld2 = m->body_weldid[b2];
+  const int pweld2 = m->body_weldid[m->body_parentid[weld2]];
+  if (b1 == 0) {
+    /* always-colliding pairs of a world body with geoms (mj_broadphase :1154-1186) */
+    if (m->body_geomnum[0] <= 0) return 0;
+    if (mjhip_filterBodyPair(0, 0, weld2, pweld2, 0)) return 0;
+  } else {
+    const int weld1 = m->body_weldid[b1];
+    const int pweld1 = m->body_weldid[m->body_parentid[weld1]];
+    if (mjhip_filterBodyPair(weld1, pweld1, weld2, pweld2,
+                             m->opt.disableflags & mjhipDSBL_FILTERPARENT)) {
+      return 0;
+    }
+  }
+  if (mjhip_filterBitmask(m->body_contype[b1], m->body_conaffinity[b1], m->body_contype[b2],
+                          m->body_conaffinity[b2])) {
+    return 0;
+  }
+  const int sig = (b1 << 16) + b2;
+  for (int i = 0; i < m->nexclude; i++) {
+    if (m->exclude_signature[i] == sig) return 0;
+  }
+  return 1;
+}
+
+/* contacts a (type-ordered t1 <= t2) geom pair can produce with the primitives implemented
+ * here: 0 = no collision function in the reference table, -1 = a reference collision
+ * function that this engine does not implement */
+MJHIP_CONTACT_HD int mjhip_pairMaxContacts(int t1, int t2) {
+  if (t1 == mjhipGEOM_PLANE && t2 <= mjhipGEOM_HFIELD) return 0;
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) return 1;
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CAPSULE) return 2;
+  if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_SPHERE) return 1;
+  if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CAPSULE) return 1;
+  if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) return 2;
+  if (t1 == mjhipGEOM_HFIELD && t2 <= mjhipGEOM_HFIELD) return 0;
+  return -1;
+}
+
+/* condim of a geom pair (mj_contactParam: higher priority wins, else the max) */
+MJHIP_CONTACT_HD int mjhip_pairCondim(const mjhipModel* m, int g1, int g2) {
+  const int p1 = m->geom_priority[g1], p2 = m->geom_priority[g2];
+  if (p1 > p2) return m->geom_condim[g1];
+  if (p1 < p2) return m->geom_condim[g2];
+  return m->geom_condim[g1] > m->geom_condim[g2] ? m->geom_condim[g1] : m->geom_condim[g2];
+}
+
+/* constraint rows of one contact (mj_instantiateContact; pyramidal cone) */
+MJHIP_CONTACT_HD int mjhip_contactRows(int condim) { return condim == 1 ? 1 : 2*(condim - 1); }
+
+/* 1 if contacts are generated at all (mj_collision :284-287) */
+MJHIP_CONTACT_HD int mjhip_contactsEnabled(const mjhipModel* m) {
+  return !(m->opt.disableflags & (mjhipDSBL_CONSTRAINT | mjhipDSBL_CONTACT)) && m->nbody >= 2;
+}
+
+/* Maximum contacts per instance (exact for the implemented primitives), or -1 if a
+ * candidate geom pair needs a collision function this engine does not implement.
+ * *rows receives the maximum number of contact constraint rows. */
+MJHIP_CONTACT_HD int mjhip_contactCapacity(const mjhipModel* m, int* rows) {
+  int ncon = 0, nrow = 0;
+  if (rows) *rows = 0;
+  if (!mjhip_contactsEnabled(m)) return 0;
+  for (int b1 = 0; b1 < m->nbody; b1++) {
+    for (int b2 = b1 + 1; b2 < m->nbody; b2++) {
+      if (!mjhip_bodyPairCandidate(m, b1, b2)) continue;
+      for (int i = 0; i < m->body_geomnum[b1]; i++) {
+        for (int j = 0; j < m->body_geomnum[b2]; j++) {
+          int g1 = m->body_geomadr[b1] + i, g2 = m->body_geomadr[b2] + j;
+          if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
+          int k = mjhip_pairMaxContacts(m->geom_type[g1], m->geom_type[g2]);
+          if (k == 0) continue;
+          if (mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
+                                  m->geom_contype[g2], m->geom_conaffinity[g2])) {
+            continue;
+          }
+          if (k < 0) return -1;
+          ncon += k;
+          nrow += k * mjhip_contactRows(mjhip_pairCondim(m, g1, g2));
+        }
+      }
+    }
+  }
+  if (rows) *rows = nrow;
+  return ncon;
+}
+
+/* constraint rows per instance: dof friction, joint/tendon limits, contacts */
+MJHIP_CONTACT_HD int mjhip_efcCapacity(const mjhipModel* m) {
+  int n = 0, crow = 0;
+  for (int i = 0; i < m->njnt; i++) {
+    if (m->jnt_limited[i]) n += (m->jnt_type[i] == mjhipJNT_BALL) ? 1 : 2;
+  }
+  for (int i = 0; i < m->ntendon; i++) {
+    if (m->tendon_limited[i]) n += 2;
+  }
+  for (int i = 0; i < m->nv; i++) {
+    if (m->dof_frictionloss[i] > 0) n += 1;
+  }
+  if (mjhip_contactCapacity(m, &crow) > 0) n += crow;
+  return n;
+}
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif  /* MJHIP_CONTACT_H_ */

@@ -48,6 +48,7 @@ static const mjhipModel* model_view(const mjModel* m, const mjData* d) {
   hm->opt.o_margin = m->opt.o_margin;
   memcpy(hm->opt.o_solref, m->opt.o_solref, sizeof(hm->opt.o_solref));
   memcpy(hm->opt.o_solimp, m->opt.o_solimp, sizeof(hm->opt.o_solimp));
+  memcpy(hm->opt.o_friction, m->opt.o_friction, sizeof(hm->opt.o_friction));
   hm->opt.integrator = m->opt.integrator;
   hm->opt.cone = m->opt.cone;
   hm->opt.jacobian = m->opt.jacobian;

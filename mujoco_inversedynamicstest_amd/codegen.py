@@ -99,6 +99,10 @@ def fast_path_supported(m) -> str | None:
     return "mocap/activations"
   if m.opt["density"] > 0 or m.opt["viscosity"] > 0:
     return "fluid"
+  dsbl = int(m.opt["disableflags"])
+  if not (dsbl & 1) and not (dsbl & (1 << 4)) and m.nbody >= 2 and \
+     np.any((m.geom_contype != 0) | (m.geom_conaffinity != 0)):
+    return "contacts (collision runs on the generic kernel)"
   return None
 
 

@@ -15,6 +15,7 @@
 #include <math.h>
 
 #include "../../include/mjhip.h"
+#include "../../include/mjhip_contact.h"
 
 #if defined(__HIPCC__)
   #define MJH_HD __host__ __device__ inline
@@ -62,13 +63,31 @@ struct SP {
   XSC(efc_vel, efc_cap)               \
   XSC(efc_aref, efc_cap)              \
   XSC(efc_force, efc_cap)             \
-  XSC(jar, efc_cap)
+  XSC(jar, efc_cap)                   \
+  XSC(con_dist, con_cap)              \
+  XSC(con_pos, 3*con_cap)             \
+  XSC(con_frame, 9*con_cap)           \
+  XSC(con_includemargin, con_cap)     \
+  XSC(con_friction, 5*con_cap)        \
+  XSC(con_solref, 2*con_cap)          \
+  XSC(con_solreffriction, 2*con_cap)  \
+  XSC(con_solimp, 5*con_cap)          \
+  XSC(con_mu, con_cap)                \
+  XSC(jac2p, 3*nv*(con_cap > 0))      \
+  XSC(jac2r, 3*nv*(con_cap > 0))      \
+  XSC(cjac, 6*nv*(con_cap > 0))       \
+  XSC(cjacdif, 6*nv*(con_cap > 0))
 
 #define MJHIP_SCRATCH_INT_FIELDS      \
   XSI(efc_type, efc_cap)              \
   XSI(efc_id, efc_cap)                \
   XSI(efc_state, efc_cap)             \
-  XSI(efc_count, 4)                   /* nefc, ne, nf, nl */
+  XSI(efc_count, 4)                   /* nefc, ne, nf, nl */ \
+  XSI(con_count, 1)                   /* ncon */ \
+  XSI(con_dim, con_cap)               \
+  XSI(con_geom, 2*con_cap)            \
+  XSI(con_exclude, con_cap)           \
+  XSI(con_efc_address, con_cap)
 
 template <int S>
 struct Lane {
@@ -82,6 +101,7 @@ struct Lane {
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
   int efc_cap;
+  int con_cap;
 };
 
 //---------------------------------- engine_util_blas.c ---------------------------------------
@@ -483,28 +503,363 @@ MJH_HD void local2Global(const Lane<S>& d, SP<S> xpos, SP<S> xmat, P pos, Q quat
   }
 }
 
-// mj_jac :389-441 (dense), into d.jacp / d.jacr
+// mj_jac :389-441 (dense), into jacp / jacr
 template <int S, class P>
-MJH_HD void jac(const mjhipModel& m, const Lane<S>& d, P point, int body) {
+MJH_HD void jacInto(const mjhipModel& m, const Lane<S>& d, SP<S> jacp, SP<S> jacr, P point,
+                    int body) {
   int nv = m.nv;
   double offset[3];
-  zero(d.jacp, 3*nv);
-  zero(d.jacr, 3*nv);
+  zero(jacp, 3*nv);
+  zero(jacr, 3*nv);
   sub3(offset, point, d.subtree_com + 3*m.body_rootid[body]);
   while (body && !m.body_dofnum[body]) body = m.body_parentid[body];
   if (!body) return;
   int i = m.body_dofadr[body] + m.body_dofnum[body] - 1;
   while (i >= 0) {
     SP<S> cdof = d.cdof + 6*i;
-    d.jacr[i+0*nv] = cdof[0];
-    d.jacr[i+1*nv] = cdof[1];
-    d.jacr[i+2*nv] = cdof[2];
+    jacr[i+0*nv] = cdof[0];
+    jacr[i+1*nv] = cdof[1];
+    jacr[i+2*nv] = cdof[2];
     double tmp[3];
     cross(tmp, cdof, offset);
-    d.jacp[i+0*nv] = cdof[3] + tmp[0];
-    d.jacp[i+1*nv] = cdof[4] + tmp[1];
-    d.jacp[i+2*nv] = cdof[5] + tmp[2];
+    jacp[i+0*nv] = cdof[3] + tmp[0];
+    jacp[i+1*nv] = cdof[4] + tmp[1];
+    jacp[i+2*nv] = cdof[5] + tmp[2];
     i = m.dof_parentid[i];
+  }
+}
+
+template <int S, class P>
+MJH_HD void jac(const mjhipModel& m, const Lane<S>& d, P point, int body) {
+  jacInto(m, d, d.jacp, d.jacr, point, body);
+}
+
+
+//---------------------------------- engine_collision_*.c -------------------------------------
+// mj_collision for the primitive pairs plane/sphere/capsule (the candidate rules are shared
+// with the oracle in include/mjhip_contact.h); contacts go to the con_* scratch fields.
+
+struct RawContact { double dist, pos[3], frame[9]; };
+
+template <class A, class B> MJH_HD double dot3(A a, B b) { return a[0]*b[0] + a[1]*b[1] + a[2]*b[2]; }
+MJH_HD double clip(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+// engine_collision_primitive.c mjraw_PlaneSphere
+template <class P1, class M1, class P2>
+MJH_HD int rawPlaneSphere(RawContact* c, double margin, P1 pos1, M1 mat1, P2 pos2, double r2) {
+  c->frame[0] = mat1[2];
+  c->frame[1] = mat1[5];
+  c->frame[2] = mat1[8];
+  double tmp[3] = {pos2[0] - pos1[0], pos2[1] - pos1[1], pos2[2] - pos1[2]};
+  double cdist = dot3(tmp, c->frame);
+  if (cdist > margin + r2) return 0;
+  c->dist = cdist - r2;
+  scl3(tmp, c->frame, -c->dist/2 - r2);
+  add3(c->pos, pos2, tmp);
+  zero3(c->frame + 3);
+  return 1;
+}
+
+// mjc_PlaneCapsule
+template <class P1, class M1, class P2, class M2>
+MJH_HD int colPlaneCapsule(RawContact* c, double margin, P1 pos1, M1 mat1, P2 pos2, M2 mat2,
+                           const double* size2) {
+  double axis[3] = {mat2[2], mat2[5], mat2[8]};
+  double seg[3] = {size2[1]*axis[0], size2[1]*axis[1], size2[1]*axis[2]};
+  double p[3];
+  add3(p, pos2, seg);
+  int n1 = rawPlaneSphere(c, margin, pos1, mat1, p, size2[0]);
+  sub3(p, pos2, seg);
+  int n2 = rawPlaneSphere(c + n1, margin, pos1, mat1, p, size2[0]);
+  if (n1) copy3(c->frame + 3, axis);
+  if (n2) copy3((c + n1)->frame + 3, axis);
+  return n1 + n2;
+}
+
+// mjraw_SphereSphere
+template <class P1, class M1, class P2, class M2>
+MJH_HD int rawSphereSphere(RawContact* c, double margin, P1 pos1, M1 mat1, double r1, P2 pos2,
+                           M2 mat2, double r2) {
+  double dif[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
+  double cdist_sqr = dot3(dif, dif);
+  double min_dist = margin + r1 + r2;
+  if (cdist_sqr > min_dist*min_dist) return 0;
+  c->dist = sqrt(cdist_sqr) - r1 - r2;
+  sub3(c->frame, pos2, pos1);
+  double len = normalize3(c->frame);
+  if (len < MINVAL) {
+    double a1[3] = {mat1[2], mat1[5], mat1[8]}, a2[3] = {mat2[2], mat2[5], mat2[8]};
+    cross(c->frame, a1, a2);
+    normalize3(c->frame);
+  }
+  scl3(c->pos, c->frame, r1 + c->dist/2);
+  addTo3(c->pos, pos1);
+  zero3(c->frame + 3);
+  return 1;
+}
+
+// mjraw_SphereCapsule
+template <class P1, class M1, class P2, class M2>
+MJH_HD int colSphereCapsule(RawContact* c, double margin, P1 pos1, M1 mat1, double r1, P2 pos2,
+                            M2 mat2, const double* size2) {
+  double len = size2[1];
+  double axis[3] = {mat2[2], mat2[5], mat2[8]};
+  double vec[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
+  double x = clip(dot3(axis, vec), -len, len);
+  scl3(vec, axis, x);
+  addTo3(vec, pos2);
+  return rawSphereSphere(c, margin, pos1, mat1, r1, vec, mat2, size2[0]);
+}
+
+// mjraw_CapsuleCapsule
+template <class P1, class M1, class P2, class M2>
+MJH_HD int colCapsuleCapsule(RawContact* c, double margin, P1 pos1, M1 mat1,
+                             const double* size1, P2 pos2, M2 mat2, const double* size2) {
+  double axis1[3] = {mat1[2]*size1[1], mat1[5]*size1[1], mat1[8]*size1[1]};
+  double axis2[3] = {mat2[2]*size2[1], mat2[5]*size2[1], mat2[8]*size2[1]};
+  double dif[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
+  double ma = dot3(axis1, axis1);
+  double mb = -dot3(axis1, axis2);
+  double mc = dot3(axis2, axis2);
+  double u = -dot3(axis1, dif);
+  double v = dot3(axis2, dif);
+  double det = ma*mc - mb*mb;
+  double vec1[3], vec2[3];
+  if (fabs(det) >= MINVAL) {
+    double x1 = (mc*u - mb*v) / det;
+    double x2 = (ma*v - mb*u) / det;
+    if (x1 > 1) {
+      x1 = 1;
+      x2 = (v - mb) / mc;
+    } else if (x1 < -1) {
+      x1 = -1;
+      x2 = (v + mb) / mc;
+    }
+    if (x2 > 1) {
+      x2 = 1;
+      x1 = clip((u - mb) / ma, -1, 1);
+    } else if (x2 < -1) {
+      x2 = -1;
+      x1 = clip((u + mb) / ma, -1, 1);
+    }
+    scl3(vec1, axis1, x1);
+    addTo3(vec1, pos1);
+    scl3(vec2, axis2, x2);
+    addTo3(vec2, pos2);
+    return rawSphereSphere(c, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
+  }
+  add3(vec1, pos1, axis1);
+  double x2 = clip((v - mb) / mc, -1, 1);
+  scl3(vec2, axis2, x2);
+  addTo3(vec2, pos2);
+  int n1 = rawSphereSphere(c, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
+  sub3(vec1, pos1, axis1);
+  x2 = clip((v + mb) / mc, -1, 1);
+  scl3(vec2, axis2, x2);
+  addTo3(vec2, pos2);
+  int n2 = rawSphereSphere(c + n1, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
+  if (n1 + n2 >= 2) return n1 + n2;
+  add3(vec2, pos2, axis2);
+  double x1 = clip((u - mb) / ma, -1, 1);
+  scl3(vec1, axis1, x1);
+  addTo3(vec1, pos1);
+  int n3 = rawSphereSphere(c + n1 + n2, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
+  if (n1 + n2 + n3 >= 2) return n1 + n2 + n3;
+  sub3(vec2, pos2, axis2);
+  x1 = clip((u + mb) / ma, -1, 1);
+  scl3(vec1, axis1, x1);
+  addTo3(vec1, pos1);
+  int n4 = rawSphereSphere(c + n1 + n2 + n3, margin, vec1, mat1, size1[0], vec2, mat2,
+                           size2[0]);
+  return n1 + n2 + n3 + n4;
+}
+
+// engine_util_spatial.c mju_makeFrame
+MJH_HD void makeFrame(double* frame) {
+  double tmp[3];
+  normalize3(frame);
+  if (sqrt(frame[3]*frame[3] + frame[4]*frame[4] + frame[5]*frame[5]) < 0.5) {
+    zero3(frame + 3);
+    if (frame[1] < 0.5 && frame[1] > -0.5) frame[4] = 1;
+    else frame[5] = 1;
+  }
+  scl3(tmp, frame, dot3(frame, frame + 3));
+  sub3(frame + 3, frame + 3, tmp);
+  normalize3(frame + 3);
+  cross(frame + 6, frame, frame + 3);
+}
+
+// mj_contactParam (engine_collision_driver.c:1289-1384), geom : geom
+MJH_HD void contactParam(const mjhipModel& m, int g1, int g2, int* condim, double* gap,
+                         double* solref, double* solimp, double* friction) {
+  double fri[3];
+  int p1 = m.geom_priority[g1], p2 = m.geom_priority[g2];
+  *gap = m.geom_gap[g1] > m.geom_gap[g2] ? m.geom_gap[g1] : m.geom_gap[g2];
+  if (p1 != p2) {
+    int g = p1 > p2 ? g1 : g2;
+    *condim = m.geom_condim[g];
+    for (int i = 0; i < 2; i++) solref[i] = m.geom_solref[2*g+i];
+    for (int i = 0; i < 5; i++) solimp[i] = m.geom_solimp[5*g+i];
+    for (int i = 0; i < 3; i++) fri[i] = m.geom_friction[3*g+i];
+  } else {
+    *condim = m.geom_condim[g1] > m.geom_condim[g2] ? m.geom_condim[g1] : m.geom_condim[g2];
+    double s1 = m.geom_solmix[g1], s2 = m.geom_solmix[g2], mix;
+    if (s1 >= MINVAL && s2 >= MINVAL) mix = s1 / (s1 + s2);
+    else if (s1 < MINVAL && s2 < MINVAL) mix = 0.5;
+    else if (s1 < MINVAL) mix = 0.0;
+    else mix = 1.0;
+    const double *r1 = m.geom_solref + 2*g1, *r2 = m.geom_solref + 2*g2;
+    if (r1[0] > 0 && r2[0] > 0) {
+      for (int i = 0; i < 2; i++) solref[i] = mix*r1[i] + (1-mix)*r2[i];
+    } else {
+      for (int i = 0; i < 2; i++) solref[i] = r1[i] < r2[i] ? r1[i] : r2[i];
+    }
+    for (int i = 0; i < 5; i++) solimp[i] = mix*m.geom_solimp[5*g1+i] + (1-mix)*m.geom_solimp[5*g2+i];
+    for (int i = 0; i < 3; i++) {
+      double a = m.geom_friction[3*g1+i], b = m.geom_friction[3*g2+i];
+      fri[i] = a > b ? a : b;
+    }
+  }
+  friction[0] = fri[0];
+  friction[1] = fri[0];
+  friction[2] = fri[1];
+  friction[3] = fri[2];
+  friction[4] = fri[2];
+}
+
+// mj_filterSphere: 1 = the bounding spheres (or the plane distance) rule the pair out
+template <int S>
+MJH_HD int filterSphere(const mjhipModel& m, const Lane<S>& d, int g1, int g2, double margin) {
+  SP<S> p1 = d.geom_xpos + 3*g1, p2 = d.geom_xpos + 3*g2;
+  double rb1 = m.geom_rbound[g1], rb2 = m.geom_rbound[g2];
+  if (rb1 > 0 && rb2 > 0) {
+    double dif[3] = {p1[0]-p2[0], p1[1]-p2[1], p1[2]-p2[2]};
+    double bound = rb1 + rb2 + margin;
+    return dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2] > bound*bound;
+  }
+  for (int side = 0; side < 2; side++) {
+    int gp = side ? g2 : g1, go = side ? g1 : g2;
+    if (m.geom_type[gp] == mjhipGEOM_PLANE && m.geom_rbound[go] > 0) {
+      SP<S> mat = d.geom_xmat + 9*gp;
+      double norm[3] = {mat[2], mat[5], mat[8]}, dif[3];
+      sub3(dif, d.geom_xpos + 3*go, d.geom_xpos + 3*gp);
+      if (dot3(dif, norm) > margin + m.geom_rbound[go]) return 1;
+    }
+  }
+  return 0;
+}
+
+// mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
+template <int S>
+MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, int* status) {
+  if (m.geom_type[g1] > m.geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
+  int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+  if (mjhip_pairMaxContacts(t1, t2) <= 0) return;
+  if (mjhip_filterBitmask(m.geom_contype[g1], m.geom_conaffinity[g1], m.geom_contype[g2],
+                          m.geom_conaffinity[g2])) {
+    return;
+  }
+  const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
+  double margin = ovr ? m.opt.o_margin : (m.geom_margin[g1] > m.geom_margin[g2] ?
+                                          m.geom_margin[g1] : m.geom_margin[g2]);
+  if (filterSphere(m, d, g1, g2, margin)) return;
+  SP<S> pos1 = d.geom_xpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
+  SP<S> pos2 = d.geom_xpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
+  const double *size1 = m.geom_size + 3*g1, *size2 = m.geom_size + 3*g2;
+  RawContact raw[2];
+  int num = 0;
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) {
+    num = rawPlaneSphere(raw, margin, pos1, mat1, pos2, size2[0]);
+  } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CAPSULE) {
+    num = colPlaneCapsule(raw, margin, pos1, mat1, pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_SPHERE) {
+    num = rawSphereSphere(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2[0]);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CAPSULE) {
+    num = colSphereCapsule(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {
+    num = colCapsuleCapsule(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
+  }
+  if (!num) return;
+  int condim;
+  double gap, solref[2], solimp[5], friction[5];
+  contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
+  for (int k = 0; k < num; k++) {
+    int i = d.con_count[0];
+    if (i >= d.con_cap) {              // mjWARN_CONTACTFULL analogue (capacity is exact)
+      *status |= MJHIP_INST_CNSTRFULL;
+      return;
+    }
+    double frame[9];
+    for (int j = 0; j < 9; j++) frame[j] = raw[k].frame[j];
+    d.con_dist[i] = raw[k].dist;
+    copy3(d.con_pos + 3*i, raw[k].pos);
+    d.con_geom[2*i] = g1;
+    d.con_geom[2*i+1] = g2;
+    d.con_dim[i] = condim;
+    double includemargin = margin - gap;
+    d.con_includemargin[i] = includemargin;
+    for (int j = 0; j < 2; j++) d.con_solref[2*i+j] = ovr ? m.opt.o_solref[j] : solref[j];
+    for (int j = 0; j < 2; j++) d.con_solreffriction[2*i+j] = ovr ? m.opt.o_solref[j] : 0.0;
+    for (int j = 0; j < 5; j++) d.con_solimp[5*i+j] = ovr ? m.opt.o_solimp[j] : solimp[j];
+    for (int j = 0; j < 5; j++) {
+      double f = ovr ? m.opt.o_friction[j] : friction[j];
+      d.con_friction[5*i+j] = f > 1e-5 ? f : 1e-5;      // mjMINMU
+    }
+    d.con_exclude[i] = raw[k].dist >= includemargin;
+    makeFrame(frame);
+    for (int j = 0; j < 9; j++) d.con_frame[9*i+j] = frame[j];
+    d.con_efc_address[i] = -1;
+    d.con_mu[i] = 0;
+    d.con_count[0] = i + 1;
+  }
+}
+
+// contactcompare (engine_collision_driver.c:223-257) on two contacts' geom ids
+template <int S>
+MJH_HD bool contactLess(const mjhipModel& m, const Lane<S>& d, int a, int b) {
+  int a1 = d.con_geom[2*a], a2 = d.con_geom[2*a+1];
+  int b1 = d.con_geom[2*b], b2 = d.con_geom[2*b+1];
+  if (m.geom_type[a1] > m.geom_type[a2]) { int t = a1; a1 = a2; a2 = t; }
+  if (m.geom_type[b1] > m.geom_type[b2]) { int t = b1; b1 = b2; b2 = t; }
+  return a1 < b1 || (a1 == b1 && a2 < b2);
+}
+
+template <int S>
+MJH_HD void swapContacts(const Lane<S>& d, int a, int b) {
+#define MJH_SWP(f, k, T) for (int j = 0; j < (k); j++) { T t = d.f[(k)*a+j]; \
+    d.f[(k)*a+j] = d.f[(k)*b+j]; d.f[(k)*b+j] = t; }
+  MJH_SWP(con_dist, 1, double) MJH_SWP(con_pos, 3, double) MJH_SWP(con_frame, 9, double)
+  MJH_SWP(con_includemargin, 1, double) MJH_SWP(con_friction, 5, double)
+  MJH_SWP(con_solref, 2, double) MJH_SWP(con_solreffriction, 2, double)
+  MJH_SWP(con_solimp, 5, double) MJH_SWP(con_mu, 1, double) MJH_SWP(con_dim, 1, int)
+  MJH_SWP(con_geom, 2, int) MJH_SWP(con_exclude, 1, int) MJH_SWP(con_efc_address, 1, int)
+#undef MJH_SWP
+}
+
+// mj_collision (engine_collision_driver.c:265-497): candidate body pairs in signature order,
+// geoms all-to-all; a midphase pair (a body with more than one geom) has its contacts stably
+// sorted by contactcompare, as mj_collideTree's callers do
+template <int S>
+MJH_HD void collision(const mjhipModel& m, const Lane<S>& d, int* status) {
+  d.con_count[0] = 0;
+  if (!mjhip_contactsEnabled(&m)) return;
+  for (int b1 = 0; b1 < m.nbody; b1++) {
+    for (int b2 = b1 + 1; b2 < m.nbody; b2++) {
+      if (!mjhip_bodyPairCandidate(&m, b1, b2)) continue;
+      int n1 = m.body_geomnum[b1], n2 = m.body_geomnum[b2];
+      int before = d.con_count[0];
+      for (int i = 0; i < n1; i++) {
+        for (int j = 0; j < n2; j++) {
+          collideGeoms(m, d, m.body_geomadr[b1] + i, m.body_geomadr[b2] + j, status);
+        }
+      }
+      if (!(m.opt.disableflags & mjhipDSBL_MIDPHASE) && !(n1 == 1 && n2 == 1)) {
+        int n = d.con_count[0];
+        for (int a = before + 1; a < n; a++) {
+          for (int b = a; b > before && contactLess(m, d, b, b - 1); b--) swapContacts(d, b, b - 1);
+        }
+      }
+    }
   }
 }
 
@@ -969,35 +1324,94 @@ MJH_HD void passive(const mjhipModel& m, const Lane<S>& d) {
 
 //---------------------------------- engine_core_constraint.c ---------------------------------
 
-// mj_addConstraint :265-356 (dense, size 1); jac is a strided row of d.jacp
+// mj_addConstraint :265-356 (dense): `size` rows of jac (strided scratch), contact rows are
+// never dropped as empty
 template <int S>
-MJH_HD void addConstraint(const mjhipModel& m, const Lane<S>& d, SP<S> jacrow, double pos,
-                          double margin, double frictionloss, int type, int id, int* status) {
+MJH_HD void addConstraint(const mjhipModel& m, const Lane<S>& d, SP<S> jac, const double* pos,
+                          const double* margin, double frictionloss, int size, int type, int id,
+                          int* status) {
   int nv = m.nv;
   int nefc = d.efc_count[0];
-  int empty = 1;
-  for (int i = 0; i < nv; i++) {
-    if (jacrow[i]) {
-      empty = 0;
-      break;
-    }
+  int empty = !(type == CNSTR_CONTACT_FRICTIONLESS || type == CNSTR_CONTACT_PYRAMIDAL ||
+                type == CNSTR_CONTACT_ELLIPTIC);
+  for (int i = 0; empty && i < size*nv; i++) {
+    if (jac[i]) empty = 0;
   }
   if (empty) return;
-  if (nefc >= d.efc_cap) {         // mjWARN_CNSTRFULL analogue: capacity exceeded
+  if (nefc + size > d.efc_cap) {   // mjWARN_CNSTRFULL analogue: capacity exceeded
     *status |= MJHIP_INST_CNSTRFULL;
     return;
   }
-  copy(d.efc_J + nefc*nv, jacrow, nv);
-  d.efc_pos[nefc] = pos;
-  d.efc_margin[nefc] = margin;
-  d.efc_frictionloss[nefc] = frictionloss;
-  d.efc_type[nefc] = type;
-  d.efc_id[nefc] = id;
-  d.efc_count[0] = nefc + 1;
+  copy(d.efc_J + nefc*nv, jac, size*nv);
+  for (int i = 0; i < size; i++) {
+    d.efc_pos[nefc+i] = pos ? pos[i] : 0;
+    d.efc_margin[nefc+i] = margin ? margin[i] : 0;
+    d.efc_frictionloss[nefc+i] = frictionloss;
+    d.efc_type[nefc+i] = type;
+    d.efc_id[nefc+i] = id;
+  }
+  d.efc_count[0] = nefc + size;
   if (type == CNSTR_FRICTION_DOF || type == CNSTR_FRICTION_TENDON) {
-    d.efc_count[2] = d.efc_count[2] + 1;
+    d.efc_count[2] = d.efc_count[2] + size;
   } else if (type == CNSTR_LIMIT_JOINT || type == CNSTR_LIMIT_TENDON) {
-    d.efc_count[3] = d.efc_count[3] + 1;
+    d.efc_count[3] = d.efc_count[3] + size;
+  }
+}
+
+template <int S>
+MJH_HD void addConstraint1(const mjhipModel& m, const Lane<S>& d, SP<S> jacrow, double pos,
+                           double margin, double frictionloss, int type, int id, int* status) {
+  addConstraint(m, d, jacrow, &pos, &margin, frictionloss, 1, type, id, status);
+}
+
+// mj_instantiateContact :964-1131 (dense; pyramidal or frictionless; elliptic cones are
+// rejected with contacts at context creation)
+template <int S>
+MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, int* status) {
+  int nv = m.nv, ncon = d.con_count[0];
+  if ((m.opt.disableflags & mjhipDSBL_CONTACT) || ncon == 0 || nv == 0) return;
+  SP<S> jacdifp = d.cjacdif, jacdifr = d.cjacdif + 3*nv, cj = d.cjac;
+  for (int i = 0; i < ncon; i++) {
+    if (d.con_exclude[i]) continue;
+    int dim = d.con_dim[i];
+    d.con_efc_address[i] = d.efc_count[0];
+    int b1 = m.geom_bodyid[d.con_geom[2*i]], b2 = m.geom_bodyid[d.con_geom[2*i+1]];
+    // mj_jacDifPair (engine_support.c:656-733), dense
+    jacInto(m, d, d.jacp, d.jacr, d.con_pos + 3*i, b1);
+    jacInto(m, d, d.jac2p, d.jac2r, d.con_pos + 3*i, b2);
+    for (int k = 0; k < 3*nv; k++) jacdifp[k] = d.jac2p[k] - d.jacp[k];
+    if (dim > 3) for (int k = 0; k < 3*nv; k++) jacdifr[k] = d.jac2r[k] - d.jacr[k];
+    // mju_mulMatMat(jac, frame, jacdif) (engine_util_blas.c:818-831)
+    SP<S> frame = d.con_frame + 9*i;
+    int rp = dim > 1 ? 3 : 1;
+    zero(cj, rp*nv);
+    for (int r = 0; r < rp; r++) {
+      for (int k = 0; k < 3; k++) {
+        double t = frame[3*r+k];
+        if (t) addToScl(cj + r*nv, jacdifp + k*nv, t, nv);
+      }
+    }
+    if (dim > 3) {
+      zero(cj + 3*nv, (dim-3)*nv);
+      for (int r = 0; r < dim-3; r++) {
+        for (int k = 0; k < 3; k++) {
+          double t = frame[3*r+k];
+          if (t) addToScl(cj + (3+r)*nv, jacdifr + k*nv, t, nv);
+        }
+      }
+    }
+    double dist = d.con_dist[i], imargin = d.con_includemargin[i];
+    if (dim == 1) {
+      addConstraint(m, d, cj, &dist, &imargin, 0, 1, CNSTR_CONTACT_FRICTIONLESS, i, status);
+    } else {
+      double cpos[2] = {dist, dist}, cmargin[2] = {imargin, imargin};
+      for (int k = 1; k < dim; k++) {
+        double f = d.con_friction[5*i + k-1];
+        for (int j = 0; j < nv; j++) jacdifp[j] = cj[j] + cj[k*nv+j]*f;
+        for (int j = 0; j < nv; j++) jacdifp[nv+j] = cj[j] + cj[k*nv+j]*(-f);
+        addConstraint(m, d, jacdifp, cpos, cmargin, 0, 2, CNSTR_CONTACT_PYRAMIDAL, i, status);
+      }
+    }
   }
 }
 
@@ -1056,7 +1470,7 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
       if (m.dof_frictionloss[i] > 0) {
         zero(jacrow, nv);
         jacrow[i] = 1;
-        addConstraint(m, d, jacrow, 0, 0, m.dof_frictionloss[i], CNSTR_FRICTION_DOF, i, status);
+        addConstraint1(m, d, jacrow, 0, 0, m.dof_frictionloss[i], CNSTR_FRICTION_DOF, i, status);
       }
     }
   }
@@ -1072,7 +1486,7 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
           if (dist < margin) {
             zero(jacrow, nv);
             jacrow[m.jnt_dofadr[i]] = -(double)side;
-            addConstraint(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status);
+            addConstraint1(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status);
           }
         }
       } else if (t == mjhipJNT_BALL) {
@@ -1086,7 +1500,7 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
         if (dist < margin) {
           zero(jacrow, nv);
           scl3(jacrow + m.jnt_dofadr[i], angleAxis, -1);
-          addConstraint(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status);
+          addConstraint1(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status);
         }
       }
     }
@@ -1098,29 +1512,63 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
         double dist = side * (m.tendon_range[2*i+(side+1)/2] - value);
         if (dist < margin) {
           scl(jacrow, d.ten_J + i*nv, -side, nv);
-          addConstraint(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_TENDON, i, status);
+          addConstraint1(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_TENDON, i, status);
         }
       }
     }
   }
+  instantiateContact(m, d, status);
   int nefc = d.efc_count[0];
+  // mj_diagApprox :1138-1311
   for (int i = 0; i < nefc; i++) {
     int id = d.efc_id[i];
     int tp = d.efc_type[i];
-    // mj_diagApprox
-    double dA = tp == CNSTR_FRICTION_DOF ? m.dof_invweight0[id] :
-                (tp == CNSTR_LIMIT_JOINT ? m.dof_invweight0[m.jnt_dofadr[id]] :
-                 m.tendon_invweight0[id]);
+    if (tp == CNSTR_FRICTION_DOF) {
+      d.efc_diagApprox[i] = m.dof_invweight0[id];
+    } else if (tp == CNSTR_LIMIT_JOINT) {
+      d.efc_diagApprox[i] = m.dof_invweight0[m.jnt_dofadr[id]];
+    } else if (tp == CNSTR_LIMIT_TENDON || tp == CNSTR_FRICTION_TENDON) {
+      d.efc_diagApprox[i] = m.tendon_invweight0[id];
+    } else {   // contact rows
+      int dim = d.con_dim[id];
+      double tran = 0, rot = 0;
+      for (int side = 0; side < 2; side++) {
+        int b = m.geom_bodyid[d.con_geom[2*id+side]];
+        tran += m.body_invweight0[2*b] * 1.0;
+        rot += m.body_invweight0[2*b+1] * 1.0;
+      }
+      if (tp == CNSTR_CONTACT_FRICTIONLESS) {
+        d.efc_diagApprox[i] = tran;
+      } else {
+        for (int j = 0; j < dim-1; j++) {
+          double fri = d.con_friction[5*id+j];
+          double v = tran + fri*fri*(j < 2 ? tran : rot);
+          d.efc_diagApprox[i+2*j] = v;
+          d.efc_diagApprox[i+2*j+1] = v;
+        }
+        i += 2*dim - 3;
+      }
+    }
+  }
+  // mj_makeImpedance :1494-1608; a pyramidal contact's 2*(condim-1) rows share one impedance
+  for (int i = 0; i < nefc; i++) {
+    int id = d.efc_id[i];
+    int tp = d.efc_type[i];
     // getsolparam :1316-1371
     double solref[2], solimp[5];
-    const double* sr = tp == CNSTR_LIMIT_JOINT ? m.jnt_solref + 2*id :
-                       (tp == CNSTR_FRICTION_DOF ? m.dof_solref + 2*id :
-                        m.tendon_solref_lim + 2*id);
-    const double* si = tp == CNSTR_LIMIT_JOINT ? m.jnt_solimp + 5*id :
-                       (tp == CNSTR_FRICTION_DOF ? m.dof_solimp + 5*id :
-                        m.tendon_solimp_lim + 5*id);
-    solref[0] = sr[0]; solref[1] = sr[1];
-    for (int k = 0; k < 5; k++) solimp[k] = si[k];
+    if (tp == CNSTR_CONTACT_FRICTIONLESS || tp == CNSTR_CONTACT_PYRAMIDAL) {
+      for (int k = 0; k < 2; k++) solref[k] = d.con_solref[2*id+k];
+      for (int k = 0; k < 5; k++) solimp[k] = d.con_solimp[5*id+k];
+    } else {
+      const double* sr = tp == CNSTR_LIMIT_JOINT ? m.jnt_solref + 2*id :
+                         (tp == CNSTR_FRICTION_DOF ? m.dof_solref + 2*id :
+                          m.tendon_solref_lim + 2*id);
+      const double* si = tp == CNSTR_LIMIT_JOINT ? m.jnt_solimp + 5*id :
+                         (tp == CNSTR_FRICTION_DOF ? m.dof_solimp + 5*id :
+                          m.tendon_solimp_lim + 5*id);
+      solref[0] = sr[0]; solref[1] = sr[1];
+      for (int k = 0; k < 5; k++) solimp[k] = si[k];
+    }
     if ((solref[0] > 0) ^ (solref[1] > 0)) {
       solref[0] = 0.02;
       solref[1] = 1;
@@ -1133,9 +1581,9 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
     solimp[2] = dmax(0, solimp[2]);
     solimp[3] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[3]));
     solimp[4] = dmax(1, solimp[4]);
+    int dim = tp == CNSTR_CONTACT_PYRAMIDAL ? 2*(d.con_dim[id]-1) : 1;
     double imp, impP;
     getimpedance(solimp, d.efc_pos[i], d.efc_margin[i], &imp, &impP);
-    double R = dmax(MINVAL, (1-imp)*dA/imp);
     double K, Bc;
     if (tp == CNSTR_FRICTION_DOF || tp == CNSTR_FRICTION_TENDON) {
       K = 0;
@@ -1149,13 +1597,31 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
     } else {
       Bc = -solref[1] / dmax(MINVAL, solimp[1]);
     }
-    d.efc_R[i] = R;
-    d.efc_KBIP[4*i] = K;
-    d.efc_KBIP[4*i+1] = Bc;
-    d.efc_KBIP[4*i+2] = imp;
-    d.efc_KBIP[4*i+3] = impP;
-    d.efc_D[i] = 1 / R;
-    d.efc_diagApprox[i] = R * imp / (1-imp);
+    for (int j = 0; j < dim; j++) {
+      int r = i + j;
+      d.efc_R[r] = dmax(MINVAL, (1-imp)*d.efc_diagApprox[r]/imp);
+      d.efc_KBIP[4*r] = K;
+      d.efc_KBIP[4*r+1] = Bc;
+      d.efc_KBIP[4*r+2] = imp;
+      d.efc_KBIP[4*r+3] = impP;
+    }
+    i += dim - 1;
+  }
+  // frictional contacts: R in the friction directions, contact mu (:1562-1598)
+  for (int i = d.efc_count[1] + d.efc_count[2]; i < nefc; i++) {
+    if (d.efc_type[i] == CNSTR_CONTACT_PYRAMIDAL) {
+      int id = d.efc_id[i], dim = d.con_dim[id];
+      d.efc_R[i+1] = d.efc_R[i]/dmax(MINVAL, m.opt.impratio);
+      double mu = d.con_friction[5*id] * sqrt(d.efc_R[i+1]/d.efc_R[i]);
+      d.con_mu[id] = mu;
+      double Rpy = 2*mu*mu*d.efc_R[i];
+      for (int j = 0; j < 2*(dim-1); j++) d.efc_R[i+j] = Rpy;
+      i += 2*(dim-1) - 1;
+    }
+  }
+  for (int i = 0; i < nefc; i++) d.efc_D[i] = 1 / d.efc_R[i];
+  for (int i = 0; i < nefc; i++) {
+    d.efc_diagApprox[i] = d.efc_R[i] * d.efc_KBIP[4*i+2] / (1-d.efc_KBIP[4*i+2]);
   }
 }
 
@@ -1213,7 +1679,7 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
 
 //---------------------------------- engine_inverse.c -----------------------------------------
 
-// mj_invPosition :37-68 (mj_flex: no flexes; mj_collision: no contacts in this subset)
+// mj_invPosition :37-68 (mj_flex: no flexes)
 template <int S>
 MJH_HD void invPosition(const mjhipModel& m, const Lane<S>& d, int* status) {
   kinematics(m, d);
@@ -1222,6 +1688,7 @@ MJH_HD void invPosition(const mjhipModel& m, const Lane<S>& d, int* status) {
   tendon(m, d);
   crb(m, d);
   factorM(m, d);
+  collision(m, d, status);
   makeConstraint(m, d, status);
   transmission(m, d);
 }
@@ -1274,6 +1741,7 @@ struct Mirror {
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
   int efc_cap;
+  int con_cap;
 };
 
 MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
@@ -1288,6 +1756,7 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
   d.efc_cap = mr.efc_cap;
+  d.con_cap = mr.con_cap;
   return d;
 }
 

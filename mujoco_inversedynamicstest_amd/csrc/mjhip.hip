@@ -213,6 +213,7 @@ struct mjhipContext_ {
   int device = 0;
   int capacity = 0;         // instances (multiple of 64)
   int efc_cap = 0;
+  int con_cap = 0;
   hipStream_t stream = nullptr;
   bool own_stream = false;
   mjhipModel hmodel{};      // host copy of sizes (pointers are host pointers of the caller)
@@ -222,6 +223,7 @@ struct mjhipContext_ {
   void* mirror_buf = nullptr;
   size_t mirror_bytes = 0;
   std::unordered_map<std::string, std::pair<double*, int>> fields;   // name -> (ptr, S)
+  std::unordered_map<std::string, std::pair<int*, int>> ifields;   // int scratch fields
   // staging for row-major host transfers
   double* stage = nullptr;
   size_t stage_bytes = 0;
@@ -255,6 +257,7 @@ static unsigned long long model_signature(const mjhipModel* m) {
   feed(&m->opt.o_margin, 8);
   feed(m->opt.o_solref, 16);
   feed(m->opt.o_solimp, 40);
+  feed(m->opt.o_friction, 40);
   feed(&m->opt.integrator, 4);
   feed(&m->opt.cone, 4);
   feed(&m->opt.jacobian, 4);
@@ -266,20 +269,6 @@ static unsigned long long model_signature(const mjhipModel* m) {
 #undef X
 #undef MJ_M
   return h;
-}
-
-static int efc_capacity(const mjhipModel* m) {
-  int n = 0;
-  for (int i = 0; i < m->njnt; i++) {
-    if (m->jnt_limited[i]) n += (m->jnt_type[i] == mjhipJNT_BALL) ? 1 : 2;
-  }
-  for (int i = 0; i < m->ntendon; i++) {
-    if (m->tendon_limited[i]) n += 2;
-  }
-  for (int i = 0; i < m->nv; i++) {
-    if (m->dof_frictionloss[i] > 0) n += 1;
-  }
-  return n;
 }
 
 // model features outside the device path: rejected at context creation (fail loudly)
@@ -304,15 +293,11 @@ static const char* unsupported(const mjhipModel* m) {
       return "ball/free joint transmissions";
     }
   }
-  if (!(m->opt.disableflags & mjhipDSBL_CONTACT) && !(m->opt.disableflags & mjhipDSBL_CONSTRAINT)) {
-    // contacts are evaluated only if some geom pair can collide: the engine does not run
-    // collision detection yet, so models with collidable geoms must disable contacts
-    for (int i = 0; i < m->ngeom; i++) {
-      if (m->geom_contype[i] || m->geom_conaffinity[i]) {
-        return "contacts (set opt.disableflags |= mjDSBL_CONTACT; collision is next)";
-      }
-    }
+  int ncon = mjhip_contactCapacity(m, nullptr);
+  if (ncon < 0) {
+    return "a collidable geom pair needs a collision function other than plane/sphere/capsule";
   }
+  if (ncon > 0 && m->opt.cone == mjhipCONE_ELLIPTIC) return "elliptic friction cones";
   return nullptr;
 }
 
@@ -375,7 +360,8 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   mjhipContext* c = new mjhipContext_();
   c->device = device;
   c->capacity = (capacity + 63) & ~63;
-  c->efc_cap = efc_capacity(m);
+  c->efc_cap = mjhip_efcCapacity(m);
+  c->con_cap = mjhip_contactCapacity(m, nullptr);
   c->hmodel = *m;
 
   // ---- model upload: one buffer, 256-byte aligned arrays
@@ -412,7 +398,7 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   // ---- mirror: per-instance fields in 64-instance blocks
   const size_t nblk = c->capacity / 64;
   size_t mb = 0;
-  const int nv = m->nv, nbody = m->nbody, efc_cap = c->efc_cap;
+  const int nv = m->nv, nbody = m->nbody, efc_cap = c->efc_cap, con_cap = c->con_cap;
   (void)nbody;
 #define MJ_M(n) m->n
 #define XD(name, d0, d1, stage) c->mirror.name##_n = (m->d0) * (d1); \
@@ -427,8 +413,9 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   mb += align256(sizeof(int) * nblk * 64 * (size_t)c->mirror.name##_n); }
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
-  (void)nv; (void)efc_cap;
+  (void)nv; (void)efc_cap; (void)con_cap;
   c->mirror.efc_cap = c->efc_cap;
+  c->mirror.con_cap = c->con_cap;
   c->mirror_bytes = mb;
   if (hipMalloc(&c->mirror_buf, mb) != hipSuccess) {
     set_error("hipMalloc(mirror, %zu bytes) failed", mb);
@@ -449,6 +436,7 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   MJHIP_SCRATCH_FIELDS
 #undef XSC
 #define XSI(name, n) c->mirror.name = (int*)p; \
+  c->ifields[#name] = {c->mirror.name, c->mirror.name##_n}; \
   p += align256(sizeof(int) * nblk * 64 * (size_t)c->mirror.name##_n);
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
@@ -646,6 +634,47 @@ MJHIP_API void* mjhip_mirrorDevicePtr(mjhipContext* c, const char* field) {
   int S;
   if (!c || find_field(c, field, &p, &S)) return nullptr;
   return p;
+}
+
+// int scratch fields (constraint row types/ids/states, counts, contact geoms/dims), one
+// instance-major row of `S` ints per instance
+MJHIP_API int mjhip_mirrorDownloadInt(mjhipContext* c, const char* field, int first, int count,
+                                      int* dst) {
+  if (!c || !field || !dst || first < 0 || count < 0 || first + count > c->capacity) {
+    return MJHIP_ERR_ARG;
+  }
+  auto it = c->ifields.find(field);
+  if (it == c->ifields.end()) {
+    set_error("unknown int mirror field '%s'", field);
+    return MJHIP_ERR_ARG;
+  }
+  int* p = it->second.first;
+  int S = it->second.second;
+  if (!count || !S) return MJHIP_OK;
+  HIPCHECK(hipSetDevice(c->device));
+  int b0 = first / 64, b1 = (first + count + 63) / 64;
+  std::vector<int> tmp((size_t)(b1 - b0) * S * 64);
+  HIPCHECK(hipMemcpyAsync(tmp.data(), p + (size_t)b0*S*64, tmp.size()*sizeof(int),
+                          hipMemcpyDeviceToHost, c->stream));
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  for (int i = 0; i < count; i++) {
+    int inst = first + i;
+    size_t base = (size_t)(inst/64 - b0) * S * 64 + (inst & 63);
+    for (int k = 0; k < S; k++) dst[(size_t)i*S + k] = tmp[base + (size_t)k*64];
+  }
+  return MJHIP_OK;
+}
+
+MJHIP_API int mjhip_mirrorFieldSize(const mjhipContext* c, const char* field) {
+  if (!c || !field) return -1;
+  auto it = c->fields.find(field);
+  return it == c->fields.end() ? -1 : it->second.second;
+}
+
+MJHIP_API int mjhip_fieldSizeInt(const mjhipContext* c, const char* field) {
+  if (!c || !field) return -1;
+  auto it = c->ifields.find(field);
+  return it == c->ifields.end() ? -1 : it->second.second;
 }
 
 // host transfers of whole 64-instance blocks, reordered on the host

@@ -58,6 +58,10 @@ SIGNATURES = {
     "mjhip_mirrorUpload": (ctypes.c_int, [_V, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                           _D]),
     "mjhip_mirrorDevicePtr": (_V, [_V, ctypes.c_char_p]),
+    "mjhip_mirrorDownloadInt": (ctypes.c_int, [_V, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
+                                               _I]),
+    "mjhip_fieldSizeInt": (ctypes.c_int, [_V, ctypes.c_char_p]),
+    "mjhip_mirrorFieldSize": (ctypes.c_int, [_V, ctypes.c_char_p]),
     "mjhip_statusDownload": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _I]),
     "mjhip_inverseFDBatch": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, ctypes.c_double,
                                             _V, _V, _V, _V, ctypes.c_int]),
@@ -210,7 +214,7 @@ class InverseEngine:
   def field(self, name, first=0, count=None):
     """Mirror field `name` of instances [first, first+count) as [count, size] (numpy)."""
     L = lib()
-    S = L.mjhip_fieldSize(ctypes.byref(self.cm), name.encode())
+    S = L.mjhip_mirrorFieldSize(self.ctx, name.encode())
     if S < 0:
       raise MJHIPError(f"unknown field {name}")
     count = self.capacity - first if count is None else count
@@ -218,6 +222,19 @@ class InverseEngine:
     if S:
       _check(L.mjhip_mirrorDownload(self.ctx, name.encode(), first, count,
                                     out.ctypes.data_as(_D)), "mjhip_mirrorDownload")
+    return out[:, :S]
+
+  def field_int(self, name, first=0, count=None):
+    """Int per-instance array `name` (efc_type, efc_count, con_count, con_geom, ...)."""
+    L = lib()
+    S = L.mjhip_fieldSizeInt(self.ctx, name.encode())
+    if S < 0:
+      raise MJHIPError(f"unknown int field {name}")
+    count = self.capacity - first if count is None else count
+    out = np.zeros((count, max(S, 1)), dtype=np.int32)
+    if S:
+      _check(L.mjhip_mirrorDownloadInt(self.ctx, name.encode(), first, count,
+                                       out.ctypes.data_as(_I)), "mjhip_mirrorDownloadInt")
     return out[:, :S]
 
   def set_field(self, name, values, first=0):

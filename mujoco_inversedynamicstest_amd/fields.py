@@ -95,6 +95,7 @@ class Option(ctypes.Structure):
       ("o_margin", ctypes.c_double),
       ("o_solref", ctypes.c_double * 2),
       ("o_solimp", ctypes.c_double * 5),
+      ("o_friction", ctypes.c_double * 5),
       ("integrator", ctypes.c_int),
       ("cone", ctypes.c_int),
       ("jacobian", ctypes.c_int),
@@ -155,6 +156,7 @@ def model_signature(m) -> int:
     feed(np.float64(o[k]).tobytes())
   feed(np.asarray(o["o_solref"], dtype=np.float64)[:2].tobytes())
   feed(np.asarray(o["o_solimp"], dtype=np.float64)[:5].tobytes())
+  feed(np.asarray(o["o_friction"], dtype=np.float64)[:5].tobytes())
   for k in ("integrator", "cone", "jacobian", "disableflags", "enableflags"):
     feed(np.int32(o[k]).tobytes())
   for f in MODEL_FIELDS:

@@ -22,7 +22,8 @@ def model_struct(m) -> fields.CModel:
   o = s.opt
   for k in ("timestep", "impratio", "density", "viscosity", "o_margin"):
     setattr(o, k, float(m.opt[k]))
-  for k, n in (("gravity", 3), ("wind", 3), ("o_solref", 2), ("o_solimp", 5)):
+  for k, n in (("gravity", 3), ("wind", 3), ("o_solref", 2), ("o_solimp", 5),
+               ("o_friction", 5)):
     arr = getattr(o, k)
     for i in range(n):
       arr[i] = float(m.opt[k][i])

@@ -422,6 +422,7 @@ class Model:
       elif k.startswith("__names_"):
         lst = [str(x) for x in z[k]]
         m.names[k[8:]] = [] if lst == [""] and m.sizes.get(_NAME_SIZE.get(k[8:], ""), 0) == 0 else lst
+    m.opt.setdefault("o_friction", [1.0, 1.0, 0.005, 0.0001, 0.0001])   # mjOption default
     for f in fields.MODEL_FIELDS:
       setattr(m, f.name, np.ascontiguousarray(z[f.name]))
     return m
@@ -446,6 +447,7 @@ class MJCFCompiler:
     self.opt = {"timestep": 0.002, "impratio": 1.0, "gravity": [0.0, 0.0, -9.81],
                 "wind": [0.0, 0.0, 0.0], "density": 0.0, "viscosity": 0.0, "o_margin": 0.0,
                 "o_solref": [0.02, 1.0], "o_solimp": [0.9, 0.95, 0.001, 0.5, 2.0],
+                "o_friction": [1.0, 1.0, 0.005, 0.0001, 0.0001],
                 "integrator": 0, "cone": 0, "jacobian": 2, "disableflags": 0,
                 "enableflags": 0}
     self.classes = {}
@@ -576,7 +578,7 @@ class MJCFCompiler:
     for k in ("timestep", "impratio", "density", "viscosity", "o_margin"):
       if k in a:
         o[k] = float(a[k])
-    for k in ("gravity", "wind", "o_solref", "o_solimp"):
+    for k in ("gravity", "wind", "o_solref", "o_solimp", "o_friction"):
       if k in a:
         o[k] = _floats(a[k])
     if "integrator" in a:

@@ -129,3 +129,32 @@ def sample_states(m, n, first=0, seed=SEED, margin=0.05, acc_std=10.0,
   qvel = vst.normal(m.nv)
   qacc = acc_std * vst.normal(m.nv)
   return qpos, qvel, qacc
+
+
+def sample_contact_states(m, n, first=0, seed=SEED + 4, hinge_std=0.02, z_noise=0.02,
+                          vel_std=0.5, acc_std=5.0):
+  """Config 4: keyframe poses with noise, contacts on.
+
+  Instance i takes keyframe i % nkey (squat, stand_on_left_leg, prone, supine for the
+  humanoid), adds N(0, hinge_std) to every hinge/slide coordinate and U(-z_noise, z_noise)
+  to the height of each free joint; qvel ~ N(0, vel_std), qacc ~ N(0, acc_std). Same
+  counter-based streams as sample_states, so shards are world-size independent.
+  """
+  if not m.nkey:
+    raise ValueError("model has no keyframes")
+  idx = np.arange(first, first + n, dtype=np.uint64)
+  st = _Stream(seed, idx, np.zeros(n, dtype=np.int64))
+  key = (np.arange(first, first + n) % m.nkey).astype(np.int64)
+  q = np.array(m.key_qpos, dtype=np.float64).reshape(m.nkey, m.nq)[key].copy()
+  noise = st.normal(m.nq)
+  zn = st.uniform(1)[:, 0] * 2 - 1
+  for j in range(m.njnt):
+    t = int(m.jnt_type[j])
+    a = int(m.jnt_qposadr[j])
+    if t in (2, 3):                       # slide, hinge
+      q[:, a] += hinge_std * noise[:, a]
+    elif t == 0:                          # free: height only
+      q[:, a + 2] += z_noise * zn
+  v = vel_std * st.normal(m.nv)
+  acc = acc_std * st.normal(m.nv)
+  return q, v, acc

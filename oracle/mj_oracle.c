@@ -7,6 +7,7 @@
  */
 #define _GNU_SOURCE
 #include "mj_oracle.h"
+#include "../include/mjhip_contact.h"
 
 #include <math.h>
 #include <pthread.h>
@@ -994,30 +995,354 @@ static void or_passive(const mjhipModel* m, mjhipData* d) {
 
 /*============================ engine_core_constraint.c ====================================*/
 
-int or_efcCapacity(const mjhipModel* m) {
-  int n = 0;
-  for (int i = 0; i < m->njnt; i++) {
-    if (m->jnt_limited[i]) n += (m->jnt_type[i] == mjhipJNT_BALL) ? 1 : 2;
+int or_efcCapacity(const mjhipModel* m) { return mjhip_efcCapacity(m); }
+
+int or_contactCapacity(const mjhipModel* m) { return mjhip_contactCapacity(m, NULL); }
+
+
+/*============================ engine_collision_*.c =========================================*/
+
+static mjtNum mju_dot3(const mjtNum* a, const mjtNum* b) { return a[0]*b[0] + a[1]*b[1] + a[2]*b[2]; }
+static mjtNum mju_norm3(const mjtNum* a) { return sqrt(a[0]*a[0] + a[1]*a[1] + a[2]*a[2]); }
+static mjtNum mju_clip(mjtNum x, mjtNum lo, mjtNum hi) { return x < lo ? lo : (x > hi ? hi : x); }
+
+/* one narrowphase result before the contact parameters are attached */
+typedef struct { mjtNum dist, pos[3], frame[9]; } orRaw;
+
+/* engine_collision_primitive.c mjraw_PlaneSphere */
+static int raw_planeSphere(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
+                           const mjtNum* pos2, mjtNum r2) {
+  c->frame[0] = mat1[2];
+  c->frame[1] = mat1[5];
+  c->frame[2] = mat1[8];
+  mjtNum tmp[3] = {pos2[0] - pos1[0], pos2[1] - pos1[1], pos2[2] - pos1[2]};
+  mjtNum cdist = mju_dot3(tmp, c->frame);
+  if (cdist > margin + r2) return 0;
+  c->dist = cdist - r2;
+  mju_scl3(tmp, c->frame, -c->dist/2 - r2);
+  mju_add3(c->pos, pos2, tmp);
+  mju_zero3(c->frame + 3);
+  return 1;
+}
+
+/* mjc_PlaneCapsule */
+static int col_planeCapsule(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
+                            const mjtNum* pos2, const mjtNum* mat2, const mjtNum* size2) {
+  mjtNum axis[3] = {mat2[2], mat2[5], mat2[8]};
+  mjtNum seg[3] = {size2[1]*axis[0], size2[1]*axis[1], size2[1]*axis[2]};
+  mjtNum p[3];
+  mju_add3(p, pos2, seg);
+  int n1 = raw_planeSphere(c, margin, pos1, mat1, p, size2[0]);
+  mju_sub3(p, pos2, seg);
+  int n2 = raw_planeSphere(c + n1, margin, pos1, mat1, p, size2[0]);
+  if (n1) mju_copy3(c->frame + 3, axis);
+  if (n2) mju_copy3((c + n1)->frame + 3, axis);
+  return n1 + n2;
+}
+
+/* mjraw_SphereSphere */
+static int raw_sphereSphere(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
+                            mjtNum r1, const mjtNum* pos2, const mjtNum* mat2, mjtNum r2) {
+  mjtNum dif[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
+  mjtNum cdist_sqr = mju_dot3(dif, dif);
+  mjtNum min_dist = margin + r1 + r2;
+  if (cdist_sqr > min_dist*min_dist) return 0;
+  c->dist = sqrt(cdist_sqr) - r1 - r2;
+  mju_sub3(c->frame, pos2, pos1);
+  mjtNum len = mju_normalize3(c->frame);
+  if (len < mjMINVAL) {
+    mjtNum a1[3] = {mat1[2], mat1[5], mat1[8]}, a2[3] = {mat2[2], mat2[5], mat2[8]};
+    mju_cross(c->frame, a1, a2);
+    mju_normalize3(c->frame);
   }
-  for (int i = 0; i < m->ntendon; i++) {
-    if (m->tendon_limited[i]) n += 2;
+  mju_scl3(c->pos, c->frame, r1 + c->dist/2);
+  mju_addTo3(c->pos, pos1);
+  mju_zero3(c->frame + 3);
+  return 1;
+}
+
+/* mjraw_SphereCapsule */
+static int col_sphereCapsule(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
+                             mjtNum r1, const mjtNum* pos2, const mjtNum* mat2,
+                             const mjtNum* size2) {
+  mjtNum len = size2[1];
+  mjtNum axis[3] = {mat2[2], mat2[5], mat2[8]};
+  mjtNum vec[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
+  mjtNum x = mju_clip(mju_dot3(axis, vec), -len, len);
+  mju_scl3(vec, axis, x);
+  mju_addTo3(vec, pos2);
+  return raw_sphereSphere(c, margin, pos1, mat1, r1, vec, mat2, size2[0]);
+}
+
+/* mjraw_CapsuleCapsule */
+static int col_capsuleCapsule(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
+                              const mjtNum* size1, const mjtNum* pos2, const mjtNum* mat2,
+                              const mjtNum* size2) {
+  mjtNum axis1[3] = {mat1[2]*size1[1], mat1[5]*size1[1], mat1[8]*size1[1]};
+  mjtNum axis2[3] = {mat2[2]*size2[1], mat2[5]*size2[1], mat2[8]*size2[1]};
+  mjtNum dif[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
+  mjtNum ma = mju_dot3(axis1, axis1);
+  mjtNum mb = -mju_dot3(axis1, axis2);
+  mjtNum mc = mju_dot3(axis2, axis2);
+  mjtNum u = -mju_dot3(axis1, dif);
+  mjtNum v = mju_dot3(axis2, dif);
+  mjtNum det = ma*mc - mb*mb;
+  mjtNum vec1[3], vec2[3];
+  if (fabs(det) >= mjMINVAL) {
+    mjtNum x1 = (mc*u - mb*v) / det;
+    mjtNum x2 = (ma*v - mb*u) / det;
+    if (x1 > 1) {
+      x1 = 1;
+      x2 = (v - mb) / mc;
+    } else if (x1 < -1) {
+      x1 = -1;
+      x2 = (v + mb) / mc;
+    }
+    if (x2 > 1) {
+      x2 = 1;
+      x1 = mju_clip((u - mb) / ma, -1, 1);
+    } else if (x2 < -1) {
+      x2 = -1;
+      x1 = mju_clip((u + mb) / ma, -1, 1);
+    }
+    mju_scl3(vec1, axis1, x1);
+    mju_addTo3(vec1, pos1);
+    mju_scl3(vec2, axis2, x2);
+    mju_addTo3(vec2, pos2);
+    return raw_sphereSphere(c, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
   }
-  for (int i = 0; i < m->nv; i++) {
-    if (m->dof_frictionloss[i] > 0) n += 1;
+  /* parallel axes: up to two contacts from the four segment ends */
+  mju_add3(vec1, pos1, axis1);
+  mjtNum x2 = mju_clip((v - mb) / mc, -1, 1);
+  mju_scl3(vec2, axis2, x2);
+  mju_addTo3(vec2, pos2);
+  int n1 = raw_sphereSphere(c, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
+  mju_sub3(vec1, pos1, axis1);
+  x2 = mju_clip((v + mb) / mc, -1, 1);
+  mju_scl3(vec2, axis2, x2);
+  mju_addTo3(vec2, pos2);
+  int n2 = raw_sphereSphere(c + n1, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
+  if (n1 + n2 >= 2) return n1 + n2;
+  mju_add3(vec2, pos2, axis2);
+  mjtNum x1 = mju_clip((u - mb) / ma, -1, 1);
+  mju_scl3(vec1, axis1, x1);
+  mju_addTo3(vec1, pos1);
+  int n3 = raw_sphereSphere(c + n1 + n2, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
+  if (n1 + n2 + n3 >= 2) return n1 + n2 + n3;
+  mju_sub3(vec2, pos2, axis2);
+  x1 = mju_clip((u + mb) / ma, -1, 1);
+  mju_scl3(vec1, axis1, x1);
+  mju_addTo3(vec1, pos1);
+  int n4 = raw_sphereSphere(c + n1 + n2 + n3, margin, vec1, mat1, size1[0], vec2, mat2,
+                            size2[0]);
+  return n1 + n2 + n3 + n4;
+}
+
+/* engine_util_spatial.c mju_makeFrame (xaxis given, yaxis optional) */
+static void mju_makeFrame(mjtNum* frame) {
+  mjtNum tmp[3];
+  mju_normalize3(frame);
+  if (mju_norm3(frame + 3) < 0.5) {
+    mju_zero3(frame + 3);
+    if (frame[1] < 0.5 && frame[1] > -0.5) frame[4] = 1;
+    else frame[5] = 1;
   }
-  return n;
+  mju_scl3(tmp, frame, mju_dot3(frame, frame + 3));
+  mju_sub3(frame + 3, frame + 3, tmp);
+  mju_normalize3(frame + 3);
+  mju_cross(frame + 6, frame, frame + 3);
+}
+
+/* engine_collision_driver.c mj_contactParam (geom : geom) */
+static void or_contactParam(const mjhipModel* m, int g1, int g2, int* condim, mjtNum* gap,
+                            mjtNum* solref, mjtNum* solimp, mjtNum* friction) {
+  mjtNum fri[3];
+  int p1 = m->geom_priority[g1], p2 = m->geom_priority[g2];
+  *gap = mjMAX(m->geom_gap[g1], m->geom_gap[g2]);
+  if (p1 != p2) {
+    int g = p1 > p2 ? g1 : g2;
+    *condim = m->geom_condim[g];
+    mju_copy(solref, m->geom_solref + 2*g, 2);
+    mju_copy(solimp, m->geom_solimp + 5*g, 5);
+    mju_copy(fri, m->geom_friction + 3*g, 3);
+  } else {
+    *condim = mjMAX(m->geom_condim[g1], m->geom_condim[g2]);
+    mjtNum s1 = m->geom_solmix[g1], s2 = m->geom_solmix[g2], mix;
+    if (s1 >= mjMINVAL && s2 >= mjMINVAL) mix = s1 / (s1 + s2);
+    else if (s1 < mjMINVAL && s2 < mjMINVAL) mix = 0.5;
+    else if (s1 < mjMINVAL) mix = 0.0;
+    else mix = 1.0;
+    const mjtNum *r1 = m->geom_solref + 2*g1, *r2 = m->geom_solref + 2*g2;
+    if (r1[0] > 0 && r2[0] > 0) {
+      for (int i = 0; i < 2; i++) solref[i] = mix*r1[i] + (1-mix)*r2[i];
+    } else {
+      for (int i = 0; i < 2; i++) solref[i] = mjMIN(r1[i], r2[i]);
+    }
+    for (int i = 0; i < 5; i++) {
+      solimp[i] = mix*m->geom_solimp[5*g1+i] + (1-mix)*m->geom_solimp[5*g2+i];
+    }
+    for (int i = 0; i < 3; i++) {
+      fri[i] = mjMAX(m->geom_friction[3*g1+i], m->geom_friction[3*g2+i]);
+    }
+  }
+  friction[0] = fri[0];
+  friction[1] = fri[0];
+  friction[2] = fri[1];
+  friction[3] = fri[2];
+  friction[4] = fri[2];
+}
+
+/* mj_filterSphere: 1 = the bounding spheres (or plane distance) rule the pair out */
+static int or_filterSphere(const mjhipModel* m, const mjhipData* d, int g1, int g2,
+                           mjtNum margin) {
+  const mjtNum *p1 = d->geom_xpos + 3*g1, *p2 = d->geom_xpos + 3*g2;
+  mjtNum rb1 = m->geom_rbound[g1], rb2 = m->geom_rbound[g2];
+  if (rb1 > 0 && rb2 > 0) {
+    mjtNum dif[3] = {p1[0]-p2[0], p1[1]-p2[1], p1[2]-p2[2]};
+    mjtNum bound = rb1 + rb2 + margin;
+    return dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2] > bound*bound;
+  }
+  for (int side = 0; side < 2; side++) {
+    int gp = side ? g2 : g1, go = side ? g1 : g2;
+    if (m->geom_type[gp] == mjhipGEOM_PLANE && m->geom_rbound[go] > 0) {
+      const mjtNum* mat = d->geom_xmat + 9*gp;
+      mjtNum norm[3] = {mat[2], mat[5], mat[8]}, dif[3];
+      mju_sub3(dif, d->geom_xpos + 3*go, d->geom_xpos + 3*gp);
+      if (mju_dot3(dif, norm) > margin + m->geom_rbound[go]) return 1;
+    }
+  }
+  return 0;
+}
+
+/* mj_collideGeoms (dynamic filters, narrowphase, mj_setContact) for geoms of two bodies */
+static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, int g1, int g2) {
+  if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
+  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  if (mjhip_pairMaxContacts(t1, t2) <= 0) return;   /* none (unsupported: rejected earlier) */
+  if (mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1], m->geom_contype[g2],
+                          m->geom_conaffinity[g2])) {
+    return;
+  }
+  mjtNum margin = mjENABLED(mjhipENBL_OVERRIDE) ? m->opt.o_margin
+                                                : mjMAX(m->geom_margin[g1], m->geom_margin[g2]);
+  if (or_filterSphere(m, d, g1, g2, margin)) return;
+  const mjtNum *pos1 = d->geom_xpos + 3*g1, *mat1 = d->geom_xmat + 9*g1;
+  const mjtNum *pos2 = d->geom_xpos + 3*g2, *mat2 = d->geom_xmat + 9*g2;
+  const mjtNum *size1 = m->geom_size + 3*g1, *size2 = m->geom_size + 3*g2;
+  orRaw raw[2];
+  int num = 0;
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) {
+    num = raw_planeSphere(raw, margin, pos1, mat1, pos2, size2[0]);
+  } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CAPSULE) {
+    num = col_planeCapsule(raw, margin, pos1, mat1, pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_SPHERE) {
+    num = raw_sphereSphere(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2[0]);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CAPSULE) {
+    num = col_sphereCapsule(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {
+    num = col_capsuleCapsule(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
+  }
+  if (!num) return;
+  int condim;
+  mjtNum gap, solref[2], solimp[5], friction[5], solreffriction[2] = {0, 0};
+  or_contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
+  for (int k = 0; k < num; k++) {
+    int i = e->ncon;
+    if (i >= e->con_capacity) return;   /* cannot happen: capacity is exact */
+    e->con_dist[i] = raw[k].dist;
+    mju_copy3(e->con_pos + 3*i, raw[k].pos);
+    mju_copy(e->con_frame + 9*i, raw[k].frame, 9);
+    e->con_geom[2*i] = g1;
+    e->con_geom[2*i+1] = g2;
+    /* mj_setContact :1387-1415 with mj_assignRef/Imp/Friction (constraint.c:122-165) */
+    e->con_dim[i] = condim;
+    e->con_includemargin[i] = margin - gap;
+    const int ovr = mjENABLED(mjhipENBL_OVERRIDE) != 0;
+    mju_copy(e->con_solref + 2*i, ovr ? m->opt.o_solref : solref, 2);
+    mju_copy(e->con_solreffriction + 2*i, ovr ? m->opt.o_solref : solreffriction, 2);
+    mju_copy(e->con_solimp + 5*i, ovr ? m->opt.o_solimp : solimp, 5);
+    for (int j = 0; j < 5; j++) {
+      e->con_friction[5*i+j] = mjMAX(1e-5, ovr ? m->opt.o_friction[j] : friction[j]);
+    }
+    e->con_exclude[i] = (e->con_dist[i] >= e->con_includemargin[i]);
+    mju_makeFrame(e->con_frame + 9*i);
+    e->con_efc_address[i] = -1;
+    e->con_mu[i] = 0;
+    e->ncon = i + 1;
+  }
+}
+
+/* contactcompare (engine_collision_driver.c:223-257) on the geom ids of two contacts */
+static int or_contactLess(const mjhipModel* m, const orEfc* e, int a, int b) {
+  int a1 = e->con_geom[2*a], a2 = e->con_geom[2*a+1];
+  int b1 = e->con_geom[2*b], b2 = e->con_geom[2*b+1];
+  if (m->geom_type[a1] > m->geom_type[a2]) { int t = a1; a1 = a2; a2 = t; }
+  if (m->geom_type[b1] > m->geom_type[b2]) { int t = b1; b1 = b2; b2 = t; }
+  return a1 < b1 || (a1 == b1 && a2 < b2);
+}
+
+static void or_swapContacts(orEfc* e, int a, int b) {
+#define SWP(arr, k) for (int j = 0; j < (k); j++) { mjtNum t = e->arr[(k)*a+j]; \
+    e->arr[(k)*a+j] = e->arr[(k)*b+j]; e->arr[(k)*b+j] = t; }
+#define SWPI(arr, k) for (int j = 0; j < (k); j++) { int t = e->arr[(k)*a+j]; \
+    e->arr[(k)*a+j] = e->arr[(k)*b+j]; e->arr[(k)*b+j] = t; }
+  SWP(con_dist, 1) SWP(con_pos, 3) SWP(con_frame, 9) SWP(con_includemargin, 1)
+  SWP(con_friction, 5) SWP(con_solref, 2) SWP(con_solreffriction, 2) SWP(con_solimp, 5)
+  SWP(con_mu, 1) SWPI(con_dim, 1) SWPI(con_geom, 2) SWPI(con_exclude, 1)
+  SWPI(con_efc_address, 1)
+#undef SWP
+#undef SWPI
+}
+
+/* mj_collision (engine_collision_driver.c:265-497): candidate body pairs in signature order
+ * (mjhip_contact.h), geoms all-to-all; a pair handled by the midphase (mj_collideTree: a
+ * body with more than one geom) has its contacts stably sorted by contactcompare */
+static void or_collision(const mjhipModel* m, const mjhipData* d, orEfc* e) {
+  e->ncon = 0;
+  if (!mjhip_contactsEnabled(m)) return;
+  for (int b1 = 0; b1 < m->nbody; b1++) {
+    for (int b2 = b1 + 1; b2 < m->nbody; b2++) {
+      if (!mjhip_bodyPairCandidate(m, b1, b2)) continue;
+      int n1 = m->body_geomnum[b1], n2 = m->body_geomnum[b2];
+      int before = e->ncon;
+      for (int i = 0; i < n1; i++) {
+        for (int j = 0; j < n2; j++) {
+          or_collideGeoms(m, d, e, m->body_geomadr[b1] + i, m->body_geomadr[b2] + j);
+        }
+      }
+      int midphase = !mjDISABLED(mjhipDSBL_MIDPHASE) && !(n1 == 1 && n2 == 1);
+      if (midphase) {   /* stable insertion sort (mjSORT is stable) */
+        for (int a = before + 1; a < e->ncon; a++) {
+          for (int b = a; b > before && or_contactLess(m, e, b, b - 1); b--) {
+            or_swapContacts(e, b, b - 1);
+          }
+        }
+      }
+    }
+  }
+}
+
+/* mju_mulMatMat (engine_util_blas.c:818-831) */
+static void mju_mulMatMat(mjtNum* res, const mjtNum* mat1, const mjtNum* mat2, int r1, int c1,
+                          int c2) {
+  mju_zero(res, r1*c2);
+  for (int i = 0; i < r1; i++) {
+    for (int k = 0; k < c1; k++) {
+      mjtNum tmp = mat1[i*c1+k];
+      if (tmp) mju_addToScl(res + i*c2, mat2 + k*c2, tmp, c2);
+    }
+  }
 }
 
 /* :265-356, dense Jacobian branch */
 static void mj_addConstraint(const mjhipModel* m, orEfc* e, const mjtNum* jac, const mjtNum* pos,
                              const mjtNum* margin, mjtNum frictionloss, int size, int type,
                              int id) {
-  int empty = 1, nv = m->nv, nefc = e->nefc;
-  for (int i = 0; i < size*nv; i++) {
-    if (jac[i]) {
-      empty = 0;
-      break;
-    }
+  int nv = m->nv, nefc = e->nefc;
+  int empty = !(type == orCNSTR_CONTACT_FRICTIONLESS || type == orCNSTR_CONTACT_PYRAMIDAL ||
+                type == orCNSTR_CONTACT_ELLIPTIC);
+  for (int i = 0; empty && i < size*nv; i++) {
+    if (jac[i]) empty = 0;
   }
   if (empty) return;
   mju_copy(e->efc_J + nefc*nv, jac, size*nv);
@@ -1098,7 +1423,51 @@ static void or_instantiateLimit(const mjhipModel* m, mjhipData* d, orEfc* e, mjt
   }
 }
 
-/* :1138-1311 (limit and friction rows) */
+/* mj_instantiateContact :964-1131, dense, pyramidal or frictionless (elliptic cones are
+ * rejected with contacts) */
+static void or_instantiateContact(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  int nv = m->nv;
+  if (mjDISABLED(mjhipDSBL_CONTACT) || e->ncon == 0 || nv == 0) return;
+  mjtNum* jac = (mjtNum*)malloc(6*nv*sizeof(mjtNum));
+  mjtNum* jacdif = (mjtNum*)malloc(6*nv*sizeof(mjtNum));
+  mjtNum* jac1p = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+  mjtNum* jac2p = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+  mjtNum* jac1r = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+  mjtNum* jac2r = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+  mjtNum *jacdifp = jacdif, *jacdifr = jacdif + 3*nv;
+  for (int i = 0; i < e->ncon; i++) {
+    if (e->con_exclude[i]) continue;
+    int dim = e->con_dim[i];
+    e->con_efc_address[i] = e->nefc;
+    int b1 = m->geom_bodyid[e->con_geom[2*i]], b2 = m->geom_bodyid[e->con_geom[2*i+1]];
+    const mjtNum* cpos_ = e->con_pos + 3*i;
+    /* mj_jacDifPair (engine_support.c:656-733), dense */
+    mj_jac(m, d, jac1p, jac1r, cpos_, b1);
+    mj_jac(m, d, jac2p, jac2r, cpos_, b2);
+    mju_sub(jacdifp, jac2p, jac1p, 3*nv);
+    if (dim > 3) mju_sub(jacdifr, jac2r, jac1r, 3*nv);
+    /* rotate to the contact frame */
+    const mjtNum* frame = e->con_frame + 9*i;
+    mju_mulMatMat(jac, frame, jacdifp, dim > 1 ? 3 : 1, 3, nv);
+    if (dim > 3) mju_mulMatMat(jac + 3*nv, frame, jacdifr, dim-3, 3, nv);
+    if (dim == 1) {
+      mj_addConstraint(m, e, jac, e->con_dist + i, e->con_includemargin + i, 0, 1,
+                       orCNSTR_CONTACT_FRICTIONLESS, i);
+    } else {
+      mjtNum cpos[2] = {e->con_dist[i], e->con_dist[i]};
+      mjtNum cmargin[2] = {e->con_includemargin[i], e->con_includemargin[i]};
+      for (int k = 1; k < dim; k++) {
+        mjtNum f = e->con_friction[5*i + k-1];
+        for (int j = 0; j < nv; j++) jacdifp[j] = jac[j] + jac[k*nv+j]*f;
+        for (int j = 0; j < nv; j++) jacdifp[nv+j] = jac[j] + jac[k*nv+j]*(-f);
+        mj_addConstraint(m, e, jacdifp, cpos, cmargin, 0, 2, orCNSTR_CONTACT_PYRAMIDAL, i);
+      }
+    }
+  }
+  free(jac); free(jacdif); free(jac1p); free(jac2p); free(jac1r); free(jac2r);
+}
+
+/* :1138-1311 (limit, friction and contact rows) */
 static void or_diagApprox(const mjhipModel* m, orEfc* e) {
   for (int i = 0; i < e->nefc; i++) {
     int id = e->efc_id[i];
@@ -1112,15 +1481,44 @@ static void or_diagApprox(const mjhipModel* m, orEfc* e) {
     case orCNSTR_LIMIT_TENDON:
       e->efc_diagApprox[i] = m->tendon_invweight0[id];
       break;
+    case orCNSTR_CONTACT_FRICTIONLESS:
+    case orCNSTR_CONTACT_PYRAMIDAL: {
+      int dim = e->con_dim[id];
+      mjtNum tran = 0, rot = 0;
+      for (int side = 0; side < 2; side++) {
+        int b = m->geom_bodyid[e->con_geom[2*id+side]];
+        tran += m->body_invweight0[2*b] * 1.0;
+        rot += m->body_invweight0[2*b+1] * 1.0;
+      }
+      if (e->efc_type[i] == orCNSTR_CONTACT_FRICTIONLESS) {
+        e->efc_diagApprox[i] = tran;
+      } else {
+        for (int j = 0; j < dim-1; j++) {
+          mjtNum fri = e->con_friction[5*id+j];
+          e->efc_diagApprox[i+2*j] = e->efc_diagApprox[i+2*j+1] =
+              tran + fri*fri*(j < 2 ? tran : rot);
+        }
+        i += 2*dim - 3;
+      }
+      break;
+    }
     }
   }
 }
 
 /* :1316-1371 (limit and friction rows; solreffriction only applies to contacts) */
 static void getsolparam(const mjhipModel* m, const orEfc* e, int i, mjtNum* solref,
-                        mjtNum* solimp) {
+                        mjtNum* solreffriction, mjtNum* solimp) {
   int id = e->efc_id[i];
+  mju_zero(solreffriction, 2);
   switch (e->efc_type[i]) {
+  case orCNSTR_CONTACT_FRICTIONLESS:
+  case orCNSTR_CONTACT_PYRAMIDAL:
+  case orCNSTR_CONTACT_ELLIPTIC:
+    mju_copy(solref, e->con_solref+2*id, 2);
+    mju_copy(solreffriction, e->con_solreffriction+2*id, 2);
+    mju_copy(solimp, e->con_solimp+5*id, 5);
+    break;
   case orCNSTR_LIMIT_JOINT:
     mju_copy(solref, m->jnt_solref+2*id, 2);
     mju_copy(solimp, m->jnt_solimp+5*id, 5);
@@ -1140,6 +1538,10 @@ static void getsolparam(const mjhipModel* m, const orEfc* e, int i, mjtNum* solr
   }
   if (!mjDISABLED(mjhipDSBL_REFSAFE) && solref[0] > 0) {
     solref[0] = mjMAX(solref[0], 2*m->opt.timestep);
+  }
+  if ((solreffriction[0] > 0) ^ (solreffriction[1] > 0)) mju_zero(solreffriction, 2);
+  if (!mjDISABLED(mjhipDSBL_REFSAFE) && solreffriction[0] > 0) {
+    solreffriction[0] = mjMAX(solreffriction[0], 2*m->opt.timestep);
   }
   solimp[0] = mjMIN(mjhipMAXIMP, mjMAX(mjhipMINIMP, solimp[0]));
   solimp[1] = mjMIN(mjhipMAXIMP, mjMAX(mjhipMINIMP, solimp[1]));
@@ -1191,32 +1593,47 @@ static void getimpedance(const mjtNum* solimp, mjtNum pos, mjtNum margin, mjtNum
   *impP = yP * sgn * (solimp[1]-solimp[0]) / solimp[2];
 }
 
-/* :1494-1608 (dim = 1 rows: limits and friction) */
+/* :1494-1608; a pyramidal contact's 2*(condim-1) rows share one impedance */
 static void or_makeImpedance(const mjhipModel* m, orEfc* e) {
   int nefc = e->nefc;
   mjtNum *R = e->efc_R, *KBIP = e->efc_KBIP;
-  mjtNum imp, impP, solref[2], solimp[5];
+  mjtNum imp, impP, solref[2], solreffriction[2], solimp[5];
   for (int i = 0; i < nefc; i++) {
-    getsolparam(m, e, i, solref, solimp);
-    mjtNum pos = e->efc_pos[i];
-    getimpedance(solimp, pos, e->efc_margin[i], &imp, &impP);
-    R[i] = mjMAX(mjMINVAL, (1-imp)*e->efc_diagApprox[i]/imp);
-    int tp = e->efc_type[i];
-    mjtNum* ref = solref;
-    if (tp == orCNSTR_FRICTION_DOF || tp == orCNSTR_FRICTION_TENDON) {
-      KBIP[4*i] = 0;
-    } else if (ref[0] > 0) {
-      KBIP[4*i] = 1 / mjMAX(mjMINVAL, solimp[1]*solimp[1] * ref[0]*ref[0] * ref[1]*ref[1]);
-    } else {
-      KBIP[4*i] = -ref[0] / mjMAX(mjMINVAL, solimp[1]*solimp[1]);
+    getsolparam(m, e, i, solref, solreffriction, solimp);
+    int dim = e->efc_type[i] == orCNSTR_CONTACT_PYRAMIDAL ? 2*(e->con_dim[e->efc_id[i]]-1) : 1;
+    getimpedance(solimp, e->efc_pos[i], e->efc_margin[i], &imp, &impP);
+    for (int j = 0; j < dim; j++) {
+      int r = i + j, tp = e->efc_type[r];
+      R[r] = mjMAX(mjMINVAL, (1-imp)*e->efc_diagApprox[r]/imp);
+      const mjtNum* ref = solref;
+      if (tp == orCNSTR_FRICTION_DOF || tp == orCNSTR_FRICTION_TENDON) {
+        KBIP[4*r] = 0;
+      } else if (ref[0] > 0) {
+        KBIP[4*r] = 1 / mjMAX(mjMINVAL, solimp[1]*solimp[1] * ref[0]*ref[0] * ref[1]*ref[1]);
+      } else {
+        KBIP[4*r] = -ref[0] / mjMAX(mjMINVAL, solimp[1]*solimp[1]);
+      }
+      if (ref[1] > 0) {
+        KBIP[4*r+1] = 2 / mjMAX(mjMINVAL, solimp[1]*ref[0]);
+      } else {
+        KBIP[4*r+1] = -ref[1] / mjMAX(mjMINVAL, solimp[1]);
+      }
+      KBIP[4*r+2] = imp;
+      KBIP[4*r+3] = impP;
     }
-    if (ref[1] > 0) {
-      KBIP[4*i+1] = 2 / mjMAX(mjMINVAL, solimp[1]*ref[0]);
-    } else {
-      KBIP[4*i+1] = -ref[1] / mjMAX(mjMINVAL, solimp[1]);
+    i += dim - 1;
+  }
+  /* frictional contacts: R in the friction directions, contact mu (:1562-1598) */
+  for (int i = e->ne + e->nf; i < nefc; i++) {
+    if (e->efc_type[i] == orCNSTR_CONTACT_PYRAMIDAL) {
+      int id = e->efc_id[i], dim = e->con_dim[id];
+      const mjtNum* friction = e->con_friction + 5*id;
+      R[i+1] = R[i]/mjMAX(mjMINVAL, m->opt.impratio);
+      e->con_mu[id] = friction[0] * sqrt(R[i+1]/R[i]);
+      mjtNum Rpy = 2*e->con_mu[id]*e->con_mu[id]*R[i];
+      for (int j = 0; j < 2*(dim-1); j++) R[i+j] = Rpy;
+      i += 2*(dim-1) - 1;
     }
-    KBIP[4*i+2] = imp;
-    KBIP[4*i+3] = impP;
   }
   for (int i = 0; i < nefc; i++) e->efc_D[i] = 1 / R[i];
   for (int i = 0; i < nefc; i++) {
@@ -1232,6 +1649,7 @@ static void or_makeConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
   or_instantiateFriction(m, d, e, jac);
   or_instantiateLimit(m, d, e, jac);
   free(jac);
+  or_instantiateContact(m, d, e);
   if (!e->nefc) return;
   or_diagApprox(m, e);
   or_makeImpedance(m, e);
@@ -1315,6 +1733,7 @@ static void or_invPosition(const mjhipModel* m, mjhipData* d, orEfc* e) {
   or_tendon(m, d);
   or_crb(m, d);
   or_factorM(m, d);
+  or_collision(m, d, e);
   or_makeConstraint(m, d, e);
   or_transmission(m, d);
 }

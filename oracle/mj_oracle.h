@@ -41,6 +41,22 @@ typedef struct orEfc_ {
   mjtNum* efc_vel;
   mjtNum* efc_aref;
   mjtNum* efc_force;
+  /* contacts (the mjContact fields this path uses), SoA over con_capacity entries */
+  int con_capacity;
+  int ncon;
+  mjtNum* con_dist;
+  mjtNum* con_pos;             /* x3 */
+  mjtNum* con_frame;           /* x9 */
+  mjtNum* con_includemargin;
+  mjtNum* con_friction;        /* x5 */
+  mjtNum* con_solref;          /* x2 */
+  mjtNum* con_solreffriction;  /* x2 */
+  mjtNum* con_solimp;          /* x5 */
+  mjtNum* con_mu;
+  int* con_dim;
+  int* con_geom;               /* x2 */
+  int* con_exclude;
+  int* con_efc_address;
 } orEfc;
 
 /* mjtConstraint / mjtConstraintState values (mjmodel.h) */
@@ -51,6 +67,7 @@ enum { orCNSTRSTATE_SATISFIED = 0, orCNSTRSTATE_QUADRATIC, orCNSTRSTATE_LINEARNE
        orCNSTRSTATE_LINEARPOS, orCNSTRSTATE_CONE };
 
 int  or_efcCapacity(const mjhipModel* m);
+int  or_contactCapacity(const mjhipModel* m);   /* -1: unsupported collision pair */
 
 /* pipeline (engine_inverse.c) */
 void or_inverseSkip(const mjhipModel* m, mjhipData* d, orEfc* efc, int skipstage,

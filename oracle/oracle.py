@@ -20,6 +20,12 @@ _lib = None
 
 _D = ctypes.POINTER(ctypes.c_double)
 
+# contact arrays of orEfc (mj_oracle.h) and their widths
+CON_DOUBLE = (("con_dist", 1), ("con_pos", 3), ("con_frame", 9), ("con_includemargin", 1),
+              ("con_friction", 5), ("con_solref", 2), ("con_solreffriction", 2),
+              ("con_solimp", 5), ("con_mu", 1))
+CON_INT = (("con_dim", 1), ("con_geom", 2), ("con_exclude", 1), ("con_efc_address", 1))
+
 
 class Efc(ctypes.Structure):
   _fields_ = ([("capacity", ctypes.c_int), ("nefc", ctypes.c_int), ("ne", ctypes.c_int),
@@ -29,7 +35,14 @@ class Efc(ctypes.Structure):
                ("efc_state", ctypes.POINTER(ctypes.c_int))] +
               [(n, _D) for n in ("efc_J", "efc_pos", "efc_margin", "efc_frictionloss",
                                  "efc_diagApprox", "efc_KBIP", "efc_D", "efc_R", "efc_vel",
-                                 "efc_aref", "efc_force")])
+                                 "efc_aref", "efc_force")] +
+              [("con_capacity", ctypes.c_int), ("ncon", ctypes.c_int)] +
+              [(n, _D) for n, _ in CON_DOUBLE] +
+              [(n, ctypes.POINTER(ctypes.c_int)) for n, _ in CON_INT])
+
+
+class UnsupportedModel(ValueError):
+  pass
 
 
 def build():
@@ -46,6 +59,7 @@ def lib():
     Dp = ctypes.POINTER(fields.CData)
     E = ctypes.POINTER(Efc)
     L.or_efcCapacity.argtypes = [M]
+    L.or_contactCapacity.argtypes = [M]
     L.or_inverseSkip.argtypes = [M, Dp, E, ctypes.c_int, ctypes.c_int]
     L.or_inverse.argtypes = [M, Dp, E]
     for fn in ("or_kinematics", "or_comPos", "or_crb", "or_factorM"):
@@ -91,6 +105,18 @@ class Oracle:
       setattr(self.efc, n, _p(a))
     for n, a in self._efc_int.items():
       setattr(self.efc, n, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    ncap = self.L.or_contactCapacity(ctypes.byref(self.cm))
+    if ncap < 0:
+      raise UnsupportedModel("a candidate geom pair needs a collision function outside the "
+                             "implemented primitives (plane/sphere/capsule)")
+    ncap = max(ncap, 1)
+    self.efc.con_capacity = ncap
+    self._con = {n: np.zeros(ncap * k) for n, k in CON_DOUBLE}
+    self._con.update({n: np.zeros(ncap * k, dtype=np.int32) for n, k in CON_INT})
+    for n, k in CON_DOUBLE:
+      setattr(self.efc, n, _p(self._con[n]))
+    for n, k in CON_INT:
+      setattr(self.efc, n, self._con[n].ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
 
   def _args(self):
     return ctypes.byref(self.cm), ctypes.byref(self.d.struct), ctypes.byref(self.efc)
@@ -129,6 +155,12 @@ class Oracle:
     out = np.zeros((self.m.nv, self.m.nv))
     self.L.or_fullM(ctypes.byref(self.cm), _p(out), _p(M))
     return out
+
+  def contact_field(self, name):
+    """Contacts of the last call, one row per contact (width = field width)."""
+    k = dict(CON_DOUBLE + CON_INT)[name]
+    return self._con[name][:self.efc.ncon * k].reshape(self.efc.ncon, k).squeeze(-1) \
+        if k == 1 else self._con[name][:self.efc.ncon * k].reshape(self.efc.ncon, k)
 
   def efc_field(self, name):
     if name in self._efc_arrays:

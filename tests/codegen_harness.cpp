@@ -15,7 +15,8 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
   Mirror mr;
   memset(&mr, 0, sizeof(mr));
   const int nv = m->nv, nbody = m->nbody;
-  (void)nv; (void)nbody;
+  const int con_cap = 0;   // generated kernels serve contact-free models only
+  (void)nv; (void)nbody; (void)con_cap;
 #define MJ_M(n) m->n
 #define XD(name, d0, d1, stage) mr.name##_n = (m->d0) * (d1); \
   mr.name = (double*)calloc((size_t)nblk * 64 * (mr.name##_n + 1), sizeof(double));
@@ -30,6 +31,7 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
   mr.efc_cap = efc_cap;
+  mr.con_cap = con_cap;
   int* wl = (int*)calloc(B + 1, sizeof(int));
   int wc = 0, wnext = 1;
   for (int i = 0; i < B; i++) {

@@ -7,35 +7,58 @@
 
 #include "../mujoco_inversedynamicstest_amd/csrc/engine_device.h"
 
-extern "C" long kh_scratch_doubles(const mjhipModel* m, int efc_cap) {
+// doubles / ints of per-instance scratch (each field padded by one element)
+extern "C" void kh_sizes(const mjhipModel* m, int efc_cap, int con_cap, long* nd, long* ni) {
   const int nv = m->nv, nbody = m->nbody;
-  long total = 0;
-#define XSC(name, n) total += (long)(n) + 1;
+  (void)nv; (void)nbody;
+  long d = 0, i = 0;
+#define XSC(name, n) d += (long)(n) + 1;
   MJHIP_SCRATCH_FIELDS
 #undef XSC
-  (void)nv; (void)nbody;
-  return total;
+#define XSI(name, n) i += (long)(n) + 1;
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+  *nd = d;
+  *ni = i;
 }
 
-// scratch: kh_scratch_doubles() doubles; iscratch: 3*efc_cap + 4 ints (kept between calls,
-// like the device mirror, so skipstage > NONE sees the earlier stages' constraint rows)
+// offset (elements) and length of a scratch field; returns 0 double, 1 int, -1 unknown
+extern "C" int kh_field(const mjhipModel* m, int efc_cap, int con_cap, const char* field,
+                        long* offset, long* len) {
+  const int nv = m->nv, nbody = m->nbody;
+  (void)nv; (void)nbody;
+  long d = 0, i = 0;
+#define XSC(name, n) if (!strcmp(field, #name)) { *offset = d; *len = (n); return 0; } \
+  d += (long)(n) + 1;
+  MJHIP_SCRATCH_FIELDS
+#undef XSC
+#define XSI(name, n) if (!strcmp(field, #name)) { *offset = i; *len = (n); return 1; } \
+  i += (long)(n) + 1;
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
+  return -1;
+}
+
+// scratch / iscratch persist between calls, like the device mirror, so skipstage > NONE sees
+// the earlier stages' constraint rows and contacts
 extern "C" int kh_inverse(const mjhipModel* m, mjhipData* d, double* scratch, int* iscratch,
-                          int efc_cap, int skipstage) {
+                          int efc_cap, int con_cap, int skipstage) {
   mjh::Lane<1> L;
 #define XD(name, d0, d1, stage) L.name.p = d->name;
   MJHIP_DATA_FIELDS
 #undef XD
   const int nv = m->nv, nbody = m->nbody;
+  (void)nv; (void)nbody;
   double* p = scratch;
 #define XSC(name, n) L.name.p = p; p += (long)(n) + 1;
   MJHIP_SCRATCH_FIELDS
 #undef XSC
-  (void)nv; (void)nbody;
-  L.efc_type.p = iscratch;
-  L.efc_id.p = iscratch + efc_cap;
-  L.efc_state.p = iscratch + 2 * efc_cap;
-  L.efc_count.p = iscratch + 3 * efc_cap;
+  int* q = iscratch;
+#define XSI(name, n) L.name.p = q; q += (long)(n) + 1;
+  MJHIP_SCRATCH_INT_FIELDS
+#undef XSI
   L.efc_cap = efc_cap;
+  L.con_cap = con_cap;
   int st = mjh::inverseSkip(*m, L, skipstage);
   d->nefc = L.efc_count[0];
   return st;

@@ -25,24 +25,37 @@ def lib():
       subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fPIC", "-shared",
                       "-o", SO, SRC[0]], check=True)
     L = ctypes.CDLL(SO)
-    L.kh_scratch_doubles.restype = ctypes.c_long
-    L.kh_scratch_doubles.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    L.kh_sizes.restype = None
+    L.kh_sizes.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                           ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long)]
+    L.kh_field.restype = ctypes.c_int
+    L.kh_field.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
+                           ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long)]
     L.kh_inverse.restype = ctypes.c_int
     L.kh_inverse.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                             ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+                             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
     _lib = L
   return _lib
 
 
 class KernelCPU:
-  def __init__(self, m, efc_cap):
+  """One instance of the device pipeline on the host. Capacities default to the engine's
+  (include/mjhip_contact.h, the same functions the oracle uses)."""
+
+  def __init__(self, m, efc_cap=None, con_cap=None):
+    from oracle.oracle import lib as olib
     self.m = m
     self.cm = host.model_struct(m)
     self.d = host.MjData(m)
-    self.efc_cap = efc_cap
-    n = lib().kh_scratch_doubles(ctypes.byref(self.cm), efc_cap)
-    self.scratch = np.zeros(n)
-    self.iscratch = np.zeros(3 * efc_cap + 8, dtype=np.int32)
+    O = olib()
+    self.efc_cap = O.or_efcCapacity(ctypes.byref(self.cm)) if efc_cap is None else efc_cap
+    self.con_cap = max(O.or_contactCapacity(ctypes.byref(self.cm)), 0) if con_cap is None \
+        else con_cap
+    nd, ni = ctypes.c_long(), ctypes.c_long()
+    lib().kh_sizes(ctypes.byref(self.cm), self.efc_cap, self.con_cap, ctypes.byref(nd),
+                   ctypes.byref(ni))
+    self.scratch = np.zeros(nd.value)
+    self.iscratch = np.zeros(ni.value, dtype=np.int32)
 
   def inverse(self, qpos=None, qvel=None, qacc=None, skipstage=0):
     if qpos is not None:
@@ -53,5 +66,15 @@ class KernelCPU:
       self.d.qacc[:] = qacc
     st = lib().kh_inverse(ctypes.byref(self.cm), ctypes.byref(self.d.struct),
                           self.scratch.ctypes.data, self.iscratch.ctypes.data, self.efc_cap,
-                          skipstage)
+                          self.con_cap, skipstage)
     return self.d.qfrc_inverse.copy(), st
+
+  def field(self, name):
+    """Whole scratch field (efc_* rows, con_* contacts, counts)."""
+    off, n = ctypes.c_long(), ctypes.c_long()
+    kind = lib().kh_field(ctypes.byref(self.cm), self.efc_cap, self.con_cap, name.encode(),
+                          ctypes.byref(off), ctypes.byref(n))
+    if kind < 0:
+      raise KeyError(name)
+    arr = self.iscratch if kind else self.scratch
+    return arr[off.value:off.value + n.value]

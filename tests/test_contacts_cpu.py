@@ -1,0 +1,216 @@
+"""Contacts on the CPU.
+
+* The oracle's collision / contact-constraint restatement is pinned by the reference's own
+  tests, restated: test/engine/engine_collision_driver_test.cc (ContactCount, FilterParent,
+  FilterParentDoesntAffectWorldBody) and test/engine/engine_core_constraint_test.cc
+  (RestPenetration), plus analytic answers of the primitive pairs.
+* The device pipeline compiled for the host (tests/cpu_kernel_harness.cpp) must equal the
+  oracle bit for bit on every output, constraint row and contact.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from mujoco_inversedynamicstest_amd import fields, host, mjcf, models
+from mujoco_inversedynamicstest_amd.sampler import sample_contact_states
+from oracle.oracle import CON_DOUBLE, CON_INT, Oracle, UnsupportedModel, lib as olib
+
+from kernel_harness import KernelCPU
+
+mjDSBL_FILTERPARENT = 1 << 9
+
+
+def _geom_pairs(m, o):
+  names = m.names["geom"]
+  return [tuple(names[g] for g in pair) for pair in o.contact_field("con_geom")]
+
+
+def test_contact_count():
+  """engine_collision_driver_test.cc:99-132 — 8 spheres resting on a plane in a body."""
+  m = mjcf.load_xml_string("""
+  <mujoco><worldbody>
+    <body><geom type="plane" size="5 5 .01"/></body>
+    <body pos="0 0 0.9"><freejoint/>
+      <geom type="sphere" size="1" pos="-1 -1 0"/><geom type="sphere" size="1" pos="-1  1 0"/>
+      <geom type="sphere" size="1" pos=" 1 -1 0"/><geom type="sphere" size="1" pos=" 1  1 0"/>
+      <geom type="sphere" size="1" pos="-2 -2 0"/><geom type="sphere" size="1" pos="-2  2 0"/>
+      <geom type="sphere" size="1" pos=" 2 -2 0"/><geom type="sphere" size="1" pos=" 2  2 0"/>
+    </body></worldbody></mujoco>""")
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  assert o.efc.ncon == 8
+  # midphase order (body with 8 geoms): sorted by geom id
+  assert list(o.contact_field("con_geom")[:, 1]) == list(range(1, 9))
+  np.testing.assert_allclose(o.contact_field("con_dist"), -0.1, atol=1e-12)
+
+
+_FILTER_PARENT = """
+  <mujoco><worldbody>
+    <body pos="0 0 0"><freejoint/>
+      <geom name="colliding1" size="1" pos="0 0 100"/>
+      <body><geom size="1"/>
+        <body><joint axis="1 0 0"/><geom size="1" pos="0 0 50"/>
+          <body><geom name="colliding2" size="1" pos="0 0 99.5"/></body>
+        </body>
+      </body>
+    </body></worldbody></mujoco>"""
+
+
+def test_filter_parent():
+  """engine_collision_driver_test.cc:134-175."""
+  m = mjcf.load_xml_string(_FILTER_PARENT)
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  assert o.efc.ncon == 0
+  m.opt["disableflags"] |= mjDSBL_FILTERPARENT
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  assert _geom_pairs(m, o) == [("colliding1", "colliding2")]
+
+
+def test_filter_parent_doesnt_affect_world_body():
+  """engine_collision_driver_test.cc:177-203."""
+  m = mjcf.load_xml_string("""
+  <mujoco><worldbody>
+    <geom name="colliding1" size="1" pos="0 0 100"/>
+    <body pos="0 0 0"><joint axis="1 0 0"/><geom name="colliding2" size="1" pos="0 0 99.5"/>
+    </body></worldbody></mujoco>""")
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  assert _geom_pairs(m, o) == [("colliding1", "colliding2")]
+
+
+@pytest.mark.parametrize("reference", [-100.0, -10.0, 0.1, 0.01])
+@pytest.mark.parametrize("impedance", [0.3, 0.9, 0.99])
+def test_rest_penetration(reference, impedance):
+  """engine_core_constraint_test.cc:161-229, restated for inverse dynamics.
+
+  The reference simulates a sphere on a slide joint until it rests and checks its
+  penetration depth: g(1-imp)/-ref (direct solref) or g(1-imp)(timeconst*dampratio)^2. At
+  that depth, at rest (qvel = qacc = 0), the soft contact force holds the weight exactly,
+  so the inverse dynamics must need no applied force: qfrc_inverse = 0.
+  """
+  m = mjcf.load_xml_string("""
+  <mujoco><worldbody>
+    <geom type="plane" size="1 1 1"/>
+    <body pos="0 0 .2"><joint type="slide" axis="0 0 1"/><geom size=".1"/></body>
+  </worldbody></mujoco>""")
+  g = -m.opt["gravity"][2]
+  dr = 0.8
+  m.geom_solimp[:, 0] = impedance
+  m.geom_solimp[:, 1] = impedance
+  m.geom_solref[:, 0] = reference
+  m.geom_solref[:, 1] = -10 if reference < 0 else dr
+  depth = g * (1 - impedance) / -reference if reference < 0 else \
+      g * (1 - impedance) * (reference * dr) ** 2
+  o = Oracle(m)
+  q = np.array([-0.1 - depth])            # sphere bottom at -depth
+  f = o.inverse(q, np.zeros(1), np.zeros(1))
+  assert o.efc.ncon == 1
+  assert -o.contact_field("con_dist")[0] == pytest.approx(depth, rel=1e-12, abs=1e-15)
+  weight = m.body_mass[1] * g
+  assert abs(f[0]) <= 1e-9 * weight, (f, weight)
+
+
+def _one_contact(xml):
+  m = mjcf.load_xml_string(xml)
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  return m, o
+
+
+def test_plane_sphere_known_answer():
+  """mjraw_PlaneSphere: dist = height - r, point midway into the gap, normal = plane z."""
+  m, o = _one_contact("""<mujoco><worldbody><geom type="plane" size="1 1 1"/>
+    <body pos=".3 -.2 .25"><freejoint/><geom size=".3"/></body></worldbody></mujoco>""")
+  assert o.efc.ncon == 1
+  assert o.contact_field("con_dist")[0] == pytest.approx(-0.05, abs=1e-15)
+  np.testing.assert_allclose(o.contact_field("con_pos")[0], [0.3, -0.2, -0.025], atol=1e-15)
+  np.testing.assert_allclose(o.contact_field("con_frame")[0][:3], [0, 0, 1])
+
+
+def test_plane_capsule_two_contacts():
+  """mjc_PlaneCapsule: a horizontal capsule touches the plane at both segment ends."""
+  m, o = _one_contact("""<mujoco><worldbody><geom type="plane" size="1 1 1"/>
+    <body pos="0 0 .09"><freejoint/><geom type="capsule" fromto="-.2 0 0 .2 0 0" size=".1"/>
+    </body></worldbody></mujoco>""")
+  assert o.efc.ncon == 2
+  np.testing.assert_allclose(o.contact_field("con_dist"), [-0.01, -0.01], atol=1e-15)
+  xs = sorted(o.contact_field("con_pos")[:, 0])
+  np.testing.assert_allclose(xs, [-0.2, 0.2], atol=1e-15)
+  # pyramidal condim 3: four rows per contact
+  assert o.efc.nefc == 8
+
+
+def test_capsule_capsule_crossing_and_sphere_sphere():
+  """mjraw_CapsuleCapsule (crossing axes -> one contact between the axes) and
+  mjraw_SphereSphere (normal from sphere 1 to sphere 2)."""
+  m, o = _one_contact("""<mujoco><option gravity="0 0 0"/><worldbody>
+    <body><freejoint/><geom type="capsule" fromto="-.5 0 0 .5 0 0" size=".1"/></body>
+    <body pos="0 0 .15"><freejoint/><geom type="capsule" fromto="0 -.5 0 0 .5 0" size=".1"/>
+    </body>
+    <body pos="2 0 0"><freejoint/><geom size=".2"/></body>
+    <body pos="2 0 .3"><freejoint/><geom size=".2"/></body>
+  </worldbody></mujoco>""")
+  assert o.efc.ncon == 2
+  np.testing.assert_allclose(o.contact_field("con_dist"), [-0.05, -0.1], atol=1e-14)
+  np.testing.assert_allclose(o.contact_field("con_frame")[:, :3], [[0, 0, 1], [0, 0, 1]],
+                             atol=1e-15)
+  np.testing.assert_allclose(o.contact_field("con_pos")[0], [0, 0, 0.075], atol=1e-15)
+  np.testing.assert_allclose(o.contact_field("con_pos")[1], [2, 0, 0.15], atol=1e-15)
+
+
+def test_unsupported_pair_rejected():
+  m = mjcf.load_xml_string("""<mujoco><worldbody><geom type="plane" size="1 1 1"/>
+    <body><freejoint/><geom type="box" size=".1 .1 .1"/></body></worldbody></mujoco>""")
+  with pytest.raises(UnsupportedModel):
+    Oracle(m)
+
+
+def test_capacity_exact():
+  m = models.load("humanoid", disable_contact=False)
+  cm = host.model_struct(m)
+  L = olib()
+  ncap = L.or_contactCapacity(ctypes.byref(cm))
+  assert ncap > 0 and L.or_efcCapacity(ctypes.byref(cm)) > ncap
+  q, v, a = sample_contact_states(m, 48)
+  o = Oracle(m)
+  for i in range(48):
+    o.inverse(q[i], v[i], a[i])
+    assert o.efc.ncon <= ncap
+
+
+CON_FIELDS = ("con_dist", "con_pos", "con_frame", "con_includemargin", "con_friction",
+              "con_solref", "con_solreffriction", "con_solimp", "con_mu", "con_dim",
+              "con_geom", "con_exclude", "con_efc_address")
+EFC_FIELDS = ("efc_J", "efc_pos", "efc_margin", "efc_frictionloss", "efc_diagApprox",
+              "efc_KBIP", "efc_D", "efc_R", "efc_vel", "efc_aref", "efc_force", "efc_type",
+              "efc_id", "efc_state")
+
+
+def test_device_code_bitexact_with_contacts():
+  """Config-4 humanoid states: every output, row and contact equals the oracle's."""
+  m = models.load("humanoid", disable_contact=False)
+  q, v, a = sample_contact_states(m, 48, first=7)
+  o, k = Oracle(m), KernelCPU(m)
+  seen = 0
+  for i in range(48):
+    o.inverse(q[i], v[i], a[i])
+    k.inverse(q[i], v[i], a[i])
+    ncon, nefc = o.efc.ncon, o.efc.nefc
+    seen += ncon > 0
+    assert k.field("con_count")[0] == ncon and k.field("efc_count")[0] == nefc
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name),
+                                      err_msg=f"{f.name} inst {i}")
+    width = dict(CON_DOUBLE + CON_INT)
+    for name in CON_FIELDS:
+      ref = o.contact_field(name).reshape(ncon, width[name])
+      got = k.field(name)[:ref.size].reshape(ncon, width[name])
+      np.testing.assert_array_equal(got, ref, err_msg=f"{name} inst {i}")
+    for name in EFC_FIELDS:
+      ref = o.efc_field(name)
+      np.testing.assert_array_equal(k.field(name)[:ref.size], ref, err_msg=f"{name} inst {i}")
+  assert seen > 30
