@@ -52,6 +52,7 @@ struct SP {
   XSC(jacp, 3*nv)                     \
   XSC(jacr, 3*nv)                     \
   XSC(qforce, nv)                     \
+  XSC(qacc_save, nv)                  \
   XSC(efc_J, efc_cap*nv)              \
   XSC(efc_pos, efc_cap)               \
   XSC(efc_margin, efc_cap)            \
@@ -1458,7 +1459,9 @@ MJH_HD void getimpedance(const double* solimp, double pos, double margin, double
 
 // mj_makeConstraint :2005-2116 with mj_instantiateFriction (dof), mj_instantiateLimit
 // :824-959 (dense), mj_diagApprox :1138-1311 and mj_makeImpedance :1494-1608 (dim-1 rows)
-template <int S>
+// CONTACT = false compiles the contact code out (models whose contact capacity is 0); the
+// contact path's private arrays would otherwise cost every launch a scratch segment
+template <int S, bool CONTACT = true>
 MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   int nv = m.nv;
   d.efc_count[0] = 0; d.efc_count[1] = 0; d.efc_count[2] = 0; d.efc_count[3] = 0;
@@ -1517,7 +1520,7 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
       }
     }
   }
-  instantiateContact(m, d, status);
+  if constexpr (CONTACT) instantiateContact(m, d, status);
   int nefc = d.efc_count[0];
   // mj_diagApprox :1138-1311
   for (int i = 0; i < nefc; i++) {
@@ -1529,7 +1532,7 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
       d.efc_diagApprox[i] = m.dof_invweight0[m.jnt_dofadr[id]];
     } else if (tp == CNSTR_LIMIT_TENDON || tp == CNSTR_FRICTION_TENDON) {
       d.efc_diagApprox[i] = m.tendon_invweight0[id];
-    } else {   // contact rows
+    } else if constexpr (CONTACT) {   // contact rows
       int dim = d.con_dim[id];
       double tran = 0, rot = 0;
       for (int side = 0; side < 2; side++) {
@@ -1556,7 +1559,7 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
     int tp = d.efc_type[i];
     // getsolparam :1316-1371
     double solref[2], solimp[5];
-    if (tp == CNSTR_CONTACT_FRICTIONLESS || tp == CNSTR_CONTACT_PYRAMIDAL) {
+    if (CONTACT && (tp == CNSTR_CONTACT_FRICTIONLESS || tp == CNSTR_CONTACT_PYRAMIDAL)) {
       for (int k = 0; k < 2; k++) solref[k] = d.con_solref[2*id+k];
       for (int k = 0; k < 5; k++) solimp[k] = d.con_solimp[5*id+k];
     } else {
@@ -1581,7 +1584,7 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
     solimp[2] = dmax(0, solimp[2]);
     solimp[3] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[3]));
     solimp[4] = dmax(1, solimp[4]);
-    int dim = tp == CNSTR_CONTACT_PYRAMIDAL ? 2*(d.con_dim[id]-1) : 1;
+    int dim = (CONTACT && tp == CNSTR_CONTACT_PYRAMIDAL) ? 2*(d.con_dim[id]-1) : 1;
     double imp, impP;
     getimpedance(solimp, d.efc_pos[i], d.efc_margin[i], &imp, &impP);
     double K, Bc;
@@ -1608,7 +1611,7 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
     i += dim - 1;
   }
   // frictional contacts: R in the friction directions, contact mu (:1562-1598)
-  for (int i = d.efc_count[1] + d.efc_count[2]; i < nefc; i++) {
+  for (int i = d.efc_count[1] + d.efc_count[2]; CONTACT && i < nefc; i++) {
     if (d.efc_type[i] == CNSTR_CONTACT_PYRAMIDAL) {
       int id = d.efc_id[i], dim = d.con_dim[id];
       d.efc_R[i+1] = d.efc_R[i]/dmax(MINVAL, m.opt.impratio);
@@ -1680,7 +1683,7 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
 //---------------------------------- engine_inverse.c -----------------------------------------
 
 // mj_invPosition :37-68 (mj_flex: no flexes)
-template <int S>
+template <int S, bool CONTACT = true>
 MJH_HD void invPosition(const mjhipModel& m, const Lane<S>& d, int* status) {
   kinematics(m, d);
   comPos(m, d);
@@ -1688,8 +1691,9 @@ MJH_HD void invPosition(const mjhipModel& m, const Lane<S>& d, int* status) {
   tendon(m, d);
   crb(m, d);
   factorM(m, d);
-  collision(m, d, status);
-  makeConstraint(m, d, status);
+  if constexpr (CONTACT) collision(m, d, status);
+  else d.con_count[0] = 0;
+  makeConstraint<S, CONTACT>(m, d, status);
   transmission(m, d);
 }
 
@@ -1712,17 +1716,89 @@ MJH_HD void invVelocity(const mjhipModel& m, const Lane<S>& d) {
 }
 
 // mj_inverseSkip :197-261 (sensors/energy: none in this subset)
+// mj_solveLD :1629-1707 on the qLD factor (one right-hand side), in place
 template <int S>
+MJH_HD void solveM(const mjhipModel& m, const Lane<S>& d, SP<S> x) {
+  const int nv = m.nv;
+  for (int i = nv-1; i > 0; i--) {
+    if (m.dof_simplenum[i]) continue;
+    int start = m.C_rowadr[i], end = start + m.C_rownnz[i] - 1;
+    double x_i = x[i];
+    if (x_i) {
+      for (int adr = start; adr < end; adr++) x[m.C_colind[adr]] -= d.qLD[adr] * x_i;
+    }
+  }
+  for (int i = 0; i < nv; i++) x[i] *= d.qLDiagInv[i];
+  for (int i = 1; i < nv; i++) {
+    if (m.dof_simplenum[i]) {
+      i += m.dof_simplenum[i] - 1;
+      continue;
+    }
+    int dd = m.C_rownnz[i] - 1;
+    if (dd > 0) {
+      int adr = m.C_rowadr[i];
+      x[i] -= dotSparse(d.qLD + adr, x, dd, m.C_colind + adr);
+    }
+  }
+}
+
+// mj_mulM engine_support.c:966-1017
+template <int S>
+MJH_HD void mulM(const mjhipModel& m, const Lane<S>& d, SP<S> res, SP<S> vec) {
+  const int nv = m.nv;
+  zero(res, nv);
+  for (int i = 0; i < nv; i++) {
+    int adr = m.dof_Madr[i];
+    res[i] = d.qM[adr]*vec[i];
+    if (m.dof_simplenum[i]) continue;
+    int j = m.dof_parentid[i];
+    while (j >= 0) {
+      adr++;
+      res[i] += d.qM[adr]*vec[j];
+      res[j] += d.qM[adr]*vec[i];
+      j = m.dof_parentid[j];
+    }
+  }
+}
+
+// mj_discreteAcc engine_inverse.c:81-164, Euler branch (the implicit integrators are rejected
+// at context creation): qacc <- M^-1 (M + h*diag(B)) qacc when implicit damping applies
+template <int S>
+MJH_HD void discreteAcc(const mjhipModel& m, const Lane<S>& d) {
+  const int nv = m.nv;
+  int dof_damping = 0;
+  if (!(m.opt.disableflags & mjhipDSBL_EULERDAMP)) {
+    for (int i = 0; i < nv; i++) {
+      if (m.dof_damping[i] > 0) {
+        dof_damping = 1;
+        break;
+      }
+    }
+  }
+  if (!dof_damping) return;
+  mulM(m, d, d.qforce, d.qacc);
+  for (int i = 0; i < nv; i++) d.qforce[i] += m.opt.timestep * m.dof_damping[i] * d.qacc[i];
+  copy(d.qacc, d.qforce, nv);
+  solveM(m, d, d.qacc);
+}
+
+template <int S, bool CONTACT = true>
 MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
   int status = 0;
-  if (skipstage < mjhipSTAGE_POS) invPosition(m, d, &status);
+  if (skipstage < mjhipSTAGE_POS) invPosition<S, CONTACT>(m, d, &status);
   if (skipstage < mjhipSTAGE_VEL) invVelocity(m, d);
+  const bool discrete = (m.opt.enableflags & mjhipENBL_INVDISCRETE) != 0;
+  if (discrete) {
+    copy(d.qacc_save, d.qacc, m.nv);
+    discreteAcc(m, d);
+  }
   invConstraint(m, d);
   rne(m, d, 1, d.qfrc_inverse);
   for (int i = 0; i < m.nv; i++) {
     d.qfrc_inverse[i] += m.dof_armature[i] * d.qacc[i]
                          - d.qfrc_passive[i] - d.qfrc_constraint[i];
   }
+  if (discrete) copy(d.qacc, d.qacc_save, m.nv);
   return status;
 }
 

@@ -44,6 +44,7 @@ static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr}};
 
 // generic pipeline over the instances of a work-list (limit-active instances of the fast
 // path); grid = ceil(B/64) blocks, threads past *count exit at once
+template <bool CONTACT>
 __global__ __launch_bounds__(64) void k_inverse_list(mjhipModel m, Mirror mr,
                                                      const int* __restrict__ worklist,
                                                      const int* __restrict__ count,
@@ -53,7 +54,7 @@ __global__ __launch_bounds__(64) void k_inverse_list(mjhipModel m, Mirror mr,
   if (g >= *count) return;
   const long inst = worklist[g];
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
-  int st = mjh::inverseSkip(m, d, mjhipSTAGE_NONE);
+  int st = mjh::inverseSkip<64, CONTACT>(m, d, mjhipSTAGE_NONE);
   if (qfrc_out) {
     for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
   }
@@ -63,7 +64,7 @@ __global__ __launch_bounds__(64) void k_inverse_list(mjhipModel m, Mirror mr,
 
 // Fused mj_inverseSkip over a batch. Optional row-major (instance-major) inputs are copied
 // into the mirror first; optional row-major qfrc_inverse output is written at the end.
-template <int SKIP>
+template <int SKIP, bool CONTACT>
 __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
                                                 const double* __restrict__ qpos_in,
                                                 const double* __restrict__ qvel_in,
@@ -83,7 +84,7 @@ __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
   if (qacc_in) {
     for (int k = 0; k < m.nv; k++) d.qacc[k] = qacc_in[inst*m.nv + k];
   }
-  int st = mjh::inverseSkip(m, d, SKIP);
+  int st = mjh::inverseSkip<64, CONTACT>(m, d, SKIP);
   if (qfrc_out) {
     for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
   }
@@ -278,7 +279,9 @@ static const char* unsupported(const mjhipModel* m) {
   }
   if (m->nmocap) return "mocap bodies";
   if (m->na) return "actuator activations";
-  if (m->opt.enableflags & mjhipENBL_INVDISCRETE) return "mjENBL_INVDISCRETE";
+  if ((m->opt.enableflags & mjhipENBL_INVDISCRETE) && m->opt.integrator != mjhipINT_EULER) {
+    return "mjENBL_INVDISCRETE with an implicit or RK4 integrator (Euler is supported)";
+  }
   if (m->opt.density > 0 || m->opt.viscosity > 0) return "fluid forces";
   for (int i = 0; i < m->ntendon; i++) {
     if (m->tendon_num[i] && m->wrap_type[m->tendon_adr[i]] != mjhipWRAP_JOINT) {
@@ -522,30 +525,41 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     c->fast->launch(grid, block, c->stream, c->mirror, B, qpos, qvel, qacc, qfrc, status,
                     c->worklist + 2, cnt, nxt, c->mirror.efc_count);
     HIPCHECK(hipGetLastError());
-    hipLaunchKernelGGL(k_inverse_list, grid, block, 0, c->stream, c->dmodel, c->mirror,
-                       (const int*)(c->worklist + 2), (const int*)cnt, qfrc, status);
+    if (c->con_cap > 0) {
+      hipLaunchKernelGGL(k_inverse_list<true>, grid, block, 0, c->stream, c->dmodel, c->mirror,
+                         (const int*)(c->worklist + 2), (const int*)cnt, qfrc, status);
+    } else {
+      hipLaunchKernelGGL(k_inverse_list<false>, grid, block, 0, c->stream, c->dmodel,
+                         c->mirror, (const int*)(c->worklist + 2), (const int*)cnt, qfrc, status);
+    }
     HIPCHECK(hipGetLastError());
     c->wl_last = c->wl_parity;
     c->wl_parity ^= 1;
     return MJHIP_OK;
   }
+#define MJHIP_LAUNCH_GENERIC(SK)                                                              \
+  if (c->con_cap > 0) {                                                                       \
+    hipLaunchKernelGGL((k_inverse<SK, true>), grid, block, 0, c->stream, c->dmodel, c->mirror, \
+                       B, qpos, qvel, qacc, qfrc, status);                                    \
+  } else {                                                                                    \
+    hipLaunchKernelGGL((k_inverse<SK, false>), grid, block, 0, c->stream, c->dmodel,           \
+                       c->mirror, B, qpos, qvel, qacc, qfrc, status);                         \
+  }
   switch (skipstage) {
   case mjhipSTAGE_NONE:
-    hipLaunchKernelGGL(k_inverse<0>, grid, block, 0, c->stream, c->dmodel, c->mirror, B, qpos,
-                       qvel, qacc, qfrc, status);
+    MJHIP_LAUNCH_GENERIC(0)
     break;
   case mjhipSTAGE_POS:
-    hipLaunchKernelGGL(k_inverse<1>, grid, block, 0, c->stream, c->dmodel, c->mirror, B, qpos,
-                       qvel, qacc, qfrc, status);
+    MJHIP_LAUNCH_GENERIC(1)
     break;
   case mjhipSTAGE_VEL:
-    hipLaunchKernelGGL(k_inverse<2>, grid, block, 0, c->stream, c->dmodel, c->mirror, B, qpos,
-                       qvel, qacc, qfrc, status);
+    MJHIP_LAUNCH_GENERIC(2)
     break;
   default:
     set_error("skipstage must be mjSTAGE_NONE, mjSTAGE_POS or mjSTAGE_VEL");
     return MJHIP_ERR_ARG;
   }
+#undef MJHIP_LAUNCH_GENERIC
   HIPCHECK(hipGetLastError());
   return MJHIP_OK;
 }

@@ -1754,17 +1754,72 @@ static void or_invConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
 
 /* engine_inverse.c:197-261 (sensors/energy: none in the supported subset;
  * mjENBL_INVDISCRETE is not supported by the oracle) */
+/* engine_support.c:966-1017 mj_mulM (res = M*vec from the sparse qM) */
+static void or_mulM(const mjhipModel* m, const mjhipData* d, mjtNum* res, const mjtNum* vec) {
+  int nv = m->nv;
+  const mjtNum* M = d->qM;
+  mju_zero(res, nv);
+  for (int i = 0; i < nv; i++) {
+    int adr = m->dof_Madr[i];
+    res[i] = M[adr]*vec[i];
+    if (m->dof_simplenum[i]) continue;
+    int j = m->dof_parentid[i];
+    while (j >= 0) {
+      adr++;
+      res[i] += M[adr]*vec[j];
+      res[j] += M[adr]*vec[i];
+      j = m->dof_parentid[j];
+    }
+  }
+}
+
+/* engine_inverse.c:81-164 mj_discreteAcc, Euler integrator: qacc <- M^-1 (M + h*B) qacc when
+ * implicit damping applies. The implicit integrators need mjd_smooth_vel and RK4 is an
+ * error in the reference: both set MJHIP_INST_UNSUPPORTED and leave qacc unchanged. */
+static void or_discreteAcc(const mjhipModel* m, mjhipData* d) {
+  int nv = m->nv;
+  if (m->opt.integrator != mjhipINT_EULER) {
+    d->status |= MJHIP_INST_UNSUPPORTED;
+    return;
+  }
+  int dof_damping = 0;
+  if (!mjDISABLED(mjhipDSBL_EULERDAMP)) {
+    for (int i = 0; i < nv; i++) {
+      if (m->dof_damping[i] > 0) {
+        dof_damping = 1;
+        break;
+      }
+    }
+  }
+  if (!dof_damping) return;
+  mjtNum* qfrc = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  or_mulM(m, d, qfrc, d->qacc);
+  for (int i = 0; i < nv; i++) qfrc[i] += m->opt.timestep * m->dof_damping[i] * d->qacc[i];
+  or_solveM(m, d, d->qacc, qfrc, 1);
+  free(qfrc);
+}
+
 void or_inverseSkip(const mjhipModel* m, mjhipData* d, orEfc* e, int skipstage,
                     int skipsensor) {
   int nv = m->nv;
   (void)skipsensor;
+  mjtNum* qacc = NULL;
   if (skipstage < mjhipSTAGE_POS) or_invPosition(m, d, e);
   if (skipstage < mjhipSTAGE_VEL) or_fwdVelocity(m, d, e);
+  if (mjENABLED(mjhipENBL_INVDISCRETE)) {
+    qacc = (mjtNum*)malloc(nv*sizeof(mjtNum));
+    mju_copy(qacc, d->qacc, nv);
+    or_discreteAcc(m, d);
+  }
   or_invConstraint(m, d, e);
   or_rne(m, d, 1, d->qfrc_inverse);
   for (int i = 0; i < nv; i++) {
     d->qfrc_inverse[i] += m->dof_armature[i] * d->qacc[i]
                           - d->qfrc_passive[i] - d->qfrc_constraint[i];
+  }
+  if (qacc) {
+    mju_copy(d->qacc, qacc, nv);
+    free(qacc);
   }
   d->nefc = e->nefc;
 }

@@ -303,3 +303,22 @@ def test_contacts_config4_parity(humanoid_contacts, humanoid_contacts_eng):
   assert_close(gpu["qfrc_constraint"], np.array(ref_c), "qfrc_constraint")
   assert (ncon_g > 0).mean() > 0.5
   assert width["con_pos"] == 3
+
+
+def test_invdiscrete_euler_parity():
+  """mjENBL_INVDISCRETE (Euler, implicit damping) on the device: matches the oracle, and
+  discrete inverse dynamics of a' = (M + hB)^-1 M a reproduces continuous forces for a."""
+  m = models.load("humanoid", disable_contact=True)
+  m.opt["enableflags"] |= 1 << 3
+  B = 512
+  q, v, a = sample_states(m, B, first=100)
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    assert e.fast_kernel is None
+    f, st = e.inverse(q, v, a, status=True)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(e.field("qacc", 0, B), a)       # restored
+  finally:
+    e.close()
+  ref, _ = oracle_batch(m, q, v, a)
+  assert_close(f, ref["qfrc_inverse"], "qfrc_inverse (INVDISCRETE)")
