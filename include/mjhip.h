@@ -207,11 +207,12 @@ typedef struct mjhipData_ {
 #define XD(name, d0, d1, stage) mjtNum* name;
   MJHIP_DATA_FIELDS
 #undef XD
-  /* fields read by the fwd/inv comparison harness (inverse_test.cpp:51-73) */
-  mjtNum* qfrc_applied;     /* nv */
-  mjtNum* xfrc_applied;     /* nbody x 6 */
-  mjtNum* qfrc_actuator;    /* nv */
-  mjtNum* ctrl;             /* nu */
+  /* forward-dynamics inputs/outputs, also read by the fwd/inv comparison harness
+   * (inverse_test.cpp:51-73): ctrl, qfrc_applied, xfrc_applied, actuator_force,
+   * qfrc_actuator, qfrc_smooth, qacc_smooth */
+#define XD(name, d0, d1, stage) mjtNum* name;
+  MJHIP_DATA_FORWARD
+#undef XD
 } mjhipData;
 
 /*---------------------------- status codes of the batch API ------------------------------*/
@@ -283,6 +284,17 @@ MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B,
                                  const mjtNum* qpos, const mjtNum* qvel, const mjtNum* qacc,
                                  mjtNum* qfrc_inverse, int skipstage, int skipsensor,
                                  int flags, int* status);
+
+/* Batched mj_forward (engine_forward.c:1054-1090 order: fwdPosition, fwdVelocity,
+ * fwdActuation, fwdAcceleration, fwdConstraint) for constraint-free states: qacc =
+ * qacc_smooth = M^-1 (qfrc_passive - qfrc_bias + qfrc_applied + qfrc_actuator + J'xfrc).
+ * The constraint solver is not implemented: an instance with constraint rows is flagged
+ * MJHIP_INST_UNSUPPORTED (its qacc is qacc_smooth). qpos/qvel (B x nq, B x nv) and optional
+ * ctrl (B x nu) are row-major inputs unless MJHIP_FLAG_MIRROR_INPUT; qfrc_applied and
+ * xfrc_applied are read from the mirror (mjhip_mirrorUpload; zero after context creation).
+ * Optional qacc (B x nv) receives the result; every mjData field is in the mirror. */
+MJHIP_API int mjhip_forwardBatch(mjhipContext* c, int B, const mjtNum* qpos, const mjtNum* qvel,
+                                 const mjtNum* ctrl, mjtNum* qacc, int flags, int* status);
 
 /* copy one mirror field (reference name) of instances [first, first+count) to/from host
  * memory in the reference's per-instance row-major layout (count x fieldSize) */

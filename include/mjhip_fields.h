@@ -243,4 +243,17 @@
   MJHIP_DATA_VELOCITY     \
   MJHIP_DATA_ACCELERATION
 
+/* Forward dynamics (mj_forward, engine_forward.c: mj_fwdActuation :276-515,
+ * mj_fwdAcceleration :520-531) and the fwd/inv comparison harness (mj_compareFwdInv
+ * engine_inverse.c:275-316): applied inputs (stage 4) and forward outputs (stage 5).
+ * Not part of mj_inverse's output contract (W), so kept out of MJHIP_DATA_FIELDS. */
+#define MJHIP_DATA_FORWARD \
+  XD(ctrl,              nu,      1,   4) \
+  XD(qfrc_applied,      nv,      1,   4) \
+  XD(xfrc_applied,      nbody,   6,   4) \
+  XD(actuator_force,    nu,      1,   5) \
+  XD(qfrc_actuator,     nv,      1,   5) \
+  XD(qfrc_smooth,       nv,      1,   5) \
+  XD(qacc_smooth,       nv,      1,   5)
+
 #endif  /* MJHIP_FIELDS_H_ */

@@ -70,10 +70,9 @@ static void data_view(mjData* d, mjhipData* hd) {
 #define XD(name, d0, d1, stage) hd->name = d->name;
   MJHIP_DATA_FIELDS
 #undef XD
-  hd->qfrc_applied = d->qfrc_applied;
-  hd->xfrc_applied = d->xfrc_applied;
-  hd->qfrc_actuator = d->qfrc_actuator;
-  hd->ctrl = d->ctrl;
+#define XD(name, d0, d1, stage) hd->name = d->name;
+  MJHIP_DATA_FORWARD
+#undef XD
 }
 
 void mj_inverseSkip(const mjModel* m, mjData* d, int skipstage, int skipsensor) {

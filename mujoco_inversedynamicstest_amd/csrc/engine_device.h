@@ -94,6 +94,7 @@ template <int S>
 struct Lane {
 #define XD(name, d0, d1, stage) SP<S> name;
   MJHIP_DATA_FIELDS
+  MJHIP_DATA_FORWARD
 #undef XD
 #define XSC(name, n) SP<S> name;
   MJHIP_SCRATCH_FIELDS
@@ -864,16 +865,23 @@ MJH_HD void collision(const mjhipModel& m, const Lane<S>& d, int* status) {
   }
 }
 
-// mj_applyFT :1194-1251 (dense), torque = 0 as used by gravcomp
-template <int S, class F, class P>
-MJH_HD void applyForce(const mjhipModel& m, const Lane<S>& d, F force, P point, int body,
-                       SP<S> qfrc_target) {
+// mj_applyFT :1194-1251 (dense)
+template <int S, class F, class T, class P>
+MJH_HD void applyFT(const mjhipModel& m, const Lane<S>& d, F force, T torque, P point, int body,
+                    SP<S> qfrc_target) {
   jac(m, d, point, body);
   mulMatTVec(d.qforce, d.jacp, force, 3, m.nv);
   addTo(qfrc_target, d.qforce, m.nv);
-  double zt[3] = {0, 0, 0};       // mj_gravcomp passes torque = {0, 0, 0}
-  mulMatTVec(d.qforce, d.jacr, zt, 3, m.nv);
+  mulMatTVec(d.qforce, d.jacr, torque, 3, m.nv);
   addTo(qfrc_target, d.qforce, m.nv);
+}
+
+// torque = 0, as mj_gravcomp passes it
+template <int S, class F, class P>
+MJH_HD void applyForce(const mjhipModel& m, const Lane<S>& d, F force, P point, int body,
+                       SP<S> qfrc_target) {
+  double zt[3] = {0, 0, 0};
+  applyFT(m, d, force, zt, point, body, qfrc_target);
 }
 
 //---------------------------------- engine_core_smooth.c -------------------------------------
@@ -1802,6 +1810,82 @@ MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
   return status;
 }
 
+//---------------------------------- engine_forward.c (constraint-free) ----------------------
+
+// mj_fwdActuation :276-515 for joint transmissions with fixed/affine gain and none/affine
+// bias (the actuator subset accepted at context creation); ctrl clamped by ctrlrange
+template <int S>
+MJH_HD void fwdActuation(const mjhipModel& m, const Lane<S>& d) {
+  const int nv = m.nv, nu = m.nu;
+  zero(d.qfrc_actuator, nv);
+  zero(d.actuator_force, nu);
+  if ((m.opt.disableflags & mjhipDSBL_ACTUATION) || !nu) return;
+  for (int i = 0; i < nu; i++) {
+    double ctrl = d.ctrl[i];
+    if (m.actuator_ctrllimited[i] && !(m.opt.disableflags & mjhipDSBL_CLAMPCTRL)) {
+      const double* r = m.actuator_ctrlrange + 2*i;
+      ctrl = ctrl < r[0] ? r[0] : (ctrl > r[1] ? r[1] : ctrl);
+    }
+    const double* prm = m.actuator_gainprm + 10*i;
+    double gain = prm[0];
+    if (m.actuator_gaintype[i] == mjhipGAIN_AFFINE) {
+      gain = prm[0] + prm[1]*d.actuator_length[i] + prm[2]*d.actuator_velocity[i];
+    }
+    double f = gain * ctrl;
+    if (m.actuator_biastype[i] == mjhipBIAS_AFFINE) {
+      prm = m.actuator_biasprm + 10*i;
+      f += prm[0] + prm[1]*d.actuator_length[i] + prm[2]*d.actuator_velocity[i];
+    }
+    if (m.actuator_forcelimited[i]) {
+      const double* r = m.actuator_forcerange + 2*i;
+      f = f < r[0] ? r[0] : (f > r[1] ? r[1] : f);
+    }
+    d.actuator_force[i] = f;
+  }
+  for (int i = 0; i < nu; i++) {            // mju_mulMatTVecSparse
+    double f = d.actuator_force[i];
+    if (!f) continue;
+    int adr = m.moment_rowadr[i];
+    for (int j = 0; j < m.moment_rownnz[i]; j++) {
+      d.qfrc_actuator[m.moment_colind[adr+j]] += d.actuator_moment[adr+j]*f;
+    }
+  }
+}
+
+// mj_xfrcAccumulate engine_support.c:1254-1261
+template <int S>
+MJH_HD void xfrcAccumulate(const mjhipModel& m, const Lane<S>& d, SP<S> qfrc) {
+  for (int i = 1; i < m.nbody; i++) {
+    SP<S> x = d.xfrc_applied + 6*i;
+    if (x[0] || x[1] || x[2] || x[3] || x[4] || x[5]) {
+      applyFT(m, d, x, x + 3, d.xipos + 3*i, i, qfrc);
+    }
+  }
+}
+
+// mj_forward without constraint rows: fwdPosition = invPosition, fwdVelocity, fwdActuation,
+// fwdAcceleration (:520-531), then mj_fwdConstraint with nefc = 0: qacc = qacc_smooth.
+// Instances with constraint rows (the constraint solver is not implemented) are flagged
+// MJHIP_INST_UNSUPPORTED and get qacc = qacc_smooth.
+template <int S, bool CONTACT = true>
+MJH_HD int forwardSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
+  int status = 0;
+  const int nv = m.nv;
+  if (skipstage < mjhipSTAGE_POS) invPosition<S, CONTACT>(m, d, &status);
+  if (skipstage < mjhipSTAGE_VEL) invVelocity(m, d);
+  fwdActuation(m, d);
+  for (int i = 0; i < nv; i++) d.qfrc_smooth[i] = d.qfrc_passive[i] - d.qfrc_bias[i];
+  addTo(d.qfrc_smooth, d.qfrc_applied, nv);
+  addTo(d.qfrc_smooth, d.qfrc_actuator, nv);
+  xfrcAccumulate(m, d, d.qfrc_smooth);
+  copy(d.qacc_smooth, d.qfrc_smooth, nv);
+  solveM(m, d, d.qacc_smooth);
+  copy(d.qacc, d.qacc_smooth, nv);
+  zero(d.qfrc_constraint, nv);
+  if (d.efc_count[0] > 0) status |= MJHIP_INST_UNSUPPORTED;
+  return status;
+}
+
 }  // namespace mjh
 
 //---------------------------------- device mirror (include/mjhip.h layout) ------------------
@@ -1809,6 +1893,7 @@ MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
 struct Mirror {
 #define XD(name, d0, d1, stage) double* name; int name##_n;
   MJHIP_DATA_FIELDS
+  MJHIP_DATA_FORWARD
 #undef XD
 #define XSC(name, n) double* name; int name##_n;
   MJHIP_SCRATCH_FIELDS
@@ -1824,6 +1909,7 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
   mjh::Lane<64> d;
 #define XD(name, d0, d1, stage) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
   MJHIP_DATA_FIELDS
+  MJHIP_DATA_FORWARD
 #undef XD
 #define XSC(name, n) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
   MJHIP_SCRATCH_FIELDS

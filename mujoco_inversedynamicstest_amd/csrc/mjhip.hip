@@ -186,6 +186,36 @@ __global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps,
   }
 }
 
+// Constraint-free mj_forward over a batch (mjh::forwardSkip). Optional row-major qpos, qvel,
+// ctrl are copied into the mirror first; qfrc_applied / xfrc_applied are read from the
+// mirror; optional row-major qacc is written at the end.
+template <bool CONTACT>
+__global__ __launch_bounds__(64) void k_forward(mjhipModel m, Mirror mr, int B,
+                                                const double* __restrict__ qpos_in,
+                                                const double* __restrict__ qvel_in,
+                                                const double* __restrict__ ctrl_in,
+                                                double* __restrict__ qacc_out,
+                                                int* __restrict__ status) {
+  const int blk = blockIdx.x, lane = threadIdx.x;
+  const long inst = (long)blk*64 + lane;
+  if (inst >= B) return;
+  Lane<64> d = lane_view(mr, blk, lane);
+  if (qpos_in) {
+    for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos_in[inst*m.nq + k];
+  }
+  if (qvel_in) {
+    for (int k = 0; k < m.nv; k++) d.qvel[k] = qvel_in[inst*m.nv + k];
+  }
+  if (ctrl_in) {
+    for (int k = 0; k < m.nu; k++) d.ctrl[k] = ctrl_in[inst*m.nu + k];
+  }
+  int st = mjh::forwardSkip<64, CONTACT>(m, d, mjhipSTAGE_NONE);
+  if (qacc_out) {
+    for (int k = 0; k < m.nv; k++) qacc_out[inst*m.nv + k] = d.qacc[k];
+  }
+  if (status) status[inst] = st;
+}
+
 //==================================== host side ==============================================
 
 static thread_local std::string g_last_error;
@@ -324,6 +354,7 @@ MJHIP_API int mjhip_fieldSize(const mjhipModel* m, const char* name) {
 #define MJ_M(n) m->n
 #define XD(nm, d0, d1, stage) if (!strcmp(name, #nm)) return (m->d0) * (d1);
   MJHIP_DATA_FIELDS
+  MJHIP_DATA_FORWARD
 #undef XD
 #undef MJ_M
   return -1;
@@ -407,6 +438,7 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
 #define XD(name, d0, d1, stage) c->mirror.name##_n = (m->d0) * (d1); \
   mb += align256(sizeof(double) * nblk * 64 * (size_t)c->mirror.name##_n);
   MJHIP_DATA_FIELDS
+  MJHIP_DATA_FORWARD
 #undef XD
 #define XSC(name, n) { const int nbody = m->nbody; (void)nbody; c->mirror.name##_n = (n); \
   mb += align256(sizeof(double) * nblk * 64 * (size_t)c->mirror.name##_n); }
@@ -432,6 +464,7 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   c->fields[#name] = {c->mirror.name, c->mirror.name##_n}; \
   p += align256(sizeof(double) * nblk * 64 * (size_t)c->mirror.name##_n);
   MJHIP_DATA_FIELDS
+  MJHIP_DATA_FORWARD
 #undef XD
 #define XSC(name, n) c->mirror.name = (double*)p; \
   c->fields[#name] = {c->mirror.name, c->mirror.name##_n}; \
@@ -445,7 +478,7 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
 #undef XSI
 #undef MJ_M
   // staging: row-major qpos, qvel, qacc, qfrc for `capacity` instances
-  c->stage_bytes = sizeof(double) * (size_t)c->capacity * (m->nq + 3*(size_t)m->nv);
+  c->stage_bytes = sizeof(double) * (size_t)c->capacity * (m->nq + 3*(size_t)m->nv + m->nu);
   if (hipMalloc((void**)&c->stage, c->stage_bytes) != hipSuccess ||
       hipMalloc((void**)&c->status, sizeof(int) * (size_t)c->capacity) != hipSuccess) {
     set_error("hipMalloc(staging) failed");
@@ -610,6 +643,78 @@ MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B, const mjtNum* qpos,
   if (qfrc_inverse && !dev) {
     HIPCHECK(hipMemcpyAsync(qfrc_inverse, sf, sizeof(double)*(size_t)B*m.nv,
                             hipMemcpyDeviceToHost, c->stream));
+  }
+  int anybad = 0;
+  if (status || !dev) {
+    std::vector<int> st(B);
+    HIPCHECK(hipMemcpyAsync(st.data(), c->status, sizeof(int)*(size_t)B, hipMemcpyDeviceToHost,
+                            c->stream));
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    for (int i = 0; i < B; i++) anybad |= st[i];
+    if (status) memcpy(status, st.data(), sizeof(int)*(size_t)B);
+  }
+  return anybad ? MJHIP_ERR_INSTANCE : MJHIP_OK;
+}
+
+MJHIP_API int mjhip_forwardBatch(mjhipContext* c, int B, const mjtNum* qpos, const mjtNum* qvel,
+                                 const mjtNum* ctrl, mjtNum* qacc, int flags, int* status) {
+  if (!c || B < 0) {
+    set_error("mjhip_forwardBatch: bad argument");
+    return MJHIP_ERR_ARG;
+  }
+  if (B > c->capacity) {
+    set_error("batch %d exceeds context capacity %d", B, c->capacity);
+    return MJHIP_ERR_CAPACITY;
+  }
+  const mjhipModel& m = c->hmodel;
+  for (int i = 0; i < m.nu; i++) {
+    if ((m.actuator_gaintype[i] != mjhipGAIN_FIXED && m.actuator_gaintype[i] != mjhipGAIN_AFFINE) ||
+        (m.actuator_biastype[i] != mjhipBIAS_NONE && m.actuator_biastype[i] != mjhipBIAS_AFFINE)) {
+      set_error("mjhip_forwardBatch: muscle/user actuator gain or bias is not supported");
+      return MJHIP_ERR_MODEL;
+    }
+  }
+  if (B == 0) return MJHIP_OK;
+  HIPCHECK(hipSetDevice(c->device));
+  const bool dev = flags & MJHIP_FLAG_DEVICE_PTRS;
+  const bool mirror_in = flags & MJHIP_FLAG_MIRROR_INPUT;
+  const double *dq = nullptr, *dv = nullptr, *dc = nullptr;
+  double* sq = c->stage;
+  double* sv = sq + (size_t)c->capacity*m.nq;
+  double* sa = sv + (size_t)c->capacity*m.nv;
+  double* sc = sa + 2*(size_t)c->capacity*m.nv;
+  if (!mirror_in) {
+    if (!qpos || !qvel) {
+      set_error("mjhip_forwardBatch: qpos/qvel required without MJHIP_FLAG_MIRROR_INPUT");
+      return MJHIP_ERR_ARG;
+    }
+    if (dev) {
+      dq = qpos; dv = qvel; dc = ctrl;
+    } else {
+      HIPCHECK(hipMemcpyAsync(sq, qpos, sizeof(double)*(size_t)B*m.nq, hipMemcpyHostToDevice,
+                              c->stream));
+      HIPCHECK(hipMemcpyAsync(sv, qvel, sizeof(double)*(size_t)B*m.nv, hipMemcpyHostToDevice,
+                              c->stream));
+      if (ctrl && m.nu) {
+        HIPCHECK(hipMemcpyAsync(sc, ctrl, sizeof(double)*(size_t)B*m.nu, hipMemcpyHostToDevice,
+                                c->stream));
+      }
+      dq = sq; dv = sv; dc = (ctrl && m.nu) ? sc : nullptr;
+    }
+  }
+  double* dqacc = qacc ? (dev ? qacc : sa) : nullptr;
+  dim3 grid((B + 63) / 64), block(64);
+  if (c->con_cap > 0) {
+    hipLaunchKernelGGL(k_forward<true>, grid, block, 0, c->stream, c->dmodel, c->mirror, B, dq,
+                       dv, dc, dqacc, c->status);
+  } else {
+    hipLaunchKernelGGL(k_forward<false>, grid, block, 0, c->stream, c->dmodel, c->mirror, B, dq,
+                       dv, dc, dqacc, c->status);
+  }
+  HIPCHECK(hipGetLastError());
+  if (qacc && !dev) {
+    HIPCHECK(hipMemcpyAsync(qacc, sa, sizeof(double)*(size_t)B*m.nv, hipMemcpyDeviceToHost,
+                            c->stream));
   }
   int anybad = 0;
   if (status || !dev) {

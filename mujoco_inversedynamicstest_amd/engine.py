@@ -53,6 +53,7 @@ SIGNATURES = {
     "mjhip_contextSetStream": (ctypes.c_int, [_V, _V]),
     "mjhip_inverseBatch": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, _V, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_int, _I]),
+    "mjhip_forwardBatch": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, _V, ctypes.c_int, _I]),
     "mjhip_mirrorDownload": (ctypes.c_int, [_V, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
                                             _D]),
     "mjhip_mirrorUpload": (ctypes.c_int, [_V, ctypes.c_char_p, ctypes.c_int, ctypes.c_int,
@@ -210,6 +211,33 @@ class InverseEngine:
     if status:
       return out, st
     return out
+
+  def forward(self, qpos, qvel, ctrl=None, qfrc_applied=None, xfrc_applied=None, out=None,
+              status=False):
+    """Batched constraint-free mj_forward (host numpy arrays). Returns qacc [B, nv].
+
+    qfrc_applied [B, nv] / xfrc_applied [B, nbody, 6] are placed in the mirror first (they
+    stay there for later calls, as in mjData); instances with constraint rows are flagged
+    MJHIP_INST_UNSUPPORTED in the status (the constraint solver is not implemented)."""
+    L = lib()
+    qpos = np.ascontiguousarray(qpos, dtype=np.float64).reshape(-1, self.nq)
+    qvel = np.ascontiguousarray(qvel, dtype=np.float64).reshape(-1, self.nv)
+    B = qpos.shape[0]
+    pc = None
+    if ctrl is not None and self.m.nu:
+      ctrl = np.ascontiguousarray(ctrl, dtype=np.float64).reshape(B, self.m.nu)
+      pc = ctrl.ctypes.data
+    if qfrc_applied is not None:
+      self.set_field("qfrc_applied", np.reshape(qfrc_applied, (B, self.nv)))
+    if xfrc_applied is not None:
+      self.set_field("xfrc_applied", np.reshape(xfrc_applied, (B, 6 * self.m.nbody)))
+    if out is None:
+      out = np.zeros((B, self.nv))
+    st = np.zeros(B, dtype=np.int32)
+    rc = L.mjhip_forwardBatch(self.ctx, B, qpos.ctypes.data, qvel.ctypes.data, pc,
+                              out.ctypes.data, 0, st.ctypes.data_as(_I))
+    _check(rc, "mjhip_forwardBatch")     # per-instance flags come back in `st`
+    return (out, st) if status else out
 
   def field(self, name, first=0, count=None):
     """Mirror field `name` of instances [first, first+count) as [count, size] (numpy)."""

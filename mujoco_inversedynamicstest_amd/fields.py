@@ -68,19 +68,20 @@ def _parse():
         r"X\(\s*(\w+)\s*,\s*(\w+)\s*,\s*(\w+)\s*,\s*([\w()]+)\s*\)",
         _macro_body(text, group)):
       model.append(ModelField(ct, nm, d0, d1))
+  def xd(group):
+    return [DataField(nm, d0, d1, int(st)) for nm, d0, d1, st in re.findall(
+        r"XD\(\s*(\w+)\s*,\s*(\w+)\s*,\s*([\w()]+)\s*,\s*(\d)\s*\)",
+        _macro_body(text, group))]
   data = []
   for group in ("MJHIP_DATA_INPUTS", "MJHIP_DATA_POSITION", "MJHIP_DATA_VELOCITY",
                 "MJHIP_DATA_ACCELERATION"):
-    for nm, d0, d1, st in re.findall(
-        r"XD\(\s*(\w+)\s*,\s*(\w+)\s*,\s*([\w()]+)\s*,\s*(\d)\s*\)",
-        _macro_body(text, group)):
-      data.append(DataField(nm, d0, d1, int(st)))
-  return sizes, model, data
+    data += xd(group)
+  return sizes, model, data, xd("MJHIP_DATA_FORWARD")
 
 
-MODEL_SIZES, MODEL_FIELDS, DATA_FIELDS = _parse()
+MODEL_SIZES, MODEL_FIELDS, DATA_FIELDS, FORWARD_FIELDS = _parse()
 MODEL_FIELD = {f.name: f for f in MODEL_FIELDS}
-DATA_FIELD = {f.name: f for f in DATA_FIELDS}
+DATA_FIELD = {f.name: f for f in DATA_FIELDS + FORWARD_FIELDS}
 
 
 class Option(ctypes.Structure):
@@ -113,10 +114,7 @@ class CData(ctypes.Structure):
   _fields_ = ([("nefc", ctypes.c_int), ("status", ctypes.c_int),
                ("solver_fwdinv", ctypes.c_double * 2)] +
               [(f.name, ctypes.POINTER(ctypes.c_double)) for f in DATA_FIELDS] +
-              [("qfrc_applied", ctypes.POINTER(ctypes.c_double)),
-               ("xfrc_applied", ctypes.POINTER(ctypes.c_double)),
-               ("qfrc_actuator", ctypes.POINTER(ctypes.c_double)),
-               ("ctrl", ctypes.POINTER(ctypes.c_double))])
+              [(f.name, ctypes.POINTER(ctypes.c_double)) for f in FORWARD_FIELDS])
 
 
 def output_doubles(sizes: dict) -> int:

@@ -47,12 +47,9 @@ class MjData:
     self.m = m
     sizes = m.sizes
     self._arrays = {}
-    for f in fields.DATA_FIELDS:
+    for f in fields.DATA_FIELDS + fields.FORWARD_FIELDS:
       n = f.size(sizes)
       self._arrays[f.name] = np.zeros(max(n, 1))
-    for name, n in (("qfrc_applied", m.nv), ("qfrc_actuator", m.nv),
-                    ("xfrc_applied", 6 * m.nbody), ("ctrl", m.nu)):
-      self._arrays[name] = np.zeros(max(n, 1))
     # reference defaults (mj_resetData): qpos = qpos0, world body identity frames
     self._arrays["qpos"][:m.nq] = m.qpos0
     self.struct = fields.CData()
@@ -64,12 +61,6 @@ class MjData:
     if arrs is not None and k in arrs:
       f = fields.DATA_FIELD.get(k)
       n = f.size(self.m.sizes) if f else len(arrs[k])
-      if k in ("qfrc_applied", "qfrc_actuator"):
-        n = self.m.nv
-      elif k == "xfrc_applied":
-        n = 6 * self.m.nbody
-      elif k == "ctrl":
-        n = self.m.nu
       return arrs[k][:n]
     raise AttributeError(k)
 

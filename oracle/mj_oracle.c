@@ -1836,8 +1836,9 @@ void or_inverse(const mjhipModel* m, mjhipData* d, orEfc* e) {
 static void or_fwdActuation(const mjhipModel* m, mjhipData* d) {
   int nv = m->nv, nu = m->nu;
   mju_zero(d->qfrc_actuator, nv);
+  mju_zero(d->actuator_force, nu);
   if (mjDISABLED(mjhipDSBL_ACTUATION) || !nu) return;
-  mjtNum* force = (mjtNum*)calloc(nu, sizeof(mjtNum));
+  mjtNum* force = d->actuator_force;
   for (int i = 0; i < nu; i++) {
     mjtNum ctrl = d->ctrl ? d->ctrl[i] : 0;
     if (m->actuator_ctrllimited[i] && !mjDISABLED(mjhipDSBL_CLAMPCTRL)) {
@@ -1866,7 +1867,6 @@ static void or_fwdActuation(const mjhipModel* m, mjhipData* d) {
       d->qfrc_actuator[m->moment_colind[adr+j]] += d->actuator_moment[adr+j]*force[i];
     }
   }
-  free(force);
 }
 
 /* mj_forward for constraint-free states: position, velocity, actuation, acceleration,
@@ -1876,14 +1876,15 @@ int or_forward(const mjhipModel* m, mjhipData* d, orEfc* e) {
   or_invPosition(m, d, e);
   or_fwdVelocity(m, d, e);
   or_fwdActuation(m, d);
-  mjtNum* qfrc_smooth = (mjtNum*)malloc(nv*sizeof(mjtNum));
-  mju_sub(qfrc_smooth, d->qfrc_passive, d->qfrc_bias, nv);
-  mju_addTo(qfrc_smooth, d->qfrc_applied, nv);
-  mju_addTo(qfrc_smooth, d->qfrc_actuator, nv);
-  or_xfrcAccumulate(m, d, qfrc_smooth);
-  or_solveM(m, d, d->qacc, qfrc_smooth, 1);
+  /* mj_fwdAcceleration engine_forward.c:520-531 */
+  mju_sub(d->qfrc_smooth, d->qfrc_passive, d->qfrc_bias, nv);
+  mju_addTo(d->qfrc_smooth, d->qfrc_applied, nv);
+  mju_addTo(d->qfrc_smooth, d->qfrc_actuator, nv);
+  or_xfrcAccumulate(m, d, d->qfrc_smooth);
+  or_solveM(m, d, d->qacc_smooth, d->qfrc_smooth, 1);
+  /* mj_fwdConstraint with nefc = 0: qacc = qacc_smooth, no constraint force */
+  mju_copy(d->qacc, d->qacc_smooth, nv);
   mju_zero(d->qfrc_constraint, nv);
-  free(qfrc_smooth);
   d->nefc = e->nefc;
   return e->nefc;
 }

@@ -41,11 +41,31 @@ extern "C" int kh_field(const mjhipModel* m, int efc_cap, int con_cap, const cha
 
 // scratch / iscratch persist between calls, like the device mirror, so skipstage > NONE sees
 // the earlier stages' constraint rows and contacts
+static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int* iscratch,
+                         int efc_cap, int con_cap);
+
 extern "C" int kh_inverse(const mjhipModel* m, mjhipData* d, double* scratch, int* iscratch,
                           int efc_cap, int con_cap, int skipstage) {
+  mjh::Lane<1> L = bind(m, d, scratch, iscratch, efc_cap, con_cap);
+  int st = mjh::inverseSkip(*m, L, skipstage);
+  d->nefc = L.efc_count[0];
+  return st;
+}
+
+extern "C" int kh_forward(const mjhipModel* m, mjhipData* d, double* scratch, int* iscratch,
+                          int efc_cap, int con_cap) {
+  mjh::Lane<1> L = bind(m, d, scratch, iscratch, efc_cap, con_cap);
+  int st = mjh::forwardSkip(*m, L, mjhipSTAGE_NONE);
+  d->nefc = L.efc_count[0];
+  return st;
+}
+
+static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int* iscratch,
+                         int efc_cap, int con_cap) {
   mjh::Lane<1> L;
 #define XD(name, d0, d1, stage) L.name.p = d->name;
   MJHIP_DATA_FIELDS
+  MJHIP_DATA_FORWARD
 #undef XD
   const int nv = m->nv, nbody = m->nbody;
   (void)nv; (void)nbody;
@@ -59,7 +79,5 @@ extern "C" int kh_inverse(const mjhipModel* m, mjhipData* d, double* scratch, in
 #undef XSI
   L.efc_cap = efc_cap;
   L.con_cap = con_cap;
-  int st = mjh::inverseSkip(*m, L, skipstage);
-  d->nefc = L.efc_count[0];
-  return st;
+  return L;
 }

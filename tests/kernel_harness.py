@@ -31,6 +31,9 @@ def lib():
     L.kh_field.restype = ctypes.c_int
     L.kh_field.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p,
                            ctypes.POINTER(ctypes.c_long), ctypes.POINTER(ctypes.c_long)]
+    L.kh_forward.restype = ctypes.c_int
+    L.kh_forward.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     L.kh_inverse.restype = ctypes.c_int
     L.kh_inverse.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
@@ -68,6 +71,14 @@ class KernelCPU:
                           self.scratch.ctypes.data, self.iscratch.ctypes.data, self.efc_cap,
                           self.con_cap, skipstage)
     return self.d.qfrc_inverse.copy(), st
+
+  def forward(self, qpos, qvel):
+    self.d.qpos[:] = qpos
+    self.d.qvel[:] = qvel
+    st = lib().kh_forward(ctypes.byref(self.cm), ctypes.byref(self.d.struct),
+                          self.scratch.ctypes.data, self.iscratch.ctypes.data, self.efc_cap,
+                          self.con_cap)
+    return self.d.qacc.copy(), st
 
   def field(self, name):
     """Whole scratch field (efc_* rows, con_* contacts, counts)."""

@@ -322,3 +322,37 @@ def test_invdiscrete_euler_parity():
     e.close()
   ref, _ = oracle_batch(m, q, v, a)
   assert_close(f, ref["qfrc_inverse"], "qfrc_inverse (INVDISCRETE)")
+
+
+def test_forward_parity_and_fwdinv_identity(humanoid):
+  """Batched constraint-free mj_forward on the device vs the oracle, then the fwd/inv
+  identity entirely on the device (mj_compareFwdInv, engine_inverse.c:275-316): inverse
+  dynamics of forward's qacc returns qfrc_applied + qfrc_actuator + J'xfrc_applied."""
+  m = humanoid
+  B = 1024
+  q, v, _ = sample_states(m, B, first=300)
+  rng = np.random.default_rng(7)
+  ctrl = rng.uniform(-1.2, 1.2, (B, m.nu))
+  qa = rng.normal(size=(B, m.nv))
+  xa = 0.3 * rng.normal(size=(B, m.nbody, 6))
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    acc, st = e.forward(q, v, ctrl, qfrc_applied=qa, xfrc_applied=xa, status=True)
+    assert (st == 0).all()
+    smooth = e.field("qfrc_smooth", 0, B)
+    f = e.inverse(q, v, acc)
+    passive, bias = e.field("qfrc_passive", 0, B), e.field("qfrc_bias", 0, B)
+  finally:
+    e.close()
+  o = Oracle(m)
+  ref = np.zeros((B, m.nv))
+  for i in range(B):
+    o.d.ctrl[:] = ctrl[i]
+    o.d.qfrc_applied[:] = qa[i]
+    o.d.xfrc_applied[:] = xa[i].ravel()
+    o.set_state(q[i], v[i])
+    o.forward()
+    ref[i] = o.d.qacc
+  assert_close(acc, ref, "forward qacc")
+  expected = smooth - passive + bias          # qfrc_applied + qfrc_actuator + J'xfrc
+  assert_close(f, expected, "fwd/inv identity")

@@ -78,3 +78,28 @@ def test_gravcomp_and_tendon_springs():
   m = mjcf.load_xml_string(xml)
   q, v, a = sample_states(m, 16)
   _compare(m, q, v, a, skip_chain=True)
+
+
+def test_forward_bitexact(humanoid):
+  """Constraint-free mj_forward of the device pipeline equals the oracle's bit for bit,
+  with ctrl, qfrc_applied and xfrc_applied set (engine_forward.c:276-531)."""
+  from mujoco_inversedynamicstest_amd.sampler import sample_states
+  m = humanoid
+  q, v, _ = sample_states(m, 16, first=9)
+  rng = np.random.default_rng(4)
+  o, k = Oracle(m), KernelCPU(m)
+  for i in range(16):
+    ctrl = rng.uniform(-1.5, 1.5, m.nu)
+    qa = rng.normal(size=m.nv)
+    xa = rng.normal(size=(m.nbody, 6)).ravel()
+    for dd in (o.d, k.d):
+      dd.ctrl[:] = ctrl
+      dd.qfrc_applied[:] = qa
+      dd.xfrc_applied[:] = xa
+    o.set_state(q[i], v[i])
+    assert o.forward() == 0
+    acc, st = k.forward(q[i], v[i])
+    assert st == 0
+    for name in ("qacc", "qacc_smooth", "qfrc_smooth", "qfrc_actuator", "actuator_force",
+                 "qfrc_bias", "qfrc_passive", "qM", "qLD"):
+      np.testing.assert_array_equal(getattr(k.d, name), getattr(o.d, name), err_msg=name)
