@@ -55,7 +55,15 @@ def main():
   ap.add_argument("--cpu-sample", type=int, default=1_500_000,
                   help="instances in the CPU-baseline sample (rank 0, N=1 only)")
   ap.add_argument("--no-cpu", action="store_true")
+  ap.add_argument("--config-batch", type=int, default=None,
+                  help="batch for --config 4 (default 4096) or base states for 5 (1024)")
+  ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
+                  help="2: the metric's workload (default). 4: contacts, keyframe poses, "
+                       "batch 4096. 5: mjd_inverseFD over 1024 base states. Configs 4/5 are "
+                       "parity cases reported for reference (DESIGN.md), not the metric")
   args = ap.parse_args()
+  if args.config != 2:
+    return other_config(args)
 
   import torch
   import torch.distributed as dist
@@ -164,6 +172,59 @@ def main():
   eng.close()
   if world > 1:
     dist.destroy_process_group()
+
+
+def other_config(args):
+  """Throughput of configs 4 (contacts) and 5 (finite-difference Jacobians), 1 GPU."""
+  import torch
+  from mujoco_inversedynamicstest_amd import engine, models
+  from mujoco_inversedynamicstest_amd.sampler import sample_contact_states, sample_states
+  torch.cuda.set_device(0)
+  if args.config == 4:
+    m = models.load(args.model, disable_contact=False)
+    B = args.config_batch or 4096
+    q, v, a = sample_contact_states(m, B)
+    eng = engine.InverseEngine(m, capacity=B)
+    eng.upload_states(q, v, a)
+    for _ in range(args.warmup):
+      eng.inverse(B, mirror_input=True)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+      eng.inverse(B, mirror_input=True)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    ncon = eng.field_int("con_count", 0, B)[:, 0]
+    nefc = eng.field_int("efc_count", 0, B)[:, 0]
+    rec = {"metric": "mj_inverse evals/sec, config 4 (contacts on)", "value": B / dt,
+           "unit": "evals/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": dt * 1e3,
+           "dtype": "f64", "kernel": "k_inverse<0, contacts> (generic)",
+           "config": {"workload": f"{args.model} keyframe poses + noise, contacts on",
+                      "batch": B},
+           "ncon_hist": np.bincount(ncon).tolist(), "nefc_max": int(nefc.max()),
+           "nefc_mean": float(nefc.mean())}
+  else:
+    m = models.load(args.model, disable_contact=True)
+    nb = args.config_batch or 1024
+    P = 3 * m.nv + 1
+    q, v, a = sample_states(m, nb)
+    eng = engine.InverseEngine(m, capacity=nb * P)
+    for _ in range(args.warmup):
+      eng.inverse_fd(q, v, a)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+      eng.inverse_fd(q, v, a)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    rec = {"metric": "mjd_inverseFD Jacobian sets/sec, config 5", "value": nb / dt,
+           "unit": "base states/s", "inverse_evals_per_s": nb * P / dt, "n_gpus": 1,
+           "steps": args.steps, "ms_per_step": dt * 1e3, "dtype": "f64",
+           "config": {"workload": f"{args.model}, {nb} base states x {P} evaluations "
+                                  f"(DfDq, DfDv, DfDa, forward differences, eps 1e-6), "
+                                  f"host arrays in/out (PCIe-inclusive)"}}
+  print(json.dumps(rec), flush=True)
+  eng.close()
 
 
 if __name__ == "__main__":
