@@ -73,11 +73,7 @@ struct SP {
   XSC(con_solref, 2*con_cap)          \
   XSC(con_solreffriction, 2*con_cap)  \
   XSC(con_solimp, 5*con_cap)          \
-  XSC(con_mu, con_cap)                \
-  XSC(jac2p, 3*nv*(con_cap > 0))      \
-  XSC(jac2r, 3*nv*(con_cap > 0))      \
-  XSC(cjac, 6*nv*(con_cap > 0))       \
-  XSC(cjacdif, 6*nv*(con_cap > 0))
+  XSC(con_mu, con_cap)
 
 #define MJHIP_SCRATCH_INT_FIELDS      \
   XSI(efc_type, efc_cap)              \
@@ -1374,53 +1370,98 @@ MJH_HD void addConstraint1(const mjhipModel& m, const Lane<S>& d, SP<S> jacrow, 
 }
 
 // mj_instantiateContact :964-1131 (dense; pyramidal or frictionless; elliptic cones are
-// rejected with contacts at context creation)
+// rejected with contacts at context creation). The reference forms the two body Jacobians
+// (mj_jacDifPair), their difference, its rotation into the contact frame (mju_mulMatMat)
+// and the pyramid rows as dense nv-arrays. Every element of those depends only on its own
+// dof, so the rows are formed here dof by dof, in the same order of operations (including
+// mju_mulMatMat's skip of zero frame entries), straight into efc_J: no Jacobian scratch.
+MJH_HD bool ancestorOrSelf(const mjhipModel& m, int a, int b) {
+  while (b > a) b = m.body_parentid[b];   // body ids are depth-first: parents come first
+  return b == a;
+}
+
 template <int S>
 MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, int* status) {
   int nv = m.nv, ncon = d.con_count[0];
   if ((m.opt.disableflags & mjhipDSBL_CONTACT) || ncon == 0 || nv == 0) return;
-  SP<S> jacdifp = d.cjacdif, jacdifr = d.cjacdif + 3*nv, cj = d.cjac;
   for (int i = 0; i < ncon; i++) {
     if (d.con_exclude[i]) continue;
-    int dim = d.con_dim[i];
-    d.con_efc_address[i] = d.efc_count[0];
-    int b1 = m.geom_bodyid[d.con_geom[2*i]], b2 = m.geom_bodyid[d.con_geom[2*i+1]];
-    // mj_jacDifPair (engine_support.c:656-733), dense
-    jacInto(m, d, d.jacp, d.jacr, d.con_pos + 3*i, b1);
-    jacInto(m, d, d.jac2p, d.jac2r, d.con_pos + 3*i, b2);
-    for (int k = 0; k < 3*nv; k++) jacdifp[k] = d.jac2p[k] - d.jacp[k];
-    if (dim > 3) for (int k = 0; k < 3*nv; k++) jacdifr[k] = d.jac2r[k] - d.jacr[k];
-    // mju_mulMatMat(jac, frame, jacdif) (engine_util_blas.c:818-831)
-    SP<S> frame = d.con_frame + 9*i;
-    int rp = dim > 1 ? 3 : 1;
-    zero(cj, rp*nv);
-    for (int r = 0; r < rp; r++) {
-      for (int k = 0; k < 3; k++) {
-        double t = frame[3*r+k];
-        if (t) addToScl(cj + r*nv, jacdifp + k*nv, t, nv);
-      }
+    const int dim = d.con_dim[i];
+    const int rows = dim == 1 ? 1 : 2*(dim - 1);
+    const int nefc = d.efc_count[0];
+    d.con_efc_address[i] = nefc;
+    if (nefc + rows > d.efc_cap) {   // mjWARN_CNSTRFULL analogue (capacity is exact)
+      *status |= MJHIP_INST_CNSTRFULL;
+      continue;
     }
-    if (dim > 3) {
-      zero(cj + 3*nv, (dim-3)*nv);
-      for (int r = 0; r < dim-3; r++) {
-        for (int k = 0; k < 3; k++) {
-          double t = frame[3*r+k];
-          if (t) addToScl(cj + (3+r)*nv, jacdifr + k*nv, t, nv);
+    const int b1 = m.geom_bodyid[d.con_geom[2*i]], b2 = m.geom_bodyid[d.con_geom[2*i+1]];
+    double pos[3], off1[3], off2[3], frame[9], fri[5];
+    copy3(pos, d.con_pos + 3*i);
+    sub3(off1, pos, d.subtree_com + 3*m.body_rootid[b1]);
+    sub3(off2, pos, d.subtree_com + 3*m.body_rootid[b2]);
+    for (int k = 0; k < 9; k++) frame[k] = d.con_frame[9*i+k];
+    for (int k = 0; k < 5; k++) fri[k] = d.con_friction[5*i+k];
+    const int rp = dim > 1 ? 3 : 1;
+    SP<S> J = d.efc_J + nefc*nv;
+    for (int j = 0; j < nv; j++) {
+      const int bj = m.dof_bodyid[j];
+      const bool in1 = ancestorOrSelf(m, bj, b1), in2 = ancestorOrSelf(m, bj, b2);
+      double cj[6] = {0, 0, 0, 0, 0, 0};
+      if (in1 || in2) {
+        SP<S> cdof = d.cdof + 6*j;
+        // mj_jac rows for this dof (engine_support.c:389-441), zero off the chain
+        double jp1[3] = {0, 0, 0}, jp2[3] = {0, 0, 0}, tmp[3];
+        if (in1) {
+          cross(tmp, cdof, off1);
+          jp1[0] = cdof[3] + tmp[0]; jp1[1] = cdof[4] + tmp[1]; jp1[2] = cdof[5] + tmp[2];
+        }
+        if (in2) {
+          cross(tmp, cdof, off2);
+          jp2[0] = cdof[3] + tmp[0]; jp2[1] = cdof[4] + tmp[1]; jp2[2] = cdof[5] + tmp[2];
+        }
+        double jd[3] = {jp2[0] - jp1[0], jp2[1] - jp1[1], jp2[2] - jp1[2]};
+        for (int r = 0; r < rp; r++) {
+          double acc = 0;
+          for (int k = 0; k < 3; k++) {
+            double f = frame[3*r+k];
+            if (f) acc += jd[k]*f;
+          }
+          cj[r] = acc;
+        }
+        if (dim > 3) {
+          double jr1[3] = {0, 0, 0}, jr2[3] = {0, 0, 0};
+          if (in1) { jr1[0] = cdof[0]; jr1[1] = cdof[1]; jr1[2] = cdof[2]; }
+          if (in2) { jr2[0] = cdof[0]; jr2[1] = cdof[1]; jr2[2] = cdof[2]; }
+          double jdr[3] = {jr2[0] - jr1[0], jr2[1] - jr1[1], jr2[2] - jr1[2]};
+          for (int r = 0; r < dim - 3; r++) {
+            double acc = 0;
+            for (int k = 0; k < 3; k++) {
+              double f = frame[3*r+k];
+              if (f) acc += jdr[k]*f;
+            }
+            cj[3+r] = acc;
+          }
+        }
+      }
+      if (dim == 1) {
+        J[j] = cj[0];
+      } else {
+        for (int k = 1; k < dim; k++) {
+          double f = fri[k-1];
+          J[(2*(k-1))*nv + j] = cj[0] + cj[k]*f;
+          J[(2*(k-1)+1)*nv + j] = cj[0] + cj[k]*(-f);
         }
       }
     }
-    double dist = d.con_dist[i], imargin = d.con_includemargin[i];
-    if (dim == 1) {
-      addConstraint(m, d, cj, &dist, &imargin, 0, 1, CNSTR_CONTACT_FRICTIONLESS, i, status);
-    } else {
-      double cpos[2] = {dist, dist}, cmargin[2] = {imargin, imargin};
-      for (int k = 1; k < dim; k++) {
-        double f = d.con_friction[5*i + k-1];
-        for (int j = 0; j < nv; j++) jacdifp[j] = cj[j] + cj[k*nv+j]*f;
-        for (int j = 0; j < nv; j++) jacdifp[nv+j] = cj[j] + cj[k*nv+j]*(-f);
-        addConstraint(m, d, jacdifp, cpos, cmargin, 0, 2, CNSTR_CONTACT_PYRAMIDAL, i, status);
-      }
+    const int type = dim == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
+    for (int r = 0; r < rows; r++) {
+      d.efc_pos[nefc+r] = d.con_dist[i];
+      d.efc_margin[nefc+r] = d.con_includemargin[i];
+      d.efc_frictionloss[nefc+r] = 0;
+      d.efc_type[nefc+r] = type;
+      d.efc_id[nefc+r] = i;
     }
+    d.efc_count[0] = nefc + rows;
   }
 }
 
