@@ -1810,11 +1810,76 @@ MJH_HD void mulM(const mjhipModel& m, const Lane<S>& d, SP<S> res, SP<S> vec) {
   }
 }
 
-// mj_discreteAcc engine_inverse.c:81-164, Euler branch (the implicit integrators are rejected
-// at context creation): qacc <- M^-1 (M + h*diag(B)) qacc when implicit damping applies
+// dense value of the sparse actuator_moment row `i` at column `col`
+template <int S>
+MJH_HD double momentAt(const mjhipModel& m, const Lane<S>& d, int i, int col) {
+  int adr = m.moment_rowadr[i];
+  for (int k = 0; k < m.moment_rownnz[i]; k++) {
+    if (m.moment_colind[adr+k] == col) return d.actuator_moment[adr+k];
+  }
+  return 0;
+}
+
+// qDeriv(r, c) of mjd_smooth_vel(flg_bias = 0) (engine_derivative.c:1522-1536): actuator
+// velocity terms (mjd_actuator_vel :812-870, addJTBJ :693-724), then dof and tendon damping
+// (mjd_passive_vel :1432-1519), in the reference's order of accumulation
+template <int S>
+MJH_HD double qDerivAt(const mjhipModel& m, const Lane<S>& d, int r, int c) {
+  const int nv = m.nv;
+  double q = 0;
+  if (!(m.opt.disableflags & mjhipDSBL_ACTUATION)) {
+    for (int i = 0; i < m.nu; i++) {
+      double bias_vel = 0, gain_vel = 0;
+      if (m.actuator_biastype[i] == mjhipBIAS_AFFINE) bias_vel = m.actuator_biasprm[10*i+2];
+      if (m.actuator_gaintype[i] == mjhipGAIN_AFFINE) gain_vel = m.actuator_gainprm[10*i+2];
+      if (gain_vel != 0) bias_vel += gain_vel * d.ctrl[i];
+      if (bias_vel != 0) {
+        double mr = momentAt(m, d, i, r);
+        if (mr) q += momentAt(m, d, i, c) * (mr * bias_vel);
+      }
+    }
+  }
+  if (!(m.opt.disableflags & mjhipDSBL_PASSIVE)) {
+    if (r == c) q -= m.dof_damping[r];
+    for (int t = 0; t < m.ntendon; t++) {
+      if (m.tendon_damping[t] > 0) {
+        double B = -m.tendon_damping[t];
+        SP<S> J = d.ten_J + t*nv;
+        if (J[r]) q += J[c] * (J[r] * B);
+      }
+    }
+  }
+  return q;
+}
+
+// mj_discreteAcc engine_inverse.c:81-164 (the implicit integrator is rejected at context
+// creation):
+//   Euler: qacc <- M^-1 (M + h*diag(B)) qacc when implicit damping applies
+//   implicitfast: qacc <- M^-1 (M - h*qDeriv) qacc, qDeriv reduced to qM's sparsity; the
+//   modified M entries are formed on the fly (same values as the reference's in-place qM)
 template <int S>
 MJH_HD void discreteAcc(const mjhipModel& m, const Lane<S>& d) {
   const int nv = m.nv;
+  if (m.opt.integrator == mjhipINT_IMPLICITFAST) {
+    const double h = m.opt.timestep;
+    zero(d.qforce, nv);
+    for (int i = 0; i < nv; i++) {          // mj_mulM with qM + qDeriv*(-h)
+      int adr = m.dof_Madr[i];
+      d.qforce[i] = (d.qM[adr] + qDerivAt(m, d, i, i) * -h)*d.qacc[i];
+      if (m.dof_simplenum[i]) continue;
+      int j = m.dof_parentid[i];
+      while (j >= 0) {
+        adr++;
+        double Mij = d.qM[adr] + qDerivAt(m, d, i, j) * -h;
+        d.qforce[i] += Mij*d.qacc[j];
+        d.qforce[j] += Mij*d.qacc[i];
+        j = m.dof_parentid[j];
+      }
+    }
+    copy(d.qacc, d.qforce, nv);
+    solveM(m, d, d.qacc);
+    return;
+  }
   int dof_damping = 0;
   if (!(m.opt.disableflags & mjhipDSBL_EULERDAMP)) {
     for (int i = 0; i < nv; i++) {

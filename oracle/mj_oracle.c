@@ -1773,11 +1773,72 @@ static void or_mulM(const mjhipModel* m, const mjhipData* d, mjtNum* res, const 
   }
 }
 
-/* engine_inverse.c:81-164 mj_discreteAcc, Euler integrator: qacc <- M^-1 (M + h*B) qacc when
- * implicit damping applies. The implicit integrators need mjd_smooth_vel and RK4 is an
- * error in the reference: both set MJHIP_INST_UNSUPPORTED and leave qacc unchanged. */
+/* dense value of the sparse actuator_moment row `i` at column `col` */
+static mjtNum moment_at(const mjhipModel* m, const mjhipData* d, int i, int col) {
+  int adr = m->moment_rowadr[i];
+  for (int k = 0; k < m->moment_rownnz[i]; k++) {
+    if (m->moment_colind[adr+k] == col) return d->actuator_moment[adr+k];
+  }
+  return 0;
+}
+
+/* qDeriv(r, c) of mjd_smooth_vel(flg_bias = 0) (engine_derivative.c:1522-1536): actuator
+ * velocity terms (mjd_actuator_vel :812-870, addJTBJ :693-724), then dof damping and tendon
+ * damping (mjd_passive_vel :1432-1519), in the reference's order of accumulation. Only the
+ * entries on qM's sparsity are needed (the implicitfast reduction through mapD2M). */
+static mjtNum or_qDeriv(const mjhipModel* m, const mjhipData* d, int r, int c) {
+  int nv = m->nv;
+  mjtNum q = 0;
+  if (!mjDISABLED(mjhipDSBL_ACTUATION)) {
+    for (int i = 0; i < m->nu; i++) {
+      mjtNum bias_vel = 0, gain_vel = 0;
+      if (m->actuator_biastype[i] == mjhipBIAS_AFFINE) bias_vel = m->actuator_biasprm[10*i+2];
+      if (m->actuator_gaintype[i] == mjhipGAIN_AFFINE) gain_vel = m->actuator_gainprm[10*i+2];
+      if (gain_vel != 0) bias_vel += gain_vel * d->ctrl[i];
+      if (bias_vel != 0) {
+        mjtNum mr = moment_at(m, d, i, r);
+        if (mr) q += moment_at(m, d, i, c) * (mr * bias_vel);
+      }
+    }
+  }
+  if (!mjDISABLED(mjhipDSBL_PASSIVE)) {
+    if (r == c) q -= m->dof_damping[r];
+    for (int t = 0; t < m->ntendon; t++) {
+      if (m->tendon_damping[t] > 0) {
+        mjtNum B = -m->tendon_damping[t];
+        const mjtNum* J = d->ten_J + t*nv;
+        if (J[r]) q += J[c] * (J[r] * B);
+      }
+    }
+  }
+  return q;
+}
+
+/* engine_inverse.c:81-164 mj_discreteAcc:
+ *   Euler: qacc <- M^-1 (M + h*diag(B)) qacc when implicit damping applies
+ *   implicitfast: qacc <- M^-1 (M - h*qDeriv) qacc, qDeriv reduced to qM's sparsity
+ * The implicit integrator (mjd_rne_vel, LU) is not implemented and RK4 is an error in the
+ * reference: both set MJHIP_INST_UNSUPPORTED and leave qacc unchanged. */
 static void or_discreteAcc(const mjhipModel* m, mjhipData* d) {
   int nv = m->nv;
+  if (m->opt.integrator == mjhipINT_IMPLICITFAST) {
+    mjtNum* qMsave = (mjtNum*)malloc(m->nM*sizeof(mjtNum));
+    mjtNum* qfrc = (mjtNum*)malloc(nv*sizeof(mjtNum));
+    mju_copy(qMsave, d->qM, m->nM);
+    for (int r = 0; r < nv; r++) {          /* qM += qDerivReduced * -h */
+      int adr = m->dof_Madr[r];
+      for (int c = r; c >= 0; c = m->dof_parentid[c]) {
+        d->qM[adr] = d->qM[adr] + or_qDeriv(m, d, r, c) * -m->opt.timestep;
+        adr++;
+      }
+    }
+    or_mulM(m, d, qfrc, d->qacc);
+    mju_copy(d->qM, qMsave, m->nM);
+    or_solveM(m, d, d->qacc, qfrc, 1);
+    free(qMsave);
+    free(qfrc);
+    return;
+  }
   if (m->opt.integrator != mjhipINT_EULER) {
     d->status |= MJHIP_INST_UNSUPPORTED;
     return;
