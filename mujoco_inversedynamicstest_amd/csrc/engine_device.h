@@ -23,6 +23,21 @@
   #define MJH_HD inline
 #endif
 
+// Phase timing for performance experiments (tools/exp_phases.py builds a separate library
+// with -DMJH_PHASE_TIMING): lane 0 of each wave adds the wall clock at phase mark k, so
+// mean(mark k) - mean(mark k-1) over waves is the mean duration of phase k. Empty otherwise.
+#if defined(MJH_PHASE_TIMING) && defined(__HIPCC__)
+__device__ unsigned long long mjh_phase_acc[32];
+#endif
+#if defined(MJH_PHASE_TIMING) && defined(__HIP_DEVICE_COMPILE__)
+#define MJH_PHASE(k)                                                                  \
+  do {                                                                                \
+    if ((threadIdx.x & 63) == 0) atomicAdd(&mjh_phase_acc[k], wall_clock64());       \
+  } while (0)
+#else
+#define MJH_PHASE(k) do {} while (0)
+#endif
+
 namespace mjh {
 
 constexpr double MINVAL = mjhipMINVAL;
@@ -1735,14 +1750,19 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
 template <int S, bool CONTACT = true>
 MJH_HD void invPosition(const mjhipModel& m, const Lane<S>& d, int* status) {
   kinematics(m, d);
+  MJH_PHASE(1);
   comPos(m, d);
   camlight(m, d);
   tendon(m, d);
+  MJH_PHASE(2);
   crb(m, d);
   factorM(m, d);
+  MJH_PHASE(3);
   if constexpr (CONTACT) collision(m, d, status);
   else d.con_count[0] = 0;
+  MJH_PHASE(4);
   makeConstraint<S, CONTACT>(m, d, status);
+  MJH_PHASE(5);
   transmission(m, d);
 }
 
@@ -1900,19 +1920,23 @@ template <int S, bool CONTACT = true>
 MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
   int status = 0;
   if (skipstage < mjhipSTAGE_POS) invPosition<S, CONTACT>(m, d, &status);
+  MJH_PHASE(6);
   if (skipstage < mjhipSTAGE_VEL) invVelocity(m, d);
+  MJH_PHASE(7);
   const bool discrete = (m.opt.enableflags & mjhipENBL_INVDISCRETE) != 0;
   if (discrete) {
     copy(d.qacc_save, d.qacc, m.nv);
     discreteAcc(m, d);
   }
   invConstraint(m, d);
+  MJH_PHASE(8);
   rne(m, d, 1, d.qfrc_inverse);
   for (int i = 0; i < m.nv; i++) {
     d.qfrc_inverse[i] += m.dof_armature[i] * d.qacc[i]
                          - d.qfrc_passive[i] - d.qfrc_constraint[i];
   }
   if (discrete) copy(d.qacc, d.qacc_save, m.nv);
+  MJH_PHASE(9);
   return status;
 }
 

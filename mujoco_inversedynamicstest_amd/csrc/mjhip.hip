@@ -84,6 +84,7 @@ __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
   if (qacc_in) {
     for (int k = 0; k < m.nv; k++) d.qacc[k] = qacc_in[inst*m.nv + k];
   }
+  MJH_PHASE(0);
   int st = mjh::inverseSkip<64, CONTACT>(m, d, SKIP);
   if (qfrc_out) {
     for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
@@ -341,6 +342,17 @@ static size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 extern "C" {
 
 MJHIP_API const char* mjhip_version(void) { return "mjhip 0.1 (gfx950)"; }
+
+#ifdef MJH_PHASE_TIMING
+// experiment builds only (tools/exp_phases.py): read and clear the phase-mark sums
+extern "C" int mjhip_phaseRead(unsigned long long* out) {
+  hipDeviceSynchronize();
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mjh_phase_acc), 32*sizeof(unsigned long long)))
+    return 1;
+  static const unsigned long long zeros[32] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(mjh_phase_acc), zeros, sizeof(zeros)) != hipSuccess;
+}
+#endif
 
 MJHIP_API const char* mjhip_lastError(void) { return g_last_error.c_str(); }
 
