@@ -33,6 +33,7 @@
   XS(nM)          \
   XS(nC)          \
   XS(nD)          \
+  XS(nB)          \
   XS(nJmom)       \
   XS(nmocap)      \
   XS(ngravcomp)   \
@@ -179,7 +180,14 @@
   X(int,     mapM2C,               nC,        1) \
   X(int,     moment_rownnz,        nu,        1) \
   X(int,     moment_rowadr,        nu,        1) \
-  X(int,     moment_colind,        nJmom,     1)
+  X(int,     moment_colind,        nJmom,     1) \
+  X(int,     B_rownnz,             nbody,     1) \
+  X(int,     B_rowadr,             nbody,     1) \
+  X(int,     B_colind,             nB,        1) \
+  X(int,     D_rownnz,             nv,        1) \
+  X(int,     D_rowadr,             nv,        1) \
+  X(int,     D_colind,             nD,        1) \
+  X(int,     mapM2D,               nD,        1)
 
 #define MJHIP_MODEL_POINTERS \
   MJHIP_MODEL_POINTERS_M      \

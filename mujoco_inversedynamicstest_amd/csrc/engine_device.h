@@ -38,6 +38,11 @@ __device__ unsigned long long mjh_phase_acc[32];
 #define MJH_PHASE(k) do {} while (0)
 #endif
 
+// 1 when mj_discreteAcc runs the implicit integrator (its mjd_rne_vel scratch is allocated)
+MJH_HD int mjh_implicit(const mjhipModel* m) {
+  return (m->opt.enableflags & mjhipENBL_INVDISCRETE) && m->opt.integrator == mjhipINT_IMPLICIT;
+}
+
 namespace mjh {
 
 constexpr double MINVAL = mjhipMINVAL;
@@ -68,6 +73,13 @@ struct SP {
   XSC(jacr, 3*nv)                     \
   XSC(qforce, nv)                     \
   XSC(qacc_save, nv)                  \
+  XSC(qDeriv, mjh_implicit(m)*m->nD)  \
+  XSC(qLU, mjh_implicit(m)*m->nD)     \
+  XSC(Dcvel, mjh_implicit(m)*6*m->nB) \
+  XSC(Dcacc, mjh_implicit(m)*6*m->nB) \
+  XSC(Dcfrc, mjh_implicit(m)*6*m->nB) \
+  XSC(Dcdofdot, mjh_implicit(m)*6*m->nD) \
+  XSC(Dtmp, mjh_implicit(m)*6*nv)     \
   XSC(efc_J, efc_cap*nv)              \
   XSC(efc_pos, efc_cap)               \
   XSC(efc_margin, efc_cap)            \
@@ -1872,14 +1884,199 @@ MJH_HD double qDerivAt(const mjhipModel& m, const Lane<S>& d, int r, int c) {
   return q;
 }
 
-// mj_discreteAcc engine_inverse.c:81-164 (the implicit integrator is rejected at context
-// creation):
+//---------------------------------- engine_derivative.c (implicit integrator) ----------------
+
+// 6x6 Jacobians of the spatial helpers (engine_derivative.c:65-213), row-major, zero
+// elsewhere: crossMotion(vel, v) and crossForce(vel, f) in vel, crossForce in f,
+// mulInertVec in v
+MJH_HD void set36(double D[36], const int (*rc)[2], const double* val, int n) {
+  for (int k = 0; k < 36; k++) D[k] = 0;
+  for (int k = 0; k < n; k++) D[rc[k][0]*6 + rc[k][1]] = val[k];
+}
+MJH_HD void crossMotionVel(double D[36], const double v[6]) {
+  const int rc[18][2] = {{0,2}, {0,1}, {1,2}, {1,0}, {2,1}, {2,0}, {3,2}, {3,1}, {3,5}, {3,4},
+                         {4,2}, {4,0}, {4,5}, {4,3}, {5,1}, {5,0}, {5,4}, {5,3}};
+  const double val[18] = {-v[1], v[2], v[0], -v[2], -v[0], v[1], -v[4], v[5], -v[1], v[2],
+                          v[3], -v[5], v[0], -v[2], -v[3], v[4], -v[0], v[1]};
+  set36(D, rc, val, 18);
+}
+MJH_HD void crossForceVel(double D[36], const double f[6]) {
+  const int rc[18][2] = {{0,2}, {0,1}, {0,5}, {0,4}, {1,2}, {1,0}, {1,5}, {1,3}, {2,1}, {2,0},
+                         {2,4}, {2,3}, {3,2}, {3,1}, {4,2}, {4,0}, {5,1}, {5,0}};
+  const double val[18] = {-f[1], f[2], -f[4], f[5], f[0], -f[2], f[3], -f[5], -f[0], f[1],
+                          -f[3], f[4], -f[4], f[5], f[3], -f[5], -f[3], f[4]};
+  set36(D, rc, val, 18);
+}
+MJH_HD void crossForceFrc(double D[36], const double v[6]) {
+  const int rc[18][2] = {{0,1}, {0,2}, {0,4}, {0,5}, {1,0}, {1,2}, {1,3}, {1,5}, {2,0}, {2,1},
+                         {2,3}, {2,4}, {3,4}, {3,5}, {4,3}, {4,5}, {5,3}, {5,4}};
+  const double val[18] = {-v[2], v[1], -v[5], v[4], v[2], -v[0], v[5], -v[3], -v[1], v[0],
+                          -v[4], v[3], -v[2], v[1], v[2], -v[0], -v[1], v[0]};
+  set36(D, rc, val, 18);
+}
+MJH_HD void mulInertVecVel(double D[36], const double i[10]) {
+  const int rc[24][2] = {{0,0}, {0,1}, {0,2}, {0,4}, {0,5}, {1,0}, {1,1}, {1,2}, {1,3}, {1,5},
+                         {2,0}, {2,1}, {2,2}, {2,3}, {2,4}, {3,1}, {3,2}, {3,3}, {4,2}, {4,0},
+                         {4,4}, {5,0}, {5,1}, {5,5}};
+  const double val[24] = {i[0], i[3], i[4], -i[8], i[7], i[3], i[1], i[5], i[8], -i[6],
+                          i[4], i[5], i[2], -i[7], i[6], i[8], -i[7], i[9], i[6], -i[8],
+                          i[9], i[7], -i[6], i[9]};
+  set36(D, rc, val, 24);
+}
+MJH_HD void transpose6(double r[36], const double a[36]) {
+  for (int i = 0; i < 6; i++) for (int j = 0; j < 6; j++) r[j*6+i] = a[i*6+j];
+}
+
+// res (r1 x 6) = a (r1 x 6) * b (6 x 6), mju_mulMatMat engine_util_blas.c:818-832 (zero
+// entries of `a` skipped)
+template <class R, class A> MJH_HD void mulMat6(R res, A a, const double* b, int r1) {
+  for (int i = 0; i < r1; i++) {
+    double out[6] = {0, 0, 0, 0, 0, 0};
+    for (int k = 0; k < 6; k++) {
+      double t = a[6*i+k];
+      if (t) for (int c = 0; c < 6; c++) out[c] += b[6*k+c]*t;
+    }
+    for (int c = 0; c < 6; c++) res[6*i+c] = out[c];
+  }
+}
+
+// number of dof ancestors of dof j (engine_derivative.c:542)
+MJH_HD int dofJadr(const mjhipModel& m, int j) {
+  return (j < m.nv - 1 ? m.dof_Madr[j+1] : m.nM) - (m.dof_Madr[j] + 1);
+}
+
+// copyFromParent :484-500 (body n's B row begins with its ancestors' dofs, as the parent's)
+template <int S> MJH_HD void bCopyFromParent(const mjhipModel& m, SP<S> mat, int n) {
+  if (n == 0 || m.body_weldid[m.body_parentid[n]] == 0) return;
+  int ndof = 0;
+  for (int p = m.body_weldid[m.body_parentid[n]]; p > 0; p = m.body_weldid[m.body_parentid[p]]) {
+    ndof += m.body_dofnum[p];
+  }
+  copy(mat + 6*m.B_rowadr[n], mat + 6*m.B_rowadr[m.body_parentid[n]], 6*ndof);
+}
+
+// addToParent :505-531 (child columns are a subset of the parent's)
+template <int S> MJH_HD void bAddToParent(const mjhipModel& m, SP<S> mat, int n) {
+  if (n == 0 || m.body_weldid[m.body_parentid[n]] == 0) return;
+  const int np = m.body_parentid[n];
+  const int* cn = m.B_colind + m.B_rowadr[n];
+  const int* cp = m.B_colind + m.B_rowadr[np];
+  for (int i = 0, ip = 0; i < m.B_rownnz[n] && ip < m.B_rownnz[np]; ip++) {
+    if (cn[i] == cp[ip]) {
+      addTo(mat + 6*(m.B_rowadr[np] + ip), mat + 6*(m.B_rowadr[n] + i), 6);
+      i++;
+    }
+  }
+}
+
+// mjd_comVel_vel :535-600: Dcvel (B sparsity) and Dcdofdot (D sparsity), 6 per nonzero
+template <int S> MJH_HD void comVelVel(const mjhipModel& m, const Lane<S>& d) {
+  double mat[36], matT[36], cd[6];
+  for (int i = 1; i < m.nbody; i++) {
+    bCopyFromParent(m, d.Dcvel, i);
+    SP<S> row = d.Dcvel + 6*m.B_rowadr[i];
+    const int last = m.body_dofadr[i] + m.body_dofnum[i];
+    for (int j = m.body_dofadr[i]; j < last; j++) {
+      int Jadr = dofJadr(m, j);
+      const int t = m.jnt_type[m.dof_jntid[j]];
+      int nrot = 1;
+      if (t == mjhipJNT_FREE) {           // translations: Dcdofdot stays zero
+        for (int k = 0; k < 3; k++) addTo(row + 6*(Jadr + k), d.cdof + 6*(j + k), 6);
+        j += 3;
+        Jadr += 3;
+        nrot = 3;
+      } else if (t == mjhipJNT_BALL) {
+        nrot = 3;
+      }
+      for (int k = 0; k < nrot; k++) {
+        for (int c = 0; c < 6; c++) cd[c] = d.cdof[6*(j + k) + c];
+        crossMotionVel(mat, cd);
+        transpose6(matT, mat);
+        mulMat6(d.Dcdofdot + 6*m.D_rowadr[j + k], row, matT, Jadr + k);
+      }
+      for (int k = 0; k < nrot; k++) addTo(row + 6*(Jadr + k), d.cdof + 6*(j + k), 6);
+      j += nrot - 1;
+    }
+  }
+}
+
+// mjd_rne_vel :604-690: qDeriv -= d qfrc_bias / d qvel on the D sparsity
+template <int S> MJH_HD void rneVel(const mjhipModel& m, const Lane<S>& d) {
+  zero(d.Dcvel, 6*m.nB);
+  zero(d.Dcacc, 6*m.nB);
+  zero(d.Dcfrc, 6*m.nB);
+  zero(d.Dcdofdot, 6*m.nD);
+  comVelVel(m, d);
+  double mat[36], mat1[36], mat2[36], dmul[36], tmp[6], in[10], vel[6];
+  for (int i = 1; i < m.nbody; i++) {
+    bCopyFromParent(m, d.Dcacc, i);
+    const int nnz = m.B_rownnz[i];
+    SP<S> acc = d.Dcacc + 6*m.B_rowadr[i];
+    const int last = m.body_dofadr[i] + m.body_dofnum[i];
+    for (int j = m.body_dofadr[i]; j < last; j++) {
+      addTo(acc + 6*dofJadr(m, j), d.cdof_dot + 6*j, 6);
+      addToScl(acc, d.Dcdofdot + 6*m.D_rowadr[j], d.qvel[j], 6*nnz);
+    }
+    for (int k = 0; k < 10; k++) in[k] = d.cinert[10*i+k];
+    for (int k = 0; k < 6; k++) vel[k] = d.cvel[6*i+k];
+    mulInertVecVel(dmul, in);
+    transpose6(mat1, dmul);
+    mulMat6(d.Dcfrc + 6*m.B_rowadr[i], acc, mat1, nnz);
+    mulInertVec(tmp, in, vel);
+    crossForceVel(mat, tmp);
+    crossForceFrc(mat1, vel);
+    for (int r = 0; r < 6; r++) {         // mat2 = mat1 * dmul (mju_mulMatMat)
+      double out[6] = {0, 0, 0, 0, 0, 0};
+      for (int k = 0; k < 6; k++) {
+        double t = mat1[6*r+k];
+        if (t) for (int c = 0; c < 6; c++) out[c] += dmul[6*k+c]*t;
+      }
+      for (int c = 0; c < 6; c++) mat2[6*r+c] = out[c];
+    }
+    for (int k = 0; k < 36; k++) mat[k] += mat2[k];
+    transpose6(mat1, mat);
+    mulMat6(d.Dtmp, d.Dcvel + 6*m.B_rowadr[i], mat1, nnz);
+    addTo(d.Dcfrc + 6*m.B_rowadr[i], d.Dtmp, 6*nnz);
+  }
+  for (int i = m.nbody - 1; i > 0; i--) bAddToParent(m, d.Dcfrc, i);
+  for (int j = 0; j < m.nv; j++) {
+    const int i = m.dof_bodyid[j], nnz = m.B_rownnz[i];
+    SP<S> fr = d.Dcfrc + 6*m.B_rowadr[i];
+    SP<S> q = d.qDeriv + m.D_rowadr[j];
+    for (int k = 0; k < nnz; k++) q[k] -= dot6(fr + 6*k, d.cdof + 6*j);
+  }
+}
+
+// mj_discreteAcc engine_inverse.c:81-164:
 //   Euler: qacc <- M^-1 (M + h*diag(B)) qacc when implicit damping applies
 //   implicitfast: qacc <- M^-1 (M - h*qDeriv) qacc, qDeriv reduced to qM's sparsity; the
 //   modified M entries are formed on the fly (same values as the reference's in-place qM)
+//   implicit: qacc <- M^-1 (M - h*qDeriv) qacc, the full qDeriv (incl. mjd_rne_vel) on the D
+//   sparsity (the reference's qLU before its factorization)
 template <int S>
 MJH_HD void discreteAcc(const mjhipModel& m, const Lane<S>& d) {
   const int nv = m.nv;
+  if (m.opt.integrator == mjhipINT_IMPLICIT) {
+    // mjd_smooth_vel(flg_bias = 1) on the D sparsity; qLU = qM (mapM2D) - h*qDeriv;
+    // qfrc = qLU*qacc (mju_mulMatVecSparse engine_util_sparse.c:156-166)
+    for (int r = 0; r < nv; r++) {
+      const int adr = m.D_rowadr[r];
+      for (int k = 0; k < m.D_rownnz[r]; k++) {
+        d.qDeriv[adr + k] = qDerivAt(m, d, r, m.D_colind[adr + k]);
+      }
+    }
+    rneVel(m, d);
+    for (int i = 0; i < m.nD; i++) {
+      d.qLU[i] = d.qM[m.mapM2D[i]] + d.qDeriv[i] * -m.opt.timestep;
+    }
+    for (int r = 0; r < nv; r++) {
+      const int adr = m.D_rowadr[r];
+      d.qforce[r] = dotSparse(d.qLU + adr, d.qacc, m.D_rownnz[r], m.D_colind + adr);
+    }
+    copy(d.qacc, d.qforce, nv);
+    solveM(m, d, d.qacc);
+    return;
+  }
   if (m.opt.integrator == mjhipINT_IMPLICITFAST) {
     const double h = m.opt.timestep;
     zero(d.qforce, nv);

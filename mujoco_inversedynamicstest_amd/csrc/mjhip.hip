@@ -310,10 +310,8 @@ static const char* unsupported(const mjhipModel* m) {
   }
   if (m->nmocap) return "mocap bodies";
   if (m->na) return "actuator activations";
-  if ((m->opt.enableflags & mjhipENBL_INVDISCRETE) && m->opt.integrator != mjhipINT_EULER &&
-      m->opt.integrator != mjhipINT_IMPLICITFAST) {
-    return "mjENBL_INVDISCRETE with the implicit or RK4 integrator (Euler and implicitfast are "
-           "supported)";
+  if ((m->opt.enableflags & mjhipENBL_INVDISCRETE) && m->opt.integrator == mjhipINT_RK4) {
+    return "mjENBL_INVDISCRETE with the RK4 integrator (an error in the reference)";
   }
   if (m->opt.density > 0 || m->opt.viscosity > 0) return "fluid forces";
   for (int i = 0; i < m->ntendon; i++) {

@@ -1360,6 +1360,59 @@ class MJCFCompiler:
           adr += 1
     if nv and (remaining != 0).any():
       raise MJCFError("unexpected remaining")  # SHOULD NOT OCCUR
+    # D sparse structure (dof x dof, ancestors and descendants) and mapM2D
+    # (engine_io.c:929-1018 with reduced=0, :1135-1232): row i lists every dof on i's chain
+    # to the root and in i's subtree, ascending
+    cols = [[i] for i in range(nv)]
+    for i in range(nv - 1, -1, -1):
+      j = dparent[i]
+      while j >= 0:
+        cols[i].append(j)
+        cols[j].append(i)
+        j = dparent[j]
+    nD = s["nD"]
+    Drownnz = arr("D_rownnz", nv, np.int32)
+    Drowadr = arr("D_rowadr", nv, np.int32)
+    Dcolind = arr("D_colind", nD, np.int32)
+    mapM2D = arr("mapM2D", nD, np.int32, -1)
+    for i in range(nv):
+      Drownnz[i] = len(cols[i])
+      Drowadr[i] = Drowadr[i-1] + Drownnz[i-1] if i else 0
+      Dcolind[Drowadr[i]:Drowadr[i] + Drownnz[i]] = sorted(cols[i])
+    for i in range(nv):                 # qM element (i, j), j on i's chain, at Madr[i] + k
+      adr, j = Madr[i], i
+      while j >= 0:
+        for r, c in ((i, j), (j, i)):
+          row = Dcolind[Drowadr[r]:Drowadr[r] + Drownnz[r]]
+          mapM2D[Drowadr[r] + int(np.searchsorted(row, c))] = adr
+        adr += 1
+        j = dparent[j]
+    if nv and ((mapM2D < 0).any() or Drowadr[-1] + Drownnz[-1] != nD):
+      raise MJCFError("D sparsity mismatch")  # SHOULD NOT OCCUR
+    # B sparse structure (body x dof: ancestor and subtree dofs, ascending),
+    # engine_io.c:1021-1106 makeBSparse
+    bcols = [set() for _ in range(nbody)]
+    for i in range(nbody - 1, 0, -1):
+      bcols[i].update(range(dofadr[i], dofadr[i] + dofnum[i]))
+      bcols[parentid[i]].update(bcols[i])
+    for i in range(nbody):
+      p = parentid[i] if i else -1
+      while p > 0:
+        bcols[i].update(range(dofadr[p], dofadr[p] + dofnum[p]))
+        p = parentid[p]
+    s["nB"] = nB = sum(len(c) for c in bcols)
+    Brownnz = arr("B_rownnz", nbody, np.int32)
+    Browadr = arr("B_rowadr", nbody, np.int32)
+    Bcolind = arr("B_colind", nB, np.int32)
+    for i in range(nbody):
+      Brownnz[i] = len(bcols[i])
+      Browadr[i] = Browadr[i-1] + Brownnz[i-1] if i else 0
+      Bcolind[Browadr[i]:Browadr[i] + Brownnz[i]] = sorted(bcols[i])
+    for j in range(nv):                 # checkDBSparse engine_io.c:1111-1130
+      b = dbody[j]
+      if list(Dcolind[Drowadr[j]:Drowadr[j] + Drownnz[j]]) != \
+         list(Bcolind[Browadr[b]:Browadr[b] + Brownnz[b]]):
+        raise MJCFError("D and B sparsity differ")  # SHOULD NOT OCCUR
     # actuator moment sparse structure for joint transmissions (smooth.c:896-916)
     nJmom = 0
     mrownnz = arr("moment_rownnz", nu, np.int32)

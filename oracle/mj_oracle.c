@@ -1814,11 +1814,183 @@ static mjtNum or_qDeriv(const mjhipModel* m, const mjhipData* d, int r, int c) {
   return q;
 }
 
+/*---------------- mjd_rne_vel: d qfrc_bias / d qvel (the implicit integrator) ---------------*/
+
+/* 6x6 Jacobians of the spatial helpers (engine_derivative.c:65-186). Each lists the nonzero
+ * entries (row, col, value) of the partial derivative of the helper's output in the given
+ * argument; everything else is zero. */
+static void or_set36(mjtNum D[36], const int* rc, const mjtNum* val, int n) {
+  mju_zero(D, 36);
+  for (int k = 0; k < n; k++) D[rc[2*k]*6 + rc[2*k+1]] = val[k];
+}
+
+/* crossMotion(vel, v) w.r.t. vel (:65-99) */
+static void or_crossMotion_vel(mjtNum D[36], const mjtNum v[6]) {
+  static const int rc[] = {0,2, 0,1, 1,2, 1,0, 2,1, 2,0, 3,2, 3,1, 3,5, 3,4,
+                           4,2, 4,0, 4,5, 4,3, 5,1, 5,0, 5,4, 5,3};
+  const mjtNum val[] = {-v[1], v[2], v[0], -v[2], -v[0], v[1], -v[4], v[5], -v[1], v[2],
+                        v[3], -v[5], v[0], -v[2], -v[3], v[4], -v[0], v[1]};
+  or_set36(D, rc, val, 18);
+}
+
+/* crossForce(vel, f) w.r.t. vel (:103-136) */
+static void or_crossForce_vel(mjtNum D[36], const mjtNum f[6]) {
+  static const int rc[] = {0,2, 0,1, 0,5, 0,4, 1,2, 1,0, 1,5, 1,3, 2,1, 2,0, 2,4, 2,3,
+                           3,2, 3,1, 4,2, 4,0, 5,1, 5,0};
+  const mjtNum val[] = {-f[1], f[2], -f[4], f[5], f[0], -f[2], f[3], -f[5], -f[0], f[1],
+                        -f[3], f[4], -f[4], f[5], f[3], -f[5], -f[3], f[4]};
+  or_set36(D, rc, val, 18);
+}
+
+/* crossForce(vel, f) w.r.t. f (:140-173) */
+static void or_crossForce_frc(mjtNum D[36], const mjtNum vel[6]) {
+  static const int rc[] = {0,1, 0,2, 0,4, 0,5, 1,0, 1,2, 1,3, 1,5, 2,0, 2,1, 2,3, 2,4,
+                           3,4, 3,5, 4,3, 4,5, 5,3, 5,4};
+  const mjtNum val[] = {-vel[2], vel[1], -vel[5], vel[4], vel[2], -vel[0], vel[5], -vel[3],
+                        -vel[1], vel[0], -vel[4], vel[3], -vel[2], vel[1], vel[2], -vel[0],
+                        -vel[1], vel[0]};
+  or_set36(D, rc, val, 18);
+}
+
+/* mulInertVec(i, v) w.r.t. v (:178-213) */
+static void or_mulInertVec_vel(mjtNum D[36], const mjtNum i[10]) {
+  static const int rc[] = {0,0, 0,1, 0,2, 0,4, 0,5, 1,0, 1,1, 1,2, 1,3, 1,5, 2,0, 2,1,
+                           2,2, 2,3, 2,4, 3,1, 3,2, 3,3, 4,2, 4,0, 4,4, 5,0, 5,1, 5,5};
+  const mjtNum val[] = {i[0], i[3], i[4], -i[8], i[7], i[3], i[1], i[5], i[8], -i[6],
+                        i[4], i[5], i[2], -i[7], i[6], i[8], -i[7], i[9], i[6], -i[8],
+                        i[9], i[7], -i[6], i[9]};
+  or_set36(D, rc, val, 24);
+}
+
+static void or_transpose6(mjtNum res[36], const mjtNum mat[36]) {
+  for (int r = 0; r < 6; r++) for (int c = 0; c < 6; c++) res[c*6+r] = mat[r*6+c];
+}
+
+/* number of dof ancestors of dof j (engine_derivative.c:542) */
+static int or_Jadr(const mjhipModel* m, int j) {
+  return (j < m->nv - 1 ? m->dof_Madr[j+1] : m->nM) - (m->dof_Madr[j] + 1);
+}
+
+/* :484-500 copyFromParent: body n's B row starts with its ancestors' dofs, as does its
+ * parent's row */
+static void or_copyFromParent(const mjhipModel* m, mjtNum* mat, int n) {
+  if (n == 0 || m->body_weldid[m->body_parentid[n]] == 0) return;
+  int ndof = 0;
+  for (int p = m->body_weldid[m->body_parentid[n]]; p > 0;
+       p = m->body_weldid[m->body_parentid[p]]) {
+    ndof += m->body_dofnum[p];
+  }
+  mju_copy(mat + 6*m->B_rowadr[n], mat + 6*m->B_rowadr[m->body_parentid[n]], 6*ndof);
+}
+
+/* :505-531 addToParent: add body n's row into its parent's at matching columns */
+static void or_addToParent(const mjhipModel* m, mjtNum* mat, int n) {
+  if (n == 0 || m->body_weldid[m->body_parentid[n]] == 0) return;
+  int np = m->body_parentid[n];
+  const int* cn = m->B_colind + m->B_rowadr[n];
+  const int* cp = m->B_colind + m->B_rowadr[np];
+  for (int i = 0, ip = 0; i < m->B_rownnz[n] && ip < m->B_rownnz[np]; ) {
+    if (cn[i] == cp[ip]) {
+      mju_addTo(mat + 6*(m->B_rowadr[np] + ip), mat + 6*(m->B_rowadr[n] + i), 6);
+      i++;
+      ip++;
+    } else {
+      ip++;                             /* child columns are a subset of the parent's */
+    }
+  }
+}
+
+/* :535-600 mjd_comVel_vel: Dcvel (B sparsity) and Dcdofdot (D sparsity), each nonzero a
+ * 6-vector */
+static void or_comVel_vel(const mjhipModel* m, const mjhipData* d, mjtNum* Dcvel,
+                          mjtNum* Dcdofdot) {
+  mjtNum mat[36], matT[36];
+  for (int i = 1; i < m->nbody; i++) {
+    or_copyFromParent(m, Dcvel, i);
+    mjtNum* row = Dcvel + 6*m->B_rowadr[i];
+    int last = m->body_dofadr[i] + m->body_dofnum[i];
+    for (int j = m->body_dofadr[i]; j < last; j++) {
+      int Jadr = or_Jadr(m, j);
+      int t = m->jnt_type[m->dof_jntid[j]];
+      int nrot = 1;                     /* rotational dofs handled below */
+      if (t == mjhipJNT_FREE) {         /* translations: Dcdofdot stays zero */
+        for (int k = 0; k < 3; k++) mju_addTo(row + 6*(Jadr + k), d->cdof + 6*(j + k), 6);
+        j += 3;
+        Jadr += 3;
+        nrot = 3;
+      } else if (t == mjhipJNT_BALL) {
+        nrot = 3;
+      }
+      for (int k = 0; k < nrot; k++) {
+        or_crossMotion_vel(mat, d->cdof + 6*(j + k));
+        or_transpose6(matT, mat);
+        mju_mulMatMat(Dcdofdot + 6*m->D_rowadr[j + k], row, matT, Jadr + k, 6, 6);
+      }
+      for (int k = 0; k < nrot; k++) mju_addTo(row + 6*(Jadr + k), d->cdof + 6*(j + k), 6);
+      j += nrot - 1;
+    }
+  }
+}
+
+/* :604-690 mjd_rne_vel: qDeriv -= d qfrc_bias / d qvel on the D sparsity */
+static void or_rne_vel(const mjhipModel* m, const mjhipData* d, mjtNum* qDeriv) {
+  const int nB = m->nB, nD = m->nD;
+  mjtNum* Dcdofdot = (mjtNum*)calloc(6*(size_t)nD + 1, sizeof(mjtNum));
+  mjtNum* Dcvel = (mjtNum*)calloc(6*(size_t)nB + 1, sizeof(mjtNum));
+  mjtNum* Dcacc = (mjtNum*)calloc(6*(size_t)nB + 1, sizeof(mjtNum));
+  mjtNum* Dcfrc = (mjtNum*)calloc(6*(size_t)nB + 1, sizeof(mjtNum));
+  mjtNum* tmp6 = (mjtNum*)calloc(6*(size_t)m->nv + 1, sizeof(mjtNum));
+  mjtNum mat[36], mat1[36], mat2[36], dmul[36], tmp[6];
+  or_comVel_vel(m, d, Dcvel, Dcdofdot);
+  for (int i = 1; i < m->nbody; i++) {
+    or_copyFromParent(m, Dcacc, i);
+    const int nnz = m->B_rownnz[i];
+    mjtNum* acc = Dcacc + 6*m->B_rowadr[i];
+    int last = m->body_dofadr[i] + m->body_dofnum[i];
+    for (int j = m->body_dofadr[i]; j < last; j++) {
+      mju_addTo(acc + 6*or_Jadr(m, j), d->cdof_dot + 6*j, 6);
+      mju_addToScl(acc, Dcdofdot + 6*m->D_rowadr[j], d->qvel[j], 6*nnz);
+    }
+    /* Dcfrc = (d mulInertVec / d cacc) Dcacc + (d crossForce / d cvel
+     *         + d crossForce / d f * d mulInertVec / d cvel) Dcvel */
+    or_mulInertVec_vel(dmul, d->cinert + 10*i);
+    or_transpose6(mat1, dmul);
+    mju_mulMatMat(Dcfrc + 6*m->B_rowadr[i], acc, mat1, nnz, 6, 6);
+    mju_mulInertVec(tmp, d->cinert + 10*i, d->cvel + 6*i);
+    or_crossForce_vel(mat, tmp);
+    or_crossForce_frc(mat1, d->cvel + 6*i);
+    mju_mulMatMat(mat2, mat1, dmul, 6, 6, 6);
+    mju_addTo(mat, mat2, 36);
+    or_transpose6(mat1, mat);
+    mju_mulMatMat(tmp6, Dcvel + 6*m->B_rowadr[i], mat1, nnz, 6, 6);
+    mju_addTo(Dcfrc + 6*m->B_rowadr[i], tmp6, 6*nnz);
+  }
+  for (int i = m->nbody - 1; i > 0; i--) or_addToParent(m, Dcfrc, i);
+  for (int j = 0; j < m->nv; j++) {
+    int i = m->dof_bodyid[j];
+    mju_mulMatVec(tmp6, Dcfrc + 6*m->B_rowadr[i], d->cdof + 6*j, m->B_rownnz[i], 6);
+    mju_subFrom(qDeriv + m->D_rowadr[j], tmp6, m->B_rownnz[i]);
+  }
+  free(Dcdofdot); free(Dcvel); free(Dcacc); free(Dcfrc); free(tmp6);
+}
+
+/* mjd_smooth_vel (engine_derivative.c:1522-1536) on the D sparsity, for the tests: uses the
+ * position/velocity quantities already in d */
+void or_smoothVel(const mjhipModel* m, const mjhipData* d, mjtNum* qDeriv, int flg_bias) {
+  for (int r = 0; r < m->nv; r++) {
+    for (int k = 0; k < m->D_rownnz[r]; k++) {
+      qDeriv[m->D_rowadr[r] + k] = or_qDeriv(m, d, r, m->D_colind[m->D_rowadr[r] + k]);
+    }
+  }
+  if (flg_bias) or_rne_vel(m, d, qDeriv);
+}
+
 /* engine_inverse.c:81-164 mj_discreteAcc:
  *   Euler: qacc <- M^-1 (M + h*diag(B)) qacc when implicit damping applies
  *   implicitfast: qacc <- M^-1 (M - h*qDeriv) qacc, qDeriv reduced to qM's sparsity
- * The implicit integrator (mjd_rne_vel, LU) is not implemented and RK4 is an error in the
- * reference: both set MJHIP_INST_UNSUPPORTED and leave qacc unchanged. */
+ *   implicit: qacc <- M^-1 (M - h*qDeriv) qacc with the full qDeriv (incl. mjd_rne_vel) on
+ *   the D sparsity (the reference's qLU before factorization)
+ * RK4 is an error in the reference: MJHIP_INST_UNSUPPORTED, qacc unchanged. */
 static void or_discreteAcc(const mjhipModel* m, mjhipData* d) {
   int nv = m->nv;
   if (m->opt.integrator == mjhipINT_IMPLICITFAST) {
@@ -1836,6 +2008,24 @@ static void or_discreteAcc(const mjhipModel* m, mjhipData* d) {
     mju_copy(d->qM, qMsave, m->nM);
     or_solveM(m, d, d->qacc, qfrc, 1);
     free(qMsave);
+    free(qfrc);
+    return;
+  }
+  if (m->opt.integrator == mjhipINT_IMPLICIT) {
+    /* mjd_smooth_vel(flg_bias = 1) on the D sparsity, qLU = qM (via mapM2D) - h*qDeriv,
+     * qfrc = qLU*qacc (mju_mulMatVecSparse, engine_util_sparse.c:156-166) */
+    mjtNum* qDeriv = (mjtNum*)malloc((m->nD + 1)*sizeof(mjtNum));
+    mjtNum* qfrc = (mjtNum*)malloc((nv + 1)*sizeof(mjtNum));
+    or_smoothVel(m, d, qDeriv, 1);
+    for (int i = 0; i < m->nD; i++) {
+      qDeriv[i] = d->qM[m->mapM2D[i]] + qDeriv[i] * -m->opt.timestep;   /* now qLU */
+    }
+    for (int r = 0; r < nv; r++) {
+      qfrc[r] = mju_dotSparse(qDeriv + m->D_rowadr[r], d->qacc, m->D_rownnz[r],
+                              m->D_colind + m->D_rowadr[r]);
+    }
+    or_solveM(m, d, d->qacc, qfrc, 1);
+    free(qDeriv);
     free(qfrc);
     return;
   }

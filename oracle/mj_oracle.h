@@ -67,6 +67,8 @@ enum { orCNSTRSTATE_SATISFIED = 0, orCNSTRSTATE_QUADRATIC, orCNSTRSTATE_LINEARNE
        orCNSTRSTATE_LINEARPOS, orCNSTRSTATE_CONE };
 
 int  or_efcCapacity(const mjhipModel* m);
+/* mjd_smooth_vel on the D sparsity (D_rowadr/D_colind), from the fields already in d */
+void or_smoothVel(const mjhipModel* m, const mjhipData* d, mjtNum* qDeriv, int flg_bias);
 int  or_contactCapacity(const mjhipModel* m);   /* -1: unsupported collision pair */
 
 /* pipeline (engine_inverse.c) */

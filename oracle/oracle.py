@@ -67,6 +67,7 @@ def lib():
     L.or_solveM.argtypes = [M, Dp, _D, _D, ctypes.c_int]
     L.or_rne.argtypes = [M, Dp, ctypes.c_int, _D]
     L.or_fullM.argtypes = [M, _D, _D]
+    L.or_smoothVel.argtypes = [M, Dp, _D, ctypes.c_int]
     L.or_forward.argtypes = [M, Dp, E]
     L.or_forward.restype = ctypes.c_int
     L.or_xfrcAccumulate.argtypes = [M, Dp, _D]
@@ -154,6 +155,17 @@ class Oracle:
     M = self.d.qM if M is None else np.ascontiguousarray(M)
     out = np.zeros((self.m.nv, self.m.nv))
     self.L.or_fullM(ctypes.byref(self.cm), _p(out), _p(M))
+    return out
+
+  def smooth_vel(self, flg_bias=1):
+    """mjd_smooth_vel of the last call's state as a dense nv x nv matrix (D sparsity)."""
+    m = self.m
+    q = np.zeros(max(m.sizes["nD"], 1))
+    self.L.or_smoothVel(ctypes.byref(self.cm), ctypes.byref(self.d.struct), _p(q), flg_bias)
+    out = np.zeros((m.nv, m.nv))
+    for r in range(m.nv):
+      a, n = m.D_rowadr[r], m.D_rownnz[r]
+      out[r, m.D_colind[a:a + n]] = q[a:a + n]
     return out
 
   def contact_field(self, name):

@@ -386,3 +386,24 @@ def test_invdiscrete_implicitfast_parity():
     o.d.ctrl[:] = ctrl[i]
     ref.append(o.inverse(q[i], v[i], a[i]))
   assert_close(f, np.array(ref), "qfrc_inverse (implicitfast INVDISCRETE)")
+
+
+@pytest.mark.parametrize("name", ["humanoid", "inertia"])
+def test_invdiscrete_implicit_parity(name):
+  """INVDISCRETE with the implicit integrator (mjd_rne_vel on the B/D sparsity, qLU product)
+  on the device vs the oracle; the inertia model covers free and ball joints."""
+  m = models.load(name, disable_contact=True)
+  m.opt["enableflags"] |= 1 << 3
+  m.opt["integrator"] = 2
+  B = 512
+  q, v, a = sample_states(m, B, first=400)
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    assert e.fast_kernel is None
+    f, st = e.inverse(q, v, a, status=True)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(e.field("qacc", 0, B), a)       # restored
+  finally:
+    e.close()
+  ref, _ = oracle_batch(m, q, v, a)
+  assert_close(f, ref["qfrc_inverse"], "qfrc_inverse (implicit INVDISCRETE)")
