@@ -18,7 +18,14 @@
 #include "../../include/mjhip_contact.h"
 
 #if defined(__HIPCC__)
-  #define MJH_HD __host__ __device__ inline
+  #define MJH_LAMBDA_INLINE __attribute__((always_inline))
+#else
+  #define MJH_LAMBDA_INLINE
+#endif
+#if defined(__HIPCC__)
+  // always inlined: an out-of-line call would pass the Lane view and the model through
+  // private (scratch) memory and reload every field pointer from there
+  #define MJH_HD __host__ __device__ inline __attribute__((always_inline))
 #else
   #define MJH_HD inline
 #endif
@@ -127,7 +134,23 @@ struct Lane {
 #undef XSI
   int efc_cap;
   int con_cap;
+  // fused constraint path only (nbody <= 64): chain[k] has bit b set when body b is body k
+  // or one of its ancestors (on the device a per-block LDS table, chainMasks)
+  const unsigned long long* chain;
 };
+
+// chain[k] for body k (the fused path's ancestor test, one bit per body)
+MJH_HD unsigned long long chainMask(const mjhipModel& m, int k) {
+  unsigned long long mk = 0;
+  for (int b = k; b > 0; b = m.body_parentid[b]) mk |= 1ull << b;
+  return mk;
+}
+
+// whether mj_inverseSkip(skipstage) can take the fused constraint path
+MJH_HD bool fusedOk(const mjhipModel& m, int skipstage) {
+  return skipstage == mjhipSTAGE_NONE && !(m.opt.enableflags & mjhipENBL_INVDISCRETE) &&
+         m.nbody <= 64;
+}
 
 //---------------------------------- engine_util_blas.c ---------------------------------------
 
@@ -569,6 +592,22 @@ struct RawContact { double dist, pos[3], frame[9]; };
 template <class A, class B> MJH_HD double dot3(A a, B b) { return a[0]*b[0] + a[1]*b[1] + a[2]*b[2]; }
 MJH_HD double clip(double x, double lo, double hi) { return x < lo ? lo : (x > hi ? hi : x); }
 
+// c[k] = t for k = 0 or 1 as value selects on constant indices (a store through a selected
+// pointer would keep c in private memory)
+MJH_HD void putRaw(RawContact* c, int k, const RawContact& t) {
+  const bool z = k == 0;
+  c[0].dist = z ? t.dist : c[0].dist;
+  c[1].dist = z ? c[1].dist : t.dist;
+  for (int j = 0; j < 3; j++) {
+    c[0].pos[j] = z ? t.pos[j] : c[0].pos[j];
+    c[1].pos[j] = z ? c[1].pos[j] : t.pos[j];
+  }
+  for (int j = 0; j < 9; j++) {
+    c[0].frame[j] = z ? t.frame[j] : c[0].frame[j];
+    c[1].frame[j] = z ? c[1].frame[j] : t.frame[j];
+  }
+}
+
 // engine_collision_primitive.c mjraw_PlaneSphere
 template <class P1, class M1, class P2>
 MJH_HD int rawPlaneSphere(RawContact* c, double margin, P1 pos1, M1 mat1, P2 pos2, double r2) {
@@ -592,13 +631,16 @@ MJH_HD int colPlaneCapsule(RawContact* c, double margin, P1 pos1, M1 mat1, P2 po
   double axis[3] = {mat2[2], mat2[5], mat2[8]};
   double seg[3] = {size2[1]*axis[0], size2[1]*axis[1], size2[1]*axis[2]};
   double p[3];
+  RawContact t;
   add3(p, pos2, seg);
-  int n1 = rawPlaneSphere(c, margin, pos1, mat1, p, size2[0]);
+  int n = rawPlaneSphere(&t, margin, pos1, mat1, p, size2[0]);
+  copy3(t.frame + 3, axis);
+  if (n) putRaw(c, 0, t);
   sub3(p, pos2, seg);
-  int n2 = rawPlaneSphere(c + n1, margin, pos1, mat1, p, size2[0]);
-  if (n1) copy3(c->frame + 3, axis);
-  if (n2) copy3((c + n1)->frame + 3, axis);
-  return n1 + n2;
+  int n2 = rawPlaneSphere(&t, margin, pos1, mat1, p, size2[0]);
+  copy3(t.frame + 3, axis);
+  if (n2) putRaw(c, n, t);
+  return n + n2;
 }
 
 // mjraw_SphereSphere
@@ -673,30 +715,33 @@ MJH_HD int colCapsuleCapsule(RawContact* c, double margin, P1 pos1, M1 mat1,
     addTo3(vec2, pos2);
     return rawSphereSphere(c, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
   }
+  // parallel axes: up to four end-point tests, at most two contacts (each appended to the
+  // next free slot of c; the count before an append is 0 or 1)
+  RawContact t;
+  int n = 0;
   add3(vec1, pos1, axis1);
   double x2 = clip((v - mb) / mc, -1, 1);
   scl3(vec2, axis2, x2);
   addTo3(vec2, pos2);
-  int n1 = rawSphereSphere(c, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
+  if (rawSphereSphere(&t, margin, vec1, mat1, size1[0], vec2, mat2, size2[0])) putRaw(c, n++, t);
   sub3(vec1, pos1, axis1);
   x2 = clip((v + mb) / mc, -1, 1);
   scl3(vec2, axis2, x2);
   addTo3(vec2, pos2);
-  int n2 = rawSphereSphere(c + n1, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
-  if (n1 + n2 >= 2) return n1 + n2;
+  if (rawSphereSphere(&t, margin, vec1, mat1, size1[0], vec2, mat2, size2[0])) putRaw(c, n++, t);
+  if (n >= 2) return n;
   add3(vec2, pos2, axis2);
   double x1 = clip((u - mb) / ma, -1, 1);
   scl3(vec1, axis1, x1);
   addTo3(vec1, pos1);
-  int n3 = rawSphereSphere(c + n1 + n2, margin, vec1, mat1, size1[0], vec2, mat2, size2[0]);
-  if (n1 + n2 + n3 >= 2) return n1 + n2 + n3;
+  if (rawSphereSphere(&t, margin, vec1, mat1, size1[0], vec2, mat2, size2[0])) putRaw(c, n++, t);
+  if (n >= 2) return n;
   sub3(vec2, pos2, axis2);
   x1 = clip((u + mb) / ma, -1, 1);
   scl3(vec1, axis1, x1);
   addTo3(vec1, pos1);
-  int n4 = rawSphereSphere(c + n1 + n2 + n3, margin, vec1, mat1, size1[0], vec2, mat2,
-                           size2[0]);
-  return n1 + n2 + n3 + n4;
+  if (rawSphereSphere(&t, margin, vec1, mat1, size1[0], vec2, mat2, size2[0])) putRaw(c, n++, t);
+  return n;
 }
 
 // engine_util_spatial.c mju_makeFrame
@@ -776,7 +821,8 @@ MJH_HD int filterSphere(const mjhipModel& m, const Lane<S>& d, int g1, int g2, d
 
 // mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
 template <int S>
-MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, int* status) {
+MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, int& ncon,
+                         int* status) {
   if (m.geom_type[g1] > m.geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   if (mjhip_pairMaxContacts(t1, t2) <= 0) return;
@@ -808,16 +854,17 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
   int condim;
   double gap, solref[2], solimp[5], friction[5];
   contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
-  for (int k = 0; k < num; k++) {
-    int i = d.con_count[0];
+  // one raw contact into the contact list (mj_setContact); false when the list is full
+  auto store = [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
+    int i = ncon;
     if (i >= d.con_cap) {              // mjWARN_CONTACTFULL analogue (capacity is exact)
       *status |= MJHIP_INST_CNSTRFULL;
-      return;
+      return false;
     }
     double frame[9];
-    for (int j = 0; j < 9; j++) frame[j] = raw[k].frame[j];
-    d.con_dist[i] = raw[k].dist;
-    copy3(d.con_pos + 3*i, raw[k].pos);
+    for (int j = 0; j < 9; j++) frame[j] = rk.frame[j];
+    d.con_dist[i] = rk.dist;
+    copy3(d.con_pos + 3*i, rk.pos);
     d.con_geom[2*i] = g1;
     d.con_geom[2*i+1] = g2;
     d.con_dim[i] = condim;
@@ -830,14 +877,16 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
       double f = ovr ? m.opt.o_friction[j] : friction[j];
       d.con_friction[5*i+j] = f > 1e-5 ? f : 1e-5;      // mjMINMU
     }
-    d.con_exclude[i] = raw[k].dist >= includemargin;
+    d.con_exclude[i] = rk.dist >= includemargin;
     makeFrame(frame);
     for (int j = 0; j < 9; j++) d.con_frame[9*i+j] = frame[j];
     d.con_efc_address[i] = -1;
     d.con_mu[i] = 0;
-    d.con_count[0] = i + 1;
-  }
-}
+    ncon = i + 1;
+    return true;
+  };
+  if (store(raw[0]) && num > 1) store(raw[1]);   // num <= 2; constant indices keep raw[]
+}                                                // in registers
 
 // contactcompare (engine_collision_driver.c:223-257) on two contacts' geom ids
 template <int S>
@@ -866,26 +915,28 @@ MJH_HD void swapContacts(const Lane<S>& d, int a, int b) {
 // sorted by contactcompare, as mj_collideTree's callers do
 template <int S>
 MJH_HD void collision(const mjhipModel& m, const Lane<S>& d, int* status) {
+  int ncon = 0;                        // in a register; written once at the end
   d.con_count[0] = 0;
   if (!mjhip_contactsEnabled(&m)) return;
   for (int b1 = 0; b1 < m.nbody; b1++) {
     for (int b2 = b1 + 1; b2 < m.nbody; b2++) {
       if (!mjhip_bodyPairCandidate(&m, b1, b2)) continue;
       int n1 = m.body_geomnum[b1], n2 = m.body_geomnum[b2];
-      int before = d.con_count[0];
+      int before = ncon;
       for (int i = 0; i < n1; i++) {
         for (int j = 0; j < n2; j++) {
-          collideGeoms(m, d, m.body_geomadr[b1] + i, m.body_geomadr[b2] + j, status);
+          collideGeoms(m, d, m.body_geomadr[b1] + i, m.body_geomadr[b2] + j, ncon, status);
         }
       }
       if (!(m.opt.disableflags & mjhipDSBL_MIDPHASE) && !(n1 == 1 && n2 == 1)) {
-        int n = d.con_count[0];
+        int n = ncon;
         for (int a = before + 1; a < n; a++) {
           for (int b = a; b > before && contactLess(m, d, b, b - 1); b--) swapContacts(d, b, b - 1);
         }
       }
     }
   }
+  d.con_count[0] = ncon;
 }
 
 // mj_applyFT :1194-1251 (dense)
@@ -1356,23 +1407,27 @@ MJH_HD void passive(const mjhipModel& m, const Lane<S>& d) {
 
 //---------------------------------- engine_core_constraint.c ---------------------------------
 
+// row counters of mj_makeConstraint (nefc, friction rows, limit rows; no equality rows in
+// the subset), kept in registers and written to efc_count once at the end
+struct RowCount { int nefc = 0, nf = 0, nl = 0; };
+
 // mj_addConstraint :265-356 (dense): `size` rows of jac (strided scratch), contact rows are
-// never dropped as empty
+// never dropped as empty. Returns whether the rows were added.
 template <int S>
-MJH_HD void addConstraint(const mjhipModel& m, const Lane<S>& d, SP<S> jac, const double* pos,
-                          const double* margin, double frictionloss, int size, int type, int id,
-                          int* status) {
+MJH_HD bool addConstraint(const mjhipModel& m, const Lane<S>& d, RowCount& rc, SP<S> jac,
+                          const double* pos, const double* margin, double frictionloss,
+                          int size, int type, int id, int* status) {
   int nv = m.nv;
-  int nefc = d.efc_count[0];
+  int nefc = rc.nefc;
   int empty = !(type == CNSTR_CONTACT_FRICTIONLESS || type == CNSTR_CONTACT_PYRAMIDAL ||
                 type == CNSTR_CONTACT_ELLIPTIC);
   for (int i = 0; empty && i < size*nv; i++) {
     if (jac[i]) empty = 0;
   }
-  if (empty) return;
+  if (empty) return false;
   if (nefc + size > d.efc_cap) {   // mjWARN_CNSTRFULL analogue: capacity exceeded
     *status |= MJHIP_INST_CNSTRFULL;
-    return;
+    return false;
   }
   copy(d.efc_J + nefc*nv, jac, size*nv);
   for (int i = 0; i < size; i++) {
@@ -1382,18 +1437,20 @@ MJH_HD void addConstraint(const mjhipModel& m, const Lane<S>& d, SP<S> jac, cons
     d.efc_type[nefc+i] = type;
     d.efc_id[nefc+i] = id;
   }
-  d.efc_count[0] = nefc + size;
+  rc.nefc = nefc + size;
   if (type == CNSTR_FRICTION_DOF || type == CNSTR_FRICTION_TENDON) {
-    d.efc_count[2] = d.efc_count[2] + size;
+    rc.nf += size;
   } else if (type == CNSTR_LIMIT_JOINT || type == CNSTR_LIMIT_TENDON) {
-    d.efc_count[3] = d.efc_count[3] + size;
+    rc.nl += size;
   }
+  return true;
 }
 
 template <int S>
-MJH_HD void addConstraint1(const mjhipModel& m, const Lane<S>& d, SP<S> jacrow, double pos,
-                           double margin, double frictionloss, int type, int id, int* status) {
-  addConstraint(m, d, jacrow, &pos, &margin, frictionloss, 1, type, id, status);
+MJH_HD bool addConstraint1(const mjhipModel& m, const Lane<S>& d, RowCount& rc, SP<S> jacrow,
+                           double pos, double margin, double frictionloss, int type, int id,
+                           int* status) {
+  return addConstraint(m, d, rc, jacrow, &pos, &margin, frictionloss, 1, type, id, status);
 }
 
 // mj_instantiateContact :964-1131 (dense; pyramidal or frictionless; elliptic cones are
@@ -1408,14 +1465,15 @@ MJH_HD bool ancestorOrSelf(const mjhipModel& m, int a, int b) {
 }
 
 template <int S>
-MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, int* status) {
+MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& rc,
+                               int* status) {
   int nv = m.nv, ncon = d.con_count[0];
   if ((m.opt.disableflags & mjhipDSBL_CONTACT) || ncon == 0 || nv == 0) return;
   for (int i = 0; i < ncon; i++) {
     if (d.con_exclude[i]) continue;
     const int dim = d.con_dim[i];
     const int rows = dim == 1 ? 1 : 2*(dim - 1);
-    const int nefc = d.efc_count[0];
+    const int nefc = rc.nefc;
     d.con_efc_address[i] = nefc;
     if (nefc + rows > d.efc_cap) {   // mjWARN_CNSTRFULL analogue (capacity is exact)
       *status |= MJHIP_INST_CNSTRFULL;
@@ -1488,7 +1546,7 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, int* statu
       d.efc_type[nefc+r] = type;
       d.efc_id[nefc+r] = i;
     }
-    d.efc_count[0] = nefc + rows;
+    rc.nefc = nefc + rows;
   }
 }
 
@@ -1537,19 +1595,355 @@ MJH_HD void getimpedance(const double* solimp, double pos, double margin, double
 // :824-959 (dense), mj_diagApprox :1138-1311 and mj_makeImpedance :1494-1608 (dim-1 rows)
 // CONTACT = false compiles the contact code out (models whose contact capacity is 0); the
 // contact path's private arrays would otherwise cost every launch a scratch segment
-template <int S, bool CONTACT = true>
+// getsolparam :1316-1371, the model-side source of a non-contact row's solref/solimp
+MJH_HD void rowSolParam(const mjhipModel& m, int tp, int id, double solref[2],
+                        double solimp[5]) {
+  const double* sr = tp == CNSTR_LIMIT_JOINT ? m.jnt_solref + 2*id :
+                     (tp == CNSTR_FRICTION_DOF ? m.dof_solref + 2*id :
+                      m.tendon_solref_lim + 2*id);
+  const double* si = tp == CNSTR_LIMIT_JOINT ? m.jnt_solimp + 5*id :
+                     (tp == CNSTR_FRICTION_DOF ? m.dof_solimp + 5*id :
+                      m.tendon_solimp_lim + 5*id);
+  solref[0] = sr[0]; solref[1] = sr[1];
+  for (int k = 0; k < 5; k++) solimp[k] = si[k];
+}
+
+// getsolparam's safety clamps (:1340-1371), then mj_makeImpedance's per-row constants
+// (:1494-1560): kbip = (K, B, imp, impP) of a row of type tp at pos/margin
+MJH_HD void rowImpedance(const mjhipModel& m, int tp, double* solref, double* solimp,
+                         double pos, double margin, double kbip[4]) {
+  if ((solref[0] > 0) ^ (solref[1] > 0)) {
+    solref[0] = 0.02;
+    solref[1] = 1;
+  }
+  if (!(m.opt.disableflags & mjhipDSBL_REFSAFE) && solref[0] > 0) {
+    solref[0] = dmax(solref[0], 2*m.opt.timestep);
+  }
+  solimp[0] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[0]));
+  solimp[1] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[1]));
+  solimp[2] = dmax(0, solimp[2]);
+  solimp[3] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[3]));
+  solimp[4] = dmax(1, solimp[4]);
+  double imp, impP;
+  getimpedance(solimp, pos, margin, &imp, &impP);
+  double K, Bc;
+  if (tp == CNSTR_FRICTION_DOF || tp == CNSTR_FRICTION_TENDON) {
+    K = 0;
+  } else if (solref[0] > 0) {
+    K = 1 / dmax(MINVAL, solimp[1]*solimp[1] * solref[0]*solref[0] * solref[1]*solref[1]);
+  } else {
+    K = -solref[0] / dmax(MINVAL, solimp[1]*solimp[1]);
+  }
+  if (solref[1] > 0) {
+    Bc = 2 / dmax(MINVAL, solimp[1]*solref[0]);
+  } else {
+    Bc = -solref[1] / dmax(MINVAL, solimp[1]);
+  }
+  kbip[0] = K;
+  kbip[1] = Bc;
+  kbip[2] = imp;
+  kbip[3] = impP;
+}
+
+//---------------------------------- fused constraint rows -----------------------------------
+// With skipstage = NONE and no INVDISCRETE, the velocity- and acceleration-stage outputs of a
+// row depend only on the row and the inputs qvel, qacc. The fused path therefore finishes
+// every row when it is created, in registers: efc_vel and J*qacc in mju_dot's order of
+// summation (engine_util_blas.c:680-741), efc_aref (mj_referenceConstraint :2362-2375), force
+// and state (mj_constraintUpdate_island :2387-2549 as in invConstraint), and KBIP, R, D and
+// diagApprox (mj_diagApprox, mj_makeImpedance). No pass reads back what another pass wrote:
+// on the device every such read-back costs a memory round trip per row.
+// qfrc_constraint = J'force is one column-blocked pass at the end (constraintForce).
+
+// the remaining outputs of row r from its impedance constants, R and its two dot products
+template <int S>
+MJH_HD void finishRowFused(const Lane<S>& d, int r, int tp, const double kb[4], double R,
+                           double pos, double margin, double frictionloss, double vel,
+                           double acc) {
+  for (int k = 0; k < 4; k++) d.efc_KBIP[4*r+k] = kb[k];
+  const double D = 1 / R;
+  d.efc_R[r] = R;
+  d.efc_D[r] = D;
+  d.efc_diagApprox[r] = R * kb[2] / (1-kb[2]);
+  d.efc_vel[r] = vel;
+  const double aref = -kb[1]*vel - kb[0]*kb[2]*(pos-margin);
+  d.efc_aref[r] = aref;
+  const double jar = acc - aref;
+  d.jar[r] = jar;
+  double force = -D * jar;
+  int state = CNSTRSTATE_QUADRATIC;
+  if (tp == CNSTR_FRICTION_DOF || tp == CNSTR_FRICTION_TENDON) {
+    const double Rf = R * frictionloss;
+    if (jar <= -Rf) {
+      force = frictionloss;
+      state = CNSTRSTATE_LINEARNEG;
+    } else if (jar >= Rf) {
+      force = -frictionloss;
+      state = CNSTRSTATE_LINEARPOS;
+    }
+  } else if (jar >= 0) {
+    force = 0;
+    state = CNSTRSTATE_SATISFIED;
+  }
+  d.efc_force[r] = force;
+  d.efc_state[r] = state;
+}
+
+// a friction or limit row just added at r (few per instance: its J row is read back)
+template <int S>
+MJH_HD void finishNonContact(const mjhipModel& m, const Lane<S>& d, int r, int tp, int id,
+                             double pos, double margin, double frictionloss) {
+  const double diag = tp == CNSTR_FRICTION_DOF ? m.dof_invweight0[id] :
+                      (tp == CNSTR_LIMIT_JOINT ? m.dof_invweight0[m.jnt_dofadr[id]] :
+                       m.tendon_invweight0[id]);
+  double solref[2], solimp[5], kb[4];
+  rowSolParam(m, tp, id, solref, solimp);
+  rowImpedance(m, tp, solref, solimp, pos, margin, kb);
+  const double R = dmax(MINVAL, (1-kb[2])*diag/kb[2]);
+  SP<S> J = d.efc_J + r*m.nv;
+  finishRowFused(d, r, tp, kb, R, pos, margin, frictionloss, dot(J, d.qvel, m.nv),
+                 dot(J, d.qacc, m.nv));
+}
+
+// One contact's rows (condim DIM) at efc row `nefc`. As instantiateContact, the rows are
+// formed dof by dof straight into efc_J, here in blocks of four dofs whose loads (cdof,
+// qvel, qacc) are issued together. The chain test is a bit test of chain masks. For DIM <= 3
+// J*qvel and J*qacc accumulate in registers in mju_dot's four partial sums; wider contacts
+// read their rows back. All rows of a contact share K, B, imp, impP and R (mj_makeImpedance:
+// one impedance per contact; pyramidal R is 2 mu^2 R0 for every row, :1562-1598).
+template <int S, int DIM>
+MJH_HD void contactRowsFused(const mjhipModel& m, const Lane<S>& d, int i, int nefc) {
+  constexpr int ROWS = DIM == 1 ? 1 : 2*(DIM - 1);
+  constexpr bool REG = DIM <= 3;
+  constexpr int NA = REG ? ROWS : 1;
+  const int nv = m.nv;
+  const int tp = DIM == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
+  const int b1 = m.geom_bodyid[d.con_geom[2*i]], b2 = m.geom_bodyid[d.con_geom[2*i+1]];
+  double pos[3], frame[9], fri[5], solref[2], solimp[5];
+  for (int k = 0; k < 3; k++) pos[k] = d.con_pos[3*i+k];
+  for (int k = 0; k < 9; k++) frame[k] = d.con_frame[9*i+k];
+  for (int k = 0; k < 5; k++) fri[k] = d.con_friction[5*i+k];
+  for (int k = 0; k < 2; k++) solref[k] = d.con_solref[2*i+k];
+  for (int k = 0; k < 5; k++) solimp[k] = d.con_solimp[5*i+k];
+  const double dist = d.con_dist[i], incl = d.con_includemargin[i];
+  double off1[3], off2[3];
+  sub3(off1, pos, d.subtree_com + 3*m.body_rootid[b1]);
+  sub3(off2, pos, d.subtree_com + 3*m.body_rootid[b2]);
+  const unsigned long long mask1 = d.chain[b1], mask2 = d.chain[b2];
+
+  // impedance and R (mj_diagApprox :1138-1311 with mj_makeImpedance)
+  double kb[4];
+  rowImpedance(m, tp, solref, solimp, dist, incl, kb);
+  double tran = 0, rot = 0;
+  tran += m.body_invweight0[2*b1] * 1.0;
+  rot += m.body_invweight0[2*b1+1] * 1.0;
+  tran += m.body_invweight0[2*b2] * 1.0;
+  rot += m.body_invweight0[2*b2+1] * 1.0;
+  (void)rot;
+  double R;
+  if constexpr (DIM == 1) {
+    R = dmax(MINVAL, (1-kb[2])*tran/kb[2]);
+  } else {
+    const double v0 = tran + fri[0]*fri[0]*tran;
+    const double R0 = dmax(MINVAL, (1-kb[2])*v0/kb[2]);
+    const double R1 = R0/dmax(MINVAL, m.opt.impratio);
+    const double mu = fri[0] * sqrt(R1/R0);
+    d.con_mu[i] = mu;
+    R = 2*mu*mu*R0;
+  }
+
+  // rows, dof by dof, in blocks of four
+  SP<S> J = d.efc_J + nefc*nv;
+  double av[NA][4], aa[NA][4], tv[NA], ta[NA];
+  for (int r = 0; r < NA; r++) {
+    for (int k = 0; k < 4; k++) av[r][k] = aa[r][k] = 0;
+    tv[r] = ta[r] = 0;
+  }
+  const int nb4 = (nv / 4) * 4;
+  constexpr int BLK = REG ? 4 : 1;   // wide contacts (rare) go one dof at a time
+  for (int jb = 0; jb < nv; jb += BLK) {
+    const bool full = jb + 4 <= nv;
+    double cd[BLK][6], qv[BLK], qa[BLK];
+#pragma unroll
+    for (int k = 0; k < BLK; k++) {
+      const int j = jb + k;
+      if (j < nv) {
+        for (int c = 0; c < 6; c++) cd[k][c] = d.cdof[6*j+c];
+        if constexpr (REG) {
+          qv[k] = d.qvel[j];
+          qa[k] = d.qacc[j];
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < BLK; k++) {
+      const int j = jb + k;
+      if (j >= nv) break;
+      const int bj = m.dof_bodyid[j];
+      const bool in1 = (mask1 >> bj) & 1, in2 = (mask2 >> bj) & 1;
+      // mj_jac rows for this dof (engine_support.c:389-441), zero off the chain
+      double t1[3], t2[3], jd[3], cj[6] = {0, 0, 0, 0, 0, 0};
+      cross(t1, cd[k], off1);
+      cross(t2, cd[k], off2);
+      for (int c = 0; c < 3; c++) {
+        const double p1 = in1 ? cd[k][3+c] + t1[c] : 0.0;
+        const double p2 = in2 ? cd[k][3+c] + t2[c] : 0.0;
+        jd[c] = p2 - p1;
+      }
+      const int rp = DIM > 1 ? 3 : 1;
+      for (int r = 0; r < rp; r++) {
+        double acc = 0;
+        for (int c = 0; c < 3; c++) {
+          const double f = frame[3*r+c];
+          if (f) acc += jd[c]*f;
+        }
+        cj[r] = acc;
+      }
+      if constexpr (DIM > 3) {
+        double jdr[3];
+        for (int c = 0; c < 3; c++) jdr[c] = (in2 ? cd[k][c] : 0.0) - (in1 ? cd[k][c] : 0.0);
+        for (int r = 0; r < DIM - 3; r++) {
+          double acc = 0;
+          for (int c = 0; c < 3; c++) {
+            const double f = frame[3*r+c];
+            if (f) acc += jdr[c]*f;
+          }
+          cj[3+r] = acc;
+        }
+      }
+      double Jv[ROWS];
+      if constexpr (DIM == 1) {
+        Jv[0] = cj[0];
+      } else {
+        for (int c = 1; c < DIM; c++) {
+          const double f = fri[c-1];
+          Jv[2*(c-1)] = cj[0] + cj[c]*f;
+          Jv[2*(c-1)+1] = cj[0] + cj[c]*(-f);
+        }
+      }
+      for (int r = 0; r < ROWS; r++) J[r*nv + j] = Jv[r];
+      if constexpr (REG) {
+        for (int r = 0; r < ROWS; r++) {
+          const double pv = Jv[r]*qv[k], pa = Jv[r]*qa[k];
+          if (full) {
+            av[r][k] += pv;
+            aa[r][k] += pa;
+          } else {
+            tv[r] = j == nb4 ? pv : tv[r] + pv;
+            ta[r] = j == nb4 ? pa : ta[r] + pa;
+          }
+        }
+      }
+    }
+  }
+  for (int r = 0; r < ROWS; r++) {
+    double vel, acc;
+    if constexpr (REG) {
+      vel = (av[r][0] + av[r][2]) + (av[r][1] + av[r][3]);
+      acc = (aa[r][0] + aa[r][2]) + (aa[r][1] + aa[r][3]);
+      if (nv > nb4) {
+        vel += tv[r];
+        acc += ta[r];
+      }
+    } else {
+      vel = dot(J + r*nv, d.qvel, nv);
+      acc = dot(J + r*nv, d.qacc, nv);
+    }
+    const int row = nefc + r;
+    d.efc_pos[row] = dist;
+    d.efc_margin[row] = incl;
+    d.efc_frictionloss[row] = 0;
+    d.efc_type[row] = tp;
+    d.efc_id[row] = i;
+    finishRowFused(d, row, tp, kb, R, dist, incl, 0, vel, acc);
+  }
+}
+
+// mj_instantiateContact :964-1131 on the fused path (pyramidal or frictionless)
+template <int S>
+MJH_HD void instantiateContactFused(const mjhipModel& m, const Lane<S>& d, RowCount& rc,
+                                    int* status) {
+  const int ncon = d.con_count[0];
+  if ((m.opt.disableflags & mjhipDSBL_CONTACT) || ncon == 0 || m.nv == 0) return;
+  for (int i = 0; i < ncon; i++) {
+    if (d.con_exclude[i]) continue;
+    const int dim = d.con_dim[i];
+    const int rows = dim == 1 ? 1 : 2*(dim - 1);
+    d.con_efc_address[i] = rc.nefc;
+    if (rc.nefc + rows > d.efc_cap) {   // mjWARN_CNSTRFULL analogue (capacity is exact)
+      *status |= MJHIP_INST_CNSTRFULL;
+      continue;
+    }
+    switch (dim) {
+      case 1: contactRowsFused<S, 1>(m, d, i, rc.nefc); break;
+      case 3: contactRowsFused<S, 3>(m, d, i, rc.nefc); break;
+      case 4: contactRowsFused<S, 4>(m, d, i, rc.nefc); break;
+      default: contactRowsFused<S, 6>(m, d, i, rc.nefc); break;
+    }
+    rc.nefc += rows;
+  }
+}
+
+// qfrc_constraint = J'force (mju_mulMatTVec engine_util_blas.c:756-766: rows in order, zero
+// forces skipped) in blocks of 8 columns x 4 rows: 36 independent loads per step
+template <int S>
+MJH_HD void constraintForce(const mjhipModel& m, const Lane<S>& d, int nefc) {
+  const int nv = m.nv;
+  for (int c0 = 0; c0 < nv; c0 += 8) {
+    double acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int r = 0;
+    for (; r + 4 <= nefc; r += 4) {
+      double f[4], Jv[4][8];
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        f[k] = d.efc_force[r+k];
+        for (int c = 0; c < 8; c++) Jv[k][c] = c0 + c < nv ? d.efc_J[(r+k)*nv + c0 + c] : 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < 4; k++) {
+        if (f[k]) {
+          for (int c = 0; c < 8; c++) acc[c] += Jv[k][c]*f[k];
+        }
+      }
+    }
+    for (; r < nefc; r++) {
+      const double f = d.efc_force[r];
+      if (f) {
+        for (int c = 0; c < 8; c++) {
+          if (c0 + c < nv) acc[c] += d.efc_J[r*nv + c0 + c]*f;
+        }
+      }
+    }
+    for (int c = 0; c < 8; c++) {
+      if (c0 + c < nv) d.qfrc_constraint[c0 + c] = acc[c];
+    }
+  }
+}
+
+template <int S, bool CONTACT = true, bool FUSED = false>
 MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   int nv = m.nv;
-  d.efc_count[0] = 0; d.efc_count[1] = 0; d.efc_count[2] = 0; d.efc_count[3] = 0;
+  RowCount rc;
   int dsbl = m.opt.disableflags;
-  if (dsbl & mjhipDSBL_CONSTRAINT) return;
+  if (dsbl & mjhipDSBL_CONSTRAINT) {
+    d.efc_count[0] = 0; d.efc_count[1] = 0; d.efc_count[2] = 0; d.efc_count[3] = 0;
+    if constexpr (FUSED) zero(d.qfrc_constraint, nv);
+    return;
+  }
+  // a just-added non-contact row, finished at once on the fused path
+  auto added = [&](bool ok, int tp, int id, double pos, double margin, double frictionloss) {
+    if constexpr (FUSED) {
+      if (ok) finishNonContact(m, d, rc.nefc - 1, tp, id, pos, margin, frictionloss);
+    }
+  };
   SP<S> jacrow = d.jacp;       // one dense row of scratch
   if (!(dsbl & mjhipDSBL_FRICTIONLOSS)) {
     for (int i = 0; i < nv; i++) {
       if (m.dof_frictionloss[i] > 0) {
         zero(jacrow, nv);
         jacrow[i] = 1;
-        addConstraint1(m, d, jacrow, 0, 0, m.dof_frictionloss[i], CNSTR_FRICTION_DOF, i, status);
+        added(addConstraint1(m, d, rc, jacrow, 0, 0, m.dof_frictionloss[i], CNSTR_FRICTION_DOF,
+                             i, status), CNSTR_FRICTION_DOF, i, 0, 0, m.dof_frictionloss[i]);
       }
     }
   }
@@ -1565,7 +1959,8 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
           if (dist < margin) {
             zero(jacrow, nv);
             jacrow[m.jnt_dofadr[i]] = -(double)side;
-            addConstraint1(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status);
+            added(addConstraint1(m, d, rc, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status),
+                  CNSTR_LIMIT_JOINT, i, dist, margin, 0);
           }
         }
       } else if (t == mjhipJNT_BALL) {
@@ -1579,7 +1974,8 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
         if (dist < margin) {
           zero(jacrow, nv);
           scl3(jacrow + m.jnt_dofadr[i], angleAxis, -1);
-          addConstraint1(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status);
+          added(addConstraint1(m, d, rc, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status),
+                CNSTR_LIMIT_JOINT, i, dist, margin, 0);
         }
       }
     }
@@ -1591,13 +1987,22 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
         double dist = side * (m.tendon_range[2*i+(side+1)/2] - value);
         if (dist < margin) {
           scl(jacrow, d.ten_J + i*nv, -side, nv);
-          addConstraint1(m, d, jacrow, dist, margin, 0, CNSTR_LIMIT_TENDON, i, status);
+          added(addConstraint1(m, d, rc, jacrow, dist, margin, 0, CNSTR_LIMIT_TENDON, i, status),
+                CNSTR_LIMIT_TENDON, i, dist, margin, 0);
         }
       }
     }
   }
-  if constexpr (CONTACT) instantiateContact(m, d, status);
-  int nefc = d.efc_count[0];
+  if constexpr (CONTACT) {
+    if constexpr (FUSED) instantiateContactFused(m, d, rc, status);
+    else instantiateContact(m, d, rc, status);
+  }
+  d.efc_count[0] = rc.nefc; d.efc_count[1] = 0; d.efc_count[2] = rc.nf; d.efc_count[3] = rc.nl;
+  const int nefc = rc.nefc;
+  if constexpr (FUSED) {
+    constraintForce(m, d, nefc);
+    return;
+  }
   // mj_diagApprox :1138-1311
   for (int i = 0; i < nefc; i++) {
     int id = d.efc_id[i];
@@ -1633,61 +2038,25 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   for (int i = 0; i < nefc; i++) {
     int id = d.efc_id[i];
     int tp = d.efc_type[i];
-    // getsolparam :1316-1371
     double solref[2], solimp[5];
     if (CONTACT && (tp == CNSTR_CONTACT_FRICTIONLESS || tp == CNSTR_CONTACT_PYRAMIDAL)) {
       for (int k = 0; k < 2; k++) solref[k] = d.con_solref[2*id+k];
       for (int k = 0; k < 5; k++) solimp[k] = d.con_solimp[5*id+k];
     } else {
-      const double* sr = tp == CNSTR_LIMIT_JOINT ? m.jnt_solref + 2*id :
-                         (tp == CNSTR_FRICTION_DOF ? m.dof_solref + 2*id :
-                          m.tendon_solref_lim + 2*id);
-      const double* si = tp == CNSTR_LIMIT_JOINT ? m.jnt_solimp + 5*id :
-                         (tp == CNSTR_FRICTION_DOF ? m.dof_solimp + 5*id :
-                          m.tendon_solimp_lim + 5*id);
-      solref[0] = sr[0]; solref[1] = sr[1];
-      for (int k = 0; k < 5; k++) solimp[k] = si[k];
+      rowSolParam(m, tp, id, solref, solimp);
     }
-    if ((solref[0] > 0) ^ (solref[1] > 0)) {
-      solref[0] = 0.02;
-      solref[1] = 1;
-    }
-    if (!(dsbl & mjhipDSBL_REFSAFE) && solref[0] > 0) {
-      solref[0] = dmax(solref[0], 2*m.opt.timestep);
-    }
-    solimp[0] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[0]));
-    solimp[1] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[1]));
-    solimp[2] = dmax(0, solimp[2]);
-    solimp[3] = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[3]));
-    solimp[4] = dmax(1, solimp[4]);
     int dim = (CONTACT && tp == CNSTR_CONTACT_PYRAMIDAL) ? 2*(d.con_dim[id]-1) : 1;
-    double imp, impP;
-    getimpedance(solimp, d.efc_pos[i], d.efc_margin[i], &imp, &impP);
-    double K, Bc;
-    if (tp == CNSTR_FRICTION_DOF || tp == CNSTR_FRICTION_TENDON) {
-      K = 0;
-    } else if (solref[0] > 0) {
-      K = 1 / dmax(MINVAL, solimp[1]*solimp[1] * solref[0]*solref[0] * solref[1]*solref[1]);
-    } else {
-      K = -solref[0] / dmax(MINVAL, solimp[1]*solimp[1]);
-    }
-    if (solref[1] > 0) {
-      Bc = 2 / dmax(MINVAL, solimp[1]*solref[0]);
-    } else {
-      Bc = -solref[1] / dmax(MINVAL, solimp[1]);
-    }
+    double kb[4];
+    rowImpedance(m, tp, solref, solimp, d.efc_pos[i], d.efc_margin[i], kb);
     for (int j = 0; j < dim; j++) {
       int r = i + j;
-      d.efc_R[r] = dmax(MINVAL, (1-imp)*d.efc_diagApprox[r]/imp);
-      d.efc_KBIP[4*r] = K;
-      d.efc_KBIP[4*r+1] = Bc;
-      d.efc_KBIP[4*r+2] = imp;
-      d.efc_KBIP[4*r+3] = impP;
+      d.efc_R[r] = dmax(MINVAL, (1-kb[2])*d.efc_diagApprox[r]/kb[2]);
+      for (int k = 0; k < 4; k++) d.efc_KBIP[4*r+k] = kb[k];
     }
     i += dim - 1;
   }
   // frictional contacts: R in the friction directions, contact mu (:1562-1598)
-  for (int i = d.efc_count[1] + d.efc_count[2]; CONTACT && i < nefc; i++) {
+  for (int i = rc.nf; CONTACT && i < nefc; i++) {
     if (d.efc_type[i] == CNSTR_CONTACT_PYRAMIDAL) {
       int id = d.efc_id[i], dim = d.con_dim[id];
       d.efc_R[i+1] = d.efc_R[i]/dmax(MINVAL, m.opt.impratio);
@@ -1759,7 +2128,7 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
 //---------------------------------- engine_inverse.c -----------------------------------------
 
 // mj_invPosition :37-68 (mj_flex: no flexes)
-template <int S, bool CONTACT = true>
+template <int S, bool CONTACT = true, bool FUSED = false>
 MJH_HD void invPosition(const mjhipModel& m, const Lane<S>& d, int* status) {
   kinematics(m, d);
   MJH_PHASE(1);
@@ -1773,13 +2142,13 @@ MJH_HD void invPosition(const mjhipModel& m, const Lane<S>& d, int* status) {
   if constexpr (CONTACT) collision(m, d, status);
   else d.con_count[0] = 0;
   MJH_PHASE(4);
-  makeConstraint<S, CONTACT>(m, d, status);
+  makeConstraint<S, CONTACT, FUSED>(m, d, status);
   MJH_PHASE(5);
   transmission(m, d);
 }
 
 // mj_invVelocity :73-76 -> mj_fwdVelocity engine_forward.c:193-231
-template <int S>
+template <int S, bool FUSED = false>
 MJH_HD void invVelocity(const mjhipModel& m, const Lane<S>& d) {
   int nv = m.nv;
   for (int r = 0; r < m.ntendon; r++) d.ten_velocity[r] = dot(d.ten_J + r*nv, d.qvel, nv);
@@ -1792,7 +2161,7 @@ MJH_HD void invVelocity(const mjhipModel& m, const Lane<S>& d) {
   }
   comVel(m, d);
   passive(m, d);
-  referenceConstraint(m, d);
+  if constexpr (!FUSED) referenceConstraint(m, d);   // fused: done with the rows
   rne(m, d, 0, d.qfrc_bias);
 }
 
@@ -2113,19 +2482,21 @@ MJH_HD void discreteAcc(const mjhipModel& m, const Lane<S>& d) {
   solveM(m, d, d.qacc);
 }
 
-template <int S, bool CONTACT = true>
+// FUSED (the constraint rows finished at creation, see contactRowsFused) requires
+// skipstage = mjSTAGE_NONE, no mjENBL_INVDISCRETE, nbody <= 64 and d.chain set (fusedOk)
+template <int S, bool CONTACT = true, bool FUSED = false>
 MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
   int status = 0;
-  if (skipstage < mjhipSTAGE_POS) invPosition<S, CONTACT>(m, d, &status);
+  if (skipstage < mjhipSTAGE_POS) invPosition<S, CONTACT, FUSED>(m, d, &status);
   MJH_PHASE(6);
-  if (skipstage < mjhipSTAGE_VEL) invVelocity(m, d);
+  if (skipstage < mjhipSTAGE_VEL) invVelocity<S, FUSED>(m, d);
   MJH_PHASE(7);
-  const bool discrete = (m.opt.enableflags & mjhipENBL_INVDISCRETE) != 0;
+  const bool discrete = !FUSED && (m.opt.enableflags & mjhipENBL_INVDISCRETE) != 0;
   if (discrete) {
     copy(d.qacc_save, d.qacc, m.nv);
     discreteAcc(m, d);
   }
-  invConstraint(m, d);
+  if constexpr (!FUSED) invConstraint(m, d);
   MJH_PHASE(8);
   rne(m, d, 1, d.qfrc_inverse);
   for (int i = 0; i < m.nv; i++) {

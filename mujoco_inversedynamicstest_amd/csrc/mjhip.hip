@@ -44,17 +44,27 @@ static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr}};
 
 // generic pipeline over the instances of a work-list (limit-active instances of the fast
 // path); grid = ceil(B/64) blocks, threads past *count exit at once
-template <bool CONTACT>
+// the fused constraint path's chain masks, one per body, shared by the block (LDS)
+#define MJHIP_CHAIN_TABLE(FUSED)                                                         \
+  __shared__ unsigned long long chain[64];                                                \
+  if (FUSED) {                                                                            \
+    if ((int)threadIdx.x < m.nbody) chain[threadIdx.x] = mjh::chainMask(m, threadIdx.x);  \
+    __syncthreads();                                                                      \
+  }
+
+template <bool CONTACT, bool FUSED>
 __global__ __launch_bounds__(64) void k_inverse_list(mjhipModel m, Mirror mr,
                                                      const int* __restrict__ worklist,
                                                      const int* __restrict__ count,
                                                      double* __restrict__ qfrc_out,
                                                      int* __restrict__ status) {
+  MJHIP_CHAIN_TABLE(FUSED)
   const long g = (long)blockIdx.x*64 + threadIdx.x;
   if (g >= *count) return;
   const long inst = worklist[g];
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
-  int st = mjh::inverseSkip<64, CONTACT>(m, d, mjhipSTAGE_NONE);
+  d.chain = chain;
+  int st = mjh::inverseSkip<64, CONTACT, FUSED>(m, d, mjhipSTAGE_NONE);
   if (qfrc_out) {
     for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
   }
@@ -64,17 +74,19 @@ __global__ __launch_bounds__(64) void k_inverse_list(mjhipModel m, Mirror mr,
 
 // Fused mj_inverseSkip over a batch. Optional row-major (instance-major) inputs are copied
 // into the mirror first; optional row-major qfrc_inverse output is written at the end.
-template <int SKIP, bool CONTACT>
+template <int SKIP, bool CONTACT, bool FUSED>
 __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
                                                 const double* __restrict__ qpos_in,
                                                 const double* __restrict__ qvel_in,
                                                 const double* __restrict__ qacc_in,
                                                 double* __restrict__ qfrc_out,
                                                 int* __restrict__ status) {
+  MJHIP_CHAIN_TABLE(FUSED)
   const int blk = blockIdx.x, lane = threadIdx.x;
   const long inst = (long)blk*64 + lane;
   if (inst >= B) return;
   Lane<64> d = lane_view(mr, blk, lane);
+  d.chain = chain;
   if (qpos_in) {
     for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos_in[inst*m.nq + k];
   }
@@ -85,7 +97,7 @@ __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
     for (int k = 0; k < m.nv; k++) d.qacc[k] = qacc_in[inst*m.nv + k];
   }
   MJH_PHASE(0);
-  int st = mjh::inverseSkip<64, CONTACT>(m, d, SKIP);
+  int st = mjh::inverseSkip<64, CONTACT, FUSED>(m, d, SKIP);
   if (qfrc_out) {
     for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
   }
@@ -570,29 +582,38 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     c->fast->launch(grid, block, c->stream, c->mirror, B, qpos, qvel, qacc, qfrc, status,
                     c->worklist + 2, cnt, nxt, c->mirror.efc_count);
     HIPCHECK(hipGetLastError());
+    // the fast path excludes INVDISCRETE: the list is fused whenever nbody allows
+    const bool fused = mjh::fusedOk(c->dmodel, mjhipSTAGE_NONE);
+#define MJHIP_LAUNCH_LIST(C, F)                                                              \
+    hipLaunchKernelGGL((k_inverse_list<C, F>), grid, block, 0, c->stream, c->dmodel,          \
+                       c->mirror, (const int*)(c->worklist + 2), (const int*)cnt, qfrc, status)
     if (c->con_cap > 0) {
-      hipLaunchKernelGGL(k_inverse_list<true>, grid, block, 0, c->stream, c->dmodel, c->mirror,
-                         (const int*)(c->worklist + 2), (const int*)cnt, qfrc, status);
+      if (fused) MJHIP_LAUNCH_LIST(true, true); else MJHIP_LAUNCH_LIST(true, false);
     } else {
-      hipLaunchKernelGGL(k_inverse_list<false>, grid, block, 0, c->stream, c->dmodel,
-                         c->mirror, (const int*)(c->worklist + 2), (const int*)cnt, qfrc, status);
+      if (fused) MJHIP_LAUNCH_LIST(false, true); else MJHIP_LAUNCH_LIST(false, false);
     }
+#undef MJHIP_LAUNCH_LIST
     HIPCHECK(hipGetLastError());
     c->wl_last = c->wl_parity;
     c->wl_parity ^= 1;
     return MJHIP_OK;
   }
+#define MJHIP_LAUNCH_K(SK, C, F)                                                              \
+  hipLaunchKernelGGL((k_inverse<SK, C, F>), grid, block, 0, c->stream, c->dmodel, c->mirror,   \
+                     B, qpos, qvel, qacc, qfrc, status)
 #define MJHIP_LAUNCH_GENERIC(SK)                                                              \
   if (c->con_cap > 0) {                                                                       \
-    hipLaunchKernelGGL((k_inverse<SK, true>), grid, block, 0, c->stream, c->dmodel, c->mirror, \
-                       B, qpos, qvel, qacc, qfrc, status);                                    \
+    MJHIP_LAUNCH_K(SK, true, false);                                                          \
   } else {                                                                                    \
-    hipLaunchKernelGGL((k_inverse<SK, false>), grid, block, 0, c->stream, c->dmodel,           \
-                       c->mirror, B, qpos, qvel, qacc, qfrc, status);                         \
+    MJHIP_LAUNCH_K(SK, false, false);                                                         \
   }
   switch (skipstage) {
   case mjhipSTAGE_NONE:
-    MJHIP_LAUNCH_GENERIC(0)
+    if (mjh::fusedOk(c->dmodel, mjhipSTAGE_NONE)) {
+      if (c->con_cap > 0) MJHIP_LAUNCH_K(0, true, true); else MJHIP_LAUNCH_K(0, false, true);
+    } else {
+      MJHIP_LAUNCH_GENERIC(0)
+    }
     break;
   case mjhipSTAGE_POS:
     MJHIP_LAUNCH_GENERIC(1)
@@ -605,6 +626,7 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     return MJHIP_ERR_ARG;
   }
 #undef MJHIP_LAUNCH_GENERIC
+#undef MJHIP_LAUNCH_K
   HIPCHECK(hipGetLastError());
   return MJHIP_OK;
 }

@@ -44,10 +44,13 @@ extern "C" int kh_field(const mjhipModel* m, int efc_cap, int con_cap, const cha
 static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int* iscratch,
                          int efc_cap, int con_cap);
 
+// classic = 1 forces the unfused constraint path; otherwise the path follows the GPU
+// dispatch (fused when mjh::fusedOk)
 extern "C" int kh_inverse(const mjhipModel* m, mjhipData* d, double* scratch, int* iscratch,
-                          int efc_cap, int con_cap, int skipstage) {
+                          int efc_cap, int con_cap, int skipstage, int classic) {
   mjh::Lane<1> L = bind(m, d, scratch, iscratch, efc_cap, con_cap);
-  int st = mjh::inverseSkip(*m, L, skipstage);
+  int st = (!classic && mjh::fusedOk(*m, skipstage)) ?
+      mjh::inverseSkip<1, true, true>(*m, L, skipstage) : mjh::inverseSkip(*m, L, skipstage);
   d->nefc = L.efc_count[0];
   return st;
 }
@@ -79,5 +82,8 @@ static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int
 #undef XSI
   L.efc_cap = efc_cap;
   L.con_cap = con_cap;
+  static unsigned long long chain[64];
+  for (int k = 0; k < m->nbody && k < 64; k++) chain[k] = mjh::chainMask(*m, k);
+  L.chain = chain;
   return L;
 }

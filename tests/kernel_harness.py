@@ -36,7 +36,8 @@ def lib():
                              ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     L.kh_inverse.restype = ctypes.c_int
     L.kh_inverse.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int]
+                             ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                             ctypes.c_int]
     _lib = L
   return _lib
 
@@ -60,7 +61,8 @@ class KernelCPU:
     self.scratch = np.zeros(nd.value)
     self.iscratch = np.zeros(ni.value, dtype=np.int32)
 
-  def inverse(self, qpos=None, qvel=None, qacc=None, skipstage=0):
+  def inverse(self, qpos=None, qvel=None, qacc=None, skipstage=0, classic=False):
+    """classic=True forces the unfused constraint path (the default follows the GPU)."""
     if qpos is not None:
       self.d.qpos[:] = qpos
     if qvel is not None:
@@ -69,7 +71,7 @@ class KernelCPU:
       self.d.qacc[:] = qacc
     st = lib().kh_inverse(ctypes.byref(self.cm), ctypes.byref(self.d.struct),
                           self.scratch.ctypes.data, self.iscratch.ctypes.data, self.efc_cap,
-                          self.con_cap, skipstage)
+                          self.con_cap, skipstage, int(classic))
     return self.d.qfrc_inverse.copy(), st
 
   def forward(self, qpos, qvel):

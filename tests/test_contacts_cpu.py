@@ -214,3 +214,45 @@ def test_device_code_bitexact_with_contacts():
       ref = o.efc_field(name)
       np.testing.assert_array_equal(k.field(name)[:ref.size], ref, err_msg=f"{name} inst {i}")
   assert seen > 30
+
+
+_MIXED = """<mujoco><worldbody><geom type="plane" size="3 3 .1" condim="1"/>
+  <body pos="0 0 .1"><freejoint/><geom size=".11" condim="1"/></body>
+  <body pos=".6 0 .1"><freejoint/><geom type="capsule" fromto="-.1 0 0 .1 0 0" size=".105"
+    condim="4"/></body>
+  <body pos="1.2 0 .1"><freejoint/><geom size=".105" condim="6"/></body>
+  <body pos="-.6 0 .5"><joint type="hinge" axis="0 1 0" range="-.1 .1" limited="true"
+      frictionloss=".3"/>
+    <geom type="capsule" fromto="0 0 0 0 0 -.45" size=".06" condim="3"/></body>
+</worldbody></mujoco>"""
+
+
+def test_fused_equals_classic_and_oracle():
+  """The fused constraint path (rows finished at creation) against the classic passes and
+  the oracle: condim 1, 3, 4 and 6 contacts, a friction-loss row and joint limits."""
+  m = mjcf.load_xml_string(_MIXED)
+  o, kf, kc = Oracle(m), KernelCPU(m), KernelCPU(m)
+  rng = np.random.default_rng(3)
+  dims = set()
+  for t in range(40):
+    q = m.qpos0.copy()
+    for b in range(3):                       # free bodies: height and small tilt
+      q[7*b + 2] = 0.1 + rng.uniform(-0.03, 0.03)
+      q[7*b + 3:7*b + 7] = [1, *rng.normal(scale=0.1, size=3)]
+      q[7*b + 3:7*b + 7] /= np.linalg.norm(q[7*b + 3:7*b + 7])
+    q[21] = rng.uniform(-0.3, 0.3)          # hinge across its limits
+    v, a = rng.normal(size=m.nv), rng.normal(size=m.nv)
+    f_o = o.inverse(q, v, a)
+    f_f, _ = kf.inverse(q, v, a)
+    f_c, _ = kc.inverse(q, v, a, classic=True)
+    np.testing.assert_array_equal(f_f, f_o)
+    np.testing.assert_array_equal(f_c, f_o)
+    nefc = o.efc.nefc
+    for name in EFC_FIELDS:
+      ref = o.efc_field(name)
+      np.testing.assert_array_equal(kf.field(name)[:ref.size], ref, err_msg=f"{name} {t}")
+      np.testing.assert_array_equal(kc.field(name)[:ref.size], ref, err_msg=f"{name} {t}")
+    np.testing.assert_array_equal(kf.field("con_mu")[:o.efc.ncon], o.contact_field("con_mu"))
+    dims.update(int(x) for x in o.contact_field("con_dim"))
+    assert kf.field("efc_count")[0] == nefc
+  assert dims == {1, 3, 4, 6}
