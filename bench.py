@@ -162,7 +162,7 @@ def main():
                      "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": bytes_per_eval * count,
                      "kernel": ("+".join(f"k_{st}_{eng.fast_kernel}" for st in codegen.STAGES)
-                                + "+k_inverse_list" if eng.fast_kernel else "k_inverse<0>"),
+                                + "+k_constraint" if eng.fast_kernel else "k_inverse<0>"),
                      "kernel_ms": kernel_ms, "generic_kernel_ms": generic_ms,
                      "bytes_per_eval": bytes_per_eval},
         "cpu_baseline": cpu,
@@ -198,7 +198,9 @@ def other_config(args):
     nefc = eng.field_int("efc_count", 0, B)[:, 0]
     rec = {"metric": "mj_inverse evals/sec, config 4 (contacts on)", "value": B / dt,
            "unit": "evals/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": dt * 1e3,
-           "dtype": "f64", "kernel": "k_inverse<0, contacts> (generic)",
+           "dtype": "f64",
+           "kernel": (f"generated k_pos/k_fac/k_va_{eng.fast_kernel} + k_constraint"
+                      if eng.fast_kernel else "k_inverse<0, contacts> (generic)"),
            "config": {"workload": f"{args.model} keyframe poses + noise, contacts on",
                       "batch": B},
            "ncon_hist": np.bincount(ncon).tolist(), "nefc_max": int(nefc.max()),

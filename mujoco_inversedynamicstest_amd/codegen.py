@@ -25,11 +25,15 @@ that traversal is exactly the descending body order of the reference's backward 
 (subtree_com, crb, cfrc accumulation), so every sum is formed in the reference's order while
 only the current root-to-body path is live.
 
-Constraint rows (joint/tendon limits) are detected per instance with the predicates of
-mj_instantiateLimit (engine_core_constraint.c:824-959). An instance with any active limit is
-appended to a device work-list. It is marked in efc_count[0] (-1) so the later stages skip it,
-and it is recomputed by the generic kernel. Results stay exact for every state; the
-straight-line path covers nefc = 0.
+Constraint rows are left to the generic constraint kernel (k_constraint, mjhip.hip:
+collision, mj_makeConstraint and its velocity/acceleration-stage parts, final assembly),
+which reads the constraint-free stages from the mirror. constraint_mode(m) says which
+instances it serves: 'list' -- joint/tendon limits only; k_pos evaluates the predicates of
+mj_instantiateLimit (engine_core_constraint.c:824-959) and appends limit-active instances to
+a device work-list, marked in efc_count[0] (-1); 'all' -- contacts or always-active friction
+loss, every instance; 'none' -- no rows possible. For a served instance k_va stores the raw
+mj_rne(flg_acc = 1) result as qfrc_inverse, so the assembly rne + ((armature*qacc - passive)
+- constraint) happens once, in the reference's order, in k_constraint.
 
 Reference functions restated (engine_core_smooth.c unless noted): mj_kinematics :38-178,
 mj_comPos :183-270, mj_camlight :275-392, mj_tendon :651-723 (fixed), mj_transmission
@@ -90,20 +94,31 @@ def fast_path_supported(m) -> str | None:
   """Return why the model cannot use the straight-line kernels, or None."""
   if m.opt["jacobian"] == 1 or (m.opt["jacobian"] == 2 and m.nv >= 60):
     return "sparse Jacobians"
-  if np.any(m.dof_frictionloss > 0) and not (m.opt["disableflags"] & (1 << 2) or
-                                            m.opt["disableflags"] & 1):
-    return "dof friction loss (always-active constraint rows)"
   if m.opt["enableflags"] & (1 << 3):
     return "INVDISCRETE"
   if m.nmocap or m.na:
     return "mocap/activations"
   if m.opt["density"] > 0 or m.opt["viscosity"] > 0:
     return "fluid"
-  dsbl = int(m.opt["disableflags"])
-  if not (dsbl & 1) and not (dsbl & (1 << 4)) and m.nbody >= 2 and \
-     np.any((m.geom_contype != 0) | (m.geom_conaffinity != 0)):
-    return "contacts (collision runs on the generic kernel)"
   return None
+
+
+def constraint_mode(m) -> str:
+  """Which instances the constraint kernel serves: 'all', 'list' or 'none' (module doc)."""
+  dsbl = int(m.opt["disableflags"])
+  if dsbl & 1:                                             # mjDSBL_CONSTRAINT
+    return "none"
+  contacts = not (dsbl & (1 << 4)) and m.nbody >= 2 and \
+      bool(np.any((m.geom_contype != 0) | (m.geom_conaffinity != 0)))
+  friction = bool(np.any(m.dof_frictionloss > 0)) and not (dsbl & (1 << 2))
+  if contacts or friction:
+    return "all"
+  limits = not (dsbl & (1 << 3)) and (bool(np.any(m.jnt_limited)) or
+                                      bool(np.any(m.tendon_limited[:m.ntendon])))
+  return "list" if limits else "none"
+
+
+CONSTRAINT_MODES = {"none": 0, "list": 1, "all": 2}
 
 
 class _Model:
@@ -121,6 +136,7 @@ class _Model:
       self.children[b].sort(reverse=True)
     self.mass = [float(x) for x in m.body_mass]
     self.dsbl = int(m.opt["disableflags"])
+    self.cmode = constraint_mode(m)
     self.bdofadr = [int(x) for x in m.body_dofadr]
     self.bdofnum = [int(x) for x in m.body_dofnum]
     self.djnt = [int(x) for x in m.dof_jntid]
@@ -192,13 +208,11 @@ class _Stage:
       if n:
         self.E(f"double* __restrict__ P_{nm} = mr.{nm} + ((long)blk*{n})*64 + lane;")
 
-  def prologue(self, check_flag=True):
+  def prologue(self):
     E = self.E
     E("const long inst = (long)blk*64 + lane;")
     E("if (inst >= B) return;")
     E("int* __restrict__ ec = efc_count + (long)blk*4*64 + lane;")
-    if check_flag:
-      E("if (ec[0] != 0) return;   // limit-active: the work-list (generic kernel) owns it")
 
   def load(self, arr, field, n, off=0):
     self.E(f"double {arr}[{max(n, 1)}];")
@@ -372,7 +386,7 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
   nq, nv, dsbl = M.nq, M.nv, M.dsbl
   # the next call's work-list counter (two alternate; stream order makes this safe)
   E("if (worklist_next && blk == 0 && lane == 0) *worklist_next = 0;")
-  G.prologue(check_flag=False)
+  G.prologue()
   G.pointers([f.name for f in fields.DATA_FIELDS if f.stage <= 1])
   E(f"double qpos[{max(nq, 1)}];")
   E("if (qpos_in) {")
@@ -387,7 +401,7 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
   # limits predicate: mj_instantiateLimit (engine_core_constraint.c:824-959)
   E("// ---- constraint detection (mj_instantiateLimit predicates)")
   E("bool active = false;")
-  limits_on = not (dsbl & 1) and not (dsbl & (1 << 3))
+  limits_on = M.cmode == "list"
   if limits_on:
     for j in range(M.njnt):
       if not m.jnt_limited[j]:
@@ -420,13 +434,14 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
           mg = lit(m.tendon_margin[t])
           E(f"active |= (-1.0*({lit(lo)} - ten_length[{t}]) < {mg}) | "
             f"(1.0*({lit(hi)} - ten_length[{t}]) < {mg});")
-  E("if (active) {")
-  E("  int slot = MJH_ATOMIC_ADD(worklist_count, 1);")
-  E("  worklist[slot] = (int)inst;")
-  E("  ec[0] = -1;")
-  E("  return;")
-  E("}")
-  E("ec[0] = 0;")
+  if M.cmode == "list":
+    E("if (active) {   // k_constraint's work-list; the stages below still run")
+    E("  int slot = MJH_ATOMIC_ADD(worklist_count, 1);")
+    E("  worklist[slot] = (int)inst;")
+    E("}")
+    E("ec[0] = active ? -1 : 0;")
+  else:
+    E("(void)active;")
 
   # tendons and transmission depend on qpos only
   if m.ntendon:
@@ -753,6 +768,8 @@ def _gen_va(M: _Model, store_fields=None) -> str:
   E, m = G.E, M.m
   nv, nq, dsbl = M.nv, M.nq, M.dsbl
   G.prologue()
+  if M.cmode == "list":   # k_pos's work-list flag: k_constraint assembles this instance
+    E("const bool cflag = ec[0] != 0;")
   G.pointers(["qpos", "qvel", "qacc", "cinert", "cdof", "xipos", "subtree_com", "ten_length",
               "ten_velocity", "actuator_velocity", "cvel", "cdof_dot", "qfrc_spring",
               "qfrc_damper", "qfrc_gravcomp", "qfrc_fluid", "qfrc_passive", "qfrc_bias",
@@ -855,8 +872,9 @@ def _gen_va(M: _Model, store_fields=None) -> str:
   E(f"double qacc[{nv}];")
   # row-major qfrc_inverse copy, or (no output array) a harmless second write of the mirror
   # slot: a select instead of a branch keeps the pass one scheduling region
-  E(f"double* qo = qfrc_out ? qfrc_out + inst*{nv} : P_qfrc_inverse;")
-  E(f"const long qo_stride = qfrc_out ? 1 : 64;")
+  if M.cmode != "all":
+    E(f"double* qo = qfrc_out ? qfrc_out + inst*{nv} : P_qfrc_inverse;")
+    E(f"const long qo_stride = qfrc_out ? 1 : 64;")
 
   def pre(i):
     if not i:
@@ -931,10 +949,17 @@ def _gen_va(M: _Model, store_fields=None) -> str:
       G.st("qfrc_bias", k, f"mjh::dot6(cdofp_{k}, cfrc_{i})")
       E.open()
       E(f"double qfi = mjh::dot6(cdofp_{k}, frca_{i});")
-      E(f"qfi += {lit(m.dof_armature[k])} * qacc[{k}] - qfp_{k} - 0.0;")
-      G.st("qfrc_constraint", k, "0.0")
-      G.st("qfrc_inverse", k, "qfi")
-      E(f"qo[{k}*qo_stride] = qfi;")
+      if M.cmode == "all":     # raw rne: k_constraint assembles every instance
+        G.st("qfrc_inverse", k, "qfi")
+      else:
+        E(f"const double qfa = qfi + ({lit(m.dof_armature[k])} * qacc[{k}] - qfp_{k} - 0.0);")
+        if M.cmode == "list":
+          E("qfi = cflag ? qfi : qfa;")
+        else:
+          E("qfi = qfa;")
+        G.st("qfrc_constraint", k, "0.0")
+        G.st("qfrc_inverse", k, "qfi")
+        E(f"qo[{k}*qo_stride] = qfi;")
       E.close()
     if M.parent[i]:
       E(f"mjh::addTo(cfrc_{M.parent[i]}, cfrc_{i}, 6);")
@@ -956,7 +981,10 @@ def _gen_va(M: _Model, store_fields=None) -> str:
     return decls, ld
 
   _prefetched_dfs(G, loads, pre, post, PREFETCH)
-  E("ec[0] = 0; ec[64] = 0; ec[128] = 0; ec[192] = 0;")
+  if M.cmode == "none":
+    E("ec[0] = 0; ec[64] = 0; ec[128] = 0; ec[192] = 0;")
+  elif M.cmode == "list":   # served instances get their counts from k_constraint
+    E("if (!cflag) { ec[0] = 0; ec[64] = 0; ec[128] = 0; ec[192] = 0; }")
   E("if (status) status[inst] = 0;")
   return E.text()
 
@@ -1077,8 +1105,9 @@ def generate_registry(entries) -> str:
   reg = []
   for name, m in entries:
     out.append(generate(m, name))
-    reg.append(f'  {{0x{fields.model_signature(m):016x}ull, launch_fast_{name}, "{name}"}},')
+    reg.append(f'  {{0x{fields.model_signature(m):016x}ull, launch_fast_{name}, "{name}", '
+               f'{CONSTRAINT_MODES[constraint_mode(m)]}}},')
   out.append("static const FastKernelEntry g_fast_kernels[] = {")
   out.extend(reg)
-  out.append("  {0ull, nullptr, nullptr}};")
+  out.append("  {0ull, nullptr, nullptr, 0}};")
   return "\n".join(out) + "\n"

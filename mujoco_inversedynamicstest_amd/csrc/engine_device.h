@@ -2508,6 +2508,32 @@ MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
   return status;
 }
 
+// The constraint part of mj_inverseSkip(mjSTAGE_NONE) for an instance whose constraint-free
+// stages the generated kernels (codegen.py) already wrote to the mirror, with the raw
+// mj_rne(flg_acc = 1) result left in qfrc_inverse: collision, mj_makeConstraint and its
+// velocity/acceleration-stage parts, then the reference's assembly
+// qfrc_inverse = rne + ((armature*qacc - qfrc_passive) - qfrc_constraint).
+template <int S, bool CONTACT, bool FUSED>
+MJH_HD int constraintOnly(const mjhipModel& m, const Lane<S>& d) {
+  int status = 0;
+  MJH_PHASE(10);
+  if constexpr (CONTACT) collision(m, d, &status);
+  else d.con_count[0] = 0;
+  MJH_PHASE(11);
+  makeConstraint<S, CONTACT, FUSED>(m, d, &status);
+  MJH_PHASE(12);
+  if constexpr (!FUSED) {
+    referenceConstraint(m, d);
+    invConstraint(m, d);
+  }
+  MJH_PHASE(13);
+  for (int i = 0; i < m.nv; i++) {
+    d.qfrc_inverse[i] += m.dof_armature[i] * d.qacc[i]
+                         - d.qfrc_passive[i] - d.qfrc_constraint[i];
+  }
+  return status;
+}
+
 //---------------------------------- engine_forward.c (constraint-free) ----------------------
 
 // mj_fwdActuation :276-515 for joint transmissions with fixed/affine gain and none/affine

@@ -35,11 +35,12 @@ struct FastKernelEntry {
   void (*launch)(dim3, dim3, hipStream_t, const Mirror&, int, const double*, const double*,
                  const double*, double*, int*, int*, int*, int*, int*);
   const char* name;
+  int cmode;   // codegen.constraint_mode: 0 none, 1 work-list, 2 every instance
 };
 #if __has_include("gen_fast.inc")
 #include "gen_fast.inc"
 #else
-static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr}};
+static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr, 0}};
 #endif
 
 // generic pipeline over the instances of a work-list (limit-active instances of the fast
@@ -52,19 +53,23 @@ static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr}};
     __syncthreads();                                                                      \
   }
 
-template <bool CONTACT, bool FUSED>
-__global__ __launch_bounds__(64) void k_inverse_list(mjhipModel m, Mirror mr,
-                                                     const int* __restrict__ worklist,
-                                                     const int* __restrict__ count,
-                                                     double* __restrict__ qfrc_out,
-                                                     int* __restrict__ status) {
+// constraint part of mj_inverseSkip after the generated kernels (mjh::constraintOnly), over
+// the work-list (LIST) or every instance; grid = ceil(B/64) blocks
+template <bool CONTACT, bool FUSED, bool LIST>
+__global__ __launch_bounds__(64) void k_constraint(mjhipModel m, Mirror mr, int B,
+                                                   const int* __restrict__ worklist,
+                                                   const int* __restrict__ count,
+                                                   double* __restrict__ qfrc_out,
+                                                   int* __restrict__ status) {
+  const long n = LIST ? (long)*count : (long)B;
+  if ((long)blockIdx.x*64 >= n) return;      // whole block idle (uniform): before the barrier
   MJHIP_CHAIN_TABLE(FUSED)
   const long g = (long)blockIdx.x*64 + threadIdx.x;
-  if (g >= *count) return;
-  const long inst = worklist[g];
+  if (g >= n) return;
+  const long inst = LIST ? worklist[g] : g;
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
   d.chain = chain;
-  int st = mjh::inverseSkip<64, CONTACT, FUSED>(m, d, mjhipSTAGE_NONE);
+  int st = mjh::constraintOnly<64, CONTACT, FUSED>(m, d);
   if (qfrc_out) {
     for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
   }
@@ -582,17 +587,23 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     c->fast->launch(grid, block, c->stream, c->mirror, B, qpos, qvel, qacc, qfrc, status,
                     c->worklist + 2, cnt, nxt, c->mirror.efc_count);
     HIPCHECK(hipGetLastError());
-    // the fast path excludes INVDISCRETE: the list is fused whenever nbody allows
+    // the fast path excludes INVDISCRETE: the constraint kernel is fused whenever nbody allows
     const bool fused = mjh::fusedOk(c->dmodel, mjhipSTAGE_NONE);
-#define MJHIP_LAUNCH_LIST(C, F)                                                              \
-    hipLaunchKernelGGL((k_inverse_list<C, F>), grid, block, 0, c->stream, c->dmodel,          \
-                       c->mirror, (const int*)(c->worklist + 2), (const int*)cnt, qfrc, status)
-    if (c->con_cap > 0) {
-      if (fused) MJHIP_LAUNCH_LIST(true, true); else MJHIP_LAUNCH_LIST(true, false);
-    } else {
-      if (fused) MJHIP_LAUNCH_LIST(false, true); else MJHIP_LAUNCH_LIST(false, false);
+    const int* wl = c->worklist + 2;
+#define MJHIP_LAUNCH_CON(C, F, L)                                                             \
+    hipLaunchKernelGGL((k_constraint<C, F, L>), grid, block, 0, c->stream, c->dmodel,         \
+                       c->mirror, B, wl, (const int*)cnt, qfrc, status)
+    if (c->fast->cmode == 2) {          // contacts or friction loss: every instance
+      if (c->con_cap > 0) {
+        if (fused) MJHIP_LAUNCH_CON(true, true, false); else MJHIP_LAUNCH_CON(true, false, false);
+      } else {
+        if (fused) MJHIP_LAUNCH_CON(false, true, false);
+        else MJHIP_LAUNCH_CON(false, false, false);
+      }
+    } else if (c->fast->cmode == 1) {   // limit-active instances (k_pos's work-list)
+      if (fused) MJHIP_LAUNCH_CON(false, true, true); else MJHIP_LAUNCH_CON(false, false, true);
     }
-#undef MJHIP_LAUNCH_LIST
+#undef MJHIP_LAUNCH_CON
     HIPCHECK(hipGetLastError());
     c->wl_last = c->wl_parity;
     c->wl_parity ^= 1;

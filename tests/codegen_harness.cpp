@@ -7,15 +7,25 @@
 #include "../mujoco_inversedynamicstest_amd/csrc/engine_device.h"
 #include GEN_INC
 
+template <bool C, bool F>
+static void constraint_part(const mjhipModel* m, Mirror& mr, int inst) {
+  static unsigned long long chain[64];
+  for (int k = 0; k < m->nbody && k < 64; k++) chain[k] = mjh::chainMask(*m, k);
+  mjh::Lane<64> d = lane_view(mr, inst / 64, inst % 64);
+  d.chain = chain;
+  mjh::constraintOnly<64, C, F>(*m, d);
+}
+
 // fields: concatenated per-instance outputs, row-major [field][inst][k] in MJHIP_DATA_FIELDS
-// order; returns the number of work-list (limit-active) instances
+// order. cmode as codegen.constraint_mode (0 none, 1 work-list, 2 all): the constraint
+// kernel's part runs on the served instances, as launch_inverse does on the device. Returns
+// the number of served instances.
 extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const double* qvel,
-                      const double* qacc, double* out, int efc_cap) {
+                      const double* qacc, double* out, int efc_cap, int con_cap, int cmode) {
   const int nblk = (B + 63) / 64;
   Mirror mr;
   memset(&mr, 0, sizeof(mr));
   const int nv = m->nv, nbody = m->nbody;
-  const int con_cap = 0;   // generated kernels serve contact-free models only
   (void)nv; (void)nbody; (void)con_cap;
 #define MJ_M(n) m->n
 #define XD(name, d0, d1, stage) mr.name##_n = (m->d0) * (d1); \
@@ -38,10 +48,17 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
     FAST_BODY(mr, i / 64, i % 64, B, qpos, qvel, qacc, nullptr, nullptr, wl, &wc, &wnext,
               mr.efc_count);
   }
-  for (int g = 0; g < wc; g++) {
-    int inst = wl[g];
-    mjh::Lane<64> d = lane_view(mr, inst / 64, inst % 64);
-    mjh::inverseSkip(*m, d, 0);
+  const bool fused = mjh::fusedOk(*m, mjhipSTAGE_NONE);
+  const int served = cmode == 2 ? B : (cmode == 1 ? wc : 0);
+  for (int g = 0; g < served; g++) {
+    const int inst = cmode == 2 ? g : wl[g];
+    if (con_cap > 0) {
+      if (fused) constraint_part<true, true>(m, mr, inst);
+      else constraint_part<true, false>(m, mr, inst);
+    } else {
+      if (fused) constraint_part<false, true>(m, mr, inst);
+      else constraint_part<false, false>(m, mr, inst);
+    }
   }
   size_t off = 0;
 #define XD(name, d0, d1, stage) { int S = mr.name##_n; \
@@ -58,5 +75,5 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
   free(wl);
-  return wc;
+  return served;
 }

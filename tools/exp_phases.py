@@ -11,16 +11,22 @@ import ctypes
 import os
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 EXP = os.path.join(ROOT, "tools", "exp")
 LIB = os.path.join(EXP, "libmjhip_phase.so")
-PHASES = ["kinematics", "comPos+camlight+tendon", "crb+factorM", "collision",
-          "makeConstraint", "transmission+invVelocity", "discrete+invConstraint",
-          "rne+assembly"]
-MARKS = [0, 1, 2, 3, 4, 5, 7, 8, 9]   # mark 6 (after invPosition) folds into phase 6
+# generic pipeline (k_inverse): marks 0-9; constraint kernel after the generated kernels
+# (k_constraint, mjh::constraintOnly): marks 10-13
+GROUPS = [
+    ("generic k_inverse", [0, 1, 2, 3, 4, 5, 7, 8, 9],   # mark 6 folds into phase 6
+     ["kinematics", "comPos+camlight+tendon", "crb+factorM", "collision", "makeConstraint",
+      "transmission+invVelocity", "discrete+invConstraint", "rne+assembly"]),
+    ("k_constraint", [10, 11, 12, 13],
+     ["collision", "makeConstraint", "reference+invConstraint"]),
+]
 
 
 def build():
@@ -45,21 +51,30 @@ def run(B=4096, reps=5):
   eng = engine.InverseEngine(m, capacity=B)
   eng.upload_states(q, v, a)
   acc = (ctypes.c_ulonglong * 32)()
-  eng.inverse(B, mirror_input=True)
-  L.mjhip_phaseRead(acc)
-  waves = (B + 63) // 64
-  tot = np.zeros(len(MARKS) - 1)
-  for _ in range(reps):
-    eng.inverse(B, mirror_input=True)
+  for generic in (False, True):
+    eng.inverse(B, mirror_input=True, generic=generic)
     torch.cuda.synchronize()
-    assert L.mjhip_phaseRead(acc) == 0
-    t = np.array([acc[k] for k in MARKS], dtype=np.float64) / waves
-    tot += np.diff(t) / 100.0          # 100 MHz ticks -> us
-  tot /= reps
-  print(f"batch {B}, {waves} waves, mean per-wave phase time (us):")
-  for name, x in zip(PHASES, tot):
-    print(f"  {name:28s} {x:9.1f}")
-  print(f"  {'total':28s} {tot.sum():9.1f}", flush=True)
+    L.mjhip_phaseRead(acc)
+    waves = (B + 63) // 64
+    sums = np.zeros(32)
+    for _ in range(reps):
+      t0 = time.perf_counter()
+      eng.inverse(B, mirror_input=True, generic=generic)
+      torch.cuda.synchronize()
+      wall = time.perf_counter() - t0
+      assert L.mjhip_phaseRead(acc) == 0
+      sums += np.array(acc[:32], dtype=np.float64)
+    print(f"batch {B}, {waves} waves, {'generic' if generic else 'default'} dispatch "
+          f"(last call {wall*1e3:.2f} ms wall); mean per-wave phase time (us):")
+    for title, marks, names in GROUPS:
+      t = sums[marks] / (reps * waves)
+      if not t.any():
+        continue
+      d = np.diff(t) / 100.0           # 100 MHz ticks -> us
+      print(f" {title}")
+      for name, x in zip(names, d):
+        print(f"  {name:28s} {x:9.1f}")
+      print(f"  {'total':28s} {d.sum():9.1f}", flush=True)
   eng.close()
 
 

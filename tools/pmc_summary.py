@@ -33,7 +33,7 @@ def main(src, dst):
   fetch = per_kernel(os.path.join(src, "pmc_2", "pmc_counter_collection.csv"), "FETCH_SIZE")
   write = per_kernel(os.path.join(src, "pmc_3", "pmc_counter_collection.csv"), "WRITE_SIZE")
   calib = 8.0 * m.nM * B / fetch["k_fac_humanoid"]
-  kernels = [k for k in fetch if k.startswith("k_") and ("humanoid" in k or k == "k_inverse_list")]
+  kernels = [k for k in fetch if k.startswith("k_") and ("humanoid" in k or k.startswith("k_constraint"))]
   rows = {k: {"fetch_bytes": fetch[k] * calib, "write_bytes": write.get(k, 0.0)} for k in kernels}
   total = sum(v["fetch_bytes"] + v["write_bytes"] for v in rows.values())
   out = {"batch": B, "model": "humanoid", "fetch_correction": calib,
