@@ -203,6 +203,8 @@ typedef struct mjhipData_ {
   int nefc;                 /* number of constraint rows of the last call */
   int status;               /* mjhipInstanceStatus bits of the last call */
   mjtNum solver_fwdinv[2];  /* mjdata.h:186, written by mjhip_compareFwdInv */
+  mjtNum energy[2];         /* potential, kinetic (mjdata.h energy): written under
+                               mjENBL_ENERGY by the stages that run (engine_inverse.c:207-223) */
   /* inputs and every fp64 output field of mj_inverseSkip, reference names */
 #define XD(name, d0, d1, stage) mjtNum* name;
   MJHIP_DATA_FIELDS

@@ -67,6 +67,7 @@ static const mjhipModel* model_view(const mjModel* m, const mjData* d) {
 
 static void data_view(mjData* d, mjhipData* hd) {
   memset(hd, 0, sizeof(*hd));
+  memcpy(hd->energy, d->energy, sizeof(hd->energy));
 #define XD(name, d0, d1, stage) hd->name = d->name;
   MJHIP_DATA_FIELDS
 #undef XD
@@ -81,6 +82,7 @@ void mj_inverseSkip(const mjModel* m, mjData* d, int skipstage, int skipsensor) 
   mjhip_inverseSkip(model_view(m, d), &hd, skipstage, skipsensor);
   d->solver_fwdinv[0] = hd.solver_fwdinv[0];
   d->solver_fwdinv[1] = hd.solver_fwdinv[1];
+  memcpy(d->energy, hd.energy, sizeof(d->energy));
 }
 
 void mj_inverse(const mjModel* m, mjData* d) {

@@ -80,6 +80,7 @@ struct SP {
   XSC(jacr, 3*nv)                     \
   XSC(qforce, nv)                     \
   XSC(qacc_save, nv)                  \
+  XSC(energy, 2)                      /* mjData energy (mjENBL_ENERGY) */ \
   XSC(qDeriv, mjh_implicit(m)*m->nD)  \
   XSC(qLU, mjh_implicit(m)*m->nD)     \
   XSC(Dcvel, mjh_implicit(m)*6*m->nB) \
@@ -137,6 +138,11 @@ struct Lane {
   // fused constraint path only (nbody <= 64): chain[k] has bit b set when body b is body k
   // or one of its ancestors (on the device a per-block LDS table, chainMasks)
   const unsigned long long* chain;
+  // geom positions as collision reads them: geom_xpos itself, or (gstage) a per-lane LDS
+  // copy that collision() fills first -- the broadphase reads every candidate pair's
+  // positions, and LDS turns those loads from memory round trips into LDS latency
+  SP<S> gxpos;
+  bool gstage;
 };
 
 // chain[k] for body k (the fused path's ancestor test, one bit per body)
@@ -149,8 +155,11 @@ MJH_HD unsigned long long chainMask(const mjhipModel& m, int k) {
 // whether mj_inverseSkip(skipstage) can take the fused constraint path
 MJH_HD bool fusedOk(const mjhipModel& m, int skipstage) {
   return skipstage == mjhipSTAGE_NONE && !(m.opt.enableflags & mjhipENBL_INVDISCRETE) &&
-         m.nbody <= 64;
+         m.nbody <= 64 && (m.ngeom <= 64 || !mjhip_contactsEnabled(&m));
 }
+
+// dynamic LDS of a fused contact kernel: the per-lane geom position copy (Lane::gxpos)
+MJH_HD unsigned gstageBytes(const mjhipModel& m) { return 3u*m.ngeom*64*sizeof(double); }
 
 //---------------------------------- engine_util_blas.c ---------------------------------------
 
@@ -800,7 +809,7 @@ MJH_HD void contactParam(const mjhipModel& m, int g1, int g2, int* condim, doubl
 // mj_filterSphere: 1 = the bounding spheres (or the plane distance) rule the pair out
 template <int S>
 MJH_HD int filterSphere(const mjhipModel& m, const Lane<S>& d, int g1, int g2, double margin) {
-  SP<S> p1 = d.geom_xpos + 3*g1, p2 = d.geom_xpos + 3*g2;
+  SP<S> p1 = d.gxpos + 3*g1, p2 = d.gxpos + 3*g2;
   double rb1 = m.geom_rbound[g1], rb2 = m.geom_rbound[g2];
   if (rb1 > 0 && rb2 > 0) {
     double dif[3] = {p1[0]-p2[0], p1[1]-p2[1], p1[2]-p2[2]};
@@ -812,7 +821,7 @@ MJH_HD int filterSphere(const mjhipModel& m, const Lane<S>& d, int g1, int g2, d
     if (m.geom_type[gp] == mjhipGEOM_PLANE && m.geom_rbound[go] > 0) {
       SP<S> mat = d.geom_xmat + 9*gp;
       double norm[3] = {mat[2], mat[5], mat[8]}, dif[3];
-      sub3(dif, d.geom_xpos + 3*go, d.geom_xpos + 3*gp);
+      sub3(dif, d.gxpos + 3*go, d.gxpos + 3*gp);
       if (dot3(dif, norm) > margin + m.geom_rbound[go]) return 1;
     }
   }
@@ -834,8 +843,8 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
   double margin = ovr ? m.opt.o_margin : (m.geom_margin[g1] > m.geom_margin[g2] ?
                                           m.geom_margin[g1] : m.geom_margin[g2]);
   if (filterSphere(m, d, g1, g2, margin)) return;
-  SP<S> pos1 = d.geom_xpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
-  SP<S> pos2 = d.geom_xpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
+  SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
+  SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
   const double *size1 = m.geom_size + 3*g1, *size2 = m.geom_size + 3*g2;
   RawContact raw[2];
   int num = 0;
@@ -918,6 +927,18 @@ MJH_HD void collision(const mjhipModel& m, const Lane<S>& d, int* status) {
   int ncon = 0;                        // in a register; written once at the end
   d.con_count[0] = 0;
   if (!mjhip_contactsEnabled(&m)) return;
+  if (d.gstage) {                      // 16 loads in flight per step
+    const int n = 3*m.ngeom;
+    for (int k = 0; k < n; k += 16) {
+      double t[16];
+#pragma unroll
+      for (int i = 0; i < 16; i++) t[i] = k + i < n ? d.geom_xpos[k+i] : 0.0;
+#pragma unroll
+      for (int i = 0; i < 16; i++) {
+        if (k + i < n) d.gxpos[k+i] = t[i];
+      }
+    }
+  }
   for (int b1 = 0; b1 < m.nbody; b1++) {
     for (int b2 = b1 + 1; b2 < m.nbody; b2++) {
       if (!mjhip_bodyPairCandidate(&m, b1, b2)) continue;
@@ -2482,14 +2503,75 @@ MJH_HD void discreteAcc(const mjhipModel& m, const Lane<S>& d) {
   solveM(m, d, d.qacc);
 }
 
+//---------------------------------- engine_sensor.c (energy) ---------------------------------
+
+// mj_energyPos engine_sensor.c:920-1008 (no flex): gravity, joint and tendon springs. As the
+// reference, the free joint's translational term normalizes (x, y, z, qw) as a quaternion
+// before differencing, and the ball term differences the raw qpos quaternion.
+template <int S>
+MJH_HD void energyPos(const mjhipModel& m, const Lane<S>& d) {
+  double e = 0, dif[3];
+  if (!(m.opt.disableflags & mjhipDSBL_GRAVITY)) {
+    const double* g = m.opt.gravity;
+    for (int i = 1; i < m.nbody; i++) {
+      SP<S> x = d.xipos + 3*i;
+      e -= m.body_mass[i] * (g[0]*x[0] + g[1]*x[1] + g[2]*x[2]);
+    }
+  }
+  if (!(m.opt.disableflags & mjhipDSBL_PASSIVE)) {
+    for (int i = 0; i < m.njnt; i++) {
+      const double k = m.jnt_stiffness[i];
+      int padr = m.jnt_qposadr[i];
+      const int t = m.jnt_type[i];
+      if (t == mjhipJNT_FREE || t == mjhipJNT_BALL) {
+        if (t == mjhipJNT_FREE) {
+          double quat[4] = {d.qpos[padr], d.qpos[padr+1], d.qpos[padr+2], d.qpos[padr+3]};
+          normalize4(quat);
+          sub3(dif, quat, m.qpos_spring + padr);
+          e += 0.5*k*(dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2]);
+          padr += 3;
+        }
+        subQuat(dif, d.qpos + padr, m.qpos_spring + padr);
+        e += 0.5*k*(dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2]);
+      } else {
+        const double x = d.qpos[padr] - m.qpos_spring[padr];
+        e += 0.5*k*x*x;
+      }
+    }
+    for (int i = 0; i < m.ntendon; i++) {
+      const double len = d.ten_length[i];
+      const double lo = m.tendon_lengthspring[2*i], hi = m.tendon_lengthspring[2*i+1];
+      double disp = 0;
+      if (len > hi) disp = hi - len;
+      else if (len < lo) disp = lo - len;
+      e += 0.5*m.tendon_stiffness[i]*disp*disp;
+    }
+  }
+  d.energy[0] = e;
+}
+
+// mj_energyVel engine_sensor.c:1011-1020: 0.5 qvel' M qvel
+template <int S>
+MJH_HD void energyVel(const mjhipModel& m, const Lane<S>& d) {
+  mulM(m, d, d.qforce, d.qvel);
+  d.energy[1] = 0.5*dot(d.qforce, d.qvel, m.nv);
+}
+
 // FUSED (the constraint rows finished at creation, see contactRowsFused) requires
 // skipstage = mjSTAGE_NONE, no mjENBL_INVDISCRETE, nbody <= 64 and d.chain set (fusedOk)
 template <int S, bool CONTACT = true, bool FUSED = false>
 MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
   int status = 0;
-  if (skipstage < mjhipSTAGE_POS) invPosition<S, CONTACT, FUSED>(m, d, &status);
+  const bool energy = (m.opt.enableflags & mjhipENBL_ENERGY) != 0;
+  if (skipstage < mjhipSTAGE_POS) {
+    invPosition<S, CONTACT, FUSED>(m, d, &status);
+    if (energy) energyPos(m, d);
+  }
   MJH_PHASE(6);
-  if (skipstage < mjhipSTAGE_VEL) invVelocity<S, FUSED>(m, d);
+  if (skipstage < mjhipSTAGE_VEL) {
+    invVelocity<S, FUSED>(m, d);
+    if (energy) energyVel(m, d);
+  }
   MJH_PHASE(7);
   const bool discrete = !FUSED && (m.opt.enableflags & mjhipENBL_INVDISCRETE) != 0;
   if (discrete) {
@@ -2643,6 +2725,9 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
 #undef XSI
   d.efc_cap = mr.efc_cap;
   d.con_cap = mr.con_cap;
+  d.chain = nullptr;
+  d.gxpos = d.geom_xpos;
+  d.gstage = false;
   return d;
 }
 

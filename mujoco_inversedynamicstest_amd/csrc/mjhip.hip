@@ -53,6 +53,15 @@ static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr, 0}};
     __syncthreads();                                                                      \
   }
 
+// fused contact kernels: collision reads geom positions from a per-lane LDS copy (dynamic
+// shared memory of mjh::gstageBytes, [3*ngeom][64 lanes])
+extern __shared__ double g_gstage[];
+#define MJHIP_GEOM_STAGE(C, F)                                                           \
+  if (C && F) {                                                                           \
+    d.gxpos.p = g_gstage + threadIdx.x;                                                   \
+    d.gstage = true;                                                                      \
+  }
+
 // constraint part of mj_inverseSkip after the generated kernels (mjh::constraintOnly), over
 // the work-list (LIST) or every instance; grid = ceil(B/64) blocks
 template <bool CONTACT, bool FUSED, bool LIST>
@@ -69,6 +78,7 @@ __global__ __launch_bounds__(64) void k_constraint(mjhipModel m, Mirror mr, int 
   const long inst = LIST ? worklist[g] : g;
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
   d.chain = chain;
+  MJHIP_GEOM_STAGE(CONTACT, FUSED)
   int st = mjh::constraintOnly<64, CONTACT, FUSED>(m, d);
   if (qfrc_out) {
     for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
@@ -92,6 +102,7 @@ __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
   if (inst >= B) return;
   Lane<64> d = lane_view(mr, blk, lane);
   d.chain = chain;
+  MJHIP_GEOM_STAGE(CONTACT, FUSED)
   if (qpos_in) {
     for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos_in[inst*m.nq + k];
   }
@@ -591,7 +602,8 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     const bool fused = mjh::fusedOk(c->dmodel, mjhipSTAGE_NONE);
     const int* wl = c->worklist + 2;
 #define MJHIP_LAUNCH_CON(C, F, L)                                                             \
-    hipLaunchKernelGGL((k_constraint<C, F, L>), grid, block, 0, c->stream, c->dmodel,         \
+    hipLaunchKernelGGL((k_constraint<C, F, L>), grid, block,                                  \
+                       (C && F) ? mjh::gstageBytes(c->dmodel) : 0, c->stream, c->dmodel,      \
                        c->mirror, B, wl, (const int*)cnt, qfrc, status)
     if (c->fast->cmode == 2) {          // contacts or friction loss: every instance
       if (c->con_cap > 0) {
@@ -610,8 +622,9 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     return MJHIP_OK;
   }
 #define MJHIP_LAUNCH_K(SK, C, F)                                                              \
-  hipLaunchKernelGGL((k_inverse<SK, C, F>), grid, block, 0, c->stream, c->dmodel, c->mirror,   \
-                     B, qpos, qvel, qacc, qfrc, status)
+  hipLaunchKernelGGL((k_inverse<SK, C, F>), grid, block,                                      \
+                     (C && F) ? mjh::gstageBytes(c->dmodel) : 0, c->stream, c->dmodel,        \
+                     c->mirror, B, qpos, qvel, qacc, qfrc, status)
 #define MJHIP_LAUNCH_GENERIC(SK)                                                              \
   if (c->con_cap > 0) {                                                                       \
     MJHIP_LAUNCH_K(SK, true, false);                                                          \
@@ -1031,6 +1044,15 @@ MJHIP_API void mjhip_inverseSkip(const mjhipModel* m, mjhipData* d, int skipstag
   MJHIP_DATA_FIELDS
 #undef XD
 #undef MJ_M
+  if (!rc && (m->opt.enableflags & mjhipENBL_ENERGY) && skipstage < mjhipSTAGE_VEL) {
+    // mj_energyPos/Vel write the energy of the stages that ran (engine_inverse.c:207-223)
+    mjtNum e[2];
+    rc = mjhip_mirrorDownload(c, "energy", 0, 1, e);
+    if (!rc) {
+      if (skipstage < mjhipSTAGE_POS) d->energy[0] = e[0];
+      d->energy[1] = e[1];
+    }
+  }
   if (!rc) {
     int cnt[4];
     if (hipMemcpy(cnt, c->mirror.efc_count, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess) {

@@ -112,7 +112,7 @@ class CModel(ctypes.Structure):
 
 class CData(ctypes.Structure):
   _fields_ = ([("nefc", ctypes.c_int), ("status", ctypes.c_int),
-               ("solver_fwdinv", ctypes.c_double * 2)] +
+               ("solver_fwdinv", ctypes.c_double * 2), ("energy", ctypes.c_double * 2)] +
               [(f.name, ctypes.POINTER(ctypes.c_double)) for f in DATA_FIELDS] +
               [(f.name, ctypes.POINTER(ctypes.c_double)) for f in FORWARD_FIELDS])
 

@@ -72,5 +72,9 @@ class MjData:
   def solver_fwdinv(self):
     return np.array(self.struct.solver_fwdinv[:2])
 
+  @property
+  def energy(self):
+    return np.array(self.struct.energy[:2])
+
   def ptr(self):
     return ctypes.byref(self.struct)

@@ -2050,13 +2050,67 @@ static void or_discreteAcc(const mjhipModel* m, mjhipData* d) {
   free(qfrc);
 }
 
+/* engine_sensor.c:920-1008 mj_energyPos: gravity, joint and tendon spring energy (no flex).
+ * As the reference, the free joint's translational term normalizes (x, y, z, qw) as a
+ * quaternion before differencing, and the ball term differences the raw qpos quaternion. */
+static void or_energyPos(const mjhipModel* m, mjhipData* d) {
+  mjtNum dif[3], quat[4];
+  d->energy[0] = 0;
+  if (!mjDISABLED(mjhipDSBL_GRAVITY)) {
+    for (int i = 1; i < m->nbody; i++) {
+      d->energy[0] -= m->body_mass[i] * mju_dot3(m->opt.gravity, d->xipos + 3*i);
+    }
+  }
+  if (mjDISABLED(mjhipDSBL_PASSIVE)) return;
+  for (int i = 0; i < m->njnt; i++) {
+    mjtNum k = m->jnt_stiffness[i];
+    int padr = m->jnt_qposadr[i];
+    int t = m->jnt_type[i];
+    if (t == mjhipJNT_FREE || t == mjhipJNT_BALL) {
+      if (t == mjhipJNT_FREE) {
+        mju_copy(quat, d->qpos + padr, 4);
+        mju_normalize4(quat);
+        mju_sub3(dif, quat, m->qpos_spring + padr);
+        d->energy[0] += 0.5*k*mju_dot3(dif, dif);
+        padr += 3;
+      }
+      mju_subQuat(dif, d->qpos + padr, m->qpos_spring + padr);
+      d->energy[0] += 0.5*k*mju_dot3(dif, dif);
+    } else {
+      mjtNum x = d->qpos[padr] - m->qpos_spring[padr];
+      d->energy[0] += 0.5*k*x*x;
+    }
+  }
+  for (int i = 0; i < m->ntendon; i++) {
+    mjtNum len = d->ten_length[i], disp = 0;
+    mjtNum lo = m->tendon_lengthspring[2*i], hi = m->tendon_lengthspring[2*i+1];
+    if (len > hi) disp = hi - len;
+    else if (len < lo) disp = lo - len;
+    d->energy[0] += 0.5*m->tendon_stiffness[i]*disp*disp;
+  }
+}
+
+/* engine_sensor.c:1011-1020 mj_energyVel: 0.5 qvel' M qvel */
+static void or_energyVel(const mjhipModel* m, mjhipData* d) {
+  mjtNum* vec = (mjtNum*)malloc((m->nv + 1)*sizeof(mjtNum));
+  or_mulM(m, d, vec, d->qvel);
+  d->energy[1] = 0.5*mju_dot(vec, d->qvel, m->nv);
+  free(vec);
+}
+
 void or_inverseSkip(const mjhipModel* m, mjhipData* d, orEfc* e, int skipstage,
                     int skipsensor) {
   int nv = m->nv;
   (void)skipsensor;
   mjtNum* qacc = NULL;
-  if (skipstage < mjhipSTAGE_POS) or_invPosition(m, d, e);
-  if (skipstage < mjhipSTAGE_VEL) or_fwdVelocity(m, d, e);
+  if (skipstage < mjhipSTAGE_POS) {
+    or_invPosition(m, d, e);
+    if (mjENABLED(mjhipENBL_ENERGY)) or_energyPos(m, d);
+  }
+  if (skipstage < mjhipSTAGE_VEL) {
+    or_fwdVelocity(m, d, e);
+    if (mjENABLED(mjhipENBL_ENERGY)) or_energyVel(m, d);
+  }
   if (mjENABLED(mjhipENBL_INVDISCRETE)) {
     qacc = (mjtNum*)malloc(nv*sizeof(mjtNum));
     mju_copy(qacc, d->qacc, nv);

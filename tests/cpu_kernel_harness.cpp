@@ -85,5 +85,7 @@ static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int
   static unsigned long long chain[64];
   for (int k = 0; k < m->nbody && k < 64; k++) chain[k] = mjh::chainMask(*m, k);
   L.chain = chain;
+  L.gxpos = L.geom_xpos;
+  L.gstage = false;
   return L;
 }

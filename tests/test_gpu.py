@@ -409,3 +409,25 @@ def test_invdiscrete_implicit_parity(name):
     e.close()
   ref, _ = oracle_batch(m, q, v, a)
   assert_close(f, ref["qfrc_inverse"], "qfrc_inverse (implicit INVDISCRETE)")
+
+
+def test_energy_parity():
+  """mjENBL_ENERGY (mj_energyPos/Vel) on the device: energy in the mirror vs the oracle."""
+  m = models.load("humanoid", disable_contact=True)
+  m.opt["enableflags"] |= 1 << 1
+  B = 512
+  q, v, a = sample_states(m, B, first=500)
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    assert e.fast_kernel is None
+    f = e.inverse(q, v, a)
+    en = e.field("energy", 0, B)
+  finally:
+    e.close()
+  o = Oracle(m)
+  ref_f, ref_e = [], []
+  for i in range(B):
+    ref_f.append(o.inverse(q[i], v[i], a[i]))
+    ref_e.append(o.d.energy)
+  assert_close(f, np.array(ref_f), "qfrc_inverse (ENERGY)")
+  assert_close(en, np.array(ref_e), "energy")
