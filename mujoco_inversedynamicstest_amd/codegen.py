@@ -874,9 +874,9 @@ def _gen_va(M: _Model, store_fields=None) -> str:
   E(f"double qacc[{nv}];")
   # row-major qfrc_inverse copy, or (no output array) a harmless second write of the mirror
   # slot: a select instead of a branch keeps the pass one scheduling region
-  if M.cmode != "all":
-    E(f"double* qo = qfrc_out ? qfrc_out + inst*{nv} : P_qfrc_inverse;")
-    E(f"const long qo_stride = qfrc_out ? 1 : 64;")
+  # the row-major qfrc_inverse copy goes through LDS (qo_lds[lane][k]); the kernel wrapper
+  # writes the block's rows out coalesced after the body (an in-place row-major store per
+  # dof would scatter 64 lanes over 64 rows)
 
   def pre(i):
     if not i:
@@ -961,7 +961,7 @@ def _gen_va(M: _Model, store_fields=None) -> str:
           E("qfi = qfa;")
         G.st("qfrc_constraint", k, "0.0")
         G.st("qfrc_inverse", k, "qfi")
-        E(f"qo[{k}*qo_stride] = qfi;")
+        E(f"qo_lds[lane*{nv} + {k}] = qfi;")
       E.close()
     if M.parent[i]:
       E(f"mjh::addTo(cfrc_{M.parent[i]}, cfrc_{i}, 6);")
@@ -1045,7 +1045,8 @@ _SIG = {
             "qpos_in, qvel_in, qacc_in, worklist, worklist_count, worklist_next, efc_count, trig"),
     "fac": ("int* __restrict__ efc_count", "efc_count"),
     "va": ("double* __restrict__ qfrc_out, int* __restrict__ status, "
-           "int* __restrict__ efc_count", "qfrc_out, status, efc_count"),
+           "int* __restrict__ efc_count, double* __restrict__ qo_lds",
+           "qfrc_out, status, efc_count, qo_lds"),
 }
 _GEN = {"pos": lambda M, sf: _gen_pos(M, sf), "fac": lambda M, sf: _gen_fac(M, sf),
         "va": lambda M, sf: _gen_va(M, sf)}
@@ -1077,23 +1078,38 @@ def generate(m, name: str, store_fields=None) -> str:
     int* __restrict__ worklist_count, int* __restrict__ worklist_next,
     int* __restrict__ efc_count) {{
   double trig[{max(1, 2 * len(M.trig) * 64)}];   // LDS on the device (k_pos)
+  double qo_lds[{64 * max(M.nv, 1)}];             // LDS on the device (k_va)
 """ + "".join(f"  fast_{st}_{name}(mr, blk, lane, B, {_SIG[st][1]});\n" for st in STAGES)
-             + "}\n")
+             + (f"""  if (qfrc_out && (long)blk*64 + lane < B) {{
+    for (int k = 0; k < {M.nv}; k++) qfrc_out[((long)blk*64 + lane)*{M.nv} + k] = qo_lds[lane*{M.nv} + k];
+  }}
+""" if M.cmode != "all" else "  (void)qo_lds;\n") + "}\n")
   out.append("#if defined(__HIPCC__)")
   for st in STAGES:
     params, args = _SIG[st]
+    tail = ""
     if st == "pos":
       params = params.replace(", double* __restrict__ trig", "")
       decl = f"  __shared__ double trig[{max(1, 2 * len(M.trig) * 64)}];\n"
+    elif st == "va":
+      params = params.replace(", double* __restrict__ qo_lds", "")
+      decl = f"  __shared__ double qo_lds[{64 * max(M.nv, 1)}];\n"
+      if M.cmode != "all":   # coalesced row-major copy of the block's qfrc_inverse rows
+        tail = (f"  if (!qfrc_out) return;\n  __syncthreads();\n"
+                f"  const long n = ((long)B - (long)blockIdx.x*64 < 64 ? "
+                f"(long)B - (long)blockIdx.x*64 : 64) * {M.nv};\n"
+                f"  double* dst = qfrc_out + (long)blockIdx.x*64*{M.nv};\n"
+                f"  for (long r = threadIdx.x; r < n; r += 64) dst[r] = qo_lds[r];\n")
     else:
       decl = ""
     out.append(f"__global__ __launch_bounds__(64, 1) void k_{st}_{name}(Mirror mr, int B, "
-               f"{params}) {{\n{decl}  fast_{st}_{name}(mr, blockIdx.x, threadIdx.x, B, {args});\n}}")
+               f"{params}) {{\n{decl}  fast_{st}_{name}(mr, blockIdx.x, threadIdx.x, B, {args});\n"
+               f"{tail}}}")
   out.append(f"""static void launch_fast_{name}(dim3 g, dim3 b, hipStream_t s, const Mirror& mr,
     int B, const double* qpos_in, const double* qvel_in, const double* qacc_in, double* qfrc_out,
     int* status, int* worklist, int* worklist_count, int* worklist_next, int* efc_count) {{""")
   for st in STAGES:
-    args = _SIG[st][1].replace(", trig", "")
+    args = _SIG[st][1].replace(", trig", "").replace(", qo_lds", "")
     out.append(f"  hipLaunchKernelGGL(k_{st}_{name}, g, b, 0, s, mr, B, {args});")
   out.append("}")
   out.append("#endif")

@@ -74,16 +74,34 @@ __global__ __launch_bounds__(64) void k_constraint(mjhipModel m, Mirror mr, int 
   if ((long)blockIdx.x*64 >= n) return;      // whole block idle (uniform): before the barrier
   MJHIP_CHAIN_TABLE(FUSED)
   const long g = (long)blockIdx.x*64 + threadIdx.x;
-  if (g >= n) return;
-  const long inst = LIST ? worklist[g] : g;
-  Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
-  d.chain = chain;
-  MJHIP_GEOM_STAGE(CONTACT, FUSED)
-  int st = mjh::constraintOnly<64, CONTACT, FUSED>(m, d);
-  if (qfrc_out) {
-    for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
+  if (LIST || !qfrc_out) {
+    if (g >= n) return;
+    const long inst = LIST ? worklist[g] : g;
+    Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
+    d.chain = chain;
+    MJHIP_GEOM_STAGE(CONTACT, FUSED)
+    const int st = mjh::constraintOnly<64, CONTACT, FUSED>(m, d);
+    if (status) status[inst] = st;
+    if (qfrc_out) {        // a few scattered work-list instances
+      for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
+    }
+    return;
   }
-  if (status) status[inst] = st;
+  // every instance with a row-major output: the block's rows go out coalesced through LDS
+  // (after the geom copy); lanes past B skip the work but join the copy
+  double* qo = g_gstage + ((CONTACT && FUSED) ? 3*m.ngeom*64 : 0);
+  if (g < n) {
+    Lane<64> d = lane_view(mr, (int)(g >> 6), (int)(g & 63));
+    d.chain = chain;
+    MJHIP_GEOM_STAGE(CONTACT, FUSED)
+    const int st = mjh::constraintOnly<64, CONTACT, FUSED>(m, d);
+    if (status) status[g] = st;
+    for (int k = 0; k < m.nv; k++) qo[threadIdx.x*m.nv + k] = d.qfrc_inverse[k];
+  }
+  __syncthreads();
+  const long rows = n - (long)blockIdx.x*64 < 64 ? n - (long)blockIdx.x*64 : 64;
+  double* dst = qfrc_out + (long)blockIdx.x*64*m.nv;
+  for (long r = threadIdx.x; r < rows*m.nv; r += 64) dst[r] = qo[r];
 }
 
 
@@ -603,8 +621,9 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     const int* wl = c->worklist + 2;
 #define MJHIP_LAUNCH_CON(C, F, L)                                                             \
     hipLaunchKernelGGL((k_constraint<C, F, L>), grid, block,                                  \
-                       (C && F) ? mjh::gstageBytes(c->dmodel) : 0, c->stream, c->dmodel,      \
-                       c->mirror, B, wl, (const int*)cnt, qfrc, status)
+                       ((C && F) ? mjh::gstageBytes(c->dmodel) : 0) +                         \
+                       ((!L && qfrc) ? 64u*sizeof(double)*c->dmodel.nv : 0), c->stream,      \
+                       c->dmodel, c->mirror, B, wl, (const int*)cnt, qfrc, status)
     if (c->fast->cmode == 2) {          // contacts or friction loss: every instance
       if (c->con_cap > 0) {
         if (fused) MJHIP_LAUNCH_CON(true, true, false); else MJHIP_LAUNCH_CON(true, false, false);

@@ -184,7 +184,8 @@ class InverseEngine:
       B = int(qpos)
       flags |= FLAG_MIRROR_INPUT
       pq = pv = pa = None
-      dev = out is not None and _dptr(out) is not None
+      # no `out`: the results stay in the device mirror (field()), nothing is copied back
+      dev = out is None or _dptr(out) is not None
     else:
       dev = _dptr(qpos) is not None
       if dev:
