@@ -34,7 +34,7 @@ def pmc_traffic(eng, model, count):
   from mujoco_inversedynamicstest_amd import codegen
   if not eng.fast_kernel:
     return None, None
-  want = {f"k_{st}_{eng.fast_kernel}" for st in codegen.STAGES}
+  want = set(codegen.hot_kernels(eng.fast_kernel))
   for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")),
                      reverse=True):
     rec = json.load(open(path))
@@ -52,7 +52,7 @@ def main():
   ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
   ap.add_argument("--model", default="humanoid")
   ap.add_argument("--cpu-threads", type=int, default=16)
-  ap.add_argument("--cpu-sample", type=int, default=1_500_000,
+  ap.add_argument("--cpu-sample", type=int, default=4_000_000,
                   help="instances in the CPU-baseline sample (rank 0, N=1 only)")
   ap.add_argument("--no-cpu", action="store_true")
   ap.add_argument("--config-batch", type=int, default=None,
@@ -161,7 +161,7 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
                      "algorithmic_bytes_per_launch": bytes_per_eval * count,
-                     "kernel": ("+".join(f"k_{st}_{eng.fast_kernel}" for st in codegen.STAGES)
+                     "kernel": ("+".join(codegen.hot_kernels(eng.fast_kernel))
                                 + "+k_constraint" if eng.fast_kernel else "k_inverse<0>"),
                      "kernel_ms": kernel_ms, "generic_kernel_ms": generic_ms,
                      "bytes_per_eval": bytes_per_eval},
@@ -177,7 +177,7 @@ def main():
 def other_config(args):
   """Throughput of configs 4 (contacts) and 5 (finite-difference Jacobians), 1 GPU."""
   import torch
-  from mujoco_inversedynamicstest_amd import engine, models
+  from mujoco_inversedynamicstest_amd import codegen, engine, models
   from mujoco_inversedynamicstest_amd.sampler import sample_contact_states, sample_states
   torch.cuda.set_device(0)
   if args.config == 4:
@@ -199,7 +199,7 @@ def other_config(args):
     rec = {"metric": "mj_inverse evals/sec, config 4 (contacts on)", "value": B / dt,
            "unit": "evals/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": dt * 1e3,
            "dtype": "f64",
-           "kernel": (f"generated k_pos/k_fac/k_va_{eng.fast_kernel} + k_constraint"
+           "kernel": (f"generated {'+'.join(codegen.hot_kernels(eng.fast_kernel))} + k_constraint"
                       if eng.fast_kernel else "k_inverse<0, contacts> (generic)"),
            "config": {"workload": f"{args.model} keyframe poses + noise, contacts on",
                       "batch": B},

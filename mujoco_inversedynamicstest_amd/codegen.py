@@ -54,6 +54,16 @@ STAGES = ("pos", "fac", "va")
 FRAMES_IN_PASS1 = True   # k_pos: pass 1 stores the frames, pass 2 cinert/cdof/crb/qM
 MAX_LDS_HINGES = 32
 PREFETCH = 1      # tree-pass events between a body's mirror loads and their first use
+FUSE = True       # one launch running the three stage bodies back to back per wave
+# lanes per workgroup of each stage kernel: 64 = one instance block per wave; 32 = a block
+# split over two half-filled waves (twice the waves per SIMD, same mirror layout)
+LANES = {"pos": 64, "fac": 64, "va": 64}
+
+
+def _ll(st):
+  """LDS lane index and stride of stage st (LDS arrays are per workgroup)."""
+  n = LANES[st]
+  return ("lane", 64) if n == 64 else (f"(lane & {n - 1})", n)
 
 
 def lit(x) -> str:
@@ -313,7 +323,8 @@ def _emit_frame(G: _Stage, i, store):
           if j in M.trig:
             h = M.trig[j]
             E(f"mjh::axisAngle2QuatSC(qloc, jaxis, qpos[{qa}] - {lit(m.qpos0[qa])}, "
-              f"trig[{2 * h}*64 + lane], trig[{2 * h + 1}*64 + lane]);")
+              f"trig[{2 * h}*{_ll('pos')[1]} + {_ll('pos')[0]}], "
+              f"trig[{2 * h + 1}*{_ll('pos')[1]} + {_ll('pos')[0]}]);")
           else:
             E(f"mjh::axisAngle2Quat(qloc, jaxis, qpos[{qa}] - {lit(m.qpos0[qa])});")
         E(f"mjh::mulQuat(xquat_{i}, xquat_{i}, qloc);")
@@ -480,7 +491,8 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
       E.open()
       E(f"double s, c, a = (qpos[{qa}] - {lit(m.qpos0[qa])})*0.5;")
       E("MJH_SINCOS(a, s, c);")
-      E(f"trig[{2 * h}*64 + lane] = s; trig[{2 * h + 1}*64 + lane] = c;")
+      li, ls = _ll("pos")
+      E(f"trig[{2 * h}*{ls} + {li}] = s; trig[{2 * h + 1}*{ls} + {li}] = c;")
       E.close()
     E("MJH_MEM_BARRIER();")
   # ---- pass 1: kinematics -> subtree centers of mass (mj_comPos :183-208)
@@ -961,7 +973,7 @@ def _gen_va(M: _Model, store_fields=None) -> str:
           E("qfi = qfa;")
         G.st("qfrc_constraint", k, "0.0")
         G.st("qfrc_inverse", k, "qfi")
-        E(f"qo_lds[lane*{nv} + {k}] = qfi;")
+        E(f"qo_lds[{_ll('va')[0]}*{nv} + {k}] = qfi;")
       E.close()
     if M.parent[i]:
       E(f"mjh::addTo(cfrc_{M.parent[i]}, cfrc_{i}, 6);")
@@ -1088,32 +1100,71 @@ def generate(m, name: str, store_fields=None) -> str:
   for st in STAGES:
     params, args = _SIG[st]
     tail = ""
+    nl = LANES[st]
+    sub = 64 // nl    # workgroups per 64-instance block
     if st == "pos":
       params = params.replace(", double* __restrict__ trig", "")
-      decl = f"  __shared__ double trig[{max(1, 2 * len(M.trig) * 64)}];\n"
+      decl = f"  __shared__ double trig[{max(1, 2 * len(M.trig) * nl)}];\n"
     elif st == "va":
       params = params.replace(", double* __restrict__ qo_lds", "")
-      decl = f"  __shared__ double qo_lds[{64 * max(M.nv, 1)}];\n"
-      if M.cmode != "all":   # coalesced row-major copy of the block's qfrc_inverse rows
+      decl = f"  __shared__ double qo_lds[{nl * max(M.nv, 1)}];\n"
+      if M.cmode != "all":   # coalesced row-major copy of the workgroup's qfrc_inverse rows
         tail = (f"  if (!qfrc_out) return;\n  __syncthreads();\n"
-                f"  const long n = ((long)B - (long)blockIdx.x*64 < 64 ? "
-                f"(long)B - (long)blockIdx.x*64 : 64) * {M.nv};\n"
-                f"  double* dst = qfrc_out + (long)blockIdx.x*64*{M.nv};\n"
-                f"  for (long r = threadIdx.x; r < n; r += 64) dst[r] = qo_lds[r];\n")
+                f"  const long r0 = (long)blockIdx.x*{nl};\n"
+                f"  const long n = ((long)B - r0 < {nl} ? (long)B - r0 : {nl}) * {M.nv};\n"
+                f"  double* dst = qfrc_out + r0*{M.nv};\n"
+                f"  for (long r = threadIdx.x; r < n; r += {nl}) dst[r] = qo_lds[r];\n")
     else:
       decl = ""
-    out.append(f"__global__ __launch_bounds__(64, 1) void k_{st}_{name}(Mirror mr, int B, "
-               f"{params}) {{\n{decl}  fast_{st}_{name}(mr, blockIdx.x, threadIdx.x, B, {args});\n"
+    if sub == 1:
+      bl = "blockIdx.x, threadIdx.x"
+    else:
+      bl = f"blockIdx.x / {sub}, (blockIdx.x % {sub})*{nl} + threadIdx.x"
+    out.append(f"__global__ __launch_bounds__({nl}, 1) void k_{st}_{name}(Mirror mr, int B, "
+               f"{params}) {{\n{decl}  fast_{st}_{name}(mr, {bl}, B, {args});\n"
                f"{tail}}}")
+  # k_all: the three stage bodies back to back in one launch. Each stage re-reads what the
+  # previous one stored (a compiler memory barrier between them keeps the reloads), so the
+  # live ranges stay those of the staged kernels; the reloads hit the wave's own freshly
+  # written lines in L2, and no wave waits for the whole grid at a kernel boundary.
+  ntrig = max(1, 2 * len(M.trig) * 64)
+  nqo = 64 * max(M.nv, 1)
+  fuse_tail = ""
+  if M.cmode != "all":
+    fuse_tail = (f"  if (!qfrc_out) return;\n  __syncthreads();\n"
+                 f"  const long n = ((long)B - (long)blockIdx.x*64 < 64 ? "
+                 f"(long)B - (long)blockIdx.x*64 : 64) * {M.nv};\n"
+                 f"  double* dst = qfrc_out + (long)blockIdx.x*64*{M.nv};\n"
+                 f"  for (long r = threadIdx.x; r < n; r += 64) dst[r] = qo_lds[r];\n")
+  out.append(f"""__global__ __launch_bounds__(64, 1) void k_all_{name}(Mirror mr, int B,
+    const double* __restrict__ qpos_in, const double* __restrict__ qvel_in,
+    const double* __restrict__ qacc_in, double* __restrict__ qfrc_out, int* __restrict__ status,
+    int* __restrict__ worklist, int* __restrict__ worklist_count, int* __restrict__ worklist_next,
+    int* __restrict__ efc_count) {{
+  __shared__ double trig[{ntrig}];
+  __shared__ double qo_lds[{nqo}];
+""" + "\n".join(f"  fast_{st}_{name}(mr, blockIdx.x, threadIdx.x, B, {_SIG[st][1]});\n"
+                f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE();" for st in STAGES)
+             + "\n" + fuse_tail + "}")
   out.append(f"""static void launch_fast_{name}(dim3 g, dim3 b, hipStream_t s, const Mirror& mr,
     int B, const double* qpos_in, const double* qvel_in, const double* qacc_in, double* qfrc_out,
     int* status, int* worklist, int* worklist_count, int* worklist_next, int* efc_count) {{""")
-  for st in STAGES:
-    args = _SIG[st][1].replace(", trig", "").replace(", qo_lds", "")
-    out.append(f"  hipLaunchKernelGGL(k_{st}_{name}, g, b, 0, s, mr, B, {args});")
+  if FUSE:
+    out.append(f"  hipLaunchKernelGGL(k_all_{name}, g, b, 0, s, mr, B, qpos_in, qvel_in, qacc_in, "
+               f"qfrc_out, status, worklist, worklist_count, worklist_next, efc_count);")
+  else:
+    for st in STAGES:
+      args = _SIG[st][1].replace(", trig", "").replace(", qo_lds", "")
+      gb = "g, b" if LANES[st] == 64 else f"dim3(g.x*{64 // LANES[st]}), dim3({LANES[st]})"
+      out.append(f"  hipLaunchKernelGGL(k_{st}_{name}, {gb}, 0, s, mr, B, {args});")
   out.append("}")
   out.append("#endif")
   return "\n".join(out) + "\n"
+
+
+def hot_kernels(name: str) -> list:
+  """Names of the kernels one fast-path launch of model `name` runs (profiles, bench)."""
+  return [f"k_all_{name}"] if FUSE else [f"k_{st}_{name}" for st in STAGES]
 
 
 def generate_registry(entries) -> str:

@@ -18,7 +18,8 @@ sys.path.insert(0, ROOT)
 from mujoco_inversedynamicstest_amd import codegen, fields, models  # noqa: E402
 
 EXP = os.path.join(ROOT, "tools", "exp")
-VARIANTS = {"p1": {"PREFETCH": 1}, "p2": {"PREFETCH": 2}, "p3": {"PREFETCH": 3}}
+VARIANTS = {"staged": {}, "half_pos": {"LANES": {"pos": 32, "fac": 64, "va": 64}},
+            "half_all": {"LANES": {"pos": 32, "fac": 32, "va": 32}}}
 
 
 def build():
@@ -33,9 +34,15 @@ def build():
       setattr(codegen, k, v)
     calls = {"pos": "mr, B, nullptr, nullptr, nullptr, wl, wc, nullptr, ec",
              "fac": "mr, B, ec", "va": "mr, B, nullptr, nullptr, ec"}
+    if settings.get("FUSE"):
+      launch.append(f"    if (variant == {vi} && stage == 0) hipLaunchKernelGGL(k_all_{name}, g, b, 0, 0, "
+                    "mr, B, nullptr, nullptr, nullptr, nullptr, nullptr, wl, wc, nullptr, ec);")
+      continue
     for si, st in enumerate(codegen.STAGES):
+      nl = settings.get("LANES", codegen.LANES)[st]
+      gb = "g, b" if nl == 64 else f"dim3(g.x*{64 // nl}), dim3({nl})"
       launch.append(f"    if (variant == {vi} && stage == {si}) "
-                    f"hipLaunchKernelGGL(k_{st}_{name}, g, b, 0, 0, {calls[st]});")
+                    f"hipLaunchKernelGGL(k_{st}_{name}, {gb}, 0, 0, {calls[st]});")
   sizes = ", ".join(f"{k} = {m.sizes.get(k, 0)}" for k in fields.MODEL_SIZES)
   src = f'''#include <hip/hip_runtime.h>
 #include <string.h>

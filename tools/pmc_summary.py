@@ -18,6 +18,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
+# FETCH_SIZE correction for this engine's 8-byte-per-lane mirror reads, calibrated on the
+# staged k_fac_humanoid, whose reads are exactly qM (profiles/r01/pmc_v7_pass2.csv: 1.9623)
+CALIB_8B = 1.9623055899886392
+
+
 def per_kernel(path, counter):
   vals = collections.defaultdict(list)
   for r in csv.DictReader(open(path)):
@@ -32,7 +37,10 @@ def main(src, dst):
   B = 65536
   fetch = per_kernel(os.path.join(src, "pmc_2", "pmc_counter_collection.csv"), "FETCH_SIZE")
   write = per_kernel(os.path.join(src, "pmc_3", "pmc_counter_collection.csv"), "WRITE_SIZE")
-  calib = 8.0 * m.nM * B / fetch["k_fac_humanoid"]
+  if "k_fac_humanoid" in fetch:
+    calib = 8.0 * m.nM * B / fetch["k_fac_humanoid"]
+  else:   # fused launch: the factor calibrated on the staged k_fac (8-byte lane accesses)
+    calib = CALIB_8B
   kernels = [k for k in fetch if k.startswith("k_") and ("humanoid" in k or k.startswith("k_constraint"))]
   rows = {k: {"fetch_bytes": fetch[k] * calib, "write_bytes": write.get(k, 0.0)} for k in kernels}
   total = sum(v["fetch_bytes"] + v["write_bytes"] for v in rows.values())
