@@ -206,27 +206,94 @@ def other_config(args):
            "ncon_hist": np.bincount(ncon).tolist(), "nefc_max": int(nefc.max()),
            "nefc_mean": float(nefc.mean())}
   else:
-    m = models.load(args.model, disable_contact=True)
-    nb = args.config_batch or 1024
-    P = 3 * m.nv + 1
-    q, v, a = sample_states(m, nb)
-    eng = engine.InverseEngine(m, capacity=nb * P)
-    for _ in range(args.warmup):
-      eng.inverse_fd(q, v, a)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-      eng.inverse_fd(q, v, a)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.steps
-    rec = {"metric": "mjd_inverseFD Jacobian sets/sec, config 5", "value": nb / dt,
-           "unit": "base states/s", "inverse_evals_per_s": nb * P / dt, "n_gpus": 1,
-           "steps": args.steps, "ms_per_step": dt * 1e3, "dtype": "f64",
-           "config": {"workload": f"{args.model}, {nb} base states x {P} evaluations "
-                                  f"(DfDq, DfDv, DfDa, forward differences, eps 1e-6), "
-                                  f"host arrays in/out (PCIe-inclusive)"}}
+    return config5(args)
   print(json.dumps(rec), flush=True)
   eng.close()
+
+
+def config5(args):
+  """Config 5: batched mjd_inverseFD over base states resident in HBM, one process per GPU.
+
+  Each rank owns a contiguous shard of the global base-state set (weak scaling: --config-batch
+  base states per GPU, default 1024), so all 3nv+1 perturbations of a base state and their
+  differencing stay on one GPU. A step is one mjd_inverseFD over the shard:
+  expand, mj_inverse over every perturbation, difference, Jacobians left in HBM. After timing,
+  rank 0 gathers every rank's DfDq/DfDv/DfDa over RCCL (timed separately), and the
+  PCIe-inclusive host-array rate is measured once for reference."""
+  import torch
+  import torch.distributed as dist
+  from mujoco_inversedynamicstest_amd import engine, models, parallel
+  from mujoco_inversedynamicstest_amd.sampler import sample_states
+  world = int(os.environ.get("WORLD_SIZE", "1"))
+  rank = int(os.environ.get("RANK", "0"))
+  local = int(os.environ.get("LOCAL_RANK", "0"))
+  torch.cuda.set_device(local)
+  dev = torch.device("cuda", local)
+  if world > 1:
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
+  m = models.load(args.model, disable_contact=True)
+  nb = args.config_batch or 1024
+  P = 3 * m.nv + 1
+  first, count = parallel.shard(nb * world, world, rank)
+  q, v, a = sample_states(m, count, first=first)
+  eng = engine.InverseEngine(m, capacity=count * P, device=local)
+  tq, tv, ta = (torch.from_numpy(x).to(dev) for x in (q, v, a))
+  mk = lambda: torch.empty((count, m.nv, m.nv), dtype=torch.float64, device=dev)
+  out = (mk(), mk(), mk(), None)
+  torch.cuda.synchronize(dev)
+
+  def step():
+    eng.inverse_fd(tq, tv, ta, out=out)
+
+  for _ in range(args.warmup):
+    step()
+  torch.cuda.synchronize(dev)
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize(dev)
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    step()
+  torch.cuda.synchronize(dev)
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize(dev)
+  elapsed = time.perf_counter() - t0
+  t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+  if world > 1:
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+  dt = float(t.item()) / args.steps
+  # gather of the Jacobians to rank 0 (RCCL point-to-point), outside the timed region
+  jac = torch.stack(out[:3])
+  torch.cuda.synchronize(dev)
+  g0 = time.perf_counter()
+  gathered = parallel.gather_to_rank0(jac, world, rank)
+  torch.cuda.synchronize(dev)
+  gather_ms = (time.perf_counter() - g0) * 1e3
+  # PCIe-inclusive reference: host arrays in, host Jacobians out, one call
+  h0 = time.perf_counter()
+  eng.inverse_fd(q, v, a)
+  host_dt = time.perf_counter() - h0
+  if rank == 0:
+    checksum = float(sum(float(x.abs().sum()) for x in gathered))
+    rec = {"metric": "mjd_inverseFD Jacobian sets/sec, config 5", "value": world * count / dt,
+           "unit": "base states/s", "inverse_evals_per_s": world * count * P / dt,
+           "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+           "ms_per_step": dt * 1e3, "higher_is_better": True, "scaling": "weak",
+           "dtype": "f64", "data": "synthetic: config-2 sampler, base states resident in HBM",
+           "config": {"workload": f"{args.model} mjd_inverseFD, {count} base states per GPU x "
+                                  f"{P} evaluations (DfDq, DfDv, DfDa, forward differences, "
+                                  f"eps 1e-6), Jacobians left in HBM",
+                      "per_gpu_base_states": count, "global_base_states": world * count,
+                      "parallelism": f"dp{world}"},
+           "gather_to_rank0_ms": gather_ms,
+           "pcie_inclusive_rank0_base_states_per_s": count / host_dt,
+           "checksum_jacobians": checksum}
+    print(json.dumps(rec), flush=True)
+  eng.close()
+  if world > 1:
+    dist.destroy_process_group()
 
 
 if __name__ == "__main__":

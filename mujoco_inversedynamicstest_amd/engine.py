@@ -287,8 +287,23 @@ class InverseEngine:
            "mjhip_timeInverseKernel")
     return ms.value
 
-  def inverse_fd(self, qpos, qvel, qacc, eps=1e-6, dmdq=False):
-    """Batched mjd_inverseFD (flg_actuation=0, no sensors): DfDq, DfDv, DfDa [B, nv, nv]."""
+  def inverse_fd(self, qpos, qvel, qacc, eps=1e-6, dmdq=False, out=None):
+    """Batched mjd_inverseFD (flg_actuation=0, no sensors): DfDq, DfDv, DfDa [B, nv, nv].
+
+    Host arrays in -> numpy arrays out (PCIe both ways). Contiguous float64 torch tensors on
+    the context's GPU in -> torch tensors out on that GPU, asynchronous on the context's
+    stream (out: optional preallocated (DfDq, DfDv, DfDa, DmDq) device tensors)."""
+    if _dptr(qpos) is not None:
+      import torch
+      B, nv = qpos.shape[0], self.nv
+      if out is None:
+        mk = lambda n: torch.empty((B, nv, n), dtype=torch.float64, device=qpos.device)
+        out = (mk(nv), mk(nv), mk(nv), mk(self.m.nM) if dmdq else None)
+      ptrs = [None if t is None else _dptr(t) for t in out]
+      _check(lib().mjhip_inverseFDBatch(self.ctx, B, _dptr(qpos), _dptr(qvel), _dptr(qacc),
+                                        eps, *ptrs, FLAG_DEVICE_PTRS),
+             "mjhip_inverseFDBatch")
+      return tuple(out)
     qpos = np.ascontiguousarray(qpos, dtype=np.float64).reshape(-1, self.nq)
     qvel = np.ascontiguousarray(qvel, dtype=np.float64).reshape(-1, self.nv)
     qacc = np.ascontiguousarray(qacc, dtype=np.float64).reshape(-1, self.nv)

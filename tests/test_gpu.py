@@ -174,6 +174,21 @@ def test_inverse_fd_parity(humanoid, eng):
     np.testing.assert_allclose(DmDq[i], rm, rtol=1e-5, atol=1e-5)
 
 
+def test_inverse_fd_device_tensors(humanoid, eng):
+  """Device-resident mjd_inverseFD (config 5 bench path) equals the host-array path bit for
+  bit: same kernels, only the transfers differ."""
+  import torch
+  q, v, a = sample_states(humanoid, 8, first=1200)
+  hq, hv, ha, hm = eng.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
+  t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+  tq, tv, ta = t(q), t(v), t(a)
+  torch.cuda.synchronize()
+  dq, dv, da, dm = eng.inverse_fd(tq, tv, ta, eps=1e-6, dmdq=True)
+  torch.cuda.synchronize()
+  for h, d in ((hq, dq), (hv, dv), (ha, da), (hm, dm)):
+    assert np.array_equal(h, d.cpu().numpy())
+
+
 def test_linear_system_inverse_on_gpu(linear):
   """LinearSystemInverse (engine_derivative_test.cc:793-868) through the GPU FD path."""
   o = Oracle(linear)
