@@ -161,6 +161,7 @@ typedef struct mjhipOption_ {
   mjtNum impratio;
   mjtNum gravity[3];
   mjtNum wind[3];
+  mjtNum magnetic[3];        /* magnetometer sensor field (mjmodel.h mjOption) */
   mjtNum density;
   mjtNum viscosity;
   mjtNum o_margin;
@@ -205,6 +206,7 @@ typedef struct mjhipData_ {
   mjtNum solver_fwdinv[2];  /* mjdata.h:186, written by mjhip_compareFwdInv */
   mjtNum energy[2];         /* potential, kinetic (mjdata.h energy): written under
                                mjENBL_ENERGY by the stages that run (engine_inverse.c:207-223) */
+  mjtNum time;              /* simulation time (mjdata.h time): read by clock sensors */
   /* inputs and every fp64 output field of mj_inverseSkip, reference names */
 #define XD(name, d0, d1, stage) mjtNum* name;
   MJHIP_DATA_FIELDS
@@ -214,6 +216,10 @@ typedef struct mjhipData_ {
    * qfrc_actuator, qfrc_smooth, qacc_smooth */
 #define XD(name, d0, d1, stage) mjtNum* name;
   MJHIP_DATA_FORWARD
+#undef XD
+  /* computed by the sensor stages when a sensor needs them (engine_sensor.c) */
+#define XD(name, d0, d1, stage) mjtNum* name;
+  MJHIP_DATA_SENSOR_AUX
 #undef XD
 } mjhipData;
 
@@ -319,15 +325,18 @@ MJHIP_API void* mjhip_mirrorDevicePtr(mjhipContext* c, const char* field);
 /* per-instance status words of the last call (device pointer, B ints) */
 MJHIP_API int mjhip_statusDownload(mjhipContext* c, int first, int count, int* dst);
 
-/* Batched mjd_inverseFD (engine_derivative_fd.c:611-719) with flg_actuation = 0 and no
- * sensor outputs: for each of B base states, forward differences with step eps of
- * qfrc_inverse w.r.t. qacc (DfDa), qvel (DfDv) and qpos (DfDq, via mj_integratePos),
- * each nv x nv in the reference's transposed layout, plus DmDq (nv x nM) if non-NULL.
- * Outputs are B x nv x nv row-major (host pointers unless MJHIP_FLAG_DEVICE_PTRS). */
+/* Batched mjd_inverseFD (engine_derivative_fd.c:611-719, mujoco.h:1244-1247) with
+ * flg_actuation = 0: for each of B base states, forward differences with step eps of
+ * qfrc_inverse w.r.t. qacc (DfDa), qvel (DfDv) and qpos (DfDq, via mj_integratePos), each
+ * nv x nv in the reference's transposed layout; of sensordata (DsDq/DsDv/DsDa, nv x
+ * nsensordata, sensors skipped when all three are NULL); of qM (DmDq, nv x nM). Every
+ * output may be NULL. Per base state the outputs are consecutive (B x nv x n row-major);
+ * host pointers unless MJHIP_FLAG_DEVICE_PTRS. Same argument order as the reference. */
 MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B,
                                    const mjtNum* qpos, const mjtNum* qvel, const mjtNum* qacc,
                                    mjtNum eps, mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa,
-                                   mjtNum* DmDq, int flags);
+                                   mjtNum* DsDq, mjtNum* DsDv, mjtNum* DsDa, mjtNum* DmDq,
+                                   int flags);
 
 /* Time `reps` back-to-back launches of the fused inverse kernel on the context's stream
  * with HIP events (device-resident mirror inputs, B instances). Writes the average

@@ -39,7 +39,9 @@
   XS(ngravcomp)   \
   XS(nexclude)    \
   XS(nkey)        \
-  XS(ntree)
+  XS(ntree)       \
+  XS(nsensor)     \
+  XS(nsensordata)
 
 /* model arrays that live in mjModel in the reference (mjxmacro.h MJMODEL_POINTERS) */
 #define MJHIP_MODEL_POINTERS_M \
@@ -168,6 +170,16 @@
   X(mjtNum,  actuator_length0,     nu,        1) \
   X(mjtNum,  actuator_acc0,        nu,        1) \
   X(int,     exclude_signature,    nexclude,  1) \
+  X(int,     sensor_type,          nsensor,   1) \
+  X(int,     sensor_datatype,      nsensor,   1) \
+  X(int,     sensor_needstage,     nsensor,   1) \
+  X(int,     sensor_objtype,       nsensor,   1) \
+  X(int,     sensor_objid,         nsensor,   1) \
+  X(int,     sensor_reftype,       nsensor,   1) \
+  X(int,     sensor_refid,         nsensor,   1) \
+  X(int,     sensor_dim,           nsensor,   1) \
+  X(int,     sensor_adr,           nsensor,   1) \
+  X(mjtNum,  sensor_cutoff,        nsensor,   1) \
   X(mjtNum,  key_qpos,             nkey,      MJ_M(nq))
 
 /* model-constant sparse structures that live in mjData in the reference
@@ -241,9 +253,12 @@
   XD(qfrc_passive,      nv,      1,   2) \
   XD(qfrc_bias,         nv,      1,   2)
 
+/* sensordata is written by mj_sensorPos/Vel/Acc in the stage each sensor needs
+ * (engine_inverse.c:203-242); listed with the acceleration stage for the W accounting */
 #define MJHIP_DATA_ACCELERATION \
   XD(qfrc_constraint,   nv,      1,   3) \
-  XD(qfrc_inverse,      nv,      1,   3)
+  XD(qfrc_inverse,      nv,      1,   3) \
+  XD(sensordata,        nsensordata, 1, 3)
 
 #define MJHIP_DATA_FIELDS \
   MJHIP_DATA_INPUTS       \
@@ -263,5 +278,17 @@
   XD(qfrc_actuator,     nv,      1,   5) \
   XD(qfrc_smooth,       nv,      1,   5) \
   XD(qacc_smooth,       nv,      1,   5)
+
+/* mjData fields the sensor stages compute on demand (stage 6): mj_subtreeVel
+ * (engine_core_smooth.c:1900-1958) for subtreelinvel/subtreeangmom sensors and
+ * mj_rnePostConstraint (:2027-2181) for accelerometer/force/torque/framelin/angacc sensors
+ * (engine_sensor.c:552-561, :712-723). Host data (mjhipData) only; on the device they are
+ * scratch fields sized only for models whose sensors need them. */
+#define MJHIP_DATA_SENSOR_AUX \
+  XD(subtree_linvel,    nbody,   3,   6) \
+  XD(subtree_angmom,    nbody,   3,   6) \
+  XD(cacc,              nbody,   6,   6) \
+  XD(cfrc_int,          nbody,   6,   6) \
+  XD(cfrc_ext,          nbody,   6,   6)
 
 #endif  /* MJHIP_FIELDS_H_ */

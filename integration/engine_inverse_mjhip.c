@@ -43,6 +43,7 @@ static const mjhipModel* model_view(const mjModel* m, const mjData* d) {
   hm->opt.impratio = m->opt.impratio;
   memcpy(hm->opt.gravity, m->opt.gravity, sizeof(hm->opt.gravity));
   memcpy(hm->opt.wind, m->opt.wind, sizeof(hm->opt.wind));
+  memcpy(hm->opt.magnetic, m->opt.magnetic, sizeof(hm->opt.magnetic));
   hm->opt.density = m->opt.density;
   hm->opt.viscosity = m->opt.viscosity;
   hm->opt.o_margin = m->opt.o_margin;

@@ -112,6 +112,8 @@ def fast_path_supported(m) -> str | None:
     return "mocap/activations"
   if m.opt["density"] > 0 or m.opt["viscosity"] > 0:
     return "fluid"
+  if m.sizes.get("nsensor", 0) and not (m.opt["disableflags"] & (1 << 12)):
+    return "sensors (mj_sensorPos/Vel/Acc run on the generic kernel)"
   return None
 
 

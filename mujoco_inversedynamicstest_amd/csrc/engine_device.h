@@ -45,6 +45,37 @@ __device__ unsigned long long mjh_phase_acc[32];
 #define MJH_PHASE(k) do {} while (0)
 #endif
 
+// mjtSensor values (include/mujoco/mjmodel.h)
+enum { mjhSENS_TOUCH = 0, mjhSENS_ACCELEROMETER, mjhSENS_VELOCIMETER, mjhSENS_GYRO,
+       mjhSENS_FORCE, mjhSENS_TORQUE, mjhSENS_MAGNETOMETER, mjhSENS_RANGEFINDER,
+       mjhSENS_CAMPROJECTION, mjhSENS_JOINTPOS, mjhSENS_JOINTVEL, mjhSENS_TENDONPOS,
+       mjhSENS_TENDONVEL, mjhSENS_ACTUATORPOS, mjhSENS_ACTUATORVEL, mjhSENS_ACTUATORFRC,
+       mjhSENS_JOINTACTFRC, mjhSENS_BALLQUAT, mjhSENS_BALLANGVEL, mjhSENS_JOINTLIMITPOS,
+       mjhSENS_JOINTLIMITVEL, mjhSENS_JOINTLIMITFRC, mjhSENS_TENDONLIMITPOS,
+       mjhSENS_TENDONLIMITVEL, mjhSENS_TENDONLIMITFRC, mjhSENS_FRAMEPOS, mjhSENS_FRAMEQUAT,
+       mjhSENS_FRAMEXAXIS, mjhSENS_FRAMEYAXIS, mjhSENS_FRAMEZAXIS, mjhSENS_FRAMELINVEL,
+       mjhSENS_FRAMEANGVEL, mjhSENS_FRAMELINACC, mjhSENS_FRAMEANGACC, mjhSENS_SUBTREECOM,
+       mjhSENS_SUBTREELINVEL, mjhSENS_SUBTREEANGMOM, mjhSENS_GEOMDIST, mjhSENS_GEOMNORMAL,
+       mjhSENS_GEOMFROMTO, mjhSENS_E_POTENTIAL, mjhSENS_E_KINETIC, mjhSENS_CLOCK };
+
+// 1 when some sensor needs mj_subtreeVel (engine_sensor.c:552-561) / mj_rnePostConstraint
+// (:712-723): their mjData outputs are then allocated as scratch
+MJH_HD int mjh_needSubtreeVel(const mjhipModel* m) {
+  for (int i = 0; i < m->nsensor; i++) {
+    const int t = m->sensor_type[i];
+    if (t == mjhSENS_SUBTREELINVEL || t == mjhSENS_SUBTREEANGMOM) return 1;
+  }
+  return 0;
+}
+MJH_HD int mjh_needRnePost(const mjhipModel* m) {
+  for (int i = 0; i < m->nsensor; i++) {
+    const int t = m->sensor_type[i];
+    if (t == mjhSENS_ACCELEROMETER || t == mjhSENS_FORCE || t == mjhSENS_TORQUE ||
+        t == mjhSENS_FRAMELINACC || t == mjhSENS_FRAMEANGACC) return 1;
+  }
+  return 0;
+}
+
 // 1 when mj_discreteAcc runs the implicit integrator (its mjd_rne_vel scratch is allocated)
 MJH_HD int mjh_implicit(const mjhipModel* m) {
   return (m->opt.enableflags & mjhipENBL_INVDISCRETE) && m->opt.integrator == mjhipINT_IMPLICIT;
@@ -81,6 +112,12 @@ struct SP {
   XSC(qforce, nv)                     \
   XSC(qacc_save, nv)                  \
   XSC(energy, 2)                      /* mjData energy (mjENBL_ENERGY) */ \
+  XSC(time, (m->nsensor > 0))         /* mjData time (clock sensors) */ \
+  XSC(subtree_linvel, mjh_needSubtreeVel(m)*3*m->nbody) \
+  XSC(subtree_angmom, mjh_needSubtreeVel(m)*3*m->nbody) \
+  XSC(body_vel, mjh_needSubtreeVel(m)*6*m->nbody)       \
+  XSC(cfrc_int, mjh_needRnePost(m)*6*m->nbody)          \
+  XSC(cfrc_ext, mjh_needRnePost(m)*6*m->nbody)          \
   XSC(qDeriv, mjh_implicit(m)*m->nD)  \
   XSC(qLU, mjh_implicit(m)*m->nD)     \
   XSC(Dcvel, mjh_implicit(m)*6*m->nB) \
@@ -2557,19 +2594,451 @@ MJH_HD void energyVel(const mjhipModel& m, const Lane<S>& d) {
   d.energy[1] = 0.5*dot(d.qforce, d.qvel, m.nv);
 }
 
+//---------------------------------- engine_sensor.c (sensors) ------------------------------
+
+// engine_util_blas.c:179-188
+template <class R, class M, class V> MJH_HD void mulMatTVec3(R res, M mat, V vec) {
+  const double t0 = mat[0]*vec[0] + mat[3]*vec[1] + mat[6]*vec[2];
+  const double t1 = mat[1]*vec[0] + mat[4]*vec[1] + mat[7]*vec[2];
+  const double t2 = mat[2]*vec[0] + mat[5]*vec[1] + mat[8]*vec[2];
+  res[0] = t0; res[1] = t1; res[2] = t2;
+}
+
+// engine_util_spatial.c:495-523; rot may be null (no rotation)
+template <class R, class V, class P, class O, class M>
+MJH_HD void transformSpatial(R res, V vec, int flg_force, P newpos, O oldpos, M rot,
+                             bool has_rot) {
+  double cros[3], dif[3], tran[6];
+  for (int i = 0; i < 6; i++) tran[i] = vec[i];
+  sub3(dif, newpos, oldpos);
+  if (flg_force) {
+    double f[3] = {vec[3], vec[4], vec[5]};
+    cross(cros, dif, f);
+    double t[3] = {vec[0], vec[1], vec[2]};
+    sub3(tran, t, cros);
+  } else {
+    double w[3] = {vec[0], vec[1], vec[2]};
+    cross(cros, dif, w);
+    double t[3] = {vec[3], vec[4], vec[5]};
+    sub3(tran + 3, t, cros);
+  }
+  if (has_rot) {
+    mulMatTVec3(res, rot, tran);
+    double r[3];
+    mulMatTVec3(r, rot, tran + 3);
+    res[3] = r[0]; res[4] = r[1]; res[5] = r[2];
+  } else {
+    for (int i = 0; i < 6; i++) res[i] = tran[i];
+  }
+}
+
+// frame (pos, rot) and body of a sensorized object (mjtObj body/xbody/geom/site/camera):
+// the switch of mj_objectVelocity (engine_support.c:1265-1312) and get_xpos_xmat
+// (engine_sensor.c:69-94)
+template <int S>
+MJH_HD int objFrame(const mjhipModel& m, const Lane<S>& d, int type, int id, SP<S>& pos,
+                    SP<S>& mat) {
+  switch (type) {
+  case 1: pos = d.xipos + 3*id; mat = d.ximat + 9*id; return id;
+  case 2: pos = d.xpos + 3*id; mat = d.xmat + 9*id; return id;
+  case 5: pos = d.geom_xpos + 3*id; mat = d.geom_xmat + 9*id; return m.geom_bodyid[id];
+  case 6: pos = d.site_xpos + 3*id; mat = d.site_xmat + 9*id; return m.site_bodyid[id];
+  default: pos = d.cam_xpos + 3*id; mat = d.cam_xmat + 9*id; return m.cam_bodyid[id];
+  }
+}
+
+// engine_support.c:1265-1312
+template <int S, class R>
+MJH_HD void objectVelocity(const mjhipModel& m, const Lane<S>& d, int type, int id, R res,
+                           int flg_local) {
+  SP<S> pos, mat;
+  const int b = objFrame(m, d, type, id, pos, mat);
+  transformSpatial(res, d.cvel + 6*b, 0, pos, d.subtree_com + 3*m.body_rootid[b], mat,
+                   flg_local != 0);
+}
+
+// engine_support.c:1317-1371
+template <int S, class R>
+MJH_HD void objectAcceleration(const mjhipModel& m, const Lane<S>& d, int type, int id, R res,
+                               int flg_local) {
+  SP<S> pos, mat;
+  double correction[3], vel[6];
+  const int b = objFrame(m, d, type, id, pos, mat);
+  SP<S> com = d.subtree_com + 3*m.body_rootid[b];
+  transformSpatial(vel, d.cvel + 6*b, 0, pos, com, mat, flg_local != 0);
+  transformSpatial(res, d.cacc + 6*b, 0, pos, com, mat, flg_local != 0);
+  cross(correction, vel, vel + 3);
+  res[3] += correction[0]; res[4] += correction[1]; res[5] += correction[2];
+}
+
+// engine_sensor.c:96-118 get_xquat
+template <int S>
+MJH_HD void objQuat(const mjhipModel& m, const Lane<S>& d, int type, int id, double q[4]) {
+  switch (type) {
+  case 2: copy4(q, d.xquat + 4*id); break;
+  case 1: mulQuat(q, d.xquat + 4*id, m.body_iquat + 4*id); break;
+  case 5: mulQuat(q, d.xquat + 4*m.geom_bodyid[id], m.geom_quat + 4*id); break;
+  case 6: mulQuat(q, d.xquat + 4*m.site_bodyid[id], m.site_quat + 4*id); break;
+  default: mulQuat(q, d.xquat + 4*m.cam_bodyid[id], m.cam_quat + 4*id); break;
+  }
+}
+
+// engine_core_smooth.c:1900-1958
+template <int S>
+MJH_HD void subtreeVel(const mjhipModel& m, const Lane<S>& d) {
+  const int nbody = m.nbody;
+  double dx[3], dv[3], dp[3], dL[3];
+  for (int i = 0; i < nbody; i++) {
+    double bv[6];
+    objectVelocity(m, d, 1, i, bv, 0);
+    for (int k = 0; k < 6; k++) d.body_vel[6*i + k] = bv[k];
+    scl3(d.subtree_linvel + 3*i, bv + 3, m.body_mass[i]);
+    mulMatTVec3(dv, d.ximat + 9*i, bv);
+    dv[0] *= m.body_inertia[3*i];
+    dv[1] *= m.body_inertia[3*i+1];
+    dv[2] *= m.body_inertia[3*i+2];
+    mulMatVec3(d.subtree_angmom + 3*i, d.ximat + 9*i, dv);
+  }
+  for (int i = nbody-1; i >= 0; i--) {
+    if (i) addTo3(d.subtree_linvel + 3*m.body_parentid[i], d.subtree_linvel + 3*i);
+    const double sm = m.body_subtreemass[i];
+    scl3(d.subtree_linvel + 3*i, d.subtree_linvel + 3*i, 1/(sm > MINVAL ? sm : MINVAL));
+  }
+  for (int i = nbody-1; i > 0; i--) {
+    const int parent = m.body_parentid[i];
+    sub3(dx, d.xipos + 3*i, d.subtree_com + 3*i);
+    sub3(dv, d.body_vel + 6*i + 3, d.subtree_linvel + 3*i);
+    scl3(dp, dv, m.body_mass[i]);
+    cross(dL, dx, dp);
+    addTo3(d.subtree_angmom + 3*i, dL);
+    addTo3(d.subtree_angmom + 3*parent, d.subtree_angmom + 3*i);
+    sub3(dx, d.subtree_com + 3*i, d.subtree_com + 3*parent);
+    sub3(dv, d.subtree_linvel + 3*i, d.subtree_linvel + 3*parent);
+    scl3(dv, dv, m.body_subtreemass[i]);
+    cross(dL, dx, dv);
+    addTo3(d.subtree_angmom + 3*parent, dL);
+  }
+}
+
+// engine_core_smooth.c:2027-2181 mj_rnePostConstraint: cacc, cfrc_int, cfrc_ext (contact
+// forces via mj_contactForce / mju_decodePyramid, engine_support.c:1459-1480,
+// engine_util_misc.c:830-850; no equality constraints in the supported subset)
+template <int S>
+MJH_HD void rnePostConstraint(const mjhipModel& m, const Lane<S>& d) {
+  const int nbody = m.nbody;
+  double cfrc_com[6], cfrc[6], lfrc[6];
+  zero(d.cacc, 6);
+  if (!(m.opt.disableflags & mjhipDSBL_GRAVITY)) {
+    d.cacc[3] = m.opt.gravity[0]*-1; d.cacc[4] = m.opt.gravity[1]*-1;
+    d.cacc[5] = m.opt.gravity[2]*-1;
+  }
+  zero(d.cfrc_ext, 6*nbody);
+  for (int i = 1; i < nbody; i++) {
+    SP<S> xf = d.xfrc_applied + 6*i;
+    bool nz = false;
+    for (int k = 0; k < 6; k++) nz |= (xf[k] != 0);
+    if (nz) {
+      cfrc[0] = xf[3]; cfrc[1] = xf[4]; cfrc[2] = xf[5];
+      cfrc[3] = xf[0]; cfrc[4] = xf[1]; cfrc[5] = xf[2];
+      transformSpatial(cfrc_com, cfrc, 1, d.subtree_com + 3*m.body_rootid[i], d.xipos + 3*i,
+                       cfrc, false);
+      addTo(d.cfrc_ext + 6*i, cfrc_com, 6);
+    }
+  }
+  const int ncon = d.con_cap ? d.con_count[0] : 0;
+  for (int i = 0; i < ncon; i++) {
+    const int adr = d.con_efc_address[i];
+    const int g0 = d.con_geom[2*i], g1 = d.con_geom[2*i + 1];
+    if (adr < 0 || g0 < 0 || g1 < 0) continue;
+    zero(lfrc, 6);
+    const int dim = d.con_dim[i];
+    if (dim == 1) {
+      lfrc[0] = d.efc_force[adr];
+    } else {
+      lfrc[0] = 0;
+      for (int k = 0; k < 2*(dim-1); k++) lfrc[0] += d.efc_force[adr + k];
+      for (int k = 0; k < dim-1; k++) {
+        lfrc[k+1] = (d.efc_force[adr + 2*k] - d.efc_force[adr + 2*k + 1]) * d.con_friction[5*i + k];
+      }
+    }
+    SP<S> frame = d.con_frame + 9*i;
+    mulMatTVec3(cfrc, frame, lfrc + 3);
+    double t[3];
+    mulMatTVec3(t, frame, lfrc);
+    cfrc[3] = t[0]; cfrc[4] = t[1]; cfrc[5] = t[2];
+    int k;
+    if ((k = m.geom_bodyid[g0])) {
+      transformSpatial(cfrc_com, cfrc, 1, d.subtree_com + 3*m.body_rootid[k], d.con_pos + 3*i,
+                       cfrc, false);
+      subFrom(d.cfrc_ext + 6*k, cfrc_com, 6);
+    }
+    if ((k = m.geom_bodyid[g1])) {
+      transformSpatial(cfrc_com, cfrc, 1, d.subtree_com + 3*m.body_rootid[k], d.con_pos + 3*i,
+                       cfrc, false);
+      addTo(d.cfrc_ext + 6*k, cfrc_com, 6);
+    }
+  }
+  double cacc[6], cfrc_body[6], cfrc_corr[6];
+  zero(d.cfrc_int, 6);
+  for (int j = 1; j < nbody; j++) {
+    const int bda = m.body_dofadr[j];
+    mulDofVec(cacc, d.cdof_dot + 6*bda, d.qvel + bda, m.body_dofnum[j]);
+    add(d.cacc + 6*j, d.cacc + 6*m.body_parentid[j], cacc, 6);
+    mulDofVec(cacc, d.cdof + 6*bda, d.qacc + bda, m.body_dofnum[j]);
+    addTo(d.cacc + 6*j, cacc, 6);
+    mulInertVec(cfrc_body, d.cinert + 10*j, d.cacc + 6*j);
+    mulInertVec(cfrc_corr, d.cinert + 10*j, d.cvel + 6*j);
+    crossForce(cfrc, d.cvel + 6*j, cfrc_corr);
+    addTo(cfrc_body, cfrc, 6);
+    for (int k = 0; k < 6; k++) d.cfrc_int[6*j + k] = cfrc_body[k] - d.cfrc_ext[6*j + k];
+  }
+  for (int j = nbody-1; j > 0; j--) {
+    addTo(d.cfrc_int + 6*m.body_parentid[j], d.cfrc_int + 6*j, 6);
+  }
+}
+
+// engine_sensor.c:38-66
+template <int S>
+MJH_HD void applyCutoff(const mjhipModel& m, const Lane<S>& d, int stage) {
+  for (int i = 0; i < m.nsensor; i++) {
+    if (m.sensor_needstage[i] == stage && m.sensor_cutoff[i] > 0) {
+      const int adr = m.sensor_adr[i], dim = m.sensor_dim[i];
+      const double cutoff = m.sensor_cutoff[i];
+      for (int j = 0; j < dim; j++) {
+        const double x = d.sensordata[adr + j];
+        if (m.sensor_datatype[i] == 0) {
+          d.sensordata[adr + j] = x < -cutoff ? -cutoff : (x > cutoff ? cutoff : x);
+        } else if (m.sensor_datatype[i] == 1) {
+          d.sensordata[adr + j] = cutoff < x ? cutoff : x;
+        }
+      }
+    }
+  }
+}
+
+// first limit row of (type, id) among rows ne+nf..nefc (engine_sensor.c:286-304); -1 if none
+template <int S>
+MJH_HD int limitRow(const Lane<S>& d, int type, int id) {
+  const int nefc = d.efc_count[0], start = d.efc_count[1] + d.efc_count[2];
+  for (int j = start; j < nefc; j++) {
+    if (d.efc_type[j] == type && d.efc_id[j] == id) return j;
+  }
+  return -1;
+}
+
+// engine_sensor.c:209-513 mj_sensorPos (no rangefinder/camprojection/geom distance/user,
+// rejected at load)
+template <int S>
+MJH_HD void sensorPos(const mjhipModel& m, const Lane<S>& d) {
+  if (m.opt.disableflags & mjhipDSBL_SENSOR) return;
+  for (int i = 0; i < m.nsensor; i++) {
+    if (m.sensor_needstage[i] != mjhipSTAGE_POS) continue;
+    const int type = m.sensor_type[i], objtype = m.sensor_objtype[i];
+    const int objid = m.sensor_objid[i], refid = m.sensor_refid[i];
+    const int reftype = m.sensor_reftype[i];
+    SP<S> out = d.sensordata + m.sensor_adr[i];
+    SP<S> xpos, xmat, xpos_ref, xmat_ref;
+    double rvec[3];
+    int r;
+    switch (type) {
+    case mjhSENS_MAGNETOMETER:
+      mulMatTVec(out, d.site_xmat + 9*objid, m.opt.magnetic, 3, 3);
+      break;
+    case mjhSENS_JOINTPOS: out[0] = d.qpos[m.jnt_qposadr[objid]]; break;
+    case mjhSENS_TENDONPOS: out[0] = d.ten_length[objid]; break;
+    case mjhSENS_ACTUATORPOS: out[0] = d.actuator_length[objid]; break;
+    case mjhSENS_BALLQUAT: {
+      double q[4];
+      copy4(q, d.qpos + m.jnt_qposadr[objid]);
+      normalize4(q);
+      copy4(out, q);
+      break;
+    }
+    case mjhSENS_JOINTLIMITPOS:
+    case mjhSENS_TENDONLIMITPOS:
+      out[0] = 0;
+      r = limitRow(d, type == mjhSENS_JOINTLIMITPOS ? CNSTR_LIMIT_JOINT : CNSTR_LIMIT_TENDON,
+                   objid);
+      if (r >= 0) out[0] = d.efc_pos[r] - d.efc_margin[r];
+      break;
+    case mjhSENS_FRAMEPOS:
+    case mjhSENS_FRAMEXAXIS:
+    case mjhSENS_FRAMEYAXIS:
+    case mjhSENS_FRAMEZAXIS:
+      objFrame(m, d, objtype, objid, xpos, xmat);
+      if (refid == -1) {
+        if (type == mjhSENS_FRAMEPOS) {
+          copy3(out, xpos);
+        } else {
+          const int off = type - mjhSENS_FRAMEXAXIS;
+          out[0] = xmat[off]; out[1] = xmat[off + 3]; out[2] = xmat[off + 6];
+        }
+      } else {
+        objFrame(m, d, reftype, refid, xpos_ref, xmat_ref);
+        if (type == mjhSENS_FRAMEPOS) {
+          sub3(rvec, xpos, xpos_ref);
+          mulMatTVec3(out, xmat_ref, rvec);
+        } else {
+          const int off = type - mjhSENS_FRAMEXAXIS;
+          double axis[3] = {xmat[off], xmat[off + 3], xmat[off + 6]};
+          mulMatTVec3(out, xmat_ref, axis);
+        }
+      }
+      break;
+    case mjhSENS_FRAMEQUAT: {
+      double objquat[4], refquat[4], q[4];
+      objQuat(m, d, objtype, objid, objquat);
+      if (refid == -1) {
+        copy4(out, objquat);
+      } else {
+        objQuat(m, d, reftype, refid, refquat);
+        refquat[1] = -refquat[1]; refquat[2] = -refquat[2]; refquat[3] = -refquat[3];
+        mulQuat(q, refquat, objquat);
+        copy4(out, q);
+      }
+      break;
+    }
+    case mjhSENS_SUBTREECOM: copy3(out, d.subtree_com + 3*objid); break;
+    case mjhSENS_E_POTENTIAL: energyPos(m, d); out[0] = d.energy[0]; break;
+    case mjhSENS_E_KINETIC: energyVel(m, d); out[0] = d.energy[1]; break;
+    case mjhSENS_CLOCK: out[0] = d.time[0]; break;
+    default: break;
+    }
+  }
+  applyCutoff(m, d, mjhipSTAGE_POS);
+}
+
+// engine_sensor.c:521-672 mj_sensorVel
+template <int S>
+MJH_HD void sensorVel(const mjhipModel& m, const Lane<S>& d) {
+  if (m.opt.disableflags & mjhipDSBL_SENSOR) return;
+  bool subtree = false;
+  double xvel[6];
+  for (int i = 0; i < m.nsensor; i++) {
+    if (m.sensor_needstage[i] != mjhipSTAGE_VEL) continue;
+    const int type = m.sensor_type[i], objtype = m.sensor_objtype[i];
+    const int objid = m.sensor_objid[i], refid = m.sensor_refid[i];
+    const int reftype = m.sensor_reftype[i];
+    SP<S> out = d.sensordata + m.sensor_adr[i];
+    int r;
+    if (!subtree && (type == mjhSENS_SUBTREELINVEL || type == mjhSENS_SUBTREEANGMOM)) {
+      subtreeVel(m, d);
+      subtree = true;
+    }
+    switch (type) {
+    case mjhSENS_VELOCIMETER:
+      objectVelocity(m, d, 6, objid, xvel, 1);
+      copy3(out, xvel + 3);
+      break;
+    case mjhSENS_GYRO:
+      objectVelocity(m, d, 6, objid, xvel, 1);
+      copy3(out, xvel);
+      break;
+    case mjhSENS_JOINTVEL: out[0] = d.qvel[m.jnt_dofadr[objid]]; break;
+    case mjhSENS_TENDONVEL: out[0] = d.ten_velocity[objid]; break;
+    case mjhSENS_ACTUATORVEL: out[0] = d.actuator_velocity[objid]; break;
+    case mjhSENS_BALLANGVEL: copy3(out, d.qvel + m.jnt_dofadr[objid]); break;
+    case mjhSENS_JOINTLIMITVEL:
+    case mjhSENS_TENDONLIMITVEL:
+      out[0] = 0;
+      r = limitRow(d, type == mjhSENS_JOINTLIMITVEL ? CNSTR_LIMIT_JOINT : CNSTR_LIMIT_TENDON,
+                   objid);
+      if (r >= 0) out[0] = d.efc_vel[r];
+      break;
+    case mjhSENS_FRAMELINVEL:
+    case mjhSENS_FRAMEANGVEL:
+      objectVelocity(m, d, objtype, objid, xvel, 0);
+      if (refid > -1) {
+        SP<S> xpos, xmat, xpos_ref, xmat_ref;
+        double xvel_ref[6], rel_vel[6], crs[3], rvec[3];
+        objFrame(m, d, objtype, objid, xpos, xmat);
+        objFrame(m, d, reftype, refid, xpos_ref, xmat_ref);
+        objectVelocity(m, d, reftype, refid, xvel_ref, 0);
+        for (int k = 0; k < 6; k++) rel_vel[k] = xvel[k] - xvel_ref[k];
+        sub3(rvec, xpos, xpos_ref);
+        cross(crs, rvec, xvel_ref);
+        addTo3(rel_vel + 3, crs);
+        mulMatTVec3(xvel, xmat_ref, rel_vel);
+        mulMatTVec3(xvel + 3, xmat_ref, rel_vel + 3);
+      }
+      copy3(out, type == mjhSENS_FRAMELINVEL ? xvel + 3 : xvel);
+      break;
+    case mjhSENS_SUBTREELINVEL: copy3(out, d.subtree_linvel + 3*objid); break;
+    case mjhSENS_SUBTREEANGMOM: copy3(out, d.subtree_angmom + 3*objid); break;
+    default: break;
+    }
+  }
+  applyCutoff(m, d, mjhipSTAGE_VEL);
+}
+
+// engine_sensor.c:677-915 mj_sensorAcc (no touch, rejected at load)
+template <int S>
+MJH_HD void sensorAcc(const mjhipModel& m, const Lane<S>& d) {
+  if (m.opt.disableflags & mjhipDSBL_SENSOR) return;
+  bool post = false;
+  double tmp[6];
+  for (int i = 0; i < m.nsensor; i++) {
+    if (m.sensor_needstage[i] != mjhipSTAGE_ACC) continue;
+    const int type = m.sensor_type[i], objtype = m.sensor_objtype[i];
+    const int objid = m.sensor_objid[i];
+    SP<S> out = d.sensordata + m.sensor_adr[i];
+    int r;
+    if (!post && (type == mjhSENS_ACCELEROMETER || type == mjhSENS_FORCE ||
+                  type == mjhSENS_TORQUE || type == mjhSENS_FRAMELINACC ||
+                  type == mjhSENS_FRAMEANGACC)) {
+      rnePostConstraint(m, d);
+      post = true;
+    }
+    switch (type) {
+    case mjhSENS_ACCELEROMETER:
+      objectAcceleration(m, d, 6, objid, tmp, 1);
+      copy3(out, tmp + 3);
+      break;
+    case mjhSENS_FORCE:
+    case mjhSENS_TORQUE: {
+      const int bodyid = m.site_bodyid[objid], rootid = m.body_rootid[bodyid];
+      transformSpatial(tmp, d.cfrc_int + 6*bodyid, 1, d.site_xpos + 3*objid,
+                       d.subtree_com + 3*rootid, d.site_xmat + 9*objid, true);
+      copy3(out, type == mjhSENS_FORCE ? tmp + 3 : tmp);
+      break;
+    }
+    case mjhSENS_ACTUATORFRC: out[0] = d.actuator_force[objid]; break;
+    case mjhSENS_JOINTACTFRC: out[0] = d.qfrc_actuator[m.jnt_dofadr[objid]]; break;
+    case mjhSENS_JOINTLIMITFRC:
+    case mjhSENS_TENDONLIMITFRC:
+      out[0] = 0;
+      r = limitRow(d, type == mjhSENS_JOINTLIMITFRC ? CNSTR_LIMIT_JOINT : CNSTR_LIMIT_TENDON,
+                   objid);
+      if (r >= 0) out[0] = d.efc_force[r];
+      break;
+    case mjhSENS_FRAMELINACC:
+    case mjhSENS_FRAMEANGACC:
+      objectAcceleration(m, d, objtype, objid, tmp, 0);
+      copy3(out, type == mjhSENS_FRAMELINACC ? tmp + 3 : tmp);
+      break;
+    default: break;
+    }
+  }
+  applyCutoff(m, d, mjhipSTAGE_ACC);
+}
+
 // FUSED (the constraint rows finished at creation, see contactRowsFused) requires
 // skipstage = mjSTAGE_NONE, no mjENBL_INVDISCRETE, nbody <= 64 and d.chain set (fusedOk)
 template <int S, bool CONTACT = true, bool FUSED = false>
-MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
+MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage,
+                       int skipsensor = 0) {
   int status = 0;
   const bool energy = (m.opt.enableflags & mjhipENBL_ENERGY) != 0;
+  const bool sensors = !skipsensor && m.nsensor > 0;
   if (skipstage < mjhipSTAGE_POS) {
     invPosition<S, CONTACT, FUSED>(m, d, &status);
+    if (sensors) sensorPos(m, d);
     if (energy) energyPos(m, d);
   }
   MJH_PHASE(6);
   if (skipstage < mjhipSTAGE_VEL) {
     invVelocity<S, FUSED>(m, d);
+    if (sensors) sensorVel(m, d);
     if (energy) energyVel(m, d);
   }
   MJH_PHASE(7);
@@ -2581,6 +3050,7 @@ MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
   if constexpr (!FUSED) invConstraint(m, d);
   MJH_PHASE(8);
   rne(m, d, 1, d.qfrc_inverse);
+  if (sensors) sensorAcc(m, d);
   for (int i = 0; i < m.nv; i++) {
     d.qfrc_inverse[i] += m.dof_armature[i] * d.qacc[i]
                          - d.qfrc_passive[i] - d.qfrc_constraint[i];

@@ -113,7 +113,7 @@ __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
                                                 const double* __restrict__ qvel_in,
                                                 const double* __restrict__ qacc_in,
                                                 double* __restrict__ qfrc_out,
-                                                int* __restrict__ status) {
+                                                int* __restrict__ status, int skipsensor) {
   MJHIP_CHAIN_TABLE(FUSED)
   const int blk = blockIdx.x, lane = threadIdx.x;
   const long inst = (long)blk*64 + lane;
@@ -131,7 +131,7 @@ __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
     for (int k = 0; k < m.nv; k++) d.qacc[k] = qacc_in[inst*m.nv + k];
   }
   MJH_PHASE(0);
-  int st = mjh::inverseSkip<64, CONTACT, FUSED>(m, d, SKIP);
+  int st = mjh::inverseSkip<64, CONTACT, FUSED>(m, d, SKIP, skipsensor);
   if (qfrc_out) {
     for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
   }
@@ -200,9 +200,15 @@ __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __
 }
 
 // diff(): DfD*[b][i][:] = (f(perturbed) - f(centre)) / eps  (engine_derivative_fd.c:48-53)
+// Sensor rows follow the reference's stage skipping: a qacc perturbation runs
+// mj_inverseSkip(mjSTAGE_VEL), so only acceleration-stage sensors change and the others keep
+// the centre's values (their difference is exactly 0); a qvel perturbation runs
+// mjSTAGE_POS, so position-stage sensors keep theirs (engine_derivative_fd.c:646-699).
 __global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps,
                           double* __restrict__ DfDq, double* __restrict__ DfDv,
-                          double* __restrict__ DfDa, double* __restrict__ DmDq) {
+                          double* __restrict__ DfDa, double* __restrict__ DsDq,
+                          double* __restrict__ DsDv, double* __restrict__ DsDa,
+                          double* __restrict__ DmDq) {
   const int nv = m.nv, P = 3*nv + 1;
   long t = (long)blockIdx.x*blockDim.x + threadIdx.x;   // one thread per (b, perturbation)
   if (t >= (long)nbase*(P-1)) return;
@@ -212,18 +218,28 @@ __global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps,
   Lane<64> c = lane_view(mr, (int)(ic >> 6), (int)(ic & 63));
   Lane<64> q = lane_view(mr, (int)(ip >> 6), (int)(ip & 63));
   double inv_h = 1/eps;
-  double* out;
-  int i;
+  double *out, *sout;
+  int i, minstage;
   if (p <= nv) {
-    out = DfDa; i = p - 1;
+    out = DfDa; sout = DsDa; i = p - 1; minstage = mjhipSTAGE_ACC;
   } else if (p <= 2*nv) {
-    out = DfDv; i = p - 1 - nv;
+    out = DfDv; sout = DsDv; i = p - 1 - nv; minstage = mjhipSTAGE_VEL;
   } else {
-    out = DfDq; i = p - 1 - 2*nv;
+    out = DfDq; sout = DsDq; i = p - 1 - 2*nv; minstage = mjhipSTAGE_POS;
   }
   if (out) {
     for (int k = 0; k < nv; k++) {
       out[(b*nv + i)*nv + k] = inv_h * (q.qfrc_inverse[k] - c.qfrc_inverse[k]);
+    }
+  }
+  if (sout) {
+    const int ns = m.nsensordata;
+    for (int s = 0; s < m.nsensor; s++) {
+      const bool ran = m.sensor_needstage[s] >= minstage;
+      for (int k = m.sensor_adr[s]; k < m.sensor_adr[s] + m.sensor_dim[s]; k++) {
+        const double x1 = c.sensordata[k], x2 = ran ? q.sensordata[k] : x1;
+        sout[(b*nv + i)*ns + k] = inv_h * (x2 - x1);
+      }
     }
   }
   if (DmDq && p > 2*nv) {
@@ -330,6 +346,7 @@ static unsigned long long model_signature(const mjhipModel* m) {
   feed(&m->opt.impratio, 8);
   feed(m->opt.gravity, 24);
   feed(m->opt.wind, 24);
+  feed(m->opt.magnetic, 24);
   feed(&m->opt.density, 8);
   feed(&m->opt.viscosity, 8);
   feed(&m->opt.o_margin, 8);
@@ -378,6 +395,13 @@ static const char* unsupported(const mjhipModel* m) {
     return "a collidable geom pair needs a collision function other than plane/sphere/capsule";
   }
   if (ncon > 0 && m->opt.cone == mjhipCONE_ELLIPTIC) return "elliptic friction cones";
+  for (int i = 0; i < m->nsensor; i++) {
+    const int t = m->sensor_type[i];
+    if (t == mjhSENS_TOUCH || t == mjhSENS_RANGEFINDER || t == mjhSENS_CAMPROJECTION ||
+        (t >= mjhSENS_GEOMDIST && t <= mjhSENS_GEOMFROMTO) || t > mjhSENS_CLOCK) {
+      return "touch/rangefinder/camprojection/geom-distance/plugin/user sensors";
+    }
+  }
   return nullptr;
 }
 
@@ -606,7 +630,7 @@ MJHIP_API int mjhip_contextSetStream(mjhipContext* c, void* stream) {
 
 static int launch_inverse(mjhipContext* c, int B, const double* qpos, const double* qvel,
                           const double* qacc, double* qfrc, int skipstage, int* status,
-                          int flags = 0) {
+                          int flags = 0, int skipsensor = 0) {
   dim3 grid((B + 63) / 64), block(64);
   if (skipstage == mjhipSTAGE_NONE && c->fast && !(flags & MJHIP_FLAG_GENERIC)) {
     // two work-list counters alternate: this launch counts into `cnt` (zeroed by the
@@ -643,7 +667,7 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
 #define MJHIP_LAUNCH_K(SK, C, F)                                                              \
   hipLaunchKernelGGL((k_inverse<SK, C, F>), grid, block,                                      \
                      (C && F) ? mjh::gstageBytes(c->dmodel) : 0, c->stream, c->dmodel,        \
-                     c->mirror, B, qpos, qvel, qacc, qfrc, status)
+                     c->mirror, B, qpos, qvel, qacc, qfrc, status, skipsensor)
 #define MJHIP_LAUNCH_GENERIC(SK)                                                              \
   if (c->con_cap > 0) {                                                                       \
     MJHIP_LAUNCH_K(SK, true, false);                                                          \
@@ -677,7 +701,6 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
 MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B, const mjtNum* qpos,
                                  const mjtNum* qvel, const mjtNum* qacc, mjtNum* qfrc_inverse,
                                  int skipstage, int skipsensor, int flags, int* status) {
-  (void)skipsensor;   // no sensors in the supported subset: skipsensor has no effect
   if (!c || B < 0) {
     set_error("mjhip_inverseBatch: bad argument");
     return MJHIP_ERR_ARG;
@@ -715,7 +738,7 @@ MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B, const mjtNum* qpos,
     }
   }
   if (qfrc_inverse) dqfrc = dev ? qfrc_inverse : sf;
-  int rc = launch_inverse(c, B, dq, dv, da, dqfrc, skipstage, c->status, flags);
+  int rc = launch_inverse(c, B, dq, dv, da, dqfrc, skipstage, c->status, flags, skipsensor);
   if (rc) return rc;
   if (qfrc_inverse && !dev) {
     HIPCHECK(hipMemcpyAsync(qfrc_inverse, sf, sizeof(double)*(size_t)B*m.nv,
@@ -939,8 +962,8 @@ MJHIP_API int mjhip_timeInverseKernel(mjhipContext* c, int B, int reps, int skip
 
 MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
                                    const mjtNum* qvel, const mjtNum* qacc, mjtNum eps,
-                                   mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DmDq,
-                                   int flags) {
+                                   mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq,
+                                   mjtNum* DsDv, mjtNum* DsDa, mjtNum* DmDq, int flags) {
   if (!c || B <= 0 || !qpos || !qvel || !qacc) return MJHIP_ERR_ARG;
   const mjhipModel& m = c->hmodel;
   const int nv = m.nv, P = 3*nv + 1;
@@ -970,12 +993,15 @@ MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
   // all perturbations run the full pipeline (the reference's stage skipping is an
   // optimisation of a serial loop; results are identical because skipped stages see
   // unchanged inputs)
+  // sensors are skipped when no sensor derivative is asked for (derivative_fd.c:628)
+  const int skipsensor = !DsDq && !DsDv && !DsDa;
   int rc = launch_inverse(c, (int)ninst, nullptr, nullptr, nullptr, nullptr, mjhipSTAGE_NONE,
-                          nullptr);
+                          nullptr, 0, skipsensor);
   if (rc) return rc;
   double *oq = DfDq, *ov = DfDv, *oa = DfDa, *om = DmDq;
+  double *sq_ = DsDq, *sv_ = DsDv, *sa_ = DsDa;
   std::vector<double*> tmp;
-  size_t nn = (size_t)B*nv*nv, nm = (size_t)B*nv*m.nM;
+  size_t nn = (size_t)B*nv*nv, nm = (size_t)B*nv*m.nM, ns = (size_t)B*nv*m.nsensordata;
   if (!dev) {
     auto alloc = [&](double* h, size_t n) -> double* {
       if (!h) return nullptr;
@@ -985,16 +1011,20 @@ MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
       return d;
     };
     oq = alloc(DfDq, nn); ov = alloc(DfDv, nn); oa = alloc(DfDa, nn); om = alloc(DmDq, nm);
+    sq_ = alloc(DsDq, ns); sv_ = alloc(DsDv, ns); sa_ = alloc(DsDa, ns);
   }
   long nd = (long)B*(P-1);
   hipLaunchKernelGGL(k_fd_diff, dim3((nd + 255)/256), dim3(256), 0, c->stream, c->dmodel,
-                     c->mirror, B, eps, oq, ov, oa, om);
+                     c->mirror, B, eps, oq, ov, oa, sq_, sv_, sa_, om);
   HIPCHECK(hipGetLastError());
   if (!dev) {
     if (DfDq) HIPCHECK(hipMemcpyAsync(DfDq, oq, nn*8, hipMemcpyDeviceToHost, c->stream));
     if (DfDv) HIPCHECK(hipMemcpyAsync(DfDv, ov, nn*8, hipMemcpyDeviceToHost, c->stream));
     if (DfDa) HIPCHECK(hipMemcpyAsync(DfDa, oa, nn*8, hipMemcpyDeviceToHost, c->stream));
     if (DmDq) HIPCHECK(hipMemcpyAsync(DmDq, om, nm*8, hipMemcpyDeviceToHost, c->stream));
+    if (DsDq) HIPCHECK(hipMemcpyAsync(DsDq, sq_, ns*8, hipMemcpyDeviceToHost, c->stream));
+    if (DsDv) HIPCHECK(hipMemcpyAsync(DsDv, sv_, ns*8, hipMemcpyDeviceToHost, c->stream));
+    if (DsDa) HIPCHECK(hipMemcpyAsync(DsDa, sa_, ns*8, hipMemcpyDeviceToHost, c->stream));
     HIPCHECK(hipStreamSynchronize(c->stream));
     for (double* p : tmp) hipFree(p);
   }
@@ -1052,6 +1082,20 @@ MJHIP_API void mjhip_inverseSkip(const mjhipModel* m, mjhipData* d, int skipstag
     rc = mjhip_mirrorUpload(c, #name, 0, 1, d->name);
   MJHIP_DATA_FIELDS
 #undef XD
+  if (!rc && m->nsensor > 0) {
+    // sensor inputs: the values of skipped stages' sensors are kept (sensordata), and the
+    // mjData inputs some sensors read (clock: time; force/torque/accelerometer via
+    // mj_rnePostConstraint: xfrc_applied; actuatorfrc/jointactuatorfrc)
+    if (skipstage > mjhipSTAGE_NONE && d->sensordata)
+      rc = mjhip_mirrorUpload(c, "sensordata", 0, 1, d->sensordata);
+    if (!rc) rc = mjhip_mirrorUpload(c, "time", 0, 1, &d->time);
+    if (!rc && d->xfrc_applied && m->nbody)
+      rc = mjhip_mirrorUpload(c, "xfrc_applied", 0, 1, d->xfrc_applied);
+    if (!rc && d->actuator_force && m->nu)
+      rc = mjhip_mirrorUpload(c, "actuator_force", 0, 1, d->actuator_force);
+    if (!rc && d->qfrc_actuator && m->nv)
+      rc = mjhip_mirrorUpload(c, "qfrc_actuator", 0, 1, d->qfrc_actuator);
+  }
   if (!rc) {
     rc = mjhip_inverseBatch(c, 1, nullptr, nullptr, nullptr, nullptr, skipstage, skipsensor,
                             MJHIP_FLAG_MIRROR_INPUT, &d->status);
@@ -1063,6 +1107,14 @@ MJHIP_API void mjhip_inverseSkip(const mjhipModel* m, mjhipData* d, int skipstag
   MJHIP_DATA_FIELDS
 #undef XD
 #undef MJ_M
+  if (!rc && m->nsensor > 0 && !skipsensor) {
+    // mjData fields the sensor stages computed on demand (scratch sized 0 when unneeded)
+#define XD(name, d0, d1, stage)                                                     \
+    if (!rc && d->name && c->mirror.name##_n > 0)                                    \
+      rc = mjhip_mirrorDownload(c, #name, 0, 1, d->name);
+    MJHIP_DATA_SENSOR_AUX
+#undef XD
+  }
   if (!rc && (m->opt.enableflags & mjhipENBL_ENERGY) && skipstage < mjhipSTAGE_VEL) {
     // mj_energyPos/Vel write the energy of the stages that ran (engine_inverse.c:207-223)
     mjtNum e[2];

@@ -65,7 +65,7 @@ SIGNATURES = {
     "mjhip_mirrorFieldSize": (ctypes.c_int, [_V, ctypes.c_char_p]),
     "mjhip_statusDownload": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _I]),
     "mjhip_inverseFDBatch": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, ctypes.c_double,
-                                            _V, _V, _V, _V, ctypes.c_int]),
+                                            _V, _V, _V, _V, _V, _V, _V, ctypes.c_int]),
     "mjhip_timeInverseKernel": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_float)]),
@@ -287,36 +287,45 @@ class InverseEngine:
            "mjhip_timeInverseKernel")
     return ms.value
 
-  def inverse_fd(self, qpos, qvel, qacc, eps=1e-6, dmdq=False, out=None):
-    """Batched mjd_inverseFD (flg_actuation=0, no sensors): DfDq, DfDv, DfDa [B, nv, nv].
+  def inverse_fd(self, qpos, qvel, qacc, eps=1e-6, dmdq=False, sensors=False, out=None):
+    """Batched mjd_inverseFD (flg_actuation=0): DfDq, DfDv, DfDa [B, nv, nv], DmDq
+    [B, nv, nM] (or None), plus (DsDq, DsDv, DsDa) [B, nv, nsensordata] when sensors.
 
     Host arrays in -> numpy arrays out (PCIe both ways). Contiguous float64 torch tensors on
     the context's GPU in -> torch tensors out on that GPU, asynchronous on the context's
-    stream (out: optional preallocated (DfDq, DfDv, DfDa, DmDq) device tensors)."""
+    stream (out: optional preallocated tuple in the same order as the return value)."""
+    nv, ns = self.nv, self.m.sizes.get("nsensordata", 0)
     if _dptr(qpos) is not None:
       import torch
-      B, nv = qpos.shape[0], self.nv
+      B = qpos.shape[0]
       if out is None:
         mk = lambda n: torch.empty((B, nv, n), dtype=torch.float64, device=qpos.device)
         out = (mk(nv), mk(nv), mk(nv), mk(self.m.nM) if dmdq else None)
-      ptrs = [None if t is None else _dptr(t) for t in out]
+        if sensors:
+          out = out + ((mk(ns), mk(ns), mk(ns)),)
+      ptr = lambda t: None if t is None else _dptr(t)
+      Ds = out[4] if len(out) > 4 else (None, None, None)
       _check(lib().mjhip_inverseFDBatch(self.ctx, B, _dptr(qpos), _dptr(qvel), _dptr(qacc),
-                                        eps, *ptrs, FLAG_DEVICE_PTRS),
+                                        eps, ptr(out[0]), ptr(out[1]), ptr(out[2]),
+                                        *map(ptr, Ds), ptr(out[3]), FLAG_DEVICE_PTRS),
              "mjhip_inverseFDBatch")
       return tuple(out)
     qpos = np.ascontiguousarray(qpos, dtype=np.float64).reshape(-1, self.nq)
     qvel = np.ascontiguousarray(qvel, dtype=np.float64).reshape(-1, self.nv)
     qacc = np.ascontiguousarray(qacc, dtype=np.float64).reshape(-1, self.nv)
-    B, nv = qpos.shape[0], self.nv
+    B = qpos.shape[0]
     DfDq = np.zeros((B, nv, nv))
     DfDv = np.zeros((B, nv, nv))
     DfDa = np.zeros((B, nv, nv))
     DmDq = np.zeros((B, nv, self.m.nM)) if dmdq else None
+    Ds = tuple(np.zeros((B, nv, ns)) for _ in range(3)) if sensors else (None, None, None)
+    p = lambda a: None if a is None else a.ctypes.data
     _check(lib().mjhip_inverseFDBatch(self.ctx, B, qpos.ctypes.data, qvel.ctypes.data,
-                                      qacc.ctypes.data, eps, DfDq.ctypes.data,
-                                      DfDv.ctypes.data, DfDa.ctypes.data,
-                                      None if DmDq is None else DmDq.ctypes.data, 0),
+                                      qacc.ctypes.data, eps, p(DfDq), p(DfDv), p(DfDa),
+                                      *map(p, Ds), p(DmDq), 0),
            "mjhip_inverseFDBatch")
+    if sensors:
+      return DfDq, DfDv, DfDa, DmDq, Ds
     return DfDq, DfDv, DfDa, DmDq
 
 

@@ -76,12 +76,12 @@ def _parse():
   for group in ("MJHIP_DATA_INPUTS", "MJHIP_DATA_POSITION", "MJHIP_DATA_VELOCITY",
                 "MJHIP_DATA_ACCELERATION"):
     data += xd(group)
-  return sizes, model, data, xd("MJHIP_DATA_FORWARD")
+  return sizes, model, data, xd("MJHIP_DATA_FORWARD"), xd("MJHIP_DATA_SENSOR_AUX")
 
 
-MODEL_SIZES, MODEL_FIELDS, DATA_FIELDS, FORWARD_FIELDS = _parse()
+MODEL_SIZES, MODEL_FIELDS, DATA_FIELDS, FORWARD_FIELDS, AUX_FIELDS = _parse()
 MODEL_FIELD = {f.name: f for f in MODEL_FIELDS}
-DATA_FIELD = {f.name: f for f in DATA_FIELDS + FORWARD_FIELDS}
+DATA_FIELD = {f.name: f for f in DATA_FIELDS + FORWARD_FIELDS + AUX_FIELDS}
 
 
 class Option(ctypes.Structure):
@@ -91,6 +91,7 @@ class Option(ctypes.Structure):
       ("impratio", ctypes.c_double),
       ("gravity", ctypes.c_double * 3),
       ("wind", ctypes.c_double * 3),
+      ("magnetic", ctypes.c_double * 3),
       ("density", ctypes.c_double),
       ("viscosity", ctypes.c_double),
       ("o_margin", ctypes.c_double),
@@ -112,9 +113,11 @@ class CModel(ctypes.Structure):
 
 class CData(ctypes.Structure):
   _fields_ = ([("nefc", ctypes.c_int), ("status", ctypes.c_int),
-               ("solver_fwdinv", ctypes.c_double * 2), ("energy", ctypes.c_double * 2)] +
+               ("solver_fwdinv", ctypes.c_double * 2), ("energy", ctypes.c_double * 2),
+               ("time", ctypes.c_double)] +
               [(f.name, ctypes.POINTER(ctypes.c_double)) for f in DATA_FIELDS] +
-              [(f.name, ctypes.POINTER(ctypes.c_double)) for f in FORWARD_FIELDS])
+              [(f.name, ctypes.POINTER(ctypes.c_double)) for f in FORWARD_FIELDS] +
+              [(f.name, ctypes.POINTER(ctypes.c_double)) for f in AUX_FIELDS])
 
 
 def output_doubles(sizes: dict) -> int:
@@ -148,7 +151,7 @@ def model_signature(m) -> int:
   o = m.opt
   for k in ("timestep", "impratio"):
     feed(np.float64(o[k]).tobytes())
-  for k, n in (("gravity", 3), ("wind", 3)):
+  for k, n in (("gravity", 3), ("wind", 3), ("magnetic", 3)):
     feed(np.asarray(o[k], dtype=np.float64)[:n].tobytes())
   for k in ("density", "viscosity", "o_margin"):
     feed(np.float64(o[k]).tobytes())

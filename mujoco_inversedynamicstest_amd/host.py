@@ -22,7 +22,7 @@ def model_struct(m) -> fields.CModel:
   o = s.opt
   for k in ("timestep", "impratio", "density", "viscosity", "o_margin"):
     setattr(o, k, float(m.opt[k]))
-  for k, n in (("gravity", 3), ("wind", 3), ("o_solref", 2), ("o_solimp", 5),
+  for k, n in (("gravity", 3), ("wind", 3), ("magnetic", 3), ("o_solref", 2), ("o_solimp", 5),
                ("o_friction", 5)):
     arr = getattr(o, k)
     for i in range(n):
@@ -47,7 +47,7 @@ class MjData:
     self.m = m
     sizes = m.sizes
     self._arrays = {}
-    for f in fields.DATA_FIELDS + fields.FORWARD_FIELDS:
+    for f in fields.DATA_FIELDS + fields.FORWARD_FIELDS + fields.AUX_FIELDS:
       n = f.size(sizes)
       self._arrays[f.name] = np.zeros(max(n, 1))
     # reference defaults (mj_resetData): qpos = qpos0, world body identity frames
@@ -75,6 +75,14 @@ class MjData:
   @property
   def energy(self):
     return np.array(self.struct.energy[:2])
+
+  @property
+  def time(self):
+    return float(self.struct.time)
+
+  @time.setter
+  def time(self, t):
+    self.struct.time = float(t)
 
   def ptr(self):
     return ctypes.byref(self.struct)

@@ -40,6 +40,39 @@ kFrameEps = 1e-6       # src/user/user_model.cc:62
 kEigEPS = 1e-12        # src/user/user_util.cc:649
 
 JNT = {"free": 0, "ball": 1, "slide": 2, "hinge": 3}
+# mjtObj (mjmodel.h) as mju_str2Type (engine_util_misc.c:1133-1236) spells them
+OBJ = {"body": 1, "xbody": 2, "joint": 3, "dof": 4, "geom": 5, "site": 6, "camera": 7,
+       "light": 8, "tendon": 18, "actuator": 19}
+# MJCF sensor element -> (mjtSensor, object attribute, mjtObj, dim, mjtDataType, mjtStage),
+# per xml_native_reader.cc:3864-4180 (element -> type/objtype) and user_objects.cc:6250-6580
+# (dim, datatype, needstage). Stages: 1 POS, 2 VEL, 3 ACC. Datatypes: 0 REAL, 1 POSITIVE,
+# 2 AXIS, 3 QUATERNION. Frame sensors read objtype/objname (+ reftype/refname).
+SENSORS = {
+    "accelerometer": (1, "site", 6, 3, 0, 3), "velocimeter": (2, "site", 6, 3, 0, 2),
+    "gyro": (3, "site", 6, 3, 0, 2), "force": (4, "site", 6, 3, 0, 3),
+    "torque": (5, "site", 6, 3, 0, 3), "magnetometer": (6, "site", 6, 3, 0, 1),
+    "jointpos": (9, "joint", 3, 1, 0, 1), "jointvel": (10, "joint", 3, 1, 0, 2),
+    "tendonpos": (11, "tendon", 18, 1, 0, 1), "tendonvel": (12, "tendon", 18, 1, 0, 2),
+    "actuatorpos": (13, "actuator", 19, 1, 0, 1), "actuatorvel": (14, "actuator", 19, 1, 0, 2),
+    "actuatorfrc": (15, "actuator", 19, 1, 0, 3),
+    "jointactuatorfrc": (16, "joint", 3, 1, 0, 3),
+    "ballquat": (17, "joint", 3, 4, 3, 1), "ballangvel": (18, "joint", 3, 3, 0, 2),
+    "jointlimitpos": (19, "joint", 3, 1, 0, 1), "jointlimitvel": (20, "joint", 3, 1, 0, 2),
+    "jointlimitfrc": (21, "joint", 3, 1, 0, 3),
+    "tendonlimitpos": (22, "tendon", 18, 1, 0, 1), "tendonlimitvel": (23, "tendon", 18, 1, 0, 2),
+    "tendonlimitfrc": (24, "tendon", 18, 1, 0, 3),
+    "framepos": (25, None, None, 3, 0, 1), "framequat": (26, None, None, 4, 3, 1),
+    "framexaxis": (27, None, None, 3, 2, 1), "frameyaxis": (28, None, None, 3, 2, 1),
+    "framezaxis": (29, None, None, 3, 2, 1), "framelinvel": (30, None, None, 3, 0, 2),
+    "frameangvel": (31, None, None, 3, 0, 2), "framelinacc": (32, None, None, 3, 0, 3),
+    "frameangacc": (33, None, None, 3, 0, 3),
+    "subtreecom": (34, "body", 1, 3, 0, 1), "subtreelinvel": (35, "body", 1, 3, 0, 2),
+    "subtreeangmom": (36, "body", 1, 3, 0, 2),
+    "e_potential": (40, None, 0, 1, 0, 1), "e_kinetic": (41, None, 0, 1, 0, 1),
+    "clock": (42, None, 0, 1, 0, 1),
+}
+SENSORS_NEXT = ("touch", "rangefinder", "camprojection", "distance", "normal", "fromto",
+                "user", "plugin")
 GEOM = {"plane": 0, "hfield": 1, "sphere": 2, "capsule": 3, "ellipsoid": 4,
         "cylinder": 5, "box": 6, "mesh": 7, "sdf": 8}
 CAMLIGHT = {"fixed": 0, "track": 1, "trackcom": 2, "targetbody": 3, "targetbodycom": 4}
@@ -423,13 +456,15 @@ class Model:
         lst = [str(x) for x in z[k]]
         m.names[k[8:]] = [] if lst == [""] and m.sizes.get(_NAME_SIZE.get(k[8:], ""), 0) == 0 else lst
     m.opt.setdefault("o_friction", [1.0, 1.0, 0.005, 0.0001, 0.0001])   # mjOption default
+    m.opt.setdefault("magnetic", [0.0, -0.5, 0.0])                      # mjOption default
     for f in fields.MODEL_FIELDS:
       setattr(m, f.name, np.ascontiguousarray(z[f.name]))
     return m
 
 
 _NAME_SIZE = {"body": "nbody", "jnt": "njnt", "geom": "ngeom", "site": "nsite", "cam": "ncam",
-              "light": "nlight", "tendon": "ntendon", "actuator": "nu", "key": "nkey"}
+              "light": "nlight", "tendon": "ntendon", "actuator": "nu", "key": "nkey",
+              "sensor": "nsensor"}
 
 
 class MJCFCompiler:
@@ -445,7 +480,7 @@ class MJCFCompiler:
     self.balanceinertia = False
     self.inertiagrouprange = (0, 5)
     self.opt = {"timestep": 0.002, "impratio": 1.0, "gravity": [0.0, 0.0, -9.81],
-                "wind": [0.0, 0.0, 0.0], "density": 0.0, "viscosity": 0.0, "o_margin": 0.0,
+                "wind": [0.0, 0.0, 0.0], "magnetic": [0.0, -0.5, 0.0], "density": 0.0, "viscosity": 0.0, "o_margin": 0.0,
                 "o_solref": [0.02, 1.0], "o_solimp": [0.9, 0.95, 0.001, 0.5, 2.0],
                 "o_friction": [1.0, 1.0, 0.005, 0.0001, 0.0001],
                 "integrator": 0, "cone": 0, "jacobian": 2, "disableflags": 0,
@@ -454,6 +489,7 @@ class MJCFCompiler:
     self.bodies = []
     self.tendons = []
     self.actuators = []
+    self.sensors = []
     self.excludes = []
     self.keys = []
 
@@ -566,8 +602,14 @@ class MJCFCompiler:
       elif t == "keyframe":
         for ch in el:
           self.keys.append(dict(ch.attrib))
-      elif t in ("visual", "asset", "statistic", "default", "compiler", "size", "sensor",
-                 "extension"):
+      elif t == "sensor":
+        for ch in el:
+          if ch.tag in SENSORS_NEXT:
+            raise MJCFError(f"sensor <{ch.tag}> is not in the supported subset (next)")
+          if ch.tag not in SENSORS:
+            raise MJCFError(f"unknown sensor <{ch.tag}>")
+          self.sensors.append((ch.tag, dict(ch.attrib)))
+      elif t in ("visual", "asset", "statistic", "default", "compiler", "size", "extension"):
         continue  # no effect on the inverse-dynamics path
       else:
         raise MJCFError(f"unsupported top-level element <{t}>")
@@ -578,7 +620,7 @@ class MJCFCompiler:
     for k in ("timestep", "impratio", "density", "viscosity", "o_margin"):
       if k in a:
         o[k] = float(a[k])
-    for k in ("gravity", "wind", "o_solref", "o_solimp", "o_friction"):
+    for k in ("gravity", "wind", "magnetic", "o_solref", "o_solimp", "o_friction"):
       if k in a:
         o[k] = _floats(a[k])
     if "integrator" in a:
@@ -707,6 +749,8 @@ class MJCFCompiler:
     return g
 
   def compile(self) -> Model:
+    if not self.bodies:                 # no <worldbody>: the world body alone
+      self._parse_worldbody(ET.Element("worldbody"))
     self._order_bodies()
     bodies = self.bodies
     nbody = len(bodies)
@@ -1273,6 +1317,68 @@ class MJCFCompiler:
       fl = a.get("forcelimited", "auto")
       afl[ai] = (not (fr[0] == 0 and fr[1] == 0)) if fl == "auto" else (fl == "true")
       afr[ai] = fr
+    # sensors (user_objects.cc mjCSensor::Compile :6250-6580, user_model.cc:3265-3286)
+    ns_ = len(self.sensors)
+    stype = arr("sensor_type", ns_, np.int32)
+    sdtype = arr("sensor_datatype", ns_, np.int32)
+    sstage = arr("sensor_needstage", ns_, np.int32)
+    sobjt = arr("sensor_objtype", ns_, np.int32)
+    sobj = arr("sensor_objid", ns_, np.int32, -1)
+    sreft = arr("sensor_reftype", ns_, np.int32)
+    sref = arr("sensor_refid", ns_, np.int32, -1)
+    sdim = arr("sensor_dim", ns_, np.int32)
+    sadr = arr("sensor_adr", ns_, np.int32)
+    scut = arr("sensor_cutoff", ns_, np.float64)
+    lookup = {1: bname, 2: bname, 3: jname,
+              5: {g["name"]: i for i, g in enumerate(geoms) if g["name"]},
+              6: {x["name"]: i for i, x in enumerate(sites) if x["name"]},
+              7: {c["name"]: i for i, c in enumerate(cams) if c["name"]},
+              18: {ta.get("name"): i for i, (ta, _) in enumerate(self.tendons) if ta.get("name")},
+              19: {a.get("name"): i for i, a in enumerate(self.actuators) if a.get("name")}}
+
+    def find(ot, name, what):
+      if not name:
+        raise MJCFError(f"missing name of {what} in sensor")
+      if name not in lookup.get(ot, {}):
+        raise MJCFError(f"unrecognized name '{name}' of {what} in sensor")
+      return lookup[ot][name]
+    sensadr = 0
+    for si_, (tag, a) in enumerate(self.sensors):
+      tp, attr, ot, dim, dt, st = SENSORS[tag]
+      cut = float(a.get("cutoff", 0.0))
+      if cut < 0 or float(a.get("noise", 0.0)) < 0:
+        raise MJCFError("negative noise/cutoff in sensor")
+      rt, rid = 0, -1
+      if attr is None and ot is None:              # frame sensors
+        ot = OBJ.get(a.get("objtype", ""), None)
+        if ot not in (1, 2, 5, 6, 7):
+          raise MJCFError("sensor must be attached to (x)body, geom, site or camera")
+        oid = find(ot, a.get("objname"), "sensorized object")
+        if "reftype" in a and tp <= 31:
+          rt = OBJ.get(a["reftype"], None)
+          if rt not in (1, 2, 5, 6, 7):
+            raise MJCFError("reference frame object must be (x)body, geom, site or camera")
+          rid = find(rt, a.get("refname"), "reference frame object")
+        elif "refname" in a and tp <= 31:
+          raise MJCFError("refname given but reftype is missing")
+      elif attr is None:                           # global sensors
+        oid = -1
+      else:
+        oid = find(ot, a.get(attr), "sensorized object")
+        if ot == 3:
+          jt = int(jtype[oid])
+          if tp in (9, 10, 16) and jt not in (2, 3):
+            raise MJCFError("joint must be slide or hinge in sensor")
+          if tp in (17, 18) and jt != 1:
+            raise MJCFError("joint must be ball in sensor")
+          if tp in (19, 20, 21) and not jlim[oid]:
+            raise MJCFError("joint must be limited in sensor")
+        if ot == 18 and tp in (22, 23, 24) and not tlim[oid]:
+          raise MJCFError("tendon must be limited in sensor")
+      stype[si_], sdtype[si_], sstage[si_], sobjt[si_], sobj[si_] = tp, dt, st, ot, oid
+      sreft[si_], sref[si_], sdim[si_], sadr[si_], scut[si_] = rt, rid, dim, sensadr, cut
+      sensadr += dim
+    s.update(nsensor=ns_, nsensordata=sensadr)
     # exclude pairs: signature = (body1 << 16) + body2 with body1 < body2
     nex = len(self.excludes)
     exs = arr("exclude_signature", nex, np.int32)
@@ -1442,6 +1548,7 @@ class MJCFCompiler:
                "cam": [c["name"] for c in cams], "light": [l["name"] for l in lights],
                "tendon": [ta.get("name", "") for ta, _ in self.tendons],
                "actuator": [a.get("name", "") for a in self.actuators],
+               "sensor": [a.get("name", "") for _, a in self.sensors],
                "key": [k.get("name", "") for k in self.keys]}
     m.model_name = getattr(self, "model_name", "")
     # check every field of the table is present with the right shape

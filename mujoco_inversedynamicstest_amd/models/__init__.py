@@ -17,14 +17,17 @@ SOURCES = {
 }
 
 mjDSBL_CONTACT = 1 << 4
+mjDSBL_SENSOR = 1 << 12
 
 
 def path(name: str) -> str:
   return os.path.join(_HERE, name + ".npz")
 
 
-def load(name: str, disable_contact: bool = False) -> Model:
+def load(name: str, disable_contact: bool = False, disable_sensor: bool = False) -> Model:
   m = Model.load(path(name))
   if disable_contact:
     m.opt["disableflags"] = int(m.opt["disableflags"]) | mjDSBL_CONTACT
+  if disable_sensor:
+    m.opt["disableflags"] = int(m.opt["disableflags"]) | mjDSBL_SENSOR
   return m

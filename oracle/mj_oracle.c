@@ -2098,17 +2098,465 @@ static void or_energyVel(const mjhipModel* m, mjhipData* d) {
   free(vec);
 }
 
+/*============================ engine_sensor.c =============================================*/
+
+/* mjtSensor / mjtObj / mjtDataType values (mjmodel.h) */
+enum { SENS_TOUCH = 0, SENS_ACCELEROMETER, SENS_VELOCIMETER, SENS_GYRO, SENS_FORCE, SENS_TORQUE,
+       SENS_MAGNETOMETER, SENS_RANGEFINDER, SENS_CAMPROJECTION, SENS_JOINTPOS, SENS_JOINTVEL,
+       SENS_TENDONPOS, SENS_TENDONVEL, SENS_ACTUATORPOS, SENS_ACTUATORVEL, SENS_ACTUATORFRC,
+       SENS_JOINTACTFRC, SENS_BALLQUAT, SENS_BALLANGVEL, SENS_JOINTLIMITPOS,
+       SENS_JOINTLIMITVEL, SENS_JOINTLIMITFRC, SENS_TENDONLIMITPOS, SENS_TENDONLIMITVEL,
+       SENS_TENDONLIMITFRC, SENS_FRAMEPOS, SENS_FRAMEQUAT, SENS_FRAMEXAXIS, SENS_FRAMEYAXIS,
+       SENS_FRAMEZAXIS, SENS_FRAMELINVEL, SENS_FRAMEANGVEL, SENS_FRAMELINACC,
+       SENS_FRAMEANGACC, SENS_SUBTREECOM, SENS_SUBTREELINVEL, SENS_SUBTREEANGMOM,
+       SENS_GEOMDIST, SENS_GEOMNORMAL, SENS_GEOMFROMTO, SENS_E_POTENTIAL, SENS_E_KINETIC,
+       SENS_CLOCK };
+enum { OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
+enum { DATATYPE_REAL = 0, DATATYPE_POSITIVE = 1 };
+
+/* engine_util_blas.c:179-188 */
+static void mju_mulMatTVec3(mjtNum res[3], const mjtNum mat[9], const mjtNum vec[3]) {
+  mjtNum tmp[3] = {mat[0]*vec[0] + mat[3]*vec[1] + mat[6]*vec[2],
+                   mat[1]*vec[0] + mat[4]*vec[1] + mat[7]*vec[2],
+                   mat[2]*vec[0] + mat[5]*vec[1] + mat[8]*vec[2]};
+  res[0] = tmp[0]; res[1] = tmp[1]; res[2] = tmp[2];
+}
+
+/* engine_util_spatial.c:495-523 */
+static void mju_transformSpatial(mjtNum res[6], const mjtNum vec[6], int flg_force,
+                                 const mjtNum newpos[3], const mjtNum oldpos[3],
+                                 const mjtNum* rotnew2old) {
+  mjtNum cros[3], dif[3], tran[6];
+  mju_copy(tran, vec, 6);
+  mju_sub3(dif, newpos, oldpos);
+  if (flg_force) {
+    mju_cross(cros, dif, vec+3);
+    mju_sub3(tran, vec, cros);
+  } else {
+    mju_cross(cros, dif, vec);
+    mju_sub3(tran+3, vec+3, cros);
+  }
+  if (rotnew2old) {
+    mju_mulMatTVec3(res, rotnew2old, tran);
+    mju_mulMatTVec3(res+3, rotnew2old, tran+3);
+  } else {
+    mju_copy(res, tran, 6);
+  }
+}
+
+/* object frame (pos, rot) and body of a sensorized object: the switch shared by
+ * mj_objectVelocity/mj_objectAcceleration (engine_support.c:1265-1312, :1317-1361) and
+ * get_xpos_xmat (engine_sensor.c:69-94) */
+static int obj_frame(const mjhipModel* m, const mjhipData* d, int type, int id,
+                     const mjtNum** pos, const mjtNum** mat) {
+  switch (type) {
+  case OBJ_BODY:   *pos = d->xipos + 3*id;     *mat = d->ximat + 9*id;     return id;
+  case OBJ_XBODY:  *pos = d->xpos + 3*id;      *mat = d->xmat + 9*id;      return id;
+  case OBJ_GEOM:   *pos = d->geom_xpos + 3*id; *mat = d->geom_xmat + 9*id; return m->geom_bodyid[id];
+  case OBJ_SITE:   *pos = d->site_xpos + 3*id; *mat = d->site_xmat + 9*id; return m->site_bodyid[id];
+  default:         *pos = d->cam_xpos + 3*id;  *mat = d->cam_xmat + 9*id;  return m->cam_bodyid[id];
+  }
+}
+
+/* engine_support.c:1265-1312 */
+static void or_objectVelocity(const mjhipModel* m, const mjhipData* d, int type, int id,
+                              mjtNum res[6], int flg_local) {
+  const mjtNum *pos, *mat;
+  int b = obj_frame(m, d, type, id, &pos, &mat);
+  mju_transformSpatial(res, d->cvel + 6*b, 0, pos, d->subtree_com + 3*m->body_rootid[b],
+                       flg_local ? mat : NULL);
+}
+
+/* engine_support.c:1317-1371 */
+static void or_objectAcceleration(const mjhipModel* m, const mjhipData* d, int type, int id,
+                                  mjtNum res[6], int flg_local) {
+  const mjtNum *pos, *mat;
+  mjtNum correction[3], vel[6];
+  int b = obj_frame(m, d, type, id, &pos, &mat);
+  const mjtNum* com = d->subtree_com + 3*m->body_rootid[b];
+  mju_transformSpatial(vel, d->cvel + 6*b, 0, pos, com, flg_local ? mat : NULL);
+  mju_transformSpatial(res, d->cacc + 6*b, 0, pos, com, flg_local ? mat : NULL);
+  mju_cross(correction, vel, vel+3);
+  mju_addTo3(res+3, correction);
+}
+
+/* engine_sensor.c:96-118 get_xquat */
+static void or_xquat(const mjhipModel* m, const mjhipData* d, int type, int id, mjtNum q[4]) {
+  switch (type) {
+  case OBJ_XBODY: mju_copy4(q, d->xquat + 4*id); break;
+  case OBJ_BODY:  mju_mulQuat(q, d->xquat + 4*id, m->body_iquat + 4*id); break;
+  case OBJ_GEOM:  mju_mulQuat(q, d->xquat + 4*m->geom_bodyid[id], m->geom_quat + 4*id); break;
+  case OBJ_SITE:  mju_mulQuat(q, d->xquat + 4*m->site_bodyid[id], m->site_quat + 4*id); break;
+  default:        mju_mulQuat(q, d->xquat + 4*m->cam_bodyid[id], m->cam_quat + 4*id); break;
+  }
+}
+
+/* engine_core_smooth.c:1900-1958 */
+static void or_subtreeVel(const mjhipModel* m, mjhipData* d) {
+  int nbody = m->nbody;
+  mjtNum dx[3], dv[3], dp[3], dL[3];
+  mjtNum* body_vel = (mjtNum*)malloc(6*(size_t)nbody*sizeof(mjtNum));
+  for (int i = 0; i < nbody; i++) {
+    or_objectVelocity(m, d, OBJ_BODY, i, body_vel + 6*i, 0);
+    mju_scl3(d->subtree_linvel + 3*i, body_vel + 6*i + 3, m->body_mass[i]);
+    mju_mulMatTVec3(dv, d->ximat + 9*i, body_vel + 6*i);
+    dv[0] *= m->body_inertia[3*i];
+    dv[1] *= m->body_inertia[3*i+1];
+    dv[2] *= m->body_inertia[3*i+2];
+    mju_mulMatVec3(d->subtree_angmom + 3*i, d->ximat + 9*i, dv);
+  }
+  for (int i = nbody-1; i >= 0; i--) {
+    if (i) mju_addTo3(d->subtree_linvel + 3*m->body_parentid[i], d->subtree_linvel + 3*i);
+    mju_scl3(d->subtree_linvel + 3*i, d->subtree_linvel + 3*i,
+             1/mjMAX(mjMINVAL, m->body_subtreemass[i]));
+  }
+  for (int i = nbody-1; i > 0; i--) {
+    int parent = m->body_parentid[i];
+    mju_sub3(dx, d->xipos + 3*i, d->subtree_com + 3*i);
+    mju_sub3(dv, body_vel + 6*i + 3, d->subtree_linvel + 3*i);
+    mju_scl3(dp, dv, m->body_mass[i]);
+    mju_cross(dL, dx, dp);
+    mju_addTo3(d->subtree_angmom + 3*i, dL);
+    mju_addTo3(d->subtree_angmom + 3*parent, d->subtree_angmom + 3*i);
+    mju_sub3(dx, d->subtree_com + 3*i, d->subtree_com + 3*parent);
+    mju_sub3(dv, d->subtree_linvel + 3*i, d->subtree_linvel + 3*parent);
+    mju_scl3(dv, dv, m->body_subtreemass[i]);
+    mju_cross(dL, dx, dv);
+    mju_addTo3(d->subtree_angmom + 3*parent, dL);
+  }
+  free(body_vel);
+}
+
+/* engine_util_misc.c:830-850 */
+static void mju_decodePyramid(mjtNum* force, const mjtNum* pyramid, const mjtNum* mu, int dim) {
+  if (dim == 1) {
+    force[0] = pyramid[0];
+    return;
+  }
+  force[0] = 0;
+  for (int i = 0; i < 2*(dim-1); i++) force[0] += pyramid[i];
+  for (int i = 0; i < dim-1; i++) force[i+1] = (pyramid[2*i] - pyramid[2*i+1]) * mu[i];
+}
+
+/* engine_support.c:1459-1480 mj_contactForce (pyramidal cones: the supported subset) */
+static void or_contactForce(const orEfc* e, int id, mjtNum result[6]) {
+  mju_zero(result, 6);
+  if (id >= 0 && id < e->ncon && e->con_efc_address[id] >= 0) {
+    mju_decodePyramid(result, e->efc_force + e->con_efc_address[id], e->con_friction + 5*id,
+                      e->con_dim[id]);
+  }
+}
+
+/* engine_core_smooth.c:2027-2181 (no equality constraints in the supported subset) */
+static void or_rnePostConstraint(const mjhipModel* m, mjhipData* d, const orEfc* e) {
+  int nbody = m->nbody;
+  mjtNum cfrc_com[6], cfrc[6], lfrc[6];
+  mju_zero(d->cacc, 6);
+  if (!mjDISABLED(mjhipDSBL_GRAVITY)) mju_scl3(d->cacc + 3, m->opt.gravity, -1);
+  mju_zero(d->cfrc_ext, 6*nbody);
+  for (int i = 1; i < nbody; i++) {
+    if (!mju_isZero(d->xfrc_applied + 6*i, 6)) {
+      mju_copy3(cfrc, d->xfrc_applied + 6*i + 3);
+      mju_copy3(cfrc + 3, d->xfrc_applied + 6*i);
+      mju_transformSpatial(cfrc_com, cfrc, 1, d->subtree_com + 3*m->body_rootid[i],
+                           d->xipos + 3*i, NULL);
+      mju_addTo(d->cfrc_ext + 6*i, cfrc_com, 6);
+    }
+  }
+  for (int i = 0; i < e->ncon; i++) {
+    if (e->con_efc_address[i] < 0) continue;
+    const int* geom = e->con_geom + 2*i;
+    if (geom[0] < 0 || geom[1] < 0) continue;
+    or_contactForce(e, i, lfrc);
+    const mjtNum* frame = e->con_frame + 9*i;
+    mju_mulMatTVec3(cfrc, frame, lfrc + 3);
+    mju_mulMatTVec3(cfrc + 3, frame, lfrc);
+    int k;
+    if ((k = m->geom_bodyid[geom[0]])) {
+      mju_transformSpatial(cfrc_com, cfrc, 1, d->subtree_com + 3*m->body_rootid[k],
+                           e->con_pos + 3*i, NULL);
+      mju_subFrom(d->cfrc_ext + 6*k, cfrc_com, 6);
+    }
+    if ((k = m->geom_bodyid[geom[1]])) {
+      mju_transformSpatial(cfrc_com, cfrc, 1, d->subtree_com + 3*m->body_rootid[k],
+                           e->con_pos + 3*i, NULL);
+      mju_addTo(d->cfrc_ext + 6*k, cfrc_com, 6);
+    }
+  }
+  mjtNum cacc[6], cfrc_body[6], cfrc_corr[6];
+  mju_zero(d->cfrc_int, 6);
+  for (int j = 1; j < nbody; j++) {
+    int bda = m->body_dofadr[j];
+    mju_mulDofVec(cacc, d->cdof_dot + 6*bda, d->qvel + bda, m->body_dofnum[j]);
+    mju_add(d->cacc + 6*j, d->cacc + 6*m->body_parentid[j], cacc, 6);
+    mju_mulDofVec(cacc, d->cdof + 6*bda, d->qacc + bda, m->body_dofnum[j]);
+    mju_addTo(d->cacc + 6*j, cacc, 6);
+    mju_mulInertVec(cfrc_body, d->cinert + 10*j, d->cacc + 6*j);
+    mju_mulInertVec(cfrc_corr, d->cinert + 10*j, d->cvel + 6*j);
+    mju_crossForce(cfrc, d->cvel + 6*j, cfrc_corr);
+    mju_addTo(cfrc_body, cfrc, 6);
+    mju_sub(d->cfrc_int + 6*j, cfrc_body, d->cfrc_ext + 6*j, 6);
+  }
+  for (int j = nbody-1; j > 0; j--) {
+    mju_addTo(d->cfrc_int + 6*m->body_parentid[j], d->cfrc_int + 6*j, 6);
+  }
+}
+
+/* engine_sensor.c:38-66 */
+static void or_applyCutoff(const mjhipModel* m, mjhipData* d, int stage) {
+  for (int i = 0; i < m->nsensor; i++) {
+    if (m->sensor_needstage[i] == stage && m->sensor_cutoff[i] > 0) {
+      int adr = m->sensor_adr[i], dim = m->sensor_dim[i];
+      mjtNum cutoff = m->sensor_cutoff[i];
+      for (int j = 0; j < dim; j++) {
+        if (m->sensor_datatype[i] == DATATYPE_REAL) {
+          d->sensordata[adr+j] = mju_clip(d->sensordata[adr+j], -cutoff, cutoff);
+        } else if (m->sensor_datatype[i] == DATATYPE_POSITIVE) {
+          d->sensordata[adr+j] = mjMIN(cutoff, d->sensordata[adr+j]);
+        }
+      }
+    }
+  }
+}
+
+/* first limit row of (type, id) among rows ne+nf..nefc (engine_sensor.c:286-304) */
+static int or_limitRow(const orEfc* e, int type, int id) {
+  for (int j = e->ne + e->nf; j < e->nefc; j++) {
+    if (e->efc_type[j] == type && e->efc_id[j] == id) return j;
+  }
+  return -1;
+}
+
+static void or_energyPos(const mjhipModel* m, mjhipData* d);
+static void or_energyVel(const mjhipModel* m, mjhipData* d);
+
+/* engine_sensor.c:209-513 mj_sensorPos (no rangefinder/camprojection/geom distance/user) */
+static void or_sensorPos(const mjhipModel* m, mjhipData* d, const orEfc* e) {
+  if (mjDISABLED(mjhipDSBL_SENSOR)) return;
+  for (int i = 0; i < m->nsensor; i++) {
+    if (m->sensor_needstage[i] != mjhipSTAGE_POS) continue;
+    int type = m->sensor_type[i], objtype = m->sensor_objtype[i], objid = m->sensor_objid[i];
+    int refid = m->sensor_refid[i], reftype = m->sensor_reftype[i], adr = m->sensor_adr[i];
+    mjtNum* out = d->sensordata + adr;
+    mjtNum rvec[3];
+    const mjtNum *xpos, *xmat, *xpos_ref, *xmat_ref;
+    int r;
+    switch (type) {
+    case SENS_MAGNETOMETER:
+      mju_mulMatTVec(out, d->site_xmat + 9*objid, m->opt.magnetic, 3, 3);
+      break;
+    case SENS_JOINTPOS:
+      out[0] = d->qpos[m->jnt_qposadr[objid]];
+      break;
+    case SENS_TENDONPOS:
+      out[0] = d->ten_length[objid];
+      break;
+    case SENS_ACTUATORPOS:
+      out[0] = d->actuator_length[objid];
+      break;
+    case SENS_BALLQUAT:
+      mju_copy4(out, d->qpos + m->jnt_qposadr[objid]);
+      mju_normalize4(out);
+      break;
+    case SENS_JOINTLIMITPOS:
+    case SENS_TENDONLIMITPOS:
+      out[0] = 0;
+      r = or_limitRow(e, type == SENS_JOINTLIMITPOS ? orCNSTR_LIMIT_JOINT : orCNSTR_LIMIT_TENDON,
+                      objid);
+      if (r >= 0) out[0] = e->efc_pos[r] - e->efc_margin[r];
+      break;
+    case SENS_FRAMEPOS:
+    case SENS_FRAMEXAXIS:
+    case SENS_FRAMEYAXIS:
+    case SENS_FRAMEZAXIS:
+      obj_frame(m, d, objtype, objid, &xpos, &xmat);
+      if (refid == -1) {
+        if (type == SENS_FRAMEPOS) {
+          mju_copy3(out, xpos);
+        } else {
+          int offset = type - SENS_FRAMEXAXIS;
+          out[0] = xmat[offset];
+          out[1] = xmat[offset+3];
+          out[2] = xmat[offset+6];
+        }
+      } else {
+        obj_frame(m, d, reftype, refid, &xpos_ref, &xmat_ref);
+        if (type == SENS_FRAMEPOS) {
+          mju_sub3(rvec, xpos, xpos_ref);
+          mju_mulMatTVec3(out, xmat_ref, rvec);
+        } else {
+          int offset = type - SENS_FRAMEXAXIS;
+          mjtNum axis[3] = {xmat[offset], xmat[offset+3], xmat[offset+6]};
+          mju_mulMatTVec3(out, xmat_ref, axis);
+        }
+      }
+      break;
+    case SENS_FRAMEQUAT: {
+      mjtNum objquat[4], refquat[4];
+      or_xquat(m, d, objtype, objid, objquat);
+      if (refid == -1) {
+        mju_copy4(out, objquat);
+      } else {
+        or_xquat(m, d, reftype, refid, refquat);
+        refquat[1] = -refquat[1]; refquat[2] = -refquat[2]; refquat[3] = -refquat[3];
+        mju_mulQuat(out, refquat, objquat);
+      }
+      break;
+    }
+    case SENS_SUBTREECOM:
+      mju_copy3(out, d->subtree_com + 3*objid);
+      break;
+    case SENS_E_POTENTIAL:
+      or_energyPos(m, d);
+      out[0] = d->energy[0];
+      break;
+    case SENS_E_KINETIC:
+      or_energyVel(m, d);
+      out[0] = d->energy[1];
+      break;
+    case SENS_CLOCK:
+      out[0] = d->time;
+      break;
+    }
+  }
+  or_applyCutoff(m, d, mjhipSTAGE_POS);
+}
+
+/* engine_sensor.c:521-672 mj_sensorVel */
+static void or_sensorVel(const mjhipModel* m, mjhipData* d, const orEfc* e) {
+  if (mjDISABLED(mjhipDSBL_SENSOR)) return;
+  int subtreeVel = 0;
+  mjtNum xvel[6];
+  for (int i = 0; i < m->nsensor; i++) {
+    if (m->sensor_needstage[i] != mjhipSTAGE_VEL) continue;
+    int type = m->sensor_type[i], objtype = m->sensor_objtype[i], objid = m->sensor_objid[i];
+    int refid = m->sensor_refid[i], reftype = m->sensor_reftype[i], adr = m->sensor_adr[i];
+    mjtNum* out = d->sensordata + adr;
+    int r;
+    if (!subtreeVel && (type == SENS_SUBTREELINVEL || type == SENS_SUBTREEANGMOM)) {
+      or_subtreeVel(m, d);
+      subtreeVel = 1;
+    }
+    switch (type) {
+    case SENS_VELOCIMETER:
+      or_objectVelocity(m, d, OBJ_SITE, objid, xvel, 1);
+      mju_copy3(out, xvel + 3);
+      break;
+    case SENS_GYRO:
+      or_objectVelocity(m, d, OBJ_SITE, objid, xvel, 1);
+      mju_copy3(out, xvel);
+      break;
+    case SENS_JOINTVEL:
+      out[0] = d->qvel[m->jnt_dofadr[objid]];
+      break;
+    case SENS_TENDONVEL:
+      out[0] = d->ten_velocity[objid];
+      break;
+    case SENS_ACTUATORVEL:
+      out[0] = d->actuator_velocity[objid];
+      break;
+    case SENS_BALLANGVEL:
+      mju_copy3(out, d->qvel + m->jnt_dofadr[objid]);
+      break;
+    case SENS_JOINTLIMITVEL:
+    case SENS_TENDONLIMITVEL:
+      out[0] = 0;
+      r = or_limitRow(e, type == SENS_JOINTLIMITVEL ? orCNSTR_LIMIT_JOINT : orCNSTR_LIMIT_TENDON,
+                      objid);
+      if (r >= 0) out[0] = e->efc_vel[r];
+      break;
+    case SENS_FRAMELINVEL:
+    case SENS_FRAMEANGVEL:
+      or_objectVelocity(m, d, objtype, objid, xvel, 0);
+      if (refid > -1) {
+        const mjtNum *xpos, *xmat, *xpos_ref, *xmat_ref;
+        mjtNum xvel_ref[6], rel_vel[6], cross[3], rvec[3];
+        obj_frame(m, d, objtype, objid, &xpos, &xmat);
+        obj_frame(m, d, reftype, refid, &xpos_ref, &xmat_ref);
+        or_objectVelocity(m, d, reftype, refid, xvel_ref, 0);
+        mju_sub(rel_vel, xvel, xvel_ref, 6);
+        mju_sub3(rvec, xpos, xpos_ref);
+        mju_cross(cross, rvec, xvel_ref);
+        mju_addTo3(rel_vel + 3, cross);
+        mju_mulMatTVec3(xvel, xmat_ref, rel_vel);
+        mju_mulMatTVec3(xvel + 3, xmat_ref, rel_vel + 3);
+      }
+      mju_copy3(out, type == SENS_FRAMELINVEL ? xvel + 3 : xvel);
+      break;
+    case SENS_SUBTREELINVEL:
+      mju_copy3(out, d->subtree_linvel + 3*objid);
+      break;
+    case SENS_SUBTREEANGMOM:
+      mju_copy3(out, d->subtree_angmom + 3*objid);
+      break;
+    }
+  }
+  or_applyCutoff(m, d, mjhipSTAGE_VEL);
+}
+
+/* engine_sensor.c:677-915 mj_sensorAcc (no touch) */
+static void or_sensorAcc(const mjhipModel* m, mjhipData* d, const orEfc* e) {
+  if (mjDISABLED(mjhipDSBL_SENSOR)) return;
+  int rnePost = 0;
+  mjtNum tmp[6];
+  for (int i = 0; i < m->nsensor; i++) {
+    if (m->sensor_needstage[i] != mjhipSTAGE_ACC) continue;
+    int type = m->sensor_type[i], objtype = m->sensor_objtype[i], objid = m->sensor_objid[i];
+    mjtNum* out = d->sensordata + m->sensor_adr[i];
+    int r, bodyid, rootid;
+    if (!rnePost && (type == SENS_ACCELEROMETER || type == SENS_FORCE || type == SENS_TORQUE ||
+                     type == SENS_FRAMELINACC || type == SENS_FRAMEANGACC)) {
+      or_rnePostConstraint(m, d, e);
+      rnePost = 1;
+    }
+    switch (type) {
+    case SENS_ACCELEROMETER:
+      or_objectAcceleration(m, d, OBJ_SITE, objid, tmp, 1);
+      mju_copy3(out, tmp + 3);
+      break;
+    case SENS_FORCE:
+    case SENS_TORQUE:
+      bodyid = m->site_bodyid[objid];
+      rootid = m->body_rootid[bodyid];
+      mju_transformSpatial(tmp, d->cfrc_int + 6*bodyid, 1, d->site_xpos + 3*objid,
+                           d->subtree_com + 3*rootid, d->site_xmat + 9*objid);
+      mju_copy3(out, type == SENS_FORCE ? tmp + 3 : tmp);
+      break;
+    case SENS_ACTUATORFRC:
+      out[0] = d->actuator_force[objid];
+      break;
+    case SENS_JOINTACTFRC:
+      out[0] = d->qfrc_actuator[m->jnt_dofadr[objid]];
+      break;
+    case SENS_JOINTLIMITFRC:
+    case SENS_TENDONLIMITFRC:
+      out[0] = 0;
+      r = or_limitRow(e, type == SENS_JOINTLIMITFRC ? orCNSTR_LIMIT_JOINT : orCNSTR_LIMIT_TENDON,
+                      objid);
+      if (r >= 0) out[0] = e->efc_force[r];
+      break;
+    case SENS_FRAMELINACC:
+    case SENS_FRAMEANGACC:
+      or_objectAcceleration(m, d, objtype, objid, tmp, 0);
+      mju_copy3(out, type == SENS_FRAMELINACC ? tmp + 3 : tmp);
+      break;
+    }
+  }
+  or_applyCutoff(m, d, mjhipSTAGE_ACC);
+}
+
 void or_inverseSkip(const mjhipModel* m, mjhipData* d, orEfc* e, int skipstage,
                     int skipsensor) {
   int nv = m->nv;
-  (void)skipsensor;
   mjtNum* qacc = NULL;
   if (skipstage < mjhipSTAGE_POS) {
     or_invPosition(m, d, e);
+    if (!skipsensor) or_sensorPos(m, d, e);
     if (mjENABLED(mjhipENBL_ENERGY)) or_energyPos(m, d);
   }
   if (skipstage < mjhipSTAGE_VEL) {
     or_fwdVelocity(m, d, e);
+    if (!skipsensor) or_sensorVel(m, d, e);
     if (mjENABLED(mjhipENBL_ENERGY)) or_energyVel(m, d);
   }
   if (mjENABLED(mjhipENBL_INVDISCRETE)) {
@@ -2118,6 +2566,7 @@ void or_inverseSkip(const mjhipModel* m, mjhipData* d, orEfc* e, int skipstage,
   }
   or_invConstraint(m, d, e);
   or_rne(m, d, 1, d->qfrc_inverse);
+  if (!skipsensor) or_sensorAcc(m, d, e);
   for (int i = 0; i < nv; i++) {
     d->qfrc_inverse[i] += m->dof_armature[i] * d->qacc[i]
                           - d->qfrc_passive[i] - d->qfrc_constraint[i];
@@ -2248,53 +2697,56 @@ static void diff(mjtNum* dx, const mjtNum* x1, const mjtNum* x2, mjtNum h, int n
   for (int i = 0; i < n; i++) dx[i] = inv_h * (x2[i] - x1[i]);
 }
 
-/* :611-719 with flg_actuation = 0, no sensor outputs */
+/* engine_derivative_fd.c:611-719 mjd_inverseFD with flg_actuation = 0 */
 void or_inverseFD(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum eps, mjtNum* DfDq,
-                  mjtNum* DfDv, mjtNum* DfDa, mjtNum* DmDq) {
-  int nq = m->nq, nv = m->nv, nM = m->nM;
+                  mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq, mjtNum* DsDv, mjtNum* DsDa,
+                  mjtNum* DmDq) {
+  int nq = m->nq, nv = m->nv, nM = m->nM, ns = m->nsensordata;
+  int skipsensor = !DsDq && !DsDv && !DsDa;
   mjtNum* pos = (mjtNum*)malloc(nq*sizeof(mjtNum));
   mjtNum* force = (mjtNum*)malloc(nv*sizeof(mjtNum));
-  mjtNum* force_plus = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  mjtNum* sensor = (mjtNum*)malloc((ns + 1)*sizeof(mjtNum));
   mjtNum* mass = (mjtNum*)malloc(nM*sizeof(mjtNum));
-  mjtNum* mass_plus = (mjtNum*)malloc(nM*sizeof(mjtNum));
   mjtNum* dpos = (mjtNum*)calloc(nv, sizeof(mjtNum));
   mju_copy(pos, d->qpos, nq);
-  or_inverseSkip(m, d, e, mjhipSTAGE_NONE, 1);
+  or_inverseSkip(m, d, e, mjhipSTAGE_NONE, skipsensor);
   mju_copy(force, d->qfrc_inverse, nv);
+  if (!skipsensor) mju_copy(sensor, d->sensordata, ns);
   mju_copy(mass, d->qM, nM);
-  if (DfDa) {
+  if (DfDa || DsDa) {
     for (int i = 0; i < nv; i++) {
       mjtNum tmp = d->qacc[i];
       d->qacc[i] += eps;
-      or_inverseSkip(m, d, e, mjhipSTAGE_VEL, 1);
+      or_inverseSkip(m, d, e, mjhipSTAGE_VEL, skipsensor);
       d->qacc[i] = tmp;
-      diff(DfDa + i*nv, force, d->qfrc_inverse, eps, nv);
+      if (DfDa) diff(DfDa + i*nv, force, d->qfrc_inverse, eps, nv);
+      if (DsDa) diff(DsDa + i*ns, sensor, d->sensordata, eps, ns);
     }
   }
-  if (DfDv) {
+  if (DfDv || DsDv) {
     for (int i = 0; i < nv; i++) {
       mjtNum tmp = d->qvel[i];
       d->qvel[i] += eps;
-      or_inverseSkip(m, d, e, mjhipSTAGE_POS, 1);
+      or_inverseSkip(m, d, e, mjhipSTAGE_POS, skipsensor);
       d->qvel[i] = tmp;
-      diff(DfDv + i*nv, force, d->qfrc_inverse, eps, nv);
+      if (DfDv) diff(DfDv + i*nv, force, d->qfrc_inverse, eps, nv);
+      if (DsDv) diff(DsDv + i*ns, sensor, d->sensordata, eps, ns);
     }
   }
-  if (DfDq || DmDq) {
+  if (DfDq || DsDq || DmDq) {
     for (int i = 0; i < nv; i++) {
       mju_zero(dpos, nv);
       dpos[i] = 1;
       mj_integratePos(m, d->qpos, dpos, eps);
-      or_inverseSkip(m, d, e, mjhipSTAGE_NONE, 1);
+      or_inverseSkip(m, d, e, mjhipSTAGE_NONE, skipsensor);
       mju_copy(d->qpos, pos, nq);
       if (DfDq) diff(DfDq + i*nv, force, d->qfrc_inverse, eps, nv);
-      mju_copy(force_plus, d->qfrc_inverse, nv);
-      mju_copy(mass_plus, d->qM, nM);
-      if (DmDq) diff(DmDq + i*nM, mass, mass_plus, eps, nM);
+      if (DsDq) diff(DsDq + i*ns, sensor, d->sensordata, eps, ns);
+      if (DmDq) diff(DmDq + i*nM, mass, d->qM, eps, nM);
     }
   }
   /* like the reference, d keeps the outputs of the last perturbed evaluation */
-  free(pos); free(force); free(force_plus); free(mass); free(mass_plus); free(dpos);
+  free(pos); free(force); free(sensor); free(mass); free(dpos);
 }
 
 /*============================ CPU baseline =================================================*/
@@ -2315,7 +2767,10 @@ static mjtNum* alloc_data(const mjhipModel* m, mjhipData* d, orEfc* e) {
 #define XD(name, d0, d1, stage) total += (size_t)(m->d0) * (d1);
   MJHIP_DATA_FIELDS
 #undef XD
-  total += 2*(size_t)m->nv + 6*(size_t)m->nbody + m->nu;
+  total += 2*(size_t)m->nv + 6*(size_t)m->nbody + 2*(size_t)m->nu;
+#define XD(name, d0, d1, stage) total += (size_t)(m->d0) * (d1);
+  MJHIP_DATA_SENSOR_AUX
+#undef XD
   total += (size_t)cap * (m->nv + 14);
   mjtNum* buf = (mjtNum*)calloc(total + 1, sizeof(mjtNum));
   mjtNum* p = buf;
@@ -2328,6 +2783,10 @@ static mjtNum* alloc_data(const mjhipModel* m, mjhipData* d, orEfc* e) {
   d->qfrc_actuator = p; p += m->nv;
   d->xfrc_applied = p; p += 6*m->nbody;
   d->ctrl = p; p += m->nu;
+  d->actuator_force = p; p += m->nu;
+#define XD(name, d0, d1, stage) d->name = p; p += (size_t)(m->d0) * (d1);
+  MJHIP_DATA_SENSOR_AUX
+#undef XD
   memset(e, 0, sizeof(*e));
   e->capacity = cap;
   e->efc_J = p; p += (size_t)cap*m->nv;

@@ -91,9 +91,11 @@ int  or_forward(const mjhipModel* m, mjhipData* d, orEfc* efc);
 void or_xfrcAccumulate(const mjhipModel* m, mjhipData* d, mjtNum* qfrc);
 void or_rungeKutta4(const mjhipModel* m, mjhipData* d, orEfc* efc);
 
-/* mjd_inverseFD (engine_derivative_fd.c:611-719), flg_actuation = 0, no sensors */
+/* mjd_inverseFD (engine_derivative_fd.c:611-719), flg_actuation = 0; any output may be NULL,
+ * sensors are skipped when DsDq, DsDv and DsDa are all NULL */
 void or_inverseFD(const mjhipModel* m, mjhipData* d, orEfc* efc, mjtNum eps,
-                  mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DmDq);
+                  mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq, mjtNum* DsDv,
+                  mjtNum* DsDa, mjtNum* DmDq);
 
 /* CPU baseline: B instances of mj_inverse over `nthread` threads, one data per thread,
  * static chunks of B/(10*nthread) (python/mujoco/rollout.cc:307-317). Returns seconds. */

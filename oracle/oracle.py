@@ -72,7 +72,7 @@ def lib():
     L.or_forward.restype = ctypes.c_int
     L.or_xfrcAccumulate.argtypes = [M, Dp, _D]
     L.or_rungeKutta4.argtypes = [M, Dp, E]
-    L.or_inverseFD.argtypes = [M, Dp, E, ctypes.c_double, _D, _D, _D, _D]
+    L.or_inverseFD.argtypes = [M, Dp, E, ctypes.c_double, _D, _D, _D, _D, _D, _D, _D]
     L.or_inverseBatch.argtypes = [M, ctypes.c_int, _D, _D, _D, _D, ctypes.c_int]
     L.or_inverseBatch.restype = ctypes.c_double
     _lib = L
@@ -180,13 +180,18 @@ class Oracle:
       return self._efc_arrays[name][:self.efc.nefc * k]
     return self._efc_int[name][:self.efc.nefc]
 
-  def inverse_fd(self, eps=1e-6, dmdq=False):
-    nv, nM = self.m.nv, self.m.nM
+  def inverse_fd(self, eps=1e-6, dmdq=False, sensors=False):
+    """mjd_inverseFD: (DfDq, DfDv, DfDa, DmDq), plus (DsDq, DsDv, DsDa) when sensors."""
+    nv, nM, ns = self.m.nv, self.m.nM, self.m.sizes.get("nsensordata", 0)
     DfDq = np.zeros((nv, nv))
     DfDv = np.zeros((nv, nv))
     DfDa = np.zeros((nv, nv))
     DmDq = np.zeros((nv, nM)) if dmdq else None
-    self.L.or_inverseFD(*self._args(), eps, _p(DfDq), _p(DfDv), _p(DfDa), _p(DmDq))
+    Ds = [np.zeros((nv, max(ns, 1))) for _ in range(3)] if sensors else [None] * 3
+    self.L.or_inverseFD(*self._args(), eps, _p(DfDq), _p(DfDv), _p(DfDa), *map(_p, Ds),
+                        _p(DmDq))
+    if sensors:
+      return DfDq, DfDv, DfDa, DmDq, tuple(x[:, :ns] for x in Ds)
     return DfDq, DfDv, DfDa, DmDq
 
   def inverse_batch(self, qpos, qvel, qacc, nthread=1):

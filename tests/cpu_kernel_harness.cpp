@@ -80,6 +80,17 @@ static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int
 #define XSI(name, n) L.name.p = q; q += (long)(n) + 1;
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
+  // mjData fields that are device scratch: bound to the host data so tests compare them
+  L.time.p = &d->time;
+  if (mjh_needSubtreeVel(m)) {
+    L.subtree_linvel.p = d->subtree_linvel;
+    L.subtree_angmom.p = d->subtree_angmom;
+  }
+  if (mjh_needRnePost(m)) {
+    L.cacc.p = d->cacc;
+    L.cfrc_int.p = d->cfrc_int;
+    L.cfrc_ext.p = d->cfrc_ext;
+  }
   L.efc_cap = efc_cap;
   L.con_cap = con_cap;
   static unsigned long long chain[64];

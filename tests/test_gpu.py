@@ -200,6 +200,77 @@ def test_linear_system_inverse_on_gpu(linear):
   np.testing.assert_allclose(DfDv[0], np.diag(linear.dof_damping), atol=1e-6)
   np.testing.assert_allclose(DfDa[0], o.fullM(), atol=1e-6)
   np.testing.assert_allclose(DmDq[0], 0, atol=1e-6)
+  # LinearSystemInverse's sensor derivatives (engine_derivative_test.cc:843-862)
+  _, _, _, _, (DsDq, DsDv, DsDa) = e.inverse_fd(o.d.qpos[None], o.d.qvel[None],
+                                                o.d.qacc[None], eps=1e-6, sensors=True)
+  ns, adr = linear.nsensordata, linear.sensor_adr
+  exp = np.zeros((3, ns)); exp[0, adr[1]] = 1
+  np.testing.assert_allclose(DsDq[0], exp, atol=1e-6)
+  exp = np.zeros((3, ns)); exp[1, adr[0]] = 1
+  np.testing.assert_allclose(DsDv[0], exp, atol=1e-6)
+  exp = np.zeros((3, ns)); exp[0, adr[2] + 1] = 1; exp[1, adr[2] + 1] = 1
+  np.testing.assert_allclose(DsDa[0], exp, atol=1e-6)
+  e.close()
+
+
+def _sensor_model():
+  import sys
+  import os
+  sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+  from test_sensors_cpu import _all_model
+  return _all_model()
+
+
+def test_sensors_parity():
+  """Every supported sensor type (mj_sensorPos/Vel/Acc, mj_subtreeVel,
+  mj_rnePostConstraint), limit rows active, time/xfrc/actuator inputs set per instance."""
+  m = _sensor_model()
+  B = 256
+  q, v, a = sample_states(m, B, first=11, margin=-0.3, resample_tendons=False)
+  rng = np.random.default_rng(5)
+  time = 0.01 * np.arange(B)[:, None]
+  xfrc = np.zeros((B, m.nbody * 6))
+  xfrc[:, 18:24] = rng.normal(size=(B, 6))
+  af = rng.normal(size=(B, m.nu))
+  qa = rng.normal(size=(B, m.nv))
+  e = engine.InverseEngine(m, capacity=B)
+  assert e.fast_kernel is None
+  for name, val in (("time", time), ("xfrc_applied", xfrc), ("actuator_force", af),
+                    ("qfrc_actuator", qa)):
+    e.set_field(name, val)
+  e.inverse(q, v, a)
+  o = Oracle(m)
+  ref = {f: [] for f in ("sensordata", "qfrc_inverse", "subtree_linvel", "subtree_angmom",
+                         "cfrc_int", "cfrc_ext")}
+  for i in range(B):
+    o.d.time = time[i, 0]
+    o.d.xfrc_applied[:] = xfrc[i]
+    o.d.actuator_force[:] = af[i]
+    o.d.qfrc_actuator[:] = qa[i]
+    o.inverse(q[i], v[i], a[i])
+    for f in ref:
+      ref[f].append(getattr(o.d, f).copy())
+  for f, r in ref.items():
+    assert_close(e.field(f, 0, B), np.array(r), f)
+  e.close()
+
+
+def test_sensor_fd_parity():
+  """mjd_inverseFD sensor derivatives (stage-skipping semantics) vs the oracle."""
+  m = _sensor_model()
+  q, v, a = sample_states(m, 6, first=40)
+  e = engine.InverseEngine(m, capacity=6 * (3 * m.nv + 1))
+  DfDq, DfDv, DfDa, _, (DsDq, DsDv, DsDa) = e.inverse_fd(q, v, a, sensors=True)
+  o = Oracle(m)
+  for i in range(6):
+    o.set_state(q[i], v[i], a[i])
+    rq, rv, ra, _, (sq, sv, sa) = o.inverse_fd(1e-6, sensors=True)
+    for g, r in ((DfDq[i], rq), (DfDv[i], rv), (DfDa[i], ra), (DsDq[i], sq), (DsDv[i], sv),
+                 (DsDa[i], sa)):
+      np.testing.assert_allclose(g, r, rtol=1e-5, atol=1e-4)
+    # entries the reference never recomputes are exactly zero
+    stage = np.repeat(m.sensor_needstage, m.sensor_dim)
+    assert (DsDa[i][:, stage < 3] == 0).all() and (DsDv[i][:, stage < 2] == 0).all()
   e.close()
 
 
@@ -446,3 +517,27 @@ def test_energy_parity():
     ref_e.append(o.d.energy)
   assert_close(f, np.array(ref_f), "qfrc_inverse (ENERGY)")
   assert_close(en, np.array(ref_e), "energy")
+
+
+def test_single_instance_sensors_dropin():
+  """mj_inverse(m, d) drop-in with sensors: sensordata and the on-demand mjData fields
+  (subtree_linvel/angmom, cacc, cfrc_int/ext) come back into d; skipstage keeps the skipped
+  stages' sensor values (engine_inverse.c:203-242)."""
+  m = _sensor_model()
+  q, v, a = sample_states(m, 3, first=7, margin=-0.3, resample_tendons=False)
+  d = host.MjData(m)
+  o = Oracle(m)
+  for dd in (d, o.d):
+    dd.time = 1.5
+    dd.xfrc_applied[18:24] = [0.1, -0.2, 0.3, 0.01, 0.02, -0.03]
+    dd.actuator_force[:] = [0.4, -0.5]
+  d.qpos[:], d.qvel[:], d.qacc[:] = q[0], v[0], a[0]
+  engine.mj_inverse(m, d)
+  o.inverse(q[0], v[0], a[0])
+  for f in ("sensordata", "subtree_linvel", "subtree_angmom", "cacc", "cfrc_int",
+            "cfrc_ext", "qfrc_inverse"):
+    assert_close(getattr(d, f)[None], getattr(o.d, f)[None], f)
+  d.qacc[:] = a[1]
+  engine.mj_inverseSkip(m, d, engine.mjSTAGE_VEL, 0)
+  o.inverse(qacc=a[1], skipstage=2)
+  assert_close(d.sensordata[None], o.d.sensordata[None], "sensordata (skip VEL)")
