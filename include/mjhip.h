@@ -66,6 +66,7 @@ typedef unsigned char mjtByte;
 #define mjhipMAXIMP  0.9999
 #define mjhipNREF    2
 #define mjhipNIMP    5
+#define mjhipNEQDATA 11
 
 /*---------------------------- enums: same values as the reference ------------------------*/
 typedef enum mjhipDisableBit_ {      /* mjmodel.h:50-68 */
@@ -110,6 +111,11 @@ typedef enum mjhipCamLight_ {        /* mjmodel.h mjtCamLight */
   mjhipCAMLIGHT_FIXED = 0, mjhipCAMLIGHT_TRACK, mjhipCAMLIGHT_TRACKCOM,
   mjhipCAMLIGHT_TARGETBODY, mjhipCAMLIGHT_TARGETBODYCOM
 } mjhipCamLight;
+
+typedef enum mjhipEq_ {              /* mjmodel.h mjtEq */
+  mjhipEQ_CONNECT = 0, mjhipEQ_WELD, mjhipEQ_JOINT, mjhipEQ_TENDON, mjhipEQ_FLEX,
+  mjhipEQ_DISTANCE
+} mjhipEq;
 
 typedef enum mjhipWrap_ {            /* mjmodel.h:191-198 */
   mjhipWRAP_NONE = 0, mjhipWRAP_JOINT, mjhipWRAP_PULLEY, mjhipWRAP_SITE,

@@ -151,6 +151,10 @@ MJHIP_CONTACT_HD int mjhip_efcCapacity(const mjhipModel* m) {
     if (m->dof_frictionloss[i] > 0) n += 1;
   }
   if (mjhip_contactCapacity(m, &crow) > 0) n += crow;
+  for (int i = 0; i < m->neq; i++) {        /* nemax (user_model.cc): rows per equality */
+    const int t = m->eq_type[i];
+    n += t == mjhipEQ_CONNECT ? 3 : (t == mjhipEQ_WELD ? 6 : 1);
+  }
   return n;
 }
 

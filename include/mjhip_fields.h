@@ -41,7 +41,8 @@
   XS(nkey)        \
   XS(ntree)       \
   XS(nsensor)     \
-  XS(nsensordata)
+  XS(nsensordata) \
+  XS(neq)
 
 /* model arrays that live in mjModel in the reference (mjxmacro.h MJMODEL_POINTERS) */
 #define MJHIP_MODEL_POINTERS_M \
@@ -170,6 +171,14 @@
   X(mjtNum,  actuator_length0,     nu,        1) \
   X(mjtNum,  actuator_acc0,        nu,        1) \
   X(int,     exclude_signature,    nexclude,  1) \
+  X(int,     eq_type,              neq,       1) \
+  X(int,     eq_obj1id,            neq,       1) \
+  X(int,     eq_obj2id,            neq,       1) \
+  X(int,     eq_objtype,           neq,       1) \
+  X(mjtByte, eq_active0,           neq,       1) \
+  X(mjtNum,  eq_solref,            neq,       2) \
+  X(mjtNum,  eq_solimp,            neq,       5) \
+  X(mjtNum,  eq_data,              neq,       11) \
   X(int,     sensor_type,          nsensor,   1) \
   X(int,     sensor_datatype,      nsensor,   1) \
   X(int,     sensor_needstage,     nsensor,   1) \

@@ -125,7 +125,8 @@ def constraint_mode(m) -> str:
   contacts = not (dsbl & (1 << 4)) and m.nbody >= 2 and \
       bool(np.any((m.geom_contype != 0) | (m.geom_conaffinity != 0)))
   friction = bool(np.any(m.dof_frictionloss > 0)) and not (dsbl & (1 << 2))
-  if contacts or friction:
+  equality = m.sizes.get("neq", 0) > 0 and bool(np.any(m.eq_active0)) and not (dsbl & (1 << 1))
+  if contacts or friction or equality:
     return "all"
   limits = not (dsbl & (1 << 3)) and (bool(np.any(m.jnt_limited)) or
                                       bool(np.any(m.tendon_limited[:m.ntendon])))

@@ -1465,9 +1465,9 @@ MJH_HD void passive(const mjhipModel& m, const Lane<S>& d) {
 
 //---------------------------------- engine_core_constraint.c ---------------------------------
 
-// row counters of mj_makeConstraint (nefc, friction rows, limit rows; no equality rows in
-// the subset), kept in registers and written to efc_count once at the end
-struct RowCount { int nefc = 0, nf = 0, nl = 0; };
+// row counters of mj_makeConstraint (nefc, equality, friction and limit rows), kept in
+// registers and written to efc_count once at the end
+struct RowCount { int nefc = 0, ne = 0, nf = 0, nl = 0; };
 
 // mj_addConstraint :265-356 (dense): `size` rows of jac (strided scratch), contact rows are
 // never dropped as empty. Returns whether the rows were added.
@@ -1496,7 +1496,9 @@ MJH_HD bool addConstraint(const mjhipModel& m, const Lane<S>& d, RowCount& rc, S
     d.efc_id[nefc+i] = id;
   }
   rc.nefc = nefc + size;
-  if (type == CNSTR_FRICTION_DOF || type == CNSTR_FRICTION_TENDON) {
+  if (type == CNSTR_EQUALITY) {
+    rc.ne += size;
+  } else if (type == CNSTR_FRICTION_DOF || type == CNSTR_FRICTION_TENDON) {
     rc.nf += size;
   } else if (type == CNSTR_LIMIT_JOINT || type == CNSTR_LIMIT_TENDON) {
     rc.nl += size;
@@ -1658,10 +1660,10 @@ MJH_HD void rowSolParam(const mjhipModel& m, int tp, int id, double solref[2],
                         double solimp[5]) {
   const double* sr = tp == CNSTR_LIMIT_JOINT ? m.jnt_solref + 2*id :
                      (tp == CNSTR_FRICTION_DOF ? m.dof_solref + 2*id :
-                      m.tendon_solref_lim + 2*id);
+                      (tp == CNSTR_EQUALITY ? m.eq_solref + 2*id : m.tendon_solref_lim + 2*id));
   const double* si = tp == CNSTR_LIMIT_JOINT ? m.jnt_solimp + 5*id :
                      (tp == CNSTR_FRICTION_DOF ? m.dof_solimp + 5*id :
-                      m.tendon_solimp_lim + 5*id);
+                      (tp == CNSTR_EQUALITY ? m.eq_solimp + 5*id : m.tendon_solimp_lim + 5*id));
   solref[0] = sr[0]; solref[1] = sr[1];
   for (int k = 0; k < 5; k++) solimp[k] = si[k];
 }
@@ -1739,7 +1741,7 @@ MJH_HD void finishRowFused(const Lane<S>& d, int r, int tp, const double kb[4], 
       force = -frictionloss;
       state = CNSTRSTATE_LINEARPOS;
     }
-  } else if (jar >= 0) {
+  } else if (tp != CNSTR_EQUALITY && jar >= 0) {
     force = 0;
     state = CNSTRSTATE_SATISFIED;
   }
@@ -1978,6 +1980,186 @@ MJH_HD void constraintForce(const mjhipModel& m, const Lane<S>& d, int nefc) {
   }
 }
 
+// mju_mulQuatAxis engine_util_spatial.c:81-92
+template <class A> MJH_HD void mulQuatAxis(double res[4], const double q[4], A axis) {
+  const double t0 = -q[1]*axis[0] - q[2]*axis[1] - q[3]*axis[2];
+  const double t1 = q[0]*axis[0] + q[2]*axis[2] - q[3]*axis[1];
+  const double t2 = q[0]*axis[1] + q[3]*axis[0] - q[1]*axis[2];
+  const double t3 = q[0]*axis[2] + q[1]*axis[1] - q[2]*axis[0];
+  res[0] = t0; res[1] = t1; res[2] = t2; res[3] = t3;
+}
+
+// diagApprox of equality row k (0-based within its constraint) of equality `id`
+// (mj_diagApprox :1151-1197; a weld's rows 0-2 are translational, 3-5 rotational)
+MJH_HD double eqDiagApprox(const mjhipModel& m, int id, int k) {
+  const int t = m.eq_type[id];
+  if (t == mjhipEQ_CONNECT || t == mjhipEQ_WELD) {
+    int b1 = m.eq_obj1id[id], b2 = m.eq_obj2id[id];
+    if (m.eq_objtype[id] == 6) {
+      b1 = m.site_bodyid[b1];
+      b2 = m.site_bodyid[b2];
+    }
+    const int r = (t == mjhipEQ_WELD && k > 2) ? 1 : 0;
+    return m.body_invweight0[2*b1 + r] + m.body_invweight0[2*b2 + r];
+  }
+  double dA = t == mjhipEQ_JOINT ? m.dof_invweight0[m.jnt_dofadr[m.eq_obj1id[id]]] :
+                                   m.tendon_invweight0[m.eq_obj1id[id]];
+  if (m.eq_obj2id[id] >= 0) {
+    dA += t == mjhipEQ_JOINT ? m.dof_invweight0[m.jnt_dofadr[m.eq_obj2id[id]]] :
+                               m.tendon_invweight0[m.eq_obj2id[id]];
+  }
+  return dA;
+}
+
+// mj_instantiateEquality :493-764 (dense; connect, weld, joint, tendon; eq_active0). The
+// rows are formed dof by dof straight into efc_J: the two body Jacobians of mj_jacDifPair
+// (dense: mj_jac twice, then jac2 - jac1) are zero off their chains, and every other step
+// (the weld's rotational correction and torquescale) acts column by column.
+template <int S, bool FUSED>
+MJH_HD void instantiateEquality(const mjhipModel& m, const Lane<S>& d, RowCount& rc,
+                                int* status) {
+  const int nv = m.nv;
+  if ((m.opt.disableflags & mjhipDSBL_EQUALITY) || m.neq == 0) return;
+  for (int i = 0; i < m.neq; i++) {
+    if (!m.eq_active0[i]) continue;
+    const double* data = m.eq_data + mjhipNEQDATA*i;
+    const int t = m.eq_type[i];
+    const int id0 = m.eq_obj1id[i], id1 = m.eq_obj2id[i];
+    const int size = t == mjhipEQ_CONNECT ? 3 : (t == mjhipEQ_WELD ? 6 : 1);
+    const int r0 = rc.nefc;
+    if (r0 + size > d.efc_cap) {
+      *status |= MJHIP_INST_CNSTRFULL;
+      continue;
+    }
+    SP<S> J = d.efc_J + r0*nv;
+    double cpos[6];
+    if (t == mjhipEQ_CONNECT || t == mjhipEQ_WELD) {
+      double pos[2][3];
+      int body[2];
+      const int ids[2] = {id0, id1};
+      for (int j = 0; j < 2; j++) {
+        if (m.eq_objtype[i] == 1) {
+          const double* anchor = data + 3*(t == mjhipEQ_WELD ? 1 - j : j);
+          mulMatVec3(pos[j], d.xmat + 9*ids[j], anchor);
+          addTo3(pos[j], d.xpos + 3*ids[j]);
+          body[j] = ids[j];
+        } else {
+          copy3(pos[j], d.site_xpos + 3*ids[j]);
+          body[j] = m.site_bodyid[ids[j]];
+        }
+      }
+      sub3(cpos, pos[0], pos[1]);
+      double off0[3], off1[3];
+      sub3(off0, pos[0], d.subtree_com + 3*m.body_rootid[body[0]]);
+      sub3(off1, pos[1], d.subtree_com + 3*m.body_rootid[body[1]]);
+      double quat[4], quat1[4], torquescale = 0;
+      if (t == mjhipEQ_WELD) {
+        torquescale = data[10];
+        if (m.eq_objtype[i] == 1) {
+          mulQuat(quat, d.xquat + 4*id0, data + 6);
+          copy4(quat1, d.xquat + 4*id1);
+        } else {
+          mulQuat(quat, d.xquat + 4*body[0], m.site_quat + 4*id0);
+          mulQuat(quat1, d.xquat + 4*body[1], m.site_quat + 4*id1);
+        }
+        quat1[1] = -quat1[1]; quat1[2] = -quat1[2]; quat1[3] = -quat1[3];
+        double quat2[4];
+        mulQuat(quat2, quat1, quat);
+        cpos[3] = quat2[1]*torquescale;
+        cpos[4] = quat2[2]*torquescale;
+        cpos[5] = quat2[3]*torquescale;
+      }
+      for (int j = 0; j < nv; j++) {
+        const int bj = m.dof_bodyid[j];
+        const bool in0 = ancestorOrSelf(m, bj, body[0]), in1 = ancestorOrSelf(m, bj, body[1]);
+        double jp0[3] = {0, 0, 0}, jp1[3] = {0, 0, 0}, jr0[3] = {0, 0, 0}, jr1[3] = {0, 0, 0};
+        SP<S> cdof = d.cdof + 6*j;
+        double tmp[3];
+        if (in0) {
+          cross(tmp, cdof, off0);
+          jp0[0] = cdof[3] + tmp[0]; jp0[1] = cdof[4] + tmp[1]; jp0[2] = cdof[5] + tmp[2];
+          jr0[0] = cdof[0]; jr0[1] = cdof[1]; jr0[2] = cdof[2];
+        }
+        if (in1) {
+          cross(tmp, cdof, off1);
+          jp1[0] = cdof[3] + tmp[0]; jp1[1] = cdof[4] + tmp[1]; jp1[2] = cdof[5] + tmp[2];
+          jr1[0] = cdof[0]; jr1[1] = cdof[1]; jr1[2] = cdof[2];
+        }
+        for (int k = 0; k < 3; k++) J[k*nv + j] = jp0[k] - jp1[k];
+        if (t == mjhipEQ_WELD) {
+          double axis[3] = {jr0[0] - jr1[0], jr0[1] - jr1[1], jr0[2] - jr1[2]};
+          double quat2[4], quat3[4];
+          mulQuatAxis(quat2, quat1, axis);
+          mulQuat(quat3, quat2, quat);
+          for (int k = 0; k < 3; k++) J[(3 + k)*nv + j] = (0.5*quat3[1 + k])*torquescale;
+        }
+      }
+    } else {
+      // joint / tendon coupling with a quartic polynomial
+      double p0, ref0;
+      if (t == mjhipEQ_JOINT) {
+        p0 = d.qpos[m.jnt_qposadr[id0]];
+        ref0 = m.qpos0[m.jnt_qposadr[id0]];
+        zero(J, nv);
+        J[m.jnt_dofadr[id0]] = 1;
+      } else {
+        p0 = d.ten_length[id0];
+        ref0 = m.tendon_length0[id0];
+        copy(J, d.ten_J + id0*nv, nv);
+      }
+      if (id1 >= 0) {
+        double p1, ref1;
+        if (t == mjhipEQ_JOINT) {
+          p1 = d.qpos[m.jnt_qposadr[id1]];
+          ref1 = m.qpos0[m.jnt_qposadr[id1]];
+        } else {
+          p1 = d.ten_length[id1];
+          ref1 = m.tendon_length0[id1];
+        }
+        const double dif = p1 - ref1;
+        cpos[0] = p0 - ref0 - data[0] -
+                  (data[1]*dif + data[2]*dif*dif + data[3]*dif*dif*dif + data[4]*dif*dif*dif*dif);
+        const double deriv = data[1] + 2*data[2]*dif + 3*data[3]*dif*dif +
+                             4*data[4]*dif*dif*dif;
+        if (t == mjhipEQ_JOINT) {
+          const int c = m.jnt_dofadr[id1];
+          J[c] = J[c] + 1*-deriv;
+        } else {
+          addToScl(J, d.ten_J + id1*nv, -deriv, nv);
+        }
+      } else {
+        cpos[0] = p0 - ref0 - data[0];
+      }
+    }
+    // mj_addConstraint: an all-zero Jacobian adds no rows
+    bool empty = true;
+    for (int k = 0; empty && k < size*nv; k++) empty = J[k] == 0;
+    if (empty) continue;
+    for (int k = 0; k < size; k++) {
+      d.efc_pos[r0+k] = cpos[k];
+      d.efc_margin[r0+k] = 0;
+      d.efc_frictionloss[r0+k] = 0;
+      d.efc_type[r0+k] = CNSTR_EQUALITY;
+      d.efc_id[r0+k] = i;
+    }
+    rc.nefc += size;
+    rc.ne += size;
+    if constexpr (FUSED) {
+      // getposdim :1392-1422: connect/weld rows share the impedance of the block's norm
+      const double ipos = size > 1 ? sqrt(dot(cpos, cpos, size)) : cpos[0];
+      double solref[2], solimp[5], kb[4];
+      rowSolParam(m, CNSTR_EQUALITY, i, solref, solimp);
+      rowImpedance(m, CNSTR_EQUALITY, solref, solimp, ipos, 0, kb);
+      for (int k = 0; k < size; k++) {
+        const double R = dmax(MINVAL, (1-kb[2])*eqDiagApprox(m, i, k)/kb[2]);
+        SP<S> Jr = J + k*nv;
+        finishRowFused(d, r0 + k, CNSTR_EQUALITY, kb, R, cpos[k], 0, 0, dot(Jr, d.qvel, nv),
+                       dot(Jr, d.qacc, nv));
+      }
+    }
+  }
+}
+
 template <int S, bool CONTACT = true, bool FUSED = false>
 MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   int nv = m.nv;
@@ -1995,6 +2177,7 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
     }
   };
   SP<S> jacrow = d.jacp;       // one dense row of scratch
+  instantiateEquality<S, FUSED>(m, d, rc, status);
   if (!(dsbl & mjhipDSBL_FRICTIONLOSS)) {
     for (int i = 0; i < nv; i++) {
       if (m.dof_frictionloss[i] > 0) {
@@ -2055,7 +2238,8 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
     if constexpr (FUSED) instantiateContactFused(m, d, rc, status);
     else instantiateContact(m, d, rc, status);
   }
-  d.efc_count[0] = rc.nefc; d.efc_count[1] = 0; d.efc_count[2] = rc.nf; d.efc_count[3] = rc.nl;
+  d.efc_count[0] = rc.nefc; d.efc_count[1] = rc.ne; d.efc_count[2] = rc.nf;
+  d.efc_count[3] = rc.nl;
   const int nefc = rc.nefc;
   if constexpr (FUSED) {
     constraintForce(m, d, nefc);
@@ -2065,7 +2249,11 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   for (int i = 0; i < nefc; i++) {
     int id = d.efc_id[i];
     int tp = d.efc_type[i];
-    if (tp == CNSTR_FRICTION_DOF) {
+    if (tp == CNSTR_EQUALITY) {
+      const int size = m.eq_type[id] == mjhipEQ_CONNECT ? 3 : (m.eq_type[id] == mjhipEQ_WELD ? 6 : 1);
+      for (int k = 0; k < size; k++) d.efc_diagApprox[i+k] = eqDiagApprox(m, id, k);
+      i += size - 1;
+    } else if (tp == CNSTR_FRICTION_DOF) {
       d.efc_diagApprox[i] = m.dof_invweight0[id];
     } else if (tp == CNSTR_LIMIT_JOINT) {
       d.efc_diagApprox[i] = m.dof_invweight0[m.jnt_dofadr[id]];
@@ -2104,8 +2292,13 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
       rowSolParam(m, tp, id, solref, solimp);
     }
     int dim = (CONTACT && tp == CNSTR_CONTACT_PYRAMIDAL) ? 2*(d.con_dim[id]-1) : 1;
+    double ipos = d.efc_pos[i];
+    if (tp == CNSTR_EQUALITY && (m.eq_type[id] == mjhipEQ_CONNECT || m.eq_type[id] == mjhipEQ_WELD)) {
+      dim = m.eq_type[id] == mjhipEQ_WELD ? 6 : 3;      // getposdim :1392-1422
+      ipos = sqrt(dot(d.efc_pos + i, d.efc_pos + i, dim));
+    }
     double kb[4];
-    rowImpedance(m, tp, solref, solimp, d.efc_pos[i], d.efc_margin[i], kb);
+    rowImpedance(m, tp, solref, solimp, ipos, d.efc_margin[i], kb);
     for (int j = 0; j < dim; j++) {
       int r = i + j;
       d.efc_R[r] = dmax(MINVAL, (1-kb[2])*d.efc_diagApprox[r]/kb[2]);
@@ -2777,6 +2970,37 @@ MJH_HD void rnePostConstraint(const mjhipModel& m, const Lane<S>& d) {
                        cfrc, false);
       addTo(d.cfrc_ext + 6*k, cfrc_com, 6);
     }
+  }
+  // connect and weld forces (:2102-2158); joint/tendon rows apply no body force
+  const int ne = d.efc_count[1];
+  for (int i = 0; i < ne;) {
+    const int id = d.efc_id[i], t = m.eq_type[id];
+    if (t != mjhipEQ_CONNECT && t != mjhipEQ_WELD) {
+      i++;
+      continue;
+    }
+    const double* eq_data = m.eq_data + mjhipNEQDATA*id;
+    cfrc[3] = d.efc_force[i]; cfrc[4] = d.efc_force[i+1]; cfrc[5] = d.efc_force[i+2];
+    if (t == mjhipEQ_WELD) {
+      cfrc[0] = d.efc_force[i+3]; cfrc[1] = d.efc_force[i+4]; cfrc[2] = d.efc_force[i+5];
+    } else {
+      cfrc[0] = 0; cfrc[1] = 0; cfrc[2] = 0;
+    }
+    const bool body_semantic = m.eq_objtype[id] == 1;
+    for (int side = 0; side < 2; side++) {
+      const int obj = side ? m.eq_obj2id[id] : m.eq_obj1id[id];
+      const int k = body_semantic ? obj : m.site_bodyid[obj];
+      if (!k) continue;
+      const int sel = side ? (t == mjhipEQ_CONNECT) : (t == mjhipEQ_WELD);
+      const double* offset = body_semantic ? eq_data + 3*sel : m.site_pos + 3*obj;
+      double pos[3];
+      mulMatVec3(pos, d.xmat + 9*k, offset);
+      addTo3(pos, d.xpos + 3*k);
+      transformSpatial(cfrc_com, cfrc, 1, d.subtree_com + 3*m.body_rootid[k], pos, cfrc, false);
+      if (side) subFrom(d.cfrc_ext + 6*k, cfrc_com, 6);
+      else addTo(d.cfrc_ext + 6*k, cfrc_com, 6);
+    }
+    i += t == mjhipEQ_WELD ? 6 : 3;
   }
   double cacc[6], cfrc_body[6], cfrc_corr[6];
   zero(d.cfrc_int, 6);

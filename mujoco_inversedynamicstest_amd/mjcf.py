@@ -490,6 +490,7 @@ class MJCFCompiler:
     self.tendons = []
     self.actuators = []
     self.sensors = []
+    self.equalities = []
     self.excludes = []
     self.keys = []
 
@@ -602,6 +603,13 @@ class MJCFCompiler:
       elif t == "keyframe":
         for ch in el:
           self.keys.append(dict(ch.attrib))
+      elif t == "equality":
+        for ch in el:
+          if ch.tag not in ("connect", "weld", "joint", "tendon"):
+            raise MJCFError(f"equality <{ch.tag}> is not in the supported subset")
+          a = self._elem_attrs(ch, "equality", None)
+          a["__tag"] = ch.tag
+          self.equalities.append(a)
       elif t == "sensor":
         for ch in el:
           if ch.tag in SENSORS_NEXT:
@@ -1317,6 +1325,76 @@ class MJCFCompiler:
       fl = a.get("forcelimited", "auto")
       afl[ai] = (not (fr[0] == 0 and fr[1] == 0)) if fl == "auto" else (fl == "true")
       afr[ai] = fr
+    # equality constraints (xml_native_reader.cc:1898-2035, user_objects.cc:5139-5220;
+    # eq_data defaults mjs_defaultEquality user_init.c:312-319; missing body-constraint
+    # data are filled by setconst.py as mj_setConst does, engine_setconst.c:289-340)
+    neq = len(self.equalities)
+    eqt = arr("eq_type", neq, np.int32)
+    eq1 = arr("eq_obj1id", neq, np.int32, -1)
+    eq2 = arr("eq_obj2id", neq, np.int32, -1)
+    eqo = arr("eq_objtype", neq, np.int32)
+    eqa = arr("eq_active0", neq, np.uint8)
+    eqsr = arr("eq_solref", (neq, 2), np.float64)
+    eqsi = arr("eq_solimp", (neq, 5), np.float64)
+    eqd = arr("eq_data", (neq, 11), np.float64)
+    sitename = {x["name"]: i for i, x in enumerate(sites) if x["name"]}
+    tendonname = {ta.get("name"): i for i, (ta, _) in enumerate(self.tendons) if ta.get("name")}
+    for ei, a in enumerate(self.equalities):
+      tag = a["__tag"]
+      data = np.zeros(11)
+      data[1] = 1
+      data[10] = 1
+      if tag in ("connect", "weld"):
+        site = "site1" in a or "site2" in a
+        if site and ("body1" in a or "body2" in a or "anchor" in a or "relpose" in a):
+          raise MJCFError("body and site semantics cannot be mixed")
+        if "anchor" in a:
+          data[0:3] = _floats(a["anchor"])
+        elif tag == "weld" and not site:
+          data[0:3] = 0
+        if tag == "weld":
+          if "relpose" in a:
+            data[3:10] = _floats(a["relpose"])
+          if "torquescale" in a:
+            data[10] = float(a["torquescale"])
+        if site:
+          if "site1" not in a or "site2" not in a:
+            raise MJCFError("both site1 and site2 must be defined")
+          eqo[ei] = 6
+          n1, n2, table = a["site1"], a["site2"], sitename
+        else:
+          if "body1" not in a or (tag == "connect" and "anchor" not in a):
+            raise MJCFError("body1 (and anchor for connect) must be defined")
+          eqo[ei] = 1
+          n1, n2, table = a["body1"], a.get("body2"), bname
+        eqt[ei] = 0 if tag == "connect" else 1
+      else:
+        eqt[ei] = 2 if tag == "joint" else 3
+        eqo[ei] = 3 if tag == "joint" else 18
+        n1, n2 = a.get(tag + "1"), a.get(tag + "2")
+        table = jname if tag == "joint" else tendonname
+        if "polycoef" in a:
+          v = _floats(a["polycoef"])
+          data[:len(v)] = v
+      if n1 not in table or (n2 is not None and n2 not in table):
+        raise MJCFError(f"unknown element in equality constraint ({n1}, {n2})")
+      eq1[ei] = table[n1]
+      eq2[ei] = table[n2] if n2 is not None else (0 if eqo[ei] == 1 else -1)
+      if eq1[ei] == eq2[ei]:
+        raise MJCFError("element is repeated in equality constraint")
+      if tag == "joint":
+        for jj in (eq1[ei], eq2[ei]):
+          if jj >= 0 and int(jtype[jj]) not in (2, 3):
+            raise MJCFError("only scalar joints can be coupled")
+      eqa[ei] = a.get("active", "true") == "true"
+      eqsr[ei] = _floats(a["solref"]) if "solref" in a else [0.02, 1.0]
+      si = [0.9, 0.95, 0.001, 0.5, 2.0]
+      if "solimp" in a:
+        v = _floats(a["solimp"])
+        si[:len(v)] = v
+      eqsi[ei] = si
+      eqd[ei] = data
+    s.update(neq=neq)
     # sensors (user_objects.cc mjCSensor::Compile :6250-6580, user_model.cc:3265-3286)
     ns_ = len(self.sensors)
     stype = arr("sensor_type", ns_, np.int32)

@@ -14,6 +14,11 @@ SOURCES = {
     "inverse_test": "src/inverse/test.xml",                      # inverse_test.cpp model
     "linear": "test/engine/testdata/derivative/linear.xml",     # LinearSystemInverse
     "inertia": "test/engine/testdata/inertia.xml",              # FactorI / FactorIs
+    "weld": "test/engine/testdata/weld.xml",                    # equality: weld variants
+    "connect": "test/engine/testdata/connect.xml",              # equality: connect
+    "equality_site": "test/engine/testdata/equality_site.xml",  # site-semantic equalities
+    # EqualityBodySite (engine_core_constraint_test.cc:253-289)
+    "equality_compare": "test/engine/testdata/equality_site_body_compare.xml",
 }
 
 mjDSBL_CONTACT = 1 << 4

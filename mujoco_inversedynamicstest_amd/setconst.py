@@ -256,6 +256,24 @@ def set_const(m):
     mom = np.zeros(nv)
     mom[m.jnt_dofadr[jid]] = g
     m.actuator_acc0[a] = np.linalg.norm(Minv @ mom) if nv else 0.0
+  # missing eq_data of body constraints (engine_setconst.c:289-340)
+  for i in range(m.sizes.get("neq", 0)):
+    id1, id2 = m.eq_obj1id[i], m.eq_obj2id[i]
+    data = m.eq_data[i]
+    if m.eq_type[i] == 0:                   # connect
+      if m.eq_objtype[i] == 1:
+        pos = e.xmat[id1] @ data[0:3] + e.xpos[id1]
+        data[3:6] = e.xmat[id2].T @ (pos - e.xpos[id2])
+      else:
+        data[:] = 0
+    elif m.eq_type[i] == 1 and m.eq_objtype[i] == 1:   # weld, body semantic
+      if np.any(data[6:10] != 0):
+        data[6:10] = data[6:10] / np.linalg.norm(data[6:10])
+        continue
+      pos = e.xmat[id2] @ data[0:3] + e.xpos[id2]
+      data[3:6] = e.xmat[id1].T @ (pos - e.xpos[id1])
+      q1 = e.xquat[id1] * np.array([1, -1, -1, -1])
+      data[6:10] = _mulquat(q1, e.xquat[id2])
   # cameras / lights at qpos0 in fixed mode (engine_setconst.c:346-373)
   for c in range(m.ncam):
     b = m.cam_bodyid[c]

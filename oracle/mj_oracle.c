@@ -21,6 +21,9 @@
 #define mjDISABLED(x) (m->opt.disableflags & (x))
 #define mjENABLED(x) (m->opt.enableflags & (x))
 
+/* mjtObj values (mjmodel.h) */
+enum { OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
+
 /*============================ engine_util_blas.c ==========================================*/
 
 static void mju_zero3(mjtNum r[3]) { r[0] = r[1] = r[2] = 0; }
@@ -1354,11 +1357,141 @@ static void mj_addConstraint(const mjhipModel* m, orEfc* e, const mjtNum* jac, c
     e->efc_id[nefc+i] = id;
   }
   e->nefc += size;
-  if (type == orCNSTR_FRICTION_DOF || type == orCNSTR_FRICTION_TENDON) {
+  if (type == orCNSTR_EQUALITY) {
+    e->ne += size;
+  } else if (type == orCNSTR_FRICTION_DOF || type == orCNSTR_FRICTION_TENDON) {
     e->nf += size;
   } else if (type == orCNSTR_LIMIT_JOINT || type == orCNSTR_LIMIT_TENDON) {
     e->nl += size;
   }
+}
+
+/* engine_util_spatial.c:81-92 */
+static void mju_mulQuatAxis(mjtNum res[4], const mjtNum quat[4], const mjtNum axis[3]) {
+  mjtNum tmp[4] = {-quat[1]*axis[0] - quat[2]*axis[1] - quat[3]*axis[2],
+                   quat[0]*axis[0] + quat[2]*axis[2] - quat[3]*axis[1],
+                   quat[0]*axis[1] + quat[3]*axis[0] - quat[1]*axis[2],
+                   quat[0]*axis[2] + quat[1]*axis[1] - quat[2]*axis[0]};
+  res[0] = tmp[0]; res[1] = tmp[1]; res[2] = tmp[2]; res[3] = tmp[3];
+}
+
+/* mj_instantiateEquality :493-764, dense; connect, weld, joint and tendon (flex is outside
+ * the supported subset). eq_active is the model's eq_active0 (mj_resetData). */
+static void or_instantiateEquality(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  int nv = m->nv;
+  if (mjDISABLED(mjhipDSBL_EQUALITY) || m->neq == 0) return;
+  mjtNum* jac0 = (mjtNum*)calloc(6*(size_t)nv + 1, sizeof(mjtNum));
+  mjtNum* jac1 = (mjtNum*)calloc(6*(size_t)nv + 1, sizeof(mjtNum));
+  mjtNum* jacdif = (mjtNum*)calloc(6*(size_t)nv + 1, sizeof(mjtNum));
+  mjtNum* jt0 = (mjtNum*)calloc(6*(size_t)nv + 1, sizeof(mjtNum));
+  mjtNum* jt1 = (mjtNum*)calloc(6*(size_t)nv + 1, sizeof(mjtNum));
+  for (int i = 0; i < m->neq; i++) {
+    if (!m->eq_active0[i]) continue;
+    const mjtNum* data = m->eq_data + mjhipNEQDATA*i;
+    int id[2] = {m->eq_obj1id[i], m->eq_obj2id[i]}, body_id[2], size = 0;
+    mjtNum cpos[6], pos[2][3], ref[2], quat[4], quat1[4], quat2[4], quat3[4], axis[3];
+    switch (m->eq_type[i]) {
+    case mjhipEQ_CONNECT:
+      if (m->eq_objtype[i] == OBJ_BODY) {
+        for (int j = 0; j < 2; j++) {
+          mju_mulMatVec3(pos[j], d->xmat + 9*id[j], data + 3*j);
+          mju_addTo3(pos[j], d->xpos + 3*id[j]);
+          body_id[j] = id[j];
+        }
+      } else {
+        for (int j = 0; j < 2; j++) {
+          mju_copy3(pos[j], d->site_xpos + 3*id[j]);
+          body_id[j] = m->site_bodyid[id[j]];
+        }
+      }
+      mju_sub3(cpos, pos[0], pos[1]);
+      /* mj_jacDifPair(b1 = body_id[1], b2 = body_id[0]), dense: jac2 - jac1 */
+      mj_jac(m, d, jt1, NULL, pos[1], body_id[1]);
+      mj_jac(m, d, jt0, NULL, pos[0], body_id[0]);
+      mju_sub(jacdif, jt0, jt1, 3*nv);
+      mju_copy(jac0, jacdif, 3*nv);
+      size = 3;
+      break;
+    case mjhipEQ_WELD: {
+      if (m->eq_objtype[i] == OBJ_BODY) {
+        for (int j = 0; j < 2; j++) {
+          const mjtNum* anchor = data + 3*(1-j);
+          mju_mulMatVec3(pos[j], d->xmat + 9*id[j], anchor);
+          mju_addTo3(pos[j], d->xpos + 3*id[j]);
+          body_id[j] = id[j];
+        }
+      } else {
+        for (int j = 0; j < 2; j++) {
+          mju_copy3(pos[j], d->site_xpos + 3*id[j]);
+          body_id[j] = m->site_bodyid[id[j]];
+        }
+      }
+      mju_sub3(cpos, pos[0], pos[1]);
+      mjtNum torquescale = data[10];
+      mj_jac(m, d, jt1, jt1 + 3*nv, pos[1], body_id[1]);
+      mj_jac(m, d, jt0, jt0 + 3*nv, pos[0], body_id[0]);
+      mju_sub(jacdif, jt0, jt1, 3*nv);
+      mju_sub(jacdif + 3*nv, jt0 + 3*nv, jt1 + 3*nv, 3*nv);
+      mju_copy(jac0, jacdif, 3*nv);
+      mju_copy(jac0 + 3*nv, jacdif + 3*nv, 3*nv);
+      if (m->eq_objtype[i] == OBJ_BODY) {
+        mju_mulQuat(quat, d->xquat + 4*id[0], data + 6);
+        mju_copy4(quat1, d->xquat + 4*id[1]);
+      } else {
+        mjtNum qs1[4];
+        mju_mulQuat(quat, d->xquat + 4*body_id[0], m->site_quat + 4*id[0]);
+        mju_mulQuat(qs1, d->xquat + 4*body_id[1], m->site_quat + 4*id[1]);
+        mju_copy4(quat1, qs1);
+      }
+      quat1[1] = -quat1[1]; quat1[2] = -quat1[2]; quat1[3] = -quat1[3];
+      mju_mulQuat(quat2, quat1, quat);
+      mju_scl3(cpos + 3, quat2 + 1, torquescale);
+      for (int j = 0; j < nv; j++) {
+        axis[0] = jac0[3*nv + j];
+        axis[1] = jac0[4*nv + j];
+        axis[2] = jac0[5*nv + j];
+        mju_mulQuatAxis(quat2, quat1, axis);
+        mju_mulQuat(quat3, quat2, quat);
+        jac0[3*nv + j] = 0.5*quat3[1];
+        jac0[4*nv + j] = 0.5*quat3[2];
+        jac0[5*nv + j] = 0.5*quat3[3];
+      }
+      mju_scl(jac0 + 3*nv, jac0 + 3*nv, torquescale, 3*nv);
+      size = 6;
+      break;
+    }
+    case mjhipEQ_JOINT:
+    case mjhipEQ_TENDON: {
+      mjtNum* jac[2] = {jac0, jac1};
+      for (int j = 0; j < 1 + (id[1] >= 0); j++) {
+        if (m->eq_type[i] == mjhipEQ_JOINT) {
+          pos[j][0] = d->qpos[m->jnt_qposadr[id[j]]];
+          ref[j] = m->qpos0[m->jnt_qposadr[id[j]]];
+          mju_zero(jac[j], nv);
+          jac[j][m->jnt_dofadr[id[j]]] = 1;
+        } else {
+          pos[j][0] = d->ten_length[id[j]];
+          ref[j] = m->tendon_length0[id[j]];
+          mju_copy(jac[j], d->ten_J + id[j]*nv, nv);
+        }
+      }
+      if (id[1] >= 0) {
+        mjtNum dif = pos[1][0] - ref[1];
+        cpos[0] = pos[0][0] - ref[0] - data[0] -
+                  (data[1]*dif + data[2]*dif*dif + data[3]*dif*dif*dif +
+                   data[4]*dif*dif*dif*dif);
+        mjtNum deriv = data[1] + 2*data[2]*dif + 3*data[3]*dif*dif + 4*data[4]*dif*dif*dif;
+        mju_addToScl(jac0, jac1, -deriv, nv);
+      } else {
+        cpos[0] = pos[0][0] - ref[0] - data[0];
+      }
+      size = 1;
+      break;
+    }
+    }
+    if (size) mj_addConstraint(m, e, jac0, cpos, 0, 0, size, orCNSTR_EQUALITY, i);
+  }
+  free(jac0); free(jac1); free(jacdif); free(jt0); free(jt1);
 }
 
 /* mj_instantiateFriction :768-822, dof friction (dense) */
@@ -1469,9 +1602,40 @@ static void or_instantiateContact(const mjhipModel* m, mjhipData* d, orEfc* e) {
 
 /* :1138-1311 (limit, friction and contact rows) */
 static void or_diagApprox(const mjhipModel* m, orEfc* e) {
+  int weldcnt = 0;
   for (int i = 0; i < e->nefc; i++) {
-    int id = e->efc_id[i];
+    int id = e->efc_id[i], b1, b2;
     switch (e->efc_type[i]) {
+    case orCNSTR_EQUALITY:
+      switch (m->eq_type[id]) {
+      case mjhipEQ_CONNECT:
+      case mjhipEQ_WELD:
+        b1 = m->eq_obj1id[id];
+        b2 = m->eq_obj2id[id];
+        if (m->eq_objtype[id] == OBJ_SITE) {
+          b1 = m->site_bodyid[b1];
+          b2 = m->site_bodyid[b2];
+        }
+        if (m->eq_type[id] == mjhipEQ_CONNECT) {
+          e->efc_diagApprox[i] = m->body_invweight0[2*b1] + m->body_invweight0[2*b2];
+        } else {
+          e->efc_diagApprox[i] = m->body_invweight0[2*b1 + (weldcnt > 2)] +
+                                 m->body_invweight0[2*b2 + (weldcnt > 2)];
+          weldcnt = (weldcnt + 1) % 6;
+        }
+        break;
+      default:
+        e->efc_diagApprox[i] = m->eq_type[id] == mjhipEQ_JOINT ?
+            m->dof_invweight0[m->jnt_dofadr[m->eq_obj1id[id]]] :
+            m->tendon_invweight0[m->eq_obj1id[id]];
+        if (m->eq_obj2id[id] >= 0) {
+          e->efc_diagApprox[i] += m->eq_type[id] == mjhipEQ_JOINT ?
+              m->dof_invweight0[m->jnt_dofadr[m->eq_obj2id[id]]] :
+              m->tendon_invweight0[m->eq_obj2id[id]];
+        }
+        break;
+      }
+      break;
     case orCNSTR_FRICTION_DOF:
       e->efc_diagApprox[i] = m->dof_invweight0[id];
       break;
@@ -1512,6 +1676,10 @@ static void getsolparam(const mjhipModel* m, const orEfc* e, int i, mjtNum* solr
   int id = e->efc_id[i];
   mju_zero(solreffriction, 2);
   switch (e->efc_type[i]) {
+  case orCNSTR_EQUALITY:
+    mju_copy(solref, m->eq_solref+2*id, 2);
+    mju_copy(solimp, m->eq_solimp+5*id, 5);
+    break;
   case orCNSTR_CONTACT_FRICTIONLESS:
   case orCNSTR_CONTACT_PYRAMIDAL:
   case orCNSTR_CONTACT_ELLIPTIC:
@@ -1600,8 +1768,17 @@ static void or_makeImpedance(const mjhipModel* m, orEfc* e) {
   mjtNum imp, impP, solref[2], solreffriction[2], solimp[5];
   for (int i = 0; i < nefc; i++) {
     getsolparam(m, e, i, solref, solreffriction, solimp);
+    /* getposdim :1392-1422 */
     int dim = e->efc_type[i] == orCNSTR_CONTACT_PYRAMIDAL ? 2*(e->con_dim[e->efc_id[i]]-1) : 1;
-    getimpedance(solimp, e->efc_pos[i], e->efc_margin[i], &imp, &impP);
+    mjtNum pos = e->efc_pos[i];
+    if (e->efc_type[i] == orCNSTR_EQUALITY) {
+      int t = m->eq_type[e->efc_id[i]];
+      if (t == mjhipEQ_WELD || t == mjhipEQ_CONNECT) {
+        dim = t == mjhipEQ_WELD ? 6 : 3;
+        pos = mju_norm(e->efc_pos + i, dim);
+      }
+    }
+    getimpedance(solimp, pos, e->efc_margin[i], &imp, &impP);
     for (int j = 0; j < dim; j++) {
       int r = i + j, tp = e->efc_type[r];
       R[r] = mjMAX(mjMINVAL, (1-imp)*e->efc_diagApprox[r]/imp);
@@ -1646,6 +1823,7 @@ static void or_makeConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
   e->ne = e->nf = e->nl = e->nefc = 0;
   if (mjDISABLED(mjhipDSBL_CONSTRAINT)) return;
   mjtNum* jac = (mjtNum*)malloc((m->nv > 0 ? m->nv : 1)*sizeof(mjtNum));
+  or_instantiateEquality(m, d, e);
   or_instantiateFriction(m, d, e, jac);
   or_instantiateLimit(m, d, e, jac);
   free(jac);
@@ -2111,7 +2289,6 @@ enum { SENS_TOUCH = 0, SENS_ACCELEROMETER, SENS_VELOCIMETER, SENS_GYRO, SENS_FOR
        SENS_FRAMEANGACC, SENS_SUBTREECOM, SENS_SUBTREELINVEL, SENS_SUBTREEANGMOM,
        SENS_GEOMDIST, SENS_GEOMNORMAL, SENS_GEOMFROMTO, SENS_E_POTENTIAL, SENS_E_KINETIC,
        SENS_CLOCK };
-enum { OBJ_BODY = 1, OBJ_XBODY = 2, OBJ_GEOM = 5, OBJ_SITE = 6, OBJ_CAMERA = 7 };
 enum { DATATYPE_REAL = 0, DATATYPE_POSITIVE = 1 };
 
 /* engine_util_blas.c:179-188 */
@@ -2281,6 +2458,36 @@ static void or_rnePostConstraint(const mjhipModel* m, mjhipData* d, const orEfc*
       mju_transformSpatial(cfrc_com, cfrc, 1, d->subtree_com + 3*m->body_rootid[k],
                            e->con_pos + 3*i, NULL);
       mju_addTo(d->cfrc_ext + 6*k, cfrc_com, 6);
+    }
+  }
+  /* connect and weld forces (:2102-2158); joint/tendon rows apply no body force */
+  for (int i = 0; i < e->ne;) {
+    int id = e->efc_id[i], t = m->eq_type[id];
+    const mjtNum* eq_data = m->eq_data + mjhipNEQDATA*id;
+    if (t == mjhipEQ_CONNECT || t == mjhipEQ_WELD) {
+      mjtNum pos[3], *offset;
+      mju_copy3(cfrc + 3, e->efc_force + i);
+      if (t == mjhipEQ_WELD) mju_copy3(cfrc, e->efc_force + i + 3);
+      else mju_zero3(cfrc);
+      int body_semantic = m->eq_objtype[id] == OBJ_BODY;
+      int obj1 = m->eq_obj1id[id], k = body_semantic ? obj1 : m->site_bodyid[obj1];
+      if (k) {
+        offset = body_semantic ? (mjtNum*)eq_data + 3*(t == mjhipEQ_WELD) : m->site_pos + 3*obj1;
+        mj_local2Global(d, pos, 0, offset, 0, k, 0);
+        mju_transformSpatial(cfrc_com, cfrc, 1, d->subtree_com + 3*m->body_rootid[k], pos, NULL);
+        mju_addTo(d->cfrc_ext + 6*k, cfrc_com, 6);
+      }
+      int obj2 = m->eq_obj2id[id];
+      k = body_semantic ? obj2 : m->site_bodyid[obj2];
+      if (k) {
+        offset = body_semantic ? (mjtNum*)eq_data + 3*(t == mjhipEQ_CONNECT) : m->site_pos + 3*obj2;
+        mj_local2Global(d, pos, 0, offset, 0, k, 0);
+        mju_transformSpatial(cfrc_com, cfrc, 1, d->subtree_com + 3*m->body_rootid[k], pos, NULL);
+        mju_subFrom(d->cfrc_ext + 6*k, cfrc_com, 6);
+      }
+      i += t == mjhipEQ_WELD ? 6 : 3;
+    } else {
+      i++;
     }
   }
   mjtNum cacc[6], cfrc_body[6], cfrc_corr[6];

@@ -11,6 +11,9 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD = os.path.join(HERE, "_build")
 SO = os.path.join(BUILD, "libkernel_cpu.so")
 SRC = [os.path.join(HERE, "cpu_kernel_harness.cpp"),
+       os.path.join(HERE, "..", "include", "mjhip.h"),
+       os.path.join(HERE, "..", "include", "mjhip_fields.h"),
+       os.path.join(HERE, "..", "include", "mjhip_contact.h"),
        os.path.join(HERE, "..", "mujoco_inversedynamicstest_amd", "csrc", "engine_device.h")]
 
 _lib = None

@@ -22,7 +22,15 @@ BUILD = os.path.join(HERE, "_build")
 
 def build(m, name):
   src = codegen.generate(m, name)
-  tag = hashlib.sha1(src.encode()).hexdigest()[:10]
+  h = hashlib.sha1(src.encode())
+  # the harness also compiles the device header and the field tables: key the cache on them
+  for dep in (os.path.join(HERE, "..", "mujoco_inversedynamicstest_amd", "csrc", "engine_device.h"),
+              os.path.join(HERE, "..", "include", "mjhip.h"),
+              os.path.join(HERE, "..", "include", "mjhip_fields.h"),
+              os.path.join(HERE, "..", "include", "mjhip_contact.h"),
+              os.path.join(HERE, "codegen_harness.cpp")):
+    h.update(open(dep, "rb").read())
+  tag = h.hexdigest()[:10]
   os.makedirs(BUILD, exist_ok=True)
   inc = os.path.join(BUILD, f"gen_{name}_{tag}.inc")
   so = os.path.join(BUILD, f"libcg_{name}_{tag}.so")
@@ -126,3 +134,28 @@ def test_friction_loss_generated_bitexact():
   assert codegen.constraint_mode(m) == "all"
   q, v, a = sample_states(m, 32, first=17)
   run_and_compare(m, "humanoid_friction", q, v, a)
+
+
+def test_generated_with_equality_constraints():
+  """Active equality constraints put every instance through the constraint kernel
+  (constraint_mode 'all'): connect, weld (body and site semantics), joint and tendon."""
+  xml = """<mujoco><option><flag contact="disable"/></option><worldbody>
+    <site name="w" pos=".3 .1 1" euler="10 0 0"/>
+    <body name="a" pos="0 0 1"><freejoint/><geom type="box" size=".1 .2 .05"/>
+      <site name="as" pos=".1 0 0"/>
+      <body name="b" pos=".2 0 0"><joint name="h1" axis="0 1 0"/>
+        <geom type="capsule" fromto="0 0 0 .3 0 0" size=".04"/>
+        <body name="c" pos=".3 0 0"><joint name="h2" axis="0 0 1"/>
+          <geom type="sphere" size=".05"/></body></body></body>
+    <body name="d" pos="1 0 1"><joint name="s" type="slide" axis="0 0 1"/>
+      <geom size=".1"/></body></worldbody>
+    <tendon><fixed name="t"><joint joint="h1" coef="1"/><joint joint="s" coef="-1"/></fixed>
+    </tendon>
+    <equality><connect body1="c" body2="d" anchor=".05 0 0"/>
+      <weld body1="a" torquescale=".3"/><weld site1="w" site2="as" solref=".03 1"/>
+      <joint joint1="h1" joint2="h2" polycoef="0 .5 0 0 0"/>
+      <tendon tendon1="t" polycoef=".01"/></equality></mujoco>"""
+  m = mjcf.load_xml_string(xml)
+  assert codegen.constraint_mode(m) == "all"
+  q, v, a = sample_states(m, 16, first=3)
+  run_and_compare(m, "equality", q, v, a)

@@ -541,3 +541,37 @@ def test_single_instance_sensors_dropin():
   engine.mj_inverseSkip(m, d, engine.mjSTAGE_VEL, 0)
   o.inverse(qacc=a[1], skipstage=2)
   assert_close(d.sensordata[None], o.d.sensordata[None], "sensordata (skip VEL)")
+
+
+@pytest.mark.parametrize("name", ["weld", "connect", "equality_site", "equality_compare"])
+def test_equality_parity(name):
+  """Equality constraints (connect, weld; body and site semantics; force/torque sensors
+  through mj_rnePostConstraint's equality branch) on the device vs the oracle. The test
+  models' viscosity is zeroed (fluid forces are outside the subset)."""
+  m = models.load(name)
+  m.opt["viscosity"] = 0.0
+  B = 512
+  q, v, a = sample_states(m, B, first=17)
+  e = engine.InverseEngine(m, capacity=B)
+  f, st = e.inverse(q, v, a, status=True)
+  assert (st == 0).all()
+  efc_g = e.field_int("efc_count", 0, B)
+  gforce = e.field("efc_force", 0, B)
+  gint = {n: e.field_int(n, 0, B) for n in ("efc_type", "efc_id", "efc_state")}
+  o = Oracle(m)
+  ref = {k: [] for k in ("qfrc_inverse", "qfrc_constraint", "sensordata")}
+  for i in range(B):
+    o.inverse(q[i], v[i], a[i])
+    for k in ref:
+      ref[k].append(getattr(o.d, k).copy())
+    assert efc_g[i, 0] == o.efc.nefc and efc_g[i, 1] == o.efc.ne
+    for n in gint:
+      np.testing.assert_array_equal(gint[n][i][:o.efc.nefc], o.efc_field(n))
+    fr = o.efc_field("efc_force")
+    assert np.abs(gforce[i][:o.efc.nefc] - fr).max() <= RTOL * max(1.0, np.abs(fr).max())
+  assert_close(f, np.array(ref["qfrc_inverse"]), "qfrc_inverse")
+  assert_close(e.field("qfrc_constraint", 0, B), np.array(ref["qfrc_constraint"]),
+               "qfrc_constraint")
+  if m.nsensordata:
+    assert_close(e.field("sensordata", 0, B), np.array(ref["sensordata"]), "sensordata")
+  e.close()
