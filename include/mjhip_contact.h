@@ -13,7 +13,7 @@
  * The broadphase's bounding boxes are inflated by each geom's rbound + margin, so they never
  * reject a pair the narrowphase would report. A body pair is therefore a candidate exactly
  * when it passes the static rules below. mj_collision processes candidates in signature
- * order ((b1 << 16) + b2, b1 < b2), and each primitive pair yields at most 2 contacts.
+ * order ((b1 << 16) + b2, b1 < b2); mjhip_pairMaxContacts bounds each primitive pair.
  */
 #ifndef MJHIP_CONTACT_H_
 #define MJHIP_CONTACT_H_
@@ -84,6 +84,8 @@ MJHIP_CONTACT_HD int mjhip_pairMaxContacts(int t1, int t2) {
   if (t1 == mjhipGEOM_PLANE && t2 <= mjhipGEOM_HFIELD) return 0;
   if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) return 1;
   if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CAPSULE) return 2;
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CYLINDER) return 4;
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_BOX) return 4;
   if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_SPHERE) return 1;
   if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CAPSULE) return 1;
   if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) return 2;

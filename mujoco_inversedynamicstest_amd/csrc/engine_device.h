@@ -654,6 +654,98 @@ MJH_HD void putRaw(RawContact* c, int k, const RawContact& t) {
   }
 }
 
+// engine_collision_primitive.c:95-195 mjc_PlaneCylinder; each contact goes to emit() as it
+// is made (up to 4), so no contact array is kept
+template <class P1, class M1, class P2, class M2, class E>
+MJH_HD void colPlaneCylinder(double margin, P1 pos1, M1 mat1, P2 pos2, M2 mat2,
+                             const double* size2, E&& emit) {
+  double normal[3] = {mat1[2], mat1[5], mat1[8]};
+  double axis[3] = {mat2[2], mat2[5], mat2[8]};
+  double prjaxis = dot3(normal, axis);
+  if (prjaxis > 0) {
+    scl3(axis, axis, -1);
+    prjaxis = -prjaxis;
+  }
+  double vec[3] = {pos2[0] - pos1[0], pos2[1] - pos1[1], pos2[2] - pos1[2]};
+  const double dist0 = dot3(vec, normal);
+  scl3(vec, axis, prjaxis);
+  vec[0] -= normal[0]; vec[1] -= normal[1]; vec[2] -= normal[2];
+  const double len_sqr = dot3(vec, vec);
+  if (len_sqr >= MINVAL*MINVAL) {
+    const double scl = size2[0]/sqrt(len_sqr);
+    vec[0] *= scl; vec[1] *= scl; vec[2] *= scl;
+  } else {
+    vec[0] = mat2[0]*size2[0];
+    vec[1] = mat2[3]*size2[0];
+    vec[2] = mat2[6]*size2[0];
+  }
+  const double prjvec = dot3(vec, normal);
+  scl3(axis, axis, size2[1]);
+  prjaxis *= size2[1];
+  RawContact c;
+  for (int k = 0; k < 3; k++) c.frame[k] = normal[k];
+  c.frame[3] = 0; c.frame[4] = 0; c.frame[5] = 0;
+  for (int k = 6; k < 9; k++) c.frame[k] = 0;
+  if (!(dist0 + prjaxis + prjvec <= margin)) return;
+  c.dist = dist0 + prjaxis + prjvec;
+  add3(c.pos, pos2, vec);
+  addTo3(c.pos, axis);
+  addToScl3(c.pos, normal, -c.dist*0.5);
+  if (!emit(c)) return;
+  if (dist0 - prjaxis + prjvec <= margin) {
+    c.dist = dist0 - prjaxis + prjvec;
+    add3(c.pos, pos2, vec);
+    c.pos[0] -= axis[0]; c.pos[1] -= axis[1]; c.pos[2] -= axis[2];
+    addToScl3(c.pos, normal, -c.dist*0.5);
+    if (!emit(c)) return;
+  }
+  const double prjvec1 = -prjvec*0.5;
+  if (dist0 + prjaxis + prjvec1 <= margin) {
+    double vec1[3];
+    cross(vec1, vec, axis);
+    normalize3(vec1);
+    scl3(vec1, vec1, size2[0]*sqrt(3.0)/2);
+    c.dist = dist0 + prjaxis + prjvec1;
+    add3(c.pos, pos2, vec1);
+    addTo3(c.pos, axis);
+    addToScl3(c.pos, vec, -0.5);
+    addToScl3(c.pos, normal, -c.dist*0.5);
+    if (!emit(c)) return;
+    c.dist = dist0 + prjaxis + prjvec1;
+    sub3(c.pos, pos2, vec1);
+    addTo3(c.pos, axis);
+    addToScl3(c.pos, vec, -0.5);
+    addToScl3(c.pos, normal, -c.dist*0.5);
+    emit(c);
+  }
+}
+
+// engine_collision_primitive.c:200-243 mjc_PlaneBox: the (up to 4) lowest corners
+template <class P1, class M1, class P2, class M2, class E>
+MJH_HD void colPlaneBox(double margin, P1 pos1, M1 mat1, P2 pos2, M2 mat2, const double* size2,
+                        E&& emit) {
+  const double norm[3] = {mat1[2], mat1[5], mat1[8]};
+  const double dif[3] = {pos2[0] - pos1[0], pos2[1] - pos1[1], pos2[2] - pos1[2]};
+  const double dist = dot3(dif, norm);
+  RawContact c;
+  for (int k = 0; k < 3; k++) c.frame[k] = norm[k];
+  for (int k = 3; k < 9; k++) c.frame[k] = 0;
+  int cnt = 0;
+  for (int i = 0; i < 8; i++) {
+    double vec[3] = {(i&1) ? size2[0] : -size2[0], (i&2) ? size2[1] : -size2[1],
+                     (i&4) ? size2[2] : -size2[2]};
+    double corner[3];
+    mulMatVec3(corner, mat2, vec);
+    const double ldist = dot3(norm, corner);
+    if (dist + ldist > margin || ldist > 0) continue;
+    c.dist = dist + ldist;
+    addTo3(corner, pos2);
+    scl3(vec, norm, -c.dist/2);
+    add3(c.pos, corner, vec);
+    if (!emit(c) || ++cnt >= 4) return;
+  }
+}
+
 // engine_collision_primitive.c mjraw_PlaneSphere
 template <class P1, class M1, class P2>
 MJH_HD int rawPlaneSphere(RawContact* c, double margin, P1 pos1, M1 mat1, P2 pos2, double r2) {
@@ -867,6 +959,10 @@ MJH_HD int filterSphere(const mjhipModel& m, const Lane<S>& d, int g1, int g2, d
 
 // mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
 template <int S>
+MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
+                               double margin, int& ncon, int* status);
+
+template <int S>
 MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, int& ncon,
                          int* status) {
   if (m.geom_type[g1] > m.geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
@@ -880,6 +976,10 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
   double margin = ovr ? m.opt.o_margin : (m.geom_margin[g1] > m.geom_margin[g2] ?
                                           m.geom_margin[g1] : m.geom_margin[g2]);
   if (filterSphere(m, d, g1, g2, margin)) return;
+  if (t1 == mjhipGEOM_PLANE && (t2 == mjhipGEOM_BOX || t2 == mjhipGEOM_CYLINDER)) {
+    collidePlaneBoxCyl(m, d, g1, g2, margin, ncon, status);
+    return;
+  }
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
   SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
   const double *size1 = m.geom_size + 3*g1, *size2 = m.geom_size + 3*g2;
@@ -933,6 +1033,51 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
   };
   if (store(raw[0]) && num > 1) store(raw[1]);   // num <= 2; constant indices keep raw[]
 }                                                // in registers
+
+// plane : box / cylinder (up to 4 contacts each): contacts are stored as they are made
+template <int S>
+MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
+                               double margin, int& ncon, int* status) {
+  const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
+  SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
+  SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
+  const double* size2 = m.geom_size + 3*g2;
+  int condim;
+  double gap, solref[2], solimp[5], friction[5];
+  contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
+  auto store = [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
+    int i = ncon;
+    if (i >= d.con_cap) {
+      *status |= MJHIP_INST_CNSTRFULL;
+      return false;
+    }
+    double frame[9];
+    for (int j = 0; j < 9; j++) frame[j] = rk.frame[j];
+    d.con_dist[i] = rk.dist;
+    copy3(d.con_pos + 3*i, rk.pos);
+    d.con_geom[2*i] = g1;
+    d.con_geom[2*i+1] = g2;
+    d.con_dim[i] = condim;
+    double includemargin = margin - gap;
+    d.con_includemargin[i] = includemargin;
+    for (int j = 0; j < 2; j++) d.con_solref[2*i+j] = ovr ? m.opt.o_solref[j] : solref[j];
+    for (int j = 0; j < 2; j++) d.con_solreffriction[2*i+j] = ovr ? m.opt.o_solref[j] : 0.0;
+    for (int j = 0; j < 5; j++) d.con_solimp[5*i+j] = ovr ? m.opt.o_solimp[j] : solimp[j];
+    for (int j = 0; j < 5; j++) {
+      double f = ovr ? m.opt.o_friction[j] : friction[j];
+      d.con_friction[5*i+j] = f > 1e-5 ? f : 1e-5;      // mjMINMU
+    }
+    d.con_exclude[i] = rk.dist >= includemargin;
+    makeFrame(frame);
+    for (int j = 0; j < 9; j++) d.con_frame[9*i+j] = frame[j];
+    d.con_efc_address[i] = -1;
+    d.con_mu[i] = 0;
+    ncon = i + 1;
+    return true;
+  };
+  if (m.geom_type[g2] == mjhipGEOM_BOX) colPlaneBox(margin, pos1, mat1, pos2, mat2, size2, store);
+  else colPlaneCylinder(margin, pos1, mat1, pos2, mat2, size2, store);
+}
 
 // contactcompare (engine_collision_driver.c:223-257) on two contacts' geom ids
 template <int S>

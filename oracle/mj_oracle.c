@@ -1012,6 +1012,106 @@ static mjtNum mju_clip(mjtNum x, mjtNum lo, mjtNum hi) { return x < lo ? lo : (x
 /* one narrowphase result before the contact parameters are attached */
 typedef struct { mjtNum dist, pos[3], frame[9]; } orRaw;
 
+/* engine_collision_primitive.c:95-195 mjc_PlaneCylinder */
+static int col_planeCylinder(orRaw* con, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
+                             const mjtNum* pos2, const mjtNum* mat2, const mjtNum* size2) {
+  mjtNum normal[3] = {mat1[2], mat1[5], mat1[8]};
+  mjtNum axis[3] = {mat2[2], mat2[5], mat2[8]};
+  mjtNum prjaxis = mju_dot3(normal, axis);
+  if (prjaxis > 0) {
+    mju_scl3(axis, axis, -1);
+    prjaxis = -prjaxis;
+  }
+  mjtNum vec[3] = {pos2[0] - pos1[0], pos2[1] - pos1[1], pos2[2] - pos1[2]};
+  mjtNum dist0 = mju_dot3(vec, normal);
+  mju_scl3(vec, axis, prjaxis);
+  vec[0] -= normal[0]; vec[1] -= normal[1]; vec[2] -= normal[2];
+  mjtNum len_sqr = mju_dot3(vec, vec);
+  if (len_sqr >= mjMINVAL*mjMINVAL) {
+    mjtNum scl = size2[0]/sqrt(len_sqr);
+    vec[0] *= scl; vec[1] *= scl; vec[2] *= scl;
+  } else {
+    vec[0] = mat2[0]*size2[0];
+    vec[1] = mat2[3]*size2[0];
+    vec[2] = mat2[6]*size2[0];
+  }
+  mjtNum prjvec = mju_dot3(vec, normal);
+  mju_scl3(axis, axis, size2[1]);
+  prjaxis *= size2[1];
+  int cnt = 0;
+  if (dist0 + prjaxis + prjvec <= margin) {
+    con[cnt].dist = dist0 + prjaxis + prjvec;
+    mju_add3(con[cnt].pos, pos2, vec);
+    mju_addTo3(con[cnt].pos, axis);
+    mju_addToScl3(con[cnt].pos, normal, -con[cnt].dist*0.5);
+    mju_copy3(con[cnt].frame, normal);
+    mju_zero3(con[cnt].frame+3);
+    cnt++;
+  } else {
+    return 0;
+  }
+  if (dist0 - prjaxis + prjvec <= margin) {
+    con[cnt].dist = dist0 - prjaxis + prjvec;
+    mju_add3(con[cnt].pos, pos2, vec);
+    con[cnt].pos[0] -= axis[0]; con[cnt].pos[1] -= axis[1]; con[cnt].pos[2] -= axis[2];
+    mju_addToScl3(con[cnt].pos, normal, -con[cnt].dist*0.5);
+    mju_copy3(con[cnt].frame, normal);
+    mju_zero3(con[cnt].frame+3);
+    cnt++;
+  }
+  mjtNum prjvec1 = -prjvec*0.5;
+  if (dist0 + prjaxis + prjvec1 <= margin) {
+    mjtNum vec1[3];
+    mju_cross(vec1, vec, axis);
+    mju_normalize3(vec1);
+    mju_scl3(vec1, vec1, size2[0]*sqrt(3.0)/2);
+    con[cnt].dist = dist0 + prjaxis + prjvec1;
+    mju_add3(con[cnt].pos, pos2, vec1);
+    mju_addTo3(con[cnt].pos, axis);
+    mju_addToScl3(con[cnt].pos, vec, -0.5);
+    mju_addToScl3(con[cnt].pos, normal, -con[cnt].dist*0.5);
+    mju_copy3(con[cnt].frame, normal);
+    mju_zero3(con[cnt].frame+3);
+    cnt++;
+    con[cnt].dist = dist0 + prjaxis + prjvec1;
+    mju_sub3(con[cnt].pos, pos2, vec1);
+    mju_addTo3(con[cnt].pos, axis);
+    mju_addToScl3(con[cnt].pos, vec, -0.5);
+    mju_addToScl3(con[cnt].pos, normal, -con[cnt].dist*0.5);
+    mju_copy3(con[cnt].frame, normal);
+    mju_zero3(con[cnt].frame+3);
+    cnt++;
+  }
+  return cnt;
+}
+
+/* engine_collision_primitive.c:200-243 mjc_PlaneBox */
+static int col_planeBox(orRaw* con, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
+                        const mjtNum* pos2, const mjtNum* mat2, const mjtNum* size2) {
+  mjtNum norm[3] = {mat1[2], mat1[5], mat1[8]};
+  mjtNum dif[3] = {pos2[0] - pos1[0], pos2[1] - pos1[1], pos2[2] - pos1[2]};
+  mjtNum dist = mju_dot3(dif, norm);
+  int cnt = 0;
+  for (int i = 0; i < 8; i++) {
+    mjtNum vec[3];
+    vec[0] = (i&1 ? size2[0] : -size2[0]);
+    vec[1] = (i&2 ? size2[1] : -size2[1]);
+    vec[2] = (i&4 ? size2[2] : -size2[2]);
+    mjtNum corner[3];
+    mju_mulMatVec3(corner, mat2, vec);
+    mjtNum ldist = mju_dot3(norm, corner);
+    if (dist + ldist > margin || ldist > 0) continue;
+    con[cnt].dist = dist + ldist;
+    mju_copy3(con[cnt].frame, norm);
+    mju_zero3(con[cnt].frame+3);
+    mju_addTo3(corner, pos2);
+    mju_scl3(vec, norm, -con[cnt].dist/2);
+    mju_add3(con[cnt].pos, corner, vec);
+    if (++cnt >= 4) return 4;
+  }
+  return cnt;
+}
+
 /* engine_collision_primitive.c mjraw_PlaneSphere */
 static int raw_planeSphere(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
                            const mjtNum* pos2, mjtNum r2) {
@@ -1232,9 +1332,13 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
   const mjtNum *pos1 = d->geom_xpos + 3*g1, *mat1 = d->geom_xmat + 9*g1;
   const mjtNum *pos2 = d->geom_xpos + 3*g2, *mat2 = d->geom_xmat + 9*g2;
   const mjtNum *size1 = m->geom_size + 3*g1, *size2 = m->geom_size + 3*g2;
-  orRaw raw[2];
+  orRaw raw[4];
   int num = 0;
-  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) {
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CYLINDER) {
+    num = col_planeCylinder(raw, margin, pos1, mat1, pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_BOX) {
+    num = col_planeBox(raw, margin, pos1, mat1, pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) {
     num = raw_planeSphere(raw, margin, pos1, mat1, pos2, size2[0]);
   } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CAPSULE) {
     num = col_planeCapsule(raw, margin, pos1, mat1, pos2, mat2, size2);

@@ -161,8 +161,91 @@ def test_capsule_capsule_crossing_and_sphere_sphere():
   np.testing.assert_allclose(o.contact_field("con_pos")[1], [2, 0, 0.15], atol=1e-15)
 
 
+def test_plane_box_four_lowest_corners():
+  """mjc_PlaneBox (engine_collision_primitive.c:200-243): a level box below its half height
+  touches at its 4 bottom corners, each midway into the gap; a tilted box at the corners
+  under the margin, at most 4."""
+  m, o = _one_contact("""<mujoco><worldbody><geom type="plane" size="1 1 1"/>
+    <body pos=".1 .2 .08"><freejoint/><geom type="box" size=".3 .2 .1"/></body>
+    </worldbody></mujoco>""")
+  assert o.efc.ncon == 4
+  np.testing.assert_allclose(o.contact_field("con_dist"), [-0.02] * 4, atol=1e-15)
+  pos = o.contact_field("con_pos")
+  np.testing.assert_allclose(sorted(map(tuple, np.round(pos, 12))),
+                             sorted((0.1 + sx * 0.3, 0.2 + sy * 0.2, -0.01)
+                                    for sx in (-1, 1) for sy in (-1, 1)), atol=1e-12)
+  m, o = _one_contact("""<mujoco><worldbody><geom type="plane" size="1 1 1"/>
+    <body pos="0 0 .15" euler="0 30 0"><freejoint/><geom type="box" size=".3 .2 .1"/></body>
+    </worldbody></mujoco>""")
+  # the two corners of the lowered edge: z = .15 - .3 sin30 - .1 cos30 < 0
+  assert o.efc.ncon == 2
+  np.testing.assert_allclose(o.contact_field("con_dist"),
+                             [0.15 - 0.3 * 0.5 - 0.1 * np.cos(np.pi / 6)] * 2, atol=1e-12)
+
+
+def test_plane_cylinder_disk_triangle():
+  """mjc_PlaneCylinder (engine_collision_primitive.c:95-195): an upright cylinder sinking
+  into the plane touches at a rim point and the two triangle points (3 contacts)."""
+  m, o = _one_contact("""<mujoco><worldbody><geom type="plane" size="1 1 1"/>
+    <body pos="0 0 .18"><freejoint/><geom type="cylinder" size=".1 .2"/></body>
+    </worldbody></mujoco>""")
+  assert o.efc.ncon == 3
+  np.testing.assert_allclose(o.contact_field("con_dist"), [-0.02] * 3, atol=1e-15)
+  r = 0.1
+  np.testing.assert_allclose(o.contact_field("con_pos"),
+                             [[r, 0, -0.01], [-r / 2, r * np.sqrt(3) / 2, -0.01],
+                              [-r / 2, -r * np.sqrt(3) / 2, -0.01]], atol=1e-15)
+  # lying on its side: both rim ends of the lowest line, no triangle points
+  m, o = _one_contact("""<mujoco><worldbody><geom type="plane" size="1 1 1"/>
+    <body pos="0 0 .09" euler="90 0 0"><freejoint/><geom type="cylinder" size=".1 .2"/></body>
+    </worldbody></mujoco>""")
+  assert o.efc.ncon == 2
+  np.testing.assert_allclose(o.contact_field("con_dist"), [-0.01, -0.01], atol=1e-15)
+
+
+def test_box_cylinder_device_bitexact():
+  """Random poses of boxes and cylinders over a plane (condim 1/3/6): the device code on the
+  host equals the oracle bit for bit on every contact, row and output."""
+  m = mjcf.load_xml_string("""<mujoco><default><geom contype="1" conaffinity="2"/></default>
+    <worldbody><geom type="plane" size="3 3 .1" contype="2" conaffinity="1"/>
+    <body pos="0 0 .1"><freejoint/><geom type="box" size=".2 .1 .05" condim="1"/></body>
+    <body pos=".8 0 .1"><freejoint/><geom type="cylinder" size=".1 .15" condim="6"/></body>
+    <body pos="-.8 0 .1"><freejoint/><geom type="box" size=".1 .1 .1"/>
+      <body pos="0 0 .2"><joint axis="1 0 0"/><geom type="cylinder" size=".05 .1"
+        pos="0 0 .1"/></body></body>
+  </worldbody></mujoco>""")
+  rng = np.random.default_rng(11)
+  o, k = Oracle(m), KernelCPU(m)
+  total = 0
+  for i in range(40):
+    q = m.qpos0.copy()
+    for b in range(3):
+      q[7 * b + 2] = 0.05 + 0.1 * rng.random()
+      qq = rng.normal(size=4)
+      q[7 * b + 3:7 * b + 7] = qq / np.linalg.norm(qq)
+    q[21] = rng.normal()
+    v, a = rng.normal(size=m.nv), rng.normal(size=m.nv)
+    o.inverse(q, v, a)
+    k.inverse(q, v, a)
+    ncon = o.efc.ncon
+    total += ncon
+    assert k.field("con_count")[0] == ncon
+    width = dict(CON_DOUBLE + CON_INT)
+    for name in CON_FIELDS:
+      ref = o.contact_field(name).reshape(ncon, width[name])
+      np.testing.assert_array_equal(k.field(name)[:ref.size].reshape(ncon, width[name]), ref,
+                                    err_msg=f"{name} inst {i}")
+    for name in EFC_FIELDS:
+      ref = o.efc_field(name)
+      np.testing.assert_array_equal(k.field(name)[:ref.size], ref, err_msg=f"{name} inst {i}")
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name))
+  assert total > 60
+
+
 def test_unsupported_pair_rejected():
-  m = mjcf.load_xml_string("""<mujoco><worldbody><geom type="plane" size="1 1 1"/>
+  m = mjcf.load_xml_string("""<mujoco><worldbody><geom type="box" size="1 1 1"/>
     <body><freejoint/><geom type="box" size=".1 .1 .1"/></body></worldbody></mujoco>""")
   with pytest.raises(UnsupportedModel):
     Oracle(m)
