@@ -220,7 +220,9 @@
 #define MJHIP_DATA_INPUTS \
   XD(qpos,              nq,      1,   0) \
   XD(qvel,              nv,      1,   0) \
-  XD(qacc,              nv,      1,   0)
+  XD(qacc,              nv,      1,   0) \
+  XD(mocap_pos,         nmocap,  3,   0) \
+  XD(mocap_quat,        nmocap,  4,   0)
 
 #define MJHIP_DATA_POSITION \
   XD(xpos,              nbody,   3,   1) \

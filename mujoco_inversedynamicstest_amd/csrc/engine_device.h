@@ -1188,8 +1188,16 @@ MJH_HD void kinematics(const mjhipModel& m, const Lane<S>& d) {
       copy3(d.xaxis + 3*jntadr, m.jnt_axis + 3*jntadr);
     } else {
       int pid = m.body_parentid[i];
-      const double* bodypos = m.body_pos + 3*i;
-      const double* bodyquat = m.body_quat + 4*i;
+      double bodypos[3], bodyquat[4];
+      const int mid = m.body_mocapid[i];
+      if (mid >= 0) {               // mocap body: pose from mjData (normalized quaternion)
+        copy3(bodypos, d.mocap_pos + 3*mid);
+        copy4(bodyquat, d.mocap_quat + 4*mid);
+        normalize4(bodyquat);
+      } else {
+        copy3(bodypos, m.body_pos + 3*i);
+        copy4(bodyquat, m.body_quat + 4*i);
+      }
       if (pid) {
         mulMatVec3(xpos, d.xmat + 9*pid, bodypos);
         addTo3(xpos, d.xpos + 3*pid);

@@ -371,8 +371,6 @@ static const char* unsupported(const mjhipModel* m) {
   if (m->opt.jacobian == mjhipJAC_SPARSE || (m->opt.jacobian == mjhipJAC_AUTO && m->nv >= 60)) {
     return "sparse Jacobians (nv >= 60 or jacobian=sparse)";
   }
-  if (m->nmocap) return "mocap bodies";
-  if (m->na) return "actuator activations";
   if ((m->opt.enableflags & mjhipENBL_INVDISCRETE) && m->opt.integrator == mjhipINT_RK4) {
     return "mjENBL_INVDISCRETE with the RK4 integrator (an error in the reference)";
   }
@@ -769,8 +767,10 @@ MJHIP_API int mjhip_forwardBatch(mjhipContext* c, int B, const mjtNum* qpos, con
   const mjhipModel& m = c->hmodel;
   for (int i = 0; i < m.nu; i++) {
     if ((m.actuator_gaintype[i] != mjhipGAIN_FIXED && m.actuator_gaintype[i] != mjhipGAIN_AFFINE) ||
-        (m.actuator_biastype[i] != mjhipBIAS_NONE && m.actuator_biastype[i] != mjhipBIAS_AFFINE)) {
-      set_error("mjhip_forwardBatch: muscle/user actuator gain or bias is not supported");
+        (m.actuator_biastype[i] != mjhipBIAS_NONE && m.actuator_biastype[i] != mjhipBIAS_AFFINE) ||
+        m.actuator_dyntype[i] != mjhipDYN_NONE) {
+      set_error("mjhip_forwardBatch: muscle/user gain or bias, or actuator dynamics (act), "
+                "is not supported");
       return MJHIP_ERR_MODEL;
     }
   }
@@ -967,6 +967,11 @@ MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
   if (!c || B <= 0 || !qpos || !qvel || !qacc) return MJHIP_ERR_ARG;
   const mjhipModel& m = c->hmodel;
   const int nv = m.nv, P = 3*nv + 1;
+  if (m.nmocap) {
+    set_error("mjhip_inverseFDBatch: mocap poses per base state are not an input of the "
+              "batched FD API");
+    return MJHIP_ERR_MODEL;
+  }
   if ((long)B*P > c->capacity) {
     set_error("FD batch needs %ld instances, context capacity %d", (long)B*P, c->capacity);
     return MJHIP_ERR_CAPACITY;

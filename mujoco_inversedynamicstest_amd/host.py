@@ -52,6 +52,11 @@ class MjData:
       self._arrays[f.name] = np.zeros(max(n, 1))
     # reference defaults (mj_resetData): qpos = qpos0, world body identity frames
     self._arrays["qpos"][:m.nq] = m.qpos0
+    for b in range(m.nbody):            # mocap_pos/quat = body_pos/quat (mj_resetData)
+      k = int(m.body_mocapid[b])
+      if k >= 0:
+        self._arrays["mocap_pos"][3*k:3*k + 3] = m.body_pos[b]
+        self._arrays["mocap_quat"][4*k:4*k + 4] = m.body_quat[b]
     self.struct = fields.CData()
     for name, a in self._arrays.items():
       setattr(self.struct, name, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))

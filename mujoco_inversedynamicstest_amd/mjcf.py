@@ -771,8 +771,8 @@ class MJCFCompiler:
       normvec(b.quat)
       b.quat = _resolve_orientation(a, self.degree, self.eulerseq, b.quat)
       b.mocap = a.get("mocap", "false") == "true"
-      if b.mocap:
-        raise MJCFError("mocap bodies are not in the supported subset")
+      if b.mocap and (b.parent is None or b.parent.name != "world" or b.joints):
+        raise MJCFError("mocap body must be a child of the world body and have no joints")
       b.gravcomp = float(a.get("gravcomp", 0.0))
       b.ipos = None
       b.iquat = [1.0, 0.0, 0.0, 0.0]
@@ -980,7 +980,13 @@ class MJCFCompiler:
     parentid = arr("body_parentid", nbody, np.int32)
     rootid = arr("body_rootid", nbody, np.int32)
     weldid = arr("body_weldid", nbody, np.int32)
-    arr("body_mocapid", nbody, np.int32, -1)
+    mocapid = arr("body_mocapid", nbody, np.int32, -1)
+    nmocap = 0
+    for b in bodies:                  # user_model.cc: mocapid in body order
+      if getattr(b, "mocap", False):
+        mocapid[b.id] = nmocap
+        nmocap += 1
+    s["nmocap"] = nmocap
     jntnum = arr("body_jntnum", nbody, np.int32)
     jntadr = arr("body_jntadr", nbody, np.int32, -1)
     dofnum = arr("body_dofnum", nbody, np.int32)
@@ -1280,6 +1286,7 @@ class MJCFCompiler:
     agear = arr("actuator_gear", (nu, 6), np.float64)
     arr("actuator_length0", nu, np.float64)
     arr("actuator_acc0", nu, np.float64)
+    na_count = 0                        # activation states (dyntype != none)
     for ai, a in enumerate(self.actuators):
       tag = a["__tag"]
       if "joint" not in a:
@@ -1303,8 +1310,14 @@ class MJCFCompiler:
           abiasprm[ai, :len(v)] = v
         again[ai] = {"fixed": 0, "affine": 1}[a.get("gaintype", "fixed")]
         abias[ai] = {"none": 0, "affine": 1}[a.get("biastype", "none")]
-        if a.get("dyntype", "none") != "none":
-          raise MJCFError("actuator dynamics are not in the supported subset")
+        dyn = a.get("dyntype", "none")
+        if dyn not in ("none", "integrator", "filter", "filterexact"):
+          raise MJCFError(f"actuator dyntype '{dyn}' is not in the supported subset")
+        adyn[ai] = {"none": 0, "integrator": 1, "filter": 2, "filterexact": 3}[dyn]
+        if "dynprm" in a:
+          v = _floats(a["dynprm"])
+          adynprm[ai, :len(v)] = v
+        na_count += adyn[ai] != 0
       elif tag == "position":
         kp = float(a.get("kp", 1.0))
         kv = float(a.get("kv", 0.0))
@@ -1470,7 +1483,7 @@ class MJCFCompiler:
       kq[ki] = qpos0
       if "qpos" in k:
         kq[ki] = _floats(k["qpos"])
-    s.update(nu=nu, ntendon=nt, nwrap=nwrap, nexclude=nex, nkey=nkey)
+    s.update(nu=nu, ntendon=nt, nwrap=nwrap, nexclude=nex, nkey=nkey, na=int(na_count))
     # ---- dof tree quantities (user_model.cc:2441-2617)
     ntree = 0
     dtree = arr("dof_treeid", nv, np.int32)

@@ -495,8 +495,16 @@ void or_kinematics(const mjhipModel* m, mjhipData* d) {
       mju_copy3(d->xaxis+3*jntadr, m->jnt_axis+3*jntadr);
     } else {
       int pid = m->body_parentid[i];
-      mjtNum* bodypos = m->body_pos+3*i;
-      mjtNum* bodyquat = m->body_quat+4*i;   /* no mocap bodies in the supported subset */
+      mjtNum *bodypos, *bodyquat, quat[4];
+      if (m->body_mocapid[i] >= 0) {
+        bodypos = d->mocap_pos + 3*m->body_mocapid[i];
+        mju_copy4(quat, d->mocap_quat + 4*m->body_mocapid[i]);
+        mju_normalize4(quat);
+        bodyquat = quat;
+      } else {
+        bodypos = m->body_pos+3*i;
+        bodyquat = m->body_quat+4*i;
+      }
       if (pid) {
         mju_mulMatVec3(xpos, d->xmat+9*pid, bodypos);
         mju_addTo3(xpos, d->xpos+3*pid);
