@@ -1532,6 +1532,52 @@ MJH_HD void rne(const mjhipModel& m, const Lane<S>& d, int flg_acc, SP<S> result
 //---------------------------------- engine_passive.c -----------------------------------------
 
 // mj_passive :436-493 with mj_springdamper :57-378 and mj_gravcomp :381-399
+template <int S, class R>
+MJH_HD void objectVelocity(const mjhipModel& m, const Lane<S>& d, int type, int id, R res,
+                           int flg_local);
+template <class R, class V, class P, class O, class M>
+MJH_HD void transformSpatial(R res, V vec, int flg_force, P newpos, O oldpos, M rot,
+                             bool has_rot);
+
+// engine_passive.c:527-585 mj_inertiaBoxFluidModel (the ellipsoid model is rejected by the
+// loader): viscous and quadratic drag of the body's equivalent inertia box, at the COM
+template <int S>
+MJH_HD void inertiaBoxFluid(const mjhipModel& m, const Lane<S>& d, int i) {
+  double lvel[6], wind[6], lwind[6], lfrc[6], bfrc[6], box[3];
+  const double* inertia = m.body_inertia + 3*i;
+  const double mass = m.body_mass[i];
+  auto mx = [](double a, double b) { return a > b ? a : b; };   // mju_max
+  box[0] = sqrt(mx(MINVAL, (inertia[1] + inertia[2] - inertia[0])) / mass * 6.0);
+  box[1] = sqrt(mx(MINVAL, (inertia[0] + inertia[2] - inertia[1])) / mass * 6.0);
+  box[2] = sqrt(mx(MINVAL, (inertia[0] + inertia[1] - inertia[2])) / mass * 6.0);
+  objectVelocity(m, d, 1, i, lvel, 1);
+  for (int k = 0; k < 3; k++) { wind[k] = 0; wind[3 + k] = m.opt.wind[k]; }
+  transformSpatial(lwind, wind, 0, d.xipos + 3*i, d.subtree_com + 3*m.body_rootid[i],
+                   d.ximat + 9*i, true);
+  lvel[3] -= lwind[3]; lvel[4] -= lwind[4]; lvel[5] -= lwind[5];
+  for (int k = 0; k < 6; k++) lfrc[k] = 0;
+  const double visc = m.opt.viscosity, dens = m.opt.density;
+  if (visc > 0) {
+    const double diam = (box[0] + box[1] + box[2])/3.0;
+    scl3(lfrc, lvel, -mjhipPI*diam*diam*diam*visc);
+    scl3(lfrc + 3, lvel + 3, -3.0*mjhipPI*diam*visc);
+  }
+  if (dens > 0) {
+    lfrc[3] -= 0.5*dens*box[1]*box[2]*fabs(lvel[3])*lvel[3];
+    lfrc[4] -= 0.5*dens*box[0]*box[2]*fabs(lvel[4])*lvel[4];
+    lfrc[5] -= 0.5*dens*box[0]*box[1]*fabs(lvel[5])*lvel[5];
+    lfrc[0] -= dens*box[0]*(box[1]*box[1]*box[1]*box[1]+box[2]*box[2]*box[2]*box[2])*
+               fabs(lvel[0])*lvel[0]/64.0;
+    lfrc[1] -= dens*box[1]*(box[0]*box[0]*box[0]*box[0]+box[2]*box[2]*box[2]*box[2])*
+               fabs(lvel[1])*lvel[1]/64.0;
+    lfrc[2] -= dens*box[2]*(box[0]*box[0]*box[0]*box[0]+box[1]*box[1]*box[1]*box[1])*
+               fabs(lvel[2])*lvel[2]/64.0;
+  }
+  mulMatVec3(bfrc, d.ximat + 9*i, lfrc);
+  mulMatVec3(bfrc + 3, d.ximat + 9*i, lfrc + 3);
+  applyFT(m, d, bfrc + 3, bfrc, d.xipos + 3*i, i, d.qfrc_fluid);
+}
+
 template <int S>
 MJH_HD void passive(const mjhipModel& m, const Lane<S>& d) {
   int nv = m.nv;
@@ -1604,7 +1650,16 @@ MJH_HD void passive(const mjhipModel& m, const Lane<S>& d) {
       }
     }
   }
+  // fluid forces (mj_fluid engine_passive.c:402-428)
+  const bool has_fluid = m.opt.viscosity > 0 || m.opt.density > 0;
+  if (has_fluid) {
+    for (int i = 1; i < m.nbody; i++) {
+      if (m.body_mass[i] < MINVAL) continue;
+      inertiaBoxFluid(m, d, i);
+    }
+  }
   add(d.qfrc_passive, d.qfrc_spring, d.qfrc_damper, nv);
+  if (has_fluid) addTo(d.qfrc_passive, d.qfrc_fluid, nv);
   if (has_gravcomp) {
     for (int i = 0; i < m.njnt; i++) {
       if (m.jnt_actgravcomp[i]) continue;

@@ -374,7 +374,6 @@ static const char* unsupported(const mjhipModel* m) {
   if ((m->opt.enableflags & mjhipENBL_INVDISCRETE) && m->opt.integrator == mjhipINT_RK4) {
     return "mjENBL_INVDISCRETE with the RK4 integrator (an error in the reference)";
   }
-  if (m->opt.density > 0 || m->opt.viscosity > 0) return "fluid forces";
   for (int i = 0; i < m->ntendon; i++) {
     if (m->tendon_num[i] && m->wrap_type[m->tendon_adr[i]] != mjhipWRAP_JOINT) {
       return "spatial tendons";

@@ -729,6 +729,9 @@ class MJCFCompiler:
     g["friction"] = [1.0, 0.005, 0.0001]
     g["friction"][:len(fr)] = fr
     g["solmix"] = float(a.get("solmix", 1.0))
+    if a.get("fluidshape", "none") != "none":
+      raise MJCFError("the ellipsoid fluid model (fluidshape) is not in the supported subset; "
+                      "the inertia-box model is")
     g["solref"] = _floats(a["solref"]) if "solref" in a else [0.02, 1.0]
     si = _floats(a["solimp"]) if "solimp" in a else []
     g["solimp"] = [0.9, 0.95, 0.001, 0.5, 2.0]

@@ -982,7 +982,9 @@ static int or_gravcomp(const mjhipModel* m, mjhipData* d) {
   return has_gravcomp;
 }
 
-/* :436-493 (fluid forces need density/viscosity > 0: not in the supported subset) */
+static int or_fluid(const mjhipModel* m, mjhipData* d);
+
+/* :436-493 */
 static void or_passive(const mjhipModel* m, mjhipData* d) {
   int nv = m->nv;
   mju_zero(d->qfrc_spring, nv);
@@ -993,7 +995,9 @@ static void or_passive(const mjhipModel* m, mjhipData* d) {
   if (mjDISABLED(mjhipDSBL_PASSIVE)) return;
   or_springdamper(m, d);
   int has_gravcomp = or_gravcomp(m, d);
+  int has_fluid = or_fluid(m, d);
   mju_add(d->qfrc_passive, d->qfrc_spring, d->qfrc_damper, nv);
+  if (has_fluid) mju_addTo(d->qfrc_passive, d->qfrc_fluid, nv);
   if (has_gravcomp) {
     for (int i = 0; i < m->njnt; i++) {
       if (m->jnt_actgravcomp[i]) continue;
@@ -2478,6 +2482,54 @@ static void or_xquat(const mjhipModel* m, const mjhipData* d, int type, int id, 
   case OBJ_SITE:  mju_mulQuat(q, d->xquat + 4*m->site_bodyid[id], m->site_quat + 4*id); break;
   default:        mju_mulQuat(q, d->xquat + 4*m->cam_bodyid[id], m->cam_quat + 4*id); break;
   }
+}
+
+/* engine_passive.c:527-585 mj_inertiaBoxFluidModel */
+static void or_inertiaBoxFluid(const mjhipModel* m, mjhipData* d, int i) {
+  mjtNum lvel[6], wind[6], lwind[6], lfrc[6], bfrc[6], box[3], diam;
+  const mjtNum* inertia = m->body_inertia + 3*i;
+  box[0] = sqrt(mjMAX(mjMINVAL, (inertia[1] + inertia[2] - inertia[0])) / m->body_mass[i] * 6.0);
+  box[1] = sqrt(mjMAX(mjMINVAL, (inertia[0] + inertia[2] - inertia[1])) / m->body_mass[i] * 6.0);
+  box[2] = sqrt(mjMAX(mjMINVAL, (inertia[0] + inertia[1] - inertia[2])) / m->body_mass[i] * 6.0);
+  or_objectVelocity(m, d, OBJ_BODY, i, lvel, 1);
+  mju_zero(wind, 6);
+  mju_copy3(wind+3, m->opt.wind);
+  mju_transformSpatial(lwind, wind, 0, d->xipos+3*i, d->subtree_com+3*m->body_rootid[i],
+                       d->ximat+9*i);
+  lvel[3] -= lwind[3]; lvel[4] -= lwind[4]; lvel[5] -= lwind[5];
+  mju_zero(lfrc, 6);
+  if (m->opt.viscosity > 0) {
+    diam = (box[0] + box[1] + box[2])/3.0;
+    mju_scl3(lfrc, lvel, -mjhipPI*diam*diam*diam*m->opt.viscosity);
+    mju_scl3(lfrc+3, lvel+3, -3.0*mjhipPI*diam*m->opt.viscosity);
+  }
+  if (m->opt.density > 0) {
+    lfrc[3] -= 0.5*m->opt.density*box[1]*box[2]*fabs(lvel[3])*lvel[3];
+    lfrc[4] -= 0.5*m->opt.density*box[0]*box[2]*fabs(lvel[4])*lvel[4];
+    lfrc[5] -= 0.5*m->opt.density*box[0]*box[1]*fabs(lvel[5])*lvel[5];
+    lfrc[0] -= m->opt.density*box[0]*(box[1]*box[1]*box[1]*box[1]+box[2]*box[2]*box[2]*box[2])*
+               fabs(lvel[0])*lvel[0]/64.0;
+    lfrc[1] -= m->opt.density*box[1]*(box[0]*box[0]*box[0]*box[0]+box[2]*box[2]*box[2]*box[2])*
+               fabs(lvel[1])*lvel[1]/64.0;
+    lfrc[2] -= m->opt.density*box[2]*(box[0]*box[0]*box[0]*box[0]+box[1]*box[1]*box[1]*box[1])*
+               fabs(lvel[2])*lvel[2]/64.0;
+  }
+  mju_mulMatVec3(bfrc, d->ximat+9*i, lfrc);
+  mju_mulMatVec3(bfrc+3, d->ximat+9*i, lfrc+3);
+  mj_applyFT(m, d, bfrc+3, bfrc, d->xipos+3*i, i, d->qfrc_fluid);
+}
+
+/* engine_passive.c:402-428 mj_fluid (inertia-box model; the ellipsoid model is rejected by
+ * the loader) */
+static int or_fluid(const mjhipModel* m, mjhipData* d) {
+  int has_fluid = m->opt.viscosity > 0 || m->opt.density > 0;
+  if (has_fluid) {
+    for (int i = 1; i < m->nbody; i++) {
+      if (m->body_mass[i] < mjMINVAL) continue;
+      or_inertiaBoxFluid(m, d, i);
+    }
+  }
+  return has_fluid;
 }
 
 /* engine_core_smooth.c:1900-1958 */

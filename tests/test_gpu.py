@@ -636,3 +636,22 @@ def test_mocap_parity():
   assert_close(f, np.array(ref), "qfrc_inverse")
   assert_close(e.field("sensordata", 0, B), np.array(sref), "sensordata")
   e.close()
+
+
+def test_fluid_parity():
+  """Inertia-box fluid forces (viscosity and density, with wind) on the device."""
+  m = models.load("equality_site")
+  m.opt["density"] = 1.3
+  m.opt["wind"] = [0.2, -0.1, 0.3]
+  B = 512
+  q, v, a = sample_states(m, B, first=21)
+  e = engine.InverseEngine(m, capacity=B)
+  f = e.inverse(q, v, a)
+  o = Oracle(m)
+  ref, fl = [], []
+  for i in range(B):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    fl.append(o.d.qfrc_fluid.copy())
+  assert_close(f, np.array(ref), "qfrc_inverse")
+  assert_close(e.field("qfrc_fluid", 0, B), np.array(fl), "qfrc_fluid")
+  e.close()
