@@ -101,8 +101,11 @@ MJHIP_CONTACT_HD int mjhip_pairCondim(const mjhipModel* m, int g1, int g2) {
   return m->geom_condim[g1] > m->geom_condim[g2] ? m->geom_condim[g1] : m->geom_condim[g2];
 }
 
-/* constraint rows of one contact (mj_instantiateContact; pyramidal cone) */
-MJHIP_CONTACT_HD int mjhip_contactRows(int condim) { return condim == 1 ? 1 : 2*(condim - 1); }
+/* constraint rows of one contact (mj_instantiateContact): 2(condim-1) for a pyramidal
+ * cone, condim for an elliptic one */
+MJHIP_CONTACT_HD int mjhip_contactRows(int condim, int elliptic) {
+  return condim == 1 ? 1 : (elliptic ? condim : 2*(condim - 1));
+}
 
 /* 1 if contacts are generated at all (mj_collision :284-287) */
 MJHIP_CONTACT_HD int mjhip_contactsEnabled(const mjhipModel* m) {
@@ -131,7 +134,8 @@ MJHIP_CONTACT_HD int mjhip_contactCapacity(const mjhipModel* m, int* rows) {
           }
           if (k < 0) return -1;
           ncon += k;
-          nrow += k * mjhip_contactRows(mjhip_pairCondim(m, g1, g2));
+          nrow += k * mjhip_contactRows(mjhip_pairCondim(m, g1, g2),
+                                        m->opt.cone == mjhipCONE_ELLIPTIC);
         }
       }
     }

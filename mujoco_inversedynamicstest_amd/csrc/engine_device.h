@@ -90,7 +90,7 @@ enum { CNSTR_EQUALITY = 0, CNSTR_FRICTION_DOF, CNSTR_FRICTION_TENDON, CNSTR_LIMI
        CNSTR_LIMIT_TENDON, CNSTR_CONTACT_FRICTIONLESS, CNSTR_CONTACT_PYRAMIDAL,
        CNSTR_CONTACT_ELLIPTIC };
 enum { CNSTRSTATE_SATISFIED = 0, CNSTRSTATE_QUADRATIC, CNSTRSTATE_LINEARNEG,
-       CNSTRSTATE_LINEARPOS };
+       CNSTRSTATE_LINEARPOS, CNSTRSTATE_CONE };
 
 //---------------------------------- strided per-lane views -----------------------------------
 
@@ -192,7 +192,8 @@ MJH_HD unsigned long long chainMask(const mjhipModel& m, int k) {
 // whether mj_inverseSkip(skipstage) can take the fused constraint path
 MJH_HD bool fusedOk(const mjhipModel& m, int skipstage) {
   return skipstage == mjhipSTAGE_NONE && !(m.opt.enableflags & mjhipENBL_INVDISCRETE) &&
-         m.nbody <= 64 && (m.ngeom <= 64 || !mjhip_contactsEnabled(&m));
+         m.nbody <= 64 && (m.ngeom <= 64 || !mjhip_contactsEnabled(&m)) &&
+         !(m.opt.cone == mjhipCONE_ELLIPTIC && mjhip_contactsEnabled(&m));
 }
 
 // dynamic LDS of a fused contact kernel: the per-lane geom position copy (Lane::gxpos)
@@ -1737,10 +1738,11 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
                                int* status) {
   int nv = m.nv, ncon = d.con_count[0];
   if ((m.opt.disableflags & mjhipDSBL_CONTACT) || ncon == 0 || nv == 0) return;
+  const bool elliptic = m.opt.cone == mjhipCONE_ELLIPTIC;
   for (int i = 0; i < ncon; i++) {
     if (d.con_exclude[i]) continue;
     const int dim = d.con_dim[i];
-    const int rows = dim == 1 ? 1 : 2*(dim - 1);
+    const int rows = mjhip_contactRows(dim, elliptic);
     const int nefc = rc.nefc;
     d.con_efc_address[i] = nefc;
     if (nefc + rows > d.efc_cap) {   // mjWARN_CNSTRFULL analogue (capacity is exact)
@@ -1798,6 +1800,8 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
       }
       if (dim == 1) {
         J[j] = cj[0];
+      } else if (elliptic) {
+        for (int k = 0; k < dim; k++) J[k*nv + j] = cj[k];
       } else {
         for (int k = 1; k < dim; k++) {
           double f = fri[k-1];
@@ -1806,10 +1810,12 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
         }
       }
     }
-    const int type = dim == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
+    const int type = dim == 1 ? CNSTR_CONTACT_FRICTIONLESS :
+                     (elliptic ? CNSTR_CONTACT_ELLIPTIC : CNSTR_CONTACT_PYRAMIDAL);
     for (int r = 0; r < rows; r++) {
-      d.efc_pos[nefc+r] = d.con_dist[i];
-      d.efc_margin[nefc+r] = d.con_includemargin[i];
+      // elliptic rows: pos = (dist, 0, ...), margin = (includemargin, 0, ...) (:1113-1126)
+      d.efc_pos[nefc+r] = (elliptic && r) ? 0.0 : d.con_dist[i];
+      d.efc_margin[nefc+r] = (elliptic && r) ? 0.0 : d.con_includemargin[i];
       d.efc_frictionloss[nefc+r] = 0;
       d.efc_type[nefc+r] = type;
       d.efc_id[nefc+r] = i;
@@ -2477,6 +2483,9 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
       }
       if (tp == CNSTR_CONTACT_FRICTIONLESS) {
         d.efc_diagApprox[i] = tran;
+      } else if (tp == CNSTR_CONTACT_ELLIPTIC) {
+        for (int j = 0; j < dim; j++) d.efc_diagApprox[i+j] = j < 3 ? tran : rot;
+        i += dim - 1;
       } else {
         for (int j = 0; j < dim-1; j++) {
           double fri = d.con_friction[5*id+j];
@@ -2492,14 +2501,19 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   for (int i = 0; i < nefc; i++) {
     int id = d.efc_id[i];
     int tp = d.efc_type[i];
-    double solref[2], solimp[5];
-    if (CONTACT && (tp == CNSTR_CONTACT_FRICTIONLESS || tp == CNSTR_CONTACT_PYRAMIDAL)) {
+    double solref[2], solimp[5], solreffriction[2] = {0, 0};
+    const bool iscontact = CONTACT && (tp == CNSTR_CONTACT_FRICTIONLESS ||
+                                       tp == CNSTR_CONTACT_PYRAMIDAL ||
+                                       tp == CNSTR_CONTACT_ELLIPTIC);
+    if (iscontact) {
       for (int k = 0; k < 2; k++) solref[k] = d.con_solref[2*id+k];
       for (int k = 0; k < 5; k++) solimp[k] = d.con_solimp[5*id+k];
+      for (int k = 0; k < 2; k++) solreffriction[k] = d.con_solreffriction[2*id+k];
     } else {
       rowSolParam(m, tp, id, solref, solimp);
     }
-    int dim = (CONTACT && tp == CNSTR_CONTACT_PYRAMIDAL) ? 2*(d.con_dim[id]-1) : 1;
+    int dim = (CONTACT && tp == CNSTR_CONTACT_PYRAMIDAL) ? 2*(d.con_dim[id]-1) :
+              ((CONTACT && tp == CNSTR_CONTACT_ELLIPTIC) ? d.con_dim[id] : 1);
     double ipos = d.efc_pos[i];
     if (tp == CNSTR_EQUALITY && (m.eq_type[id] == mjhipEQ_CONNECT || m.eq_type[id] == mjhipEQ_WELD)) {
       dim = m.eq_type[id] == mjhipEQ_WELD ? 6 : 3;      // getposdim :1392-1422
@@ -2507,16 +2521,40 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
     }
     double kb[4];
     rowImpedance(m, tp, solref, solimp, ipos, d.efc_margin[i], kb);
+    // elliptic friction rows: K = 0, B from solreffriction when set (:1511-1524; its
+    // getsolparam clamps :1358-1366)
+    double kbf[4] = {0, kb[1], kb[2], kb[3]};
+    if (CONTACT && tp == CNSTR_CONTACT_ELLIPTIC) {
+      double sf[2] = {solreffriction[0], solreffriction[1]};
+      if ((sf[0] > 0) ^ (sf[1] > 0)) { sf[0] = 0; sf[1] = 0; }
+      if (!(m.opt.disableflags & mjhipDSBL_REFSAFE) && sf[0] > 0) {
+        sf[0] = dmax(sf[0], 2*m.opt.timestep);
+      }
+      const double* ref = (sf[0] || sf[1]) ? sf : solref;
+      const double dmaxi = dmin(mjhipMAXIMP, dmax(mjhipMINIMP, solimp[1]));
+      kbf[1] = ref[1] > 0 ? 2 / dmax(MINVAL, dmaxi*ref[0]) : -ref[1] / dmax(MINVAL, dmaxi);
+    }
     for (int j = 0; j < dim; j++) {
       int r = i + j;
       d.efc_R[r] = dmax(MINVAL, (1-kb[2])*d.efc_diagApprox[r]/kb[2]);
-      for (int k = 0; k < 4; k++) d.efc_KBIP[4*r+k] = kb[k];
+      const double* k4 = (CONTACT && tp == CNSTR_CONTACT_ELLIPTIC && j > 0) ? kbf : kb;
+      for (int k = 0; k < 4; k++) d.efc_KBIP[4*r+k] = k4[k];
     }
     i += dim - 1;
   }
   // frictional contacts: R in the friction directions, contact mu (:1562-1598)
   for (int i = rc.nf; CONTACT && i < nefc; i++) {
-    if (d.efc_type[i] == CNSTR_CONTACT_PYRAMIDAL) {
+    if (d.efc_type[i] == CNSTR_CONTACT_ELLIPTIC) {
+      int id = d.efc_id[i], dim = d.con_dim[id];
+      d.efc_R[i+1] = d.efc_R[i]/dmax(MINVAL, m.opt.impratio);
+      const double f0 = d.con_friction[5*id];
+      d.con_mu[id] = f0 * sqrt(d.efc_R[i+1]/d.efc_R[i]);
+      for (int j = 1; j < dim-1; j++) {
+        const double fj = d.con_friction[5*id+j];
+        d.efc_R[i+j+1] = d.efc_R[i+1]*f0*f0/(fj*fj);
+      }
+      i += dim - 1;
+    } else if (d.efc_type[i] == CNSTR_CONTACT_PYRAMIDAL) {
       int id = d.efc_id[i], dim = d.con_dim[id];
       d.efc_R[i+1] = d.efc_R[i]/dmax(MINVAL, m.opt.impratio);
       double mu = d.con_friction[5*id] * sqrt(d.efc_R[i+1]/d.efc_R[i]);
@@ -2579,6 +2617,31 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
       } else {
         d.efc_state[i] = CNSTRSTATE_QUADRATIC;
       }
+    } else {
+      // elliptic cone :2459-2540 (no cost, no cone Hessian)
+      const int id = d.efc_id[i], dim = d.con_dim[id];
+      const double mu = d.con_mu[id];
+      double U[6];
+      U[0] = jr*mu;
+      for (int j = 1; j < dim; j++) U[j] = d.jar[i+j]*d.con_friction[5*id+j-1];
+      const double N = U[0];
+      const double T = sqrt(dot(U + 1, U + 1, dim - 1));
+      int state;
+      if (N >= mu*T || (T <= 0 && N >= 0)) {
+        for (int j = 0; j < dim; j++) d.efc_force[i+j] = 0;
+        state = CNSTRSTATE_SATISFIED;
+      } else if (mu*N + T <= 0 || (T <= 0 && N < 0)) {
+        state = CNSTRSTATE_QUADRATIC;
+      } else {
+        const double Dm = d.efc_D[i] / (mu*mu*(1 + mu*mu));
+        const double NmT = N - mu*T;
+        const double f0 = -Dm*NmT*mu;
+        d.efc_force[i] = f0;
+        for (int j = 1; j < dim; j++) d.efc_force[i+j] = -f0/T*U[j]*d.con_friction[5*id+j-1];
+        state = CNSTRSTATE_CONE;
+      }
+      for (int j = 0; j < dim; j++) d.efc_state[i+j] = state;
+      i += dim - 1;
     }
   }
   mulMatTVec(d.qfrc_constraint, d.efc_J, d.efc_force, nefc, nv);
@@ -3153,7 +3216,9 @@ MJH_HD void rnePostConstraint(const mjhipModel& m, const Lane<S>& d) {
     if (adr < 0 || g0 < 0 || g1 < 0) continue;
     zero(lfrc, 6);
     const int dim = d.con_dim[i];
-    if (dim == 1) {
+    if (m.opt.cone == mjhipCONE_ELLIPTIC) {        // mj_contactForce: the cone's own force
+      for (int k = 0; k < dim; k++) lfrc[k] = d.efc_force[adr + k];
+    } else if (dim == 1) {
       lfrc[0] = d.efc_force[adr];
     } else {
       lfrc[0] = 0;

@@ -391,7 +391,6 @@ static const char* unsupported(const mjhipModel* m) {
   if (ncon < 0) {
     return "a collidable geom pair needs a collision function other than plane/sphere/capsule";
   }
-  if (ncon > 0 && m->opt.cone == mjhipCONE_ELLIPTIC) return "elliptic friction cones";
   for (int i = 0; i < m->nsensor; i++) {
     const int t = m->sensor_type[i];
     if (t == mjhSENS_TOUCH || t == mjhSENS_RANGEFINDER || t == mjhSENS_CAMPROJECTION ||

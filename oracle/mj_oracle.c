@@ -1702,6 +1702,12 @@ static void or_instantiateContact(const mjhipModel* m, mjhipData* d, orEfc* e) {
     if (dim == 1) {
       mj_addConstraint(m, e, jac, e->con_dist + i, e->con_includemargin + i, 0, 1,
                        orCNSTR_CONTACT_FRICTIONLESS, i);
+    } else if (m->opt.cone == mjhipCONE_ELLIPTIC) {
+      /* elliptic cone :1113-1126: the dim rotated rows, pos = (dist, 0, ...) */
+      mjtNum cpos[6] = {0}, cmargin[6] = {0};
+      cpos[0] = e->con_dist[i];
+      cmargin[0] = e->con_includemargin[i];
+      mj_addConstraint(m, e, jac, cpos, cmargin, 0, dim, orCNSTR_CONTACT_ELLIPTIC, i);
     } else {
       mjtNum cpos[2] = {e->con_dist[i], e->con_dist[i]};
       mjtNum cmargin[2] = {e->con_includemargin[i], e->con_includemargin[i]};
@@ -1762,7 +1768,8 @@ static void or_diagApprox(const mjhipModel* m, orEfc* e) {
       e->efc_diagApprox[i] = m->tendon_invweight0[id];
       break;
     case orCNSTR_CONTACT_FRICTIONLESS:
-    case orCNSTR_CONTACT_PYRAMIDAL: {
+    case orCNSTR_CONTACT_PYRAMIDAL:
+    case orCNSTR_CONTACT_ELLIPTIC: {
       int dim = e->con_dim[id];
       mjtNum tran = 0, rot = 0;
       for (int side = 0; side < 2; side++) {
@@ -1772,6 +1779,9 @@ static void or_diagApprox(const mjhipModel* m, orEfc* e) {
       }
       if (e->efc_type[i] == orCNSTR_CONTACT_FRICTIONLESS) {
         e->efc_diagApprox[i] = tran;
+      } else if (e->efc_type[i] == orCNSTR_CONTACT_ELLIPTIC) {
+        for (int j = 0; j < dim; j++) e->efc_diagApprox[i+j] = j < 3 ? tran : rot;
+        i += dim - 1;
       } else {
         for (int j = 0; j < dim-1; j++) {
           mjtNum fri = e->con_friction[5*id+j];
@@ -1885,7 +1895,8 @@ static void or_makeImpedance(const mjhipModel* m, orEfc* e) {
   for (int i = 0; i < nefc; i++) {
     getsolparam(m, e, i, solref, solreffriction, solimp);
     /* getposdim :1392-1422 */
-    int dim = e->efc_type[i] == orCNSTR_CONTACT_PYRAMIDAL ? 2*(e->con_dim[e->efc_id[i]]-1) : 1;
+    int dim = e->efc_type[i] == orCNSTR_CONTACT_PYRAMIDAL ? 2*(e->con_dim[e->efc_id[i]]-1) :
+              (e->efc_type[i] == orCNSTR_CONTACT_ELLIPTIC ? e->con_dim[e->efc_id[i]] : 1);
     mjtNum pos = e->efc_pos[i];
     if (e->efc_type[i] == orCNSTR_EQUALITY) {
       int t = m->eq_type[e->efc_id[i]];
@@ -1898,8 +1909,10 @@ static void or_makeImpedance(const mjhipModel* m, orEfc* e) {
     for (int j = 0; j < dim; j++) {
       int r = i + j, tp = e->efc_type[r];
       R[r] = mjMAX(mjMINVAL, (1-imp)*e->efc_diagApprox[r]/imp);
-      const mjtNum* ref = solref;
-      if (tp == orCNSTR_FRICTION_DOF || tp == orCNSTR_FRICTION_TENDON) {
+      int elliptic_friction = tp == orCNSTR_CONTACT_ELLIPTIC && j > 0;
+      const mjtNum* ref = elliptic_friction && (solreffriction[0] || solreffriction[1]) ?
+                          solreffriction : solref;
+      if (tp == orCNSTR_FRICTION_DOF || tp == orCNSTR_FRICTION_TENDON || elliptic_friction) {
         KBIP[4*r] = 0;
       } else if (ref[0] > 0) {
         KBIP[4*r] = 1 / mjMAX(mjMINVAL, solimp[1]*solimp[1] * ref[0]*ref[0] * ref[1]*ref[1]);
@@ -1918,7 +1931,16 @@ static void or_makeImpedance(const mjhipModel* m, orEfc* e) {
   }
   /* frictional contacts: R in the friction directions, contact mu (:1562-1598) */
   for (int i = e->ne + e->nf; i < nefc; i++) {
-    if (e->efc_type[i] == orCNSTR_CONTACT_PYRAMIDAL) {
+    if (e->efc_type[i] == orCNSTR_CONTACT_ELLIPTIC) {
+      int id = e->efc_id[i], dim = e->con_dim[id];
+      const mjtNum* friction = e->con_friction + 5*id;
+      R[i+1] = R[i]/mjMAX(mjMINVAL, m->opt.impratio);
+      e->con_mu[id] = friction[0] * sqrt(R[i+1]/R[i]);
+      for (int j = 1; j < dim-1; j++) {
+        R[i+j+1] = R[i+1]*friction[0]*friction[0]/(friction[j]*friction[j]);
+      }
+      i += dim - 1;
+    } else if (e->efc_type[i] == orCNSTR_CONTACT_PYRAMIDAL) {
       int id = e->efc_id[i], dim = e->con_dim[id];
       const mjtNum* friction = e->con_friction + 5*id;
       R[i+1] = R[i]/mjMAX(mjMINVAL, m->opt.impratio);
@@ -1995,6 +2017,29 @@ static void or_constraintUpdate(const mjhipModel* m, mjhipData* d, orEfc* e, con
       } else {
         e->efc_state[i] = orCNSTRSTATE_QUADRATIC;
       }
+    } else {
+      /* elliptic cone :2459-2540 (no cost, no cone Hessian) */
+      int id = e->efc_id[i], dim = e->con_dim[id];
+      mjtNum mu = e->con_mu[id];
+      const mjtNum* friction = e->con_friction + 5*id;
+      mjtNum U[6];
+      U[0] = jar[i]*mu;
+      for (int j = 1; j < dim; j++) U[j] = jar[i+j]*friction[j-1];
+      mjtNum N = U[0], T = mju_norm(U+1, dim-1);
+      if (N >= mu*T || (T <= 0 && N >= 0)) {
+        mju_zero(force+i, dim);
+        e->efc_state[i] = orCNSTRSTATE_SATISFIED;
+      } else if (mu*N + T <= 0 || (T <= 0 && N < 0)) {
+        e->efc_state[i] = orCNSTRSTATE_QUADRATIC;
+      } else {
+        mjtNum Dm = D[i] / (mu*mu*(1 + mu*mu));
+        mjtNum NmT = N - mu*T;
+        force[i] = -Dm*NmT*mu;
+        for (int j = 1; j < dim; j++) force[i+j] = -force[i]/T*U[j]*friction[j-1];
+        e->efc_state[i] = orCNSTRSTATE_CONE;
+      }
+      for (int j = 1; j < dim; j++) e->efc_state[i+j] = e->efc_state[i];
+      i += dim - 1;
     }
   }
   /* mj_mulJacTVec, dense: mju_mulMatTVec (engine_core_constraint.c:426-442) */
@@ -2580,11 +2625,15 @@ static void mju_decodePyramid(mjtNum* force, const mjtNum* pyramid, const mjtNum
 }
 
 /* engine_support.c:1459-1480 mj_contactForce (pyramidal cones: the supported subset) */
-static void or_contactForce(const orEfc* e, int id, mjtNum result[6]) {
+static void or_contactForce(const mjhipModel* m, const orEfc* e, int id, mjtNum result[6]) {
   mju_zero(result, 6);
   if (id >= 0 && id < e->ncon && e->con_efc_address[id] >= 0) {
-    mju_decodePyramid(result, e->efc_force + e->con_efc_address[id], e->con_friction + 5*id,
-                      e->con_dim[id]);
+    if (m->opt.cone != mjhipCONE_ELLIPTIC) {
+      mju_decodePyramid(result, e->efc_force + e->con_efc_address[id], e->con_friction + 5*id,
+                        e->con_dim[id]);
+    } else {
+      mju_copy(result, e->efc_force + e->con_efc_address[id], e->con_dim[id]);
+    }
   }
 }
 
@@ -2608,7 +2657,7 @@ static void or_rnePostConstraint(const mjhipModel* m, mjhipData* d, const orEfc*
     if (e->con_efc_address[i] < 0) continue;
     const int* geom = e->con_geom + 2*i;
     if (geom[0] < 0 || geom[1] < 0) continue;
-    or_contactForce(e, i, lfrc);
+    or_contactForce(m, e, i, lfrc);
     const mjtNum* frame = e->con_frame + 9*i;
     mju_mulMatTVec3(cfrc, frame, lfrc + 3);
     mju_mulMatTVec3(cfrc + 3, frame, lfrc);

@@ -339,3 +339,65 @@ def test_fused_equals_classic_and_oracle():
     dims.update(int(x) for x in o.contact_field("con_dim"))
     assert kf.field("efc_count")[0] == nefc
   assert dims == {1, 3, 4, 6}
+
+
+@pytest.mark.parametrize("impedance", [0.3, 0.9, 0.99])
+def test_rest_penetration_elliptic(impedance):
+  """RestPenetration with an elliptic cone: the normal row of the cone holds the weight at
+  the reference's rest depth exactly as the pyramid does (mj_makeImpedance keeps the
+  normal R of the elliptic cone; friction rows carry no load at rest)."""
+  m = mjcf.load_xml_string("""
+  <mujoco><option cone="elliptic"/><worldbody>
+    <geom type="plane" size="1 1 1"/>
+    <body pos="0 0 .2"><joint type="slide" axis="0 0 1"/><geom size=".1"/></body>
+  </worldbody></mujoco>""")
+  g, dr, reference = -m.opt["gravity"][2], 0.8, 0.01
+  m.geom_solimp[:, 0] = impedance
+  m.geom_solimp[:, 1] = impedance
+  m.geom_solref[:, 0] = reference
+  m.geom_solref[:, 1] = dr
+  depth = g * (1 - impedance) * (reference * dr) ** 2
+  o = Oracle(m)
+  f = o.inverse(np.array([-0.1 - depth]), np.zeros(1), np.zeros(1))
+  assert o.efc.nefc == 3 and list(o.efc_field("efc_type")) == [7, 7, 7]
+  assert abs(f[0]) <= 1e-9 * m.body_mass[1] * g
+
+
+_ELLIPTIC = _MIXED.replace("<mujoco>", '<mujoco><option cone="elliptic" impratio="3"/>').replace(
+    'condim="6"/>', 'condim="6" solreffriction=".05 1"/>')
+
+
+def test_elliptic_cone_states_and_device_bitexact():
+  """Elliptic cones (condim 1, 3, 4, 6; solreffriction; impratio): every cone state occurs;
+  in the CONE state the force lies on the cone, |f_T / mu| = f_N; the device code on the
+  host equals the oracle bit for bit."""
+  m = mjcf.load_xml_string(_ELLIPTIC)
+  o, k = Oracle(m), KernelCPU(m)
+  rng = np.random.default_rng(13)
+  states = set()
+  for i in range(60):
+    q = m.qpos0.copy()
+    for b in range(3):
+      q[7 * b + 2] = 0.09 + 0.02 * rng.random()
+      qq = np.array([1, 0, 0, 0]) + 0.2 * rng.normal(size=4)
+      q[7 * b + 3:7 * b + 7] = qq / np.linalg.norm(qq)
+    q[21] = 0.2 * rng.normal()
+    v, a = 0.5 * rng.normal(size=m.nv), 3 * rng.normal(size=m.nv)
+    o.inverse(q, v, a)
+    k.inverse(q, v, a)
+    st, tp = o.efc_field("efc_state"), o.efc_field("efc_type")
+    fr = o.efc_field("efc_force")
+    states |= set(st[tp == 7].tolist())
+    for c in range(o.efc.ncon):
+      adr, dim = o.contact_field("con_efc_address")[c], o.contact_field("con_dim")[c]
+      if adr >= 0 and dim > 1 and st[adr] == 4:       # CONE
+        mu = o.contact_field("con_friction")[c][:dim - 1]
+        np.testing.assert_allclose(np.linalg.norm(fr[adr + 1:adr + dim] / mu), fr[adr],
+                                   rtol=1e-10)
+    for name in EFC_FIELDS:
+      ref = o.efc_field(name)
+      np.testing.assert_array_equal(k.field(name)[:ref.size], ref, err_msg=f"{name} inst {i}")
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name))
+  assert {0, 1, 4} <= states, states

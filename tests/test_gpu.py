@@ -655,3 +655,25 @@ def test_fluid_parity():
   assert_close(f, np.array(ref), "qfrc_inverse")
   assert_close(e.field("qfrc_fluid", 0, B), np.array(fl), "qfrc_fluid")
   e.close()
+
+
+def test_elliptic_cone_parity():
+  """Elliptic friction cones (classic constraint passes) on the device: humanoid config-4
+  states with cone="elliptic"."""
+  from mujoco_inversedynamicstest_amd.sampler import sample_contact_states
+  m = models.load("humanoid")
+  m.opt["cone"] = 1
+  B = 512
+  q, v, a = sample_contact_states(m, B, first=3)
+  e = engine.InverseEngine(m, capacity=B)
+  f, st = e.inverse(q, v, a, status=True)
+  assert (st == 0).all()
+  nefc_g = e.field_int("efc_count", 0, B)[:, 0]
+  o = Oracle(m)
+  ref = []
+  for i in range(B):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    assert nefc_g[i] == o.efc.nefc
+  assert_close(f, np.array(ref), "qfrc_inverse")
+  assert nefc_g.sum() > 0
+  e.close()
