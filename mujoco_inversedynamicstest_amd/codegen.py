@@ -112,6 +112,9 @@ def fast_path_supported(m) -> str | None:
     return "mocap/activations"
   if m.opt["density"] > 0 or m.opt["viscosity"] > 0:
     return "fluid"
+  for a in range(m.nu):
+    if m.actuator_trntype[a] not in (0, 1) or m.jnt_type[m.actuator_trnid[a, 0]] not in (2, 3):
+      return "ball/free-joint or tendon transmissions"
   if m.sizes.get("nsensor", 0) and not (m.opt["disableflags"] & (1 << 12)):
     return "sensors (mj_sensorPos/Vel/Acc run on the generic kernel)"
   return None

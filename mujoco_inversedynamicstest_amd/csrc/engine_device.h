@@ -1412,9 +1412,48 @@ MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d) {
   for (int i = 0; i < m.nu; i++) {
     int adr = m.moment_rowadr[i];
     int id = m.actuator_trnid[2*i];
-    double g = m.actuator_gear[6*i];
-    d.actuator_length[i] = d.qpos[m.jnt_qposadr[id]]*g;
-    d.actuator_moment[adr] = g;
+    const double* gear = m.actuator_gear + 6*i;
+    const int trn = m.actuator_trntype[i];
+    SP<S> moment = d.actuator_moment + adr;
+    if (trn == mjhipTRN_JOINT || trn == mjhipTRN_JOINTINPARENT) {
+      const int t = m.jnt_type[id];
+      if (t == mjhipJNT_SLIDE || t == mjhipJNT_HINGE) {
+        d.actuator_length[i] = d.qpos[m.jnt_qposadr[id]]*gear[0];
+        moment[0] = gear[0];
+      } else if (t == mjhipJNT_BALL) {     // :912-942 expmap axis . gear axis
+        double axis[3], quat[4], gearAxis[3];
+        copy4(quat, d.qpos + m.jnt_qposadr[id]);
+        normalize4(quat);
+        quat2Vel(axis, quat, 1);
+        if (trn == mjhipTRN_JOINT) {
+          copy3(gearAxis, gear);
+        } else {
+          quat[1] = -quat[1]; quat[2] = -quat[2]; quat[3] = -quat[3];
+          rotVecQuat(gearAxis, gear, quat);
+        }
+        d.actuator_length[i] = axis[0]*gearAxis[0] + axis[1]*gearAxis[1] + axis[2]*gearAxis[2];
+        copy3(moment, gearAxis);
+      } else {                              // free joint :944-971
+        double gearAxis[3];
+        d.actuator_length[i] = 0;
+        if (trn == mjhipTRN_JOINT) {
+          copy3(gearAxis, gear + 3);
+        } else {
+          double quat[4];
+          copy4(quat, d.qpos + m.jnt_qposadr[id] + 3);
+          normalize4(quat);
+          quat[1] = -quat[1]; quat[2] = -quat[2]; quat[3] = -quat[3];
+          rotVecQuat(gearAxis, gear + 3, quat);
+        }
+        copy3(moment, gear);
+        moment[3] = gearAxis[0]; moment[4] = gearAxis[1]; moment[5] = gearAxis[2];
+      }
+    } else {                                // fixed tendon :1053-1081 (model-constant nonzeros)
+      d.actuator_length[i] = d.ten_length[id]*gear[0];
+      for (int k = 0; k < m.moment_rownnz[i]; k++) {
+        moment[k] = d.ten_J[id*m.nv + m.moment_colind[adr+k]]*gear[0];
+      }
+    }
   }
 }
 

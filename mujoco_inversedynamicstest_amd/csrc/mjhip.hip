@@ -381,10 +381,8 @@ static const char* unsupported(const mjhipModel* m) {
   }
   for (int i = 0; i < m->nu; i++) {
     int t = m->actuator_trntype[i];
-    if (t != mjhipTRN_JOINT && t != mjhipTRN_JOINTINPARENT) return "non-joint transmissions";
-    int j = m->actuator_trnid[2*i];
-    if (m->jnt_type[j] != mjhipJNT_HINGE && m->jnt_type[j] != mjhipJNT_SLIDE) {
-      return "ball/free joint transmissions";
+    if (t != mjhipTRN_JOINT && t != mjhipTRN_JOINTINPARENT && t != mjhipTRN_TENDON) {
+      return "slider-crank/site/body transmissions";
     }
   }
   int ncon = mjhip_contactCapacity(m, nullptr);

@@ -1292,11 +1292,18 @@ class MJCFCompiler:
     na_count = 0                        # activation states (dyntype != none)
     for ai, a in enumerate(self.actuators):
       tag = a["__tag"]
-      if "joint" not in a:
-        raise MJCFError("only joint transmissions are in the supported subset "
-                        "(slider-crank/site/tendon/body transmissions are next)")
-      atrn[ai] = 0
-      atrnid[ai, 0] = jname[a["joint"]]
+      tname = {"joint": jname, "jointinparent": jname,
+               "tendon": {ta.get("name"): i for i, (ta, _) in enumerate(self.tendons)
+                          if ta.get("name")}}
+      trn = [k for k in ("joint", "jointinparent", "tendon") if k in a]
+      if len(trn) != 1:
+        raise MJCFError("only joint, jointinparent and fixed-tendon transmissions are in "
+                        "the supported subset (slider-crank/site/body transmissions are next)"
+                        if not trn else "actuator has more than one transmission target")
+      if a[trn[0]] not in tname[trn[0]]:
+        raise MJCFError(f"unknown {trn[0]} '{a[trn[0]]}' in actuator")
+      atrn[ai] = {"joint": 0, "jointinparent": 1, "tendon": 3}[trn[0]]
+      atrnid[ai, 0] = tname[trn[0]][a[trn[0]]]
       gear = [1.0, 0, 0, 0, 0, 0]
       if "gear" in a:
         g = _floats(a["gear"])
@@ -1613,21 +1620,33 @@ class MJCFCompiler:
       if list(Dcolind[Drowadr[j]:Drowadr[j] + Drownnz[j]]) != \
          list(Bcolind[Browadr[b]:Browadr[b] + Brownnz[b]]):
         raise MJCFError("D and B sparsity differ")  # SHOULD NOT OCCUR
-    # actuator moment sparse structure for joint transmissions (smooth.c:896-916)
-    nJmom = 0
+    # actuator moment sparsity (mj_transmission, engine_core_smooth.c:884-1081). For the
+    # transmissions in the subset it depends on the model only: a joint's dofs, or the dofs
+    # where a fixed tendon's dense ten_J row times gear[0] is nonzero (the dense compress
+    # loop :1070-1079; ten_J entries are the wrap coefficients, last one per joint wins,
+    # smooth.c mj_tendon dense branch). rowadr is cumulative (:896).
     mrownnz = arr("moment_rownnz", nu, np.int32)
     mrowadr = arr("moment_rowadr", nu, np.int32)
+    cols = []
     for ai in range(nu):
-      jid = atrnid[ai, 0]
-      cnt = {0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[jid])]
-      if cnt != 1:
-        raise MJCFError("ball/free joint transmissions are not in the supported subset")
-      mrownnz[ai] = 1
-      mrowadr[ai] = nJmom
-      nJmom += cnt
+      tid = int(atrnid[ai, 0])
+      if atrn[ai] in (0, 1):
+        cnt = {0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[tid])]
+        c = list(range(jdadr[tid], jdadr[tid] + cnt))
+      else:
+        row = np.zeros(nv)
+        for wi in range(tadr[tid], tadr[tid] + tnum[tid]):
+          row[jdadr[wobj[wi]]] = wprm[wi]
+        c = [j for j in range(nv) if row[j] * agear[ai, 0] != 0]
+      mrownnz[ai] = len(c)
+      mrowadr[ai] = mrowadr[ai - 1] + mrownnz[ai - 1] if ai else 0
+      cols.extend(c)
+    # nJmom as CountNJmom (user_model.cc:2703-2750): 1/3/6 per joint transmission, nv per
+    # tendon, so actuator_moment has the reference's size; colind past the nonzeros is 0
+    nJmom = sum({0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[atrnid[ai, 0]])] if atrn[ai] in (0, 1)
+                else nv for ai in range(nu))
     mcol = arr("moment_colind", nJmom, np.int32)
-    for ai in range(nu):
-      mcol[mrowadr[ai]] = jdadr[atrnid[ai, 0]]
+    mcol[:len(cols)] = cols
     s["nJmom"] = nJmom
     # scalars and names
     m.opt = {k: (list(v) if isinstance(v, list) else v) for k, v in self.opt.items()}

@@ -46,6 +46,25 @@ def _axis_angle_quat(axis, ang):
   return np.array([np.cos(ang*0.5), axis[0]*s, axis[1]*s, axis[2]*s])
 
 
+def _quat_neg(q):
+  return np.array([q[0], -q[1], -q[2], -q[3]])
+
+
+def _rot_vec_quat(v, q):
+  return _rot(v, q)
+
+
+def _quat2vel(q):
+  """mju_quat2Vel with dt = 1 (engine_util_spatial.c): the expmap axis*angle."""
+  axis = np.array(q[1:4], dtype=np.float64)
+  n = np.linalg.norm(axis)
+  axis = axis / n if n >= 1e-15 else np.array([1.0, 0, 0])
+  speed = 2 * np.arctan2(n, q[0])
+  if speed > np.pi:
+    speed -= 2 * np.pi
+  return axis * speed
+
+
 def _normq(q):
   n = np.linalg.norm(q)
   return q / n if n > 1e-15 else np.array([1.0, 0, 0, 0])
@@ -248,13 +267,32 @@ def set_const(m):
   m.tendon_length0[:] = L0
   for t in range(m.ntendon):
     m.tendon_invweight0[t] = J0[t] @ Minv @ J0[t] if nv else 0.0
-  # actuators (joint transmission)
+  # actuators: mj_transmission at qpos0 (engine_core_smooth.c:884-1081), dense moment
   for a in range(m.nu):
-    jid = m.actuator_trnid[a, 0]
-    g = m.actuator_gear[a, 0]
-    m.actuator_length0[a] = m.qpos0[m.jnt_qposadr[jid]] * g
+    tid = m.actuator_trnid[a, 0]
+    gear = m.actuator_gear[a]
     mom = np.zeros(nv)
-    mom[m.jnt_dofadr[jid]] = g
+    if m.actuator_trntype[a] in (0, 1):
+      jt, qa, da = m.jnt_type[tid], m.jnt_qposadr[tid], m.jnt_dofadr[tid]
+      inparent = m.actuator_trntype[a] == 1
+      if jt in (2, 3):
+        length = m.qpos0[qa] * gear[0]
+        mom[da] = gear[0]
+      elif jt == 1:
+        quat = m.qpos0[qa:qa + 4] / np.linalg.norm(m.qpos0[qa:qa + 4])
+        ga = _rot_vec_quat(gear[:3], _quat_neg(quat)) if inparent else gear[:3]
+        length = float(_quat2vel(quat) @ ga)
+        mom[da:da + 3] = ga
+      else:
+        quat = m.qpos0[qa + 3:qa + 7] / np.linalg.norm(m.qpos0[qa + 3:qa + 7])
+        ga = _rot_vec_quat(gear[3:], _quat_neg(quat)) if inparent else gear[3:]
+        length = 0.0
+        mom[da:da + 3] = gear[:3]
+        mom[da + 3:da + 6] = ga
+    else:
+      length = L0[tid] * gear[0]
+      mom = J0[tid] * gear[0]
+    m.actuator_length0[a] = length
     m.actuator_acc0[a] = np.linalg.norm(Minv @ mom) if nv else 0.0
   # missing eq_data of body constraints (engine_setconst.c:289-340)
   for i in range(m.sizes.get("neq", 0)):

@@ -715,15 +715,60 @@ static void or_tendon(const mjhipModel* m, mjhipData* d) {
 }
 
 /* :865-916, joint transmission (slide/hinge) */
+static mjtNum mju_dot3(const mjtNum* a, const mjtNum* b);
+
+/* engine_core_smooth.c:862-1100 mj_transmission: joint (slide/hinge/ball/free, in the
+ * joint or the parent frame) and tendon transmissions (fixed tendons: their sparsity is a
+ * model constant, moment_* model fields) */
 static void or_transmission(const mjhipModel* m, mjhipData* d) {
-  int nu = m->nu;
+  int nu = m->nu, nv = m->nv;
   int* rowadr = m->moment_rowadr;
   for (int i = 0; i < nu; i++) {
     int adr = rowadr[i];
     int id = m->actuator_trnid[2*i];
     mjtNum* gear = m->actuator_gear+6*i;
-    d->actuator_length[i] = d->qpos[m->jnt_qposadr[id]]*gear[0];
-    d->actuator_moment[adr] = gear[0];
+    mjtNum* length = d->actuator_length + i;
+    mjtNum* moment = d->actuator_moment + adr;
+    int trn = m->actuator_trntype[i];
+    if (trn == mjhipTRN_JOINT || trn == mjhipTRN_JOINTINPARENT) {
+      int t = m->jnt_type[id];
+      if (t == mjhipJNT_SLIDE || t == mjhipJNT_HINGE) {
+        *length = d->qpos[m->jnt_qposadr[id]]*gear[0];
+        moment[0] = gear[0];
+      } else if (t == mjhipJNT_BALL) {
+        mjtNum axis[3], quat[4], gearAxis[3];
+        mju_copy4(quat, d->qpos+m->jnt_qposadr[id]);
+        mju_normalize4(quat);
+        mju_quat2Vel(axis, quat, 1);
+        if (trn == mjhipTRN_JOINT) {
+          mju_copy3(gearAxis, gear);
+        } else {
+          quat[1] = -quat[1]; quat[2] = -quat[2]; quat[3] = -quat[3];
+          mju_rotVecQuat(gearAxis, gear, quat);
+        }
+        *length = mju_dot3(axis, gearAxis);
+        mju_copy3(moment, gearAxis);
+      } else {
+        mjtNum gearAxis[3];
+        *length = 0;
+        if (trn == mjhipTRN_JOINT) {
+          mju_copy3(gearAxis, gear+3);
+        } else {
+          mjtNum quat[4];
+          mju_copy4(quat, d->qpos+m->jnt_qposadr[id]+3);
+          mju_normalize4(quat);
+          quat[1] = -quat[1]; quat[2] = -quat[2]; quat[3] = -quat[3];
+          mju_rotVecQuat(gearAxis, gear+3, quat);
+        }
+        mju_copy3(moment, gear);
+        mju_copy3(moment+3, gearAxis);
+      }
+    } else {   /* mjTRN_TENDON, dense: gear*ten_J compressed to its nonzeros */
+      *length = d->ten_length[id]*gear[0];
+      for (int k = 0; k < m->moment_rownnz[i]; k++) {
+        moment[k] = d->ten_J[id*nv + m->moment_colind[adr+k]]*gear[0];
+      }
+    }
   }
 }
 
