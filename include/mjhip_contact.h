@@ -14,6 +14,12 @@
  * reject a pair the narrowphase would report. A body pair is therefore a candidate exactly
  * when it passes the static rules below. mj_collision processes candidates in signature
  * order ((b1 << 16) + b2, b1 < b2); mjhip_pairMaxContacts bounds each primitive pair.
+ *
+ * A candidate pair whose collision function is not implemented here (box-box, the convex
+ * pairs mjc_Convex serves, ellipsoids) adds no capacity. At run time it goes through the
+ * same bitmask and bounding-sphere filters as the reference (mj_collideGeoms :1470-1497);
+ * an instance where one survives them is flagged MJHIP_INST_UNSUPPORTED instead of getting
+ * contacts, so every unflagged instance is exact.
  */
 #ifndef MJHIP_CONTACT_H_
 #define MJHIP_CONTACT_H_
@@ -112,9 +118,9 @@ MJHIP_CONTACT_HD int mjhip_contactsEnabled(const mjhipModel* m) {
   return !(m->opt.disableflags & (mjhipDSBL_CONSTRAINT | mjhipDSBL_CONTACT)) && m->nbody >= 2;
 }
 
-/* Maximum contacts per instance (exact for the implemented primitives), or -1 if a
- * candidate geom pair needs a collision function this engine does not implement.
- * *rows receives the maximum number of contact constraint rows. */
+/* Maximum contacts per instance (exact for the implemented primitives; pairs without an
+ * implemented function add none, see above). *rows receives the maximum number of contact
+ * constraint rows. */
 MJHIP_CONTACT_HD int mjhip_contactCapacity(const mjhipModel* m, int* rows) {
   int ncon = 0, nrow = 0;
   if (rows) *rows = 0;
@@ -132,7 +138,7 @@ MJHIP_CONTACT_HD int mjhip_contactCapacity(const mjhipModel* m, int* rows) {
                                   m->geom_contype[g2], m->geom_conaffinity[g2])) {
             continue;
           }
-          if (k < 0) return -1;
+          if (k < 0) continue;                 /* flagged per instance at run time */
           ncon += k;
           nrow += k * mjhip_contactRows(mjhip_pairCondim(m, g1, g2),
                                         m->opt.cone == mjhipCONE_ELLIPTIC);

@@ -168,6 +168,7 @@
   X(mjtNum,  actuator_ctrlrange,   nu,        2) \
   X(mjtNum,  actuator_forcerange,  nu,        2) \
   X(mjtNum,  actuator_gear,        nu,        6) \
+  X(mjtNum,  actuator_cranklength, nu,        1) \
   X(mjtNum,  actuator_length0,     nu,        1) \
   X(mjtNum,  actuator_acc0,        nu,        1) \
   X(int,     exclude_signature,    nexclude,  1) \

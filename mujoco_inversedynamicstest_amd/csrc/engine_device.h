@@ -67,6 +67,13 @@ MJH_HD int mjh_needSubtreeVel(const mjhipModel* m) {
   }
   return 0;
 }
+// 1 when an actuator has a slider-crank transmission (three 3 x nv Jacobians at once)
+MJH_HD int mjh_needSliderCrank(const mjhipModel* m) {
+  for (int i = 0; i < m->nu; i++) {
+    if (m->actuator_trntype[i] == mjhipTRN_SLIDERCRANK) return 1;
+  }
+  return 0;
+}
 MJH_HD int mjh_needRnePost(const mjhipModel* m) {
   for (int i = 0; i < m->nsensor; i++) {
     const int t = m->sensor_type[i];
@@ -109,6 +116,7 @@ struct SP {
   XSC(cfrc, 6*nbody)                  \
   XSC(jacp, 3*nv)                     \
   XSC(jacr, 3*nv)                     \
+  XSC(jacsc, mjh_needSliderCrank(m)*6*nv) /* slider-crank site Jacobians */ \
   XSC(qforce, nv)                     \
   XSC(qacc_save, nv)                  \
   XSC(energy, 2)                      /* mjData energy (mjENBL_ENERGY) */ \
@@ -968,7 +976,8 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
                          int* status) {
   if (m.geom_type[g1] > m.geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
-  if (mjhip_pairMaxContacts(t1, t2) <= 0) return;
+  const int kmax = mjhip_pairMaxContacts(t1, t2);
+  if (kmax == 0) return;
   if (mjhip_filterBitmask(m.geom_contype[g1], m.geom_conaffinity[g1], m.geom_contype[g2],
                           m.geom_conaffinity[g2])) {
     return;
@@ -977,6 +986,10 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
   double margin = ovr ? m.opt.o_margin : (m.geom_margin[g1] > m.geom_margin[g2] ?
                                           m.geom_margin[g1] : m.geom_margin[g2]);
   if (filterSphere(m, d, g1, g2, margin)) return;
+  if (kmax < 0) {                       // the reference would run a function not built here
+    *status |= MJHIP_INST_UNSUPPORTED;
+    return;
+  }
   if (t1 == mjhipGEOM_PLANE && (t2 == mjhipGEOM_BOX || t2 == mjhipGEOM_CYLINDER)) {
     collidePlaneBoxCyl(m, d, g1, g2, margin, ncon, status);
     return;
@@ -1448,6 +1461,50 @@ MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d) {
         copy3(moment, gear);
         moment[3] = gearAxis[0]; moment[4] = gearAxis[1]; moment[5] = gearAxis[2];
       }
+    } else if (trn == mjhipTRN_SLIDERCRANK) {   // :1000-1052
+      const int ids = m.actuator_trnid[2*i+1];
+      const double rod = m.actuator_cranklength[i];
+      SP<S> smat = d.site_xmat + 9*ids;
+      const double axis[3] = {smat[2], smat[5], smat[8]};
+      double vec[3], dlda[3], dldv[3];
+      sub3(vec, d.site_xpos + 3*id, d.site_xpos + 3*ids);
+      const double av = dot3(vec, axis);
+      const double det = av*av + rod*rod - dot3(vec, vec);
+      if (det <= 0) {                       // crank too short: length = a'v
+        d.actuator_length[i] = av;
+        copy3(dlda, vec);
+        copy3(dldv, axis);
+      } else {
+        const double sdet = sqrt(det);
+        d.actuator_length[i] = av - sdet;
+        const double c = 1 - av/sdet, r = 1/sdet;
+        for (int k = 0; k < 3; k++) {
+          dldv[k] = axis[k]*c;
+          dldv[k] += vec[k]*r;
+          dlda[k] = vec[k]*c;
+        }
+      }
+      // jacS = d.jacp (slider point), jacA = rotation Jacobian x axis (in d.jacr),
+      // jac = crank-site Jacobian - jacS (in d.jacsc)
+      const int nv = m.nv;
+      jacInto(m, d, d.jacp, d.jacr, d.site_xpos + 3*ids, m.site_bodyid[ids]);
+      for (int j = 0; j < nv; j++) {
+        const double r0 = d.jacr[j], r1 = d.jacr[nv+j], r2 = d.jacr[2*nv+j];
+        d.jacr[j] = r1*axis[2] - r2*axis[1];
+        d.jacr[nv+j] = r2*axis[0] - r0*axis[2];
+        d.jacr[2*nv+j] = r0*axis[1] - r1*axis[0];
+      }
+      jacInto(m, d, d.jacsc, d.jacsc + 3*nv, d.site_xpos + 3*id, m.site_bodyid[id]);
+      for (int j = 0; j < 3*nv; j++) d.jacsc[j] -= d.jacp[j];
+      // dense chain rule into the row (the next rows are written after this one), then
+      // gathered to the structural nonzeros (ascending, so in place)
+      for (int j = 0; j < nv; j++) {
+        double mj = 0;
+        for (int k = 0; k < 3; k++) mj += dlda[k]*d.jacr[k*nv+j] + dldv[k]*d.jacsc[k*nv+j];
+        moment[j] = mj*gear[0];            // scale by gear ratio (:1039-1043)
+      }
+      d.actuator_length[i] = d.actuator_length[i]*gear[0];
+      for (int k = 0; k < m.moment_rownnz[i]; k++) moment[k] = moment[m.moment_colind[adr+k]];
     } else {                                // fixed tendon :1053-1081 (model-constant nonzeros)
       d.actuator_length[i] = d.ten_length[id]*gear[0];
       for (int k = 0; k < m.moment_rownnz[i]; k++) {

@@ -381,13 +381,10 @@ static const char* unsupported(const mjhipModel* m) {
   }
   for (int i = 0; i < m->nu; i++) {
     int t = m->actuator_trntype[i];
-    if (t != mjhipTRN_JOINT && t != mjhipTRN_JOINTINPARENT && t != mjhipTRN_TENDON) {
-      return "slider-crank/site/body transmissions";
+    if (t != mjhipTRN_JOINT && t != mjhipTRN_JOINTINPARENT && t != mjhipTRN_TENDON &&
+        t != mjhipTRN_SLIDERCRANK) {
+      return "site/body transmissions";
     }
-  }
-  int ncon = mjhip_contactCapacity(m, nullptr);
-  if (ncon < 0) {
-    return "a collidable geom pair needs a collision function other than plane/sphere/capsule";
   }
   for (int i = 0; i < m->nsensor; i++) {
     const int t = m->sensor_type[i];

@@ -74,6 +74,11 @@ class MjData:
     return self.struct.nefc
 
   @property
+  def status(self):
+    """mjhipInstanceStatus bits of the last call."""
+    return self.struct.status
+
+  @property
   def solver_fwdinv(self):
     return np.array(self.struct.solver_fwdinv[:2])
 

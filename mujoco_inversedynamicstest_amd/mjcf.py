@@ -1287,23 +1287,34 @@ class MJCFCompiler:
     actr = arr("actuator_ctrlrange", (nu, 2), np.float64)
     afr = arr("actuator_forcerange", (nu, 2), np.float64)
     agear = arr("actuator_gear", (nu, 6), np.float64)
+    acrank = arr("actuator_cranklength", nu, np.float64)
     arr("actuator_length0", nu, np.float64)
     arr("actuator_acc0", nu, np.float64)
     na_count = 0                        # activation states (dyntype != none)
     for ai, a in enumerate(self.actuators):
       tag = a["__tag"]
-      tname = {"joint": jname, "jointinparent": jname,
+      sitename = {x["name"]: i for i, x in enumerate(sites) if x["name"]}
+      tname = {"joint": jname, "jointinparent": jname, "cranksite": sitename,
                "tendon": {ta.get("name"): i for i, (ta, _) in enumerate(self.tendons)
                           if ta.get("name")}}
-      trn = [k for k in ("joint", "jointinparent", "tendon") if k in a]
+      trn = [k for k in ("joint", "jointinparent", "tendon", "cranksite") if k in a]
       if len(trn) != 1:
-        raise MJCFError("only joint, jointinparent and fixed-tendon transmissions are in "
-                        "the supported subset (slider-crank/site/body transmissions are next)"
+        raise MJCFError("only joint, jointinparent, fixed-tendon and slider-crank "
+                        "transmissions are in the supported subset (site/body are next)"
                         if not trn else "actuator has more than one transmission target")
       if a[trn[0]] not in tname[trn[0]]:
         raise MJCFError(f"unknown {trn[0]} '{a[trn[0]]}' in actuator")
-      atrn[ai] = {"joint": 0, "jointinparent": 1, "tendon": 3}[trn[0]]
+      atrn[ai] = {"joint": 0, "jointinparent": 1, "cranksite": 2, "tendon": 3}[trn[0]]
       atrnid[ai, 0] = tname[trn[0]][a[trn[0]]]
+      if trn[0] == "cranksite":         # mjCActuator::ResolveReferences (user_objects.cc:5858-5877)
+        if not a.get("slidersite"):
+          raise MJCFError("missing base site for slider-crank")
+        if a["slidersite"] not in sitename:
+          raise MJCFError(f"base site '{a['slidersite']}' not found")
+        atrnid[ai, 1] = sitename[a["slidersite"]]
+        acrank[ai] = float(a.get("cranklength", 0.0))
+        if acrank[ai] <= 0:
+          raise MJCFError("crank length must be positive")
       gear = [1.0, 0, 0, 0, 0, 0]
       if "gear" in a:
         g = _floats(a["gear"])
@@ -1633,6 +1644,16 @@ class MJCFCompiler:
       if atrn[ai] in (0, 1):
         cnt = {0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[tid])]
         c = list(range(jdadr[tid], jdadr[tid] + cnt))
+      elif atrn[ai] == 2:
+        # slider-crank: the dense moment is the chain rule over the two sites' Jacobians
+        # (:1035-1052); its structural nonzeros are the dofs of both sites' body chains
+        c = set()
+        for sid in atrnid[ai]:
+          b = int(sbody[sid])
+          while b > 0:
+            c.update(range(dofadr[b], dofadr[b] + dofnum[b]))
+            b = int(parentid[b])
+        c = sorted(c) if agear[ai, 0] != 0 else []
       else:
         row = np.zeros(nv)
         for wi in range(tadr[tid], tadr[tid] + tnum[tid]):
@@ -1644,7 +1665,7 @@ class MJCFCompiler:
     # nJmom as CountNJmom (user_model.cc:2703-2750): 1/3/6 per joint transmission, nv per
     # tendon, so actuator_moment has the reference's size; colind past the nonzeros is 0
     nJmom = sum({0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[atrnid[ai, 0]])] if atrn[ai] in (0, 1)
-                else nv for ai in range(nu))
+                else nv for ai in range(nu))    # slider-crank and tendon: nv
     mcol = arr("moment_colind", nJmom, np.int32)
     mcol[:len(cols)] = cols
     s["nJmom"] = nJmom

@@ -289,6 +289,31 @@ def set_const(m):
         length = 0.0
         mom[da:da + 3] = gear[:3]
         mom[da + 3:da + 6] = ga
+    elif m.actuator_trntype[a] == 2:   # slider-crank (:1000-1052)
+      def site(s):
+        b = m.site_bodyid[s]
+        return e.xmat[b] @ m.site_pos[s] + e.xpos[b], \
+            _quat2mat(_mulquat(e.xquat[b], m.site_quat[s]))
+      sl = m.actuator_trnid[a, 1]
+      ps, ms = site(sl)
+      pc, _ = site(tid)
+      axis = ms[:, 2]
+      vec = pc - ps
+      av = vec @ axis
+      rod = m.actuator_cranklength[a]
+      det = av * av + rod * rod - vec @ vec
+      if det <= 0:
+        length, dlda, dldv = av, vec, axis
+      else:
+        sdet = np.sqrt(det)
+        length = av - sdet
+        dldv = axis * (1 - av / sdet) + vec / sdet
+        dlda = vec * (1 - av / sdet)
+      jS, jr = e.jac_point(m, m.site_bodyid[sl], ps)
+      jA = np.cross(jr.T, axis).T                       # mj_jacPointAxis
+      jC, _ = e.jac_point(m, m.site_bodyid[tid], pc)
+      length = length * gear[0]
+      mom = (dlda @ jA + dldv @ (jC - jS)) * gear[0]
     else:
       length = L0[tid] * gear[0]
       mom = J0[tid] * gear[0]

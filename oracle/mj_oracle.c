@@ -763,6 +763,58 @@ static void or_transmission(const mjhipModel* m, mjhipData* d) {
         mju_copy3(moment, gear);
         mju_copy3(moment+3, gearAxis);
       }
+    } else if (trn == mjhipTRN_SLIDERCRANK) {   /* :1000-1052 */
+      int idslider = m->actuator_trnid[2*i+1];
+      mjtNum rod = m->actuator_cranklength[i];
+      mjtNum axis[3] = {d->site_xmat[9*idslider+2], d->site_xmat[9*idslider+5],
+                        d->site_xmat[9*idslider+8]};
+      mjtNum vec[3], dlda[3], dldv[3];
+      mju_sub3(vec, d->site_xpos+3*id, d->site_xpos+3*idslider);
+      mjtNum av = mju_dot3(vec, axis);
+      mjtNum sdet, det = av*av + rod*rod - mju_dot3(vec, vec);
+      int ok = 1;
+      if (det <= 0) {
+        ok = 0;
+        sdet = 0;
+        *length = av;
+      } else {
+        sdet = sqrt(det);
+        *length = av - sdet;
+      }
+      if (ok) {
+        mju_scl3(dldv, axis, 1-av/sdet);
+        mju_scl3(dlda, vec, 1/sdet);
+        mju_addTo3(dldv, dlda);
+        mju_scl3(dlda, vec, 1-av/sdet);
+      } else {
+        mju_copy3(dlda, vec);
+        mju_copy3(dldv, axis);
+      }
+      /* mj_jacPointAxis (engine_support.c:501-521) and mj_jacSite */
+      mjtNum* jacS = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+      mjtNum* jacr = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+      mjtNum* jacA = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+      mjtNum* jac = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+      mj_jac(m, d, jacS, jacr, d->site_xpos+3*idslider, m->site_bodyid[idslider]);
+      for (int j = 0; j < nv; j++) {
+        jacA[j]      = jacr[nv+j]*axis[2] - jacr[2*nv+j]*axis[1];
+        jacA[nv+j]   = jacr[2*nv+j]*axis[0] - jacr[j]*axis[2];
+        jacA[2*nv+j] = jacr[j]*axis[1] - jacr[nv+j]*axis[0];
+      }
+      mj_jac(m, d, jac, NULL, d->site_xpos+3*id, m->site_bodyid[id]);
+      for (int j = 0; j < 3*nv; j++) jac[j] -= jacS[j];
+      mju_zero(moment, nv);
+      for (int j = 0; j < nv; j++) {
+        for (int k = 0; k < 3; k++) {
+          moment[j] += dlda[k]*jacA[k*nv+j] + dldv[k]*jac[k*nv+j];
+        }
+      }
+      *length *= gear[0];
+      for (int j = 0; j < nv; j++) moment[j] *= gear[0];
+      /* compress to the structural nonzeros (the reference drops entries that evaluate
+       * to exactly 0; the structure here is the two sites' dof chains) */
+      for (int k = 0; k < m->moment_rownnz[i]; k++) moment[k] = moment[m->moment_colind[adr+k]];
+      free(jacS); free(jacr); free(jacA); free(jac);
     } else {   /* mjTRN_TENDON, dense: gear*ten_J compressed to its nonzeros */
       *length = d->ten_length[id]*gear[0];
       for (int k = 0; k < m->moment_rownnz[i]; k++) {
@@ -1378,7 +1430,8 @@ static int or_filterSphere(const mjhipModel* m, const mjhipData* d, int g1, int 
 static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, int g1, int g2) {
   if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
-  if (mjhip_pairMaxContacts(t1, t2) <= 0) return;   /* none (unsupported: rejected earlier) */
+  const int kmax = mjhip_pairMaxContacts(t1, t2);
+  if (kmax == 0) return;
   if (mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1], m->geom_contype[g2],
                           m->geom_conaffinity[g2])) {
     return;
@@ -1386,6 +1439,10 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
   mjtNum margin = mjENABLED(mjhipENBL_OVERRIDE) ? m->opt.o_margin
                                                 : mjMAX(m->geom_margin[g1], m->geom_margin[g2]);
   if (or_filterSphere(m, d, g1, g2, margin)) return;
+  if (kmax < 0) {              /* a collision function outside the subset would run: flag */
+    ((mjhipData*)d)->status |= MJHIP_INST_UNSUPPORTED;
+    return;
+  }
   const mjtNum *pos1 = d->geom_xpos + 3*g1, *mat1 = d->geom_xmat + 9*g1;
   const mjtNum *pos2 = d->geom_xpos + 3*g2, *mat2 = d->geom_xmat + 9*g2;
   const mjtNum *size1 = m->geom_size + 3*g1, *size2 = m->geom_size + 3*g2;
@@ -3014,6 +3071,7 @@ void or_inverseSkip(const mjhipModel* m, mjhipData* d, orEfc* e, int skipstage,
                     int skipsensor) {
   int nv = m->nv;
   mjtNum* qacc = NULL;
+  d->status = 0;
   if (skipstage < mjhipSTAGE_POS) {
     or_invPosition(m, d, e);
     if (!skipsensor) or_sensorPos(m, d, e);
@@ -3092,6 +3150,7 @@ static void or_fwdActuation(const mjhipModel* m, mjhipData* d) {
  * with qacc = qacc_smooth (engine_forward.c:520-531, :654-: nefc = 0) */
 int or_forward(const mjhipModel* m, mjhipData* d, orEfc* e) {
   int nv = m->nv;
+  d->status = 0;
   or_invPosition(m, d, e);
   or_fwdVelocity(m, d, e);
   or_fwdActuation(m, d);

@@ -106,11 +106,7 @@ class Oracle:
       setattr(self.efc, n, _p(a))
     for n, a in self._efc_int.items():
       setattr(self.efc, n, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
-    ncap = self.L.or_contactCapacity(ctypes.byref(self.cm))
-    if ncap < 0:
-      raise UnsupportedModel("a candidate geom pair needs a collision function outside the "
-                             "implemented primitives (plane/sphere/capsule)")
-    ncap = max(ncap, 1)
+    ncap = max(self.L.or_contactCapacity(ctypes.byref(self.cm)), 1)
     self.efc.con_capacity = ncap
     self._con = {n: np.zeros(ncap * k) for n, k in CON_DOUBLE}
     self._con.update({n: np.zeros(ncap * k, dtype=np.int32) for n, k in CON_INT})

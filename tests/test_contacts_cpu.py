@@ -244,11 +244,29 @@ def test_box_cylinder_device_bitexact():
   assert total > 60
 
 
-def test_unsupported_pair_rejected():
-  m = mjcf.load_xml_string("""<mujoco><worldbody><geom type="box" size="1 1 1"/>
-    <body><freejoint/><geom type="box" size=".1 .1 .1"/></body></worldbody></mujoco>""")
-  with pytest.raises(UnsupportedModel):
-    Oracle(m)
+def test_unimplemented_pair_flagged_per_instance():
+  """A box-box pair (mjc_BoxBox, outside the subset) adds no capacity; an instance whose
+  pair passes the bounding-sphere filter is flagged MJHIP_INST_UNSUPPORTED, the others are
+  exact (here: the plane-sphere contact of the same instance is still made)."""
+  m = mjcf.load_xml_string("""<mujoco><worldbody><geom type="plane" size="5 5 .1"/>
+    <geom type="box" size=".5 .5 .5" pos="0 0 2"/>
+    <body pos="0 0 2"><freejoint/><geom type="box" size=".1 .1 .1" contype="2"
+      conaffinity="2"/><geom type="sphere" size=".1" pos="0 0 -.1" contype="1"
+      conaffinity="1"/></body></worldbody></mujoco>""")
+  cm = host.model_struct(m)
+  assert olib().or_contactCapacity(ctypes.byref(cm)) == 1       # plane-sphere only
+  o = Oracle(m)
+  k = KernelCPU(m, o.efc.capacity)
+  outs = [f.name for f in fields.DATA_FIELDS if f.stage > 0]
+  for z, flag in ((0.05, 0), (2.3, 32)):   # far from the world box / overlapping it
+    q = np.array([0, 0, z, 1, 0, 0, 0.0])
+    v, a = np.zeros(6), np.zeros(6)
+    o.inverse(q, v, a)
+    _, st = k.inverse(q, v, a)
+    assert o.d.status == st == flag
+    assert o.efc.ncon == (1 if z < 1 else 0)
+    for f in outs:
+      np.testing.assert_array_equal(getattr(k.d, f), getattr(o.d, f), err_msg=f)
 
 
 def test_capacity_exact():

@@ -662,6 +662,30 @@ def test_transmission_parity():
   e.close()
 
 
+def test_slider_crank_parity():
+  """BASELINE.json config 1 model: slider-crank transmissions, per-instance UNSUPPORTED
+  flags where a convex pair passes the bounding-sphere filter, exact elsewhere."""
+  m = models.load("slider_crank")
+  B = 256
+  rng = np.random.default_rng(11)
+  q, v, a = rng.uniform(-np.pi, np.pi, (B, 3)), rng.normal(size=(B, 3)), rng.normal(size=(B, 3))
+  e = engine.InverseEngine(m, capacity=B)
+  f, st = e.inverse(q, v, a, status=True)
+  o = Oracle(m)
+  ref, lref, mref, oref = [], [], [], []
+  for i in range(B):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    oref.append(o.d.status)
+    lref.append(o.d.actuator_length.copy())
+    mref.append(o.d.actuator_moment.copy())
+  np.testing.assert_array_equal(st, oref)
+  assert 0 < np.count_nonzero(st) < B
+  assert_close(f, np.array(ref), "qfrc_inverse")
+  assert_close(e.field("actuator_length", 0, B), np.array(lref), "actuator_length")
+  assert_close(e.field("actuator_moment", 0, B), np.array(mref), "actuator_moment")
+  e.close()
+
+
 def test_fluid_parity():
   """Inertia-box fluid forces (viscosity and density, with wind) on the device."""
   m = models.load("equality_site")
