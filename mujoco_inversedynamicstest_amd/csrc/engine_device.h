@@ -1505,6 +1505,17 @@ MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d) {
       }
       d.actuator_length[i] = d.actuator_length[i]*gear[0];
       for (int k = 0; k < m.moment_rownnz[i]; k++) moment[k] = moment[m.moment_colind[adr+k]];
+    } else if (trn == mjhipTRN_SITE) {      // :1083-1103, no reference site: length 0
+      const int nv = m.nv;
+      double wrench[6];
+      jacInto(m, d, d.jacp, d.jacr, d.site_xpos + 3*id, m.site_bodyid[id]);
+      d.actuator_length[i] = 0;
+      mulMatVec3(wrench, d.site_xmat + 9*id, gear);
+      mulMatVec3(wrench + 3, d.site_xmat + 9*id, gear + 3);
+      mulMatTVec(moment, d.jacp, wrench, 3, nv);
+      mulMatTVec(d.jacp, d.jacr, wrench + 3, 3, nv);
+      for (int j = 0; j < nv; j++) moment[j] += d.jacp[j];
+      for (int k = 0; k < m.moment_rownnz[i]; k++) moment[k] = moment[m.moment_colind[adr+k]];
     } else {                                // fixed tendon :1053-1081 (model-constant nonzeros)
       d.actuator_length[i] = d.ten_length[id]*gear[0];
       for (int k = 0; k < m.moment_rownnz[i]; k++) {

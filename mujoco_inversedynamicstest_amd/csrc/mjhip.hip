@@ -382,8 +382,11 @@ static const char* unsupported(const mjhipModel* m) {
   for (int i = 0; i < m->nu; i++) {
     int t = m->actuator_trntype[i];
     if (t != mjhipTRN_JOINT && t != mjhipTRN_JOINTINPARENT && t != mjhipTRN_TENDON &&
-        t != mjhipTRN_SLIDERCRANK) {
-      return "site/body transmissions";
+        t != mjhipTRN_SLIDERCRANK && t != mjhipTRN_SITE) {
+      return "body transmissions";
+    }
+    if (t == mjhipTRN_SITE && m->actuator_trnid[2*i+1] >= 0) {
+      return "site transmissions with a reference site";
     }
   }
   for (int i = 0; i < m->nsensor; i++) {

@@ -1294,17 +1294,20 @@ class MJCFCompiler:
     for ai, a in enumerate(self.actuators):
       tag = a["__tag"]
       sitename = {x["name"]: i for i, x in enumerate(sites) if x["name"]}
-      tname = {"joint": jname, "jointinparent": jname, "cranksite": sitename,
+      tname = {"joint": jname, "jointinparent": jname, "cranksite": sitename, "site": sitename,
                "tendon": {ta.get("name"): i for i, (ta, _) in enumerate(self.tendons)
                           if ta.get("name")}}
-      trn = [k for k in ("joint", "jointinparent", "tendon", "cranksite") if k in a]
+      trn = [k for k in ("joint", "jointinparent", "tendon", "cranksite", "site") if k in a]
       if len(trn) != 1:
-        raise MJCFError("only joint, jointinparent, fixed-tendon and slider-crank "
-                        "transmissions are in the supported subset (site/body are next)"
+        raise MJCFError("only joint, jointinparent, fixed-tendon, slider-crank and site "
+                        "transmissions are in the supported subset (body is next)"
                         if not trn else "actuator has more than one transmission target")
+      if "refsite" in a:
+        raise MJCFError("site transmissions with a reference site are not in the subset")
       if a[trn[0]] not in tname[trn[0]]:
         raise MJCFError(f"unknown {trn[0]} '{a[trn[0]]}' in actuator")
-      atrn[ai] = {"joint": 0, "jointinparent": 1, "cranksite": 2, "tendon": 3}[trn[0]]
+      atrn[ai] = {"joint": 0, "jointinparent": 1, "cranksite": 2, "tendon": 3,
+                  "site": 4}[trn[0]]
       atrnid[ai, 0] = tname[trn[0]][a[trn[0]]]
       if trn[0] == "cranksite":         # mjCActuator::ResolveReferences (user_objects.cc:5858-5877)
         if not a.get("slidersite"):
@@ -1644,16 +1647,19 @@ class MJCFCompiler:
       if atrn[ai] in (0, 1):
         cnt = {0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[tid])]
         c = list(range(jdadr[tid], jdadr[tid] + cnt))
-      elif atrn[ai] == 2:
+      elif atrn[ai] in (2, 4):
         # slider-crank: the dense moment is the chain rule over the two sites' Jacobians
         # (:1035-1052); its structural nonzeros are the dofs of both sites' body chains
         c = set()
         for sid in atrnid[ai]:
+          if sid < 0:
+            continue
           b = int(sbody[sid])
           while b > 0:
             c.update(range(dofadr[b], dofadr[b] + dofnum[b]))
             b = int(parentid[b])
-        c = sorted(c) if agear[ai, 0] != 0 else []
+        gzero = agear[ai, 0] == 0 if atrn[ai] == 2 else not np.any(agear[ai])
+        c = [] if gzero else sorted(c)
       else:
         row = np.zeros(nv)
         for wi in range(tadr[tid], tadr[tid] + tnum[tid]):

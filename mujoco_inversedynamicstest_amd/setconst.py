@@ -314,6 +314,13 @@ def set_const(m):
       jC, _ = e.jac_point(m, m.site_bodyid[tid], pc)
       length = length * gear[0]
       mom = (dlda @ jA + dldv @ (jC - jS)) * gear[0]
+    elif m.actuator_trntype[a] == 4:   # site, no reference site (:1083-1103)
+      b = m.site_bodyid[tid]
+      p = e.xmat[b] @ m.site_pos[tid] + e.xpos[b]
+      R = _quat2mat(_mulquat(e.xquat[b], m.site_quat[tid]))
+      jp, jr = e.jac_point(m, b, p)
+      length = 0.0
+      mom = jp.T @ (R @ gear[:3]) + jr.T @ (R @ gear[3:])
     else:
       length = L0[tid] * gear[0]
       mom = J0[tid] * gear[0]

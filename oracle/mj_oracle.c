@@ -815,6 +815,19 @@ static void or_transmission(const mjhipModel* m, mjhipData* d) {
        * to exactly 0; the structure here is the two sites' dof chains) */
       for (int k = 0; k < m->moment_rownnz[i]; k++) moment[k] = moment[m->moment_colind[adr+k]];
       free(jacS); free(jacr); free(jacA); free(jac);
+    } else if (trn == mjhipTRN_SITE) {   /* :1083-1103, no reference site */
+      mjtNum wrench[6];
+      mjtNum* jac = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+      mjtNum* jacS = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+      mj_jac(m, d, jac, jacS, d->site_xpos+3*id, m->site_bodyid[id]);
+      *length = 0;
+      mju_mulMatVec3(wrench, d->site_xmat+9*id, gear);
+      mju_mulMatVec3(wrench+3, d->site_xmat+9*id, gear+3);
+      mju_mulMatTVec(moment, jac, wrench, 3, nv);
+      mju_mulMatTVec(jac, jacS, wrench+3, 3, nv);
+      mju_addTo(moment, jac, nv);
+      for (int k = 0; k < m->moment_rownnz[i]; k++) moment[k] = moment[m->moment_colind[adr+k]];
+      free(jac); free(jacS);
     } else {   /* mjTRN_TENDON, dense: gear*ten_J compressed to its nonzeros */
       *length = d->ten_length[id]*gear[0];
       for (int k = 0; k < m->moment_rownnz[i]; k++) {

@@ -27,6 +27,7 @@ XML = """<mujoco><option><flag contact="disable"/></option><worldbody>
     <geom type="capsule" fromto="0 0 0 .4 0 0" size=".04"/>
     <body name="b" pos=".4 0 0"><joint name="ball" type="ball"/>
       <geom type="capsule" fromto="0 0 0 .3 0 0" size=".03"/>
+      <site name="tip" pos=".3 0 0" euler="10 20 30"/>
       <body pos=".3 0 0"><joint name="s" type="slide" axis="1 0 0"/><geom size=".05"/></body>
     </body></body>
   <body name="f" pos="1 0 1" quat="0.9 0.1 -0.3 0.2"><freejoint name="free"/>
@@ -42,6 +43,7 @@ XML = """<mujoco><option><flag contact="disable"/></option><worldbody>
     <motor tendon="t" gear="2"/>
     <motor tendon="z" gear="-1.5"/>
     <position joint="h" kp="10"/>
+    <general site="tip" gear="1 -2 .5 .3 .2 -.1"/>
   </actuator>
   <sensor><actuatorpos actuator="m0"/></sensor></mujoco>"""
 
@@ -69,10 +71,11 @@ def model():
 
 def test_structure(model):
   m = model
-  assert list(m.actuator_trntype) == [0, 1, 0, 1, 3, 3, 0]
-  assert list(m.moment_rownnz) == [3, 3, 6, 6, 2, 1, 1]
-  assert list(m.moment_rowadr) == [0, 3, 6, 12, 18, 20, 21]
-  assert m.nJmom == 3 + 3 + 6 + 6 + m.nv + m.nv + 1       # CountNJmom
+  assert list(m.actuator_trntype) == [0, 1, 0, 1, 3, 3, 0, 4]
+  assert list(m.moment_rownnz) == [3, 3, 6, 6, 2, 1, 1, 4]
+  assert list(m.moment_rowadr) == [0, 3, 6, 12, 18, 20, 21, 22]
+  assert m.nJmom == 3 + 3 + 6 + 6 + m.nv + m.nv + 1 + m.nv       # CountNJmom
+  assert list(m.moment_colind[22:26]) == [0, 1, 2, 3]      # the site body's dof chain
   h, ball, s, free = (m.jnt_dofadr[i] for i in range(4))
   assert list(m.moment_colind[18:22]) == [h, s, s, h]
   assert codegen.fast_path_supported(m) is not None
@@ -137,7 +140,7 @@ def test_device_bitexact(model):
       np.testing.assert_array_equal(getattr(k.d, f), getattr(o.d, f), err_msg=f"{f} {i}")
 
 
-@pytest.mark.parametrize("attr", ["site", "body", "cranksite"])
+@pytest.mark.parametrize("attr", ["body", "cranksite"])
 def test_other_transmissions_rejected(attr):
   with pytest.raises(mjcf.MJCFError):
     mjcf.load_xml_string(f"""<mujoco><worldbody><body name="b"><joint/><geom size=".1"/>
@@ -233,3 +236,26 @@ def test_slider_crank_device_bitexact_and_flags():
     for f in outs:
       np.testing.assert_array_equal(getattr(k.d, f), getattr(o.d, f), err_msg=f"{f} {i}")
   assert 0 < flagged < 64
+
+
+def test_site_transmission_hinge_closed_form():
+  """Site transmission without a reference site (:1083-1103): length 0, moment = J'wrench
+  with the gear in the site frame; on a hinge arm of length L about z, a force along the
+  site's y and a torque about its z give L*g_y + g_rz at every angle."""
+  m = mjcf.load_xml_string("""<mujoco><worldbody><body><joint name="h" axis="0 0 1"/>
+    <geom type="capsule" fromto="0 0 0 .7 0 0" size=".05"/><site name="s" pos=".7 0 0"/>
+    </body></worldbody><actuator><general site="s" gear="0.4 1.5 0 0 0 2"/></actuator>
+    </mujoco>""")
+  o = Oracle(m)
+  for th in (-2.0, 0.3, 1.1):
+    o.inverse(np.array([th]), np.zeros(1), np.zeros(1))
+    assert o.d.actuator_length[0] == 0
+    np.testing.assert_allclose(o.d.actuator_moment[0], 0.7 * 1.5 + 2, rtol=1e-14)
+  np.testing.assert_allclose(m.actuator_acc0[0], (0.7 * 1.5 + 2) / o.fullM()[0, 0], rtol=1e-12)
+
+
+def test_site_refsite_rejected():
+  with pytest.raises(mjcf.MJCFError):
+    mjcf.load_xml_string("""<mujoco><worldbody><body><joint/><geom size=".1"/><site name="a"/>
+      <site name="b" pos=".1 0 0"/></body></worldbody><actuator><general site="a"
+      refsite="b"/></actuator></mujoco>""")
