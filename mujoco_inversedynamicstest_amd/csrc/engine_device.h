@@ -812,6 +812,53 @@ MJH_HD int rawSphereSphere(RawContact* c, double margin, P1 pos1, M1 mat1, doubl
   return 1;
 }
 
+template <class R, class M, class V> MJH_HD void mulMatTVec3(R res, M mat, V vec);
+
+// engine_collision_box.c:38-92 mjraw_SphereBox (the box's size clamps the sphere centre)
+template <class P1, class P2, class M2>
+MJH_HD int rawSphereBox(RawContact* c, double margin, P1 pos1, double r1, P2 pos2, M2 mat2,
+                        const double* size2) {
+  double tmp[3], center[3], clamped[3], deepest[3], pos[3];
+  sub3(tmp, pos1, pos2);
+  mulMatTVec3(center, mat2, tmp);
+  copy3(clamped, center);
+  for (int i = 0; i < 3; i++) {        // mju_clampVec
+    if (size2[i] > 0) {
+      if (clamped[i] < -size2[i]) clamped[i] = -size2[i];
+      else if (clamped[i] > size2[i]) clamped[i] = size2[i];
+    }
+  }
+  copy3(deepest, center);
+  sub3(tmp, clamped, center);
+  double dist = normalize3(tmp);
+  if (dist - r1 > margin) return 0;
+  if (dist <= MINVAL) {                 // centre inside the box: nearest face
+    double closest = (size2[0] + size2[1] + size2[2])*2;
+    int k = 0;
+    for (int i = 0; i < 6; i++) {
+      const double f = fabs((i % 2 ? 1 : -1)*size2[i/2] - center[i/2]);
+      if (closest > f) { closest = f; k = i; }
+    }
+    double nearest[3] = {0, 0, 0};
+    nearest[k/2] = (k % 2 ? -1 : 1);
+    copy3(pos, center);
+    addToScl3(pos, nearest, (r1 - closest)/2);
+    mulMatVec3(c->frame, mat2, nearest);
+    dist = -closest;
+  } else {
+    addToScl3(deepest, tmp, r1);
+    zero3(pos);
+    addToScl3(pos, clamped, 0.5);
+    addToScl3(pos, deepest, 0.5);
+    mulMatVec3(c->frame, mat2, tmp);
+  }
+  mulMatVec3(tmp, mat2, pos);
+  add3(c->pos, tmp, pos2);
+  c->dist = dist - r1;
+  zero3(c->frame + 3);
+  return 1;
+}
+
 // mjraw_SphereCapsule
 template <class P1, class M1, class P2, class M2>
 MJH_HD int colSphereCapsule(RawContact* c, double margin, P1 pos1, M1 mat1, double r1, P2 pos2,
@@ -1007,6 +1054,8 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
     num = rawSphereSphere(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2[0]);
   } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CAPSULE) {
     num = colSphereCapsule(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_BOX) {
+    num = rawSphereBox(raw, margin, pos1, size1[0], pos2, mat2, size2);
   } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {
     num = colCapsuleCapsule(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
   }

@@ -1266,6 +1266,54 @@ static int col_planeCapsule(orRaw* c, mjtNum margin, const mjtNum* pos1, const m
 }
 
 /* mjraw_SphereSphere */
+static void mju_mulMatTVec3(mjtNum res[3], const mjtNum mat[9], const mjtNum vec[3]);
+
+/* engine_collision_box.c:21-92 mju_clampVec + mjraw_SphereBox */
+static int raw_sphereBox(orRaw* c, mjtNum margin, const mjtNum* pos1, mjtNum r1,
+                         const mjtNum* pos2, const mjtNum* mat2, const mjtNum* size2) {
+  mjtNum tmp[3], center[3], clamped[3], deepest[3], pos[3], dist, closest;
+  int k = 0;
+  mju_sub3(tmp, pos1, pos2);
+  mju_mulMatTVec3(center, mat2, tmp);
+  mju_copy3(clamped, center);
+  for (int i = 0; i < 3; i++) {
+    if (size2[i] > 0) {
+      if (clamped[i] < -size2[i]) clamped[i] = -size2[i];
+      else if (clamped[i] > size2[i]) clamped[i] = size2[i];
+    }
+  }
+  mju_copy3(deepest, center);
+  mju_sub3(tmp, clamped, center);
+  dist = mju_normalize3(tmp);
+  if (dist - r1 > margin) return 0;
+  if (dist <= mjMINVAL) {
+    closest = (size2[0] + size2[1] + size2[2]) * 2;
+    for (int i = 0; i < 6; i++) {
+      if (closest > fabs((i % 2 ? 1 : -1)*size2[i/2] - center[i/2])) {
+        closest = fabs((i % 2 ? 1 : -1)*size2[i/2] - center[i/2]);
+        k = i;
+      }
+    }
+    mjtNum nearest[3] = {0, 0, 0};
+    nearest[k/2] = (k % 2 ? -1 : 1);
+    mju_copy3(pos, center);
+    mju_addToScl3(pos, nearest, (r1 - closest) / 2);
+    mju_mulMatVec3(c->frame, mat2, nearest);
+    dist = -closest;
+  } else {
+    mju_addToScl3(deepest, tmp, r1);
+    mju_zero3(pos);
+    mju_addToScl3(pos, clamped, 0.5);
+    mju_addToScl3(pos, deepest, 0.5);
+    mju_mulMatVec3(c->frame, mat2, tmp);
+  }
+  mju_mulMatVec3(tmp, mat2, pos);
+  mju_add3(c->pos, tmp, pos2);
+  c->dist = dist - r1;
+  mju_zero3(c->frame + 3);
+  return 1;
+}
+
 static int raw_sphereSphere(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
                             mjtNum r1, const mjtNum* pos2, const mjtNum* mat2, mjtNum r2) {
   mjtNum dif[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
@@ -1473,6 +1521,8 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
     num = raw_sphereSphere(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2[0]);
   } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CAPSULE) {
     num = col_sphereCapsule(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_BOX) {
+    num = raw_sphereBox(raw, margin, pos1, size1[0], pos2, mat2, size2);
   } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {
     num = col_capsuleCapsule(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
   }

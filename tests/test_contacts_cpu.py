@@ -254,7 +254,7 @@ def test_unimplemented_pair_flagged_per_instance():
       conaffinity="2"/><geom type="sphere" size=".1" pos="0 0 -.1" contype="1"
       conaffinity="1"/></body></worldbody></mujoco>""")
   cm = host.model_struct(m)
-  assert olib().or_contactCapacity(ctypes.byref(cm)) == 1       # plane-sphere only
+  assert olib().or_contactCapacity(ctypes.byref(cm)) == 2       # plane-sphere, sphere-box
   o = Oracle(m)
   k = KernelCPU(m, o.efc.capacity)
   outs = [f.name for f in fields.DATA_FIELDS if f.stage > 0]
@@ -264,7 +264,7 @@ def test_unimplemented_pair_flagged_per_instance():
     o.inverse(q, v, a)
     _, st = k.inverse(q, v, a)
     assert o.d.status == st == flag
-    assert o.efc.ncon == (1 if z < 1 else 0)
+    assert o.efc.ncon == 1                 # plane-sphere low, sphere-box high
     for f in outs:
       np.testing.assert_array_equal(getattr(k.d, f), getattr(o.d, f), err_msg=f)
 
