@@ -249,7 +249,7 @@ def test_unimplemented_pair_flagged_per_instance():
   pair passes the bounding-sphere filter is flagged MJHIP_INST_UNSUPPORTED, the others are
   exact (here: the plane-sphere contact of the same instance is still made)."""
   m = mjcf.load_xml_string("""<mujoco><worldbody><geom type="plane" size="5 5 .1"/>
-    <geom type="box" size=".5 .5 .5" pos="0 0 2"/>
+    <geom type="box" size=".5 .5 .5" pos="0 0 2" contype="3" conaffinity="3"/>
     <body pos="0 0 2"><freejoint/><geom type="box" size=".1 .1 .1" contype="2"
       conaffinity="2"/><geom type="sphere" size=".1" pos="0 0 -.1" contype="1"
       conaffinity="1"/></body></worldbody></mujoco>""")
