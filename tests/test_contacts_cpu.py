@@ -203,6 +203,30 @@ def test_plane_cylinder_disk_triangle():
   np.testing.assert_allclose(o.contact_field("con_dist"), [-0.01, -0.01], atol=1e-15)
 
 
+def test_box_sphere_reference():
+  """BoxSphere (engine_collision_box_test.cc:247-273): a sphere at the top face of a box
+  that sits under a plane touches both, with equal distances, at every depth; the device
+  code equals the oracle bit for bit."""
+  m = mjcf.load_xml_string("""<mujoco><worldbody>
+    <geom type="plane" size="0.05 0.05 0.001"/>
+    <geom type="box" pos="0 0 -0.025" size="0.05 0.05 .025"/>
+    <body><freejoint/><geom type="sphere" mass="1" size="0.005"/></body>
+    </worldbody></mujoco>""")
+  o = Oracle(m)
+  k = KernelCPU(m, o.efc.capacity)
+  for z in (-.015, -.00501, -.005, -.00499, 0.0, 0.004):
+    q = m.qpos0.copy()
+    q[2] = z
+    o.inverse(q, np.zeros(6), np.zeros(6))
+    k.inverse(q, np.zeros(6), np.zeros(6))
+    assert o.efc.ncon == 2
+    d = o.contact_field("con_dist")
+    assert abs(d[0] - d[1]) < 1e-8
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name))
+
+
 def test_box_cylinder_device_bitexact():
   """Random poses of boxes and cylinders over a plane (condim 1/3/6): the device code on the
   host equals the oracle bit for bit on every contact, row and output."""
