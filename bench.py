@@ -3,18 +3,23 @@
 A step is one pass of the fused HIP mj_inverse over one batch of 65,536 synthetic humanoid
 states (config-2 sampler, contacts disabled, every limit inactive) whose inputs are already
 resident in the device mirror (HBM); every mjData output field of mj_inverse is written
-(2,563 doubles per instance). With N GPUs each rank owns its own 65,536-instance shard of
-the global batch (weak scaling, no collective in the timed region); after timing, rank 0
-gathers a checksum of every rank's qfrc_inverse over RCCL.
+(2,563 doubles per instance). With N GPUs each rank owns a contiguous shard of the global
+batch and there is no collective in the timed region. After that region, rank 0 gathers
+every rank's full qfrc_inverse (B x nv fp64) over RCCL point-to-point, and a second timed
+region runs step + gather back to back, so scaling is reported with and without the gather
+(SURVEY.md §8e).
 
-  python bench.py [--gpus N] [--steps K] [--warmup W]
-  torchrun --nproc-per-node N bench.py --gpus N ...
+  python bench.py [--gpus N] [--steps K] [--warmup W]      # spawns N ranks itself
+  python bench.py --gpus 8 --global-batch 262144           # config 3 (32,768 per GPU)
+  torchrun --nproc-per-node N bench.py --gpus N ...        # what the driver runs
 
-Prints ONE JSON line on rank 0 (contract in the task statement).
+Default per-GPU batch is 65,536 (weak scaling); --global-batch fixes the total instead
+(strong scaling). Prints ONE JSON line on rank 0 (contract in the task statement).
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -25,6 +30,33 @@ sys.path.insert(0, ROOT)
 
 METRIC = "mj_inverse evals/sec, humanoid 27-DoF, batch=65536 @ 1/2/4/8 MI355X vs host CPU"
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md chip table (spec)
+
+
+def available_cores() -> int:
+  """Host cores this process may run on: the affinity mask, capped by a cgroup-v2 CPU quota
+  (a container's cpu.max) when one is set."""
+  n = len(os.sched_getaffinity(0))
+  try:
+    quota, period = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+    if quota != "max":
+      n = min(n, max(1, int(quota) // int(period)))
+  except (OSError, ValueError):
+    pass
+  return n
+
+
+def spawn_ranks(gpus: int) -> int:
+  """Relaunch this script as `gpus` ranks (one process per GPU, torch.distributed.run on
+  127.0.0.1) and return their exit code. Called before anything touches the GPU: the parent
+  only waits for its child."""
+  import socket
+  with socket.socket() as s:
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+  cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+         f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+         os.path.abspath(__file__)] + sys.argv[1:]
+  return subprocess.call(cmd)
 
 
 def pmc_traffic(eng, model, count):
@@ -44,24 +76,50 @@ def pmc_traffic(eng, model, count):
   return None, None
 
 
+def timed(fn, steps, world, dist, torch, dev):
+  """Run fn `steps` times between barrier + device syncs; max wall time over ranks (s)."""
+  torch.cuda.synchronize(dev)
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize(dev)
+  t0 = time.perf_counter()
+  for _ in range(steps):
+    fn()
+  torch.cuda.synchronize(dev)
+  if world > 1:
+    dist.barrier()
+  torch.cuda.synchronize(dev)
+  t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64, device=dev)
+  if world > 1:
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+  return float(t.item())
+
+
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("--gpus", type=int, default=1)
   ap.add_argument("--steps", type=int, default=20)
   ap.add_argument("--warmup", type=int, default=5)
-  ap.add_argument("--batch", type=int, default=65536, help="instances per GPU")
+  ap.add_argument("--batch", type=int, default=65536, help="instances per GPU (weak scaling)")
+  ap.add_argument("--global-batch", type=int, default=None,
+                  help="total instances over all GPUs (strong scaling; config 3: 262144)")
   ap.add_argument("--model", default="humanoid")
-  ap.add_argument("--cpu-threads", type=int, default=16)
-  ap.add_argument("--cpu-sample", type=int, default=4_000_000,
-                  help="instances in the CPU-baseline sample (rank 0, N=1 only)")
+  ap.add_argument("--cpu-threads", type=int, default=None,
+                  help="CPU-baseline threads (default: every core available to the process)")
+  ap.add_argument("--cpu-sample", type=int, default=None,
+                  help="instances in the CPU-baseline sample (rank 0, N=1 only; default "
+                       "150k per thread, about 2-3 s of CPU work per thread)")
   ap.add_argument("--no-cpu", action="store_true")
   ap.add_argument("--config-batch", type=int, default=None,
                   help="batch for --config 4 (default 4096) or base states for 5 (1024)")
   ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
-                  help="2: the metric's workload (default). 4: contacts, keyframe poses, "
-                       "batch 4096. 5: mjd_inverseFD over 1024 base states. Configs 4/5 are "
-                       "parity cases reported for reference (DESIGN.md), not the metric")
+                  help="2: the metric's workload (default; with --global-batch 262144 and "
+                       "--gpus 8 it is config 3). 4: contacts, keyframe poses, batch 4096. "
+                       "5: mjd_inverseFD over 1024 base states. Configs 4/5 are parity cases "
+                       "reported for reference (DESIGN.md), not the metric")
   args = ap.parse_args()
+  if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+    sys.exit(spawn_ranks(args.gpus))
   if args.config != 2:
     return other_config(args)
 
@@ -71,21 +129,22 @@ def main():
   world = int(os.environ.get("WORLD_SIZE", "1"))
   rank = int(os.environ.get("RANK", "0"))
   local = int(os.environ.get("LOCAL_RANK", "0"))
+  if world != args.gpus:
+    raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}")
+  torch.cuda.set_device(local)
+  dev = torch.device("cuda", local)
   if world > 1:
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    torch.cuda.set_device(local)
-    dist.init_process_group("nccl", rank=rank, world_size=world,
-                            device_id=torch.device("cuda", local))
-  else:
-    torch.cuda.set_device(local)
-  dev = torch.device("cuda", local)
+    dist.init_process_group("nccl", rank=rank, world_size=world, device_id=dev)
 
-  from mujoco_inversedynamicstest_amd import codegen, engine, fields, models, parallel
+  from mujoco_inversedynamicstest_amd import codegen, engine, models, parallel
   from mujoco_inversedynamicstest_amd.sampler import sample_states
 
   m = models.load(args.model, disable_contact=True)
-  B = args.batch
-  first, count = parallel.shard(B * world, world, rank)
+  strong = args.global_batch is not None
+  total = args.global_batch if strong else args.batch * world
+  first, count = parallel.shard(total, world, rank)
+  counts = parallel.shard_counts(total, world)
   q, v, a = sample_states(m, count, first=first)
   eng = engine.InverseEngine(m, capacity=count, device=local)
   eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
@@ -95,24 +154,16 @@ def main():
   def step():
     eng.inverse(count, out=out, mirror_input=True)
 
+  def step_gather():
+    step()
+    parallel.gather_to_rank0(out, world, rank, counts)
+
   for _ in range(args.warmup):
     step()
-  torch.cuda.synchronize(dev)
-  if world > 1:
-    dist.barrier()
-  torch.cuda.synchronize(dev)
-  t0 = time.perf_counter()
-  for _ in range(args.steps):
-    step()
-  torch.cuda.synchronize(dev)
-  if world > 1:
-    dist.barrier()
-  torch.cuda.synchronize(dev)
-  elapsed = time.perf_counter() - t0
-  t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-  if world > 1:
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-  elapsed = float(t.item())
+  elapsed = timed(step, args.steps, world, dist, torch, dev)
+  # the same steps followed by the gather of every rank's qfrc_inverse to rank 0
+  step_gather()
+  elapsed_g = timed(step_gather, args.steps, world, dist, torch, dev)
 
   # kernel-only average launch time (HIP events on the context's stream) for the roofline
   kernel_ms = eng.time_kernel(count, reps=max(args.steps, 10))
@@ -121,25 +172,32 @@ def main():
   achieved = bytes_per_eval * count / (kernel_ms * 1e-3) / 1e9
   traffic, traffic_src = pmc_traffic(eng, args.model, count)
 
-  # after timing: rank 0 gathers every rank's qfrc_inverse checksum over RCCL
-  chk = out.sum(dim=0)
-  gathered = parallel.gather_to_rank0(chk, world, rank) if world > 1 else [chk]
-  checksum = float(sum(float(x.abs().sum()) for x in gathered)) if rank == 0 else None
+  # every rank's full qfrc_inverse on rank 0 (outside the timed regions): a checksum of
+  # checksums over the whole global batch, and a spot check of the gathered rows
+  gathered = parallel.gather_to_rank0(out, world, rank, counts)
+  torch.cuda.synchronize(dev)
+  checksum = None
+  if rank == 0:
+    full = torch.cat(gathered)
+    assert full.shape == (total, m.nv)
+    checksum = float(full.abs().sum(dim=1).sum())
 
   cpu = None
   if rank == 0 and world == 1 and not args.no_cpu:
     from oracle.oracle import Oracle
-    n = args.cpu_sample
+    nthread = args.cpu_threads or available_cores()
+    n = args.cpu_sample or 150_000 * nthread
     cq, cv, ca = sample_states(m, n, first=0)
     o = Oracle(m)
-    _, secs = o.inverse_batch(cq, cv, ca, nthread=args.cpu_threads)
-    cpu = {"value": n / secs, "unit": "evals/s", "cores": args.cpu_threads, "kind": "port",
+    _, secs = o.inverse_batch(cq, cv, ca, nthread=nthread)
+    cpu = {"value": n / secs, "unit": "evals/s", "cores": nthread, "kind": "port",
            "sample": f"{n} humanoid states (first {n} of the same sampler stream), "
-                     f"{args.cpu_threads} threads, oracle/mj_oracle.c -O2, "
-                     f"{secs:.2f} s wall"}
+                     f"{nthread} threads (cores available to the process: "
+                     f"{available_cores()}, os.cpu_count {os.cpu_count()}), "
+                     f"oracle/mj_oracle.c -O2, {secs:.2f} s wall"}
 
   if rank == 0:
-    value = world * count * args.steps / elapsed
+    value = total * args.steps / elapsed
     rec = {
         "metric": METRIC,
         "value": value,
@@ -149,17 +207,22 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic: config-2 sampler (seed 20250314), inputs resident in HBM",
         "config": {"workload": f"{args.model} 27-DoF mj_inverse (skipstage NONE), contacts "
                                f"disabled, nefc=0, full mjData mirror written",
-                   "per_gpu_batch": count, "global_batch": world * count,
+                   "per_gpu_batch": count, "global_batch": total,
                    "parallelism": f"dp{world}"},
+        "with_gather": {"value": total * args.steps / elapsed_g,
+                        "ms_per_step": elapsed_g / args.steps * 1e3,
+                        "bytes_to_rank0_per_step": 8 * m.nv * (total - counts[0]),
+                        "collective": "RCCL point-to-point sends of qfrc_inverse to rank 0"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
+                     "traffic_ratio": (traffic / (bytes_per_eval * count)) if traffic else None,
                      "algorithmic_bytes_per_launch": bytes_per_eval * count,
                      "kernel": ("+".join(codegen.hot_kernels(eng.fast_kernel))
                                 + "+k_constraint" if eng.fast_kernel else "k_inverse<0>"),
@@ -178,35 +241,36 @@ def other_config(args):
   """Throughput of configs 4 (contacts) and 5 (finite-difference Jacobians), 1 GPU."""
   import torch
   from mujoco_inversedynamicstest_amd import codegen, engine, models
-  from mujoco_inversedynamicstest_amd.sampler import sample_contact_states, sample_states
-  torch.cuda.set_device(0)
-  if args.config == 4:
-    m = models.load(args.model, disable_contact=False)
-    B = args.config_batch or 4096
-    q, v, a = sample_contact_states(m, B)
-    eng = engine.InverseEngine(m, capacity=B)
-    eng.upload_states(q, v, a)
-    for _ in range(args.warmup):
-      eng.inverse(B, mirror_input=True)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-      eng.inverse(B, mirror_input=True)
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / args.steps
-    ncon = eng.field_int("con_count", 0, B)[:, 0]
-    nefc = eng.field_int("efc_count", 0, B)[:, 0]
-    rec = {"metric": "mj_inverse evals/sec, config 4 (contacts on)", "value": B / dt,
-           "unit": "evals/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": dt * 1e3,
-           "dtype": "f64",
-           "kernel": (f"generated {'+'.join(codegen.hot_kernels(eng.fast_kernel))} + k_constraint"
-                      if eng.fast_kernel else "k_inverse<0, contacts> (generic)"),
-           "config": {"workload": f"{args.model} keyframe poses + noise, contacts on",
-                      "batch": B},
-           "ncon_hist": np.bincount(ncon).tolist(), "nefc_max": int(nefc.max()),
-           "nefc_mean": float(nefc.mean())}
-  else:
+  from mujoco_inversedynamicstest_amd.sampler import sample_contact_states
+  if args.config == 5:
     return config5(args)
+  torch.cuda.set_device(0)
+  m = models.load(args.model, disable_contact=False)
+  B = args.config_batch or 4096
+  q, v, a = sample_contact_states(m, B)
+  eng = engine.InverseEngine(m, capacity=B)
+  eng.upload_states(q, v, a)
+  for _ in range(args.warmup):
+    eng.inverse(B, mirror_input=True)
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(args.steps):
+    eng.inverse(B, mirror_input=True)
+  torch.cuda.synchronize()
+  dt = (time.perf_counter() - t0) / args.steps
+  kernel_ms = eng.time_kernel(B, reps=max(args.steps, 10))
+  ncon = eng.field_int("con_count", 0, B)[:, 0]
+  nefc = eng.field_int("efc_count", 0, B)[:, 0]
+  rec = {"metric": "mj_inverse evals/sec, config 4 (contacts on)", "value": B / dt,
+         "unit": "evals/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": dt * 1e3,
+         "kernel_ms": kernel_ms, "dtype": "f64",
+         "kernel": (f"generated {'+'.join(codegen.hot_kernels(eng.fast_kernel))} + "
+                    f"{getattr(eng, 'constraint_kernel', 'k_constraint')}" if eng.fast_kernel
+                    else "k_inverse<0, contacts> (generic)"),
+         "config": {"workload": f"{args.model} keyframe poses + noise, contacts on",
+                    "batch": B},
+         "ncon_hist": np.bincount(ncon).tolist(), "nefc_max": int(nefc.max()),
+         "nefc_mean": float(nefc.mean())}
   print(json.dumps(rec), flush=True)
   eng.close()
 
@@ -248,22 +312,7 @@ def config5(args):
 
   for _ in range(args.warmup):
     step()
-  torch.cuda.synchronize(dev)
-  if world > 1:
-    dist.barrier()
-  torch.cuda.synchronize(dev)
-  t0 = time.perf_counter()
-  for _ in range(args.steps):
-    step()
-  torch.cuda.synchronize(dev)
-  if world > 1:
-    dist.barrier()
-  torch.cuda.synchronize(dev)
-  elapsed = time.perf_counter() - t0
-  t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-  if world > 1:
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-  dt = float(t.item()) / args.steps
+  dt = timed(step, args.steps, world, dist, torch, dev) / args.steps
   # gather of the Jacobians to rank 0 (RCCL point-to-point), outside the timed region
   jac = torch.stack(out[:3])
   torch.cuda.synchronize(dev)

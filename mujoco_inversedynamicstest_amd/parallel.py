@@ -15,23 +15,35 @@ def shard(total: int, world: int, rank: int):
   return first, base + (1 if rank < rem else 0)
 
 
-def gather_to_rank0(tensor, world: int, rank: int):
-  """Gather equal-shaped tensors to rank 0 (RCCL on GPU tensors, gloo on CPU tensors).
+def shard_counts(total: int, world: int):
+  """Rows of every rank's shard (what rank 0 receives from each peer)."""
+  return [shard(total, world, r)[1] for r in range(world)]
 
-  Returns the list of gathered tensors on rank 0 and None elsewhere. Uses point-to-point
-  sends into rank 0 (RCCL has no native gather; each peer uses its own xGMI link).
+
+def gather_to_rank0(tensor, world: int, rank: int, counts=None):
+  """Gather every rank's tensor to rank 0 (RCCL on GPU tensors, gloo on CPU tensors).
+
+  Returns the list of gathered tensors on rank 0 (rank order) and None elsewhere. Uses
+  point-to-point sends into rank 0 (RCCL has no native gather; each peer uses its own xGMI
+  link). `counts` gives the leading dimension of each rank's tensor when shards are uneven
+  (shard_counts); by default every rank's tensor has this rank's shape.
   """
   import torch
   import torch.distributed as dist
   if world == 1:
     return [tensor]
   if rank == 0:
-    bufs = [tensor] + [torch.empty_like(tensor) for _ in range(world - 1)]
-    ops = [dist.P2POp(dist.irecv, bufs[r], r) for r in range(1, world)]
-    for req in dist.batch_isend_irecv(ops):
+    shape = list(tensor.shape)
+    bufs = [tensor]
+    for r in range(1, world):
+      if counts is not None:
+        shape[0] = counts[r]
+      bufs.append(torch.empty(shape, dtype=tensor.dtype, device=tensor.device))
+    ops = [dist.P2POp(dist.irecv, bufs[r], r) for r in range(1, world) if bufs[r].numel()]
+    for req in (dist.batch_isend_irecv(ops) if ops else []):
       req.wait()
     return bufs
-  req = dist.batch_isend_irecv([dist.P2POp(dist.isend, tensor, 0)])
-  for r in req:
-    r.wait()
+  if tensor.numel():
+    for r in dist.batch_isend_irecv([dist.P2POp(dist.isend, tensor, 0)]):
+      r.wait()
   return None

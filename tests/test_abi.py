@@ -67,9 +67,11 @@ def test_no_cpu_fallback_without_device(humanoid):
 
 
 def test_unsupported_model_rejected():
-  """Models with collidable geoms and contacts enabled are rejected (collision is next)."""
+  """A model outside the device subset (here: sparse constraint Jacobians, jacobian=sparse)
+  is rejected at context creation with MJHIP_ERR_MODEL, never run approximately."""
   if engine.lib().mjhip_deviceCount() == 0:
     pytest.skip("rejection happens after the device check")
   m = models.load("humanoid")
+  m.opt["jacobian"] = 1
   with pytest.raises(engine.MJHIPError, match="MODEL"):
     engine.InverseEngine(m, capacity=64)

@@ -343,7 +343,7 @@ def test_fast_vs_generic_and_worklist(humanoid, eng):
 
 @pytest.fixture(scope="module")
 def humanoid_contacts_eng(humanoid_contacts):
-  e = engine.InverseEngine(humanoid_contacts, capacity=1024)
+  e = engine.InverseEngine(humanoid_contacts, capacity=4096)
   yield e
   e.close()
 
@@ -359,7 +359,7 @@ def test_contacts_config4_parity(humanoid_contacts, humanoid_contacts_eng, gener
   from oracle.oracle import CON_DOUBLE, CON_INT
   m, e = humanoid_contacts, humanoid_contacts_eng
   assert e.fast_kernel == "humanoid_contact"
-  B = 1024
+  B = 4096                              # config 4's batch
   q, v, a = sample_contact_states(m, B)
   f, st = e.inverse(q, v, a, status=True, generic=generic)
   assert (st == 0).all()
@@ -725,3 +725,106 @@ def test_elliptic_cone_parity():
   assert_close(f, np.array(ref), "qfrc_inverse")
   assert nefc_g.sum() > 0
   e.close()
+
+
+@pytest.mark.parametrize("lanes", ["0", "8", "16"])
+def test_constraint_coop_lanes(humanoid_contacts, lanes, monkeypatch):
+  """The cooperative constraint kernel (G lanes per instance: collision pairs, rows and
+  J'force split over the group) against the one-lane kernel and the oracle, config-4 states
+  with limits and contacts: counts, row types/ids and contact pairs exact."""
+  from mujoco_inversedynamicstest_amd.sampler import sample_contact_states
+  m = humanoid_contacts
+  monkeypatch.setenv("MJHIP_COOP_LANES", lanes)
+  B = 2048
+  q, v, a = sample_contact_states(m, B, first=10000)
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    f, st = e.inverse(q, v, a, status=True)
+    ints = {n: e.field_int(n, 0, B) for n in ("con_count", "efc_count", "con_geom", "efc_type",
+                                              "efc_id", "efc_state", "con_efc_address")}
+    force = e.field("efc_force", 0, B)
+    qc = e.field("qfrc_constraint", 0, B)
+  finally:
+    e.close()
+  assert (st == 0).all()
+  o = Oracle(m)
+  ref, refc = [], []
+  for i in range(0, B, 4):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    refc.append(o.d.qfrc_constraint.copy())
+    ncon, nefc = o.efc.ncon, o.efc.nefc
+    assert ints["con_count"][i, 0] == ncon and ints["efc_count"][i, 0] == nefc
+    np.testing.assert_array_equal(ints["con_geom"][i][:2 * ncon],
+                                  o.contact_field("con_geom").ravel())
+    np.testing.assert_array_equal(ints["con_efc_address"][i][:ncon],
+                                  o.contact_field("con_efc_address"))
+    for n in ("efc_type", "efc_id", "efc_state"):
+      np.testing.assert_array_equal(ints[n][i][:nefc], o.efc_field(n))
+    fr = o.efc_field("efc_force")
+    assert np.abs(force[i][:nefc] - fr).max(initial=0) <= RTOL * max(1.0, np.abs(fr).max(initial=0))
+  assert_close(f[::4], np.array(ref), "qfrc_inverse")
+  assert_close(qc[::4], np.array(refc), "qfrc_constraint")
+  assert (ints["con_count"][:, 0] > 0).mean() > 0.5
+
+
+def _bad_inputs(m, B, first):
+  q, v, a = sample_states(m, B, first=first)
+  q[3, 5] = np.nan                      # BADQPOS (and a NaN pivot: INERTIA)
+  v[5, 2] = 2e10                        # BADQVEL
+  a[7, 0] = np.inf                      # BADQACC
+  a[9, 1] = -1e11
+  return q, v, a
+
+
+@pytest.mark.parametrize("generic", [False, True])
+def test_status_bits_bad_inputs(humanoid, eng, generic):
+  """mj_checkPos/Vel/Acc (engine_forward.c:53-102) and the INERTIA pivot test as per-instance
+  status bits, identical to the oracle's, on the straight-line and the generic kernels; good
+  instances stay at 0 and nothing aborts the batch."""
+  q, v, a = _bad_inputs(humanoid, 64, 50)
+  _, st = eng.inverse(q, v, a, status=True, generic=generic)
+  o = Oracle(humanoid)
+  ref = []
+  for i in range(64):
+    o.inverse(q[i], v[i], a[i])
+    ref.append(o.d.status)
+  np.testing.assert_array_equal(st, ref)
+  assert st[3] & 1 and st[3] & 8 and st[5] == 2 and st[7] == 4 and st[9] == 4
+  assert (np.delete(st, [3, 5, 7, 9]) == 0).all()
+
+
+def test_config3_full_batch_one_gpu(humanoid):
+  """Config 3's whole global batch (262,144 humanoid states) on one GPU: 8 contiguous
+  32,768-instance shards (one per rank of the 8-GPU run) equal the single batch bit for bit,
+  the affine-in-qacc identity holds at full size, and an oracle subsample matches."""
+  B, world = 262144, 8
+  from mujoco_inversedynamicstest_amd import parallel
+  q, v, a = sample_states(humanoid, B)
+  e = engine.InverseEngine(humanoid, capacity=B)
+  try:
+    f, st = e.inverse(q, v, a, status=True)
+    assert (st == 0).all()
+    for r in range(world):
+      first, count = parallel.shard(B, world, r)
+      fr = e.inverse(q[first:first + count], v[first:first + count], a[first:first + count])
+      np.testing.assert_array_equal(fr, f[first:first + count])
+    sub = np.arange(0, B, B // 1024)
+    f0 = e.inverse(q[sub], v[sub], np.zeros_like(a[sub]))
+    qM = e.field("qM", 0, len(sub))
+  finally:
+    e.close()
+  nv = humanoid.nv
+  Mx = np.zeros((len(sub), nv))
+  adr = 0
+  for i in range(nv):
+    j = i
+    while j >= 0:
+      Mx[:, i] += qM[:, adr] * a[sub, j]
+      if j != i:
+        Mx[:, j] += qM[:, adr] * a[sub, i]
+      j = humanoid.dof_parentid[j]
+      adr += 1
+  scale = np.maximum(1.0, np.abs(f[sub]).max(axis=1))
+  assert (np.abs((f[sub] - f0) - Mx).max(axis=1) / scale).max() < 1e-9
+  ref, _ = oracle_batch(humanoid, q[sub[:256]], v[sub[:256]], a[sub[:256]])
+  assert_close(f[sub[:256]], ref["qfrc_inverse"], "qfrc_inverse (config 3 subsample)")
