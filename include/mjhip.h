@@ -227,6 +227,20 @@ typedef struct mjhipData_ {
 #define XD(name, d0, d1, stage) mjtNum* name;
   MJHIP_DATA_SENSOR_AUX
 #undef XD
+  /* Constraint rows and contacts (MJHIP_DATA_EFC / MJHIP_DATA_CONTACT; the reference's
+   * d->efc_* arena arrays and d->contact): caller-owned buffers of efc_capacity rows and
+   * con_capacity contacts (capacity 0: none kept). A call with skipstage > NONE reads the rows
+   * and contacts of the stages it skips from here, as the reference reads the d->efc_* that
+   * the preceding mj_forward left (engine_inverse.c:169-192); every call writes back the rows
+   * its stages make, with the counts nefc/ne/nf/nl and ncon. */
+  int efc_capacity, ne, nf, nl;
+  int con_capacity, ncon;
+#define XE(type, name, w, stage) type* name;
+  MJHIP_DATA_EFC
+#undef XE
+#define XC(type, name, w, stage) type* name;
+  MJHIP_DATA_CONTACT
+#undef XC
 } mjhipData;
 
 /*---------------------------- status codes of the batch API ------------------------------*/

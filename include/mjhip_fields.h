@@ -303,4 +303,43 @@
   XD(cfrc_int,          nbody,   6,   6) \
   XD(cfrc_ext,          nbody,   6,   6)
 
+/* Constraint rows of one instance: the reference's efc_* arena arrays of the dense path
+ * (mjxmacro.h:707-732 MJDATA_ARENA_POINTERS_SOLVER; efc_J is nefc x nv, efc_KBIP nefc x 4).
+ * XE(type, name, width, stage): `width` elements per row; `stage` is the inverse stage that
+ * writes the field (1 mj_makeConstraint, 2 mj_referenceConstraint, 3 mj_invConstraint).
+ * The host data (mjhipData) holds caller-owned buffers of efc_capacity rows. */
+#define MJHIP_DATA_EFC \
+  XE(int,    efc_type,          1,        1) \
+  XE(int,    efc_id,            1,        1) \
+  XE(mjtNum, efc_J,             MJ_M(nv), 1) \
+  XE(mjtNum, efc_pos,           1,        1) \
+  XE(mjtNum, efc_margin,        1,        1) \
+  XE(mjtNum, efc_frictionloss,  1,        1) \
+  XE(mjtNum, efc_diagApprox,    1,        1) \
+  XE(mjtNum, efc_KBIP,          4,        1) \
+  XE(mjtNum, efc_D,             1,        1) \
+  XE(mjtNum, efc_R,             1,        1) \
+  XE(mjtNum, efc_vel,           1,        2) \
+  XE(mjtNum, efc_aref,          1,        2) \
+  XE(mjtNum, efc_force,         1,        3) \
+  XE(int,    efc_state,         1,        3)
+
+/* Contacts of one instance (mjContact, mjdata.h, the fields this path reads or writes) as
+ * parallel arrays of con_capacity entries: XC(type, name, width, stage) as above (stage 1
+ * mj_collision / mj_makeConstraint; con_mu is set by mj_makeImpedance). */
+#define MJHIP_DATA_CONTACT \
+  XC(mjtNum, con_dist,          1, 1) \
+  XC(mjtNum, con_pos,           3, 1) \
+  XC(mjtNum, con_frame,         9, 1) \
+  XC(mjtNum, con_includemargin, 1, 1) \
+  XC(mjtNum, con_friction,      5, 1) \
+  XC(mjtNum, con_solref,        2, 1) \
+  XC(mjtNum, con_solreffriction, 2, 1) \
+  XC(mjtNum, con_solimp,        5, 1) \
+  XC(mjtNum, con_mu,            1, 1) \
+  XC(int,    con_dim,           1, 1) \
+  XC(int,    con_geom,          2, 1) \
+  XC(int,    con_exclude,       1, 1) \
+  XC(int,    con_efc_address,   1, 1)
+
 #endif  /* MJHIP_FIELDS_H_ */

@@ -118,6 +118,7 @@ struct SP {
   XSC(jacr, 3*nv)                     \
   XSC(jacsc, mjh_needSliderCrank(m)*6*nv) /* slider-crank site Jacobians */ \
   XSC(qforce, nv)                     \
+  XSC(qfrc_tmp, nv)                   /* single-instance mj_rne / mj_xfrcAccumulate result */ \
   XSC(qacc_save, nv)                  \
   XSC(energy, 2)                      /* mjData energy (mjENBL_ENERGY) */ \
   XSC(time, (m->nsensor > 0))         /* mjData time (clock sensors) */ \
@@ -1014,11 +1015,13 @@ MJH_HD int filterSphere(const mjhipModel& m, const Lane<S>& d, int g1, int g2, d
 }
 
 // mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
-template <int S>
+// WRITE = false only counts the contacts the pair produces (the cooperative constraint
+// kernel's first pass: it needs each pair's count to place the contacts in order)
+template <int S, bool WRITE = true>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
                                double margin, int& ncon, int* status);
 
-template <int S>
+template <int S, bool WRITE = true>
 MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, int& ncon,
                          int* status) {
   if (m.geom_type[g1] > m.geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
@@ -1038,7 +1041,7 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
     return;
   }
   if (t1 == mjhipGEOM_PLANE && (t2 == mjhipGEOM_BOX || t2 == mjhipGEOM_CYLINDER)) {
-    collidePlaneBoxCyl(m, d, g1, g2, margin, ncon, status);
+    collidePlaneBoxCyl<S, WRITE>(m, d, g1, g2, margin, ncon, status);
     return;
   }
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
@@ -1060,6 +1063,10 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
     num = colCapsuleCapsule(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
   }
   if (!num) return;
+  if constexpr (!WRITE) {
+    ncon += num;
+    return;
+  }
   int condim;
   double gap, solref[2], solimp[5], friction[5];
   contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
@@ -1098,7 +1105,7 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
 }                                                // in registers
 
 // plane : box / cylinder (up to 4 contacts each): contacts are stored as they are made
-template <int S>
+template <int S, bool WRITE>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
                                double margin, int& ncon, int* status) {
   const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
@@ -1109,6 +1116,10 @@ MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, in
   double gap, solref[2], solimp[5], friction[5];
   contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
   auto store = [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
+    if constexpr (!WRITE) {
+      ncon++;
+      return true;
+    }
     int i = ncon;
     if (i >= d.con_cap) {
       *status |= MJHIP_INST_CNSTRFULL;
@@ -1599,15 +1610,18 @@ MJH_HD void crb(const mjhipModel& m, const Lane<S>& d) {
   }
 }
 
-// mj_factorM / mj_factorI :1470-1511
+// mj_factorM / mj_factorI :1470-1511. A pivot below mjMINVAL (or NaN) sets
+// MJHIP_INST_INERTIA, the condition mj_factorI_legacy reports as mjWARN_INERTIA (:1426-1430);
+// the factor itself is left as mj_factorI computes it (no clamping on this path)
 template <int S>
-MJH_HD void factorM(const mjhipModel& m, const Lane<S>& d) {
+MJH_HD void factorM(const mjhipModel& m, const Lane<S>& d, int* status = nullptr) {
   for (int i = 0; i < m.nC; i++) d.qLD[i] = d.qM[m.mapM2C[i]];
   SP<S> mat = d.qLD;
   const int *rownnz = m.C_rownnz, *rowadr = m.C_rowadr, *colind = m.C_colind;
   for (int k = m.nv-1; k >= 0; k--) {
     int rowadr_k = rowadr[k];
     int diag_k = rowadr_k + rownnz[k] - 1;
+    if (status && !(mat[diag_k] >= MINVAL)) *status |= MJHIP_INST_INERTIA;
     double invD = 1 / mat[diag_k];
     d.qLDiagInv[k] = invD;
     if (m.dof_simplenum[k]) continue;
@@ -2815,7 +2829,7 @@ MJH_HD void invPosition(const mjhipModel& m, const Lane<S>& d, int* status) {
   tendon(m, d);
   MJH_PHASE(2);
   crb(m, d);
-  factorM(m, d);
+  factorM(m, d, status);
   MJH_PHASE(3);
   if constexpr (CONTACT) collision(m, d, status);
   else d.con_count[0] = 0;
@@ -3675,12 +3689,31 @@ MJH_HD void sensorAcc(const mjhipModel& m, const Lane<S>& d) {
   applyCutoff(m, d, mjhipSTAGE_ACC);
 }
 
+// mju_isBad (engine_util_misc.c:1315-1317): NaN or |x| > mjMAXVAL
+MJH_HD bool isBad(double x) { return x != x || x > mjhipMAXVAL || x < -mjhipMAXVAL; }
+
+// mj_checkPos / mj_checkVel / mj_checkAcc (engine_forward.c:53-102) on the inputs a call
+// reads, as status bits: the batched analogue of their mjWARN_BADQPOS/QVEL/QACC warnings.
+// Nothing is reset (a batch never aborts) and no result changes.
+template <int S>
+MJH_HD int checkInputs(const mjhipModel& m, const Lane<S>& d, int skipstage) {
+  int st = 0;
+  if (skipstage < mjhipSTAGE_POS) {
+    for (int i = 0; i < m.nq; i++) st |= isBad(d.qpos[i]) ? MJHIP_INST_BADQPOS : 0;
+  }
+  if (skipstage < mjhipSTAGE_VEL) {
+    for (int i = 0; i < m.nv; i++) st |= isBad(d.qvel[i]) ? MJHIP_INST_BADQVEL : 0;
+  }
+  for (int i = 0; i < m.nv; i++) st |= isBad(d.qacc[i]) ? MJHIP_INST_BADQACC : 0;
+  return st;
+}
+
 // FUSED (the constraint rows finished at creation, see contactRowsFused) requires
 // skipstage = mjSTAGE_NONE, no mjENBL_INVDISCRETE, nbody <= 64 and d.chain set (fusedOk)
 template <int S, bool CONTACT = true, bool FUSED = false>
 MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage,
                        int skipsensor = 0) {
-  int status = 0;
+  int status = checkInputs(m, d, skipstage);
   const bool energy = (m.opt.enableflags & mjhipENBL_ENERGY) != 0;
   const bool sensors = !skipsensor && m.nsensor > 0;
   if (skipstage < mjhipSTAGE_POS) {
@@ -3798,8 +3831,10 @@ MJH_HD void xfrcAccumulate(const mjhipModel& m, const Lane<S>& d, SP<S> qfrc) {
 // MJHIP_INST_UNSUPPORTED and get qacc = qacc_smooth.
 template <int S, bool CONTACT = true>
 MJH_HD int forwardSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
-  int status = 0;
   const int nv = m.nv;
+  int status = 0;
+  for (int i = 0; i < m.nq; i++) status |= isBad(d.qpos[i]) ? MJHIP_INST_BADQPOS : 0;
+  for (int i = 0; i < nv; i++) status |= isBad(d.qvel[i]) ? MJHIP_INST_BADQVEL : 0;
   if (skipstage < mjhipSTAGE_POS) invPosition<S, CONTACT>(m, d, &status);
   if (skipstage < mjhipSTAGE_VEL) invVelocity(m, d);
   fwdActuation(m, d);
@@ -3811,6 +3846,7 @@ MJH_HD int forwardSkip(const mjhipModel& m, const Lane<S>& d, int skipstage) {
   solveM(m, d, d.qacc_smooth);
   copy(d.qacc, d.qacc_smooth, nv);
   zero(d.qfrc_constraint, nv);
+  for (int i = 0; i < nv; i++) status |= isBad(d.qacc[i]) ? MJHIP_INST_BADQACC : 0;
   if (d.efc_count[0] > 0) status |= MJHIP_INST_UNSUPPORTED;
   return status;
 }

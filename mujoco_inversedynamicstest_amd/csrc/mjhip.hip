@@ -15,9 +15,11 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <algorithm>
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <utility>
 #include <vector>
 
 #include "engine_device.h"
@@ -81,7 +83,7 @@ __global__ __launch_bounds__(64) void k_constraint(mjhipModel m, Mirror mr, int 
     d.chain = chain;
     MJHIP_GEOM_STAGE(CONTACT, FUSED)
     const int st = mjh::constraintOnly<64, CONTACT, FUSED>(m, d);
-    if (status) status[inst] = st;
+    if (status && st) status[inst] |= st;   // after the generated kernels' input checks
     if (qfrc_out) {        // a few scattered work-list instances
       for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
     }
@@ -95,7 +97,7 @@ __global__ __launch_bounds__(64) void k_constraint(mjhipModel m, Mirror mr, int 
     d.chain = chain;
     MJHIP_GEOM_STAGE(CONTACT, FUSED)
     const int st = mjh::constraintOnly<64, CONTACT, FUSED>(m, d);
-    if (status) status[g] = st;
+    if (status && st) status[g] |= st;
     for (int k = 0; k < m.nv; k++) qo[threadIdx.x*m.nv + k] = d.qfrc_inverse[k];
   }
   __syncthreads();
@@ -104,6 +106,237 @@ __global__ __launch_bounds__(64) void k_constraint(mjhipModel m, Mirror mr, int 
   for (long r = threadIdx.x; r < rows*m.nv; r += 64) dst[r] = qo[r];
 }
 
+
+// Cooperative constraint part (the fused path of k_constraint, G lanes per instance).
+//
+// One wave holds 64/G instances; the G lanes of an instance's group split its work:
+//   collision   the model's static geom-pair program (collisionPairs, host-built in the order
+//               the serial mj_collision emits contacts), G pairs per round: each lane counts
+//               its pair's contacts, a group prefix sum places them, the lane writes them
+//   rows        equality (lane 0), then friction and limit rows: every lane evaluates the
+//               predicates (so all agree on the row numbers), the owner of row r (r % G)
+//               writes and finishes it; contact rows: contact c belongs to lane c % G, a
+//               prefix sum over the contacts' row counts gives each its first row
+//   J'force     column-parallel (column j on lane j % G): each column's sum runs over the
+//               rows in order, as mju_mulMatTVec's, then the mj_inverse assembly
+// Every output equals the serial (one lane per instance) fused path's.
+template <int G>
+__device__ __forceinline__ int groupScan(int x, int sub, int* total) {
+  for (int o = 1; o < G; o <<= 1) {
+    const int y = __shfl_up(x, o, G);
+    if (sub >= o) x += y;
+  }
+  *total = __shfl(x, G - 1, G);
+  return x;                               // inclusive
+}
+
+template <int S>
+__device__ __forceinline__ void rowFields(const Lane<S>& d, int r, double pos, double margin,
+                                          double frictionloss, int type, int id) {
+  d.efc_pos[r] = pos;
+  d.efc_margin[r] = margin;
+  d.efc_frictionloss[r] = frictionloss;
+  d.efc_type[r] = type;
+  d.efc_id[r] = id;
+}
+
+template <int G, bool CONTACT, bool LIST>
+__global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr, int B,
+                                                        const int* __restrict__ worklist,
+                                                        const int* __restrict__ count,
+                                                        const int2* __restrict__ pairs,
+                                                        int npair,
+                                                        double* __restrict__ qfrc_out,
+                                                        int* __restrict__ status) {
+  constexpr int IPB = 64 / G;               // instances per wave
+  const long n = LIST ? (long)*count : (long)B;
+  if ((long)blockIdx.x*IPB >= n) return;    // whole block idle (uniform): before the barriers
+  __shared__ unsigned long long chain[64];
+  if ((int)threadIdx.x < m.nbody) chain[threadIdx.x] = mjh::chainMask(m, threadIdx.x);
+  __syncthreads();
+  const int sub = threadIdx.x % G;
+  const long g = (long)blockIdx.x*IPB + threadIdx.x / G;
+  const bool active = g < n;                // uniform within a group
+  const long inst = active ? (LIST ? (long)worklist[g] : g) : 0;
+  Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
+  d.chain = chain;
+  const int nv = m.nv, dsbl = m.opt.disableflags;
+  int st = 0, ncon = 0;
+
+  // ---- mj_collision over the static pair program
+  if (CONTACT && active && mjhip_contactsEnabled(&m)) {
+    for (int p0 = 0; p0 < npair; p0 += G) {
+      const int p = p0 + sub;
+      int2 pr = make_int2(0, 0);
+      int cnt = 0;
+      if (p < npair) {
+        pr = pairs[p];
+        mjh::collideGeoms<64, false>(m, d, pr.x, pr.y, cnt, &st);
+      }
+      int total;
+      const int excl = groupScan<G>(cnt, sub, &total) - cnt;
+      if (cnt) {
+        int c = ncon + excl;
+        mjh::collideGeoms<64, true>(m, d, pr.x, pr.y, c, &st);
+      }
+      ncon += total;
+    }
+  }
+  if (active && sub == 0) d.con_count[0] = ncon < d.con_cap ? ncon : d.con_cap;
+  if (ncon > d.con_cap) ncon = d.con_cap;
+  __syncthreads();                          // contacts visible to every lane of the group
+
+  // ---- mj_makeConstraint: non-contact rows, then contact rows (all finished at creation)
+  mjh::RowCount rc;
+  if (active && !(dsbl & mjhipDSBL_CONSTRAINT)) {
+    if (m.neq) {
+      if (sub == 0) mjh::instantiateEquality<64, true>(m, d, rc, &st);
+      rc.nefc = __shfl(rc.nefc, 0, G);
+      rc.ne = __shfl(rc.ne, 0, G);
+    }
+    // a non-contact row r: the owner writes J (jval(k) for column k) and finishes it
+    auto addRow = [&](auto jval, double pos, double margin, double floss, int tp, int id)
+        MJH_LAMBDA_INLINE {
+      const int r = rc.nefc;
+      if (r + 1 > d.efc_cap) {
+        st |= MJHIP_INST_CNSTRFULL;
+        return false;
+      }
+      if (r % G == sub) {
+        mjh::SP<64> J = d.efc_J + (long)r*nv;
+        for (int k = 0; k < nv; k++) J[k] = jval(k);
+        rowFields(d, r, pos, margin, floss, tp, id);
+        mjh::finishNonContact(m, d, r, tp, id, pos, margin, floss);
+      }
+      rc.nefc++;
+      return true;
+    };
+    if (!(dsbl & mjhipDSBL_FRICTIONLOSS)) {
+      for (int i = 0; i < nv; i++) {
+        const double fl = m.dof_frictionloss[i];
+        if (fl > 0 && addRow([&](int k) { return k == i ? 1.0 : 0.0; }, 0, 0, fl,
+                             mjh::CNSTR_FRICTION_DOF, i)) {
+          rc.nf++;
+        }
+      }
+    }
+    if (!(dsbl & mjhipDSBL_LIMIT)) {
+      for (int i = 0; i < m.njnt; i++) {
+        if (!m.jnt_limited[i]) continue;
+        const double margin = m.jnt_margin[i];
+        const int t = m.jnt_type[i], da = m.jnt_dofadr[i];
+        if (t == mjhipJNT_SLIDE || t == mjhipJNT_HINGE) {
+          const double value = d.qpos[m.jnt_qposadr[i]];
+          for (int side = -1; side <= 1; side += 2) {
+            const double dist = side * (m.jnt_range[2*i+(side+1)/2] - value);
+            if (dist < margin &&
+                addRow([&](int k) { return k == da ? -(double)side : 0.0; }, dist, margin, 0,
+                       mjh::CNSTR_LIMIT_JOINT, i)) {
+              rc.nl++;
+            }
+          }
+        } else if (t == mjhipJNT_BALL) {
+          const int adr = m.jnt_qposadr[i];
+          double quat[4] = {d.qpos[adr], d.qpos[adr+1], d.qpos[adr+2], d.qpos[adr+3]};
+          double aa[3];
+          mjh::normalize4(quat);
+          mjh::quat2Vel(aa, quat, 1);
+          const double value = mjh::normalize3(aa);
+          const double dist = mjh::dmax(m.jnt_range[2*i], m.jnt_range[2*i+1]) - value;
+          const bool nonempty = aa[0] != 0 || aa[1] != 0 || aa[2] != 0;
+          if (dist < margin && nonempty &&
+              addRow([&](int k) { return (k >= da && k < da + 3) ? aa[k-da]*-1 : 0.0; },
+                     dist, margin, 0, mjh::CNSTR_LIMIT_JOINT, i)) {
+            rc.nl++;
+          }
+        }
+      }
+      for (int i = 0; i < m.ntendon; i++) {
+        if (!m.tendon_limited[i]) continue;
+        const double value = d.ten_length[i], margin = m.tendon_margin[i];
+        mjh::SP<64> tj = d.ten_J + (long)i*nv;
+        bool nonempty = false;
+        for (int k = 0; k < nv && !nonempty; k++) nonempty = tj[k] != 0;
+        for (int side = -1; side <= 1; side += 2) {
+          const double dist = side * (m.tendon_range[2*i+(side+1)/2] - value);
+          if (dist < margin && nonempty &&
+              addRow([&](int k) { return tj[k]*(double)(-side); }, dist, margin, 0,
+                     mjh::CNSTR_LIMIT_TENDON, i)) {
+            rc.nl++;
+          }
+        }
+      }
+    }
+    // contact rows (pyramidal or frictionless: the fused path excludes elliptic cones)
+    if (CONTACT && !(dsbl & mjhipDSBL_CONTACT) && nv) {
+      int nef = rc.nefc;
+      for (int c0 = 0; c0 < ncon; c0 += G) {
+        const int c = c0 + sub;
+        int rows = 0, dim = 0;
+        if (c < ncon && !d.con_exclude[c]) {
+          dim = d.con_dim[c];
+          rows = dim == 1 ? 1 : 2*(dim - 1);
+        }
+        int total;
+        const int off = nef + groupScan<G>(rows, sub, &total) - rows;
+        if (rows) {
+          if (off + rows > d.efc_cap) {     // mjWARN_CNSTRFULL analogue (capacity is exact)
+            st |= MJHIP_INST_CNSTRFULL;
+          } else {
+            d.con_efc_address[c] = off;
+            switch (dim) {
+              case 1: mjh::contactRowsFused<64, 1>(m, d, c, off); break;
+              case 3: mjh::contactRowsFused<64, 3>(m, d, c, off); break;
+              case 4: mjh::contactRowsFused<64, 4>(m, d, c, off); break;
+              default: mjh::contactRowsFused<64, 6>(m, d, c, off); break;
+            }
+          }
+        }
+        nef += total;
+      }
+      rc.nefc = nef < d.efc_cap ? nef : d.efc_cap;
+    }
+  }
+  if (active && sub == 0) {
+    d.efc_count[0] = rc.nefc; d.efc_count[1] = rc.ne; d.efc_count[2] = rc.nf;
+    d.efc_count[3] = rc.nl;
+  }
+  __syncthreads();                          // rows and forces visible to every lane
+
+  // ---- qfrc_constraint = J'force (column-parallel) and the mj_inverse assembly
+  if (active) {
+    const int nefc = rc.nefc;
+    for (int j = sub; j < nv; j += G) {
+      double acc = 0;
+      for (int r = 0; r < nefc; r++) {
+        const double f = d.efc_force[r];
+        if (f) acc += d.efc_J[(long)r*nv + j]*f;
+      }
+      d.qfrc_constraint[j] = acc;
+      d.qfrc_inverse[j] += m.dof_armature[j] * d.qacc[j] - d.qfrc_passive[j] - acc;
+      if (qfrc_out) qfrc_out[inst*nv + j] = d.qfrc_inverse[j];
+    }
+    for (int o = G/2; o; o >>= 1) st |= __shfl_xor(st, o, G);
+    if (sub == 0 && status && st) status[inst] |= st;
+  }
+}
+
+// Status checks of the straight-line path: mj_checkPos/Vel/Acc (engine_forward.c:53-102)
+// on the inputs and the pivot test behind MJHIP_INST_INERTIA on qLD's diagonal, ORed into
+// the status words the generated kernels and k_constraint wrote. A separate launch, run
+// only when statuses are asked for: inside the generated kernels the extra live values
+// cost spills (tools/kernel_resources.py).
+__global__ __launch_bounds__(64) void k_check(mjhipModel m, Mirror mr, int B,
+                                              int* __restrict__ status) {
+  const long inst = (long)blockIdx.x*64 + threadIdx.x;
+  if (inst >= B) return;
+  Lane<64> d = lane_view(mr, blockIdx.x, threadIdx.x);
+  int st = mjh::checkInputs(m, d, mjhipSTAGE_NONE);
+  for (int k = 0; k < m.nv; k++) {
+    if (!(d.qLD[m.C_rowadr[k] + m.C_rownnz[k] - 1] >= mjh::MINVAL)) st |= MJHIP_INST_INERTIA;
+  }
+  if (st) status[inst] |= st;
+}
 
 // Fused mj_inverseSkip over a batch. Optional row-major (instance-major) inputs are copied
 // into the mirror first; optional row-major qfrc_inverse output is written at the end.
@@ -160,7 +393,7 @@ __global__ void k_from_mirror(const double* __restrict__ src, double* __restrict
 // integrated along e_i by eps). Instances are base-major: inst = b*(3nv+1) + p.
 __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __restrict__ qpos,
                             const double* __restrict__ qvel, const double* __restrict__ qacc,
-                            double eps, int devptr_rowmajor) {
+                            const double* __restrict__ ctrl, double eps) {
   const int P = 3*m.nv + 1;
   long inst = (long)blockIdx.x*blockDim.x + threadIdx.x;
   if (inst >= (long)nbase*P) return;
@@ -170,7 +403,9 @@ __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __
   for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos[b*m.nq + k];
   for (int k = 0; k < m.nv; k++) d.qvel[k] = qvel[b*m.nv + k];
   for (int k = 0; k < m.nv; k++) d.qacc[k] = qacc[b*m.nv + k];
-  (void)devptr_rowmajor;
+  if (ctrl) {                          // flg_actuation: the base state's controls
+    for (int k = 0; k < m.nu; k++) d.ctrl[k] = ctrl[b*m.nu + k];
+  }
   int nv = m.nv;
   if (p >= 1 && p <= nv) {
     d.qacc[p-1] = d.qacc[p-1] + eps;
@@ -204,7 +439,16 @@ __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __
 // mj_inverseSkip(mjSTAGE_VEL), so only acceleration-stage sensors change and the others keep
 // the centre's values (their difference is exactly 0); a qvel perturbation runs
 // mjSTAGE_POS, so position-stage sensors keep theirs (engine_derivative_fd.c:646-699).
-__global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps,
+// flg_actuation (inverseSkip, engine_derivative_fd.c:160-168): every evaluation's force is
+// qfrc_inverse - qfrc_actuator, with mj_fwdActuation run after the inverse (k_fd_act)
+__global__ void k_fd_act(mjhipModel m, Mirror mr, long ninst) {
+  const long inst = (long)blockIdx.x*blockDim.x + threadIdx.x;
+  if (inst >= ninst) return;
+  Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
+  mjh::fwdActuation(m, d);
+}
+
+__global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps, int flg_actuation,
                           double* __restrict__ DfDq, double* __restrict__ DfDv,
                           double* __restrict__ DfDa, double* __restrict__ DsDq,
                           double* __restrict__ DsDv, double* __restrict__ DsDa,
@@ -229,7 +473,12 @@ __global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps,
   }
   if (out) {
     for (int k = 0; k < nv; k++) {
-      out[(b*nv + i)*nv + k] = inv_h * (q.qfrc_inverse[k] - c.qfrc_inverse[k]);
+      double fq = q.qfrc_inverse[k], fc = c.qfrc_inverse[k];
+      if (flg_actuation) {
+        fq -= q.qfrc_actuator[k];
+        fc -= c.qfrc_actuator[k];
+      }
+      out[(b*nv + i)*nv + k] = inv_h * (fq - fc);
     }
   }
   if (sout) {
@@ -327,7 +576,52 @@ struct mjhipContext_ {
   int* worklist = nullptr;                 // capacity + 2 ints: [count0, count1, list...]
   int wl_parity = 0;                       // counter the next fast launch uses
   int wl_last = 0;                         // counter the last fast launch used
+  int2* pairs = nullptr;                   // static geom-pair program (collisionPairs)
+  int npair = 0;
+  int coop = 16;                           // lanes per instance of k_constraint_coop (0: off)
 };
+
+// The static geom-pair program of mj_collision (engine_collision_driver.c:265-497) for the
+// cooperative constraint kernel: candidate body pairs in signature order (mjhip_contact.h),
+// their geoms all-to-all, minus the pairs no run can collide (no collision function, geom
+// bitmask); a body pair the midphase handles (a body with more than one geom) has its geom
+// pairs stably sorted by contactcompare's key (:227-257), the type-ordered geom ids. Every
+// contact of a pair carries that key, so this is the order the serial collision() leaves
+// its contacts in, and the cooperative kernel concatenates the pairs' contacts in it.
+static std::vector<int2> collision_pairs(const mjhipModel* m) {
+  std::vector<int2> out;
+  if (!mjhip_contactsEnabled(m)) return out;
+  const bool midphase = !(m->opt.disableflags & mjhipDSBL_MIDPHASE);
+  auto key = [&](int2 p) {
+    return m->geom_type[p.x] > m->geom_type[p.y] ? std::make_pair(p.y, p.x)
+                                                 : std::make_pair(p.x, p.y);
+  };
+  for (int b1 = 0; b1 < m->nbody; b1++) {
+    for (int b2 = b1 + 1; b2 < m->nbody; b2++) {
+      if (!mjhip_bodyPairCandidate(m, b1, b2)) continue;
+      const int n1 = m->body_geomnum[b1], n2 = m->body_geomnum[b2];
+      std::vector<int2> list;
+      for (int i = 0; i < n1; i++) {
+        for (int j = 0; j < n2; j++) {
+          const int g1 = m->body_geomadr[b1] + i, g2 = m->body_geomadr[b2] + j;
+          const std::pair<int, int> k = key(make_int2(g1, g2));
+          if (!mjhip_pairMaxContacts(m->geom_type[k.first], m->geom_type[k.second])) continue;
+          if (mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
+                                  m->geom_contype[g2], m->geom_conaffinity[g2])) {
+            continue;
+          }
+          list.push_back(make_int2(g1, g2));
+        }
+      }
+      if (midphase && !(n1 == 1 && n2 == 1)) {
+        std::stable_sort(list.begin(), list.end(),
+                         [&](int2 a, int2 b) { return key(a) < key(b); });
+      }
+      out.insert(out.end(), list.begin(), list.end());
+    }
+  }
+  return out;
+}
 
 // FNV-1a 64 over sizes, options and every model array (= fields.model_signature in Python)
 static unsigned long long model_signature(const mjhipModel* m) {
@@ -553,17 +847,21 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
 #undef MJ_M
+  // every failure below releases the partial context through mjhip_contextFree
+  auto fail = [&](const char* what) {
+    set_error("%s failed", what);
+    mjhip_contextFree(c);
+    return MJHIP_ERR_HIP;
+  };
   // staging: row-major qpos, qvel, qacc, qfrc for `capacity` instances
   c->stage_bytes = sizeof(double) * (size_t)c->capacity * (m->nq + 3*(size_t)m->nv + m->nu);
   if (hipMalloc((void**)&c->stage, c->stage_bytes) != hipSuccess ||
       hipMalloc((void**)&c->status, sizeof(int) * (size_t)c->capacity) != hipSuccess) {
-    set_error("hipMalloc(staging) failed");
-    return MJHIP_ERR_HIP;
+    return fail("hipMalloc(staging)");
   }
   if (hipMalloc((void**)&c->worklist, sizeof(int) * ((size_t)c->capacity + 2)) != hipSuccess ||
       hipMemset(c->worklist, 0, 2 * sizeof(int)) != hipSuccess) {
-    set_error("hipMalloc(worklist) failed");
-    return MJHIP_ERR_HIP;
+    return fail("hipMalloc(worklist)");
   }
   const char* nofast = getenv("MJHIP_DISABLE_FAST");
   if (!(nofast && nofast[0] == '1')) {
@@ -572,10 +870,30 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
       if (e->sig == sig) c->fast = e;
     }
   }
-  HIPCHECK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+  // the cooperative constraint kernel's pair program (lanes per instance: MJHIP_COOP_LANES =
+  // 8 or 16, 0 = the one-lane k_constraint)
+  if (const char* lanes = getenv("MJHIP_COOP_LANES")) {
+    const int v = atoi(lanes);
+    c->coop = (v == 0 || v == 8 || v == 16) ? v : 16;
+  }
+  if (c->con_cap > 0) {
+    std::vector<int2> pairs = collision_pairs(m);
+    c->npair = (int)pairs.size();
+    if (c->npair) {
+      if (hipMalloc((void**)&c->pairs, sizeof(int2) * pairs.size()) != hipSuccess ||
+          hipMemcpy(c->pairs, pairs.data(), sizeof(int2) * pairs.size(),
+                    hipMemcpyHostToDevice) != hipSuccess) {
+        return fail("pair program upload");
+      }
+    }
+  }
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    return fail("hipStreamCreate");
+  }
   c->own_stream = true;
-  HIPCHECK(hipEventCreate(&c->ev0));
-  HIPCHECK(hipEventCreate(&c->ev1));
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess) {
+    return fail("hipEventCreate");
+  }
   *out = c;
   return MJHIP_OK;
 }
@@ -590,6 +908,7 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->stage);
   hipFree(c->status);
   hipFree(c->worklist);
+  hipFree(c->pairs);
   hipFree(c->mirror_buf);
   hipFree(c->dmodel_buf);
   delete c;
@@ -637,6 +956,25 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     // the fast path excludes INVDISCRETE: the constraint kernel is fused whenever nbody allows
     const bool fused = mjh::fusedOk(c->dmodel, mjhipSTAGE_NONE);
     const int* wl = c->worklist + 2;
+    if (fused && c->coop && c->fast->cmode) {   // cooperative lanes per instance
+      const bool contact = c->con_cap > 0, list = c->fast->cmode == 1;
+#define MJHIP_LAUNCH_COOP(G, C, L)                                                            \
+      hipLaunchKernelGGL((k_constraint_coop<G, C, L>), dim3((B + 64/G - 1) / (64/G)),         \
+                         dim3(64), 0, c->stream, c->dmodel, c->mirror, B, wl,                 \
+                         (const int*)cnt, c->pairs, c->npair, qfrc, status)
+      if (c->coop == 8) {
+        if (contact) { if (list) MJHIP_LAUNCH_COOP(8, true, true);
+                       else MJHIP_LAUNCH_COOP(8, true, false); }
+        else { if (list) MJHIP_LAUNCH_COOP(8, false, true);
+               else MJHIP_LAUNCH_COOP(8, false, false); }
+      } else {
+        if (contact) { if (list) MJHIP_LAUNCH_COOP(16, true, true);
+                       else MJHIP_LAUNCH_COOP(16, true, false); }
+        else { if (list) MJHIP_LAUNCH_COOP(16, false, true);
+               else MJHIP_LAUNCH_COOP(16, false, false); }
+      }
+#undef MJHIP_LAUNCH_COOP
+    } else {
 #define MJHIP_LAUNCH_CON(C, F, L)                                                             \
     hipLaunchKernelGGL((k_constraint<C, F, L>), grid, block,                                  \
                        ((C && F) ? mjh::gstageBytes(c->dmodel) : 0) +                         \
@@ -653,7 +991,12 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
       if (fused) MJHIP_LAUNCH_CON(false, true, true); else MJHIP_LAUNCH_CON(false, false, true);
     }
 #undef MJHIP_LAUNCH_CON
+    }
     HIPCHECK(hipGetLastError());
+    if (status) {
+      hipLaunchKernelGGL(k_check, grid, block, 0, c->stream, c->dmodel, c->mirror, B, status);
+      HIPCHECK(hipGetLastError());
+    }
     c->wl_last = c->wl_parity;
     c->wl_parity ^= 1;
     return MJHIP_OK;
@@ -732,14 +1075,18 @@ MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B, const mjtNum* qpos,
     }
   }
   if (qfrc_inverse) dqfrc = dev ? qfrc_inverse : sf;
-  int rc = launch_inverse(c, B, dq, dv, da, dqfrc, skipstage, c->status, flags, skipsensor);
+  // per-instance statuses only when the caller can see them (status array, or the host path's
+  // return code): a device-pointer call without them skips the input checks entirely
+  const bool want_status = status || !dev;
+  int rc = launch_inverse(c, B, dq, dv, da, dqfrc, skipstage, want_status ? c->status : nullptr,
+                          flags, skipsensor);
   if (rc) return rc;
   if (qfrc_inverse && !dev) {
     HIPCHECK(hipMemcpyAsync(qfrc_inverse, sf, sizeof(double)*(size_t)B*m.nv,
                             hipMemcpyDeviceToHost, c->stream));
   }
   int anybad = 0;
-  if (status || !dev) {
+  if (want_status) {
     std::vector<int> st(B);
     HIPCHECK(hipMemcpyAsync(st.data(), c->status, sizeof(int)*(size_t)B, hipMemcpyDeviceToHost,
                             c->stream));
@@ -956,17 +1303,44 @@ MJHIP_API int mjhip_timeInverseKernel(mjhipContext* c, int B, int reps, int skip
   return MJHIP_OK;
 }
 
-MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
-                                   const mjtNum* qvel, const mjtNum* qacc, mjtNum eps,
-                                   mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq,
-                                   mjtNum* DsDv, mjtNum* DsDa, mjtNum* DmDq, int flags) {
-  if (!c || B <= 0 || !qpos || !qvel || !qacc) return MJHIP_ERR_ARG;
+// actuator subset of the device mj_fwdActuation (mjh::fwdActuation): fixed/affine gain,
+// none/affine bias, no activation dynamics
+static const char* actuation_unsupported(const mjhipModel& m) {
+  for (int i = 0; i < m.nu; i++) {
+    if ((m.actuator_gaintype[i] != mjhipGAIN_FIXED && m.actuator_gaintype[i] != mjhipGAIN_AFFINE) ||
+        (m.actuator_biastype[i] != mjhipBIAS_NONE && m.actuator_biastype[i] != mjhipBIAS_AFFINE) ||
+        m.actuator_dyntype[i] != mjhipDYN_NONE) {
+      return "muscle/user gain or bias, or actuator dynamics (act)";
+    }
+  }
+  return nullptr;
+}
+
+MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
+                                     const mjtNum* qvel, const mjtNum* qacc, const mjtNum* ctrl,
+                                     mjtNum eps, int flg_actuation, mjtNum* DfDq, mjtNum* DfDv,
+                                     mjtNum* DfDa, mjtNum* DsDq, mjtNum* DsDv, mjtNum* DsDa,
+                                     mjtNum* DmDq, int flags) {
+  if (!c || B <= 0 || !qpos || !qvel || !qacc || (flg_actuation && c->hmodel.nu && !ctrl)) {
+    set_error("mjhip_inverseFDBatch: bad argument");
+    return MJHIP_ERR_ARG;
+  }
   const mjhipModel& m = c->hmodel;
   const int nv = m.nv, P = 3*nv + 1;
+  if (m.opt.integrator == mjhipINT_RK4) {       // engine_derivative_fd.c:619-621
+    set_error("mjd_inverseFD: RK4 integrator is not supported");
+    return MJHIP_ERR_MODEL;
+  }
   if (m.nmocap) {
     set_error("mjhip_inverseFDBatch: mocap poses per base state are not an input of the "
               "batched FD API");
     return MJHIP_ERR_MODEL;
+  }
+  if (flg_actuation) {
+    if (const char* why = actuation_unsupported(m)) {
+      set_error("mjhip_inverseFDBatch(flg_actuation): %s is not supported", why);
+      return MJHIP_ERR_MODEL;
+    }
   }
   if ((long)B*P > c->capacity) {
     set_error("FD batch needs %ld instances, context capacity %d", (long)B*P, c->capacity);
@@ -974,11 +1348,19 @@ MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
   }
   HIPCHECK(hipSetDevice(c->device));
   const bool dev = flags & MJHIP_FLAG_DEVICE_PTRS;
-  const double *dq = qpos, *dv = qvel, *da = qacc;
-  double* sq = c->stage;
-  double* sv = sq + (size_t)c->capacity*m.nq;
-  double* sa = sv + (size_t)c->capacity*m.nv;
+  const double *dq = qpos, *dv = qvel, *da = qacc, *dc = flg_actuation ? ctrl : nullptr;
+  std::vector<double*> tmp;
+  auto release = [&]() { for (double* p : tmp) hipFree(p); };
+  auto alloc = [&](size_t n) -> double* {
+    double* d = nullptr;
+    if (hipMalloc((void**)&d, (n ? n : 1)*sizeof(double)) != hipSuccess) return nullptr;
+    tmp.push_back(d);
+    return d;
+  };
   if (!dev) {
+    double* sq = c->stage;
+    double* sv = sq + (size_t)c->capacity*m.nq;
+    double* sa = sv + (size_t)c->capacity*m.nv;
     HIPCHECK(hipMemcpyAsync(sq, qpos, sizeof(double)*(size_t)B*m.nq, hipMemcpyHostToDevice,
                             c->stream));
     HIPCHECK(hipMemcpyAsync(sv, qvel, sizeof(double)*(size_t)B*nv, hipMemcpyHostToDevice,
@@ -986,10 +1368,21 @@ MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
     HIPCHECK(hipMemcpyAsync(sa, qacc, sizeof(double)*(size_t)B*nv, hipMemcpyHostToDevice,
                             c->stream));
     dq = sq; dv = sv; da = sa;
+    if (dc && m.nu) {
+      double* sc = alloc((size_t)B*m.nu);
+      if (!sc) { set_error("hipMalloc(ctrl) failed"); return MJHIP_ERR_HIP; }
+      if (hipMemcpyAsync(sc, ctrl, sizeof(double)*(size_t)B*m.nu, hipMemcpyHostToDevice,
+                         c->stream) != hipSuccess) {
+        release();
+        set_error("ctrl upload failed");
+        return MJHIP_ERR_HIP;
+      }
+      dc = sc;
+    }
   }
   long ninst = (long)B*P;
   hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream, c->dmodel,
-                     c->mirror, B, dq, dv, da, eps, 0);
+                     c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps);
   HIPCHECK(hipGetLastError());
   // all perturbations run the full pipeline (the reference's stage skipping is an
   // optimisation of a serial loop; results are identical because skipped stages see
@@ -998,38 +1391,65 @@ MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
   const int skipsensor = !DsDq && !DsDv && !DsDa;
   int rc = launch_inverse(c, (int)ninst, nullptr, nullptr, nullptr, nullptr, mjhipSTAGE_NONE,
                           nullptr, 0, skipsensor);
-  if (rc) return rc;
+  if (rc) { release(); return rc; }
+  if (flg_actuation) {
+    hipLaunchKernelGGL(k_fd_act, dim3((ninst + 255)/256), dim3(256), 0, c->stream, c->dmodel,
+                       c->mirror, ninst);
+    HIPCHECK(hipGetLastError());
+  }
   double *oq = DfDq, *ov = DfDv, *oa = DfDa, *om = DmDq;
   double *sq_ = DsDq, *sv_ = DsDv, *sa_ = DsDa;
-  std::vector<double*> tmp;
   size_t nn = (size_t)B*nv*nv, nm = (size_t)B*nv*m.nM, ns = (size_t)B*nv*m.nsensordata;
   if (!dev) {
-    auto alloc = [&](double* h, size_t n) -> double* {
+    bool ok = true;
+    auto dalloc = [&](double* h, size_t n) -> double* {
       if (!h) return nullptr;
-      double* d = nullptr;
-      if (hipMalloc((void**)&d, n*sizeof(double)) != hipSuccess) return nullptr;
-      tmp.push_back(d);
+      double* d = alloc(n);
+      ok = ok && d;
       return d;
     };
-    oq = alloc(DfDq, nn); ov = alloc(DfDv, nn); oa = alloc(DfDa, nn); om = alloc(DmDq, nm);
-    sq_ = alloc(DsDq, ns); sv_ = alloc(DsDv, ns); sa_ = alloc(DsDa, ns);
+    oq = dalloc(DfDq, nn); ov = dalloc(DfDv, nn); oa = dalloc(DfDa, nn); om = dalloc(DmDq, nm);
+    sq_ = dalloc(DsDq, ns); sv_ = dalloc(DsDv, ns); sa_ = dalloc(DsDa, ns);
+    if (!ok) {
+      release();
+      set_error("hipMalloc(FD outputs) failed");
+      return MJHIP_ERR_HIP;
+    }
   }
   long nd = (long)B*(P-1);
   hipLaunchKernelGGL(k_fd_diff, dim3((nd + 255)/256), dim3(256), 0, c->stream, c->dmodel,
-                     c->mirror, B, eps, oq, ov, oa, sq_, sv_, sa_, om);
-  HIPCHECK(hipGetLastError());
+                     c->mirror, B, eps, flg_actuation, oq, ov, oa, sq_, sv_, sa_, om);
+  if (hipGetLastError() != hipSuccess) {
+    release();
+    set_error("k_fd_diff launch failed");
+    return MJHIP_ERR_HIP;
+  }
   if (!dev) {
-    if (DfDq) HIPCHECK(hipMemcpyAsync(DfDq, oq, nn*8, hipMemcpyDeviceToHost, c->stream));
-    if (DfDv) HIPCHECK(hipMemcpyAsync(DfDv, ov, nn*8, hipMemcpyDeviceToHost, c->stream));
-    if (DfDa) HIPCHECK(hipMemcpyAsync(DfDa, oa, nn*8, hipMemcpyDeviceToHost, c->stream));
-    if (DmDq) HIPCHECK(hipMemcpyAsync(DmDq, om, nm*8, hipMemcpyDeviceToHost, c->stream));
-    if (DsDq) HIPCHECK(hipMemcpyAsync(DsDq, sq_, ns*8, hipMemcpyDeviceToHost, c->stream));
-    if (DsDv) HIPCHECK(hipMemcpyAsync(DsDv, sv_, ns*8, hipMemcpyDeviceToHost, c->stream));
-    if (DsDa) HIPCHECK(hipMemcpyAsync(DsDa, sa_, ns*8, hipMemcpyDeviceToHost, c->stream));
+    bool ok = true;
+    auto get = [&](double* h, const double* d, size_t n) {
+      if (h) ok = ok && hipMemcpyAsync(h, d, n*8, hipMemcpyDeviceToHost, c->stream) == hipSuccess;
+    };
+    get(DfDq, oq, nn); get(DfDv, ov, nn); get(DfDa, oa, nn); get(DmDq, om, nm);
+    get(DsDq, sq_, ns); get(DsDv, sv_, ns); get(DsDa, sa_, ns);
+    ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
+    release();
+    if (!ok) {
+      set_error("FD output download failed");
+      return MJHIP_ERR_HIP;
+    }
+  } else if (!tmp.empty()) {
     HIPCHECK(hipStreamSynchronize(c->stream));
-    for (double* p : tmp) hipFree(p);
+    release();
   }
   return MJHIP_OK;
+}
+
+MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
+                                   const mjtNum* qvel, const mjtNum* qacc, mjtNum eps,
+                                   mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq,
+                                   mjtNum* DsDv, mjtNum* DsDa, mjtNum* DmDq, int flags) {
+  return mjhip_inverseFDBatchEx(c, B, qpos, qvel, qacc, nullptr, eps, 0, DfDq, DfDv, DfDa,
+                                DsDq, DsDv, DsDa, DmDq, flags);
 }
 
 //---------------------------------- single-instance drop-in ---------------------------------

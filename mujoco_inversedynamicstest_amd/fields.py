@@ -76,10 +76,29 @@ def _parse():
   for group in ("MJHIP_DATA_INPUTS", "MJHIP_DATA_POSITION", "MJHIP_DATA_VELOCITY",
                 "MJHIP_DATA_ACCELERATION"):
     data += xd(group)
-  return sizes, model, data, xd("MJHIP_DATA_FORWARD"), xd("MJHIP_DATA_SENSOR_AUX")
+
+  def rows(group, tag):
+    return [RowField(ct, nm, w, int(st)) for ct, nm, w, st in re.findall(
+        tag + r"\(\s*(\w+)\s*,\s*(\w+)\s*,\s*([\w()]+)\s*,\s*(\d)\s*\)",
+        _macro_body(text, group))]
+  return (sizes, model, data, xd("MJHIP_DATA_FORWARD"), xd("MJHIP_DATA_SENSOR_AUX"),
+          rows("MJHIP_DATA_EFC", "XE"), rows("MJHIP_DATA_CONTACT", "XC"))
 
 
-MODEL_SIZES, MODEL_FIELDS, DATA_FIELDS, FORWARD_FIELDS, AUX_FIELDS = _parse()
+@dataclass(frozen=True)
+class RowField:
+  """A per-row (efc_*) or per-contact (con_*) array: `width` elements per row."""
+  ctype: str
+  name: str
+  width: str   # integer literal or MJ_M(size)
+  stage: int
+
+  def row_size(self, sizes: dict) -> int:
+    return _dim(self.width, sizes)
+
+
+(MODEL_SIZES, MODEL_FIELDS, DATA_FIELDS, FORWARD_FIELDS, AUX_FIELDS, EFC_FIELDS,
+ CONTACT_FIELDS) = _parse()
 MODEL_FIELD = {f.name: f for f in MODEL_FIELDS}
 DATA_FIELD = {f.name: f for f in DATA_FIELDS + FORWARD_FIELDS + AUX_FIELDS}
 
@@ -117,7 +136,10 @@ class CData(ctypes.Structure):
                ("time", ctypes.c_double)] +
               [(f.name, ctypes.POINTER(ctypes.c_double)) for f in DATA_FIELDS] +
               [(f.name, ctypes.POINTER(ctypes.c_double)) for f in FORWARD_FIELDS] +
-              [(f.name, ctypes.POINTER(ctypes.c_double)) for f in AUX_FIELDS])
+              [(f.name, ctypes.POINTER(ctypes.c_double)) for f in AUX_FIELDS] +
+              [(k, ctypes.c_int) for k in ("efc_capacity", "ne", "nf", "nl", "con_capacity",
+                                           "ncon")] +
+              [(f.name, ctypes.POINTER(CTYPE[f.ctype])) for f in EFC_FIELDS + CONTACT_FIELDS])
 
 
 def output_doubles(sizes: dict) -> int:

@@ -40,16 +40,36 @@ def model_struct(m) -> fields.CModel:
   return s
 
 
-class MjData:
-  """One instance of the per-instance fields (mjData subset), numpy-backed."""
+def model_capacity(m):
+  """(constraint rows, contacts) one instance of model m can produce on the device path
+  (mjhip_modelCapacity: exact for the implemented functions)."""
+  from . import engine
+  rows, cons = ctypes.c_int(), ctypes.c_int()
+  cm = model_struct(m)
+  engine.lib().mjhip_modelCapacity(ctypes.byref(cm), ctypes.byref(rows), ctypes.byref(cons))
+  return rows.value, cons.value
 
-  def __init__(self, m):
+
+class MjData:
+  """One instance of the per-instance fields (mjData subset), numpy-backed, with buffers for
+  the constraint rows and contacts (the reference's d->efc_* / d->contact)."""
+
+  def __init__(self, m, efc_capacity=None, con_capacity=None):
     self.m = m
     sizes = m.sizes
     self._arrays = {}
     for f in fields.DATA_FIELDS + fields.FORWARD_FIELDS + fields.AUX_FIELDS:
       n = f.size(sizes)
       self._arrays[f.name] = np.zeros(max(n, 1))
+    if efc_capacity is None or con_capacity is None:
+      rows, cons = model_capacity(m)
+      efc_capacity = rows if efc_capacity is None else efc_capacity
+      con_capacity = cons if con_capacity is None else con_capacity
+    self._rows = {}
+    for f, cap in ([(f, efc_capacity) for f in fields.EFC_FIELDS] +
+                   [(f, con_capacity) for f in fields.CONTACT_FIELDS]):
+      self._rows[f.name] = np.zeros(max(cap * f.row_size(sizes), 1),
+                                    dtype=fields.NPTYPE[f.ctype])
     # reference defaults (mj_resetData): qpos = qpos0, world body identity frames
     self._arrays["qpos"][:m.nq] = m.qpos0
     for b in range(m.nbody):            # mocap_pos/quat = body_pos/quat (mj_resetData)
@@ -60,6 +80,11 @@ class MjData:
     self.struct = fields.CData()
     for name, a in self._arrays.items():
       setattr(self.struct, name, a.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    self.struct.efc_capacity = efc_capacity
+    self.struct.con_capacity = con_capacity
+    for f in fields.EFC_FIELDS + fields.CONTACT_FIELDS:
+      setattr(self.struct, f.name,
+              self._rows[f.name].ctypes.data_as(ctypes.POINTER(fields.CTYPE[f.ctype])))
 
   def __getattr__(self, k):
     arrs = self.__dict__.get("_arrays")
@@ -69,9 +94,36 @@ class MjData:
       return arrs[k][:n]
     raise AttributeError(k)
 
+  def efc(self, name):
+    """Constraint-row (efc_*) or contact (con_*) array of the current rows / contacts, one
+    row per constraint (contact); a writable view of the buffer."""
+    f = {x.name: x for x in fields.EFC_FIELDS + fields.CONTACT_FIELDS}[name]
+    w = f.row_size(self.m.sizes)
+    n = self.struct.ncon if name.startswith("con_") else self.struct.nefc
+    return self._rows[name][:n * w].reshape(n, w)
+
+  def set_rows(self, nefc=None, ne=None, nf=None, nl=None, ncon=None, **arrays):
+    """Fill the constraint rows / contacts (as a forward pass would leave them)."""
+    for k, v in (("nefc", nefc), ("ne", ne), ("nf", nf), ("nl", nl), ("ncon", ncon)):
+      if v is not None:
+        setattr(self.struct, k, int(v))
+    for name, vals in arrays.items():
+      vals = np.ravel(vals)
+      self._rows[name][:len(vals)] = vals
+
   @property
   def nefc(self):
     return self.struct.nefc
+
+  @property
+  def ncon(self):
+    return self.struct.ncon
+
+  @property
+  def efc_counts(self):
+    """(nefc, ne, nf, nl)"""
+    s = self.struct
+    return s.nefc, s.ne, s.nf, s.nl
 
   @property
   def status(self):

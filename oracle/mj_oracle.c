@@ -885,6 +885,26 @@ void or_factorM(const mjhipModel* m, mjhipData* d) {
   for (int i = 0; i < m->nC; i++) d->qLD[i] = d->qM[m->mapM2C[i]];
   mj_factorI(d->qLD, d->qLDiagInv, m->nv, m->C_rownnz, m->C_rowadr, m->dof_simplenum,
              m->C_colind);
+  /* the engine's status word: a pivot D(k) below mjMINVAL, the condition the legacy
+   * factorization reports as mjWARN_INERTIA (:1426-1430); no clamping on this path */
+  for (int k = 0; k < m->nv; k++) {
+    if (!(d->qLD[m->C_rowadr[k] + m->C_rownnz[k] - 1] >= mjMINVAL)) {
+      d->status |= MJHIP_INST_INERTIA;
+    }
+  }
+}
+
+/* mju_isBad (engine_util_misc.c:1315-1317) */
+static int mju_isBad(mjtNum x) { return x != x || x > mjhipMAXVAL || x < -mjhipMAXVAL; }
+
+/* mj_checkPos/Vel/Acc (engine_forward.c:53-102) as the engine's per-instance status bits:
+ * on the inputs a call reads; no reset, no change to any result */
+static int or_checkInputs(const mjhipModel* m, const mjhipData* d, int pos, int vel, int acc) {
+  int st = 0;
+  for (int i = 0; pos && i < m->nq; i++) if (mju_isBad(d->qpos[i])) st |= MJHIP_INST_BADQPOS;
+  for (int i = 0; vel && i < m->nv; i++) if (mju_isBad(d->qvel[i])) st |= MJHIP_INST_BADQVEL;
+  for (int i = 0; acc && i < m->nv; i++) if (mju_isBad(d->qacc[i])) st |= MJHIP_INST_BADQACC;
+  return st;
 }
 
 /* :1629-1707 */
@@ -3134,7 +3154,7 @@ void or_inverseSkip(const mjhipModel* m, mjhipData* d, orEfc* e, int skipstage,
                     int skipsensor) {
   int nv = m->nv;
   mjtNum* qacc = NULL;
-  d->status = 0;
+  d->status = or_checkInputs(m, d, skipstage < mjhipSTAGE_POS, skipstage < mjhipSTAGE_VEL, 1);
   if (skipstage < mjhipSTAGE_POS) {
     or_invPosition(m, d, e);
     if (!skipsensor) or_sensorPos(m, d, e);
@@ -3213,7 +3233,7 @@ static void or_fwdActuation(const mjhipModel* m, mjhipData* d) {
  * with qacc = qacc_smooth (engine_forward.c:520-531, :654-: nefc = 0) */
 int or_forward(const mjhipModel* m, mjhipData* d, orEfc* e) {
   int nv = m->nv;
-  d->status = 0;
+  d->status = or_checkInputs(m, d, 1, 1, 0);
   or_invPosition(m, d, e);
   or_fwdVelocity(m, d, e);
   or_fwdActuation(m, d);
@@ -3226,6 +3246,7 @@ int or_forward(const mjhipModel* m, mjhipData* d, orEfc* e) {
   /* mj_fwdConstraint with nefc = 0: qacc = qacc_smooth, no constraint force */
   mju_copy(d->qacc, d->qacc_smooth, nv);
   mju_zero(d->qfrc_constraint, nv);
+  d->status |= or_checkInputs(m, d, 0, 0, 1);      /* mj_checkAcc after mj_forward */
   d->nefc = e->nefc;
   return e->nefc;
 }

@@ -90,7 +90,8 @@ class Oracle:
     self.m = m
     self.cm = host.model_struct(m)
     self.L = lib()
-    self.d = host.MjData(m)
+    # the oracle keeps its rows in its own orEfc (below), not in the data's row buffers
+    self.d = host.MjData(m, efc_capacity=0, con_capacity=0)
     cap = max(self.L.or_efcCapacity(ctypes.byref(self.cm)), 1)
     nv = max(m.nv, 1)
     self._efc_arrays = {n: np.zeros(cap * k) for n, k in
