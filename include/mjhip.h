@@ -358,6 +358,21 @@ MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B,
                                    mjtNum* DsDq, mjtNum* DsDv, mjtNum* DsDa, mjtNum* DmDq,
                                    int flags);
 
+/* mjhip_inverseFDBatch with the reference's flg_actuation (engine_derivative_fd.c:160-168):
+ * when set, every evaluation's force is qfrc_inverse - qfrc_actuator (mj_fwdActuation of the
+ * base state's controls `ctrl`, B x nu, which may be NULL when nu == 0). Actuators with
+ * activation dynamics or muscle/user gain and bias are MJHIP_ERR_MODEL. */
+MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
+                                     const mjtNum* qvel, const mjtNum* qacc, const mjtNum* ctrl,
+                                     mjtNum eps, int flg_actuation, mjtNum* DfDq, mjtNum* DfDv,
+                                     mjtNum* DfDa, mjtNum* DsDq, mjtNum* DsDv, mjtNum* DsDa,
+                                     mjtNum* DmDq, int flags);
+
+/* Per-instance row capacities of a model on the device path: constraint rows (efc) and
+ * contacts an instance can produce (exact upper bounds for the implemented functions). Size
+ * mjhipData's efc_* / con_* buffers with these. */
+MJHIP_API int mjhip_modelCapacity(const mjhipModel* m, int* efc_rows, int* contacts);
+
 /* Time `reps` back-to-back launches of the fused inverse kernel on the context's stream
  * with HIP events (device-resident mirror inputs, B instances). Writes the average
  * milliseconds per launch to *ms. Used by bench.py for the roofline figure. */
@@ -365,9 +380,15 @@ MJHIP_API int mjhip_timeInverseKernel(mjhipContext* c, int B, int reps, int skip
                                       int flags, float* ms);
 
 /*---------------------------- single-instance drop-in -------------------------------------*/
-/* Same semantics and outputs as the reference functions named above; they run a batch of
- * one instance on the GPU (device 0 unless mjhip_setDevice), uploading the fields a
- * skipped stage would have read from d and writing every output field back into d. */
+/* Same semantics and outputs as the reference functions of the same name (engine_inverse.c,
+ * engine_core_smooth.c, engine_support.c, engine_derivative_fd.c); they run one instance on
+ * the GPU (device 0 unless mjhip_setDevice). Each uploads the fields of d the reference
+ * function reads -- for mj_inverseSkip(skipstage) the inputs, the outputs of the skipped
+ * stages and their constraint rows / contacts (d->nefc, ne, nf, nl, ncon and the efc_* /
+ * con_* arrays) -- and writes back exactly the fields the reference function writes,
+ * including the rows of the stages that ran. Device state is cached per model content
+ * (at most 16 models, least recently used released first). Errors go to the error
+ * callback (or stderr); per-instance conditions to d->status. */
 MJHIP_API void mjhip_setDevice(int device);
 MJHIP_API void mjhip_inverse(const mjhipModel* m, mjhipData* d);
 MJHIP_API void mjhip_inverseSkip(const mjhipModel* m, mjhipData* d, int skipstage,
@@ -376,7 +397,18 @@ MJHIP_API void mjhip_invPosition(const mjhipModel* m, mjhipData* d);
 MJHIP_API void mjhip_invVelocity(const mjhipModel* m, mjhipData* d);
 MJHIP_API void mjhip_invConstraint(const mjhipModel* m, mjhipData* d);
 MJHIP_API void mjhip_rne(const mjhipModel* m, mjhipData* d, int flg_acc, mjtNum* result);
+/* mj_xfrcAccumulate (engine_support.c:1254-1261): qfrc += J' xfrc_applied over bodies 1..
+ * nbody-1, from d's xipos, subtree_com and cdof */
+MJHIP_API void mjhip_xfrcAccumulate(const mjhipModel* m, mjhipData* d, mjtNum* qfrc);
+/* mj_compareFwdInv (engine_inverse.c:275-316): from a forward pass's state and constraint
+ * rows in d, solver_fwdinv = (|qfrc_constraint fwd - inv|, |qfrc_applied + qfrc_actuator +
+ * J'xfrc_applied - qfrc_inverse|); qfrc_constraint and efc_force keep the forward values */
 MJHIP_API void mjhip_compareFwdInv(const mjhipModel* m, mjhipData* d);
+/* mjd_inverseFD (engine_derivative_fd.c:611-719) for one mjData; d keeps its qpos/qvel/qacc
+ * and holds the outputs of the reference's last evaluation afterwards */
+MJHIP_API void mjhip_inverseFD(const mjhipModel* m, mjhipData* d, mjtNum eps,
+                               mjtByte flg_actuation, mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa,
+                               mjtNum* DsDq, mjtNum* DsDv, mjtNum* DsDa, mjtNum* DmDq);
 /* release the per-model device state cached by the single-instance entry points */
 MJHIP_API void mjhip_releaseModel(const mjhipModel* m);
 

@@ -1453,10 +1453,48 @@ MJHIP_API int mjhip_inverseFDBatch(mjhipContext* c, int B, const mjtNum* qpos,
 }
 
 //---------------------------------- single-instance drop-in ---------------------------------
+// The reference's single-mjData entry points run as a batch of one on instance 0 of a
+// per-model context: the fields a call reads are uploaded from the host mjhipData, one kernel
+// runs the stages the reference function runs, and the fields it writes come back.
+
+MJHIP_API int mjhip_modelCapacity(const mjhipModel* m, int* efc_rows, int* contacts) {
+  if (!m) return MJHIP_ERR_ARG;
+  if (efc_rows) *efc_rows = mjhip_efcCapacity(m);
+  if (contacts) *contacts = mjhip_contactCapacity(m, nullptr);
+  return MJHIP_OK;
+}
+
+// one stage of mj_inverseSkip (or a helper it calls) on instance 0 (the reference function
+// is named in the comment); lane 0 of one 64-lane block runs it. ST_INV is the whole
+// mj_inverseSkip on the unfused path, which leaves every constraint row in the mirror.
+extern "C++" {
+enum { ST_INV = 0, ST_POS, ST_VEL, ST_CON, ST_RNE0, ST_RNE1, ST_XFRC };
+template <bool CONTACT>
+__global__ __launch_bounds__(64) void k_stage(mjhipModel m, Mirror mr, int what, int skipstage,
+                                              int skipsensor, int* __restrict__ status) {
+  if (threadIdx.x) return;
+  Lane<64> d = lane_view(mr, 0, 0);
+  int st = 0;
+  switch (what) {
+    case ST_INV: st = mjh::inverseSkip<64, CONTACT, false>(m, d, skipstage, skipsensor); break;
+    case ST_POS: mjh::invPosition<64, CONTACT, false>(m, d, &st); break;   // mj_invPosition
+    case ST_VEL: mjh::invVelocity<64, false>(m, d); break;                 // mj_invVelocity
+    case ST_CON: mjh::invConstraint(m, d); break;                          // mj_invConstraint
+    case ST_RNE0: mjh::rne(m, d, 0, d.qfrc_tmp); break;                    // mj_rne(flg_acc=0)
+    case ST_RNE1: mjh::rne(m, d, 1, d.qfrc_tmp); break;                    // mj_rne(flg_acc=1)
+    case ST_XFRC: mjh::xfrcAccumulate(m, d, d.qfrc_tmp); break;            // mj_xfrcAccumulate
+  }
+  if (status) status[0] = st;
+}
+}  // extern "C++"
 
 static int g_device = 0;
 static std::mutex g_mu;
-static std::unordered_map<const mjhipModel*, mjhipContext*> g_ctx;
+// contexts of the single-instance calls, keyed by the model's content signature (sizes,
+// options, every array): a new or edited model at a reused address gets its own context
+struct CachedCtx { unsigned long long sig; mjhipContext* c; };
+static std::vector<CachedCtx> g_ctx;        // most recently used last, at most kMaxCtx
+static const size_t kMaxCtx = 16;
 
 static void report(const char* what) {
   std::string msg = std::string(what) + ": " + g_last_error;
@@ -1468,27 +1506,175 @@ static void report(const char* what) {
 }
 
 static mjhipContext* ctx_for(const mjhipModel* m) {
+  const unsigned long long sig = model_signature(m);
   std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_ctx.find(m);
-  if (it != g_ctx.end()) return it->second;
+  for (size_t i = 0; i < g_ctx.size(); i++) {
+    if (g_ctx[i].sig == sig) {
+      CachedCtx e = g_ctx[i];
+      g_ctx.erase(g_ctx.begin() + i);
+      g_ctx.push_back(e);
+      return e.c;
+    }
+  }
   mjhipContext* c = nullptr;
   if (mjhip_contextCreate(m, g_device, 64, &c) != MJHIP_OK) return nullptr;
-  g_ctx[m] = c;
+  if (g_ctx.size() >= kMaxCtx) {            // evict the least recently used
+    mjhip_contextFree(g_ctx.front().c);
+    g_ctx.erase(g_ctx.begin());
+  }
+  g_ctx.push_back({sig, c});
   return c;
 }
 
 MJHIP_API void mjhip_setDevice(int device) { g_device = device; }
 
 MJHIP_API void mjhip_releaseModel(const mjhipModel* m) {
+  const unsigned long long sig = model_signature(m);
   std::lock_guard<std::mutex> lk(g_mu);
-  auto it = g_ctx.find(m);
-  if (it != g_ctx.end()) {
-    mjhip_contextFree(it->second);
-    g_ctx.erase(it);
+  for (size_t i = 0; i < g_ctx.size(); i++) {
+    if (g_ctx[i].sig == sig) {
+      mjhip_contextFree(g_ctx[i].c);
+      g_ctx.erase(g_ctx.begin() + i);
+      return;
+    }
   }
 }
 
-// upload the fields a skipped stage reads, run one instance, download every output field
+extern "C++" {
+// instance 0 of a mirror field: element k at F[k*64] (block 0, lane 0)
+template <class T>
+static int put0(mjhipContext* c, T* dev, const T* host, long n) {
+  if (n <= 0 || !dev || !host) return MJHIP_OK;
+  HIPCHECK(hipMemcpy2DAsync(dev, 64*sizeof(T), host, sizeof(T), sizeof(T), n,
+                            hipMemcpyHostToDevice, c->stream));
+  return MJHIP_OK;
+}
+
+template <class T>
+static int get0(mjhipContext* c, T* host, const T* dev, long n) {
+  if (n <= 0 || !dev || !host) return MJHIP_OK;
+  HIPCHECK(hipMemcpy2DAsync(host, sizeof(T), dev, 64*sizeof(T), sizeof(T), n,
+                            hipMemcpyDeviceToHost, c->stream));
+  return MJHIP_OK;
+}
+}  // extern "C++"
+
+// data fields of stages lo..hi (MJHIP_DATA_FIELDS stage numbers) host -> instance 0
+static int put_stages(mjhipContext* c, const mjhipModel* m, const mjhipData* d, int lo, int hi) {
+  int rc = 0;
+#define MJ_M(n) m->n
+#define XD(name, d0, d1, stage)                                                          \
+  if (!rc && stage >= lo && stage <= hi) rc = put0(c, c->mirror.name, (const double*)d->name, \
+                                                   (long)(m->d0) * (d1));
+  MJHIP_DATA_FIELDS
+#undef XD
+#undef MJ_M
+  return rc;
+}
+
+static int get_stages(mjhipContext* c, const mjhipModel* m, mjhipData* d, int lo, int hi) {
+  int rc = 0;
+#define MJ_M(n) m->n
+#define XD(name, d0, d1, stage)                                                          \
+  if (!rc && stage >= lo && stage <= hi) rc = get0(c, d->name, (const double*)c->mirror.name, \
+                                                   (long)(m->d0) * (d1));
+  MJHIP_DATA_FIELDS
+#undef XD
+#undef MJ_M
+  return rc;
+}
+
+// constraint rows (XE) and contacts (XC) written by stages lo..hi, host -> instance 0, with
+// the counts. Rows beyond the context's capacity cannot come from a supported model.
+static int put_rows(mjhipContext* c, const mjhipModel* m, const mjhipData* d, int lo, int hi) {
+  if (d->nefc > c->efc_cap || d->ncon > c->con_cap || d->nefc < 0 || d->ncon < 0) {
+    set_error("%d constraint rows / %d contacts exceed the model's device capacity (%d / %d)",
+              d->nefc, d->ncon, c->efc_cap, c->con_cap);
+    return MJHIP_ERR_CAPACITY;
+  }
+  if ((d->nefc && d->efc_capacity < d->nefc) || (d->ncon && d->con_capacity < d->ncon)) {
+    set_error("mjhipData holds %d rows / %d contacts but capacities %d / %d",
+              d->nefc, d->ncon, d->efc_capacity, d->con_capacity);
+    return MJHIP_ERR_ARG;
+  }
+  const int cnt[4] = {d->nefc, d->ne, d->nf, d->nl};
+  int rc = put0(c, c->mirror.efc_count, cnt, 4);
+  if (!rc) rc = put0(c, c->mirror.con_count, &d->ncon, 1);
+  const int nv = m->nv;
+  (void)nv;
+#define MJ_M(n) m->n
+#define XE(type, name, w, stage) \
+  if (!rc && stage >= lo && stage <= hi) rc = put0(c, c->mirror.name, (const type*)d->name, \
+                                                   (long)d->nefc * (w));
+  MJHIP_DATA_EFC
+#undef XE
+#define XC(type, name, w, stage) \
+  if (!rc && stage >= lo && stage <= hi) rc = put0(c, c->mirror.name, (const type*)d->name, \
+                                                   (long)d->ncon * (w));
+  MJHIP_DATA_CONTACT
+#undef XC
+#undef MJ_M
+  return rc;
+}
+
+// rows written by stages lo..hi, instance 0 -> host, and the counts (contacts when lo <= 1);
+// the caller synchronizes. Reading the counts needs one blocking copy first.
+static int get_rows(mjhipContext* c, const mjhipModel* m, mjhipData* d, int lo, int hi) {
+  int cnt[4] = {0, 0, 0, 0}, ncon = 0;
+  int rc = get0(c, cnt, (const int*)c->mirror.efc_count, 4);
+  if (!rc) rc = get0(c, &ncon, (const int*)c->mirror.con_count, 1);
+  if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) {
+    set_error("hipStreamSynchronize failed");
+    rc = MJHIP_ERR_HIP;
+  }
+  if (rc) return rc;
+  d->nefc = cnt[0]; d->ne = cnt[1]; d->nf = cnt[2]; d->nl = cnt[3];
+  if (lo <= 1) d->ncon = ncon;
+  // rows a caller's buffers cannot hold: mjWARN_CNSTRFULL analogue, nothing written
+  if ((cnt[0] && d->efc_capacity < cnt[0]) || (lo <= 1 && ncon && d->con_capacity < ncon)) {
+    if (d->efc_capacity > 0 || d->con_capacity > 0) d->status |= MJHIP_INST_CNSTRFULL;
+    return MJHIP_OK;
+  }
+#define MJ_M(n) m->n
+#define XE(type, name, w, stage) \
+  if (!rc && stage >= lo && stage <= hi) rc = get0(c, (type*)d->name, (const type*)c->mirror.name, \
+                                                   (long)cnt[0] * (w));
+  MJHIP_DATA_EFC
+#undef XE
+#define XC(type, name, w, stage) \
+  if (!rc && lo <= 1 && stage >= lo && stage <= hi) \
+    rc = get0(c, (type*)d->name, (const type*)c->mirror.name, (long)ncon * (w));
+  MJHIP_DATA_CONTACT
+#undef XC
+#undef MJ_M
+  return rc;
+}
+
+static int sync_stream(mjhipContext* c) {
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  return MJHIP_OK;
+}
+
+// run one k_stage on instance 0; status comes back into d->status
+static int run_stage(mjhipContext* c, mjhipData* d, int what, int skipstage = 0,
+                     int skipsensor = 1) {
+  if (c->con_cap > 0) {
+    hipLaunchKernelGGL(k_stage<true>, dim3(1), dim3(64), 0, c->stream, c->dmodel, c->mirror,
+                       what, skipstage, skipsensor, c->status);
+  } else {
+    hipLaunchKernelGGL(k_stage<false>, dim3(1), dim3(64), 0, c->stream, c->dmodel, c->mirror,
+                       what, skipstage, skipsensor, c->status);
+  }
+  HIPCHECK(hipGetLastError());
+  int st = 0;
+  if (int rc = get0(c, &st, (const int*)c->status, 1)) return rc;
+  if (int rc = sync_stream(c)) return rc;
+  d->status = st;
+  return MJHIP_OK;
+}
+
+// upload the fields a skipped stage reads (data fields, constraint rows, contacts), run one
+// instance, download every output field of the stages that ran
 MJHIP_API void mjhip_inverseSkip(const mjhipModel* m, mjhipData* d, int skipstage,
                                  int skipsensor) {
   mjhipContext* c = ctx_for(m);
@@ -1496,60 +1682,51 @@ MJHIP_API void mjhip_inverseSkip(const mjhipModel* m, mjhipData* d, int skipstag
     report("mjhip_inverseSkip");
     return;
   }
-  int rc = 0;
-#define MJ_M(n) m->n
-#define XD(name, d0, d1, stage)                                                     \
-  if (!rc && d->name && (stage == 0 || stage <= skipstage) && (m->d0) * (d1) > 0)    \
-    rc = mjhip_mirrorUpload(c, #name, 0, 1, d->name);
-  MJHIP_DATA_FIELDS
-#undef XD
+  int rc = hipSetDevice(c->device) == hipSuccess ? 0 : MJHIP_ERR_HIP;
+  if (!rc) rc = put_stages(c, m, d, 0, skipstage);
+  // the constraint rows of the skipped stages: mj_makeConstraint's (skipstage >= POS) and
+  // mj_referenceConstraint's efc_vel / efc_aref (skipstage >= VEL)
+  if (!rc && skipstage >= mjhipSTAGE_POS) rc = put_rows(c, m, d, 1, skipstage);
   if (!rc && m->nsensor > 0) {
     // sensor inputs: the values of skipped stages' sensors are kept (sensordata), and the
     // mjData inputs some sensors read (clock: time; force/torque/accelerometer via
     // mj_rnePostConstraint: xfrc_applied; actuatorfrc/jointactuatorfrc)
     if (skipstage > mjhipSTAGE_NONE && d->sensordata)
-      rc = mjhip_mirrorUpload(c, "sensordata", 0, 1, d->sensordata);
-    if (!rc) rc = mjhip_mirrorUpload(c, "time", 0, 1, &d->time);
-    if (!rc && d->xfrc_applied && m->nbody)
-      rc = mjhip_mirrorUpload(c, "xfrc_applied", 0, 1, d->xfrc_applied);
-    if (!rc && d->actuator_force && m->nu)
-      rc = mjhip_mirrorUpload(c, "actuator_force", 0, 1, d->actuator_force);
-    if (!rc && d->qfrc_actuator && m->nv)
-      rc = mjhip_mirrorUpload(c, "qfrc_actuator", 0, 1, d->qfrc_actuator);
+      rc = put0(c, c->mirror.sensordata, (const double*)d->sensordata, m->nsensordata);
+    if (!rc) rc = put0(c, c->mirror.time, &d->time, 1);
+    if (!rc && d->xfrc_applied) rc = put0(c, c->mirror.xfrc_applied, (const double*)d->xfrc_applied,
+                                          6L*m->nbody);
+    if (!rc && d->actuator_force) rc = put0(c, c->mirror.actuator_force,
+                                            (const double*)d->actuator_force, (long)m->nu);
+    if (!rc && d->qfrc_actuator) rc = put0(c, c->mirror.qfrc_actuator,
+                                           (const double*)d->qfrc_actuator, (long)m->nv);
   }
-  if (!rc) {
-    rc = mjhip_inverseBatch(c, 1, nullptr, nullptr, nullptr, nullptr, skipstage, skipsensor,
-                            MJHIP_FLAG_MIRROR_INPUT, &d->status);
-    if (rc == MJHIP_ERR_INSTANCE) rc = 0;
+  if (!rc && (skipstage < mjhipSTAGE_NONE || skipstage > mjhipSTAGE_VEL)) {
+    set_error("skipstage must be mjSTAGE_NONE, mjSTAGE_POS or mjSTAGE_VEL");
+    rc = MJHIP_ERR_ARG;
   }
-#define XD(name, d0, d1, stage)                                                     \
-  if (!rc && d->name && stage > skipstage && (m->d0) * (d1) > 0)                     \
-    rc = mjhip_mirrorDownload(c, #name, 0, 1, d->name);
-  MJHIP_DATA_FIELDS
-#undef XD
-#undef MJ_M
+  if (!rc) rc = run_stage(c, d, ST_INV, skipstage, skipsensor);
+  if (!rc) rc = get_stages(c, m, d, skipstage + 1, 3);
   if (!rc && m->nsensor > 0 && !skipsensor) {
     // mjData fields the sensor stages computed on demand (scratch sized 0 when unneeded)
+#define MJ_M(n) m->n
 #define XD(name, d0, d1, stage)                                                     \
     if (!rc && d->name && c->mirror.name##_n > 0)                                    \
-      rc = mjhip_mirrorDownload(c, #name, 0, 1, d->name);
+      rc = get0(c, d->name, (const double*)c->mirror.name, (long)(m->d0) * (d1));
     MJHIP_DATA_SENSOR_AUX
 #undef XD
+#undef MJ_M
   }
-  if (!rc && (m->opt.enableflags & mjhipENBL_ENERGY) && skipstage < mjhipSTAGE_VEL) {
+  mjtNum e[2] = {0, 0};
+  const bool energy = (m->opt.enableflags & mjhipENBL_ENERGY) && skipstage < mjhipSTAGE_VEL;
+  if (!rc && energy) rc = get0(c, e, (const double*)c->mirror.energy, 2);
+  // the rows of the stages that ran (and the counts); get_rows synchronizes the stream
+  if (!rc) rc = get_rows(c, m, d, skipstage + 1, 3);
+  if (!rc) rc = sync_stream(c);
+  if (!rc && energy) {
     // mj_energyPos/Vel write the energy of the stages that ran (engine_inverse.c:207-223)
-    mjtNum e[2];
-    rc = mjhip_mirrorDownload(c, "energy", 0, 1, e);
-    if (!rc) {
-      if (skipstage < mjhipSTAGE_POS) d->energy[0] = e[0];
-      d->energy[1] = e[1];
-    }
-  }
-  if (!rc) {
-    int cnt[4];
-    if (hipMemcpy(cnt, c->mirror.efc_count, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess) {
-      d->nefc = cnt[0];
-    }
+    if (skipstage < mjhipSTAGE_POS) d->energy[0] = e[0];
+    d->energy[1] = e[1];
   }
   if (rc) report("mjhip_inverseSkip");
 }
@@ -1558,37 +1735,180 @@ MJHIP_API void mjhip_inverse(const mjhipModel* m, mjhipData* d) {
   mjhip_inverseSkip(m, d, mjhipSTAGE_NONE, 0);
 }
 
+// mj_invPosition / mj_invVelocity / mj_invConstraint (engine_inverse.c:37-76, :169-192): only
+// that stage runs, it reads the inputs and earlier stages' fields from d and writes only its
+// own outputs into d
+static void single_stage(const mjhipModel* m, mjhipData* d, int what, const char* name) {
+  mjhipContext* c = ctx_for(m);
+  int rc = c ? 0 : MJHIP_ERR_HIP;
+  if (!rc && hipSetDevice(c->device) != hipSuccess) rc = MJHIP_ERR_HIP;
+  const int stage = what;                  // ST_POS/VEL/CON = position/velocity/acceleration
+  if (!rc) rc = put_stages(c, m, d, 0, stage - 1);
+  if (!rc && stage > ST_POS) rc = put_rows(c, m, d, 1, stage - 1);
+  if (!rc) rc = run_stage(c, d, what);
+  if (!rc) {
+    if (what == ST_CON) {                  // qfrc_constraint only (qfrc_inverse is not its output)
+      rc = get0(c, d->qfrc_constraint, (const double*)c->mirror.qfrc_constraint, (long)m->nv);
+    } else {
+      rc = get_stages(c, m, d, stage, stage);
+    }
+  }
+  if (!rc) rc = get_rows(c, m, d, stage, stage);
+  if (!rc) rc = sync_stream(c);
+  if (rc) report(name);
+}
+
 MJHIP_API void mjhip_invPosition(const mjhipModel* m, mjhipData* d) {
-  // a full evaluation computes the position stage; later-stage outputs are also refreshed
-  mjhip_inverseSkip(m, d, mjhipSTAGE_NONE, 1);
+  single_stage(m, d, ST_POS, "mjhip_invPosition");
 }
 
 MJHIP_API void mjhip_invVelocity(const mjhipModel* m, mjhipData* d) {
-  mjhip_inverseSkip(m, d, mjhipSTAGE_POS, 1);
+  single_stage(m, d, ST_VEL, "mjhip_invVelocity");
 }
 
 MJHIP_API void mjhip_invConstraint(const mjhipModel* m, mjhipData* d) {
-  mjhip_inverseSkip(m, d, mjhipSTAGE_VEL, 1);
+  single_stage(m, d, ST_CON, "mjhip_invConstraint");
 }
 
+// mj_rne (engine_core_smooth.c:1969-2023): reads the caller's cdof, cinert, cvel, cdof_dot,
+// qvel (and qacc with flg_acc) and writes only `result`
 MJHIP_API void mjhip_rne(const mjhipModel* m, mjhipData* d, int flg_acc, mjtNum* result) {
-  // mj_rne(flg_acc=1) is the qfrc_inverse core before the armature/passive/constraint
-  // terms; flg_acc=0 is qfrc_bias: both are produced by the fused pipeline
-  mjhip_inverseSkip(m, d, mjhipSTAGE_NONE, 1);
-  if (!result) return;
-  for (int i = 0; i < m->nv; i++) {
-    result[i] = flg_acc ? d->qfrc_inverse[i] - m->dof_armature[i]*d->qacc[i]
-                              + d->qfrc_passive[i] + d->qfrc_constraint[i]
-                        : d->qfrc_bias[i];
-  }
+  mjhipContext* c = ctx_for(m);
+  int rc = c ? 0 : MJHIP_ERR_HIP;
+  if (!rc && hipSetDevice(c->device) != hipSuccess) rc = MJHIP_ERR_HIP;
+  if (!rc) rc = put0(c, c->mirror.cdof, (const double*)d->cdof, 6L*m->nv);
+  if (!rc) rc = put0(c, c->mirror.cinert, (const double*)d->cinert, 10L*m->nbody);
+  if (!rc) rc = put0(c, c->mirror.cvel, (const double*)d->cvel, 6L*m->nbody);
+  if (!rc) rc = put0(c, c->mirror.cdof_dot, (const double*)d->cdof_dot, 6L*m->nv);
+  if (!rc) rc = put0(c, c->mirror.qvel, (const double*)d->qvel, (long)m->nv);
+  if (!rc && flg_acc) rc = put0(c, c->mirror.qacc, (const double*)d->qacc, (long)m->nv);
+  int st = d->status;
+  if (!rc) rc = run_stage(c, d, flg_acc ? ST_RNE1 : ST_RNE0);
+  d->status = st;                          // mj_rne leaves d alone
+  if (!rc && result) rc = get0(c, result, (const double*)c->mirror.qfrc_tmp, (long)m->nv);
+  if (!rc) rc = sync_stream(c);
+  if (rc) report("mjhip_rne");
 }
 
+// mj_xfrcAccumulate (engine_support.c:1254-1261): qfrc += J' xfrc_applied over bodies 1..,
+// through mj_applyFT (its mj_jac reads d's xipos, subtree_com and cdof)
+MJHIP_API void mjhip_xfrcAccumulate(const mjhipModel* m, mjhipData* d, mjtNum* qfrc) {
+  mjhipContext* c = ctx_for(m);
+  int rc = c ? 0 : MJHIP_ERR_HIP;
+  if (!rc && hipSetDevice(c->device) != hipSuccess) rc = MJHIP_ERR_HIP;
+  if (!rc) rc = put0(c, c->mirror.xipos, (const double*)d->xipos, 3L*m->nbody);
+  if (!rc) rc = put0(c, c->mirror.subtree_com, (const double*)d->subtree_com, 3L*m->nbody);
+  if (!rc) rc = put0(c, c->mirror.cdof, (const double*)d->cdof, 6L*m->nv);
+  if (!rc) rc = put0(c, c->mirror.xfrc_applied, (const double*)d->xfrc_applied, 6L*m->nbody);
+  if (!rc) rc = put0(c, c->mirror.qfrc_tmp, (const double*)qfrc, (long)m->nv);
+  int st = d->status;
+  if (!rc) rc = run_stage(c, d, ST_XFRC);
+  d->status = st;
+  if (!rc) rc = get0(c, qfrc, (const double*)c->mirror.qfrc_tmp, (long)m->nv);
+  if (!rc) rc = sync_stream(c);
+  if (rc) report("mjhip_xfrcAccumulate");
+}
+
+// mju_dot (engine_util_blas.c:680-741, four partial sums) and mju_norm, for the two norms of
+// mj_compareFwdInv
+static double dot4(const double* a, const double* b, int n) {
+  double r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  int i = 0;
+  for (; i + 4 <= n; i += 4) {
+    r0 += a[i]*b[i];
+    r1 += a[i+1]*b[i+1];
+    r2 += a[i+2]*b[i+2];
+    r3 += a[i+3]*b[i+3];
+  }
+  double res = (r0 + r2) + (r1 + r3);
+  const int left = n - i;           // the tail is one sum added to res, as mju_dot's
+  if (left == 3) {
+    res += a[i]*b[i] + a[i+1]*b[i+1] + a[i+2]*b[i+2];
+  } else if (left == 2) {
+    res += a[i]*b[i] + a[i+1]*b[i+1];
+  } else if (left == 1) {
+    res += a[i]*b[i];
+  }
+  return res;
+}
+
+// mj_compareFwdInv (engine_inverse.c:275-316): with constraint rows, qforce = qfrc_applied +
+// qfrc_actuator + J'xfrc_applied (mj_xfrcAccumulate) is what inverse dynamics of the forward
+// pass's qacc must return; mj_inverseSkip(VEL, 1) runs on the device with the forward pass's
+// rows; solver_fwdinv = (|fwd - inv qfrc_constraint|, |qforce - qfrc_inverse|); the forward
+// qfrc_constraint and efc_force are restored.
 MJHIP_API void mjhip_compareFwdInv(const mjhipModel* m, mjhipData* d) {
-  // engine_inverse.c:275-316: returns immediately when nefc == 0
+  const int nv = m->nv, nefc = d->nefc;
   d->solver_fwdinv[0] = d->solver_fwdinv[1] = 0;
-  if (!d->nefc) return;
-  set_error("mj_compareFwdInv with active constraints needs the forward solver (next)");
-  report("mjhip_compareFwdInv");
+  if (!nefc) return;
+  if (!d->efc_force || d->efc_capacity < nefc) {
+    set_error("mj_compareFwdInv: the data holds no constraint rows (efc_capacity %d < nefc %d)",
+              d->efc_capacity, nefc);
+    report("mjhip_compareFwdInv");
+    return;
+  }
+  std::vector<double> qforce(nv), dif(nv), save_qc(d->qfrc_constraint, d->qfrc_constraint + nv),
+                      save_force(d->efc_force, d->efc_force + nefc);
+  for (int i = 0; i < nv; i++) qforce[i] = d->qfrc_applied[i] + d->qfrc_actuator[i];
+  mjhip_xfrcAccumulate(m, d, qforce.data());
+  mjhip_inverseSkip(m, d, mjhipSTAGE_VEL, 1);
+  for (int i = 0; i < nv; i++) dif[i] = save_qc[i] - d->qfrc_constraint[i];
+  d->solver_fwdinv[0] = sqrt(dot4(dif.data(), dif.data(), nv));
+  for (int i = 0; i < nv; i++) dif[i] = qforce[i] - d->qfrc_inverse[i];
+  d->solver_fwdinv[1] = sqrt(dot4(dif.data(), dif.data(), nv));
+  memcpy(d->qfrc_constraint, save_qc.data(), sizeof(double)*nv);
+  memcpy(d->efc_force, save_force.data(), sizeof(double)*nefc);
+}
+
+// mjd_inverseFD (engine_derivative_fd.c:611-719, mujoco.h:1244-1247) for one mjData: the
+// batched FD with one base state (d's qpos, qvel, qacc, ctrl). Like the reference, d is left
+// with the outputs of the last evaluation (the last qpos perturbation) and its own qpos.
+MJHIP_API void mjhip_inverseFD(const mjhipModel* m, mjhipData* d, mjtNum eps,
+                               mjtByte flg_actuation, mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa,
+                               mjtNum* DsDq, mjtNum* DsDv, mjtNum* DsDa, mjtNum* DmDq) {
+  const int P = 3*m->nv + 1;
+  mjhipContext* c = nullptr;
+  {
+    // an FD batch of one needs 3nv+1 instances: a context of that capacity, cached like the
+    // single-instance ones under a signature salted with the capacity
+    const unsigned long long sig = model_signature(m) ^ 0x9E3779B97F4A7C15ull;
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (size_t i = 0; i < g_ctx.size() && !c; i++) {
+      if (g_ctx[i].sig == sig) c = g_ctx[i].c;
+    }
+    if (!c && mjhip_contextCreate(m, g_device, P, &c) == MJHIP_OK) {
+      if (g_ctx.size() >= kMaxCtx) {
+        mjhip_contextFree(g_ctx.front().c);
+        g_ctx.erase(g_ctx.begin());
+      }
+      g_ctx.push_back({sig, c});
+    }
+  }
+  int rc = c ? 0 : MJHIP_ERR_HIP;
+  if (!rc && m->nsensor && (DsDq || DsDv || DsDa)) {
+    std::vector<double> t(P, d->time);                    // clock sensors of every evaluation
+    rc = mjhip_mirrorUpload(c, "time", 0, P, t.data());
+  }
+  if (!rc) rc = mjhip_inverseFDBatchEx(c, 1, d->qpos, d->qvel, d->qacc, d->ctrl, eps,
+                                       flg_actuation, DfDq, DfDv, DfDa, DsDq, DsDv, DsDa, DmDq,
+                                       0);
+  if (!rc) {
+    // the reference's last evaluation (engine_derivative_fd.c:646-715): the last qpos
+    // perturbation, else the last qvel one, else the last qacc one, else the centre
+    const int nv = m->nv;
+    const int last = (DfDq || DsDq || DmDq) ? P - 1 : (DfDv || DsDv) ? 2*nv
+                     : (DfDa || DsDa) ? nv : 0;
+    std::vector<double> keep(d->qpos, d->qpos + m->nq);
+#define MJ_M(n) m->n
+#define XD(name, d0, d1, stage)                                                     \
+    if (!rc && d->name && stage > 0 && (m->d0) * (d1) > 0)                           \
+      rc = mjhip_mirrorDownload(c, #name, last, 1, d->name);
+    MJHIP_DATA_FIELDS
+#undef XD
+#undef MJ_M
+    memcpy(d->qpos, keep.data(), sizeof(double)*m->nq);
+  }
+  if (rc) report("mjhip_inverseFD");
 }
 
 }  // extern "C"

@@ -66,6 +66,10 @@ SIGNATURES = {
     "mjhip_statusDownload": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, _I]),
     "mjhip_inverseFDBatch": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, ctypes.c_double,
                                             _V, _V, _V, _V, _V, _V, _V, ctypes.c_int]),
+    "mjhip_inverseFDBatchEx": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, _V,
+                                              ctypes.c_double, ctypes.c_int, _V, _V, _V, _V,
+                                              _V, _V, _V, ctypes.c_int]),
+    "mjhip_modelCapacity": (ctypes.c_int, [_V, _I, _I]),
     "mjhip_timeInverseKernel": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_float)]),
@@ -76,7 +80,10 @@ SIGNATURES = {
     "mjhip_invVelocity": (None, [_V, _V]),
     "mjhip_invConstraint": (None, [_V, _V]),
     "mjhip_rne": (None, [_V, _V, ctypes.c_int, _D]),
+    "mjhip_xfrcAccumulate": (None, [_V, _V, _D]),
     "mjhip_compareFwdInv": (None, [_V, _V]),
+    "mjhip_inverseFD": (None, [_V, _V, ctypes.c_double, ctypes.c_ubyte, _D, _D, _D, _D, _D,
+                               _D, _D]),
     "mjhip_releaseModel": (None, [_V]),
 }
 
@@ -287,9 +294,11 @@ class InverseEngine:
            "mjhip_timeInverseKernel")
     return ms.value
 
-  def inverse_fd(self, qpos, qvel, qacc, eps=1e-6, dmdq=False, sensors=False, out=None):
-    """Batched mjd_inverseFD (flg_actuation=0): DfDq, DfDv, DfDa [B, nv, nv], DmDq
-    [B, nv, nM] (or None), plus (DsDq, DsDv, DsDa) [B, nv, nsensordata] when sensors.
+  def inverse_fd(self, qpos, qvel, qacc, eps=1e-6, dmdq=False, sensors=False, out=None,
+                 ctrl=None, flg_actuation=False):
+    """Batched mjd_inverseFD: DfDq, DfDv, DfDa [B, nv, nv], DmDq [B, nv, nM] (or None), plus
+    (DsDq, DsDv, DsDa) [B, nv, nsensordata] when sensors. With flg_actuation the forces are
+    qfrc_inverse - qfrc_actuator of the base states' controls ctrl [B, nu].
 
     Host arrays in -> numpy arrays out (PCIe both ways). Contiguous float64 torch tensors on
     the context's GPU in -> torch tensors out on that GPU, asynchronous on the context's
@@ -305,10 +314,12 @@ class InverseEngine:
           out = out + ((mk(ns), mk(ns), mk(ns)),)
       ptr = lambda t: None if t is None else _dptr(t)
       Ds = out[4] if len(out) > 4 else (None, None, None)
-      _check(lib().mjhip_inverseFDBatch(self.ctx, B, _dptr(qpos), _dptr(qvel), _dptr(qacc),
-                                        eps, ptr(out[0]), ptr(out[1]), ptr(out[2]),
-                                        *map(ptr, Ds), ptr(out[3]), FLAG_DEVICE_PTRS),
-             "mjhip_inverseFDBatch")
+      _check(lib().mjhip_inverseFDBatchEx(self.ctx, B, _dptr(qpos), _dptr(qvel), _dptr(qacc),
+                                          None if ctrl is None else _dptr(ctrl), eps,
+                                          int(bool(flg_actuation)), ptr(out[0]), ptr(out[1]),
+                                          ptr(out[2]), *map(ptr, Ds), ptr(out[3]),
+                                          FLAG_DEVICE_PTRS),
+             "mjhip_inverseFDBatchEx")
       return tuple(out)
     qpos = np.ascontiguousarray(qpos, dtype=np.float64).reshape(-1, self.nq)
     qvel = np.ascontiguousarray(qvel, dtype=np.float64).reshape(-1, self.nv)
@@ -320,10 +331,13 @@ class InverseEngine:
     DmDq = np.zeros((B, nv, self.m.nM)) if dmdq else None
     Ds = tuple(np.zeros((B, nv, ns)) for _ in range(3)) if sensors else (None, None, None)
     p = lambda a: None if a is None else a.ctypes.data
-    _check(lib().mjhip_inverseFDBatch(self.ctx, B, qpos.ctypes.data, qvel.ctypes.data,
-                                      qacc.ctypes.data, eps, p(DfDq), p(DfDv), p(DfDa),
-                                      *map(p, Ds), p(DmDq), 0),
-           "mjhip_inverseFDBatch")
+    if ctrl is not None:
+      ctrl = np.ascontiguousarray(ctrl, dtype=np.float64).reshape(B, -1)
+    _check(lib().mjhip_inverseFDBatchEx(self.ctx, B, qpos.ctypes.data, qvel.ctypes.data,
+                                        qacc.ctypes.data, p(ctrl), eps,
+                                        int(bool(flg_actuation)), p(DfDq), p(DfDv), p(DfDa),
+                                        *map(p, Ds), p(DmDq), 0),
+           "mjhip_inverseFDBatchEx")
     if sensors:
       return DfDq, DfDv, DfDa, DmDq, Ds
     return DfDq, DfDv, DfDa, DmDq
@@ -335,14 +349,20 @@ def output_bytes_per_eval(model) -> int:
 
 
 # ---------------------------------------------------------------- single-instance drop-ins
-_structs = {}
+# The model struct is rebuilt per call (its option block is a copy), so edits of the Model
+# between calls are seen; the library caches device state by the model's content.
 
 
 def _cm(m):
-  key = id(m)
-  if key not in _structs:
-    _structs[key] = (m, host.model_struct(m))
-  return _structs[key][1]
+  return host.model_struct(m)
+
+
+def _out(a, n, what):
+  """A caller's float64 output vector, written in place (no silent copies)."""
+  if not (isinstance(a, np.ndarray) and a.dtype == np.float64 and a.flags.c_contiguous
+          and a.size >= n):
+    raise MJHIPError(f"{what}: expected a C-contiguous float64 array of {n} values")
+  return a.ctypes.data_as(_D)
 
 
 def mj_inverse(m, d: host.MjData):
@@ -351,14 +371,55 @@ def mj_inverse(m, d: host.MjData):
 
 
 def mj_inverseSkip(m, d: host.MjData, skipstage: int, skipsensor: int):
-  """mj_inverseSkip (engine_inverse.c:197) on the GPU."""
+  """mj_inverseSkip (engine_inverse.c:197) on the GPU: reads the skipped stages' fields and
+  constraint rows from d, writes the outputs and rows of the stages that ran."""
   lib().mjhip_inverseSkip(ctypes.byref(_cm(m)), d.ptr(), skipstage, skipsensor)
 
 
+def mj_invPosition(m, d: host.MjData):
+  """mj_invPosition (engine_inverse.c:37-68): position stage only."""
+  lib().mjhip_invPosition(ctypes.byref(_cm(m)), d.ptr())
+
+
+def mj_invVelocity(m, d: host.MjData):
+  """mj_invVelocity (engine_inverse.c:73-76): velocity stage only."""
+  lib().mjhip_invVelocity(ctypes.byref(_cm(m)), d.ptr())
+
+
+def mj_invConstraint(m, d: host.MjData):
+  """mj_invConstraint (engine_inverse.c:169-192): qfrc_constraint, efc_force, efc_state."""
+  lib().mjhip_invConstraint(ctypes.byref(_cm(m)), d.ptr())
+
+
 def mj_rne(m, d: host.MjData, flg_acc: int, result):
-  lib().mjhip_rne(ctypes.byref(_cm(m)), d.ptr(), flg_acc,
-                  np.ascontiguousarray(result).ctypes.data_as(_D))
+  """mj_rne (engine_core_smooth.c:1969): result = RNE of d's cdof/cinert/cvel/cdof_dot."""
+  lib().mjhip_rne(ctypes.byref(_cm(m)), d.ptr(), flg_acc, _out(result, m.nv, "mj_rne"))
+
+
+def mj_xfrcAccumulate(m, d: host.MjData, qfrc):
+  """mj_xfrcAccumulate (engine_support.c:1254): qfrc += J' xfrc_applied, in place."""
+  lib().mjhip_xfrcAccumulate(ctypes.byref(_cm(m)), d.ptr(), _out(qfrc, m.nv,
+                                                                   "mj_xfrcAccumulate"))
 
 
 def mj_compareFwdInv(m, d: host.MjData):
+  """mj_compareFwdInv (engine_inverse.c:275-316): fills d.solver_fwdinv."""
   lib().mjhip_compareFwdInv(ctypes.byref(_cm(m)), d.ptr())
+
+
+def mjd_inverseFD(m, d: host.MjData, eps, flg_actuation, DfDq=None, DfDv=None, DfDa=None,
+                  DsDq=None, DsDv=None, DsDa=None, DmDq=None):
+  """mjd_inverseFD (engine_derivative_fd.c:611-719); outputs are filled in place (None to
+  skip), in the reference's transposed layout (nv x nv, nv x nsensordata, nv x nM)."""
+  nv, ns, nM = m.nv, m.sizes.get("nsensordata", 0), m.nM
+  p = lambda a, n, w: None if a is None else _out(a, n, "mjd_inverseFD " + w)
+  lib().mjhip_inverseFD(ctypes.byref(_cm(m)), d.ptr(), float(eps), int(bool(flg_actuation)),
+                        p(DfDq, nv * nv, "DfDq"), p(DfDv, nv * nv, "DfDv"),
+                        p(DfDa, nv * nv, "DfDa"), p(DsDq, nv * ns, "DsDq"),
+                        p(DsDv, nv * ns, "DsDv"), p(DsDa, nv * ns, "DsDa"),
+                        p(DmDq, nv * nM, "DmDq"))
+
+
+def release_model(m):
+  """Release the device state the single-instance calls cached for model m."""
+  lib().mjhip_releaseModel(ctypes.byref(_cm(m)))

@@ -3305,29 +3305,41 @@ static void diff(mjtNum* dx, const mjtNum* x1, const mjtNum* x2, mjtNum h, int n
   for (int i = 0; i < n; i++) dx[i] = inv_h * (x2[i] - x1[i]);
 }
 
-/* engine_derivative_fd.c:611-719 mjd_inverseFD with flg_actuation = 0 */
-void or_inverseFD(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum eps, mjtNum* DfDq,
-                  mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq, mjtNum* DsDv, mjtNum* DsDa,
-                  mjtNum* DmDq) {
+/* engine_derivative_fd.c:160-168: one evaluation, force = qfrc_inverse (- qfrc_actuator of
+ * mj_fwdActuation when flg_actuation) */
+static void fd_eval(const mjhipModel* m, mjhipData* d, orEfc* e, int stage, int skipsensor,
+                    int flg_actuation, mjtNum* force) {
+  or_inverseSkip(m, d, e, stage, skipsensor);
+  mju_copy(force, d->qfrc_inverse, m->nv);
+  if (flg_actuation) {
+    or_fwdActuation(m, d);
+    for (int i = 0; i < m->nv; i++) force[i] -= d->qfrc_actuator[i];
+  }
+}
+
+/* engine_derivative_fd.c:611-719 mjd_inverseFD */
+void or_inverseFDEx(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum eps, int flg_actuation,
+                    mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq, mjtNum* DsDv,
+                    mjtNum* DsDa, mjtNum* DmDq) {
   int nq = m->nq, nv = m->nv, nM = m->nM, ns = m->nsensordata;
   int skipsensor = !DsDq && !DsDv && !DsDa;
   mjtNum* pos = (mjtNum*)malloc(nq*sizeof(mjtNum));
   mjtNum* force = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  mjtNum* force_plus = (mjtNum*)malloc(nv*sizeof(mjtNum));
   mjtNum* sensor = (mjtNum*)malloc((ns + 1)*sizeof(mjtNum));
   mjtNum* mass = (mjtNum*)malloc(nM*sizeof(mjtNum));
   mjtNum* dpos = (mjtNum*)calloc(nv, sizeof(mjtNum));
   mju_copy(pos, d->qpos, nq);
-  or_inverseSkip(m, d, e, mjhipSTAGE_NONE, skipsensor);
-  mju_copy(force, d->qfrc_inverse, nv);
+  fd_eval(m, d, e, mjhipSTAGE_NONE, skipsensor, flg_actuation, force);
   if (!skipsensor) mju_copy(sensor, d->sensordata, ns);
   mju_copy(mass, d->qM, nM);
   if (DfDa || DsDa) {
     for (int i = 0; i < nv; i++) {
       mjtNum tmp = d->qacc[i];
       d->qacc[i] += eps;
-      or_inverseSkip(m, d, e, mjhipSTAGE_VEL, skipsensor);
+      fd_eval(m, d, e, mjhipSTAGE_VEL, skipsensor, flg_actuation, force_plus);
       d->qacc[i] = tmp;
-      if (DfDa) diff(DfDa + i*nv, force, d->qfrc_inverse, eps, nv);
+      if (DfDa) diff(DfDa + i*nv, force, force_plus, eps, nv);
       if (DsDa) diff(DsDa + i*ns, sensor, d->sensordata, eps, ns);
     }
   }
@@ -3335,9 +3347,9 @@ void or_inverseFD(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum eps, mjtNu
     for (int i = 0; i < nv; i++) {
       mjtNum tmp = d->qvel[i];
       d->qvel[i] += eps;
-      or_inverseSkip(m, d, e, mjhipSTAGE_POS, skipsensor);
+      fd_eval(m, d, e, mjhipSTAGE_POS, skipsensor, flg_actuation, force_plus);
       d->qvel[i] = tmp;
-      if (DfDv) diff(DfDv + i*nv, force, d->qfrc_inverse, eps, nv);
+      if (DfDv) diff(DfDv + i*nv, force, force_plus, eps, nv);
       if (DsDv) diff(DsDv + i*ns, sensor, d->sensordata, eps, ns);
     }
   }
@@ -3346,15 +3358,45 @@ void or_inverseFD(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum eps, mjtNu
       mju_zero(dpos, nv);
       dpos[i] = 1;
       mj_integratePos(m, d->qpos, dpos, eps);
-      or_inverseSkip(m, d, e, mjhipSTAGE_NONE, skipsensor);
+      fd_eval(m, d, e, mjhipSTAGE_NONE, skipsensor, flg_actuation, force_plus);
       mju_copy(d->qpos, pos, nq);
-      if (DfDq) diff(DfDq + i*nv, force, d->qfrc_inverse, eps, nv);
+      if (DfDq) diff(DfDq + i*nv, force, force_plus, eps, nv);
       if (DsDq) diff(DsDq + i*ns, sensor, d->sensordata, eps, ns);
       if (DmDq) diff(DmDq + i*nM, mass, d->qM, eps, nM);
     }
   }
   /* like the reference, d keeps the outputs of the last perturbed evaluation */
-  free(pos); free(force); free(sensor); free(mass); free(dpos);
+  free(pos); free(force); free(force_plus); free(sensor); free(mass); free(dpos);
+}
+
+void or_inverseFD(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum eps, mjtNum* DfDq,
+                  mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq, mjtNum* DsDv, mjtNum* DsDa,
+                  mjtNum* DmDq) {
+  or_inverseFDEx(m, d, e, eps, 0, DfDq, DfDv, DfDa, DsDq, DsDv, DsDa, DmDq);
+}
+
+/* engine_inverse.c:275-316 mj_compareFwdInv: with rows from a forward pass in e, the
+ * inverse of the forward qacc against the forward constraint force and applied forces */
+void or_compareFwdInv(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  int nv = m->nv, nefc = e->nefc;
+  d->solver_fwdinv[0] = d->solver_fwdinv[1] = 0;
+  if (!nefc) return;
+  mjtNum* qforce = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  mjtNum* dif = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  mjtNum* save_qfrc_constraint = (mjtNum*)malloc(nv*sizeof(mjtNum));
+  mjtNum* save_efc_force = (mjtNum*)malloc(nefc*sizeof(mjtNum));
+  for (int i = 0; i < nv; i++) qforce[i] = d->qfrc_applied[i] + d->qfrc_actuator[i];
+  or_xfrcAccumulate(m, d, qforce);
+  mju_copy(save_qfrc_constraint, d->qfrc_constraint, nv);
+  mju_copy(save_efc_force, e->efc_force, nefc);
+  or_inverseSkip(m, d, e, mjhipSTAGE_VEL, 1);
+  for (int i = 0; i < nv; i++) dif[i] = save_qfrc_constraint[i] - d->qfrc_constraint[i];
+  d->solver_fwdinv[0] = mju_norm(dif, nv);
+  for (int i = 0; i < nv; i++) dif[i] = qforce[i] - d->qfrc_inverse[i];
+  d->solver_fwdinv[1] = mju_norm(dif, nv);
+  mju_copy(d->qfrc_constraint, save_qfrc_constraint, nv);
+  mju_copy(e->efc_force, save_efc_force, nefc);
+  free(qforce); free(dif); free(save_qfrc_constraint); free(save_efc_force);
 }
 
 /*============================ CPU baseline =================================================*/

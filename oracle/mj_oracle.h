@@ -96,6 +96,14 @@ void or_rungeKutta4(const mjhipModel* m, mjhipData* d, orEfc* efc);
 void or_inverseFD(const mjhipModel* m, mjhipData* d, orEfc* efc, mjtNum eps,
                   mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq, mjtNum* DsDv,
                   mjtNum* DsDa, mjtNum* DmDq);
+/* the same with the reference's flg_actuation (force = qfrc_inverse - qfrc_actuator of
+ * mj_fwdActuation, engine_derivative_fd.c:160-168; d->ctrl is the control) */
+void or_inverseFDEx(const mjhipModel* m, mjhipData* d, orEfc* efc, mjtNum eps,
+                    int flg_actuation, mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq,
+                    mjtNum* DsDv, mjtNum* DsDa, mjtNum* DmDq);
+
+/* mj_compareFwdInv (engine_inverse.c:275-316) on the rows in efc (a forward pass's) */
+void or_compareFwdInv(const mjhipModel* m, mjhipData* d, orEfc* efc);
 
 /* CPU baseline: B instances of mj_inverse over `nthread` threads, one data per thread,
  * static chunks of B/(10*nthread) (python/mujoco/rollout.cc:307-317). Returns seconds. */

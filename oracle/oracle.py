@@ -73,6 +73,9 @@ def lib():
     L.or_xfrcAccumulate.argtypes = [M, Dp, _D]
     L.or_rungeKutta4.argtypes = [M, Dp, E]
     L.or_inverseFD.argtypes = [M, Dp, E, ctypes.c_double, _D, _D, _D, _D, _D, _D, _D]
+    L.or_inverseFDEx.argtypes = [M, Dp, E, ctypes.c_double, ctypes.c_int, _D, _D, _D, _D, _D,
+                                 _D, _D]
+    L.or_compareFwdInv.argtypes = [M, Dp, E]
     L.or_inverseBatch.argtypes = [M, ctypes.c_int, _D, _D, _D, _D, ctypes.c_int]
     L.or_inverseBatch.restype = ctypes.c_double
     _lib = L
@@ -177,7 +180,35 @@ class Oracle:
       return self._efc_arrays[name][:self.efc.nefc * k]
     return self._efc_int[name][:self.efc.nefc]
 
-  def inverse_fd(self, eps=1e-6, dmdq=False, sensors=False):
+  def rne(self, flg_acc):
+    """mj_rne of the data's current cdof/cinert/cvel/cdof_dot/qvel/qacc."""
+    out = np.zeros(self.m.nv)
+    self.L.or_rne(ctypes.byref(self.cm), ctypes.byref(self.d.struct), flg_acc, _p(out))
+    return out
+
+  def compare_fwd_inv(self):
+    """mj_compareFwdInv on the rows of the last call; returns solver_fwdinv."""
+    self.L.or_compareFwdInv(*self._args())
+    return self.d.solver_fwdinv
+
+  def export(self, d, rows=True):
+    """Copy this data's fields (and, with rows, its constraint rows and contacts) into a
+    product MjData d, as a forward pass would leave them for the single-instance calls."""
+    for f in fields.DATA_FIELDS + fields.FORWARD_FIELDS + fields.AUX_FIELDS:
+      src, dst = getattr(self.d, f.name), getattr(d, f.name)
+      dst[:] = src
+    d.struct.time = self.d.struct.time
+    if not rows:
+      return
+    e = self.efc
+    arrays = {}
+    for f in fields.EFC_FIELDS:
+      arrays[f.name] = self.efc_field(f.name)
+    for f in fields.CONTACT_FIELDS:
+      arrays[f.name] = self.contact_field(f.name)
+    d.set_rows(nefc=e.nefc, ne=e.ne, nf=e.nf, nl=e.nl, ncon=e.ncon, **arrays)
+
+  def inverse_fd(self, eps=1e-6, dmdq=False, sensors=False, flg_actuation=False):
     """mjd_inverseFD: (DfDq, DfDv, DfDa, DmDq), plus (DsDq, DsDv, DsDa) when sensors."""
     nv, nM, ns = self.m.nv, self.m.nM, self.m.sizes.get("nsensordata", 0)
     DfDq = np.zeros((nv, nv))
@@ -185,8 +216,8 @@ class Oracle:
     DfDa = np.zeros((nv, nv))
     DmDq = np.zeros((nv, nM)) if dmdq else None
     Ds = [np.zeros((nv, max(ns, 1))) for _ in range(3)] if sensors else [None] * 3
-    self.L.or_inverseFD(*self._args(), eps, _p(DfDq), _p(DfDv), _p(DfDa), *map(_p, Ds),
-                        _p(DmDq))
+    self.L.or_inverseFDEx(*self._args(), eps, int(bool(flg_actuation)), _p(DfDq), _p(DfDv),
+                          _p(DfDa), *map(_p, Ds), _p(DmDq))
     if sensors:
       return DfDq, DfDv, DfDa, DmDq, tuple(x[:, :ns] for x in Ds)
     return DfDq, DfDv, DfDa, DmDq

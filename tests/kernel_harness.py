@@ -25,8 +25,11 @@ def lib():
     os.makedirs(BUILD, exist_ok=True)
     if not os.path.exists(SO) or any(os.path.getmtime(s) > os.path.getmtime(SO) for s in SRC):
       # -ffp-contract=off: same rounding as the oracle's scalar C build
+      # built under a private name and renamed: parallel test workers never see half a file
+      tmp = f"{SO}.{os.getpid()}"
       subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fPIC", "-shared",
-                      "-o", SO, SRC[0]], check=True)
+                      "-o", tmp, SRC[0]], check=True)
+      os.replace(tmp, SO)
     L = ctypes.CDLL(SO)
     L.kh_sizes.restype = None
     L.kh_sizes.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int,

@@ -35,10 +35,15 @@ def build(m, name):
   inc = os.path.join(BUILD, f"gen_{name}_{tag}.inc")
   so = os.path.join(BUILD, f"libcg_{name}_{tag}.so")
   if not os.path.exists(so):
+    # private file names, then an atomic rename (parallel test workers)
+    inc = f"{inc}.{os.getpid()}"
     open(inc, "w").write(src)
+    tmp = f"{so}.{os.getpid()}"
     subprocess.run(["g++", "-std=c++17", "-O1", "-ffp-contract=off", "-fPIC", "-shared",
-                    f'-DGEN_INC="{inc}"', f"-DFAST_BODY=fast_body_{name}", "-o", so,
+                    f'-DGEN_INC="{inc}"', f"-DFAST_BODY=fast_body_{name}", "-o", tmp,
                     os.path.join(HERE, "codegen_harness.cpp")], check=True)
+    os.replace(tmp, so)
+    os.remove(inc)
   L = ctypes.CDLL(so)
   L.cg_run.restype = ctypes.c_int
   L.cg_run.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4 + \

@@ -203,3 +203,59 @@ def test_bias_matches_euler_lagrange(humanoid):
     # the Lagrangian identity holds in the hinge coordinates (dofs 6..)
     lag = Mdot_v - dT + dV
     np.testing.assert_allclose(bias[6:], lag[6:], rtol=2e-5, atol=2e-5)
+
+
+@pytest.mark.parametrize("contacts", [False, True])
+def test_compare_fwd_inv_constrained(contacts, rng):
+  """mj_compareFwdInv (engine_inverse.c:275-316) with constraint rows: applied forces chosen
+  so that the step's qacc is their forward solution (soft constraints make the forward
+  problem's solution unique and the inverse its exact inverse) give solver_fwdinv ~ 0 on
+  limit and contact rows; a perturbed forward constraint force shows up in fwdinv[0] only,
+  and the forward qfrc_constraint / efc_force are restored."""
+  from mujoco_inversedynamicstest_amd import models
+  from mujoco_inversedynamicstest_amd.sampler import sample_contact_states
+  m = models.load("humanoid", disable_contact=not contacts)
+  q, v, a = (sample_contact_states(m, 12, first=40) if contacts else
+             sample_states(m, 12, first=5000, margin=-0.25, resample_tendons=False))
+  o = Oracle(m)
+  rows = 0
+  for i in range(12):
+    o.d.qfrc_actuator[:] = 0.4 * (rng.random(m.nv) - 0.5)
+    o.d.xfrc_applied[:] = 0.8 * (rng.random(6 * m.nbody) - 0.5)
+    f = o.inverse(q[i], v[i], a[i])
+    jx = np.zeros(m.nv)
+    o.xfrc_accumulate(jx)
+    o.d.qfrc_applied[:] = f - o.d.qfrc_actuator - jx
+    rows += o.efc.nefc
+    fw = o.compare_fwd_inv()
+    if o.efc.nefc:
+      assert fw.max() < 1e-9 * max(1, np.abs(f).max())
+    dq = 1e-3 * (rng.random(m.nv) - 0.5)
+    qc = o.d.qfrc_constraint + dq
+    o.d.qfrc_constraint[:] = qc
+    force = o.efc_field("efc_force").copy()
+    fw = o.compare_fwd_inv()
+    if o.efc.nefc:
+      assert abs(fw[0] - np.linalg.norm(dq)) < 1e-12 * max(1, np.abs(qc).max()) and fw[1] < 1e-9 * max(1, np.abs(f).max())
+    np.testing.assert_array_equal(o.d.qfrc_constraint, qc)
+    np.testing.assert_array_equal(o.efc_field("efc_force"), force)
+  assert rows > 12
+
+
+def test_inverse_fd_flg_actuation():
+  """mjd_inverseFD(flg_actuation=1) (engine_derivative_fd.c:160-168) on the slider-crank:
+  actuator forces do not depend on qacc (DfDa unchanged up to the rounding of subtracting the
+  same qfrc_actuator from both forces), and the position
+  derivative moves by -d(qfrc_actuator)/dqpos (the transmission's moment depends on qpos)."""
+  from mujoco_inversedynamicstest_amd import models
+  m = models.load("slider_crank", disable_contact=True)
+  q, v, a = sample_states(m, 3, first=2)
+  o = Oracle(m)
+  for i in range(3):
+    o.d.ctrl[:] = np.linspace(-0.5, 0.5, m.nu)
+    o.set_state(q[i], v[i], a[i])
+    f0 = o.inverse_fd(1e-6)
+    o.set_state(q[i], v[i], a[i])
+    f1 = o.inverse_fd(1e-6, flg_actuation=True)
+    np.testing.assert_allclose(f0[2], f1[2], rtol=0, atol=1e-9)
+    assert np.abs(f0[0] - f1[0]).max() > 1e-6
