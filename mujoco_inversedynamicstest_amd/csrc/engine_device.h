@@ -189,6 +189,11 @@ struct Lane {
   // positions, and LDS turns those loads from memory round trips into LDS latency
   SP<S> gxpos;
   bool gstage;
+  // cooperative constraint kernel only (else nullptr), per-instance LDS copies: cdq[8*j+c]
+  // holds cdof (c < 6), qvel (c = 6) and qacc (c = 7) of dof j for the contact rows; fst[r]
+  // receives efc_force[r] as a row is finished, for the J'force pass
+  const double* cdq;
+  double* fst;
 };
 
 // chain[k] for body k (the fused path's ancestor test, one bit per body)
@@ -1021,33 +1026,33 @@ template <int S, bool WRITE = true>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
                                double margin, int& ncon, int* status);
 
-template <int S, bool WRITE = true>
-MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, int& ncon,
-                         int* status) {
+// mj_collideGeoms up to the narrowphase: type-orders (g1, g2), applies the static and
+// bounding-sphere filters and returns the raw contacts of a primitive pair in raw (<= 2,
+// with the pair's margin), 0 for none, or -1 for plane : box / cylinder, whose contacts
+// collidePlaneBoxCyl stores as it makes them
+template <int S>
+MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
+                       double& margin, RawContact raw[2], int* status) {
   if (m.geom_type[g1] > m.geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   const int kmax = mjhip_pairMaxContacts(t1, t2);
-  if (kmax == 0) return;
+  if (kmax == 0) return 0;
   if (mjhip_filterBitmask(m.geom_contype[g1], m.geom_conaffinity[g1], m.geom_contype[g2],
                           m.geom_conaffinity[g2])) {
-    return;
+    return 0;
   }
   const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
-  double margin = ovr ? m.opt.o_margin : (m.geom_margin[g1] > m.geom_margin[g2] ?
-                                          m.geom_margin[g1] : m.geom_margin[g2]);
-  if (filterSphere(m, d, g1, g2, margin)) return;
+  margin = ovr ? m.opt.o_margin : (m.geom_margin[g1] > m.geom_margin[g2] ?
+                                   m.geom_margin[g1] : m.geom_margin[g2]);
+  if (filterSphere(m, d, g1, g2, margin)) return 0;
   if (kmax < 0) {                       // the reference would run a function not built here
     *status |= MJHIP_INST_UNSUPPORTED;
-    return;
+    return 0;
   }
-  if (t1 == mjhipGEOM_PLANE && (t2 == mjhipGEOM_BOX || t2 == mjhipGEOM_CYLINDER)) {
-    collidePlaneBoxCyl<S, WRITE>(m, d, g1, g2, margin, ncon, status);
-    return;
-  }
+  if (t1 == mjhipGEOM_PLANE && (t2 == mjhipGEOM_BOX || t2 == mjhipGEOM_CYLINDER)) return -1;
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
   SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
   const double *size1 = m.geom_size + 3*g1, *size2 = m.geom_size + 3*g2;
-  RawContact raw[2];
   int num = 0;
   if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) {
     num = rawPlaneSphere(raw, margin, pos1, mat1, pos2, size2[0]);
@@ -1062,11 +1067,14 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
   } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {
     num = colCapsuleCapsule(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
   }
-  if (!num) return;
-  if constexpr (!WRITE) {
-    ncon += num;
-    return;
-  }
+  return num;
+}
+
+// mj_setContact (:1387-1415) for a primitive pair's raw contacts at contact index ncon on
+template <int S>
+MJH_HD void setContacts(const mjhipModel& m, const Lane<S>& d, int g1, int g2, double margin,
+                        const RawContact raw[2], int num, int& ncon, int* status) {
+  const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
   int condim;
   double gap, solref[2], solimp[5], friction[5];
   contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
@@ -1103,6 +1111,26 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
   };
   if (store(raw[0]) && num > 1) store(raw[1]);   // num <= 2; constant indices keep raw[]
 }                                                // in registers
+
+// mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
+// WRITE = false only counts the contacts the pair produces
+template <int S, bool WRITE = true>
+MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, int& ncon,
+                         int* status) {
+  double margin = 0;
+  RawContact raw[2];
+  const int num = narrowGeoms(m, d, g1, g2, margin, raw, status);
+  if (num < 0) {
+    collidePlaneBoxCyl<S, WRITE>(m, d, g1, g2, margin, ncon, status);
+    return;
+  }
+  if (!num) return;
+  if constexpr (!WRITE) {
+    ncon += num;
+    return;
+  }
+  setContacts(m, d, g1, g2, margin, raw, num, ncon, status);
+}
 
 // plane : box / cylinder (up to 4 contacts each): contacts are stored as they are made
 template <int S, bool WRITE>
@@ -2130,13 +2158,16 @@ MJH_HD void finishRowFused(const Lane<S>& d, int r, int tp, const double kb[4], 
     state = CNSTRSTATE_SATISFIED;
   }
   d.efc_force[r] = force;
+  if (d.fst) d.fst[r] = force;
   d.efc_state[r] = state;
 }
 
 // a friction or limit row just added at r (few per instance: its J row is read back)
+// (vel, acc = J*qvel, J*qacc of the row, already formed)
 template <int S>
-MJH_HD void finishNonContact(const mjhipModel& m, const Lane<S>& d, int r, int tp, int id,
-                             double pos, double margin, double frictionloss) {
+MJH_HD void finishNonContactVA(const mjhipModel& m, const Lane<S>& d, int r, int tp, int id,
+                               double pos, double margin, double frictionloss, double vel,
+                               double acc) {
   const double diag = tp == CNSTR_FRICTION_DOF ? m.dof_invweight0[id] :
                       (tp == CNSTR_LIMIT_JOINT ? m.dof_invweight0[m.jnt_dofadr[id]] :
                        m.tendon_invweight0[id]);
@@ -2144,10 +2175,28 @@ MJH_HD void finishNonContact(const mjhipModel& m, const Lane<S>& d, int r, int t
   rowSolParam(m, tp, id, solref, solimp);
   rowImpedance(m, tp, solref, solimp, pos, margin, kb);
   const double R = dmax(MINVAL, (1-kb[2])*diag/kb[2]);
-  SP<S> J = d.efc_J + r*m.nv;
-  finishRowFused(d, r, tp, kb, R, pos, margin, frictionloss, dot(J, d.qvel, m.nv),
-                 dot(J, d.qacc, m.nv));
+  finishRowFused(d, r, tp, kb, R, pos, margin, frictionloss, vel, acc);
 }
+
+template <int S>
+MJH_HD void finishNonContact(const mjhipModel& m, const Lane<S>& d, int r, int tp, int id,
+                             double pos, double margin, double frictionloss) {
+  SP<S> J = d.efc_J + r*m.nv;
+  finishNonContactVA(m, d, r, tp, id, pos, margin, frictionloss, dot(J, d.qvel, m.nv),
+                     dot(J, d.qacc, m.nv));
+}
+
+// indexable views for dot(): a generator of row values, and a strided (LDS) column
+template <class F>
+struct FnIdx {
+  F f;
+  MJH_HD double operator[](int k) const { return f(k); }
+};
+template <int STRIDE>
+struct StridedIdx {
+  const double* p;
+  MJH_HD double operator[](int k) const { return p[k*STRIDE]; }
+};
 
 // One contact's rows (condim DIM) at efc row `nefc`. As instantiateContact, the rows are
 // formed dof by dof straight into efc_J, here in blocks of four dofs whose loads (cdof,
@@ -2211,7 +2260,14 @@ MJH_HD void contactRowsFused(const mjhipModel& m, const Lane<S>& d, int i, int n
 #pragma unroll
     for (int k = 0; k < BLK; k++) {
       const int j = jb + k;
-      if (j < nv) {
+      if (j < nv && d.cdq) {            // the cooperative kernel's LDS copy
+        const double* p = d.cdq + 8*j;
+        for (int c = 0; c < 6; c++) cd[k][c] = p[c];
+        if constexpr (REG) {
+          qv[k] = p[6];
+          qa[k] = p[7];
+        }
+      } else if (j < nv) {
         for (int c = 0; c < 6; c++) cd[k][c] = d.cdof[6*j+c];
         if constexpr (REG) {
           qv[k] = d.qvel[j];
@@ -3887,6 +3943,8 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
   d.chain = nullptr;
   d.gxpos = d.geom_xpos;
   d.gstage = false;
+  d.cdq = nullptr;
+  d.fst = nullptr;
   return d;
 }
 

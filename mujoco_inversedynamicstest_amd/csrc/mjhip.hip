@@ -140,6 +140,12 @@ __device__ __forceinline__ void rowFields(const Lane<S>& d, int r, double pos, d
   d.efc_id[r] = id;
 }
 
+// dynamic LDS of k_constraint_coop: per instance 8 nv doubles (cdof, qvel, qacc), qpos and
+// efc_cap row forces
+static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap) {
+  return (unsigned)((64 / G) * (8*m.nv + m.nq + efc_cap) * sizeof(double));
+}
+
 template <int G, bool CONTACT, bool LIST>
 __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr, int B,
                                                         const int* __restrict__ worklist,
@@ -154,30 +160,58 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   __shared__ unsigned long long chain[64];
   if ((int)threadIdx.x < m.nbody) chain[threadIdx.x] = mjh::chainMask(m, threadIdx.x);
   __syncthreads();
-  const int sub = threadIdx.x % G;
-  const long g = (long)blockIdx.x*IPB + threadIdx.x / G;
+  const int sub = threadIdx.x % G, slot = threadIdx.x / G;
+  const long g = (long)blockIdx.x*IPB + slot;
   const bool active = g < n;                // uniform within a group
   const long inst = active ? (LIST ? (long)worklist[g] : g) : 0;
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
   d.chain = chain;
   const int nv = m.nv, dsbl = m.opt.disableflags;
   int st = 0, ncon = 0;
+  MJH_PHASE(14);
+  // per-instance LDS (dynamic, coopLdsBytes): cdof/qvel/qacc for the contact rows, staged by
+  // the group while collision runs, and the row forces for J'force
+  const int nq = m.nq, per = 8*nv + nq;
+  double* cdq = g_gstage + (long)slot*per;
+  double* qp = cdq + 8*nv;
+  double* fst = g_gstage + (long)IPB*per + (long)slot*d.efc_cap;
+  if (active) {
+    for (int e = sub; e < 8*nv; e += G) {
+      const int j = e >> 3, c = e & 7;
+      cdq[e] = c < 6 ? d.cdof[6*j+c] : (c == 6 ? d.qvel[j] : d.qacc[j]);
+    }
+    for (int e = sub; e < nq; e += G) qp[e] = d.qpos[e];
+  }
+  d.cdq = cdq;
+  d.fst = fst;
 
   // ---- mj_collision over the static pair program
   if (CONTACT && active && mjhip_contactsEnabled(&m)) {
     for (int p0 = 0; p0 < npair; p0 += G) {
       const int p = p0 + sub;
-      int2 pr = make_int2(0, 0);
-      int cnt = 0;
-      if (p < npair) {
-        pr = pairs[p];
-        mjh::collideGeoms<64, false>(m, d, pr.x, pr.y, cnt, &st);
+      int g1 = 0, g2 = 0, num = 0, cnt = 0;
+      double margin = 0;
+      mjh::RawContact raw[2];
+      if (p < npair) {                      // narrowphase once: raw contacts kept in registers
+        const int2 pr = pairs[p];
+        g1 = pr.x;
+        g2 = pr.y;
+        num = mjh::narrowGeoms<64>(m, d, g1, g2, margin, raw, &st);
+        if (num < 0) {                      // plane : box / cylinder counts, then stores
+          mjh::collidePlaneBoxCyl<64, false>(m, d, g1, g2, margin, cnt, &st);
+        } else {
+          cnt = num;
+        }
       }
       int total;
       const int excl = groupScan<G>(cnt, sub, &total) - cnt;
       if (cnt) {
         int c = ncon + excl;
-        mjh::collideGeoms<64, true>(m, d, pr.x, pr.y, c, &st);
+        if (num < 0) {
+          mjh::collidePlaneBoxCyl<64, true>(m, d, g1, g2, margin, c, &st);
+        } else {
+          mjh::setContacts<64>(m, d, g1, g2, margin, raw, num, c, &st);
+        }
       }
       ncon += total;
     }
@@ -185,6 +219,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   if (active && sub == 0) d.con_count[0] = ncon < d.con_cap ? ncon : d.con_cap;
   if (ncon > d.con_cap) ncon = d.con_cap;
   __syncthreads();                          // contacts visible to every lane of the group
+  MJH_PHASE(15);
 
   // ---- mj_makeConstraint: non-contact rows, then contact rows (all finished at creation)
   mjh::RowCount rc;
@@ -206,7 +241,12 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         mjh::SP<64> J = d.efc_J + (long)r*nv;
         for (int k = 0; k < nv; k++) J[k] = jval(k);
         rowFields(d, r, pos, margin, floss, tp, id);
-        mjh::finishNonContact(m, d, r, tp, id, pos, margin, floss);
+        // J*qvel, J*qacc from the row's generator and the LDS copies (the values stored in
+        // efc_J, in mju_dot's order), not read back from memory
+        const mjh::FnIdx<decltype(jval)> jv{jval};
+        mjh::finishNonContactVA(m, d, r, tp, id, pos, margin, floss,
+                                mjh::dot(jv, mjh::StridedIdx<8>{cdq + 6}, nv),
+                                mjh::dot(jv, mjh::StridedIdx<8>{cdq + 7}, nv));
       }
       rc.nefc++;
       return true;
@@ -226,7 +266,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         const double margin = m.jnt_margin[i];
         const int t = m.jnt_type[i], da = m.jnt_dofadr[i];
         if (t == mjhipJNT_SLIDE || t == mjhipJNT_HINGE) {
-          const double value = d.qpos[m.jnt_qposadr[i]];
+          const double value = qp[m.jnt_qposadr[i]];
           for (int side = -1; side <= 1; side += 2) {
             const double dist = side * (m.jnt_range[2*i+(side+1)/2] - value);
             if (dist < margin &&
@@ -237,7 +277,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
           }
         } else if (t == mjhipJNT_BALL) {
           const int adr = m.jnt_qposadr[i];
-          double quat[4] = {d.qpos[adr], d.qpos[adr+1], d.qpos[adr+2], d.qpos[adr+3]};
+          double quat[4] = {qp[adr], qp[adr+1], qp[adr+2], qp[adr+3]};
           double aa[3];
           mjh::normalize4(quat);
           mjh::quat2Vel(aa, quat, 1);
@@ -255,10 +295,13 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         if (!m.tendon_limited[i]) continue;
         const double value = d.ten_length[i], margin = m.tendon_margin[i];
         mjh::SP<64> tj = d.ten_J + (long)i*nv;
-        bool nonempty = false;
-        for (int k = 0; k < nv && !nonempty; k++) nonempty = tj[k] != 0;
+        int nonempty = -1;                  // ten_J row scanned only for an active side
         for (int side = -1; side <= 1; side += 2) {
           const double dist = side * (m.tendon_range[2*i+(side+1)/2] - value);
+          if (dist < margin && nonempty < 0) {
+            nonempty = 0;
+            for (int k = 0; k < nv && !nonempty; k++) nonempty = tj[k] != 0;
+          }
           if (dist < margin && nonempty &&
               addRow([&](int k) { return tj[k]*(double)(-side); }, dist, margin, 0,
                      mjh::CNSTR_LIMIT_TENDON, i)) {
@@ -267,6 +310,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         }
       }
     }
+    MJH_PHASE(18);
     // contact rows (pyramidal or frictionless: the fused path excludes elliptic cones)
     if (CONTACT && !(dsbl & mjhipDSBL_CONTACT) && nv) {
       int nef = rc.nefc;
@@ -302,23 +346,47 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
     d.efc_count[3] = rc.nl;
   }
   __syncthreads();                          // rows and forces visible to every lane
+  MJH_PHASE(16);
 
-  // ---- qfrc_constraint = J'force (column-parallel) and the mj_inverse assembly
+  // ---- qfrc_constraint = J'force (column-parallel, two columns per lane per pass, eight
+  // rows' loads in flight; forces from LDS) and the mj_inverse assembly
   if (active) {
     const int nefc = rc.nefc;
-    for (int j = sub; j < nv; j += G) {
-      double acc = 0;
-      for (int r = 0; r < nefc; r++) {
-        const double f = d.efc_force[r];
-        if (f) acc += d.efc_J[(long)r*nv + j]*f;
+    for (int j0 = sub; j0 < nv; j0 += 2*G) {
+      const int j1 = j0 + G;
+      const bool has1 = j1 < nv;
+      double acc0 = 0, acc1 = 0;
+      for (int r0 = 0; r0 < nefc; r0 += 8) {
+        double f[8], x0[8], x1[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) f[u] = r0 + u < nefc ? fst[r0+u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+          mjh::SP<64> Jr = d.efc_J + (long)(r0 + u)*nv;
+          x0[u] = f[u] != 0 ? Jr[j0] : 0.0;
+          x1[u] = (f[u] != 0 && has1) ? Jr[j1] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; u++) {   // mju_mulMatTVec's row order, zero forces skipped
+          if (f[u] != 0) {
+            acc0 += x0[u]*f[u];
+            acc1 += x1[u]*f[u];
+          }
+        }
       }
-      d.qfrc_constraint[j] = acc;
-      d.qfrc_inverse[j] += m.dof_armature[j] * d.qacc[j] - d.qfrc_passive[j] - acc;
-      if (qfrc_out) qfrc_out[inst*nv + j] = d.qfrc_inverse[j];
+      d.qfrc_constraint[j0] = acc0;
+      d.qfrc_inverse[j0] += m.dof_armature[j0] * d.qacc[j0] - d.qfrc_passive[j0] - acc0;
+      if (qfrc_out) qfrc_out[inst*nv + j0] = d.qfrc_inverse[j0];
+      if (has1) {
+        d.qfrc_constraint[j1] = acc1;
+        d.qfrc_inverse[j1] += m.dof_armature[j1] * d.qacc[j1] - d.qfrc_passive[j1] - acc1;
+        if (qfrc_out) qfrc_out[inst*nv + j1] = d.qfrc_inverse[j1];
+      }
     }
     for (int o = G/2; o; o >>= 1) st |= __shfl_xor(st, o, G);
     if (sub == 0 && status && st) status[inst] |= st;
   }
+  MJH_PHASE(17);
 }
 
 // Status checks of the straight-line path: mj_checkPos/Vel/Acc (engine_forward.c:53-102)
@@ -874,7 +942,7 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   // 8 or 16, 0 = the one-lane k_constraint)
   if (const char* lanes = getenv("MJHIP_COOP_LANES")) {
     const int v = atoi(lanes);
-    c->coop = (v == 0 || v == 8 || v == 16) ? v : 16;
+    c->coop = (v == 0 || v == 8 || v == 16 || v == 32) ? v : 16;
   }
   if (c->con_cap > 0) {
     std::vector<int2> pairs = collision_pairs(m);
@@ -960,13 +1028,19 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
       const bool contact = c->con_cap > 0, list = c->fast->cmode == 1;
 #define MJHIP_LAUNCH_COOP(G, C, L)                                                            \
       hipLaunchKernelGGL((k_constraint_coop<G, C, L>), dim3((B + 64/G - 1) / (64/G)),         \
-                         dim3(64), 0, c->stream, c->dmodel, c->mirror, B, wl,                 \
+                         dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap), c->stream,         \
+                         c->dmodel, c->mirror, B, wl,                                         \
                          (const int*)cnt, c->pairs, c->npair, qfrc, status)
       if (c->coop == 8) {
         if (contact) { if (list) MJHIP_LAUNCH_COOP(8, true, true);
                        else MJHIP_LAUNCH_COOP(8, true, false); }
         else { if (list) MJHIP_LAUNCH_COOP(8, false, true);
                else MJHIP_LAUNCH_COOP(8, false, false); }
+      } else if (c->coop == 32) {
+        if (contact) { if (list) MJHIP_LAUNCH_COOP(32, true, true);
+                       else MJHIP_LAUNCH_COOP(32, true, false); }
+        else { if (list) MJHIP_LAUNCH_COOP(32, false, true);
+               else MJHIP_LAUNCH_COOP(32, false, false); }
       } else {
         if (contact) { if (list) MJHIP_LAUNCH_COOP(16, true, true);
                        else MJHIP_LAUNCH_COOP(16, true, false); }

@@ -1342,13 +1342,45 @@ class MJCFCompiler:
           v = _floats(a["dynprm"])
           adynprm[ai, :len(v)] = v
         na_count += adyn[ai] != 0
-      elif tag == "position":
+      elif tag == "position":          # xml_native_reader.cc:2190-2240
         kp = float(a.get("kp", 1.0))
-        kv = float(a.get("kv", 0.0))
+        kv = float(a.get("kv", -1.0))
+        dampratio = float(a.get("dampratio", -1.0))
+        if "kv" in a and kv < 0:
+          raise MJCFError("kv cannot be negative")
+        if dampratio > 0 and kv > 0:
+          raise MJCFError("kv and dampratio cannot both be defined")
         againprm[ai, 0] = kp
         abias[ai] = 1
         abiasprm[ai, 1] = -kp
-        abiasprm[ai, 2] = -kv
+        if kv > 0:
+          abiasprm[ai, 2] = -kv
+        if dampratio > 0:
+          raise MJCFError("position actuator dampratio (resolved by mj_setConst) is not in "
+                          "the supported subset")
+        inherit = float(a.get("inheritrange", 0.0))
+        if inherit > 0:
+          if "ctrlrange" in a and any(_floats(a["ctrlrange"])):
+            raise MJCFError("ctrlrange and inheritrange cannot both be defined")
+          # mjCActuator::Compile (user_objects.cc:5940-5982): the compiled (radian) range of
+          # the hinge/slide joint or tendon, scaled about its mean
+          if trn[0] in ("joint", "jointinparent"):
+            jt = jtype[atrnid[ai, 0]]
+            if jt not in (JNT["hinge"], JNT["slide"]):
+              raise MJCFError("inheritrange can only be used with hinge and slide joints, "
+                              "actuator")
+            rng = jrange[atrnid[ai, 0]]
+          elif trn[0] == "tendon":
+            rng = trange[atrnid[ai, 0]]
+          else:
+            raise MJCFError("inheritrange can only be used with joint and tendon "
+                            "transmission, actuator")
+          if rng[0] == rng[1]:
+            raise MJCFError(f"inheritrange used but target '{a[trn[0]]}' has no range "
+                            f"defined in actuator {ai}")
+          mean = 0.5 * (rng[1] + rng[0])
+          radius = 0.5 * (rng[1] - rng[0]) * inherit
+          a = dict(a, ctrlrange=f"{float(mean - radius)!r} {float(mean + radius)!r}")
       elif tag == "velocity":
         kv = float(a.get("kv", 1.0))
         againprm[ai, 0] = kv

@@ -7,7 +7,6 @@
  */
 #define _GNU_SOURCE
 #include "mj_oracle.h"
-#include "../include/mjhip_contact.h"
 
 #include <math.h>
 #include <pthread.h>
@@ -1140,9 +1139,6 @@ static void or_passive(const mjhipModel* m, mjhipData* d) {
 
 /*============================ engine_core_constraint.c ====================================*/
 
-int or_efcCapacity(const mjhipModel* m) { return mjhip_efcCapacity(m); }
-
-int or_contactCapacity(const mjhipModel* m) { return mjhip_contactCapacity(m, NULL); }
 
 
 /*============================ engine_collision_*.c =========================================*/
@@ -1507,14 +1503,367 @@ static int or_filterSphere(const mjhipModel* m, const mjhipData* d, int g1, int 
   return 0;
 }
 
+/*---------------- collision driver rules (engine_collision_driver.c), restated here ----------
+ * The oracle keeps its own copy of the driver's static rules and of its broadphase (sweep and
+ * prune in the covariance frame) so that the HIP engine's candidate-pair program
+ * (include/mjhip_contact.h: every statically admissible body pair, brute force) is checked
+ * against the reference's algorithm, not against itself. */
+
+/* filterBitmask :101-105 */
+static int or_filterBitmask(int contype1, int conaffinity1, int contype2, int conaffinity2) {
+  return !(contype1 & conaffinity2) && !(contype2 & conaffinity1);
+}
+
+/* filterBodyPair :165-182 */
+static int or_filterBodyPair(int weldbody1, int weldparent1, int weldbody2, int weldparent2,
+                             int dsbl_filterparent) {
+  if (weldbody1 == weldbody2) return 1;
+  if ((!dsbl_filterparent && weldbody1 != 0 && weldbody2 != 0) &&
+      (weldbody1 == weldparent2 || weldbody2 == weldparent1)) {
+    return 1;
+  }
+  return 0;
+}
+
+/* canCollide :187-195 and canCollide2 :200-210 (bodies only: flex is outside the subset) */
+static int or_canCollide(const mjhipModel* m, int b) {
+  return m->body_contype[b] || m->body_conaffinity[b];
+}
+
+static int or_canCollide2(const mjhipModel* m, int b1, int b2) {
+  return !or_filterBitmask(m->body_contype[b1], m->body_conaffinity[b1], m->body_contype[b2],
+                           m->body_conaffinity[b2]);
+}
+
+/* hasPlane :84-97 */
+static int or_hasPlane(const mjhipModel* m, int b) {
+  for (int g = m->body_geomadr[b]; g < m->body_geomadr[b] + m->body_geomnum[b]; g++) {
+    if (m->geom_type[g] == mjhipGEOM_PLANE) return 1;
+  }
+  return 0;
+}
+
+/* mjCOLLISIONFUNC (:41-52) for type-ordered t1 <= t2: 0 = no function, otherwise the most
+ * contacts the function returns when it is one of the primitives restated here, or -1 for a
+ * function outside the subset (mjc_Convex, mjc_BoxBox, mjc_CapsuleBox, mjc_SphereCylinder,
+ * height fields, SDFs) */
+static int or_collisionFunc(int t1, int t2) {
+  static const int table[9][9] = {
+    /*           PLANE HFIELD SPHERE CAPSULE ELLIPS CYL BOX MESH SDF */
+    /*PLANE  */ {0,    0,     1,     2,      -1,    4,  4,  -1,  -1},
+    /*HFIELD */ {0,    0,     -1,    -1,     -1,    -1, -1, -1,  -1},
+    /*SPHERE */ {0,    0,     1,     1,      -1,    -1, 1,  -1,  -1},
+    /*CAPSULE*/ {0,    0,     0,     2,      -1,    -1, -1, -1,  -1},
+    /*ELLIPS */ {0,    0,     0,     0,      -1,    -1, -1, -1,  -1},
+    /*CYL    */ {0,    0,     0,     0,      0,     -1, -1, -1,  -1},
+    /*BOX    */ {0,    0,     0,     0,      0,     0,  -1, -1,  -1},
+    /*MESH   */ {0,    0,     0,     0,      0,     0,  0,  -1,  -1},
+    /*SDF    */ {0,    0,     0,     0,      0,     0,  0,  0,   -1}};
+  if (t1 < 0 || t2 < 0 || t1 > 8 || t2 > 8) return -1;
+  return table[t1][t2];
+}
+
+/* add_pair :937-990: geom-level (OR over the body's geoms) bitmask check, ordered ids */
+static void or_addPair(const mjhipModel* m, int b1, int b2, int* npair, int* pair) {
+  int ct[2] = {0, 0}, ca[2] = {0, 0}, b[2] = {b1, b2};
+  for (int k = 0; k < 2; k++) {
+    for (int g = m->body_geomadr[b[k]]; g < m->body_geomadr[b[k]] + m->body_geomnum[b[k]];
+         g++) {
+      ct[k] |= m->geom_contype[g];
+      ca[k] |= m->geom_conaffinity[g];
+    }
+  }
+  if (!(ct[0] & ca[1]) && !(ct[1] & ca[0])) return;
+  pair[(*npair)++] = b1 < b2 ? (b1 << 16) + b2 : (b2 << 16) + b1;
+}
+
+/* mju_eig3 (engine_util_solve.c:683-781): Jacobi iterations on a quaternion */
+static void or_eig3(mjtNum eigval[3], mjtNum eigvec[9], const mjtNum mat[9]) {
+  const mjtNum eigEPS = 1e-12;
+  mjtNum quat[4] = {1, 0, 0, 0}, D[9], tmp[9];
+  for (int iter = 0; iter < 500; iter++) {
+    mju_quat2Mat(eigvec, quat);
+    for (int i = 0; i < 3; i++) {         /* tmp = eigvec' * mat (mju_mulMatTMat3) */
+      for (int j = 0; j < 3; j++) {
+        tmp[3*i+j] = eigvec[i]*mat[j] + eigvec[3+i]*mat[3+j] + eigvec[6+i]*mat[6+j];
+      }
+    }
+    for (int i = 0; i < 3; i++) {         /* D = tmp * eigvec (mju_mulMatMat3) */
+      for (int j = 0; j < 3; j++) {
+        D[3*i+j] = tmp[3*i]*eigvec[j] + tmp[3*i+1]*eigvec[3+j] + tmp[3*i+2]*eigvec[6+j];
+      }
+    }
+    eigval[0] = D[0];
+    eigval[1] = D[4];
+    eigval[2] = D[8];
+    int rk, ck, rotk;
+    if (fabs(D[1]) > fabs(D[2]) && fabs(D[1]) > fabs(D[5])) {
+      rk = 0; ck = 1; rotk = 2;
+    } else if (fabs(D[2]) > fabs(D[5])) {
+      rk = 0; ck = 2; rotk = 1;
+    } else {
+      rk = 1; ck = 2; rotk = 0;
+    }
+    if (fabs(D[3*rk+ck]) < eigEPS) break;
+    mjtNum tau = (D[4*ck]-D[4*rk])/(2*D[3*rk+ck]), t;
+    if (tau >= 0) {
+      t = 1.0/(tau + sqrt(1 + tau*tau));
+    } else {
+      t = -1.0/(-tau + sqrt(1 + tau*tau));
+    }
+    mjtNum c = 1.0/sqrt(1 + t*t);
+    if (c > 1.0-eigEPS) break;
+    tmp[1] = tmp[2] = tmp[3] = 0;
+    tmp[rotk+1] = (tau >= 0 ? -sqrt(0.5-0.5*c) : sqrt(0.5-0.5*c));
+    if (rotk == 1) tmp[rotk+1] = -tmp[rotk+1];
+    tmp[0] = sqrt(1.0 - tmp[rotk+1]*tmp[rotk+1]);
+    mju_normalize4(tmp);
+    mju_mulQuat(quat, quat, tmp);
+    mju_normalize4(quat);
+  }
+  /* the broadphase uses only the frame's rows; the reference sorts the eigenpairs in
+   * decreasing order (bubble sort 0, 1, 0, swapping columns and eigenvalues) */
+  for (int j = 0; j < 3; j++) {
+    int j1 = j % 2;
+    if (eigval[j1] + eigEPS < eigval[j1+1]) {
+      mjtNum e = eigval[j1];
+      eigval[j1] = eigval[j1+1];
+      eigval[j1+1] = e;
+      for (int k = 0; k < 3; k++) {
+        mjtNum v = eigvec[3*k+j1];
+        eigvec[3*k+j1] = eigvec[3*k+j1+1];
+        eigvec[3*k+j1+1] = v;
+      }
+    }
+  }
+}
+
+/* makeAAMM :862-895 for a body: geom centers in `frame`, inflated by rbound + margin */
+static void or_makeAAMM(const mjhipModel* m, const mjhipData* d, mjtNum aamm[6], int b,
+                        const mjtNum frame[9]) {
+  for (int i = 0; i < m->body_geomnum[b]; i++) {
+    int g = m->body_geomadr[b] + i;
+    mjtNum margin = mjENABLED(mjhipENBL_OVERRIDE) ? 0.5*m->opt.o_margin : m->geom_margin[g];
+    mjtNum a[6];
+    for (int j = 0; j < 3; j++) {
+      const mjtNum* x = d->geom_xpos + 3*g;
+      mjtNum cen = x[0]*frame[3*j] + x[1]*frame[3*j+1] + x[2]*frame[3*j+2];
+      a[j] = cen - m->geom_rbound[g] - margin;
+      a[j+3] = cen + m->geom_rbound[g] + margin;
+    }
+    if (i == 0) {
+      for (int j = 0; j < 6; j++) aamm[j] = a[j];
+    } else {
+      for (int j = 0; j < 3; j++) {
+        aamm[j] = mjMIN(aamm[j], a[j]);
+        aamm[j+3] = mjMAX(aamm[j+3], a[j+3]);
+      }
+    }
+  }
+}
+
+/* mj_SAP :1006-1100 along axis 0: float keys, stable sort (mjSORT is stable), active list */
+typedef struct { float value; int id_ismax; } orSAP;
+
+static int or_SAP(const mjtNum* aamm, int n, int* pair) {
+  orSAP* sb = (orSAP*)malloc(sizeof(orSAP) * 2 * (n > 0 ? n : 1));
+  orSAP* ab = (orSAP*)malloc(sizeof(orSAP) * 2 * (n > 0 ? n : 1));
+  for (int i = 0; i < n; i++) {
+    sb[2*i].id_ismax = i;
+    sb[2*i].value = (float)aamm[6*i];
+    sb[2*i+1].id_ismax = i + 0x10000;
+    sb[2*i+1].value = (float)aamm[6*i+3];
+  }
+  for (int j = 1; j < 2*n; j++) {         /* stable insertion sort by value */
+    orSAP t = sb[j];
+    int k = j - 1;
+    for (; k >= 0 && sb[k].value > t.value; k--) sb[k+1] = sb[k];
+    sb[k+1] = t;
+  }
+  int cnt = 0, npair = 0;
+  for (int i = 0; i < 2*n; i++) {
+    if (!(sb[i].id_ismax & 0x10000)) {
+      for (int j = 0; j < cnt; j++) {
+        int id1 = ab[j].id_ismax, id2 = sb[i].id_ismax;
+        if (aamm[6*id1+1] > aamm[6*id2+4] || aamm[6*id1+2] > aamm[6*id2+5] ||
+            aamm[6*id2+1] > aamm[6*id1+4] || aamm[6*id2+2] > aamm[6*id1+5]) {
+          continue;
+        }
+        pair[npair++] = (id1 << 16) + id2;
+      }
+      ab[cnt++] = sb[i];
+    } else {
+      int toremove = sb[i].id_ismax & 0xFFFF;
+      for (int j = 0; j < cnt; j++) {
+        if (ab[j].id_ismax == toremove) {
+          for (int k = j; k < cnt - 1; k++) ab[k] = ab[k+1];
+          cnt--;
+          break;
+        }
+      }
+    }
+  }
+  free(sb);
+  free(ab);
+  return npair;
+}
+
+/* mj_broadphase :1148-1286: always-colliding pairs of the world body (or a world-welded body
+ * with a plane), then SAP pairs in the geom covariance frame filtered by weld; the result is
+ * sorted by signature (duplicates are skipped by the caller) */
+static int or_broadphase(const mjhipModel* m, const mjhipData* d, int* pair) {
+  int npair = 0, nbody = m->nbody;
+  int dsbl_filterparent = mjDISABLED(mjhipDSBL_FILTERPARENT);
+  for (int b1 = 0; b1 < nbody; b1++) {
+    if (!or_canCollide(m, b1)) continue;
+    if ((b1 == 0 && m->body_geomnum[b1] > 0) || (m->body_weldid[b1] == 0 && or_hasPlane(m, b1))) {
+      for (int b2 = 0; b2 < nbody; b2++) {
+        if (!or_canCollide(m, b2)) continue;
+        int weld2 = m->body_weldid[b2];
+        int pweld2 = m->body_weldid[m->body_parentid[weld2]];
+        if (or_filterBodyPair(0, 0, weld2, pweld2, dsbl_filterparent)) continue;
+        or_addPair(m, b1, b2, &npair, pair);
+      }
+    }
+  }
+  int cnt = 0;
+  mjtNum cen[3] = {0, 0, 0};
+  for (int i = 0; i < m->ngeom; i++) {
+    if (m->geom_bodyid[i]) {
+      for (int k = 0; k < 3; k++) cen[k] += d->geom_xpos[3*i+k];
+      cnt++;
+    }
+  }
+  if (cnt == 0) goto sort;
+  for (int k = 0; k < 3; k++) cen[k] *= 1.0/cnt;
+  {
+    mjtNum cov[9] = {0}, eigval[3], frame[9];
+    for (int i = 0; i < m->ngeom; i++) {
+      if (!m->geom_bodyid[i]) continue;
+      const mjtNum* v = d->geom_xpos + 3*i;
+      mjtNum dif[3] = {v[0]-cen[0], v[1]-cen[1], v[2]-cen[2]};
+      mjtNum D00 = dif[0]*dif[0], D01 = dif[0]*dif[1], D02 = dif[0]*dif[2];
+      mjtNum D11 = dif[1]*dif[1], D12 = dif[1]*dif[2], D22 = dif[2]*dif[2];
+      cov[0] += D00; cov[1] += D01; cov[2] += D02;
+      cov[3] += D01; cov[4] += D11; cov[5] += D12;
+      cov[6] += D02; cov[7] += D12; cov[8] += D22;
+    }
+    for (int k = 0; k < 9; k++) cov[k] *= 1.0/cnt;
+    or_eig3(eigval, frame, cov);
+    int* bid = (int*)malloc(sizeof(int) * nbody);
+    int ncollide = 0;
+    for (int i = 1; i < nbody; i++) {
+      if (or_canCollide(m, i)) bid[ncollide++] = i;
+    }
+    if (ncollide > 1) {
+      mjtNum* aamm = (mjtNum*)malloc(sizeof(mjtNum) * 6 * ncollide);
+      int* sap = (int*)malloc(sizeof(int) * ncollide * (ncollide - 1) / 2);
+      for (int i = 0; i < ncollide; i++) or_makeAAMM(m, d, aamm + 6*i, bid[i], frame);
+      int nsap = or_SAP(aamm, ncollide, sap);
+      for (int i = 0; i < nsap; i++) {
+        int b1 = bid[sap[i] >> 16], b2 = bid[sap[i] & 0xFFFF];
+        int weld1 = m->body_weldid[b1], weld2 = m->body_weldid[b2];
+        int pweld1 = m->body_weldid[m->body_parentid[weld1]];
+        int pweld2 = m->body_weldid[m->body_parentid[weld2]];
+        if (or_filterBodyPair(weld1, pweld1, weld2, pweld2, dsbl_filterparent)) continue;
+        or_addPair(m, b1, b2, &npair, pair);
+      }
+      free(aamm);
+      free(sap);
+    }
+    free(bid);
+  }
+sort:
+  for (int j = 1; j < npair; j++) {       /* bfsort: unsigned signature order */
+    int t = pair[j], k = j - 1;
+    for (; k >= 0 && (unsigned)pair[k] > (unsigned)t; k--) pair[k+1] = pair[k];
+    pair[k+1] = t;
+  }
+  return npair;
+}
+
+/* contacts enabled at all (mj_collision :282-287; nconmax is unbounded here) */
+static int or_contactsEnabled(const mjhipModel* m) {
+  return !mjDISABLED(mjhipDSBL_CONSTRAINT) && !mjDISABLED(mjhipDSBL_CONTACT) && m->nbody >= 2;
+}
+
+/* condim of a geom pair as mj_contactParam (:1289-1384) resolves it */
+static int or_pairCondim(const mjhipModel* m, int g1, int g2) {
+  int p1 = m->geom_priority[g1], p2 = m->geom_priority[g2];
+  if (p1 != p2) return p1 > p2 ? m->geom_condim[g1] : m->geom_condim[g2];
+  return mjMAX(m->geom_condim[g1], m->geom_condim[g2]);
+}
+
+/* Array sizing of the oracle's contact and constraint buffers (test infrastructure, not a
+ * reference rule: the reference sizes its arena by nconmax/njmax). Worst case over every
+ * body pair the broadphase could return: the most contacts of each geom pair's restated
+ * function, with the pyramidal/elliptic rows per contact (mj_instantiateContact). */
+static void or_contactBounds(const mjhipModel* m, int* ncon, int* nrow) {
+  *ncon = *nrow = 0;
+  if (!or_contactsEnabled(m)) return;
+  int dsbl_filterparent = mjDISABLED(mjhipDSBL_FILTERPARENT);
+  int ell = m->opt.cone == mjhipCONE_ELLIPTIC;
+  for (int b1 = 0; b1 < m->nbody; b1++) {
+    for (int b2 = b1 + 1; b2 < m->nbody; b2++) {
+      if (!or_canCollide(m, b1) || !or_canCollide(m, b2) || !or_canCollide2(m, b1, b2)) continue;
+      int weld1 = m->body_weldid[b1], weld2 = m->body_weldid[b2];
+      int pweld1 = m->body_weldid[m->body_parentid[weld1]];
+      int pweld2 = m->body_weldid[m->body_parentid[weld2]];
+      if (or_filterBodyPair(weld1, pweld1, weld2, pweld2, dsbl_filterparent)) continue;
+      int excluded = 0;
+      for (int i = 0; i < m->nexclude; i++) excluded |= m->exclude_signature[i] == (b1 << 16) + b2;
+      if (excluded) continue;
+      for (int g1 = m->body_geomadr[b1]; g1 < m->body_geomadr[b1] + m->body_geomnum[b1]; g1++) {
+        for (int g2 = m->body_geomadr[b2]; g2 < m->body_geomadr[b2] + m->body_geomnum[b2]; g2++) {
+          int t1 = mjMIN(m->geom_type[g1], m->geom_type[g2]);
+          int t2 = mjMAX(m->geom_type[g1], m->geom_type[g2]);
+          int k = or_collisionFunc(t1, t2);
+          if (k > 0 && !or_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
+                                         m->geom_contype[g2], m->geom_conaffinity[g2])) {
+            int condim = or_pairCondim(m, g1, g2);
+            *ncon += k;
+            *nrow += k * (condim == 1 ? 1 : (ell ? condim : 2*(condim - 1)));
+          }
+        }
+      }
+    }
+  }
+}
+
+int or_contactCapacity(const mjhipModel* m) {
+  int ncon, nrow;
+  or_contactBounds(m, &ncon, &nrow);
+  return ncon;
+}
+
+int or_efcCapacity(const mjhipModel* m) {
+  int n = 0;
+  for (int i = 0; i < m->njnt; i++) {
+    if (m->jnt_limited[i]) n += (m->jnt_type[i] == mjhipJNT_BALL) ? 1 : 2;
+  }
+  for (int i = 0; i < m->ntendon; i++) {
+    if (m->tendon_limited[i]) n += 2;
+  }
+  for (int i = 0; i < m->nv; i++) {
+    if (m->dof_frictionloss[i] > 0) n++;
+  }
+  for (int i = 0; i < m->neq; i++) {
+    int t = m->eq_type[i];
+    n += t == mjhipEQ_CONNECT ? 3 : (t == mjhipEQ_WELD ? 6 : 1);
+  }
+  int ncon, nrow;
+  or_contactBounds(m, &ncon, &nrow);
+  return n + nrow;
+}
+
 /* mj_collideGeoms (dynamic filters, narrowphase, mj_setContact) for geoms of two bodies */
 static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, int g1, int g2) {
   if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
-  const int kmax = mjhip_pairMaxContacts(t1, t2);
+  const int kmax = or_collisionFunc(t1, t2);
   if (kmax == 0) return;
-  if (mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1], m->geom_contype[g2],
-                          m->geom_conaffinity[g2])) {
+  if (or_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1], m->geom_contype[g2],
+                       m->geom_conaffinity[g2])) {
     return;
   }
   mjtNum margin = mjENABLED(mjhipENBL_OVERRIDE) ? m->opt.o_margin
@@ -1598,32 +1947,44 @@ static void or_swapContacts(orEfc* e, int a, int b) {
 #undef SWPI
 }
 
-/* mj_collision (engine_collision_driver.c:265-497): candidate body pairs in signature order
- * (mjhip_contact.h), geoms all-to-all; a pair handled by the midphase (mj_collideTree: a
- * body with more than one geom) has its contacts stably sorted by contactcompare */
+/* mj_collision (engine_collision_driver.c:265-497): the broadphase's body pairs in signature
+ * order (repeats skipped), the body bitmask and exclude filters, then a single-geom pair, the
+ * midphase (mj_collideTree, whose contacts are stably sorted by contactcompare) or all-to-all.
+ * The midphase's bounding-volume tests are inflated by the margins, so visiting the pair's
+ * geoms all-to-all yields the same contacts before the sort. */
 static void or_collision(const mjhipModel* m, const mjhipData* d, orEfc* e) {
   e->ncon = 0;
-  if (!mjhip_contactsEnabled(m)) return;
-  for (int b1 = 0; b1 < m->nbody; b1++) {
-    for (int b2 = b1 + 1; b2 < m->nbody; b2++) {
-      if (!mjhip_bodyPairCandidate(m, b1, b2)) continue;
-      int n1 = m->body_geomnum[b1], n2 = m->body_geomnum[b2];
-      int before = e->ncon;
-      for (int i = 0; i < n1; i++) {
-        for (int j = 0; j < n2; j++) {
-          or_collideGeoms(m, d, e, m->body_geomadr[b1] + i, m->body_geomadr[b2] + j);
-        }
+  if (!or_contactsEnabled(m)) return;
+  int nb = m->nbody;
+  int* pair = (int*)malloc(sizeof(int) * (nb*nb + nb*(nb - 1)/2 + 1));
+  int np = or_broadphase(m, d, pair);
+  unsigned last_signature = (unsigned)-1;
+  for (int i = 0; i < np; i++) {
+    int b1 = (pair[i] >> 16) & 0xFFFF, b2 = pair[i] & 0xFFFF;
+    unsigned signature = ((unsigned)b1 << 16) + b2;
+    if (signature == last_signature) continue;
+    last_signature = signature;
+    if (!or_canCollide2(m, b1, b2)) continue;
+    int exadr = 0;
+    while (exadr < m->nexclude && (unsigned)m->exclude_signature[exadr] < signature) exadr++;
+    if (exadr < m->nexclude && (unsigned)m->exclude_signature[exadr] == signature) continue;
+    int n1 = m->body_geomnum[b1], n2 = m->body_geomnum[b2];
+    int before = e->ncon;
+    for (int a = 0; a < n1; a++) {
+      for (int c = 0; c < n2; c++) {
+        or_collideGeoms(m, d, e, m->body_geomadr[b1] + a, m->body_geomadr[b2] + c);
       }
-      int midphase = !mjDISABLED(mjhipDSBL_MIDPHASE) && !(n1 == 1 && n2 == 1);
-      if (midphase) {   /* stable insertion sort (mjSORT is stable) */
-        for (int a = before + 1; a < e->ncon; a++) {
-          for (int b = a; b > before && or_contactLess(m, e, b, b - 1); b--) {
-            or_swapContacts(e, b, b - 1);
-          }
+    }
+    int midphase = !mjDISABLED(mjhipDSBL_MIDPHASE) && !(n1 == 1 && n2 == 1);
+    if (midphase) {   /* stable insertion sort (mjSORT is stable) */
+      for (int a = before + 1; a < e->ncon; a++) {
+        for (int b = a; b > before && or_contactLess(m, e, b, b - 1); b--) {
+          or_swapContacts(e, b, b - 1);
         }
       }
     }
   }
+  free(pair);
 }
 
 /* mju_mulMatMat (engine_util_blas.c:818-831) */

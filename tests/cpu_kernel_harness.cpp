@@ -98,5 +98,7 @@ static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int
   L.chain = chain;
   L.gxpos = L.geom_xpos;
   L.gstage = false;
+  L.cdq = nullptr;
+  L.fst = nullptr;
   return L;
 }

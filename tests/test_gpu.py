@@ -727,7 +727,7 @@ def test_elliptic_cone_parity():
   e.close()
 
 
-@pytest.mark.parametrize("lanes", ["0", "8", "16"])
+@pytest.mark.parametrize("lanes", ["0", "8", "16", "32"])
 def test_constraint_coop_lanes(humanoid_contacts, lanes, monkeypatch):
   """The cooperative constraint kernel (G lanes per instance: collision pairs, rows and
   J'force split over the group) against the one-lane kernel and the oracle, config-4 states

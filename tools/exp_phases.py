@@ -26,6 +26,8 @@ GROUPS = [
       "transmission+invVelocity", "discrete+invConstraint", "rne+assembly"]),
     ("k_constraint", [10, 11, 12, 13],
      ["collision", "makeConstraint", "reference+invConstraint"]),
+    ("k_constraint_coop", [14, 15, 18, 16, 17],
+     ["collision", "equality+friction+limit rows", "contact rows", "J'force+assembly"]),
 ]
 
 
@@ -50,6 +52,7 @@ def run(B=4096, reps=5):
   q, v, a = sample_contact_states(m, B)
   eng = engine.InverseEngine(m, capacity=B)
   eng.upload_states(q, v, a)
+  G = int(os.environ.get("MJHIP_COOP_LANES", "16")) or 64
   acc = (ctypes.c_ulonglong * 32)()
   for generic in (False, True):
     eng.inverse(B, mirror_input=True, generic=generic)
@@ -67,7 +70,9 @@ def run(B=4096, reps=5):
     print(f"batch {B}, {waves} waves, {'generic' if generic else 'default'} dispatch "
           f"(last call {wall*1e3:.2f} ms wall); mean per-wave phase time (us):")
     for title, marks, names in GROUPS:
-      t = sums[marks] / (reps * waves)
+      # the cooperative kernel runs G lanes per instance: 64/G instances per wave
+      nw = (B + 64 // G - 1) // (64 // G) if title == "k_constraint_coop" else waves
+      t = sums[marks] / (reps * nw)
       if not t.any():
         continue
       d = np.diff(t) / 100.0           # 100 MHz ticks -> us
