@@ -293,6 +293,16 @@ MJHIP_API int mjhip_contextCapacity(const mjhipContext* c);
 /* name of the straight-line (model-specialized) kernel selected for the context's model by
  * signature, or NULL when the generic kernel runs */
 MJHIP_API const char* mjhip_contextFastKernel(const mjhipContext* c);
+/* Run-time specialization: load a straight-line kernel generated for this
+ * context's model after the library was built. `image` is a gfx950 code object (hipcc
+ * --genco of codegen.py's source for the model, mujoco_inversedynamicstest_amd/
+ * specialize.py) holding extern "C" k_all_<name>; `signature` is the model signature it was
+ * generated for (MJHIP_ERR_MODEL if it is not this model's) and `cmode` its constraint mode
+ * (0 none, 1 work-list, 2 every instance). The kernel then serves skipstage = NONE calls
+ * exactly as a bundled one does; mjhip_contextFastKernel returns `name`. */
+MJHIP_API int mjhip_contextLoadKernel(mjhipContext* c, const void* image, size_t size,
+                                      const char* name, unsigned long long signature,
+                                      int cmode);
 /* instances of the last fast-path call that had active constraint rows and were recomputed
  * by the generic kernel (blocking read; -1 on error) */
 MJHIP_API int mjhip_worklistCount(mjhipContext* c);

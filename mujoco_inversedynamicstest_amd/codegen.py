@@ -1070,13 +1070,15 @@ _GEN = {"pos": lambda M, sf: _gen_pos(M, sf), "fac": lambda M, sf: _gen_fac(M, s
         "va": lambda M, sf: _gen_va(M, sf)}
 
 
-def generate(m, name: str, store_fields=None) -> str:
+def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   """HIP source of the four stage kernels of model `m` (skipstage = mjSTAGE_NONE).
 
   Also emits `fast_body_<name>`, which runs the four stage bodies for one instance in
   order (the host harness's entry), and `launch_fast_<name>`, which launches the kernels.
   store_fields: optional set of mirror fields to store (default: all); used only by
   performance experiments (tools/exp_bounds.py) to separate compute from store costs.
+  extern_c: give k_all_<name> C linkage (a run-time code object, specialize.py, whose
+  kernel mjhip_contextLoadKernel looks up by name).
   """
   why = fast_path_supported(m)
   if why:
@@ -1142,7 +1144,8 @@ def generate(m, name: str, store_fields=None) -> str:
                  f"(long)B - (long)blockIdx.x*64 : 64) * {M.nv};\n"
                  f"  double* dst = qfrc_out + (long)blockIdx.x*64*{M.nv};\n"
                  f"  for (long r = threadIdx.x; r < n; r += 64) dst[r] = qo_lds[r];\n")
-  out.append(f"""__global__ __launch_bounds__(64, 1) void k_all_{name}(Mirror mr, int B,
+  linkage = 'extern "C" ' if extern_c else ""
+  out.append(f"""{linkage}__global__ __launch_bounds__(64, 1) void k_all_{name}(Mirror mr, int B,
     const double* __restrict__ qpos_in, const double* __restrict__ qvel_in,
     const double* __restrict__ qacc_in, double* __restrict__ qfrc_out, int* __restrict__ status,
     int* __restrict__ worklist, int* __restrict__ worklist_count, int* __restrict__ worklist_next,

@@ -647,6 +647,13 @@ struct mjhipContext_ {
   int2* pairs = nullptr;                   // static geom-pair program (collisionPairs)
   int npair = 0;
   int coop = 16;                           // lanes per instance of k_constraint_coop (0: off)
+  // a straight-line kernel specialized for this model at run time (mjhip_contextLoadKernel):
+  // a gfx950 code object holding extern "C" k_all_<name>; rt.launch stays null
+  unsigned long long sig = 0;              // model_signature of the model at creation
+  hipModule_t rt_module = nullptr;
+  hipFunction_t rt_fn = nullptr;
+  FastKernelEntry rt{};
+  std::string rt_name;
 };
 
 // The static geom-pair program of mj_collision (engine_collision_driver.c:265-497) for the
@@ -932,10 +939,10 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
     return fail("hipMalloc(worklist)");
   }
   const char* nofast = getenv("MJHIP_DISABLE_FAST");
+  c->sig = model_signature(m);
   if (!(nofast && nofast[0] == '1')) {
-    unsigned long long sig = model_signature(m);
     for (const FastKernelEntry* e = g_fast_kernels; e->launch; e++) {
-      if (e->sig == sig) c->fast = e;
+      if (e->sig == c->sig) c->fast = e;
     }
   }
   // the cooperative constraint kernel's pair program (lanes per instance: MJHIP_COOP_LANES =
@@ -979,7 +986,43 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->pairs);
   hipFree(c->mirror_buf);
   hipFree(c->dmodel_buf);
+  if (c->rt_module) hipModuleUnload(c->rt_module);
   delete c;
+}
+
+MJHIP_API int mjhip_contextLoadKernel(mjhipContext* c, const void* image, size_t size,
+                                      const char* name, unsigned long long signature,
+                                      int cmode) {
+  if (!c || !image || !size || !name || cmode < 0 || cmode > 2) {
+    set_error("mjhip_contextLoadKernel: bad arguments");
+    return MJHIP_ERR_ARG;
+  }
+  if (signature != c->sig) {
+    set_error("mjhip_contextLoadKernel: kernel '%s' was generated for another model "
+              "(signature %016llx, context %016llx)", name, signature, c->sig);
+    return MJHIP_ERR_MODEL;
+  }
+  hipSetDevice(c->device);
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr;
+  const std::string kname = std::string("k_all_") + name;
+  if (hipModuleLoadData(&mod, image) != hipSuccess) {
+    set_error("mjhip_contextLoadKernel: hipModuleLoadData failed (not a gfx950 code object?)");
+    return MJHIP_ERR_HIP;
+  }
+  if (hipModuleGetFunction(&fn, mod, kname.c_str()) != hipSuccess) {
+    hipModuleUnload(mod);
+    set_error("mjhip_contextLoadKernel: no kernel '%s' in the code object", kname.c_str());
+    return MJHIP_ERR_HIP;
+  }
+  if (c->rt_module) hipModuleUnload(c->rt_module);
+  c->rt_module = mod;
+  c->rt_fn = fn;
+  c->rt_name = name;
+  c->rt = FastKernelEntry{signature, nullptr, c->rt_name.c_str(), cmode};
+  c->fast = &c->rt;
+  c->wl_parity = 0;                        // the run-time kernel zeroes the counters as the
+  return hipMemset(c->worklist, 0, 2 * sizeof(int)) == hipSuccess ? MJHIP_OK : MJHIP_ERR_HIP;
 }
 
 MJHIP_API int mjhip_contextCapacity(const mjhipContext* c) { return c ? c->capacity : 0; }
@@ -1018,9 +1061,18 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     // previous launch's k_pos, or at context creation) and zeroes `nxt` for the next one
     int* cnt = c->worklist + c->wl_parity;
     int* nxt = c->worklist + (c->wl_parity ^ 1);
-    c->fast->launch(grid, block, c->stream, c->mirror, B, qpos, qvel, qacc, qfrc, status,
-                    c->worklist + 2, cnt, nxt, c->mirror.efc_count);
-    HIPCHECK(hipGetLastError());
+    if (c->fast->launch) {
+      c->fast->launch(grid, block, c->stream, c->mirror, B, qpos, qvel, qacc, qfrc, status,
+                      c->worklist + 2, cnt, nxt, c->mirror.efc_count);
+      HIPCHECK(hipGetLastError());
+    } else {                             // run-time specialized k_all_<name> (same arguments)
+      int* wl = c->worklist + 2;
+      int* efc = c->mirror.efc_count;
+      void* args[] = {&c->mirror, &B, &qpos, &qvel, &qacc, &qfrc, &status, &wl, &cnt, &nxt,
+                      &efc};
+      HIPCHECK(hipModuleLaunchKernel(c->rt_fn, grid.x, 1, 1, 64, 1, 1, 0, c->stream, args,
+                                     nullptr));
+    }
     // the fast path excludes INVDISCRETE: the constraint kernel is fused whenever nbody allows
     const bool fused = mjh::fusedOk(c->dmodel, mjhipSTAGE_NONE);
     const int* wl = c->worklist + 2;

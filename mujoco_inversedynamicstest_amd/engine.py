@@ -48,6 +48,8 @@ SIGNATURES = {
     "mjhip_contextFree": (None, [_V]),
     "mjhip_contextCapacity": (ctypes.c_int, [_V]),
     "mjhip_contextFastKernel": (ctypes.c_char_p, [_V]),
+    "mjhip_contextLoadKernel": (ctypes.c_int, [_V, _V, ctypes.c_size_t, ctypes.c_char_p,
+                                               ctypes.c_ulonglong, ctypes.c_int]),
     "mjhip_worklistCount": (ctypes.c_int, [_V]),
     "mjhip_contextStream": (_V, [_V]),
     "mjhip_contextSetStream": (ctypes.c_int, [_V, _V]),
@@ -139,7 +141,10 @@ def _dptr(a):
 class InverseEngine:
   """Batched mj_inverse for one model on one device (an mjhipContext)."""
 
-  def __init__(self, model, capacity: int, device: int = 0):
+  def __init__(self, model, capacity: int, device: int = 0, specialize=None):
+    """specialize: generate and load a straight-line kernel for a model that has no bundled
+    one (specialize.py; compiled once per model, then cached). None = the MJHIP_SPECIALIZE
+    environment variable ("1" default, "0" off)."""
     self.m = model
     self.cm = host.model_struct(model)
     L = lib()
@@ -150,6 +155,13 @@ class InverseEngine:
     self.device = device
     self.capacity = L.mjhip_contextCapacity(ctx)
     self.nv, self.nq = model.nv, model.nq
+    if specialize is None:
+      specialize = os.environ.get("MJHIP_SPECIALIZE", "1") != "0"
+    if specialize and self.fast_kernel is None and os.environ.get("MJHIP_DISABLE_FAST") != "1":
+      from . import codegen
+      from . import specialize as spec
+      if codegen.fast_path_supported(model) is None:
+        spec.load(self)
 
   def close(self):
     if getattr(self, "ctx", None):

@@ -1,0 +1,121 @@
+"""Run-time kernel specialization: straight-line mj_inverse kernels for any supported model.
+
+The library ships straight-line kernels (codegen.py) for the bundled models only, selected by
+model signature at mjhip_contextCreate. For any other model whose features the generated
+kernels cover (codegen.fast_path_supported), this module generates the same source for that
+model when an engine is created, compiles it to a gfx950 code object (hipcc --genco, the
+image's compiler driver) and hands it to the context (mjhip_contextLoadKernel), so a user's
+MJCF runs the fast path instead of the generic kernel ("template codegen at
+load").
+
+Code objects are cached by the SHA-256 of their generated source in MJHIP_KERNEL_CACHE
+(default: kernel_cache/ next to this file), so a model compiles once. A C host loads the
+same code object: `python -m mujoco_inversedynamicstest_amd.specialize
+model.xml` writes it and prints the name, signature and constraint mode to pass.
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import subprocess
+import sys
+import tempfile
+
+from . import codegen, fields
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(_HERE, "csrc")
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+FLAGS = ["--genco", "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-value",
+         "-Wno-unused-result"]
+
+
+def cache_dir() -> str:
+  return os.environ.get("MJHIP_KERNEL_CACHE", os.path.join(_HERE, "kernel_cache"))
+
+
+class SpecializeError(RuntimeError):
+  pass
+
+
+def source(m) -> tuple[str, str]:
+  """(kernel name, complete HIP source) of the straight-line kernel for model m."""
+  name = f"rt_{codegen.model_hash(m)}"
+  body = codegen.generate(m, name, extern_c=True)
+  src = ('#include <hip/hip_runtime.h>\n'
+         f'#include "{os.path.join(CSRC, "engine_device.h")}"\n' + body)
+  return name, src
+
+
+def code_object(m) -> tuple[bytes, str, int, int]:
+  """Compile (or fetch from the cache) the code object for model m.
+
+  Returns (image, name, signature, cmode) — the arguments of mjhip_contextLoadKernel.
+  Raises SpecializeError when the model is outside the generated kernels' subset."""
+  why = codegen.fast_path_supported(m)
+  if why:
+    raise SpecializeError(f"no straight-line kernel for this model: {why}")
+  name, src = source(m)
+  # the headers are part of what the code object depends on
+  h = hashlib.sha256(src.encode())
+  for hdr in ("engine_device.h",):
+    h.update(open(os.path.join(CSRC, hdr), "rb").read())
+  for hdr in ("mjhip.h", "mjhip_fields.h", "mjhip_contact.h"):
+    h.update(open(os.path.join(_HERE, "..", "include", hdr), "rb").read())
+  key = h.hexdigest()[:32]
+  d = cache_dir()
+  path = os.path.join(d, f"{name}_{key}.hsaco")
+  if not os.path.exists(path):
+    os.makedirs(d, exist_ok=True)
+    with tempfile.TemporaryDirectory() as tmp:
+      hip = os.path.join(tmp, f"{name}.hip")
+      out = os.path.join(tmp, f"{name}.hsaco")
+      with open(hip, "w") as f:
+        f.write(src)
+      r = subprocess.run([HIPCC, *FLAGS, "-o", out, hip], capture_output=True, text=True)
+      if r.returncode != 0:
+        raise SpecializeError(f"hipcc failed for {name}:\n{r.stderr[-4000:]}")
+      _copy(out, path)
+  with open(path, "rb") as f:
+    image = f.read()
+  cmode = codegen.CONSTRAINT_MODES[codegen.constraint_mode(m)]
+  return image, name, fields.model_signature(m), cmode
+
+
+def _copy(src, dst):
+  tmp = dst + f".{os.getpid()}.tmp"
+  with open(src, "rb") as f, open(tmp, "wb") as g:
+    g.write(f.read())
+  os.replace(tmp, dst)                  # atomic: concurrent builders never see a partial file
+
+
+def load(engine) -> str:
+  """Specialize an InverseEngine's context for its model; returns the kernel name."""
+  from .engine import _check, lib
+  image, name, sig, cmode = code_object(engine.m)
+  buf = ctypes.create_string_buffer(image, len(image))
+  _check(lib().mjhip_contextLoadKernel(engine.ctx, buf, len(image), name.encode(),
+                                       ctypes.c_ulonglong(sig), cmode),
+         "mjhip_contextLoadKernel")
+  return name
+
+
+def main(argv=None):
+  """Write the code object for an MJCF file (for C hosts) and print its load arguments."""
+  import argparse
+  from . import mjcf
+  ap = argparse.ArgumentParser(description=main.__doc__)
+  ap.add_argument("xml")
+  ap.add_argument("-o", "--output", help="code object path (default: the cache entry)")
+  args = ap.parse_args(argv)
+  m = mjcf.load_xml(args.xml)
+  image, name, sig, cmode = code_object(m)
+  if args.output:
+    with open(args.output, "wb") as f:
+      f.write(image)
+  print(f"name={name} signature=0x{sig:016x} cmode={cmode} bytes={len(image)}")
+
+
+if __name__ == "__main__":
+  sys.exit(main())
