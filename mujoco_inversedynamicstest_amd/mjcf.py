@@ -1578,135 +1578,11 @@ class MJCFCompiler:
             nOD += 1
           j = dparent[j]
     s["nC"] = nC = nOD + nv
-    # C sparse structure and mapM2C (engine_io.c:929-1018, 1135-1259; reduced=1)
-    rownnz = arr("C_rownnz", nv, np.int32)
-    rowadr = arr("C_rowadr", nv, np.int32)
-    colind = arr("C_colind", nC, np.int32)
-    mapM2C = arr("mapM2C", nC, np.int32, -1)
-    for i in range(nv - 1, -1, -1):
-      rownnz[i] += 1
-      if not simplenum[i]:
-        j = i
-        while True:
-          j = dparent[j]
-          if j < 0:
-            break
-          rownnz[i] += 1
-    for i in range(1, nv):
-      rowadr[i] = rowadr[i-1] + rownnz[i-1]
-    remaining = rownnz.copy()
-    for i in range(nv - 1, -1, -1):
-      remaining[i] -= 1
-      colind[rowadr[i] + remaining[i]] = i
-      adr = Madr[i]
-      mapM2C[rowadr[i] + remaining[i]] = adr
-      adr += 1
-      if not simplenum[i]:
-        j = i
-        while True:
-          j = dparent[j]
-          if j < 0:
-            break
-          remaining[i] -= 1
-          colind[rowadr[i] + remaining[i]] = j
-          mapM2C[rowadr[i] + remaining[i]] = adr
-          adr += 1
-    if nv and (remaining != 0).any():
-      raise MJCFError("unexpected remaining")  # SHOULD NOT OCCUR
-    # D sparse structure (dof x dof, ancestors and descendants) and mapM2D
-    # (engine_io.c:929-1018 with reduced=0, :1135-1232): row i lists every dof on i's chain
-    # to the root and in i's subtree, ascending
-    cols = [[i] for i in range(nv)]
-    for i in range(nv - 1, -1, -1):
-      j = dparent[i]
-      while j >= 0:
-        cols[i].append(j)
-        cols[j].append(i)
-        j = dparent[j]
-    nD = s["nD"]
-    Drownnz = arr("D_rownnz", nv, np.int32)
-    Drowadr = arr("D_rowadr", nv, np.int32)
-    Dcolind = arr("D_colind", nD, np.int32)
-    mapM2D = arr("mapM2D", nD, np.int32, -1)
-    for i in range(nv):
-      Drownnz[i] = len(cols[i])
-      Drowadr[i] = Drowadr[i-1] + Drownnz[i-1] if i else 0
-      Dcolind[Drowadr[i]:Drowadr[i] + Drownnz[i]] = sorted(cols[i])
-    for i in range(nv):                 # qM element (i, j), j on i's chain, at Madr[i] + k
-      adr, j = Madr[i], i
-      while j >= 0:
-        for r, c in ((i, j), (j, i)):
-          row = Dcolind[Drowadr[r]:Drowadr[r] + Drownnz[r]]
-          mapM2D[Drowadr[r] + int(np.searchsorted(row, c))] = adr
-        adr += 1
-        j = dparent[j]
-    if nv and ((mapM2D < 0).any() or Drowadr[-1] + Drownnz[-1] != nD):
-      raise MJCFError("D sparsity mismatch")  # SHOULD NOT OCCUR
-    # B sparse structure (body x dof: ancestor and subtree dofs, ascending),
-    # engine_io.c:1021-1106 makeBSparse
-    bcols = [set() for _ in range(nbody)]
-    for i in range(nbody - 1, 0, -1):
-      bcols[i].update(range(dofadr[i], dofadr[i] + dofnum[i]))
-      bcols[parentid[i]].update(bcols[i])
-    for i in range(nbody):
-      p = parentid[i] if i else -1
-      while p > 0:
-        bcols[i].update(range(dofadr[p], dofadr[p] + dofnum[p]))
-        p = parentid[p]
-    s["nB"] = nB = sum(len(c) for c in bcols)
-    Brownnz = arr("B_rownnz", nbody, np.int32)
-    Browadr = arr("B_rowadr", nbody, np.int32)
-    Bcolind = arr("B_colind", nB, np.int32)
-    for i in range(nbody):
-      Brownnz[i] = len(bcols[i])
-      Browadr[i] = Browadr[i-1] + Brownnz[i-1] if i else 0
-      Bcolind[Browadr[i]:Browadr[i] + Brownnz[i]] = sorted(bcols[i])
-    for j in range(nv):                 # checkDBSparse engine_io.c:1111-1130
-      b = dbody[j]
-      if list(Dcolind[Drowadr[j]:Drowadr[j] + Drownnz[j]]) != \
-         list(Bcolind[Browadr[b]:Browadr[b] + Brownnz[b]]):
-        raise MJCFError("D and B sparsity differ")  # SHOULD NOT OCCUR
-    # actuator moment sparsity (mj_transmission, engine_core_smooth.c:884-1081). For the
-    # transmissions in the subset it depends on the model only: a joint's dofs, or the dofs
-    # where a fixed tendon's dense ten_J row times gear[0] is nonzero (the dense compress
-    # loop :1070-1079; ten_J entries are the wrap coefficients, last one per joint wins,
-    # smooth.c mj_tendon dense branch). rowadr is cumulative (:896).
-    mrownnz = arr("moment_rownnz", nu, np.int32)
-    mrowadr = arr("moment_rowadr", nu, np.int32)
-    cols = []
-    for ai in range(nu):
-      tid = int(atrnid[ai, 0])
-      if atrn[ai] in (0, 1):
-        cnt = {0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[tid])]
-        c = list(range(jdadr[tid], jdadr[tid] + cnt))
-      elif atrn[ai] in (2, 4):
-        # slider-crank: the dense moment is the chain rule over the two sites' Jacobians
-        # (:1035-1052); its structural nonzeros are the dofs of both sites' body chains
-        c = set()
-        for sid in atrnid[ai]:
-          if sid < 0:
-            continue
-          b = int(sbody[sid])
-          while b > 0:
-            c.update(range(dofadr[b], dofadr[b] + dofnum[b]))
-            b = int(parentid[b])
-        gzero = agear[ai, 0] == 0 if atrn[ai] == 2 else not np.any(agear[ai])
-        c = [] if gzero else sorted(c)
-      else:
-        row = np.zeros(nv)
-        for wi in range(tadr[tid], tadr[tid] + tnum[tid]):
-          row[jdadr[wobj[wi]]] = wprm[wi]
-        c = [j for j in range(nv) if row[j] * agear[ai, 0] != 0]
-      mrownnz[ai] = len(c)
-      mrowadr[ai] = mrowadr[ai - 1] + mrownnz[ai - 1] if ai else 0
-      cols.extend(c)
     # nJmom as CountNJmom (user_model.cc:2703-2750): 1/3/6 per joint transmission, nv per
-    # tendon, so actuator_moment has the reference's size; colind past the nonzeros is 0
-    nJmom = sum({0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[atrnid[ai, 0]])] if atrn[ai] in (0, 1)
-                else nv for ai in range(nu))    # slider-crank and tendon: nv
-    mcol = arr("moment_colind", nJmom, np.int32)
-    mcol[:len(cols)] = cols
-    s["nJmom"] = nJmom
+    # tendon, slider-crank or site transmission, so actuator_moment has the reference's size
+    s["nJmom"] = sum({0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[atrnid[ai, 0]])] if atrn[ai] in (0, 1)
+                     else nv for ai in range(nu))
+    A.update(sparse_structures(s, A))
     # scalars and names
     m.opt = {k: (list(v) if isinstance(v, list) else v) for k, v in self.opt.items()}
     for k, v in A.items():
@@ -1731,6 +1607,168 @@ class MJCFCompiler:
         want = want[:1]
       setattr(m, f.name, np.ascontiguousarray(a.reshape(want).astype(fields.NPTYPE[f.ctype])))
     return m
+
+
+def sparse_structures(sizes: dict, A) -> dict:
+  """The model-constant sparse structures the reference keeps in mjData (mj_makeData):
+  C (reduced LTDL pattern) and mapM2C, D (dof x dof) and mapM2D, B (body x dof), and the
+  actuator moment pattern. `A` maps mjModel field names to arrays (the compiler's, or an
+  imported .mjb's, mjb.py); sizes needs nv, nbody, nu, nM, nC, nD, nB, nJmom. Returns the
+  new arrays by field name; raises MJCFError on an inconsistent model."""
+  nv, nbody, nu = sizes["nv"], sizes["nbody"], sizes["nu"]
+  nC, nD, nJmom = sizes["nC"], sizes["nD"], sizes["nJmom"]
+  dparent = np.asarray(A["dof_parentid"]).reshape(-1)
+  simplenum = np.asarray(A["dof_simplenum"]).reshape(-1)
+  Madr = np.asarray(A["dof_Madr"]).reshape(-1)
+  dbody = np.asarray(A["dof_bodyid"]).reshape(-1)
+  parentid = np.asarray(A["body_parentid"]).reshape(-1)
+  dofadr = np.asarray(A["body_dofadr"]).reshape(-1)
+  dofnum = np.asarray(A["body_dofnum"]).reshape(-1)
+  atrn = np.asarray(A["actuator_trntype"]).reshape(-1)
+  atrnid = np.asarray(A["actuator_trnid"]).reshape(-1, 2)
+  agear = np.asarray(A["actuator_gear"]).reshape(-1, 6)
+  jtype = np.asarray(A["jnt_type"]).reshape(-1)
+  jdadr = np.asarray(A["jnt_dofadr"]).reshape(-1)
+  sbody = np.asarray(A["site_bodyid"]).reshape(-1)
+  tadr = np.asarray(A["tendon_adr"]).reshape(-1)
+  tnum = np.asarray(A["tendon_num"]).reshape(-1)
+  wobj = np.asarray(A["wrap_objid"]).reshape(-1)
+  wprm = np.asarray(A["wrap_prm"]).reshape(-1)
+  out = {}
+
+  def arr(name, shape, dtype, fill=0):
+    out[name] = np.full(shape, fill, dtype=dtype)
+    return out[name]
+
+  # C sparse structure and mapM2C (engine_io.c:929-1018, 1135-1259; reduced=1)
+  rownnz = arr("C_rownnz", nv, np.int32)
+  rowadr = arr("C_rowadr", nv, np.int32)
+  colind = arr("C_colind", nC, np.int32)
+  mapM2C = arr("mapM2C", nC, np.int32, -1)
+  for i in range(nv - 1, -1, -1):
+    rownnz[i] += 1
+    if not simplenum[i]:
+      j = i
+      while True:
+        j = dparent[j]
+        if j < 0:
+          break
+        rownnz[i] += 1
+  for i in range(1, nv):
+    rowadr[i] = rowadr[i-1] + rownnz[i-1]
+  remaining = rownnz.copy()
+  for i in range(nv - 1, -1, -1):
+    remaining[i] -= 1
+    colind[rowadr[i] + remaining[i]] = i
+    adr = Madr[i]
+    mapM2C[rowadr[i] + remaining[i]] = adr
+    adr += 1
+    if not simplenum[i]:
+      j = i
+      while True:
+        j = dparent[j]
+        if j < 0:
+          break
+        remaining[i] -= 1
+        colind[rowadr[i] + remaining[i]] = j
+        mapM2C[rowadr[i] + remaining[i]] = adr
+        adr += 1
+  if nv and (remaining != 0).any():
+    raise MJCFError("unexpected remaining")  # SHOULD NOT OCCUR
+  # D sparse structure (dof x dof, ancestors and descendants) and mapM2D
+  # (engine_io.c:929-1018 with reduced=0, :1135-1232): row i lists every dof on i's chain
+  # to the root and in i's subtree, ascending
+  cols = [[i] for i in range(nv)]
+  for i in range(nv - 1, -1, -1):
+    j = dparent[i]
+    while j >= 0:
+      cols[i].append(j)
+      cols[j].append(i)
+      j = dparent[j]
+  Drownnz = arr("D_rownnz", nv, np.int32)
+  Drowadr = arr("D_rowadr", nv, np.int32)
+  Dcolind = arr("D_colind", nD, np.int32)
+  mapM2D = arr("mapM2D", nD, np.int32, -1)
+  for i in range(nv):
+    Drownnz[i] = len(cols[i])
+    Drowadr[i] = Drowadr[i-1] + Drownnz[i-1] if i else 0
+    Dcolind[Drowadr[i]:Drowadr[i] + Drownnz[i]] = sorted(cols[i])
+  for i in range(nv):                 # qM element (i, j), j on i's chain, at Madr[i] + k
+    adr, j = Madr[i], i
+    while j >= 0:
+      for r, c in ((i, j), (j, i)):
+        row = Dcolind[Drowadr[r]:Drowadr[r] + Drownnz[r]]
+        mapM2D[Drowadr[r] + int(np.searchsorted(row, c))] = adr
+      adr += 1
+      j = dparent[j]
+  if nv and ((mapM2D < 0).any() or Drowadr[-1] + Drownnz[-1] != nD):
+    raise MJCFError("D sparsity mismatch")  # SHOULD NOT OCCUR
+  # B sparse structure (body x dof: ancestor and subtree dofs, ascending),
+  # engine_io.c:1021-1106 makeBSparse
+  bcols = [set() for _ in range(nbody)]
+  for i in range(nbody - 1, 0, -1):
+    bcols[i].update(range(dofadr[i], dofadr[i] + dofnum[i]))
+    bcols[parentid[i]].update(bcols[i])
+  for i in range(nbody):
+    p = parentid[i] if i else -1
+    while p > 0:
+      bcols[i].update(range(dofadr[p], dofadr[p] + dofnum[p]))
+      p = parentid[p]
+  nB = sum(len(c) for c in bcols)
+  if nB != sizes.setdefault("nB", nB):
+    raise MJCFError("B sparsity size mismatch")
+  Brownnz = arr("B_rownnz", nbody, np.int32)
+  Browadr = arr("B_rowadr", nbody, np.int32)
+  Bcolind = arr("B_colind", nB, np.int32)
+  for i in range(nbody):
+    Brownnz[i] = len(bcols[i])
+    Browadr[i] = Browadr[i-1] + Brownnz[i-1] if i else 0
+    Bcolind[Browadr[i]:Browadr[i] + Brownnz[i]] = sorted(bcols[i])
+  for j in range(nv):                 # checkDBSparse engine_io.c:1111-1130
+    b = dbody[j]
+    if list(Dcolind[Drowadr[j]:Drowadr[j] + Drownnz[j]]) != \
+       list(Bcolind[Browadr[b]:Browadr[b] + Brownnz[b]]):
+      raise MJCFError("D and B sparsity differ")  # SHOULD NOT OCCUR
+  # actuator moment sparsity (mj_transmission, engine_core_smooth.c:884-1081). For the
+  # transmissions in the subset it depends on the model only: a joint's dofs, or the dofs
+  # where a fixed tendon's dense ten_J row times gear[0] is nonzero (the dense compress
+  # loop :1070-1079; ten_J entries are the wrap coefficients, last one per joint wins,
+  # smooth.c mj_tendon dense branch). rowadr is cumulative (:896).
+  mrownnz = arr("moment_rownnz", nu, np.int32)
+  mrowadr = arr("moment_rowadr", nu, np.int32)
+  cols = []
+  for ai in range(nu):
+    tid = int(atrnid[ai, 0])
+    if atrn[ai] in (0, 1):
+      cnt = {0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[tid])]
+      c = list(range(jdadr[tid], jdadr[tid] + cnt))
+    elif atrn[ai] in (2, 4):
+      # slider-crank: the dense moment is the chain rule over the two sites' Jacobians
+      # (:1035-1052); its structural nonzeros are the dofs of both sites' body chains
+      c = set()
+      for sid in atrnid[ai]:
+        if sid < 0:
+          continue
+        b = int(sbody[sid])
+        while b > 0:
+          c.update(range(dofadr[b], dofadr[b] + dofnum[b]))
+          b = int(parentid[b])
+      gzero = agear[ai, 0] == 0 if atrn[ai] == 2 else not np.any(agear[ai])
+      c = [] if gzero else sorted(c)
+    else:
+      row = np.zeros(nv)
+      for wi in range(tadr[tid], tadr[tid] + tnum[tid]):
+        row[jdadr[wobj[wi]]] = wprm[wi]
+      c = [j for j in range(nv) if row[j] * agear[ai, 0] != 0]
+    mrownnz[ai] = len(c)
+    mrowadr[ai] = mrowadr[ai - 1] + mrownnz[ai - 1] if ai else 0
+    cols.extend(c)
+  mcol = arr("moment_colind", nJmom, np.int32)
+  if len(cols) > nJmom:
+    raise MJCFError("actuator moment pattern exceeds nJmom")
+  mcol[:len(cols)] = cols
+
+  return out
 
 
 def _sameframe(pos, quat, ipos, iquat):

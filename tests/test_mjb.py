@@ -1,0 +1,174 @@
+""".mjb model files (mjb.py): the reference's binary layout, read and written.
+
+  * round trip: every bundled model -> mjb.write -> mjb.read equals the model field for field
+    (and by model signature, so the engine selects the same kernel)
+  * header and consistency checks with mj_loadModelBuffer's messages (engine_io.c:776-890)
+  * models outside the device subset are refused
+  * the layout table and struct sizes against the reference headers (only where
+    /root/reference exists: this container, never the GPU box)
+"""
+import os
+import re
+import struct
+import subprocess
+
+import numpy as np
+import pytest
+
+from mujoco_inversedynamicstest_amd import engine, fields, mjb, models
+
+REF = "/root/reference"
+BUNDLED = ["humanoid", "slider_crank", "inverse_test", "inertia", "linear", "weld", "connect",
+           "equality_site", "equality_compare"]
+
+
+@pytest.mark.parametrize("name", BUNDLED)
+def test_round_trip(name, tmp_path):
+  m = models.load(name)
+  path = tmp_path / f"{name}.mjb"
+  mjb.save(m, str(path))
+  r = mjb.load(str(path))
+  for f in fields.MODEL_FIELDS:
+    a, b = getattr(m, f.name), getattr(r, f.name)
+    assert a.shape == b.shape and a.dtype == b.dtype, f.name
+    np.testing.assert_array_equal(a, b, err_msg=f.name)
+  assert r.sizes == m.sizes
+  assert r.names == m.names
+  for k, v in m.opt.items():
+    assert r.opt[k] == v, k
+  assert fields.model_signature(r) == fields.model_signature(m)
+
+
+def test_header_and_sizes(humanoid):
+  buf = mjb.write(humanoid)
+  hdr = struct.unpack_from("<5i", buf, 0)
+  assert hdr == (54321, 8, 83, 2, 399)
+  ints = dict(zip(mjb.INTS, struct.unpack_from("<83i", buf, 20)))
+  narena, nbuffer = struct.unpack_from("<2Q", buf, 20 + 4 * 83)
+  assert nbuffer == mjb.buffer_size(ints)
+  assert ints["nq"] == 28 and ints["nv"] == 27 and ints["nM"] == 243 and ints["nbody"] == 17
+  assert len(buf) == mjb.offsets(ints)["__end__"]
+
+
+def _patch(buf, offset, fmt, *vals):
+  b = bytearray(buf)
+  struct.pack_into(fmt, b, offset, *vals)
+  return bytes(b)
+
+
+@pytest.mark.parametrize("idx,msg", [
+    (0, "Model missing header ID"),
+    (1, "different floating point precision"),
+    (2, "different number of ints"),
+    (3, "different number of size_t"),
+    (4, "different number of pointers")])
+def test_header_checks(humanoid, idx, msg):
+  buf = mjb.write(humanoid)
+  hdr = list(struct.unpack_from("<5i", buf, 0))
+  hdr[idx] += 1
+  with pytest.raises(mjb.MJBError, match=msg):
+    mjb.read(_patch(buf, 0, "<5i", *hdr))
+
+
+def test_truncation_and_size_checks(humanoid):
+  buf = mjb.write(humanoid)
+  with pytest.raises(mjb.MJBError, match="incomplete header"):
+    mjb.read(buf[:12])
+  with pytest.raises(mjb.MJBError, match="while reading sizes"):
+    mjb.read(buf[:40])
+  with pytest.raises(mjb.MJBError, match="while reading structs"):
+    mjb.read(buf[:20 + 4 * 83 + 16 + 100])
+  ints = dict(zip(mjb.INTS, struct.unpack_from("<83i", buf, 20)))
+  off = mjb.offsets(ints)
+  with pytest.raises(mjb.MJBError, match="while reading body_mass"):
+    mjb.read(buf[:off["body_mass"] + 8])
+  with pytest.raises(mjb.MJBError, match="too large"):
+    mjb.read(buf + b"\0")
+  nb = struct.unpack_from("<Q", buf, 20 + 4 * 83 + 8)[0]
+  with pytest.raises(mjb.MJBError, match="wrong size parameters"):
+    mjb.read(_patch(buf, 20 + 4 * 83 + 8, "<Q", nb + 64))
+
+
+def test_options_survive(humanoid):
+  m = models.load("humanoid", disable_contact=True)
+  r = mjb.read(mjb.write(m))
+  assert r.opt["disableflags"] == m.opt["disableflags"] != 0
+  assert r.opt["timestep"] == m.opt["timestep"]
+  assert r.opt["iterations"] == 100          # mj_defaultOption for members the loader skips
+
+
+@pytest.mark.parametrize("field,value,msg", [
+    ("tendon_frictionloss", 0.5, "tendon frictionloss"),
+    ("geom_fluid", 1.0, "ellipsoid fluid"),
+    ("wrap_type", 3, "spatial tendons")])
+def test_unsupported_features_refused(humanoid, field, value, msg):
+  buf = mjb.write(humanoid)
+  ints = dict(zip(mjb.INTS, struct.unpack_from("<83i", buf, 20)))
+  off = mjb.offsets(ints)[field]
+  code = next(c for n, r, c, _ in mjb.LAYOUT if n == field)
+  b = _patch(buf, off, "<d" if code == "d" else "<i", value)
+  with pytest.raises(mjb.MJBError, match=msg):
+    mjb.read(b)
+
+
+def test_pairs_refused(humanoid):
+  """npair > 0: the predefined-pair arrays grow, and the model is refused."""
+  buf = bytearray(mjb.write(humanoid))
+  ints = dict(zip(mjb.INTS, struct.unpack_from("<83i", buf, 20)))
+  ints["npair"] = 1
+  off = mjb.offsets(dict(ints, npair=0))
+  grow = mjb.offsets(ints)["__end__"] - off["__end__"]
+  at = off["pair_dim"]
+  new = bytes(buf[:at]) + b"\0" * grow + bytes(buf[at:])
+  new = _patch(new, 20, "<83i", *[ints[k] for k in mjb.INTS])
+  new = _patch(new, 20 + 4 * 83 + 8, "<Q", mjb.buffer_size(ints))
+  with pytest.raises(mjb.MJBError, match="explicit contact pairs"):
+    mjb.read(new)
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="reference headers not present")
+def test_layout_matches_reference_headers(tmp_path):
+  """The transcribed field table and struct sizes against include/mujoco (read as text, and
+  sizeof from a probe compiled against the public headers; the reference is not built)."""
+  text = open(os.path.join(REF, "include/mujoco/mjxmacro.h")).read()
+  ints = re.findall(r"X(?:MJV)?\s*\(\s*(\w+)\s*\)",
+                    text[text.index("#define MJMODEL_INTS"):text.index("#define MJMODEL_POINTERS_PREAMBLE")])
+  assert ints == mjb.INTS + ["narena", "nbuffer"]
+  body = text[text.index("#define MJMODEL_POINTERS "):text.index("#define MJDATA_POINTERS_PREAMBLE")]
+  ref = re.findall(r"X(?:MJV|NV)?\s*\(\s*(\w+)\s*,\s*(\w+)\s*,\s*(\w+)\s*,\s*(.+?)\s*\)\s*\\",
+                   body)
+  consts = {"mjNREF": "2", "mjNIMP": "5", "mjNEQDATA": "11", "mjNDYN": "10", "mjNGAIN": "10",
+            "mjNBIAS": "10", "mjNFLUID": "12", "mjNTEXROLE": "10"}
+  tmap = {"mjtNum": "d", "float": "f", "int": "i", "mjtByte": "b", "char": "c"}
+  got = []
+  for t, n, r, c in ref:
+    c = re.sub(r"MJ_M\((\w+)\)", r"\1", c).replace(" ", "")
+    got.append((n, r, tmap[t], consts.get(c, c)))
+  assert got == [tuple(x) for x in mjb.LAYOUT]
+  probe = tmp_path / "probe.c"
+  probe.write_text('#include <stdio.h>\n#include <mujoco/mjmodel.h>\n'
+                   'int main(void){printf("%zu %zu %zu", sizeof(mjOption), sizeof(mjVisual),'
+                   ' sizeof(mjStatistic)); return 0;}\n')
+  exe = tmp_path / "probe"
+  subprocess.run(["gcc", "-I", os.path.join(REF, "include"), "-o", str(exe), str(probe)],
+                 check=True)
+  sizes = subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()
+  assert [int(x) for x in sizes] == [mjb.SIZEOF_OPTION, mjb.SIZEOF_VISUAL,
+                                     mjb.SIZEOF_STATISTIC]
+
+
+@pytest.mark.gpu
+def test_engine_on_imported_model(humanoid):
+  """The engine on an imported .mjb selects the same straight-line kernel and returns
+  bit-identical results."""
+  from mujoco_inversedynamicstest_amd.sampler import sample_states
+  r = mjb.read(mjb.write(humanoid))
+  q, v, a = sample_states(humanoid, 1024, first=7)
+  e1 = engine.InverseEngine(humanoid, capacity=1024)
+  e2 = engine.InverseEngine(r, capacity=1024)
+  try:
+    assert e2.fast_kernel == e1.fast_kernel == "humanoid"
+    np.testing.assert_array_equal(e1.inverse(q, v, a), e2.inverse(q, v, a))
+  finally:
+    e1.close()
+    e2.close()
