@@ -15,7 +15,8 @@ import numpy as np
 from mujoco_inversedynamicstest_amd import fields, host
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB = os.path.join(_HERE, "liboracle.so")
+# ORACLE_LIB: another build of the same source (tests/test_asan.py: the sanitizer build)
+_LIB = os.environ.get("ORACLE_LIB", os.path.join(_HERE, "liboracle.so"))
 _lib = None
 
 _D = ctypes.POINTER(ctypes.c_double)

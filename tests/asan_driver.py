@@ -1,0 +1,54 @@
+"""Child process of tests/test_asan.py: exercises the sanitizer builds of the oracle
+(ORACLE_LIB) and of the host-compiled device pipeline (KERNEL_HARNESS_FLAGS) on every code
+path the CPU tests reach, and checks that both still agree bit for bit. Any invalid access
+or undefined behaviour aborts the process (AddressSanitizer / -fno-sanitize-recover)."""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+from kernel_harness import KernelCPU  # noqa: E402
+from mujoco_inversedynamicstest_amd import models  # noqa: E402
+from mujoco_inversedynamicstest_amd.sampler import sample_contact_states, sample_states  # noqa
+from oracle.oracle import Oracle  # noqa: E402
+
+
+def check(name, m, q, v, a, fd=False):
+  o, k = Oracle(m), KernelCPU(m)
+  for i in range(len(q)):
+    ref = o.inverse(q[i], v[i], a[i])
+    got, _ = k.inverse(q[i], v[i], a[i])
+    if not np.array_equal(ref, got):
+      raise SystemExit(f"{name}[{i}]: host device build differs from the oracle")
+    k.inverse(q[i], v[i], a[i], classic=True)
+    o.inverse(skipstage=2)            # mjSTAGE_VEL
+    o.rne(1)
+  if fd:
+    o.set_state(q[0], v[0], a[0])
+    o.inverse_fd(1e-6, dmdq=True, sensors=m.nsensor > 0)
+  o.forward()
+  o.compare_fwd_inv()
+  print(f"{name}: {len(q)} states ok", flush=True)
+
+
+def main():
+  hc = models.load("humanoid")
+  q, v, a = sample_contact_states(hc, 24)
+  check("humanoid+contacts", hc, q, v, a)
+  h = models.load("humanoid", disable_contact=True)
+  q, v, a = sample_states(h, 16, margin=-0.1)        # limits active
+  check("humanoid+limits", h, q, v, a, fd=True)
+  for name in ("slider_crank", "inverse_test", "inertia", "linear", "weld", "connect",
+               "equality_site", "equality_compare"):
+    m = models.load(name)
+    q, v, a = sample_states(m, 8, margin=-0.1)
+    check(name, m, q, v, a, fd=name != "slider_crank")
+  print("ASAN_DRIVER_OK", flush=True)
+
+
+if __name__ == "__main__":
+  main()

@@ -10,6 +10,10 @@ from mujoco_inversedynamicstest_amd import fields, host
 HERE = os.path.dirname(os.path.abspath(__file__))
 BUILD = os.path.join(HERE, "_build")
 SO = os.path.join(BUILD, "libkernel_cpu.so")
+# KERNEL_HARNESS_FLAGS: extra g++ flags, built under another name (tests/test_asan.py)
+EXTRA = os.environ.get("KERNEL_HARNESS_FLAGS", "").split()
+if EXTRA:
+  SO = os.path.join(BUILD, "libkernel_cpu_san.so")
 SRC = [os.path.join(HERE, "cpu_kernel_harness.cpp"),
        os.path.join(HERE, "..", "include", "mjhip.h"),
        os.path.join(HERE, "..", "include", "mjhip_fields.h"),
@@ -28,7 +32,7 @@ def lib():
       # built under a private name and renamed: parallel test workers never see half a file
       tmp = f"{SO}.{os.getpid()}"
       subprocess.run(["g++", "-std=c++17", "-O2", "-ffp-contract=off", "-fPIC", "-shared",
-                      "-o", tmp, SRC[0]], check=True)
+                      *EXTRA, "-o", tmp, SRC[0]], check=True)
       os.replace(tmp, SO)
     L = ctypes.CDLL(SO)
     L.kh_sizes.restype = None

@@ -159,12 +159,32 @@ def test_full_size_properties(humanoid, eng):
   assert np.isfinite(f).all()
 
 
-def test_inverse_fd_parity(humanoid, eng):
-  """Config 5 kernel: batched mjd_inverseFD vs the oracle's serial mjd_inverseFD."""
-  q, v, a = sample_states(humanoid, 16, first=900)
-  DfDq, DfDv, DfDa, DmDq = eng.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
+def test_inverse_fd_parity(humanoid):
+  """Config 5 at its configured size: batched mjd_inverseFD over 1,024 base states (x 82
+  evaluations) vs the oracle's serial mjd_inverseFD on a subsample, and on every base state
+  the size-independent property DfDa = M (inverse dynamics is affine in qacc with slope M;
+  forward differences of an affine map are exact up to rounding / eps)."""
+  NB = 1024
+  q, v, a = sample_states(humanoid, NB, first=900)
+  e = engine.InverseEngine(humanoid, capacity=NB * (3 * humanoid.nv + 1))
+  try:
+    DfDq, DfDv, DfDa, DmDq = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
+    e.inverse(q, v, a)
+    qM = e.field("qM", 0, NB)
+  finally:
+    e.close()
+  nv = humanoid.nv
+  madr, parent = humanoid.dof_Madr, humanoid.dof_parentid
+  for i in range(NB):                   # dense M from the sparse qM of the base state
+    M = np.zeros((nv, nv))
+    for r in range(nv):
+      adr, c = madr[r], r
+      while c >= 0:
+        M[r, c] = M[c, r] = qM[i, adr]
+        adr, c = adr + 1, parent[c]
+    np.testing.assert_allclose(DfDa[i], M, rtol=1e-6, atol=1e-6 * np.abs(M).max())
   o = Oracle(humanoid)
-  for i in range(16):
+  for i in range(0, NB, 64):
     o.set_state(q[i], v[i], a[i])
     rq, rv, ra, rm = o.inverse_fd(1e-6, dmdq=True)
     # FD amplifies last-bit differences of the two builds by 1/eps = 1e6
