@@ -55,6 +55,13 @@ FRAMES_IN_PASS1 = True   # k_pos: pass 1 stores the frames, pass 2 cinert/cdof/c
 MAX_LDS_HINGES = 32
 PREFETCH = 1      # tree-pass events between a body's mirror loads and their first use
 FUSE = True       # one launch running the three stage bodies back to back per wave
+# k_va recomputes each body's frame, cinert and pre-visit cdof along its tree pass (from
+# qpos, the root's subtree_com and k_pos's hinge sin/cos in LDS) instead of re-reading them
+# from the mirror (332 fewer doubles read per humanoid instance; needs the fused kernel's LDS
+# trig). Off: the frames kept along the path make k_all spill 844 B/lane (1,228 B when cdof
+# is kept for the projections too), far worse than the reads it saves
+# (tools/kernel_resources.py). Bit-exact either way (tests/test_codegen_cpu.py).
+VA_RECOMPUTE = False
 # lanes per workgroup of each stage kernel: 64 = one instance block per wave; 32 = a block
 # split over two half-filled waves (twice the waves per SIMD, same mirror layout)
 LANES = {"pos": 64, "fac": 64, "va": 64}
@@ -787,6 +794,7 @@ def _gen_va(M: _Model, store_fields=None) -> str:
   G = _Stage(M, store_fields)
   E, m = G.E, M.m
   nv, nq, dsbl = M.nv, M.nq, M.dsbl
+  recompute = VA_RECOMPUTE and FUSE
   G.prologue()
   if M.cmode == "list":   # k_pos's work-list flag: k_constraint assembles this instance
     E("const bool cflag = ec[0] != 0;")
@@ -885,6 +893,15 @@ def _gen_va(M: _Model, store_fields=None) -> str:
 
   # mj_comVel (:1833-1896) and both mj_rne calls (:1969-2023) in one tree pass
   E("// ---- tree pass: mj_comVel + mj_rne(flg_acc=0) + mj_rne(flg_acc=1)")
+  if recompute:
+    # frames, cinert and cdof recomputed along the pass as k_pos's pass 2 computes them (the
+    # same operations on the same inputs: bit-identical values)
+    roots = sorted(set(M.rootid[1:]))
+    for r in roots:
+      E(f"double keep_stc_{r}[3];")
+      for c in range(3):
+        E(f"keep_stc_{r}[{c}] = P_subtree_com[{3 * r + c}*64];")
+    _world_frame(E)
   E("double cvel_0[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};")
   G.stv("cvel", 0, "cvel_0", 6)
   _gravity_acc(M, E)
@@ -896,12 +913,49 @@ def _gen_va(M: _Model, store_fields=None) -> str:
   # writes the block's rows out coalesced after the body (an in-place row-major store per
   # dof would scatter 64 lanes over 64 rows)
 
+  def recompute_body(i):
+    """Body i's frame, cinert_i and cdof of its dofs (mj_kinematics, mj_comPos :211-268)."""
+    _emit_frame(G, i, store=False)
+    _emit_local2global(G, f"xipos_{i}", f"ximat_{i}", m.body_ipos[i], m.body_iquat[i], i,
+                       int(m.body_sameframe[i]))
+    E(f"double cinert_{i}[10];")
+    E.open()
+    E("double off[3];")
+    E(f"mjh::sub3(off, xipos_{i}, keep_stc_{M.rootid[i]});")
+    E(f"const double inert[3] = {arr_lit(m.body_inertia[i])};")
+    E(f"mjh::inertCom(cinert_{i}, inert, ximat_{i}, off, {lit(M.mass[i])});")
+    E.close()
+    ja, jn = int(m.body_jntadr[i]), int(m.body_jntnum[i])
+    for j in range(ja, ja + jn):
+      da, t = int(m.jnt_dofadr[j]), int(m.jnt_type[j])
+      for k in range(M.jnt_ndof(j)):
+        E(f"double cdof_{da + k}[6];")
+      E.open()
+      E("double off[3], axis[3];")
+      E(f"mjh::sub3(off, keep_stc_{M.rootid[i]}, xanchor_{j});")
+      skip = 0
+      if t == FREE:
+        for k in range(3):
+          E(f"mjh::zero(cdof_{da + k}, 6); cdof_{da + k}[{3 + k}] = 1.0;")
+        skip = 3
+      if t in (FREE, BALL):
+        for k in range(3):
+          E(f"axis[0] = xmat_{i}[{k}]; axis[1] = xmat_{i}[{k + 3}]; axis[2] = xmat_{i}[{k + 6}];")
+          E(f"mjh::dofComHinge(cdof_{da + skip + k}, axis, off);")
+      elif t == SLIDE:
+        E(f"mjh::zero3(cdof_{da}); mjh::copy3(cdof_{da} + 3, xaxis_{j});")
+      else:
+        E(f"mjh::dofComHinge(cdof_{da}, xaxis_{j}, off);")
+      E.close()
+
   def pre(i):
     if not i:
       return
     bda, dn = M.bdofadr[i], M.bdofnum[i]
     p = M.parent[i]
     E.open(f"{{  // body {i}")
+    if recompute:
+      recompute_body(i)
     E(f"double cvel_{i}[6];")
     E(f"mjh::copy(cvel_{i}, cvel_{p}, 6);")
     j = 0
@@ -965,10 +1019,11 @@ def _gen_va(M: _Model, store_fields=None) -> str:
       return
     # cfrc_i is final (children added in descending order): project, then add to the parent
     # (engine_core_smooth.c:2008-2022); qfrc_inverse += armature*qacc - passive - constraint
+    cd = "cdofp"
     for k in range(M.bdofadr[i], M.bdofadr[i] + M.bdofnum[i]):
-      G.st("qfrc_bias", k, f"mjh::dot6(cdofp_{k}, cfrc_{i})")
+      G.st("qfrc_bias", k, f"mjh::dot6({cd}_{k}, cfrc_{i})")
       E.open()
-      E(f"double qfi = mjh::dot6(cdofp_{k}, frca_{i});")
+      E(f"double qfi = mjh::dot6({cd}_{k}, frca_{i});")
       if M.cmode == "all":     # raw rne: k_constraint assembles every instance
         G.st("qfrc_inverse", k, "qfi")
       else:
@@ -988,6 +1043,8 @@ def _gen_va(M: _Model, store_fields=None) -> str:
 
   def loads(kind, i):
     dofs = range(M.bdofadr[i], M.bdofadr[i] + M.bdofnum[i])
+    if recompute and kind == "pre":     # cinert and cdof recomputed, qacc from the mirror
+      return [], [(f"qacc[{k}]", "qacc", k) for k in dofs]
     if kind == "pre":
       decls = [f"double cinert_{i}[10];"] + [f"double cdof_{k}[6];" for k in dofs]
       ld = _vec_loads(f"cinert_{i}", "cinert", 10 * i, 10)
@@ -1063,8 +1120,9 @@ _SIG = {
             "qpos_in, qvel_in, qacc_in, worklist, worklist_count, worklist_next, efc_count, trig"),
     "fac": ("int* __restrict__ efc_count", "efc_count"),
     "va": ("double* __restrict__ qfrc_out, int* __restrict__ status, "
-           "int* __restrict__ efc_count, double* __restrict__ qo_lds",
-           "qfrc_out, status, efc_count, qo_lds"),
+           "int* __restrict__ efc_count, double* __restrict__ qo_lds, "
+           "double* __restrict__ trig",
+           "qfrc_out, status, efc_count, qo_lds, trig"),
 }
 _GEN = {"pos": lambda M, sf: _gen_pos(M, sf), "fac": lambda M, sf: _gen_fac(M, sf),
         "va": lambda M, sf: _gen_va(M, sf)}
@@ -1115,6 +1173,8 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
       decl = f"  __shared__ double trig[{max(1, 2 * len(M.trig) * nl)}];\n"
     elif st == "va":
       params = params.replace(", double* __restrict__ qo_lds", "")
+      params = params.replace(", double* __restrict__ trig", "")
+      args = args.replace(", trig", ", nullptr")   # staged k_va: no LDS trig (not fused)
       decl = f"  __shared__ double qo_lds[{nl * max(M.nv, 1)}];\n"
       if M.cmode != "all":   # coalesced row-major copy of the workgroup's qfrc_inverse rows
         tail = (f"  if (!qfrc_out) return;\n  __syncthreads();\n"
