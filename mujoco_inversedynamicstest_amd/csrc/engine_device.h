@@ -3694,7 +3694,175 @@ MJH_HD void sensorVel(const mjhipModel& m, const Lane<S>& d) {
   applyCutoff(m, d, mjhipSTAGE_VEL);
 }
 
-// engine_sensor.c:677-915 mj_sensorAcc (no touch, rejected at load)
+// engine_ray.c ray-zone tests for the touch sensor (mju_rayGeom :818-846 and the primitive
+// intersections :37-445), on local copies of the zone's frame
+MJH_HD void rayMap(const double* pos, const double* mat, const double* pnt, const double* vec,
+                   double* lpnt, double* lvec) {
+  const double dif[3] = {pnt[0]-pos[0], pnt[1]-pos[1], pnt[2]-pos[2]};
+  lpnt[0] = mat[0]*dif[0] + mat[3]*dif[1] + mat[6]*dif[2];
+  lpnt[1] = mat[1]*dif[0] + mat[4]*dif[1] + mat[7]*dif[2];
+  lpnt[2] = mat[2]*dif[0] + mat[5]*dif[1] + mat[8]*dif[2];
+  lvec[0] = mat[0]*vec[0] + mat[3]*vec[1] + mat[6]*vec[2];
+  lvec[1] = mat[1]*vec[0] + mat[4]*vec[1] + mat[7]*vec[2];
+  lvec[2] = mat[2]*vec[0] + mat[5]*vec[1] + mat[8]*vec[2];
+}
+
+MJH_HD double rayQuad(double a, double b, double c, double* x) {
+  double det = b*b - a*c;
+  if (det < MINVAL) {
+    x[0] = -1;
+    x[1] = -1;
+    return -1;
+  }
+  det = sqrt(det);
+  x[0] = (-b-det)/a;
+  x[1] = (-b+det)/a;
+  if (x[0] >= 0) return x[0];
+  if (x[1] >= 0) return x[1];
+  return -1;
+}
+
+MJH_HD double raySphere(const double* pos, double dist_sqr, const double* pnt,
+                        const double* vec) {
+  const double dif[3] = {pnt[0]-pos[0], pnt[1]-pos[1], pnt[2]-pos[2]};
+  const double a = vec[0]*vec[0] + vec[1]*vec[1] + vec[2]*vec[2];
+  const double b = vec[0]*dif[0] + vec[1]*dif[1] + vec[2]*dif[2];
+  const double c = dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2] - dist_sqr;
+  double xx[2];
+  return rayQuad(a, b, c, xx);
+}
+
+MJH_HD double rayGeom(const double* pos, const double* mat, const double* size,
+                      const double* pnt, const double* vec, int type) {
+  double lpnt[3], lvec[3], xx[2], x = -1, sol;
+  if (type == mjhipGEOM_SPHERE) return raySphere(pos, size[0]*size[0], pnt, vec);
+  if (type == mjhipGEOM_CAPSULE) {
+    const double ssz = size[0] + size[1];
+    if (raySphere(pos, ssz*ssz, pnt, vec) < 0) return -1;
+  } else if (type == mjhipGEOM_CYLINDER) {
+    if (raySphere(pos, size[0]*size[0] + size[1]*size[1], pnt, vec) < 0) return -1;
+  } else if (type == mjhipGEOM_BOX) {
+    if (raySphere(pos, size[0]*size[0] + size[1]*size[1] + size[2]*size[2], pnt, vec) < 0) {
+      return -1;
+    }
+  } else if (type != mjhipGEOM_PLANE && type != mjhipGEOM_ELLIPSOID) {
+    return -1;
+  }
+  rayMap(pos, mat, pnt, vec, lpnt, lvec);
+  if (type == mjhipGEOM_PLANE) {                        // ray_plane :191-218
+    if (lvec[2] > -MINVAL) return -1;
+    x = -lpnt[2]/lvec[2];
+    if (x < 0) return -1;
+    const double p0 = lpnt[0] + x*lvec[0], p1 = lpnt[1] + x*lvec[1];
+    return ((size[0] <= 0 || fabs(p0) <= size[0]) && (size[1] <= 0 || fabs(p1) <= size[1]))
+           ? x : -1;
+  }
+  if (type == mjhipGEOM_ELLIPSOID) {                    // ray_ellipsoid :305-323
+    const double sx = 1/(size[0]*size[0]), sy = 1/(size[1]*size[1]), sz = 1/(size[2]*size[2]);
+    const double a = sx*lvec[0]*lvec[0] + sy*lvec[1]*lvec[1] + sz*lvec[2]*lvec[2];
+    const double b = sx*lvec[0]*lpnt[0] + sy*lvec[1]*lpnt[1] + sz*lvec[2]*lpnt[2];
+    const double c = sx*lpnt[0]*lpnt[0] + sy*lpnt[1]*lpnt[1] + sz*lpnt[2]*lpnt[2] - 1;
+    return rayQuad(a, b, c, xx);
+  }
+  if (type == mjhipGEOM_BOX) {                          // ray_box :387-445
+    const int iface[3][2] = {{1, 2}, {0, 2}, {0, 1}};
+    for (int i = 0; i < 3; i++) {
+      if (fabs(lvec[i]) > MINVAL) {
+        for (int side = -1; side <= 1; side += 2) {
+          sol = (side*size[i]-lpnt[i])/lvec[i];
+          if (sol >= 0) {
+            const double p0 = lpnt[iface[i][0]] + sol*lvec[iface[i][0]];
+            const double p1 = lpnt[iface[i][1]] + sol*lvec[iface[i][1]];
+            if (fabs(p0) <= size[iface[i][0]] && fabs(p1) <= size[iface[i][1]]) {
+              if (x < 0 || sol < x) x = sol;
+            }
+          }
+        }
+      }
+    }
+    return x;
+  }
+  if (type == mjhipGEOM_CYLINDER && fabs(lvec[2]) > MINVAL) {   // ray_cylinder flat sides
+    for (int side = -1; side <= 1; side += 2) {
+      sol = (side*size[1]-lpnt[2])/lvec[2];
+      if (sol >= 0) {
+        const double p0 = lpnt[0] + sol*lvec[0], p1 = lpnt[1] + sol*lvec[1];
+        if (p0*p0 + p1*p1 <= size[0]*size[0]) {
+          if (x < 0 || sol < x) x = sol;
+        }
+      }
+    }
+  }
+  // round side between the flat sides (cylinder :360-380, capsule :250-265)
+  double a = lvec[0]*lvec[0] + lvec[1]*lvec[1];
+  double b = lvec[0]*lpnt[0] + lvec[1]*lpnt[1];
+  double c = lpnt[0]*lpnt[0] + lpnt[1]*lpnt[1] - size[0]*size[0];
+  sol = rayQuad(a, b, c, xx);
+  if (sol >= 0 && fabs(lpnt[2]+sol*lvec[2]) <= size[1]) {
+    if (x < 0 || sol < x) x = sol;
+  }
+  if (type == mjhipGEOM_CAPSULE) {                      // hemispheres :267-300
+    double ldif[3] = {lpnt[0], lpnt[1], lpnt[2]-size[1]};
+    a = lvec[0]*lvec[0] + lvec[1]*lvec[1] + lvec[2]*lvec[2];
+    b = lvec[0]*ldif[0] + lvec[1]*ldif[1] + lvec[2]*ldif[2];
+    c = ldif[0]*ldif[0] + ldif[1]*ldif[1] + ldif[2]*ldif[2] - size[0]*size[0];
+    rayQuad(a, b, c, xx);
+    for (int i = 0; i < 2; i++) {
+      if (xx[i] >= 0 && lpnt[2]+xx[i]*lvec[2] >= size[1]) {
+        if (x < 0 || xx[i] < x) x = xx[i];
+      }
+    }
+    ldif[2] = lpnt[2]+size[1];
+    b = lvec[0]*ldif[0] + lvec[1]*ldif[1] + lvec[2]*ldif[2];
+    c = ldif[0]*ldif[0] + ldif[1]*ldif[1] + ldif[2]*ldif[2] - size[0]*size[0];
+    rayQuad(a, b, c, xx);
+    for (int i = 0; i < 2; i++) {
+      if (xx[i] >= 0 && lpnt[2]+xx[i]*lvec[2] <= -size[1]) {
+        if (x < 0 || xx[i] < x) x = xx[i];
+      }
+    }
+  }
+  return x;
+}
+
+// the touch sensor (engine_sensor.c:750-793): the normal forces of the site body's contacts
+// whose normal ray from the contact point hits the site's zone
+template <int S>
+MJH_HD double touchSensor(const mjhipModel& m, const Lane<S>& d, int objid) {
+  const int bodyid = m.site_bodyid[objid];
+  const int ncon = d.con_cap ? d.con_count[0] : 0;
+  double pos[3], mat[9], total = 0;
+  for (int k = 0; k < 3; k++) pos[k] = d.site_xpos[3*objid + k];
+  for (int k = 0; k < 9; k++) mat[k] = d.site_xmat[9*objid + k];
+  for (int j = 0; j < ncon; j++) {
+    const int g0 = d.con_geom[2*j], g1 = d.con_geom[2*j + 1];
+    const int b0 = g0 >= 0 ? m.geom_bodyid[g0] : -1, b1 = g1 >= 0 ? m.geom_bodyid[g1] : -1;
+    const int adr = d.con_efc_address[j];
+    if (adr < 0 || (bodyid != b0 && bodyid != b1)) continue;
+    double fn;                                         // mj_contactForce, normal component
+    const int dim = d.con_dim[j];
+    if (m.opt.cone == mjhipCONE_ELLIPTIC || dim == 1) {
+      fn = d.efc_force[adr];
+    } else {
+      fn = 0;
+      for (int k = 0; k < 2*(dim-1); k++) fn += d.efc_force[adr + k];
+    }
+    if (fn <= 0) continue;
+    double ray[3], pnt[3];
+    for (int k = 0; k < 3; k++) ray[k] = d.con_frame[9*j + k]*fn;
+    normalize3(ray);
+    if (bodyid == b1) {
+      for (int k = 0; k < 3; k++) ray[k] = ray[k]*-1;
+    }
+    for (int k = 0; k < 3; k++) pnt[k] = d.con_pos[3*j + k];
+    if (rayGeom(pos, mat, m.site_size + 3*objid, pnt, ray, m.site_type[objid]) >= 0) {
+      total += fn;
+    }
+  }
+  return total;
+}
+
+// engine_sensor.c:677-915 mj_sensorAcc
 template <int S>
 MJH_HD void sensorAcc(const mjhipModel& m, const Lane<S>& d) {
   if (m.opt.disableflags & mjhipDSBL_SENSOR) return;
@@ -3713,6 +3881,7 @@ MJH_HD void sensorAcc(const mjhipModel& m, const Lane<S>& d) {
       post = true;
     }
     switch (type) {
+    case mjhSENS_TOUCH: out[0] = touchSensor(m, d, objid); break;
     case mjhSENS_ACCELEROMETER:
       objectAcceleration(m, d, 6, objid, tmp, 1);
       copy3(out, tmp + 3);

@@ -760,9 +760,9 @@ static const char* unsupported(const mjhipModel* m) {
   }
   for (int i = 0; i < m->nsensor; i++) {
     const int t = m->sensor_type[i];
-    if (t == mjhSENS_TOUCH || t == mjhSENS_RANGEFINDER || t == mjhSENS_CAMPROJECTION ||
+    if (t == mjhSENS_RANGEFINDER || t == mjhSENS_CAMPROJECTION ||
         (t >= mjhSENS_GEOMDIST && t <= mjhSENS_GEOMFROMTO) || t > mjhSENS_CLOCK) {
-      return "touch/rangefinder/camprojection/geom-distance/plugin/user sensors";
+      return "rangefinder/camprojection/geom-distance/plugin/user sensors";
     }
   }
   return nullptr;

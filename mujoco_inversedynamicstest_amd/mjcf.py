@@ -48,6 +48,7 @@ OBJ = {"body": 1, "xbody": 2, "joint": 3, "dof": 4, "geom": 5, "site": 6, "camer
 # (dim, datatype, needstage). Stages: 1 POS, 2 VEL, 3 ACC. Datatypes: 0 REAL, 1 POSITIVE,
 # 2 AXIS, 3 QUATERNION. Frame sensors read objtype/objname (+ reftype/refname).
 SENSORS = {
+    "touch": (0, "site", 6, 1, 1, 3),
     "accelerometer": (1, "site", 6, 3, 0, 3), "velocimeter": (2, "site", 6, 3, 0, 2),
     "gyro": (3, "site", 6, 3, 0, 2), "force": (4, "site", 6, 3, 0, 3),
     "torque": (5, "site", 6, 3, 0, 3), "magnetometer": (6, "site", 6, 3, 0, 1),
@@ -71,7 +72,7 @@ SENSORS = {
     "e_potential": (40, None, 0, 1, 0, 1), "e_kinetic": (41, None, 0, 1, 0, 1),
     "clock": (42, None, 0, 1, 0, 1),
 }
-SENSORS_NEXT = ("touch", "rangefinder", "camprojection", "distance", "normal", "fromto",
+SENSORS_NEXT = ("rangefinder", "camprojection", "distance", "normal", "fromto",
                 "user", "plugin")
 GEOM = {"plane": 0, "hfield": 1, "sphere": 2, "capsule": 3, "ellipsoid": 4,
         "cylinder": 5, "box": 6, "mesh": 7, "sdf": 8}

@@ -3460,7 +3460,207 @@ static void or_sensorVel(const mjhipModel* m, mjhipData* d, const orEfc* e) {
   or_applyCutoff(m, d, mjhipSTAGE_VEL);
 }
 
-/* engine_sensor.c:677-915 mj_sensorAcc (no touch) */
+/*================================= engine_ray.c (touch zones) =============================*/
+
+/* ray_map :37-52: ray in the geom's local frame */
+static void or_rayMap(const mjtNum* pos, const mjtNum* mat, const mjtNum* pnt, const mjtNum* vec,
+                      mjtNum* lpnt, mjtNum* lvec) {
+  const mjtNum dif[3] = {pnt[0]-pos[0], pnt[1]-pos[1], pnt[2]-pos[2]};
+  lpnt[0] = mat[0]*dif[0] + mat[3]*dif[1] + mat[6]*dif[2];
+  lpnt[1] = mat[1]*dif[0] + mat[4]*dif[1] + mat[7]*dif[2];
+  lpnt[2] = mat[2]*dif[0] + mat[5]*dif[1] + mat[8]*dif[2];
+  lvec[0] = mat[0]*vec[0] + mat[3]*vec[1] + mat[6]*vec[2];
+  lvec[1] = mat[1]*vec[0] + mat[4]*vec[1] + mat[7]*vec[2];
+  lvec[2] = mat[2]*vec[0] + mat[5]*vec[1] + mat[8]*vec[2];
+}
+
+/* ray_quad :105-127: a x^2 + 2 b x + c = 0, smallest non-negative root or -1 */
+static mjtNum or_rayQuad(mjtNum a, mjtNum b, mjtNum c, mjtNum* x) {
+  mjtNum det = b*b - a*c;
+  if (det < mjMINVAL) {
+    x[0] = -1;
+    x[1] = -1;
+    return -1;
+  }
+  det = sqrt(det);
+  x[0] = (-b-det)/a;
+  x[1] = (-b+det)/a;
+  if (x[0] >= 0) return x[0];
+  if (x[1] >= 0) return x[1];
+  return -1;
+}
+
+/* ray_plane :191-218 */
+static mjtNum or_rayPlane(const mjtNum* pos, const mjtNum* mat, const mjtNum* size,
+                          const mjtNum* pnt, const mjtNum* vec) {
+  mjtNum lpnt[3], lvec[3];
+  or_rayMap(pos, mat, pnt, vec, lpnt, lvec);
+  if (lvec[2] > -mjMINVAL) return -1;
+  const mjtNum x = -lpnt[2]/lvec[2];
+  if (x < 0) return -1;
+  mjtNum p0 = lpnt[0] + x*lvec[0], p1 = lpnt[1] + x*lvec[1];
+  if ((size[0] <= 0 || fabs(p0) <= size[0]) && (size[1] <= 0 || fabs(p1) <= size[1])) return x;
+  return -1;
+}
+
+/* ray_sphere :222-235 (mat unused) */
+static mjtNum or_raySphere(const mjtNum* pos, mjtNum dist_sqr, const mjtNum* pnt,
+                           const mjtNum* vec) {
+  mjtNum dif[3] = {pnt[0]-pos[0], pnt[1]-pos[1], pnt[2]-pos[2]};
+  mjtNum a = vec[0]*vec[0] + vec[1]*vec[1] + vec[2]*vec[2];
+  mjtNum b = vec[0]*dif[0] + vec[1]*dif[1] + vec[2]*dif[2];
+  mjtNum c = dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2] - dist_sqr;
+  mjtNum xx[2];
+  return or_rayQuad(a, b, c, xx);
+}
+
+/* ray_capsule :238-301: round side between the flat sides, then the two hemispheres */
+static mjtNum or_rayCapsule(const mjtNum* pos, const mjtNum* mat, const mjtNum* size,
+                            const mjtNum* pnt, const mjtNum* vec) {
+  mjtNum ssz = size[0] + size[1];
+  if (or_raySphere(pos, ssz*ssz, pnt, vec) < 0) return -1;
+  mjtNum lpnt[3], lvec[3];
+  or_rayMap(pos, mat, pnt, vec, lpnt, lvec);
+  mjtNum x = -1, sol, xx[2];
+  mjtNum a = lvec[0]*lvec[0] + lvec[1]*lvec[1];
+  mjtNum b = lvec[0]*lpnt[0] + lvec[1]*lpnt[1];
+  mjtNum c = lpnt[0]*lpnt[0] + lpnt[1]*lpnt[1] - size[0]*size[0];
+  sol = or_rayQuad(a, b, c, xx);
+  if (sol >= 0 && fabs(lpnt[2]+sol*lvec[2]) <= size[1]) {
+    if (x < 0 || sol < x) x = sol;
+  }
+  mjtNum ldif[3] = {lpnt[0], lpnt[1], lpnt[2]-size[1]};
+  a = lvec[0]*lvec[0] + lvec[1]*lvec[1] + lvec[2]*lvec[2];
+  b = lvec[0]*ldif[0] + lvec[1]*ldif[1] + lvec[2]*ldif[2];
+  c = ldif[0]*ldif[0] + ldif[1]*ldif[1] + ldif[2]*ldif[2] - size[0]*size[0];
+  or_rayQuad(a, b, c, xx);
+  for (int i = 0; i < 2; i++) {
+    if (xx[i] >= 0 && lpnt[2]+xx[i]*lvec[2] >= size[1]) {
+      if (x < 0 || xx[i] < x) x = xx[i];
+    }
+  }
+  ldif[2] = lpnt[2]+size[1];
+  b = lvec[0]*ldif[0] + lvec[1]*ldif[1] + lvec[2]*ldif[2];
+  c = ldif[0]*ldif[0] + ldif[1]*ldif[1] + ldif[2]*ldif[2] - size[0]*size[0];
+  or_rayQuad(a, b, c, xx);
+  for (int i = 0; i < 2; i++) {
+    if (xx[i] >= 0 && lpnt[2]+xx[i]*lvec[2] <= -size[1]) {
+      if (x < 0 || xx[i] < x) x = xx[i];
+    }
+  }
+  return x;
+}
+
+/* ray_ellipsoid :305-323 */
+static mjtNum or_rayEllipsoid(const mjtNum* pos, const mjtNum* mat, const mjtNum* size,
+                              const mjtNum* pnt, const mjtNum* vec) {
+  mjtNum lpnt[3], lvec[3];
+  or_rayMap(pos, mat, pnt, vec, lpnt, lvec);
+  mjtNum s[3] = {1/(size[0]*size[0]), 1/(size[1]*size[1]), 1/(size[2]*size[2])};
+  mjtNum a = s[0]*lvec[0]*lvec[0] + s[1]*lvec[1]*lvec[1] + s[2]*lvec[2]*lvec[2];
+  mjtNum b = s[0]*lvec[0]*lpnt[0] + s[1]*lvec[1]*lpnt[1] + s[2]*lvec[2]*lpnt[2];
+  mjtNum c = s[0]*lpnt[0]*lpnt[0] + s[1]*lpnt[1]*lpnt[1] + s[2]*lpnt[2]*lpnt[2] - 1;
+  mjtNum xx[2];
+  return or_rayQuad(a, b, c, xx);
+}
+
+/* ray_cylinder :327-383: the flat sides, then the round side between them */
+static mjtNum or_rayCylinder(const mjtNum* pos, const mjtNum* mat, const mjtNum* size,
+                             const mjtNum* pnt, const mjtNum* vec) {
+  mjtNum ssz = size[0]*size[0] + size[1]*size[1];
+  if (or_raySphere(pos, ssz, pnt, vec) < 0) return -1;
+  mjtNum lpnt[3], lvec[3];
+  or_rayMap(pos, mat, pnt, vec, lpnt, lvec);
+  mjtNum x = -1, sol;
+  if (fabs(lvec[2]) > mjMINVAL) {
+    for (int side = -1; side <= 1; side += 2) {
+      sol = (side*size[1]-lpnt[2])/lvec[2];
+      if (sol >= 0) {
+        mjtNum p0 = lpnt[0] + sol*lvec[0], p1 = lpnt[1] + sol*lvec[1];
+        if (p0*p0 + p1*p1 <= size[0]*size[0]) {
+          if (x < 0 || sol < x) x = sol;
+        }
+      }
+    }
+  }
+  mjtNum a = lvec[0]*lvec[0] + lvec[1]*lvec[1];
+  mjtNum b = lvec[0]*lpnt[0] + lvec[1]*lpnt[1];
+  mjtNum c = lpnt[0]*lpnt[0] + lpnt[1]*lpnt[1] - size[0]*size[0];
+  mjtNum xx[2];
+  sol = or_rayQuad(a, b, c, xx);
+  if (sol >= 0 && fabs(lpnt[2]+sol*lvec[2]) <= size[1]) {
+    if (x < 0 || sol < x) x = sol;
+  }
+  return x;
+}
+
+/* ray_box :387-445 (without the per-face output) */
+static mjtNum or_rayBox(const mjtNum* pos, const mjtNum* mat, const mjtNum* size,
+                        const mjtNum* pnt, const mjtNum* vec) {
+  mjtNum ssz = size[0]*size[0] + size[1]*size[1] + size[2]*size[2];
+  if (or_raySphere(pos, ssz, pnt, vec) < 0) return -1;
+  const int iface[3][2] = {{1, 2}, {0, 2}, {0, 1}};
+  mjtNum lpnt[3], lvec[3];
+  or_rayMap(pos, mat, pnt, vec, lpnt, lvec);
+  mjtNum x = -1, sol;
+  for (int i = 0; i < 3; i++) {
+    if (fabs(lvec[i]) > mjMINVAL) {
+      for (int side = -1; side <= 1; side += 2) {
+        sol = (side*size[i]-lpnt[i])/lvec[i];
+        if (sol >= 0) {
+          mjtNum p0 = lpnt[iface[i][0]] + sol*lvec[iface[i][0]];
+          mjtNum p1 = lpnt[iface[i][1]] + sol*lvec[iface[i][1]];
+          if (fabs(p0) <= size[iface[i][0]] && fabs(p1) <= size[iface[i][1]]) {
+            if (x < 0 || sol < x) x = sol;
+          }
+        }
+      }
+    }
+  }
+  return x;
+}
+
+/* mju_rayGeom :818-846 for the primitive types a site can have */
+static mjtNum or_rayGeom(const mjtNum* pos, const mjtNum* mat, const mjtNum* size,
+                         const mjtNum* pnt, const mjtNum* vec, int type) {
+  switch (type) {
+  case mjhipGEOM_PLANE:     return or_rayPlane(pos, mat, size, pnt, vec);
+  case mjhipGEOM_SPHERE:    return or_raySphere(pos, size[0]*size[0], pnt, vec);
+  case mjhipGEOM_CAPSULE:   return or_rayCapsule(pos, mat, size, pnt, vec);
+  case mjhipGEOM_ELLIPSOID: return or_rayEllipsoid(pos, mat, size, pnt, vec);
+  case mjhipGEOM_CYLINDER:  return or_rayCylinder(pos, mat, size, pnt, vec);
+  case mjhipGEOM_BOX:       return or_rayBox(pos, mat, size, pnt, vec);
+  default:                  return -1;
+  }
+}
+
+/* the touch sensor (engine_sensor.c:750-793): normal forces of the contacts of the site's
+ * body whose normal ray, from the contact point, hits the site's zone */
+static mjtNum or_touch(const mjhipModel* m, const mjhipData* d, const orEfc* e, int objid) {
+  int bodyid = m->site_bodyid[objid];
+  mjtNum total = 0, conforce[6], conray[3];
+  for (int j = 0; j < e->ncon; j++) {
+    int conbody[2];
+    for (int k = 0; k < 2; k++) {
+      int g = e->con_geom[2*j+k];
+      conbody[k] = g >= 0 ? m->geom_bodyid[g] : -1;
+    }
+    if (e->con_efc_address[j] >= 0 && (bodyid == conbody[0] || bodyid == conbody[1])) {
+      or_contactForce(m, e, j, conforce);
+      if (conforce[0] <= 0) continue;
+      mju_scl3(conray, e->con_frame + 9*j, conforce[0]);
+      mju_normalize3(conray);
+      if (bodyid == conbody[1]) mju_scl3(conray, conray, -1);
+      if (or_rayGeom(d->site_xpos + 3*objid, d->site_xmat + 9*objid, m->site_size + 3*objid,
+                     e->con_pos + 3*j, conray, m->site_type[objid]) >= 0) {
+        total += conforce[0];
+      }
+    }
+  }
+  return total;
+}
+
+/* engine_sensor.c:677-915 mj_sensorAcc */
 static void or_sensorAcc(const mjhipModel* m, mjhipData* d, const orEfc* e) {
   if (mjDISABLED(mjhipDSBL_SENSOR)) return;
   int rnePost = 0;
@@ -3476,6 +3676,9 @@ static void or_sensorAcc(const mjhipModel* m, mjhipData* d, const orEfc* e) {
       rnePost = 1;
     }
     switch (type) {
+    case SENS_TOUCH:
+      out[0] = or_touch(m, d, e, objid);
+      break;
     case SENS_ACCELEROMETER:
       or_objectAcceleration(m, d, OBJ_SITE, objid, tmp, 1);
       mju_copy3(out, tmp + 3);

@@ -387,7 +387,7 @@ def test_sensor_skip_stages_keep_values():
 
 
 def test_unsupported_sensors_rejected():
-  for tag in ("touch", "rangefinder"):
+  for tag in ("rangefinder", "camprojection"):
     with pytest.raises(mjcf.MJCFError):
       mjcf.load_xml_string(f"""<mujoco><worldbody><site name="s"/></worldbody>
         <sensor><{tag} site="s"/></sensor></mujoco>""")
@@ -427,3 +427,83 @@ def test_contact_forces_in_rne_post_constraint_bitexact():
     for f in ("sensordata", "cfrc_ext", "cfrc_int", "cacc", "qfrc_inverse"):
       np.testing.assert_array_equal(getattr(k.d, f), getattr(o.d, f), err_msg=f"{f} {i}")
   assert ncon > 0
+
+
+# the touch sensor (engine_sensor.c:750-793, mju_rayGeom engine_ray.c:818-846)
+_TOUCH_XML = """<mujoco><default><geom solimp="0.9 0.9 .001"/></default>
+  <worldbody><geom type="plane" size="1 1 1"/>
+  <body pos="0 0 .2"><joint type="slide" axis="0 0 1"/><geom size=".1"/>
+    <site name="all" type="{zone}" size="{size}"/>
+    <site name="top" type="box" size=".2 .2 .02" pos="0 0 .1"/></body>
+  </worldbody>
+  <sensor><touch site="all"/><touch site="top"/></sensor></mujoco>"""
+
+
+@pytest.mark.parametrize("zone,size", [("box", ".2 .2 .2"), ("sphere", ".15"),
+                                       ("capsule", ".12 .1"), ("ellipsoid", ".2 .2 .15"),
+                                       ("cylinder", ".15 .15")])
+def test_touch_holds_the_weight_at_rest(zone, size):
+  """At the RestPenetration depth (test_contacts_cpu.py, engine_core_constraint_test.cc
+  :161-229) the contact's normal force equals the weight: a touch zone of any primitive
+  shape around the sphere's bottom reports m g; a zone the contact ray misses (a thin box on
+  the sphere's top, whose ray points up from the contact at the bottom) reports 0. Device on
+  the host equals the oracle bit for bit."""
+  m = mjcf.load_xml_string(_TOUCH_XML.format(zone=zone, size=size))
+  g = -m.opt["gravity"][2]
+  imp, ref = 0.9, 0.02
+  depth = g * (1 - imp) * ref ** 2            # solref (0.02, 1) timeconst/dampratio
+  o = Oracle(m)
+  q = np.array([-0.1 - depth])
+  o.inverse(q, np.zeros(1), np.zeros(1))
+  weight = m.body_mass[1] * g
+  assert o.efc.ncon == 1
+  assert _sensor(m, o.d, 0)[0] == pytest.approx(weight, rel=1e-9)
+  assert _sensor(m, o.d, 1)[0] == 0.0
+  k = KernelCPU(m)
+  k.inverse(q, np.zeros(1), np.zeros(1))
+  np.testing.assert_array_equal(k.d.sensordata, o.d.sensordata)
+
+
+def test_touch_sums_contacts_and_flips_for_body2():
+  """Touch zones on a free box resting on a plane (corner contacts) with a sphere lying on
+  it. For the box the plane contacts' normal points into it (it is the contacts' second
+  geom, so the ray flips to point down): the zone around the whole box contains every
+  contact point and sums all of the box's normal forces; a small cylinder zone on the box's
+  top holds only the sphere contact's point and sums only its force (the corner rays point
+  down, away from it); the sphere's zone reports the sphere contact. Random states, device
+  on the host vs the oracle bit for bit."""
+  m = mjcf.load_xml_string("""<mujoco><worldbody><geom type="plane" size="2 2 1"/>
+    <body name="box" pos="0 0 .1"><freejoint/><geom type="box" size=".2 .15 .1"/>
+      <site name="zb" type="box" size=".25 .2 .12"/>
+      <site name="zt" type="cylinder" size=".1 .05" pos="0 0 .1"/></body>
+    <body name="ball" pos="0 0 .29"><freejoint/><geom size=".09"/>
+      <site name="zs" type="sphere" size=".12"/></body></worldbody>
+    <sensor><touch site="zb"/><touch site="zt"/><touch site="zs"/></sensor></mujoco>""")
+  o, k = Oracle(m), KernelCPU(m)
+  rng = np.random.default_rng(11)
+  hits = np.zeros(3)
+  for i in range(16):
+    q = np.array(m.qpos0, dtype=float)
+    q[2] = 0.1 - 0.002 + 0.001 * rng.normal()
+    q[3:7] += 0.01 * rng.normal(size=4)
+    q[9] = 0.29 - 0.003 + 0.001 * rng.normal()
+    v = 0.05 * rng.normal(size=m.nv)
+    a = rng.normal(size=m.nv)
+    o.inverse(q, v, a)
+    k.inverse(q, v, a)
+    np.testing.assert_array_equal(k.d.sensordata, o.d.sensordata, err_msg=str(i))
+    hits += o.d.sensordata > 0
+    plane, ball = 0.0, 0.0
+    for c in range(o.efc.ncon):
+      adr = o.contact_field("con_efc_address")[c]
+      fr = o.efc_field("efc_force")[adr:adr + 4].sum()
+      g1, g2 = o.contact_field("con_geom")[c]
+      bodies = {int(m.geom_bodyid[g1]), int(m.geom_bodyid[g2])}
+      if fr > 0 and bodies == {0, 1}:
+        plane += fr
+      elif fr > 0 and bodies == {1, 2}:
+        ball += fr
+    assert o.d.sensordata[0] == pytest.approx(plane + ball, rel=1e-12, abs=1e-12)
+    assert o.d.sensordata[1] == pytest.approx(ball, rel=1e-12, abs=1e-12)
+    assert o.d.sensordata[2] == pytest.approx(ball, rel=1e-12, abs=1e-12)
+  assert hits.min() > 0
