@@ -138,8 +138,37 @@ def _dptr(a):
   return None
 
 
+class _TorchOrder:
+  """Orders a device-pointer call after the work queued on torch's current stream and
+  torch's later work after the call: the context's stream waits on an event recorded on
+  torch's stream, and torch's stream waits on one recorded after the launch. Nothing is
+  added when the context already runs on torch's current stream (set_stream)."""
+
+  def __init__(self, engine):
+    self.engine = engine
+    self.ts = self.cs = None
+
+  def __enter__(self):
+    import torch
+    ts = torch.cuda.current_stream(self.engine.device)
+    if ts.cuda_stream != (self.engine.stream or 0):
+      self.ts = ts
+      self.cs = torch.cuda.ExternalStream(self.engine.stream, device=self.engine.device)
+      self.cs.wait_stream(ts)
+    return self
+
+  def __exit__(self, *exc):
+    if self.ts is not None:
+      self.ts.wait_stream(self.cs)
+    return False
+
+
 class InverseEngine:
-  """Batched mj_inverse for one model on one device (an mjhipContext)."""
+  """Batched mj_inverse for one model on one device (an mjhipContext).
+
+  Calls with torch tensors run asynchronously on the context's stream, ordered with torch's
+  current stream (inputs written by earlier torch work are read, and later torch work sees
+  the outputs); host-array calls are synchronous."""
 
   def __init__(self, model, capacity: int, device: int = 0, specialize=None):
     """specialize: generate and load a straight-line kernel for a model that has no bundled
@@ -225,8 +254,13 @@ class InverseEngine:
         out = np.zeros((B, self.nv))
       po = out.ctypes.data
       st = np.zeros(B, dtype=np.int32)
-    rc = L.mjhip_inverseBatch(self.ctx, B, pq, pv, pa, po, skipstage, skipsensor, flags,
-                              st.ctypes.data_as(_I) if st is not None else None)
+    if dev and (out is not None or not mirror_input):
+      with _TorchOrder(self):
+        rc = L.mjhip_inverseBatch(self.ctx, B, pq, pv, pa, po, skipstage, skipsensor, flags,
+                                  None)
+    else:
+      rc = L.mjhip_inverseBatch(self.ctx, B, pq, pv, pa, po, skipstage, skipsensor, flags,
+                                st.ctypes.data_as(_I) if st is not None else None)
     _check(rc, "mjhip_inverseBatch")
     if status:
       return out, st
@@ -326,12 +360,13 @@ class InverseEngine:
           out = out + ((mk(ns), mk(ns), mk(ns)),)
       ptr = lambda t: None if t is None else _dptr(t)
       Ds = out[4] if len(out) > 4 else (None, None, None)
-      _check(lib().mjhip_inverseFDBatchEx(self.ctx, B, _dptr(qpos), _dptr(qvel), _dptr(qacc),
+      with _TorchOrder(self):
+        rc = lib().mjhip_inverseFDBatchEx(self.ctx, B, _dptr(qpos), _dptr(qvel), _dptr(qacc),
                                           None if ctrl is None else _dptr(ctrl), eps,
                                           int(bool(flg_actuation)), ptr(out[0]), ptr(out[1]),
                                           ptr(out[2]), *map(ptr, Ds), ptr(out[3]),
-                                          FLAG_DEVICE_PTRS),
-             "mjhip_inverseFDBatchEx")
+                                          FLAG_DEVICE_PTRS)
+      _check(rc, "mjhip_inverseFDBatchEx")
       return tuple(out)
     qpos = np.ascontiguousarray(qpos, dtype=np.float64).reshape(-1, self.nq)
     qvel = np.ascontiguousarray(qvel, dtype=np.float64).reshape(-1, self.nv)

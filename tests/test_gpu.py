@@ -374,9 +374,39 @@ def test_device_tensor_io(humanoid, eng):
   torch.cuda.synchronize()
   eng.inverse(tq, tv, ta, out=out)
   torch.cuda.synchronize()
-  # the library stream is non-blocking w.r.t. torch: synchronize it too
   ref = eng.inverse(q, v, a)
   np.testing.assert_array_equal(out.cpu().numpy(), ref)
+
+
+def test_device_tensor_stream_order(humanoid):
+  """Device-tensor calls are ordered with torch's current stream without any explicit
+  synchronization: inputs produced by queued torch work on a side stream are read after it,
+  and torch work queued after the call sees the outputs (engine._TorchOrder)."""
+  torch = pytest.importorskip("torch")
+  B = 4096
+  q, v, a = sample_states(humanoid, B, first=777)
+  ref = None
+  e = engine.InverseEngine(humanoid, capacity=B)
+  try:
+    ref = e.inverse(q, v, a)
+    dev = torch.device("cuda:0")
+    side = torch.cuda.Stream(dev)
+    hq, hv, ha = (torch.from_numpy(x).pin_memory() for x in (q, v, a))
+    torch.cuda.synchronize()
+    with torch.cuda.stream(side):
+      big = torch.randn(4096, 4096, device=dev, dtype=torch.float64)
+      for _ in range(4):                 # keep the side stream busy before the inputs land
+        big = big @ big * 1e-3
+      tq = hq.to(dev, non_blocking=True) + 0 * big[0, 0]
+      tv = hv.to(dev, non_blocking=True)
+      ta = ha.to(dev, non_blocking=True)
+      out = torch.full((B, humanoid.nv), float("nan"), dtype=torch.float64, device=dev)
+      e.inverse(tq, tv, ta, out=out)
+      res = (out * 1.0).to("cpu", non_blocking=False)
+  finally:
+    torch.cuda.synchronize()
+    e.close()
+  np.testing.assert_array_equal(res.numpy(), ref)
 
 
 def test_fast_kernel_selected(eng):
