@@ -878,6 +878,59 @@ MJH_HD int colSphereCapsule(RawContact* c, double margin, P1 pos1, M1 mat1, doub
   return rawSphereSphere(c, margin, pos1, mat1, r1, vec, mat2, size2[0]);
 }
 
+// mjc_SphereCylinder (engine_collision_primitive.c:323-391): side (sphere-sphere with the
+// axis point), cap (plane-sphere on the cap plane, normal flipped) or rim corner (sphere-
+// sphere with a point sphere at the corner)
+template <class P1, class M1, class P2, class M2>
+MJH_HD int colSphereCylinder(RawContact* c, double margin, P1 pos1, M1 mat1, double r1,
+                             P2 pos2, M2 mat2, const double* size2) {
+  const double radius = size2[0], height = size2[1];
+  double axis[3] = {mat2[2], mat2[5], mat2[8]};
+  double vec[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
+  const double x = dot3(axis, vec);
+  double a_proj[3], p_proj[3];
+  scl3(a_proj, axis, x);
+  sub3(p_proj, vec, a_proj);
+  const double p_proj_sqr = dot3(p_proj, p_proj);
+  bool collide_side = fabs(x) < height;
+  bool collide_cap = p_proj_sqr < radius*radius;
+  if (collide_side && collide_cap) {
+    const double dist_cap = height - fabs(x);
+    const double dist_radius = radius - sqrt(p_proj_sqr);
+    if (dist_cap < dist_radius) {
+      collide_side = false;
+    } else {
+      collide_cap = false;
+    }
+  }
+  if (collide_side) {
+    addTo3(a_proj, pos2);
+    return rawSphereSphere(c, margin, pos1, mat1, r1, a_proj, mat2, size2[0]);
+  }
+  if (collide_cap) {
+    double mcap[9], pos_cap[3];
+    const double sgn = x > 0 ? 1.0 : -1.0;
+    for (int k = 0; k < 9; k++) mcap[k] = mat2[k];
+    if (x <= 0) {                       // bottom cap: the flipped frame
+      for (int r = 0; r < 3; r++) {
+        mcap[3*r] = -mat2[3*r];
+        mcap[3*r+2] = -mat2[3*r+2];
+      }
+    }
+    for (int k = 0; k < 3; k++) pos_cap[k] = pos2[k] + (sgn*height)*axis[k];
+    const int ncon = rawPlaneSphere(c, margin, pos_cap, mcap, pos1, r1);
+    if (ncon) {
+      for (int k = 0; k < 3; k++) c->frame[k] = c->frame[k]*-1;
+    }
+    return ncon;
+  }
+  scl3(p_proj, p_proj, size2[0] / sqrt(p_proj_sqr));
+  scl3(vec, axis, x > 0 ? height : -height);
+  addTo3(vec, p_proj);
+  addTo3(vec, pos2);
+  return rawSphereSphere(c, margin, pos1, mat1, r1, vec, mat2, 0.0);
+}
+
 // mjraw_CapsuleCapsule
 template <class P1, class M1, class P2, class M2>
 MJH_HD int colCapsuleCapsule(RawContact* c, double margin, P1 pos1, M1 mat1,
@@ -1062,6 +1115,8 @@ MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
     num = rawSphereSphere(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2[0]);
   } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CAPSULE) {
     num = colSphereCapsule(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CYLINDER) {
+    num = colSphereCylinder(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
   } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_BOX) {
     num = rawSphereBox(raw, margin, pos1, size1[0], pos2, mat2, size2);
   } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {

@@ -1363,6 +1363,65 @@ static int col_sphereCapsule(orRaw* c, mjtNum margin, const mjtNum* pos1, const 
   return raw_sphereSphere(c, margin, pos1, mat1, r1, vec, mat2, size2[0]);
 }
 
+/* mju_addScl3 (engine_util_blas.c): res = vec1 + scl*vec2 */
+static void mju_addScl3(mjtNum res[3], const mjtNum vec1[3], const mjtNum vec2[3], mjtNum scl) {
+  res[0] = vec1[0] + scl*vec2[0];
+  res[1] = vec1[1] + scl*vec2[1];
+  res[2] = vec1[2] + scl*vec2[2];
+}
+
+/* mjc_SphereCylinder (engine_collision_primitive.c:323-391): side (sphere-sphere with the
+ * axis point), cap (plane-sphere on the cap plane, normal flipped) or rim corner (sphere-
+ * sphere with a point sphere at the corner) */
+static int col_sphereCylinder(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
+                              mjtNum r1, const mjtNum* pos2, const mjtNum* mat2,
+                              const mjtNum* size2) {
+  mjtNum radius = size2[0], height = size2[1];
+  mjtNum axis[3] = {mat2[2], mat2[5], mat2[8]};
+  mjtNum vec[3] = {pos1[0] - pos2[0], pos1[1] - pos2[1], pos1[2] - pos2[2]};
+  mjtNum x = mju_dot3(axis, vec);
+  mjtNum a_proj[3], p_proj[3];
+  mju_scl3(a_proj, axis, x);
+  mju_sub3(p_proj, vec, a_proj);
+  mjtNum p_proj_sqr = mju_dot3(p_proj, p_proj);
+  int collide_side = fabs(x) < height;
+  int collide_cap = p_proj_sqr < radius*radius;
+  if (collide_side && collide_cap) {
+    mjtNum dist_cap = height - fabs(x);
+    mjtNum dist_radius = radius - sqrt(p_proj_sqr);
+    if (dist_cap < dist_radius) {
+      collide_side = 0;
+    } else {
+      collide_cap = 0;
+    }
+  }
+  if (collide_side) {
+    mju_addTo3(a_proj, pos2);
+    return raw_sphereSphere(c, margin, pos1, mat1, r1, a_proj, mat2, size2[0]);
+  }
+  if (collide_cap) {
+    const mjtNum flipmat[9] = {-mat2[0], mat2[1], -mat2[2], -mat2[3], mat2[4], -mat2[5],
+                               -mat2[6], mat2[7], -mat2[8]};
+    const mjtNum* mat_cap;
+    mjtNum pos_cap[3];
+    if (x > 0) {
+      mju_addScl3(pos_cap, pos2, axis, height);
+      mat_cap = mat2;
+    } else {
+      mju_addScl3(pos_cap, pos2, axis, -height);
+      mat_cap = flipmat;
+    }
+    int ncon = raw_planeSphere(c, margin, pos_cap, mat_cap, pos1, r1);
+    if (ncon) mju_scl3(c->frame, c->frame, -1);
+    return ncon;
+  }
+  mju_scl3(p_proj, p_proj, size2[0] / sqrt(p_proj_sqr));
+  mju_scl3(vec, axis, x > 0 ? height : -height);
+  mju_addTo3(vec, p_proj);
+  mju_addTo3(vec, pos2);
+  return raw_sphereSphere(c, margin, pos1, mat1, r1, vec, mat2, 0);
+}
+
 /* mjraw_CapsuleCapsule */
 static int col_capsuleCapsule(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
                               const mjtNum* size1, const mjtNum* pos2, const mjtNum* mat2,
@@ -1552,7 +1611,7 @@ static int or_collisionFunc(int t1, int t2) {
     /*           PLANE HFIELD SPHERE CAPSULE ELLIPS CYL BOX MESH SDF */
     /*PLANE  */ {0,    0,     1,     2,      -1,    4,  4,  -1,  -1},
     /*HFIELD */ {0,    0,     -1,    -1,     -1,    -1, -1, -1,  -1},
-    /*SPHERE */ {0,    0,     1,     1,      -1,    -1, 1,  -1,  -1},
+    /*SPHERE */ {0,    0,     1,     1,      -1,    1,  1,  -1,  -1},
     /*CAPSULE*/ {0,    0,     0,     2,      -1,    -1, -1, -1,  -1},
     /*ELLIPS */ {0,    0,     0,     0,      -1,    -1, -1, -1,  -1},
     /*CYL    */ {0,    0,     0,     0,      0,     -1, -1, -1,  -1},
@@ -1890,6 +1949,8 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
     num = raw_sphereSphere(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2[0]);
   } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CAPSULE) {
     num = col_sphereCapsule(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CYLINDER) {
+    num = col_sphereCylinder(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
   } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_BOX) {
     num = raw_sphereBox(raw, margin, pos1, size1[0], pos2, mat2, size2);
   } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {

@@ -443,3 +443,71 @@ def test_elliptic_cone_states_and_device_bitexact():
       if f.stage > 0:
         np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name))
   assert {0, 1, 4} <= states, states
+
+
+@pytest.mark.parametrize("where,pos,dist,normal", [
+    # side: sphere beside the upright cylinder (r=.1, half-height .2), sphere r=.05
+    ("side", (0.14, 0.0, 0.05), -0.01, (1.0, 0.0, 0.0)),
+    # top cap: sphere above the top face, inside the radius
+    ("cap", (0.03, 0.02, 0.24), -0.01, (0.0, 0.0, 1.0)),
+    # bottom cap: the flipped frame
+    ("bottom", (0.0, -0.04, -0.24), -0.01, (0.0, 0.0, -1.0)),
+    # rim corner: beyond both the radius and the top
+    ("rim", (0.13, 0.0, 0.23), np.hypot(0.03, 0.03) - 0.05, (np.sqrt(.5), 0.0, np.sqrt(.5)))])
+def test_sphere_cylinder_known_answers(where, pos, dist, normal):
+  """mjc_SphereCylinder (engine_collision_primitive.c:323-391): side contacts are
+  sphere-sphere with the nearest axis point, cap contacts plane-sphere on the cap plane
+  (the bottom cap through the flipped frame) with the normal flipped, rim contacts
+  sphere-sphere with the corner point. The frame normal points from geom 1 (the sphere)
+  into geom 2 (the cylinder): minus the face normal `normal` listed here."""
+  m = mjcf.load_xml_string(f"""<mujoco><worldbody>
+    <geom type="cylinder" size=".1 .2" contype="1" conaffinity="1"/>
+    <body pos="{pos[0]} {pos[1]} {pos[2]}"><freejoint/><geom size=".05"/></body>
+    </worldbody></mujoco>""")
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  assert o.efc.ncon == 1
+  assert o.contact_field("con_dist")[0] == pytest.approx(dist, abs=1e-15)
+  # contact frame normal points from geom 1 (sphere) to geom 2 (cylinder)
+  np.testing.assert_allclose(o.contact_field("con_frame")[0][:3], -np.asarray(normal),
+                             atol=1e-15)
+  k = KernelCPU(m)
+  k.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  for name in ("con_dist", "con_pos", "con_frame"):
+    np.testing.assert_array_equal(k.field(name)[:o.contact_field(name).size],
+                                  o.contact_field(name).ravel())
+
+
+def test_sphere_cylinder_device_bitexact():
+  """Random poses of spheres around a free cylinder (side, caps, rims, deep penetration):
+  the device code on the host equals the oracle bit for bit on contacts, rows and outputs."""
+  m = mjcf.load_xml_string("""<mujoco><worldbody>
+    <body pos="0 0 .5"><freejoint/><geom type="cylinder" size=".12 .2"/></body>
+    <body pos=".3 0 .5"><freejoint/><geom size=".06" condim="1"/></body>
+    <body pos="-.3 0 .5"><freejoint/><geom size=".08" condim="4"/></body>
+    </worldbody></mujoco>""")
+  rng = np.random.default_rng(21)
+  o, k = Oracle(m), KernelCPU(m)
+  total = 0
+  for i in range(60):
+    q = m.qpos0.copy()
+    qq = rng.normal(size=4)
+    q[3:7] = qq / np.linalg.norm(qq)
+    for b in (1, 2):
+      q[7 * b:7 * b + 3] = q[:3] + rng.uniform(-0.25, 0.25, size=3)
+    v, a = rng.normal(size=m.nv), rng.normal(size=m.nv)
+    o.inverse(q, v, a)
+    _, st = k.inverse(q, v, a)
+    assert st == o.d.status == 0
+    ncon = o.efc.ncon
+    total += ncon
+    assert k.field("con_count")[0] == ncon
+    width = dict(CON_DOUBLE + CON_INT)
+    for name in CON_FIELDS:
+      ref = o.contact_field(name).reshape(ncon, width[name])
+      np.testing.assert_array_equal(k.field(name)[:ref.size].reshape(ncon, width[name]), ref,
+                                    err_msg=f"{name} inst {i}")
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name))
+  assert total > 30
