@@ -140,6 +140,13 @@ __device__ __forceinline__ void rowFields(const Lane<S>& d, int r, double pos, d
   d.efc_id[r] = id;
 }
 
+// grid of k_constraint_coop: one group per instance, or for a work-list (whose length only
+// the device knows) at most one block per SIMD striding over it
+static unsigned coopGrid(int B, int G, bool list) {
+  const unsigned full = (unsigned)((B + 64/G - 1) / (64/G));
+  return list && full > 1024u ? 1024u : full;
+}
+
 // dynamic LDS of k_constraint_coop: per instance 8 nv doubles (cdof, qvel, qacc), qpos and
 // efc_cap row forces
 static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap) {
@@ -161,7 +168,10 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   if ((int)threadIdx.x < m.nbody) chain[threadIdx.x] = mjh::chainMask(m, threadIdx.x);
   __syncthreads();
   const int sub = threadIdx.x % G, slot = threadIdx.x / G;
-  const long g = (long)blockIdx.x*IPB + slot;
+  // grid-stride over the instances (a work-list launch uses at most one block per SIMD, so
+  // an empty or short list costs few workgroups); the bound is uniform over the block
+  for (long base = (long)blockIdx.x*IPB; base < n; base += (long)gridDim.x*IPB) {
+  const long g = base + slot;
   const bool active = g < n;                // uniform within a group
   const long inst = active ? (LIST ? (long)worklist[g] : g) : 0;
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
@@ -387,6 +397,8 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
     if (sub == 0 && status && st) status[inst] |= st;
   }
   MJH_PHASE(17);
+  __syncthreads();                          // the group's LDS is reused by the next round
+  }
 }
 
 // Status checks of the straight-line path: mj_checkPos/Vel/Acc (engine_forward.c:53-102)
@@ -1079,7 +1091,7 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     if (fused && c->coop && c->fast->cmode) {   // cooperative lanes per instance
       const bool contact = c->con_cap > 0, list = c->fast->cmode == 1;
 #define MJHIP_LAUNCH_COOP(G, C, L)                                                            \
-      hipLaunchKernelGGL((k_constraint_coop<G, C, L>), dim3((B + 64/G - 1) / (64/G)),         \
+      hipLaunchKernelGGL((k_constraint_coop<G, C, L>), dim3(coopGrid(B, G, L)),               \
                          dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap), c->stream,         \
                          c->dmodel, c->mirror, B, wl,                                         \
                          (const int*)cnt, c->pairs, c->npair, qfrc, status)
