@@ -97,6 +97,7 @@ MJHIP_CONTACT_HD int mjhip_pairMaxContacts(int t1, int t2) {
   if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CYLINDER) return 1;
   if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_BOX) return 1;
   if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) return 2;
+  if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_BOX) return 2;
   if (t1 == mjhipGEOM_HFIELD && t2 <= mjhipGEOM_HFIELD) return 0;
   return -1;
 }

@@ -1422,6 +1422,192 @@ static int col_sphereCylinder(orRaw* c, mjtNum margin, const mjtNum* pos1, const
   return raw_sphereSphere(c, margin, pos1, mat1, r1, vec, mat2, 0);
 }
 
+/* mjraw_CapsuleBox (engine_collision_box.c:121-594): the box feature closest to the capsule
+ * segment (an end point against a face, or the segment against one of the 12 edges, in the
+ * box frame), the second point along the segment that can still touch the box, then one
+ * sphere-box contact of the capsule's radius at each point (at most 2). The reference's
+ * j == 2 block inside the edge loop computes nothing that is used later; it is omitted. */
+static int col_capsuleBox(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
+                          const mjtNum* size1, const mjtNum* pos2, const mjtNum* mat2,
+                          const mjtNum* size2) {
+  mjtNum tmp[3], pos[3], axis[3], halfaxis[3];
+  const mjtNum hl = size1[1];
+  mju_sub3(tmp, pos1, pos2);
+  mju_mulMatTVec3(pos, mat2, tmp);
+  const mjtNum a1[3] = {mat1[2], mat1[5], mat1[8]};
+  mju_mulMatTVec3(axis, mat2, a1);
+  mju_scl3(halfaxis, axis, hl);
+  const int axisdir = (halfaxis[0] > 0) + 2*(halfaxis[1] > 0) + 4*(halfaxis[2] > 0);
+  mjtNum bestdist = margin + 2*(size1[0] + hl + size2[0] + size2[1] + size2[2]);
+  mjtNum bestseg = 0, bestbox = 0, secondpos = -4;
+  int cltype = -4, clface = -1, clcorner = 0, cledge = 0;
+
+  /* a segment end against a face: the end clamped onto the box along at most one axis */
+  for (int e = -1; e <= 1; e += 2) {
+    mjtNum p[3], q[3];
+    int nclamp = 0, face = -1;
+    for (int k = 0; k < 3; k++) {
+      p[k] = pos[k] + halfaxis[k]*e;
+      q[k] = p[k];
+      if (p[k] < -size2[k]) {
+        nclamp++;
+        face = k;
+        p[k] = -size2[k];
+      } else if (p[k] > size2[k]) {
+        nclamp++;
+        face = k;
+        p[k] = size2[k];
+      }
+    }
+    if (nclamp > 1) continue;
+    for (int k = 0; k < 3; k++) p[k] -= q[k];
+    const mjtNum dist = mju_dot3(p, p);
+    if (dist < bestdist) {
+      bestdist = dist;
+      bestseg = e;
+      cltype = -2 + e;
+      clface = face;
+    }
+  }
+
+  /* the segment against each edge: closest points of two segments, clamped */
+  for (int j = 0; j < 3; j++) {
+    for (int i = 0; i < 8; i++) {
+      if (i & (1 << j)) continue;
+      mjtNum corner[3] = {((i & 1) ? 1 : -1)*size2[0], ((i & 2) ? 1 : -1)*size2[1],
+                          ((i & 4) ? 1 : -1)*size2[2]};
+      corner[j] = 0;
+      mjtNum dif[3];
+      mju_sub3(dif, corner, pos);
+      const mjtNum ma = size2[j]*size2[j], mb = -size2[j]*halfaxis[j], mc = size1[1]*size1[1];
+      const mjtNum u = -size2[j]*dif[j], v = mju_dot3(halfaxis, dif);
+      const mjtNum det = ma*mc - mb*mb;
+      if (fabs(det) < mjMINVAL) continue;
+      const mjtNum idet = 1/det;
+      mjtNum x1 = (mc*u - mb*v)*idet, x2 = (ma*v - mb*u)*idet;
+      int s1 = 1, s2 = 1;
+      if (x1 > 1) {
+        x1 = 1;
+        s1 = 2;
+        x2 = (v - mb)*(1/mc);
+      } else if (x1 < -1) {
+        x1 = -1;
+        s1 = 0;
+        x2 = (v + mb)*(1/mc);
+      }
+      if (x2 > 1 || x2 < -1) {
+        const int hi = x2 > 1;
+        x2 = hi ? 1 : -1;
+        s2 = hi ? 2 : 0;
+        x1 = (hi ? u - mb : u + mb)*(1/ma);
+        if (x1 > 1) {
+          x1 = 1;
+          s1 = 2;
+        } else if (x1 < -1) {
+          x1 = -1;
+          s1 = 0;
+        }
+      }
+      mju_sub3(dif, corner, pos);
+      mju_addToScl3(dif, halfaxis, -x2);
+      dif[j] += size2[j]*x1;
+      const mjtNum d2 = mju_dot3(dif, dif);
+      const int t = s1*3 + s2;
+      if (d2 < bestdist - mjMINVAL) {
+        bestdist = d2;
+        bestseg = x2;
+        bestbox = x1;
+        clcorner = i + (1 << j)*(t / 6);
+        cledge = j;
+        cltype = t;
+      }
+    }
+  }
+  if (cltype == -4) return 0;
+
+  /* the second point along the segment (:392-559) */
+  mjtNum mul = 0, e1, e2;
+  if (cltype >= 0 && cltype / 3 != 1) {           /* a box corner is closest */
+    int c1 = axisdir ^ clcorner, ax = 0, ax1 = 0, ax2 = 0;
+    if (c1 != 0 && c1 != 7) {                     /* not pointing at or away from it */
+      mjtNum de, dp;
+      if (c1 == 1 || c1 == 2 || c1 == 4) {
+        mul = 1;
+        de = 1 - bestseg;
+        dp = 1 + bestseg;
+      } else {
+        mul = -1;
+        c1 = 7 - c1;
+        dp = 1 - bestseg;
+        de = 1 + bestseg;
+      }
+      if (c1 == 1) { ax = 0; ax1 = 1; ax2 = 2; }
+      if (c1 == 2) { ax = 1; ax1 = 2; ax2 = 0; }
+      if (c1 == 4) { ax = 2; ax1 = 0; ax2 = 1; }
+      if (axis[ax]*axis[ax] > 0.5) {              /* along the box edge */
+        secondpos = de;
+        e1 = 2*size2[ax]/fabs(halfaxis[ax]);
+        if (e1 < secondpos) secondpos = e1;
+        secondpos *= mul;
+      } else {                                    /* along a box face */
+        secondpos = dp;
+        e1 = 2*size2[ax1]/fabs(halfaxis[ax1]);
+        if (e1 < secondpos) secondpos = e1;
+        e1 = 2*size2[ax2]/fabs(halfaxis[ax2]);
+        if (e1 < secondpos) secondpos = e1;
+        secondpos *= -mul;
+      }
+    }
+  } else if (cltype >= 0) {                       /* the middle of a box edge is closest */
+    const int c1 = (axisdir ^ clcorner) & (7 - (1 << cledge));
+    if (c1 == 1 || c1 == 2 || c1 == 4) {         /* crossing the edge, not a T */
+      int ax = cledge, ax1 = (cledge + 1) % 3, ax2 = (cledge + 2) % 3;
+      if (fabs(axis[ax1]) > fabs(axis[ax2])) ax1 = ax2;
+      ax2 = 3 - ax - ax1;
+      if (c1 & (1 << ax2)) {
+        mul = 1;
+        secondpos = 1 - bestseg;
+      } else {
+        mul = -1;
+        secondpos = 1 + bestseg;
+      }
+      e1 = 2*size2[ax2]/fabs(halfaxis[ax2]);
+      if (e1 < secondpos) secondpos = e1;
+      e2 = (((axisdir & (1 << ax)) != 0) == ((c1 & (1 << ax2)) != 0)) ? 1 - bestbox : 1 + bestbox;
+      e1 = size2[ax]*e2/fabs(halfaxis[ax]);
+      if (e1 < secondpos) secondpos = e1;
+      secondpos *= mul;
+    }
+  } else if (clface != -1) {                      /* an end against a face, outside the box */
+    mul = cltype == -3 ? 1 : -1;
+    secondpos = 2;
+    mjtNum p[3];
+    for (int k = 0; k < 3; k++) p[k] = pos[k] + halfaxis[k]*-mul;
+    for (int k = 0; k < 3; k++) {
+      if (k == clface) continue;
+      e1 = (size2[k] - p[k]) / halfaxis[k] * mul;
+      if (e1 > 0 && e1 < secondpos) secondpos = e1;
+      e1 = (-size2[k] - p[k]) / halfaxis[k] * mul;
+      if (e1 > 0 && e1 < secondpos) secondpos = e1;
+    }
+    secondpos *= mul;
+  }
+
+  /* spheres of the capsule's radius at the two points, collided with the box */
+  mjtNum sp[3], w[3];
+  for (int k = 0; k < 3; k++) sp[k] = pos[k] + halfaxis[k]*bestseg;
+  mju_mulMatVec3(w, mat2, sp);
+  mju_addTo3(w, pos2);
+  int n = raw_sphereBox(c, margin, w, size1[0], pos2, mat2, size2);
+  if (secondpos > -3) {
+    for (int k = 0; k < 3; k++) sp[k] = pos[k] + halfaxis[k]*(secondpos + bestseg);
+    mju_mulMatVec3(w, mat2, sp);
+    mju_addTo3(w, pos2);
+    n += raw_sphereBox(c + n, margin, w, size1[0], pos2, mat2, size2);
+  }
+  return n;
+}
+
 /* mjraw_CapsuleCapsule */
 static int col_capsuleCapsule(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
                               const mjtNum* size1, const mjtNum* pos2, const mjtNum* mat2,
@@ -1612,7 +1798,7 @@ static int or_collisionFunc(int t1, int t2) {
     /*PLANE  */ {0,    0,     1,     2,      -1,    4,  4,  -1,  -1},
     /*HFIELD */ {0,    0,     -1,    -1,     -1,    -1, -1, -1,  -1},
     /*SPHERE */ {0,    0,     1,     1,      -1,    1,  1,  -1,  -1},
-    /*CAPSULE*/ {0,    0,     0,     2,      -1,    -1, -1, -1,  -1},
+    /*CAPSULE*/ {0,    0,     0,     2,      -1,    -1, 2,  -1,  -1},
     /*ELLIPS */ {0,    0,     0,     0,      -1,    -1, -1, -1,  -1},
     /*CYL    */ {0,    0,     0,     0,      0,     -1, -1, -1,  -1},
     /*BOX    */ {0,    0,     0,     0,      0,     0,  -1, -1,  -1},
@@ -1951,6 +2137,8 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
     num = col_sphereCapsule(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
   } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CYLINDER) {
     num = col_sphereCylinder(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_BOX) {
+    num = col_capsuleBox(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
   } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_BOX) {
     num = raw_sphereBox(raw, margin, pos1, size1[0], pos2, mat2, size2);
   } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {

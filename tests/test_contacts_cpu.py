@@ -511,3 +511,78 @@ def test_sphere_cylinder_device_bitexact():
       if f.stage > 0:
         np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name))
   assert total > 30
+
+
+def test_capsule_box_known_answers():
+  """mjraw_CapsuleBox (engine_collision_box.c:121-594): a capsule lying on a box's top face
+  touches it at both segment ends (two sphere-box contacts, normal along the face normal); a
+  capsule standing on its end touches once; one crossing a box edge diagonally touches at
+  the edge point."""
+  def contacts(cap_pos, cap_euler):
+    m = mjcf.load_xml_string(f"""<mujoco><worldbody>
+      <geom type="box" size=".5 .5 .1"/>
+      <body pos="{cap_pos}" euler="{cap_euler}"><freejoint/>
+        <geom type="capsule" size=".05 .2"/></body></worldbody></mujoco>""")
+    o = Oracle(m)
+    o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+    k = KernelCPU(m)
+    k.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+    for name in ("con_dist", "con_pos", "con_frame"):
+      np.testing.assert_array_equal(k.field(name)[:o.contact_field(name).size],
+                                    o.contact_field(name).ravel())
+    return o.contact_field("con_dist"), o.contact_field("con_pos"), o.contact_field("con_frame")
+  # lying along x on the top face, 0.01 deep: both ends
+  d, p, f = contacts("0 0 .14", "0 90 0")
+  assert len(d) == 2
+  np.testing.assert_allclose(d, [-0.01, -0.01], atol=1e-15)
+  np.testing.assert_allclose(sorted(p[:, 0]), [-0.2, 0.2], atol=1e-12)
+  np.testing.assert_allclose(np.abs(f[:, 2]), [1, 1], atol=1e-15)
+  # standing on its lower end, 0.01 deep: one contact below the lower end
+  d, p, f = contacts("0.1 -0.2 .34", "0 0 0")
+  assert len(d) == 1
+  assert d[0] == pytest.approx(-0.01, abs=1e-15)
+  np.testing.assert_allclose(p[0][:2], [0.1, -0.2], atol=1e-15)
+  # crossing the edge x = .5 (along y) horizontally above its top corner line
+  d, p, f = contacts(".5 0 .14", "90 0 0")
+  assert len(d) >= 1
+  assert min(d) == pytest.approx(-0.01, abs=1e-12)
+
+
+def test_capsule_box_device_bitexact():
+  """Random poses of capsules around a free box (faces, edges and corners closest, every
+  second-point branch): the device code on the host equals the oracle bit for bit on
+  contacts, rows and outputs."""
+  m = mjcf.load_xml_string("""<mujoco><worldbody>
+    <body pos="0 0 .5"><freejoint/><geom type="box" size=".2 .15 .1"/></body>
+    <body pos=".4 0 .5"><freejoint/><geom type="capsule" size=".05 .15" condim="1"/></body>
+    <body pos="-.4 0 .5"><freejoint/><geom type="capsule" size=".03 .25"/></body>
+    </worldbody></mujoco>""")
+  rng = np.random.default_rng(31)
+  o, k = Oracle(m), KernelCPU(m)
+  total, two = 0, 0
+  for i in range(200):
+    q = m.qpos0.copy()
+    for b in range(3):
+      qq = rng.normal(size=4)
+      q[7 * b + 3:7 * b + 7] = qq / np.linalg.norm(qq)
+    for b in (1, 2):
+      q[7 * b:7 * b + 3] = q[:3] + rng.uniform(-0.3, 0.3, size=3)
+    v, a = rng.normal(size=m.nv), rng.normal(size=m.nv)
+    o.inverse(q, v, a)
+    _, st = k.inverse(q, v, a)
+    assert st == o.d.status == 0
+    ncon = o.efc.ncon
+    total += ncon
+    g = o.contact_field("con_geom").reshape(ncon, 2)
+    for b in (1, 2):
+      two += int(((g == b).any(axis=1)).sum() == 2)
+    assert k.field("con_count")[0] == ncon
+    width = dict(CON_DOUBLE + CON_INT)
+    for name in CON_FIELDS:
+      ref = o.contact_field(name).reshape(ncon, width[name])
+      np.testing.assert_array_equal(k.field(name)[:ref.size].reshape(ncon, width[name]), ref,
+                                    err_msg=f"{name} inst {i}")
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name))
+  assert total > 50 and two > 5
