@@ -117,6 +117,8 @@ def fast_path_supported(m) -> str | None:
     return "ENERGY (mj_energyPos/Vel run on the generic kernel)"
   if m.nmocap or m.na:
     return "mocap/activations"
+  if m.sizes.get("nwrap", 0) and np.any(np.asarray(m.wrap_type) != 1):
+    return "spatial tendons (generic kernel)"
   if m.opt["density"] > 0 or m.opt["viscosity"] > 0:
     return "fluid"
   for a in range(m.nu):

@@ -67,6 +67,13 @@ MJH_HD int mjh_needSubtreeVel(const mjhipModel* m) {
   }
   return 0;
 }
+// 1 when a tendon is spatial (two 3 x nv site Jacobians per path segment)
+MJH_HD int mjh_needSpatial(const mjhipModel* m) {
+  for (int i = 0; i < m->nwrap; i++) {
+    if (m->wrap_type[i] != mjhipWRAP_JOINT) return 1;
+  }
+  return 0;
+}
 // 1 when an actuator has a slider-crank transmission (three 3 x nv Jacobians at once)
 MJH_HD int mjh_needSliderCrank(const mjhipModel* m) {
   for (int i = 0; i < m->nu; i++) {
@@ -117,6 +124,7 @@ struct SP {
   XSC(jacp, 3*nv)                     \
   XSC(jacr, 3*nv)                     \
   XSC(jacsc, mjh_needSliderCrank(m)*6*nv) /* slider-crank site Jacobians */ \
+  XSC(jact, mjh_needSpatial(m)*6*nv)  /* spatial tendon segment end Jacobians */ \
   XSC(qforce, nv)                     \
   XSC(qfrc_tmp, nv)                   /* single-instance mj_rne / mj_xfrcAccumulate result */ \
   XSC(qacc_save, nv)                  \
@@ -1732,7 +1740,7 @@ MJH_HD void camlight(const mjhipModel& m, const Lane<S>& d) {
   }
 }
 
-// mj_tendon :651-723 (fixed tendons, dense ten_J)
+// mj_tendon :651-860 (fixed tendons; spatial tendons through sites and pulleys; dense ten_J)
 template <int S>
 MJH_HD void tendon(const mjhipModel& m, const Lane<S>& d) {
   int nv = m.nv, nten = m.ntendon;
@@ -1742,10 +1750,44 @@ MJH_HD void tendon(const mjhipModel& m, const Lane<S>& d) {
   for (int i = 0; i < nten; i++) {
     int adr = m.tendon_adr[i];
     int num = m.tendon_num[i];
-    for (int j = 0; j < num; j++) {
-      int k = m.wrap_objid[adr+j];
-      d.ten_length[i] += m.wrap_prm[adr+j] * d.qpos[m.jnt_qposadr[k]];
-      d.ten_J[i*nv + m.jnt_dofadr[k]] = m.wrap_prm[adr+j];
+    if (m.wrap_type[adr] == mjhipWRAP_JOINT) {
+      for (int j = 0; j < num; j++) {
+        int k = m.wrap_objid[adr+j];
+        d.ten_length[i] += m.wrap_prm[adr+j] * d.qpos[m.jnt_qposadr[k]];
+        d.ten_J[i*nv + m.jnt_dofadr[k]] = m.wrap_prm[adr+j];
+      }
+      continue;
+    }
+    // spatial: consecutive site pairs; a pulley divides the length and moment that follow
+    double divisor = 1;
+    for (int j = 0; j < num - 1; j++) {
+      const int type0 = m.wrap_type[adr+j], type1 = m.wrap_type[adr+j+1];
+      if (type0 == mjhipWRAP_PULLEY || type1 == mjhipWRAP_PULLEY) {
+        if (type0 == mjhipWRAP_PULLEY) divisor = m.wrap_prm[adr+j];
+        continue;
+      }
+      const int id0 = m.wrap_objid[adr+j], id1 = m.wrap_objid[adr+j+1];
+      double p0[3], p1[3], dif[3];
+      for (int k = 0; k < 3; k++) {
+        p0[k] = d.site_xpos[3*id0 + k];
+        p1[k] = d.site_xpos[3*id1 + k];
+      }
+      sub3(dif, p1, p0);
+      d.ten_length[i] += sqrt(dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2]) / divisor;
+      const int b0 = m.site_bodyid[id0], b1 = m.site_bodyid[id1];
+      if (b0 == b1) continue;
+      normalize3(dif);
+      SP<S> j1 = d.jact, j2 = d.jact + 3*nv;
+      jacInto(m, d, j1, d.jacr, p0, b0);
+      jacInto(m, d, j2, d.jacr, p1, b1);
+      const double inv = 1/divisor;
+      for (int c = 0; c < nv; c++) {   // mju_mulMatTVec of (jac2 - jac1) with dif, then
+        double t = 0;                   // mju_addToScl(ten_J row, ., 1/divisor)
+        for (int r = 0; r < 3; r++) {
+          if (dif[r]) t += (j2[r*nv + c] - j1[r*nv + c])*dif[r];
+        }
+        d.ten_J[i*nv + c] += t*inv;
+      }
     }
   }
 }

@@ -756,8 +756,10 @@ static const char* unsupported(const mjhipModel* m) {
     return "mjENBL_INVDISCRETE with the RK4 integrator (an error in the reference)";
   }
   for (int i = 0; i < m->ntendon; i++) {
-    if (m->tendon_num[i] && m->wrap_type[m->tendon_adr[i]] != mjhipWRAP_JOINT) {
-      return "spatial tendons";
+    for (int w = m->tendon_adr[i]; w < m->tendon_adr[i] + m->tendon_num[i]; w++) {
+      if (m->wrap_type[w] == mjhipWRAP_SPHERE || m->wrap_type[w] == mjhipWRAP_CYLINDER) {
+        return "spatial tendons wrapping around geoms";
+      }
     }
   }
   for (int i = 0; i < m->nu; i++) {

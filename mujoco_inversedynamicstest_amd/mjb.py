@@ -452,8 +452,8 @@ def unsupported(ints, arrays) -> str | None:
     return "tendon frictionloss (FRICTION_TENDON rows)"
   if ints["ngeom"] and (arrays["geom_fluid"][:, 0] > 0).any():
     return "the ellipsoid fluid model (geom fluidshape)"
-  if ints["nwrap"] and (arrays["wrap_type"] != 1).any():     # mjWRAP_JOINT
-    return "spatial tendons"
+  if ints["nwrap"] and np.isin(arrays["wrap_type"], (4, 5)).any():   # sphere, cylinder
+    return "spatial tendons wrapping around geoms"
   return None
 
 

@@ -583,11 +583,25 @@ class MJCFCompiler:
         self._parse_worldbody(el)
       elif t == "tendon":
         for ch in el:
-          if ch.tag != "fixed":
-            raise MJCFError(f"unsupported tendon <{ch.tag}> (spatial tendons are next)")
+          if ch.tag not in ("fixed", "spatial"):
+            raise MJCFError(f"unsupported tendon <{ch.tag}>")
           a = self._elem_attrs(ch, "tendon", None)
-          joints = [(j.get("joint"), float(j.get("coef", "1"))) for j in ch if j.tag == "joint"]
-          self.tendons.append((a, joints))
+          a["__kind"] = ch.tag
+          if ch.tag == "fixed":
+            path = [(j.get("joint"), float(j.get("coef", "1"))) for j in ch if j.tag == "joint"]
+          else:                             # xml_native_reader.cc:3780-3820
+            path = []
+            for w in ch:
+              if w.tag == "site":
+                path.append(("site", w.get("site")))
+              elif w.tag == "pulley":
+                path.append(("pulley", float(w.get("divisor", "0"))))
+              elif w.tag == "geom":
+                raise MJCFError("spatial tendons wrapping around geoms (sphere/cylinder "
+                                "wrapping) are not in the supported subset")
+              else:
+                raise MJCFError(f"unsupported spatial tendon element <{w.tag}>")
+          self.tendons.append((a, path))
       elif t == "actuator":
         for ch in el:
           if ch.tag not in ACTUATOR_TAGS:
@@ -1240,6 +1254,7 @@ class MJCFCompiler:
     wobj = arr("wrap_objid", nwrap, np.int32)
     wprm = arr("wrap_prm", nwrap, np.float64)
     w = 0
+    sitename_t = {x["name"]: i for i, x in enumerate(sites) if x["name"]}
     for ti, (ta, jl) in enumerate(self.tendons):
       tadr[ti] = w
       tnum[ti] = len(jl)
@@ -1266,6 +1281,35 @@ class MJCFCompiler:
       if len(sl) == 1:
         sl = [sl[0], sl[0]]
       tls[ti] = sl
+      if ta["__kind"] == "spatial":
+        # mjCTendon::Compile (user_objects.cc:5448-5570): path rules; wraps compiled as
+        # user_model.cc:3215-3222 (site: prm 0; pulley: prm = divisor, objid -1)
+        sz = len(jl)
+        if sz < 2:
+          raise MJCFError(f"tendon '{ta.get('name', '')}' (id = {ti}): spatial path must "
+                          "contain at least two objects")
+        if float(ta.get("width", 0.003)) <= 0:
+          raise MJCFError(f"tendon '{ta.get('name', '')}' (id = {ti}) must have positive width")
+        for i, (kind, val) in enumerate(jl):
+          if kind == "pulley":
+            if i > 0 and jl[i - 1][0] == "pulley":
+              raise MJCFError(f"tendon (id = {ti}): consecutive pulleys (pos {i})")
+            if i == sz - 1:
+              raise MJCFError(f"tendon (id = {ti}): path ends with pulley")
+            wtype[w], wobj[w], wprm[w] = 2, -1, val     # mjWRAP_PULLEY
+          else:
+            if val not in sitename_t:
+              raise MJCFError(f"unknown site '{val}' in tendon")
+            if (i == 0 or jl[i - 1][0] == "pulley") and (i == sz - 1 or jl[i + 1][0] == "pulley"):
+              raise MJCFError(f"tendon (id = {ti}): site {i} needs a neighbor that is not a "
+                              "pulley")
+            if i < sz - 1 and jl[i + 1][0] == "site" and jl[i + 1][1] == val:
+              raise MJCFError(f"tendon (id = {ti}): site {i} is repeated")
+            wtype[w], wobj[w], wprm[w] = 3, sitename_t[val], 0.0   # mjWRAP_SITE
+          w += 1
+        if sl[0] > sl[1]:
+          raise MJCFError("invalid springlength in tendon")
+        continue
       for jn, coef in jl:
         if jn not in jname:
           raise MJCFError(f"unknown joint '{jn}' in tendon")
@@ -1756,6 +1800,20 @@ def sparse_structures(sizes: dict, A) -> dict:
           b = int(parentid[b])
       gzero = agear[ai, 0] == 0 if atrn[ai] == 2 else not np.any(agear[ai])
       c = [] if gzero else sorted(c)
+    elif int(np.asarray(A["wrap_type"]).reshape(-1)[tadr[tid]]) != 1:
+      # spatial tendon: ten_J is nonzero on the dof chains of the path's site bodies (the
+      # reference compresses its dense row by value, :1070-1079; generic states have no
+      # exact zeros there)
+      wtype = np.asarray(A["wrap_type"]).reshape(-1)
+      c = set()
+      for wi in range(tadr[tid], tadr[tid] + tnum[tid]):
+        if wtype[wi] != 3:
+          continue
+        b = int(sbody[wobj[wi]])
+        while b > 0:
+          c.update(range(dofadr[b], dofadr[b] + dofnum[b]))
+          b = int(parentid[b])
+      c = [] if agear[ai, 0] == 0 else sorted(c)
     else:
       row = np.zeros(nv)
       for wi in range(tadr[tid], tadr[tid] + tnum[tid]):

@@ -95,7 +95,7 @@ def _positions(m, st, margin):
 def _tendon_ok(m, q, tmargin):
   ok = np.ones(q.shape[0], dtype=bool)
   for t in range(m.ntendon):
-    if not m.tendon_limited[t]:
+    if not m.tendon_limited[t] or m.wrap_type[m.tendon_adr[t]] != 1:   # fixed tendons only
       continue
     L = np.zeros(q.shape[0])
     for w in range(m.tendon_adr[t], m.tendon_adr[t] + m.tendon_num[t]):

@@ -252,18 +252,39 @@ def set_const(m):
       m.dof_invweight0[da:da+3] = np.trace(A) / 3
     else:
       m.dof_invweight0[da] = A[0, 0]
-  # tendons (fixed): length and dense J at qpos0
-  def tendon(q):
+  # tendons: length and dense J (mj_tendon, engine_core_smooth.c:651-860; spatial paths
+  # through sites and pulleys)
+  def tendon(q, ev):
     L = np.zeros(m.ntendon)
     J = np.zeros((m.ntendon, nv))
     for t in range(m.ntendon):
       adr, num = m.tendon_adr[t], m.tendon_num[t]
-      for w in range(adr, adr + num):
-        k = m.wrap_objid[w]
-        L[t] += m.wrap_prm[w] * q[m.jnt_qposadr[k]]
-        J[t, m.jnt_dofadr[k]] = m.wrap_prm[w]
+      if m.wrap_type[adr] == 1:
+        for w in range(adr, adr + num):
+          k = m.wrap_objid[w]
+          L[t] += m.wrap_prm[w] * q[m.jnt_qposadr[k]]
+          J[t, m.jnt_dofadr[k]] = m.wrap_prm[w]
+        continue
+      divisor = 1.0
+      for w in range(adr, adr + num - 1):
+        if m.wrap_type[w] == 2 or m.wrap_type[w + 1] == 2:
+          if m.wrap_type[w] == 2:
+            divisor = m.wrap_prm[w]
+          continue
+        s0, s1 = m.wrap_objid[w], m.wrap_objid[w + 1]
+        b0, b1 = m.site_bodyid[s0], m.site_bodyid[s1]
+        p0 = ev.xmat[b0] @ m.site_pos[s0] + ev.xpos[b0]
+        p1 = ev.xmat[b1] @ m.site_pos[s1] + ev.xpos[b1]
+        dif = p1 - p0
+        L[t] += np.linalg.norm(dif) / divisor
+        if b0 != b1:
+          n = np.linalg.norm(dif)
+          dif = dif / n if n >= 1e-15 else np.array([1.0, 0, 0])
+          j0, _ = ev.jac_point(m, b0, p0)
+          j1, _ = ev.jac_point(m, b1, p1)
+          J[t] += (dif @ (j1 - j0)) / divisor
     return L, J
-  L0, J0 = tendon(m.qpos0)
+  L0, J0 = tendon(m.qpos0, e)
   m.tendon_length0[:] = L0
   for t in range(m.ntendon):
     m.tendon_invweight0[t] = J0[t] @ Minv @ J0[t] if nv else 0.0
@@ -364,7 +385,7 @@ def set_const(m):
     m.light_poscom0[l] = pos - e.subtree_com[t if t >= 0 else b]
     m.light_dir0[l] = d
   # tendon spring length at qpos_spring (setSpring)
-  Ls, _ = tendon(m.qpos_spring)
+  Ls, _ = tendon(m.qpos_spring, _Eval(m, m.qpos_spring.astype(np.float64)))
   for t in range(m.ntendon):
     if m.tendon_lengthspring[t, 0] == -1 and m.tendon_lengthspring[t, 1] == -1:
       m.tendon_lengthspring[t] = Ls[t]

@@ -693,13 +693,20 @@ static void or_camlight(const mjhipModel* m, mjhipData* d) {
   }
 }
 
-/* :651-723, fixed tendons, dense Jacobian */
+/* :651-860, fixed tendons and spatial tendons through sites and pulleys, dense Jacobian
+ * (the wrap visualization outputs ten_wrapadr/ten_wrapnum/wrap_obj/wrap_xpos are not kept;
+ * sphere/cylinder wrapping is outside the subset, the loader rejects it) */
+static void mju_mulMatTVec(mjtNum* res, const mjtNum* mat, const mjtNum* vec, int nr, int nc);
+
 static void or_tendon(const mjhipModel* m, mjhipData* d) {
   int nv = m->nv, nten = m->ntendon;
   mjtNum *L = d->ten_length, *J = d->ten_J;
   if (!nten) return;
   mju_zero(L, nten);
   mju_zero(J, nten*nv);
+  mjtNum* jac1 = (mjtNum*)malloc(sizeof(mjtNum)*3*(nv ? nv : 1));
+  mjtNum* jac2 = (mjtNum*)malloc(sizeof(mjtNum)*3*(nv ? nv : 1));
+  mjtNum* tmp = (mjtNum*)malloc(sizeof(mjtNum)*(nv ? nv : 1));
   for (int i = 0; i < nten; i++) {
     int adr = m->tendon_adr[i];
     int tendon_num = m->tendon_num[i];
@@ -709,8 +716,35 @@ static void or_tendon(const mjhipModel* m, mjhipData* d) {
         L[i] += m->wrap_prm[adr+j] * d->qpos[m->jnt_qposadr[k]];
         J[i*nv + m->jnt_dofadr[k]] = m->wrap_prm[adr+j];
       }
+      continue;
+    }
+    /* spatial: consecutive site pairs, a pulley divides what follows (:725-855) */
+    mjtNum divisor = 1;
+    for (int j = 0; j < tendon_num - 1; j++) {
+      int type0 = m->wrap_type[adr+j], type1 = m->wrap_type[adr+j+1];
+      if (type0 == mjhipWRAP_PULLEY || type1 == mjhipWRAP_PULLEY) {
+        if (type0 == mjhipWRAP_PULLEY) divisor = m->wrap_prm[adr+j];
+        continue;
+      }
+      int id0 = m->wrap_objid[adr+j], id1 = m->wrap_objid[adr+j+1];
+      const mjtNum* p0 = d->site_xpos + 3*id0;
+      const mjtNum* p1 = d->site_xpos + 3*id1;
+      int b0 = m->site_bodyid[id0], b1 = m->site_bodyid[id1];
+      mjtNum dif[3] = {p1[0]-p0[0], p1[1]-p0[1], p1[2]-p0[2]};
+      L[i] += sqrt(dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2]) / divisor;
+      if (b0 != b1) {
+        mju_normalize3(dif);
+        mj_jac(m, d, jac1, NULL, p0, b0);
+        mj_jac(m, d, jac2, NULL, p1, b1);
+        for (int k = 0; k < 3*nv; k++) jac2[k] = jac2[k] - jac1[k];
+        mju_mulMatTVec(tmp, jac2, dif, 3, nv);
+        mju_addToScl(J + i*nv, tmp, 1/divisor, nv);
+      }
     }
   }
+  free(jac1);
+  free(jac2);
+  free(tmp);
 }
 
 /* :865-916, joint transmission (slide/hinge) */

@@ -981,3 +981,40 @@ def test_config3_full_batch_one_gpu(humanoid):
   assert (np.abs((f[sub] - f0) - Mx).max(axis=1) / scale).max() < 1e-9
   ref, _ = oracle_batch(humanoid, q[sub[:256]], v[sub[:256]], a[sub[:256]])
   assert_close(f[sub[:256]], ref["qfrc_inverse"], "qfrc_inverse (config 3 subsample)")
+
+
+def test_spatial_tendon_parity():
+  """Spatial tendons through sites and pulleys (lengths, Jacobians, limit rows, spring-
+  damper, tendon actuators) on the device vs the oracle; the model has no straight-line
+  kernel (the generic pipeline serves it)."""
+  import os
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+  from test_tendon_cpu import ARM, _states
+  from mujoco_inversedynamicstest_amd import mjcf
+  m = mjcf.load_xml_string(ARM)
+  st = _states(m, 2048, 5)
+  q = np.array([x[0] for x in st])
+  v = np.array([x[1] for x in st])
+  a = np.array([x[2] for x in st])
+  e = engine.InverseEngine(m, capacity=len(q))
+  try:
+    assert e.fast_kernel is None
+    f, status = e.inverse(q, v, a, status=True)
+    tl = e.field("ten_length", 0, len(q))
+    tj = e.field("ten_J", 0, len(q))
+    nefc = e.field_int("efc_count", 0, len(q))[:, 0]
+  finally:
+    e.close()
+  assert (status == 0).all()
+  o = Oracle(m)
+  ref, rl, rj = [], [], []
+  for i in range(len(q)):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    rl.append(o.d.ten_length.copy())
+    rj.append(o.d.ten_J.copy())
+    assert nefc[i] == o.d.nefc
+  assert_close(f, np.array(ref), "qfrc_inverse")
+  assert_close(tl, np.array(rl), "ten_length")
+  assert_close(tj, np.array(rj), "ten_J")
+  assert nefc.sum() > 0
