@@ -1740,7 +1740,208 @@ MJH_HD void camlight(const mjhipModel& m, const Lane<S>& d) {
   }
 }
 
-// mj_tendon :651-860 (fixed tendons; spatial tendons through sites and pulleys; dense ten_J)
+// ---- tendon wrapping around spheres and cylinders (engine_util_misc.c:33-418), on plain
+// per-lane doubles
+MJH_HD double dot2(const double* a, const double* b) { return 0.0 + (a[0]*b[0] + a[1]*b[1]); }
+
+// mju_normalize, n = 2 (engine_util_blas.c:651-668)
+MJH_HD double normalize2(double* v) {
+  double norm = sqrt(dot2(v, v));
+  if (norm < MINVAL) {
+    v[0] = 1; v[1] = 0;
+  } else {
+    double inv = 1/norm;
+    v[0] *= inv; v[1] *= inv;
+  }
+  return norm;
+}
+
+// :33-50 segments p1-p2 and p3-p4 intersect
+MJH_HD bool wrapIntersect(const double* p1, const double* p2, const double* p3,
+                          const double* p4) {
+  double det = (p4[1]-p3[1])*(p2[0]-p1[0]) - (p4[0]-p3[0])*(p2[1]-p1[1]);
+  if (fabs(det) < MINVAL) return false;
+  double a = ((p4[0]-p3[0])*(p1[1]-p3[1]) - (p4[1]-p3[1])*(p1[0]-p3[0])) / det;
+  double b = ((p2[0]-p1[0])*(p1[1]-p3[1]) - (p2[1]-p1[1])*(p1[0]-p3[0])) / det;
+  return a >= 0 && a <= 1 && b >= 0 && b <= 1;
+}
+
+// :77-151 circle wrap: tangent points pnt[4] and arc length, or -1 when the segment clears
+MJH_HD double wrapCircle(double pnt[4], const double end[4], const double* side,
+                         double radius) {
+  const double sqlen0 = end[0]*end[0] + end[1]*end[1];
+  const double sqlen1 = end[2]*end[2] + end[3]*end[3];
+  const double sqrad = radius*radius;
+  if (sqlen0 < sqrad || sqlen1 < sqrad || radius < MINVAL) return -1;
+  const double dif[2] = {end[2]-end[0], end[3]-end[1]};
+  const double dd = dif[0]*dif[0] + dif[1]*dif[1];
+  if (dd < MINVAL) return -1;
+  double a = -(dif[0]*end[0] + dif[1]*end[1])/dd;
+  a = a < 0 ? 0 : (a > 1 ? 1 : a);
+  double tmp[2] = {a*dif[0] + end[0], a*dif[1] + end[1]};
+  if (tmp[0]*tmp[0] + tmp[1]*tmp[1] > sqrad && (!side || dot2(side, tmp) >= 0)) return -1;
+  const double sqrt0 = sqrt(sqlen0 - sqrad), sqrt1 = sqrt(sqlen1 - sqrad);
+  double sol[2][4], good[2];
+  for (int i = 0; i < 2; i++) {
+    const int sgn = i == 0 ? 1 : -1;
+    sol[i][0] = (end[0]*sqrad + sgn*radius*end[1]*sqrt0)/sqlen0;
+    sol[i][1] = (end[1]*sqrad - sgn*radius*end[0]*sqrt0)/sqlen0;
+    sol[i][2] = (end[2]*sqrad - sgn*radius*end[3]*sqrt1)/sqlen1;
+    sol[i][3] = (end[3]*sqrad + sgn*radius*end[2]*sqrt1)/sqlen1;
+    if (side) {
+      tmp[0] = sol[i][0] + sol[i][2];
+      tmp[1] = sol[i][1] + sol[i][3];
+      normalize2(tmp);
+      good[i] = dot2(tmp, side);
+    } else {
+      tmp[0] = sol[i][0] - sol[i][2];
+      tmp[1] = sol[i][1] - sol[i][3];
+      good[i] = -dot2(tmp, tmp);
+    }
+    if (wrapIntersect(end, sol[i], end + 2, sol[i] + 2)) good[i] = -10000;
+  }
+  const int i = good[0] > good[1] ? 0 : 1;
+  for (int k = 0; k < 4; k++) pnt[k] = sol[i][k];
+  if (wrapIntersect(end, pnt, end + 2, pnt + 2)) return -1;
+  // :55-71 arc length, the long way round for the second solution's orientation
+  double p0n[2] = {pnt[0], pnt[1]}, p1n[2] = {pnt[2], pnt[3]};
+  normalize2(p0n);
+  normalize2(p1n);
+  double angle = acos(dot2(p0n, p1n));
+  const double cr = pnt[1]*pnt[2] - pnt[0]*pnt[3];
+  if ((cr > 0 && i) || (cr < 0 && !i)) angle = 2*mjhipPI - angle;
+  return radius*angle;
+}
+
+// :157-272 inside wrap (side site within the circle): one contact point by Newton
+// iterations on asin(A z) + asin(B z) - 2 asin(z) + G = 0; returns 0, or -1
+MJH_HD double wrapInside(double pnt[4], const double end[4], double radius) {
+  const double len0 = sqrt(dot2(end, end)), len1 = sqrt(dot2(end + 2, end + 2));
+  const double dif[2] = {end[2]-end[0], end[3]-end[1]};
+  const double dd = dif[0]*dif[0] + dif[1]*dif[1];
+  if (len0 <= radius || len1 <= radius || radius < MINVAL || len0 < MINVAL || len1 < MINVAL) {
+    return -1;
+  }
+  if (dd > MINVAL) {
+    const double a = -(dif[0]*end[0] + dif[1]*end[1]) / dd;
+    if (a > 0 && a < 1) {
+      const double tmp[2] = {end[0] + a*dif[0], end[1] + a*dif[1]};
+      if (sqrt(dot2(tmp, tmp)) <= radius) return -1;
+    }
+  }
+  pnt[0] = 0.5*(end[0] + end[2]);
+  pnt[1] = 0.5*(end[1] + end[3]);
+  normalize2(pnt);
+  pnt[0] *= radius;
+  pnt[1] *= radius;
+  pnt[2] = pnt[0];
+  pnt[3] = pnt[1];
+  const double A = radius/len0, B = radius/len1;
+  const double cosG = (len0*len0 + len1*len1 - dd) / (2*len0*len1);
+  if (cosG < -1 + MINVAL) return -1;
+  if (cosG > 1 - MINVAL) return 0;
+  const double G = acos(cosG);
+  double z = 1 - 1e-7;
+  double f = asin(A*z) + asin(B*z) - 2*asin(z) + G;
+  if (f > 0) return 0;
+  int iter;
+  for (iter = 0; iter < 20 && fabs(f) > 1e-6; iter++) {
+    const double df = A/fmax(MINVAL, sqrt(1 - z*z*A*A)) + B/fmax(MINVAL, sqrt(1 - z*z*B*B)) -
+                      2/fmax(MINVAL, sqrt(1 - z*z));
+    if (df > -MINVAL) return 0;
+    const double z1 = z - f/df;
+    if (z1 > z) return 0;
+    z = z1;
+    f = asin(A*z) + asin(B*z) - 2*asin(z) + G;
+    if (f > 1e-6) return 0;
+  }
+  if (iter >= 20) return 0;
+  double vec[2], ang;
+  if (end[0]*end[3] - end[1]*end[2] > 0) {
+    vec[0] = end[0]; vec[1] = end[1];
+    ang = asin(z) - asin(A*z);
+  } else {
+    vec[0] = end[2]; vec[1] = end[3];
+    ang = asin(z) - asin(B*z);
+  }
+  normalize2(vec);
+  pnt[0] = radius*(cos(ang)*vec[0] - sin(ang)*vec[1]);
+  pnt[1] = radius*(sin(ang)*vec[0] + cos(ang)*vec[1]);
+  pnt[2] = pnt[0];
+  pnt[3] = pnt[1];
+  return 0;
+}
+
+// :282-418 mju_wrap: segment x0-x1 around the sphere/cylinder at xpos/xmat; the tangent
+// points (global frame) in wpnt[6] and the wrapped length, or -1 for no wrap
+MJH_HD double wrapGeom(double wpnt[6], const double x0[3], const double x1[3],
+                       const double xpos[3], const double xmat[9], double radius, int type,
+                       const double* side) {
+  double tmp[3], p0[3], p1[3];
+  sub3(tmp, x0, xpos);
+  mulMatTVec3(p0, xmat, tmp);
+  sub3(tmp, x1, xpos);
+  mulMatTVec3(p1, xmat, tmp);
+  if (sqrt(dot3(p0, p0)) < MINVAL || sqrt(dot3(p1, p1)) < MINVAL) return -1;
+  double ax0[3], ax1[3];
+  if (type == mjhipWRAP_SPHERE) {
+    copy3(ax0, p0);
+    normalize3(ax0);
+    double normal[3];
+    cross(normal, p0, p1);
+    if (normalize3(normal) < MINVAL) {        // p0, p1 parallel: any normal
+      int i = 0;
+      if (fabs(ax0[1]) > fabs(ax0[0]) && fabs(ax0[1]) > fabs(ax0[2])) i = 1;
+      if (fabs(ax0[2]) > fabs(ax0[0]) && fabs(ax0[2]) > fabs(ax0[1])) i = 2;
+      ax1[0] = 1; ax1[1] = 1; ax1[2] = 1;
+      ax1[i] = 0;
+      cross(normal, ax0, ax1);
+      normalize3(normal);
+    }
+    cross(ax1, normal, ax0);
+    normalize3(ax1);
+  } else {
+    ax0[0] = 1; ax0[1] = 0; ax0[2] = 0;
+    ax1[0] = 0; ax1[1] = 1; ax1[2] = 0;
+  }
+  const double end[4] = {dot3(p0, ax0), dot3(p0, ax1), dot3(p1, ax0), dot3(p1, ax1)};
+  double s[3], sd[2];
+  if (side) {
+    sub3(tmp, side, xpos);
+    mulMatTVec3(s, xmat, tmp);
+    sd[0] = dot3(s, ax0);
+    sd[1] = dot3(s, ax1);
+    normalize2(sd);
+    sd[0] *= radius;
+    sd[1] *= radius;
+  }
+  double pnt[4];
+  double wlen = side && sqrt(dot3(s, s)) < radius ? wrapInside(pnt, end, radius)
+                                                  : wrapCircle(pnt, end, side ? sd : nullptr, radius);
+  if (wlen < 0) return -1;
+  double res[6];
+  for (int i = 0; i < 2; i++) {
+    scl3(res + 3*i, ax0, pnt[2*i]);
+    scl3(tmp, ax1, pnt[2*i + 1]);
+    addTo3(res + 3*i, tmp);
+  }
+  if (type == mjhipWRAP_CYLINDER) {           // spread the height change along the path
+    const double L0 = sqrt((p0[0]-res[0])*(p0[0]-res[0]) + (p0[1]-res[1])*(p0[1]-res[1]));
+    const double L1 = sqrt((p1[0]-res[3])*(p1[0]-res[3]) + (p1[1]-res[4])*(p1[1]-res[4]));
+    res[2] = p0[2] + (p1[2] - p0[2])*L0 / (L0+wlen+L1);
+    res[5] = p0[2] + (p1[2] - p0[2])*(L0+wlen) / (L0+wlen+L1);
+    const double height = fabs(res[5] - res[2]);
+    wlen = sqrt(wlen*wlen + height*height);
+  }
+  mulMatVec3(wpnt, xmat, res);
+  mulMatVec3(wpnt + 3, xmat, res + 3);
+  addTo3(wpnt, xpos);
+  addTo3(wpnt + 3, xpos);
+  return wlen;
+}
+
+// mj_tendon :651-860 (fixed tendons; spatial tendons through sites, pulleys and wrapping
+// spheres/cylinders; dense ten_J)
 template <int S>
 MJH_HD void tendon(const mjhipModel& m, const Lane<S>& d) {
   int nv = m.nv, nten = m.ntendon;
@@ -1758,36 +1959,72 @@ MJH_HD void tendon(const mjhipModel& m, const Lane<S>& d) {
       }
       continue;
     }
-    // spatial: consecutive site pairs; a pulley divides the length and moment that follow
+    // spatial: site-site or site-geom-site sequences; a pulley divides the length and
+    // moment that follow
     double divisor = 1;
-    for (int j = 0; j < num - 1; j++) {
+    int j = 0;
+    while (j < num - 1) {
       const int type0 = m.wrap_type[adr+j], type1 = m.wrap_type[adr+j+1];
       if (type0 == mjhipWRAP_PULLEY || type1 == mjhipWRAP_PULLEY) {
         if (type0 == mjhipWRAP_PULLEY) divisor = m.wrap_prm[adr+j];
+        j++;
         continue;
       }
-      const int id0 = m.wrap_objid[adr+j], id1 = m.wrap_objid[adr+j+1];
-      double p0[3], p1[3], dif[3];
+      const bool wrapped = type1 == mjhipWRAP_SPHERE || type1 == mjhipWRAP_CYLINDER;
+      const int id0 = m.wrap_objid[adr+j];
+      const int id1 = m.wrap_objid[adr + j + (wrapped ? 2 : 1)];
+      double wpnt[12], x1[3], wlen = -1;
+      int wbody[4];
       for (int k = 0; k < 3; k++) {
-        p0[k] = d.site_xpos[3*id0 + k];
-        p1[k] = d.site_xpos[3*id1 + k];
+        wpnt[k] = d.site_xpos[3*id0 + k];
+        x1[k] = d.site_xpos[3*id1 + k];
       }
-      sub3(dif, p1, p0);
-      d.ten_length[i] += sqrt(dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2]) / divisor;
-      const int b0 = m.site_bodyid[id0], b1 = m.site_bodyid[id1];
-      if (b0 == b1) continue;
-      normalize3(dif);
-      SP<S> j1 = d.jact, j2 = d.jact + 3*nv;
-      jacInto(m, d, j1, d.jacr, p0, b0);
-      jacInto(m, d, j2, d.jacr, p1, b1);
-      const double inv = 1/divisor;
-      for (int c = 0; c < nv; c++) {   // mju_mulMatTVec of (jac2 - jac1) with dif, then
-        double t = 0;                   // mju_addToScl(ten_J row, ., 1/divisor)
-        for (int r = 0; r < 3; r++) {
-          if (dif[r]) t += (j2[r*nv + c] - j1[r*nv + c])*dif[r];
+      wbody[0] = m.site_bodyid[id0];
+      int g = -1;
+      if (wrapped) {
+        g = m.wrap_objid[adr+j+1];
+        const int side = (int)lround(m.wrap_prm[adr+j+1]);
+        double gpos[3], gmat[9], spos[3];
+        for (int k = 0; k < 3; k++) gpos[k] = d.geom_xpos[3*g + k];
+        for (int k = 0; k < 9; k++) gmat[k] = d.geom_xmat[9*g + k];
+        if (side >= 0) {
+          for (int k = 0; k < 3; k++) spos[k] = d.site_xpos[3*side + k];
         }
-        d.ten_J[i*nv + c] += t*inv;
+        wlen = wrapGeom(wpnt + 3, wpnt, x1, gpos, gmat, m.geom_size[3*g], type1,
+                        side >= 0 ? spos : nullptr);
       }
+      double dif[3];
+      if (wlen < 0) {
+        copy3(wpnt + 3, x1);
+        wbody[1] = m.site_bodyid[id1];
+        sub3(dif, wpnt, wpnt + 3);
+        d.ten_length[i] += sqrt(dot3(dif, dif)) / divisor;
+      } else {
+        copy3(wpnt + 9, x1);
+        wbody[1] = wbody[2] = m.geom_bodyid[g];
+        wbody[3] = m.site_bodyid[id1];
+        double d2[3];
+        sub3(dif, wpnt, wpnt + 3);
+        sub3(d2, wpnt + 6, wpnt + 9);
+        d.ten_length[i] += (sqrt(dot3(dif, dif)) + wlen + sqrt(dot3(d2, d2))) / divisor;
+      }
+      for (int k = 0; k < (wlen < 0 ? 1 : 3); k++) {
+        if (wbody[k] == wbody[k+1]) continue;
+        sub3(dif, wpnt + 3*k + 3, wpnt + 3*k);
+        normalize3(dif);
+        SP<S> j1 = d.jact, j2 = d.jact + 3*nv;
+        jacInto(m, d, j1, d.jacr, wpnt + 3*k, wbody[k]);
+        jacInto(m, d, j2, d.jacr, wpnt + 3*k + 3, wbody[k+1]);
+        const double inv = 1/divisor;
+        for (int c = 0; c < nv; c++) {   // mju_mulMatTVec of (jac2 - jac1) with dif, then
+          double t = 0;                   // mju_addToScl(ten_J row, ., 1/divisor)
+          for (int r = 0; r < 3; r++) {
+            if (dif[r]) t += (j2[r*nv + c] - j1[r*nv + c])*dif[r];
+          }
+          d.ten_J[i*nv + c] += t*inv;
+        }
+      }
+      j += wrapped ? 2 : 1;
     }
   }
 }

@@ -757,8 +757,8 @@ static const char* unsupported(const mjhipModel* m) {
   }
   for (int i = 0; i < m->ntendon; i++) {
     for (int w = m->tendon_adr[i]; w < m->tendon_adr[i] + m->tendon_num[i]; w++) {
-      if (m->wrap_type[w] == mjhipWRAP_SPHERE || m->wrap_type[w] == mjhipWRAP_CYLINDER) {
-        return "spatial tendons wrapping around geoms";
+      if (m->wrap_type[w] < mjhipWRAP_JOINT || m->wrap_type[w] > mjhipWRAP_CYLINDER) {
+        return "unknown tendon wrap object type";
       }
     }
   }

@@ -452,8 +452,8 @@ def unsupported(ints, arrays) -> str | None:
     return "tendon frictionloss (FRICTION_TENDON rows)"
   if ints["ngeom"] and (arrays["geom_fluid"][:, 0] > 0).any():
     return "the ellipsoid fluid model (geom fluidshape)"
-  if ints["nwrap"] and np.isin(arrays["wrap_type"], (4, 5)).any():   # sphere, cylinder
-    return "spatial tendons wrapping around geoms"
+  if ints["nwrap"] and not np.isin(arrays["wrap_type"], (1, 2, 3, 4, 5)).all():
+    return "unknown tendon wrap object type"
   return None
 
 

@@ -597,8 +597,7 @@ class MJCFCompiler:
               elif w.tag == "pulley":
                 path.append(("pulley", float(w.get("divisor", "0"))))
               elif w.tag == "geom":
-                raise MJCFError("spatial tendons wrapping around geoms (sphere/cylinder "
-                                "wrapping) are not in the supported subset")
+                path.append(("geom", (w.get("geom"), w.get("sidesite"))))
               else:
                 raise MJCFError(f"unsupported spatial tendon element <{w.tag}>")
           self.tendons.append((a, path))
@@ -1255,6 +1254,7 @@ class MJCFCompiler:
     wprm = arr("wrap_prm", nwrap, np.float64)
     w = 0
     sitename_t = {x["name"]: i for i, x in enumerate(sites) if x["name"]}
+    geomname_t = {g["name"]: i for i, g in enumerate(geoms) if g["name"]}
     for ti, (ta, jl) in enumerate(self.tendons):
       tadr[ti] = w
       tnum[ti] = len(jl)
@@ -1297,6 +1297,27 @@ class MJCFCompiler:
             if i == sz - 1:
               raise MJCFError(f"tendon (id = {ti}): path ends with pulley")
             wtype[w], wobj[w], wprm[w] = 2, -1, val     # mjWRAP_PULLEY
+          elif kind == "geom":
+            # mjCWrap::Compile (user_objects.cc:5647-5676): sphere or cylinder geom, optional
+            # side site; wrap_prm = side site id or -1 (user_model.cc:3219-3221)
+            gname, side = val
+            if gname not in geomname_t:
+              raise MJCFError(f"geom '{gname}' not found in tendon {ti}, wrap {i}")
+            gi = geomname_t[gname]
+            gt = geoms[gi]["type"]
+            if gt not in (GEOM["sphere"], GEOM["cylinder"]):
+              raise MJCFError(f"geom '{gname}' in tendon {ti}, wrap {i} is not sphere or "
+                              "cylinder")
+            sid = -1
+            if side is not None:
+              if side not in sitename_t:
+                raise MJCFError(f"side site '{side}' not found in tendon {ti}, wrap {i}")
+              sid = sitename_t[side]
+            if i == 0 or i == sz - 1 or jl[i - 1][0] != "site" or jl[i + 1][0] != "site":
+              raise MJCFError(f"tendon '{ta.get('name', '')}' (id = {ti}): geom at pos {i} "
+                              "not bracketed by sites")
+            wtype[w] = 4 if gt == GEOM["sphere"] else 5   # mjWRAP_SPHERE / mjWRAP_CYLINDER
+            wobj[w], wprm[w] = gi, float(sid)
           else:
             if val not in sitename_t:
               raise MJCFError(f"unknown site '{val}' in tendon")
@@ -1801,15 +1822,16 @@ def sparse_structures(sizes: dict, A) -> dict:
       gzero = agear[ai, 0] == 0 if atrn[ai] == 2 else not np.any(agear[ai])
       c = [] if gzero else sorted(c)
     elif int(np.asarray(A["wrap_type"]).reshape(-1)[tadr[tid]]) != 1:
-      # spatial tendon: ten_J is nonzero on the dof chains of the path's site bodies (the
-      # reference compresses its dense row by value, :1070-1079; generic states have no
-      # exact zeros there)
+      # spatial tendon: ten_J is nonzero on the dof chains of the path's site and wrap-geom
+      # bodies (the reference compresses its dense row by value, :1070-1079; generic states
+      # have no exact zeros there)
       wtype = np.asarray(A["wrap_type"]).reshape(-1)
+      gbody = np.asarray(A["geom_bodyid"]).reshape(-1)
       c = set()
       for wi in range(tadr[tid], tadr[tid] + tnum[tid]):
-        if wtype[wi] != 3:
+        if wtype[wi] not in (3, 4, 5):
           continue
-        b = int(sbody[wobj[wi]])
+        b = int(sbody[wobj[wi]] if wtype[wi] == 3 else gbody[wobj[wi]])
         while b > 0:
           c.update(range(dofadr[b], dofadr[b] + dofnum[b]))
           b = int(parentid[b])

@@ -209,6 +209,146 @@ class _Eval:
     return jacp, jacr
 
 
+_MINVAL = 1e-15
+
+
+def _norm2(v):
+  n = np.sqrt(v[0]*v[0] + v[1]*v[1])
+  return np.array([1.0, 0.0]) if n < _MINVAL else v / n
+
+
+def _intersect(p1, p2, p3, p4):
+  """is_intersect (engine_util_misc.c:33-50)."""
+  det = (p4[1]-p3[1])*(p2[0]-p1[0]) - (p4[0]-p3[0])*(p2[1]-p1[1])
+  if abs(det) < _MINVAL:
+    return False
+  a = ((p4[0]-p3[0])*(p1[1]-p3[1]) - (p4[1]-p3[1])*(p1[0]-p3[0])) / det
+  b = ((p2[0]-p1[0])*(p1[1]-p3[1]) - (p2[1]-p1[1])*(p1[0]-p3[0])) / det
+  return 0 <= a <= 1 and 0 <= b <= 1
+
+
+def _wrap_circle(e0, e1, side, r):
+  """wrap_circle + length_circle (engine_util_misc.c:55-151): tangent points, arc length."""
+  sq0, sq1, sqr = e0 @ e0, e1 @ e1, r * r
+  if sq0 < sqr or sq1 < sqr or r < _MINVAL:
+    return None
+  dif = e1 - e0
+  dd = dif @ dif
+  if dd < _MINVAL:
+    return None
+  a = min(max(-(dif @ e0) / dd, 0.0), 1.0)
+  near = a * dif + e0
+  if near @ near > sqr and (side is None or side @ near >= 0):
+    return None
+  s0, s1 = np.sqrt(sq0 - sqr), np.sqrt(sq1 - sqr)
+  sols, good = [], []
+  for sgn in (1, -1):
+    t0 = np.array([e0[0]*sqr + sgn*r*e0[1]*s0, e0[1]*sqr - sgn*r*e0[0]*s0]) / sq0
+    t1 = np.array([e1[0]*sqr - sgn*r*e1[1]*s1, e1[1]*sqr + sgn*r*e1[0]*s1]) / sq1
+    g = _norm2(t0 + t1) @ side if side is not None else -((t0 - t1) @ (t0 - t1))
+    if _intersect(e0, t0, e1, t1):
+      g = -10000
+    sols.append((t0, t1))
+    good.append(g)
+  i = 0 if good[0] > good[1] else 1
+  t0, t1 = sols[i]
+  if _intersect(e0, t0, e1, t1):
+    return None
+  ang = np.arccos(_norm2(t0) @ _norm2(t1))
+  cr = t0[1]*t1[0] - t0[0]*t1[1]
+  if (cr > 0 and i) or (cr < 0 and not i):
+    ang = 2 * np.pi - ang
+  return t0, t1, r * ang
+
+
+def _wrap_inside(e0, e1, r):
+  """wrap_inside (engine_util_misc.c:157-272): the side site inside the circle."""
+  l0, l1 = np.sqrt(e0 @ e0), np.sqrt(e1 @ e1)
+  dif = e1 - e0
+  dd = dif @ dif
+  if l0 <= r or l1 <= r or r < _MINVAL or l0 < _MINVAL or l1 < _MINVAL:
+    return None
+  if dd > _MINVAL:
+    a = -(dif @ e0) / dd
+    if 0 < a < 1 and np.linalg.norm(e0 + a * dif) <= r:
+      return None
+  p = _norm2(0.5 * (e0 + e1)) * r
+  A, B = r / l0, r / l1
+  cosG = (l0*l0 + l1*l1 - dd) / (2*l0*l1)
+  if cosG < -1 + _MINVAL:
+    return None
+  if cosG > 1 - _MINVAL:
+    return p, p, 0.0
+  G = np.arccos(cosG)
+  z = 1 - 1e-7
+  f = np.arcsin(A*z) + np.arcsin(B*z) - 2*np.arcsin(z) + G
+  if f > 0:
+    return p, p, 0.0
+  it = 0
+  while it < 20 and abs(f) > 1e-6:
+    df = (A / max(_MINVAL, np.sqrt(1 - z*z*A*A)) + B / max(_MINVAL, np.sqrt(1 - z*z*B*B))
+          - 2 / max(_MINVAL, np.sqrt(1 - z*z)))
+    if df > -_MINVAL:
+      return p, p, 0.0
+    z1 = z - f / df
+    if z1 > z:
+      return p, p, 0.0
+    z = z1
+    f = np.arcsin(A*z) + np.arcsin(B*z) - 2*np.arcsin(z) + G
+    if f > 1e-6:
+      return p, p, 0.0
+    it += 1
+  if it >= 20:
+    return p, p, 0.0
+  if e0[0]*e1[1] - e0[1]*e1[0] > 0:
+    vec, ang = _norm2(e0), np.arcsin(z) - np.arcsin(A*z)
+  else:
+    vec, ang = _norm2(e1), np.arcsin(z) - np.arcsin(B*z)
+  p = r * np.array([np.cos(ang)*vec[0] - np.sin(ang)*vec[1],
+                    np.sin(ang)*vec[0] + np.cos(ang)*vec[1]])
+  return p, p, 0.0
+
+
+def wrap(x0, x1, xpos, xmat, r, wtype, side):
+  """mju_wrap (engine_util_misc.c:282-418): (tangent point 0, tangent point 1, length) of
+  the segment x0-x1 around a sphere (wtype 4) or cylinder (5), or None when it clears."""
+  p0, p1 = xmat.T @ (x0 - xpos), xmat.T @ (x1 - xpos)
+  if np.linalg.norm(p0) < _MINVAL or np.linalg.norm(p1) < _MINVAL:
+    return None
+  if wtype == 4:
+    ax0 = p0 / max(np.linalg.norm(p0), _MINVAL)
+    n = np.cross(p0, p1)
+    if np.linalg.norm(n) < _MINVAL:
+      a = np.abs(ax0)
+      i = 2 if a[2] > a[0] and a[2] > a[1] else (1 if a[1] > a[0] and a[1] > a[2] else 0)
+      ax1 = np.ones(3)
+      ax1[i] = 0
+      n = np.cross(ax0, ax1)
+    n = n / np.linalg.norm(n)
+    ax1 = np.cross(n, ax0)
+    ax1 = ax1 / np.linalg.norm(ax1)
+  else:
+    ax0, ax1 = np.array([1.0, 0, 0]), np.array([0, 1.0, 0])
+  e0, e1 = np.array([p0 @ ax0, p0 @ ax1]), np.array([p1 @ ax0, p1 @ ax1])
+  if side is not None:
+    s = xmat.T @ (side - xpos)
+    sd = _norm2(np.array([s @ ax0, s @ ax1])) * r
+    out = _wrap_inside(e0, e1, r) if np.linalg.norm(s) < r else _wrap_circle(e0, e1, sd, r)
+  else:
+    out = _wrap_circle(e0, e1, None, r)
+  if out is None:
+    return None
+  t0, t1, wlen = out
+  r0, r1 = ax0 * t0[0] + ax1 * t0[1], ax0 * t1[0] + ax1 * t1[1]
+  if wtype == 5:
+    L0 = np.hypot(p0[0] - r0[0], p0[1] - r0[1])
+    L1 = np.hypot(p1[0] - r1[0], p1[1] - r1[1])
+    r0[2] = p0[2] + (p1[2] - p0[2]) * L0 / (L0 + wlen + L1)
+    r1[2] = p0[2] + (p1[2] - p0[2]) * (L0 + wlen) / (L0 + wlen + L1)
+    wlen = np.sqrt(wlen * wlen + (r1[2] - r0[2]) ** 2)
+  return xmat @ r0 + xpos, xmat @ r1 + xpos, wlen
+
+
 def set_const(m):
   """Fill the compile-time constants of `m` in place (mj_setConst subset)."""
   nv, nb = m.nv, m.nbody
@@ -266,23 +406,45 @@ def set_const(m):
           J[t, m.jnt_dofadr[k]] = m.wrap_prm[w]
         continue
       divisor = 1.0
-      for w in range(adr, adr + num - 1):
+      site = lambda s: ev.xmat[m.site_bodyid[s]] @ m.site_pos[s] + ev.xpos[m.site_bodyid[s]]
+      w = adr
+      while w < adr + num - 1:
         if m.wrap_type[w] == 2 or m.wrap_type[w + 1] == 2:
           if m.wrap_type[w] == 2:
             divisor = m.wrap_prm[w]
+          w += 1
           continue
-        s0, s1 = m.wrap_objid[w], m.wrap_objid[w + 1]
-        b0, b1 = m.site_bodyid[s0], m.site_bodyid[s1]
-        p0 = ev.xmat[b0] @ m.site_pos[s0] + ev.xpos[b0]
-        p1 = ev.xmat[b1] @ m.site_pos[s1] + ev.xpos[b1]
-        dif = p1 - p0
-        L[t] += np.linalg.norm(dif) / divisor
-        if b0 != b1:
+        wrapped = m.wrap_type[w + 1] in (4, 5)
+        s0, s1 = m.wrap_objid[w], m.wrap_objid[w + (2 if wrapped else 1)]
+        pts, bodies = [site(s0)], [m.site_bodyid[s0]]
+        out = None
+        if wrapped:
+          g = m.wrap_objid[w + 1]
+          gb = m.geom_bodyid[g]
+          gpos = ev.xmat[gb] @ m.geom_pos[g] + ev.xpos[gb]
+          gmat = _quat2mat(_normq(_mulquat(ev.xquat[gb], m.geom_quat[g])))
+          sid = int(round(m.wrap_prm[w + 1]))
+          out = wrap(pts[0], site(s1), gpos, gmat, m.geom_size[g, 0], m.wrap_type[w + 1],
+                     site(sid) if sid >= 0 else None)
+        if out is None:
+          pts.append(site(s1))
+          bodies.append(m.site_bodyid[s1])
+          L[t] += np.linalg.norm(pts[1] - pts[0]) / divisor
+        else:
+          pts += [out[0], out[1], site(s1)]
+          bodies += [gb, gb, m.site_bodyid[s1]]
+          L[t] += (np.linalg.norm(pts[1] - pts[0]) + out[2]
+                   + np.linalg.norm(pts[3] - pts[2])) / divisor
+        for k in range(len(pts) - 1):
+          if bodies[k] == bodies[k + 1]:
+            continue
+          dif = pts[k + 1] - pts[k]
           n = np.linalg.norm(dif)
           dif = dif / n if n >= 1e-15 else np.array([1.0, 0, 0])
-          j0, _ = ev.jac_point(m, b0, p0)
-          j1, _ = ev.jac_point(m, b1, p1)
+          j0, _ = ev.jac_point(m, bodies[k], pts[k])
+          j1, _ = ev.jac_point(m, bodies[k + 1], pts[k + 1])
           J[t] += (dif @ (j1 - j0)) / divisor
+        w += 2 if wrapped else 1
     return L, J
   L0, J0 = tendon(m.qpos0, e)
   m.tendon_length0[:] = L0

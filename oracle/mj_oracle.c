@@ -693,9 +693,231 @@ static void or_camlight(const mjhipModel* m, mjhipData* d) {
   }
 }
 
-/* :651-860, fixed tendons and spatial tendons through sites and pulleys, dense Jacobian
- * (the wrap visualization outputs ten_wrapadr/ten_wrapnum/wrap_obj/wrap_xpos are not kept;
- * sphere/cylinder wrapping is outside the subset, the loader rejects it) */
+/* ---- tendon wrapping around spheres and cylinders (engine_util_misc.c:33-418) ---- */
+static mjtNum mju_dot3(const mjtNum* a, const mjtNum* b);
+static mjtNum mju_norm3(const mjtNum* a);
+static void mju_mulMatTVec3(mjtNum res[3], const mjtNum mat[9], const mjtNum vec[3]);
+
+/* mju_normalize for n = 2 (engine_util_blas.c:651-668) */
+static mjtNum or_normalize2(mjtNum* v) {
+  mjtNum norm = sqrt(mju_dot(v, v, 2));
+  if (norm < mjMINVAL) {
+    v[0] = 1; v[1] = 0;
+  } else {
+    mjtNum inv = 1/norm;
+    v[0] *= inv; v[1] *= inv;
+  }
+  return norm;
+}
+
+/* :33-50 do segments p1-p2 and p3-p4 intersect */
+static int or_isIntersect(const mjtNum* p1, const mjtNum* p2, const mjtNum* p3,
+                          const mjtNum* p4) {
+  mjtNum det = (p4[1]-p3[1])*(p2[0]-p1[0]) - (p4[0]-p3[0])*(p2[1]-p1[1]);
+  if (fabs(det) < mjMINVAL) return 0;
+  mjtNum a = ((p4[0]-p3[0])*(p1[1]-p3[1]) - (p4[1]-p3[1])*(p1[0]-p3[0])) / det;
+  mjtNum b = ((p2[0]-p1[0])*(p1[1]-p3[1]) - (p2[1]-p1[1])*(p1[0]-p3[0])) / det;
+  return a >= 0 && a <= 1 && b >= 0 && b <= 1;
+}
+
+/* :55-71 arc length from p0 to p1 on the circle, the long way for the flipped solution */
+static mjtNum or_lengthCircle(const mjtNum* p0, const mjtNum* p1, int ind, mjtNum radius) {
+  mjtNum a[2] = {p0[0], p0[1]}, b[2] = {p1[0], p1[1]};
+  or_normalize2(a);
+  or_normalize2(b);
+  mjtNum angle = acos(mju_dot(a, b, 2));
+  mjtNum cross = p0[1]*p1[0] - p0[0]*p1[1];
+  if ((cross > 0 && ind) || (cross < 0 && !ind)) angle = 2*mjhipPI - angle;
+  return radius*angle;
+}
+
+/* :77-151 wrap a 2D segment around the circle of the given radius: tangent points in
+ * pnt[4], the arc length, or -1 when the segment clears the circle */
+static mjtNum or_wrapCircle(mjtNum pnt[4], const mjtNum end[4], const mjtNum* side,
+                            mjtNum radius) {
+  mjtNum sqlen0 = end[0]*end[0] + end[1]*end[1];
+  mjtNum sqlen1 = end[2]*end[2] + end[3]*end[3];
+  mjtNum sqrad = radius*radius;
+  if (sqlen0 < sqrad || sqlen1 < sqrad || radius < mjMINVAL) return -1;
+  mjtNum dif[2] = {end[2]-end[0], end[3]-end[1]};
+  mjtNum dd = dif[0]*dif[0] + dif[1]*dif[1];
+  if (dd < mjMINVAL) return -1;
+  mjtNum a = -(dif[0]*end[0] + dif[1]*end[1])/dd;
+  if (a < 0) a = 0;
+  else if (a > 1) a = 1;
+  mjtNum tmp[2] = {a*dif[0] + end[0], a*dif[1] + end[1]};
+  if (tmp[0]*tmp[0] + tmp[1]*tmp[1] > sqrad && (!side || mju_dot(side, tmp, 2) >= 0)) {
+    return -1;
+  }
+  mjtNum sol[2][2][2], good[2];
+  for (int i = 0; i < 2; i++) {
+    mjtNum sqrt0 = sqrt(sqlen0 - sqrad);
+    mjtNum sqrt1 = sqrt(sqlen1 - sqrad);
+    int sgn = i == 0 ? 1 : -1;
+    sol[i][0][0] = (end[0]*sqrad + sgn*radius*end[1]*sqrt0)/sqlen0;
+    sol[i][0][1] = (end[1]*sqrad - sgn*radius*end[0]*sqrt0)/sqlen0;
+    sol[i][1][0] = (end[2]*sqrad - sgn*radius*end[3]*sqrt1)/sqlen1;
+    sol[i][1][1] = (end[3]*sqrad + sgn*radius*end[2]*sqrt1)/sqlen1;
+    if (side) {
+      mju_add(tmp, sol[i][0], sol[i][1], 2);
+      or_normalize2(tmp);
+      good[i] = mju_dot(tmp, side, 2);
+    } else {
+      mju_sub(tmp, sol[i][0], sol[i][1], 2);
+      good[i] = -mju_dot(tmp, tmp, 2);
+    }
+    if (or_isIntersect(end, sol[i][0], end+2, sol[i][1])) good[i] = -10000;
+  }
+  int i = good[0] > good[1] ? 0 : 1;
+  pnt[0] = sol[i][0][0];
+  pnt[1] = sol[i][0][1];
+  pnt[2] = sol[i][1][0];
+  pnt[3] = sol[i][1][1];
+  if (or_isIntersect(end, pnt, end+2, pnt+2)) return -1;
+  return or_lengthCircle(sol[i][0], sol[i][1], i, radius);
+}
+
+/* :157-272 wrap with the side site inside the circle: one contact point found by Newton
+ * iterations on asin(A z) + asin(B z) - 2 asin(z) + G = 0; length 0, or -1 */
+static mjtNum or_wrapInside(mjtNum pnt[4], const mjtNum end[4], mjtNum radius) {
+  const int maxiter = 20;
+  const mjtNum zinit = 1 - 1e-7, tolerance = 1e-6;
+  mjtNum len0 = mju_norm(end, 2);
+  mjtNum len1 = mju_norm(end+2, 2);
+  mjtNum dif[2] = {end[2]-end[0], end[3]-end[1]};
+  mjtNum dd = dif[0]*dif[0] + dif[1]*dif[1];
+  if (len0 <= radius || len1 <= radius || radius < mjMINVAL || len0 < mjMINVAL ||
+      len1 < mjMINVAL) {
+    return -1;
+  }
+  if (dd > mjMINVAL) {
+    mjtNum a = -(dif[0]*end[0] + dif[1]*end[1]) / dd;
+    if (a > 0 && a < 1) {
+      mjtNum tmp[2] = {end[0] + a*dif[0], end[1] + a*dif[1]};
+      if (mju_norm(tmp, 2) <= radius) return -1;
+    }
+  }
+  pnt[0] = 0.5*(end[0] + end[2]);
+  pnt[1] = 0.5*(end[1] + end[3]);
+  or_normalize2(pnt);
+  pnt[0] *= radius;
+  pnt[1] *= radius;
+  pnt[2] = pnt[0];
+  pnt[3] = pnt[1];
+  mjtNum A = radius/len0, B = radius/len1;
+  mjtNum cosG = (len0*len0 + len1*len1 - dd) / (2*len0*len1);
+  if (cosG < -1+mjMINVAL) return -1;
+  if (cosG > 1-mjMINVAL) return 0;
+  mjtNum G = acos(cosG);
+  mjtNum z = zinit;
+  mjtNum f = asin(A*z) + asin(B*z) - 2*asin(z) + G;
+  if (f > 0) return 0;
+  int iter;
+  for (iter = 0; iter < maxiter && fabs(f) > tolerance; iter++) {
+    mjtNum df = A/fmax(mjMINVAL, sqrt(1-z*z*A*A)) + B/fmax(mjMINVAL, sqrt(1-z*z*B*B)) -
+                2/fmax(mjMINVAL, sqrt(1-z*z));
+    if (df > -mjMINVAL) return 0;
+    mjtNum z1 = z - f/df;
+    if (z1 > z) return 0;
+    z = z1;
+    f = asin(A*z) + asin(B*z) - 2*asin(z) + G;
+    if (f > tolerance) return 0;
+  }
+  if (iter >= maxiter) return 0;
+  mjtNum vec[2], ang;
+  if (end[0]*end[3] - end[1]*end[2] > 0) {
+    vec[0] = end[0]; vec[1] = end[1];
+    ang = asin(z) - asin(A*z);
+  } else {
+    vec[0] = end[2]; vec[1] = end[3];
+    ang = asin(z) - asin(B*z);
+  }
+  or_normalize2(vec);
+  pnt[0] = radius*(cos(ang)*vec[0] - sin(ang)*vec[1]);
+  pnt[1] = radius*(sin(ang)*vec[0] + cos(ang)*vec[1]);
+  pnt[2] = pnt[0];
+  pnt[3] = pnt[1];
+  return 0;
+}
+
+/* :282-418 mju_wrap: the segment x0-x1 around a sphere or cylinder at xpos/xmat; the two
+ * tangent points in wpnt[6] (global frame) and the wrapped length, or -1 for no wrap */
+static mjtNum or_wrap(mjtNum wpnt[6], const mjtNum x0[3], const mjtNum x1[3],
+                      const mjtNum xpos[3], const mjtNum xmat[9], mjtNum radius, int type,
+                      const mjtNum* side) {
+  mjtNum tmp[3], p[2][3];
+  mju_sub3(tmp, x0, xpos);
+  mju_mulMatTVec3(p[0], xmat, tmp);
+  mju_sub3(tmp, x1, xpos);
+  mju_mulMatTVec3(p[1], xmat, tmp);
+  if (mju_norm3(p[0]) < mjMINVAL || mju_norm3(p[1]) < mjMINVAL) return -1;
+  mjtNum axis[2][3];
+  if (type == mjhipWRAP_SPHERE) {
+    mju_copy3(axis[0], p[0]);
+    mju_normalize3(axis[0]);
+    mjtNum normal[3];
+    mju_cross(normal, p[0], p[1]);
+    mjtNum nrm = mju_normalize3(normal);
+    if (nrm < mjMINVAL) {
+      int i = 0;
+      if (fabs(axis[0][1]) > fabs(axis[0][0]) && fabs(axis[0][1]) > fabs(axis[0][2])) i = 1;
+      if (fabs(axis[0][2]) > fabs(axis[0][0]) && fabs(axis[0][2]) > fabs(axis[0][1])) i = 2;
+      axis[1][0] = 1; axis[1][1] = 1; axis[1][2] = 1;
+      axis[1][i] = 0;
+      mju_cross(normal, axis[0], axis[1]);
+      mju_normalize3(normal);
+    }
+    mju_cross(axis[1], normal, axis[0]);
+    mju_normalize3(axis[1]);
+  } else {
+    axis[0][0] = 1; axis[0][1] = 0; axis[0][2] = 0;
+    axis[1][0] = 0; axis[1][1] = 1; axis[1][2] = 0;
+  }
+  mjtNum s[3], dd[4], sd[2];
+  dd[0] = mju_dot3(p[0], axis[0]);
+  dd[1] = mju_dot3(p[0], axis[1]);
+  dd[2] = mju_dot3(p[1], axis[0]);
+  dd[3] = mju_dot3(p[1], axis[1]);
+  if (side) {
+    mju_sub3(tmp, side, xpos);
+    mju_mulMatTVec3(s, xmat, tmp);
+    sd[0] = mju_dot3(s, axis[0]);
+    sd[1] = mju_dot3(s, axis[1]);
+    or_normalize2(sd);
+    sd[0] *= radius;
+    sd[1] *= radius;
+  }
+  mjtNum wlen, pnt[4];
+  if (side && mju_norm3(s) < radius) {
+    wlen = or_wrapInside(pnt, dd, radius);
+  } else {
+    wlen = or_wrapCircle(pnt, dd, side ? sd : NULL, radius);
+  }
+  if (wlen < 0) return -1;
+  mjtNum res[6];
+  for (int i = 0; i < 2; i++) {
+    mju_scl3(res+3*i, axis[0], pnt[2*i]);
+    mju_scl3(tmp, axis[1], pnt[2*i+1]);
+    mju_addTo3(res+3*i, tmp);
+  }
+  if (type == mjhipWRAP_CYLINDER) {
+    mjtNum L0 = sqrt((p[0][0]-res[0])*(p[0][0]-res[0]) + (p[0][1]-res[1])*(p[0][1]-res[1]));
+    mjtNum L1 = sqrt((p[1][0]-res[3])*(p[1][0]-res[3]) + (p[1][1]-res[4])*(p[1][1]-res[4]));
+    res[2] = p[0][2] + (p[1][2] - p[0][2])*L0 / (L0+wlen+L1);
+    res[5] = p[0][2] + (p[1][2] - p[0][2])*(L0+wlen) / (L0+wlen+L1);
+    mjtNum height = fabs(res[5] - res[2]);
+    wlen = sqrt(wlen*wlen + height*height);
+  }
+  mju_mulMatVec3(wpnt, xmat, res);
+  mju_mulMatVec3(wpnt+3, xmat, res+3);
+  mju_addTo3(wpnt, xpos);
+  mju_addTo3(wpnt+3, xpos);
+  return wlen;
+}
+
+/* :651-860, fixed tendons and spatial tendons through sites, pulleys and wrapping spheres
+ * and cylinders, dense Jacobian (the wrap visualization outputs ten_wrapadr/ten_wrapnum/
+ * wrap_obj/wrap_xpos are not kept) */
 static void mju_mulMatTVec(mjtNum* res, const mjtNum* mat, const mjtNum* vec, int nr, int nc);
 
 static void or_tendon(const mjhipModel* m, mjhipData* d) {
@@ -718,28 +940,59 @@ static void or_tendon(const mjhipModel* m, mjhipData* d) {
       }
       continue;
     }
-    /* spatial: consecutive site pairs, a pulley divides what follows (:725-855) */
+    /* spatial: site-site or site-geom-site sequences, a pulley divides what follows
+     * (:725-855) */
     mjtNum divisor = 1;
-    for (int j = 0; j < tendon_num - 1; j++) {
+    int j = 0;
+    while (j < tendon_num - 1) {
       int type0 = m->wrap_type[adr+j], type1 = m->wrap_type[adr+j+1];
       if (type0 == mjhipWRAP_PULLEY || type1 == mjhipWRAP_PULLEY) {
         if (type0 == mjhipWRAP_PULLEY) divisor = m->wrap_prm[adr+j];
+        j++;
         continue;
       }
       int id0 = m->wrap_objid[adr+j], id1 = m->wrap_objid[adr+j+1];
-      const mjtNum* p0 = d->site_xpos + 3*id0;
-      const mjtNum* p1 = d->site_xpos + 3*id1;
-      int b0 = m->site_bodyid[id0], b1 = m->site_bodyid[id1];
-      mjtNum dif[3] = {p1[0]-p0[0], p1[1]-p0[1], p1[2]-p0[2]};
-      L[i] += sqrt(dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2]) / divisor;
-      if (b0 != b1) {
+      mjtNum wlen = -1, wpnt[12];
+      int wrapid = -1, wrapped = 0, wbody[4];
+      mju_copy3(wpnt, d->site_xpos + 3*id0);
+      wbody[0] = m->site_bodyid[id0];
+      if (type1 == mjhipWRAP_SPHERE || type1 == mjhipWRAP_CYLINDER) {
+        wrapped = 1;
+        wrapid = id1;
+        id1 = m->wrap_objid[adr+j+2];
+        int sideid = (int)lround(m->wrap_prm[adr+j+1]);
+        wlen = or_wrap(wpnt+3, d->site_xpos + 3*id0, d->site_xpos + 3*id1,
+                       d->geom_xpos + 3*wrapid, d->geom_xmat + 9*wrapid,
+                       m->geom_size[3*wrapid], type1,
+                       sideid >= 0 ? d->site_xpos + 3*sideid : NULL);
+      }
+      if (wlen < 0) {
+        mju_copy3(wpnt+3, d->site_xpos + 3*id1);
+        wbody[1] = m->site_bodyid[id1];
+        mjtNum dif[3];
+        mju_sub3(dif, wpnt, wpnt+3);
+        L[i] += mju_norm3(dif) / divisor;
+      } else {
+        mju_copy3(wpnt+9, d->site_xpos + 3*id1);
+        wbody[1] = wbody[2] = m->geom_bodyid[wrapid];
+        wbody[3] = m->site_bodyid[id1];
+        mjtNum d0[3], d2[3];
+        mju_sub3(d0, wpnt, wpnt+3);
+        mju_sub3(d2, wpnt+6, wpnt+9);
+        L[i] += (mju_norm3(d0) + wlen + mju_norm3(d2)) / divisor;
+      }
+      for (int k = 0; k < (wlen < 0 ? 1 : 3); k++) {
+        if (wbody[k] == wbody[k+1]) continue;
+        mjtNum dif[3];
+        mju_sub3(dif, wpnt+3*k+3, wpnt+3*k);
         mju_normalize3(dif);
-        mj_jac(m, d, jac1, NULL, p0, b0);
-        mj_jac(m, d, jac2, NULL, p1, b1);
-        for (int k = 0; k < 3*nv; k++) jac2[k] = jac2[k] - jac1[k];
+        mj_jac(m, d, jac1, NULL, wpnt+3*k, wbody[k]);
+        mj_jac(m, d, jac2, NULL, wpnt+3*k+3, wbody[k+1]);
+        for (int c = 0; c < 3*nv; c++) jac2[c] = jac2[c] - jac1[c];
         mju_mulMatTVec(tmp, jac2, dif, 3, nv);
         mju_addToScl(J + i*nv, tmp, 1/divisor, nv);
       }
+      j += wrapped ? 2 : 1;
     }
   }
   free(jac1);

@@ -983,17 +983,19 @@ def test_config3_full_batch_one_gpu(humanoid):
   assert_close(f[sub[:256]], ref["qfrc_inverse"], "qfrc_inverse (config 3 subsample)")
 
 
-def test_spatial_tendon_parity():
-  """Spatial tendons through sites and pulleys (lengths, Jacobians, limit rows, spring-
-  damper, tendon actuators) on the device vs the oracle; the model has no straight-line
-  kernel (the generic pipeline serves it)."""
+@pytest.mark.parametrize("which", ["sites", "wrap"])
+def test_spatial_tendon_parity(which):
+  """Spatial tendons through sites and pulleys, and wrapping around spheres and cylinders
+  (with side sites outside and inside the wrap geom, and without one): lengths, Jacobians,
+  limit rows, spring-damper, tendon actuators on the device vs the oracle; the models have
+  no straight-line kernel (the generic pipeline serves them)."""
   import os
   import sys
   sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
-  from test_tendon_cpu import ARM, _states
+  import test_tendon_cpu as T
   from mujoco_inversedynamicstest_amd import mjcf
-  m = mjcf.load_xml_string(ARM)
-  st = _states(m, 2048, 5)
+  m = mjcf.load_xml_string(T.ARM if which == "sites" else T.WRAP)
+  st = (T._states if which == "sites" else T._wrap_states)(m, 2048, 5)
   q = np.array([x[0] for x in st])
   v = np.array([x[1] for x in st])
   a = np.array([x[2] for x in st])

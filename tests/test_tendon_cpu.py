@@ -162,10 +162,181 @@ def test_device_bitexact(arm):
     ('<site site="s0"/><pulley divisor="2"/><site site="s1"/><site site="s2"/>',
      "needs a neighbor"),
     ('<site site="s0"/><site site="s0"/>', "is repeated"),
-    ('<site site="s0"/><geom geom="g"/><site site="s1"/>', "wrapping")])
+    ('<site site="s0"/><geom geom="bx"/><site site="s1"/>', "is not sphere or cylinder"),
+    ('<site site="s0"/><geom geom="g"/>', "not bracketed by sites"),
+    ('<geom geom="g"/><site site="s0"/>', "not bracketed by sites"),
+    ('<site site="s0"/><geom geom="g" sidesite="nope"/><site site="s1"/>',
+     "side site 'nope' not found")])
 def test_path_rules(path, msg):
   xml = f"""<mujoco><worldbody><body><joint/><geom name="g" size=".1"/>
+    <geom name="bx" type="box" size=".1 .1 .1"/>
     <site name="s0"/><site name="s1" pos=".1 0 0"/><site name="s2" pos="0 .1 0"/></body>
     </worldbody><tendon><spatial>{path}</spatial></tendon></mujoco>"""
   with pytest.raises(mjcf.MJCFError, match=msg):
     mjcf.load_xml_string(xml)
+
+
+# ---- wrapping around spheres and cylinders (mju_wrap, engine_util_misc.c:282-418) ----
+
+WRAP = """<mujoco><option gravity="0 0 -9.81"/>
+  <default><geom contype="0" conaffinity="0"/></default><worldbody>
+  <site name="top" pos="0 0 1.2"/>
+  <body name="base" pos="0 0 .5"><joint name="sl" type="slide" axis="0 0 1"/>
+    <geom type="box" size=".05 .05 .05"/><site name="b0" pos=".05 0 .05"/>
+    <body name="a" pos=".1 0 0"><joint name="h1" axis="0 1 0"/>
+      <geom name="ball" type="sphere" size=".06"/><site name="side_out" pos="0 0 .1"/>
+      <geom size=".03" fromto="0 0 0 .3 0 0" type="capsule"/>
+      <site name="a1" pos=".25 0 .06"/>
+      <body name="b" pos=".3 0 0"><joint name="bj" type="ball"/>
+        <geom name="cyl" type="cylinder" size=".05 .05" zaxis="0 1 0"/>
+        <site name="side_in" pos="0 0 .01"/><site name="side_cyl" pos="0 0 .2"/>
+        <geom size=".03" fromto="0 0 0 .3 0 0" type="capsule"/>
+        <site name="b1" pos=".3 0 -.04"/></body></body></body>
+  </worldbody>
+  <tendon>
+    <spatial name="sph" limited="true" range="0.1 0.5" stiffness="3" damping=".2">
+      <site site="b0"/><geom geom="ball" sidesite="side_out"/><site site="a1"/>
+      <pulley divisor="2"/><site site="a1"/><geom geom="cyl" sidesite="side_cyl"/>
+      <site site="b1"/></spatial>
+    <spatial name="inside" limited="true" range="0.2 0.3">
+      <site site="a1"/><geom geom="cyl" sidesite="side_in"/><site site="b1"/></spatial>
+    <spatial name="noside"><site site="top"/><geom geom="ball"/><site site="b1"/></spatial>
+  </tendon>
+  <actuator><motor tendon="sph" gear="2"/><motor tendon="inside"/><motor tendon="noside"/>
+  </actuator></mujoco>"""
+
+
+@pytest.fixture(scope="module")
+def wrapm():
+  return mjcf.load_xml_string(WRAP)
+
+
+def _wrap_states(m, n, seed):
+  rng = np.random.default_rng(seed)
+  out = []
+  for _ in range(n):
+    q = np.array(m.qpos0, dtype=float)
+    q[0] += 0.05 * rng.normal()
+    q[1] = rng.uniform(-0.6, 0.6)
+    q[2:6] += 0.4 * rng.normal(size=4)
+    out.append((q, rng.normal(size=m.nv), rng.normal(size=m.nv)))
+  return out
+
+
+def _straight(m, o, t):
+  """Length of tendon t with the geoms ignored (site to site, pulleys dividing)."""
+  sx = o.d.site_xpos.reshape(-1, 3)
+  adr, num = m.tendon_adr[t], m.tendon_num[t]
+  objs = [(m.wrap_type[w], m.wrap_objid[w], m.wrap_prm[w]) for w in range(adr, adr + num)
+          if m.wrap_type[w] in (2, 3)]
+  L, div = 0.0, 1.0
+  for (t0, i0, p0), (t1, i1, _) in zip(objs, objs[1:]):
+    if t0 == 2:
+      div = p0
+    if t0 == 2 or t1 == 2:
+      continue
+    L += np.linalg.norm(sx[i1] - sx[i0]) / div
+  return L
+
+
+def test_wrap_compiled(wrapm):
+  m = wrapm
+  assert list(m.wrap_type[:7]) == [3, 4, 3, 2, 3, 5, 3]
+  assert m.wrap_prm[1] == 2 and m.wrap_prm[5] == 5        # side site ids (body order)
+  assert m.wrap_prm[m.tendon_adr[2] + 1] == -1
+  assert m.moment_rownnz[0] == m.nv
+
+
+def test_wrap_known_answer():
+  """Sites on either side of a sphere with the side site above: two tangent segments and
+  the arc between the tangent points; a cylinder seen along its axis gives the same."""
+  d, r = 0.3, 0.1
+  for gtype, extra in (("sphere", ""), ("cylinder", ' size=".1 .2" zaxis="0 1 0"')):
+    size = "" if extra else ' size=".1"'
+    xml = f"""<mujoco><worldbody><body><joint type="slide"/>
+      <geom name="w" type="{gtype}"{size}{extra}/>
+      <site name="up" pos="0 0 .5"/></body>
+      <site name="l" pos="-{d} 0 0"/><site name="r" pos="{d} 0 0"/></worldbody>
+      <tendon><spatial><site site="l"/><geom geom="w" sidesite="up"/><site site="r"/>
+      </spatial></tendon></mujoco>"""
+    m = mjcf.load_xml_string(xml)
+    o = Oracle(m)
+    o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+    want = 2*np.sqrt(d*d - r*r) + r*(np.pi - 2*np.arccos(r/d))
+    assert o.d.ten_length[0] == pytest.approx(want, rel=1e-14), gtype
+    assert m.tendon_length0[0] == pytest.approx(want, rel=1e-13), gtype
+
+
+def test_wrap_cases_exercised(wrapm):
+  """Across the sampled states each tendon is sometimes wrapped (longer than its straight
+  path) and the no-wrap case also occurs."""
+  m = wrapm
+  o = Oracle(m)
+  wrapped = np.zeros(m.ntendon, int)
+  for q, v, a in _wrap_states(m, 40, 5):
+    o.inverse(q, v, a)
+    for t in range(m.ntendon):
+      wrapped[t] += o.d.ten_length[t] > _straight(m, o, t) + 1e-12
+  assert (wrapped > 0).all() and (wrapped[[0, 2]] < 40).all(), wrapped
+
+
+def test_wrap_jacobian_is_derivative(wrapm):
+  m = wrapm
+  o = Oracle(m)
+  eps = 1e-6
+  for q, v, a in _wrap_states(m, 6, 6):
+    o.inverse(q, v, a)
+    J = o.d.ten_J.reshape(m.ntendon, m.nv).copy()
+    num = np.zeros_like(J)
+    for k in range(m.nv):
+      dv = np.zeros(m.nv)
+      dv[k] = eps
+      L = []
+      for s in (1, -1):
+        qq = q.copy()
+        qq[:2] += s * dv[:2]
+        qq[2:6] = _integrate_ball(q[2:6], s * dv[2:5])
+        o.inverse(qq, v, a)
+        L.append(o.d.ten_length.copy())
+      num[:, k] = (L[0] - L[1]) / (2 * eps)
+    np.testing.assert_allclose(J, num, atol=2e-6)
+
+
+def _integrate_ball(quat, w):
+  quat = quat / np.linalg.norm(quat)
+  ang = np.linalg.norm(w)
+  if ang < 1e-15:
+    return quat
+  dq = np.concatenate([[np.cos(ang / 2)], np.sin(ang / 2) * w / ang])
+  a, b = quat, dq
+  r = np.array([a[0]*b[0] - a[1:] @ b[1:], *(a[0]*b[1:] + b[0]*a[1:] + np.cross(a[1:], b[1:]))])
+  return r / np.linalg.norm(r)
+
+
+def test_wrap_setconst(wrapm):
+  """The compiler's numpy restatement of mju_wrap (setconst.wrap) against the oracle's C
+  one: tendon_length0 and tendon_invweight0 at qpos0."""
+  m = wrapm
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  np.testing.assert_allclose(m.tendon_length0, o.d.ten_length, rtol=1e-13)
+  J = o.d.ten_J.reshape(m.ntendon, m.nv)
+  Minv = np.linalg.inv(o.fullM())
+  for t in range(m.ntendon):
+    assert m.tendon_invweight0[t] == pytest.approx(J[t] @ Minv @ J[t], rel=1e-9)
+
+
+def test_wrap_device_bitexact(wrapm):
+  m = wrapm
+  o, k = Oracle(m), KernelCPU(m)
+  nl = 0
+  for q, v, a in _wrap_states(m, 40, 7):
+    ref = o.inverse(q, v, a)
+    got, st = k.inverse(q, v, a)
+    assert st == o.d.status == 0
+    np.testing.assert_array_equal(got, ref)
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name), err_msg=f.name)
+    nl += o.d.nefc
+  assert nl > 0
