@@ -64,6 +64,12 @@ FUSE = True       # one launch running the three stage bodies back to back per w
 VA_RECOMPUTE = False
 # lanes per workgroup of each stage kernel: 64 = one instance block per wave; 32 = a block
 # split over two half-filled waves (twice the waves per SIMD, same mirror layout)
+# Experiment (round 2, off): k_all hands qM from the pos stage to the fac stage in a
+# kernel-local array the compiler promotes to registers, instead of fac re-reading it from
+# the mirror (the staged kernels pass nullptr and keep the re-read). Exact, but the 243 qM
+# values live across pos's post-order push k_all from 20 B to 1,968 B of scratch per lane
+# (tools/kernel_resources.py), and every spill reload waits for the store stream.
+QM_FORWARD = False
 LANES = {"pos": 64, "fac": 64, "va": 64}
 
 
@@ -222,6 +228,12 @@ class _Stage:
     self.store_fields = store_fields
 
   def st(self, field, k, expr):
+    if field == "qM" and QM_FORWARD:
+      self.E(f"{{ const double v_ = {expr}; if (qmr) qmr[{k}] = v_;")
+      if self.store_fields is None or field in self.store_fields:
+        self.E(f"  P_qM[{k}*64] = v_;")
+      self.E("}")
+      return
     if self.store_fields is None or field in self.store_fields:
       self.E(f"P_{field}[{k}*64] = {expr};")
 
@@ -741,7 +753,8 @@ def _gen_fac(M: _Model, store_fields=None) -> str:
   G.prologue()
   G.pointers(["qM", "qLD", "qLDiagInv"])
   for a in range(m.nM):
-    E(f"const double M_{a} = P_qM[{a}*64];")
+    E(f"const double M_{a} = qmr ? qmr[{a}] : P_qM[{a}*64];" if QM_FORWARD
+      else f"const double M_{a} = P_qM[{a}*64];")
   rownnz = [int(x) for x in m.C_rownnz]
   rowadr = [int(x) for x in m.C_rowadr]
   colind = [int(x) for x in m.C_colind]
@@ -1118,9 +1131,10 @@ _SIG = {
     "pos": ("const double* __restrict__ qpos_in, const double* __restrict__ qvel_in, "
             "const double* __restrict__ qacc_in, int* __restrict__ worklist, "
             "int* __restrict__ worklist_count, int* __restrict__ worklist_next, "
-            "int* __restrict__ efc_count, double* __restrict__ trig",
-            "qpos_in, qvel_in, qacc_in, worklist, worklist_count, worklist_next, efc_count, trig"),
-    "fac": ("int* __restrict__ efc_count", "efc_count"),
+            "int* __restrict__ efc_count, double* __restrict__ trig, double* __restrict__ qmr",
+            "qpos_in, qvel_in, qacc_in, worklist, worklist_count, worklist_next, efc_count, trig, "
+            "qmr"),
+    "fac": ("int* __restrict__ efc_count, const double* __restrict__ qmr", "efc_count, qmr"),
     "va": ("double* __restrict__ qfrc_out, int* __restrict__ status, "
            "int* __restrict__ efc_count, double* __restrict__ qo_lds, "
            "double* __restrict__ trig",
@@ -1159,6 +1173,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
     int* __restrict__ efc_count) {{
   double trig[{max(1, 2 * len(M.trig) * 64)}];   // LDS on the device (k_pos)
   double qo_lds[{64 * max(M.nv, 1)}];             // LDS on the device (k_va)
+  double qmr[{max(1, m.nM)}];                        // registers on the device (k_all)
 """ + "".join(f"  fast_{st}_{name}(mr, blk, lane, B, {_SIG[st][1]});\n" for st in STAGES)
              + (f"""  if (qfrc_out && (long)blk*64 + lane < B) {{
     for (int k = 0; k < {M.nv}; k++) qfrc_out[((long)blk*64 + lane)*{M.nv} + k] = qo_lds[lane*{M.nv} + k];
@@ -1170,6 +1185,9 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
     tail = ""
     nl = LANES[st]
     sub = 64 // nl    # workgroups per 64-instance block
+    params = params.replace(", double* __restrict__ qmr", "").replace(
+        ", const double* __restrict__ qmr", "")
+    args = args.replace(", qmr", ", nullptr")      # staged: qM goes through the mirror
     if st == "pos":
       params = params.replace(", double* __restrict__ trig", "")
       decl = f"  __shared__ double trig[{max(1, 2 * len(M.trig) * nl)}];\n"
@@ -1214,6 +1232,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
     int* __restrict__ efc_count) {{
   __shared__ double trig[{ntrig}];
   __shared__ double qo_lds[{nqo}];
+  double qmr[{max(1, m.nM)}];
 """ + "\n".join(f"  fast_{st}_{name}(mr, blockIdx.x, threadIdx.x, B, {_SIG[st][1]});\n"
                 f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE();" for st in STAGES)
              + "\n" + fuse_tail + "}")
@@ -1225,7 +1244,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
                f"qfrc_out, status, worklist, worklist_count, worklist_next, efc_count);")
   else:
     for st in STAGES:
-      args = _SIG[st][1].replace(", trig", "").replace(", qo_lds", "")
+      args = _SIG[st][1].replace(", trig", "").replace(", qo_lds", "").replace(", qmr", ", nullptr")
       gb = "g, b" if LANES[st] == 64 else f"dim3(g.x*{64 // LANES[st]}), dim3({LANES[st]})"
       out.append(f"  hipLaunchKernelGGL(k_{st}_{name}, {gb}, 0, s, mr, B, {args});")
   out.append("}")
