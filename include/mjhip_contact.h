@@ -15,8 +15,8 @@
  * when it passes the static rules below. mj_collision processes candidates in signature
  * order ((b1 << 16) + b2, b1 < b2); mjhip_pairMaxContacts bounds each primitive pair.
  *
- * A candidate pair whose collision function is not implemented here (box-box, the convex
- * pairs mjc_Convex serves, ellipsoids) adds no capacity. At run time it goes through the
+ * A candidate pair whose collision function is not implemented here (the convex pairs
+ * mjc_Convex serves, ellipsoids) adds no capacity. At run time it goes through the
  * same bitmask and bounding-sphere filters as the reference (mj_collideGeoms :1470-1497);
  * an instance where one survives them is flagged MJHIP_INST_UNSUPPORTED instead of getting
  * contacts, so every unflagged instance is exact.
@@ -98,6 +98,7 @@ MJHIP_CONTACT_HD int mjhip_pairMaxContacts(int t1, int t2) {
   if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_BOX) return 1;
   if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) return 2;
   if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_BOX) return 2;
+  if (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX) return 24;   /* mjc_BoxBox's most */
   if (t1 == mjhipGEOM_HFIELD && t2 <= mjhipGEOM_HFIELD) return 0;
   return -1;
 }

@@ -1266,12 +1266,402 @@ MJH_HD int filterSphere(const mjhipModel& m, const Lane<S>& d, int g1, int g2, d
   return 0;
 }
 
+//---------------------------------- box : box (engine_collision_box.c:607-1343) --------------
+// Every contact of mjc_BoxBox is final when it is made, so the restatement hands each one
+// to emit(RawContact) in the reference's order instead of collecting them in an array.
+MJH_HD void bbFaceFrame(int f, double rotmore[9], int idx[3], double sg[3]) {
+  for (int k = 0; k < 9; k++) rotmore[k] = 0;
+  idx[0] = 0; idx[1] = 1; idx[2] = 2;
+  sg[0] = sg[1] = sg[2] = 1;
+  switch (f) {
+  case 0: rotmore[2] = -1; rotmore[4] = 1; rotmore[6] = 1; idx[0] = 2; sg[0] = -1; idx[2] = 0; break;
+  case 1: rotmore[0] = 1; rotmore[5] = -1; rotmore[7] = 1; idx[1] = 2; sg[1] = -1; idx[2] = 1; break;
+  case 2: rotmore[0] = 1; rotmore[4] = 1; rotmore[8] = 1; break;
+  case 3: rotmore[2] = 1; rotmore[4] = 1; rotmore[6] = -1; idx[0] = 2; idx[2] = 0; sg[2] = -1; break;
+  case 4: rotmore[0] = 1; rotmore[5] = 1; rotmore[7] = -1; idx[1] = 2; idx[2] = 1; sg[2] = -1; break;
+  default: rotmore[0] = -1; rotmore[4] = 1; rotmore[8] = -1; sg[0] = -1; sg[2] = -1; break;
+  }
+}
+MJH_HD void bbMulMatTMat3(double r[9], const double a[9], const double b[9]) {
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) r[3*i+j] = a[i]*b[j] + a[3+i]*b[3+j] + a[6+i]*b[6+j];
+}
+MJH_HD void bbMulMatMatT3(double r[9], const double a[9], const double b[9]) {
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) r[3*i+j] = a[3*i]*b[3*j] + a[3*i+1]*b[3*j+1] + a[3*i+2]*b[3*j+2];
+}
+
+template <class F>
+MJH_HD void colBoxBox(double margin, const double pos1[3], const double mat1[9],
+                      const double size1[3], const double pos2[3], const double mat2[9],
+                      const double size2[3], F&& emit) {
+  double pos12[3], pos21[3], rot[9], rott[9], rotabs[9], rottabs[9], tmp1[3], tmp2[3];
+  double plen1[3], plen2[3], rotmore[9], p[3], r[9], s[3], ss[3], rt[9], sg[3];
+  double clnorm[3] = {0, 0, 0}, rnorm[3];
+  int idx[3];
+  int code = -1, cle1 = 0, cle2 = 0, in = 0;
+  const double margin2 = margin*margin;
+  sub3(tmp1, pos2, pos1);
+  mulMatTVec3(pos21, mat1, tmp1);
+  sub3(tmp1, pos1, pos2);
+  mulMatTVec3(pos12, mat2, tmp1);
+  bbMulMatTMat3(rot, mat1, mat2);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) rott[3*j+i] = rot[3*i+j];
+  for (int i = 0; i < 9; i++) rotabs[i] = fabs(rot[i]);
+  for (int i = 0; i < 9; i++) rottabs[i] = fabs(rott[i]);
+  mulMatVec3(plen2, rotabs, size2);
+  mulMatTVec3(plen1, rotabs, size1);
+  // separating axes: the six face normals
+  double penetration = margin;
+  for (int i = 0; i < 3; i++) penetration += size1[i]*3 + size2[i]*3;
+  for (int i = 0; i < 3; i++) {
+    const double c1 = -fabs(pos21[i]) + size1[i] + plen2[i];
+    const double c2 = -fabs(pos12[i]) + size2[i] + plen1[i];
+    if (c1 < -margin || c2 < -margin) return;
+    if (c1 < penetration) { penetration = c1; code = i + 3*(pos21[i] < 0); }
+    if (c2 < penetration) { penetration = c2; code = i + 3*(pos12[i] < 0) + 6; }
+  }
+  // the nine edge-edge cross products, in box 1's frame
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) {
+      tmp2[0] = tmp2[1] = tmp2[2] = 0;
+      if (i == 0) { tmp2[1] = -rott[3*j+2]; tmp2[2] = rott[3*j+1]; }
+      else if (i == 1) { tmp2[0] = rott[3*j+2]; tmp2[2] = -rott[3*j]; }
+      else { tmp2[0] = -rott[3*j+1]; tmp2[1] = rott[3*j]; }
+      const double c1 = normalize3(tmp2);
+      if (c1 < MINVAL) continue;
+      const double c2 = dot3(pos21, tmp2);
+      double c3 = 0;
+      for (int k = 0; k < 3; k++) if (k != i) c3 += size1[k]*fabs(tmp2[k]);
+      for (int k = 0; k < 3; k++) if (k != j) c3 += size2[k]*rotabs[3*i + 3 - k - j] / c1;
+      c3 -= fabs(c2);
+      if (c3 < -margin) return;
+      if (c3 < penetration*(1 - 1e-12)) {
+        penetration = c3;
+        cle1 = 0;
+        for (int k = 0; k < 3; k++) if (k != i && ((tmp2[k] > 0) ^ (c2 < 0))) cle1 += 1 << k;
+        cle2 = 0;
+        for (int k = 0; k < 3; k++) {
+          if (k != j && ((rot[3*i + 3 - k - j] > 0) ^ (c2 < 0) ^ ((k - j + 3) % 3 == 1))) {
+            cle2 += 1 << k;
+          }
+        }
+        code = 12 + 3*i + j;
+        copy3(clnorm, tmp2);
+        in = c2 < 0;
+      }
+    }
+  }
+  if (code == -1) return;
+  RawContact t;
+  for (int k = 3; k < 9; k++) t.frame[k] = 0;
+
+  if (code < 12) {
+    // ---- a face of one box against the other box
+    const int q1 = code % 6, q2 = code / 6;
+    bbFaceFrame(q1, rotmore, idx, sg);
+    if (q2) {
+      bbMulMatMatT3(r, rotmore, rot);
+      for (int k = 0; k < 3; k++) { p[k] = pos12[idx[k]]*sg[k]; tmp1[k] = size2[idx[k]]*sg[k]; }
+      copy3(s, size1);
+    } else {
+      for (int k = 0; k < 3; k++) scl3(r + 3*k, rot + 3*idx[k], sg[k]);
+      for (int k = 0; k < 3; k++) { p[k] = pos21[idx[k]]*sg[k]; tmp1[k] = size1[idx[k]]*sg[k]; }
+      copy3(s, size2);
+    }
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) rt[3*j+i] = r[3*i+j];
+    for (int i = 0; i < 3; i++) ss[i] = fabs(tmp1[i]);
+    const double lx = ss[0], ly = ss[1], hz = ss[2];
+    p[2] -= hz;
+    double pts[6][3], lines[4][6];
+    copy3(pts[0], p);
+    int clcorner = 0;
+    for (int i = 0; i < 3; i++) if (r[6+i] < 0) clcorner += 1 << i;
+    addToScl3(pts[0], rt, s[0]*((clcorner & 1) ? 1 : -1));
+    addToScl3(pts[0], rt + 3, s[1]*((clcorner & 2) ? 1 : -1));
+    addToScl3(pts[0], rt + 6, s[2]*((clcorner & 4) ? 1 : -1));
+    int m = 1;
+    for (int i = 0; i < 3; i++) {
+      if (fabs(r[6+i]) < 0.5) {
+        scl3(m == 1 ? pts[1] : pts[2], rt + 3*i, s[i]*((clcorner & (1 << i)) ? -2 : 2));
+        m++;
+      }
+    }
+    add3(pts[3], pts[0], pts[1]);
+    add3(pts[4], pts[0], pts[2]);
+    add3(pts[5], pts[3], pts[2]);
+    int k = 0;
+    if (m > 1) { copy3(lines[0], pts[0]); copy3(lines[0] + 3, pts[1]); k = 1; }
+    if (m > 2) {
+      copy3(lines[1], pts[0]); copy3(lines[1] + 3, pts[2]);
+      copy3(lines[2], pts[3]); copy3(lines[2] + 3, pts[2]);
+      copy3(lines[3], pts[4]); copy3(lines[3] + 3, pts[1]);
+      k = 4;
+    }
+    // the contact frame: box q2's face normal, mapped back to the global frame
+    double rg[9], pg[3];
+    bbMulMatMatT3(rg, q2 ? mat2 : mat1, rotmore);
+    copy3(pg, q2 ? pos2 : pos1);
+    const double f = q2 ? -1 : 1;
+    t.frame[0] = f*rg[2]; t.frame[1] = f*rg[5]; t.frame[2] = f*rg[8];
+    auto put = [&](const double pt[3]) MJH_LAMBDA_INLINE {
+      if (pt[2] > margin) return;              // the reference's depth filter
+      double q[3] = {pt[0], pt[1], pt[2]*0.5};
+      t.dist = q[2];                            // half the face depth, as the reference
+      q[2] += hz;
+      double w[3];
+      mulMatVec3(w, rg, q);
+      add3(t.pos, w, pg);
+      emit(t);
+    };
+    for (int i = 0; i < k; i++) {             // incident edges against the face's rectangle
+      for (int q = 0; q < 2; q++) {
+        const double a = lines[i][q], b = lines[i][3+q], cc = lines[i][1-q], dd = lines[i][4-q];
+        if (fabs(b) > MINVAL) {
+          for (int j = -1; j <= 1; j += 2) {
+            const double l = ss[q]*j;
+            const double c1 = (l - a)*(1/b);
+            if (c1 < 0 || c1 > 1) continue;
+            const double c2 = cc + dd*c1;
+            if (fabs(c2) > ss[1-q]) continue;
+            double pt[3];
+            copy3(pt, lines[i]);
+            addToScl3(pt, lines[i] + 3, c1);
+            put(pt);
+          }
+        }
+      }
+    }
+    const double a = pts[1][0], b = pts[2][0], cc = pts[1][1], dd = pts[2][1];
+    const double c1 = a*dd - b*cc;
+    if (m > 2) {                              // face corners inside the incident face
+      for (int i = 0; i < 4; i++) {
+        const double llx = i/2 ? lx : -lx, lly = i % 2 ? ly : -ly;
+        const double x = llx - pts[0][0], y = lly - pts[0][1];
+        const double u = (x*dd - y*b)*(1/c1), v = (y*a - x*cc)*(1/c1);
+        if (u <= 0 || v <= 0 || u >= 1 || v >= 1) continue;
+        const double pt[3] = {llx, lly, pts[0][2] + u*pts[1][2] + v*pts[2][2]};
+        put(pt);
+      }
+    }
+    for (int i = 0; i < (1 << (m - 1)); i++) {  // incident corners inside the face
+      const double* q = pts[i == 0 ? 0 : i + 2];
+      if (i && (q[0] <= -lx || q[0] >= lx)) continue;
+      if (i && (q[1] <= -ly || q[1] >= ly)) continue;
+      put(q);
+    }
+    return;
+  }
+
+  // ---- edge against edge
+  code -= 12;
+  const int q1 = code / 3, q2 = code % 3;
+  int ax1 = q2 == 0 ? 1 : (q2 == 1 ? 0 : 1), ax2 = q2 == 2 ? 0 : 2;
+  int pax1 = q1 == 0 ? 1 : (q1 == 1 ? 0 : 1), pax2 = q1 == 2 ? 0 : 2;
+  if (rotabs[3*q1 + ax1] < rotabs[3*q1 + ax2]) { ax1 = ax2; ax2 = 3 - q2 - ax1; }
+  if (rottabs[3*q2 + pax1] < rottabs[3*q2 + pax2]) { pax1 = pax2; pax2 = 3 - q1 - pax1; }
+  const int clface = (cle1 & (1 << pax2)) ? pax2 : pax2 + 3;
+  bbFaceFrame(clface, rotmore, idx, sg);
+  for (int k = 0; k < 3; k++) { p[k] = pos21[idx[k]]*sg[k]; rnorm[k] = clnorm[idx[k]]*sg[k]; }
+  for (int k = 0; k < 3; k++) scl3(r + 3*k, rot + 3*idx[k], sg[k]);
+  mulMatTVec3(tmp1, rotmore, size1);
+  for (int i = 0; i < 3; i++) s[i] = fabs(tmp1[i]);
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) rt[3*j+i] = r[3*i+j];
+  const double lx = s[0], ly = s[1], hz = s[2];
+  p[2] -= hz;
+  double pu[4][3], ppts2[4][2], axi[3][3], pts[3][3], lines[4][6], linesu[4][6];
+  for (int e = 0; e < 2; e++) {            // the incident edge's end points, and the parallel edge's
+    double* p0 = pu[2*e];
+    copy3(p0, p);
+    addToScl3(p0, rt + 3*ax1, size2[ax1]*(((cle2 & (1 << ax1)) ? 1 : -1)*(e ? -1 : 1)));
+    addToScl3(p0, rt + 3*ax2, size2[ax2]*((cle2 & (1 << ax2)) ? 1 : -1));
+    copy3(pu[2*e + 1], p0);
+    addToScl3(p0, rt + 3*q2, size2[q2]);
+    addToScl3(pu[2*e + 1], rt + 3*q2, -size2[q2]);
+  }
+  copy3(axi[0], pu[0]);
+  sub3(axi[1], pu[1], pu[0]);
+  sub3(axi[2], pu[2], pu[0]);
+  if (fabs(rnorm[2]) < MINVAL) return;
+  const double innorm = (1/rnorm[2])*(in ? -1 : 1);
+  double proj[4][3];
+  for (int i = 0; i < 4; i++) {            // project onto the reference face along the normal
+    const double c1 = -pu[i][2]*(1/rnorm[2]);
+    copy3(proj[i], pu[i]);
+    addToScl3(proj[i], rnorm, c1);
+    ppts2[i][0] = proj[i][0];
+    ppts2[i][1] = proj[i][1];
+  }
+  copy3(pts[0], proj[0]);
+  sub3(pts[1], proj[1], proj[0]);
+  sub3(pts[2], proj[2], proj[0]);
+  copy3(lines[0], pts[0]); copy3(lines[0] + 3, pts[1]);
+  copy3(linesu[0], axi[0]); copy3(linesu[0] + 3, axi[1]);
+  copy3(lines[1], pts[0]); copy3(lines[1] + 3, pts[2]);
+  copy3(linesu[1], axi[0]); copy3(linesu[1] + 3, axi[2]);
+  add3(lines[2], pts[0], pts[1]); copy3(lines[2] + 3, pts[2]);
+  add3(linesu[2], axi[0], axi[1]); copy3(linesu[2] + 3, axi[2]);
+  add3(lines[3], pts[0], pts[2]); copy3(lines[3] + 3, pts[1]);
+  add3(linesu[3], axi[0], axi[2]); copy3(linesu[3] + 3, axi[1]);
+  double rg[9];
+  bbMulMatMatT3(rg, mat1, rotmore);
+  mulMatVec3(tmp1, rg, rnorm);
+  scl3(t.frame, tmp1, in ? -1 : 1);
+  auto put = [&](double pt[3], double depth) MJH_LAMBDA_INLINE {
+    t.dist = depth;
+    pt[2] += hz;
+    double w[3];
+    mulMatVec3(w, rg, pt);
+    add3(t.pos, w, pos1);
+    emit(t);
+  };
+  int n = 0;
+  for (int i = 0; i < 4; i++) {            // quadrilateral edges against the face rectangle
+    for (int q = 0; q < 2; q++) {
+      const double a = lines[i][q], b = lines[i][3+q], cc = lines[i][1-q], dd = lines[i][4-q];
+      if (fabs(b) > MINVAL) {
+        for (int j = -1; j <= 1; j += 2) {
+          const double l = s[q]*j;
+          const double c1 = (l - a)*(1/b);
+          if (c1 < 0 || c1 > 1) continue;
+          const double c2 = cc + dd*c1;
+          if (fabs(c2) > s[1-q]) continue;
+          if ((linesu[i][2] + linesu[i][5]*c1)*innorm > margin) continue;
+          double pt[3];
+          scl3(pt, linesu[i], 0.5);
+          addToScl3(pt, linesu[i] + 3, 0.5*c1);
+          pt[q] += 0.5*l;
+          pt[1-q] += 0.5*c2;
+          put(pt, pt[2]*innorm*2);
+          n++;
+        }
+      }
+    }
+  }
+  const int nl = n;
+  const double a = pts[1][0], b = pts[2][0], cc = pts[1][1], dd = pts[2][1];
+  double c1 = a*dd - b*cc;
+  for (int i = 0; i < 4; i++) {            // face corners against the quadrilateral
+    const double llx = i/2 ? lx : -lx, lly = i % 2 ? ly : -ly;
+    const double x = llx - pts[0][0], y = lly - pts[0][1];
+    double u = (x*dd - y*b)*(1/c1), v = (y*a - x*cc)*(1/c1);
+    if (nl == 0) {
+      if ((u < 0 || u > 1) && (v < 0 || v > 1)) continue;
+    } else if (u < 0 || u > 1 || v < 0 || v > 1) {
+      continue;
+    }
+    u = u < 0 ? 0 : (u > 1 ? 1 : u);
+    v = v < 0 ? 0 : (v > 1 ? 1 : v);
+    scl3(tmp1, pu[0], 1 - u - v);
+    addToScl3(tmp1, pu[1], u);
+    addToScl3(tmp1, pu[2], v);
+    double pt[3] = {llx, lly, 0};
+    sub3(tmp2, pt, tmp1);
+    c1 = dot3(tmp2, tmp2);                   // the reference reuses c1 for later corners
+    if (tmp1[2] > 0 && c1 > margin2) continue;
+    add3(pt, pt, tmp1);
+    scl3(pt, pt, 0.5);
+    put(pt, sqrt(c1)*(tmp1[2] < 0 ? -1 : 1));
+    n++;
+  }
+  const int nf = n;
+  for (int i = 0; i < 4; i++) {            // quadrilateral corners over the face
+    const double x = ppts2[i][0], y = ppts2[i][1];
+    if (nl == 0) {
+      if (nf != 0 && (x < -lx || x > lx) && (y < -ly || y > ly)) continue;
+    } else if (x < -lx || x > lx || y < -ly || y > ly) {
+      continue;
+    }
+    double d2 = 0;
+    for (int j = 0; j < 2; j++) {
+      if (ppts2[i][j] < -s[j]) d2 += (ppts2[i][j] + s[j])*(ppts2[i][j] + s[j]);
+      else if (ppts2[i][j] > s[j]) d2 += (ppts2[i][j] - s[j])*(ppts2[i][j] - s[j]);
+    }
+    d2 += pu[i][2]*innorm*pu[i][2]*innorm;
+    if (pu[i][2] > 0 && d2 > margin2) continue;
+    double pt[3] = {ppts2[i][0]*0.5, ppts2[i][1]*0.5, 0};
+    for (int j = 0; j < 2; j++) {
+      if (ppts2[i][j] < -s[j]) pt[j] = -s[j]*0.5;
+      else if (ppts2[i][j] > s[j]) pt[j] = s[j]*0.5;
+    }
+    addToScl3(pt, pu[i], 0.5);
+    put(pt, sqrt(d2)*(pu[i][2] < 0 ? -1 : 1));
+  }
+}
+
+// mju_outsideBox (engine_util_misc.c:911-950): 1 outside the inflated box, -1 inside the
+// deflated one, 0 between
+MJH_HD int outsideBox(const double point[3], const double pos[3], const double mat[9],
+                      const double size[3], double inflate) {
+  double vec[3] = {point[0]-pos[0], point[1]-pos[1], point[2]-pos[2]}, v[3];
+  mulMatTVec3(v, mat, vec);
+  if (v[0] > size[0]*inflate || v[0] < -(size[0]*inflate) || v[1] > size[1]*inflate ||
+      v[1] < -(size[1]*inflate) || v[2] > size[2]*inflate || v[2] < -(size[2]*inflate)) {
+    return 1;
+  }
+  const double s0 = size[0]/inflate, s1 = size[1]/inflate, s2 = size[2]/inflate;
+  if (v[0] < s0 && v[0] > -s0 && v[1] < s1 && v[1] > -s1 && v[2] < s2 && v[2] > -s2) return -1;
+  return 0;
+}
+
+// box : box with mj_collideGeoms' clean-up (engine_collision_driver.c:1522-1588): contacts
+// outside one box (by 1%) and not inside the other, and earlier copies of a repeated position,
+// are dropped. Pass 1 writes each raw contact's position to buf (3 doubles each, at most 24)
+// and returns the mask of survivors; pass 2 (boxBoxEmit) regenerates the contacts, which are
+// bit-identical, and hands the survivors to store in order.
+template <class B>
+MJH_HD unsigned boxBoxKeep(double margin, const double pos1[3], const double mat1[9],
+                           const double size1[3], const double pos2[3], const double mat2[9],
+                           const double size2[3], B buf) {
+  const double sz1[3] = {size1[0] + margin, size1[1] + margin, size1[2] + margin};
+  const double sz2[3] = {size2[0] + margin, size2[1] + margin, size2[2] + margin};
+  unsigned good = 0;
+  int num = 0;
+  colBoxBox(margin, pos1, mat1, size1, pos2, mat2, size2,
+            [&](const RawContact& t) MJH_LAMBDA_INLINE {
+    const int o1 = outsideBox(t.pos, pos1, mat1, sz1, 1.01);
+    const int o2 = outsideBox(t.pos, pos2, mat2, sz2, 1.01);
+    if (!((o1 == 1 && o2 != -1) || (o2 == 1 && o1 != -1))) good |= 1u << num;
+    for (int k = 0; k < 3; k++) buf[3*num + k] = t.pos[k];
+    num++;
+  });
+  unsigned keep = good;
+  for (int i = 0; i < num - 1; i++) {
+    if (!(good >> i & 1)) continue;
+    for (int j = i + 1; j < num; j++) {
+      if (!(good >> j & 1)) continue;
+      if (buf[3*i] == buf[3*j] && buf[3*i+1] == buf[3*j+1] && buf[3*i+2] == buf[3*j+2]) {
+        keep &= ~(1u << i);
+        break;
+      }
+    }
+  }
+  return keep;
+}
+
+template <class F>
+MJH_HD void boxBoxEmit(double margin, const double pos1[3], const double mat1[9],
+                       const double size1[3], const double pos2[3], const double mat2[9],
+                       const double size2[3], unsigned keep, F&& store) {
+  int num = 0;
+  colBoxBox(margin, pos1, mat1, size1, pos2, mat2, size2,
+            [&](const RawContact& t) MJH_LAMBDA_INLINE {
+    if (keep >> num & 1) store(t);
+    num++;
+  });
+}
+
 // mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
 // WRITE = false only counts the contacts the pair produces (the cooperative constraint
 // kernel's first pass: it needs each pair's count to place the contacts in order)
+// bbuf: per-lane room for box-box positions (24 x 3 doubles), or nullptr to use the
+// contact list's free tail at ncon (the capacity holds 24 contacts for every box pair)
 template <int S, bool WRITE = true>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
-                               double margin, int& ncon, int* status);
+                               double margin, int& ncon, int* status, double* bbuf = nullptr);
 
 // mj_collideGeoms up to the narrowphase: type-orders (g1, g2), applies the static and
 // bounding-sphere filters and returns the raw contacts of a primitive pair in raw (<= 2,
@@ -1297,6 +1687,7 @@ MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
     return 0;
   }
   if (t1 == mjhipGEOM_PLANE && (t2 == mjhipGEOM_BOX || t2 == mjhipGEOM_CYLINDER)) return -1;
+  if (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX) return -1;
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
   SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
   const double *size1 = m.geom_size + 3*g1, *size2 = m.geom_size + 3*g2;
@@ -1383,10 +1774,11 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
   setContacts(m, d, g1, g2, margin, raw, num, ncon, status);
 }
 
-// plane : box / cylinder (up to 4 contacts each): contacts are stored as they are made
+// plane : box / cylinder (up to 4 contacts each) and box : box (up to 24): contacts are
+// stored as they are made
 template <int S, bool WRITE>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
-                               double margin, int& ncon, int* status) {
+                               double margin, int& ncon, int* status, double* bbuf) {
   const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
   SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
@@ -1428,8 +1820,27 @@ MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, in
     ncon = i + 1;
     return true;
   };
-  if (m.geom_type[g2] == mjhipGEOM_BOX) colPlaneBox(margin, pos1, mat1, pos2, mat2, size2, store);
-  else colPlaneCylinder(margin, pos1, mat1, pos2, mat2, size2, store);
+  if (m.geom_type[g1] == mjhipGEOM_BOX) {
+    double p1[3], m1[9], p2[3], m2[9];
+    for (int k = 0; k < 3; k++) { p1[k] = pos1[k]; p2[k] = pos2[k]; }
+    for (int k = 0; k < 9; k++) { m1[k] = mat1[k]; m2[k] = mat2[k]; }
+    const double* size1 = m.geom_size + 3*g1;
+    unsigned keep;
+    if (bbuf) {
+      keep = boxBoxKeep(margin, p1, m1, size1, p2, m2, size2, bbuf);
+    } else {
+      if (ncon + 24 > d.con_cap) {          // cannot happen: 24 per box pair is in the capacity
+        *status |= MJHIP_INST_CNSTRFULL;
+        return;
+      }
+      keep = boxBoxKeep(margin, p1, m1, size1, p2, m2, size2, d.con_pos + 3*ncon);
+    }
+    boxBoxEmit(margin, p1, m1, size1, p2, m2, size2, keep, store);
+  } else if (m.geom_type[g2] == mjhipGEOM_BOX) {
+    colPlaneBox(margin, pos1, mat1, pos2, mat2, size2, store);
+  } else {
+    colPlaneCylinder(margin, pos1, mat1, pos2, mat2, size2, store);
+  }
 }
 
 // contactcompare (engine_collision_driver.c:223-257) on two contacts' geom ids

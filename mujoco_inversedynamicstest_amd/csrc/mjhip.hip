@@ -148,9 +148,11 @@ static unsigned coopGrid(int B, int G, bool list) {
 }
 
 // dynamic LDS of k_constraint_coop: per instance 8 nv doubles (cdof, qvel, qacc), qpos and
-// efc_cap row forces
-static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap) {
-  return (unsigned)((64 / G) * (8*m.nv + m.nq + efc_cap) * sizeof(double));
+// efc_cap row forces; with box-box pairs, 72 doubles per lane for their contact positions
+constexpr int kBoxBoxBuf = 72;
+static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap, bool boxpair) {
+  return (unsigned)(((64 / G) * (8*m.nv + m.nq + efc_cap) + (boxpair ? 64*kBoxBoxBuf : 0)) *
+                    sizeof(double));
 }
 
 template <int G, bool CONTACT, bool LIST>
@@ -185,6 +187,8 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   double* cdq = g_gstage + (long)slot*per;
   double* qp = cdq + 8*nv;
   double* fst = g_gstage + (long)IPB*per + (long)slot*d.efc_cap;
+  // box-box contact positions of this lane's pair (only models with box pairs get the room)
+  double* bbuf = g_gstage + (long)IPB*(per + d.efc_cap) + (long)threadIdx.x*kBoxBoxBuf;
   if (active) {
     for (int e = sub; e < 8*nv; e += G) {
       const int j = e >> 3, c = e & 7;
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         g2 = pr.y;
         num = mjh::narrowGeoms<64>(m, d, g1, g2, margin, raw, &st);
         if (num < 0) {                      // plane : box / cylinder counts, then stores
-          mjh::collidePlaneBoxCyl<64, false>(m, d, g1, g2, margin, cnt, &st);
+          mjh::collidePlaneBoxCyl<64, false>(m, d, g1, g2, margin, cnt, &st, bbuf);
         } else {
           cnt = num;
         }
@@ -218,7 +222,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       if (cnt) {
         int c = ncon + excl;
         if (num < 0) {
-          mjh::collidePlaneBoxCyl<64, true>(m, d, g1, g2, margin, c, &st);
+          mjh::collidePlaneBoxCyl<64, true>(m, d, g1, g2, margin, c, &st, bbuf);
         } else {
           mjh::setContacts<64>(m, d, g1, g2, margin, raw, num, c, &st);
         }
@@ -658,6 +662,7 @@ struct mjhipContext_ {
   int wl_last = 0;                         // counter the last fast launch used
   int2* pairs = nullptr;                   // static geom-pair program (collisionPairs)
   int npair = 0;
+  bool boxpair = false;                    // a box-box pair is in the program (coop LDS)
   int coop = 16;                           // lanes per instance of k_constraint_coop (0: off)
   // a straight-line kernel specialized for this model at run time (mjhip_contextLoadKernel):
   // a gfx950 code object holding extern "C" k_all_<name>; rt.launch stays null
@@ -968,6 +973,9 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   if (c->con_cap > 0) {
     std::vector<int2> pairs = collision_pairs(m);
     c->npair = (int)pairs.size();
+    for (const int2& pr : pairs) {
+      c->boxpair |= m->geom_type[pr.x] == mjhipGEOM_BOX && m->geom_type[pr.y] == mjhipGEOM_BOX;
+    }
     if (c->npair) {
       if (hipMalloc((void**)&c->pairs, sizeof(int2) * pairs.size()) != hipSuccess ||
           hipMemcpy(c->pairs, pairs.data(), sizeof(int2) * pairs.size(),
@@ -1094,7 +1102,8 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
       const bool contact = c->con_cap > 0, list = c->fast->cmode == 1;
 #define MJHIP_LAUNCH_COOP(G, C, L)                                                            \
       hipLaunchKernelGGL((k_constraint_coop<G, C, L>), dim3(coopGrid(B, G, L)),               \
-                         dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap), c->stream,         \
+                         dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap, c->boxpair),        \
+                         c->stream,                                                           \
                          c->dmodel, c->mirror, B, wl,                                         \
                          (const int*)cnt, c->pairs, c->npair, qfrc, status)
       if (c->coop == 8) {

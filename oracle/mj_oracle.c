@@ -2075,10 +2075,418 @@ static int or_hasPlane(const mjhipModel* m, int b) {
   return 0;
 }
 
+/* ---- mjc_BoxBox (engine_collision_box.c:607-1343) ---- */
+static void bb_mulMatTMat3(mjtNum r[9], const mjtNum a[9], const mjtNum b[9]) {
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) r[3*i+j] = a[i]*b[j] + a[3+i]*b[3+j] + a[6+i]*b[6+j];
+}
+static void bb_mulMatMatT3(mjtNum r[9], const mjtNum a[9], const mjtNum b[9]) {
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) r[3*i+j] = a[3*i]*b[3*j] + a[3*i+1]*b[3*j+1] + a[3*i+2]*b[3*j+2];
+}
+static void bb_transpose3(mjtNum r[9], const mjtNum a[9]) {
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) r[3*j+i] = a[3*i+j];
+}
+
+/* the axis permutation and signs that turn face `f` (0-2: -x,-y,-z side... as the reference
+ * numbers them, 3-5 the opposite) into +z: rotmore and its (index, sign) form */
+static void bb_faceFrame(int f, mjtNum rotmore[9], int idx[3], mjtNum sgn[3]) {
+  mju_zero(rotmore, 9);
+  idx[0] = 0; idx[1] = 1; idx[2] = 2;
+  sgn[0] = sgn[1] = sgn[2] = 1;
+  switch (f) {
+  case 0: rotmore[2] = -1; rotmore[4] = 1; rotmore[6] = 1; idx[0] = 2; sgn[0] = -1; idx[2] = 0; break;
+  case 1: rotmore[0] = 1; rotmore[5] = -1; rotmore[7] = 1; idx[1] = 2; sgn[1] = -1; idx[2] = 1; break;
+  case 2: rotmore[0] = 1; rotmore[4] = 1; rotmore[8] = 1; break;
+  case 3: rotmore[2] = 1; rotmore[4] = 1; rotmore[6] = -1; idx[0] = 2; idx[2] = 0; sgn[2] = -1; break;
+  case 4: rotmore[0] = 1; rotmore[5] = 1; rotmore[7] = -1; idx[1] = 2; idx[2] = 1; sgn[2] = -1; break;
+  default: rotmore[0] = -1; rotmore[4] = 1; rotmore[8] = -1; sgn[0] = -1; sgn[2] = -1; break;
+  }
+}
+
+/* Separating-axis test over the 6 face normals and 9 edge-edge cross products, then contact
+ * points either by clipping the incident box's face/edges against the reference face
+ * (face code < 12) or by clipping the two closest edges' quadrilateral (edge-edge). Raw
+ * contacts in c (at most 24), normal in frame[0:3]; returns the count. */
+static int col_boxBox(orRaw* c, mjtNum margin, const mjtNum* pos1, const mjtNum* mat1,
+                      const mjtNum* size1, const mjtNum* pos2, const mjtNum* mat2,
+                      const mjtNum* size2) {
+  mjtNum pos12[3], pos21[3], rot[9], rott[9], rotabs[9], rottabs[9], tmp1[3], tmp2[3];
+  mjtNum plen1[3], plen2[3], rotmore[9], p[3], r[9], s[3], ss[3], lp[3], rt[9];
+  mjtNum points[24][3], depth[24], pts[6][3], ppts2[4][2], pu[4][3], axi[3][3];
+  mjtNum linesu[4][6], lines[4][6], clnorm[3] = {0, 0, 0}, rnorm[3], sg[3];
+  int idx[3];
+  int code = -1, cle1 = 0, cle2 = 0, in = 0, n = 0;
+  const mjtNum margin2 = margin*margin;
+
+  mju_sub3(tmp1, pos2, pos1);
+  mju_mulMatTVec3(pos21, mat1, tmp1);
+  mju_sub3(tmp1, pos1, pos2);
+  mju_mulMatTVec3(pos12, mat2, tmp1);
+  bb_mulMatTMat3(rot, mat1, mat2);
+  bb_transpose3(rott, rot);
+  for (int i = 0; i < 9; i++) rotabs[i] = fabs(rot[i]);
+  for (int i = 0; i < 9; i++) rottabs[i] = fabs(rott[i]);
+  mju_mulMatVec3(plen2, rotabs, size2);
+  mju_mulMatTVec3(plen1, rotabs, size1);
+
+  /* face axes */
+  mjtNum penetration = margin;
+  for (int i = 0; i < 3; i++) penetration += size1[i]*3 + size2[i]*3;
+  for (int i = 0; i < 3; i++) {
+    mjtNum c1 = -fabs(pos21[i]) + size1[i] + plen2[i];
+    mjtNum c2 = -fabs(pos12[i]) + size2[i] + plen1[i];
+    if (c1 < -margin || c2 < -margin) return 0;
+    if (c1 < penetration) { penetration = c1; code = i + 3*(pos21[i] < 0); }
+    if (c2 < penetration) { penetration = c2; code = i + 3*(pos12[i] < 0) + 6; }
+  }
+  /* edge-edge axes: cross(e1_i, e2_j) in box 1's frame */
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) {
+      mju_zero3(tmp2);
+      if (i == 0) { tmp2[1] = -rott[3*j+2]; tmp2[2] = rott[3*j+1]; }
+      else if (i == 1) { tmp2[0] = rott[3*j+2]; tmp2[2] = -rott[3*j]; }
+      else { tmp2[0] = -rott[3*j+1]; tmp2[1] = rott[3*j]; }
+      mjtNum c1 = mju_normalize3(tmp2);
+      if (c1 < mjMINVAL) continue;
+      mjtNum c2 = mju_dot3(pos21, tmp2);
+      mjtNum c3 = 0;
+      for (int k = 0; k < 3; k++) if (k != i) c3 += size1[k]*fabs(tmp2[k]);
+      for (int k = 0; k < 3; k++) if (k != j) c3 += size2[k]*rotabs[3*i + 3 - k - j] / c1;
+      c3 -= fabs(c2);
+      if (c3 < -margin) return 0;
+      if (c3 < penetration*(1 - 1e-12)) {
+        penetration = c3;
+        cle1 = 0;
+        for (int k = 0; k < 3; k++) if (k != i && ((tmp2[k] > 0) ^ (c2 < 0))) cle1 += 1 << k;
+        cle2 = 0;
+        for (int k = 0; k < 3; k++) {
+          if (k != j && ((rot[3*i + 3 - k - j] > 0) ^ (c2 < 0) ^ ((k - j + 3) % 3 == 1))) {
+            cle2 += 1 << k;
+          }
+        }
+        code = 12 + 3*i + j;
+        mju_copy3(clnorm, tmp2);
+        in = c2 < 0;
+      }
+    }
+  }
+  if (code == -1) return 0;
+
+  if (code < 12) {
+    /* ---- face of one box against the other box */
+    const int q1 = code % 6, q2 = code / 6;
+    bb_faceFrame(q1, rotmore, idx, sg);
+    if (q2) {
+      bb_mulMatMatT3(r, rotmore, rot);
+      for (int k = 0; k < 3; k++) { p[k] = pos12[idx[k]]*sg[k]; tmp1[k] = size2[idx[k]]*sg[k]; }
+      mju_copy3(s, size1);
+    } else {
+      for (int k = 0; k < 3; k++) mju_scl3(r + 3*k, rot + 3*idx[k], sg[k]);
+      for (int k = 0; k < 3; k++) { p[k] = pos21[idx[k]]*sg[k]; tmp1[k] = size1[idx[k]]*sg[k]; }
+      mju_copy3(s, size2);
+    }
+    bb_transpose3(rt, r);
+    for (int i = 0; i < 3; i++) ss[i] = fabs(tmp1[i]);
+    const mjtNum lx = ss[0], ly = ss[1], hz = ss[2];
+    p[2] -= hz;
+    mju_copy3(lp, p);
+    int clcorner = 0;
+    for (int i = 0; i < 3; i++) if (r[6+i] < 0) clcorner += 1 << i;
+    mju_addToScl3(lp, rt, s[0]*((clcorner & 1) ? 1 : -1));
+    mju_addToScl3(lp, rt + 3, s[1]*((clcorner & 2) ? 1 : -1));
+    mju_addToScl3(lp, rt + 6, s[2]*((clcorner & 4) ? 1 : -1));
+    int m = 0, k = 0;
+    mju_copy3(pts[m++], lp);
+    for (int i = 0; i < 3; i++) {
+      if (fabs(r[6+i]) < 0.5) mju_scl3(pts[m++], rt + 3*i, s[i]*((clcorner & (1 << i)) ? -2 : 2));
+    }
+    mju_add3(pts[3], pts[0], pts[1]);
+    mju_add3(pts[4], pts[0], pts[2]);
+    mju_add3(pts[5], pts[3], pts[2]);
+    if (m > 1) { mju_copy3(lines[k], pts[0]); mju_copy3(lines[k++] + 3, pts[1]); }
+    if (m > 2) {
+      mju_copy3(lines[k], pts[0]); mju_copy3(lines[k++] + 3, pts[2]);
+      mju_copy3(lines[k], pts[3]); mju_copy3(lines[k++] + 3, pts[2]);
+      mju_copy3(lines[k], pts[4]); mju_copy3(lines[k++] + 3, pts[1]);
+    }
+    for (int i = 0; i < k; i++) {        /* incident edges against the face's rectangle */
+      for (int q = 0; q < 2; q++) {
+        mjtNum a = lines[i][q], b = lines[i][3+q], cc = lines[i][1-q], dd = lines[i][4-q];
+        if (fabs(b) > mjMINVAL) {
+          for (int j = -1; j <= 1; j += 2) {
+            mjtNum l = ss[q]*j;
+            mjtNum c1 = (l - a)*(1/b);
+            if (c1 < 0 || c1 > 1) continue;
+            mjtNum c2 = cc + dd*c1;
+            if (fabs(c2) > ss[1-q]) continue;
+            mju_copy3(points[n], lines[i]);
+            mju_addToScl3(points[n++], lines[i] + 3, c1);
+          }
+        }
+      }
+    }
+    mjtNum a = pts[1][0], b = pts[2][0], cc = pts[1][1], dd = pts[2][1];
+    mjtNum c1 = a*dd - b*cc;
+    if (m > 2) {                         /* face corners inside the incident face */
+      for (int i = 0; i < 4; i++) {
+        mjtNum llx = i/2 ? lx : -lx, lly = i % 2 ? ly : -ly;
+        mjtNum x = llx - pts[0][0], y = lly - pts[0][1];
+        mjtNum u = (x*dd - y*b)*(1/c1), v = (y*a - x*cc)*(1/c1);
+        if (u <= 0 || v <= 0 || u >= 1 || v >= 1) continue;
+        points[n][0] = llx;
+        points[n][1] = lly;
+        points[n][2] = pts[0][2] + u*pts[1][2] + v*pts[2][2];
+        n++;
+      }
+    }
+    for (int i = 0; i < (1 << (m - 1)); i++) {   /* incident corners inside the face */
+      mju_copy3(tmp1, pts[i == 0 ? 0 : i + 2]);
+      if (i && (tmp1[0] <= -lx || tmp1[0] >= lx)) continue;
+      if (i && (tmp1[1] <= -ly || tmp1[1] >= ly)) continue;
+      mju_copy3(points[n++], tmp1);
+    }
+    m = n;
+    n = 0;
+    for (int i = 0; i < m; i++) {
+      if (points[i][2] > margin) continue;
+      mju_copy3(points[n], points[i]);
+      depth[n] = points[n][2];
+      points[n][2] *= 0.5;
+      n++;
+    }
+    bb_mulMatMatT3(r, q2 ? mat2 : mat1, rotmore);
+    mju_copy3(p, q2 ? pos2 : pos1);
+    const mjtNum f = q2 ? -1 : 1;
+    tmp2[0] = f*r[2]; tmp2[1] = f*r[5]; tmp2[2] = f*r[8];
+    for (int i = 0; i < n; i++) {
+      c[i].dist = points[i][2];            /* the reference reports half the face depth */
+      points[i][2] += hz;
+      mju_mulMatVec3(tmp1, r, points[i]);
+      mju_add3(c[i].pos, tmp1, p);
+      mju_copy3(c[i].frame, tmp2);
+      mju_zero(c[i].frame + 3, 6);
+    }
+    (void)depth;
+    return n;
+  }
+
+  /* ---- edge against edge */
+  code -= 12;
+  const int q1 = code / 3, q2 = code % 3;
+  int ax1 = q2 == 0 ? 1 : (q2 == 1 ? 0 : 1), ax2 = q2 == 2 ? 0 : 2;
+  int pax1 = q1 == 0 ? 1 : (q1 == 1 ? 0 : 1), pax2 = q1 == 2 ? 0 : 2;
+  if (rotabs[3*q1 + ax1] < rotabs[3*q1 + ax2]) { ax1 = ax2; ax2 = 3 - q2 - ax1; }
+  if (rottabs[3*q2 + pax1] < rottabs[3*q2 + pax2]) { pax1 = pax2; pax2 = 3 - q1 - pax1; }
+  const int clface = (cle1 & (1 << pax2)) ? pax2 : pax2 + 3;
+  bb_faceFrame(clface, rotmore, idx, sg);
+  for (int k = 0; k < 3; k++) { p[k] = pos21[idx[k]]*sg[k]; rnorm[k] = clnorm[idx[k]]*sg[k]; }
+  for (int k = 0; k < 3; k++) mju_scl3(r + 3*k, rot + 3*idx[k], sg[k]);
+  mju_mulMatTVec3(tmp1, rotmore, size1);
+  for (int i = 0; i < 3; i++) s[i] = fabs(tmp1[i]);
+  bb_transpose3(rt, r);
+  const mjtNum lx = s[0], ly = s[1], hz = s[2];
+  p[2] -= hz;
+  /* the incident edge's two end points, and the parallel edge's */
+  for (int e = 0; e < 2; e++) {
+    mjtNum* p0 = points[2*e];
+    mju_copy3(p0, p);
+    mju_addToScl3(p0, rt + 3*ax1, size2[ax1]*(((cle2 & (1 << ax1)) ? 1 : -1)*(e ? -1 : 1)));
+    mju_addToScl3(p0, rt + 3*ax2, size2[ax2]*((cle2 & (1 << ax2)) ? 1 : -1));
+    mju_copy3(points[2*e + 1], p0);
+    mju_addToScl3(p0, rt + 3*q2, size2[q2]);
+    mju_addToScl3(points[2*e + 1], rt + 3*q2, -size2[q2]);
+  }
+  mju_copy3(axi[0], points[0]);
+  mju_sub3(axi[1], points[1], points[0]);
+  mju_sub3(axi[2], points[2], points[0]);
+  if (fabs(rnorm[2]) < mjMINVAL) return 0;
+  const mjtNum innorm = (1/rnorm[2])*(in ? -1 : 1);
+  for (int i = 0; i < 4; i++) {          /* project onto the reference face along the normal */
+    mjtNum c1 = -points[i][2]*(1/rnorm[2]);
+    mju_copy3(pu[i], points[i]);
+    mju_addToScl3(points[i], rnorm, c1);
+    ppts2[i][0] = points[i][0];
+    ppts2[i][1] = points[i][1];
+  }
+  mju_copy3(pts[0], points[0]);
+  mju_sub3(pts[1], points[1], points[0]);
+  mju_sub3(pts[2], points[2], points[0]);
+  int k = 0;
+  mju_copy3(lines[k], pts[0]); mju_copy3(lines[k] + 3, pts[1]);
+  mju_copy3(linesu[k], axi[0]); mju_copy3(linesu[k++] + 3, axi[1]);
+  mju_copy3(lines[k], pts[0]); mju_copy3(lines[k] + 3, pts[2]);
+  mju_copy3(linesu[k], axi[0]); mju_copy3(linesu[k++] + 3, axi[2]);
+  mju_add3(lines[k], pts[0], pts[1]); mju_copy3(lines[k] + 3, pts[2]);
+  mju_add3(linesu[k], axi[0], axi[1]); mju_copy3(linesu[k++] + 3, axi[2]);
+  mju_add3(lines[k], pts[0], pts[2]); mju_copy3(lines[k] + 3, pts[1]);
+  mju_add3(linesu[k], axi[0], axi[2]); mju_copy3(linesu[k++] + 3, axi[1]);
+  n = 0;
+  for (int i = 0; i < k; i++) {          /* quadrilateral edges against the face rectangle */
+    for (int q = 0; q < 2; q++) {
+      mjtNum a = lines[i][q], b = lines[i][3+q], cc = lines[i][1-q], dd = lines[i][4-q];
+      if (fabs(b) > mjMINVAL) {
+        for (int j = -1; j <= 1; j += 2) {
+          mjtNum l = s[q]*j;
+          mjtNum c1 = (l - a)*(1/b);
+          if (c1 < 0 || c1 > 1) continue;
+          mjtNum c2 = cc + dd*c1;
+          if (fabs(c2) > s[1-q]) continue;
+          if ((linesu[i][2] + linesu[i][5]*c1)*innorm > margin) continue;
+          mju_scl3(points[n], linesu[i], 0.5);
+          mju_addToScl3(points[n], linesu[i] + 3, 0.5*c1);
+          points[n][q] += 0.5*l;
+          points[n][1-q] += 0.5*c2;
+          depth[n] = points[n][2]*innorm*2;
+          n++;
+        }
+      }
+    }
+  }
+  const int nl = n;
+  mjtNum a = pts[1][0], b = pts[2][0], cc = pts[1][1], dd = pts[2][1];
+  mjtNum c1 = a*dd - b*cc;
+  for (int i = 0; i < 4; i++) {          /* face corners against the quadrilateral */
+    mjtNum llx = i/2 ? lx : -lx, lly = i % 2 ? ly : -ly;
+    mjtNum x = llx - pts[0][0], y = lly - pts[0][1];
+    mjtNum u = (x*dd - y*b)*(1/c1), v = (y*a - x*cc)*(1/c1);
+    if (nl == 0) {
+      if ((u < 0 || u > 1) && (v < 0 || v > 1)) continue;
+    } else if (u < 0 || u > 1 || v < 0 || v > 1) {
+      continue;
+    }
+    u = u < 0 ? 0 : (u > 1 ? 1 : u);
+    v = v < 0 ? 0 : (v > 1 ? 1 : v);
+    mju_scl3(tmp1, pu[0], 1 - u - v);
+    mju_addToScl3(tmp1, pu[1], u);
+    mju_addToScl3(tmp1, pu[2], v);
+    points[n][0] = llx;
+    points[n][1] = lly;
+    points[n][2] = 0;
+    mju_sub3(tmp2, points[n], tmp1);
+    /* the reference reuses c1 here: later corners divide by this squared distance */
+    c1 = mju_dot3(tmp2, tmp2);
+    if (tmp1[2] > 0 && c1 > margin2) continue;
+    mju_add3(points[n], points[n], tmp1);
+    mju_scl3(points[n], points[n], 0.5);
+    depth[n] = sqrt(c1)*(tmp1[2] < 0 ? -1 : 1);
+    n++;
+  }
+  const int nf = n;
+  for (int i = 0; i < 4; i++) {          /* quadrilateral corners over the face */
+    mjtNum x = ppts2[i][0], y = ppts2[i][1];
+    if (nl == 0) {
+      if (nf != 0 && (x < -lx || x > lx) && (y < -ly || y > ly)) continue;
+    } else if (x < -lx || x > lx || y < -ly || y > ly) {
+      continue;
+    }
+    mjtNum d2 = 0;
+    for (int j = 0; j < 2; j++) {
+      if (ppts2[i][j] < -s[j]) d2 += (ppts2[i][j] + s[j])*(ppts2[i][j] + s[j]);
+      else if (ppts2[i][j] > s[j]) d2 += (ppts2[i][j] - s[j])*(ppts2[i][j] - s[j]);
+    }
+    d2 += pu[i][2]*innorm*pu[i][2]*innorm;
+    if (pu[i][2] > 0 && d2 > margin2) continue;
+    tmp1[0] = ppts2[i][0]*0.5;
+    tmp1[1] = ppts2[i][1]*0.5;
+    tmp1[2] = 0;
+    for (int j = 0; j < 2; j++) {
+      if (ppts2[i][j] < -s[j]) tmp1[j] = -s[j]*0.5;
+      else if (ppts2[i][j] > s[j]) tmp1[j] = s[j]*0.5;
+    }
+    mju_addToScl3(tmp1, pu[i], 0.5);
+    mju_copy3(points[n], tmp1);
+    depth[n] = sqrt(d2)*(pu[i][2] < 0 ? -1 : 1);
+    n++;
+  }
+  bb_mulMatMatT3(r, mat1, rotmore);
+  mju_mulMatVec3(tmp1, r, rnorm);
+  mju_scl3(tmp2, tmp1, in ? -1 : 1);
+  for (int i = 0; i < n; i++) {
+    c[i].dist = depth[i];
+    points[i][2] += hz;
+    mju_mulMatVec3(tmp1, r, points[i]);
+    mju_add3(c[i].pos, tmp1, pos1);
+    mju_copy3(c[i].frame, tmp2);
+    mju_zero(c[i].frame + 3, 6);
+  }
+  return n;
+}
+
+/* mju_outsideBox (engine_util_misc.c:911-950): 1 outside the inflated box, -1 inside the
+ * deflated one, 0 between */
+static int or_outsideBox(const mjtNum point[3], const mjtNum pos[3], const mjtNum mat[9],
+                         const mjtNum size[3], mjtNum inflate) {
+  mjtNum vec[3] = {point[0]-pos[0], point[1]-pos[1], point[2]-pos[2]};
+  mju_mulMatTVec3(vec, mat, vec);
+  mjtNum big[3] = {size[0]*inflate, size[1]*inflate, size[2]*inflate};
+  if (vec[0] > big[0] || vec[0] < -big[0] || vec[1] > big[1] || vec[1] < -big[1] ||
+      vec[2] > big[2] || vec[2] < -big[2]) {
+    return 1;
+  }
+  mjtNum small[3] = {size[0]/inflate, size[1]/inflate, size[2]/inflate};
+  if (vec[0] < small[0] && vec[0] > -small[0] && vec[1] < small[1] && vec[1] > -small[1] &&
+      vec[2] < small[2] && vec[2] > -small[2]) {
+    return -1;
+  }
+  return 0;
+}
+
+/* mj_collideGeoms' box-box clean-up (engine_collision_driver.c:1522-1588): drop contacts
+ * outside one box (by 1%) and not inside the other, and earlier copies of repeated
+ * positions; the survivors keep their order */
+static int or_boxBoxFilter(orRaw* c, int num, mjtNum margin, const mjtNum* pos1,
+                           const mjtNum* mat1, const mjtNum* size1, const mjtNum* pos2,
+                           const mjtNum* mat2, const mjtNum* size2) {
+  int bad[24];
+  const mjtNum sz1[3] = {size1[0] + margin, size1[1] + margin, size1[2] + margin};
+  const mjtNum sz2[3] = {size2[0] + margin, size2[1] + margin, size2[2] + margin};
+  for (int i = 0; i < num; i++) {
+    int out1 = or_outsideBox(c[i].pos, pos1, mat1, sz1, 1.01);
+    int out2 = or_outsideBox(c[i].pos, pos2, mat2, sz2, 1.01);
+    bad[i] = (out1 == 1 && out2 != -1) || (out2 == 1 && out1 != -1);
+  }
+  for (int i = 0; i < num - 1; i++) {
+    if (bad[i]) continue;
+    for (int j = i + 1; j < num; j++) {
+      if (bad[j]) continue;
+      if (c[i].pos[0] == c[j].pos[0] && c[i].pos[1] == c[j].pos[1] && c[i].pos[2] == c[j].pos[2]) {
+        bad[i] = 1;
+        break;
+      }
+    }
+  }
+  int n = 0;
+  for (int j = 0; j < num; j++) {
+    if (!bad[j]) {
+      if (n < j) c[n] = c[j];
+      n++;
+    }
+  }
+  return n;
+}
+
+/* test entry: mjc_BoxBox alone (before mj_collideGeoms' clean-up) on the current geom
+ * poses, as the reference's BadContacts/DuplicateContacts tests call it; out holds
+ * (dist, pos[3], normal[3]) per contact */
+int or_boxBoxRaw(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum margin,
+                 mjtNum* out) {
+  orRaw raw[24];
+  int num = col_boxBox(raw, margin, d->geom_xpos + 3*g1, d->geom_xmat + 9*g1,
+                       m->geom_size + 3*g1, d->geom_xpos + 3*g2, d->geom_xmat + 9*g2,
+                       m->geom_size + 3*g2);
+  for (int i = 0; i < num; i++) {
+    out[7*i] = raw[i].dist;
+    mju_copy3(out + 7*i + 1, raw[i].pos);
+    mju_copy3(out + 7*i + 4, raw[i].frame);
+  }
+  return num;
+}
+
 /* mjCOLLISIONFUNC (:41-52) for type-ordered t1 <= t2: 0 = no function, otherwise the most
  * contacts the function returns when it is one of the primitives restated here, or -1 for a
- * function outside the subset (mjc_Convex, mjc_BoxBox, mjc_CapsuleBox, mjc_SphereCylinder,
- * height fields, SDFs) */
+ * function outside the subset (mjc_Convex, height fields, SDFs) */
 static int or_collisionFunc(int t1, int t2) {
   static const int table[9][9] = {
     /*           PLANE HFIELD SPHERE CAPSULE ELLIPS CYL BOX MESH SDF */
@@ -2088,7 +2496,7 @@ static int or_collisionFunc(int t1, int t2) {
     /*CAPSULE*/ {0,    0,     0,     2,      -1,    -1, 2,  -1,  -1},
     /*ELLIPS */ {0,    0,     0,     0,      -1,    -1, -1, -1,  -1},
     /*CYL    */ {0,    0,     0,     0,      0,     -1, -1, -1,  -1},
-    /*BOX    */ {0,    0,     0,     0,      0,     0,  -1, -1,  -1},
+    /*BOX    */ {0,    0,     0,     0,      0,     0,  24, -1,  -1},
     /*MESH   */ {0,    0,     0,     0,      0,     0,  0,  -1,  -1},
     /*SDF    */ {0,    0,     0,     0,      0,     0,  0,  0,   -1}};
   if (t1 < 0 || t2 < 0 || t1 > 8 || t2 > 8) return -1;
@@ -2408,7 +2816,7 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
   const mjtNum *pos1 = d->geom_xpos + 3*g1, *mat1 = d->geom_xmat + 9*g1;
   const mjtNum *pos2 = d->geom_xpos + 3*g2, *mat2 = d->geom_xmat + 9*g2;
   const mjtNum *size1 = m->geom_size + 3*g1, *size2 = m->geom_size + 3*g2;
-  orRaw raw[4];
+  orRaw raw[24];
   int num = 0;
   if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CYLINDER) {
     num = col_planeCylinder(raw, margin, pos1, mat1, pos2, mat2, size2);
@@ -2430,6 +2838,9 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
     num = raw_sphereBox(raw, margin, pos1, size1[0], pos2, mat2, size2);
   } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {
     num = col_capsuleCapsule(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX) {
+    num = col_boxBox(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
+    if (num) num = or_boxBoxFilter(raw, num, margin, pos1, mat1, size1, pos2, mat2, size2);
   }
   if (!num) return;
   int condim;

@@ -72,6 +72,8 @@ def lib():
     L.or_forward.argtypes = [M, Dp, E]
     L.or_forward.restype = ctypes.c_int
     L.or_xfrcAccumulate.argtypes = [M, Dp, _D]
+    L.or_boxBoxRaw.argtypes = [M, Dp, ctypes.c_int, ctypes.c_int, ctypes.c_double, _D]
+    L.or_boxBoxRaw.restype = ctypes.c_int
     L.or_rungeKutta4.argtypes = [M, Dp, E]
     L.or_inverseFD.argtypes = [M, Dp, E, ctypes.c_double, _D, _D, _D, _D, _D, _D, _D]
     L.or_inverseFDEx.argtypes = [M, Dp, E, ctypes.c_double, ctypes.c_int, _D, _D, _D, _D, _D,
@@ -180,6 +182,15 @@ class Oracle:
       k = self._efc_arrays[name].size // self.efc.capacity
       return self._efc_arrays[name][:self.efc.nefc * k]
     return self._efc_int[name][:self.efc.nefc]
+
+  def box_box_raw(self, g1, g2, margin):
+    """mjc_BoxBox's raw contacts on the current geom poses (after inverse/forward):
+    (dist, pos, normal) arrays, before the driver's bad/duplicate clean-up."""
+    out = np.zeros(24 * 7)
+    n = self.L.or_boxBoxRaw(ctypes.byref(self.cm), ctypes.byref(self.d.struct), g1, g2,
+                            margin, _p(out))
+    out = out[:7 * n].reshape(n, 7)
+    return out[:, 0], out[:, 1:4], out[:, 4:7]
 
   def rne(self, flg_acc):
     """mj_rne of the data's current cdof/cinert/cvel/cdof_dot/qvel/qacc."""

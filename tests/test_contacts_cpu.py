@@ -269,12 +269,12 @@ def test_box_cylinder_device_bitexact():
 
 
 def test_unimplemented_pair_flagged_per_instance():
-  """A box-box pair (mjc_BoxBox, outside the subset) adds no capacity; an instance whose
-  pair passes the bounding-sphere filter is flagged MJHIP_INST_UNSUPPORTED, the others are
-  exact (here: the plane-sphere contact of the same instance is still made)."""
+  """A cylinder-box pair (mjc_Convex, outside the subset) adds no capacity; an instance
+  whose pair passes the bounding-sphere filter is flagged MJHIP_INST_UNSUPPORTED, the others
+  are exact (here: the plane-sphere contact of the same instance is still made)."""
   m = mjcf.load_xml_string("""<mujoco><worldbody><geom type="plane" size="5 5 .1"/>
     <geom type="box" size=".5 .5 .5" pos="0 0 2" contype="3" conaffinity="3"/>
-    <body pos="0 0 2"><freejoint/><geom type="box" size=".1 .1 .1" contype="2"
+    <body pos="0 0 2"><freejoint/><geom type="cylinder" size=".1 .1" contype="2"
       conaffinity="2"/><geom type="sphere" size=".1" pos="0 0 -.1" contype="1"
       conaffinity="1"/></body></worldbody></mujoco>""")
   cm = host.model_struct(m)
@@ -586,3 +586,163 @@ def test_capsule_box_device_bitexact():
       if f.stage > 0:
         np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name))
   assert total > 50 and two > 5
+
+
+# ---- box : box (mjc_BoxBox, engine_collision_box.c:607-1343, with mj_collideGeoms' clean-up
+# at engine_collision_driver.c:1522-1588). The models below are the reference's own test
+# fixtures (test/engine/testdata/collision_box/*.xml), held here as data.
+BOXBOX_BAD0 = """<mujoco><default><geom rgba="1 1 1 1" margin="1e-3" gap="1e-3"/></default>
+  <worldbody>
+    <geom name="ground" pos="0 0 0" quat="1 0 0 0" size="50 50 1" type="plane"/>
+    <body name="block01" pos="-0.9 0 1.5" quat="1 0 0 0"><freejoint/>
+      <geom mass="1" name="geom01" size="0.5 0.5 1.5" type="box"/></body>
+    <body name="block02" pos="-0.7 0 3.5" quat="1 0 0 0"><freejoint/>
+      <geom mass="1" name="geom02" size="1.5 0.5 0.5" type="box"/></body>
+    <body name="block03" pos="0.3 0 5.5" quat="1 0 0 0"><freejoint/>
+      <geom mass="1" name="geom03" size="0.5 0.5 1.5" type="box"/></body>
+    <body name="block04" pos="0.200 1e-9 7.5" quat="1 0 0 0"><freejoint/>
+      <geom mass="1" name="geom04" size="1.5 0.5 0.5" type="box"/></body>
+  </worldbody>
+  <contact><exclude body1="world" body2="block01"/><exclude body1="block03" body2="block02"/>
+  </contact></mujoco>"""
+BOXBOX_DUPLICATE = """<mujoco><worldbody><geom type="box" size="1 1 1"/>
+  <body pos="0 0 2"><freejoint/><geom type="box" size="1 1 1"/></body></worldbody></mujoco>"""
+BOXBOX_DEEP = """<mujoco><worldbody><geom type="box" size="1 1 1"/>
+  <body pos=".1 .2 .3"><freejoint/><geom type="box" size=".2 .2 .2"/></body></worldbody>
+  </mujoco>"""
+
+
+def _box_pairs(m, o):
+  g = o.contact_field("con_geom").reshape(-1, 2)
+  out = []
+  for g1, g2 in g:
+    if m.geom_type[g1] == 6 and m.geom_type[g2] == 6 and (g1, g2) not in out:
+      out.append((int(g1), int(g2)))
+  return out
+
+
+def _outside(point, pos, mat, size, inflate):
+  """mju_outsideBox (engine_util_misc.c:911-950), restated in numpy for the test."""
+  v = mat.reshape(3, 3).T @ (point - pos)
+  big = size * inflate
+  if (v > big).any() or (v < -big).any():
+    return 1
+  small = size / inflate
+  return -1 if ((v < small) & (v > -small)).all() else 0
+
+
+def _raw_vs_kept(m, o):
+  """Per box pair: the raw mjc_BoxBox contacts and which of them survive in the list."""
+  pos = o.contact_field("con_pos").reshape(-1, 3)
+  g = o.contact_field("con_geom").reshape(-1, 2)
+  for g1, g2 in _box_pairs(m, o):
+    margin = max(m.geom_margin[g1], m.geom_margin[g2])
+    _, raw, _ = o.box_box_raw(g1, g2, margin)
+    kept = pos[(g[:, 0] == g1) & (g[:, 1] == g2)]
+    matched = np.zeros(len(raw), bool)
+    used = np.zeros(len(kept), bool)
+    for i, p in enumerate(raw):
+      for j, q in enumerate(kept):
+        if not used[j] and (p == q).all():
+          matched[i] = used[j] = True
+          break
+    assert used.all()                       # every kept contact is a raw one
+    yield g1, g2, margin, raw, matched
+
+
+def test_boxbox_bad_contacts():
+  """BadContacts (engine_collision_box_test.cc:34-133): some raw contacts are removed, and
+  every removed one lies outside one box (by 1%) without being inside the other."""
+  m = mjcf.load_xml_string(BOXBOX_BAD0)
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  npairs = 0
+  for g1, g2, margin, raw, matched in _raw_vs_kept(m, o):
+    npairs += 1
+    assert matched.sum() < len(raw)
+    gx = o.d.geom_xpos.reshape(-1, 3)
+    gm = o.d.geom_xmat.reshape(-1, 9)
+    s1 = m.geom_size[g1] + margin
+    s2 = m.geom_size[g2] + margin
+    for i in np.flatnonzero(~matched):
+      o1 = _outside(raw[i], gx[g1], gm[g1], s1, 1.01)
+      o2 = _outside(raw[i], gx[g2], gm[g2], s2, 1.01)
+      assert (o1 == 1 and o2 != -1) or (o2 == 1 and o1 != -1)
+  assert npairs == 2
+
+
+def test_boxbox_duplicate_contacts():
+  """DuplicateContacts (engine_collision_box_test.cc:138-227): a box resting exactly on an
+  equal box; removed raw contacts are repeats of another raw contact."""
+  m = mjcf.load_xml_string(BOXBOX_DUPLICATE)
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  for g1, g2, margin, raw, matched in _raw_vs_kept(m, o):
+    assert matched.sum() < len(raw)
+    for i in np.flatnonzero(~matched):
+      assert any((raw[i] == raw[j]).all() for j in range(len(raw)) if j != i)
+  assert o.efc.ncon == 4
+
+
+def test_boxbox_deep_penetration():
+  """DeepPenetration (engine_collision_box_test.cc:233-245): 4 contacts."""
+  m = mjcf.load_xml_string(BOXBOX_DEEP)
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  assert o.efc.ncon == 4
+
+
+def test_boxbox_resting_known_answer():
+  """A level box 0.01 into a wide slab: the face path gives the small box's 4 bottom corners,
+  midway into the overlap, normal +z; the reference reports half the face depth as dist."""
+  m = mjcf.load_xml_string("""<mujoco><worldbody><geom type="box" size="1 1 .1"/>
+    <body pos=".1 .2 .29"><freejoint/><geom type="box" size=".2 .2 .2"/></body></worldbody>
+    </mujoco>""")
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  assert o.efc.ncon == 4
+  np.testing.assert_allclose(o.contact_field("con_dist"), [-0.005] * 4, atol=1e-15)
+  pos = o.contact_field("con_pos").reshape(4, 3)
+  np.testing.assert_allclose(sorted(map(tuple, np.round(pos, 12))),
+                             sorted((0.1 + sx * 0.2, 0.2 + sy * 0.2, 0.095)
+                                    for sx in (-1, 1) for sy in (-1, 1)), atol=1e-12)
+  np.testing.assert_allclose(o.contact_field("con_frame").reshape(4, 9)[:, :3],
+                             [[0, 0, 1]] * 4, atol=1e-15)
+
+
+def test_boxbox_device_bitexact():
+  """Random poses of boxes around a free box (face-face, face-edge and edge-edge separating
+  axes, the clean-up of bad and repeated contacts): the device code on the host equals the
+  oracle bit for bit on contacts, rows and outputs."""
+  m = mjcf.load_xml_string("""<mujoco><worldbody>
+    <body pos="0 0 .5"><freejoint/><geom type="box" size=".2 .15 .1"/></body>
+    <body pos=".4 0 .5"><freejoint/><geom type="box" size=".1 .12 .08" condim="1"/></body>
+    <body pos="-.4 0 .5"><freejoint/><geom type="box" size=".25 .05 .06" margin=".01"/></body>
+    </worldbody></mujoco>""")
+  rng = np.random.default_rng(41)
+  o, k = Oracle(m), KernelCPU(m)
+  total, many = 0, 0
+  for i in range(300):
+    q = m.qpos0.copy()
+    for b in range(3):
+      qq = rng.normal(size=4)
+      q[7 * b + 3:7 * b + 7] = qq / np.linalg.norm(qq)
+    for b in (1, 2):
+      q[7 * b:7 * b + 3] = q[:3] + rng.uniform(-0.3, 0.3, size=3)
+    v, a = rng.normal(size=m.nv), rng.normal(size=m.nv)
+    o.inverse(q, v, a)
+    _, st = k.inverse(q, v, a)
+    assert st == o.d.status == 0
+    ncon = o.efc.ncon
+    total += ncon
+    many += ncon > 4
+    assert k.field("con_count")[0] == ncon
+    width = dict(CON_DOUBLE + CON_INT)
+    for name in CON_FIELDS:
+      ref = o.contact_field(name).reshape(ncon, width[name])
+      np.testing.assert_array_equal(k.field(name)[:ref.size].reshape(ncon, width[name]), ref,
+                                    err_msg=f"{name} inst {i}")
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name))
+  assert total > 100 and many > 5

@@ -730,6 +730,49 @@ def test_sphere_cylinder_contacts_parity():
   assert ncon_g.sum() > B // 4
 
 
+def test_box_box_contacts_parity():
+  """mjc_BoxBox contacts (face and edge-edge separating axes, up to 24 raw contacts per pair,
+  bad and repeated ones removed) on the device: the cooperative kernel (positions staged in
+  LDS) and the generic pipeline (positions in the contact list's free tail)."""
+  from mujoco_inversedynamicstest_amd import mjcf
+  m = mjcf.load_xml_string("""<mujoco><worldbody>
+    <body pos="0 0 .5"><freejoint/><geom type="box" size=".2 .15 .1"/></body>
+    <body pos=".4 0 .5"><freejoint/><geom type="box" size=".1 .12 .08" condim="1"/></body>
+    <body pos="-.4 0 .5"><freejoint/><geom type="box" size=".25 .05 .06" margin=".01"/></body>
+    </worldbody></mujoco>""")
+  B = 4096
+  rng = np.random.default_rng(41)
+  q = np.tile(m.qpos0, (B, 1))
+  for b in range(3):
+    qq = rng.normal(size=(B, 4))
+    q[:, 7 * b + 3:7 * b + 7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
+  for b in (1, 2):
+    q[:, 7 * b:7 * b + 3] = q[:, :3] + rng.uniform(-0.3, 0.3, size=(B, 3))
+  v, a = rng.normal(size=(B, m.nv)), rng.normal(size=(B, m.nv))
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    f, st = e.inverse(q, v, a, status=True)
+    ncon_g = e.field_int("con_count", 0, B)[:, 0]
+    pos_g = e.field("con_pos", 0, B)
+    g = e.inverse(q, v, a, generic=True)
+    ncon_gen = e.field_int("con_count", 0, B)[:, 0]
+  finally:
+    e.close()
+  assert (st == 0).all()
+  np.testing.assert_array_equal(ncon_gen, ncon_g)
+  o = Oracle(m)
+  ref = []
+  for i in range(B):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    assert ncon_g[i] == o.efc.ncon
+    if i % 16 == 0 and ncon_g[i]:
+      rp = o.contact_field("con_pos").reshape(-1)
+      assert np.abs(pos_g[i][:rp.size] - rp).max() <= 1e-10 * max(1.0, np.abs(rp).max())
+  assert_close(f, np.array(ref), "qfrc_inverse")
+  assert_close(g, np.array(ref), "qfrc_inverse (generic)")
+  assert ncon_g.sum() > B // 4
+
+
 def test_capsule_box_contacts_parity():
   """mjc_CapsuleBox contacts (face, edge and corner closest; one or two per pair) on the
   device."""
