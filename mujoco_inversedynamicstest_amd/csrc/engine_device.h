@@ -74,10 +74,12 @@ MJH_HD int mjh_needSpatial(const mjhipModel* m) {
   }
   return 0;
 }
-// 1 when an actuator has a slider-crank transmission (three 3 x nv Jacobians at once)
+// 1 when an actuator has a slider-crank transmission or a site transmission with a
+// reference site (three or four 3 x nv Jacobians at once)
 MJH_HD int mjh_needSliderCrank(const mjhipModel* m) {
   for (int i = 0; i < m->nu; i++) {
     if (m->actuator_trntype[i] == mjhipTRN_SLIDERCRANK) return 1;
+    if (m->actuator_trntype[i] == mjhipTRN_SITE && m->actuator_trnid[2*i+1] >= 0) return 1;
   }
   return 0;
 }
@@ -2526,16 +2528,63 @@ MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d) {
       }
       d.actuator_length[i] = d.actuator_length[i]*gear[0];
       for (int k = 0; k < m.moment_rownnz[i]; k++) moment[k] = moment[m.moment_colind[adr+k]];
-    } else if (trn == mjhipTRN_SITE) {      // :1083-1103, no reference site: length 0
+    } else if (trn == mjhipTRN_SITE) {      // :1084-1225
       const int nv = m.nv;
       double wrench[6];
       jacInto(m, d, d.jacp, d.jacr, d.site_xpos + 3*id, m.site_bodyid[id]);
       d.actuator_length[i] = 0;
-      mulMatVec3(wrench, d.site_xmat + 9*id, gear);
-      mulMatVec3(wrench + 3, d.site_xmat + 9*id, gear + 3);
-      mulMatTVec(moment, d.jacp, wrench, 3, nv);
-      mulMatTVec(d.jacp, d.jacr, wrench + 3, 3, nv);
-      for (int j = 0; j < nv; j++) moment[j] += d.jacp[j];
+      const int refid = m.actuator_trnid[2*i+1];
+      if (refid < 0) {                      // gear in the site frame, length 0
+        mulMatVec3(wrench, d.site_xmat + 9*id, gear);
+        mulMatVec3(wrench + 3, d.site_xmat + 9*id, gear + 3);
+        mulMatTVec(moment, d.jacp, wrench, 3, nv);
+        mulMatTVec(d.jacp, d.jacr, wrench + 3, 3, nv);
+        for (int j = 0; j < nv; j++) moment[j] += d.jacp[j];
+      } else {                              // relative to the reference site (:1105-1212)
+        // deepest dof shared by the two sites' chains: its chain cancels in the difference
+        const int b0 = m.body_weldid[m.site_bodyid[id]], b1 = m.body_weldid[m.site_bodyid[refid]];
+        int da0 = m.body_dofadr[b0] + m.body_dofnum[b0] - 1;
+        int da1 = m.body_dofadr[b1] + m.body_dofnum[b1] - 1;
+        int common = -1;
+        if (da0 >= 0 && da1 >= 0) {
+          while (da0 != da1) {
+            if (da0 < da1) da1 = m.dof_parentid[da1];
+            else da0 = m.dof_parentid[da0];
+            if (da0 == -1 || da1 == -1) break;
+          }
+          if (da0 == da1) common = da0;
+        }
+        for (int j = 0; j < nv; j++) moment[j] = 0;
+        SP<S> jref = d.jacsc, jrefr = d.jacsc + 3*nv;
+        if (gear[0] != 0 || gear[1] != 0 || gear[2] != 0) {
+          double vec[3], loc[3];
+          sub3(vec, d.site_xpos + 3*id, d.site_xpos + 3*refid);
+          mulMatTVec3(loc, d.site_xmat + 9*refid, vec);
+          d.actuator_length[i] += dot3(loc, gear);
+          jacInto(m, d, jref, jrefr, d.site_xpos + 3*refid, m.site_bodyid[refid]);
+          for (int j = 0; j < 3*nv; j++) d.jacp[j] -= jref[j];
+          for (int da = common; da >= 0; da = m.dof_parentid[da]) {
+            d.jacp[da] = 0; d.jacp[nv+da] = 0; d.jacp[2*nv+da] = 0;
+          }
+          mulMatVec3(wrench, d.site_xmat + 9*refid, gear);
+          mulMatTVec(moment, d.jacp, wrench, 3, nv);
+        }
+        if (gear[3] != 0 || gear[4] != 0 || gear[5] != 0) {
+          double quat[4], refquat[4], vec[3];
+          mulQuat(quat, m.site_quat + 4*id, d.xquat + 4*m.site_bodyid[id]);
+          mulQuat(refquat, m.site_quat + 4*refid, d.xquat + 4*m.site_bodyid[refid]);
+          subQuat(vec, quat, refquat);
+          d.actuator_length[i] += dot3(vec, gear + 3);
+          jacInto(m, d, jref, jrefr, d.site_xpos + 3*refid, m.site_bodyid[refid]);
+          for (int j = 0; j < 3*nv; j++) d.jacr[j] -= jrefr[j];
+          for (int da = common; da >= 0; da = m.dof_parentid[da]) {
+            d.jacr[da] = 0; d.jacr[nv+da] = 0; d.jacr[2*nv+da] = 0;
+          }
+          mulMatVec3(wrench, d.site_xmat + 9*refid, gear + 3);
+          mulMatTVec(d.jacp, d.jacr, wrench, 3, nv);
+          for (int j = 0; j < nv; j++) moment[j] += d.jacp[j];
+        }
+      }
       for (int k = 0; k < m.moment_rownnz[i]; k++) moment[k] = moment[m.moment_colind[adr+k]];
     } else {                                // fixed tendon :1053-1081 (model-constant nonzeros)
       d.actuator_length[i] = d.ten_length[id]*gear[0];

@@ -773,9 +773,6 @@ static const char* unsupported(const mjhipModel* m) {
         t != mjhipTRN_SLIDERCRANK && t != mjhipTRN_SITE) {
       return "body transmissions";
     }
-    if (t == mjhipTRN_SITE && m->actuator_trnid[2*i+1] >= 0) {
-      return "site transmissions with a reference site";
-    }
   }
   for (int i = 0; i < m->nsensor; i++) {
     const int t = m->sensor_type[i];

@@ -1368,8 +1368,8 @@ class MJCFCompiler:
         raise MJCFError("only joint, jointinparent, fixed-tendon, slider-crank and site "
                         "transmissions are in the supported subset (body is next)"
                         if not trn else "actuator has more than one transmission target")
-      if "refsite" in a:
-        raise MJCFError("site transmissions with a reference site are not in the subset")
+      if "refsite" in a and trn[0] != "site":
+        raise MJCFError("reference site is only allowed with a site transmission")
       if a[trn[0]] not in tname[trn[0]]:
         raise MJCFError(f"unknown {trn[0]} '{a[trn[0]]}' in actuator")
       atrn[ai] = {"joint": 0, "jointinparent": 1, "cranksite": 2, "tendon": 3,
@@ -1384,6 +1384,10 @@ class MJCFCompiler:
         acrank[ai] = float(a.get("cranklength", 0.0))
         if acrank[ai] <= 0:
           raise MJCFError("crank length must be positive")
+      if trn[0] == "site" and "refsite" in a:   # user_objects.cc ResolveReferences
+        if a["refsite"] not in sitename:
+          raise MJCFError(f"reference site '{a['refsite']}' not found")
+        atrnid[ai, 1] = sitename[a["refsite"]]
       gear = [1.0, 0, 0, 0, 0, 0]
       if "gear" in a:
         g = _floats(a["gear"])
@@ -1808,6 +1812,19 @@ def sparse_structures(sizes: dict, A) -> dict:
     if atrn[ai] in (0, 1):
       cnt = {0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[tid])]
       c = list(range(jdadr[tid], jdadr[tid] + cnt))
+    elif atrn[ai] == 4 and atrnid[ai, 1] >= 0:
+      # site relative to a reference site (:1105-1212): the difference of the two sites'
+      # Jacobians with the shared ancestral chain cleared, i.e. the symmetric difference of
+      # the two dof chains
+      chains = []
+      for sid in atrnid[ai]:
+        c = set()
+        b = int(sbody[sid])
+        while b > 0:
+          c.update(range(dofadr[b], dofadr[b] + dofnum[b]))
+          b = int(parentid[b])
+        chains.append(c)
+      c = [] if not np.any(agear[ai]) else sorted(chains[0] ^ chains[1])
     elif atrn[ai] in (2, 4):
       # slider-crank: the dense moment is the chain rule over the two sites' Jacobians
       # (:1035-1052); its structural nonzeros are the dofs of both sites' body chains

@@ -212,6 +212,21 @@ class _Eval:
 _MINVAL = 1e-15
 
 
+def _ancestor_dof(m, body, dof):
+  """dof belongs to body or one of its ancestors."""
+  b = int(body)
+  while b > 0:
+    if m.body_dofadr[b] <= dof < m.body_dofadr[b] + m.body_dofnum[b]:
+      return True
+    b = int(m.body_parentid[b])
+  return False
+
+
+def _subquat(qa, qb):
+  """mju_subQuat (engine_util_spatial.c): expmap of qb^-1 * qa."""
+  return _quat2vel(_mulquat(_quat_neg(qb), qa))
+
+
 def _norm2(v):
   n = np.sqrt(v[0]*v[0] + v[1]*v[1])
   return np.array([1.0, 0.0]) if n < _MINVAL else v / n
@@ -497,13 +512,30 @@ def set_const(m):
       jC, _ = e.jac_point(m, m.site_bodyid[tid], pc)
       length = length * gear[0]
       mom = (dlda @ jA + dldv @ (jC - jS)) * gear[0]
-    elif m.actuator_trntype[a] == 4:   # site, no reference site (:1083-1103)
+    elif m.actuator_trntype[a] == 4 and m.actuator_trnid[a, 1] < 0:   # site (:1092-1102)
       b = m.site_bodyid[tid]
       p = e.xmat[b] @ m.site_pos[tid] + e.xpos[b]
       R = _quat2mat(_mulquat(e.xquat[b], m.site_quat[tid]))
       jp, jr = e.jac_point(m, b, p)
       length = 0.0
       mom = jp.T @ (R @ gear[:3]) + jr.T @ (R @ gear[3:])
+    elif m.actuator_trntype[a] == 4:   # site relative to a reference site (:1105-1212)
+      rid = m.actuator_trnid[a, 1]
+      b, br = m.site_bodyid[tid], m.site_bodyid[rid]
+      p = e.xmat[b] @ m.site_pos[tid] + e.xpos[b]
+      pr = e.xmat[br] @ m.site_pos[rid] + e.xpos[br]
+      q = _mulquat(m.site_quat[tid], e.xquat[b])
+      qr = _mulquat(m.site_quat[rid], e.xquat[br])
+      Rr = _quat2mat(_mulquat(e.xquat[br], m.site_quat[rid]))
+      jp, jr = e.jac_point(m, b, p)
+      jpr, jrr = e.jac_point(m, br, pr)
+      chain = lambda body: {d for d in range(nv) if _ancestor_dof(m, body, d)}
+      shared = sorted(chain(b) & chain(br))
+      djp, djr = jp - jpr, jr - jrr
+      djp[:, shared] = 0
+      djr[:, shared] = 0
+      length = (Rr.T @ (p - pr)) @ gear[:3] + _subquat(q, qr) @ gear[3:]
+      mom = djp.T @ (Rr @ gear[:3]) + djr.T @ (Rr @ gear[3:])
     else:
       length = L0[tid] * gear[0]
       mom = J0[tid] * gear[0]

@@ -1101,17 +1101,66 @@ static void or_transmission(const mjhipModel* m, mjhipData* d) {
        * to exactly 0; the structure here is the two sites' dof chains) */
       for (int k = 0; k < m->moment_rownnz[i]; k++) moment[k] = moment[m->moment_colind[adr+k]];
       free(jacS); free(jacr); free(jacA); free(jac);
-    } else if (trn == mjhipTRN_SITE) {   /* :1083-1103, no reference site */
+    } else if (trn == mjhipTRN_SITE) {   /* :1084-1225 */
       mjtNum wrench[6];
       mjtNum* jac = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
       mjtNum* jacS = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
       mj_jac(m, d, jac, jacS, d->site_xpos+3*id, m->site_bodyid[id]);
       *length = 0;
-      mju_mulMatVec3(wrench, d->site_xmat+9*id, gear);
-      mju_mulMatVec3(wrench+3, d->site_xmat+9*id, gear+3);
-      mju_mulMatTVec(moment, jac, wrench, 3, nv);
-      mju_mulMatTVec(jac, jacS, wrench+3, 3, nv);
-      mju_addTo(moment, jac, nv);
+      const int refid = m->actuator_trnid[2*i+1];
+      if (refid == -1) {                 /* :1092-1102 gear in the site frame */
+        mju_mulMatVec3(wrench, d->site_xmat+9*id, gear);
+        mju_mulMatVec3(wrench+3, d->site_xmat+9*id, gear+3);
+        mju_mulMatTVec(moment, jac, wrench, 3, nv);
+        mju_mulMatTVec(jac, jacS, wrench+3, 3, nv);
+        mju_addTo(moment, jac, nv);
+      } else {                           /* :1105-1212 relative to the reference site */
+        mjtNum* jacref = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+        mjtNum* jtmp = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+        int b0 = m->body_weldid[m->site_bodyid[id]];
+        int b1 = m->body_weldid[m->site_bodyid[refid]];
+        int dofadr0 = m->body_dofadr[b0] + m->body_dofnum[b0] - 1;
+        int dofadr1 = m->body_dofadr[b1] + m->body_dofnum[b1] - 1;
+        int common = -1;
+        if (dofadr0 >= 0 && dofadr1 >= 0) {
+          while (dofadr0 != dofadr1) {
+            if (dofadr0 < dofadr1) dofadr1 = m->dof_parentid[dofadr1];
+            else dofadr0 = m->dof_parentid[dofadr0];
+            if (dofadr0 == -1 || dofadr1 == -1) break;
+          }
+          if (dofadr0 == dofadr1) common = dofadr0;
+        }
+        mju_zero(moment, nv);
+        if (!mju_isZero(gear, 3)) {      /* translation: site position in the refsite frame */
+          mjtNum vec[3];
+          mju_sub3(vec, d->site_xpos+3*id, d->site_xpos+3*refid);
+          mju_mulMatTVec3(vec, d->site_xmat+9*refid, vec);
+          *length += mju_dot3(vec, gear);
+          mj_jac(m, d, jacref, jtmp, d->site_xpos+3*refid, m->site_bodyid[refid]);
+          mju_subFrom(jac, jacref, 3*nv);
+          for (int da = common; da >= 0; da = m->dof_parentid[da]) {
+            jac[da] = 0; jac[nv+da] = 0; jac[2*nv+da] = 0;
+          }
+          mju_mulMatVec3(wrench, d->site_xmat+9*refid, gear);
+          mju_mulMatTVec(moment, jac, wrench, 3, nv);
+        }
+        if (!mju_isZero(gear+3, 3)) {    /* rotation: expmap of the relative orientation */
+          mjtNum quat[4], refquat[4], vec[3];
+          mju_mulQuat(quat, m->site_quat+4*id, d->xquat+4*m->site_bodyid[id]);
+          mju_mulQuat(refquat, m->site_quat+4*refid, d->xquat+4*m->site_bodyid[refid]);
+          mju_subQuat(vec, quat, refquat);
+          *length += mju_dot3(vec, gear+3);
+          mj_jac(m, d, jtmp, jacref, d->site_xpos+3*refid, m->site_bodyid[refid]);
+          mju_subFrom(jacS, jacref, 3*nv);
+          for (int da = common; da >= 0; da = m->dof_parentid[da]) {
+            jacS[da] = 0; jacS[nv+da] = 0; jacS[2*nv+da] = 0;
+          }
+          mju_mulMatVec3(wrench, d->site_xmat+9*refid, gear+3);
+          mju_mulMatTVec(jtmp, jacS, wrench, 3, nv);
+          mju_addTo(moment, jtmp, nv);
+        }
+        free(jacref); free(jtmp);
+      }
       for (int k = 0; k < m->moment_rownnz[i]; k++) moment[k] = moment[m->moment_colind[adr+k]];
       free(jac); free(jacS);
     } else {   /* mjTRN_TENDON, dense: gear*ten_J compressed to its nonzeros */

@@ -123,6 +123,12 @@ def test_length0_matches_qpos0(model):
   o = Oracle(m)
   o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
   np.testing.assert_allclose(m.actuator_length0, o.d.actuator_length, rtol=1e-13, atol=1e-15)
+  Minv = np.linalg.inv(o.fullM())
+  for i in range(m.nu):                 # actuator_acc0 = |M^-1 moment| from setconst's numpy
+    adr, n = m.moment_rowadr[i], m.moment_rownnz[i]
+    mom = np.zeros(m.nv)
+    mom[m.moment_colind[adr:adr + n]] = o.d.actuator_moment[adr:adr + n]
+    assert m.actuator_acc0[i] == pytest.approx(np.linalg.norm(Minv @ mom), rel=1e-10)
   assert np.all(m.actuator_acc0 > 0)
 
 
@@ -254,8 +260,99 @@ def test_site_transmission_hinge_closed_form():
   np.testing.assert_allclose(m.actuator_acc0[0], (0.7 * 1.5 + 2) / o.fullM()[0, 0], rtol=1e-12)
 
 
-def test_site_refsite_rejected():
-  with pytest.raises(mjcf.MJCFError):
+REFSITE = """<mujoco><worldbody>
+  <site name="ref" pos=".1 -.2 .3" euler="10 20 30"/>
+  <body name="base" pos="0 0 .5"><joint name="s" type="slide" axis="1 0 0"/>
+    <joint name="h0" axis="0 0 1"/><geom size=".1"/>
+    <site name="bref" pos=".05 .02 0" euler="0 30 0"/>
+    <body name="a" pos=".3 0 0"><joint name="h1" axis="0 1 0"/>
+      <geom type="capsule" fromto="0 0 0 .3 0 0" size=".04"/>
+      <body name="b" pos=".3 0 0"><joint name="h2" axis="1 0 0"/><joint name="h3" axis="0 0 1"/>
+        <geom type="capsule" fromto="0 0 0 .2 0 0" size=".03"/>
+        <site name="tip" pos=".2 0 0" euler="15 -5 40"/></body></body>
+    <body name="c" pos="0 .3 0"><joint name="h4" axis="1 0 0"/><geom size=".05"/>
+      <site name="side" pos="0 .1 0"/></body></body>
+  </worldbody><actuator>
+    <general site="tip" refsite="ref" gear=".3 -1 .5 0 0 0"/>
+    <general site="tip" refsite="bref" gear="1 .5 0 0 0 0"/>
+    <general site="tip" refsite="bref" gear="0 0 0 .1 -.3 .8"/>
+    <general site="tip" refsite="side" gear=".4 .4 .2 .3 .2 .1"/>
+    <general site="tip" refsite="ref" gear=".3 -1 .5 .2 .7 -.4"/>
+  </actuator></mujoco>"""
+
+
+def test_site_refsite_moment_is_length_derivative():
+  """Site transmission relative to a reference site (:1105-1212): the translational length
+  (the site's position in the refsite frame . gear[:3]) has the moment as its derivative in
+  qpos (hinge/slide model: qvel = dq; the rotational moment is the reference's angular
+  Jacobian projection, not the expmap's derivative, so it is pinned by the known answer and
+  the compiler's numpy restatement instead); the dofs shared by the two sites' chains drop
+  out (refsite on the base)."""
+  m = mjcf.load_xml_string(REFSITE)
+  o = Oracle(m)
+  rng = np.random.default_rng(5)
+  eps = 1e-6
+  for _ in range(6):
+    q = rng.uniform(-1, 1, m.nq)
+    o.inverse(q, np.zeros(m.nv), np.zeros(m.nv))
+    mom = np.zeros((m.nu, m.nv))
+    for i in range(m.nu):
+      adr, n = m.moment_rowadr[i], m.moment_rownnz[i]
+      mom[i, m.moment_colind[adr:adr + n]] = o.d.actuator_moment[adr:adr + n]
+    num = np.zeros_like(mom)
+    for k in range(m.nv):
+      dq = np.zeros(m.nq)
+      dq[k] = eps
+      o.inverse(q + dq, np.zeros(m.nv), np.zeros(m.nv))
+      lp = o.d.actuator_length.copy()
+      o.inverse(q - dq, np.zeros(m.nv), np.zeros(m.nv))
+      num[:, k] = (lp - o.d.actuator_length) / (2 * eps)
+    np.testing.assert_allclose(mom[:2], num[:2], atol=1e-8)
+  # base dofs (slide s, hinge h0) are shared with the refsite "bref"
+  for i in (1, 2):
+    cols = m.moment_colind[m.moment_rowadr[i]:m.moment_rowadr[i] + m.moment_rownnz[i]]
+    assert 0 not in cols and 1 not in cols and len(cols) == 3
+
+
+def test_site_refsite_length_known_answer():
+  """A slide body moving a site along the world x axis, measured in a refsite frame turned
+  90 degrees about z: the translational length is -x . gear_y; the rotational length is
+  the relative rotation's expmap."""
+  m = mjcf.load_xml_string("""<mujoco><worldbody><site name="r" euler="0 0 90"/>
+    <body><joint type="slide" axis="1 0 0"/><joint name="h" axis="0 0 1"/><geom size=".1"/>
+      <site name="s"/></body></worldbody><actuator>
+    <general site="s" refsite="r" gear="0 2 0 0 0 3"/></actuator></mujoco>""")
+  o = Oracle(m)
+  for x, th in ((0.3, 0.2), (-0.7, -1.1)):
+    o.inverse(np.array([x, th]), np.zeros(2), np.zeros(2))
+    # site at (x, 0, 0), frame turned by th about z; refsite turned by pi/2
+    assert o.d.actuator_length[0] == pytest.approx(-x * 2 + (th - np.pi / 2) * 3, abs=1e-14)
+
+
+def test_site_refsite_setconst_and_device_bitexact():
+  m = mjcf.load_xml_string(REFSITE)
+  o, k = Oracle(m), KernelCPU(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  np.testing.assert_allclose(m.actuator_length0, o.d.actuator_length, rtol=1e-13, atol=1e-15)
+  Minv = np.linalg.inv(o.fullM())
+  for i in range(m.nu):                 # actuator_acc0 = |M^-1 moment| from setconst's numpy
+    adr, n = m.moment_rowadr[i], m.moment_rownnz[i]
+    mom = np.zeros(m.nv)
+    mom[m.moment_colind[adr:adr + n]] = o.d.actuator_moment[adr:adr + n]
+    assert m.actuator_acc0[i] == pytest.approx(np.linalg.norm(Minv @ mom), rel=1e-10)
+  rng = np.random.default_rng(8)
+  outs = [f.name for f in fields.DATA_FIELDS if f.stage > 0]
+  for i in range(24):
+    q, v, a = rng.uniform(-1, 1, m.nq), rng.normal(size=m.nv), rng.normal(size=m.nv)
+    ref = o.inverse(q, v, a)
+    got, st = k.inverse(q, v, a)
+    assert st == o.d.status == 0
+    np.testing.assert_array_equal(got, ref)
+    for f in outs:
+      np.testing.assert_array_equal(getattr(k.d, f), getattr(o.d, f), err_msg=f"{f} {i}")
+
+
+def test_site_refsite_unknown_rejected():
+  with pytest.raises(mjcf.MJCFError, match="reference site 'zz' not found"):
     mjcf.load_xml_string("""<mujoco><worldbody><body><joint/><geom size=".1"/><site name="a"/>
-      <site name="b" pos=".1 0 0"/></body></worldbody><actuator><general site="a"
-      refsite="b"/></actuator></mujoco>""")
+      </body></worldbody><actuator><general site="a" refsite="zz"/></actuator></mujoco>""")
