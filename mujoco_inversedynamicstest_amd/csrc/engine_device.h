@@ -80,6 +80,7 @@ MJH_HD int mjh_needSliderCrank(const mjhipModel* m) {
   for (int i = 0; i < m->nu; i++) {
     if (m->actuator_trntype[i] == mjhipTRN_SLIDERCRANK) return 1;
     if (m->actuator_trntype[i] == mjhipTRN_SITE && m->actuator_trnid[2*i+1] >= 0) return 1;
+    if (m->actuator_trntype[i] == mjhipTRN_BODY) return 1;
   }
   return 0;
 }
@@ -2583,6 +2584,55 @@ MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d) {
           mulMatVec3(wrench, d.site_xmat + 9*refid, gear + 3);
           mulMatTVec(d.jacp, d.jacr, wrench, 3, nv);
           for (int j = 0; j < nv; j++) moment[j] += d.jacp[j];
+        }
+      }
+      for (int k = 0; k < m.moment_rownnz[i]; k++) moment[k] = moment[m.moment_colind[adr+k]];
+    } else if (trn == mjhipTRN_BODY) {      // :1228-1318 adhesion: mean contact normal Jacobian
+      const int nv = m.nv, ncon = d.con_count[0];
+      d.actuator_length[i] = 0;
+      for (int j = 0; j < nv; j++) moment[j] = 0;
+      SP<S> mexcl = d.jacsc, jrow = d.jacsc + nv;
+      for (int j = 0; j < nv; j++) mexcl[j] = 0;
+      int counter = 0;
+      // the normal rows' J' * weight in row order (mj_mulJacTVec skips zero weights; the
+      // rows of contact j follow those of contact j-1), the in-gap contacts' normal
+      // Jacobians on the side
+      for (int c = 0; c < ncon; c++) {
+        const int g1 = d.con_geom[2*c], g2 = d.con_geom[2*c+1];
+        if (g1 < 0 || g2 < 0) continue;
+        const int b1 = m.geom_bodyid[g1], b2 = m.geom_bodyid[g2];
+        if (b1 != id && b2 != id) continue;
+        const int ex = d.con_exclude[c];
+        if (!ex) {
+          counter++;
+          const int dim = d.con_dim[c], adrc = d.con_efc_address[c];
+          const bool one = dim == 1 || m.opt.cone == mjhipCONE_ELLIPTIC;
+          const int nr = one ? 1 : 2*(dim - 1);
+          const double w = one ? 1.0 : 0.5/(dim - 1);
+          for (int r = adrc; r < adrc + nr; r++) {
+            SP<S> J = d.efc_J + (long)r*nv;
+            for (int k = 0; k < nv; k++) moment[k] += J[k]*w;
+          }
+        } else if (ex == 1) {
+          counter++;
+          double pos[3], frame[3];
+          for (int k = 0; k < 3; k++) { pos[k] = d.con_pos[3*c+k]; frame[k] = d.con_frame[9*c+k]; }
+          jacInto(m, d, d.jacp, d.jacr, pos, b1);
+          jacInto(m, d, d.jacr, d.jacsc + 2*nv, pos, b2);   // translation only is used
+          for (int k = 0; k < nv; k++) jrow[k] = 0;
+          for (int q = 0; q < 3; q++) {
+            if (frame[q]) {
+              for (int k = 0; k < nv; k++) jrow[k] += (d.jacr[q*nv+k] - d.jacp[q*nv+k])*frame[q];
+            }
+          }
+          for (int k = 0; k < nv; k++) mexcl[k] += jrow[k];
+        }
+      }
+      if (counter) {
+        const double s = -1.0/counter;
+        for (int k = 0; k < nv; k++) {
+          moment[k] += mexcl[k];
+          moment[k] = moment[k]*s;
         }
       }
       for (int k = 0; k < m.moment_rownnz[i]; k++) moment[k] = moment[m.moment_colind[adr+k]];

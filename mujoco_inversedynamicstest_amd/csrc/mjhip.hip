@@ -770,8 +770,8 @@ static const char* unsupported(const mjhipModel* m) {
   for (int i = 0; i < m->nu; i++) {
     int t = m->actuator_trntype[i];
     if (t != mjhipTRN_JOINT && t != mjhipTRN_JOINTINPARENT && t != mjhipTRN_TENDON &&
-        t != mjhipTRN_SLIDERCRANK && t != mjhipTRN_SITE) {
-      return "body transmissions";
+        t != mjhipTRN_SLIDERCRANK && t != mjhipTRN_SITE && t != mjhipTRN_BODY) {
+      return "unknown transmission type";
     }
   }
   for (int i = 0; i < m->nsensor; i++) {

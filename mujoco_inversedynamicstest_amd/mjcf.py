@@ -338,7 +338,7 @@ class _Defaults:
     return out
 
 
-ACTUATOR_TAGS = ("general", "motor", "position", "velocity")
+ACTUATOR_TAGS = ("general", "motor", "position", "velocity", "adhesion")
 
 
 def _resolve_orientation(attrs, degree, eulerseq, quat):
@@ -1362,18 +1362,19 @@ class MJCFCompiler:
       sitename = {x["name"]: i for i, x in enumerate(sites) if x["name"]}
       tname = {"joint": jname, "jointinparent": jname, "cranksite": sitename, "site": sitename,
                "tendon": {ta.get("name"): i for i, (ta, _) in enumerate(self.tendons)
-                          if ta.get("name")}}
-      trn = [k for k in ("joint", "jointinparent", "tendon", "cranksite", "site") if k in a]
+                          if ta.get("name")},
+               "body": {b.name: b.id for b in self.bodies if b.name}}
+      trn = [k for k in ("joint", "jointinparent", "tendon", "cranksite", "site", "body")
+             if k in a]
       if len(trn) != 1:
-        raise MJCFError("only joint, jointinparent, fixed-tendon, slider-crank and site "
-                        "transmissions are in the supported subset (body is next)"
-                        if not trn else "actuator has more than one transmission target")
+        raise MJCFError("actuator has no transmission target" if not trn
+                        else "actuator has more than one transmission target")
       if "refsite" in a and trn[0] != "site":
         raise MJCFError("reference site is only allowed with a site transmission")
       if a[trn[0]] not in tname[trn[0]]:
         raise MJCFError(f"unknown {trn[0]} '{a[trn[0]]}' in actuator")
       atrn[ai] = {"joint": 0, "jointinparent": 1, "cranksite": 2, "tendon": 3,
-                  "site": 4}[trn[0]]
+                  "site": 4, "body": 5}[trn[0]]
       atrnid[ai, 0] = tname[trn[0]][a[trn[0]]]
       if trn[0] == "cranksite":         # mjCActuator::ResolveReferences (user_objects.cc:5858-5877)
         if not a.get("slidersite"):
@@ -1456,6 +1457,14 @@ class MJCFCompiler:
         againprm[ai, 0] = kv
         abias[ai] = 1
         abiasprm[ai, 2] = -kv
+      elif tag == "adhesion":           # xml_native_reader.cc:2341-2356
+        againprm[ai, 0] = float(a.get("gain", 1.0))
+        if againprm[ai, 0] < 0:
+          raise MJCFError("adhesion gain cannot be negative")
+        cr = _floats(a["ctrlrange"]) if "ctrlrange" in a else [0.0, 0.0]
+        if cr[0] < 0 or cr[1] < 0:
+          raise MJCFError("adhesion control range cannot be negative")
+        a = dict(a, ctrllimited="true")
       cr = _floats(a["ctrlrange"]) if "ctrlrange" in a else [0.0, 0.0]
       cl = a.get("ctrllimited", "auto")
       actl[ai] = (not (cr[0] == 0 and cr[1] == 0)) if cl == "auto" else (cl == "true")
@@ -1812,6 +1821,10 @@ def sparse_structures(sizes: dict, A) -> dict:
     if atrn[ai] in (0, 1):
       cnt = {0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[tid])]
       c = list(range(jdadr[tid], jdadr[tid] + cnt))
+    elif atrn[ai] == 5:
+      # body (adhesion): the mean normal Jacobian of the body's contacts (:1228-1318); any
+      # dof can appear (the other body of a contact), so the row is dense
+      c = list(range(nv))
     elif atrn[ai] == 4 and atrnid[ai, 1] >= 0:
       # site relative to a reference site (:1105-1212): the difference of the two sites'
       # Jacobians with the shared ancestral chain cleared, i.e. the symmetric difference of

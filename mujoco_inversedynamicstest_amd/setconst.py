@@ -536,6 +536,9 @@ def set_const(m):
       djr[:, shared] = 0
       length = (Rr.T @ (p - pr)) @ gear[:3] + _subquat(q, qr) @ gear[3:]
       mom = djp.T @ (Rr @ gear[:3]) + djr.T @ (Rr @ gear[3:])
+    elif m.actuator_trntype[a] == 5:   # body (adhesion): no length; the moment needs the
+      length = 0.0                     # contacts at qpos0, which the compiler does not make
+      mom = np.zeros(nv)
     else:
       length = L0[tid] * gear[0]
       mom = J0[tid] * gear[0]

@@ -1006,7 +1006,7 @@ static mjtNum mju_dot3(const mjtNum* a, const mjtNum* b);
 /* engine_core_smooth.c:862-1100 mj_transmission: joint (slide/hinge/ball/free, in the
  * joint or the parent frame) and tendon transmissions (fixed tendons: their sparsity is a
  * model constant, moment_* model fields) */
-static void or_transmission(const mjhipModel* m, mjhipData* d) {
+static void or_transmission(const mjhipModel* m, mjhipData* d, const orEfc* e) {
   int nu = m->nu, nv = m->nv;
   int* rowadr = m->moment_rowadr;
   for (int i = 0; i < nu; i++) {
@@ -1163,6 +1163,50 @@ static void or_transmission(const mjhipModel* m, mjhipData* d) {
       }
       for (int k = 0; k < m->moment_rownnz[i]; k++) moment[k] = moment[m->moment_colind[adr+k]];
       free(jac); free(jacS);
+    } else if (trn == mjhipTRN_BODY) {   /* :1228-1318 adhesion: the contacts' normals */
+      *length = 0;
+      mju_zero(moment, nv);
+      mjtNum* force = (mjtNum*)calloc(e->nefc ? e->nefc : 1, sizeof(mjtNum));
+      mjtNum* mexcl = (mjtNum*)calloc(nv ? nv : 1, sizeof(mjtNum));
+      mjtNum* jac1 = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+      mjtNum* jac2 = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+      mjtNum* jrow = (mjtNum*)malloc(nv*sizeof(mjtNum));
+      int counter = 0;
+      for (int j = 0; j < e->ncon; j++) {
+        int g1 = e->con_geom[2*j], g2 = e->con_geom[2*j+1];
+        if (g1 < 0 || g2 < 0) continue;
+        int b1 = m->geom_bodyid[g1], b2 = m->geom_bodyid[g2];
+        if (b1 != id && b2 != id) continue;
+        if (!e->con_exclude[j]) {          /* normal rows get weight in efc_force */
+          counter++;
+          int dim = e->con_dim[j], adrj = e->con_efc_address[j];
+          if (dim == 1 || m->opt.cone == mjhipCONE_ELLIPTIC) {
+            force[adrj] = 1;
+          } else {
+            int npyramid = dim - 1;
+            for (int k = 0; k < 2*npyramid; k++) force[adrj + k] = 0.5/npyramid;
+          }
+        } else if (e->con_exclude[j] == 1) {   /* in the gap: the normal's Jacobian */
+          counter++;
+          const mjtNum* pos = e->con_pos + 3*j;
+          const mjtNum* frame = e->con_frame + 9*j;
+          mj_jac(m, d, jac1, NULL, pos, b1);
+          mj_jac(m, d, jac2, NULL, pos, b2);
+          for (int k = 0; k < 3*nv; k++) jac2[k] = jac2[k] - jac1[k];
+          mju_zero(jrow, nv);              /* mju_mulMatMat(jac, frame, jacdif, 1, 3, nv) */
+          for (int k = 0; k < 3; k++) {
+            if (frame[k]) mju_addToScl(jrow, jac2 + k*nv, frame[k], nv);
+          }
+          mju_addTo(mexcl, jrow, nv);
+        }
+      }
+      if (counter) {
+        mju_mulMatTVec(moment, e->efc_J, force, e->nefc, nv);   /* mj_mulJacTVec, dense */
+        mju_addTo(moment, mexcl, nv);
+        mju_scl(moment, moment, -1.0/counter, nv);
+      }
+      for (int k = 0; k < m->moment_rownnz[i]; k++) moment[k] = moment[m->moment_colind[adr+k]];
+      free(force); free(mexcl); free(jac1); free(jac2); free(jrow);
     } else {   /* mjTRN_TENDON, dense: gear*ten_J compressed to its nonzeros */
       *length = d->ten_length[id]*gear[0];
       for (int k = 0; k < m->moment_rownnz[i]; k++) {
@@ -3616,7 +3660,7 @@ static void or_invPosition(const mjhipModel* m, mjhipData* d, orEfc* e) {
   or_factorM(m, d);
   or_collision(m, d, e);
   or_makeConstraint(m, d, e);
-  or_transmission(m, d);
+  or_transmission(m, d, e);
 }
 
 /* engine_inverse.c:169-192 */

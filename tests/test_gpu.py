@@ -889,6 +889,41 @@ def test_site_refsite_transmission_parity():
   assert_close(mg, np.array(mref), "actuator_moment")
 
 
+@pytest.mark.parametrize("cone,condim", [("pyramidal", 3), ("elliptic", 6), ("pyramidal", 1)])
+def test_adhesion_transmission_parity(cone, condim):
+  """Body (adhesion) transmissions: the moment from the body's contact rows and in-gap
+  contacts, on the device."""
+  import os
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+  from test_transmission_cpu import _adhesion
+  m = _adhesion(cone, condim, 0.01, 0.005, 0.1)
+  B = 1024
+  rng = np.random.default_rng(19)
+  q = np.tile(m.qpos0, (B, 1))
+  q[:, 2] = 0.1 + 0.03 * rng.normal(size=B)
+  qq = np.array([1, 0, 0, 0]) + 0.15 * rng.normal(size=(B, 4))
+  q[:, 3:7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
+  q[:, 7:9] = q[:, 0:2] + rng.uniform(-0.4, 0.4, (B, 2))
+  q[:, 9] = 0.1 + 0.05 * rng.normal(size=B)
+  v, a = rng.normal(size=(B, m.nv)), rng.normal(size=(B, m.nv))
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    f, st = e.inverse(q, v, a, status=True)
+    mg = e.field("actuator_moment", 0, B)
+  finally:
+    e.close()
+  assert (st == 0).all()
+  o = Oracle(m)
+  ref, mref = [], []
+  for i in range(B):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    mref.append(o.d.actuator_moment.copy())
+  assert_close(f, np.array(ref), "qfrc_inverse")
+  assert_close(mg, np.array(mref), "actuator_moment")
+  assert np.abs(np.array(mref)).max() > 0.5
+
+
 def test_slider_crank_parity():
   """BASELINE.json config 1 model: slider-crank transmissions, per-instance UNSUPPORTED
   flags where a convex pair passes the bounding-sphere filter, exact elsewhere."""

@@ -146,12 +146,15 @@ def test_device_bitexact(model):
       np.testing.assert_array_equal(getattr(k.d, f), getattr(o.d, f), err_msg=f"{f} {i}")
 
 
-@pytest.mark.parametrize("attr", ["body", "cranksite"])
-def test_other_transmissions_rejected(attr):
-  with pytest.raises(mjcf.MJCFError):
+@pytest.mark.parametrize("attrs,msg", [
+    ('cranksite="x"', "missing base site for slider-crank"),
+    ('body="nope"', "unknown body 'nope'"),
+    ('body="b" site="x"', "more than one transmission target"),
+    ('', "no transmission target")])
+def test_bad_transmissions_rejected(attrs, msg):
+  with pytest.raises(mjcf.MJCFError, match=msg):
     mjcf.load_xml_string(f"""<mujoco><worldbody><body name="b"><joint/><geom size=".1"/>
-      <site name="x"/></body></worldbody><actuator><general {attr}="{'b' if attr == 'body'
-      else 'x'}"/></actuator></mujoco>""")
+      <site name="x"/></body></worldbody><actuator><general {attrs}/></actuator></mujoco>""")
 
 
 # ---- slider-crank (BASELINE.json config 1: model/slider_crank/slider_crank.xml) ----------
@@ -356,3 +359,74 @@ def test_site_refsite_unknown_rejected():
   with pytest.raises(mjcf.MJCFError, match="reference site 'zz' not found"):
     mjcf.load_xml_string("""<mujoco><worldbody><body><joint/><geom size=".1"/><site name="a"/>
       </body></worldbody><actuator><general site="a" refsite="zz"/></actuator></mujoco>""")
+
+
+ADHESION = """<mujoco><option cone="{cone}"/><worldbody>
+  <geom type="plane" size="2 2 .1" margin="{margin}" gap="{gap}"/>
+  <body name="box" pos="0 0 {z}"><freejoint/>
+    <geom type="box" size=".2 .2 .1" condim="{condim}" margin="{margin}" gap="{gap}"/></body>
+  <body name="ball" pos=".6 0 .3"><freejoint/><geom size=".1" condim="{condim}"/></body>
+  </worldbody><actuator><adhesion body="box" ctrlrange="0 1" gain="3"/>
+  <general body="ball"/></actuator></mujoco>"""
+
+
+def _adhesion(cone="pyramidal", condim=3, margin=0, gap=0, z=0.099):
+  return mjcf.load_xml_string(ADHESION.format(cone=cone, condim=condim, margin=margin,
+                                              gap=gap, z=z))
+
+
+def test_adhesion_compiled():
+  m = _adhesion()
+  assert list(m.actuator_trntype) == [5, 5]
+  assert m.actuator_gainprm[0, 0] == 3 and m.actuator_ctrllimited[0] == 1
+  assert list(m.moment_rownnz) == [m.nv, m.nv]
+  with pytest.raises(mjcf.MJCFError, match="adhesion control range cannot be negative"):
+    mjcf.load_xml_string(ADHESION.replace('ctrlrange="0 1"', 'ctrlrange="-1 1"').format(
+        cone="pyramidal", condim=3, margin=0, gap=0, z=.099))
+
+
+@pytest.mark.parametrize("cone,condim,margin,gap,z", [
+    ("pyramidal", 3, 0, 0, 0.099),        # active contacts, pyramid rows averaged
+    ("elliptic", 4, 0, 0, 0.099),         # elliptic: the normal row
+    ("pyramidal", 1, 0, 0, 0.099),        # frictionless: the normal row
+    ("pyramidal", 3, 0.02, 0.01, 0.115)])  # in the gap: excluded, normal Jacobian directly
+def test_adhesion_level_box_pulls_down(cone, condim, margin, gap, z):
+  """Body transmission (:1228-1318): the moment is minus the mean of the body's contact
+  normal Jacobians. A level box on a plane touches at 4 symmetric corners with normal +z, so
+  the moment is -1 on the box's z translation and ~0 elsewhere, whichever branch (pyramid
+  average, normal row, or the in-gap contact's own Jacobian) supplies it."""
+  m = _adhesion(cone, condim, margin, gap, z)
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  assert o.efc.ncon == 4
+  assert (o.contact_field("con_exclude") == (1 if gap else 0)).all()
+  want = np.zeros(m.nv)
+  want[2] = -1
+  np.testing.assert_allclose(o.d.actuator_moment[:m.nv], want, atol=1e-12)
+  assert o.d.actuator_length[0] == 0
+  np.testing.assert_array_equal(o.d.actuator_moment[m.nv:], 0)    # the ball touches nothing
+
+
+@pytest.mark.parametrize("cone,condim", [("pyramidal", 3), ("elliptic", 6), ("pyramidal", 1)])
+def test_adhesion_device_bitexact(cone, condim):
+  m = _adhesion(cone, condim, 0.01, 0.005, 0.1)
+  o, k = Oracle(m), KernelCPU(m)
+  rng = np.random.default_rng(17)
+  outs = [f.name for f in fields.DATA_FIELDS if f.stage > 0]
+  nonzero = 0
+  for i in range(40):
+    q = m.qpos0.copy()
+    q[2] = 0.1 + 0.03 * rng.normal()
+    qq = np.array([1, 0, 0, 0]) + 0.15 * rng.normal(size=4)
+    q[3:7] = qq / np.linalg.norm(qq)
+    q[7:9] = q[0:2] + rng.uniform(-0.4, 0.4, 2)
+    q[9] = 0.1 + 0.05 * rng.normal()
+    v, a = rng.normal(size=m.nv), rng.normal(size=m.nv)
+    ref = o.inverse(q, v, a)
+    got, st = k.inverse(q, v, a)
+    assert st == o.d.status == 0
+    np.testing.assert_array_equal(got, ref)
+    for f in outs:
+      np.testing.assert_array_equal(getattr(k.d, f), getattr(o.d, f), err_msg=f"{f} {i}")
+    nonzero += np.any(o.d.actuator_moment != 0)
+  assert nonzero > 10
