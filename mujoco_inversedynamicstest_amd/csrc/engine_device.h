@@ -1662,7 +1662,7 @@ MJH_HD void boxBoxEmit(double margin, const double pos1[3], const double mat1[9]
 // kernel's first pass: it needs each pair's count to place the contacts in order)
 // bbuf: per-lane room for box-box positions (24 x 3 doubles), or nullptr to use the
 // contact list's free tail at ncon (the capacity holds 24 contacts for every box pair)
-template <int S, bool WRITE = true>
+template <int S, bool WRITE = true, bool BOX = true>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
                                double margin, int& ncon, int* status, double* bbuf = nullptr);
 
@@ -1777,12 +1777,86 @@ MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, 
   setContacts(m, d, g1, g2, margin, raw, num, ncon, status);
 }
 
-// plane : box / cylinder (up to 4 contacts each) and box : box (up to 24): contacts are
-// stored as they are made
+// mj_setContact (:1387-1415) of one raw contact at index ncon; false when the list is full
 template <int S, bool WRITE>
+MJH_HD bool putContact(const mjhipModel& m, const Lane<S>& d, int g1, int g2, double margin,
+                       int condim, double gap, const double solref[2], const double solimp[5],
+                       const double friction[5], const RawContact& rk, int& ncon, int* status) {
+  if constexpr (!WRITE) {
+    ncon++;
+    return true;
+  }
+  const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
+  int i = ncon;
+  if (i >= d.con_cap) {
+    *status |= MJHIP_INST_CNSTRFULL;
+    return false;
+  }
+  double frame[9];
+  for (int j = 0; j < 9; j++) frame[j] = rk.frame[j];
+  d.con_dist[i] = rk.dist;
+  copy3(d.con_pos + 3*i, rk.pos);
+  d.con_geom[2*i] = g1;
+  d.con_geom[2*i+1] = g2;
+  d.con_dim[i] = condim;
+  double includemargin = margin - gap;
+  d.con_includemargin[i] = includemargin;
+  for (int j = 0; j < 2; j++) d.con_solref[2*i+j] = ovr ? m.opt.o_solref[j] : solref[j];
+  for (int j = 0; j < 2; j++) d.con_solreffriction[2*i+j] = ovr ? m.opt.o_solref[j] : 0.0;
+  for (int j = 0; j < 5; j++) d.con_solimp[5*i+j] = ovr ? m.opt.o_solimp[j] : solimp[j];
+  for (int j = 0; j < 5; j++) {
+    double f = ovr ? m.opt.o_friction[j] : friction[j];
+    d.con_friction[5*i+j] = f > 1e-5 ? f : 1e-5;      // mjMINMU
+  }
+  d.con_exclude[i] = rk.dist >= includemargin;
+  makeFrame(frame);
+  for (int j = 0; j < 9; j++) d.con_frame[9*i+j] = frame[j];
+  d.con_efc_address[i] = -1;
+  d.con_mu[i] = 0;
+  ncon = i + 1;
+  return true;
+}
+
+// box : box (up to 24 raw contacts)
+template <int S, bool WRITE>
+MJH_HD void collideBoxBox(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
+                          double margin, int& ncon, int* status, double* bbuf) {
+  int condim;
+  double gap, solref[2], solimp[5], friction[5];
+  contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
+  double p1[3], m1[9], p2[3], m2[9];
+  for (int k = 0; k < 3; k++) { p1[k] = d.gxpos[3*g1 + k]; p2[k] = d.gxpos[3*g2 + k]; }
+  for (int k = 0; k < 9; k++) { m1[k] = d.geom_xmat[9*g1 + k]; m2[k] = d.geom_xmat[9*g2 + k]; }
+  const double *size1 = m.geom_size + 3*g1, *size2 = m.geom_size + 3*g2;
+  unsigned keep;
+  if (bbuf) {
+    keep = boxBoxKeep(margin, p1, m1, size1, p2, m2, size2, bbuf);
+  } else {
+    if (ncon + 24 > d.con_cap) {            // cannot happen: 24 per box pair is in the capacity
+      *status |= MJHIP_INST_CNSTRFULL;
+      return;
+    }
+    keep = boxBoxKeep(margin, p1, m1, size1, p2, m2, size2, d.con_pos + 3*ncon);
+  }
+  bool ok = true;
+  boxBoxEmit(margin, p1, m1, size1, p2, m2, size2, keep,
+             [&](const RawContact& rk) MJH_LAMBDA_INLINE {
+    if (ok) ok = putContact<S, WRITE>(m, d, g1, g2, margin, condim, gap, solref, solimp,
+                                      friction, rk, ncon, status);
+  });
+}
+
+// plane : box / cylinder (up to 4 contacts each) and box : box (up to 24): contacts are
+// stored as they are made. BOX = false compiles the box-box path out (kernels launched for
+// models without a box pair: its private arrays would otherwise cost every contact kernel)
+template <int S, bool WRITE, bool BOX>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
                                double margin, int& ncon, int* status, double* bbuf) {
-  const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
+  if (m.geom_type[g1] == mjhipGEOM_BOX) {
+    if constexpr (BOX) collideBoxBox<S, WRITE>(m, d, g1, g2, margin, ncon, status, bbuf);
+    else *status |= MJHIP_INST_UNSUPPORTED;   // not reached: the launch saw no box pair
+    return;
+  }
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
   SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
   const double* size2 = m.geom_size + 3*g2;
@@ -1790,56 +1864,10 @@ MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, in
   double gap, solref[2], solimp[5], friction[5];
   contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
   auto store = [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
-    if constexpr (!WRITE) {
-      ncon++;
-      return true;
-    }
-    int i = ncon;
-    if (i >= d.con_cap) {
-      *status |= MJHIP_INST_CNSTRFULL;
-      return false;
-    }
-    double frame[9];
-    for (int j = 0; j < 9; j++) frame[j] = rk.frame[j];
-    d.con_dist[i] = rk.dist;
-    copy3(d.con_pos + 3*i, rk.pos);
-    d.con_geom[2*i] = g1;
-    d.con_geom[2*i+1] = g2;
-    d.con_dim[i] = condim;
-    double includemargin = margin - gap;
-    d.con_includemargin[i] = includemargin;
-    for (int j = 0; j < 2; j++) d.con_solref[2*i+j] = ovr ? m.opt.o_solref[j] : solref[j];
-    for (int j = 0; j < 2; j++) d.con_solreffriction[2*i+j] = ovr ? m.opt.o_solref[j] : 0.0;
-    for (int j = 0; j < 5; j++) d.con_solimp[5*i+j] = ovr ? m.opt.o_solimp[j] : solimp[j];
-    for (int j = 0; j < 5; j++) {
-      double f = ovr ? m.opt.o_friction[j] : friction[j];
-      d.con_friction[5*i+j] = f > 1e-5 ? f : 1e-5;      // mjMINMU
-    }
-    d.con_exclude[i] = rk.dist >= includemargin;
-    makeFrame(frame);
-    for (int j = 0; j < 9; j++) d.con_frame[9*i+j] = frame[j];
-    d.con_efc_address[i] = -1;
-    d.con_mu[i] = 0;
-    ncon = i + 1;
-    return true;
+    return putContact<S, WRITE>(m, d, g1, g2, margin, condim, gap, solref, solimp, friction,
+                                rk, ncon, status);
   };
-  if (m.geom_type[g1] == mjhipGEOM_BOX) {
-    double p1[3], m1[9], p2[3], m2[9];
-    for (int k = 0; k < 3; k++) { p1[k] = pos1[k]; p2[k] = pos2[k]; }
-    for (int k = 0; k < 9; k++) { m1[k] = mat1[k]; m2[k] = mat2[k]; }
-    const double* size1 = m.geom_size + 3*g1;
-    unsigned keep;
-    if (bbuf) {
-      keep = boxBoxKeep(margin, p1, m1, size1, p2, m2, size2, bbuf);
-    } else {
-      if (ncon + 24 > d.con_cap) {          // cannot happen: 24 per box pair is in the capacity
-        *status |= MJHIP_INST_CNSTRFULL;
-        return;
-      }
-      keep = boxBoxKeep(margin, p1, m1, size1, p2, m2, size2, d.con_pos + 3*ncon);
-    }
-    boxBoxEmit(margin, p1, m1, size1, p2, m2, size2, keep, store);
-  } else if (m.geom_type[g2] == mjhipGEOM_BOX) {
+  if (m.geom_type[g2] == mjhipGEOM_BOX) {
     colPlaneBox(margin, pos1, mat1, pos2, mat2, size2, store);
   } else {
     colPlaneCylinder(margin, pos1, mat1, pos2, mat2, size2, store);

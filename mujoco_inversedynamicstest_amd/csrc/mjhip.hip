@@ -155,7 +155,7 @@ static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap, bool boxpa
                     sizeof(double));
 }
 
-template <int G, bool CONTACT, bool LIST>
+template <int G, bool CONTACT, bool LIST, bool BOX = false>
 __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr, int B,
                                                         const int* __restrict__ worklist,
                                                         const int* __restrict__ count,
@@ -212,7 +212,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         g2 = pr.y;
         num = mjh::narrowGeoms<64>(m, d, g1, g2, margin, raw, &st);
         if (num < 0) {                      // plane : box / cylinder counts, then stores
-          mjh::collidePlaneBoxCyl<64, false>(m, d, g1, g2, margin, cnt, &st, bbuf);
+          mjh::collidePlaneBoxCyl<64, false, BOX>(m, d, g1, g2, margin, cnt, &st, bbuf);
         } else {
           cnt = num;
         }
@@ -222,7 +222,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       if (cnt) {
         int c = ncon + excl;
         if (num < 0) {
-          mjh::collidePlaneBoxCyl<64, true>(m, d, g1, g2, margin, c, &st, bbuf);
+          mjh::collidePlaneBoxCyl<64, true, BOX>(m, d, g1, g2, margin, c, &st, bbuf);
         } else {
           mjh::setContacts<64>(m, d, g1, g2, margin, raw, num, c, &st);
         }
@@ -1097,27 +1097,30 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     const int* wl = c->worklist + 2;
     if (fused && c->coop && c->fast->cmode) {   // cooperative lanes per instance
       const bool contact = c->con_cap > 0, list = c->fast->cmode == 1;
-#define MJHIP_LAUNCH_COOP(G, C, L)                                                            \
-      hipLaunchKernelGGL((k_constraint_coop<G, C, L>), dim3(coopGrid(B, G, L)),               \
+#define MJHIP_LAUNCH_COOP(G, C, L, X)                                                         \
+      hipLaunchKernelGGL((k_constraint_coop<G, C, L, X>), dim3(coopGrid(B, G, L)),            \
                          dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap, c->boxpair),        \
                          c->stream,                                                           \
                          c->dmodel, c->mirror, B, wl,                                         \
                          (const int*)cnt, c->pairs, c->npair, qfrc, status)
-      if (c->coop == 8) {
-        if (contact) { if (list) MJHIP_LAUNCH_COOP(8, true, true);
-                       else MJHIP_LAUNCH_COOP(8, true, false); }
-        else { if (list) MJHIP_LAUNCH_COOP(8, false, true);
-               else MJHIP_LAUNCH_COOP(8, false, false); }
+      if (contact && c->boxpair) {       // the box-box path is compiled in only here
+        if (list) MJHIP_LAUNCH_COOP(16, true, true, true);
+        else MJHIP_LAUNCH_COOP(16, true, false, true);
+      } else if (c->coop == 8) {
+        if (contact) { if (list) MJHIP_LAUNCH_COOP(8, true, true, false);
+                       else MJHIP_LAUNCH_COOP(8, true, false, false); }
+        else { if (list) MJHIP_LAUNCH_COOP(8, false, true, false);
+               else MJHIP_LAUNCH_COOP(8, false, false, false); }
       } else if (c->coop == 32) {
-        if (contact) { if (list) MJHIP_LAUNCH_COOP(32, true, true);
-                       else MJHIP_LAUNCH_COOP(32, true, false); }
-        else { if (list) MJHIP_LAUNCH_COOP(32, false, true);
-               else MJHIP_LAUNCH_COOP(32, false, false); }
+        if (contact) { if (list) MJHIP_LAUNCH_COOP(32, true, true, false);
+                       else MJHIP_LAUNCH_COOP(32, true, false, false); }
+        else { if (list) MJHIP_LAUNCH_COOP(32, false, true, false);
+               else MJHIP_LAUNCH_COOP(32, false, false, false); }
       } else {
-        if (contact) { if (list) MJHIP_LAUNCH_COOP(16, true, true);
-                       else MJHIP_LAUNCH_COOP(16, true, false); }
-        else { if (list) MJHIP_LAUNCH_COOP(16, false, true);
-               else MJHIP_LAUNCH_COOP(16, false, false); }
+        if (contact) { if (list) MJHIP_LAUNCH_COOP(16, true, true, false);
+                       else MJHIP_LAUNCH_COOP(16, true, false, false); }
+        else { if (list) MJHIP_LAUNCH_COOP(16, false, true, false);
+               else MJHIP_LAUNCH_COOP(16, false, false, false); }
       }
 #undef MJHIP_LAUNCH_COOP
     } else {
