@@ -128,8 +128,11 @@ def fast_path_supported(m) -> str | None:
   if m.opt["density"] > 0 or m.opt["viscosity"] > 0:
     return "fluid"
   for a in range(m.nu):
-    if m.actuator_trntype[a] not in (0, 1) or m.jnt_type[m.actuator_trnid[a, 0]] not in (2, 3):
-      return "ball/free-joint or tendon transmissions"
+    trn = m.actuator_trntype[a]
+    if trn == 3:                       # fixed tendon (spatial ones are rejected above)
+      continue
+    if trn not in (0, 1) or m.jnt_type[m.actuator_trnid[a, 0]] not in (2, 3):
+      return "ball/free-joint, slider-crank, site or body transmissions"
   if m.sizes.get("nsensor", 0) and not (m.opt["disableflags"] & (1 << 12)):
     return "sensors (mj_sensorPos/Vel/Acc run on the generic kernel)"
   return None
@@ -492,12 +495,19 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
       for k in range(nv):
         G.st("ten_J", t * nv + k, lit(J[k]))
   if m.nu:
-    E("// ---- mj_transmission (joint)")
+    E("// ---- mj_transmission (hinge/slide joint, fixed tendon)")
     for a in range(m.nu):
       jid = int(m.actuator_trnid[a, 0])
       g = float(m.actuator_gear[a, 0])
+      adr = int(m.moment_rowadr[a])
+      if m.actuator_trntype[a] == 3:   # :1053-1081: gear * ten_J over the row's nonzeros
+        G.st("actuator_length", a, f"ten_length[{jid}]*{lit(g)}")
+        J = M.ten_row(jid)
+        for k in range(int(m.moment_rownnz[a])):
+          G.st("actuator_moment", adr + k, lit(float(J[int(m.moment_colind[adr + k])]) * g))
+        continue
       G.st("actuator_length", a, f"qpos[{int(m.jnt_qposadr[jid])}]*{lit(g)}")
-      G.st("actuator_moment", int(m.moment_rowadr[a]), lit(g))
+      G.st("actuator_moment", adr, lit(g))
 
   cams = {}
   for c in range(m.ncam):
@@ -842,8 +852,21 @@ def _gen_va(M: _Model, store_fields=None) -> str:
     G.st("ten_velocity", t, f"ten_velocity_{t}")
   if m.nu and not (dsbl & (1 << 10)):
     for a in range(m.nu):
-      col = int(m.moment_colind[m.moment_rowadr[a]])
+      adr, n = int(m.moment_rowadr[a]), int(m.moment_rownnz[a])
       g = float(m.actuator_gear[a, 0])
+      if m.actuator_trntype[a] == 3:   # mju_dotSparse over the tendon row's nonzeros
+        if not n:
+          G.st("actuator_velocity", a, "0.0")
+          continue
+        J = M.ten_row(int(m.actuator_trnid[a, 0]))
+        cols = [int(c) for c in m.moment_colind[adr:adr + n]]
+        E.open()
+        E(f"const double mom[{n}] = {arr_lit([float(J[c]) * g for c in cols])};")
+        E(f"const int ind[{n}] = {{{', '.join(str(c) for c in cols)}}};")
+        G.st("actuator_velocity", a, f"mjh::dotSparse(mom, qvel, {n}, ind)")
+        E.close()
+        continue
+      col = int(m.moment_colind[adr])
       G.st("actuator_velocity", a, f"((0.0 + 0.0) + (0.0 + 0.0)) + {lit(g)}*qvel[{col}]")
 
   # mj_passive: springs, dampers, tendon spring-dampers (engine_passive.c:436-493)

@@ -164,3 +164,25 @@ def test_generated_with_equality_constraints():
   assert codegen.constraint_mode(m) == "all"
   q, v, a = sample_states(m, 16, first=3)
   run_and_compare(m, "equality", q, v, a)
+
+
+def test_generated_tendon_transmissions():
+  """Fixed-tendon transmissions on the straight-line path: length gear*ten_length, the
+  model-constant moment row gear*coef, actuator_velocity by mju_dotSparse over the row;
+  a zero coefficient drops its column."""
+  xml = """<mujoco><option><flag contact="disable"/></option><worldbody>
+    <body pos="0 0 1"><joint name="a" axis="0 1 0" range="-60 60"/>
+      <geom type="capsule" fromto="0 0 0 .3 0 0" size=".05"/>
+      <body pos=".3 0 0"><joint name="b" axis="0 0 1"/><geom size=".05"/>
+        <body pos=".1 0 0"><joint name="c" type="slide" axis="1 0 0"/><geom size=".03"/>
+        </body></body></body></worldbody>
+    <tendon><fixed name="t1" limited="true" range="-.5 .6"><joint joint="a" coef="1.5"/>
+      <joint joint="c" coef="-.25"/></fixed>
+      <fixed name="t2"><joint joint="b" coef="0"/><joint joint="c" coef="2"/>
+      <joint joint="a" coef=".5"/></fixed></tendon>
+    <actuator><motor tendon="t1" gear="3"/><motor joint="b"/><motor tendon="t2" gear="-.7"/>
+    </actuator></mujoco>"""
+  m = mjcf.load_xml_string(xml)
+  assert codegen.fast_path_supported(m) is None
+  q, v, a = sample_states(m, 48, margin=-0.2)
+  run_and_compare(m, "tendontrn", q, v, a)

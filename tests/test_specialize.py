@@ -13,7 +13,7 @@ from mujoco_inversedynamicstest_amd import codegen, engine, fields, mjcf, specia
 from mujoco_inversedynamicstest_amd.sampler import sample_states
 
 # not bundled: a slide base, hinges with limits and springs, a limited fixed tendon, a ball
-# joint, motors on the hinges (codegen.fast_path_supported covers all of it)
+# joint, motors on the hinges and the tendon (codegen.fast_path_supported covers all of it)
 ARM_XML = """
 <mujoco model="rt_arm">
   <option gravity="0 0 -9.81" timestep="0.002"/>
@@ -53,6 +53,7 @@ ARM_XML = """
     <motor joint="h1" gear="2"/>
     <motor joint="h2"/>
     <motor joint="slide"/>
+    <motor tendon="t12" gear="1.5"/>
   </actuator>
 </mujoco>
 """
