@@ -133,8 +133,6 @@ def fast_path_supported(m) -> str | None:
       continue
     if trn not in (0, 1) or m.jnt_type[m.actuator_trnid[a, 0]] not in (2, 3):
       return "ball/free-joint, slider-crank, site or body transmissions"
-  if m.sizes.get("nsensor", 0) and not (m.opt["disableflags"] & (1 << 12)):
-    return "sensors (mj_sensorPos/Vel/Acc run on the generic kernel)"
   return None
 
 

@@ -5031,6 +5031,18 @@ MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage,
   return status;
 }
 
+// mj_sensorPos/Vel/Acc of mj_inverseSkip(mjSTAGE_NONE, skipsensor = 0) after the generated
+// kernels and the constraint part: every sensor reads only its own stage's fields, which no
+// later stage rewrites, and none reads qfrc_inverse, so running the three after the whole
+// pass gives the reference's values
+template <int S>
+MJH_HD void sensorsAfter(const mjhipModel& m, const Lane<S>& d) {
+  if (!m.nsensor || (m.opt.disableflags & mjhipDSBL_SENSOR)) return;
+  sensorPos(m, d);
+  sensorVel(m, d);
+  sensorAcc(m, d);
+}
+
 // The constraint part of mj_inverseSkip(mjSTAGE_NONE) for an instance whose constraint-free
 // stages the generated kernels (codegen.py) already wrote to the mirror, with the raw
 // mj_rne(flg_acc = 1) result left in qfrc_inverse: collision, mj_makeConstraint and its

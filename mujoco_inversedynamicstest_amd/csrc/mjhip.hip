@@ -455,6 +455,14 @@ __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
   if (status) status[inst] = st;
 }
 
+// sensors after the generated kernels and the constraint kernel (mjh::sensorsAfter)
+__global__ __launch_bounds__(64) void k_sensors(mjhipModel m, Mirror mr, int B) {
+  const int blk = blockIdx.x, lane = threadIdx.x;
+  if ((long)blk*64 + lane >= B) return;
+  Lane<64> d = lane_view(mr, blk, lane);
+  mjh::sensorsAfter<64>(m, d);
+}
+
 // row-major (B x n) <-> mirror block layout
 __global__ void k_to_mirror(const double* __restrict__ src, double* __restrict__ dst, int B,
                             int n) {
@@ -1142,6 +1150,10 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
 #undef MJHIP_LAUNCH_CON
     }
     HIPCHECK(hipGetLastError());
+    if (!skipsensor && c->hmodel.nsensor > 0 && !(c->hmodel.opt.disableflags & mjhipDSBL_SENSOR)) {
+      hipLaunchKernelGGL(k_sensors, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
+      HIPCHECK(hipGetLastError());
+    }
     if (status) {
       hipLaunchKernelGGL(k_check, grid, block, 0, c->stream, c->dmodel, c->mirror, B, status);
       HIPCHECK(hipGetLastError());

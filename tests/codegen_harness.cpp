@@ -31,6 +31,7 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
 #define XD(name, d0, d1, stage) mr.name##_n = (m->d0) * (d1); \
   mr.name = (double*)calloc((size_t)nblk * 64 * (mr.name##_n + 1), sizeof(double));
   MJHIP_DATA_FIELDS
+  MJHIP_DATA_FORWARD              /* zero inputs the sensor pass reads (xfrc_applied, ...) */
 #undef XD
 #define XSC(name, n) mr.name##_n = (n); \
   mr.name = (double*)calloc((size_t)nblk * 64 * ((n) + 1), sizeof(double));
@@ -60,12 +61,19 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
       else constraint_part<false, false>(m, mr, inst);
     }
   }
+  for (int i = 0; i < B; i++) {         // the sensor pass (k_sensors on the device)
+    mjh::Lane<64> d = lane_view(mr, i / 64, i % 64);
+    mjh::sensorsAfter<64>(*m, d);
+  }
   size_t off = 0;
 #define XD(name, d0, d1, stage) { int S = mr.name##_n; \
   for (int i = 0; i < B; i++) for (int k = 0; k < S; k++) \
     out[off + (size_t)i*S + k] = mr.name[((size_t)(i/64)*S + k)*64 + (i%64)]; \
   off += (size_t)B*S; free(mr.name); }
   MJHIP_DATA_FIELDS
+#undef XD
+#define XD(name, d0, d1, stage) free(mr.name);
+  MJHIP_DATA_FORWARD
 #undef XD
 #undef MJ_M
 #define XSC(name, n) free(mr.name);

@@ -93,9 +93,8 @@ def test_humanoid_generated_worklist(humanoid):
 
 @pytest.mark.parametrize("name", ["inverse_test", "linear", "inertia"])
 def test_small_models_generated_bitexact(name):
-  # linear.xml has sensors, which the generic kernel evaluates: its generated kernel is
-  # built for the sensor-disabled variant
-  m = models.load(name, disable_contact=True, disable_sensor=(name == "linear"))
+  # linear.xml has sensors: they run in the sensor pass after the generated kernels
+  m = models.load(name, disable_contact=True)
   q, v, a = sample_states(m, 40, first=3)
   run_and_compare(m, name, q, v, a)
 
@@ -186,3 +185,16 @@ def test_generated_tendon_transmissions():
   assert codegen.fast_path_supported(m) is None
   q, v, a = sample_states(m, 48, margin=-0.2)
   run_and_compare(m, "tendontrn", q, v, a)
+
+
+def test_generated_then_sensor_pass():
+  """Sensor models on the straight-line path: every supported sensor type (limit and
+  contact rows active) computed by the sensor pass after the generated kernels and the
+  constraint part equals the oracle bit for bit."""
+  import sys
+  sys.path.insert(0, HERE)
+  from test_sensors_cpu import _all_model
+  m = _all_model()
+  assert codegen.fast_path_supported(m) is None
+  q, v, a = sample_states(m, 32, first=11, margin=-0.3, resample_tendons=False)
+  run_and_compare(m, "allsensors", q, v, a)

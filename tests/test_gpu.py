@@ -254,11 +254,15 @@ def test_sensors_parity():
   af = rng.normal(size=(B, m.nu))
   qa = rng.normal(size=(B, m.nv))
   e = engine.InverseEngine(m, capacity=B)
-  assert e.fast_kernel is None
+  # the run-time straight-line kernel with the sensor pass after it, and the generic kernel
+  assert e.fast_kernel and e.fast_kernel.startswith("rt_")
   for name, val in (("time", time), ("xfrc_applied", xfrc), ("actuator_force", af),
                     ("qfrc_actuator", qa)):
     e.set_field(name, val)
   e.inverse(q, v, a)
+  got = {f: e.field(f, 0, B) for f in ("sensordata", "qfrc_inverse", "subtree_linvel",
+                                        "subtree_angmom", "cfrc_int", "cfrc_ext")}
+  e.inverse(q, v, a, generic=True)
   o = Oracle(m)
   ref = {f: [] for f in ("sensordata", "qfrc_inverse", "subtree_linvel", "subtree_angmom",
                          "cfrc_int", "cfrc_ext")}
@@ -271,7 +275,8 @@ def test_sensors_parity():
     for f in ref:
       ref[f].append(getattr(o.d, f).copy())
   for f, r in ref.items():
-    assert_close(e.field(f, 0, B), np.array(r), f)
+    assert_close(got[f], np.array(r), f + " (straight-line + sensor pass)")
+    assert_close(e.field(f, 0, B), np.array(r), f + " (generic)")
   e.close()
 
 
