@@ -131,8 +131,8 @@ def fast_path_supported(m) -> str | None:
     trn = m.actuator_trntype[a]
     if trn == 3:                       # fixed tendon (spatial ones are rejected above)
       continue
-    if trn not in (0, 1) or m.jnt_type[m.actuator_trnid[a, 0]] not in (2, 3):
-      return "ball/free-joint, slider-crank, site or body transmissions"
+    if trn not in (0, 1):
+      return "slider-crank, site or body transmissions"
   return None
 
 
@@ -504,7 +504,44 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
         for k in range(int(m.moment_rownnz[a])):
           G.st("actuator_moment", adr + k, lit(float(J[int(m.moment_colind[adr + k])]) * g))
         continue
-      G.st("actuator_length", a, f"qpos[{int(m.jnt_qposadr[jid])}]*{lit(g)}")
+      jt, qa = int(m.jnt_type[jid]), int(m.jnt_qposadr[jid])
+      inparent = m.actuator_trntype[a] == 1
+      gear = [float(x) for x in m.actuator_gear[a]]
+      if jt == BALL:                   # :912-942 expmap axis . gear axis
+        E.open()
+        E("double axis[3], quat[4], ga[3];")
+        E(f"mjh::copy4(quat, qpos + {qa});")
+        E("mjh::normalize4(quat);")
+        E("mjh::quat2Vel(axis, quat, 1);")
+        E(f"const double g3[3] = {arr_lit(gear[:3])};")
+        if inparent:
+          E("quat[1] = -quat[1]; quat[2] = -quat[2]; quat[3] = -quat[3];")
+          E("mjh::rotVecQuat(ga, g3, quat);")
+        else:
+          E("mjh::copy3(ga, g3);")
+        G.st("actuator_length", a, "axis[0]*ga[0] + axis[1]*ga[1] + axis[2]*ga[2]")
+        G.stv("actuator_moment", adr, "ga", 3)
+        E.close()
+        continue
+      if jt == FREE:                   # :944-971 length 0, moment = (gear, gear axis)
+        E.open()
+        E("double ga[3];")
+        E(f"const double g3[3] = {arr_lit(gear[3:6])};")
+        if inparent:
+          E("double quat[4];")
+          E(f"mjh::copy4(quat, qpos + {qa + 3});")
+          E("mjh::normalize4(quat);")
+          E("quat[1] = -quat[1]; quat[2] = -quat[2]; quat[3] = -quat[3];")
+          E("mjh::rotVecQuat(ga, g3, quat);")
+        else:
+          E("mjh::copy3(ga, g3);")
+        G.st("actuator_length", a, "0.0")
+        for k in range(3):
+          G.st("actuator_moment", adr + k, lit(gear[k]))
+        G.stv("actuator_moment", adr + 3, "ga", 3)
+        E.close()
+        continue
+      G.st("actuator_length", a, f"qpos[{qa}]*{lit(g)}")
       G.st("actuator_moment", adr, lit(g))
 
   cams = {}
@@ -822,7 +859,8 @@ def _gen_va(M: _Model, store_fields=None) -> str:
   if M.cmode == "list":   # k_pos's work-list flag: k_constraint assembles this instance
     E("const bool cflag = ec[0] != 0;")
   G.pointers(["qpos", "qvel", "qacc", "cinert", "cdof", "xipos", "subtree_com", "ten_length",
-              "ten_velocity", "actuator_velocity", "cvel", "cdof_dot", "qfrc_spring",
+              "ten_velocity", "actuator_velocity", "actuator_moment", "cvel", "cdof_dot",
+              "qfrc_spring",
               "qfrc_damper", "qfrc_gravcomp", "qfrc_fluid", "qfrc_passive", "qfrc_bias",
               "qfrc_constraint", "qfrc_inverse"])
   G.load("qpos", "qpos", nq)
@@ -860,6 +898,16 @@ def _gen_va(M: _Model, store_fields=None) -> str:
         cols = [int(c) for c in m.moment_colind[adr:adr + n]]
         E.open()
         E(f"const double mom[{n}] = {arr_lit([float(J[c]) * g for c in cols])};")
+        E(f"const int ind[{n}] = {{{', '.join(str(c) for c in cols)}}};")
+        G.st("actuator_velocity", a, f"mjh::dotSparse(mom, qvel, {n}, ind)")
+        E.close()
+        continue
+      if int(m.jnt_type[int(m.actuator_trnid[a, 0])]) in (BALL, FREE):
+        cols = [int(c) for c in m.moment_colind[adr:adr + n]]
+        E.open()                       # the row k_pos stored, over its 3 or 6 columns
+        E(f"double mom[{n}];")
+        for k in range(n):
+          E(f"mom[{k}] = P_actuator_moment[{adr + k}*64];")
         E(f"const int ind[{n}] = {{{', '.join(str(c) for c in cols)}}};")
         G.st("actuator_velocity", a, f"mjh::dotSparse(mom, qvel, {n}, ind)")
         E.close()

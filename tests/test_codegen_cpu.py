@@ -198,3 +198,17 @@ def test_generated_then_sensor_pass():
   assert codegen.fast_path_supported(m) is None
   q, v, a = sample_states(m, 32, first=11, margin=-0.3, resample_tendons=False)
   run_and_compare(m, "allsensors", q, v, a)
+
+
+def test_generated_ball_free_transmissions():
+  """Ball and free-joint transmissions, in the joint and the parent frame, on the
+  straight-line path (the model of tests/test_transmission_cpu.py)."""
+  import sys
+  sys.path.insert(0, HERE)
+  import re
+  from test_transmission_cpu import XML
+  m = mjcf.load_xml_string(re.sub(r'<general site="tip"[^>]*/>', "", XML))   # site: generic
+  assert codegen.fast_path_supported(m) is None
+  assert set(int(t) for t in m.actuator_trntype) >= {0, 1}
+  q, v, a = sample_states(m, 40, first=5)
+  run_and_compare(m, "ballfree", q, v, a)

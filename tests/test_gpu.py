@@ -839,17 +839,23 @@ def test_mocap_parity():
   e.close()
 
 
-def test_transmission_parity():
-  """Ball/free-joint and fixed-tendon transmissions: actuator_length/moment on the device."""
+@pytest.mark.parametrize("path", ["generic", "straight-line"])
+def test_transmission_parity(path):
+  """Ball/free-joint and fixed-tendon transmissions: actuator_length/moment on the device,
+  through the generic kernel (with a site transmission) and through the run-time
+  straight-line kernel (without it)."""
   import os
+  import re
   import sys
   sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
   from test_transmission_cpu import XML
   from mujoco_inversedynamicstest_amd import mjcf
-  m = mjcf.load_xml_string(XML)
+  xml = XML if path == "generic" else re.sub(r'<general site="tip"[^>]*/>', "", XML)
+  m = mjcf.load_xml_string(xml)
   B = 256
   q, v, a = sample_states(m, B, first=5)
   e = engine.InverseEngine(m, capacity=B)
+  assert (e.fast_kernel is None) == (path == "generic")
   f = e.inverse(q, v, a)
   o = Oracle(m)
   ref, lref, mref = [], [], []
