@@ -119,8 +119,6 @@ def fast_path_supported(m) -> str | None:
     return "sparse Jacobians"
   if m.opt["enableflags"] & (1 << 3):
     return "INVDISCRETE"
-  if m.opt["enableflags"] & (1 << 1):
-    return "ENERGY (mj_energyPos/Vel run on the generic kernel)"
   if m.nmocap or m.na:
     return "mocap/activations"
   if m.sizes.get("nwrap", 0) and np.any(np.asarray(m.wrap_type) != 1):

@@ -5031,16 +5031,19 @@ MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage,
   return status;
 }
 
-// mj_sensorPos/Vel/Acc of mj_inverseSkip(mjSTAGE_NONE, skipsensor = 0) after the generated
-// kernels and the constraint part: every sensor reads only its own stage's fields, which no
-// later stage rewrites, and none reads qfrc_inverse, so running the three after the whole
-// pass gives the reference's values
+// mj_sensorPos/Vel/Acc and mj_energyPos/Vel of mj_inverseSkip(mjSTAGE_NONE) after the
+// generated kernels and the constraint part, in the reference's order: every sensor and
+// energy term reads only its own stage's fields, which no later stage rewrites, and none
+// reads qfrc_inverse, so running them after the whole pass gives the reference's values
 template <int S>
-MJH_HD void sensorsAfter(const mjhipModel& m, const Lane<S>& d) {
-  if (!m.nsensor || (m.opt.disableflags & mjhipDSBL_SENSOR)) return;
-  sensorPos(m, d);
-  sensorVel(m, d);
-  sensorAcc(m, d);
+MJH_HD void sensorsAfter(const mjhipModel& m, const Lane<S>& d, bool sensors = true) {
+  sensors = sensors && m.nsensor > 0;
+  const bool energy = (m.opt.enableflags & mjhipENBL_ENERGY) != 0;
+  if (sensors) sensorPos(m, d);
+  if (energy) energyPos(m, d);
+  if (sensors) sensorVel(m, d);
+  if (energy) energyVel(m, d);
+  if (sensors) sensorAcc(m, d);
 }
 
 // The constraint part of mj_inverseSkip(mjSTAGE_NONE) for an instance whose constraint-free

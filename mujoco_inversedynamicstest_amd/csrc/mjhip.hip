@@ -455,12 +455,13 @@ __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
   if (status) status[inst] = st;
 }
 
-// sensors after the generated kernels and the constraint kernel (mjh::sensorsAfter)
-__global__ __launch_bounds__(64) void k_sensors(mjhipModel m, Mirror mr, int B) {
+// sensors and energy after the generated kernels and the constraint kernel
+// (mjh::sensorsAfter)
+__global__ __launch_bounds__(64) void k_sensors(mjhipModel m, Mirror mr, int B, int sensors) {
   const int blk = blockIdx.x, lane = threadIdx.x;
   if ((long)blk*64 + lane >= B) return;
   Lane<64> d = lane_view(mr, blk, lane);
-  mjh::sensorsAfter<64>(m, d);
+  mjh::sensorsAfter<64>(m, d, sensors != 0);
 }
 
 // row-major (B x n) <-> mirror block layout
@@ -1150,8 +1151,11 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
 #undef MJHIP_LAUNCH_CON
     }
     HIPCHECK(hipGetLastError());
-    if (!skipsensor && c->hmodel.nsensor > 0 && !(c->hmodel.opt.disableflags & mjhipDSBL_SENSOR)) {
-      hipLaunchKernelGGL(k_sensors, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
+    const int sensors = !skipsensor && c->hmodel.nsensor > 0 &&
+                        !(c->hmodel.opt.disableflags & mjhipDSBL_SENSOR);
+    if (sensors || (c->hmodel.opt.enableflags & mjhipENBL_ENERGY)) {
+      hipLaunchKernelGGL(k_sensors, grid, block, 0, c->stream, c->dmodel, c->mirror, B,
+                         sensors);
       HIPCHECK(hipGetLastError());
     }
     if (status) {

@@ -212,3 +212,14 @@ def test_generated_ball_free_transmissions():
   assert set(int(t) for t in m.actuator_trntype) >= {0, 1}
   q, v, a = sample_states(m, 40, first=5)
   run_and_compare(m, "ballfree", q, v, a)
+
+
+def test_generated_with_energy():
+  """mjENBL_ENERGY on the straight-line path: mj_energyPos/Vel in the pass after the
+  generated kernels (the humanoid, limits active on some instances); every mirror output
+  here, the energy values themselves on the GPU (test_gpu.py::test_energy_parity)."""
+  m = models.load("humanoid", disable_contact=True)
+  m.opt["enableflags"] |= 1 << 1
+  assert codegen.fast_path_supported(m) is None
+  q, v, a = sample_states(m, 32, first=500, margin=-0.1, resample_tendons=False)
+  run_and_compare(m, "humanoid_energy", q, v, a)

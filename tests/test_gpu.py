@@ -597,9 +597,13 @@ def test_energy_parity():
   q, v, a = sample_states(m, B, first=500)
   e = engine.InverseEngine(m, capacity=B)
   try:
-    assert e.fast_kernel is None
+    # the humanoid with ENERGY has its own signature: a run-time straight-line kernel, the
+    # energy terms in the pass after it; then the generic kernel
+    assert e.fast_kernel and e.fast_kernel.startswith("rt_")
     f = e.inverse(q, v, a)
     en = e.field("energy", 0, B)
+    g = e.inverse(q, v, a, generic=True)
+    eg = e.field("energy", 0, B)
   finally:
     e.close()
   o = Oracle(m)
@@ -609,6 +613,8 @@ def test_energy_parity():
     ref_e.append(o.d.energy)
   assert_close(f, np.array(ref_f), "qfrc_inverse (ENERGY)")
   assert_close(en, np.array(ref_e), "energy")
+  assert_close(g, np.array(ref_f), "qfrc_inverse (ENERGY, generic)")
+  assert_close(eg, np.array(ref_e), "energy (generic)")
 
 
 def test_single_instance_sensors_dropin():
