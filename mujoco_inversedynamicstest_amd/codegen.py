@@ -119,8 +119,6 @@ def fast_path_supported(m) -> str | None:
     return "sparse Jacobians"
   if m.opt["enableflags"] & (1 << 3):
     return "INVDISCRETE"
-  if m.nmocap or m.na:
-    return "mocap/activations"
   if m.sizes.get("nwrap", 0) and np.any(np.asarray(m.wrap_type) != 1):
     return "spatial tendons (generic kernel)"
   if m.opt["density"] > 0 or m.opt["viscosity"] > 0:
@@ -318,8 +316,15 @@ def _emit_frame(G: _Stage, i, store):
   else:
     pid = M.parent[i]
     E.open()
-    E(f"const double bpos[3] = {arr_lit(m.body_pos[i])};")
-    E(f"const double bquat[4] = {arr_lit(m.body_quat[i])};")
+    mid = int(m.body_mocapid[i]) if m.nmocap else -1
+    if mid >= 0:                       # :72-82 mocap body: the per-instance input pose
+      E(f"double bpos[3], bquat[4];")
+      E(f"for (int k = 0; k < 3; k++) bpos[k] = P_mocap_pos[({3 * mid} + k)*64];")
+      E(f"for (int k = 0; k < 4; k++) bquat[k] = P_mocap_quat[({4 * mid} + k)*64];")
+      E("mjh::normalize4s(bquat);")
+    else:
+      E(f"const double bpos[3] = {arr_lit(m.body_pos[i])};")
+      E(f"const double bquat[4] = {arr_lit(m.body_quat[i])};")
     if pid:
       E(f"mjh::mulMatVec3(xpos_{i}, xmat_{pid}, bpos);")
       E(f"mjh::addTo3(xpos_{i}, xpos_{pid});")

@@ -831,9 +831,14 @@ def test_mocap_parity():
   rng = np.random.default_rng(8)
   mp, mq = rng.normal(size=(B, 3)), rng.normal(size=(B, 4))
   e = engine.InverseEngine(m, capacity=B)
+  # the run-time straight-line kernel reads the mocap inputs; then the generic kernel
+  assert e.fast_kernel and e.fast_kernel.startswith("rt_")
   e.set_field("mocap_pos", mp)
   e.set_field("mocap_quat", mq)
   f = e.inverse(q, v, a)
+  sf = e.field("sensordata", 0, B)
+  g = e.inverse(q, v, a, generic=True)
+  sg = e.field("sensordata", 0, B)
   o = Oracle(m)
   ref, sref = [], []
   for i in range(B):
@@ -841,7 +846,9 @@ def test_mocap_parity():
     ref.append(o.inverse(q[i], v[i], a[i]))
     sref.append(o.d.sensordata.copy())
   assert_close(f, np.array(ref), "qfrc_inverse")
-  assert_close(e.field("sensordata", 0, B), np.array(sref), "sensordata")
+  assert_close(sf, np.array(sref), "sensordata")
+  assert_close(g, np.array(ref), "qfrc_inverse (generic)")
+  assert_close(sg, np.array(sref), "sensordata (generic)")
   e.close()
 
 
