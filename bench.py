@@ -59,18 +59,19 @@ def spawn_ranks(gpus: int) -> int:
   return subprocess.call(cmd)
 
 
-def pmc_traffic(eng, model, count):
+def pmc_traffic(eng, m, model, count):
   """HBM bytes per launch from the newest committed PMC summary (tools/pmc.sh +
-  tools/pmc_summary.py) if it was measured on the kernels this run used, else None."""
+  tools/pmc_summary.py) whose kernels were built from the same generated source as the one
+  this run launches (matched by codegen.source_hash, not by name), else None."""
   import glob
   from mujoco_inversedynamicstest_amd import codegen
   if not eng.fast_kernel:
     return None, None
-  want = set(codegen.hot_kernels(eng.fast_kernel))
+  sha = codegen.source_hash(m, eng.fast_kernel)
   for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")),
                      reverse=True):
     rec = json.load(open(path))
-    if rec.get("model") == model and want <= set(rec["kernels"]):
+    if rec.get("model") == model and rec.get("source_sha") == sha:
       per_eval = rec["traffic_bytes_per_eval"]
       return per_eval * count, os.path.relpath(path, ROOT)
   return None, None
@@ -170,7 +171,7 @@ def main():
   generic_ms = eng.time_kernel(count, reps=5, generic=True)
   bytes_per_eval = engine.output_bytes_per_eval(m)
   achieved = bytes_per_eval * count / (kernel_ms * 1e-3) / 1e9
-  traffic, traffic_src = pmc_traffic(eng, args.model, count)
+  traffic, traffic_src = pmc_traffic(eng, m, args.model, count)
 
   # every rank's full qfrc_inverse on rank 0 (outside the timed regions): a checksum of
   # checksums over the whole global batch, and a spot check of the gathered rows
@@ -226,7 +227,13 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_per_eval * count,
                      "kernel": ("+".join(codegen.hot_kernels(eng.fast_kernel))
                                 + "+k_constraint" if eng.fast_kernel else "k_inverse<0>"),
-                     "kernel_ms": kernel_ms, "generic_kernel_ms": generic_ms,
+                     "kernel_ms": kernel_ms,
+                     "kernel_ms_method": "HIP events on the context's stream around `reps` "
+                                         "back-to-back launches of the hot path, divided by "
+                                         "reps (rocprof's per-dispatch durations each include "
+                                         "their own dispatch ramp, so their sum reads a few "
+                                         "us higher)",
+                     "generic_kernel_ms": generic_ms,
                      "bytes_per_eval": bytes_per_eval},
         "cpu_baseline": cpu,
         "checksum_qfrc_inverse": checksum,
@@ -291,6 +298,8 @@ def config5(args):
   world = int(os.environ.get("WORLD_SIZE", "1"))
   rank = int(os.environ.get("RANK", "0"))
   local = int(os.environ.get("LOCAL_RANK", "0"))
+  if world != args.gpus:
+    raise SystemExit(f"bench.py --config 5: --gpus {args.gpus} but WORLD_SIZE={world}")
   torch.cuda.set_device(local)
   dev = torch.device("cuda", local)
   if world > 1:

@@ -1324,6 +1324,18 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   return "\n".join(out) + "\n"
 
 
+def source_hash(m, name: str) -> str:
+  """Identity of the code a kernel of model m named `name` is built from: its generated
+  source and the device header it includes (keys committed PMC summaries to the kernel they
+  measured; a run-time kernel, rt_*, has C linkage)."""
+  import os
+  h = hashlib.sha256(generate(m, name, extern_c=name.startswith("rt_")).encode())
+  with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
+                         "engine_device.h"), "rb") as f:
+    h.update(f.read())
+  return h.hexdigest()[:16]
+
+
 def hot_kernels(name: str) -> list:
   """Names of the kernels one fast-path launch of model `name` runs (profiles, bench)."""
   return [f"k_all_{name}"] if FUSE else [f"k_{st}_{name}" for st in STAGES]

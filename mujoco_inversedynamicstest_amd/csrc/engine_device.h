@@ -656,8 +656,9 @@ MJH_HD void jac(const mjhipModel& m, const Lane<S>& d, P point, int body) {
 
 
 //---------------------------------- engine_collision_*.c -------------------------------------
-// mj_collision for the primitive pairs plane/sphere/capsule (the candidate rules are shared
-// with the oracle in include/mjhip_contact.h); contacts go to the con_* scratch fields.
+// mj_collision for the primitive pairs (the static candidate rules are in
+// include/mjhip_contact.h; the oracle restates the reference's broadphase on its own, so the
+// parity tests check these rules against it); contacts go to the con_* scratch fields.
 
 struct RawContact { double dist, pos[3], frame[9]; };
 

@@ -16,6 +16,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <unordered_map>
@@ -990,6 +991,16 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
       }
     }
   }
+  if (c->coop) {
+    // the cooperative kernel's dynamic LDS must fit one block: many box pairs (a large
+    // efc_cap) or few lanes per instance can exceed it, and then the one-lane k_constraint
+    // serves the model instead of every launch failing
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) != hipSuccess) return fail("hipGetDeviceProperties");
+    if (coopLdsBytes(*m, c->coop, c->efc_cap, c->boxpair) > (unsigned)prop.sharedMemPerBlock) {
+      c->coop = 0;
+    }
+  }
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     return fail("hipStreamCreate");
   }
@@ -1656,10 +1667,58 @@ __global__ __launch_bounds__(64) void k_stage(mjhipModel m, Mirror mr, int what,
 static int g_device = 0;
 static std::mutex g_mu;
 // contexts of the single-instance calls, keyed by the model's content signature (sizes,
-// options, every array): a new or edited model at a reused address gets its own context
-struct CachedCtx { unsigned long long sig; mjhipContext* c; };
-static std::vector<CachedCtx> g_ctx;        // most recently used last, at most kMaxCtx
+// options, every array): a new or edited model at a reused address gets its own context.
+// A call leases its entry for its whole upload/launch/download sequence: the lease holds a
+// reference (an entry evicted or released meanwhile is freed when its last lease ends) and
+// the entry's call lock (the calls share instance 0 and the stream of the context).
+struct CtxEntry {
+  unsigned long long sig = 0;
+  mjhipContext* c = nullptr;
+  std::mutex call_mu;
+  ~CtxEntry() { if (c) mjhip_contextFree(c); }
+};
+using CtxRef = std::shared_ptr<CtxEntry>;
+// most recently used last, at most kMaxCtx; never destroyed (contexts are not freed during
+// static destruction, after the HIP runtime may have gone)
+static std::vector<CtxRef>& g_ctx = *new std::vector<CtxRef>;
 static const size_t kMaxCtx = 16;
+// mjhip_inverseFD's context (capacity 3nv+1) is cached under the signature with this salt
+static const unsigned long long kFDSalt = 0x9E3779B97F4A7C15ull;
+
+struct CtxLease {
+  CtxRef e;
+  std::unique_lock<std::mutex> lk;
+  mjhipContext* get() const { return e ? e->c : nullptr; }
+};
+
+static CtxLease lease_ctx(const mjhipModel* m, unsigned long long salt, int capacity) {
+  const unsigned long long sig = model_signature(m) ^ salt;
+  CtxRef e;
+  {
+    std::lock_guard<std::mutex> lk(g_mu);
+    for (size_t i = 0; i < g_ctx.size(); i++) {
+      if (g_ctx[i]->sig == sig) {
+        e = g_ctx[i];
+        g_ctx.erase(g_ctx.begin() + i);
+        g_ctx.push_back(e);
+        break;
+      }
+    }
+    if (!e) {
+      mjhipContext* c = nullptr;
+      if (mjhip_contextCreate(m, g_device, capacity, &c) != MJHIP_OK) return {};
+      e = std::make_shared<CtxEntry>();
+      e->sig = sig;
+      e->c = c;
+      if (g_ctx.size() >= kMaxCtx) g_ctx.erase(g_ctx.begin());   // least recently used
+      g_ctx.push_back(e);
+    }
+  }
+  CtxLease L;
+  L.e = e;
+  L.lk = std::unique_lock<std::mutex>(e->call_mu);
+  return L;
+}
 
 static void report(const char* what) {
   std::string msg = std::string(what) + ": " + g_last_error;
@@ -1670,38 +1729,13 @@ static void report(const char* what) {
   }
 }
 
-static mjhipContext* ctx_for(const mjhipModel* m) {
-  const unsigned long long sig = model_signature(m);
-  std::lock_guard<std::mutex> lk(g_mu);
-  for (size_t i = 0; i < g_ctx.size(); i++) {
-    if (g_ctx[i].sig == sig) {
-      CachedCtx e = g_ctx[i];
-      g_ctx.erase(g_ctx.begin() + i);
-      g_ctx.push_back(e);
-      return e.c;
-    }
-  }
-  mjhipContext* c = nullptr;
-  if (mjhip_contextCreate(m, g_device, 64, &c) != MJHIP_OK) return nullptr;
-  if (g_ctx.size() >= kMaxCtx) {            // evict the least recently used
-    mjhip_contextFree(g_ctx.front().c);
-    g_ctx.erase(g_ctx.begin());
-  }
-  g_ctx.push_back({sig, c});
-  return c;
-}
-
 MJHIP_API void mjhip_setDevice(int device) { g_device = device; }
 
 MJHIP_API void mjhip_releaseModel(const mjhipModel* m) {
   const unsigned long long sig = model_signature(m);
   std::lock_guard<std::mutex> lk(g_mu);
-  for (size_t i = 0; i < g_ctx.size(); i++) {
-    if (g_ctx[i].sig == sig) {
-      mjhip_contextFree(g_ctx[i].c);
-      g_ctx.erase(g_ctx.begin() + i);
-      return;
-    }
+  for (size_t i = g_ctx.size(); i-- > 0;) {
+    if (g_ctx[i]->sig == sig || g_ctx[i]->sig == (sig ^ kFDSalt)) g_ctx.erase(g_ctx.begin() + i);
   }
 }
 
@@ -1842,7 +1876,8 @@ static int run_stage(mjhipContext* c, mjhipData* d, int what, int skipstage = 0,
 // instance, download every output field of the stages that ran
 MJHIP_API void mjhip_inverseSkip(const mjhipModel* m, mjhipData* d, int skipstage,
                                  int skipsensor) {
-  mjhipContext* c = ctx_for(m);
+  CtxLease lease = lease_ctx(m, 0, 64);
+  mjhipContext* c = lease.get();
   if (!c) {
     report("mjhip_inverseSkip");
     return;
@@ -1904,7 +1939,8 @@ MJHIP_API void mjhip_inverse(const mjhipModel* m, mjhipData* d) {
 // that stage runs, it reads the inputs and earlier stages' fields from d and writes only its
 // own outputs into d
 static void single_stage(const mjhipModel* m, mjhipData* d, int what, const char* name) {
-  mjhipContext* c = ctx_for(m);
+  CtxLease lease = lease_ctx(m, 0, 64);
+  mjhipContext* c = lease.get();
   int rc = c ? 0 : MJHIP_ERR_HIP;
   if (!rc && hipSetDevice(c->device) != hipSuccess) rc = MJHIP_ERR_HIP;
   const int stage = what;                  // ST_POS/VEL/CON = position/velocity/acceleration
@@ -1938,7 +1974,8 @@ MJHIP_API void mjhip_invConstraint(const mjhipModel* m, mjhipData* d) {
 // mj_rne (engine_core_smooth.c:1969-2023): reads the caller's cdof, cinert, cvel, cdof_dot,
 // qvel (and qacc with flg_acc) and writes only `result`
 MJHIP_API void mjhip_rne(const mjhipModel* m, mjhipData* d, int flg_acc, mjtNum* result) {
-  mjhipContext* c = ctx_for(m);
+  CtxLease lease = lease_ctx(m, 0, 64);
+  mjhipContext* c = lease.get();
   int rc = c ? 0 : MJHIP_ERR_HIP;
   if (!rc && hipSetDevice(c->device) != hipSuccess) rc = MJHIP_ERR_HIP;
   if (!rc) rc = put0(c, c->mirror.cdof, (const double*)d->cdof, 6L*m->nv);
@@ -1958,7 +1995,8 @@ MJHIP_API void mjhip_rne(const mjhipModel* m, mjhipData* d, int flg_acc, mjtNum*
 // mj_xfrcAccumulate (engine_support.c:1254-1261): qfrc += J' xfrc_applied over bodies 1..,
 // through mj_applyFT (its mj_jac reads d's xipos, subtree_com and cdof)
 MJHIP_API void mjhip_xfrcAccumulate(const mjhipModel* m, mjhipData* d, mjtNum* qfrc) {
-  mjhipContext* c = ctx_for(m);
+  CtxLease lease = lease_ctx(m, 0, 64);
+  mjhipContext* c = lease.get();
   int rc = c ? 0 : MJHIP_ERR_HIP;
   if (!rc && hipSetDevice(c->device) != hipSuccess) rc = MJHIP_ERR_HIP;
   if (!rc) rc = put0(c, c->mirror.xipos, (const double*)d->xipos, 3L*m->nbody);
@@ -2032,23 +2070,10 @@ MJHIP_API void mjhip_inverseFD(const mjhipModel* m, mjhipData* d, mjtNum eps,
                                mjtByte flg_actuation, mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa,
                                mjtNum* DsDq, mjtNum* DsDv, mjtNum* DsDa, mjtNum* DmDq) {
   const int P = 3*m->nv + 1;
-  mjhipContext* c = nullptr;
-  {
-    // an FD batch of one needs 3nv+1 instances: a context of that capacity, cached like the
-    // single-instance ones under a signature salted with the capacity
-    const unsigned long long sig = model_signature(m) ^ 0x9E3779B97F4A7C15ull;
-    std::lock_guard<std::mutex> lk(g_mu);
-    for (size_t i = 0; i < g_ctx.size() && !c; i++) {
-      if (g_ctx[i].sig == sig) c = g_ctx[i].c;
-    }
-    if (!c && mjhip_contextCreate(m, g_device, P, &c) == MJHIP_OK) {
-      if (g_ctx.size() >= kMaxCtx) {
-        mjhip_contextFree(g_ctx.front().c);
-        g_ctx.erase(g_ctx.begin());
-      }
-      g_ctx.push_back({sig, c});
-    }
-  }
+  // an FD batch of one needs 3nv+1 instances: a context of that capacity, leased like the
+  // single-instance ones under the salted signature
+  CtxLease lease = lease_ctx(m, kFDSalt, P);
+  mjhipContext* c = lease.get();
   int rc = c ? 0 : MJHIP_ERR_HIP;
   if (!rc && m->nsensor && (DsDq || DsDv || DsDa)) {
     std::vector<double> t(P, d->time);                    // clock sensors of every evaluation

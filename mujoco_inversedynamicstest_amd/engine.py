@@ -184,13 +184,23 @@ class InverseEngine:
     self.device = device
     self.capacity = L.mjhip_contextCapacity(ctx)
     self.nv, self.nq = model.nv, model.nq
+    explicit = specialize is True
     if specialize is None:
       specialize = os.environ.get("MJHIP_SPECIALIZE", "1") != "0"
     if specialize and self.fast_kernel is None and os.environ.get("MJHIP_DISABLE_FAST") != "1":
       from . import codegen
       from . import specialize as spec
       if codegen.fast_path_supported(model) is None:
-        spec.load(self)
+        try:
+          spec.load(self)
+        except (spec.SpecializeError, OSError) as e:
+          # no compiler, a read-only cache or a failed compile: the generic kernel still
+          # serves the model (it did before specialization); only an explicit request fails
+          if explicit:
+            raise
+          import warnings
+          warnings.warn(f"run-time kernel specialization unavailable, using the generic "
+                        f"kernel: {e}", RuntimeWarning, stacklevel=2)
 
   def close(self):
     if getattr(self, "ctx", None):
@@ -353,6 +363,15 @@ class InverseEngine:
     if _dptr(qpos) is not None:
       import torch
       B = qpos.shape[0]
+      # the kernels index these by B without bounds: check the shapes before the launch
+      if tuple(qpos.shape) != (B, self.nq) or tuple(qvel.shape) != (B, nv) or \
+         tuple(qacc.shape) != (B, nv):
+        raise MJHIPError(f"inverse_fd: expected qpos [{B}, {self.nq}], qvel and qacc "
+                         f"[{B}, {nv}]")
+      if ctrl is not None and ctrl.numel() != B * self.m.nu:
+        raise MJHIPError(f"inverse_fd: ctrl must hold B x nu = {B * self.m.nu} values")
+      if flg_actuation and self.m.nu and ctrl is None:
+        raise MJHIPError("inverse_fd: flg_actuation needs ctrl [B, nu]")
       if out is None:
         mk = lambda n: torch.empty((B, nv, n), dtype=torch.float64, device=qpos.device)
         out = (mk(nv), mk(nv), mk(nv), mk(self.m.nM) if dmdq else None)

@@ -8,8 +8,9 @@ image's compiler driver) and hands it to the context (mjhip_contextLoadKernel), 
 MJCF runs the fast path instead of the generic kernel ("template codegen at
 load").
 
-Code objects are cached by the SHA-256 of their generated source in MJHIP_KERNEL_CACHE
-(default: kernel_cache/ next to this file), so a model compiles once. A C host loads the
+Code objects are cached by the SHA-256 of their generated source, the headers it includes,
+the compiler flags and `hipcc --version`, in MJHIP_KERNEL_CACHE (default: mjhip_kernels/ in
+the user's cache directory), so a model compiles once per compiler. A C host loads the
 same code object: `python -m mujoco_inversedynamicstest_amd.specialize
 model.xml` writes it and prints the name, signature and constraint mode to pass.
 """
@@ -32,7 +33,26 @@ FLAGS = ["--genco", "--offload-arch=gfx950", "-O3", "-std=c++17", "-Wno-unused-v
 
 
 def cache_dir() -> str:
-  return os.environ.get("MJHIP_KERNEL_CACHE", os.path.join(_HERE, "kernel_cache"))
+  """MJHIP_KERNEL_CACHE, else the user's cache directory (the package may be read-only)."""
+  if os.environ.get("MJHIP_KERNEL_CACHE"):
+    return os.environ["MJHIP_KERNEL_CACHE"]
+  base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
+  return os.path.join(base, "mjhip_kernels")
+
+
+_compiler_id = None
+
+
+def compiler_id() -> str:
+  """`hipcc --version` of the compiler in use (part of the cache key: a code object built
+  by another compiler or with other flags is never reused)."""
+  global _compiler_id
+  if _compiler_id is None:
+    r = subprocess.run([HIPCC, "--version"], capture_output=True, text=True)
+    if r.returncode != 0:
+      raise SpecializeError(f"{HIPCC} --version failed: {r.stderr[-400:]}")
+    _compiler_id = HIPCC + "\n" + r.stdout
+  return _compiler_id
 
 
 class SpecializeError(RuntimeError):
@@ -59,6 +79,8 @@ def code_object(m) -> tuple[bytes, str, int, int]:
   name, src = source(m)
   # the headers are part of what the code object depends on
   h = hashlib.sha256(src.encode())
+  h.update(" ".join(FLAGS).encode())
+  h.update(compiler_id().encode())
   for hdr in ("engine_device.h",):
     h.update(open(os.path.join(CSRC, hdr), "rb").read())
   for hdr in ("mjhip.h", "mjhip_fields.h", "mjhip_contact.h"):

@@ -66,11 +66,11 @@ def test_no_cpu_fallback_without_device(humanoid):
     engine.InverseEngine(humanoid, capacity=64)
 
 
+@pytest.mark.gpu
 def test_unsupported_model_rejected():
   """A model outside the device subset (here: sparse constraint Jacobians, jacobian=sparse)
-  is rejected at context creation with MJHIP_ERR_MODEL, never run approximately."""
-  if engine.lib().mjhip_deviceCount() == 0:
-    pytest.skip("rejection happens after the device check")
+  is rejected at context creation with MJHIP_ERR_MODEL, never run approximately (the
+  rejection happens after the device check, so this needs the GPU)."""
   m = models.load("humanoid")
   m.opt["jacobian"] = 1
   with pytest.raises(engine.MJHIPError, match="MODEL"):

@@ -226,3 +226,45 @@ def test_model_cache_follows_content(humanoid):
   close(d.qfrc_inverse, o.inverse(q[0], v[0], a[0]), "edited model")
   assert not np.allclose(d.qfrc_inverse, f0)
   engine.release_model(m)
+
+
+def test_context_cache_threads_past_capacity():
+  """The single-instance calls cache at most 16 device contexts (least recently used
+  evicted). 4 threads cycle through 20 distinct models (the inverse_test arm with its
+  gravity changed, so each has its own content signature) concurrently: a call keeps its
+  context alive and to itself until it returns, so every result matches the oracle."""
+  import threading
+  base = models.load("inverse_test", disable_contact=True)
+  ms = []
+  for k in range(20):
+    mk = models.load("inverse_test", disable_contact=True)
+    mk.opt["gravity"] = np.asarray(base.opt["gravity"], dtype=float) * (1.0 + 0.05 * k)
+    ms.append(mk)
+  q, v, a = sample_states(base, 8, first=3)
+  refs = []
+  for mk in ms:
+    o = Oracle(mk)
+    refs.append([o.inverse(q[i], v[i], a[i]) for i in range(len(q))])
+  errors = []
+
+  def work(t):
+    try:
+      for rep in range(3):
+        for j in range(len(ms)):
+          k = (j + 7 * t + rep) % len(ms)
+          d = host.MjData(ms[k])
+          i = (t + j) % len(q)
+          d.qpos[:], d.qvel[:], d.qacc[:] = q[i], v[i], a[i]
+          engine.mj_inverse(ms[k], d)
+          close(d.qfrc_inverse, refs[k][i], f"model {k} state {i}")
+    except Exception as e:   # reported on the main thread
+      errors.append(e)
+
+  threads = [threading.Thread(target=work, args=(t,)) for t in range(4)]
+  for th in threads:
+    th.start()
+  for th in threads:
+    th.join()
+  for mk in ms:
+    engine.release_model(mk)
+  assert not errors, errors[0]

@@ -53,15 +53,18 @@ def _worker(rank, world, port, total, q):
   qp, qv, qa = sample_states(m, count, first=first)
   o = Oracle(m)
   out = torch.tensor(np.array([o.inverse(qp[i], qv[i], qa[i]) for i in range(count)]))
-  got = parallel.gather_to_rank0(out, world, rank)
+  got = parallel.gather_to_rank0(out, world, rank, parallel.shard_counts(total, world))
   if rank == 0:
     q.put(torch.cat(got).numpy())
   dist.barrier()
   dist.destroy_process_group()
 
 
-def test_gloo_world2_gather_matches_single_process(humanoid):
-  total, world = 64, 2
+@pytest.mark.parametrize("total", [64, 65])
+def test_gloo_world2_gather_matches_single_process(humanoid, total):
+  """Even shards (64 over 2) and uneven ones (65: rank 0 holds 33 rows, rank 1 32), the
+  receive sizes then coming from shard_counts as bench.py's --global-batch passes them."""
+  world = 2
   ctx = mp.get_context("spawn")
   q = ctx.Queue()
   port = _free_port()

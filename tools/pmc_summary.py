@@ -44,7 +44,9 @@ def main(src, dst):
   kernels = [k for k in fetch if k.startswith("k_") and ("humanoid" in k or k.startswith("k_constraint"))]
   rows = {k: {"fetch_bytes": fetch[k] * calib, "write_bytes": write.get(k, 0.0)} for k in kernels}
   total = sum(v["fetch_bytes"] + v["write_bytes"] for v in rows.values())
+  from mujoco_inversedynamicstest_amd import codegen
   out = {"batch": B, "model": "humanoid", "fetch_correction": calib,
+         "source_sha": codegen.source_hash(m, "humanoid"),
          "kernels": rows, "traffic_bytes_per_launch": total,
          "traffic_bytes_per_eval": total / B,
          "note": "FETCH_SIZE x correction (calibrated on k_fac reading exactly qM) + WRITE_SIZE, "
