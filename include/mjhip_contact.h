@@ -154,7 +154,8 @@ MJHIP_CONTACT_HD int mjhip_contactCapacity(const mjhipModel* m, int* rows) {
   return ncon;
 }
 
-/* constraint rows per instance: dof friction, joint/tendon limits, contacts */
+/* constraint rows per instance: dof/tendon friction, joint/tendon limits, contacts,
+   equalities */
 MJHIP_CONTACT_HD int mjhip_efcCapacity(const mjhipModel* m) {
   int n = 0, crow = 0;
   for (int i = 0; i < m->njnt; i++) {
@@ -165,6 +166,9 @@ MJHIP_CONTACT_HD int mjhip_efcCapacity(const mjhipModel* m) {
   }
   for (int i = 0; i < m->nv; i++) {
     if (m->dof_frictionloss[i] > 0) n += 1;
+  }
+  for (int i = 0; i < m->ntendon; i++) {
+    if (m->tendon_frictionloss[i] > 0) n += 1;
   }
   if (mjhip_contactCapacity(m, &crow) > 0) n += crow;
   for (int i = 0; i < m->neq; i++) {        /* nemax (user_model.cc): rows per equality */

@@ -145,10 +145,13 @@
   X(mjtByte, tendon_limited,       ntendon,   1) \
   X(mjtNum,  tendon_solref_lim,    ntendon,   2) \
   X(mjtNum,  tendon_solimp_lim,    ntendon,   5) \
+  X(mjtNum,  tendon_solref_fri,    ntendon,   2) \
+  X(mjtNum,  tendon_solimp_fri,    ntendon,   5) \
   X(mjtNum,  tendon_range,         ntendon,   2) \
   X(mjtNum,  tendon_margin,        ntendon,   1) \
   X(mjtNum,  tendon_stiffness,     ntendon,   1) \
   X(mjtNum,  tendon_damping,       ntendon,   1) \
+  X(mjtNum,  tendon_frictionloss,  ntendon,   1) \
   X(mjtNum,  tendon_lengthspring,  ntendon,   2) \
   X(mjtNum,  tendon_length0,       ntendon,   1) \
   X(mjtNum,  tendon_invweight0,    ntendon,   1) \

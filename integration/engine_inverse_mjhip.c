@@ -41,9 +41,6 @@ void* mj_arenaAllocByte(mjData* d, size_t bytes, size_t alignment);
 
 /* features outside the device subset that mjhipModel cannot show; NULL when supported */
 static const char* adapter_unsupported(const mjModel* m) {
-  for (int i = 0; i < m->ntendon; i++) {
-    if (m->tendon_frictionloss[i] > 0) return "tendon frictionloss (FRICTION_TENDON rows)";
-  }
   for (int g = 0; g < m->ngeom; g++) {
     if (m->geom_fluid[mjNFLUID*g] > 0) return "the ellipsoid fluid model (geom fluidshape)";
   }

@@ -139,7 +139,9 @@ def constraint_mode(m) -> str:
     return "none"
   contacts = not (dsbl & (1 << 4)) and m.nbody >= 2 and \
       bool(np.any((m.geom_contype != 0) | (m.geom_conaffinity != 0)))
-  friction = bool(np.any(m.dof_frictionloss > 0)) and not (dsbl & (1 << 2))
+  friction = (bool(np.any(m.dof_frictionloss > 0)) or
+              bool(np.any(np.asarray(m.tendon_frictionloss)[:m.ntendon] > 0))) and \
+      not (dsbl & (1 << 2))
   equality = m.sizes.get("neq", 0) > 0 and bool(np.any(m.eq_active0)) and not (dsbl & (1 << 1))
   if contacts or friction or equality:
     return "all"

@@ -3124,7 +3124,7 @@ MJH_HD void getimpedance(const double* solimp, double pos, double margin, double
   *impP = yP * sgn * (solimp[1]-solimp[0]) / solimp[2];
 }
 
-// mj_makeConstraint :2005-2116 with mj_instantiateFriction (dof), mj_instantiateLimit
+// mj_makeConstraint :2005-2116 with mj_instantiateFriction (dof, tendon), mj_instantiateLimit
 // :824-959 (dense), mj_diagApprox :1138-1311 and mj_makeImpedance :1494-1608 (dim-1 rows)
 // CONTACT = false compiles the contact code out (models whose contact capacity is 0); the
 // contact path's private arrays would otherwise cost every launch a scratch segment
@@ -3133,10 +3133,14 @@ MJH_HD void rowSolParam(const mjhipModel& m, int tp, int id, double solref[2],
                         double solimp[5]) {
   const double* sr = tp == CNSTR_LIMIT_JOINT ? m.jnt_solref + 2*id :
                      (tp == CNSTR_FRICTION_DOF ? m.dof_solref + 2*id :
-                      (tp == CNSTR_EQUALITY ? m.eq_solref + 2*id : m.tendon_solref_lim + 2*id));
+                      (tp == CNSTR_EQUALITY ? m.eq_solref + 2*id :
+                       (tp == CNSTR_FRICTION_TENDON ? m.tendon_solref_fri + 2*id :
+                        m.tendon_solref_lim + 2*id)));
   const double* si = tp == CNSTR_LIMIT_JOINT ? m.jnt_solimp + 5*id :
                      (tp == CNSTR_FRICTION_DOF ? m.dof_solimp + 5*id :
-                      (tp == CNSTR_EQUALITY ? m.eq_solimp + 5*id : m.tendon_solimp_lim + 5*id));
+                      (tp == CNSTR_EQUALITY ? m.eq_solimp + 5*id :
+                       (tp == CNSTR_FRICTION_TENDON ? m.tendon_solimp_fri + 5*id :
+                        m.tendon_solimp_lim + 5*id)));
   solref[0] = sr[0]; solref[1] = sr[1];
   for (int k = 0; k < 5; k++) solimp[k] = si[k];
 }
@@ -3686,6 +3690,14 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
         jacrow[i] = 1;
         added(addConstraint1(m, d, rc, jacrow, 0, 0, m.dof_frictionloss[i], CNSTR_FRICTION_DOF,
                              i, status), CNSTR_FRICTION_DOF, i, 0, 0, m.dof_frictionloss[i]);
+      }
+    }
+    // :801-815: tendon friction on the tendon's ten_J row (dropped when the row is empty)
+    for (int i = 0; i < m.ntendon; i++) {
+      if (m.tendon_frictionloss[i] > 0) {
+        added(addConstraint1(m, d, rc, d.ten_J + i*nv, 0, 0, m.tendon_frictionloss[i],
+                             CNSTR_FRICTION_TENDON, i, status),
+              CNSTR_FRICTION_TENDON, i, 0, 0, m.tendon_frictionloss[i]);
       }
     }
   }

@@ -274,6 +274,18 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
           rc.nf++;
         }
       }
+      // tendon friction (:801-815) on the ten_J row; mj_addConstraint drops an empty row
+      for (int i = 0; i < m.ntendon; i++) {
+        const double fl = m.tendon_frictionloss[i];
+        if (!(fl > 0)) continue;
+        mjh::SP<64> tj = d.ten_J + (long)i*nv;
+        bool nonempty = false;
+        for (int k = 0; k < nv && !nonempty; k++) nonempty = tj[k] != 0;
+        if (nonempty && addRow([&](int k) { return tj[k]; }, 0, 0, fl,
+                               mjh::CNSTR_FRICTION_TENDON, i)) {
+          rc.nf++;
+        }
+      }
     }
     if (!(dsbl & mjhipDSBL_LIMIT)) {
       for (int i = 0; i < m.njnt; i++) {

@@ -1246,6 +1246,9 @@ class MJCFCompiler:
     tmargin = arr("tendon_margin", nt, np.float64)
     tstiff = arr("tendon_stiffness", nt, np.float64)
     tdamp = arr("tendon_damping", nt, np.float64)
+    tfloss = arr("tendon_frictionloss", nt, np.float64)
+    tsolref_f = arr("tendon_solref_fri", (nt, 2), np.float64)
+    tsolimp_f = arr("tendon_solimp_fri", (nt, 5), np.float64)
     tls = arr("tendon_lengthspring", (nt, 2), np.float64)
     arr("tendon_length0", nt, np.float64)
     arr("tendon_invweight0", nt, np.float64)
@@ -1277,6 +1280,18 @@ class MJCFCompiler:
       tmargin[ti] = float(ta.get("margin", 0.0))
       tstiff[ti] = float(ta.get("stiffness", 0.0))
       tdamp[ti] = float(ta.get("damping", 0.0))
+      # friction loss (mj_instantiateFriction's FRICTION_TENDON rows) and its solver
+      # parameters, defaults as mjCTendon's (solreffriction / solimpfriction)
+      tfloss[ti] = float(ta.get("frictionloss", 0.0))
+      if tfloss[ti] < 0:
+        raise MJCFError(f"tendon '{ta.get('name', '')}' (id = {ti}): frictionloss must be "
+                        "nonnegative")
+      tsolref_f[ti] = _floats(ta["solreffriction"]) if "solreffriction" in ta else [0.02, 1.0]
+      si = [0.9, 0.95, 0.001, 0.5, 2.0]
+      if "solimpfriction" in ta:
+        v = _floats(ta["solimpfriction"])
+        si[:len(v)] = v
+      tsolimp_f[ti] = si
       sl = _floats(ta["springlength"]) if "springlength" in ta else [-1.0, -1.0]
       if len(sl) == 1:
         sl = [sl[0], sl[0]]

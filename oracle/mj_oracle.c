@@ -2880,6 +2880,9 @@ int or_efcCapacity(const mjhipModel* m) {
   for (int i = 0; i < m->nv; i++) {
     if (m->dof_frictionloss[i] > 0) n++;
   }
+  for (int i = 0; i < m->ntendon; i++) {
+    if (m->tendon_frictionloss[i] > 0) n++;
+  }
   for (int i = 0; i < m->neq; i++) {
     int t = m->eq_type[i];
     n += t == mjhipEQ_CONNECT ? 3 : (t == mjhipEQ_WELD ? 6 : 1);
@@ -3196,16 +3199,22 @@ static void or_instantiateEquality(const mjhipModel* m, mjhipData* d, orEfc* e) 
   free(jac0); free(jac1); free(jacdif); free(jt0); free(jt1);
 }
 
-/* mj_instantiateFriction :768-822, dof friction (dense) */
+/* mj_instantiateFriction :768-822 (dense): dof friction, then tendon friction on the
+   tendon's ten_J row (mj_addConstraint skips a row whose Jacobian is all zero) */
 static void or_instantiateFriction(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum* jac) {
   int nv = m->nv;
-  (void)d;
   if (mjDISABLED(mjhipDSBL_FRICTIONLOSS)) return;
   for (int i = 0; i < nv; i++) {
     if (m->dof_frictionloss[i] > 0) {
       mju_zero(jac, nv);
       jac[i] = 1;
       mj_addConstraint(m, e, jac, 0, 0, m->dof_frictionloss[i], 1, orCNSTR_FRICTION_DOF, i);
+    }
+  }
+  for (int i = 0; i < m->ntendon; i++) {
+    if (m->tendon_frictionloss[i] > 0) {
+      mj_addConstraint(m, e, d->ten_J + i*nv, 0, 0, m->tendon_frictionloss[i], 1,
+                       orCNSTR_FRICTION_TENDON, i);
     }
   }
 }
@@ -3350,6 +3359,7 @@ static void or_diagApprox(const mjhipModel* m, orEfc* e) {
     case orCNSTR_LIMIT_JOINT:
       e->efc_diagApprox[i] = m->dof_invweight0[m->jnt_dofadr[id]];
       break;
+    case orCNSTR_FRICTION_TENDON:
     case orCNSTR_LIMIT_TENDON:
       e->efc_diagApprox[i] = m->tendon_invweight0[id];
       break;
@@ -3410,6 +3420,10 @@ static void getsolparam(const mjhipModel* m, const orEfc* e, int i, mjtNum* solr
   case orCNSTR_LIMIT_TENDON:
     mju_copy(solref, m->tendon_solref_lim+2*id, 2);
     mju_copy(solimp, m->tendon_solimp_lim+5*id, 5);
+    break;
+  case orCNSTR_FRICTION_TENDON:
+    mju_copy(solref, m->tendon_solref_fri+2*id, 2);
+    mju_copy(solimp, m->tendon_solimp_fri+5*id, 5);
     break;
   }
   if ((solref[0] > 0) ^ (solref[1] > 0)) {   /* mixed format: default (0.02, 1) */

@@ -98,7 +98,6 @@ def test_options_survive(humanoid):
 
 
 @pytest.mark.parametrize("field,value,msg", [
-    ("tendon_frictionloss", 0.5, "tendon frictionloss"),
     ("geom_fluid", 1.0, "ellipsoid fluid"),
     ("wrap_type", 7, "unknown tendon wrap object type")])
 def test_unsupported_features_refused(humanoid, field, value, msg):

@@ -1,0 +1,54 @@
+"""Tendon friction rows on the MI355X vs the oracle: the generic kernel, the straight-line
+kernels with the cooperative constraint kernel (fixed tendons only: a run-time kernel) and
+the one-lane constraint kernel (MJHIP_COOP_LANES=0); row counts, types and ids exact,
+forces and qfrc_inverse within 1e-10."""
+import numpy as np
+import pytest
+
+from mujoco_inversedynamicstest_amd import engine, mjcf
+from mujoco_inversedynamicstest_amd.sampler import sample_states
+from oracle.oracle import Oracle
+
+from test_gpu import assert_close
+from test_tendon_friction_cpu import XML
+
+pytestmark = pytest.mark.gpu
+FIXED_ONLY = XML.replace('<spatial name="t3" frictionloss="0.3"><site site="s1"/><site site="s2"/>'
+                         '</spatial>', '')
+
+
+@pytest.mark.parametrize("xml,lanes,generic", [(XML, None, True), (FIXED_ONLY, None, False),
+                                               (FIXED_ONLY, "0", False),
+                                               (FIXED_ONLY, None, True)])
+def test_tendon_friction_parity(xml, lanes, generic, monkeypatch):
+  if lanes is not None:
+    monkeypatch.setenv("MJHIP_COOP_LANES", lanes)
+  m = mjcf.load_xml_string(xml)
+  B = 1024
+  q, v, a = sample_states(m, B, first=9)
+  a = a * np.where(np.arange(B) % 3 == 0, 1e-4, np.where(np.arange(B) % 3 == 1, 1.0, 50.0))[:, None]
+  e = engine.InverseEngine(m, capacity=B)
+  if not generic and xml is FIXED_ONLY:
+    assert e.fast_kernel is not None
+  f, st = e.inverse(q, v, a, status=True, generic=generic)
+  assert (st == 0).all()
+  counts = e.field_int("efc_count", 0, B)
+  types = e.field_int("efc_type", 0, B)
+  ids = e.field_int("efc_id", 0, B)
+  force = e.field("efc_force", 0, B)
+  qc = e.field("qfrc_constraint", 0, B)
+  e.close()
+  o = Oracle(m)
+  ref_f, ref_qc = [], []
+  for i in range(B):
+    o.inverse(q[i], v[i], a[i])
+    n = o.efc.nefc
+    assert counts[i, 0] == n and counts[i, 2] == o.efc.nf
+    np.testing.assert_array_equal(types[i, :n], o.efc_field("efc_type"))
+    np.testing.assert_array_equal(ids[i, :n], o.efc_field("efc_id"))
+    fr = o.efc_field("efc_force")
+    assert np.abs(force[i, :n] - fr).max() <= 1e-10 * max(1.0, np.abs(fr).max())
+    ref_f.append(o.d.qfrc_inverse.copy())
+    ref_qc.append(o.d.qfrc_constraint.copy())
+  assert_close(f, np.array(ref_f), "qfrc_inverse")
+  assert_close(qc, np.array(ref_qc), "qfrc_constraint")
