@@ -268,6 +268,11 @@ def other_config(args):
   kernel_ms = eng.time_kernel(B, reps=max(args.steps, 10))
   ncon = eng.field_int("con_count", 0, B)[:, 0]
   nefc = eng.field_int("efc_count", 0, B)[:, 0]
+  # algorithmic bytes of one launch: B_eval per instance plus the rows and contacts this
+  # batch actually produced (engine.constraint_bytes)
+  base = engine.output_bytes_per_eval(m) * B
+  extra = engine.constraint_bytes(m, nefc.sum(), ncon.sum(), B)
+  achieved = (base + extra) / (kernel_ms * 1e-3) / 1e9
   rec = {"metric": "mj_inverse evals/sec, config 4 (contacts on)", "value": B / dt,
          "unit": "evals/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": dt * 1e3,
          "kernel_ms": kernel_ms, "dtype": "f64",
@@ -277,7 +282,16 @@ def other_config(args):
          "config": {"workload": f"{args.model} keyframe poses + noise, contacts on",
                     "batch": B},
          "ncon_hist": np.bincount(ncon).tolist(), "nefc_max": int(nefc.max()),
-         "nefc_mean": float(nefc.mean())}
+         "nefc_mean": float(nefc.mean()),
+         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
+                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                      "algorithmic_bytes_per_launch": base + extra,
+                      "bytes_detail": {"b_eval_per_instance": engine.output_bytes_per_eval(m),
+                                       "rows": int(nefc.sum()), "contacts": int(ncon.sum()),
+                                       "constraint_bytes": extra},
+                      "kernel_ms": kernel_ms,
+                      "kernel_ms_method": "HIP events on the context's stream around reps "
+                                          "back-to-back launches of every kernel of one call"}}
   print(json.dumps(rec), flush=True)
   eng.close()
 

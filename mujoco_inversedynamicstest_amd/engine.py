@@ -414,6 +414,16 @@ def output_bytes_per_eval(model) -> int:
   return 8 * (fields.input_doubles(model.sizes) + fields.output_doubles(model.sizes))
 
 
+def constraint_bytes(model, nefc_total: int, ncon_total: int, B: int) -> int:
+  """Algorithmic bytes the constraint part of B evaluations writes on top of B_eval: per row
+  the efc_* arrays of MJHIP_DATA_EFC (nv + 13 doubles: J, pos, margin, frictionloss,
+  diagApprox, KBIP[4], D, R, vel, aref, force; 3 ints: type, id, state), per contact the
+  con_* arrays of MJHIP_DATA_CON (29 doubles, 5 ints), per instance its 4 count words."""
+  row = 8 * (model.nv + 13) + 4 * 3
+  con = 8 * 29 + 4 * 5
+  return row * int(nefc_total) + con * int(ncon_total) + 16 * int(B)
+
+
 # ---------------------------------------------------------------- single-instance drop-ins
 # The model struct is rebuilt per call (its option block is a copy), so edits of the Model
 # between calls are seen; the library caches device state by the model's content.
