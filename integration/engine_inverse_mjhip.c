@@ -7,7 +7,7 @@
  * shapes, so the views below are plain pointer copies generated from the same X-macro
  * tables (include/mjhip_fields.h); a name or type mismatch with mjModel/mjData is a
  * compile error (tests/test_integration.py compiles this file against the reference's
- * public headers).
+ * public headers, tests/test_adapter_exec.py runs it on real mjModel/mjData structs).
  *
  * Constraint rows and contacts. The reference keeps them in the mjData arena: mj_collision
  * resets it and lays the contacts at its start (engine_collision_driver.c:265-285), and
@@ -20,8 +20,7 @@
  * included (rules of engine_core_constraint.c:668-671, :811-814, :949-952).
  *
  * Models are checked for features the device path does not implement and which mjhipModel
- * does not carry (tendon friction loss, the ellipsoid fluid model, explicit contact pairs,
- * flexes, plugins): such a model is an mju_error, never a silently different result.
+ * does not carry (the ellipsoid fluid model, explicit contact pairs, flexes, plugins): such a model is an mju_error, never a silently different result.
  *
  * Build (in the reference tree): drop engine_inverse.c from src/engine/CMakeLists.txt,
  * add this file, add <repo>/include to the include path and link libmjhip.so.
@@ -147,28 +146,25 @@ static void contacts_to_soa(const mjData* d, mjhipData* hd) {
   }
 }
 
-static void contacts_from_soa(const mjhipData* hd, mjContact* out, int ncon) {
-  for (int i = 0; i < ncon; i++) {
-    mjContact* c = out + i;
-    memset(c, 0, sizeof(*c));
-    c->dist = hd->con_dist[i];
-    memcpy(c->pos, hd->con_pos + 3*i, 3*sizeof(mjtNum));
-    memcpy(c->frame, hd->con_frame + 9*i, 9*sizeof(mjtNum));
-    c->includemargin = hd->con_includemargin[i];
-    memcpy(c->friction, hd->con_friction + 5*i, 5*sizeof(mjtNum));
-    memcpy(c->solref, hd->con_solref + 2*i, 2*sizeof(mjtNum));
-    memcpy(c->solreffriction, hd->con_solreffriction + 2*i, 2*sizeof(mjtNum));
-    memcpy(c->solimp, hd->con_solimp + 5*i, 5*sizeof(mjtNum));
-    c->mu = hd->con_mu[i];
-    c->dim = hd->con_dim[i];
-    c->geom[0] = c->geom1 = hd->con_geom[2*i];
-    c->geom[1] = c->geom2 = hd->con_geom[2*i+1];
-    c->flex[0] = c->flex[1] = -1;
-    c->elem[0] = c->elem[1] = -1;
-    c->vert[0] = c->vert[1] = -1;
-    c->exclude = hd->con_exclude[i];
-    c->efc_address = hd->con_efc_address[i];
-  }
+static void contact_from_soa(const mjhipData* hd, int i, mjContact* c) {
+  memset(c, 0, sizeof(*c));
+  c->dist = hd->con_dist[i];
+  memcpy(c->pos, hd->con_pos + 3*i, 3*sizeof(mjtNum));
+  memcpy(c->frame, hd->con_frame + 9*i, 9*sizeof(mjtNum));
+  c->includemargin = hd->con_includemargin[i];
+  memcpy(c->friction, hd->con_friction + 5*i, 5*sizeof(mjtNum));
+  memcpy(c->solref, hd->con_solref + 2*i, 2*sizeof(mjtNum));
+  memcpy(c->solreffriction, hd->con_solreffriction + 2*i, 2*sizeof(mjtNum));
+  memcpy(c->solimp, hd->con_solimp + 5*i, 5*sizeof(mjtNum));
+  c->mu = hd->con_mu[i];
+  c->dim = hd->con_dim[i];
+  c->geom[0] = c->geom1 = hd->con_geom[2*i];
+  c->geom[1] = c->geom2 = hd->con_geom[2*i+1];
+  c->flex[0] = c->flex[1] = -1;
+  c->elem[0] = c->elem[1] = -1;
+  c->vert[0] = c->vert[1] = -1;
+  c->exclude = hd->con_exclude[i];
+  c->efc_address = hd->con_efc_address[i];
 }
 
 /* carve the XE arrays of `rows` rows and/or the XC arrays of `cons` contacts out of one
@@ -227,51 +223,70 @@ static void view_new_rows(const mjModel* m, const mjhipModel* hm, mjData* d, Dat
   v->stage = stage_alloc(m, &v->hd, rows, cons, 1, 1);
 }
 
-/* d's arena as mj_collision + mj_makeConstraint leave it, filled from the staged rows */
-static void arena_from_rows(const mjModel* m, mjData* d, const mjhipData* hd) {
-  /* mj_collision: reset the arena, contacts at its start (engine_collision_driver.c:60, :274) */
-  d->parena = 0;
+/* mj_clearEfc (engine_io.h:156-163): every arena array invalidated, contacts kept at the
+ * arena start */
+static void clear_efc(mjData* d) {
 #define X(type, name, nr, nc) d->name = NULL;
   MJDATA_ARENA_POINTERS
 #undef X
-  d->nefc = d->ne = d->nf = d->nl = d->nJ = d->nA = 0;
+  d->nefc = 0;
   d->nisland = 0;
   d->contact = (mjContact*)d->arena;
+}
+
+/* d's arena as mj_collision + mj_makeConstraint leave it, filled from the staged rows */
+static void arena_from_rows(const mjModel* m, mjData* d, const mjhipData* hd) {
+  /* mj_collision: reset the arena and the efc arrays (engine_collision_driver.c:270-273) */
   d->ncon = 0;
-  if (hd->ncon) {
-    mjContact* c = (mjContact*)mj_arenaAllocByte(d, sizeof(mjContact)*hd->ncon,
-                                                 _Alignof(mjContact));
-    if (!c) {
-      mj_warning(d, mjWARN_CONTACTFULL, hd->ncon);
-      return;
+  d->parena = 0;
+  clear_efc(d);
+  d->ne = d->nf = d->nl = d->nJ = d->nA = 0;
+  /* mj_addContact (engine_core_constraint.c:234-260), one contact at a time at the arena
+   * start; one that does not fit (nconmax or the arena) is dropped with mjWARN_CONTACTFULL */
+  int dropped = 0;
+  for (int i = 0; i < hd->ncon; i++) {
+    mjContact* c = NULL;
+    if (m->nconmax == -1 || d->ncon < m->nconmax) {
+      d->parena = d->ncon * sizeof(mjContact);
+      c = (mjContact*)mj_arenaAllocByte(d, sizeof(mjContact), _Alignof(mjContact));
     }
-    contacts_from_soa(hd, c, hd->ncon);
-    d->contact = c;
-    d->ncon = hd->ncon;
+    if (!c) {
+      mj_warning(d, mjWARN_CONTACTFULL, d->ncon);
+      dropped++;
+      continue;
+    }
+    contact_from_soa(hd, i, c);
+    d->ncon++;
   }
-  d->maxuse_con = d->maxuse_con > d->ncon ? d->maxuse_con : d->ncon;
-  /* mj_makeConstraint's arenaAllocEfc (engine_core_constraint.c:50-80), dense Jacobian */
+  /* mj_makeConstraint (engine_core_constraint.c:2005-2075): sizes, then arenaAllocEfc
+   * (:50-80) with the dense Jacobian */
   if (m->opt.disableflags & mjDSBL_CONSTRAINT) return;
   const int nefc = hd->nefc;
-  d->nefc = nefc;
   d->nJ = nefc * m->nv;
+  d->nefc = nefc;
   d->parena = d->ncon * sizeof(mjContact);
+  /* the device made rows for every contact: with contacts dropped they are not the rows the
+   * reference would make, so the efc arrays are treated as not fitting either */
+  int ok = !dropped;
 #undef MJ_M
 #define MJ_M(n) m->n
 #undef MJ_D
 #define MJ_D(n) d->n
-#define X(type, name, nr, nc)                                                 \
-  d->name = mj_arenaAllocByte(d, sizeof(type) * (nr) * (nc), _Alignof(type)); \
-  if (!d->name) {                                                             \
-    mj_warning(d, mjWARN_CNSTRFULL, (int)d->narena);                          \
-    d->nefc = d->nJ = 0;                                                      \
-    d->parena = d->ncon * sizeof(mjContact);                                  \
-    return;                                                                   \
+#define X(type, name, nr, nc)                                                   \
+  if (ok) {                                                                     \
+    d->name = mj_arenaAllocByte(d, sizeof(type) * (nr) * (nc), _Alignof(type)); \
+    if (!d->name) ok = 0;                                                       \
   }
   MJDATA_ARENA_POINTERS_SOLVER
 #undef X
 #undef MJ_D
 #define MJ_D(n) n
+  if (!ok) {
+    mj_warning(d, mjWARN_CNSTRFULL, (int)d->narena);
+    clear_efc(d);
+    d->parena = d->ncon * sizeof(mjContact);
+    return;
+  }
   d->ne = hd->ne;
   d->nf = hd->nf;
   d->nl = hd->nl;
@@ -280,6 +295,7 @@ static void arena_from_rows(const mjModel* m, mjData* d, const mjhipData* hd) {
 #undef XE
 #undef MJ_M
 #define MJ_M(n) n
+  d->maxuse_con = d->maxuse_con > d->ncon ? d->maxuse_con : d->ncon;
   d->maxuse_efc = d->maxuse_efc > nefc ? d->maxuse_efc : nefc;
   /* tendon_efcadr: tendon equalities record the equality id, tendon friction and limit rows
    * their first row (engine_core_constraint.c:668-671, :811-814, :949-952) */

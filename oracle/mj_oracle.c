@@ -3665,7 +3665,7 @@ static void or_fwdVelocity(const mjhipModel* m, mjhipData* d, orEfc* e) {
 }
 
 /* engine_inverse.c:37-68 (mj_collision: no contacts in the supported subset) */
-static void or_invPosition(const mjhipModel* m, mjhipData* d, orEfc* e) {
+void or_invPosition(const mjhipModel* m, mjhipData* d, orEfc* e) {
   or_kinematics(m, d);
   or_comPos(m, d);
   or_camlight(m, d);
@@ -3677,8 +3677,13 @@ static void or_invPosition(const mjhipModel* m, mjhipData* d, orEfc* e) {
   or_transmission(m, d, e);
 }
 
+/* engine_inverse.c:73-76 */
+void or_invVelocity(const mjhipModel* m, mjhipData* d, orEfc* e) {
+  or_fwdVelocity(m, d, e);
+}
+
 /* engine_inverse.c:169-192 */
-static void or_invConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
+void or_invConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
   int nefc = e->nefc;
   if (!nefc) {
     mju_zero(d->qfrc_constraint, m->nv);

@@ -76,6 +76,11 @@ void or_inverseSkip(const mjhipModel* m, mjhipData* d, orEfc* efc, int skipstage
                     int skipsensor);
 void or_inverse(const mjhipModel* m, mjhipData* d, orEfc* efc);
 
+/* the stage functions of mj_inverseSkip (engine_inverse.c:37-68, :73-76, :169-192) */
+void or_invPosition(const mjhipModel* m, mjhipData* d, orEfc* efc);
+void or_invVelocity(const mjhipModel* m, mjhipData* d, orEfc* efc);
+void or_invConstraint(const mjhipModel* m, mjhipData* d, orEfc* efc);
+
 /* individual stages, exported for the pin tests */
 void or_kinematics(const mjhipModel* m, mjhipData* d);
 void or_comPos(const mjhipModel* m, mjhipData* d);
