@@ -20,7 +20,8 @@
  * included (rules of engine_core_constraint.c:668-671, :811-814, :949-952).
  *
  * Models are checked for features the device path does not implement and which mjhipModel
- * does not carry (the ellipsoid fluid model, explicit contact pairs, flexes, plugins): such a model is an mju_error, never a silently different result.
+ * does not carry (the ellipsoid fluid model, explicit contact pairs, flexes, plugins):
+ * such a model is an mju_error, never a silently different result.
  *
  * Build (in the reference tree): drop engine_inverse.c from src/engine/CMakeLists.txt,
  * add this file, add <repo>/include to the include path and link libmjhip.so.
