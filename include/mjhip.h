@@ -174,11 +174,13 @@ typedef struct mjhipOption_ {
   mjtNum o_solref[mjhipNREF];
   mjtNum o_solimp[mjhipNIMP];
   mjtNum o_friction[5];
+  mjtNum ccd_tolerance;      /* convex collision solver tolerance (mjOption ccd_tolerance) */
   int integrator;
   int cone;
   int jacobian;
   int disableflags;
   int enableflags;
+  int ccd_iterations;        /* convex collision solver iterations (mjOption ccd_iterations) */
 } mjhipOption;
 
 /*---------------------------- model: sizes + field pointers ------------------------------*/

@@ -15,8 +15,8 @@
  * when it passes the static rules below. mj_collision processes candidates in signature
  * order ((b1 << 16) + b2, b1 < b2); mjhip_pairMaxContacts bounds each primitive pair.
  *
- * A candidate pair whose collision function is not implemented here (the convex pairs
- * mjc_Convex serves, ellipsoids) adds no capacity. At run time it goes through the
+ * A candidate pair whose collision function is not implemented here (meshes, height fields,
+ * SDFs; mjc_Convex with the libccd fallback or MULTICCD) adds no capacity. At run time it goes through the
  * same bitmask and bounding-sphere filters as the reference (mj_collideGeoms :1470-1497);
  * an instance where one survives them is flagged MJHIP_INST_UNSUPPORTED instead of getting
  * contacts, so every unflagged instance is exact.
@@ -83,10 +83,35 @@ MJHIP_CONTACT_HD int mjhip_bodyPairCandidate(const mjhipModel* m, int b1, int b2
   return 1;
 }
 
-/* contacts a (type-ordered t1 <= t2) geom pair can produce with the primitives implemented
+/* pairs mjCOLLISIONFUNC serves with mjc_Convex (engine_collision_driver.c:41-52) among the
+ * geom types built here: sphere-ellipsoid, capsule-ellipsoid/cylinder, ellipsoid and cylinder
+ * pairs among themselves and with boxes (type-ordered t1 <= t2) */
+MJHIP_CONTACT_HD int mjhip_isConvexPair(int t1, int t2) {
+  if (t1 == mjhipGEOM_PLANE || t1 == mjhipGEOM_HFIELD) return 0;
+  if (t2 == mjhipGEOM_ELLIPSOID) return 1;
+  if (t2 == mjhipGEOM_CYLINDER) {
+    return t1 == mjhipGEOM_CAPSULE || t1 == mjhipGEOM_ELLIPSOID || t1 == mjhipGEOM_CYLINDER;
+  }
+  if (t2 == mjhipGEOM_BOX) return t1 == mjhipGEOM_ELLIPSOID || t1 == mjhipGEOM_CYLINDER;
+  return 0;
+}
+
+/* contacts a (type-ordered t1 <= t2) geom pair can produce with the functions implemented
  * here: 0 = no collision function in the reference table, -1 = a reference collision
- * function that this engine does not implement */
-MJHIP_CONTACT_HD int mjhip_pairMaxContacts(int t1, int t2) {
+ * function that this engine does not implement. mjc_Convex runs the native GJK/EPA solver
+ * for one contact (mjc_CCDIteration, engine_collision_convex.c:792-819); with the libccd MPR
+ * fallback (mjDSBL_NATIVECCD) or MULTICCD's perturbed extra contacts (pairs without a
+ * sphere or an ellipsoid, :936-999) it is not built here. */
+MJHIP_CONTACT_HD int mjhip_pairMaxContacts(const mjhipModel* m, int t1, int t2) {
+  if (mjhip_isConvexPair(t1, t2)) {
+    if (m->opt.disableflags & mjhipDSBL_NATIVECCD) return -1;
+    if ((m->opt.enableflags & mjhipENBL_MULTICCD) && t1 != mjhipGEOM_SPHERE &&
+        t1 != mjhipGEOM_ELLIPSOID && t2 != mjhipGEOM_ELLIPSOID) {
+      return -1;
+    }
+    return 1;
+  }
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_ELLIPSOID) return 1;   /* mjc_PlaneConvex */
   if (t1 == mjhipGEOM_PLANE && t2 <= mjhipGEOM_HFIELD) return 0;
   if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) return 1;
   if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CAPSULE) return 2;
@@ -136,7 +161,7 @@ MJHIP_CONTACT_HD int mjhip_contactCapacity(const mjhipModel* m, int* rows) {
         for (int j = 0; j < m->body_geomnum[b2]; j++) {
           int g1 = m->body_geomadr[b1] + i, g2 = m->body_geomadr[b2] + j;
           if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
-          int k = mjhip_pairMaxContacts(m->geom_type[g1], m->geom_type[g2]);
+          int k = mjhip_pairMaxContacts(m, m->geom_type[g1], m->geom_type[g2]);
           if (k == 0) continue;
           if (mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
                                   m->geom_contype[g2], m->geom_conaffinity[g2])) {

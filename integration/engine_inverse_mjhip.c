@@ -71,6 +71,8 @@ static void model_view(const mjModel* m, const mjData* d, mjhipModel* hm) {
   memcpy(hm->opt.o_solref, m->opt.o_solref, sizeof(hm->opt.o_solref));
   memcpy(hm->opt.o_solimp, m->opt.o_solimp, sizeof(hm->opt.o_solimp));
   memcpy(hm->opt.o_friction, m->opt.o_friction, sizeof(hm->opt.o_friction));
+  hm->opt.ccd_tolerance = m->opt.ccd_tolerance;
+  hm->opt.ccd_iterations = m->opt.ccd_iterations;
   hm->opt.integrator = m->opt.integrator;
   hm->opt.cone = m->opt.cone;
   hm->opt.jacobian = m->opt.jacobian;

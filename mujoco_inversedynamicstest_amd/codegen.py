@@ -71,6 +71,12 @@ VA_RECOMPUTE = False
 # (tools/kernel_resources.py), and every spill reload waits for the store stream.
 QM_FORWARD = False
 LANES = {"pos": 64, "fac": 64, "va": 64}
+# k_all's workgroup: ALL_LANES lanes (64 = one instance block per wave; 32 = each block split
+# over two half-filled waves, so batch 65,536 is 2,048 waves) and the waves per SIMD it is
+# compiled for (__launch_bounds__'s second argument: 2 caps the kernel at 256 registers so
+# two waves share a SIMD)
+ALL_LANES = 64
+ALL_WAVES = 1
 
 
 def _ll(st):
@@ -124,12 +130,16 @@ def fast_path_supported(m) -> str | None:
   if m.opt["density"] > 0 or m.opt["viscosity"] > 0:
     return "fluid"
   for a in range(m.nu):
-    trn = m.actuator_trntype[a]
-    if trn == 3:                       # fixed tendon (spatial ones are rejected above)
-      continue
-    if trn not in (0, 1):
-      return "slider-crank, site or body transmissions"
+    if m.actuator_trntype[a] not in (0, 1, 2, 3, 4, 5):
+      return "unknown transmission"
   return None
+
+
+# transmissions the generated kernels leave to the pass after the constraint kernel
+# (mjh::transmissionAfter in k_sensors): slider-crank, site and body. Inverse dynamics does not
+# read actuators, so their actuator_length/moment/velocity can come last; a body transmission
+# needs the instance's contacts, which only the constraint kernel makes.
+TRN_AFTER = (2, 4, 5)
 
 
 def constraint_mode(m) -> str:
@@ -498,8 +508,10 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
       for k in range(nv):
         G.st("ten_J", t * nv + k, lit(J[k]))
   if m.nu:
-    E("// ---- mj_transmission (hinge/slide joint, fixed tendon)")
+    E("// ---- mj_transmission (hinge/slide/ball/free joint, fixed tendon)")
     for a in range(m.nu):
+      if int(m.actuator_trntype[a]) in TRN_AFTER:
+        continue                       # k_sensors' mjh::transmissionAfter
       jid = int(m.actuator_trnid[a, 0])
       g = float(m.actuator_gear[a, 0])
       adr = int(m.moment_rowadr[a])
@@ -895,6 +907,8 @@ def _gen_va(M: _Model, store_fields=None) -> str:
     for a in range(m.nu):
       adr, n = int(m.moment_rowadr[a]), int(m.moment_rownnz[a])
       g = float(m.actuator_gear[a, 0])
+      if int(m.actuator_trntype[a]) in TRN_AFTER:
+        continue                       # with its transmission, after the constraint kernel
       if m.actuator_trntype[a] == 3:   # mju_dotSparse over the tendon row's nonzeros
         if not n:
           G.st("actuator_velocity", a, "0.0")
@@ -1289,17 +1303,23 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   # previous one stored (a compiler memory barrier between them keeps the reloads), so the
   # live ranges stay those of the staged kernels; the reloads hit the wave's own freshly
   # written lines in L2, and no wave waits for the whole grid at a kernel boundary.
-  ntrig = max(1, 2 * len(M.trig) * 64)
-  nqo = 64 * max(M.nv, 1)
+  nl = ALL_LANES
+  if nl != 64:
+    assert all(LANES[st] == nl for st in STAGES), "stage LDS indexing must match ALL_LANES"
+  sub = 64 // nl
+  ntrig = max(1, 2 * len(M.trig) * nl)
+  nqo = nl * max(M.nv, 1)
   fuse_tail = ""
   if M.cmode != "all":
     fuse_tail = (f"  if (!qfrc_out) return;\n  __syncthreads();\n"
-                 f"  const long n = ((long)B - (long)blockIdx.x*64 < 64 ? "
-                 f"(long)B - (long)blockIdx.x*64 : 64) * {M.nv};\n"
-                 f"  double* dst = qfrc_out + (long)blockIdx.x*64*{M.nv};\n"
-                 f"  for (long r = threadIdx.x; r < n; r += 64) dst[r] = qo_lds[r];\n")
+                 f"  const long r0 = (long)blockIdx.x*{nl};\n"
+                 f"  const long n = ((long)B - r0 < {nl} ? (long)B - r0 : {nl}) * {M.nv};\n"
+                 f"  double* dst = qfrc_out + r0*{M.nv};\n"
+                 f"  for (long r = threadIdx.x; r < n; r += {nl}) dst[r] = qo_lds[r];\n")
+  bl = "blockIdx.x, threadIdx.x" if sub == 1 else \
+      f"blockIdx.x / {sub}, (blockIdx.x % {sub})*{nl} + threadIdx.x"
   linkage = 'extern "C" ' if extern_c else ""
-  out.append(f"""{linkage}__global__ __launch_bounds__(64, 1) void k_all_{name}(Mirror mr, int B,
+  out.append(f"""{linkage}__global__ __launch_bounds__({nl}, {ALL_WAVES}) void k_all_{name}(Mirror mr, int B,
     const double* __restrict__ qpos_in, const double* __restrict__ qvel_in,
     const double* __restrict__ qacc_in, double* __restrict__ qfrc_out, int* __restrict__ status,
     int* __restrict__ worklist, int* __restrict__ worklist_count, int* __restrict__ worklist_next,
@@ -1307,14 +1327,15 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   __shared__ double trig[{ntrig}];
   __shared__ double qo_lds[{nqo}];
   double qmr[{max(1, m.nM)}];
-""" + "\n".join(f"  fast_{st}_{name}(mr, blockIdx.x, threadIdx.x, B, {_SIG[st][1]});\n"
+""" + "\n".join(f"  fast_{st}_{name}(mr, {bl}, B, {_SIG[st][1]});\n"
                 f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE();" for st in STAGES)
              + "\n" + fuse_tail + "}")
   out.append(f"""static void launch_fast_{name}(dim3 g, dim3 b, hipStream_t s, const Mirror& mr,
     int B, const double* qpos_in, const double* qvel_in, const double* qacc_in, double* qfrc_out,
     int* status, int* worklist, int* worklist_count, int* worklist_next, int* efc_count) {{""")
   if FUSE:
-    out.append(f"  hipLaunchKernelGGL(k_all_{name}, g, b, 0, s, mr, B, qpos_in, qvel_in, qacc_in, "
+    gb = "g, b" if ALL_LANES == 64 else f"dim3(g.x*{64 // ALL_LANES}), dim3({ALL_LANES})"
+    out.append(f"  hipLaunchKernelGGL(k_all_{name}, {gb}, 0, s, mr, B, qpos_in, qvel_in, qacc_in, "
                f"qfrc_out, status, worklist, worklist_count, worklist_next, efc_count);")
   else:
     for st in STAGES:

@@ -84,6 +84,47 @@ MJH_HD int mjh_needSliderCrank(const mjhipModel* m) {
   }
   return 0;
 }
+// 1 when a candidate geom pair of the model runs mjc_Convex's native GJK/EPA solver: its
+// per-instance scratch (mjh::CcdMem) is allocated, 6 ccd_iterations + 6 faces
+MJH_HD int mjh_needConvex(const mjhipModel* m) {
+  if (!mjhip_contactsEnabled(m)) return 0;
+  for (int b1 = 0; b1 < m->nbody; b1++) {
+    for (int b2 = b1 + 1; b2 < m->nbody; b2++) {
+      if (!mjhip_bodyPairCandidate(m, b1, b2)) continue;
+      for (int i = 0; i < m->body_geomnum[b1]; i++) {
+        for (int j = 0; j < m->body_geomnum[b2]; j++) {
+          int g1 = m->body_geomadr[b1] + i, g2 = m->body_geomadr[b2] + j;
+          if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
+          const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+          if (mjhip_isConvexPair(t1, t2) && mjhip_pairMaxContacts(m, t1, t2) > 0 &&
+              !mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
+                                   m->geom_contype[g2], m->geom_conaffinity[g2])) {
+            return 1;
+          }
+        }
+      }
+    }
+  }
+  return 0;
+}
+MJH_HD int mjh_ccdFaceCap(const mjhipModel* m) { return 6*m->opt.ccd_iterations + 6; }
+MJH_HD int mjh_ccdDoubles(const mjhipModel* m) {
+  return mjh_needConvex(m) ? 72 + 9*(5 + m->opt.ccd_iterations) + 4*mjh_ccdFaceCap(m) : 0;
+}
+MJH_HD int mjh_ccdInts(const mjhipModel* m) {
+  return mjh_needConvex(m) ? 13*mjh_ccdFaceCap(m) : 0;
+}
+// transmissions the generated kernels leave to the pass after the constraint kernel
+// (mjh::transmissionAfter): slider-crank, site and body (adhesion) ones
+MJH_HD int mjh_trnAfter(int trn) {
+  return trn == mjhipTRN_SLIDERCRANK || trn == mjhipTRN_SITE || trn == mjhipTRN_BODY;
+}
+MJH_HD int mjh_needTrnAfter(const mjhipModel* m) {
+  for (int i = 0; i < m->nu; i++) {
+    if (mjh_trnAfter(m->actuator_trntype[i])) return 1;
+  }
+  return 0;
+}
 MJH_HD int mjh_needRnePost(const mjhipModel* m) {
   for (int i = 0; i < m->nsensor; i++) {
     const int t = m->sensor_type[i];
@@ -165,7 +206,8 @@ struct SP {
   XSC(con_solref, 2*con_cap)          \
   XSC(con_solreffriction, 2*con_cap)  \
   XSC(con_solimp, 5*con_cap)          \
-  XSC(con_mu, con_cap)
+  XSC(con_mu, con_cap)                \
+  XSC(ccd, mjh_ccdDoubles(m))         /* native convex solver (mjh::CcdMem) */
 
 #define MJHIP_SCRATCH_INT_FIELDS      \
   XSI(efc_type, efc_cap)              \
@@ -176,7 +218,8 @@ struct SP {
   XSI(con_dim, con_cap)               \
   XSI(con_geom, 2*con_cap)            \
   XSI(con_exclude, con_cap)           \
-  XSI(con_efc_address, con_cap)
+  XSI(con_efc_address, con_cap)       \
+  XSI(ccdi, mjh_ccdInts(m))
 
 template <int S>
 struct Lane {
@@ -1658,6 +1701,1033 @@ MJH_HD void boxBoxEmit(double margin, const double pos1[3], const double mat1[9]
   });
 }
 
+//---------------------------------- native convex collision ----------------------------------
+// mjc_Convex (engine_collision_convex.c:915-1001, mjENBL_MULTICCD off: one contact) and
+// mjc_PlaneConvex (:1045-1080, a geom without mesh data: the ellipsoid) on MuJoCo's native
+// GJK/EPA solver mjc_ccd (engine_collision_gjk.c:2215-2343). Everything the solver indexes at
+// run time lives in the instance's mirror scratch (d.ccd, d.ccdi, sized by mjh_ccdDoubles /
+// mjh_ccdInts), so the contact kernels keep no private arrays:
+//   d.ccd   [0, 36)     the GJK simplex, 4 vertices of 9 doubles (Minkowski point, witness on
+//                       geom 1, witness on geom 2)
+//           [36, 72)    the working simplex of gjkIntersect
+//           [72, ...)   the EPA polytope's vertices (5 + ccd_iterations), then per face its
+//                       origin projection and distance (4 doubles)
+//   d.ccdi  per face vi[3], adj[3] and its slot in the candidate list (-1 none, -2 deleted);
+//           the candidate list; the horizon's faces and edges; the horizon search's stack
+// The face capacity is 6 ccd_iterations + 6; the reference's is max(6 N, 1000), so a polytope
+// that would outgrow ours (never seen) flags the instance MJHIP_INST_UNSUPPORTED instead of
+// diverging. The arithmetic is the reference's, operation by operation.
+
+enum { CCD_POINT = 100, CCD_LINE = 101 };   // the shrunken sphere / capsule supports
+
+struct CcdShape {
+  int kind, gtype;                          // support in use, the geom's own type
+  double pos[3], mat[9], size[3], margin;
+};
+
+template <int S>
+struct CcdMem {
+  SP<S> x;                                  // d.ccd
+  SP<S, int> i;                             // d.ccdi
+  int nvmax, cap;                           // vertices, faces
+  MJH_HD SP<S> sim(int k) const { return x + 9*k; }
+  MJH_HD SP<S> wrk(int k) const { return x + 36 + 9*k; }
+  MJH_HD SP<S> vtx(int k) const { return x + 72 + 9*k; }
+  MJH_HD SP<S> fproj(int f) const { return x + 72 + 9*nvmax + 4*f; }
+  MJH_HD SP<S, int> fint(int f) const { return i + 7*f; }   // vi[0..2], adj[3..5], slot[6]
+  MJH_HD SP<S, int> list() const { return i + 7*cap; }
+  MJH_HD SP<S, int> hface() const { return i + 8*cap; }
+  MJH_HD SP<S, int> hedge() const { return i + 9*cap; }
+  MJH_HD SP<S, int> stack() const { return i + 10*cap; }
+};
+
+// mulMatTVec3 / localToGlobal (convex.c:122-141)
+MJH_HD void ccdToGlobal(double r[3], const double mat[9], const double t[3],
+                        const double pos[3]) {
+  r[0] = mat[0]*t[0] + mat[1]*t[1] + mat[2]*t[2];
+  r[1] = mat[3]*t[0] + mat[4]*t[1] + mat[5]*t[2];
+  r[2] = mat[6]*t[0] + mat[7]*t[1] + mat[8]*t[2];
+  r[0] += pos[0];
+  r[1] += pos[1];
+  r[2] += pos[2];
+}
+
+// the native support functions (convex.c:146-327), unit direction
+MJH_HD void ccdSupport1(double r[3], const CcdShape& s, const double dir[3]) {
+  if (s.kind == CCD_POINT) {
+    r[0] = s.pos[0]; r[1] = s.pos[1]; r[2] = s.pos[2];
+    return;
+  }
+  if (s.kind == mjhipGEOM_SPHERE) {
+    r[0] = s.size[0]*dir[0] + s.pos[0];
+    r[1] = s.size[0]*dir[1] + s.pos[1];
+    r[2] = s.size[0]*dir[2] + s.pos[2];
+    return;
+  }
+  double ld[3], t[3];
+  mulMatTVec3(ld, s.mat, dir);
+  if (s.kind == CCD_LINE) {
+    t[0] = 0;
+    t[1] = 0;
+    t[2] = ld[2] >= 0 ? s.size[1] : -s.size[1];
+  } else if (s.kind == mjhipGEOM_CAPSULE) {
+    t[0] = ld[0]*s.size[0];
+    t[1] = ld[1]*s.size[0];
+    t[2] = ld[2]*s.size[0];
+    t[2] += ld[2] >= 0 ? s.size[1] : -s.size[1];
+  } else if (s.kind == mjhipGEOM_ELLIPSOID) {
+    t[0] = ld[0]*s.size[0];
+    t[1] = ld[1]*s.size[1];
+    t[2] = ld[2]*s.size[2];
+    const double nrm = sqrt(t[0]*t[0] + t[1]*t[1] + t[2]*t[2]);
+    if (nrm < MINVAL) {
+      t[0] = s.size[0]; t[1] = 0; t[2] = 0;
+    } else {
+      const double inv = 1/nrm;
+      t[0] *= inv*s.size[0];
+      t[1] *= inv*s.size[1];
+      t[2] *= inv*s.size[2];
+    }
+  } else if (s.kind == mjhipGEOM_CYLINDER) {
+    double n = ld[0]*ld[0] + ld[1]*ld[1];
+    if (n > MINVAL*MINVAL) {
+      n = s.size[0] / sqrt(n);
+      t[0] = ld[0]*n;
+      t[1] = ld[1]*n;
+    } else {
+      t[0] = 0; t[1] = 0;
+    }
+    t[2] = (ld[2] < 0 ? -1.0 : (ld[2] > 0 ? 1.0 : 0.0))*s.size[1];
+  } else {                                  // box
+    t[0] = (ld[0] >= 0 ? 1.0 : -1.0)*s.size[0];
+    t[1] = (ld[1] >= 0 ? 1.0 : -1.0)*s.size[1];
+    t[2] = (ld[2] >= 0 ? 1.0 : -1.0)*s.size[2];
+  }
+  ccdToGlobal(r, s.mat, t, s.pos);
+}
+
+// support (gjk.c:277-296) into a 9-double vertex: each shape inflated by half its margin
+template <class V>
+MJH_HD void ccdSupport(V v, const CcdShape& a, const CcdShape& b, const double dir[3],
+                       const double ndir[3]) {
+  double p1[3], p2[3];
+  ccdSupport1(p1, a, dir);
+  if (a.margin > 0) {
+    const double h = 0.5*a.margin;
+    p1[0] += dir[0]*h; p1[1] += dir[1]*h; p1[2] += dir[2]*h;
+  }
+  ccdSupport1(p2, b, ndir);
+  if (b.margin > 0) {
+    const double h = 0.5*b.margin;
+    p2[0] += ndir[0]*h; p2[1] += ndir[1]*h; p2[2] += ndir[2]*h;
+  }
+  v[0] = p1[0] - p2[0]; v[1] = p1[1] - p2[1]; v[2] = p1[2] - p2[2];
+  v[3] = p1[0]; v[4] = p1[1]; v[5] = p1[2];
+  v[6] = p2[0]; v[7] = p2[1]; v[8] = p2[2];
+}
+
+template <class A, class B> MJH_HD void ccdCopyV(A dst, B src) {
+  for (int k = 0; k < 9; k++) dst[k] = src[k];
+}
+
+MJH_HD double ccdDet3(const double a[3], const double b[3], const double c[3]) {
+  return a[0]*(b[1]*c[2] - b[2]*c[1]) + a[1]*(b[2]*c[0] - b[0]*c[2])
+       + a[2]*(b[0]*c[1] - b[1]*c[0]);
+}
+
+MJH_HD int ccdSameSign(double a, double b) {
+  if (a > 0 && b > 0) return 1;
+  if (a < 0 && b < 0) return -1;
+  return 0;
+}
+
+// projectOriginPlane (gjk.c:482-515): 1 if the plane is degenerate
+MJH_HD int ccdProjPlane(double r[3], const double a[3], const double b[3], const double c[3]) {
+  double ba[3], ca[3], cb[3], n[3], nv, nn;
+  sub3(ba, b, a);
+  sub3(ca, c, a);
+  sub3(cb, c, b);
+  cross(n, cb, ba);
+  nv = dot3(n, b);
+  nn = dot3(n, n);
+  if (nn == 0) return 1;
+  if (nv != 0 && nn > MINVAL) {
+    scl3(r, n, nv / nn);
+    return 0;
+  }
+  cross(n, ba, ca);
+  nv = dot3(n, a);
+  nn = dot3(n, n);
+  if (nn == 0) return 1;
+  if (nv != 0 && nn > MINVAL) {
+    scl3(r, n, nv / nn);
+    return 0;
+  }
+  cross(n, ca, cb);
+  nv = dot3(n, c);
+  nn = dot3(n, n);
+  scl3(r, n, nv / nn);
+  return 0;
+}
+
+// S1D (gjk.c:787-814)
+MJH_HD void ccdS1D(double lam[2], const double a[3], const double b[3]) {
+  double d[3], p[3];
+  sub3(d, b, a);
+  const double s = -(dot3(b, d) / dot3(d, d));
+  p[0] = b[0] + s*d[0];
+  p[1] = b[1] + s*d[1];
+  p[2] = b[2] + s*d[2];
+  double mu = 0, pi = 0, bi = 0, ai = 0;
+  for (int i = 0; i < 3; i++) {
+    const double t = a[i] - b[i];
+    if (fabs(t) >= fabs(mu)) {
+      mu = t; pi = p[i]; bi = b[i]; ai = a[i];
+    }
+  }
+  const double c1 = pi - bi, c2 = ai - pi;
+  if (ccdSameSign(mu, c1) && ccdSameSign(mu, c2)) {
+    lam[0] = c1 / mu;
+    lam[1] = c2 / mu;
+  } else {
+    lam[0] = 0;
+    lam[1] = 1;
+  }
+}
+
+// minors M_14, M_24, M_34 and the two kept axes (gjk.c:667-714, :979-999); returns M_max
+MJH_HD double ccdAxes(const double a[3], const double b[3], const double c[3], int* x, int* y) {
+  const double M1 = b[1]*c[2] - b[2]*c[1] - a[1]*c[2] + a[2]*c[1] + a[1]*b[2] - a[2]*b[1];
+  const double M2 = b[0]*c[2] - b[2]*c[0] - a[0]*c[2] + a[2]*c[0] + a[0]*b[2] - a[2]*b[0];
+  const double M3 = b[0]*c[1] - b[1]*c[0] - a[0]*c[1] + a[1]*c[0] + a[0]*b[1] - a[1]*b[0];
+  const double m1 = fabs(M1), m2 = fabs(M2), m3 = fabs(M3);
+  if (m1 >= m2 && m1 >= m3) { *x = 1; *y = 2; return M1; }
+  if (m2 >= m3) { *x = 0; *y = 2; return M2; }
+  *x = 0; *y = 1;
+  return M3;
+}
+
+// signed area cofactor of (p, u, w) in the kept axes (gjk.c:722-731)
+MJH_HD double ccdArea(const double p[3], const double u[3], const double w[3], int x, int y) {
+  const double px = x == 0 ? p[0] : p[1], py = y == 1 ? p[1] : p[2];
+  const double ux = x == 0 ? u[0] : u[1], uy = y == 1 ? u[1] : u[2];
+  const double wx = x == 0 ? w[0] : w[1], wy = y == 1 ? w[1] : w[2];
+  return px*uy + py*wx + ux*wy - px*wy - py*ux - wx*uy;
+}
+
+// sum of c[k]*v_k, left to right (lincomb, gjk.c:453-477), for 2 or 3 points
+MJH_HD void ccdComb2(double r[3], const double l[2], const double a[3], const double b[3]) {
+  for (int k = 0; k < 3; k++) r[k] = l[0]*a[k] + l[1]*b[k];
+}
+MJH_HD void ccdComb3(double r[3], const double l[3], const double a[3], const double b[3],
+                     const double c[3]) {
+  for (int k = 0; k < 3; k++) r[k] = l[0]*a[k] + l[1]*b[k] + l[2]*c[k];
+}
+
+// S2D (gjk.c:653-783)
+MJH_HD void ccdS2D(double lam[3], const double a[3], const double b[3], const double c[3]) {
+  double p[3];
+  if (ccdProjPlane(p, a, b, c)) {
+    ccdS1D(lam, a, b);
+    lam[2] = 0;
+    return;
+  }
+  int x, y;
+  const double Mmax = ccdAxes(a, b, c, &x, &y);
+  const double C1 = ccdArea(p, b, c, x, y), C2 = ccdArea(p, c, a, x, y),
+               C3 = ccdArea(p, a, b, x, y);
+  const int k1 = ccdSameSign(Mmax, C1), k2 = ccdSameSign(Mmax, C2), k3 = ccdSameSign(Mmax, C3);
+  if (k1 && k2 && k3) {
+    lam[0] = C1 / Mmax;
+    lam[1] = C2 / Mmax;
+    lam[2] = C3 / Mmax;
+    return;
+  }
+  double dmin = mjhipMAXVAL, l[2], q[3], dd;
+  if (!k1) {
+    ccdS1D(l, b, c);
+    ccdComb2(q, l, b, c);
+    dd = dot3(q, q);
+    lam[0] = 0; lam[1] = l[0]; lam[2] = l[1];
+    dmin = dd;
+  }
+  if (!k2) {
+    ccdS1D(l, a, c);
+    ccdComb2(q, l, a, c);
+    dd = dot3(q, q);
+    if (dd < dmin) {
+      lam[0] = l[0]; lam[1] = 0; lam[2] = l[1];
+      dmin = dd;
+    }
+  }
+  if (!k3) {
+    ccdS1D(l, a, b);
+    ccdComb2(q, l, a, b);
+    dd = dot3(q, q);
+    if (dd < dmin) {
+      lam[0] = l[0]; lam[1] = l[1]; lam[2] = 0;
+    }
+  }
+}
+
+// S3D (gjk.c:560-649)
+MJH_HD void ccdS3D(double lam[4], const double a[3], const double b[3], const double c[3],
+                   const double e[3]) {
+  const double C1 = -ccdDet3(b, c, e), C2 = ccdDet3(a, c, e), C3 = -ccdDet3(a, b, e),
+               C4 = ccdDet3(a, b, c);
+  const double det = C1 + C2 + C3 + C4;
+  const int k1 = ccdSameSign(det, C1), k2 = ccdSameSign(det, C2), k3 = ccdSameSign(det, C3),
+            k4 = ccdSameSign(det, C4);
+  if (k1 && k2 && k3 && k4) {
+    lam[0] = C1 / det;
+    lam[1] = C2 / det;
+    lam[2] = C3 / det;
+    lam[3] = C4 / det;
+    return;
+  }
+  double dmin = mjhipMAXVAL, l[3], q[3], dd;
+  if (!k1) {
+    ccdS2D(l, b, c, e);
+    ccdComb3(q, l, b, c, e);
+    dd = dot3(q, q);
+    lam[0] = 0; lam[1] = l[0]; lam[2] = l[1]; lam[3] = l[2];
+    dmin = dd;
+  }
+  if (!k2) {
+    ccdS2D(l, a, c, e);
+    ccdComb3(q, l, a, c, e);
+    dd = dot3(q, q);
+    if (dd < dmin) {
+      lam[0] = l[0]; lam[1] = 0; lam[2] = l[1]; lam[3] = l[2];
+      dmin = dd;
+    }
+  }
+  if (!k3) {
+    ccdS2D(l, a, b, e);
+    ccdComb3(q, l, a, b, e);
+    dd = dot3(q, q);
+    if (dd < dmin) {
+      lam[0] = l[0]; lam[1] = l[1]; lam[2] = 0; lam[3] = l[2];
+      dmin = dd;
+    }
+  }
+  if (!k4) {
+    ccdS2D(l, a, b, c);
+    ccdComb3(q, l, a, b, c);
+    dd = dot3(q, q);
+    if (dd < dmin) {
+      lam[0] = l[0]; lam[1] = l[1]; lam[2] = l[2]; lam[3] = 0;
+    }
+  }
+}
+
+// the solver state of one mjc_ccd call (mjCCDStatus, gjk.h:70-89: the fields this path uses)
+struct CcdState {
+  double dist, x1[3], x2[3];
+  int nx, iters, nsimplex, kmax, unsupported;
+  double tol, cutoff;
+};
+
+template <class V> MJH_HD void ccdLoad3(double r[3], V v) { r[0] = v[0]; r[1] = v[1]; r[2] = v[2]; }
+
+// the face of 3 working-simplex vertices: unit normal and signed distance (gjk.c:375-388)
+template <int S>
+MJH_HD double ccdFaceDist(double n[3], SP<S> a, SP<S> b, SP<S> c) {
+  double va[3], vb[3], vc[3], d1[3], d2[3];
+  ccdLoad3(va, a); ccdLoad3(vb, b); ccdLoad3(vc, c);
+  sub3(d1, vc, va);
+  sub3(d2, vb, va);
+  cross(n, d1, d2);
+  double nn = dot3(n, n);
+  if (nn > MINVAL*MINVAL && nn < mjhipMAXVAL*mjhipMAXVAL) {
+    nn = 1/sqrt(nn);
+    scl3(n, n, nn);
+    return dot3(n, va);
+  }
+  return mjhipMAXVAL;
+}
+
+MJH_HD int ccdPick(int o0, int o1, int o2, int o3, int k) {
+  return k == 0 ? o0 : (k == 1 ? o1 : (k == 2 ? o2 : o3));
+}
+
+// gjkIntersect (gjk.c:393-448): 1 contact, 0 none, -1 inconclusive
+template <int S>
+MJH_HD int ccdIntersect(CcdState& st, const CcdMem<S>& M, const CcdShape& A, const CcdShape& B) {
+  for (int q = 0; q < 4; q++) ccdCopyV(M.wrk(q), M.sim(q));
+  int o0 = 0, o1 = 1, o2 = 2, o3 = 3;
+  int k = st.iters;
+  for (; k < st.kmax; k++) {
+    double n0[3], n1[3], n2[3], n3[3];
+    const double d0 = ccdFaceDist<S>(n0, M.wrk(o2), M.wrk(o1), M.wrk(o3));
+    const double d1 = ccdFaceDist<S>(n1, M.wrk(o0), M.wrk(o2), M.wrk(o3));
+    const double d2 = ccdFaceDist<S>(n2, M.wrk(o1), M.wrk(o0), M.wrk(o3));
+    const double d3 = ccdFaceDist<S>(n3, M.wrk(o0), M.wrk(o1), M.wrk(o2));
+    if (!d3 || !d2 || !d1 || !d0) {
+      st.iters = k;
+      return -1;
+    }
+    const int i = d0 < d1 ? 0 : 1, j = d2 < d3 ? 2 : 3;
+    const double di = i == 0 ? d0 : d1, dj = j == 2 ? d2 : d3;
+    const int w = di < dj ? i : j;
+    const double dw = di < dj ? di : dj;
+    if (dw > 0) {
+      st.nsimplex = 4;
+      for (int q = 0; q < 4; q++) ccdCopyV(M.sim(q), M.wrk(ccdPick(o0, o1, o2, o3, q)));
+      st.iters = k;
+      return 1;
+    }
+    double nw[3];
+    for (int c = 0; c < 3; c++) nw[c] = w == 0 ? n0[c] : (w == 1 ? n1[c] : (w == 2 ? n2[c] : n3[c]));
+    const double nd[3] = {-nw[0], -nw[1], -nw[2]};
+    SP<S> vw = M.wrk(ccdPick(o0, o1, o2, o3, w));
+    ccdSupport(vw, A, B, nw, nd);
+    if (nw[0]*vw[0] + nw[1]*vw[1] + nw[2]*vw[2] < 0) {
+      st.nsimplex = 0;
+      st.iters = k;
+      return 0;
+    }
+    // swap entries (w + 1) & 3 and (w + 2) & 3 of the order
+    const int a = (w + 1) & 3, b = (w + 2) & 3;
+    const int oa = ccdPick(o0, o1, o2, o3, a), ob = ccdPick(o0, o1, o2, o3, b);
+    o0 = a == 0 ? ob : (b == 0 ? oa : o0);
+    o1 = a == 1 ? ob : (b == 1 ? oa : o1);
+    o2 = a == 2 ? ob : (b == 2 ? oa : o2);
+    o3 = a == 3 ? ob : (b == 3 ? oa : o3);
+  }
+  st.iters = k;
+  return -1;
+}
+
+// gjk (gjk.c:163-272)
+template <int S>
+MJH_HD void ccdGjk(CcdState& st, const CcdMem<S>& M, const CcdShape& A, const CcdShape& B) {
+  const int get_dist = st.cutoff > 0;
+  int backup = !get_dist, n = 0, k = 0;
+  double x[3], l0 = 1, l1 = 0, l2 = 0, l3 = 0;
+  const double cut2 = st.cutoff*st.cutoff;
+  const bool discrete = A.margin == 0 && B.margin == 0 && A.gtype == mjhipGEOM_BOX &&
+                        B.gtype == mjhipGEOM_BOX;
+  const double eps = discrete ? 0 : st.tol*st.tol;
+  sub3(x, st.x1, st.x2);
+  for (; k < st.kmax; k++) {
+    double dir[3] = {-1, 0, 0}, ndir[3] = {1, 0, 0};     // gjkSupport (:301-323)
+    double nn = dot3(x, x);
+    if (nn > MINVAL*MINVAL) {
+      nn = 1/sqrt(nn);
+      scl3(ndir, x, nn);
+      scl3(dir, ndir, -1);
+    }
+    SP<S> vn = M.sim(n);
+    ccdSupport(vn, A, B, dir, ndir);
+    double sk[3], diff[3];
+    ccdLoad3(sk, vn);
+    sub3(diff, x, sk);
+    if (2*dot3(x, diff) < eps) {
+      if (!k) n = 1;
+      break;
+    }
+    if (!get_dist) {
+      if (dot3(x, sk) > 0) {
+        st.iters = k; st.nsimplex = 0; st.nx = 0; st.dist = mjhipMAXVAL;
+        return;
+      }
+    } else if (st.cutoff < mjhipMAXVAL) {
+      const double vs = dot3(x, sk), vv = dot3(x, x);
+      if (dot3(x, sk) > 0 && (vs*vs / vv) >= cut2) {
+        st.iters = k; st.nsimplex = 0; st.nx = 0; st.dist = mjhipMAXVAL;
+        return;
+      }
+    }
+    if (n == 3 && backup) {
+      st.iters = k;
+      const int r = ccdIntersect(st, M, A, B);
+      if (r != -1) {
+        st.nx = 0;
+        st.dist = r > 0 ? 0 : mjhipMAXVAL;
+        return;
+      }
+      k = st.iters;
+      backup = 0;
+    }
+    // subdistance (:544-556) on the n + 1 simplex vertices
+    double s0[3], s1[3], s2[3], s3[3], lam[4] = {0, 0, 0, 0};
+    ccdLoad3(s0, M.sim(0));
+    if (n + 1 >= 2) ccdLoad3(s1, M.sim(1));
+    if (n + 1 >= 3) ccdLoad3(s2, M.sim(2));
+    if (n + 1 == 4) ccdLoad3(s3, M.sim(3));
+    if (n + 1 == 4) ccdS3D(lam, s0, s1, s2, s3);
+    else if (n + 1 == 3) ccdS2D(lam, s0, s1, s2);
+    else if (n + 1 == 2) ccdS1D(lam, s0, s1);
+    else lam[0] = 1;
+    // drop the vertices with zero weight, in order
+    const double L[4] = {lam[0], lam[1], lam[2], lam[3]};
+    n = 0;
+    l0 = 0; l1 = 0; l2 = 0; l3 = 0;
+#pragma unroll
+    for (int i = 0; i < 4; i++) {
+      if (L[i] == 0) continue;
+      if (n != i) ccdCopyV(M.sim(n), M.sim(i));
+      l0 = n == 0 ? L[i] : l0;
+      l1 = n == 1 ? L[i] : l1;
+      l2 = n == 2 ? L[i] : l2;
+      l3 = n == 3 ? L[i] : l3;
+      n++;
+    }
+    // the next iterate (lincomb of the n kept vertices)
+    double nx[3];
+    for (int c = 0; c < 3; c++) {
+      double s = l0*M.sim(0)[c];
+      if (n > 1) s = s + l1*M.sim(1)[c];
+      if (n > 2) s = s + l2*M.sim(2)[c];
+      if (n > 3) s = s + l3*M.sim(3)[c];
+      nx[c] = s;
+    }
+    if (fabs(nx[0] - x[0]) < MINVAL && fabs(nx[1] - x[1]) < MINVAL &&
+        fabs(nx[2] - x[2]) < MINVAL) {
+      break;
+    }
+    copy3(x, nx);
+    if (n == 4) break;
+  }
+  // the witness points: lincomb of the kept vertices' witnesses
+  for (int c = 0; c < 3; c++) {
+    double s1v = l0*M.sim(0)[3 + c], s2v = l0*M.sim(0)[6 + c];
+    if (n > 1) { s1v = s1v + l1*M.sim(1)[3 + c]; s2v = s2v + l1*M.sim(1)[6 + c]; }
+    if (n > 2) { s1v = s1v + l2*M.sim(2)[3 + c]; s2v = s2v + l2*M.sim(2)[6 + c]; }
+    if (n > 3) { s1v = s1v + l3*M.sim(3)[3 + c]; s2v = s2v + l3*M.sim(3)[6 + c]; }
+    st.x1[c] = s1v;
+    st.x2[c] = s2v;
+  }
+  st.nx = 1;
+  st.iters = k;
+  st.nsimplex = n;
+  st.dist = sqrt(x[0]*x[0] + x[1]*x[1] + x[2]*x[2]);
+}
+
+//------------------------------------- EPA (gjk.c:820-1459) ----------------------------------
+
+// polytope bookkeeping kept in registers
+struct CcdPoly {
+  int nvtx, nface, nlist, nh;
+};
+
+template <int S>
+MJH_HD int ccdAddVertex(const CcdMem<S>& M, CcdPoly& P, SP<S> v) {
+  SP<S> t = M.vtx(P.nvtx);
+  for (int k = 3; k < 9; k++) t[k] = v[k];
+  t[0] = v[3] - v[6]; t[1] = v[4] - v[7]; t[2] = v[5] - v[8];
+  return P.nvtx++;
+}
+
+// epaSupport (:328-353)
+template <int S>
+MJH_HD int ccdNewVertex(const CcdMem<S>& M, CcdPoly& P, const CcdShape& A, const CcdShape& B,
+                        const double d[3], double dn) {
+  double dir[3] = {1, 0, 0}, ndir[3] = {-1, 0, 0};
+  if (dn > MINVAL) {
+    dir[0] = d[0] / dn;
+    dir[1] = d[1] / dn;
+    dir[2] = d[2] / dn;
+    scl3(ndir, dir, -1);
+  }
+  ccdSupport(M.vtx(P.nvtx), A, B, dir, ndir);
+  return P.nvtx++;
+}
+
+// attachFace (:1192-1213)
+template <int S>
+MJH_HD double ccdAttach(const CcdMem<S>& M, CcdPoly& P, int a, int b, int c, int j1, int j2,
+                        int j3) {
+  const int f = P.nface++;
+  SP<S, int> fi = M.fint(f);
+  fi[0] = a; fi[1] = b; fi[2] = c; fi[3] = j1; fi[4] = j2; fi[5] = j3;
+  double va[3], vb[3], vc[3], pr[3];
+  ccdLoad3(va, M.vtx(a)); ccdLoad3(vb, M.vtx(b)); ccdLoad3(vc, M.vtx(c));
+  if (ccdProjPlane(pr, vc, vb, va)) return 0;
+  SP<S> fp = M.fproj(f);
+  fp[0] = pr[0]; fp[1] = pr[1]; fp[2] = pr[2];
+  const double dist = sqrt(pr[0]*pr[0] + pr[1]*pr[1] + pr[2]*pr[2]);
+  fp[3] = dist;
+  fi[6] = -1;
+  return dist;
+}
+
+template <int S>
+MJH_HD void ccdListAll(const CcdMem<S>& M, CcdPoly& P, int n) {
+  for (int i = 0; i < n; i++) {
+    M.list()[i] = i;
+    M.fint(i)[6] = i;
+  }
+  P.nlist = n;
+}
+
+// replaceSimplex3 (:820-837)
+template <int S>
+MJH_HD void ccdToTriangle(const CcdMem<S>& M, CcdPoly& P, CcdState& st, int a, int b, int c) {
+  st.nsimplex = 3;
+  ccdCopyV(M.sim(0), M.vtx(a));
+  ccdCopyV(M.sim(1), M.vtx(b));
+  ccdCopyV(M.sim(2), M.vtx(c));
+  P.nface = 0;
+  P.nvtx = 0;
+}
+
+// sameSide / testTetra (:842-868)
+MJH_HD int ccdSameSide(const double p0[3], const double p1[3], const double p2[3],
+                       const double p3[3]) {
+  double e1[3], e2[3], e3[3], e4[3], n[3];
+  sub3(e1, p1, p0);
+  sub3(e2, p2, p0);
+  cross(n, e1, e2);
+  sub3(e3, p3, p0);
+  const double d1 = dot3(n, e3);
+  scl3(e4, p0, -1);
+  const double d2 = dot3(n, e4);
+  return (d1 > 0 && d2 > 0) || (d1 < 0 && d2 < 0);
+}
+
+MJH_HD int ccdInTetra(const double a[3], const double b[3], const double c[3],
+                      const double d[3]) {
+  return ccdSameSide(a, b, c, d) && ccdSameSide(b, c, d, a) && ccdSameSide(c, d, a, b) &&
+         ccdSameSide(d, a, b, c);
+}
+
+// triAffineCoord / triPointIntersect (:976-1035)
+MJH_HD void ccdAffine(double lam[3], const double a[3], const double b[3], const double c[3],
+                      const double p[3]) {
+  int x, y;
+  const double Mmax = ccdAxes(a, b, c, &x, &y);
+  lam[0] = ccdArea(p, b, c, x, y) / Mmax;
+  lam[1] = ccdArea(p, c, a, x, y) / Mmax;
+  lam[2] = ccdArea(p, a, b, x, y) / Mmax;
+}
+
+MJH_HD int ccdOnTriangle(const double a[3], const double b[3], const double c[3],
+                         const double p[3]) {
+  double lam[3], q[3], d[3];
+  ccdAffine(lam, a, b, c, p);
+  if (lam[0] < 0 || lam[1] < 0 || lam[2] < 0) return 0;
+  q[0] = a[0]*lam[0] + b[0]*lam[1] + c[0]*lam[2];
+  q[1] = a[1]*lam[0] + b[1]*lam[1] + c[1]*lam[2];
+  q[2] = a[2]*lam[0] + b[2]*lam[1] + c[2]*lam[2];
+  sub3(d, q, p);
+  return sqrt(d[0]*d[0] + d[1]*d[1] + d[2]*d[2]) < MINVAL;
+}
+
+// polytope3 (:1040-1117)
+template <int S>
+MJH_HD int ccdFromTriangle(const CcdMem<S>& M, CcdPoly& P, CcdState& st, const CcdShape& A,
+                           const CcdShape& B) {
+  double a[3], b[3], c[3], e1[3], e2[3], n[3], nn[3];
+  ccdLoad3(a, M.sim(0)); ccdLoad3(b, M.sim(1)); ccdLoad3(c, M.sim(2));
+  sub3(e1, b, a);
+  sub3(e2, c, a);
+  cross(n, e1, e2);
+  const double nrm = sqrt(n[0]*n[0] + n[1]*n[1] + n[2]*n[2]);
+  if (nrm < MINVAL) return 4;                           // mjEPA_P3_BAD_NORMAL
+  scl3(nn, n, -1);
+  const int i1 = ccdAddVertex(M, P, M.sim(0));
+  const int i2 = ccdAddVertex(M, P, M.sim(1));
+  const int i3 = ccdAddVertex(M, P, M.sim(2));
+  const int i5 = ccdNewVertex(M, P, A, B, nn, nrm);
+  const int i4 = ccdNewVertex(M, P, A, B, n, nrm);
+  double v4[3], v5[3];
+  ccdLoad3(v4, M.vtx(i4));
+  ccdLoad3(v5, M.vtx(i5));
+  if (ccdOnTriangle(a, b, c, v4)) return 5;            // mjEPA_P3_INVALID_V4
+  if (ccdOnTriangle(a, b, c, v5)) return 6;            // mjEPA_P3_INVALID_V5
+  if (st.dist > 10*MINVAL && !ccdInTetra(a, b, c, v4) && !ccdInTetra(a, b, c, v5)) return 7;
+  if (ccdAttach(M, P, i4, i1, i2, 1, 3, 2) < MINVAL) return 8;
+  if (ccdAttach(M, P, i4, i3, i1, 2, 4, 0) < MINVAL) return 8;
+  if (ccdAttach(M, P, i4, i2, i3, 0, 5, 1) < MINVAL) return 8;
+  if (ccdAttach(M, P, i5, i2, i1, 5, 0, 4) < MINVAL) return 8;
+  if (ccdAttach(M, P, i5, i1, i3, 3, 1, 5) < MINVAL) return 8;
+  if (ccdAttach(M, P, i5, i3, i2, 4, 2, 3) < MINVAL) return 8;   // mjEPA_P3_ORIGIN_ON_FACE
+  ccdListAll(M, P, 6);
+  return 0;
+}
+
+// polytope2 (:892-971)
+template <int S>
+MJH_HD int ccdFromSegment(const CcdMem<S>& M, CcdPoly& P, CcdState& st, const CcdShape& A,
+                          const CcdShape& B) {
+  double a[3], b[3], d[3];
+  ccdLoad3(a, M.sim(0)); ccdLoad3(b, M.sim(1));
+  sub3(d, b, a);
+  double best = mjhipMAXVAL;
+  int ix = 0;
+  for (int i = 0; i < 3; i++) {
+    if (fabs(d[i]) < best) {
+      best = fabs(d[i]);
+      ix = i;
+    }
+  }
+  double e[3] = {ix == 0 ? 1.0 : 0.0, ix == 1 ? 1.0 : 0.0, ix == 2 ? 1.0 : 0.0};
+  double d1[3], d2[3], d3[3], R[9];
+  cross(d1, e, d);
+  {                                                     // rotmat (:873-887): 120 degrees
+    const double n = sqrt(d[0]*d[0] + d[1]*d[1] + d[2]*d[2]);
+    const double u1 = d[0] / n, u2 = d[1] / n, u3 = d[2] / n;
+    const double sn = 0.86602540378, cs = -0.5;
+    R[0] = cs + u1*u1*(1 - cs);
+    R[1] = u1*u2*(1 - cs) - u3*sn;
+    R[2] = u1*u3*(1 - cs) + u2*sn;
+    R[3] = u2*u1*(1 - cs) + u3*sn;
+    R[4] = cs + u2*u2*(1 - cs);
+    R[5] = u2*u3*(1 - cs) - u1*sn;
+    R[6] = u1*u3*(1 - cs) - u2*sn;
+    R[7] = u2*u3*(1 - cs) + u1*sn;
+    R[8] = cs + u3*u3*(1 - cs);
+  }
+  mulMatVec3(d2, R, d1);
+  mulMatVec3(d3, R, d2);
+  const int i1 = ccdAddVertex(M, P, M.sim(0));
+  const int i2 = ccdAddVertex(M, P, M.sim(1));
+  const int i3 = ccdNewVertex(M, P, A, B, d1, sqrt(d1[0]*d1[0] + d1[1]*d1[1] + d1[2]*d1[2]));
+  const int i4 = ccdNewVertex(M, P, A, B, d2, sqrt(d2[0]*d2[0] + d2[1]*d2[1] + d2[2]*d2[2]));
+  const int i5 = ccdNewVertex(M, P, A, B, d3, sqrt(d3[0]*d3[0] + d3[1]*d3[1] + d3[2]*d3[2]));
+  // the hexahedron's faces (vertices, adjacent faces); a face through the origin makes the
+  // simplex that face's triangle
+  const int tv[6][3] = {{i1, i3, i4}, {i1, i5, i3}, {i1, i4, i5},
+                        {i2, i4, i3}, {i2, i3, i5}, {i2, i5, i4}};
+  const int ta[6][3] = {{1, 3, 2}, {2, 4, 0}, {0, 5, 1}, {5, 0, 4}, {3, 1, 5}, {4, 2, 3}};
+#pragma unroll
+  for (int f = 0; f < 6; f++) {
+    if (ccdAttach(M, P, tv[f][0], tv[f][1], tv[f][2], ta[f][0], ta[f][1], ta[f][2]) < MINVAL) {
+      ccdToTriangle(M, P, st, tv[f][0], tv[f][1], tv[f][2]);
+      return ccdFromTriangle(M, P, st, A, B);
+    }
+  }
+  double v1[3], v2[3], v3[3], v4[3], v5[3];
+  ccdLoad3(v1, M.vtx(i1)); ccdLoad3(v2, M.vtx(i2)); ccdLoad3(v3, M.vtx(i3));
+  ccdLoad3(v4, M.vtx(i4)); ccdLoad3(v5, M.vtx(i5));
+  if (st.dist > 10*MINVAL && !ccdInTetra(v1, v3, v4, v5) && !ccdInTetra(v2, v3, v4, v5)) {
+    return 2;                                           // mjEPA_P2_MISSING_ORIGIN
+  }
+  ccdListAll(M, P, 6);
+  return 0;
+}
+
+// polytope4 (:1122-1156)
+template <int S>
+MJH_HD int ccdFromTetra(const CcdMem<S>& M, CcdPoly& P, CcdState& st, const CcdShape& A,
+                        const CcdShape& B) {
+  const int i1 = ccdAddVertex(M, P, M.sim(0));
+  const int i2 = ccdAddVertex(M, P, M.sim(1));
+  const int i3 = ccdAddVertex(M, P, M.sim(2));
+  const int i4 = ccdAddVertex(M, P, M.sim(3));
+  const int tv[4][3] = {{i1, i2, i3}, {i1, i4, i2}, {i1, i3, i4}, {i4, i3, i2}};
+  const int ta[4][3] = {{1, 3, 2}, {2, 3, 0}, {0, 3, 1}, {2, 0, 1}};
+#pragma unroll
+  for (int f = 0; f < 4; f++) {
+    if (ccdAttach(M, P, tv[f][0], tv[f][1], tv[f][2], ta[f][0], ta[f][1], ta[f][2]) < MINVAL) {
+      ccdToTriangle(M, P, st, tv[f][0], tv[f][1], tv[f][2]);
+      return ccdFromTriangle(M, P, st, A, B);
+    }
+  }
+  double v1[3], v2[3], v3[3], v4[3];
+  ccdLoad3(v1, M.vtx(i1)); ccdLoad3(v2, M.vtx(i2)); ccdLoad3(v3, M.vtx(i3));
+  ccdLoad3(v4, M.vtx(i4));
+  if (!ccdInTetra(v1, v2, v3, v4)) return 9;            // mjEPA_P4_MISSING_ORIGIN
+  ccdListAll(M, P, 4);
+  return 0;
+}
+
+// deleteFace (:1174-1180)
+template <int S>
+MJH_HD void ccdUnlist(const CcdMem<S>& M, CcdPoly& P, int f) {
+  SP<S, int> fi = M.fint(f);
+  const int slot = fi[6];
+  if (slot >= 0) {
+    const int moved = M.list()[--P.nlist];
+    M.list()[slot] = moved;
+    M.fint(moved)[6] = slot;
+  }
+  fi[6] = -2;
+}
+
+template <int S>
+MJH_HD int ccdEdgeOf(const CcdMem<S>& M, int f, int v) {
+  SP<S, int> fi = M.fint(f);
+  if (fi[0] == v) return 0;
+  if (fi[1] == v) return 1;
+  return 2;
+}
+
+// whether face f sees w (horizonRec's test, :1247-1250)
+template <int S>
+MJH_HD bool ccdSees(const CcdMem<S>& M, int f, const double w[3]) {
+  SP<S> fp = M.fproj(f);
+  const double d2 = fp[3]*fp[3];
+  return fp[0]*w[0] + fp[1]*w[1] + fp[2]*w[2] >= d2;
+}
+
+// horizon (:1217-1295): the depth-first search of horizonRec with an explicit stack of
+// (face, entry edge, next k); a neighbour that does not see w is a horizon edge, one that
+// does is deleted and searched, in the recursion's order. false: more horizon edges than the
+// reference's horizon arrays hold, or the stack outgrew the face capacity
+template <int S>
+MJH_HD bool ccdHorizon(const CcdMem<S>& M, CcdPoly& P, int f0, const double w[3], int hmax) {
+  SP<S, int> stk = M.stack();
+  SP<S, int> hf = M.hface(), he = M.hedge();
+  ccdUnlist(M, P, f0);
+  for (int k0 = 0; k0 < 3; k0++) {
+    const int g = M.fint(f0)[3 + k0];
+    const int ge = ccdEdgeOf(M, g, M.fint(f0)[(k0 + 1) % 3]);
+    if (k0 > 0 && M.fint(g)[6] <= -2) continue;
+    if (!ccdSees(M, g, w)) {
+      if (P.nh >= hmax) return false;
+      hf[P.nh] = g; he[P.nh] = ge; P.nh++;
+      continue;
+    }
+    ccdUnlist(M, P, g);
+    int top = 0;
+    stk[0] = g; stk[1] = ge; stk[2] = 1;
+    while (top >= 0) {
+      SP<S, int> fr = stk + 3*top;
+      const int f = fr[0], e = fr[1], k = fr[2];
+      if (k == 3) {
+        top--;
+        continue;
+      }
+      fr[2] = k + 1;
+      const int i = (e + k) % 3;
+      const int h = M.fint(f)[3 + i];
+      if (M.fint(h)[6] > -2) {
+        const int hge = ccdEdgeOf(M, h, M.fint(f)[(i + 1) % 3]);
+        if (ccdSees(M, h, w)) {
+          ccdUnlist(M, P, h);
+          if (3*(top + 2) > 3*M.cap) return false;
+          top++;
+          SP<S, int> nf = stk + 3*top;
+          nf[0] = h; nf[1] = hge; nf[2] = 1;
+        } else {
+          if (P.nh >= hmax) return false;
+          hf[P.nh] = h; he[P.nh] = hge; P.nh++;
+        }
+      }
+    }
+  }
+  return true;
+}
+
+// epa (:1329-1459) + epaWitness (:1300-1323): the face closest to the origin, or -1
+template <int S>
+MJH_HD int ccdEpa(CcdState& st, const CcdMem<S>& M, CcdPoly& P, const CcdShape& A,
+                  const CcdShape& B) {
+  const double FLTMAX = 3.40282346638528859811704183484516925e+38;   // FLT_MAX
+  const int refmax = 6*st.kmax > 1000 ? 6*st.kmax : 1000;            // the reference's faces
+  double lower, upper = FLTMAX;
+  int f = -1, pf = -1, k;
+  P.nh = 0;
+  for (k = 0; k < st.kmax; k++) {
+    pf = f;
+    lower = FLTMAX;
+    for (int i = 0; i < P.nlist; i++) {
+      const int g = M.list()[i];
+      const double dg = M.fproj(g)[3];
+      if (dg < lower) {
+        f = g;
+        lower = dg;
+      }
+    }
+    if (lower > upper || f < 0) {
+      f = pf;
+      break;
+    }
+    if (lower <= 0) break;                              // origin on a face (a warning)
+    double fp[3], w[3];
+    ccdLoad3(fp, M.fproj(f));
+    if (P.nvtx >= M.nvmax) {                            // cannot happen: one per iteration
+      st.unsupported = 1;
+      return -1;
+    }
+    const int wi = ccdNewVertex(M, P, A, B, fp, lower);
+    ccdLoad3(w, M.vtx(wi));
+    const double up = (fp[0]*w[0] + fp[1]*w[1] + fp[2]*w[2]) / lower;
+    if (up < upper) upper = up;
+    if (upper - lower < st.tol) break;
+    if (!ccdHorizon(M, P, f, w, 6 + st.kmax)) {
+      st.unsupported = 1;
+      return -1;
+    }
+    if (P.nh < 3) {
+      f = -1;
+      break;
+    }
+    const int nf = P.nface, ne = P.nh;
+    if (ne > refmax - P.nface) break;                   // out of face memory (a warning)
+    if (ne > M.cap - P.nface) {                         // ours is smaller: not this engine's
+      st.unsupported = 1;
+      return -1;
+    }
+    for (int i = 0; i < ne; i++) {
+      const int cur = nf + i, prev = i ? cur - 1 : nf + ne - 1, next = nf + (i + 1) % ne;
+      const int hfi = M.hface()[i], e = M.hedge()[i];
+      SP<S, int> H = M.fint(hfi);
+      const int a = H[e], b = H[(e + 1) % 3];
+      H[3 + e] = cur;
+      const double dd = ccdAttach(M, P, wi, b, a, prev, hfi, next);
+      if (dd == 0) {
+        f = -1;
+        break;
+      }
+      if (dd >= lower && dd <= upper) {
+        const int s = P.nlist++;
+        M.list()[s] = P.nface - 1;
+        M.fint(P.nface - 1)[6] = s;
+      }
+    }
+    P.nh = 0;
+    if (!P.nlist || f < 0) break;
+  }
+  if (f >= 0) {
+    SP<S, int> F = M.fint(f);
+    double a[3], b[3], c[3], pr[3], lam[3];
+    ccdLoad3(a, M.vtx(F[0])); ccdLoad3(b, M.vtx(F[1])); ccdLoad3(c, M.vtx(F[2]));
+    ccdLoad3(pr, M.fproj(f));
+    ccdAffine(lam, a, b, c, pr);
+    SP<S> va = M.vtx(F[0]), vb = M.vtx(F[1]), vc = M.vtx(F[2]);
+    for (int i = 0; i < 3; i++) {
+      st.x1[i] = va[3 + i]*lam[0] + vb[3 + i]*lam[1] + vc[3 + i]*lam[2];
+      st.x2[i] = va[6 + i]*lam[0] + vb[6 + i]*lam[1] + vc[6 + i]*lam[2];
+    }
+    st.nx = 1;
+    st.dist = -M.fproj(f)[3];
+  } else {
+    st.nx = 0;
+    st.dist = 0;
+  }
+  return f;
+}
+
+// mjc_ccd (:2215-2343) with max_contacts = 1 and dist_cutoff = 0
+template <int S>
+MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B, int kmax,
+                     double tol) {
+  copy3(st.x1, A.pos);
+  copy3(st.x2, B.pos);
+  st.iters = 0;
+  st.tol = tol;
+  st.kmax = kmax;
+  st.cutoff = 0;
+  st.unsupported = 0;
+  const bool shrinkA = A.gtype == mjhipGEOM_SPHERE || A.gtype == mjhipGEOM_CAPSULE;
+  const bool shrinkB = B.gtype == mjhipGEOM_SPHERE || B.gtype == mjhipGEOM_CAPSULE;
+  if (shrinkA || shrinkB) {
+    double full1 = 0, full2 = 0;
+    const double m1 = A.margin, m2 = B.margin;
+    if (shrinkA) {
+      full1 = A.size[0] + 0.5*m1;
+      A.kind = A.gtype == mjhipGEOM_SPHERE ? CCD_POINT : CCD_LINE;
+      A.margin = 0;
+    }
+    if (shrinkB) {
+      full2 = B.size[0] + 0.5*m2;
+      B.kind = B.gtype == mjhipGEOM_SPHERE ? CCD_POINT : CCD_LINE;
+      B.margin = 0;
+    }
+    st.cutoff += full1 + full2;
+    ccdGjk(st, M, A, B);
+    st.cutoff = 0;
+    A.margin = m1;
+    B.margin = m2;
+    A.kind = A.gtype;
+    B.kind = B.gtype;
+    if (st.dist > st.tol) {                             // shallow: inflate (:2195-2210)
+      double n[3];
+      sub3(n, st.x2, st.x1);
+      normalize3(n);
+      if (full1) {
+        st.x1[0] += full1*n[0]; st.x1[1] += full1*n[1]; st.x1[2] += full1*n[2];
+      }
+      if (full2) {
+        st.x2[0] -= full2*n[0]; st.x2[1] -= full2*n[1]; st.x2[2] -= full2*n[2];
+      }
+      st.dist -= (full1 + full2);
+      if (st.dist > st.cutoff) st.dist = mjhipMAXVAL;
+      return st.dist;
+    }
+    st.iters = 0;
+    copy3(st.x1, A.pos);
+    copy3(st.x2, B.pos);
+  }
+  ccdGjk(st, M, A, B);
+  if (st.dist <= tol && st.nsimplex > 1) {
+    st.dist = 0;
+    CcdPoly P{0, 0, 0, 0};
+    const int ret = st.nsimplex == 2 ? ccdFromSegment(M, P, st, A, B) :
+                    st.nsimplex == 3 ? ccdFromTriangle(M, P, st, A, B) :
+                                       ccdFromTetra(M, P, st, A, B);
+    if (!ret) ccdEpa(st, M, P, A, B);
+  }
+  return st.dist;
+}
+
+template <int S>
+MJH_HD void ccdShape(CcdShape& s, const mjhipModel& m, const Lane<S>& d, int g, double margin) {
+  s.kind = s.gtype = m.geom_type[g];
+  for (int k = 0; k < 3; k++) s.pos[k] = d.geom_xpos[3*g + k];
+  for (int k = 0; k < 9; k++) s.mat[k] = d.geom_xmat[9*g + k];
+  for (int k = 0; k < 3; k++) s.size[k] = m.geom_size[3*g + k];
+  s.margin = margin;
+}
+
+// mjc_Convex through mjc_CCDIteration (convex.c:792-819, :915-1001): 0 or 1 contacts
+template <int S>
+MJH_HD int colConvex(RawContact& c, const mjhipModel& m, const Lane<S>& d, int g1, int g2,
+                     double margin, int* status) {
+  const int N = m.opt.ccd_iterations;
+  CcdMem<S> M{d.ccd, d.ccdi, 5 + N, mjh_ccdFaceCap(&m)};
+  CcdShape A, B;
+  ccdShape(A, m, d, g1, margin);
+  ccdShape(B, m, d, g2, margin);
+  CcdState st;
+  const double dist = ccdRun(st, M, A, B, N, m.opt.ccd_tolerance);
+  if (st.unsupported) {
+    *status |= MJHIP_INST_UNSUPPORTED;
+    return 0;
+  }
+  if (!(dist < 0) || st.nx < 1) return 0;
+  c.dist = margin + dist;
+  c.frame[0] = st.x1[0] - st.x2[0];
+  c.frame[1] = st.x1[1] - st.x2[1];
+  c.frame[2] = st.x1[2] - st.x2[2];
+  normalize3(c.frame);
+  c.pos[0] = 0.5*(st.x1[0] + st.x2[0]);
+  c.pos[1] = 0.5*(st.x1[1] + st.x2[1]);
+  c.pos[2] = 0.5*(st.x1[2] + st.x2[2]);
+  for (int k = 3; k < 9; k++) c.frame[k] = 0;
+  return 1;
+}
+
+// mjc_PlaneConvex (convex.c:1045-1080) for an ellipsoid: the libccd support (mjccd_support
+// :501-704) at -normal, object margin 0, one contact
+template <class P1, class M1, class P2, class M2>
+MJH_HD int colPlaneEllipsoid(RawContact& c, double margin, P1 pos1, M1 mat1, P2 pos2, M2 mat2,
+                             const double size[3]) {
+  const double normal[3] = {mat1[2], mat1[5], mat1[8]};
+  const double dir[3] = {-mat1[2], -mat1[5], -mat1[8]};
+  double ld[3], v[3], dif[3];
+  mulMatTVec3(ld, mat2, dir);
+  for (int i = 0; i < 3; i++) v[i] = ld[i]*size[i];
+  normalize3(v);
+  for (int i = 0; i < 3; i++) v[i] *= size[i];
+  for (int i = 0; i < 3; i++) v[i] += ld[i]*0.0/2;
+  mulMatVec3(v, mat2, v);
+  addTo3(v, pos2);
+  sub3(dif, v, pos1);
+  const double dist = dot3(normal, dif);
+  if (dist > margin) return 0;
+  c.dist = dist;
+  copy3(c.pos, v);
+  addToScl3(c.pos, normal, -0.5*dist);
+  copy3(c.frame, normal);
+  for (int k = 3; k < 9; k++) c.frame[k] = 0;
+  return 1;
+}
+
 // mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
 // WRITE = false only counts the contacts the pair produces (the cooperative constraint
 // kernel's first pass: it needs each pair's count to place the contacts in order)
@@ -1668,15 +2738,16 @@ MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, in
                                double margin, int& ncon, int* status, double* bbuf = nullptr);
 
 // mj_collideGeoms up to the narrowphase: type-orders (g1, g2), applies the static and
-// bounding-sphere filters and returns the raw contacts of a primitive pair in raw (<= 2,
-// with the pair's margin), 0 for none, or -1 for plane : box / cylinder, whose contacts
-// collidePlaneBoxCyl stores as it makes them
-template <int S>
+// bounding-sphere filters and returns the raw contacts of a primitive or convex pair in raw
+// (<= 2, with the pair's margin), 0 for none, or -1 for plane : box / cylinder, whose contacts
+// collidePlaneBoxCyl stores as it makes them. CONVEX = false (the cooperative kernel, which
+// no model with a convex pair launches) compiles the GJK/EPA path out.
+template <int S, bool CONVEX = true>
 MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
                        double& margin, RawContact raw[2], int* status) {
   if (m.geom_type[g1] > m.geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
-  const int kmax = mjhip_pairMaxContacts(t1, t2);
+  const int kmax = mjhip_pairMaxContacts(&m, t1, t2);
   if (kmax == 0) return 0;
   if (mjhip_filterBitmask(m.geom_contype[g1], m.geom_conaffinity[g1], m.geom_contype[g2],
                           m.geom_conaffinity[g2])) {
@@ -1695,6 +2766,17 @@ MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
   SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
   const double *size1 = m.geom_size + 3*g1, *size2 = m.geom_size + 3*g2;
+  if (mjhip_isConvexPair(t1, t2)) {
+    if constexpr (CONVEX) {
+      return colConvex(raw[0], m, d, g1, g2, margin, status);
+    } else {
+      *status |= MJHIP_INST_UNSUPPORTED;   // not reached: such models use one lane each
+      return 0;
+    }
+  }
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_ELLIPSOID) {
+    return colPlaneEllipsoid(raw[0], margin, pos1, mat1, pos2, mat2, size2);
+  }
   int num = 0;
   if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) {
     num = rawPlaneSphere(raw, margin, pos1, mat1, pos2, size2[0]);
@@ -2474,12 +3556,13 @@ MJH_HD void tendon(const mjhipModel& m, const Lane<S>& d) {
 
 // mj_transmission :865-916 (joint transmission of slide/hinge joints)
 template <int S>
-MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d) {
+MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d, bool after_only = false) {
   for (int i = 0; i < m.nu; i++) {
     int adr = m.moment_rowadr[i];
     int id = m.actuator_trnid[2*i];
     const double* gear = m.actuator_gear + 6*i;
     const int trn = m.actuator_trntype[i];
+    if (after_only && !mjh_trnAfter(trn)) continue;
     SP<S> moment = d.actuator_moment + adr;
     if (trn == mjhipTRN_JOINT || trn == mjhipTRN_JOINTINPARENT) {
       const int t = m.jnt_type[id];
@@ -5044,12 +6127,31 @@ MJH_HD int inverseSkip(const mjhipModel& m, const Lane<S>& d, int skipstage,
   return status;
 }
 
+// mj_transmission (engine_core_smooth.c:996-1318) of the slider-crank, site and body
+// actuators and their actuator_velocity (mj_fwdVelocity, engine_forward.c:214-219) after the
+// generated kernels and the constraint part. No other mj_inverse output reads them (the
+// inverse forces do not involve actuators), the sensors after this do, and a body
+// transmission reads this instance's contacts, which the constraint part made.
+template <int S>
+MJH_HD void transmissionAfter(const mjhipModel& m, const Lane<S>& d) {
+  transmission(m, d, true);
+  if (m.opt.disableflags & mjhipDSBL_ACTUATION) return;
+  for (int r = 0; r < m.nu; r++) {
+    if (!mjh_trnAfter(m.actuator_trntype[r])) continue;
+    const int adr = m.moment_rowadr[r];
+    d.actuator_velocity[r] = dotSparse(d.actuator_moment + adr, d.qvel, m.moment_rownnz[r],
+                                       m.moment_colind + adr);
+  }
+}
+
 // mj_sensorPos/Vel/Acc and mj_energyPos/Vel of mj_inverseSkip(mjSTAGE_NONE) after the
 // generated kernels and the constraint part, in the reference's order: every sensor and
 // energy term reads only its own stage's fields, which no later stage rewrites, and none
 // reads qfrc_inverse, so running them after the whole pass gives the reference's values
 template <int S>
-MJH_HD void sensorsAfter(const mjhipModel& m, const Lane<S>& d, bool sensors = true) {
+MJH_HD void sensorsAfter(const mjhipModel& m, const Lane<S>& d, bool sensors = true,
+                         bool trn = false) {
+  if (trn) transmissionAfter(m, d);
   sensors = sensors && m.nsensor > 0;
   const bool energy = (m.opt.enableflags & mjhipENBL_ENERGY) != 0;
   if (sensors) sensorPos(m, d);

@@ -1,0 +1,22 @@
+// fast_kernels.h — the registry entry of a straight-line (model-specialized) kernel, shared by
+// mjhip.hip and gen_fast.hip (the bundled models' kernels, a translation unit of their own so
+// the two compile in parallel).
+#ifndef MJHIP_FAST_KERNELS_H_
+#define MJHIP_FAST_KERNELS_H_
+
+#include <hip/hip_runtime.h>
+
+#include "engine_device.h"
+
+struct FastKernelEntry {
+  unsigned long long sig;
+  void (*launch)(dim3, dim3, hipStream_t, const Mirror&, int, const double*, const double*,
+                 const double*, double*, int*, int*, int*, int*, int*);
+  const char* name;
+  int cmode;   // codegen.constraint_mode: 0 none, 1 work-list, 2 every instance
+};
+
+// the bundled models' kernels (gen_fast.hip), terminated by an entry with launch = nullptr
+const FastKernelEntry* mjhip_fastKernels();
+
+#endif  // MJHIP_FAST_KERNELS_H_

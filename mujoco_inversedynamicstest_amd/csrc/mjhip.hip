@@ -24,27 +24,16 @@
 #include <vector>
 
 #include "engine_device.h"
+#include "fast_kernels.h"
 
 using mjh::Lane;
 using mjh::SP;
 
 //==================================== kernels ===============================================
 
-// Straight-line kernels generated per bundled model by codegen.py (build()), selected by
-// model signature; each appends limit-active instances to a work-list that k_inverse_list
-// then recomputes with the generic pipeline.
-struct FastKernelEntry {
-  unsigned long long sig;
-  void (*launch)(dim3, dim3, hipStream_t, const Mirror&, int, const double*, const double*,
-                 const double*, double*, int*, int*, int*, int*, int*);
-  const char* name;
-  int cmode;   // codegen.constraint_mode: 0 none, 1 work-list, 2 every instance
-};
-#if __has_include("gen_fast.inc")
-#include "gen_fast.inc"
-#else
-static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr, 0}};
-#endif
+// Straight-line kernels generated per bundled model by codegen.py (build(), gen_fast.hip),
+// selected by model signature (mjhip_fastKernels); each appends limit-active instances to a
+// work-list that the constraint kernel then serves.
 
 // generic pipeline over the instances of a work-list (limit-active instances of the fast
 // path); grid = ceil(B/64) blocks, threads past *count exit at once
@@ -211,7 +200,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         const int2 pr = pairs[p];
         g1 = pr.x;
         g2 = pr.y;
-        num = mjh::narrowGeoms<64>(m, d, g1, g2, margin, raw, &st);
+        num = mjh::narrowGeoms<64, false>(m, d, g1, g2, margin, raw, &st);
         if (num < 0) {                      // plane : box / cylinder counts, then stores
           mjh::collidePlaneBoxCyl<64, false, BOX>(m, d, g1, g2, margin, cnt, &st, bbuf);
         } else {
@@ -468,13 +457,14 @@ __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
   if (status) status[inst] = st;
 }
 
-// sensors and energy after the generated kernels and the constraint kernel
-// (mjh::sensorsAfter)
-__global__ __launch_bounds__(64) void k_sensors(mjhipModel m, Mirror mr, int B, int sensors) {
+// slider-crank/site/body transmissions, sensors and energy after the generated kernels and
+// the constraint kernel (mjh::transmissionAfter, mjh::sensorsAfter)
+__global__ __launch_bounds__(64) void k_sensors(mjhipModel m, Mirror mr, int B, int sensors,
+                                                int trn) {
   const int blk = blockIdx.x, lane = threadIdx.x;
   if ((long)blk*64 + lane >= B) return;
   Lane<64> d = lane_view(mr, blk, lane);
-  mjh::sensorsAfter<64>(m, d, sensors != 0);
+  mjh::sensorsAfter<64>(m, d, sensors != 0, trn != 0);
 }
 
 // row-major (B x n) <-> mirror block layout
@@ -719,7 +709,7 @@ static std::vector<int2> collision_pairs(const mjhipModel* m) {
         for (int j = 0; j < n2; j++) {
           const int g1 = m->body_geomadr[b1] + i, g2 = m->body_geomadr[b2] + j;
           const std::pair<int, int> k = key(make_int2(g1, g2));
-          if (!mjhip_pairMaxContacts(m->geom_type[k.first], m->geom_type[k.second])) continue;
+          if (!mjhip_pairMaxContacts(m, m->geom_type[k.first], m->geom_type[k.second])) continue;
           if (mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
                                   m->geom_contype[g2], m->geom_conaffinity[g2])) {
             continue;
@@ -766,6 +756,8 @@ static unsigned long long model_signature(const mjhipModel* m) {
   feed(&m->opt.jacobian, 4);
   feed(&m->opt.disableflags, 4);
   feed(&m->opt.enableflags, 4);
+  feed(&m->opt.ccd_tolerance, 8);
+  feed(&m->opt.ccd_iterations, 4);
 #define MJ_M(n) m->n
 #define X(type, name, d0, d1) if (m->name) feed(m->name, sizeof(type) * (size_t)(m->d0) * (d1));
   MJHIP_MODEL_POINTERS
@@ -979,7 +971,7 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   const char* nofast = getenv("MJHIP_DISABLE_FAST");
   c->sig = model_signature(m);
   if (!(nofast && nofast[0] == '1')) {
-    for (const FastKernelEntry* e = g_fast_kernels; e->launch; e++) {
+    for (const FastKernelEntry* e = mjhip_fastKernels(); e->launch; e++) {
       if (e->sig == c->sig) c->fast = e;
     }
   }
@@ -1003,6 +995,9 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
       }
     }
   }
+  // the native convex solver keeps its polytope in the instance's scratch: one lane per
+  // instance (the cooperative kernel would run several pairs of an instance at once)
+  if (mjh_needConvex(m)) c->coop = 0;
   if (c->coop) {
     // the cooperative kernel's dynamic LDS must fit one block: many box pairs (a large
     // efc_cap) or few lanes per instance can exceed it, and then the one-lane k_constraint
@@ -1176,9 +1171,10 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     HIPCHECK(hipGetLastError());
     const int sensors = !skipsensor && c->hmodel.nsensor > 0 &&
                         !(c->hmodel.opt.disableflags & mjhipDSBL_SENSOR);
-    if (sensors || (c->hmodel.opt.enableflags & mjhipENBL_ENERGY)) {
+    const int trn = mjh_needTrnAfter(&c->hmodel);
+    if (sensors || trn || (c->hmodel.opt.enableflags & mjhipENBL_ENERGY)) {
       hipLaunchKernelGGL(k_sensors, grid, block, 0, c->stream, c->dmodel, c->mirror, B,
-                         sensors);
+                         sensors, trn);
       HIPCHECK(hipGetLastError());
     }
     if (status) {

@@ -117,11 +117,13 @@ class Option(ctypes.Structure):
       ("o_solref", ctypes.c_double * 2),
       ("o_solimp", ctypes.c_double * 5),
       ("o_friction", ctypes.c_double * 5),
+      ("ccd_tolerance", ctypes.c_double),
       ("integrator", ctypes.c_int),
       ("cone", ctypes.c_int),
       ("jacobian", ctypes.c_int),
       ("disableflags", ctypes.c_int),
       ("enableflags", ctypes.c_int),
+      ("ccd_iterations", ctypes.c_int),
   ]
 
 
@@ -182,6 +184,8 @@ def model_signature(m) -> int:
   feed(np.asarray(o["o_friction"], dtype=np.float64)[:5].tobytes())
   for k in ("integrator", "cone", "jacobian", "disableflags", "enableflags"):
     feed(np.int32(o[k]).tobytes())
+  feed(np.float64(o.get("ccd_tolerance", 1e-6)).tobytes())
+  feed(np.int32(o.get("ccd_iterations", 50)).tobytes())
   for f in MODEL_FIELDS:
     feed(np.ascontiguousarray(getattr(m, f.name), dtype=NPTYPE[f.ctype]).tobytes())
   return h

@@ -22,6 +22,8 @@ def model_struct(m) -> fields.CModel:
   o = s.opt
   for k in ("timestep", "impratio", "density", "viscosity", "o_margin"):
     setattr(o, k, float(m.opt[k]))
+  o.ccd_tolerance = float(m.opt.get("ccd_tolerance", 1e-6))
+  o.ccd_iterations = int(m.opt.get("ccd_iterations", 50))
   for k, n in (("gravity", 3), ("wind", 3), ("magnetic", 3), ("o_solref", 2), ("o_solimp", 5),
                ("o_friction", 5)):
     arr = getattr(o, k)

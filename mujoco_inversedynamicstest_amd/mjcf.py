@@ -458,6 +458,8 @@ class Model:
         m.names[k[8:]] = [] if lst == [""] and m.sizes.get(_NAME_SIZE.get(k[8:], ""), 0) == 0 else lst
     m.opt.setdefault("o_friction", [1.0, 1.0, 0.005, 0.0001, 0.0001])   # mjOption default
     m.opt.setdefault("magnetic", [0.0, -0.5, 0.0])                      # mjOption default
+    m.opt.setdefault("ccd_tolerance", 1e-6)                             # engine_io.c:128
+    m.opt.setdefault("ccd_iterations", 50)                              # engine_io.c:160
     for f in fields.MODEL_FIELDS:
       setattr(m, f.name, np.ascontiguousarray(z[f.name]))
     return m
@@ -485,7 +487,7 @@ class MJCFCompiler:
                 "o_solref": [0.02, 1.0], "o_solimp": [0.9, 0.95, 0.001, 0.5, 2.0],
                 "o_friction": [1.0, 1.0, 0.005, 0.0001, 0.0001],
                 "integrator": 0, "cone": 0, "jacobian": 2, "disableflags": 0,
-                "enableflags": 0}
+                "enableflags": 0, "ccd_tolerance": 1e-6, "ccd_iterations": 50}
     self.classes = {}
     self.bodies = []
     self.tendons = []
@@ -639,9 +641,11 @@ class MJCFCompiler:
   def _parse_option(self, el):
     a = el.attrib
     o = self.opt
-    for k in ("timestep", "impratio", "density", "viscosity", "o_margin"):
+    for k in ("timestep", "impratio", "density", "viscosity", "o_margin", "ccd_tolerance"):
       if k in a:
         o[k] = float(a[k])
+    if "ccd_iterations" in a:
+      o["ccd_iterations"] = int(a["ccd_iterations"])
     for k in ("gravity", "wind", "magnetic", "o_solref", "o_solimp", "o_friction"):
       if k in a:
         o[k] = _floats(a[k])

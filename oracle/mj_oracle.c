@@ -8,6 +8,7 @@
 #define _GNU_SOURCE
 #include "mj_oracle.h"
 
+#include <float.h>
 #include <math.h>
 #include <pthread.h>
 #include <stdlib.h>
@@ -2577,23 +2578,996 @@ int or_boxBoxRaw(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum
   return num;
 }
 
+/*============== native convex collision: mjc_Convex / mjc_PlaneConvex on mjc_ccd ==============
+ * engine_collision_convex.c (supports :146-327, mjc_initCCDObj :716-768, mjc_CCDIteration
+ * :792-819, mjc_Convex :915-1001 with mjENBL_MULTICCD off, mjc_PlaneConvex :1045-1080 for a
+ * geom without mesh data) and engine_collision_gjk.c (gjk :163-272, supports :277-370,
+ * gjkIntersect :393-448, the subdistance algorithm :482-814, polytope2/3/4 :892-1156, the EPA
+ * :1161-1459, inflate and mjc_ccd :2195-2343). Only the native solver (mjDSBL_NATIVECCD
+ * clear) with one contact per pair is restated; mesh, height-field and SDF geoms are not. */
+
+enum { CCD_POINT = 100, CCD_LINE = 101 };      /* shrunken sphere / capsule supports */
+
+typedef struct { mjtNum v[3], p1[3], p2[3]; } orVtx;   /* Minkowski vertex, both witnesses */
+
+typedef struct {
+  int kind;                /* mjtGeom of the geom, or CCD_POINT / CCD_LINE */
+  int gtype;               /* the geom's own type (geom_type) */
+  const mjtNum* pos;       /* geom_xpos, geom_xmat, geom_size of the geom */
+  const mjtNum* mat;
+  const mjtNum* size;
+  mjtNum margin;
+} orShape;
+
+/* mulMatTVec3 / localToGlobal of engine_collision_convex.c:122-141 */
+static void ccd_toLocal(mjtNum r[3], const mjtNum* mat, const mjtNum d[3]) {
+  r[0] = mat[0]*d[0] + mat[3]*d[1] + mat[6]*d[2];
+  r[1] = mat[1]*d[0] + mat[4]*d[1] + mat[7]*d[2];
+  r[2] = mat[2]*d[0] + mat[5]*d[1] + mat[8]*d[2];
+}
+
+static void ccd_toGlobal(mjtNum r[3], const mjtNum* mat, const mjtNum t[3], const mjtNum* pos) {
+  r[0] = mat[0]*t[0] + mat[1]*t[1] + mat[2]*t[2];
+  r[1] = mat[3]*t[0] + mat[4]*t[1] + mat[5]*t[2];
+  r[2] = mat[6]*t[0] + mat[7]*t[1] + mat[8]*t[2];
+  r[0] += pos[0];
+  r[1] += pos[1];
+  r[2] += pos[2];
+}
+
+static mjtNum ccd_sign(mjtNum x) { return x < 0 ? -1 : (x > 0 ? 1 : 0); }
+
+/* the native support functions (convex.c:146-327) */
+static void ccd_support1(mjtNum r[3], const orShape* s, const mjtNum dir[3]) {
+  mjtNum ld[3], t[3];
+  switch (s->kind) {
+  case CCD_POINT:
+    mju_copy3(r, s->pos);
+    return;
+  case mjhipGEOM_SPHERE:
+    r[0] = s->size[0]*dir[0] + s->pos[0];
+    r[1] = s->size[0]*dir[1] + s->pos[1];
+    r[2] = s->size[0]*dir[2] + s->pos[2];
+    return;
+  case CCD_LINE:
+    ccd_toLocal(ld, s->mat, dir);
+    t[0] = 0;
+    t[1] = 0;
+    t[2] = ld[2] >= 0 ? s->size[1] : -s->size[1];
+    break;
+  case mjhipGEOM_CAPSULE:
+    ccd_toLocal(ld, s->mat, dir);
+    t[0] = ld[0]*s->size[0];
+    t[1] = ld[1]*s->size[0];
+    t[2] = ld[2]*s->size[0];
+    t[2] += ld[2] >= 0 ? s->size[1] : -s->size[1];
+    break;
+  case mjhipGEOM_ELLIPSOID: {
+    ccd_toLocal(ld, s->mat, dir);
+    t[0] = ld[0]*s->size[0];
+    t[1] = ld[1]*s->size[1];
+    t[2] = ld[2]*s->size[2];
+    mjtNum nrm = sqrt(t[0]*t[0] + t[1]*t[1] + t[2]*t[2]);
+    if (nrm < mjMINVAL) {
+      t[0] = s->size[0];
+      t[1] = 0;
+      t[2] = 0;
+    } else {
+      mjtNum inv = 1/nrm;
+      t[0] *= inv*s->size[0];
+      t[1] *= inv*s->size[1];
+      t[2] *= inv*s->size[2];
+    }
+    break;
+  }
+  case mjhipGEOM_CYLINDER: {
+    ccd_toLocal(ld, s->mat, dir);
+    mjtNum n = ld[0]*ld[0] + ld[1]*ld[1];
+    if (n > mjMINVAL*mjMINVAL) {
+      n = s->size[0] / sqrt(n);
+      t[0] = ld[0]*n;
+      t[1] = ld[1]*n;
+    } else {
+      t[0] = t[1] = 0;
+    }
+    t[2] = ccd_sign(ld[2])*s->size[1];
+    break;
+  }
+  default:   /* box */
+    ccd_toLocal(ld, s->mat, dir);
+    t[0] = (ld[0] >= 0 ? 1 : -1)*s->size[0];
+    t[1] = (ld[1] >= 0 ? 1 : -1)*s->size[1];
+    t[2] = (ld[2] >= 0 ? 1 : -1)*s->size[2];
+    break;
+  }
+  ccd_toGlobal(r, s->mat, t, s->pos);
+}
+
+/* support (gjk.c:277-296): each shape inflated by half its margin */
+static void ccd_support(orVtx* v, const orShape* a, const orShape* b, const mjtNum dir[3],
+                        const mjtNum ndir[3]) {
+  ccd_support1(v->p1, a, dir);
+  if (a->margin > 0) {
+    mjtNum h = 0.5*a->margin;
+    v->p1[0] += dir[0]*h;
+    v->p1[1] += dir[1]*h;
+    v->p1[2] += dir[2]*h;
+  }
+  ccd_support1(v->p2, b, ndir);
+  if (b->margin > 0) {
+    mjtNum h = 0.5*b->margin;
+    v->p2[0] += ndir[0]*h;
+    v->p2[1] += ndir[1]*h;
+    v->p2[2] += ndir[2]*h;
+  }
+  mju_sub3(v->v, v->p1, v->p2);
+}
+
+static mjtNum ccd_det3(const mjtNum a[3], const mjtNum b[3], const mjtNum c[3]) {
+  return a[0]*(b[1]*c[2] - b[2]*c[1]) + a[1]*(b[2]*c[0] - b[0]*c[2])
+       + a[2]*(b[0]*c[1] - b[1]*c[0]);
+}
+
+static int ccd_sameSign(mjtNum a, mjtNum b) {
+  if (a > 0 && b > 0) return 1;
+  if (a < 0 && b < 0) return -1;
+  return 0;
+}
+
+/* lincomb (gjk.c:453-477): sum of the first n coef[i]*v[i], left to right */
+static void ccd_lincomb(mjtNum r[3], const mjtNum* c, int n, const mjtNum* v1, const mjtNum* v2,
+                        const mjtNum* v3, const mjtNum* v4) {
+  for (int k = 0; k < 3; k++) {
+    mjtNum s = c[0]*v1[k];
+    if (n > 1) s = s + c[1]*v2[k];
+    if (n > 2) s = s + c[2]*v3[k];
+    if (n > 3) s = s + c[3]*v4[k];
+    r[k] = s;
+  }
+}
+
+/* projectOriginPlane (gjk.c:482-515): 1 if the plane is degenerate */
+static int ccd_projPlane(mjtNum r[3], const mjtNum a[3], const mjtNum b[3], const mjtNum c[3]) {
+  mjtNum ba[3], ca[3], cb[3], n[3], nv, nn;
+  mju_sub3(ba, b, a);
+  mju_sub3(ca, c, a);
+  mju_sub3(cb, c, b);
+  mju_cross(n, cb, ba);
+  nv = mju_dot3(n, b);
+  nn = mju_dot3(n, n);
+  if (nn == 0) return 1;
+  if (nv != 0 && nn > mjMINVAL) {
+    mju_scl3(r, n, nv / nn);
+    return 0;
+  }
+  mju_cross(n, ba, ca);
+  nv = mju_dot3(n, a);
+  nn = mju_dot3(n, n);
+  if (nn == 0) return 1;
+  if (nv != 0 && nn > mjMINVAL) {
+    mju_scl3(r, n, nv / nn);
+    return 0;
+  }
+  mju_cross(n, ca, cb);
+  nv = mju_dot3(n, c);
+  nn = mju_dot3(n, n);
+  mju_scl3(r, n, nv / nn);
+  return 0;
+}
+
+/* S1D (gjk.c:787-814) */
+static void ccd_S1D(mjtNum lam[2], const mjtNum a[3], const mjtNum b[3]) {
+  mjtNum d[3], p[3];
+  mju_sub3(d, b, a);
+  mjtNum s = -(mju_dot3(b, d) / mju_dot3(d, d));
+  p[0] = b[0] + s*d[0];
+  p[1] = b[1] + s*d[1];
+  p[2] = b[2] + s*d[2];
+  mjtNum mu = 0;
+  int ix = 0;
+  for (int i = 0; i < 3; i++) {
+    mjtNum t = a[i] - b[i];
+    if (fabs(t) >= fabs(mu)) {
+      mu = t;
+      ix = i;
+    }
+  }
+  mjtNum c1 = p[ix] - b[ix], c2 = a[ix] - p[ix];
+  if (ccd_sameSign(mu, c1) && ccd_sameSign(mu, c2)) {
+    lam[0] = c1 / mu;
+    lam[1] = c2 / mu;
+  } else {
+    lam[0] = 0;
+    lam[1] = 1;
+  }
+}
+
+/* the minors M_14, M_24, M_34 of S2D / triAffineCoord (gjk.c:667-669, :979-981) */
+static void ccd_minors(mjtNum M[3], const mjtNum a[3], const mjtNum b[3], const mjtNum c[3]) {
+  M[0] = b[1]*c[2] - b[2]*c[1] - a[1]*c[2] + a[2]*c[1] + a[1]*b[2] - a[2]*b[1];
+  M[1] = b[0]*c[2] - b[2]*c[0] - a[0]*c[2] + a[2]*c[0] + a[0]*b[2] - a[2]*b[0];
+  M[2] = b[0]*c[1] - b[1]*c[0] - a[0]*c[1] + a[1]*c[0] + a[0]*b[1] - a[1]*b[0];
+}
+
+/* the axes kept after dropping the one of largest projection; returns M_max */
+static mjtNum ccd_axes(const mjtNum M[3], int* x, int* y) {
+  mjtNum m1 = fabs(M[0]), m2 = fabs(M[1]), m3 = fabs(M[2]);
+  if (m1 >= m2 && m1 >= m3) { *x = 1; *y = 2; return M[0]; }
+  if (m2 >= m3) { *x = 0; *y = 2; return M[1]; }
+  *x = 0; *y = 1;
+  return M[2];
+}
+
+/* signed area cofactor of (p, u, w) in the kept axes (gjk.c:722-731) */
+static mjtNum ccd_area(const mjtNum* p, const mjtNum* u, const mjtNum* w, int x, int y) {
+  return p[x]*u[y] + p[y]*w[x] + u[x]*w[y] - p[x]*w[y] - p[y]*u[x] - w[x]*u[y];
+}
+
+/* S2D (gjk.c:653-783) */
+static void ccd_S2D(mjtNum lam[3], const mjtNum a[3], const mjtNum b[3], const mjtNum c[3]) {
+  mjtNum p[3];
+  if (ccd_projPlane(p, a, b, c)) {
+    ccd_S1D(lam, a, b);
+    lam[2] = 0;
+    return;
+  }
+  mjtNum M[3];
+  int x, y;
+  ccd_minors(M, a, b, c);
+  mjtNum Mmax = ccd_axes(M, &x, &y);
+  mjtNum C1 = ccd_area(p, b, c, x, y), C2 = ccd_area(p, c, a, x, y), C3 = ccd_area(p, a, b, x, y);
+  int k1 = ccd_sameSign(Mmax, C1), k2 = ccd_sameSign(Mmax, C2), k3 = ccd_sameSign(Mmax, C3);
+  if (k1 && k2 && k3) {
+    lam[0] = C1 / Mmax;
+    lam[1] = C2 / Mmax;
+    lam[2] = C3 / Mmax;
+    return;
+  }
+  mjtNum dmin = mjhipMAXVAL, l[2], q[3], dd;
+  if (!k1) {
+    ccd_S1D(l, b, c);
+    ccd_lincomb(q, l, 2, b, c, NULL, NULL);
+    dd = mju_dot3(q, q);
+    lam[0] = 0; lam[1] = l[0]; lam[2] = l[1];
+    dmin = dd;
+  }
+  if (!k2) {
+    ccd_S1D(l, a, c);
+    ccd_lincomb(q, l, 2, a, c, NULL, NULL);
+    dd = mju_dot3(q, q);
+    if (dd < dmin) {
+      lam[0] = l[0]; lam[1] = 0; lam[2] = l[1];
+      dmin = dd;
+    }
+  }
+  if (!k3) {
+    ccd_S1D(l, a, b);
+    ccd_lincomb(q, l, 2, a, b, NULL, NULL);
+    dd = mju_dot3(q, q);
+    if (dd < dmin) {
+      lam[0] = l[0]; lam[1] = l[1]; lam[2] = 0;
+    }
+  }
+}
+
+/* S3D (gjk.c:560-649) */
+static void ccd_S3D(mjtNum lam[4], const mjtNum a[3], const mjtNum b[3], const mjtNum c[3],
+                    const mjtNum e[3]) {
+  mjtNum C1 = -ccd_det3(b, c, e), C2 = ccd_det3(a, c, e), C3 = -ccd_det3(a, b, e),
+         C4 = ccd_det3(a, b, c);
+  mjtNum det = C1 + C2 + C3 + C4;
+  int k1 = ccd_sameSign(det, C1), k2 = ccd_sameSign(det, C2), k3 = ccd_sameSign(det, C3),
+      k4 = ccd_sameSign(det, C4);
+  if (k1 && k2 && k3 && k4) {
+    lam[0] = C1 / det;
+    lam[1] = C2 / det;
+    lam[2] = C3 / det;
+    lam[3] = C4 / det;
+    return;
+  }
+  mjtNum dmin = mjhipMAXVAL, l[3], q[3], dd;
+  if (!k1) {
+    ccd_S2D(l, b, c, e);
+    ccd_lincomb(q, l, 3, b, c, e, NULL);
+    dd = mju_dot3(q, q);
+    lam[0] = 0; lam[1] = l[0]; lam[2] = l[1]; lam[3] = l[2];
+    dmin = dd;
+  }
+  if (!k2) {
+    ccd_S2D(l, a, c, e);
+    ccd_lincomb(q, l, 3, a, c, e, NULL);
+    dd = mju_dot3(q, q);
+    if (dd < dmin) {
+      lam[0] = l[0]; lam[1] = 0; lam[2] = l[1]; lam[3] = l[2];
+      dmin = dd;
+    }
+  }
+  if (!k3) {
+    ccd_S2D(l, a, b, e);
+    ccd_lincomb(q, l, 3, a, b, e, NULL);
+    dd = mju_dot3(q, q);
+    if (dd < dmin) {
+      lam[0] = l[0]; lam[1] = l[1]; lam[2] = 0; lam[3] = l[2];
+      dmin = dd;
+    }
+  }
+  if (!k4) {
+    ccd_S2D(l, a, b, c);
+    ccd_lincomb(q, l, 3, a, b, c, NULL);
+    dd = mju_dot3(q, q);
+    if (dd < dmin) {
+      lam[0] = l[0]; lam[1] = l[1]; lam[2] = l[2]; lam[3] = 0;
+    }
+  }
+}
+
+/* the solver state of one mjc_ccd call (mjCCDStatus, gjk.h:70-89, the fields this path uses) */
+typedef struct {
+  mjtNum dist, x1[3], x2[3];
+  int nx, iters, nsimplex;
+  int kmax;
+  mjtNum tol, cutoff;
+  orVtx simplex[4];
+} orCCD;
+
+/* gjkIntersect (gjk.c:393-448): 1 contact, 0 none, -1 inconclusive */
+static mjtNum ccd_faceDist(mjtNum n[3], const orVtx* a, const orVtx* b, const orVtx* c) {
+  mjtNum d1[3], d2[3];
+  mju_sub3(d1, c->v, a->v);
+  mju_sub3(d2, b->v, a->v);
+  mju_cross(n, d1, d2);
+  mjtNum nn = mju_dot3(n, n);
+  if (nn > mjMINVAL*mjMINVAL && nn < mjhipMAXVAL*mjhipMAXVAL) {
+    nn = 1/sqrt(nn);
+    mju_scl3(n, n, nn);
+    return mju_dot3(n, a->v);
+  }
+  return mjhipMAXVAL;
+}
+
+static int ccd_intersect(orCCD* st, const orShape* A, const orShape* B) {
+  orVtx s[4] = {st->simplex[0], st->simplex[1], st->simplex[2], st->simplex[3]};
+  int o[4] = {0, 1, 2, 3};
+  int k = st->iters;
+  for (; k < st->kmax; k++) {
+    mjtNum dist[4], nrm[12];
+    dist[0] = ccd_faceDist(nrm + 0, s + o[2], s + o[1], s + o[3]);
+    dist[1] = ccd_faceDist(nrm + 3, s + o[0], s + o[2], s + o[3]);
+    dist[2] = ccd_faceDist(nrm + 6, s + o[1], s + o[0], s + o[3]);
+    dist[3] = ccd_faceDist(nrm + 9, s + o[0], s + o[1], s + o[2]);
+    if (!dist[3] || !dist[2] || !dist[1] || !dist[0]) {
+      st->iters = k;
+      return -1;
+    }
+    int i = dist[0] < dist[1] ? 0 : 1, j = dist[2] < dist[3] ? 2 : 3;
+    int w = dist[i] < dist[j] ? i : j;
+    if (dist[w] > 0) {
+      st->nsimplex = 4;
+      for (int q = 0; q < 4; q++) st->simplex[q] = s[o[q]];
+      st->iters = k;
+      return 1;
+    }
+    mjtNum ndir[3] = {-nrm[3*w], -nrm[3*w+1], -nrm[3*w+2]};
+    ccd_support(s + o[w], A, B, nrm + 3*w, ndir);
+    if (mju_dot3(nrm + 3*w, s[o[w]].v) < 0) {
+      st->nsimplex = 0;
+      st->iters = k;
+      return 0;
+    }
+    i = (w + 1) & 3;
+    j = (w + 2) & 3;
+    int t = o[i];
+    o[i] = o[j];
+    o[j] = t;
+  }
+  st->iters = k;
+  return -1;
+}
+
+/* gjk (gjk.c:163-272) */
+static void ccd_gjk(orCCD* st, const orShape* A, const orShape* B) {
+  const int get_dist = st->cutoff > 0;
+  int backup = !get_dist, n = 0, k = 0;
+  orVtx* S = st->simplex;
+  mjtNum x[3], lam[4] = {1, 0, 0, 0}, cut2 = st->cutoff*st->cutoff;
+  const int discrete = A->margin == 0 && B->margin == 0 && A->gtype == mjhipGEOM_BOX &&
+                       B->gtype == mjhipGEOM_BOX;
+  const mjtNum eps = discrete ? 0 : st->tol*st->tol;
+  mju_sub3(x, st->x1, st->x2);
+  for (; k < st->kmax; k++) {
+    /* gjkSupport (:301-323) */
+    mjtNum dir[3] = {-1, 0, 0}, ndir[3] = {1, 0, 0};
+    mjtNum nn = mju_dot3(x, x);
+    if (nn > mjMINVAL*mjMINVAL) {
+      nn = 1/sqrt(nn);
+      mju_scl3(ndir, x, nn);
+      mju_scl3(dir, ndir, -1);
+    }
+    ccd_support(S + n, A, B, dir, ndir);
+    const mjtNum* sk = S[n].v;
+    mjtNum diff[3];
+    mju_sub3(diff, x, sk);
+    if (2*mju_dot3(x, diff) < eps) {
+      if (!k) n = 1;
+      break;
+    }
+    if (!get_dist) {
+      if (mju_dot3(x, sk) > 0) {
+        st->iters = k;
+        st->nsimplex = 0;
+        st->nx = 0;
+        st->dist = mjhipMAXVAL;
+        return;
+      }
+    } else if (st->cutoff < mjhipMAXVAL) {
+      mjtNum vs = mju_dot3(x, sk), vv = mju_dot3(x, x);
+      if (mju_dot3(x, sk) > 0 && (vs*vs / vv) >= cut2) {
+        st->iters = k;
+        st->nsimplex = 0;
+        st->nx = 0;
+        st->dist = mjhipMAXVAL;
+        return;
+      }
+    }
+    if (n == 3 && backup) {
+      st->iters = k;
+      int r = ccd_intersect(st, A, B);
+      if (r != -1) {
+        st->nx = 0;
+        st->dist = r > 0 ? 0 : mjhipMAXVAL;
+        return;
+      }
+      k = st->iters;
+      backup = 0;
+    }
+    /* subdistance (:544-556) */
+    lam[0] = lam[1] = lam[2] = lam[3] = 0;
+    if (n + 1 == 4) ccd_S3D(lam, S[0].v, S[1].v, S[2].v, S[3].v);
+    else if (n + 1 == 3) ccd_S2D(lam, S[0].v, S[1].v, S[2].v);
+    else if (n + 1 == 2) ccd_S1D(lam, S[0].v, S[1].v);
+    else lam[0] = 1;
+    n = 0;
+    for (int i = 0; i < 4; i++) {
+      if (lam[i] == 0) continue;
+      S[n] = S[i];
+      lam[n++] = lam[i];
+    }
+    mjtNum nx[3];
+    ccd_lincomb(nx, lam, n, S[0].v, S[1].v, S[2].v, S[3].v);
+    if (fabs(nx[0] - x[0]) < mjMINVAL && fabs(nx[1] - x[1]) < mjMINVAL &&
+        fabs(nx[2] - x[2]) < mjMINVAL) {
+      break;
+    }
+    mju_copy3(x, nx);
+    if (n == 4) break;
+  }
+  ccd_lincomb(st->x1, lam, n, S[0].p1, S[1].p1, S[2].p1, S[3].p1);
+  ccd_lincomb(st->x2, lam, n, S[0].p2, S[1].p2, S[2].p2, S[3].p2);
+  st->nx = 1;
+  st->iters = k;
+  st->nsimplex = n;
+  st->dist = mju_norm3(x);
+}
+
+/*------------------------------- EPA (gjk.c:820-1459) ----------------------------------------*/
+typedef struct {
+  int vi[3], adj[3];
+  mjtNum proj[3], dist;
+  int slot;              /* position in the candidate list; -1 not listed; -2 deleted */
+} orFace;
+
+typedef struct {
+  orVtx* vtx;
+  int nvtx;
+  orFace* face;
+  int nface, maxface;
+  int* list;             /* candidate faces (the reference's map) */
+  int nlist;
+  int* hface;            /* horizon: faces and their edges */
+  int* hedge;
+  int nh;
+  const mjtNum* w;
+} orPoly;
+
+static int ccd_addVertex(orPoly* P, const orVtx* v) {
+  orVtx* t = P->vtx + P->nvtx;
+  mju_copy3(t->p1, v->p1);
+  mju_copy3(t->p2, v->p2);
+  mju_sub3(t->v, v->p1, v->p2);
+  return P->nvtx++;
+}
+
+/* epaSupport (:328-353) */
+static int ccd_newVertex(orPoly* P, const orShape* A, const orShape* B, const mjtNum d[3],
+                         mjtNum dn) {
+  mjtNum dir[3] = {1, 0, 0}, ndir[3] = {-1, 0, 0};
+  if (dn > mjMINVAL) {
+    dir[0] = d[0] / dn;
+    dir[1] = d[1] / dn;
+    dir[2] = d[2] / dn;
+    mju_scl3(ndir, dir, -1);
+  }
+  ccd_support(P->vtx + P->nvtx, A, B, dir, ndir);
+  return P->nvtx++;
+}
+
+/* attachFace (:1192-1213) */
+static mjtNum ccd_attach(orPoly* P, int a, int b, int c, int j1, int j2, int j3) {
+  orFace* f = P->face + P->nface++;
+  f->vi[0] = a; f->vi[1] = b; f->vi[2] = c;
+  f->adj[0] = j1; f->adj[1] = j2; f->adj[2] = j3;
+  if (ccd_projPlane(f->proj, P->vtx[c].v, P->vtx[b].v, P->vtx[a].v)) return 0;
+  f->dist = mju_norm3(f->proj);
+  f->slot = -1;
+  return f->dist;
+}
+
+static void ccd_listAll(orPoly* P, int n) {
+  for (int i = 0; i < n; i++) {
+    P->list[i] = i;
+    P->face[i].slot = i;
+  }
+  P->nlist = n;
+}
+
+/* replaceSimplex3 (:820-837) */
+static void ccd_toTriangle(orPoly* P, orCCD* st, int a, int b, int c) {
+  st->nsimplex = 3;
+  const int id[3] = {a, b, c};
+  for (int i = 0; i < 3; i++) {
+    mju_copy3(st->simplex[i].p1, P->vtx[id[i]].p1);
+    mju_copy3(st->simplex[i].p2, P->vtx[id[i]].p2);
+    mju_copy3(st->simplex[i].v, P->vtx[id[i]].v);
+  }
+  P->nface = 0;
+  P->nvtx = 0;
+}
+
+/* sameSide / testTetra (:842-868) */
+static int ccd_sameSide(const mjtNum p0[3], const mjtNum p1[3], const mjtNum p2[3],
+                        const mjtNum p3[3]) {
+  mjtNum e1[3], e2[3], e3[3], e4[3], n[3];
+  mju_sub3(e1, p1, p0);
+  mju_sub3(e2, p2, p0);
+  mju_cross(n, e1, e2);
+  mju_sub3(e3, p3, p0);
+  mjtNum d1 = mju_dot3(n, e3);
+  mju_scl3(e4, p0, -1);
+  mjtNum d2 = mju_dot3(n, e4);
+  return (d1 > 0 && d2 > 0) || (d1 < 0 && d2 < 0);
+}
+
+static int ccd_inTetra(const mjtNum* a, const mjtNum* b, const mjtNum* c, const mjtNum* d) {
+  return ccd_sameSide(a, b, c, d) && ccd_sameSide(b, c, d, a) && ccd_sameSide(c, d, a, b) &&
+         ccd_sameSide(d, a, b, c);
+}
+
+/* triAffineCoord / triPointIntersect (:976-1035) */
+static void ccd_affine(mjtNum lam[3], const mjtNum a[3], const mjtNum b[3], const mjtNum c[3],
+                       const mjtNum p[3]) {
+  mjtNum M[3];
+  int x, y;
+  ccd_minors(M, a, b, c);
+  mjtNum Mmax = ccd_axes(M, &x, &y);
+  lam[0] = ccd_area(p, b, c, x, y) / Mmax;
+  lam[1] = ccd_area(p, c, a, x, y) / Mmax;
+  lam[2] = ccd_area(p, a, b, x, y) / Mmax;
+}
+
+static int ccd_onTriangle(const mjtNum a[3], const mjtNum b[3], const mjtNum c[3],
+                          const mjtNum p[3]) {
+  mjtNum lam[3], q[3], d[3];
+  ccd_affine(lam, a, b, c, p);
+  if (lam[0] < 0 || lam[1] < 0 || lam[2] < 0) return 0;
+  q[0] = a[0]*lam[0] + b[0]*lam[1] + c[0]*lam[2];
+  q[1] = a[1]*lam[0] + b[1]*lam[1] + c[1]*lam[2];
+  q[2] = a[2]*lam[0] + b[2]*lam[1] + c[2]*lam[2];
+  mju_sub3(d, q, p);
+  return mju_norm3(d) < mjMINVAL;
+}
+
+/* polytope3 (:1040-1117) */
+static int ccd_fromTriangle(orPoly* P, orCCD* st, const orShape* A, const orShape* B) {
+  const mjtNum *a = st->simplex[0].v, *b = st->simplex[1].v, *c = st->simplex[2].v;
+  mjtNum e1[3], e2[3], n[3], nn[3];
+  mju_sub3(e1, b, a);
+  mju_sub3(e2, c, a);
+  mju_cross(n, e1, e2);
+  mjtNum nrm = mju_norm3(n);
+  if (nrm < mjMINVAL) return 4;                        /* mjEPA_P3_BAD_NORMAL */
+  mju_scl3(nn, n, -1);
+  int i1 = ccd_addVertex(P, st->simplex + 0);
+  int i2 = ccd_addVertex(P, st->simplex + 1);
+  int i3 = ccd_addVertex(P, st->simplex + 2);
+  int i5 = ccd_newVertex(P, A, B, nn, nrm);
+  int i4 = ccd_newVertex(P, A, B, n, nrm);
+  const mjtNum *v4 = P->vtx[i4].v, *v5 = P->vtx[i5].v;
+  if (ccd_onTriangle(a, b, c, v4)) return 5;            /* mjEPA_P3_INVALID_V4 */
+  if (ccd_onTriangle(a, b, c, v5)) return 6;            /* mjEPA_P3_INVALID_V5 */
+  if (st->dist > 10*mjMINVAL && !ccd_inTetra(a, b, c, v4) && !ccd_inTetra(a, b, c, v5)) {
+    return 7;                                          /* mjEPA_P3_MISSING_ORIGIN */
+  }
+  if (ccd_attach(P, i4, i1, i2, 1, 3, 2) < mjMINVAL) return 8;
+  if (ccd_attach(P, i4, i3, i1, 2, 4, 0) < mjMINVAL) return 8;
+  if (ccd_attach(P, i4, i2, i3, 0, 5, 1) < mjMINVAL) return 8;
+  if (ccd_attach(P, i5, i2, i1, 5, 0, 4) < mjMINVAL) return 8;
+  if (ccd_attach(P, i5, i1, i3, 3, 1, 5) < mjMINVAL) return 8;
+  if (ccd_attach(P, i5, i3, i2, 4, 2, 3) < mjMINVAL) return 8;   /* mjEPA_P3_ORIGIN_ON_FACE */
+  ccd_listAll(P, 6);
+  return 0;
+}
+
+/* rotmat (:873-887): 120 degrees about axis */
+static void ccd_rot120(mjtNum R[9], const mjtNum axis[3]) {
+  mjtNum n = mju_norm3(axis);
+  mjtNum u1 = axis[0] / n, u2 = axis[1] / n, u3 = axis[2] / n;
+  const mjtNum s = 0.86602540378, c = -0.5;
+  R[0] = c + u1*u1*(1 - c);
+  R[1] = u1*u2*(1 - c) - u3*s;
+  R[2] = u1*u3*(1 - c) + u2*s;
+  R[3] = u2*u1*(1 - c) + u3*s;
+  R[4] = c + u2*u2*(1 - c);
+  R[5] = u2*u3*(1 - c) - u1*s;
+  R[6] = u1*u3*(1 - c) - u2*s;
+  R[7] = u2*u3*(1 - c) + u1*s;
+  R[8] = c + u3*u3*(1 - c);
+}
+
+/* polytope2 (:892-971) */
+static int ccd_fromSegment(orPoly* P, orCCD* st, const orShape* A, const orShape* B) {
+  const mjtNum *a = st->simplex[0].v, *b = st->simplex[1].v;
+  mjtNum d[3];
+  mju_sub3(d, b, a);
+  mjtNum best = mjhipMAXVAL;
+  int ix = 0;
+  for (int i = 0; i < 3; i++) {
+    if (fabs(d[i]) < best) {
+      best = fabs(d[i]);
+      ix = i;
+    }
+  }
+  mjtNum e[3] = {0, 0, 0}, d1[3], d2[3], d3[3], R[9];
+  e[ix] = 1;
+  mju_cross(d1, e, d);
+  ccd_rot120(R, d);
+  mju_mulMatVec3(d2, R, d1);
+  mju_mulMatVec3(d3, R, d2);
+  int i1 = ccd_addVertex(P, st->simplex + 0);
+  int i2 = ccd_addVertex(P, st->simplex + 1);
+  int i3 = ccd_newVertex(P, A, B, d1, mju_norm3(d1));
+  int i4 = ccd_newVertex(P, A, B, d2, mju_norm3(d2));
+  int i5 = ccd_newVertex(P, A, B, d3, mju_norm3(d3));
+  const int tri[6][6] = {{i1, i3, i4, 1, 3, 2}, {i1, i5, i3, 2, 4, 0}, {i1, i4, i5, 0, 5, 1},
+                         {i2, i4, i3, 5, 0, 4}, {i2, i3, i5, 3, 1, 5}, {i2, i5, i4, 4, 2, 3}};
+  for (int f = 0; f < 6; f++) {
+    if (ccd_attach(P, tri[f][0], tri[f][1], tri[f][2], tri[f][3], tri[f][4], tri[f][5]) <
+        mjMINVAL) {
+      ccd_toTriangle(P, st, tri[f][0], tri[f][1], tri[f][2]);
+      return ccd_fromTriangle(P, st, A, B);
+    }
+  }
+  const mjtNum *v1 = P->vtx[i1].v, *v2 = P->vtx[i2].v, *v3 = P->vtx[i3].v,
+               *v4 = P->vtx[i4].v, *v5 = P->vtx[i5].v;
+  if (st->dist > 10*mjMINVAL && !ccd_inTetra(v1, v3, v4, v5) && !ccd_inTetra(v2, v3, v4, v5)) {
+    return 2;                                          /* mjEPA_P2_MISSING_ORIGIN */
+  }
+  ccd_listAll(P, 6);
+  return 0;
+}
+
+/* polytope4 (:1122-1156) */
+static int ccd_fromTetra(orPoly* P, orCCD* st, const orShape* A, const orShape* B) {
+  int i1 = ccd_addVertex(P, st->simplex + 0);
+  int i2 = ccd_addVertex(P, st->simplex + 1);
+  int i3 = ccd_addVertex(P, st->simplex + 2);
+  int i4 = ccd_addVertex(P, st->simplex + 3);
+  const int tri[4][6] = {{i1, i2, i3, 1, 3, 2}, {i1, i4, i2, 2, 3, 0}, {i1, i3, i4, 0, 3, 1},
+                         {i4, i3, i2, 2, 0, 1}};
+  for (int f = 0; f < 4; f++) {
+    if (ccd_attach(P, tri[f][0], tri[f][1], tri[f][2], tri[f][3], tri[f][4], tri[f][5]) <
+        mjMINVAL) {
+      ccd_toTriangle(P, st, tri[f][0], tri[f][1], tri[f][2]);
+      return ccd_fromTriangle(P, st, A, B);
+    }
+  }
+  if (!ccd_inTetra(P->vtx[i1].v, P->vtx[i2].v, P->vtx[i3].v, P->vtx[i4].v)) return 9;
+  ccd_listAll(P, 4);
+  return 0;
+}
+
+/* deleteFace (:1174-1180) */
+static void ccd_unlist(orPoly* P, int f) {
+  orFace* F = P->face + f;
+  if (F->slot >= 0) {
+    P->list[F->slot] = P->list[--P->nlist];
+    P->face[P->list[F->slot]].slot = F->slot;
+  }
+  F->slot = -2;
+}
+
+static int ccd_edgeOf(const orFace* F, int v) {
+  if (F->vi[0] == v) return 0;
+  if (F->vi[1] == v) return 1;
+  return 2;
+}
+
+/* horizonRec (:1246-1267) */
+static int ccd_visible(orPoly* P, int f, int e) {
+  orFace* F = P->face + f;
+  mjtNum d2 = F->dist*F->dist;
+  if (mju_dot3(F->proj, P->w) >= d2) {
+    ccd_unlist(P, f);
+    for (int k = 1; k < 3; k++) {
+      int i = (e + k) % 3;
+      int g = F->adj[i];
+      if (P->face[g].slot > -2) {
+        int ge = ccd_edgeOf(P->face + g, F->vi[(i + 1) % 3]);
+        if (!ccd_visible(P, g, ge)) {
+          P->hface[P->nh] = g;
+          P->hedge[P->nh++] = ge;
+        }
+      }
+    }
+    return 1;
+  }
+  return 0;
+}
+
+/* horizon (:1272-1295) */
+static void ccd_horizon(orPoly* P, int f) {
+  ccd_unlist(P, f);
+  const orFace* F = P->face + f;
+  for (int k = 0; k < 3; k++) {
+    int g = F->adj[k];
+    int ge = ccd_edgeOf(P->face + g, F->vi[(k + 1) % 3]);
+    if ((k == 0 || P->face[g].slot > -2) && !ccd_visible(P, g, ge)) {
+      P->hface[P->nh] = g;
+      P->hedge[P->nh++] = ge;
+    }
+  }
+}
+
+/* epa (:1329-1459) + epaWitness (:1300-1323); returns the face or -1 */
+static int ccd_epa(orCCD* st, orPoly* P, const orShape* A, const orShape* B) {
+  mjtNum lower, upper = FLT_MAX;
+  int f = -1, pf = -1, k;
+  P->nh = 0;
+  for (k = 0; k < st->kmax; k++) {
+    pf = f;
+    lower = FLT_MAX;
+    for (int i = 0; i < P->nlist; i++) {
+      if (P->face[P->list[i]].dist < lower) {
+        f = P->list[i];
+        lower = P->face[f].dist;
+      }
+    }
+    if (lower > upper || f < 0) {
+      f = pf;
+      break;
+    }
+    if (lower <= 0) break;                              /* warning: origin on a face */
+    orFace* F = P->face + f;
+    int wi = ccd_newVertex(P, A, B, F->proj, lower);
+    const mjtNum* w = P->vtx[wi].v;
+    mjtNum up = mju_dot3(F->proj, w) / lower;
+    if (up < upper) upper = up;
+    if (upper - lower < st->tol) break;
+    P->w = w;
+    ccd_horizon(P, f);
+    if (P->nh < 3) {
+      f = -1;
+      break;
+    }
+    const int nf = P->nface, ne = P->nh;
+    if (ne > P->maxface - P->nface) break;              /* warning: out of face memory */
+    for (int i = 0; i < ne; i++) {
+      const int cur = nf + i, prev = i ? cur - 1 : nf + ne - 1, next = nf + (i + 1) % ne;
+      orFace* H = P->face + P->hface[i];
+      const int e = P->hedge[i];
+      const int a = H->vi[e], b = H->vi[(e + 1) % 3];
+      H->adj[e] = cur;
+      mjtNum dd = ccd_attach(P, wi, b, a, prev, P->hface[i], next);
+      if (dd == 0) {
+        f = -1;
+        break;
+      }
+      if (dd >= lower && dd <= upper) {
+        int s = P->nlist++;
+        P->list[s] = P->nface - 1;
+        P->face[P->nface - 1].slot = s;
+      }
+    }
+    P->nh = 0;
+    if (!P->nlist || f < 0) break;
+  }
+  if (f >= 0) {
+    const orFace* F = P->face + f;
+    mjtNum lam[3];
+    ccd_affine(lam, P->vtx[F->vi[0]].v, P->vtx[F->vi[1]].v, P->vtx[F->vi[2]].v, F->proj);
+    const mjtNum *a1 = P->vtx[F->vi[0]].p1, *b1 = P->vtx[F->vi[1]].p1, *c1 = P->vtx[F->vi[2]].p1;
+    const mjtNum *a2 = P->vtx[F->vi[0]].p2, *b2 = P->vtx[F->vi[1]].p2, *c2 = P->vtx[F->vi[2]].p2;
+    for (int i = 0; i < 3; i++) {
+      st->x1[i] = a1[i]*lam[0] + b1[i]*lam[1] + c1[i]*lam[2];
+      st->x2[i] = a2[i]*lam[0] + b2[i]*lam[1] + c2[i]*lam[2];
+    }
+    st->nx = 1;
+    st->dist = -F->dist;
+  } else {
+    st->nx = 0;
+    st->dist = 0;
+  }
+  return f;
+}
+
+/* mjc_ccd (:2215-2343) with max_contacts = 1 and dist_cutoff = 0; the geoms' margins are in
+ * A->margin / B->margin */
+static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol) {
+  mju_copy3(st->x1, A->pos);
+  mju_copy3(st->x2, B->pos);
+  st->iters = 0;
+  st->tol = tol;
+  st->kmax = kmax;
+  st->cutoff = 0;
+  const int shrinkA = A->gtype == mjhipGEOM_SPHERE || A->gtype == mjhipGEOM_CAPSULE;
+  const int shrinkB = B->gtype == mjhipGEOM_SPHERE || B->gtype == mjhipGEOM_CAPSULE;
+  if (shrinkA || shrinkB) {
+    mjtNum full1 = 0, full2 = 0, m1 = A->margin, m2 = B->margin;
+    if (shrinkA) {
+      full1 = A->size[0] + 0.5*m1;
+      A->kind = A->gtype == mjhipGEOM_SPHERE ? CCD_POINT : CCD_LINE;
+      A->margin = 0;
+    }
+    if (shrinkB) {
+      full2 = B->size[0] + 0.5*m2;
+      B->kind = B->gtype == mjhipGEOM_SPHERE ? CCD_POINT : CCD_LINE;
+      B->margin = 0;
+    }
+    st->cutoff += full1 + full2;
+    ccd_gjk(st, A, B);
+    st->cutoff = 0;
+    A->margin = m1;
+    B->margin = m2;
+    A->kind = A->gtype;
+    B->kind = B->gtype;
+    if (st->dist > st->tol) {               /* shallow: inflate (:2195-2210) */
+      mjtNum n[3];
+      mju_sub3(n, st->x2, st->x1);
+      mju_normalize3(n);
+      if (full1) {
+        st->x1[0] += full1*n[0];
+        st->x1[1] += full1*n[1];
+        st->x1[2] += full1*n[2];
+      }
+      if (full2) {
+        st->x2[0] -= full2*n[0];
+        st->x2[1] -= full2*n[1];
+        st->x2[2] -= full2*n[2];
+      }
+      st->dist -= (full1 + full2);
+      if (st->dist > st->cutoff) st->dist = mjhipMAXVAL;
+      return st->dist;
+    }
+    st->iters = 0;
+    mju_copy3(st->x1, A->pos);
+    mju_copy3(st->x2, B->pos);
+  }
+  ccd_gjk(st, A, B);
+  if (st->dist <= tol && st->nsimplex > 1) {
+    st->dist = 0;
+    const int N = kmax;
+    orPoly P;
+    P.maxface = 6*N > 1000 ? 6*N : 1000;
+    P.vtx = (orVtx*)malloc(sizeof(orVtx)*(5 + N));
+    P.face = (orFace*)malloc(sizeof(orFace)*P.maxface);
+    P.list = (int*)malloc(sizeof(int)*P.maxface);
+    P.hface = (int*)malloc(sizeof(int)*(6 + N));
+    P.hedge = (int*)malloc(sizeof(int)*(6 + N));
+    P.nvtx = P.nface = P.nlist = P.nh = 0;
+    int ret = st->nsimplex == 2 ? ccd_fromSegment(&P, st, A, B) :
+              st->nsimplex == 3 ? ccd_fromTriangle(&P, st, A, B) : ccd_fromTetra(&P, st, A, B);
+    if (!ret) ccd_epa(st, &P, A, B);
+    free(P.vtx);
+    free(P.face);
+    free(P.list);
+    free(P.hface);
+    free(P.hedge);
+  }
+  return st->dist;
+}
+
+static void or_shape(orShape* s, const mjhipModel* m, const mjhipData* d, int g, mjtNum margin) {
+  s->kind = s->gtype = m->geom_type[g];
+  s->pos = d->geom_xpos + 3*g;
+  s->mat = d->geom_xmat + 9*g;
+  s->size = m->geom_size + 3*g;
+  s->margin = margin;
+}
+
+/* mjc_Convex (convex.c:915-1001) through mjc_CCDIteration (:792-819), native solver, one
+ * contact (mjENBL_MULTICCD off) */
+static int col_convex(orRaw* c, const mjhipModel* m, const mjhipData* d, int g1, int g2,
+                      mjtNum margin) {
+  orShape A, B;
+  or_shape(&A, m, d, g1, margin);
+  or_shape(&B, m, d, g2, margin);
+  orCCD st;
+  mjtNum dist = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance);
+  if (!(dist < 0) || st.nx < 1) return 0;
+  c->dist = margin + dist;
+  mju_sub3(c->frame, st.x1, st.x2);
+  mju_normalize3(c->frame);
+  c->pos[0] = 0.5*(st.x1[0] + st.x2[0]);
+  c->pos[1] = 0.5*(st.x1[1] + st.x2[1]);
+  c->pos[2] = 0.5*(st.x1[2] + st.x2[2]);
+  mju_zero3(c->frame + 3);
+  return 1;
+}
+
+/* mjc_PlaneConvex (convex.c:1045-1080) for a geom without mesh data (the ellipsoid): the
+ * libccd support (mjccd_support :501-704) of geom 2 at -normal, one contact */
+static int col_planeConvex(orRaw* c, const mjhipModel* m, const mjhipData* d, int g1, int g2,
+                           mjtNum margin) {
+  const mjtNum *pos1 = d->geom_xpos + 3*g1, *mat1 = d->geom_xmat + 9*g1;
+  const mjtNum *pos2 = d->geom_xpos + 3*g2, *mat2 = d->geom_xmat + 9*g2;
+  const mjtNum* size = m->geom_size + 3*g2;
+  mjtNum normal[3] = {mat1[2], mat1[5], mat1[8]}, dir[3] = {-mat1[2], -mat1[5], -mat1[8]};
+  mjtNum ld[3], v[3], dif[3];
+  mju_mulMatTVec3(ld, mat2, dir);
+  for (int i = 0; i < 3; i++) v[i] = ld[i]*size[i];      /* ellipsoid case (:570-580) */
+  mju_normalize3(v);
+  for (int i = 0; i < 3; i++) v[i] *= size[i];
+  for (int i = 0; i < 3; i++) v[i] += ld[i]*0.0/2;        /* the object's margin is 0 */
+  mju_mulMatVec3(v, mat2, v);
+  mju_addTo3(v, pos2);
+  mju_sub3(dif, v, pos1);
+  mjtNum dist = mju_dot3(normal, dif);
+  if (dist > margin) return 0;
+  c->dist = dist;
+  mju_copy3(c->pos, v);
+  mju_addToScl3(c->pos, normal, -0.5*dist);
+  mju_copy3(c->frame, normal);
+  mju_zero3(c->frame + 3);
+  return 1;
+}
+
+/* pairs served by mjc_Convex in mjCOLLISIONFUNC (capsule-ellipsoid/cylinder, sphere-ellipsoid,
+ * ellipsoid and cylinder pairs among themselves and with boxes) */
+static int or_isConvexPair(int t1, int t2) {
+  if (t1 == mjhipGEOM_PLANE || t1 == mjhipGEOM_HFIELD) return 0;
+  if (t2 == mjhipGEOM_ELLIPSOID) return 1;
+  if (t2 == mjhipGEOM_CYLINDER) return t1 == mjhipGEOM_CAPSULE || t1 == mjhipGEOM_CYLINDER ||
+                                        t1 == mjhipGEOM_ELLIPSOID;
+  if (t2 == mjhipGEOM_BOX) return t1 == mjhipGEOM_ELLIPSOID || t1 == mjhipGEOM_CYLINDER;
+  return 0;
+}
+
 /* mjCOLLISIONFUNC (:41-52) for type-ordered t1 <= t2: 0 = no function, otherwise the most
  * contacts the function returns when it is one of the primitives restated here, or -1 for a
  * function outside the subset (mjc_Convex, height fields, SDFs) */
-static int or_collisionFunc(int t1, int t2) {
+static int or_collisionFunc(const mjhipModel* m, int t1, int t2) {
   static const int table[9][9] = {
     /*           PLANE HFIELD SPHERE CAPSULE ELLIPS CYL BOX MESH SDF */
-    /*PLANE  */ {0,    0,     1,     2,      -1,    4,  4,  -1,  -1},
+    /*PLANE  */ {0,    0,     1,     2,      1,     4,  4,  -1,  -1},
     /*HFIELD */ {0,    0,     -1,    -1,     -1,    -1, -1, -1,  -1},
-    /*SPHERE */ {0,    0,     1,     1,      -1,    1,  1,  -1,  -1},
-    /*CAPSULE*/ {0,    0,     0,     2,      -1,    -1, 2,  -1,  -1},
-    /*ELLIPS */ {0,    0,     0,     0,      -1,    -1, -1, -1,  -1},
-    /*CYL    */ {0,    0,     0,     0,      0,     -1, -1, -1,  -1},
+    /*SPHERE */ {0,    0,     1,     1,      1,     1,  1,  -1,  -1},
+    /*CAPSULE*/ {0,    0,     0,     2,      1,     1,  2,  -1,  -1},
+    /*ELLIPS */ {0,    0,     0,     0,      1,     1,  1,  -1,  -1},
+    /*CYL    */ {0,    0,     0,     0,      0,     1,  1,  -1,  -1},
     /*BOX    */ {0,    0,     0,     0,      0,     0,  24, -1,  -1},
     /*MESH   */ {0,    0,     0,     0,      0,     0,  0,  -1,  -1},
     /*SDF    */ {0,    0,     0,     0,      0,     0,  0,  0,   -1}};
   if (t1 < 0 || t2 < 0 || t1 > 8 || t2 > 8) return -1;
-  return table[t1][t2];
+  const int k = table[t1][t2];
+  if (k > 0 && or_isConvexPair(t1, t2)) {
+    /* mjc_Convex with the libccd MPR fallback, or MULTICCD's perturbed extra contacts (pairs
+       without a sphere or ellipsoid, convex.c:936-999): not restated */
+    if (mjDISABLED(mjhipDSBL_NATIVECCD)) return -1;
+    if (mjENABLED(mjhipENBL_MULTICCD) && t1 != mjhipGEOM_SPHERE && t1 != mjhipGEOM_ELLIPSOID &&
+        t2 != mjhipGEOM_ELLIPSOID) {
+      return -1;
+    }
+  }
+  return k;
 }
 
 /* add_pair :937-990: geom-level (OR over the body's geoms) bitmask check, ordered ids */
@@ -2850,7 +3824,7 @@ static void or_contactBounds(const mjhipModel* m, int* ncon, int* nrow) {
         for (int g2 = m->body_geomadr[b2]; g2 < m->body_geomadr[b2] + m->body_geomnum[b2]; g2++) {
           int t1 = mjMIN(m->geom_type[g1], m->geom_type[g2]);
           int t2 = mjMAX(m->geom_type[g1], m->geom_type[g2]);
-          int k = or_collisionFunc(t1, t2);
+          int k = or_collisionFunc(m, t1, t2);
           if (k > 0 && !or_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
                                          m->geom_contype[g2], m->geom_conaffinity[g2])) {
             int condim = or_pairCondim(m, g1, g2);
@@ -2896,7 +3870,7 @@ int or_efcCapacity(const mjhipModel* m) {
 static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, int g1, int g2) {
   if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
-  const int kmax = or_collisionFunc(t1, t2);
+  const int kmax = or_collisionFunc(m, t1, t2);
   if (kmax == 0) return;
   if (or_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1], m->geom_contype[g2],
                        m->geom_conaffinity[g2])) {
@@ -2937,6 +3911,10 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
   } else if (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX) {
     num = col_boxBox(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
     if (num) num = or_boxBoxFilter(raw, num, margin, pos1, mat1, size1, pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_ELLIPSOID) {
+    num = col_planeConvex(raw, m, d, g1, g2, margin);
+  } else if (or_isConvexPair(t1, t2)) {
+    num = col_convex(raw, m, d, g1, g2, margin);
   }
   if (!num) return;
   int condim;

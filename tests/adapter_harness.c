@@ -76,6 +76,8 @@ HX* hx_create(const mjhipModel* hm, long narena) {
   memcpy(m->opt.o_solref, hm->opt.o_solref, sizeof(m->opt.o_solref));
   memcpy(m->opt.o_solimp, hm->opt.o_solimp, sizeof(m->opt.o_solimp));
   memcpy(m->opt.o_friction, hm->opt.o_friction, sizeof(m->opt.o_friction));
+  m->opt.ccd_tolerance = hm->opt.ccd_tolerance;
+  m->opt.ccd_iterations = hm->opt.ccd_iterations;
   m->opt.integrator = hm->opt.integrator;
   m->opt.cone = hm->opt.cone;
   m->opt.jacobian = hm->opt.jacobian;

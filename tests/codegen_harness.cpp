@@ -61,9 +61,9 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
       else constraint_part<false, false>(m, mr, inst);
     }
   }
-  for (int i = 0; i < B; i++) {         // the sensor/energy pass (k_sensors on the device)
+  for (int i = 0; i < B; i++) {   // transmission/sensor/energy pass (k_sensors on the device)
     mjh::Lane<64> d = lane_view(mr, i / 64, i % 64);
-    mjh::sensorsAfter<64>(*m, d);
+    mjh::sensorsAfter<64>(*m, d, true, mjh_needTrnAfter(m) != 0);
   }
   size_t off = 0;
 #define XD(name, d0, d1, stage) { int S = mr.name##_n; \

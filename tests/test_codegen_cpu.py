@@ -223,3 +223,34 @@ def test_generated_with_energy():
   assert codegen.fast_path_supported(m) is None
   q, v, a = sample_states(m, 32, first=500, margin=-0.1, resample_tendons=False)
   run_and_compare(m, "humanoid_energy", q, v, a)
+
+
+def test_generated_site_slidercrank_body_transmissions():
+  """Slider-crank, site (with and without a reference site) and body (adhesion)
+  transmissions on the straight-line path: the generated kernels skip them and
+  mjh::transmissionAfter computes them (and their actuator_velocity) after the constraint
+  part, the body ones from the instance's contacts. Every output equals the oracle's; the
+  slider-crank model (BASELINE.json config 1) also exercises its capsule-cylinder pair."""
+  import sys
+  sys.path.insert(0, HERE)
+  from test_transmission_cpu import ADHESION, REFSITE, XML
+  m = mjcf.load_xml_string(XML)
+  assert codegen.fast_path_supported(m) is None and 4 in set(int(t) for t in m.actuator_trntype)
+  q, v, a = sample_states(m, 40, first=9)
+  run_and_compare(m, "sitetrn", q, v, a)
+  m = mjcf.load_xml_string(REFSITE)
+  rng = np.random.default_rng(8)
+  q, v, a = rng.uniform(-1, 1, (24, m.nq)), rng.normal(size=(24, m.nv)), rng.normal(size=(24, m.nv))
+  run_and_compare(m, "refsite", q, v, a)
+  m = models.load("slider_crank")
+  assert codegen.fast_path_supported(m) is None and codegen.constraint_mode(m) == "all"
+  rng = np.random.default_rng(11)
+  q = rng.uniform(-np.pi, np.pi, (64, m.nq))
+  run_and_compare(m, "slider_crank", q, rng.normal(size=(64, m.nv)), rng.normal(size=(64, m.nv)))
+  m = mjcf.load_xml_string(ADHESION.format(cone="pyramidal", condim=3, margin=0.01, gap=0.005,
+                                           z=0.1))
+  q = np.tile(m.qpos0, (32, 1))
+  q[:, 2] = 0.1 + 0.03 * rng.normal(size=32)
+  q[:, 7:9] = q[:, 0:2] + rng.uniform(-0.4, 0.4, (32, 2))
+  q[:, 9] = 0.1 + 0.05 * rng.normal(size=32)
+  run_and_compare(m, "adhesion", q, rng.normal(size=(32, m.nv)), rng.normal(size=(32, m.nv)))

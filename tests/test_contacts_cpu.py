@@ -269,10 +269,12 @@ def test_box_cylinder_device_bitexact():
 
 
 def test_unimplemented_pair_flagged_per_instance():
-  """A cylinder-box pair (mjc_Convex, outside the subset) adds no capacity; an instance
-  whose pair passes the bounding-sphere filter is flagged MJHIP_INST_UNSUPPORTED, the others
-  are exact (here: the plane-sphere contact of the same instance is still made)."""
-  m = mjcf.load_xml_string("""<mujoco><worldbody><geom type="plane" size="5 5 .1"/>
+  """A cylinder-box pair under mjDSBL_NATIVECCD (mjc_Convex on libccd's MPR, outside the
+  subset) adds no capacity; an instance whose pair passes the bounding-sphere filter is
+  flagged MJHIP_INST_UNSUPPORTED, the others are exact (here: the plane-sphere contact of the
+  same instance is still made)."""
+  m = mjcf.load_xml_string("""<mujoco><option><flag nativeccd="disable"/></option><worldbody>
+    <geom type="plane" size="5 5 .1"/>
     <geom type="box" size=".5 .5 .5" pos="0 0 2" contype="3" conaffinity="3"/>
     <body pos="0 0 2"><freejoint/><geom type="cylinder" size=".1 .1" contype="2"
       conaffinity="2"/><geom type="sphere" size=".1" pos="0 0 -.1" contype="1"

@@ -1,0 +1,207 @@
+"""Convex pairs: mjc_Convex on the native GJK/EPA solver (engine_collision_convex.c:915-1001,
+engine_collision_gjk.c:2215-2343) and mjc_PlaneConvex for ellipsoids (convex.c:1045-1080).
+
+Pins:
+  * closed-form answers where the geometry has one: plane-ellipsoid (exact), coaxial
+    cylinders and a capsule resting across a cylinder's cap (shallow GJK distance and deep
+    EPA depth), a sphere against a round ellipsoid (the sphere-sphere answer), a box against
+    an ellipsoid; GJK/EPA stop at ccd_tolerance, so the iterative cases are checked to it;
+  * the reference's model/slider_crank/slider_crank.xml (BASELINE.json config 1) has a
+    capsule-cylinder pair, which no longer flags any state;
+  * the device pipeline compiled for the host equals the oracle bit for bit on every contact,
+    row and output over random poses of every convex pair type, shallow and deep, with margins;
+  * what stays outside: the libccd fallback (mjDSBL_NATIVECCD) and MULTICCD's extra contacts
+    flag the instance, as before.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from kernel_harness import KernelCPU
+from mujoco_inversedynamicstest_amd import fields, host, mjcf, models
+from oracle.oracle import CON_DOUBLE, CON_INT, Oracle, lib as olib
+
+TOL = 1e-6        # mjOption ccd_tolerance default (engine_io.c:128)
+
+
+def _one(xml):
+  m = mjcf.load_xml_string(xml)
+  o = Oracle(m)
+  o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+  return m, o
+
+
+def test_plane_ellipsoid_exact():
+  """mjc_PlaneConvex: the support point along -normal; level ellipsoid, then tilted."""
+  m, o = _one("""<mujoco><worldbody><geom type="plane" size="1 1 1"/>
+    <body pos=".1 .2 .25"><freejoint/><geom type="ellipsoid" size=".2 .1 .3"/></body>
+    </worldbody></mujoco>""")
+  assert o.efc.ncon == 1 and o.d.status == 0
+  assert o.contact_field("con_dist")[0] == pytest.approx(-0.05, abs=1e-15)
+  np.testing.assert_allclose(o.contact_field("con_pos")[0], [0.1, 0.2, -0.025], atol=1e-15)
+  np.testing.assert_allclose(o.contact_field("con_frame")[0][:3], [0, 0, 1])
+  # rotated 90 degrees about x: the y semi-axis (.1) points down
+  m, o = _one("""<mujoco><worldbody><geom type="plane" size="1 1 1"/>
+    <body pos="0 0 .08" euler="90 0 0"><freejoint/><geom type="ellipsoid" size=".2 .1 .3"/>
+    </body></worldbody></mujoco>""")
+  assert o.efc.ncon == 1
+  assert o.contact_field("con_dist")[0] == pytest.approx(-0.02, abs=1e-14)
+
+
+def test_cylinders_and_capsule_on_cap():
+  """Coaxial cylinders overlapping by .03 (GJK intersection, EPA depth, normal +z from the
+  lower to the upper), a capsule lying across a cylinder's cap (shallow: segment-to-cylinder
+  distance less the radius) and pushed in deeper (EPA on the full capsule)."""
+  m, o = _one("""<mujoco><option gravity="0 0 0"/><worldbody>
+    <body><freejoint/><geom type="cylinder" size=".2 .1"/></body>
+    <body pos=".05 0 .17"><freejoint/><geom type="cylinder" size=".1 .1"/></body>
+    </worldbody></mujoco>""")
+  assert o.efc.ncon == 1
+  assert o.contact_field("con_dist")[0] == pytest.approx(-0.03, abs=TOL)
+  np.testing.assert_allclose(o.contact_field("con_frame")[0][:3], [0, 0, 1], atol=TOL)
+  assert o.contact_field("con_pos")[0][2] == pytest.approx(0.085, abs=TOL)
+  for z, depth in ((0.18, -0.02), (0.10, -0.10)):
+    m, o = _one(f"""<mujoco><option gravity="0 0 0"/><worldbody>
+      <body><freejoint/><geom type="cylinder" size=".2 .1"/></body>
+      <body pos=".05 0 {z}"><freejoint/><geom type="capsule" fromto="-.1 0 0 .1 0 0"
+        size=".1"/></body></worldbody></mujoco>""")
+    assert o.efc.ncon == 1
+    assert o.contact_field("con_dist")[0] == pytest.approx(depth, abs=TOL)
+    # capsule (type 3) is geom 1 of the pair: the normal points down into the cylinder
+    np.testing.assert_allclose(o.contact_field("con_frame")[0][:3], [0, 0, -1], atol=1e-6)
+    assert o.contact_field("con_pos")[0][2] == pytest.approx(0.1 + depth / 2, abs=TOL)
+
+
+def test_sphere_round_ellipsoid_and_box_ellipsoid():
+  """A round ellipsoid is a sphere: the sphere-sphere depth and normal along the centres; an
+  ellipsoid standing on a box's top face: depth = overlap along z."""
+  c = np.array([0.12, 0.08, 0.24])
+  m, o = _one(f"""<mujoco><option gravity="0 0 0"/><worldbody>
+    <body><freejoint/><geom type="sphere" size=".2"/></body>
+    <body pos="{c[0]} {c[1]} {c[2]}"><freejoint/><geom type="ellipsoid" size=".15 .15 .15"/>
+    </body></worldbody></mujoco>""")
+  assert o.efc.ncon == 1
+  assert o.contact_field("con_dist")[0] == pytest.approx(np.linalg.norm(c) - 0.35, abs=TOL)
+  np.testing.assert_allclose(o.contact_field("con_frame")[0][:3], c / np.linalg.norm(c),
+                             atol=1e-5)
+  m, o = _one("""<mujoco><option gravity="0 0 0"/><worldbody>
+    <body><freejoint/><geom type="box" size=".2 .2 .1"/></body>
+    <body pos=".05 0 .27"><freejoint/><geom type="ellipsoid" size=".1 .15 .2"/></body>
+    </worldbody></mujoco>""")
+  assert o.efc.ncon == 1
+  assert o.contact_field("con_dist")[0] == pytest.approx(-0.03, abs=10 * TOL)
+  np.testing.assert_allclose(o.contact_field("con_frame")[0][:3], [0, 0, -1], atol=1e-5)
+
+
+def test_separated_pairs_make_no_contact():
+  """Inside the bounding spheres but apart: GJK finds a separating direction (no contact),
+  or, with a margin wider than the gap, reports the gap as a contact inside the margin."""
+  xml = """<mujoco><option gravity="0 0 0"/><worldbody>
+    <body><freejoint/><geom type="cylinder" size=".2 .1" margin="{mg}"/></body>
+    <body pos=".25 0 .25" euler="0 45 0"><freejoint/><geom type="cylinder" size=".1 .1"
+      margin="{mg}"/></body></worldbody></mujoco>"""
+  m, o = _one(xml.format(mg=0))
+  assert o.efc.ncon == 0 and o.d.status == 0
+  m, o = _one(xml.format(mg=0.2))
+  assert o.efc.ncon == 1
+  dist = o.contact_field("con_dist")[0]
+  assert 0 < dist < 0.2
+  assert o.contact_field("con_includemargin")[0] == pytest.approx(0.2)
+
+
+_PAIRS = """<mujoco><option gravity="0 0 0"/><default><geom margin="{mg}"/></default>
+  <worldbody><geom type="plane" size="3 3 .1" pos="0 0 -1"/>
+  <body pos="0 0 0"><freejoint/><geom type="{t1}" size="{s1}"/></body>
+  <body pos=".1 0 .2"><freejoint/><geom type="{t2}" size="{s2}"/></body>
+  </worldbody></mujoco>"""
+_SIZES = {"sphere": ".15", "capsule": ".08 .15", "ellipsoid": ".15 .1 .2", "cylinder": ".12 .15",
+          "box": ".15 .1 .12"}
+_CASES = [("sphere", "ellipsoid"), ("capsule", "ellipsoid"), ("capsule", "cylinder"),
+          ("ellipsoid", "ellipsoid"), ("ellipsoid", "cylinder"), ("ellipsoid", "box"),
+          ("cylinder", "cylinder"), ("cylinder", "box")]
+CON_FIELDS = [n for n, _ in CON_DOUBLE] + [n for n, _ in CON_INT]
+EFC_FIELDS = ("efc_J", "efc_pos", "efc_margin", "efc_frictionloss", "efc_diagApprox",
+              "efc_KBIP", "efc_D", "efc_R", "efc_vel", "efc_aref", "efc_force", "efc_type",
+              "efc_id", "efc_state")
+
+
+def _random_pose(rng, q, b, spread):
+  q[7*b:7*b + 3] = rng.uniform(-spread, spread, 3)
+  qq = rng.normal(size=4)
+  q[7*b + 3:7*b + 7] = qq / np.linalg.norm(qq)
+
+
+@pytest.mark.parametrize("t1,t2", _CASES)
+@pytest.mark.parametrize("mg", [0, 0.02])
+def test_device_code_bitexact(t1, t2, mg):
+  """Random relative poses (overlapping, touching, apart): the device pipeline on the host
+  equals the oracle bit for bit on every contact field, row and output."""
+  m = mjcf.load_xml_string(_PAIRS.format(t1=t1, t2=t2, s1=_SIZES[t1], s2=_SIZES[t2], mg=mg))
+  o, k = Oracle(m), KernelCPU(m)
+  rng = np.random.default_rng(_CASES.index((t1, t2)) * 10 + int(mg * 100))
+  width = dict(CON_DOUBLE + CON_INT)
+  hits = 0
+  for i in range(60):
+    q = m.qpos0.copy()
+    _random_pose(rng, q, 0, 0.05)
+    _random_pose(rng, q, 1, 0.2)
+    v, a = rng.normal(size=m.nv), rng.normal(size=m.nv)
+    o.inverse(q, v, a)
+    _, st = k.inverse(q, v, a)
+    assert st == o.d.status == 0, (i, st, o.d.status)
+    ncon = o.efc.ncon
+    hits += ncon
+    assert k.field("con_count")[0] == ncon
+    for name in CON_FIELDS:
+      ref = o.contact_field(name).reshape(ncon, width[name])
+      np.testing.assert_array_equal(k.field(name)[:ref.size].reshape(ncon, width[name]), ref,
+                                    err_msg=f"{name} inst {i}")
+    for name in EFC_FIELDS:
+      ref = o.efc_field(name)
+      np.testing.assert_array_equal(k.field(name)[:ref.size], ref, err_msg=f"{name} inst {i}")
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name),
+                                      err_msg=f"{f.name} inst {i}")
+  assert hits >= 15, hits
+
+
+def test_slider_crank_no_longer_flagged():
+  """BASELINE.json config 1's model: its capsule-cylinder pair (mjc_Convex) used to flag
+  about 30% of uniform states MJHIP_INST_UNSUPPORTED; every state is computed now, and the
+  device code on the host equals the oracle bit for bit."""
+  m = models.load("slider_crank")
+  rng = np.random.default_rng(11)
+  q, v, a = (rng.uniform(-np.pi, np.pi, (200, 3)), rng.normal(size=(200, 3)),
+             rng.normal(size=(200, 3)))
+  o, k = Oracle(m), KernelCPU(m)
+  contacts = 0
+  for i in range(200):
+    f = o.inverse(q[i], v[i], a[i])
+    g, st = k.inverse(q[i], v[i], a[i])
+    assert o.d.status == st == 0
+    contacts += o.efc.ncon
+    np.testing.assert_array_equal(g, f)
+  assert contacts > 20
+
+
+def test_outside_the_native_single_contact_path_is_flagged():
+  """mjDSBL_NATIVECCD (libccd's MPR) and mjENBL_MULTICCD on a pair without a sphere or an
+  ellipsoid (the perturbed extra contacts) are not built: such a pair adds no capacity and an
+  instance where it passes the filters is flagged; MULTICCD with an ellipsoid is computed
+  (the reference takes the single-contact path for it)."""
+  base = """<mujoco><option gravity="0 0 0">{flag}</option><worldbody>
+    <body><freejoint/><geom type="cylinder" size=".2 .1"/></body>
+    <body pos=".05 0 .17"><freejoint/><geom type="{t2}" size="{s2}"/></body>
+    </worldbody></mujoco>"""
+  for flag, t2, s2, want in (('<flag nativeccd="disable"/>', "cylinder", ".1 .1", 32),
+                             ('<flag multiccd="enable"/>', "cylinder", ".1 .1", 32),
+                             ('<flag multiccd="enable"/>', "ellipsoid", ".1 .1 .1", 0)):
+    m = mjcf.load_xml_string(base.format(flag=flag, t2=t2, s2=s2))
+    cm = host.model_struct(m)
+    assert olib().or_contactCapacity(ctypes.byref(cm)) == (0 if want else 1)
+    o, k = Oracle(m), KernelCPU(m)
+    o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+    _, st = k.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
+    assert o.d.status == st == want, (flag, t2)

@@ -1,0 +1,103 @@
+"""GPU parity of the convex pairs (mjc_Convex on native GJK/EPA, mjc_PlaneConvex for
+ellipsoids): the HIP engine vs the CPU oracle on the same states.
+
+Counts, statuses, contact geoms and row types are exact. Floating-point outputs are held to
+the north-star bar (1e-10 normwise relative per instance, test_gpu.py). GJK and EPA are
+iterative (they stop at ccd_tolerance), and the device's kinematics contract multiply-adds,
+so an input differing in its last bit could in principle end an iteration one step earlier;
+the host build of the same device code equals the oracle bit for bit (test_convex_cpu.py),
+and the errors seen here are reported.
+"""
+import numpy as np
+import pytest
+
+from mujoco_inversedynamicstest_amd import engine, mjcf, models
+from oracle.oracle import Oracle
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-10
+
+
+def _err(gpu, cpu):
+  gpu = np.asarray(gpu).reshape(len(gpu), -1)
+  cpu = np.asarray(cpu).reshape(len(cpu), -1)
+  scale = np.maximum(1.0, np.abs(cpu).max(axis=1))
+  return np.abs(gpu - cpu).max(axis=1) / scale
+
+
+def _run(m, q, v, a):
+  B = len(q)
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    f, st = e.inverse(q, v, a, status=True)
+    ncon = e.field_int("con_count", 0, B)[:, 0]
+    nefc = e.field_int("efc_count", 0, B)[:, 0]
+    geoms = e.field_int("con_geom", 0, B)
+    dist = e.field("con_dist", 0, B)
+  finally:
+    e.close()
+  o = Oracle(m)
+  ref, rst, rncon, rnefc, rgeoms, rdist = [], [], [], [], [], []
+  for i in range(B):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    rst.append(o.d.status)
+    rncon.append(o.efc.ncon)
+    rnefc.append(o.efc.nefc)
+    rgeoms.append(o.contact_field("con_geom").ravel())
+    rdist.append(o.contact_field("con_dist").ravel())
+  np.testing.assert_array_equal(st, rst)
+  np.testing.assert_array_equal(ncon, rncon)
+  np.testing.assert_array_equal(nefc, rnefc)
+  for i in range(B):
+    np.testing.assert_array_equal(geoms[i, :2 * rncon[i]], rgeoms[i])
+  derr = max((np.abs(dist[i, :rncon[i]] - rdist[i]).max() for i in range(B) if rncon[i]),
+             default=0.0)
+  return f, np.array(ref), np.array(rncon), derr
+
+
+def test_slider_crank_every_state_computed():
+  """BASELINE.json config 1's model over uniform crank angles: no state is flagged any more
+  (the capsule-cylinder pair runs mjc_Convex), results match the oracle."""
+  m = models.load("slider_crank")
+  B = 512
+  rng = np.random.default_rng(11)
+  q = rng.uniform(-np.pi, np.pi, (B, 3))
+  v, a = rng.normal(size=(B, 3)), rng.normal(size=(B, 3))
+  f, ref, ncon, derr = _run(m, q, v, a)
+  assert ncon.sum() > 50
+  err = _err(f, ref)
+  print(f"slider_crank: {int((ncon > 0).sum())} instances with contacts, max qfrc_inverse "
+        f"error {err.max():.2e}, max con_dist error {derr:.2e}")
+  assert err.max() <= RTOL
+
+
+_MODEL = """<mujoco><option gravity="0 0 -9.81"/><worldbody>
+  <geom type="plane" size="5 5 .1"/>
+  <body pos="0 0 .3"><freejoint/><geom type="ellipsoid" size=".15 .1 .2"/></body>
+  <body pos=".5 0 .3"><freejoint/><geom type="cylinder" size=".12 .15"/></body>
+  <body pos=".5 .2 .3"><freejoint/><geom type="capsule" size=".08 .15"/></body>
+  <body pos="0 .3 .3"><freejoint/><geom type="box" size=".15 .1 .12"/></body>
+  <body pos=".2 .5 .3"><freejoint/><geom type="sphere" size=".12"/></body>
+</worldbody></mujoco>"""
+
+
+def test_convex_pairs_parity():
+  """Five free bodies (ellipsoid, cylinder, capsule, box, sphere) packed closely above a
+  plane: plane-ellipsoid, sphere/capsule-ellipsoid, capsule-cylinder, ellipsoid-cylinder/box,
+  cylinder-box and the primitive pairs, all on the device at once."""
+  m = mjcf.load_xml_string(_MODEL)
+  B = 1024
+  rng = np.random.default_rng(5)
+  q = np.tile(m.qpos0, (B, 1))
+  for b in range(5):
+    q[:, 7*b:7*b + 2] = rng.uniform(-0.25, 0.25, (B, 2))
+    q[:, 7*b + 2] = rng.uniform(0.05, 0.35, B)
+    qq = rng.normal(size=(B, 4))
+    q[:, 7*b + 3:7*b + 7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
+  v, a = rng.normal(size=(B, m.nv)), rng.normal(size=(B, m.nv))
+  f, ref, ncon, derr = _run(m, q, v, a)
+  assert ncon.sum() > 2 * B
+  err = _err(f, ref)
+  print(f"convex pairs: {int(ncon.sum())} contacts, max qfrc_inverse error {err.max():.2e}, "
+        f"instances above {RTOL}: {int((err > RTOL).sum())}, max con_dist error {derr:.2e}")
+  assert err.max() <= RTOL
