@@ -116,6 +116,7 @@
   X(mjtNum,  geom_pos,             ngeom,     3) \
   X(mjtNum,  geom_quat,            ngeom,     4) \
   X(mjtNum,  geom_friction,        ngeom,     3) \
+  X(mjtNum,  geom_fluid,           ngeom,     12) \
   X(mjtNum,  geom_margin,          ngeom,     1) \
   X(mjtNum,  geom_gap,             ngeom,     1) \
   X(int,     site_type,            nsite,     1) \

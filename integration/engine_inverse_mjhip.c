@@ -20,7 +20,7 @@
  * included (rules of engine_core_constraint.c:668-671, :811-814, :949-952).
  *
  * Models are checked for features the device path does not implement and which mjhipModel
- * does not carry (the ellipsoid fluid model, explicit contact pairs, flexes, plugins):
+ * does not carry (explicit contact pairs, flexes, plugins):
  * such a model is an mju_error, never a silently different result.
  *
  * Build (in the reference tree): drop engine_inverse.c from src/engine/CMakeLists.txt,
@@ -41,9 +41,6 @@ void* mj_arenaAllocByte(mjData* d, size_t bytes, size_t alignment);
 
 /* features outside the device subset that mjhipModel cannot show; NULL when supported */
 static const char* adapter_unsupported(const mjModel* m) {
-  for (int g = 0; g < m->ngeom; g++) {
-    if (m->geom_fluid[mjNFLUID*g] > 0) return "the ellipsoid fluid model (geom fluidshape)";
-  }
   if (m->npair) return "explicit contact pairs (<contact><pair>)";
   if (m->nflex) return "flexes";
   if (m->nplugin) return "plugins";

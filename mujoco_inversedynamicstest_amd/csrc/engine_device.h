@@ -3882,8 +3882,8 @@ template <class R, class V, class P, class O, class M>
 MJH_HD void transformSpatial(R res, V vec, int flg_force, P newpos, O oldpos, M rot,
                              bool has_rot);
 
-// engine_passive.c:527-585 mj_inertiaBoxFluidModel (the ellipsoid model is rejected by the
-// loader): viscous and quadratic drag of the body's equivalent inertia box, at the COM
+// engine_passive.c:527-585 mj_inertiaBoxFluidModel: viscous and quadratic drag of the body's
+// equivalent inertia box, at the COM
 template <int S>
 MJH_HD void inertiaBoxFluid(const mjhipModel& m, const Lane<S>& d, int i) {
   double lvel[6], wind[6], lwind[6], lfrc[6], bfrc[6], box[3];
@@ -3919,6 +3919,108 @@ MJH_HD void inertiaBoxFluid(const mjhipModel& m, const Lane<S>& d, int i) {
   mulMatVec3(bfrc, d.ximat + 9*i, lfrc);
   mulMatVec3(bfrc + 3, d.ximat + 9*i, lfrc + 3);
   applyFT(m, d, bfrc + 3, bfrc, d.xipos + 3*i, i, d.qfrc_fluid);
+}
+
+// engine_passive.c:650-687 mj_addedMassForces (no accelerations: the reference passes none)
+MJH_HD void addedMassForces(const double v[6], double rho, const double* vm, const double* vi,
+                            double f[6]) {
+  const double lin[3] = {v[3], v[4], v[5]}, ang[3] = {v[0], v[1], v[2]};
+  const double plin[3] = {rho*vm[0]*lin[0], rho*vm[1]*lin[1], rho*vm[2]*lin[2]};
+  const double pang[3] = {rho*vi[0]*ang[0], rho*vi[1]*ang[1], rho*vi[2]*ang[2]};
+  double fa[3], t1[3], t2[3];
+  cross(fa, plin, ang);
+  cross(t1, plin, lin);
+  cross(t2, pang, ang);
+  addTo3(f, t1);
+  addTo3(f, t2);
+  addTo3(f + 3, fa);
+}
+
+MJH_HD double pow4(double x) { return (x*x)*(x*x); }
+
+// engine_passive.c:705-790 mj_viscousForces: Magnus and Kutta-Joukowski lift, Stokes and
+// quadratic (blunt/slender) drag of the equivalent ellipsoid with semi-axes s
+MJH_HD void viscousForces(const double v[6], double rho, double mu, const double s[3],
+                          double magnus, double kutta, double blunt, double slender,
+                          double angdrag, double f[6]) {
+  auto mx = [](double a, double b) { return a > b ? a : b; };
+  auto mn = [](double a, double b) { return a < b ? a : b; };
+  const double lin[3] = {v[3], v[4], v[5]}, ang[3] = {v[0], v[1], v[2]};
+  const double volume = 4.0/3.0 * mjhipPI * s[0] * s[1] * s[2];
+  const double dmax = mx(mx(s[0], s[1]), s[2]);
+  const double dmin = mn(mn(s[0], s[1]), s[2]);
+  const double dmid = s[0] + s[1] + s[2] - dmax - dmin;
+  const double Amax = mjhipPI * dmax * dmid;
+  double mf[3];
+  cross(mf, ang, lin);
+  mf[0] *= magnus * rho * volume;
+  mf[1] *= magnus * rho * volume;
+  mf[2] *= magnus * rho * volume;
+  const double den = pow4(s[1]*s[2]) * (lin[0]*lin[0]) + pow4(s[2]*s[0]) * (lin[1]*lin[1]) +
+                     pow4(s[0]*s[1]) * (lin[2]*lin[2]);
+  const double num = (s[1]*s[2]*lin[0])*(s[1]*s[2]*lin[0]) +
+                     (s[2]*s[0]*lin[1])*(s[2]*s[0]*lin[1]) +
+                     (s[0]*s[1]*lin[2])*(s[0]*s[1]*lin[2]);
+  const double Aproj = mjhipPI * sqrt(den/mx(MINVAL, num));
+  const double nrm[3] = {(s[1]*s[2])*(s[1]*s[2]) * lin[0], (s[2]*s[0])*(s[2]*s[0]) * lin[1],
+                         (s[0]*s[1])*(s[0]*s[1]) * lin[2]};
+  const double linn = sqrt(lin[0]*lin[0] + lin[1]*lin[1] + lin[2]*lin[2]);
+  const double cosa = num / mx(MINVAL, linn * den);
+  double kc[3], kf[3];
+  cross(kc, nrm, lin);
+  kc[0] *= kutta * rho * cosa * Aproj;
+  kc[1] *= kutta * rho * cosa * Aproj;
+  kc[2] *= kutta * rho * cosa * Aproj;
+  cross(kf, kc, lin);
+  const double D = 2.0/3.0 * (s[0] + s[1] + s[2]);
+  const double cf = 3.0 * mjhipPI * D, ct = mjhipPI * D*D*D;
+  const double Imax = 8.0/15.0 * mjhipPI * dmid * pow4(dmax);
+  double II[3];
+  for (int k = 0; k < 3; k++) {          // mji_ellipsoid_max_moment (:697-701)
+    II[k] = 8.0/15.0 * mjhipPI * s[k] * pow4(mx(s[(k+1) % 3], s[(k+2) % 3]));
+  }
+  const double mom[3] = {ang[0] * (angdrag*II[0] + slender*(Imax - II[0])),
+                         ang[1] * (angdrag*II[1] + slender*(Imax - II[1])),
+                         ang[2] * (angdrag*II[2] + slender*(Imax - II[2]))};
+  const double dlin = mu*cf + rho*linn*(Aproj*blunt + slender*(Amax - Aproj));
+  const double dang = mu * ct + rho * sqrt(mom[0]*mom[0] + mom[1]*mom[1] + mom[2]*mom[2]);
+  f[0] -= dang * ang[0];
+  f[1] -= dang * ang[1];
+  f[2] -= dang * ang[2];
+  f[3] += mf[0] + kf[0] - dlin*lin[0];
+  f[4] += mf[1] + kf[1] - dlin*lin[1];
+  f[5] += mf[2] + kf[2] - dlin*lin[2];
+}
+
+// engine_passive.c:588-646 mj_ellipsoidFluidModel over body b's geoms (geom_fluid holds the
+// compiler's coefficients: readFluidGeomInteraction :793-821)
+template <int S>
+MJH_HD void ellipsoidFluid(const mjhipModel& m, const Lane<S>& d, int b) {
+  for (int j = 0; j < m.body_geomnum[b]; j++) {
+    const int g = m.body_geomadr[b] + j;
+    const double* c = m.geom_fluid + 12*g;
+    const double* sz = m.geom_size + 3*g;
+    double ax[3];                         // mju_geomSemiAxes (engine_util_misc.c:425-451)
+    const int t = m.geom_type[g];
+    if (t == mjhipGEOM_SPHERE) { ax[0] = sz[0]; ax[1] = sz[0]; ax[2] = sz[0]; }
+    else if (t == mjhipGEOM_CAPSULE) { ax[0] = sz[0]; ax[1] = sz[0]; ax[2] = sz[1] + sz[0]; }
+    else if (t == mjhipGEOM_CYLINDER) { ax[0] = sz[0]; ax[1] = sz[0]; ax[2] = sz[1]; }
+    else { ax[0] = sz[0]; ax[1] = sz[1]; ax[2] = sz[2]; }
+    if (c[0] == 0.0) continue;
+    double lvel[6], wind[6], lwind[6], lfrc[6], bfrc[6];
+    objectVelocity(m, d, 5, g, lvel, 1);  // mjOBJ_GEOM
+    for (int k = 0; k < 3; k++) { wind[k] = 0; wind[3 + k] = m.opt.wind[k]; }
+    transformSpatial(lwind, wind, 0, d.geom_xpos + 3*g, d.subtree_com + 3*m.body_rootid[b],
+                     d.geom_xmat + 9*g, true);
+    lvel[3] -= lwind[3]; lvel[4] -= lwind[4]; lvel[5] -= lwind[5];
+    for (int k = 0; k < 6; k++) lfrc[k] = 0;
+    addedMassForces(lvel, m.opt.density, c + 6, c + 9, lfrc);
+    viscousForces(lvel, m.opt.density, m.opt.viscosity, ax, c[5], c[4], c[1], c[2], c[3], lfrc);
+    for (int k = 0; k < 6; k++) lfrc[k] = lfrc[k]*c[0];
+    mulMatVec3(bfrc, d.geom_xmat + 9*g, lfrc);
+    mulMatVec3(bfrc + 3, d.geom_xmat + 9*g, lfrc + 3);
+    applyFT(m, d, bfrc + 3, bfrc, d.geom_xpos + 3*g, b, d.qfrc_fluid);
+  }
 }
 
 template <int S>
@@ -3993,12 +4095,18 @@ MJH_HD void passive(const mjhipModel& m, const Lane<S>& d) {
       }
     }
   }
-  // fluid forces (mj_fluid engine_passive.c:402-428)
+  // fluid forces (mj_fluid engine_passive.c:402-428): the ellipsoid model for a body with a
+  // geom that uses it, the inertia-box model otherwise
   const bool has_fluid = m.opt.viscosity > 0 || m.opt.density > 0;
   if (has_fluid) {
     for (int i = 1; i < m.nbody; i++) {
       if (m.body_mass[i] < MINVAL) continue;
-      inertiaBoxFluid(m, d, i);
+      int ell = 0;
+      for (int j = 0; j < m.body_geomnum[i] && ell == 0; j++) {
+        ell += m.geom_fluid[12*(m.body_geomadr[i] + j)] > 0;
+      }
+      if (ell) ellipsoidFluid(m, d, i);
+      else inertiaBoxFluid(m, d, i);
     }
   }
   add(d.qfrc_passive, d.qfrc_spring, d.qfrc_damper, nv);

@@ -448,8 +448,6 @@ def unsupported(ints, arrays) -> str | None:
     return "flexes"
   if ints["nplugin"]:
     return "plugins"
-  if ints["ngeom"] and (arrays["geom_fluid"][:, 0] > 0).any():
-    return "the ellipsoid fluid model (geom fluidshape)"
   if ints["nwrap"] and not np.isin(arrays["wrap_type"], (1, 2, 3, 4, 5)).all():
     return "unknown tendon wrap object type"
   return None

@@ -747,9 +747,14 @@ class MJCFCompiler:
     g["friction"] = [1.0, 0.005, 0.0001]
     g["friction"][:len(fr)] = fr
     g["solmix"] = float(a.get("solmix", 1.0))
-    if a.get("fluidshape", "none") != "none":
-      raise MJCFError("the ellipsoid fluid model (fluidshape) is not in the supported subset; "
-                      "the inertia-box model is")
+    shape = a.get("fluidshape", "none")        # xml_native_reader.cc:1701-1704
+    if shape not in ("none", "ellipsoid"):
+      raise MJCFError(f"invalid fluidshape '{shape}'")
+    g["fluid_ellipsoid"] = 1.0 if shape == "ellipsoid" else 0.0
+    coefs = [0.5, 0.25, 1.5, 1.0, 1.0]         # user_init.c:143-147
+    fc = _floats(a["fluidcoef"]) if "fluidcoef" in a else []
+    coefs[:len(fc)] = fc
+    g["fluid_coefs"] = coefs
     g["solref"] = _floats(a["solref"]) if "solref" in a else [0.02, 1.0]
     si = _floats(a["solimp"]) if "solimp" in a else []
     g["solimp"] = [0.9, 0.95, 0.001, 0.5, 2.0]
@@ -775,6 +780,9 @@ class MJCFCompiler:
           g["mass"] = density * vol
           g["inertia"] = _geom_inertia(t, size, g["mass"])
     g["rbound"] = _geom_rbound(t, size)
+    # fluid-interaction coefficients (user_objects.cc:3081-3084)
+    g["fluid"] = _fluid_coefs(t, size, g["fluid_ellipsoid"], g["fluid_coefs"]) \
+        if g["fluid_ellipsoid"] > 0 else [0.0] * 12
     return g
 
   def compile(self) -> Model:
@@ -1162,6 +1170,7 @@ class MJCFCompiler:
     gpos = arr("geom_pos", (ng, 3), np.float64)
     gquat = arr("geom_quat", (ng, 4), np.float64)
     gfric = arr("geom_friction", (ng, 3), np.float64)
+    gfluid = arr("geom_fluid", (ng, 12), np.float64)
     for gi, g in enumerate(geoms):
       b = bodies[g["body"]]
       if geomadr[b.id] < 0:
@@ -1185,6 +1194,7 @@ class MJCFCompiler:
       gpos[gi] = g["pos"]
       gquat[gi] = g["quat"]
       gfric[gi] = g["friction"]
+      gfluid[gi] = g["fluid"]
       gsf[gi] = _sameframe(g["pos"], g["quat"], b.ipos, b.iquat)
       bcontype[b.id] |= g["contype"]
       bconaff[b.id] |= g["conaffinity"]
@@ -1973,6 +1983,60 @@ def _geom_inertia(t, size, mass):
     return [mass * (s[1]*s[1] + s[2]*s[2]) / 3, mass * (s[0]*s[0] + s[2]*s[2]) / 3,
             mass * (s[0]*s[0] + s[1]*s[1]) / 3]
   return [0.0, 0.0, 0.0]
+
+
+def _added_mass_kappa(dx, dy, dz):
+  """mjCGeom::GetAddedMassKappa (user_objects.cc:2738-2785): 15-point Gauss-Kronrod
+  quadrature of dx dy dz / sqrt((dx^2 + l)^3 (dy^2 + l)(dz^2 + l)) over l in [0, inf), after
+  l = x^3 / (1 - x)^2, in the reference's operation order."""
+  w = (0.01146766, 0.03154605, 0.05239501, 0.07032663, 0.08450236, 0.09517529, 0.10221647,
+       0.10474107, 0.10221647, 0.09517529, 0.08450236, 0.07032663, 0.05239501, 0.03154605,
+       0.01146766)
+  ls = (7.865151709349917e-08, 1.7347976913907274e-05, 0.0003548008144506193,
+        0.002846636252924549, 0.014094260903596077, 0.053063261727396636,
+        0.17041978741317773, 0.5, 1.4036301548686991, 3.9353484827022642,
+        11.644841677041734, 39.53187807410903, 177.5711362220801, 1429.4772912937397,
+        54087.416549217705)
+  ds = (5.538677720489877e-05, 0.002080868285293228, 0.016514126520723166,
+        0.07261900344370877, 0.23985243401862602, 0.6868318249020725, 1.8551129519182894,
+        5.0, 14.060031152313941, 43.28941239611009, 156.58546376397112, 747.9826085305024,
+        5827.4042950027115, 116754.0197944512, 25482945.327264845)
+  ix, iy, iz = 1.0 / (dx * dx), 1.0 / (dy * dy), 1.0 / (dz * dz)
+  scale = math.pow(dx*dx*dx * dy * dz, 0.4)
+  kappa = 0.0
+  for i in range(15):
+    lam = scale * ls[i]
+    denom = (1 + lam*ix) * math.sqrt((1 + lam*ix) * (1 + lam*iy) * (1 + lam*iz))
+    kappa += scale * ds[i] / denom * w[i]
+  return kappa * ix
+
+
+def _fluid_coefs(t, size, ellipsoid, coefs):
+  """mjCGeom::SetFluidCoefs (user_objects.cc:2788-2849): geom_fluid = [ellipsoid flag, the
+  5 coefficients, virtual mass (3), virtual inertia (3)] of the equivalent ellipsoid."""
+  if t == GEOM["sphere"]:
+    dx = dy = dz = size[0]
+  elif t == GEOM["capsule"]:
+    dx, dy, dz = size[0], size[0], size[1] + size[0]
+  elif t == GEOM["cylinder"]:
+    dx, dy, dz = size[0], size[0], size[1]
+  else:
+    dx, dy, dz = size[0], size[1], size[2]
+  volume = 4.0 / 3.0 * mjPI * dx * dy * dz
+  kx = _added_mass_kappa(dx, dy, dz)
+  ky = _added_mass_kappa(dy, dz, dx)
+  kz = _added_mass_kappa(dz, dx, dy)
+  p2 = lambda v: v * v                       # noqa: E731
+  ixf = p2(dy*dy - dz*dz) * abs(kz - ky) / max(
+      mjEPS, abs(2*(dy*dy - dz*dz) + (dy*dy + dz*dz)*(ky - kz)))
+  iyf = p2(dz*dz - dx*dx) * abs(kx - kz) / max(
+      mjEPS, abs(2*(dz*dz - dx*dx) + (dz*dz + dx*dx)*(kz - kx)))
+  izf = p2(dx*dx - dy*dy) * abs(ky - kx) / max(
+      mjEPS, abs(2*(dx*dx - dy*dy) + (dx*dx + dy*dy)*(kx - ky)))
+  vm = [volume * kx / max(mjEPS, 2 - kx), volume * ky / max(mjEPS, 2 - ky),
+        volume * kz / max(mjEPS, 2 - kz)]
+  vi = [volume*ixf/5, volume*iyf/5, volume*izf/5]
+  return [float(ellipsoid)] + [float(c) for c in coefs] + vm + vi
 
 
 def _geom_rbound(t, size):

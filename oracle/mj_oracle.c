@@ -5147,14 +5147,124 @@ static void or_inertiaBoxFluid(const mjhipModel* m, mjhipData* d, int i) {
   mj_applyFT(m, d, bfrc+3, bfrc, d->xipos+3*i, i, d->qfrc_fluid);
 }
 
-/* engine_passive.c:402-428 mj_fluid (inertia-box model; the ellipsoid model is rejected by
- * the loader) */
+/* engine_passive.c:650-687 mj_addedMassForces without accelerations */
+static void or_addedMass(const mjtNum v[6], mjtNum rho, const mjtNum vm[3], const mjtNum vi[3],
+                         mjtNum f[6]) {
+  const mjtNum lin[3] = {v[3], v[4], v[5]}, ang[3] = {v[0], v[1], v[2]};
+  const mjtNum plin[3] = {rho*vm[0]*lin[0], rho*vm[1]*lin[1], rho*vm[2]*lin[2]};
+  const mjtNum pang[3] = {rho*vi[0]*ang[0], rho*vi[1]*ang[1], rho*vi[2]*ang[2]};
+  mjtNum fa[3], t1[3], t2[3];
+  mju_cross(fa, plin, ang);
+  mju_cross(t1, plin, lin);
+  mju_cross(t2, pang, ang);
+  mju_addTo3(f, t1);
+  mju_addTo3(f, t2);
+  mju_addTo3(f+3, fa);
+}
+
+static mjtNum or_pow4(mjtNum x) { return (x*x)*(x*x); }
+
+/* engine_passive.c:697-701 */
+static mjtNum or_maxMoment(const mjtNum s[3], int k) {
+  const mjtNum d0 = s[k], d1 = s[(k+1) % 3], d2 = s[(k+2) % 3];
+  return 8.0/15.0 * mjhipPI * d0 * or_pow4(mjMAX(d1, d2));
+}
+
+/* engine_passive.c:705-790 mj_viscousForces */
+static void or_viscousForces(const mjtNum v[6], mjtNum rho, mjtNum mu, const mjtNum s[3],
+                             mjtNum magnus, mjtNum kutta, mjtNum blunt, mjtNum slender,
+                             mjtNum angdrag, mjtNum f[6]) {
+  const mjtNum lin[3] = {v[3], v[4], v[5]}, ang[3] = {v[0], v[1], v[2]};
+  const mjtNum volume = 4.0/3.0 * mjhipPI * s[0] * s[1] * s[2];
+  const mjtNum dmax = mjMAX(mjMAX(s[0], s[1]), s[2]);
+  const mjtNum dmin = mjMIN(mjMIN(s[0], s[1]), s[2]);
+  const mjtNum dmid = s[0] + s[1] + s[2] - dmax - dmin;
+  const mjtNum Amax = mjhipPI * dmax * dmid;
+  mjtNum mf[3];
+  mju_cross(mf, ang, lin);
+  mf[0] *= magnus * rho * volume;
+  mf[1] *= magnus * rho * volume;
+  mf[2] *= magnus * rho * volume;
+  const mjtNum den = or_pow4(s[1]*s[2]) * (lin[0]*lin[0]) + or_pow4(s[2]*s[0]) * (lin[1]*lin[1]) +
+                     or_pow4(s[0]*s[1]) * (lin[2]*lin[2]);
+  const mjtNum num = (s[1]*s[2]*lin[0])*(s[1]*s[2]*lin[0]) + (s[2]*s[0]*lin[1])*(s[2]*s[0]*lin[1]) +
+                     (s[0]*s[1]*lin[2])*(s[0]*s[1]*lin[2]);
+  const mjtNum Aproj = mjhipPI * sqrt(den/mjMAX(mjMINVAL, num));
+  const mjtNum nrm[3] = {(s[1]*s[2])*(s[1]*s[2]) * lin[0], (s[2]*s[0])*(s[2]*s[0]) * lin[1],
+                         (s[0]*s[1])*(s[0]*s[1]) * lin[2]};
+  const mjtNum cosa = num / mjMAX(mjMINVAL, mju_norm3(lin) * den);
+  mjtNum kc[3], kf[3];
+  mju_cross(kc, nrm, lin);
+  kc[0] *= kutta * rho * cosa * Aproj;
+  kc[1] *= kutta * rho * cosa * Aproj;
+  kc[2] *= kutta * rho * cosa * Aproj;
+  mju_cross(kf, kc, lin);
+  const mjtNum D = 2.0/3.0 * (s[0] + s[1] + s[2]);
+  const mjtNum cf = 3.0 * mjhipPI * D, ct = mjhipPI * D*D*D;
+  const mjtNum Imax = 8.0/15.0 * mjhipPI * dmid * or_pow4(dmax);
+  const mjtNum II[3] = {or_maxMoment(s, 0), or_maxMoment(s, 1), or_maxMoment(s, 2)};
+  const mjtNum mom[3] = {ang[0] * (angdrag*II[0] + slender*(Imax - II[0])),
+                         ang[1] * (angdrag*II[1] + slender*(Imax - II[1])),
+                         ang[2] * (angdrag*II[2] + slender*(Imax - II[2]))};
+  const mjtNum dlin = mu*cf + rho*mju_norm3(lin)*(Aproj*blunt + slender*(Amax - Aproj));
+  const mjtNum dang = mu * ct + rho * mju_norm3(mom);
+  f[0] -= dang * ang[0];
+  f[1] -= dang * ang[1];
+  f[2] -= dang * ang[2];
+  f[3] += mf[0] + kf[0] - dlin*lin[0];
+  f[4] += mf[1] + kf[1] - dlin*lin[1];
+  f[5] += mf[2] + kf[2] - dlin*lin[2];
+}
+
+/* engine_util_misc.c:425-451 mju_geomSemiAxes */
+static void or_semiAxes(const mjhipModel* m, int g, mjtNum ax[3]) {
+  const mjtNum* s = m->geom_size + 3*g;
+  switch (m->geom_type[g]) {
+  case mjhipGEOM_SPHERE:   ax[0] = s[0]; ax[1] = s[0]; ax[2] = s[0]; break;
+  case mjhipGEOM_CAPSULE:  ax[0] = s[0]; ax[1] = s[0]; ax[2] = s[1] + s[0]; break;
+  case mjhipGEOM_CYLINDER: ax[0] = s[0]; ax[1] = s[0]; ax[2] = s[1]; break;
+  default:                 ax[0] = s[0]; ax[1] = s[1]; ax[2] = s[2];
+  }
+}
+
+/* engine_passive.c:588-646 mj_ellipsoidFluidModel */
+static void or_ellipsoidFluid(const mjhipModel* m, mjhipData* d, int b) {
+  for (int j = 0; j < m->body_geomnum[b]; j++) {
+    const int g = m->body_geomadr[b] + j;
+    const mjtNum* c = m->geom_fluid + 12*g;    /* readFluidGeomInteraction (:793-821) */
+    mjtNum ax[3], lvel[6], wind[6], lwind[6], lfrc[6], bfrc[6];
+    or_semiAxes(m, g, ax);
+    if (c[0] == 0.0) continue;
+    or_objectVelocity(m, d, OBJ_GEOM, g, lvel, 1);
+    mju_zero(wind, 6);
+    mju_copy3(wind+3, m->opt.wind);
+    mju_transformSpatial(lwind, wind, 0, d->geom_xpos + 3*g,
+                         d->subtree_com + 3*m->body_rootid[b], d->geom_xmat + 9*g);
+    lvel[3] -= lwind[3]; lvel[4] -= lwind[4]; lvel[5] -= lwind[5];
+    mju_zero(lfrc, 6);
+    or_addedMass(lvel, m->opt.density, c + 6, c + 9, lfrc);
+    or_viscousForces(lvel, m->opt.density, m->opt.viscosity, ax, c[5], c[4], c[1], c[2], c[3],
+                     lfrc);
+    mju_scl(lfrc, lfrc, c[0], 6);
+    mju_mulMatVec3(bfrc, d->geom_xmat + 9*g, lfrc);
+    mju_mulMatVec3(bfrc+3, d->geom_xmat + 9*g, lfrc+3);
+    mj_applyFT(m, d, bfrc+3, bfrc, d->geom_xpos + 3*g, b, d->qfrc_fluid);
+  }
+}
+
+/* engine_passive.c:402-428 mj_fluid: the ellipsoid model for a body with a geom that uses
+ * it (geom_fluid[0] > 0), the inertia-box model otherwise */
 static int or_fluid(const mjhipModel* m, mjhipData* d) {
   int has_fluid = m->opt.viscosity > 0 || m->opt.density > 0;
   if (has_fluid) {
     for (int i = 1; i < m->nbody; i++) {
       if (m->body_mass[i] < mjMINVAL) continue;
-      or_inertiaBoxFluid(m, d, i);
+      int ell = 0;
+      for (int j = 0; j < m->body_geomnum[i] && ell == 0; j++) {
+        ell += m->geom_fluid[12*(m->body_geomadr[i] + j)] > 0;
+      }
+      if (ell) or_ellipsoidFluid(m, d, i);
+      else or_inertiaBoxFluid(m, d, i);
     }
   }
   return has_fluid;

@@ -86,7 +86,6 @@ HX* hx_create(const mjhipModel* hm, long narena) {
 #define X(type, name, d0, d1) m->name = hm->name;
   MJHIP_MODEL_POINTERS_M
 #undef X
-  m->geom_fluid = (mjtNum*)calloc((size_t)m->ngeom * mjNFLUID + 1, sizeof(mjtNum));
   m->nconmax = -1;   /* the compiler defaults (mjmodel.h: -1 = no limit but the arena) */
   m->njmax = -1;
 
@@ -120,7 +119,6 @@ void hx_free(HX* h) {
 #undef XD
   free(d->arena);
   free(d);
-  free(h->m->geom_fluid);
   free(h->m);
   free(h);
 }

@@ -1,8 +1,10 @@
-"""Fluid forces on the inverse path (mj_fluid, inertia-box model, engine_passive.c:402-428,
-:527-585) — CPU.
+"""Fluid forces on the inverse path (mj_fluid, engine_passive.c:402-428: the inertia-box model
+:527-585 and the ellipsoid model :588-790) — CPU.
 
-The reference's own fluid tests (engine_passive_test.cc) cover only the ellipsoid model,
-which the loader rejects; the inertia-box model is pinned here by its closed forms:
+The ellipsoid model is pinned by the reference's own tests (engine_passive_test.cc:42-135,
+GeomsEquivalentToBodies and DefaultsPropagate, restated) and by the Stokes limit of a sphere
+(force -6 pi mu r v, torque -8 pi mu r^3 w) and its classical added mass (half the displaced
+volume). The inertia-box model is pinned by its closed forms:
   * Stokes drag of a sphere: the equivalent box of a solid sphere of radius r has sides
     r*sqrt(12/5), so a free sphere translating at v in still fluid feels
     -3*pi*diam*viscosity*(v - wind), diam = r*sqrt(12/5), on its free-joint translation dofs;
@@ -71,7 +73,93 @@ def test_fluid_is_dissipative_and_device_bitexact():
       np.testing.assert_array_equal(getattr(k.d, f), getattr(o.d, f), err_msg=f"{f} {i}")
 
 
-def test_ellipsoid_fluid_model_rejected():
-  with pytest.raises(mjcf.MJCFError):
-    mjcf.load_xml_string("""<mujoco><option viscosity="1"/><worldbody><body><freejoint/>
-      <geom size=".1" fluidshape="ellipsoid"/></body></worldbody></mujoco>""")
+_TWO_BODIES = """<mujoco><option wind="5 5 0" density="10"/><worldbody><body><freejoint/>
+  <body><geom type="box" size=".1 .01 0.01" pos="0.1 0 0" euler="40 0 0" fluidshape="ellipsoid"/>
+  </body>
+  <body><geom type="box" size=".1 .01 0.01" pos="-.1 0 0" euler="0 20 0" fluidshape="ellipsoid"/>
+  </body></body></worldbody></mujoco>"""
+_ONE_BODY = """<mujoco><option wind="5 5 0" density="10"/><worldbody><body pos="1 2 3">
+  <freejoint align="false"/>
+  <geom type="box" size=".1 .01 0.01" pos="0.1 0 0" euler="40 0 0" fluidshape="ellipsoid"/>
+  <geom type="box" size=".1 .01 0.01" pos="-.1 0 0" euler="0 20 0" fluidshape="ellipsoid"/>
+  </body></worldbody></mujoco>"""
+
+
+def test_ellipsoid_geoms_equivalent_to_bodies():
+  """EllipsoidFluidTest.GeomsEquivalentToBodies (engine_passive_test.cc:42-106): two
+  ellipsoid-model geoms on one free body or on two welded child bodies give the same
+  qfrc_passive to 1e-14 (qvel = 1..6, quaternion (.5, .5, .5, .5))."""
+  out = []
+  for xml in (_TWO_BODIES, _ONE_BODY):
+    m = mjcf.load_xml_string(xml)
+    q = m.qpos0.copy()
+    q[3:7] = 0.5
+    o = Oracle(m)
+    o.inverse(q, np.arange(1.0, 7.0), np.zeros(6))
+    out.append(o.d.qfrc_passive.copy())
+  assert np.abs(out[0]).max() > 1e-3
+  np.testing.assert_allclose(out[0], out[1], rtol=0, atol=1e-14)
+
+
+def test_ellipsoid_defaults_propagate():
+  """EllipsoidFluidTest.DefaultsPropagate (engine_passive_test.cc:109-135)."""
+  m = mjcf.load_xml_string("""<mujoco><option wind="5 5 0" density="10"/><default>
+    <geom fluidshape="ellipsoid" fluidcoef="2 3 4 5 6"/><default class="test_class">
+    <geom fluidshape="none" fluidcoef="5 4 3 2 1"/></default></default>
+    <worldbody><body><freejoint/>
+    <geom type="box" size=".1 .01 0.01" pos="0.1 0 0" class="test_class"/>
+    <geom type="box" size=".1 .01 0.01" pos="-0.1 0 0"/></body></worldbody></mujoco>""")
+  np.testing.assert_array_equal(m.geom_fluid[0, :6], [0, 0, 0, 0, 0, 0])
+  np.testing.assert_array_equal(m.geom_fluid[1, :6], [1, 2, 3, 4, 5, 6])
+
+
+def test_ellipsoid_sphere_stokes_and_added_mass():
+  """A sphere in the ellipsoid model: with viscosity only, Stokes' drag -6 pi mu r v and
+  rotational drag -8 pi mu r^3 w exactly (the equivalent sphere diameter is 2r); the
+  compiler's Gauss-Kronrod added-mass coefficient approximates the sphere's kappa = 2/3, so
+  its virtual mass is half the displaced volume and its virtual inertia vanishes."""
+  r, mu = 0.2, 0.7
+  m = mjcf.load_xml_string(f"""<mujoco><option viscosity="{mu}"><flag contact="disable"
+    gravity="disable"/></option><worldbody><body pos="0 0 1"><freejoint/>
+    <geom size="{r}" mass="3" fluidshape="ellipsoid"/></body></worldbody></mujoco>""")
+  vol = 4 / 3 * np.pi * r**3
+  np.testing.assert_allclose(m.geom_fluid[0, 6:9], vol / 2, rtol=1e-5)
+  np.testing.assert_allclose(m.geom_fluid[0, 9:12], 0, atol=1e-12)
+  o = Oracle(m)
+  v = np.array([1.0, -2.0, 0.5, 0.3, -0.4, 0.8])
+  o.inverse(m.qpos0, v, np.zeros(6))
+  np.testing.assert_allclose(o.d.qfrc_fluid[:3], -6 * np.pi * mu * r * v[:3], rtol=1e-12)
+  np.testing.assert_allclose(o.d.qfrc_fluid[3:], -8 * np.pi * mu * r**3 * v[3:], rtol=1e-12)
+
+
+def test_ellipsoid_model_device_bitexact():
+  """Bodies with ellipsoid-model geoms (box, capsule, cylinder, ellipsoid; density, viscosity
+  and wind: added mass, Magnus and Kutta lift, blunt/slender/angular drag) next to an
+  inertia-box body: the device pipeline on the host equals the oracle bit for bit."""
+  m = mjcf.load_xml_string("""<mujoco><option density="1.2" viscosity=".3" wind=".4 -.2 .1">
+    <flag contact="disable"/></option><worldbody>
+    <body pos="0 0 1"><freejoint/><geom type="box" size=".2 .1 .05" fluidshape="ellipsoid"
+      fluidcoef=".4 .3 1.2 .9 1.1"/><geom type="capsule" size=".05 .1" pos=".2 0 0"
+      fluidshape="ellipsoid"/>
+      <body pos="0 .3 0"><joint axis="1 0 0"/><geom type="cylinder" size=".05 .2"
+        fluidshape="ellipsoid"/>
+        <body pos="0 .3 0"><joint axis="0 1 1"/><geom type="ellipsoid" size=".1 .05 .2"
+          fluidshape="ellipsoid"/></body></body></body>
+    <body pos="1 0 1"><freejoint/><geom type="box" size=".1 .2 .3"/></body>
+    </worldbody></mujoco>""")
+  rng = np.random.default_rng(23)
+  o = Oracle(m)
+  k = KernelCPU(m, o.efc.capacity)
+  outs = [f.name for f in fields.DATA_FIELDS if f.stage > 0]
+  for i in range(24):
+    q = m.qpos0.copy()
+    for b in (0, 9):
+      qq = rng.normal(size=4)
+      q[b + 3:b + 7] = qq / np.linalg.norm(qq)
+    q[7:9] = rng.uniform(-1, 1, 2)
+    v, a = 2 * rng.normal(size=m.nv), rng.normal(size=m.nv)
+    o.inverse(q, v, a)
+    k.inverse(q, v, a)
+    assert np.abs(o.d.qfrc_fluid).max() > 1e-3
+    for f in outs:
+      np.testing.assert_array_equal(getattr(k.d, f), getattr(o.d, f), err_msg=f"{f} {i}")

@@ -991,6 +991,40 @@ def test_fluid_parity():
   e.close()
 
 
+def test_ellipsoid_fluid_parity():
+  """The ellipsoid fluid model (added mass, Magnus and Kutta lift, viscous drag; density,
+  viscosity and wind) on box/capsule/cylinder/ellipsoid geoms next to an inertia-box body."""
+  from mujoco_inversedynamicstest_amd import mjcf
+  m = mjcf.load_xml_string("""<mujoco><option density="1.2" viscosity=".3" wind=".4 -.2 .1">
+    <flag contact="disable"/></option><worldbody>
+    <body pos="0 0 1"><freejoint/><geom type="box" size=".2 .1 .05" fluidshape="ellipsoid"
+      fluidcoef=".4 .3 1.2 .9 1.1"/><geom type="capsule" size=".05 .1" pos=".2 0 0"
+      fluidshape="ellipsoid"/>
+      <body pos="0 .3 0"><joint axis="1 0 0"/><geom type="cylinder" size=".05 .2"
+        fluidshape="ellipsoid"/>
+        <body pos="0 .3 0"><joint axis="0 1 1"/><geom type="ellipsoid" size=".1 .05 .2"
+          fluidshape="ellipsoid"/></body></body></body>
+    <body pos="1 0 1"><freejoint/><geom type="box" size=".1 .2 .3"/></body>
+    </worldbody></mujoco>""")
+  B = 1024
+  q, v, a = sample_states(m, B, first=3)
+  v = 2 * v
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    f = e.inverse(q, v, a)
+    fl_gpu = e.field("qfrc_fluid", 0, B)
+  finally:
+    e.close()
+  o = Oracle(m)
+  ref, fl = [], []
+  for i in range(B):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    fl.append(o.d.qfrc_fluid.copy())
+  assert np.abs(np.array(fl)).max() > 1e-2
+  assert_close(f, np.array(ref), "qfrc_inverse")
+  assert_close(fl_gpu, np.array(fl), "qfrc_fluid")
+
+
 def test_elliptic_cone_parity():
   """Elliptic friction cones (classic constraint passes) on the device: humanoid config-4
   states with cone="elliptic"."""

@@ -15,7 +15,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from mujoco_inversedynamicstest_amd import engine, fields, mjb, models
+from mujoco_inversedynamicstest_amd import engine, fields, mjb, mjcf, models
 
 REF = "/root/reference"
 BUNDLED = ["humanoid", "slider_crank", "inverse_test", "inertia", "linear", "weld", "connect",
@@ -97,8 +97,17 @@ def test_options_survive(humanoid):
   assert r.opt["iterations"] == 100          # mj_defaultOption for members the loader skips
 
 
+def test_ellipsoid_fluid_survives():
+  """geom_fluid (the ellipsoid fluid model's 12 coefficients per geom) round-trips."""
+  m = mjcf.load_xml_string("""<mujoco><option density="1.2" viscosity=".1"/><worldbody>
+    <body><freejoint/><geom type="box" size=".2 .1 .05" fluidshape="ellipsoid"/>
+    <geom type="sphere" size=".1" pos=".3 0 0"/></body></worldbody></mujoco>""")
+  r = mjb.read(mjb.write(m))
+  assert m.geom_fluid[0, 0] == 1 and m.geom_fluid[1, 0] == 0
+  np.testing.assert_array_equal(r.geom_fluid, m.geom_fluid)
+
+
 @pytest.mark.parametrize("field,value,msg", [
-    ("geom_fluid", 1.0, "ellipsoid fluid"),
     ("wrap_type", 7, "unknown tendon wrap object type")])
 def test_unsupported_features_refused(humanoid, field, value, msg):
   buf = mjb.write(humanoid)
