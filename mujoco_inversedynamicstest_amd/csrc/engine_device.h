@@ -2737,6 +2737,36 @@ template <int S, bool WRITE = true, bool BOX = true>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
                                double margin, int& ncon, int* status, double* bbuf = nullptr);
 
+// the narrowphase of a type-ordered primitive pair past the filters (mj_collideGeoms' call of
+// mjCOLLISIONFUNC, engine_collision_driver.c:1500-1510): its raw contacts (<= 2) in raw. The
+// frames may live in the mirror (SP) or in LDS (plain pointers).
+template <class P, class M>
+MJH_HD int narrowPrimitive(int t1, int t2, double margin, P pos1, M mat1, const double* size1,
+                           P pos2, M mat2, const double* size2, RawContact raw[2]) {
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_ELLIPSOID) {
+    return colPlaneEllipsoid(raw[0], margin, pos1, mat1, pos2, mat2, size2);
+  }
+  int num = 0;
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) {
+    num = rawPlaneSphere(raw, margin, pos1, mat1, pos2, size2[0]);
+  } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CAPSULE) {
+    num = colPlaneCapsule(raw, margin, pos1, mat1, pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_SPHERE) {
+    num = rawSphereSphere(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2[0]);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CAPSULE) {
+    num = colSphereCapsule(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CYLINDER) {
+    num = colSphereCylinder(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_BOX) {
+    num = colCapsuleBox(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_BOX) {
+    num = rawSphereBox(raw, margin, pos1, size1[0], pos2, mat2, size2);
+  } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {
+    num = colCapsuleCapsule(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
+  }
+  return num;
+}
+
 // mj_collideGeoms up to the narrowphase: type-orders (g1, g2), applies the static and
 // bounding-sphere filters and returns the raw contacts of a primitive or convex pair in raw
 // (<= 2, with the pair's margin), 0 for none, or -1 for plane : box / cylinder, whose contacts
@@ -2774,28 +2804,7 @@ MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
       return 0;
     }
   }
-  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_ELLIPSOID) {
-    return colPlaneEllipsoid(raw[0], margin, pos1, mat1, pos2, mat2, size2);
-  }
-  int num = 0;
-  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_SPHERE) {
-    num = rawPlaneSphere(raw, margin, pos1, mat1, pos2, size2[0]);
-  } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CAPSULE) {
-    num = colPlaneCapsule(raw, margin, pos1, mat1, pos2, mat2, size2);
-  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_SPHERE) {
-    num = rawSphereSphere(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2[0]);
-  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CAPSULE) {
-    num = colSphereCapsule(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
-  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_CYLINDER) {
-    num = colSphereCylinder(raw, margin, pos1, mat1, size1[0], pos2, mat2, size2);
-  } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_BOX) {
-    num = colCapsuleBox(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
-  } else if (t1 == mjhipGEOM_SPHERE && t2 == mjhipGEOM_BOX) {
-    num = rawSphereBox(raw, margin, pos1, size1[0], pos2, mat2, size2);
-  } else if (t1 == mjhipGEOM_CAPSULE && t2 == mjhipGEOM_CAPSULE) {
-    num = colCapsuleCapsule(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
-  }
-  return num;
+  return narrowPrimitive(t1, t2, margin, pos1, mat1, size1, pos2, mat2, size2, raw);
 }
 
 // mj_setContact (:1387-1415) for a primitive pair's raw contacts at contact index ncon on

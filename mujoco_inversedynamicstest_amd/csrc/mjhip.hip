@@ -137,19 +137,37 @@ static unsigned coopGrid(int B, int G, bool list) {
   return list && full > 1024u ? 1024u : full;
 }
 
-// dynamic LDS of k_constraint_coop: per instance 8 nv doubles (cdof, qvel, qacc), qpos and
-// efc_cap row forces; with box-box pairs, 72 doubles per lane for their contact positions
+// one entry of the cooperative kernel's pair program (host-built by coop_program in the order
+// of collision_pairs): the type-ordered geoms and their types, the pair's contact bound
+// (mjhip_pairMaxContacts; < 0: no collision function built here), its margin, and which
+// mj_filterSphere test applies with its bound formed as the reference forms it
+// (engine_collision_driver.c:1470-1497): filt 0 = bounding spheres, rb1 + rb2 + margin;
+// 1 = plane g1, margin + rb2; 2 = plane g2, margin + rb1; 3 = none
+struct CoopPair {
+  int g1, g2, t1, t2, kmax, filt;
+  double margin, bound;
+};
+constexpr int kCoopPairDoubles = (int)(sizeof(CoopPair) / sizeof(double));
+static_assert(sizeof(CoopPair) % sizeof(double) == 0, "CoopPair packs into doubles");
+
+// dynamic LDS of k_constraint_coop: the pair program once per block; per instance 8 nv
+// doubles (cdof, qvel, qacc), qpos, the geom frames (geom_xpos, geom_xmat) and the
+// survivor list of the sphere filter (npair ints); efc_cap row forces per instance; with
+// box-box pairs, 72 doubles per lane for their contact positions
 constexpr int kBoxBoxBuf = 72;
-static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap, bool boxpair) {
-  return (unsigned)(((64 / G) * (8*m.nv + m.nq + efc_cap) + (boxpair ? 64*kBoxBoxBuf : 0)) *
-                    sizeof(double));
+__host__ __device__ static inline int coopPerInstance(const mjhipModel& m, int npair) {
+  return 8*m.nv + m.nq + 12*m.ngeom + (npair + 1) / 2;
+}
+static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap, bool boxpair, int npair) {
+  return (unsigned)((kCoopPairDoubles*npair + (64 / G) * (coopPerInstance(m, npair) + efc_cap) +
+                     (boxpair ? 64*kBoxBoxBuf : 0)) * sizeof(double));
 }
 
 template <int G, bool CONTACT, bool LIST, bool BOX = false>
 __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr, int B,
                                                         const int* __restrict__ worklist,
                                                         const int* __restrict__ count,
-                                                        const int2* __restrict__ pairs,
+                                                        const CoopPair* __restrict__ pairs,
                                                         int npair,
                                                         double* __restrict__ qfrc_out,
                                                         int* __restrict__ status) {
@@ -158,8 +176,16 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   if ((long)blockIdx.x*IPB >= n) return;    // whole block idle (uniform): before the barriers
   __shared__ unsigned long long chain[64];
   if ((int)threadIdx.x < m.nbody) chain[threadIdx.x] = mjh::chainMask(m, threadIdx.x);
+  // the pair program, once per block
+  CoopPair* prog = reinterpret_cast<CoopPair*>(g_gstage);
+  if (CONTACT) {
+    for (int e = threadIdx.x; e < kCoopPairDoubles*npair; e += 64) {
+      g_gstage[e] = reinterpret_cast<const double*>(pairs)[e];
+    }
+  }
   __syncthreads();
   const int sub = threadIdx.x % G, slot = threadIdx.x / G;
+  const int ngeom = m.ngeom;
   // grid-stride over the instances (a work-list launch uses at most one block per SIMD, so
   // an empty or short list costs few workgroups); the bound is uniform over the block
   for (long base = (long)blockIdx.x*IPB; base < n; base += (long)gridDim.x*IPB) {
@@ -171,39 +197,92 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   const int nv = m.nv, dsbl = m.opt.disableflags;
   int st = 0, ncon = 0;
   MJH_PHASE(14);
-  // per-instance LDS (dynamic, coopLdsBytes): cdof/qvel/qacc for the contact rows, staged by
-  // the group while collision runs, and the row forces for J'force
-  const int nq = m.nq, per = 8*nv + nq;
-  double* cdq = g_gstage + (long)slot*per;
+  // per-instance LDS (dynamic, coopLdsBytes): cdof/qvel/qacc for the contact rows, qpos,
+  // the geom frames for the collision phase, its survivor list, and the row forces for
+  // J'force; all staged by the group with independent loads
+  const int nq = m.nq, per = coopPerInstance(m, npair);
+  double* lbase = g_gstage + kCoopPairDoubles*npair;
+  double* cdq = lbase + (long)slot*per;
   double* qp = cdq + 8*nv;
-  double* fst = g_gstage + (long)IPB*per + (long)slot*d.efc_cap;
+  double* gx = qp + nq;                     // geom_xpos (3 ngeom)
+  double* gm = gx + 3*ngeom;                // geom_xmat (9 ngeom)
+  int* surv = reinterpret_cast<int*>(gm + 9*ngeom);
+  double* fst = lbase + (long)IPB*per + (long)slot*d.efc_cap;
   // box-box contact positions of this lane's pair (only models with box pairs get the room)
-  double* bbuf = g_gstage + (long)IPB*(per + d.efc_cap) + (long)threadIdx.x*kBoxBoxBuf;
+  double* bbuf = lbase + (long)IPB*(per + d.efc_cap) + (long)threadIdx.x*kBoxBoxBuf;
+  const bool collide = CONTACT && mjhip_contactsEnabled(&m) && npair > 0;
   if (active) {
     for (int e = sub; e < 8*nv; e += G) {
       const int j = e >> 3, c = e & 7;
       cdq[e] = c < 6 ? d.cdof[6*j+c] : (c == 6 ? d.qvel[j] : d.qacc[j]);
     }
     for (int e = sub; e < nq; e += G) qp[e] = d.qpos[e];
+    if (collide) {
+      for (int e = sub; e < 3*ngeom; e += G) gx[e] = d.geom_xpos[e];
+      for (int e = sub; e < 9*ngeom; e += G) gm[e] = d.geom_xmat[e];
+    }
   }
   d.cdq = cdq;
   d.fst = fst;
+  __syncthreads();                          // the staged frames visible to the group
 
-  // ---- mj_collision over the static pair program
-  if (CONTACT && active && mjhip_contactsEnabled(&m)) {
+  // ---- mj_collision over the static pair program: first mj_filterSphere on every pair
+  // (G pairs per round, frames from LDS) into an ordered survivor list, then the
+  // narrowphase of the survivors only, G per round
+  if (collide) {
+    const unsigned long long gmask = G == 64 ? ~0ull : ((1ull << G) - 1) << (slot*G);
+    const unsigned long long below = (1ull << (threadIdx.x % 64)) - 1;
+    int nsurv = 0;
     for (int p0 = 0; p0 < npair; p0 += G) {
       const int p = p0 + sub;
+      bool keep = false;
+      if (active && p < npair) {
+        const CoopPair& P = prog[p];
+        const double* p1 = gx + 3*P.g1;
+        const double* p2 = gx + 3*P.g2;
+        if (P.filt == 0) {
+          const double dif[3] = {p1[0]-p2[0], p1[1]-p2[1], p1[2]-p2[2]};
+          keep = !(dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2] > P.bound*P.bound);
+        } else if (P.filt <= 2) {           // the plane's normal against the other's centre
+          const bool pl1 = P.filt == 1;
+          const double* mat = gm + 9*(pl1 ? P.g1 : P.g2);
+          const double norm[3] = {mat[2], mat[5], mat[8]};
+          double dif[3];
+          mjh::sub3(dif, pl1 ? p2 : p1, pl1 ? p1 : p2);
+          keep = !(mjh::dot3(dif, norm) > P.bound);
+        } else {
+          keep = true;
+        }
+      }
+      const unsigned long long bal = __ballot(keep) & gmask;
+      if (keep) surv[nsurv + __popcll(bal & below)] = p;
+      nsurv += __popcll(bal);
+    }
+    // rounds over the survivors: the wave runs as many as its busiest group needs
+    int rounds = (nsurv + G - 1) / G;
+    for (int o = G; o < 64; o <<= 1) rounds = max(rounds, __shfl_xor(rounds, o));
+    for (int r = 0; r < rounds; r++) {
+      const int s0 = r*G, k = s0 + sub;
       int g1 = 0, g2 = 0, num = 0, cnt = 0;
       double margin = 0;
       mjh::RawContact raw[2];
-      if (p < npair) {                      // narrowphase once: raw contacts kept in registers
-        const int2 pr = pairs[p];
-        g1 = pr.x;
-        g2 = pr.y;
-        num = mjh::narrowGeoms<64, false>(m, d, g1, g2, margin, raw, &st);
-        if (num < 0) {                      // plane : box / cylinder counts, then stores
+      if (active && k < nsurv) {            // narrowphase once: raw contacts kept in registers
+        const CoopPair P = prog[surv[k]];
+        g1 = P.g1;
+        g2 = P.g2;
+        margin = P.margin;
+        if (P.kmax < 0) {                   // the reference would run a function not built here
+          st |= MJHIP_INST_UNSUPPORTED;
+        } else if ((P.t1 == mjhipGEOM_PLANE &&
+                    (P.t2 == mjhipGEOM_BOX || P.t2 == mjhipGEOM_CYLINDER)) ||
+                   (P.t1 == mjhipGEOM_BOX && P.t2 == mjhipGEOM_BOX)) {
+          num = -1;                         // plane : box / cylinder, box : box: counts, then stores
           mjh::collidePlaneBoxCyl<64, false, BOX>(m, d, g1, g2, margin, cnt, &st, bbuf);
         } else {
+          num = mjh::narrowPrimitive(P.t1, P.t2, margin, (const double*)(gx + 3*g1),
+                                     (const double*)(gm + 9*g1), m.geom_size + 3*g1,
+                                     (const double*)(gx + 3*g2), (const double*)(gm + 9*g2),
+                                     m.geom_size + 3*g2, raw);
           cnt = num;
         }
       }
@@ -255,12 +334,38 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       rc.nefc++;
       return true;
     };
+    // rows of one G-wide round of dofs or joints, placed by a group prefix sum over each
+    // lane's row count in the reference's order; a row past the capacity is dropped and
+    // flagged, as addRow does
+    auto placeRound = [&](int nr, int& counter) MJH_LAMBDA_INLINE {
+      int total;
+      const int first = rc.nefc + groupScan<G>(nr, sub, &total) - nr;
+      const int end = rc.nefc + total < d.efc_cap ? rc.nefc + total : d.efc_cap;
+      if (rc.nefc + total > d.efc_cap) st |= MJHIP_INST_CNSTRFULL;
+      counter += end - rc.nefc;
+      rc.nefc = end;
+      return first;
+    };
+    auto putRow = [&](int r, auto jval, double pos, double margin, double floss, int tp, int id)
+        MJH_LAMBDA_INLINE {
+      if (r >= d.efc_cap) return;
+      mjh::SP<64> J = d.efc_J + (long)r*nv;
+      for (int k = 0; k < nv; k++) J[k] = jval(k);
+      rowFields(d, r, pos, margin, floss, tp, id);
+      const mjh::FnIdx<decltype(jval)> jv{jval};
+      mjh::finishNonContactVA(m, d, r, tp, id, pos, margin, floss,
+                              mjh::dot(jv, mjh::StridedIdx<8>{cdq + 6}, nv),
+                              mjh::dot(jv, mjh::StridedIdx<8>{cdq + 7}, nv));
+    };
     if (!(dsbl & mjhipDSBL_FRICTIONLOSS)) {
-      for (int i = 0; i < nv; i++) {
-        const double fl = m.dof_frictionloss[i];
-        if (fl > 0 && addRow([&](int k) { return k == i ? 1.0 : 0.0; }, 0, 0, fl,
-                             mjh::CNSTR_FRICTION_DOF, i)) {
-          rc.nf++;
+      // dof friction (:785-799), G dofs per round
+      for (int i0 = 0; i0 < nv; i0 += G) {
+        const int i = i0 + sub;
+        const double fl = i < nv ? m.dof_frictionloss[i] : 0.0;
+        const int first = placeRound(fl > 0 ? 1 : 0, rc.nf);
+        if (fl > 0) {
+          putRow(first, [&](int k) { return k == i ? 1.0 : 0.0; }, 0, 0, fl,
+                 mjh::CNSTR_FRICTION_DOF, i);
         }
       }
       // tendon friction (:801-815) on the ten_J row; mj_addConstraint drops an empty row
@@ -277,34 +382,47 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       }
     }
     if (!(dsbl & mjhipDSBL_LIMIT)) {
-      for (int i = 0; i < m.njnt; i++) {
-        if (!m.jnt_limited[i]) continue;
-        const double margin = m.jnt_margin[i];
-        const int t = m.jnt_type[i], da = m.jnt_dofadr[i];
-        if (t == mjhipJNT_SLIDE || t == mjhipJNT_HINGE) {
-          const double value = qp[m.jnt_qposadr[i]];
-          for (int side = -1; side <= 1; side += 2) {
-            const double dist = side * (m.jnt_range[2*i+(side+1)/2] - value);
-            if (dist < margin &&
-                addRow([&](int k) { return k == da ? -(double)side : 0.0; }, dist, margin, 0,
-                       mjh::CNSTR_LIMIT_JOINT, i)) {
-              rc.nl++;
+      // joint limits (:824-900), G joints per round: a slide/hinge joint gives up to two
+      // rows (lower side first), a ball joint one
+      for (int i0 = 0; i0 < m.njnt; i0 += G) {
+        const int i = i0 + sub;
+        int nr = 0, t = -1, da = 0;
+        bool on[2] = {false, false};
+        double dist[2] = {0, 0}, aa[3] = {0, 0, 0}, margin = 0;
+        if (i < m.njnt && m.jnt_limited[i]) {
+          margin = m.jnt_margin[i];
+          t = m.jnt_type[i];
+          da = m.jnt_dofadr[i];
+          if (t == mjhipJNT_SLIDE || t == mjhipJNT_HINGE) {
+            const double value = qp[m.jnt_qposadr[i]];
+            for (int k = 0; k < 2; k++) {
+              const int side = 2*k - 1;
+              dist[k] = side * (m.jnt_range[2*i+k] - value);
+              on[k] = dist[k] < margin;
+              nr += on[k];
             }
+          } else if (t == mjhipJNT_BALL) {
+            const int adr = m.jnt_qposadr[i];
+            double quat[4] = {qp[adr], qp[adr+1], qp[adr+2], qp[adr+3]};
+            mjh::normalize4(quat);
+            mjh::quat2Vel(aa, quat, 1);
+            const double value = mjh::normalize3(aa);
+            dist[0] = mjh::dmax(m.jnt_range[2*i], m.jnt_range[2*i+1]) - value;
+            on[0] = dist[0] < margin && (aa[0] != 0 || aa[1] != 0 || aa[2] != 0);
+            nr = on[0];
           }
-        } else if (t == mjhipJNT_BALL) {
-          const int adr = m.jnt_qposadr[i];
-          double quat[4] = {qp[adr], qp[adr+1], qp[adr+2], qp[adr+3]};
-          double aa[3];
-          mjh::normalize4(quat);
-          mjh::quat2Vel(aa, quat, 1);
-          const double value = mjh::normalize3(aa);
-          const double dist = mjh::dmax(m.jnt_range[2*i], m.jnt_range[2*i+1]) - value;
-          const bool nonempty = aa[0] != 0 || aa[1] != 0 || aa[2] != 0;
-          if (dist < margin && nonempty &&
-              addRow([&](int k) { return (k >= da && k < da + 3) ? aa[k-da]*-1 : 0.0; },
-                     dist, margin, 0, mjh::CNSTR_LIMIT_JOINT, i)) {
-            rc.nl++;
+        }
+        int r = placeRound(nr, rc.nl);
+        if (t == mjhipJNT_SLIDE || t == mjhipJNT_HINGE) {
+          for (int k = 0; k < 2; k++) {
+            if (!on[k]) continue;
+            const double sg = -(double)(2*k - 1);
+            putRow(r++, [&](int c) { return c == da ? sg : 0.0; }, dist[k], margin, 0,
+                   mjh::CNSTR_LIMIT_JOINT, i);
           }
+        } else if (t == mjhipJNT_BALL && on[0]) {
+          putRow(r, [&](int c) { return (c >= da && c < da + 3) ? aa[c-da]*-1 : 0.0; },
+                 dist[0], margin, 0, mjh::CNSTR_LIMIT_JOINT, i);
         }
       }
       for (int i = 0; i < m.ntendon; i++) {
@@ -672,7 +790,7 @@ struct mjhipContext_ {
   int* worklist = nullptr;                 // capacity + 2 ints: [count0, count1, list...]
   int wl_parity = 0;                       // counter the next fast launch uses
   int wl_last = 0;                         // counter the last fast launch used
-  int2* pairs = nullptr;                   // static geom-pair program (collisionPairs)
+  CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
   int npair = 0;
   bool boxpair = false;                    // a box-box pair is in the program (coop LDS)
   int coop = 16;                           // lanes per instance of k_constraint_coop (0: off)
@@ -723,6 +841,39 @@ static std::vector<int2> collision_pairs(const mjhipModel* m) {
       }
       out.insert(out.end(), list.begin(), list.end());
     }
+  }
+  return out;
+}
+
+// the cooperative kernel's program for collision_pairs' pairs: what mj_collideGeoms derives
+// from the model alone, type-ordered as narrowGeoms does (engine_collision_driver.c:1440-1497)
+static std::vector<CoopPair> coop_program(const mjhipModel* m, const std::vector<int2>& pairs) {
+  std::vector<CoopPair> out;
+  const bool ovr = (m->opt.enableflags & mjhipENBL_OVERRIDE) != 0;
+  for (const int2& pr : pairs) {
+    CoopPair P{};
+    P.g1 = pr.x;
+    P.g2 = pr.y;
+    if (m->geom_type[P.g1] > m->geom_type[P.g2]) std::swap(P.g1, P.g2);
+    P.t1 = m->geom_type[P.g1];
+    P.t2 = m->geom_type[P.g2];
+    P.kmax = mjhip_pairMaxContacts(m, P.t1, P.t2);
+    const double mg1 = m->geom_margin[P.g1], mg2 = m->geom_margin[P.g2];
+    P.margin = ovr ? m->opt.o_margin : (mg1 > mg2 ? mg1 : mg2);
+    const double rb1 = m->geom_rbound[P.g1], rb2 = m->geom_rbound[P.g2];
+    if (rb1 > 0 && rb2 > 0) {
+      P.filt = 0;
+      P.bound = rb1 + rb2 + P.margin;
+    } else if (P.t1 == mjhipGEOM_PLANE && rb2 > 0) {
+      P.filt = 1;
+      P.bound = P.margin + rb2;
+    } else if (P.t2 == mjhipGEOM_PLANE && rb1 > 0) {
+      P.filt = 2;
+      P.bound = P.margin + rb1;
+    } else {
+      P.filt = 3;
+    }
+    out.push_back(P);
   }
   return out;
 }
@@ -975,12 +1126,10 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
       if (e->sig == c->sig) c->fast = e;
     }
   }
-  // the cooperative constraint kernel's pair program (lanes per instance: MJHIP_COOP_LANES =
-  // 8 or 16, 0 = the one-lane k_constraint)
-  if (const char* lanes = getenv("MJHIP_COOP_LANES")) {
-    const int v = atoi(lanes);
-    c->coop = (v == 0 || v == 8 || v == 16 || v == 32) ? v : 16;
-  }
+  // the cooperative constraint kernel's pair program (16 lanes per instance: 8 and 32 were
+  // slower, profiles/r02/bench_c4_L*.json; MJHIP_COOP_LANES=0 selects the one-lane
+  // k_constraint)
+  if (const char* lanes = getenv("MJHIP_COOP_LANES")) c->coop = atoi(lanes) == 0 ? 0 : 16;
   if (c->con_cap > 0) {
     std::vector<int2> pairs = collision_pairs(m);
     c->npair = (int)pairs.size();
@@ -988,8 +1137,9 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
       c->boxpair |= m->geom_type[pr.x] == mjhipGEOM_BOX && m->geom_type[pr.y] == mjhipGEOM_BOX;
     }
     if (c->npair) {
-      if (hipMalloc((void**)&c->pairs, sizeof(int2) * pairs.size()) != hipSuccess ||
-          hipMemcpy(c->pairs, pairs.data(), sizeof(int2) * pairs.size(),
+      const std::vector<CoopPair> prog = coop_program(m, pairs);
+      if (hipMalloc((void**)&c->pairs, sizeof(CoopPair) * prog.size()) != hipSuccess ||
+          hipMemcpy(c->pairs, prog.data(), sizeof(CoopPair) * prog.size(),
                     hipMemcpyHostToDevice) != hipSuccess) {
         return fail("pair program upload");
       }
@@ -1004,7 +1154,8 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
     // serves the model instead of every launch failing
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return fail("hipGetDeviceProperties");
-    if (coopLdsBytes(*m, c->coop, c->efc_cap, c->boxpair) > (unsigned)prop.sharedMemPerBlock) {
+    if (coopLdsBytes(*m, c->coop, c->efc_cap, c->boxpair, c->npair) >
+        (unsigned)prop.sharedMemPerBlock) {
       c->coop = 0;
     }
   }
@@ -1126,28 +1277,20 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
       const bool contact = c->con_cap > 0, list = c->fast->cmode == 1;
 #define MJHIP_LAUNCH_COOP(G, C, L, X)                                                         \
       hipLaunchKernelGGL((k_constraint_coop<G, C, L, X>), dim3(coopGrid(B, G, L)),            \
-                         dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap, c->boxpair),        \
+                         dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap, c->boxpair,         \
+                                                      c->npair),                              \
                          c->stream,                                                           \
                          c->dmodel, c->mirror, B, wl,                                         \
                          (const int*)cnt, c->pairs, c->npair, qfrc, status)
       if (contact && c->boxpair) {       // the box-box path is compiled in only here
         if (list) MJHIP_LAUNCH_COOP(16, true, true, true);
         else MJHIP_LAUNCH_COOP(16, true, false, true);
-      } else if (c->coop == 8) {
-        if (contact) { if (list) MJHIP_LAUNCH_COOP(8, true, true, false);
-                       else MJHIP_LAUNCH_COOP(8, true, false, false); }
-        else { if (list) MJHIP_LAUNCH_COOP(8, false, true, false);
-               else MJHIP_LAUNCH_COOP(8, false, false, false); }
-      } else if (c->coop == 32) {
-        if (contact) { if (list) MJHIP_LAUNCH_COOP(32, true, true, false);
-                       else MJHIP_LAUNCH_COOP(32, true, false, false); }
-        else { if (list) MJHIP_LAUNCH_COOP(32, false, true, false);
-               else MJHIP_LAUNCH_COOP(32, false, false, false); }
+      } else if (contact) {
+        if (list) MJHIP_LAUNCH_COOP(16, true, true, false);
+        else MJHIP_LAUNCH_COOP(16, true, false, false);
       } else {
-        if (contact) { if (list) MJHIP_LAUNCH_COOP(16, true, true, false);
-                       else MJHIP_LAUNCH_COOP(16, true, false, false); }
-        else { if (list) MJHIP_LAUNCH_COOP(16, false, true, false);
-               else MJHIP_LAUNCH_COOP(16, false, false, false); }
+        if (list) MJHIP_LAUNCH_COOP(16, false, true, false);
+        else MJHIP_LAUNCH_COOP(16, false, false, false);
       }
 #undef MJHIP_LAUNCH_COOP
     } else {

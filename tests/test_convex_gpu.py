@@ -43,8 +43,8 @@ def _run(m, q, v, a):
     rst.append(o.d.status)
     rncon.append(o.efc.ncon)
     rnefc.append(o.efc.nefc)
-    rgeoms.append(o.contact_field("con_geom").ravel())
-    rdist.append(o.contact_field("con_dist").ravel())
+    rgeoms.append(o.contact_field("con_geom").ravel().copy())
+    rdist.append(o.contact_field("con_dist").ravel().copy())
   np.testing.assert_array_equal(st, rst)
   np.testing.assert_array_equal(ncon, rncon)
   np.testing.assert_array_equal(nefc, rnefc)

@@ -17,7 +17,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 EXP = os.path.join(ROOT, "tools", "exp")
-LIB = os.path.join(EXP, "libmjhip_phase.so")
+LIB = os.path.join(ROOT, "tools", "exp_lib", "libmjhip_phase.so")   # travels to the GPU box
 # generic pipeline (k_inverse): marks 0-9; constraint kernel after the generated kernels
 # (k_constraint, mjh::constraintOnly): marks 10-13
 GROUPS = [
@@ -35,8 +35,20 @@ def build():
   import __graft_entry__ as ge
   ge.generate_fast_kernels()
   os.makedirs(EXP, exist_ok=True)
-  subprocess.run(["/opt/rocm/bin/hipcc", *ge.HIPCC_FLAGS, "-DMJH_PHASE_TIMING", "-o", LIB,
-                  os.path.join(ge.CSRC, "mjhip.hip")], check=True)
+  # the two translation units of libmjhip (the generated kernels need no phase marks; their
+  # object is kept between builds), then one shared library
+  hipcc = "/opt/rocm/bin/hipcc"
+  gen_o, main_o = os.path.join(EXP, "gen_fast.o"), os.path.join(EXP, "mjhip_phase.o")
+  procs = [subprocess.Popen([hipcc, *ge.HIPCC_FLAGS, "-DMJH_PHASE_TIMING", "-c", "-o", main_o,
+                             os.path.join(ge.CSRC, "mjhip.hip")])]
+  if not ge._newer(gen_o, [os.path.join(ge.CSRC, "gen_fast.inc")]):
+    procs.append(subprocess.Popen([hipcc, *ge.HIPCC_FLAGS, "-c", "-o", gen_o,
+                                   os.path.join(ge.CSRC, "gen_fast.hip")]))
+  if any(p.wait() for p in procs):
+    raise RuntimeError("hipcc failed")
+  os.makedirs(os.path.dirname(LIB), exist_ok=True)
+  subprocess.run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB, main_o, gen_o],
+                 check=True)
 
 
 def run(B=4096, reps=5):
@@ -52,7 +64,7 @@ def run(B=4096, reps=5):
   q, v, a = sample_contact_states(m, B)
   eng = engine.InverseEngine(m, capacity=B)
   eng.upload_states(q, v, a)
-  G = int(os.environ.get("MJHIP_COOP_LANES", "16")) or 64
+  G = 16 if os.environ.get("MJHIP_COOP_LANES", "16") != "0" else 64
   acc = (ctypes.c_ulonglong * 32)()
   for generic in (False, True):
     eng.inverse(B, mirror_input=True, generic=generic)

@@ -5,7 +5,7 @@ cd "${GRAFT_REPO_ROOT:-$(pwd)}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 echo "== pytest"
-timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu \
+timeout -k 10 900 python -u -m pytest -x -v -s --timeout 300 --timeout-method thread tests -m gpu \
   > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
 tail -3 gpurun_out/pytest_gpu.log
 grep -h "convex pairs:\|slider_crank:" gpurun_out/pytest_gpu.log || true
