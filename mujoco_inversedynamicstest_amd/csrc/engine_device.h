@@ -248,6 +248,12 @@ struct Lane {
   // receives efc_force[r] as a row is finished, for the J'force pass
   const double* cdq;
   double* fst;
+  int nfst;                                  // rows r < nfst have fst[r]
+  // cooperative constraint kernel only (else nullptr): per contact, its bodies and their
+  // roots (b1, b2, body_rootid[b1], body_rootid[b2]) in LDS, written with the contact, for
+  // contacts i < ncbody
+  const int* cbody;
+  int ncbody;
 };
 
 // chain[k] for body k (the fused path's ancestor test, one bit per body)
@@ -4423,7 +4429,7 @@ MJH_HD void finishRowFused(const Lane<S>& d, int r, int tp, const double kb[4], 
     state = CNSTRSTATE_SATISFIED;
   }
   d.efc_force[r] = force;
-  if (d.fst) d.fst[r] = force;
+  if (d.fst && r < d.nfst) d.fst[r] = force;
   d.efc_state[r] = state;
 }
 
@@ -4476,7 +4482,18 @@ MJH_HD void contactRowsFused(const mjhipModel& m, const Lane<S>& d, int i, int n
   constexpr int NA = REG ? ROWS : 1;
   const int nv = m.nv;
   const int tp = DIM == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
-  const int b1 = m.geom_bodyid[d.con_geom[2*i]], b2 = m.geom_bodyid[d.con_geom[2*i+1]];
+  int b1, b2, rt1, rt2;
+  if (d.cbody && i < d.ncbody) {
+    b1 = d.cbody[4*i];
+    b2 = d.cbody[4*i+1];
+    rt1 = d.cbody[4*i+2];
+    rt2 = d.cbody[4*i+3];
+  } else {
+    b1 = m.geom_bodyid[d.con_geom[2*i]];
+    b2 = m.geom_bodyid[d.con_geom[2*i+1]];
+    rt1 = m.body_rootid[b1];
+    rt2 = m.body_rootid[b2];
+  }
   double pos[3], frame[9], fri[5], solref[2], solimp[5];
   for (int k = 0; k < 3; k++) pos[k] = d.con_pos[3*i+k];
   for (int k = 0; k < 9; k++) frame[k] = d.con_frame[9*i+k];
@@ -4485,8 +4502,8 @@ MJH_HD void contactRowsFused(const mjhipModel& m, const Lane<S>& d, int i, int n
   for (int k = 0; k < 5; k++) solimp[k] = d.con_solimp[5*i+k];
   const double dist = d.con_dist[i], incl = d.con_includemargin[i];
   double off1[3], off2[3];
-  sub3(off1, pos, d.subtree_com + 3*m.body_rootid[b1]);
-  sub3(off2, pos, d.subtree_com + 3*m.body_rootid[b2]);
+  sub3(off1, pos, d.subtree_com + 3*rt1);
+  sub3(off2, pos, d.subtree_com + 3*rt2);
   const unsigned long long mask1 = d.chain[b1], mask2 = d.chain[b2];
 
   // impedance and R (mj_diagApprox :1138-1311 with mj_makeImpedance)
@@ -6421,6 +6438,9 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
   d.gstage = false;
   d.cdq = nullptr;
   d.fst = nullptr;
+  d.nfst = 0;
+  d.cbody = nullptr;
+  d.ncbody = 0;
   return d;
 }
 

@@ -145,21 +145,37 @@ static unsigned coopGrid(int B, int G, bool list) {
 // 1 = plane g1, margin + rb2; 2 = plane g2, margin + rb1; 3 = none
 struct CoopPair {
   int g1, g2, t1, t2, kmax, filt;
+  int b1, b2, rt1, rt2;                     // the geoms' bodies and their roots
   double margin, bound;
 };
 constexpr int kCoopPairDoubles = (int)(sizeof(CoopPair) / sizeof(double));
 static_assert(sizeof(CoopPair) % sizeof(double) == 0, "CoopPair packs into doubles");
 
 // dynamic LDS of k_constraint_coop: the pair program once per block; per instance 8 nv
-// doubles (cdof, qvel, qacc), qpos, the geom frames (geom_xpos, geom_xmat) and the
-// survivor list of the sphere filter (npair ints); efc_cap row forces per instance; with
-// box-box pairs, 72 doubles per lane for their contact positions
+// doubles (cdof, qvel, qacc), qpos, the geom frames (geom_xpos, geom_xmat), the survivor
+// list of the sphere filter (npair ints), the bodies of the first kCoopContacts contacts (4
+// ints each) and the forces of the first kCoopRows rows (later ones are read back from
+// efc_force); with box-box pairs, 72 doubles per lane for their contact positions. The caps
+// keep a block small enough that every wave of a 4,096 batch is resident at once (the
+// humanoid's worst-case capacities, 273 contacts and 424 rows, would allow two blocks per CU).
 constexpr int kBoxBoxBuf = 72;
-__host__ __device__ static inline int coopPerInstance(const mjhipModel& m, int npair) {
-  return 8*m.nv + m.nq + 12*m.ngeom + (npair + 1) / 2;
+constexpr int kCoopContacts = 64;
+constexpr int kCoopRows = 128;
+__host__ __device__ static inline int coopContacts(int con_cap) {
+  return con_cap < kCoopContacts ? con_cap : kCoopContacts;
 }
-static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap, bool boxpair, int npair) {
-  return (unsigned)((kCoopPairDoubles*npair + (64 / G) * (coopPerInstance(m, npair) + efc_cap) +
+__host__ __device__ static inline int coopRows(int efc_cap) {
+  return efc_cap < kCoopRows ? efc_cap : kCoopRows;
+}
+__host__ __device__ static inline int coopPerInstance(const mjhipModel& m, int npair,
+                                                      int con_cap, int efc_cap) {
+  return 8*m.nv + m.nq + 12*m.ngeom + (npair + 1) / 2 + 2*coopContacts(con_cap) +
+         coopRows(efc_cap);
+}
+static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap, bool boxpair, int npair,
+                             int con_cap) {
+  return (unsigned)((kCoopPairDoubles*npair + (64 / G) * coopPerInstance(m, npair, con_cap,
+                                                                           efc_cap) +
                      (boxpair ? 64*kBoxBoxBuf : 0)) * sizeof(double));
 }
 
@@ -200,16 +216,18 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   // per-instance LDS (dynamic, coopLdsBytes): cdof/qvel/qacc for the contact rows, qpos,
   // the geom frames for the collision phase, its survivor list, and the row forces for
   // J'force; all staged by the group with independent loads
-  const int nq = m.nq, per = coopPerInstance(m, npair);
+  const int nq = m.nq, per = coopPerInstance(m, npair, d.con_cap, d.efc_cap);
   double* lbase = g_gstage + kCoopPairDoubles*npair;
   double* cdq = lbase + (long)slot*per;
   double* qp = cdq + 8*nv;
   double* gx = qp + nq;                     // geom_xpos (3 ngeom)
   double* gm = gx + 3*ngeom;                // geom_xmat (9 ngeom)
   int* surv = reinterpret_cast<int*>(gm + 9*ngeom);
-  double* fst = lbase + (long)IPB*per + (long)slot*d.efc_cap;
+  int* cbody = reinterpret_cast<int*>(gm + 9*ngeom + (npair + 1) / 2);
+  const int ncb = coopContacts(d.con_cap);
+  double* fst = gm + 9*ngeom + (npair + 1) / 2 + 2*ncb;
   // box-box contact positions of this lane's pair (only models with box pairs get the room)
-  double* bbuf = lbase + (long)IPB*(per + d.efc_cap) + (long)threadIdx.x*kBoxBoxBuf;
+  double* bbuf = lbase + (long)IPB*per + (long)threadIdx.x*kBoxBoxBuf;
   const bool collide = CONTACT && mjhip_contactsEnabled(&m) && npair > 0;
   if (active) {
     for (int e = sub; e < 8*nv; e += G) {
@@ -224,6 +242,9 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   }
   d.cdq = cdq;
   d.fst = fst;
+  d.nfst = coopRows(d.efc_cap);
+  d.cbody = cbody;
+  d.ncbody = ncb;
   __syncthreads();                          // the staged frames visible to the group
 
   // ---- mj_collision over the static pair program: first mj_filterSphere on every pair
@@ -263,7 +284,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
     for (int o = G; o < 64; o <<= 1) rounds = max(rounds, __shfl_xor(rounds, o));
     for (int r = 0; r < rounds; r++) {
       const int s0 = r*G, k = s0 + sub;
-      int g1 = 0, g2 = 0, num = 0, cnt = 0;
+      int g1 = 0, g2 = 0, num = 0, cnt = 0, bodies[4] = {0, 0, 0, 0};
       double margin = 0;
       mjh::RawContact raw[2];
       if (active && k < nsurv) {            // narrowphase once: raw contacts kept in registers
@@ -271,6 +292,10 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         g1 = P.g1;
         g2 = P.g2;
         margin = P.margin;
+        bodies[0] = P.b1;
+        bodies[1] = P.b2;
+        bodies[2] = P.rt1;
+        bodies[3] = P.rt2;
         if (P.kmax < 0) {                   // the reference would run a function not built here
           st |= MJHIP_INST_UNSUPPORTED;
         } else if ((P.t1 == mjhipGEOM_PLANE &&
@@ -294,6 +319,9 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
           mjh::collidePlaneBoxCyl<64, true, BOX>(m, d, g1, g2, margin, c, &st, bbuf);
         } else {
           mjh::setContacts<64>(m, d, g1, g2, margin, raw, num, c, &st);
+        }
+        for (int q = ncon + excl; q < c && q < ncb; q++) {   // the contacts just stored
+          for (int e = 0; e < 4; e++) cbody[4*q + e] = bodies[e];
         }
       }
       ncon += total;
@@ -493,7 +521,10 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       for (int r0 = 0; r0 < nefc; r0 += 8) {
         double f[8], x0[8], x1[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) f[u] = r0 + u < nefc ? fst[r0+u] : 0.0;
+        for (int u = 0; u < 8; u++) {
+          const int r = r0 + u;
+          f[u] = r < nefc ? (r < d.nfst ? fst[r] : d.efc_force[r]) : 0.0;
+        }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
           mjh::SP<64> Jr = d.efc_J + (long)(r0 + u)*nv;
@@ -858,6 +889,10 @@ static std::vector<CoopPair> coop_program(const mjhipModel* m, const std::vector
     P.t1 = m->geom_type[P.g1];
     P.t2 = m->geom_type[P.g2];
     P.kmax = mjhip_pairMaxContacts(m, P.t1, P.t2);
+    P.b1 = m->geom_bodyid[P.g1];
+    P.b2 = m->geom_bodyid[P.g2];
+    P.rt1 = m->body_rootid[P.b1];
+    P.rt2 = m->body_rootid[P.b2];
     const double mg1 = m->geom_margin[P.g1], mg2 = m->geom_margin[P.g2];
     P.margin = ovr ? m->opt.o_margin : (mg1 > mg2 ? mg1 : mg2);
     const double rb1 = m->geom_rbound[P.g1], rb2 = m->geom_rbound[P.g2];
@@ -1154,7 +1189,7 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
     // serves the model instead of every launch failing
     hipDeviceProp_t prop;
     if (hipGetDeviceProperties(&prop, device) != hipSuccess) return fail("hipGetDeviceProperties");
-    if (coopLdsBytes(*m, c->coop, c->efc_cap, c->boxpair, c->npair) >
+    if (coopLdsBytes(*m, c->coop, c->efc_cap, c->boxpair, c->npair, c->con_cap) >
         (unsigned)prop.sharedMemPerBlock) {
       c->coop = 0;
     }
@@ -1278,7 +1313,7 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
 #define MJHIP_LAUNCH_COOP(G, C, L, X)                                                         \
       hipLaunchKernelGGL((k_constraint_coop<G, C, L, X>), dim3(coopGrid(B, G, L)),            \
                          dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap, c->boxpair,         \
-                                                      c->npair),                              \
+                                                      c->npair, c->con_cap),                  \
                          c->stream,                                                           \
                          c->dmodel, c->mirror, B, wl,                                         \
                          (const int*)cnt, c->pairs, c->npair, qfrc, status)

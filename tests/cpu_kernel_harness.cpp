@@ -100,5 +100,8 @@ static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int
   L.gstage = false;
   L.cdq = nullptr;
   L.fst = nullptr;
+  L.nfst = 0;
+  L.cbody = nullptr;
+  L.ncbody = 0;
   return L;
 }
