@@ -42,7 +42,8 @@
   XS(ntree)       \
   XS(nsensor)     \
   XS(nsensordata) \
-  XS(neq)
+  XS(neq)         \
+  XS(nmat)
 
 /* model arrays that live in mjModel in the reference (mjxmacro.h MJMODEL_POINTERS) */
 #define MJHIP_MODEL_POINTERS_M \
@@ -119,6 +120,8 @@
   X(mjtNum,  geom_fluid,           ngeom,     12) \
   X(mjtNum,  geom_margin,          ngeom,     1) \
   X(mjtNum,  geom_gap,             ngeom,     1) \
+  X(int,     geom_matid,           ngeom,     1) \
+  X(float,   geom_rgba,            ngeom,     4) \
   X(int,     site_type,            nsite,     1) \
   X(int,     site_bodyid,          nsite,     1) \
   X(mjtByte, site_sameframe,       nsite,     1) \
@@ -194,6 +197,7 @@
   X(int,     sensor_dim,           nsensor,   1) \
   X(int,     sensor_adr,           nsensor,   1) \
   X(mjtNum,  sensor_cutoff,        nsensor,   1) \
+  X(float,   mat_rgba,             nmat,      4) \
   X(mjtNum,  key_qpos,             nkey,      MJ_M(nq))
 
 /* model-constant sparse structures that live in mjData in the reference

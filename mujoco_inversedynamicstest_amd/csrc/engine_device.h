@@ -41,8 +41,20 @@ __device__ unsigned long long mjh_phase_acc[32];
   do {                                                                                \
     if ((threadIdx.x & 63) == 0) atomicAdd(&mjh_phase_acc[k], wall_clock64());       \
   } while (0)
+// spans inside a lane's own work (lane 0's): MJH_TICK(t) reads the clock, MJH_SPAN(k, a, b)
+// adds b - a to slot k (slot k + 1 counts the spans)
+#define MJH_TICK(t) const unsigned long long t = wall_clock64()
+#define MJH_SPAN(k, a, b)                                                             \
+  do {                                                                                \
+    if ((threadIdx.x & 63) == 0) {                                                    \
+      atomicAdd(&mjh_phase_acc[k], (b) - (a));                                        \
+      atomicAdd(&mjh_phase_acc[(k) + 1], 1ull);                                       \
+    }                                                                                 \
+  } while (0)
 #else
 #define MJH_PHASE(k) do {} while (0)
+#define MJH_TICK(t) do {} while (0)
+#define MJH_SPAN(k, a, b) do {} while (0)
 #endif
 
 // mjtSensor values (include/mujoco/mjmodel.h)
@@ -238,6 +250,9 @@ struct Lane {
   // fused constraint path only (nbody <= 64): chain[k] has bit b set when body b is body k
   // or one of its ancestors (on the device a per-block LDS table, chainMasks)
   const unsigned long long* chain;
+  // cooperative constraint kernel only (else nullptr; nv <= 64): dchain[k] has bit j set when
+  // dof j belongs to body k or one of its ancestors (a per-block LDS table)
+  const unsigned long long* dchain;
   // geom positions as collision reads them: geom_xpos itself, or (gstage) a per-lane LDS
   // copy that collision() fills first -- the broadphase reads every candidate pair's
   // positions, and LDS turns those loads from memory round trips into LDS latency
@@ -2813,14 +2828,20 @@ MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
   return narrowPrimitive(t1, t2, margin, pos1, mat1, size1, pos2, mat2, size2, raw);
 }
 
-// mj_setContact (:1387-1415) for a primitive pair's raw contacts at contact index ncon on
-template <int S>
-MJH_HD void setContacts(const mjhipModel& m, const Lane<S>& d, int g1, int g2, double margin,
-                        const RawContact raw[2], int num, int& ncon, int* status) {
-  const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
+// a geom pair's contact parameters (mj_contactParam, engine_collision_driver.c:1326-1384):
+// model constants, so the cooperative kernel's pair program carries them precomputed
+struct ContactParam {
   int condim;
   double gap, solref[2], solimp[5], friction[5];
-  contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
+};
+
+// mj_setContact (:1387-1415) for a primitive pair's raw contacts at contact index ncon on,
+// with the pair's parameters
+template <int S>
+MJH_HD void storeContacts(const mjhipModel& m, const Lane<S>& d, int g1, int g2, double margin,
+                          const ContactParam& cp, const RawContact raw[2], int num, int& ncon,
+                          int* status) {
+  const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
   // one raw contact into the contact list (mj_setContact); false when the list is full
   auto store = [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
     int i = ncon;
@@ -2834,14 +2855,14 @@ MJH_HD void setContacts(const mjhipModel& m, const Lane<S>& d, int g1, int g2, d
     copy3(d.con_pos + 3*i, rk.pos);
     d.con_geom[2*i] = g1;
     d.con_geom[2*i+1] = g2;
-    d.con_dim[i] = condim;
-    double includemargin = margin - gap;
+    d.con_dim[i] = cp.condim;
+    double includemargin = margin - cp.gap;
     d.con_includemargin[i] = includemargin;
-    for (int j = 0; j < 2; j++) d.con_solref[2*i+j] = ovr ? m.opt.o_solref[j] : solref[j];
+    for (int j = 0; j < 2; j++) d.con_solref[2*i+j] = ovr ? m.opt.o_solref[j] : cp.solref[j];
     for (int j = 0; j < 2; j++) d.con_solreffriction[2*i+j] = ovr ? m.opt.o_solref[j] : 0.0;
-    for (int j = 0; j < 5; j++) d.con_solimp[5*i+j] = ovr ? m.opt.o_solimp[j] : solimp[j];
+    for (int j = 0; j < 5; j++) d.con_solimp[5*i+j] = ovr ? m.opt.o_solimp[j] : cp.solimp[j];
     for (int j = 0; j < 5; j++) {
-      double f = ovr ? m.opt.o_friction[j] : friction[j];
+      double f = ovr ? m.opt.o_friction[j] : cp.friction[j];
       d.con_friction[5*i+j] = f > 1e-5 ? f : 1e-5;      // mjMINMU
     }
     d.con_exclude[i] = rk.dist >= includemargin;
@@ -2854,6 +2875,15 @@ MJH_HD void setContacts(const mjhipModel& m, const Lane<S>& d, int g1, int g2, d
   };
   if (store(raw[0]) && num > 1) store(raw[1]);   // num <= 2; constant indices keep raw[]
 }                                                // in registers
+
+// storeContacts with the pair's parameters from the model
+template <int S>
+MJH_HD void setContacts(const mjhipModel& m, const Lane<S>& d, int g1, int g2, double margin,
+                        const RawContact raw[2], int num, int& ncon, int* status) {
+  ContactParam cp;
+  contactParam(m, g1, g2, &cp.condim, &cp.gap, cp.solref, cp.solimp, cp.friction);
+  storeContacts(m, d, g1, g2, margin, cp, raw, num, ncon, status);
+}
 
 // mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
 // WRITE = false only counts the contacts the pair produces
@@ -4482,6 +4512,7 @@ MJH_HD void contactRowsFused(const mjhipModel& m, const Lane<S>& d, int i, int n
   constexpr int NA = REG ? ROWS : 1;
   const int nv = m.nv;
   const int tp = DIM == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
+  MJH_TICK(tc0);
   int b1, b2, rt1, rt2;
   if (d.cbody && i < d.ncbody) {
     b1 = d.cbody[4*i];
@@ -4527,6 +4558,7 @@ MJH_HD void contactRowsFused(const mjhipModel& m, const Lane<S>& d, int i, int n
     R = 2*mu*mu*R0;
   }
 
+  MJH_TICK(tc1);
   // rows, dof by dof, in blocks of four
   SP<S> J = d.efc_J + nefc*nv;
   double av[NA][4], aa[NA][4], tv[NA], ta[NA];
@@ -4618,6 +4650,7 @@ MJH_HD void contactRowsFused(const mjhipModel& m, const Lane<S>& d, int i, int n
       }
     }
   }
+  MJH_TICK(tc2);
   for (int r = 0; r < ROWS; r++) {
     double vel, acc;
     if constexpr (REG) {
@@ -4639,7 +4672,176 @@ MJH_HD void contactRowsFused(const mjhipModel& m, const Lane<S>& d, int i, int n
     d.efc_id[row] = i;
     finishRowFused(d, row, tp, kb, R, dist, incl, 0, vel, acc);
   }
+  MJH_TICK(tc3);
+  MJH_SPAN(20, tc0, tc1);       // contact data, impedance, R
+  MJH_SPAN(22, tc1, tc2);       // the dof loop
+  MJH_SPAN(24, tc2, tc3);       // row fields and finish
 }
+
+#if defined(__HIPCC__)   // wave shuffles: HIP builds only (the host harness has no lanes)
+// contactRowsFused for a frictionless or condim-3 pyramidal contact split over Q lanes (the
+// cooperative constraint kernel; q = this lane's index in the contact's lane group, the group
+// aligned to Q in the wave). Lane q forms the dofs j of the four-dof blocks with j % 4 = q
+// (mod Q): exactly mju_dot's partial sums res0..res3 (engine_util_blas.c:720-729) for
+// J*qvel and J*qacc, which two shuffle steps then combine as (res0 + res2) + (res1 + res3);
+// lane 0 adds the tail (:733-741). Lane q finishes rows r % Q = q. Every value equals
+// contactRowsFused's.
+template <int S, int DIM, int Q>
+MJH_HD void contactRowsSplit(const mjhipModel& m, const Lane<S>& d, int i, int nefc, int q) {
+  static_assert(DIM == 1 || DIM == 3, "wide contacts keep one lane");
+  static_assert(Q == 1 || Q == 2 || Q == 4, "a divisor of mju_dot's four partial sums");
+  constexpr int ROWS = DIM == 1 ? 1 : 4;
+  constexpr int T = 4 / Q;                 // partial sums per lane: k = q + Q t
+  const int nv = m.nv;
+  const int tp = DIM == 1 ? CNSTR_CONTACT_FRICTIONLESS : CNSTR_CONTACT_PYRAMIDAL;
+  int b1, b2, rt1, rt2;
+  if (d.cbody && i < d.ncbody) {
+    b1 = d.cbody[4*i];
+    b2 = d.cbody[4*i+1];
+    rt1 = d.cbody[4*i+2];
+    rt2 = d.cbody[4*i+3];
+  } else {
+    b1 = m.geom_bodyid[d.con_geom[2*i]];
+    b2 = m.geom_bodyid[d.con_geom[2*i+1]];
+    rt1 = m.body_rootid[b1];
+    rt2 = m.body_rootid[b2];
+  }
+  double pos[3], frame[9], fri[5], solref[2], solimp[5];
+  for (int k = 0; k < 3; k++) pos[k] = d.con_pos[3*i+k];
+  for (int k = 0; k < 9; k++) frame[k] = d.con_frame[9*i+k];
+  for (int k = 0; k < 5; k++) fri[k] = d.con_friction[5*i+k];
+  for (int k = 0; k < 2; k++) solref[k] = d.con_solref[2*i+k];
+  for (int k = 0; k < 5; k++) solimp[k] = d.con_solimp[5*i+k];
+  const double dist = d.con_dist[i], incl = d.con_includemargin[i];
+  double off1[3], off2[3];
+  sub3(off1, pos, d.subtree_com + 3*rt1);
+  sub3(off2, pos, d.subtree_com + 3*rt2);
+  // the dofs on each body's chain: a bit test per dof (the per-dof body id is lane-dependent
+  // here, and a memory load of it would wait for the lane's earlier row stores)
+  const bool bydof = d.dchain != nullptr;
+  const unsigned long long mask1 = bydof ? d.dchain[b1] : d.chain[b1];
+  const unsigned long long mask2 = bydof ? d.dchain[b2] : d.chain[b2];
+  double kb[4];
+  rowImpedance(m, tp, solref, solimp, dist, incl, kb);
+  double tran = 0;
+  tran += m.body_invweight0[2*b1] * 1.0;
+  tran += m.body_invweight0[2*b2] * 1.0;
+  double R;
+  if constexpr (DIM == 1) {
+    R = dmax(MINVAL, (1-kb[2])*tran/kb[2]);
+  } else {
+    const double v0 = tran + fri[0]*fri[0]*tran;
+    const double R0 = dmax(MINVAL, (1-kb[2])*v0/kb[2]);
+    const double R1 = R0/dmax(MINVAL, m.opt.impratio);
+    const double mu = fri[0] * sqrt(R1/R0);
+    if (q == 0) d.con_mu[i] = mu;
+    R = 2*mu*mu*R0;
+  }
+
+  SP<S> J = d.efc_J + nefc*nv;
+  // one dof's rows into efc_J, returned in Jv (as contactRowsFused forms them)
+  auto dofRows = [&](int j, const double* cd, double Jv[ROWS]) MJH_LAMBDA_INLINE {
+    const int bj = bydof ? j : m.dof_bodyid[j];
+    const bool in1 = (mask1 >> bj) & 1, in2 = (mask2 >> bj) & 1;
+    double t1[3], t2[3], jd[3], cj[3] = {0, 0, 0};
+    cross(t1, cd, off1);
+    cross(t2, cd, off2);
+    for (int c = 0; c < 3; c++) {
+      const double p1 = in1 ? cd[3+c] + t1[c] : 0.0;
+      const double p2 = in2 ? cd[3+c] + t2[c] : 0.0;
+      jd[c] = p2 - p1;
+    }
+    constexpr int rp = DIM > 1 ? 3 : 1;
+    for (int r = 0; r < rp; r++) {
+      double acc = 0;
+      for (int c = 0; c < 3; c++) {
+        const double f = frame[3*r+c];
+        if (f) acc += jd[c]*f;
+      }
+      cj[r] = acc;
+    }
+    if constexpr (DIM == 1) {
+      Jv[0] = cj[0];
+    } else {
+      for (int c = 1; c < 3; c++) {
+        const double f = fri[c-1];
+        Jv[2*(c-1)] = cj[0] + cj[c]*f;
+        Jv[2*(c-1)+1] = cj[0] + cj[c]*(-f);
+      }
+    }
+    for (int r = 0; r < ROWS; r++) J[r*nv + j] = Jv[r];
+  };
+  double av[ROWS][T], aa[ROWS][T], tv[ROWS], ta[ROWS];
+  for (int r = 0; r < ROWS; r++) {
+    for (int t = 0; t < T; t++) av[r][t] = aa[r][t] = 0;
+    tv[r] = ta[r] = 0;
+  }
+  const int nb4 = (nv / 4) * 4;
+  for (int jb = 0; jb < nb4; jb += 4) {
+    double cd[T][6], qv[T], qa[T];
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+      const double* p = d.cdq + 8*(jb + q + Q*t);
+      for (int c = 0; c < 6; c++) cd[t][c] = p[c];
+      qv[t] = p[6];
+      qa[t] = p[7];
+    }
+#pragma unroll
+    for (int t = 0; t < T; t++) {
+      double Jv[ROWS];
+      dofRows(jb + q + Q*t, cd[t], Jv);
+      for (int r = 0; r < ROWS; r++) {
+        av[r][t] += Jv[r]*qv[t];
+        aa[r][t] += Jv[r]*qa[t];
+      }
+    }
+  }
+  if (q == 0) {                           // the tail dofs, summed on their own (:733-741)
+    for (int j = nb4; j < nv; j++) {
+      const double* p = d.cdq + 8*j;
+      double cd[6], Jv[ROWS];
+      for (int c = 0; c < 6; c++) cd[c] = p[c];
+      dofRows(j, cd, Jv);
+      for (int r = 0; r < ROWS; r++) {
+        const double pv = Jv[r]*p[6], pa = Jv[r]*p[7];
+        tv[r] = j == nb4 ? pv : tv[r] + pv;
+        ta[r] = j == nb4 ? pa : ta[r] + pa;
+      }
+    }
+  }
+  for (int r = 0; r < ROWS; r++) {
+    // (res0 + res2) + (res1 + res3): addition commutes exactly, so each lane may add its
+    // partner's partial to its own
+    double sv, sa;
+    if constexpr (Q == 4) {
+      sv = av[r][0] + __shfl_xor(av[r][0], 2, 4);
+      sa = aa[r][0] + __shfl_xor(aa[r][0], 2, 4);
+      sv = sv + __shfl_xor(sv, 1, 4);
+      sa = sa + __shfl_xor(sa, 1, 4);
+    } else if constexpr (Q == 2) {
+      sv = av[r][0] + av[r][1];
+      sa = aa[r][0] + aa[r][1];
+      sv = sv + __shfl_xor(sv, 1, 2);
+      sa = sa + __shfl_xor(sa, 1, 2);
+    } else {
+      sv = (av[r][0] + av[r][2]) + (av[r][1] + av[r][3]);
+      sa = (aa[r][0] + aa[r][2]) + (aa[r][1] + aa[r][3]);
+    }
+    if (nv > nb4) {
+      sv += Q > 1 ? __shfl(tv[r], 0, Q) : tv[r];
+      sa += Q > 1 ? __shfl(ta[r], 0, Q) : ta[r];
+    }
+    if (r % Q != q) continue;
+    const int row = nefc + r;
+    d.efc_pos[row] = dist;
+    d.efc_margin[row] = incl;
+    d.efc_frictionloss[row] = 0;
+    d.efc_type[row] = tp;
+    d.efc_id[row] = i;
+    finishRowFused(d, row, tp, kb, R, dist, incl, 0, sv, sa);
+  }
+}
+#endif
 
 // mj_instantiateContact :964-1131 on the fused path (pyramidal or frictionless)
 template <int S>
@@ -5839,8 +6041,13 @@ MJH_HD int limitRow(const Lane<S>& d, int type, int id) {
   return -1;
 }
 
-// engine_sensor.c:209-513 mj_sensorPos (no rangefinder/camprojection/geom distance/user,
-// rejected at load)
+// mj_ray for the rangefinder (defined with the touch sensor's ray functions below)
+template <int S>
+MJH_HD double ray(const mjhipModel& m, const Lane<S>& d, const double pnt[3],
+                  const double vec[3], int bodyexclude);
+
+// engine_sensor.c:209-513 mj_sensorPos (no camprojection/geom distance/user, rejected at
+// load)
 template <int S>
 MJH_HD void sensorPos(const mjhipModel& m, const Lane<S>& d) {
   if (m.opt.disableflags & mjhipDSBL_SENSOR) return;
@@ -5856,6 +6063,16 @@ MJH_HD void sensorPos(const mjhipModel& m, const Lane<S>& d) {
     switch (type) {
     case mjhSENS_MAGNETOMETER:
       mulMatTVec(out, d.site_xmat + 9*objid, m.opt.magnetic, 3, 3);
+      break;
+    case mjhSENS_RANGEFINDER:              // the site's z axis, its own body excluded
+      rvec[0] = d.site_xmat[9*objid+2];
+      rvec[1] = d.site_xmat[9*objid+5];
+      rvec[2] = d.site_xmat[9*objid+8];
+      {
+        double pnt[3];
+        for (int k = 0; k < 3; k++) pnt[k] = d.site_xpos[3*objid+k];
+        out[0] = ray(m, d, pnt, rvec, m.site_bodyid[objid]);
+      }
       break;
     case mjhSENS_JOINTPOS: out[0] = d.qpos[m.jnt_qposadr[objid]]; break;
     case mjhSENS_TENDONPOS: out[0] = d.ten_length[objid]; break;
@@ -6114,6 +6331,34 @@ MJH_HD double rayGeom(const double* pos, const double* mat, const double* size,
   }
   return x;
 }
+
+// the rangefinder (engine_sensor.c mjSENS_RANGEFINDER): mj_ray from the site along its z
+// axis, geomgroup NULL, flg_static 1, the site's body excluded
+// :69-100 ray_eliminate (geomgroup NULL, flg_static 1): the excluded body and invisible geoms
+MJH_HD bool rayEliminate(const mjhipModel& m, int g, int bodyexclude) {
+  if (m.geom_bodyid[g] == bodyexclude) return true;
+  const int mat = m.geom_matid[g];
+  if (mat < 0) return m.geom_rgba[4*g+3] == 0;
+  return m.mat_rgba[4*mat+3] == 0;
+}
+
+// :1145-1185 mj_ray (geomgroup NULL, flg_static 1): the nearest hit distance, -1 for none
+// (mju_rayGeom is the touch sensor's rayGeom; the mirror's frames go through registers)
+template <int S>
+MJH_HD double ray(const mjhipModel& m, const Lane<S>& d, const double pnt[3],
+                  const double vec[3], int bodyexclude) {
+  double dist = -1;
+  for (int g = 0; g < m.ngeom; g++) {
+    if (rayEliminate(m, g, bodyexclude)) continue;
+    double pos[3], mat[9];
+    for (int k = 0; k < 3; k++) pos[k] = d.geom_xpos[3*g+k];
+    for (int k = 0; k < 9; k++) mat[k] = d.geom_xmat[9*g+k];
+    const double nd = rayGeom(pos, mat, m.geom_size + 3*g, pnt, vec, m.geom_type[g]);
+    if (nd >= 0 && (nd < dist || dist < 0)) dist = nd;
+  }
+  return dist;
+}
+
 
 // the touch sensor (engine_sensor.c:750-793): the normal forces of the site body's contacts
 // whose normal ray from the contact point hits the site's zone
@@ -6441,6 +6686,7 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
   d.nfst = 0;
   d.cbody = nullptr;
   d.ncbody = 0;
+  d.dchain = nullptr;
   return d;
 }
 

@@ -151,7 +151,8 @@ struct CoopPair {
 constexpr int kCoopPairDoubles = (int)(sizeof(CoopPair) / sizeof(double));
 static_assert(sizeof(CoopPair) % sizeof(double) == 0, "CoopPair packs into doubles");
 
-// dynamic LDS of k_constraint_coop: the pair program once per block; per instance 8 nv
+// dynamic LDS of k_constraint_coop: the pair program and geom_size once per block; per
+// instance 8 nv
 // doubles (cdof, qvel, qacc), qpos, the geom frames (geom_xpos, geom_xmat), the survivor
 // list of the sphere filter (npair ints), the bodies of the first kCoopContacts contacts (4
 // ints each) and the forces of the first kCoopRows rows (later ones are read back from
@@ -160,6 +161,10 @@ static_assert(sizeof(CoopPair) % sizeof(double) == 0, "CoopPair packs into doubl
 // humanoid's worst-case capacities, 273 contacts and 424 rows, would allow two blocks per CU).
 constexpr int kBoxBoxBuf = 72;
 constexpr int kCoopContacts = 64;
+#ifndef MJHIP_COOP_CQ
+#define MJHIP_COOP_CQ 4
+#endif
+constexpr int kCoopContactLanes = MJHIP_COOP_CQ;   // lanes per contact in the contact rows
 constexpr int kCoopRows = 128;
 __host__ __device__ static inline int coopContacts(int con_cap) {
   return con_cap < kCoopContacts ? con_cap : kCoopContacts;
@@ -174,8 +179,8 @@ __host__ __device__ static inline int coopPerInstance(const mjhipModel& m, int n
 }
 static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap, bool boxpair, int npair,
                              int con_cap) {
-  return (unsigned)((kCoopPairDoubles*npair + (64 / G) * coopPerInstance(m, npair, con_cap,
-                                                                           efc_cap) +
+  return (unsigned)((kCoopPairDoubles*npair + 3*m.ngeom +
+                     (64 / G) * coopPerInstance(m, npair, con_cap, efc_cap) +
                      (boxpair ? 64*kBoxBoxBuf : 0)) * sizeof(double));
 }
 
@@ -184,20 +189,33 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
                                                         const int* __restrict__ worklist,
                                                         const int* __restrict__ count,
                                                         const CoopPair* __restrict__ pairs,
+                                                        const mjh::ContactParam* __restrict__ cparams,
                                                         int npair,
                                                         double* __restrict__ qfrc_out,
                                                         int* __restrict__ status) {
   constexpr int IPB = 64 / G;               // instances per wave
   const long n = LIST ? (long)*count : (long)B;
   if ((long)blockIdx.x*IPB >= n) return;    // whole block idle (uniform): before the barriers
-  __shared__ unsigned long long chain[64];
+  __shared__ unsigned long long chain[64], dchain[64];
   if ((int)threadIdx.x < m.nbody) chain[threadIdx.x] = mjh::chainMask(m, threadIdx.x);
-  // the pair program, once per block
+  // the pair program and the geom sizes, once per block
   CoopPair* prog = reinterpret_cast<CoopPair*>(g_gstage);
+  double* gsize = g_gstage + kCoopPairDoubles*npair;
   if (CONTACT) {
     for (int e = threadIdx.x; e < kCoopPairDoubles*npair; e += 64) {
       g_gstage[e] = reinterpret_cast<const double*>(pairs)[e];
     }
+    for (int e = threadIdx.x; e < 3*m.ngeom; e += 64) gsize[e] = m.geom_size[e];
+  }
+  __syncthreads();
+  // the dofs on each body's chain (contactRowsSplit's bit test; nv <= 64 only)
+  const bool bydof = m.nv <= 64;
+  if (bydof && (int)threadIdx.x < m.nbody) {
+    unsigned long long dm = 0;
+    for (int j = 0; j < m.nv; j++) {
+      if ((chain[threadIdx.x] >> m.dof_bodyid[j]) & 1) dm |= 1ull << j;
+    }
+    dchain[threadIdx.x] = dm;
   }
   __syncthreads();
   const int sub = threadIdx.x % G, slot = threadIdx.x / G;
@@ -210,6 +228,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   const long inst = active ? (LIST ? (long)worklist[g] : g) : 0;
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
   d.chain = chain;
+  d.dchain = bydof ? dchain : nullptr;
   const int nv = m.nv, dsbl = m.opt.disableflags;
   int st = 0, ncon = 0;
   MJH_PHASE(14);
@@ -217,7 +236,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   // the geom frames for the collision phase, its survivor list, and the row forces for
   // J'force; all staged by the group with independent loads
   const int nq = m.nq, per = coopPerInstance(m, npair, d.con_cap, d.efc_cap);
-  double* lbase = g_gstage + kCoopPairDoubles*npair;
+  double* lbase = g_gstage + kCoopPairDoubles*npair + 3*ngeom;
   double* cdq = lbase + (long)slot*per;
   double* qp = cdq + 8*nv;
   double* gx = qp + nq;                     // geom_xpos (3 ngeom)
@@ -287,8 +306,10 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       int g1 = 0, g2 = 0, num = 0, cnt = 0, bodies[4] = {0, 0, 0, 0};
       double margin = 0;
       mjh::RawContact raw[2];
+      mjh::ContactParam cp{};
       if (active && k < nsurv) {            // narrowphase once: raw contacts kept in registers
         const CoopPair P = prog[surv[k]];
+        cp = cparams[surv[k]];              // in flight while the narrowphase computes
         g1 = P.g1;
         g2 = P.g2;
         margin = P.margin;
@@ -305,9 +326,9 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
           mjh::collidePlaneBoxCyl<64, false, BOX>(m, d, g1, g2, margin, cnt, &st, bbuf);
         } else {
           num = mjh::narrowPrimitive(P.t1, P.t2, margin, (const double*)(gx + 3*g1),
-                                     (const double*)(gm + 9*g1), m.geom_size + 3*g1,
+                                     (const double*)(gm + 9*g1), gsize + 3*g1,
                                      (const double*)(gx + 3*g2), (const double*)(gm + 9*g2),
-                                     m.geom_size + 3*g2, raw);
+                                     gsize + 3*g2, raw);
           cnt = num;
         }
       }
@@ -318,7 +339,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         if (num < 0) {
           mjh::collidePlaneBoxCyl<64, true, BOX>(m, d, g1, g2, margin, c, &st, bbuf);
         } else {
-          mjh::setContacts<64>(m, d, g1, g2, margin, raw, num, c, &st);
+          mjh::storeContacts<64>(m, d, g1, g2, margin, cp, raw, num, c, &st);
         }
         for (int q = ncon + excl; q < c && q < ncb; q++) {   // the contacts just stored
           for (int e = 0; e < 4; e++) cbody[4*q + e] = bodies[e];
@@ -473,28 +494,35 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       }
     }
     MJH_PHASE(18);
-    // contact rows (pyramidal or frictionless: the fused path excludes elliptic cones)
+    // contact rows (pyramidal or frictionless: the fused path excludes elliptic cones):
+    // kCoopContactLanes lanes per contact (contactRowsSplit), G / kCoopContactLanes contacts
+    // per round; a prefix sum over the contacts' row counts (held by each contact's first
+    // lane) gives each its first row; wide contacts (condim 4, 6) run on their first lane
     if (CONTACT && !(dsbl & mjhipDSBL_CONTACT) && nv) {
+      constexpr int Q = kCoopContactLanes, CPR = G / Q;
+      const int cq = sub % Q;
       int nef = rc.nefc;
-      for (int c0 = 0; c0 < ncon; c0 += G) {
-        const int c = c0 + sub;
+      for (int c0 = 0; c0 < ncon; c0 += CPR) {
+        const int c = c0 + sub / Q;
         int rows = 0, dim = 0;
         if (c < ncon && !d.con_exclude[c]) {
           dim = d.con_dim[c];
           rows = dim == 1 ? 1 : 2*(dim - 1);
         }
+        const int mine = cq == 0 ? rows : 0;
         int total;
-        const int off = nef + groupScan<G>(rows, sub, &total) - rows;
+        const int off = __shfl(nef + groupScan<G>(mine, sub, &total) - mine,
+                               (int)(threadIdx.x & ~(unsigned)(Q - 1)));
         if (rows) {
           if (off + rows > d.efc_cap) {     // mjWARN_CNSTRFULL analogue (capacity is exact)
             st |= MJHIP_INST_CNSTRFULL;
           } else {
-            d.con_efc_address[c] = off;
+            if (cq == 0) d.con_efc_address[c] = off;
             switch (dim) {
-              case 1: mjh::contactRowsFused<64, 1>(m, d, c, off); break;
-              case 3: mjh::contactRowsFused<64, 3>(m, d, c, off); break;
-              case 4: mjh::contactRowsFused<64, 4>(m, d, c, off); break;
-              default: mjh::contactRowsFused<64, 6>(m, d, c, off); break;
+              case 1: mjh::contactRowsSplit<64, 1, Q>(m, d, c, off, cq); break;
+              case 3: mjh::contactRowsSplit<64, 3, Q>(m, d, c, off, cq); break;
+              case 4: if (cq == 0) mjh::contactRowsFused<64, 4>(m, d, c, off); break;
+              default: if (cq == 0) mjh::contactRowsFused<64, 6>(m, d, c, off); break;
             }
           }
         }
@@ -822,6 +850,7 @@ struct mjhipContext_ {
   int wl_parity = 0;                       // counter the next fast launch uses
   int wl_last = 0;                         // counter the last fast launch used
   CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
+  mjh::ContactParam* cparams = nullptr;    // each program pair's mj_contactParam
   int npair = 0;
   bool boxpair = false;                    // a box-box pair is in the program (coop LDS)
   int coop = 16;                           // lanes per instance of k_constraint_coop (0: off)
@@ -976,9 +1005,19 @@ static const char* unsupported(const mjhipModel* m) {
   }
   for (int i = 0; i < m->nsensor; i++) {
     const int t = m->sensor_type[i];
-    if (t == mjhSENS_RANGEFINDER || t == mjhSENS_CAMPROJECTION ||
-        (t >= mjhSENS_GEOMDIST && t <= mjhSENS_GEOMFROMTO) || t > mjhSENS_CLOCK) {
-      return "rangefinder/camprojection/geom-distance/plugin/user sensors";
+    if (t == mjhSENS_CAMPROJECTION || (t >= mjhSENS_GEOMDIST && t <= mjhSENS_GEOMFROMTO) ||
+        t > mjhSENS_CLOCK) {
+      return "camprojection/geom-distance/plugin/user sensors";
+    }
+    if (t == mjhSENS_RANGEFINDER) {   // mj_ray's mesh, height-field and SDF paths are not built
+      const int body = m->site_bodyid[m->sensor_objid[i]];
+      for (int g = 0; g < m->ngeom; g++) {
+        const int gt = m->geom_type[g];
+        if ((gt == mjhipGEOM_MESH || gt == mjhipGEOM_HFIELD || gt == mjhipGEOM_SDF) &&
+            !mjh::rayEliminate(*m, g, body)) {
+          return "a rangefinder that can see a mesh, height field or SDF geom";
+        }
+      }
     }
   }
   return nullptr;
@@ -1173,8 +1212,19 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
     }
     if (c->npair) {
       const std::vector<CoopPair> prog = coop_program(m, pairs);
+      // contact parameters are model constants: formed here once per pair, by the same
+      // function (host arithmetic, as the reference's)
+      std::vector<mjh::ContactParam> cps(prog.size());
+      for (size_t i = 0; i < prog.size(); i++) {
+        mjh::ContactParam& q = cps[i];
+        mjh::contactParam(*m, prog[i].g1, prog[i].g2, &q.condim, &q.gap, q.solref, q.solimp,
+                          q.friction);
+      }
       if (hipMalloc((void**)&c->pairs, sizeof(CoopPair) * prog.size()) != hipSuccess ||
           hipMemcpy(c->pairs, prog.data(), sizeof(CoopPair) * prog.size(),
+                    hipMemcpyHostToDevice) != hipSuccess ||
+          hipMalloc((void**)&c->cparams, sizeof(mjh::ContactParam) * cps.size()) != hipSuccess ||
+          hipMemcpy(c->cparams, cps.data(), sizeof(mjh::ContactParam) * cps.size(),
                     hipMemcpyHostToDevice) != hipSuccess) {
         return fail("pair program upload");
       }
@@ -1216,6 +1266,7 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->status);
   hipFree(c->worklist);
   hipFree(c->pairs);
+  hipFree(c->cparams);
   hipFree(c->mirror_buf);
   hipFree(c->dmodel_buf);
   if (c->rt_module) hipModuleUnload(c->rt_module);
@@ -1316,7 +1367,7 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
                                                       c->npair, c->con_cap),                  \
                          c->stream,                                                           \
                          c->dmodel, c->mirror, B, wl,                                         \
-                         (const int*)cnt, c->pairs, c->npair, qfrc, status)
+                         (const int*)cnt, c->pairs, c->cparams, c->npair, qfrc, status)
       if (contact && c->boxpair) {       // the box-box path is compiled in only here
         if (list) MJHIP_LAUNCH_COOP(16, true, true, true);
         else MJHIP_LAUNCH_COOP(16, true, false, true);

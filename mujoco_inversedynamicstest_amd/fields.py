@@ -19,8 +19,9 @@ REPO_ROOT = os.path.dirname(_HERE)
 INCLUDE_DIR = os.path.join(REPO_ROOT, "include")
 FIELDS_HEADER = os.path.join(INCLUDE_DIR, "mjhip_fields.h")
 
-CTYPE = {"mjtNum": ctypes.c_double, "int": ctypes.c_int, "mjtByte": ctypes.c_ubyte}
-NPTYPE = {"mjtNum": np.float64, "int": np.int32, "mjtByte": np.uint8}
+CTYPE = {"mjtNum": ctypes.c_double, "int": ctypes.c_int, "mjtByte": ctypes.c_ubyte,
+         "float": ctypes.c_float}
+NPTYPE = {"mjtNum": np.float64, "int": np.int32, "mjtByte": np.uint8, "float": np.float32}
 
 
 @dataclass(frozen=True)

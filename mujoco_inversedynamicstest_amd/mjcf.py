@@ -48,7 +48,7 @@ OBJ = {"body": 1, "xbody": 2, "joint": 3, "dof": 4, "geom": 5, "site": 6, "camer
 # (dim, datatype, needstage). Stages: 1 POS, 2 VEL, 3 ACC. Datatypes: 0 REAL, 1 POSITIVE,
 # 2 AXIS, 3 QUATERNION. Frame sensors read objtype/objname (+ reftype/refname).
 SENSORS = {
-    "touch": (0, "site", 6, 1, 1, 3),
+    "touch": (0, "site", 6, 1, 1, 3), "rangefinder": (7, "site", 6, 1, 1, 1),
     "accelerometer": (1, "site", 6, 3, 0, 3), "velocimeter": (2, "site", 6, 3, 0, 2),
     "gyro": (3, "site", 6, 3, 0, 2), "force": (4, "site", 6, 3, 0, 3),
     "torque": (5, "site", 6, 3, 0, 3), "magnetometer": (6, "site", 6, 3, 0, 1),
@@ -72,7 +72,7 @@ SENSORS = {
     "e_potential": (40, None, 0, 1, 0, 1), "e_kinetic": (41, None, 0, 1, 0, 1),
     "clock": (42, None, 0, 1, 0, 1),
 }
-SENSORS_NEXT = ("rangefinder", "camprojection", "distance", "normal", "fromto",
+SENSORS_NEXT = ("camprojection", "distance", "normal", "fromto",
                 "user", "plugin")
 GEOM = {"plane": 0, "hfield": 1, "sphere": 2, "capsule": 3, "ellipsoid": 4,
         "cylinder": 5, "box": 6, "mesh": 7, "sdf": 8}
@@ -493,6 +493,7 @@ class MJCFCompiler:
     self.tendons = []
     self.actuators = []
     self.sensors = []
+    self.materials = {}                 # name -> rgba (<asset><material>)
     self.equalities = []
     self.excludes = []
     self.keys = []
@@ -633,7 +634,17 @@ class MJCFCompiler:
           if ch.tag not in SENSORS:
             raise MJCFError(f"unknown sensor <{ch.tag}>")
           self.sensors.append((ch.tag, dict(ch.attrib)))
-      elif t in ("visual", "asset", "statistic", "default", "compiler", "size", "extension"):
+      elif t == "asset":
+        # materials matter to mj_ray's visibility test (engine_ray.c:76-84); the rest of the
+        # assets has no effect on the inverse-dynamics path
+        for ch in el:
+          if ch.tag == "material":
+            a = self._elem_attrs(ch, "material", None)
+            rgba = [1.0, 1.0, 1.0, 1.0]                 # user_objects.cc mjCMaterial
+            v = _floats(a["rgba"]) if "rgba" in a else []
+            rgba[:len(v)] = v
+            self.materials[a.get("name", f"__material{len(self.materials)}")] = rgba
+      elif t in ("visual", "statistic", "default", "compiler", "size", "extension"):
         continue  # no effect on the inverse-dynamics path
       else:
         raise MJCFError(f"unsupported top-level element <{t}>")
@@ -762,6 +773,11 @@ class MJCFCompiler:
     g["margin"] = float(a.get("margin", 0.0))
     g["gap"] = float(a.get("gap", 0.0))
     g["name"] = a.get("name", "")
+    rgba = [0.5, 0.5, 0.5, 1.0]                  # user_init.c mjs_defaultGeom
+    v = _floats(a["rgba"]) if "rgba" in a else []
+    rgba[:len(v)] = v
+    g["rgba"] = rgba
+    g["material"] = a.get("material")
     # mass and inertia (user_objects.cc:3052-3080), typeinertia = volume
     g["mass"] = 0.0
     g["inertia"] = [0.0, 0.0, 0.0]
@@ -1171,6 +1187,13 @@ class MJCFCompiler:
     gquat = arr("geom_quat", (ng, 4), np.float64)
     gfric = arr("geom_friction", (ng, 3), np.float64)
     gfluid = arr("geom_fluid", (ng, 12), np.float64)
+    gmatid = arr("geom_matid", ng, np.int32, -1)
+    grgba = arr("geom_rgba", (ng, 4), np.float32)
+    matnames = list(self.materials)
+    s.update(nmat=len(matnames))
+    matrgba = arr("mat_rgba", (len(matnames), 4), np.float32)
+    for mi, name in enumerate(matnames):
+      matrgba[mi] = self.materials[name]
     for gi, g in enumerate(geoms):
       b = bodies[g["body"]]
       if geomadr[b.id] < 0:
@@ -1195,6 +1218,11 @@ class MJCFCompiler:
       gquat[gi] = g["quat"]
       gfric[gi] = g["friction"]
       gfluid[gi] = g["fluid"]
+      grgba[gi] = g["rgba"]
+      if g["material"] is not None:
+        if g["material"] not in self.materials:
+          raise MJCFError(f"unknown material '{g['material']}' in geom")
+        gmatid[gi] = matnames.index(g["material"])
       gsf[gi] = _sameframe(g["pos"], g["quat"], b.ipos, b.iquat)
       bcontype[b.id] |= g["contype"]
       bconaff[b.id] |= g["conaffinity"]

@@ -5440,10 +5440,14 @@ static int or_limitRow(const orEfc* e, int type, int id) {
   return -1;
 }
 
+/* mj_ray for the rangefinder (defined with the touch sensor's ray functions below) */
+static mjtNum or_ray(const mjhipModel* m, const mjhipData* d, const mjtNum* pnt,
+                     const mjtNum* vec, int bodyexclude, int* geomid);
+
 static void or_energyPos(const mjhipModel* m, mjhipData* d);
 static void or_energyVel(const mjhipModel* m, mjhipData* d);
 
-/* engine_sensor.c:209-513 mj_sensorPos (no rangefinder/camprojection/geom distance/user) */
+/* engine_sensor.c:209-513 mj_sensorPos (no camprojection/geom distance/user) */
 static void or_sensorPos(const mjhipModel* m, mjhipData* d, const orEfc* e) {
   if (mjDISABLED(mjhipDSBL_SENSOR)) return;
   for (int i = 0; i < m->nsensor; i++) {
@@ -5457,6 +5461,12 @@ static void or_sensorPos(const mjhipModel* m, mjhipData* d, const orEfc* e) {
     switch (type) {
     case SENS_MAGNETOMETER:
       mju_mulMatTVec(out, d->site_xmat + 9*objid, m->opt.magnetic, 3, 3);
+      break;
+    case SENS_RANGEFINDER:                   /* the site's z axis, its own body excluded */
+      rvec[0] = d->site_xmat[9*objid+2];
+      rvec[1] = d->site_xmat[9*objid+5];
+      rvec[2] = d->site_xmat[9*objid+8];
+      out[0] = or_ray(m, d, d->site_xpos + 3*objid, rvec, m->site_bodyid[objid], NULL);
       break;
     case SENS_JOINTPOS:
       out[0] = d->qpos[m->jnt_qposadr[objid]];
@@ -5780,6 +5790,37 @@ static mjtNum or_rayGeom(const mjtNum* pos, const mjtNum* mat, const mjtNum* siz
   default:                  return -1;
   }
 }
+
+/* the rangefinder (engine_sensor.c mjSENS_RANGEFINDER): mj_ray from the site along its z
+ * axis, geomgroup NULL, flg_static 1, the site's body excluded */
+/* :69-100 ray_eliminate with geomgroup NULL and flg_static 1: the excluded body's geoms and
+ * invisible geoms (alpha 0 of the geom, or of its material) */
+static int or_rayEliminate(const mjhipModel* m, int g, int bodyexclude) {
+  if (m->geom_bodyid[g] == bodyexclude) return 1;
+  const int mat = m->geom_matid[g];
+  if (mat < 0 && m->geom_rgba[4*g+3] == 0) return 1;
+  if (mat >= 0 && m->mat_rgba[4*mat+3] == 0) return 1;
+  return 0;
+}
+
+/* :1145-1185 mj_ray (geomgroup NULL, flg_static 1): the nearest hit, -1 for none; the geom hit
+ * in *geomid */
+static mjtNum or_ray(const mjhipModel* m, const mjhipData* d, const mjtNum* pnt, const mjtNum* vec,
+              int bodyexclude, int* geomid) {
+  mjtNum dist = -1;
+  if (geomid) *geomid = -1;
+  for (int g = 0; g < m->ngeom; g++) {
+    if (or_rayEliminate(m, g, bodyexclude)) continue;
+    const mjtNum nd = or_rayGeom(d->geom_xpos+3*g, d->geom_xmat+9*g, m->geom_size+3*g, pnt, vec,
+                                 m->geom_type[g]);
+    if (nd >= 0 && (nd < dist || dist < 0)) {
+      dist = nd;
+      if (geomid) *geomid = g;
+    }
+  }
+  return dist;
+}
+
 
 /* the touch sensor (engine_sensor.c:750-793): normal forces of the contacts of the site's
  * body whose normal ray, from the contact point, hits the site's zone */

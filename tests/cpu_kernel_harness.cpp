@@ -103,5 +103,6 @@ static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int
   L.nfst = 0;
   L.cbody = nullptr;
   L.ncbody = 0;
+  L.dchain = nullptr;
   return L;
 }

@@ -1023,6 +1023,41 @@ def test_ellipsoid_fluid_parity():
   assert_close(fl_gpu, np.array(fl), "qfrc_fluid")
 
 
+def test_rangefinder_parity():
+  """Rangefinders on moving bodies among every primitive type (one geom half transparent, one
+  invisible, one sensor with a cutoff): sensordata on the device vs the oracle."""
+  import os
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+  from test_rangefinder_cpu import SCENE
+  from mujoco_inversedynamicstest_amd import mjcf
+  m = mjcf.load_xml_string(SCENE)
+  B = 1024
+  rng = np.random.default_rng(8)
+  q = np.tile(m.qpos0, (B, 1))
+  q[:, :3] = rng.uniform(-1, 1, (B, 3)) + [0, 0, 1]
+  qq = rng.normal(size=(B, 4))
+  q[:, 3:7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
+  q[:, 7:] = rng.uniform(-2, 2, (B, 2))
+  v, a = rng.normal(size=(B, m.nv)), rng.normal(size=(B, m.nv))
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    f = e.inverse(q, v, a)
+    sd = e.field("sensordata", 0, B)
+  finally:
+    e.close()
+  o = Oracle(m)
+  ref, rsd = [], []
+  for i in range(B):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    rsd.append(o.d.sensordata.copy())
+  rsd = np.array(rsd)
+  assert (rsd >= 0).sum() > 1000 and (rsd < 0).sum() > 200
+  np.testing.assert_array_equal(sd < 0, rsd < 0)        # hit or miss, exactly
+  assert_close(sd, rsd, "sensordata")
+  assert_close(f, np.array(ref), "qfrc_inverse")
+
+
 def test_elliptic_cone_parity():
   """Elliptic friction cones (classic constraint passes) on the device: humanoid config-4
   states with cone="elliptic"."""

@@ -387,7 +387,7 @@ def test_sensor_skip_stages_keep_values():
 
 
 def test_unsupported_sensors_rejected():
-  for tag in ("rangefinder", "camprojection"):
+  for tag in ("camprojection",):
     with pytest.raises(mjcf.MJCFError):
       mjcf.load_xml_string(f"""<mujoco><worldbody><site name="s"/></worldbody>
         <sensor><{tag} site="s"/></sensor></mujoco>""")

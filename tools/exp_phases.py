@@ -92,6 +92,13 @@ def run(B=4096, reps=5):
       for name, x in zip(names, d):
         print(f"  {name:28s} {x:9.1f}")
       print(f"  {'total':28s} {d.sum():9.1f}", flush=True)
+    # spans inside one contact's rows (lane 0 of each wave): slot k sums, k + 1 counts
+    spans = [("contact data+impedance", 20), ("contact dof loop", 22), ("contact finish", 24)]
+    if sums[21] > 0:
+      print(" per contact (lane 0's contacts, mean us)")
+      for name, k in spans:
+        print(f"  {name:28s} {sums[k] / sums[k + 1] / 100.0:9.2f}  ({int(sums[k + 1] / reps)} "
+              f"contacts per call)")
   eng.close()
 
 
