@@ -77,6 +77,11 @@ LANES = {"pos": 64, "fac": 64, "va": 64}
 # two waves share a SIMD)
 ALL_LANES = 64
 ALL_WAVES = 1
+# stores of mirror fields no later stage of the kernel re-reads go out as streaming
+# (non-temporal) stores, MJH_NT_STORE in engine_device.h, so they do not displace the lines
+# the later stages re-read (qM, cinert, cdof) from L2; -DMJHIP_NO_NT compiles them as plain
+# stores (the A/B build)
+NT_STORES = True
 
 
 def _ll(st):
@@ -1247,6 +1252,17 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
     raise ValueError(f"model '{name}' cannot use the straight-line kernels: {why}")
   M = _Model(m)
   bodies = {st: _GEN[st](M, store_fields) for st in STAGES}
+  if NT_STORES:
+    import re
+    reread = set(re.findall(r"= P_(\w+)\[", "\n".join(bodies.values())))
+    store = re.compile(r"^(\s*)P_(\w+)\[(\d+)\*64\] = (.+);$")
+
+    def nt(line):
+      mt = store.match(line)
+      if not mt or mt.group(2) in reread:
+        return line
+      return f"{mt.group(1)}MJH_NT_STORE(P_{mt.group(2)}[{mt.group(3)}*64], {mt.group(4)});"
+    bodies = {st: "\n".join(nt(x) for x in b.split("\n")) for st, b in bodies.items()}
   out = [f"// GENERATED by mujoco_inversedynamicstest_amd/codegen.py -- do not edit.",
          f"// model '{name}' (nq={m.nq} nv={m.nv} nbody={m.nbody}), hash {model_hash(m)}"]
   for st in STAGES:

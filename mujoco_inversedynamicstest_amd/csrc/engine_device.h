@@ -57,6 +57,14 @@ __device__ unsigned long long mjh_phase_acc[32];
 #define MJH_SPAN(k, a, b) do {} while (0)
 #endif
 
+// a streaming (non-temporal) store of a mirror value the kernel does not read back (the
+// generated kernels, codegen.NT_STORES); a plain store in host builds and with -DMJHIP_NO_NT
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(MJHIP_NO_NT)
+#define MJH_NT_STORE(lv, v) __builtin_nontemporal_store((double)(v), &(lv))
+#else
+#define MJH_NT_STORE(lv, v) ((lv) = (v))
+#endif
+
 // mjtSensor values (include/mujoco/mjmodel.h)
 enum { mjhSENS_TOUCH = 0, mjhSENS_ACCELEROMETER, mjhSENS_VELOCIMETER, mjhSENS_GYRO,
        mjhSENS_FORCE, mjhSENS_TORQUE, mjhSENS_MAGNETOMETER, mjhSENS_RANGEFINDER,
@@ -250,8 +258,8 @@ struct Lane {
   // fused constraint path only (nbody <= 64): chain[k] has bit b set when body b is body k
   // or one of its ancestors (on the device a per-block LDS table, chainMasks)
   const unsigned long long* chain;
-  // cooperative constraint kernel only (else nullptr; nv <= 64): dchain[k] has bit j set when
-  // dof j belongs to body k or one of its ancestors (a per-block LDS table)
+  // cooperative constraint kernel only (else nullptr; it runs only when nv <= 64): dchain[k]
+  // has bit j set when dof j belongs to body k or one of its ancestors (a per-block LDS table)
   const unsigned long long* dchain;
   // geom positions as collision reads them: geom_xpos itself, or (gstage) a per-lane LDS
   // copy that collision() fills first -- the broadphase reads every candidate pair's
@@ -4716,11 +4724,10 @@ MJH_HD void contactRowsSplit(const mjhipModel& m, const Lane<S>& d, int i, int n
   double off1[3], off2[3];
   sub3(off1, pos, d.subtree_com + 3*rt1);
   sub3(off2, pos, d.subtree_com + 3*rt2);
-  // the dofs on each body's chain: a bit test per dof (the per-dof body id is lane-dependent
-  // here, and a memory load of it would wait for the lane's earlier row stores)
-  const bool bydof = d.dchain != nullptr;
-  const unsigned long long mask1 = bydof ? d.dchain[b1] : d.chain[b1];
-  const unsigned long long mask2 = bydof ? d.dchain[b2] : d.chain[b2];
+  // the dofs on each body's chain (d.dchain, the kernel's LDS table): a bit test per dof. The
+  // dof is lane-dependent here, so reading its body id from memory would be a vector load,
+  // and every vector load waits for the lane's earlier row stores.
+  const unsigned long long mask1 = d.dchain[b1], mask2 = d.dchain[b2];
   double kb[4];
   rowImpedance(m, tp, solref, solimp, dist, incl, kb);
   double tran = 0;
@@ -4741,8 +4748,7 @@ MJH_HD void contactRowsSplit(const mjhipModel& m, const Lane<S>& d, int i, int n
   SP<S> J = d.efc_J + nefc*nv;
   // one dof's rows into efc_J, returned in Jv (as contactRowsFused forms them)
   auto dofRows = [&](int j, const double* cd, double Jv[ROWS]) MJH_LAMBDA_INLINE {
-    const int bj = bydof ? j : m.dof_bodyid[j];
-    const bool in1 = (mask1 >> bj) & 1, in2 = (mask2 >> bj) & 1;
+    const bool in1 = (mask1 >> j) & 1, in2 = (mask2 >> j) & 1;
     double t1[3], t2[3], jd[3], cj[3] = {0, 0, 0};
     cross(t1, cd, off1);
     cross(t2, cd, off2);

@@ -162,7 +162,7 @@ static_assert(sizeof(CoopPair) % sizeof(double) == 0, "CoopPair packs into doubl
 constexpr int kBoxBoxBuf = 72;
 constexpr int kCoopContacts = 64;
 #ifndef MJHIP_COOP_CQ
-#define MJHIP_COOP_CQ 4
+#define MJHIP_COOP_CQ 2
 #endif
 constexpr int kCoopContactLanes = MJHIP_COOP_CQ;   // lanes per contact in the contact rows
 constexpr int kCoopRows = 128;
@@ -208,9 +208,8 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
     for (int e = threadIdx.x; e < 3*m.ngeom; e += 64) gsize[e] = m.geom_size[e];
   }
   __syncthreads();
-  // the dofs on each body's chain (contactRowsSplit's bit test; nv <= 64 only)
-  const bool bydof = m.nv <= 64;
-  if (bydof && (int)threadIdx.x < m.nbody) {
+  // the dofs on each body's chain (contactRowsSplit's bit test; the kernel runs for nv <= 64)
+  if ((int)threadIdx.x < m.nbody) {
     unsigned long long dm = 0;
     for (int j = 0; j < m.nv; j++) {
       if ((chain[threadIdx.x] >> m.dof_bodyid[j]) & 1) dm |= 1ull << j;
@@ -228,7 +227,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   const long inst = active ? (LIST ? (long)worklist[g] : g) : 0;
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
   d.chain = chain;
-  d.dchain = bydof ? dchain : nullptr;
+  d.dchain = dchain;
   const int nv = m.nv, dsbl = m.opt.disableflags;
   int st = 0, ncon = 0;
   MJH_PHASE(14);
@@ -545,6 +544,14 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
     for (int j0 = sub; j0 < nv; j0 += 2*G) {
       const int j1 = j0 + G;
       const bool has1 = j1 < nv;
+      // the assembly's inputs, loaded ahead of the rows (a load issued after this lane's
+      // stores would wait for them)
+      const double rne0 = d.qfrc_inverse[j0], arm0 = m.dof_armature[j0];
+      const double pas0 = d.qfrc_passive[j0], qa0 = cdq[8*j0 + 7];
+      const double rne1 = has1 ? (double)d.qfrc_inverse[j1] : 0.0;
+      const double arm1 = has1 ? m.dof_armature[j1] : 0.0;
+      const double pas1 = has1 ? (double)d.qfrc_passive[j1] : 0.0;
+      const double qa1 = has1 ? cdq[8*j1 + 7] : 0.0;
       double acc0 = 0, acc1 = 0;
       for (int r0 = 0; r0 < nefc; r0 += 8) {
         double f[8], x0[8], x1[8];
@@ -567,13 +574,15 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
           }
         }
       }
+      const double out0 = rne0 + (arm0 * qa0 - pas0 - acc0);
       d.qfrc_constraint[j0] = acc0;
-      d.qfrc_inverse[j0] += m.dof_armature[j0] * d.qacc[j0] - d.qfrc_passive[j0] - acc0;
-      if (qfrc_out) qfrc_out[inst*nv + j0] = d.qfrc_inverse[j0];
+      d.qfrc_inverse[j0] = out0;
+      if (qfrc_out) qfrc_out[inst*nv + j0] = out0;
       if (has1) {
+        const double out1 = rne1 + (arm1 * qa1 - pas1 - acc1);
         d.qfrc_constraint[j1] = acc1;
-        d.qfrc_inverse[j1] += m.dof_armature[j1] * d.qacc[j1] - d.qfrc_passive[j1] - acc1;
-        if (qfrc_out) qfrc_out[inst*nv + j1] = d.qfrc_inverse[j1];
+        d.qfrc_inverse[j1] = out1;
+        if (qfrc_out) qfrc_out[inst*nv + j1] = out1;
       }
     }
     for (int o = G/2; o; o >>= 1) st |= __shfl_xor(st, o, G);
@@ -1233,6 +1242,8 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   // the native convex solver keeps its polytope in the instance's scratch: one lane per
   // instance (the cooperative kernel would run several pairs of an instance at once)
   if (mjh_needConvex(m)) c->coop = 0;
+  // the cooperative kernel's per-dof chain masks are 64-bit
+  if (m->nv > 64) c->coop = 0;
   if (c->coop) {
     // the cooperative kernel's dynamic LDS must fit one block: many box pairs (a large
     // efc_cap) or few lanes per instance can exceed it, and then the one-lane k_constraint

@@ -22,7 +22,9 @@ import numpy as np
 from . import fields, host
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmjhip.so")
+# MJHIP_LIB: an experiment build of the same library (tools/exp_phases.py variants); the
+# default is the in-tree build, and a missing library is an error (no fallback path)
+LIB_PATH = os.environ.get("MJHIP_LIB") or os.path.join(_HERE, "libmjhip.so")
 
 mjSTAGE_NONE, mjSTAGE_POS, mjSTAGE_VEL = 0, 1, 2
 FLAG_DEVICE_PTRS, FLAG_MIRROR_INPUT, FLAG_NO_MIRROR, FLAG_GENERIC = 1, 2, 4, 8

@@ -17,7 +17,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 EXP = os.path.join(ROOT, "tools", "exp")
-LIB = os.path.join(ROOT, "tools", "exp_lib", "libmjhip_phase.so")   # travels to the GPU box
+# PHASE_CQ=n builds/runs a variant with n lanes per contact in the cooperative contact rows
+CQ = os.environ.get("PHASE_CQ", "")
+LIB = os.path.join(ROOT, "tools", "exp_lib",
+                   f"libmjhip_phase{'_cq' + CQ if CQ else ''}.so")   # travels to the GPU box
 # generic pipeline (k_inverse): marks 0-9; constraint kernel after the generated kernels
 # (k_constraint, mjh::constraintOnly): marks 10-13
 GROUPS = [
@@ -38,9 +41,11 @@ def build():
   # the two translation units of libmjhip (the generated kernels need no phase marks; their
   # object is kept between builds), then one shared library
   hipcc = "/opt/rocm/bin/hipcc"
-  gen_o, main_o = os.path.join(EXP, "gen_fast.o"), os.path.join(EXP, "mjhip_phase.o")
-  procs = [subprocess.Popen([hipcc, *ge.HIPCC_FLAGS, "-DMJH_PHASE_TIMING", "-c", "-o", main_o,
-                             os.path.join(ge.CSRC, "mjhip.hip")])]
+  gen_o = os.path.join(EXP, "gen_fast.o")
+  main_o = os.path.join(EXP, f"mjhip_phase{CQ}.o")
+  cq = [f"-DMJHIP_COOP_CQ={CQ}"] if CQ else []
+  procs = [subprocess.Popen([hipcc, *ge.HIPCC_FLAGS, "-DMJH_PHASE_TIMING", *cq, "-c", "-o",
+                             main_o, os.path.join(ge.CSRC, "mjhip.hip")])]
   if not ge._newer(gen_o, [os.path.join(ge.CSRC, "gen_fast.inc")]):
     procs.append(subprocess.Popen([hipcc, *ge.HIPCC_FLAGS, "-c", "-o", gen_o,
                                    os.path.join(ge.CSRC, "gen_fast.hip")]))

@@ -20,6 +20,13 @@ tail -1 gpurun_out/c4_64k.json
 echo "== phases (tools/exp_lib build must match the tree)"
 timeout -k 10 120 python tools/exp_phases.py run 4096 > gpurun_out/phase16.log 2>&1 || exit 1
 cat gpurun_out/phase16.log
+for cq in 1 2; do
+  if [ -f tools/exp_lib/libmjhip_phase_cq$cq.so ]; then
+    echo "-- $cq lane(s) per contact"
+    PHASE_CQ=$cq timeout -k 10 120 python tools/exp_phases.py run 4096 > gpurun_out/phase16_cq$cq.log 2>&1 || exit 1
+    grep -A6 "k_constraint_coop\|per contact" gpurun_out/phase16_cq$cq.log | grep -v generic
+  fi
+done
 echo "== rocprof config4"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o prof --output-format csv -- python bench.py --config 4 --steps 10 --warmup 3 > gpurun_out/prof_c4.log 2>&1 || exit 1
 find gpurun_out/prof_c4 -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-160
