@@ -136,6 +136,10 @@
   X(mjtNum,  cam_poscom0,          ncam,      3) \
   X(mjtNum,  cam_pos0,             ncam,      3) \
   X(mjtNum,  cam_mat0,             ncam,      9) \
+  X(mjtNum,  cam_fovy,             ncam,      1) \
+  X(int,     cam_resolution,       ncam,      2) \
+  X(float,   cam_sensorsize,       ncam,      2) \
+  X(float,   cam_intrinsic,        ncam,      4) \
   X(int,     light_mode,           nlight,    1) \
   X(int,     light_bodyid,         nlight,    1) \
   X(int,     light_targetbodyid,   nlight,    1) \

@@ -4441,16 +4441,17 @@ template <int S>
 MJH_HD void finishRowFused(const Lane<S>& d, int r, int tp, const double kb[4], double R,
                            double pos, double margin, double frictionloss, double vel,
                            double acc) {
-  for (int k = 0; k < 4; k++) d.efc_KBIP[4*r+k] = kb[k];
+  // outputs no kernel of the call reads back go out as streaming stores
+  for (int k = 0; k < 4; k++) MJH_NT_STORE(d.efc_KBIP[4*r+k], kb[k]);
   const double D = 1 / R;
-  d.efc_R[r] = R;
-  d.efc_D[r] = D;
-  d.efc_diagApprox[r] = R * kb[2] / (1-kb[2]);
-  d.efc_vel[r] = vel;
+  MJH_NT_STORE(d.efc_R[r], R);
+  MJH_NT_STORE(d.efc_D[r], D);
+  MJH_NT_STORE(d.efc_diagApprox[r], R * kb[2] / (1-kb[2]));
+  MJH_NT_STORE(d.efc_vel[r], vel);
   const double aref = -kb[1]*vel - kb[0]*kb[2]*(pos-margin);
-  d.efc_aref[r] = aref;
+  MJH_NT_STORE(d.efc_aref[r], aref);
   const double jar = acc - aref;
-  d.jar[r] = jar;
+  MJH_NT_STORE(d.jar[r], jar);
   double force = -D * jar;
   int state = CNSTRSTATE_QUADRATIC;
   if (tp == CNSTR_FRICTION_DOF || tp == CNSTR_FRICTION_TENDON) {
@@ -6047,13 +6048,52 @@ MJH_HD int limitRow(const Lane<S>& d, int type, int id) {
   return -1;
 }
 
+// engine_sensor.c:126-215 cam_project (the oracle's or_camProject): the reference's explicit
+// 4x4 product image * focal * rotation * translation, every term in its loop order
+template <class Q, class P, class M>
+MJH_HD void camProject(double out[2], Q target, P cpos, M cmat, const int* res, double fovy,
+                       const float* intr, const float* size) {
+  double T[4][4] = {{0}}, Rm[4][4] = {{0}}, F[3][4] = {{0}}, I[3][3] = {{0}}, Pm[3][4] = {{0}};
+  double fx, fy;
+  for (int i = 0; i < 4; i++) T[i][i] = Rm[i][i] = 1;
+  for (int i = 0; i < 3; i++) T[i][3] = -cpos[i];
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) Rm[i][j] = cmat[3*j+i];
+  }
+  if (size[0] && size[1]) {
+    fx = intr[0] / size[0] * res[0];
+    fy = intr[1] / size[1] * res[1];
+  } else {
+    fx = fy = .5 / tan(fovy * mjhipPI / 360.) * res[1];
+  }
+  F[0][0] = -fx;
+  F[1][1] = fy;
+  F[2][2] = 1.0;
+  I[0][0] = I[1][1] = I[2][2] = 1;
+  I[0][2] = (double)res[0] / 2.0;
+  I[1][2] = (double)res[1] / 2.0;
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++)
+      for (int k = 0; k < 4; k++)
+        for (int l = 0; l < 4; l++)
+          for (int n = 0; n < 4; n++) Pm[i][n] += I[i][j] * F[j][k] * Rm[k][l] * T[l][n];
+  const double ph[4] = {target[0], target[1], target[2], 1};
+  double px[3] = {0, 0, 0};
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 4; j++) px[i] += Pm[i][j] * ph[j];
+  }
+  double den = px[2];
+  if (fabs(den) < MINVAL) den = den < 0 ? dmin(den, -MINVAL) : dmax(den, MINVAL);
+  out[0] = px[0] / den;
+  out[1] = px[1] / den;
+}
+
 // mj_ray for the rangefinder (defined with the touch sensor's ray functions below)
 template <int S>
 MJH_HD double ray(const mjhipModel& m, const Lane<S>& d, const double pnt[3],
                   const double vec[3], int bodyexclude);
 
-// engine_sensor.c:209-513 mj_sensorPos (no camprojection/geom distance/user, rejected at
-// load)
+// engine_sensor.c:209-513 mj_sensorPos (no geom distance/user, rejected at load)
 template <int S>
 MJH_HD void sensorPos(const mjhipModel& m, const Lane<S>& d) {
   if (m.opt.disableflags & mjhipDSBL_SENSOR) return;
@@ -6070,6 +6110,15 @@ MJH_HD void sensorPos(const mjhipModel& m, const Lane<S>& d) {
     case mjhSENS_MAGNETOMETER:
       mulMatTVec(out, d.site_xmat + 9*objid, m.opt.magnetic, 3, 3);
       break;
+    case mjhSENS_CAMPROJECTION: {
+      double px[2];
+      camProject(px, d.site_xpos + 3*objid, d.cam_xpos + 3*refid, d.cam_xmat + 9*refid,
+                 m.cam_resolution + 2*refid, m.cam_fovy[refid], m.cam_intrinsic + 4*refid,
+                 m.cam_sensorsize + 2*refid);
+      out[0] = px[0];
+      out[1] = px[1];
+      break;
+    }
     case mjhSENS_RANGEFINDER:              // the site's z axis, its own body excluded
       rvec[0] = d.site_xmat[9*objid+2];
       rvec[1] = d.site_xmat[9*objid+5];

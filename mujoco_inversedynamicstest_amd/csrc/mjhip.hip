@@ -1014,9 +1014,8 @@ static const char* unsupported(const mjhipModel* m) {
   }
   for (int i = 0; i < m->nsensor; i++) {
     const int t = m->sensor_type[i];
-    if (t == mjhSENS_CAMPROJECTION || (t >= mjhSENS_GEOMDIST && t <= mjhSENS_GEOMFROMTO) ||
-        t > mjhSENS_CLOCK) {
-      return "camprojection/geom-distance/plugin/user sensors";
+    if ((t >= mjhSENS_GEOMDIST && t <= mjhSENS_GEOMFROMTO) || t > mjhSENS_CLOCK) {
+      return "geom-distance/plugin/user sensors";
     }
     if (t == mjhSENS_RANGEFINDER) {   // mj_ray's mesh, height-field and SDF paths are not built
       const int body = m->site_bodyid[m->sensor_objid[i]];

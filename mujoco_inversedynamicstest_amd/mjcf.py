@@ -49,6 +49,7 @@ OBJ = {"body": 1, "xbody": 2, "joint": 3, "dof": 4, "geom": 5, "site": 6, "camer
 # 2 AXIS, 3 QUATERNION. Frame sensors read objtype/objname (+ reftype/refname).
 SENSORS = {
     "touch": (0, "site", 6, 1, 1, 3), "rangefinder": (7, "site", 6, 1, 1, 1),
+    "camprojection": (8, "site", 6, 2, 0, 1),
     "accelerometer": (1, "site", 6, 3, 0, 3), "velocimeter": (2, "site", 6, 3, 0, 2),
     "gyro": (3, "site", 6, 3, 0, 2), "force": (4, "site", 6, 3, 0, 3),
     "torque": (5, "site", 6, 3, 0, 3), "magnetometer": (6, "site", 6, 3, 0, 1),
@@ -72,7 +73,7 @@ SENSORS = {
     "e_potential": (40, None, 0, 1, 0, 1), "e_kinetic": (41, None, 0, 1, 0, 1),
     "clock": (42, None, 0, 1, 0, 1),
 }
-SENSORS_NEXT = ("camprojection", "distance", "normal", "fromto",
+SENSORS_NEXT = ("distance", "normal", "fromto",
                 "user", "plugin")
 GEOM = {"plane": 0, "hfield": 1, "sphere": 2, "capsule": 3, "ellipsoid": 4,
         "cylinder": 5, "box": 6, "mesh": 7, "sdf": 8}
@@ -992,8 +993,32 @@ class MJCFCompiler:
     quat = _floats(a["quat"]) if "quat" in a else [1.0, 0.0, 0.0, 0.0]
     normvec(quat)
     quat = _resolve_orientation(a, self.degree, self.eulerseq, quat)
+    # intrinsics (user_objects.cc mjCCamera::Compile :3383-3420, float arithmetic)
+    f32 = np.float32
+    fovy = float(a.get("fovy", 45.0))
+    if fovy >= 180:
+      raise MJCFError("fovy too large in camera")
+    res = [int(x) for x in a["resolution"].split()] if "resolution" in a else [1, 1]
+    size = [f32(x) for x in _floats(a["sensorsize"])] if "sensorsize" in a else [f32(0)] * 2
+
+    def pair(name):
+      return [f32(x) for x in _floats(a[name])] if name in a else [f32(0)] * 2
+    fl, fp, pl, pp = pair("focal"), pair("focalpixel"), pair("principal"), pair("principalpixel")
+    if (pl[0] and pp[0]) or (pl[1] and pp[1]):
+      raise MJCFError("principal length duplicated in camera")
+    if (fl[0] and fp[0]) or (fl[1] and fp[1]):
+      raise MJCFError("focal length duplicated in camera")
+    if size[0] > 0 and size[1] > 0:
+      dens = [f32(res[0]) / size[0], f32(res[1]) / size[1]]
+      intr = [fp[0] / dens[0] + fl[0], fp[1] / dens[1] + fl[1],
+              pp[0] / dens[0] + pl[0], pp[1] / dens[1] + pl[1]]
+      fovy = float(np.arctan2(float(size[1]) / 2, float(intr[1])) * 360.0 / np.pi)
+    else:
+      znear = f32(0.01)                        # visual.map.znear (the <visual> element is not read)
+      intr = [znear, znear, f32(0), f32(0)]
     return {"body": bid, "pos": pos, "quat": quat, "mode": CAMLIGHT[a.get("mode", "fixed")],
-            "target": a.get("target"), "name": a.get("name", "")}
+            "target": a.get("target"), "name": a.get("name", ""), "fovy": fovy,
+            "resolution": res, "sensorsize": size, "intrinsic": intr}
 
   def _compile_light(self, a, bid):
     pos = _floats(a["pos"]) if "pos" in a else [0.0, 0.0, 0.0]
@@ -1253,7 +1278,15 @@ class MJCFCompiler:
     arr("cam_poscom0", (nc, 3), np.float64)
     arr("cam_pos0", (nc, 3), np.float64)
     arr("cam_mat0", (nc, 9), np.float64)
+    cfovy = arr("cam_fovy", nc, np.float64)
+    cres = arr("cam_resolution", (nc, 2), np.int32)
+    csize = arr("cam_sensorsize", (nc, 2), np.float32)
+    cintr = arr("cam_intrinsic", (nc, 4), np.float32)
     for ci, c in enumerate(cams):
+      cfovy[ci] = c["fovy"]
+      cres[ci] = c["resolution"]
+      csize[ci] = c["sensorsize"]
+      cintr[ci] = c["intrinsic"]
       cmode[ci] = c["mode"]
       cbody[ci] = c["body"]
       cpos[ci] = c["pos"]
@@ -1648,6 +1681,8 @@ class MJCFCompiler:
         oid = -1
       else:
         oid = find(ot, a.get(attr), "sensorized object")
+        if tp == 8:                                # camprojection: the camera is the reference
+          rt, rid = 7, find(7, a.get("camera"), "camera")
         if ot == 3:
           jt = int(jtype[oid])
           if tp in (9, 10, 16) and jt not in (2, 3):

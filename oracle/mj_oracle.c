@@ -5440,6 +5440,47 @@ static int or_limitRow(const orEfc* e, int type, int id) {
   return -1;
 }
 
+/* engine_sensor.c:126-215 cam_project: the pixel coordinates of a point in a camera's image,
+ * through the reference's explicit 4x4 product image * focal * rotation * translation (every
+ * term in its loop order, zeros included) */
+static void or_camProject(mjtNum out[2], const mjtNum* target, const mjtNum* cpos,
+                          const mjtNum* cmat, const int* res, mjtNum fovy, const float* intr,
+                          const float* size) {
+  mjtNum T[4][4] = {{0}}, Rm[4][4] = {{0}}, F[3][4] = {{0}}, I[3][3] = {{0}}, P[3][4] = {{0}};
+  mjtNum fx, fy;
+  for (int i = 0; i < 4; i++) T[i][i] = Rm[i][i] = 1;
+  for (int i = 0; i < 3; i++) T[i][3] = -cpos[i];
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) Rm[i][j] = cmat[3*j+i];
+  }
+  if (size[0] && size[1]) {
+    fx = intr[0] / size[0] * res[0];
+    fy = intr[1] / size[1] * res[1];
+  } else {
+    fx = fy = .5 / tan(fovy * mjhipPI / 360.) * res[1];
+  }
+  F[0][0] = -fx;
+  F[1][1] = fy;
+  F[2][2] = 1.0;
+  I[0][0] = I[1][1] = I[2][2] = 1;
+  I[0][2] = (mjtNum)res[0] / 2.0;
+  I[1][2] = (mjtNum)res[1] / 2.0;
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++)
+      for (int k = 0; k < 4; k++)
+        for (int l = 0; l < 4; l++)
+          for (int n = 0; n < 4; n++) P[i][n] += I[i][j] * F[j][k] * Rm[k][l] * T[l][n];
+  const mjtNum ph[4] = {target[0], target[1], target[2], 1};
+  mjtNum px[3] = {0, 0, 0};
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 4; j++) px[i] += P[i][j] * ph[j];
+  }
+  mjtNum den = px[2];
+  if (fabs(den) < mjMINVAL) den = den < 0 ? mjMIN(den, -mjMINVAL) : mjMAX(den, mjMINVAL);
+  out[0] = px[0] / den;
+  out[1] = px[1] / den;
+}
+
 /* mj_ray for the rangefinder (defined with the touch sensor's ray functions below) */
 static mjtNum or_ray(const mjhipModel* m, const mjhipData* d, const mjtNum* pnt,
                      const mjtNum* vec, int bodyexclude, int* geomid);
@@ -5447,7 +5488,7 @@ static mjtNum or_ray(const mjhipModel* m, const mjhipData* d, const mjtNum* pnt,
 static void or_energyPos(const mjhipModel* m, mjhipData* d);
 static void or_energyVel(const mjhipModel* m, mjhipData* d);
 
-/* engine_sensor.c:209-513 mj_sensorPos (no camprojection/geom distance/user) */
+/* engine_sensor.c:209-513 mj_sensorPos (no geom distance/user) */
 static void or_sensorPos(const mjhipModel* m, mjhipData* d, const orEfc* e) {
   if (mjDISABLED(mjhipDSBL_SENSOR)) return;
   for (int i = 0; i < m->nsensor; i++) {
@@ -5461,6 +5502,11 @@ static void or_sensorPos(const mjhipModel* m, mjhipData* d, const orEfc* e) {
     switch (type) {
     case SENS_MAGNETOMETER:
       mju_mulMatTVec(out, d->site_xmat + 9*objid, m->opt.magnetic, 3, 3);
+      break;
+    case SENS_CAMPROJECTION:
+      or_camProject(out, d->site_xpos + 3*objid, d->cam_xpos + 3*refid, d->cam_xmat + 9*refid,
+                    m->cam_resolution + 2*refid, m->cam_fovy[refid],
+                    m->cam_intrinsic + 4*refid, m->cam_sensorsize + 2*refid);
       break;
     case SENS_RANGEFINDER:                   /* the site's z axis, its own body excluded */
       rvec[0] = d->site_xmat[9*objid+2];

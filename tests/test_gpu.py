@@ -1058,6 +1058,37 @@ def test_rangefinder_parity():
   assert_close(f, np.array(ref), "qfrc_inverse")
 
 
+def test_camprojection_parity():
+  """Camera projections from cameras on a free body and a hinge body (fovy and pinhole
+  intrinsics) on the device vs the oracle."""
+  import os
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+  from test_camprojection_cpu import MOVING
+  from mujoco_inversedynamicstest_amd import mjcf
+  m = mjcf.load_xml_string(MOVING)
+  B = 1024
+  rng = np.random.default_rng(12)
+  q = np.tile(m.qpos0, (B, 1))
+  q[:, :3] += rng.uniform(-.3, .3, (B, 3))
+  qq = rng.normal(size=(B, 4))
+  q[:, 3:7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
+  q[:, 7] = rng.uniform(-3, 3, B)
+  v, a = rng.normal(size=(B, m.nv)), rng.normal(size=(B, m.nv))
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    e.inverse(q, v, a)
+    sd = e.field("sensordata", 0, B)
+  finally:
+    e.close()
+  o = Oracle(m)
+  rsd = []
+  for i in range(B):
+    o.inverse(q[i], v[i], a[i])
+    rsd.append(o.d.sensordata.copy())
+  assert_close(sd, np.array(rsd), "sensordata")
+
+
 def test_elliptic_cone_parity():
   """Elliptic friction cones (classic constraint passes) on the device: humanoid config-4
   states with cone="elliptic"."""

@@ -387,10 +387,12 @@ def test_sensor_skip_stages_keep_values():
 
 
 def test_unsupported_sensors_rejected():
-  for tag in ("camprojection",):
-    with pytest.raises(mjcf.MJCFError):
-      mjcf.load_xml_string(f"""<mujoco><worldbody><site name="s"/></worldbody>
-        <sensor><{tag} site="s"/></sensor></mujoco>""")
+  """The geom-distance family is outside the subset: the loader says so."""
+  for tag in ("distance", "normal", "fromto"):
+    with pytest.raises(mjcf.MJCFError, match="not in the supported subset"):
+      mjcf.load_xml_string(f"""<mujoco><worldbody><geom name="a" size=".1"/>
+        <geom name="b" size=".1" pos="1 0 0"/></worldbody>
+        <sensor><{tag} geom1="a" geom2="b"/></sensor></mujoco>""")
 
 
 def test_bundled_linear_model_has_reference_sensors(linear):
