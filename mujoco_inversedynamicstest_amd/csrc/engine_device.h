@@ -127,12 +127,37 @@ MJH_HD int mjh_needConvex(const mjhipModel* m) {
   }
   return 0;
 }
+// a geom-distance sensor (mj_geomDistance) whose geom pairs include one the native solver
+// measures (mjc_Convex or box-box pairs)
+MJH_HD int mjh_needDistanceCcd(const mjhipModel* m) {
+  if (m->opt.disableflags & mjhipDSBL_NATIVECCD) return 0;
+  for (int i = 0; i < m->nsensor; i++) {
+    const int t = m->sensor_type[i];
+    if (t < mjhSENS_GEOMDIST || t > mjhSENS_GEOMFROMTO) continue;
+    const int o = m->sensor_objid[i], r = m->sensor_refid[i];
+    const int n1 = m->sensor_objtype[i] == 1 ? m->body_geomnum[o] : 1;
+    const int a1 = m->sensor_objtype[i] == 1 ? m->body_geomadr[o] : o;
+    const int n2 = m->sensor_reftype[i] == 1 ? m->body_geomnum[r] : 1;
+    const int a2 = m->sensor_reftype[i] == 1 ? m->body_geomadr[r] : r;
+    for (int g1 = a1; g1 < a1 + n1; g1++) {
+      for (int g2 = a2; g2 < a2 + n2; g2++) {
+        int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+        if (t1 > t2) { const int x = t1; t1 = t2; t2 = x; }
+        if (mjhip_isConvexPair(t1, t2) || (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX)) return 1;
+      }
+    }
+  }
+  return 0;
+}
 MJH_HD int mjh_ccdFaceCap(const mjhipModel* m) { return 6*m->opt.ccd_iterations + 6; }
+MJH_HD int mjh_needCcd(const mjhipModel* m) {
+  return mjh_needConvex(m) || mjh_needDistanceCcd(m);
+}
 MJH_HD int mjh_ccdDoubles(const mjhipModel* m) {
-  return mjh_needConvex(m) ? 72 + 9*(5 + m->opt.ccd_iterations) + 4*mjh_ccdFaceCap(m) : 0;
+  return mjh_needCcd(m) ? 72 + 9*(5 + m->opt.ccd_iterations) + 4*mjh_ccdFaceCap(m) : 0;
 }
 MJH_HD int mjh_ccdInts(const mjhipModel* m) {
-  return mjh_needConvex(m) ? 13*mjh_ccdFaceCap(m) : 0;
+  return mjh_needCcd(m) ? 13*mjh_ccdFaceCap(m) : 0;
 }
 // transmissions the generated kernels leave to the pass after the constraint kernel
 // (mjh::transmissionAfter): slider-crank, site and body (adhesion) ones
@@ -2631,16 +2656,17 @@ MJH_HD int ccdEpa(CcdState& st, const CcdMem<S>& M, CcdPoly& P, const CcdShape& 
   return f;
 }
 
-// mjc_ccd (:2215-2343) with max_contacts = 1 and dist_cutoff = 0
+// mjc_ccd (:2215-2343) with max_contacts = 1 and the distance cutoff `cutoff` (0 for
+// mjc_Convex's contacts, the bound for mj_geomDistanceCCD)
 template <int S>
 MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B, int kmax,
-                     double tol) {
+                     double tol, double cutoff) {
   copy3(st.x1, A.pos);
   copy3(st.x2, B.pos);
   st.iters = 0;
   st.tol = tol;
   st.kmax = kmax;
-  st.cutoff = 0;
+  st.cutoff = cutoff;
   st.unsupported = 0;
   const bool shrinkA = A.gtype == mjhipGEOM_SPHERE || A.gtype == mjhipGEOM_CAPSULE;
   const bool shrinkB = B.gtype == mjhipGEOM_SPHERE || B.gtype == mjhipGEOM_CAPSULE;
@@ -2659,7 +2685,7 @@ MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B,
     }
     st.cutoff += full1 + full2;
     ccdGjk(st, M, A, B);
-    st.cutoff = 0;
+    st.cutoff = cutoff;
     A.margin = m1;
     B.margin = m2;
     A.kind = A.gtype;
@@ -2713,7 +2739,7 @@ MJH_HD int colConvex(RawContact& c, const mjhipModel& m, const Lane<S>& d, int g
   ccdShape(A, m, d, g1, margin);
   ccdShape(B, m, d, g2, margin);
   CcdState st;
-  const double dist = ccdRun(st, M, A, B, N, m.opt.ccd_tolerance);
+  const double dist = ccdRun(st, M, A, B, N, m.opt.ccd_tolerance, 0.0);
   if (st.unsupported) {
     *status |= MJHIP_INST_UNSUPPORTED;
     return 0;
@@ -3008,6 +3034,79 @@ MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, in
   } else {
     colPlaneCylinder(margin, pos1, mat1, pos2, mat2, size2, store);
   }
+}
+
+// engine_support.c:1407-1450 mj_geomDistance (the oracle's or_geomDistance): the smallest
+// signed distance between two geoms up to distmax and the segment between the nearest
+// points (zeros when none is found); mjc_Convex and box-box pairs through the native solver
+// with the bound as its cutoff (mj_geomDistanceCCD :1379-1402), the rest through their
+// collision functions with the bound as the margin. Functions outside the subset flag.
+template <int S>
+MJH_HD double geomDistance(const mjhipModel& m, const Lane<S>& d, int geom1, int geom2,
+                           double distmax, double fromto[6], int* status) {
+  double dist = distmax;
+  for (int k = 0; k < 6; k++) fromto[k] = 0;
+  const bool flip = m.geom_type[geom1] > m.geom_type[geom2];
+  const int g1 = flip ? geom2 : geom1, g2 = flip ? geom1 : geom2;
+  const int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
+  const bool nccd = !(m.opt.disableflags & mjhipDSBL_NATIVECCD);
+  const bool ccd = nccd && (mjhip_isConvexPair(t1, t2) ||
+                            (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX));
+  const int kmax = mjhip_pairMaxContacts(&m, t1, t2);
+  if (kmax == 0) return dist;
+  if ((kmax < 0 && !ccd) || (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX && !ccd)) {
+    *status |= MJHIP_INST_UNSUPPORTED;   // refused at context creation (mjhip.hip)
+    return dist;
+  }
+  if (ccd) {
+    const int N = m.opt.ccd_iterations;
+    CcdMem<S> M{d.ccd, d.ccdi, 5 + N, mjh_ccdFaceCap(&m)};
+    CcdShape A, B;
+    ccdShape(A, m, d, g1, 0.0);
+    ccdShape(B, m, d, g2, 0.0);
+    CcdState st;
+    const double r = ccdRun(st, M, A, B, N, m.opt.ccd_tolerance, distmax);
+    if (st.unsupported) *status |= MJHIP_INST_UNSUPPORTED;
+    if (st.nx > 0) {
+      for (int k = 0; k < 3; k++) fromto[k] = st.x1[k];
+      for (int k = 0; k < 3; k++) fromto[3+k] = st.x2[k];
+    }
+    return r;
+  }
+  double pos1[3], mat1[9], pos2[3], mat2[9];
+  for (int k = 0; k < 3; k++) { pos1[k] = d.geom_xpos[3*g1+k]; pos2[k] = d.geom_xpos[3*g2+k]; }
+  for (int k = 0; k < 9; k++) { mat1[k] = d.geom_xmat[9*g1+k]; mat2[k] = d.geom_xmat[9*g2+k]; }
+  const double *size1 = m.geom_size + 3*g1, *size2 = m.geom_size + 3*g2;
+  RawContact best;
+  bool found = false;
+  auto take = [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
+    if (rk.dist < dist) {
+      dist = rk.dist;
+      best = rk;
+      found = true;
+    }
+    return true;
+  };
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_BOX) {
+    colPlaneBox(distmax, (const double*)pos1, (const double*)mat1, (const double*)pos2,
+                (const double*)mat2, size2, take);
+  } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CYLINDER) {
+    colPlaneCylinder(distmax, (const double*)pos1, (const double*)mat1, (const double*)pos2,
+                     (const double*)mat2, size2, take);
+  } else {
+    RawContact raw[2];
+    const int num = narrowPrimitive(t1, t2, distmax, (const double*)pos1, (const double*)mat1,
+                                    size1, (const double*)pos2, (const double*)mat2, size2, raw);
+    for (int i = 0; i < num && i < 2; i++) take(raw[i]);
+  }
+  if (found) {
+    const double sign = flip ? -1 : 1;
+    for (int k = 0; k < 3; k++) {
+      fromto[k] = best.pos[k] + best.frame[k]*(-0.5*sign*dist);
+      fromto[3+k] = best.pos[k] + best.frame[k]*(0.5*sign*dist);
+    }
+  }
+  return dist;
 }
 
 // contactcompare (engine_collision_driver.c:223-257) on two contacts' geom ids
@@ -6024,6 +6123,7 @@ template <int S>
 MJH_HD void applyCutoff(const mjhipModel& m, const Lane<S>& d, int stage) {
   for (int i = 0; i < m.nsensor; i++) {
     if (m.sensor_needstage[i] == stage && m.sensor_cutoff[i] > 0) {
+      if (m.sensor_type[i] == mjhSENS_GEOMFROMTO) continue;   // :44-47
       const int adr = m.sensor_adr[i], dim = m.sensor_dim[i];
       const double cutoff = m.sensor_cutoff[i];
       for (int j = 0; j < dim; j++) {
@@ -6093,7 +6193,7 @@ template <int S>
 MJH_HD double ray(const mjhipModel& m, const Lane<S>& d, const double pnt[3],
                   const double vec[3], int bodyexclude);
 
-// engine_sensor.c:209-513 mj_sensorPos (no geom distance/user, rejected at load)
+// engine_sensor.c:209-513 mj_sensorPos (no user/plugin sensors, rejected at load)
 template <int S>
 MJH_HD void sensorPos(const mjhipModel& m, const Lane<S>& d) {
   if (m.opt.disableflags & mjhipDSBL_SENSOR) return;
@@ -6110,6 +6210,40 @@ MJH_HD void sensorPos(const mjhipModel& m, const Lane<S>& d) {
     case mjhSENS_MAGNETOMETER:
       mulMatTVec(out, d.site_xmat + 9*objid, m.opt.magnetic, 3, 3);
       break;
+    case mjhSENS_GEOMDIST:
+    case mjhSENS_GEOMNORMAL:
+    case mjhSENS_GEOMFROMTO: {
+      // engine_sensor.c:378-460: the smallest distance over the two bodies'/geoms' geom
+      // pairs, cutoff as the bound (the reference shares one evaluation among consecutive
+      // sensors of the same pair and cutoff; recomputing gives the same values)
+      const double margin = m.sensor_cutoff[i];
+      double dist = margin, fromto[6] = {0, 0, 0, 0, 0, 0};
+      const int n1 = objtype == 1 ? m.body_geomnum[objid] : 1;
+      const int id1 = objtype == 1 ? m.body_geomadr[objid] : objid;
+      const int n2 = reftype == 1 ? m.body_geomnum[refid] : 1;
+      const int id2 = reftype == 1 ? m.body_geomadr[refid] : refid;
+      int unused = 0;
+      for (int a = id1; a < id1 + n1; a++) {
+        for (int b = id2; b < id2 + n2; b++) {
+          double ft[6];
+          const double dn = geomDistance(m, d, a, b, margin, ft, &unused);
+          if (dn < dist) {
+            dist = dn;
+            for (int k = 0; k < 6; k++) fromto[k] = ft[k];
+          }
+        }
+      }
+      if (type == mjhSENS_GEOMDIST) {
+        out[0] = dist;
+      } else if (type == mjhSENS_GEOMNORMAL) {
+        double nrm[3] = {fromto[3]-fromto[0], fromto[4]-fromto[1], fromto[5]-fromto[2]};
+        if (nrm[0] || nrm[1] || nrm[2]) normalize3(nrm);
+        for (int k = 0; k < 3; k++) out[k] = nrm[k];
+      } else {
+        for (int k = 0; k < 6; k++) out[k] = fromto[k];
+      }
+      break;
+    }
     case mjhSENS_CAMPROJECTION: {
       double px[2];
       camProject(px, d.site_xpos + 3*objid, d.cam_xpos + 3*refid, d.cam_xmat + 9*refid,

@@ -1014,8 +1014,28 @@ static const char* unsupported(const mjhipModel* m) {
   }
   for (int i = 0; i < m->nsensor; i++) {
     const int t = m->sensor_type[i];
-    if ((t >= mjhSENS_GEOMDIST && t <= mjhSENS_GEOMFROMTO) || t > mjhSENS_CLOCK) {
-      return "geom-distance/plugin/user sensors";
+    if (t > mjhSENS_CLOCK) return "plugin/user sensors";
+    if (t >= mjhSENS_GEOMDIST && t <= mjhSENS_GEOMFROMTO) {
+      // mj_geomDistance's functions outside the subset: meshes, height fields, SDFs, and
+      // libccd's MPR (convex and box-box pairs with the native solver disabled)
+      const int o = m->sensor_objid[i], r = m->sensor_refid[i];
+      const int n1 = m->sensor_objtype[i] == 1 ? m->body_geomnum[o] : 1;
+      const int a1 = m->sensor_objtype[i] == 1 ? m->body_geomadr[o] : o;
+      const int n2 = m->sensor_reftype[i] == 1 ? m->body_geomnum[r] : 1;
+      const int a2 = m->sensor_reftype[i] == 1 ? m->body_geomadr[r] : r;
+      const bool nccd = !(m->opt.disableflags & mjhipDSBL_NATIVECCD);
+      for (int g1 = a1; g1 < a1 + n1; g1++) {
+        for (int g2 = a2; g2 < a2 + n2; g2++) {
+          int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+          if (t1 > t2) std::swap(t1, t2);
+          const bool ccd = mjhip_isConvexPair(t1, t2) ||
+                           (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX);
+          if ((ccd && !nccd) || (!ccd && mjhip_pairMaxContacts(m, t1, t2) < 0)) {
+            return "a geom-distance sensor on a mesh, height field or SDF geom, or on a "
+                   "convex pair with the native CCD solver disabled";
+          }
+        }
+      }
     }
     if (t == mjhSENS_RANGEFINDER) {   // mj_ray's mesh, height-field and SDF paths are not built
       const int body = m->site_bodyid[m->sensor_objid[i]];

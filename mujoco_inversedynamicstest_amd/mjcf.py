@@ -50,6 +50,9 @@ OBJ = {"body": 1, "xbody": 2, "joint": 3, "dof": 4, "geom": 5, "site": 6, "camer
 SENSORS = {
     "touch": (0, "site", 6, 1, 1, 3), "rangefinder": (7, "site", 6, 1, 1, 1),
     "camprojection": (8, "site", 6, 2, 0, 1),
+    # geom distance (geom1|body1, geom2|body2; xml_native_reader.cc:4105-4116)
+    "distance": (37, "geom1", None, 1, 1, 1), "normal": (38, "geom1", None, 3, 2, 1),
+    "fromto": (39, "geom1", None, 6, 0, 1),
     "accelerometer": (1, "site", 6, 3, 0, 3), "velocimeter": (2, "site", 6, 3, 0, 2),
     "gyro": (3, "site", 6, 3, 0, 2), "force": (4, "site", 6, 3, 0, 3),
     "torque": (5, "site", 6, 3, 0, 3), "magnetometer": (6, "site", 6, 3, 0, 1),
@@ -73,8 +76,7 @@ SENSORS = {
     "e_potential": (40, None, 0, 1, 0, 1), "e_kinetic": (41, None, 0, 1, 0, 1),
     "clock": (42, None, 0, 1, 0, 1),
 }
-SENSORS_NEXT = ("distance", "normal", "fromto",
-                "user", "plugin")
+SENSORS_NEXT = ("user", "plugin")
 GEOM = {"plane": 0, "hfield": 1, "sphere": 2, "capsule": 3, "ellipsoid": 4,
         "cylinder": 5, "box": 6, "mesh": 7, "sdf": 8}
 CAMLIGHT = {"fixed": 0, "track": 1, "trackcom": 2, "targetbody": 3, "targetbodycom": 4}
@@ -1665,7 +1667,21 @@ class MJCFCompiler:
       if cut < 0 or float(a.get("noise", 0.0)) < 0:
         raise MJCFError("negative noise/cutoff in sensor")
       rt, rid = 0, -1
-      if attr is None and ot is None:              # frame sensors
+      if tp in (37, 38, 39):                       # geom distance: (geom1|body1, geom2|body2)
+        sides = []
+        for k in ("1", "2"):
+          hb, hg = f"body{k}" in a, f"geom{k}" in a
+          if hb == hg:
+            raise MJCFError(f"exactly one of (geom{k}, body{k}) must be specified")
+          t_ = 1 if hb else 5
+          sides.append((t_, find(t_, a[f"body{k}" if hb else f"geom{k}"], "sensorized object")))
+        (ot, oid), (rt, rid) = sides
+        if (ot, oid) == (rt, rid):
+          raise MJCFError("1st body/geom must be different from 2nd body/geom")
+        for t_, i_ in sides:
+          if t_ == 5 and g_int["type"][i_] == GEOM["hfield"]:
+            raise MJCFError("height fields are not supported in geom distance sensors")
+      elif attr is None and ot is None:              # frame sensors
         ot = OBJ.get(a.get("objtype", ""), None)
         if ot not in (1, 2, 5, 6, 7):
           raise MJCFError("sensor must be attached to (x)body, geom, site or camera")

@@ -3399,15 +3399,16 @@ static int ccd_epa(orCCD* st, orPoly* P, const orShape* A, const orShape* B) {
   return f;
 }
 
-/* mjc_ccd (:2215-2343) with max_contacts = 1 and dist_cutoff = 0; the geoms' margins are in
+/* mjc_ccd (:2215-2343) with max_contacts = 1 and the distance cutoff `cutoff` (0 for contacts,
+ * mjc_Convex; the distance bound for mj_geomDistanceCCD); the geoms' margins are in
  * A->margin / B->margin */
-static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol) {
+static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol, mjtNum cutoff) {
   mju_copy3(st->x1, A->pos);
   mju_copy3(st->x2, B->pos);
   st->iters = 0;
   st->tol = tol;
   st->kmax = kmax;
-  st->cutoff = 0;
+  st->cutoff = cutoff;
   const int shrinkA = A->gtype == mjhipGEOM_SPHERE || A->gtype == mjhipGEOM_CAPSULE;
   const int shrinkB = B->gtype == mjhipGEOM_SPHERE || B->gtype == mjhipGEOM_CAPSULE;
   if (shrinkA || shrinkB) {
@@ -3424,7 +3425,7 @@ static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol) {
     }
     st->cutoff += full1 + full2;
     ccd_gjk(st, A, B);
-    st->cutoff = 0;
+    st->cutoff = cutoff;
     A->margin = m1;
     B->margin = m2;
     A->kind = A->gtype;
@@ -3491,7 +3492,7 @@ static int col_convex(orRaw* c, const mjhipModel* m, const mjhipData* d, int g1,
   or_shape(&A, m, d, g1, margin);
   or_shape(&B, m, d, g2, margin);
   orCCD st;
-  mjtNum dist = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance);
+  mjtNum dist = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, 0);
   if (!(dist < 0) || st.nx < 1) return 0;
   c->dist = margin + dist;
   mju_sub3(c->frame, st.x1, st.x2);
@@ -3866,27 +3867,14 @@ int or_efcCapacity(const mjhipModel* m) {
   return n + nrow;
 }
 
-/* mj_collideGeoms (dynamic filters, narrowphase, mj_setContact) for geoms of two bodies */
-static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, int g1, int g2) {
-  if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
-  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
-  const int kmax = or_collisionFunc(m, t1, t2);
-  if (kmax == 0) return;
-  if (or_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1], m->geom_contype[g2],
-                       m->geom_conaffinity[g2])) {
-    return;
-  }
-  mjtNum margin = mjENABLED(mjhipENBL_OVERRIDE) ? m->opt.o_margin
-                                                : mjMAX(m->geom_margin[g1], m->geom_margin[g2]);
-  if (or_filterSphere(m, d, g1, g2, margin)) return;
-  if (kmax < 0) {              /* a collision function outside the subset would run: flag */
-    ((mjhipData*)d)->status |= MJHIP_INST_UNSUPPORTED;
-    return;
-  }
+/* the narrowphase of type-ordered geoms g1, g2 (mjCOLLISIONFUNC's primitive and convex
+ * functions): raw contacts closer than margin into raw[] (<= 24), their count */
+static int or_narrow(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum margin,
+                     orRaw* raw) {
+  const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   const mjtNum *pos1 = d->geom_xpos + 3*g1, *mat1 = d->geom_xmat + 9*g1;
   const mjtNum *pos2 = d->geom_xpos + 3*g2, *mat2 = d->geom_xmat + 9*g2;
   const mjtNum *size1 = m->geom_size + 3*g1, *size2 = m->geom_size + 3*g2;
-  orRaw raw[24];
   int num = 0;
   if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CYLINDER) {
     num = col_planeCylinder(raw, margin, pos1, mat1, pos2, mat2, size2);
@@ -3916,6 +3904,28 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
   } else if (or_isConvexPair(t1, t2)) {
     num = col_convex(raw, m, d, g1, g2, margin);
   }
+  return num;
+}
+
+/* mj_collideGeoms (dynamic filters, narrowphase, mj_setContact) for geoms of two bodies */
+static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, int g1, int g2) {
+  if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
+  int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  const int kmax = or_collisionFunc(m, t1, t2);
+  if (kmax == 0) return;
+  if (or_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1], m->geom_contype[g2],
+                       m->geom_conaffinity[g2])) {
+    return;
+  }
+  mjtNum margin = mjENABLED(mjhipENBL_OVERRIDE) ? m->opt.o_margin
+                                                : mjMAX(m->geom_margin[g1], m->geom_margin[g2]);
+  if (or_filterSphere(m, d, g1, g2, margin)) return;
+  if (kmax < 0) {              /* a collision function outside the subset would run: flag */
+    ((mjhipData*)d)->status |= MJHIP_INST_UNSUPPORTED;
+    return;
+  }
+  orRaw raw[24];
+  const int num = or_narrow(m, d, g1, g2, margin, raw);
   if (!num) return;
   int condim;
   mjtNum gap, solref[2], solimp[5], friction[5], solreffriction[2] = {0, 0};
@@ -3944,6 +3954,54 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
     e->con_mu[i] = 0;
     e->ncon = i + 1;
   }
+}
+
+/* engine_support.c:1407-1450 mj_geomDistance (with mj_geomDistanceCCD :1379-1402): the
+ * smallest signed distance between two geoms up to distmax, and the segment between the
+ * nearest points in fromto (zeros when none is found). mjc_Convex and box-box pairs go
+ * through the native solver with the distance bound as its cutoff; the other functions
+ * return their contacts closer than distmax. Functions outside the subset flag the state. */
+static mjtNum or_geomDistance(const mjhipModel* m, mjhipData* d, int geom1, int geom2,
+                              mjtNum distmax, mjtNum fromto[6]) {
+  mjtNum dist = distmax;
+  mju_zero(fromto, 6);
+  const int flip = m->geom_type[geom1] > m->geom_type[geom2];
+  const int g1 = flip ? geom2 : geom1, g2 = flip ? geom1 : geom2;
+  const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  const int ccd = or_isConvexPair(t1, t2) || (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX);
+  const int kmax = or_collisionFunc(m, t1, t2);
+  if (kmax == 0) return dist;                 /* no collision function */
+  if (kmax < 0 && !(ccd && !mjDISABLED(mjhipDSBL_NATIVECCD))) {
+    d->status |= MJHIP_INST_UNSUPPORTED;      /* mesh, height field, SDF or libccd's MPR */
+    return dist;
+  }
+  if (ccd && !mjDISABLED(mjhipDSBL_NATIVECCD)) {
+    orShape A, B;
+    or_shape(&A, m, d, g1, 0);
+    or_shape(&B, m, d, g2, 0);
+    orCCD st;
+    const mjtNum r = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, distmax);
+    if (st.nx > 0) {
+      mju_copy3(fromto, st.x1);
+      mju_copy3(fromto + 3, st.x2);
+    }
+    return r;
+  }
+  orRaw raw[24];
+  const int num = or_narrow(m, d, g1, g2, distmax, raw);
+  int best = -1;
+  for (int i = 0; i < num; i++) {
+    if (raw[i].dist < dist) {
+      dist = raw[i].dist;
+      best = i;
+    }
+  }
+  if (best >= 0) {
+    const mjtNum sign = flip ? -1 : 1;
+    mju_addScl3(fromto, raw[best].pos, raw[best].frame, -0.5*sign*dist);
+    mju_addScl3(fromto + 3, raw[best].pos, raw[best].frame, 0.5*sign*dist);
+  }
+  return dist;
 }
 
 /* contactcompare (engine_collision_driver.c:223-257) on the geom ids of two contacts */
@@ -5419,6 +5477,7 @@ static void or_rnePostConstraint(const mjhipModel* m, mjhipData* d, const orEfc*
 static void or_applyCutoff(const mjhipModel* m, mjhipData* d, int stage) {
   for (int i = 0; i < m->nsensor; i++) {
     if (m->sensor_needstage[i] == stage && m->sensor_cutoff[i] > 0) {
+      if (m->sensor_type[i] == SENS_GEOMFROMTO) continue;   /* :44-47 */
       int adr = m->sensor_adr[i], dim = m->sensor_dim[i];
       mjtNum cutoff = m->sensor_cutoff[i];
       for (int j = 0; j < dim; j++) {
@@ -5488,7 +5547,7 @@ static mjtNum or_ray(const mjhipModel* m, const mjhipData* d, const mjtNum* pnt,
 static void or_energyPos(const mjhipModel* m, mjhipData* d);
 static void or_energyVel(const mjhipModel* m, mjhipData* d);
 
-/* engine_sensor.c:209-513 mj_sensorPos (no geom distance/user) */
+/* engine_sensor.c:209-513 mj_sensorPos (no user/plugin sensors) */
 static void or_sensorPos(const mjhipModel* m, mjhipData* d, const orEfc* e) {
   if (mjDISABLED(mjhipDSBL_SENSOR)) return;
   for (int i = 0; i < m->nsensor; i++) {
@@ -5575,6 +5634,39 @@ static void or_sensorPos(const mjhipModel* m, mjhipData* d, const orEfc* e) {
     case SENS_SUBTREECOM:
       mju_copy3(out, d->subtree_com + 3*objid);
       break;
+    case SENS_GEOMDIST:
+    case SENS_GEOMNORMAL:
+    case SENS_GEOMFROMTO: {
+      /* :378-460: the smallest distance over the geom pairs of the two bodies/geoms, cutoff
+       * as the bound (the reference shares one evaluation among consecutive sensors of the
+       * same pair and cutoff; recomputing gives the same values) */
+      const mjtNum margin = m->sensor_cutoff[i];
+      mjtNum dist = margin, fromto[6] = {0, 0, 0, 0, 0, 0};
+      const int n1 = objtype == OBJ_BODY ? m->body_geomnum[objid] : 1;
+      const int id1 = objtype == OBJ_BODY ? m->body_geomadr[objid] : objid;
+      const int n2 = reftype == OBJ_BODY ? m->body_geomnum[refid] : 1;
+      const int id2 = reftype == OBJ_BODY ? m->body_geomadr[refid] : refid;
+      for (int a = id1; a < id1 + n1; a++) {
+        for (int b = id2; b < id2 + n2; b++) {
+          mjtNum ft[6];
+          const mjtNum dn = or_geomDistance(m, d, a, b, margin, ft);
+          if (dn < dist) {
+            dist = dn;
+            mju_copy(fromto, ft, 6);
+          }
+        }
+      }
+      if (type == SENS_GEOMDIST) {
+        out[0] = dist;
+      } else if (type == SENS_GEOMNORMAL) {
+        mjtNum nrm[3] = {fromto[3]-fromto[0], fromto[4]-fromto[1], fromto[5]-fromto[2]};
+        if (nrm[0] || nrm[1] || nrm[2]) mju_normalize3(nrm);
+        mju_copy3(out, nrm);
+      } else {
+        mju_copy(out, fromto, 6);
+      }
+      break;
+    }
     case SENS_E_POTENTIAL:
       or_energyPos(m, d);
       out[0] = d->energy[0];

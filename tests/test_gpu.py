@@ -1089,6 +1089,46 @@ def test_camprojection_parity():
   assert_close(sd, np.array(rsd), "sensordata")
 
 
+def test_geom_distance_parity():
+  """Geom-distance sensors (distance, normal, fromto; primitive pairs, the native solver's
+  pairs and a body-level sensor) on the device vs the oracle. The native solver's pairs are
+  iterative (test_convex_gpu.py explains their conditioning): distances are held to
+  10 ccd_tolerance, everything else to the north-star bar."""
+  import os
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+  from test_geomdist_cpu import SCENE
+  from mujoco_inversedynamicstest_amd import mjcf
+  m = mjcf.load_xml_string(SCENE)
+  B = 1024
+  rng = np.random.default_rng(14)
+  q = np.tile(m.qpos0, (B, 1))
+  q[:, :3] = rng.uniform(-.6, .6, (B, 3)) + [0, 0, 1]
+  qq = rng.normal(size=(B, 4))
+  q[:, 3:7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
+  q[:, 7] = rng.uniform(-3, 3, B)
+  v, a = rng.normal(size=(B, m.nv)), rng.normal(size=(B, m.nv))
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    f, st = e.inverse(q, v, a, status=True)
+    sd = e.field("sensordata", 0, B)
+  finally:
+    e.close()
+  assert (st == 0).all()
+  o = Oracle(m)
+  rsd = []
+  for i in range(B):
+    o.inverse(q[i], v[i], a[i])
+    rsd.append(o.d.sensordata.copy())
+  rsd = np.array(rsd)
+  err = np.abs(sd - rsd).max()
+  print(f"geom distance sensors: max abs difference {err:.2e}")
+  assert err <= 10 * m.opt["ccd_tolerance"]
+  # the primitive pairs (ball-floor: sensor 0; blk-floor: the last) to the north-star bar
+  for k in (0, m.nsensordata - 1):
+    assert_close(sd[:, k:k + 1], rsd[:, k:k + 1], f"sensordata[{k}]")
+
+
 def test_elliptic_cone_parity():
   """Elliptic friction cones (classic constraint passes) on the device: humanoid config-4
   states with cone="elliptic"."""

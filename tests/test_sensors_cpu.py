@@ -387,12 +387,12 @@ def test_sensor_skip_stages_keep_values():
 
 
 def test_unsupported_sensors_rejected():
-  """The geom-distance family is outside the subset: the loader says so."""
-  for tag in ("distance", "normal", "fromto"):
+  """User and plugin sensors are outside the subset: the loader says so."""
+  for tag in ("user", "plugin"):
     with pytest.raises(mjcf.MJCFError, match="not in the supported subset"):
-      mjcf.load_xml_string(f"""<mujoco><worldbody><geom name="a" size=".1"/>
-        <geom name="b" size=".1" pos="1 0 0"/></worldbody>
-        <sensor><{tag} geom1="a" geom2="b"/></sensor></mujoco>""")
+      mjcf.load_xml_string(f"""<mujoco><worldbody><site name="s"/></worldbody>
+        <sensor><{tag} objtype="site" objname="s" dim="1" needstage="pos"/></sensor>
+        </mujoco>""")
 
 
 def test_bundled_linear_model_has_reference_sensors(linear):
