@@ -132,8 +132,6 @@ def fast_path_supported(m) -> str | None:
     return "INVDISCRETE"
   if m.sizes.get("nwrap", 0) and np.any(np.asarray(m.wrap_type) != 1):
     return "spatial tendons (generic kernel)"
-  if m.opt["density"] > 0 or m.opt["viscosity"] > 0:
-    return "fluid"
   for a in range(m.nu):
     if m.actuator_trntype[a] not in (0, 1, 2, 3, 4, 5):
       return "unknown transmission"
@@ -150,6 +148,9 @@ TRN_AFTER = (2, 4, 5)
 def constraint_mode(m) -> str:
   """Which instances the constraint kernel serves: 'all', 'list' or 'none' (module doc)."""
   dsbl = int(m.opt["disableflags"])
+  if (m.opt["density"] > 0 or m.opt["viscosity"] > 0) and not dsbl & (1 << 5):
+    return "all"          # fluid: the post pass (csrc/post_pass.h) updates qfrc_passive, and
+                          # the constraint kernel assembles qfrc_inverse for every instance
   if dsbl & 1:                                             # mjDSBL_CONSTRAINT
     return "none"
   contacts = not (dsbl & (1 << 4)) and m.nbody >= 2 and \

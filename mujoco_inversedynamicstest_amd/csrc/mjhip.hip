@@ -25,6 +25,7 @@
 
 #include "engine_device.h"
 #include "fast_kernels.h"
+#include "post_pass.h"
 
 using mjh::Lane;
 using mjh::SP;
@@ -174,7 +175,7 @@ __host__ __device__ static inline int coopRows(int efc_cap) {
 }
 __host__ __device__ static inline int coopPerInstance(const mjhipModel& m, int npair,
                                                       int con_cap, int efc_cap) {
-  return 8*m.nv + m.nq + 12*m.ngeom + (npair + 1) / 2 + 2*coopContacts(con_cap) +
+  return 8*m.nv + m.nq + 12*m.ngeom + (npair + 1) / 2 + 3*coopContacts(con_cap) +
          coopRows(efc_cap);
 }
 static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap, bool boxpair, int npair,
@@ -190,6 +191,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
                                                         const int* __restrict__ count,
                                                         const CoopPair* __restrict__ pairs,
                                                         const mjh::ContactParam* __restrict__ cparams,
+                                                        const unsigned long long* __restrict__ masks,
                                                         int npair,
                                                         double* __restrict__ qfrc_out,
                                                         int* __restrict__ status) {
@@ -197,8 +199,15 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   const long n = LIST ? (long)*count : (long)B;
   if ((long)blockIdx.x*IPB >= n) return;    // whole block idle (uniform): before the barriers
   __shared__ unsigned long long chain[64], dchain[64];
-  if ((int)threadIdx.x < m.nbody) chain[threadIdx.x] = mjh::chainMask(m, threadIdx.x);
-  // the pair program and the geom sizes, once per block
+  __shared__ long s_inst[64 / G];            // the instance of each group (pooled contact rows)
+  __shared__ int s_ntask[64 / G];            // its staged contacts with rows
+  // the chain masks (host-built, coop_masks: bodies, then dofs on each body's chain for
+  // contactRowsSplit's bit test; the kernel runs for nbody, nv <= 64), the pair program and
+  // the geom sizes, once per block, all with independent loads
+  if ((int)threadIdx.x < m.nbody) {
+    chain[threadIdx.x] = masks[threadIdx.x];
+    dchain[threadIdx.x] = masks[m.nbody + threadIdx.x];
+  }
   CoopPair* prog = reinterpret_cast<CoopPair*>(g_gstage);
   double* gsize = g_gstage + kCoopPairDoubles*npair;
   if (CONTACT) {
@@ -206,15 +215,6 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       g_gstage[e] = reinterpret_cast<const double*>(pairs)[e];
     }
     for (int e = threadIdx.x; e < 3*m.ngeom; e += 64) gsize[e] = m.geom_size[e];
-  }
-  __syncthreads();
-  // the dofs on each body's chain (contactRowsSplit's bit test; the kernel runs for nv <= 64)
-  if ((int)threadIdx.x < m.nbody) {
-    unsigned long long dm = 0;
-    for (int j = 0; j < m.nv; j++) {
-      if ((chain[threadIdx.x] >> m.dof_bodyid[j]) & 1) dm |= 1ull << j;
-    }
-    dchain[threadIdx.x] = dm;
   }
   __syncthreads();
   const int sub = threadIdx.x % G, slot = threadIdx.x / G;
@@ -243,7 +243,8 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   int* surv = reinterpret_cast<int*>(gm + 9*ngeom);
   int* cbody = reinterpret_cast<int*>(gm + 9*ngeom + (npair + 1) / 2);
   const int ncb = coopContacts(d.con_cap);
-  double* fst = gm + 9*ngeom + (npair + 1) / 2 + 2*ncb;
+  int* task = cbody + 4*ncb;                // per staged contact: its first row, its condim
+  double* fst = gm + 9*ngeom + (npair + 1) / 2 + 3*ncb;
   // box-box contact positions of this lane's pair (only models with box pairs get the room)
   double* bbuf = lbase + (long)IPB*per + (long)threadIdx.x*kBoxBoxBuf;
   const bool collide = CONTACT && mjhip_contactsEnabled(&m) && npair > 0;
@@ -498,36 +499,83 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
     // per round; a prefix sum over the contacts' row counts (held by each contact's first
     // lane) gives each its first row; wide contacts (condim 4, 6) run on their first lane
     if (CONTACT && !(dsbl & mjhipDSBL_CONTACT) && nv) {
-      constexpr int Q = kCoopContactLanes, CPR = G / Q;
-      const int cq = sub % Q;
+      // the contacts' first rows: a group prefix sum over their row counts, G per round; the
+      // first kCoopContacts contacts become tasks for the whole wave (below), the rest (rare)
+      // are formed here by the lane that placed them
       int nef = rc.nefc;
-      for (int c0 = 0; c0 < ncon; c0 += CPR) {
-        const int c = c0 + sub / Q;
+      for (int c0 = 0; c0 < ncon; c0 += G) {
+        const int c = c0 + sub;
         int rows = 0, dim = 0;
         if (c < ncon && !d.con_exclude[c]) {
           dim = d.con_dim[c];
           rows = dim == 1 ? 1 : 2*(dim - 1);
         }
-        const int mine = cq == 0 ? rows : 0;
         int total;
-        const int off = __shfl(nef + groupScan<G>(mine, sub, &total) - mine,
-                               (int)(threadIdx.x & ~(unsigned)(Q - 1)));
-        if (rows) {
-          if (off + rows > d.efc_cap) {     // mjWARN_CNSTRFULL analogue (capacity is exact)
-            st |= MJHIP_INST_CNSTRFULL;
-          } else {
-            if (cq == 0) d.con_efc_address[c] = off;
+        const int off = nef + groupScan<G>(rows, sub, &total) - rows;
+        bool fits = true;
+        if (rows && off + rows > d.efc_cap) {   // mjWARN_CNSTRFULL analogue (capacity is exact)
+          st |= MJHIP_INST_CNSTRFULL;
+          fits = false;
+        }
+        if (c < ncb && c < ncon) {
+          task[2*c] = off;
+          task[2*c+1] = fits ? dim : 0;     // 0: no rows
+        }
+        if (rows && fits) {
+          d.con_efc_address[c] = off;
+          if (c >= ncb) {
             switch (dim) {
-              case 1: mjh::contactRowsSplit<64, 1, Q>(m, d, c, off, cq); break;
-              case 3: mjh::contactRowsSplit<64, 3, Q>(m, d, c, off, cq); break;
-              case 4: if (cq == 0) mjh::contactRowsFused<64, 4>(m, d, c, off); break;
-              default: if (cq == 0) mjh::contactRowsFused<64, 6>(m, d, c, off); break;
+              case 1: mjh::contactRowsFused<64, 1>(m, d, c, off); break;
+              case 3: mjh::contactRowsFused<64, 3>(m, d, c, off); break;
+              case 4: mjh::contactRowsFused<64, 4>(m, d, c, off); break;
+              default: mjh::contactRowsFused<64, 6>(m, d, c, off); break;
             }
           }
         }
         nef += total;
       }
       rc.nefc = nef < d.efc_cap ? nef : d.efc_cap;
+    }
+  }
+  if (sub == 0) {
+    s_inst[slot] = inst;
+    s_ntask[slot] = (CONTACT && active && !(dsbl & (mjhipDSBL_CONSTRAINT | mjhipDSBL_CONTACT)) &&
+                     nv) ? (ncon < ncb ? ncon : ncb) : 0;
+  }
+  __syncthreads();                          // the tasks and the staged data visible to all
+
+  // ---- contact rows, pooled over the wave: kCoopContactLanes lanes per contact
+  // (contactRowsSplit), 64 / kCoopContactLanes contacts per round whichever instance they
+  // belong to, so an instance with many contacts does not hold its wave for many rounds
+  if (CONTACT) {
+    constexpr int Q = kCoopContactLanes;
+    int ntot = 0;
+    for (int k = 0; k < IPB; k++) ntot += s_ntask[k];
+    const int cq = threadIdx.x % Q;
+    for (int t0 = 0; t0 < ntot; t0 += 64 / Q) {
+      int t = t0 + threadIdx.x / Q, sl = 0;
+      while (sl < IPB && t >= s_ntask[sl]) t -= s_ntask[sl++];
+      if (sl >= IPB) continue;              // past the wave's tasks (uniform per Q lanes)
+      const long ti = s_inst[sl];
+      Lane<64> dt = lane_view(mr, (int)(ti >> 6), (int)(ti & 63));
+      double* tb = lbase + (long)sl*per;
+      int* tcb = reinterpret_cast<int*>(tb + 8*nv + nq + 12*ngeom + (npair + 1) / 2);
+      int* ttask = tcb + 4*ncb;
+      dt.chain = chain;
+      dt.dchain = dchain;
+      dt.cdq = tb;
+      dt.cbody = tcb;
+      dt.ncbody = ncb;
+      dt.fst = tb + 8*nv + nq + 12*ngeom + (npair + 1) / 2 + 3*ncb;
+      dt.nfst = coopRows(dt.efc_cap);
+      const int off = ttask[2*t], dim = ttask[2*t+1];
+      switch (dim) {
+        case 0: break;
+        case 1: mjh::contactRowsSplit<64, 1, Q>(m, dt, t, off, cq); break;
+        case 3: mjh::contactRowsSplit<64, 3, Q>(m, dt, t, off, cq); break;
+        case 4: if (cq == 0) mjh::contactRowsFused<64, 4>(m, dt, t, off); break;
+        default: if (cq == 0) mjh::contactRowsFused<64, 6>(m, dt, t, off); break;
+      }
     }
   }
   if (active && sub == 0) {
@@ -591,6 +639,14 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   MJH_PHASE(17);
   __syncthreads();                          // the group's LDS is reused by the next round
   }
+}
+
+// fluid forces after the generated kernels (csrc/post_pass.h): one lane per instance
+__global__ __launch_bounds__(64) void k_fluid_after(mjhipModel m, Mirror mr, int B) {
+  const long inst = (long)blockIdx.x*64 + threadIdx.x;
+  if (inst >= B) return;
+  Lane<64> d = lane_view(mr, blockIdx.x, threadIdx.x);
+  mjh::fluidAfter(m, d);
 }
 
 // Status checks of the straight-line path: mj_checkPos/Vel/Acc (engine_forward.c:53-102)
@@ -860,6 +916,7 @@ struct mjhipContext_ {
   int wl_last = 0;                         // counter the last fast launch used
   CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
   mjh::ContactParam* cparams = nullptr;    // each program pair's mj_contactParam
+  unsigned long long* masks = nullptr;     // the cooperative kernel's chain masks (coop_masks)
   int npair = 0;
   bool boxpair = false;                    // a box-box pair is in the program (coop LDS)
   int coop = 16;                           // lanes per instance of k_constraint_coop (0: off)
@@ -1264,6 +1321,22 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   // the cooperative kernel's per-dof chain masks are 64-bit
   if (m->nv > 64) c->coop = 0;
   if (c->coop) {
+    // chain masks (mjh::chainMask per body: the body and its ancestors), then per body the
+    // dofs of those bodies: model constants, formed here once
+    std::vector<unsigned long long> mk(2 * (size_t)m->nbody, 0);
+    for (int b = 0; b < m->nbody && b < 64; b++) mk[b] = mjh::chainMask(*m, b);
+    for (int b = 0; b < m->nbody && b < 64; b++) {
+      for (int j = 0; j < m->nv; j++) {
+        if ((mk[b] >> m->dof_bodyid[j]) & 1) mk[m->nbody + b] |= 1ull << j;
+      }
+    }
+    if (hipMalloc((void**)&c->masks, sizeof(unsigned long long) * mk.size()) != hipSuccess ||
+        hipMemcpy(c->masks, mk.data(), sizeof(unsigned long long) * mk.size(),
+                  hipMemcpyHostToDevice) != hipSuccess) {
+      return fail("chain mask upload");
+    }
+  }
+  if (c->coop) {
     // the cooperative kernel's dynamic LDS must fit one block: many box pairs (a large
     // efc_cap) or few lanes per instance can exceed it, and then the one-lane k_constraint
     // serves the model instead of every launch failing
@@ -1297,6 +1370,7 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->worklist);
   hipFree(c->pairs);
   hipFree(c->cparams);
+  hipFree(c->masks);
   hipFree(c->mirror_buf);
   hipFree(c->dmodel_buf);
   if (c->rt_module) hipModuleUnload(c->rt_module);
@@ -1386,6 +1460,9 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
       HIPCHECK(hipModuleLaunchKernel(c->rt_fn, grid.x, 1, 1, 64, 1, 1, 0, c->stream, args,
                                      nullptr));
     }
+    if (mjh::hasFluid(c->dmodel)) {       // fluid forces into qfrc_passive before the assembly
+      hipLaunchKernelGGL(k_fluid_after, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
+    }
     // the fast path excludes INVDISCRETE: the constraint kernel is fused whenever nbody allows
     const bool fused = mjh::fusedOk(c->dmodel, mjhipSTAGE_NONE);
     const int* wl = c->worklist + 2;
@@ -1397,7 +1474,8 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
                                                       c->npair, c->con_cap),                  \
                          c->stream,                                                           \
                          c->dmodel, c->mirror, B, wl,                                         \
-                         (const int*)cnt, c->pairs, c->cparams, c->npair, qfrc, status)
+                         (const int*)cnt, c->pairs, c->cparams, c->masks, c->npair, qfrc,    \
+                         status)
       if (contact && c->boxpair) {       // the box-box path is compiled in only here
         if (list) MJHIP_LAUNCH_COOP(16, true, true, true);
         else MJHIP_LAUNCH_COOP(16, true, false, true);

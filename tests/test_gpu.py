@@ -978,6 +978,7 @@ def test_fluid_parity():
   B = 512
   q, v, a = sample_states(m, B, first=21)
   e = engine.InverseEngine(m, capacity=B)
+  assert e.fast_kernel is not None        # straight-line kernel + the fluid pass
   f = e.inverse(q, v, a)
   o = Oracle(m)
   ref, fl = [], []
@@ -1009,10 +1010,13 @@ def test_ellipsoid_fluid_parity():
   v = 2 * v
   e = engine.InverseEngine(m, capacity=B)
   try:
+    assert e.fast_kernel is not None      # straight-line kernel + the fluid pass
     f = e.inverse(q, v, a)
     fl_gpu = e.field("qfrc_fluid", 0, B)
+    fg = e.inverse(q, v, a, generic=True)
   finally:
     e.close()
+  assert_close(f, fg, "straight-line vs generic qfrc_inverse")
   o = Oracle(m)
   ref, fl = [], []
   for i in range(B):

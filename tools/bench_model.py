@@ -1,0 +1,42 @@
+"""Throughput of one model's inverse pipeline (not the headline bench): inputs resident in
+the device mirror, HIP-synchronized wall time over repeated calls. For rocprof lines of the
+kernels a model selects (bundled or run-time generated, generic).
+
+  python tools/bench_model.py slider_crank [B] [reps]
+  python tools/bench_model.py path/to/model.xml [B] [reps]
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+  import torch
+  from mujoco_inversedynamicstest_amd import engine, mjcf, models
+  from mujoco_inversedynamicstest_amd.sampler import sample_states
+  name = sys.argv[1]
+  B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
+  reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
+  m = mjcf.load_xml(name) if name.endswith(".xml") else models.load(name)
+  q, v, a = sample_states(m, B)
+  torch.cuda.set_device(0)
+  e = engine.InverseEngine(m, capacity=B)
+  e.upload_states(q, v, a)
+  for _ in range(3):
+    e.inverse(B, mirror_input=True)
+  torch.cuda.synchronize()
+  t0 = time.perf_counter()
+  for _ in range(reps):
+    e.inverse(B, mirror_input=True)
+  torch.cuda.synchronize()
+  dt = (time.perf_counter() - t0) / reps
+  print(f"{name}: batch {B}, kernel {e.fast_kernel or 'generic'}, {dt*1e3:.3f} ms per call, "
+        f"{B/dt/1e6:.1f}M evals/s")
+  e.close()
+
+
+if __name__ == "__main__":
+  main()

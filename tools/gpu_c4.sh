@@ -30,3 +30,7 @@ done
 echo "== rocprof config4"
 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o prof --output-format csv -- python bench.py --config 4 --steps 10 --warmup 3 > gpurun_out/prof_c4.log 2>&1 || exit 1
 find gpurun_out/prof_c4 -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-160
+echo "== slider_crank (config-1 model) straight-line kernel"
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sc -o sc --output-format csv -- python tools/bench_model.py slider_crank 65536 20 > gpurun_out/sc.log 2>&1 || exit 1
+grep "evals/s" gpurun_out/sc.log
+find gpurun_out/prof_sc -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-160 | head -5
