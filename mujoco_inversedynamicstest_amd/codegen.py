@@ -130,8 +130,6 @@ def fast_path_supported(m) -> str | None:
     return "sparse Jacobians"
   if m.opt["enableflags"] & (1 << 3):
     return "INVDISCRETE"
-  if m.sizes.get("nwrap", 0) and np.any(np.asarray(m.wrap_type) != 1):
-    return "spatial tendons (generic kernel)"
   for a in range(m.nu):
     if m.actuator_trntype[a] not in (0, 1, 2, 3, 4, 5):
       return "unknown transmission"
@@ -145,9 +143,18 @@ def fast_path_supported(m) -> str | None:
 TRN_AFTER = (2, 4, 5)
 
 
+def spatial_tendons(m) -> list:
+  """Tendons whose path is spatial (their first wrap is not a joint, engine_core_smooth.c
+  mj_tendon): their length, Jacobian and velocity, the tendon transmissions on them and
+  mj_passive are left to the pass before the constraint kernel (csrc/post_pass.h)."""
+  return [t for t in range(m.ntendon) if int(m.wrap_type[int(m.tendon_adr[t])]) != 1]
+
+
 def constraint_mode(m) -> str:
   """Which instances the constraint kernel serves: 'all', 'list' or 'none' (module doc)."""
   dsbl = int(m.opt["disableflags"])
+  if spatial_tendons(m):
+    return "all"          # the tendon pass (csrc/post_pass.h) forms ten_J and qfrc_passive
   if (m.opt["density"] > 0 or m.opt["viscosity"] > 0) and not dsbl & (1 << 5):
     return "all"          # fluid: the post pass (csrc/post_pass.h) updates qfrc_passive, and
                           # the constraint kernel assembles qfrc_inverse for every instance
@@ -205,14 +212,19 @@ class _Model:
     # 4 waves per CU must fit in 160 KB)
     hinges = [j for j in range(m.njnt) if int(m.jnt_type[j]) == HINGE]
     self.trig = {j: h for h, j in enumerate(hinges)} if 0 < len(hinges) <= MAX_LDS_HINGES else {}
+    self.spatial = set(spatial_tendons(m))
     self.ten_terms = []
     for t in range(m.ntendon):
       adr, num = int(m.tendon_adr[t]), int(m.tendon_num[t])
+      if t in self.spatial:
+        self.ten_terms.append(None)      # formed by the tendon pass, never emitted here
+        continue
       self.ten_terms.append([(float(m.wrap_prm[w]), int(m.jnt_qposadr[m.wrap_objid[w]]),
                               int(m.jnt_dofadr[m.wrap_objid[w]]))
                              for w in range(adr, adr + num)])
 
   def ten_row(self, t):
+    assert t not in self.spatial, "spatial tendon rows are formed at run time"
     J = np.zeros(self.nv)
     for prm, _, da in self.ten_terms[t]:
       J[da] = prm
@@ -486,12 +498,14 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
   if m.ntendon:
     E(f"double ten_length[{m.ntendon}];")
     for t, terms in enumerate(M.ten_terms):
+      if terms is None:
+        continue
       E(f"ten_length[{t}] = 0.0;")
       for prm, qa, _ in terms:
         E(f"ten_length[{t}] += {lit(prm)} * qpos[{qa}];")
     if limits_on:
       for t in range(m.ntendon):
-        if m.tendon_limited[t]:
+        if m.tendon_limited[t] and t not in M.spatial:
           lo, hi = m.tendon_range[t]
           mg = lit(m.tendon_margin[t])
           E(f"active |= (-1.0*({lit(lo)} - ten_length[{t}]) < {mg}) | "
@@ -507,8 +521,10 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
 
   # tendons and transmission depend on qpos only
   if m.ntendon:
-    E("// ---- mj_tendon (fixed, dense ten_J)")
+    E("// ---- mj_tendon (fixed, dense ten_J)")   # spatial ones: the tendon pass
     for t in range(m.ntendon):
+      if t in M.spatial:
+        continue
       G.st("ten_length", t, f"ten_length[{t}]")
       J = M.ten_row(t)
       for k in range(nv):
@@ -519,6 +535,8 @@ def _gen_pos(M: _Model, store_fields=None) -> str:
       if int(m.actuator_trntype[a]) in TRN_AFTER:
         continue                       # k_sensors' mjh::transmissionAfter
       jid = int(m.actuator_trnid[a, 0])
+      if m.actuator_trntype[a] == 3 and jid in M.spatial:
+        continue                       # the tendon pass (csrc/post_pass.h)
       g = float(m.actuator_gear[a, 0])
       adr = int(m.moment_rowadr[a])
       if m.actuator_trntype[a] == 3:   # :1053-1081: gear * ten_J over the row's nonzeros
@@ -903,6 +921,8 @@ def _gen_va(M: _Model, store_fields=None) -> str:
 
   E("// ---- mj_fwdVelocity (engine_forward.c:193-231)")
   for t in range(m.ntendon):
+    if t in M.spatial:
+      continue
     E(f"double ten_velocity_{t};")
     E.open()
     E(f"const double J[{nv}] = {arr_lit(M.ten_row(t))};")
@@ -915,6 +935,8 @@ def _gen_va(M: _Model, store_fields=None) -> str:
       g = float(m.actuator_gear[a, 0])
       if int(m.actuator_trntype[a]) in TRN_AFTER:
         continue                       # with its transmission, after the constraint kernel
+      if m.actuator_trntype[a] == 3 and int(m.actuator_trnid[a, 0]) in M.spatial:
+        continue                       # the tendon pass (csrc/post_pass.h)
       if m.actuator_trntype[a] == 3:   # mju_dotSparse over the tendon row's nonzeros
         if not n:
           G.st("actuator_velocity", a, "0.0")
@@ -972,8 +994,8 @@ def _gen_va(M: _Model, store_fields=None) -> str:
         E(f"qfd[{dof}] = -{lit(b)}*qvel[{dof}];")
     for t in range(m.ntendon):
       k, b = float(m.tendon_stiffness[t]), float(m.tendon_damping[t])
-      if k == 0 and b == 0:
-        continue
+      if (k == 0 and b == 0) or t in M.spatial:
+        continue                       # spatial: the tendon pass re-forms mj_passive
       lo, hi = m.tendon_lengthspring[t]
       E.open()
       E(f"const double J[{nv}] = {arr_lit(M.ten_row(t))};")

@@ -649,6 +649,15 @@ __global__ __launch_bounds__(64) void k_fluid_after(mjhipModel m, Mirror mr, int
   mjh::fluidAfter(m, d);
 }
 
+// spatial tendons, their transmissions and mj_passive after the generated kernels
+// (csrc/post_pass.h): one lane per instance
+__global__ __launch_bounds__(64) void k_tendon_after(mjhipModel m, Mirror mr, int B) {
+  const long inst = (long)blockIdx.x*64 + threadIdx.x;
+  if (inst >= B) return;
+  Lane<64> d = lane_view(mr, blockIdx.x, threadIdx.x);
+  mjh::tendonAfter(m, d);
+}
+
 // Status checks of the straight-line path: mj_checkPos/Vel/Acc (engine_forward.c:53-102)
 // on the inputs and the pivot test behind MJHIP_INST_INERTIA on qLD's diagonal, ORed into
 // the status words the generated kernels and k_constraint wrote. A separate launch, run
@@ -920,6 +929,7 @@ struct mjhipContext_ {
   int npair = 0;
   bool boxpair = false;                    // a box-box pair is in the program (coop LDS)
   int coop = 16;                           // lanes per instance of k_constraint_coop (0: off)
+  bool spatial = false;                    // spatial tendons: k_tendon_after runs (post_pass.h)
   // a straight-line kernel specialized for this model at run time (mjhip_contextLoadKernel):
   // a gfx950 code object holding extern "C" k_all_<name>; rt.launch stays null
   unsigned long long sig = 0;              // model_signature of the model at creation
@@ -1318,6 +1328,7 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   // the native convex solver keeps its polytope in the instance's scratch: one lane per
   // instance (the cooperative kernel would run several pairs of an instance at once)
   if (mjh_needConvex(m)) c->coop = 0;
+  c->spatial = mjh::hasSpatial(*m);
   // the cooperative kernel's per-dof chain masks are 64-bit
   if (m->nv > 64) c->coop = 0;
   if (c->coop) {
@@ -1460,7 +1471,9 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
       HIPCHECK(hipModuleLaunchKernel(c->rt_fn, grid.x, 1, 1, 64, 1, 1, 0, c->stream, args,
                                      nullptr));
     }
-    if (mjh::hasFluid(c->dmodel)) {       // fluid forces into qfrc_passive before the assembly
+    if (c->spatial) {                    // spatial tendons and all of mj_passive
+      hipLaunchKernelGGL(k_tendon_after, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
+    } else if (mjh::hasFluid(c->dmodel)) {   // fluid forces into qfrc_passive
       hipLaunchKernelGGL(k_fluid_after, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
     }
     // the fast path excludes INVDISCRETE: the constraint kernel is fused whenever nbody allows

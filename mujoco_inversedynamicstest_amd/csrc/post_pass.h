@@ -7,6 +7,13 @@
 // zero), then this pass, then the constraint kernel for every instance (codegen's
 // constraint_mode 'all'), and every output equals the generic pipeline's: qfrc_passive is
 // re-formed here in mj_passive's own order (spring + damper, + fluid, + gravcomp, :461-493).
+//
+// Spatial tendons (mj_tendon, engine_core_smooth.c:651-860) depend on site and geom frames
+// at run time, so the generated kernel leaves their length, Jacobian and velocity, the
+// tendon transmissions on them and every tendon term of mj_passive to tendonAfter below,
+// which runs before the constraint kernel (constraint_mode 'all'): mj_tendon, the
+// ten_velocity of mj_fwdVelocity, those transmissions and all of mj_passive (fluid included)
+// are re-formed with the generic functions, over the frames the generated kernel stored.
 #ifndef MJHIP_POST_PASS_H_
 #define MJHIP_POST_PASS_H_
 
@@ -49,6 +56,36 @@ MJH_HD void fluidAfter(const mjhipModel& m, const Lane<S>& d) {
       for (int j = 0; j < dofnum; j++) d.qfrc_passive[dofadr+j] += d.qfrc_gravcomp[dofadr+j];
     }
   }
+}
+
+MJH_HD bool hasSpatial(const mjhipModel& m) {
+  for (int i = 0; i < m.ntendon; i++) {
+    if (m.wrap_type[m.tendon_adr[i]] != mjhipWRAP_JOINT) return true;
+  }
+  return false;
+}
+
+template <int S>
+MJH_HD void tendonAfter(const mjhipModel& m, const Lane<S>& d) {
+  const int nv = m.nv;
+  tendon(m, d);                             // fixed tendons re-formed to the same values
+  for (int r = 0; r < m.ntendon; r++) d.ten_velocity[r] = dot(d.ten_J + r*nv, d.qvel, nv);
+  for (int i = 0; i < m.nu; i++) {          // mj_transmission :1053-1081 on spatial tendons
+    if (m.actuator_trntype[i] != mjhipTRN_TENDON) continue;
+    const int id = m.actuator_trnid[2*i];
+    if (m.wrap_type[m.tendon_adr[id]] == mjhipWRAP_JOINT) continue;
+    const int adr = m.moment_rowadr[i];
+    const double gear = m.actuator_gear[6*i];
+    d.actuator_length[i] = d.ten_length[id]*gear;
+    for (int k = 0; k < m.moment_rownnz[i]; k++) {
+      d.actuator_moment[adr+k] = d.ten_J[id*nv + m.moment_colind[adr+k]]*gear;
+    }
+    if (!(m.opt.disableflags & mjhipDSBL_ACTUATION)) {
+      d.actuator_velocity[i] = dotSparse(d.actuator_moment + adr, d.qvel, m.moment_rownnz[i],
+                                         m.moment_colind + adr);
+    }
+  }
+  passive(m, d);
 }
 
 }  // namespace mjh

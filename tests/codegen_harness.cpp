@@ -50,9 +50,11 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
     FAST_BODY(mr, i / 64, i % 64, B, qpos, qvel, qacc, nullptr, nullptr, wl, &wc, &wnext,
               mr.efc_count);
   }
-  for (int i = 0; i < B; i++) {   // fluid forces (k_fluid_after on the device)
+  const bool spatial = mjh::hasSpatial(*m);
+  for (int i = 0; i < B; i++) {   // k_tendon_after, else k_fluid_after, on the device
     mjh::Lane<64> d = lane_view(mr, i / 64, i % 64);
-    mjh::fluidAfter<64>(*m, d);
+    if (spatial) mjh::tendonAfter<64>(*m, d);
+    else mjh::fluidAfter<64>(*m, d);
   }
   const bool fused = mjh::fusedOk(*m, mjhipSTAGE_NONE);
   const int served = cmode == 2 ? B : (cmode == 1 ? wc : 0);

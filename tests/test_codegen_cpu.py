@@ -207,6 +207,47 @@ def test_generated_tendon_transmissions():
   run_and_compare(m, "tendontrn", q, v, a)
 
 
+MIXED_TENDONS = """<mujoco><option density="1.1" viscosity=".2"/><worldbody>
+  <geom type="plane" size="3 3 .1" pos="0 0 1"/><site name="top" pos="0 0 2"/>
+  <body pos="0 0 1" gravcomp=".4"><freejoint/><geom type="box" size=".1 .1 .05"/>
+    <site name="s0" pos=".1 0 .05"/>
+    <body pos=".1 0 0"><joint name="h1" axis="0 1 0" range="-80 80"/>
+      <geom name="ball" type="sphere" size=".06"/><site name="side" pos="0 0 .1"/>
+      <geom type="capsule" fromto="0 0 0 .3 0 0" size=".03"/><site name="s1" pos=".25 0 .06"/>
+      <body pos=".3 0 0"><joint name="h2" axis="0 0 1" damping=".1"/>
+        <geom type="capsule" fromto="0 0 0 .3 0 0" size=".03"/>
+        <site name="s2" pos=".3 0 -.04"/></body></body></body>
+  </worldbody>
+  <tendon>
+    <fixed name="fx" stiffness="4" damping=".2" limited="true" range="-.6 .6">
+      <joint joint="h1" coef="1"/><joint joint="h2" coef="-.5"/></fixed>
+    <spatial name="sp" limited="true" range=".2 .9" stiffness="3" damping=".3"
+        frictionloss=".05">
+      <site site="top"/><site site="s0"/><geom geom="ball" sidesite="side"/>
+      <site site="s1"/><pulley divisor="2"/><site site="s1"/><site site="s2"/></spatial>
+  </tendon>
+  <actuator><motor tendon="fx" gear="2"/><motor name="asp" tendon="sp" gear="-1.5"/>
+    <motor joint="h2"/></actuator>
+  <sensor><tendonpos tendon="sp"/><tendonvel tendon="sp"/><actuatorpos actuator="asp"/>
+    <actuatorvel actuator="asp"/><tendonpos tendon="fx"/></sensor></mujoco>"""
+
+
+@pytest.mark.parametrize("which", ["arm", "wrap", "mixed"])
+def test_spatial_tendons_generated_bitexact(which):
+  """Spatial tendons on the straight-line path: the generated kernel leaves their length,
+  Jacobian, velocity, transmissions and mj_passive to the tendon pass (csrc/post_pass.h),
+  which runs before the constraint kernel serves every instance. Sites and pulleys (ARM),
+  sphere and cylinder wrapping (WRAP), and a model mixing a fixed and a spatial tendon with
+  limits, friction loss, contacts, fluid, gravity compensation and tendon sensors: every
+  output equals the oracle's bit for bit."""
+  from test_tendon_cpu import ARM, WRAP
+  m = mjcf.load_xml_string({"arm": ARM, "wrap": WRAP, "mixed": MIXED_TENDONS}[which])
+  assert codegen.fast_path_supported(m) is None and codegen.constraint_mode(m) == "all"
+  assert codegen.spatial_tendons(m)
+  q, v, a = sample_states(m, 48, first=3, margin=-0.1)
+  assert run_and_compare(m, f"spatial_{which}", q, v, a) == 48
+
+
 def test_generated_then_sensor_pass():
   """Sensor models on the straight-line path: every supported sensor type (limit and
   contact rows active) computed by the sensor pass after the generated kernels and the

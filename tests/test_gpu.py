@@ -1258,12 +1258,17 @@ def test_config3_full_batch_one_gpu(humanoid):
   assert_close(f[sub[:256]], ref["qfrc_inverse"], "qfrc_inverse (config 3 subsample)")
 
 
-@pytest.mark.parametrize("which", ["sites", "wrap"])
-def test_spatial_tendon_parity(which):
+@pytest.mark.parametrize("which,path", [("sites", "fast"), ("wrap", "fast"),
+                                        ("sites", "onelane"), ("wrap", "onelane"),
+                                        ("sites", "generic"), ("wrap", "generic")])
+def test_spatial_tendon_parity(which, path, monkeypatch):
   """Spatial tendons through sites and pulleys, and wrapping around spheres and cylinders
   (with side sites outside and inside the wrap geom, and without one): lengths, Jacobians,
-  limit rows, spring-damper, tendon actuators on the device vs the oracle; the models have
-  no straight-line kernel (the generic pipeline serves them)."""
+  limit rows, spring-damper, tendon actuators on the device vs the oracle, through the
+  run-time straight-line kernel with the tendon pass (csrc/post_pass.h) and the cooperative
+  or the one-lane constraint kernel, and through the generic kernel."""
+  if path == "onelane":
+    monkeypatch.setenv("MJHIP_COOP_LANES", "0")
   import os
   import sys
   sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -1276,8 +1281,11 @@ def test_spatial_tendon_parity(which):
   a = np.array([x[2] for x in st])
   e = engine.InverseEngine(m, capacity=len(q))
   try:
-    assert e.fast_kernel is None
-    f, status = e.inverse(q, v, a, status=True)
+    assert e.fast_kernel is not None
+    f, status = e.inverse(q, v, a, status=True, generic=path == "generic")
+    vel = e.field("ten_velocity", 0, len(q))
+    sd = e.field("qfrc_passive", 0, len(q))
+    am = e.field("actuator_moment", 0, len(q))
     tl = e.field("ten_length", 0, len(q))
     tj = e.field("ten_J", 0, len(q))
     nefc = e.field_int("efc_count", 0, len(q))[:, 0]
@@ -1285,13 +1293,54 @@ def test_spatial_tendon_parity(which):
     e.close()
   assert (status == 0).all()
   o = Oracle(m)
-  ref, rl, rj = [], [], []
+  ref, rl, rj, rv, rp, rm = [], [], [], [], [], []
   for i in range(len(q)):
     ref.append(o.inverse(q[i], v[i], a[i]))
     rl.append(o.d.ten_length.copy())
     rj.append(o.d.ten_J.copy())
+    rv.append(o.d.ten_velocity.copy())
+    rp.append(o.d.qfrc_passive.copy())
+    rm.append(o.d.actuator_moment.copy())
     assert nefc[i] == o.d.nefc
   assert_close(f, np.array(ref), "qfrc_inverse")
   assert_close(tl, np.array(rl), "ten_length")
   assert_close(tj, np.array(rj), "ten_J")
+  assert_close(vel, np.array(rv), "ten_velocity")
+  assert_close(sd, np.array(rp), "qfrc_passive")
+  assert_close(am, np.array(rm), "actuator_moment")
   assert nefc.sum() > 0
+
+
+def test_spatial_tendon_mixed_parity():
+  """A fixed and a spatial tendon (limits, friction loss, spring-damper, transmissions,
+  tendon and actuator sensors) with contacts, fluid and gravity compensation: the run-time
+  straight-line kernel, the tendon pass and the cooperative constraint kernel vs the oracle
+  on qfrc_inverse, qfrc_passive and the sensors."""
+  import os
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+  from test_codegen_cpu import MIXED_TENDONS
+  from mujoco_inversedynamicstest_amd import mjcf
+  m = mjcf.load_xml_string(MIXED_TENDONS)
+  B = 2048
+  q, v, a = sample_states(m, B, first=3, margin=-0.1)
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    assert e.fast_kernel is not None
+    f, status = e.inverse(q, v, a, status=True)
+    pas = e.field("qfrc_passive", 0, B)
+    sd = e.field("sensordata", 0, B)
+    ncon = e.field_int("efc_count", 0, B)
+  finally:
+    e.close()
+  assert (status == 0).all()
+  o = Oracle(m)
+  ref, rp, rs = [], [], []
+  for i in range(B):
+    ref.append(o.inverse(q[i], v[i], a[i]))
+    rp.append(o.d.qfrc_passive.copy())
+    rs.append(o.d.sensordata.copy())
+  assert_close(f, np.array(ref), "qfrc_inverse")
+  assert_close(pas, np.array(rp), "qfrc_passive")
+  assert_close(sd, np.array(rs), "sensordata")
+  assert ncon[:, 0].sum() > 0

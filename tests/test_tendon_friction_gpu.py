@@ -1,6 +1,7 @@
 """Tendon friction rows on the MI355X vs the oracle: the generic kernel, the straight-line
-kernels with the cooperative constraint kernel (fixed tendons only: a run-time kernel) and
-the one-lane constraint kernel (MJHIP_COOP_LANES=0); row counts, types and ids exact,
+kernels (a run-time kernel; with a spatial tendon, the tendon pass of csrc/post_pass.h)
+with the cooperative constraint kernel and the one-lane constraint kernel
+(MJHIP_COOP_LANES=0); row counts, types and ids exact,
 forces and qfrc_inverse within 1e-10."""
 import numpy as np
 import pytest
@@ -17,7 +18,8 @@ FIXED_ONLY = XML.replace('<spatial name="t3" frictionloss="0.3"><site site="s1"/
                          '</spatial>', '')
 
 
-@pytest.mark.parametrize("xml,lanes,generic", [(XML, None, True), (FIXED_ONLY, None, False),
+@pytest.mark.parametrize("xml,lanes,generic", [(XML, None, True), (XML, None, False),
+                                               (XML, "0", False), (FIXED_ONLY, None, False),
                                                (FIXED_ONLY, "0", False),
                                                (FIXED_ONLY, None, True)])
 def test_tendon_friction_parity(xml, lanes, generic, monkeypatch):
@@ -28,7 +30,7 @@ def test_tendon_friction_parity(xml, lanes, generic, monkeypatch):
   q, v, a = sample_states(m, B, first=9)
   a = a * np.where(np.arange(B) % 3 == 0, 1e-4, np.where(np.arange(B) % 3 == 1, 1.0, 50.0))[:, None]
   e = engine.InverseEngine(m, capacity=B)
-  if not generic and xml is FIXED_ONLY:
+  if not generic:
     assert e.fast_kernel is not None
   f, st = e.inverse(q, v, a, status=True, generic=generic)
   assert (st == 0).all()
