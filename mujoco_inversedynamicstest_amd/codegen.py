@@ -129,7 +129,12 @@ def fast_path_supported(m) -> str | None:
   if m.opt["jacobian"] == 1 or (m.opt["jacobian"] == 2 and m.nv >= 60):
     return "sparse Jacobians"
   if m.opt["enableflags"] & (1 << 3):
-    return "INVDISCRETE"
+    if int(m.opt["integrator"]) == 1:
+      return "INVDISCRETE with RK4 (an error in the reference)"
+    if any(int(t) in TRN_AFTER for t in m.actuator_trntype[:m.nu]):
+      # implicit damping reads actuator_moment before the constraint kernel, and a body
+      # transmission needs the contacts that kernel makes
+      return "INVDISCRETE with slider-crank, site or body transmissions"
   for a in range(m.nu):
     if m.actuator_trntype[a] not in (0, 1, 2, 3, 4, 5):
       return "unknown transmission"
@@ -155,6 +160,9 @@ def constraint_mode(m) -> str:
   dsbl = int(m.opt["disableflags"])
   if spatial_tendons(m):
     return "all"          # the tendon pass (csrc/post_pass.h) forms ten_J and qfrc_passive
+  if int(m.opt["enableflags"]) & (1 << 3):
+    return "all"          # the discrete pass (csrc/post_pass.h) changes qacc before the
+                          # constraint kernel, which assembles qfrc_inverse from it
   if (m.opt["density"] > 0 or m.opt["viscosity"] > 0) and not dsbl & (1 << 5):
     return "all"          # fluid: the post pass (csrc/post_pass.h) updates qfrc_passive, and
                           # the constraint kernel assembles qfrc_inverse for every instance

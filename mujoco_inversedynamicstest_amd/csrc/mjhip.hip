@@ -658,6 +658,22 @@ __global__ __launch_bounds__(64) void k_tendon_after(mjhipModel m, Mirror mr, in
   mjh::tendonAfter(m, d);
 }
 
+// mjENBL_INVDISCRETE on the straight-line path (csrc/post_pass.h): mj_discreteAcc and the
+// RNE over its qacc before the constraint kernel; the caller's qacc back after the sensors
+__global__ __launch_bounds__(64) void k_discrete_before(mjhipModel m, Mirror mr, int B) {
+  const long inst = (long)blockIdx.x*64 + threadIdx.x;
+  if (inst >= B) return;
+  Lane<64> d = lane_view(mr, blockIdx.x, threadIdx.x);
+  mjh::discreteBefore(m, d);
+}
+
+__global__ __launch_bounds__(64) void k_discrete_restore(mjhipModel m, Mirror mr, int B) {
+  const long inst = (long)blockIdx.x*64 + threadIdx.x;
+  if (inst >= B) return;
+  Lane<64> d = lane_view(mr, blockIdx.x, threadIdx.x);
+  mjh::discreteRestore(m, d);
+}
+
 // Status checks of the straight-line path: mj_checkPos/Vel/Acc (engine_forward.c:53-102)
 // on the inputs and the pivot test behind MJHIP_INST_INERTIA on qLD's diagonal, ORed into
 // the status words the generated kernels and k_constraint wrote. A separate launch, run
@@ -1476,7 +1492,11 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     } else if (mjh::hasFluid(c->dmodel)) {   // fluid forces into qfrc_passive
       hipLaunchKernelGGL(k_fluid_after, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
     }
-    // the fast path excludes INVDISCRETE: the constraint kernel is fused whenever nbody allows
+    const bool discrete = mjh::hasDiscrete(c->hmodel);
+    if (discrete) {                      // mj_discreteAcc and its RNE before the constraints
+      hipLaunchKernelGGL(k_discrete_before, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
+    }
+    // INVDISCRETE takes the unfused rows (fusedOk); otherwise fused whenever nbody allows
     const bool fused = mjh::fusedOk(c->dmodel, mjhipSTAGE_NONE);
     const int* wl = c->worklist + 2;
     if (fused && c->coop && c->fast->cmode) {   // cooperative lanes per instance
@@ -1526,6 +1546,10 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
       hipLaunchKernelGGL(k_sensors, grid, block, 0, c->stream, c->dmodel, c->mirror, B,
                          sensors, trn);
       HIPCHECK(hipGetLastError());
+    }
+    if (discrete) {                      // the caller's qacc back, after mj_sensorAcc
+      hipLaunchKernelGGL(k_discrete_restore, grid, block, 0, c->stream, c->dmodel, c->mirror,
+                         B);
     }
     if (status) {
       hipLaunchKernelGGL(k_check, grid, block, 0, c->stream, c->dmodel, c->mirror, B, status);

@@ -14,6 +14,15 @@
 // which runs before the constraint kernel (constraint_mode 'all'): mj_tendon, the
 // ten_velocity of mj_fwdVelocity, those transmissions and all of mj_passive (fluid included)
 // are re-formed with the generic functions, over the frames the generated kernel stored.
+//
+// mjENBL_INVDISCRETE (mj_inverseSkip, engine_inverse.c:197-256): the generated kernel runs
+// the position and velocity stages and an RNE over the caller's qacc. discreteBefore then
+// saves qacc, replaces it with mj_discreteAcc's (engine_inverse.c:81-164) and redoes
+// mj_rne(flg_acc = 1) over it; the constraint kernel (constraint_mode 'all', the unfused
+// rows: referenceConstraint, then invConstraint on the new qacc) assembles qfrc_inverse, the
+// sensor pass runs mj_sensorAcc on it, and discreteRestore puts the caller's qacc back, as
+// the reference does after its sensors. It runs after the tendon or fluid pass: implicit
+// damping reads tendon Jacobians and the passive derivatives.
 #ifndef MJHIP_POST_PASS_H_
 #define MJHIP_POST_PASS_H_
 
@@ -86,6 +95,22 @@ MJH_HD void tendonAfter(const mjhipModel& m, const Lane<S>& d) {
     }
   }
   passive(m, d);
+}
+
+MJH_HD bool hasDiscrete(const mjhipModel& m) {
+  return (m.opt.enableflags & mjhipENBL_INVDISCRETE) != 0;
+}
+
+template <int S>
+MJH_HD void discreteBefore(const mjhipModel& m, const Lane<S>& d) {
+  copy(d.qacc_save, d.qacc, m.nv);
+  discreteAcc(m, d);
+  rne(m, d, 1, d.qfrc_inverse);
+}
+
+template <int S>
+MJH_HD void discreteRestore(const mjhipModel& m, const Lane<S>& d) {
+  copy(d.qacc, d.qacc_save, m.nv);
 }
 
 }  // namespace mjh

@@ -55,6 +55,7 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
     mjh::Lane<64> d = lane_view(mr, i / 64, i % 64);
     if (spatial) mjh::tendonAfter<64>(*m, d);
     else mjh::fluidAfter<64>(*m, d);
+    if (mjh::hasDiscrete(*m)) mjh::discreteBefore<64>(*m, d);   // k_discrete_before
   }
   const bool fused = mjh::fusedOk(*m, mjhipSTAGE_NONE);
   const int served = cmode == 2 ? B : (cmode == 1 ? wc : 0);
@@ -71,6 +72,7 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
   for (int i = 0; i < B; i++) {   // transmission/sensor/energy pass (k_sensors on the device)
     mjh::Lane<64> d = lane_view(mr, i / 64, i % 64);
     mjh::sensorsAfter<64>(*m, d, true, mjh_needTrnAfter(m) != 0);
+    if (mjh::hasDiscrete(*m)) mjh::discreteRestore<64>(*m, d);  // k_discrete_restore
   }
   size_t off = 0;
 #define XD(name, d0, d1, stage) { int S = mr.name##_n; \

@@ -248,6 +248,36 @@ def test_spatial_tendons_generated_bitexact(which):
   assert run_and_compare(m, f"spatial_{which}", q, v, a) == 48
 
 
+@pytest.mark.parametrize("integrator", [0, 2, 3])
+def test_invdiscrete_generated_bitexact(integrator):
+  """mjENBL_INVDISCRETE on the straight-line path: the generated kernel, then the discrete
+  pass (mj_discreteAcc and mj_rne over its qacc, csrc/post_pass.h), the unfused constraint
+  kernel for every instance, the sensor pass on the discrete qacc, and qacc restored.
+  Euler (implicit damping), implicit and implicitfast on the humanoid with dof damping,
+  contacts and acceleration sensors: every output equals the oracle's bit for bit."""
+  m = models.load("humanoid", disable_contact=False)
+  m.opt["enableflags"] |= 1 << 3
+  m.opt["integrator"] = integrator
+  assert codegen.fast_path_supported(m) is None and codegen.constraint_mode(m) == "all"
+  q, v, a = sample_contact_states(m, 24, first=5)
+  run_and_compare(m, f"invdiscrete{integrator}", q, v, a)
+
+
+def test_invdiscrete_generated_sensors_tendons():
+  """INVDISCRETE (implicitfast: actuator, dof and tendon damping derivatives) with a spatial
+  tendon pass before it and acceleration sensors after it."""
+  xml = MIXED_TENDONS.replace('<option density="1.1" viscosity=".2"/>',
+                              '<option timestep=".01" integrator="implicitfast">'
+                              '<flag invdiscrete="enable"/></option>')
+  xml = xml.replace('<tendonpos tendon="fx"/>', '<tendonpos tendon="fx"/>'
+                    '<accelerometer site="s1"/><framelinacc objtype="site" objname="s2"/>')
+  xml = xml.replace('<motor joint="h2"/>', '<velocity joint="h2" kv="2"/>')
+  m = mjcf.load_xml_string(xml)
+  assert codegen.fast_path_supported(m) is None
+  q, v, a = sample_states(m, 32, first=7, margin=-0.1)
+  run_and_compare(m, "invdiscrete_tendons", q, v, a)
+
+
 def test_generated_then_sensor_pass():
   """Sensor models on the straight-line path: every supported sensor type (limit and
   contact rows active) computed by the sensor pass after the generated kernels and the

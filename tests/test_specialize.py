@@ -87,7 +87,7 @@ def test_code_object_compiles_and_caches(arm, tmp_path, monkeypatch):
 
 def test_unsupported_model_raises():
   m = mjcf.load_xml_string(ARM_XML.replace('<option gravity="0 0 -9.81" timestep="0.002"/>',
-                                           '<option integrator="Euler">'
+                                           '<option integrator="RK4">'
                                            '<flag invdiscrete="enable"/></option>'))
   with pytest.raises(specialize.SpecializeError, match="INVDISCRETE"):
     specialize.code_object(m)
