@@ -1496,8 +1496,8 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     if (discrete) {                      // mj_discreteAcc and its RNE before the constraints
       hipLaunchKernelGGL(k_discrete_before, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
     }
-    // INVDISCRETE takes the unfused rows (fusedOk); otherwise fused whenever nbody allows
-    const bool fused = mjh::fusedOk(c->dmodel, mjhipSTAGE_NONE);
+    // fused rows whenever nbody allows, INVDISCRETE included (post_pass.h fastFusedOk)
+    const bool fused = mjh::fastFusedOk(c->dmodel);
     const int* wl = c->worklist + 2;
     if (fused && c->coop && c->fast->cmode) {   // cooperative lanes per instance
       const bool contact = c->con_cap > 0, list = c->fast->cmode == 1;

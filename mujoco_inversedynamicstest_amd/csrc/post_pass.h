@@ -18,8 +18,8 @@
 // mjENBL_INVDISCRETE (mj_inverseSkip, engine_inverse.c:197-256): the generated kernel runs
 // the position and velocity stages and an RNE over the caller's qacc. discreteBefore then
 // saves qacc, replaces it with mj_discreteAcc's (engine_inverse.c:81-164) and redoes
-// mj_rne(flg_acc = 1) over it; the constraint kernel (constraint_mode 'all', the unfused
-// rows: referenceConstraint, then invConstraint on the new qacc) assembles qfrc_inverse, the
+// mj_rne(flg_acc = 1) over it; the constraint kernel (constraint_mode 'all', its rows made
+// after the new qacc is in place, fastFusedOk) assembles qfrc_inverse, the
 // sensor pass runs mj_sensorAcc on it, and discreteRestore puts the caller's qacc back, as
 // the reference does after its sensors. It runs after the tendon or fluid pass: implicit
 // damping reads tendon Jacobians and the passive derivatives.
@@ -99,6 +99,16 @@ MJH_HD void tendonAfter(const mjhipModel& m, const Lane<S>& d) {
 
 MJH_HD bool hasDiscrete(const mjhipModel& m) {
   return (m.opt.enableflags & mjhipENBL_INVDISCRETE) != 0;
+}
+
+// whether the constraint kernel after the generated kernels takes the fused rows. The
+// generic pipeline cannot under INVDISCRETE (its rows would be finished before
+// mj_discreteAcc), but here the discrete pass has replaced qacc before the constraint kernel
+// starts, so the fused rows see the qacc the reference's mj_invConstraint sees.
+MJH_HD bool fastFusedOk(const mjhipModel& m) {
+  mjhipModel f = m;
+  f.opt.enableflags &= ~mjhipENBL_INVDISCRETE;
+  return fusedOk(f, mjhipSTAGE_NONE);
 }
 
 template <int S>

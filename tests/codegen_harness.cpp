@@ -57,7 +57,7 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
     else mjh::fluidAfter<64>(*m, d);
     if (mjh::hasDiscrete(*m)) mjh::discreteBefore<64>(*m, d);   // k_discrete_before
   }
-  const bool fused = mjh::fusedOk(*m, mjhipSTAGE_NONE);
+  const bool fused = mjh::fastFusedOk(*m);
   const int served = cmode == 2 ? B : (cmode == 1 ? wc : 0);
   for (int g = 0; g < served; g++) {
     const int inst = cmode == 2 ? g : wl[g];
