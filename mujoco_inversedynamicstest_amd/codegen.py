@@ -1377,6 +1377,44 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
 """ + "\n".join(f"  fast_{st}_{name}(mr, {bl}, B, {_SIG[st][1]});\n"
                 f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE();" for st in STAGES)
              + "\n" + fuse_tail + "}")
+  # k_vaskip: the va stage of mj_inverseSkip(mjSTAGE_POS) for mjd_inverseFD's qvel and qacc
+  # perturbations (engine_derivative_fd.c:646-699). Instance off + t reads every position-
+  # stage output (the va pointers it never stores) from its centre instance
+  # (t / per)*sstride, which ran the full kernel; its own qvel/qacc and every field the stage
+  # stores stay its own. Skipped stages see unchanged inputs, so the result is the full
+  # pipeline's bit for bit. Work-list models: a centre with limit rows sets *needfull (the
+  # caller then runs the full pipeline on every perturbation).
+  if M.cmode in ("none", "list"):
+    import re
+    vb = bodies["va"]
+    stored = set(re.findall(r"P_(\w+)\[\d+\*64\]\)? ?=", vb)) | \
+        set(re.findall(r"MJH_NT_STORE\(P_(\w+)\[", vb))
+    own = {"qpos", "qvel", "qacc"} | stored
+    skip_body = re.sub(r"(double\* __restrict__ P_(\w+) = mr\.\w+ \+ \(\(long\))blk(\*\d+\)\*64 \+ )lane;",
+                       lambda mt: mt.group(0) if mt.group(2) in own else
+                       f"{mt.group(1)}sblk{mt.group(3)}slane;", vb)
+    skip_body = skip_body.replace("const bool cflag = ec[0] != 0;",
+                                  "const bool cflag = ecs[0] != 0;")
+    out.append(f"MJH_HD void fast_vaskip_{name}(const Mirror& mr, int blk, int lane, int sblk, "
+               f"int slane, int B, const int* __restrict__ ecs, {_SIG['va'][0]}) {{\n"
+               f"{skip_body}\n}}\n")
+  if M.cmode in ("none", "list"):
+    flag = ("  if (ecs[0] != 0) needfull[0] = 1;\n" if M.cmode == "list" else "")
+    out.append(f"""__global__ __launch_bounds__(64, 1) void k_vaskip_{name}(Mirror mr, int B, int off,
+    int per, int sstride, int* __restrict__ efc_count, int* __restrict__ needfull) {{
+  __shared__ double qo_lds[{64 * max(M.nv, 1)}];
+  const long gi = (long)off + (long)blockIdx.x*64 + threadIdx.x;
+  if (gi >= B) return;
+  const long si = (gi - off) / per * sstride;
+  const int* ecs = efc_count + (si >> 6)*4*64 + (si & 63);
+{flag}  fast_vaskip_{name}(mr, (int)(gi >> 6), (int)(gi & 63), (int)(si >> 6), (int)(si & 63), B,
+                    ecs, nullptr, nullptr, efc_count, qo_lds, nullptr);
+}}
+static void launch_vaskip_{name}(hipStream_t s, const Mirror& mr, int B, int off, int per,
+                                int sstride, int* efc_count, int* needfull) {{
+  hipLaunchKernelGGL(k_vaskip_{name}, dim3((B - off + 63) / 64), dim3(64), 0, s, mr, B, off,
+                     per, sstride, efc_count, needfull);
+}}""")
   out.append(f"""static void launch_fast_{name}(dim3 g, dim3 b, hipStream_t s, const Mirror& mr,
     int B, const double* qpos_in, const double* qvel_in, const double* qacc_in, double* qfrc_out,
     int* status, int* worklist, int* worklist_count, int* worklist_next, int* efc_count) {{""")
@@ -1419,8 +1457,9 @@ def generate_registry(entries) -> str:
   for name, m in entries:
     out.append(generate(m, name))
     reg.append(f'  {{0x{fields.model_signature(m):016x}ull, launch_fast_{name}, "{name}", '
-               f'{CONSTRAINT_MODES[constraint_mode(m)]}}},')
+               f'{CONSTRAINT_MODES[constraint_mode(m)]}, '
+               f'{"launch_vaskip_" + name if constraint_mode(m) in ("none", "list") else "nullptr"}}},')
   out.append("static const FastKernelEntry g_fast_kernels[] = {")
   out.extend(reg)
-  out.append("  {0ull, nullptr, nullptr, 0}};")
+  out.append("  {0ull, nullptr, nullptr, 0, nullptr}};")
   return "\n".join(out) + "\n"

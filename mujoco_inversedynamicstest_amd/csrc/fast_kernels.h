@@ -14,6 +14,10 @@ struct FastKernelEntry {
                  const double*, double*, int*, int*, int*, int*, int*);
   const char* name;
   int cmode;   // codegen.constraint_mode: 0 none, 1 work-list, 2 every instance
+  // mj_inverseSkip(mjSTAGE_POS) for mjd_inverseFD's qvel/qacc perturbations: the va stage of
+  // instances [off, B), position-stage inputs from centre (t - off)/per*sstride (codegen.py
+  // k_vaskip); null for run-time kernels and models whose rows serve every instance
+  void (*launch_vaskip)(hipStream_t, const Mirror&, int, int, int, int, int*, int*);
 };
 
 // the bundled models' kernels (gen_fast.hip), terminated by an entry with launch = nullptr

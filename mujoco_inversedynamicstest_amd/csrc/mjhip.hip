@@ -754,14 +754,36 @@ __global__ void k_from_mirror(const double* __restrict__ src, double* __restrict
 // mjd_inverseFD expansion (engine_derivative_fd.c:611-719): base state b and perturbation
 // p (0 = centre, 1..nv = qacc_i + eps, nv+1..2nv = qvel_i + eps, 2nv+1..3nv = qpos
 // integrated along e_i by eps). Instances are base-major: inst = b*(3nv+1) + p.
+// Layout 1 (stage skipping, mj_inverseSkip(mjSTAGE_POS) for the qvel/qacc perturbations):
+// the instances that run the position stage first, b*(nv+1) + j (j = 0 centre, j = i+1 the
+// qpos perturbation of dof i), then from A = nbase*(nv+1) the others, A + b*2nv + (p-1).
+__device__ static inline long fd_inst(int layout, long nbase, long b, int p, int nv) {
+  if (!layout) return b*(3*nv + 1) + p;
+  if (p == 0) return b*(nv + 1);
+  if (p > 2*nv) return b*(nv + 1) + (p - 2*nv);
+  return nbase*(nv + 1) + b*2*nv + (p - 1);
+}
+
 __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __restrict__ qpos,
                             const double* __restrict__ qvel, const double* __restrict__ qacc,
-                            const double* __restrict__ ctrl, double eps) {
+                            const double* __restrict__ ctrl, double eps, int layout) {
   const int P = 3*m.nv + 1;
   long inst = (long)blockIdx.x*blockDim.x + threadIdx.x;
   if (inst >= (long)nbase*P) return;
-  long b = inst / P;
-  int p = (int)(inst % P);
+  long b;
+  int p;
+  if (!layout) {
+    b = inst / P;
+    p = (int)(inst % P);
+  } else if (inst < (long)nbase*(m.nv + 1)) {
+    b = inst / (m.nv + 1);
+    const int j = (int)(inst % (m.nv + 1));
+    p = j ? 2*m.nv + j : 0;
+  } else {
+    const long t = inst - (long)nbase*(m.nv + 1);
+    b = t / (2*m.nv);
+    p = 1 + (int)(t % (2*m.nv));
+  }
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
   for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos[b*m.nq + k];
   for (int k = 0; k < m.nv; k++) d.qvel[k] = qvel[b*m.nv + k];
@@ -815,13 +837,13 @@ __global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps, int fl
                           double* __restrict__ DfDq, double* __restrict__ DfDv,
                           double* __restrict__ DfDa, double* __restrict__ DsDq,
                           double* __restrict__ DsDv, double* __restrict__ DsDa,
-                          double* __restrict__ DmDq) {
+                          double* __restrict__ DmDq, int layout) {
   const int nv = m.nv, P = 3*nv + 1;
   long t = (long)blockIdx.x*blockDim.x + threadIdx.x;   // one thread per (b, perturbation)
   if (t >= (long)nbase*(P-1)) return;
   long b = t / (P-1);
   int p = (int)(t % (P-1)) + 1;
-  long ic = b*P, ip = b*P + p;
+  long ic = fd_inst(layout, nbase, b, 0, nv), ip = fd_inst(layout, nbase, b, p, nv);
   Lane<64> c = lane_view(mr, (int)(ic >> 6), (int)(ic & 63));
   Lane<64> q = lane_view(mr, (int)(ip >> 6), (int)(ip & 63));
   double inv_h = 1/eps;
@@ -1939,17 +1961,59 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
     }
   }
   long ninst = (long)B*P;
-  hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream, c->dmodel,
-                     c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps);
-  HIPCHECK(hipGetLastError());
-  // all perturbations run the full pipeline (the reference's stage skipping is an
-  // optimisation of a serial loop; results are identical because skipped stages see
-  // unchanged inputs)
   // sensors are skipped when no sensor derivative is asked for (derivative_fd.c:628)
   const int skipsensor = !DsDq && !DsDv && !DsDa;
-  int rc = launch_inverse(c, (int)ninst, nullptr, nullptr, nullptr, nullptr, mjhipSTAGE_NONE,
-                          nullptr, 0, skipsensor);
-  if (rc) { release(); return rc; }
+  // Stage skipping as the reference's loop does (engine_derivative_fd.c:646-699): the qvel
+  // and qacc perturbations run mj_inverseSkip(mjSTAGE_POS), i.e. only the generated va stage
+  // (k_vaskip) over their centre's position-stage outputs. Skipped stages would see
+  // unchanged inputs, so the Jacobians equal the full pipeline's bit for bit. Taken only
+  // where the straight-line kernel is the whole pipeline (no post passes, sensors or
+  // actuation terms) and the position-stage block ends on a wave boundary; a work-list
+  // model whose centres have limit rows falls back to the full pipeline.
+  const long nA = (long)B*(nv + 1);
+  const char* noskip = getenv("MJHIP_FD_NOSKIP");
+  int layout = c->fast && c->fast->launch_vaskip && !(flags & MJHIP_FLAG_GENERIC) &&
+               skipsensor && !flg_actuation && !c->spatial && !mjh::hasFluid(c->hmodel) &&
+               !mjh::hasDiscrete(c->hmodel) && !mjh_needTrnAfter(&c->hmodel) &&
+               !(m.opt.enableflags & mjhipENBL_ENERGY) && nA % 64 == 0 &&
+               !(noskip && noskip[0] == '1');
+  int rc = MJHIP_OK;
+  if (layout) {
+    int* needfull = reinterpret_cast<int*>(alloc(1));
+    if (!needfull) { set_error("hipMalloc(FD flag) failed"); return MJHIP_ERR_HIP; }
+    hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream,
+                       c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, 1);
+    HIPCHECK(hipGetLastError());
+    rc = launch_inverse(c, (int)nA, nullptr, nullptr, nullptr, nullptr, mjhipSTAGE_NONE,
+                        nullptr, 0, skipsensor);
+    if (rc) { release(); return rc; }
+    int full = 0;
+    if (hipMemsetAsync(needfull, 0, sizeof(int), c->stream) != hipSuccess) {
+      release();
+      set_error("FD flag reset failed");
+      return MJHIP_ERR_HIP;
+    }
+    c->fast->launch_vaskip(c->stream, c->mirror, (int)ninst, (int)nA, 2*nv, nv + 1,
+                           c->mirror.efc_count, needfull);
+    HIPCHECK(hipGetLastError());
+    if (c->fast->cmode == 1) {
+      if (hipMemcpyAsync(&full, needfull, sizeof(int), hipMemcpyDeviceToHost, c->stream) !=
+              hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+        release();
+        set_error("FD flag read failed");
+        return MJHIP_ERR_HIP;
+      }
+    }
+    if (full) layout = 0;
+  }
+  if (!layout) {
+    hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream,
+                       c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, 0);
+    HIPCHECK(hipGetLastError());
+    rc = launch_inverse(c, (int)ninst, nullptr, nullptr, nullptr, nullptr, mjhipSTAGE_NONE,
+                        nullptr, 0, skipsensor);
+    if (rc) { release(); return rc; }
+  }
   if (flg_actuation) {
     hipLaunchKernelGGL(k_fd_act, dim3((ninst + 255)/256), dim3(256), 0, c->stream, c->dmodel,
                        c->mirror, ninst);
@@ -1976,7 +2040,7 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
   }
   long nd = (long)B*(P-1);
   hipLaunchKernelGGL(k_fd_diff, dim3((nd + 255)/256), dim3(256), 0, c->stream, c->dmodel,
-                     c->mirror, B, eps, flg_actuation, oq, ov, oa, sq_, sv_, sa_, om);
+                     c->mirror, B, eps, flg_actuation, oq, ov, oa, sq_, sv_, sa_, om, layout);
   if (hipGetLastError() != hipSuccess) {
     release();
     set_error("k_fd_diff launch failed");

@@ -194,6 +194,29 @@ def test_inverse_fd_parity(humanoid):
     np.testing.assert_allclose(DmDq[i], rm, rtol=1e-5, atol=1e-5)
 
 
+@pytest.mark.parametrize("NB,limits", [(1024, False), (64, True), (3, False)])
+def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
+  """mjd_inverseFD's stage skipping (engine_derivative_fd.c:646-699: the qvel and qacc
+  perturbations run mj_inverseSkip(mjSTAGE_POS), here the generated va stage over the
+  centre's position-stage outputs) equals every perturbation through the full pipeline
+  (MJHIP_FD_NOSKIP=1) bit for bit. NB=1024 takes the skip layout; with joint limits active
+  on the centres the work-list model falls back to the full pipeline; NB=3 (28*3 instances,
+  not a whole wave) never takes it."""
+  q, v, a = sample_states(humanoid, NB, first=300)
+  if limits:                            # push a limited hinge past its range on every state
+    j = int(np.flatnonzero(np.asarray(humanoid.jnt_limited))[3])
+    q[:, humanoid.jnt_qposadr[j]] = humanoid.jnt_range[j][1] + 0.2
+  e = engine.InverseEngine(humanoid, capacity=NB * (3 * humanoid.nv + 1))
+  try:
+    got = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
+    monkeypatch.setenv("MJHIP_FD_NOSKIP", "1")
+    ref = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
+  finally:
+    e.close()
+  for g, r in zip(got, ref):
+    assert np.array_equal(g, r)
+
+
 def test_inverse_fd_device_tensors(humanoid, eng):
   """Device-resident mjd_inverseFD (config 5 bench path) equals the host-array path bit for
   bit: same kernels, only the transfers differ."""

@@ -1,0 +1,23 @@
+#!/bin/bash
+# mjd_inverseFD stage skipping on the GPU box: the FD tests, the config-5 bench line with and
+# without skipping (MJHIP_FD_NOSKIP=1), its rocprof summary, then the whole GPU suite
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+echo "== fd tests"
+timeout -k 10 300 python -u -m pytest -x -v --timeout 120 --timeout-method thread tests/test_gpu.py -m gpu \
+  -k "fd or linear_system" > gpurun_out/pytest_fd.log 2>&1 || { tail -30 gpurun_out/pytest_fd.log; exit 1; }
+tail -3 gpurun_out/pytest_fd.log
+echo "== config 5"
+timeout -k 10 180 python bench.py --config 5 > gpurun_out/c5.json 2> gpurun_out/c5.err || { tail gpurun_out/c5.err; exit 1; }
+tail -1 gpurun_out/c5.json | cut -c1-400
+MJHIP_FD_NOSKIP=1 timeout -k 10 180 python bench.py --config 5 > gpurun_out/c5_noskip.json 2> gpurun_out/c5_noskip.err || exit 1
+tail -1 gpurun_out/c5_noskip.json | cut -c1-400
+echo "== rocprof config 5"
+timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o c5 --output-format csv -- python bench.py --config 5 --steps 10 --warmup 3 > gpurun_out/prof_c5.log 2>&1 || exit 1
+find gpurun_out/prof_c5 -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-120
+echo "== full gpu suite"
+timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests -m gpu \
+  > gpurun_out/pytest_gpu.log 2>&1 || { tail -30 gpurun_out/pytest_gpu.log; exit 1; }
+tail -3 gpurun_out/pytest_gpu.log
