@@ -833,6 +833,40 @@ __global__ void k_fd_act(mjhipModel m, Mirror mr, long ninst) {
   mjh::fwdActuation(m, d);
 }
 
+// DfDq/DfDv/DfDa (engine_derivative_fd.c:48-53) one thread per output element, the row's
+// element k fastest, so a wave's stores are contiguous (the same difference and scaling as
+// k_fd_diff, which keeps the sensor rows and DmDq)
+__global__ void k_fd_dfd(mjhipModel m, Mirror mr, int nbase, double eps, int flg_actuation,
+                         double* __restrict__ DfDq, double* __restrict__ DfDv,
+                         double* __restrict__ DfDa, int layout) {
+  const int nv = m.nv, P = 3*nv + 1;
+  const long t = (long)blockIdx.x*blockDim.x + threadIdx.x;
+  if (t >= (long)nbase*(P-1)*nv) return;
+  const int k = (int)(t % nv);
+  const long r = t / nv;
+  const long b = r / (P-1);
+  const int p = (int)(r % (P-1)) + 1;
+  double* out;
+  int i;
+  if (p <= nv) {
+    out = DfDa; i = p - 1;
+  } else if (p <= 2*nv) {
+    out = DfDv; i = p - 1 - nv;
+  } else {
+    out = DfDq; i = p - 1 - 2*nv;
+  }
+  if (!out) return;
+  const long ic = fd_inst(layout, nbase, b, 0, nv), ip = fd_inst(layout, nbase, b, p, nv);
+  Lane<64> c = lane_view(mr, (int)(ic >> 6), (int)(ic & 63));
+  Lane<64> q = lane_view(mr, (int)(ip >> 6), (int)(ip & 63));
+  double fq = q.qfrc_inverse[k], fc = c.qfrc_inverse[k];
+  if (flg_actuation) {
+    fq -= q.qfrc_actuator[k];
+    fc -= c.qfrc_actuator[k];
+  }
+  out[(b*nv + i)*nv + k] = (1/eps) * (fq - fc);
+}
+
 __global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps, int flg_actuation,
                           double* __restrict__ DfDq, double* __restrict__ DfDv,
                           double* __restrict__ DfDa, double* __restrict__ DsDq,
@@ -959,6 +993,7 @@ struct mjhipContext_ {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   const FastKernelEntry* fast = nullptr;   // straight-line kernel for this model, if any
   int* worklist = nullptr;                 // capacity + 2 ints: [count0, count1, list...]
+  int* fdflag = nullptr;                   // k_vaskip's fall-back flag (allocated on first use)
   int wl_parity = 0;                       // counter the next fast launch uses
   int wl_last = 0;                         // counter the last fast launch used
   CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
@@ -1417,6 +1452,7 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->stage);
   hipFree(c->status);
   hipFree(c->worklist);
+  hipFree(c->fdflag);
   hipFree(c->pairs);
   hipFree(c->cparams);
   hipFree(c->masks);
@@ -1979,8 +2015,13 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
                !(noskip && noskip[0] == '1');
   int rc = MJHIP_OK;
   if (layout) {
-    int* needfull = reinterpret_cast<int*>(alloc(1));
-    if (!needfull) { set_error("hipMalloc(FD flag) failed"); return MJHIP_ERR_HIP; }
+    if (!c->fdflag && hipMalloc((void**)&c->fdflag, sizeof(int)) != hipSuccess) {
+      c->fdflag = nullptr;
+      release();
+      set_error("hipMalloc(FD flag) failed");
+      return MJHIP_ERR_HIP;
+    }
+    int* needfull = c->fdflag;
     hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream,
                        c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, 1);
     HIPCHECK(hipGetLastError());
@@ -2039,8 +2080,15 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
     }
   }
   long nd = (long)B*(P-1);
-  hipLaunchKernelGGL(k_fd_diff, dim3((nd + 255)/256), dim3(256), 0, c->stream, c->dmodel,
-                     c->mirror, B, eps, flg_actuation, oq, ov, oa, sq_, sv_, sa_, om, layout);
+  if (oq || ov || oa) {
+    hipLaunchKernelGGL(k_fd_dfd, dim3((nd*nv + 255)/256), dim3(256), 0, c->stream, c->dmodel,
+                       c->mirror, B, eps, flg_actuation, oq, ov, oa, layout);
+  }
+  if (sq_ || sv_ || sa_ || om) {
+    hipLaunchKernelGGL(k_fd_diff, dim3((nd + 255)/256), dim3(256), 0, c->stream, c->dmodel,
+                       c->mirror, B, eps, flg_actuation, nullptr, nullptr, nullptr, sq_, sv_,
+                       sa_, om, layout);
+  }
   if (hipGetLastError() != hipSuccess) {
     release();
     set_error("k_fd_diff launch failed");
