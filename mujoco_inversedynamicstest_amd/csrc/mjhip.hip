@@ -993,7 +993,6 @@ struct mjhipContext_ {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   const FastKernelEntry* fast = nullptr;   // straight-line kernel for this model, if any
   int* worklist = nullptr;                 // capacity + 2 ints: [count0, count1, list...]
-  int* fdflag = nullptr;                   // k_vaskip's fall-back flag (allocated on first use)
   int wl_parity = 0;                       // counter the next fast launch uses
   int wl_last = 0;                         // counter the last fast launch used
   CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
@@ -1452,7 +1451,6 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->stage);
   hipFree(c->status);
   hipFree(c->worklist);
-  hipFree(c->fdflag);
   hipFree(c->pairs);
   hipFree(c->cparams);
   hipFree(c->masks);
@@ -2015,13 +2013,11 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
                !(noskip && noskip[0] == '1');
   int rc = MJHIP_OK;
   if (layout) {
-    if (!c->fdflag && hipMalloc((void**)&c->fdflag, sizeof(int)) != hipSuccess) {
-      c->fdflag = nullptr;
-      release();
-      set_error("hipMalloc(FD flag) failed");
-      return MJHIP_ERR_HIP;
-    }
-    int* needfull = c->fdflag;
+    // a per-call allocation: its hipFree at the end of the call drains the device, and
+    // back-to-back calls without that drain measured k_all_humanoid 131 -> 185 us
+    // (profiles/r03/fdskip)
+    int* needfull = reinterpret_cast<int*>(alloc(1));
+    if (!needfull) { set_error("hipMalloc(FD flag) failed"); return MJHIP_ERR_HIP; }
     hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream,
                        c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, 1);
     HIPCHECK(hipGetLastError());
