@@ -77,6 +77,52 @@ def pmc_traffic(eng, m, model, count):
   return None, None
 
 
+def rocprof_kernel_ms(eng, m, model):
+  """Per-dispatch average duration (ms) of the hot-path kernels from the newest committed
+  rocprofv3 --kernel-trace --stats summary (tools/rocprof_summary.py) of the same generated
+  source as this run's kernel, summed over the kernels of one launch, else (None, None)."""
+  import glob
+  from mujoco_inversedynamicstest_amd import codegen
+  if not eng.fast_kernel:
+    return None, None
+  sha = codegen.source_hash(m, eng.fast_kernel)
+  for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "rocprof_bench.json")),
+                     reverse=True):
+    rec = json.load(open(path))
+    if rec.get("model") == model and rec.get("source_sha") == sha:
+      return rec["launch_ms"], os.path.relpath(path, ROOT)
+  return None, None
+
+
+def cpu_baseline(m, args):
+  """The oracle (kind "port": the CPU restatement of the reference's mj_inverse) compiled for
+  this host's CPU at -O3 -march=native, on every core available to the process, one thread per
+  core over dynamic chunks (or_inverseBatch). One warm-up pass, then the median of five timed
+  passes over the same bounded sample (BASELINE.md's CPU plan)."""
+  from mujoco_inversedynamicstest_amd.sampler import sample_states
+  from oracle.oracle import Oracle, native_baseline_lib
+  nthread = args.cpu_threads or available_cores()
+  n = args.cpu_sample or 150_000 * nthread
+  cq, cv, ca = sample_states(m, n, first=0)
+  o = Oracle(m)
+  L, flags = native_baseline_lib()
+  warm = max(n // 10, nthread)
+  o.inverse_batch(cq[:warm], cv[:warm], ca[:warm], nthread=nthread, lib=L)
+  secs = sorted(o.inverse_batch(cq, cv, ca, nthread=nthread, lib=L)[1] for _ in range(5))
+  # the baseline build must compute what the checker build computes
+  k = min(n, 2048)
+  same = bool(np.array_equal(o.inverse_batch(cq[:k], cv[:k], ca[:k], lib=L)[0],
+                             o.inverse_batch(cq[:k], cv[:k], ca[:k])[0]))
+  med = secs[2]
+  return {"value": n / med, "unit": "evals/s", "cores": nthread, "kind": "port",
+          "sample": f"{n} humanoid states (first {n} of the same sampler stream), {nthread} "
+                    f"threads (cores available to the process: {available_cores()}, "
+                    f"os.cpu_count {os.cpu_count()}), oracle/mj_oracle.c {flags}; one warm-up "
+                    f"pass of {warm}, median of 5 passes: {med:.3f} s wall "
+                    f"(min {secs[0]:.3f}, max {secs[-1]:.3f}); bit-identical to the checker "
+                    f"build on the first {k}: {same}"}
+
+
 def timed(fn, steps, world, dist, torch, dev):
   """Run fn `steps` times between barrier + device syncs; max wall time over ranks (s)."""
   torch.cuda.synchronize(dev)
@@ -172,6 +218,9 @@ def main():
   bytes_per_eval = engine.output_bytes_per_eval(m)
   achieved = bytes_per_eval * count / (kernel_ms * 1e-3) / 1e9
   traffic, traffic_src = pmc_traffic(eng, m, args.model, count)
+  prof_ms, prof_src = rocprof_kernel_ms(eng, m, args.model)
+  if prof_ms is not None and count != 65536:
+    prof_ms = None        # the committed summary is of the 65,536 launch
 
   # every rank's full qfrc_inverse on rank 0 (outside the timed regions): a checksum of
   # checksums over the whole global batch, and a spot check of the gathered rows
@@ -185,17 +234,7 @@ def main():
 
   cpu = None
   if rank == 0 and world == 1 and not args.no_cpu:
-    from oracle.oracle import Oracle
-    nthread = args.cpu_threads or available_cores()
-    n = args.cpu_sample or 150_000 * nthread
-    cq, cv, ca = sample_states(m, n, first=0)
-    o = Oracle(m)
-    _, secs = o.inverse_batch(cq, cv, ca, nthread=nthread)
-    cpu = {"value": n / secs, "unit": "evals/s", "cores": nthread, "kind": "port",
-           "sample": f"{n} humanoid states (first {n} of the same sampler stream), "
-                     f"{nthread} threads (cores available to the process: "
-                     f"{available_cores()}, os.cpu_count {os.cpu_count()}), "
-                     f"oracle/mj_oracle.c -O2, {secs:.2f} s wall"}
+    cpu = cpu_baseline(m, args)
 
   if rank == 0:
     value = total * args.steps / elapsed
@@ -233,6 +272,10 @@ def main():
                                          "reps (rocprof's per-dispatch durations each include "
                                          "their own dispatch ramp, so their sum reads a few "
                                          "us higher)",
+                     "rocprof_kernel_ms": prof_ms,
+                     "rocprof_source": prof_src,
+                     "frac_rocprof": (bytes_per_eval * count / (prof_ms * 1e-3) / 1e9
+                                      / HBM_PEAK_GBPS if prof_ms else None),
                      "generic_kernel_ms": generic_ms,
                      "bytes_per_eval": bytes_per_eval},
         "cpu_baseline": cpu,

@@ -261,8 +261,10 @@ class _Stage:
     self.M = M
     self.E = _Emitter()
     self.store_fields = store_fields
+    self.stored = set()      # mirror fields this stage stores through (k_vaskip's own set)
 
   def st(self, field, k, expr):
+    self.stored.add(field)
     if field == "qM" and QM_FORWARD:
       self.E(f"{{ const double v_ = {expr}; if (qmr) qmr[{k}] = v_;")
       if self.store_fields is None or field in self.store_fields:
@@ -901,6 +903,7 @@ def _gen_va(M: _Model, store_fields=None) -> str:
   The two RNE recursions share cdof_dot*qvel and the gyroscopic term cvel x (cinert*cvel),
   which the reference computes identically in each call."""
   G = _Stage(M, store_fields)
+  M.va_stored = G.stored     # filled as the body is emitted; read by generate (k_vaskip)
   E, m = G.E, M.m
   nv, nq, dsbl = M.nv, M.nq, M.dsbl
   recompute = VA_RECOMPUTE and FUSE
@@ -1363,18 +1366,28 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
                  f"  const long n = ((long)B - r0 < {nl} ? (long)B - r0 : {nl}) * {M.nv};\n"
                  f"  double* dst = qfrc_out + r0*{M.nv};\n"
                  f"  for (long r = threadIdx.x; r < n; r += {nl}) dst[r] = qo_lds[r];\n")
-  bl = "blockIdx.x, threadIdx.x" if sub == 1 else \
-      f"blockIdx.x / {sub}, (blockIdx.x % {sub})*{nl} + threadIdx.x"
+  bl = "blk0 + blockIdx.x, threadIdx.x" if sub == 1 else \
+      f"blk0 + blockIdx.x / {sub}, (blockIdx.x % {sub})*{nl} + threadIdx.x"
+  fuse_tail = fuse_tail.replace("(long)blockIdx.x*", f"((long)blk0*{sub} + blockIdx.x)*")
   linkage = 'extern "C" ' if extern_c else ""
+  # range: null, or a device-side instance range {first, end} (first a multiple of 64) read
+  # at the start of the launch, so a launch's extent can be decided by an earlier kernel on
+  # the stream (mjhip_inverseFDBatch's limit-centre fall-back) without a host round trip.
+  # The next call's work-list counter is zeroed by the launch's first thread, before any
+  # instance bound, so an empty range still hands the counters on.
   out.append(f"""{linkage}__global__ __launch_bounds__({nl}, {ALL_WAVES}) void k_all_{name}(Mirror mr, int B,
     const double* __restrict__ qpos_in, const double* __restrict__ qvel_in,
     const double* __restrict__ qacc_in, double* __restrict__ qfrc_out, int* __restrict__ status,
     int* __restrict__ worklist, int* __restrict__ worklist_count, int* __restrict__ worklist_next,
-    int* __restrict__ efc_count) {{
+    int* __restrict__ efc_count, const int* __restrict__ range) {{
   __shared__ double trig[{ntrig}];
   __shared__ double qo_lds[{nqo}];
   double qmr[{max(1, m.nM)}];
-""" + "\n".join(f"  fast_{st}_{name}(mr, {bl}, B, {_SIG[st][1]});\n"
+  if (worklist_next && blockIdx.x == 0 && threadIdx.x == 0) *worklist_next = 0;
+  int blk0 = 0;
+  if (range) {{ blk0 = range[0] >> 6; B = range[1]; }}
+""" + "\n".join(f"  fast_{st}_{name}(mr, {bl}, B, "
+                f"{_SIG[st][1].replace('worklist_next', 'nullptr')});\n"
                 f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE();" for st in STAGES)
              + "\n" + fuse_tail + "}")
   # k_vaskip: the va stage of mj_inverseSkip(mjSTAGE_POS) for mjd_inverseFD's qvel and qacc
@@ -1382,14 +1395,20 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   # stage output (the va pointers it never stores) from its centre instance
   # (t / per)*sstride, which ran the full kernel; its own qvel/qacc and every field the stage
   # stores stay its own. Skipped stages see unchanged inputs, so the result is the full
-  # pipeline's bit for bit. Work-list models: a centre with limit rows sets *needfull (the
-  # caller then runs the full pipeline on every perturbation).
+  # pipeline's bit for bit. Work-list models: a centre with limit rows sets *needfull, and
+  # k_fd_gate (mjhip.hip) then opens the range of a second k_all over the qvel/qacc
+  # perturbations, which runs their full pipeline.
   if M.cmode in ("none", "list"):
     import re
     vb = bodies["va"]
-    stored = set(re.findall(r"P_(\w+)\[\d+\*64\]\)? ?=", vb)) | \
+    # the fields the va stage stores, as recorded by _Stage.st while emitting it; a store the
+    # record missed would leave that pointer based at the centre instance, and all 2nv
+    # perturbations would write the centre's slot concurrently, so the text is checked too
+    textual = set(re.findall(r"P_(\w+)\[[^\]]+\]\)? ?=[^=]", vb)) | \
         set(re.findall(r"MJH_NT_STORE\(P_(\w+)\[", vb))
-    own = {"qpos", "qvel", "qacc"} | stored
+    assert textual <= M.va_stored | {"qpos", "qvel", "qacc"}, \
+        f"k_vaskip: va stores outside the record: {textual - M.va_stored}"
+    own = {"qpos", "qvel", "qacc"} | M.va_stored
     skip_body = re.sub(r"(double\* __restrict__ P_(\w+) = mr\.\w+ \+ \(\(long\))blk(\*\d+\)\*64 \+ )lane;",
                        lambda mt: mt.group(0) if mt.group(2) in own else
                        f"{mt.group(1)}sblk{mt.group(3)}slane;", vb)
@@ -1417,12 +1436,14 @@ static void launch_vaskip_{name}(hipStream_t s, const Mirror& mr, int B, int off
 }}""")
   out.append(f"""static void launch_fast_{name}(dim3 g, dim3 b, hipStream_t s, const Mirror& mr,
     int B, const double* qpos_in, const double* qvel_in, const double* qacc_in, double* qfrc_out,
-    int* status, int* worklist, int* worklist_count, int* worklist_next, int* efc_count) {{""")
+    int* status, int* worklist, int* worklist_count, int* worklist_next, int* efc_count,
+    const int* range) {{""")
   if FUSE:
     gb = "g, b" if ALL_LANES == 64 else f"dim3(g.x*{64 // ALL_LANES}), dim3({ALL_LANES})"
     out.append(f"  hipLaunchKernelGGL(k_all_{name}, {gb}, 0, s, mr, B, qpos_in, qvel_in, qacc_in, "
-               f"qfrc_out, status, worklist, worklist_count, worklist_next, efc_count);")
-  else:
+               f"qfrc_out, status, worklist, worklist_count, worklist_next, efc_count, range);")
+  else:   # staged kernels (experiments): the whole [0, B) range only
+    out.append("  if (range) return;   // device-side ranges need k_all")
     for st in STAGES:
       args = _SIG[st][1].replace(", trig", "").replace(", qo_lds", "").replace(", qmr", ", nullptr")
       gb = "g, b" if LANES[st] == 64 else f"dim3(g.x*{64 // LANES[st]}), dim3({LANES[st]})"

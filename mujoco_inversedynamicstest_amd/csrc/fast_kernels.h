@@ -11,7 +11,8 @@
 struct FastKernelEntry {
   unsigned long long sig;
   void (*launch)(dim3, dim3, hipStream_t, const Mirror&, int, const double*, const double*,
-                 const double*, double*, int*, int*, int*, int*, int*);
+                 const double*, double*, int*, int*, int*, int*, int*,
+                 const int* /* device-side instance range {first, end}, or null */);
   const char* name;
   int cmode;   // codegen.constraint_mode: 0 none, 1 work-list, 2 every instance
   // mj_inverseSkip(mjSTAGE_POS) for mjd_inverseFD's qvel/qacc perturbations: the va stage of

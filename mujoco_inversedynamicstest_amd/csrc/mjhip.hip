@@ -766,9 +766,11 @@ __device__ static inline long fd_inst(int layout, long nbase, long b, int p, int
 
 __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __restrict__ qpos,
                             const double* __restrict__ qvel, const double* __restrict__ qacc,
-                            const double* __restrict__ ctrl, double eps, int layout) {
+                            const double* __restrict__ ctrl, double eps, int layout,
+                            int* __restrict__ fdflag) {
   const int P = 3*m.nv + 1;
   long inst = (long)blockIdx.x*blockDim.x + threadIdx.x;
+  if (fdflag && inst == 0) fdflag[0] = 0;     // k_vaskip raises it later in stream order
   if (inst >= (long)nbase*P) return;
   long b;
   int p;
@@ -819,6 +821,14 @@ __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __
   }
 }
 
+// The stage-skip fall-back of mjhip_inverseFDBatch, decided on the device: when k_vaskip
+// found a centre with limit rows (fdflag[0]), the qvel/qacc perturbations [first, end) run the
+// full pipeline as well (their own position stage and rows), else the range is empty.
+__global__ void k_fd_gate(int* __restrict__ fdflag, int first, int end) {
+  fdflag[1] = first;
+  fdflag[2] = fdflag[0] ? end : first;
+}
+
 // diff(): DfD*[b][i][:] = (f(perturbed) - f(centre)) / eps  (engine_derivative_fd.c:48-53)
 // Sensor rows follow the reference's stage skipping: a qacc perturbation runs
 // mj_inverseSkip(mjSTAGE_VEL), so only acceleration-stage sensors change and the others keep
@@ -826,6 +836,7 @@ __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __
 // mjSTAGE_POS, so position-stage sensors keep theirs (engine_derivative_fd.c:646-699).
 // flg_actuation (inverseSkip, engine_derivative_fd.c:160-168): every evaluation's force is
 // qfrc_inverse - qfrc_actuator, with mj_fwdActuation run after the inverse (k_fd_act)
+
 __global__ void k_fd_act(mjhipModel m, Mirror mr, long ninst) {
   const long inst = (long)blockIdx.x*blockDim.x + threadIdx.x;
   if (inst >= ninst) return;
@@ -995,6 +1006,9 @@ struct mjhipContext_ {
   int* worklist = nullptr;                 // capacity + 2 ints: [count0, count1, list...]
   int wl_parity = 0;                       // counter the next fast launch uses
   int wl_last = 0;                         // counter the last fast launch used
+  // mjhip_inverseFDBatch's stage-skip fall-back, decided on the device: [0] a centre has limit
+  // rows (k_vaskip), [1..2] the instance range {first, end} k_fd_gate hands to k_all
+  int* fdflag = nullptr;
   CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
   mjh::ContactParam* cparams = nullptr;    // each program pair's mj_contactParam
   unsigned long long* masks = nullptr;     // the cooperative kernel's chain masks (coop_masks)
@@ -1360,6 +1374,10 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
       hipMemset(c->worklist, 0, 2 * sizeof(int)) != hipSuccess) {
     return fail("hipMalloc(worklist)");
   }
+  if (hipMalloc((void**)&c->fdflag, 4 * sizeof(int)) != hipSuccess ||
+      hipMemset(c->fdflag, 0, 4 * sizeof(int)) != hipSuccess) {
+    return fail("hipMalloc(FD flag)");
+  }
   const char* nofast = getenv("MJHIP_DISABLE_FAST");
   c->sig = model_signature(m);
   if (!(nofast && nofast[0] == '1')) {
@@ -1451,6 +1469,7 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->stage);
   hipFree(c->status);
   hipFree(c->worklist);
+  hipFree(c->fdflag);
   hipFree(c->pairs);
   hipFree(c->cparams);
   hipFree(c->masks);
@@ -1522,10 +1541,20 @@ MJHIP_API int mjhip_contextSetStream(mjhipContext* c, void* stream) {
   return MJHIP_OK;
 }
 
+// range: null, or a device-side instance range {first, end} for the straight-line kernel (B
+// then only sizes the grid: end - first <= B); only the FD fall-back uses it, on models whose
+// whole pipeline is the straight-line and constraint kernels
 static int launch_inverse(mjhipContext* c, int B, const double* qpos, const double* qvel,
                           const double* qacc, double* qfrc, int skipstage, int* status,
-                          int flags = 0, int skipsensor = 0) {
+                          int flags = 0, int skipsensor = 0, const int* range = nullptr) {
   dim3 grid((B + 63) / 64), block(64);
+  if (range && (skipstage != mjhipSTAGE_NONE || !c->fast || (flags & MJHIP_FLAG_GENERIC) ||
+                status || qpos || qfrc || c->spatial || mjh::hasFluid(c->hmodel) ||
+                mjh::hasDiscrete(c->hmodel) || mjh_needTrnAfter(&c->hmodel) || !skipsensor ||
+                (c->hmodel.opt.enableflags & mjhipENBL_ENERGY))) {
+    set_error("launch_inverse: a device-side range needs the bare straight-line pipeline");
+    return MJHIP_ERR_ARG;
+  }
   if (skipstage == mjhipSTAGE_NONE && c->fast && !(flags & MJHIP_FLAG_GENERIC)) {
     // two work-list counters alternate: this launch counts into `cnt` (zeroed by the
     // previous launch's k_pos, or at context creation) and zeroes `nxt` for the next one
@@ -1533,13 +1562,13 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     int* nxt = c->worklist + (c->wl_parity ^ 1);
     if (c->fast->launch) {
       c->fast->launch(grid, block, c->stream, c->mirror, B, qpos, qvel, qacc, qfrc, status,
-                      c->worklist + 2, cnt, nxt, c->mirror.efc_count);
+                      c->worklist + 2, cnt, nxt, c->mirror.efc_count, range);
       HIPCHECK(hipGetLastError());
     } else {                             // run-time specialized k_all_<name> (same arguments)
       int* wl = c->worklist + 2;
       int* efc = c->mirror.efc_count;
       void* args[] = {&c->mirror, &B, &qpos, &qvel, &qacc, &qfrc, &status, &wl, &cnt, &nxt,
-                      &efc};
+                      &efc, (void*)&range};
       HIPCHECK(hipModuleLaunchKernel(c->rt_fn, grid.x, 1, 1, 64, 1, 1, 0, c->stream, args,
                                      nullptr));
     }
@@ -1963,34 +1992,47 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
   HIPCHECK(hipSetDevice(c->device));
   const bool dev = flags & MJHIP_FLAG_DEVICE_PTRS;
   const double *dq = qpos, *dv = qvel, *da = qacc, *dc = flg_actuation ? ctrl : nullptr;
-  std::vector<double*> tmp;
-  auto release = [&]() { for (double* p : tmp) hipFree(p); };
-  auto alloc = [&](size_t n) -> double* {
-    double* d = nullptr;
-    if (hipMalloc((void**)&d, (n ? n : 1)*sizeof(double)) != hipSuccess) return nullptr;
-    tmp.push_back(d);
-    return d;
-  };
+  // per-call device buffers of the host-array form (ctrl, the Jacobians); freed on every
+  // return path, after the stream has finished with them (the device-pointer form has none
+  // and returns without waiting for the device)
+  struct Scratch {
+    mjhipContext* c;
+    std::vector<double*> p;
+    ~Scratch() {
+      if (p.empty()) return;
+      hipStreamSynchronize(c->stream);
+      for (double* d : p) hipFree(d);
+    }
+    double* alloc(size_t n) {
+      double* d = nullptr;
+      if (hipMalloc((void**)&d, (n ? n : 1)*sizeof(double)) != hipSuccess) return nullptr;
+      p.push_back(d);
+      return d;
+    }
+  } tmp{c, {}};
+#define FDCHECK(expr, what)                                                                   \
+  do {                                                                                        \
+    if ((expr) != hipSuccess) {                                                               \
+      set_error("mjhip_inverseFDBatch: %s failed", what);                                    \
+      return MJHIP_ERR_HIP;                                                                   \
+    }                                                                                         \
+  } while (0)
   if (!dev) {
     double* sq = c->stage;
     double* sv = sq + (size_t)c->capacity*m.nq;
     double* sa = sv + (size_t)c->capacity*m.nv;
-    HIPCHECK(hipMemcpyAsync(sq, qpos, sizeof(double)*(size_t)B*m.nq, hipMemcpyHostToDevice,
-                            c->stream));
-    HIPCHECK(hipMemcpyAsync(sv, qvel, sizeof(double)*(size_t)B*nv, hipMemcpyHostToDevice,
-                            c->stream));
-    HIPCHECK(hipMemcpyAsync(sa, qacc, sizeof(double)*(size_t)B*nv, hipMemcpyHostToDevice,
-                            c->stream));
+    FDCHECK(hipMemcpyAsync(sq, qpos, sizeof(double)*(size_t)B*m.nq, hipMemcpyHostToDevice,
+                           c->stream), "qpos upload");
+    FDCHECK(hipMemcpyAsync(sv, qvel, sizeof(double)*(size_t)B*nv, hipMemcpyHostToDevice,
+                           c->stream), "qvel upload");
+    FDCHECK(hipMemcpyAsync(sa, qacc, sizeof(double)*(size_t)B*nv, hipMemcpyHostToDevice,
+                           c->stream), "qacc upload");
     dq = sq; dv = sv; da = sa;
     if (dc && m.nu) {
-      double* sc = alloc((size_t)B*m.nu);
+      double* sc = tmp.alloc((size_t)B*m.nu);
       if (!sc) { set_error("hipMalloc(ctrl) failed"); return MJHIP_ERR_HIP; }
-      if (hipMemcpyAsync(sc, ctrl, sizeof(double)*(size_t)B*m.nu, hipMemcpyHostToDevice,
-                         c->stream) != hipSuccess) {
-        release();
-        set_error("ctrl upload failed");
-        return MJHIP_ERR_HIP;
-      }
+      FDCHECK(hipMemcpyAsync(sc, ctrl, sizeof(double)*(size_t)B*m.nu, hipMemcpyHostToDevice,
+                             c->stream), "ctrl upload");
       dc = sc;
     }
   }
@@ -2002,59 +2044,50 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
   // (k_vaskip) over their centre's position-stage outputs. Skipped stages would see
   // unchanged inputs, so the Jacobians equal the full pipeline's bit for bit. Taken only
   // where the straight-line kernel is the whole pipeline (no post passes, sensors or
-  // actuation terms) and the position-stage block ends on a wave boundary; a work-list
-  // model whose centres have limit rows falls back to the full pipeline.
+  // actuation terms) and the position-stage block ends on a wave boundary.
   const long nA = (long)B*(nv + 1);
   const char* noskip = getenv("MJHIP_FD_NOSKIP");
-  int layout = c->fast && c->fast->launch_vaskip && !(flags & MJHIP_FLAG_GENERIC) &&
-               skipsensor && !flg_actuation && !c->spatial && !mjh::hasFluid(c->hmodel) &&
-               !mjh::hasDiscrete(c->hmodel) && !mjh_needTrnAfter(&c->hmodel) &&
-               !(m.opt.enableflags & mjhipENBL_ENERGY) && nA % 64 == 0 &&
-               !(noskip && noskip[0] == '1');
+  const int layout = c->fast && c->fast->launch_vaskip && !(flags & MJHIP_FLAG_GENERIC) &&
+                     skipsensor && !flg_actuation && !c->spatial && !mjh::hasFluid(c->hmodel) &&
+                     !mjh::hasDiscrete(c->hmodel) && !mjh_needTrnAfter(&c->hmodel) &&
+                     !(m.opt.enableflags & mjhipENBL_ENERGY) && nA % 64 == 0 &&
+                     !(noskip && noskip[0] == '1');
   int rc = MJHIP_OK;
+  hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream,
+                     c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, layout,
+                     layout ? c->fdflag : nullptr);
+  FDCHECK(hipGetLastError(), "k_fd_expand launch");
   if (layout) {
-    // a per-call allocation: its hipFree at the end of the call drains the device, and
-    // back-to-back calls without that drain measured k_all_humanoid 131 -> 185 us
-    // (profiles/r03/fdskip)
-    int* needfull = reinterpret_cast<int*>(alloc(1));
-    if (!needfull) { set_error("hipMalloc(FD flag) failed"); return MJHIP_ERR_HIP; }
-    hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream,
-                       c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, 1);
-    HIPCHECK(hipGetLastError());
+    // the nv+1 position-stage instances of every base state: the full pipeline
     rc = launch_inverse(c, (int)nA, nullptr, nullptr, nullptr, nullptr, mjhipSTAGE_NONE,
                         nullptr, 0, skipsensor);
-    if (rc) { release(); return rc; }
-    int full = 0;
-    if (hipMemsetAsync(needfull, 0, sizeof(int), c->stream) != hipSuccess) {
-      release();
-      set_error("FD flag reset failed");
-      return MJHIP_ERR_HIP;
-    }
+    if (rc) return rc;
+    // the 2nv qvel/qacc perturbations: the va stage over their centre's position stage
     c->fast->launch_vaskip(c->stream, c->mirror, (int)ninst, (int)nA, 2*nv, nv + 1,
-                           c->mirror.efc_count, needfull);
-    HIPCHECK(hipGetLastError());
+                           c->mirror.efc_count, c->fdflag);
+    FDCHECK(hipGetLastError(), "k_vaskip launch");
     if (c->fast->cmode == 1) {
-      if (hipMemcpyAsync(&full, needfull, sizeof(int), hipMemcpyDeviceToHost, c->stream) !=
-              hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
-        release();
-        set_error("FD flag read failed");
-        return MJHIP_ERR_HIP;
-      }
+      // a work-list model whose centre has limit rows: its perturbations need the rows'
+      // velocity and acceleration terms, so every qvel/qacc perturbation then runs the full
+      // pipeline over its own slot (the same layout; results as without skipping). Decided on
+      // the device: k_fd_gate turns the flag into the range k_all reads, empty when no centre
+      // has rows, so the call needs no host round trip.
+      hipLaunchKernelGGL(k_fd_gate, dim3(1), dim3(1), 0, c->stream, c->fdflag, (int)nA,
+                         (int)ninst);
+      FDCHECK(hipGetLastError(), "k_fd_gate launch");
+      rc = launch_inverse(c, (int)(ninst - nA), nullptr, nullptr, nullptr, nullptr,
+                          mjhipSTAGE_NONE, nullptr, 0, skipsensor, c->fdflag + 1);
+      if (rc) return rc;
     }
-    if (full) layout = 0;
-  }
-  if (!layout) {
-    hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream,
-                       c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, 0);
-    HIPCHECK(hipGetLastError());
+  } else {
     rc = launch_inverse(c, (int)ninst, nullptr, nullptr, nullptr, nullptr, mjhipSTAGE_NONE,
                         nullptr, 0, skipsensor);
-    if (rc) { release(); return rc; }
+    if (rc) return rc;
   }
   if (flg_actuation) {
     hipLaunchKernelGGL(k_fd_act, dim3((ninst + 255)/256), dim3(256), 0, c->stream, c->dmodel,
                        c->mirror, ninst);
-    HIPCHECK(hipGetLastError());
+    FDCHECK(hipGetLastError(), "k_fd_act launch");
   }
   double *oq = DfDq, *ov = DfDv, *oa = DfDa, *om = DmDq;
   double *sq_ = DsDq, *sv_ = DsDv, *sa_ = DsDa;
@@ -2063,14 +2096,13 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
     bool ok = true;
     auto dalloc = [&](double* h, size_t n) -> double* {
       if (!h) return nullptr;
-      double* d = alloc(n);
+      double* d = tmp.alloc(n);
       ok = ok && d;
       return d;
     };
     oq = dalloc(DfDq, nn); ov = dalloc(DfDv, nn); oa = dalloc(DfDa, nn); om = dalloc(DmDq, nm);
     sq_ = dalloc(DsDq, ns); sv_ = dalloc(DsDv, ns); sa_ = dalloc(DsDa, ns);
     if (!ok) {
-      release();
       set_error("hipMalloc(FD outputs) failed");
       return MJHIP_ERR_HIP;
     }
@@ -2085,28 +2117,16 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
                        c->mirror, B, eps, flg_actuation, nullptr, nullptr, nullptr, sq_, sv_,
                        sa_, om, layout);
   }
-  if (hipGetLastError() != hipSuccess) {
-    release();
-    set_error("k_fd_diff launch failed");
-    return MJHIP_ERR_HIP;
-  }
+  FDCHECK(hipGetLastError(), "k_fd_diff launch");
   if (!dev) {
-    bool ok = true;
     auto get = [&](double* h, const double* d, size_t n) {
-      if (h) ok = ok && hipMemcpyAsync(h, d, n*8, hipMemcpyDeviceToHost, c->stream) == hipSuccess;
+      return !h || hipMemcpyAsync(h, d, n*8, hipMemcpyDeviceToHost, c->stream) == hipSuccess;
     };
-    get(DfDq, oq, nn); get(DfDv, ov, nn); get(DfDa, oa, nn); get(DmDq, om, nm);
-    get(DsDq, sq_, ns); get(DsDv, sv_, ns); get(DsDa, sa_, ns);
-    ok = ok && hipStreamSynchronize(c->stream) == hipSuccess;
-    release();
-    if (!ok) {
-      set_error("FD output download failed");
-      return MJHIP_ERR_HIP;
-    }
-  } else if (!tmp.empty()) {
-    HIPCHECK(hipStreamSynchronize(c->stream));
-    release();
+    bool ok = get(DfDq, oq, nn) && get(DfDv, ov, nn) && get(DfDa, oa, nn) && get(DmDq, om, nm) &&
+              get(DsDq, sq_, ns) && get(DsDv, sv_, ns) && get(DsDa, sa_, ns);
+    FDCHECK(ok ? hipStreamSynchronize(c->stream) : hipErrorUnknown, "FD output download");
   }
+#undef FDCHECK
   return MJHIP_OK;
 }
 

@@ -234,13 +234,33 @@ class Oracle:
       return DfDq, DfDv, DfDa, DmDq, tuple(x[:, :ns] for x in Ds)
     return DfDq, DfDv, DfDa, DmDq
 
-  def inverse_batch(self, qpos, qvel, qacc, nthread=1):
-    """CPU baseline over B instances; returns (qfrc_inverse [B, nv], seconds)."""
+  def inverse_batch(self, qpos, qvel, qacc, nthread=1, lib=None):
+    """CPU baseline over B instances; returns (qfrc_inverse [B, nv], seconds). lib: another
+    build of the same source (native_baseline_lib()), default the checker build."""
     qpos = np.ascontiguousarray(qpos, dtype=np.float64)
     qvel = np.ascontiguousarray(qvel, dtype=np.float64)
     qacc = np.ascontiguousarray(qacc, dtype=np.float64)
     B = qpos.shape[0]
     out = np.zeros((B, self.m.nv))
-    t = self.L.or_inverseBatch(ctypes.byref(self.cm), B, _p(qpos), _p(qvel), _p(qacc),
-                               _p(out), nthread)
+    L = lib or self.L
+    t = L.or_inverseBatch(ctypes.byref(self.cm), B, _p(qpos), _p(qvel), _p(qacc), _p(out),
+                          nthread)
     return out, t
+
+
+def native_baseline_lib():
+  """The oracle compiled for THIS host's CPU (-O3 -march=native, BASELINE.md's CPU plan) into
+  a temporary directory, for bench.py's cpu_baseline leg only. ISO C mode keeps gcc from
+  contracting multiply-adds, so the arithmetic is the checker build's; only the instruction
+  selection and scheduling differ. Built where it runs (the GPU box's host CPU may not be this
+  container's), about 6 s. Returns (ctypes library, compiler flags)."""
+  import tempfile
+  flags = ["-std=c11", "-O3", "-march=native", "-ffp-contract=off", "-fPIC", "-shared"]
+  out = os.path.join(tempfile.mkdtemp(prefix="oracle_native_"), "liboracle_native.so")
+  subprocess.run([os.environ.get("CC", "gcc"), *flags, "-o", out,
+                  os.path.join(_HERE, "mj_oracle.c"), "-lm", "-lpthread"], check=True)
+  L = ctypes.CDLL(out)
+  L.or_inverseBatch.argtypes = [ctypes.POINTER(fields.CModel), ctypes.c_int, _D, _D, _D, _D,
+                                ctypes.c_int]
+  L.or_inverseBatch.restype = ctypes.c_double
+  return L, " ".join(flags)

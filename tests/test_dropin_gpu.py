@@ -30,6 +30,10 @@ def close(gpu, cpu, what, rtol=RTOL):
 
 
 def _states(m, kind, n):
+  if kind == "slider_crank":     # BASELINE config 1's model: uniform crank/slider states
+    rng = np.random.default_rng(31)
+    return (rng.uniform(-np.pi, np.pi, (n, m.nq)), rng.normal(size=(n, m.nv)),
+            rng.normal(size=(n, m.nv)))
   if kind == "limits":
     return sample_states(m, n, first=5000, margin=-0.25, resample_tendons=False)
   return sample_contact_states(m, n, first=700)
@@ -44,12 +48,19 @@ def _forward_state(o, m, q, v, a, rng):
   o.d.qfrc_constraint[:] += 1e-3 * (rng.random(m.nv) - 0.5)   # unconverged forward solve
 
 
-@pytest.mark.parametrize("kind", ["limits", "contacts"])
+def _model(kind):
+  if kind == "slider_crank":
+    return models.load("slider_crank")
+  return models.load("humanoid", disable_contact=(kind == "limits"))
+
+
+@pytest.mark.parametrize("kind", ["limits", "contacts", "slider_crank"])
 def test_inverse_test_loop_constrained(kind, rng):
   """inverse_test.cpp:43-112 with the GPU mj_compareFwdInv / mj_inverseSkip(VEL, 1) on the
-  humanoid, limit rows active (config 2 with margin -0.25) and contacts on (config 4)."""
-  m = models.load("humanoid", disable_contact=(kind == "limits"))
-  n = 40
+  humanoid, limit rows active (config 2 with margin -0.25) and contacts on (config 4), and on
+  BASELINE config 1's slider_crank.xml (its capsule-cylinder contact rows on GJK/EPA)."""
+  m = _model(kind)
+  n = 64 if kind == "slider_crank" else 40
   q, v, a = _states(m, kind, n)
   o = Oracle(m)
   d = host.MjData(m)
@@ -78,7 +89,7 @@ def test_inverse_test_loop_constrained(kind, rng):
     close(d.efc("efc_force"), o.efc_field("efc_force"), f"efc_force {i}")
     np.testing.assert_array_equal(d.efc("efc_state").ravel(), o.efc_field("efc_state"))
     assert d.status == 0
-  assert rows > n
+  assert rows > (n // 4 if kind == "slider_crank" else n)
 
 
 @pytest.mark.parametrize("kind", ["limits", "contacts"])

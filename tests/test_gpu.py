@@ -194,18 +194,20 @@ def test_inverse_fd_parity(humanoid):
     np.testing.assert_allclose(DmDq[i], rm, rtol=1e-5, atol=1e-5)
 
 
-@pytest.mark.parametrize("NB,limits", [(1024, False), (64, True), (3, False)])
+@pytest.mark.parametrize("NB,limits", [(1024, "none"), (64, "all"), (64, "some"),
+                                       (3, "none")])
 def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
   """mjd_inverseFD's stage skipping (engine_derivative_fd.c:646-699: the qvel and qacc
   perturbations run mj_inverseSkip(mjSTAGE_POS), here the generated va stage over the
   centre's position-stage outputs) equals every perturbation through the full pipeline
   (MJHIP_FD_NOSKIP=1) bit for bit. NB=1024 takes the skip layout; with joint limits active
-  on the centres the work-list model falls back to the full pipeline; NB=3 (28*3 instances,
-  not a whole wave) never takes it."""
+  on every centre, or on every fifth, the work-list model falls back on the device to the full
+  pipeline over the perturbations; NB=3 (28*3 instances, not a whole wave) never takes it."""
   q, v, a = sample_states(humanoid, NB, first=300)
-  if limits:                            # push a limited hinge past its range on every state
+  if limits != "none":                  # push a limited hinge past its range
     j = int(np.flatnonzero(np.asarray(humanoid.jnt_limited))[3])
-    q[:, humanoid.jnt_qposadr[j]] = humanoid.jnt_range[j][1] + 0.2
+    rows = slice(None) if limits == "all" else slice(None, None, 5)
+    q[rows, humanoid.jnt_qposadr[j]] = humanoid.jnt_range[j][1] + 0.2
   e = engine.InverseEngine(humanoid, capacity=NB * (3 * humanoid.nv + 1))
   try:
     got = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
@@ -215,6 +217,41 @@ def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
     e.close()
   for g, r in zip(got, ref):
     assert np.array_equal(g, r)
+
+
+@pytest.mark.parametrize("name", ["inverse_test", "linear", "inertia"])
+def test_inverse_fd_stage_skip_other_models(name, monkeypatch):
+  """The stage-skip layout on the other bundled models with a k_vaskip kernel (work-list or
+  row-free), device-resident and back to back (no host wait between calls), against the full
+  pipeline bit for bit and the oracle's serial mjd_inverseFD."""
+  import torch
+  m = models.load(name, disable_contact=True, disable_sensor=(name == "linear"))
+  NB = 64
+  q, v, a = sample_states(m, NB, first=40)
+  e = engine.InverseEngine(m, capacity=NB * (3 * m.nv + 1))
+  try:
+    assert e.fast_kernel == name
+    t = lambda x: torch.from_numpy(np.ascontiguousarray(x)).cuda()
+    tq, tv, ta = t(q), t(v), t(a)
+    outs = [e.inverse_fd(tq, tv, ta, eps=1e-6) for _ in range(3)]
+    torch.cuda.synchronize()
+    got = [x.cpu().numpy() for x in outs[-1][:3]]
+    for o in outs[:-1]:
+      for x, y in zip(o[:3], got):
+        assert np.array_equal(x.cpu().numpy(), y)
+    monkeypatch.setenv("MJHIP_FD_NOSKIP", "1")
+    ref = e.inverse_fd(q, v, a, eps=1e-6)
+  finally:
+    e.close()
+  for g, r in zip(got, ref[:3]):
+    assert np.array_equal(g, r)
+  o = Oracle(m)
+  for i in range(0, NB, 8):
+    o.set_state(q[i], v[i], a[i])
+    rq, rv, ra, _ = o.inverse_fd(1e-6)
+    np.testing.assert_allclose(got[2][i], ra, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(got[1][i], rv, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(got[0][i], rq, rtol=1e-5, atol=1e-4)
 
 
 def test_inverse_fd_device_tensors(humanoid, eng):

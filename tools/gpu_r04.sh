@@ -1,0 +1,37 @@
+#!/bin/bash
+# Round-4 GPU steps, chosen by name: tests (a pytest -k filter in PYTEST_K), bench, c4, c5
+# (config 5 under a rocprofv3 kernel trace), prof (rocprof stats of the bench + PMC passes).
+#   bash tools/gpu_r04.sh tests bench c5
+set -u
+cd "${GRAFT_REPO_ROOT:-$(pwd)}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+for step in "$@"; do
+  echo "== $step"
+  case $step in
+    tests)
+      timeout -k 10 900 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests \
+        -m gpu ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1 \
+        || { tail -40 gpurun_out/pytest_gpu.log; exit 1; }
+      tail -3 gpurun_out/pytest_gpu.log ;;
+    bench)
+      timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || exit 1
+      cat gpurun_out/bench.json ;;
+    c4)
+      timeout -k 10 120 python bench.py --config 4 --steps 20 --warmup 3 > gpurun_out/c4.json 2>&1 || exit 1
+      tail -1 gpurun_out/c4.json ;;
+    c5)
+      timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o c5 \
+        --output-format csv -- python bench.py --config 5 --steps 20 --warmup 3 \
+        > gpurun_out/c5.json 2> gpurun_out/c5.err || exit 1
+      tail -1 gpurun_out/c5.json
+      find gpurun_out/prof_c5 -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-150 ;;
+    c5plain)
+      timeout -k 10 120 python bench.py --config 5 --steps 20 --warmup 3 > gpurun_out/c5plain.json 2>&1 || exit 1
+      tail -1 gpurun_out/c5plain.json ;;
+    prof)
+      bash tools/gpu_profile.sh || exit 1 ;;
+    *)
+      echo "unknown step $step"; exit 2 ;;
+  esac
+done
