@@ -15,8 +15,8 @@
  * when it passes the static rules below. mj_collision processes candidates in signature
  * order ((b1 << 16) + b2, b1 < b2); mjhip_pairMaxContacts bounds each primitive pair.
  *
- * A candidate pair whose collision function is not implemented here (meshes, height fields,
- * SDFs; mjc_Convex with the libccd fallback or MULTICCD) adds no capacity. At run time it goes through the
+ * A candidate pair whose collision function is not implemented here (SDFs; mjc_Convex and
+ * height fields with the libccd fallback, MULTICCD's extra contacts) adds no capacity. At run time it goes through the
  * same bitmask and bounding-sphere filters as the reference (mj_collideGeoms :1470-1497);
  * an instance where one survives them is flagged MJHIP_INST_UNSUPPORTED instead of getting
  * contacts, so every unflagged instance is exact.
@@ -85,10 +85,11 @@ MJHIP_CONTACT_HD int mjhip_bodyPairCandidate(const mjhipModel* m, int b1, int b2
 
 /* pairs mjCOLLISIONFUNC serves with mjc_Convex (engine_collision_driver.c:41-52) among the
  * geom types built here: sphere-ellipsoid, capsule-ellipsoid/cylinder, ellipsoid and cylinder
- * pairs among themselves and with boxes (type-ordered t1 <= t2) */
+ * pairs among themselves and with boxes, and every primitive or mesh with a mesh
+ * (type-ordered t1 <= t2) */
 MJHIP_CONTACT_HD int mjhip_isConvexPair(int t1, int t2) {
   if (t1 == mjhipGEOM_PLANE || t1 == mjhipGEOM_HFIELD) return 0;
-  if (t2 == mjhipGEOM_ELLIPSOID) return 1;
+  if (t2 == mjhipGEOM_ELLIPSOID || t2 == mjhipGEOM_MESH) return 1;
   if (t2 == mjhipGEOM_CYLINDER) {
     return t1 == mjhipGEOM_CAPSULE || t1 == mjhipGEOM_ELLIPSOID || t1 == mjhipGEOM_CYLINDER;
   }
@@ -101,8 +102,14 @@ MJHIP_CONTACT_HD int mjhip_isConvexPair(int t1, int t2) {
  * function that this engine does not implement. mjc_Convex runs the native GJK/EPA solver
  * for one contact (mjc_CCDIteration, engine_collision_convex.c:792-819); with the libccd MPR
  * fallback (mjDSBL_NATIVECCD) or MULTICCD's perturbed extra contacts (pairs without a
- * sphere or an ellipsoid, :936-999) it is not built here. */
+ * sphere or an ellipsoid, :936-999) it is not built here. mjc_PlaneConvex gives a mesh up to
+ * maxplanemesh = 3 contacts (:1006), mjc_ConvexHField up to mjMAXCONPAIR = 50 (one per prism,
+ * mjhip_geomPairMaxContacts bounds it by the field's grid). */
 MJHIP_CONTACT_HD int mjhip_pairMaxContacts(const mjhipModel* m, int t1, int t2) {
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_MESH) return 3;
+  if (t1 == mjhipGEOM_HFIELD && t2 >= mjhipGEOM_SPHERE && t2 <= mjhipGEOM_MESH) {
+    return (m->opt.disableflags & mjhipDSBL_NATIVECCD) ? -1 : 50;
+  }
   if (mjhip_isConvexPair(t1, t2)) {
     if (m->opt.disableflags & mjhipDSBL_NATIVECCD) return -1;
     if ((m->opt.enableflags & mjhipENBL_MULTICCD) && t1 != mjhipGEOM_SPHERE &&
@@ -126,6 +133,24 @@ MJHIP_CONTACT_HD int mjhip_pairMaxContacts(const mjhipModel* m, int t1, int t2) 
   if (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX) return 24;   /* mjc_BoxBox's most */
   if (t1 == mjhipGEOM_HFIELD && t2 <= mjhipGEOM_HFIELD) return 0;
   return -1;
+}
+
+/* pairs whose function runs the native GJK/EPA solver (mjc_Convex, mjc_ConvexHField) */
+MJHIP_CONTACT_HD int mjhip_pairUsesCcd(int t1, int t2) {
+  return mjhip_isConvexPair(t1, t2) ||
+         (t1 == mjhipGEOM_HFIELD && t2 >= mjhipGEOM_SPHERE && t2 <= mjhipGEOM_MESH);
+}
+
+/* mjhip_pairMaxContacts for type-ordered geoms g1, g2: a height field's bound is one contact
+ * per triangular prism of its grid, at most 50 */
+MJHIP_CONTACT_HD int mjhip_geomPairMaxContacts(const mjhipModel* m, int g1, int g2) {
+  const int k = mjhip_pairMaxContacts(m, m->geom_type[g1], m->geom_type[g2]);
+  if (k > 0 && m->geom_type[g1] == mjhipGEOM_HFIELD) {
+    const int h = m->geom_dataid[g1];
+    const int n = 2*(m->hfield_nrow[h] - 1)*(m->hfield_ncol[h] - 1);
+    return n < k ? n : k;
+  }
+  return k;
 }
 
 /* condim of a geom pair (mj_contactParam: higher priority wins, else the max) */
@@ -161,7 +186,7 @@ MJHIP_CONTACT_HD int mjhip_contactCapacity(const mjhipModel* m, int* rows) {
         for (int j = 0; j < m->body_geomnum[b2]; j++) {
           int g1 = m->body_geomadr[b1] + i, g2 = m->body_geomadr[b2] + j;
           if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
-          int k = mjhip_pairMaxContacts(m, m->geom_type[g1], m->geom_type[g2]);
+          int k = mjhip_geomPairMaxContacts(m, g1, g2);
           if (k == 0) continue;
           if (mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
                                   m->geom_contype[g2], m->geom_conaffinity[g2])) {

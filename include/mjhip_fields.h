@@ -43,7 +43,13 @@
   XS(nsensor)     \
   XS(nsensordata) \
   XS(neq)         \
-  XS(nmat)
+  XS(nmat)        \
+  XS(nmesh)       \
+  XS(nmeshvert)   \
+  XS(nmeshface)   \
+  XS(nmeshgraph)  \
+  XS(nhfield)     \
+  XS(nhfielddata)
 
 /* model arrays that live in mjModel in the reference (mjxmacro.h MJMODEL_POINTERS) */
 #define MJHIP_MODEL_POINTERS_M \
@@ -120,6 +126,7 @@
   X(mjtNum,  geom_fluid,           ngeom,     12) \
   X(mjtNum,  geom_margin,          ngeom,     1) \
   X(mjtNum,  geom_gap,             ngeom,     1) \
+  X(int,     geom_dataid,          ngeom,     1) \
   X(int,     geom_matid,           ngeom,     1) \
   X(float,   geom_rgba,            ngeom,     4) \
   X(int,     site_type,            nsite,     1) \
@@ -202,6 +209,19 @@
   X(int,     sensor_adr,           nsensor,   1) \
   X(mjtNum,  sensor_cutoff,        nsensor,   1) \
   X(float,   mat_rgba,             nmat,      4) \
+  X(int,     mesh_vertadr,         nmesh,     1) \
+  X(int,     mesh_vertnum,         nmesh,     1) \
+  X(int,     mesh_faceadr,         nmesh,     1) \
+  X(int,     mesh_facenum,         nmesh,     1) \
+  X(int,     mesh_graphadr,        nmesh,     1) \
+  X(float,   mesh_vert,            nmeshvert, 3) \
+  X(int,     mesh_face,            nmeshface, 3) \
+  X(int,     mesh_graph,           nmeshgraph, 1) \
+  X(mjtNum,  hfield_size,          nhfield,   4) \
+  X(int,     hfield_nrow,          nhfield,   1) \
+  X(int,     hfield_ncol,          nhfield,   1) \
+  X(int,     hfield_adr,           nhfield,   1) \
+  X(float,   hfield_data,          nhfielddata, 1) \
   X(mjtNum,  key_qpos,             nkey,      MJ_M(nq))
 
 /* model-constant sparse structures that live in mjData in the reference

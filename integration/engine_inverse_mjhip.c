@@ -44,6 +44,19 @@ static const char* adapter_unsupported(const mjModel* m) {
   if (m->npair) return "explicit contact pairs (<contact><pair>)";
   if (m->nflex) return "flexes";
   if (m->nplugin) return "plugins";
+  for (int i = 0; i < m->nu; i++) {
+    /* mjd_actuator_vel reads mjData.act for these (engine_derivative.c:855-863) */
+    if (m->actuator_dyntype[i] != mjDYN_NONE && m->actuator_gaintype[i] == mjGAIN_AFFINE &&
+        m->actuator_gainprm[mjNGAIN*i + 2] != 0) {
+      return "an affine velocity gain with activation dynamics";
+    }
+    if (m->actuator_gaintype[i] >= mjGAIN_MUSCLE || m->actuator_biastype[i] >= mjBIAS_MUSCLE) {
+      return "muscle or user actuator gain/bias";
+    }
+  }
+  for (int i = 0; i < m->ngeom; i++) {
+    if (m->geom_type[i] == mjGEOM_SDF) return "SDF geoms";
+  }
   return NULL;
 }
 

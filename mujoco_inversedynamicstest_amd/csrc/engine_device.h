@@ -104,7 +104,8 @@ MJH_HD int mjh_needSliderCrank(const mjhipModel* m) {
   }
   return 0;
 }
-// 1 when a candidate geom pair of the model runs mjc_Convex's native GJK/EPA solver: its
+// 1 when a candidate geom pair of the model runs the native GJK/EPA solver (mjc_Convex,
+// mjc_ConvexHField): its
 // per-instance scratch (mjh::CcdMem) is allocated, 6 ccd_iterations + 6 faces
 MJH_HD int mjh_needConvex(const mjhipModel* m) {
   if (!mjhip_contactsEnabled(m)) return 0;
@@ -116,7 +117,7 @@ MJH_HD int mjh_needConvex(const mjhipModel* m) {
           int g1 = m->body_geomadr[b1] + i, g2 = m->body_geomadr[b2] + j;
           if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
           const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
-          if (mjhip_isConvexPair(t1, t2) && mjhip_pairMaxContacts(m, t1, t2) > 0 &&
+          if (mjhip_pairUsesCcd(t1, t2) && mjhip_pairMaxContacts(m, t1, t2) > 0 &&
               !mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
                                    m->geom_contype[g2], m->geom_conaffinity[g2])) {
             return 1;
@@ -184,6 +185,17 @@ MJH_HD int mjh_implicit(const mjhipModel* m) {
   return (m->opt.enableflags & mjhipENBL_INVDISCRETE) && m->opt.integrator == mjhipINT_IMPLICIT;
 }
 
+// 1 when mj_discreteAcc's qDeriv has fluid terms (mjd_passive_vel engine_derivative.c:1494-1513
+// under the implicit or implicitfast integrator): qDeriv is then held on the D sparsity, and
+// Dtmp holds the local 6 x nv Jacobian of each fluid body or geom
+MJH_HD int mjh_fluidDeriv(const mjhipModel* m) {
+  return (m->opt.enableflags & mjhipENBL_INVDISCRETE) &&
+         (m->opt.integrator == mjhipINT_IMPLICIT || m->opt.integrator == mjhipINT_IMPLICITFAST) &&
+         !(m->opt.disableflags & mjhipDSBL_PASSIVE) &&
+         (m->opt.viscosity > 0 || m->opt.density > 0);
+}
+MJH_HD int mjh_qDerivStored(const mjhipModel* m) { return mjh_implicit(m) || mjh_fluidDeriv(m); }
+
 namespace mjh {
 
 constexpr double MINVAL = mjhipMINVAL;
@@ -224,13 +236,13 @@ struct SP {
   XSC(body_vel, mjh_needSubtreeVel(m)*6*m->nbody)       \
   XSC(cfrc_int, mjh_needRnePost(m)*6*m->nbody)          \
   XSC(cfrc_ext, mjh_needRnePost(m)*6*m->nbody)          \
-  XSC(qDeriv, mjh_implicit(m)*m->nD)  \
+  XSC(qDeriv, mjh_qDerivStored(m)*m->nD)  \
   XSC(qLU, mjh_implicit(m)*m->nD)     \
   XSC(Dcvel, mjh_implicit(m)*6*m->nB) \
   XSC(Dcacc, mjh_implicit(m)*6*m->nB) \
   XSC(Dcfrc, mjh_implicit(m)*6*m->nB) \
   XSC(Dcdofdot, mjh_implicit(m)*6*m->nD) \
-  XSC(Dtmp, mjh_implicit(m)*6*nv)     \
+  XSC(Dtmp, mjh_qDerivStored(m)*6*nv) \
   XSC(efc_J, efc_cap*nv)              \
   XSC(efc_pos, efc_cap)               \
   XSC(efc_margin, efc_cap)            \
@@ -1777,6 +1789,14 @@ enum { CCD_POINT = 100, CCD_LINE = 101 };   // the shrunken sphere / capsule sup
 struct CcdShape {
   int kind, gtype;                          // support in use, the geom's own type
   double pos[3], mat[9], size[3], margin;
+  // mesh geoms: the mesh's float vertices and convex-hull graph (null: none), and the warm
+  // starts the supports keep between calls (mjCCDObj.vertindex / meshindex)
+  const float* vert;
+  const int* graph;
+  int nvert, vertindex, meshindex;
+  // a height-field prism (mjCCDObj.prism): its three corners' x, y, their top z and the
+  // common bottom z (the reference's six vertices share x, y and the bottom z)
+  double px[3], py[3], pzt[3], pzb;
 };
 
 template <int S>
@@ -1806,8 +1826,90 @@ MJH_HD void ccdToGlobal(double r[3], const double mat[9], const double t[3],
   r[2] += pos[2];
 }
 
+// dot product between double and float (convex.c:332-334)
+MJH_HD double ccdDot3f(const double a[3], const float* b) {
+  return a[0]*(double)b[0] + a[1]*(double)b[1] + a[2]*(double)b[2];
+}
+
+// mjc_meshSupport (convex.c:339-382, exhaustive) and mjc_hillclimbSupport (:387-433), as
+// mjc_initCCDObj (:735-743) picks them: hill climbing on the hull graph from
+// mjMESH_HILLCLIMB_MIN (10) vertices
+MJH_HD void ccdMeshSupport(double r[3], CcdShape& s, const double dir[3]) {
+  double ld[3], t[3];
+  mulMatTVec3(ld, s.mat, dir);
+  const float* V = s.vert;
+  int imax;
+  if (!s.graph || s.nvert < 10) {
+    double mx = -3.40282346638528859811704183484516925e+38;   // -FLT_MAX
+    imax = 0;
+    if (s.vertindex >= 0) {
+      imax = s.vertindex;
+      mx = ccdDot3f(ld, V + 3*imax);
+    }
+    for (int i = 0; i < s.nvert; i++) {
+      const double vdot = ccdDot3f(ld, V + 3*i);
+      if (vdot > mx) {
+        mx = vdot;
+        imax = i;
+      }
+    }
+    s.vertindex = imax;
+  } else {
+    const int numvert = s.graph[0];
+    const int* edgeadr = s.graph + 2;
+    const int* globalid = s.graph + 2 + numvert;
+    const int* localid = s.graph + 2 + 2*numvert;
+    double mx = -3.40282346638528859811704183484516925e+38;   // -FLT_MAX
+    int prev;
+    imax = s.meshindex < 0 ? 0 : s.meshindex;
+    do {
+      prev = imax;
+      for (int i = edgeadr[imax]; localid[i] >= 0; i++) {
+        const double vdot = ccdDot3f(ld, V + 3*globalid[localid[i]]);
+        if (vdot > mx) {
+          mx = vdot;
+          imax = localid[i];
+        }
+      }
+    } while (imax != prev);
+    s.meshindex = imax;
+    imax = globalid[imax];
+    s.vertindex = imax;
+  }
+  t[0] = (double)V[3*imax];
+  t[1] = (double)V[3*imax + 1];
+  t[2] = (double)V[3*imax + 2];
+  ccdToGlobal(r, s.mat, t, s.pos);
+}
+
+// mjc_prism_support (convex.c:438-455): the best of the three vertices of the half (bottom
+// for dir.z < 0, else top), the first on ties, by mju_dot3 of the vertex and dir
+MJH_HD void ccdPrismSupport(double r[3], const CcdShape& s, const double dir[3]) {
+  const bool bot = dir[2] < 0;
+  double z0 = bot ? s.pzb : s.pzt[0];
+  double best = s.px[0]*dir[0] + s.py[0]*dir[1] + z0*dir[2];
+  double bx = s.px[0], by = s.py[0], bz = z0;
+  for (int i = 1; i < 3; i++) {
+    const double z = bot ? s.pzb : s.pzt[i];
+    const double tmp = s.px[i]*dir[0] + s.py[i]*dir[1] + z*dir[2];
+    if (tmp > best) {
+      best = tmp;
+      bx = s.px[i]; by = s.py[i]; bz = z;
+    }
+  }
+  r[0] = bx; r[1] = by; r[2] = bz;
+}
+
 // the native support functions (convex.c:146-327), unit direction
-MJH_HD void ccdSupport1(double r[3], const CcdShape& s, const double dir[3]) {
+MJH_HD void ccdSupport1(double r[3], CcdShape& s, const double dir[3]) {
+  if (s.kind == mjhipGEOM_MESH) {
+    ccdMeshSupport(r, s, dir);
+    return;
+  }
+  if (s.kind == mjhipGEOM_HFIELD) {
+    ccdPrismSupport(r, s, dir);
+    return;
+  }
   if (s.kind == CCD_POINT) {
     r[0] = s.pos[0]; r[1] = s.pos[1]; r[2] = s.pos[2];
     return;
@@ -1862,7 +1964,7 @@ MJH_HD void ccdSupport1(double r[3], const CcdShape& s, const double dir[3]) {
 
 // support (gjk.c:277-296) into a 9-double vertex: each shape inflated by half its margin
 template <class V>
-MJH_HD void ccdSupport(V v, const CcdShape& a, const CcdShape& b, const double dir[3],
+MJH_HD void ccdSupport(V v, CcdShape& a, CcdShape& b, const double dir[3],
                        const double ndir[3]) {
   double p1[3], p2[3];
   ccdSupport1(p1, a, dir);
@@ -2107,7 +2209,7 @@ MJH_HD int ccdPick(int o0, int o1, int o2, int o3, int k) {
 
 // gjkIntersect (gjk.c:393-448): 1 contact, 0 none, -1 inconclusive
 template <int S>
-MJH_HD int ccdIntersect(CcdState& st, const CcdMem<S>& M, const CcdShape& A, const CcdShape& B) {
+MJH_HD int ccdIntersect(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B) {
   for (int q = 0; q < 4; q++) ccdCopyV(M.wrk(q), M.sim(q));
   int o0 = 0, o1 = 1, o2 = 2, o3 = 3;
   int k = st.iters;
@@ -2155,13 +2257,17 @@ MJH_HD int ccdIntersect(CcdState& st, const CcdMem<S>& M, const CcdShape& A, con
 
 // gjk (gjk.c:163-272)
 template <int S>
-MJH_HD void ccdGjk(CcdState& st, const CcdMem<S>& M, const CcdShape& A, const CcdShape& B) {
+MJH_HD void ccdGjk(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B) {
   const int get_dist = st.cutoff > 0;
   int backup = !get_dist, n = 0, k = 0;
   double x[3], l0 = 1, l1 = 0, l2 = 0, l3 = 0;
   const double cut2 = st.cutoff*st.cutoff;
-  const bool discrete = A.margin == 0 && B.margin == 0 && A.gtype == mjhipGEOM_BOX &&
-                        B.gtype == mjhipGEOM_BOX;
+  // discreteGeoms (gjk.c:150-158)
+  const bool dA = A.gtype == mjhipGEOM_BOX || A.gtype == mjhipGEOM_MESH ||
+                  A.gtype == mjhipGEOM_HFIELD;
+  const bool dB = B.gtype == mjhipGEOM_BOX || B.gtype == mjhipGEOM_MESH ||
+                  B.gtype == mjhipGEOM_HFIELD;
+  const bool discrete = A.margin == 0 && B.margin == 0 && dA && dB;
   const double eps = discrete ? 0 : st.tol*st.tol;
   sub3(x, st.x1, st.x2);
   for (; k < st.kmax; k++) {
@@ -2276,7 +2382,7 @@ MJH_HD int ccdAddVertex(const CcdMem<S>& M, CcdPoly& P, SP<S> v) {
 
 // epaSupport (:328-353)
 template <int S>
-MJH_HD int ccdNewVertex(const CcdMem<S>& M, CcdPoly& P, const CcdShape& A, const CcdShape& B,
+MJH_HD int ccdNewVertex(const CcdMem<S>& M, CcdPoly& P, CcdShape& A, CcdShape& B,
                         const double d[3], double dn) {
   double dir[3] = {1, 0, 0}, ndir[3] = {-1, 0, 0};
   if (dn > MINVAL) {
@@ -2371,8 +2477,8 @@ MJH_HD int ccdOnTriangle(const double a[3], const double b[3], const double c[3]
 
 // polytope3 (:1040-1117)
 template <int S>
-MJH_HD int ccdFromTriangle(const CcdMem<S>& M, CcdPoly& P, CcdState& st, const CcdShape& A,
-                           const CcdShape& B) {
+MJH_HD int ccdFromTriangle(const CcdMem<S>& M, CcdPoly& P, CcdState& st, CcdShape& A,
+                           CcdShape& B) {
   double a[3], b[3], c[3], e1[3], e2[3], n[3], nn[3];
   ccdLoad3(a, M.sim(0)); ccdLoad3(b, M.sim(1)); ccdLoad3(c, M.sim(2));
   sub3(e1, b, a);
@@ -2404,8 +2510,8 @@ MJH_HD int ccdFromTriangle(const CcdMem<S>& M, CcdPoly& P, CcdState& st, const C
 
 // polytope2 (:892-971)
 template <int S>
-MJH_HD int ccdFromSegment(const CcdMem<S>& M, CcdPoly& P, CcdState& st, const CcdShape& A,
-                          const CcdShape& B) {
+MJH_HD int ccdFromSegment(const CcdMem<S>& M, CcdPoly& P, CcdState& st, CcdShape& A,
+                          CcdShape& B) {
   double a[3], b[3], d[3];
   ccdLoad3(a, M.sim(0)); ccdLoad3(b, M.sim(1));
   sub3(d, b, a);
@@ -2465,8 +2571,8 @@ MJH_HD int ccdFromSegment(const CcdMem<S>& M, CcdPoly& P, CcdState& st, const Cc
 
 // polytope4 (:1122-1156)
 template <int S>
-MJH_HD int ccdFromTetra(const CcdMem<S>& M, CcdPoly& P, CcdState& st, const CcdShape& A,
-                        const CcdShape& B) {
+MJH_HD int ccdFromTetra(const CcdMem<S>& M, CcdPoly& P, CcdState& st, CcdShape& A,
+                        CcdShape& B) {
   const int i1 = ccdAddVertex(M, P, M.sim(0));
   const int i2 = ccdAddVertex(M, P, M.sim(1));
   const int i3 = ccdAddVertex(M, P, M.sim(2));
@@ -2568,8 +2674,8 @@ MJH_HD bool ccdHorizon(const CcdMem<S>& M, CcdPoly& P, int f0, const double w[3]
 
 // epa (:1329-1459) + epaWitness (:1300-1323): the face closest to the origin, or -1
 template <int S>
-MJH_HD int ccdEpa(CcdState& st, const CcdMem<S>& M, CcdPoly& P, const CcdShape& A,
-                  const CcdShape& B) {
+MJH_HD int ccdEpa(CcdState& st, const CcdMem<S>& M, CcdPoly& P, CcdShape& A,
+                  CcdShape& B) {
   const double FLTMAX = 3.40282346638528859811704183484516925e+38;   // FLT_MAX
   const int refmax = 6*st.kmax > 1000 ? 6*st.kmax : 1000;            // the reference's faces
   double lower, upper = FLTMAX;
@@ -2656,13 +2762,26 @@ MJH_HD int ccdEpa(CcdState& st, const CcdMem<S>& M, CcdPoly& P, const CcdShape& 
   return f;
 }
 
+// obj->center: the geom position (mjc_center convex.c:78-98), or a prism's mean vertex
+// (mjc_prism_center :103-110: zero, add the six vertices in order, scale by 1/6)
+MJH_HD void ccdCenter(double c[3], const CcdShape& s) {
+  if (s.gtype == mjhipGEOM_HFIELD) {
+    c[0] = 0; c[1] = 0; c[2] = 0;
+    for (int i = 0; i < 3; i++) { c[0] += s.px[i]; c[1] += s.py[i]; c[2] += s.pzb; }
+    for (int i = 0; i < 3; i++) { c[0] += s.px[i]; c[1] += s.py[i]; c[2] += s.pzt[i]; }
+    scl3(c, c, 1.0/6.0);
+  } else {
+    copy3(c, s.pos);
+  }
+}
+
 // mjc_ccd (:2215-2343) with max_contacts = 1 and the distance cutoff `cutoff` (0 for
 // mjc_Convex's contacts, the bound for mj_geomDistanceCCD)
 template <int S>
 MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B, int kmax,
                      double tol, double cutoff) {
-  copy3(st.x1, A.pos);
-  copy3(st.x2, B.pos);
+  ccdCenter(st.x1, A);
+  ccdCenter(st.x2, B);
   st.iters = 0;
   st.tol = tol;
   st.kmax = kmax;
@@ -2705,8 +2824,8 @@ MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B,
       return st.dist;
     }
     st.iters = 0;
-    copy3(st.x1, A.pos);
-    copy3(st.x2, B.pos);
+    ccdCenter(st.x1, A);
+    ccdCenter(st.x2, B);
   }
   ccdGjk(st, M, A, B);
   if (st.dist <= tol && st.nsimplex > 1) {
@@ -2720,6 +2839,20 @@ MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B,
   return st.dist;
 }
 
+// the mesh fields of a geom's solver object (mjc_initCCDObj :716-743)
+MJH_HD void ccdMeshData(CcdShape& s, const mjhipModel& m, int g) {
+  s.vert = nullptr;
+  s.graph = nullptr;
+  s.nvert = 0;
+  s.vertindex = s.meshindex = -1;
+  if (s.gtype == mjhipGEOM_MESH) {
+    const int id = m.geom_dataid[g];
+    s.vert = m.mesh_vert + 3*m.mesh_vertadr[id];
+    s.nvert = m.mesh_vertnum[id];
+    s.graph = m.mesh_graphadr[id] >= 0 ? m.mesh_graph + m.mesh_graphadr[id] : nullptr;
+  }
+}
+
 template <int S>
 MJH_HD void ccdShape(CcdShape& s, const mjhipModel& m, const Lane<S>& d, int g, double margin) {
   s.kind = s.gtype = m.geom_type[g];
@@ -2727,6 +2860,7 @@ MJH_HD void ccdShape(CcdShape& s, const mjhipModel& m, const Lane<S>& d, int g, 
   for (int k = 0; k < 9; k++) s.mat[k] = d.geom_xmat[9*g + k];
   for (int k = 0; k < 3; k++) s.size[k] = m.geom_size[3*g + k];
   s.margin = margin;
+  ccdMeshData(s, m, g);
 }
 
 // mjc_Convex through mjc_CCDIteration (convex.c:792-819, :915-1001): 0 or 1 contacts
@@ -2783,12 +2917,432 @@ MJH_HD int colPlaneEllipsoid(RawContact& c, double margin, P1 pos1, M1 mat1, P2 
   return 1;
 }
 
+// mjccd_support (convex.c:501-704), the libccd-style support of a geom at unit direction dir
+// in its current frame (s.pos / s.mat): a mesh hill-climbs from s.meshindex with the start
+// vertex's own value as the first bound and records the result in s.meshindex; the result is
+// inflated by half the object's margin
+MJH_HD void ccdSupportLib(double r[3], CcdShape& s, const double dir[3]) {
+  double ld[3], res[3];
+  mulMatTVec3(ld, s.mat, dir);
+  const double* size = s.size;
+  const int t = s.gtype;
+  if (t == mjhipGEOM_SPHERE) {
+    scl3(res, ld, size[0]);
+  } else if (t == mjhipGEOM_CAPSULE) {
+    scl3(res, ld, size[0]);
+    res[2] += (ld[2] < 0 ? -1.0 : (ld[2] > 0 ? 1.0 : 0.0)) * size[1];
+  } else if (t == mjhipGEOM_ELLIPSOID) {
+    for (int i = 0; i < 3; i++) res[i] = ld[i] * size[i];
+    normalize3(res);
+    for (int i = 0; i < 3; i++) res[i] *= size[i];
+  } else if (t == mjhipGEOM_CYLINDER) {
+    const double tmp = sqrt(ld[0]*ld[0] + ld[1]*ld[1]);
+    if (tmp > MINVAL) {
+      res[0] = ld[0]/tmp*size[0];
+      res[1] = ld[1]/tmp*size[0];
+    } else {
+      res[0] = res[1] = 0;
+    }
+    res[2] = (ld[2] < 0 ? -1.0 : (ld[2] > 0 ? 1.0 : 0.0)) * size[1];
+  } else if (t == mjhipGEOM_BOX) {
+    for (int i = 0; i < 3; i++) res[i] = (ld[i] < 0 ? -1.0 : (ld[i] > 0 ? 1.0 : 0.0)) * size[i];
+  } else {                                  // mesh
+    const float* V = s.vert;
+    double tmp = -1E+10;
+    int ibest = -1;
+    if (!s.graph) {
+      for (int i = 0; i < s.nvert; i++) {
+        const double vdot = ld[0]*(double)V[3*i] + ld[1]*(double)V[3*i+1] +
+                            ld[2]*(double)V[3*i+2];
+        if (vdot > tmp) {
+          tmp = vdot;
+          ibest = i;
+        }
+      }
+      s.meshindex = ibest;
+    } else {
+      const int numvert = s.graph[0];
+      const int* edgeadr = s.graph + 2;
+      const int* globalid = s.graph + 2 + numvert;
+      const int* localid = s.graph + 2 + 2*numvert;
+      ibest = s.meshindex < 0 ? 0 : s.meshindex;
+      const float* vb = V + 3*globalid[ibest];
+      tmp = ld[0]*(double)vb[0] + ld[1]*(double)vb[1] + ld[2]*(double)vb[2];
+      int change = 1, locid;
+      while (change) {
+        change = 0;
+        int i = edgeadr[ibest];
+        while ((locid = localid[i]) >= 0) {
+          const float* vx = V + 3*globalid[locid];
+          const double vdot = ld[0]*(double)vx[0] + ld[1]*(double)vx[1] + ld[2]*(double)vx[2];
+          if (vdot > tmp) {
+            tmp = vdot;
+            ibest = locid;
+            change = 1;
+          }
+          i++;
+        }
+      }
+      s.meshindex = ibest;
+      ibest = globalid[ibest];
+    }
+    if (ibest < 0) {
+      res[0] = res[1] = res[2] = 0;
+    } else {
+      for (int i = 0; i < 3; i++) res[i] = (double)V[3*ibest + i];
+    }
+  }
+  for (int i = 0; i < 3; i++) res[i] += ld[i] * s.margin/2;
+  mulMatVec3(res, s.mat, res);
+  addTo3(res, s.pos);
+  copy3(r, res);
+}
+
+// addplanemesh (convex.c:1010-1040)
+MJH_HD bool planeMeshContact(RawContact& c, const float* vertex, const double pos1[3],
+                             const double normal1[3], const double pos2[3],
+                             const double mat2[9], const double first[3], double rbound) {
+  double pnt[3], v[3] = {vertex[0], vertex[1], vertex[2]}, dif[3];
+  mulMatVec3(pnt, mat2, v);
+  addTo3(pnt, pos2);
+  const double dd[3] = {pnt[0] - first[0], pnt[1] - first[1], pnt[2] - first[2]};
+  if (sqrt(dd[0]*dd[0] + dd[1]*dd[1] + dd[2]*dd[2]) < 0.3*rbound) return false;
+  sub3(dif, pnt, pos1);
+  c.dist = dot3(normal1, dif);
+  copy3(c.pos, pnt);
+  addToScl3(c.pos, normal1, -0.5*c.dist);
+  copy3(c.frame, normal1);
+  for (int k = 3; k < 9; k++) c.frame[k] = 0;
+  return true;
+}
+
+// mjc_PlaneConvex (convex.c:1045-1141) for a mesh: the libccd support at -normal gives the
+// first contact, then up to maxplanemesh = 3 in all with the vertices below the margin around
+// the support vertex (its hull-graph neighbours, else every vertex); each contact goes to
+// emit as it is made
+template <int S, class Emit>
+MJH_HD void colPlaneMesh(const mjhipModel& m, const Lane<S>& d, int g1, int g2, double margin,
+                         Emit&& emit) {
+  double pos1[3], mat1[9], pos2[3], mat2[9];
+  for (int k = 0; k < 3; k++) { pos1[k] = d.gxpos[3*g1 + k]; pos2[k] = d.gxpos[3*g2 + k]; }
+  for (int k = 0; k < 9; k++) { mat1[k] = d.geom_xmat[9*g1 + k]; mat2[k] = d.geom_xmat[9*g2 + k]; }
+  const double normal[3] = {mat1[2], mat1[5], mat1[8]};
+  const double dir[3] = {-mat1[2], -mat1[5], -mat1[8]};
+  CcdShape obj;
+  obj.kind = obj.gtype = mjhipGEOM_MESH;
+  copy3(obj.pos, pos2);
+  for (int k = 0; k < 9; k++) obj.mat[k] = mat2[k];
+  for (int k = 0; k < 3; k++) obj.size[k] = m.geom_size[3*g2 + k];
+  obj.margin = 0;
+  ccdMeshData(obj, m, g2);
+  double v[3], dif[3];
+  ccdSupportLib(v, obj, dir);
+  sub3(dif, v, pos1);
+  const double dist = dot3(normal, dif);
+  if (dist > margin) return;
+  RawContact c;
+  c.dist = dist;
+  copy3(c.pos, v);
+  addToScl3(c.pos, normal, -0.5*dist);
+  copy3(c.frame, normal);
+  for (int k = 3; k < 9; k++) c.frame[k] = 0;
+  const double first[3] = {c.pos[0], c.pos[1], c.pos[2]};
+  if (!emit(c)) return;
+  int count = 1;
+  const int id = m.geom_dataid[g2];
+  const float* vertdata = m.mesh_vert + 3*m.mesh_vertadr[id];
+  double locdir[3];
+  mulMatTVec3(locdir, mat2, dir);
+  sub3(dif, pos2, pos1);
+  const double threshold = dot3(normal, dif) - margin;
+  const double rbound = m.geom_rbound[g2];
+  if (m.mesh_graphadr[id] < 0) {
+    for (int i = 0; i < m.mesh_vertnum[id] && count < 3; i++) {
+      const float* vx = vertdata + 3*i;
+      const double vdot = locdir[0]*(double)vx[0] + locdir[1]*(double)vx[1] +
+                          locdir[2]*(double)vx[2];
+      if (vdot > threshold && i != obj.meshindex) {
+        RawContact e;
+        if (planeMeshContact(e, vx, pos1, normal, pos2, mat2, first, rbound)) {
+          count++;
+          if (!emit(e)) return;
+        }
+      }
+    }
+  } else if (obj.meshindex >= 0) {
+    const int* graph = m.mesh_graph + m.mesh_graphadr[id];
+    const int numvert = graph[0];
+    const int* edgeadr = graph + 2;
+    const int* globalid = graph + 2 + numvert;
+    const int* localid = graph + 2 + 2*numvert;
+    int i = edgeadr[obj.meshindex], locid;
+    while ((locid = localid[i]) >= 0 && count < 3) {
+      const float* vx = vertdata + 3*globalid[locid];
+      const double vdot = locdir[0]*(double)vx[0] + locdir[1]*(double)vx[1] +
+                          locdir[2]*(double)vx[2];
+      if (vdot > threshold) {
+        RawContact e;
+        if (planeMeshContact(e, vx, pos1, normal, pos2, mat2, first, rbound)) {
+          count++;
+          if (!emit(e)) return;
+        }
+      }
+      i++;
+    }
+  }
+}
+
+// mjc_ellipsoidInside (convex.c:1363-1414) and mjc_ellipsoidOutside (:1419-1464)
+MJH_HD int ellipsoidInside(double nrm[3], const double pos[3], const double size[3]) {
+  const double S2inv[3] = {1/(size[0]*size[0]), 1/(size[1]*size[1]), 1/(size[2]*size[2])};
+  const double C = pos[0]*pos[0]*S2inv[0] + pos[1]*pos[1]*S2inv[1] + pos[2]*pos[2]*S2inv[2] - 1;
+  if (C > 0) return 0;
+  normalize3(nrm);
+  for (int iter = 0; iter < 30; iter++) {
+    const double A = nrm[0]*nrm[0]*S2inv[0] + nrm[1]*nrm[1]*S2inv[1] + nrm[2]*nrm[2]*S2inv[2];
+    const double B = pos[0]*nrm[0]*S2inv[0] + pos[1]*nrm[1]*S2inv[1] + pos[2]*nrm[2]*S2inv[2];
+    const double det = B*B - A*C;
+    if (det < MINVAL || A < MINVAL) return iter > 0;
+    const double x = (-B + sqrt(det))/A;
+    if (x < 0) return iter > 0;
+    double pnt[3];
+    for (int k = 0; k < 3; k++) pnt[k] = pos[k] + nrm[k]*x;   // mju_addScl3
+    double nn[3] = {pnt[0]*S2inv[0], pnt[1]*S2inv[1], pnt[2]*S2inv[2]};
+    normalize3(nn);
+    const double dd[3] = {nrm[0] - nn[0], nrm[1] - nn[1], nrm[2] - nn[2]};
+    const double change = sqrt(dd[0]*dd[0] + dd[1]*dd[1] + dd[2]*dd[2]);
+    copy3(nrm, nn);
+    if (change < 1e-6) break;
+  }
+  return 1;
+}
+
+MJH_HD int ellipsoidOutside(double nrm[3], const double pos[3], const double size[3]) {
+  const double S2[3] = {size[0]*size[0], size[1]*size[1], size[2]*size[2]};
+  const double PS2[3] = {pos[0]*pos[0]*S2[0], pos[1]*pos[1]*S2[1], pos[2]*pos[2]*S2[2]};
+  double la = 0;
+  for (int iter = 0; iter < 30; iter++) {
+    const double R[3] = {1/(S2[0]+la), 1/(S2[1]+la), 1/(S2[2]+la)};
+    const double val = PS2[0]*R[0]*R[0] + PS2[1]*R[1]*R[1] + PS2[2]*R[2]*R[2] - 1;
+    if (val < 1e-6) break;
+    const double deriv = -2*(PS2[0]*R[0]*R[0]*R[0] + PS2[1]*R[1]*R[1]*R[1] +
+                             PS2[2]*R[2]*R[2]*R[2]);
+    if (deriv > -MINVAL) break;
+    const double delta = -val/deriv;
+    if (delta < 1e-6) break;
+    la += delta;
+  }
+  nrm[0] = pos[0]/(S2[0]+la);
+  nrm[1] = pos[1]/(S2[1]+la);
+  nrm[2] = pos[2]/(S2[2]+la);
+  normalize3(nrm);
+  return 1;
+}
+
+// mjc_fixNormal (convex.c:1469-1614): the contact normal from the smooth geom's surface
+template <int S>
+MJH_HD void fixNormal(const mjhipModel& m, const Lane<S>& d, RawContact& con, int g1, int g2) {
+  const int gid[2] = {g1, g2};
+  int type[2];
+  for (int i = 0; i < 2; i++) {
+    type[i] = m.geom_type[gid[i]];
+    if (type[i] != mjhipGEOM_SPHERE && type[i] != mjhipGEOM_CAPSULE &&
+        type[i] != mjhipGEOM_ELLIPSOID && type[i] != mjhipGEOM_CYLINDER) {
+      type[i] = -1;
+    }
+  }
+  if (type[0] == -1 && type[1] == -1) return;
+  double normal[2][3] = {{con.frame[0], con.frame[1], con.frame[2]},
+                         {-con.frame[0], -con.frame[1], -con.frame[2]}};
+  int processed[2] = {0, 0};
+  for (int i = 0; i < 2; i++) {
+    if (type[i] == -1) continue;
+    double mat[9], gp[3];
+    for (int k = 0; k < 9; k++) mat[k] = d.geom_xmat[9*gid[i] + k];
+    for (int k = 0; k < 3; k++) gp[k] = d.gxpos[3*gid[i] + k];
+    const double* size = m.geom_size + 3*gid[i];
+    double dif[3], pos[3], nrm[3], dst1, dst2;
+    sub3(dif, con.pos, gp);
+    mulMatTVec3(pos, mat, dif);
+    mulMatTVec3(nrm, mat, normal[i]);
+    if (type[i] == mjhipGEOM_SPHERE) {
+      copy3(nrm, pos);
+      processed[i] = 1;
+    } else if (type[i] == mjhipGEOM_CAPSULE) {
+      if (pos[2] < -size[1]) {
+        nrm[2] = pos[2] + size[1];
+      } else if (pos[2] > size[1]) {
+        nrm[2] = pos[2] - size[1];
+      } else {
+        nrm[2] = 0;
+      }
+      nrm[0] = pos[0];
+      nrm[1] = pos[1];
+      processed[i] = 1;
+    } else if (type[i] == mjhipGEOM_ELLIPSOID) {
+      if (!(size[0] < MINVAL || size[1] < MINVAL || size[2] < MINVAL)) {
+        dst1 = pos[0]*pos[0]/(size[0]*size[0]) + pos[1]*pos[1]/(size[1]*size[1]) +
+               pos[2]*pos[2]/(size[2]*size[2]);
+        processed[i] = dst1 <= 1 ? ellipsoidInside(nrm, pos, size)
+                                 : ellipsoidOutside(nrm, pos, size);
+      }
+    } else {                                // cylinder
+      if (!(fabs(pos[2]) > 0.95*size[1])) {
+        dst1 = fabs(size[1] - fabs(pos[2]));
+        dst2 = fabs(size[0] - sqrt(pos[0]*pos[0] + pos[1]*pos[1]));
+        if (!(dst1 < 0.25*dst2)) {
+          nrm[0] = pos[0];
+          nrm[1] = pos[1];
+          nrm[2] = 0;
+          processed[i] = 1;
+        }
+      }
+    }
+    if (processed[i]) {
+      normalize3(nrm);
+      mulMatVec3(normal[i], mat, nrm);
+    }
+  }
+  if (processed[0] && processed[1]) {
+    sub3(con.frame, normal[0], normal[1]);
+    normalize3(con.frame);
+  } else if (processed[0]) {
+    copy3(con.frame, normal[0]);
+  } else if (processed[1]) {
+    scl3(con.frame, normal[1], -1);
+  }
+  if (processed[0] || processed[1]) {
+    for (int k = 3; k < 6; k++) con.frame[k] = 0;
+  }
+}
+
+// addVert (convex.c:1154-1168) on the compressed prism
+MJH_HD void prismAddVert(int& nvert, CcdShape& s, double x, double y, double z) {
+  s.px[0] = s.px[1]; s.py[0] = s.py[1]; s.pzt[0] = s.pzt[1];
+  s.px[1] = s.px[2]; s.py[1] = s.py[2]; s.pzt[1] = s.pzt[2];
+  s.px[2] = x; s.py[2] = y; s.pzt[2] = z;
+  nvert++;
+}
+
+// mjc_ConvexHField (convex.c:1173-1356): geom 2 expressed in the height field's frame, its
+// support box against the field's box, then the native solver (mjc_penetration :34-68, one
+// contact) against every triangular prism of the covered sub-grid; each contact's normal is
+// fixed by mjc_fixNormal and it goes to emit as it is made (the reference fixes the normals
+// after the loop; each depends on its own contact only). The warm starts of geom 2 carry over
+// from the support-box calls through every prism, as in the reference's single mjCCDObj.
+template <int S, class Emit>
+MJH_HD void colConvexHField(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
+                            double margin, int* status, Emit&& emit) {
+  double pos1[3], mat1[9], gp2[3], gm2[9];
+  for (int k = 0; k < 3; k++) { pos1[k] = d.gxpos[3*g1 + k]; gp2[k] = d.gxpos[3*g2 + k]; }
+  for (int k = 0; k < 9; k++) { mat1[k] = d.geom_xmat[9*g1 + k]; gm2[k] = d.geom_xmat[9*g2 + k]; }
+  const int hid = m.geom_dataid[g1];
+  const int nrow = m.hfield_nrow[hid], ncol = m.hfield_ncol[hid];
+  const float* data = m.hfield_data + m.hfield_adr[hid];
+  const double* size1 = m.hfield_size + 4*hid;
+  double vec[3], pos[3];
+  sub3(vec, gp2, pos1);
+  // mju_mulMatTVec (engine_util_blas.c): rows accumulated in order, zero entries skipped
+  pos[0] = pos[1] = pos[2] = 0;
+  for (int i = 0; i < 3; i++) {
+    if (vec[i] != 0) {
+      for (int j = 0; j < 3; j++) pos[j] += mat1[3*i + j]*vec[i];
+    }
+  }
+  const double r2 = m.geom_rbound[g2];
+  for (int i = 0; i < 2; i++) {
+    if ((size1[i] < pos[i] - r2 - margin) || (-size1[i] > pos[i] + r2 + margin)) return;
+  }
+  if (size1[2] < pos[2] - r2 - margin) return;
+  if (-size1[3] > pos[2] + r2 + margin) return;
+  CcdShape B;
+  B.kind = B.gtype = m.geom_type[g2];
+  copy3(B.pos, pos);
+  for (int i = 0; i < 3; i++) {                // mju_mulMatTMat3(mat, mat1, mat2)
+    for (int j = 0; j < 3; j++) {
+      B.mat[3*i + j] = mat1[i]*gm2[j] + mat1[3 + i]*gm2[3 + j] + mat1[6 + i]*gm2[6 + j];
+    }
+  }
+  for (int k = 0; k < 3; k++) B.size[k] = m.geom_size[3*g2 + k];
+  B.margin = 0;
+  ccdMeshData(B, m, g2);
+  double sv[3];
+  const double ax[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+  ccdSupportLib(sv, B, ax[0]); const double xmax = sv[0];
+  ccdSupportLib(sv, B, ax[1]); const double xmin = sv[0];
+  ccdSupportLib(sv, B, ax[2]); const double ymax = sv[1];
+  ccdSupportLib(sv, B, ax[3]); const double ymin = sv[1];
+  ccdSupportLib(sv, B, ax[4]); const double zmax = sv[2];
+  ccdSupportLib(sv, B, ax[5]); const double zmin = sv[2];
+  if ((xmin - margin > size1[0]) || (xmax + margin < -size1[0]) ||
+      (ymin - margin > size1[1]) || (ymax + margin < -size1[1]) ||
+      (zmin - margin > size1[2]) || (zmax + margin < -size1[3])) {
+    return;
+  }
+  int cmin = (int)floor((xmin + size1[0]) / (2*size1[0]) * (ncol - 1));
+  int cmax = (int)ceil((xmax + size1[0]) / (2*size1[0]) * (ncol - 1));
+  int rmin = (int)floor((ymin + size1[1]) / (2*size1[1]) * (nrow - 1));
+  int rmax = (int)ceil((ymax + size1[1]) / (2*size1[1]) * (nrow - 1));
+  cmin = cmin > 0 ? cmin : 0;
+  cmax = cmax < ncol - 1 ? cmax : ncol - 1;
+  rmin = rmin > 0 ? rmin : 0;
+  rmax = rmax < nrow - 1 ? rmax : nrow - 1;
+  B.margin = margin;
+  CcdShape A;
+  A.kind = A.gtype = mjhipGEOM_HFIELD;
+  A.margin = 0;
+  A.vert = nullptr;
+  A.graph = nullptr;
+  A.nvert = 0;
+  A.vertindex = A.meshindex = -1;
+  for (int k = 0; k < 3; k++) { A.px[k] = A.py[k] = A.pzt[k] = 0; A.pos[k] = 0; A.size[k] = 0; }
+  A.pzb = -size1[3];
+  const double dx = (2.0*size1[0]) / (ncol - 1), dy = (2.0*size1[1]) / (nrow - 1);
+  const int N = m.opt.ccd_iterations;
+  CcdMem<S> M{d.ccd, d.ccdi, 5 + N, mjh_ccdFaceCap(&m)};
+  int cnt = 0;
+  for (int r = rmin; r < rmax; r++) {
+    int nvert = 0;
+    for (int c = cmin; c <= cmax; c++) {
+      for (int i = 0; i < 2; i++) {
+        const int rr = r + (i == 0 ? 1 : 0);
+        prismAddVert(nvert, A, dx*c - size1[0], dy*rr - size1[1],
+                     (double)data[rr*ncol + c]*size1[2] + margin);
+        if (nvert <= 2) continue;
+        if (A.pzt[0] < zmin && A.pzt[1] < zmin && A.pzt[2] < zmin) continue;
+        CcdState st;
+        const double dist = ccdRun(st, M, A, B, N, m.opt.ccd_tolerance, 0.0);
+        if (st.unsupported) {
+          *status |= MJHIP_INST_UNSUPPORTED;
+          return;
+        }
+        if (!(dist < 0)) continue;
+        double dir[3], vp[3];
+        sub3(dir, st.x1, st.x2);
+        normalize3(dir);
+        vp[0] = 0.5*(st.x1[0] + st.x2[0]);
+        vp[1] = 0.5*(st.x1[1] + st.x2[1]);
+        vp[2] = 0.5*(st.x1[2] + st.x2[2]);
+        RawContact con;
+        con.dist = dist;
+        mulMatVec3(con.frame, mat1, dir);
+        mulMatVec3(con.pos, mat1, vp);
+        addTo3(con.pos, pos1);
+        for (int k = 3; k < 9; k++) con.frame[k] = 0;
+        fixNormal(m, d, con, g1, g2);
+        if (!emit(con)) return;
+        if (++cnt >= 50) return;
+      }
+    }
+  }
+}
+
 // mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
 // WRITE = false only counts the contacts the pair produces (the cooperative constraint
 // kernel's first pass: it needs each pair's count to place the contacts in order)
 // bbuf: per-lane room for box-box positions (24 x 3 doubles), or nullptr to use the
 // contact list's free tail at ncon (the capacity holds 24 contacts for every box pair)
-template <int S, bool WRITE = true, bool BOX = true>
+template <int S, bool WRITE = true, bool BOX = true, bool CONVEX = true>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
                                double margin, int& ncon, int* status, double* bbuf = nullptr);
 
@@ -2848,6 +3402,8 @@ MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
   }
   if (t1 == mjhipGEOM_PLANE && (t2 == mjhipGEOM_BOX || t2 == mjhipGEOM_CYLINDER)) return -1;
   if (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX) return -1;
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_MESH) return -1;   // up to 3, stored as made
+  if (t1 == mjhipGEOM_HFIELD) return -1;                            // up to 50, stored as made
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
   SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
   const double *size1 = m.geom_size + 3*g1, *size2 = m.geom_size + 3*g2;
@@ -3008,15 +3564,36 @@ MJH_HD void collideBoxBox(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
   });
 }
 
-// plane : box / cylinder (up to 4 contacts each) and box : box (up to 24): contacts are
-// stored as they are made. BOX = false compiles the box-box path out (kernels launched for
-// models without a box pair: its private arrays would otherwise cost every contact kernel)
-template <int S, bool WRITE, bool BOX>
+// plane : box / cylinder (up to 4 contacts each), box : box (up to 24), plane : mesh (up to
+// 3) and height field : geom (up to 50): contacts are stored as they are made. BOX = false
+// compiles the box-box path out (kernels launched for models without a box pair: its private
+// arrays would otherwise cost every contact kernel); CONVEX = false compiles the mesh and
+// height-field paths out (the cooperative kernel, which no such model launches)
+template <int S, bool WRITE, bool BOX, bool CONVEX>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
                                double margin, int& ncon, int* status, double* bbuf) {
   if (m.geom_type[g1] == mjhipGEOM_BOX) {
     if constexpr (BOX) collideBoxBox<S, WRITE>(m, d, g1, g2, margin, ncon, status, bbuf);
     else *status |= MJHIP_INST_UNSUPPORTED;   // not reached: the launch saw no box pair
+    return;
+  }
+  if (m.geom_type[g1] == mjhipGEOM_HFIELD || m.geom_type[g2] == mjhipGEOM_MESH) {
+    if constexpr (CONVEX) {
+      int condim;
+      double gap, solref[2], solimp[5], friction[5];
+      contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
+      auto store = [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
+        return putContact<S, WRITE>(m, d, g1, g2, margin, condim, gap, solref, solimp,
+                                    friction, rk, ncon, status);
+      };
+      if (m.geom_type[g1] == mjhipGEOM_HFIELD) {
+        colConvexHField(m, d, g1, g2, margin, status, store);
+      } else {
+        colPlaneMesh(m, d, g1, g2, margin, store);
+      }
+    } else {
+      *status |= MJHIP_INST_UNSUPPORTED;      // not reached: such models use one lane each
+    }
     return;
   }
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
@@ -3087,7 +3664,9 @@ MJH_HD double geomDistance(const mjhipModel& m, const Lane<S>& d, int geom1, int
     }
     return true;
   };
-  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_BOX) {
+  if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_MESH) {
+    colPlaneMesh(m, d, g1, g2, distmax, take);
+  } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_BOX) {
     colPlaneBox(distmax, (const double*)pos1, (const double*)mat1, (const double*)pos2,
                 (const double*)mat2, size2, take);
   } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_CYLINDER) {
@@ -5762,6 +6341,279 @@ template <int S> MJH_HD void rneVel(const mjhipModel& m, const Lane<S>& d) {
   }
 }
 
+//---------------------------------- engine_derivative.c (fluid) ------------------------------
+
+// addJTBJ :693-724: qDeriv (D sparsity) += J' B J for the n x n B and the n rows of J (Dtmp)
+template <int S>
+MJH_HD void addJTBJ(const mjhipModel& m, const Lane<S>& d, SP<S> J, const double* B, int n) {
+  const int nv = m.nv;
+  for (int i = 0; i < n; i++) {
+    for (int j = 0; j < n; j++) {
+      if (!B[i*n+j]) continue;
+      for (int k = 0; k < nv; k++) {
+        const double jik = J[i*nv+k];
+        if (!jik) continue;
+        const double s = jik * B[i*n+j];
+        const int adr = m.D_rowadr[k], end = adr + m.D_rownnz[k];
+        for (int a = adr; a < end; a++) d.qDeriv[a] += J[j*nv + m.D_colind[a]] * s;
+      }
+    }
+  }
+}
+
+// :898-909 addToQuadrant (the reference indexes B column-major in 3x3 blocks)
+MJH_HD void addToQuadrant(double* B, const double D[9], int col_quad, int row_quad) {
+  const int r = 3*row_quad, c = 3*col_quad;
+  for (int k = 0; k < 3; k++) {
+    for (int l = 0; l < 3; l++) B[6*(c+k) + r+l] += D[3*k+l];
+  }
+}
+
+// :38-61 mjd_cross
+MJH_HD void dcross(const double a[3], const double b[3], double* Da, double* Db) {
+  for (int k = 0; k < 9; k++) Da[k] = Db[k] = 0;
+  Da[1] =  b[2]; Da[2] = -b[1]; Da[3] = -b[2]; Da[5] =  b[0]; Da[6] =  b[1]; Da[7] = -b[0];
+  Db[1] = -a[2]; Db[2] =  a[1]; Db[3] =  a[2]; Db[5] = -a[0]; Db[6] = -a[1]; Db[7] =  a[0];
+}
+
+// the ellipsoid model's 6x6 B of one geom (:1239-1259): Magnus, Kutta, viscous drag and
+// torque (:962-1161) and added mass (:916-957) in the reference's order of accumulation
+MJH_HD void ellipsoidFluidB(double* B, const double lv[6], double rho, double mu,
+                            const double s[3], const double* c, bool symmetric) {
+  auto mx = [](double a, double b) { return a > b ? a : b; };
+  auto mn = [](double a, double b) { return a < b ? a : b; };
+  double D[9], Da[9], Db[9];
+  for (int k = 0; k < 36; k++) B[k] = 0;
+  const double blunt = c[1], slender = c[2], angdrag = c[3], kutta = c[4], magnus = c[5];
+  const double* vm = c + 6;
+  const double* vi = c + 9;
+  {                                       // mjd_magnus_force
+    const double volume = 4.0/3.0 * mjhipPI * s[0] * s[1] * s[2];
+    const double coef = magnus * rho * volume;
+    const double lin[3] = {coef * lv[3], coef * lv[4], coef * lv[5]};
+    const double ang[3] = {coef * lv[0], coef * lv[1], coef * lv[2]};
+    dcross(ang, lin, Da, Db);
+    addToQuadrant(B, Da, 1, 0);
+    addToQuadrant(B, Db, 1, 1);
+  }
+  const double a = (s[1]*s[2])*(s[1]*s[2]), b = (s[2]*s[0])*(s[2]*s[0]);
+  const double cz = (s[0]*s[1])*(s[0]*s[1]);
+  const double aa = a*a, bb = b*b, cc = cz*cz;
+  const double x = lv[3], y = lv[4], z = lv[5];
+  const double xx = x*x, yy = y*y, zz = z*z, xy = x*y, yz = y*z, xz = x*z;
+  const double pden = aa*xx + bb*yy + cc*zz;
+  const double pnum = a*xx + b*yy + cz*zz;
+  {                                       // mjd_kutta_lift
+    const double norm2 = xx + yy + zz;
+    const double df_denom = mjhipPI * kutta * rho / mx(MINVAL, sqrt(pden * pnum * norm2));
+    const double dfx = yy * (a - b) + zz * (a - cz);
+    const double dfy = xx * (b - a) + zz * (b - cz);
+    const double dfz = xx * (cz - a) + yy * (cz - b);
+    const double proj_term = pnum / mx(MINVAL, pden);
+    const double cos_term = pnum / mx(MINVAL, norm2);
+    D[0] = a-a;  D[1] = b-a;  D[2] = cz-a;
+    D[3] = a-b;  D[4] = b-b;  D[5] = cz-b;
+    D[6] = a-cz; D[7] = b-cz; D[8] = cz-cz;
+    for (int k = 0; k < 9; k++) D[k] = D[k]*(2 * pnum);
+    const double inner[3] = {aa * proj_term - a + cos_term, bb * proj_term - b + cos_term,
+                             cc * proj_term - cz + cos_term};
+    addToScl3(D + 0, inner, dfx);
+    addToScl3(D + 3, inner, dfy);
+    addToScl3(D + 6, inner, dfz);
+    D[0] *= xx; D[1] *= xy; D[2] *= xz;
+    D[3] *= xy; D[4] *= yy; D[5] *= yz;
+    D[6] *= xz; D[7] *= yz; D[8] *= zz;
+    D[0] -= dfx * pnum;
+    D[4] -= dfy * pnum;
+    D[8] -= dfz * pnum;
+    for (int k = 0; k < 9; k++) D[k] = D[k]*df_denom;
+    addToQuadrant(B, D, 1, 1);
+  }
+  const double dmax = mx(mx(s[0], s[1]), s[2]);
+  const double dmin = mn(mn(s[0], s[1]), s[2]);
+  const double dmid = s[0] + s[1] + s[2] - dmax - dmin;
+  const double eqD = 2.0/3.0 * (s[0] + s[1] + s[2]);
+  {                                       // mjd_viscous_drag
+    const double Amax = mjhipPI * dmax * dmid;
+    const double dA = mjhipPI / mx(MINVAL, sqrt(pnum*pnum*pnum * pden));
+    const double Aproj = mjhipPI * sqrt(pden/mx(MINVAL, pnum));
+    const double norm = sqrt(xx + yy + zz);
+    const double inv_norm = 1.0 / mx(MINVAL, norm);
+    const double lin_coef = mu * 3.0 * mjhipPI * eqD;
+    const double quad_coef = rho * (Aproj*blunt + slender*(Amax - Aproj));
+    const double Ac = rho * norm * (blunt - slender);
+    const double dAv[3] = {Ac * dA * a * x * (b * yy * (a - b) + cz * zz * (a - cz)),
+                           Ac * dA * b * y * (a * xx * (b - a) + cz * zz * (b - cz)),
+                           Ac * dA * cz * z * (a * xx * (cz - a) + b * yy * (cz - b))};
+    D[0] = xx; D[1] = xy; D[2] = xz;
+    D[3] = xy; D[4] = yy; D[5] = yz;
+    D[6] = xz; D[7] = yz; D[8] = zz;
+    const double inner = xx + yy + zz;
+    D[0] += inner; D[4] += inner; D[8] += inner;
+    const double sc = -quad_coef*inv_norm;
+    for (int k = 0; k < 9; k++) D[k] = D[k]*sc;
+    addToScl3(D + 0, dAv, -x);
+    addToScl3(D + 3, dAv, -y);
+    addToScl3(D + 6, dAv, -z);
+    D[0] -= lin_coef; D[4] -= lin_coef; D[8] -= lin_coef;
+    addToQuadrant(B, D, 1, 1);
+  }
+  {                                       // mjd_viscous_torque
+    const double lin_visc = mjhipPI * eqD*eqD*eqD;
+    const double Imax = 8.0/15.0 * mjhipPI * dmid * (dmax*dmax)*(dmax*dmax);
+    double II[3];
+    for (int k = 0; k < 3; k++) {         // ellipsoid_max_moment (:887-892)
+      II[k] = 8.0/15.0 * mjhipPI * s[k] * pow4(mx(s[(k+1) % 3], s[(k+2) % 3]));
+    }
+    const double ax = lv[0], ay = lv[1], az = lv[2];
+    const double mc[3] = {angdrag*II[0] + slender*(Imax - II[0]),
+                          angdrag*II[1] + slender*(Imax - II[1]),
+                          angdrag*II[2] + slender*(Imax - II[2])};
+    const double mv[3] = {ax * mc[0], ay * mc[1], az * mc[2]};
+    const double density = rho / mx(MINVAL, sqrt(mv[0]*mv[0] + mv[1]*mv[1] + mv[2]*mv[2]));
+    const double msq[3] = {-density * ax * mc[0] * mc[0], -density * ay * mc[1] * mc[1],
+                           -density * az * mc[2] * mc[2]};
+    const double lin_coef = mu * lin_visc;
+    for (int k = 0; k < 9; k++) D[k] = 0;
+    D[0] = D[4] = D[8] = ax*msq[0] + ay*msq[1] + az*msq[2] - lin_coef;
+    addToScl3(D, msq, ax);
+    addToScl3(D + 3, msq, ay);
+    addToScl3(D + 6, msq, az);
+    addToQuadrant(B, D, 0, 0);
+  }
+  {                                       // mjd_addedMassForces
+    const double lin[3] = {lv[3], lv[4], lv[5]}, ang[3] = {lv[0], lv[1], lv[2]};
+    const double plin[3] = {rho*vm[0]*lin[0], rho*vm[1]*lin[1], rho*vm[2]*lin[2]};
+    const double pang[3] = {rho*vi[0]*ang[0], rho*vi[1]*ang[1], rho*vi[2]*ang[2]};
+    dcross(pang, ang, Da, Db);
+    addToQuadrant(B, Db, 0, 0);
+    for (int k = 0; k < 9; k++) Da[k] *= rho * vi[k % 3];
+    addToQuadrant(B, Da, 0, 0);
+    dcross(plin, lin, Da, Db);
+    addToQuadrant(B, Db, 0, 1);
+    for (int k = 0; k < 9; k++) Da[k] *= rho * vm[k % 3];
+    addToQuadrant(B, Da, 0, 1);
+    dcross(plin, ang, Da, Db);
+    addToQuadrant(B, Db, 1, 0);
+    for (int k = 0; k < 9; k++) Da[k] *= rho * vm[k % 3];
+    addToQuadrant(B, Da, 1, 1);
+  }
+  if (symmetric) {                        // mju_symmetrize (engine_util_blas.c:794-801)
+    for (int r = 0; r < 6; r++) {
+      for (int k = 0; k < r; k++) B[r*6+k] = B[k*6+r] = 0.5 * (B[r*6+k] + B[k*6+r]);
+    }
+  }
+}
+
+// the local 6 x nv Jacobian of a frame into Dtmp (rotation rows, then translation): mj_jac at
+// `point`, each half rotated by mju_mulMatTMat(xmat, ., 3, 3, nv) (engine_util_blas.c:884-897,
+// zero entries of xmat skipped)
+template <int S, class P, class X>
+MJH_HD void localJac(const mjhipModel& m, const Lane<S>& d, P point, X xmat, int body) {
+  const int nv = m.nv;
+  jacInto(m, d, d.jacp, d.jacr, point, body);
+  double R[9];
+  for (int k = 0; k < 9; k++) R[k] = xmat[k];
+  for (int h = 0; h < 2; h++) {
+    SP<S> src = h ? d.jacp : d.jacr;
+    SP<S> dst = d.Dtmp + 3*h*nv;
+    for (int k = 0; k < nv; k++) {
+      const double v0 = src[k], v1 = src[nv + k], v2 = src[2*nv + k];
+      for (int j = 0; j < 3; j++) {
+        double t = 0;
+        if (R[j]) t += v0*R[j];
+        if (R[3 + j]) t += v1*R[3 + j];
+        if (R[6 + j]) t += v2*R[6 + j];
+        dst[j*nv + k] = t;
+      }
+    }
+  }
+}
+
+// mjd_passive_vel :1494-1513: qDeriv += the fluid models' d qfrc_fluid / d qvel
+// (mjd_ellipsoidFluid :1168-1270, mjd_inertiaBoxFluid :1275-1425, dense Jacobians)
+template <int S>
+MJH_HD void fluidDeriv(const mjhipModel& m, const Lane<S>& d) {
+  const int nv = m.nv;
+  const double rho = m.opt.density, mu = m.opt.viscosity;
+  for (int i = 1; i < m.nbody; i++) {
+    if (m.body_mass[i] < MINVAL) continue;
+    int ell = 0;
+    for (int j = 0; j < m.body_geomnum[i] && ell == 0; j++) {
+      ell += m.geom_fluid[12*(m.body_geomadr[i] + j)] > 0;
+    }
+    double lvel[6], wind[6], lwind[6];
+    for (int k = 0; k < 3; k++) { wind[k] = 0; wind[3 + k] = m.opt.wind[k]; }
+    if (ell) {
+      for (int j = 0; j < m.body_geomnum[i]; j++) {
+        const int g = m.body_geomadr[i] + j;
+        const double* c = m.geom_fluid + 12*g;
+        const double* sz = m.geom_size + 3*g;
+        double ax[3], B[36];                // mju_geomSemiAxes (engine_util_misc.c:425-451)
+        const int t = m.geom_type[g];
+        if (t == mjhipGEOM_SPHERE) { ax[0] = sz[0]; ax[1] = sz[0]; ax[2] = sz[0]; }
+        else if (t == mjhipGEOM_CAPSULE) { ax[0] = sz[0]; ax[1] = sz[0]; ax[2] = sz[1] + sz[0]; }
+        else if (t == mjhipGEOM_CYLINDER) { ax[0] = sz[0]; ax[1] = sz[0]; ax[2] = sz[1]; }
+        else { ax[0] = sz[0]; ax[1] = sz[1]; ax[2] = sz[2]; }
+        if (c[0] == 0.0) continue;
+        objectVelocity(m, d, 5, g, lvel, 1);   // mjOBJ_GEOM
+        transformSpatial(lwind, wind, 0, d.geom_xpos + 3*g, d.subtree_com + 3*m.body_rootid[i],
+                         d.geom_xmat + 9*g, true);
+        lvel[3] -= lwind[3]; lvel[4] -= lwind[4]; lvel[5] -= lwind[5];
+        localJac(m, d, d.geom_xpos + 3*g, d.geom_xmat + 9*g, m.geom_bodyid[g]);
+        ellipsoidFluidB(B, lvel, rho, mu, ax, c, m.opt.integrator == mjhipINT_IMPLICITFAST);
+        addJTBJ(m, d, d.Dtmp, B, 6);
+      }
+      continue;
+    }
+    const double* inertia = m.body_inertia + 3*i;
+    const double mass = m.body_mass[i];
+    auto mx = [](double a, double b) { return a > b ? a : b; };
+    double box[3], B;
+    box[0] = sqrt(mx(MINVAL, (inertia[1] + inertia[2] - inertia[0])) / mass * 6.0);
+    box[1] = sqrt(mx(MINVAL, (inertia[0] + inertia[2] - inertia[1])) / mass * 6.0);
+    box[2] = sqrt(mx(MINVAL, (inertia[0] + inertia[1] - inertia[2])) / mass * 6.0);
+    objectVelocity(m, d, 1, i, lvel, 1);
+    transformSpatial(lwind, wind, 0, d.xipos + 3*i, d.subtree_com + 3*m.body_rootid[i],
+                     d.ximat + 9*i, true);
+    lvel[3] -= lwind[3]; lvel[4] -= lwind[4]; lvel[5] -= lwind[5];
+    localJac(m, d, d.xipos + 3*i, d.ximat + 9*i, i);
+    SP<S> J = d.Dtmp;
+    if (mu > 0) {
+      const double diam = (box[0] + box[1] + box[2])/3.0;
+      B = -mjhipPI*diam*diam*diam*mu;
+      for (int j = 0; j < 3; j++) addJTBJ(m, d, J + j*nv, &B, 1);
+      B = -3.0*mjhipPI*diam*mu;
+      for (int j = 0; j < 3; j++) addJTBJ(m, d, J + 3*nv + j*nv, &B, 1);
+    }
+    if (rho > 0) {
+      B = -rho*box[0]*(box[1]*box[1]*box[1]*box[1]+box[2]*box[2]*box[2]*box[2])*
+          2*fabs(lvel[0])/64.0;
+      addJTBJ(m, d, J, &B, 1);
+      B = -rho*box[1]*(box[0]*box[0]*box[0]*box[0]+box[2]*box[2]*box[2]*box[2])*
+          2*fabs(lvel[1])/64.0;
+      addJTBJ(m, d, J + nv, &B, 1);
+      B = -rho*box[2]*(box[0]*box[0]*box[0]*box[0]+box[1]*box[1]*box[1]*box[1])*
+          2*fabs(lvel[2])/64.0;
+      addJTBJ(m, d, J + 2*nv, &B, 1);
+      B = -0.5*rho*box[1]*box[2]*2*fabs(lvel[3]);
+      addJTBJ(m, d, J + 3*nv, &B, 1);
+      B = -0.5*rho*box[0]*box[2]*2*fabs(lvel[4]);
+      addJTBJ(m, d, J + 4*nv, &B, 1);
+      B = -0.5*rho*box[0]*box[1]*2*fabs(lvel[5]);
+      addJTBJ(m, d, J + 5*nv, &B, 1);
+    }
+  }
+}
+
+// address of (r, c) in the D sparsity (c an ancestor of r: the inverse of mapD2M)
+MJH_HD int dAdr(const mjhipModel& m, int r, int c) {
+  const int adr = m.D_rowadr[r];
+  int k = 0;
+  while (k < m.D_rownnz[r] - 1 && m.D_colind[adr + k] != c) k++;
+  return adr + k;
+}
+
 // mj_discreteAcc engine_inverse.c:81-164:
 //   Euler: qacc <- M^-1 (M + h*diag(B)) qacc when implicit damping applies
 //   implicitfast: qacc <- M^-1 (M - h*qDeriv) qacc, qDeriv reduced to qM's sparsity; the
@@ -5780,6 +6632,7 @@ MJH_HD void discreteAcc(const mjhipModel& m, const Lane<S>& d) {
         d.qDeriv[adr + k] = qDerivAt(m, d, r, m.D_colind[adr + k]);
       }
     }
+    if (mjh_fluidDeriv(&m)) fluidDeriv(m, d);
     rneVel(m, d);
     for (int i = 0; i < m.nD; i++) {
       d.qLU[i] = d.qM[m.mapM2D[i]] + d.qDeriv[i] * -m.opt.timestep;
@@ -5787,6 +6640,34 @@ MJH_HD void discreteAcc(const mjhipModel& m, const Lane<S>& d) {
     for (int r = 0; r < nv; r++) {
       const int adr = m.D_rowadr[r];
       d.qforce[r] = dotSparse(d.qLU + adr, d.qacc, m.D_rownnz[r], m.D_colind + adr);
+    }
+    copy(d.qacc, d.qforce, nv);
+    solveM(m, d, d.qacc);
+    return;
+  }
+  if (m.opt.integrator == mjhipINT_IMPLICITFAST && mjh_fluidDeriv(&m)) {
+    // mjd_smooth_vel(flg_bias = 0) on the D sparsity with the fluid terms, then mj_mulM with
+    // qM + qDeriv*(-h) reduced to qM's sparsity
+    for (int r = 0; r < nv; r++) {
+      const int adr = m.D_rowadr[r];
+      for (int k = 0; k < m.D_rownnz[r]; k++) {
+        d.qDeriv[adr + k] = qDerivAt(m, d, r, m.D_colind[adr + k]);
+      }
+    }
+    fluidDeriv(m, d);
+    const double h = m.opt.timestep;
+    for (int i = 0; i < nv; i++) {
+      int adr = m.dof_Madr[i];
+      d.qforce[i] = (d.qM[adr] + d.qDeriv[dAdr(m, i, i)] * -h)*d.qacc[i];
+      if (m.dof_simplenum[i]) continue;
+      int j = m.dof_parentid[i];
+      while (j >= 0) {
+        adr++;
+        double Mij = d.qM[adr] + d.qDeriv[dAdr(m, i, j)] * -h;
+        d.qforce[i] += Mij*d.qacc[j];
+        d.qforce[j] += Mij*d.qacc[i];
+        j = m.dof_parentid[j];
+      }
     }
     copy(d.qacc, d.qforce, nv);
     solveM(m, d, d.qacc);
@@ -6521,6 +7402,189 @@ MJH_HD double rayGeom(const double* pos, const double* mat, const double* size,
   return x;
 }
 
+// ray_box :387-445 with each face's hit in all (-1 for none)
+MJH_HD double rayBoxAll(const double* pos, const double* mat, const double* size,
+                        const double* pnt, const double* vec, double all[6]) {
+  for (int i = 0; i < 6; i++) all[i] = -1;
+  if (raySphere(pos, size[0]*size[0] + size[1]*size[1] + size[2]*size[2], pnt, vec) < 0) {
+    return -1;
+  }
+  const int iface[3][2] = {{1, 2}, {0, 2}, {0, 1}};
+  double lpnt[3], lvec[3], x = -1, sol;
+  rayMap(pos, mat, pnt, vec, lpnt, lvec);
+  for (int i = 0; i < 3; i++) {
+    if (fabs(lvec[i]) > MINVAL) {
+      for (int side = -1; side <= 1; side += 2) {
+        sol = (side*size[i]-lpnt[i])/lvec[i];
+        if (sol >= 0) {
+          const double p0 = lpnt[iface[i][0]] + sol*lvec[iface[i][0]];
+          const double p1 = lpnt[iface[i][1]] + sol*lvec[iface[i][1]];
+          if (fabs(p0) <= size[iface[i][0]] && fabs(p1) <= size[iface[i][1]]) {
+            if (x < 0 || sol < x) x = sol;
+            all[2*i + (side + 1)/2] = sol;
+          }
+        }
+      }
+    }
+  }
+  return x;
+}
+
+// ray_triangle :132-186
+MJH_HD double rayTriangle(const double v[3][3], const double* lpnt, const double* lvec,
+                          const double* b0, const double* b1) {
+  double dif[3][3], planar[3][2];
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) dif[i][j] = v[i][j] - lpnt[j];
+  }
+  for (int i = 0; i < 3; i++) {
+    planar[i][0] = dot3(b0, dif[i]);
+    planar[i][1] = dot3(b1, dif[i]);
+  }
+  if ((planar[0][0] > 0 && planar[1][0] > 0 && planar[2][0] > 0) ||
+      (planar[0][0] < 0 && planar[1][0] < 0 && planar[2][0] < 0) ||
+      (planar[0][1] > 0 && planar[1][1] > 0 && planar[2][1] > 0) ||
+      (planar[0][1] < 0 && planar[1][1] < 0 && planar[2][1] < 0)) {
+    return -1;
+  }
+  const double A[4] = {planar[0][0]-planar[2][0], planar[1][0]-planar[2][0],
+                       planar[0][1]-planar[2][1], planar[1][1]-planar[2][1]};
+  const double b[2] = {-planar[2][0], -planar[2][1]};
+  const double det = A[0]*A[3] - A[1]*A[2];
+  if (fabs(det) < MINVAL) return -1;
+  const double t0 = (A[3]*b[0] - A[1]*b[1]) / det;
+  const double t1 = (-A[2]*b[0] + A[0]*b[1]) / det;
+  if (t0 < 0 || t1 < 0 || t0 + t1 > 1) return -1;
+  double e0[3], e1[3], e2[3], nrm[3];
+  sub3(e0, v[0], v[2]);
+  sub3(e1, v[1], v[2]);
+  sub3(e2, lpnt, v[2]);
+  cross(nrm, e0, e1);
+  const double denom = dot3(lvec, nrm);
+  if (fabs(denom) < MINVAL) return -1;
+  return -dot3(e2, nrm) / denom;
+}
+
+// the basis of the plane normal to the local ray (mj_rayHfield :497-509, mju_rayTree :651-663)
+MJH_HD void rayBasis(const double lvec[3], double b0[3], double b1[3]) {
+  b0[0] = b0[1] = b0[2] = 1;
+  if (fabs(lvec[0]) >= fabs(lvec[1]) && fabs(lvec[0]) >= fabs(lvec[2])) {
+    b0[0] = 0;
+  } else if (fabs(lvec[1]) >= fabs(lvec[2])) {
+    b0[1] = 0;
+  } else {
+    b0[2] = 0;
+  }
+  const double s = -dot3(lvec, b0)/dot3(lvec, lvec);
+  for (int k = 0; k < 3; k++) b1[k] = b0[k] + lvec[k]*s;          // mju_addScl3
+  normalize3(b1);
+  cross(b0, b1, lvec);
+  normalize3(b0);
+}
+
+// mj_rayHfield :453-595 (the reference's side-face indexing by nrow kept)
+MJH_HD double rayHfield(const mjhipModel& m, int id, const double xpos[3], const double xmat[9],
+                        const double* pnt, const double* vec) {
+  const int hid = m.geom_dataid[id];
+  const int nrow = m.hfield_nrow[hid], ncol = m.hfield_ncol[hid];
+  const double* size = m.hfield_size + 4*hid;
+  const float* data = m.hfield_data + m.hfield_adr[hid];
+  const double base_size[3] = {size[0], size[1], size[3]*0.5};
+  const double base_pos[3] = {xpos[0] - xmat[2]*size[3]*0.5, xpos[1] - xmat[5]*size[3]*0.5,
+                              xpos[2] - xmat[8]*size[3]*0.5};
+  const double top_size[3] = {size[0], size[1], size[2]*0.5};
+  const double top_pos[3] = {xpos[0] + xmat[2]*size[2]*0.5, xpos[1] + xmat[5]*size[2]*0.5,
+                             xpos[2] + xmat[8]*size[2]*0.5};
+  double all[6];
+  double x = rayBoxAll(base_pos, xmat, base_size, pnt, vec, all);
+  const double top_intersect = rayBoxAll(top_pos, xmat, top_size, pnt, vec, all);
+  if (top_intersect < 0) return x;
+  double lpnt[3], lvec[3], b0[3], b1[3];
+  rayMap(xpos, xmat, pnt, vec, lpnt, lvec);
+  rayBasis(lvec, b0, b1);
+  double seg[2] = {0, top_intersect};
+  for (int i = 0; i < 6; i++) {
+    if (all[i] > seg[1]) {
+      seg[0] = top_intersect;
+      seg[1] = all[i];
+    }
+  }
+  const double dx = (2.0*size[0]) / (ncol-1), dy = (2.0*size[1]) / (nrow-1);
+  double SX[2], SY[2];
+  for (int i = 0; i < 2; i++) {
+    SX[i] = (lpnt[0] + seg[i]*lvec[0] + size[0]) / dx;
+    SY[i] = (lpnt[1] + seg[i]*lvec[1] + size[1]) / dy;
+  }
+  int cmin = (int)floor(SX[0] < SX[1] ? SX[0] : SX[1]) - 1;
+  int cmax = (int)ceil(SX[0] > SX[1] ? SX[0] : SX[1]) + 1;
+  int rmin = (int)floor(SY[0] < SY[1] ? SY[0] : SY[1]) - 1;
+  int rmax = (int)ceil(SY[0] > SY[1] ? SY[0] : SY[1]) + 1;
+  cmin = cmin > 0 ? cmin : 0;
+  cmax = cmax < ncol-1 ? cmax : ncol-1;
+  rmin = rmin > 0 ? rmin : 0;
+  rmax = rmax < nrow-1 ? rmax : nrow-1;
+  for (int r = rmin; r < rmax; r++) {
+    for (int c = cmin; c < cmax; c++) {
+      const double va[3][3] = {
+        {dx*c-size[0], dy*r-size[1], data[r*ncol+c]*size[2]},
+        {dx*(c+1)-size[0], dy*(r+1)-size[1], data[(r+1)*ncol+(c+1)]*size[2]},
+        {dx*(c+1)-size[0], dy*r-size[1], data[r*ncol+(c+1)]*size[2]}};
+      double sol = rayTriangle(va, lpnt, lvec, b0, b1);
+      if (sol >= 0 && (x < 0 || sol < x)) x = sol;
+      const double vb[3][3] = {
+        {dx*c-size[0], dy*r-size[1], data[r*ncol+c]*size[2]},
+        {dx*(c+1)-size[0], dy*(r+1)-size[1], data[(r+1)*ncol+(c+1)]*size[2]},
+        {dx*c-size[0], dy*(r+1)-size[1], data[(r+1)*ncol+c]*size[2]}};
+      sol = rayTriangle(vb, lpnt, lvec, b0, b1);
+      if (sol >= 0 && (x < 0 || sol < x)) x = sol;
+    }
+  }
+  for (int i = 0; i < 4; i++) {
+    if (all[i] >= 0 && (all[i] < x || x < 0)) {
+      const double z = (lpnt[2] + all[i]*lvec[2]) / size[2];
+      double y, y0, z0, z1;
+      if (i < 2) {
+        y = (lpnt[1] + all[i]*lvec[1] + size[1]) / dy;
+        y0 = floor(y) < nrow-2 ? floor(y) : nrow-2;
+        y0 = y0 > 0 ? y0 : 0;
+        z0 = (double)data[(int)round(y0)*nrow + (i == 1 ? ncol-1 : 0)];
+        z1 = (double)data[(int)round(y0+1)*nrow + (i == 1 ? ncol-1 : 0)];
+      } else {
+        y = (lpnt[0] + all[i]*lvec[0] + size[0]) / dx;
+        y0 = floor(y) < ncol-2 ? floor(y) : ncol-2;
+        y0 = y0 > 0 ? y0 : 0;
+        z0 = (double)data[(int)round(y0) + (i == 3 ? (nrow-1)*ncol : 0)];
+        z1 = (double)data[(int)round(y0+1) + (i == 3 ? (nrow-1)*ncol : 0)];
+      }
+      if (z < z0*(y0+1-y) + z1*(y-y0)) x = all[i];
+    }
+  }
+  return x;
+}
+
+// mj_rayMesh :800-813: the bounding box, then every face (mju_rayTree :628-730 visits the
+// faces whose bounding volumes the ray crosses; the nearest hit over all faces is the same)
+MJH_HD double rayMesh(const mjhipModel& m, int id, const double xpos[3], const double xmat[9],
+                      const double* pnt, const double* vec) {
+  double all[6];
+  if (rayBoxAll(xpos, xmat, m.geom_size + 3*id, pnt, vec, all) < 0) return -1;
+  const int mid = m.geom_dataid[id];
+  double lpnt[3], lvec[3], b0[3], b1[3];
+  rayMap(xpos, xmat, pnt, vec, lpnt, lvec);
+  rayBasis(lvec, b0, b1);
+  double x = -1;
+  for (int f = m.mesh_faceadr[mid]; f < m.mesh_faceadr[mid] + m.mesh_facenum[mid]; f++) {
+    double v[3][3];
+    for (int i = 0; i < 3; i++) {
+      const float* vf = m.mesh_vert + 3*(m.mesh_face[3*f + i] + m.mesh_vertadr[mid]);
+      for (int j = 0; j < 3; j++) v[i][j] = (double)vf[j];
+    }
+    const double sol = rayTriangle(v, lpnt, lvec, b0, b1);
+    if (sol >= 0 && (x < 0 || sol < x)) x = sol;
+  }
+  return x;
+}
+
 // the rangefinder (engine_sensor.c mjSENS_RANGEFINDER): mj_ray from the site along its z
 // axis, geomgroup NULL, flg_static 1, the site's body excluded
 // :69-100 ray_eliminate (geomgroup NULL, flg_static 1): the excluded body and invisible geoms
@@ -6542,7 +7606,10 @@ MJH_HD double ray(const mjhipModel& m, const Lane<S>& d, const double pnt[3],
     double pos[3], mat[9];
     for (int k = 0; k < 3; k++) pos[k] = d.geom_xpos[3*g+k];
     for (int k = 0; k < 9; k++) mat[k] = d.geom_xmat[9*g+k];
-    const double nd = rayGeom(pos, mat, m.geom_size + 3*g, pnt, vec, m.geom_type[g]);
+    const int t = m.geom_type[g];
+    const double nd = t == mjhipGEOM_MESH ? rayMesh(m, g, pos, mat, pnt, vec) :
+                      t == mjhipGEOM_HFIELD ? rayHfield(m, g, pos, mat, pnt, vec) :
+                      rayGeom(pos, mat, m.geom_size + 3*g, pnt, vec, t);
     if (nd >= 0 && (nd < dist || dist < 0)) dist = nd;
   }
   return dist;

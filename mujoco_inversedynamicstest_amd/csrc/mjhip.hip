@@ -323,7 +323,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
                     (P.t2 == mjhipGEOM_BOX || P.t2 == mjhipGEOM_CYLINDER)) ||
                    (P.t1 == mjhipGEOM_BOX && P.t2 == mjhipGEOM_BOX)) {
           num = -1;                         // plane : box / cylinder, box : box: counts, then stores
-          mjh::collidePlaneBoxCyl<64, false, BOX>(m, d, g1, g2, margin, cnt, &st, bbuf);
+          mjh::collidePlaneBoxCyl<64, false, BOX, false>(m, d, g1, g2, margin, cnt, &st, bbuf);
         } else {
           num = mjh::narrowPrimitive(P.t1, P.t2, margin, (const double*)(gx + 3*g1),
                                      (const double*)(gm + 9*g1), gsize + 3*g1,
@@ -337,7 +337,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       if (cnt) {
         int c = ncon + excl;
         if (num < 0) {
-          mjh::collidePlaneBoxCyl<64, true, BOX>(m, d, g1, g2, margin, c, &st, bbuf);
+          mjh::collidePlaneBoxCyl<64, true, BOX, false>(m, d, g1, g2, margin, c, &st, bbuf);
         } else {
           mjh::storeContacts<64>(m, d, g1, g2, margin, cp, raw, num, c, &st);
         }
@@ -1184,19 +1184,17 @@ static const char* unsupported(const mjhipModel* m) {
           const bool ccd = mjhip_isConvexPair(t1, t2) ||
                            (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX);
           if ((ccd && !nccd) || (!ccd && mjhip_pairMaxContacts(m, t1, t2) < 0)) {
-            return "a geom-distance sensor on a mesh, height field or SDF geom, or on a "
+            return "a geom-distance sensor on a height field or SDF geom, or on a "
                    "convex pair with the native CCD solver disabled";
           }
         }
       }
     }
-    if (t == mjhSENS_RANGEFINDER) {   // mj_ray's mesh, height-field and SDF paths are not built
+    if (t == mjhSENS_RANGEFINDER) {   // mj_ray's SDF path is not built
       const int body = m->site_bodyid[m->sensor_objid[i]];
       for (int g = 0; g < m->ngeom; g++) {
-        const int gt = m->geom_type[g];
-        if ((gt == mjhipGEOM_MESH || gt == mjhipGEOM_HFIELD || gt == mjhipGEOM_SDF) &&
-            !mjh::rayEliminate(*m, g, body)) {
-          return "a rangefinder that can see a mesh, height field or SDF geom";
+        if (m->geom_type[g] == mjhipGEOM_SDF && !mjh::rayEliminate(*m, g, body)) {
+          return "a rangefinder that can see an SDF geom";
         }
       }
     }
@@ -1417,7 +1415,7 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   }
   // the native convex solver keeps its polytope in the instance's scratch: one lane per
   // instance (the cooperative kernel would run several pairs of an instance at once)
-  if (mjh_needConvex(m)) c->coop = 0;
+  if (mjh_needConvex(m) || m->nmesh || m->nhfield) c->coop = 0;
   c->spatial = mjh::hasSpatial(*m);
   // the cooperative kernel's per-dof chain masks are 64-bit
   if (m->nv > 64) c->coop = 0;

@@ -12,7 +12,8 @@ The format is the one of src/engine/engine_io.c (MuJoCo 3.3.1):
 The field table below is the mjModel layout of include/mujoco/mjxmacro.h (MJMODEL_INTS,
 MJMODEL_POINTERS) written as a compact list: the file is a byte-exact dump of the model
 arrays in that order, so reading it needs every array's type and shape, including the ones
-(meshes, textures, flexes, skins, ...) that the inverse-dynamics path never reads.
+(textures, flexes, skins, mesh normals and polygons, ...) that the inverse-dynamics path never
+reads. Collision meshes (vertices, faces, convex-hull graph) and height fields are read.
 
 `read` returns the same compiled-model object the MJCF loader produces (mjcf.Model), with the
 sparse structures the reference derives in mj_makeData (C, D, B, mapM2C, mapM2D, moment
@@ -450,6 +451,16 @@ def unsupported(ints, arrays) -> str | None:
     return "plugins"
   if ints["nwrap"] and not np.isin(arrays["wrap_type"], (1, 2, 3, 4, 5)).all():
     return "unknown tendon wrap object type"
+  if ints["nu"]:
+    dyn = np.asarray(arrays["actuator_dyntype"]).reshape(-1)
+    gain = np.asarray(arrays["actuator_gaintype"]).reshape(-1)
+    kv = np.asarray(arrays["actuator_gainprm"]).reshape(ints["nu"], -1)[:, 2]
+    if np.any((dyn != 0) & (gain == 1) & (kv != 0)):
+      return "an affine velocity gain with activation dynamics (reads mjData.act)"
+    if np.any(gain >= 2) or np.any(np.asarray(arrays["actuator_biastype"]) >= 2):
+      return "muscle or user actuator gain/bias"
+  if ints["ngeom"] and np.any(np.asarray(arrays["geom_type"]) == 8):
+    return "SDF geoms"
   return None
 
 

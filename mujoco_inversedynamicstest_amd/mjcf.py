@@ -341,7 +341,7 @@ class _Defaults:
     return out
 
 
-ACTUATOR_TAGS = ("general", "motor", "position", "velocity", "adhesion")
+ACTUATOR_TAGS = ("general", "motor", "position", "velocity", "intvelocity", "adhesion")
 
 
 def _resolve_orientation(attrs, degree, eulerseq, quat):
@@ -463,8 +463,16 @@ class Model:
     m.opt.setdefault("magnetic", [0.0, -0.5, 0.0])                      # mjOption default
     m.opt.setdefault("ccd_tolerance", 1e-6)                             # engine_io.c:128
     m.opt.setdefault("ccd_iterations", 50)                              # engine_io.c:160
+    for k in fields.MODEL_SIZES:               # sizes added to the table after the file
+      m.sizes.setdefault(k, 0)
     for f in fields.MODEL_FIELDS:
-      setattr(m, f.name, np.ascontiguousarray(z[f.name]))
+      if f.name in z.files:
+        setattr(m, f.name, np.ascontiguousarray(z[f.name]))
+      else:                                    # a field added after the file: its empty value
+        shape = f.shape(m.sizes)
+        fill = -1 if f.name == "geom_dataid" or f.name == "mesh_graphadr" else 0
+        a = np.full(shape if shape[1] != 1 else shape[:1], fill, dtype=fields.NPTYPE[f.ctype])
+        setattr(m, f.name, a)
     return m
 
 
@@ -497,6 +505,8 @@ class MJCFCompiler:
     self.actuators = []
     self.sensors = []
     self.materials = {}                 # name -> rgba (<asset><material>)
+    self.meshes = {}                    # name -> meshes.Mesh (<asset><mesh>)
+    self.hfields = {}                   # name -> meshes.HField (<asset><hfield>)
     self.equalities = []
     self.excludes = []
     self.keys = []
@@ -638,8 +648,8 @@ class MJCFCompiler:
             raise MJCFError(f"unknown sensor <{ch.tag}>")
           self.sensors.append((ch.tag, dict(ch.attrib)))
       elif t == "asset":
-        # materials matter to mj_ray's visibility test (engine_ray.c:76-84); the rest of the
-        # assets has no effect on the inverse-dynamics path
+        # materials matter to mj_ray's visibility test (engine_ray.c:76-84); meshes and height
+        # fields are collision geometry (meshes.py); textures have no effect on the path
         for ch in el:
           if ch.tag == "material":
             a = self._elem_attrs(ch, "material", None)
@@ -647,10 +657,59 @@ class MJCFCompiler:
             v = _floats(a["rgba"]) if "rgba" in a else []
             rgba[:len(v)] = v
             self.materials[a.get("name", f"__material{len(self.materials)}")] = rgba
-      elif t in ("visual", "statistic", "default", "compiler", "size", "extension"):
+          elif ch.tag == "mesh":
+            self._parse_mesh(ch)
+          elif ch.tag == "hfield":
+            self._parse_hfield(ch)
+          elif ch.tag == "texture":
+            continue
+          else:
+            raise MJCFError(f"unsupported asset <{ch.tag}>")
+      elif t in ("visual", "statistic", "default", "compiler", "size", "extension", "custom"):
         continue  # no effect on the inverse-dynamics path
       else:
         raise MJCFError(f"unsupported top-level element <{t}>")
+
+  def _parse_mesh(self, el):
+    """<mesh> with inline vertex (and optional face) data (xml_native_reader.cc:1405-1480);
+    mesh files are not read (no file assets on the path)."""
+    from . import meshes
+    a = self._elem_attrs(el, "mesh", None)
+    if "file" in a:
+      raise MJCFError("mesh files are not in the supported subset (give vertex data)")
+    if "vertex" not in a:
+      raise MJCFError("mesh needs vertex data")
+    name = a.get("name", f"__mesh{len(self.meshes)}")
+    inertia = a.get("inertia", "legacy")
+    if inertia not in ("convex", "legacy", "exact", "shell"):
+      raise MJCFError(f"invalid mesh inertia '{inertia}'")
+    cls = el.get("class", "main")
+    try:
+      self.meshes[name] = meshes.Mesh(
+          name, np.array(a["vertex"].split(), dtype=np.float32),
+          face=[int(x) for x in a["face"].split()] if "face" in a else None,
+          scale=_floats(a["scale"]) if "scale" in a else (1, 1, 1),
+          refpos=_floats(a["refpos"]) if "refpos" in a else (0, 0, 0),
+          refquat=_floats(a["refquat"]) if "refquat" in a else (1, 0, 0, 0),
+          inertia=inertia, maxhullvert=int(a.get("maxhullvert", -1)))
+    except meshes.MeshError as e:
+      raise MJCFError(str(e)) from e
+    # Process() weighs the mesh with its class's default geom density (user_mesh.cc:1466)
+    self.meshes[name].density = float(self.classes[cls].get("geom").get("density", "1000"))
+
+  def _parse_hfield(self, el):
+    """<hfield> with inline elevation (xml_native_reader.cc:3249-3300)."""
+    from . import meshes
+    a = dict(el.attrib)
+    if "file" in a:
+      raise MJCFError("hfield files are not in the supported subset (give elevation data)")
+    name = a.get("name", f"__hfield{len(self.hfields)}")
+    try:
+      self.hfields[name] = meshes.HField(
+          name, int(a.get("nrow", 0)), int(a.get("ncol", 0)), _floats(a.get("size", "")),
+          np.array(a["elevation"].split(), dtype=np.float32) if "elevation" in a else None)
+    except meshes.MeshError as e:
+      raise MJCFError(str(e)) from e
 
   def _parse_option(self, el):
     a = el.attrib
@@ -747,8 +806,41 @@ class MJCFCompiler:
     else:
       quat = _resolve_orientation(a, self.degree, self.eulerseq, quat)
     t = g["type"]
-    if t == GEOM["mesh"] or t == GEOM["hfield"] or t == GEOM["sdf"]:
-      raise MJCFError("mesh/hfield/sdf geoms are not in the supported subset")
+    if t == GEOM["sdf"]:
+      raise MJCFError("sdf geoms are not in the supported subset")
+    # mesh and height-field references (mjCGeom::Compile, user_objects.cc:2932-3041)
+    mesh = hfield = None
+    g["dataid"] = -1
+    if "mesh" in a:
+      if a["mesh"] not in self.meshes:
+        raise MJCFError(f"mesh '{a['mesh']}' not found in geom")
+      mesh = self.meshes[a["mesh"]]
+      if t != GEOM["mesh"]:
+        raise MJCFError("fitting a primitive geom to a mesh is not in the supported subset")
+      if "fromto" in a:
+        raise MJCFError("fromto cannot be used with mesh geom")
+      g["dataid"] = list(self.meshes).index(a["mesh"])
+    if t == GEOM["mesh"] and mesh is None:
+      raise MJCFError("mesh geom must have valid meshid")
+    if "hfield" in a:
+      if a["hfield"] not in self.hfields:
+        raise MJCFError(f"hfield '{a['hfield']}' not found in geom")
+      hfield = self.hfields[a["hfield"]]
+      g["dataid"] = list(self.hfields).index(a["hfield"])
+    if (t == GEOM["hfield"]) != (hfield is not None):
+      raise MJCFError("hfield geom must have valid hfieldid")
+    if mesh is not None:                 # mjuu_frameaccum(pos, quat, mesh pos, mesh quat)
+      mat = quat2mat(quat)
+      mp = mesh.pos
+      vec = mulvecmat(mp, mat)
+      pos = [pos[0] + vec[0], pos[1] + vec[1], pos[2] + vec[2]]
+      quat = mulquat(quat, mesh.quat)
+      aamm = mesh.aamm
+      size = [max(abs(aamm[0]), abs(aamm[3])), max(abs(aamm[1]), abs(aamm[4])),
+              max(abs(aamm[2]), abs(aamm[5]))]
+    elif hfield is not None:
+      hs = hfield.size
+      size = [hs[0], hs[1], 0.25*hs[2] + 0.5*hs[3]]
     g["size"] = size
     g["pos"] = pos
     g["quat"] = quat
@@ -785,20 +877,36 @@ class MJCFCompiler:
     g["mass"] = 0.0
     g["inertia"] = [0.0, 0.0, 0.0]
     if inferinertia:
-      vol = _geom_volume(t, size)
+      vol = mesh.volume if mesh is not None else _geom_volume(t, size)
+
+      def inertia(mass):
+        if mesh is None:
+          return _geom_inertia(t, size, mass)
+        bs = mesh.boxsz                   # the mesh's equivalent inertia box
+        return [mass * (bs[1]*bs[1] + bs[2]*bs[2]) / 3, mass * (bs[0]*bs[0] + bs[2]*bs[2]) / 3,
+                mass * (bs[0]*bs[0] + bs[1]*bs[1]) / 3]
       if "mass" in a:
         mass = float(a["mass"])
         if mass == 0:
           g["mass"] = 0.0
         elif vol > mjEPS:
           g["mass"] = mass
-          g["inertia"] = _geom_inertia(t, size, mass)
+          g["inertia"] = inertia(mass)
       else:
         density = float(a.get("density", 1000.0))
         if density != 0:
           g["mass"] = density * vol
-          g["inertia"] = _geom_inertia(t, size, g["mass"])
-    g["rbound"] = _geom_rbound(t, size)
+          g["inertia"] = inertia(g["mass"])
+    if mesh is not None:                 # GetRBound (user_objects.cc:2723-2729)
+      aamm = mesh.aamm
+      h = [max(abs(aamm[0]), abs(aamm[3])), max(abs(aamm[1]), abs(aamm[4])),
+           max(abs(aamm[2]), abs(aamm[5]))]
+      g["rbound"] = math.sqrt(h[0]*h[0] + h[1]*h[1] + h[2]*h[2])
+    elif hfield is not None:             # (:2703-2706)
+      hs = hfield.size
+      g["rbound"] = math.sqrt(hs[0]*hs[0] + hs[1]*hs[1] + max(hs[2]*hs[2], hs[3]*hs[3]))
+    else:
+      g["rbound"] = _geom_rbound(t, size)
     # fluid-interaction coefficients (user_objects.cc:3081-3084)
     g["fluid"] = _fluid_coefs(t, size, g["fluid_ellipsoid"], g["fluid_coefs"]) \
         if g["fluid_ellipsoid"] > 0 else [0.0] * 12
@@ -810,6 +918,21 @@ class MJCFCompiler:
     self._order_bodies()
     bodies = self.bodies
     nbody = len(bodies)
+    # meshes before geoms (mjCModel::TryCompile, user_model.cc:4269-4290): a mesh gets its
+    # convex-hull graph when a collidable mesh geom uses it or its inertia is "convex"
+    from . import meshes
+    for b in bodies:
+      for ga in b.geoms:
+        if ga.get("type") == "mesh" and ga.get("mesh") in self.meshes:
+          mesh = self.meshes[ga["mesh"]]
+          if (int(ga.get("contype", 1)) or int(ga.get("conaffinity", 1)) or
+              mesh.inertia == "convex"):
+            mesh.needhull = True
+    for mesh in self.meshes.values():
+      try:
+        mesh.compile(mesh.density)
+      except meshes.MeshError as e:
+        raise MJCFError(str(e)) from e
     # ---- per-body compile (mjCBody::Compile)
     jnts, geoms, sites, cams, lights = [], [], [], [], []
     for b in bodies:
@@ -1221,8 +1344,10 @@ class MJCFCompiler:
     matrgba = arr("mat_rgba", (len(matnames), 4), np.float32)
     for mi, name in enumerate(matnames):
       matrgba[mi] = self.materials[name]
+    gdataid = arr("geom_dataid", ng, np.int32, -1)
     for gi, g in enumerate(geoms):
       b = bodies[g["body"]]
+      gdataid[gi] = g["dataid"]
       if geomadr[b.id] < 0:
         geomadr[b.id] = gi
       g_int["type"][gi] = g["type"]
@@ -1254,6 +1379,41 @@ class MJCFCompiler:
       bcontype[b.id] |= g["contype"]
       bconaff[b.id] |= g["conaffinity"]
       bmargin[b.id] = max(bmargin[b.id], g["margin"])
+    # meshes and height fields (user_model.cc:2785-2830, hfield arrays alike)
+    mlist, hlist = list(self.meshes.values()), list(self.hfields.values())
+    s.update(nmesh=len(mlist), nmeshvert=sum(x.nvert for x in mlist),
+             nmeshface=sum(x.nface for x in mlist),
+             nmeshgraph=sum(len(x.graph) if x.graph else 0 for x in mlist),
+             nhfield=len(hlist), nhfielddata=sum(x.nrow*x.ncol for x in hlist))
+    mva = arr("mesh_vertadr", len(mlist), np.int32)
+    mvn = arr("mesh_vertnum", len(mlist), np.int32)
+    mfa = arr("mesh_faceadr", len(mlist), np.int32)
+    mfn = arr("mesh_facenum", len(mlist), np.int32)
+    mga = arr("mesh_graphadr", len(mlist), np.int32, -1)
+    mvert = arr("mesh_vert", (s["nmeshvert"], 3), np.float32)
+    mface = arr("mesh_face", (s["nmeshface"], 3), np.int32)
+    mgraph = arr("mesh_graph", s["nmeshgraph"], np.int32)
+    va = fa = ga_ = 0
+    for mi, x in enumerate(mlist):
+      mva[mi], mvn[mi], mfa[mi], mfn[mi] = va, x.nvert, fa, x.nface
+      mvert[va:va + x.nvert] = x.vert.reshape(-1, 3)
+      mface[fa:fa + x.nface] = x.face.reshape(-1, 3)
+      if x.graph:
+        mga[mi] = ga_
+        mgraph[ga_:ga_ + len(x.graph)] = x.graph
+        ga_ += len(x.graph)
+      va += x.nvert
+      fa += x.nface
+    hsz = arr("hfield_size", (len(hlist), 4), np.float64)
+    hnr = arr("hfield_nrow", len(hlist), np.int32)
+    hnc = arr("hfield_ncol", len(hlist), np.int32)
+    hadr = arr("hfield_adr", len(hlist), np.int32)
+    hdata = arr("hfield_data", s["nhfielddata"], np.float32)
+    da = 0
+    for hi, x in enumerate(hlist):
+      hsz[hi], hnr[hi], hnc[hi], hadr[hi] = x.size, x.nrow, x.ncol, da
+      hdata[da:da + x.nrow*x.ncol] = x.data
+      da += x.nrow*x.ncol
     # sites
     ns = len(sites)
     stype = arr("site_type", ns, np.int32)
@@ -1501,6 +1661,11 @@ class MJCFCompiler:
         if dyn not in ("none", "integrator", "filter", "filterexact"):
           raise MJCFError(f"actuator dyntype '{dyn}' is not in the supported subset")
         adyn[ai] = {"none": 0, "integrator": 1, "filter": 2, "filterexact": 3}[dyn]
+        if adyn[ai] and again[ai] == 1 and againprm[ai, 2] != 0:
+          # mjd_actuator_vel (engine_derivative.c:855-863) multiplies the velocity gain by
+          # mjData.act[last] for such an actuator; act is not an input of this path
+          raise MJCFError("an affine velocity gain with activation dynamics is not in the "
+                          "supported subset")
         if "dynprm" in a:
           v = _floats(a["dynprm"])
           adynprm[ai, :len(v)] = v
@@ -1549,6 +1714,15 @@ class MJCFCompiler:
         againprm[ai, 0] = kv
         abias[ai] = 1
         abiasprm[ai, 2] = -kv
+      elif tag == "intvelocity":        # mjs_setToIntVelocity: an integrator driving a
+        kp = float(a.get("kp", 1.0))    # position servo on the activation
+        kv = float(a.get("kv", 0.0))
+        adyn[ai] = 1
+        againprm[ai, 0] = kp
+        abias[ai] = 1
+        abiasprm[ai, 1] = -kp
+        abiasprm[ai, 2] = -kv
+        na_count += 1
       elif tag == "adhesion":           # xml_native_reader.cc:2341-2356
         againprm[ai, 0] = float(a.get("gain", 1.0))
         if againprm[ai, 0] < 0:
@@ -2057,7 +2231,7 @@ def _geom_inertia(t, size, mass):
     s = size
     return [mass * (s[1]*s[1] + s[2]*s[2]) / 5, mass * (s[0]*s[0] + s[2]*s[2]) / 5,
             mass * (s[0]*s[0] + s[1]*s[1]) / 5]
-  if t == GEOM["box"]:
+  if t in (GEOM["box"], GEOM["hfield"]):
     s = size
     return [mass * (s[1]*s[1] + s[2]*s[2]) / 3, mass * (s[0]*s[0] + s[2]*s[2]) / 3,
             mass * (s[0]*s[0] + s[1]*s[1]) / 3]

@@ -2597,6 +2597,15 @@ typedef struct {
   const mjtNum* mat;
   const mjtNum* size;
   mjtNum margin;
+  /* mesh geoms: the mesh's float vertices and convex-hull graph (NULL: none), and the
+     warm starts the supports keep between calls (mjCCDObj.vertindex / meshindex) */
+  const float* vert;
+  int nvert;
+  const int* graph;
+  int vertindex, meshindex;
+  /* height-field prism (mjCCDObj.prism) and its centre (mjc_prism_center) */
+  mjtNum prism[6][3];
+  mjtNum pcenter[3];
 } orShape;
 
 /* mulMatTVec3 / localToGlobal of engine_collision_convex.c:122-141 */
@@ -2618,9 +2627,80 @@ static void ccd_toGlobal(mjtNum r[3], const mjtNum* mat, const mjtNum t[3], cons
 static mjtNum ccd_sign(mjtNum x) { return x < 0 ? -1 : (x > 0 ? 1 : 0); }
 
 /* the native support functions (convex.c:146-327) */
-static void ccd_support1(mjtNum r[3], const orShape* s, const mjtNum dir[3]) {
+/* dot product between mjtNum and float (convex.c:332-334) */
+static mjtNum ccd_dot3f(const mjtNum a[3], const float b[3]) {
+  return a[0]*(mjtNum)b[0] + a[1]*(mjtNum)b[1] + a[2]*(mjtNum)b[2];
+}
+
+/* mjc_meshSupport (:339-382, exhaustive) and mjc_hillclimbSupport (:387-433), as
+   mjc_initCCDObj (:735-743) picks them: hill climbing on the hull graph from mjMESH_HILLCLIMB_MIN
+   (10) vertices */
+static void ccd_meshSupport(mjtNum r[3], orShape* s, const mjtNum dir[3]) {
+  mjtNum ld[3], t[3];
+  ccd_toLocal(ld, s->mat, dir);
+  const float* V = s->vert;
+  int imax;
+  if (!s->graph || s->nvert < 10) {
+    mjtNum max = -FLT_MAX;
+    imax = 0;
+    if (s->vertindex >= 0) {
+      imax = s->vertindex;
+      max = ccd_dot3f(ld, V + 3*imax);
+    }
+    for (int i = 0; i < s->nvert; i++) {
+      mjtNum vdot = ccd_dot3f(ld, V + 3*i);
+      if (vdot > max) {
+        max = vdot;
+        imax = i;
+      }
+    }
+    s->vertindex = imax;
+  } else {
+    const int numvert = s->graph[0];
+    const int* edgeadr = s->graph + 2;
+    const int* globalid = s->graph + 2 + numvert;
+    const int* localid = s->graph + 2 + 2*numvert;
+    mjtNum max = -FLT_MAX;
+    int prev;
+    imax = s->meshindex < 0 ? 0 : s->meshindex;
+    do {
+      prev = imax;
+      for (int i = edgeadr[imax]; localid[i] >= 0; i++) {
+        mjtNum vdot = ccd_dot3f(ld, V + 3*globalid[localid[i]]);
+        if (vdot > max) {
+          max = vdot;
+          imax = localid[i];
+        }
+      }
+    } while (imax != prev);
+    s->meshindex = imax;
+    imax = globalid[imax];
+    s->vertindex = imax;
+  }
+  t[0] = (mjtNum)V[3*imax];
+  t[1] = (mjtNum)V[3*imax + 1];
+  t[2] = (mjtNum)V[3*imax + 2];
+  ccd_toGlobal(r, s->mat, t, s->pos);
+}
+
+static void ccd_support1(mjtNum r[3], orShape* s, const mjtNum dir[3]) {
   mjtNum ld[3], t[3];
   switch (s->kind) {
+  case mjhipGEOM_MESH:
+    ccd_meshSupport(r, s, dir);
+    return;
+  case mjhipGEOM_HFIELD: {             /* mjc_prism_support (:438-455) */
+    int istart = dir[2] < 0 ? 0 : 3, ibest = istart;
+    mjtNum best = mju_dot3(s->prism[istart], dir), tmp;
+    for (int i = istart + 1; i < istart + 3; i++) {
+      if ((tmp = mju_dot3(s->prism[i], dir)) > best) {
+        ibest = i;
+        best = tmp;
+      }
+    }
+    mju_copy3(r, s->prism[ibest]);
+    return;
+  }
   case CCD_POINT:
     mju_copy3(r, s->pos);
     return;
@@ -2684,7 +2764,7 @@ static void ccd_support1(mjtNum r[3], const orShape* s, const mjtNum dir[3]) {
 }
 
 /* support (gjk.c:277-296): each shape inflated by half its margin */
-static void ccd_support(orVtx* v, const orShape* a, const orShape* b, const mjtNum dir[3],
+static void ccd_support(orVtx* v, orShape* a, orShape* b, const mjtNum dir[3],
                         const mjtNum ndir[3]) {
   ccd_support1(v->p1, a, dir);
   if (a->margin > 0) {
@@ -2925,7 +3005,7 @@ static mjtNum ccd_faceDist(mjtNum n[3], const orVtx* a, const orVtx* b, const or
   return mjhipMAXVAL;
 }
 
-static int ccd_intersect(orCCD* st, const orShape* A, const orShape* B) {
+static int ccd_intersect(orCCD* st, orShape* A, orShape* B) {
   orVtx s[4] = {st->simplex[0], st->simplex[1], st->simplex[2], st->simplex[3]};
   int o[4] = {0, 1, 2, 3};
   int k = st->iters;
@@ -2965,13 +3045,17 @@ static int ccd_intersect(orCCD* st, const orShape* A, const orShape* B) {
 }
 
 /* gjk (gjk.c:163-272) */
-static void ccd_gjk(orCCD* st, const orShape* A, const orShape* B) {
+static void ccd_gjk(orCCD* st, orShape* A, orShape* B) {
   const int get_dist = st->cutoff > 0;
   int backup = !get_dist, n = 0, k = 0;
   orVtx* S = st->simplex;
   mjtNum x[3], lam[4] = {1, 0, 0, 0}, cut2 = st->cutoff*st->cutoff;
-  const int discrete = A->margin == 0 && B->margin == 0 && A->gtype == mjhipGEOM_BOX &&
-                       B->gtype == mjhipGEOM_BOX;
+  /* discreteGeoms (gjk.c:150-158) */
+  const int dA = A->gtype == mjhipGEOM_BOX || A->gtype == mjhipGEOM_MESH ||
+                 A->gtype == mjhipGEOM_HFIELD;
+  const int dB = B->gtype == mjhipGEOM_BOX || B->gtype == mjhipGEOM_MESH ||
+                 B->gtype == mjhipGEOM_HFIELD;
+  const int discrete = A->margin == 0 && B->margin == 0 && dA && dB;
   const mjtNum eps = discrete ? 0 : st->tol*st->tol;
   mju_sub3(x, st->x1, st->x2);
   for (; k < st->kmax; k++) {
@@ -3078,7 +3162,7 @@ static int ccd_addVertex(orPoly* P, const orVtx* v) {
 }
 
 /* epaSupport (:328-353) */
-static int ccd_newVertex(orPoly* P, const orShape* A, const orShape* B, const mjtNum d[3],
+static int ccd_newVertex(orPoly* P, orShape* A, orShape* B, const mjtNum d[3],
                          mjtNum dn) {
   mjtNum dir[3] = {1, 0, 0}, ndir[3] = {-1, 0, 0};
   if (dn > mjMINVAL) {
@@ -3167,7 +3251,7 @@ static int ccd_onTriangle(const mjtNum a[3], const mjtNum b[3], const mjtNum c[3
 }
 
 /* polytope3 (:1040-1117) */
-static int ccd_fromTriangle(orPoly* P, orCCD* st, const orShape* A, const orShape* B) {
+static int ccd_fromTriangle(orPoly* P, orCCD* st, orShape* A, orShape* B) {
   const mjtNum *a = st->simplex[0].v, *b = st->simplex[1].v, *c = st->simplex[2].v;
   mjtNum e1[3], e2[3], n[3], nn[3];
   mju_sub3(e1, b, a);
@@ -3214,7 +3298,7 @@ static void ccd_rot120(mjtNum R[9], const mjtNum axis[3]) {
 }
 
 /* polytope2 (:892-971) */
-static int ccd_fromSegment(orPoly* P, orCCD* st, const orShape* A, const orShape* B) {
+static int ccd_fromSegment(orPoly* P, orCCD* st, orShape* A, orShape* B) {
   const mjtNum *a = st->simplex[0].v, *b = st->simplex[1].v;
   mjtNum d[3];
   mju_sub3(d, b, a);
@@ -3256,7 +3340,7 @@ static int ccd_fromSegment(orPoly* P, orCCD* st, const orShape* A, const orShape
 }
 
 /* polytope4 (:1122-1156) */
-static int ccd_fromTetra(orPoly* P, orCCD* st, const orShape* A, const orShape* B) {
+static int ccd_fromTetra(orPoly* P, orCCD* st, orShape* A, orShape* B) {
   int i1 = ccd_addVertex(P, st->simplex + 0);
   int i2 = ccd_addVertex(P, st->simplex + 1);
   int i3 = ccd_addVertex(P, st->simplex + 2);
@@ -3328,7 +3412,7 @@ static void ccd_horizon(orPoly* P, int f) {
 }
 
 /* epa (:1329-1459) + epaWitness (:1300-1323); returns the face or -1 */
-static int ccd_epa(orCCD* st, orPoly* P, const orShape* A, const orShape* B) {
+static int ccd_epa(orCCD* st, orPoly* P, orShape* A, orShape* B) {
   mjtNum lower, upper = FLT_MAX;
   int f = -1, pf = -1, k;
   P->nh = 0;
@@ -3402,9 +3486,21 @@ static int ccd_epa(orCCD* st, orPoly* P, const orShape* A, const orShape* B) {
 /* mjc_ccd (:2215-2343) with max_contacts = 1 and the distance cutoff `cutoff` (0 for contacts,
  * mjc_Convex; the distance bound for mj_geomDistanceCCD); the geoms' margins are in
  * A->margin / B->margin */
+/* obj->center: the geom position (mjc_center :78-98), or a prism's mean vertex
+   (mjc_prism_center :103-110) */
+static void ccd_center(mjtNum c[3], const orShape* s) {
+  if (s->gtype == mjhipGEOM_HFIELD) {
+    mju_zero3(c);
+    for (int i = 0; i < 6; i++) mju_addTo3(c, s->prism[i]);
+    mju_scl3(c, c, 1.0/6.0);
+  } else {
+    mju_copy3(c, s->pos);
+  }
+}
+
 static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol, mjtNum cutoff) {
-  mju_copy3(st->x1, A->pos);
-  mju_copy3(st->x2, B->pos);
+  ccd_center(st->x1, A);
+  ccd_center(st->x2, B);
   st->iters = 0;
   st->tol = tol;
   st->kmax = kmax;
@@ -3449,8 +3545,8 @@ static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol, mj
       return st->dist;
     }
     st->iters = 0;
-    mju_copy3(st->x1, A->pos);
-    mju_copy3(st->x2, B->pos);
+    ccd_center(st->x1, A);
+    ccd_center(st->x2, B);
   }
   ccd_gjk(st, A, B);
   if (st->dist <= tol && st->nsimplex > 1) {
@@ -3482,6 +3578,16 @@ static void or_shape(orShape* s, const mjhipModel* m, const mjhipData* d, int g,
   s->mat = d->geom_xmat + 9*g;
   s->size = m->geom_size + 3*g;
   s->margin = margin;
+  s->vert = NULL;
+  s->graph = NULL;
+  s->nvert = 0;
+  s->vertindex = s->meshindex = -1;
+  if (s->gtype == mjhipGEOM_MESH) {
+    const int id = m->geom_dataid[g];
+    s->vert = m->mesh_vert + 3*m->mesh_vertadr[id];
+    s->nvert = m->mesh_vertnum[id];
+    s->graph = m->mesh_graphadr[id] >= 0 ? m->mesh_graph + m->mesh_graphadr[id] : NULL;
+  }
 }
 
 /* mjc_Convex (convex.c:915-1001) through mjc_CCDIteration (:792-819), native solver, one
@@ -3504,22 +3610,144 @@ static int col_convex(orRaw* c, const mjhipModel* m, const mjhipData* d, int g1,
   return 1;
 }
 
-/* mjc_PlaneConvex (convex.c:1045-1080) for a geom without mesh data (the ellipsoid): the
- * libccd support (mjccd_support :501-704) of geom 2 at -normal, one contact */
+/* mju_sign (engine_util_misc.c:1018-1026), mju_dist3 (engine_util_blas.c:157-160),
+   mju_mulMatTMat3 (:208-218) */
+static mjtNum mju_sign(mjtNum x) { return x < 0 ? -1 : (x > 0 ? 1 : 0); }
+
+static mjtNum mju_dist3(const mjtNum a[3], const mjtNum b[3]) {
+  mjtNum dif[3] = {a[0]-b[0], a[1]-b[1], a[2]-b[2]};
+  return sqrt(dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2]);
+}
+
+static void mju_mulMatTMat3(mjtNum r[9], const mjtNum a[9], const mjtNum b[9]) {
+  r[0] = a[0]*b[0] + a[3]*b[3] + a[6]*b[6];
+  r[1] = a[0]*b[1] + a[3]*b[4] + a[6]*b[7];
+  r[2] = a[0]*b[2] + a[3]*b[5] + a[6]*b[8];
+  r[3] = a[1]*b[0] + a[4]*b[3] + a[7]*b[6];
+  r[4] = a[1]*b[1] + a[4]*b[4] + a[7]*b[7];
+  r[5] = a[1]*b[2] + a[4]*b[5] + a[7]*b[8];
+  r[6] = a[2]*b[0] + a[5]*b[3] + a[8]*b[6];
+  r[7] = a[2]*b[1] + a[5]*b[4] + a[8]*b[7];
+  r[8] = a[2]*b[2] + a[5]*b[5] + a[8]*b[8];
+}
+
+/* mjccd_support (convex.c:501-704), the libccd-style support of a geom at unit direction dir
+   in its current frame (s->pos / s->mat): the mesh case hill-climbs from s->meshindex with the
+   start vertex's own value as the first bound and records the result in s->meshindex; the
+   result is inflated by half the object's margin */
+static void or_ccdSupportLib(mjtNum r[3], orShape* s, const mjtNum dir[3]) {
+  mjtNum ld[3], res[3];
+  mju_mulMatTVec3(ld, s->mat, dir);
+  const mjtNum* size = s->size;
+  switch (s->gtype) {
+  case mjhipGEOM_SPHERE:
+    mju_scl3(res, ld, size[0]);
+    break;
+  case mjhipGEOM_CAPSULE:
+    mju_scl3(res, ld, size[0]);
+    res[2] += mju_sign(ld[2]) * size[1];
+    break;
+  case mjhipGEOM_ELLIPSOID:
+    for (int i = 0; i < 3; i++) res[i] = ld[i] * size[i];
+    mju_normalize3(res);
+    for (int i = 0; i < 3; i++) res[i] *= size[i];
+    break;
+  case mjhipGEOM_CYLINDER: {
+    mjtNum tmp = sqrt(ld[0]*ld[0] + ld[1]*ld[1]);
+    if (tmp > mjMINVAL) {
+      res[0] = ld[0]/tmp*size[0];
+      res[1] = ld[1]/tmp*size[0];
+    } else {
+      res[0] = res[1] = 0;
+    }
+    res[2] = mju_sign(ld[2]) * size[1];
+    break;
+  }
+  case mjhipGEOM_BOX:
+    for (int i = 0; i < 3; i++) res[i] = mju_sign(ld[i]) * size[i];
+    break;
+  default: {                            /* mesh */
+    const float* V = s->vert;
+    mjtNum tmp = -1E+10;
+    int ibest = -1;
+    if (!s->graph) {
+      for (int i = 0; i < s->nvert; i++) {
+        mjtNum vdot = ld[0]*(mjtNum)V[3*i] + ld[1]*(mjtNum)V[3*i+1] + ld[2]*(mjtNum)V[3*i+2];
+        if (vdot > tmp) {
+          tmp = vdot;
+          ibest = i;
+        }
+      }
+      s->meshindex = ibest;
+    } else {
+      const int numvert = s->graph[0];
+      const int* edgeadr = s->graph + 2;
+      const int* globalid = s->graph + 2 + numvert;
+      const int* localid = s->graph + 2 + 2*numvert;
+      ibest = s->meshindex < 0 ? 0 : s->meshindex;
+      tmp = ld[0]*(mjtNum)V[3*globalid[ibest]] + ld[1]*(mjtNum)V[3*globalid[ibest]+1] +
+            ld[2]*(mjtNum)V[3*globalid[ibest]+2];
+      int change = 1, locid;
+      while (change) {
+        change = 0;
+        int i = edgeadr[ibest];
+        while ((locid = localid[i]) >= 0) {
+          mjtNum vdot = ld[0]*(mjtNum)V[3*globalid[locid]] + ld[1]*(mjtNum)V[3*globalid[locid]+1] +
+                        ld[2]*(mjtNum)V[3*globalid[locid]+2];
+          if (vdot > tmp) {
+            tmp = vdot;
+            ibest = locid;
+            change = 1;
+          }
+          i++;
+        }
+      }
+      s->meshindex = ibest;
+      ibest = globalid[ibest];
+    }
+    if (ibest < 0) {
+      mju_zero3(res);
+    } else {
+      for (int i = 0; i < 3; i++) res[i] = (mjtNum)V[3*ibest + i];
+    }
+    break;
+  }
+  }
+  for (int i = 0; i < 3; i++) res[i] += ld[i] * s->margin/2;
+  mju_mulMatVec3(res, s->mat, res);
+  mju_addTo3(res, s->pos);
+  mju_copy3(r, res);
+}
+
+/* addplanemesh (convex.c:1010-1040) */
+static int or_addPlaneMesh(orRaw* c, const float vertex[3], const mjtNum pos1[3],
+                           const mjtNum normal1[3], const mjtNum pos2[3], const mjtNum mat2[9],
+                           const mjtNum first[3], mjtNum rbound) {
+  mjtNum pnt[3], v[3] = {vertex[0], vertex[1], vertex[2]}, dif[3];
+  mju_mulMatVec3(pnt, mat2, v);
+  mju_addTo3(pnt, pos2);
+  if (mju_dist3(pnt, first) < 0.3*rbound) return 0;
+  mju_sub3(dif, pnt, pos1);
+  c->dist = mju_dot3(normal1, dif);
+  mju_copy3(c->pos, pnt);
+  mju_addToScl3(c->pos, normal1, -0.5*c->dist);
+  mju_copy3(c->frame, normal1);
+  mju_zero3(c->frame + 3);
+  return 1;
+}
+
+/* mjc_PlaneConvex (convex.c:1045-1141): the libccd support of geom 2 at -normal gives the first
+   contact; for a mesh, up to maxplanemesh = 3 in all with the vertices below the margin around
+   the support vertex (the hull graph's neighbours, else every vertex) */
 static int col_planeConvex(orRaw* c, const mjhipModel* m, const mjhipData* d, int g1, int g2,
                            mjtNum margin) {
   const mjtNum *pos1 = d->geom_xpos + 3*g1, *mat1 = d->geom_xmat + 9*g1;
   const mjtNum *pos2 = d->geom_xpos + 3*g2, *mat2 = d->geom_xmat + 9*g2;
-  const mjtNum* size = m->geom_size + 3*g2;
   mjtNum normal[3] = {mat1[2], mat1[5], mat1[8]}, dir[3] = {-mat1[2], -mat1[5], -mat1[8]};
-  mjtNum ld[3], v[3], dif[3];
-  mju_mulMatTVec3(ld, mat2, dir);
-  for (int i = 0; i < 3; i++) v[i] = ld[i]*size[i];      /* ellipsoid case (:570-580) */
-  mju_normalize3(v);
-  for (int i = 0; i < 3; i++) v[i] *= size[i];
-  for (int i = 0; i < 3; i++) v[i] += ld[i]*0.0/2;        /* the object's margin is 0 */
-  mju_mulMatVec3(v, mat2, v);
-  mju_addTo3(v, pos2);
+  mjtNum v[3], dif[3];
+  orShape obj;
+  or_shape(&obj, m, d, g2, 0);
+  or_ccdSupportLib(v, &obj, dir);
   mju_sub3(dif, v, pos1);
   mjtNum dist = mju_dot3(normal, dif);
   if (dist > margin) return 0;
@@ -3528,6 +3756,289 @@ static int col_planeConvex(orRaw* c, const mjhipModel* m, const mjhipData* d, in
   mju_addToScl3(c->pos, normal, -0.5*dist);
   mju_copy3(c->frame, normal);
   mju_zero3(c->frame + 3);
+  int count = 1;
+  const int id = m->geom_dataid[g2];
+  if (id == -1) return count;
+  const float* vertdata = m->mesh_vert + 3*m->mesh_vertadr[id];
+  mjtNum locdir[3];
+  mju_mulMatTVec3(locdir, mat2, dir);
+  mju_sub3(dif, pos2, pos1);
+  const mjtNum threshold = mju_dot3(normal, dif) - margin;
+  const mjtNum rbound = m->geom_rbound[g2];
+  if (m->mesh_graphadr[id] < 0) {
+    for (int i = 0; i < m->mesh_vertnum[id] && count < 3; i++) {
+      mjtNum vdot = locdir[0]*(mjtNum)vertdata[3*i] + locdir[1]*(mjtNum)vertdata[3*i+1] +
+                    locdir[2]*(mjtNum)vertdata[3*i+2];
+      if (vdot > threshold && i != obj.meshindex) {
+        count += or_addPlaneMesh(c + count, vertdata + 3*i, pos1, normal, pos2, mat2, c->pos,
+                                 rbound);
+      }
+    }
+  } else if (obj.meshindex >= 0) {
+    const int* graph = m->mesh_graph + m->mesh_graphadr[id];
+    const int numvert = graph[0];
+    const int* edgeadr = graph + 2;
+    const int* globalid = graph + 2 + numvert;
+    const int* localid = graph + 2 + 2*numvert;
+    int i = edgeadr[obj.meshindex], locid;
+    while ((locid = localid[i]) >= 0 && count < 3) {
+      const float* vx = vertdata + 3*globalid[locid];
+      mjtNum vdot = locdir[0]*(mjtNum)vx[0] + locdir[1]*(mjtNum)vx[1] + locdir[2]*(mjtNum)vx[2];
+      if (vdot > threshold) {
+        count += or_addPlaneMesh(c + count, vx, pos1, normal, pos2, mat2, c->pos, rbound);
+      }
+      i++;
+    }
+  }
+  return count;
+}
+
+/* mjc_ellipsoidInside (convex.c:1363-1414) and mjc_ellipsoidOutside (:1419-1464) */
+static int or_ellipsoidInside(mjtNum nrm[3], const mjtNum pos[3], const mjtNum size[3]) {
+  mjtNum S2inv[3] = {1/(size[0]*size[0]), 1/(size[1]*size[1]), 1/(size[2]*size[2])};
+  mjtNum C = pos[0]*pos[0]*S2inv[0] + pos[1]*pos[1]*S2inv[1] + pos[2]*pos[2]*S2inv[2] - 1;
+  if (C > 0) return 0;
+  mju_normalize3(nrm);
+  for (int iter = 0; iter < 30; iter++) {
+    mjtNum A = nrm[0]*nrm[0]*S2inv[0] + nrm[1]*nrm[1]*S2inv[1] + nrm[2]*nrm[2]*S2inv[2];
+    mjtNum B = pos[0]*nrm[0]*S2inv[0] + pos[1]*nrm[1]*S2inv[1] + pos[2]*nrm[2]*S2inv[2];
+    mjtNum det = B*B - A*C;
+    if (det < mjMINVAL || A < mjMINVAL) return iter > 0;
+    mjtNum x = (-B + sqrt(det))/A;
+    if (x < 0) return iter > 0;
+    mjtNum pnt[3];
+    mju_addScl3(pnt, pos, nrm, x);
+    mjtNum newnrm[3] = {pnt[0]*S2inv[0], pnt[1]*S2inv[1], pnt[2]*S2inv[2]};
+    mju_normalize3(newnrm);
+    mjtNum change = mju_dist3(nrm, newnrm);
+    mju_copy3(nrm, newnrm);
+    if (change < 1e-6) break;
+  }
+  return 1;
+}
+
+static int or_ellipsoidOutside(mjtNum nrm[3], const mjtNum pos[3], const mjtNum size[3]) {
+  mjtNum S2[3] = {size[0]*size[0], size[1]*size[1], size[2]*size[2]};
+  mjtNum PS2[3] = {pos[0]*pos[0]*S2[0], pos[1]*pos[1]*S2[1], pos[2]*pos[2]*S2[2]};
+  mjtNum la = 0;
+  for (int iter = 0; iter < 30; iter++) {
+    mjtNum R[3] = {1/(S2[0]+la), 1/(S2[1]+la), 1/(S2[2]+la)};
+    mjtNum val = PS2[0]*R[0]*R[0] + PS2[1]*R[1]*R[1] + PS2[2]*R[2]*R[2] - 1;
+    if (val < 1e-6) break;
+    mjtNum deriv = -2*(PS2[0]*R[0]*R[0]*R[0] + PS2[1]*R[1]*R[1]*R[1] + PS2[2]*R[2]*R[2]*R[2]);
+    if (deriv > -mjMINVAL) break;
+    mjtNum delta = -val/deriv;
+    if (delta < 1e-6) break;
+    la += delta;
+  }
+  nrm[0] = pos[0]/(S2[0]+la);
+  nrm[1] = pos[1]/(S2[1]+la);
+  nrm[2] = pos[2]/(S2[2]+la);
+  mju_normalize3(nrm);
+  return 1;
+}
+
+/* mjc_fixNormal (convex.c:1469-1614): the contact normal from the smooth geom's surface */
+static void or_fixNormal(const mjhipModel* m, const mjhipData* d, orRaw* con, int g1, int g2) {
+  int gid[2] = {g1, g2}, type[2];
+  for (int i = 0; i < 2; i++) {
+    type[i] = m->geom_type[gid[i]];
+    if (type[i] != mjhipGEOM_SPHERE && type[i] != mjhipGEOM_CAPSULE &&
+        type[i] != mjhipGEOM_ELLIPSOID && type[i] != mjhipGEOM_CYLINDER) {
+      type[i] = -1;
+    }
+  }
+  if (type[0] == -1 && type[1] == -1) return;
+  mjtNum normal[2][3] = {{con->frame[0], con->frame[1], con->frame[2]},
+                         {-con->frame[0], -con->frame[1], -con->frame[2]}};
+  int processed[2] = {0, 0};
+  for (int i = 0; i < 2; i++) {
+    if (type[i] == -1) continue;
+    const mjtNum* mat = d->geom_xmat + 9*gid[i];
+    const mjtNum* size = m->geom_size + 3*gid[i];
+    mjtNum dif[3], pos[3], nrm[3], dst1, dst2;
+    mju_sub3(dif, con->pos, d->geom_xpos + 3*gid[i]);
+    mju_mulMatTVec3(pos, mat, dif);
+    mju_mulMatTVec3(nrm, mat, normal[i]);
+    switch (type[i]) {
+    case mjhipGEOM_SPHERE:
+      mju_copy3(nrm, pos);
+      processed[i] = 1;
+      break;
+    case mjhipGEOM_CAPSULE:
+      if (pos[2] < -size[1]) {
+        nrm[2] = pos[2] + size[1];
+      } else if (pos[2] > size[1]) {
+        nrm[2] = pos[2] - size[1];
+      } else {
+        nrm[2] = 0;
+      }
+      nrm[0] = pos[0];
+      nrm[1] = pos[1];
+      processed[i] = 1;
+      break;
+    case mjhipGEOM_ELLIPSOID:
+      if (size[0] < mjMINVAL || size[1] < mjMINVAL || size[2] < mjMINVAL) break;
+      dst1 = pos[0]*pos[0]/(size[0]*size[0]) + pos[1]*pos[1]/(size[1]*size[1]) +
+             pos[2]*pos[2]/(size[2]*size[2]);
+      processed[i] = dst1 <= 1 ? or_ellipsoidInside(nrm, pos, size)
+                               : or_ellipsoidOutside(nrm, pos, size);
+      break;
+    default:                                /* cylinder */
+      if (fabs(pos[2]) > 0.95*size[1]) break;
+      dst1 = fabs(size[1] - fabs(pos[2]));
+      dst2 = fabs(size[0] - sqrt(pos[0]*pos[0] + pos[1]*pos[1]));
+      if (dst1 < 0.25*dst2) break;
+      nrm[0] = pos[0];
+      nrm[1] = pos[1];
+      nrm[2] = 0;
+      processed[i] = 1;
+      break;
+    }
+    if (processed[i]) {
+      mju_normalize3(nrm);
+      mju_mulMatVec3(normal[i], mat, nrm);
+    }
+  }
+  if (processed[0] && processed[1]) {
+    mju_sub3(con->frame, normal[0], normal[1]);
+    mju_normalize3(con->frame);
+  } else if (processed[0]) {
+    mju_copy3(con->frame, normal[0]);
+  } else if (processed[1]) {
+    mju_scl3(con->frame, normal[1], -1);
+  }
+  if (processed[0] || processed[1]) mju_zero3(con->frame + 3);
+}
+
+/* addVert (convex.c:1154-1168) */
+static void or_prismAddVert(int* nvert, orShape* s, mjtNum x, mjtNum y, mjtNum z) {
+  mju_copy3(s->prism[0], s->prism[1]);
+  mju_copy3(s->prism[1], s->prism[2]);
+  mju_copy3(s->prism[3], s->prism[4]);
+  mju_copy3(s->prism[4], s->prism[5]);
+  s->prism[2][0] = s->prism[5][0] = x;
+  s->prism[2][1] = s->prism[5][1] = y;
+  s->prism[5][2] = z;
+  (*nvert)++;
+}
+
+/* most contacts of mjc_ConvexHField for a height field: one per triangular prism of the grid,
+   at most mjMAXCONPAIR (50) */
+static int or_hfieldMaxContacts(const mjhipModel* m, int hid) {
+  int n = 2*(m->hfield_nrow[hid] - 1)*(m->hfield_ncol[hid] - 1);
+  return n < 50 ? n : 50;
+}
+
+/* mjc_ConvexHField (convex.c:1173-1356): geom 2 expressed in the height field's frame, its
+   support box against the field's box, then the native solver (mjc_penetration :34-68, one
+   contact) against every triangular prism of the covered sub-grid, each contact's normal fixed
+   by mjc_fixNormal. The solver's warm starts of geom 2 carry over from the support-box calls
+   through every prism, as in the reference's single mjCCDObj. */
+static int col_convexHField(orRaw* con, const mjhipModel* m, const mjhipData* d, int g1, int g2,
+                            mjtNum margin) {
+  const mjtNum *pos1 = d->geom_xpos + 3*g1, *mat1 = d->geom_xmat + 9*g1;
+  const mjtNum *pos2 = d->geom_xpos + 3*g2, *mat2 = d->geom_xmat + 9*g2;
+  const int hid = m->geom_dataid[g1];
+  const int nrow = m->hfield_nrow[hid], ncol = m->hfield_ncol[hid];
+  const float* data = m->hfield_data + m->hfield_adr[hid];
+  const mjtNum* size1 = m->hfield_size + 4*hid;
+  mjtNum vec[3], pos[3], mat[9];
+  mju_sub3(vec, pos2, pos1);
+  mju_mulMatTVec(pos, mat1, vec, 3, 3);
+  const mjtNum r2 = m->geom_rbound[g2];
+  for (int i = 0; i < 2; i++) {
+    if ((size1[i] < pos[i] - r2 - margin) || (-size1[i] > pos[i] + r2 + margin)) return 0;
+  }
+  if (size1[2] < pos[2] - r2 - margin) return 0;
+  if (-size1[3] > pos[2] + r2 + margin) return 0;
+  mju_mulMatTMat3(mat, mat1, mat2);
+  /* geom 2 in the field's frame (the reference overwrites its geom_xmat/xpos meanwhile) */
+  orShape B;
+  or_shape(&B, m, d, g2, 0);
+  B.pos = pos;
+  B.mat = mat;
+  mjtNum sv[3], xmin, xmax, ymin, ymax, zmin, zmax;
+  const mjtNum ax[6][3] = {{1, 0, 0}, {-1, 0, 0}, {0, 1, 0}, {0, -1, 0}, {0, 0, 1}, {0, 0, -1}};
+  or_ccdSupportLib(sv, &B, ax[0]); xmax = sv[0];
+  or_ccdSupportLib(sv, &B, ax[1]); xmin = sv[0];
+  or_ccdSupportLib(sv, &B, ax[2]); ymax = sv[1];
+  or_ccdSupportLib(sv, &B, ax[3]); ymin = sv[1];
+  or_ccdSupportLib(sv, &B, ax[4]); zmax = sv[2];
+  or_ccdSupportLib(sv, &B, ax[5]); zmin = sv[2];
+  if ((xmin - margin > size1[0]) || (xmax + margin < -size1[0]) ||
+      (ymin - margin > size1[1]) || (ymax + margin < -size1[1]) ||
+      (zmin - margin > size1[2]) || (zmax + margin < -size1[3])) {
+    return 0;
+  }
+  int cmin = (int)floor((xmin + size1[0]) / (2*size1[0]) * (ncol - 1));
+  int cmax = (int)ceil((xmax + size1[0]) / (2*size1[0]) * (ncol - 1));
+  int rmin = (int)floor((ymin + size1[1]) / (2*size1[1]) * (nrow - 1));
+  int rmax = (int)ceil((ymax + size1[1]) / (2*size1[1]) * (nrow - 1));
+  cmin = mjMAX(0, cmin);
+  cmax = mjMIN(ncol - 1, cmax);
+  rmin = mjMAX(0, rmin);
+  rmax = mjMIN(nrow - 1, rmax);
+  B.margin = margin;
+  orShape A;
+  memset(&A, 0, sizeof(A));
+  A.kind = A.gtype = mjhipGEOM_HFIELD;
+  A.vertindex = A.meshindex = -1;
+  const mjtNum dx = (2.0*size1[0]) / (ncol - 1), dy = (2.0*size1[1]) / (nrow - 1);
+  const int dr[2] = {1, 0};
+  A.prism[0][2] = A.prism[1][2] = A.prism[2][2] = -size1[3];
+  int cnt = 0;
+  for (int r = rmin; r < rmax; r++) {
+    int nvert = 0;
+    for (int c = cmin; c <= cmax; c++) {
+      for (int i = 0; i < 2; i++) {
+        or_prismAddVert(&nvert, &A, dx*c - size1[0], dy*(r + dr[i]) - size1[1],
+                        data[(r + dr[i])*ncol + c]*size1[2] + margin);
+        if (nvert <= 2) continue;
+        if (A.prism[3][2] < zmin && A.prism[4][2] < zmin && A.prism[5][2] < zmin) continue;
+        orCCD st;
+        const mjtNum dist = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, 0);
+        if (!(dist < 0)) continue;              /* mjc_penetration: no penetration */
+        mjtNum dir[3], vp[3];
+        mju_sub3(dir, st.x1, st.x2);
+        mju_normalize3(dir);
+        vp[0] = 0.5*(st.x1[0] + st.x2[0]);
+        vp[1] = 0.5*(st.x1[1] + st.x2[1]);
+        vp[2] = 0.5*(st.x1[2] + st.x2[2]);
+        if (dir[0] == 0 && dir[1] == 0 && dir[2] == 0) continue;   /* ccdVec3Eq(dir, origin) */
+        con[cnt].dist = dist;                    /* -depth */
+        mju_mulMatVec3(con[cnt].frame, mat1, dir);
+        mju_mulMatVec3(con[cnt].pos, mat1, vp);
+        mju_addTo3(con[cnt].pos, pos1);
+        mju_zero3(con[cnt].frame + 3);
+        if (++cnt >= 50) {
+          r = rmax + 1;
+          c = cmax + 1;
+          break;
+        }
+      }
+    }
+  }
+  for (int i = 0; i < cnt; i++) or_fixNormal(m, d, con + i, g1, g2);
+  return cnt;
+}
+
+/* Test hook restating the reference's Penetration helper (test/engine/
+   engine_collision_gjk_test.cc:86-150): mjc_ccd on geoms g1, g2 with the given margin,
+   tolerance and iterations, one contact, no distance cutoff. Returns the number of contacts
+   (0 or 1); out = {dist, dir[3], pos[3]}. */
+int or_ccdPenetration(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum margin,
+                      mjtNum tol, int kmax, mjtNum* out) {
+  orShape A, B;
+  or_shape(&A, m, d, g1, margin);
+  or_shape(&B, m, d, g2, margin);
+  orCCD st;
+  mjtNum dist = or_ccd(&st, &A, &B, kmax, tol, 0);
+  if (!(dist < 0) || st.nx < 1) return 0;
+  out[0] = dist;
+  mju_sub3(out + 1, st.x1, st.x2);
+  mju_normalize3(out + 1);
+  for (int k = 0; k < 3; k++) out[4 + k] = 0.5*(st.x1[k] + st.x2[k]);
   return 1;
 }
 
@@ -3535,7 +4046,7 @@ static int col_planeConvex(orRaw* c, const mjhipModel* m, const mjhipData* d, in
  * ellipsoid and cylinder pairs among themselves and with boxes) */
 static int or_isConvexPair(int t1, int t2) {
   if (t1 == mjhipGEOM_PLANE || t1 == mjhipGEOM_HFIELD) return 0;
-  if (t2 == mjhipGEOM_ELLIPSOID) return 1;
+  if (t2 == mjhipGEOM_ELLIPSOID || t2 == mjhipGEOM_MESH) return 1;
   if (t2 == mjhipGEOM_CYLINDER) return t1 == mjhipGEOM_CAPSULE || t1 == mjhipGEOM_CYLINDER ||
                                         t1 == mjhipGEOM_ELLIPSOID;
   if (t2 == mjhipGEOM_BOX) return t1 == mjhipGEOM_ELLIPSOID || t1 == mjhipGEOM_CYLINDER;
@@ -3543,22 +4054,27 @@ static int or_isConvexPair(int t1, int t2) {
 }
 
 /* mjCOLLISIONFUNC (:41-52) for type-ordered t1 <= t2: 0 = no function, otherwise the most
- * contacts the function returns when it is one of the primitives restated here, or -1 for a
- * function outside the subset (mjc_Convex, height fields, SDFs) */
+ * contacts the function returns when it is one of the primitives restated here (a height
+ * field's, 50, is bounded per field by or_pairMaxContacts), or -1 for a function outside the
+ * subset (SDFs, libccd's MPR) */
 static int or_collisionFunc(const mjhipModel* m, int t1, int t2) {
   static const int table[9][9] = {
     /*           PLANE HFIELD SPHERE CAPSULE ELLIPS CYL BOX MESH SDF */
-    /*PLANE  */ {0,    0,     1,     2,      1,     4,  4,  -1,  -1},
-    /*HFIELD */ {0,    0,     -1,    -1,     -1,    -1, -1, -1,  -1},
-    /*SPHERE */ {0,    0,     1,     1,      1,     1,  1,  -1,  -1},
-    /*CAPSULE*/ {0,    0,     0,     2,      1,     1,  2,  -1,  -1},
-    /*ELLIPS */ {0,    0,     0,     0,      1,     1,  1,  -1,  -1},
-    /*CYL    */ {0,    0,     0,     0,      0,     1,  1,  -1,  -1},
-    /*BOX    */ {0,    0,     0,     0,      0,     0,  24, -1,  -1},
-    /*MESH   */ {0,    0,     0,     0,      0,     0,  0,  -1,  -1},
+    /*PLANE  */ {0,    0,     1,     2,      1,     4,  4,  3,   -1},
+    /*HFIELD */ {0,    0,     50,    50,     50,    50, 50, 50,  -1},
+    /*SPHERE */ {0,    0,     1,     1,      1,     1,  1,  1,   -1},
+    /*CAPSULE*/ {0,    0,     0,     2,      1,     1,  2,  1,   -1},
+    /*ELLIPS */ {0,    0,     0,     0,      1,     1,  1,  1,   -1},
+    /*CYL    */ {0,    0,     0,     0,      0,     1,  1,  1,   -1},
+    /*BOX    */ {0,    0,     0,     0,      0,     0,  24, 1,   -1},
+    /*MESH   */ {0,    0,     0,     0,      0,     0,  0,  1,   -1},
     /*SDF    */ {0,    0,     0,     0,      0,     0,  0,  0,   -1}};
   if (t1 < 0 || t2 < 0 || t1 > 8 || t2 > 8) return -1;
   const int k = table[t1][t2];
+  if (k > 0 && (t1 == mjhipGEOM_HFIELD || (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_MESH))) {
+    /* mjc_ConvexHField / the plane-mesh path through mjc_penetration / the native solver */
+    if (mjDISABLED(mjhipDSBL_NATIVECCD) && t1 == mjhipGEOM_HFIELD) return -1;
+  }
   if (k > 0 && or_isConvexPair(t1, t2)) {
     /* mjc_Convex with the libccd MPR fallback, or MULTICCD's perturbed extra contacts (pairs
        without a sphere or ellipsoid, convex.c:936-999): not restated */
@@ -3567,6 +4083,15 @@ static int or_collisionFunc(const mjhipModel* m, int t1, int t2) {
         t2 != mjhipGEOM_ELLIPSOID) {
       return -1;
     }
+  }
+  return k;
+}
+
+/* the most contacts of type-ordered geoms g1, g2 (0: no function, -1: outside the subset) */
+static int or_pairMaxContacts(const mjhipModel* m, int g1, int g2) {
+  const int k = or_collisionFunc(m, m->geom_type[g1], m->geom_type[g2]);
+  if (k > 0 && m->geom_type[g1] == mjhipGEOM_HFIELD) {
+    return or_hfieldMaxContacts(m, m->geom_dataid[g1]);
   }
   return k;
 }
@@ -3823,9 +4348,8 @@ static void or_contactBounds(const mjhipModel* m, int* ncon, int* nrow) {
       if (excluded) continue;
       for (int g1 = m->body_geomadr[b1]; g1 < m->body_geomadr[b1] + m->body_geomnum[b1]; g1++) {
         for (int g2 = m->body_geomadr[b2]; g2 < m->body_geomadr[b2] + m->body_geomnum[b2]; g2++) {
-          int t1 = mjMIN(m->geom_type[g1], m->geom_type[g2]);
-          int t2 = mjMAX(m->geom_type[g1], m->geom_type[g2]);
-          int k = or_collisionFunc(m, t1, t2);
+          const int flip = m->geom_type[g1] > m->geom_type[g2];
+          int k = or_pairMaxContacts(m, flip ? g2 : g1, flip ? g1 : g2);
           if (k > 0 && !or_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
                                          m->geom_contype[g2], m->geom_conaffinity[g2])) {
             int condim = or_pairCondim(m, g1, g2);
@@ -3868,7 +4392,7 @@ int or_efcCapacity(const mjhipModel* m) {
 }
 
 /* the narrowphase of type-ordered geoms g1, g2 (mjCOLLISIONFUNC's primitive and convex
- * functions): raw contacts closer than margin into raw[] (<= 24), their count */
+ * functions): raw contacts closer than margin into raw[] (<= 50), their count */
 static int or_narrow(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum margin,
                      orRaw* raw) {
   const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
@@ -3899,8 +4423,10 @@ static int or_narrow(const mjhipModel* m, const mjhipData* d, int g1, int g2, mj
   } else if (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX) {
     num = col_boxBox(raw, margin, pos1, mat1, size1, pos2, mat2, size2);
     if (num) num = or_boxBoxFilter(raw, num, margin, pos1, mat1, size1, pos2, mat2, size2);
-  } else if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_ELLIPSOID) {
+  } else if (t1 == mjhipGEOM_PLANE && (t2 == mjhipGEOM_ELLIPSOID || t2 == mjhipGEOM_MESH)) {
     num = col_planeConvex(raw, m, d, g1, g2, margin);
+  } else if (t1 == mjhipGEOM_HFIELD) {
+    num = col_convexHField(raw, m, d, g1, g2, margin);
   } else if (or_isConvexPair(t1, t2)) {
     num = col_convex(raw, m, d, g1, g2, margin);
   }
@@ -3924,7 +4450,7 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
     ((mjhipData*)d)->status |= MJHIP_INST_UNSUPPORTED;
     return;
   }
-  orRaw raw[24];
+  orRaw raw[50];
   const int num = or_narrow(m, d, g1, g2, margin, raw);
   if (!num) return;
   int condim;
@@ -3987,7 +4513,7 @@ static mjtNum or_geomDistance(const mjhipModel* m, mjhipData* d, int geom1, int 
     }
     return r;
   }
-  orRaw raw[24];
+  orRaw raw[50];
   const int num = or_narrow(m, d, g1, g2, distmax, raw);
   int best = -1;
   for (int i = 0; i < num; i++) {
@@ -4954,15 +5480,316 @@ static void or_rne_vel(const mjhipModel* m, const mjhipData* d, mjtNum* qDeriv) 
   free(Dcdofdot); free(Dcvel); free(Dcacc); free(Dcfrc); free(tmp6);
 }
 
-/* mjd_smooth_vel (engine_derivative.c:1522-1536) on the D sparsity, for the tests: uses the
- * position/velocity quantities already in d */
+/*---------------- fluid force derivatives (mjd_passive_vel's fluid part) ---------------------*/
+
+static mjtNum or_maxMoment(const mjtNum s[3], int k);
+static void or_semiAxes(const mjhipModel* m, int g, mjtNum ax[3]);
+static void or_objectVelocity(const mjhipModel* m, const mjhipData* d, int type, int id,
+                              mjtNum res[6], int flg_local);
+static void mju_transformSpatial(mjtNum res[6], const mjtNum vec[6], int flg_force,
+                                 const mjtNum newpos[3], const mjtNum oldpos[3],
+                                 const mjtNum* rotnew2old);
+
+/* addJTBJ :693-724: qDeriv (D sparsity) += J' B J for the n x n matrix B and the n rows of J */
+static void or_addJTBJ(const mjhipModel* m, mjtNum* qDeriv, const mjtNum* J, const mjtNum* B,
+                       int n) {
+  const int nv = m->nv;
+  for (int i = 0; i < n; i++) {
+    for (int j = 0; j < n; j++) {
+      if (!B[i*n+j]) continue;
+      for (int k = 0; k < nv; k++) {
+        if (!J[i*nv+k]) continue;
+        const mjtNum s = J[i*nv+k] * B[i*n+j];
+        for (int a = m->D_rowadr[k]; a < m->D_rowadr[k] + m->D_rownnz[k]; a++) {
+          qDeriv[a] += J[j*nv + m->D_colind[a]] * s;
+        }
+      }
+    }
+  }
+}
+
+/* :898-909 addToQuadrant (B is indexed column-major in 3x3 blocks) */
+static void or_addToQuadrant(mjtNum* B, const mjtNum D[9], int col_quad, int row_quad) {
+  const int r = 3*row_quad, c = 3*col_quad;
+  for (int k = 0; k < 3; k++) {
+    for (int l = 0; l < 3; l++) B[6*(c+k) + r+l] += D[3*k+l];
+  }
+}
+
+/* :38-61 mjd_cross */
+static void or_dcross(const mjtNum a[3], const mjtNum b[3], mjtNum* Da, mjtNum* Db) {
+  mju_zero(Da, 9);
+  Da[1] =  b[2]; Da[2] = -b[1]; Da[3] = -b[2]; Da[5] =  b[0]; Da[6] =  b[1]; Da[7] = -b[0];
+  mju_zero(Db, 9);
+  Db[1] = -a[2]; Db[2] =  a[1]; Db[3] =  a[2]; Db[5] = -a[0]; Db[6] = -a[1]; Db[7] =  a[0];
+}
+
+static void or_addToScl3(mjtNum* r, const mjtNum* a, mjtNum s) {
+  r[0] += a[0]*s; r[1] += a[1]*s; r[2] += a[2]*s;
+}
+
+/* :916-957 mjd_addedMassForces */
+static void or_dAddedMass(mjtNum* B, const mjtNum lv[6], mjtNum rho, const mjtNum vm[3],
+                          const mjtNum vi[3]) {
+  const mjtNum lin[3] = {lv[3], lv[4], lv[5]}, ang[3] = {lv[0], lv[1], lv[2]};
+  const mjtNum plin[3] = {rho*vm[0]*lin[0], rho*vm[1]*lin[1], rho*vm[2]*lin[2]};
+  const mjtNum pang[3] = {rho*vi[0]*ang[0], rho*vi[1]*ang[1], rho*vi[2]*ang[2]};
+  mjtNum Da[9], Db[9];
+  or_dcross(pang, ang, Da, Db);
+  or_addToQuadrant(B, Db, 0, 0);
+  for (int i = 0; i < 9; i++) Da[i] *= rho * vi[i % 3];
+  or_addToQuadrant(B, Da, 0, 0);
+  or_dcross(plin, lin, Da, Db);
+  or_addToQuadrant(B, Db, 0, 1);
+  for (int i = 0; i < 9; i++) Da[i] *= rho * vm[i % 3];
+  or_addToQuadrant(B, Da, 0, 1);
+  or_dcross(plin, ang, Da, Db);
+  or_addToQuadrant(B, Db, 1, 0);
+  for (int i = 0; i < 9; i++) Da[i] *= rho * vm[i % 3];
+  or_addToQuadrant(B, Da, 1, 1);
+}
+
+/* :962-1011 mjd_viscous_torque */
+static void or_dViscousTorque(mjtNum* D, const mjtNum lv[6], mjtNum rho, mjtNum mu,
+                              const mjtNum s[3], mjtNum slender, mjtNum angdrag) {
+  const mjtNum dmax = mjMAX(mjMAX(s[0], s[1]), s[2]);
+  const mjtNum dmin = mjMIN(mjMIN(s[0], s[1]), s[2]);
+  const mjtNum dmid = s[0] + s[1] + s[2] - dmax - dmin;
+  const mjtNum eqD = 2.0/3.0 * (s[0] + s[1] + s[2]);
+  const mjtNum lin_visc = mjhipPI * eqD*eqD*eqD;
+  const mjtNum Imax = 8.0/15.0 * mjhipPI * dmid * (dmax*dmax)*(dmax*dmax);
+  const mjtNum II[3] = {or_maxMoment(s, 0), or_maxMoment(s, 1), or_maxMoment(s, 2)};
+  const mjtNum x = lv[0], y = lv[1], z = lv[2];
+  const mjtNum mc[3] = {angdrag*II[0] + slender*(Imax - II[0]),
+                        angdrag*II[1] + slender*(Imax - II[1]),
+                        angdrag*II[2] + slender*(Imax - II[2])};
+  const mjtNum mv[3] = {x * mc[0], y * mc[1], z * mc[2]};
+  const mjtNum density = rho / mjMAX(mjMINVAL, mju_norm3(mv));
+  const mjtNum msq[3] = {-density * x * mc[0] * mc[0], -density * y * mc[1] * mc[1],
+                         -density * z * mc[2] * mc[2]};
+  const mjtNum lin_coef = mu * lin_visc;
+  mju_zero(D, 9);
+  D[0] = D[4] = D[8] = x*msq[0] + y*msq[1] + z*msq[2] - lin_coef;
+  or_addToScl3(D, msq, x);
+  or_addToScl3(D+3, msq, y);
+  or_addToScl3(D+6, msq, z);
+}
+
+/* :1016-1079 mjd_viscous_drag */
+static void or_dViscousDrag(mjtNum* D, const mjtNum lv[6], mjtNum rho, mjtNum mu,
+                            const mjtNum s[3], mjtNum blunt, mjtNum slender) {
+  const mjtNum dmax = mjMAX(mjMAX(s[0], s[1]), s[2]);
+  const mjtNum dmin = mjMIN(mjMIN(s[0], s[1]), s[2]);
+  const mjtNum dmid = s[0] + s[1] + s[2] - dmax - dmin;
+  const mjtNum eqD = 2.0/3.0 * (s[0] + s[1] + s[2]);
+  const mjtNum Amax = mjhipPI * dmax * dmid;
+  const mjtNum a = (s[1]*s[2])*(s[1]*s[2]), b = (s[2]*s[0])*(s[2]*s[0]);
+  const mjtNum c = (s[0]*s[1])*(s[0]*s[1]);
+  const mjtNum aa = a*a, bb = b*b, cc = c*c;
+  const mjtNum x = lv[3], y = lv[4], z = lv[5];
+  const mjtNum xx = x*x, yy = y*y, zz = z*z, xy = x*y, yz = y*z, xz = x*z;
+  const mjtNum pden = aa*xx + bb*yy + cc*zz;
+  const mjtNum pnum = a*xx + b*yy + c*zz;
+  const mjtNum dA = mjhipPI / mjMAX(mjMINVAL, sqrt(pnum*pnum*pnum * pden));
+  const mjtNum Aproj = mjhipPI * sqrt(pden/mjMAX(mjMINVAL, pnum));
+  const mjtNum norm = sqrt(xx + yy + zz);
+  const mjtNum inv_norm = 1.0 / mjMAX(mjMINVAL, norm);
+  const mjtNum lin_coef = mu * 3.0 * mjhipPI * eqD;
+  const mjtNum quad_coef = rho * (Aproj*blunt + slender*(Amax - Aproj));
+  const mjtNum Ac = rho * norm * (blunt - slender);
+  const mjtNum dAv[3] = {Ac * dA * a * x * (b * yy * (a - b) + c * zz * (a - c)),
+                         Ac * dA * b * y * (a * xx * (b - a) + c * zz * (b - c)),
+                         Ac * dA * c * z * (a * xx * (c - a) + b * yy * (c - b))};
+  D[0] = xx; D[1] = xy; D[2] = xz;
+  D[3] = xy; D[4] = yy; D[5] = yz;
+  D[6] = xz; D[7] = yz; D[8] = zz;
+  const mjtNum inner = xx + yy + zz;
+  D[0] += inner; D[4] += inner; D[8] += inner;
+  mju_scl(D, D, -quad_coef*inv_norm, 9);
+  or_addToScl3(D+0, dAv, -x);
+  or_addToScl3(D+3, dAv, -y);
+  or_addToScl3(D+6, dAv, -z);
+  D[0] -= lin_coef; D[4] -= lin_coef; D[8] -= lin_coef;
+}
+
+/* :1084-1133 mjd_kutta_lift */
+static void or_dKuttaLift(mjtNum* D, const mjtNum lv[6], mjtNum rho, const mjtNum s[3],
+                          mjtNum kutta) {
+  const mjtNum a = (s[1]*s[2])*(s[1]*s[2]), b = (s[2]*s[0])*(s[2]*s[0]);
+  const mjtNum c = (s[0]*s[1])*(s[0]*s[1]);
+  const mjtNum aa = a*a, bb = b*b, cc = c*c;
+  const mjtNum x = lv[3], y = lv[4], z = lv[5];
+  const mjtNum xx = x*x, yy = y*y, zz = z*z, xy = x*y, yz = y*z, xz = x*z;
+  const mjtNum pden = aa*xx + bb*yy + cc*zz;
+  const mjtNum pnum = a*xx + b*yy + c*zz;
+  const mjtNum norm2 = xx + yy + zz;
+  const mjtNum df_denom = mjhipPI * kutta * rho / mjMAX(mjMINVAL, sqrt(pden * pnum * norm2));
+  const mjtNum dfx = yy * (a - b) + zz * (a - c);
+  const mjtNum dfy = xx * (b - a) + zz * (b - c);
+  const mjtNum dfz = xx * (c - a) + yy * (c - b);
+  const mjtNum proj_term = pnum / mjMAX(mjMINVAL, pden);
+  const mjtNum cos_term = pnum / mjMAX(mjMINVAL, norm2);
+  D[0] = a-a; D[1] = b-a; D[2] = c-a;
+  D[3] = a-b; D[4] = b-b; D[5] = c-b;
+  D[6] = a-c; D[7] = b-c; D[8] = c-c;
+  mju_scl(D, D, 2 * pnum, 9);
+  const mjtNum inner[3] = {aa * proj_term - a + cos_term, bb * proj_term - b + cos_term,
+                           cc * proj_term - c + cos_term};
+  or_addToScl3(D + 0, inner, dfx);
+  or_addToScl3(D + 3, inner, dfy);
+  or_addToScl3(D + 6, inner, dfz);
+  D[0] *= xx; D[1] *= xy; D[2] *= xz;
+  D[3] *= xy; D[4] *= yy; D[5] *= yz;
+  D[6] *= xz; D[7] *= yz; D[8] *= zz;
+  D[0] -= dfx * pnum;
+  D[4] -= dfy * pnum;
+  D[8] -= dfz * pnum;
+  mju_scl(D, D, df_denom, 9);
+}
+
+/* :1138-1161 mjd_magnus_force */
+static void or_dMagnus(mjtNum* B, const mjtNum lv[6], mjtNum rho, const mjtNum s[3],
+                       mjtNum magnus) {
+  const mjtNum volume = 4.0/3.0 * mjhipPI * s[0] * s[1] * s[2];
+  const mjtNum coef = magnus * rho * volume;
+  mjtNum Dlin[9], Dang[9];
+  const mjtNum lin[3] = {coef * lv[3], coef * lv[4], coef * lv[5]};
+  const mjtNum ang[3] = {coef * lv[0], coef * lv[1], coef * lv[2]};
+  or_dcross(ang, lin, Dang, Dlin);
+  or_addToQuadrant(B, Dang, 1, 0);
+  or_addToQuadrant(B, Dlin, 1, 1);
+}
+
+/* the local 6 x nv Jacobian of a frame (rotation rows, then translation): mj_jac at `point`,
+ * each half rotated by mju_mulMatTMat(xmat, ., 3, 3, nv) (engine_util_blas.c:884-897) */
+static void or_localJac(const mjhipModel* m, const mjhipData* d, mjtNum* J, mjtNum* tmp,
+                        const mjtNum* point, const mjtNum* xmat, int body) {
+  const int nv = m->nv;
+  mj_jac(m, d, J + 3*nv, J, point, body);
+  for (int h = 0; h < 2; h++) {
+    mju_zero(tmp, 3*nv);
+    for (int i = 0; i < 3; i++) {
+      for (int j = 0; j < 3; j++) {
+        if (xmat[3*i+j]) mju_addToScl(tmp + j*nv, J + 3*h*nv + i*nv, xmat[3*i+j], nv);
+      }
+    }
+    mju_copy(J + 3*h*nv, tmp, 3*nv);
+  }
+}
+
+/* :1168-1270 mjd_ellipsoidFluid (dense) */
+static void or_dEllipsoidFluid(const mjhipModel* m, const mjhipData* d, mjtNum* qDeriv,
+                               int b, mjtNum* J, mjtNum* tmp) {
+  for (int j = 0; j < m->body_geomnum[b]; j++) {
+    const int g = m->body_geomadr[b] + j;
+    const mjtNum* c = m->geom_fluid + 12*g;
+    mjtNum ax[3], lvel[6], wind[6], lwind[6], B[36], D[9];
+    or_semiAxes(m, g, ax);
+    if (c[0] == 0.0) continue;
+    or_objectVelocity(m, d, OBJ_GEOM, g, lvel, 1);
+    mju_zero(wind, 6);
+    mju_copy3(wind+3, m->opt.wind);
+    mju_transformSpatial(lwind, wind, 0, d->geom_xpos + 3*g,
+                         d->subtree_com + 3*m->body_rootid[b], d->geom_xmat + 9*g);
+    lvel[3] -= lwind[3]; lvel[4] -= lwind[4]; lvel[5] -= lwind[5];
+    or_localJac(m, d, J, tmp, d->geom_xpos + 3*g, d->geom_xmat + 9*g, m->geom_bodyid[g]);
+    mju_zero(B, 36);
+    or_dMagnus(B, lvel, m->opt.density, ax, c[5]);
+    or_dKuttaLift(D, lvel, m->opt.density, ax, c[4]);
+    or_addToQuadrant(B, D, 1, 1);
+    or_dViscousDrag(D, lvel, m->opt.density, m->opt.viscosity, ax, c[1], c[2]);
+    or_addToQuadrant(B, D, 1, 1);
+    or_dViscousTorque(D, lvel, m->opt.density, m->opt.viscosity, ax, c[2], c[3]);
+    or_addToQuadrant(B, D, 0, 0);
+    or_dAddedMass(B, lvel, m->opt.density, c + 6, c + 9);
+    if (m->opt.integrator == mjhipINT_IMPLICITFAST) {     /* mju_symmetrize (blas.c:794-801) */
+      for (int r = 0; r < 6; r++) {
+        for (int k = 0; k < r; k++) B[r*6+k] = B[k*6+r] = 0.5 * (B[r*6+k] + B[k*6+r]);
+      }
+    }
+    or_addJTBJ(m, qDeriv, J, B, 6);
+  }
+}
+
+/* :1275-1425 mjd_inertiaBoxFluid (dense) */
+static void or_dInertiaBoxFluid(const mjhipModel* m, const mjhipData* d, mjtNum* qDeriv,
+                                int i, mjtNum* J, mjtNum* tmp) {
+  const int nv = m->nv;
+  const mjtNum* inertia = m->body_inertia + 3*i;
+  const mjtNum rho = m->opt.density, mu = m->opt.viscosity;
+  mjtNum lvel[6], wind[6], lwind[6], box[3], B;
+  box[0] = sqrt(mjMAX(mjMINVAL, (inertia[1] + inertia[2] - inertia[0])) / m->body_mass[i] * 6.0);
+  box[1] = sqrt(mjMAX(mjMINVAL, (inertia[0] + inertia[2] - inertia[1])) / m->body_mass[i] * 6.0);
+  box[2] = sqrt(mjMAX(mjMINVAL, (inertia[0] + inertia[1] - inertia[2])) / m->body_mass[i] * 6.0);
+  or_objectVelocity(m, d, OBJ_BODY, i, lvel, 1);
+  mju_zero(wind, 6);
+  mju_copy3(wind+3, m->opt.wind);
+  mju_transformSpatial(lwind, wind, 0, d->xipos+3*i, d->subtree_com+3*m->body_rootid[i],
+                       d->ximat+9*i);
+  lvel[3] -= lwind[3]; lvel[4] -= lwind[4]; lvel[5] -= lwind[5];
+  or_localJac(m, d, J, tmp, d->xipos + 3*i, d->ximat + 9*i, i);
+  if (mu > 0) {
+    const mjtNum diam = (box[0] + box[1] + box[2])/3.0;
+    B = -mjhipPI*diam*diam*diam*mu;
+    for (int j = 0; j < 3; j++) or_addJTBJ(m, qDeriv, J + j*nv, &B, 1);
+    B = -3.0*mjhipPI*diam*mu;
+    for (int j = 0; j < 3; j++) or_addJTBJ(m, qDeriv, J + 3*nv + j*nv, &B, 1);
+  }
+  if (rho > 0) {
+    B = -rho*box[0]*(box[1]*box[1]*box[1]*box[1]+box[2]*box[2]*box[2]*box[2])*
+        2*fabs(lvel[0])/64.0;
+    or_addJTBJ(m, qDeriv, J, &B, 1);
+    B = -rho*box[1]*(box[0]*box[0]*box[0]*box[0]+box[2]*box[2]*box[2]*box[2])*
+        2*fabs(lvel[1])/64.0;
+    or_addJTBJ(m, qDeriv, J + nv, &B, 1);
+    B = -rho*box[2]*(box[0]*box[0]*box[0]*box[0]+box[1]*box[1]*box[1]*box[1])*
+        2*fabs(lvel[2])/64.0;
+    or_addJTBJ(m, qDeriv, J + 2*nv, &B, 1);
+    B = -0.5*rho*box[1]*box[2]*2*fabs(lvel[3]);
+    or_addJTBJ(m, qDeriv, J + 3*nv, &B, 1);
+    B = -0.5*rho*box[0]*box[2]*2*fabs(lvel[4]);
+    or_addJTBJ(m, qDeriv, J + 4*nv, &B, 1);
+    B = -0.5*rho*box[0]*box[1]*2*fabs(lvel[5]);
+    or_addJTBJ(m, qDeriv, J + 5*nv, &B, 1);
+  }
+}
+
+/* mjd_passive_vel :1494-1513: the fluid models' derivatives, per body as mj_fluid chooses */
+static void or_dFluid(const mjhipModel* m, const mjhipData* d, mjtNum* qDeriv) {
+  if (mjDISABLED(mjhipDSBL_PASSIVE) || !(m->opt.viscosity > 0 || m->opt.density > 0)) return;
+  mjtNum* J = (mjtNum*)malloc((6*(size_t)m->nv + 1)*sizeof(mjtNum));
+  mjtNum* tmp = (mjtNum*)malloc((3*(size_t)m->nv + 1)*sizeof(mjtNum));
+  for (int i = 1; i < m->nbody; i++) {
+    if (m->body_mass[i] < mjMINVAL) continue;
+    int ell = 0;
+    for (int j = 0; j < m->body_geomnum[i] && ell == 0; j++) {
+      ell += m->geom_fluid[12*(m->body_geomadr[i] + j)] > 0;
+    }
+    if (ell) or_dEllipsoidFluid(m, d, qDeriv, i, J, tmp);
+    else or_dInertiaBoxFluid(m, d, qDeriv, i, J, tmp);
+  }
+  free(J);
+  free(tmp);
+}
+
+/* mjd_smooth_vel (engine_derivative.c:1522-1536) on the D sparsity: uses the position/velocity
+ * quantities already in d */
 void or_smoothVel(const mjhipModel* m, const mjhipData* d, mjtNum* qDeriv, int flg_bias) {
   for (int r = 0; r < m->nv; r++) {
     for (int k = 0; k < m->D_rownnz[r]; k++) {
       qDeriv[m->D_rowadr[r] + k] = or_qDeriv(m, d, r, m->D_colind[m->D_rowadr[r] + k]);
     }
   }
+  or_dFluid(m, d, qDeriv);
   if (flg_bias) or_rne_vel(m, d, qDeriv);
+}
+
+/* address of (r, c) in the D sparsity (mapD2M's inverse lookup; c is an ancestor of r) */
+static int or_Dadr(const mjhipModel* m, int r, int c) {
+  for (int a = m->D_rowadr[r]; a < m->D_rowadr[r] + m->D_rownnz[r]; a++) {
+    if (m->D_colind[a] == c) return a;
+  }
+  return -1;                                  /* SHOULD NOT OCCUR */
 }
 
 /* engine_inverse.c:81-164 mj_discreteAcc:
@@ -4974,16 +5801,20 @@ void or_smoothVel(const mjhipModel* m, const mjhipData* d, mjtNum* qDeriv, int f
 static void or_discreteAcc(const mjhipModel* m, mjhipData* d) {
   int nv = m->nv;
   if (m->opt.integrator == mjhipINT_IMPLICITFAST) {
+    /* mjd_smooth_vel(flg_bias = 0) on the D sparsity, reduced to qM's (mapD2M) */
     mjtNum* qMsave = (mjtNum*)malloc(m->nM*sizeof(mjtNum));
     mjtNum* qfrc = (mjtNum*)malloc(nv*sizeof(mjtNum));
+    mjtNum* qDeriv = (mjtNum*)malloc((m->nD + 1)*sizeof(mjtNum));
+    or_smoothVel(m, d, qDeriv, 0);
     mju_copy(qMsave, d->qM, m->nM);
     for (int r = 0; r < nv; r++) {          /* qM += qDerivReduced * -h */
       int adr = m->dof_Madr[r];
       for (int c = r; c >= 0; c = m->dof_parentid[c]) {
-        d->qM[adr] = d->qM[adr] + or_qDeriv(m, d, r, c) * -m->opt.timestep;
+        d->qM[adr] = d->qM[adr] + qDeriv[or_Dadr(m, r, c)] * -m->opt.timestep;
         adr++;
       }
     }
+    free(qDeriv);
     or_mulM(m, d, qfrc, d->qacc);
     mju_copy(d->qM, qMsave, m->nM);
     or_solveM(m, d, d->qacc, qfrc, 1);
@@ -5889,9 +6720,12 @@ static mjtNum or_rayCylinder(const mjtNum* pos, const mjtNum* mat, const mjtNum*
   return x;
 }
 
-/* ray_box :387-445 (without the per-face output) */
-static mjtNum or_rayBox(const mjtNum* pos, const mjtNum* mat, const mjtNum* size,
-                        const mjtNum* pnt, const mjtNum* vec) {
+/* ray_box :387-445; all (may be NULL): each face's hit, -1 for none */
+static mjtNum or_rayBoxAll(const mjtNum* pos, const mjtNum* mat, const mjtNum* size,
+                           const mjtNum* pnt, const mjtNum* vec, mjtNum* all) {
+  if (all) {
+    for (int i = 0; i < 6; i++) all[i] = -1;
+  }
   mjtNum ssz = size[0]*size[0] + size[1]*size[1] + size[2]*size[2];
   if (or_raySphere(pos, ssz, pnt, vec) < 0) return -1;
   const int iface[3][2] = {{1, 2}, {0, 2}, {0, 1}};
@@ -5907,10 +6741,167 @@ static mjtNum or_rayBox(const mjtNum* pos, const mjtNum* mat, const mjtNum* size
           mjtNum p1 = lpnt[iface[i][1]] + sol*lvec[iface[i][1]];
           if (fabs(p0) <= size[iface[i][0]] && fabs(p1) <= size[iface[i][1]]) {
             if (x < 0 || sol < x) x = sol;
+            if (all) all[2*i + (side + 1)/2] = sol;
           }
         }
       }
     }
+  }
+  return x;
+}
+
+static mjtNum or_rayBox(const mjtNum* pos, const mjtNum* mat, const mjtNum* size,
+                        const mjtNum* pnt, const mjtNum* vec) {
+  return or_rayBoxAll(pos, mat, size, pnt, vec, NULL);
+}
+
+/* ray_triangle :132-186 */
+static mjtNum or_rayTriangle(mjtNum v[][3], const mjtNum* lpnt, const mjtNum* lvec,
+                             const mjtNum* b0, const mjtNum* b1) {
+  mjtNum dif[3][3], planar[3][2];
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) dif[i][j] = v[i][j] - lpnt[j];
+  }
+  for (int i = 0; i < 3; i++) {
+    planar[i][0] = mju_dot3(b0, dif[i]);
+    planar[i][1] = mju_dot3(b1, dif[i]);
+  }
+  if ((planar[0][0] > 0 && planar[1][0] > 0 && planar[2][0] > 0) ||
+      (planar[0][0] < 0 && planar[1][0] < 0 && planar[2][0] < 0) ||
+      (planar[0][1] > 0 && planar[1][1] > 0 && planar[2][1] > 0) ||
+      (planar[0][1] < 0 && planar[1][1] < 0 && planar[2][1] < 0)) {
+    return -1;
+  }
+  mjtNum A[4] = {planar[0][0]-planar[2][0], planar[1][0]-planar[2][0],
+                 planar[0][1]-planar[2][1], planar[1][1]-planar[2][1]};
+  mjtNum b[2] = {-planar[2][0], -planar[2][1]};
+  mjtNum det = A[0]*A[3] - A[1]*A[2];
+  if (fabs(det) < mjMINVAL) return -1;
+  mjtNum t0 = (A[3]*b[0] - A[1]*b[1]) / det;
+  mjtNum t1 = (-A[2]*b[0] + A[0]*b[1]) / det;
+  if (t0 < 0 || t1 < 0 || t0 + t1 > 1) return -1;
+  mju_sub3(dif[0], v[0], v[2]);
+  mju_sub3(dif[1], v[1], v[2]);
+  mju_sub3(dif[2], lpnt, v[2]);
+  mjtNum nrm[3];
+  mju_cross(nrm, dif[0], dif[1]);
+  mjtNum denom = mju_dot3(lvec, nrm);
+  if (fabs(denom) < mjMINVAL) return -1;
+  return -mju_dot3(dif[2], nrm) / denom;
+}
+
+/* the basis b0, b1 of the plane normal to the local ray (mj_rayHfield :497-509, mju_rayTree
+   :651-663) */
+static void or_rayBasis(const mjtNum lvec[3], mjtNum b0[3], mjtNum b1[3]) {
+  b0[0] = b0[1] = b0[2] = 1;
+  if (fabs(lvec[0]) >= fabs(lvec[1]) && fabs(lvec[0]) >= fabs(lvec[2])) {
+    b0[0] = 0;
+  } else if (fabs(lvec[1]) >= fabs(lvec[2])) {
+    b0[1] = 0;
+  } else {
+    b0[2] = 0;
+  }
+  mju_addScl3(b1, b0, lvec, -mju_dot3(lvec, b0)/mju_dot3(lvec, lvec));
+  mju_normalize3(b1);
+  mju_cross(b0, b1, lvec);
+  mju_normalize3(b0);
+}
+
+/* mj_rayHfield :453-595 (the reference's side-face indexing by nrow kept) */
+static mjtNum or_rayHfield(const mjhipModel* m, const mjhipData* d, int id, const mjtNum* pnt,
+                           const mjtNum* vec) {
+  const int hid = m->geom_dataid[id];
+  const int nrow = m->hfield_nrow[hid], ncol = m->hfield_ncol[hid];
+  const mjtNum* size = m->hfield_size + 4*hid;
+  const float* data = m->hfield_data + m->hfield_adr[hid];
+  const mjtNum* xpos = d->geom_xpos + 3*id;
+  const mjtNum* xmat = d->geom_xmat + 9*id;
+  mjtNum base_size[3] = {size[0], size[1], size[3]*0.5};
+  mjtNum base_pos[3] = {xpos[0] - xmat[2]*size[3]*0.5, xpos[1] - xmat[5]*size[3]*0.5,
+                        xpos[2] - xmat[8]*size[3]*0.5};
+  mjtNum top_size[3] = {size[0], size[1], size[2]*0.5};
+  mjtNum top_pos[3] = {xpos[0] + xmat[2]*size[2]*0.5, xpos[1] + xmat[5]*size[2]*0.5,
+                       xpos[2] + xmat[8]*size[2]*0.5};
+  mjtNum x = or_rayBoxAll(base_pos, xmat, base_size, pnt, vec, NULL);
+  mjtNum all[6];
+  mjtNum top_intersect = or_rayBoxAll(top_pos, xmat, top_size, pnt, vec, all);
+  if (top_intersect < 0) return x;
+  mjtNum lpnt[3], lvec[3], b0[3], b1[3];
+  or_rayMap(xpos, xmat, pnt, vec, lpnt, lvec);
+  or_rayBasis(lvec, b0, b1);
+  mjtNum seg[2] = {0, top_intersect};
+  for (int i = 0; i < 6; i++) {
+    if (all[i] > seg[1]) {
+      seg[0] = top_intersect;
+      seg[1] = all[i];
+    }
+  }
+  mjtNum dx = (2.0*size[0]) / (ncol-1), dy = (2.0*size[1]) / (nrow-1), SX[2], SY[2];
+  for (int i = 0; i < 2; i++) {
+    SX[i] = (lpnt[0] + seg[i]*lvec[0] + size[0]) / dx;
+    SY[i] = (lpnt[1] + seg[i]*lvec[1] + size[1]) / dy;
+  }
+  int cmin = mjMAX(0, (int)floor(mjMIN(SX[0], SX[1]))-1);
+  int cmax = mjMIN(ncol-1, (int)ceil(mjMAX(SX[0], SX[1]))+1);
+  int rmin = mjMAX(0, (int)floor(mjMIN(SY[0], SY[1]))-1);
+  int rmax = mjMIN(nrow-1, (int)ceil(mjMAX(SY[0], SY[1]))+1);
+  for (int r = rmin; r < rmax; r++) {
+    for (int c = cmin; c < cmax; c++) {
+      mjtNum va[3][3] = {
+        {dx*c-size[0], dy*r-size[1], data[r*ncol+c]*size[2]},
+        {dx*(c+1)-size[0], dy*(r+1)-size[1], data[(r+1)*ncol+(c+1)]*size[2]},
+        {dx*(c+1)-size[0], dy*r-size[1], data[r*ncol+(c+1)]*size[2]}};
+      mjtNum sol = or_rayTriangle(va, lpnt, lvec, b0, b1);
+      if (sol >= 0 && (x < 0 || sol < x)) x = sol;
+      mjtNum vb[3][3] = {
+        {dx*c-size[0], dy*r-size[1], data[r*ncol+c]*size[2]},
+        {dx*(c+1)-size[0], dy*(r+1)-size[1], data[(r+1)*ncol+(c+1)]*size[2]},
+        {dx*c-size[0], dy*(r+1)-size[1], data[(r+1)*ncol+c]*size[2]}};
+      sol = or_rayTriangle(vb, lpnt, lvec, b0, b1);
+      if (sol >= 0 && (x < 0 || sol < x)) x = sol;
+    }
+  }
+  for (int i = 0; i < 4; i++) {
+    if (all[i] >= 0 && (all[i] < x || x < 0)) {
+      mjtNum z = (lpnt[2] + all[i]*lvec[2]) / size[2];
+      mjtNum y, y0, z0, z1;
+      if (i < 2) {
+        y = (lpnt[1] + all[i]*lvec[1] + size[1]) / dy;
+        y0 = mjMAX(0, mjMIN(nrow-2, floor(y)));
+        z0 = (mjtNum)data[(int)round(y0)*nrow + (i == 1 ? ncol-1 : 0)];
+        z1 = (mjtNum)data[(int)round(y0+1)*nrow + (i == 1 ? ncol-1 : 0)];
+      } else {
+        y = (lpnt[0] + all[i]*lvec[0] + size[0]) / dx;
+        y0 = mjMAX(0, mjMIN(ncol-2, floor(y)));
+        z0 = (mjtNum)data[(int)round(y0) + (i == 3 ? (nrow-1)*ncol : 0)];
+        z1 = (mjtNum)data[(int)round(y0+1) + (i == 3 ? (nrow-1)*ncol : 0)];
+      }
+      if (z < z0*(y0+1-y) + z1*(y-y0)) x = all[i];
+    }
+  }
+  return x;
+}
+
+/* mj_rayMesh :800-813: the bounding box, then every face (mju_rayTree :628-730 visits the
+   faces whose bounding volumes the ray crosses; the nearest hit over all faces is the same) */
+static mjtNum or_rayMesh(const mjhipModel* m, const mjhipData* d, int id, const mjtNum* pnt,
+                         const mjtNum* vec) {
+  const mjtNum* xpos = d->geom_xpos + 3*id;
+  const mjtNum* xmat = d->geom_xmat + 9*id;
+  if (or_rayBoxAll(xpos, xmat, m->geom_size + 3*id, pnt, vec, NULL) < 0) return -1;
+  const int mid = m->geom_dataid[id];
+  mjtNum lpnt[3], lvec[3], b0[3], b1[3];
+  or_rayMap(xpos, xmat, pnt, vec, lpnt, lvec);
+  or_rayBasis(lvec, b0, b1);
+  mjtNum x = -1;
+  for (int f = m->mesh_faceadr[mid]; f < m->mesh_faceadr[mid] + m->mesh_facenum[mid]; f++) {
+    mjtNum v[3][3];
+    for (int i = 0; i < 3; i++) {
+      const float* vf = m->mesh_vert + 3*(m->mesh_face[3*f + i] + m->mesh_vertadr[mid]);
+      for (int j = 0; j < 3; j++) v[i][j] = (mjtNum)vf[j];
+    }
+    mjtNum sol = or_rayTriangle(v, lpnt, lvec, b0, b1);
+    if (sol >= 0 && (x < 0 || sol < x)) x = sol;
   }
   return x;
 }
@@ -5942,15 +6933,24 @@ static int or_rayEliminate(const mjhipModel* m, int g, int bodyexclude) {
 }
 
 /* :1145-1185 mj_ray (geomgroup NULL, flg_static 1): the nearest hit, -1 for none; the geom hit
- * in *geomid */
+ * in *geomid (exported below for the tests as or_rayTest) */
+static mjtNum or_ray(const mjhipModel* m, const mjhipData* d, const mjtNum* pnt, const mjtNum* vec,
+              int bodyexclude, int* geomid);
+mjtNum or_rayTest(const mjhipModel* m, const mjhipData* d, const mjtNum* pnt,
+                  const mjtNum* vec, int bodyexclude, int* geomid) {
+  return or_ray(m, d, pnt, vec, bodyexclude, geomid);
+}
 static mjtNum or_ray(const mjhipModel* m, const mjhipData* d, const mjtNum* pnt, const mjtNum* vec,
               int bodyexclude, int* geomid) {
   mjtNum dist = -1;
   if (geomid) *geomid = -1;
   for (int g = 0; g < m->ngeom; g++) {
     if (or_rayEliminate(m, g, bodyexclude)) continue;
-    const mjtNum nd = or_rayGeom(d->geom_xpos+3*g, d->geom_xmat+9*g, m->geom_size+3*g, pnt, vec,
-                                 m->geom_type[g]);
+    const int t = m->geom_type[g];
+    const mjtNum nd = t == mjhipGEOM_MESH ? or_rayMesh(m, d, g, pnt, vec) :
+                      t == mjhipGEOM_HFIELD ? or_rayHfield(m, d, g, pnt, vec) :
+                      or_rayGeom(d->geom_xpos+3*g, d->geom_xmat+9*g, m->geom_size+3*g, pnt, vec,
+                                 t);
     if (nd >= 0 && (nd < dist || dist < 0)) {
       dist = nd;
       if (geomid) *geomid = g;

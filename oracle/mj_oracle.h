@@ -107,6 +107,13 @@ void or_inverseFDEx(const mjhipModel* m, mjhipData* d, orEfc* efc, mjtNum eps,
                     int flg_actuation, mjtNum* DfDq, mjtNum* DfDv, mjtNum* DfDa, mjtNum* DsDq,
                     mjtNum* DsDv, mjtNum* DsDa, mjtNum* DmDq);
 
+/* test hooks: the reference tests' Penetration helper (mjc_ccd, one contact; returns the
+ * count, out = dist, dir[3], pos[3]) and mj_ray (geomgroup NULL, flg_static 1) */
+int or_ccdPenetration(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum margin,
+                      mjtNum tol, int kmax, mjtNum* out);
+mjtNum or_rayTest(const mjhipModel* m, const mjhipData* d, const mjtNum* pnt,
+                  const mjtNum* vec, int bodyexclude, int* geomid);
+
 /* mj_compareFwdInv (engine_inverse.c:275-316) on the rows in efc (a forward pass's) */
 void or_compareFwdInv(const mjhipModel* m, mjhipData* d, orEfc* efc);
 

@@ -80,6 +80,11 @@ def lib():
                                  _D, _D]
     L.or_compareFwdInv.argtypes = [M, Dp, E]
     L.or_inverseBatch.argtypes = [M, ctypes.c_int, _D, _D, _D, _D, ctypes.c_int]
+    L.or_ccdPenetration.argtypes = [M, Dp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                    ctypes.c_double, ctypes.c_int, _D]
+    L.or_ccdPenetration.restype = ctypes.c_int
+    L.or_rayTest.argtypes = [M, Dp, _D, _D, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
+    L.or_rayTest.restype = ctypes.c_double
     L.or_inverseBatch.restype = ctypes.c_double
     _lib = L
   return _lib
@@ -233,6 +238,21 @@ class Oracle:
     if sensors:
       return DfDq, DfDv, DfDa, DmDq, tuple(x[:, :ns] for x in Ds)
     return DfDq, DfDv, DfDa, DmDq
+
+  def penetration(self, g1, g2, margin=0.0, tol=1e-6, kmax=1000):
+    """The reference tests' Penetration helper (engine_collision_gjk_test.cc:86-150) on the
+    current frames (run inverse() first): (ncon, dist, dir, pos)."""
+    out = np.zeros(7)
+    n = self.L.or_ccdPenetration(*self._args()[:2], g1, g2, margin, tol, kmax, _p(out))
+    return n, out[0], out[1:4], out[4:7]
+
+  def ray(self, pnt, vec, bodyexclude=-1):
+    """mj_ray (geomgroup NULL, flg_static 1) on the current frames: (distance, geomid)."""
+    gid = ctypes.c_int(-1)
+    pnt = np.ascontiguousarray(pnt, dtype=np.float64)
+    vec = np.ascontiguousarray(vec, dtype=np.float64)
+    x = self.L.or_rayTest(*self._args()[:2], _p(pnt), _p(vec), bodyexclude, ctypes.byref(gid))
+    return x, gid.value
 
   def inverse_batch(self, qpos, qvel, qacc, nthread=1, lib=None):
     """CPU baseline over B instances; returns (qfrc_inverse [B, nv], seconds). lib: another

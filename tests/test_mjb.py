@@ -248,3 +248,26 @@ def test_round_trip_round2_features(name, tmp_path):
   for f in fields.MODEL_FIELDS:
     np.testing.assert_array_equal(getattr(m, f.name), getattr(r, f.name), err_msg=f.name)
   assert fields.model_signature(r) == fields.model_signature(m)
+
+
+def test_round_trip_reference_model(tmp_path):
+  """The reference's inverse-test model (mesh, height field, fluid, actuator dynamics):
+  collision-mesh vertices, faces and hull graph and the height-field data survive the .mjb
+  layout; a model with an SDF geom is refused."""
+  import sys
+  sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+  import reference_model_states as R
+  m = R.model()
+  path = tmp_path / "model.mjb"
+  mjb.save(m, str(path))
+  r = mjb.load(str(path))
+  for f in fields.MODEL_FIELDS:
+    np.testing.assert_array_equal(getattr(m, f.name), getattr(r, f.name), err_msg=f.name)
+  assert r.sizes["nmeshgraph"] == m.sizes["nmeshgraph"] > 0
+  assert fields.model_signature(r) == fields.model_signature(m)
+  buf = bytearray(mjb.write(m))
+  ints = dict(zip(mjb.INTS, struct.unpack_from("<83i", buf, 20)))
+  off = mjb.offsets(ints)["geom_type"]
+  struct.pack_into("<i", buf, off + 4 * 5, 8)
+  with pytest.raises(mjb.MJBError, match="SDF"):
+    mjb.read(bytes(buf))

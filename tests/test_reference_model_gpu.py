@@ -1,0 +1,111 @@
+"""The reference's own inverse-dynamics test model on the GPU.
+
+test/testdata/model.xml (engine_inverse_test.cc:32-123; fixture tests/golden/testdata_model.npz
+made by tests/golden/make_reference_model.py) through the engine: the keyframe state of the
+reference's own simulation (its wheel resting on the height field), the free boxes on the
+icosahedron mesh and on the height field's peak, and perturbations of them. Counts exact, every
+contact and qfrc_inverse against the oracle; no instance flagged UNSUPPORTED.
+
+Tolerance: box-mesh, cylinder-box and every height-field pair come from the iterative native
+solver (GJK/EPA; hill-climbing support over the hull graph for the mesh, one triangular prism
+per grid cell for the height field), whose depth is defined to ccd_tolerance and moves under
+the device's FMA contraction of its inputs (convex pairs): instances with such a
+contact are held to 1e-6 relative, the others to the north-star 1e-10, and the closed-form
+contacts (plane-cylinder, plane-ellipsoid, box-box) to 1e-12 in the contact list itself.
+"""
+import numpy as np
+import pytest
+
+from mujoco_inversedynamicstest_amd import engine
+
+import reference_model_states as R
+
+pytestmark = pytest.mark.gpu
+
+HFIELD, MESH = 1, 7
+
+
+def uses_ccd(t1, t2):
+  """mjhip_pairUsesCcd (include/mjhip_contact.h) for type-ordered t1 <= t2."""
+  if t1 == HFIELD:
+    return 2 <= t2 <= MESH
+  if t1 == 0:
+    return False
+  if t2 in (4, MESH):
+    return True
+  if t2 == 5:
+    return t1 in (3, 4, 5)
+  if t2 == 6:
+    return t1 in (4, 5)
+  return False
+
+
+def _oracle_run(m, q, v, a):
+  from oracle.oracle import Oracle
+  o = Oracle(m)
+  f, st, nefc, ncon, ccd = [], [], [], [], []
+  for i in range(len(q)):
+    f.append(o.inverse(q[i], v[i], a[i]).copy())
+    st.append(o.d.status)
+    nefc.append(o.d.nefc)
+    ncon.append(o.efc.ncon)
+    g = o.contact_field("con_geom").reshape(-1, 2)
+    ccd.append(any(uses_ccd(m.geom_type[x[0]], m.geom_type[x[1]]) for x in g))
+  return np.array(f), np.array(st), np.array(nefc), np.array(ncon), np.array(ccd)
+
+
+@pytest.mark.parametrize("specialize", [False, True])
+def test_reference_model_vs_oracle(specialize):
+  m = R.model()
+  q, v, a = R.states(m, 96, seed=11)
+  B = len(q)
+  e = engine.InverseEngine(m, capacity=B, specialize=specialize)
+  try:
+    f, st = e.inverse(q, v, a, status=True)
+    nefc = e.field_int("efc_count", 0, B)[:, 0]
+    ncon = e.field_int("con_count", 0, B)[:, 0]
+  finally:
+    e.close()
+  ref, rst, rnefc, rncon, ccd = _oracle_run(m, q, v, a)
+  np.testing.assert_array_equal(st, rst)
+  assert (st == 0).all()
+  np.testing.assert_array_equal(ncon, rncon)
+  np.testing.assert_array_equal(nefc, rnefc)
+  scale = np.maximum(1.0, np.abs(ref).max(axis=1))
+  err = np.abs(f - ref).max(axis=1) / scale
+  assert err[~ccd].max(initial=0) <= 1e-10, f"error {err[~ccd].max():.3e}"
+  assert err[ccd].max(initial=0) <= 1e-6, f"mesh-contact error {err[ccd].max():.3e}"
+  print(f"qfrc_inverse error: median {np.median(err):.2e}, max {err.max():.2e}")
+  assert (rncon > 0).all() and ccd.sum() >= B // 4
+
+
+def test_reference_model_contacts_on_device():
+  """The contact list itself (geom pair, distance, frame): closed-form pairs equal to the
+  oracle to 1e-12, pairs from the native solver to 1e-6 (its tolerance)."""
+  from oracle.oracle import Oracle
+  m = R.model()
+  q, v, a = R.states(m, 24, seed=4)
+  B = len(q)
+  e = engine.InverseEngine(m, capacity=B, specialize=False)
+  try:
+    e.inverse(q, v, a)
+    ncon = e.field_int("con_count", 0, B)[:, 0]
+    geom = e.field_int("con_geom", 0, B)
+    dist = e.field("con_dist", 0, B)
+    frame = e.field("con_frame", 0, B)
+  finally:
+    e.close()
+  o = Oracle(m)
+  hf = 0
+  for i in range(B):
+    o.inverse(q[i], v[i], a[i])
+    n = o.efc.ncon
+    assert ncon[i] == n
+    np.testing.assert_array_equal(geom[i, :2*n], o.contact_field("con_geom").reshape(-1))
+    tol = np.array([1e-6 if uses_ccd(*m.geom_type[geom[i, 2*k:2*k+2]]) else 1e-12
+                    for k in range(n)])
+    assert (np.abs(dist[i, :n] - o.contact_field("con_dist").reshape(-1)) <= tol).all()
+    dframe = np.abs(frame[i, :9*n] - o.contact_field("con_frame").reshape(-1)).reshape(n, 9)
+    assert (dframe.max(axis=1) <= tol).all()
+    hf += int(np.sum(m.geom_type[geom[i, :2*n:2]] == HFIELD))
+  assert hf >= B                    # height-field contacts on every state
