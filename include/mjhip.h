@@ -391,6 +391,39 @@ MJHIP_API int mjhip_modelCapacity(const mjhipModel* m, int* efc_rows, int* conta
 MJHIP_API int mjhip_timeInverseKernel(mjhipContext* c, int B, int reps, int skipstage,
                                       int flags, float* ms);
 
+/* Per-stage timers: the reference's mjtTimer slots (include/mujoco/mjdata.h) and mjTimerStat,
+ * which mj_invPosition, mj_invConstraint and mj_inverseSkip accumulate
+ * (engine_inverse.c:38-67, :170-191, :199-260). With timers on (mjhip_contextTimers),
+ * every mjhip_inverseBatch call of the context adds to them:
+ *   INVERSE         device wall time of the call (HIP events on its stream, milliseconds)
+ *   POSITION        POS_KINEMATICS + POS_INERTIA + POS_COLLISION + POS_MAKE
+ *   POS_KINEMATICS  kinematics, comPos, camlight, tendons, transmission (the straight-line
+ *                   kernels' position stage, which also forms qM by crb)
+ *   POS_INERTIA     crb + factorM (factorM alone on the straight-line path)
+ *   POS_COLLISION   mj_collision          POS_MAKE    mj_makeConstraint
+ *   VELOCITY        mj_invVelocity (comVel, passive, RNE bias; the straight-line kernels'
+ *                   velocity stage, RNE with qacc included)
+ *   CONSTRAINT      mj_discreteAcc + mj_invConstraint (reference, update, J'force)
+ * Stage durations are the mean wall time (the 100 MHz device clock) a wavefront of 64
+ * instances spends in the stage, in milliseconds; `number` counts the calls. The phase marks
+ * are read by lane 0 of each wave: timed calls synchronize the stream, and one context per
+ * process is timed at a time. */
+typedef enum mjhipTimer_ {
+  mjhipTIMER_STEP = 0, mjhipTIMER_FORWARD, mjhipTIMER_INVERSE, mjhipTIMER_POSITION,
+  mjhipTIMER_VELOCITY, mjhipTIMER_ACTUATION, mjhipTIMER_CONSTRAINT, mjhipTIMER_ADVANCE,
+  mjhipTIMER_POS_KINEMATICS, mjhipTIMER_POS_INERTIA, mjhipTIMER_POS_COLLISION,
+  mjhipTIMER_POS_MAKE, mjhipTIMER_POS_PROJECT, mjhipTIMER_COL_BROAD, mjhipTIMER_COL_NARROW,
+  mjhipNTIMER
+} mjhipTimer;
+typedef struct mjhipTimerStat_ {
+  mjtNum duration;                  /* accumulated milliseconds */
+  int number;                       /* number of calls */
+} mjhipTimerStat;
+/* enable != 0: allocate the accumulator and time the following calls; 0: stop timing */
+MJHIP_API int mjhip_contextTimers(mjhipContext* c, int enable);
+/* copy the mjhipNTIMER slots to out; reset != 0 clears them afterwards */
+MJHIP_API int mjhip_timerRead(mjhipContext* c, mjhipTimerStat* out, int reset);
+
 /*---------------------------- single-instance drop-in -------------------------------------*/
 /* Same semantics and outputs as the reference functions of the same name (engine_inverse.c,
  * engine_core_smooth.c, engine_support.c, engine_derivative_fd.c); they run one instance on

@@ -82,6 +82,9 @@ ALL_WAVES = 1
 # the later stages re-read (qM, cinert, cdof) from L2; -DMJHIP_NO_NT compiles them as plain
 # stores (the A/B build)
 NT_STORES = True
+# experiment knob (tools/exp_variants.py): None = keep every re-read field temporal; else the
+# set of fields whose stores stay temporal (all others stream, re-read or not)
+NT_TEMPORAL = None
 
 
 def _ll(st):
@@ -146,6 +149,44 @@ def fast_path_supported(m) -> str | None:
 # read actuators, so their actuator_length/moment/velocity can come last; a body transmission
 # needs the instance's contacts, which only the constraint kernel makes.
 TRN_AFTER = (2, 4, 5)
+
+
+def _pair_uses_ccd(t1, t2) -> bool:
+  """mjhip_pairUsesCcd (include/mjhip_contact.h) for type-ordered t1 <= t2: the pair runs
+  the iterative native solver (mjc_Convex, mjc_ConvexHField)."""
+  if t1 == 1:                                           # height field
+    return 2 <= t2 <= 7
+  if t1 == 0:
+    return False
+  if t2 in (4, 7):                                      # ellipsoid, mesh
+    return True
+  if t2 == 5:                                           # cylinder
+    return t1 in (3, 4, 5)
+  if t2 == 6:                                           # box
+    return t1 in (4, 5)
+  return False
+
+
+def exact_fp(m) -> bool:
+  """True when some collidable geom pair runs the iterative native solver. Its result moves
+  by up to ccd_tolerance under a last-bit change of the geom frames, so the generated
+  kernels of such a model compute the frames without multiply-add contraction, rounding
+  each operation as the reference does (the solver itself is compiled that way too,
+  csrc/engine_device.h)."""
+  if int(m.opt["disableflags"]) & ((1 << 4) | 1):       # contact or constraint disabled
+    return False
+  ng = m.sizes["ngeom"]
+  t = np.asarray(m.geom_type)[:ng]
+  ct = np.asarray(m.geom_contype)[:ng]
+  ca = np.asarray(m.geom_conaffinity)[:ng]
+  wb = np.asarray(m.body_weldid)[np.asarray(m.geom_bodyid)[:ng]]
+  for i in range(ng):
+    for j in range(i + 1, ng):
+      if wb[i] == wb[j] or not ((ct[i] & ca[j]) or (ct[j] & ca[i])):
+        continue
+      if _pair_uses_ccd(min(t[i], t[j]), max(t[i], t[j])):
+        return True
+  return False
 
 
 def spatial_tendons(m) -> list:
@@ -1289,6 +1330,8 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   if NT_STORES:
     import re
     reread = set(re.findall(r"= P_(\w+)\[", "\n".join(bodies.values())))
+    if NT_TEMPORAL is not None:
+      reread = set(NT_TEMPORAL)
     store = re.compile(r"^(\s*)P_(\w+)\[(\d+)\*64\] = (.+);$")
 
     def nt(line):
@@ -1299,6 +1342,9 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
     bodies = {st: "\n".join(nt(x) for x in b.split("\n")) for st, b in bodies.items()}
   out = [f"// GENERATED by mujoco_inversedynamicstest_amd/codegen.py -- do not edit.",
          f"// model '{name}' (nq={m.nq} nv={m.nv} nbody={m.nbody}), hash {model_hash(m)}"]
+  exact = exact_fp(m)
+  if exact:   # frames for the native solver: every operation rounded (exact_fp)
+    out.append("#if defined(__clang__)\n#pragma clang fp contract(off)\n#endif")
   for st in STAGES:
     params, args = _SIG[st]
     out.append(f"MJH_HD void fast_{st}_{name}(const Mirror& mr, int blk, int lane, int B, "
@@ -1386,9 +1432,11 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   if (worklist_next && blockIdx.x == 0 && threadIdx.x == 0) *worklist_next = 0;
   int blk0 = 0;
   if (range) {{ blk0 = range[0] >> 6; B = range[1]; }}
+  MJH_PHASE0(19, 27);
 """ + "\n".join(f"  fast_{st}_{name}(mr, {bl}, B, "
                 f"{_SIG[st][1].replace('worklist_next', 'nullptr')});\n"
-                f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE();" for st in STAGES)
+                f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE(); MJH_PHASE({20 + k});"
+                for k, st in enumerate(STAGES))
              + "\n" + fuse_tail + "}")
   # k_vaskip: the va stage of mj_inverseSkip(mjSTAGE_POS) for mjd_inverseFD's qvel and qacc
   # perturbations (engine_derivative_fd.c:646-699). Instance off + t reads every position-
@@ -1450,6 +1498,8 @@ static void launch_vaskip_{name}(hipStream_t s, const Mirror& mr, int B, int off
       out.append(f"  hipLaunchKernelGGL(k_{st}_{name}, {gb}, 0, s, mr, B, {args});")
   out.append("}")
   out.append("#endif")
+  if exact:
+    out.append("#if defined(__clang__)\n#pragma clang fp contract(fast)\n#endif")
   return "\n".join(out) + "\n"
 
 

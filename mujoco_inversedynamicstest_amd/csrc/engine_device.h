@@ -30,29 +30,55 @@
   #define MJH_HD inline
 #endif
 
-// Phase timing for performance experiments (tools/exp_phases.py builds a separate library
-// with -DMJH_PHASE_TIMING): lane 0 of each wave adds the wall clock at phase mark k, so
-// mean(mark k) - mean(mark k-1) over waves is the mean duration of phase k. Empty otherwise.
-#if defined(MJH_PHASE_TIMING) && defined(__HIPCC__)
-__device__ unsigned long long mjh_phase_acc[32];
+// Per-stage timers (mjhip_contextTimers: the reference's mjTIMER_* table, include/mjhip.h).
+// While a context has them on, mjh_tbuf points at its accumulator (MJH_TSLOTS counters) and
+// lane 0 of every wave adds the 100 MHz wall clock at each phase mark, so the mean over
+// waves of mark k minus mark k-1 is the mean wall time a wave spends in phase k; a group's
+// first mark also counts the waves. Null otherwise: one scalar load and a branch per mark.
+// Marks: generic k_inverse 0-9 (waves counted in 24), k_constraint 10-13 (25),
+// k_constraint_coop 14-18 (26), the straight-line k_all 19-22 (27). Experiment builds
+// (-DMJH_PHASE_TIMING, tools/exp_phases.py) add per-contact spans in slots 40-45.
+#define MJH_TSLOTS 48
+#if defined(__HIPCC__)
+#if defined(MJH_TBUF_EXTERN)                // a run-time code object: found by name
+extern "C" {
+__device__ unsigned long long* mjh_tbuf = nullptr;
+}
+#else
+static __device__ unsigned long long* mjh_tbuf = nullptr;
 #endif
-#if defined(MJH_PHASE_TIMING) && defined(__HIP_DEVICE_COMPILE__)
+#endif
+#if defined(__HIP_DEVICE_COMPILE__)
 #define MJH_PHASE(k)                                                                  \
   do {                                                                                \
-    if ((threadIdx.x & 63) == 0) atomicAdd(&mjh_phase_acc[k], wall_clock64());       \
+    unsigned long long* tb_ = mjh_tbuf;                                               \
+    if (tb_ && (threadIdx.x & 63) == 0) atomicAdd(&tb_[k], wall_clock64());            \
   } while (0)
-// spans inside a lane's own work (lane 0's): MJH_TICK(t) reads the clock, MJH_SPAN(k, a, b)
-// adds b - a to slot k (slot k + 1 counts the spans)
-#define MJH_TICK(t) const unsigned long long t = wall_clock64()
-#define MJH_SPAN(k, a, b)                                                             \
+#define MJH_PHASE0(k, c)                                                              \
   do {                                                                                \
-    if ((threadIdx.x & 63) == 0) {                                                    \
-      atomicAdd(&mjh_phase_acc[k], (b) - (a));                                        \
-      atomicAdd(&mjh_phase_acc[(k) + 1], 1ull);                                       \
+    unsigned long long* tb_ = mjh_tbuf;                                               \
+    if (tb_ && (threadIdx.x & 63) == 0) {                                             \
+      atomicAdd(&tb_[k], wall_clock64());                                             \
+      atomicAdd(&tb_[c], 1ull);                                                       \
     }                                                                                 \
   } while (0)
 #else
 #define MJH_PHASE(k) do {} while (0)
+#define MJH_PHASE0(k, c) do {} while (0)
+#endif
+#if defined(MJH_PHASE_TIMING) && defined(__HIP_DEVICE_COMPILE__)
+// spans inside a lane's own work (lane 0's): MJH_TICK(t) reads the clock, MJH_SPAN(k, a, b)
+// adds b - a to slot 40 + k (slot 41 + k counts the spans)
+#define MJH_TICK(t) const unsigned long long t = wall_clock64()
+#define MJH_SPAN(k, a, b)                                                             \
+  do {                                                                                \
+    unsigned long long* tb_ = mjh_tbuf;                                               \
+    if (tb_ && (threadIdx.x & 63) == 0) {                                             \
+      atomicAdd(&tb_[40 + (k)], (b) - (a));                                           \
+      atomicAdd(&tb_[41 + (k)], 1ull);                                                \
+    }                                                                                 \
+  } while (0)
+#else
 #define MJH_TICK(t) do {} while (0)
 #define MJH_SPAN(k, a, b) do {} while (0)
 #endif
@@ -1768,6 +1794,14 @@ MJH_HD void boxBoxEmit(double margin, const double pos1[3], const double mat1[9]
 }
 
 //---------------------------------- native convex collision ----------------------------------
+// The solver is iterative and stops at ccd_tolerance, so a last-bit change of an operation
+// can move its result by that much: everything from here to the end of mjc_ConvexHField is
+// compiled without multiply-add contraction, so each operation rounds as in the reference
+// (and in the oracle's -ffp-contract=off build); the kernels that feed it their geom frames
+// do the same for models with such pairs (codegen.py, exact_fp).
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
 // mjc_Convex (engine_collision_convex.c:915-1001, mjENBL_MULTICCD off: one contact) and
 // mjc_PlaneConvex (:1045-1080, a geom without mesh data: the ellipsoid) on MuJoCo's native
 // GJK/EPA solver mjc_ccd (engine_collision_gjk.c:2215-2343). Everything the solver indexes at
@@ -3336,6 +3370,9 @@ MJH_HD void colConvexHField(const mjhipModel& m, const Lane<S>& d, int g1, int g
     }
   }
 }
+#if defined(__clang__)
+#pragma clang fp contract(fast)          // the default of this build again (see above)
+#endif
 
 // mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
 // WRITE = false only counts the contacts the pair produces (the cooperative constraint
@@ -5360,9 +5397,9 @@ MJH_HD void contactRowsFused(const mjhipModel& m, const Lane<S>& d, int i, int n
     finishRowFused(d, row, tp, kb, R, dist, incl, 0, vel, acc);
   }
   MJH_TICK(tc3);
-  MJH_SPAN(20, tc0, tc1);       // contact data, impedance, R
-  MJH_SPAN(22, tc1, tc2);       // the dof loop
-  MJH_SPAN(24, tc2, tc3);       // row fields and finish
+  MJH_SPAN(0, tc0, tc1);        // contact data, impedance, R
+  MJH_SPAN(2, tc1, tc2);        // the dof loop
+  MJH_SPAN(4, tc2, tc3);        // row fields and finish
 }
 
 #if defined(__HIPCC__)   // wave shuffles: HIP builds only (the host harness has no lanes)
@@ -7804,7 +7841,7 @@ MJH_HD void sensorsAfter(const mjhipModel& m, const Lane<S>& d, bool sensors = t
 template <int S, bool CONTACT, bool FUSED>
 MJH_HD int constraintOnly(const mjhipModel& m, const Lane<S>& d) {
   int status = 0;
-  MJH_PHASE(10);
+  MJH_PHASE0(10, 25);
   if constexpr (CONTACT) collision(m, d, &status);
   else d.con_count[0] = 0;
   MJH_PHASE(11);

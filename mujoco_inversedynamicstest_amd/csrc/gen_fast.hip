@@ -10,3 +10,9 @@ static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr, 0}};
 #endif
 
 const FastKernelEntry* mjhip_fastKernels() { return g_fast_kernels; }
+
+// this translation unit's copy of the per-stage timer pointer (engine_device.h mjh_tbuf;
+// mjhip_contextTimers); a blocking copy: timed calls are synchronous
+int mjhip_genSetTimerBuf(unsigned long long* p) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(mjh_tbuf), &p, sizeof(p)) != hipSuccess;
+}

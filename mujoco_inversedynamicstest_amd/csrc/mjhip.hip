@@ -25,621 +25,13 @@
 
 #include "engine_device.h"
 #include "fast_kernels.h"
+#include "kernels.h"
 #include "post_pass.h"
-
-using mjh::Lane;
-using mjh::SP;
 
 //==================================== kernels ===============================================
 
-// Straight-line kernels generated per bundled model by codegen.py (build(), gen_fast.hip),
-// selected by model signature (mjhip_fastKernels); each appends limit-active instances to a
-// work-list that the constraint kernel then serves.
-
-// generic pipeline over the instances of a work-list (limit-active instances of the fast
-// path); grid = ceil(B/64) blocks, threads past *count exit at once
-// the fused constraint path's chain masks, one per body, shared by the block (LDS)
-#define MJHIP_CHAIN_TABLE(FUSED)                                                         \
-  __shared__ unsigned long long chain[64];                                                \
-  if (FUSED) {                                                                            \
-    if ((int)threadIdx.x < m.nbody) chain[threadIdx.x] = mjh::chainMask(m, threadIdx.x);  \
-    __syncthreads();                                                                      \
-  }
-
-// fused contact kernels: collision reads geom positions from a per-lane LDS copy (dynamic
-// shared memory of mjh::gstageBytes, [3*ngeom][64 lanes])
-extern __shared__ double g_gstage[];
-#define MJHIP_GEOM_STAGE(C, F)                                                           \
-  if (C && F) {                                                                           \
-    d.gxpos.p = g_gstage + threadIdx.x;                                                   \
-    d.gstage = true;                                                                      \
-  }
-
-// constraint part of mj_inverseSkip after the generated kernels (mjh::constraintOnly), over
-// the work-list (LIST) or every instance; grid = ceil(B/64) blocks
-template <bool CONTACT, bool FUSED, bool LIST>
-__global__ __launch_bounds__(64) void k_constraint(mjhipModel m, Mirror mr, int B,
-                                                   const int* __restrict__ worklist,
-                                                   const int* __restrict__ count,
-                                                   double* __restrict__ qfrc_out,
-                                                   int* __restrict__ status) {
-  const long n = LIST ? (long)*count : (long)B;
-  if ((long)blockIdx.x*64 >= n) return;      // whole block idle (uniform): before the barrier
-  MJHIP_CHAIN_TABLE(FUSED)
-  const long g = (long)blockIdx.x*64 + threadIdx.x;
-  if (LIST || !qfrc_out) {
-    if (g >= n) return;
-    const long inst = LIST ? worklist[g] : g;
-    Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
-    d.chain = chain;
-    MJHIP_GEOM_STAGE(CONTACT, FUSED)
-    const int st = mjh::constraintOnly<64, CONTACT, FUSED>(m, d);
-    if (status && st) status[inst] |= st;   // after the generated kernels' input checks
-    if (qfrc_out) {        // a few scattered work-list instances
-      for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
-    }
-    return;
-  }
-  // every instance with a row-major output: the block's rows go out coalesced through LDS
-  // (after the geom copy); lanes past B skip the work but join the copy
-  double* qo = g_gstage + ((CONTACT && FUSED) ? 3*m.ngeom*64 : 0);
-  if (g < n) {
-    Lane<64> d = lane_view(mr, (int)(g >> 6), (int)(g & 63));
-    d.chain = chain;
-    MJHIP_GEOM_STAGE(CONTACT, FUSED)
-    const int st = mjh::constraintOnly<64, CONTACT, FUSED>(m, d);
-    if (status && st) status[g] |= st;
-    for (int k = 0; k < m.nv; k++) qo[threadIdx.x*m.nv + k] = d.qfrc_inverse[k];
-  }
-  __syncthreads();
-  const long rows = n - (long)blockIdx.x*64 < 64 ? n - (long)blockIdx.x*64 : 64;
-  double* dst = qfrc_out + (long)blockIdx.x*64*m.nv;
-  for (long r = threadIdx.x; r < rows*m.nv; r += 64) dst[r] = qo[r];
-}
-
-
-// Cooperative constraint part (the fused path of k_constraint, G lanes per instance).
-//
-// One wave holds 64/G instances; the G lanes of an instance's group split its work:
-//   collision   the model's static geom-pair program (collisionPairs, host-built in the order
-//               the serial mj_collision emits contacts), G pairs per round: each lane counts
-//               its pair's contacts, a group prefix sum places them, the lane writes them
-//   rows        equality (lane 0), then friction and limit rows: every lane evaluates the
-//               predicates (so all agree on the row numbers), the owner of row r (r % G)
-//               writes and finishes it; contact rows: contact c belongs to lane c % G, a
-//               prefix sum over the contacts' row counts gives each its first row
-//   J'force     column-parallel (column j on lane j % G): each column's sum runs over the
-//               rows in order, as mju_mulMatTVec's, then the mj_inverse assembly
-// Every output equals the serial (one lane per instance) fused path's.
-template <int G>
-__device__ __forceinline__ int groupScan(int x, int sub, int* total) {
-  for (int o = 1; o < G; o <<= 1) {
-    const int y = __shfl_up(x, o, G);
-    if (sub >= o) x += y;
-  }
-  *total = __shfl(x, G - 1, G);
-  return x;                               // inclusive
-}
-
-template <int S>
-__device__ __forceinline__ void rowFields(const Lane<S>& d, int r, double pos, double margin,
-                                          double frictionloss, int type, int id) {
-  d.efc_pos[r] = pos;
-  d.efc_margin[r] = margin;
-  d.efc_frictionloss[r] = frictionloss;
-  d.efc_type[r] = type;
-  d.efc_id[r] = id;
-}
-
-// grid of k_constraint_coop: one group per instance, or for a work-list (whose length only
-// the device knows) at most one block per SIMD striding over it
-static unsigned coopGrid(int B, int G, bool list) {
-  const unsigned full = (unsigned)((B + 64/G - 1) / (64/G));
-  return list && full > 1024u ? 1024u : full;
-}
-
-// one entry of the cooperative kernel's pair program (host-built by coop_program in the order
-// of collision_pairs): the type-ordered geoms and their types, the pair's contact bound
-// (mjhip_pairMaxContacts; < 0: no collision function built here), its margin, and which
-// mj_filterSphere test applies with its bound formed as the reference forms it
-// (engine_collision_driver.c:1470-1497): filt 0 = bounding spheres, rb1 + rb2 + margin;
-// 1 = plane g1, margin + rb2; 2 = plane g2, margin + rb1; 3 = none
-struct CoopPair {
-  int g1, g2, t1, t2, kmax, filt;
-  int b1, b2, rt1, rt2;                     // the geoms' bodies and their roots
-  double margin, bound;
-};
-constexpr int kCoopPairDoubles = (int)(sizeof(CoopPair) / sizeof(double));
-static_assert(sizeof(CoopPair) % sizeof(double) == 0, "CoopPair packs into doubles");
-
-// dynamic LDS of k_constraint_coop: the pair program and geom_size once per block; per
-// instance 8 nv
-// doubles (cdof, qvel, qacc), qpos, the geom frames (geom_xpos, geom_xmat), the survivor
-// list of the sphere filter (npair ints), the bodies of the first kCoopContacts contacts (4
-// ints each) and the forces of the first kCoopRows rows (later ones are read back from
-// efc_force); with box-box pairs, 72 doubles per lane for their contact positions. The caps
-// keep a block small enough that every wave of a 4,096 batch is resident at once (the
-// humanoid's worst-case capacities, 273 contacts and 424 rows, would allow two blocks per CU).
-constexpr int kBoxBoxBuf = 72;
-constexpr int kCoopContacts = 64;
-#ifndef MJHIP_COOP_CQ
-#define MJHIP_COOP_CQ 2
-#endif
-constexpr int kCoopContactLanes = MJHIP_COOP_CQ;   // lanes per contact in the contact rows
-constexpr int kCoopRows = 128;
-__host__ __device__ static inline int coopContacts(int con_cap) {
-  return con_cap < kCoopContacts ? con_cap : kCoopContacts;
-}
-__host__ __device__ static inline int coopRows(int efc_cap) {
-  return efc_cap < kCoopRows ? efc_cap : kCoopRows;
-}
-__host__ __device__ static inline int coopPerInstance(const mjhipModel& m, int npair,
-                                                      int con_cap, int efc_cap) {
-  return 8*m.nv + m.nq + 12*m.ngeom + (npair + 1) / 2 + 3*coopContacts(con_cap) +
-         coopRows(efc_cap);
-}
-static unsigned coopLdsBytes(const mjhipModel& m, int G, int efc_cap, bool boxpair, int npair,
-                             int con_cap) {
-  return (unsigned)((kCoopPairDoubles*npair + 3*m.ngeom +
-                     (64 / G) * coopPerInstance(m, npair, con_cap, efc_cap) +
-                     (boxpair ? 64*kBoxBoxBuf : 0)) * sizeof(double));
-}
-
-template <int G, bool CONTACT, bool LIST, bool BOX = false>
-__global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr, int B,
-                                                        const int* __restrict__ worklist,
-                                                        const int* __restrict__ count,
-                                                        const CoopPair* __restrict__ pairs,
-                                                        const mjh::ContactParam* __restrict__ cparams,
-                                                        const unsigned long long* __restrict__ masks,
-                                                        int npair,
-                                                        double* __restrict__ qfrc_out,
-                                                        int* __restrict__ status) {
-  constexpr int IPB = 64 / G;               // instances per wave
-  const long n = LIST ? (long)*count : (long)B;
-  if ((long)blockIdx.x*IPB >= n) return;    // whole block idle (uniform): before the barriers
-  __shared__ unsigned long long chain[64], dchain[64];
-  __shared__ long s_inst[64 / G];            // the instance of each group (pooled contact rows)
-  __shared__ int s_ntask[64 / G];            // its staged contacts with rows
-  // the chain masks (host-built, coop_masks: bodies, then dofs on each body's chain for
-  // contactRowsSplit's bit test; the kernel runs for nbody, nv <= 64), the pair program and
-  // the geom sizes, once per block, all with independent loads
-  if ((int)threadIdx.x < m.nbody) {
-    chain[threadIdx.x] = masks[threadIdx.x];
-    dchain[threadIdx.x] = masks[m.nbody + threadIdx.x];
-  }
-  CoopPair* prog = reinterpret_cast<CoopPair*>(g_gstage);
-  double* gsize = g_gstage + kCoopPairDoubles*npair;
-  if (CONTACT) {
-    for (int e = threadIdx.x; e < kCoopPairDoubles*npair; e += 64) {
-      g_gstage[e] = reinterpret_cast<const double*>(pairs)[e];
-    }
-    for (int e = threadIdx.x; e < 3*m.ngeom; e += 64) gsize[e] = m.geom_size[e];
-  }
-  __syncthreads();
-  const int sub = threadIdx.x % G, slot = threadIdx.x / G;
-  const int ngeom = m.ngeom;
-  // grid-stride over the instances (a work-list launch uses at most one block per SIMD, so
-  // an empty or short list costs few workgroups); the bound is uniform over the block
-  for (long base = (long)blockIdx.x*IPB; base < n; base += (long)gridDim.x*IPB) {
-  const long g = base + slot;
-  const bool active = g < n;                // uniform within a group
-  const long inst = active ? (LIST ? (long)worklist[g] : g) : 0;
-  Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
-  d.chain = chain;
-  d.dchain = dchain;
-  const int nv = m.nv, dsbl = m.opt.disableflags;
-  int st = 0, ncon = 0;
-  MJH_PHASE(14);
-  // per-instance LDS (dynamic, coopLdsBytes): cdof/qvel/qacc for the contact rows, qpos,
-  // the geom frames for the collision phase, its survivor list, and the row forces for
-  // J'force; all staged by the group with independent loads
-  const int nq = m.nq, per = coopPerInstance(m, npair, d.con_cap, d.efc_cap);
-  double* lbase = g_gstage + kCoopPairDoubles*npair + 3*ngeom;
-  double* cdq = lbase + (long)slot*per;
-  double* qp = cdq + 8*nv;
-  double* gx = qp + nq;                     // geom_xpos (3 ngeom)
-  double* gm = gx + 3*ngeom;                // geom_xmat (9 ngeom)
-  int* surv = reinterpret_cast<int*>(gm + 9*ngeom);
-  int* cbody = reinterpret_cast<int*>(gm + 9*ngeom + (npair + 1) / 2);
-  const int ncb = coopContacts(d.con_cap);
-  int* task = cbody + 4*ncb;                // per staged contact: its first row, its condim
-  double* fst = gm + 9*ngeom + (npair + 1) / 2 + 3*ncb;
-  // box-box contact positions of this lane's pair (only models with box pairs get the room)
-  double* bbuf = lbase + (long)IPB*per + (long)threadIdx.x*kBoxBoxBuf;
-  const bool collide = CONTACT && mjhip_contactsEnabled(&m) && npair > 0;
-  if (active) {
-    for (int e = sub; e < 8*nv; e += G) {
-      const int j = e >> 3, c = e & 7;
-      cdq[e] = c < 6 ? d.cdof[6*j+c] : (c == 6 ? d.qvel[j] : d.qacc[j]);
-    }
-    for (int e = sub; e < nq; e += G) qp[e] = d.qpos[e];
-    if (collide) {
-      for (int e = sub; e < 3*ngeom; e += G) gx[e] = d.geom_xpos[e];
-      for (int e = sub; e < 9*ngeom; e += G) gm[e] = d.geom_xmat[e];
-    }
-  }
-  d.cdq = cdq;
-  d.fst = fst;
-  d.nfst = coopRows(d.efc_cap);
-  d.cbody = cbody;
-  d.ncbody = ncb;
-  __syncthreads();                          // the staged frames visible to the group
-
-  // ---- mj_collision over the static pair program: first mj_filterSphere on every pair
-  // (G pairs per round, frames from LDS) into an ordered survivor list, then the
-  // narrowphase of the survivors only, G per round
-  if (collide) {
-    const unsigned long long gmask = G == 64 ? ~0ull : ((1ull << G) - 1) << (slot*G);
-    const unsigned long long below = (1ull << (threadIdx.x % 64)) - 1;
-    int nsurv = 0;
-    for (int p0 = 0; p0 < npair; p0 += G) {
-      const int p = p0 + sub;
-      bool keep = false;
-      if (active && p < npair) {
-        const CoopPair& P = prog[p];
-        const double* p1 = gx + 3*P.g1;
-        const double* p2 = gx + 3*P.g2;
-        if (P.filt == 0) {
-          const double dif[3] = {p1[0]-p2[0], p1[1]-p2[1], p1[2]-p2[2]};
-          keep = !(dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2] > P.bound*P.bound);
-        } else if (P.filt <= 2) {           // the plane's normal against the other's centre
-          const bool pl1 = P.filt == 1;
-          const double* mat = gm + 9*(pl1 ? P.g1 : P.g2);
-          const double norm[3] = {mat[2], mat[5], mat[8]};
-          double dif[3];
-          mjh::sub3(dif, pl1 ? p2 : p1, pl1 ? p1 : p2);
-          keep = !(mjh::dot3(dif, norm) > P.bound);
-        } else {
-          keep = true;
-        }
-      }
-      const unsigned long long bal = __ballot(keep) & gmask;
-      if (keep) surv[nsurv + __popcll(bal & below)] = p;
-      nsurv += __popcll(bal);
-    }
-    // rounds over the survivors: the wave runs as many as its busiest group needs
-    int rounds = (nsurv + G - 1) / G;
-    for (int o = G; o < 64; o <<= 1) rounds = max(rounds, __shfl_xor(rounds, o));
-    for (int r = 0; r < rounds; r++) {
-      const int s0 = r*G, k = s0 + sub;
-      int g1 = 0, g2 = 0, num = 0, cnt = 0, bodies[4] = {0, 0, 0, 0};
-      double margin = 0;
-      mjh::RawContact raw[2];
-      mjh::ContactParam cp{};
-      if (active && k < nsurv) {            // narrowphase once: raw contacts kept in registers
-        const CoopPair P = prog[surv[k]];
-        cp = cparams[surv[k]];              // in flight while the narrowphase computes
-        g1 = P.g1;
-        g2 = P.g2;
-        margin = P.margin;
-        bodies[0] = P.b1;
-        bodies[1] = P.b2;
-        bodies[2] = P.rt1;
-        bodies[3] = P.rt2;
-        if (P.kmax < 0) {                   // the reference would run a function not built here
-          st |= MJHIP_INST_UNSUPPORTED;
-        } else if ((P.t1 == mjhipGEOM_PLANE &&
-                    (P.t2 == mjhipGEOM_BOX || P.t2 == mjhipGEOM_CYLINDER)) ||
-                   (P.t1 == mjhipGEOM_BOX && P.t2 == mjhipGEOM_BOX)) {
-          num = -1;                         // plane : box / cylinder, box : box: counts, then stores
-          mjh::collidePlaneBoxCyl<64, false, BOX, false>(m, d, g1, g2, margin, cnt, &st, bbuf);
-        } else {
-          num = mjh::narrowPrimitive(P.t1, P.t2, margin, (const double*)(gx + 3*g1),
-                                     (const double*)(gm + 9*g1), gsize + 3*g1,
-                                     (const double*)(gx + 3*g2), (const double*)(gm + 9*g2),
-                                     gsize + 3*g2, raw);
-          cnt = num;
-        }
-      }
-      int total;
-      const int excl = groupScan<G>(cnt, sub, &total) - cnt;
-      if (cnt) {
-        int c = ncon + excl;
-        if (num < 0) {
-          mjh::collidePlaneBoxCyl<64, true, BOX, false>(m, d, g1, g2, margin, c, &st, bbuf);
-        } else {
-          mjh::storeContacts<64>(m, d, g1, g2, margin, cp, raw, num, c, &st);
-        }
-        for (int q = ncon + excl; q < c && q < ncb; q++) {   // the contacts just stored
-          for (int e = 0; e < 4; e++) cbody[4*q + e] = bodies[e];
-        }
-      }
-      ncon += total;
-    }
-  }
-  if (active && sub == 0) d.con_count[0] = ncon < d.con_cap ? ncon : d.con_cap;
-  if (ncon > d.con_cap) ncon = d.con_cap;
-  __syncthreads();                          // contacts visible to every lane of the group
-  MJH_PHASE(15);
-
-  // ---- mj_makeConstraint: non-contact rows, then contact rows (all finished at creation)
-  mjh::RowCount rc;
-  if (active && !(dsbl & mjhipDSBL_CONSTRAINT)) {
-    if (m.neq) {
-      if (sub == 0) mjh::instantiateEquality<64, true>(m, d, rc, &st);
-      rc.nefc = __shfl(rc.nefc, 0, G);
-      rc.ne = __shfl(rc.ne, 0, G);
-    }
-    // a non-contact row r: the owner writes J (jval(k) for column k) and finishes it
-    auto addRow = [&](auto jval, double pos, double margin, double floss, int tp, int id)
-        MJH_LAMBDA_INLINE {
-      const int r = rc.nefc;
-      if (r + 1 > d.efc_cap) {
-        st |= MJHIP_INST_CNSTRFULL;
-        return false;
-      }
-      if (r % G == sub) {
-        mjh::SP<64> J = d.efc_J + (long)r*nv;
-        for (int k = 0; k < nv; k++) J[k] = jval(k);
-        rowFields(d, r, pos, margin, floss, tp, id);
-        // J*qvel, J*qacc from the row's generator and the LDS copies (the values stored in
-        // efc_J, in mju_dot's order), not read back from memory
-        const mjh::FnIdx<decltype(jval)> jv{jval};
-        mjh::finishNonContactVA(m, d, r, tp, id, pos, margin, floss,
-                                mjh::dot(jv, mjh::StridedIdx<8>{cdq + 6}, nv),
-                                mjh::dot(jv, mjh::StridedIdx<8>{cdq + 7}, nv));
-      }
-      rc.nefc++;
-      return true;
-    };
-    // rows of one G-wide round of dofs or joints, placed by a group prefix sum over each
-    // lane's row count in the reference's order; a row past the capacity is dropped and
-    // flagged, as addRow does
-    auto placeRound = [&](int nr, int& counter) MJH_LAMBDA_INLINE {
-      int total;
-      const int first = rc.nefc + groupScan<G>(nr, sub, &total) - nr;
-      const int end = rc.nefc + total < d.efc_cap ? rc.nefc + total : d.efc_cap;
-      if (rc.nefc + total > d.efc_cap) st |= MJHIP_INST_CNSTRFULL;
-      counter += end - rc.nefc;
-      rc.nefc = end;
-      return first;
-    };
-    auto putRow = [&](int r, auto jval, double pos, double margin, double floss, int tp, int id)
-        MJH_LAMBDA_INLINE {
-      if (r >= d.efc_cap) return;
-      mjh::SP<64> J = d.efc_J + (long)r*nv;
-      for (int k = 0; k < nv; k++) J[k] = jval(k);
-      rowFields(d, r, pos, margin, floss, tp, id);
-      const mjh::FnIdx<decltype(jval)> jv{jval};
-      mjh::finishNonContactVA(m, d, r, tp, id, pos, margin, floss,
-                              mjh::dot(jv, mjh::StridedIdx<8>{cdq + 6}, nv),
-                              mjh::dot(jv, mjh::StridedIdx<8>{cdq + 7}, nv));
-    };
-    if (!(dsbl & mjhipDSBL_FRICTIONLOSS)) {
-      // dof friction (:785-799), G dofs per round
-      for (int i0 = 0; i0 < nv; i0 += G) {
-        const int i = i0 + sub;
-        const double fl = i < nv ? m.dof_frictionloss[i] : 0.0;
-        const int first = placeRound(fl > 0 ? 1 : 0, rc.nf);
-        if (fl > 0) {
-          putRow(first, [&](int k) { return k == i ? 1.0 : 0.0; }, 0, 0, fl,
-                 mjh::CNSTR_FRICTION_DOF, i);
-        }
-      }
-      // tendon friction (:801-815) on the ten_J row; mj_addConstraint drops an empty row
-      for (int i = 0; i < m.ntendon; i++) {
-        const double fl = m.tendon_frictionloss[i];
-        if (!(fl > 0)) continue;
-        mjh::SP<64> tj = d.ten_J + (long)i*nv;
-        bool nonempty = false;
-        for (int k = 0; k < nv && !nonempty; k++) nonempty = tj[k] != 0;
-        if (nonempty && addRow([&](int k) { return tj[k]; }, 0, 0, fl,
-                               mjh::CNSTR_FRICTION_TENDON, i)) {
-          rc.nf++;
-        }
-      }
-    }
-    if (!(dsbl & mjhipDSBL_LIMIT)) {
-      // joint limits (:824-900), G joints per round: a slide/hinge joint gives up to two
-      // rows (lower side first), a ball joint one
-      for (int i0 = 0; i0 < m.njnt; i0 += G) {
-        const int i = i0 + sub;
-        int nr = 0, t = -1, da = 0;
-        bool on[2] = {false, false};
-        double dist[2] = {0, 0}, aa[3] = {0, 0, 0}, margin = 0;
-        if (i < m.njnt && m.jnt_limited[i]) {
-          margin = m.jnt_margin[i];
-          t = m.jnt_type[i];
-          da = m.jnt_dofadr[i];
-          if (t == mjhipJNT_SLIDE || t == mjhipJNT_HINGE) {
-            const double value = qp[m.jnt_qposadr[i]];
-            for (int k = 0; k < 2; k++) {
-              const int side = 2*k - 1;
-              dist[k] = side * (m.jnt_range[2*i+k] - value);
-              on[k] = dist[k] < margin;
-              nr += on[k];
-            }
-          } else if (t == mjhipJNT_BALL) {
-            const int adr = m.jnt_qposadr[i];
-            double quat[4] = {qp[adr], qp[adr+1], qp[adr+2], qp[adr+3]};
-            mjh::normalize4(quat);
-            mjh::quat2Vel(aa, quat, 1);
-            const double value = mjh::normalize3(aa);
-            dist[0] = mjh::dmax(m.jnt_range[2*i], m.jnt_range[2*i+1]) - value;
-            on[0] = dist[0] < margin && (aa[0] != 0 || aa[1] != 0 || aa[2] != 0);
-            nr = on[0];
-          }
-        }
-        int r = placeRound(nr, rc.nl);
-        if (t == mjhipJNT_SLIDE || t == mjhipJNT_HINGE) {
-          for (int k = 0; k < 2; k++) {
-            if (!on[k]) continue;
-            const double sg = -(double)(2*k - 1);
-            putRow(r++, [&](int c) { return c == da ? sg : 0.0; }, dist[k], margin, 0,
-                   mjh::CNSTR_LIMIT_JOINT, i);
-          }
-        } else if (t == mjhipJNT_BALL && on[0]) {
-          putRow(r, [&](int c) { return (c >= da && c < da + 3) ? aa[c-da]*-1 : 0.0; },
-                 dist[0], margin, 0, mjh::CNSTR_LIMIT_JOINT, i);
-        }
-      }
-      for (int i = 0; i < m.ntendon; i++) {
-        if (!m.tendon_limited[i]) continue;
-        const double value = d.ten_length[i], margin = m.tendon_margin[i];
-        mjh::SP<64> tj = d.ten_J + (long)i*nv;
-        int nonempty = -1;                  // ten_J row scanned only for an active side
-        for (int side = -1; side <= 1; side += 2) {
-          const double dist = side * (m.tendon_range[2*i+(side+1)/2] - value);
-          if (dist < margin && nonempty < 0) {
-            nonempty = 0;
-            for (int k = 0; k < nv && !nonempty; k++) nonempty = tj[k] != 0;
-          }
-          if (dist < margin && nonempty &&
-              addRow([&](int k) { return tj[k]*(double)(-side); }, dist, margin, 0,
-                     mjh::CNSTR_LIMIT_TENDON, i)) {
-            rc.nl++;
-          }
-        }
-      }
-    }
-    MJH_PHASE(18);
-    // contact rows (pyramidal or frictionless: the fused path excludes elliptic cones):
-    // kCoopContactLanes lanes per contact (contactRowsSplit), G / kCoopContactLanes contacts
-    // per round; a prefix sum over the contacts' row counts (held by each contact's first
-    // lane) gives each its first row; wide contacts (condim 4, 6) run on their first lane
-    if (CONTACT && !(dsbl & mjhipDSBL_CONTACT) && nv) {
-      // the contacts' first rows: a group prefix sum over their row counts, G per round; the
-      // first kCoopContacts contacts become tasks for the whole wave (below), the rest (rare)
-      // are formed here by the lane that placed them
-      int nef = rc.nefc;
-      for (int c0 = 0; c0 < ncon; c0 += G) {
-        const int c = c0 + sub;
-        int rows = 0, dim = 0;
-        if (c < ncon && !d.con_exclude[c]) {
-          dim = d.con_dim[c];
-          rows = dim == 1 ? 1 : 2*(dim - 1);
-        }
-        int total;
-        const int off = nef + groupScan<G>(rows, sub, &total) - rows;
-        bool fits = true;
-        if (rows && off + rows > d.efc_cap) {   // mjWARN_CNSTRFULL analogue (capacity is exact)
-          st |= MJHIP_INST_CNSTRFULL;
-          fits = false;
-        }
-        if (c < ncb && c < ncon) {
-          task[2*c] = off;
-          task[2*c+1] = fits ? dim : 0;     // 0: no rows
-        }
-        if (rows && fits) {
-          d.con_efc_address[c] = off;
-          if (c >= ncb) {
-            switch (dim) {
-              case 1: mjh::contactRowsFused<64, 1>(m, d, c, off); break;
-              case 3: mjh::contactRowsFused<64, 3>(m, d, c, off); break;
-              case 4: mjh::contactRowsFused<64, 4>(m, d, c, off); break;
-              default: mjh::contactRowsFused<64, 6>(m, d, c, off); break;
-            }
-          }
-        }
-        nef += total;
-      }
-      rc.nefc = nef < d.efc_cap ? nef : d.efc_cap;
-    }
-  }
-  if (sub == 0) {
-    s_inst[slot] = inst;
-    s_ntask[slot] = (CONTACT && active && !(dsbl & (mjhipDSBL_CONSTRAINT | mjhipDSBL_CONTACT)) &&
-                     nv) ? (ncon < ncb ? ncon : ncb) : 0;
-  }
-  __syncthreads();                          // the tasks and the staged data visible to all
-
-  // ---- contact rows, pooled over the wave: kCoopContactLanes lanes per contact
-  // (contactRowsSplit), 64 / kCoopContactLanes contacts per round whichever instance they
-  // belong to, so an instance with many contacts does not hold its wave for many rounds
-  if (CONTACT) {
-    constexpr int Q = kCoopContactLanes;
-    int ntot = 0;
-    for (int k = 0; k < IPB; k++) ntot += s_ntask[k];
-    const int cq = threadIdx.x % Q;
-    for (int t0 = 0; t0 < ntot; t0 += 64 / Q) {
-      int t = t0 + threadIdx.x / Q, sl = 0;
-      while (sl < IPB && t >= s_ntask[sl]) t -= s_ntask[sl++];
-      if (sl >= IPB) continue;              // past the wave's tasks (uniform per Q lanes)
-      const long ti = s_inst[sl];
-      Lane<64> dt = lane_view(mr, (int)(ti >> 6), (int)(ti & 63));
-      double* tb = lbase + (long)sl*per;
-      int* tcb = reinterpret_cast<int*>(tb + 8*nv + nq + 12*ngeom + (npair + 1) / 2);
-      int* ttask = tcb + 4*ncb;
-      dt.chain = chain;
-      dt.dchain = dchain;
-      dt.cdq = tb;
-      dt.cbody = tcb;
-      dt.ncbody = ncb;
-      dt.fst = tb + 8*nv + nq + 12*ngeom + (npair + 1) / 2 + 3*ncb;
-      dt.nfst = coopRows(dt.efc_cap);
-      const int off = ttask[2*t], dim = ttask[2*t+1];
-      switch (dim) {
-        case 0: break;
-        case 1: mjh::contactRowsSplit<64, 1, Q>(m, dt, t, off, cq); break;
-        case 3: mjh::contactRowsSplit<64, 3, Q>(m, dt, t, off, cq); break;
-        case 4: if (cq == 0) mjh::contactRowsFused<64, 4>(m, dt, t, off); break;
-        default: if (cq == 0) mjh::contactRowsFused<64, 6>(m, dt, t, off); break;
-      }
-    }
-  }
-  if (active && sub == 0) {
-    d.efc_count[0] = rc.nefc; d.efc_count[1] = rc.ne; d.efc_count[2] = rc.nf;
-    d.efc_count[3] = rc.nl;
-  }
-  __syncthreads();                          // rows and forces visible to every lane
-  MJH_PHASE(16);
-
-  // ---- qfrc_constraint = J'force (column-parallel, two columns per lane per pass, eight
-  // rows' loads in flight; forces from LDS) and the mj_inverse assembly
-  if (active) {
-    const int nefc = rc.nefc;
-    for (int j0 = sub; j0 < nv; j0 += 2*G) {
-      const int j1 = j0 + G;
-      const bool has1 = j1 < nv;
-      // the assembly's inputs, loaded ahead of the rows (a load issued after this lane's
-      // stores would wait for them)
-      const double rne0 = d.qfrc_inverse[j0], arm0 = m.dof_armature[j0];
-      const double pas0 = d.qfrc_passive[j0], qa0 = cdq[8*j0 + 7];
-      const double rne1 = has1 ? (double)d.qfrc_inverse[j1] : 0.0;
-      const double arm1 = has1 ? m.dof_armature[j1] : 0.0;
-      const double pas1 = has1 ? (double)d.qfrc_passive[j1] : 0.0;
-      const double qa1 = has1 ? cdq[8*j1 + 7] : 0.0;
-      double acc0 = 0, acc1 = 0;
-      for (int r0 = 0; r0 < nefc; r0 += 8) {
-        double f[8], x0[8], x1[8];
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          const int r = r0 + u;
-          f[u] = r < nefc ? (r < d.nfst ? fst[r] : d.efc_force[r]) : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {
-          mjh::SP<64> Jr = d.efc_J + (long)(r0 + u)*nv;
-          x0[u] = f[u] != 0 ? Jr[j0] : 0.0;
-          x1[u] = (f[u] != 0 && has1) ? Jr[j1] : 0.0;
-        }
-#pragma unroll
-        for (int u = 0; u < 8; u++) {   // mju_mulMatTVec's row order, zero forces skipped
-          if (f[u] != 0) {
-            acc0 += x0[u]*f[u];
-            acc1 += x1[u]*f[u];
-          }
-        }
-      }
-      const double out0 = rne0 + (arm0 * qa0 - pas0 - acc0);
-      d.qfrc_constraint[j0] = acc0;
-      d.qfrc_inverse[j0] = out0;
-      if (qfrc_out) qfrc_out[inst*nv + j0] = out0;
-      if (has1) {
-        const double out1 = rne1 + (arm1 * qa1 - pas1 - acc1);
-        d.qfrc_constraint[j1] = acc1;
-        d.qfrc_inverse[j1] = out1;
-        if (qfrc_out) qfrc_out[inst*nv + j1] = out1;
-      }
-    }
-    for (int o = G/2; o; o >>= 1) st |= __shfl_xor(st, o, G);
-    if (sub == 0 && status && st) status[inst] |= st;
-  }
-  MJH_PHASE(17);
-  __syncthreads();                          // the group's LDS is reused by the next round
-  }
-}
+// k_constraint, k_constraint_coop (kern_constraint.hip) and k_inverse (kern_inverse.hip):
+// kernels.h
 
 // fluid forces after the generated kernels (csrc/post_pass.h): one lane per instance
 __global__ __launch_bounds__(64) void k_fluid_after(mjhipModel m, Mirror mr, int B) {
@@ -689,39 +81,6 @@ __global__ __launch_bounds__(64) void k_check(mjhipModel m, Mirror mr, int B,
     if (!(d.qLD[m.C_rowadr[k] + m.C_rownnz[k] - 1] >= mjh::MINVAL)) st |= MJHIP_INST_INERTIA;
   }
   if (st) status[inst] |= st;
-}
-
-// Fused mj_inverseSkip over a batch. Optional row-major (instance-major) inputs are copied
-// into the mirror first; optional row-major qfrc_inverse output is written at the end.
-template <int SKIP, bool CONTACT, bool FUSED>
-__global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
-                                                const double* __restrict__ qpos_in,
-                                                const double* __restrict__ qvel_in,
-                                                const double* __restrict__ qacc_in,
-                                                double* __restrict__ qfrc_out,
-                                                int* __restrict__ status, int skipsensor) {
-  MJHIP_CHAIN_TABLE(FUSED)
-  const int blk = blockIdx.x, lane = threadIdx.x;
-  const long inst = (long)blk*64 + lane;
-  if (inst >= B) return;
-  Lane<64> d = lane_view(mr, blk, lane);
-  d.chain = chain;
-  MJHIP_GEOM_STAGE(CONTACT, FUSED)
-  if (qpos_in) {
-    for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos_in[inst*m.nq + k];
-  }
-  if (qvel_in) {
-    for (int k = 0; k < m.nv; k++) d.qvel[k] = qvel_in[inst*m.nv + k];
-  }
-  if (qacc_in) {
-    for (int k = 0; k < m.nv; k++) d.qacc[k] = qacc_in[inst*m.nv + k];
-  }
-  MJH_PHASE(0);
-  int st = mjh::inverseSkip<64, CONTACT, FUSED>(m, d, SKIP, skipsensor);
-  if (qfrc_out) {
-    for (int k = 0; k < m.nv; k++) qfrc_out[inst*m.nv + k] = d.qfrc_inverse[k];
-  }
-  if (status) status[inst] = st;
 }
 
 // slider-crank/site/body transmissions, sensors and energy after the generated kernels and
@@ -1023,6 +382,13 @@ struct mjhipContext_ {
   hipFunction_t rt_fn = nullptr;
   FastKernelEntry rt{};
   std::string rt_name;
+  hipDeviceptr_t rt_tbuf = nullptr;        // the code object's mjh_tbuf (null: none)
+  // per-stage timers (mjhip_contextTimers): the device accumulator the phase marks add to,
+  // the reference's mjTimerStat table, and the events around each timed call
+  unsigned long long* tbuf = nullptr;
+  mjhipTimerStat timer[mjhipNTIMER]{};
+  unsigned long long traw[MJH_TSLOTS]{};   // the raw mark sums (tools/exp_phases.py)
+  hipEvent_t tev0 = nullptr, tev1 = nullptr;
 };
 
 // The static geom-pair program of mj_collision (engine_collision_driver.c:265-497) for the
@@ -1209,13 +575,12 @@ extern "C" {
 MJHIP_API const char* mjhip_version(void) { return "mjhip 0.1 (gfx950)"; }
 
 #ifdef MJH_PHASE_TIMING
-// experiment builds only (tools/exp_phases.py): read and clear the phase-mark sums
-extern "C" int mjhip_phaseRead(unsigned long long* out) {
-  hipDeviceSynchronize();
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(mjh_phase_acc), 32*sizeof(unsigned long long)))
-    return 1;
-  static const unsigned long long zeros[32] = {};
-  return hipMemcpyToSymbol(HIP_SYMBOL(mjh_phase_acc), zeros, sizeof(zeros)) != hipSuccess;
+// experiment builds only (tools/exp_phases.py): the raw phase-mark sums of a timed context
+extern "C" int mjhip_phaseRead(mjhipContext* c, unsigned long long* out) {
+  if (!c) return 1;
+  memcpy(out, c->traw, sizeof(c->traw));
+  memset(c->traw, 0, sizeof(c->traw));
+  return 0;
 }
 #endif
 
@@ -1464,6 +829,9 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
+  if (c->tev0) hipEventDestroy(c->tev0);
+  if (c->tev1) hipEventDestroy(c->tev1);
+  hipFree(c->tbuf);
   hipFree(c->stage);
   hipFree(c->status);
   hipFree(c->worklist);
@@ -1505,6 +873,12 @@ MJHIP_API int mjhip_contextLoadKernel(mjhipContext* c, const void* image, size_t
   if (c->rt_module) hipModuleUnload(c->rt_module);
   c->rt_module = mod;
   c->rt_fn = fn;
+  size_t tbytes = 0;                       // its per-stage timer pointer (MJH_TBUF_EXTERN)
+  if (hipModuleGetGlobal(&c->rt_tbuf, &tbytes, mod, "mjh_tbuf") != hipSuccess ||
+      tbytes != sizeof(void*)) {
+    c->rt_tbuf = nullptr;
+    (void)hipGetLastError();
+  }
   c->rt_name = name;
   c->rt = FastKernelEntry{signature, nullptr, c->rt_name.c_str(), cmode};
   c->fast = &c->rt;
@@ -1676,6 +1050,99 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
   return MJHIP_OK;
 }
 
+//---------------------------------- per-stage timers ------------------------------------------
+
+// point every copy of mjh_tbuf (this unit's, the generated kernels' and the run-time code
+// object's) at p; blocking copies, after the stream's earlier work
+static int timers_attach(mjhipContext* c, unsigned long long* p) {
+  HIPCHECK(hipStreamSynchronize(c->stream));
+  HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(mjh_tbuf), &p, sizeof(p)));
+  if (mjhip_genSetTimerBuf(p) || mjhip_setTimerBufConstraint(p) ||
+      mjhip_setTimerBufInverse(p)) {
+    set_error("setting the kernel units' timer pointers failed");
+    return MJHIP_ERR_HIP;
+  }
+  if (c->rt_tbuf) HIPCHECK(hipMemcpyHtoD(c->rt_tbuf, &p, sizeof(p)));
+  return MJHIP_OK;
+}
+
+// fold one call's phase-mark sums (engine_device.h MJH_PHASE: slots and wave counts) into
+// the reference's timer slots: mean wave time per stage, 100 MHz ticks -> milliseconds
+static void timers_fold(mjhipContext* c, const unsigned long long* t, float call_ms) {
+  auto span = [&](int a, int b, int n) {
+    return t[n] ? (double)(long long)(t[b] - t[a]) / (double)t[n] / 1e5 : 0.0;
+  };
+  double kin = 0, inertia = 0, col = 0, make = 0, vel = 0, con = 0;
+  if (t[24]) {                             // generic k_inverse, marks 0-9
+    kin += span(0, 1, 24) + span(1, 2, 24) + span(5, 6, 24);
+    inertia += span(2, 3, 24);
+    col += span(3, 4, 24);
+    make += span(4, 5, 24);
+    vel += span(6, 7, 24);
+    con += span(7, 8, 24);
+  }
+  if (t[27]) {                             // straight-line k_all, marks 19-22
+    kin += span(19, 20, 27);
+    inertia += span(20, 21, 27);
+    vel += span(21, 22, 27);
+  }
+  if (t[25]) {                             // one-lane k_constraint, marks 10-13
+    col += span(10, 11, 25);
+    make += span(11, 12, 25);
+    con += span(12, 13, 25);
+  }
+  if (t[26]) {                             // k_constraint_coop, marks 14, 15, (18,) 16, 17
+    col += span(14, 15, 26);
+    make += t[18] ? span(15, 18, 26) + span(18, 16, 26) : span(15, 16, 26);
+    con += span(16, 17, 26);
+  }
+  auto add = [&](int slot, double ms) {
+    c->timer[slot].duration += ms;
+    c->timer[slot].number += 1;
+  };
+  add(mjhipTIMER_INVERSE, call_ms);
+  add(mjhipTIMER_POSITION, kin + inertia + col + make);
+  add(mjhipTIMER_POS_KINEMATICS, kin);
+  add(mjhipTIMER_POS_INERTIA, inertia);
+  add(mjhipTIMER_POS_COLLISION, col);
+  add(mjhipTIMER_POS_MAKE, make);
+  add(mjhipTIMER_VELOCITY, vel);
+  add(mjhipTIMER_CONSTRAINT, con);
+}
+
+MJHIP_API int mjhip_contextTimers(mjhipContext* c, int enable) {
+  if (!c) {
+    set_error("mjhip_contextTimers: null context");
+    return MJHIP_ERR_ARG;
+  }
+  HIPCHECK(hipSetDevice(c->device));
+  if (!enable) {
+    if (c->tbuf) {
+      HIPCHECK(hipStreamSynchronize(c->stream));
+      HIPCHECK(hipFree(c->tbuf));
+      c->tbuf = nullptr;
+    }
+    return MJHIP_OK;
+  }
+  if (!c->tbuf) {
+    HIPCHECK(hipMalloc((void**)&c->tbuf, MJH_TSLOTS * sizeof(unsigned long long)));
+    HIPCHECK(hipMemset(c->tbuf, 0, MJH_TSLOTS * sizeof(unsigned long long)));
+  }
+  if (!c->tev0) HIPCHECK(hipEventCreate(&c->tev0));
+  if (!c->tev1) HIPCHECK(hipEventCreate(&c->tev1));
+  return MJHIP_OK;
+}
+
+MJHIP_API int mjhip_timerRead(mjhipContext* c, mjhipTimerStat* out, int reset) {
+  if (!c || !out) {
+    set_error("mjhip_timerRead: bad argument");
+    return MJHIP_ERR_ARG;
+  }
+  memcpy(out, c->timer, sizeof(c->timer));
+  if (reset) memset(c->timer, 0, sizeof(c->timer));
+  return MJHIP_OK;
+}
+
 MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B, const mjtNum* qpos,
                                  const mjtNum* qvel, const mjtNum* qacc, mjtNum* qfrc_inverse,
                                  int skipstage, int skipsensor, int flags, int* status) {
@@ -1719,8 +1186,27 @@ MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B, const mjtNum* qpos,
   // per-instance statuses only when the caller can see them (status array, or the host path's
   // return code): a device-pointer call without them skips the input checks entirely
   const bool want_status = status || !dev;
+  const bool timed = c->tbuf != nullptr;
+  if (timed) {
+    int trc = timers_attach(c, c->tbuf);
+    if (trc) return trc;
+    HIPCHECK(hipEventRecord(c->tev0, c->stream));
+  }
   int rc = launch_inverse(c, B, dq, dv, da, dqfrc, skipstage, want_status ? c->status : nullptr,
                           flags, skipsensor);
+  if (timed) {
+    HIPCHECK(hipEventRecord(c->tev1, c->stream));
+    const int arc = timers_attach(c, nullptr);   // synchronizes the stream first
+    if (rc) return rc;
+    if (arc) return arc;
+    unsigned long long t[MJH_TSLOTS];
+    float call_ms = 0;
+    HIPCHECK(hipMemcpy(t, c->tbuf, sizeof(t), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemset(c->tbuf, 0, sizeof(t)));
+    HIPCHECK(hipEventElapsedTime(&call_ms, c->tev0, c->tev1));
+    for (int k = 0; k < MJH_TSLOTS; k++) c->traw[k] += t[k];
+    timers_fold(c, t, call_ms);
+  }
   if (rc) return rc;
   if (qfrc_inverse && !dev) {
     HIPCHECK(hipMemcpyAsync(qfrc_inverse, sf, sizeof(double)*(size_t)B*m.nv,

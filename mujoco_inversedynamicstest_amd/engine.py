@@ -77,6 +77,8 @@ SIGNATURES = {
     "mjhip_timeInverseKernel": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_float)]),
+    "mjhip_contextTimers": (ctypes.c_int, [_V, ctypes.c_int]),
+    "mjhip_timerRead": (ctypes.c_int, [_V, _V, ctypes.c_int]),
     "mjhip_setDevice": (None, [ctypes.c_int]),
     "mjhip_inverse": (None, [_V, _V]),
     "mjhip_inverseSkip": (None, [_V, _V, ctypes.c_int, ctypes.c_int]),
@@ -94,6 +96,17 @@ SIGNATURES = {
 
 class MJHIPError(RuntimeError):
   pass
+
+
+# the reference's mjtTimer slots (include/mujoco/mjdata.h), mjhipTimer in include/mjhip.h
+TIMERS = ("STEP", "FORWARD", "INVERSE", "POSITION", "VELOCITY", "ACTUATION", "CONSTRAINT",
+          "ADVANCE", "POS_KINEMATICS", "POS_INERTIA", "POS_COLLISION", "POS_MAKE",
+          "POS_PROJECT", "COL_BROAD", "COL_NARROW")
+
+
+class TimerStat(ctypes.Structure):
+  """mjhipTimerStat (= the reference's mjTimerStat)."""
+  _fields_ = [("duration", ctypes.c_double), ("number", ctypes.c_int)]
 
 
 _lib = None
@@ -342,6 +355,16 @@ class InverseEngine:
     self.set_field("qpos", qpos, first)
     self.set_field("qvel", qvel, first)
     self.set_field("qacc", qacc, first)
+
+  def timers(self, enable=True):
+    """Per-stage timers on or off (mjhip_contextTimers): timed inverse calls synchronize."""
+    _check(lib().mjhip_contextTimers(self.ctx, int(bool(enable))), "mjhip_contextTimers")
+
+  def timer_read(self, reset=False):
+    """{mjTIMER name: (milliseconds, calls)} accumulated since the last reset."""
+    out = (TimerStat * len(TIMERS))()
+    _check(lib().mjhip_timerRead(self.ctx, out, int(bool(reset))), "mjhip_timerRead")
+    return {n: (out[i].duration, out[i].number) for i, n in enumerate(TIMERS)}
 
   def time_kernel(self, B, reps=20, skipstage=mjSTAGE_NONE, generic=False):
     """Average ms per launch of the mj_inverse kernels on mirror-resident inputs (HIP

@@ -63,7 +63,9 @@ def source(m) -> tuple[str, str]:
   """(kernel name, complete HIP source) of the straight-line kernel for model m."""
   name = f"rt_{codegen.model_hash(m)}"
   body = codegen.generate(m, name, extern_c=True)
-  src = ('#include <hip/hip_runtime.h>\n'
+  # MJH_TBUF_EXTERN: the per-stage timer pointer gets C linkage, so the library finds it in
+  # the code object by name (mjhip_contextLoadKernel) and points it at the context's timers
+  src = ('#include <hip/hip_runtime.h>\n#define MJH_TBUF_EXTERN 1\n'
          f'#include "{os.path.join(CSRC, "engine_device.h")}"\n' + body)
   return name, src
 

@@ -109,3 +109,27 @@ def test_reference_model_contacts_on_device():
     assert (dframe.max(axis=1) <= tol).all()
     hf += int(np.sum(m.geom_type[geom[i, :2*n:2]] == HFIELD))
   assert hf >= B                    # height-field contacts on every state
+
+
+@pytest.mark.parametrize("integ", [0, 2, 3])
+def test_reference_model_invdiscrete(integ):
+  """mjENBL_INVDISCRETE on the reference model for Euler, implicit and implicitfast (the
+  fluid models' velocity derivatives in qDeriv): device vs oracle, same bounds as above."""
+  m = R.model()
+  m.opt["integrator"] = integ
+  m.opt["enableflags"] |= 1 << 3
+  q, v, a = R.states(m, 48, seed=12)
+  B = len(q)
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    f, st = e.inverse(q, v, a, status=True)
+  finally:
+    e.close()
+  ref, rst, _, _, ccd = _oracle_run(m, q, v, a)
+  np.testing.assert_array_equal(st, rst)
+  assert (st == 0).all()
+  scale = np.maximum(1.0, np.abs(ref).max(axis=1))
+  err = np.abs(f - ref).max(axis=1) / scale
+  print(f"integrator {integ}: median {np.median(err):.2e}, max {err.max():.2e}")
+  assert err[~ccd].max(initial=0) <= 1e-10
+  assert err[ccd].max(initial=0) <= 1e-6

@@ -3,9 +3,10 @@
   python tools/exp_phases.py            # build tools/exp/libmjhip_phase.so (no GPU needed)
   python tools/exp_phases.py run [B]    # GPU box: config-4 humanoid (contacts on)
 
-Builds libmjhip with -DMJH_PHASE_TIMING: lane 0 of every wave of k_inverse<0, CONTACT> adds
-the wall clock (100 MHz) at the MJH_PHASE marks of engine_device.h. The mean over waves of
-mark k minus mark k-1 is the mean wall time a wave spends in phase k.
+Builds libmjhip with -DMJH_PHASE_TIMING (which adds per-contact spans to the product's
+per-stage timer marks) and reads the raw mark sums of a timed context (mjhip_contextTimers):
+lane 0 of every wave adds the wall clock (100 MHz) at the MJH_PHASE marks of engine_device.h.
+The mean over waves of mark k minus mark k-1 is the mean wall time a wave spends in phase k.
 """
 import ctypes
 import os
@@ -37,23 +38,12 @@ GROUPS = [
 def build():
   import __graft_entry__ as ge
   ge.generate_fast_kernels()
-  os.makedirs(EXP, exist_ok=True)
-  # the two translation units of libmjhip (the generated kernels need no phase marks; their
-  # object is kept between builds), then one shared library
-  hipcc = "/opt/rocm/bin/hipcc"
-  gen_o = os.path.join(EXP, "gen_fast.o")
-  main_o = os.path.join(EXP, f"mjhip_phase{CQ}.o")
+  # every unit with the spans compiled in (the generated kernels' object is kept between
+  # builds: they carry the product's stage marks only)
   cq = [f"-DMJHIP_COOP_CQ={CQ}"] if CQ else []
-  procs = [subprocess.Popen([hipcc, *ge.HIPCC_FLAGS, "-DMJH_PHASE_TIMING", *cq, "-c", "-o",
-                             main_o, os.path.join(ge.CSRC, "mjhip.hip")])]
-  if not ge._newer(gen_o, [os.path.join(ge.CSRC, "gen_fast.inc")]):
-    procs.append(subprocess.Popen([hipcc, *ge.HIPCC_FLAGS, "-c", "-o", gen_o,
-                                   os.path.join(ge.CSRC, "gen_fast.hip")]))
-  if any(p.wait() for p in procs):
-    raise RuntimeError("hipcc failed")
   os.makedirs(os.path.dirname(LIB), exist_ok=True)
-  subprocess.run([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", LIB, main_o, gen_o],
-                 check=True)
+  ge.compile_library(LIB, os.path.join(EXP, f"obj{CQ}"), ["-DMJH_PHASE_TIMING", *cq],
+                     reuse=("gen_fast.hip",))
 
 
 def run(B=4096, reps=5):
@@ -63,27 +53,28 @@ def run(B=4096, reps=5):
   from mujoco_inversedynamicstest_amd.sampler import sample_contact_states
   engine.LIB_PATH = LIB
   L = engine.lib()
-  L.mjhip_phaseRead.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+  L.mjhip_phaseRead.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_ulonglong)]
   torch.cuda.set_device(0)
   m = models.load("humanoid", disable_contact=False)
   q, v, a = sample_contact_states(m, B)
   eng = engine.InverseEngine(m, capacity=B)
   eng.upload_states(q, v, a)
+  eng.timers(True)
   G = 16 if os.environ.get("MJHIP_COOP_LANES", "16") != "0" else 64
-  acc = (ctypes.c_ulonglong * 32)()
+  acc = (ctypes.c_ulonglong * 48)()
   for generic in (False, True):
     eng.inverse(B, mirror_input=True, generic=generic)
     torch.cuda.synchronize()
-    L.mjhip_phaseRead(acc)
+    L.mjhip_phaseRead(eng.ctx, acc)
     waves = (B + 63) // 64
-    sums = np.zeros(32)
+    sums = np.zeros(48)
     for _ in range(reps):
       t0 = time.perf_counter()
       eng.inverse(B, mirror_input=True, generic=generic)
       torch.cuda.synchronize()
       wall = time.perf_counter() - t0
-      assert L.mjhip_phaseRead(acc) == 0
-      sums += np.array(acc[:32], dtype=np.float64)
+      assert L.mjhip_phaseRead(eng.ctx, acc) == 0
+      sums += np.array(acc[:48], dtype=np.float64)
     print(f"batch {B}, {waves} waves, {'generic' if generic else 'default'} dispatch "
           f"(last call {wall*1e3:.2f} ms wall); mean per-wave phase time (us):")
     for title, marks, names in GROUPS:
@@ -98,8 +89,8 @@ def run(B=4096, reps=5):
         print(f"  {name:28s} {x:9.1f}")
       print(f"  {'total':28s} {d.sum():9.1f}", flush=True)
     # spans inside one contact's rows (lane 0 of each wave): slot k sums, k + 1 counts
-    spans = [("contact data+impedance", 20), ("contact dof loop", 22), ("contact finish", 24)]
-    if sums[21] > 0:
+    spans = [("contact data+impedance", 40), ("contact dof loop", 42), ("contact finish", 44)]
+    if sums[41] > 0:
       print(" per contact (lane 0's contacts, mean us)")
       for name, k in spans:
         print(f"  {name:28s} {sums[k] / sums[k + 1] / 100.0:9.2f}  ({int(sums[k + 1] / reps)} "

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 GPU steps, chosen by name: tests (a pytest -k filter in PYTEST_K), bench, c4, c5
-# (config 5 under a rocprofv3 kernel trace), prof (rocprof stats of the bench + PMC passes).
+# (config 5 under a rocprofv3 kernel trace), prof (rocprof stats of the bench + PMC passes),
+# variants (tools/exp_variants.py run).
 #   bash tools/gpu_r04.sh tests bench c5
 set -u
 cd "${GRAFT_REPO_ROOT:-$(pwd)}"
@@ -31,6 +32,9 @@ for step in "$@"; do
       tail -1 gpurun_out/c5plain.json ;;
     prof)
       bash tools/gpu_profile.sh || exit 1 ;;
+    variants)
+      timeout -k 10 300 python tools/exp_variants.py run > gpurun_out/variants.log 2>&1 || { tail -20 gpurun_out/variants.log; exit 1; }
+      cat gpurun_out/variants.log ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
