@@ -32,6 +32,9 @@ for step in "$@"; do
       tail -1 gpurun_out/c5plain.json ;;
     prof)
       bash tools/gpu_profile.sh || exit 1 ;;
+    store)
+      timeout -k 10 120 tools/exp_lib/exp_store > gpurun_out/store.log 2>&1 || { cat gpurun_out/store.log; exit 1; }
+      cat gpurun_out/store.log ;;
     variants)
       timeout -k 10 300 python tools/exp_variants.py run > gpurun_out/variants.log 2>&1 || { tail -20 gpurun_out/variants.log; exit 1; }
       cat gpurun_out/variants.log ;;
