@@ -44,6 +44,12 @@ static const char* adapter_unsupported(const mjModel* m) {
   if (m->npair) return "explicit contact pairs (<contact><pair>)";
   if (m->nflex) return "flexes";
   if (m->nplugin) return "plugins";
+  /* mj_isSparse (engine_core_constraint.c:96-103): the arena would hold compressed efc_J
+   * rows over the dof chains, which this adapter does not lay out (the library computes
+   * such models; its batched and single-instance APIs return dense rows) */
+  if (m->opt.jacobian == mjJAC_SPARSE || (m->opt.jacobian == mjJAC_AUTO && m->nv >= 60)) {
+    return "sparse Jacobians (the compressed efc_J arena layout)";
+  }
   for (int i = 0; i < m->nu; i++) {
     /* mjd_actuator_vel reads mjData.act for these (engine_derivative.c:855-863) */
     if (m->actuator_dyntype[i] != mjDYN_NONE && m->actuator_gaintype[i] == mjGAIN_AFFINE &&

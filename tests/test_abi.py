@@ -68,11 +68,12 @@ def test_no_cpu_fallback_without_device(humanoid):
 
 @pytest.mark.gpu
 def test_unsupported_model_rejected():
-  """A model outside the device subset (here: sparse constraint Jacobians, jacobian=sparse)
-  is rejected at context creation with MJHIP_ERR_MODEL, never run approximately (the
-  rejection happens after the device check, so this needs the GPU)."""
+  """A model outside the device subset (here: mjENBL_INVDISCRETE with RK4, an mjERROR in
+  the reference) is rejected at context creation with MJHIP_ERR_MODEL, never run
+  approximately (the rejection happens after the device check, so this needs the GPU)."""
   m = models.load("humanoid")
-  m.opt["jacobian"] = 1
+  m.opt["enableflags"] |= 1 << 3
+  m.opt["integrator"] = 1
   with pytest.raises(engine.MJHIPError, match="MODEL"):
     engine.InverseEngine(m, capacity=64)
 
