@@ -340,6 +340,12 @@ struct Lane {
   // contacts i < ncbody
   const int* cbody;
   int ncbody;
+  // the native solver's scratch (the ccd / ccdi fields) seen per lane: the lane's contiguous
+  // slice of the field's block storage, so a polytope vertex (9 doubles) or face (4 doubles,
+  // 7 ints) is one or two cache lines of its own rather than one line per component shared
+  // with lanes that are elsewhere in their iterations
+  double* ccdx;
+  int* ccdxi;
 };
 
 // chain[k] for body k (the fused path's ancestor test, one bit per body)
@@ -2902,7 +2908,7 @@ template <int S>
 MJH_HD int colConvex(RawContact& c, const mjhipModel& m, const Lane<S>& d, int g1, int g2,
                      double margin, int* status) {
   const int N = m.opt.ccd_iterations;
-  CcdMem<S> M{d.ccd, d.ccdi, 5 + N, mjh_ccdFaceCap(&m)};
+  CcdMem<1> M{{d.ccdx}, {d.ccdxi}, 5 + N, mjh_ccdFaceCap(&m)};
   CcdShape A, B;
   ccdShape(A, m, d, g1, margin);
   ccdShape(B, m, d, g2, margin);
@@ -3333,7 +3339,7 @@ MJH_HD void colConvexHField(const mjhipModel& m, const Lane<S>& d, int g1, int g
   A.pzb = -size1[3];
   const double dx = (2.0*size1[0]) / (ncol - 1), dy = (2.0*size1[1]) / (nrow - 1);
   const int N = m.opt.ccd_iterations;
-  CcdMem<S> M{d.ccd, d.ccdi, 5 + N, mjh_ccdFaceCap(&m)};
+  CcdMem<1> M{{d.ccdx}, {d.ccdxi}, 5 + N, mjh_ccdFaceCap(&m)};
   int cnt = 0;
   for (int r = rmin; r < rmax; r++) {
     int nvert = 0;
@@ -3674,7 +3680,7 @@ MJH_HD double geomDistance(const mjhipModel& m, const Lane<S>& d, int geom1, int
   }
   if (ccd) {
     const int N = m.opt.ccd_iterations;
-    CcdMem<S> M{d.ccd, d.ccdi, 5 + N, mjh_ccdFaceCap(&m)};
+    CcdMem<1> M{{d.ccdx}, {d.ccdxi}, 5 + N, mjh_ccdFaceCap(&m)};
     CcdShape A, B;
     ccdShape(A, m, d, g1, 0.0);
     ccdShape(B, m, d, g2, 0.0);
@@ -7980,6 +7986,8 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
   d.cbody = nullptr;
   d.ncbody = 0;
   d.dchain = nullptr;
+  d.ccdx = mr.ccd + ((long)blk*mr.ccd_n)*64 + (long)lane*mr.ccd_n;
+  d.ccdxi = mr.ccdi + ((long)blk*mr.ccdi_n)*64 + (long)lane*mr.ccdi_n;
   return d;
 }
 

@@ -104,5 +104,7 @@ static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int
   L.cbody = nullptr;
   L.ncbody = 0;
   L.dchain = nullptr;
+  L.ccdx = L.ccd.p;
+  L.ccdxi = L.ccdi.p;
   return L;
 }

@@ -35,6 +35,10 @@ def main():
   dt = (time.perf_counter() - t0) / reps
   print(f"{name}: batch {B}, kernel {e.fast_kernel or 'generic'}, {dt*1e3:.3f} ms per call, "
         f"{B/dt/1e6:.1f}M evals/s")
+  e.timers(True)                   # one timed call: the per-stage table (mjhip_timerRead)
+  e.inverse(B, mirror_input=True)
+  t = e.timer_read()
+  print("  timers (ms): " + ", ".join(f"{k} {x:.4f}" for k, (x, n) in t.items() if n))
   e.close()
 
 

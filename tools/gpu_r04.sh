@@ -32,6 +32,12 @@ for step in "$@"; do
       tail -1 gpurun_out/c5plain.json ;;
     prof)
       bash tools/gpu_profile.sh || exit 1 ;;
+    sc)
+      timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_sc -o sc \
+        --output-format csv -- python tools/bench_model.py slider_crank 65536 20 \
+        > gpurun_out/sc.log 2>&1 || { tail -20 gpurun_out/sc.log; exit 1; }
+      grep -v "^W\|^\[" gpurun_out/sc.log | tail -3
+      find gpurun_out/prof_sc -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-150 ;;
     store)
       timeout -k 10 120 tools/exp_lib/exp_store > gpurun_out/store.log 2>&1 || { cat gpurun_out/store.log; exit 1; }
       cat gpurun_out/store.log ;;
