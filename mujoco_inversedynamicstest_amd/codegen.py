@@ -82,9 +82,11 @@ ALL_WAVES = 1
 # the later stages re-read (qM, cinert, cdof) from L2; -DMJHIP_NO_NT compiles them as plain
 # stores (the A/B build)
 NT_STORES = True
-# experiment knob (tools/exp_variants.py): None = keep every re-read field temporal; else the
-# set of fields whose stores stay temporal (all others stream, re-read or not)
+# experiment knobs (tools/exp_variants.py): NT_TEMPORAL None = keep every re-read field
+# temporal, else the set of fields whose stores stay temporal (all others stream, re-read or
+# not); NT_STAGES: the stages whose stores may stream
 NT_TEMPORAL = None
+NT_STAGES = ("pos", "fac", "va")
 
 
 def _ll(st):
@@ -1341,7 +1343,8 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
       if not mt or mt.group(2) in reread:
         return line
       return f"{mt.group(1)}MJH_NT_STORE(P_{mt.group(2)}[{mt.group(3)}*64], {mt.group(4)});"
-    bodies = {st: "\n".join(nt(x) for x in b.split("\n")) for st, b in bodies.items()}
+    bodies = {st: ("\n".join(nt(x) for x in b.split("\n")) if st in NT_STAGES else b)
+              for st, b in bodies.items()}
   out = [f"// GENERATED by mujoco_inversedynamicstest_amd/codegen.py -- do not edit.",
          f"// model '{name}' (nq={m.nq} nv={m.nv} nbody={m.nbody}), hash {model_hash(m)}"]
   exact = exact_fp(m)

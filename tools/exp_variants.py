@@ -22,8 +22,11 @@ OUT = os.path.join(ROOT, "tools", "exp_lib", "variants")
 VARIANTS = {
     "control": {},
     "qM_only_temporal": {"NT_TEMPORAL": {"qM"}},
-    "all_streaming": {"NT_TEMPORAL": set()},
-    "no_streaming": {"NT_STORES": False},
+    "qM_pos_nt_only": {"NT_TEMPORAL": {"qM"}, "NT_STAGES": ("pos",)},
+    "qM_pos_fac_nt": {"NT_TEMPORAL": {"qM"}, "NT_STAGES": ("pos", "fac")},
+    "qM_small": {"NT_TEMPORAL": {"qM", "qfrc_passive", "ten_length"}},
+    "qM_cdof": {"NT_TEMPORAL": {"qM", "cdof"}},
+    "qM_cinert": {"NT_TEMPORAL": {"qM", "cinert"}},
 }
 
 
