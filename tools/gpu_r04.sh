@@ -44,6 +44,9 @@ for step in "$@"; do
     store)
       timeout -k 10 120 tools/exp_lib/exp_store > gpurun_out/store.log 2>&1 || { cat gpurun_out/store.log; exit 1; }
       cat gpurun_out/store.log ;;
+    lanes)
+      timeout -k 10 600 python tools/exp_lanes.py run > gpurun_out/lanes.log 2>&1 || { tail -30 gpurun_out/lanes.log; exit 1; }
+      cat gpurun_out/lanes.log ;;
     variants)
       timeout -k 10 300 python tools/exp_variants.py run > gpurun_out/variants.log 2>&1 || { tail -20 gpurun_out/variants.log; exit 1; }
       cat gpurun_out/variants.log ;;
