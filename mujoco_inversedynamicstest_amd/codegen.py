@@ -77,14 +77,17 @@ LANES = {"pos": 64, "fac": 64, "va": 64}
 # two waves share a SIMD)
 ALL_LANES = 64
 ALL_WAVES = 1
-# stores of mirror fields no later stage of the kernel re-reads go out as streaming
-# (non-temporal) stores, MJH_NT_STORE in engine_device.h, so they do not displace the lines
-# the later stages re-read (qM, cinert, cdof) from L2; -DMJHIP_NO_NT compiles them as plain
-# stores (the A/B build)
+# stores of mirror fields go out as streaming (non-temporal) stores, MJH_NT_STORE in
+# engine_device.h, except those the fac stage re-reads right after the pos stage stored them
+# (qM): those stay in L2 for it. The va stage's re-reads (cinert, cdof) come long after their
+# stores, by which time 32 waves per XCD have written far more than its 4 MB L2 holds, so
+# keeping them temporal only displaced qM (round 4 A/B, tools/exp_variants.py: 347.6 us with
+# every re-read field temporal, 317.4 us with qM alone, 338.4 us with none; bit-identical
+# outputs). -DMJHIP_NO_NT compiles them as plain stores (the A/B build)
 NT_STORES = True
-# experiment knobs (tools/exp_variants.py): NT_TEMPORAL None = keep every re-read field
-# temporal, else the set of fields whose stores stay temporal (all others stream, re-read or
-# not); NT_STAGES: the stages whose stores may stream
+# experiment knobs (tools/exp_variants.py): NT_TEMPORAL None = the rule above, else the set
+# of fields whose stores stay temporal (all others stream); NT_STAGES: the stages whose
+# stores may stream
 NT_TEMPORAL = None
 NT_STAGES = ("pos", "fac", "va")
 
@@ -1333,7 +1336,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   bodies = {st: _GEN[st](M, store_fields) for st in STAGES}
   if NT_STORES:
     import re
-    reread = set(re.findall(r"= P_(\w+)\[", "\n".join(bodies.values())))
+    reread = set(re.findall(r"= P_(\w+)\[", bodies["fac"]))
     if NT_TEMPORAL is not None:
       reread = set(NT_TEMPORAL)
     store = re.compile(r"^(\s*)P_(\w+)\[(\d+)\*64\] = (.+);$")

@@ -21,6 +21,8 @@ OUT = os.path.join(ROOT, "tools", "exp_lib", "variants")
 # name -> codegen attribute overrides
 VARIANTS = {
     "control": {},
+    "every_reread_temporal": {"NT_TEMPORAL": {"qM", "cdof", "cinert", "qacc", "qfrc_passive",
+                                              "qpos", "qvel", "ten_length"}},
     "qM_only_temporal": {"NT_TEMPORAL": {"qM"}},
     "qM_pos_nt_only": {"NT_TEMPORAL": {"qM"}, "NT_STAGES": ("pos",)},
     "qM_pos_fac_nt": {"NT_TEMPORAL": {"qM"}, "NT_STAGES": ("pos", "fac")},
