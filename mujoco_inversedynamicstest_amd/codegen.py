@@ -90,6 +90,9 @@ NT_STORES = True
 # stores may stream
 NT_TEMPORAL = None
 NT_STAGES = ("pos", "fac", "va")
+# experiment knob: stages whose re-reads of the mirror load as streaming (non-temporal)
+# loads (MJH_NT_LOAD), so they do not displace the lines a later stage re-reads
+NT_LOAD_STAGES = ()
 
 
 def _ll(st):
@@ -1348,6 +1351,9 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
       return f"{mt.group(1)}MJH_NT_STORE(P_{mt.group(2)}[{mt.group(3)}*64], {mt.group(4)});"
     bodies = {st: ("\n".join(nt(x) for x in b.split("\n")) if st in NT_STAGES else b)
               for st, b in bodies.items()}
+    load = re.compile(r"= P_(\w+)\[(\d+)\*64\];")
+    bodies = {st: (load.sub(lambda mt: f"= MJH_NT_LOAD(P_{mt.group(1)}[{mt.group(2)}*64]);", b)
+                   if st in NT_LOAD_STAGES else b) for st, b in bodies.items()}
   out = [f"// GENERATED by mujoco_inversedynamicstest_amd/codegen.py -- do not edit.",
          f"// model '{name}' (nq={m.nq} nv={m.nv} nbody={m.nbody}), hash {model_hash(m)}"]
   exact = exact_fp(m)

@@ -87,8 +87,10 @@ static __device__ unsigned long long* mjh_tbuf = nullptr;
 // generated kernels, codegen.NT_STORES); a plain store in host builds and with -DMJHIP_NO_NT
 #if defined(__HIP_DEVICE_COMPILE__) && !defined(MJHIP_NO_NT)
 #define MJH_NT_STORE(lv, v) __builtin_nontemporal_store((double)(v), &(lv))
+#define MJH_NT_LOAD(lv) __builtin_nontemporal_load(&(lv))
 #else
 #define MJH_NT_STORE(lv, v) ((lv) = (v))
+#define MJH_NT_LOAD(lv) (lv)
 #endif
 
 // mjtSensor values (include/mujoco/mjmodel.h)

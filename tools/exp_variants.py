@@ -24,11 +24,9 @@ VARIANTS = {
     "every_reread_temporal": {"NT_TEMPORAL": {"qM", "cdof", "cinert", "qacc", "qfrc_passive",
                                               "qpos", "qvel", "ten_length"}},
     "qM_only_temporal": {"NT_TEMPORAL": {"qM"}},
-    "qM_pos_nt_only": {"NT_TEMPORAL": {"qM"}, "NT_STAGES": ("pos",)},
-    "qM_pos_fac_nt": {"NT_TEMPORAL": {"qM"}, "NT_STAGES": ("pos", "fac")},
-    "qM_small": {"NT_TEMPORAL": {"qM", "qfrc_passive", "ten_length"}},
-    "qM_cdof": {"NT_TEMPORAL": {"qM", "cdof"}},
-    "qM_cinert": {"NT_TEMPORAL": {"qM", "cinert"}},
+    "va_nt_loads": {"NT_LOAD_STAGES": ("va",)},
+    "pos_va_nt_loads": {"NT_LOAD_STAGES": ("pos", "va")},
+    "fac_va_nt_loads": {"NT_LOAD_STAGES": ("fac", "va")},
 }
 
 
