@@ -23,10 +23,7 @@ VARIANTS = {
     "control": {},
     "every_reread_temporal": {"NT_TEMPORAL": {"qM", "cdof", "cinert", "qacc", "qfrc_passive",
                                               "qpos", "qvel", "ten_length"}},
-    "qM_only_temporal": {"NT_TEMPORAL": {"qM"}},
     "va_nt_loads": {"NT_LOAD_STAGES": ("va",)},
-    "pos_va_nt_loads": {"NT_LOAD_STAGES": ("pos", "va")},
-    "fac_va_nt_loads": {"NT_LOAD_STAGES": ("fac", "va")},
 }
 
 
@@ -98,6 +95,8 @@ def run(B=65536, reps=50, rounds=3):
 
 if __name__ == "__main__":
   if len(sys.argv) > 1 and sys.argv[1] == "run":
-    run()
+    for b in os.environ.get("VARIANT_B", "65536").split(","):
+      print(f"== batch {b}", flush=True)
+      run(B=int(b))
   else:
     build()
