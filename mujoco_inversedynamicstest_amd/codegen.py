@@ -90,6 +90,10 @@ NT_STORES = True
 # stores may stream
 NT_TEMPORAL = None
 NT_STAGES = ("pos", "fac", "va")
+# batches from which k_all also streams the stores the va stage re-reads (SV = true): below
+# it, L2 is not oversubscribed and keeping them pays (mjd_inverseFD's position-stage launch,
+# whose centres' fields k_vaskip re-reads)
+NT_SV_MIN_B = 49152
 # experiment knob: stages whose re-reads of the mirror load as streaming (non-temporal)
 # loads (MJH_NT_LOAD), so they do not displace the lines a later stage re-reads
 NT_LOAD_STAGES = ()
@@ -1339,15 +1343,21 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   bodies = {st: _GEN[st](M, store_fields) for st in STAGES}
   if NT_STORES:
     import re
+    # the fac stage's re-reads stay temporal; the other stages' re-reads stream only in the
+    # SV = true instantiation of k_all (a batch large enough to oversubscribe L2, NT_SV_MIN_B)
     reread = set(re.findall(r"= P_(\w+)\[", bodies["fac"]))
+    later = set(re.findall(r"= P_(\w+)\[", "\n".join(bodies.values()))) - reread
     if NT_TEMPORAL is not None:
-      reread = set(NT_TEMPORAL)
+      reread, later = set(NT_TEMPORAL), set()
     store = re.compile(r"^(\s*)P_(\w+)\[(\d+)\*64\] = (.+);$")
 
     def nt(line):
       mt = store.match(line)
       if not mt or mt.group(2) in reread:
         return line
+      if mt.group(2) in later:
+        return (f"{mt.group(1)}MJH_NT_STORE_IF(SV, P_{mt.group(2)}[{mt.group(3)}*64], "
+                f"{mt.group(4)});")
       return f"{mt.group(1)}MJH_NT_STORE(P_{mt.group(2)}[{mt.group(3)}*64], {mt.group(4)});"
     bodies = {st: ("\n".join(nt(x) for x in b.split("\n")) if st in NT_STAGES else b)
               for st, b in bodies.items()}
@@ -1361,7 +1371,8 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
     out.append("#if defined(__clang__)\n#pragma clang fp contract(off)\n#endif")
   for st in STAGES:
     params, args = _SIG[st]
-    out.append(f"MJH_HD void fast_{st}_{name}(const Mirror& mr, int blk, int lane, int B, "
+    out.append(f"template <bool SV = true>\n"
+               f"MJH_HD void fast_{st}_{name}(const Mirror& mr, int blk, int lane, int B, "
                f"{params}) {{\n{bodies[st]}\n}}\n")
   out.append(f"""MJH_HD void fast_body_{name}(
     const Mirror& mr, int blk, int lane, int B, const double* __restrict__ qpos_in,
@@ -1435,7 +1446,11 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   # the stream (mjhip_inverseFDBatch's limit-centre fall-back) without a host round trip.
   # The next call's work-list counter is zeroed by the launch's first thread, before any
   # instance bound, so an empty range still hands the counters on.
-  out.append(f"""{linkage}__global__ __launch_bounds__({nl}, {ALL_WAVES}) void k_all_{name}(Mirror mr, int B,
+  # SV: the va stage's re-read fields stream too (a batch that oversubscribes L2); a
+  # run-time code object (C linkage, no template) has the SV = true kernel only
+  tmpl = "" if extern_c else "template <bool SV>\n"
+  sv = "true" if extern_c else "SV"
+  out.append(f"""{tmpl}{linkage}__global__ __launch_bounds__({nl}, {ALL_WAVES}) void k_all_{name}(Mirror mr, int B,
     const double* __restrict__ qpos_in, const double* __restrict__ qvel_in,
     const double* __restrict__ qacc_in, double* __restrict__ qfrc_out, int* __restrict__ status,
     int* __restrict__ worklist, int* __restrict__ worklist_count, int* __restrict__ worklist_next,
@@ -1447,7 +1462,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
   int blk0 = 0;
   if (range) {{ blk0 = range[0] >> 6; B = range[1]; }}
   MJH_PHASE0(19, 27);
-""" + "\n".join(f"  fast_{st}_{name}(mr, {bl}, B, "
+""" + "\n".join(f"  fast_{st}_{name}<{sv}>(mr, {bl}, B, "
                 f"{_SIG[st][1].replace('worklist_next', 'nullptr')});\n"
                 f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE(); MJH_PHASE({20 + k});"
                 for k, st in enumerate(STAGES))
@@ -1476,6 +1491,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
                        f"{mt.group(1)}sblk{mt.group(3)}slane;", vb)
     skip_body = skip_body.replace("const bool cflag = ec[0] != 0;",
                                   "const bool cflag = ecs[0] != 0;")
+    skip_body = skip_body.replace("MJH_NT_STORE_IF(SV, ", "MJH_NT_STORE_IF(true, ")
     out.append(f"MJH_HD void fast_vaskip_{name}(const Mirror& mr, int blk, int lane, int sblk, "
                f"int slane, int B, const int* __restrict__ ecs, {_SIG['va'][0]}) {{\n"
                f"{skip_body}\n}}\n")
@@ -1502,8 +1518,12 @@ static void launch_vaskip_{name}(hipStream_t s, const Mirror& mr, int B, int off
     const int* range) {{""")
   if FUSE:
     gb = "g, b" if ALL_LANES == 64 else f"dim3(g.x*{64 // ALL_LANES}), dim3({ALL_LANES})"
-    out.append(f"  hipLaunchKernelGGL(k_all_{name}, {gb}, 0, s, mr, B, qpos_in, qvel_in, qacc_in, "
-               f"qfrc_out, status, worklist, worklist_count, worklist_next, efc_count, range);")
+    variants = ((f"B >= {NT_SV_MIN_B}", "<true>"), ("true", "<false>")) if not extern_c \
+        else (("true", ""),)
+    for cond, v in variants:
+      out.append(f"  if ({cond}) {{\n    hipLaunchKernelGGL(k_all_{name}{v}, {gb}, 0, s, mr, B, "
+                 f"qpos_in, qvel_in, qacc_in, qfrc_out, status, worklist, worklist_count, "
+                 f"worklist_next, efc_count, range);\n    return;\n  }}")
   else:   # staged kernels (experiments): the whole [0, B) range only
     out.append("  if (range) return;   // device-side ranges need k_all")
     for st in STAGES:

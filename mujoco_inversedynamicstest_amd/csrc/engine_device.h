@@ -92,6 +92,11 @@ static __device__ unsigned long long* mjh_tbuf = nullptr;
 #define MJH_NT_STORE(lv, v) ((lv) = (v))
 #define MJH_NT_LOAD(lv) (lv)
 #endif
+// a store that streams in one instantiation of a generated kernel (nt a template argument)
+#define MJH_NT_STORE_IF(nt, lv, v)                                                      \
+  do {                                                                                  \
+    if constexpr (nt) { MJH_NT_STORE(lv, v); } else { (lv) = (v); }                     \
+  } while (0)
 
 // mjtSensor values (include/mujoco/mjmodel.h)
 enum { mjhSENS_TOUCH = 0, mjhSENS_ACCELEROMETER, mjhSENS_VELOCIMETER, mjhSENS_GYRO,

@@ -27,7 +27,8 @@ def per_kernel(path, counter):
   vals = collections.defaultdict(list)
   for r in csv.DictReader(open(path)):
     if r["Counter_Name"] == counter:
-      vals[r["Kernel_Name"].split("(")[0]].append(float(r["Counter_Value"]) * 1024.0)
+      vals[r["Kernel_Name"].split("(")[0].replace("void ", "").split("<")[0]].append(
+          float(r["Counter_Value"]) * 1024.0)
   return {k: sum(v) / len(v) for k, v in vals.items()}
 
 

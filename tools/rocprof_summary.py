@@ -25,7 +25,7 @@ def main(src, dst, model="humanoid"):
   kernels = {}
   for r in csv.DictReader(open(path)):
     name = r["Name"]
-    base = name.split("(")[0].replace("void ", "")
+    base = name.split("(")[0].replace("void ", "").split("<")[0]
     if base == f"k_all_{model}" or base.startswith("k_constraint"):
       kernels[base] = {"calls": int(r["Calls"]), "avg_us": float(r["AverageNs"]) / 1e3,
                        "min_us": float(r["MinNs"]) / 1e3, "max_us": float(r["MaxNs"]) / 1e3}
