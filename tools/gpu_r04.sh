@@ -50,6 +50,9 @@ for step in "$@"; do
     variants)
       timeout -k 10 300 python tools/exp_variants.py run > gpurun_out/variants.log 2>&1 || { tail -20 gpurun_out/variants.log; exit 1; }
       cat gpurun_out/variants.log ;;
+    step)
+      timeout -k 10 180 python tools/exp_step.py > gpurun_out/step.log 2>&1 || { tail -20 gpurun_out/step.log; exit 1; }
+      cat gpurun_out/step.log ;;
     *)
       echo "unknown step $step"; exit 2 ;;
   esac
