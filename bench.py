@@ -145,8 +145,8 @@ def timed(fn, steps, world, dist, torch, dev):
 def main():
   ap = argparse.ArgumentParser()
   ap.add_argument("--gpus", type=int, default=1)
-  ap.add_argument("--steps", type=int, default=20)
-  ap.add_argument("--warmup", type=int, default=5)
+  ap.add_argument("--steps", type=int, default=200)
+  ap.add_argument("--warmup", type=int, default=20)
   ap.add_argument("--batch", type=int, default=65536, help="instances per GPU (weak scaling)")
   ap.add_argument("--global-batch", type=int, default=None,
                   help="total instances over all GPUs (strong scaling; config 3: 262144)")

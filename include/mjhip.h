@@ -290,6 +290,14 @@ typedef struct mjhipContext_ mjhipContext;
 /* upload the model to `device` and allocate a mirror for `capacity` instances */
 MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
                                   mjhipContext** out);
+/* mjhip_contextCreate with per-instance caps on contacts and constraint rows (0 = the exact
+ * worst case of mjhip_modelCapacity), the analogue of the reference's <size nconmax njmax>
+ * / memory arena bound (user_model.cc, mj_makeData): a model whose worst case is far beyond
+ * what its states produce (model/humanoid/humanoid100.xml: 16,123 contacts, 68,644 rows of
+ * 627 columns) sizes the mirror for what it needs. An instance that exceeds a cap is flagged
+ * MJHIP_INST_CNSTRFULL (mjWARN_CONTACTFULL / mjWARN_CNSTRFULL). */
+MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int capacity,
+                                        int max_contacts, int max_rows, mjhipContext** out);
 MJHIP_API void mjhip_contextFree(mjhipContext* c);
 MJHIP_API int mjhip_contextCapacity(const mjhipContext* c);
 /* name of the straight-line (model-specialized) kernel selected for the context's model by

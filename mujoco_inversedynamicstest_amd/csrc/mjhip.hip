@@ -618,7 +618,12 @@ MJHIP_API int mjhip_outputDoubles(const mjhipModel* m) {
 
 MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
                                   mjhipContext** out) {
-  if (!m || !out || capacity <= 0) {
+  return mjhip_contextCreateCapped(m, device, capacity, 0, 0, out);
+}
+
+MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int capacity,
+                                        int max_contacts, int max_rows, mjhipContext** out) {
+  if (!m || !out || capacity <= 0 || max_contacts < 0 || max_rows < 0) {
     set_error("mjhip_contextCreate: bad argument");
     return MJHIP_ERR_ARG;
   }
@@ -642,6 +647,10 @@ MJHIP_API int mjhip_contextCreate(const mjhipModel* m, int device, int capacity,
   c->capacity = (capacity + 63) & ~63;
   c->efc_cap = mjhip_efcCapacity(m);
   c->con_cap = mjhip_contactCapacity(m, nullptr);
+  // caller caps (the reference's <size nconmax njmax> / arena bound): an instance that needs
+  // more is flagged MJHIP_INST_CNSTRFULL, as mjWARN_CONTACTFULL / mjWARN_CNSTRFULL
+  if (max_contacts && max_contacts < c->con_cap) c->con_cap = max_contacts;
+  if (max_rows && max_rows < c->efc_cap) c->efc_cap = max_rows;
   c->hmodel = *m;
 
   // ---- model upload: one buffer, 256-byte aligned arrays

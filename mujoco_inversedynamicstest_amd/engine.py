@@ -47,6 +47,8 @@ SIGNATURES = {
     "mjhip_outputDoubles": (ctypes.c_int, [_V]),
     "mjhip_contextCreate": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int,
                                            ctypes.POINTER(_V)]),
+    "mjhip_contextCreateCapped": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                 ctypes.c_int, ctypes.POINTER(_V)]),
     "mjhip_contextFree": (None, [_V]),
     "mjhip_contextCapacity": (ctypes.c_int, [_V]),
     "mjhip_contextFastKernel": (ctypes.c_char_p, [_V]),
@@ -185,16 +187,19 @@ class InverseEngine:
   current stream (inputs written by earlier torch work are read, and later torch work sees
   the outputs); host-array calls are synchronous."""
 
-  def __init__(self, model, capacity: int, device: int = 0, specialize=None):
+  def __init__(self, model, capacity: int, device: int = 0, specialize=None,
+               max_contacts: int = 0, max_rows: int = 0):
     """specialize: generate and load a straight-line kernel for a model that has no bundled
     one (specialize.py; compiled once per model, then cached). None = the MJHIP_SPECIALIZE
-    environment variable ("1" default, "0" off)."""
+    environment variable ("1" default, "0" off). max_contacts / max_rows: per-instance caps
+    below the exact worst case (mjhip_contextCreateCapped; 0 = no cap)."""
     self.m = model
     self.cm = host.model_struct(model)
     L = lib()
     ctx = _V()
-    _check(L.mjhip_contextCreate(ctypes.byref(self.cm), device, capacity, ctypes.byref(ctx)),
-           "mjhip_contextCreate")
+    _check(L.mjhip_contextCreateCapped(ctypes.byref(self.cm), device, capacity, max_contacts,
+                                       max_rows, ctypes.byref(ctx)),
+           "mjhip_contextCreateCapped")
     self.ctx = ctx
     self.device = device
     self.capacity = L.mjhip_contextCapacity(ctx)

@@ -198,7 +198,25 @@ def mulvecmat(vec, mat):
 
 
 def rotvecquat(vec, quat):
-  return mulvecmat(vec, quat2mat(quat))
+  """mjuu_rotVecQuat (user_util.cc:572): v + 2 q_xyz x (q_w v + q_xyz x v)."""
+  if vec[0] == 0 and vec[1] == 0 and vec[2] == 0:
+    return [0.0, 0.0, 0.0]
+  if quat[0] == 1 and quat[1] == 0 and quat[2] == 0 and quat[3] == 0:
+    return list(vec)
+  t = [quat[0]*vec[0] + quat[2]*vec[2] - quat[3]*vec[1],
+       quat[0]*vec[1] + quat[3]*vec[0] - quat[1]*vec[2],
+       quat[0]*vec[2] + quat[1]*vec[1] - quat[2]*vec[0]]
+  return [vec[0] + 2 * (quat[2]*t[2] - quat[3]*t[1]),
+          vec[1] + 2 * (quat[3]*t[0] - quat[1]*t[2]),
+          vec[2] + 2 * (quat[1]*t[1] - quat[2]*t[0])]
+
+
+def frameaccum(pos, quat, childpos, childquat):
+  """mjuu_frameaccum (user_util.cc:458): the child frame expressed through (pos, quat);
+  returns the new (pos, quat). mjuu_frameaccumChild (:472) is the same with the result
+  stored in the child."""
+  vec = mulvecmat(childpos, quat2mat(quat))
+  return [pos[0] + vec[0], pos[1] + vec[1], pos[2] + vec[2]], mulquat(quat, childquat)
 
 
 def globalinertia(local, quat):
@@ -343,6 +361,38 @@ class _Defaults:
 
 ACTUATOR_TAGS = ("general", "motor", "position", "velocity", "intvelocity", "adhesion")
 
+# name references of the referencing elements an <attach>/<replicate> namespaces (attribute
+# -> kind of object it names; mjCEquality/mjCActuator/mjCSensor::NameSpace,
+# user_objects.cc:5119, 5811, 6147)
+EQ_REFS = {"body1": "body", "body2": "body", "joint1": "joint", "joint2": "joint",
+           "tendon1": "tendon", "tendon2": "tendon", "site1": "site", "site2": "site"}
+ACT_REFS = {"joint": "joint", "jointinparent": "joint", "tendon": "tendon", "site": "site",
+            "refsite": "site", "body": "body", "cranksite": "site", "slidersite": "site"}
+SENSOR_REFS = {"site": "site", "joint": "joint", "tendon": "tendon", "actuator": "actuator",
+               "body": "body", "geom1": "geom", "geom2": "geom", "body1": "body",
+               "body2": "body", "objname": "any", "refname": "any"}
+
+
+def _prefixed(a, prefix, keys, suffix=""):
+  """A copy of attribute dict `a` with the non-empty names under `keys` namespaced
+  (mjCBase::NameSpace, user_objects.cc:707-714)."""
+  return {k: (prefix + v + suffix if k in keys and isinstance(v, str) and v else v)
+          for k, v in a.items()}
+
+
+def _namespace(b, prefix, suffix, own=True):
+  """mjCBody::NameSpace_ (user_objects.cc:1129-1175) over a parsed subtree, in place: the
+  body's name (unless own=False), its elements' names and its descendants'."""
+  if own and b.name:
+    b.name = prefix + b.name + suffix
+    b.attrs["name"] = b.name
+  for lst in (b.joints, b.geoms, b.sites, b.cams, b.lights):
+    for a in lst:
+      if a.get("name"):
+        a["name"] = prefix + a["name"] + suffix
+  for c in b.children:
+    _namespace(c, prefix, suffix)
+
 
 def _resolve_orientation(attrs, degree, eulerseq, quat):
   """ResolveOrientation (user_objects.cc:240) for axisangle/xyaxes/zaxis/euler."""
@@ -377,21 +427,25 @@ def _resolve_orientation(attrs, degree, eulerseq, quat):
       raise MJCFError("zaxis too small")
     return z2quat(z)
   if "euler" in attrs:
-    eu = _floats(attrs["euler"])
-    if degree:
-      eu = [e / 180.0 * mjPI for e in eu]
-    q = [1.0, 0.0, 0.0, 0.0]
-    for i in range(3):
-      qrot = [math.cos(eu[i]/2), 0.0, 0.0, 0.0]
-      sa = math.sin(eu[i]/2)
-      ax = eulerseq[i]
-      qrot["xyz".index(ax.lower()) + 1] = sa
-      if ax.islower():   # moving axes: post-multiply
-        q = mulquat(q, qrot)
-      else:              # fixed axes: pre-multiply
-        q = mulquat(qrot, q)
-    return q
+    return _euler_quat(_floats(attrs["euler"]), degree, eulerseq)
   return quat
+
+
+def _euler_quat(eu, degree, eulerseq):
+  """The euler branch of ResolveOrientation (user_objects.cc:300-330)."""
+  if degree:
+    eu = [e / 180.0 * mjPI for e in eu]
+  q = [1.0, 0.0, 0.0, 0.0]
+  for i in range(3):
+    qrot = [math.cos(eu[i]/2), 0.0, 0.0, 0.0]
+    sa = math.sin(eu[i]/2)
+    ax = eulerseq[i]
+    qrot["xyz".index(ax.lower()) + 1] = sa
+    if ax.islower():   # moving axes: post-multiply
+      q = mulquat(q, qrot)
+    else:              # fixed axes: pre-multiply
+      q = mulquat(qrot, q)
+  return q
 
 
 #--------------------------------- compiled objects ----------------------------------------
@@ -411,6 +465,38 @@ class Body:
     self.inertial = None
     self.id = -1
     self.name = attrs.get("name", "")
+    self.frame = None              # the <frame> (or replicate/attach frame) it sits in
+
+
+class Frame:
+  """A coordinate frame around body children (mjCFrame): a <frame> element, one copy of a
+  <replicate> (explicit pos/quat) or an <attach> point. Elements inside one carry it (bodies
+  in .frame, element attribute dicts under "__frame") and compose it into their own pose at
+  the end of their compile, as mjuu_frameaccumChild does (user_objects.cc:1739, 2222-2243,
+  3104, 3260, 3368, 3504)."""
+
+  def __init__(self, parent, attrs=None, pos=None, quat=None):
+    self.parent = parent
+    self.attrs = attrs or {}
+    self._pos, self._quat = pos, quat
+    self.pose = None
+
+  def compile(self, c):
+    """mjCFrame::Compile (user_objects.cc:2001-2019): own orientation, then the parent frame
+    accumulated, then normalized; once."""
+    if self.pose is None:
+      a = self.attrs
+      pos = list(self._pos) if self._pos is not None else (
+          _floats(a["pos"]) if "pos" in a else [0.0, 0.0, 0.0])
+      quat = list(self._quat) if self._quat is not None else (
+          _floats(a["quat"]) if "quat" in a else [1.0, 0.0, 0.0, 0.0])
+      quat = _resolve_orientation(a, c.degree, c.eulerseq, quat)
+      if self.parent is not None:
+        ppos, pquat = self.parent.compile(c)
+        pos, quat = frameaccum(ppos, pquat, pos, quat)
+      normvec(quat)
+      self.pose = (pos, quat)
+    return self.pose
 
 
 class Model:
@@ -510,6 +596,8 @@ class MJCFCompiler:
     self.equalities = []
     self.excludes = []
     self.keys = []
+    self.models = {}                    # name -> MJCFCompiler (<asset><model>, parsed only)
+    self.basedir = None
 
   # ---------------------------------------------------------------- parsing
   def _parse_defaults(self, el, parent):
@@ -531,36 +619,206 @@ class MJCFCompiler:
     a.update(el.attrib)
     return a
 
-  def _parse_body(self, el, parent, childclass):
+  def _parse_body(self, el, parent, childclass, frame=None):
     attrs = dict(el.attrib)
     cc = attrs.get("childclass", childclass)
     b = Body(parent, attrs, attrs.get("class", childclass), cc)
+    b.frame = frame
     self.bodies.append(b)
+    self._parse_children(el, b, cc, None)
+    return b
+
+  def _parse_children(self, el, b, cc, frame):
+    """The child elements of a body (or of a <frame>/<replicate> inside it): mjXReader::Body
+    (xml_native_reader.cc:3380-3640). Elements inside a frame carry it."""
+    world = b.parent is None and b.name == "world"
+
+    def framed(a):
+      if frame is not None:
+        a["__frame"] = frame
+      return a
     for ch in el:
       t = ch.tag
       if t == "body":
-        b.children.append(self._parse_body(ch, b, cc))
+        b.children.append(self._parse_body(ch, b, cc, frame))
+      elif t in ("joint", "freejoint", "inertial") and world:
+        raise MJCFError(f"<{t}> is not allowed in the world body")
       elif t == "joint":
-        b.joints.append(self._elem_attrs(ch, "joint", cc))
+        b.joints.append(framed(self._elem_attrs(ch, "joint", cc)))
       elif t == "freejoint":
         a = {"type": "free"}
         for k in ("name", "align", "group"):
           if k in ch.attrib:
             a[k] = ch.attrib[k]
-        b.joints.append(a)
+        b.joints.append(framed(a))
       elif t == "geom":
-        b.geoms.append(self._elem_attrs(ch, "geom", cc))
+        b.geoms.append(framed(self._elem_attrs(ch, "geom", cc)))
       elif t == "site":
-        b.sites.append(self._elem_attrs(ch, "site", cc))
+        b.sites.append(framed(self._elem_attrs(ch, "site", cc)))
       elif t == "camera":
-        b.cams.append(self._elem_attrs(ch, "camera", cc))
+        b.cams.append(framed(self._elem_attrs(ch, "camera", cc)))
       elif t == "light":
-        b.lights.append(self._elem_attrs(ch, "light", cc))
+        b.lights.append(framed(self._elem_attrs(ch, "light", cc)))
       elif t == "inertial":
         b.inertial = dict(ch.attrib)
+      elif t == "frame":                    # xml_native_reader.cc:3477-3500
+        fcc = ch.get("childclass", cc)
+        if fcc is not None and fcc not in self.classes:
+          raise MJCFError(f"unknown default childclass '{fcc}'")
+        self._parse_children(ch, b, fcc, Frame(frame, dict(ch.attrib)))
+      elif t == "replicate":
+        self._parse_replicate(ch, b, cc, frame)
+      elif t == "attach":
+        self._parse_attach(ch, b, frame)
       else:
         raise MJCFError(f"unsupported body child element <{t}>")
-    return b
+
+  def _parse_replicate(self, el, b, cc, frame):
+    """<replicate> (xml_native_reader.cc:3503-3572): `count` copies of the children, copy i
+    in a frame at the accumulated offset, rotated by i*euler, its element names suffixed
+    with sep + i zero-padded to the digits of count (UpdateString, :83-91). The reference
+    parses the children once into a scratch body and attaches copies of its frame; each copy
+    here is parsed afresh into a scratch body with its own frame objects, which yields the
+    same elements, order and names (inner copies of nested replicates get their suffix
+    first). As the reference's self-attach, each copy also appends the suffixed copies of
+    the referencing elements parsed so far whose suffixed references resolve."""
+    if "count" not in el.attrib:
+      raise MJCFError("replicate needs a count")
+    count = int(el.get("count"))
+    offset = _floats(el.get("offset", "0 0 0"))
+    euler = _floats(el.get("euler", "0 0 0"))
+    sep = el.get("sep", "")
+    rcc = el.get("childclass", cc)
+    if rcc is not None and rcc not in self.classes:
+      raise MJCFError(f"unknown default childclass '{rcc}'")
+    rotation = _euler_quat(euler, self.degree, self.eulerseq)
+    pos, quat = [0.0, 0.0, 0.0], [1.0, 0.0, 0.0, 0.0]
+    for i in range(count):
+      fpos = list(pos)
+      pos, quat = frameaccum(pos, quat, offset, rotation)
+      quat = _euler_quat([i * e for e in euler], self.degree, self.eulerseq)
+      suffix = sep + str(i).zfill(len(str(count)))
+      scratch = Body(b.parent, {"name": b.name}, b.cls, rcc)
+      self._parse_children(el, scratch, rcc, Frame(frame, pos=fpos, quat=list(quat)))
+      if scratch.inertial is not None:
+        raise MJCFError("<inertial> inside <replicate>")
+      _namespace(scratch, "", suffix, own=False)
+      for lst in ("joints", "geoms", "sites", "cams", "lights"):
+        getattr(b, lst).extend(getattr(scratch, lst))
+      for c in scratch.children:
+        c.parent = b
+        b.children.append(c)
+      self._append_referencing(self, "", suffix)
+
+  def _parse_attach(self, el, b, frame):
+    """<attach model body prefix> (xml_native_reader.cc:3621-3646, mjCBody::operator+=
+    user_objects.cc:865-955, mjCModel::operator+= user_model.cc:404-464): a copy of body
+    `body` of the <asset><model> `model`, with its subtree, at the enclosing frame (a new
+    identity frame without one); every name prefixed. The model's assets follow with
+    prefixed names, and its excludes, tendons, equalities, actuators and sensors whose
+    (prefixed) references all resolve in this model are appended in that order. The
+    attached model's keyframes are not carried over (keyframes are not on the path)."""
+    for k in ("model", "body", "prefix"):
+      if k not in el.attrib:
+        raise MJCFError(f"attach needs '{k}'")
+    name, bname, prefix = el.get("model"), el.get("body"), el.get("prefix")
+    sub = self.models.get(name)
+    if sub is None:
+      raise MJCFError(f"could not find model '{name}'")
+    if any(x.name == prefix + bname for x in self.bodies):
+      raise MJCFError("attach to an existing body (frame only) is not in the supported subset")
+    for k in ("degree", "eulerseq", "inertiafromgeom", "autolimits", "boundmass",
+              "boundinertia", "balanceinertia", "inertiagrouprange"):
+      if getattr(sub, k) != getattr(self, k):
+        raise MJCFError(f"attached model '{name}' has a different compiler {k}")
+    src = next((x for x in sub.bodies if x.name == bname and x.parent is not None), None)
+    if src is None:
+      raise MJCFError(f"could not find body '{bname}' in model '{name}'")
+    top = self._clone_body(src, b, prefix)
+    top.frame = frame if frame is not None else Frame(None)
+    b.children.append(top)
+    # assets (all of them, as the reference's CopyList), then the referencing elements
+    for nm, rgba in sub.materials.items():
+      self.materials[prefix + nm] = rgba
+    for nm, mesh in sub.meshes.items():
+      self.meshes[prefix + nm] = mesh
+    for nm, hf in sub.hfields.items():
+      self.hfields[prefix + nm] = hf
+    self._append_referencing(sub, prefix, "")
+
+  def _append_referencing(self, src, prefix, suffix):
+    """mjCModel::operator+= (user_model.cc:427-432) over CopyList (:223-261): each exclude,
+    tendon, equality, actuator and sensor of `src` (another model for attach, this one for a
+    replicate copy) is namespaced -- its name and references -- and appended when every
+    reference resolves in this model; the others are skipped."""
+    names = self._names()
+    p = lambda s: None if s is None else prefix + s + suffix
+    ns = lambda a, keys: {k: (p(v) if k in keys and isinstance(v, str) and v else v)
+                          for k, v in a.items()}
+    lists = [list(src.excludes), list(src.tendons), list(src.equalities),
+             list(src.actuators), list(src.sensors)]
+    for b1, b2 in lists[0]:
+      if p(b1) in names["body"] and p(b2) in names["body"]:
+        self.excludes.append((p(b1), p(b2)))
+    for a, path in lists[1]:
+      a = ns(a, ("name",))
+      if a.get("__kind") == "fixed":
+        path = [(p(j), c) for j, c in path]
+        ok = all(j in names["joint"] for j, _ in path)
+      else:
+        path = [(k, p(v) if k == "site" else (p(v[0]), p(v[1])) if k == "geom" else v)
+                for k, v in path]
+        ok = all((k != "site" or v in names["site"]) and
+                 (k != "geom" or (v[0] in names["geom"] and
+                                  (v[1] is None or v[1] in names["site"]))) for k, v in path)
+      if ok:
+        self.tendons.append((a, path))
+        names["tendon"].add(a.get("name"))
+    for lst, refs, dst in ((lists[2], EQ_REFS, self.equalities),
+                           (lists[3], ACT_REFS, self.actuators)):
+      for a in lst:
+        a = ns(a, ("name",) + tuple(refs))
+        if all(a[k] in names[kind] for k, kind in refs.items() if k in a):
+          dst.append(a)
+          if dst is self.actuators:
+            names["actuator"].add(a.get("name"))
+    for tag, a in lists[4]:
+      a = ns(a, ("name",) + tuple(SENSOR_REFS))
+      if all(a[k] in names[kind] for k, kind in SENSOR_REFS.items() if k in a):
+        self.sensors.append((tag, a))
+
+  def _clone_body(self, src, parent, prefix):
+    """A copy of an attached model's body subtree with prefixed names (mjCBody copy +
+    NameSpace, user_objects.cc:1122-1175, 2365-2379, 3180-3185); frames inside the subtree
+    are shared with the source (they are not modified)."""
+    nb = Body(parent, _prefixed(src.attrs, prefix, ("name",)), src.cls, src.childclass)
+    nb.frame = src.frame
+    nb.inertial = dict(src.inertial) if src.inertial is not None else None
+    nb.joints = [_prefixed(a, prefix, ("name",)) for a in src.joints]
+    nb.geoms = [_prefixed(a, prefix, ("name", "material", "mesh", "hfield")) for a in src.geoms]
+    nb.sites = [_prefixed(a, prefix, ("name", "material")) for a in src.sites]
+    nb.cams = [_prefixed(a, prefix, ("name", "target")) for a in src.cams]
+    nb.lights = [_prefixed(a, prefix, ("name", "target")) for a in src.lights]
+    self.bodies.append(nb)
+    nb.children = [self._clone_body(c, nb, prefix) for c in src.children]
+    return nb
+
+  def _names(self):
+    """Names of the elements parsed so far, per kind (reference resolution of attached
+    referencing elements)."""
+    out = {"body": set(), "joint": set(), "geom": set(), "site": set(), "camera": set(),
+           "tendon": {a.get("name") for a, _ in self.tendons},
+           "actuator": {a.get("name") for a in self.actuators}}
+    for b in self.bodies:
+      out["body"].add(b.name)
+      for kind, lst in (("joint", b.joints), ("geom", b.geoms), ("site", b.sites),
+                        ("camera", b.cams)):
+        out[kind].update(a.get("name") for a in lst)
+    for v in out.values():
+      v.discard(None)
+      v.discard("")
+    out["any"] = set().union(*out.values())
+    return out
 
   def parse(self, root):
     if root.tag != "mujoco":
@@ -663,12 +921,32 @@ class MJCFCompiler:
             self._parse_hfield(ch)
           elif ch.tag == "texture":
             continue
+          elif ch.tag == "model":
+            self._parse_model_asset(ch)
           else:
             raise MJCFError(f"unsupported asset <{ch.tag}>")
       elif t in ("visual", "statistic", "default", "compiler", "size", "extension", "custom"):
         continue  # no effect on the inverse-dynamics path
       else:
         raise MJCFError(f"unsupported top-level element <{t}>")
+
+  def _parse_model_asset(self, el):
+    """<asset><model file name> (xml_native_reader.cc:3307-3336): another MJCF file, parsed
+    (not compiled) for <attach>; named by `name`, else by its own model name."""
+    if el.get("content_type", "text/xml") != "text/xml":
+      raise MJCFError(f"unsupported content_type: {el.get('content_type')}")
+    if "file" not in el.attrib:
+      raise MJCFError("model asset needs a file")
+    if self.basedir is None:
+      raise MJCFError("a model asset needs the directory of the including file (load_xml)")
+    path = os.path.join(self.basedir, el.get("file"))
+    sub = MJCFCompiler()
+    sub.basedir = os.path.dirname(os.path.abspath(path))
+    try:
+      sub.parse(ET.parse(path).getroot())
+    except (OSError, ET.ParseError) as e:
+      raise MJCFError(f"could not parse model file: {e}") from e
+    self.models[el.get("name", sub.model_name)] = sub
 
   def _parse_mesh(self, el):
     """<mesh> with inline vertex (and optional face) data (xml_native_reader.cc:1405-1480);
@@ -749,20 +1027,7 @@ class MJCFCompiler:
   def _parse_worldbody(self, el):
     world = Body(None, {"name": "world"}, None, None)
     self.bodies.insert(0, world)
-    for ch in el:
-      t = ch.tag
-      if t == "body":
-        world.children.append(self._parse_body(ch, world, None))
-      elif t == "geom":
-        world.geoms.append(self._elem_attrs(ch, "geom", None))
-      elif t == "site":
-        world.sites.append(self._elem_attrs(ch, "site", None))
-      elif t == "camera":
-        world.cams.append(self._elem_attrs(ch, "camera", None))
-      elif t == "light":
-        world.lights.append(self._elem_attrs(ch, "light", None))
-      else:
-        raise MJCFError(f"unsupported worldbody element <{t}>")
+    self._parse_children(el, world, None, None)
 
   # ---------------------------------------------------------------- compile
   def _order_bodies(self):
@@ -910,6 +1175,9 @@ class MJCFCompiler:
     # fluid-interaction coefficients (user_objects.cc:3081-3084)
     g["fluid"] = _fluid_coefs(t, size, g["fluid_ellipsoid"], g["fluid_coefs"]) \
         if g["fluid_ellipsoid"] > 0 else [0.0] * 12
+    if "__frame" in a:                   # end of mjCGeom::Compile (user_objects.cc:3102-3105)
+      fpos, fquat = a["__frame"].compile(self)
+      g["pos"], g["quat"] = frameaccum(fpos, fquat, g["pos"], g["quat"])
     return g
 
   def compile(self) -> Model:
@@ -972,6 +1240,9 @@ class MJCFCompiler:
       if b.ipos is None:
         b.ipos = list(b.pos)
         b.iquat = list(b.quat)
+      if b.frame is not None:           # after the inertial copy (user_objects.cc:1737-1740)
+        fpos, fquat = b.frame.compile(self)
+        b.pos, b.quat = frameaccum(fpos, fquat, b.pos, b.quat)
       if b.id > 0:
         b.mass = max(b.mass, self.boundmass)
         b.inertia = [max(x, self.boundinertia) for x in b.inertia]
@@ -1067,13 +1338,18 @@ class MJCFCompiler:
         if rng[1]:
           rng[1] *= mjPI/180.0
     axis = _floats(a["axis"]) if "axis" in a else [0.0, 0.0, 1.0]
+    frame = a["__frame"].compile(self) if "__frame" in a else None
     if t in (JNT["free"], JNT["ball"]):
       axis = [0.0, 0.0, 1.0]
+    elif frame is not None:              # user_objects.cc:2220-2223
+      axis = rotvecquat(axis, frame[1])
     if normvec(axis) < mjEPS:
       raise MJCFError("axis too small in joint")
     pos = _floats(a["pos"]) if "pos" in a else [0.0, 0.0, 0.0]
     if t == JNT["free"]:
       pos = [0.0, 0.0, 0.0]
+    elif frame is not None:              # (:2240-2244)
+      pos = frameaccum(frame[0], frame[1], pos, [1.0, 0.0, 0.0, 0.0])[0]
     ref = float(a.get("ref", 0.0))
     springref = float(a.get("springref", 0.0))
     if t == JNT["hinge"] and self.degree:
@@ -1106,6 +1382,10 @@ class MJCFCompiler:
     quat = _floats(a["quat"]) if "quat" in a else [1.0, 0.0, 0.0, 0.0]
     normvec(quat)
     quat = _resolve_orientation(a, self.degree, self.eulerseq, quat)
+    if "__frame" in a:                   # user_objects.cc:3258-3264
+      fpos, fquat = a["__frame"].compile(self)
+      pos, quat = frameaccum(fpos, fquat, pos, quat)
+      normvec(quat)
     size = [0.005, 0.005, 0.005]
     if "size" in a:
       s = _floats(a["size"])
@@ -1118,6 +1398,10 @@ class MJCFCompiler:
     quat = _floats(a["quat"]) if "quat" in a else [1.0, 0.0, 0.0, 0.0]
     normvec(quat)
     quat = _resolve_orientation(a, self.degree, self.eulerseq, quat)
+    if "__frame" in a:                   # user_objects.cc:3366-3372
+      fpos, fquat = a["__frame"].compile(self)
+      pos, quat = frameaccum(fpos, fquat, pos, quat)
+      normvec(quat)
     # intrinsics (user_objects.cc mjCCamera::Compile :3383-3420, float arithmetic)
     f32 = np.float32
     fovy = float(a.get("fovy", 45.0))
@@ -1148,6 +1432,10 @@ class MJCFCompiler:
   def _compile_light(self, a, bid):
     pos = _floats(a["pos"]) if "pos" in a else [0.0, 0.0, 0.0]
     d = _floats(a["dir"]) if "dir" in a else [0.0, 0.0, -1.0]
+    if "__frame" in a:                   # user_objects.cc:3500-3508
+      fpos, fquat = a["__frame"].compile(self)
+      pos = frameaccum(fpos, fquat, pos, [1.0, 0.0, 0.0, 0.0])[0]
+      d = rotvecquat(d, fquat)
     normvec(d)
     return {"body": bid, "pos": pos, "dir": d, "mode": CAMLIGHT[a.get("mode", "fixed")],
             "target": a.get("target"), "name": a.get("name", "")}
@@ -2312,6 +2600,7 @@ def load_xml_string(text: str, basedir: str | None = None) -> Model:
   from . import setconst
   root = ET.fromstring(text)
   c = MJCFCompiler()
+  c.basedir = basedir
   c.parse(root)
   m = c.compile()
   setconst.set_const(m)

@@ -11,6 +11,8 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 # name -> MJCF path relative to the reference root
 SOURCES = {
     "humanoid": "model/humanoid/humanoid.xml",                  # BASELINE.json configs 2-5
+    # the reference's 627-dof benchmark model: humanoid.xml attached + 100 replicated bodies
+    "humanoid100": "model/humanoid/humanoid100.xml",
     "slider_crank": "model/slider_crank/slider_crank.xml",      # BASELINE.json config 1
     "inverse_test": "src/inverse/test.xml",                      # inverse_test.cpp model
     "linear": "test/engine/testdata/derivative/linear.xml",     # LinearSystemInverse

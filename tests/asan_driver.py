@@ -17,8 +17,8 @@ from mujoco_inversedynamicstest_amd.sampler import sample_contact_states, sample
 from oracle.oracle import Oracle  # noqa: E402
 
 
-def check(name, m, q, v, a, fd=False):
-  o, k = Oracle(m), KernelCPU(m)
+def check(name, m, q, v, a, fd=False, caps=(None, None)):
+  o, k = Oracle(m), KernelCPU(m, efc_cap=caps[0], con_cap=caps[1])
   for i in range(len(q)):
     ref = o.inverse(q[i], v[i], a[i])
     got, _ = k.inverse(q[i], v[i], a[i])
@@ -73,6 +73,10 @@ def main():
     q[:, 7 * b + 3:7 * b + 7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
   q[:, 7:10] = q[:, 0:3] + rng.uniform(-0.25, 0.25, (16, 3))
   check("boxbox", bm, q, rng.normal(size=(16, bm.nv)), rng.normal(size=(16, bm.nv)))
+  # round 4: the 627-dof humanoid100 (attach/replicate) with ~150 contacts, capped context
+  import humanoid100_states as H
+  m = H.model()
+  check("humanoid100", m, *H.states(m, 2, seed=9), caps=(H.MAX_ROWS, H.MAX_CONTACTS))
   print("ASAN_DRIVER_OK", flush=True)
 
 

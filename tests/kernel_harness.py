@@ -60,7 +60,7 @@ class KernelCPU:
     from oracle.oracle import lib as olib
     self.m = m
     self.cm = host.model_struct(m)
-    self.d = host.MjData(m)
+    self.d = host.MjData(m, efc_capacity=efc_cap, con_capacity=con_cap)
     O = olib()
     self.efc_cap = O.or_efcCapacity(ctypes.byref(self.cm)) if efc_cap is None else efc_cap
     self.con_cap = max(O.or_contactCapacity(ctypes.byref(self.cm)), 0) if con_cap is None \
