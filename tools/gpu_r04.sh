@@ -50,6 +50,20 @@ for step in "$@"; do
     variants)
       timeout -k 10 300 python tools/exp_variants.py run > gpurun_out/variants.log 2>&1 || { tail -20 gpurun_out/variants.log; exit 1; }
       cat gpurun_out/variants.log ;;
+    h100)
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_h100 -o h100 \
+        --output-format csv -- python tools/bench_model.py humanoid100 ${H100_B:-4096} 10 \
+        > gpurun_out/h100.log 2>&1 || { tail -20 gpurun_out/h100.log; exit 1; }
+      grep -v "^W\|^\[" gpurun_out/h100.log | tail -3
+      find gpurun_out/prof_h100 -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-150 ;;
+    c4t)
+      timeout -k 10 120 python tools/bench_model.py humanoid_contacts 4096 20 > gpurun_out/c4t.log 2>&1 || { tail -20 gpurun_out/c4t.log; exit 1; }
+      grep -v "^W\|^\[" gpurun_out/c4t.log | tail -3 ;;
+    ccdblocks)
+      for w in 1 2; do for nb in 512 1024 2048 4096; do
+        MJHIP_CCD_WPE=$w MJHIP_CCD_BLOCKS=$nb timeout -k 10 120 python tools/bench_model.py slider_crank 65536 20 > gpurun_out/ccdb_${w}_${nb}.log 2>&1 || { tail -20 gpurun_out/ccdb_${w}_${nb}.log; exit 1; }
+        echo "wpe $w blocks $nb: $(grep 'ms per call' gpurun_out/ccdb_${w}_${nb}.log)"
+      done; done ;;
     step)
       timeout -k 10 180 python tools/exp_step.py > gpurun_out/step.log 2>&1 || { tail -20 gpurun_out/step.log; exit 1; }
       cat gpurun_out/step.log ;;
