@@ -3,10 +3,16 @@
 The reference switches to compressed rows when mj_isSparse (engine_core_constraint.c:96-103):
 efc_J and ten_J hold each row's entries over the merged dof chains of its bodies, and
 mj_mulJacVec / mj_mulJacTVec / the J'force of mj_constraintUpdate run the sparse kernels
-(mju_mulMatVecSparse, mju_mulMatTVecSparse, engine_util_sparse.c). Every entry those form is
-the same product or sum, in the same order, as the dense path's, which only adds exact zeros
-(x + 0*y == x for finite x other than -0), so the engine computes these models with dense
-rows and reproduces the sparse path's results.
+(mju_mulMatVecSparse, mju_mulMatTVecSparse, engine_util_sparse.c). The engine computes these
+models with dense rows:
+  * J'force (mju_mulMatTVecSparse scatters row by row) is the dense per-column sum in row
+    order plus exact zeros (x + 0*y == x for finite x other than -0): identical bits;
+  * J*v (efc_vel, jar) is mju_dotSparse, a 4-way unrolled sum grouped by position in the
+    row's colind (engine_util_sparse.h:115-160), where the dense mju_dot groups by column
+    index: the same terms in other partial sums, so the two differ in the last bits on some
+    rows (measured below); the dense result is within an ulp-level bound of the sparse one,
+    far inside the path's 1e-10 bar. Reproducing those bits needs the compressed row layout
+    (sparse Jacobians).
 
 Checked here: the model compiles in the sparse range and runs the generic kernel (the
 straight-line kernels stop at nv = 60); the device pipeline compiled for the host equals the
@@ -59,14 +65,47 @@ def _chain(m, body):
   return sorted(out)
 
 
+def _dot4(a, b):
+  """mju_dot's scalar branch (engine_util_blas.c:680-720): four partial sums by index."""
+  n, i, r = len(a), 0, [0.0, 0.0, 0.0, 0.0]
+  while i <= n - 4:
+    for k in range(4):
+      r[k] += a[i + k] * b[i + k]
+    i += 4
+  res = (r[0] + r[2]) + (r[1] + r[3])
+  if n - i == 3:
+    res += a[i] * b[i] + a[i + 1] * b[i + 1] + a[i + 2] * b[i + 2]
+  elif n - i == 2:
+    res += a[i] * b[i] + a[i + 1] * b[i + 1]
+  elif n - i == 1:
+    res += a[i] * b[i]
+  return res
+
+
+def _dot_sparse(vals, x, ind):
+  """mju_dotSparse's scalar branch (engine_util_sparse.h:115-160): partial sums by position."""
+  n, i, r = len(ind), 0, [0.0, 0.0, 0.0, 0.0]
+  while i <= n - 4:
+    for k in range(4):
+      r[k] += vals[i + k] * x[ind[i + k]]
+    i += 4
+  res = (r[0] + r[2]) + (r[1] + r[3])
+  while i < n:
+    res += vals[i] * x[ind[i]]
+    i += 1
+  return res
+
+
 def test_dense_rows_equal_sparse_kernels():
-  """mju_mulMatVecSparse / mju_mulMatTVecSparse restated over (a) each row's nonzeros and
-  (b) the union of the contact's two body chains (the reference's merged chain, zeros
-  stored), against the dense sums the engine forms: identical bits."""
+  """Sequential sums over (a) each row's nonzeros and (b) the union of the contact's two
+  body chains (the reference's merged chain, zeros stored) equal the dense sequential sums
+  bit for bit; mju_mulMatTVecSparse's row-by-row scatter equals the engine's J'force bit for
+  bit; mju_dotSparse over the merged chain (4-way unrolled by position) differs from the
+  dense 4-way mju_dot by at most a few ulps of the row's term magnitudes."""
   m = S.pile()
   q, v, a = S.states(m, 12, seed=2)
   o = Oracle(m)
-  checked = 0
+  checked = differ = 0
   for i in range(12):
     o.inverse(q[i], v[i], a[i])
     nefc = o.efc.nefc
@@ -106,5 +145,16 @@ def test_dense_rows_equal_sparse_kernels():
           sparse_t[c] += J[r, c] * force[r]
     np.testing.assert_array_equal(sparse_t, dense_t)
     np.testing.assert_array_equal(dense_t, o.d.qfrc_constraint)
+    # the unrolled dots: dense mju_dot (the engine) vs mju_dotSparse over the merged chain
+    for r in range(nefc):
+      if types[r] < 5:
+        continue
+      g1, g2 = geoms[ids[r]]
+      chain = sorted(set(_chain(m, m.geom_bodyid[g1])) | set(_chain(m, m.geom_bodyid[g2])))
+      d1, d2 = _dot4(J[r], x), _dot_sparse(J[r][chain], x, chain)
+      scale = float(np.sum(np.abs(J[r] * x)))
+      assert abs(d1 - d2) <= 8 * np.finfo(float).eps * scale
+      differ += d1 != d2
     checked += nefc
   assert checked > 100
+  print(f"contact rows whose unrolled dense and sparse dots differ in the last bits: {differ}")
