@@ -140,6 +140,15 @@ MJH_HD int mjh_needSliderCrank(const mjhipModel* m) {
 // 1 when a candidate geom pair of the model runs the native GJK/EPA solver (mjc_Convex,
 // mjc_ConvexHField): its
 // per-instance scratch (mjh::CcdMem) is allocated, 6 ccd_iterations + 6 faces
+// mj_isSparse (engine_core_constraint.c:96-103): the reference keeps compressed constraint
+// rows. Here the rows stay dense, but each row records its dof span (efc_lo, efc_hi): the
+// producers write and the J*v / J'force consumers visit only the span, the rest of the row
+// being zero (the previous call's spans are cleared first), so the arithmetic is the dense
+// path's bit for bit. Such models never take the fused row paths (fusedOk).
+MJH_HD int mjh_rowSpans(const mjhipModel* m) {
+  return m->opt.jacobian == mjhipJAC_SPARSE || (m->opt.jacobian == mjhipJAC_AUTO && m->nv >= 60);
+}
+
 MJH_HD int mjh_needConvex(const mjhipModel* m) {
   if (!mjhip_contactsEnabled(m)) return 0;
   for (int b1 = 0; b1 < m->nbody; b1++) {
@@ -303,6 +312,9 @@ struct SP {
   XSI(efc_type, efc_cap)              \
   XSI(efc_id, efc_cap)                \
   XSI(efc_state, efc_cap)             \
+  XSI(efc_lo, mjh_rowSpans(m)*efc_cap) /* sparse-mode models: each row's dof span */ \
+  XSI(efc_hi, mjh_rowSpans(m)*efc_cap) \
+  XSI(efc_spanrows, mjh_rowSpans(m))  /* rows whose spans hold values (next call clears) */ \
   XSI(efc_count, 4)                   /* nefc, ne, nf, nl */ \
   XSI(con_count, 1)                   /* ncon */ \
   XSI(con_dim, con_cap)               \
@@ -365,6 +377,7 @@ MJH_HD unsigned long long chainMask(const mjhipModel& m, int k) {
 // whether mj_inverseSkip(skipstage) can take the fused constraint path
 MJH_HD bool fusedOk(const mjhipModel& m, int skipstage) {
   return skipstage == mjhipSTAGE_NONE && !(m.opt.enableflags & mjhipENBL_INVDISCRETE) &&
+         !mjh_rowSpans(&m) &&
          m.nbody <= 64 && (m.ngeom <= 64 || !mjhip_contactsEnabled(&m)) &&
          !(m.opt.cone == mjhipCONE_ELLIPTIC && mjhip_contactsEnabled(&m));
 }
@@ -495,6 +508,30 @@ template <class A, class B> MJH_HD double dot(A a, B b, int n) {
   }
   double res = (r0 + r2) + (r1 + r3);
   int n_i = n - i;
+  if (n_i == 3) {
+    res += a[i]*b[i] + a[i+1]*b[i+1] + a[i+2]*b[i+2];
+  } else if (n_i == 2) {
+    res += a[i]*b[i] + a[i+1]*b[i+1];
+  } else if (n_i == 1) {
+    res += a[i]*b[i];
+  }
+  return res;
+}
+
+// dot(a, b, n) for an `a` that is zero outside [lo, hi): the same four partial sums by index
+// (the zero products skipped are exact no-ops) and the same dense tail, so the same bits
+template <class A, class B> MJH_HD double dotSpan(A a, B b, int lo, int hi, int n) {
+  const int iend = n - n % 4, top = hi < iend ? hi : iend;
+  double r0 = 0, r1 = 0, r2 = 0, r3 = 0;
+  for (int j = lo; j < top; j++) {
+    const int k = j & 3;
+    if (k == 0) r0 += a[j]*b[j];
+    else if (k == 1) r1 += a[j]*b[j];
+    else if (k == 2) r2 += a[j]*b[j];
+    else r3 += a[j]*b[j];
+  }
+  double res = (r0 + r2) + (r1 + r3);
+  const int i = iend, n_i = n - iend;
   if (n_i == 3) {
     res += a[i]*b[i] + a[i+1]*b[i+1] + a[i+2]*b[i+2];
   } else if (n_i == 2) {
@@ -4909,8 +4946,27 @@ MJH_HD void passive(const mjhipModel& m, const Lane<S>& d) {
 // registers and written to efc_count once at the end
 struct RowCount { int nefc = 0, ne = 0, nf = 0, nl = 0; };
 
+// row spans of sparse-mode models (mjh_rowSpans): record row r's span, or clear the spans
+// the previous call's rows hold (their entries outside are zero, so the rows are dense again)
+template <int S>
+MJH_HD void recordSpan(const Lane<S>& d, int r, int lo, int hi) {
+  d.efc_lo[r] = lo;
+  d.efc_hi[r] = hi;
+}
+template <int S>
+MJH_HD void clearSpans(const mjhipModel& m, const Lane<S>& d) {
+  const int n = d.efc_spanrows[0], nv = m.nv;
+  for (int r = 0; r < n; r++) {
+    SP<S> J = d.efc_J + (long)r*nv;
+    const int hi = d.efc_hi[r];
+    for (int j = d.efc_lo[r]; j < hi; j++) J[j] = 0;
+  }
+  d.efc_spanrows[0] = 0;
+}
+
 // mj_addConstraint :265-356 (dense): `size` rows of jac (strided scratch), contact rows are
-// never dropped as empty. Returns whether the rows were added.
+// never dropped as empty. Returns whether the rows were added. With row spans each row is
+// copied over its nonzero span only.
 template <int S>
 MJH_HD bool addConstraint(const mjhipModel& m, const Lane<S>& d, RowCount& rc, SP<S> jac,
                           const double* pos, const double* margin, double frictionloss,
@@ -4927,7 +4983,23 @@ MJH_HD bool addConstraint(const mjhipModel& m, const Lane<S>& d, RowCount& rc, S
     *status |= MJHIP_INST_CNSTRFULL;
     return false;
   }
-  copy(d.efc_J + nefc*nv, jac, size*nv);
+  if (mjh_rowSpans(&m)) {
+    for (int i = 0; i < size; i++) {
+      SP<S> src = jac + i*nv;
+      int lo = 0, hi = 0;
+      for (int j = 0; j < nv; j++) {
+        if (src[j]) {
+          if (hi == 0) lo = j;
+          hi = j + 1;
+        }
+      }
+      SP<S> dst = d.efc_J + (long)(nefc + i)*nv;
+      for (int j = lo; j < hi; j++) dst[j] = src[j];
+      recordSpan(d, nefc + i, lo, hi);
+    }
+  } else {
+    copy(d.efc_J + nefc*nv, jac, size*nv);
+  }
   for (int i = 0; i < size; i++) {
     d.efc_pos[nefc+i] = pos ? pos[i] : 0;
     d.efc_margin[nefc+i] = margin ? margin[i] : 0;
@@ -4989,7 +5061,23 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
     for (int k = 0; k < 5; k++) fri[k] = d.con_friction[5*i+k];
     const int rp = dim > 1 ? 3 : 1;
     SP<S> J = d.efc_J + nefc*nv;
-    for (int j = 0; j < nv; j++) {
+    // row spans: the dofs of the two bodies' chains lie in [jlo, jhi), the rest is zero
+    int jlo = 0, jhi = nv;
+    if (mjh_rowSpans(&m)) {
+      jlo = nv;
+      jhi = 0;
+      for (int e = 0; e < 2; e++) {
+        for (int b = e ? b2 : b1; b > 0; b = m.body_parentid[b]) {
+          if (!m.body_dofnum[b]) continue;
+          jlo = m.body_dofadr[b] < jlo ? m.body_dofadr[b] : jlo;
+          const int top = m.body_dofadr[b] + m.body_dofnum[b];
+          jhi = top > jhi ? top : jhi;
+        }
+      }
+      if (jlo > jhi) jlo = jhi = 0;
+      for (int r = 0; r < rows; r++) recordSpan(d, nefc + r, jlo, jhi);
+    }
+    for (int j = jlo; j < jhi; j++) {
       const int bj = m.dof_bodyid[j];
       const bool in1 = ancestorOrSelf(m, bj, b1), in2 = ancestorOrSelf(m, bj, b2);
       double cj[6] = {0, 0, 0, 0, 0, 0};
@@ -5801,6 +5889,9 @@ MJH_HD void instantiateEquality(const mjhipModel& m, const Lane<S>& d, RowCount&
       d.efc_type[r0+k] = CNSTR_EQUALITY;
       d.efc_id[r0+k] = i;
     }
+    if (!FUSED && mjh_rowSpans(&m)) {     // the rows are written whole
+      for (int k = 0; k < size; k++) recordSpan(d, r0 + k, 0, nv);
+    }
     rc.nefc += size;
     rc.ne += size;
     if constexpr (FUSED) {
@@ -5824,6 +5915,8 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   int nv = m.nv;
   RowCount rc;
   int dsbl = m.opt.disableflags;
+  const bool spans = !FUSED && mjh_rowSpans(&m);
+  if (spans) clearSpans(m, d);
   if (dsbl & mjhipDSBL_CONSTRAINT) {
     d.efc_count[0] = 0; d.efc_count[1] = 0; d.efc_count[2] = 0; d.efc_count[3] = 0;
     if constexpr (FUSED) zero(d.qfrc_constraint, nv);
@@ -5908,6 +6001,7 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   d.efc_count[0] = rc.nefc; d.efc_count[1] = rc.ne; d.efc_count[2] = rc.nf;
   d.efc_count[3] = rc.nl;
   const int nefc = rc.nefc;
+  if (spans) d.efc_spanrows[0] = nefc;
   if constexpr (FUSED) {
     constraintForce(m, d, nefc);
     return;
@@ -6027,8 +6121,10 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
 template <int S>
 MJH_HD void referenceConstraint(const mjhipModel& m, const Lane<S>& d) {
   int nefc = d.efc_count[0];
+  const bool spans = mjh_rowSpans(&m);
   for (int i = 0; i < nefc; i++) {
-    d.efc_vel[i] = dot(d.efc_J + i*m.nv, d.qvel, m.nv);
+    d.efc_vel[i] = spans ? dotSpan(d.efc_J + i*m.nv, d.qvel, d.efc_lo[i], d.efc_hi[i], m.nv)
+                         : dot(d.efc_J + i*m.nv, d.qvel, m.nv);
     d.efc_aref[i] = -d.efc_KBIP[4*i+1]*d.efc_vel[i]
                     -d.efc_KBIP[4*i]*d.efc_KBIP[4*i+2]*(d.efc_pos[i]-d.efc_margin[i]);
   }
@@ -6044,8 +6140,10 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
     return;
   }
   int ne = d.efc_count[1], nf = d.efc_count[2];
+  const bool spans = mjh_rowSpans(&m);
   for (int i = 0; i < nefc; i++) {
-    d.jar[i] = dot(d.efc_J + i*nv, d.qacc, nv) - d.efc_aref[i];
+    d.jar[i] = (spans ? dotSpan(d.efc_J + i*nv, d.qacc, d.efc_lo[i], d.efc_hi[i], nv)
+                      : dot(d.efc_J + i*nv, d.qacc, nv)) - d.efc_aref[i];
   }
   for (int i = 0; i < nefc; i++) d.efc_force[i] = -d.efc_D[i] * d.jar[i];
   for (int i = 0; i < nefc; i++) {
@@ -6097,7 +6195,18 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
       i += dim - 1;
     }
   }
-  mulMatTVec(d.qfrc_constraint, d.efc_J, d.efc_force, nefc, nv);
+  if (spans) {                          // mulMatTVec over each row's span
+    zero(d.qfrc_constraint, nv);
+    for (int r = 0; r < nefc; r++) {
+      const double tmp = d.efc_force[r];
+      if (!tmp) continue;
+      SP<S> J = d.efc_J + (long)r*nv;
+      const int hi = d.efc_hi[r];
+      for (int j = d.efc_lo[r]; j < hi; j++) d.qfrc_constraint[j] += J[j]*tmp;
+    }
+  } else {
+    mulMatTVec(d.qfrc_constraint, d.efc_J, d.efc_force, nefc, nv);
+  }
 }
 
 //---------------------------------- engine_inverse.c -----------------------------------------

@@ -180,6 +180,15 @@ __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __
   }
 }
 
+// rows uploaded whole into instance 0 (the single-instance drop-ins' put_rows): their row
+// spans (mjh_rowSpans models) cover every column; rows past them keep theirs for the next
+// clear
+__global__ void k_full_spans(mjhipModel m, Mirror mr, int nefc) {
+  Lane<64> d = lane_view(mr, 0, 0);
+  for (int r = 0; r < nefc; r++) mjh::recordSpan(d, r, 0, m.nv);
+  if (d.efc_spanrows[0] < nefc) d.efc_spanrows[0] = nefc;
+}
+
 // The stage-skip fall-back of mjhip_inverseFDBatch, decided on the device: when k_vaskip
 // found a centre with limit rows (fdflag[0]), the qvel/qacc perturbations [first, end) run the
 // full pipeline as well (their own position stage and rows), else the range is empty.
@@ -511,10 +520,9 @@ static unsigned long long model_signature(const mjhipModel* m) {
 
 // model features outside the device path: rejected at context creation (fail loudly)
 // Sparse-Jacobian models (mj_isSparse: jacobian=sparse, or auto with nv >= 60) are not one:
-// the reference's sparse path (compressed efc_J/ten_J rows over the bodies' dof chains,
-// mju_mulMatVecSparse/mju_mulMatTVecSparse) forms every entry with the same operations in
-// the same order as the dense path, whose extra terms are exact zeros, so the dense rows here
-// give its results (sparse Jacobians).
+// the reference's sparse path keeps compressed rows over the bodies' dof chains; here the
+// rows stay dense with per-row dof spans (mjh_rowSpans), which gives the sparse path's J'force
+// bit for bit and its J*v to the last bits (sparse Jacobians).
 static const char* unsupported(const mjhipModel* m) {
   if ((m->opt.enableflags & mjhipENBL_INVDISCRETE) && m->opt.integrator == mjhipINT_RK4) {
     return "mjENBL_INVDISCRETE with the RK4 integrator (an error in the reference)";
@@ -1812,6 +1820,14 @@ static int put_rows(mjhipContext* c, const mjhipModel* m, const mjhipData* d, in
                                                    (long)d->nefc * (w));
   MJHIP_DATA_EFC
 #undef XE
+  if (!rc && lo <= 1 && hi >= 1 && mjh_rowSpans(m)) {
+    hipLaunchKernelGGL(k_full_spans, dim3(1), dim3(1), 0, c->stream, c->dmodel, c->mirror,
+                       d->nefc);
+    if (hipGetLastError() != hipSuccess) {
+      set_error("k_full_spans launch");
+      rc = MJHIP_ERR_HIP;
+    }
+  }
 #define XC(type, name, w, stage) \
   if (!rc && stage >= lo && stage <= hi) rc = put0(c, c->mirror.name, (const type*)d->name, \
                                                    (long)d->ncon * (w));

@@ -50,6 +50,8 @@ def test_device_code_bitexact_sparse_models():
       np.testing.assert_array_equal(g, f)
       nefc = o.efc.nefc
       np.testing.assert_array_equal(k.field("efc_force")[:nefc], o.efc_field("efc_force"))
+      # rows written over their dof spans, the previous state's spans cleared: whole rows
+      np.testing.assert_array_equal(k.field("efc_J")[:nefc * m.nv], o.efc_field("efc_J"))
       rows += nefc
     assert rows > 10 * n
 
