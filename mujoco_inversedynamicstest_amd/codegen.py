@@ -97,6 +97,11 @@ NT_SV_MIN_B = 49152
 # experiment knob: stages whose re-reads of the mirror load as streaming (non-temporal)
 # loads (MJH_NT_LOAD), so they do not displace the lines a later stage re-reads
 NT_LOAD_STAGES = ()
+# stages whose mirror loads stream in the SV instantiation only (batches >= NT_SV_MIN_B, where
+# the va stage's re-read fields stream as well): 319.7 against 324.2 us per 65,536 in the A/B
+# (profiles/r04/experiments/nt_variants_3.log); below it, and in k_vaskip (whose loads of the
+# centre's fields are shared by 54 perturbations), they stay temporal
+NT_LOAD_SV_STAGES = ("va",)
 
 
 def _ll(st):
@@ -1364,6 +1369,10 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
     load = re.compile(r"= P_(\w+)\[(\d+)\*64\];")
     bodies = {st: (load.sub(lambda mt: f"= MJH_NT_LOAD(P_{mt.group(1)}[{mt.group(2)}*64]);", b)
                    if st in NT_LOAD_STAGES else b) for st, b in bodies.items()}
+    bodies = {st: (load.sub(lambda mt: f"= MJH_NT_LOAD_IF(SV, P_{mt.group(1)}[{mt.group(2)}*64]);",
+                            b)
+                   if st in NT_LOAD_SV_STAGES and st not in NT_LOAD_STAGES else b)
+              for st, b in bodies.items()}
   out = [f"// GENERATED by mujoco_inversedynamicstest_amd/codegen.py -- do not edit.",
          f"// model '{name}' (nq={m.nq} nv={m.nv} nbody={m.nbody}), hash {model_hash(m)}"]
   exact = exact_fp(m)
@@ -1492,6 +1501,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
     skip_body = skip_body.replace("const bool cflag = ec[0] != 0;",
                                   "const bool cflag = ecs[0] != 0;")
     skip_body = skip_body.replace("MJH_NT_STORE_IF(SV, ", "MJH_NT_STORE_IF(true, ")
+    skip_body = skip_body.replace("MJH_NT_LOAD_IF(SV, ", "MJH_NT_LOAD_IF(false, ")
     out.append(f"MJH_HD void fast_vaskip_{name}(const Mirror& mr, int blk, int lane, int sblk, "
                f"int slane, int B, const int* __restrict__ ecs, {_SIG['va'][0]}) {{\n"
                f"{skip_body}\n}}\n")

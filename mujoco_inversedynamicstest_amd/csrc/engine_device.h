@@ -92,6 +92,8 @@ static __device__ unsigned long long* mjh_tbuf = nullptr;
 #define MJH_NT_STORE(lv, v) ((lv) = (v))
 #define MJH_NT_LOAD(lv) (lv)
 #endif
+// a load that streams in one instantiation of a generated kernel (nt a template argument)
+#define MJH_NT_LOAD_IF(nt, lv) ((nt) ? MJH_NT_LOAD(lv) : (lv))
 // a store that streams in one instantiation of a generated kernel (nt a template argument)
 #define MJH_NT_STORE_IF(nt, lv, v)                                                      \
   do {                                                                                  \
