@@ -3423,7 +3423,11 @@ MJH_HD void colConvexHField(const mjhipModel& m, const Lane<S>& d, int g1, int g
   }
 }
 #if defined(__clang__)
+#if defined(MJH_CONTRACT_OFF)
+#pragma clang fp contract(off)           // a unit compiled without contraction throughout
+#else
 #pragma clang fp contract(fast)          // the default of this build again (see above)
+#endif
 #endif
 
 // mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)

@@ -65,7 +65,12 @@ def source(m) -> tuple[str, str]:
   body = codegen.generate(m, name, extern_c=True)
   # MJH_TBUF_EXTERN: the per-stage timer pointer gets C linkage, so the library finds it in
   # the code object by name (mjhip_contextLoadKernel) and points it at the context's timers
-  src = ('#include <hip/hip_runtime.h>\n#define MJH_TBUF_EXTERN 1\n'
+  # a model with native-solver pairs rounds every operation as the oracle does: the whole
+  # code object, engine_device.h's helpers included, without multiply-add contraction
+  # (MJH_CONTRACT_OFF keeps the header from re-enabling it after the solver's region)
+  exact = ('#define MJH_CONTRACT_OFF 1\n#pragma clang fp contract(off)\n'
+           if codegen.exact_fp(m) else '')
+  src = ('#include <hip/hip_runtime.h>\n#define MJH_TBUF_EXTERN 1\n' + exact +
          f'#include "{os.path.join(CSRC, "engine_device.h")}"\n' + body)
   return name, src
 

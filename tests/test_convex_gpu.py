@@ -1,19 +1,17 @@
 """GPU parity of the convex pairs (mjc_Convex on native GJK/EPA, mjc_PlaneConvex for
 ellipsoids): the HIP engine vs the CPU oracle on the same states.
 
-Counts, statuses and contact geoms are exact. GJK and EPA are iterative: they stop once the
-distance bounds are within ccd_tolerance, so their result is only defined to that tolerance.
-The reference algorithm itself is not stable to 1e-10 under a last-bit change of its inputs:
-for the five-body scene below, perturbing qpos by one ulp moves the oracle's own qfrc_inverse
-by up to ~3e-3 (relative) in about a quarter of the instances (a contact depth moves by
-O(ccd_tolerance), and a stiff contact turns that into force). The device's kinematics
-contract multiply-adds, which is such a perturbation. So the floating-point bar here is:
-  * every contact depth within 10 ccd_tolerance of the oracle's;
-  * every instance whose contacts (depth, position, frame) match the oracle's to 1e-12 meets
-    the north-star 1e-10;
-  * the instances that do not are no more frequent than the oracle's own under a one-ulp
-    input perturbation (measured in the test) -- the device adds no error of its own.
-The host build of the same device code equals the oracle bit for bit (test_convex_cpu.py).
+GJK and EPA are iterative and stop once the distance bounds are within ccd_tolerance, so a
+last-bit change of their inputs moves a depth by up to that much and a stiff contact turns it
+into force: perturbing qpos by one ulp moves the oracle's own qfrc_inverse by up to ~1e-2
+(relative) in about a quarter of the five-body scene's instances (measured below). The device
+therefore rounds every operation of these models as the oracle does: the constraint, generic
+and host-API units are compiled without multiply-add contraction throughout
+(__graft_entry__.UNIT_FLAGS, MJH_CONTRACT_OFF), and so are the run-time straight-line kernels
+of models with native-solver pairs (specialize.py). The bar is exact: every contact (geoms,
+depth, position, frame) equal to the oracle's bit for bit and every qfrc_inverse within the
+north-star 1e-10 (in practice equal). The bundled slider_crank kernel shares its unit with the
+headline kernel, which keeps contraction; its test holds the 1e-10 bar.
 """
 import numpy as np
 import pytest
@@ -133,6 +131,7 @@ def test_convex_pairs_parity():
         f"{err[same].max():.2e}; instances above {RTOL}: device {gpu_frac:.3f}, oracle under a "
         f"one-ulp qpos change {self_frac:.3f} (max {spread.max():.2e}); device max "
         f"{err.max():.2e}")
-  assert derr.max() <= 10 * m.opt["ccd_tolerance"]
-  assert err[same].max() <= RTOL
-  assert gpu_frac <= 1.5 * self_frac + 0.02
+  assert derr.max() == 0                      # every depth bit for bit
+  assert same.all()
+  assert err.max() <= RTOL
+  assert self_frac > 0.1                      # the scene is one where that matters

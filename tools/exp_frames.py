@@ -1,0 +1,69 @@
+"""Parity experiment (not part of the product): where do the device and the oracle first
+differ on the reference model's contact states? Runs the generic kernel (its unit compiled
+without contraction) and the oracle on tests/reference_model_states.py's states and reports,
+per instance, whether the kinematic frames (xpos, xquat, xmat, geom_xpos, geom_xmat) are bit
+for bit equal, against whether qfrc_inverse meets 1e-10.
+
+  python tools/exp_frames.py        # GPU box
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+FRAMES = ("xpos", "xquat", "xmat", "xipos", "geom_xpos", "geom_xmat")
+
+
+def main():
+  for spec in (False, True):
+    run(spec)
+
+
+def run(spec):
+  from mujoco_inversedynamicstest_amd import engine
+  from oracle.oracle import Oracle
+  import reference_model_states as R
+  m = R.model()
+  q, v, a = R.states(m, 96, seed=11)
+  B = len(q)
+  e = engine.InverseEngine(m, capacity=B, specialize=spec)
+  kern = e.fast_kernel or "generic"
+  f = e.inverse(q, v, a)
+  dev = {k: e.field(k, 0, B) for k in FRAMES}
+  dist = e.field("con_dist", 0, B)
+  e.close()
+  o = Oracle(m)
+  same_frames = np.zeros(B, bool)
+  same_dist = np.zeros(B, bool)
+  first = {}
+  ok = np.zeros(B, bool)
+  for i in range(B):
+    ref = o.inverse(q[i], v[i], a[i])
+    rd = o.contact_field("con_dist").ravel()
+    same_dist[i] = np.array_equal(dist[i, :rd.size], rd)
+    eq = True
+    for k in FRAMES:
+      r = np.asarray(getattr(o.d, k)).ravel()
+      d = dev[k][i, :r.size]
+      if not np.array_equal(d, r):
+        if eq:
+          first[k] = first.get(k, 0) + 1
+        eq = False
+    same_frames[i] = eq
+    ok[i] = np.abs(f[i] - ref).max() / max(1.0, np.abs(ref).max()) <= 1e-10
+  print(f"[{kern}] {B} states: contact depths bit-equal in {int(same_dist.sum())}; "
+        f"kinematic frames bit-equal in {int(same_frames.sum())}; "
+        f"qfrc_inverse within 1e-10 in {int(ok.sum())}")
+  print(f"  frames equal and qfrc within 1e-10: {int((same_frames & ok).sum())}; frames equal "
+        f"but qfrc off: {int((same_frames & ~ok).sum())}; frames differ and qfrc off: "
+        f"{int((~same_frames & ~ok).sum())}; frames differ but qfrc within: "
+        f"{int((~same_frames & ok).sum())}")
+  print(f"  first differing frame field per instance: {first}")
+
+
+if __name__ == "__main__":
+  main()
