@@ -1331,13 +1331,15 @@ _GEN = {"pos": lambda M, sf: _gen_pos(M, sf), "fac": lambda M, sf: _gen_fac(M, s
         "va": lambda M, sf: _gen_va(M, sf)}
 
 
-def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
+def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bool = False) -> str:
   """HIP source of the four stage kernels of model `m` (skipstage = mjSTAGE_NONE).
 
   Also emits `fast_body_<name>`, which runs the four stage bodies for one instance in
   order (the host harness's entry), and `launch_fast_<name>`, which launches the kernels.
   store_fields: optional set of mirror fields to store (default: all); used only by
   performance experiments (tools/exp_bounds.py) to separate compute from store costs.
+  shared: the launch functions get external linkage (a model compiled in another
+  translation unit than the registry, generate_registries).
   extern_c: give k_all_<name> C linkage (a run-time code object, specialize.py, whose
   kernel mjhip_contextLoadKernel looks up by name).
   """
@@ -1517,12 +1519,12 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False) -> str:
 {flag}  fast_vaskip_{name}(mr, (int)(gi >> 6), (int)(gi & 63), (int)(si >> 6), (int)(si & 63), B,
                     ecs, nullptr, nullptr, efc_count, qo_lds, nullptr);
 }}
-static void launch_vaskip_{name}(hipStream_t s, const Mirror& mr, int B, int off, int per,
+{"" if shared else "static "}void launch_vaskip_{name}(hipStream_t s, const Mirror& mr, int B, int off, int per,
                                 int sstride, int* efc_count, int* needfull) {{
   hipLaunchKernelGGL(k_vaskip_{name}, dim3((B - off + 63) / 64), dim3(64), 0, s, mr, B, off,
                      per, sstride, efc_count, needfull);
 }}""")
-  out.append(f"""static void launch_fast_{name}(dim3 g, dim3 b, hipStream_t s, const Mirror& mr,
+  out.append(f"""{"" if shared else "static "}void launch_fast_{name}(dim3 g, dim3 b, hipStream_t s, const Mirror& mr,
     int B, const double* qpos_in, const double* qvel_in, const double* qacc_in, double* qfrc_out,
     int* status, int* worklist, int* worklist_count, int* worklist_next, int* efc_count,
     const int* range) {{""")
@@ -1562,6 +1564,36 @@ def source_hash(m, name: str) -> str:
 def hot_kernels(name: str) -> list:
   """Names of the kernels one fast-path launch of model `name` runs (profiles, bench)."""
   return [f"k_all_{name}"] if FUSE else [f"k_{st}_{name}" for st in STAGES]
+
+
+def generate_registries(entries) -> tuple:
+  """entries: list of (name, model). Returns (gen_fast.inc, gen_fast_exact.inc): the models
+  with native-solver pairs (exact_fp) go to a translation unit of their own, compiled without
+  multiply-add contraction throughout (gen_fast_exact.hip) so they round every operation as
+  the oracle does; the others, and the registry of all, to gen_fast.inc."""
+  head = ["// GENERATED by mujoco_inversedynamicstest_amd/codegen.py (build()) -- do not edit."]
+  main = head + ["// Straight-line mj_inverse kernels for the bundled models + their signatures.", ""]
+  exact = head + ["// Straight-line kernels of the bundled models with native-solver pairs.", ""]
+  reg = []
+  for name, m in entries:
+    vaskip = constraint_mode(m) in ("none", "list")
+    if exact_fp(m):
+      exact.append(generate(m, name, shared=True))
+      main.append(f"void launch_fast_{name}(dim3, dim3, hipStream_t, const Mirror&, int, "
+                  "const double*, const double*, const double*, double*, int*, int*, int*, "
+                  "int*, int*, const int*);")
+      if vaskip:
+        main.append(f"void launch_vaskip_{name}(hipStream_t, const Mirror&, int, int, int, int, "
+                    "int*, int*);")
+    else:
+      main.append(generate(m, name))
+    reg.append(f'  {{0x{fields.model_signature(m):016x}ull, launch_fast_{name}, "{name}", '
+               f'{CONSTRAINT_MODES[constraint_mode(m)]}, '
+               f'{"launch_vaskip_" + name if vaskip else "nullptr"}}},')
+  main.append("static const FastKernelEntry g_fast_kernels[] = {")
+  main.extend(reg)
+  main.append("  {0ull, nullptr, nullptr, 0, nullptr}};")
+  return "\n".join(main) + "\n", "\n".join(exact) + "\n"
 
 
 def generate_registry(entries) -> str:

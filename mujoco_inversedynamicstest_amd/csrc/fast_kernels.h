@@ -24,5 +24,6 @@ struct FastKernelEntry {
 // the bundled models' kernels (gen_fast.hip), terminated by an entry with launch = nullptr
 const FastKernelEntry* mjhip_fastKernels();
 int mjhip_genSetTimerBuf(unsigned long long* p);   // gen_fast.hip's mjh_tbuf
+int mjhip_genExactSetTimerBuf(unsigned long long* p);   // gen_fast_exact.hip's
 
 #endif  // MJHIP_FAST_KERNELS_H_

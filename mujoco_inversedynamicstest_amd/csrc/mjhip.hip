@@ -1076,7 +1076,8 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
 static int timers_attach(mjhipContext* c, unsigned long long* p) {
   HIPCHECK(hipStreamSynchronize(c->stream));
   HIPCHECK(hipMemcpyToSymbol(HIP_SYMBOL(mjh_tbuf), &p, sizeof(p)));
-  if (mjhip_genSetTimerBuf(p) || mjhip_setTimerBufConstraint(p) ||
+  if (mjhip_genSetTimerBuf(p) || mjhip_genExactSetTimerBuf(p) ||
+      mjhip_setTimerBufConstraint(p) ||
       mjhip_setTimerBufInverse(p)) {
     set_error("setting the kernel units' timer pointers failed");
     return MJHIP_ERR_HIP;
