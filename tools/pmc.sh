@@ -10,7 +10,7 @@ for group in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY" "F
              "WRITE_SIZE"; do
   n=$((n+1))
   timeout -k 10 240 rocprofv3 --kernel-trace --pmc $group -d gpurun_out/pmc_$n -o pmc \
-    --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu \
+    --output-format csv -- python bench.py ${PMC_ARGS:---steps 3 --warmup 1 --no-cpu} \
     > gpurun_out/pmc_$n.log 2>&1
   rc=$?
   echo "pmc pass $n ($group) rc=$rc"
