@@ -157,6 +157,9 @@ def main():
                   help="instances in the CPU-baseline sample (rank 0, N=1 only; default "
                        "150k per thread, about 2-3 s of CPU work per thread)")
   ap.add_argument("--no-cpu", action="store_true")
+  ap.add_argument("--own-stream", action="store_true",
+                  help="config 5: keep the context's own stream (ordered with torch's by "
+                       "events around every call) instead of running it on torch's stream")
   ap.add_argument("--config-batch", type=int, default=None,
                   help="batch for --config 4 (default 4096) or base states for 5 (1024)")
   ap.add_argument("--config", type=int, default=2, choices=(2, 4, 5),
@@ -368,6 +371,9 @@ def config5(args):
   first, count = parallel.shard(nb * world, world, rank)
   q, v, a = sample_states(m, count, first=first)
   eng = engine.InverseEngine(m, capacity=count * P, device=local)
+  if not args.own_stream:
+    # the context runs on torch's stream: no cross-stream event waits around each call
+    eng.set_stream(torch.cuda.current_stream(dev).cuda_stream)
   tq, tv, ta = (torch.from_numpy(x).to(dev) for x in (q, v, a))
   mk = lambda: torch.empty((count, m.nv, m.nv), dtype=torch.float64, device=dev)
   out = (mk(), mk(), mk(), None)

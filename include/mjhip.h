@@ -243,6 +243,16 @@ typedef struct mjhipData_ {
 #define XC(type, name, w, stage) type* name;
   MJHIP_DATA_CONTACT
 #undef XC
+  /* Compressed Jacobians of sparse-mode models (mj_isSparse: jacobian="sparse", or "auto" with
+   * nv >= 60, engine_core_constraint.c:99-106). ten_J (ntendon x nv doubles) and efc_J
+   * (efc_capacity x nv doubles) then hold compressed rows as the reference's mjData does
+   * (mj_tendon engine_core_smooth.c:651-860; mj_addConstraint engine_core_constraint.c:265-356),
+   * described by the arrays below; efc_JT is the transpose (mju_transposeSparse, :2083-2104).
+   * Dense-mode models leave them untouched (they may be NULL). */
+  int nJ;                   /* nonzeros of efc_J (mjData nJ) */
+#define XJ(type, name, dim) type* name;
+  MJHIP_DATA_SPARSE
+#undef XJ
 } mjhipData;
 
 /*---------------------------- status codes of the batch API ------------------------------*/

@@ -374,4 +374,19 @@
   XC(int,    con_exclude,       1, 1) \
   XC(int,    con_efc_address,   1, 1)
 
+/* Sparse structures of sparse-Jacobian models (mjData ten_J_*, efc_J_*, efc_JT*; mjxmacro.h
+ * MJDATA_POINTERS and MJDATA_ARENA_POINTERS_SOLVER): XJ(type, name, dim) with dim one of
+ * ntendon, ntendon_nv (ntendon x nv), efc (efc_capacity), efc_nv (efc_capacity x nv), nv. */
+#define MJHIP_DATA_SPARSE \
+  XJ(int,    ten_J_rownnz,      ntendon)    \
+  XJ(int,    ten_J_rowadr,      ntendon)    \
+  XJ(int,    ten_J_colind,      ntendon_nv) \
+  XJ(int,    efc_J_rownnz,      efc)        \
+  XJ(int,    efc_J_rowadr,      efc)        \
+  XJ(int,    efc_J_colind,      efc_nv)     \
+  XJ(mjtNum, efc_JT,            efc_nv)     \
+  XJ(int,    efc_JT_rownnz,     nv)         \
+  XJ(int,    efc_JT_rowadr,     nv)         \
+  XJ(int,    efc_JT_colind,     efc_nv)
+
 #endif  /* MJHIP_FIELDS_H_ */

@@ -19,6 +19,12 @@
  * start, then every MJDATA_ARENA_POINTERS_SOLVER array of the counted size, tendon_efcadr
  * included (rules of engine_core_constraint.c:668-671, :811-814, :949-952).
  *
+ * Sparse-Jacobian models (mj_isSparse, engine_core_constraint.c:99-106: jacobian="sparse",
+ * or "auto" with nv >= 60) get the reference's compressed layout: ten_J and its
+ * rownnz/rowadr/colind in place in mjData, and in the arena efc_J/efc_JT over nJ entries with
+ * their rownnz/rowadr/colind, and the row supernodes mj_makeConstraint derives from them
+ * (:2083-2104, mju_superSparse engine_util_sparse.c:520-550, restated below).
+ *
  * Models are checked for features the device path does not implement and which mjhipModel
  * does not carry (explicit contact pairs, flexes, plugins):
  * such a model is an mju_error, never a silently different result.
@@ -44,12 +50,6 @@ static const char* adapter_unsupported(const mjModel* m) {
   if (m->npair) return "explicit contact pairs (<contact><pair>)";
   if (m->nflex) return "flexes";
   if (m->nplugin) return "plugins";
-  /* mj_isSparse (engine_core_constraint.c:96-103): the arena would hold compressed efc_J
-   * rows over the dof chains, which this adapter does not lay out (the library computes
-   * such models; its batched and single-instance APIs return dense rows) */
-  if (m->opt.jacobian == mjJAC_SPARSE || (m->opt.jacobian == mjJAC_AUTO && m->nv >= 60)) {
-    return "sparse Jacobians (the compressed efc_J arena layout)";
-  }
   for (int i = 0; i < m->nu; i++) {
     /* mjd_actuator_vel reads mjData.act for these (engine_derivative.c:855-863) */
     if (m->actuator_dyntype[i] != mjDYN_NONE && m->actuator_gaintype[i] == mjGAIN_AFFINE &&
@@ -106,6 +106,26 @@ static void model_view(const mjModel* m, const mjData* d, mjhipModel* hm) {
 
 /*------------------------------------------------------------------ data ---------------*/
 
+/* mj_isSparse (engine_core_constraint.c:99-106) */
+static int is_sparse(const mjModel* m) {
+  return m->opt.jacobian == mjJAC_SPARSE || (m->opt.jacobian == mjJAC_AUTO && m->nv >= 60);
+}
+
+/* mju_superSparse (engine_util_sparse.c:520-550): rowsuper[r] = how many following rows share
+ * row r's pattern */
+static void super_sparse(int nr, int* rowsuper, const int* rownnz, const int* rowadr,
+                         const int* colind) {
+  if (!nr) return;
+  for (int r = 0; r < nr-1; r++) {
+    rowsuper[r] = rownnz[r] == rownnz[r+1] &&
+                  !memcmp(colind + rowadr[r], colind + rowadr[r+1], rownnz[r]*sizeof(int));
+  }
+  rowsuper[nr-1] = 0;
+  for (int r = nr-2; r >= 0; r--) {
+    if (rowsuper[r]) rowsuper[r] += rowsuper[r+1];
+  }
+}
+
 /* per-call view of d plus the staging it needs */
 typedef struct {
   mjhipData hd;
@@ -121,6 +141,17 @@ static void data_fields(mjData* d, mjhipData* hd) {
   MJHIP_DATA_FORWARD
   MJHIP_DATA_SENSOR_AUX
 #undef XD
+  /* the tendon Jacobian's compressed structure (used by sparse-mode models) */
+  hd->ten_J_rownnz = d->ten_J_rownnz;
+  hd->ten_J_rowadr = d->ten_J_rowadr;
+  hd->ten_J_colind = d->ten_J_colind;
+}
+
+/* bytes per row of the efc arrays of MJHIP_DATA_SPARSE (rows x 1 or rows x nv) plus the two
+ * nv-sized ones, for a sparse-mode model's staging */
+static size_t sparse_bytes(const mjModel* m, int rows) {
+  return sizeof(int) * (size_t)rows * (2 + 2*(size_t)m->nv) + sizeof(mjtNum) * (size_t)rows *
+         m->nv + sizeof(int) * 2 * (size_t)m->nv + 8*8;
 }
 
 /* bytes of one row (XE) / one contact (XC) over every array */
@@ -191,7 +222,8 @@ static void contact_from_soa(const mjhipData* hd, int i, mjContact* c) {
 static void* stage_alloc(const mjModel* m, mjhipData* hd, int rows, int cons, int efc,
                          int con) {
   size_t total = (efc ? row_bytes(m) * (size_t)rows : 0) +
-                 (con ? contact_bytes() * (size_t)cons : 0) + 8*64;
+                 (con ? contact_bytes() * (size_t)cons : 0) + 8*64 +
+                 (efc && is_sparse(m) ? sparse_bytes(m, rows) : 0);
   char* p = (char*)malloc(total);
   if (!p) mju_error("mjhip: out of host memory for %d constraint rows", rows);
   char* q = p;
@@ -203,6 +235,18 @@ static void* stage_alloc(const mjModel* m, mjhipData* hd, int rows, int cons, in
     hd->name = (type*)q; q += (sizeof(type) * (size_t)(w) * rows + 7) & ~(size_t)7;
     MJHIP_DATA_EFC
 #undef XE
+    if (is_sparse(m)) {
+      const size_t rn = (size_t)rows * m->nv;
+#define CARVE(name, type, n) hd->name = (type*)q; q += (sizeof(type) * (n) + 7) & ~(size_t)7;
+      CARVE(efc_J_rownnz, int, (size_t)rows)
+      CARVE(efc_J_rowadr, int, (size_t)rows)
+      CARVE(efc_J_colind, int, rn)
+      CARVE(efc_JT, mjtNum, rn)
+      CARVE(efc_JT_rownnz, int, (size_t)m->nv)
+      CARVE(efc_JT_rowadr, int, (size_t)m->nv)
+      CARVE(efc_JT_colind, int, rn)
+#undef CARVE
+    }
   }
   if (con) {
     hd->con_capacity = cons;
@@ -230,6 +274,15 @@ static void view_existing_rows(const mjModel* m, mjData* d, DataView* v) {
 #define XE(type, name, w, stage) hd->name = d->name;
   MJHIP_DATA_EFC
 #undef XE
+  /* compressed rows of a sparse-mode model, in place in the arena */
+  hd->nJ = d->nJ;
+  hd->efc_J_rownnz = d->efc_J_rownnz;
+  hd->efc_J_rowadr = d->efc_J_rowadr;
+  hd->efc_J_colind = d->efc_J_colind;
+  hd->efc_JT = d->efc_JT;
+  hd->efc_JT_rownnz = d->efc_JT_rownnz;
+  hd->efc_JT_rowadr = d->efc_JT_rowadr;
+  hd->efc_JT_colind = d->efc_JT_colind;
   v->stage = d->ncon ? stage_alloc(m, hd, 0, d->ncon, 0, 1) : NULL;
   if (d->ncon) contacts_to_soa(d, hd);
 }
@@ -280,8 +333,8 @@ static void arena_from_rows(const mjModel* m, mjData* d, const mjhipData* hd) {
   /* mj_makeConstraint (engine_core_constraint.c:2005-2075): sizes, then arenaAllocEfc
    * (:50-80) with the dense Jacobian */
   if (m->opt.disableflags & mjDSBL_CONSTRAINT) return;
-  const int nefc = hd->nefc;
-  d->nJ = nefc * m->nv;
+  const int nefc = hd->nefc, sparse = is_sparse(m);
+  d->nJ = sparse ? hd->nJ : nefc * m->nv;
   d->nefc = nefc;
   d->parena = d->ncon * sizeof(mjContact);
   /* the device made rows for every contact: with contacts dropped they are not the rows the
@@ -309,11 +362,26 @@ static void arena_from_rows(const mjModel* m, mjData* d, const mjhipData* hd) {
   d->ne = hd->ne;
   d->nf = hd->nf;
   d->nl = hd->nl;
-#define XE(type, name, w, stage) memcpy(d->name, hd->name, sizeof(type) * (size_t)(w) * nefc);
+#define XE(type, name, w, stage) \
+  memcpy(d->name, hd->name, sparse && !strcmp(#name, "efc_J") ? sizeof(type) * (size_t)d->nJ \
+                                                                : sizeof(type) * (size_t)(w) * nefc);
   MJHIP_DATA_EFC
 #undef XE
 #undef MJ_M
 #define MJ_M(n) n
+  if (sparse && nefc) {
+    /* :2083-2104: the transpose, the rows' and the transpose's supernodes */
+    memcpy(d->efc_J_rownnz, hd->efc_J_rownnz, sizeof(int) * nefc);
+    memcpy(d->efc_J_rowadr, hd->efc_J_rowadr, sizeof(int) * nefc);
+    memcpy(d->efc_J_colind, hd->efc_J_colind, sizeof(int) * d->nJ);
+    memcpy(d->efc_JT, hd->efc_JT, sizeof(mjtNum) * d->nJ);
+    memcpy(d->efc_JT_rownnz, hd->efc_JT_rownnz, sizeof(int) * m->nv);
+    memcpy(d->efc_JT_rowadr, hd->efc_JT_rowadr, sizeof(int) * m->nv);
+    memcpy(d->efc_JT_colind, hd->efc_JT_colind, sizeof(int) * d->nJ);
+    super_sparse(nefc, d->efc_J_rowsuper, d->efc_J_rownnz, d->efc_J_rowadr, d->efc_J_colind);
+    super_sparse(m->nv, d->efc_JT_rowsuper, d->efc_JT_rownnz, d->efc_JT_rowadr,
+                 d->efc_JT_colind);
+  }
   d->maxuse_con = d->maxuse_con > d->ncon ? d->maxuse_con : d->ncon;
   d->maxuse_efc = d->maxuse_efc > nefc ? d->maxuse_efc : nefc;
   /* tendon_efcadr: tendon equalities record the equality id, tendon friction and limit rows

@@ -150,6 +150,9 @@ def fast_path_supported(m) -> str | None:
     # straight-line code grows with the tree; large models (the reference's sparse-Jacobian
     # range) run the generic kernel
     return "large model (nv >= 60)"
+  if fields.is_sparse(m):
+    # compressed constraint rows (mj_isSparse) are built by the generic kernel only
+    return "sparse-Jacobian model (jacobian=\"sparse\")"
   if m.opt["enableflags"] & (1 << 3):
     if int(m.opt["integrator"]) == 1:
       return "INVDISCRETE with RK4 (an error in the reference)"

@@ -142,13 +142,52 @@ MJH_HD int mjh_needSliderCrank(const mjhipModel* m) {
 // 1 when a candidate geom pair of the model runs the native GJK/EPA solver (mjc_Convex,
 // mjc_ConvexHField): its
 // per-instance scratch (mjh::CcdMem) is allocated, 6 ccd_iterations + 6 faces
-// mj_isSparse (engine_core_constraint.c:96-103): the reference keeps compressed constraint
-// rows. Here the rows stay dense, but each row records its dof span (efc_lo, efc_hi): the
-// producers write and the J*v / J'force consumers visit only the span, the rest of the row
-// being zero (the previous call's spans are cleared first), so the arithmetic is the dense
-// path's bit for bit. Such models never take the fused row paths (fusedOk).
-MJH_HD int mjh_rowSpans(const mjhipModel* m) {
+// mj_isSparse (engine_core_constraint.c:99-106): jacobian="sparse", or "auto" with nv >= 60.
+// Such models keep the reference's compressed rows: ten_J (mj_tendon, engine_core_smooth.c:
+// 651-860) and efc_J (mj_addConstraint :265-356) hold each row's values over its dof chain,
+// with rownnz/rowadr/colind per instance, efc_JT is their transpose (:2083-2104), and J*v and
+// J'*f are mju_mulMatVecSparse over the rows of J and JT (:361-377, :426-442). They run the
+// generic kernel only (never the fused or cooperative row paths, nor the straight-line kernels).
+MJH_HD int mjh_isSparse(const mjhipModel* m) {
   return m->opt.jacobian == mjhipJAC_SPARSE || (m->opt.jacobian == mjhipJAC_AUTO && m->nv >= 60);
+}
+
+// dofs of body b and its ancestors (the length of mj_bodyChain, engine_support.c:341-381)
+MJH_HD int mjh_chainLength(const mjhipModel* m, int b) {
+  int n = 0;
+  for (; b > 0; b = m->body_parentid[b]) n += m->body_dofnum[b];
+  return n;
+}
+
+// an upper bound on the nonzeros of one compressed row of a sparse-mode model: a contact or
+// connect/weld row spans two bodies' chains, a tendon row its path's chains (two tendons for a
+// tendon coupling), a ball-joint limit 3 dofs (host only: sizes the per-instance CSR arrays)
+MJH_HD int mjh_rowNnzMax(const mjhipModel* m) {
+  int chain = 0, ten = 0;
+  for (int b = 1; b < m->nbody; b++) {
+    const int c = mjh_chainLength(m, b);
+    chain = c > chain ? c : chain;
+  }
+  for (int i = 0; i < m->ntendon; i++) {
+    int t = 0;
+    for (int w = m->tendon_adr[i]; w < m->tendon_adr[i] + m->tendon_num[i]; w++) {
+      const int type = m->wrap_type[w], obj = m->wrap_objid[w];
+      if (type == mjhipWRAP_JOINT) t += 1;
+      else if (type == mjhipWRAP_SITE) t += mjh_chainLength(m, m->site_bodyid[obj]);
+      else if (type == mjhipWRAP_SPHERE || type == mjhipWRAP_CYLINDER)
+        t += mjh_chainLength(m, m->geom_bodyid[obj]);
+    }
+    ten = t > ten ? t : ten;
+  }
+  int r = 2*chain;
+  r = 2*ten > r ? 2*ten : r;
+  r = r < 3 ? 3 : r;
+  return r < m->nv ? r : m->nv;
+}
+
+// compressed-row capacity (values) of one instance: efc_cap rows of at most mjh_rowNnzMax
+MJH_HD long mjh_njCap(const mjhipModel* m, int efc_cap) {
+  return mjh_isSparse(m) ? (long)efc_cap * mjh_rowNnzMax(m) : 0;
 }
 
 MJH_HD int mjh_needConvex(const mjhipModel* m) {
@@ -287,7 +326,9 @@ struct SP {
   XSC(Dcfrc, mjh_implicit(m)*6*m->nB) \
   XSC(Dcdofdot, mjh_implicit(m)*6*m->nD) \
   XSC(Dtmp, mjh_qDerivStored(m)*6*nv) \
-  XSC(efc_J, efc_cap*nv)              \
+  XSC(efc_J, mjh_isSparse(m) ? mjh_njCap(m, efc_cap) : (long)efc_cap*nv) \
+  XSC(efc_JT, mjh_njCap(m, efc_cap))   /* sparse mode: the rows' transpose */ \
+  XSC(sparse_buf, mjh_isSparse(m)*nv)  /* sparse mode: mju_combineSparse's buffer */ \
   XSC(efc_pos, efc_cap)               \
   XSC(efc_margin, efc_cap)            \
   XSC(efc_frictionloss, efc_cap)      \
@@ -314,9 +355,17 @@ struct SP {
   XSI(efc_type, efc_cap)              \
   XSI(efc_id, efc_cap)                \
   XSI(efc_state, efc_cap)             \
-  XSI(efc_lo, mjh_rowSpans(m)*efc_cap) /* sparse-mode models: each row's dof span */ \
-  XSI(efc_hi, mjh_rowSpans(m)*efc_cap) \
-  XSI(efc_spanrows, mjh_rowSpans(m))  /* rows whose spans hold values (next call clears) */ \
+  XSI(efc_J_rownnz, mjh_isSparse(m)*efc_cap)   /* sparse mode: compressed rows */ \
+  XSI(efc_J_rowadr, mjh_isSparse(m)*efc_cap)   \
+  XSI(efc_J_colind, mjh_njCap(m, efc_cap))      \
+  XSI(efc_JT_rownnz, mjh_isSparse(m)*nv)         \
+  XSI(efc_JT_rowadr, mjh_isSparse(m)*nv)         \
+  XSI(efc_JT_colind, mjh_njCap(m, efc_cap))     \
+  XSI(ten_J_rownnz, mjh_isSparse(m)*m->ntendon) \
+  XSI(ten_J_rowadr, mjh_isSparse(m)*m->ntendon) \
+  XSI(ten_J_colind, mjh_isSparse(m)*m->ntendon*nv) \
+  XSI(chainbuf, mjh_isSparse(m)*3*nv)  /* sparse mode: two chains and a merge buffer */ \
+  XSI(nJ, mjh_isSparse(m))            /* sparse mode: nonzeros of efc_J */ \
   XSI(efc_count, 4)                   /* nefc, ne, nf, nl */ \
   XSI(con_count, 1)                   /* ncon */ \
   XSI(con_dim, con_cap)               \
@@ -339,6 +388,7 @@ struct Lane {
 #undef XSI
   int efc_cap;
   int con_cap;
+  long nj_cap;                               // sparse mode: compressed-row capacity (values)
   // fused constraint path only (nbody <= 64): chain[k] has bit b set when body b is body k
   // or one of its ancestors (on the device a per-block LDS table, chainMasks)
   const unsigned long long* chain;
@@ -379,7 +429,7 @@ MJH_HD unsigned long long chainMask(const mjhipModel& m, int k) {
 // whether mj_inverseSkip(skipstage) can take the fused constraint path
 MJH_HD bool fusedOk(const mjhipModel& m, int skipstage) {
   return skipstage == mjhipSTAGE_NONE && !(m.opt.enableflags & mjhipENBL_INVDISCRETE) &&
-         !mjh_rowSpans(&m) &&
+         !mjh_isSparse(&m) &&
          m.nbody <= 64 && (m.ngeom <= 64 || !mjhip_contactsEnabled(&m)) &&
          !(m.opt.cone == mjhipCONE_ELLIPTIC && mjhip_contactsEnabled(&m));
 }
@@ -520,30 +570,6 @@ template <class A, class B> MJH_HD double dot(A a, B b, int n) {
   return res;
 }
 
-// dot(a, b, n) for an `a` that is zero outside [lo, hi): the same four partial sums by index
-// (the zero products skipped are exact no-ops) and the same dense tail, so the same bits
-template <class A, class B> MJH_HD double dotSpan(A a, B b, int lo, int hi, int n) {
-  const int iend = n - n % 4, top = hi < iend ? hi : iend;
-  double r0 = 0, r1 = 0, r2 = 0, r3 = 0;
-  for (int j = lo; j < top; j++) {
-    const int k = j & 3;
-    if (k == 0) r0 += a[j]*b[j];
-    else if (k == 1) r1 += a[j]*b[j];
-    else if (k == 2) r2 += a[j]*b[j];
-    else r3 += a[j]*b[j];
-  }
-  double res = (r0 + r2) + (r1 + r3);
-  const int i = iend, n_i = n - iend;
-  if (n_i == 3) {
-    res += a[i]*b[i] + a[i+1]*b[i+1] + a[i+2]*b[i+2];
-  } else if (n_i == 2) {
-    res += a[i]*b[i] + a[i+1]*b[i+1];
-  } else if (n_i == 1) {
-    res += a[i]*b[i];
-  }
-  return res;
-}
-
 // mju_dot for n = 6 (the spatial-vector case): ((p0+p2)+(p1+p3)) + (p4+p5)
 template <class A, class B> MJH_HD double dot6(A a, B b) {
   double r0 = a[0]*b[0], r1 = a[1]*b[1], r2 = a[2]*b[2], r3 = a[3]*b[3];
@@ -561,8 +587,9 @@ template <class R, class M, class V> MJH_HD void mulMatTVec(R res, M mat, V vec,
   }
 }
 
-// engine_util_sparse.h:115-160 (scalar branch)
-template <class V1, class V2> MJH_HD double dotSparse(V1 v1, V2 v2, int nnz1, const int* ind1) {
+// engine_util_sparse.h:115-160 (scalar branch; the AVX branch, engine_util_sparse_avx.h:34-
+// 105, groups the products the same way)
+template <class V1, class V2, class I> MJH_HD double dotSparse(V1 v1, V2 v2, int nnz1, I ind1) {
   int i = 0, n_4 = nnz1 - 4;
   double r0 = 0, r1 = 0, r2 = 0, r3 = 0;
   for (; i <= n_4; i += 4) {
@@ -4290,21 +4317,35 @@ MJH_HD double wrapGeom(double wpnt[6], const double x0[3], const double x1[3],
 }
 
 // mj_tendon :651-860 (fixed tendons; spatial tendons through sites, pulleys and wrapping
-// spheres/cylinders; dense ten_J)
+// spheres/cylinders); dense ten_J, or the compressed rows of a sparse-mode model (:668-719,
+// :801-819: each joint / path segment merged into the row by mju_combineSparse)
 template <int S>
 MJH_HD void tendon(const mjhipModel& m, const Lane<S>& d) {
   int nv = m.nv, nten = m.ntendon;
   if (!nten) return;
+  const bool sparse = mjh_isSparse(&m);
   zero(d.ten_length, nten);
-  zero(d.ten_J, nten*nv);
+  if (sparse) {
+    for (int i = 0; i < nten; i++) d.ten_J_rownnz[i] = 0;
+  } else {
+    zero(d.ten_J, nten*nv);
+  }
   for (int i = 0; i < nten; i++) {
     int adr = m.tendon_adr[i];
     int num = m.tendon_num[i];
+    const int radr = sparse ? (i ? d.ten_J_rowadr[i-1] + d.ten_J_rownnz[i-1] : 0) : 0;
+    if (sparse) d.ten_J_rowadr[i] = radr;
     if (m.wrap_type[adr] == mjhipWRAP_JOINT) {
       for (int j = 0; j < num; j++) {
         int k = m.wrap_objid[adr+j];
         d.ten_length[i] += m.wrap_prm[adr+j] * d.qpos[m.jnt_qposadr[k]];
-        d.ten_J[i*nv + m.jnt_dofadr[k]] = m.wrap_prm[adr+j];
+        if (sparse) {
+          d.ten_J_rownnz[i] = combineSparse(d.ten_J + radr, m.wrap_prm + adr + j, 1.0, 1.0,
+                                            d.ten_J_rownnz[i], 1, d.ten_J_colind + radr,
+                                            m.jnt_dofadr + k, d.sparse_buf, d.chainbuf + 2*nv);
+        } else {
+          d.ten_J[i*nv + m.jnt_dofadr[k]] = m.wrap_prm[adr+j];
+        }
       }
       continue;
     }
@@ -4365,6 +4406,25 @@ MJH_HD void tendon(const mjhipModel& m, const Lane<S>& d) {
         jacInto(m, d, j1, d.jacr, wpnt + 3*k, wbody[k]);
         jacInto(m, d, j2, d.jacr, wpnt + 3*k + 3, wbody[k+1]);
         const double inv = 1/divisor;
+        if (sparse) {
+          // mj_jacDifPair over the merged chain (its entries are the dense Jacobians' at the
+          // chain's dofs), mju_mulMatTVec with dif, then combined into the row
+          SP<S, int> chain = d.chainbuf;
+          const int NV = mergeChain(m, chain, wbody[k], wbody[k+1]);
+          if (!NV) continue;
+          for (int p = 0; p < NV; p++) {
+            const int c = chain[p];
+            double t = 0;
+            for (int r = 0; r < 3; r++) {
+              if (dif[r]) t += (j2[r*nv + c] - j1[r*nv + c])*dif[r];
+            }
+            d.jacp[p] = t;
+          }
+          d.ten_J_rownnz[i] = combineSparse(d.ten_J + radr, d.jacp, 1.0, inv, d.ten_J_rownnz[i],
+                                            NV, d.ten_J_colind + radr, chain, d.sparse_buf,
+                                            d.chainbuf + 2*nv);
+          continue;
+        }
         for (int c = 0; c < nv; c++) {   // mju_mulMatTVec of (jac2 - jac1) with dif, then
           double t = 0;                   // mju_addToScl(ten_J row, ., 1/divisor)
           for (int r = 0; r < 3; r++) {
@@ -4533,6 +4593,12 @@ MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d, bool after_only 
       // the normal rows' J' * weight in row order (mj_mulJacTVec skips zero weights; the
       // rows of contact j follow those of contact j-1), the in-gap contacts' normal
       // Jacobians on the side
+      // sparse mode: mj_mulJacTVec over efc_JT of the weights (d.jar as the reference's
+      // efc_force marker array; invConstraint forms jar later)
+      const bool sparse = mjh_isSparse(&m);
+      if (sparse) {
+        for (int r = 0; r < d.efc_count[0]; r++) d.jar[r] = 0;
+      }
       for (int c = 0; c < ncon; c++) {
         const int g1 = d.con_geom[2*c], g2 = d.con_geom[2*c+1];
         if (g1 < 0 || g2 < 0) continue;
@@ -4546,6 +4612,10 @@ MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d, bool after_only 
           const int nr = one ? 1 : 2*(dim - 1);
           const double w = one ? 1.0 : 0.5/(dim - 1);
           for (int r = adrc; r < adrc + nr; r++) {
+            if (sparse) {
+              d.jar[r] = w;
+              continue;
+            }
             SP<S> J = d.efc_J + (long)r*nv;
             for (int k = 0; k < nv; k++) moment[k] += J[k]*w;
           }
@@ -4565,6 +4635,9 @@ MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d, bool after_only 
         }
       }
       if (counter) {
+        if (sparse && d.efc_count[0]) {
+          for (int k = 0; k < nv; k++) moment[k] = jacColDot(d, k, d.jar);
+        }
         const double s = -1.0/counter;
         for (int k = 0; k < nv; k++) {
           moment[k] += mexcl[k];
@@ -4572,6 +4645,10 @@ MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d, bool after_only 
         }
       }
       for (int k = 0; k < m.moment_rownnz[i]; k++) moment[k] = moment[m.moment_colind[adr+k]];
+    } else if (mjh_isSparse(&m)) {          // tendon, sparse (:1060-1067): the tendon's row
+      d.actuator_length[i] = d.ten_length[id]*gear[0];
+      const int tadr = d.ten_J_rowadr[id];
+      for (int k = 0; k < m.moment_rownnz[i]; k++) moment[k] = d.ten_J[tadr + k]*gear[0];
     } else {                                // fixed tendon :1053-1081 (model-constant nonzeros)
       d.actuator_length[i] = d.ten_length[id]*gear[0];
       for (int k = 0; k < m.moment_rownnz[i]; k++) {
@@ -4903,6 +4980,18 @@ MJH_HD void passive(const mjhipModel& m, const Lane<S>& d) {
       frc_spring = stiffness * (lower - length);
     }
     double frc_damper = -damping * d.ten_velocity[i];
+    if (mjh_isSparse(&m)) {                // :361-370 over the tendon's compressed row
+      if (frc_spring || frc_damper) {
+        const int a = d.ten_J_rowadr[i], e = a + d.ten_J_rownnz[i];
+        for (int j = a; j < e; j++) {
+          const int k = d.ten_J_colind[j];
+          const double J = d.ten_J[j];
+          d.qfrc_spring[k] += J * frc_spring;
+          d.qfrc_damper[k] += J * frc_damper;
+        }
+      }
+      continue;
+    }
     if (frc_spring) addToScl(d.qfrc_spring, d.ten_J + i*nv, frc_spring, nv);
     if (frc_damper) addToScl(d.qfrc_damper, d.ten_J + i*nv, frc_damper, nv);
   }
@@ -4952,31 +5041,178 @@ MJH_HD void passive(const mjhipModel& m, const Lane<S>& d) {
 // registers and written to efc_count once at the end
 struct RowCount { int nefc = 0, ne = 0, nf = 0, nl = 0; };
 
-// row spans of sparse-mode models (mjh_rowSpans): record row r's span, or clear the spans
-// the previous call's rows hold (their entries outside are zero, so the rows are dense again)
-template <int S>
-MJH_HD void recordSpan(const Lane<S>& d, int r, int lo, int hi) {
-  d.efc_lo[r] = lo;
-  d.efc_hi[r] = hi;
-}
-template <int S>
-MJH_HD void clearSpans(const mjhipModel& m, const Lane<S>& d) {
-  const int n = d.efc_spanrows[0], nv = m.nv;
-  for (int r = 0; r < n; r++) {
-    SP<S> J = d.efc_J + (long)r*nv;
-    const int hi = d.efc_hi[r];
-    for (int j = d.efc_lo[r]; j < hi; j++) J[j] = 0;
+//------------------- compressed rows of sparse-mode models (mjh_isSparse) --------------------
+
+// mj_mergeChain engine_support.c:264-304 / mj_mergeChainSimple :309-336: the merged dof chain
+// of two bodies, increasing, into chain; returns its length
+template <class C>
+MJH_HD int mergeChain(const mjhipModel& m, C chain, int b1, int b2) {
+  if (m.body_simple[b1] && m.body_simple[b2]) {
+    if (b1 > b2) { const int t = b1; b1 = b2; b2 = t; }
+    const int n1 = m.body_dofnum[b1], n2 = m.body_dofnum[b2];
+    for (int i = 0; i < n1; i++) chain[i] = m.body_dofadr[b1] + i;
+    for (int i = 0; i < n2; i++) chain[n1+i] = m.body_dofadr[b2] + i;
+    return n1 + n2;
   }
-  d.efc_spanrows[0] = 0;
+  while (b1 && !m.body_dofnum[b1]) b1 = m.body_parentid[b1];
+  while (b2 && !m.body_dofnum[b2]) b2 = m.body_parentid[b2];
+  if (b1 == 0 && b2 == 0) return 0;
+  int da1 = m.body_dofadr[b1] + m.body_dofnum[b1] - 1;
+  int da2 = m.body_dofadr[b2] + m.body_dofnum[b2] - 1;
+  int NV = 0;
+  while (da1 >= 0 || da2 >= 0) {
+    const int c = da1 > da2 ? da1 : da2;
+    chain[NV++] = c;
+    if (da1 == c) da1 = m.dof_parentid[da1];
+    if (da2 == c) da2 = m.dof_parentid[da2];
+  }
+  for (int i = 0; i < NV/2; i++) {
+    const int t = chain[i];
+    chain[i] = chain[NV-i-1];
+    chain[NV-i-1] = t;
+  }
+  return NV;
+}
+
+// mju_combineSparse engine_util_sparse.h:244-303: dst = a*dst + b*src over the union of the two
+// index sets (buf, buf_ind: scratch of nv entries); returns the result's nnz
+template <class D, class DI, class V, class VI, class B, class BI>
+MJH_HD int combineSparse(D dst, V src, double a, double b, int dst_nnz, int src_nnz, DI dst_ind,
+                         VI src_ind, B buf, BI buf_ind) {
+  bool same = dst_nnz == src_nnz;
+  for (int i = 0; same && i < dst_nnz; i++) same = dst_ind[i] == src_ind[i];
+  if (same) {
+    for (int i = 0; i < dst_nnz; i++) dst[i] = dst[i]*a + src[i]*b;   // mju_addToSclScl
+    return dst_nnz;
+  }
+  for (int i = 0; i < dst_nnz; i++) {
+    buf[i] = dst[i];
+    buf_ind[i] = dst_ind[i];
+  }
+  int bi = 0, si = 0, nnz = 0;
+  while (bi < dst_nnz && si < src_nnz) {
+    const int badr = buf_ind[bi], sadr = src_ind[si];
+    if (badr == sadr) {
+      dst[nnz] = a*buf[bi++] + b*src[si++];
+      dst_ind[nnz++] = badr;
+    } else if (badr < sadr) {
+      dst[nnz] = a*buf[bi++];
+      dst_ind[nnz++] = badr;
+    } else {
+      dst[nnz] = b*src[si++];
+      dst_ind[nnz++] = sadr;
+    }
+  }
+  while (si < src_nnz) {
+    dst[nnz] = b*src[si];
+    dst_ind[nnz++] = src_ind[si++];
+  }
+  while (bi < dst_nnz) {
+    dst[nnz] = a*buf[bi];
+    dst_ind[nnz++] = buf_ind[bi++];
+  }
+  return nnz;
+}
+
+// mj_addConstraint :300-331, sparse branch: `size` rows of NV values each (jac, row-major
+// size x NV) over `chain`, appended to the compressed rows; returns false when the rows were
+// not added (an empty chain of a non-contact row, or the capacity)
+template <int S, class J, class C>
+MJH_HD bool addRowsSparse(const mjhipModel& m, const Lane<S>& d, RowCount& rc, J jac, int NV,
+                          C chain, const double* pos, const double* margin, double frictionloss,
+                          int size, int type, int id, int* status) {
+  const bool contact = type == CNSTR_CONTACT_FRICTIONLESS || type == CNSTR_CONTACT_PYRAMIDAL ||
+                       type == CNSTR_CONTACT_ELLIPTIC;
+  NV = NV > 0 ? NV : 0;
+  if (!NV && !contact) return false;
+  const int nefc = rc.nefc;
+  const int adr0 = nefc ? d.efc_J_rowadr[nefc-1] + d.efc_J_rownnz[nefc-1] : 0;
+  if (nefc + size > d.efc_cap || adr0 + (long)size*NV > d.nj_cap) {
+    *status |= MJHIP_INST_CNSTRFULL;   // mjWARN_CNSTRFULL analogue: capacity exceeded
+    return false;
+  }
+  for (int i = 0; i < size; i++) {
+    const int adr = adr0 + i*NV;
+    d.efc_J_rowadr[nefc+i] = adr;
+    d.efc_J_rownnz[nefc+i] = NV;
+    for (int k = 0; k < NV; k++) {
+      d.efc_J_colind[adr+k] = chain[k];
+      d.efc_J[adr+k] = jac[i*NV+k];
+    }
+  }
+  for (int i = 0; i < size; i++) {
+    d.efc_pos[nefc+i] = pos ? pos[i] : 0;
+    d.efc_margin[nefc+i] = margin ? margin[i] : 0;
+    d.efc_frictionloss[nefc+i] = frictionloss;
+    d.efc_type[nefc+i] = type;
+    d.efc_id[nefc+i] = id;
+  }
+  rc.nefc = nefc + size;
+  if (type == CNSTR_EQUALITY) {
+    rc.ne += size;
+  } else if (type == CNSTR_FRICTION_DOF || type == CNSTR_FRICTION_TENDON) {
+    rc.nf += size;
+  } else if (type == CNSTR_LIMIT_JOINT || type == CNSTR_LIMIT_TENDON) {
+    rc.nl += size;
+  }
+  return true;
+}
+
+// mju_transposeSparse engine_util_sparse.c:474-515: efc_JT from the compressed efc_J rows
+template <int S>
+MJH_HD void transposeRows(const mjhipModel& m, const Lane<S>& d, int nefc) {
+  const int nv = m.nv;
+  for (int j = 0; j < nv; j++) d.efc_JT_rownnz[j] = 0;
+  for (int r = 0; r < nefc; r++) {
+    const int a = d.efc_J_rowadr[r], e = a + d.efc_J_rownnz[r];
+    for (int k = a; k < e; k++) {
+      const int c = d.efc_J_colind[k];
+      d.efc_JT_rownnz[c] = d.efc_JT_rownnz[c] + 1;
+    }
+  }
+  int acc = 0;
+  for (int j = 0; j < nv; j++) {             // rowadr as the next free slot of each row
+    d.efc_JT_rowadr[j] = acc;
+    acc += d.efc_JT_rownnz[j];
+  }
+  for (int r = 0; r < nefc; r++) {
+    const int a = d.efc_J_rowadr[r], e = a + d.efc_J_rownnz[r];
+    for (int k = a; k < e; k++) {
+      const int c = d.efc_J_colind[k];
+      const int slot = d.efc_JT_rowadr[c];
+      d.efc_JT_rowadr[c] = slot + 1;
+      d.efc_JT_colind[slot] = r;
+      d.efc_JT[slot] = d.efc_J[k];
+    }
+  }
+  for (int j = 0; j < nv; j++) d.efc_JT_rowadr[j] = d.efc_JT_rowadr[j] - d.efc_JT_rownnz[j];
+}
+
+// mj_mulJacVec :361-377 / mj_mulJacTVec :426-442 of a sparse-mode model: mju_mulMatVecSparse
+// over the rows of efc_J / efc_JT
+template <int S, class V>
+MJH_HD double jacRowDot(const Lane<S>& d, int r, V vec) {
+  const int a = d.efc_J_rowadr[r];
+  return dotSparse(d.efc_J + a, vec, d.efc_J_rownnz[r], d.efc_J_colind + a);
+}
+template <int S, class V>
+MJH_HD double jacColDot(const Lane<S>& d, int j, V vec) {
+  const int a = d.efc_JT_rowadr[j];
+  return dotSparse(d.efc_JT + a, vec, d.efc_JT_rownnz[j], d.efc_JT_colind + a);
 }
 
 // mj_addConstraint :265-356 (dense): `size` rows of jac (strided scratch), contact rows are
-// never dropped as empty. Returns whether the rows were added. With row spans each row is
-// copied over its nonzero span only.
+// never dropped as empty. Returns whether the rows were added. Sparse-mode models come with
+// their row's chain (jac is then size x NV) and take the compressed branch.
 template <int S>
 MJH_HD bool addConstraint(const mjhipModel& m, const Lane<S>& d, RowCount& rc, SP<S> jac,
                           const double* pos, const double* margin, double frictionloss,
-                          int size, int type, int id, int* status) {
+                          int size, int type, int id, int* status, int NV = 0,
+                          SP<S, int> chain = SP<S, int>{nullptr}) {
+  if (mjh_isSparse(&m)) {
+    return addRowsSparse(m, d, rc, jac, NV, chain, pos, margin, frictionloss, size, type, id,
+                         status);
+  }
   int nv = m.nv;
   int nefc = rc.nefc;
   int empty = !(type == CNSTR_CONTACT_FRICTIONLESS || type == CNSTR_CONTACT_PYRAMIDAL ||
@@ -4989,23 +5225,7 @@ MJH_HD bool addConstraint(const mjhipModel& m, const Lane<S>& d, RowCount& rc, S
     *status |= MJHIP_INST_CNSTRFULL;
     return false;
   }
-  if (mjh_rowSpans(&m)) {
-    for (int i = 0; i < size; i++) {
-      SP<S> src = jac + i*nv;
-      int lo = 0, hi = 0;
-      for (int j = 0; j < nv; j++) {
-        if (src[j]) {
-          if (hi == 0) lo = j;
-          hi = j + 1;
-        }
-      }
-      SP<S> dst = d.efc_J + (long)(nefc + i)*nv;
-      for (int j = lo; j < hi; j++) dst[j] = src[j];
-      recordSpan(d, nefc + i, lo, hi);
-    }
-  } else {
-    copy(d.efc_J + nefc*nv, jac, size*nv);
-  }
+  copy(d.efc_J + nefc*nv, jac, size*nv);
   for (int i = 0; i < size; i++) {
     d.efc_pos[nefc+i] = pos ? pos[i] : 0;
     d.efc_margin[nefc+i] = margin ? margin[i] : 0;
@@ -5027,8 +5247,9 @@ MJH_HD bool addConstraint(const mjhipModel& m, const Lane<S>& d, RowCount& rc, S
 template <int S>
 MJH_HD bool addConstraint1(const mjhipModel& m, const Lane<S>& d, RowCount& rc, SP<S> jacrow,
                            double pos, double margin, double frictionloss, int type, int id,
-                           int* status) {
-  return addConstraint(m, d, rc, jacrow, &pos, &margin, frictionloss, 1, type, id, status);
+                           int* status, int NV = 0, SP<S, int> chain = SP<S, int>{nullptr}) {
+  return addConstraint(m, d, rc, jacrow, &pos, &margin, frictionloss, 1, type, id, status, NV,
+                       chain);
 }
 
 // mj_instantiateContact :964-1131 (dense; pyramidal or frictionless; elliptic cones are
@@ -5059,6 +5280,30 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
       continue;
     }
     const int b1 = m.geom_bodyid[d.con_geom[2*i]], b2 = m.geom_bodyid[d.con_geom[2*i+1]];
+    // dense rows of nv values, or (sparse mode) compressed rows over the bodies' merged chain
+    // (mj_jacDifPair :659-731; a contact whose chain is empty is excluded, :1071-1076)
+    const bool sparse = mjh_isSparse(&m);
+    SP<S, int> chain = d.chainbuf;
+    int NV = nv;
+    long adr0 = (long)nefc*nv;
+    if (sparse) {
+      NV = mergeChain(m, chain, b1, b2);
+      if (!NV) {
+        d.con_efc_address[i] = -1;
+        d.con_exclude[i] = 3;
+        continue;
+      }
+      adr0 = nefc ? d.efc_J_rowadr[nefc-1] + d.efc_J_rownnz[nefc-1] : 0;
+      if (adr0 + (long)rows*NV > d.nj_cap) {
+        *status |= MJHIP_INST_CNSTRFULL;
+        continue;
+      }
+      for (int r = 0; r < rows; r++) {
+        d.efc_J_rowadr[nefc + r] = (int)(adr0 + (long)r*NV);
+        d.efc_J_rownnz[nefc + r] = NV;
+        for (int p = 0; p < NV; p++) d.efc_J_colind[adr0 + (long)r*NV + p] = chain[p];
+      }
+    }
     double pos[3], off1[3], off2[3], frame[9], fri[5];
     copy3(pos, d.con_pos + 3*i);
     sub3(off1, pos, d.subtree_com + 3*m.body_rootid[b1]);
@@ -5066,24 +5311,9 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
     for (int k = 0; k < 9; k++) frame[k] = d.con_frame[9*i+k];
     for (int k = 0; k < 5; k++) fri[k] = d.con_friction[5*i+k];
     const int rp = dim > 1 ? 3 : 1;
-    SP<S> J = d.efc_J + nefc*nv;
-    // row spans: the dofs of the two bodies' chains lie in [jlo, jhi), the rest is zero
-    int jlo = 0, jhi = nv;
-    if (mjh_rowSpans(&m)) {
-      jlo = nv;
-      jhi = 0;
-      for (int e = 0; e < 2; e++) {
-        for (int b = e ? b2 : b1; b > 0; b = m.body_parentid[b]) {
-          if (!m.body_dofnum[b]) continue;
-          jlo = m.body_dofadr[b] < jlo ? m.body_dofadr[b] : jlo;
-          const int top = m.body_dofadr[b] + m.body_dofnum[b];
-          jhi = top > jhi ? top : jhi;
-        }
-      }
-      if (jlo > jhi) jlo = jhi = 0;
-      for (int r = 0; r < rows; r++) recordSpan(d, nefc + r, jlo, jhi);
-    }
-    for (int j = jlo; j < jhi; j++) {
+    SP<S> J = d.efc_J + adr0;                // row k's entry p at J[k*NV + p]
+    for (int p = 0; p < NV; p++) {
+      const int j = sparse ? chain[p] : p;
       const int bj = m.dof_bodyid[j];
       const bool in1 = ancestorOrSelf(m, bj, b1), in2 = ancestorOrSelf(m, bj, b2);
       double cj[6] = {0, 0, 0, 0, 0, 0};
@@ -5124,14 +5354,14 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
         }
       }
       if (dim == 1) {
-        J[j] = cj[0];
+        J[p] = cj[0];
       } else if (elliptic) {
-        for (int k = 0; k < dim; k++) J[k*nv + j] = cj[k];
+        for (int k = 0; k < dim; k++) J[k*NV + p] = cj[k];
       } else {
         for (int k = 1; k < dim; k++) {
           double f = fri[k-1];
-          J[(2*(k-1))*nv + j] = cj[0] + cj[k]*f;
-          J[(2*(k-1)+1)*nv + j] = cj[0] + cj[k]*(-f);
+          J[(2*(k-1))*NV + p] = cj[0] + cj[k]*f;
+          J[(2*(k-1)+1)*NV + p] = cj[0] + cj[k]*(-f);
         }
       }
     }
@@ -5768,11 +5998,19 @@ MJH_HD double eqDiagApprox(const mjhipModel& m, int id, int k) {
 // rows are formed dof by dof straight into efc_J: the two body Jacobians of mj_jacDifPair
 // (dense: mj_jac twice, then jac2 - jac1) are zero off their chains, and every other step
 // (the weld's rotational correction and torquescale) acts column by column.
+template <int S>
+MJH_HD void instantiateEqualitySparse(const mjhipModel& m, const Lane<S>& d, RowCount& rc,
+                                      int* status);
+
 template <int S, bool FUSED>
 MJH_HD void instantiateEquality(const mjhipModel& m, const Lane<S>& d, RowCount& rc,
                                 int* status) {
   const int nv = m.nv;
   if ((m.opt.disableflags & mjhipDSBL_EQUALITY) || m.neq == 0) return;
+  if (!FUSED && mjh_isSparse(&m)) {
+    instantiateEqualitySparse(m, d, rc, status);
+    return;
+  }
   for (int i = 0; i < m.neq; i++) {
     if (!m.eq_active0[i]) continue;
     const double* data = m.eq_data + mjhipNEQDATA*i;
@@ -5895,9 +6133,6 @@ MJH_HD void instantiateEquality(const mjhipModel& m, const Lane<S>& d, RowCount&
       d.efc_type[r0+k] = CNSTR_EQUALITY;
       d.efc_id[r0+k] = i;
     }
-    if (!FUSED && mjh_rowSpans(&m)) {     // the rows are written whole
-      for (int k = 0; k < size; k++) recordSpan(d, r0 + k, 0, nv);
-    }
     rc.nefc += size;
     rc.ne += size;
     if constexpr (FUSED) {
@@ -5916,15 +6151,158 @@ MJH_HD void instantiateEquality(const mjhipModel& m, const Lane<S>& d, RowCount&
   }
 }
 
+// mj_instantiateEquality :493-764, sparse branch: connect and weld rows over the merged chain
+// of the two bodies (mj_jacDifPair), joint and tendon couplings over the objects' chains
+// combined by mju_combineSparse (:702-707); the values are the dense rows' at the chain's dofs
+template <int S>
+MJH_HD void instantiateEqualitySparse(const mjhipModel& m, const Lane<S>& d, RowCount& rc,
+                                      int* status) {
+  const int nv = m.nv;
+  SP<S, int> chain = d.chainbuf, chain2 = d.chainbuf + nv, bufind = d.chainbuf + 2*nv;
+  for (int i = 0; i < m.neq; i++) {
+    if (!m.eq_active0[i]) continue;
+    const double* data = m.eq_data + mjhipNEQDATA*i;
+    const int t = m.eq_type[i];
+    const int id0 = m.eq_obj1id[i], id1 = m.eq_obj2id[i];
+    double cpos[6];
+    if (t == mjhipEQ_CONNECT || t == mjhipEQ_WELD) {
+      const int size = t == mjhipEQ_CONNECT ? 3 : 6;
+      double pos[2][3];
+      int body[2];
+      const int ids[2] = {id0, id1};
+      for (int j = 0; j < 2; j++) {
+        if (m.eq_objtype[i] == 1) {
+          const double* anchor = data + 3*(t == mjhipEQ_WELD ? 1 - j : j);
+          mulMatVec3(pos[j], d.xmat + 9*ids[j], anchor);
+          addTo3(pos[j], d.xpos + 3*ids[j]);
+          body[j] = ids[j];
+        } else {
+          copy3(pos[j], d.site_xpos + 3*ids[j]);
+          body[j] = m.site_bodyid[ids[j]];
+        }
+      }
+      sub3(cpos, pos[0], pos[1]);
+      double off0[3], off1[3];
+      sub3(off0, pos[0], d.subtree_com + 3*m.body_rootid[body[0]]);
+      sub3(off1, pos[1], d.subtree_com + 3*m.body_rootid[body[1]]);
+      double quat[4], quat1[4], torquescale = 0;
+      if (t == mjhipEQ_WELD) {
+        torquescale = data[10];
+        if (m.eq_objtype[i] == 1) {
+          mulQuat(quat, d.xquat + 4*id0, data + 6);
+          copy4(quat1, d.xquat + 4*id1);
+        } else {
+          mulQuat(quat, d.xquat + 4*body[0], m.site_quat + 4*id0);
+          mulQuat(quat1, d.xquat + 4*body[1], m.site_quat + 4*id1);
+        }
+        quat1[1] = -quat1[1]; quat1[2] = -quat1[2]; quat1[3] = -quat1[3];
+        double quat2[4];
+        mulQuat(quat2, quat1, quat);
+        cpos[3] = quat2[1]*torquescale;
+        cpos[4] = quat2[2]*torquescale;
+        cpos[5] = quat2[3]*torquescale;
+      }
+      const int NV = mergeChain(m, chain, body[1], body[0]);
+      if (!NV) continue;                   // mj_addConstraint: empty chain, no rows
+      const int r0 = rc.nefc;
+      const long adr0 = r0 ? d.efc_J_rowadr[r0-1] + d.efc_J_rownnz[r0-1] : 0;
+      if (r0 + size > d.efc_cap || adr0 + (long)size*NV > d.nj_cap) {
+        *status |= MJHIP_INST_CNSTRFULL;
+        continue;
+      }
+      SP<S> J = d.efc_J + adr0;
+      for (int p = 0; p < NV; p++) {
+        const int j = chain[p];
+        const int bj = m.dof_bodyid[j];
+        const bool in0 = ancestorOrSelf(m, bj, body[0]), in1 = ancestorOrSelf(m, bj, body[1]);
+        double jp0[3] = {0, 0, 0}, jp1[3] = {0, 0, 0}, jr0[3] = {0, 0, 0}, jr1[3] = {0, 0, 0};
+        SP<S> cdof = d.cdof + 6*j;
+        double tmp[3];
+        if (in0) {
+          cross(tmp, cdof, off0);
+          jp0[0] = cdof[3] + tmp[0]; jp0[1] = cdof[4] + tmp[1]; jp0[2] = cdof[5] + tmp[2];
+          jr0[0] = cdof[0]; jr0[1] = cdof[1]; jr0[2] = cdof[2];
+        }
+        if (in1) {
+          cross(tmp, cdof, off1);
+          jp1[0] = cdof[3] + tmp[0]; jp1[1] = cdof[4] + tmp[1]; jp1[2] = cdof[5] + tmp[2];
+          jr1[0] = cdof[0]; jr1[1] = cdof[1]; jr1[2] = cdof[2];
+        }
+        for (int k = 0; k < 3; k++) J[k*NV + p] = jp0[k] - jp1[k];
+        if (t == mjhipEQ_WELD) {
+          double axis[3] = {jr0[0] - jr1[0], jr0[1] - jr1[1], jr0[2] - jr1[2]};
+          double quat2[4], quat3[4];
+          mulQuatAxis(quat2, quat1, axis);
+          mulQuat(quat3, quat2, quat);
+          for (int k = 0; k < 3; k++) J[(3 + k)*NV + p] = (0.5*quat3[1 + k])*torquescale;
+        }
+      }
+      for (int k = 0; k < size; k++) {
+        d.efc_J_rowadr[r0+k] = (int)(adr0 + (long)k*NV);
+        d.efc_J_rownnz[r0+k] = NV;
+        for (int p = 0; p < NV; p++) d.efc_J_colind[adr0 + (long)k*NV + p] = chain[p];
+        d.efc_pos[r0+k] = cpos[k];
+        d.efc_margin[r0+k] = 0;
+        d.efc_frictionloss[r0+k] = 0;
+        d.efc_type[r0+k] = CNSTR_EQUALITY;
+        d.efc_id[r0+k] = i;
+      }
+      rc.nefc += size;
+      rc.ne += size;
+      continue;
+    }
+    // joint / tendon coupling: the first object's row in jacp[0, nv), the second's in
+    // jacp[nv, 2nv), combined into the first
+    SP<S> jac0 = d.jacp, jac1 = d.jacp + nv;
+    int NV = 0, NV2 = 0;
+    double pv[2], ref[2];
+    const int ids[2] = {id0, id1};
+    for (int j = 0; j < 1 + (id1 >= 0); j++) {
+      SP<S> jac = j ? jac1 : jac0;
+      SP<S, int> ch = j ? chain2 : chain;
+      int n;
+      if (t == mjhipEQ_JOINT) {
+        pv[j] = d.qpos[m.jnt_qposadr[ids[j]]];
+        ref[j] = m.qpos0[m.jnt_qposadr[ids[j]]];
+        n = 1;
+        ch[0] = m.jnt_dofadr[ids[j]];
+        jac[0] = 1;
+      } else {
+        pv[j] = d.ten_length[ids[j]];
+        ref[j] = m.tendon_length0[ids[j]];
+        const int a = d.ten_J_rowadr[ids[j]];
+        n = d.ten_J_rownnz[ids[j]];
+        for (int k = 0; k < n; k++) {
+          ch[k] = d.ten_J_colind[a+k];
+          jac[k] = d.ten_J[a+k];
+        }
+      }
+      if (j) NV2 = n; else NV = n;
+    }
+    if (id1 >= 0) {
+      const double dif = pv[1] - ref[1];
+      cpos[0] = pv[0] - ref[0] - data[0] -
+                (data[1]*dif + data[2]*dif*dif + data[3]*dif*dif*dif + data[4]*dif*dif*dif*dif);
+      const double deriv = data[1] + 2*data[2]*dif + 3*data[3]*dif*dif + 4*data[4]*dif*dif*dif;
+      NV = combineSparse(jac0, jac1, 1.0, -deriv, NV, NV2, chain, chain2, d.sparse_buf, bufind);
+    } else {
+      cpos[0] = pv[0] - ref[0] - data[0];
+    }
+    addRowsSparse(m, d, rc, jac0, NV, chain, cpos, (const double*)nullptr, 0.0, 1,
+                  CNSTR_EQUALITY, i, status);
+  }
+}
+
 template <int S, bool CONTACT = true, bool FUSED = false>
 MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   int nv = m.nv;
   RowCount rc;
   int dsbl = m.opt.disableflags;
-  const bool spans = !FUSED && mjh_rowSpans(&m);
-  if (spans) clearSpans(m, d);
+  // sparse mode: rows over their chains (one-entry chains of a single dof in chainbuf)
+  const bool sparse = !FUSED && mjh_isSparse(&m);
   if (dsbl & mjhipDSBL_CONSTRAINT) {
     d.efc_count[0] = 0; d.efc_count[1] = 0; d.efc_count[2] = 0; d.efc_count[3] = 0;
+    if (sparse) d.nJ[0] = 0;
     if constexpr (FUSED) zero(d.qfrc_constraint, nv);
     return;
   }
@@ -5935,21 +6313,31 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
     }
   };
   SP<S> jacrow = d.jacp;       // one dense row of scratch
+  SP<S, int> one = d.chainbuf;
   instantiateEquality<S, FUSED>(m, d, rc, status);
   if (!(dsbl & mjhipDSBL_FRICTIONLOSS)) {
     for (int i = 0; i < nv; i++) {
       if (m.dof_frictionloss[i] > 0) {
-        zero(jacrow, nv);
-        jacrow[i] = 1;
+        if (sparse) {
+          jacrow[0] = 1;
+          one[0] = i;
+        } else {
+          zero(jacrow, nv);
+          jacrow[i] = 1;
+        }
         added(addConstraint1(m, d, rc, jacrow, 0, 0, m.dof_frictionloss[i], CNSTR_FRICTION_DOF,
-                             i, status), CNSTR_FRICTION_DOF, i, 0, 0, m.dof_frictionloss[i]);
+                             i, status, 1, one), CNSTR_FRICTION_DOF, i, 0, 0,
+              m.dof_frictionloss[i]);
       }
     }
-    // :801-815: tendon friction on the tendon's ten_J row (dropped when the row is empty)
+    // :801-815: tendon friction on the tendon's ten_J row (dense: dropped when the row is
+    // empty; sparse: when its chain is)
     for (int i = 0; i < m.ntendon; i++) {
       if (m.tendon_frictionloss[i] > 0) {
-        added(addConstraint1(m, d, rc, d.ten_J + i*nv, 0, 0, m.tendon_frictionloss[i],
-                             CNSTR_FRICTION_TENDON, i, status),
+        const int ta = sparse ? d.ten_J_rowadr[i] : i*nv;
+        added(addConstraint1(m, d, rc, d.ten_J + ta, 0, 0, m.tendon_frictionloss[i],
+                             CNSTR_FRICTION_TENDON, i, status,
+                             sparse ? d.ten_J_rownnz[i] : 0, d.ten_J_colind + (sparse ? ta : 0)),
               CNSTR_FRICTION_TENDON, i, 0, 0, m.tendon_frictionloss[i]);
       }
     }
@@ -5964,9 +6352,15 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
         for (int side = -1; side <= 1; side += 2) {
           double dist = side * (m.jnt_range[2*i+(side+1)/2] - value);
           if (dist < margin) {
-            zero(jacrow, nv);
-            jacrow[m.jnt_dofadr[i]] = -(double)side;
-            added(addConstraint1(m, d, rc, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status),
+            if (sparse) {
+              jacrow[0] = -(double)side;
+              one[0] = m.jnt_dofadr[i];
+            } else {
+              zero(jacrow, nv);
+              jacrow[m.jnt_dofadr[i]] = -(double)side;
+            }
+            added(addConstraint1(m, d, rc, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status,
+                                 1, one),
                   CNSTR_LIMIT_JOINT, i, dist, margin, 0);
           }
         }
@@ -5979,9 +6373,15 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
         double value = normalize3(angleAxis);
         double dist = dmax(m.jnt_range[2*i], m.jnt_range[2*i+1]) - value;
         if (dist < margin) {
-          zero(jacrow, nv);
-          scl3(jacrow + m.jnt_dofadr[i], angleAxis, -1);
-          added(addConstraint1(m, d, rc, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status),
+          if (sparse) {
+            scl3(jacrow, angleAxis, -1);
+            for (int k = 0; k < 3; k++) one[k] = m.jnt_dofadr[i] + k;
+          } else {
+            zero(jacrow, nv);
+            scl3(jacrow + m.jnt_dofadr[i], angleAxis, -1);
+          }
+          added(addConstraint1(m, d, rc, jacrow, dist, margin, 0, CNSTR_LIMIT_JOINT, i, status,
+                               3, one),
                 CNSTR_LIMIT_JOINT, i, dist, margin, 0);
         }
       }
@@ -5993,8 +6393,14 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
       for (int side = -1; side <= 1; side += 2) {
         double dist = side * (m.tendon_range[2*i+(side+1)/2] - value);
         if (dist < margin) {
-          scl(jacrow, d.ten_J + i*nv, -side, nv);
-          added(addConstraint1(m, d, rc, jacrow, dist, margin, 0, CNSTR_LIMIT_TENDON, i, status),
+          if (sparse) {
+            scl(jacrow, d.ten_J + d.ten_J_rowadr[i], -side, d.ten_J_rownnz[i]);
+          } else {
+            scl(jacrow, d.ten_J + i*nv, -side, nv);
+          }
+          added(addConstraint1(m, d, rc, jacrow, dist, margin, 0, CNSTR_LIMIT_TENDON, i, status,
+                               sparse ? d.ten_J_rownnz[i] : 0,
+                               d.ten_J_colind + (sparse ? d.ten_J_rowadr[i] : 0)),
                 CNSTR_LIMIT_TENDON, i, dist, margin, 0);
         }
       }
@@ -6007,7 +6413,10 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   d.efc_count[0] = rc.nefc; d.efc_count[1] = rc.ne; d.efc_count[2] = rc.nf;
   d.efc_count[3] = rc.nl;
   const int nefc = rc.nefc;
-  if (spans) d.efc_spanrows[0] = nefc;
+  if (sparse) {                 // :2044-2104: nJ, the transpose (supernodes are AVX-only)
+    d.nJ[0] = nefc ? d.efc_J_rowadr[nefc-1] + d.efc_J_rownnz[nefc-1] : 0;
+    if (nefc) transposeRows(m, d, nefc);
+  }
   if constexpr (FUSED) {
     constraintForce(m, d, nefc);
     return;
@@ -6123,14 +6532,13 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
   }
 }
 
-// mj_referenceConstraint :2362-2375 (dense mju_mulMatVec for efc_vel)
+// mj_referenceConstraint :2362-2375 (efc_vel = mj_mulJacVec, dense or sparse)
 template <int S>
 MJH_HD void referenceConstraint(const mjhipModel& m, const Lane<S>& d) {
   int nefc = d.efc_count[0];
-  const bool spans = mjh_rowSpans(&m);
+  const bool sparse = mjh_isSparse(&m);
   for (int i = 0; i < nefc; i++) {
-    d.efc_vel[i] = spans ? dotSpan(d.efc_J + i*m.nv, d.qvel, d.efc_lo[i], d.efc_hi[i], m.nv)
-                         : dot(d.efc_J + i*m.nv, d.qvel, m.nv);
+    d.efc_vel[i] = sparse ? jacRowDot(d, i, d.qvel) : dot(d.efc_J + i*m.nv, d.qvel, m.nv);
     d.efc_aref[i] = -d.efc_KBIP[4*i+1]*d.efc_vel[i]
                     -d.efc_KBIP[4*i]*d.efc_KBIP[4*i+2]*(d.efc_pos[i]-d.efc_margin[i]);
   }
@@ -6146,10 +6554,10 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
     return;
   }
   int ne = d.efc_count[1], nf = d.efc_count[2];
-  const bool spans = mjh_rowSpans(&m);
+  const bool sparse = mjh_isSparse(&m);
   for (int i = 0; i < nefc; i++) {
-    d.jar[i] = (spans ? dotSpan(d.efc_J + i*nv, d.qacc, d.efc_lo[i], d.efc_hi[i], nv)
-                      : dot(d.efc_J + i*nv, d.qacc, nv)) - d.efc_aref[i];
+    d.jar[i] = (sparse ? jacRowDot(d, i, d.qacc) : dot(d.efc_J + i*nv, d.qacc, nv)) -
+               d.efc_aref[i];
   }
   for (int i = 0; i < nefc; i++) d.efc_force[i] = -d.efc_D[i] * d.jar[i];
   for (int i = 0; i < nefc; i++) {
@@ -6201,15 +6609,8 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
       i += dim - 1;
     }
   }
-  if (spans) {                          // mulMatTVec over each row's span
-    zero(d.qfrc_constraint, nv);
-    for (int r = 0; r < nefc; r++) {
-      const double tmp = d.efc_force[r];
-      if (!tmp) continue;
-      SP<S> J = d.efc_J + (long)r*nv;
-      const int hi = d.efc_hi[r];
-      for (int j = d.efc_lo[r]; j < hi; j++) d.qfrc_constraint[j] += J[j]*tmp;
-    }
+  if (sparse) {                         // mju_mulMatVecSparse over the rows of efc_JT
+    for (int j = 0; j < nv; j++) d.qfrc_constraint[j] = jacColDot(d, j, d.efc_force);
   } else {
     mulMatTVec(d.qfrc_constraint, d.efc_J, d.efc_force, nefc, nv);
   }
@@ -6241,7 +6642,14 @@ MJH_HD void invPosition(const mjhipModel& m, const Lane<S>& d, int* status) {
 template <int S, bool FUSED = false>
 MJH_HD void invVelocity(const mjhipModel& m, const Lane<S>& d) {
   int nv = m.nv;
-  for (int r = 0; r < m.ntendon; r++) d.ten_velocity[r] = dot(d.ten_J + r*nv, d.qvel, nv);
+  if (mjh_isSparse(&m)) {                  // engine_forward.c:206-212, sparse
+    for (int r = 0; r < m.ntendon; r++) {
+      const int a = d.ten_J_rowadr[r];
+      d.ten_velocity[r] = dotSparse(d.ten_J + a, d.qvel, d.ten_J_rownnz[r], d.ten_J_colind + a);
+    }
+  } else {
+    for (int r = 0; r < m.ntendon; r++) d.ten_velocity[r] = dot(d.ten_J + r*nv, d.qvel, nv);
+  }
   if (!(m.opt.disableflags & mjhipDSBL_ACTUATION)) {
     for (int r = 0; r < m.nu; r++) {
       int adr = m.moment_rowadr[r];
@@ -6311,12 +6719,22 @@ MJH_HD double momentAt(const mjhipModel& m, const Lane<S>& d, int i, int col) {
   return 0;
 }
 
+// ten_J of tendon t at dof col: the dense row, or the compressed row of a sparse-mode model
+template <int S>
+MJH_HD double tenJAt(const mjhipModel& m, const Lane<S>& d, int t, int col) {
+  if (!mjh_isSparse(&m)) return d.ten_J[t*m.nv + col];
+  const int a = d.ten_J_rowadr[t], n = d.ten_J_rownnz[t];
+  for (int k = 0; k < n; k++) {
+    if (d.ten_J_colind[a+k] == col) return d.ten_J[a+k];
+  }
+  return 0;
+}
+
 // qDeriv(r, c) of mjd_smooth_vel(flg_bias = 0) (engine_derivative.c:1522-1536): actuator
 // velocity terms (mjd_actuator_vel :812-870, addJTBJ :693-724), then dof and tendon damping
 // (mjd_passive_vel :1432-1519), in the reference's order of accumulation
 template <int S>
 MJH_HD double qDerivAt(const mjhipModel& m, const Lane<S>& d, int r, int c) {
-  const int nv = m.nv;
   double q = 0;
   if (!(m.opt.disableflags & mjhipDSBL_ACTUATION)) {
     for (int i = 0; i < m.nu; i++) {
@@ -6334,9 +6752,11 @@ MJH_HD double qDerivAt(const mjhipModel& m, const Lane<S>& d, int r, int c) {
     if (r == c) q -= m.dof_damping[r];
     for (int t = 0; t < m.ntendon; t++) {
       if (m.tendon_damping[t] > 0) {
+        // addJTBJ :693-724, or addJTBJSparse :729-755 for a sparse-mode model, whose only
+        // extra terms are exact zeros (structural entries of value 0)
         double B = -m.tendon_damping[t];
-        SP<S> J = d.ten_J + t*nv;
-        if (J[r]) q += J[c] * (J[r] * B);
+        const double Jr = tenJAt(m, d, t, r);
+        if (Jr) q += tenJAt(m, d, t, c) * (Jr * B);
       }
     }
   }
@@ -8083,6 +8503,7 @@ struct Mirror {
 #undef XSI
   int efc_cap;
   int con_cap;
+  long nj_cap;
 };
 
 MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
@@ -8099,6 +8520,7 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
 #undef XSI
   d.efc_cap = mr.efc_cap;
   d.con_cap = mr.con_cap;
+  d.nj_cap = mr.nj_cap;
   d.chain = nullptr;
   d.gxpos = d.geom_xpos;
   d.gstage = false;

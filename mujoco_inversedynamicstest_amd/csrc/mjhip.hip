@@ -180,15 +180,6 @@ __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __
   }
 }
 
-// rows uploaded whole into instance 0 (the single-instance drop-ins' put_rows): their row
-// spans (mjh_rowSpans models) cover every column; rows past them keep theirs for the next
-// clear
-__global__ void k_full_spans(mjhipModel m, Mirror mr, int nefc) {
-  Lane<64> d = lane_view(mr, 0, 0);
-  for (int r = 0; r < nefc; r++) mjh::recordSpan(d, r, 0, m.nv);
-  if (d.efc_spanrows[0] < nefc) d.efc_spanrows[0] = nefc;
-}
-
 // The stage-skip fall-back of mjhip_inverseFDBatch, decided on the device: when k_vaskip
 // found a centre with limit rows (fdflag[0]), the qvel/qacc perturbations [first, end) run the
 // full pipeline as well (their own position stage and rows), else the range is empty.
@@ -519,10 +510,6 @@ static unsigned long long model_signature(const mjhipModel* m) {
 }
 
 // model features outside the device path: rejected at context creation (fail loudly)
-// Sparse-Jacobian models (mj_isSparse: jacobian=sparse, or auto with nv >= 60) are not one:
-// the reference's sparse path keeps compressed rows over the bodies' dof chains; here the
-// rows stay dense with per-row dof spans (mjh_rowSpans), which gives the sparse path's J'force
-// bit for bit and its J*v to the last bits (sparse Jacobians).
 static const char* unsupported(const mjhipModel* m) {
   if ((m->opt.enableflags & mjhipENBL_INVDISCRETE) && m->opt.integrator == mjhipINT_RK4) {
     return "mjENBL_INVDISCRETE with the RK4 integrator (an error in the reference)";
@@ -539,6 +526,16 @@ static const char* unsupported(const mjhipModel* m) {
     if (t != mjhipTRN_JOINT && t != mjhipTRN_JOINTINPARENT && t != mjhipTRN_TENDON &&
         t != mjhipTRN_SLIDERCRANK && t != mjhipTRN_SITE && t != mjhipTRN_BODY) {
       return "unknown transmission type";
+    }
+  }
+  if (mjh_isSparse(m)) {
+    for (int i = 0; i < m->nu; i++) {
+      if (m->actuator_trntype[i] == mjhipTRN_TENDON &&
+          m->wrap_type[m->tendon_adr[m->actuator_trnid[2*i]]] != mjhipWRAP_JOINT) {
+        // the reference's moment row is the tendon's compressed ten_J row (:1060-1067), whose
+        // pattern follows the wrapping state; actuator_moment's pattern is model-constant here
+        return "a spatial-tendon transmission in a sparse-Jacobian model";
+      }
     }
   }
   for (int i = 0; i < m->nsensor; i++) {
@@ -714,6 +711,7 @@ MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int cap
   (void)nv; (void)efc_cap; (void)con_cap;
   c->mirror.efc_cap = c->efc_cap;
   c->mirror.con_cap = c->con_cap;
+  c->mirror.nj_cap = mjh_njCap(m, c->efc_cap);
   c->mirror_bytes = mb;
   if (hipMalloc(&c->mirror_buf, mb) != hipSuccess) {
     set_error("hipMalloc(mirror, %zu bytes) failed", mb);
@@ -841,6 +839,8 @@ MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int cap
   return MJHIP_OK;
 }
 
+static void timers_detach(mjhipContext* c);
+
 MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   if (!c) return;
   hipSetDevice(c->device);
@@ -850,6 +850,7 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->tev0) hipEventDestroy(c->tev0);
   if (c->tev1) hipEventDestroy(c->tev1);
+  if (c->tbuf) timers_detach(c);
   hipFree(c->tbuf);
   hipFree(c->stage);
   hipFree(c->status);
@@ -874,6 +875,11 @@ MJHIP_API int mjhip_contextLoadKernel(mjhipContext* c, const void* image, size_t
   if (signature != c->sig) {
     set_error("mjhip_contextLoadKernel: kernel '%s' was generated for another model "
               "(signature %016llx, context %016llx)", name, signature, c->sig);
+    return MJHIP_ERR_MODEL;
+  }
+  if (mjh_isSparse(&c->hmodel)) {
+    // the straight-line kernels and their constraint kernels keep dense rows
+    set_error("mjhip_contextLoadKernel: sparse-Jacobian models run the generic kernel");
     return MJHIP_ERR_MODEL;
   }
   hipSetDevice(c->device);
@@ -1086,6 +1092,18 @@ static int timers_attach(mjhipContext* c, unsigned long long* p) {
   return MJHIP_OK;
 }
 
+// the one context per process whose accumulator the phase marks may add into: mjh_tbuf is a
+// process-wide device global per unit, so a second context's kernels would add into the
+// first's accumulator
+static mjhipContext* g_timed_ctx = nullptr;
+
+// point every mjh_tbuf copy back at null (after the stream's earlier work), so that no kernel
+// adds into an accumulator that is about to be freed
+static void timers_detach(mjhipContext* c) {
+  timers_attach(c, nullptr);
+  if (g_timed_ctx == c) g_timed_ctx = nullptr;
+}
+
 // fold one call's phase-mark sums (engine_device.h MJH_PHASE: slots and wave counts) into
 // the reference's timer slots: mean wave time per stage, 100 MHz ticks -> milliseconds
 static void timers_fold(mjhipContext* c, const unsigned long long* t, float call_ms) {
@@ -1138,12 +1156,17 @@ MJHIP_API int mjhip_contextTimers(mjhipContext* c, int enable) {
   HIPCHECK(hipSetDevice(c->device));
   if (!enable) {
     if (c->tbuf) {
-      HIPCHECK(hipStreamSynchronize(c->stream));
+      timers_detach(c);
       HIPCHECK(hipFree(c->tbuf));
       c->tbuf = nullptr;
     }
     return MJHIP_OK;
   }
+  if (g_timed_ctx && g_timed_ctx != c) {
+    set_error("mjhip_contextTimers: another context of this process is being timed");
+    return MJHIP_ERR_ARG;
+  }
+  g_timed_ctx = c;
   if (!c->tbuf) {
     HIPCHECK(hipMalloc((void**)&c->tbuf, MJH_TSLOTS * sizeof(unsigned long long)));
     HIPCHECK(hipMemset(c->tbuf, 0, MJH_TSLOTS * sizeof(unsigned long long)));
@@ -1209,7 +1232,10 @@ MJHIP_API int mjhip_inverseBatch(mjhipContext* c, int B, const mjtNum* qpos,
   const bool timed = c->tbuf != nullptr;
   if (timed) {
     int trc = timers_attach(c, c->tbuf);
-    if (trc) return trc;
+    if (trc) {
+      timers_attach(c, nullptr);
+      return trc;
+    }
     HIPCHECK(hipEventRecord(c->tev0, c->stream));
   }
   int rc = launch_inverse(c, B, dq, dv, da, dqfrc, skipstage, want_status ? c->status : nullptr,
@@ -1810,6 +1836,21 @@ static int put_rows(mjhipContext* c, const mjhipModel* m, const mjhipData* d, in
               d->nefc, d->ncon, d->efc_capacity, d->con_capacity);
     return MJHIP_ERR_ARG;
   }
+  // sparse-mode models: compressed rows (nJ values) and the tendon rows' structure
+  const bool sparse = mjh_isSparse(m);
+  if (sparse && lo <= 1 && hi >= 1) {
+    if (d->nJ < 0 || d->nJ > c->mirror.nj_cap) {
+      set_error("%d compressed Jacobian entries exceed the device capacity (%ld)", d->nJ,
+                c->mirror.nj_cap);
+      return MJHIP_ERR_CAPACITY;
+    }
+    if ((m->ntendon && (!d->ten_J_rownnz || !d->ten_J_rowadr || !d->ten_J_colind)) ||
+        (d->nefc && (!d->efc_J_rownnz || !d->efc_J_rowadr || !d->efc_J_colind || !d->efc_JT ||
+                     !d->efc_JT_rownnz || !d->efc_JT_rowadr || !d->efc_JT_colind))) {
+      set_error("sparse-Jacobian model: mjhipData lacks the compressed Jacobian arrays");
+      return MJHIP_ERR_ARG;
+    }
+  }
   const int cnt[4] = {d->nefc, d->ne, d->nf, d->nl};
   int rc = put0(c, c->mirror.efc_count, cnt, 4);
   if (!rc) rc = put0(c, c->mirror.con_count, &d->ncon, 1);
@@ -1817,17 +1858,24 @@ static int put_rows(mjhipContext* c, const mjhipModel* m, const mjhipData* d, in
   (void)nv;
 #define MJ_M(n) m->n
 #define XE(type, name, w, stage) \
-  if (!rc && stage >= lo && stage <= hi) rc = put0(c, c->mirror.name, (const type*)d->name, \
-                                                   (long)d->nefc * (w));
+  if (!rc && stage >= lo && stage <= hi) \
+    rc = put0(c, c->mirror.name, (const type*)d->name, \
+              (sparse && !strcmp(#name, "efc_J")) ? (long)d->nJ : (long)d->nefc * (w));
   MJHIP_DATA_EFC
 #undef XE
-  if (!rc && lo <= 1 && hi >= 1 && mjh_rowSpans(m)) {
-    hipLaunchKernelGGL(k_full_spans, dim3(1), dim3(1), 0, c->stream, c->dmodel, c->mirror,
-                       d->nefc);
-    if (hipGetLastError() != hipSuccess) {
-      set_error("k_full_spans launch");
-      rc = MJHIP_ERR_HIP;
-    }
+  if (!rc && sparse && lo <= 1 && hi >= 1) {
+    const long nt = m->ntendon, nJ = d->nJ, ne = d->nefc;
+    rc = put0(c, c->mirror.nJ, &d->nJ, 1);
+    if (!rc) rc = put0(c, c->mirror.ten_J_rownnz, (const int*)d->ten_J_rownnz, nt);
+    if (!rc) rc = put0(c, c->mirror.ten_J_rowadr, (const int*)d->ten_J_rowadr, nt);
+    if (!rc) rc = put0(c, c->mirror.ten_J_colind, (const int*)d->ten_J_colind, nt*nv);
+    if (!rc) rc = put0(c, c->mirror.efc_J_rownnz, (const int*)d->efc_J_rownnz, ne);
+    if (!rc) rc = put0(c, c->mirror.efc_J_rowadr, (const int*)d->efc_J_rowadr, ne);
+    if (!rc) rc = put0(c, c->mirror.efc_J_colind, (const int*)d->efc_J_colind, nJ);
+    if (!rc) rc = put0(c, c->mirror.efc_JT, (const double*)d->efc_JT, nJ);
+    if (!rc && ne) rc = put0(c, c->mirror.efc_JT_rownnz, (const int*)d->efc_JT_rownnz, (long)nv);
+    if (!rc && ne) rc = put0(c, c->mirror.efc_JT_rowadr, (const int*)d->efc_JT_rowadr, (long)nv);
+    if (!rc) rc = put0(c, c->mirror.efc_JT_colind, (const int*)d->efc_JT_colind, nJ);
   }
 #define XC(type, name, w, stage) \
   if (!rc && stage >= lo && stage <= hi) rc = put0(c, c->mirror.name, (const type*)d->name, \
@@ -1841,9 +1889,11 @@ static int put_rows(mjhipContext* c, const mjhipModel* m, const mjhipData* d, in
 // rows written by stages lo..hi, instance 0 -> host, and the counts (contacts when lo <= 1);
 // the caller synchronizes. Reading the counts needs one blocking copy first.
 static int get_rows(mjhipContext* c, const mjhipModel* m, mjhipData* d, int lo, int hi) {
-  int cnt[4] = {0, 0, 0, 0}, ncon = 0;
+  int cnt[4] = {0, 0, 0, 0}, ncon = 0, nJ = 0;
+  const bool sparse = mjh_isSparse(m);
   int rc = get0(c, cnt, (const int*)c->mirror.efc_count, 4);
   if (!rc) rc = get0(c, &ncon, (const int*)c->mirror.con_count, 1);
+  if (!rc && sparse) rc = get0(c, &nJ, (const int*)c->mirror.nJ, 1);
   if (!rc && hipStreamSynchronize(c->stream) != hipSuccess) {
     set_error("hipStreamSynchronize failed");
     rc = MJHIP_ERR_HIP;
@@ -1851,17 +1901,42 @@ static int get_rows(mjhipContext* c, const mjhipModel* m, mjhipData* d, int lo, 
   if (rc) return rc;
   d->nefc = cnt[0]; d->ne = cnt[1]; d->nf = cnt[2]; d->nl = cnt[3];
   if (lo <= 1) d->ncon = ncon;
+  if (sparse && lo <= 1) d->nJ = nJ;
+  if (sparse && lo <= 1 &&
+      ((m->ntendon && (!d->ten_J_rownnz || !d->ten_J_rowadr || !d->ten_J_colind)) ||
+       (cnt[0] && d->efc_capacity >= cnt[0] &&
+        (!d->efc_J_rownnz || !d->efc_J_rowadr || !d->efc_J_colind || !d->efc_JT ||
+         !d->efc_JT_rownnz || !d->efc_JT_rowadr || !d->efc_JT_colind)))) {
+    set_error("sparse-Jacobian model: mjhipData lacks the compressed Jacobian arrays");
+    return MJHIP_ERR_ARG;
+  }
   // rows a caller's buffers cannot hold: mjWARN_CNSTRFULL analogue, nothing written
   if ((cnt[0] && d->efc_capacity < cnt[0]) || (lo <= 1 && ncon && d->con_capacity < ncon)) {
     if (d->efc_capacity > 0 || d->con_capacity > 0) d->status |= MJHIP_INST_CNSTRFULL;
     return MJHIP_OK;
   }
+  const int nv = m->nv;
+  (void)nv;
 #define MJ_M(n) m->n
 #define XE(type, name, w, stage) \
-  if (!rc && stage >= lo && stage <= hi) rc = get0(c, (type*)d->name, (const type*)c->mirror.name, \
-                                                   (long)cnt[0] * (w));
+  if (!rc && stage >= lo && stage <= hi) \
+    rc = get0(c, (type*)d->name, (const type*)c->mirror.name, \
+              (sparse && !strcmp(#name, "efc_J")) ? (long)nJ : (long)cnt[0] * (w));
   MJHIP_DATA_EFC
 #undef XE
+  if (!rc && sparse && lo <= 1) {
+    const long nt = m->ntendon, ne = cnt[0];
+    rc = get0(c, (int*)d->ten_J_rownnz, (const int*)c->mirror.ten_J_rownnz, nt);
+    if (!rc) rc = get0(c, (int*)d->ten_J_rowadr, (const int*)c->mirror.ten_J_rowadr, nt);
+    if (!rc) rc = get0(c, (int*)d->ten_J_colind, (const int*)c->mirror.ten_J_colind, nt*nv);
+    if (!rc) rc = get0(c, (int*)d->efc_J_rownnz, (const int*)c->mirror.efc_J_rownnz, ne);
+    if (!rc) rc = get0(c, (int*)d->efc_J_rowadr, (const int*)c->mirror.efc_J_rowadr, ne);
+    if (!rc) rc = get0(c, (int*)d->efc_J_colind, (const int*)c->mirror.efc_J_colind, (long)nJ);
+    if (!rc) rc = get0(c, (double*)d->efc_JT, (const double*)c->mirror.efc_JT, (long)nJ);
+    if (!rc && ne) rc = get0(c, (int*)d->efc_JT_rownnz, (const int*)c->mirror.efc_JT_rownnz, (long)nv);
+    if (!rc && ne) rc = get0(c, (int*)d->efc_JT_rowadr, (const int*)c->mirror.efc_JT_rowadr, (long)nv);
+    if (!rc) rc = get0(c, (int*)d->efc_JT_colind, (const int*)c->mirror.efc_JT_colind, (long)nJ);
+  }
 #define XC(type, name, w, stage) \
   if (!rc && lo <= 1 && stage >= lo && stage <= hi) \
     rc = get0(c, (type*)d->name, (const type*)c->mirror.name, (long)ncon * (w));

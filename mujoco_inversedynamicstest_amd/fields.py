@@ -82,8 +82,10 @@ def _parse():
     return [RowField(ct, nm, w, int(st)) for ct, nm, w, st in re.findall(
         tag + r"\(\s*(\w+)\s*,\s*(\w+)\s*,\s*([\w()]+)\s*,\s*(\d)\s*\)",
         _macro_body(text, group))]
+  sparse = [SparseField(ct, nm, dim) for ct, nm, dim in re.findall(
+      r"XJ\(\s*(\w+)\s*,\s*(\w+)\s*,\s*(\w+)\s*\)", _macro_body(text, "MJHIP_DATA_SPARSE"))]
   return (sizes, model, data, xd("MJHIP_DATA_FORWARD"), xd("MJHIP_DATA_SENSOR_AUX"),
-          rows("MJHIP_DATA_EFC", "XE"), rows("MJHIP_DATA_CONTACT", "XC"))
+          rows("MJHIP_DATA_EFC", "XE"), rows("MJHIP_DATA_CONTACT", "XC"), sparse)
 
 
 @dataclass(frozen=True)
@@ -98,8 +100,21 @@ class RowField:
     return _dim(self.width, sizes)
 
 
+@dataclass(frozen=True)
+class SparseField:
+  """An array of the compressed Jacobians of sparse-mode models (MJHIP_DATA_SPARSE)."""
+  ctype: str
+  name: str
+  dim: str     # ntendon, ntendon_nv, efc, efc_nv or nv
+
+  def size(self, sizes: dict, efc_capacity: int) -> int:
+    nt, nv = sizes["ntendon"], sizes["nv"]
+    return {"ntendon": nt, "ntendon_nv": nt * nv, "efc": efc_capacity,
+            "efc_nv": efc_capacity * nv, "nv": nv}[self.dim]
+
+
 (MODEL_SIZES, MODEL_FIELDS, DATA_FIELDS, FORWARD_FIELDS, AUX_FIELDS, EFC_FIELDS,
- CONTACT_FIELDS) = _parse()
+ CONTACT_FIELDS, SPARSE_FIELDS) = _parse()
 MODEL_FIELD = {f.name: f for f in MODEL_FIELDS}
 DATA_FIELD = {f.name: f for f in DATA_FIELDS + FORWARD_FIELDS + AUX_FIELDS}
 
@@ -142,7 +157,15 @@ class CData(ctypes.Structure):
               [(f.name, ctypes.POINTER(ctypes.c_double)) for f in AUX_FIELDS] +
               [(k, ctypes.c_int) for k in ("efc_capacity", "ne", "nf", "nl", "con_capacity",
                                            "ncon")] +
-              [(f.name, ctypes.POINTER(CTYPE[f.ctype])) for f in EFC_FIELDS + CONTACT_FIELDS])
+              [(f.name, ctypes.POINTER(CTYPE[f.ctype])) for f in EFC_FIELDS + CONTACT_FIELDS] +
+              [("nJ", ctypes.c_int)] +
+              [(f.name, ctypes.POINTER(CTYPE[f.ctype])) for f in SPARSE_FIELDS])
+
+
+def is_sparse(m) -> bool:
+  """mj_isSparse (engine_core_constraint.c:99-106): jacobian="sparse", or "auto" with nv >= 60."""
+  jac = int(m.opt["jacobian"])
+  return jac == 1 or (jac == 2 and m.sizes["nv"] >= 60)
 
 
 def output_doubles(sizes: dict) -> int:

@@ -87,6 +87,13 @@ class MjData:
     for f in fields.EFC_FIELDS + fields.CONTACT_FIELDS:
       setattr(self.struct, f.name,
               self._rows[f.name].ctypes.data_as(ctypes.POINTER(fields.CTYPE[f.ctype])))
+    # compressed-Jacobian structures (sparse-mode models only; NULL otherwise)
+    self._sparse = {}
+    if fields.is_sparse(m):
+      for f in fields.SPARSE_FIELDS:
+        a = np.zeros(max(f.size(sizes, efc_capacity), 1), dtype=fields.NPTYPE[f.ctype])
+        self._sparse[f.name] = a
+        setattr(self.struct, f.name, a.ctypes.data_as(ctypes.POINTER(fields.CTYPE[f.ctype])))
 
   def __getattr__(self, k):
     arrs = self.__dict__.get("_arrays")
@@ -95,6 +102,10 @@ class MjData:
       n = f.size(self.m.sizes) if f else len(arrs[k])
       return arrs[k][:n]
     raise AttributeError(k)
+
+  def sparse(self, name):
+    """A compressed-Jacobian array of a sparse-mode model (MJHIP_DATA_SPARSE), whole buffer."""
+    return self._sparse[name]
 
   def efc(self, name):
     """Constraint-row (efc_*) or contact (con_*) array of the current rows / contacts, one

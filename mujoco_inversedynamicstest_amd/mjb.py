@@ -476,7 +476,7 @@ def read(buf: bytes):
   m.opt = opt
   A = {k: v for k, v in arrays.items()}
   try:
-    derived = mjcf.sparse_structures(dict(m.sizes), A)
+    derived = mjcf.sparse_structures(dict(m.sizes), A, jacobian=int(opt["jacobian"]))
   except mjcf.MJCFError as e:
     raise MJBError(f"inconsistent model: {e}") from e
   A.update(derived)

@@ -2231,7 +2231,7 @@ class MJCFCompiler:
     # tendon, slider-crank or site transmission, so actuator_moment has the reference's size
     s["nJmom"] = sum({0: 6, 1: 3, 2: 1, 3: 1}[int(jtype[atrnid[ai, 0]])] if atrn[ai] in (0, 1)
                      else nv for ai in range(nu))
-    A.update(sparse_structures(s, A))
+    A.update(sparse_structures(s, A, jacobian=int(self.opt["jacobian"])))
     # scalars and names
     m.opt = {k: (list(v) if isinstance(v, list) else v) for k, v in self.opt.items()}
     for k, v in A.items():
@@ -2258,7 +2258,7 @@ class MJCFCompiler:
     return m
 
 
-def sparse_structures(sizes: dict, A) -> dict:
+def sparse_structures(sizes: dict, A, jacobian: int = 2) -> dict:
   """The model-constant sparse structures the reference keeps in mjData (mj_makeData):
   C (reduced LTDL pattern) and mapM2C, D (dof x dof) and mapM2D, B (body x dof), and the
   actuator moment pattern. `A` maps mjModel field names to arrays (the compiler's, or an
@@ -2266,6 +2266,7 @@ def sparse_structures(sizes: dict, A) -> dict:
   new arrays by field name; raises MJCFError on an inconsistent model."""
   nv, nbody, nu = sizes["nv"], sizes["nbody"], sizes["nu"]
   nC, nD, nJmom = sizes["nC"], sizes["nD"], sizes["nJmom"]
+  sparse_jac = jacobian == 1 or (jacobian == 2 and nv >= 60)     # mj_isSparse
   dparent = np.asarray(A["dof_parentid"]).reshape(-1)
   simplenum = np.asarray(A["dof_simplenum"]).reshape(-1)
   Madr = np.asarray(A["dof_Madr"]).reshape(-1)
@@ -2436,6 +2437,11 @@ def sparse_structures(sizes: dict, A) -> dict:
           c.update(range(dofadr[b], dofadr[b] + dofnum[b]))
           b = int(parentid[b])
       c = [] if agear[ai, 0] == 0 else sorted(c)
+    elif sparse_jac:
+      # fixed tendon of a sparse-mode model (:1060-1067): the tendon's compressed ten_J row,
+      # i.e. the merged dofs of its joints (mj_tendon's mju_combineSparse, smooth.c:709-714),
+      # whatever the coefficients and gear
+      c = sorted({int(jdadr[wobj[wi]]) for wi in range(tadr[tid], tadr[tid] + tnum[tid])})
     else:
       row = np.zeros(nv)
       for wi in range(tadr[tid], tadr[tid] + tnum[tid]):

@@ -413,7 +413,234 @@ static void mj_jac(const mjhipModel* m, const mjhipData* d, mjtNum* jacp, mjtNum
   }
 }
 
-/* :1194-1251, dense case */
+/*---------------------------- sparse Jacobians (mj_isSparse models) -----------------------*/
+
+/* mj_isSparse, engine_core_constraint.c:99-106 */
+static int mj_isSparse(const mjhipModel* m) {
+  return m->opt.jacobian == mjhipJAC_SPARSE || (m->opt.jacobian == mjhipJAC_AUTO && m->nv >= 60);
+}
+
+/* mj_mergeChain :264-304: the union of two bodies' dof ancestor chains, increasing */
+static int mj_mergeChain(const mjhipModel* m, int* chain, int b1, int b2) {
+  int da1, da2, NV = 0;
+  while (b1 && !m->body_dofnum[b1]) b1 = m->body_parentid[b1];
+  while (b2 && !m->body_dofnum[b2]) b2 = m->body_parentid[b2];
+  if (b1 == 0 && b2 == 0) return 0;
+  da1 = m->body_dofadr[b1] + m->body_dofnum[b1] - 1;
+  da2 = m->body_dofadr[b2] + m->body_dofnum[b2] - 1;
+  while (da1 >= 0 || da2 >= 0) {
+    chain[NV] = mjMAX(da1, da2);
+    if (da1 == chain[NV]) da1 = m->dof_parentid[da1];
+    if (da2 == chain[NV]) da2 = m->dof_parentid[da2];
+    NV++;
+  }
+  for (int i = 0; i < NV/2; i++) {
+    int tmp = chain[i];
+    chain[i] = chain[NV-i-1];
+    chain[NV-i-1] = tmp;
+  }
+  return NV;
+}
+
+/* mj_mergeChainSimple :309-336 */
+static int mj_mergeChainSimple(const mjhipModel* m, int* chain, int b1, int b2) {
+  if (b1 > b2) {
+    int tmp = b1;
+    b1 = b2;
+    b2 = tmp;
+  }
+  int n1 = m->body_dofnum[b1], n2 = m->body_dofnum[b2];
+  if (n1 == 0 && n2 == 0) return 0;
+  for (int i = 0; i < n1; i++) chain[i] = m->body_dofadr[b1] + i;
+  for (int i = 0; i < n2; i++) chain[n1+i] = m->body_dofadr[b2] + i;
+  return n1 + n2;
+}
+
+/* mj_jacSparse :526-591: the 3 x NV Jacobians over `chain` */
+static void mj_jacSparse(const mjhipModel* m, const mjhipData* d, mjtNum* jacp, mjtNum* jacr,
+                         const mjtNum* point, int body, int NV, const int* chain) {
+  if (jacp) mju_zero(jacp, 3*NV);
+  if (jacr) mju_zero(jacr, 3*NV);
+  mjtNum offset[3];
+  mju_sub3(offset, point, d->subtree_com+3*m->body_rootid[body]);
+  while (body && !m->body_dofnum[body]) body = m->body_parentid[body];
+  if (!body) return;
+  int da = m->body_dofadr[body] + m->body_dofnum[body] - 1;
+  int ci = NV-1;
+  while (da >= 0) {
+    while (ci >= 0 && chain[ci] > da) ci--;
+    /* chain[ci] == da: the chain holds every ancestral dof (SHOULD NOT OCCUR otherwise) */
+    const mjtNum* cdof = d->cdof + 6*da;
+    if (jacr) {
+      jacr[ci+0*NV] = cdof[0];
+      jacr[ci+1*NV] = cdof[1];
+      jacr[ci+2*NV] = cdof[2];
+    }
+    if (jacp) {
+      mjtNum tmp[3];
+      mju_cross(tmp, cdof, offset);
+      jacp[ci+0*NV] = cdof[3] + tmp[0];
+      jacp[ci+1*NV] = cdof[4] + tmp[1];
+      jacp[ci+2*NV] = cdof[5] + tmp[2];
+    }
+    da = m->dof_parentid[da];
+  }
+}
+
+/* mj_jacSparseSimple :596-654: the signed Jacobian of a simple body straight into the
+ * difference, at chain positions start.. */
+static void mj_jacSparseSimple(const mjhipModel* m, const mjhipData* d, mjtNum* jacdifp,
+                               mjtNum* jacdifr, const mjtNum* point, int body, int flg_second,
+                               int NV, int start) {
+  mjtNum offset[3];
+  mju_sub3(offset, point, d->subtree_com+3*m->body_rootid[body]);
+  if (!m->body_dofnum[body]) return;
+  int ci = start;
+  int end = m->body_dofadr[body] + m->body_dofnum[body];
+  for (int da = m->body_dofadr[body]; da < end; da++) {
+    const mjtNum* cdof = d->cdof+6*da;
+    if (jacdifr) {
+      if (flg_second) {
+        jacdifr[ci+0*NV] = cdof[0];
+        jacdifr[ci+1*NV] = cdof[1];
+        jacdifr[ci+2*NV] = cdof[2];
+      } else {
+        jacdifr[ci+0*NV] = -cdof[0];
+        jacdifr[ci+1*NV] = -cdof[1];
+        jacdifr[ci+2*NV] = -cdof[2];
+      }
+    }
+    if (jacdifp) {
+      mjtNum tmp[3];
+      mju_cross(tmp, cdof, offset);
+      if (flg_second) {
+        jacdifp[ci+0*NV] = (cdof[3] + tmp[0]);
+        jacdifp[ci+1*NV] = (cdof[4] + tmp[1]);
+        jacdifp[ci+2*NV] = (cdof[5] + tmp[2]);
+      } else {
+        jacdifp[ci+0*NV] = -(cdof[3] + tmp[0]);
+        jacdifp[ci+1*NV] = -(cdof[4] + tmp[1]);
+        jacdifp[ci+2*NV] = -(cdof[5] + tmp[2]);
+      }
+    }
+    ci++;
+  }
+}
+
+/* mj_jacDifPair :659-731: pos2 - pos1 Jacobians, dense (NV = nv) or over the merged chain */
+static int mj_jacDifPair(const mjhipModel* m, const mjhipData* d, int* chain, int b1, int b2,
+                         const mjtNum pos1[3], const mjtNum pos2[3], mjtNum* jac1p,
+                         mjtNum* jac2p, mjtNum* jacdifp, mjtNum* jac1r, mjtNum* jac2r,
+                         mjtNum* jacdifr) {
+  int issimple = (m->body_simple[b1] && m->body_simple[b2]);
+  int issparse = mj_isSparse(m);
+  int NV = m->nv;
+  if (!NV) return 0;
+  if (issparse) {
+    NV = issimple ? mj_mergeChainSimple(m, chain, b1, b2) : mj_mergeChain(m, chain, b1, b2);
+  }
+  if (!NV) return 0;
+  if (issparse) {
+    if (issimple) {
+      mj_jacSparseSimple(m, d, jacdifp, jacdifr, pos1, b1, 0, NV,
+                         b1 < b2 ? 0 : m->body_dofnum[b2]);
+      mj_jacSparseSimple(m, d, jacdifp, jacdifr, pos2, b2, 1, NV,
+                         b2 < b1 ? 0 : m->body_dofnum[b1]);
+    } else {
+      mj_jacSparse(m, d, jac1p, jac1r, pos1, b1, NV, chain);
+      mj_jacSparse(m, d, jac2p, jac2r, pos2, b2, NV, chain);
+      if (jacdifp) mju_sub(jacdifp, jac2p, jac1p, 3*NV);
+      if (jacdifr) mju_sub(jacdifr, jac2r, jac1r, 3*NV);
+    }
+  } else {
+    mj_jac(m, d, jac1p, jac1r, pos1, b1);
+    mj_jac(m, d, jac2p, jac2r, pos2, b2);
+    if (jacdifp) mju_sub(jacdifp, jac2p, jac1p, 3*NV);
+    if (jacdifr) mju_sub(jacdifr, jac2r, jac1r, 3*NV);
+  }
+  return NV;
+}
+
+/* mju_combineSparse engine_util_sparse.h:244-303: dst = a*dst + b*src over the union of the
+ * two index sets (buf/buf_ind: scratch of the result's size) */
+static int mju_combineSparse(mjtNum* dst, const mjtNum* src, mjtNum a, mjtNum b, int dst_nnz,
+                             int src_nnz, int* dst_ind, const int* src_ind, mjtNum* buf,
+                             int* buf_ind) {
+  if (dst_nnz == src_nnz && !memcmp(dst_ind, src_ind, dst_nnz*sizeof(int))) {
+    for (int i = 0; i < dst_nnz; i++) dst[i] = dst[i]*a + src[i]*b;   /* mju_addToSclScl */
+    return dst_nnz;
+  }
+  if (dst_nnz) {
+    memcpy(buf, dst, dst_nnz*sizeof(mjtNum));
+    memcpy(buf_ind, dst_ind, dst_nnz*sizeof(int));
+  }
+  int bi = 0, si = 0, nnz = 0, buf_nnz = dst_nnz;
+  while (bi < buf_nnz && si < src_nnz) {
+    int badr = buf_ind[bi], sadr = src_ind[si];
+    if (badr == sadr) {
+      dst[nnz] = a*buf[bi++] + b*src[si++];
+      dst_ind[nnz++] = badr;
+    } else if (badr < sadr) {
+      dst[nnz] = a*buf[bi++];
+      dst_ind[nnz++] = badr;
+    } else {
+      dst[nnz] = b*src[si++];
+      dst_ind[nnz++] = sadr;
+    }
+  }
+  while (si < src_nnz) {
+    dst[nnz] = b*src[si];
+    dst_ind[nnz++] = src_ind[si++];
+  }
+  while (bi < buf_nnz) {
+    dst[nnz] = a*buf[bi];
+    dst_ind[nnz++] = buf_ind[bi++];
+  }
+  return nnz;
+}
+
+/* mju_mulMatVecSparse engine_util_sparse.c:156-167 (the AVX build's supernode path groups
+ * each row's products the same way, engine_util_sparse_avx.h:116-249) */
+static void mju_mulMatVecSparse(mjtNum* res, const mjtNum* mat, const mjtNum* vec, int nr,
+                                const int* rownnz, const int* rowadr, const int* colind) {
+  for (int r = 0; r < nr; r++) {
+    res[r] = mju_dotSparse(mat+rowadr[r], vec, rownnz[r], colind+rowadr[r]);
+  }
+}
+
+/* mju_transposeSparse engine_util_sparse.c:474-515 */
+static void mju_transposeSparse(mjtNum* res, const mjtNum* mat, int nr, int nc, int* res_rownnz,
+                                int* res_rowadr, int* res_colind, const int* rownnz,
+                                const int* rowadr, const int* colind) {
+  memset(res_rownnz, 0, nc*sizeof(int));
+  for (int r = 0; r < nr; r++) {
+    for (int j = rowadr[r]; j < rowadr[r] + rownnz[r]; j++) res_rownnz[colind[j]]++;
+  }
+  res_rowadr[0] = 0;
+  for (int i = 1; i < nc; i++) res_rowadr[i] = res_rowadr[i-1] + res_rownnz[i-1];
+  for (int r = 0; r < nr; r++) {
+    for (int i = rowadr[r]; i < rowadr[r] + rownnz[r]; i++) {
+      int c = res_rowadr[colind[i]]++;
+      res_colind[c] = r;
+      res[c] = mat[i];
+    }
+  }
+  for (int i = nc-1; i > 0; i--) res_rowadr[i] = res_rowadr[i-1];
+  res_rowadr[0] = 0;
+}
+
+/* value of tendon t's Jacobian at dof col: dense row, or the compressed row of a sparse
+ * model (the derivative code reads single entries) */
+static mjtNum ten_J_at(const mjhipModel* m, const mjhipData* d, int t, int col) {
+  if (!mj_isSparse(m)) return d->ten_J[t*m->nv + col];
+  for (int k = 0; k < d->ten_J_rownnz[t]; k++) {
+    if (d->ten_J_colind[d->ten_J_rowadr[t]+k] == col) return d->ten_J[d->ten_J_rowadr[t]+k];
+  }
+  return 0;
+}
+
+/* :1194-1251, dense case. The sparse case (:1211-1230) forms the same column values over
+ * the body's chain and adds only those, so qfrc_target gets the same values. */
 static void mj_applyFT(const mjhipModel* m, mjhipData* d, const mjtNum force[3],
                        const mjtNum torque[3], const mjtNum point[3], int body,
                        mjtNum* qfrc_target) {
@@ -464,11 +691,6 @@ static void mj_integratePos(const mjhipModel* m, mjtNum* qpos, const mjtNum* qve
 }
 
 /*============================ engine_core_smooth.c ========================================*/
-
-/* mj_isSparse, engine_core_constraint.c:96-103 */
-static int mj_isSparse(const mjhipModel* m) {
-  return m->opt.jacobian == mjhipJAC_SPARSE || (m->opt.jacobian == mjhipJAC_AUTO && m->nv >= 60);
-}
 
 /* :38-178 */
 void or_kinematics(const mjhipModel* m, mjhipData* d) {
@@ -922,22 +1144,40 @@ static mjtNum or_wrap(mjtNum wpnt[6], const mjtNum x0[3], const mjtNum x1[3],
 static void mju_mulMatTVec(mjtNum* res, const mjtNum* mat, const mjtNum* vec, int nr, int nc);
 
 static void or_tendon(const mjhipModel* m, mjhipData* d) {
-  int nv = m->nv, nten = m->ntendon;
+  int nv = m->nv, nten = m->ntendon, issparse = mj_isSparse(m);
   mjtNum *L = d->ten_length, *J = d->ten_J;
+  int *rownnz = d->ten_J_rownnz, *rowadr = d->ten_J_rowadr, *colind = d->ten_J_colind;
   if (!nten) return;
   mju_zero(L, nten);
-  mju_zero(J, nten*nv);
+  /* clear the Jacobian: sparse or dense (:677-682) */
+  if (issparse) {
+    memset(rownnz, 0, nten*sizeof(int));
+  } else {
+    mju_zero(J, nten*nv);
+  }
   mjtNum* jac1 = (mjtNum*)malloc(sizeof(mjtNum)*3*(nv ? nv : 1));
   mjtNum* jac2 = (mjtNum*)malloc(sizeof(mjtNum)*3*(nv ? nv : 1));
+  mjtNum* jacdif = (mjtNum*)malloc(sizeof(mjtNum)*3*(nv ? nv : 1));
   mjtNum* tmp = (mjtNum*)malloc(sizeof(mjtNum)*(nv ? nv : 1));
+  mjtNum* sparse_buf = (mjtNum*)malloc(sizeof(mjtNum)*(nv ? nv : 1));
+  int* chain = (int*)malloc(sizeof(int)*(nv ? nv : 1));
+  int* buf_ind = (int*)malloc(sizeof(int)*(nv ? nv : 1));
   for (int i = 0; i < nten; i++) {
     int adr = m->tendon_adr[i];
     int tendon_num = m->tendon_num[i];
+    if (issparse) rowadr[i] = (i > 0 ? rowadr[i-1] + rownnz[i-1] : 0);
     if (m->wrap_type[adr] == mjhipWRAP_JOINT) {
       for (int j = 0; j < tendon_num; j++) {
         int k = m->wrap_objid[adr+j];
         L[i] += m->wrap_prm[adr+j] * d->qpos[m->jnt_qposadr[k]];
-        J[i*nv + m->jnt_dofadr[k]] = m->wrap_prm[adr+j];
+        if (issparse) {
+          /* :709-714: combine the joint's coefficient into the row (a repeated joint adds) */
+          rownnz[i] = mju_combineSparse(J+rowadr[i], &m->wrap_prm[adr+j], 1, 1, rownnz[i], 1,
+                                        colind+rowadr[i], &m->jnt_dofadr[k], sparse_buf,
+                                        buf_ind);
+        } else {
+          J[i*nv + m->jnt_dofadr[k]] = m->wrap_prm[adr+j];
+        }
       }
       continue;
     }
@@ -987,22 +1227,39 @@ static void or_tendon(const mjhipModel* m, mjhipData* d) {
         mjtNum dif[3];
         mju_sub3(dif, wpnt+3*k+3, wpnt+3*k);
         mju_normalize3(dif);
-        mj_jac(m, d, jac1, NULL, wpnt+3*k, wbody[k]);
-        mj_jac(m, d, jac2, NULL, wpnt+3*k+3, wbody[k+1]);
-        for (int c = 0; c < 3*nv; c++) jac2[c] = jac2[c] - jac1[c];
-        mju_mulMatTVec(tmp, jac2, dif, 3, nv);
-        mju_addToScl(J + i*nv, tmp, 1/divisor, nv);
+        if (issparse) {
+          /* :801-819: the chain rule over the merged chain, combined into the row */
+          int NV = mj_jacDifPair(m, d, chain, wbody[k], wbody[k+1], wpnt+3*k, wpnt+3*k+3,
+                                 jac1, jac2, jacdif, NULL, NULL, NULL);
+          if (!NV) continue;
+          mju_mulMatTVec(tmp, jacdif, dif, 3, NV);
+          rownnz[i] = mju_combineSparse(J+rowadr[i], tmp, 1, 1/divisor, rownnz[i], NV,
+                                        colind+rowadr[i], chain, sparse_buf, buf_ind);
+        } else {
+          mj_jac(m, d, jac1, NULL, wpnt+3*k, wbody[k]);
+          mj_jac(m, d, jac2, NULL, wpnt+3*k+3, wbody[k+1]);
+          for (int c = 0; c < 3*nv; c++) jac2[c] = jac2[c] - jac1[c];
+          mju_mulMatTVec(tmp, jac2, dif, 3, nv);
+          mju_addToScl(J + i*nv, tmp, 1/divisor, nv);
+        }
       }
       j += wrapped ? 2 : 1;
     }
   }
   free(jac1);
   free(jac2);
+  free(jacdif);
   free(tmp);
+  free(sparse_buf);
+  free(chain);
+  free(buf_ind);
 }
 
 /* :865-916, joint transmission (slide/hinge) */
 static mjtNum mju_dot3(const mjtNum* a, const mjtNum* b);
+
+static void or_mulJacTVec(const mjhipModel* m, const orEfc* e, mjtNum* res,
+                          const mjtNum* vec);
 
 /* engine_core_smooth.c:862-1100 mj_transmission: joint (slide/hinge/ball/free, in the
  * joint or the parent frame) and tendon transmissions (fixed tendons: their sparsity is a
@@ -1191,23 +1448,41 @@ static void or_transmission(const mjhipModel* m, mjhipData* d, const orEfc* e) {
           counter++;
           const mjtNum* pos = e->con_pos + 3*j;
           const mjtNum* frame = e->con_frame + 9*j;
-          mj_jac(m, d, jac1, NULL, pos, b1);
-          mj_jac(m, d, jac2, NULL, pos, b2);
-          for (int k = 0; k < 3*nv; k++) jac2[k] = jac2[k] - jac1[k];
-          mju_zero(jrow, nv);              /* mju_mulMatMat(jac, frame, jacdif, 1, 3, nv) */
+          int* chain = (int*)malloc(sizeof(int)*(nv ? nv : 1));
+          mjtNum* jacd = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+          int NV = mj_jacDifPair(m, d, chain, b1, b2, pos, pos, jac1, jac2, jacd, NULL, NULL,
+                                 NULL);
+          mju_zero(jrow, nv);              /* mju_mulMatMat(jac, frame, jacdif, 1, 3, NV) */
           for (int k = 0; k < 3; k++) {
-            if (frame[k]) mju_addToScl(jrow, jac2 + k*nv, frame[k], nv);
+            if (frame[k]) mju_addToScl(jrow, jacd + k*NV, frame[k], NV);
           }
-          mju_addTo(mexcl, jrow, nv);
+          if (mj_isSparse(m)) {            /* :1304-1307 */
+            for (int k = 0; k < NV; k++) mexcl[chain[k]] += jrow[k];
+          } else {
+            mju_addTo(mexcl, jrow, nv);
+          }
+          free(chain);
+          free(jacd);
         }
       }
       if (counter) {
-        mju_mulMatTVec(moment, e->efc_J, force, e->nefc, nv);   /* mj_mulJacTVec, dense */
+        or_mulJacTVec(m, e, moment, force);   /* mj_mulJacTVec :426-442 */
         mju_addTo(moment, mexcl, nv);
         mju_scl(moment, moment, -1.0/counter, nv);
       }
       for (int k = 0; k < m->moment_rownnz[i]; k++) moment[k] = moment[m->moment_colind[adr+k]];
       free(force); free(mexcl); free(jac1); free(jac2); free(jrow);
+    } else if (mj_isSparse(m)) {   /* mjTRN_TENDON, sparse (:1060-1067): gear*ten_J over
+                                       the tendon's row, whose pattern the model's must be */
+      *length = d->ten_length[id]*gear[0];
+      int nnz = d->ten_J_rownnz[id], tadr = d->ten_J_rowadr[id];
+      if (nnz != m->moment_rownnz[i] ||
+          memcmp(d->ten_J_colind + tadr, m->moment_colind + adr, nnz*sizeof(int))) {
+        d->status |= MJHIP_INST_UNSUPPORTED;   /* a state-dependent pattern (spatial tendon) */
+      }
+      for (int k = 0; k < m->moment_rownnz[i] && k < nnz; k++) {
+        moment[k] = d->ten_J[tadr + k]*gear[0];
+      }
     } else {   /* mjTRN_TENDON, dense: gear*ten_J compressed to its nonzeros */
       *length = d->ten_length[id]*gear[0];
       for (int k = 0; k < m->moment_rownnz[i]; k++) {
@@ -1417,7 +1692,7 @@ void or_rne(const mjhipModel* m, mjhipData* d, int flg_acc, mjtNum* result) {
 
 /*============================ engine_passive.c ============================================*/
 
-/* :57-378 (joint springs, dof dampers, dense tendon spring-dampers) */
+/* :57-378 (joint springs, dof dampers, tendon spring-dampers) */
 static void or_springdamper(const mjhipModel* m, mjhipData* d) {
   int nv = m->nv, njnt = m->njnt, ntendon = m->ntendon;
   for (int i = 0; i < njnt; i++) {
@@ -1468,8 +1743,20 @@ static void or_springdamper(const mjhipModel* m, mjhipData* d) {
       frc_spring = stiffness * (lower - length);
     }
     mjtNum frc_damper = -damping * d->ten_velocity[i];
-    if (frc_spring) mju_addToScl(d->qfrc_spring, d->ten_J+i*nv, frc_spring, nv);
-    if (frc_damper) mju_addToScl(d->qfrc_damper, d->ten_J+i*nv, frc_damper, nv);
+    if (mj_isSparse(m)) {                  /* :361-370 */
+      if (frc_spring || frc_damper) {
+        int end = d->ten_J_rowadr[i] + d->ten_J_rownnz[i];
+        for (int j = d->ten_J_rowadr[i]; j < end; j++) {
+          int k = d->ten_J_colind[j];
+          mjtNum J = d->ten_J[j];
+          d->qfrc_spring[k] += J * frc_spring;
+          d->qfrc_damper[k] += J * frc_damper;
+        }
+      }
+    } else {
+      if (frc_spring) mju_addToScl(d->qfrc_spring, d->ten_J+i*nv, frc_spring, nv);
+      if (frc_damper) mju_addToScl(d->qfrc_damper, d->ten_J+i*nv, frc_damper, nv);
+    }
   }
 }
 
@@ -4604,18 +4891,37 @@ static void mju_mulMatMat(mjtNum* res, const mjtNum* mat1, const mjtNum* mat2, i
   }
 }
 
-/* :265-356, dense Jacobian branch */
+/* :265-356 mj_addConstraint: dense rows are dropped when all-zero (non-contact types); sparse
+ * rows copy the chain and are dropped only when it is empty */
 static void mj_addConstraint(const mjhipModel* m, orEfc* e, const mjtNum* jac, const mjtNum* pos,
                              const mjtNum* margin, mjtNum frictionloss, int size, int type,
-                             int id) {
+                             int id, int NV, const int* chain) {
   int nv = m->nv, nefc = e->nefc;
+  int *nnz = e->efc_J_rownnz, *adr = e->efc_J_rowadr, *ind = e->efc_J_colind;
   int empty = !(type == orCNSTR_CONTACT_FRICTIONLESS || type == orCNSTR_CONTACT_PYRAMIDAL ||
                 type == orCNSTR_CONTACT_ELLIPTIC);
-  for (int i = 0; empty && i < size*nv; i++) {
-    if (jac[i]) empty = 0;
+  if (!mj_isSparse(m)) {
+    for (int i = 0; empty && i < size*nv; i++) {
+      if (jac[i]) empty = 0;
+    }
+    if (!empty) mju_copy(e->efc_J + nefc*nv, jac, size*nv);
+  } else {
+    NV = mjMAX(0, NV);
+    if (NV) {
+      empty = 0;
+    } else if (empty) {
+      return;
+    }
+    for (int i = 0; i < size; i++) {
+      adr[nefc+i] = (nefc+i ? adr[nefc+i-1]+nnz[nefc+i-1] : 0);
+      nnz[nefc+i] = NV;
+      if (NV) {
+        memcpy(ind + adr[nefc+i], chain, NV*sizeof(int));
+        mju_copy(e->efc_J + adr[nefc+i], jac + i*NV, NV);
+      }
+    }
   }
   if (empty) return;
-  mju_copy(e->efc_J + nefc*nv, jac, size*nv);
   for (int i = 0; i < size; i++) {
     e->efc_pos[nefc+i] = (pos ? pos[i] : 0);
     e->efc_margin[nefc+i] = (margin ? margin[i] : 0);
@@ -4642,20 +4948,23 @@ static void mju_mulQuatAxis(mjtNum res[4], const mjtNum quat[4], const mjtNum ax
   res[0] = tmp[0]; res[1] = tmp[1]; res[2] = tmp[2]; res[3] = tmp[3];
 }
 
-/* mj_instantiateEquality :493-764, dense; connect, weld, joint and tendon (flex is outside
- * the supported subset). eq_active is the model's eq_active0 (mj_resetData). */
+/* mj_instantiateEquality :493-764: connect, weld, joint and tendon (flex is outside the
+ * supported subset), dense (NV = nv) or over the merged chain of a sparse model. eq_active is
+ * the model's eq_active0 (mj_resetData). */
 static void or_instantiateEquality(const mjhipModel* m, mjhipData* d, orEfc* e) {
-  int nv = m->nv;
+  int nv = m->nv, issparse = mj_isSparse(m);
   if (mjDISABLED(mjhipDSBL_EQUALITY) || m->neq == 0) return;
-  mjtNum* jac0 = (mjtNum*)calloc(6*(size_t)nv + 1, sizeof(mjtNum));
-  mjtNum* jac1 = (mjtNum*)calloc(6*(size_t)nv + 1, sizeof(mjtNum));
-  mjtNum* jacdif = (mjtNum*)calloc(6*(size_t)nv + 1, sizeof(mjtNum));
-  mjtNum* jt0 = (mjtNum*)calloc(6*(size_t)nv + 1, sizeof(mjtNum));
-  mjtNum* jt1 = (mjtNum*)calloc(6*(size_t)nv + 1, sizeof(mjtNum));
+  size_t n6 = 6*(size_t)nv + 1;
+  mjtNum* jac[2] = {(mjtNum*)calloc(n6, sizeof(mjtNum)), (mjtNum*)calloc(n6, sizeof(mjtNum))};
+  mjtNum* jacdif = (mjtNum*)calloc(n6, sizeof(mjtNum));
+  mjtNum* sparse_buf = (mjtNum*)calloc(nv + 1, sizeof(mjtNum));
+  int* chain = (int*)calloc(nv + 1, sizeof(int));
+  int* chain2 = (int*)calloc(nv + 1, sizeof(int));
+  int* buf_ind = (int*)calloc(nv + 1, sizeof(int));
   for (int i = 0; i < m->neq; i++) {
     if (!m->eq_active0[i]) continue;
     const mjtNum* data = m->eq_data + mjhipNEQDATA*i;
-    int id[2] = {m->eq_obj1id[i], m->eq_obj2id[i]}, body_id[2], size = 0;
+    int id[2] = {m->eq_obj1id[i], m->eq_obj2id[i]}, body_id[2], size = 0, NV = 0, NV2 = 0;
     mjtNum cpos[6], pos[2][3], ref[2], quat[4], quat1[4], quat2[4], quat3[4], axis[3];
     switch (m->eq_type[i]) {
     case mjhipEQ_CONNECT:
@@ -4672,11 +4981,10 @@ static void or_instantiateEquality(const mjhipModel* m, mjhipData* d, orEfc* e) 
         }
       }
       mju_sub3(cpos, pos[0], pos[1]);
-      /* mj_jacDifPair(b1 = body_id[1], b2 = body_id[0]), dense: jac2 - jac1 */
-      mj_jac(m, d, jt1, NULL, pos[1], body_id[1]);
-      mj_jac(m, d, jt0, NULL, pos[0], body_id[0]);
-      mju_sub(jacdif, jt0, jt1, 3*nv);
-      mju_copy(jac0, jacdif, 3*nv);
+      /* Jacobian difference (opposite of contact: 0 - 1) */
+      NV = mj_jacDifPair(m, d, chain, body_id[1], body_id[0], pos[1], pos[0], jac[1], jac[0],
+                         jacdif, NULL, NULL, NULL);
+      mju_copy(jac[0], jacdif, 3*NV);
       size = 3;
       break;
     case mjhipEQ_WELD: {
@@ -4695,12 +5003,11 @@ static void or_instantiateEquality(const mjhipModel* m, mjhipData* d, orEfc* e) 
       }
       mju_sub3(cpos, pos[0], pos[1]);
       mjtNum torquescale = data[10];
-      mj_jac(m, d, jt1, jt1 + 3*nv, pos[1], body_id[1]);
-      mj_jac(m, d, jt0, jt0 + 3*nv, pos[0], body_id[0]);
-      mju_sub(jacdif, jt0, jt1, 3*nv);
-      mju_sub(jacdif + 3*nv, jt0 + 3*nv, jt1 + 3*nv, 3*nv);
-      mju_copy(jac0, jacdif, 3*nv);
-      mju_copy(jac0 + 3*nv, jacdif + 3*nv, 3*nv);
+      NV = mj_jacDifPair(m, d, chain, body_id[1], body_id[0], pos[1], pos[0], jac[1], jac[0],
+                         jacdif, jac[1] + 3*nv, jac[0] + 3*nv, jacdif + 3*nv);
+      /* translation:rotation compressed to NV columns each */
+      mju_copy(jac[0], jacdif, 3*NV);
+      mju_copy(jac[0] + 3*NV, jacdif + 3*nv, 3*NV);
       if (m->eq_objtype[i] == OBJ_BODY) {
         mju_mulQuat(quat, d->xquat + 4*id[0], data + 6);
         mju_copy4(quat1, d->xquat + 4*id[1]);
@@ -4713,33 +5020,45 @@ static void or_instantiateEquality(const mjhipModel* m, mjhipData* d, orEfc* e) 
       quat1[1] = -quat1[1]; quat1[2] = -quat1[2]; quat1[3] = -quat1[3];
       mju_mulQuat(quat2, quat1, quat);
       mju_scl3(cpos + 3, quat2 + 1, torquescale);
-      for (int j = 0; j < nv; j++) {
-        axis[0] = jac0[3*nv + j];
-        axis[1] = jac0[4*nv + j];
-        axis[2] = jac0[5*nv + j];
+      for (int j = 0; j < NV; j++) {
+        axis[0] = jac[0][3*NV + j];
+        axis[1] = jac[0][4*NV + j];
+        axis[2] = jac[0][5*NV + j];
         mju_mulQuatAxis(quat2, quat1, axis);
         mju_mulQuat(quat3, quat2, quat);
-        jac0[3*nv + j] = 0.5*quat3[1];
-        jac0[4*nv + j] = 0.5*quat3[2];
-        jac0[5*nv + j] = 0.5*quat3[3];
+        jac[0][3*NV + j] = 0.5*quat3[1];
+        jac[0][4*NV + j] = 0.5*quat3[2];
+        jac[0][5*NV + j] = 0.5*quat3[3];
       }
-      mju_scl(jac0 + 3*nv, jac0 + 3*nv, torquescale, 3*nv);
+      mju_scl(jac[0] + 3*NV, jac[0] + 3*NV, torquescale, 3*NV);
       size = 6;
       break;
     }
     case mjhipEQ_JOINT:
     case mjhipEQ_TENDON: {
-      mjtNum* jac[2] = {jac0, jac1};
       for (int j = 0; j < 1 + (id[1] >= 0); j++) {
         if (m->eq_type[i] == mjhipEQ_JOINT) {
           pos[j][0] = d->qpos[m->jnt_qposadr[id[j]]];
           ref[j] = m->qpos0[m->jnt_qposadr[id[j]]];
-          mju_zero(jac[j], nv);
-          jac[j][m->jnt_dofadr[id[j]]] = 1;
+          if (issparse) {
+            *(j == 0 ? &NV : &NV2) = 1;
+            (j == 0 ? chain : chain2)[0] = m->jnt_dofadr[id[j]];
+            jac[j][0] = 1;
+          } else {
+            mju_zero(jac[j], nv);
+            jac[j][m->jnt_dofadr[id[j]]] = 1;
+          }
         } else {
           pos[j][0] = d->ten_length[id[j]];
           ref[j] = m->tendon_length0[id[j]];
-          mju_copy(jac[j], d->ten_J + id[j]*nv, nv);
+          if (issparse) {
+            int tn = d->ten_J_rownnz[id[j]], ta = d->ten_J_rowadr[id[j]];
+            *(j == 0 ? &NV : &NV2) = tn;
+            memcpy(j == 0 ? chain : chain2, d->ten_J_colind + ta, tn*sizeof(int));
+            mju_copy(jac[j], d->ten_J + ta, tn);
+          } else {
+            mju_copy(jac[j], d->ten_J + id[j]*nv, nv);
+          }
         }
       }
       if (id[1] >= 0) {
@@ -4748,7 +5067,12 @@ static void or_instantiateEquality(const mjhipModel* m, mjhipData* d, orEfc* e) 
                   (data[1]*dif + data[2]*dif*dif + data[3]*dif*dif*dif +
                    data[4]*dif*dif*dif*dif);
         mjtNum deriv = data[1] + 2*data[2]*dif + 3*data[3]*dif*dif + 4*data[4]*dif*dif*dif;
-        mju_addToScl(jac0, jac1, -deriv, nv);
+        if (issparse) {
+          NV = mju_combineSparse(jac[0], jac[1], 1, -deriv, NV, NV2, chain, chain2, sparse_buf,
+                                 buf_ind);
+        } else {
+          mju_addToScl(jac[0], jac[1], -deriv, nv);
+        }
       } else {
         cpos[0] = pos[0][0] - ref[0] - data[0];
       }
@@ -4756,34 +5080,45 @@ static void or_instantiateEquality(const mjhipModel* m, mjhipData* d, orEfc* e) 
       break;
     }
     }
-    if (size) mj_addConstraint(m, e, jac0, cpos, 0, 0, size, orCNSTR_EQUALITY, i);
+    if (size) {
+      mj_addConstraint(m, e, jac[0], cpos, 0, 0, size, orCNSTR_EQUALITY, i,
+                       issparse ? NV : 0, issparse ? chain : NULL);
+    }
   }
-  free(jac0); free(jac1); free(jacdif); free(jt0); free(jt1);
+  free(jac[0]); free(jac[1]); free(jacdif); free(sparse_buf);
+  free(chain); free(chain2); free(buf_ind);
 }
 
-/* mj_instantiateFriction :768-822 (dense): dof friction, then tendon friction on the
-   tendon's ten_J row (mj_addConstraint skips a row whose Jacobian is all zero) */
+/* mj_instantiateFriction :768-822: dof friction, then tendon friction on the tendon's ten_J
+   row (dense: a row whose Jacobian is all zero is skipped; sparse: one whose chain is) */
 static void or_instantiateFriction(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum* jac) {
-  int nv = m->nv;
+  int nv = m->nv, issparse = mj_isSparse(m);
   if (mjDISABLED(mjhipDSBL_FRICTIONLOSS)) return;
   for (int i = 0; i < nv; i++) {
     if (m->dof_frictionloss[i] > 0) {
-      mju_zero(jac, nv);
-      jac[i] = 1;
-      mj_addConstraint(m, e, jac, 0, 0, m->dof_frictionloss[i], 1, orCNSTR_FRICTION_DOF, i);
+      if (issparse) {
+        jac[0] = 1;
+      } else {
+        mju_zero(jac, nv);
+        jac[i] = 1;
+      }
+      mj_addConstraint(m, e, jac, 0, 0, m->dof_frictionloss[i], 1, orCNSTR_FRICTION_DOF, i,
+                       issparse ? 1 : 0, issparse ? &i : NULL);
     }
   }
   for (int i = 0; i < m->ntendon; i++) {
     if (m->tendon_frictionloss[i] > 0) {
-      mj_addConstraint(m, e, d->ten_J + i*nv, 0, 0, m->tendon_frictionloss[i], 1,
-                       orCNSTR_FRICTION_TENDON, i);
+      mj_addConstraint(m, e, d->ten_J + (issparse ? d->ten_J_rowadr[i] : i*nv), 0, 0,
+                       m->tendon_frictionloss[i], 1, orCNSTR_FRICTION_TENDON, i,
+                       issparse ? d->ten_J_rownnz[i] : 0,
+                       issparse ? d->ten_J_colind + d->ten_J_rowadr[i] : NULL);
     }
   }
 }
 
-/* :824-959, dense */
+/* :824-959 */
 static void or_instantiateLimit(const mjhipModel* m, mjhipData* d, orEfc* e, mjtNum* jac) {
-  int side, nv = m->nv;
+  int side, nv = m->nv, issparse = mj_isSparse(m);
   mjtNum margin, value, dist, angleAxis[3];
   if (mjDISABLED(mjhipDSBL_LIMIT)) return;
   for (int i = 0; i < m->njnt; i++) {
@@ -4794,9 +5129,14 @@ static void or_instantiateLimit(const mjhipModel* m, mjhipData* d, orEfc* e, mjt
         for (side = -1; side <= 1; side += 2) {
           dist = side * (m->jnt_range[2*i+(side+1)/2] - value);
           if (dist < margin) {
-            mju_zero(jac, nv);
-            jac[m->jnt_dofadr[i]] = -(mjtNum)side;
-            mj_addConstraint(m, e, jac, &dist, &margin, 0, 1, orCNSTR_LIMIT_JOINT, i);
+            if (issparse) {
+              jac[0] = -(mjtNum)side;
+            } else {
+              mju_zero(jac, nv);
+              jac[m->jnt_dofadr[i]] = -(mjtNum)side;
+            }
+            mj_addConstraint(m, e, jac, &dist, &margin, 0, 1, orCNSTR_LIMIT_JOINT, i,
+                             issparse ? 1 : 0, issparse ? m->jnt_dofadr + i : NULL);
           }
         }
       } else if (m->jnt_type[i] == mjhipJNT_BALL) {
@@ -4807,9 +5147,15 @@ static void or_instantiateLimit(const mjhipModel* m, mjhipData* d, orEfc* e, mjt
         value = mju_normalize3(angleAxis);
         dist = mjMAX(m->jnt_range[2*i], m->jnt_range[2*i+1]) - value;
         if (dist < margin) {
-          mju_zero(jac, nv);
-          mju_scl3(jac + m->jnt_dofadr[i], angleAxis, -1);
-          mj_addConstraint(m, e, jac, &dist, &margin, 0, 1, orCNSTR_LIMIT_JOINT, i);
+          if (issparse) {
+            int chain[3] = {m->jnt_dofadr[i], m->jnt_dofadr[i] + 1, m->jnt_dofadr[i] + 2};
+            mju_scl3(jac, angleAxis, -1);
+            mj_addConstraint(m, e, jac, &dist, &margin, 0, 1, orCNSTR_LIMIT_JOINT, i, 3, chain);
+          } else {
+            mju_zero(jac, nv);
+            mju_scl3(jac + m->jnt_dofadr[i], angleAxis, -1);
+            mj_addConstraint(m, e, jac, &dist, &margin, 0, 1, orCNSTR_LIMIT_JOINT, i, 0, NULL);
+          }
         }
       }
     }
@@ -4821,18 +5167,25 @@ static void or_instantiateLimit(const mjhipModel* m, mjhipData* d, orEfc* e, mjt
       for (side = -1; side <= 1; side += 2) {
         dist = side * (m->tendon_range[2*i+(side+1)/2] - value);
         if (dist < margin) {
-          mju_scl(jac, d->ten_J+i*nv, -side, nv);
-          mj_addConstraint(m, e, jac, &dist, &margin, 0, 1, orCNSTR_LIMIT_TENDON, i);
+          if (issparse) {
+            mju_scl(jac, d->ten_J + d->ten_J_rowadr[i], -side, d->ten_J_rownnz[i]);
+          } else {
+            mju_scl(jac, d->ten_J+i*nv, -side, nv);
+          }
+          mj_addConstraint(m, e, jac, &dist, &margin, 0, 1, orCNSTR_LIMIT_TENDON, i,
+                           issparse ? d->ten_J_rownnz[i] : 0,
+                           issparse ? d->ten_J_colind + d->ten_J_rowadr[i] : NULL);
         }
       }
     }
   }
 }
 
-/* mj_instantiateContact :964-1131, dense, pyramidal or frictionless (elliptic cones are
- * rejected with contacts) */
+/* mj_instantiateContact :964-1131, pyramidal, elliptic or frictionless, dense (NV = nv) or
+ * over the merged chain of a sparse model (a contact whose chain is empty is excluded,
+ * exclude = 3) */
 static void or_instantiateContact(const mjhipModel* m, mjhipData* d, orEfc* e) {
-  int nv = m->nv;
+  int nv = m->nv, issparse = mj_isSparse(m);
   if (mjDISABLED(mjhipDSBL_CONTACT) || e->ncon == 0 || nv == 0) return;
   mjtNum* jac = (mjtNum*)malloc(6*nv*sizeof(mjtNum));
   mjtNum* jacdif = (mjtNum*)malloc(6*nv*sizeof(mjtNum));
@@ -4840,6 +5193,7 @@ static void or_instantiateContact(const mjhipModel* m, mjhipData* d, orEfc* e) {
   mjtNum* jac2p = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
   mjtNum* jac1r = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
   mjtNum* jac2r = (mjtNum*)malloc(3*nv*sizeof(mjtNum));
+  int* chain = (int*)malloc(nv*sizeof(int));
   mjtNum *jacdifp = jacdif, *jacdifr = jacdif + 3*nv;
   for (int i = 0; i < e->ncon; i++) {
     if (e->con_exclude[i]) continue;
@@ -4847,36 +5201,42 @@ static void or_instantiateContact(const mjhipModel* m, mjhipData* d, orEfc* e) {
     e->con_efc_address[i] = e->nefc;
     int b1 = m->geom_bodyid[e->con_geom[2*i]], b2 = m->geom_bodyid[e->con_geom[2*i+1]];
     const mjtNum* cpos_ = e->con_pos + 3*i;
-    /* mj_jacDifPair (engine_support.c:656-733), dense */
-    mj_jac(m, d, jac1p, jac1r, cpos_, b1);
-    mj_jac(m, d, jac2p, jac2r, cpos_, b2);
-    mju_sub(jacdifp, jac2p, jac1p, 3*nv);
-    if (dim > 3) mju_sub(jacdifr, jac2r, jac1r, 3*nv);
+    int NV = mj_jacDifPair(m, d, chain, b1, b2, cpos_, cpos_, jac1p, jac2p, jacdifp,
+                           dim > 3 ? jac1r : NULL, dim > 3 ? jac2r : NULL,
+                           dim > 3 ? jacdifr : NULL);
+    if (NV == 0) {                         /* :1071-1076 */
+      e->con_efc_address[i] = -1;
+      e->con_exclude[i] = 3;
+      continue;
+    }
     /* rotate to the contact frame */
     const mjtNum* frame = e->con_frame + 9*i;
-    mju_mulMatMat(jac, frame, jacdifp, dim > 1 ? 3 : 1, 3, nv);
-    if (dim > 3) mju_mulMatMat(jac + 3*nv, frame, jacdifr, dim-3, 3, nv);
+    mju_mulMatMat(jac, frame, jacdifp, dim > 1 ? 3 : 1, 3, NV);
+    if (dim > 3) mju_mulMatMat(jac + 3*NV, frame, jacdifr, dim-3, 3, NV);
     if (dim == 1) {
       mj_addConstraint(m, e, jac, e->con_dist + i, e->con_includemargin + i, 0, 1,
-                       orCNSTR_CONTACT_FRICTIONLESS, i);
+                       orCNSTR_CONTACT_FRICTIONLESS, i, issparse ? NV : 0,
+                       issparse ? chain : NULL);
     } else if (m->opt.cone == mjhipCONE_ELLIPTIC) {
       /* elliptic cone :1113-1126: the dim rotated rows, pos = (dist, 0, ...) */
       mjtNum cpos[6] = {0}, cmargin[6] = {0};
       cpos[0] = e->con_dist[i];
       cmargin[0] = e->con_includemargin[i];
-      mj_addConstraint(m, e, jac, cpos, cmargin, 0, dim, orCNSTR_CONTACT_ELLIPTIC, i);
+      mj_addConstraint(m, e, jac, cpos, cmargin, 0, dim, orCNSTR_CONTACT_ELLIPTIC, i,
+                       issparse ? NV : 0, issparse ? chain : NULL);
     } else {
       mjtNum cpos[2] = {e->con_dist[i], e->con_dist[i]};
       mjtNum cmargin[2] = {e->con_includemargin[i], e->con_includemargin[i]};
       for (int k = 1; k < dim; k++) {
         mjtNum f = e->con_friction[5*i + k-1];
-        for (int j = 0; j < nv; j++) jacdifp[j] = jac[j] + jac[k*nv+j]*f;
-        for (int j = 0; j < nv; j++) jacdifp[nv+j] = jac[j] + jac[k*nv+j]*(-f);
-        mj_addConstraint(m, e, jacdifp, cpos, cmargin, 0, 2, orCNSTR_CONTACT_PYRAMIDAL, i);
+        for (int j = 0; j < NV; j++) jacdifp[j] = jac[j] + jac[k*NV+j]*f;
+        for (int j = 0; j < NV; j++) jacdifp[NV+j] = jac[j] + jac[k*NV+j]*(-f);
+        mj_addConstraint(m, e, jacdifp, cpos, cmargin, 0, 2, orCNSTR_CONTACT_PYRAMIDAL, i,
+                         issparse ? NV : 0, issparse ? chain : NULL);
       }
     }
   }
-  free(jac); free(jacdif); free(jac1p); free(jac2p); free(jac1r); free(jac2r);
+  free(jac); free(jacdif); free(jac1p); free(jac2p); free(jac1r); free(jac2r); free(chain);
 }
 
 /* :1138-1311 (limit, friction and contact rows) */
@@ -5128,16 +5488,47 @@ static void or_makeConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
   or_instantiateLimit(m, d, e, jac);
   free(jac);
   or_instantiateContact(m, d, e);
+  e->nJ = 0;
   if (!e->nefc) return;
+  /* transpose the sparse Jacobian (:2083-2104; the row supernodes only select the AVX
+     kernels, whose per-row sums group as mju_dotSparse's) */
+  if (mj_isSparse(m)) {
+    e->nJ = e->efc_J_rowadr[e->nefc-1] + e->efc_J_rownnz[e->nefc-1];
+    mju_transposeSparse(e->efc_JT, e->efc_J, e->nefc, m->nv, e->efc_JT_rownnz, e->efc_JT_rowadr,
+                        e->efc_JT_colind, e->efc_J_rownnz, e->efc_J_rowadr, e->efc_J_colind);
+  }
   or_diagApprox(m, e);
   or_makeImpedance(m, e);
+}
+
+/* mj_mulJacVec :361-377: res = J*vec (sparse: mju_mulMatVecSparse over the rows) */
+static void or_mulJacVec(const mjhipModel* m, const orEfc* e, mjtNum* res, const mjtNum* vec) {
+  if (!e->nefc) return;
+  if (mj_isSparse(m)) {
+    mju_mulMatVecSparse(res, e->efc_J, vec, e->nefc, e->efc_J_rownnz, e->efc_J_rowadr,
+                        e->efc_J_colind);
+  } else {
+    mju_mulMatVec(res, e->efc_J, vec, e->nefc, m->nv);
+  }
+}
+
+/* mj_mulJacTVec :426-442: res = J'*vec (sparse: mju_mulMatVecSparse over the rows of JT,
+ * each dof's terms grouped by their position in its JT row) */
+static void or_mulJacTVec(const mjhipModel* m, const orEfc* e, mjtNum* res, const mjtNum* vec) {
+  if (!e->nefc) return;
+  if (mj_isSparse(m)) {
+    mju_mulMatVecSparse(res, e->efc_JT, vec, m->nv, e->efc_JT_rownnz, e->efc_JT_rowadr,
+                        e->efc_JT_colind);
+  } else {
+    mju_mulMatTVec(res, e->efc_J, vec, e->nefc, m->nv);
+  }
 }
 
 /* :2362-2375 */
 static void or_referenceConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
   int nefc = e->nefc;
   mjtNum* KBIP = e->efc_KBIP;
-  if (nefc) mju_mulMatVec(e->efc_vel, e->efc_J, d->qvel, nefc, m->nv);
+  or_mulJacVec(m, e, e->efc_vel, d->qvel);
   for (int i = 0; i < nefc; i++) {
     e->efc_aref[i] = -KBIP[4*i+1]*e->efc_vel[i]
                      -KBIP[4*i]*KBIP[4*i+2]*(e->efc_pos[i]-e->efc_margin[i]);
@@ -5204,15 +5595,21 @@ static void or_constraintUpdate(const mjhipModel* m, mjhipData* d, orEfc* e, con
       i += dim - 1;
     }
   }
-  /* mj_mulJacTVec, dense: mju_mulMatTVec (engine_core_constraint.c:426-442) */
-  mju_mulMatTVec(d->qfrc_constraint, e->efc_J, e->efc_force, nefc, m->nv);
+  /* mj_mulJacTVec_island(island < 0) = mj_mulJacTVec (engine_core_constraint.c:426-442) */
+  or_mulJacTVec(m, e, d->qfrc_constraint, e->efc_force);
 }
 
 /*============================ engine_forward.c / engine_inverse.c =========================*/
 
 /* engine_forward.c:193-231 */
 static void or_fwdVelocity(const mjhipModel* m, mjhipData* d, orEfc* e) {
-  mju_mulMatVec(d->ten_velocity, d->ten_J, d->qvel, m->ntendon, m->nv);
+  /* tendon velocity: dense or sparse (:206-212) */
+  if (mj_isSparse(m)) {
+    mju_mulMatVecSparse(d->ten_velocity, d->ten_J, d->qvel, m->ntendon, d->ten_J_rownnz,
+                        d->ten_J_rowadr, d->ten_J_colind);
+  } else {
+    mju_mulMatVec(d->ten_velocity, d->ten_J, d->qvel, m->ntendon, m->nv);
+  }
   if (!mjDISABLED(mjhipDSBL_ACTUATION)) {
     for (int r = 0; r < m->nu; r++) {
       d->actuator_velocity[r] = mju_dotSparse(d->actuator_moment + m->moment_rowadr[r], d->qvel,
@@ -5252,7 +5649,7 @@ void or_invConstraint(const mjhipModel* m, mjhipData* d, orEfc* e) {
     return;
   }
   mjtNum* jar = (mjtNum*)malloc(nefc*sizeof(mjtNum));
-  mju_mulMatVec(jar, e->efc_J, d->qacc, nefc, m->nv);
+  or_mulJacVec(m, e, jar, d->qacc);
   mju_subFrom(jar, e->efc_aref, nefc);
   or_constraintUpdate(m, d, e, jar);
   free(jar);
@@ -5293,7 +5690,6 @@ static mjtNum moment_at(const mjhipModel* m, const mjhipData* d, int i, int col)
  * damping (mjd_passive_vel :1432-1519), in the reference's order of accumulation. Only the
  * entries on qM's sparsity are needed (the implicitfast reduction through mapD2M). */
 static mjtNum or_qDeriv(const mjhipModel* m, const mjhipData* d, int r, int c) {
-  int nv = m->nv;
   mjtNum q = 0;
   if (!mjDISABLED(mjhipDSBL_ACTUATION)) {
     for (int i = 0; i < m->nu; i++) {
@@ -5312,8 +5708,10 @@ static mjtNum or_qDeriv(const mjhipModel* m, const mjhipData* d, int r, int c) {
     for (int t = 0; t < m->ntendon; t++) {
       if (m->tendon_damping[t] > 0) {
         mjtNum B = -m->tendon_damping[t];
-        const mjtNum* J = d->ten_J + t*nv;
-        if (J[r]) q += J[c] * (J[r] * B);
+        /* addJTBJ :693-724, or addJTBJSparse :729-755 for a sparse model, whose only extra
+           terms are exact zeros (structural entries of value 0) */
+        mjtNum Jr = ten_J_at(m, d, t, r);
+        if (Jr) q += ten_J_at(m, d, t, c) * (Jr * B);
       }
     }
   }
@@ -7343,6 +7741,21 @@ static mjtNum* alloc_data(const mjhipModel* m, mjhipData* d, orEfc* e) {
   e->efc_type = (int*)calloc(3*(size_t)cap + 1, sizeof(int));
   e->efc_id = e->efc_type + cap;
   e->efc_state = e->efc_id + cap;
+  if (mj_isSparse(m)) {                    /* compressed rows and tendon Jacobians */
+    size_t cn = (size_t)cap*m->nv, tn = (size_t)m->ntendon;
+    int* ip = (int*)calloc(2*tn + tn*m->nv + 2*(size_t)cap + 2*cn + 2*(size_t)m->nv + 1,
+                           sizeof(int));
+    e->efc_JT = (mjtNum*)calloc(cn + 1, sizeof(mjtNum));
+    d->ten_J_rownnz = ip; ip += tn;
+    d->ten_J_rowadr = ip; ip += tn;
+    d->ten_J_colind = ip; ip += tn*m->nv;
+    e->efc_J_rownnz = ip; ip += cap;
+    e->efc_J_rowadr = ip; ip += cap;
+    e->efc_J_colind = ip; ip += cn;
+    e->efc_JT_rownnz = ip; ip += m->nv;
+    e->efc_JT_rowadr = ip; ip += m->nv;
+    e->efc_JT_colind = ip;
+  }
   return buf;
 }
 
@@ -7368,6 +7781,8 @@ static void* worker(void* arg) {
     }
   }
   free(e.efc_type);
+  free(d.ten_J_rownnz);
+  free(e.efc_JT);
   free(buf);
   return NULL;
 }

@@ -30,7 +30,7 @@ typedef struct orEfc_ {
   int* efc_type;      /* mjtConstraint */
   int* efc_id;
   int* efc_state;     /* mjtConstraintState */
-  mjtNum* efc_J;      /* capacity x nv, dense */
+  mjtNum* efc_J;      /* capacity x nv: dense rows, or compressed rows (sparse mode) */
   mjtNum* efc_pos;
   mjtNum* efc_margin;
   mjtNum* efc_frictionloss;
@@ -57,6 +57,17 @@ typedef struct orEfc_ {
   int* con_geom;               /* x2 */
   int* con_exclude;
   int* con_efc_address;
+  /* sparse-mode models (mj_isSparse): efc_J holds compressed rows (capacity x nv doubles of
+   * room), described by these arrays, and efc_JT their transpose (mj_makeConstraint
+   * engine_core_constraint.c:2083-2104) */
+  int nJ;
+  int* efc_J_rownnz;           /* capacity */
+  int* efc_J_rowadr;           /* capacity */
+  int* efc_J_colind;           /* capacity x nv */
+  mjtNum* efc_JT;              /* capacity x nv */
+  int* efc_JT_rownnz;          /* nv */
+  int* efc_JT_rowadr;          /* nv */
+  int* efc_JT_colind;          /* capacity x nv */
 } orEfc;
 
 /* mjtConstraint / mjtConstraintState values (mjmodel.h) */

@@ -39,7 +39,20 @@ class Efc(ctypes.Structure):
                                  "efc_aref", "efc_force")] +
               [("con_capacity", ctypes.c_int), ("ncon", ctypes.c_int)] +
               [(n, _D) for n, _ in CON_DOUBLE] +
-              [(n, ctypes.POINTER(ctypes.c_int)) for n, _ in CON_INT])
+              [(n, ctypes.POINTER(ctypes.c_int)) for n, _ in CON_INT] +
+              [("nJ", ctypes.c_int)] +
+              [(n, ctypes.POINTER(ctypes.c_int)) for n in ("efc_J_rownnz", "efc_J_rowadr",
+                                                           "efc_J_colind")] +
+              [("efc_JT", _D)] +
+              [(n, ctypes.POINTER(ctypes.c_int)) for n in ("efc_JT_rownnz", "efc_JT_rowadr",
+                                                           "efc_JT_colind")])
+
+# compressed-row arrays of orEfc (sparse-mode models): (name, dtype, size per capacity row or
+# per dof)
+EFC_SPARSE = (("efc_J_rownnz", np.int32, "row"), ("efc_J_rowadr", np.int32, "row"),
+              ("efc_J_colind", np.int32, "row_nv"), ("efc_JT", np.float64, "row_nv"),
+              ("efc_JT_rownnz", np.int32, "nv"), ("efc_JT_rowadr", np.int32, "nv"),
+              ("efc_JT_colind", np.int32, "row_nv"))
 
 
 class UnsupportedModel(ValueError):
@@ -118,6 +131,11 @@ class Oracle:
       setattr(self.efc, n, _p(a))
     for n, a in self._efc_int.items():
       setattr(self.efc, n, a.ctypes.data_as(ctypes.POINTER(ctypes.c_int)))
+    self._efc_sparse = {}
+    for n, dt, k in EFC_SPARSE:
+      a = np.zeros({"row": cap, "row_nv": cap * nv, "nv": nv}[k], dtype=dt)
+      self._efc_sparse[n] = a
+      setattr(self.efc, n, a.ctypes.data_as(ctypes.POINTER(np.ctypeslib.as_ctypes_type(dt))))
     ncap = max(self.L.or_contactCapacity(ctypes.byref(self.cm)), 1)
     self.efc.con_capacity = ncap
     self._con = {n: np.zeros(ncap * k) for n, k in CON_DOUBLE}
@@ -183,10 +201,54 @@ class Oracle:
         if k == 1 else self._con[name][:self.efc.ncon * k].reshape(self.efc.ncon, k)
 
   def efc_field(self, name):
+    """Rows of the last call. efc_J: dense nefc x nv rows (flattened), also for a sparse-mode
+    model, whose compressed rows are expanded (efc_sparse() has them as they are)."""
+    if name == "efc_J" and fields.is_sparse(self.m):
+      return self.efc_dense().ravel()
     if name in self._efc_arrays:
       k = self._efc_arrays[name].size // self.efc.capacity
       return self._efc_arrays[name][:self.efc.nefc * k]
     return self._efc_int[name][:self.efc.nefc]
+
+  def efc_sparse(self):
+    """Compressed rows of a sparse-mode model's last call: dict of efc_J (nJ values),
+    efc_J_rownnz/rowadr (nefc), efc_J_colind (nJ), efc_JT (nJ), efc_JT_rownnz/rowadr (nv),
+    efc_JT_colind (nJ)."""
+    e, nv = self.efc, self.m.nv
+    nJ, nefc = e.nJ, e.nefc
+    S = self._efc_sparse
+    return {"efc_J": self._efc_arrays["efc_J"][:nJ].copy(),
+            "efc_J_rownnz": S["efc_J_rownnz"][:nefc].copy(),
+            "efc_J_rowadr": S["efc_J_rowadr"][:nefc].copy(),
+            "efc_J_colind": S["efc_J_colind"][:nJ].copy(),
+            "efc_JT": S["efc_JT"][:nJ].copy(),
+            "efc_JT_rownnz": S["efc_JT_rownnz"][:nv].copy(),
+            "efc_JT_rowadr": S["efc_JT_rowadr"][:nv].copy(),
+            "efc_JT_colind": S["efc_JT_colind"][:nJ].copy()}
+
+  def efc_dense(self):
+    """efc_J of the last call as a dense nefc x nv matrix (a sparse model's rows expanded)."""
+    e, nv = self.efc, self.m.nv
+    if not fields.is_sparse(self.m):
+      return self._efc_arrays["efc_J"][:e.nefc * nv].reshape(e.nefc, nv).copy()
+    S = self._efc_sparse
+    out = np.zeros((e.nefc, nv))
+    for r in range(e.nefc):
+      a, n = S["efc_J_rowadr"][r], S["efc_J_rownnz"][r]
+      out[r, S["efc_J_colind"][a:a + n]] = self._efc_arrays["efc_J"][a:a + n]
+    return out
+
+  def ten_J_dense(self):
+    """ten_J of the last call as ntendon x nv (a sparse model's compressed rows expanded)."""
+    m, d = self.m, self.d
+    nt, nv = m.sizes["ntendon"], m.nv
+    if not fields.is_sparse(m):
+      return d.ten_J.reshape(nt, nv).copy()
+    out = np.zeros((nt, nv))
+    for t in range(nt):
+      a, n = d.sparse("ten_J_rowadr")[t], d.sparse("ten_J_rownnz")[t]
+      out[t, d.sparse("ten_J_colind")[a:a + n]] = d.ten_J[a:a + n]
+    return out
 
   def box_box_raw(self, g1, g2, margin):
     """mjc_BoxBox's raw contacts on the current geom poses (after inverse/forward):

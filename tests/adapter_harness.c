@@ -102,6 +102,10 @@ HX* hx_create(const mjhipModel* hm, long narena) {
 #define X(type, name, d0, d1) d->name = hm->name;
   MJHIP_MODEL_POINTERS_D
 #undef X
+  /* ten_J's compressed structure (mjData, used by sparse-mode models) */
+  d->ten_J_rownnz = (int*)calloc((size_t)hm->ntendon + 1, sizeof(int));
+  d->ten_J_rowadr = (int*)calloc((size_t)hm->ntendon + 1, sizeof(int));
+  d->ten_J_colind = (int*)calloc((size_t)hm->ntendon * hm->nv + 1, sizeof(int));
   memcpy(d->qpos, hm->qpos0, sizeof(mjtNum) * hm->nq);
   d->narena = (size_t)narena;
   d->arena = aligned_alloc(64, ((size_t)narena + 63) & ~(size_t)63);
@@ -117,6 +121,9 @@ void hx_free(HX* h) {
   MJHIP_DATA_FORWARD
   MJHIP_DATA_SENSOR_AUX
 #undef XD
+  free(d->ten_J_rownnz);
+  free(d->ten_J_rowadr);
+  free(d->ten_J_colind);
   free(d->arena);
   free(d);
   free(h->m);
@@ -157,6 +164,9 @@ void* hx_field(HX* h, const char* name) {
   MJDATA_ARENA_POINTERS
 #undef X
   if (!strcmp(name, "arena")) return d->arena;
+  if (!strcmp(name, "ten_J_rownnz")) return d->ten_J_rownnz;
+  if (!strcmp(name, "ten_J_rowadr")) return d->ten_J_rowadr;
+  if (!strcmp(name, "ten_J_colind")) return d->ten_J_colind;
   return NULL;
 }
 

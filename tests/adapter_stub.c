@@ -29,6 +29,15 @@ static orEfc efc_view(mjhipData* d) {
 #define XC(type, name, w, stage) e.name = d->name;
   MJHIP_DATA_CONTACT
 #undef XC
+  /* compressed rows of a sparse-mode model */
+  e.nJ = d->nJ;
+  e.efc_J_rownnz = d->efc_J_rownnz;
+  e.efc_J_rowadr = d->efc_J_rowadr;
+  e.efc_J_colind = d->efc_J_colind;
+  e.efc_JT = d->efc_JT;
+  e.efc_JT_rownnz = d->efc_JT_rownnz;
+  e.efc_JT_rowadr = d->efc_JT_rowadr;
+  e.efc_JT_colind = d->efc_JT_colind;
   return e;
 }
 
@@ -38,6 +47,7 @@ static void counts_back(mjhipData* d, const orEfc* e) {
   d->nf = e->nf;
   d->nl = e->nl;
   d->ncon = e->ncon;
+  d->nJ = e->nJ;
 }
 
 int mjhip_modelCapacity(const mjhipModel* m, int* efc_rows, int* contacts) {

@@ -44,6 +44,7 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
 #undef XSI
   mr.efc_cap = efc_cap;
   mr.con_cap = con_cap;
+  mr.nj_cap = mjh_njCap(m, efc_cap);
   int* wl = (int*)calloc(B + 1, sizeof(int));
   int wc = 0, wnext = 1;
   for (int i = 0; i < B; i++) {

@@ -93,6 +93,7 @@ static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int
   }
   L.efc_cap = efc_cap;
   L.con_cap = con_cap;
+  L.nj_cap = mjh_njCap(m, efc_cap);
   static unsigned long long chain[64];
   for (int k = 0; k < m->nbody && k < 64; k++) chain[k] = mjh::chainMask(*m, k);
   L.chain = chain;

@@ -51,3 +51,61 @@ def states(m, n, seed=0):
     q[:, a + 3:a + 7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
   q[:, 7 * nfree:] = rng.uniform(-1.8, 1.8, (n, m.nq - 7 * nfree))
   return q, rng.normal(size=(n, m.nv)), rng.normal(size=(n, m.nv))
+
+
+# Every sparse-mode row type: a free box with an adhesion actuator (body
+# transmission through mj_mulJacTVec), a free ball, an arm with a limited ball joint (a 3-dof
+# limit row), a slide and dof friction loss, a spatial tendon wrapping a cylinder with a side
+# site (limits, friction loss, spring-damper), a limited fixed tendon with friction loss and a
+# motor (tendon transmission), and connect / weld / joint / tendon equalities.
+MISC = """<mujoco><option timestep=".002" jacobian="{jacobian}" {extra}/>{flags}
+  <worldbody>
+  <geom type="plane" size="3 3 .1"/>
+  <site name="w" pos=".3 .4 .6" euler="10 0 0"/>
+  <body name="box" pos=".4 0 .1"><freejoint/><geom type="box" size=".08 .06 .05"/></body>
+  <body name="ball" pos="-.3 .3 .2"><freejoint/><geom type="sphere" size=".07"/></body>
+  <body name="base" pos="0 0 .5"><joint name="h0" axis="0 0 1" frictionloss=".05"/>
+    <geom type="capsule" fromto="0 0 0 .25 0 0" size=".04"/><site name="s0" pos=".02 0 .05"/>
+    <body name="link" pos=".25 0 0"><joint name="bj" type="ball" range="0 40" limited="true"/>
+      <geom type="capsule" fromto="0 0 0 .25 0 0" size=".035"/>
+      <geom name="wrap" type="cylinder" size=".05 .05" pos=".1 0 0" euler="90 0 0"
+        contype="0" conaffinity="0"/>
+      <site name="side" pos=".1 0 .2"/><site name="s1" pos=".24 0 .04"/>
+      <body name="tip" pos=".25 0 0"><joint name="sl" type="slide" axis="1 0 0"
+          range="-.05 .05" limited="true"/><geom type="sphere" size=".04"/>
+        <site name="ts" pos=".02 0 0"/></body></body></body>
+  </worldbody>
+  <tendon>
+    <spatial name="sp" limited="true" range=".1 .33" stiffness="20" damping=".5"
+        frictionloss=".02"><site site="s0"/><geom geom="wrap" sidesite="side"/>
+      <site site="s1"/></spatial>
+    <fixed name="fx" limited="true" range="-.3 .4" frictionloss=".03" damping=".2">
+      <joint joint="h0" coef="1"/><joint joint="sl" coef="-2"/></fixed>
+  </tendon>
+  <equality><connect body1="tip" body2="ball" anchor=".05 0 0" solref=".04 1"/>
+    <weld site1="w" site2="ts" torquescale=".4"/>
+    <joint joint1="h0" joint2="sl" polycoef="0 .3 .1 0 0"/>
+    <tendon tendon1="fx" tendon2="sp" polycoef=".01 .5"/></equality>
+  <actuator><motor tendon="fx" gear="2"/><motor joint="h0"/>
+    <adhesion body="box" ctrlrange="0 1" gain="3"/></actuator>
+</mujoco>"""
+
+
+def misc(jacobian="sparse", extra="", flags=""):
+  return mjcf.load_xml_string(MISC.format(jacobian=jacobian, extra=extra, flags=flags))
+
+
+def misc_states(m, n, seed=0):
+  """The free bodies just touching or above the floor, the arm's joints through their limits."""
+  rng = np.random.default_rng(seed)
+  q = np.tile(np.asarray(m.qpos0, dtype=float), (n, 1))
+  for a, h in ((0, 0.05), (7, 0.07)):
+    q[:, a:a + 2] += rng.uniform(-0.05, 0.05, (n, 2))
+    q[:, a + 2] = h + rng.uniform(-0.01, 0.02, n)
+    qq = np.tile([1.0, 0, 0, 0], (n, 1)) + 0.15 * rng.normal(size=(n, 4))
+    q[:, a + 3:a + 7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
+  q[:, 14] = rng.uniform(-2, 2, n)                              # h0
+  qq = np.tile([1.0, 0, 0, 0], (n, 1)) + 0.5 * rng.normal(size=(n, 4))
+  q[:, 15:19] = qq / np.linalg.norm(qq, axis=1, keepdims=True)  # ball
+  q[:, 19] = rng.uniform(-0.08, 0.08, n)                        # slide
+  return q, rng.normal(size=(n, m.nv)), rng.normal(size=(n, m.nv))

@@ -108,12 +108,14 @@ def _assert_contacts_equal(A, o):
   assert (iv[:, 7:] == -1).all()                                  # flex, elem, vert
 
 
-def _assert_layout(A, m, tables):
-  """The arena as mj_collision + mj_makeConstraint leave it."""
+def _assert_layout(A, m, tables, nJ=None):
+  """The arena as mj_collision + mj_makeConstraint leave it (nJ: a sparse-mode model's
+  compressed entries; dense: nefc x nv)."""
   ncon, nefc = A.s("ncon"), A.s("nefc")
+  nJ = nefc * m.nv if nJ is None else nJ
   assert A.off("contact") == 0
-  assert A.s("nJ") == nefc * m.nv and A.s("nA") == 0 and A.s("nisland") == 0
-  size = {"MJ_D(nefc)": nefc, "MJ_D(nJ)": nefc * m.nv, "MJ_M(nv)": m.nv,
+  assert A.s("nJ") == nJ and A.s("nA") == 0 and A.s("nisland") == 0
+  size = {"MJ_D(nefc)": nefc, "MJ_D(nJ)": nJ, "MJ_M(nv)": m.nv,
           "MJ_M(ntendon)": m.ntendon}
   off = ncon * A.sizeof_contact
   for t, name, r, c in tables["SOLVER"]:
@@ -266,5 +268,89 @@ def test_refused_models_are_an_error(lib):
       lib.hx_set_model_int(A.h, what.encode(), 1)
       rc, err = A.call(1)
       assert rc == 1 and msg in err, (what, err)
+    finally:
+      A.close()
+
+
+def _super_sparse(rownnz, rowadr, colind):
+  """mju_superSparse (engine_util_sparse.c:520-550)."""
+  n = len(rownnz)
+  sup = [0] * n
+  for r in range(n - 1):
+    sup[r] = int(rownnz[r] == rownnz[r + 1] and
+                 list(colind[rowadr[r]:rowadr[r] + rownnz[r]]) ==
+                 list(colind[rowadr[r + 1]:rowadr[r + 1] + rownnz[r + 1]]))
+  for r in range(n - 2, -1, -1):
+    if sup[r]:
+      sup[r] += sup[r + 1]
+  return sup
+
+
+def _sparse_cases():
+  import humanoid100_states as H
+  import sparse_models as S
+  mp = S.pile()
+  qp, vp, ap = S.states(mp, 4, seed=8)
+  mm = S.misc()
+  qm, vm, am = S.misc_states(mm, 4, seed=8)
+  mh = H.model()
+  qh, vh, ah = H.states(mh, 2, seed=8)
+  return [(mp, qp[i], vp[i], ap[i]) for i in range(4)] + \
+         [(mm, qm[i], vm[i], am[i]) for i in range(4)] + \
+         [(mh, qh[i], vh[i], ah[i]) for i in range(2)]
+
+
+def test_sparse_models_compressed_arena(lib):
+  """Sparse-Jacobian models (mj_isSparse) through the adapter: the arena holds the
+  reference's compressed layout -- efc_J/efc_JT over nJ entries with their rownnz/rowadr/colind
+  and the supernodes (engine_core_constraint.c:2083-2104) -- ten_J is compressed in place
+  with its rownnz/rowadr/colind, outputs equal the oracle's bit for bit, and skip POS/VEL
+  calls read and update the compressed rows in place."""
+  tables = _solver_table()
+  rng = np.random.default_rng(4)
+  narena = 64 << 20
+  for m, q, v, a in _sparse_cases():
+    A, o = Adapter(lib, m, narena=narena), Oracle(m)
+    try:
+      A.set_state(q, v, a)
+      assert A.call(0, 0) == (0, "")
+      ref = o.inverse(q, v, a)
+      np.testing.assert_array_equal(A.field("qfrc_inverse"), ref)
+      for f in fields.DATA_FIELDS:
+        np.testing.assert_array_equal(A.field(f.name), getattr(o.d, f.name), err_msg=f.name)
+      nt = m.ntendon
+      for name in ("ten_J_rownnz", "ten_J_rowadr"):
+        np.testing.assert_array_equal(A.arr(name, nt, np.int32), o.d.sparse(name)[:nt])
+      sp, nefc, nJ = o.efc_sparse(), o.efc.nefc, o.efc.nJ
+      _assert_contacts_equal(A, o)
+      _assert_layout(A, m, tables, nJ=nJ)
+      assert nJ < nefc * m.nv
+      np.testing.assert_array_equal(A.arr("efc_J", nJ), sp["efc_J"])
+      np.testing.assert_array_equal(A.arr("efc_JT", nJ), sp["efc_JT"])
+      for name in ("efc_J_colind", "efc_JT_colind"):
+        np.testing.assert_array_equal(A.arr(name, nJ, np.int32), sp[name])
+      for name in ("efc_J_rownnz", "efc_J_rowadr"):
+        np.testing.assert_array_equal(A.arr(name, nefc, np.int32), sp[name])
+      for name in ("efc_JT_rownnz", "efc_JT_rowadr"):
+        np.testing.assert_array_equal(A.arr(name, m.nv, np.int32), sp[name])
+      np.testing.assert_array_equal(
+          A.arr("efc_J_rowsuper", nefc, np.int32),
+          _super_sparse(sp["efc_J_rownnz"], sp["efc_J_rowadr"], sp["efc_J_colind"]))
+      np.testing.assert_array_equal(
+          A.arr("efc_JT_rowsuper", m.nv, np.int32),
+          _super_sparse(sp["efc_JT_rownnz"], sp["efc_JT_rowadr"], sp["efc_JT_colind"]))
+      for name, w in EFC_DOUBLE[1:]:
+        np.testing.assert_array_equal(A.efc(name, w), o.efc_field(name), err_msg=name)
+      layout = {n: A.off(n) for _, n, _, _ in tables["SOLVER"]}
+      for skip in (1, 2):
+        v2 = v if skip == 2 else v + rng.normal(size=m.nv)
+        a2 = a + rng.normal(size=m.nv)
+        A.field("qvel")[:] = v2
+        A.field("qacc")[:] = a2
+        assert A.call(0, skip) == (0, "")
+        o.set_state(None, v2, a2)
+        np.testing.assert_array_equal(A.field("qfrc_inverse"), o.inverse(skipstage=skip))
+        np.testing.assert_array_equal(A.efc("efc_force"), o.efc_field("efc_force"))
+        assert {n: A.off(n) for _, n, _, _ in tables["SOLVER"]} == layout
     finally:
       A.close()

@@ -116,3 +116,47 @@ def test_stage_functions_and_compare_fwd_inv_through_adapter(lib):
       np.testing.assert_allclose(fw, ref, rtol=1e-8, atol=1e-10)
     finally:
       A.close()
+
+
+def test_humanoid100_through_adapter(lib):
+  """The reference's 627-dof humanoid100 (sparse Jacobians, mj_isSparse) through
+  mj_inverseSkip(NONE, POS, VEL) into the real libmjhip.so: the adapter lays out the
+  reference's compressed arena (efc_J/efc_JT over nJ entries, their rownnz/rowadr/colind,
+  ten_J's structure); counts and structure exact, qfrc_inverse and the rows to 1e-10, and
+  the position-skipping calls read and update the compressed rows in place."""
+  import humanoid100_states as H
+  m = H.model()
+  q, v, a = H.states(m, 3, seed=9)
+  rng = np.random.default_rng(9)
+  for i in range(3):
+    A, o = Adapter(lib, m, narena=256 << 20), Oracle(m)
+    try:
+      A.set_state(q[i], v[i], a[i])
+      assert A.call(0, 0) == (0, "")
+      ref = o.inverse(q[i], v[i], a[i])
+      _close(A.field("qfrc_inverse"), ref, RTOL, "qfrc_inverse")
+      sp, nefc, nJ = o.efc_sparse(), o.efc.nefc, o.efc.nJ
+      assert (A.s("nefc"), A.s("nJ"), A.s("ncon")) == (nefc, nJ, o.efc.ncon)
+      assert nJ < nefc * m.nv // 20
+      for name in ("efc_type", "efc_id", "efc_state"):
+        np.testing.assert_array_equal(A.efc(name, 1, np.int32), o.efc_field(name))
+      for name in ("efc_J_rownnz", "efc_J_rowadr"):
+        np.testing.assert_array_equal(A.arr(name, nefc, np.int32), sp[name])
+      for name in ("efc_J_colind", "efc_JT_colind"):
+        np.testing.assert_array_equal(A.arr(name, nJ, np.int32), sp[name])
+      _close(A.arr("efc_J", nJ), sp["efc_J"], RTOL, "efc_J")
+      _close(A.arr("efc_JT", nJ), sp["efc_JT"], RTOL, "efc_JT")
+      for name in ("efc_force", "efc_aref"):
+        _close(A.efc(name), o.efc_field(name), RTOL, name)
+      for skip in (1, 2):
+        v2 = v[i] if skip == 2 else v[i] + rng.normal(size=m.nv)
+        a2 = a[i] + rng.normal(size=m.nv)
+        A.field("qvel")[:] = v2
+        A.field("qacc")[:] = a2
+        assert A.call(0, skip) == (0, "")
+        o.set_state(None, v2, a2)
+        _close(A.field("qfrc_inverse"), o.inverse(skipstage=skip), RTOL, f"skip {skip}")
+        _close(A.efc("efc_force"), o.efc_field("efc_force"), RTOL, "efc_force")
+        assert A.s("nJ") == nJ
+    finally:
+      A.close()

@@ -2,8 +2,10 @@
 on the GPU: the humanoid plus 100 free primitives in contact with the floor and each other
 (tests/humanoid100_states.py), through a context capped at 1,024 contacts / 4,096 rows per
 instance (mjhip_contextCreateCapped; the exact worst case is 344 MB of efc_J per instance).
-Jacobian "auto" with nv = 627 is the reference's sparse path: the generic kernel computes
-the same sums on dense rows (sparse Jacobians).
+Jacobian "auto" with nv = 627 is the reference's sparse path (mj_isSparse): the generic
+kernel builds the compressed rows over the bodies' dof chains, their transpose, and the
+position-grouped sums of mju_mulMatVecSparse, as the oracle restates them (sparse
+Jacobians); the compressed structure is compared exactly.
 
 Floating point: the generic kernel's unit rounds every operation as the oracle does (no
 multiply-add contraction, DESIGN.md build), so, as for tests/test_reference_model_gpu.py, the
@@ -37,6 +39,8 @@ def _oracle(m, q, v, a, perturb=False):
     out["dist"].append(o.contact_field("con_dist").ravel().copy())
     out["pf"].append(np.concatenate([o.contact_field("con_pos").ravel(),
                                      o.contact_field("con_frame").ravel()]))
+    if not perturb:
+      out.setdefault("sp", []).append(o.efc_sparse())
   out["f"] = np.array(out["f"])
   return out
 
@@ -58,9 +62,26 @@ def test_humanoid100_vs_oracle():
     geom = e.field_int("con_geom", 0, B)
     dist = e.field("con_dist", 0, B)
     pos, frame = e.field("con_pos", 0, B), e.field("con_frame", 0, B)
+    nJ = e.field_int("nJ", 0, B)[:, 0]
+    J = e.field("efc_J", 0, B)
+    ints = {n: e.field_int(n, 0, B) for n in ("efc_J_rownnz", "efc_J_colind",
+                                             "efc_JT_rownnz", "efc_JT_colind")}
   finally:
     e.close()
   o = _oracle(m, q, v, a)
+  # the compressed rows (mj_isSparse): structure exact, values to the bar
+  jerr = 0.0
+  for i in range(B):
+    sp = o["sp"][i]
+    assert nJ[i] == sp["efc_J"].size
+    np.testing.assert_array_equal(ints["efc_J_rownnz"][i, :nefc[i]], sp["efc_J_rownnz"])
+    np.testing.assert_array_equal(ints["efc_J_colind"][i, :nJ[i]], sp["efc_J_colind"])
+    np.testing.assert_array_equal(ints["efc_JT_rownnz"][i, :m.nv], sp["efc_JT_rownnz"])
+    np.testing.assert_array_equal(ints["efc_JT_colind"][i, :nJ[i]], sp["efc_JT_colind"])
+    jerr = max(jerr, np.abs(J[i, :nJ[i]] - sp["efc_J"]).max() / max(1, np.abs(sp["efc_J"]).max()))
+  print(f"humanoid100: {int(nJ.sum())} compressed Jacobian entries (dense rows would hold "
+        f"{int(nefc.sum()) * m.nv}), max efc_J error {jerr:.2e}")
+  assert jerr <= RTOL
   np.testing.assert_array_equal(st, o["st"])
   assert (st == 0).all()
   np.testing.assert_array_equal(ncon, o["ncon"])

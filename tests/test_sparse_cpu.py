@@ -1,59 +1,44 @@
-"""Sparse-Jacobian models (SURVEY.md §8 row a12/f; VERDICT r03 item 7), CPU side.
+"""Sparse-Jacobian models (SURVEY.md §8 rows a7/a12/a19/a20; VERDICT r04 item 1), CPU side.
 
-The reference switches to compressed rows when mj_isSparse (engine_core_constraint.c:96-103):
-efc_J and ten_J hold each row's entries over the merged dof chains of its bodies, and
-mj_mulJacVec / mj_mulJacTVec / the J'force of mj_constraintUpdate run the sparse kernels
-(mju_mulMatVecSparse, mju_mulMatTVecSparse, engine_util_sparse.c). The engine computes these
-models with dense rows:
-  * J'force (mju_mulMatTVecSparse scatters row by row) is the dense per-column sum in row
-    order plus exact zeros (x + 0*y == x for finite x other than -0): identical bits;
-  * J*v (efc_vel, jar) is mju_dotSparse, a 4-way unrolled sum grouped by position in the
-    row's colind (engine_util_sparse.h:115-160), where the dense mju_dot groups by column
-    index: the same terms in other partial sums, so the two differ in the last bits on some
-    rows (measured below); the dense result is within an ulp-level bound of the sparse one,
-    far inside the path's 1e-10 bar. Reproducing those bits needs the compressed row layout
-    (sparse Jacobians).
+When mj_isSparse (engine_core_constraint.c:99-106: jacobian="sparse", or "auto" with
+nv >= 60) the reference keeps compressed rows:
+  * mj_tendon builds ten_J row by row with mju_combineSparse over each joint / path segment's
+    merged dof chain (engine_core_smooth.c:651-860);
+  * mj_addConstraint copies each row's values over its chain (:265-356): a contact's or a
+    connect/weld's the merged chain of its two bodies (mj_jacDifPair, engine_support.c:
+    659-731), a joint limit / dof friction row its dof, a tendon row the tendon's ten_J
+    pattern, a joint/tendon coupling both objects' patterns combined (:640-719); a non-
+    contact row is dropped only when its chain is empty, a contact whose chain is empty is
+    excluded (exclude = 3, :1071-1076);
+  * mj_makeConstraint transposes the rows into efc_JT (mju_transposeSparse, :2083-2104);
+  * efc_vel and jar are mju_mulMatVecSparse over the rows of efc_J, qfrc_constraint over the
+    rows of efc_JT (mj_mulJacVec :361-377, mj_mulJacTVec :426-442), i.e. mju_dotSparse: four
+    partial sums by POSITION in the row (engine_util_sparse.h:115-160; the AVX build groups
+    the same way, engine_util_sparse_avx.h:34-249), where the dense mju_dot groups by column;
+  * ten_velocity is mju_mulMatVecSparse over ten_J (engine_forward.c:206-212); the tendon
+    spring-damper scatters over the row (engine_passive.c:361-370); a tendon transmission's
+    moment row is the tendon's ten_J row (engine_core_smooth.c:1060-1067); a body
+    transmission's J'weights is mj_mulJacTVec (:1317).
 
-Checked here: the model compiles in the sparse range and runs the generic kernel (the
-straight-line kernels stop at nv = 60); the device pipeline compiled for the host equals the
-oracle bit for bit on contact-rich states; the dense row products equal the sparse kernels'
-restated sums over the rows' nonzero pattern bit for bit, and over the reference's chain
-pattern (which may include stored zeros) as well.
+The oracle restates that path (oracle/mj_oracle.c). Checked here:
+  * the oracle's compressed structures against numpy restatements from the model alone
+    (merged chains, the transpose) and its sums against a Python restatement of
+    mju_dotSparse over them (an independent statement of the grouping);
+  * the dense-mode twin of each model (jacobian="dense") agrees to 1e-12 with the same
+    rows, while the sums differ in the last bits (the grouping is in effect);
+  * the device pipeline compiled for the host equals the oracle bit for bit on every output
+    and on the compressed arrays, on the 63-dof pile (auto), a 27-dof jacobian="sparse" pile,
+    a model with every row type, and the reference's 627-dof humanoid100.
 """
 import numpy as np
+import pytest
 
 from kernel_harness import KernelCPU
-from mujoco_inversedynamicstest_amd import codegen
+from mujoco_inversedynamicstest_amd import codegen, fields
 from oracle.oracle import Oracle
 
+import humanoid100_states as H
 import sparse_models as S
-
-
-def test_model_in_sparse_range():
-  m = S.pile()
-  assert m.nv == 63 and m.opt["jacobian"] == 2           # auto, nv >= 60: mj_isSparse
-  assert codegen.fast_path_supported(m) == "large model (nv >= 60)"
-  ms = S.pile(nfree=4, jacobian="sparse")
-  assert ms.nv == 27 and ms.opt["jacobian"] == 1
-  assert codegen.fast_path_supported(ms) is None
-
-
-def test_device_code_bitexact_sparse_models():
-  for m, n in ((S.pile(), 24), (S.pile(nfree=4, jacobian="sparse"), 16)):
-    q, v, a = S.states(m, n, seed=1)
-    o, k = Oracle(m), KernelCPU(m)
-    rows = 0
-    for i in range(n):
-      f = o.inverse(q[i], v[i], a[i])
-      g, st = k.inverse(q[i], v[i], a[i])
-      assert st == o.d.status == 0
-      np.testing.assert_array_equal(g, f)
-      nefc = o.efc.nefc
-      np.testing.assert_array_equal(k.field("efc_force")[:nefc], o.efc_field("efc_force"))
-      # rows written over their dof spans, the previous state's spans cleared: whole rows
-      np.testing.assert_array_equal(k.field("efc_J")[:nefc * m.nv], o.efc_field("efc_J"))
-      rows += nefc
-    assert rows > 10 * n
 
 
 def _chain(m, body):
@@ -61,14 +46,27 @@ def _chain(m, body):
   out = []
   b = int(body)
   while b > 0:
-    for j in range(int(m.body_dofnum[b]) - 1, -1, -1):
-      out.append(int(m.body_dofadr[b]) + j)
+    out += range(int(m.body_dofadr[b]), int(m.body_dofadr[b]) + int(m.body_dofnum[b]))
     b = int(m.body_parentid[b])
   return sorted(out)
 
 
-def _dot4(a, b):
-  """mju_dot's scalar branch (engine_util_blas.c:680-720): four partial sums by index."""
+def _dot_sparse(vals, x, ind):
+  """mju_dotSparse (engine_util_sparse.h:115-160): partial sums by position in the row."""
+  n, i, r = len(ind), 0, [0.0, 0.0, 0.0, 0.0]
+  while i <= n - 4:
+    for k in range(4):
+      r[k] += vals[i + k] * x[ind[i + k]]
+    i += 4
+  res = (r[0] + r[2]) + (r[1] + r[3])
+  while i < n:
+    res += vals[i] * x[ind[i]]
+    i += 1
+  return res
+
+
+def _dot_dense(a, b):
+  """mju_dot (engine_util_blas.c:680-741): partial sums by column index."""
   n, i, r = len(a), 0, [0.0, 0.0, 0.0, 0.0]
   while i <= n - 4:
     for k in range(4):
@@ -84,79 +82,218 @@ def _dot4(a, b):
   return res
 
 
-def _dot_sparse(vals, x, ind):
-  """mju_dotSparse's scalar branch (engine_util_sparse.h:115-160): partial sums by position."""
-  n, i, r = len(ind), 0, [0.0, 0.0, 0.0, 0.0]
-  while i <= n - 4:
-    for k in range(4):
-      r[k] += vals[i + k] * x[ind[i + k]]
-    i += 4
-  res = (r[0] + r[2]) + (r[1] + r[3])
-  while i < n:
-    res += vals[i] * x[ind[i]]
-    i += 1
-  return res
-
-
-def test_dense_rows_equal_sparse_kernels():
-  """Sequential sums over (a) each row's nonzeros and (b) the union of the contact's two
-  body chains (the reference's merged chain, zeros stored) equal the dense sequential sums
-  bit for bit; mju_mulMatTVecSparse's row-by-row scatter equals the engine's J'force bit for
-  bit; mju_dotSparse over the merged chain (4-way unrolled by position) differs from the
-  dense 4-way mju_dot by at most a few ulps of the row's term magnitudes."""
+def test_models_in_sparse_range():
   m = S.pile()
-  q, v, a = S.states(m, 12, seed=2)
-  o = Oracle(m)
-  checked = differ = 0
-  for i in range(12):
+  assert m.nv == 63 and m.opt["jacobian"] == 2 and fields.is_sparse(m)
+  assert codegen.fast_path_supported(m) == "large model (nv >= 60)"
+  ms = S.pile(nfree=4, jacobian="sparse")
+  assert ms.nv == 27 and ms.opt["jacobian"] == 1 and fields.is_sparse(ms)
+  # compressed rows are built by the generic kernel only
+  assert codegen.fast_path_supported(ms).startswith("sparse-Jacobian model")
+  assert not fields.is_sparse(S.pile(nfree=4))
+  # a fixed-tendon transmission's moment pattern is the tendon's compressed row: every
+  # joint's dof, whatever the coefficient (mj_tendon's mju_combineSparse)
+  mm = S.misc()
+  fx = 1                                         # motor on tendon fx (h0: dof 12, sl: dof 16)
+  assert mm.moment_rownnz[0] == 2
+  assert list(mm.moment_colind[mm.moment_rowadr[0]:mm.moment_rowadr[0] + 2]) == [12, 16]
+  assert mm.tendon_num[fx] == 2
+
+
+@pytest.mark.parametrize("case", ["pile63", "pile27", "misc"])
+def test_oracle_compressed_structures(case):
+  """Row patterns against the model: contact and connect/weld rows over the merged chains of
+  their two bodies, joint rows over their dofs, tendon rows over the tendon's pattern (the
+  union of its segments' chains); efc_JT the transpose, row order kept in each dof's list;
+  the rows' values equal the dense-mode twin's at the pattern, zero elsewhere."""
+  m, md, (q, v, a) = {
+      "pile63": lambda: (S.pile(), S.pile(jacobian="dense"), S.states(S.pile(), 6, seed=3)),
+      "pile27": lambda: (S.pile(4, "sparse"), S.pile(4, "dense"),
+                         S.states(S.pile(4, "sparse"), 6, seed=3)),
+      "misc": lambda: (S.misc(), S.misc("dense"), S.misc_states(S.misc(), 6, seed=3))}[case]()
+  o, od = Oracle(m), Oracle(md)
+  nv = m.nv
+  checked = 0
+  for i in range(len(q)):
     o.inverse(q[i], v[i], a[i])
+    od.inverse(q[i], v[i], a[i])
+    sp = o.efc_sparse()
     nefc = o.efc.nefc
-    if not nefc:
-      continue
-    J = o.efc_field("efc_J").reshape(nefc, m.nv)
-    force = o.efc_field("efc_force")
+    assert nefc == od.efc.nefc
+    np.testing.assert_array_equal(o.efc_field("efc_type"), od.efc_field("efc_type"))
     types, ids = o.efc_field("efc_type"), o.efc_field("efc_id")
     geoms = o.contact_field("con_geom").reshape(-1, 2)
-    x = a[i]                                 # J*qacc, as mj_invConstraint's jar
+    ten = o.ten_J_dense()
+    tpat = [sorted(o.d.sparse("ten_J_colind")[o.d.sparse("ten_J_rowadr")[t]:][
+        :o.d.sparse("ten_J_rownnz")[t]]) for t in range(m.sizes["ntendon"])]
+    adr = 0
     for r in range(nefc):
-      dense = 0.0
-      for c in range(m.nv):
-        dense += J[r, c] * x[c]
-      cols_nz = [c for c in range(m.nv) if J[r, c] != 0]
-      sparse = 0.0
-      for c in cols_nz:
-        sparse += J[r, c] * x[c]
-      assert sparse == dense
-      if types[r] >= 5:                      # contact rows: the two bodies' merged chain
-        g1, g2 = geoms[ids[r]]
-        chain = sorted(set(_chain(m, m.geom_bodyid[g1])) | set(_chain(m, m.geom_bodyid[g2])))
-        assert set(cols_nz) <= set(chain)
-        merged = 0.0
-        for c in chain:
-          merged += J[r, c] * x[c]
-        assert merged == dense
-    # J' force: per column, over the rows in order (mju_mulMatTVecSparse scatters row by row)
-    dense_t = np.zeros(m.nv)
-    for r in range(nefc):
-      for c in range(m.nv):
-        dense_t[c] += J[r, c] * force[r]
-    sparse_t = np.zeros(m.nv)
-    for r in range(nefc):
-      for c in range(m.nv):
-        if J[r, c] != 0:
-          sparse_t[c] += J[r, c] * force[r]
-    np.testing.assert_array_equal(sparse_t, dense_t)
-    np.testing.assert_array_equal(dense_t, o.d.qfrc_constraint)
-    # the unrolled dots: dense mju_dot (the engine) vs mju_dotSparse over the merged chain
-    for r in range(nefc):
-      if types[r] < 5:
-        continue
-      g1, g2 = geoms[ids[r]]
-      chain = sorted(set(_chain(m, m.geom_bodyid[g1])) | set(_chain(m, m.geom_bodyid[g2])))
-      d1, d2 = _dot4(J[r], x), _dot_sparse(J[r][chain], x, chain)
-      scale = float(np.sum(np.abs(J[r] * x)))
-      assert abs(d1 - d2) <= 8 * np.finfo(float).eps * scale
-      differ += d1 != d2
+      n = sp["efc_J_rownnz"][r]
+      assert sp["efc_J_rowadr"][r] == adr
+      cols = list(sp["efc_J_colind"][adr:adr + n])
+      tp, idx = int(types[r]), int(ids[r])
+      if tp >= 5:                                     # contact: both bodies' chains merged
+        g1, g2 = geoms[idx]
+        want = sorted(set(_chain(m, m.geom_bodyid[g1])) | set(_chain(m, m.geom_bodyid[g2])))
+      elif tp in (1, 3):                              # dof friction / joint limit
+        if tp == 1:
+          want = [idx]
+        else:
+          da, t = int(m.jnt_dofadr[idx]), int(m.jnt_type[idx])
+          want = list(range(da, da + (3 if t == 1 else 1)))
+      elif tp in (2, 4):                              # tendon friction / limit
+        want = tpat[idx]
+      else:                                           # equality
+        et = int(m.eq_type[idx])
+        o1, o2 = int(m.eq_obj1id[idx]), int(m.eq_obj2id[idx])
+        if et in (0, 1):
+          if int(m.eq_objtype[idx]) == 6:
+            o1, o2 = int(m.site_bodyid[o1]), int(m.site_bodyid[o2])
+          want = sorted(set(_chain(m, o1)) | set(_chain(m, o2)))
+        elif et == 2:
+          want = sorted({int(m.jnt_dofadr[o1])} | ({int(m.jnt_dofadr[o2])} if o2 >= 0 else set()))
+        else:
+          want = sorted(set(tpat[o1]) | (set(tpat[o2]) if o2 >= 0 else set()))
+      assert cols == want, (r, tp, cols, want)
+      dense_row = np.zeros(nv)
+      dense_row[cols] = sp["efc_J"][adr:adr + n]
+      ref_row = od.efc_dense()[r]
+      scale = max(1.0, np.abs(ref_row).max())
+      assert np.abs(dense_row - ref_row).max() <= 1e-14 * scale
+      adr += n
+    assert sp["efc_J"].size == adr == o.efc.nJ
+    # the transpose: each dof's rows in increasing order, values as in the rows
+    J = o.efc_dense()
+    for j in range(nv):
+      a0, n = sp["efc_JT_rowadr"][j], sp["efc_JT_rownnz"][j]
+      rows = list(sp["efc_JT_colind"][a0:a0 + n])
+      assert rows == sorted(rows)
+      want = [r for r in range(nefc)
+              if j in sp["efc_J_colind"][sp["efc_J_rowadr"][r]:][:sp["efc_J_rownnz"][r]]]
+      assert rows == want
+      np.testing.assert_array_equal(sp["efc_JT"][a0:a0 + n], J[rows, j])
+    np.testing.assert_allclose(ten, od.ten_J_dense(), rtol=0, atol=1e-14)
     checked += nefc
-  assert checked > 100
-  print(f"contact rows whose unrolled dense and sparse dots differ in the last bits: {differ}")
+  assert checked > 20
+
+
+@pytest.mark.parametrize("case", ["pile63", "misc"])
+def test_oracle_sums_restated(case):
+  """efc_vel, jar (via efc_force's quadratic rows), qfrc_constraint and ten_velocity equal a
+  Python mju_dotSparse over the oracle's compressed rows bit for bit; the dense mju_dot over
+  the same rows (the dense path's grouping) differs in the last bits on some of them."""
+  m = S.pile() if case == "pile63" else S.misc()
+  q, v, a = (S.states if case == "pile63" else S.misc_states)(m, 8, seed=4)
+  o = Oracle(m)
+  nv = m.nv
+  differ = total = 0
+  for i in range(len(q)):
+    o.inverse(q[i], v[i], a[i])
+    sp = o.efc_sparse()
+    nefc = o.efc.nefc
+    vel = o.efc_field("efc_vel")
+    for r in range(nefc):
+      a0, n = sp["efc_J_rowadr"][r], sp["efc_J_rownnz"][r]
+      vals, ind = sp["efc_J"][a0:a0 + n], sp["efc_J_colind"][a0:a0 + n]
+      assert _dot_sparse(vals, v[i], ind) == vel[r]
+      dense = np.zeros(nv)
+      dense[ind] = vals
+      differ += _dot_dense(dense, v[i]) != vel[r]
+      total += 1
+    force = o.efc_field("efc_force")
+    for j in range(nv):
+      a0, n = sp["efc_JT_rowadr"][j], sp["efc_JT_rownnz"][j]
+      want = _dot_sparse(sp["efc_JT"][a0:a0 + n], force, sp["efc_JT_colind"][a0:a0 + n])
+      assert o.d.qfrc_constraint[j] == (want if n else o.d.qfrc_constraint[j])
+    for t in range(m.sizes["ntendon"]):
+      a0, n = o.d.sparse("ten_J_rowadr")[t], o.d.sparse("ten_J_rownnz")[t]
+      assert o.d.ten_velocity[t] == _dot_sparse(o.d.ten_J[a0:a0 + n], v[i],
+                                                o.d.sparse("ten_J_colind")[a0:a0 + n])
+  assert total > 50 and differ > 0
+  print(f"{case}: rows whose J*qvel by column (dense mju_dot) differs from the reference's "
+        f"sparse grouping: {differ} of {total}")
+
+
+@pytest.mark.parametrize("case", ["pile63", "pile27", "misc", "misc_implicit",
+                                  "misc_implicitfast"])
+def test_sparse_vs_dense_twin(case):
+  """The same model with jacobian="dense": same counts, states and contacts, qfrc_inverse to
+  1e-12 (the two paths differ only in summation order), and not bit-identical everywhere.
+  The implicit variants run mj_discreteAcc with the tendon's damping in qDeriv."""
+  extra = {"misc_implicit": 'integrator="implicit"',
+           "misc_implicitfast": 'integrator="implicitfast"'}.get(case, "")
+  flags = '<option><flag invdiscrete="enable"/></option>' if extra else ""
+  if case.startswith("pile"):
+    nf = 10 if case == "pile63" else 4
+    ms, md = S.pile(nf, "sparse" if nf == 4 else None), S.pile(nf, "dense")
+    q, v, a = S.states(ms, 24, seed=5)
+  else:
+    ms, md = S.misc("sparse", extra, flags), S.misc("dense", extra, flags)
+    q, v, a = S.misc_states(ms, 24, seed=5)
+  os_, od = Oracle(ms), Oracle(md)
+  exact = 0
+  for i in range(len(q)):
+    fs = os_.inverse(q[i], v[i], a[i])
+    fd = od.inverse(q[i], v[i], a[i])
+    assert os_.d.status == od.d.status == 0
+    assert os_.efc.nefc == od.efc.nefc and os_.efc.ncon == od.efc.ncon
+    np.testing.assert_array_equal(os_.efc_field("efc_state"), od.efc_field("efc_state"))
+    assert np.abs(fs - fd).max() <= 1e-12 * max(1.0, np.abs(fd).max())
+    exact += np.array_equal(fs, fd)
+  assert exact < len(q)
+
+
+def _bitexact(m, q, v, a, efc_cap=None, con_cap=None):
+  o, k = Oracle(m), KernelCPU(m, efc_cap=efc_cap, con_cap=con_cap)
+  rows = 0
+  for i in range(len(q)):
+    f = o.inverse(q[i], v[i], a[i])
+    g, st = k.inverse(q[i], v[i], a[i])
+    assert st == o.d.status == 0
+    np.testing.assert_array_equal(g, f)
+    nefc = o.efc.nefc
+    assert k.field("efc_count")[0] == nefc
+    np.testing.assert_array_equal(k.field("efc_force")[:nefc], o.efc_field("efc_force"))
+    np.testing.assert_array_equal(k.field("efc_vel")[:nefc], o.efc_field("efc_vel"))
+    sp = o.efc_sparse()
+    nJ = o.efc.nJ
+    assert k.field("nJ")[0] == nJ
+    for name in ("efc_J", "efc_J_colind", "efc_JT", "efc_JT_colind"):
+      np.testing.assert_array_equal(k.field(name)[:nJ], sp[name])
+    for name in ("efc_J_rownnz", "efc_J_rowadr"):
+      np.testing.assert_array_equal(k.field(name)[:nefc], sp[name])
+    if nefc:
+      for name in ("efc_JT_rownnz", "efc_JT_rowadr"):
+        np.testing.assert_array_equal(k.field(name)[:m.nv], sp[name])
+    nt = m.sizes["ntendon"]
+    for name in ("ten_J_rownnz", "ten_J_rowadr"):
+      np.testing.assert_array_equal(k.field(name)[:nt], o.d.sparse(name)[:nt])
+    nnz = int(o.d.sparse("ten_J_rownnz")[:nt].sum())
+    np.testing.assert_array_equal(k.field("ten_J_colind")[:nnz], o.d.sparse("ten_J_colind")[:nnz])
+    for f_ in ("ten_J", "ten_velocity", "actuator_moment", "actuator_velocity", "qfrc_passive",
+               "qfrc_constraint"):
+      np.testing.assert_array_equal(getattr(k.d, f_), getattr(o.d, f_))
+    rows += nefc
+  return rows
+
+
+def test_device_code_bitexact_sparse_models():
+  for m, n in ((S.pile(), 24), (S.pile(nfree=4, jacobian="sparse"), 16)):
+    q, v, a = S.states(m, n, seed=1)
+    assert _bitexact(m, q, v, a) > 10 * n
+
+
+@pytest.mark.parametrize("extra", ["", 'integrator="implicit"', 'integrator="implicitfast"'])
+def test_device_code_bitexact_every_row_type(extra):
+  flags = '<option><flag invdiscrete="enable"/></option>' if extra else ""
+  m = S.misc("sparse", extra, flags)
+  q, v, a = S.misc_states(m, 32, seed=6)
+  assert _bitexact(m, q, v, a) > 20 * 32
+
+
+def test_device_code_bitexact_humanoid100():
+  """The reference's 627-dof model: ~150 contacts and ~630 rows per state, ~7.3K compressed
+  entries where the dense rows held ~400K."""
+  m = H.model()
+  q, v, a = H.states(m, 6, seed=5)
+  assert _bitexact(m, q, v, a, efc_cap=H.MAX_ROWS, con_cap=H.MAX_CONTACTS) > 3000

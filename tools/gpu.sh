@@ -41,6 +41,10 @@ for step in "$@"; do
     c5)
       timeout -k 10 180 python bench.py --config 5 > gpurun_out/c5.json 2> gpurun_out/c5.err || exit 1
       tail -1 gpurun_out/c5.json ;;
+    c5own)
+      timeout -k 10 180 python bench.py --config 5 --own-stream > gpurun_out/c5own.json \
+        2> gpurun_out/c5own.err || exit 1
+      tail -1 gpurun_out/c5own.json ;;
     c5trace)
       timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o c5 \
         --output-format csv -- python bench.py --config 5 --steps 20 --warmup 3 \
