@@ -323,6 +323,10 @@ MJHIP_API const char* mjhip_contextFastKernel(const mjhipContext* c);
 MJHIP_API int mjhip_contextLoadKernel(mjhipContext* c, const void* image, size_t size,
                                       const char* name, unsigned long long signature,
                                       int cmode);
+/* kernels the context's last batched mj_inverseSkip ran on: 0 the generic kernel, 1 the
+ * straight-line pipeline (skipstage NONE), 2 the straight-line mj_inverseSkip(POS / VEL)
+ * kernels (k_va / k_acc of the model's generated code); -1 before any call */
+MJHIP_API int mjhip_contextLastPath(const mjhipContext* c);
 /* instances of the last fast-path call that had active constraint rows and were recomputed
  * by the generic kernel (blocking read; -1 on error) */
 MJHIP_API int mjhip_worklistCount(mjhipContext* c);

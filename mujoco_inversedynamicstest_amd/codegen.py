@@ -1207,6 +1207,7 @@ def _gen_va(M: _Model, store_fields=None) -> str:
     E.open()
     E("double tmp[6], tmp1[6];")
     _emit_muldofvec(E, "tmp", "cdofdot", bda, dn, "qvel")
+    E("mjh::pin(tmp, 6);")       # shared with _gen_acc: both round these terms alike
     E(f"mjh::add(cacc_{i}, cacc_{p}, tmp, 6);")
     E(f"mjh::add(acca_{i}, acca_{p}, tmp, 6);")
     _emit_muldofvec(E, "tmp", "cdof", bda, dn, "qacc")
@@ -1215,6 +1216,7 @@ def _gen_va(M: _Model, store_fields=None) -> str:
     E(f"mjh::mulInertVec(frca_{i}, cinert_{i}, acca_{i});")
     E(f"mjh::mulInertVec(tmp, cinert_{i}, cvel_{i});")
     E(f"mjh::crossForce(tmp1, cvel_{i}, tmp);")
+    E("mjh::pin(tmp1, 6);")
     E(f"mjh::addTo(cfrc_{i}, tmp1, 6);")
     E(f"mjh::addTo(frca_{i}, tmp1, 6);")
     E.close()
@@ -1267,6 +1269,90 @@ def _gen_va(M: _Model, store_fields=None) -> str:
     E("ec[0] = 0; ec[64] = 0; ec[128] = 0; ec[192] = 0;")
   elif M.cmode == "list":   # served instances get their counts from k_constraint
     E("if (!cflag) { ec[0] = 0; ec[64] = 0; ec[128] = 0; ec[192] = 0; }")
+  E("if (status) status[inst] = 0;")
+  return E.text()
+
+
+def _gen_acc(M: _Model, store_fields=None) -> str:
+  """The acceleration stage alone: mj_inverseSkip(mjSTAGE_VEL) (engine_inverse.c:197-261)
+  with the position and velocity stages' outputs read from the mirror. One tree pass of
+  mj_rne(flg_acc = 1) (engine_core_smooth.c:1969-2023) over the stored cinert, cdof, cvel and
+  cdof_dot, then the assembly qfrc_inverse += armature*qacc - passive - constraint, with the
+  same operations as the va stage's second recursion, so the result is its bit for bit. An
+  instance with rows (work-list models) stores the raw RNE for the rows pass (k_skip_rows)."""
+  G = _Stage(M, store_fields)
+  M.acc_stored = G.stored
+  E, m = G.E, M.m
+  nv = M.nv
+  G.prologue()
+  if M.cmode == "list":
+    E("const bool cflag = ec[0] != 0;")
+  G.pointers(["qvel", "qacc", "cinert", "cdof", "cvel", "cdof_dot", "qfrc_passive",
+              "qfrc_constraint", "qfrc_inverse"])
+  G.load("qvel", "qvel", nv)
+  E(f"double qacc[{nv}];")
+  E("// ---- tree pass: mj_rne(flg_acc=1) over the stored velocity-stage outputs")
+  _gravity_acc(M, E)
+  E("double acca_0[6]; mjh::copy(acca_0, cacc_0, 6);")
+
+  def pre(i):
+    if not i:
+      return
+    bda, dn = M.bdofadr[i], M.bdofnum[i]
+    p = M.parent[i]
+    E.open(f"{{  // body {i}")
+    E(f"double acca_{i}[6], frca_{i}[6];")
+    E.open()
+    E("double tmp[6], tmp1[6];")
+    _emit_muldofvec(E, "tmp", "cdofdot", bda, dn, "qvel")
+    E("mjh::pin(tmp, 6);")       # as _gen_va pins them (there each has two uses)
+    E(f"mjh::add(acca_{i}, acca_{p}, tmp, 6);")
+    _emit_muldofvec(E, "tmp", "cdof", bda, dn, "qacc")
+    E(f"mjh::addTo(acca_{i}, tmp, 6);")
+    E(f"mjh::mulInertVec(frca_{i}, cinert_{i}, acca_{i});")
+    E(f"mjh::mulInertVec(tmp, cinert_{i}, cvel_{i});")
+    E(f"mjh::crossForce(tmp1, cvel_{i}, tmp);")
+    E("mjh::pin(tmp1, 6);")
+    E(f"mjh::addTo(frca_{i}, tmp1, 6);")
+    E.close()
+
+  def post(i):
+    if not i:
+      return
+    for k in range(M.bdofadr[i], M.bdofadr[i] + M.bdofnum[i]):
+      E.open()
+      E(f"double qfi = mjh::dot6(cdofp_{k}, frca_{i});")
+      if M.cmode == "all":
+        G.st("qfrc_inverse", k, "qfi")
+      else:
+        E(f"const double qfa = qfi + ({lit(m.dof_armature[k])} * qacc[{k}] - qfp_{k} - 0.0);")
+        E("qfi = cflag ? qfi : qfa;" if M.cmode == "list" else "qfi = qfa;")
+        G.st("qfrc_constraint", k, "0.0")
+        G.st("qfrc_inverse", k, "qfi")
+        E(f"qo_lds[{_ll('va')[0]}*{nv} + {k}] = qfi;")
+      E.close()
+    if M.parent[i]:
+      E(f"mjh::addTo(frca_{M.parent[i]}, frca_{i}, 6);")
+    E.close()
+
+  def loads(kind, i):
+    dofs = range(M.bdofadr[i], M.bdofadr[i] + M.bdofnum[i])
+    if kind == "pre":
+      decls = [f"double cinert_{i}[10], cvel_{i}[6];"] + \
+          [f"double cdof_{k}[6], cdofdot_{k}[6];" for k in dofs]
+      ld = _vec_loads(f"cinert_{i}", "cinert", 10 * i, 10) + \
+          _vec_loads(f"cvel_{i}", "cvel", 6 * i, 6)
+      for k in dofs:
+        ld += _vec_loads(f"cdof_{k}", "cdof", 6 * k, 6) + \
+            _vec_loads(f"cdofdot_{k}", "cdof_dot", 6 * k, 6) + [(f"qacc[{k}]", "qacc", k)]
+    else:
+      decls = [f"double cdofp_{k}[6], qfp_{k};" for k in dofs]
+      ld = []
+      for k in dofs:
+        ld += _vec_loads(f"cdofp_{k}", "cdof", 6 * k, 6) + [(f"qfp_{k}", "qfrc_passive", k)]
+    return decls, ld
+
+  _prefetched_dfs(G, loads, pre, post, PREFETCH)
   E("if (status) status[inst] = 0;")
   return E.text()
 
@@ -1511,6 +1597,26 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
                f"int slane, int B, const int* __restrict__ ecs, {_SIG['va'][0]}) {{\n"
                f"{skip_body}\n}}\n")
   if M.cmode in ("none", "list"):
+    # the acceleration stage alone (mj_inverseSkip(mjSTAGE_VEL)): k_acc for batched calls, and
+    # in k_fdskip for mjd_inverseFD's qacc perturbations, whose velocity-stage inputs (cvel,
+    # cdof_dot, qfrc_passive) and position-stage inputs are their centre's
+    import re
+    ab = _gen_acc(M)
+    if NT_STORES:
+      ab = re.sub(r"^(\s*)P_(\w+)\[(\d+)\*64\] = (.+);$",
+                  lambda mt: f"{mt.group(1)}MJH_NT_STORE(P_{mt.group(2)}[{mt.group(3)}*64], "
+                             f"{mt.group(4)});", ab, flags=re.M)
+    out.append(f"MJH_HD void fast_acc_{name}(const Mirror& mr, int blk, int lane, int B, "
+               f"{_SIG['va'][0]}) {{\n{ab}\n}}\n")
+    own_acc = {"qacc"} | M.acc_stored
+    acc_skip = re.sub(r"(double\* __restrict__ P_(\w+) = mr\.\w+ \+ \(\(long\))blk(\*\d+\)\*64 \+ )lane;",
+                      lambda mt: mt.group(0) if mt.group(2) in own_acc else
+                      f"{mt.group(1)}sblk{mt.group(3)}slane;", ab)
+    acc_skip = acc_skip.replace("const bool cflag = ec[0] != 0;", "const bool cflag = ecs[0] != 0;")
+    out.append(f"MJH_HD void fast_accskip_{name}(const Mirror& mr, int blk, int lane, int sblk, "
+               f"int slane, int B, const int* __restrict__ ecs, {_SIG['va'][0]}) {{\n"
+               f"{acc_skip}\n}}\n")
+  if M.cmode in ("none", "list"):
     flag = ("  if (ecs[0] != 0) needfull[0] = 1;\n" if M.cmode == "list" else "")
     out.append(f"""__global__ __launch_bounds__(64, 1) void k_vaskip_{name}(Mirror mr, int B, int off,
     int per, int sstride, int* __restrict__ efc_count, int* __restrict__ needfull) {{
@@ -1526,6 +1632,57 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
                                 int sstride, int* efc_count, int* needfull) {{
   hipLaunchKernelGGL(k_vaskip_{name}, dim3((B - off + 63) / 64), dim3(64), 0, s, mr, B, off,
                      per, sstride, efc_count, needfull);
+}}
+// mjd_inverseFD layout 2 in one launch over [off, B): the nq = (B - off)/2 qvel perturbations
+// (mj_inverseSkip(mjSTAGE_POS): the va stage over the centre's position stage) on the first
+// blocks, the longer waves, then the nq qacc perturbations (mjSTAGE_VEL: the acceleration
+// stage over the centre's position and velocity stages). nq is a multiple of 64, so each wave
+// has one role; the two run side by side instead of as two under-filled launches.
+__global__ __launch_bounds__(64, 1) void k_fdskip_{name}(Mirror mr, int B, int off,
+    int per, int sstride, int* __restrict__ efc_count, int* __restrict__ needfull) {{
+  __shared__ double qo_lds[{64 * max(M.nv, 1)}];
+  const long nq = ((long)B - off) / 2;
+  const long t = (long)blockIdx.x*64 + threadIdx.x;
+  if (t >= 2*nq) return;
+  const bool vel = t < nq;
+  const long gi = vel ? off + nq + t : off + (t - nq);
+  const long si = (vel ? t : t - nq) / per * sstride;
+  const int* ecs = efc_count + (si >> 6)*4*64 + (si & 63);
+{flag}  if (vel) {{
+    fast_vaskip_{name}(mr, (int)(gi >> 6), (int)(gi & 63), (int)(si >> 6), (int)(si & 63), B,
+                      ecs, nullptr, nullptr, efc_count, qo_lds, nullptr);
+  }} else {{
+    fast_accskip_{name}(mr, (int)(gi >> 6), (int)(gi & 63), (int)(si >> 6), (int)(si & 63), B,
+                       ecs, nullptr, nullptr, efc_count, qo_lds, nullptr);
+  }}
+}}
+{"" if shared else "static "}void launch_fdskip_{name}(hipStream_t s, const Mirror& mr, int B, int off, int per,
+                                int sstride, int* efc_count, int* needfull) {{
+  hipLaunchKernelGGL(k_fdskip_{name}, dim3((B - off + 63) / 64), dim3(64), 0, s, mr, B, off,
+                     per, sstride, efc_count, needfull);
+}}
+// batched mj_inverseSkip on the straight-line path: POS runs the va stage (k_va), VEL the
+// acceleration stage (k_acc); rows of the previous call go through k_skip_rows (mjhip.hip)
+__global__ __launch_bounds__(64, 1) void k_acc_{name}(Mirror mr, int B,
+    double* __restrict__ qfrc_out, int* __restrict__ status, int* __restrict__ efc_count) {{
+  __shared__ double qo_lds[{64 * max(M.nv, 1)}];
+  fast_acc_{name}(mr, blockIdx.x, threadIdx.x, B, qfrc_out, status, efc_count, qo_lds, nullptr);
+  if (!qfrc_out) return;
+  __syncthreads();
+  const long r0 = (long)blockIdx.x*64;
+  const long n = ((long)B - r0 < 64 ? (long)B - r0 : 64) * {M.nv};
+  double* dst = qfrc_out + r0*{M.nv};
+  for (long r = threadIdx.x; r < n; r += 64) dst[r] = qo_lds[r];
+}}
+{"" if shared else "static "}void launch_skip_{name}(hipStream_t s, const Mirror& mr, int B, int skipstage,
+                              double* qfrc_out, int* status, int* efc_count) {{
+  if (skipstage == 1) {{
+    hipLaunchKernelGGL(k_va_{name}, dim3((B + 63) / 64), dim3(64), 0, s, mr, B, qfrc_out,
+                       status, efc_count);
+  }} else {{
+    hipLaunchKernelGGL(k_acc_{name}, dim3((B + 63) / 64), dim3(64), 0, s, mr, B, qfrc_out,
+                       status, efc_count);
+  }}
 }}""")
   out.append(f"""{"" if shared else "static "}void launch_fast_{name}(dim3 g, dim3 b, hipStream_t s, const Mirror& mr,
     int B, const double* qpos_in, const double* qvel_in, const double* qacc_in, double* qfrc_out,
@@ -1586,16 +1743,20 @@ def generate_registries(entries) -> tuple:
                   "const double*, const double*, const double*, double*, int*, int*, int*, "
                   "int*, int*, const int*);")
       if vaskip:
-        main.append(f"void launch_vaskip_{name}(hipStream_t, const Mirror&, int, int, int, int, "
+        for k in ("vaskip", "fdskip"):
+          main.append(f"void launch_{k}_{name}(hipStream_t, const Mirror&, int, int, int, int, "
+                      "int*, int*);")
+        main.append(f"void launch_skip_{name}(hipStream_t, const Mirror&, int, int, double*, "
                     "int*, int*);")
     else:
       main.append(generate(m, name))
+    fns = ", ".join(f"launch_{k}_{name}" if vaskip else "nullptr"
+                    for k in ("vaskip", "fdskip", "skip"))
     reg.append(f'  {{0x{fields.model_signature(m):016x}ull, launch_fast_{name}, "{name}", '
-               f'{CONSTRAINT_MODES[constraint_mode(m)]}, '
-               f'{"launch_vaskip_" + name if vaskip else "nullptr"}}},')
+               f'{CONSTRAINT_MODES[constraint_mode(m)]}, {fns}}},')
   main.append("static const FastKernelEntry g_fast_kernels[] = {")
   main.extend(reg)
-  main.append("  {0ull, nullptr, nullptr, 0, nullptr}};")
+  main.append("  {0ull, nullptr, nullptr, 0, nullptr, nullptr, nullptr}};")
   return "\n".join(main) + "\n", "\n".join(exact) + "\n"
 
 
@@ -1606,10 +1767,12 @@ def generate_registry(entries) -> str:
   reg = []
   for name, m in entries:
     out.append(generate(m, name))
+    sk = constraint_mode(m) in ("none", "list")
+    fns = ", ".join(f"launch_{k}_{name}" if sk else "nullptr"
+                    for k in ("vaskip", "fdskip", "skip"))
     reg.append(f'  {{0x{fields.model_signature(m):016x}ull, launch_fast_{name}, "{name}", '
-               f'{CONSTRAINT_MODES[constraint_mode(m)]}, '
-               f'{"launch_vaskip_" + name if constraint_mode(m) in ("none", "list") else "nullptr"}}},')
+               f'{CONSTRAINT_MODES[constraint_mode(m)]}, {fns}}},')
   out.append("static const FastKernelEntry g_fast_kernels[] = {")
   out.extend(reg)
-  out.append("  {0ull, nullptr, nullptr, 0, nullptr}};")
+  out.append("  {0ull, nullptr, nullptr, 0, nullptr, nullptr, nullptr}};")
   return "\n".join(out) + "\n"

@@ -467,6 +467,15 @@ template <class R> MJH_HD void zero(R r, int n) { for (int i = 0; i < n; i++) r[
 template <class R, class A> MJH_HD void copy(R r, A a, int n) {
   for (int i = 0; i < n; i++) r[i] = a[i];
 }
+// a value barrier: r[0..n) stay the rounded values computed, so no later multiply-add is
+// contracted or re-associated through them. The straight-line va stage and the acceleration
+// stage alone (codegen.py _gen_acc) pin the same shared terms of their RNE recursion, so the
+// two round identically whatever the compiler fuses in either (mjd_inverseFD's k_accskip).
+template <class R> MJH_HD void pin(R r, int n) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  for (int i = 0; i < n; i++) __asm__("" : "+v"(r[i]));
+#endif
+}
 template <class R, class A> MJH_HD void scl(R r, A a, double s, int n) {
   for (int i = 0; i < n; i++) r[i] = a[i]*s;
 }

@@ -19,6 +19,14 @@ struct FastKernelEntry {
   // instances [off, B), position-stage inputs from centre (t - off)/per*sstride (codegen.py
   // k_vaskip); null for run-time kernels and models whose rows serve every instance
   void (*launch_vaskip)(hipStream_t, const Mirror&, int, int, int, int, int*, int*);
+  // mjd_inverseFD layout 2 in one launch over [off, B) (k_fdskip): the first half of the
+  // instances qacc perturbations, mj_inverseSkip(mjSTAGE_VEL), the acceleration stage alone
+  // over the centre's position- and velocity-stage outputs; the second half qvel
+  // perturbations, mjSTAGE_POS, as k_vaskip (centres (t - off)/per*sstride within each half)
+  void (*launch_fdskip)(hipStream_t, const Mirror&, int, int, int, int, int*, int*);
+  // batched mj_inverseSkip(skipstage) for skipstage POS (k_va) or VEL (k_acc) over [0, B)
+  // (qfrc_out row-major or null, status or null, efc_count)
+  void (*launch_skip)(hipStream_t, const Mirror&, int, int, double*, int*, int*);
 };
 
 // the bundled models' kernels (gen_fast.hip), terminated by an entry with launch = nullptr

@@ -6,7 +6,8 @@
 #if __has_include("gen_fast.inc")
 #include "gen_fast.inc"
 #else
-static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr, 0}};
+static const FastKernelEntry g_fast_kernels[] = {{0ull, nullptr, nullptr, 0, nullptr, nullptr,
+                                                  nullptr}};
 #endif
 
 const FastKernelEntry* mjhip_fastKernels() { return g_fast_kernels; }

@@ -72,15 +72,37 @@ __global__ __launch_bounds__(64) void k_discrete_restore(mjhipModel m, Mirror mr
 // only when statuses are asked for: inside the generated kernels the extra live values
 // cost spills (tools/kernel_resources.py).
 __global__ __launch_bounds__(64) void k_check(mjhipModel m, Mirror mr, int B,
-                                              int* __restrict__ status) {
+                                              int* __restrict__ status, int skipstage) {
   const long inst = (long)blockIdx.x*64 + threadIdx.x;
   if (inst >= B) return;
   Lane<64> d = lane_view(mr, blockIdx.x, threadIdx.x);
-  int st = mjh::checkInputs(m, d, mjhipSTAGE_NONE);
-  for (int k = 0; k < m.nv; k++) {
+  int st = mjh::checkInputs(m, d, skipstage);
+  for (int k = 0; skipstage == mjhipSTAGE_NONE && k < m.nv; k++) {
     if (!(d.qLD[m.C_rowadr[k] + m.C_rownnz[k] - 1] >= mjh::MINVAL)) st |= MJHIP_INST_INERTIA;
   }
   if (st) status[inst] |= st;
+}
+
+// Batched mj_inverseSkip(POS / VEL) on the straight-line path: the generated k_va (POS) or
+// k_acc (VEL) ran the remaining stages and, for an instance with constraint rows (made by the
+// previous call), left the raw mj_rne(flg_acc = 1) in qfrc_inverse. Here those instances
+// finish as the reference does on the rows it kept: mj_referenceConstraint when the velocity
+// stage ran (POS), mj_invConstraint, then the assembly (engine_inverse.c:169-252).
+__global__ __launch_bounds__(64) void k_skip_rows(mjhipModel m, Mirror mr, int B, int skipstage,
+                                                  double* __restrict__ qfrc_out) {
+  const long inst = (long)blockIdx.x*64 + threadIdx.x;
+  if (inst >= B) return;
+  Lane<64> d = lane_view(mr, blockIdx.x, threadIdx.x);
+  if (!d.efc_count[0]) return;
+  if (skipstage == mjhipSTAGE_POS) mjh::referenceConstraint(m, d);
+  mjh::invConstraint(m, d);
+  for (int i = 0; i < m.nv; i++) {
+    d.qfrc_inverse[i] += m.dof_armature[i] * d.qacc[i] - d.qfrc_passive[i] -
+                         d.qfrc_constraint[i];
+  }
+  if (qfrc_out) {
+    for (int i = 0; i < m.nv; i++) qfrc_out[inst*m.nv + i] = d.qfrc_inverse[i];
+  }
 }
 
 // slider-crank/site/body transmissions, sensors and energy after the generated kernels and
@@ -116,11 +138,17 @@ __global__ void k_from_mirror(const double* __restrict__ src, double* __restrict
 // Layout 1 (stage skipping, mj_inverseSkip(mjSTAGE_POS) for the qvel/qacc perturbations):
 // the instances that run the position stage first, b*(nv+1) + j (j = 0 centre, j = i+1 the
 // qpos perturbation of dof i), then from A = nbase*(nv+1) the others, A + b*2nv + (p-1).
+// Layout 2 (the qacc perturbations run mj_inverseSkip(mjSTAGE_VEL), the qvel ones
+// mjSTAGE_POS, engine_derivative_fd.c:646-699): the same position-stage block, then the qacc
+// perturbations A + b*nv + (p-1), then the qvel ones A + nbase*nv + b*nv + (p-1-nv), so that
+// each skip kernel covers whole waves of one kind.
 __device__ static inline long fd_inst(int layout, long nbase, long b, int p, int nv) {
   if (!layout) return b*(3*nv + 1) + p;
   if (p == 0) return b*(nv + 1);
   if (p > 2*nv) return b*(nv + 1) + (p - 2*nv);
-  return nbase*(nv + 1) + b*2*nv + (p - 1);
+  if (layout == 1) return nbase*(nv + 1) + b*2*nv + (p - 1);
+  if (p <= nv) return nbase*(nv + 1) + b*nv + (p - 1);
+  return nbase*(nv + 1) + nbase*nv + b*nv + (p - 1 - nv);
 }
 
 __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __restrict__ qpos,
@@ -140,10 +168,16 @@ __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __
     b = inst / (m.nv + 1);
     const int j = (int)(inst % (m.nv + 1));
     p = j ? 2*m.nv + j : 0;
-  } else {
+  } else if (layout == 1) {
     const long t = inst - (long)nbase*(m.nv + 1);
     b = t / (2*m.nv);
     p = 1 + (int)(t % (2*m.nv));
+  } else {
+    long t = inst - (long)nbase*(m.nv + 1);
+    const bool vel = t >= (long)nbase*m.nv;
+    if (vel) t -= (long)nbase*m.nv;
+    b = t / m.nv;
+    p = 1 + (int)(t % m.nv) + (vel ? m.nv : 0);
   }
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
   for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos[b*m.nq + k];
@@ -365,6 +399,7 @@ struct mjhipContext_ {
   int* worklist = nullptr;                 // capacity + 2 ints: [count0, count1, list...]
   int wl_parity = 0;                       // counter the next fast launch uses
   int wl_last = 0;                         // counter the last fast launch used
+  int last_path = -1;                      // mjhip_contextLastPath
   // mjhip_inverseFDBatch's stage-skip fall-back, decided on the device: [0] a centre has limit
   // rows (k_vaskip), [1..2] the instance range {first, end} k_fd_gate hands to k_all
   int* fdflag = nullptr;
@@ -917,6 +952,8 @@ MJHIP_API const char* mjhip_contextFastKernel(const mjhipContext* c) {
   return (c && c->fast) ? c->fast->name : nullptr;
 }
 
+MJHIP_API int mjhip_contextLastPath(const mjhipContext* c) { return c ? c->last_path : -1; }
+
 MJHIP_API int mjhip_worklistCount(mjhipContext* c) {
   if (!c) return -1;
   int n = 0;
@@ -952,7 +989,9 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     set_error("launch_inverse: a device-side range needs the bare straight-line pipeline");
     return MJHIP_ERR_ARG;
   }
+  c->last_path = 0;
   if (skipstage == mjhipSTAGE_NONE && c->fast && !(flags & MJHIP_FLAG_GENERIC)) {
+    c->last_path = 1;
     // two work-list counters alternate: this launch counts into `cnt` (zeroed by the
     // previous launch's k_pos, or at context creation) and zeroes `nxt` for the next one
     int* cnt = c->worklist + c->wl_parity;
@@ -1034,11 +1073,51 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
                          B);
     }
     if (status) {
-      hipLaunchKernelGGL(k_check, grid, block, 0, c->stream, c->dmodel, c->mirror, B, status);
+      hipLaunchKernelGGL(k_check, grid, block, 0, c->stream, c->dmodel, c->mirror, B, status,
+                         (int)mjhipSTAGE_NONE);
       HIPCHECK(hipGetLastError());
     }
     c->wl_last = c->wl_parity;
     c->wl_parity ^= 1;
+    return MJHIP_OK;
+  }
+  // mj_inverseSkip(POS / VEL) on the straight-line kernels: the bare pipeline (no passes
+  // after the generated kernels) of a model whose rows serve only limit-active instances
+  const char* noskip = getenv("MJHIP_SKIP_GENERIC");
+  if ((skipstage == mjhipSTAGE_POS || skipstage == mjhipSTAGE_VEL) && c->fast &&
+      c->fast->launch_skip && !(flags & MJHIP_FLAG_GENERIC) && !c->spatial &&
+      !mjh::hasFluid(c->hmodel) && !mjh::hasDiscrete(c->hmodel) &&
+      !mjh_needTrnAfter(&c->hmodel) && !(c->hmodel.opt.enableflags & mjhipENBL_ENERGY) &&
+      (skipsensor || !c->hmodel.nsensor || (c->hmodel.opt.disableflags & mjhipDSBL_SENSOR)) &&
+      !(noskip && noskip[0] == '1')) {
+    // row-major inputs into the mirror, as k_inverse copies them: the remaining stages read
+    // qpos (springs) and qvel (mj_rne's cdof_dot * qvel) even when their own stage is skipped
+    const int nq = c->hmodel.nq, nv = c->hmodel.nv;
+    if (qpos) {
+      hipLaunchKernelGGL(k_to_mirror, dim3(((long)B*nq + 255)/256), dim3(256), 0, c->stream,
+                         qpos, c->mirror.qpos, B, nq);
+    }
+    if (qvel) {
+      hipLaunchKernelGGL(k_to_mirror, dim3(((long)B*nv + 255)/256), dim3(256), 0, c->stream,
+                         qvel, c->mirror.qvel, B, nv);
+    }
+    if (qacc) {
+      hipLaunchKernelGGL(k_to_mirror, dim3(((long)B*nv + 255)/256), dim3(256), 0, c->stream,
+                         qacc, c->mirror.qacc, B, nv);
+    }
+    c->last_path = 2;
+    c->fast->launch_skip(c->stream, c->mirror, B, skipstage, qfrc, status, c->mirror.efc_count);
+    HIPCHECK(hipGetLastError());
+    if (c->fast->cmode == 1) {
+      hipLaunchKernelGGL(k_skip_rows, grid, block, 0, c->stream, c->dmodel, c->mirror, B,
+                         skipstage, qfrc);
+      HIPCHECK(hipGetLastError());
+    }
+    if (status) {
+      hipLaunchKernelGGL(k_check, grid, block, 0, c->stream, c->dmodel, c->mirror, B, status,
+                         skipstage);
+      HIPCHECK(hipGetLastError());
+    }
     return MJHIP_OK;
   }
 #define MJHIP_LAUNCH_K(SK, C, F)                                                              \
@@ -1570,18 +1649,27 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
   // sensors are skipped when no sensor derivative is asked for (derivative_fd.c:628)
   const int skipsensor = !DsDq && !DsDv && !DsDa;
   // Stage skipping as the reference's loop does (engine_derivative_fd.c:646-699): the qvel
-  // and qacc perturbations run mj_inverseSkip(mjSTAGE_POS), i.e. only the generated va stage
-  // (k_vaskip) over their centre's position-stage outputs. Skipped stages would see
-  // unchanged inputs, so the Jacobians equal the full pipeline's bit for bit. Taken only
-  // where the straight-line kernel is the whole pipeline (no post passes, sensors or
-  // actuation terms) and the position-stage block ends on a wave boundary.
-  const long nA = (long)B*(nv + 1);
+  // perturbations run mj_inverseSkip(mjSTAGE_POS), only the generated va stage over their
+  // centre's position-stage outputs, and the qacc ones mjSTAGE_VEL, the acceleration stage
+  // alone over the centre's position and velocity stages (layout 2, k_fdskip; layout 1 runs
+  // both kinds on the va stage, k_vaskip). Skipped stages would see unchanged inputs: layout 1
+  // equals the full pipeline bit for bit; layout 2 is the same arithmetic in a differently
+  // shaped kernel, where the compiler's multiply-add contraction can round a term differently
+  // (a few ulp of qfrc_inverse). Taken only where the straight-line kernel
+  // is the whole pipeline (no post passes, sensors or actuation terms) and the
+  // position-stage block ends on a wave boundary.
+  const long nA = (long)B*(nv + 1), nQ = (long)B*nv;
   const char* noskip = getenv("MJHIP_FD_NOSKIP");
-  const int layout = c->fast && c->fast->launch_vaskip && !(flags & MJHIP_FLAG_GENERIC) &&
-                     skipsensor && !flg_actuation && !c->spatial && !mjh::hasFluid(c->hmodel) &&
-                     !mjh::hasDiscrete(c->hmodel) && !mjh_needTrnAfter(&c->hmodel) &&
-                     !(m.opt.enableflags & mjhipENBL_ENERGY) && nA % 64 == 0 &&
-                     !(noskip && noskip[0] == '1');
+  const char* accskip = getenv("MJHIP_FD_ACCSKIP");
+  int layout = c->fast && c->fast->launch_vaskip && !(flags & MJHIP_FLAG_GENERIC) &&
+               skipsensor && !flg_actuation && !c->spatial && !mjh::hasFluid(c->hmodel) &&
+               !mjh::hasDiscrete(c->hmodel) && !mjh_needTrnAfter(&c->hmodel) &&
+               !(m.opt.enableflags & mjhipENBL_ENERGY) && nA % 64 == 0 &&
+               !(noskip && noskip[0] == '1');
+  // layout 2 on request (MJHIP_FD_ACCSKIP=1), when the two perturbation blocks are whole waves
+  // each: not the default, as it measured no faster (k_fdskip 62-64 us against k_vaskip's
+  // 56 us over the same 55,296 instances)
+  if (layout && c->fast->launch_fdskip && nQ % 64 == 0 && accskip && accskip[0] == '1') layout = 2;
   int rc = MJHIP_OK;
   hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream,
                      c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, layout,
@@ -1592,9 +1680,16 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
     rc = launch_inverse(c, (int)nA, nullptr, nullptr, nullptr, nullptr, mjhipSTAGE_NONE,
                         nullptr, 0, skipsensor);
     if (rc) return rc;
-    // the 2nv qvel/qacc perturbations: the va stage over their centre's position stage
-    c->fast->launch_vaskip(c->stream, c->mirror, (int)ninst, (int)nA, 2*nv, nv + 1,
-                           c->mirror.efc_count, c->fdflag);
+    if (layout == 2) {
+      // the nv qacc perturbations: the acceleration stage over their centre's position and
+      // velocity stages; the nv qvel ones: the va stage over their centre's position stage
+      c->fast->launch_fdskip(c->stream, c->mirror, (int)ninst, (int)nA, nv, nv + 1,
+                             c->mirror.efc_count, c->fdflag);
+    } else {
+      // the 2nv qvel/qacc perturbations: the va stage over their centre's position stage
+      c->fast->launch_vaskip(c->stream, c->mirror, (int)ninst, (int)nA, 2*nv, nv + 1,
+                             c->mirror.efc_count, c->fdflag);
+    }
     FDCHECK(hipGetLastError(), "k_vaskip launch");
     if (c->fast->cmode == 1) {
       // a work-list model whose centre has limit rows: its perturbations need the rows'

@@ -55,6 +55,7 @@ SIGNATURES = {
     "mjhip_contextLoadKernel": (ctypes.c_int, [_V, _V, ctypes.c_size_t, ctypes.c_char_p,
                                                ctypes.c_ulonglong, ctypes.c_int]),
     "mjhip_worklistCount": (ctypes.c_int, [_V]),
+    "mjhip_contextLastPath": (ctypes.c_int, [_V]),
     "mjhip_contextStream": (_V, [_V]),
     "mjhip_contextSetStream": (ctypes.c_int, [_V, _V]),
     "mjhip_inverseBatch": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, _V, ctypes.c_int,
@@ -245,6 +246,12 @@ class InverseEngine:
     """Name of the model-specialized kernel in use, or None (generic kernel)."""
     n = lib().mjhip_contextFastKernel(self.ctx)
     return n.decode() if n else None
+
+  @property
+  def last_path(self):
+    """Kernels of the last batched inverse: 0 generic, 1 straight-line pipeline, 2 the
+    straight-line mj_inverseSkip(POS / VEL) kernels."""
+    return lib().mjhip_contextLastPath(self.ctx)
 
   def worklist_count(self):
     return lib().mjhip_worklistCount(self.ctx)

@@ -100,6 +100,56 @@ def test_skipstage_chain(humanoid, eng):
   assert_close(f_pos, rp, "skip POS")
 
 
+@pytest.mark.parametrize("name", ["humanoid", "inverse_test", "linear", "inertia"])
+def test_skipstage_straight_line(name, monkeypatch):
+  """Batched mj_inverseSkip(POS / VEL) on the straight-line kernels (k_va for POS, k_acc for
+  VEL): the path is asserted (mjhip_contextLastPath = 2), on the humanoid
+  a fifth of the instances carry limit rows from the full call (k_skip_rows finishes them), and
+  the results match the oracle's serial mj_inverseSkip chain and the generic kernel
+  (MJHIP_SKIP_GENERIC=1) to the north-star tolerance, with inputs given for every field."""
+  m = models.load(name, disable_contact=True, disable_sensor=(name == "linear"))
+  B = 200
+  q, v, a = sample_states(m, B, first=21)
+  if name == "humanoid":
+    j = int(np.flatnonzero(np.asarray(m.jnt_limited))[3])
+    q[::5, m.jnt_qposadr[j]] = m.jnt_range[j][1] + 0.2
+  a2, v2 = a + 0.25, v * 0.9
+  e = engine.InverseEngine(m, capacity=256)
+  try:
+    assert e.fast_kernel == name
+    got = []
+    for generic in (False, True):
+      if generic:
+        monkeypatch.setenv("MJHIP_SKIP_GENERIC", "1")
+      e.inverse(q, v, a)
+      assert e.last_path == 1
+      fv, sv = e.inverse(q, v, a2, skipstage=engine.mjSTAGE_VEL, status=True)
+      assert e.last_path == (0 if generic else 2)
+      fp, sp = e.inverse(q, v2, a2, skipstage=engine.mjSTAGE_POS, status=True)
+      assert e.last_path == (0 if generic else 2)
+      assert (sv == 0).all() and (sp == 0).all()
+      got.append((fv, fp, e.field("qfrc_constraint", 0, B), e.field("efc_force", 0, B)))
+    nefc = e.field_int("efc_count", 0, B)[:, 0]
+  finally:
+    e.close()
+  o = Oracle(m)
+  rv, rp, rc = [], [], []
+  for i in range(B):
+    o.inverse(q[i], v[i], a[i])
+    rv.append(o.inverse(qacc=a2[i], skipstage=2))
+    rp.append(o.inverse(qvel=v2[i], skipstage=1))
+    rc.append(o.d.qfrc_constraint.copy())
+    assert o.d.nefc == nefc[i]
+  if name == "humanoid":
+    assert (nefc[::5] > 0).all()
+  for (fv, fp, qc, _), what in zip(got, ("straight-line", "generic")):
+    assert_close(fv, rv, f"{name} skip VEL ({what})")
+    assert_close(fp, rp, f"{name} skip POS ({what})")
+    assert_close(qc, rc, f"{name} qfrc_constraint ({what})")
+  assert_close(got[0][0], got[1][0], "VEL straight-line vs generic")
+  assert_close(got[0][1], got[1][1], "POS straight-line vs generic")
+
+
 @pytest.mark.parametrize("B", [1, 63, 64, 65, 1000])
 def test_ragged_batches(humanoid, eng, B):
   q, v, a = sample_states(humanoid, B, first=500)
@@ -197,12 +247,15 @@ def test_inverse_fd_parity(humanoid):
 @pytest.mark.parametrize("NB,limits", [(1024, "none"), (64, "all"), (64, "some"),
                                        (3, "none")])
 def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
-  """mjd_inverseFD's stage skipping (engine_derivative_fd.c:646-699: the qvel and qacc
-  perturbations run mj_inverseSkip(mjSTAGE_POS), here the generated va stage over the
-  centre's position-stage outputs) equals every perturbation through the full pipeline
-  (MJHIP_FD_NOSKIP=1) bit for bit. NB=1024 takes the skip layout; with joint limits active
-  on every centre, or on every fifth, the work-list model falls back on the device to the full
-  pipeline over the perturbations; NB=3 (28*3 instances, not a whole wave) never takes it."""
+  """mjd_inverseFD's stage skipping (engine_derivative_fd.c:646-699: the qvel perturbations
+  run mj_inverseSkip(mjSTAGE_POS), the qacc ones mjSTAGE_VEL) against every perturbation
+  through the full pipeline (MJHIP_FD_NOSKIP=1). Layout 1 (both kinds on the va stage over the
+  centre's position-stage outputs, k_vaskip, the default) equals it bit for bit; layout 2
+  (MJHIP_FD_ACCSKIP=1: the qacc perturbations on the acceleration stage alone over the centre's velocity stage,
+  k_fdskip) equals it bit for bit in DfDq, DfDv and DmDq and within the contraction bound in
+  DfDa. NB=1024 takes the skip layouts; with joint limits active on every centre, or on every
+  fifth, the work-list model falls back on the device to the full pipeline over the
+  perturbations; NB=3 (28*3 instances, not a whole wave) never takes them."""
   q, v, a = sample_states(humanoid, NB, first=300)
   if limits != "none":                  # push a limited hinge past its range
     j = int(np.flatnonzero(np.asarray(humanoid.jnt_limited))[3])
@@ -210,20 +263,37 @@ def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
     q[rows, humanoid.jnt_qposadr[j]] = humanoid.jnt_range[j][1] + 0.2
   e = engine.InverseEngine(humanoid, capacity=NB * (3 * humanoid.nv + 1))
   try:
+    got1 = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)      # layout 1, the default
+    monkeypatch.setenv("MJHIP_FD_ACCSKIP", "1")             # layout 2
     got = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
     monkeypatch.setenv("MJHIP_FD_NOSKIP", "1")
     ref = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
   finally:
     e.close()
-  for g, r in zip(got, ref):
-    assert np.array_equal(g, r)
+  for name, g, g1, r in zip(("DfDq", "DfDv", "DfDa", "DmDq"), got, got1, ref):
+    assert np.array_equal(g1, r), name
+    if name == "DfDa":
+      _assert_fd_contraction_close(g, r)
+    else:
+      assert np.array_equal(g, r), name
+
+
+def _assert_fd_contraction_close(g, r, eps=1e-6):
+  """Layout 2's acceleration stage alone (k_fdskip) against the full pipeline: the same
+  operations, but the compiler contracts multiply-adds per kernel, so a term of qfrc_inverse
+  can round differently by a few ulp; the forward difference scales that by 1/eps. Bound: 16
+  ulp of the largest |qfrc_inverse| (<= 1e3 on these states) over eps."""
+  tol = 16 * np.finfo(float).eps * 1e3 / eps
+  err = np.abs(g - r).max()
+  assert err <= tol, f"DfDa layout 2 vs full pipeline {err:.3e} > {tol:.3e}"
 
 
 @pytest.mark.parametrize("name", ["inverse_test", "linear", "inertia"])
 def test_inverse_fd_stage_skip_other_models(name, monkeypatch):
-  """The stage-skip layout on the other bundled models with a k_vaskip kernel (work-list or
-  row-free), device-resident and back to back (no host wait between calls), against the full
-  pipeline bit for bit and the oracle's serial mjd_inverseFD."""
+  """The stage-skip layouts on the other bundled models with a k_vaskip kernel (work-list or
+  row-free): layout 1 device-resident and back to back (no host wait between calls) against
+  the full pipeline bit for bit, layout 2 (k_fdskip) within the contraction bound in DfDa and
+  bit for bit elsewhere, and both against the oracle's serial mjd_inverseFD."""
   import torch
   m = models.load(name, disable_contact=True, disable_sensor=(name == "linear"))
   NB = 64
@@ -239,12 +309,18 @@ def test_inverse_fd_stage_skip_other_models(name, monkeypatch):
     for o in outs[:-1]:
       for x, y in zip(o[:3], got):
         assert np.array_equal(x.cpu().numpy(), y)
+    monkeypatch.setenv("MJHIP_FD_ACCSKIP", "1")             # layout 2, k_fdskip
+    got2 = e.inverse_fd(q, v, a, eps=1e-6)
     monkeypatch.setenv("MJHIP_FD_NOSKIP", "1")
     ref = e.inverse_fd(q, v, a, eps=1e-6)
   finally:
     e.close()
-  for g, r in zip(got, ref[:3]):
-    assert np.array_equal(g, r)
+  for name, g, g2, r in zip(("DfDq", "DfDv", "DfDa"), got, got2, ref[:3]):
+    assert np.array_equal(g, r), name
+    if name == "DfDa":
+      _assert_fd_contraction_close(g2, r)
+    else:
+      assert np.array_equal(g2, r), name
   o = Oracle(m)
   for i in range(0, NB, 8):
     o.set_state(q[i], v[i], a[i])
