@@ -9,6 +9,7 @@
  *   mj_collision: body bitmask, exclude signatures, geom pairs  :265-497
  *   mj_collideGeoms: type order, collision table, geom bitmask  :1440-1620
  *   mj_contactParam (condim)  :1289-1384
+ *   predefined pairs: merged in signature order :316-327, :432-437; mj_collideGeomPair :499-523
  *
  * The broadphase's bounding boxes are inflated by each geom's rbound + margin, so they never
  * reject a pair the narrowphase would report. A body pair is therefore a candidate exactly
@@ -81,6 +82,19 @@ MJHIP_CONTACT_HD int mjhip_bodyPairCandidate(const mjhipModel* m, int b1, int b2
     if (m->exclude_signature[i] == sig) return 0;
   }
   return 1;
+}
+
+/* 1 if geoms g1, g2 (either order) form a predefined <pair>: the body-pair sweep then leaves
+ * them to it (mj_collideGeomPair's merged test, engine_collision_driver.c:499-523; the pair
+ * shares the body pair's signature, so it is among those merged for it) */
+MJHIP_CONTACT_HD int mjhip_isPredefinedPair(const mjhipModel* m, int g1, int g2) {
+  for (int k = 0; k < m->npair; k++) {
+    if ((m->pair_geom1[k] == g1 && m->pair_geom2[k] == g2) ||
+        (m->pair_geom1[k] == g2 && m->pair_geom2[k] == g1)) {
+      return 1;
+    }
+  }
+  return 0;
 }
 
 /* pairs mjCOLLISIONFUNC serves with mjc_Convex (engine_collision_driver.c:41-52) among the
@@ -185,6 +199,7 @@ MJHIP_CONTACT_HD int mjhip_contactCapacity(const mjhipModel* m, int* rows) {
       for (int i = 0; i < m->body_geomnum[b1]; i++) {
         for (int j = 0; j < m->body_geomnum[b2]; j++) {
           int g1 = m->body_geomadr[b1] + i, g2 = m->body_geomadr[b2] + j;
+          if (mjhip_isPredefinedPair(m, g1, g2)) continue;   /* counted below */
           if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
           int k = mjhip_geomPairMaxContacts(m, g1, g2);
           if (k == 0) continue;
@@ -199,6 +214,14 @@ MJHIP_CONTACT_HD int mjhip_contactCapacity(const mjhipModel* m, int* rows) {
         }
       }
     }
+  }
+  for (int k = 0; k < m->npair; k++) {     /* predefined pairs: no bitmask, their own condim */
+    int g1 = m->pair_geom1[k], g2 = m->pair_geom2[k];
+    if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
+    const int kk = mjhip_geomPairMaxContacts(m, g1, g2);
+    if (kk <= 0) continue;
+    ncon += kk;
+    nrow += kk * mjhip_contactRows(m->pair_dim[k], m->opt.cone == mjhipCONE_ELLIPTIC);
   }
   if (rows) *rows = nrow;
   return ncon;

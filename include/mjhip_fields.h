@@ -38,6 +38,7 @@
   XS(nmocap)      \
   XS(ngravcomp)   \
   XS(nexclude)    \
+  XS(npair)       \
   XS(nkey)        \
   XS(ntree)       \
   XS(nsensor)     \
@@ -190,6 +191,16 @@
   X(mjtNum,  actuator_length0,     nu,        1) \
   X(mjtNum,  actuator_acc0,        nu,        1) \
   X(int,     exclude_signature,    nexclude,  1) \
+  X(int,     pair_dim,             npair,     1) \
+  X(int,     pair_geom1,           npair,     1) \
+  X(int,     pair_geom2,           npair,     1) \
+  X(int,     pair_signature,       npair,     1) \
+  X(mjtNum,  pair_solref,          npair,     2) \
+  X(mjtNum,  pair_solreffriction,  npair,     2) \
+  X(mjtNum,  pair_solimp,          npair,     5) \
+  X(mjtNum,  pair_margin,          npair,     1) \
+  X(mjtNum,  pair_gap,             npair,     1) \
+  X(mjtNum,  pair_friction,        npair,     5) \
   X(int,     eq_type,              neq,       1) \
   X(int,     eq_obj1id,            neq,       1) \
   X(int,     eq_obj2id,            neq,       1) \

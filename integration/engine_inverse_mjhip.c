@@ -47,7 +47,6 @@ void* mj_arenaAllocByte(mjData* d, size_t bytes, size_t alignment);
 
 /* features outside the device subset that mjhipModel cannot show; NULL when supported */
 static const char* adapter_unsupported(const mjModel* m) {
-  if (m->npair) return "explicit contact pairs (<contact><pair>)";
   if (m->nflex) return "flexes";
   if (m->nplugin) return "plugins";
   for (int i = 0; i < m->nu; i++) {

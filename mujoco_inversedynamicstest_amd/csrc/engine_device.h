@@ -209,6 +209,11 @@ MJH_HD int mjh_needConvex(const mjhipModel* m) {
       }
     }
   }
+  for (int k = 0; k < m->npair; k++) {       // predefined pairs: no bitmask filter
+    int t1 = m->geom_type[m->pair_geom1[k]], t2 = m->geom_type[m->pair_geom2[k]];
+    if (t1 > t2) { int t = t1; t1 = t2; t2 = t; }
+    if (mjhip_pairUsesCcd(t1, t2) && mjhip_pairMaxContacts(m, t1, t2) > 0) return 1;
+  }
   return 0;
 }
 // a geom-distance sensor (mj_geomDistance) whose geom pairs include one the native solver
@@ -3471,9 +3476,11 @@ MJH_HD void colConvexHField(const mjhipModel& m, const Lane<S>& d, int g1, int g
 // kernel's first pass: it needs each pair's count to place the contacts in order)
 // bbuf: per-lane room for box-box positions (24 x 3 doubles), or nullptr to use the
 // contact list's free tail at ncon (the capacity holds 24 contacts for every box pair)
+struct ContactParam;
 template <int S, bool WRITE = true, bool BOX = true, bool CONVEX = true>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
-                               double margin, int& ncon, int* status, double* bbuf = nullptr);
+                               double margin, const ContactParam& cp, int& ncon, int* status,
+                               double* bbuf = nullptr);
 
 // the narrowphase of a type-ordered primitive pair past the filters (mj_collideGeoms' call of
 // mjCOLLISIONFUNC, engine_collision_driver.c:1500-1510): its raw contacts (<= 2) in raw. The
@@ -3510,20 +3517,22 @@ MJH_HD int narrowPrimitive(int t1, int t2, double margin, P pos1, M mat1, const 
 // (<= 2, with the pair's margin), 0 for none, or -1 for plane : box / cylinder, whose contacts
 // collidePlaneBoxCyl stores as it makes them. CONVEX = false (the cooperative kernel, which
 // no model with a convex pair launches) compiles the GJK/EPA path out.
+// A predefined pair (ipair >= 0, its geoms in g1, g2) skips the bitmask filter and takes the
+// pair's margin (mj_collideGeoms :1445-1492).
 template <int S, bool CONVEX = true>
 MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
-                       double& margin, RawContact raw[2], int* status) {
+                       double& margin, RawContact raw[2], int* status, int ipair = -1) {
   if (m.geom_type[g1] > m.geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
   int t1 = m.geom_type[g1], t2 = m.geom_type[g2];
   const int kmax = mjhip_pairMaxContacts(&m, t1, t2);
   if (kmax == 0) return 0;
-  if (mjhip_filterBitmask(m.geom_contype[g1], m.geom_conaffinity[g1], m.geom_contype[g2],
-                          m.geom_conaffinity[g2])) {
+  if (ipair < 0 && mjhip_filterBitmask(m.geom_contype[g1], m.geom_conaffinity[g1],
+                                       m.geom_contype[g2], m.geom_conaffinity[g2])) {
     return 0;
   }
   const int ovr = (m.opt.enableflags & mjhipENBL_OVERRIDE) != 0;
-  margin = ovr ? m.opt.o_margin : (m.geom_margin[g1] > m.geom_margin[g2] ?
-                                   m.geom_margin[g1] : m.geom_margin[g2]);
+  margin = ovr ? m.opt.o_margin : ipair >= 0 ? m.pair_margin[ipair] :
+           (m.geom_margin[g1] > m.geom_margin[g2] ? m.geom_margin[g1] : m.geom_margin[g2]);
   if (filterSphere(m, d, g1, g2, margin)) return 0;
   if (kmax < 0) {                       // the reference would run a function not built here
     *status |= MJHIP_INST_UNSUPPORTED;
@@ -3552,7 +3561,29 @@ MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
 struct ContactParam {
   int condim;
   double gap, solref[2], solimp[5], friction[5];
+  double solreffriction[2];            // a predefined pair's, else 0 (mj_collideGeoms :1443)
 };
+
+// the contact parameters of geoms g1, g2: a predefined pair's own (mj_collideGeoms
+// :1597-1609: solreffriction only when one of its two values is nonzero), else
+// mj_contactParam's mix of the two geoms'
+MJH_HD void pairParam(const mjhipModel& m, int g1, int g2, int ipair, ContactParam& cp) {
+  cp.solreffriction[0] = cp.solreffriction[1] = 0;
+  if (ipair < 0) {
+    contactParam(m, g1, g2, &cp.condim, &cp.gap, cp.solref, cp.solimp, cp.friction);
+    return;
+  }
+  cp.condim = m.pair_dim[ipair];
+  cp.gap = m.pair_gap[ipair];
+  for (int i = 0; i < 2; i++) cp.solref[i] = m.pair_solref[2*ipair + i];
+  for (int i = 0; i < 5; i++) cp.solimp[i] = m.pair_solimp[5*ipair + i];
+  for (int i = 0; i < 5; i++) cp.friction[i] = m.pair_friction[5*ipair + i];
+  const double* sf = m.pair_solreffriction + 2*ipair;
+  if (sf[0] || sf[1]) {
+    cp.solreffriction[0] = sf[0];
+    cp.solreffriction[1] = sf[1];
+  }
+}
 
 // mj_setContact (:1387-1415) for a primitive pair's raw contacts at contact index ncon on,
 // with the pair's parameters
@@ -3578,7 +3609,9 @@ MJH_HD void storeContacts(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
     double includemargin = margin - cp.gap;
     d.con_includemargin[i] = includemargin;
     for (int j = 0; j < 2; j++) d.con_solref[2*i+j] = ovr ? m.opt.o_solref[j] : cp.solref[j];
-    for (int j = 0; j < 2; j++) d.con_solreffriction[2*i+j] = ovr ? m.opt.o_solref[j] : 0.0;
+    for (int j = 0; j < 2; j++) {
+      d.con_solreffriction[2*i+j] = ovr ? m.opt.o_solref[j] : cp.solreffriction[j];
+    }
     for (int j = 0; j < 5; j++) d.con_solimp[5*i+j] = ovr ? m.opt.o_solimp[j] : cp.solimp[j];
     for (int j = 0; j < 5; j++) {
       double f = ovr ? m.opt.o_friction[j] : cp.friction[j];
@@ -3595,40 +3628,33 @@ MJH_HD void storeContacts(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
   if (store(raw[0]) && num > 1) store(raw[1]);   // num <= 2; constant indices keep raw[]
 }                                                // in registers
 
-// storeContacts with the pair's parameters from the model
-template <int S>
-MJH_HD void setContacts(const mjhipModel& m, const Lane<S>& d, int g1, int g2, double margin,
-                        const RawContact raw[2], int num, int& ncon, int* status) {
-  ContactParam cp;
-  contactParam(m, g1, g2, &cp.condim, &cp.gap, cp.solref, cp.solimp, cp.friction);
-  storeContacts(m, d, g1, g2, margin, cp, raw, num, ncon, status);
-}
-
-// mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415)
+// mj_collideGeoms (engine_collision_driver.c:1440-1620) + mj_setContact (:1387-1415) of
+// geoms g1, g2, or of predefined pair ipair (g1, g2 then its geoms)
 // WRITE = false only counts the contacts the pair produces
 template <int S, bool WRITE = true>
 MJH_HD void collideGeoms(const mjhipModel& m, const Lane<S>& d, int g1, int g2, int& ncon,
-                         int* status) {
+                         int* status, int ipair = -1) {
   double margin = 0;
   RawContact raw[2];
-  const int num = narrowGeoms(m, d, g1, g2, margin, raw, status);
-  if (num < 0) {
-    collidePlaneBoxCyl<S, WRITE>(m, d, g1, g2, margin, ncon, status);
-    return;
-  }
+  const int num = narrowGeoms(m, d, g1, g2, margin, raw, status, ipair);
   if (!num) return;
-  if constexpr (!WRITE) {
+  if (num > 0 && !WRITE) {
     ncon += num;
     return;
   }
-  setContacts(m, d, g1, g2, margin, raw, num, ncon, status);
+  ContactParam cp;
+  pairParam(m, g1, g2, ipair, cp);
+  if (num < 0) {
+    collidePlaneBoxCyl<S, WRITE>(m, d, g1, g2, margin, cp, ncon, status);
+    return;
+  }
+  if constexpr (WRITE) storeContacts(m, d, g1, g2, margin, cp, raw, num, ncon, status);
 }
 
 // mj_setContact (:1387-1415) of one raw contact at index ncon; false when the list is full
 template <int S, bool WRITE>
 MJH_HD bool putContact(const mjhipModel& m, const Lane<S>& d, int g1, int g2, double margin,
-                       int condim, double gap, const double solref[2], const double solimp[5],
-                       const double friction[5], const RawContact& rk, int& ncon, int* status) {
+                       const ContactParam& cp, const RawContact& rk, int& ncon, int* status) {
   if constexpr (!WRITE) {
     ncon++;
     return true;
@@ -3645,14 +3671,16 @@ MJH_HD bool putContact(const mjhipModel& m, const Lane<S>& d, int g1, int g2, do
   copy3(d.con_pos + 3*i, rk.pos);
   d.con_geom[2*i] = g1;
   d.con_geom[2*i+1] = g2;
-  d.con_dim[i] = condim;
-  double includemargin = margin - gap;
+  d.con_dim[i] = cp.condim;
+  double includemargin = margin - cp.gap;
   d.con_includemargin[i] = includemargin;
-  for (int j = 0; j < 2; j++) d.con_solref[2*i+j] = ovr ? m.opt.o_solref[j] : solref[j];
-  for (int j = 0; j < 2; j++) d.con_solreffriction[2*i+j] = ovr ? m.opt.o_solref[j] : 0.0;
-  for (int j = 0; j < 5; j++) d.con_solimp[5*i+j] = ovr ? m.opt.o_solimp[j] : solimp[j];
+  for (int j = 0; j < 2; j++) d.con_solref[2*i+j] = ovr ? m.opt.o_solref[j] : cp.solref[j];
+  for (int j = 0; j < 2; j++) {
+    d.con_solreffriction[2*i+j] = ovr ? m.opt.o_solref[j] : cp.solreffriction[j];
+  }
+  for (int j = 0; j < 5; j++) d.con_solimp[5*i+j] = ovr ? m.opt.o_solimp[j] : cp.solimp[j];
   for (int j = 0; j < 5; j++) {
-    double f = ovr ? m.opt.o_friction[j] : friction[j];
+    double f = ovr ? m.opt.o_friction[j] : cp.friction[j];
     d.con_friction[5*i+j] = f > 1e-5 ? f : 1e-5;      // mjMINMU
   }
   d.con_exclude[i] = rk.dist >= includemargin;
@@ -3667,10 +3695,8 @@ MJH_HD bool putContact(const mjhipModel& m, const Lane<S>& d, int g1, int g2, do
 // box : box (up to 24 raw contacts)
 template <int S, bool WRITE>
 MJH_HD void collideBoxBox(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
-                          double margin, int& ncon, int* status, double* bbuf) {
-  int condim;
-  double gap, solref[2], solimp[5], friction[5];
-  contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
+                          double margin, const ContactParam& cp, int& ncon, int* status,
+                          double* bbuf) {
   double p1[3], m1[9], p2[3], m2[9];
   for (int k = 0; k < 3; k++) { p1[k] = d.gxpos[3*g1 + k]; p2[k] = d.gxpos[3*g2 + k]; }
   for (int k = 0; k < 9; k++) { m1[k] = d.geom_xmat[9*g1 + k]; m2[k] = d.geom_xmat[9*g2 + k]; }
@@ -3688,8 +3714,7 @@ MJH_HD void collideBoxBox(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
   bool ok = true;
   boxBoxEmit(margin, p1, m1, size1, p2, m2, size2, keep,
              [&](const RawContact& rk) MJH_LAMBDA_INLINE {
-    if (ok) ok = putContact<S, WRITE>(m, d, g1, g2, margin, condim, gap, solref, solimp,
-                                      friction, rk, ncon, status);
+    if (ok) ok = putContact<S, WRITE>(m, d, g1, g2, margin, cp, rk, ncon, status);
   });
 }
 
@@ -3700,20 +3725,17 @@ MJH_HD void collideBoxBox(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
 // height-field paths out (the cooperative kernel, which no such model launches)
 template <int S, bool WRITE, bool BOX, bool CONVEX>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
-                               double margin, int& ncon, int* status, double* bbuf) {
+                               double margin, const ContactParam& cp, int& ncon, int* status,
+                               double* bbuf) {
   if (m.geom_type[g1] == mjhipGEOM_BOX) {
-    if constexpr (BOX) collideBoxBox<S, WRITE>(m, d, g1, g2, margin, ncon, status, bbuf);
+    if constexpr (BOX) collideBoxBox<S, WRITE>(m, d, g1, g2, margin, cp, ncon, status, bbuf);
     else *status |= MJHIP_INST_UNSUPPORTED;   // not reached: the launch saw no box pair
     return;
   }
   if (m.geom_type[g1] == mjhipGEOM_HFIELD || m.geom_type[g2] == mjhipGEOM_MESH) {
     if constexpr (CONVEX) {
-      int condim;
-      double gap, solref[2], solimp[5], friction[5];
-      contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
       auto store = [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
-        return putContact<S, WRITE>(m, d, g1, g2, margin, condim, gap, solref, solimp,
-                                    friction, rk, ncon, status);
+        return putContact<S, WRITE>(m, d, g1, g2, margin, cp, rk, ncon, status);
       };
       if (m.geom_type[g1] == mjhipGEOM_HFIELD) {
         colConvexHField(m, d, g1, g2, margin, status, store);
@@ -3728,12 +3750,8 @@ MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, in
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
   SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
   const double* size2 = m.geom_size + 3*g2;
-  int condim;
-  double gap, solref[2], solimp[5], friction[5];
-  contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
   auto store = [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
-    return putContact<S, WRITE>(m, d, g1, g2, margin, condim, gap, solref, solimp, friction,
-                                rk, ncon, status);
+    return putContact<S, WRITE>(m, d, g1, g2, margin, cp, rk, ncon, status);
   };
   if (m.geom_type[g2] == mjhipGEOM_BOX) {
     colPlaneBox(margin, pos1, mat1, pos2, mat2, size2, store);
@@ -3841,7 +3859,11 @@ MJH_HD void swapContacts(const Lane<S>& d, int a, int b) {
 
 // mj_collision (engine_collision_driver.c:265-497): candidate body pairs in signature order,
 // geoms all-to-all; a midphase pair (a body with more than one geom) has its contacts stably
-// sorted by contactcompare, as mj_collideTree's callers do
+// sorted by contactcompare, as mj_collideTree's callers do. The predefined pairs (sorted by
+// signature) merge in ahead of the first body pair whose signature is not below theirs
+// (:316-327; the broadphase pairs in between that are not candidates add no contacts), the
+// rest after the sweep (:432-437), and a candidate's geom pair that is also a predefined pair
+// is left to it (mj_collideGeomPair :499-523).
 template <int S>
 MJH_HD void collision(const mjhipModel& m, const Lane<S>& d, int* status) {
   int ncon = 0;                        // in a register; written once at the end
@@ -3859,22 +3881,46 @@ MJH_HD void collision(const mjhipModel& m, const Lane<S>& d, int* status) {
       }
     }
   }
-  for (int b1 = 0; b1 < m.nbody; b1++) {
-    for (int b2 = b1 + 1; b2 < m.nbody; b2++) {
-      if (!mjhip_bodyPairCandidate(&m, b1, b2)) continue;
-      int n1 = m.body_geomnum[b1], n2 = m.body_geomnum[b2];
-      int before = ncon;
-      for (int i = 0; i < n1; i++) {
-        for (int j = 0; j < n2; j++) {
-          collideGeoms(m, d, m.body_geomadr[b1] + i, m.body_geomadr[b2] + j, ncon, status);
-        }
+  // one loop over the body pairs in signature order and a final step for the predefined pairs
+  // left after the sweep, with a single narrowphase call site (each one is inlined whole)
+  const int nb = m.nbody;
+  const long npb = (long)nb*(nb - 1)/2;
+  const bool midphase = !(m.opt.disableflags & mjhipDSBL_MIDPHASE);
+  int pairadr = 0, b1 = 0, b2 = 1;
+  for (long pb = 0; pb <= npb; pb++) {
+    const bool end = pb == npb;
+    const int sig = (b1 << 16) + b2;
+    int pend = pairadr;                  // predefined pairs merged ahead of this body pair
+    while (pend < m.npair && (end || m.pair_signature[pend] <= sig)) pend++;
+    const int npre = pend - pairadr;
+    const bool cand = !end && mjhip_bodyPairCandidate(&m, b1, b2);
+    const int n1 = cand ? m.body_geomnum[b1] : 0, n2 = cand ? m.body_geomnum[b2] : 0;
+    int before = ncon;
+    for (int t = 0; t < npre + n1*n2; t++) {
+      int g1, g2, ip = -1;
+      if (t < npre) {
+        ip = pairadr + t;
+        g1 = m.pair_geom1[ip];
+        g2 = m.pair_geom2[ip];
+      } else {
+        if (t == npre) before = ncon;    // the swept contacts start here
+        const int k = t - npre;
+        g1 = m.body_geomadr[b1] + k / n2;
+        g2 = m.body_geomadr[b2] + k % n2;
+        if (m.npair && mjhip_isPredefinedPair(&m, g1, g2)) continue;
       }
-      if (!(m.opt.disableflags & mjhipDSBL_MIDPHASE) && !(n1 == 1 && n2 == 1)) {
-        int n = ncon;
-        for (int a = before + 1; a < n; a++) {
-          for (int b = a; b > before && contactLess(m, d, b, b - 1); b--) swapContacts(d, b, b - 1);
-        }
+      collideGeoms(m, d, g1, g2, ncon, status, ip);
+    }
+    pairadr = pend;
+    if (cand && midphase && !(n1 == 1 && n2 == 1)) {
+      int n = ncon;
+      for (int a = before + 1; a < n; a++) {
+        for (int b = a; b > before && contactLess(m, d, b, b - 1); b--) swapContacts(d, b, b - 1);
       }
+    }
+    if (++b2 >= nb) {
+      b1++;
+      b2 = b1 + 1;
     }
   }
   d.con_count[0] = ncon;

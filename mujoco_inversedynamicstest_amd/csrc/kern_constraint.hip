@@ -185,7 +185,8 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
                     (P.t2 == mjhipGEOM_BOX || P.t2 == mjhipGEOM_CYLINDER)) ||
                    (P.t1 == mjhipGEOM_BOX && P.t2 == mjhipGEOM_BOX)) {
           num = -1;                         // plane : box / cylinder, box : box: counts, then stores
-          mjh::collidePlaneBoxCyl<64, false, BOX, false>(m, d, g1, g2, margin, cnt, &st, bbuf);
+          mjh::collidePlaneBoxCyl<64, false, BOX, false>(m, d, g1, g2, margin, cp, cnt, &st,
+                                                         bbuf);
         } else {
           num = mjh::narrowPrimitive(P.t1, P.t2, margin, (const double*)(gx + 3*g1),
                                      (const double*)(gm + 9*g1), gsize + 3*g1,
@@ -199,7 +200,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       if (cnt) {
         int c = ncon + excl;
         if (num < 0) {
-          mjh::collidePlaneBoxCyl<64, true, BOX, false>(m, d, g1, g2, margin, c, &st, bbuf);
+          mjh::collidePlaneBoxCyl<64, true, BOX, false>(m, d, g1, g2, margin, cp, c, &st, bbuf);
         } else {
           mjh::storeContacts<64>(m, d, g1, g2, margin, cp, raw, num, c, &st);
         }

@@ -433,9 +433,20 @@ struct mjhipContext_ {
 // pairs stably sorted by contactcompare's key (:227-257), the type-ordered geom ids. Every
 // contact of a pair carries that key, so this is the order the serial collision() leaves
 // its contacts in, and the cooperative kernel concatenates the pairs' contacts in it.
-static std::vector<int2> collision_pairs(const mjhipModel* m) {
-  std::vector<int2> out;
+// Predefined pairs (z = the pair's index, else -1) merge in as the device collision() does:
+// ahead of the first body pair whose signature is not below theirs, the rest at the end, and
+// a candidate's geom pair that is a predefined pair is left to it.
+static std::vector<int3> collision_pairs(const mjhipModel* m) {
+  std::vector<int3> out;
   if (!mjhip_contactsEnabled(m)) return out;
+  int pairadr = 0;
+  auto predefined = [&](int k) {
+    const int g1 = m->pair_geom1[k], g2 = m->pair_geom2[k];
+    const bool flip = m->geom_type[g1] > m->geom_type[g2];
+    if (mjhip_pairMaxContacts(m, m->geom_type[flip ? g2 : g1], m->geom_type[flip ? g1 : g2])) {
+      out.push_back(make_int3(g1, g2, k));
+    }
+  };
   const bool midphase = !(m->opt.disableflags & mjhipDSBL_MIDPHASE);
   auto key = [&](int2 p) {
     return m->geom_type[p.x] > m->geom_type[p.y] ? std::make_pair(p.y, p.x)
@@ -443,12 +454,16 @@ static std::vector<int2> collision_pairs(const mjhipModel* m) {
   };
   for (int b1 = 0; b1 < m->nbody; b1++) {
     for (int b2 = b1 + 1; b2 < m->nbody; b2++) {
+      for (; pairadr < m->npair && m->pair_signature[pairadr] <= (b1 << 16) + b2; pairadr++) {
+        predefined(pairadr);
+      }
       if (!mjhip_bodyPairCandidate(m, b1, b2)) continue;
       const int n1 = m->body_geomnum[b1], n2 = m->body_geomnum[b2];
       std::vector<int2> list;
       for (int i = 0; i < n1; i++) {
         for (int j = 0; j < n2; j++) {
           const int g1 = m->body_geomadr[b1] + i, g2 = m->body_geomadr[b2] + j;
+          if (m->npair && mjhip_isPredefinedPair(m, g1, g2)) continue;
           const std::pair<int, int> k = key(make_int2(g1, g2));
           if (!mjhip_pairMaxContacts(m, m->geom_type[k.first], m->geom_type[k.second])) continue;
           if (mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
@@ -462,18 +477,19 @@ static std::vector<int2> collision_pairs(const mjhipModel* m) {
         std::stable_sort(list.begin(), list.end(),
                          [&](int2 a, int2 b) { return key(a) < key(b); });
       }
-      out.insert(out.end(), list.begin(), list.end());
+      for (const int2& p : list) out.push_back(make_int3(p.x, p.y, -1));
     }
   }
+  for (; pairadr < m->npair; pairadr++) predefined(pairadr);
   return out;
 }
 
 // the cooperative kernel's program for collision_pairs' pairs: what mj_collideGeoms derives
 // from the model alone, type-ordered as narrowGeoms does (engine_collision_driver.c:1440-1497)
-static std::vector<CoopPair> coop_program(const mjhipModel* m, const std::vector<int2>& pairs) {
+static std::vector<CoopPair> coop_program(const mjhipModel* m, const std::vector<int3>& pairs) {
   std::vector<CoopPair> out;
   const bool ovr = (m->opt.enableflags & mjhipENBL_OVERRIDE) != 0;
-  for (const int2& pr : pairs) {
+  for (const int3& pr : pairs) {
     CoopPair P{};
     P.g1 = pr.x;
     P.g2 = pr.y;
@@ -486,7 +502,7 @@ static std::vector<CoopPair> coop_program(const mjhipModel* m, const std::vector
     P.rt1 = m->body_rootid[P.b1];
     P.rt2 = m->body_rootid[P.b2];
     const double mg1 = m->geom_margin[P.g1], mg2 = m->geom_margin[P.g2];
-    P.margin = ovr ? m->opt.o_margin : (mg1 > mg2 ? mg1 : mg2);
+    P.margin = ovr ? m->opt.o_margin : pr.z >= 0 ? m->pair_margin[pr.z] : (mg1 > mg2 ? mg1 : mg2);
     const double rb1 = m->geom_rbound[P.g1], rb2 = m->geom_rbound[P.g2];
     if (rb1 > 0 && rb2 > 0) {
       P.filt = 0;
@@ -805,9 +821,9 @@ MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int cap
   // k_constraint)
   if (const char* lanes = getenv("MJHIP_COOP_LANES")) c->coop = atoi(lanes) == 0 ? 0 : 16;
   if (c->con_cap > 0) {
-    std::vector<int2> pairs = collision_pairs(m);
+    std::vector<int3> pairs = collision_pairs(m);
     c->npair = (int)pairs.size();
-    for (const int2& pr : pairs) {
+    for (const int3& pr : pairs) {
       c->boxpair |= m->geom_type[pr.x] == mjhipGEOM_BOX && m->geom_type[pr.y] == mjhipGEOM_BOX;
     }
     if (c->npair) {
@@ -816,9 +832,7 @@ MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int cap
       // function (host arithmetic, as the reference's)
       std::vector<mjh::ContactParam> cps(prog.size());
       for (size_t i = 0; i < prog.size(); i++) {
-        mjh::ContactParam& q = cps[i];
-        mjh::contactParam(*m, prog[i].g1, prog[i].g2, &q.condim, &q.gap, q.solref, q.solimp,
-                          q.friction);
+        mjh::pairParam(*m, prog[i].g1, prog[i].g2, pairs[i].z, cps[i]);
       }
       if (hipMalloc((void**)&c->pairs, sizeof(CoopPair) * prog.size()) != hipSuccess ||
           hipMemcpy(c->pairs, prog.data(), sizeof(CoopPair) * prog.size(),

@@ -443,8 +443,6 @@ def _names(ints, arrays):
 def unsupported(ints, arrays) -> str | None:
   """Features outside the device subset that the compiled-model arrays cannot express
   (the adapter's adapter_unsupported list plus the loader's subset)."""
-  if ints["npair"]:
-    return "explicit contact pairs (<contact><pair>)"
   if ints["nflex"]:
     return "flexes"
   if ints["nplugin"]:

@@ -595,9 +595,58 @@ class MJCFCompiler:
     self.hfields = {}                   # name -> meshes.HField (<asset><hfield>)
     self.equalities = []
     self.excludes = []
+    self.pairs = []                     # <contact><pair> attribute dicts (class defaults applied)
     self.keys = []
     self.models = {}                    # name -> MJCFCompiler (<asset><model>, parsed only)
     self.basedir = None
+
+  def _compile_pairs(self, arr, s, geoms):
+    """Predefined geom pairs: mjs_defaultPair (user_init.c:298-307) under the class defaults
+    and the element's attributes (mjXReader::OnePair, xml_native_reader.cc:1866-1893; partial
+    vectors keep the remaining defaults), the geoms swapped so that body1 <= body2 and the
+    body signature (mjCPair::ResolveReferences, user_objects.cc:4777-4817), condim checked
+    (mjCPair::Compile :4822-4828), then stably sorted by signature (user_model.cc:4321-4324)
+    and written as in mjCModel::CopyObjects (:3153-3164). The pair's values are always
+    defined in this version, so Compile's fall-backs to the geoms' parameters never apply."""
+    gid = {g["name"]: i for i, g in enumerate(geoms) if g.get("name")}
+    recs = []
+    for a in self.pairs:
+      vals = {"condim": 3, "solref": [0.02, 1.0], "solreffriction": [0.0, 0.0],
+              "solimp": [0.9, 0.95, 0.001, 0.5, 2.0], "margin": [0.0], "gap": [0.0],
+              "friction": [1.0, 1.0, 0.005, 0.0001, 0.0001]}
+      for k in ("solref", "solreffriction", "solimp", "margin", "gap", "friction"):
+        if k in a:
+          v = _floats(a[k])
+          if len(v) > len(vals[k]):
+            raise MJCFError(f"pair attribute '{k}' has too many values")
+          vals[k][:len(v)] = v
+      if "condim" in a:
+        vals["condim"] = int(a["condim"])
+      if vals["condim"] not in (1, 3, 4, 6):
+        raise MJCFError("invalid condim in contact pair")
+      n1, n2 = a.get("geom1"), a.get("geom2")
+      for n in (n1, n2):
+        if n not in gid:
+          raise MJCFError(f"geom '{n}' not found in collision")
+      g1, g2 = gid[n1], gid[n2]
+      if geoms[g1]["body"] > geoms[g2]["body"]:
+        g1, g2 = g2, g1
+      recs.append(((geoms[g1]["body"] << 16) + geoms[g2]["body"], g1, g2, vals))
+    recs.sort(key=lambda r: r[0])            # list.sort is stable
+    npair = len(recs)
+    pdim, pg1, pg2, psig = (arr("pair_" + k, npair, np.int32)
+                            for k in ("dim", "geom1", "geom2", "signature"))
+    psolref = arr("pair_solref", (npair, 2), np.float64)
+    psolreffriction = arr("pair_solreffriction", (npair, 2), np.float64)
+    psolimp = arr("pair_solimp", (npair, 5), np.float64)
+    pmargin = arr("pair_margin", npair, np.float64)
+    pgap = arr("pair_gap", npair, np.float64)
+    pfriction = arr("pair_friction", (npair, 5), np.float64)
+    for i, (sig, g1, g2, v) in enumerate(recs):
+      pdim[i], pg1[i], pg2[i], psig[i] = v["condim"], g1, g2, sig
+      psolref[i], psolreffriction[i], psolimp[i] = v["solref"], v["solreffriction"], v["solimp"]
+      pmargin[i], pgap[i], pfriction[i] = v["margin"][0], v["gap"][0], v["friction"]
+    s.update(npair=npair)
 
   # ---------------------------------------------------------------- parsing
   def _parse_defaults(self, el, parent):
@@ -757,6 +806,10 @@ class MJCFCompiler:
                           for k, v in a.items()}
     lists = [list(src.excludes), list(src.tendons), list(src.equalities),
              list(src.actuators), list(src.sensors)]
+    for a in list(src.pairs):            # CopyList(pairs_) precedes the excludes (:427)
+      a = ns(a, ("name", "geom1", "geom2"))
+      if a.get("geom1") in names["geom"] and a.get("geom2") in names["geom"]:
+        self.pairs.append(a)
     for b1, b2 in lists[0]:
       if p(b1) in names["body"] and p(b2) in names["body"]:
         self.excludes.append((p(b1), p(b2)))
@@ -886,6 +939,8 @@ class MJCFCompiler:
         for ch in el:
           if ch.tag == "exclude":
             self.excludes.append((ch.get("body1"), ch.get("body2")))
+          elif ch.tag == "pair":           # mjXReader::OnePair (xml_native_reader.cc:1866)
+            self.pairs.append(self._elem_attrs(ch, "pair", None))
           else:
             raise MJCFError(f"unsupported contact element <{ch.tag}>")
       elif t == "keyframe":
@@ -2175,12 +2230,16 @@ class MJCFCompiler:
       sreft[si_], sref[si_], sdim[si_], sadr[si_], scut[si_] = rt, rid, dim, sensadr, cut
       sensadr += dim
     s.update(nsensor=ns_, nsensordata=sensadr)
-    # exclude pairs: signature = (body1 << 16) + body2 with body1 < body2
+    # exclude pairs: signature = (body1 << 16) + body2 with body1 < body2, stably sorted by
+    # signature (user_model.cc:4321-4324)
     nex = len(self.excludes)
     exs = arr("exclude_signature", nex, np.int32)
-    for ei, (b1, b2) in enumerate(self.excludes):
+    sigs = []
+    for b1, b2 in self.excludes:
       i1, i2 = bname[b1], bname[b2]
-      exs[ei] = (min(i1, i2) << 16) + max(i1, i2)
+      sigs.append((min(i1, i2) << 16) + max(i1, i2))
+    exs[:] = sorted(sigs)
+    self._compile_pairs(arr, s, geoms)
     # keyframes
     nkey = len(self.keys)
     kq = arr("key_qpos", (nkey, nq), np.float64)

@@ -4607,6 +4607,18 @@ static int or_contactsEnabled(const mjhipModel* m) {
   return !mjDISABLED(mjhipDSBL_CONSTRAINT) && !mjDISABLED(mjhipDSBL_CONTACT) && m->nbody >= 2;
 }
 
+/* mj_collideGeomPair's merged test (:499-523): geoms g1, g2 (either order) form one of the
+ * predefined pairs [startadr, pairadr) merged for this body pair */
+static int or_mergedPair(const mjhipModel* m, int g1, int g2, int startadr, int pairadr) {
+  for (int k = startadr; k < pairadr; k++) {
+    if ((m->pair_geom1[k] == g1 && m->pair_geom2[k] == g2) ||
+        (m->pair_geom1[k] == g2 && m->pair_geom2[k] == g1)) {
+      return 1;
+    }
+  }
+  return 0;
+}
+
 /* condim of a geom pair as mj_contactParam (:1289-1384) resolves it */
 static int or_pairCondim(const mjhipModel* m, int g1, int g2) {
   int p1 = m->geom_priority[g1], p2 = m->geom_priority[g2];
@@ -4635,6 +4647,7 @@ static void or_contactBounds(const mjhipModel* m, int* ncon, int* nrow) {
       if (excluded) continue;
       for (int g1 = m->body_geomadr[b1]; g1 < m->body_geomadr[b1] + m->body_geomnum[b1]; g1++) {
         for (int g2 = m->body_geomadr[b2]; g2 < m->body_geomadr[b2] + m->body_geomnum[b2]; g2++) {
+          if (or_mergedPair(m, g1, g2, 0, m->npair)) continue;   /* counted below */
           const int flip = m->geom_type[g1] > m->geom_type[g2];
           int k = or_pairMaxContacts(m, flip ? g2 : g1, flip ? g1 : g2);
           if (k > 0 && !or_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
@@ -4645,6 +4658,16 @@ static void or_contactBounds(const mjhipModel* m, int* ncon, int* nrow) {
           }
         }
       }
+    }
+  }
+  for (int p = 0; p < m->npair; p++) {      /* predefined pairs: no bitmask, their condim */
+    const int a = m->pair_geom1[p], b = m->pair_geom2[p];
+    const int flip = m->geom_type[a] > m->geom_type[b];
+    const int k = or_pairMaxContacts(m, flip ? b : a, flip ? a : b);
+    if (k > 0) {
+      const int condim = m->pair_dim[p];
+      *ncon += k;
+      *nrow += k * (condim == 1 ? 1 : (ell ? condim : 2*(condim - 1)));
     }
   }
 }
@@ -4720,18 +4743,23 @@ static int or_narrow(const mjhipModel* m, const mjhipData* d, int g1, int g2, mj
   return num;
 }
 
-/* mj_collideGeoms (dynamic filters, narrowphase, mj_setContact) for geoms of two bodies */
-static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, int g1, int g2) {
+/* mj_collideGeoms (engine_collision_driver.c:1440-1632: dynamic filters, narrowphase,
+ * mj_setContact) for geoms of two bodies (ipair = -1), or for predefined pair ipair (g1, g2
+ * its geoms): no bitmask filter, the pair's margin (mj_assignMargin), condim, gap, solref,
+ * solimp, friction, and its solreffriction when either value is nonzero (:1597-1609) */
+static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, int g1, int g2,
+                            int ipair) {
   if (m->geom_type[g1] > m->geom_type[g2]) { int t = g1; g1 = g2; g2 = t; }
   int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
   const int kmax = or_collisionFunc(m, t1, t2);
   if (kmax == 0) return;
-  if (or_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1], m->geom_contype[g2],
-                       m->geom_conaffinity[g2])) {
+  if (ipair < 0 && or_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
+                                    m->geom_contype[g2], m->geom_conaffinity[g2])) {
     return;
   }
-  mjtNum margin = mjENABLED(mjhipENBL_OVERRIDE) ? m->opt.o_margin
-                                                : mjMAX(m->geom_margin[g1], m->geom_margin[g2]);
+  mjtNum margin = mjENABLED(mjhipENBL_OVERRIDE) ? m->opt.o_margin :
+                  ipair >= 0 ? m->pair_margin[ipair] :
+                  mjMAX(m->geom_margin[g1], m->geom_margin[g2]);
   if (or_filterSphere(m, d, g1, g2, margin)) return;
   if (kmax < 0) {              /* a collision function outside the subset would run: flag */
     ((mjhipData*)d)->status |= MJHIP_INST_UNSUPPORTED;
@@ -4742,7 +4770,18 @@ static void or_collideGeoms(const mjhipModel* m, const mjhipData* d, orEfc* e, i
   if (!num) return;
   int condim;
   mjtNum gap, solref[2], solimp[5], friction[5], solreffriction[2] = {0, 0};
-  or_contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
+  if (ipair < 0) {
+    or_contactParam(m, g1, g2, &condim, &gap, solref, solimp, friction);
+  } else {
+    condim = m->pair_dim[ipair];
+    gap = m->pair_gap[ipair];
+    mju_copy(solref, m->pair_solref + 2*ipair, 2);
+    mju_copy(solimp, m->pair_solimp + 5*ipair, 5);
+    mju_copy(friction, m->pair_friction + 5*ipair, 5);
+    if (m->pair_solreffriction[2*ipair] || m->pair_solreffriction[2*ipair + 1]) {
+      mju_copy(solreffriction, m->pair_solreffriction + 2*ipair, 2);
+    }
+  }
   for (int k = 0; k < num; k++) {
     int i = e->ncon;
     if (i >= e->con_capacity) return;   /* cannot happen: capacity is exact */
@@ -4840,10 +4879,13 @@ static void or_swapContacts(orEfc* e, int a, int b) {
 }
 
 /* mj_collision (engine_collision_driver.c:265-497): the broadphase's body pairs in signature
- * order (repeats skipped), the body bitmask and exclude filters, then a single-geom pair, the
- * midphase (mj_collideTree, whose contacts are stably sorted by contactcompare) or all-to-all.
- * The midphase's bounding-volume tests are inflated by the margins, so visiting the pair's
- * geoms all-to-all yields the same contacts before the sort. */
+ * order (repeats skipped); ahead of each, the predefined pairs whose signature is not above
+ * its own (:316-327, before the filters); then the body bitmask and exclude filters, then a
+ * single-geom pair, the midphase (mj_collideTree, whose contacts are stably sorted by
+ * contactcompare) or all-to-all, skipping the geom pairs merged as predefined pairs; the
+ * predefined pairs left after the sweep last (:432-437). The midphase's bounding-volume tests
+ * are inflated by the margins, so visiting the pair's geoms all-to-all yields the same
+ * contacts before the sort. */
 static void or_collision(const mjhipModel* m, const mjhipData* d, orEfc* e) {
   e->ncon = 0;
   if (!or_contactsEnabled(m)) return;
@@ -4851,11 +4893,18 @@ static void or_collision(const mjhipModel* m, const mjhipData* d, orEfc* e) {
   int* pair = (int*)malloc(sizeof(int) * (nb*nb + nb*(nb - 1)/2 + 1));
   int np = or_broadphase(m, d, pair);
   unsigned last_signature = (unsigned)-1;
+  int pairadr = 0;
   for (int i = 0; i < np; i++) {
     int b1 = (pair[i] >> 16) & 0xFFFF, b2 = pair[i] & 0xFFFF;
     unsigned signature = ((unsigned)b1 << 16) + b2;
     if (signature == last_signature) continue;
     last_signature = signature;
+    int merged = 0, startadr = pairadr;
+    while (pairadr < m->npair && (unsigned)m->pair_signature[pairadr] <= signature) {
+      if ((unsigned)m->pair_signature[pairadr] == signature) merged = 1;
+      or_collideGeoms(m, d, e, m->pair_geom1[pairadr], m->pair_geom2[pairadr], pairadr);
+      pairadr++;
+    }
     if (!or_canCollide2(m, b1, b2)) continue;
     int exadr = 0;
     while (exadr < m->nexclude && (unsigned)m->exclude_signature[exadr] < signature) exadr++;
@@ -4864,7 +4913,9 @@ static void or_collision(const mjhipModel* m, const mjhipData* d, orEfc* e) {
     int before = e->ncon;
     for (int a = 0; a < n1; a++) {
       for (int c = 0; c < n2; c++) {
-        or_collideGeoms(m, d, e, m->body_geomadr[b1] + a, m->body_geomadr[b2] + c);
+        const int g1 = m->body_geomadr[b1] + a, g2 = m->body_geomadr[b2] + c;
+        if (merged && or_mergedPair(m, g1, g2, startadr, pairadr)) continue;
+        or_collideGeoms(m, d, e, g1, g2, -1);
       }
     }
     int midphase = !mjDISABLED(mjhipDSBL_MIDPHASE) && !(n1 == 1 && n2 == 1);
@@ -4875,6 +4926,10 @@ static void or_collision(const mjhipModel* m, const mjhipData* d, orEfc* e) {
         }
       }
     }
+  }
+  while (pairadr < m->npair) {
+    or_collideGeoms(m, d, e, m->pair_geom1[pairadr], m->pair_geom2[pairadr], pairadr);
+    pairadr++;
   }
   free(pair);
 }

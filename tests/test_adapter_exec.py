@@ -261,8 +261,7 @@ def test_arena_too_small_for_rows_or_contacts(lib):
 
 def test_refused_models_are_an_error(lib):
   m = models.load("humanoid")
-  for what, msg in (("npair", "explicit contact pairs"), ("nflex", "flexes"),
-                    ("nplugin", "plugins")):
+  for what, msg in (("nflex", "flexes"), ("nplugin", "plugins")):
     A = Adapter(lib, m)
     try:
       lib.hx_set_model_int(A.h, what.encode(), 1)
@@ -354,3 +353,29 @@ def test_sparse_models_compressed_arena(lib):
         assert {n: A.off(n) for _, n, _, _ in tables["SOLVER"]} == layout
     finally:
       A.close()
+
+
+def test_predefined_pairs_through_adapter(lib):
+  """A model with predefined <pair>s (tests/pair_models.py MIXED) through the adapter: the
+  merged contacts, rows and outputs equal the oracle's bit for bit, in the reference's arena
+  layout, over contact-rich states."""
+  import pair_models as P
+  m = P.mixed()
+  tables = _solver_table()
+  q, v, a = P.mixed_states(m, 12, seed=3)
+  A, o = Adapter(lib, m), Oracle(m)
+  ncon = 0
+  try:
+    for i in range(len(q)):
+      A.set_state(q[i], v[i], a[i])
+      assert A.call(0, 0) == (0, "")
+      ref = o.inverse(q[i], v[i], a[i])
+      np.testing.assert_array_equal(A.field("qfrc_inverse"), ref)
+      for f in fields.DATA_FIELDS:
+        np.testing.assert_array_equal(A.field(f.name), getattr(o.d, f.name), err_msg=f.name)
+      _assert_contacts_equal(A, o)
+      _assert_layout(A, m, tables)
+      ncon += o.efc.ncon
+  finally:
+    A.close()
+  assert ncon > 2 * len(q)

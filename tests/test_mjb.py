@@ -119,19 +119,16 @@ def test_unsupported_features_refused(humanoid, field, value, msg):
     mjb.read(b)
 
 
-def test_pairs_refused(humanoid):
-  """npair > 0: the predefined-pair arrays grow, and the model is refused."""
-  buf = bytearray(mjb.write(humanoid))
-  ints = dict(zip(mjb.INTS, struct.unpack_from("<83i", buf, 20)))
-  ints["npair"] = 1
-  off = mjb.offsets(dict(ints, npair=0))
-  grow = mjb.offsets(ints)["__end__"] - off["__end__"]
-  at = off["pair_dim"]
-  new = bytes(buf[:at]) + b"\0" * grow + bytes(buf[at:])
-  new = _patch(new, 20, "<83i", *[ints[k] for k in mjb.INTS])
-  new = _patch(new, 20 + 4 * 83 + 8, "<Q", mjb.buffer_size(ints))
-  with pytest.raises(mjb.MJBError, match="explicit contact pairs"):
-    mjb.read(new)
+def test_pairs_roundtrip():
+  """npair > 0: the predefined-pair arrays go through the .mjb layout and back unchanged
+  (they were refused before this round)."""
+  import pair_models as P
+  m = P.mixed()
+  m2 = mjb.read(mjb.write(m))
+  assert m2.sizes["npair"] == m.sizes["npair"] == 5
+  for f in ("pair_dim", "pair_geom1", "pair_geom2", "pair_signature", "pair_solref",
+            "pair_solreffriction", "pair_solimp", "pair_margin", "pair_gap", "pair_friction"):
+    np.testing.assert_array_equal(getattr(m2, f), getattr(m, f), err_msg=f)
 
 
 @pytest.mark.skipif(not os.path.isdir(REF), reason="reference headers not present")

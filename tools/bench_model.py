@@ -6,6 +6,8 @@ kernels a model selects (bundled or run-time generated, generic).
   python tools/bench_model.py path/to/model.xml [B] [reps]
   python tools/bench_model.py humanoid100 [B] [reps]   # contact states, capped context
   python tools/bench_model.py humanoid_contacts [B]    # config 4's states
+  python tools/bench_model.py humanoid_nocontact [B]   # config 2's model (contacts disabled)
+  SKIP=1|2 python tools/bench_model.py humanoid [B]    # mj_inverseSkip(POS|VEL) after a full call
 """
 import os
 import sys
@@ -23,8 +25,9 @@ def main():
   B = int(sys.argv[2]) if len(sys.argv) > 2 else 65536
   reps = int(sys.argv[3]) if len(sys.argv) > 3 else 20
   contacts = name == "humanoid_contacts"
+  nocontact = name.endswith("_nocontact")   # e.g. humanoid_nocontact: config 2's model
   m = mjcf.load_xml(name) if name.endswith(".xml") else models.load(
-      "humanoid" if contacts else name)
+      "humanoid" if contacts else name.replace("_nocontact", ""), disable_contact=nocontact)
   caps = {}
   if name == "humanoid100":        # ~150 contacts per state (tests/humanoid100_states.py)
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -40,16 +43,19 @@ def main():
   torch.cuda.set_device(0)
   e = engine.InverseEngine(m, capacity=B, **caps)
   e.upload_states(q, v, a)
+  skip = int(os.environ.get("SKIP", "0"))
+  e.inverse(B, mirror_input=True)        # the skipped stages' outputs for SKIP calls
   for _ in range(3):
-    e.inverse(B, mirror_input=True)
+    e.inverse(B, mirror_input=True, skipstage=skip)
   torch.cuda.synchronize()
   t0 = time.perf_counter()
   for _ in range(reps):
-    e.inverse(B, mirror_input=True)
+    e.inverse(B, mirror_input=True, skipstage=skip)
   torch.cuda.synchronize()
   dt = (time.perf_counter() - t0) / reps
-  print(f"{name}: batch {B}, kernel {e.fast_kernel or 'generic'}, {dt*1e3:.3f} ms per call, "
-        f"{B/dt/1e6:.1f}M evals/s")
+  path = {0: "generic", 1: "straight-line", 2: "straight-line skip"}.get(e.last_path)
+  print(f"{name}: batch {B}, skipstage {skip}, kernel {e.fast_kernel or 'generic'} ({path}), "
+        f"{dt*1e3:.3f} ms per call, {B/dt/1e6:.1f}M evals/s")
   if caps:
     _, st = e.inverse(q, v, a, status=True)
     print(f"  instances flagged (status != 0): {int((st != 0).sum())} of {B}")

@@ -6,10 +6,12 @@
 #   smoke     __graft_entry__.smoke()
 #   bench     the default bench line                         -> gpurun_out/bench.json
 #   c4 / c5   config 4 / config 5 bench lines                 -> gpurun_out/c4.json, c5.json
-#   c5trace   config 5 under a rocprofv3 kernel trace + stats -> gpurun_out/prof_c5/
+#   c4trace / c5trace   config 4 / 5 under a rocprofv3 kernel trace + stats
+#             -> gpurun_out/prof_c4/, prof_c5/
 #   prof      rocprofv3 stats of the bench line, then the PMC passes (tools/pmc.sh)
 #   pmc       the PMC passes alone (PMC_ARGS: bench arguments, default the headline)
 #   model     tools/bench_model.py $MODEL $B (default humanoid100 4096) under a kernel trace
+#             (SKIP=1|2: mj_inverseSkip(POS|VEL) calls)
 #   store     the store-layout microbenchmark, built from tools/exp_store.hip
 #   lanes / variants / step   tools/exp_lanes.py, exp_variants.py, exp_step.py
 # A failing pytest (status 1) does not stop the later steps; any other failure (a timeout,
@@ -45,6 +47,12 @@ for step in "$@"; do
       timeout -k 10 180 python bench.py --config 5 --own-stream > gpurun_out/c5own.json \
         2> gpurun_out/c5own.err || exit 1
       tail -1 gpurun_out/c5own.json ;;
+    c4trace)
+      timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4 -o c4 \
+        --output-format csv -- python bench.py --config 4 --steps 20 --warmup 3 \
+        > gpurun_out/c4trace.json 2> gpurun_out/c4trace.err || exit 1
+      tail -1 gpurun_out/c4trace.json
+      find gpurun_out/prof_c4 -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-150 ;;
     c5trace)
       timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c5 -o c5 \
         --output-format csv -- python bench.py --config 5 --steps 20 --warmup 3 \
@@ -66,11 +74,12 @@ for step in "$@"; do
       cat gpurun_out/pmc_summary.log ;;
     model)
       m=${MODEL:-humanoid100}
-      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$m -o $m \
+      t=$m${SKIP:+_skip$SKIP}
+      timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_$t -o $t \
         --output-format csv -- python tools/bench_model.py $m ${B:-4096} ${REPS:-10} \
-        > gpurun_out/model_$m.log 2>&1 || { tail -20 gpurun_out/model_$m.log; exit 1; }
-      grep -v "^W\|^\[" gpurun_out/model_$m.log | tail -3
-      find gpurun_out/prof_$m -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-150 ;;
+        > gpurun_out/model_$t.log 2>&1 || { tail -20 gpurun_out/model_$t.log; exit 1; }
+      grep -v "^W\|^\[" gpurun_out/model_$t.log | tail -3
+      find gpurun_out/prof_$t -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-150 ;;
     store)
       /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -o /tmp/exp_store tools/exp_store.hip || exit 1
       timeout -k 10 120 /tmp/exp_store > gpurun_out/store.log 2>&1 || { cat gpurun_out/store.log; exit 1; }
