@@ -284,6 +284,20 @@ MJH_HD int mjh_fluidDeriv(const mjhipModel* m) {
 }
 MJH_HD int mjh_qDerivStored(const mjhipModel* m) { return mjh_implicit(m) || mjh_fluidDeriv(m); }
 
+// one entry of the static collision program (host-built by coop_program in the order of
+// collision_pairs, csrc/pair_program.h), read by the cooperative kernel and collision(): the type-ordered geoms and their types, the pair's contact bound
+// (mjhip_pairMaxContacts; < 0: no collision function built here), its margin, and which
+// mj_filterSphere test applies with its bound formed as the reference forms it
+// (engine_collision_driver.c:1470-1497): filt 0 = bounding spheres, rb1 + rb2 + margin;
+// 1 = plane g1, margin + rb2; 2 = plane g2, margin + rb1; 3 = none
+struct CoopPair {
+  int g1, g2, t1, t2, kmax, filt;
+  int b1, b2, rt1, rt2;                     // the geoms' bodies and their roots
+  double margin, bound;
+};
+constexpr int kCoopPairDoubles = (int)(sizeof(CoopPair) / sizeof(double));
+static_assert(sizeof(CoopPair) % sizeof(double) == 0, "CoopPair packs into doubles");
+
 namespace mjh {
 
 constexpr double MINVAL = mjhipMINVAL;
@@ -405,6 +419,13 @@ struct Lane {
   // positions, and LDS turns those loads from memory round trips into LDS latency
   SP<S> gxpos;
   bool gstage;
+  // the static collision program (csrc/pair_program.h: candidate geom pairs in the order the
+  // serial mj_collision emits contacts, midphase sort and predefined pairs included) with each
+  // entry's predefined-pair index (-1 for a swept pair); nullptr: collision() walks the body
+  // pairs itself
+  const CoopPair* prog;
+  const int* prog_ipair;
+  int nprog;
   // cooperative constraint kernel only (else nullptr), per-instance LDS copies: cdq[8*j+c]
   // holds cdof (c < 6), qvel (c = 6) and qacc (c = 7) of dof j for the contact rows; fst[r]
   // receives efc_force[r] as a row is finished, for the J'force pass
@@ -3705,7 +3726,11 @@ MJH_HD void collideBoxBox(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
   if (bbuf) {
     keep = boxBoxKeep(margin, p1, m1, size1, p2, m2, size2, bbuf);
   } else {
-    if (ncon + 24 > d.con_cap) {            // cannot happen: 24 per box pair is in the capacity
+    // the exact capacity holds 24 contacts for every box pair, so this is reached only in a
+    // capped context (mjhip_contextCreateCapped): the instance is flagged CNSTRFULL, as the
+    // reference warns mjWARN_CONTACTFULL, but the pair is dropped whole where the reference
+    // would keep its first contacts up to the cap (the list's tail is this path's scratch)
+    if (ncon + 24 > d.con_cap) {
       *status |= MJHIP_INST_CNSTRFULL;
       return;
     }
@@ -3835,35 +3860,33 @@ MJH_HD double geomDistance(const mjhipModel& m, const Lane<S>& d, int geom1, int
   return dist;
 }
 
-// contactcompare (engine_collision_driver.c:223-257) on two contacts' geom ids
+// mj_filterSphere (engine_collision_driver.c:1470-1497) of a program entry: 1 = the bounding
+// spheres (filt 0, bound rb1 + rb2 + margin) or the plane distance (filt 1/2: plane g1/g2,
+// bound margin + rb of the other geom) rule the pair out; filt 3: no test
 template <int S>
-MJH_HD bool contactLess(const mjhipModel& m, const Lane<S>& d, int a, int b) {
-  int a1 = d.con_geom[2*a], a2 = d.con_geom[2*a+1];
-  int b1 = d.con_geom[2*b], b2 = d.con_geom[2*b+1];
-  if (m.geom_type[a1] > m.geom_type[a2]) { int t = a1; a1 = a2; a2 = t; }
-  if (m.geom_type[b1] > m.geom_type[b2]) { int t = b1; b1 = b2; b2 = t; }
-  return a1 < b1 || (a1 == b1 && a2 < b2);
+MJH_HD bool programFilter(const Lane<S>& d, const CoopPair& P) {
+  SP<S> p1 = d.gxpos + 3*P.g1, p2 = d.gxpos + 3*P.g2;
+  if (P.filt == 0) {
+    const double dif[3] = {p1[0]-p2[0], p1[1]-p2[1], p1[2]-p2[2]};
+    return dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2] > P.bound*P.bound;
+  }
+  if (P.filt <= 2) {
+    const bool pl1 = P.filt == 1;
+    SP<S> mat = d.geom_xmat + 9*(pl1 ? P.g1 : P.g2);
+    const double norm[3] = {mat[2], mat[5], mat[8]};
+    double dif[3];
+    sub3(dif, pl1 ? p2 : p1, pl1 ? p1 : p2);
+    return dot3(dif, norm) > P.bound;
+  }
+  return false;
 }
 
-template <int S>
-MJH_HD void swapContacts(const Lane<S>& d, int a, int b) {
-#define MJH_SWP(f, k, T) for (int j = 0; j < (k); j++) { T t = d.f[(k)*a+j]; \
-    d.f[(k)*a+j] = d.f[(k)*b+j]; d.f[(k)*b+j] = t; }
-  MJH_SWP(con_dist, 1, double) MJH_SWP(con_pos, 3, double) MJH_SWP(con_frame, 9, double)
-  MJH_SWP(con_includemargin, 1, double) MJH_SWP(con_friction, 5, double)
-  MJH_SWP(con_solref, 2, double) MJH_SWP(con_solreffriction, 2, double)
-  MJH_SWP(con_solimp, 5, double) MJH_SWP(con_mu, 1, double) MJH_SWP(con_dim, 1, int)
-  MJH_SWP(con_geom, 2, int) MJH_SWP(con_exclude, 1, int) MJH_SWP(con_efc_address, 1, int)
-#undef MJH_SWP
-}
-
-// mj_collision (engine_collision_driver.c:265-497): candidate body pairs in signature order,
-// geoms all-to-all; a midphase pair (a body with more than one geom) has its contacts stably
-// sorted by contactcompare, as mj_collideTree's callers do. The predefined pairs (sorted by
-// signature) merge in ahead of the first body pair whose signature is not below theirs
-// (:316-327; the broadphase pairs in between that are not candidates add no contacts), the
-// rest after the sweep (:432-437), and a candidate's geom pair that is also a predefined pair
-// is left to it (mj_collideGeomPair :499-523).
+// mj_collision (engine_collision_driver.c:265-497) over the static collision program
+// (csrc/pair_program.h, built once per context): the candidate body pairs in signature order,
+// their geom pairs all-to-all (a midphase pair's stably sorted by contactcompare's key, as
+// mj_collideTree's callers sort its contacts), and the predefined pairs merged in ahead of the
+// first body pair whose signature is not below theirs (:316-327), the rest after the sweep
+// (:432-437), a swept geom pair that is a predefined pair left to it (:499-523).
 template <int S>
 MJH_HD void collision(const mjhipModel& m, const Lane<S>& d, int* status) {
   int ncon = 0;                        // in a register; written once at the end
@@ -3881,46 +3904,23 @@ MJH_HD void collision(const mjhipModel& m, const Lane<S>& d, int* status) {
       }
     }
   }
-  // one loop over the body pairs in signature order and a final step for the predefined pairs
-  // left after the sweep, with a single narrowphase call site (each one is inlined whole)
-  const int nb = m.nbody;
-  const long npb = (long)nb*(nb - 1)/2;
-  const bool midphase = !(m.opt.disableflags & mjhipDSBL_MIDPHASE);
-  int pairadr = 0, b1 = 0, b2 = 1;
-  for (long pb = 0; pb <= npb; pb++) {
-    const bool end = pb == npb;
-    const int sig = (b1 << 16) + b2;
-    int pend = pairadr;                  // predefined pairs merged ahead of this body pair
-    while (pend < m.npair && (end || m.pair_signature[pend] <= sig)) pend++;
-    const int npre = pend - pairadr;
-    const bool cand = !end && mjhip_bodyPairCandidate(&m, b1, b2);
-    const int n1 = cand ? m.body_geomnum[b1] : 0, n2 = cand ? m.body_geomnum[b2] : 0;
-    int before = ncon;
-    for (int t = 0; t < npre + n1*n2; t++) {
-      int g1, g2, ip = -1;
-      if (t < npre) {
-        ip = pairadr + t;
-        g1 = m.pair_geom1[ip];
-        g2 = m.pair_geom2[ip];
-      } else {
-        if (t == npre) before = ncon;    // the swept contacts start here
-        const int k = t - npre;
-        g1 = m.body_geomadr[b1] + k / n2;
-        g2 = m.body_geomadr[b2] + k % n2;
-        if (m.npair && mjhip_isPredefinedPair(&m, g1, g2)) continue;
-      }
-      collideGeoms(m, d, g1, g2, ncon, status, ip);
+  // the static program (csrc/pair_program.h; nullptr when it is empty: no geom pair of the
+  // model can collide): its bounding-sphere tests eight entries at a time (their position
+  // loads in flight together), then the narrowphase of the survivors in program order. The
+  // filter is mj_filterSphere's test with the entry's bound formed as the reference forms it,
+  // so the entries it drops are the ones collideGeoms would return no contact for.
+  const int np = d.prog ? d.nprog : 0;
+  for (int p0 = 0; p0 < np; p0 += 8) {
+    bool hit[8];
+#pragma unroll
+    for (int u = 0; u < 8; u++) {
+      hit[u] = false;
+      if (p0 + u < np) hit[u] = !programFilter(d, d.prog[p0 + u]);
     }
-    pairadr = pend;
-    if (cand && midphase && !(n1 == 1 && n2 == 1)) {
-      int n = ncon;
-      for (int a = before + 1; a < n; a++) {
-        for (int b = a; b > before && contactLess(m, d, b, b - 1); b--) swapContacts(d, b, b - 1);
-      }
-    }
-    if (++b2 >= nb) {
-      b1++;
-      b2 = b1 + 1;
+    for (int u = 0; u < 8 && p0 + u < np; u++) {
+      if (!hit[u]) continue;
+      const CoopPair& P = d.prog[p0 + u];
+      collideGeoms(m, d, P.g1, P.g2, ncon, status, d.prog_ipair[p0 + u]);
     }
   }
   d.con_count[0] = ncon;
@@ -5213,32 +5213,56 @@ MJH_HD bool addRowsSparse(const mjhipModel& m, const Lane<S>& d, RowCount& rc, J
   return true;
 }
 
-// mju_transposeSparse engine_util_sparse.c:474-515: efc_JT from the compressed efc_J rows
+// mju_transposeSparse engine_util_sparse.c:474-515: efc_JT from the compressed efc_J rows.
+// The rows of one contact share its chain (instantiateContact), so they are transposed as a
+// group: one count and one slot update per chain column for the whole group, its rows then
+// written to consecutive slots in row order -- the same efc_JT, with a quarter of the
+// read-modify-write round trips on the per-column counters (each waits for the previous one
+// in memory) for pyramidal contacts.
+template <int S>
+MJH_HD int transposeGroup(const Lane<S>& d, int r, int nefc) {
+  const int t = d.efc_type[r];
+  if (t != CNSTR_CONTACT_FRICTIONLESS && t != CNSTR_CONTACT_PYRAMIDAL &&
+      t != CNSTR_CONTACT_ELLIPTIC) {
+    return 1;
+  }
+  const int id = d.efc_id[r];
+  int g = 1;
+  while (r + g < nefc && d.efc_id[r + g] == id && d.efc_type[r + g] == t) g++;
+  return g;
+}
+
 template <int S>
 MJH_HD void transposeRows(const mjhipModel& m, const Lane<S>& d, int nefc) {
   const int nv = m.nv;
   for (int j = 0; j < nv; j++) d.efc_JT_rownnz[j] = 0;
-  for (int r = 0; r < nefc; r++) {
+  for (int r = 0; r < nefc;) {
+    const int g = transposeGroup(d, r, nefc);
     const int a = d.efc_J_rowadr[r], e = a + d.efc_J_rownnz[r];
     for (int k = a; k < e; k++) {
       const int c = d.efc_J_colind[k];
-      d.efc_JT_rownnz[c] = d.efc_JT_rownnz[c] + 1;
+      d.efc_JT_rownnz[c] = d.efc_JT_rownnz[c] + g;
     }
+    r += g;
   }
   int acc = 0;
   for (int j = 0; j < nv; j++) {             // rowadr as the next free slot of each row
     d.efc_JT_rowadr[j] = acc;
     acc += d.efc_JT_rownnz[j];
   }
-  for (int r = 0; r < nefc; r++) {
-    const int a = d.efc_J_rowadr[r], e = a + d.efc_J_rownnz[r];
-    for (int k = a; k < e; k++) {
-      const int c = d.efc_J_colind[k];
+  for (int r = 0; r < nefc;) {
+    const int g = transposeGroup(d, r, nefc);
+    const int a = d.efc_J_rowadr[r], n = d.efc_J_rownnz[r];
+    for (int k = 0; k < n; k++) {
+      const int c = d.efc_J_colind[a + k];
       const int slot = d.efc_JT_rowadr[c];
-      d.efc_JT_rowadr[c] = slot + 1;
-      d.efc_JT_colind[slot] = r;
-      d.efc_JT[slot] = d.efc_J[k];
+      d.efc_JT_rowadr[c] = slot + g;
+      for (int i = 0; i < g; i++) {            // row r+i's entry k (rows of a group: stride n)
+        d.efc_JT_colind[slot + i] = r + i;
+        d.efc_JT[slot + i] = d.efc_J[a + i*n + k];
+      }
     }
+    r += g;
   }
   for (int j = 0; j < nv; j++) d.efc_JT_rowadr[j] = d.efc_JT_rowadr[j] - d.efc_JT_rownnz[j];
 }
@@ -8559,6 +8583,9 @@ struct Mirror {
   int efc_cap;
   int con_cap;
   long nj_cap;
+  const CoopPair* prog;                      // the static collision program (Lane::prog)
+  const int* prog_ipair;
+  int nprog;
 };
 
 MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
@@ -8579,6 +8606,9 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
   d.chain = nullptr;
   d.gxpos = d.geom_xpos;
   d.gstage = false;
+  d.prog = mr.prog;
+  d.prog_ipair = mr.prog_ipair;
+  d.nprog = mr.nprog;
   d.cdq = nullptr;
   d.fst = nullptr;
   d.nfst = 0;

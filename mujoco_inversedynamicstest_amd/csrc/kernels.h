@@ -76,19 +76,7 @@ static unsigned coopGrid(int B, int G, bool list) {
   return list && full > 1024u ? 1024u : full;
 }
 
-// one entry of the cooperative kernel's pair program (host-built by coop_program in the order
-// of collision_pairs): the type-ordered geoms and their types, the pair's contact bound
-// (mjhip_pairMaxContacts; < 0: no collision function built here), its margin, and which
-// mj_filterSphere test applies with its bound formed as the reference forms it
-// (engine_collision_driver.c:1470-1497): filt 0 = bounding spheres, rb1 + rb2 + margin;
-// 1 = plane g1, margin + rb2; 2 = plane g2, margin + rb1; 3 = none
-struct CoopPair {
-  int g1, g2, t1, t2, kmax, filt;
-  int b1, b2, rt1, rt2;                     // the geoms' bodies and their roots
-  double margin, bound;
-};
-constexpr int kCoopPairDoubles = (int)(sizeof(CoopPair) / sizeof(double));
-static_assert(sizeof(CoopPair) % sizeof(double) == 0, "CoopPair packs into doubles");
+// CoopPair, the pair program entry: engine_device.h (the generic collision() reads it too)
 
 // dynamic LDS of k_constraint_coop: the pair program and geom_size once per block; per
 // instance 8 nv

@@ -26,6 +26,7 @@
 #include "engine_device.h"
 #include "fast_kernels.h"
 #include "kernels.h"
+#include "pair_program.h"
 #include "post_pass.h"
 
 //==================================== kernels ===============================================
@@ -405,6 +406,7 @@ struct mjhipContext_ {
   int* fdflag = nullptr;
   CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
   mjh::ContactParam* cparams = nullptr;    // each program pair's mj_contactParam
+  int* prog_ipair = nullptr;               // each program pair's predefined-pair index or -1
   unsigned long long* masks = nullptr;     // the cooperative kernel's chain masks (coop_masks)
   int npair = 0;
   bool boxpair = false;                    // a box-box pair is in the program (coop LDS)
@@ -425,101 +427,6 @@ struct mjhipContext_ {
   unsigned long long traw[MJH_TSLOTS]{};   // the raw mark sums (tools/exp_phases.py)
   hipEvent_t tev0 = nullptr, tev1 = nullptr;
 };
-
-// The static geom-pair program of mj_collision (engine_collision_driver.c:265-497) for the
-// cooperative constraint kernel: candidate body pairs in signature order (mjhip_contact.h),
-// their geoms all-to-all, minus the pairs no run can collide (no collision function, geom
-// bitmask); a body pair the midphase handles (a body with more than one geom) has its geom
-// pairs stably sorted by contactcompare's key (:227-257), the type-ordered geom ids. Every
-// contact of a pair carries that key, so this is the order the serial collision() leaves
-// its contacts in, and the cooperative kernel concatenates the pairs' contacts in it.
-// Predefined pairs (z = the pair's index, else -1) merge in as the device collision() does:
-// ahead of the first body pair whose signature is not below theirs, the rest at the end, and
-// a candidate's geom pair that is a predefined pair is left to it.
-static std::vector<int3> collision_pairs(const mjhipModel* m) {
-  std::vector<int3> out;
-  if (!mjhip_contactsEnabled(m)) return out;
-  int pairadr = 0;
-  auto predefined = [&](int k) {
-    const int g1 = m->pair_geom1[k], g2 = m->pair_geom2[k];
-    const bool flip = m->geom_type[g1] > m->geom_type[g2];
-    if (mjhip_pairMaxContacts(m, m->geom_type[flip ? g2 : g1], m->geom_type[flip ? g1 : g2])) {
-      out.push_back(make_int3(g1, g2, k));
-    }
-  };
-  const bool midphase = !(m->opt.disableflags & mjhipDSBL_MIDPHASE);
-  auto key = [&](int2 p) {
-    return m->geom_type[p.x] > m->geom_type[p.y] ? std::make_pair(p.y, p.x)
-                                                 : std::make_pair(p.x, p.y);
-  };
-  for (int b1 = 0; b1 < m->nbody; b1++) {
-    for (int b2 = b1 + 1; b2 < m->nbody; b2++) {
-      for (; pairadr < m->npair && m->pair_signature[pairadr] <= (b1 << 16) + b2; pairadr++) {
-        predefined(pairadr);
-      }
-      if (!mjhip_bodyPairCandidate(m, b1, b2)) continue;
-      const int n1 = m->body_geomnum[b1], n2 = m->body_geomnum[b2];
-      std::vector<int2> list;
-      for (int i = 0; i < n1; i++) {
-        for (int j = 0; j < n2; j++) {
-          const int g1 = m->body_geomadr[b1] + i, g2 = m->body_geomadr[b2] + j;
-          if (m->npair && mjhip_isPredefinedPair(m, g1, g2)) continue;
-          const std::pair<int, int> k = key(make_int2(g1, g2));
-          if (!mjhip_pairMaxContacts(m, m->geom_type[k.first], m->geom_type[k.second])) continue;
-          if (mjhip_filterBitmask(m->geom_contype[g1], m->geom_conaffinity[g1],
-                                  m->geom_contype[g2], m->geom_conaffinity[g2])) {
-            continue;
-          }
-          list.push_back(make_int2(g1, g2));
-        }
-      }
-      if (midphase && !(n1 == 1 && n2 == 1)) {
-        std::stable_sort(list.begin(), list.end(),
-                         [&](int2 a, int2 b) { return key(a) < key(b); });
-      }
-      for (const int2& p : list) out.push_back(make_int3(p.x, p.y, -1));
-    }
-  }
-  for (; pairadr < m->npair; pairadr++) predefined(pairadr);
-  return out;
-}
-
-// the cooperative kernel's program for collision_pairs' pairs: what mj_collideGeoms derives
-// from the model alone, type-ordered as narrowGeoms does (engine_collision_driver.c:1440-1497)
-static std::vector<CoopPair> coop_program(const mjhipModel* m, const std::vector<int3>& pairs) {
-  std::vector<CoopPair> out;
-  const bool ovr = (m->opt.enableflags & mjhipENBL_OVERRIDE) != 0;
-  for (const int3& pr : pairs) {
-    CoopPair P{};
-    P.g1 = pr.x;
-    P.g2 = pr.y;
-    if (m->geom_type[P.g1] > m->geom_type[P.g2]) std::swap(P.g1, P.g2);
-    P.t1 = m->geom_type[P.g1];
-    P.t2 = m->geom_type[P.g2];
-    P.kmax = mjhip_pairMaxContacts(m, P.t1, P.t2);
-    P.b1 = m->geom_bodyid[P.g1];
-    P.b2 = m->geom_bodyid[P.g2];
-    P.rt1 = m->body_rootid[P.b1];
-    P.rt2 = m->body_rootid[P.b2];
-    const double mg1 = m->geom_margin[P.g1], mg2 = m->geom_margin[P.g2];
-    P.margin = ovr ? m->opt.o_margin : pr.z >= 0 ? m->pair_margin[pr.z] : (mg1 > mg2 ? mg1 : mg2);
-    const double rb1 = m->geom_rbound[P.g1], rb2 = m->geom_rbound[P.g2];
-    if (rb1 > 0 && rb2 > 0) {
-      P.filt = 0;
-      P.bound = rb1 + rb2 + P.margin;
-    } else if (P.t1 == mjhipGEOM_PLANE && rb2 > 0) {
-      P.filt = 1;
-      P.bound = P.margin + rb2;
-    } else if (P.t2 == mjhipGEOM_PLANE && rb1 > 0) {
-      P.filt = 2;
-      P.bound = P.margin + rb1;
-    } else {
-      P.filt = 3;
-    }
-    out.push_back(P);
-  }
-  return out;
-}
 
 // FNV-1a 64 over sizes, options and every model array (= fields.model_signature in Python)
 static unsigned long long model_signature(const mjhipModel* m) {
@@ -821,29 +728,36 @@ MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int cap
   // k_constraint)
   if (const char* lanes = getenv("MJHIP_COOP_LANES")) c->coop = atoi(lanes) == 0 ? 0 : 16;
   if (c->con_cap > 0) {
-    std::vector<int3> pairs = collision_pairs(m);
+    // the static collision program (csrc/pair_program.h): the cooperative kernel's pair
+    // program, and collision()'s candidate list in every other kernel (Mirror::prog)
+    std::vector<ProgItem> pairs = collision_pairs(m);
     c->npair = (int)pairs.size();
-    for (const int3& pr : pairs) {
-      c->boxpair |= m->geom_type[pr.x] == mjhipGEOM_BOX && m->geom_type[pr.y] == mjhipGEOM_BOX;
+    for (const ProgItem& pr : pairs) {
+      c->boxpair |= m->geom_type[pr.g1] == mjhipGEOM_BOX && m->geom_type[pr.g2] == mjhipGEOM_BOX;
     }
     if (c->npair) {
       const std::vector<CoopPair> prog = coop_program(m, pairs);
       // contact parameters are model constants: formed here once per pair, by the same
       // function (host arithmetic, as the reference's)
-      std::vector<mjh::ContactParam> cps(prog.size());
-      for (size_t i = 0; i < prog.size(); i++) {
-        mjh::pairParam(*m, prog[i].g1, prog[i].g2, pairs[i].z, cps[i]);
-      }
+      const std::vector<mjh::ContactParam> cps = program_params(m, prog, pairs);
+      std::vector<int> ipair(pairs.size());
+      for (size_t i = 0; i < pairs.size(); i++) ipair[i] = pairs[i].ipair;
       if (hipMalloc((void**)&c->pairs, sizeof(CoopPair) * prog.size()) != hipSuccess ||
           hipMemcpy(c->pairs, prog.data(), sizeof(CoopPair) * prog.size(),
                     hipMemcpyHostToDevice) != hipSuccess ||
           hipMalloc((void**)&c->cparams, sizeof(mjh::ContactParam) * cps.size()) != hipSuccess ||
           hipMemcpy(c->cparams, cps.data(), sizeof(mjh::ContactParam) * cps.size(),
+                    hipMemcpyHostToDevice) != hipSuccess ||
+          hipMalloc((void**)&c->prog_ipair, sizeof(int) * ipair.size()) != hipSuccess ||
+          hipMemcpy(c->prog_ipair, ipair.data(), sizeof(int) * ipair.size(),
                     hipMemcpyHostToDevice) != hipSuccess) {
         return fail("pair program upload");
       }
     }
   }
+  c->mirror.prog = c->npair ? c->pairs : nullptr;
+  c->mirror.prog_ipair = c->npair ? c->prog_ipair : nullptr;
+  c->mirror.nprog = c->npair;
   // the native convex solver keeps its polytope in the instance's scratch: one lane per
   // instance (the cooperative kernel would run several pairs of an instance at once)
   if (mjh_needConvex(m) || m->nmesh || m->nhfield) c->coop = 0;
@@ -907,6 +821,7 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->fdflag);
   hipFree(c->pairs);
   hipFree(c->cparams);
+  hipFree(c->prog_ipair);
   hipFree(c->masks);
   hipFree(c->mirror_buf);
   hipFree(c->dmodel_buf);

@@ -19,11 +19,23 @@ float/double mix: float *= double rounds back to float after a double product, t
 sums of ComputeInertia are float products of float vertices, and so on.
 
 The hull comes from scipy's Qhull (scipy.spatial.ConvexHull, option Qt) where the reference
-links Qhull itself; the facets and the per-vertex edge lists of the graph are ordered by
-facet index and point id here, which may differ from the order Qhull's internal lists give
-the reference. The graph's content (which hull vertices are adjacent) is the same; the order
-only decides ties in mjc_hillclimbSupport, and the face order only changes the rounding of
-the mass-property sums (their last bits).
+links Qhull itself. The graph's content (which hull vertices are adjacent) is the same, but
+its ORDER is not pinned: here the vertices are in point-id order and each vertex's edge list
+follows its facets in scipy's facet order with the vertices of each facet as scipy lists
+them, where the reference walks Qhull's vertex list (FORALLvertices) and each vertex's
+neighbour facets (user_mesh.cc:1732-1781). scipy exposes neither list, and neither Qhull's
+headers nor its library are in this image, so the reference's order cannot be derived here.
+The order is observable in three places:
+  * mjc_hillclimbSupport: which support vertex wins a tie (a hull face parallel to the
+    search direction);
+  * mjc_PlaneConvex (engine_collision_convex.c:1110-1131): after the support vertex it walks
+    that vertex's edge list and stops at maxplanemesh = 3 contacts, so when more than two
+    neighbours lie within the plane's threshold (a flat face resting on the plane) the order
+    picks which two become contacts, and in any case it sets the contacts' order;
+  * the face order changes the rounding of the mass-property sums (their last bits).
+Plane-mesh contact sets and orders are therefore a known deviation: the oracle compiles from
+this module, so tests/test_mesh_hfield_cpu.py pins the device against the oracle, not
+against the reference's contact set (Meshes and height fields).
 """
 from __future__ import annotations
 

@@ -6,6 +6,7 @@
 #include <string.h>
 
 #include "../mujoco_inversedynamicstest_amd/csrc/engine_device.h"
+#include "../mujoco_inversedynamicstest_amd/csrc/pair_program.h"
 
 // doubles / ints of per-instance scratch (each field padded by one element)
 extern "C" void kh_sizes(const mjhipModel* m, int efc_cap, int con_cap, long* nd, long* ni) {
@@ -107,5 +108,17 @@ static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int
   L.dchain = nullptr;
   L.ccdx = L.ccd.p;
   L.ccdxi = L.ccdi.p;
+  // the static collision program, as libmjhip.so builds it per context (rebuilt per call
+  // here: the harness keeps no per-model state)
+  static std::vector<CoopPair> prog;
+  static std::vector<int> ipair;
+  const std::vector<ProgItem> items = collision_pairs(m);
+  prog = coop_program(m, items);
+  ipair.resize(items.size());
+  for (size_t k = 0; k < items.size(); k++) ipair[k] = items[k].ipair;
+  const bool use = !prog.empty();
+  L.prog = use ? prog.data() : nullptr;
+  L.prog_ipair = use ? ipair.data() : nullptr;
+  L.nprog = use ? (int)prog.size() : 0;
   return L;
 }

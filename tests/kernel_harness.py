@@ -18,7 +18,8 @@ SRC = [os.path.join(HERE, "cpu_kernel_harness.cpp"),
        os.path.join(HERE, "..", "include", "mjhip.h"),
        os.path.join(HERE, "..", "include", "mjhip_fields.h"),
        os.path.join(HERE, "..", "include", "mjhip_contact.h"),
-       os.path.join(HERE, "..", "mujoco_inversedynamicstest_amd", "csrc", "engine_device.h")]
+       os.path.join(HERE, "..", "mujoco_inversedynamicstest_amd", "csrc", "engine_device.h"),
+       os.path.join(HERE, "..", "mujoco_inversedynamicstest_amd", "csrc", "pair_program.h")]
 
 _lib = None
 

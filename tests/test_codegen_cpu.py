@@ -29,6 +29,7 @@ def build(m, name):
               os.path.join(HERE, "..", "include", "mjhip_fields.h"),
               os.path.join(HERE, "..", "include", "mjhip_contact.h"),
               os.path.join(HERE, "..", "mujoco_inversedynamicstest_amd", "csrc", "post_pass.h"),
+              os.path.join(HERE, "..", "mujoco_inversedynamicstest_amd", "csrc", "pair_program.h"),
               os.path.join(HERE, "codegen_harness.cpp")):
     h.update(open(dep, "rb").read())
   tag = h.hexdigest()[:10]
