@@ -1273,6 +1273,20 @@ def _gen_va(M: _Model, store_fields=None) -> str:
   return E.text()
 
 
+def _perturb_loads(body: str, which: dict) -> str:
+  """mjd_inverseFD's perturbation applied as an input lands: `arr[k] = <load>;` becomes
+  `arr[k] = k == idx ? <load> + eps : <load>;` for arr in `which` (arr -> index variable), the
+  sum k_fd_expand would have stored (engine_derivative_fd.c:646-699: x[i] + eps)."""
+  import re
+
+  def sub(mt):
+    arr, k, rhs = mt.group(2), mt.group(3), mt.group(4)
+    return (f"{mt.group(1)}{arr}[{k}] = ({which[arr]} == {k}) ? ({rhs}) + eps : ({rhs});")
+  names = "|".join(which)
+  return re.sub(rf"^(\s*)({names})\[(\d+)\] = (.*P_(?:{names})\[\d+\*64\].*);$", sub, body,
+                flags=re.M)
+
+
 def _gen_acc(M: _Model, store_fields=None) -> str:
   """The acceleration stage alone: mj_inverseSkip(mjSTAGE_VEL) (engine_inverse.c:197-261)
   with the position and velocity stages' outputs read from the mirror. One tree pass of
@@ -1585,7 +1599,10 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
         set(re.findall(r"MJH_NT_STORE\(P_(\w+)\[", vb))
     assert textual <= M.va_stored | {"qpos", "qvel", "qacc"}, \
         f"k_vaskip: va stores outside the record: {textual - M.va_stored}"
-    own = {"qpos", "qvel", "qacc"} | M.va_stored
+    # qpos, qvel and qacc are read from the centre too: k_fd_expand writes only the
+    # position-stage block, and the perturbed component is added as the loads land (pa / pv:
+    # the qacc / qvel dof this instance perturbs, -1 for none)
+    own = set(M.va_stored)
     skip_body = re.sub(r"(double\* __restrict__ P_(\w+) = mr\.\w+ \+ \(\(long\))blk(\*\d+\)\*64 \+ )lane;",
                        lambda mt: mt.group(0) if mt.group(2) in own else
                        f"{mt.group(1)}sblk{mt.group(3)}slane;", vb)
@@ -1593,9 +1610,10 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
                                   "const bool cflag = ecs[0] != 0;")
     skip_body = skip_body.replace("MJH_NT_STORE_IF(SV, ", "MJH_NT_STORE_IF(true, ")
     skip_body = skip_body.replace("MJH_NT_LOAD_IF(SV, ", "MJH_NT_LOAD_IF(false, ")
+    skip_body = _perturb_loads(skip_body, {"qvel": "pv", "qacc": "pa"})
     out.append(f"MJH_HD void fast_vaskip_{name}(const Mirror& mr, int blk, int lane, int sblk, "
-               f"int slane, int B, const int* __restrict__ ecs, {_SIG['va'][0]}) {{\n"
-               f"{skip_body}\n}}\n")
+               f"int slane, int B, const int* __restrict__ ecs, int pa, int pv, double eps, "
+               f"{_SIG['va'][0]}) {{\n{skip_body}\n}}\n")
   if M.cmode in ("none", "list"):
     # the acceleration stage alone (mj_inverseSkip(mjSTAGE_VEL)): k_acc for batched calls, and
     # in k_fdskip for mjd_inverseFD's qacc perturbations, whose velocity-stage inputs (cvel,
@@ -1608,30 +1626,35 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
                              f"{mt.group(4)});", ab, flags=re.M)
     out.append(f"MJH_HD void fast_acc_{name}(const Mirror& mr, int blk, int lane, int B, "
                f"{_SIG['va'][0]}) {{\n{ab}\n}}\n")
-    own_acc = {"qacc"} | M.acc_stored
+    own_acc = set(M.acc_stored)          # qacc from the centre, perturbed at pa
     acc_skip = re.sub(r"(double\* __restrict__ P_(\w+) = mr\.\w+ \+ \(\(long\))blk(\*\d+\)\*64 \+ )lane;",
                       lambda mt: mt.group(0) if mt.group(2) in own_acc else
                       f"{mt.group(1)}sblk{mt.group(3)}slane;", ab)
     acc_skip = acc_skip.replace("const bool cflag = ec[0] != 0;", "const bool cflag = ecs[0] != 0;")
+    acc_skip = _perturb_loads(acc_skip, {"qacc": "pa"})
     out.append(f"MJH_HD void fast_accskip_{name}(const Mirror& mr, int blk, int lane, int sblk, "
-               f"int slane, int B, const int* __restrict__ ecs, {_SIG['va'][0]}) {{\n"
-               f"{acc_skip}\n}}\n")
+               f"int slane, int B, const int* __restrict__ ecs, int pa, double eps, "
+               f"{_SIG['va'][0]}) {{\n{acc_skip}\n}}\n")
   if M.cmode in ("none", "list"):
     flag = ("  if (ecs[0] != 0) needfull[0] = 1;\n" if M.cmode == "list" else "")
-    out.append(f"""__global__ __launch_bounds__(64, 1) void k_vaskip_{name}(Mirror mr, int B, int off,
-    int per, int sstride, int* __restrict__ efc_count, int* __restrict__ needfull) {{
+    out.append(f"""// layout 1 over [off, B): per = 2nv perturbations per centre, the first nv of qacc, the
+// next nv of qvel (engine_derivative_fd.c:646-699 order)
+__global__ __launch_bounds__(64, 1) void k_vaskip_{name}(Mirror mr, int B, int off,
+    int per, int sstride, int* __restrict__ efc_count, int* __restrict__ needfull, double eps) {{
   __shared__ double qo_lds[{64 * max(M.nv, 1)}];
   const long gi = (long)off + (long)blockIdx.x*64 + threadIdx.x;
   if (gi >= B) return;
   const long si = (gi - off) / per * sstride;
+  const int j = (int)((gi - off) % per);
   const int* ecs = efc_count + (si >> 6)*4*64 + (si & 63);
 {flag}  fast_vaskip_{name}(mr, (int)(gi >> 6), (int)(gi & 63), (int)(si >> 6), (int)(si & 63), B,
-                    ecs, nullptr, nullptr, efc_count, qo_lds, nullptr);
+                    ecs, j < {M.nv} ? j : -1, j < {M.nv} ? -1 : j - {M.nv}, eps, nullptr,
+                    nullptr, efc_count, qo_lds, nullptr);
 }}
 {"" if shared else "static "}void launch_vaskip_{name}(hipStream_t s, const Mirror& mr, int B, int off, int per,
-                                int sstride, int* efc_count, int* needfull) {{
+                                int sstride, int* efc_count, int* needfull, double eps) {{
   hipLaunchKernelGGL(k_vaskip_{name}, dim3((B - off + 63) / 64), dim3(64), 0, s, mr, B, off,
-                     per, sstride, efc_count, needfull);
+                     per, sstride, efc_count, needfull, eps);
 }}
 // mjd_inverseFD layout 2 in one launch over [off, B): the nq = (B - off)/2 qvel perturbations
 // (mj_inverseSkip(mjSTAGE_POS): the va stage over the centre's position stage) on the first
@@ -1639,7 +1662,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
 // stage over the centre's position and velocity stages). nq is a multiple of 64, so each wave
 // has one role; the two run side by side instead of as two under-filled launches.
 __global__ __launch_bounds__(64, 1) void k_fdskip_{name}(Mirror mr, int B, int off,
-    int per, int sstride, int* __restrict__ efc_count, int* __restrict__ needfull) {{
+    int per, int sstride, int* __restrict__ efc_count, int* __restrict__ needfull, double eps) {{
   __shared__ double qo_lds[{64 * max(M.nv, 1)}];
   const long nq = ((long)B - off) / 2;
   const long t = (long)blockIdx.x*64 + threadIdx.x;
@@ -1647,19 +1670,20 @@ __global__ __launch_bounds__(64, 1) void k_fdskip_{name}(Mirror mr, int B, int o
   const bool vel = t < nq;
   const long gi = vel ? off + nq + t : off + (t - nq);
   const long si = (vel ? t : t - nq) / per * sstride;
+  const int j = (int)((vel ? t : t - nq) % per);
   const int* ecs = efc_count + (si >> 6)*4*64 + (si & 63);
 {flag}  if (vel) {{
     fast_vaskip_{name}(mr, (int)(gi >> 6), (int)(gi & 63), (int)(si >> 6), (int)(si & 63), B,
-                      ecs, nullptr, nullptr, efc_count, qo_lds, nullptr);
+                      ecs, -1, j, eps, nullptr, nullptr, efc_count, qo_lds, nullptr);
   }} else {{
     fast_accskip_{name}(mr, (int)(gi >> 6), (int)(gi & 63), (int)(si >> 6), (int)(si & 63), B,
-                       ecs, nullptr, nullptr, efc_count, qo_lds, nullptr);
+                       ecs, j, eps, nullptr, nullptr, efc_count, qo_lds, nullptr);
   }}
 }}
 {"" if shared else "static "}void launch_fdskip_{name}(hipStream_t s, const Mirror& mr, int B, int off, int per,
-                                int sstride, int* efc_count, int* needfull) {{
+                                int sstride, int* efc_count, int* needfull, double eps) {{
   hipLaunchKernelGGL(k_fdskip_{name}, dim3((B - off + 63) / 64), dim3(64), 0, s, mr, B, off,
-                     per, sstride, efc_count, needfull);
+                     per, sstride, efc_count, needfull, eps);
 }}
 // batched mj_inverseSkip on the straight-line path: POS runs the va stage (k_va), VEL the
 // acceleration stage (k_acc); rows of the previous call go through k_skip_rows (mjhip.hip)
@@ -1745,7 +1769,7 @@ def generate_registries(entries) -> tuple:
       if vaskip:
         for k in ("vaskip", "fdskip"):
           main.append(f"void launch_{k}_{name}(hipStream_t, const Mirror&, int, int, int, int, "
-                      "int*, int*);")
+                      "int*, int*, double);")
         main.append(f"void launch_skip_{name}(hipStream_t, const Mirror&, int, int, double*, "
                     "int*, int*);")
     else:

@@ -18,12 +18,14 @@ struct FastKernelEntry {
   // mj_inverseSkip(mjSTAGE_POS) for mjd_inverseFD's qvel/qacc perturbations: the va stage of
   // instances [off, B), position-stage inputs from centre (t - off)/per*sstride (codegen.py
   // k_vaskip); null for run-time kernels and models whose rows serve every instance
-  void (*launch_vaskip)(hipStream_t, const Mirror&, int, int, int, int, int*, int*);
+  // (the last argument is eps: each skip instance reads its centre's qpos/qvel/qacc and adds
+  // eps to the component it perturbs, so k_fd_expand writes only the position-stage block)
+  void (*launch_vaskip)(hipStream_t, const Mirror&, int, int, int, int, int*, int*, double);
   // mjd_inverseFD layout 2 in one launch over [off, B) (k_fdskip): the first half of the
   // instances qacc perturbations, mj_inverseSkip(mjSTAGE_VEL), the acceleration stage alone
   // over the centre's position- and velocity-stage outputs; the second half qvel
   // perturbations, mjSTAGE_POS, as k_vaskip (centres (t - off)/per*sstride within each half)
-  void (*launch_fdskip)(hipStream_t, const Mirror&, int, int, int, int, int*, int*);
+  void (*launch_fdskip)(hipStream_t, const Mirror&, int, int, int, int, int*, int*, double);
   // batched mj_inverseSkip(skipstage) for skipstage POS (k_va) or VEL (k_acc) over [0, B)
   // (qfrc_out row-major or null, status or null, efc_count)
   void (*launch_skip)(hipStream_t, const Mirror&, int, int, double*, int*, int*);

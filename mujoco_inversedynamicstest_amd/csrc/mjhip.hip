@@ -152,14 +152,18 @@ __device__ static inline long fd_inst(int layout, long nbase, long b, int p, int
   return nbase*(nv + 1) + nbase*nv + b*nv + (p - 1 - nv);
 }
 
+// instances [first + thread, end) of the layout, and within a device-side range {lo, hi}
+// when one is given (the fall-back's: empty unless a centre has limit rows)
 __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __restrict__ qpos,
                             const double* __restrict__ qvel, const double* __restrict__ qacc,
                             const double* __restrict__ ctrl, double eps, int layout,
-                            int* __restrict__ fdflag) {
+                            int* __restrict__ fdflag, long first, long end,
+                            const int* __restrict__ range) {
   const int P = 3*m.nv + 1;
-  long inst = (long)blockIdx.x*blockDim.x + threadIdx.x;
-  if (fdflag && inst == 0) fdflag[0] = 0;     // k_vaskip raises it later in stream order
-  if (inst >= (long)nbase*P) return;
+  long inst = first + (long)blockIdx.x*blockDim.x + threadIdx.x;
+  if (fdflag && inst == first) fdflag[0] = 0;   // k_vaskip raises it later in stream order
+  if (inst >= end || inst >= (long)nbase*P) return;
+  if (range && (inst < range[0] || inst >= range[1])) return;
   long b;
   int p;
   if (!layout) {
@@ -1600,9 +1604,12 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
   // 56 us over the same 55,296 instances)
   if (layout && c->fast->launch_fdskip && nQ % 64 == 0 && accskip && accskip[0] == '1') layout = 2;
   int rc = MJHIP_OK;
-  hipLaunchKernelGGL(k_fd_expand, dim3((ninst + 255)/256), dim3(256), 0, c->stream,
+  // with a skip layout only the position-stage block is expanded: the skip kernels read their
+  // centre's inputs and perturb them in registers (the fall-back expands the rest, below)
+  const long nexp = layout ? nA : ninst;
+  hipLaunchKernelGGL(k_fd_expand, dim3((nexp + 255)/256), dim3(256), 0, c->stream,
                      c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, layout,
-                     layout ? c->fdflag : nullptr);
+                     layout ? c->fdflag : nullptr, (long)0, nexp, (const int*)nullptr);
   FDCHECK(hipGetLastError(), "k_fd_expand launch");
   if (layout) {
     // the nv+1 position-stage instances of every base state: the full pipeline
@@ -1613,11 +1620,11 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
       // the nv qacc perturbations: the acceleration stage over their centre's position and
       // velocity stages; the nv qvel ones: the va stage over their centre's position stage
       c->fast->launch_fdskip(c->stream, c->mirror, (int)ninst, (int)nA, nv, nv + 1,
-                             c->mirror.efc_count, c->fdflag);
+                             c->mirror.efc_count, c->fdflag, eps);
     } else {
       // the 2nv qvel/qacc perturbations: the va stage over their centre's position stage
       c->fast->launch_vaskip(c->stream, c->mirror, (int)ninst, (int)nA, 2*nv, nv + 1,
-                             c->mirror.efc_count, c->fdflag);
+                             c->mirror.efc_count, c->fdflag, eps);
     }
     FDCHECK(hipGetLastError(), "k_vaskip launch");
     if (c->fast->cmode == 1) {
@@ -1629,6 +1636,12 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
       hipLaunchKernelGGL(k_fd_gate, dim3(1), dim3(1), 0, c->stream, c->fdflag, (int)nA,
                          (int)ninst);
       FDCHECK(hipGetLastError(), "k_fd_gate launch");
+      // the perturbations' own inputs, for the full pipeline over them: the gate's range,
+      // empty when no centre has rows
+      hipLaunchKernelGGL(k_fd_expand, dim3((ninst - nA + 255)/256), dim3(256), 0, c->stream,
+                         c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, layout,
+                         (int*)nullptr, nA, ninst, (const int*)(c->fdflag + 1));
+      FDCHECK(hipGetLastError(), "k_fd_expand (fall-back) launch");
       rc = launch_inverse(c, (int)(ninst - nA), nullptr, nullptr, nullptr, nullptr,
                           mjhipSTAGE_NONE, nullptr, 0, skipsensor, c->fdflag + 1);
       if (rc) return rc;
