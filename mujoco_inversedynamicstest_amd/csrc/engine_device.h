@@ -5391,12 +5391,21 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
     for (int k = 0; k < 5; k++) fri[k] = d.con_friction[5*i+k];
     const int rp = dim > 1 ? 3 : 1;
     SP<S> J = d.efc_J + adr0;                // row k's entry p at J[k*NV + p]
-    for (int p = 0; p < NV; p++) {
-      const int j = sparse ? chain[p] : p;
-      const int bj = m.dof_bodyid[j];
-      const bool in1 = ancestorOrSelf(m, bj, b1), in2 = ancestorOrSelf(m, bj, b2);
-      double cj[6] = {0, 0, 0, 0, 0, 0};
-      if (in1 || in2) {
+    // eight dofs at a time: their loads (chain, cdof) are issued before the chunk's J stores,
+    // so each chunk waits once for the stores before it instead of once per dof (the device
+    // orders a load after the older stores it cannot prove disjoint)
+    constexpr int CH = 8;
+    for (int p0 = 0; p0 < NV; p0 += CH) {
+      double cj[CH][6];
+#pragma unroll
+      for (int u = 0; u < CH; u++) {
+        for (int r = 0; r < 6; r++) cj[u][r] = 0;
+        const int p = p0 + u;
+        if (p >= NV) continue;
+        const int j = sparse ? chain[p] : p;
+        const int bj = m.dof_bodyid[j];
+        const bool in1 = ancestorOrSelf(m, bj, b1), in2 = ancestorOrSelf(m, bj, b2);
+        if (!(in1 || in2)) continue;
         SP<S> cdof = d.cdof + 6*j;
         // mj_jac rows for this dof (engine_support.c:389-441), zero off the chain
         double jp1[3] = {0, 0, 0}, jp2[3] = {0, 0, 0}, tmp[3];
@@ -5415,7 +5424,7 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
             double f = frame[3*r+k];
             if (f) acc += jd[k]*f;
           }
-          cj[r] = acc;
+          cj[u][r] = acc;
         }
         if (dim > 3) {
           double jr1[3] = {0, 0, 0}, jr2[3] = {0, 0, 0};
@@ -5428,19 +5437,24 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
               double f = frame[3*r+k];
               if (f) acc += jdr[k]*f;
             }
-            cj[3+r] = acc;
+            cj[u][3+r] = acc;
           }
         }
       }
-      if (dim == 1) {
-        J[p] = cj[0];
-      } else if (elliptic) {
-        for (int k = 0; k < dim; k++) J[k*NV + p] = cj[k];
-      } else {
-        for (int k = 1; k < dim; k++) {
-          double f = fri[k-1];
-          J[(2*(k-1))*NV + p] = cj[0] + cj[k]*f;
-          J[(2*(k-1)+1)*NV + p] = cj[0] + cj[k]*(-f);
+#pragma unroll
+      for (int u = 0; u < CH; u++) {
+        const int p = p0 + u;
+        if (p >= NV) continue;
+        if (dim == 1) {
+          J[p] = cj[u][0];
+        } else if (elliptic) {
+          for (int k = 0; k < dim; k++) J[k*NV + p] = cj[u][k];
+        } else {
+          for (int k = 1; k < dim; k++) {
+            double f = fri[k-1];
+            J[(2*(k-1))*NV + p] = cj[u][0] + cj[u][k]*f;
+            J[(2*(k-1)+1)*NV + p] = cj[u][0] + cj[u][k]*(-f);
+          }
         }
       }
     }
