@@ -59,17 +59,17 @@ def spawn_ranks(gpus: int) -> int:
   return subprocess.call(cmd)
 
 
-def pmc_traffic(eng, m, model, count):
+def pmc_traffic(eng, m, model, count, name="pmc_traffic.json"):
   """HBM bytes per launch from the newest committed PMC summary (tools/pmc.sh +
   tools/pmc_summary.py) whose kernels were built from the same generated source as the one
-  this run launches (matched by codegen.source_hash, not by name), else None."""
+  this run launches (matched by codegen.source_hash, not by name), else None. Config 4's
+  summary (pmc_traffic_c4.json) is per eval at its own batch and row counts."""
   import glob
   from mujoco_inversedynamicstest_amd import codegen
   if not eng.fast_kernel:
     return None, None
   sha = codegen.source_hash(m, eng.fast_kernel)
-  for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", "pmc_traffic.json")),
-                     reverse=True):
+  for path in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*", name)), reverse=True):
     rec = json.load(open(path))
     if rec.get("model") == model and rec.get("source_sha") == sha:
       per_eval = rec["traffic_bytes_per_eval"]
@@ -319,6 +319,7 @@ def other_config(args):
   base = engine.output_bytes_per_eval(m) * B
   extra = engine.constraint_bytes(m, nefc.sum(), ncon.sum(), B)
   achieved = (base + extra) / (kernel_ms * 1e-3) / 1e9
+  traffic, traffic_src = pmc_traffic(eng, m, "humanoid_contact", B, "pmc_traffic_c4.json")
   rec = {"metric": "mj_inverse evals/sec, config 4 (contacts on)", "value": B / dt,
          "unit": "evals/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": dt * 1e3,
          "kernel_ms": kernel_ms, "dtype": "f64",
@@ -330,7 +331,9 @@ def other_config(args):
          "ncon_hist": np.bincount(ncon).tolist(), "nefc_max": int(nefc.max()),
          "nefc_mean": float(nefc.mean()),
          "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBPS,
-                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": None,
+                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
+                      "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
+                      "traffic_ratio": (traffic / (base + extra)) if traffic else None,
                       "algorithmic_bytes_per_launch": base + extra,
                       "bytes_detail": {"b_eval_per_instance": engine.output_bytes_per_eval(m),
                                        "rows": int(nefc.sum()), "contacts": int(ncon.sum()),

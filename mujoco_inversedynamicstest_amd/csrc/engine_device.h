@@ -6626,14 +6626,32 @@ MJH_HD void makeConstraint(const mjhipModel& m, const Lane<S>& d, int* status) {
 }
 
 // mj_referenceConstraint :2362-2375 (efc_vel = mj_mulJacVec, dense or sparse)
+// The row loops here and in invConstraint run eight rows at a time: a chunk's loads are
+// issued before its stores, so it waits once for the stores before it, not once per row
+// (the device orders a load after every older store it cannot prove disjoint). Same
+// operations per row.
+constexpr int kRowChunk = 8;
+
 template <int S>
 MJH_HD void referenceConstraint(const mjhipModel& m, const Lane<S>& d) {
   int nefc = d.efc_count[0];
   const bool sparse = mjh_isSparse(&m);
-  for (int i = 0; i < nefc; i++) {
-    d.efc_vel[i] = sparse ? jacRowDot(d, i, d.qvel) : dot(d.efc_J + i*m.nv, d.qvel, m.nv);
-    d.efc_aref[i] = -d.efc_KBIP[4*i+1]*d.efc_vel[i]
-                    -d.efc_KBIP[4*i]*d.efc_KBIP[4*i+2]*(d.efc_pos[i]-d.efc_margin[i]);
+  for (int i0 = 0; i0 < nefc; i0 += kRowChunk) {
+    double vel[kRowChunk], aref[kRowChunk];
+#pragma unroll
+    for (int u = 0; u < kRowChunk; u++) {
+      const int i = i0 + u;
+      if (i >= nefc) continue;
+      vel[u] = sparse ? jacRowDot(d, i, d.qvel) : dot(d.efc_J + i*m.nv, d.qvel, m.nv);
+      aref[u] = -d.efc_KBIP[4*i+1]*vel[u]
+                -d.efc_KBIP[4*i]*d.efc_KBIP[4*i+2]*(d.efc_pos[i]-d.efc_margin[i]);
+    }
+#pragma unroll
+    for (int u = 0; u < kRowChunk; u++) {
+      if (i0 + u >= nefc) continue;
+      d.efc_vel[i0 + u] = vel[u];
+      d.efc_aref[i0 + u] = aref[u];
+    }
   }
 }
 
@@ -6648,11 +6666,23 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
   }
   int ne = d.efc_count[1], nf = d.efc_count[2];
   const bool sparse = mjh_isSparse(&m);
-  for (int i = 0; i < nefc; i++) {
-    d.jar[i] = (sparse ? jacRowDot(d, i, d.qacc) : dot(d.efc_J + i*nv, d.qacc, nv)) -
+  for (int i0 = 0; i0 < nefc; i0 += kRowChunk) {
+    double jar[kRowChunk];
+#pragma unroll
+    for (int u = 0; u < kRowChunk; u++) {
+      const int i = i0 + u;
+      if (i >= nefc) continue;
+      jar[u] = (sparse ? jacRowDot(d, i, d.qacc) : dot(d.efc_J + i*nv, d.qacc, nv)) -
                d.efc_aref[i];
+    }
+#pragma unroll
+    for (int u = 0; u < kRowChunk; u++) {
+      const int i = i0 + u;
+      if (i >= nefc) continue;
+      d.jar[i] = jar[u];
+      d.efc_force[i] = -d.efc_D[i] * jar[u];
+    }
   }
-  for (int i = 0; i < nefc; i++) d.efc_force[i] = -d.efc_D[i] * d.jar[i];
   for (int i = 0; i < nefc; i++) {
     double jr = d.jar[i];
     if (i < ne) {
@@ -6703,7 +6733,17 @@ MJH_HD void invConstraint(const mjhipModel& m, const Lane<S>& d) {
     }
   }
   if (sparse) {                         // mju_mulMatVecSparse over the rows of efc_JT
-    for (int j = 0; j < nv; j++) d.qfrc_constraint[j] = jacColDot(d, j, d.efc_force);
+    for (int j0 = 0; j0 < nv; j0 += kRowChunk) {
+      double q[kRowChunk];
+#pragma unroll
+      for (int u = 0; u < kRowChunk; u++) {
+        if (j0 + u < nv) q[u] = jacColDot(d, j0 + u, d.efc_force);
+      }
+#pragma unroll
+      for (int u = 0; u < kRowChunk; u++) {
+        if (j0 + u < nv) d.qfrc_constraint[j0 + u] = q[u];
+      }
+    }
   } else {
     mulMatTVec(d.qfrc_constraint, d.efc_J, d.efc_force, nefc, nv);
   }

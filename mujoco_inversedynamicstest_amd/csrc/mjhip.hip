@@ -184,37 +184,50 @@ __global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __
     b = t / m.nv;
     p = 1 + (int)(t % m.nv) + (vel ? m.nv : 0);
   }
+  // every value is formed in registers from the base state and stored once: a load after
+  // the instance's own stores would wait for all of them (one vmcnt counter)
   Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
-  for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos[b*m.nq + k];
-  for (int k = 0; k < m.nv; k++) d.qvel[k] = qvel[b*m.nv + k];
-  for (int k = 0; k < m.nv; k++) d.qacc[k] = qacc[b*m.nv + k];
+  const int nv = m.nv;
+  const long bq = b*m.nq, bv = b*m.nv;
+  const int pa = (p >= 1 && p <= nv) ? p - 1 : -1;          // qacc_i + eps
+  const int pv = (p > nv && p <= 2*nv) ? p - 1 - nv : -1;   // qvel_i + eps
+  for (int k = 0; k < nv; k++) {
+    const double x = qvel[bv + k];
+    d.qvel[k] = k == pv ? x + eps : x;
+  }
+  for (int k = 0; k < nv; k++) {
+    const double x = qacc[bv + k];
+    d.qacc[k] = k == pa ? x + eps : x;
+  }
   if (ctrl) {                          // flg_actuation: the base state's controls
     for (int k = 0; k < m.nu; k++) d.ctrl[k] = ctrl[b*m.nu + k];
   }
-  int nv = m.nv;
-  if (p >= 1 && p <= nv) {
-    d.qacc[p-1] = d.qacc[p-1] + eps;
-  } else if (p > nv && p <= 2*nv) {
-    d.qvel[p-1-nv] = d.qvel[p-1-nv] + eps;
-  } else if (p > 2*nv) {
-    // mj_integratePos(m, qpos, e_i, eps), engine_support.c:1518-1550
-    int i = p - 1 - 2*nv;
-    for (int j = 0; j < m.njnt; j++) {
-      int padr = m.jnt_qposadr[j], vadr = m.jnt_dofadr[j];
-      int t = m.jnt_type[j];
-      if (t == mjhipJNT_FREE) {
-        for (int c = 0; c < 3; c++) d.qpos[padr+c] += eps * (vadr + c == i ? 1.0 : 0.0);
-        padr += 3;
-        vadr += 3;
-        t = mjhipJNT_BALL;
+  if (p <= 2*nv) {
+    for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos[bq + k];
+    return;
+  }
+  // mj_integratePos(m, qpos, e_i, eps), engine_support.c:1518-1550, joint by joint
+  const int i = p - 1 - 2*nv;
+  for (int j = 0; j < m.njnt; j++) {
+    int padr = m.jnt_qposadr[j], vadr = m.jnt_dofadr[j];
+    int t = m.jnt_type[j];
+    if (t == mjhipJNT_FREE) {
+      for (int c = 0; c < 3; c++) {
+        d.qpos[padr+c] = qpos[bq + padr + c] + eps * (vadr + c == i ? 1.0 : 0.0);
       }
-      if (t == mjhipJNT_BALL) {
-        double vel[3] = {vadr == i ? 1.0 : 0.0, vadr + 1 == i ? 1.0 : 0.0,
-                         vadr + 2 == i ? 1.0 : 0.0};
-        mjh::quatIntegrate(d.qpos + padr, vel, eps);
-      } else {
-        d.qpos[padr] += eps * (vadr == i ? 1.0 : 0.0);
-      }
+      padr += 3;
+      vadr += 3;
+      t = mjhipJNT_BALL;
+    }
+    if (t == mjhipJNT_BALL) {
+      double q[4] = {qpos[bq + padr], qpos[bq + padr + 1], qpos[bq + padr + 2],
+                     qpos[bq + padr + 3]};
+      double vel[3] = {vadr == i ? 1.0 : 0.0, vadr + 1 == i ? 1.0 : 0.0,
+                       vadr + 2 == i ? 1.0 : 0.0};
+      mjh::quatIntegrate(q, vel, eps);
+      for (int c = 0; c < 4; c++) d.qpos[padr+c] = q[c];
+    } else {
+      d.qpos[padr] = qpos[bq + padr] + eps * (vadr == i ? 1.0 : 0.0);
     }
   }
 }

@@ -10,6 +10,7 @@
 #             -> gpurun_out/prof_c4/, prof_c5/
 #   prof      rocprofv3 stats of the bench line, then the PMC passes (tools/pmc.sh)
 #   pmc       the PMC passes alone (PMC_ARGS: bench arguments, default the headline)
+#   pmc4      config 4's PMC passes (-> gpurun_out/pmc_traffic_c4.json)
 #   model     tools/bench_model.py $MODEL $B (default humanoid100 4096) under a kernel trace
 #             (SKIP=1|2: mj_inverseSkip(POS|VEL) calls)
 #   store     the store-layout microbenchmark, built from tools/exp_store.hip
@@ -71,6 +72,9 @@ for step in "$@"; do
       cat gpurun_out/pmc_summary.log ;;
     pmc)
       bash tools/pmc.sh || exit 1
+      cat gpurun_out/pmc_summary.log ;;
+    pmc4)                                   # config 4's PMC passes -> pmc_traffic_c4.json
+      PMC_ARGS="--config 4 --steps 3 --warmup 1" PMC_CONFIG="4 4096" bash tools/pmc.sh || exit 1
       cat gpurun_out/pmc_summary.log ;;
     model)
       m=${MODEL:-humanoid100}

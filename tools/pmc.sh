@@ -16,5 +16,10 @@ for group in "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY" "F
   echo "pmc pass $n ($group) rc=$rc"
   [ $rc -ne 0 ] && exit $rc
 done
-python tools/pmc_summary.py gpurun_out gpurun_out/pmc_traffic.json > gpurun_out/pmc_summary.log 2>&1
+if [ -n "${PMC_CONFIG:-}" ]; then        # e.g. PMC_CONFIG="4 4096" with PMC_ARGS="--config 4 ..."
+  python tools/pmc_summary.py gpurun_out gpurun_out/pmc_traffic_c4.json $PMC_CONFIG \
+    > gpurun_out/pmc_summary.log 2>&1
+else
+  python tools/pmc_summary.py gpurun_out gpurun_out/pmc_traffic.json > gpurun_out/pmc_summary.log 2>&1
+fi
 exit $?

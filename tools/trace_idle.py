@@ -1,8 +1,9 @@
-"""Per-step busy and idle time of a rocprofv3 kernel trace (config 5: a step starts at each
-k_fd_expand). Steps whose span is far above the median (warm-up edges, host work between the
-timed regions) are reported separately.
+"""Per-step busy and idle time of a rocprofv3 kernel trace: a step starts at each launch of
+the given kernel (config 5: the position-stage `k_all_humanoid<false>`, once per
+mjd_inverseFD call). Steps whose span is far above the median (warm-up edges, host work
+between the timed regions) are left out.
 
-  python tools/trace_idle.py profiles/r05/head1/c5_kernel_trace.csv [first_kernel_prefix]
+  python tools/trace_idle.py profiles/r05/head2/c5_kernel_trace.csv [first_kernel_prefix]
 """
 import csv
 import statistics
@@ -11,7 +12,7 @@ import sys
 
 def main():
   path = sys.argv[1]
-  first = sys.argv[2] if len(sys.argv) > 2 else "k_fd_expand"
+  first = sys.argv[2] if len(sys.argv) > 2 else "void k_all_humanoid<false>"
   rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
   idx = [i for i, r in enumerate(rows) if r["Kernel_Name"].startswith(first)]
   steps = []
