@@ -1373,7 +1373,9 @@ MJH_HD int colCapsuleBox(RawContact* c, double margin, P1 pos1, M1 mat1, const d
     for (int k = 0; k < 3; k++) sp[k] = pos[k] + halfaxis[k]*(secondpos + bestseg);
     mulMatVec3(w, mat2, sp);
     addTo3(w, pos2);
-    n += rawSphereBox(c + n, margin, w, size1[0], pos2, mat2, size2);
+    // appended by value (a store through c + n would keep c in private memory)
+    RawContact t;
+    if (rawSphereBox(&t, margin, w, size1[0], pos2, mat2, size2)) putRaw(c, n++, t);
   }
   return n;
 }
@@ -3848,7 +3850,8 @@ MJH_HD double geomDistance(const mjhipModel& m, const Lane<S>& d, int geom1, int
     RawContact raw[2];
     const int num = narrowPrimitive(t1, t2, distmax, (const double*)pos1, (const double*)mat1,
                                     size1, (const double*)pos2, (const double*)mat2, size2, raw);
-    for (int i = 0; i < num && i < 2; i++) take(raw[i]);
+    if (num > 0) take(raw[0]);             // constant indices keep raw[] in registers
+    if (num > 1) take(raw[1]);
   }
   if (found) {
     const double sign = flip ? -1 : 1;

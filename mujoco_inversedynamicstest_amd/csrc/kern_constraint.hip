@@ -47,6 +47,18 @@ __global__ __launch_bounds__(64) void k_constraint(mjhipModel m, Mirror mr, int 
 }
 
 
+// XCD-aware block order: the dispatcher deals workgroups round-robin over the 8 XCDs (block
+// b to XCD b % 8), each with its own L2. The logical block returned here numbers the blocks
+// an XCD receives consecutively, so the 64 / IPB workgroups of k_constraint_coop that share
+// one 64-instance mirror block (a mirror line holds 16 instances' copies of one element) run
+// behind one L2 instead of fetching and writing back the same partial lines on eight.
+// A bijection on [0, nb) for any nb.
+__device__ __forceinline__ long xcdBlock(unsigned b, unsigned nb) {
+  constexpr unsigned X = 8;
+  const unsigned x = b % X, per = nb / X, rem = nb % X;
+  return (long)x*per + (x < rem ? x : rem) + b / X;
+}
+
 template <int G, bool CONTACT, bool LIST, bool BOX>
 __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr, int B,
                                                         const int* __restrict__ worklist,
@@ -59,7 +71,8 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
                                                         int* __restrict__ status) {
   constexpr int IPB = 64 / G;               // instances per wave
   const long n = LIST ? (long)*count : (long)B;
-  if ((long)blockIdx.x*IPB >= n) return;    // whole block idle (uniform): before the barriers
+  const long bid = xcdBlock(blockIdx.x, gridDim.x);
+  if (bid*IPB >= n) return;                 // whole block idle (uniform): before the barriers
   __shared__ unsigned long long chain[64], dchain[64];
   __shared__ long s_inst[64 / G];            // the instance of each group (pooled contact rows)
   __shared__ int s_ntask[64 / G];            // its staged contacts with rows
@@ -83,7 +96,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
   const int ngeom = m.ngeom;
   // grid-stride over the instances (a work-list launch uses at most one block per SIMD, so
   // an empty or short list costs few workgroups); the bound is uniform over the block
-  for (long base = (long)blockIdx.x*IPB; base < n; base += (long)gridDim.x*IPB) {
+  for (long base = bid*IPB; base < n; base += (long)gridDim.x*IPB) {
   const long g = base + slot;
   const bool active = g < n;                // uniform within a group
   const long inst = active ? (LIST ? (long)worklist[g] : g) : 0;
