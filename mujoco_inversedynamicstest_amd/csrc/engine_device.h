@@ -319,7 +319,16 @@ struct SP {
 };
 
 // scratch fields (not part of the mjData contract) and constraint rows (the reference's
-// efc_* arena arrays, mjxmacro.h MJDATA_ARENA_POINTERS_SOLVER), per instance
+// efc_* arena arrays, mjxmacro.h MJDATA_ARENA_POINTERS_SOLVER), per instance.
+// XSCC / XSIC mark the instance-contiguous ones: the Jacobian values and column indices,
+// whose element a lane touches next depends on its own rows (rowadr, nonzeros), so lanes at
+// the same step of a loop address unrelated elements. They keep the block storage of the
+// others (64 instances' copies in one block of 64 n elements) but store each instance's n
+// elements consecutively, F[(blk*64 + lane)*n + k], so a lane walks its own cache lines
+// instead of taking 8 bytes of a line shared with 15 instances that are elsewhere in their
+// rows. Where a list is expanded without a definition of its own they read as XSC / XSI.
+#define XSCC(name, n) XSC(name, n)
+#define XSIC(name, n) XSI(name, n)
 #define MJHIP_SCRATCH_FIELDS          \
   XSC(mass_subtree, nbody)            \
   XSC(cacc, 6*nbody)                  \
@@ -345,8 +354,8 @@ struct SP {
   XSC(Dcfrc, mjh_implicit(m)*6*m->nB) \
   XSC(Dcdofdot, mjh_implicit(m)*6*m->nD) \
   XSC(Dtmp, mjh_qDerivStored(m)*6*nv) \
-  XSC(efc_J, mjh_isSparse(m) ? mjh_njCap(m, efc_cap) : (long)efc_cap*nv) \
-  XSC(efc_JT, mjh_njCap(m, efc_cap))   /* sparse mode: the rows' transpose */ \
+  XSCC(efc_J, mjh_isSparse(m) ? mjh_njCap(m, efc_cap) : (long)efc_cap*nv) \
+  XSCC(efc_JT, mjh_njCap(m, efc_cap))   /* sparse mode: the rows' transpose */ \
   XSC(sparse_buf, mjh_isSparse(m)*nv)  /* sparse mode: mju_combineSparse's buffer */ \
   XSC(efc_pos, efc_cap)               \
   XSC(efc_margin, efc_cap)            \
@@ -376,10 +385,10 @@ struct SP {
   XSI(efc_state, efc_cap)             \
   XSI(efc_J_rownnz, mjh_isSparse(m)*efc_cap)   /* sparse mode: compressed rows */ \
   XSI(efc_J_rowadr, mjh_isSparse(m)*efc_cap)   \
-  XSI(efc_J_colind, mjh_njCap(m, efc_cap))      \
+  XSIC(efc_J_colind, mjh_njCap(m, efc_cap))      \
   XSI(efc_JT_rownnz, mjh_isSparse(m)*nv)         \
   XSI(efc_JT_rowadr, mjh_isSparse(m)*nv)         \
-  XSI(efc_JT_colind, mjh_njCap(m, efc_cap))     \
+  XSIC(efc_JT_colind, mjh_njCap(m, efc_cap))     \
   XSI(ten_J_rownnz, mjh_isSparse(m)*m->ntendon) \
   XSI(ten_J_rowadr, mjh_isSparse(m)*m->ntendon) \
   XSI(ten_J_colind, mjh_isSparse(m)*m->ntendon*nv) \
@@ -399,12 +408,20 @@ struct Lane {
   MJHIP_DATA_FIELDS
   MJHIP_DATA_FORWARD
 #undef XD
+#undef XSCC
+#undef XSIC
 #define XSC(name, n) SP<S> name;
+#define XSCC(name, n) SP<1> name;            // instance-contiguous (see the field lists)
   MJHIP_SCRATCH_FIELDS
 #undef XSC
+#undef XSCC
 #define XSI(name, n) SP<S, int> name;
+#define XSIC(name, n) SP<1, int> name;
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
+#undef XSIC
+#define XSCC(name, n) XSC(name, n)
+#define XSIC(name, n) XSI(name, n)
   int efc_cap;
   int con_cap;
   long nj_cap;                               // sparse mode: compressed-row capacity (values)
@@ -2834,7 +2851,26 @@ MJH_HD int ccdEpa(CcdState& st, const CcdMem<S>& M, CcdPoly& P, CcdShape& A,
   for (k = 0; k < st.kmax; k++) {
     pf = f;
     lower = FLTMAX;
-    for (int i = 0; i < P.nlist; i++) {
+    // the closest listed face, scanned in list order (ties keep the earlier face); eight
+    // entries' loads are issued before their compares, so a scan of n faces waits for n / 8
+    // memory round trips rather than 2 n
+    int i = 0;
+    for (; i + 8 <= P.nlist; i += 8) {
+      int g8[8];
+      double d8[8];
+#pragma unroll
+      for (int u = 0; u < 8; u++) g8[u] = M.list()[i + u];
+#pragma unroll
+      for (int u = 0; u < 8; u++) d8[u] = M.fproj(g8[u])[3];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (d8[u] < lower) {
+          f = g8[u];
+          lower = d8[u];
+        }
+      }
+    }
+    for (; i < P.nlist; i++) {
       const int g = M.list()[i];
       const double dg = M.fproj(g)[3];
       if (dg < lower) {
@@ -4674,7 +4710,7 @@ MJH_HD void transmission(const mjhipModel& m, const Lane<S>& d, bool after_only 
               d.jar[r] = w;
               continue;
             }
-            SP<S> J = d.efc_J + (long)r*nv;
+            auto J = d.efc_J + (long)r*nv;
             for (int k = 0; k < nv; k++) moment[k] += J[k]*w;
           }
         } else if (ex == 1) {
@@ -5393,7 +5429,7 @@ MJH_HD void instantiateContact(const mjhipModel& m, const Lane<S>& d, RowCount& 
     for (int k = 0; k < 9; k++) frame[k] = d.con_frame[9*i+k];
     for (int k = 0; k < 5; k++) fri[k] = d.con_friction[5*i+k];
     const int rp = dim > 1 ? 3 : 1;
-    SP<S> J = d.efc_J + adr0;                // row k's entry p at J[k*NV + p]
+    auto J = d.efc_J + adr0;                // row k's entry p at J[k*NV + p]
     // eight dofs at a time: their loads (chain, cdof) are issued before the chunk's J stores,
     // so each chunk waits once for the stores before it instead of once per dof (the device
     // orders a load after the older stores it cannot prove disjoint)
@@ -5639,7 +5675,7 @@ MJH_HD void finishNonContactVA(const mjhipModel& m, const Lane<S>& d, int r, int
 template <int S>
 MJH_HD void finishNonContact(const mjhipModel& m, const Lane<S>& d, int r, int tp, int id,
                              double pos, double margin, double frictionloss) {
-  SP<S> J = d.efc_J + r*m.nv;
+  auto J = d.efc_J + r*m.nv;
   finishNonContactVA(m, d, r, tp, id, pos, margin, frictionloss, dot(J, d.qvel, m.nv),
                      dot(J, d.qacc, m.nv));
 }
@@ -5717,7 +5753,7 @@ MJH_HD void contactRowsFused(const mjhipModel& m, const Lane<S>& d, int i, int n
 
   MJH_TICK(tc1);
   // rows, dof by dof, in blocks of four
-  SP<S> J = d.efc_J + nefc*nv;
+  auto J = d.efc_J + nefc*nv;
   double av[NA][4], aa[NA][4], tv[NA], ta[NA];
   for (int r = 0; r < NA; r++) {
     for (int k = 0; k < 4; k++) av[r][k] = aa[r][k] = 0;
@@ -5894,7 +5930,7 @@ MJH_HD void contactRowsSplit(const mjhipModel& m, const Lane<S>& d, int i, int n
     R = 2*mu*mu*R0;
   }
 
-  SP<S> J = d.efc_J + nefc*nv;
+  auto J = d.efc_J + nefc*nv;
   // one dof's rows into efc_J, returned in Jv (as contactRowsFused forms them)
   auto dofRows = [&](int j, const double* cd, double Jv[ROWS]) MJH_LAMBDA_INLINE {
     const bool in1 = (mask1 >> j) & 1, in2 = (mask2 >> j) & 1;
@@ -6118,7 +6154,7 @@ MJH_HD void instantiateEquality(const mjhipModel& m, const Lane<S>& d, RowCount&
       *status |= MJHIP_INST_CNSTRFULL;
       continue;
     }
-    SP<S> J = d.efc_J + r0*nv;
+    auto J = d.efc_J + r0*nv;
     double cpos[6];
     if (t == mjhipEQ_CONNECT || t == mjhipEQ_WELD) {
       double pos[2][3];
@@ -6239,7 +6275,7 @@ MJH_HD void instantiateEquality(const mjhipModel& m, const Lane<S>& d, RowCount&
       rowImpedance(m, CNSTR_EQUALITY, solref, solimp, ipos, 0, kb);
       for (int k = 0; k < size; k++) {
         const double R = dmax(MINVAL, (1-kb[2])*eqDiagApprox(m, i, k)/kb[2]);
-        SP<S> Jr = J + k*nv;
+        const auto Jr = J + k*nv;
         finishRowFused(d, r0 + k, CNSTR_EQUALITY, kb, R, cpos[k], 0, 0, dot(Jr, d.qvel, nv),
                        dot(Jr, d.qacc, nv));
       }
@@ -6306,7 +6342,7 @@ MJH_HD void instantiateEqualitySparse(const mjhipModel& m, const Lane<S>& d, Row
         *status |= MJHIP_INST_CNSTRFULL;
         continue;
       }
-      SP<S> J = d.efc_J + adr0;
+      auto J = d.efc_J + adr0;
       for (int p = 0; p < NV; p++) {
         const int j = chain[p];
         const int bj = m.dof_bodyid[j];
@@ -8651,12 +8687,20 @@ MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {
   MJHIP_DATA_FIELDS
   MJHIP_DATA_FORWARD
 #undef XD
+#undef XSCC
+#undef XSIC
 #define XSC(name, n) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
+#define XSCC(name, n) d.name.p = mr.name + ((long)blk*64 + lane)*mr.name##_n;
   MJHIP_SCRATCH_FIELDS
 #undef XSC
 #define XSI(name, n) d.name.p = mr.name + ((long)blk*mr.name##_n)*64 + lane;
+#define XSIC(name, n) d.name.p = mr.name + ((long)blk*64 + lane)*mr.name##_n;
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
+#undef XSCC
+#undef XSIC
+#define XSCC(name, n) XSC(name, n)
+#define XSIC(name, n) XSI(name, n)
   d.efc_cap = mr.efc_cap;
   d.con_cap = mr.con_cap;
   d.nj_cap = mr.nj_cap;

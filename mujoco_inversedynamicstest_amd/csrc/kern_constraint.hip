@@ -246,7 +246,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         return false;
       }
       if (r % G == sub) {
-        mjh::SP<64> J = d.efc_J + (long)r*nv;
+        auto J = d.efc_J + (long)r*nv;
         for (int k = 0; k < nv; k++) J[k] = jval(k);
         rowFields(d, r, pos, margin, floss, tp, id);
         // J*qvel, J*qacc from the row's generator and the LDS copies (the values stored in
@@ -274,7 +274,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
     auto putRow = [&](int r, auto jval, double pos, double margin, double floss, int tp, int id)
         MJH_LAMBDA_INLINE {
       if (r >= d.efc_cap) return;
-      mjh::SP<64> J = d.efc_J + (long)r*nv;
+      auto J = d.efc_J + (long)r*nv;
       for (int k = 0; k < nv; k++) J[k] = jval(k);
       rowFields(d, r, pos, margin, floss, tp, id);
       const mjh::FnIdx<decltype(jval)> jv{jval};
@@ -486,7 +486,7 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
         }
 #pragma unroll
         for (int u = 0; u < 8; u++) {
-          mjh::SP<64> Jr = d.efc_J + (long)(r0 + u)*nv;
+          auto Jr = d.efc_J + (long)(r0 + u)*nv;
           x0[u] = f[u] != 0 ? Jr[j0] : 0.0;
           x1[u] = (f[u] != 0 && has1) ? Jr[j1] : 0.0;
         }

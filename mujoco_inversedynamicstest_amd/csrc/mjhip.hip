@@ -20,6 +20,7 @@
 #include <mutex>
 #include <string>
 #include <unordered_map>
+#include <unordered_set>
 #include <utility>
 #include <vector>
 
@@ -408,6 +409,7 @@ struct mjhipContext_ {
   size_t mirror_bytes = 0;
   std::unordered_map<std::string, std::pair<double*, int>> fields;   // name -> (ptr, S)
   std::unordered_map<std::string, std::pair<int*, int>> ifields;   // int scratch fields
+  std::unordered_set<std::string> contig;  // instance-contiguous fields (XSCC / XSIC)
   // staging for row-major host transfers
   double* stage = nullptr;
   size_t stage_bytes = 0;
@@ -705,13 +707,21 @@ MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int cap
 #define XSC(name, n) c->mirror.name = (double*)p; \
   c->fields[#name] = {c->mirror.name, c->mirror.name##_n}; \
   p += align256(sizeof(double) * nblk * 64 * (size_t)c->mirror.name##_n);
+#undef XSCC
+#define XSCC(name, n) c->contig.insert(#name); XSC(name, n)
   MJHIP_SCRATCH_FIELDS
 #undef XSC
 #define XSI(name, n) c->mirror.name = (int*)p; \
   c->ifields[#name] = {c->mirror.name, c->mirror.name##_n}; \
   p += align256(sizeof(int) * nblk * 64 * (size_t)c->mirror.name##_n);
+#undef XSIC
+#define XSIC(name, n) c->contig.insert(#name); XSI(name, n)
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
+#undef XSCC
+#undef XSIC
+#define XSCC(name, n) XSC(name, n)
+#define XSIC(name, n) XSI(name, n)
 #undef MJ_M
   // every failure below releases the partial context through mjhip_contextFree
   auto fail = [&](const char* what) {
@@ -1378,6 +1388,19 @@ MJHIP_API int mjhip_statusDownload(mjhipContext* c, int first, int count, int* d
   return MJHIP_OK;
 }
 
+// element k of instance i (counted from the first fetched block) of an S-element field at
+// tmp[base + k*step]: lane-interleaved (F[(blk*S + k)*64 + lane]) or instance-contiguous
+// (F[(blk*64 + lane)*S + k], the XSCC / XSIC fields)
+static void blockIndex(int i, int S, bool contig, size_t* base, size_t* step) {
+  if (contig) {
+    *base = (size_t)i * S;
+    *step = 1;
+  } else {
+    *base = (size_t)(i / 64) * S * 64 + (i & 63);
+    *step = 64;
+  }
+}
+
 static int find_field(mjhipContext* c, const char* field, double** ptr, int* S) {
   auto it = c->fields.find(field);
   if (it == c->fields.end()) {
@@ -1417,10 +1440,12 @@ MJHIP_API int mjhip_mirrorDownloadInt(mjhipContext* c, const char* field, int fi
   HIPCHECK(hipMemcpyAsync(tmp.data(), p + (size_t)b0*S*64, tmp.size()*sizeof(int),
                           hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
+  const bool ct = c->contig.count(field) > 0;
   for (int i = 0; i < count; i++) {
     int inst = first + i;
-    size_t base = (size_t)(inst/64 - b0) * S * 64 + (inst & 63);
-    for (int k = 0; k < S; k++) dst[(size_t)i*S + k] = tmp[base + (size_t)k*64];
+    size_t base, step;
+    blockIndex(inst - b0*64, S, ct, &base, &step);
+    for (int k = 0; k < S; k++) dst[(size_t)i*S + k] = tmp[base + (size_t)k*step];
   }
   return MJHIP_OK;
 }
@@ -1451,10 +1476,12 @@ MJHIP_API int mjhip_mirrorDownload(mjhipContext* c, const char* field, int first
   HIPCHECK(hipMemcpyAsync(tmp.data(), p + (size_t)b0*S*64, tmp.size()*sizeof(double),
                           hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
+  const bool ct = c->contig.count(field) > 0;
   for (int i = 0; i < count; i++) {
     int inst = first + i;
-    size_t base = (size_t)(inst/64 - b0) * S * 64 + (inst & 63);
-    for (int k = 0; k < S; k++) dst[(size_t)i*S + k] = tmp[base + (size_t)k*64];
+    size_t base, step;
+    blockIndex(inst - b0*64, S, ct, &base, &step);
+    for (int k = 0; k < S; k++) dst[(size_t)i*S + k] = tmp[base + (size_t)k*step];
   }
   return MJHIP_OK;
 }
@@ -1472,10 +1499,12 @@ MJHIP_API int mjhip_mirrorUpload(mjhipContext* c, const char* field, int first, 
   HIPCHECK(hipMemcpyAsync(tmp.data(), p + (size_t)b0*S*64, tmp.size()*sizeof(double),
                           hipMemcpyDeviceToHost, c->stream));
   HIPCHECK(hipStreamSynchronize(c->stream));
+  const bool ct = c->contig.count(field) > 0;
   for (int i = 0; i < count; i++) {
     int inst = first + i;
-    size_t base = (size_t)(inst/64 - b0) * S * 64 + (inst & 63);
-    for (int k = 0; k < S; k++) tmp[base + (size_t)k*64] = src[(size_t)i*S + k];
+    size_t base, step;
+    blockIndex(inst - b0*64, S, ct, &base, &step);
+    for (int k = 0; k < S; k++) tmp[base + (size_t)k*step] = src[(size_t)i*S + k];
   }
   HIPCHECK(hipMemcpyAsync(p + (size_t)b0*S*64, tmp.data(), tmp.size()*sizeof(double),
                           hipMemcpyHostToDevice, c->stream));
@@ -1830,18 +1859,27 @@ MJHIP_API void mjhip_releaseModel(const mjhipModel* m) {
 }
 
 extern "C++" {
-// instance 0 of a mirror field: element k at F[k*64] (block 0, lane 0)
+// instance 0 of a mirror field: element k at F[k*64] (block 0, lane 0), or at F[k] for an
+// instance-contiguous field (contig: the XSCC / XSIC fields)
 template <class T>
-static int put0(mjhipContext* c, T* dev, const T* host, long n) {
+static int put0(mjhipContext* c, T* dev, const T* host, long n, bool contig = false) {
   if (n <= 0 || !dev || !host) return MJHIP_OK;
+  if (contig) {
+    HIPCHECK(hipMemcpyAsync(dev, host, sizeof(T)*n, hipMemcpyHostToDevice, c->stream));
+    return MJHIP_OK;
+  }
   HIPCHECK(hipMemcpy2DAsync(dev, 64*sizeof(T), host, sizeof(T), sizeof(T), n,
                             hipMemcpyHostToDevice, c->stream));
   return MJHIP_OK;
 }
 
 template <class T>
-static int get0(mjhipContext* c, T* host, const T* dev, long n) {
+static int get0(mjhipContext* c, T* host, const T* dev, long n, bool contig = false) {
   if (n <= 0 || !dev || !host) return MJHIP_OK;
+  if (contig) {
+    HIPCHECK(hipMemcpyAsync(host, dev, sizeof(T)*n, hipMemcpyDeviceToHost, c->stream));
+    return MJHIP_OK;
+  }
   HIPCHECK(hipMemcpy2DAsync(host, sizeof(T), dev, 64*sizeof(T), sizeof(T), n,
                             hipMemcpyDeviceToHost, c->stream));
   return MJHIP_OK;
@@ -1910,7 +1948,8 @@ static int put_rows(mjhipContext* c, const mjhipModel* m, const mjhipData* d, in
 #define XE(type, name, w, stage) \
   if (!rc && stage >= lo && stage <= hi) \
     rc = put0(c, c->mirror.name, (const type*)d->name, \
-              (sparse && !strcmp(#name, "efc_J")) ? (long)d->nJ : (long)d->nefc * (w));
+              (sparse && !strcmp(#name, "efc_J")) ? (long)d->nJ : (long)d->nefc * (w), \
+              c->contig.count(#name) > 0);
   MJHIP_DATA_EFC
 #undef XE
   if (!rc && sparse && lo <= 1 && hi >= 1) {
@@ -1921,11 +1960,11 @@ static int put_rows(mjhipContext* c, const mjhipModel* m, const mjhipData* d, in
     if (!rc) rc = put0(c, c->mirror.ten_J_colind, (const int*)d->ten_J_colind, nt*nv);
     if (!rc) rc = put0(c, c->mirror.efc_J_rownnz, (const int*)d->efc_J_rownnz, ne);
     if (!rc) rc = put0(c, c->mirror.efc_J_rowadr, (const int*)d->efc_J_rowadr, ne);
-    if (!rc) rc = put0(c, c->mirror.efc_J_colind, (const int*)d->efc_J_colind, nJ);
-    if (!rc) rc = put0(c, c->mirror.efc_JT, (const double*)d->efc_JT, nJ);
+    if (!rc) rc = put0(c, c->mirror.efc_J_colind, (const int*)d->efc_J_colind, nJ, true);
+    if (!rc) rc = put0(c, c->mirror.efc_JT, (const double*)d->efc_JT, nJ, true);
     if (!rc && ne) rc = put0(c, c->mirror.efc_JT_rownnz, (const int*)d->efc_JT_rownnz, (long)nv);
     if (!rc && ne) rc = put0(c, c->mirror.efc_JT_rowadr, (const int*)d->efc_JT_rowadr, (long)nv);
-    if (!rc) rc = put0(c, c->mirror.efc_JT_colind, (const int*)d->efc_JT_colind, nJ);
+    if (!rc) rc = put0(c, c->mirror.efc_JT_colind, (const int*)d->efc_JT_colind, nJ, true);
   }
 #define XC(type, name, w, stage) \
   if (!rc && stage >= lo && stage <= hi) rc = put0(c, c->mirror.name, (const type*)d->name, \
@@ -1971,7 +2010,8 @@ static int get_rows(mjhipContext* c, const mjhipModel* m, mjhipData* d, int lo, 
 #define XE(type, name, w, stage) \
   if (!rc && stage >= lo && stage <= hi) \
     rc = get0(c, (type*)d->name, (const type*)c->mirror.name, \
-              (sparse && !strcmp(#name, "efc_J")) ? (long)nJ : (long)cnt[0] * (w));
+              (sparse && !strcmp(#name, "efc_J")) ? (long)nJ : (long)cnt[0] * (w), \
+              c->contig.count(#name) > 0);
   MJHIP_DATA_EFC
 #undef XE
   if (!rc && sparse && lo <= 1) {
@@ -1981,11 +2021,11 @@ static int get_rows(mjhipContext* c, const mjhipModel* m, mjhipData* d, int lo, 
     if (!rc) rc = get0(c, (int*)d->ten_J_colind, (const int*)c->mirror.ten_J_colind, nt*nv);
     if (!rc) rc = get0(c, (int*)d->efc_J_rownnz, (const int*)c->mirror.efc_J_rownnz, ne);
     if (!rc) rc = get0(c, (int*)d->efc_J_rowadr, (const int*)c->mirror.efc_J_rowadr, ne);
-    if (!rc) rc = get0(c, (int*)d->efc_J_colind, (const int*)c->mirror.efc_J_colind, (long)nJ);
-    if (!rc) rc = get0(c, (double*)d->efc_JT, (const double*)c->mirror.efc_JT, (long)nJ);
+    if (!rc) rc = get0(c, (int*)d->efc_J_colind, (const int*)c->mirror.efc_J_colind, (long)nJ, true);
+    if (!rc) rc = get0(c, (double*)d->efc_JT, (const double*)c->mirror.efc_JT, (long)nJ, true);
     if (!rc && ne) rc = get0(c, (int*)d->efc_JT_rownnz, (const int*)c->mirror.efc_JT_rownnz, (long)nv);
     if (!rc && ne) rc = get0(c, (int*)d->efc_JT_rowadr, (const int*)c->mirror.efc_JT_rowadr, (long)nv);
-    if (!rc) rc = get0(c, (int*)d->efc_JT_colind, (const int*)c->mirror.efc_JT_colind, (long)nJ);
+    if (!rc) rc = get0(c, (int*)d->efc_JT_colind, (const int*)c->mirror.efc_JT_colind, (long)nJ, true);
   }
 #define XC(type, name, w, stage) \
   if (!rc && lo <= 1 && stage >= lo && stage <= hi) \
