@@ -243,7 +243,7 @@ MJH_HD int mjh_needCcd(const mjhipModel* m) {
   return mjh_needConvex(m) || mjh_needDistanceCcd(m);
 }
 MJH_HD int mjh_ccdDoubles(const mjhipModel* m) {
-  return mjh_needCcd(m) ? 72 + 9*(5 + m->opt.ccd_iterations) + 4*mjh_ccdFaceCap(m) : 0;
+  return mjh_needCcd(m) ? 72 + 9*(5 + m->opt.ccd_iterations) + 5*mjh_ccdFaceCap(m) : 0;
 }
 MJH_HD int mjh_ccdInts(const mjhipModel* m) {
   return mjh_needCcd(m) ? 13*mjh_ccdFaceCap(m) : 0;
@@ -1975,6 +1975,9 @@ struct CcdMem {
   MJH_HD SP<S> wrk(int k) const { return x + 36 + 9*k; }
   MJH_HD SP<S> vtx(int k) const { return x + 72 + 9*k; }
   MJH_HD SP<S> fproj(int f) const { return x + 72 + 9*nvmax + 4*f; }
+  // the listed faces' distances, parallel to list(): the closest-face scan reads both
+  // arrays in order instead of chasing each entry's face
+  MJH_HD SP<S> listd() const { return x + 72 + 9*nvmax + 4*cap; }
   MJH_HD SP<S, int> fint(int f) const { return i + 7*f; }   // vi[0..2], adj[3..5], slot[6]
   MJH_HD SP<S, int> list() const { return i + 7*cap; }
   MJH_HD SP<S, int> hface() const { return i + 8*cap; }
@@ -2548,9 +2551,10 @@ MJH_HD int ccdAddVertex(const CcdMem<S>& M, CcdPoly& P, SP<S> v) {
 }
 
 // epaSupport (:328-353)
+// (w, when given, receives the vertex's Minkowski point from registers)
 template <int S>
 MJH_HD int ccdNewVertex(const CcdMem<S>& M, CcdPoly& P, CcdShape& A, CcdShape& B,
-                        const double d[3], double dn) {
+                        const double d[3], double dn, double* w = nullptr) {
   double dir[3] = {1, 0, 0}, ndir[3] = {-1, 0, 0};
   if (dn > MINVAL) {
     dir[0] = d[0] / dn;
@@ -2558,7 +2562,13 @@ MJH_HD int ccdNewVertex(const CcdMem<S>& M, CcdPoly& P, CcdShape& A, CcdShape& B
     dir[2] = d[2] / dn;
     scl3(ndir, dir, -1);
   }
-  ccdSupport(M.vtx(P.nvtx), A, B, dir, ndir);
+  double v[9];
+  ccdSupport(v, A, B, dir, ndir);
+  SP<S> t = M.vtx(P.nvtx);
+  for (int k = 0; k < 9; k++) t[k] = v[k];
+  if (w) {
+    w[0] = v[0]; w[1] = v[1]; w[2] = v[2];
+  }
   return P.nvtx++;
 }
 
@@ -2584,6 +2594,7 @@ template <int S>
 MJH_HD void ccdListAll(const CcdMem<S>& M, CcdPoly& P, int n) {
   for (int i = 0; i < n; i++) {
     M.list()[i] = i;
+    M.listd()[i] = M.fproj(i)[3];
     M.fint(i)[6] = i;
   }
   P.nlist = n;
@@ -2768,7 +2779,9 @@ MJH_HD void ccdUnlist(const CcdMem<S>& M, CcdPoly& P, int f) {
   const int slot = fi[6];
   if (slot >= 0) {
     const int moved = M.list()[--P.nlist];
+    const double md = M.listd()[P.nlist];
     M.list()[slot] = moved;
+    M.listd()[slot] = md;
     M.fint(moved)[6] = slot;
   }
   fi[6] = -2;
@@ -2793,42 +2806,86 @@ MJH_HD bool ccdSees(const CcdMem<S>& M, int f, const double w[3]) {
 // horizon (:1217-1295): the depth-first search of horizonRec with an explicit stack of
 // (face, entry edge, next k); a neighbour that does not see w is a horizon edge, one that
 // does is deleted and searched, in the recursion's order. false: more horizon edges than the
-// reference's horizon arrays hold, or the stack outgrew the face capacity
+// reference's horizon arrays hold, or the stack outgrew the face capacity.
+// The polytope lives in memory, where a load issued after a store waits for it: the frame
+// being searched stays in registers (only its parents go to the stack), a face's vertices,
+// neighbours and projection never change during the search and are loaded with its list
+// slot in one batch, so a step of the search costs one memory round trip.
 template <int S>
 MJH_HD bool ccdHorizon(const CcdMem<S>& M, CcdPoly& P, int f0, const double w[3], int hmax) {
   SP<S, int> stk = M.stack();
   SP<S, int> hf = M.hface(), he = M.hedge();
-  ccdUnlist(M, P, f0);
+  // face x: fi[0..6] (vertices, neighbours, list slot) and fp[0..3] (projection)
+  auto loadFace = [&](int x, int fi[7], double fp[4]) MJH_LAMBDA_INLINE {
+    SP<S, int> F = M.fint(x);
+    SP<S> Q = M.fproj(x);
+    for (int q = 0; q < 7; q++) fi[q] = F[q];
+    for (int q = 0; q < 4; q++) fp[q] = Q[q];
+  };
+  auto sees = [&](const double fp[4]) MJH_LAMBDA_INLINE {
+    return fp[0]*w[0] + fp[1]*w[1] + fp[2]*w[2] >= fp[3]*fp[3];
+  };
+  auto edgeOf = [&](const int fi[7], int v) MJH_LAMBDA_INLINE {
+    return fi[0] == v ? 0 : (fi[1] == v ? 1 : 2);
+  };
+  // deleteFace with the face's list slot already loaded
+  auto unlist = [&](int x, int slot) MJH_LAMBDA_INLINE {
+    if (slot >= 0) {
+      const int moved = M.list()[--P.nlist];
+      const double md = M.listd()[P.nlist];
+      M.list()[slot] = moved;
+      M.listd()[slot] = md;
+      M.fint(moved)[6] = slot;
+    }
+    M.fint(x)[6] = -2;
+  };
+  int a0[7];
+  double p0[4];
+  loadFace(f0, a0, p0);
+  unlist(f0, a0[6]);
   for (int k0 = 0; k0 < 3; k0++) {
-    const int g = M.fint(f0)[3 + k0];
-    const int ge = ccdEdgeOf(M, g, M.fint(f0)[(k0 + 1) % 3]);
-    if (k0 > 0 && M.fint(g)[6] <= -2) continue;
-    if (!ccdSees(M, g, w)) {
+    const int g = a0[3 + k0];
+    int gi[7];
+    double gp[4];
+    loadFace(g, gi, gp);                   // after the previous searches' deletions
+    const int ge = edgeOf(gi, a0[(k0 + 1) % 3]);
+    if (k0 > 0 && gi[6] <= -2) continue;
+    if (!sees(gp)) {
       if (P.nh >= hmax) return false;
       hf[P.nh] = g; he[P.nh] = ge; P.nh++;
       continue;
     }
-    ccdUnlist(M, P, g);
-    int top = 0;
-    stk[0] = g; stk[1] = ge; stk[2] = 1;
-    while (top >= 0) {
-      SP<S, int> fr = stk + 3*top;
-      const int f = fr[0], e = fr[1], k = fr[2];
+    unlist(g, gi[6]);
+    int top = 0;                            // frames below the current one on the stack
+    int f = g, e = ge, k = 1;
+    int fa[7];
+    for (int q = 0; q < 7; q++) fa[q] = gi[q];
+    while (true) {
       if (k == 3) {
+        if (top == 0) break;
         top--;
+        SP<S, int> fr = stk + 3*top;
+        f = fr[0]; e = fr[1]; k = fr[2];
+        SP<S, int> F = M.fint(f);
+        for (int q = 0; q < 6; q++) fa[q] = F[q];
         continue;
       }
-      fr[2] = k + 1;
       const int i = (e + k) % 3;
-      const int h = M.fint(f)[3 + i];
-      if (M.fint(h)[6] > -2) {
-        const int hge = ccdEdgeOf(M, h, M.fint(f)[(i + 1) % 3]);
-        if (ccdSees(M, h, w)) {
-          ccdUnlist(M, P, h);
+      k++;
+      const int h = fa[3 + i];
+      int hi[7];
+      double hp[4];
+      loadFace(h, hi, hp);
+      if (hi[6] > -2) {
+        const int hge = edgeOf(hi, fa[(i + 1) % 3]);
+        if (sees(hp)) {
+          unlist(h, hi[6]);
           if (3*(top + 2) > 3*M.cap) return false;
+          SP<S, int> fr = stk + 3*top;      // the parent, resumed at its next k
+          fr[0] = f; fr[1] = e; fr[2] = k;
           top++;
-          SP<S, int> nf = stk + 3*top;
-          nf[0] = h; nf[1] = hge; nf[2] = 1;
+          f = h; e = hge; k = 1;
+          for (int q = 0; q < 7; q++) fa[q] = hi[q];
         } else {
           if (P.nh >= hmax) return false;
           hf[P.nh] = h; he[P.nh] = hge; P.nh++;
@@ -2851,28 +2908,29 @@ MJH_HD int ccdEpa(CcdState& st, const CcdMem<S>& M, CcdPoly& P, CcdShape& A,
   for (k = 0; k < st.kmax; k++) {
     pf = f;
     lower = FLTMAX;
-    // the closest listed face, scanned in list order (ties keep the earlier face); eight
-    // entries' loads are issued before their compares, so a scan of n faces waits for n / 8
-    // memory round trips rather than 2 n
+    // the closest listed face, scanned in list order (ties keep the earlier face) over the
+    // list and its parallel distances (listd): sixteen entries' loads are issued before
+    // their compares, so a scan of n faces waits for n / 16 memory round trips
     int i = 0;
-    for (; i + 8 <= P.nlist; i += 8) {
-      int g8[8];
-      double d8[8];
+    for (; i + 16 <= P.nlist; i += 16) {
+      int g16[16];
+      double d16[16];
 #pragma unroll
-      for (int u = 0; u < 8; u++) g8[u] = M.list()[i + u];
+      for (int u = 0; u < 16; u++) {
+        g16[u] = M.list()[i + u];
+        d16[u] = M.listd()[i + u];
+      }
 #pragma unroll
-      for (int u = 0; u < 8; u++) d8[u] = M.fproj(g8[u])[3];
-#pragma unroll
-      for (int u = 0; u < 8; u++) {
-        if (d8[u] < lower) {
-          f = g8[u];
-          lower = d8[u];
+      for (int u = 0; u < 16; u++) {
+        if (d16[u] < lower) {
+          f = g16[u];
+          lower = d16[u];
         }
       }
     }
     for (; i < P.nlist; i++) {
       const int g = M.list()[i];
-      const double dg = M.fproj(g)[3];
+      const double dg = M.listd()[i];
       if (dg < lower) {
         f = g;
         lower = dg;
@@ -2889,8 +2947,7 @@ MJH_HD int ccdEpa(CcdState& st, const CcdMem<S>& M, CcdPoly& P, CcdShape& A,
       st.unsupported = 1;
       return -1;
     }
-    const int wi = ccdNewVertex(M, P, A, B, fp, lower);
-    ccdLoad3(w, M.vtx(wi));
+    const int wi = ccdNewVertex(M, P, A, B, fp, lower, w);
     const double up = (fp[0]*w[0] + fp[1]*w[1] + fp[2]*w[2]) / lower;
     if (up < upper) upper = up;
     if (upper - lower < st.tol) break;
@@ -2908,21 +2965,64 @@ MJH_HD int ccdEpa(CcdState& st, const CcdMem<S>& M, CcdPoly& P, CcdShape& A,
       st.unsupported = 1;
       return -1;
     }
-    for (int i = 0; i < ne; i++) {
-      const int cur = nf + i, prev = i ? cur - 1 : nf + ne - 1, next = nf + (i + 1) % ne;
-      const int hfi = M.hface()[i], e = M.hedge()[i];
-      SP<S, int> H = M.fint(hfi);
-      const int a = H[e], b = H[(e + 1) % 3];
-      H[3 + e] = cur;
-      const double dd = ccdAttach(M, P, wi, b, a, prev, hfi, next);
-      if (dd == 0) {
-        f = -1;
-        break;
+    // the new faces (attachFace per horizon edge, in order), eight edges at a time: what
+    // they read (the horizon faces' vertices, the vertices' points) never changes here, so
+    // it is loaded before the chunk's stores; a degenerate face ends the search (f = -1,
+    // after which the polytope is not read again)
+    for (int i0 = 0; i0 < ne && f >= 0; i0 += 8) {
+      const int cnt = ne - i0 < 8 ? ne - i0 : 8;
+      int hfi[8], he8[8], a8[8], b8[8];
+      double va[8][3], vb[8][3];
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (u < cnt) {
+          hfi[u] = M.hface()[i0 + u];
+          he8[u] = M.hedge()[i0 + u];
+        }
       }
-      if (dd >= lower && dd <= upper) {
-        const int s = P.nlist++;
-        M.list()[s] = P.nface - 1;
-        M.fint(P.nface - 1)[6] = s;
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (u < cnt) {
+          SP<S, int> H = M.fint(hfi[u]);
+          a8[u] = H[he8[u]];
+          b8[u] = H[(he8[u] + 1) % 3];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (u < cnt) {
+          ccdLoad3(va[u], M.vtx(a8[u]));
+          ccdLoad3(vb[u], M.vtx(b8[u]));
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < 8; u++) {
+        if (u >= cnt) break;
+        const int i = i0 + u;
+        const int cur = nf + i, prev = i ? cur - 1 : nf + ne - 1, next = nf + (i + 1) % ne;
+        M.fint(hfi[u])[3 + he8[u]] = cur;
+        // attachFace(wi, b, a, prev, hfi, next) with its vertices from registers
+        const int nfc = P.nface++;
+        SP<S, int> fi = M.fint(nfc);
+        fi[0] = wi; fi[1] = b8[u]; fi[2] = a8[u]; fi[3] = prev; fi[4] = hfi[u]; fi[5] = next;
+        double pr[3], dd = 0;
+        if (!ccdProjPlane(pr, va[u], vb[u], w)) {
+          SP<S> fq = M.fproj(nfc);
+          fq[0] = pr[0]; fq[1] = pr[1]; fq[2] = pr[2];
+          dd = sqrt(pr[0]*pr[0] + pr[1]*pr[1] + pr[2]*pr[2]);
+          fq[3] = dd;
+          fi[6] = -1;
+        }
+        if (dd == 0) {
+          f = -1;
+          break;
+        }
+        if (dd >= lower && dd <= upper) {
+          const int s = P.nlist++;
+          M.list()[s] = nfc;
+          M.listd()[s] = dd;
+          fi[6] = s;
+        }
       }
     }
     P.nh = 0;
