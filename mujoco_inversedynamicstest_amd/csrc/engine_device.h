@@ -357,34 +357,34 @@ struct SP {
   XSCC(efc_J, mjh_isSparse(m) ? mjh_njCap(m, efc_cap) : (long)efc_cap*nv) \
   XSCC(efc_JT, mjh_njCap(m, efc_cap))   /* sparse mode: the rows' transpose */ \
   XSC(sparse_buf, mjh_isSparse(m)*nv)  /* sparse mode: mju_combineSparse's buffer */ \
-  XSC(efc_pos, efc_cap)               \
-  XSC(efc_margin, efc_cap)            \
-  XSC(efc_frictionloss, efc_cap)      \
-  XSC(efc_diagApprox, efc_cap)        \
-  XSC(efc_KBIP, 4*efc_cap)            \
-  XSC(efc_D, efc_cap)                 \
-  XSC(efc_R, efc_cap)                 \
-  XSC(efc_vel, efc_cap)               \
-  XSC(efc_aref, efc_cap)              \
-  XSC(efc_force, efc_cap)             \
-  XSC(jar, efc_cap)                   \
-  XSC(con_dist, con_cap)              \
-  XSC(con_pos, 3*con_cap)             \
-  XSC(con_frame, 9*con_cap)           \
-  XSC(con_includemargin, con_cap)     \
-  XSC(con_friction, 5*con_cap)        \
-  XSC(con_solref, 2*con_cap)          \
-  XSC(con_solreffriction, 2*con_cap)  \
-  XSC(con_solimp, 5*con_cap)          \
-  XSC(con_mu, con_cap)                \
+  XSCC(efc_pos, efc_cap)               \
+  XSCC(efc_margin, efc_cap)            \
+  XSCC(efc_frictionloss, efc_cap)      \
+  XSCC(efc_diagApprox, efc_cap)        \
+  XSCC(efc_KBIP, 4*efc_cap)            \
+  XSCC(efc_D, efc_cap)                 \
+  XSCC(efc_R, efc_cap)                 \
+  XSCC(efc_vel, efc_cap)               \
+  XSCC(efc_aref, efc_cap)              \
+  XSCC(efc_force, efc_cap)             \
+  XSCC(jar, efc_cap)                   \
+  XSCC(con_dist, con_cap)              \
+  XSCC(con_pos, 3*con_cap)             \
+  XSCC(con_frame, 9*con_cap)           \
+  XSCC(con_includemargin, con_cap)     \
+  XSCC(con_friction, 5*con_cap)        \
+  XSCC(con_solref, 2*con_cap)          \
+  XSCC(con_solreffriction, 2*con_cap)  \
+  XSCC(con_solimp, 5*con_cap)          \
+  XSCC(con_mu, con_cap)                \
   XSC(ccd, mjh_ccdDoubles(m))         /* native convex solver (mjh::CcdMem) */
 
 #define MJHIP_SCRATCH_INT_FIELDS      \
-  XSI(efc_type, efc_cap)              \
-  XSI(efc_id, efc_cap)                \
-  XSI(efc_state, efc_cap)             \
-  XSI(efc_J_rownnz, mjh_isSparse(m)*efc_cap)   /* sparse mode: compressed rows */ \
-  XSI(efc_J_rowadr, mjh_isSparse(m)*efc_cap)   \
+  XSIC(efc_type, efc_cap)              \
+  XSIC(efc_id, efc_cap)                \
+  XSIC(efc_state, efc_cap)             \
+  XSIC(efc_J_rownnz, mjh_isSparse(m)*efc_cap)   /* sparse mode: compressed rows */ \
+  XSIC(efc_J_rowadr, mjh_isSparse(m)*efc_cap)   \
   XSIC(efc_J_colind, mjh_njCap(m, efc_cap))      \
   XSI(efc_JT_rownnz, mjh_isSparse(m)*nv)         \
   XSI(efc_JT_rowadr, mjh_isSparse(m)*nv)         \
@@ -396,10 +396,10 @@ struct SP {
   XSI(nJ, mjh_isSparse(m))            /* sparse mode: nonzeros of efc_J */ \
   XSI(efc_count, 4)                   /* nefc, ne, nf, nl */ \
   XSI(con_count, 1)                   /* ncon */ \
-  XSI(con_dim, con_cap)               \
-  XSI(con_geom, 2*con_cap)            \
-  XSI(con_exclude, con_cap)           \
-  XSI(con_efc_address, con_cap)       \
+  XSIC(con_dim, con_cap)               \
+  XSIC(con_geom, 2*con_cap)            \
+  XSIC(con_exclude, con_cap)           \
+  XSIC(con_efc_address, con_cap)       \
   XSI(ccdi, mjh_ccdInts(m))
 
 template <int S>
@@ -7789,7 +7789,7 @@ MJH_HD void rnePostConstraint(const mjhipModel& m, const Lane<S>& d) {
         lfrc[k+1] = (d.efc_force[adr + 2*k] - d.efc_force[adr + 2*k + 1]) * d.con_friction[5*i + k];
       }
     }
-    SP<S> frame = d.con_frame + 9*i;
+    auto frame = d.con_frame + 9*i;
     mulMatTVec3(cfrc, frame, lfrc + 3);
     double t[3];
     mulMatTVec3(t, frame, lfrc);

@@ -410,6 +410,7 @@ struct mjhipContext_ {
   std::unordered_map<std::string, std::pair<double*, int>> fields;   // name -> (ptr, S)
   std::unordered_map<std::string, std::pair<int*, int>> ifields;   // int scratch fields
   std::unordered_set<std::string> contig;  // instance-contiguous fields (XSCC / XSIC)
+  std::unordered_set<const void*> contig_ptr;   // and their device storage
   // staging for row-major host transfers
   double* stage = nullptr;
   size_t stage_bytes = 0;
@@ -708,14 +709,16 @@ MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int cap
   c->fields[#name] = {c->mirror.name, c->mirror.name##_n}; \
   p += align256(sizeof(double) * nblk * 64 * (size_t)c->mirror.name##_n);
 #undef XSCC
-#define XSCC(name, n) c->contig.insert(#name); XSC(name, n)
+#define XSCC(name, n) c->contig.insert(#name); \
+  if (c->mirror.name##_n > 0) c->contig_ptr.insert(p); XSC(name, n)
   MJHIP_SCRATCH_FIELDS
 #undef XSC
 #define XSI(name, n) c->mirror.name = (int*)p; \
   c->ifields[#name] = {c->mirror.name, c->mirror.name##_n}; \
   p += align256(sizeof(int) * nblk * 64 * (size_t)c->mirror.name##_n);
 #undef XSIC
-#define XSIC(name, n) c->contig.insert(#name); XSI(name, n)
+#define XSIC(name, n) c->contig.insert(#name); \
+  if (c->mirror.name##_n > 0) c->contig_ptr.insert(p); XSI(name, n)
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
 #undef XSCC
@@ -1860,11 +1863,11 @@ MJHIP_API void mjhip_releaseModel(const mjhipModel* m) {
 
 extern "C++" {
 // instance 0 of a mirror field: element k at F[k*64] (block 0, lane 0), or at F[k] for an
-// instance-contiguous field (contig: the XSCC / XSIC fields)
+// instance-contiguous field (the XSCC / XSIC fields)
 template <class T>
-static int put0(mjhipContext* c, T* dev, const T* host, long n, bool contig = false) {
+static int put0(mjhipContext* c, T* dev, const T* host, long n) {
   if (n <= 0 || !dev || !host) return MJHIP_OK;
-  if (contig) {
+  if (c->contig_ptr.count((const void*)dev)) {
     HIPCHECK(hipMemcpyAsync(dev, host, sizeof(T)*n, hipMemcpyHostToDevice, c->stream));
     return MJHIP_OK;
   }
@@ -1874,9 +1877,9 @@ static int put0(mjhipContext* c, T* dev, const T* host, long n, bool contig = fa
 }
 
 template <class T>
-static int get0(mjhipContext* c, T* host, const T* dev, long n, bool contig = false) {
+static int get0(mjhipContext* c, T* host, const T* dev, long n) {
   if (n <= 0 || !dev || !host) return MJHIP_OK;
-  if (contig) {
+  if (c->contig_ptr.count((const void*)dev)) {
     HIPCHECK(hipMemcpyAsync(host, dev, sizeof(T)*n, hipMemcpyDeviceToHost, c->stream));
     return MJHIP_OK;
   }
@@ -1948,8 +1951,7 @@ static int put_rows(mjhipContext* c, const mjhipModel* m, const mjhipData* d, in
 #define XE(type, name, w, stage) \
   if (!rc && stage >= lo && stage <= hi) \
     rc = put0(c, c->mirror.name, (const type*)d->name, \
-              (sparse && !strcmp(#name, "efc_J")) ? (long)d->nJ : (long)d->nefc * (w), \
-              c->contig.count(#name) > 0);
+              (sparse && !strcmp(#name, "efc_J")) ? (long)d->nJ : (long)d->nefc * (w));
   MJHIP_DATA_EFC
 #undef XE
   if (!rc && sparse && lo <= 1 && hi >= 1) {
@@ -1960,11 +1962,11 @@ static int put_rows(mjhipContext* c, const mjhipModel* m, const mjhipData* d, in
     if (!rc) rc = put0(c, c->mirror.ten_J_colind, (const int*)d->ten_J_colind, nt*nv);
     if (!rc) rc = put0(c, c->mirror.efc_J_rownnz, (const int*)d->efc_J_rownnz, ne);
     if (!rc) rc = put0(c, c->mirror.efc_J_rowadr, (const int*)d->efc_J_rowadr, ne);
-    if (!rc) rc = put0(c, c->mirror.efc_J_colind, (const int*)d->efc_J_colind, nJ, true);
-    if (!rc) rc = put0(c, c->mirror.efc_JT, (const double*)d->efc_JT, nJ, true);
+    if (!rc) rc = put0(c, c->mirror.efc_J_colind, (const int*)d->efc_J_colind, nJ);
+    if (!rc) rc = put0(c, c->mirror.efc_JT, (const double*)d->efc_JT, nJ);
     if (!rc && ne) rc = put0(c, c->mirror.efc_JT_rownnz, (const int*)d->efc_JT_rownnz, (long)nv);
     if (!rc && ne) rc = put0(c, c->mirror.efc_JT_rowadr, (const int*)d->efc_JT_rowadr, (long)nv);
-    if (!rc) rc = put0(c, c->mirror.efc_JT_colind, (const int*)d->efc_JT_colind, nJ, true);
+    if (!rc) rc = put0(c, c->mirror.efc_JT_colind, (const int*)d->efc_JT_colind, nJ);
   }
 #define XC(type, name, w, stage) \
   if (!rc && stage >= lo && stage <= hi) rc = put0(c, c->mirror.name, (const type*)d->name, \
@@ -2010,8 +2012,7 @@ static int get_rows(mjhipContext* c, const mjhipModel* m, mjhipData* d, int lo, 
 #define XE(type, name, w, stage) \
   if (!rc && stage >= lo && stage <= hi) \
     rc = get0(c, (type*)d->name, (const type*)c->mirror.name, \
-              (sparse && !strcmp(#name, "efc_J")) ? (long)nJ : (long)cnt[0] * (w), \
-              c->contig.count(#name) > 0);
+              (sparse && !strcmp(#name, "efc_J")) ? (long)nJ : (long)cnt[0] * (w));
   MJHIP_DATA_EFC
 #undef XE
   if (!rc && sparse && lo <= 1) {
@@ -2021,11 +2022,11 @@ static int get_rows(mjhipContext* c, const mjhipModel* m, mjhipData* d, int lo, 
     if (!rc) rc = get0(c, (int*)d->ten_J_colind, (const int*)c->mirror.ten_J_colind, nt*nv);
     if (!rc) rc = get0(c, (int*)d->efc_J_rownnz, (const int*)c->mirror.efc_J_rownnz, ne);
     if (!rc) rc = get0(c, (int*)d->efc_J_rowadr, (const int*)c->mirror.efc_J_rowadr, ne);
-    if (!rc) rc = get0(c, (int*)d->efc_J_colind, (const int*)c->mirror.efc_J_colind, (long)nJ, true);
-    if (!rc) rc = get0(c, (double*)d->efc_JT, (const double*)c->mirror.efc_JT, (long)nJ, true);
+    if (!rc) rc = get0(c, (int*)d->efc_J_colind, (const int*)c->mirror.efc_J_colind, (long)nJ);
+    if (!rc) rc = get0(c, (double*)d->efc_JT, (const double*)c->mirror.efc_JT, (long)nJ);
     if (!rc && ne) rc = get0(c, (int*)d->efc_JT_rownnz, (const int*)c->mirror.efc_JT_rownnz, (long)nv);
     if (!rc && ne) rc = get0(c, (int*)d->efc_JT_rowadr, (const int*)c->mirror.efc_JT_rowadr, (long)nv);
-    if (!rc) rc = get0(c, (int*)d->efc_JT_colind, (const int*)c->mirror.efc_JT_colind, (long)nJ, true);
+    if (!rc) rc = get0(c, (int*)d->efc_JT_colind, (const int*)c->mirror.efc_JT_colind, (long)nJ);
   }
 #define XC(type, name, w, stage) \
   if (!rc && lo <= 1 && stage >= lo && stage <= hi) \
