@@ -28,6 +28,9 @@
 #include "fast_kernels.h"
 #include "kernels.h"
 #include "pair_program.h"
+// lane-count variants of the cooperative kernel (kern_constraint.hip), measurement only
+extern template __global__ void k_constraint_coop<8, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
+extern template __global__ void k_constraint_coop<32, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
 #include "post_pass.h"
 
 //==================================== kernels ===============================================
@@ -756,7 +759,10 @@ MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int cap
   // the cooperative constraint kernel's pair program (16 lanes per instance: 8 and 32 were
   // slower, profiles/r02/bench_c4_L*.json; MJHIP_COOP_LANES=0 selects the one-lane
   // k_constraint)
-  if (const char* lanes = getenv("MJHIP_COOP_LANES")) c->coop = atoi(lanes) == 0 ? 0 : 16;
+  if (const char* lanes = getenv("MJHIP_COOP_LANES")) {
+    const int n = atoi(lanes);             // 8 and 32: the contact path's lane-count variants
+    c->coop = n == 0 ? 0 : (n == 8 || n == 32) ? n : 16;
+  }
   if (c->con_cap > 0) {
     // the static collision program (csrc/pair_program.h): the cooperative kernel's pair
     // program, and collision()'s candidate list in every other kernel (Mirror::prog)
@@ -994,6 +1000,8 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
         else MJHIP_LAUNCH_COOP(16, true, false, true);
       } else if (contact) {
         if (list) MJHIP_LAUNCH_COOP(16, true, true, false);
+        else if (c->coop == 8) MJHIP_LAUNCH_COOP(8, true, false, false);
+        else if (c->coop == 32) MJHIP_LAUNCH_COOP(32, true, false, false);
         else MJHIP_LAUNCH_COOP(16, true, false, false);
       } else {
         if (list) MJHIP_LAUNCH_COOP(16, false, true, false);
