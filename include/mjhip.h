@@ -277,7 +277,12 @@ typedef enum mjhipStatus_ {
  * every per-instance field F of size S = d0*d1 is stored as
  *     F[(blk*S + k)*64 + lane],  instance = blk*64 + lane,  k = 0..S-1
  * i.e. 64-instance blocks (one wavefront), component-major inside a block, so one
- * wavefront's access to component k of F is one contiguous 512-byte segment. */
+ * wavefront's access to component k of F is one contiguous 512-byte segment.
+ * The constraint-row, contact and Jacobian fields (efc_* rows and compressed-row arrays,
+ * jar, con_*), which lanes index by their own row or contact counts, are instance-major
+ * inside the same 64-instance blocks instead:
+ *     F[(blk*64 + lane)*S + k]
+ * mjhip_mirrorDownload / mjhip_mirrorUpload hide the difference (one row per instance). */
 #define MJHIP_BLOCK 64
 
 /*---------------------------- library / device ---------------------------------------------*/
