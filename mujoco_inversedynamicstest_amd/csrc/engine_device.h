@@ -3865,9 +3865,11 @@ MJH_HD void collideBoxBox(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
     keep = boxBoxKeep(margin, p1, m1, size1, p2, m2, size2, bbuf);
   } else {
     // the exact capacity holds 24 contacts for every box pair, so this is reached only in a
-    // capped context (mjhip_contextCreateCapped): the instance is flagged CNSTRFULL, as the
-    // reference warns mjWARN_CONTACTFULL, but the pair is dropped whole where the reference
-    // would keep its first contacts up to the cap (the list's tail is this path's scratch)
+    // capped context (mjhip_contextCreateCapped): the instance is flagged CNSTRFULL and the
+    // pair is dropped whole, as the reference drops a pair whose mjContact[mjMAXCONPAIR]
+    // scratch does not fit in the arena (mj_collideGeoms, engine_collision_driver.c:1499-1505,
+    // mjWARN_CONTACTFULL). The threshold differs: the reference's is the arena's free bytes
+    // for 50 contacts, ours the list's tail for this path's 24 (its scratch)
     if (ncon + 24 > d.con_cap) {
       *status |= MJHIP_INST_CNSTRFULL;
       return;
