@@ -412,6 +412,21 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
  * mjhipData's efc_* / con_* buffers with these. */
 MJHIP_API int mjhip_modelCapacity(const mjhipModel* m, int* efc_rows, int* contacts);
 
+/* mjc_ccd (engine_collision_gjk.c:2215-2343; MJAPI, engine_collision_gjk.h:92), the native
+ * GJK/EPA solver, over n geom pairs of the context's model, one device lane per pair. Pair i
+ * is geoms g1[i], g2[i] at the caller's frames pos1/pos2 (n x 3) and mat1/mat2 (n x 9,
+ * row-major geom_xmat), both inflated by margin[i] (mjc_initCCDObj's margin; NULL: 0), with
+ * the mjCCDConfig {max_iterations, tolerance, max_contacts, dist_cutoff}. max_contacts 0 asks
+ * for the distance alone (no penetration recovery), 1 for one contact. Outputs (host arrays):
+ * dist[n] (mjc_ccd's return value), nx[n] (status.nx), x1/x2 (n x 3, status.x1/x2: the
+ * witness points). Status codes as everywhere; MJHIP_ERR_ARG for max_contacts outside
+ * {0, 1}, MJHIP_ERR_MODEL when a pair's polytope outgrew the solver's face capacity. */
+MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g2,
+                             const mjtNum* pos1, const mjtNum* mat1, const mjtNum* pos2,
+                             const mjtNum* mat2, const mjtNum* margin, int max_iterations,
+                             mjtNum tolerance, int max_contacts, mjtNum dist_cutoff,
+                             mjtNum* dist, int* nx, mjtNum* x1, mjtNum* x2);
+
 /* Time `reps` back-to-back launches of the fused inverse kernel on the context's stream
  * with HIP events (device-resident mirror inputs, B instances). Writes the average
  * milliseconds per launch to *ms. Used by bench.py for the roofline figure. */

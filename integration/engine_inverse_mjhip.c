@@ -26,8 +26,9 @@
  * (:2083-2104, mju_superSparse engine_util_sparse.c:520-550, restated below).
  *
  * Models are checked for features the device path does not implement and which mjhipModel
- * does not carry (explicit contact pairs, flexes, plugins):
- * such a model is an mju_error, never a silently different result.
+ * does not carry (flexes, plugins, muscle/user actuator gains and biases, an affine velocity
+ * gain with activation dynamics, SDF geoms; adapter_unsupported): such a model is an
+ * mju_error, never a silently different result. Predefined <contact><pair>s are carried.
  *
  * Build (in the reference tree): drop engine_inverse.c from src/engine/CMakeLists.txt,
  * add this file, add <repo>/include to the include path and link libmjhip.so.

@@ -44,6 +44,7 @@ mj_rne :1969-2023, mj_inverseSkip engine_inverse.c:197-261.
 from __future__ import annotations
 
 import hashlib
+import re
 
 import numpy as np
 
@@ -1283,8 +1284,13 @@ def _perturb_loads(body: str, which: dict) -> str:
     arr, k, rhs = mt.group(2), mt.group(3), mt.group(4)
     return (f"{mt.group(1)}{arr}[{k}] = ({which[arr]} == {k}) ? ({rhs}) + eps : ({rhs});")
   names = "|".join(which)
-  return re.sub(rf"^(\s*)({names})\[(\d+)\] = (.*P_(?:{names})\[\d+\*64\].*);$", sub, body,
-                flags=re.M)
+  out, n = re.subn(rf"^(\s*)({names})\[(\d+)\] = (.*P_(?:{names})\[\d+\*64\].*);$", sub,
+                   body, flags=re.M)
+  # every line that loads a perturbed input must have been rewritten: a load of another shape
+  # would silently leave that Jacobian column unperturbed (zero)
+  loads = len(re.findall(rf"^.*P_(?:{names})\[[^\]]+\](?!\)? ?=[^=]).*$", body, flags=re.M))
+  assert n == loads, f"_perturb_loads: rewrote {n} of {loads} lines loading {sorted(which)}"
+  return out
 
 
 def _gen_acc(M: _Model, store_fields=None) -> str:
@@ -1597,7 +1603,8 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
     # perturbations would write the centre's slot concurrently, so the text is checked too
     textual = set(re.findall(r"P_(\w+)\[[^\]]+\]\)? ?=[^=]", vb)) | \
         set(re.findall(r"MJH_NT_STORE\(P_(\w+)\[", vb))
-    assert textual <= M.va_stored | {"qpos", "qvel", "qacc"}, \
+    # qpos/qvel/qacc are based at the centre instance unless stored (then `own` keeps them)
+    assert textual <= M.va_stored, \
         f"k_vaskip: va stores outside the record: {textual - M.va_stored}"
     # qpos, qvel and qacc are read from the centre too: k_fd_expand writes only the
     # position-stage block, and the perturbed component is added as the loads land (pa / pv:
@@ -1733,15 +1740,45 @@ __global__ __launch_bounds__(64, 1) void k_acc_{name}(Mirror mr, int B,
   return "\n".join(out) + "\n"
 
 
+_TOKEN = re.compile(r'"(?:\\.|[^"\\\n])*"|\'(?:\\.|[^\'\\\n])*\'|//[^\n]*|/\*.*?\*/|\s+',
+                    re.S)
+
+
+def code_text(src: str) -> str:
+  """C/C++ source with comments removed and every whitespace run collapsed to one space
+  (string and character literals kept as written): what the compiler sees, so an edit to a
+  comment or to indentation does not change it."""
+  parts, pos = [], 0
+  for mt in _TOKEN.finditer(src):
+    if mt.start() > pos:
+      parts.append(src[pos:mt.start()])
+    t = mt.group(0)
+    if t[0] in "\"'":
+      parts.append(t)
+    elif parts and parts[-1] != " ":
+      parts.append(" ")
+    pos = mt.end()
+  parts.append(src[pos:])
+  return "".join(parts).strip()
+
+
+# the device sources a generated kernel's translation unit compiles besides its own text
+HASHED_HEADERS = ("engine_device.h", "fast_kernels.h", "kernels.h", "post_pass.h",
+                  "pair_program.h", "kern_constraint.hip")
+
+
 def source_hash(m, name: str) -> str:
   """Identity of the code a kernel of model m named `name` is built from: its generated
-  source and the device header it includes (keys committed PMC summaries to the kernel they
-  measured; a run-time kernel, rt_*, has C linkage)."""
+  source, the device headers it includes and the constraint kernels launched beside it, each
+  with comments and whitespace removed (code_text). Keys committed PMC and rocprof summaries
+  to the kernels they measured, so a comment edit after the final profiles keeps them
+  matched; a run-time kernel, rt_*, has C linkage."""
   import os
-  h = hashlib.sha256(generate(m, name, extern_c=name.startswith("rt_")).encode())
-  with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc",
-                         "engine_device.h"), "rb") as f:
-    h.update(f.read())
+  h = hashlib.sha256(code_text(generate(m, name, extern_c=name.startswith("rt_"))).encode())
+  csrc = os.path.join(os.path.dirname(os.path.abspath(__file__)), "csrc")
+  for f in HASHED_HEADERS:
+    with open(os.path.join(csrc, f), encoding="utf-8") as fh:
+      h.update(code_text(fh.read()).encode())
   return h.hexdigest()[:16]
 
 

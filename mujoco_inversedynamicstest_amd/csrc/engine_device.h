@@ -3061,11 +3061,12 @@ MJH_HD void ccdCenter(double c[3], const CcdShape& s) {
   }
 }
 
-// mjc_ccd (:2215-2343) with max_contacts = 1 and the distance cutoff `cutoff` (0 for
-// mjc_Convex's contacts, the bound for mj_geomDistanceCCD)
+// mjc_ccd (:2215-2343) with max_contacts `maxc` (1: mjc_Convex and mj_geomDistanceCCD; 0: the
+// distance alone, no penetration recovery, mjhip_ccdBatch) and the distance cutoff `cutoff`
+// (0 for mjc_Convex's contacts, the bound for mj_geomDistanceCCD)
 template <int S>
 MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B, int kmax,
-                     double tol, double cutoff) {
+                     double tol, double cutoff, int maxc = 1) {
   ccdCenter(st.x1, A);
   ccdCenter(st.x2, B);
   st.iters = 0;
@@ -3109,11 +3110,17 @@ MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B,
       if (st.dist > st.cutoff) st.dist = mjhipMAXVAL;
       return st.dist;
     }
+    if (!maxc) {                                        // contact not needed
+      st.nx = 0;
+      st.dist = 0;
+      return 0;
+    }
     st.iters = 0;
     ccdCenter(st.x1, A);
     ccdCenter(st.x2, B);
   }
   ccdGjk(st, M, A, B);
+  if (!maxc) return st.dist;                            // no penetration recovery
   if (st.dist <= tol && st.nsimplex > 1) {
     st.dist = 0;
     CcdPoly P{0, 0, 0, 0};
@@ -3147,6 +3154,46 @@ MJH_HD void ccdShape(CcdShape& s, const mjhipModel& m, const Lane<S>& d, int g, 
   for (int k = 0; k < 3; k++) s.size[k] = m.geom_size[3*g + k];
   s.margin = margin;
   ccdMeshData(s, m, g);
+}
+
+// scratch of one standalone mjc_ccd call with max_iterations N (ccdGeneral): the CcdMem
+// layout of the mirror's ccd / ccdi fields with the face capacity 6 N + 6
+MJH_HD long ccdScratchDoubles(int N) { return 72 + 9L*(5 + N) + 5L*(6*N + 6); }
+MJH_HD long ccdScratchInts(int N) { return 13L*(6*N + 6); }
+
+// mjc_ccd (engine_collision_gjk.c:2215-2343, MJAPI) as the reference's own tests call it
+// (engine_collision_gjk_test.cc:62-84 GeomDist, :86-150 Penetration): geoms g1, g2 of m at the
+// given frames, object margin `margin` on both (mjc_initCCDObj), config {N, tol, maxc (0 or 1),
+// cutoff}, contiguous scratch x / xi (ccdScratchDoubles / Ints). out: dist, nx, x1[3], x2[3].
+// Returns 0, or 1 when the polytope outgrew the face capacity (MJHIP_INST_UNSUPPORTED).
+MJH_HD int ccdGeneral(const mjhipModel& m, int g1, int g2, const double* pos1,
+                      const double* mat1, const double* pos2, const double* mat2,
+                      double margin, int N, double tol, int maxc, double cutoff, double* x,
+                      int* xi, double* out) {
+  CcdMem<1> M{{x}, {xi}, 5 + N, 6*N + 6};
+  CcdShape sh[2];
+  const int g[2] = {g1, g2};
+  const double* pos[2] = {pos1, pos2};
+  const double* mat[2] = {mat1, mat2};
+  for (int j = 0; j < 2; j++) {
+    CcdShape& s = sh[j];
+    s.kind = s.gtype = m.geom_type[g[j]];
+    for (int k = 0; k < 3; k++) s.pos[k] = pos[j][k];
+    for (int k = 0; k < 9; k++) s.mat[k] = mat[j][k];
+    for (int k = 0; k < 3; k++) s.size[k] = m.geom_size[3*g[j] + k];
+    s.margin = margin;
+    ccdMeshData(s, m, g[j]);
+  }
+  CcdState st;
+  st.nx = 0;
+  const double dist = ccdRun(st, M, sh[0], sh[1], N, tol, cutoff, maxc);
+  out[0] = dist;
+  out[1] = st.nx;
+  for (int k = 0; k < 3; k++) {
+    out[2 + k] = st.x1[k];
+    out[5 + k] = st.x2[k];
+  }
+  return st.unsupported ? 1 : 0;
 }
 
 // mjc_Convex through mjc_CCDIteration (convex.c:792-819, :915-1001): 0 or 1 contacts

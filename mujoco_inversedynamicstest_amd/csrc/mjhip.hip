@@ -343,6 +343,25 @@ __global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps, int fl
   }
 }
 
+// mjhip_ccdBatch: mjc_ccd on pair i's geoms at its frames (in: 24 doubles per pair, pos1,
+// mat1, pos2, mat2; out: 8 per pair, dist, nx, x1, x2), scratch contiguous per pair
+__global__ __launch_bounds__(64) void k_ccd(mjhipModel m, int n, const int* __restrict__ g1,
+                                            const int* __restrict__ g2,
+                                            const double* __restrict__ in,
+                                            const double* __restrict__ margin, int N,
+                                            double tol, int maxc, double cutoff,
+                                            double* __restrict__ x, int* __restrict__ xi,
+                                            double* __restrict__ out, int* __restrict__ bad) {
+  const int i = blockIdx.x*64 + threadIdx.x;
+  if (i >= n) return;
+  const double* f = in + 24L*i;
+  if (mjh::ccdGeneral(m, g1[i], g2[i], f, f + 3, f + 12, f + 15, margin ? margin[i] : 0.0, N,
+                      tol, maxc, cutoff, x + (long)i*mjh::ccdScratchDoubles(N),
+                      xi + (long)i*mjh::ccdScratchInts(N), out + 8L*i)) {
+    bad[i] = 1;
+  }
+}
+
 // Constraint-free mj_forward over a batch (mjh::forwardSkip). Optional row-major qpos, qvel,
 // ctrl are copied into the mirror first; qfrc_applied / xfrc_applied are read from the
 // mirror; optional row-major qacc is written at the end.
@@ -838,19 +857,26 @@ MJHIP_API int mjhip_contextCreateCapped(const mjhipModel* m, int device, int cap
   return MJHIP_OK;
 }
 
-static void timers_detach(mjhipContext* c);
+static int timers_detach(mjhipContext* c);
+// the one context per process whose accumulator the phase marks may add into: mjh_tbuf is a
+// process-wide device global per unit, so a second context's kernels would add into the
+// first's accumulator
+static mjhipContext* g_timed_ctx = nullptr;
 
 MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   if (!c) return;
   hipSetDevice(c->device);
   if (c->stream) hipStreamSynchronize(c->stream);
+  // the timer pointers go back to null while the stream still exists (timers_attach
+  // synchronizes it); an accumulator some unit may still point at is leaked, not freed
+  const bool detached = !c->tbuf || timers_detach(c) == MJHIP_OK;
+  if (g_timed_ctx == c) g_timed_ctx = nullptr;
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->tev0) hipEventDestroy(c->tev0);
   if (c->tev1) hipEventDestroy(c->tev1);
-  if (c->tbuf) timers_detach(c);
-  hipFree(c->tbuf);
+  if (detached) hipFree(c->tbuf);
   hipFree(c->stage);
   hipFree(c->status);
   hipFree(c->worklist);
@@ -909,6 +935,80 @@ MJHIP_API int mjhip_contextLoadKernel(mjhipContext* c, const void* image, size_t
   c->fast = &c->rt;
   c->wl_parity = 0;                        // the run-time kernel zeroes the counters as the
   return hipMemset(c->worklist, 0, 2 * sizeof(int)) == hipSuccess ? MJHIP_OK : MJHIP_ERR_HIP;
+}
+
+MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g2,
+                             const mjtNum* pos1, const mjtNum* mat1, const mjtNum* pos2,
+                             const mjtNum* mat2, const mjtNum* margin, int max_iterations,
+                             mjtNum tolerance, int max_contacts, mjtNum dist_cutoff,
+                             mjtNum* dist, int* nx, mjtNum* x1, mjtNum* x2) {
+  if (!c || n < 0 || (n && (!g1 || !g2 || !pos1 || !mat1 || !pos2 || !mat2 || !dist || !nx ||
+                            !x1 || !x2)) || max_iterations < 1 || max_contacts < 0 ||
+      max_contacts > 1) {
+    set_error("mjhip_ccdBatch: bad argument (max_contacts must be 0 or 1)");
+    return MJHIP_ERR_ARG;
+  }
+  if (!n) return MJHIP_OK;
+  const int ng = c->hmodel.ngeom;
+  for (int i = 0; i < n; i++) {            // every index the kernel reads, checked here
+    if (g1[i] < 0 || g1[i] >= ng || g2[i] < 0 || g2[i] >= ng) {
+      set_error("mjhip_ccdBatch: geom id out of range at pair %d", i);
+      return MJHIP_ERR_ARG;
+    }
+  }
+  HIPCHECK(hipSetDevice(c->device));
+  const long nd = mjh::ccdScratchDoubles(max_iterations), ni = mjh::ccdScratchInts(max_iterations);
+  std::vector<double> in(24L*n), out(8L*n);
+  for (int i = 0; i < n; i++) {
+    memcpy(&in[24L*i], pos1 + 3L*i, 3*sizeof(double));
+    memcpy(&in[24L*i + 3], mat1 + 9L*i, 9*sizeof(double));
+    memcpy(&in[24L*i + 12], pos2 + 3L*i, 3*sizeof(double));
+    memcpy(&in[24L*i + 15], mat2 + 9L*i, 9*sizeof(double));
+  }
+  // one allocation: inputs, margins, outputs, scratch, then the int arrays
+  const size_t bytes = sizeof(double)*(24L*n + n + 8L*n + nd*n) + sizeof(int)*(2L*n + ni*n + n);
+  char* buf = nullptr;
+  HIPCHECK(hipMalloc((void**)&buf, bytes));
+  double* d_in = (double*)buf;
+  double* d_margin = d_in + 24L*n;
+  double* d_out = d_margin + n;
+  double* d_x = d_out + 8L*n;
+  int* d_g = (int*)(d_x + nd*n);
+  int* d_xi = d_g + 2L*n;
+  int* d_bad = d_xi + ni*n;
+  std::vector<double> mg(n, 0.0);
+  if (margin) memcpy(mg.data(), margin, n*sizeof(double));
+  std::vector<int> bad(n);
+  int rc = MJHIP_OK;
+  auto run = [&]() -> int {
+    HIPCHECK(hipMemcpy(d_in, in.data(), 24L*n*sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d_margin, mg.data(), n*sizeof(double), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d_g, g1, n*sizeof(int), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemcpy(d_g + n, g2, n*sizeof(int), hipMemcpyHostToDevice));
+    HIPCHECK(hipMemset(d_bad, 0, n*sizeof(int)));
+    hipLaunchKernelGGL(k_ccd, dim3((n + 63)/64), dim3(64), 0, c->stream, c->dmodel, n, d_g,
+                       d_g + n, d_in, d_margin, max_iterations, tolerance, max_contacts,
+                       dist_cutoff, d_x, d_xi, d_out, d_bad);
+    HIPCHECK(hipGetLastError());
+    HIPCHECK(hipStreamSynchronize(c->stream));
+    HIPCHECK(hipMemcpy(out.data(), d_out, 8L*n*sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(bad.data(), d_bad, n*sizeof(int), hipMemcpyDeviceToHost));
+    return MJHIP_OK;
+  };
+  rc = run();
+  hipFree(buf);
+  if (rc) return rc;
+  for (int i = 0; i < n; i++) {
+    if (bad[i]) {
+      set_error("mjhip_ccdBatch: pair %d outgrew the solver's polytope capacity", i);
+      return MJHIP_ERR_MODEL;
+    }
+    dist[i] = out[8L*i];
+    nx[i] = (int)out[8L*i + 1];
+    memcpy(x1 + 3L*i, &out[8L*i + 2], 3*sizeof(double));
+    memcpy(x2 + 3L*i, &out[8L*i + 5], 3*sizeof(double));
+  }
+  return MJHIP_OK;
 }
 
 MJHIP_API int mjhip_contextCapacity(const mjhipContext* c) { return c ? c->capacity : 0; }
@@ -1138,16 +1238,12 @@ static int timers_attach(mjhipContext* c, unsigned long long* p) {
   return MJHIP_OK;
 }
 
-// the one context per process whose accumulator the phase marks may add into: mjh_tbuf is a
-// process-wide device global per unit, so a second context's kernels would add into the
-// first's accumulator
-static mjhipContext* g_timed_ctx = nullptr;
-
 // point every mjh_tbuf copy back at null (after the stream's earlier work), so that no kernel
-// adds into an accumulator that is about to be freed
-static void timers_detach(mjhipContext* c) {
-  timers_attach(c, nullptr);
+// adds into an accumulator that is about to be freed; the caller frees it only on success
+static int timers_detach(mjhipContext* c) {
+  const int rc = timers_attach(c, nullptr);
   if (g_timed_ctx == c) g_timed_ctx = nullptr;
+  return rc;
 }
 
 // fold one call's phase-mark sums (engine_device.h MJH_PHASE: slots and wave counts) into
@@ -1202,23 +1298,30 @@ MJHIP_API int mjhip_contextTimers(mjhipContext* c, int enable) {
   HIPCHECK(hipSetDevice(c->device));
   if (!enable) {
     if (c->tbuf) {
-      timers_detach(c);
+      if (const int rc = timers_detach(c)) return rc;   // a unit may still point at it
       HIPCHECK(hipFree(c->tbuf));
       c->tbuf = nullptr;
     }
+    if (g_timed_ctx == c) g_timed_ctx = nullptr;
     return MJHIP_OK;
   }
   if (g_timed_ctx && g_timed_ctx != c) {
     set_error("mjhip_contextTimers: another context of this process is being timed");
     return MJHIP_ERR_ARG;
   }
-  g_timed_ctx = c;
   if (!c->tbuf) {
-    HIPCHECK(hipMalloc((void**)&c->tbuf, MJH_TSLOTS * sizeof(unsigned long long)));
-    HIPCHECK(hipMemset(c->tbuf, 0, MJH_TSLOTS * sizeof(unsigned long long)));
+    unsigned long long* buf = nullptr;
+    HIPCHECK(hipMalloc((void**)&buf, MJH_TSLOTS * sizeof(unsigned long long)));
+    if (hipMemset(buf, 0, MJH_TSLOTS * sizeof(unsigned long long)) != hipSuccess) {
+      hipFree(buf);
+      set_error("mjhip_contextTimers: hipMemset failed");
+      return MJHIP_ERR_HIP;
+    }
+    c->tbuf = buf;
   }
   if (!c->tev0) HIPCHECK(hipEventCreate(&c->tev0));
   if (!c->tev1) HIPCHECK(hipEventCreate(&c->tev1));
+  g_timed_ctx = c;                         // only once everything it needs exists
   return MJHIP_OK;
 }
 

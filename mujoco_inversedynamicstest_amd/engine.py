@@ -77,6 +77,9 @@ SIGNATURES = {
                                               ctypes.c_double, ctypes.c_int, _V, _V, _V, _V,
                                               _V, _V, _V, ctypes.c_int]),
     "mjhip_modelCapacity": (ctypes.c_int, [_V, _I, _I]),
+    "mjhip_ccdBatch": (ctypes.c_int, [_V, ctypes.c_int, _I, _I, _D, _D, _D, _D, _D,
+                                      ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                                      ctypes.c_double, _D, _I, _D, _D]),
     "mjhip_timeInverseKernel": (ctypes.c_int, [_V, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                ctypes.c_int,
                                                ctypes.POINTER(ctypes.c_float)]),
@@ -367,6 +370,26 @@ class InverseEngine:
     self.set_field("qpos", qpos, first)
     self.set_field("qvel", qvel, first)
     self.set_field("qacc", qacc, first)
+
+  def ccd(self, g1, g2, pos1, mat1, pos2, mat2, margin=None, max_iterations=1000,
+          tolerance=1e-6, max_contacts=1, dist_cutoff=0.0):
+    """mjc_ccd on the device over pairs (g1[i], g2[i]) at frames pos (n x 3) / mat (n x 9)
+    (mjhip_ccdBatch): (dist [n], nx [n], x1 [n, 3], x2 [n, 3])."""
+    g1 = np.ascontiguousarray(g1, dtype=np.int32)
+    g2 = np.ascontiguousarray(g2, dtype=np.int32)
+    n = g1.size
+    f = [np.ascontiguousarray(a, dtype=np.float64).reshape(n, -1)
+         for a in (pos1, mat1, pos2, mat2)]
+    mg = None if margin is None else np.ascontiguousarray(
+        np.broadcast_to(margin, (n,)), dtype=np.float64)
+    dist, nx = np.zeros(n), np.zeros(n, dtype=np.int32)
+    x1, x2 = np.zeros((n, 3)), np.zeros((n, 3))
+    D = lambda a: a.ctypes.data_as(_D)
+    _check(lib().mjhip_ccdBatch(self.ctx, n, g1.ctypes.data_as(_I), g2.ctypes.data_as(_I),
+                                *map(D, f), D(mg) if mg is not None else None,
+                                max_iterations, tolerance, max_contacts, dist_cutoff, D(dist),
+                                nx.ctypes.data_as(_I), D(x1), D(x2)), "mjhip_ccdBatch")
+    return dist, nx, x1, x2
 
   def timers(self, enable=True):
     """Per-stage timers on or off (mjhip_contextTimers): timed inverse calls synchronize."""

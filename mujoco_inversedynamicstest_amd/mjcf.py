@@ -601,9 +601,11 @@ class MJCFCompiler:
     self.basedir = None
 
   def _compile_pairs(self, arr, s, geoms):
-    """Predefined geom pairs: mjs_defaultPair (user_init.c:298-307) under the class defaults
-    and the element's attributes (mjXReader::OnePair, xml_native_reader.cc:1866-1893; partial
-    vectors keep the remaining defaults), the geoms swapped so that body1 <= body2 and the
+    """Predefined geom pairs: mjs_defaultPair (user_init.c:298-307) under the class chain's
+    defaults, root first, and the element's attributes (mjXReader::OnePair,
+    xml_native_reader.cc:1866-1893, applied to each default class's copy of its parent's
+    mjsPair and then to the element's; ReadAttr copies only the values given, xml_util.cc:681,
+    so a partial vector keeps the rest of the level below), the geoms swapped so that body1 <= body2 and the
     body signature (mjCPair::ResolveReferences, user_objects.cc:4777-4817), condim checked
     (mjCPair::Compile :4822-4828), then stably sorted by signature (user_model.cc:4321-4324)
     and written as in mjCModel::CopyObjects (:3153-3164). The pair's values are always
@@ -614,14 +616,15 @@ class MJCFCompiler:
       vals = {"condim": 3, "solref": [0.02, 1.0], "solreffriction": [0.0, 0.0],
               "solimp": [0.9, 0.95, 0.001, 0.5, 2.0], "margin": [0.0], "gap": [0.0],
               "friction": [1.0, 1.0, 0.005, 0.0001, 0.0001]}
-      for k in ("solref", "solreffriction", "solimp", "margin", "gap", "friction"):
-        if k in a:
-          v = _floats(a[k])
-          if len(v) > len(vals[k]):
-            raise MJCFError(f"pair attribute '{k}' has too many values")
-          vals[k][:len(v)] = v
-      if "condim" in a:
-        vals["condim"] = int(a["condim"])
+      for layer in a.get("_layers", [a]):
+        for k in ("solref", "solreffriction", "solimp", "margin", "gap", "friction"):
+          if k in layer:
+            v = _floats(layer[k])
+            if len(v) > len(vals[k]):
+              raise MJCFError(f"pair attribute '{k}' has too many values")
+            vals[k][:len(v)] = v
+        if "condim" in layer:
+          vals["condim"] = int(layer["condim"])
       if vals["condim"] not in (1, 3, 4, 6):
         raise MJCFError("invalid condim in contact pair")
       n1, n2 = a.get("geom1"), a.get("geom2")
@@ -940,7 +943,15 @@ class MJCFCompiler:
           if ch.tag == "exclude":
             self.excludes.append((ch.get("body1"), ch.get("body2")))
           elif ch.tag == "pair":           # mjXReader::OnePair (xml_native_reader.cc:1866)
-            self.pairs.append(self._elem_attrs(ch, "pair", None))
+            a = self._elem_attrs(ch, "pair", None)
+            # the class chain's own pair attributes, root first, then the element's: vectors
+            # overlay element-wise level by level (a default class holds a whole mjsPair)
+            chain, d = [], self.classes[ch.get("class", "main")]
+            while d is not None:
+              chain.append(dict(d.attrs.get("pair", {})))
+              d = d.parent
+            a["_layers"] = chain[::-1] + [dict(ch.attrib)]
+            self.pairs.append(a)
           else:
             raise MJCFError(f"unsupported contact element <{ch.tag}>")
       elif t == "keyframe":

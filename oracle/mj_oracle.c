@@ -3785,7 +3785,8 @@ static void ccd_center(mjtNum c[3], const orShape* s) {
   }
 }
 
-static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol, mjtNum cutoff) {
+static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol, mjtNum cutoff,
+                     int maxc) {
   ccd_center(st->x1, A);
   ccd_center(st->x2, B);
   st->iters = 0;
@@ -3831,11 +3832,17 @@ static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol, mj
       if (st->dist > st->cutoff) st->dist = mjhipMAXVAL;
       return st->dist;
     }
+    if (!maxc) {                            /* contact not needed (:2267-2272) */
+      st->nx = 0;
+      st->dist = 0;
+      return 0;
+    }
     st->iters = 0;
     ccd_center(st->x1, A);
     ccd_center(st->x2, B);
   }
   ccd_gjk(st, A, B);
+  if (!maxc) return st->dist;               /* penetration recovery not needed (:2280-2283) */
   if (st->dist <= tol && st->nsimplex > 1) {
     st->dist = 0;
     const int N = kmax;
@@ -3885,7 +3892,7 @@ static int col_convex(orRaw* c, const mjhipModel* m, const mjhipData* d, int g1,
   or_shape(&A, m, d, g1, margin);
   or_shape(&B, m, d, g2, margin);
   orCCD st;
-  mjtNum dist = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, 0);
+  mjtNum dist = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, 0, 1);
   if (!(dist < 0) || st.nx < 1) return 0;
   c->dist = margin + dist;
   mju_sub3(c->frame, st.x1, st.x2);
@@ -4284,7 +4291,7 @@ static int col_convexHField(orRaw* con, const mjhipModel* m, const mjhipData* d,
         if (nvert <= 2) continue;
         if (A.prism[3][2] < zmin && A.prism[4][2] < zmin && A.prism[5][2] < zmin) continue;
         orCCD st;
-        const mjtNum dist = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, 0);
+        const mjtNum dist = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, 0, 1);
         if (!(dist < 0)) continue;              /* mjc_penetration: no penetration */
         mjtNum dir[3], vp[3];
         mju_sub3(dir, st.x1, st.x2);
@@ -4320,13 +4327,34 @@ int or_ccdPenetration(const mjhipModel* m, const mjhipData* d, int g1, int g2, m
   or_shape(&A, m, d, g1, margin);
   or_shape(&B, m, d, g2, margin);
   orCCD st;
-  mjtNum dist = or_ccd(&st, &A, &B, kmax, tol, 0);
+  mjtNum dist = or_ccd(&st, &A, &B, kmax, tol, 0, 1);
   if (!(dist < 0) || st.nx < 1) return 0;
   out[0] = dist;
   mju_sub3(out + 1, st.x1, st.x2);
   mju_normalize3(out + 1);
   for (int k = 0; k < 3; k++) out[4 + k] = 0.5*(st.x1[k] + st.x2[k]);
   return 1;
+}
+
+/* mjc_ccd (engine_collision_gjk.c:2215-2343) as the reference's GJK tests call it
+   (engine_collision_gjk_test.cc:62-84 GeomDist, :86-150 Penetration): geoms g1, g2 at the
+   data's current frames, object margin `margin` on both, config {kmax, tol, maxc (0 or 1),
+   cutoff}. out: dist, nx, x1[3], x2[3]. Returns dist. */
+mjtNum or_ccdGeneral(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum margin,
+                     mjtNum tol, int kmax, int maxc, mjtNum cutoff, mjtNum* out) {
+  orShape A, B;
+  or_shape(&A, m, d, g1, margin);
+  or_shape(&B, m, d, g2, margin);
+  orCCD st;
+  st.nx = 0;
+  mjtNum dist = or_ccd(&st, &A, &B, kmax, tol, cutoff, maxc);
+  out[0] = dist;
+  out[1] = st.nx;
+  for (int k = 0; k < 3; k++) {
+    out[2 + k] = st.x1[k];
+    out[5 + k] = st.x2[k];
+  }
+  return dist;
 }
 
 /* pairs served by mjc_Convex in mjCOLLISIONFUNC (capsule-ellipsoid/cylinder, sphere-ellipsoid,
@@ -4832,7 +4860,7 @@ static mjtNum or_geomDistance(const mjhipModel* m, mjhipData* d, int geom1, int 
     or_shape(&A, m, d, g1, 0);
     or_shape(&B, m, d, g2, 0);
     orCCD st;
-    const mjtNum r = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, distmax);
+    const mjtNum r = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, distmax, 1);
     if (st.nx > 0) {
       mju_copy3(fromto, st.x1);
       mju_copy3(fromto + 3, st.x2);

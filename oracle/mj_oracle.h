@@ -122,6 +122,8 @@ void or_inverseFDEx(const mjhipModel* m, mjhipData* d, orEfc* efc, mjtNum eps,
  * count, out = dist, dir[3], pos[3]) and mj_ray (geomgroup NULL, flg_static 1) */
 int or_ccdPenetration(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum margin,
                       mjtNum tol, int kmax, mjtNum* out);
+mjtNum or_ccdGeneral(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum margin,
+                     mjtNum tol, int kmax, int maxc, mjtNum cutoff, mjtNum* out);
 mjtNum or_rayTest(const mjhipModel* m, const mjhipData* d, const mjtNum* pnt,
                   const mjtNum* vec, int bodyexclude, int* geomid);
 

@@ -96,6 +96,9 @@ def lib():
     L.or_ccdPenetration.argtypes = [M, Dp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                     ctypes.c_double, ctypes.c_int, _D]
     L.or_ccdPenetration.restype = ctypes.c_int
+    L.or_ccdGeneral.argtypes = [M, Dp, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                ctypes.c_double, ctypes.c_int, ctypes.c_int, ctypes.c_double, _D]
+    L.or_ccdGeneral.restype = ctypes.c_double
     L.or_rayTest.argtypes = [M, Dp, _D, _D, ctypes.c_int, ctypes.POINTER(ctypes.c_int)]
     L.or_rayTest.restype = ctypes.c_double
     L.or_inverseBatch.restype = ctypes.c_double
@@ -307,6 +310,14 @@ class Oracle:
     out = np.zeros(7)
     n = self.L.or_ccdPenetration(*self._args()[:2], g1, g2, margin, tol, kmax, _p(out))
     return n, out[0], out[1:4], out[4:7]
+
+  def ccd(self, g1, g2, margin=0.0, tol=1e-6, kmax=1000, max_contacts=1, cutoff=0.0):
+    """mjc_ccd (engine_collision_gjk.c:2215-2343) on the current frames with the reference
+    tests' config (engine_collision_gjk_test.cc:62-150): (dist, nx, x1, x2)."""
+    out = np.zeros(8)
+    dist = self.L.or_ccdGeneral(*self._args()[:2], g1, g2, margin, tol, kmax, max_contacts,
+                                cutoff, _p(out))
+    return dist, int(out[1]), out[2:5].copy(), out[5:8].copy()
 
   def ray(self, pnt, vec, bodyexclude=-1):
     """mj_ray (geomgroup NULL, flg_static 1) on the current frames: (distance, geomid)."""

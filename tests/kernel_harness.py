@@ -49,8 +49,28 @@ def lib():
     L.kh_inverse.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                              ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                              ctypes.c_int]
+    D = ctypes.POINTER(ctypes.c_double)
+    L.kh_ccd.restype = ctypes.c_int
+    L.kh_ccd.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, D, D, D, D,
+                         ctypes.c_double, ctypes.c_int, ctypes.c_double, ctypes.c_int,
+                         ctypes.c_double, D]
     _lib = L
   return _lib
+
+
+def ccd_host(m, g1, g2, xpos, xmat, margin=0.0, tol=1e-6, kmax=1000, max_contacts=1,
+             cutoff=0.0):
+  """The device's mjc_ccd (mjh::ccdGeneral) compiled for the host, on geoms g1, g2 at the
+  frames xpos [ngeom, 3], xmat [ngeom, 9]: (dist, nx, x1, x2), as Oracle.ccd."""
+  cm = host.model_struct(m)
+  D = ctypes.POINTER(ctypes.c_double)
+  out = np.zeros(8)
+  a = [np.ascontiguousarray(v, dtype=np.float64) for v in (xpos[g1], xmat[g1], xpos[g2],
+                                                            xmat[g2])]
+  st = lib().kh_ccd(ctypes.byref(cm), g1, g2, *(x.ctypes.data_as(D) for x in a), margin,
+                    kmax, tol, max_contacts, cutoff, out.ctypes.data_as(D))
+  assert st == 0, "face capacity exceeded"
+  return out[0], int(out[1]), out[2:5].copy(), out[5:8].copy()
 
 
 class KernelCPU:

@@ -83,3 +83,26 @@ def test_timers_no_contacts():
     assert t["POS_INERTIA"][0] > 0 and t["POS_COLLISION"][0] == 0
   finally:
     e.close()
+
+
+def test_timed_context_freed_then_another():
+  """A timed context freed while timing is on detaches every unit's timer pointer before its
+  stream and accumulator go: a second context then runs with identical results,
+  may enable timers itself, and counts only its own calls."""
+  m = models.load("humanoid")
+  B = 1024
+  q, v, a = sample_contact_states(m, B)
+  e1 = engine.InverseEngine(m, capacity=B)
+  f0 = e1.inverse(q, v, a)
+  e1.timers(True)
+  e1.inverse(q, v, a)
+  e1.close()                               # freed with timers on
+  e2 = engine.InverseEngine(m, capacity=B)
+  try:
+    np.testing.assert_array_equal(e2.inverse(q, v, a), f0)
+    assert all(x == (0.0, 0) for x in e2.timer_read().values())
+    e2.timers(True)                        # the freed context no longer holds the slot
+    np.testing.assert_array_equal(e2.inverse(q, v, a), f0)
+    _check(e2.timer_read(), 1, collision=True)
+  finally:
+    e2.close()
