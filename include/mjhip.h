@@ -330,7 +330,10 @@ MJHIP_API int mjhip_contextLoadKernel(mjhipContext* c, const void* image, size_t
                                       int cmode);
 /* kernels the context's last batched mj_inverseSkip ran on: 0 the generic kernel, 1 the
  * straight-line pipeline (skipstage NONE), 2 the straight-line mj_inverseSkip(POS / VEL)
- * kernels (k_va / k_acc of the model's generated code); -1 before any call */
+ * kernels (k_va / k_acc of the model's generated code), 3 the straight-line pipeline of a
+ * contact model split over two streams (position stage, then the cooperative constraint
+ * kernel beside the fac / va stages, joined by the assembly; opt-in with MJHIP_SPLIT=1);
+ * -1 before any call */
 MJHIP_API int mjhip_contextLastPath(const mjhipContext* c);
 /* instances of the last fast-path call that had active constraint rows and were recomputed
  * by the generic kernel (blocking read; -1 on error) */
@@ -417,10 +420,12 @@ MJHIP_API int mjhip_modelCapacity(const mjhipModel* m, int* efc_rows, int* conta
  * is geoms g1[i], g2[i] at the caller's frames pos1/pos2 (n x 3) and mat1/mat2 (n x 9,
  * row-major geom_xmat), both inflated by margin[i] (mjc_initCCDObj's margin; NULL: 0), with
  * the mjCCDConfig {max_iterations, tolerance, max_contacts, dist_cutoff}. max_contacts 0 asks
- * for the distance alone (no penetration recovery), 1 for one contact. Outputs (host arrays):
- * dist[n] (mjc_ccd's return value), nx[n] (status.nx), x1/x2 (n x 3, status.x1/x2: the
- * witness points). Status codes as everywhere; MJHIP_ERR_ARG for max_contacts outside
- * {0, 1}, MJHIP_ERR_MODEL when a pair's polytope outgrew the solver's face capacity. */
+ * for the distance alone (no penetration recovery), 1 for one contact, more for the
+ * multicontact polygon of a penetrating box pair (gjk.c:1460-2193). Outputs (host arrays):
+ * dist[n] (mjc_ccd's return value), nx[n] (status.nx), x1/x2 (n x xcap x 3, status.x1/x2: the
+ * witness points, xcap = max(1, min(max_contacts, mjMAXCONPAIR = 50))). Status codes as
+ * everywhere; MJHIP_ERR_MODEL when a pair's polytope outgrew the solver's face capacity or
+ * needs multicontact on a mesh (the mesh polygon data is not compiled). */
 MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g2,
                              const mjtNum* pos1, const mjtNum* mat1, const mjtNum* pos2,
                              const mjtNum* mat2, const mjtNum* margin, int max_iterations,

@@ -1587,6 +1587,81 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
                 f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE(); MJH_PHASE({20 + k});"
                 for k, st in enumerate(STAGES))
              + "\n" + fuse_tail + "}")
+  # the split launch of a model whose constraint rows serve every instance (contacts): the
+  # position stage alone (k_spos), then the fac and va stages (k_sfv), so that the
+  # cooperative constraint kernel -- which reads only position-stage outputs and the inputs
+  # -- runs on a second stream beside k_sfv, and the assembly kernel (mjhip.hip k_assemble)
+  # joins them (mjhip.hip launch_inverse). Same stage bodies as k_all, so the same results.
+  if M.cmode == "all" and not extern_c:
+    pos_args = _SIG["pos"][1].replace("trig, qmr", "trig, nullptr")
+    out.append(f"""template <bool SV>
+__global__ __launch_bounds__(64, 1) void k_spos_{name}(Mirror mr, int B,
+    const double* __restrict__ qpos_in, const double* __restrict__ qvel_in,
+    const double* __restrict__ qacc_in, int* __restrict__ worklist,
+    int* __restrict__ worklist_count, int* __restrict__ worklist_next,
+    int* __restrict__ efc_count) {{
+  __shared__ double trig[{ntrig}];
+  MJH_PHASE0(19, 27);
+  fast_pos_{name}<SV>(mr, blockIdx.x, threadIdx.x, B, {pos_args});
+}}
+template <bool SV>
+__global__ __launch_bounds__(64, 1) void k_sfv_{name}(Mirror mr, int B,
+    double* __restrict__ qfrc_out, int* __restrict__ status, int* __restrict__ efc_count) {{
+  __shared__ double qo_lds[{nqo}];
+  MJH_PHASE(20);     // the position span runs from k_spos's start to here (launch gap included)
+  fast_fac_{name}<SV>(mr, blockIdx.x, threadIdx.x, B, efc_count, nullptr);
+  asm volatile("" ::: "memory"); MJH_SCHED_FENCE(); MJH_PHASE(21);
+  fast_va_{name}<SV>(mr, blockIdx.x, threadIdx.x, B, qfrc_out, status, efc_count, qo_lds,
+                     nullptr);
+  asm volatile("" ::: "memory"); MJH_SCHED_FENCE(); MJH_PHASE(22);
+}}
+{"" if shared else "static "}void launch_split_{name}(hipStream_t s, const Mirror& mr, int B, int part,
+    const double* qpos_in, const double* qvel_in, const double* qacc_in, int* status,
+    int* worklist_next, int* efc_count) {{
+  const dim3 g((B + 63) / 64), b(64);
+  if (part == 0) {{
+    if (B >= {NT_SV_MIN_B}) {{
+      hipLaunchKernelGGL(k_spos_{name}<true>, g, b, 0, s, mr, B, qpos_in, qvel_in, qacc_in,
+                         nullptr, nullptr, worklist_next, efc_count);
+    }} else {{
+      hipLaunchKernelGGL(k_spos_{name}<false>, g, b, 0, s, mr, B, qpos_in, qvel_in, qacc_in,
+                         nullptr, nullptr, worklist_next, efc_count);
+    }}
+  }} else if (B >= {NT_SV_MIN_B}) {{
+    hipLaunchKernelGGL(k_sfv_{name}<true>, g, b, 0, s, mr, B, nullptr, status, efc_count);
+  }} else {{
+    hipLaunchKernelGGL(k_sfv_{name}<false>, g, b, 0, s, mr, B, nullptr, status, efc_count);
+  }}
+}}""")
+  # batched mj_inverseSkip(POS / VEL) of a model whose rows serve every instance (contacts):
+  # k_va (the staged va kernel) or k_acc store the raw RNE, and k_skip_rows (mjhip.hip)
+  # finishes every instance -- the previous call's rows (referenceConstraint for POS,
+  # invConstraint) and the assembly -- and writes the row-major output
+  if M.cmode == "all" and not extern_c:
+    import re
+    ab = _gen_acc(M)
+    if NT_STORES:
+      ab = re.sub(r"^(\s*)P_(\w+)\[(\d+)\*64\] = (.+);$",
+                  lambda mt: f"{mt.group(1)}MJH_NT_STORE(P_{mt.group(2)}[{mt.group(3)}*64], "
+                             f"{mt.group(4)});", ab, flags=re.M)
+    out.append(f"MJH_HD void fast_acc_{name}(const Mirror& mr, int blk, int lane, int B, "
+               f"{_SIG['va'][0]}) {{\n{ab}\n}}\n")
+    out.append(f"""__global__ __launch_bounds__(64, 1) void k_acc_{name}(Mirror mr, int B,
+    double* __restrict__ qfrc_out, int* __restrict__ status, int* __restrict__ efc_count) {{
+  fast_acc_{name}(mr, blockIdx.x, threadIdx.x, B, qfrc_out, status, efc_count, nullptr,
+                  nullptr);
+}}
+{"" if shared else "static "}void launch_skip_{name}(hipStream_t s, const Mirror& mr, int B, int skipstage,
+                              double* qfrc_out, int* status, int* efc_count) {{
+  (void)qfrc_out;      // raw RNE only: k_skip_rows assembles and writes the output
+  if (skipstage == 1) {{
+    hipLaunchKernelGGL(k_va_{name}, dim3((B + 63) / 64), dim3(64), 0, s, mr, B, nullptr,
+                       status, efc_count);
+  }} else {{
+    hipLaunchKernelGGL(k_acc_{name}, dim3((B + 63) / 64), dim3(64), 0, s, mr, B, nullptr,
+                       status, efc_count);
+  }}
+}}""")
   # k_vaskip: the va stage of mj_inverseSkip(mjSTAGE_POS) for mjd_inverseFD's qvel and qacc
   # perturbations (engine_derivative_fd.c:646-699). Instance off + t reads every position-
   # stage output (the va pointers it never stores) from its centre instance
@@ -1807,17 +1882,20 @@ def generate_registries(entries) -> tuple:
         for k in ("vaskip", "fdskip"):
           main.append(f"void launch_{k}_{name}(hipStream_t, const Mirror&, int, int, int, int, "
                       "int*, int*, double);")
-        main.append(f"void launch_skip_{name}(hipStream_t, const Mirror&, int, int, double*, "
-                    "int*, int*);")
+      main.append(f"void launch_skip_{name}(hipStream_t, const Mirror&, int, int, double*, "
+                  "int*, int*);")
+      if constraint_mode(m) == "all":
+        main.append(f"void launch_split_{name}(hipStream_t, const Mirror&, int, int, "
+                    "const double*, const double*, const double*, int*, int*, int*);")
     else:
       main.append(generate(m, name))
-    fns = ", ".join(f"launch_{k}_{name}" if vaskip else "nullptr"
-                    for k in ("vaskip", "fdskip", "skip"))
+    fns = ", ".join(f"launch_{k}_{name}" if vaskip else "nullptr" for k in ("vaskip", "fdskip"))
+    split = f"launch_split_{name}" if constraint_mode(m) == "all" else "nullptr"
     reg.append(f'  {{0x{fields.model_signature(m):016x}ull, launch_fast_{name}, "{name}", '
-               f'{CONSTRAINT_MODES[constraint_mode(m)]}, {fns}}},')
+               f'{CONSTRAINT_MODES[constraint_mode(m)]}, {fns}, launch_skip_{name}, {split}}},')
   main.append("static const FastKernelEntry g_fast_kernels[] = {")
   main.extend(reg)
-  main.append("  {0ull, nullptr, nullptr, 0, nullptr, nullptr, nullptr}};")
+  main.append("  {0ull, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr}};")
   return "\n".join(main) + "\n", "\n".join(exact) + "\n"
 
 
@@ -1829,11 +1907,11 @@ def generate_registry(entries) -> str:
   for name, m in entries:
     out.append(generate(m, name))
     sk = constraint_mode(m) in ("none", "list")
-    fns = ", ".join(f"launch_{k}_{name}" if sk else "nullptr"
-                    for k in ("vaskip", "fdskip", "skip"))
+    fns = ", ".join(f"launch_{k}_{name}" if sk else "nullptr" for k in ("vaskip", "fdskip"))
+    split = f"launch_split_{name}" if constraint_mode(m) == "all" else "nullptr"
     reg.append(f'  {{0x{fields.model_signature(m):016x}ull, launch_fast_{name}, "{name}", '
-               f'{CONSTRAINT_MODES[constraint_mode(m)]}, {fns}}},')
+               f'{CONSTRAINT_MODES[constraint_mode(m)]}, {fns}, launch_skip_{name}, {split}}},')
   out.append("static const FastKernelEntry g_fast_kernels[] = {")
   out.extend(reg)
-  out.append("  {0ull, nullptr, nullptr, 0, nullptr, nullptr, nullptr}};")
+  out.append("  {0ull, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr}};")
   return "\n".join(out) + "\n"

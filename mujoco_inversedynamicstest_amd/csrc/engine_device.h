@@ -3061,12 +3061,388 @@ MJH_HD void ccdCenter(double c[3], const CcdShape& s) {
   }
 }
 
+// ---- multicontact (engine_collision_gjk.c:1460-2193), box pairs: with max_contacts > 1 the
+// EPA's final face becomes a contact polygon -- each geom's feature spanned by the face's three
+// vertices, the face normals around it, a pair of anti-aligned faces (or an edge perpendicular
+// to a face), one face clipped by the other's edge planes. The reference keeps each polytope
+// vertex's box corner (Vertex.index1/2, set by mjc_boxSupport's vertindex); here the corner is
+// read back from the witness point itself -- the sign pattern of its box-frame coordinates,
+// which is the support's `tmp` sign pattern -- so the solver's memory layout is unchanged.
+// Meshes need the compiler's polygon data (not built): unsupported. Only k_ccd
+// (mjhip_ccdBatch) compiles this in (ccdRun's MULTI), with private arrays.
+constexpr double CCD_FACE_TOL = 0.99999872;     // mjFACE_TOL (gjk.h:29)
+constexpr double CCD_EDGE_TOL = 0.00159999931;  // mjEDGE_TOL (gjk.h:32)
+constexpr int CCD_MAXCON = 50;                  // mjMAXCONPAIR: the witness capacity
+constexpr int CCD_MAXPOLY = 16;                 // clipped polygon capacity (box faces: <= 8)
+
+// the box corner a support point is (mjc_boxSupport's vertindex bits, convex.c:319-323)
+MJH_HD int ccdBoxCorner(const CcdShape& s, const double* p) {
+  double d[3], l[3];
+  sub3(d, p, s.pos);
+  mulMatTVec3(l, s.mat, d);
+  return (l[0] > 0 ? 1 : 0) | (l[1] > 0 ? 2 : 0) | (l[2] > 0 ? 4 : 0);
+}
+
+// area4 (:1463-1476)
+MJH_HD double ccdArea4(const double* a, const double* b, const double* c, const double* d) {
+  double ad[3] = {d[0] - a[0], d[1] - a[1], d[2] - a[2]};
+  double db[3] = {b[0] - d[0], b[1] - d[1], b[2] - d[2]};
+  double bc[3] = {c[0] - b[0], c[1] - b[1], c[2] - b[2]};
+  double ca[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]};
+  double e[3], f[3], g[3];
+  cross(e, ad, db);
+  cross(f, bc, ca);
+  add3(g, e, f);
+  return 0.5 * sqrt(dot3(g, g));
+}
+
+MJH_HD int ccdNext(int n, int i) { return i == n - 1 ? 0 : i + 1; }
+
+// polygonQuad (:1491-1535), on vertex indices
+MJH_HD void ccdPolygonQuad(int res[4], const double* P, int n) {
+  int a = 0, b = 1, c = 2, d = 3;
+  res[0] = a; res[1] = b; res[2] = c; res[3] = d;
+  double m = ccdArea4(P + 3*a, P + 3*b, P + 3*c, P + 3*d), mn;
+  for (; a < n; a++) {
+    while (true) {
+      mn = ccdArea4(P + 3*a, P + 3*b, P + 3*c, P + 3*ccdNext(n, d));
+      if (mn <= m) break;
+      m = mn;
+      d = ccdNext(n, d);
+      res[0] = a; res[1] = b; res[2] = c; res[3] = d;
+      while (true) {
+        mn = ccdArea4(P + 3*a, P + 3*b, P + 3*ccdNext(n, c), P + 3*d);
+        if (mn <= m) break;
+        m = mn;
+        c = ccdNext(n, c);
+        res[0] = a; res[1] = b; res[2] = c; res[3] = d;
+      }
+      while (true) {
+        mn = ccdArea4(P + 3*a, P + 3*ccdNext(n, b), P + 3*c, P + 3*d);
+        if (mn <= m) break;
+        m = mn;
+        b = ccdNext(n, b);
+        res[0] = a; res[1] = b; res[2] = c; res[3] = d;
+      }
+    }
+    if (b == a) {
+      b = ccdNext(n, b);
+      if (c == b) {
+        c = ccdNext(n, c);
+        if (d == c) d = ccdNext(n, d);
+      }
+    }
+  }
+}
+
+// the contact list of a multicontact call: x1 / x2 [3 CCD_MAXCON], nx
+struct CcdContacts {
+  double* x1;
+  double* x2;
+  int nx, maxc, bad;
+};
+
+// polygonClip (:1579-1690): face2 clipped by face1's edge planes (normal n), the vertices the
+// contacts' x2, x1 = x2 - dir
+MJH_HD void ccdPolygonClip(CcdContacts& C, const double* face1, int nf1, const double* face2,
+                           int nf2, const double n[3], const double dir[3]) {
+  if (nf1 < 3) return;
+  double pn[3*4], pd[4];
+  for (int i = 0; i < nf1; i++) {                       // planeNormal (:1540-1549)
+    const double* v1 = face1 + 3*i;
+    const double* v2 = face1 + 3*(i < nf1 - 1 ? i + 1 : 0);
+    double v3[3], d1[3], d2[3];
+    add3(v3, v1, n);
+    sub3(d1, v2, v1);
+    sub3(d2, v3, v1);
+    cross(pn + 3*i, d1, d2);
+    pd[i] = dot3(pn + 3*i, v1);
+  }
+  double buf[2][3*CCD_MAXPOLY];
+  double* poly = buf[0];
+  double* clip = buf[1];
+  int np = nf2, nc = 0;
+  for (int i = 0; i < nf2; i++) copy3(poly + 3*i, face2 + 3*i);
+  for (int e = 0; e < nf1; e++) {
+    const double* a = face1 + 3*e;
+    for (int i = 0; i < np; i++) {
+      const double* P = poly + 3*i;
+      const double* Q = i < np - 1 ? poly + 3*(i + 1) : poly;
+      const double dp[3] = {P[0] - a[0], P[1] - a[1], P[2] - a[2]};
+      const double dq[3] = {Q[0] - a[0], Q[1] - a[1], Q[2] - a[2]};
+      const bool in1 = dot3(dp, pn + 3*e) > 0, in2 = dot3(dq, pn + 3*e) > 0;   // halfspace
+      if (!in1 && !in2) continue;
+      if (nc + 2 > CCD_MAXPOLY) {                       // cannot happen for box faces
+        C.bad = 1;
+        return;
+      }
+      if (in1 && in2) {
+        copy3(clip + 3*nc++, Q);
+        continue;
+      }
+      // planeIntersect (:1561-1574)
+      double ab[3];
+      sub3(ab, Q, P);
+      const double temp = dot3(pn + 3*e, ab);
+      double t = mjhipMAXVAL;
+      if (temp != 0.0) {
+        t = (pd[e] - dot3(pn + 3*e, P)) / temp;
+        if (t >= 0.0 && t <= 1.0) {
+          double* r = clip + 3*nc;
+          r[0] = P[0] + t*ab[0];
+          r[1] = P[1] + t*ab[1];
+          r[2] = P[2] + t*ab[2];
+        }
+      }
+      nc++;
+      if (t < 0.0 || t > 1.0) nc--;
+      if (in2) copy3(clip + 3*nc++, Q);
+    }
+    double* tmp = poly;
+    poly = clip;
+    clip = tmp;
+    np = nc;
+    nc = 0;
+  }
+  if (np < 1) return;
+  if (C.maxc < 5 && np > 4) {
+    int rect[4];
+    ccdPolygonQuad(rect, poly, np);
+    C.nx = 4;
+    for (int i = 0; i < 4; i++) {
+      copy3(C.x2 + 3*i, poly + 3*rect[i]);
+      sub3(C.x1 + 3*i, C.x2 + 3*i, dir);
+    }
+    return;
+  }
+  int k = 0;                                            // np <= CCD_MAXPOLY < mjMAXCONPAIR
+  for (int i = 0; i < np; i++) {
+    const double* q = poly + 3*i;
+    bool skip = false;
+    for (int j = 0; j < k && !skip; j++) {              // equal3 (:116-120)
+      const double* x = C.x2 + 3*j;
+      skip = fabs(x[0] - q[0]) < MINVAL && fabs(x[1] - q[1]) < MINVAL &&
+             fabs(x[2] - q[2]) < MINVAL;
+    }
+    if (skip) continue;
+    copy3(C.x2 + 3*k, q);
+    sub3(C.x1 + 3*k, C.x2 + 3*k, dir);
+    k++;
+  }
+  C.nx = k;
+}
+
+// globalcoord (:1695-1707)
+MJH_HD void ccdGlobal(double r[3], const double mat[9], const double* pos, double l1,
+                      double l2, double l3) {
+  r[0] = mat[0]*l1 + mat[1]*l2 + mat[2]*l3;
+  r[1] = mat[3]*l1 + mat[4]*l2 + mat[5]*l3;
+  r[2] = mat[6]*l1 + mat[7]*l2 + mat[8]*l3;
+  if (pos) {
+    r[0] += pos[0];
+    r[1] += pos[1];
+    r[2] += pos[2];
+  }
+}
+
+// boxNormals (:1846-1899)
+MJH_HD int ccdBoxNormals(double res[9], int ind[3], int dim, const CcdShape& s, int v1, int v2,
+                         int v3) {
+  if (dim == 3) {
+    const int x = ((v1 & 1) && (v2 & 1) && (v3 & 1)) - (!(v1 & 1) && !(v2 & 1) && !(v3 & 1));
+    const int y = ((v1 & 2) && (v2 & 2) && (v3 & 2)) - (!(v1 & 2) && !(v2 & 2) && !(v3 & 2));
+    const int z = ((v1 & 4) && (v2 & 4) && (v3 & 4)) - (!(v1 & 4) && !(v2 & 4) && !(v3 & 4));
+    ccdGlobal(res, s.mat, nullptr, x, y, z);
+    if (x) ind[0] = 0;
+    if (y) ind[0] = 2;
+    if (z) ind[0] = 4;
+    if (x + y + z == -1) ind[0]++;
+    return 1;
+  }
+  if (dim == 2) {
+    const int x = ((v1 & 1) && (v2 & 1)) - (!(v1 & 1) && !(v2 & 1));
+    const int y = ((v1 & 2) && (v2 & 2)) - (!(v1 & 2) && !(v2 & 2));
+    const int z = ((v1 & 4) && (v2 & 4)) - (!(v1 & 4) && !(v2 & 4));
+    if (x) {
+      ccdGlobal(res, s.mat, nullptr, x, 0, 0);
+      ind[0] = x > 0 ? 0 : 1;
+    }
+    if (y) {
+      const int i = x ? 1 : 0;
+      ccdGlobal(res + 3*i, s.mat, nullptr, 0, y, 0);
+      ind[i] = y > 0 ? 2 : 3;
+    }
+    if (z) {
+      ccdGlobal(res + 3, s.mat, nullptr, 0, 0, z);
+      ind[1] = z > 0 ? 4 : 5;
+    }
+    return 2;
+  }
+  if (dim == 1) {
+    const double x = (v1 & 1) ? 1 : -1, y = (v1 & 2) ? 1 : -1, z = (v1 & 4) ? 1 : -1;
+    ccdGlobal(res, s.mat, nullptr, x, 0, 0);
+    ccdGlobal(res + 3, s.mat, nullptr, 0, y, 0);
+    ccdGlobal(res + 6, s.mat, nullptr, 0, 0, z);
+    ind[0] = x > 0 ? 0 : 1;
+    ind[1] = y > 0 ? 2 : 3;
+    ind[2] = z > 0 ? 4 : 5;
+    return 3;
+  }
+  return 0;
+}
+
+// boxEdgeNormals (:1903-1938)
+MJH_HD int ccdBoxEdgeNormals(double res[9], double ends[9], int dim, const CcdShape& s,
+                             const double* v1, const double* v2, int v1i) {
+  if (dim == 2) {
+    copy3(ends, v2);
+    sub3(res, v2, v1);
+    normalize3(res);
+    return 1;
+  }
+  if (dim == 1) {
+    const double x = (v1i & 1) ? s.size[0] : -s.size[0];
+    const double y = (v1i & 2) ? s.size[1] : -s.size[1];
+    const double z = (v1i & 4) ? s.size[2] : -s.size[2];
+    ccdGlobal(ends, s.mat, s.pos, -x, y, z);
+    sub3(res, ends, v1);
+    normalize3(res);
+    ccdGlobal(ends + 3, s.mat, s.pos, x, -y, z);
+    sub3(res + 3, ends + 3, v1);
+    normalize3(res + 3);
+    ccdGlobal(ends + 6, s.mat, s.pos, x, y, -z);
+    sub3(res + 6, ends + 6, v1);
+    normalize3(res + 6);
+    return 3;
+  }
+  return 0;
+}
+
+// boxFace (:1942-1990): the four corners of face idx (right, left, top, bottom, front, back)
+MJH_HD int ccdBoxFace(double res[12], const CcdShape& s, int idx) {
+  // corner sign bits per face vertex: x (1), y (2), z (4) positive
+  constexpr unsigned char corner[6][4] = {{7, 3, 1, 5}, {2, 6, 4, 0}, {2, 3, 7, 6},
+                                          {4, 5, 1, 0}, {6, 7, 5, 4}, {3, 2, 0, 1}};
+  if (idx < 0 || idx > 5) return 0;
+  for (int k = 0; k < 4; k++) {
+    const int c = corner[idx][k];
+    ccdGlobal(res + 3*k, s.mat, s.pos, (c & 1) ? s.size[0] : -s.size[0],
+              (c & 2) ? s.size[1] : -s.size[1], (c & 4) ? s.size[2] : -s.size[2]);
+  }
+  return 4;
+}
+
+// simplexDim (:2052-2067)
+MJH_HD int ccdSimplexDim(int* i1, int* i2, int* i3, const double** v1, const double** v2,
+                         const double** v3) {
+  const int a = *i1, b = *i2, c = *i3;
+  if (a != b) return (c == a || c == b) ? 2 : 3;
+  if (a != c) {
+    *i2 = *i3;
+    *v2 = *v3;
+    return 2;
+  }
+  return 1;
+}
+
+// multicontact (:2071-2193) on the EPA's final face f
+template <int S>
+MJH_HD void ccdMultiContact(CcdContacts& C, const CcdState& st, const CcdMem<S>& M, int f,
+                            const CcdShape& A, const CcdShape& B) {
+  if (A.gtype != mjhipGEOM_BOX || B.gtype != mjhipGEOM_BOX) {
+    C.bad = 1;                                          // meshes: polygon data not compiled
+    return;
+  }
+  SP<S, int> F = M.fint(f);
+  double w[3][9];                                       // the face's vertices: v, p1, p2
+  for (int k = 0; k < 3; k++) {
+    SP<S> v = M.vtx(F[k]);
+    for (int c = 0; c < 9; c++) w[k][c] = v[c];
+  }
+  int v11i = ccdBoxCorner(A, w[0] + 3), v12i = ccdBoxCorner(A, w[1] + 3);
+  int v13i = ccdBoxCorner(A, w[2] + 3);
+  int v21i = ccdBoxCorner(B, w[0] + 6), v22i = ccdBoxCorner(B, w[1] + 6);
+  int v23i = ccdBoxCorner(B, w[2] + 6);
+  const double *v11 = w[0] + 3, *v12 = w[1] + 3, *v13 = w[2] + 3;
+  const double *v21 = w[0] + 6, *v22 = w[1] + 6, *v23 = w[2] + 6;
+  int nf1 = ccdSimplexDim(&v11i, &v12i, &v13i, &v11, &v12, &v13);
+  int nf2 = ccdSimplexDim(&v21i, &v22i, &v23i, &v21, &v22, &v23);
+  double n1[9], n2[9], ends[9], face1[12], face2[12];
+  int idx1[3] = {0, 0, 0}, idx2[3] = {0, 0, 0};
+  int nn1 = ccdBoxNormals(n1, idx1, nf1, A, v11i, v12i, v13i);
+  int nn2 = ccdBoxNormals(n2, idx2, nf2, B, v21i, v22i, v23i);
+  int i = 0, j = 0;
+  bool found = false, edge1 = false, edge2 = false;
+  for (int a = 0; a < nn1 && !found; a++) {             // alignedFaces (:2019-2031)
+    for (int b = 0; b < nn2 && !found; b++) {
+      if (dot3(n1 + 3*a, n2 + 3*b) < -CCD_FACE_TOL) {
+        i = a;
+        j = b;
+        found = true;
+      }
+    }
+  }
+  // alignedFaceEdge (:2036-2048): the first (face, edge) pair within the tolerance
+  auto faceEdge = [&](const double* edge, int ne, const double* face, int nfc) MJH_LAMBDA_INLINE {
+    for (int a = 0; a < nfc; a++) {
+      for (int b = 0; b < ne; b++) {
+        if (fabs(dot3(edge + 3*b, face + 3*a)) < CCD_EDGE_TOL) {
+          i = b;
+          j = a;
+          return true;
+        }
+      }
+    }
+    return false;
+  };
+  if (!found) {
+    if (nf1 < 3 && nf1 <= nf2) {
+      nn1 = ccdBoxEdgeNormals(n1, ends, nf1, A, v11, v12, v11i);
+      if (!faceEdge(n1, nn1, n2, nn2)) return;
+      edge1 = true;
+    } else if (nf2 < 3) {
+      nn2 = ccdBoxEdgeNormals(n2, ends, nf2, B, v21, v22, v21i);
+      if (!faceEdge(n2, nn2, n1, nn1)) return;
+      edge2 = true;
+    } else {
+      return;
+    }
+  }
+  if (edge1) {
+    copy3(face1, w[0] + 3);
+    copy3(face1 + 3, ends + 3*i);
+    nf1 = 2;
+  } else {
+    nf1 = ccdBoxFace(face1, A, edge2 ? idx1[j] : idx1[i]);
+  }
+  if (edge2) {
+    copy3(face2, w[0] + 6);
+    copy3(face2 + 3, ends + 3*i);
+    nf2 = 2;
+  } else {
+    nf2 = ccdBoxFace(face2, B, idx2[j]);
+  }
+  double diff[3], dir[3];
+  sub3(diff, st.x2, st.x1);
+  const double nd = sqrt(dot3(diff, diff));
+  if (edge1) {
+    scl3(dir, n2 + 3*j, nd);
+    ccdPolygonClip(C, face2, nf2, face1, nf1, n2 + 3*j, dir);
+  } else if (edge2) {
+    scl3(dir, n1 + 3*j, -nd);
+    ccdPolygonClip(C, face1, nf1, face2, nf2, n1 + 3*j, dir);
+  } else {
+    scl3(dir, n2 + 3*j, nd);
+    ccdPolygonClip(C, face1, nf1, face2, nf2, n1 + 3*i, dir);
+  }
+}
+
 // mjc_ccd (:2215-2343) with max_contacts `maxc` (1: mjc_Convex and mj_geomDistanceCCD; 0: the
 // distance alone, no penetration recovery, mjhip_ccdBatch) and the distance cutoff `cutoff`
 // (0 for mjc_Convex's contacts, the bound for mj_geomDistanceCCD)
-template <int S>
+template <int S, bool MULTI = false>
 MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B, int kmax,
-                     double tol, double cutoff, int maxc = 1) {
+                     double tol, double cutoff, int maxc = 1, CcdContacts* multi = nullptr) {
   ccdCenter(st.x1, A);
   ccdCenter(st.x2, B);
   st.iters = 0;
@@ -3127,7 +3503,10 @@ MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B,
     const int ret = st.nsimplex == 2 ? ccdFromSegment(M, P, st, A, B) :
                     st.nsimplex == 3 ? ccdFromTriangle(M, P, st, A, B) :
                                        ccdFromTetra(M, P, st, A, B);
-    if (!ret) ccdEpa(st, M, P, A, B);
+    if (!ret) {
+      const int f = ccdEpa(st, M, P, A, B);
+      if (MULTI && maxc > 1 && f >= 0) ccdMultiContact(*multi, st, M, f, A, B);
+    }
   }
   return st.dist;
 }
@@ -3163,9 +3542,12 @@ MJH_HD long ccdScratchInts(int N) { return 13L*(6*N + 6); }
 
 // mjc_ccd (engine_collision_gjk.c:2215-2343, MJAPI) as the reference's own tests call it
 // (engine_collision_gjk_test.cc:62-84 GeomDist, :86-150 Penetration): geoms g1, g2 of m at the
-// given frames, object margin `margin` on both (mjc_initCCDObj), config {N, tol, maxc (0 or 1),
-// cutoff}, contiguous scratch x / xi (ccdScratchDoubles / Ints). out: dist, nx, x1[3], x2[3].
-// Returns 0, or 1 when the polytope outgrew the face capacity (MJHIP_INST_UNSUPPORTED).
+// given frames, object margin `margin` on both (mjc_initCCDObj), config {N, tol, maxc,
+// cutoff}, contiguous scratch x / xi (ccdScratchDoubles / Ints). out (2 + 6 CCD_MAXCON): dist,
+// nx, x1[3 CCD_MAXCON], x2[3 CCD_MAXCON]; MULTI: maxc > 1 runs multicontact. Returns 0, 1
+// when the polytope outgrew the face capacity, 2 for a multicontact outside the built subset
+// (a mesh).
+template <bool MULTI = false>
 MJH_HD int ccdGeneral(const mjhipModel& m, int g1, int g2, const double* pos1,
                       const double* mat1, const double* pos2, const double* mat2,
                       double margin, int N, double tol, int maxc, double cutoff, double* x,
@@ -3186,14 +3568,19 @@ MJH_HD int ccdGeneral(const mjhipModel& m, int g1, int g2, const double* pos1,
   }
   CcdState st;
   st.nx = 0;
-  const double dist = ccdRun(st, M, sh[0], sh[1], N, tol, cutoff, maxc);
+  CcdContacts C{out + 2, out + 2 + 3*CCD_MAXCON, 0, maxc, 0};
+  const double dist = ccdRun<1, MULTI>(st, M, sh[0], sh[1], N, tol, cutoff, maxc, &C);
   out[0] = dist;
-  out[1] = st.nx;
-  for (int k = 0; k < 3; k++) {
-    out[2 + k] = st.x1[k];
-    out[5 + k] = st.x2[k];
+  if (MULTI && C.nx) {
+    out[1] = C.nx;                                      // the polygon's contacts, in place
+  } else {
+    out[1] = st.nx;
+    for (int k = 0; k < 3; k++) {
+      out[2 + k] = st.x1[k];
+      out[2 + 3*CCD_MAXCON + k] = st.x2[k];
+    }
   }
-  return st.unsupported ? 1 : 0;
+  return st.unsupported ? 1 : (C.bad ? 2 : 0);
 }
 
 // mjc_Convex through mjc_CCDIteration (convex.c:792-819, :915-1001): 0 or 1 contacts

@@ -29,6 +29,12 @@ struct FastKernelEntry {
   // batched mj_inverseSkip(skipstage) for skipstage POS (k_va) or VEL (k_acc) over [0, B)
   // (qfrc_out row-major or null, status or null, efc_count)
   void (*launch_skip)(hipStream_t, const Mirror&, int, int, double*, int*, int*);
+  // models whose rows serve every instance (contacts): the straight-line pipeline in two
+  // launches, part 0 the position stage (k_spos), part 1 the fac and va stages (k_sfv), so
+  // that the cooperative constraint kernel runs beside part 1 on a second stream (arguments:
+  // B, part, qpos/qvel/qacc row-major inputs or null, status, worklist_next, efc_count)
+  void (*launch_split)(hipStream_t, const Mirror&, int, int, const double*, const double*,
+                       const double*, int*, int*, int*);
 };
 
 // the bundled models' kernels (gen_fast.hip), terminated by an entry with launch = nullptr

@@ -68,7 +68,11 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
                                                         const unsigned long long* __restrict__ masks,
                                                         int npair,
                                                         double* __restrict__ qfrc_out,
-                                                        int* __restrict__ status) {
+                                                        int* __restrict__ status,
+                                                        int* __restrict__ cstat) {
+  // cstat non-null: a split launch (mjhip.hip launch_inverse) running beside the fac / va
+  // stages: qfrc_constraint and this kernel's status bits (into cstat) only, k_assemble
+  // forms qfrc_inverse after both
   constexpr int IPB = 64 / G;               // instances per wave
   const long n = LIST ? (long)*count : (long)B;
   const long bid = xcdBlock(blockIdx.x, gridDim.x);
@@ -469,12 +473,13 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
       const int j1 = j0 + G;
       const bool has1 = j1 < nv;
       // the assembly's inputs, loaded ahead of the rows (a load issued after this lane's
-      // stores would wait for them)
-      const double rne0 = d.qfrc_inverse[j0], arm0 = m.dof_armature[j0];
-      const double pas0 = d.qfrc_passive[j0], qa0 = cdq[8*j0 + 7];
-      const double rne1 = has1 ? (double)d.qfrc_inverse[j1] : 0.0;
+      // stores would wait for them); a split launch assembles in k_assemble
+      const bool asmb = !cstat;
+      const double rne0 = asmb ? (double)d.qfrc_inverse[j0] : 0.0, arm0 = m.dof_armature[j0];
+      const double pas0 = asmb ? (double)d.qfrc_passive[j0] : 0.0, qa0 = cdq[8*j0 + 7];
+      const double rne1 = (asmb && has1) ? (double)d.qfrc_inverse[j1] : 0.0;
       const double arm1 = has1 ? m.dof_armature[j1] : 0.0;
-      const double pas1 = has1 ? (double)d.qfrc_passive[j1] : 0.0;
+      const double pas1 = (asmb && has1) ? (double)d.qfrc_passive[j1] : 0.0;
       const double qa1 = has1 ? cdq[8*j1 + 7] : 0.0;
       double acc0 = 0, acc1 = 0;
       for (int r0 = 0; r0 < nefc; r0 += 8) {
@@ -498,19 +503,21 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
           }
         }
       }
-      const double out0 = rne0 + (arm0 * qa0 - pas0 - acc0);
       d.qfrc_constraint[j0] = acc0;
+      if (has1) d.qfrc_constraint[j1] = acc1;
+      if (!asmb) continue;
+      const double out0 = rne0 + (arm0 * qa0 - pas0 - acc0);
       d.qfrc_inverse[j0] = out0;
       if (qfrc_out) qfrc_out[inst*nv + j0] = out0;
       if (has1) {
         const double out1 = rne1 + (arm1 * qa1 - pas1 - acc1);
-        d.qfrc_constraint[j1] = acc1;
         d.qfrc_inverse[j1] = out1;
         if (qfrc_out) qfrc_out[inst*nv + j1] = out1;
       }
     }
     for (int o = G/2; o; o >>= 1) st |= __shfl_xor(st, o, G);
-    if (sub == 0 && status && st) status[inst] |= st;
+    if (sub == 0 && cstat) cstat[inst] = st;
+    else if (sub == 0 && status && st) status[inst] |= st;
   }
   MJH_PHASE(17);
   __syncthreads();                          // the group's LDS is reused by the next round
@@ -523,14 +530,14 @@ template __global__ void k_constraint<false, true, false>(mjhipModel, Mirror, in
 template __global__ void k_constraint<false, false, false>(mjhipModel, Mirror, int, const int*, const int*, double*, int*);
 template __global__ void k_constraint<false, true, true>(mjhipModel, Mirror, int, const int*, const int*, double*, int*);
 template __global__ void k_constraint<false, false, true>(mjhipModel, Mirror, int, const int*, const int*, double*, int*);
-template __global__ void k_constraint_coop<16, true, true, true>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-template __global__ void k_constraint_coop<16, true, false, true>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-template __global__ void k_constraint_coop<16, true, true, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-template __global__ void k_constraint_coop<16, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-template __global__ void k_constraint_coop<16, false, true, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-template __global__ void k_constraint_coop<16, false, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
+template __global__ void k_constraint_coop<16, true, true, true>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+template __global__ void k_constraint_coop<16, true, false, true>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+template __global__ void k_constraint_coop<16, true, true, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+template __global__ void k_constraint_coop<16, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+template __global__ void k_constraint_coop<16, false, true, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+template __global__ void k_constraint_coop<16, false, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
 // lane-count variants of the contact path (MJHIP_COOP_LANES=8 / 32, measurement only)
-template __global__ void k_constraint_coop<8, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-template __global__ void k_constraint_coop<32, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
+template __global__ void k_constraint_coop<8, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+template __global__ void k_constraint_coop<32, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
 
 MJHIP_TIMER_SETTER(mjhip_setTimerBufConstraint)

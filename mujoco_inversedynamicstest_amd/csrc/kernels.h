@@ -126,7 +126,8 @@ __global__ __launch_bounds__(64) void k_constraint_coop(mjhipModel m, Mirror mr,
                                                         const unsigned long long* __restrict__ masks,
                                                         int npair,
                                                         double* __restrict__ qfrc_out,
-                                                        int* __restrict__ status);
+                                                        int* __restrict__ status,
+                                                        int* __restrict__ cstat);
 template <int SKIP, bool CONTACT, bool FUSED>
 __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
                                                 const double* __restrict__ qpos_in,
@@ -143,12 +144,12 @@ extern template __global__ void k_constraint<false, true, false>(mjhipModel, Mir
 extern template __global__ void k_constraint<false, false, false>(mjhipModel, Mirror, int, const int*, const int*, double*, int*);
 extern template __global__ void k_constraint<false, true, true>(mjhipModel, Mirror, int, const int*, const int*, double*, int*);
 extern template __global__ void k_constraint<false, false, true>(mjhipModel, Mirror, int, const int*, const int*, double*, int*);
-extern template __global__ void k_constraint_coop<16, true, true, true>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-extern template __global__ void k_constraint_coop<16, true, false, true>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-extern template __global__ void k_constraint_coop<16, true, true, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-extern template __global__ void k_constraint_coop<16, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-extern template __global__ void k_constraint_coop<16, false, true, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-extern template __global__ void k_constraint_coop<16, false, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
+extern template __global__ void k_constraint_coop<16, true, true, true>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+extern template __global__ void k_constraint_coop<16, true, false, true>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+extern template __global__ void k_constraint_coop<16, true, true, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+extern template __global__ void k_constraint_coop<16, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+extern template __global__ void k_constraint_coop<16, false, true, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+extern template __global__ void k_constraint_coop<16, false, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
 extern template __global__ void k_inverse<0, true, false>(mjhipModel, Mirror, int, const double*, const double*, const double*, double*, int*, int);
 extern template __global__ void k_inverse<0, false, false>(mjhipModel, Mirror, int, const double*, const double*, const double*, double*, int*, int);
 extern template __global__ void k_inverse<1, true, false>(mjhipModel, Mirror, int, const double*, const double*, const double*, double*, int*, int);

@@ -29,8 +29,8 @@
 #include "kernels.h"
 #include "pair_program.h"
 // lane-count variants of the cooperative kernel (kern_constraint.hip), measurement only
-extern template __global__ void k_constraint_coop<8, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
-extern template __global__ void k_constraint_coop<32, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*);
+extern template __global__ void k_constraint_coop<8, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
+extern template __global__ void k_constraint_coop<32, true, false, false>(mjhipModel, Mirror, int, const int*, const int*, const CoopPair*, const mjh::ContactParam*, const unsigned long long*, int, double*, int*, int*);
 #include "post_pass.h"
 
 //==================================== kernels ===============================================
@@ -93,13 +93,16 @@ __global__ __launch_bounds__(64) void k_check(mjhipModel m, Mirror mr, int B,
 // previous call), left the raw mj_rne(flg_acc = 1) in qfrc_inverse. Here those instances
 // finish as the reference does on the rows it kept: mj_referenceConstraint when the velocity
 // stage ran (POS), mj_invConstraint, then the assembly (engine_inverse.c:169-252).
+// all != 0: a model whose rows serve every instance (contacts): the straight-line stage
+// stored the raw RNE for every instance, which is assembled here, rows or none
+// (mj_invConstraint with nefc = 0 zeroes qfrc_constraint, engine_inverse.c:168-177)
 __global__ __launch_bounds__(64) void k_skip_rows(mjhipModel m, Mirror mr, int B, int skipstage,
-                                                  double* __restrict__ qfrc_out) {
+                                                  double* __restrict__ qfrc_out, int all) {
   const long inst = (long)blockIdx.x*64 + threadIdx.x;
   if (inst >= B) return;
   Lane<64> d = lane_view(mr, blockIdx.x, threadIdx.x);
-  if (!d.efc_count[0]) return;
-  if (skipstage == mjhipSTAGE_POS) mjh::referenceConstraint(m, d);
+  if (!d.efc_count[0] && !all) return;
+  if (d.efc_count[0] && skipstage == mjhipSTAGE_POS) mjh::referenceConstraint(m, d);
   mjh::invConstraint(m, d);
   for (int i = 0; i < m.nv; i++) {
     d.qfrc_inverse[i] += m.dof_armature[i] * d.qacc[i] - d.qfrc_passive[i] -
@@ -343,8 +346,31 @@ __global__ void k_fd_diff(mjhipModel m, Mirror mr, int nbase, double eps, int fl
   }
 }
 
+// the mj_inverse assembly of a split launch (k_spos, then k_sfv beside k_constraint_coop on
+// the second stream): qfrc_inverse = rne + ((armature*qacc - passive) - constraint), in the
+// reference's order and with k_constraint_coop's own expression (engine_inverse.c:132-153),
+// the constraint kernel's status bits, and the row-major output through LDS (coalesced)
+// One thread per (instance, dof), block (blk, dof k) over the block's 64 instances: the mirror
+// reads are whole 512-byte lines; the row-major writes of a block land in one 64 nv region.
+__global__ __launch_bounds__(64) void k_assemble(mjhipModel m, Mirror mr, int B,
+                                                 const int* __restrict__ cstat,
+                                                 double* __restrict__ qfrc_out,
+                                                 int* __restrict__ status) {
+  const int nv = m.nv, blk = blockIdx.x / nv, k = blockIdx.x % nv, lane = threadIdx.x;
+  const long inst = (long)blk*64 + lane;
+  if (inst >= B) return;
+  const long e = ((long)blk*nv + k)*64 + lane;       // the mirror's [blk][k][lane] element
+  const double out = mr.qfrc_inverse[e] + (m.dof_armature[k] * mr.qacc[e] -
+                                           mr.qfrc_passive[e] - mr.qfrc_constraint[e]);
+  mr.qfrc_inverse[e] = out;
+  if (qfrc_out) qfrc_out[inst*nv + k] = out;
+  if (k == 0 && status && cstat[inst]) status[inst] |= cstat[inst];
+}
+
 // mjhip_ccdBatch: mjc_ccd on pair i's geoms at its frames (in: 24 doubles per pair, pos1,
-// mat1, pos2, mat2; out: 8 per pair, dist, nx, x1, x2), scratch contiguous per pair
+// mat1, pos2, mat2; out: kCcdOut per pair, dist, nx, x1[3 mjMAXCONPAIR], x2[...]), scratch
+// contiguous per pair; bad[i]: 1 polytope capacity, 2 multicontact outside the subset
+constexpr long kCcdOut = 2 + 6*mjh::CCD_MAXCON;
 __global__ __launch_bounds__(64) void k_ccd(mjhipModel m, int n, const int* __restrict__ g1,
                                             const int* __restrict__ g2,
                                             const double* __restrict__ in,
@@ -355,11 +381,10 @@ __global__ __launch_bounds__(64) void k_ccd(mjhipModel m, int n, const int* __re
   const int i = blockIdx.x*64 + threadIdx.x;
   if (i >= n) return;
   const double* f = in + 24L*i;
-  if (mjh::ccdGeneral(m, g1[i], g2[i], f, f + 3, f + 12, f + 15, margin ? margin[i] : 0.0, N,
-                      tol, maxc, cutoff, x + (long)i*mjh::ccdScratchDoubles(N),
-                      xi + (long)i*mjh::ccdScratchInts(N), out + 8L*i)) {
-    bad[i] = 1;
-  }
+  bad[i] = mjh::ccdGeneral<true>(m, g1[i], g2[i], f, f + 3, f + 12, f + 15,
+                                 margin ? margin[i] : 0.0, N, tol, maxc, cutoff,
+                                 x + (long)i*mjh::ccdScratchDoubles(N),
+                                 xi + (long)i*mjh::ccdScratchInts(N), out + kCcdOut*i);
 }
 
 // Constraint-free mj_forward over a batch (mjh::forwardSkip). Optional row-major qpos, qvel,
@@ -453,6 +478,11 @@ struct mjhipContext_ {
   int npair = 0;
   bool boxpair = false;                    // a box-box pair is in the program (coop LDS)
   int coop = 16;                           // lanes per instance of k_constraint_coop (0: off)
+  // the split launch (FastKernelEntry.launch_split): the cooperative constraint kernel on a
+  // second stream beside the fac/va stages, joined by k_assemble; created on first use
+  hipStream_t aux = nullptr;
+  hipEvent_t evpos = nullptr, evcon = nullptr;
+  int* cstat = nullptr;                    // the constraint kernel's status bits per instance
   bool spatial = false;                    // spatial tendons: k_tendon_after runs (post_pass.h)
   // a straight-line kernel specialized for this model at run time (mjhip_contextLoadKernel):
   // a gfx950 code object holding extern "C" k_all_<name>; rt.launch stays null
@@ -872,6 +902,13 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   const bool detached = !c->tbuf || timers_detach(c) == MJHIP_OK;
   if (g_timed_ctx == c) g_timed_ctx = nullptr;
   if (c->own_stream && c->stream) hipStreamDestroy(c->stream);
+  if (c->aux) {
+    hipStreamSynchronize(c->aux);
+    hipStreamDestroy(c->aux);
+  }
+  if (c->evpos) hipEventDestroy(c->evpos);
+  if (c->evcon) hipEventDestroy(c->evcon);
+  hipFree(c->cstat);
   if (c->ev0) hipEventDestroy(c->ev0);
   if (c->ev1) hipEventDestroy(c->ev1);
   if (c->tev0) hipEventDestroy(c->tev0);
@@ -943,11 +980,13 @@ MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g
                              mjtNum tolerance, int max_contacts, mjtNum dist_cutoff,
                              mjtNum* dist, int* nx, mjtNum* x1, mjtNum* x2) {
   if (!c || n < 0 || (n && (!g1 || !g2 || !pos1 || !mat1 || !pos2 || !mat2 || !dist || !nx ||
-                            !x1 || !x2)) || max_iterations < 1 || max_contacts < 0 ||
-      max_contacts > 1) {
-    set_error("mjhip_ccdBatch: bad argument (max_contacts must be 0 or 1)");
+                            !x1 || !x2)) || max_iterations < 1 || max_contacts < 0) {
+    set_error("mjhip_ccdBatch: bad argument");
     return MJHIP_ERR_ARG;
   }
+  // witness points kept per pair: mjCCDStatus holds mjMAXCONPAIR
+  const int xcap = max_contacts <= 1 ? 1 :
+                   (max_contacts < mjh::CCD_MAXCON ? max_contacts : mjh::CCD_MAXCON);
   if (!n) return MJHIP_OK;
   const int ng = c->hmodel.ngeom;
   for (int i = 0; i < n; i++) {            // every index the kernel reads, checked here
@@ -958,7 +997,7 @@ MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g
   }
   HIPCHECK(hipSetDevice(c->device));
   const long nd = mjh::ccdScratchDoubles(max_iterations), ni = mjh::ccdScratchInts(max_iterations);
-  std::vector<double> in(24L*n), out(8L*n);
+  std::vector<double> in(24L*n), out(kCcdOut*n);
   for (int i = 0; i < n; i++) {
     memcpy(&in[24L*i], pos1 + 3L*i, 3*sizeof(double));
     memcpy(&in[24L*i + 3], mat1 + 9L*i, 9*sizeof(double));
@@ -966,13 +1005,14 @@ MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g
     memcpy(&in[24L*i + 15], mat2 + 9L*i, 9*sizeof(double));
   }
   // one allocation: inputs, margins, outputs, scratch, then the int arrays
-  const size_t bytes = sizeof(double)*(24L*n + n + 8L*n + nd*n) + sizeof(int)*(2L*n + ni*n + n);
+  const size_t bytes = sizeof(double)*(24L*n + n + kCcdOut*n + nd*n) +
+                       sizeof(int)*(2L*n + ni*n + n);
   char* buf = nullptr;
   HIPCHECK(hipMalloc((void**)&buf, bytes));
   double* d_in = (double*)buf;
   double* d_margin = d_in + 24L*n;
   double* d_out = d_margin + n;
-  double* d_x = d_out + 8L*n;
+  double* d_x = d_out + kCcdOut*n;
   int* d_g = (int*)(d_x + nd*n);
   int* d_xi = d_g + 2L*n;
   int* d_bad = d_xi + ni*n;
@@ -991,7 +1031,7 @@ MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g
                        dist_cutoff, d_x, d_xi, d_out, d_bad);
     HIPCHECK(hipGetLastError());
     HIPCHECK(hipStreamSynchronize(c->stream));
-    HIPCHECK(hipMemcpy(out.data(), d_out, 8L*n*sizeof(double), hipMemcpyDeviceToHost));
+    HIPCHECK(hipMemcpy(out.data(), d_out, kCcdOut*n*sizeof(double), hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(bad.data(), d_bad, n*sizeof(int), hipMemcpyDeviceToHost));
     return MJHIP_OK;
   };
@@ -1000,13 +1040,17 @@ MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g
   if (rc) return rc;
   for (int i = 0; i < n; i++) {
     if (bad[i]) {
-      set_error("mjhip_ccdBatch: pair %d outgrew the solver's polytope capacity", i);
+      set_error(bad[i] == 1 ? "mjhip_ccdBatch: pair %d outgrew the solver's polytope capacity"
+                            : "mjhip_ccdBatch: pair %d needs multicontact on a mesh (its "
+                              "polygon data is not compiled)", i);
       return MJHIP_ERR_MODEL;
     }
-    dist[i] = out[8L*i];
-    nx[i] = (int)out[8L*i + 1];
-    memcpy(x1 + 3L*i, &out[8L*i + 2], 3*sizeof(double));
-    memcpy(x2 + 3L*i, &out[8L*i + 5], 3*sizeof(double));
+    const double* o = &out[kCcdOut*i];
+    dist[i] = o[0];
+    nx[i] = (int)o[1];
+    const int k = nx[i] < xcap ? (nx[i] > 1 ? nx[i] : 1) : xcap;
+    memcpy(x1 + 3L*xcap*i, o + 2, 3*k*sizeof(double));
+    memcpy(x2 + 3L*xcap*i, o + 2 + 3*mjh::CCD_MAXCON, 3*k*sizeof(double));
   }
   return MJHIP_OK;
 }
@@ -1040,6 +1084,49 @@ MJHIP_API int mjhip_contextSetStream(mjhipContext* c, void* stream) {
   return MJHIP_OK;
 }
 
+// the split launch of a contact model is opt-in (MJHIP_SPLIT=1): measured slower than the
+// one-stream path at config 4, kept for the experiment
+static bool split_disabled() {
+  const char* e = getenv("MJHIP_SPLIT");
+  return !(e && e[0] == '1');
+}
+
+// the split launch's second stream, its two events and the status-bit buffer (first use)
+static int split_ready(mjhipContext* c) {
+  if (c->aux) return MJHIP_OK;
+  HIPCHECK(hipMalloc((void**)&c->cstat, sizeof(int)*(size_t)c->capacity));
+  HIPCHECK(hipEventCreateWithFlags(&c->evpos, hipEventDisableTiming));
+  HIPCHECK(hipEventCreateWithFlags(&c->evcon, hipEventDisableTiming));
+  HIPCHECK(hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking));
+  return MJHIP_OK;
+}
+
+// the straight-line path's passes after the constraint part: sensors (and the transmission
+// and energy terms they carry), INVDISCRETE's qacc restore, the status checks; then the
+// work-list counters change hands
+static int finish_fast(mjhipContext* c, int B, dim3 grid, dim3 block, int skipsensor,
+                       int* status, bool discrete) {
+  const int sensors = !skipsensor && c->hmodel.nsensor > 0 &&
+                      !(c->hmodel.opt.disableflags & mjhipDSBL_SENSOR);
+  const int trn = mjh_needTrnAfter(&c->hmodel);
+  if (sensors || trn || (c->hmodel.opt.enableflags & mjhipENBL_ENERGY)) {
+    hipLaunchKernelGGL(k_sensors, grid, block, 0, c->stream, c->dmodel, c->mirror, B,
+                       sensors, trn);
+    HIPCHECK(hipGetLastError());
+  }
+  if (discrete) {                        // the caller's qacc back, after mj_sensorAcc
+    hipLaunchKernelGGL(k_discrete_restore, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
+  }
+  if (status) {
+    hipLaunchKernelGGL(k_check, grid, block, 0, c->stream, c->dmodel, c->mirror, B, status,
+                       (int)mjhipSTAGE_NONE);
+    HIPCHECK(hipGetLastError());
+  }
+  c->wl_last = c->wl_parity;
+  c->wl_parity ^= 1;
+  return MJHIP_OK;
+}
+
 // range: null, or a device-side instance range {first, end} for the straight-line kernel (B
 // then only sizes the grid: end - first <= B); only the FD fall-back uses it, on models whose
 // whole pipeline is the straight-line and constraint kernels
@@ -1061,6 +1148,47 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     // previous launch's k_pos, or at context creation) and zeroes `nxt` for the next one
     int* cnt = c->worklist + c->wl_parity;
     int* nxt = c->worklist + (c->wl_parity ^ 1);
+    const bool discrete = mjh::hasDiscrete(c->hmodel);
+    // fused rows whenever nbody allows, INVDISCRETE included (post_pass.h fastFusedOk)
+    const bool fused = mjh::fastFusedOk(c->dmodel);
+    if (c->fast->launch_split && !range && fused && c->coop && c->fast->cmode == 2 &&
+        c->con_cap > 0 && !c->spatial && !mjh::hasFluid(c->dmodel) && !discrete &&
+        !split_disabled()) {
+      // rows on every instance: the position stage, then the cooperative constraint kernel
+      // (position-stage outputs and inputs only) on the second stream beside the fac / va
+      // stages, joined by the assembly
+      if (const int rc = split_ready(c)) return rc;
+      c->last_path = 3;
+      const int* wl = c->worklist + 2;
+      c->fast->launch_split(c->stream, c->mirror, B, 0, qpos, qvel, qacc, status, nxt,
+                            c->mirror.efc_count);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipEventRecord(c->evpos, c->stream));
+      // the fac / va stages are queued first: their 64-lane waves need a whole SIMD's
+      // registers, which the constraint kernel's waves would otherwise take
+      c->fast->launch_split(c->stream, c->mirror, B, 1, nullptr, nullptr, nullptr, status, nxt,
+                            c->mirror.efc_count);
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipStreamWaitEvent(c->aux, c->evpos, 0));
+#define MJHIP_LAUNCH_COOP_SPLIT(G, X)                                                         \
+      hipLaunchKernelGGL((k_constraint_coop<G, true, false, X>), dim3(coopGrid(B, G, false)),   \
+                         dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap, c->boxpair,         \
+                                                      c->npair, c->con_cap),                  \
+                         c->aux, c->dmodel, c->mirror, B, wl, (const int*)cnt, c->pairs,      \
+                         c->cparams, c->masks, c->npair, nullptr, nullptr, c->cstat)
+      if (c->boxpair) MJHIP_LAUNCH_COOP_SPLIT(16, true);
+      else if (c->coop == 8) MJHIP_LAUNCH_COOP_SPLIT(8, false);
+      else if (c->coop == 32) MJHIP_LAUNCH_COOP_SPLIT(32, false);
+      else MJHIP_LAUNCH_COOP_SPLIT(16, false);
+#undef MJHIP_LAUNCH_COOP_SPLIT
+      HIPCHECK(hipGetLastError());
+      HIPCHECK(hipEventRecord(c->evcon, c->aux));
+      HIPCHECK(hipStreamWaitEvent(c->stream, c->evcon, 0));
+      hipLaunchKernelGGL(k_assemble, dim3(grid.x*c->hmodel.nv), block, 0, c->stream, c->dmodel,
+                         c->mirror, B, c->cstat, qfrc, status);
+      HIPCHECK(hipGetLastError());
+      return finish_fast(c, B, grid, block, skipsensor, status, false);
+    }
     if (c->fast->launch) {
       c->fast->launch(grid, block, c->stream, c->mirror, B, qpos, qvel, qacc, qfrc, status,
                       c->worklist + 2, cnt, nxt, c->mirror.efc_count, range);
@@ -1078,12 +1206,9 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     } else if (mjh::hasFluid(c->dmodel)) {   // fluid forces into qfrc_passive
       hipLaunchKernelGGL(k_fluid_after, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
     }
-    const bool discrete = mjh::hasDiscrete(c->hmodel);
     if (discrete) {                      // mj_discreteAcc and its RNE before the constraints
       hipLaunchKernelGGL(k_discrete_before, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
     }
-    // fused rows whenever nbody allows, INVDISCRETE included (post_pass.h fastFusedOk)
-    const bool fused = mjh::fastFusedOk(c->dmodel);
     const int* wl = c->worklist + 2;
     if (fused && c->coop && c->fast->cmode) {   // cooperative lanes per instance
       const bool contact = c->con_cap > 0, list = c->fast->cmode == 1;
@@ -1094,7 +1219,7 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
                          c->stream,                                                           \
                          c->dmodel, c->mirror, B, wl,                                         \
                          (const int*)cnt, c->pairs, c->cparams, c->masks, c->npair, qfrc,    \
-                         status)
+                         status, nullptr)
       if (contact && c->boxpair) {       // the box-box path is compiled in only here
         if (list) MJHIP_LAUNCH_COOP(16, true, true, true);
         else MJHIP_LAUNCH_COOP(16, true, false, true);
@@ -1127,26 +1252,7 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
 #undef MJHIP_LAUNCH_CON
     }
     HIPCHECK(hipGetLastError());
-    const int sensors = !skipsensor && c->hmodel.nsensor > 0 &&
-                        !(c->hmodel.opt.disableflags & mjhipDSBL_SENSOR);
-    const int trn = mjh_needTrnAfter(&c->hmodel);
-    if (sensors || trn || (c->hmodel.opt.enableflags & mjhipENBL_ENERGY)) {
-      hipLaunchKernelGGL(k_sensors, grid, block, 0, c->stream, c->dmodel, c->mirror, B,
-                         sensors, trn);
-      HIPCHECK(hipGetLastError());
-    }
-    if (discrete) {                      // the caller's qacc back, after mj_sensorAcc
-      hipLaunchKernelGGL(k_discrete_restore, grid, block, 0, c->stream, c->dmodel, c->mirror,
-                         B);
-    }
-    if (status) {
-      hipLaunchKernelGGL(k_check, grid, block, 0, c->stream, c->dmodel, c->mirror, B, status,
-                         (int)mjhipSTAGE_NONE);
-      HIPCHECK(hipGetLastError());
-    }
-    c->wl_last = c->wl_parity;
-    c->wl_parity ^= 1;
-    return MJHIP_OK;
+    return finish_fast(c, B, grid, block, skipsensor, status, discrete);
   }
   // mj_inverseSkip(POS / VEL) on the straight-line kernels: the bare pipeline (no passes
   // after the generated kernels) of a model whose rows serve only limit-active instances
@@ -1175,9 +1281,9 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     c->last_path = 2;
     c->fast->launch_skip(c->stream, c->mirror, B, skipstage, qfrc, status, c->mirror.efc_count);
     HIPCHECK(hipGetLastError());
-    if (c->fast->cmode == 1) {
+    if (c->fast->cmode) {                // work-list rows, or every instance (contacts)
       hipLaunchKernelGGL(k_skip_rows, grid, block, 0, c->stream, c->dmodel, c->mirror, B,
-                         skipstage, qfrc);
+                         skipstage, qfrc, (int)(c->fast->cmode == 2));
       HIPCHECK(hipGetLastError());
     }
     if (status) {

@@ -253,7 +253,8 @@ class InverseEngine:
   @property
   def last_path(self):
     """Kernels of the last batched inverse: 0 generic, 1 straight-line pipeline, 2 the
-    straight-line mj_inverseSkip(POS / VEL) kernels."""
+    straight-line mj_inverseSkip(POS / VEL) kernels, 3 the straight-line pipeline of a contact
+    model split over two streams."""
     return lib().mjhip_contextLastPath(self.ctx)
 
   def worklist_count(self):
@@ -374,7 +375,8 @@ class InverseEngine:
   def ccd(self, g1, g2, pos1, mat1, pos2, mat2, margin=None, max_iterations=1000,
           tolerance=1e-6, max_contacts=1, dist_cutoff=0.0):
     """mjc_ccd on the device over pairs (g1[i], g2[i]) at frames pos (n x 3) / mat (n x 9)
-    (mjhip_ccdBatch): (dist [n], nx [n], x1 [n, 3], x2 [n, 3])."""
+    (mjhip_ccdBatch): (dist [n], nx [n], x1 [n, 3], x2 [n, 3]); with max_contacts > 1, x1 / x2
+    are [n, min(max_contacts, 50), 3] (multicontact; the first nx[i] rows hold pair i's)."""
     g1 = np.ascontiguousarray(g1, dtype=np.int32)
     g2 = np.ascontiguousarray(g2, dtype=np.int32)
     n = g1.size
@@ -383,12 +385,15 @@ class InverseEngine:
     mg = None if margin is None else np.ascontiguousarray(
         np.broadcast_to(margin, (n,)), dtype=np.float64)
     dist, nx = np.zeros(n), np.zeros(n, dtype=np.int32)
-    x1, x2 = np.zeros((n, 3)), np.zeros((n, 3))
+    xcap = 1 if max_contacts <= 1 else min(max_contacts, 50)
+    x1, x2 = np.zeros((n, xcap, 3)), np.zeros((n, xcap, 3))
     D = lambda a: a.ctypes.data_as(_D)
     _check(lib().mjhip_ccdBatch(self.ctx, n, g1.ctypes.data_as(_I), g2.ctypes.data_as(_I),
                                 *map(D, f), D(mg) if mg is not None else None,
                                 max_iterations, tolerance, max_contacts, dist_cutoff, D(dist),
                                 nx.ctypes.data_as(_I), D(x1), D(x2)), "mjhip_ccdBatch")
+    if xcap == 1:
+      return dist, nx, x1[:, 0], x2[:, 0]
     return dist, nx, x1, x2
 
   def timers(self, enable=True):

@@ -2875,7 +2875,9 @@ int or_boxBoxRaw(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum
 
 enum { CCD_POINT = 100, CCD_LINE = 101 };      /* shrunken sphere / capsule supports */
 
-typedef struct { mjtNum v[3], p1[3], p2[3]; } orVtx;   /* Minkowski vertex, both witnesses */
+/* Minkowski vertex, both witnesses, and the box corner / mesh vertex each support returned
+   (Vertex.index1 / index2, gjk.h:51-57: the shape's vertindex after the support call) */
+typedef struct { mjtNum v[3], p1[3], p2[3]; int i1, i2; } orVtx;
 
 typedef struct {
   int kind;                /* mjtGeom of the geom, or CCD_POINT / CCD_LINE */
@@ -3040,11 +3042,12 @@ static void ccd_support1(mjtNum r[3], orShape* s, const mjtNum dir[3]) {
     t[2] = ccd_sign(ld[2])*s->size[1];
     break;
   }
-  default:   /* box */
+  default:   /* box; the corner's index for multicontact (mjc_boxSupport :314-323) */
     ccd_toLocal(ld, s->mat, dir);
     t[0] = (ld[0] >= 0 ? 1 : -1)*s->size[0];
     t[1] = (ld[1] >= 0 ? 1 : -1)*s->size[1];
     t[2] = (ld[2] >= 0 ? 1 : -1)*s->size[2];
+    s->vertindex = (t[0] > 0 ? 1 : 0) | (t[1] > 0 ? 2 : 0) | (t[2] > 0 ? 4 : 0);
     break;
   }
   ccd_toGlobal(r, s->mat, t, s->pos);
@@ -3068,6 +3071,8 @@ static void ccd_support(orVtx* v, orShape* a, orShape* b, const mjtNum dir[3],
     v->p2[2] += ndir[2]*h;
   }
   mju_sub3(v->v, v->p1, v->p2);
+  v->i1 = a->vertindex;       /* gjkSupport / epaSupport (:316-322, :346-351) */
+  v->i2 = b->vertindex;
 }
 
 static mjtNum ccd_det3(const mjtNum a[3], const mjtNum b[3], const mjtNum c[3]) {
@@ -3269,10 +3274,12 @@ static void ccd_S3D(mjtNum lam[4], const mjtNum a[3], const mjtNum b[3], const m
 }
 
 /* the solver state of one mjc_ccd call (mjCCDStatus, gjk.h:70-89, the fields this path uses) */
+#define OR_MAXCONPAIR 50       /* mjMAXCONPAIR: the status's witness capacity */
 typedef struct {
-  mjtNum dist, x1[3], x2[3];
+  mjtNum dist, x1[3*OR_MAXCONPAIR], x2[3*OR_MAXCONPAIR];
   int nx, iters, nsimplex;
-  int kmax;
+  int kmax, maxc;
+  int unsupported;          /* multicontact on a mesh (its polygon data is not compiled) */
   mjtNum tol, cutoff;
   orVtx simplex[4];
 } orCCD;
@@ -3444,6 +3451,8 @@ static int ccd_addVertex(orPoly* P, const orVtx* v) {
   orVtx* t = P->vtx + P->nvtx;
   mju_copy3(t->p1, v->p1);
   mju_copy3(t->p2, v->p2);
+  t->i1 = v->i1;
+  t->i2 = v->i2;
   mju_sub3(t->v, v->p1, v->p2);
   return P->nvtx++;
 }
@@ -3785,6 +3794,406 @@ static void ccd_center(mjtNum c[3], const orShape* s) {
   }
 }
 
+/*------------------ multicontact (engine_collision_gjk.c:1460-2193) ------------------------
+ * With max_contacts > 1 the EPA's final face is turned into a contact polygon: the feature
+ * (vertex, edge or face) of each geom the face's three vertices span, the geoms' face normals
+ * around it, a pair of anti-aligned faces (or an edge perpendicular to a face), and the
+ * clipping of one face polygon by the other. Boxes are restated; a mesh needs the compiler's
+ * polygon data (mesh_polynormal, mesh_polymap, ...), which this compiler does not build, so
+ * a mesh sets st->unsupported and keeps the single contact. */
+#define OR_FACE_TOL 0.99999872      /* mjFACE_TOL (gjk.h:29) */
+#define OR_EDGE_TOL 0.00159999931   /* mjEDGE_TOL (gjk.h:32) */
+#define OR_MAX_POLYVERT 150         /* mjMAX_POLYVERT (gjk.h:35) */
+
+static mjtNum mc_dot3(const mjtNum a[3], const mjtNum b[3]) {
+  return a[0]*b[0] + a[1]*b[1] + a[2]*b[2];
+}
+
+/* equal3 (:116-120) */
+static int mc_equal3(const mjtNum a[3], const mjtNum b[3]) {
+  return fabs(a[0] - b[0]) < mjMINVAL && fabs(a[1] - b[1]) < mjMINVAL &&
+         fabs(a[2] - b[2]) < mjMINVAL;
+}
+
+/* area4 (:1463-1476) */
+static mjtNum mc_area4(const mjtNum a[3], const mjtNum b[3], const mjtNum c[3],
+                       const mjtNum d[3]) {
+  mjtNum ad[3] = {d[0] - a[0], d[1] - a[1], d[2] - a[2]};
+  mjtNum db[3] = {b[0] - d[0], b[1] - d[1], b[2] - d[2]};
+  mjtNum bc[3] = {c[0] - b[0], c[1] - b[1], c[2] - b[2]};
+  mjtNum ca[3] = {a[0] - c[0], a[1] - c[1], a[2] - c[2]};
+  mjtNum e[3], f[3], g[3];
+  mju_cross(e, ad, db);
+  mju_cross(f, bc, ca);
+  mju_add3(g, e, f);
+  return 0.5 * sqrt(mc_dot3(g, g));
+}
+
+/* next (:1481-1486), on vertex indices */
+static int mc_next(int nvert, int i) { return i == nvert - 1 ? 0 : i + 1; }
+
+/* polygonQuad (:1491-1535): the maximum-area quadrilateral, as vertex indices */
+static void mc_polygonQuad(int res[4], const mjtNum* poly, int nvert) {
+  int a = 0, b = 1, c = 2, d = 3;
+  res[0] = a; res[1] = b; res[2] = c; res[3] = d;
+  mjtNum m = mc_area4(poly + 3*a, poly + 3*b, poly + 3*c, poly + 3*d), mn;
+  for (; a < nvert; a++) {
+    while (1) {
+      mn = mc_area4(poly + 3*a, poly + 3*b, poly + 3*c, poly + 3*mc_next(nvert, d));
+      if (mn <= m) break;
+      m = mn;
+      d = mc_next(nvert, d);
+      res[0] = a; res[1] = b; res[2] = c; res[3] = d;
+      while (1) {
+        mn = mc_area4(poly + 3*a, poly + 3*b, poly + 3*mc_next(nvert, c), poly + 3*d);
+        if (mn <= m) break;
+        m = mn;
+        c = mc_next(nvert, c);
+        res[0] = a; res[1] = b; res[2] = c; res[3] = d;
+      }
+      while (1) {
+        mn = mc_area4(poly + 3*a, poly + 3*mc_next(nvert, b), poly + 3*c, poly + 3*d);
+        if (mn <= m) break;
+        m = mn;
+        b = mc_next(nvert, b);
+        res[0] = a; res[1] = b; res[2] = c; res[3] = d;
+      }
+    }
+    if (b == a) {
+      b = mc_next(nvert, b);
+      if (c == b) {
+        c = mc_next(nvert, c);
+        if (d == c) d = mc_next(nvert, d);
+      }
+    }
+  }
+}
+
+/* planeNormal (:1540-1549) */
+static mjtNum mc_planeNormal(mjtNum res[3], const mjtNum v1[3], const mjtNum v2[3],
+                             const mjtNum n[3]) {
+  mjtNum v3[3], d1[3], d2[3];
+  mju_add3(v3, v1, n);
+  mju_sub3(d1, v2, v1);
+  mju_sub3(d2, v3, v1);
+  mju_cross(res, d1, d2);
+  return mc_dot3(res, v1);
+}
+
+/* halfspace (:1553-1557) */
+static int mc_halfspace(const mjtNum a[3], const mjtNum n[3], const mjtNum p[3]) {
+  mjtNum diff[3] = {p[0] - a[0], p[1] - a[1], p[2] - a[2]};
+  return mc_dot3(diff, n) > 0;
+}
+
+/* planeIntersect (:1561-1574) */
+static mjtNum mc_planeIntersect(mjtNum res[3], const mjtNum pn[3], mjtNum pd, const mjtNum a[3],
+                                const mjtNum b[3]) {
+  mjtNum ab[3];
+  mju_sub3(ab, b, a);
+  mjtNum temp = mc_dot3(pn, ab);
+  if (temp == 0.0) return mjhipMAXVAL;
+  mjtNum t = (pd - mc_dot3(pn, a)) / temp;
+  if (t >= 0.0 && t <= 1.0) {
+    res[0] = a[0] + t*ab[0];
+    res[1] = a[1] + t*ab[1];
+    res[2] = a[2] + t*ab[2];
+  }
+  return t;
+}
+
+/* polygonClip (:1579-1690): face2 clipped by the edge planes of face1 (normal n); the
+   vertices become the contacts' x2, x1 = x2 - dir */
+static void mc_polygonClip(orCCD* st, const mjtNum* face1, int nface1, const mjtNum* face2,
+                           int nface2, const mjtNum n[3], const mjtNum dir[3]) {
+  if (nface1 < 3) return;
+  mjtNum pn[3*OR_MAX_POLYVERT], pd[OR_MAX_POLYVERT];
+  for (int i = 0; i < nface1 - 1; i++) {
+    pd[i] = mc_planeNormal(pn + 3*i, face1 + 3*i, face1 + 3*i + 3, n);
+  }
+  pd[nface1 - 1] = mc_planeNormal(pn + 3*(nface1 - 1), face1 + 3*(nface1 - 1), face1, n);
+  mjtNum buf1[6*OR_MAX_POLYVERT], buf2[6*OR_MAX_POLYVERT];
+  mjtNum *polygon = buf1, *clipped = buf2;
+  int npolygon = nface2, nclipped = 0;
+  for (int i = 0; i < nface2; i++) mju_copy3(polygon + 3*i, face2 + 3*i);
+  for (int e = 0; e < 3*nface1; e += 3) {
+    for (int i = 0; i < npolygon; i++) {
+      mjtNum* P = polygon + 3*i;
+      mjtNum* Q = (i < npolygon - 1) ? polygon + 3*(i + 1) : polygon;
+      int in1 = mc_halfspace(face1 + e, pn + e, P);
+      int in2 = mc_halfspace(face1 + e, pn + e, Q);
+      if (!in1 && !in2) continue;
+      if (in1 && in2) {
+        mju_copy3(clipped + 3*nclipped++, Q);
+        continue;
+      }
+      mjtNum t = mc_planeIntersect(clipped + 3*nclipped++, pn + e, pd[e/3], P, Q);
+      if (t < 0.0 || t > 1.0) nclipped--;
+      if (in2) mju_copy3(clipped + 3*nclipped++, Q);
+    }
+    mjtNum* tmp = polygon;
+    polygon = clipped;
+    clipped = tmp;
+    npolygon = nclipped;
+    nclipped = 0;
+  }
+  if (npolygon < 1) return;
+  if (st->maxc < 5 && npolygon > 4) {
+    int rect[4];
+    mc_polygonQuad(rect, polygon, npolygon);
+    st->nx = 4;
+    for (int i = 0; i < 4; i++) {
+      mju_copy3(st->x2 + 3*i, polygon + 3*rect[i]);
+      mju_sub3(st->x1 + 3*i, st->x2 + 3*i, dir);
+    }
+    return;
+  }
+  if (npolygon > OR_MAXCONPAIR) {
+    st->nx = OR_MAXCONPAIR;
+    for (int i = 0; i < 3*OR_MAXCONPAIR; i += 3) {
+      mju_copy3(st->x2 + i, polygon + i);
+      mju_sub3(st->x1 + i, st->x2 + i, dir);
+    }
+    return;
+  }
+  int k = 0;
+  for (int i = 0; i < 3*npolygon; i += 3) {
+    int skip = 0;
+    for (int j = 0; j < k; j += 3) {
+      if (mc_equal3(st->x2 + j, polygon + i)) {
+        skip = 1;
+        break;
+      }
+    }
+    if (skip) continue;
+    mju_copy3(st->x2 + k, polygon + i);
+    mju_sub3(st->x1 + k, st->x2 + k, dir);
+    k += 3;
+  }
+  st->nx = k/3;
+}
+
+/* globalcoord (:1695-1707) */
+static void mc_global(mjtNum res[3], const mjtNum* mat, const mjtNum* pos, mjtNum l1, mjtNum l2,
+                      mjtNum l3) {
+  res[0] = mat[0]*l1 + mat[1]*l2 + mat[2]*l3;
+  res[1] = mat[3]*l1 + mat[4]*l2 + mat[5]*l3;
+  res[2] = mat[6]*l1 + mat[7]*l2 + mat[8]*l3;
+  if (pos) {
+    res[0] += pos[0];
+    res[1] += pos[1];
+    res[2] += pos[2];
+  }
+}
+
+/* boxNormals (:1846-1899) */
+static int mc_boxNormals(mjtNum res[9], int resind[3], int dim, const orShape* s, int v1, int v2,
+                         int v3) {
+  const mjtNum* mat = s->mat;
+  if (dim == 3) {
+    int x = ((v1 & 1) && (v2 & 1) && (v3 & 1)) - (!(v1 & 1) && !(v2 & 1) && !(v3 & 1));
+    int y = ((v1 & 2) && (v2 & 2) && (v3 & 2)) - (!(v1 & 2) && !(v2 & 2) && !(v3 & 2));
+    int z = ((v1 & 4) && (v2 & 4) && (v3 & 4)) - (!(v1 & 4) && !(v2 & 4) && !(v3 & 4));
+    mc_global(res, mat, NULL, x, y, z);
+    int sgn = x + y + z;
+    if (x) resind[0] = 0;
+    if (y) resind[0] = 2;
+    if (z) resind[0] = 4;
+    if (sgn == -1) resind[0]++;
+    return 1;
+  }
+  if (dim == 2) {
+    int x = ((v1 & 1) && (v2 & 1)) - (!(v1 & 1) && !(v2 & 1));
+    int y = ((v1 & 2) && (v2 & 2)) - (!(v1 & 2) && !(v2 & 2));
+    int z = ((v1 & 4) && (v2 & 4)) - (!(v1 & 4) && !(v2 & 4));
+    if (x) {
+      mc_global(res, mat, NULL, x, 0, 0);
+      resind[0] = (x > 0) ? 0 : 1;
+    }
+    if (y) {
+      int i = (x ? 1 : 0);
+      mc_global(res + 3*i, mat, NULL, 0, y, 0);
+      resind[i] = (y > 0) ? 2 : 3;
+    }
+    if (z) {
+      mc_global(res + 3, mat, NULL, 0, 0, z);
+      resind[1] = (z > 0) ? 4 : 5;
+    }
+    return 2;
+  }
+  if (dim == 1) {
+    mjtNum x = (v1 & 1) ? 1 : -1, y = (v1 & 2) ? 1 : -1, z = (v1 & 4) ? 1 : -1;
+    mc_global(res + 0, mat, NULL, x, 0, 0);
+    mc_global(res + 3, mat, NULL, 0, y, 0);
+    mc_global(res + 6, mat, NULL, 0, 0, z);
+    resind[0] = (x > 0) ? 0 : 1;
+    resind[1] = (y > 0) ? 2 : 3;
+    resind[2] = (z > 0) ? 4 : 5;
+    return 3;
+  }
+  return 0;
+}
+
+/* boxEdgeNormals (:1903-1938) */
+static int mc_boxEdgeNormals(mjtNum res[9], mjtNum endverts[9], int dim, const orShape* s,
+                             const mjtNum v1[3], const mjtNum v2[3], int v1i) {
+  const mjtNum *mat = s->mat, *pos = s->pos, *size = s->size;
+  if (dim == 2) {
+    mju_copy3(endverts, v2);
+    mju_sub3(res, v2, v1);
+    mju_normalize3(res);
+    return 1;
+  }
+  if (dim == 1) {
+    mjtNum x = (v1i & 1) ? size[0] : -size[0];
+    mjtNum y = (v1i & 2) ? size[1] : -size[1];
+    mjtNum z = (v1i & 4) ? size[2] : -size[2];
+    mc_global(endverts, mat, pos, -x, y, z);
+    mju_sub3(res, endverts, v1);
+    mju_normalize3(res);
+    mc_global(endverts + 3, mat, pos, x, -y, z);
+    mju_sub3(res + 3, endverts + 3, v1);
+    mju_normalize3(res + 3);
+    mc_global(endverts + 6, mat, pos, x, y, -z);
+    mju_sub3(res + 6, endverts + 6, v1);
+    mju_normalize3(res + 6);
+    return 3;
+  }
+  return 0;
+}
+
+/* boxFace (:1942-1990) */
+static int mc_boxFace(mjtNum res[12], const orShape* s, int idx) {
+  const mjtNum *mat = s->mat, *pos = s->pos, *z = s->size;
+  static const signed char corner[6][4][3] = {
+    {{ 1,  1,  1}, { 1,  1, -1}, { 1, -1, -1}, { 1, -1,  1}},     /* right */
+    {{-1,  1, -1}, {-1,  1,  1}, {-1, -1,  1}, {-1, -1, -1}},     /* left */
+    {{-1,  1, -1}, { 1,  1, -1}, { 1,  1,  1}, {-1,  1,  1}},     /* top */
+    {{-1, -1,  1}, { 1, -1,  1}, { 1, -1, -1}, {-1, -1, -1}},     /* bottom */
+    {{-1,  1,  1}, { 1,  1,  1}, { 1, -1,  1}, {-1, -1,  1}},     /* front */
+    {{ 1,  1, -1}, {-1,  1, -1}, {-1, -1, -1}, { 1, -1, -1}}};    /* back */
+  if (idx < 0 || idx > 5) return 0;
+  for (int k = 0; k < 4; k++) {
+    const signed char* c = corner[idx][k];
+    mc_global(res + 3*k, mat, pos, c[0] > 0 ? z[0] : -z[0], c[1] > 0 ? z[1] : -z[1],
+              c[2] > 0 ? z[2] : -z[2]);
+  }
+  return 4;
+}
+
+/* alignedFaces (:2019-2031) */
+static int mc_alignedFaces(int res[2], const mjtNum* v, int nv, const mjtNum* w, int nw) {
+  for (int i = 0; i < nv; i++) {
+    for (int j = 0; j < nw; j++) {
+      if (mc_dot3(v + 3*i, w + 3*j) < -OR_FACE_TOL) {
+        res[0] = i;
+        res[1] = j;
+        return 1;
+      }
+    }
+  }
+  return 0;
+}
+
+/* alignedFaceEdge (:2036-2048) */
+static int mc_alignedFaceEdge(int res[2], const mjtNum* edge, int nedge, const mjtNum* face,
+                              int nface) {
+  for (int i = 0; i < nface; i++) {
+    for (int j = 0; j < nedge; j++) {
+      if (fabs(mc_dot3(edge + 3*j, face + 3*i)) < OR_EDGE_TOL) {
+        res[0] = j;
+        res[1] = i;
+        return 1;
+      }
+    }
+  }
+  return 0;
+}
+
+/* simplexDim (:2052-2067) */
+static int mc_simplexDim(int* v1i, int* v2i, int* v3i, const mjtNum** v1, const mjtNum** v2,
+                         const mjtNum** v3) {
+  int a = *v1i, b = *v2i, c = *v3i;
+  if (a != b) return (c == a || c == b) ? 2 : 3;
+  if (a != c) {
+    *v2i = *v3i;
+    *v2 = *v3;
+    return 2;
+  }
+  return 1;
+}
+
+/* multicontact (:2071-2193) for box pairs */
+static void ccd_multicontact(orCCD* st, const orPoly* P, int f, const orShape* A,
+                             const orShape* B) {
+  if (A->gtype == mjhipGEOM_MESH || B->gtype == mjhipGEOM_MESH) {
+    st->unsupported = 1;                  /* the mesh's polygon data is not compiled */
+    return;
+  }
+  const orFace* F = P->face + f;
+  const orVtx *p0 = P->vtx + F->vi[0], *p1 = P->vtx + F->vi[1], *p2 = P->vtx + F->vi[2];
+  int v11i = p0->i1, v12i = p1->i1, v13i = p2->i1;
+  int v21i = p0->i2, v22i = p1->i2, v23i = p2->i2;
+  const mjtNum *v11 = p0->p1, *v12 = p1->p1, *v13 = p2->p1;
+  const mjtNum *v21 = p0->p2, *v22 = p1->p2, *v23 = p2->p2;
+  int nface1 = mc_simplexDim(&v11i, &v12i, &v13i, &v11, &v12, &v13);
+  int nface2 = mc_simplexDim(&v21i, &v22i, &v23i, &v21, &v22, &v23);
+  int nn1 = 0, nn2 = 0, idx1[3] = {0, 0, 0}, idx2[3] = {0, 0, 0};
+  mjtNum n1[9], n2[9], endverts[9], face1[12], face2[12];
+  if (A->gtype == mjhipGEOM_BOX) nn1 = mc_boxNormals(n1, idx1, nface1, A, v11i, v12i, v13i);
+  if (B->gtype == mjhipGEOM_BOX) nn2 = mc_boxNormals(n2, idx2, nface2, B, v21i, v22i, v23i);
+  int res[2], edgecon1 = 0, edgecon2 = 0;
+  if (!mc_alignedFaces(res, n1, nn1, n2, nn2)) {
+    if (nface1 < 3 && nface1 <= nface2) {
+      nn1 = 0;
+      if (A->gtype == mjhipGEOM_BOX) {
+        nn1 = mc_boxEdgeNormals(n1, endverts, nface1, A, v11, v12, v11i);
+      }
+      if (!mc_alignedFaceEdge(res, n1, nn1, n2, nn2)) return;
+      edgecon1 = 1;
+    } else if (nface2 < 3) {
+      nn2 = 0;
+      if (B->gtype == mjhipGEOM_BOX) {
+        nn2 = mc_boxEdgeNormals(n2, endverts, nface2, B, v21, v22, v21i);
+      }
+      if (!mc_alignedFaceEdge(res, n2, nn2, n1, nn1)) return;
+      edgecon2 = 1;
+    } else {
+      return;
+    }
+  }
+  int i = res[0], j = res[1];
+  if (edgecon1) {
+    mju_copy3(face1, p0->p1);
+    mju_copy3(face1 + 3, endverts + 3*i);
+    nface1 = 2;
+  } else {
+    nface1 = mc_boxFace(face1, A, edgecon2 ? idx1[j] : idx1[i]);
+  }
+  if (edgecon2) {
+    mju_copy3(face2, p0->p2);
+    mju_copy3(face2 + 3, endverts + 3*i);
+    nface2 = 2;
+  } else {
+    nface2 = mc_boxFace(face2, B, idx2[j]);
+  }
+  mjtNum diff[3], dir[3];
+  mju_sub3(diff, st->x2, st->x1);
+  const mjtNum nd = sqrt(mc_dot3(diff, diff));
+  if (edgecon1) {
+    mju_scl3(dir, n2 + 3*j, nd);
+    mc_polygonClip(st, face2, nface2, face1, nface1, n2 + 3*j, dir);
+    return;
+  }
+  if (edgecon2) {
+    mju_scl3(dir, n1 + 3*j, -nd);
+    mc_polygonClip(st, face1, nface1, face2, nface2, n1 + 3*j, dir);
+    return;
+  }
+  mju_scl3(dir, n2 + 3*j, nd);
+  mc_polygonClip(st, face1, nface1, face2, nface2, n1 + 3*i, dir);
+}
+
 static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol, mjtNum cutoff,
                      int maxc) {
   ccd_center(st->x1, A);
@@ -3792,6 +4201,8 @@ static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol, mj
   st->iters = 0;
   st->tol = tol;
   st->kmax = kmax;
+  st->maxc = maxc;
+  st->unsupported = 0;
   st->cutoff = cutoff;
   const int shrinkA = A->gtype == mjhipGEOM_SPHERE || A->gtype == mjhipGEOM_CAPSULE;
   const int shrinkB = B->gtype == mjhipGEOM_SPHERE || B->gtype == mjhipGEOM_CAPSULE;
@@ -3856,7 +4267,10 @@ static mjtNum or_ccd(orCCD* st, orShape* A, orShape* B, int kmax, mjtNum tol, mj
     P.nvtx = P.nface = P.nlist = P.nh = 0;
     int ret = st->nsimplex == 2 ? ccd_fromSegment(&P, st, A, B) :
               st->nsimplex == 3 ? ccd_fromTriangle(&P, st, A, B) : ccd_fromTetra(&P, st, A, B);
-    if (!ret) ccd_epa(st, &P, A, B);
+    if (!ret) {
+      const int f = ccd_epa(st, &P, A, B);
+      if (maxc > 1 && f >= 0) ccd_multicontact(st, &P, f, A, B);
+    }
     free(P.vtx);
     free(P.face);
     free(P.list);
@@ -4338,8 +4752,8 @@ int or_ccdPenetration(const mjhipModel* m, const mjhipData* d, int g1, int g2, m
 
 /* mjc_ccd (engine_collision_gjk.c:2215-2343) as the reference's GJK tests call it
    (engine_collision_gjk_test.cc:62-84 GeomDist, :86-150 Penetration): geoms g1, g2 at the
-   data's current frames, object margin `margin` on both, config {kmax, tol, maxc (0 or 1),
-   cutoff}. out: dist, nx, x1[3], x2[3]. Returns dist. */
+   data's current frames, object margin `margin` on both, config {kmax, tol, maxc, cutoff}.
+   out: dist, nx, unsupported (multicontact on a mesh), x1[3*50], x2[3*50]. Returns dist. */
 mjtNum or_ccdGeneral(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum margin,
                      mjtNum tol, int kmax, int maxc, mjtNum cutoff, mjtNum* out) {
   orShape A, B;
@@ -4350,9 +4764,10 @@ mjtNum or_ccdGeneral(const mjhipModel* m, const mjhipData* d, int g1, int g2, mj
   mjtNum dist = or_ccd(&st, &A, &B, kmax, tol, cutoff, maxc);
   out[0] = dist;
   out[1] = st.nx;
-  for (int k = 0; k < 3; k++) {
-    out[2 + k] = st.x1[k];
-    out[5 + k] = st.x2[k];
+  out[2] = st.unsupported;
+  for (int k = 0; k < 3*OR_MAXCONPAIR; k++) {
+    out[3 + k] = st.x1[k];
+    out[3 + 3*OR_MAXCONPAIR + k] = st.x2[k];
   }
   return dist;
 }

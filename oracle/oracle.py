@@ -313,11 +313,17 @@ class Oracle:
 
   def ccd(self, g1, g2, margin=0.0, tol=1e-6, kmax=1000, max_contacts=1, cutoff=0.0):
     """mjc_ccd (engine_collision_gjk.c:2215-2343) on the current frames with the reference
-    tests' config (engine_collision_gjk_test.cc:62-150): (dist, nx, x1, x2)."""
-    out = np.zeros(8)
+    tests' config (engine_collision_gjk_test.cc:62-150): (dist, nx, x1, x2); with
+    max_contacts > 1, x1 / x2 are [nx, 3] (multicontact)."""
+    out = np.zeros(3 + 300)
     dist = self.L.or_ccdGeneral(*self._args()[:2], g1, g2, margin, tol, kmax, max_contacts,
                                 cutoff, _p(out))
-    return dist, int(out[1]), out[2:5].copy(), out[5:8].copy()
+    if out[2]:
+      raise NotImplementedError("multicontact on a mesh: the mesh polygon data is not compiled")
+    nx = int(out[1])
+    if max_contacts <= 1:
+      return dist, nx, out[3:6].copy(), out[153:156].copy()
+    return dist, nx, out[3:3 + 3*nx].reshape(nx, 3).copy(), out[153:153 + 3*nx].reshape(nx, 3).copy()
 
   def ray(self, pnt, vec, bodyexclude=-1):
     """mj_ray (geomgroup NULL, flg_static 1) on the current frames: (distance, geomid)."""

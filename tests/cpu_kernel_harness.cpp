@@ -124,12 +124,12 @@ static mjh::Lane<1> bind(const mjhipModel* m, mjhipData* d, double* scratch, int
 }
 
 // mjc_ccd on two geoms at the given frames (mjh::ccdGeneral, the function mjhip_ccdBatch runs
-// per pair on the device); out: dist, nx, x1[3], x2[3]
+// per pair on the device); out: dist, nx, x1[3*50], x2[3*50]
 extern "C" int kh_ccd(const mjhipModel* m, int g1, int g2, const double* pos1,
                       const double* mat1, const double* pos2, const double* mat2,
                       double margin, int N, double tol, int maxc, double cutoff, double* out) {
   std::vector<double> x(mjh::ccdScratchDoubles(N));
   std::vector<int> xi(mjh::ccdScratchInts(N));
-  return mjh::ccdGeneral(*m, g1, g2, pos1, mat1, pos2, mat2, margin, N, tol, maxc, cutoff,
-                         x.data(), xi.data(), out);
+  return mjh::ccdGeneral<true>(*m, g1, g2, pos1, mat1, pos2, mat2, margin, N, tol, maxc, cutoff,
+                               x.data(), xi.data(), out);
 }

@@ -64,13 +64,17 @@ def ccd_host(m, g1, g2, xpos, xmat, margin=0.0, tol=1e-6, kmax=1000, max_contact
   frames xpos [ngeom, 3], xmat [ngeom, 9]: (dist, nx, x1, x2), as Oracle.ccd."""
   cm = host.model_struct(m)
   D = ctypes.POINTER(ctypes.c_double)
-  out = np.zeros(8)
+  out = np.zeros(2 + 300)
   a = [np.ascontiguousarray(v, dtype=np.float64) for v in (xpos[g1], xmat[g1], xpos[g2],
                                                             xmat[g2])]
   st = lib().kh_ccd(ctypes.byref(cm), g1, g2, *(x.ctypes.data_as(D) for x in a), margin,
                     kmax, tol, max_contacts, cutoff, out.ctypes.data_as(D))
-  assert st == 0, "face capacity exceeded"
-  return out[0], int(out[1]), out[2:5].copy(), out[5:8].copy()
+  assert st == 0, f"ccdGeneral status {st}"
+  nx = int(out[1])
+  if max_contacts <= 1:
+    return out[0], nx, out[2:5].copy(), out[152:155].copy()
+  return (out[0], nx, out[2:2 + 3*nx].reshape(nx, 3).copy(),
+          out[152:152 + 3*nx].reshape(nx, 3).copy())
 
 
 class KernelCPU:

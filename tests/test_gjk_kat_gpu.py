@@ -43,8 +43,9 @@ def test_gjk_known_answers_device():
 
 
 def test_ccd_batch_arguments():
-  """Bad arguments fail loudly (no launch): geom ids out of range, max_contacts outside the
-  built range."""
+  """Bad arguments fail loudly (no launch): geom ids out of range, a negative max_contacts;
+  multicontact on a mesh pair (its polygon data is not compiled) is refused, not
+  approximated."""
   m = mjcf.load_xml_string(K.SPHERES)
   e = engine.InverseEngine(m, capacity=64)
   try:
@@ -52,7 +53,16 @@ def test_ccd_batch_arguments():
     with pytest.raises(engine.MJHIPError):
       e.ccd([0], [5], f[0], f[1], f[0], f[1])
     with pytest.raises(engine.MJHIPError):
-      e.ccd([0], [1], f[0], f[1], f[0], f[1], max_contacts=2)
+      e.ccd([0], [1], f[0], f[1], f[0], f[1], max_contacts=-1)
+  finally:
+    e.close()
+  m = mjcf.load_xml_string(K.LONG_BOX)
+  o = Oracle(m)
+  xpos, xmat = K.frames(m, o, None, {})
+  e = engine.InverseEngine(m, capacity=64)
+  try:
+    with pytest.raises(engine.MJHIPError, match="polygon"):
+      e.ccd([0], [1], xpos[:1], xmat[:1], xpos[1:2], xmat[1:2], max_contacts=1000)
   finally:
     e.close()
 
@@ -73,3 +83,29 @@ def test_cylinder_box_margin_device():
   finally:
     e.close()
   np.testing.assert_allclose(f[0], ref, rtol=0, atol=1e-12)
+
+
+def test_gjk_multicontact_known_answers_device():
+  """Multicontact on the device (max_contacts > 1, box pairs; mjhip_ccdBatch): the reference's
+  BoxBoxMultiCCD*, BoxEdge* known answers, and the oracle's contacts bit for bit."""
+  for name, xml, overrides, geoms, maxc, expected in K.MULTI_CASES:
+    m = mjcf.load_xml_string(xml)
+    o = Oracle(m)
+    xpos, xmat = K.frames(m, o, None, overrides)
+    g1, g2 = (m.names["geom"].index(g) for g in geoms)
+    e = engine.InverseEngine(m, capacity=64)
+    try:
+      n = 3
+      dist, nx, x1, x2 = e.ccd([g1] * n, [g2] * n, [xpos[g1]] * n, [xmat[g1]] * n,
+                               [xpos[g2]] * n, [xmat[g2]] * n, 0.0, K.KMAX, K.KTOL, maxc, 0.0)
+    finally:
+      e.close()
+    assert (dist == dist[0]).all() and (nx == nx[0]).all(), name
+    k = nx[0]
+    K.check(name + " (device)", expected, K.report_multi(dist[0], k, x1[0, :k], x2[0, :k]))
+    o.d.geom_xpos[:] = xpos.ravel()
+    o.d.geom_xmat[:] = xmat.ravel()
+    ro = o.ccd(g1, g2, 0.0, K.KTOL, K.KMAX, maxc, 0.0)
+    assert dist[0] == ro[0] and k == ro[1], (name, dist[0], ro[0], k, ro[1])
+    np.testing.assert_array_equal(x1[0, :k], ro[2], err_msg=name)
+    np.testing.assert_array_equal(x2[0, :k], ro[3], err_msg=name)

@@ -12,7 +12,7 @@ import numpy as np
 import pytest
 
 from mujoco_inversedynamicstest_amd import engine, fields, host, models
-from mujoco_inversedynamicstest_amd.sampler import sample_states
+from mujoco_inversedynamicstest_amd.sampler import sample_contact_states, sample_states
 from oracle.oracle import Oracle
 
 pytestmark = pytest.mark.gpu
@@ -100,16 +100,22 @@ def test_skipstage_chain(humanoid, eng):
   assert_close(f_pos, rp, "skip POS")
 
 
-@pytest.mark.parametrize("name", ["humanoid", "inverse_test", "linear", "inertia"])
+@pytest.mark.parametrize("name", ["humanoid", "humanoid_contact", "inverse_test", "linear",
+                                  "inertia"])
 def test_skipstage_straight_line(name, monkeypatch):
   """Batched mj_inverseSkip(POS / VEL) on the straight-line kernels (k_va for POS, k_acc for
   VEL): the path is asserted (mjhip_contextLastPath = 2), on the humanoid
   a fifth of the instances carry limit rows from the full call (k_skip_rows finishes them), and
   the results match the oracle's serial mj_inverseSkip chain and the generic kernel
   (MJHIP_SKIP_GENERIC=1) to the north-star tolerance, with inputs given for every field."""
-  m = models.load(name, disable_contact=True, disable_sensor=(name == "linear"))
+  contact = name == "humanoid_contact"
+  m = models.load("humanoid" if contact else name, disable_contact=not contact,
+                  disable_sensor=(name == "linear"))
   B = 200
-  q, v, a = sample_states(m, B, first=21)
+  # humanoid_contact (rows on every instance: contacts and their rows from the full call,
+  # finished for every instance by k_skip_rows; the reference driver's own call,
+  # inverse_test.cpp:93, on a model with contacts)
+  q, v, a = sample_contact_states(m, B) if contact else sample_states(m, B, first=21)
   if name == "humanoid":
     j = int(np.flatnonzero(np.asarray(m.jnt_limited))[3])
     q[::5, m.jnt_qposadr[j]] = m.jnt_range[j][1] + 0.2
@@ -142,6 +148,8 @@ def test_skipstage_straight_line(name, monkeypatch):
     assert o.d.nefc == nefc[i]
   if name == "humanoid":
     assert (nefc[::5] > 0).all()
+  if contact:
+    assert (nefc > 0).mean() > 0.5 and (nefc == 0).any()
   for (fv, fp, qc, _), what in zip(got, ("straight-line", "generic")):
     assert_close(fv, rv, f"{name} skip VEL ({what})")
     assert_close(fp, rp, f"{name} skip POS ({what})")

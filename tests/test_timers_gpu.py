@@ -19,7 +19,7 @@ pytestmark = pytest.mark.gpu
 PARTS = ("POS_KINEMATICS", "POS_INERTIA", "POS_COLLISION", "POS_MAKE")
 
 
-def _check(t, calls, collision):
+def _check(t, calls, collision, overlap=False):
   assert t["INVERSE"][1] == calls and t["INVERSE"][0] > 0
   for k in ("POSITION", "VELOCITY", "CONSTRAINT") + PARTS:
     assert t[k][1] == calls, k
@@ -27,8 +27,13 @@ def _check(t, calls, collision):
   assert t["POS_KINEMATICS"][0] > 0 and t["VELOCITY"][0] > 0 and t["CONSTRAINT"][0] > 0
   if collision:
     assert t["POS_COLLISION"][0] > 0 and t["POS_MAKE"][0] > 0
-  stages = t["POSITION"][0] + t["VELOCITY"][0] + t["CONSTRAINT"][0]
-  assert stages <= t["INVERSE"][0] * 1.05
+  if overlap:   # split launch (path 3): the constraint kernel runs beside the fac / va stages
+    smooth = t["POS_KINEMATICS"][0] + t["POS_INERTIA"][0] + t["VELOCITY"][0]
+    rows = t["POS_COLLISION"][0] + t["POS_MAKE"][0] + t["CONSTRAINT"][0]
+    assert smooth <= t["INVERSE"][0] * 1.05 and rows <= t["INVERSE"][0] * 1.05
+  else:
+    stages = t["POSITION"][0] + t["VELOCITY"][0] + t["CONSTRAINT"][0]
+    assert stages <= t["INVERSE"][0] * 1.05
   for k in ("STEP", "FORWARD", "ACTUATION", "ADVANCE", "POS_PROJECT", "COL_BROAD",
             "COL_NARROW"):
     assert t[k] == (0.0, 0), k
@@ -56,7 +61,7 @@ def test_timers(case):
       np.testing.assert_array_equal(f1, f0)
     t = e.timer_read()
     print(case, {k: (round(x, 4), n) for k, (x, n) in t.items() if n})
-    _check(t, 3, collision=True)
+    _check(t, 3, collision=True, overlap=e.last_path == 3)
     t2 = e.timer_read(reset=True)
     assert t2 == t
     assert all(x == (0.0, 0) for x in e.timer_read().values())
@@ -103,6 +108,6 @@ def test_timed_context_freed_then_another():
     assert all(x == (0.0, 0) for x in e2.timer_read().values())
     e2.timers(True)                        # the freed context no longer holds the slot
     np.testing.assert_array_equal(e2.inverse(q, v, a), f0)
-    _check(e2.timer_read(), 1, collision=True)
+    _check(e2.timer_read(), 1, collision=True, overlap=e2.last_path == 3)
   finally:
     e2.close()

@@ -41,6 +41,15 @@ for step in "$@"; do
       timeout -k 10 120 python bench.py --config 4 --steps 20 --warmup 3 > gpurun_out/c4.json \
         2> gpurun_out/c4.err || exit 1
       tail -1 gpurun_out/c4.json ;;
+    c4split)                                # config 4 with the split launch on (A/B)
+      MJHIP_SPLIT=1 timeout -k 10 120 python bench.py --config 4 --steps 20 --warmup 3 \
+        > gpurun_out/c4split.json 2> gpurun_out/c4split.err || exit 1
+      tail -1 gpurun_out/c4split.json ;;
+    c4splittrace)
+      MJHIP_SPLIT=1 timeout -k 10 240 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c4s \
+        -o c4s --output-format csv -- python bench.py --config 4 --steps 20 --warmup 3 \
+        > gpurun_out/c4splittrace.json 2> gpurun_out/c4splittrace.err || exit 1
+      find gpurun_out/prof_c4s -name "*kernel_stats.csv" -exec cat {} \; | cut -c1-150 ;;
     c5)
       timeout -k 10 180 python bench.py --config 5 > gpurun_out/c5.json 2> gpurun_out/c5.err || exit 1
       tail -1 gpurun_out/c5.json ;;
