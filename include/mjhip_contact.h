@@ -17,7 +17,8 @@
  * order ((b1 << 16) + b2, b1 < b2); mjhip_pairMaxContacts bounds each primitive pair.
  *
  * A candidate pair whose collision function is not implemented here (SDFs; mjc_Convex and
- * height fields with the libccd fallback, MULTICCD's extra contacts) adds no capacity. At run time it goes through the
+ * height fields with the libccd fallback; MULTICCD with a mesh) adds no capacity. At run
+ * time it goes through the
  * same bitmask and bounding-sphere filters as the reference (mj_collideGeoms :1470-1497);
  * an instance where one survives them is flagged MJHIP_INST_UNSUPPORTED instead of getting
  * contacts, so every unflagged instance is exact.
@@ -114,9 +115,10 @@ MJHIP_CONTACT_HD int mjhip_isConvexPair(int t1, int t2) {
 /* contacts a (type-ordered t1 <= t2) geom pair can produce with the functions implemented
  * here: 0 = no collision function in the reference table, -1 = a reference collision
  * function that this engine does not implement. mjc_Convex runs the native GJK/EPA solver
- * for one contact (mjc_CCDIteration, engine_collision_convex.c:792-819); with the libccd MPR
- * fallback (mjDSBL_NATIVECCD) or MULTICCD's perturbed extra contacts (pairs without a
- * sphere or an ellipsoid, :936-999) it is not built here. mjc_PlaneConvex gives a mesh up to
+ * for one contact (mjc_CCDIteration, engine_collision_convex.c:792-819); with MULTICCD, a
+ * pair without a sphere or an ellipsoid adds up to four perturbed contacts (:933-999), 5 in
+ * all, except with a mesh (the box / mesh single pass's polygon needs the mesh polygon data,
+ * not compiled here); the libccd MPR fallback (mjDSBL_NATIVECCD) is not built. mjc_PlaneConvex gives a mesh up to
  * maxplanemesh = 3 contacts (:1006), mjc_ConvexHField up to mjMAXCONPAIR = 50 (one per prism,
  * mjhip_geomPairMaxContacts bounds it by the field's grid). */
 MJHIP_CONTACT_HD int mjhip_pairMaxContacts(const mjhipModel* m, int t1, int t2) {
@@ -128,7 +130,7 @@ MJHIP_CONTACT_HD int mjhip_pairMaxContacts(const mjhipModel* m, int t1, int t2) 
     if (m->opt.disableflags & mjhipDSBL_NATIVECCD) return -1;
     if ((m->opt.enableflags & mjhipENBL_MULTICCD) && t1 != mjhipGEOM_SPHERE &&
         t1 != mjhipGEOM_ELLIPSOID && t2 != mjhipGEOM_ELLIPSOID) {
-      return -1;
+      return t2 == mjhipGEOM_MESH ? -1 : 5;
     }
     return 1;
   }

@@ -147,6 +147,9 @@ class _Emitter:
 
 def fast_path_supported(m) -> str | None:
   """Return why the model cannot use the straight-line kernels, or None."""
+  if m.nv == 0:
+    # nothing to unroll (and zero-length arrays are not valid device code)
+    return "no degrees of freedom"
   if m.nv >= 60:
     # straight-line code grows with the tree; large models (the reference's sparse-Jacobian
     # range) run the generic kernel

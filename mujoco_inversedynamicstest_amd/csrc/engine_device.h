@@ -3583,17 +3583,12 @@ MJH_HD int ccdGeneral(const mjhipModel& m, int g1, int g2, const double* pos1,
   return st.unsupported ? 1 : (C.bad ? 2 : 0);
 }
 
-// mjc_Convex through mjc_CCDIteration (convex.c:792-819, :915-1001): 0 or 1 contacts
+// mjc_CCDIteration (convex.c:792-819) on the shapes' current frames: 0 or 1 contacts
 template <int S>
-MJH_HD int colConvex(RawContact& c, const mjhipModel& m, const Lane<S>& d, int g1, int g2,
-                     double margin, int* status) {
-  const int N = m.opt.ccd_iterations;
-  CcdMem<1> M{{d.ccdx}, {d.ccdxi}, 5 + N, mjh_ccdFaceCap(&m)};
-  CcdShape A, B;
-  ccdShape(A, m, d, g1, margin);
-  ccdShape(B, m, d, g2, margin);
+MJH_HD int ccdIteration(RawContact& c, const mjhipModel& m, const CcdMem<S>& M, CcdShape& A,
+                        CcdShape& B, double margin, int* status) {
   CcdState st;
-  const double dist = ccdRun(st, M, A, B, N, m.opt.ccd_tolerance, 0.0);
+  const double dist = ccdRun(st, M, A, B, m.opt.ccd_iterations, m.opt.ccd_tolerance, 0.0);
   if (st.unsupported) {
     *status |= MJHIP_INST_UNSUPPORTED;
     return 0;
@@ -3609,6 +3604,105 @@ MJH_HD int colConvex(RawContact& c, const mjhipModel& m, const Lane<S>& d, int g
   c.pos[2] = 0.5*(st.x1[2] + st.x2[2]);
   for (int k = 3; k < 9; k++) c.frame[k] = 0;
   return 1;
+}
+
+// mjc_Convex through mjc_CCDIteration (convex.c:792-819, :915-1001): 0 or 1 contacts
+template <int S>
+MJH_HD int colConvex(RawContact& c, const mjhipModel& m, const Lane<S>& d, int g1, int g2,
+                     double margin, int* status) {
+  CcdMem<1> M{{d.ccdx}, {d.ccdxi}, 5 + m.opt.ccd_iterations, mjh_ccdFaceCap(&m)};
+  CcdShape A, B;
+  ccdShape(A, m, d, g1, margin);
+  ccdShape(B, m, d, g2, margin);
+  return ccdIteration(c, m, M, A, B, margin, status);
+}
+
+// mju_rotateFrame (convex.c:862-880): the frame rotated by rot about origin
+MJH_HD void ccdRotateFrame(const double origin[3], const double rot[9], double xmat[9],
+                           double xpos[3]) {
+  double mat[9], vec[3], rel[3];
+  for (int i = 0; i < 3; i++) {           // mju_mulMatMat3 (engine_util_blas.c:193-203)
+    for (int j = 0; j < 3; j++) {
+      mat[3*i+j] = rot[3*i]*xmat[j] + rot[3*i+1]*xmat[3+j] + rot[3*i+2]*xmat[6+j];
+    }
+  }
+  for (int k = 0; k < 9; k++) xmat[k] = mat[k];
+  sub3(rel, origin, xpos);
+  mulMatVec3(vec, rot, rel);
+  sub3(vec, vec, rel);
+  sub3(xpos, xpos, vec);
+}
+
+// mjc_Convex with mjENBL_MULTICCD (convex.c:915-1001) for a pair without a sphere, ellipsoid
+// or mesh: the first contact, then the four perturbed ones (:933-999) -- both geoms rotated
+// about the first contact by -+1e-3 rad around its frame's y and z axes (geom 2 by the
+// inverse), each new contact farther than 1e-3 min(rbound) from all earlier ones kept with
+// the first one's depth -- handed to `store` in order (false: the list is full). The frames
+// are perturbed on the solver's own copies (the reference rotates mjData's and restores
+// them). sin / cos of the half angle are the correctly rounded constants, so the device
+// libm cannot move a last bit.
+template <int S, class Store>
+MJH_HD void colConvexMulti(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
+                           double margin, int* status, Store store) {
+  CcdMem<1> M{{d.ccdx}, {d.ccdxi}, 5 + m.opt.ccd_iterations, mjh_ccdFaceCap(&m)};
+  CcdShape A, B;
+  ccdShape(A, m, d, g1, margin);
+  ccdShape(B, m, d, g2, margin);
+  RawContact c0;
+  if (!ccdIteration(c0, m, M, A, B, margin, status)) return;
+  if (!store(c0)) return;
+  double frame[9];
+  for (int k = 0; k < 9; k++) frame[k] = c0.frame[k];
+  makeFrame(frame);
+  const double rb1 = m.geom_rbound[g1], rb2 = m.geom_rbound[g2];
+  const double tolerance = 1e-3 * (rb1 < rb2 ? rb1 : rb2);
+  double p1[3], r1[9], p2[3], r2[9];
+  copy3(p1, A.pos);
+  copy3(p2, B.pos);
+  for (int k = 0; k < 9; k++) { r1[k] = A.mat[k]; r2[k] = B.mat[k]; }
+  double kept[5][3];
+  copy3(kept[0], c0.pos);
+  int ncon = 1;
+  constexpr double kSin = 0.0004999999791666669;   // sin(1e-3 / 2)
+  constexpr double kCos = 0.9999998750000026;      // cos(1e-3 / 2)
+  for (int ai = 0; ai < 2; ai++) {
+    const double* axis = frame + 3 + 3*ai;
+    for (int gi = 0; gi < 2; gi++) {
+      const double s = gi ? kSin : -kSin;               // angles {-1e-3, 1e-3}
+      const double quat[4] = {kCos, axis[0]*s, axis[1]*s, axis[2]*s};   // axisAngle2Quat
+      double rot[9], inv[9];
+      quat2Mat(rot, quat);
+      ccdRotateFrame(c0.pos, rot, A.mat, A.pos);
+      for (int i = 0; i < 3; i++) {
+        for (int j = 0; j < 3; j++) inv[3*j+i] = rot[3*i+j];
+      }
+      ccdRotateFrame(c0.pos, inv, B.mat, B.pos);
+      RawContact ck;
+      bool fresh = ccdIteration(ck, m, M, A, B, margin, status) != 0;
+      for (int i = 0; i < ncon && fresh; i++) {          // mjc_isDistinctContact (:851-858)
+        double dif[3];
+        sub3(dif, kept[i], ck.pos);
+        if (sqrt(dif[0]*dif[0] + dif[1]*dif[1] + dif[2]*dif[2]) <= tolerance) fresh = false;
+      }
+      if (fresh) {
+        ck.dist = c0.dist;
+        copy3(kept[ncon], ck.pos);
+        ncon++;
+        if (!store(ck)) return;
+      }
+      copy3(A.pos, p1);
+      copy3(B.pos, p2);
+      for (int k = 0; k < 9; k++) { A.mat[k] = r1[k]; B.mat[k] = r2[k]; }
+    }
+  }
+}
+
+// the pair runs MULTICCD's perturbation pass (colConvexMulti): a convex pair without a
+// sphere or an ellipsoid with the flag on (meshes are refused by mjhip_pairMaxContacts)
+MJH_HD bool multiCcdPair(const mjhipModel& m, int t1, int t2) {
+  return (m.opt.enableflags & mjhipENBL_MULTICCD) && mjhip_isConvexPair(t1, t2) &&
+         t1 != mjhipGEOM_SPHERE && t1 != mjhipGEOM_ELLIPSOID && t2 != mjhipGEOM_ELLIPSOID &&
+         t2 != mjhipGEOM_MESH;
 }
 
 // mjc_PlaneConvex (convex.c:1045-1080) for an ellipsoid: the libccd support (mjccd_support
@@ -4135,6 +4229,7 @@ MJH_HD int narrowGeoms(const mjhipModel& m, const Lane<S>& d, int& g1, int& g2,
   if (t1 == mjhipGEOM_BOX && t2 == mjhipGEOM_BOX) return -1;
   if (t1 == mjhipGEOM_PLANE && t2 == mjhipGEOM_MESH) return -1;   // up to 3, stored as made
   if (t1 == mjhipGEOM_HFIELD) return -1;                            // up to 50, stored as made
+  if (CONVEX && multiCcdPair(m, t1, t2)) return -1;                 // up to 5, stored as made
   SP<S> pos1 = d.gxpos + 3*g1, mat1 = d.geom_xmat + 9*g1;
   SP<S> pos2 = d.gxpos + 3*g2, mat2 = d.geom_xmat + 9*g2;
   const double *size1 = m.geom_size + 3*g1, *size2 = m.geom_size + 3*g2;
@@ -4329,6 +4424,17 @@ MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, in
   if (m.geom_type[g1] == mjhipGEOM_BOX) {
     if constexpr (BOX) collideBoxBox<S, WRITE>(m, d, g1, g2, margin, cp, ncon, status, bbuf);
     else *status |= MJHIP_INST_UNSUPPORTED;   // not reached: the launch saw no box pair
+    return;
+  }
+  if (multiCcdPair(m, m.geom_type[g1], m.geom_type[g2])) {
+    if constexpr (CONVEX) {
+      colConvexMulti(m, d, g1, g2, margin, status,
+                     [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
+        return putContact<S, WRITE>(m, d, g1, g2, margin, cp, rk, ncon, status);
+      });
+    } else {
+      *status |= MJHIP_INST_UNSUPPORTED;      // not reached: such models use one lane each
+    }
     return;
   }
   if (m.geom_type[g1] == mjhipGEOM_HFIELD || m.geom_type[g2] == mjhipGEOM_MESH) {

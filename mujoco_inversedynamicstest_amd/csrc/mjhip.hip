@@ -159,92 +159,103 @@ __device__ static inline long fd_inst(int layout, long nbase, long b, int p, int
   return nbase*(nv + 1) + nbase*nv + b*nv + (p - 1 - nv);
 }
 
-// instances [first + thread, end) of the layout, and within a device-side range {lo, hi}
-// when one is given (the fall-back's: empty unless a centre has limit rows)
-__global__ void k_fd_expand(mjhipModel m, Mirror mr, int nbase, const double* __restrict__ qpos,
-                            const double* __restrict__ qvel, const double* __restrict__ qacc,
-                            const double* __restrict__ ctrl, double eps, int layout,
-                            int* __restrict__ fdflag, long first, long end,
-                            const int* __restrict__ range) {
-  const int P = 3*m.nv + 1;
-  long inst = first + (long)blockIdx.x*blockDim.x + threadIdx.x;
-  if (fdflag && inst == first) fdflag[0] = 0;   // k_vaskip raises it later in stream order
+// instances [first, end) of the layout (first a multiple of 64), one block per 64 instances
+// and input component: qvel[k], qacc[k] (k < nv), joint j's qpos (mj_integratePos on dof i
+// for the qpos perturbations), ctrl[k]. A block's 64 lanes write one 512-byte mirror line per
+// value. gate: the stage-skip fall-back's expansion (mjhip_inverseFDBatch): it runs only when
+// k_vaskip found a centre with limit rows (fdflag[0]), and its first thread hands the range
+// {first, end} -- or the empty {first, first} -- to the fall-back k_all (fdflag[1..2])
+__global__ __launch_bounds__(64) void k_fd_expand(mjhipModel m, Mirror mr, int nbase,
+                                                  const double* __restrict__ qpos,
+                                                  const double* __restrict__ qvel,
+                                                  const double* __restrict__ qacc,
+                                                  const double* __restrict__ ctrl, double eps,
+                                                  int layout, int* __restrict__ fdflag,
+                                                  long first, long end, int gate) {
+  const int nv = m.nv, nq = m.nq, P = 3*nv + 1;
+  const int ncomp = 2*nv + m.njnt + (ctrl ? m.nu : 0);
+  // the gated launch has one block per 64 instances looping over the components, so that
+  // the usual empty call costs few blocks
+  const int per = gate ? 1 : ncomp;
+  const long blk = first/64 + blockIdx.x / per;
+  const int lane = threadIdx.x;
+  if (gate) {
+    if (blockIdx.x == 0 && lane == 0) {
+      fdflag[1] = (int)first;
+      fdflag[2] = fdflag[0] ? (int)end : (int)first;
+    }
+    if (!fdflag[0]) return;
+  } else if (fdflag && blockIdx.x == 0 && lane == 0) {
+    fdflag[0] = 0;                       // k_vaskip raises it later in stream order
+  }
+  const long inst = blk*64 + lane;
   if (inst >= end || inst >= (long)nbase*P) return;
-  if (range && (inst < range[0] || inst >= range[1])) return;
+  for (int comp = gate ? 0 : blockIdx.x % ncomp; comp < (gate ? ncomp : blockIdx.x % ncomp + 1);
+       comp++) {
   long b;
   int p;
   if (!layout) {
     b = inst / P;
     p = (int)(inst % P);
-  } else if (inst < (long)nbase*(m.nv + 1)) {
-    b = inst / (m.nv + 1);
-    const int j = (int)(inst % (m.nv + 1));
-    p = j ? 2*m.nv + j : 0;
+  } else if (inst < (long)nbase*(nv + 1)) {
+    b = inst / (nv + 1);
+    const int j = (int)(inst % (nv + 1));
+    p = j ? 2*nv + j : 0;
   } else if (layout == 1) {
-    const long t = inst - (long)nbase*(m.nv + 1);
-    b = t / (2*m.nv);
-    p = 1 + (int)(t % (2*m.nv));
+    const long t = inst - (long)nbase*(nv + 1);
+    b = t / (2*nv);
+    p = 1 + (int)(t % (2*nv));
   } else {
-    long t = inst - (long)nbase*(m.nv + 1);
-    const bool vel = t >= (long)nbase*m.nv;
-    if (vel) t -= (long)nbase*m.nv;
-    b = t / m.nv;
-    p = 1 + (int)(t % m.nv) + (vel ? m.nv : 0);
+    long t = inst - (long)nbase*(nv + 1);
+    const bool vel = t >= (long)nbase*nv;
+    if (vel) t -= (long)nbase*nv;
+    b = t / nv;
+    p = 1 + (int)(t % nv) + (vel ? nv : 0);
   }
-  // every value is formed in registers from the base state and stored once: a load after
-  // the instance's own stores would wait for all of them (one vmcnt counter)
-  Lane<64> d = lane_view(mr, (int)(inst >> 6), (int)(inst & 63));
-  const int nv = m.nv;
-  const long bq = b*m.nq, bv = b*m.nv;
-  const int pa = (p >= 1 && p <= nv) ? p - 1 : -1;          // qacc_i + eps
-  const int pv = (p > nv && p <= 2*nv) ? p - 1 - nv : -1;   // qvel_i + eps
-  for (int k = 0; k < nv; k++) {
-    const double x = qvel[bv + k];
-    d.qvel[k] = k == pv ? x + eps : x;
+  Lane<64> d = lane_view(mr, (int)(inst >> 6), lane);
+  if (comp < nv) {                       // qvel_k (+ eps on the qvel perturbation k)
+    const double x = qvel[b*nv + comp];
+    d.qvel[comp] = p - 1 - nv == comp ? x + eps : x;
+    continue;
   }
-  for (int k = 0; k < nv; k++) {
-    const double x = qacc[bv + k];
-    d.qacc[k] = k == pa ? x + eps : x;
+  if (comp < 2*nv) {                     // qacc_k (+ eps on the qacc perturbation k)
+    const int k = comp - nv;
+    const double x = qacc[b*nv + k];
+    d.qacc[k] = p - 1 == k ? x + eps : x;
+    continue;
   }
-  if (ctrl) {                          // flg_actuation: the base state's controls
-    for (int k = 0; k < m.nu; k++) d.ctrl[k] = ctrl[b*m.nu + k];
+  if (comp >= 2*nv + m.njnt) {           // flg_actuation: the base state's controls
+    const int k = comp - 2*nv - m.njnt;
+    d.ctrl[k] = ctrl[b*m.nu + k];
+    continue;
   }
-  if (p <= 2*nv) {
-    for (int k = 0; k < m.nq; k++) d.qpos[k] = qpos[bq + k];
-    return;
-  }
-  // mj_integratePos(m, qpos, e_i, eps), engine_support.c:1518-1550, joint by joint
-  const int i = p - 1 - 2*nv;
-  for (int j = 0; j < m.njnt; j++) {
-    int padr = m.jnt_qposadr[j], vadr = m.jnt_dofadr[j];
-    int t = m.jnt_type[j];
-    if (t == mjhipJNT_FREE) {
-      for (int c = 0; c < 3; c++) {
-        d.qpos[padr+c] = qpos[bq + padr + c] + eps * (vadr + c == i ? 1.0 : 0.0);
-      }
-      padr += 3;
-      vadr += 3;
-      t = mjhipJNT_BALL;
+  // joint j's qpos: the base state's, or mj_integratePos(m, qpos, e_i, eps) for the qpos
+  // perturbation of dof i (engine_support.c:1518-1550)
+  const int j = comp - 2*nv, i = p > 2*nv ? p - 1 - 2*nv : -1;
+  int padr = m.jnt_qposadr[j], vadr = m.jnt_dofadr[j], t = m.jnt_type[j];
+  const long bq = b*nq;
+  if (t == mjhipJNT_FREE) {
+    for (int c = 0; c < 3; c++) {
+      d.qpos[padr+c] = i < 0 ? qpos[bq + padr + c]
+                             : qpos[bq + padr + c] + eps * (vadr + c == i ? 1.0 : 0.0);
     }
-    if (t == mjhipJNT_BALL) {
-      double q[4] = {qpos[bq + padr], qpos[bq + padr + 1], qpos[bq + padr + 2],
-                     qpos[bq + padr + 3]};
-      double vel[3] = {vadr == i ? 1.0 : 0.0, vadr + 1 == i ? 1.0 : 0.0,
-                       vadr + 2 == i ? 1.0 : 0.0};
+    padr += 3;
+    vadr += 3;
+    t = mjhipJNT_BALL;
+  }
+  if (t == mjhipJNT_BALL) {
+    double q[4] = {qpos[bq + padr], qpos[bq + padr + 1], qpos[bq + padr + 2],
+                   qpos[bq + padr + 3]};
+    if (i >= 0) {
+      const double vel[3] = {vadr == i ? 1.0 : 0.0, vadr + 1 == i ? 1.0 : 0.0,
+                             vadr + 2 == i ? 1.0 : 0.0};
       mjh::quatIntegrate(q, vel, eps);
-      for (int c = 0; c < 4; c++) d.qpos[padr+c] = q[c];
-    } else {
-      d.qpos[padr] = qpos[bq + padr] + eps * (vadr == i ? 1.0 : 0.0);
     }
+    for (int c = 0; c < 4; c++) d.qpos[padr+c] = q[c];
+  } else {
+    d.qpos[padr] = i < 0 ? qpos[bq + padr] : qpos[bq + padr] + eps * (vadr == i ? 1.0 : 0.0);
   }
-}
-
-// The stage-skip fall-back of mjhip_inverseFDBatch, decided on the device: when k_vaskip
-// found a centre with limit rows (fdflag[0]), the qvel/qacc perturbations [first, end) run the
-// full pipeline as well (their own position stage and rows), else the range is empty.
-__global__ void k_fd_gate(int* __restrict__ fdflag, int first, int end) {
-  fdflag[1] = first;
-  fdflag[2] = fdflag[0] ? end : first;
+  }
 }
 
 // diff(): DfD*[b][i][:] = (f(perturbed) - f(centre)) / eps  (engine_derivative_fd.c:48-53)
@@ -469,7 +480,8 @@ struct mjhipContext_ {
   int wl_last = 0;                         // counter the last fast launch used
   int last_path = -1;                      // mjhip_contextLastPath
   // mjhip_inverseFDBatch's stage-skip fall-back, decided on the device: [0] a centre has limit
-  // rows (k_vaskip), [1..2] the instance range {first, end} k_fd_gate hands to k_all
+  // rows (k_vaskip), [1..2] the instance range {first, end} the gated k_fd_expand hands to
+  // k_all
   int* fdflag = nullptr;
   CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
   mjh::ContactParam* cparams = nullptr;    // each program pair's mj_contactParam
@@ -1127,6 +1139,11 @@ static int finish_fast(mjhipContext* c, int B, dim3 grid, dim3 block, int skipse
   return MJHIP_OK;
 }
 
+// internal launch_inverse flag (not a public MJHIP_FLAG_*): run the straight-line kernel of a
+// work-list model without its constraint kernel; the next launch_inverse call continues the
+// same work-list and serves both (the bare pipeline only: the FD stage-skip layout)
+constexpr int kFlagDeferRows = 1 << 30;
+
 // range: null, or a device-side instance range {first, end} for the straight-line kernel (B
 // then only sizes the grid: end - first <= B); only the FD fall-back uses it, on models whose
 // whole pipeline is the straight-line and constraint kernels
@@ -1200,6 +1217,11 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
                       &efc, (void*)&range};
       HIPCHECK(hipModuleLaunchKernel(c->rt_fn, grid.x, 1, 1, 64, 1, 1, 0, c->stream, args,
                                      nullptr));
+    }
+    if (flags & kFlagDeferRows) {
+      // mjhip_inverseFDBatch: the work-list this launch filled is served after the next
+      // launch, which appends to the same counter (the parity is not flipped)
+      return MJHIP_OK;
     }
     if (c->spatial) {                    // spatial tendons and all of mj_passive
       hipLaunchKernelGGL(k_tendon_after, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
@@ -1869,14 +1891,17 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
   // with a skip layout only the position-stage block is expanded: the skip kernels read their
   // centre's inputs and perturb them in registers (the fall-back expands the rest, below)
   const long nexp = layout ? nA : ninst;
-  hipLaunchKernelGGL(k_fd_expand, dim3((nexp + 255)/256), dim3(256), 0, c->stream,
-                     c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, layout,
-                     layout ? c->fdflag : nullptr, (long)0, nexp, (const int*)nullptr);
+  const int ncomp = 2*nv + m.njnt + ((m.nu && dc) ? m.nu : 0);
+  hipLaunchKernelGGL(k_fd_expand, dim3((unsigned)(((nexp + 63)/64)*ncomp)), dim3(64), 0,
+                     c->stream, c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr),
+                     eps, layout, layout ? c->fdflag : nullptr, (long)0, nexp, 0);
   FDCHECK(hipGetLastError(), "k_fd_expand launch");
   if (layout) {
-    // the nv+1 position-stage instances of every base state: the full pipeline
+    // the nv+1 position-stage instances of every base state: the full pipeline (a work-list
+    // model's rows are served once, after the fall-back below has added its own)
+    const bool defer = c->fast->cmode == 1 && c->fast->launch;
     rc = launch_inverse(c, (int)nA, nullptr, nullptr, nullptr, nullptr, mjhipSTAGE_NONE,
-                        nullptr, 0, skipsensor);
+                        nullptr, defer ? kFlagDeferRows : 0, skipsensor);
     if (rc) return rc;
     if (layout == 2) {
       // the nv qacc perturbations: the acceleration stage over their centre's position and
@@ -1893,16 +1918,13 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
       // a work-list model whose centre has limit rows: its perturbations need the rows'
       // velocity and acceleration terms, so every qvel/qacc perturbation then runs the full
       // pipeline over its own slot (the same layout; results as without skipping). Decided on
-      // the device: k_fd_gate turns the flag into the range k_all reads, empty when no centre
-      // has rows, so the call needs no host round trip.
-      hipLaunchKernelGGL(k_fd_gate, dim3(1), dim3(1), 0, c->stream, c->fdflag, (int)nA,
-                         (int)ninst);
-      FDCHECK(hipGetLastError(), "k_fd_gate launch");
-      // the perturbations' own inputs, for the full pipeline over them: the gate's range,
-      // empty when no centre has rows
-      hipLaunchKernelGGL(k_fd_expand, dim3((ninst - nA + 255)/256), dim3(256), 0, c->stream,
-                         c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr), eps, layout,
-                         (int*)nullptr, nA, ninst, (const int*)(c->fdflag + 1));
+      // the device: the gated expansion below turns the flag into the range k_all reads,
+      // empty when no centre has rows, so the call needs no host round trip.
+      // the perturbations' own inputs, for the full pipeline over them (only when a centre
+      // has rows)
+      hipLaunchKernelGGL(k_fd_expand, dim3((unsigned)((ninst - nA + 63)/64)), dim3(64),
+                         0, c->stream, c->dmodel, c->mirror, B, dq, dv, da,
+                         (m.nu ? dc : nullptr), eps, layout, c->fdflag, nA, ninst, 1);
       FDCHECK(hipGetLastError(), "k_fd_expand (fall-back) launch");
       rc = launch_inverse(c, (int)(ninst - nA), nullptr, nullptr, nullptr, nullptr,
                           mjhipSTAGE_NONE, nullptr, 0, skipsensor, c->fdflag + 1);

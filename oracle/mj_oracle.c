@@ -4298,15 +4298,12 @@ static void or_shape(orShape* s, const mjhipModel* m, const mjhipData* d, int g,
   }
 }
 
-/* mjc_Convex (convex.c:915-1001) through mjc_CCDIteration (:792-819), native solver, one
- * contact (mjENBL_MULTICCD off) */
-static int col_convex(orRaw* c, const mjhipModel* m, const mjhipData* d, int g1, int g2,
-                      mjtNum margin) {
-  orShape A, B;
-  or_shape(&A, m, d, g1, margin);
-  or_shape(&B, m, d, g2, margin);
+/* mjc_CCDIteration (convex.c:792-819), native solver, one contact, on the shapes' current
+ * frames */
+static int col_ccdIteration(orRaw* c, const mjhipModel* m, orShape* A, orShape* B,
+                            mjtNum margin) {
   orCCD st;
-  mjtNum dist = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, 0, 1);
+  mjtNum dist = or_ccd(&st, A, B, m->opt.ccd_iterations, m->opt.ccd_tolerance, 0, 1);
   if (!(dist < 0) || st.nx < 1) return 0;
   c->dist = margin + dist;
   mju_sub3(c->frame, st.x1, st.x2);
@@ -4316,6 +4313,98 @@ static int col_convex(orRaw* c, const mjhipModel* m, const mjhipData* d, int g1,
   c->pos[2] = 0.5*(st.x1[2] + st.x2[2]);
   mju_zero3(c->frame + 3);
   return 1;
+}
+
+static mjtNum mju_dist3(const mjtNum a[3], const mjtNum b[3]);
+
+/* mju_mulMatMat3 (engine_util_blas.c:193-203) */
+static void mju_mulMatMat3(mjtNum r[9], const mjtNum a[9], const mjtNum b[9]) {
+  for (int i = 0; i < 3; i++) {
+    for (int j = 0; j < 3; j++) {
+      r[3*i+j] = a[3*i]*b[j] + a[3*i+1]*b[3+j] + a[3*i+2]*b[6+j];
+    }
+  }
+}
+
+/* mju_rotateFrame (convex.c:862-880): the frame rotated by rot about origin */
+static void or_rotateFrame(const mjtNum origin[3], const mjtNum rot[9], mjtNum xmat[9],
+                           mjtNum xpos[3]) {
+  mjtNum mat[9], vec[3], rel[3];
+  mju_mulMatMat3(mat, rot, xmat);
+  mju_copy(xmat, mat, 9);
+  mju_sub3(rel, origin, xpos);
+  mju_mulMatVec3(vec, rot, rel);
+  mju_sub3(vec, vec, rel);
+  mju_sub3(xpos, xpos, vec);
+}
+
+/* mjc_Convex (convex.c:915-1001) through mjc_CCDIteration (:792-819), native solver: one
+ * contact, then with mjENBL_MULTICCD, for pairs without a sphere or an ellipsoid and outside
+ * the box / mesh single pass (meshes are outside this restatement's multiccd subset), the
+ * extra contacts of the perturbed frames (:933-999): both geoms rotated about the first
+ * contact by -+1e-3 rad around its frame's y and z axes (geom 2 the other way), each new
+ * contact farther than 1e-3 min(rbound) from every earlier one kept with the first one's
+ * depth. The frames are perturbed on local copies (the reference rotates mjData's in place
+ * and restores them). */
+static int col_convex(orRaw* c, const mjhipModel* m, const mjhipData* d, int g1, int g2,
+                      mjtNum margin) {
+  orShape A, B;
+  mjtNum xpos1[3], xmat1[9], xpos2[3], xmat2[9];
+  mju_copy3(xpos1, d->geom_xpos + 3*g1);
+  mju_copy(xmat1, d->geom_xmat + 9*g1, 9);
+  mju_copy3(xpos2, d->geom_xpos + 3*g2);
+  mju_copy(xmat2, d->geom_xmat + 9*g2, 9);
+  or_shape(&A, m, d, g1, margin);
+  or_shape(&B, m, d, g2, margin);
+  mjtNum p1[3], r1[9], p2[3], r2[9];
+  mju_copy3(p1, xpos1);
+  mju_copy(r1, xmat1, 9);
+  mju_copy3(p2, xpos2);
+  mju_copy(r2, xmat2, 9);
+  A.pos = p1; A.mat = r1;
+  B.pos = p2; B.mat = r2;
+  int ncon = col_ccdIteration(c, m, &A, &B, margin);
+  const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  if (ncon == 1 && mjENABLED(mjhipENBL_MULTICCD) && t1 != mjhipGEOM_ELLIPSOID &&
+      t1 != mjhipGEOM_SPHERE && t2 != mjhipGEOM_ELLIPSOID && t2 != mjhipGEOM_SPHERE) {
+    const mjtNum relative_tolerance = 1e-3, perturbation_angle = 1e-3;
+    mjtNum frame[9];
+    mju_copy(frame, c[0].frame, 9);
+    mju_makeFrame(frame);
+    const mjtNum tolerance = relative_tolerance * mjMIN(m->geom_rbound[g1], m->geom_rbound[g2]);
+    const mjtNum* axes[2] = {frame + 3, frame + 6};
+    const mjtNum angles[2] = {-perturbation_angle, perturbation_angle};
+    for (int ai = 0; ai < 2; ai++) {
+      for (int gi = 0; gi < 2; gi++) {
+        mjtNum quat[4], rot[9], invrot[9];
+        mju_axisAngle2Quat(quat, axes[ai], angles[gi]);
+        mju_quat2Mat(rot, quat);
+        or_rotateFrame(c[0].pos, rot, r1, p1);
+        for (int i = 0; i < 3; i++) {
+          for (int j = 0; j < 3; j++) invrot[3*j+i] = rot[3*i+j];
+        }
+        or_rotateFrame(c[0].pos, invrot, r2, p2);
+        int fresh = col_ccdIteration(c + ncon, m, &A, &B, margin);
+        if (fresh) {                          /* mjc_isDistinctContact (:851-858) */
+          for (int i = 0; i < ncon; i++) {
+            if (mju_dist3(c[i].pos, c[ncon].pos) <= tolerance) {
+              fresh = 0;
+              break;
+            }
+          }
+        }
+        if (fresh) {
+          c[ncon].dist = c[0].dist;
+          ncon++;
+        }
+        mju_copy3(p1, xpos1);
+        mju_copy(r1, xmat1, 9);
+        mju_copy3(p2, xpos2);
+        mju_copy(r2, xmat2, 9);
+      }
+    }
+  }
+  return ncon;
 }
 
 /* mju_sign (engine_util_misc.c:1018-1026), mju_dist3 (engine_util_blas.c:157-160),
@@ -4806,12 +4895,14 @@ static int or_collisionFunc(const mjhipModel* m, int t1, int t2) {
     if (mjDISABLED(mjhipDSBL_NATIVECCD) && t1 == mjhipGEOM_HFIELD) return -1;
   }
   if (k > 0 && or_isConvexPair(t1, t2)) {
-    /* mjc_Convex with the libccd MPR fallback, or MULTICCD's perturbed extra contacts (pairs
-       without a sphere or ellipsoid, convex.c:936-999): not restated */
+    /* mjc_Convex with the libccd MPR fallback: not restated. MULTICCD (pairs without a
+       sphere or ellipsoid): up to 5 contacts (the first and four perturbed ones,
+       convex.c:933-999); with a mesh the box/mesh single pass's polygon or the perturbation
+       of mesh supports is not restated */
     if (mjDISABLED(mjhipDSBL_NATIVECCD)) return -1;
     if (mjENABLED(mjhipENBL_MULTICCD) && t1 != mjhipGEOM_SPHERE && t1 != mjhipGEOM_ELLIPSOID &&
         t2 != mjhipGEOM_ELLIPSOID) {
-      return -1;
+      return t2 == mjhipGEOM_MESH ? -1 : 5;
     }
   }
   return k;

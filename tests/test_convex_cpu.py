@@ -187,21 +187,100 @@ def test_slider_crank_no_longer_flagged():
 
 
 def test_outside_the_native_single_contact_path_is_flagged():
-  """mjDSBL_NATIVECCD (libccd's MPR) and mjENBL_MULTICCD on a pair without a sphere or an
-  ellipsoid (the perturbed extra contacts) are not built: such a pair adds no capacity and an
+  """mjDSBL_NATIVECCD (libccd's MPR) and mjENBL_MULTICCD on a mesh pair (the box / mesh single
+  pass needs the mesh polygon data) are not built: such a pair adds no capacity and an
   instance where it passes the filters is flagged; MULTICCD with an ellipsoid is computed
-  (the reference takes the single-contact path for it)."""
-  base = """<mujoco><option gravity="0 0 0">{flag}</option><worldbody>
+  (the reference takes the single-contact path for it), and on a pair of cylinders the
+  perturbation pass gives it up to five contacts."""
+  base = """<mujoco><option gravity="0 0 0">{flag}</option>
+    <asset><mesh name="tet" vertex="0 0 0  .2 0 0  0 .2 0  0 0 .2"/></asset><worldbody>
     <body><freejoint/><geom type="cylinder" size=".2 .1"/></body>
-    <body pos=".05 0 .17"><freejoint/><geom type="{t2}" size="{s2}"/></body>
+    <body pos=".05 0 .17"><freejoint/><geom type="{t2}" size="{s2}" {mesh}/></body>
     </worldbody></mujoco>"""
-  for flag, t2, s2, want in (('<flag nativeccd="disable"/>', "cylinder", ".1 .1", 32),
-                             ('<flag multiccd="enable"/>', "cylinder", ".1 .1", 32),
-                             ('<flag multiccd="enable"/>', "ellipsoid", ".1 .1 .1", 0)):
-    m = mjcf.load_xml_string(base.format(flag=flag, t2=t2, s2=s2))
+  for flag, t2, s2, want, cap in (
+      ('<flag nativeccd="disable"/>', "cylinder", ".1 .1", 32, 0),
+      ('<flag multiccd="enable"/>', "mesh", "", 32, 0),
+      ('<flag multiccd="enable"/>', "ellipsoid", ".1 .1 .1", 0, 1),
+      ('<flag multiccd="enable"/>', "cylinder", ".1 .1", 0, 5)):
+    m = mjcf.load_xml_string(base.format(flag=flag, t2=t2, s2=s2,
+                                         mesh='mesh="tet"' if t2 == "mesh" else ""))
     cm = host.model_struct(m)
-    assert olib().or_contactCapacity(ctypes.byref(cm)) == (0 if want else 1)
+    assert olib().or_contactCapacity(ctypes.byref(cm)) == cap
     o, k = Oracle(m), KernelCPU(m)
     o.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
     _, st = k.inverse(m.qpos0, np.zeros(m.nv), np.zeros(m.nv))
     assert o.d.status == st == want, (flag, t2)
+
+
+# engine_collision_convex_test.cc:60-77 (CylinderBox): testdata/collision_convex/cylinder_box.xml
+CYLINDER_BOX = """<mujoco><option><flag multiccd="enable"/></option><worldbody>
+  <geom type="box" size="1 1 .3" pos="0 0 -.3"/>
+  <body pos="0 0 .02"><freejoint/><geom type="cylinder" size=".4 .03"/></body>
+  </worldbody></mujoco>"""
+
+
+def test_multiccd_cylinder_box_known_answer():
+  """MjcConvexTest.CylinderBox (engine_collision_convex_test.cc:60-77): the cylinder lying in
+  the box face gives 5 contacts with mjENBL_MULTICCD (mjc_Convex's perturbation pass,
+  engine_collision_convex.c:933-999) and 1 without; the device code on the host agrees with
+  the oracle bit for bit on every contact, row and output."""
+  for multi, want in ((True, 5), (False, 1)):
+    m = mjcf.load_xml_string(CYLINDER_BOX if multi else CYLINDER_BOX.replace(
+        '<flag multiccd="enable"/>', ''))
+    o, k = Oracle(m), KernelCPU(m)
+    z = np.zeros(m.nv)
+    o.inverse(m.qpos0, z, z)
+    _, st = k.inverse(m.qpos0, z, z)
+    assert o.d.status == st == 0
+    assert o.efc.ncon == want and k.field("con_count")[0] == want
+    width = dict(CON_DOUBLE + CON_INT)
+    for name in CON_FIELDS:
+      ref = o.contact_field(name).reshape(want, width[name])
+      np.testing.assert_array_equal(k.field(name)[:ref.size].reshape(want, width[name]), ref,
+                                    err_msg=name)
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name),
+                                      err_msg=f.name)
+    # with the flag, the four perturbed contacts carry the first one's depth
+    dist = o.contact_field("con_dist")
+    assert (dist == dist[0]).all()
+
+
+_MULTI_CASES = [("capsule", "cylinder"), ("cylinder", "cylinder"), ("cylinder", "box")]
+
+
+@pytest.mark.parametrize("t1,t2", _MULTI_CASES)
+def test_multiccd_device_code_bitexact(t1, t2):
+  """mjENBL_MULTICCD's perturbation pass on random relative poses: the device pipeline on the
+  host equals the oracle bit for bit on every contact field, row and output, and some poses
+  give several contacts."""
+  xml = _PAIRS.format(t1=t1, t2=t2, s1=_SIZES[t1], s2=_SIZES[t2], mg=0).replace(
+      '<option gravity="0 0 0"/>', '<option gravity="0 0 0"><flag multiccd="enable"/></option>')
+  m = mjcf.load_xml_string(xml)
+  o, k = Oracle(m), KernelCPU(m)
+  rng = np.random.default_rng(7 + _MULTI_CASES.index((t1, t2)))
+  width = dict(CON_DOUBLE + CON_INT)
+  multi = 0
+  for i in range(60):
+    q = m.qpos0.copy()
+    _random_pose(rng, q, 0, 0.05)
+    _random_pose(rng, q, 1, 0.2)
+    v, a = rng.normal(size=m.nv), rng.normal(size=m.nv)
+    o.inverse(q, v, a)
+    _, st = k.inverse(q, v, a)
+    assert st == o.d.status == 0, (i, st, o.d.status)
+    ncon = o.efc.ncon
+    geoms = o.contact_field("con_geom").reshape(ncon, 2)
+    per = np.bincount([0 if m.geom_type[g[0]] == 0 else 1 for g in geoms], minlength=2)
+    multi += per[1] > 1
+    assert k.field("con_count")[0] == ncon
+    for name in CON_FIELDS:
+      ref = o.contact_field(name).reshape(ncon, width[name])
+      np.testing.assert_array_equal(k.field(name)[:ref.size].reshape(ncon, width[name]), ref,
+                                    err_msg=f"{name} inst {i}")
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name),
+                                      err_msg=f"{f.name} inst {i}")
+  assert multi >= 3, multi

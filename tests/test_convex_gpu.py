@@ -135,3 +135,39 @@ def test_convex_pairs_parity():
   assert same.all()
   assert err.max() <= RTOL
   assert self_frac > 0.1                      # the scene is one where that matters
+
+
+def test_multiccd_parity():
+  """mjENBL_MULTICCD on the device: the reference's CylinderBox known answer
+  (engine_collision_convex_test.cc:60-77: 5 contacts with the flag, 1 without) and the
+  five-body scene with the flag on (mjc_Convex's perturbation pass on the capsule-cylinder,
+  cylinder-cylinder and cylinder-box pairs, engine_collision_convex.c:933-999), contacts bit
+  for bit and qfrc_inverse within the north-star bar against the oracle."""
+  from test_convex_cpu import CYLINDER_BOX
+  for xml, want in ((CYLINDER_BOX, 5),
+                    (CYLINDER_BOX.replace('<flag multiccd="enable"/>', ''), 1)):
+    m = mjcf.load_xml_string(xml)
+    q = np.tile(m.qpos0, (64, 1))
+    z = np.zeros((64, m.nv))
+    f, ref, ncon, derr, cerr = _run(m, q, z, z)
+    assert (ncon == want).all(), (ncon[:4], want)
+    assert derr.max() == 0 and cerr.max() == 0
+    assert _err(f, ref).max() <= RTOL
+  m = mjcf.load_xml_string(_MODEL.replace('<option gravity="0 0 -9.81"/>',
+                                          '<option gravity="0 0 -9.81"><flag multiccd="enable"/>'
+                                          '</option>'))
+  B = 512
+  rng = np.random.default_rng(9)
+  q = np.tile(m.qpos0, (B, 1))
+  for b in range(5):
+    q[:, 7*b:7*b + 2] = rng.uniform(-0.25, 0.25, (B, 2))
+    q[:, 7*b + 2] = rng.uniform(0.05, 0.35, B)
+    qq = rng.normal(size=(B, 4))
+    q[:, 7*b + 3:7*b + 7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
+  v, a = rng.normal(size=(B, m.nv)), rng.normal(size=(B, m.nv))
+  f, ref, ncon, derr, cerr = _run(m, q, v, a)
+  err = _err(f, ref)
+  print(f"multiccd scene: {int(ncon.sum())} contacts, max con_dist error {derr.max():.2e}, "
+        f"max contact field error {cerr.max():.2e}, max qfrc_inverse error {err.max():.2e}")
+  assert derr.max() == 0 and cerr.max() <= 1e-12
+  assert err.max() <= RTOL
