@@ -267,8 +267,9 @@ def main():
                      "traffic_unit": "bytes per launch", "traffic_source": traffic_src,
                      "traffic_ratio": (traffic / (bytes_per_eval * count)) if traffic else None,
                      "algorithmic_bytes_per_launch": bytes_per_eval * count,
-                     "kernel": ("+".join(codegen.hot_kernels(eng.fast_kernel))
-                                + "+k_constraint" if eng.fast_kernel else "k_inverse<0>"),
+                     "kernel": ("+".join(codegen.hot_kernels(eng.fast_kernel)
+                                         + [eng.constraint_kernel])
+                                if eng.fast_kernel else "k_inverse<0>"),
                      "kernel_ms": kernel_ms,
                      "kernel_ms_method": "HIP events on the context's stream around `reps` "
                                          "back-to-back launches of the hot path, divided by "
@@ -324,7 +325,7 @@ def other_config(args):
          "unit": "evals/s", "n_gpus": 1, "steps": args.steps, "ms_per_step": dt * 1e3,
          "kernel_ms": kernel_ms, "dtype": "f64",
          "kernel": (f"generated {'+'.join(codegen.hot_kernels(eng.fast_kernel))} + "
-                    f"{getattr(eng, 'constraint_kernel', 'k_constraint')}" if eng.fast_kernel
+                    f"{eng.constraint_kernel}" if eng.fast_kernel
                     else "k_inverse<0, contacts> (generic)"),
          "config": {"workload": f"{args.model} keyframe poses + noise, contacts on",
                     "batch": B},

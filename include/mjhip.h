@@ -335,6 +335,10 @@ MJHIP_API int mjhip_contextLoadKernel(mjhipContext* c, const void* image, size_t
  * kernel beside the fac / va stages, joined by the assembly; opt-in with MJHIP_SPLIT=1);
  * -1 before any call */
 MJHIP_API int mjhip_contextLastPath(const mjhipContext* c);
+/* the constraint kernel the context's last straight-line call launched, e.g.
+ * "k_constraint_coop<16, false, true, false>" (the work-list kernel of a limits-only model) or
+ * "k_constraint<true, true, false>"; "none" when it launched none (profiles name it) */
+MJHIP_API const char* mjhip_contextConstraintKernel(const mjhipContext* c);
 /* instances of the last fast-path call that had active constraint rows and were recomputed
  * by the generic kernel (blocking read; -1 on error) */
 MJHIP_API int mjhip_worklistCount(mjhipContext* c);
@@ -421,11 +425,13 @@ MJHIP_API int mjhip_modelCapacity(const mjhipModel* m, int* efc_rows, int* conta
  * row-major geom_xmat), both inflated by margin[i] (mjc_initCCDObj's margin; NULL: 0), with
  * the mjCCDConfig {max_iterations, tolerance, max_contacts, dist_cutoff}. max_contacts 0 asks
  * for the distance alone (no penetration recovery), 1 for one contact, more for the
- * multicontact polygon of a penetrating box pair (gjk.c:1460-2193). Outputs (host arrays):
+ * multicontact polygon of a penetrating box / mesh pair (gjk.c:1460-2193; mesh polygons from
+ * the compiler, mjCMesh::MakePolygons). Outputs (host arrays):
  * dist[n] (mjc_ccd's return value), nx[n] (status.nx), x1/x2 (n x xcap x 3, status.x1/x2: the
  * witness points, xcap = max(1, min(max_contacts, mjMAXCONPAIR = 50))). Status codes as
  * everywhere; MJHIP_ERR_MODEL when a pair's polytope outgrew the solver's face capacity or
- * needs multicontact on a mesh (the mesh polygon data is not compiled). */
+ * needs multicontact beyond the device's polygon capacity (a mesh polygon of more than 16
+ * vertices, or a vertex on more than 16 polygons; the reference allows 150). */
 MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g2,
                              const mjtNum* pos1, const mjtNum* mat1, const mjtNum* pos2,
                              const mjtNum* mat2, const mjtNum* margin, int max_iterations,

@@ -117,8 +117,8 @@ MJHIP_CONTACT_HD int mjhip_isConvexPair(int t1, int t2) {
  * function that this engine does not implement. mjc_Convex runs the native GJK/EPA solver
  * for one contact (mjc_CCDIteration, engine_collision_convex.c:792-819); with MULTICCD, a
  * pair without a sphere or an ellipsoid adds up to four perturbed contacts (:933-999), 5 in
- * all, except with a mesh (the box / mesh single pass's polygon needs the mesh polygon data,
- * not compiled here); the libccd MPR fallback (mjDSBL_NATIVECCD) is not built. mjc_PlaneConvex gives a mesh up to
+ * all (a box / mesh pair without margin: up to 4 from the multicontact polygon, :895-909);
+ * the libccd MPR fallback (mjDSBL_NATIVECCD) is not built. mjc_PlaneConvex gives a mesh up to
  * maxplanemesh = 3 contacts (:1006), mjc_ConvexHField up to mjMAXCONPAIR = 50 (one per prism,
  * mjhip_geomPairMaxContacts bounds it by the field's grid). */
 MJHIP_CONTACT_HD int mjhip_pairMaxContacts(const mjhipModel* m, int t1, int t2) {
@@ -130,7 +130,7 @@ MJHIP_CONTACT_HD int mjhip_pairMaxContacts(const mjhipModel* m, int t1, int t2) 
     if (m->opt.disableflags & mjhipDSBL_NATIVECCD) return -1;
     if ((m->opt.enableflags & mjhipENBL_MULTICCD) && t1 != mjhipGEOM_SPHERE &&
         t1 != mjhipGEOM_ELLIPSOID && t2 != mjhipGEOM_ELLIPSOID) {
-      return t2 == mjhipGEOM_MESH ? -1 : 5;
+      return 5;
     }
     return 1;
   }

@@ -49,6 +49,9 @@
   XS(nmeshvert)   \
   XS(nmeshface)   \
   XS(nmeshgraph)  \
+  XS(nmeshpoly)   \
+  XS(nmeshpolyvert) \
+  XS(nmeshpolymap) \
   XS(nhfield)     \
   XS(nhfielddata)
 
@@ -228,6 +231,15 @@
   X(float,   mesh_vert,            nmeshvert, 3) \
   X(int,     mesh_face,            nmeshface, 3) \
   X(int,     mesh_graph,           nmeshgraph, 1) \
+  X(int,     mesh_polynum,         nmesh,     1) \
+  X(int,     mesh_polyadr,         nmesh,     1) \
+  X(mjtNum,  mesh_polynormal,      nmeshpoly, 3) \
+  X(int,     mesh_polyvertadr,     nmeshpoly, 1) \
+  X(int,     mesh_polyvertnum,     nmeshpoly, 1) \
+  X(int,     mesh_polyvert,        nmeshpolyvert, 1) \
+  X(int,     mesh_polymapadr,      nmeshvert, 1) \
+  X(int,     mesh_polymapnum,      nmeshvert, 1) \
+  X(int,     mesh_polymap,         nmeshpolymap, 1) \
   X(mjtNum,  hfield_size,          nhfield,   4) \
   X(int,     hfield_nrow,          nhfield,   1) \
   X(int,     hfield_ncol,          nhfield,   1) \

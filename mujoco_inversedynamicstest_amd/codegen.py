@@ -105,6 +105,39 @@ NT_LOAD_STAGES = ()
 NT_LOAD_SV_STAGES = ("va",)
 
 
+# mjd_inverseFD's perturbed instances (mjhip_inverseFDBatch with a stage-skip layout, whose
+# centres come first): a mirror field the straight-line stages store but never load is read
+# by no later kernel of that call either -- the finite differences read qfrc_inverse (and qM
+# for DmDq), a work-list model's limit rows the fields below -- so for instance blocks at or
+# past Mirror::full_blk its stores go to the context's sink (Mirror::sink: one small region
+# that every such wave overwrites, so its lines stay in L2) instead of the instance's slot.
+# The stores themselves stay: the arithmetic, and so every result, is the full kernel's bit
+# for bit. Mirror::sink null (every other launch) stores everything.
+FD_KEEP = frozenset({"qpos", "qvel", "qacc", "qfrc_inverse", "qfrc_passive", "qfrc_constraint",
+                     "qfrc_actuator", "ten_length", "ten_J", "ten_velocity", "actuator_length",
+                     "actuator_moment", "actuator_velocity", "qM", "sensordata"})
+
+
+def fd_elided(bodies) -> set:
+  """The mirror fields the stage bodies store and never load, less FD_KEEP."""
+  import re
+  text = re.sub(r"double\* __restrict__ P_\w+ = [^;]*;", "", "\n".join(bodies))
+  store_nt = re.compile(r"MJH_NT_STORE(?:_IF)?\((?:\w+, )?P_(\w+)\[")
+  store_eq = re.compile(r"^\s*P_(\w+)\[[^\]]+\] = ", re.M)
+  stores = set(store_nt.findall(text)) | set(store_eq.findall(text))
+  loads = set(re.findall(r"P_(\w+)\[", store_eq.sub("", store_nt.sub("", text))))
+  return stores - loads - FD_KEEP
+
+
+def _sink_stores(body: str, elided) -> str:
+  """Point the elided fields' stores of instance blocks past Mirror::full_blk at the sink."""
+  import re
+  decl = re.compile(r"double\* __restrict__ P_(\w+) = (mr\.\w+ \+ \(\(long\)blk\*\d+\)\*64) \+ lane;")
+  return decl.sub(lambda mt: mt.group(0) if mt.group(1) not in elided else
+                  f"double* __restrict__ P_{mt.group(1)} = (mr.sink && blk >= mr.full_blk ? "
+                  f"mr.sink : {mt.group(2)}) + lane;", body)
+
+
 def _ll(st):
   """LDS lane index and stride of stage st (LDS arrays are per workgroup)."""
   n = LANES[st]
@@ -1487,6 +1520,9 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
                             b)
                    if st in NT_LOAD_SV_STAGES and st not in NT_LOAD_STAGES else b)
               for st, b in bodies.items()}
+  if M.cmode in ("none", "list") and store_fields is None:
+    elided = fd_elided(bodies.values())
+    bodies = {st: _sink_stores(b, elided) for st, b in bodies.items()}
   out = [f"// GENERATED by mujoco_inversedynamicstest_amd/codegen.py -- do not edit.",
          f"// model '{name}' (nq={m.nq} nv={m.nv} nbody={m.nbody}), hash {model_hash(m)}"]
   exact = exact_fp(m)

@@ -1961,6 +1961,7 @@ struct CcdShape {
   const float* vert;
   const int* graph;
   int nvert, vertindex, meshindex;
+  int meshid;                               // the mesh (multicontact's polygon data), or -1
   // a height-field prism (mjCCDObj.prism): its three corners' x, y, their top z and the
   // common bottom z (the reference's six vertices share x, y and the bottom z)
   double px[3], py[3], pzt[3], pzb;
@@ -3068,12 +3069,17 @@ MJH_HD void ccdCenter(double c[3], const CcdShape& s) {
 // vertex's box corner (Vertex.index1/2, set by mjc_boxSupport's vertindex); here the corner is
 // read back from the witness point itself -- the sign pattern of its box-frame coordinates,
 // which is the support's `tmp` sign pattern -- so the solver's memory layout is unchanged.
-// Meshes need the compiler's polygon data (not built): unsupported. Only k_ccd
-// (mjhip_ccdBatch) compiles this in (ccdRun's MULTI), with private arrays.
+// A mesh vertex is read back by finding the vertex whose global position is the witness point
+// bit for bit (the support computed it from that vertex with the same operations); the mesh
+// polygons are the compiler's (mjCMesh::MakePolygons, meshes.py). Only k_ccd (mjhip_ccdBatch)
+// compiles this in (ccdRun's MULTI), with private arrays sized for polygons of up to
+// CCD_MAXFACE vertices and vertices on up to CCD_MAXFACE polygons (the reference's bound is
+// mjMAX_POLYVERT = 150; a larger one is refused, MJHIP_ERR_MODEL).
 constexpr double CCD_FACE_TOL = 0.99999872;     // mjFACE_TOL (gjk.h:29)
 constexpr double CCD_EDGE_TOL = 0.00159999931;  // mjEDGE_TOL (gjk.h:32)
 constexpr int CCD_MAXCON = 50;                  // mjMAXCONPAIR: the witness capacity
-constexpr int CCD_MAXPOLY = 16;                 // clipped polygon capacity (box faces: <= 8)
+constexpr int CCD_MAXFACE = 16;                 // polygon vertices / polygons at a vertex
+constexpr int CCD_MAXPOLY = 2*CCD_MAXFACE;      // clipped polygon capacity
 
 // the box corner a support point is (mjc_boxSupport's vertindex bits, convex.c:319-323)
 MJH_HD int ccdBoxCorner(const CcdShape& s, const double* p) {
@@ -3140,6 +3146,7 @@ struct CcdContacts {
   double* x1;
   double* x2;
   int nx, maxc, bad;
+  const mjhipModel* m;                                  // the mesh polygon data
 };
 
 // polygonClip (:1579-1690): face2 clipped by face1's edge planes (normal n), the vertices the
@@ -3147,7 +3154,11 @@ struct CcdContacts {
 MJH_HD void ccdPolygonClip(CcdContacts& C, const double* face1, int nf1, const double* face2,
                            int nf2, const double n[3], const double dir[3]) {
   if (nf1 < 3) return;
-  double pn[3*4], pd[4];
+  if (nf1 > CCD_MAXFACE || nf2 > CCD_MAXFACE) {
+    C.bad = 1;
+    return;
+  }
+  double pn[3*CCD_MAXFACE], pd[CCD_MAXFACE];
   for (int i = 0; i < nf1; i++) {                       // planeNormal (:1540-1549)
     const double* v1 = face1 + 3*i;
     const double* v2 = face1 + 3*(i < nf1 - 1 ? i + 1 : 0);
@@ -3243,6 +3254,130 @@ MJH_HD void ccdGlobal(double r[3], const double mat[9], const double* pos, doubl
     r[1] += pos[1];
     r[2] += pos[2];
   }
+}
+
+// the mesh vertex a support point is: the vertex whose global position (ccdToGlobal, as
+// ccdMeshSupport forms it) equals p, or -1
+MJH_HD int ccdMeshVertex(const CcdShape& s, const double* p) {
+  for (int i = 0; i < s.nvert; i++) {
+    const double t[3] = {(double)s.vert[3*i], (double)s.vert[3*i+1], (double)s.vert[3*i+2]};
+    double r[3];
+    ccdToGlobal(r, s.mat, t, s.pos);
+    if (r[0] == p[0] && r[1] == p[1] && r[2] == p[2]) return i;
+  }
+  return -1;
+}
+
+// intersect (:1711-1723): up to 2 common entries of two arrays
+MJH_HD int ccdIntersect(int res[2], const int* a, const int* b, int n, int k) {
+  int count = 0;
+  for (int i = 0; i < n; i++) {
+    for (int j = 0; j < k; j++) {
+      if (a[i] == b[j]) {
+        res[count++] = a[i];
+        if (count == 2) return 2;
+      }
+    }
+  }
+  return count;
+}
+
+// meshNormals (:1727-1792): the normals of the mesh polygons through the feature's vertices;
+// -1 when a vertex is on more than CCD_MAXFACE polygons
+MJH_HD int ccdMeshNormals(const mjhipModel& m, double* res, int* ind, int dim,
+                          const CcdShape& s, int v1, int v2, int v3) {
+  const int polyadr = m.mesh_polyadr[s.meshid], vertadr = m.mesh_vertadr[s.meshid];
+  const int* pm = m.mesh_polymap;
+  if (dim == 3) {
+    const int a1 = m.mesh_polymapadr[vertadr + v1], n1 = m.mesh_polymapnum[vertadr + v1];
+    const int a2 = m.mesh_polymapadr[vertadr + v2], n2 = m.mesh_polymapnum[vertadr + v2];
+    const int a3 = m.mesh_polymapadr[vertadr + v3], n3 = m.mesh_polymapnum[vertadr + v3];
+    int edgeset[2], faceset[2];
+    int n = ccdIntersect(edgeset, pm + a1, pm + a2, n1, n2);
+    if (n == 0) return 0;
+    n = ccdIntersect(faceset, edgeset, pm + a3, n, n3);
+    if (n == 0) return 0;
+    const double* nrm = m.mesh_polynormal + 3*(polyadr + faceset[0]);
+    ccdGlobal(res, s.mat, nullptr, nrm[0], nrm[1], nrm[2]);
+    ind[0] = faceset[0];
+    return 1;
+  }
+  if (dim == 2) {
+    const int a1 = m.mesh_polymapadr[vertadr + v1], n1 = m.mesh_polymapnum[vertadr + v1];
+    const int a2 = m.mesh_polymapadr[vertadr + v2], n2 = m.mesh_polymapnum[vertadr + v2];
+    int edgeset[2];
+    const int n = ccdIntersect(edgeset, pm + a1, pm + a2, n1, n2);
+    for (int i = 0; i < n; i++) {
+      const double* nrm = m.mesh_polynormal + 3*(polyadr + edgeset[i]);
+      ccdGlobal(res + 3*i, s.mat, nullptr, nrm[0], nrm[1], nrm[2]);
+      ind[i] = edgeset[i];
+    }
+    return n;
+  }
+  if (dim == 1) {
+    const int a1 = m.mesh_polymapadr[vertadr + v1];
+    int n1 = m.mesh_polymapnum[vertadr + v1];
+    if (n1 > 150) n1 = 150;                             // mjMAX_POLYVERT
+    if (n1 > CCD_MAXFACE) return -1;
+    for (int i = 0; i < n1; i++) {
+      const int index = pm[a1 + i];
+      const double* nrm = m.mesh_polynormal + 3*(polyadr + index);
+      ccdGlobal(res + 3*i, s.mat, nullptr, nrm[0], nrm[1], nrm[2]);
+      ind[i] = index;
+    }
+    return n1;
+  }
+  return 0;
+}
+
+// meshEdgeNormals (:1796-1842): the directions of the mesh edges from the feature's vertex;
+// as in the reference, the edge's other end is read at the polygon-local position k of the
+// previous vertex (verts + 3k), not at that vertex's id
+MJH_HD int ccdMeshEdgeNormals(const mjhipModel& m, double* res, double* ends, int dim,
+                              const CcdShape& s, const double* v1, const double* v2, int v1i) {
+  if (dim == 2) {
+    copy3(ends, v2);
+    sub3(res, v2, v1);
+    normalize3(res);
+    return 1;
+  }
+  if (dim == 1) {
+    const int polyadr = m.mesh_polyadr[s.meshid], vertadr = m.mesh_vertadr[s.meshid];
+    const int a1 = m.mesh_polymapadr[vertadr + v1i];
+    int n1 = m.mesh_polymapnum[vertadr + v1i];
+    if (n1 > 150) n1 = 150;
+    if (n1 > CCD_MAXFACE) return -1;
+    for (int i = 0; i < n1; i++) {
+      const int idx = m.mesh_polymap[a1 + i];
+      const int adr = m.mesh_polyvertadr[polyadr + idx];
+      const int nvert = m.mesh_polyvertnum[polyadr + idx];
+      for (int j = 0; j < nvert; j++) {
+        if (m.mesh_polyvert[adr + j] == v1i) {
+          const float* vert = m.mesh_vert + 3*vertadr + 3*(j == 0 ? nvert - 1 : j - 1);
+          ccdGlobal(ends + 3*i, s.mat, s.pos, vert[0], vert[1], vert[2]);
+          sub3(res + 3*i, ends + 3*i, v1);
+          normalize3(res + 3*i);
+        }
+      }
+    }
+    return n1;
+  }
+  return 0;
+}
+
+// meshFace (:1994-2015): polygon idx's vertices, in reverse order, in the global frame; -1
+// for a polygon over CCD_MAXFACE vertices
+MJH_HD int ccdMeshFace(const mjhipModel& m, double* res, const CcdShape& s, int idx) {
+  const int polyadr = m.mesh_polyadr[s.meshid], vertadr = m.mesh_vertadr[s.meshid];
+  const int adr = m.mesh_polyvertadr[polyadr + idx];
+  int nvert = m.mesh_polyvertnum[polyadr + idx], j = 0;
+  if (nvert > 150) nvert = 150;
+  if (nvert > CCD_MAXFACE) return -1;
+  for (int i = nvert - 1; i >= 0; i--) {
+    const float* vert = m.mesh_vert + 3*vertadr + 3*m.mesh_polyvert[adr + i];
+    ccdGlobal(res + 3*j++, s.mat, s.pos, vert[0], vert[1], vert[2]);
+  }
+  return nvert;
 }
 
 // boxNormals (:1846-1899)
@@ -3345,12 +3480,13 @@ MJH_HD int ccdSimplexDim(int* i1, int* i2, int* i3, const double** v1, const dou
   return 1;
 }
 
-// multicontact (:2071-2193) on the EPA's final face f
+// multicontact (:2071-2193) on the EPA's final face f, box and mesh pairs
 template <int S>
-MJH_HD void ccdMultiContact(CcdContacts& C, const CcdState& st, const CcdMem<S>& M, int f,
-                            const CcdShape& A, const CcdShape& B) {
-  if (A.gtype != mjhipGEOM_BOX || B.gtype != mjhipGEOM_BOX) {
-    C.bad = 1;                                          // meshes: polygon data not compiled
+MJH_HD void ccdMultiContact(const mjhipModel& m, CcdContacts& C, const CcdState& st,
+                            const CcdMem<S>& M, int f, const CcdShape& A, const CcdShape& B) {
+  const bool mesh1 = A.gtype == mjhipGEOM_MESH, mesh2 = B.gtype == mjhipGEOM_MESH;
+  if ((!mesh1 && A.gtype != mjhipGEOM_BOX) || (!mesh2 && B.gtype != mjhipGEOM_BOX)) {
+    C.bad = 1;                                          // not a box or mesh pair
     return;
   }
   SP<S, int> F = M.fint(f);
@@ -3359,18 +3495,32 @@ MJH_HD void ccdMultiContact(CcdContacts& C, const CcdState& st, const CcdMem<S>&
     SP<S> v = M.vtx(F[k]);
     for (int c = 0; c < 9; c++) w[k][c] = v[c];
   }
-  int v11i = ccdBoxCorner(A, w[0] + 3), v12i = ccdBoxCorner(A, w[1] + 3);
-  int v13i = ccdBoxCorner(A, w[2] + 3);
-  int v21i = ccdBoxCorner(B, w[0] + 6), v22i = ccdBoxCorner(B, w[1] + 6);
-  int v23i = ccdBoxCorner(B, w[2] + 6);
+  auto corner = [&](const CcdShape& s, bool mesh, const double* p) MJH_LAMBDA_INLINE {
+    return mesh ? ccdMeshVertex(s, p) : ccdBoxCorner(s, p);
+  };
+  int v11i = corner(A, mesh1, w[0] + 3), v12i = corner(A, mesh1, w[1] + 3);
+  int v13i = corner(A, mesh1, w[2] + 3);
+  int v21i = corner(B, mesh2, w[0] + 6), v22i = corner(B, mesh2, w[1] + 6);
+  int v23i = corner(B, mesh2, w[2] + 6);
+  if (v11i < 0 || v12i < 0 || v13i < 0 || v21i < 0 || v22i < 0 || v23i < 0) {
+    C.bad = 1;                                          // a support point off the mesh's
+    return;                                             // vertices (an inflated margin)
+  }
   const double *v11 = w[0] + 3, *v12 = w[1] + 3, *v13 = w[2] + 3;
   const double *v21 = w[0] + 6, *v22 = w[1] + 6, *v23 = w[2] + 6;
   int nf1 = ccdSimplexDim(&v11i, &v12i, &v13i, &v11, &v12, &v13);
   int nf2 = ccdSimplexDim(&v21i, &v22i, &v23i, &v21, &v22, &v23);
-  double n1[9], n2[9], ends[9], face1[12], face2[12];
-  int idx1[3] = {0, 0, 0}, idx2[3] = {0, 0, 0};
-  int nn1 = ccdBoxNormals(n1, idx1, nf1, A, v11i, v12i, v13i);
-  int nn2 = ccdBoxNormals(n2, idx2, nf2, B, v21i, v22i, v23i);
+  double n1[3*CCD_MAXFACE], n2[3*CCD_MAXFACE], ends[3*CCD_MAXFACE];
+  double face1[3*CCD_MAXFACE], face2[3*CCD_MAXFACE];
+  int idx1[CCD_MAXFACE], idx2[CCD_MAXFACE];
+  int nn1 = mesh1 ? ccdMeshNormals(m, n1, idx1, nf1, A, v11i, v12i, v13i)
+                  : ccdBoxNormals(n1, idx1, nf1, A, v11i, v12i, v13i);
+  int nn2 = mesh2 ? ccdMeshNormals(m, n2, idx2, nf2, B, v21i, v22i, v23i)
+                  : ccdBoxNormals(n2, idx2, nf2, B, v21i, v22i, v23i);
+  if (nn1 < 0 || nn2 < 0) {
+    C.bad = 1;
+    return;
+  }
   int i = 0, j = 0;
   bool found = false, edge1 = false, edge2 = false;
   for (int a = 0; a < nn1 && !found; a++) {             // alignedFaces (:2019-2031)
@@ -3397,11 +3547,21 @@ MJH_HD void ccdMultiContact(CcdContacts& C, const CcdState& st, const CcdMem<S>&
   };
   if (!found) {
     if (nf1 < 3 && nf1 <= nf2) {
-      nn1 = ccdBoxEdgeNormals(n1, ends, nf1, A, v11, v12, v11i);
+      nn1 = mesh1 ? ccdMeshEdgeNormals(m, n1, ends, nf1, A, v11, v12, v11i)
+                  : ccdBoxEdgeNormals(n1, ends, nf1, A, v11, v12, v11i);
+      if (nn1 < 0) {
+        C.bad = 1;
+        return;
+      }
       if (!faceEdge(n1, nn1, n2, nn2)) return;
       edge1 = true;
     } else if (nf2 < 3) {
-      nn2 = ccdBoxEdgeNormals(n2, ends, nf2, B, v21, v22, v21i);
+      nn2 = mesh2 ? ccdMeshEdgeNormals(m, n2, ends, nf2, B, v21, v22, v21i)
+                  : ccdBoxEdgeNormals(n2, ends, nf2, B, v21, v22, v21i);
+      if (nn2 < 0) {
+        C.bad = 1;
+        return;
+      }
       if (!faceEdge(n2, nn2, n1, nn1)) return;
       edge2 = true;
     } else {
@@ -3413,14 +3573,19 @@ MJH_HD void ccdMultiContact(CcdContacts& C, const CcdState& st, const CcdMem<S>&
     copy3(face1 + 3, ends + 3*i);
     nf1 = 2;
   } else {
-    nf1 = ccdBoxFace(face1, A, edge2 ? idx1[j] : idx1[i]);
+    const int ind = edge2 ? idx1[j] : idx1[i];
+    nf1 = mesh1 ? ccdMeshFace(m, face1, A, ind) : ccdBoxFace(face1, A, ind);
   }
   if (edge2) {
     copy3(face2, w[0] + 6);
     copy3(face2 + 3, ends + 3*i);
     nf2 = 2;
   } else {
-    nf2 = ccdBoxFace(face2, B, idx2[j]);
+    nf2 = mesh2 ? ccdMeshFace(m, face2, B, idx2[j]) : ccdBoxFace(face2, B, idx2[j]);
+  }
+  if (nf1 < 0 || nf2 < 0) {
+    C.bad = 1;
+    return;
   }
   double diff[3], dir[3];
   sub3(diff, st.x2, st.x1);
@@ -3505,7 +3670,7 @@ MJH_HD double ccdRun(CcdState& st, const CcdMem<S>& M, CcdShape& A, CcdShape& B,
                                        ccdFromTetra(M, P, st, A, B);
     if (!ret) {
       const int f = ccdEpa(st, M, P, A, B);
-      if (MULTI && maxc > 1 && f >= 0) ccdMultiContact(*multi, st, M, f, A, B);
+      if (MULTI && maxc > 1 && f >= 0) ccdMultiContact(*multi->m, *multi, st, M, f, A, B);
     }
   }
   return st.dist;
@@ -3517,8 +3682,10 @@ MJH_HD void ccdMeshData(CcdShape& s, const mjhipModel& m, int g) {
   s.graph = nullptr;
   s.nvert = 0;
   s.vertindex = s.meshindex = -1;
+  s.meshid = -1;
   if (s.gtype == mjhipGEOM_MESH) {
     const int id = m.geom_dataid[g];
+    s.meshid = id;
     s.vert = m.mesh_vert + 3*m.mesh_vertadr[id];
     s.nvert = m.mesh_vertnum[id];
     s.graph = m.mesh_graphadr[id] >= 0 ? m.mesh_graph + m.mesh_graphadr[id] : nullptr;
@@ -3568,7 +3735,7 @@ MJH_HD int ccdGeneral(const mjhipModel& m, int g1, int g2, const double* pos1,
   }
   CcdState st;
   st.nx = 0;
-  CcdContacts C{out + 2, out + 2 + 3*CCD_MAXCON, 0, maxc, 0};
+  CcdContacts C{out + 2, out + 2 + 3*CCD_MAXCON, 0, maxc, 0, &m};
   const double dist = ccdRun<1, MULTI>(st, M, sh[0], sh[1], N, tol, cutoff, maxc, &C);
   out[0] = dist;
   if (MULTI && C.nx) {
@@ -3633,8 +3800,10 @@ MJH_HD void ccdRotateFrame(const double origin[3], const double rot[9], double x
   sub3(xpos, xpos, vec);
 }
 
-// mjc_Convex with mjENBL_MULTICCD (convex.c:915-1001) for a pair without a sphere, ellipsoid
-// or mesh: the first contact, then the four perturbed ones (:933-999) -- both geoms rotated
+// mjc_Convex with mjENBL_MULTICCD (convex.c:915-1001) for a pair without a sphere or an
+// ellipsoid. A box / mesh pair without margin (singlePass :895-909) asks mjc_ccd for up to 4
+// contacts -- the multicontact polygon (ccdMultiContact), or the one EPA contact -- and stops
+// there. Other pairs: the first contact, then the four perturbed ones (:933-999) -- both geoms rotated
 // about the first contact by -+1e-3 rad around its frame's y and z axes (geom 2 by the
 // inverse), each new contact farther than 1e-3 min(rbound) from all earlier ones kept with
 // the first one's depth -- handed to `store` in order (false: the list is full). The frames
@@ -3648,6 +3817,36 @@ MJH_HD void colConvexMulti(const mjhipModel& m, const Lane<S>& d, int g1, int g2
   CcdShape A, B;
   ccdShape(A, m, d, g1, margin);
   ccdShape(B, m, d, g2, margin);
+  if (margin <= 0 && (A.gtype == mjhipGEOM_BOX || A.gtype == mjhipGEOM_MESH) &&
+      (B.gtype == mjhipGEOM_BOX || B.gtype == mjhipGEOM_MESH)) {
+    double x1[12], x2[12];                              // max_contacts 4: at most 4 contacts
+    CcdContacts C{x1, x2, 0, 4, 0, &m};
+    CcdState st;
+    const double dist = ccdRun<1, true>(st, M, A, B, m.opt.ccd_iterations,
+                                        m.opt.ccd_tolerance, 0.0, 4, &C);
+    if (st.unsupported || C.bad) {
+      *status |= MJHIP_INST_UNSUPPORTED;
+      return;
+    }
+    if (!(dist < 0)) return;
+    const int n = C.nx ? C.nx : st.nx;
+    for (int i = 0; i < n; i++) {
+      const double* a = C.nx ? x1 + 3*i : st.x1;
+      const double* b = C.nx ? x2 + 3*i : st.x2;
+      RawContact c;
+      c.dist = margin + dist;
+      c.frame[0] = a[0] - b[0];
+      c.frame[1] = a[1] - b[1];
+      c.frame[2] = a[2] - b[2];
+      normalize3(c.frame);
+      c.pos[0] = 0.5*(a[0] + b[0]);
+      c.pos[1] = 0.5*(a[1] + b[1]);
+      c.pos[2] = 0.5*(a[2] + b[2]);
+      for (int k = 3; k < 9; k++) c.frame[k] = 0;
+      if (!store(c)) return;
+    }
+    return;
+  }
   RawContact c0;
   if (!ccdIteration(c0, m, M, A, B, margin, status)) return;
   if (!store(c0)) return;
@@ -3697,12 +3896,11 @@ MJH_HD void colConvexMulti(const mjhipModel& m, const Lane<S>& d, int g1, int g2
   }
 }
 
-// the pair runs MULTICCD's perturbation pass (colConvexMulti): a convex pair without a
-// sphere or an ellipsoid with the flag on (meshes are refused by mjhip_pairMaxContacts)
+// the pair runs MULTICCD (colConvexMulti): a convex pair without a sphere or an ellipsoid
+// with the flag on
 MJH_HD bool multiCcdPair(const mjhipModel& m, int t1, int t2) {
   return (m.opt.enableflags & mjhipENBL_MULTICCD) && mjhip_isConvexPair(t1, t2) &&
-         t1 != mjhipGEOM_SPHERE && t1 != mjhipGEOM_ELLIPSOID && t2 != mjhipGEOM_ELLIPSOID &&
-         t2 != mjhipGEOM_MESH;
+         t1 != mjhipGEOM_SPHERE && t1 != mjhipGEOM_ELLIPSOID && t2 != mjhipGEOM_ELLIPSOID;
 }
 
 // mjc_PlaneConvex (convex.c:1045-1080) for an ellipsoid: the libccd support (mjccd_support
@@ -4421,12 +4619,7 @@ template <int S, bool WRITE, bool BOX, bool CONVEX>
 MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, int g2,
                                double margin, const ContactParam& cp, int& ncon, int* status,
                                double* bbuf) {
-  if (m.geom_type[g1] == mjhipGEOM_BOX) {
-    if constexpr (BOX) collideBoxBox<S, WRITE>(m, d, g1, g2, margin, cp, ncon, status, bbuf);
-    else *status |= MJHIP_INST_UNSUPPORTED;   // not reached: the launch saw no box pair
-    return;
-  }
-  if (multiCcdPair(m, m.geom_type[g1], m.geom_type[g2])) {
+  if (multiCcdPair(m, m.geom_type[g1], m.geom_type[g2])) {     // before box-box: box-mesh
     if constexpr (CONVEX) {
       colConvexMulti(m, d, g1, g2, margin, status,
                      [&](const RawContact& rk) MJH_LAMBDA_INLINE -> bool {
@@ -4435,6 +4628,11 @@ MJH_HD void collidePlaneBoxCyl(const mjhipModel& m, const Lane<S>& d, int g1, in
     } else {
       *status |= MJHIP_INST_UNSUPPORTED;      // not reached: such models use one lane each
     }
+    return;
+  }
+  if (m.geom_type[g1] == mjhipGEOM_BOX) {
+    if constexpr (BOX) collideBoxBox<S, WRITE>(m, d, g1, g2, margin, cp, ncon, status, bbuf);
+    else *status |= MJHIP_INST_UNSUPPORTED;   // not reached: the launch saw no box pair
     return;
   }
   if (m.geom_type[g1] == mjhipGEOM_HFIELD || m.geom_type[g2] == mjhipGEOM_MESH) {
@@ -9321,6 +9519,10 @@ struct Mirror {
   const CoopPair* prog;                      // the static collision program (Lane::prog)
   const int* prog_ipair;
   int nprog;
+  // mjd_inverseFD's perturbed instances (codegen.FD_KEEP): non-null, instance blocks from
+  // full_blk on send the stores no later kernel reads to this region instead of their slots
+  double* sink;
+  int full_blk;
 };
 
 MJH_HD mjh::Lane<64> lane_view(const Mirror& mr, int blk, int lane) {

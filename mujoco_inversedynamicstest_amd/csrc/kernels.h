@@ -136,6 +136,13 @@ __global__ __launch_bounds__(64) void k_inverse(mjhipModel m, Mirror mr, int B,
                                                 double* __restrict__ qfrc_out,
                                                 int* __restrict__ status, int skipsensor);
 
+// mjhip_ccdBatch's kernel (kern_ccd.hip): kCcdOut doubles per pair out (dist, nx, x1[3*50],
+// x2[3*50]); nonzero when the launch failed
+constexpr long kCcdOut = 2 + 6*mjh::CCD_MAXCON;
+int mjhip_launchCcd(hipStream_t s, const mjhipModel& m, int n, const int* g1, const int* g2,
+                    const double* in, const double* margin, int N, double tol, int maxc,
+                    double cutoff, double* x, int* xi, double* out, int* bad);
+
 // the instantiations libmjhip.so launches (launch_inverse)
 #ifndef MJHIP_KERNEL_UNIT
 extern template __global__ void k_constraint<true, true, false>(mjhipModel, Mirror, int, const int*, const int*, double*, int*);

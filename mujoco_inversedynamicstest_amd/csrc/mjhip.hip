@@ -144,28 +144,57 @@ __global__ void k_from_mirror(const double* __restrict__ src, double* __restrict
 // p (0 = centre, 1..nv = qacc_i + eps, nv+1..2nv = qvel_i + eps, 2nv+1..3nv = qpos
 // integrated along e_i by eps). Instances are base-major: inst = b*(3nv+1) + p.
 // Layout 1 (stage skipping, mj_inverseSkip(mjSTAGE_POS) for the qvel/qacc perturbations):
-// the instances that run the position stage first, b*(nv+1) + j (j = 0 centre, j = i+1 the
-// qpos perturbation of dof i), then from A = nbase*(nv+1) the others, A + b*2nv + (p-1).
+// the instances that run the position stage first -- the centres b, then the qpos
+// perturbations nbase + b*nv + i (dof i) -- then from A = nbase*(nv+1) the others,
+// A + b*2nv + (p-1). The centres lead so that they fill whole waves: only their mirror slots
+// keep every field (Mirror::sink, codegen.FD_KEEP).
 // Layout 2 (the qacc perturbations run mj_inverseSkip(mjSTAGE_VEL), the qvel ones
 // mjSTAGE_POS, engine_derivative_fd.c:646-699): the same position-stage block, then the qacc
 // perturbations A + b*nv + (p-1), then the qvel ones A + nbase*nv + b*nv + (p-1-nv), so that
 // each skip kernel covers whole waves of one kind.
 __device__ static inline long fd_inst(int layout, long nbase, long b, int p, int nv) {
   if (!layout) return b*(3*nv + 1) + p;
-  if (p == 0) return b*(nv + 1);
-  if (p > 2*nv) return b*(nv + 1) + (p - 2*nv);
+  if (p == 0) return b;
+  if (p > 2*nv) return nbase + b*nv + (p - 2*nv - 1);
   if (layout == 1) return nbase*(nv + 1) + b*2*nv + (p - 1);
   if (p <= nv) return nbase*(nv + 1) + b*nv + (p - 1);
   return nbase*(nv + 1) + nbase*nv + b*nv + (p - 1 - nv);
 }
 
-// instances [first, end) of the layout (first a multiple of 64), one block per 64 instances
-// and input component: qvel[k], qacc[k] (k < nv), joint j's qpos (mj_integratePos on dof i
-// for the qpos perturbations), ctrl[k]. A block's 64 lanes write one 512-byte mirror line per
-// value. gate: the stage-skip fall-back's expansion (mjhip_inverseFDBatch): it runs only when
+// instances [first, end) of the layout (first a multiple of 64), one block per 64 instances,
+// its kExpandWaves waves taking turns over the input components: qvel[k], qacc[k] (k < nv), joint j's
+// qpos (mj_integratePos on dof i for the qpos perturbations), ctrl[k]. The 64 lanes of a wave
+// write one 512-byte mirror line per value. gate: the stage-skip fall-back's expansion (mjhip_inverseFDBatch): it runs only when
 // k_vaskip found a centre with limit rows (fdflag[0]), and its first thread hands the range
 // {first, end} -- or the empty {first, first} -- to the fall-back k_all (fdflag[1..2])
-__global__ __launch_bounds__(64) void k_fd_expand(mjhipModel m, Mirror mr, int nbase,
+// the base state b and perturbation p of instance inst in the layout (the inverse of fd_inst)
+__device__ static inline void fd_bp(int layout, long nbase, long inst, int nv, long* b, int* p) {
+  const int P = 3*nv + 1;
+  if (!layout) {
+    *b = inst / P;
+    *p = (int)(inst % P);
+  } else if (inst < nbase) {
+    *b = inst;
+    *p = 0;
+  } else if (inst < nbase*(nv + 1)) {
+    const long t = inst - nbase;
+    *b = t / nv;
+    *p = 2*nv + 1 + (int)(t % nv);
+  } else if (layout == 1) {
+    const long t = inst - nbase*(nv + 1);
+    *b = t / (2*nv);
+    *p = 1 + (int)(t % (2*nv));
+  } else {
+    long t = inst - nbase*(nv + 1);
+    const bool vel = t >= nbase*nv;
+    if (vel) t -= nbase*nv;
+    *b = t / nv;
+    *p = 1 + (int)(t % nv) + (vel ? nv : 0);
+  }
+}
+
+constexpr int kExpandWaves = 16;   // 4 measured 13 us per 28,672 instances (latency-bound)
+__global__ __launch_bounds__(64*kExpandWaves) void k_fd_expand(mjhipModel m, Mirror mr, int nbase,
                                                   const double* __restrict__ qpos,
                                                   const double* __restrict__ qvel,
                                                   const double* __restrict__ qacc,
@@ -174,45 +203,26 @@ __global__ __launch_bounds__(64) void k_fd_expand(mjhipModel m, Mirror mr, int n
                                                   long first, long end, int gate) {
   const int nv = m.nv, nq = m.nq, P = 3*nv + 1;
   const int ncomp = 2*nv + m.njnt + (ctrl ? m.nu : 0);
-  // the gated launch has one block per 64 instances looping over the components, so that
-  // the usual empty call costs few blocks
-  const int per = gate ? 1 : ncomp;
-  const long blk = first/64 + blockIdx.x / per;
-  const int lane = threadIdx.x;
+  // one block of kExpandWaves waves per 64 instances: wave w writes components w,
+  // w + kExpandWaves, ...
+  const long blk = first/64 + blockIdx.x;
+  const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
   if (gate) {
-    if (blockIdx.x == 0 && lane == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
       fdflag[1] = (int)first;
       fdflag[2] = fdflag[0] ? (int)end : (int)first;
     }
     if (!fdflag[0]) return;
-  } else if (fdflag && blockIdx.x == 0 && lane == 0) {
+  } else if (fdflag && blockIdx.x == 0 && threadIdx.x == 0) {
     fdflag[0] = 0;                       // k_vaskip raises it later in stream order
   }
   const long inst = blk*64 + lane;
   if (inst >= end || inst >= (long)nbase*P) return;
-  for (int comp = gate ? 0 : blockIdx.x % ncomp; comp < (gate ? ncomp : blockIdx.x % ncomp + 1);
-       comp++) {
   long b;
   int p;
-  if (!layout) {
-    b = inst / P;
-    p = (int)(inst % P);
-  } else if (inst < (long)nbase*(nv + 1)) {
-    b = inst / (nv + 1);
-    const int j = (int)(inst % (nv + 1));
-    p = j ? 2*nv + j : 0;
-  } else if (layout == 1) {
-    const long t = inst - (long)nbase*(nv + 1);
-    b = t / (2*nv);
-    p = 1 + (int)(t % (2*nv));
-  } else {
-    long t = inst - (long)nbase*(nv + 1);
-    const bool vel = t >= (long)nbase*nv;
-    if (vel) t -= (long)nbase*nv;
-    b = t / nv;
-    p = 1 + (int)(t % nv) + (vel ? nv : 0);
-  }
+  fd_bp(layout, nbase, inst, nv, &b, &p);
   Lane<64> d = lane_view(mr, (int)(inst >> 6), lane);
+  for (int comp = wave; comp < ncomp; comp += kExpandWaves) {
   if (comp < nv) {                       // qvel_k (+ eps on the qvel perturbation k)
     const double x = qvel[b*nv + comp];
     d.qvel[comp] = p - 1 - nv == comp ? x + eps : x;
@@ -275,7 +285,8 @@ __global__ void k_fd_act(mjhipModel m, Mirror mr, long ninst) {
 
 // DfDq/DfDv/DfDa (engine_derivative_fd.c:48-53) one thread per output element, the row's
 // element k fastest, so a wave's stores are contiguous (the same difference and scaling as
-// k_fd_diff, which keeps the sensor rows and DmDq)
+// k_fd_diff, which keeps the sensor rows and DmDq; an LDS-tiled form, one block per 64
+// instances, measured slower: 17.5 against 15.8 us at 1,024 base states)
 __global__ void k_fd_dfd(mjhipModel m, Mirror mr, int nbase, double eps, int flg_actuation,
                          double* __restrict__ DfDq, double* __restrict__ DfDv,
                          double* __restrict__ DfDa, int layout) {
@@ -378,26 +389,6 @@ __global__ __launch_bounds__(64) void k_assemble(mjhipModel m, Mirror mr, int B,
   if (k == 0 && status && cstat[inst]) status[inst] |= cstat[inst];
 }
 
-// mjhip_ccdBatch: mjc_ccd on pair i's geoms at its frames (in: 24 doubles per pair, pos1,
-// mat1, pos2, mat2; out: kCcdOut per pair, dist, nx, x1[3 mjMAXCONPAIR], x2[...]), scratch
-// contiguous per pair; bad[i]: 1 polytope capacity, 2 multicontact outside the subset
-constexpr long kCcdOut = 2 + 6*mjh::CCD_MAXCON;
-__global__ __launch_bounds__(64) void k_ccd(mjhipModel m, int n, const int* __restrict__ g1,
-                                            const int* __restrict__ g2,
-                                            const double* __restrict__ in,
-                                            const double* __restrict__ margin, int N,
-                                            double tol, int maxc, double cutoff,
-                                            double* __restrict__ x, int* __restrict__ xi,
-                                            double* __restrict__ out, int* __restrict__ bad) {
-  const int i = blockIdx.x*64 + threadIdx.x;
-  if (i >= n) return;
-  const double* f = in + 24L*i;
-  bad[i] = mjh::ccdGeneral<true>(m, g1[i], g2[i], f, f + 3, f + 12, f + 15,
-                                 margin ? margin[i] : 0.0, N, tol, maxc, cutoff,
-                                 x + (long)i*mjh::ccdScratchDoubles(N),
-                                 xi + (long)i*mjh::ccdScratchInts(N), out + kCcdOut*i);
-}
-
 // Constraint-free mj_forward over a batch (mjh::forwardSkip). Optional row-major qpos, qvel,
 // ctrl are copied into the mirror first; qfrc_applied / xfrc_applied are read from the
 // mirror; optional row-major qacc is written at the end.
@@ -479,10 +470,12 @@ struct mjhipContext_ {
   int wl_parity = 0;                       // counter the next fast launch uses
   int wl_last = 0;                         // counter the last fast launch used
   int last_path = -1;                      // mjhip_contextLastPath
+  const char* con_kernel = "none";         // mjhip_contextConstraintKernel
   // mjhip_inverseFDBatch's stage-skip fall-back, decided on the device: [0] a centre has limit
   // rows (k_vaskip), [1..2] the instance range {first, end} the gated k_fd_expand hands to
   // k_all
   int* fdflag = nullptr;
+  double* sink = nullptr;                  // Mirror::sink of mjhip_inverseFDBatch's layouts
   CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
   mjh::ContactParam* cparams = nullptr;    // each program pair's mj_contactParam
   int* prog_ipair = nullptr;               // each program pair's predefined-pair index or -1
@@ -930,6 +923,7 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->status);
   hipFree(c->worklist);
   hipFree(c->fdflag);
+  hipFree(c->sink);
   hipFree(c->pairs);
   hipFree(c->cparams);
   hipFree(c->prog_ipair);
@@ -1038,10 +1032,11 @@ MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g
     HIPCHECK(hipMemcpy(d_g, g1, n*sizeof(int), hipMemcpyHostToDevice));
     HIPCHECK(hipMemcpy(d_g + n, g2, n*sizeof(int), hipMemcpyHostToDevice));
     HIPCHECK(hipMemset(d_bad, 0, n*sizeof(int)));
-    hipLaunchKernelGGL(k_ccd, dim3((n + 63)/64), dim3(64), 0, c->stream, c->dmodel, n, d_g,
-                       d_g + n, d_in, d_margin, max_iterations, tolerance, max_contacts,
-                       dist_cutoff, d_x, d_xi, d_out, d_bad);
-    HIPCHECK(hipGetLastError());
+    if (mjhip_launchCcd(c->stream, c->dmodel, n, d_g, d_g + n, d_in, d_margin, max_iterations,
+                        tolerance, max_contacts, dist_cutoff, d_x, d_xi, d_out, d_bad)) {
+      set_error("mjhip_ccdBatch: kernel launch failed");
+      return MJHIP_ERR_HIP;
+    }
     HIPCHECK(hipStreamSynchronize(c->stream));
     HIPCHECK(hipMemcpy(out.data(), d_out, kCcdOut*n*sizeof(double), hipMemcpyDeviceToHost));
     HIPCHECK(hipMemcpy(bad.data(), d_bad, n*sizeof(int), hipMemcpyDeviceToHost));
@@ -1053,8 +1048,9 @@ MJHIP_API int mjhip_ccdBatch(mjhipContext* c, int n, const int* g1, const int* g
   for (int i = 0; i < n; i++) {
     if (bad[i]) {
       set_error(bad[i] == 1 ? "mjhip_ccdBatch: pair %d outgrew the solver's polytope capacity"
-                            : "mjhip_ccdBatch: pair %d needs multicontact on a mesh (its "
-                              "polygon data is not compiled)", i);
+                            : "mjhip_ccdBatch: pair %d needs multicontact outside the built "
+                              "subset (a shape other than a box or mesh, or a mesh polygon "
+                              "or vertex fan over 16)", i);
       return MJHIP_ERR_MODEL;
     }
     const double* o = &out[kCcdOut*i];
@@ -1074,6 +1070,10 @@ MJHIP_API const char* mjhip_contextFastKernel(const mjhipContext* c) {
 }
 
 MJHIP_API int mjhip_contextLastPath(const mjhipContext* c) { return c ? c->last_path : -1; }
+
+MJHIP_API const char* mjhip_contextConstraintKernel(const mjhipContext* c) {
+  return c ? c->con_kernel : nullptr;
+}
 
 MJHIP_API int mjhip_worklistCount(mjhipContext* c) {
   if (!c) return -1;
@@ -1143,6 +1143,9 @@ static int finish_fast(mjhipContext* c, int B, dim3 grid, dim3 block, int skipse
 // work-list model without its constraint kernel; the next launch_inverse call continues the
 // same work-list and serves both (the bare pipeline only: the FD stage-skip layout)
 constexpr int kFlagDeferRows = 1 << 30;
+// internal mjhip_inverseFDBatchEx flag: no stage-skip layout (every instance base-major, every
+// field stored): the single-instance mjd_inverseFD reads back its last evaluation's fields
+constexpr int kFlagFDFull = 1 << 29;
 
 // range: null, or a device-side instance range {first, end} for the straight-line kernel (B
 // then only sizes the grid: end - first <= B); only the FD fall-back uses it, on models whose
@@ -1235,13 +1238,16 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
     if (fused && c->coop && c->fast->cmode) {   // cooperative lanes per instance
       const bool contact = c->con_cap > 0, list = c->fast->cmode == 1;
 #define MJHIP_LAUNCH_COOP(G, C, L, X)                                                         \
-      hipLaunchKernelGGL((k_constraint_coop<G, C, L, X>), dim3(coopGrid(B, G, L)),            \
-                         dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap, c->boxpair,         \
-                                                      c->npair, c->con_cap),                  \
-                         c->stream,                                                           \
-                         c->dmodel, c->mirror, B, wl,                                         \
-                         (const int*)cnt, c->pairs, c->cparams, c->masks, c->npair, qfrc,    \
-                         status, nullptr)
+      do {                                                                                    \
+        c->con_kernel = "k_constraint_coop<" #G ", " #C ", " #L ", " #X ">";                \
+        hipLaunchKernelGGL((k_constraint_coop<G, C, L, X>), dim3(coopGrid(B, G, L)),          \
+                           dim3(64), coopLdsBytes(c->dmodel, G, c->efc_cap, c->boxpair,       \
+                                                  c->npair, c->con_cap),                      \
+                           c->stream,                                                         \
+                           c->dmodel, c->mirror, B, wl,                                       \
+                           (const int*)cnt, c->pairs, c->cparams, c->masks, c->npair, qfrc,  \
+                           status, nullptr);                                                  \
+      } while (0)
       if (contact && c->boxpair) {       // the box-box path is compiled in only here
         if (list) MJHIP_LAUNCH_COOP(16, true, true, true);
         else MJHIP_LAUNCH_COOP(16, true, false, true);
@@ -1257,10 +1263,13 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
 #undef MJHIP_LAUNCH_COOP
     } else {
 #define MJHIP_LAUNCH_CON(C, F, L)                                                             \
-    hipLaunchKernelGGL((k_constraint<C, F, L>), grid, block,                                  \
-                       ((C && F) ? mjh::gstageBytes(c->dmodel) : 0) +                         \
-                       ((!L && qfrc) ? 64u*sizeof(double)*c->dmodel.nv : 0), c->stream,      \
-                       c->dmodel, c->mirror, B, wl, (const int*)cnt, qfrc, status)
+    do {                                                                                      \
+      c->con_kernel = "k_constraint<" #C ", " #F ", " #L ">";                               \
+      hipLaunchKernelGGL((k_constraint<C, F, L>), grid, block,                                \
+                         ((C && F) ? mjh::gstageBytes(c->dmodel) : 0) +                       \
+                         ((!L && qfrc) ? 64u*sizeof(double)*c->dmodel.nv : 0), c->stream,    \
+                         c->dmodel, c->mirror, B, wl, (const int*)cnt, qfrc, status);         \
+    } while (0)
     if (c->fast->cmode == 2) {          // contacts or friction loss: every instance
       if (c->con_cap > 0) {
         if (fused) MJHIP_LAUNCH_CON(true, true, false); else MJHIP_LAUNCH_CON(true, false, false);
@@ -1882,17 +1891,32 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
                skipsensor && !flg_actuation && !c->spatial && !mjh::hasFluid(c->hmodel) &&
                !mjh::hasDiscrete(c->hmodel) && !mjh_needTrnAfter(&c->hmodel) &&
                !(m.opt.enableflags & mjhipENBL_ENERGY) && nA % 64 == 0 &&
-               !(noskip && noskip[0] == '1');
+               !(noskip && noskip[0] == '1') && !(flags & kFlagFDFull);
   // layout 2 on request (MJHIP_FD_ACCSKIP=1), when the two perturbation blocks are whole waves
   // each: not the default, as it measured no faster (k_fdskip 62-64 us against k_vaskip's
   // 56 us over the same 55,296 instances)
   if (layout && c->fast->launch_fdskip && nQ % 64 == 0 && accskip && accskip[0] == '1') layout = 2;
   int rc = MJHIP_OK;
+  // a skip layout's perturbed instances store only what a later kernel of this call reads
+  // (codegen.FD_KEEP): instance blocks past the centres' write the rest into the sink, which
+  // the launches below see through the mirror; restored on every return path
+  struct SinkGuard {
+    Mirror* mr;
+    ~SinkGuard() { mr->sink = nullptr; mr->full_blk = 0; }
+  } sink_guard{&c->mirror};
+  if (layout) {
+    if (!c->sink) {
+      int maxs = 1;
+      for (const auto& f : c->fields) maxs = f.second.second > maxs ? f.second.second : maxs;
+      FDCHECK(hipMalloc((void**)&c->sink, sizeof(double)*64*(size_t)maxs), "hipMalloc(sink)");
+    }
+    c->mirror.sink = c->sink;
+    c->mirror.full_blk = (B + 63) / 64;
+  }
   // with a skip layout only the position-stage block is expanded: the skip kernels read their
   // centre's inputs and perturb them in registers (the fall-back expands the rest, below)
   const long nexp = layout ? nA : ninst;
-  const int ncomp = 2*nv + m.njnt + ((m.nu && dc) ? m.nu : 0);
-  hipLaunchKernelGGL(k_fd_expand, dim3((unsigned)(((nexp + 63)/64)*ncomp)), dim3(64), 0,
+  hipLaunchKernelGGL(k_fd_expand, dim3((unsigned)((nexp + 63)/64)), dim3(64*kExpandWaves), 0,
                      c->stream, c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr),
                      eps, layout, layout ? c->fdflag : nullptr, (long)0, nexp, 0);
   FDCHECK(hipGetLastError(), "k_fd_expand launch");
@@ -1906,11 +1930,11 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
     if (layout == 2) {
       // the nv qacc perturbations: the acceleration stage over their centre's position and
       // velocity stages; the nv qvel ones: the va stage over their centre's position stage
-      c->fast->launch_fdskip(c->stream, c->mirror, (int)ninst, (int)nA, nv, nv + 1,
+      c->fast->launch_fdskip(c->stream, c->mirror, (int)ninst, (int)nA, nv, 1,
                              c->mirror.efc_count, c->fdflag, eps);
     } else {
       // the 2nv qvel/qacc perturbations: the va stage over their centre's position stage
-      c->fast->launch_vaskip(c->stream, c->mirror, (int)ninst, (int)nA, 2*nv, nv + 1,
+      c->fast->launch_vaskip(c->stream, c->mirror, (int)ninst, (int)nA, 2*nv, 1,
                              c->mirror.efc_count, c->fdflag, eps);
     }
     FDCHECK(hipGetLastError(), "k_vaskip launch");
@@ -1922,8 +1946,8 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
       // empty when no centre has rows, so the call needs no host round trip.
       // the perturbations' own inputs, for the full pipeline over them (only when a centre
       // has rows)
-      hipLaunchKernelGGL(k_fd_expand, dim3((unsigned)((ninst - nA + 63)/64)), dim3(64),
-                         0, c->stream, c->dmodel, c->mirror, B, dq, dv, da,
+      hipLaunchKernelGGL(k_fd_expand, dim3((unsigned)((ninst - nA + 63)/64)),
+                         dim3(64*kExpandWaves), 0, c->stream, c->dmodel, c->mirror, B, dq, dv, da,
                          (m.nu ? dc : nullptr), eps, layout, c->fdflag, nA, ninst, 1);
       FDCHECK(hipGetLastError(), "k_fd_expand (fall-back) launch");
       rc = launch_inverse(c, (int)(ninst - nA), nullptr, nullptr, nullptr, nullptr,
@@ -2508,7 +2532,7 @@ MJHIP_API void mjhip_inverseFD(const mjhipModel* m, mjhipData* d, mjtNum eps,
   }
   if (!rc) rc = mjhip_inverseFDBatchEx(c, 1, d->qpos, d->qvel, d->qacc, d->ctrl, eps,
                                        flg_actuation, DfDq, DfDv, DfDa, DsDq, DsDv, DsDa, DmDq,
-                                       0);
+                                       kFlagFDFull);
   if (!rc) {
     // the reference's last evaluation (engine_derivative_fd.c:646-715): the last qpos
     // perturbation, else the last qvel one, else the last qacc one, else the centre

@@ -56,6 +56,7 @@ SIGNATURES = {
                                                ctypes.c_ulonglong, ctypes.c_int]),
     "mjhip_worklistCount": (ctypes.c_int, [_V]),
     "mjhip_contextLastPath": (ctypes.c_int, [_V]),
+    "mjhip_contextConstraintKernel": (ctypes.c_char_p, [_V]),
     "mjhip_contextStream": (_V, [_V]),
     "mjhip_contextSetStream": (ctypes.c_int, [_V, _V]),
     "mjhip_inverseBatch": (ctypes.c_int, [_V, ctypes.c_int, _V, _V, _V, _V, ctypes.c_int,
@@ -248,6 +249,12 @@ class InverseEngine:
   def fast_kernel(self):
     """Name of the model-specialized kernel in use, or None (generic kernel)."""
     n = lib().mjhip_contextFastKernel(self.ctx)
+    return n.decode() if n else None
+
+  @property
+  def constraint_kernel(self):
+    """The constraint kernel the last straight-line call launched ("none" if none)."""
+    n = lib().mjhip_contextConstraintKernel(self.ctx)
     return n.decode() if n else None
 
   @property

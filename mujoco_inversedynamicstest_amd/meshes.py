@@ -115,6 +115,134 @@ def hull_graph(vert):
   return ([numvert, numface] + edgeadr + gid + edges + [v for f in faces for v in f])
 
 
+def _makenormal(a, b, c):
+  """mjuu_makenormal (user_util.cc:362-380) on float vertices: the unit normal of (a, b, c) in
+  double (a degenerate triangle keeps the reference's (1, 0, 0) / nrm)."""
+  v1 = [float(a[0]), float(a[1]), float(a[2])]
+  v2 = [float(b[0]), float(b[1]), float(b[2])]
+  v3 = [float(c[0]), float(c[1]), float(c[2])]
+  ab = [v2[0]-v1[0], v2[1]-v1[1], v2[2]-v1[2]]
+  ac = [v3[0]-v1[0], v3[1]-v1[1], v3[2]-v1[2]]
+  n = _cross(ab, ac)
+  nrm = math.sqrt(n[0]*n[0] + n[1]*n[1] + n[2]*n[2])
+  if nrm < mjEPS:
+    n = [1.0, 0.0, 0.0]
+  with np.errstate(divide="ignore", invalid="ignore"):
+    return [float(np.float64(n[0]) / nrm), float(np.float64(n[1]) / nrm),
+            float(np.float64(n[2]) / nrm)]
+
+
+class _MeshPolygon:
+  """MeshPolygon (user_mesh.cc:2058-2269): coplanar faces merged into polygonal sides."""
+
+  def __init__(self, v1, v2, v3, i1, i2, i3):
+    self.normal = _makenormal(v1, v2, v3)
+    self.edges = [(i1, i2), (i2, i3), (i3, i1)]
+    self.islands = [0, 0, 0]
+    self.nisland = 1
+
+  def _combine(self, a, b):
+    """CombineIslands (:2124-2141): the larger island renumbered into the smaller."""
+    if b < a:
+      a, b = b, a
+    for k in range(len(self.islands)):
+      if self.islands[k] == b:
+        self.islands[k] = a
+      elif self.islands[k] > b:
+        self.islands[k] -= 1
+    return a, b
+
+  def insert_face(self, v1, v2, v3):
+    """InsertFace (:2145-2215)."""
+    add = [1, 1, 1]
+    island = -1
+    for slot, (a, b) in enumerate(((v2, v1), (v3, v2), (v1, v3))):
+      for i, e in enumerate(self.edges):
+        if e == (a, b):
+          other = self.islands[i]
+          if slot == 0 or island == -1:
+            island = other
+          elif other != island:
+            self.nisland -= 1
+            island, _ = self._combine(island, other)
+          add[slot] = 0
+          del self.edges[i]
+          del self.islands[i]
+          break
+    if island == -1:
+      island = self.nisland
+      self.nisland += 1
+    for slot, e in enumerate(((v1, v2), (v2, v3), (v3, v1))):
+      if add[slot]:
+        self.edges.append(e)
+        self.islands.append(island)
+
+  def paths(self):
+    """Paths (:2218-2269): the vertex cycle of each connected component."""
+    E = self.edges
+    if len(E) == 3:
+      return [[E[0][0], E[1][0], E[2][0]]]
+    out = []
+    for i in range(self.nisland):
+      path = []
+      for j in range(len(E)):
+        if self.islands[j] == i:
+          path = [E[j][0], E[j][1]]
+          break
+      if not path:
+        continue
+      nxt = path[-1]
+      for _ in range(len(E)):
+        finished = False
+        for k in range(1, len(E)):        # the reference starts at edge 1
+          if self.islands[k] == i and E[k][0] == nxt:
+            nxt = E[k][1]
+            if nxt == path[0]:
+              out.append(path)
+              finished = True
+              break
+            path.append(nxt)
+            break
+        if finished:
+          break
+    return out
+
+
+def _polygon_less(n1, n2):
+  """PolygonCmp (user_mesh.cc:2098-2121): the std::set order of the polygons by normal
+  (equivalent within the face tolerance, else descending components)."""
+  if n1[0]*n2[0] + n1[1]*n2[1] + n1[2]*n2[2] > 0.99999872:
+    return False
+  for k in range(3):
+    if abs(n1[k] - n2[k]) > mjMINVAL:
+      return n1[k] > n2[k]
+  return False
+
+
+def make_polygons(vert, faces):
+  """mjCMesh::MakePolygons (user_mesh.cc:2272-2330) on the user (unprocessed) float vertices:
+  faces of the same plane merged into polygons, kept in a std::set ordered by PolygonCmp
+  (restated as a sorted list searched by lower bound), then each polygon's vertex cycles.
+  Returns the list of vertex cycles (local vertex ids)."""
+  v = np.asarray(vert, dtype=np.float32).reshape(-1, 3)
+  polys = []                               # the set, in order
+  for f in np.asarray(faces).reshape(-1, 3):
+    a, b, c = int(f[0]), int(f[1]), int(f[2])
+    face = _MeshPolygon(v[a], v[b], v[c], a, b, c)
+    lo, hi = 0, len(polys)
+    while lo < hi:                         # lower_bound: first element not less than face
+      mid = (lo + hi) // 2
+      if _polygon_less(polys[mid].normal, face.normal):
+        lo = mid + 1
+      else:
+        hi = mid
+    if lo < len(polys) and not _polygon_less(face.normal, polys[lo].normal):
+      polys[lo].insert_face(a, b, c)
+    else:
+      polys.insert(lo, face)
+  return [path for p in polys for path in p.paths() if len(path) >= 3]
+
+
 class Mesh:
   """One compiled <mesh> asset."""
 
@@ -135,6 +263,7 @@ class Mesh:
     self.aamm = [1e10, 1e10, 1e10, -1e10, -1e10, -1e10]
     self.volume = 0.0
     self.boxsz = [0.0, 0.0, 0.0]
+    self.polygons, self.polygon_normals, self.polygon_map = [], [], []
 
   @property
   def nvert(self):
@@ -164,7 +293,22 @@ class Mesh:
       g = self.graph
       nv, nf = g[0], g[1]
       self.face = np.asarray(g[2 + 3*nv + 3*nf:], dtype=np.int64)
+    # MakePolygons (:597) on the graph's faces when there is a graph, before Process
+    if self.graph:
+      nv, nf = self.graph[0], self.graph[1]
+      pfaces = self.graph[2 + 3*nv + 3*nf:]
+    else:
+      pfaces = self.face
+    self.polygons = make_polygons(self.vert, pfaces)
     self._process(density)
+    # MakePolygonNormals (:2044-2053) on the processed vertices: the first three of each cycle
+    v = self.vert.reshape(-1, 3)
+    self.polygon_normals = [_makenormal(v[p[0]], v[p[1]], v[p[2]]) for p in self.polygons]
+    # the polygon map (:2320-2326): per vertex, the polygons through it, in order
+    self.polygon_map = [[] for _ in range(self.nvert)]
+    for i, p in enumerate(self.polygons):
+      for vi in p:
+        self.polygon_map[vi].append(i)
     return self
 
   def _apply_transformations(self):

@@ -1738,6 +1738,9 @@ class MJCFCompiler:
     s.update(nmesh=len(mlist), nmeshvert=sum(x.nvert for x in mlist),
              nmeshface=sum(x.nface for x in mlist),
              nmeshgraph=sum(len(x.graph) if x.graph else 0 for x in mlist),
+             nmeshpoly=sum(len(x.polygons) for x in mlist),
+             nmeshpolyvert=sum(len(p) for x in mlist for p in x.polygons),
+             nmeshpolymap=sum(len(p) for x in mlist for p in x.polygon_map),
              nhfield=len(hlist), nhfielddata=sum(x.nrow*x.ncol for x in hlist))
     mva = arr("mesh_vertadr", len(mlist), np.int32)
     mvn = arr("mesh_vertnum", len(mlist), np.int32)
@@ -1747,6 +1750,32 @@ class MJCFCompiler:
     mvert = arr("mesh_vert", (s["nmeshvert"], 3), np.float32)
     mface = arr("mesh_face", (s["nmeshface"], 3), np.int32)
     mgraph = arr("mesh_graph", s["nmeshgraph"], np.int32)
+    # the polygons (CopyPolygonNormals / CopyPolygons / CopyPolygonMap, user_mesh.cc:715-750,
+    # user_model.cc:2794-2829): global addresses, mesh-local vertex and polygon ids
+    mpn = arr("mesh_polynum", len(mlist), np.int32)
+    mpa = arr("mesh_polyadr", len(mlist), np.int32)
+    pnormal = arr("mesh_polynormal", (s["nmeshpoly"], 3), np.float64)
+    pva = arr("mesh_polyvertadr", s["nmeshpoly"], np.int32)
+    pvn = arr("mesh_polyvertnum", s["nmeshpoly"], np.int32)
+    pvert = arr("mesh_polyvert", s["nmeshpolyvert"], np.int32)
+    pma = arr("mesh_polymapadr", s["nmeshvert"], np.int32)
+    pmn = arr("mesh_polymapnum", s["nmeshvert"], np.int32)
+    pmap = arr("mesh_polymap", s["nmeshpolymap"], np.int32)
+    poly_adr = polyvert_adr = polymap_adr = 0
+    vadr = 0
+    for mi, x in enumerate(mlist):
+      mpa[mi], mpn[mi] = poly_adr, len(x.polygons)
+      for i, (p, n) in enumerate(zip(x.polygons, x.polygon_normals)):
+        pnormal[poly_adr + i] = n
+        pva[poly_adr + i], pvn[poly_adr + i] = polyvert_adr, len(p)
+        pvert[polyvert_adr:polyvert_adr + len(p)] = p
+        polyvert_adr += len(p)
+      for v, lst in enumerate(x.polygon_map):
+        pma[vadr + v], pmn[vadr + v] = polymap_adr, len(lst)
+        pmap[polymap_adr:polymap_adr + len(lst)] = lst
+        polymap_adr += len(lst)
+      poly_adr += len(x.polygons)
+      vadr += x.nvert
     va = fa = ga_ = 0
     for mi, x in enumerate(mlist):
       mva[mi], mvn[mi], mfa[mi], mfn[mi] = va, x.nvert, fa, x.nface

@@ -2892,6 +2892,9 @@ typedef struct {
   int nvert;
   const int* graph;
   int vertindex, meshindex;
+  /* mesh geoms: the model and the mesh (the polygon data multicontact reads) */
+  const mjhipModel* model;
+  int meshid;
   /* height-field prism (mjCCDObj.prism) and its centre (mjc_prism_center) */
   mjtNum prism[6][3];
   mjtNum pcenter[3];
@@ -3279,7 +3282,7 @@ typedef struct {
   mjtNum dist, x1[3*OR_MAXCONPAIR], x2[3*OR_MAXCONPAIR];
   int nx, iters, nsimplex;
   int kmax, maxc;
-  int unsupported;          /* multicontact on a mesh (its polygon data is not compiled) */
+  int unsupported;          /* a multicontact feature the restatement does not cover (none) */
   mjtNum tol, cutoff;
   orVtx simplex[4];
 } orCCD;
@@ -3798,9 +3801,8 @@ static void ccd_center(mjtNum c[3], const orShape* s) {
  * With max_contacts > 1 the EPA's final face is turned into a contact polygon: the feature
  * (vertex, edge or face) of each geom the face's three vertices span, the geoms' face normals
  * around it, a pair of anti-aligned faces (or an edge perpendicular to a face), and the
- * clipping of one face polygon by the other. Boxes are restated; a mesh needs the compiler's
- * polygon data (mesh_polynormal, mesh_polymap, ...), which this compiler does not build, so
- * a mesh sets st->unsupported and keeps the single contact. */
+ * clipping of one face polygon by the other, for boxes and meshes (the mesh polygons of
+ * mjCMesh::MakePolygons, meshes.py make_polygons). */
 #define OR_FACE_TOL 0.99999872      /* mjFACE_TOL (gjk.h:29) */
 #define OR_EDGE_TOL 0.00159999931   /* mjEDGE_TOL (gjk.h:32) */
 #define OR_MAX_POLYVERT 150         /* mjMAX_POLYVERT (gjk.h:35) */
@@ -3986,6 +3988,118 @@ static void mc_global(mjtNum res[3], const mjtNum* mat, const mjtNum* pos, mjtNu
   }
 }
 
+/* intersect (:1711-1723): up to 2 common entries of two arrays */
+static int mc_intersect(int res[2], const int* a, const int* b, int n, int m) {
+  int count = 0;
+  for (int i = 0; i < n; i++) {
+    for (int j = 0; j < m; j++) {
+      if (a[i] == b[j]) {
+        res[count++] = a[i];
+        if (count == 2) return 2;
+      }
+    }
+  }
+  return count;
+}
+
+/* meshNormals (:1727-1792): the normals of the mesh polygons through the feature's vertices */
+static int mc_meshNormals(mjtNum* res, int* resind, int dim, const orShape* s, int v1, int v2,
+                          int v3) {
+  const mjhipModel* m = s->model;
+  const int polyadr = m->mesh_polyadr[s->meshid], vertadr = m->mesh_vertadr[s->meshid];
+  const mjtNum* mat = s->mat;
+  if (dim == 3) {
+    const int a1 = m->mesh_polymapadr[vertadr + v1], n1 = m->mesh_polymapnum[vertadr + v1];
+    const int a2 = m->mesh_polymapadr[vertadr + v2], n2 = m->mesh_polymapnum[vertadr + v2];
+    const int a3 = m->mesh_polymapadr[vertadr + v3], n3 = m->mesh_polymapnum[vertadr + v3];
+    int edgeset[2], faceset[2];
+    int n = mc_intersect(edgeset, m->mesh_polymap + a1, m->mesh_polymap + a2, n1, n2);
+    if (n == 0) return 0;
+    n = mc_intersect(faceset, edgeset, m->mesh_polymap + a3, n, n3);
+    if (n == 0) return 0;
+    const mjtNum* nrm = m->mesh_polynormal + 3*(polyadr + faceset[0]);
+    mc_global(res, mat, NULL, nrm[0], nrm[1], nrm[2]);
+    resind[0] = faceset[0];
+    return 1;
+  }
+  if (dim == 2) {
+    const int a1 = m->mesh_polymapadr[vertadr + v1], n1 = m->mesh_polymapnum[vertadr + v1];
+    const int a2 = m->mesh_polymapadr[vertadr + v2], n2 = m->mesh_polymapnum[vertadr + v2];
+    int edgeset[2];
+    const int n = mc_intersect(edgeset, m->mesh_polymap + a1, m->mesh_polymap + a2, n1, n2);
+    for (int i = 0; i < n; i++) {
+      const mjtNum* nrm = m->mesh_polynormal + 3*(polyadr + edgeset[i]);
+      mc_global(res + 3*i, mat, NULL, nrm[0], nrm[1], nrm[2]);
+      resind[i] = edgeset[i];
+    }
+    return n;
+  }
+  if (dim == 1) {
+    const int a1 = m->mesh_polymapadr[vertadr + v1];
+    int n1 = m->mesh_polymapnum[vertadr + v1];
+    if (n1 > OR_MAX_POLYVERT) n1 = OR_MAX_POLYVERT;
+    for (int i = 0; i < n1; i++) {
+      const int index = m->mesh_polymap[a1 + i];
+      const mjtNum* nrm = m->mesh_polynormal + 3*(polyadr + index);
+      mc_global(res + 3*i, mat, NULL, nrm[0], nrm[1], nrm[2]);
+      resind[i] = index;
+    }
+    return n1;
+  }
+  return 0;
+}
+
+/* meshEdgeNormals (:1796-1842): the directions of the mesh edges from the feature's vertex.
+   As in the reference, the edge's other end is read at the polygon-local position k of the
+   previous vertex (verts + 3k), not at that vertex's id. */
+static int mc_meshEdgeNormals(mjtNum* res, mjtNum* endverts, int dim, const orShape* s,
+                              const mjtNum v1[3], const mjtNum v2[3], int v1i) {
+  if (dim == 2) {
+    mju_copy3(endverts, v2);
+    mju_sub3(res, v2, v1);
+    mju_normalize3(res);
+    return 1;
+  }
+  if (dim == 1) {
+    const mjhipModel* m = s->model;
+    const int polyadr = m->mesh_polyadr[s->meshid], vertadr = m->mesh_vertadr[s->meshid];
+    const int a1 = m->mesh_polymapadr[vertadr + v1i];
+    int n1 = m->mesh_polymapnum[vertadr + v1i];
+    if (n1 > OR_MAX_POLYVERT) n1 = OR_MAX_POLYVERT;
+    for (int i = 0; i < n1; i++) {
+      const int idx = m->mesh_polymap[a1 + i];
+      const int adr = m->mesh_polyvertadr[polyadr + idx];
+      const int nvert = m->mesh_polyvertnum[polyadr + idx];
+      for (int j = 0; j < nvert; j++) {
+        if (m->mesh_polyvert[adr + j] == v1i) {
+          const float* verts = m->mesh_vert + 3*vertadr;
+          const int k = j == 0 ? nvert - 1 : j - 1;
+          const float* vert = verts + 3*k;
+          mc_global(endverts + 3*i, s->mat, s->pos, vert[0], vert[1], vert[2]);
+          mju_sub3(res + 3*i, endverts + 3*i, v1);
+          mju_normalize3(res + 3*i);
+        }
+      }
+    }
+    return n1;
+  }
+  return 0;
+}
+
+/* meshFace (:1994-2015): polygon idx's vertices, in reverse order, in the global frame */
+static int mc_meshFace(mjtNum* res, const orShape* s, int idx) {
+  const mjhipModel* m = s->model;
+  const int polyadr = m->mesh_polyadr[s->meshid], vertadr = m->mesh_vertadr[s->meshid];
+  const int adr = m->mesh_polyvertadr[polyadr + idx];
+  int nvert = m->mesh_polyvertnum[polyadr + idx], j = 0;
+  if (nvert > OR_MAX_POLYVERT) nvert = OR_MAX_POLYVERT;
+  for (int i = nvert - 1; i >= 0; i--) {
+    const float* vert = m->mesh_vert + 3*vertadr + 3*m->mesh_polyvert[adr + i];
+    mc_global(res + 3*j++, s->mat, s->pos, vert[0], vert[1], vert[2]);
+  }
+  return nvert;
+}
+
 /* boxNormals (:1846-1899) */
 static int mc_boxNormals(mjtNum res[9], int resind[3], int dim, const orShape* s, int v1, int v2,
                          int v3) {
@@ -4123,13 +4237,9 @@ static int mc_simplexDim(int* v1i, int* v2i, int* v3i, const mjtNum** v1, const 
   return 1;
 }
 
-/* multicontact (:2071-2193) for box pairs */
+/* multicontact (:2071-2193) */
 static void ccd_multicontact(orCCD* st, const orPoly* P, int f, const orShape* A,
                              const orShape* B) {
-  if (A->gtype == mjhipGEOM_MESH || B->gtype == mjhipGEOM_MESH) {
-    st->unsupported = 1;                  /* the mesh's polygon data is not compiled */
-    return;
-  }
   const orFace* F = P->face + f;
   const orVtx *p0 = P->vtx + F->vi[0], *p1 = P->vtx + F->vi[1], *p2 = P->vtx + F->vi[2];
   int v11i = p0->i1, v12i = p1->i1, v13i = p2->i1;
@@ -4138,16 +4248,25 @@ static void ccd_multicontact(orCCD* st, const orPoly* P, int f, const orShape* A
   const mjtNum *v21 = p0->p2, *v22 = p1->p2, *v23 = p2->p2;
   int nface1 = mc_simplexDim(&v11i, &v12i, &v13i, &v11, &v12, &v13);
   int nface2 = mc_simplexDim(&v21i, &v22i, &v23i, &v21, &v22, &v23);
-  int nn1 = 0, nn2 = 0, idx1[3] = {0, 0, 0}, idx2[3] = {0, 0, 0};
-  mjtNum n1[9], n2[9], endverts[9], face1[12], face2[12];
+  int nn1 = 0, nn2 = 0, idx1[OR_MAX_POLYVERT], idx2[OR_MAX_POLYVERT];
+  mjtNum n1[3*OR_MAX_POLYVERT], n2[3*OR_MAX_POLYVERT], endverts[3*OR_MAX_POLYVERT];
+  mjtNum face1[3*OR_MAX_POLYVERT], face2[3*OR_MAX_POLYVERT];
   if (A->gtype == mjhipGEOM_BOX) nn1 = mc_boxNormals(n1, idx1, nface1, A, v11i, v12i, v13i);
+  else if (A->gtype == mjhipGEOM_MESH) {
+    nn1 = mc_meshNormals(n1, idx1, nface1, A, v11i, v12i, v13i);
+  }
   if (B->gtype == mjhipGEOM_BOX) nn2 = mc_boxNormals(n2, idx2, nface2, B, v21i, v22i, v23i);
+  else if (B->gtype == mjhipGEOM_MESH) {
+    nn2 = mc_meshNormals(n2, idx2, nface2, B, v21i, v22i, v23i);
+  }
   int res[2], edgecon1 = 0, edgecon2 = 0;
   if (!mc_alignedFaces(res, n1, nn1, n2, nn2)) {
     if (nface1 < 3 && nface1 <= nface2) {
       nn1 = 0;
       if (A->gtype == mjhipGEOM_BOX) {
         nn1 = mc_boxEdgeNormals(n1, endverts, nface1, A, v11, v12, v11i);
+      } else if (A->gtype == mjhipGEOM_MESH) {
+        nn1 = mc_meshEdgeNormals(n1, endverts, nface1, A, v11, v12, v11i);
       }
       if (!mc_alignedFaceEdge(res, n1, nn1, n2, nn2)) return;
       edgecon1 = 1;
@@ -4155,6 +4274,8 @@ static void ccd_multicontact(orCCD* st, const orPoly* P, int f, const orShape* A
       nn2 = 0;
       if (B->gtype == mjhipGEOM_BOX) {
         nn2 = mc_boxEdgeNormals(n2, endverts, nface2, B, v21, v22, v21i);
+      } else if (B->gtype == mjhipGEOM_MESH) {
+        nn2 = mc_meshEdgeNormals(n2, endverts, nface2, B, v21, v22, v21i);
       }
       if (!mc_alignedFaceEdge(res, n2, nn2, n1, nn1)) return;
       edgecon2 = 1;
@@ -4168,14 +4289,16 @@ static void ccd_multicontact(orCCD* st, const orPoly* P, int f, const orShape* A
     mju_copy3(face1 + 3, endverts + 3*i);
     nface1 = 2;
   } else {
-    nface1 = mc_boxFace(face1, A, edgecon2 ? idx1[j] : idx1[i]);
+    const int ind = edgecon2 ? idx1[j] : idx1[i];
+    nface1 = A->gtype == mjhipGEOM_BOX ? mc_boxFace(face1, A, ind) : mc_meshFace(face1, A, ind);
   }
   if (edgecon2) {
     mju_copy3(face2, p0->p2);
     mju_copy3(face2 + 3, endverts + 3*i);
     nface2 = 2;
   } else {
-    nface2 = mc_boxFace(face2, B, idx2[j]);
+    nface2 = B->gtype == mjhipGEOM_BOX ? mc_boxFace(face2, B, idx2[j])
+                                       : mc_meshFace(face2, B, idx2[j]);
   }
   mjtNum diff[3], dir[3];
   mju_sub3(diff, st->x2, st->x1);
@@ -4290,8 +4413,11 @@ static void or_shape(orShape* s, const mjhipModel* m, const mjhipData* d, int g,
   s->graph = NULL;
   s->nvert = 0;
   s->vertindex = s->meshindex = -1;
+  s->model = m;
+  s->meshid = -1;
   if (s->gtype == mjhipGEOM_MESH) {
     const int id = m->geom_dataid[g];
+    s->meshid = id;
     s->vert = m->mesh_vert + 3*m->mesh_vertadr[id];
     s->nvert = m->mesh_vertnum[id];
     s->graph = m->mesh_graphadr[id] >= 0 ? m->mesh_graph + m->mesh_graphadr[id] : NULL;
@@ -4339,9 +4465,10 @@ static void or_rotateFrame(const mjtNum origin[3], const mjtNum rot[9], mjtNum x
 }
 
 /* mjc_Convex (convex.c:915-1001) through mjc_CCDIteration (:792-819), native solver: one
- * contact, then with mjENBL_MULTICCD, for pairs without a sphere or an ellipsoid and outside
- * the box / mesh single pass (meshes are outside this restatement's multiccd subset), the
- * extra contacts of the perturbed frames (:933-999): both geoms rotated about the first
+ * contact; with mjENBL_MULTICCD, a box / mesh pair without margin (singlePass :895-909) asks
+ * mjc_ccd for up to 4 contacts (the multicontact polygon) and stops there; other pairs without
+ * a sphere or an ellipsoid add the extra contacts of the perturbed frames (:933-999): both
+ * geoms rotated about the first
  * contact by -+1e-3 rad around its frame's y and z axes (geom 2 the other way), each new
  * contact farther than 1e-3 min(rbound) from every earlier one kept with the first one's
  * depth. The frames are perturbed on local copies (the reference rotates mjData's in place
@@ -4363,8 +4490,25 @@ static int col_convex(orRaw* c, const mjhipModel* m, const mjhipData* d, int g1,
   mju_copy(r2, xmat2, 9);
   A.pos = p1; A.mat = r1;
   B.pos = p2; B.mat = r2;
-  int ncon = col_ccdIteration(c, m, &A, &B, margin);
   const int t1 = m->geom_type[g1], t2 = m->geom_type[g2];
+  if (mjENABLED(mjhipENBL_MULTICCD) && margin <= 0 &&
+      (t1 == mjhipGEOM_BOX || t1 == mjhipGEOM_MESH) &&
+      (t2 == mjhipGEOM_BOX || t2 == mjhipGEOM_MESH)) {
+    orCCD st;                         /* mjc_CCDIteration with max_contacts 4 (:792-819) */
+    const mjtNum dist = or_ccd(&st, &A, &B, m->opt.ccd_iterations, m->opt.ccd_tolerance, 0, 4);
+    if (!(dist < 0)) return 0;
+    for (int i = 0; i < st.nx; i++) {
+      c[i].dist = margin + dist;
+      mju_sub3(c[i].frame, st.x1 + 3*i, st.x2 + 3*i);
+      mju_normalize3(c[i].frame);
+      c[i].pos[0] = 0.5*(st.x1[3*i] + st.x2[3*i]);
+      c[i].pos[1] = 0.5*(st.x1[3*i + 1] + st.x2[3*i + 1]);
+      c[i].pos[2] = 0.5*(st.x1[3*i + 2] + st.x2[3*i + 2]);
+      mju_zero3(c[i].frame + 3);
+    }
+    return st.nx;
+  }
+  int ncon = col_ccdIteration(c, m, &A, &B, margin);
   if (ncon == 1 && mjENABLED(mjhipENBL_MULTICCD) && t1 != mjhipGEOM_ELLIPSOID &&
       t1 != mjhipGEOM_SPHERE && t2 != mjhipGEOM_ELLIPSOID && t2 != mjhipGEOM_SPHERE) {
     const mjtNum relative_tolerance = 1e-3, perturbation_angle = 1e-3;
@@ -4842,7 +4986,7 @@ int or_ccdPenetration(const mjhipModel* m, const mjhipData* d, int g1, int g2, m
 /* mjc_ccd (engine_collision_gjk.c:2215-2343) as the reference's GJK tests call it
    (engine_collision_gjk_test.cc:62-84 GeomDist, :86-150 Penetration): geoms g1, g2 at the
    data's current frames, object margin `margin` on both, config {kmax, tol, maxc, cutoff}.
-   out: dist, nx, unsupported (multicontact on a mesh), x1[3*50], x2[3*50]. Returns dist. */
+   out: dist, nx, unsupported (always 0), x1[3*50], x2[3*50]. Returns dist. */
 mjtNum or_ccdGeneral(const mjhipModel* m, const mjhipData* d, int g1, int g2, mjtNum margin,
                      mjtNum tol, int kmax, int maxc, mjtNum cutoff, mjtNum* out) {
   orShape A, B;
@@ -4897,12 +5041,11 @@ static int or_collisionFunc(const mjhipModel* m, int t1, int t2) {
   if (k > 0 && or_isConvexPair(t1, t2)) {
     /* mjc_Convex with the libccd MPR fallback: not restated. MULTICCD (pairs without a
        sphere or ellipsoid): up to 5 contacts (the first and four perturbed ones,
-       convex.c:933-999); with a mesh the box/mesh single pass's polygon or the perturbation
-       of mesh supports is not restated */
+       convex.c:933-999; a box / mesh pair without margin: up to 4 from one pass) */
     if (mjDISABLED(mjhipDSBL_NATIVECCD)) return -1;
     if (mjENABLED(mjhipENBL_MULTICCD) && t1 != mjhipGEOM_SPHERE && t1 != mjhipGEOM_ELLIPSOID &&
         t2 != mjhipGEOM_ELLIPSOID) {
-      return t2 == mjhipGEOM_MESH ? -1 : 5;
+      return 5;
     }
   }
   return k;

@@ -319,7 +319,7 @@ class Oracle:
     dist = self.L.or_ccdGeneral(*self._args()[:2], g1, g2, margin, tol, kmax, max_contacts,
                                 cutoff, _p(out))
     if out[2]:
-      raise NotImplementedError("multicontact on a mesh: the mesh polygon data is not compiled")
+      raise NotImplementedError("multicontact: a feature the restatement does not cover")
     nx = int(out[1])
     if max_contacts <= 1:
       return dist, nx, out[3:6].copy(), out[153:156].copy()

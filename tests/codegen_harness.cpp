@@ -18,6 +18,11 @@ static void constraint_part(const mjhipModel* m, Mirror& mr, int inst) {
   mjh::constraintOnly<64, C, F>(*m, d);
 }
 
+// mjd_inverseFD's store elision (Mirror::sink, codegen.FD_KEEP): instance blocks from
+// full_blk on send their elided stores to a sink; -1 (the default) stores everything
+static int g_full_blk = -1;
+extern "C" void cg_set_full_blk(int full_blk) { g_full_blk = full_blk; }
+
 // fields: concatenated per-instance outputs, row-major [field][inst][k] in MJHIP_DATA_FIELDS
 // order. cmode as codegen.constraint_mode (0 none, 1 work-list, 2 all): the constraint
 // kernel's part runs on the served instances, as launch_inverse does on the device. Returns
@@ -30,7 +35,9 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
   const int nv = m->nv, nbody = m->nbody;
   (void)nv; (void)nbody; (void)con_cap;
 #define MJ_M(n) m->n
+  int maxs = 1;
 #define XD(name, d0, d1, stage) mr.name##_n = (m->d0) * (d1); \
+  maxs = mr.name##_n > maxs ? mr.name##_n : maxs; \
   mr.name = (double*)calloc((size_t)nblk * 64 * (mr.name##_n + 1), sizeof(double));
   MJHIP_DATA_FIELDS
   MJHIP_DATA_FORWARD              /* zero inputs the sensor pass reads (xfrc_applied, ...) */
@@ -43,6 +50,10 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
   mr.name = (int*)calloc((size_t)nblk * 64 * ((n) + 1), sizeof(int));
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
+  if (g_full_blk >= 0) {
+    mr.sink = (double*)calloc((size_t)64 * maxs, sizeof(double));
+    mr.full_blk = g_full_blk;
+  }
   mr.efc_cap = efc_cap;
   mr.con_cap = con_cap;
   mr.nj_cap = mjh_njCap(m, efc_cap);
@@ -102,5 +113,6 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
   free(wl);
+  free(mr.sink);
   return served;
 }

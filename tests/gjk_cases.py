@@ -435,3 +435,48 @@ def report_multi(dist, nx, x1, x2):
   d = x1 - x2
   d = d / np.sqrt((d * d).sum(axis=1))[:, None]
   return {"ncon": nx, "dist": dist, "dir": d[0], "pos": 0.5 * (x1 + x2)}
+
+
+# ---- multicontact on meshes (the compiler's mesh polygons, mjCMesh::MakePolygons)
+PENTAPRISM = """<mesh name="pentaprism"
+    vertex="1 0 0 0.309 0.951 0 -0.809 0.588 0 -0.809 -0.588 0 0.309 -0.951 0
+            1 0 1 0.309 0.951 1 -0.809 0.588 1 -0.809 -0.588 1 0.309 -0.951 1"
+    scale=".2 .2 .1"/>"""
+BOX_MESH = ('<mujoco><asset>' + PENTAPRISM + '</asset><worldbody>'
+            '<geom name="geom1" type="box" pos="0 0 -.01" size="3 3 .01"/>'
+            '<geom name="geom2" pos="0 0 0.157" euler="0 -90 0" type="mesh" mesh="pentaprism"/>'
+            '</worldbody></mujoco>')
+BOX_MESH2 = ('<mujoco><asset>' + PENTAPRISM + '</asset><worldbody>'
+             '<geom name="geom1" type="box" pos="0 0 -.01" size="3 3 .01"/>'
+             '<geom name="geom2" pos="0 0 -0.001" type="mesh" mesh="pentaprism"/>'
+             '</worldbody></mujoco>')
+MESH_MESH = ('<mujoco><asset><mesh name="box" vertex="-1 -1 -1 1 -1 -1 1 1 -1 1 1 1 1 -1 1 '
+             '-1 1 -1 -1 1 1 -1 -1 1" scale="1 1 .01"/>' + PENTAPRISM + '</asset><worldbody>'
+             '<geom name="geom1" type="mesh" pos="0 0 -0.01" mesh="box"/>'
+             '<geom name="geom2" pos="0 0 -0.001" type="mesh" mesh="pentaprism"/>'
+             '</worldbody></mujoco>')
+MESH_EDGE = """<mujoco>
+  <option><flag nativeccd="enable" multiccd="enable"/></option>
+  <asset>
+    <mesh name="smallbox" vertex="-1 -1 -1  1 -1 -1   1  1 -1 1  1  1  1 -1  1  -1  1 -1
+                                  -1  1  1 -1 -1  1"/>
+    <mesh name="floor" vertex="-1 -1 -1  1 -1 -1  1  1 -1 1  1  1  1 -1  1 -1  1 -1
+                               -1  1  1 -1 -1  1" scale="5 5 1"/>
+  </asset>
+  <worldbody>
+    <geom type="mesh" name="box1" mesh="floor" pos="0 0 0"/>
+    <body pos="0 0 2"><freejoint/><geom type="mesh" mesh="smallbox" name="box2"/></body>
+    <body pos="0 0 4.4" euler="0 90 40"><freejoint/>
+      <geom type="mesh" mesh="smallbox" name="box3"/></body>
+  </worldbody></mujoco>"""
+
+# the same shape as MULTI_CASES
+MESH_MULTI_CASES = [
+    ("BoxMesh", BOX_MESH, {}, ("geom2", "geom1"), 1000, {"ncon": ("eq", 4)}),     # :1001-1032
+    ("BoxMesh2", BOX_MESH2, {}, ("geom2", "geom1"), 1000, {"ncon": ("eq", 5)}),   # :1034-1065
+    ("BoxMeshPrune", BOX_MESH2, {}, ("geom2", "geom1"), 4, {"ncon": ("eq", 4)}),  # :1067-1098
+    ("MeshMesh", MESH_MESH, {}, ("geom1", "geom2"), 1000, {"ncon": ("eq", 5)}),   # :1100-1133
+    ("MeshMeshPrune", MESH_MESH, {}, ("geom1", "geom2"), 4, {"ncon": ("eq", 4)}),  # :1135-1168
+    ("MeshEdge", MESH_EDGE, {}, ("box2", "box3"), 4, {"ncon": ("eq", 2)}),        # :1353-1399
+    ("LongBoxMulti", LONG_BOX, {}, ("geom1", "geom2"), 1000, {"ncon": ("eq", 4)}),  # :1513-1515
+]

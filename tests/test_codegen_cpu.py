@@ -50,11 +50,17 @@ def build(m, name):
   L.cg_run.restype = ctypes.c_int
   L.cg_run.argtypes = [ctypes.c_void_p, ctypes.c_int] + [ctypes.c_void_p] * 4 + \
       [ctypes.c_int] * 3
+  L.cg_set_full_blk.restype = None
+  L.cg_set_full_blk.argtypes = [ctypes.c_int]
   return L
 
 
-def run_and_compare(m, name, q, v, a):
+def run_and_compare(m, name, q, v, a, full_blk=-1):
+  """full_blk >= 0: Mirror::sink set, instance blocks from full_blk on store only what
+  mjd_inverseFD's later kernels read (codegen.FD_KEEP and every re-read field); those are
+  compared, and the elided fields must stay untouched (zero)."""
   L = build(m, name)
+  L.cg_set_full_blk(full_blk)
   o = Oracle(m)
   cm = host.model_struct(m)
   B = len(q)
@@ -70,12 +76,22 @@ def run_and_compare(m, name, q, v, a):
   for f in fields.DATA_FIELDS:
     res[f.name] = out[off:off + B * sizes[f.name]].reshape(B, sizes[f.name])
     off += B * sizes[f.name]
+  L.cg_set_full_blk(-1)
+  elided = set()
+  if full_blk >= 0:
+    M = codegen._Model(m)
+    elided = codegen.fd_elided(codegen._GEN[st](M, None) for st in codegen.STAGES)
+    assert elided and not elided & codegen.FD_KEEP
   nefc = 0
   for i in range(B):
     o.inverse(q[i], v[i], a[i])
     nefc += o.d.nefc > 0
+    sunk = full_blk >= 0 and i // 64 >= full_blk
     for f in fields.DATA_FIELDS:
       if f.stage > 0:
+        if sunk and f.name in elided:
+          assert not res[f.name][i].any(), f"{name}.{f.name} inst {i} stored"
+          continue
         np.testing.assert_array_equal(res[f.name][i], getattr(o.d, f.name),
                                       err_msg=f"{name}.{f.name} inst {i}")
   if cmode == 1:
@@ -91,6 +107,15 @@ def test_humanoid_generated_bitexact(humanoid):
 def test_humanoid_generated_worklist(humanoid):
   q, v, a = sample_states(humanoid, 64, first=5000, margin=-0.1, resample_tendons=False)
   assert run_and_compare(humanoid, "humanoid", q, v, a) > 10
+
+
+def test_fd_store_elision_bitexact(humanoid):
+  """mjd_inverseFD's perturbed instances (Mirror::sink from block 1 on): the fields a later
+  kernel reads -- FD_KEEP and every field a stage re-loads -- equal the oracle's bit for bit,
+  limit rows (the work-list's generic constraint part) included, and the elided ones are
+  never written to the instance's slot; block 0 (the centres) keeps every field."""
+  q, v, a = sample_states(humanoid, 128, first=5000, margin=-0.1, resample_tendons=False)
+  assert run_and_compare(humanoid, "humanoid", q, v, a, full_blk=1) > 10
 
 
 def test_fluid_model_generated_bitexact():

@@ -187,11 +187,10 @@ def test_slider_crank_no_longer_flagged():
 
 
 def test_outside_the_native_single_contact_path_is_flagged():
-  """mjDSBL_NATIVECCD (libccd's MPR) and mjENBL_MULTICCD on a mesh pair (the box / mesh single
-  pass needs the mesh polygon data) are not built: such a pair adds no capacity and an
+  """mjDSBL_NATIVECCD (libccd's MPR) is not built: such a pair adds no capacity and an
   instance where it passes the filters is flagged; MULTICCD with an ellipsoid is computed
-  (the reference takes the single-contact path for it), and on a pair of cylinders the
-  perturbation pass gives it up to five contacts."""
+  (the reference takes the single-contact path for it), and on a pair of cylinders or a
+  cylinder and a mesh the perturbation pass gives it up to five contacts."""
   base = """<mujoco><option gravity="0 0 0">{flag}</option>
     <asset><mesh name="tet" vertex="0 0 0  .2 0 0  0 .2 0  0 0 .2"/></asset><worldbody>
     <body><freejoint/><geom type="cylinder" size=".2 .1"/></body>
@@ -199,7 +198,7 @@ def test_outside_the_native_single_contact_path_is_flagged():
     </worldbody></mujoco>"""
   for flag, t2, s2, want, cap in (
       ('<flag nativeccd="disable"/>', "cylinder", ".1 .1", 32, 0),
-      ('<flag multiccd="enable"/>', "mesh", "", 32, 0),
+      ('<flag multiccd="enable"/>', "mesh", "", 0, 5),
       ('<flag multiccd="enable"/>', "ellipsoid", ".1 .1 .1", 0, 1),
       ('<flag multiccd="enable"/>', "cylinder", ".1 .1", 0, 5)):
     m = mjcf.load_xml_string(base.format(flag=flag, t2=t2, s2=s2,
@@ -284,3 +283,96 @@ def test_multiccd_device_code_bitexact(t1, t2):
         np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name),
                                       err_msg=f"{f.name} inst {i}")
   assert multi >= 3, multi
+
+
+# testdata/collision_convex/long_box.xml (the reference's LongBox scene, gjk_test.cc:1401-1516)
+LONG_BOX_SCENE = """<mujoco><option>{flag}</option><asset>
+  <mesh name="long_box" vertex="-1 -1 -1 1 -1 -1 1 1 -1 1 1 1 1 -1 1 -1 1 -1 -1 1 1 -1 -1 1"
+        scale=".6 .03 .03"/></asset><worldbody>
+  <geom type="box" size="1 1 .3" pos="0 0 -.3"/>
+  <body pos="0 0 .02" euler="0 0 40"><freejoint/><geom type="mesh" mesh="long_box"/></body>
+  </worldbody></mujoco>"""
+
+# mesh boxes, a pentagonal prism and a box on a box floor (stacked_boxes.xml's kind of scene)
+MESH_PILE = """<mujoco><option gravity="0 0 -9.81"><flag multiccd="enable"/></option>
+  <asset><mesh name="box" vertex="-1 -1 -1 1 -1 -1 1 1 -1 1 1 1 1 -1 1 -1 1 -1 -1 1 1 -1 -1 1"
+               scale=".05 .05 .05"/>
+    <mesh name="prism" vertex="1 0 0 0.309 0.951 0 -0.809 0.588 0 -0.809 -0.588 0
+          0.309 -0.951 0 1 0 1 0.309 0.951 1 -0.809 0.588 1 -0.809 -0.588 1 0.309 -0.951 1"
+          scale=".06 .06 .05"/></asset>
+  <worldbody><geom type="box" size=".5 .5 .1" pos="0 0 -.1" margin="{mg}"/>
+    <body pos="0 0 .05"><freejoint/><geom type="mesh" mesh="box" margin="{mg}"/></body>
+    <body pos=".08 0 .05"><freejoint/><geom type="mesh" mesh="box" margin="{mg}"/></body>
+    <body pos="0 .08 .05"><freejoint/><geom type="mesh" mesh="prism" margin="{mg}"/></body>
+    <body pos=".08 .08 .05"><freejoint/><geom type="box" size=".05 .05 .05" margin="{mg}"/></body>
+  </worldbody></mujoco>"""
+
+
+def _mesh_pile_states(m, rng, n):
+  q = np.tile(m.qpos0, (n, 1))
+  for b in range(4):
+    q[:, 7*b:7*b + 2] += rng.uniform(-0.03, 0.03, (n, 2))
+    q[:, 7*b + 2] = rng.uniform(0.03, 0.07, n)
+    tilt = rng.uniform(0, 1, n) < 0.5            # half the bodies lie flat (face contacts)
+    qq = np.where(tilt[:, None], rng.normal(size=(n, 4)), [1.0, 0, 0, 0])
+    qq[:, 1:] += np.where(tilt[:, None], 0, rng.normal(scale=0.003, size=(n, 3)))
+    q[:, 7*b + 3:7*b + 7] = qq / np.linalg.norm(qq, axis=1, keepdims=True)
+  return q
+
+
+def test_multiccd_mesh_single_pass_known_answer():
+  """mjc_Convex with MULTICCD on a box / mesh pair without margin (singlePass,
+  engine_collision_convex.c:895-930): one mjc_ccd call with max_contacts 4 gives the
+  multicontact polygon. In long_box.xml's rest pose that is LongBox's known answer
+  (gjk_test.cc:1513-1515: 4 contacts), all at the EPA depth; without the flag, 1 contact.
+  The device code on the host equals the oracle bit for bit."""
+  for flag, want in (('<flag multiccd="enable"/>', 4), ('', 1)):
+    m = mjcf.load_xml_string(LONG_BOX_SCENE.format(flag=flag))
+    o, k = Oracle(m), KernelCPU(m)
+    z = np.zeros(m.nv)
+    o.inverse(m.qpos0, z, z)
+    _, st = k.inverse(m.qpos0, z, z)
+    assert o.d.status == st == 0
+    assert o.efc.ncon == want and k.field("con_count")[0] == want
+    width = dict(CON_DOUBLE + CON_INT)
+    for name in CON_FIELDS:
+      ref = o.contact_field(name).reshape(want, width[name])
+      np.testing.assert_array_equal(k.field(name)[:ref.size].reshape(want, width[name]), ref,
+                                    err_msg=name)
+    dist = o.contact_field("con_dist")
+    assert (dist == dist[0]).all() and dist[0] == pytest.approx(-0.01, abs=TOL)
+
+
+@pytest.mark.parametrize("margin", [0, 0.005])
+def test_multiccd_mesh_pile_bitexact(margin):
+  """MULTICCD on box-mesh, mesh-mesh and mesh-prism pairs over random poses: without margin
+  the single pass (multicontact polygons from the compiled mesh polygons), with a margin the
+  perturbation pass on mesh supports. The device pipeline on the host equals the oracle bit
+  for bit on every contact field, row and output, and some pairs give several contacts."""
+  m = mjcf.load_xml_string(MESH_PILE.format(mg=margin))
+  o, k = Oracle(m), KernelCPU(m)
+  rng = np.random.default_rng(31 + int(margin * 1000))
+  q = _mesh_pile_states(m, rng, 40)
+  width = dict(CON_DOUBLE + CON_INT)
+  multi = 0
+  for i in range(len(q)):
+    v, a = rng.normal(size=m.nv), rng.normal(size=m.nv)
+    o.inverse(q[i], v, a)
+    _, st = k.inverse(q[i], v, a)
+    assert st == o.d.status == 0, (i, st, o.d.status)
+    ncon = o.efc.ncon
+    geoms = o.contact_field("con_geom").reshape(ncon, 2)
+    pairs = {}
+    for g in geoms:
+      pairs[tuple(g)] = pairs.get(tuple(g), 0) + 1
+    multi += sum(c > 1 for c in pairs.values())
+    assert k.field("con_count")[0] == ncon
+    for name in CON_FIELDS:
+      ref = o.contact_field(name).reshape(ncon, width[name])
+      np.testing.assert_array_equal(k.field(name)[:ref.size].reshape(ncon, width[name]), ref,
+                                    err_msg=f"{name} inst {i}")
+    for f in fields.DATA_FIELDS:
+      if f.stage > 0:
+        np.testing.assert_array_equal(getattr(k.d, f.name), getattr(o.d, f.name),
+                                      err_msg=f"{f.name} inst {i}")
+  assert multi >= 10, multi

@@ -171,3 +171,29 @@ def test_multiccd_parity():
         f"max contact field error {cerr.max():.2e}, max qfrc_inverse error {err.max():.2e}")
   assert derr.max() == 0 and cerr.max() <= 1e-12
   assert err.max() <= RTOL
+
+
+def test_multiccd_mesh_parity():
+  """MULTICCD on mesh pairs on the device: long_box.xml's rest pose (the single pass's
+  multicontact polygon: LongBox's 4 contacts, gjk_test.cc:1513-1515) and the mesh pile over
+  random poses without margin (single pass) and with one (perturbation pass on mesh
+  supports), contacts bit for bit and qfrc_inverse within the north-star bar."""
+  from test_convex_cpu import LONG_BOX_SCENE, MESH_PILE, _mesh_pile_states
+  m = mjcf.load_xml_string(LONG_BOX_SCENE.format(flag='<flag multiccd="enable"/>'))
+  q = np.tile(m.qpos0, (64, 1))
+  z = np.zeros((64, m.nv))
+  f, ref, ncon, derr, cerr = _run(m, q, z, z)
+  assert (ncon == 4).all(), ncon[:4]
+  assert derr.max() == 0 and cerr.max() == 0
+  assert _err(f, ref).max() <= RTOL
+  for margin in (0, 0.005):
+    m = mjcf.load_xml_string(MESH_PILE.format(mg=margin))
+    rng = np.random.default_rng(41)
+    q = _mesh_pile_states(m, rng, 256)
+    v, a = rng.normal(size=(256, m.nv)), rng.normal(size=(256, m.nv))
+    f, ref, ncon, derr, cerr = _run(m, q, v, a)
+    err = _err(f, ref)
+    print(f"mesh pile margin {margin}: {int(ncon.sum())} contacts, max contact field error "
+          f"{cerr.max():.2e}, max qfrc_inverse error {err.max():.2e}")
+    assert derr.max() == 0 and cerr.max() == 0
+    assert err.max() <= RTOL

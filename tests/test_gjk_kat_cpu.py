@@ -5,9 +5,9 @@ reference's own tests assert, at their tolerances (tests/gjk_cases.py). The two 
 also agree bit for bit with each other: they restate the same operations in the same order.
 
 CylinderBoxMargin (:1571-1600) runs the whole pipeline: one contact, no constraint row.
-Cases that ask for more than one contact (max_contacts > 1: the multi-contact polytope path,
-BoxBoxMultiCCD*, BoxMesh*, MeshMesh*, BoxEdge*, MeshEdge, LongBox's second half) are outside
-this file.
+Cases that ask for more than one contact (max_contacts > 1: the multicontact polygon path,
+BoxBoxMultiCCD*, BoxEdge*, and on meshes through the compiler's polygons BoxMesh*, MeshMesh*,
+MeshEdge, LongBox's second half) run on both builds as well.
 """
 import numpy as np
 import pytest
@@ -56,12 +56,16 @@ def test_cylinder_box_margin():
   assert o.efc.nefc == 0
 
 
-@pytest.mark.parametrize("case", K.MULTI_CASES, ids=[c[0] for c in K.MULTI_CASES])
+ALL_MULTI = K.MULTI_CASES + K.MESH_MULTI_CASES
+
+
+@pytest.mark.parametrize("case", ALL_MULTI, ids=[c[0] for c in ALL_MULTI])
 def test_gjk_multicontact_known_answer(case):
-  """Multicontact (max_contacts > 1; engine_collision_gjk.c:1460-2193) on box pairs: the
-  oracle tracks each polytope vertex's box corners through the supports as the reference does
-  (Vertex.index1/2); the counts, depths, first normals and, where the test lists them, every
-  contact position are the reference's."""
+  """Multicontact (max_contacts > 1; engine_collision_gjk.c:1460-2193) on box and mesh pairs:
+  the oracle tracks each polytope vertex's box corner / mesh vertex through the supports as
+  the reference does (Vertex.index1/2) and reads mesh faces from the compiler's polygons; the
+  counts, depths, first normals and, where the test lists them, every contact position are
+  the reference's."""
   name, xml, overrides, geoms, maxc, expected = case
   m = mjcf.load_xml_string(xml)
   o = Oracle(m)
@@ -73,11 +77,12 @@ def test_gjk_multicontact_known_answer(case):
   K.check(name + " (oracle)", expected, K.report_multi(*ro))
 
 
-@pytest.mark.parametrize("case", K.MULTI_CASES, ids=[c[0] for c in K.MULTI_CASES])
+@pytest.mark.parametrize("case", ALL_MULTI, ids=[c[0] for c in ALL_MULTI])
 def test_gjk_multicontact_host_build(case):
-  """The device's multicontact compiled for the host (mjh::ccdMultiContact, box corners read
-  back from the witness points) against the same known answers, and bit for bit against the
-  oracle (which tracks the corners through the supports, as the reference does)."""
+  """The device's multicontact compiled for the host (mjh::ccdMultiContact, box corners and
+  mesh vertices read back from the witness points) against the same known answers, and bit
+  for bit against the oracle (which tracks them through the supports, as the reference
+  does)."""
   name, xml, overrides, geoms, maxc, expected = case
   m = mjcf.load_xml_string(xml)
   o = Oracle(m)

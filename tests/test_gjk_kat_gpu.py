@@ -43,9 +43,7 @@ def test_gjk_known_answers_device():
 
 
 def test_ccd_batch_arguments():
-  """Bad arguments fail loudly (no launch): geom ids out of range, a negative max_contacts;
-  multicontact on a mesh pair (its polygon data is not compiled) is refused, not
-  approximated."""
+  """Bad arguments fail loudly (no launch): geom ids out of range, a negative max_contacts."""
   m = mjcf.load_xml_string(K.SPHERES)
   e = engine.InverseEngine(m, capacity=64)
   try:
@@ -54,15 +52,6 @@ def test_ccd_batch_arguments():
       e.ccd([0], [5], f[0], f[1], f[0], f[1])
     with pytest.raises(engine.MJHIPError):
       e.ccd([0], [1], f[0], f[1], f[0], f[1], max_contacts=-1)
-  finally:
-    e.close()
-  m = mjcf.load_xml_string(K.LONG_BOX)
-  o = Oracle(m)
-  xpos, xmat = K.frames(m, o, None, {})
-  e = engine.InverseEngine(m, capacity=64)
-  try:
-    with pytest.raises(engine.MJHIPError, match="polygon"):
-      e.ccd([0], [1], xpos[:1], xmat[:1], xpos[1:2], xmat[1:2], max_contacts=1000)
   finally:
     e.close()
 
@@ -86,9 +75,10 @@ def test_cylinder_box_margin_device():
 
 
 def test_gjk_multicontact_known_answers_device():
-  """Multicontact on the device (max_contacts > 1, box pairs; mjhip_ccdBatch): the reference's
-  BoxBoxMultiCCD*, BoxEdge* known answers, and the oracle's contacts bit for bit."""
-  for name, xml, overrides, geoms, maxc, expected in K.MULTI_CASES:
+  """Multicontact on the device (max_contacts > 1, box and mesh pairs; mjhip_ccdBatch): the
+  reference's BoxBoxMultiCCD*, BoxEdge*, BoxMesh*, MeshMesh*, MeshEdge and LongBox known
+  answers, and the oracle's contacts bit for bit."""
+  for name, xml, overrides, geoms, maxc, expected in K.MULTI_CASES + K.MESH_MULTI_CASES:
     m = mjcf.load_xml_string(xml)
     o = Oracle(m)
     xpos, xmat = K.frames(m, o, None, overrides)
