@@ -103,16 +103,27 @@ NT_LOAD_STAGES = ()
 # (profiles/r04/experiments/nt_variants_3.log); below it, and in k_vaskip (whose loads of the
 # centre's fields are shared by 54 perturbations), they stay temporal
 NT_LOAD_SV_STAGES = ("va",)
+# k_fdall: polls of a centre block's flag before a skip wave gives up (each poll sleeps
+# 8 x 64 cycles; 2^22 polls is about a second -- the flag is raised within the launch's
+# first hundred microseconds, as every centre block is dispatched before any waiting one)
+FD_WAIT_ITERS = 1 << 22
 
 
 # mjd_inverseFD's perturbed instances (mjhip_inverseFDBatch with a stage-skip layout, whose
 # centres come first): a mirror field the straight-line stages store but never load is read
 # by no later kernel of that call either -- the finite differences read qfrc_inverse (and qM
-# for DmDq), a work-list model's limit rows the fields below -- so for instance blocks at or
-# past Mirror::full_blk its stores go to the context's sink (Mirror::sink: one small region
-# that every such wave overwrites, so its lines stay in L2) instead of the instance's slot.
-# The stores themselves stay: the arithmetic, and so every result, is the full kernel's bit
-# for bit. Mirror::sink null (every other launch) stores everything.
+# for DmDq), a work-list model's limit rows the fields below -- so in instance blocks at or
+# past Mirror::full_blk (Mirror::sink set) its stores go to the sink, one small region every
+# such wave overwrites, as plain stores, so its lines stay dirty in L2 instead of streaming
+# to memory. Only the FD = true instantiation of the stage bodies does this (k_all's,
+# launched when Mirror::sink is set, k_vaskip's and k_fdall's); it stores the elided fields
+# temporally everywhere and selects each one's base per wave. Every other instantiation is
+# the plain kernel. The arithmetic is untouched, so every result is the full kernel's bit for
+# bit. Measured (28,672 instances of the humanoid, mjd_inverseFD's position stage): 134.6 us
+# storing everything, 126.6 us with streaming stores into the sink, 148 us skipping the
+# stores behind a wave-uniform branch each (which also moved results by an ulp: the
+# branches split the blocks the multiply-adds are formed in); the base selects in every
+# instantiation cost the headline kernel 4%.
 FD_KEEP = frozenset({"qpos", "qvel", "qacc", "qfrc_inverse", "qfrc_passive", "qfrc_constraint",
                      "qfrc_actuator", "ten_length", "ten_J", "ten_velocity", "actuator_length",
                      "actuator_moment", "actuator_velocity", "qM", "sensordata"})
@@ -129,13 +140,33 @@ def fd_elided(bodies) -> set:
   return stores - loads - FD_KEEP
 
 
-def _sink_stores(body: str, elided) -> str:
-  """Point the elided fields' stores of instance blocks past Mirror::full_blk at the sink."""
+def _elide_stores(body: str, elided) -> str:
+  """FD instantiation: the elided fields' stores are temporal, and from Mirror::full_blk on
+  (Mirror::sink set) they land in the sink."""
   import re
   decl = re.compile(r"double\* __restrict__ P_(\w+) = (mr\.\w+ \+ \(\(long\)blk\*\d+\)\*64) \+ lane;")
-  return decl.sub(lambda mt: mt.group(0) if mt.group(1) not in elided else
-                  f"double* __restrict__ P_{mt.group(1)} = (mr.sink && blk >= mr.full_blk ? "
+  body = decl.sub(lambda mt: mt.group(0) if mt.group(1) not in elided else
+                  f"double* __restrict__ P_{mt.group(1)} = (FD && mr.sink && blk >= mr.full_blk ? "
                   f"mr.sink : {mt.group(2)}) + lane;", body)
+  nt = re.compile(r"^(\s*)MJH_NT_STORE\(P_(\w+)\[(.*)$")
+  ntif = re.compile(r"^(\s*)MJH_NT_STORE_IF\((\w+), P_(\w+)\[(.*)$")
+
+  def one(line):
+    mt = nt.match(line)
+    if mt and mt.group(2) in elided:
+      return f"{mt.group(1)}MJH_NT_STORE_IF(!FD, P_{mt.group(2)}[{mt.group(3)}"
+    mt = ntif.match(line)
+    if mt and mt.group(3) in elided:
+      return f"{mt.group(1)}MJH_NT_STORE_IF(!FD && {mt.group(2)}, P_{mt.group(3)}[{mt.group(4)}"
+    return line
+  return "\n".join(one(x) for x in body.split("\n"))
+
+
+def fdall_ok(m) -> bool:
+  """The model gets k_fdall (mjd_inverseFD layout 1 in one launch): it has k_vaskip and the
+  stage bodies index their LDS by a 64-lane block."""
+  return constraint_mode(m) in ("none", "list") and ALL_LANES == 64 and \
+      all(n == 64 for n in LANES.values())
 
 
 def _ll(st):
@@ -1522,7 +1553,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
               for st, b in bodies.items()}
   if M.cmode in ("none", "list") and store_fields is None:
     elided = fd_elided(bodies.values())
-    bodies = {st: _sink_stores(b, elided) for st, b in bodies.items()}
+    bodies = {st: _elide_stores(b, elided) for st, b in bodies.items()}
   out = [f"// GENERATED by mujoco_inversedynamicstest_amd/codegen.py -- do not edit.",
          f"// model '{name}' (nq={m.nq} nv={m.nv} nbody={m.nbody}), hash {model_hash(m)}"]
   exact = exact_fp(m)
@@ -1530,7 +1561,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
     out.append("#if defined(__clang__)\n#pragma clang fp contract(off)\n#endif")
   for st in STAGES:
     params, args = _SIG[st]
-    out.append(f"template <bool SV = true>\n"
+    out.append(f"template <bool SV = true, bool FD = false>\n"
                f"MJH_HD void fast_{st}_{name}(const Mirror& mr, int blk, int lane, int B, "
                f"{params}) {{\n{bodies[st]}\n}}\n")
   out.append(f"""MJH_HD void fast_body_{name}(
@@ -1542,7 +1573,8 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
   double trig[{max(1, 2 * len(M.trig) * 64)}];   // LDS on the device (k_pos)
   double qo_lds[{64 * max(M.nv, 1)}];             // LDS on the device (k_va)
   double qmr[{max(1, m.nM)}];                        // registers on the device (k_all)
-""" + "".join(f"  fast_{st}_{name}(mr, blk, lane, B, {_SIG[st][1]});\n" for st in STAGES)
+""" + "".join(f"  fast_{st}_{name}<true, true>(mr, blk, lane, B, {_SIG[st][1]});\n"
+              for st in STAGES)
              + (f"""  if (qfrc_out && (long)blk*64 + lane < B) {{
     for (int k = 0; k < {M.nv}; k++) qfrc_out[((long)blk*64 + lane)*{M.nv} + k] = qo_lds[lane*{M.nv} + k];
   }}
@@ -1607,8 +1639,9 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
   # instance bound, so an empty range still hands the counters on.
   # SV: the va stage's re-read fields stream too (a batch that oversubscribes L2); a
   # run-time code object (C linkage, no template) has the SV = true kernel only
-  tmpl = "" if extern_c else "template <bool SV>\n"
+  tmpl = "" if extern_c else "template <bool SV, bool FD>\n"
   sv = "true" if extern_c else "SV"
+  fdv = "false" if extern_c else "FD"
   out.append(f"""{tmpl}{linkage}__global__ __launch_bounds__({nl}, {ALL_WAVES}) void k_all_{name}(Mirror mr, int B,
     const double* __restrict__ qpos_in, const double* __restrict__ qvel_in,
     const double* __restrict__ qacc_in, double* __restrict__ qfrc_out, int* __restrict__ status,
@@ -1621,7 +1654,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
   int blk0 = 0;
   if (range) {{ blk0 = range[0] >> 6; B = range[1]; }}
   MJH_PHASE0(19, 27);
-""" + "\n".join(f"  fast_{st}_{name}<{sv}>(mr, {bl}, B, "
+""" + "\n".join(f"  fast_{st}_{name}<{sv}, {fdv}>(mr, {bl}, B, "
                 f"{_SIG[st][1].replace('worklist_next', 'nullptr')});\n"
                 f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE(); MJH_PHASE({20 + k});"
                 for k, st in enumerate(STAGES))
@@ -1730,6 +1763,10 @@ __global__ __launch_bounds__(64, 1) void k_sfv_{name}(Mirror mr, int B,
     skip_body = skip_body.replace("const bool cflag = ec[0] != 0;",
                                   "const bool cflag = ecs[0] != 0;")
     skip_body = skip_body.replace("MJH_NT_STORE_IF(SV, ", "MJH_NT_STORE_IF(true, ")
+    skip_body = skip_body.replace("(FD && mr.sink", "(mr.sink").replace(
+        "MJH_NT_STORE_IF(!FD && SV, ", "MJH_NT_STORE_IF(false, ").replace(
+        "MJH_NT_STORE_IF(!FD, ", "MJH_NT_STORE_IF(false, ")
+    assert "FD" not in re.sub(r"\w*FD\w+|\w+FD\w*", "", skip_body), "k_vaskip: FD left"
     skip_body = skip_body.replace("MJH_NT_LOAD_IF(SV, ", "MJH_NT_LOAD_IF(false, ")
     skip_body = _perturb_loads(skip_body, {"qvel": "pv", "qacc": "pa"})
     out.append(f"MJH_HD void fast_vaskip_{name}(const Mirror& mr, int blk, int lane, int sblk, "
@@ -1758,6 +1795,10 @@ __global__ __launch_bounds__(64, 1) void k_sfv_{name}(Mirror mr, int B,
                f"{_SIG['va'][0]}) {{\n{acc_skip}\n}}\n")
   if M.cmode in ("none", "list"):
     flag = ("  if (ecs[0] != 0) needfull[0] = 1;\n" if M.cmode == "list" else "")
+    pos_call = _SIG["pos"][1].replace("worklist_next", "nullptr")
+    fac_call, va_call = _SIG["fac"][1], _SIG["va"][1]
+    linkage_fd = "" if shared else "static "
+    nv = M.nv
     out.append(f"""// layout 1 over [off, B): per = 2nv perturbations per centre, the first nv of qacc, the
 // next nv of qvel (engine_derivative_fd.c:646-699 order)
 __global__ __launch_bounds__(64, 1) void k_vaskip_{name}(Mirror mr, int B, int off,
@@ -1776,6 +1817,78 @@ __global__ __launch_bounds__(64, 1) void k_vaskip_{name}(Mirror mr, int B, int o
                                 int sstride, int* efc_count, int* needfull, double eps) {{
   hipLaunchKernelGGL(k_vaskip_{name}, dim3((B - off + 63) / 64), dim3(64), 0, s, mr, B, off,
                      per, sstride, efc_count, needfull, eps);
+}}
+// mjd_inverseFD layout 1 in one launch (k_fdall, opt-in: MJHIP_FD_FUSED=1, measured slower
+// than k_all then k_vaskip): the position-stage instances [0, B) -- the
+// centres, then the qpos perturbations -- run the whole pipeline (FD: elided stores) on the
+// first B/64 blocks, and the 2nv qvel/qacc perturbations per base state [B, ninst) run
+// k_vaskip's va stage on the blocks after them, beside the qpos perturbations instead of
+// after them. A skip lane reads its centre's position-stage outputs, so it first waits for
+// the centre block's flag (flags[block] == epoch), which that block raises after its
+// position stage behind a device-scope fence (its stores are visible on every XCD); the
+// waiting side fences again before its loads. Blocks are dispatched in index order, so
+// every centre block is running before any block that waits; the wait is bounded all the
+// same, and a wave that gives up raises needfull[3] (the host reports it).
+template <bool SV>
+__global__ __launch_bounds__(64, 1) void k_fdall_{name}(Mirror mr, int B, int ninst, int per,
+    double eps, int* __restrict__ worklist, int* __restrict__ worklist_count,
+    int* __restrict__ worklist_next, int* __restrict__ efc_count, int* __restrict__ needfull,
+    int* __restrict__ flags, int epoch) {{
+  __shared__ double trig[{ntrig}];
+  __shared__ double qo_lds[{nqo}];
+  if (worklist_next && blockIdx.x == 0 && threadIdx.x == 0) *worklist_next = 0;
+  const int nblk = B / 64;                  // B: a whole number of waves
+  if ((int)blockIdx.x < nblk) {{
+    double qmr[{max(1, m.nM)}];
+    const double* qpos_in = nullptr;
+    const double* qvel_in = nullptr;
+    const double* qacc_in = nullptr;
+    double* qfrc_out = nullptr;
+    int* status = nullptr;
+    const int blk = blockIdx.x, lane = threadIdx.x;
+    fast_pos_{name}<SV, true>(mr, blk, lane, B, {pos_call});
+    asm volatile("" ::: "memory");
+    if (blk < mr.full_blk) {{               // a centre block: its position stage is out
+      __threadfence();
+      if (lane == 0) __hip_atomic_store(flags + blk, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }}
+    MJH_SCHED_FENCE();
+    fast_fac_{name}<SV, true>(mr, blk, lane, B, {fac_call});
+    asm volatile("" ::: "memory"); MJH_SCHED_FENCE();
+    fast_va_{name}<SV, true>(mr, blk, lane, B, {va_call});
+    (void)qpos_in; (void)qvel_in; (void)qacc_in; (void)qfrc_out; (void)status;
+    return;
+  }}
+  const long gi = (long)B + (long)(blockIdx.x - nblk)*64 + threadIdx.x;
+  if (gi >= ninst) return;
+  const long si = (gi - B) / per;
+  const int j = (int)((gi - B) % per);
+  for (int it = 0; __hip_atomic_load(flags + (si >> 6), __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_AGENT) != epoch; it++) {{
+    if (it >= {FD_WAIT_ITERS}) {{
+      __hip_atomic_store(needfull + 3, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      break;
+    }}
+    __builtin_amdgcn_s_sleep(8);
+  }}
+  __threadfence();
+  const int* ecs = efc_count + (si >> 6)*4*64 + (si & 63);
+{flag}  fast_vaskip_{name}(mr, (int)(gi >> 6), (int)(gi & 63), (int)(si >> 6), (int)(si & 63), ninst,
+                    ecs, j < {nv} ? j : -1, j < {nv} ? -1 : j - {nv}, eps, nullptr,
+                    nullptr, efc_count, qo_lds, nullptr);
+}}
+{linkage_fd}void launch_fdall_{name}(hipStream_t s, const Mirror& mr, int B, int ninst, int per,
+                               double eps, int* worklist, int* worklist_count,
+                               int* worklist_next, int* efc_count, int* needfull, int* flags,
+                               int epoch) {{
+  const dim3 g((unsigned)((ninst + 63) / 64)), b(64);
+  if (B >= {NT_SV_MIN_B}) {{
+    hipLaunchKernelGGL((k_fdall_{name}<true>), g, b, 0, s, mr, B, ninst, per, eps, worklist,
+                       worklist_count, worklist_next, efc_count, needfull, flags, epoch);
+  }} else {{
+    hipLaunchKernelGGL((k_fdall_{name}<false>), g, b, 0, s, mr, B, ninst, per, eps, worklist,
+                       worklist_count, worklist_next, efc_count, needfull, flags, epoch);
+  }}
 }}
 // mjd_inverseFD layout 2 in one launch over [off, B): the nq = (B - off)/2 qvel perturbations
 // (mj_inverseSkip(mjSTAGE_POS): the va stage over the centre's position stage) on the first
@@ -1835,10 +1948,13 @@ __global__ __launch_bounds__(64, 1) void k_acc_{name}(Mirror mr, int B,
     const int* range) {{""")
   if FUSE:
     gb = "g, b" if ALL_LANES == 64 else f"dim3(g.x*{64 // ALL_LANES}), dim3({ALL_LANES})"
-    variants = ((f"B >= {NT_SV_MIN_B}", "<true>"), ("true", "<false>")) if not extern_c \
-        else (("true", ""),)
+    variants = ((f"B >= {NT_SV_MIN_B}", "<true, false>"), ("true", "<false, false>")) \
+        if not extern_c else (("true", ""),)
+    if not extern_c and M.cmode in ("none", "list"):   # mjd_inverseFD's perturbed instances
+      variants = ((f"mr.sink && B >= {NT_SV_MIN_B}", "<true, true>"),
+                  ("mr.sink", "<false, true>")) + variants
     for cond, v in variants:
-      out.append(f"  if ({cond}) {{\n    hipLaunchKernelGGL(k_all_{name}{v}, {gb}, 0, s, mr, B, "
+      out.append(f"  if ({cond}) {{\n    hipLaunchKernelGGL((k_all_{name}{v}), {gb}, 0, s, mr, B, "
                  f"qpos_in, qvel_in, qacc_in, qfrc_out, status, worklist, worklist_count, "
                  f"worklist_next, efc_count, range);\n    return;\n  }}")
   else:   # staged kernels (experiments): the whole [0, B) range only
@@ -1926,15 +2042,20 @@ def generate_registries(entries) -> tuple:
       if constraint_mode(m) == "all":
         main.append(f"void launch_split_{name}(hipStream_t, const Mirror&, int, int, "
                     "const double*, const double*, const double*, int*, int*, int*);")
+      if fdall_ok(m):
+        main.append(f"void launch_fdall_{name}(hipStream_t, const Mirror&, int, int, int, double, "
+                    "int*, int*, int*, int*, int*, int*, int);")
     else:
       main.append(generate(m, name))
     fns = ", ".join(f"launch_{k}_{name}" if vaskip else "nullptr" for k in ("vaskip", "fdskip"))
     split = f"launch_split_{name}" if constraint_mode(m) == "all" else "nullptr"
+    fdall = f"launch_fdall_{name}" if fdall_ok(m) else "nullptr"
     reg.append(f'  {{0x{fields.model_signature(m):016x}ull, launch_fast_{name}, "{name}", '
-               f'{CONSTRAINT_MODES[constraint_mode(m)]}, {fns}, launch_skip_{name}, {split}}},')
+               f'{CONSTRAINT_MODES[constraint_mode(m)]}, {fns}, launch_skip_{name}, {split}, '
+               f'{fdall}}},')
   main.append("static const FastKernelEntry g_fast_kernels[] = {")
   main.extend(reg)
-  main.append("  {0ull, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr}};")
+  main.append("  {0ull, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr}};")
   return "\n".join(main) + "\n", "\n".join(exact) + "\n"
 
 
@@ -1948,9 +2069,11 @@ def generate_registry(entries) -> str:
     sk = constraint_mode(m) in ("none", "list")
     fns = ", ".join(f"launch_{k}_{name}" if sk else "nullptr" for k in ("vaskip", "fdskip"))
     split = f"launch_split_{name}" if constraint_mode(m) == "all" else "nullptr"
+    fdall = f"launch_fdall_{name}" if fdall_ok(m) else "nullptr"
     reg.append(f'  {{0x{fields.model_signature(m):016x}ull, launch_fast_{name}, "{name}", '
-               f'{CONSTRAINT_MODES[constraint_mode(m)]}, {fns}, launch_skip_{name}, {split}}},')
+               f'{CONSTRAINT_MODES[constraint_mode(m)]}, {fns}, launch_skip_{name}, {split}, '
+               f'{fdall}}},')
   out.append("static const FastKernelEntry g_fast_kernels[] = {")
   out.extend(reg)
-  out.append("  {0ull, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr}};")
+  out.append("  {0ull, nullptr, nullptr, 0, nullptr, nullptr, nullptr, nullptr, nullptr}};")
   return "\n".join(out) + "\n"

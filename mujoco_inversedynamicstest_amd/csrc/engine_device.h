@@ -9519,8 +9519,9 @@ struct Mirror {
   const CoopPair* prog;                      // the static collision program (Lane::prog)
   const int* prog_ipair;
   int nprog;
-  // mjd_inverseFD's perturbed instances (codegen.FD_KEEP): non-null, instance blocks from
-  // full_blk on send the stores no later kernel reads to this region instead of their slots
+  // mjd_inverseFD's perturbed instances (codegen.FD_KEEP): non-null, the FD instantiation of
+  // the generated kernels sends, from instance block full_blk on, the stores no later kernel
+  // reads to this region (64 x the widest field) instead of the instances' slots
   double* sink;
   int full_blk;
 };

@@ -35,6 +35,12 @@ struct FastKernelEntry {
   // B, part, qpos/qvel/qacc row-major inputs or null, status, worklist_next, efc_count)
   void (*launch_split)(hipStream_t, const Mirror&, int, int, const double*, const double*,
                        const double*, int*, int*, int*);
+  // mjd_inverseFD layout 1 in one launch (k_fdall): the position-stage instances [0, A) and
+  // the 2nv skip perturbations per base state after them, each skip wave waiting for its
+  // centres' flags (arguments: A, ninst, 2nv, eps, worklist, its counter, the next counter,
+  // efc_count, fdflag, the flags, the epoch); null where there is no k_vaskip
+  void (*launch_fdall)(hipStream_t, const Mirror&, int, int, int, double, int*, int*, int*,
+                       int*, int*, int*, int);
 };
 
 // the bundled models' kernels (gen_fast.hip), terminated by an entry with launch = nullptr

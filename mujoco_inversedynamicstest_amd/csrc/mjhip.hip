@@ -215,6 +215,7 @@ __global__ __launch_bounds__(64*kExpandWaves) void k_fd_expand(mjhipModel m, Mir
     if (!fdflag[0]) return;
   } else if (fdflag && blockIdx.x == 0 && threadIdx.x == 0) {
     fdflag[0] = 0;                       // k_vaskip raises it later in stream order
+    fdflag[3] = 0;                       // and k_fdall this one, should a wait time out
   }
   const long inst = blk*64 + lane;
   if (inst >= end || inst >= (long)nbase*P) return;
@@ -476,6 +477,8 @@ struct mjhipContext_ {
   // k_all
   int* fdflag = nullptr;
   double* sink = nullptr;                  // Mirror::sink of mjhip_inverseFDBatch's layouts
+  int* fdflags = nullptr;                  // k_fdall's centre-block flags (capacity/64)
+  int fd_epoch = 0;                        // the value k_fdall's flags are raised to
   CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
   mjh::ContactParam* cparams = nullptr;    // each program pair's mj_contactParam
   int* prog_ipair = nullptr;               // each program pair's predefined-pair index or -1
@@ -924,6 +927,7 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->worklist);
   hipFree(c->fdflag);
   hipFree(c->sink);
+  hipFree(c->fdflags);
   hipFree(c->pairs);
   hipFree(c->cparams);
   hipFree(c->prog_ipair);
@@ -1898,8 +1902,8 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
   if (layout && c->fast->launch_fdskip && nQ % 64 == 0 && accskip && accskip[0] == '1') layout = 2;
   int rc = MJHIP_OK;
   // a skip layout's perturbed instances store only what a later kernel of this call reads
-  // (codegen.FD_KEEP): instance blocks past the centres' write the rest into the sink, which
-  // the launches below see through the mirror; restored on every return path
+  // (codegen.FD_KEEP): instance blocks past the centres' send the rest to the sink, as the
+  // launches below see through the mirror; restored on every return path
   struct SinkGuard {
     Mirror* mr;
     ~SinkGuard() { mr->sink = nullptr; mr->full_blk = 0; }
@@ -1920,7 +1924,37 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
                      c->stream, c->dmodel, c->mirror, B, dq, dv, da, (m.nu ? dc : nullptr),
                      eps, layout, layout ? c->fdflag : nullptr, (long)0, nexp, 0);
   FDCHECK(hipGetLastError(), "k_fd_expand launch");
-  if (layout) {
+  // MJHIP_FD_FUSED=1: layout 1 in one launch (k_fdall) -- measured slower than the two
+  // launches (config 5: 4.81M against 5.13M Jacobian sets/s on one box), kept for
+  // the A/B
+  const char* fusedfd = getenv("MJHIP_FD_FUSED");
+  if (layout == 1 && c->fast->launch_fdall && c->fast->launch && fusedfd && fusedfd[0] == '1') {
+    // one launch (k_fdall): the position-stage instances' full pipeline on the first blocks,
+    // the qvel/qacc perturbations' va stage beside them, each skip wave once its centres'
+    // position stage is out (a work-list model's rows are served after the fall-back, as
+    // below; a model without rows hands the work-list counters on as launch_inverse does)
+    if (!c->fdflags) {
+      const size_t n = (size_t)c->capacity / 64 + 1;
+      FDCHECK(hipMalloc((void**)&c->fdflags, n*sizeof(int)), "hipMalloc(FD flags)");
+      FDCHECK(hipMemset(c->fdflags, 0, n*sizeof(int)), "hipMemset(FD flags)");
+      c->fd_epoch = 0;
+    }
+    if (++c->fd_epoch == 0x7fffffff) {     // flags from 2^31 calls ago could match again
+      FDCHECK(hipMemsetAsync(c->fdflags, 0, ((size_t)c->capacity / 64 + 1)*sizeof(int),
+                             c->stream), "hipMemset(FD flags)");
+      c->fd_epoch = 1;
+    }
+    int* cnt = c->worklist + c->wl_parity;
+    int* nxt = c->worklist + (c->wl_parity ^ 1);
+    c->last_path = 1;
+    c->fast->launch_fdall(c->stream, c->mirror, (int)nA, (int)ninst, 2*nv, eps, c->worklist + 2,
+                          cnt, nxt, c->mirror.efc_count, c->fdflag, c->fdflags, c->fd_epoch);
+    FDCHECK(hipGetLastError(), "k_fdall launch");
+    if (c->fast->cmode != 1) {
+      c->wl_last = c->wl_parity;
+      c->wl_parity ^= 1;
+    }
+  } else if (layout) {
     // the nv+1 position-stage instances of every base state: the full pipeline (a work-list
     // model's rows are served once, after the fall-back below has added its own)
     const bool defer = c->fast->cmode == 1 && c->fast->launch;
@@ -1938,6 +1972,8 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
                              c->mirror.efc_count, c->fdflag, eps);
     }
     FDCHECK(hipGetLastError(), "k_vaskip launch");
+  }
+  if (layout) {
     if (c->fast->cmode == 1) {
       // a work-list model whose centre has limit rows: its perturbations need the rows'
       // velocity and acceleration terms, so every qvel/qacc perturbation then runs the full
@@ -1999,7 +2035,16 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
     };
     bool ok = get(DfDq, oq, nn) && get(DfDv, ov, nn) && get(DfDa, oa, nn) && get(DmDq, om, nm) &&
               get(DsDq, sq_, ns) && get(DsDv, sv_, ns) && get(DsDa, sa_, ns);
+    int flags[4] = {0, 0, 0, 0};
+    if (ok && layout) {
+      ok = hipMemcpyAsync(flags, c->fdflag, sizeof(flags), hipMemcpyDeviceToHost,
+                          c->stream) == hipSuccess;
+    }
     FDCHECK(ok ? hipStreamSynchronize(c->stream) : hipErrorUnknown, "FD output download");
+    if (flags[3]) {
+      set_error("mjhip_inverseFDBatch: a k_fdall wave's wait for its centre timed out");
+      return MJHIP_ERR_HIP;
+    }
   }
 #undef FDCHECK
   return MJHIP_OK;

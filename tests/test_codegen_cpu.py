@@ -110,7 +110,7 @@ def test_humanoid_generated_worklist(humanoid):
 
 
 def test_fd_store_elision_bitexact(humanoid):
-  """mjd_inverseFD's perturbed instances (Mirror::sink from block 1 on): the fields a later
+  """mjd_inverseFD's perturbed instances (Mirror::sink, from block 1 on): the fields a later
   kernel reads -- FD_KEEP and every field a stage re-loads -- equal the oracle's bit for bit,
   limit rows (the work-list's generic constraint part) included, and the elided ones are
   never written to the instance's slot; block 0 (the centres) keeps every field."""

@@ -221,14 +221,19 @@ def test_inverse_fd_parity(humanoid):
   """Config 5 at its configured size: batched mjd_inverseFD over 1,024 base states (x 82
   evaluations) vs the oracle's serial mjd_inverseFD on a subsample, and on every base state
   the size-independent property DfDa = M (inverse dynamics is affine in qacc with slope M;
-  forward differences of an affine map are exact up to rounding / eps)."""
+  forward differences of an affine map are exact up to rounding / eps). The stage-skip
+  layout puts the centres first and they keep every field: the fields the perturbed
+  instances send to the sink (codegen.FD_KEEP) equal a plain mj_inverse of the base states."""
   NB = 1024
   q, v, a = sample_states(humanoid, NB, first=900)
   e = engine.InverseEngine(humanoid, capacity=NB * (3 * humanoid.nv + 1))
   try:
     DfDq, DfDv, DfDa, DmDq = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
+    centre = {f: e.field(f, 0, NB) for f in ("xpos", "xmat", "crb", "qLD", "cvel", "qfrc_bias")}
     e.inverse(q, v, a)
     qM = e.field("qM", 0, NB)
+    for f, x in centre.items():
+      np.testing.assert_array_equal(x, e.field(f, 0, NB), err_msg=f)
   finally:
     e.close()
   nv = humanoid.nv
@@ -258,7 +263,9 @@ def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
   """mjd_inverseFD's stage skipping (engine_derivative_fd.c:646-699: the qvel perturbations
   run mj_inverseSkip(mjSTAGE_POS), the qacc ones mjSTAGE_VEL) against every perturbation
   through the full pipeline (MJHIP_FD_NOSKIP=1). Layout 1 (both kinds on the va stage over the
-  centre's position-stage outputs, k_vaskip, the default) equals it bit for bit; layout 2
+  centre's position-stage outputs; the default runs k_all then k_vaskip, MJHIP_FD_FUSED=1 one
+  launch, k_fdall, whose skip waves wait for their centres' flags; both send the perturbed
+  instances' unread stores to the sink) equals it bit for bit; layout 2
   (MJHIP_FD_ACCSKIP=1: the qacc perturbations on the acceleration stage alone over the centre's velocity stage,
   k_fdskip) equals it bit for bit in DfDq, DfDv and DmDq and within the contraction bound in
   DfDa. NB=1024 takes the skip layouts; with joint limits active on every centre, or on every
@@ -272,14 +279,18 @@ def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
   e = engine.InverseEngine(humanoid, capacity=NB * (3 * humanoid.nv + 1))
   try:
     got1 = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)      # layout 1, the default
+    monkeypatch.setenv("MJHIP_FD_FUSED", "1")               # layout 1 in one launch (k_fdall)
+    got1u = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
+    monkeypatch.delenv("MJHIP_FD_FUSED")
     monkeypatch.setenv("MJHIP_FD_ACCSKIP", "1")             # layout 2
     got = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
     monkeypatch.setenv("MJHIP_FD_NOSKIP", "1")
     ref = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
   finally:
     e.close()
-  for name, g, g1, r in zip(("DfDq", "DfDv", "DfDa", "DmDq"), got, got1, ref):
+  for name, g, g1, g1u, r in zip(("DfDq", "DfDv", "DfDa", "DmDq"), got, got1, got1u, ref):
     assert np.array_equal(g1, r), name
+    assert np.array_equal(g1u, r), name
     if name == "DfDa":
       _assert_fd_contraction_close(g, r)
     else:

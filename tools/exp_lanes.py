@@ -33,7 +33,8 @@ def build():
                  for n, src, dc, ds in ge.FAST_MODELS]
       inc = os.path.join(exp, f"gen_fast_l{nl}.inc")
       with open(inc, "w") as f:
-        f.write(codegen.generate_registry(entries))
+        # the main unit only: the exact models' kernels stay in build/obj/gen_fast_exact.o
+        f.write(codegen.generate_registries(entries)[0])
     finally:
       codegen.ALL_LANES, codegen.LANES = saved[0], saved[1]
     unit = os.path.join(exp, f"gen_fast_l{nl}.hip")

@@ -53,6 +53,10 @@ for step in "$@"; do
     c5)
       timeout -k 10 180 python bench.py --config 5 > gpurun_out/c5.json 2> gpurun_out/c5.err || exit 1
       tail -1 gpurun_out/c5.json ;;
+    c5fused)                                # layout 1 in one launch, k_fdall (A/B)
+      MJHIP_FD_FUSED=1 timeout -k 10 180 python bench.py --config 5 > gpurun_out/c5fused.json \
+        2> gpurun_out/c5fused.err || exit 1
+      tail -1 gpurun_out/c5fused.json ;;
     c5own)
       timeout -k 10 180 python bench.py --config 5 --own-stream > gpurun_out/c5own.json \
         2> gpurun_out/c5own.err || exit 1
