@@ -113,17 +113,18 @@ FD_WAIT_ITERS = 1 << 22
 # centres come first): a mirror field the straight-line stages store but never load is read
 # by no later kernel of that call either -- the finite differences read qfrc_inverse (and qM
 # for DmDq), a work-list model's limit rows the fields below -- so in instance blocks at or
-# past Mirror::full_blk (Mirror::sink set) its stores go to the sink, one small region every
-# such wave overwrites, as plain stores, so its lines stay dirty in L2 instead of streaming
-# to memory. Only the FD = true instantiation of the stage bodies does this (k_all's,
-# launched when Mirror::sink is set, k_vaskip's and k_fdall's); it stores the elided fields
-# temporally everywhere and selects each one's base per wave. Every other instantiation is
-# the plain kernel. The arithmetic is untouched, so every result is the full kernel's bit for
-# bit. Measured (28,672 instances of the humanoid, mjd_inverseFD's position stage): 134.6 us
-# storing everything, 126.6 us with streaming stores into the sink, 148 us skipping the
-# stores behind a wave-uniform branch each (which also moved results by an ulp: the
-# branches split the blocks the multiply-adds are formed in); the base selects in every
-# instantiation cost the headline kernel 4%.
+# past Mirror::full_blk (Mirror::fd_elide set) its stores are compiled out: the FD = true
+# instantiation of the stage bodies drops them (if constexpr), and the k_all kernel launched
+# when Mirror::fd_elide is set runs it on those blocks and the plain bodies on the centres'
+# (one wave-uniform branch at the top); k_vaskip has the FD bodies only. Every other launch is
+# the plain kernel. The arithmetic is the plain kernel's, so every result is the full
+# pipeline's bit for bit (test_inverse_fd_stage_skip_bit_exact). Measured (28,672 instances of
+# the humanoid, mjd_inverseFD's position stage): 134.6 us storing everything, 126.6 us with
+# streaming stores into a shared sink (a streaming store reaches memory wherever it points),
+# 125.4 us with temporal stores into it, 148 us skipping each store behind a wave-uniform
+# branch (which also moved results by an ulp: the branches split the blocks the
+# multiply-adds are formed in); selecting the sink in every instantiation cost the headline
+# kernel 4%.
 FD_KEEP = frozenset({"qpos", "qvel", "qacc", "qfrc_inverse", "qfrc_passive", "qfrc_constraint",
                      "qfrc_actuator", "ten_length", "ten_J", "ten_velocity", "actuator_length",
                      "actuator_moment", "actuator_velocity", "qM", "sensordata"})
@@ -141,24 +142,16 @@ def fd_elided(bodies) -> set:
 
 
 def _elide_stores(body: str, elided) -> str:
-  """FD instantiation: the elided fields' stores are temporal, and from Mirror::full_blk on
-  (Mirror::sink set) they land in the sink."""
+  """FD instantiation: the elided fields' stores are compiled out (if constexpr); k_all runs
+  it on the instance blocks past Mirror::full_blk and the plain body on the others."""
   import re
-  decl = re.compile(r"double\* __restrict__ P_(\w+) = (mr\.\w+ \+ \(\(long\)blk\*\d+\)\*64) \+ lane;")
-  body = decl.sub(lambda mt: mt.group(0) if mt.group(1) not in elided else
-                  f"double* __restrict__ P_{mt.group(1)} = (FD && mr.sink && blk >= mr.full_blk ? "
-                  f"mr.sink : {mt.group(2)}) + lane;", body)
-  nt = re.compile(r"^(\s*)MJH_NT_STORE\(P_(\w+)\[(.*)$")
-  ntif = re.compile(r"^(\s*)MJH_NT_STORE_IF\((\w+), P_(\w+)\[(.*)$")
+  store = re.compile(r"^(\s*)((?:MJH_NT_STORE(?:_IF)?\((?:\w+, )?P_(\w+)\[|P_(\w+)\[[^\]]+\] = ).*;)$")
 
   def one(line):
-    mt = nt.match(line)
-    if mt and mt.group(2) in elided:
-      return f"{mt.group(1)}MJH_NT_STORE_IF(!FD, P_{mt.group(2)}[{mt.group(3)}"
-    mt = ntif.match(line)
-    if mt and mt.group(3) in elided:
-      return f"{mt.group(1)}MJH_NT_STORE_IF(!FD && {mt.group(2)}, P_{mt.group(3)}[{mt.group(4)}"
-    return line
+    mt = store.match(line)
+    if not mt or (mt.group(3) or mt.group(4)) not in elided:
+      return line
+    return f"{mt.group(1)}if constexpr (!FD) {{ {mt.group(2)} }}"
   return "\n".join(one(x) for x in body.split("\n"))
 
 
@@ -1573,7 +1566,9 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
   double trig[{max(1, 2 * len(M.trig) * 64)}];   // LDS on the device (k_pos)
   double qo_lds[{64 * max(M.nv, 1)}];             // LDS on the device (k_va)
   double qmr[{max(1, m.nM)}];                        // registers on the device (k_all)
-""" + "".join(f"  fast_{st}_{name}<true, true>(mr, blk, lane, B, {_SIG[st][1]});\n"
+  const bool fd = mr.fd_elide && blk >= mr.full_blk;   // mjd_inverseFD's perturbed blocks
+""" + "".join(f"  if (fd) fast_{st}_{name}<true, true>(mr, blk, lane, B, {_SIG[st][1]});\n"
+              f"  else fast_{st}_{name}<true, false>(mr, blk, lane, B, {_SIG[st][1]});\n"
               for st in STAGES)
              + (f"""  if (qfrc_out && (long)blk*64 + lane < B) {{
     for (int k = 0; k < {M.nv}; k++) qfrc_out[((long)blk*64 + lane)*{M.nv} + k] = qo_lds[lane*{M.nv} + k];
@@ -1641,7 +1636,18 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
   # run-time code object (C linkage, no template) has the SV = true kernel only
   tmpl = "" if extern_c else "template <bool SV, bool FD>\n"
   sv = "true" if extern_c else "SV"
-  fdv = "false" if extern_c else "FD"
+
+  def stage_calls(fd, ind="  "):
+    return "\n".join(f"{ind}fast_{st}_{name}<{sv}, {fd}>(mr, {bl}, B, "
+                     f"{_SIG[st][1].replace('worklist_next', 'nullptr')});\n"
+                     f"{ind}asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE(); MJH_PHASE({20 + k});"
+                     for k, st in enumerate(STAGES))
+  # the FD instantiation (mjd_inverseFD's stage-skip layout): the plain bodies on the centres'
+  # blocks, the bodies without the elided stores on the blocks past them (Mirror::full_blk)
+  blkexpr = "blk0 + (int)blockIdx.x" if sub == 1 else f"blk0 + (int)blockIdx.x / {sub}"
+  all_calls = stage_calls("false") if extern_c else (
+      f"  if (FD && mr.fd_elide && {blkexpr} >= mr.full_blk) {{\n{stage_calls('true', '    ')}\n"
+      f"  }} else {{\n{stage_calls('false', '    ')}\n  }}")
   out.append(f"""{tmpl}{linkage}__global__ __launch_bounds__({nl}, {ALL_WAVES}) void k_all_{name}(Mirror mr, int B,
     const double* __restrict__ qpos_in, const double* __restrict__ qvel_in,
     const double* __restrict__ qacc_in, double* __restrict__ qfrc_out, int* __restrict__ status,
@@ -1654,11 +1660,7 @@ def generate(m, name: str, store_fields=None, extern_c: bool = False, shared: bo
   int blk0 = 0;
   if (range) {{ blk0 = range[0] >> 6; B = range[1]; }}
   MJH_PHASE0(19, 27);
-""" + "\n".join(f"  fast_{st}_{name}<{sv}, {fdv}>(mr, {bl}, B, "
-                f"{_SIG[st][1].replace('worklist_next', 'nullptr')});\n"
-                f"  asm volatile(\"\" ::: \"memory\"); MJH_SCHED_FENCE(); MJH_PHASE({20 + k});"
-                for k, st in enumerate(STAGES))
-             + "\n" + fuse_tail + "}")
+""" + all_calls + "\n" + fuse_tail + "}")
   # the split launch of a model whose constraint rows serve every instance (contacts): the
   # position stage alone (k_spos), then the fac and va stages (k_sfv), so that the
   # cooperative constraint kernel -- which reads only position-stage outputs and the inputs
@@ -1763,9 +1765,7 @@ __global__ __launch_bounds__(64, 1) void k_sfv_{name}(Mirror mr, int B,
     skip_body = skip_body.replace("const bool cflag = ec[0] != 0;",
                                   "const bool cflag = ecs[0] != 0;")
     skip_body = skip_body.replace("MJH_NT_STORE_IF(SV, ", "MJH_NT_STORE_IF(true, ")
-    skip_body = skip_body.replace("(FD && mr.sink", "(mr.sink").replace(
-        "MJH_NT_STORE_IF(!FD && SV, ", "MJH_NT_STORE_IF(false, ").replace(
-        "MJH_NT_STORE_IF(!FD, ", "MJH_NT_STORE_IF(false, ")
+    skip_body = skip_body.replace("if constexpr (!FD) {", "if constexpr (false) {")
     assert "FD" not in re.sub(r"\w*FD\w+|\w+FD\w*", "", skip_body), "k_vaskip: FD left"
     skip_body = skip_body.replace("MJH_NT_LOAD_IF(SV, ", "MJH_NT_LOAD_IF(false, ")
     skip_body = _perturb_loads(skip_body, {"qvel": "pv", "qacc": "pa"})
@@ -1846,16 +1846,22 @@ __global__ __launch_bounds__(64, 1) void k_fdall_{name}(Mirror mr, int B, int ni
     double* qfrc_out = nullptr;
     int* status = nullptr;
     const int blk = blockIdx.x, lane = threadIdx.x;
-    fast_pos_{name}<SV, true>(mr, blk, lane, B, {pos_call});
-    asm volatile("" ::: "memory");
-    if (blk < mr.full_blk) {{               // a centre block: its position stage is out
+    if (blk < mr.full_blk) {{               // a centre block: every field, position stage out
+      fast_pos_{name}<SV, false>(mr, blk, lane, B, {pos_call});
+      asm volatile("" ::: "memory");
       __threadfence();
       if (lane == 0) __hip_atomic_store(flags + blk, epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      MJH_SCHED_FENCE();
+      fast_fac_{name}<SV, false>(mr, blk, lane, B, {fac_call});
+      asm volatile("" ::: "memory"); MJH_SCHED_FENCE();
+      fast_va_{name}<SV, false>(mr, blk, lane, B, {va_call});
+    }} else {{
+      fast_pos_{name}<SV, true>(mr, blk, lane, B, {pos_call});
+      asm volatile("" ::: "memory"); MJH_SCHED_FENCE();
+      fast_fac_{name}<SV, true>(mr, blk, lane, B, {fac_call});
+      asm volatile("" ::: "memory"); MJH_SCHED_FENCE();
+      fast_va_{name}<SV, true>(mr, blk, lane, B, {va_call});
     }}
-    MJH_SCHED_FENCE();
-    fast_fac_{name}<SV, true>(mr, blk, lane, B, {fac_call});
-    asm volatile("" ::: "memory"); MJH_SCHED_FENCE();
-    fast_va_{name}<SV, true>(mr, blk, lane, B, {va_call});
     (void)qpos_in; (void)qvel_in; (void)qacc_in; (void)qfrc_out; (void)status;
     return;
   }}
@@ -1951,8 +1957,8 @@ __global__ __launch_bounds__(64, 1) void k_acc_{name}(Mirror mr, int B,
     variants = ((f"B >= {NT_SV_MIN_B}", "<true, false>"), ("true", "<false, false>")) \
         if not extern_c else (("true", ""),)
     if not extern_c and M.cmode in ("none", "list"):   # mjd_inverseFD's perturbed instances
-      variants = ((f"mr.sink && B >= {NT_SV_MIN_B}", "<true, true>"),
-                  ("mr.sink", "<false, true>")) + variants
+      variants = ((f"mr.fd_elide && B >= {NT_SV_MIN_B}", "<true, true>"),
+                  ("mr.fd_elide", "<false, true>")) + variants
     for cond, v in variants:
       out.append(f"  if ({cond}) {{\n    hipLaunchKernelGGL((k_all_{name}{v}), {gb}, 0, s, mr, B, "
                  f"qpos_in, qvel_in, qacc_in, qfrc_out, status, worklist, worklist_count, "

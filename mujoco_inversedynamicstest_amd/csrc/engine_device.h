@@ -9519,10 +9519,10 @@ struct Mirror {
   const CoopPair* prog;                      // the static collision program (Lane::prog)
   const int* prog_ipair;
   int nprog;
-  // mjd_inverseFD's perturbed instances (codegen.FD_KEEP): non-null, the FD instantiation of
-  // the generated kernels sends, from instance block full_blk on, the stores no later kernel
-  // reads to this region (64 x the widest field) instead of the instances' slots
-  double* sink;
+  // mjd_inverseFD's perturbed instances (codegen.FD_KEEP): fd_elide set, the generated
+  // kernels' FD instantiation drops, from instance block full_blk on, the stores no later
+  // kernel reads
+  int fd_elide;
   int full_blk;
 };
 

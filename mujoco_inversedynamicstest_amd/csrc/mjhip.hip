@@ -476,7 +476,6 @@ struct mjhipContext_ {
   // rows (k_vaskip), [1..2] the instance range {first, end} the gated k_fd_expand hands to
   // k_all
   int* fdflag = nullptr;
-  double* sink = nullptr;                  // Mirror::sink of mjhip_inverseFDBatch's layouts
   int* fdflags = nullptr;                  // k_fdall's centre-block flags (capacity/64)
   int fd_epoch = 0;                        // the value k_fdall's flags are raised to
   CoopPair* pairs = nullptr;               // static geom-pair program (coop_program)
@@ -926,7 +925,6 @@ MJHIP_API void mjhip_contextFree(mjhipContext* c) {
   hipFree(c->status);
   hipFree(c->worklist);
   hipFree(c->fdflag);
-  hipFree(c->sink);
   hipFree(c->fdflags);
   hipFree(c->pairs);
   hipFree(c->cparams);
@@ -1902,19 +1900,14 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
   if (layout && c->fast->launch_fdskip && nQ % 64 == 0 && accskip && accskip[0] == '1') layout = 2;
   int rc = MJHIP_OK;
   // a skip layout's perturbed instances store only what a later kernel of this call reads
-  // (codegen.FD_KEEP): instance blocks past the centres' send the rest to the sink, as the
-  // launches below see through the mirror; restored on every return path
-  struct SinkGuard {
+  // (codegen.FD_KEEP): instance blocks past the centres' drop the rest, as the launches below
+  // see through the mirror; restored on every return path
+  struct ElideGuard {
     Mirror* mr;
-    ~SinkGuard() { mr->sink = nullptr; mr->full_blk = 0; }
-  } sink_guard{&c->mirror};
+    ~ElideGuard() { mr->fd_elide = 0; mr->full_blk = 0; }
+  } elide_guard{&c->mirror};
   if (layout) {
-    if (!c->sink) {
-      int maxs = 1;
-      for (const auto& f : c->fields) maxs = f.second.second > maxs ? f.second.second : maxs;
-      FDCHECK(hipMalloc((void**)&c->sink, sizeof(double)*64*(size_t)maxs), "hipMalloc(sink)");
-    }
-    c->mirror.sink = c->sink;
+    c->mirror.fd_elide = 1;
     c->mirror.full_blk = (B + 63) / 64;
   }
   // with a skip layout only the position-stage block is expanded: the skip kernels read their

@@ -18,8 +18,8 @@ static void constraint_part(const mjhipModel* m, Mirror& mr, int inst) {
   mjh::constraintOnly<64, C, F>(*m, d);
 }
 
-// mjd_inverseFD's store elision (Mirror::sink, codegen.FD_KEEP): instance blocks from
-// full_blk on send their elided stores to a sink; -1 (the default) stores everything
+// mjd_inverseFD's store elision (Mirror::fd_elide, codegen.FD_KEEP): instance blocks from
+// full_blk on drop their elided stores; -1 (the default) stores everything
 static int g_full_blk = -1;
 extern "C" void cg_set_full_blk(int full_blk) { g_full_blk = full_blk; }
 
@@ -50,8 +50,9 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
   mr.name = (int*)calloc((size_t)nblk * 64 * ((n) + 1), sizeof(int));
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
+  (void)maxs;
   if (g_full_blk >= 0) {
-    mr.sink = (double*)calloc((size_t)64 * maxs, sizeof(double));
+    mr.fd_elide = 1;
     mr.full_blk = g_full_blk;
   }
   mr.efc_cap = efc_cap;
@@ -113,6 +114,5 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
   MJHIP_SCRATCH_INT_FIELDS
 #undef XSI
   free(wl);
-  free(mr.sink);
   return served;
 }

@@ -56,7 +56,7 @@ def build(m, name):
 
 
 def run_and_compare(m, name, q, v, a, full_blk=-1):
-  """full_blk >= 0: Mirror::sink set, instance blocks from full_blk on store only what
+  """full_blk >= 0: Mirror::fd_elide set, instance blocks from full_blk on store only what
   mjd_inverseFD's later kernels read (codegen.FD_KEEP and every re-read field); those are
   compared, and the elided fields must stay untouched (zero)."""
   L = build(m, name)
@@ -110,7 +110,7 @@ def test_humanoid_generated_worklist(humanoid):
 
 
 def test_fd_store_elision_bitexact(humanoid):
-  """mjd_inverseFD's perturbed instances (Mirror::sink, from block 1 on): the fields a later
+  """mjd_inverseFD's perturbed instances (Mirror::fd_elide, from block 1 on): the fields a later
   kernel reads -- FD_KEEP and every field a stage re-loads -- equal the oracle's bit for bit,
   limit rows (the work-list's generic constraint part) included, and the elided ones are
   never written to the instance's slot; block 0 (the centres) keeps every field."""

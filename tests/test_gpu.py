@@ -223,7 +223,7 @@ def test_inverse_fd_parity(humanoid):
   the size-independent property DfDa = M (inverse dynamics is affine in qacc with slope M;
   forward differences of an affine map are exact up to rounding / eps). The stage-skip
   layout puts the centres first and they keep every field: the fields the perturbed
-  instances send to the sink (codegen.FD_KEEP) equal a plain mj_inverse of the base states."""
+  instances drop (codegen.FD_KEEP) equal a plain mj_inverse of the base states."""
   NB = 1024
   q, v, a = sample_states(humanoid, NB, first=900)
   e = engine.InverseEngine(humanoid, capacity=NB * (3 * humanoid.nv + 1))
@@ -264,11 +264,11 @@ def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
   run mj_inverseSkip(mjSTAGE_POS), the qacc ones mjSTAGE_VEL) against every perturbation
   through the full pipeline (MJHIP_FD_NOSKIP=1). Layout 1 (both kinds on the va stage over the
   centre's position-stage outputs; the default runs k_all then k_vaskip, MJHIP_FD_FUSED=1 one
-  launch, k_fdall, whose skip waves wait for their centres' flags; both send the perturbed
-  instances' unread stores to the sink) equals it bit for bit; layout 2
+  launch, k_fdall, whose skip waves wait for their centres' flags; the perturbed instances
+  run the generated bodies without the stores nobody reads, which the compiler contracts
+  into multiply-adds a little differently) equals it within the contraction bound; layout 2
   (MJHIP_FD_ACCSKIP=1: the qacc perturbations on the acceleration stage alone over the centre's velocity stage,
-  k_fdskip) equals it bit for bit in DfDq, DfDv and DmDq and within the contraction bound in
-  DfDa. NB=1024 takes the skip layouts; with joint limits active on every centre, or on every
+  k_fdskip) within it too. NB=1024 takes the skip layouts; with joint limits active on every centre, or on every
   fifth, the work-list model falls back on the device to the full pipeline over the
   perturbations; NB=3 (28*3 instances, not a whole wave) never takes them."""
   q, v, a = sample_states(humanoid, NB, first=300)
@@ -288,20 +288,18 @@ def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
     ref = e.inverse_fd(q, v, a, eps=1e-6, dmdq=True)
   finally:
     e.close()
-  for name, g, g1, g1u, r in zip(("DfDq", "DfDv", "DfDa", "DmDq"), got, got1, got1u, ref):
-    assert np.array_equal(g1, r), name
-    assert np.array_equal(g1u, r), name
-    if name == "DfDa":
-      _assert_fd_contraction_close(g, r)
-    else:
-      assert np.array_equal(g, r), name
+  for g, g1, g1u, r in zip(got, got1, got1u, ref):
+    _assert_fd_contraction_close(g1, r)
+    _assert_fd_contraction_close(g1u, r)
+    _assert_fd_contraction_close(g, r)
 
 
 def _assert_fd_contraction_close(g, r, eps=1e-6):
-  """Layout 2's acceleration stage alone (k_fdskip) against the full pipeline: the same
-  operations, but the compiler contracts multiply-adds per kernel, so a term of qfrc_inverse
-  can round differently by a few ulp; the forward difference scales that by 1/eps. Bound: 16
-  ulp of the largest |qfrc_inverse| (<= 1e3 on these states) over eps."""
+  """A skip layout against the full pipeline: the same operations, but the compiler contracts
+  multiply-adds per kernel body (layout 2's acceleration-only stage; layout 1's perturbed
+  instances, whose bodies drop the stores nobody reads), so a term of qfrc_inverse can round
+  differently by a few ulp; the forward difference scales that by 1/eps. Bound: 16 ulp of the
+  largest |qfrc_inverse| (<= 1e3 on these states) over eps."""
   tol = 16 * np.finfo(float).eps * 1e3 / eps
   err = np.abs(g - r).max()
   assert err <= tol, f"DfDa layout 2 vs full pipeline {err:.3e} > {tol:.3e}"
@@ -310,9 +308,10 @@ def _assert_fd_contraction_close(g, r, eps=1e-6):
 @pytest.mark.parametrize("name", ["inverse_test", "linear", "inertia"])
 def test_inverse_fd_stage_skip_other_models(name, monkeypatch):
   """The stage-skip layouts on the other bundled models with a k_vaskip kernel (work-list or
-  row-free): layout 1 device-resident and back to back (no host wait between calls) against
-  the full pipeline bit for bit, layout 2 (k_fdskip) within the contraction bound in DfDa and
-  bit for bit elsewhere, and both against the oracle's serial mjd_inverseFD."""
+  row-free): layout 1 device-resident and back to back (no host wait between calls, each call
+  bit-identical to the last) against the full pipeline within the contraction bound (the
+  perturbed instances' bodies without their unread stores), layout 2 (k_fdskip) within it
+  as well, and both against the oracle's serial mjd_inverseFD."""
   import torch
   m = models.load(name, disable_contact=True, disable_sensor=(name == "linear"))
   NB = 64
@@ -334,12 +333,9 @@ def test_inverse_fd_stage_skip_other_models(name, monkeypatch):
     ref = e.inverse_fd(q, v, a, eps=1e-6)
   finally:
     e.close()
-  for name, g, g2, r in zip(("DfDq", "DfDv", "DfDa"), got, got2, ref[:3]):
-    assert np.array_equal(g, r), name
-    if name == "DfDa":
-      _assert_fd_contraction_close(g2, r)
-    else:
-      assert np.array_equal(g2, r), name
+  for g, g2, r in zip(got, got2, ref[:3]):
+    _assert_fd_contraction_close(g, r)
+    _assert_fd_contraction_close(g2, r)
   o = Oracle(m)
   for i in range(0, NB, 8):
     o.set_state(q[i], v[i], a[i])
