@@ -217,10 +217,11 @@ def fast_path_supported(m) -> str | None:
   if m.opt["enableflags"] & (1 << 3):
     if int(m.opt["integrator"]) == 1:
       return "INVDISCRETE with RK4 (an error in the reference)"
-    if any(int(t) in TRN_AFTER for t in m.actuator_trntype[:m.nu]):
-      # implicit damping reads actuator_moment before the constraint kernel, and a body
+    if any(int(t) == 5 for t in m.actuator_trntype[:m.nu]):
+      # mj_discreteAcc's implicit damping reads actuator_moment before the constraint kernel
+      # (k_discrete_before forms the slider-crank and site ones first), but a body
       # transmission needs the contacts that kernel makes
-      return "INVDISCRETE with slider-crank, site or body transmissions"
+      return "INVDISCRETE with body (adhesion) transmissions"
   for a in range(m.nu):
     if m.actuator_trntype[a] not in (0, 1, 2, 3, 4, 5):
       return "unknown transmission"

@@ -56,11 +56,16 @@ __global__ __launch_bounds__(64) void k_tendon_after(mjhipModel m, Mirror mr, in
 }
 
 // mjENBL_INVDISCRETE on the straight-line path (csrc/post_pass.h): mj_discreteAcc and the
-// RNE over its qacc before the constraint kernel; the caller's qacc back after the sensors
-__global__ __launch_bounds__(64) void k_discrete_before(mjhipModel m, Mirror mr, int B) {
+// RNE over its qacc before the constraint kernel; the caller's qacc back after the sensors.
+// trn: the slider-crank and site transmissions the generated kernels leave to the pass after
+// the constraint kernel are formed here first (mj_discreteAcc's implicit damping reads their
+// actuator_moment; the reference has them from mj_fwdPosition, before mj_discreteAcc)
+__global__ __launch_bounds__(64) void k_discrete_before(mjhipModel m, Mirror mr, int B,
+                                                        int trn) {
   const long inst = (long)blockIdx.x*64 + threadIdx.x;
   if (inst >= B) return;
   Lane<64> d = lane_view(mr, blockIdx.x, threadIdx.x);
+  if (trn) mjh::transmissionAfter(m, d);
   mjh::discreteBefore(m, d);
 }
 
@@ -1122,7 +1127,7 @@ static int finish_fast(mjhipContext* c, int B, dim3 grid, dim3 block, int skipse
                        int* status, bool discrete) {
   const int sensors = !skipsensor && c->hmodel.nsensor > 0 &&
                       !(c->hmodel.opt.disableflags & mjhipDSBL_SENSOR);
-  const int trn = mjh_needTrnAfter(&c->hmodel);
+  const int trn = mjh_needTrnAfter(&c->hmodel) && !discrete;   // discrete: already formed
   if (sensors || trn || (c->hmodel.opt.enableflags & mjhipENBL_ENERGY)) {
     hipLaunchKernelGGL(k_sensors, grid, block, 0, c->stream, c->dmodel, c->mirror, B,
                        sensors, trn);
@@ -1234,7 +1239,8 @@ static int launch_inverse(mjhipContext* c, int B, const double* qpos, const doub
       hipLaunchKernelGGL(k_fluid_after, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
     }
     if (discrete) {                      // mj_discreteAcc and its RNE before the constraints
-      hipLaunchKernelGGL(k_discrete_before, grid, block, 0, c->stream, c->dmodel, c->mirror, B);
+      hipLaunchKernelGGL(k_discrete_before, grid, block, 0, c->stream, c->dmodel, c->mirror, B,
+                         mjh_needTrnAfter(&c->hmodel));
     }
     const int* wl = c->worklist + 2;
     if (fused && c->coop && c->fast->cmode) {   // cooperative lanes per instance

@@ -77,7 +77,10 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
     mjh::Lane<64> d = lane_view(mr, i / 64, i % 64);
     if (spatial) mjh::tendonAfter<64>(*m, d);
     else mjh::fluidAfter<64>(*m, d);
-    if (mjh::hasDiscrete(*m)) mjh::discreteBefore<64>(*m, d);   // k_discrete_before
+    if (mjh::hasDiscrete(*m)) {                                  // k_discrete_before
+      if (mjh_needTrnAfter(m)) mjh::transmissionAfter<64>(*m, d);
+      mjh::discreteBefore<64>(*m, d);
+    }
   }
   const bool fused = mjh::fastFusedOk(*m);
   const int served = cmode == 2 ? B : (cmode == 1 ? wc : 0);
@@ -93,7 +96,7 @@ extern "C" int cg_run(const mjhipModel* m, int B, const double* qpos, const doub
   }
   for (int i = 0; i < B; i++) {   // transmission/sensor/energy pass (k_sensors on the device)
     mjh::Lane<64> d = lane_view(mr, i / 64, i % 64);
-    mjh::sensorsAfter<64>(*m, d, true, mjh_needTrnAfter(m) != 0);
+    mjh::sensorsAfter<64>(*m, d, true, mjh_needTrnAfter(m) && !mjh::hasDiscrete(*m));
     if (mjh::hasDiscrete(*m)) mjh::discreteRestore<64>(*m, d);  // k_discrete_restore
   }
   size_t off = 0;

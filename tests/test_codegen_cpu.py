@@ -371,3 +371,38 @@ def test_generated_site_slidercrank_body_transmissions():
   q[:, 7:9] = q[:, 0:2] + rng.uniform(-0.4, 0.4, (32, 2))
   q[:, 9] = 0.1 + 0.05 * rng.normal(size=32)
   run_and_compare(m, "adhesion", q, rng.normal(size=(32, m.nv)), rng.normal(size=(32, m.nv)))
+
+
+# slider-crank and site transmissions (left by the generated kernels to the pass after the
+# constraint kernel), damped so that mj_discreteAcc's implicit integrators read their moments
+TRN_AFTER_XML = """<mujoco><option integrator="{integ}"><flag invdiscrete="enable" contact="disable"/>
+  </option><worldbody>
+  <body name="crank"><joint name="c" axis="0 1 0" damping=".1"/>
+    <geom type="capsule" fromto="0 0 0 .2 0 0" size=".02"/><site name="pin" pos=".2 0 0"/></body>
+  <body name="slider" pos=".5 0 0"><joint name="s" type="slide" axis="1 0 0" damping=".2"/>
+    <geom type="box" size=".05 .05 .05"/><site name="slide" zaxis="1 0 0"/></body>
+  <body name="arm" pos="0 0 .5"><joint name="a" axis="1 0 0" damping=".05"/>
+    <geom type="capsule" fromto="0 0 0 0 .2 0" size=".03"/>
+    <site name="tip" pos="0 .2 0"/><site name="ref" pos="0 0 .1"/></body>
+  </worldbody><actuator>
+  <general cranksite="pin" slidersite="slide" cranklength=".45" biastype="affine"
+           biasprm="0 0 -0.5"/>
+  <velocity site="tip" gear="0 0 1 0 0 0" kv="0.7"/>
+  <general site="tip" refsite="ref" gear="0 1 0 0 0 0" gaintype="affine" gainprm="1 0 0.3"/>
+  </actuator></mujoco>"""
+
+
+@pytest.mark.parametrize("integ", ["Euler", "implicit", "implicitfast"])
+def test_invdiscrete_trn_after_generated_bitexact(integ):
+  """INVDISCRETE with slider-crank and site transmissions on the straight-line path: the
+  discrete pass forms those transmissions first (k_discrete_before; the reference has them
+  from mj_fwdPosition before mj_discreteAcc), so the implicit damping reads their moments;
+  every output equals the oracle's bit for bit."""
+  m = mjcf.load_xml_string(TRN_AFTER_XML.format(integ=integ))
+  assert codegen.fast_path_supported(m) is None
+  assert any(int(t) in codegen.TRN_AFTER for t in m.actuator_trntype[:m.nu])
+  rng = np.random.default_rng(12)
+  B = 48
+  q = rng.uniform(-1, 1, (B, m.nq)) * 0.5
+  v, a = rng.normal(size=(B, m.nv)), rng.normal(size=(B, m.nv))
+  run_and_compare(m, f"trn_after_{integ}", q, v, a)

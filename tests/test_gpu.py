@@ -1537,3 +1537,31 @@ def test_spatial_tendon_mixed_parity():
   assert_close(pas, np.array(rp), "qfrc_passive")
   assert_close(sd, np.array(rs), "sensordata")
   assert ncon[:, 0].sum() > 0
+
+
+@pytest.mark.parametrize("integ", ["Euler", "implicit", "implicitfast"])
+def test_invdiscrete_trn_after_parity(integ):
+  """INVDISCRETE with slider-crank and site transmissions now on the straight-line path
+  (run-time specialized kernel, the transmissions formed by the discrete pass): qfrc_inverse
+  and the actuator moments vs the oracle, the generic kernel alike, qacc restored."""
+  from test_codegen_cpu import TRN_AFTER_XML
+  from mujoco_inversedynamicstest_amd import mjcf
+  m = mjcf.load_xml_string(TRN_AFTER_XML.format(integ=integ))
+  B = 256
+  rng = np.random.default_rng(13)
+  q = rng.uniform(-1, 1, (B, m.nq)) * 0.5
+  v, a = rng.normal(size=(B, m.nv)), rng.normal(size=(B, m.nv))
+  e = engine.InverseEngine(m, capacity=B)
+  try:
+    assert e.fast_kernel is not None and e.fast_kernel.startswith("rt_")
+    f, st = e.inverse(q, v, a, status=True)
+    assert (st == 0).all()
+    np.testing.assert_array_equal(e.field("qacc", 0, B), a)       # restored
+    mom = e.field("actuator_moment", 0, B)
+    g = e.inverse(q, v, a, generic=True)
+  finally:
+    e.close()
+  ref, _ = oracle_batch(m, q, v, a, ("qfrc_inverse", "actuator_moment"))
+  assert_close(f, ref["qfrc_inverse"], f"qfrc_inverse (INVDISCRETE {integ}, TRN_AFTER)")
+  assert_close(g, ref["qfrc_inverse"], f"qfrc_inverse (INVDISCRETE {integ}, generic)")
+  assert_close(mom, ref["actuator_moment"], "actuator_moment")
