@@ -208,10 +208,10 @@ __global__ __launch_bounds__(64*kExpandWaves) void k_fd_expand(mjhipModel m, Mir
                                                   long first, long end, int gate) {
   const int nv = m.nv, nq = m.nq, P = 3*nv + 1;
   const int ncomp = 2*nv + m.njnt + (ctrl ? m.nu : 0);
-  // one block of kExpandWaves waves per 64 instances: wave w writes components w,
-  // w + kExpandWaves, ...
-  const long blk = first/64 + blockIdx.x;
-  const int lane = threadIdx.x % 64, wave = threadIdx.x / 64;
+  // blocks of blockDim.x / 64 waves, striding over the 64-instance blocks of [first, end)
+  // (the main expansion: one block each; the gated one: a few one-wave blocks, so that the
+  // usual empty launch dispatches little): wave w writes components w, w + waves, ...
+  const int lane = threadIdx.x % 64, wave = threadIdx.x / 64, waves = blockDim.x / 64;
   if (gate) {
     if (blockIdx.x == 0 && threadIdx.x == 0) {
       fdflag[1] = (int)first;
@@ -222,13 +222,14 @@ __global__ __launch_bounds__(64*kExpandWaves) void k_fd_expand(mjhipModel m, Mir
     fdflag[0] = 0;                       // k_vaskip raises it later in stream order
     fdflag[3] = 0;                       // and k_fdall this one, should a wait time out
   }
+  for (long blk = first/64 + blockIdx.x; blk*64 < end; blk += gridDim.x) {
   const long inst = blk*64 + lane;
-  if (inst >= end || inst >= (long)nbase*P) return;
+  if (inst >= end || inst >= (long)nbase*P) continue;
   long b;
   int p;
   fd_bp(layout, nbase, inst, nv, &b, &p);
   Lane<64> d = lane_view(mr, (int)(inst >> 6), lane);
-  for (int comp = wave; comp < ncomp; comp += kExpandWaves) {
+  for (int comp = wave; comp < ncomp; comp += waves) {
   if (comp < nv) {                       // qvel_k (+ eps on the qvel perturbation k)
     const double x = qvel[b*nv + comp];
     d.qvel[comp] = p - 1 - nv == comp ? x + eps : x;
@@ -270,6 +271,7 @@ __global__ __launch_bounds__(64*kExpandWaves) void k_fd_expand(mjhipModel m, Mir
     for (int c = 0; c < 4; c++) d.qpos[padr+c] = q[c];
   } else {
     d.qpos[padr] = i < 0 ? qpos[bq + padr] : qpos[bq + padr] + eps * (vadr == i ? 1.0 : 0.0);
+  }
   }
   }
 }
@@ -1981,8 +1983,11 @@ MJHIP_API int mjhip_inverseFDBatchEx(mjhipContext* c, int B, const mjtNum* qpos,
       // empty when no centre has rows, so the call needs no host round trip.
       // the perturbations' own inputs, for the full pipeline over them (only when a centre
       // has rows)
-      hipLaunchKernelGGL(k_fd_expand, dim3((unsigned)((ninst - nA + 63)/64)),
-                         dim3(64*kExpandWaves), 0, c->stream, c->dmodel, c->mirror, B, dq, dv, da,
+      // gated: usually empty, so a few one-wave blocks striding over the range (an empty
+      // launch of one 16-wave block per 64 instances took 5 us)
+      const long gblk = (ninst - nA + 63)/64;
+      hipLaunchKernelGGL(k_fd_expand, dim3((unsigned)(gblk < 256 ? gblk : 256)), dim3(64), 0,
+                         c->stream, c->dmodel, c->mirror, B, dq, dv, da,
                          (m.nu ? dc : nullptr), eps, layout, c->fdflag, nA, ninst, 1);
       FDCHECK(hipGetLastError(), "k_fd_expand (fall-back) launch");
       rc = launch_inverse(c, (int)(ninst - nA), nullptr, nullptr, nullptr, nullptr,
