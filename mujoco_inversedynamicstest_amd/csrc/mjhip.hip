@@ -152,7 +152,7 @@ __global__ void k_from_mirror(const double* __restrict__ src, double* __restrict
 // the instances that run the position stage first -- the centres b, then the qpos
 // perturbations nbase + b*nv + i (dof i) -- then from A = nbase*(nv+1) the others,
 // A + b*2nv + (p-1). The centres lead so that they fill whole waves: only their mirror slots
-// keep every field (Mirror::sink, codegen.FD_KEEP).
+// keep every field (Mirror::fd_elide, codegen.FD_KEEP).
 // Layout 2 (the qacc perturbations run mj_inverseSkip(mjSTAGE_VEL), the qvel ones
 // mjSTAGE_POS, engine_derivative_fd.c:646-699): the same position-stage block, then the qacc
 // perturbations A + b*nv + (p-1), then the qvel ones A + nbase*nv + b*nv + (p-1-nv), so that

@@ -261,6 +261,7 @@ def test_round_trip_reference_model(tmp_path):
   for f in fields.MODEL_FIELDS:
     np.testing.assert_array_equal(getattr(m, f.name), getattr(r, f.name), err_msg=f.name)
   assert r.sizes["nmeshgraph"] == m.sizes["nmeshgraph"] > 0
+  assert r.sizes["nmeshpoly"] == m.sizes["nmeshpoly"] > 0       # the compiled mesh polygons
   assert fields.model_signature(r) == fields.model_signature(m)
   buf = bytearray(mjb.write(m))
   ints = dict(zip(mjb.INTS, struct.unpack_from("<83i", buf, 20)))
