@@ -258,7 +258,7 @@ def test_inverse_fd_parity(humanoid):
 
 
 @pytest.mark.parametrize("NB,limits", [(1024, "none"), (64, "all"), (64, "some"),
-                                       (3, "none")])
+                                       (48, "some"), (3, "none")])
 def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
   """mjd_inverseFD's stage skipping (engine_derivative_fd.c:646-699: the qvel perturbations
   run mj_inverseSkip(mjSTAGE_POS), the qacc ones mjSTAGE_VEL) against every perturbation
@@ -270,7 +270,8 @@ def test_inverse_fd_stage_skip_bit_exact(humanoid, NB, limits, monkeypatch):
   (MJHIP_FD_ACCSKIP=1: the qacc perturbations on the acceleration stage alone over the centre's velocity stage,
   k_fdskip) within it too. NB=1024 takes the skip layouts; with joint limits active on every centre, or on every
   fifth, the work-list model falls back on the device to the full pipeline over the
-  perturbations; NB=3 (28*3 instances, not a whole wave) never takes them."""
+  perturbations; NB=48 puts 16 qpos perturbations in the centres' block (which stores every
+  field); NB=3 (28*3 instances, not a whole wave) never takes them."""
   q, v, a = sample_states(humanoid, NB, first=300)
   if limits != "none":                  # push a limited hinge past its range
     j = int(np.flatnonzero(np.asarray(humanoid.jnt_limited))[3])
